@@ -1,0 +1,341 @@
+// pybind11 bindings for avenir_amd._C — the only translation unit that includes torch.
+//
+// Each binding validates device / dtype / contiguity / shape on the host BEFORE launching (a bad
+// shape must never reach a hand-written kernel), fetches the current HIP stream of the tensor's
+// device, and calls the torch-free launcher in csrc/kernels/*.hip.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "avenir_kernels.h"
+#include "avenir_host.h"
+
+namespace {
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+#define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DTYPE(t, d) TORCH_CHECK((t).scalar_type() == (d), #t " must be " #d)
+#define CHECK_DEV(t) \
+  CHECK_CUDA(t);     \
+  CHECK_CONTIG(t)
+
+template <typename T>
+T* ptr_or_null(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 class-conditional histogram.  codes uint8 [F][ld] (ld >= n), labels uint8 [>=n] or None,
+// bins/offs int32 [F] (device), h_bins list[int]; out int64 [C][TB] (accumulated into).
+void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at::Tensor>& labels,
+                     const at::Tensor& bins, const at::Tensor& offs, std::vector<int64_t> h_bins,
+                     int64_t total_bins, int64_t n_classes, at::Tensor& out, int64_t mode,
+                     bool count_labels) {
+  CHECK_DEV(codes);
+  CHECK_DTYPE(codes, at::kByte);
+  TORCH_CHECK(codes.dim() == 2, "codes must be [F, ld]");
+  const int64_t F = codes.size(0), ld = codes.size(1);
+  TORCH_CHECK(n <= ld, "n exceeds codes leading dimension");
+  TORCH_CHECK((int64_t)h_bins.size() == F, "h_bins length != F");
+  CHECK_DEV(bins);
+  CHECK_DTYPE(bins, at::kInt);
+  CHECK_DEV(offs);
+  CHECK_DTYPE(offs, at::kInt);
+  TORCH_CHECK(bins.numel() == F && offs.numel() == F, "bins/offs must have F entries");
+  CHECK_DEV(out);
+  CHECK_DTYPE(out, at::kLong);
+  TORCH_CHECK(out.numel() == n_classes * total_bins, "out must be [C*TB]");
+  int64_t sum_bins = 0;
+  std::vector<int> hb(F);
+  for (int64_t f = 0; f < F; ++f) {
+    TORCH_CHECK(h_bins[f] > 0 && h_bins[f] <= 255, "bins per feature must be in [1,255]");
+    hb[f] = (int)h_bins[f];
+    sum_bins += h_bins[f];
+  }
+  TORCH_CHECK(sum_bins + (count_labels ? 1 : 0) <= total_bins, "sum(bins) > total_bins");
+  TORCH_CHECK(n_classes >= 1 && n_classes <= 255, "n_classes must be in [1,255]");
+  const uint8_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    CHECK_DEV((*labels));
+    CHECK_DTYPE((*labels), at::kByte);
+    TORCH_CHECK(labels->numel() >= n, "labels shorter than n");
+    lab = labels->data_ptr<uint8_t>();
+  }
+  c10::hip::HIPGuard g(codes.device());
+  avk::class_histogram(codes.data_ptr<uint8_t>(), ld, n, lab, bins.data_ptr<int>(),
+                       offs.data_ptr<int>(), hb.data(), (int)F, (int)total_bins, (int)n_classes,
+                       count_labels ? 1 : 0,
+                       reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), (int)mode,
+                       cur_stream(codes));
+}
+
+void pair_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at::Tensor>& labels,
+                    const at::Tensor& bins, const at::Tensor& pairs, const at::Tensor& poff,
+                    int64_t max_tab, int64_t n_classes, at::Tensor& out) {
+  CHECK_DEV(codes);
+  CHECK_DTYPE(codes, at::kByte);
+  TORCH_CHECK(codes.dim() == 2 && n <= codes.size(1), "codes must be [F, ld>=n]");
+  CHECK_DEV(bins);
+  CHECK_DTYPE(bins, at::kInt);
+  CHECK_DEV(pairs);
+  CHECK_DTYPE(pairs, at::kInt);
+  CHECK_DEV(poff);
+  CHECK_DTYPE(poff, at::kLong);
+  CHECK_DEV(out);
+  CHECK_DTYPE(out, at::kLong);
+  TORCH_CHECK(pairs.dim() == 2 && pairs.size(1) == 2, "pairs must be [P,2]");
+  TORCH_CHECK(poff.numel() == pairs.size(0), "poff must be [P]");
+  const uint8_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    CHECK_DEV((*labels));
+    CHECK_DTYPE((*labels), at::kByte);
+    TORCH_CHECK(labels->numel() >= n, "labels shorter than n");
+    lab = labels->data_ptr<uint8_t>();
+  }
+  c10::hip::HIPGuard g(codes.device());
+  avk::pair_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, lab, bins.data_ptr<int>(),
+                      pairs.data_ptr<int>(), reinterpret_cast<const long long*>(poff.data_ptr<int64_t>()), (int)pairs.size(0),
+                      (int)max_tab, (int)n_classes,
+                      reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()),
+                      cur_stream(codes));
+}
+
+void bigram_histogram(const at::Tensor& states, const c10::optional<at::Tensor>& labels,
+                      int64_t n_classes, int64_t S, at::Tensor& out) {
+  CHECK_DEV(states);
+  CHECK_DTYPE(states, at::kShort);
+  TORCH_CHECK(states.dim() == 2, "states must be [N, L]");
+  CHECK_DEV(out);
+  CHECK_DTYPE(out, at::kLong);
+  TORCH_CHECK(out.numel() == n_classes * S * S, "out must be [C*S*S]");
+  TORCH_CHECK(S >= 1 && S <= 32767, "bad S");
+  const uint8_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    CHECK_DEV((*labels));
+    CHECK_DTYPE((*labels), at::kByte);
+    TORCH_CHECK(labels->numel() >= states.size(0), "labels shorter than N");
+    lab = labels->data_ptr<uint8_t>();
+  }
+  c10::hip::HIPGuard g(states.device());
+  avk::bigram_histogram(states.data_ptr<int16_t>(), states.size(0), (int)states.size(1), lab,
+                        (int)n_classes, (int)S,
+                        reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()),
+                        cur_stream(states));
+}
+
+at::Tensor class_moments(const at::Tensor& x, int64_t n, const c10::optional<at::Tensor>& labels,
+                         int64_t n_classes) {
+  CHECK_DEV(x);
+  CHECK_DTYPE(x, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && n <= x.size(1), "x must be [F, ld>=n]");
+  const uint8_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    CHECK_DEV((*labels));
+    CHECK_DTYPE((*labels), at::kByte);
+    TORCH_CHECK(labels->numel() >= n, "labels shorter than n");
+    lab = labels->data_ptr<uint8_t>();
+  }
+  const int64_t F = x.size(0);
+  c10::hip::HIPGuard g(x.device());
+  auto opts = x.options().dtype(at::kDouble);
+  auto out = at::zeros({n_classes, F, 3}, opts);
+  const int nb = avk::moments_blocks(n);
+  auto part = at::empty({nb, n_classes, F, 3}, opts);
+  avk::class_moments(x.data_ptr<float>(), x.size(1), n, (int)F, lab, (int)n_classes,
+                     part.data_ptr<double>(), nb, out.data_ptr<double>(), cur_stream(x));
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+void nb_predict(const at::Tensor& codes, int64_t n, const at::Tensor& offs, const at::Tensor& logp,
+                const c10::optional<at::Tensor>& logfp, const c10::optional<at::Tensor>& x,
+                const c10::optional<at::Tensor>& gmean, const c10::optional<at::Tensor>& ginvstd,
+                const c10::optional<at::Tensor>& glognorm, const c10::optional<at::Tensor>& pmean,
+                const c10::optional<at::Tensor>& pinvstd, const c10::optional<at::Tensor>& plognorm,
+                const at::Tensor& logprior, bool ref_scale, const c10::optional<at::Tensor>& post,
+                at::Tensor& pred, const c10::optional<at::Tensor>& labels,
+                const c10::optional<at::Tensor>& confusion) {
+  CHECK_DEV(codes);
+  CHECK_DTYPE(codes, at::kByte);
+  TORCH_CHECK(codes.dim() == 2 && n <= codes.size(1), "codes must be [F, ld>=n]");
+  CHECK_DEV(logp);
+  CHECK_DTYPE(logp, at::kFloat);
+  TORCH_CHECK(logp.dim() == 2, "logp must be [C, TB]");
+  const int C = (int)logp.size(0), TB = (int)logp.size(1);
+  CHECK_DEV(offs);
+  CHECK_DTYPE(offs, at::kInt);
+  TORCH_CHECK(offs.numel() == codes.size(0), "offs must be [F]");
+  CHECK_DEV(logprior);
+  CHECK_DTYPE(logprior, at::kFloat);
+  TORCH_CHECK(logprior.numel() == C, "logprior must be [C]");
+  CHECK_DEV(pred);
+  CHECK_DTYPE(pred, at::kInt);
+  TORCH_CHECK(pred.numel() >= n, "pred too short");
+  int ncont = 0;
+  long long ldx = 0;
+  if (x.has_value() && x->defined()) {
+    CHECK_DEV((*x));
+    CHECK_DTYPE((*x), at::kFloat);
+    TORCH_CHECK(x->dim() == 2 && n <= x->size(1), "x must be [Fc, ld>=n]");
+    ncont = (int)x->size(0);
+    ldx = x->size(1);
+    TORCH_CHECK(gmean.has_value() && gmean->numel() == (int64_t)C * ncont, "gmean must be [C,Fc]");
+    TORCH_CHECK(ginvstd.has_value() && ginvstd->numel() == (int64_t)C * ncont, "ginvstd");
+    TORCH_CHECK(glognorm.has_value() && glognorm->numel() == (int64_t)C * ncont, "glognorm");
+    if (ref_scale)
+      TORCH_CHECK(pmean.has_value() && pinvstd.has_value() && plognorm.has_value(),
+                  "feature-prior Gaussian params required with ref_scale");
+  }
+  if (ref_scale) TORCH_CHECK(logfp.has_value() && logfp->numel() == TB, "logfp must be [TB]");
+  if (post.has_value() && post->defined()) {
+    CHECK_DEV((*post));
+    TORCH_CHECK(post->numel() >= n * C, "post too short");
+  }
+  const uint8_t* lab = nullptr;
+  unsigned long long* conf = nullptr;
+  if (confusion.has_value() && confusion->defined()) {
+    TORCH_CHECK(labels.has_value() && labels->defined(), "confusion requires labels");
+    CHECK_DEV((*labels));
+    CHECK_DTYPE((*labels), at::kByte);
+    TORCH_CHECK(labels->numel() >= n, "labels too short");
+    CHECK_DEV((*confusion));
+    CHECK_DTYPE((*confusion), at::kLong);
+    TORCH_CHECK(confusion->numel() == (int64_t)C * C, "confusion must be [C,C]");
+    lab = labels->data_ptr<uint8_t>();
+    conf = reinterpret_cast<unsigned long long*>(confusion->data_ptr<int64_t>());
+  }
+  c10::hip::HIPGuard g(codes.device());
+  avk::nb_predict(codes.data_ptr<uint8_t>(), codes.size(1), n, (int)codes.size(0),
+                  offs.data_ptr<int>(), logp.data_ptr<float>(), ptr_or_null<float>(logfp), TB,
+                  ptr_or_null<float>(x), ldx, ncont, ptr_or_null<float>(gmean),
+                  ptr_or_null<float>(ginvstd), ptr_or_null<float>(glognorm),
+                  ptr_or_null<float>(pmean), ptr_or_null<float>(pinvstd),
+                  ptr_or_null<float>(plognorm), logprior.data_ptr<float>(), C, ref_scale ? 1 : 0,
+                  ptr_or_null<float>(post), pred.data_ptr<int>(), lab, conf, cur_stream(codes));
+}
+
+// ---------------------------------------------------------------------------------------------
+// host runtime
+// ---------------------------------------------------------------------------------------------
+// specs: list of (ordinal, kind, vocab, bucket_width, bucket_offset, max_code).  Returns one
+// CPU tensor per spec: uint8 [ld] for CAT/BUCKET (ld = n rounded up to 16, padding = 255),
+// float32 [n] for FLOAT, int64 [n] for INT; plus the malformed-row count.
+py::tuple csv_parse(avh::CsvFile& f, py::list specs_py, int64_t row_begin, int64_t row_end) {
+  std::vector<avh::ColSpec> specs;
+  for (auto item : specs_py) {
+    auto t = item.cast<py::tuple>();
+    avh::ColSpec s;
+    s.ordinal = t[0].cast<int>();
+    s.kind = t[1].cast<int>();
+    s.vocab = t[2].cast<std::vector<std::string>>();
+    s.bucket_width = t[3].cast<double>();
+    s.bucket_offset = t[4].cast<int>();
+    s.max_code = t[5].cast<int>();
+    TORCH_CHECK(s.ordinal >= 0, "negative ordinal");
+    if (s.kind == avh::BUCKET) TORCH_CHECK(s.bucket_width > 0, "bucket width must be > 0");
+    specs.push_back(std::move(s));
+  }
+  row_begin = std::max<int64_t>(0, row_begin);
+  if (row_end < 0 || row_end > f.num_rows()) row_end = f.num_rows();
+  const int64_t n = std::max<int64_t>(0, row_end - row_begin);
+  const int64_t ld = ((n + 15) / 16) * 16;
+  std::vector<at::Tensor> outs;
+  std::vector<void*> ptrs;
+  for (auto& s : specs) {
+    at::Tensor t;
+    if (s.kind == avh::CAT || s.kind == avh::BUCKET)
+      t = at::full({std::max<int64_t>(ld, 16)}, 255, at::TensorOptions().dtype(at::kByte));
+    else if (s.kind == avh::FLOAT)
+      t = at::empty({n}, at::TensorOptions().dtype(at::kFloat));
+    else
+      t = at::empty({n}, at::TensorOptions().dtype(at::kLong));
+    ptrs.push_back(t.data_ptr());
+    outs.push_back(t);
+  }
+  int64_t bad;
+  {
+    py::gil_scoped_release rel;
+    bad = f.parse(specs, ptrs, row_begin, row_end);
+  }
+  py::list res;
+  for (auto& t : outs) res.append(t);
+  return py::make_tuple(res, bad);
+}
+
+std::string format_rows(py::object prefix, const at::Tensor& cols, std::vector<int> precision,
+                        std::string delim, int nthreads) {
+  TORCH_CHECK(!cols.is_cuda() && cols.scalar_type() == at::kDouble && cols.dim() == 2,
+              "cols must be CPU float64 [ncol, n]");
+  auto c = cols.contiguous();
+  std::vector<std::string> pre;
+  const std::vector<std::string>* pp = nullptr;
+  if (!prefix.is_none()) {
+    pre = prefix.cast<std::vector<std::string>>();
+    TORCH_CHECK((int64_t)pre.size() == c.size(1), "prefix length != n");
+    pp = &pre;
+  }
+  py::gil_scoped_release rel;
+  return avh::format_rows(pp, c.data_ptr<double>(), (int)c.size(0), c.size(1), precision,
+                          delim.empty() ? ',' : delim[0], nthreads);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "avenir_amd native kernels (HIP/CDNA4 gfx950) and host runtime";
+  m.def("class_histogram", &class_histogram);
+  m.def("pair_histogram", &pair_histogram);
+  m.def("bigram_histogram", &bigram_histogram);
+  m.def("class_moments", &class_moments);
+  m.def("nb_predict", &nb_predict);
+
+  py::class_<avh::CsvFile>(m, "CsvFile")
+      .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',
+           py::arg("skip_header") = false, py::arg("nthreads") = 8)
+      .def("num_rows", &avh::CsvFile::num_rows)
+      .def("max_fields", &avh::CsvFile::max_fields)
+      .def("distinct", &avh::CsvFile::distinct)
+      .def("column_strings", &avh::CsvFile::column_strings)
+      .def("line", &avh::CsvFile::line)
+      .def("lines", &avh::CsvFile::lines)
+      .def("parse", &csv_parse, py::arg("specs"), py::arg("row_begin") = 0, py::arg("row_end") = -1);
+  m.def("format_rows", &format_rows);
+  py::class_<avh::SpscRing>(m, "SpscRing")
+      .def(py::init<size_t, int>())
+      .def("push", [](avh::SpscRing& r, std::vector<int64_t> rec) {
+        TORCH_CHECK((int)rec.size() == r.rec_len(), "record length mismatch");
+        return r.push(rec.data());
+      })
+      .def("pop_batch", [](avh::SpscRing& r, size_t max_n) {
+        auto t = at::empty({(int64_t)max_n, r.rec_len()}, at::TensorOptions().dtype(at::kLong));
+        size_t k = r.pop_batch(t.data_ptr<int64_t>(), max_n);
+        return t.narrow(0, 0, (int64_t)k);
+      })
+      .def("size", &avh::SpscRing::size);
+  m.def("write_container", [](const std::string& path, const std::string& header,
+                              std::vector<at::Tensor> blobs) {
+    std::vector<const void*> ptrs;
+    std::vector<size_t> sizes;
+    std::vector<at::Tensor> keep;
+    for (auto& b : blobs) {
+      auto c = b.cpu().contiguous();
+      keep.push_back(c);
+      ptrs.push_back(c.data_ptr());
+      sizes.push_back((size_t)c.nbytes());
+    }
+    avh::write_container(path, header, ptrs, sizes);
+  });
+  m.def("read_container_header", [](const std::string& path) {
+    uint64_t off = 0;
+    std::string h = avh::read_container_header(path, &off);
+    return py::make_tuple(h, off);
+  });
+  m.def("crc32", [](const at::Tensor& t, uint32_t seed) {
+    auto c = t.cpu().contiguous();
+    return avh::crc32(c.data_ptr(), (size_t)c.nbytes(), seed);
+  }, py::arg("t"), py::arg("seed") = 0);
+}

@@ -1,0 +1,349 @@
+// K1 host half: memory-mapped multi-threaded CSV -> columnar encoder (see avenir_host.h).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string_view>
+#include <thread>
+
+#include "avenir_host.h"
+
+namespace avh {
+
+namespace {
+
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r'; }
+
+inline std::string_view trim(std::string_view s) {
+  while (!s.empty() && is_space(s.front())) s.remove_prefix(1);
+  while (!s.empty() && is_space(s.back())) s.remove_suffix(1);
+  return s;
+}
+
+// Fast decimal parser: [+-]digits[.digits][(e|E)[+-]digits]; NaN on garbage / empty.
+inline double parse_double(std::string_view s) {
+  s = trim(s);
+  if (s.empty()) return std::nan("");
+  const char* p = s.data();
+  const char* e = p + s.size();
+  bool neg = false;
+  if (*p == '+' || *p == '-') { neg = (*p == '-'); ++p; }
+  double v = 0;
+  int digits = 0;
+  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++digits; }
+  if (p < e && *p == '.') {
+    ++p;
+    double scale = 0.1;
+    while (p < e && *p >= '0' && *p <= '9') { v += (*p - '0') * scale; scale *= 0.1; ++p; ++digits; }
+  }
+  if (digits == 0) return std::nan("");
+  if (p < e && (*p == 'e' || *p == 'E')) {
+    ++p;
+    bool eneg = false;
+    if (p < e && (*p == '+' || *p == '-')) { eneg = (*p == '-'); ++p; }
+    int ex = 0;
+    while (p < e && *p >= '0' && *p <= '9') { ex = ex * 10 + (*p - '0'); ++p; }
+    v *= std::pow(10.0, eneg ? -ex : ex);
+  }
+  if (p != e) return std::nan("");
+  return neg ? -v : v;
+}
+
+inline int64_t parse_int(std::string_view s, bool* ok) {
+  s = trim(s);
+  *ok = false;
+  if (s.empty()) return 0;
+  const char* p = s.data();
+  const char* e = p + s.size();
+  bool neg = false;
+  if (*p == '+' || *p == '-') { neg = (*p == '-'); ++p; }
+  int64_t v = 0;
+  int d = 0;
+  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++d; }
+  if (p < e && *p == '.') {  // tolerate "12.0" style ints (truncate like the reference's casts)
+    ++p;
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+  }
+  if (d == 0 || p != e) return 0;
+  *ok = true;
+  return neg ? -v : v;
+}
+
+struct CatLookup {
+  std::vector<std::string> vocab;
+  std::unordered_map<std::string_view, uint8_t> map;
+  explicit CatLookup(const std::vector<std::string>& v) : vocab(v) {
+    if (vocab.size() > 255) throw std::runtime_error("categorical cardinality > 255 not supported");
+    for (size_t i = 0; i < vocab.size(); ++i) map.emplace(std::string_view(vocab[i]), (uint8_t)i);
+  }
+  inline uint8_t code(std::string_view s) const {
+    s = trim(s);
+    if (vocab.size() <= 8) {
+      for (size_t i = 0; i < vocab.size(); ++i)
+        if (s.size() == vocab[i].size() && std::memcmp(s.data(), vocab[i].data(), s.size()) == 0)
+          return (uint8_t)i;
+      return 255;
+    }
+    auto it = map.find(s);
+    return it == map.end() ? 255 : it->second;
+  }
+};
+
+}  // namespace
+
+CsvFile::CsvFile(const std::string& path, char delim, bool skip_header, int nthreads)
+    : delim_(delim), nthreads_(std::max(1, nthreads)) {
+  fd_ = ::open(path.c_str(), O_RDONLY);
+  if (fd_ < 0) throw std::runtime_error("cannot open " + path);
+  struct stat st;
+  if (fstat(fd_, &st) != 0) throw std::runtime_error("cannot stat " + path);
+  size_ = (size_t)st.st_size;
+  if (size_ > 0) {
+    void* m = mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (m == MAP_FAILED) throw std::runtime_error("mmap failed for " + path);
+    madvise(m, size_, MADV_SEQUENTIAL);
+    data_ = static_cast<const char*>(m);
+  }
+  index_lines(skip_header);
+}
+
+CsvFile::~CsvFile() {
+  if (data_) munmap(const_cast<char*>(data_), size_);
+  if (fd_ >= 0) ::close(fd_);
+}
+
+void CsvFile::index_lines(bool skip_header) {
+  // chunk boundaries aligned to line starts, one thread per chunk
+  const int T = (size_ < (1u << 20)) ? 1 : nthreads_;
+  std::vector<size_t> bounds(T + 1, 0);
+  bounds[T] = size_;
+  for (int t = 1; t < T; ++t) {
+    size_t b = size_ * t / T;
+    while (b < size_ && data_[b - 1] != '\n') ++b;
+    bounds[t] = b;
+  }
+  std::vector<std::vector<int64_t>> st(T), en(T);
+  std::vector<int> mf(T, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([&, t] {
+      size_t p = bounds[t], e = bounds[t + 1];
+      while (p < e) {
+        const char* nl = static_cast<const char*>(std::memchr(data_ + p, '\n', e - p));
+        size_t q = nl ? (size_t)(nl - data_) : e;
+        size_t qe = q;
+        if (qe > p && data_[qe - 1] == '\r') --qe;
+        if (qe > p) {  // skip blank lines
+          st[t].push_back((int64_t)p);
+          en[t].push_back((int64_t)qe);
+          int nf = 1;
+          for (size_t k = p; k < qe; ++k) nf += (data_[k] == delim_);
+          mf[t] = std::max(mf[t], nf);
+        }
+        p = q + 1;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  size_t total = 0;
+  for (int t = 0; t < T; ++t) total += st[t].size();
+  line_start_.reserve(total);
+  line_end_.reserve(total);
+  for (int t = 0; t < T; ++t) {
+    line_start_.insert(line_start_.end(), st[t].begin(), st[t].end());
+    line_end_.insert(line_end_.end(), en[t].begin(), en[t].end());
+    max_fields_ = std::max(max_fields_, mf[t]);
+  }
+  if (skip_header && !line_start_.empty()) {
+    line_start_.erase(line_start_.begin());
+    line_end_.erase(line_end_.begin());
+  }
+}
+
+int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void*>& outs,
+                       int64_t row_begin, int64_t row_end) {
+  if (specs.size() != outs.size()) throw std::runtime_error("specs/outs length mismatch");
+  row_begin = std::max<int64_t>(0, row_begin);
+  row_end = std::min<int64_t>(num_rows(), row_end < 0 ? num_rows() : row_end);
+  const int64_t base = row_begin;
+  const int64_t n = std::max<int64_t>(0, row_end - row_begin);
+  std::vector<std::unique_ptr<CatLookup>> cats(specs.size());
+  int max_ord = 0;
+  for (size_t i = 0; i < specs.size(); ++i) {
+    if (specs[i].kind == CAT) cats[i] = std::make_unique<CatLookup>(specs[i].vocab);
+    max_ord = std::max(max_ord, specs[i].ordinal);
+  }
+  // ordinal -> list of spec indices
+  std::vector<std::vector<int>> by_ord(max_ord + 1);
+  for (size_t i = 0; i < specs.size(); ++i) by_ord[specs[i].ordinal].push_back((int)i);
+
+  const int T = n < 4096 ? 1 : nthreads_;
+  std::vector<int64_t> bad(T, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([&, t] {
+      const int64_t r0 = n * t / T, r1 = n * (t + 1) / T;
+      std::vector<std::string_view> fields;
+      fields.reserve(max_ord + 2);
+      for (int64_t r = r0; r < r1; ++r) {
+        const char* p = data_ + line_start_[base + r];
+        const char* e = data_ + line_end_[base + r];
+        fields.clear();
+        const char* s = p;
+        for (const char* q = p; q <= e; ++q) {
+          if (q == e || *q == delim_) {
+            fields.emplace_back(s, (size_t)(q - s));
+            s = q + 1;
+            if ((int)fields.size() > max_ord) break;
+          }
+        }
+        for (int o = 0; o <= max_ord; ++o) {
+          if (by_ord[o].empty()) continue;
+          const bool have = o < (int)fields.size();
+          if (!have) ++bad[t];
+          for (int si : by_ord[o]) {
+            const ColSpec& sp = specs[si];
+            switch (sp.kind) {
+              case CAT: {
+                static_cast<uint8_t*>(outs[si])[r] = have ? cats[si]->code(fields[o]) : 255;
+                break;
+              }
+              case BUCKET: {
+                uint8_t c = 255;
+                if (have) {
+                  const double v = parse_double(fields[o]);
+                  if (!std::isnan(v)) {
+                    // the reference uses integer division: Integer.parseInt(v) / bucketWidth
+                    const long long b = (long long)std::floor(v / sp.bucket_width) - sp.bucket_offset;
+                    if (b >= 0 && b <= sp.max_code) c = (uint8_t)b;
+                  }
+                }
+                static_cast<uint8_t*>(outs[si])[r] = c;
+                break;
+              }
+              case FLOAT: {
+                static_cast<float*>(outs[si])[r] = have ? (float)parse_double(fields[o]) : NAN;
+                break;
+              }
+              case INT: {
+                bool ok = false;
+                int64_t v = have ? parse_int(fields[o], &ok) : 0;
+                static_cast<int64_t*>(outs[si])[r] = ok ? v : INT64_MIN;
+                break;
+              }
+              default:
+                break;
+            }
+          }
+        }
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  int64_t b = 0;
+  for (auto v : bad) b += v;
+  return b;
+}
+
+std::vector<std::string> CsvFile::distinct(int ordinal, size_t limit) {
+  std::vector<std::string> out;
+  std::unordered_map<std::string, int> seen;
+  const int64_t n = num_rows();
+  for (int64_t r = 0; r < n; ++r) {
+    std::string_view line(data_ + line_start_[r], (size_t)(line_end_[r] - line_start_[r]));
+    int f = 0;
+    size_t s = 0;
+    for (size_t q = 0; q <= line.size(); ++q) {
+      if (q == line.size() || line[q] == delim_) {
+        if (f == ordinal) {
+          std::string v(trim(line.substr(s, q - s)));
+          if (seen.emplace(v, 1).second) {
+            out.push_back(v);
+            if (out.size() >= limit) return out;
+          }
+          break;
+        }
+        ++f;
+        s = q + 1;
+      }
+    }
+  }
+  return out;
+}
+
+std::vector<std::string> CsvFile::column_strings(int ordinal) {
+  const int64_t n = num_rows();
+  std::vector<std::string> out(n);
+  for (int64_t r = 0; r < n; ++r) {
+    std::string_view line(data_ + line_start_[r], (size_t)(line_end_[r] - line_start_[r]));
+    int f = 0;
+    size_t s = 0;
+    for (size_t q = 0; q <= line.size(); ++q) {
+      if (q == line.size() || line[q] == delim_) {
+        if (f == ordinal) { out[r] = std::string(trim(line.substr(s, q - s))); break; }
+        ++f;
+        s = q + 1;
+      }
+    }
+  }
+  return out;
+}
+
+std::string CsvFile::line(int64_t i) const {
+  if (i < 0 || i >= num_rows()) throw std::out_of_range("line index");
+  return std::string(data_ + line_start_[i], (size_t)(line_end_[i] - line_start_[i]));
+}
+
+std::vector<std::string> CsvFile::lines(int64_t b, int64_t e) const {
+  b = std::max<int64_t>(0, b);
+  e = std::min<int64_t>(num_rows(), e);
+  std::vector<std::string> out;
+  out.reserve(std::max<int64_t>(0, e - b));
+  for (int64_t i = b; i < e; ++i)
+    out.emplace_back(data_ + line_start_[i], (size_t)(line_end_[i] - line_start_[i]));
+  return out;
+}
+
+std::string format_rows(const std::vector<std::string>* prefix, const double* cols, int ncol,
+                        int64_t n, const std::vector<int>& precision, char delim, int nthreads) {
+  const int T = n < 8192 ? 1 : std::max(1, nthreads);
+  std::vector<std::string> parts(T);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([&, t] {
+      const int64_t r0 = n * t / T, r1 = n * (t + 1) / T;
+      std::string& s = parts[t];
+      s.reserve((size_t)(r1 - r0) * (16 + 12 * ncol));
+      char buf[64];
+      for (int64_t r = r0; r < r1; ++r) {
+        bool first = true;
+        if (prefix) { s += (*prefix)[r]; first = false; }
+        for (int c = 0; c < ncol; ++c) {
+          if (!first) s.push_back(delim);
+          first = false;
+          const double v = cols[(int64_t)c * n + r];
+          const int pr = c < (int)precision.size() ? precision[c] : 6;
+          int len;
+          if (pr < 0) len = snprintf(buf, sizeof buf, "%lld", (long long)std::llround(v));
+          else len = snprintf(buf, sizeof buf, "%.*f", pr, v);
+          s.append(buf, (size_t)len);
+        }
+        s.push_back('\n');
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  size_t tot = 0;
+  for (auto& p : parts) tot += p.size();
+  std::string out;
+  out.reserve(tot);
+  for (auto& p : parts) out += p;
+  return out;
+}
+
+}  // namespace avh

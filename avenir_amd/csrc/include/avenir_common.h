@@ -1,0 +1,133 @@
+// avenir_amd — shared CDNA4 (gfx950) device helpers.
+//
+// Everything here is written for 64-lane wavefronts: lane = threadIdx.x & 63, ballots are 64-bit,
+// reductions use __shfl_xor over offsets 32..1.  No CUDA shims, no warp-32 idioms.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define AV_WAVE 64
+
+#define AV_HIP_CHECK(expr)                                                                 \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) {                                                                 \
+      av_report_hip_error(_e, #expr, __FILE__, __LINE__);                                   \
+    }                                                                                       \
+  } while (0)
+
+// defined in host/runtime.cpp — throws std::runtime_error (turned into a Python exception)
+void av_report_hip_error(hipError_t e, const char* expr, const char* file, int line);
+
+namespace av {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_xor(v, o, 64);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_xor(v, o, 64);
+    v = v < w ? v : w;
+  }
+  return v;
+}
+
+// (value, index) argmax over the wave; ties -> lowest index (deterministic).
+__device__ __forceinline__ void wave_argmax(float& v, int& idx) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float w = __shfl_xor(v, o, 64);
+    int j = __shfl_xor(idx, o, 64);
+    if (w > v || (w == v && j < idx)) { v = w; idx = j; }
+  }
+}
+__device__ __forceinline__ void wave_argmin(float& v, int& idx) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float w = __shfl_xor(v, o, 64);
+    int j = __shfl_xor(idx, o, 64);
+    if (w < v || (w == v && j < idx)) { v = w; idx = j; }
+  }
+}
+
+// 64-bit wave sum built from two 32-bit shuffles per step.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned lo = __shfl_xor((unsigned)(v & 0xffffffffu), o, 64);
+    unsigned hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+    v += ((unsigned long long)hi << 32) | lo;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG (Salmon et al. 2011).  Stateless: (key, counter) -> 4 x u32.
+// Every device sampler in avenir_amd draws from this so results are reproducible for a given
+// (seed, offset) independent of grid shape and world size.
+// ---------------------------------------------------------------------------------------------
+struct u4 { uint32_t x, y, z, w; };
+
+__host__ __device__ __forceinline__ u4 philox4x32_10(u4 ctr, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint64_t p0 = (uint64_t)M0 * ctr.x;
+    uint64_t p1 = (uint64_t)M1 * ctr.z;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    u4 n;
+    n.x = hi1 ^ ctr.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ ctr.w ^ k1;
+    n.w = lo0;
+    ctr = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return ctr;
+}
+
+// uniform in (0, 1]  (never 0: safe for log)
+__host__ __device__ __forceinline__ float u32_to_unit(uint32_t x) {
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ u4 philox_draw(uint64_t seed, uint64_t offset, uint64_t idx) {
+  u4 c;
+  c.x = (uint32_t)idx;
+  c.y = (uint32_t)(idx >> 32);
+  c.z = (uint32_t)offset;
+  c.w = (uint32_t)(offset >> 32);
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// Grid sizing for memory-bound streaming kernels: enough waves to fill 256 CUs several times
+// over, capped so the tail is short (Guideline 11).
+inline int stream_grid(long long work_items, int block, int per_thread = 1, int cap = 2048) {
+  long long g = (work_items + (long long)block * per_thread - 1) / ((long long)block * per_thread);
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace av

@@ -1,0 +1,92 @@
+// Host-side (CPU) C++ runtime of avenir_amd: declarations.
+//
+//  * CsvFile   — K1: memory-mapped, multi-threaded CSV -> columnar encoder driven by the JSON
+//                FeatureSchema (categoricals dictionary-coded to uint8 with 255 = unknown/missing,
+//                ints bucketized by bucketWidth, doubles parsed to f32).  Replaces every mapper's
+//                `value.toString().split(fieldDelimRegex)` + schema lookup in the reference
+//                (e.g. J/bayesian/BayesianDistribution.java:137-178).
+//  * SpscRing  — lock-free single-producer/single-consumer ring buffer used by the online bandit
+//                service (replaces the Storm spout/bolt + Redis queues, J/storm/*).
+//  * checkpoint container read/write (safetensors-compatible layout, JSON header).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace avh {
+
+enum ColKind : int { CAT = 0, BUCKET = 1, FLOAT = 2, INT = 3 };
+
+struct ColSpec {
+  int ordinal = 0;
+  int kind = CAT;
+  std::vector<std::string> vocab;  // CAT: known values, code = index (255 = unknown)
+  double bucket_width = 1.0;       // BUCKET: code = (int)(v / width) - offset
+  int bucket_offset = 0;
+  int max_code = 254;              // BUCKET: codes > max_code -> 255
+};
+
+class CsvFile {
+ public:
+  CsvFile(const std::string& path, char delim, bool skip_header, int nthreads);
+  ~CsvFile();
+  int64_t num_rows() const { return (int64_t)line_start_.size(); }
+  int max_fields() const { return max_fields_; }
+  // Parse the given specs into caller-owned buffers.  out_u8[i] is [ld] for CAT/BUCKET specs,
+  // out_f32 for FLOAT, out_i64 for INT (nullptr for kinds not matching).  Returns number of
+  // malformed (short) rows encountered.
+  int64_t parse(const std::vector<ColSpec>& specs, const std::vector<void*>& outs,
+                int64_t row_begin = 0, int64_t row_end = -1);
+  // Discover distinct values of a column (in first-seen order) — used when the schema omits
+  // cardinality.
+  std::vector<std::string> distinct(int ordinal, size_t limit);
+  std::vector<std::string> column_strings(int ordinal);
+  std::string line(int64_t i) const;
+  std::vector<std::string> lines(int64_t begin, int64_t end) const;
+
+ private:
+  void index_lines(bool skip_header);
+  const char* data_ = nullptr;
+  size_t size_ = 0;
+  int fd_ = -1;
+  char delim_;
+  int nthreads_;
+  int max_fields_ = 0;
+  std::vector<int64_t> line_start_;
+  std::vector<int64_t> line_end_;
+};
+
+// Format rows of numeric columns to CSV text quickly (multi-threaded).  prefix: optional per-row
+// leading text (e.g. the original record); cols are f64 column-major [ncol][n].
+std::string format_rows(const std::vector<std::string>* prefix, const double* cols, int ncol,
+                        int64_t n, const std::vector<int>& precision, char delim, int nthreads);
+
+// Lock-free SPSC ring of fixed-size int64 records.
+class SpscRing {
+ public:
+  SpscRing(size_t capacity_pow2, int rec_len);
+  bool push(const int64_t* rec);
+  bool pop(int64_t* rec);
+  size_t pop_batch(int64_t* recs, size_t max_n);
+  size_t size() const;
+  int rec_len() const { return rec_len_; }
+
+ private:
+  std::vector<int64_t> buf_;
+  size_t mask_;
+  int rec_len_;
+  alignas(64) std::atomic<size_t> head_{0};
+  alignas(64) std::atomic<size_t> tail_{0};
+};
+
+// Checkpoint container: 8-byte little-endian header length, JSON header, raw tensor bytes
+// (exactly the safetensors layout, so files open with the safetensors library too).
+void write_container(const std::string& path, const std::string& header_json,
+                     const std::vector<const void*>& blobs, const std::vector<size_t>& sizes);
+std::string read_container_header(const std::string& path, uint64_t* data_offset);
+uint32_t crc32(const void* data, size_t n, uint32_t seed = 0);
+
+}  // namespace avh

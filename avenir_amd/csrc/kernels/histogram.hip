@@ -1,0 +1,444 @@
+// K2 / K3 / K4 counting kernels for CDNA4 (gfx950).
+//
+// K2  class-conditional categorical histogram  out[c][off_f + b]  (Naive Bayes training,
+//     categorical encodings, class affinity, Fisher/KS stats, event-time distributions ...).
+//     Replaces the per-record emit + shuffle of BayesianDistribution's mapper/reducer
+//     (reference: src/main/java/org/avenir/bayesian/BayesianDistribution.java:137-178, :263-327).
+// K3  pair / contingency histogram  out[p][c][b1][b2]   (MutualInformation, CramerCorrelation,
+//     HeterogeneityReductionCorrelation: J/explore/MutualInformation.java:138-216,
+//     J/explore/CramerCorrelation.java:162-182).
+// K4  Markov bigram histogram  out[c][s][s']  (J/markov/MarkovStateTransitionModel.java:116-133).
+//
+// Data layout (SoA, feature-major): codes are uint8 [F][ld] with ld % 16 == 0, so every lane
+// streams 16 rows per 128-bit load.  A code is either < bins[f] or the missing sentinel 255.
+//
+// Fast path (every C*bins[f] <= 16): each lane keeps 16 one-hot BYTE counters packed in two
+// u64 registers; incrementing bin i is `acc += 1 << 8*(i&7)` — no LDS, no atomics in the hot
+// loop.  Every 15 tiles (<= 240 increments/byte) the wave widens bytes to 16-bit lanes,
+// reduces them with 64-lane shuffles (64*240 < 2^16) and lane 0 adds into an LDS table.
+// This keeps the kernel at the HBM roofline even with 2 classes (where a plain atomic
+// histogram would serialise on a handful of hot addresses).
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+constexpr int HB = 256;          // threads per block for the histogram kernels
+constexpr int FLUSH_EVERY = 15;  // tiles between byte-counter flushes (16 rows/lane/tile)
+
+__device__ __forceinline__ void flush_packed(unsigned long long& lo, unsigned long long& hi,
+                                             unsigned int* s_bins /*16*/) {
+  const unsigned long long M = 0x00FF00FF00FF00FFull;
+  unsigned long long w[4] = {lo & M, (lo >> 8) & M, hi & M, (hi >> 8) & M};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] = av::wave_sum_u64(w[q]);
+  if (av::lane_id() == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int base = (q >> 1) * 8 + (q & 1);  // even bytes / odd bytes of lo / hi
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        unsigned v = (unsigned)((w[q] >> (16 * k)) & 0xFFFFu);
+        if (v) atomicAdd(&s_bins[base + 2 * k], v);
+      }
+    }
+  }
+  lo = 0;
+  hi = 0;
+}
+
+__device__ __forceinline__ void acc_byte(unsigned idx, unsigned long long& lo,
+                                         unsigned long long& hi) {
+  const unsigned long long b = 1ull << ((idx & 7u) << 3);
+  const bool in = idx < 16u;
+  const bool h = idx >= 8u;
+  lo += (in && !h) ? b : 0ull;
+  hi += (in && h) ? b : 0ull;
+}
+
+__device__ __forceinline__ void acc_word(unsigned cw, unsigned vw, unsigned B,
+                                         unsigned long long& lo, unsigned long long& hi) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const unsigned c = (cw >> (8 * j)) & 0xFFu;
+    const unsigned v = (vw >> (8 * j)) & 0xFFu;
+    acc_byte(c * B + v, lo, hi);
+  }
+}
+
+template <int NF>
+__global__ __launch_bounds__(HB) void hist_packed_kernel(
+    const uint8_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const int* __restrict__ bins, const int* __restrict__ offs, int f0, int nfeat, int total_bins,
+    int n_classes, int count_labels, unsigned long long* __restrict__ out) {
+  // s_bins[NF*16 .. NF*16+15]: per-class record counts (count_labels), stored in column TB-1
+  __shared__ unsigned int s_bins[NF * 16 + 16];
+  for (int i = threadIdx.x; i < NF * 16 + 16; i += HB) s_bins[i] = 0;
+  __syncthreads();
+
+  unsigned B[NF];
+  const uint4* col[NF];
+#pragma unroll
+  for (int k = 0; k < NF; ++k) {
+    const int f = f0 + (k < nfeat ? k : 0);
+    B[k] = (unsigned)bins[f];
+    col[k] = reinterpret_cast<const uint4*>(codes + (long long)f * ld);
+  }
+  const uint4* lab = reinterpret_cast<const uint4*>(labels);
+
+  unsigned long long lo[NF], hi[NF], clo = 0, chi = 0;
+#pragma unroll
+  for (int k = 0; k < NF; ++k) { lo[k] = 0; hi[k] = 0; }
+  const bool cl_cnt = count_labels && f0 == 0;
+
+  const long long nvec = n >> 4;  // full 16-row vectors
+  const long long ntiles = (nvec + AV_WAVE - 1) / AV_WAVE;
+  const int waves_per_block = HB / AV_WAVE;
+  const long long gw = (long long)blockIdx.x * waves_per_block + av::wave_id();
+  const long long nw = (long long)gridDim.x * waves_per_block;
+  int since_flush = 0;
+  for (long long t = gw; t < ntiles; t += nw) {
+    const long long v = t * AV_WAVE + av::lane_id();
+    if (v < nvec) {
+      uint4 cl = lab ? lab[v] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        if (k < nfeat) {
+          const uint4 x = col[k][v];
+          acc_word(cl.x, x.x, B[k], lo[k], hi[k]);
+          acc_word(cl.y, x.y, B[k], lo[k], hi[k]);
+          acc_word(cl.z, x.z, B[k], lo[k], hi[k]);
+          acc_word(cl.w, x.w, B[k], lo[k], hi[k]);
+        }
+      }
+      if (cl_cnt) {  // class-only counter: bin index = class code
+        acc_word(cl.x, 0u, 1u, clo, chi);
+        acc_word(cl.y, 0u, 1u, clo, chi);
+        acc_word(cl.z, 0u, 1u, clo, chi);
+        acc_word(cl.w, 0u, 1u, clo, chi);
+      }
+    }
+    if (++since_flush == FLUSH_EVERY) {  // wave-uniform
+#pragma unroll
+      for (int k = 0; k < NF; ++k)
+        if (k < nfeat) flush_packed(lo[k], hi[k], &s_bins[k * 16]);
+      if (cl_cnt) flush_packed(clo, chi, &s_bins[NF * 16]);
+      since_flush = 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NF; ++k)
+    if (k < nfeat) flush_packed(lo[k], hi[k], &s_bins[k * 16]);
+  if (cl_cnt) flush_packed(clo, chi, &s_bins[NF * 16]);
+
+  // tail rows (n % 16) — block 0 only, scalar
+  if (blockIdx.x == 0) {
+    for (long long r = nvec * 16 + threadIdx.x; r < n; r += HB) {
+      const unsigned c = labels ? labels[r] : 0u;
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        if (k < nfeat) {
+          const unsigned v = codes[(long long)(f0 + k) * ld + r];
+          if (c < (unsigned)n_classes && v < B[k]) atomicAdd(&s_bins[k * 16 + c * B[k] + v], 1u);
+        }
+      }
+      if (cl_cnt && c < (unsigned)n_classes) atomicAdd(&s_bins[NF * 16 + c], 1u);
+    }
+  }
+  __syncthreads();
+  if (cl_cnt && threadIdx.x < n_classes && s_bins[NF * 16 + threadIdx.x])
+    atomicAdd(&out[(long long)threadIdx.x * total_bins + total_bins - 1],
+              (unsigned long long)s_bins[NF * 16 + threadIdx.x]);
+  for (int i = threadIdx.x; i < NF * 16; i += HB) {
+    const int k = i >> 4, idx = i & 15;
+    if (k >= nfeat) continue;
+    const unsigned v = s_bins[i];
+    const int Bk = bins[f0 + k];
+    if (v && idx < n_classes * Bk) {
+      const int c = idx / Bk, b = idx - c * Bk;
+      atomicAdd(&out[(long long)c * total_bins + offs[f0 + k] + b], (unsigned long long)v);
+    }
+  }
+}
+
+// General path: LDS-privatised table with R replicas (one per wave when it fits) so that lanes of
+// different waves never contend; replicas are summed once per block.
+__global__ __launch_bounds__(HB) void hist_lds_kernel(
+    const uint8_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const int* __restrict__ bins, const int* __restrict__ offs, int nfeat, int total_bins,
+    int n_classes, int count_labels, int replicas, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned int s_tab[];
+  const int tab = n_classes * total_bins;
+  for (int i = threadIdx.x; i < tab * replicas; i += HB) s_tab[i] = 0;
+  __syncthreads();
+  unsigned int* my = s_tab + (av::wave_id() % replicas) * tab;
+  const long long stride = (long long)gridDim.x * HB;
+  for (long long r = (long long)blockIdx.x * HB + threadIdx.x; r < n; r += stride) {
+    const unsigned c = labels ? labels[r] : 0u;
+    if (c >= (unsigned)n_classes) continue;
+    for (int f = 0; f < nfeat; ++f) {
+      const unsigned v = codes[(long long)f * ld + r];
+      if (v < (unsigned)bins[f]) atomicAdd(&my[c * total_bins + offs[f] + v], 1u);
+    }
+    if (count_labels) atomicAdd(&my[c * total_bins + total_bins - 1], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < tab; i += HB) {
+    unsigned long long s = 0;
+    for (int q = 0; q < replicas; ++q) s += s_tab[q * tab + i];
+    if (s) atomicAdd(&out[i], s);
+  }
+}
+
+// Fallback for tables larger than LDS: global 64-bit atomics.
+__global__ __launch_bounds__(HB) void hist_global_kernel(
+    const uint8_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const int* __restrict__ bins, const int* __restrict__ offs, int nfeat, int total_bins,
+    int n_classes, int count_labels, unsigned long long* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * HB;
+  for (long long r = (long long)blockIdx.x * HB + threadIdx.x; r < n; r += stride) {
+    const unsigned c = labels ? labels[r] : 0u;
+    if (c >= (unsigned)n_classes) continue;
+    for (int f = 0; f < nfeat; ++f) {
+      const unsigned v = codes[(long long)f * ld + r];
+      if (v < (unsigned)bins[f])
+        atomicAdd(&out[(long long)c * total_bins + offs[f] + v], 1ull);
+    }
+    if (count_labels) atomicAdd(&out[(long long)c * total_bins + total_bins - 1], 1ull);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3: pair histograms.  pairs[p] = (fa, fb); out[p][c][ba][bb] at offset poff[p].
+// grid = (row_blocks, n_pairs); LDS table per block (replicated per wave when it fits).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(HB) void pair_hist_kernel(
+    const uint8_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const int* __restrict__ bins, const int* __restrict__ pairs, const long long* __restrict__ poff,
+    int n_classes, int replicas, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned int s_tab[];
+  const int p = blockIdx.y;
+  const int fa = pairs[2 * p], fb = pairs[2 * p + 1];
+  const int Ba = bins[fa], Bb = bins[fb];
+  const int tab = n_classes * Ba * Bb;
+  for (int i = threadIdx.x; i < tab * replicas; i += HB) s_tab[i] = 0;
+  __syncthreads();
+  unsigned int* my = s_tab + (av::wave_id() % replicas) * tab;
+  const uint8_t* ca = codes + (long long)fa * ld;
+  const uint8_t* cb = codes + (long long)fb * ld;
+  const long long stride = (long long)gridDim.x * HB;
+  for (long long r = (long long)blockIdx.x * HB + threadIdx.x; r < n; r += stride) {
+    const unsigned c = labels ? labels[r] : 0u;
+    const unsigned a = ca[r], b = cb[r];
+    if (c < (unsigned)n_classes && a < (unsigned)Ba && b < (unsigned)Bb)
+      atomicAdd(&my[(c * Ba + a) * Bb + b], 1u);
+  }
+  __syncthreads();
+  unsigned long long* o = out + poff[p];
+  for (int i = threadIdx.x; i < tab; i += HB) {
+    unsigned long long s = 0;
+    for (int q = 0; q < replicas; ++q) s += s_tab[q * tab + i];
+    if (s) atomicAdd(&o[i], s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K4: Markov bigram counts.  states int16 [N][L] row-major (padding value < 0 ends a sequence),
+// labels (optional) uint8 [N] select one of C models.  out[c][s][s'].
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(HB) void bigram_kernel(const int16_t* __restrict__ st, long long n,
+                                                    int L, const uint8_t* __restrict__ labels,
+                                                    int n_classes, int S, int replicas,
+                                                    unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned int s_tab[];
+  const int tab = n_classes * S * S;
+  const bool use_lds = replicas > 0;
+  if (use_lds) {
+    for (int i = threadIdx.x; i < tab * replicas; i += HB) s_tab[i] = 0;
+    __syncthreads();
+  }
+  unsigned int* my = use_lds ? s_tab + (av::wave_id() % replicas) * tab : nullptr;
+  const long long total = n * (long long)(L - 1);
+  const long long stride = (long long)gridDim.x * HB;
+  for (long long e = (long long)blockIdx.x * HB + threadIdx.x; e < total; e += stride) {
+    const long long r = e / (L - 1);
+    const int j = (int)(e - r * (L - 1));
+    const int a = st[r * L + j], b = st[r * L + j + 1];
+    if (a < 0 || b < 0 || a >= S || b >= S) continue;
+    const unsigned c = labels ? labels[r] : 0u;
+    if (c >= (unsigned)n_classes) continue;
+    const int idx = (c * S + a) * S + b;
+    if (use_lds) atomicAdd(&my[idx], 1u);
+    else atomicAdd(&out[idx], 1ull);
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < tab; i += HB) {
+      unsigned long long s = 0;
+      for (int q = 0; q < replicas; ++q) s += s_tab[q * tab + i];
+      if (s) atomicAdd(&out[i], s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Class-conditional moments (count, sum, sum of squares) of continuous features — deterministic:
+// per-block partials in a fixed order, then an ordered cross-block reduction (no float atomics).
+// x f32 [F][ld]; part f64 [blocks][C][F][3]; out f64 [C][F][3].
+// ---------------------------------------------------------------------------------------------
+constexpr int MC = 8;  // classes per pass held in registers
+
+__global__ __launch_bounds__(HB) void moments_partial_kernel(
+    const float* __restrict__ x, long long ld, long long n, int nfeat,
+    const uint8_t* __restrict__ labels, int c0, int nc, int n_classes, double* __restrict__ part) {
+  __shared__ double s_red[HB / AV_WAVE][MC][3];
+  const long long per_block = (n + gridDim.x - 1) / gridDim.x;
+  const long long r0 = (long long)blockIdx.x * per_block;
+  const long long r1 = min(n, r0 + per_block);
+  for (int f = 0; f < nfeat; ++f) {
+    double cnt[MC], sm[MC], sq[MC];
+#pragma unroll
+    for (int k = 0; k < MC; ++k) { cnt[k] = 0; sm[k] = 0; sq[k] = 0; }
+    const float* xf = x + (long long)f * ld;
+    for (long long r = r0 + threadIdx.x; r < r1; r += HB) {
+      const int c = (labels ? (int)labels[r] : 0) - c0;
+      const double v = (double)xf[r];
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {
+        const bool m = (k == c) && (k < nc);
+        cnt[k] += m ? 1.0 : 0.0;
+        sm[k] += m ? v : 0.0;
+        sq[k] += m ? v * v : 0.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MC; ++k) {
+      cnt[k] = av::wave_sum(cnt[k]);
+      sm[k] = av::wave_sum(sm[k]);
+      sq[k] = av::wave_sum(sq[k]);
+    }
+    if (av::lane_id() == 0) {
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {
+        s_red[av::wave_id()][k][0] = cnt[k];
+        s_red[av::wave_id()][k][1] = sm[k];
+        s_red[av::wave_id()][k][2] = sq[k];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < nc * 3) {
+      const int k = threadIdx.x / 3, q = threadIdx.x % 3;
+      double s = 0;
+      for (int w = 0; w < HB / AV_WAVE; ++w) s += s_red[w][k][q];
+      part[(((long long)blockIdx.x * n_classes + (c0 + k)) * nfeat + f) * 3 + q] = s;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void moments_reduce_kernel(const double* __restrict__ part, int nblocks, int len,
+                                      double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  double s = 0;
+  for (int b = 0; b < nblocks; ++b) s += part[(long long)b * len + i];
+  out[i] += s;
+}
+
+}  // namespace
+
+// ============================================================================================
+// host launchers
+// ============================================================================================
+namespace avk {
+
+void class_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
+                     const int* d_bins, const int* d_offs, const int* h_bins, int nfeat,
+                     int total_bins, int n_classes, int count_labels, unsigned long long* out,
+                     int mode, hipStream_t stream) {
+  if (n <= 0 || (nfeat <= 0 && !count_labels)) return;
+  int max_cb = 0;
+  for (int f = 0; f < nfeat; ++f) max_cb = std::max(max_cb, n_classes * h_bins[f]);
+  const bool aligned = (ld % 16 == 0) && ((uintptr_t)codes % 16 == 0) &&
+                       (labels == nullptr || (uintptr_t)labels % 16 == 0);
+  if (mode == 0 && max_cb <= 16 && n_classes <= 16 && aligned && nfeat > 0) {
+    const long long nvec = n >> 4;
+    const int grid = av::stream_grid(std::max(1LL, nvec), HB, 4, 2048);
+    for (int f0 = 0; f0 < nfeat; f0 += 8) {
+      const int nf = std::min(8, nfeat - f0);
+      if (nf <= 1)
+        hist_packed_kernel<1><<<grid, HB, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, f0, nf,
+                                                      total_bins, n_classes, count_labels, out);
+      else if (nf <= 2)
+        hist_packed_kernel<2><<<grid, HB, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, f0, nf,
+                                                      total_bins, n_classes, count_labels, out);
+      else if (nf <= 4)
+        hist_packed_kernel<4><<<grid, HB, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, f0, nf,
+                                                      total_bins, n_classes, count_labels, out);
+      else
+        hist_packed_kernel<8><<<grid, HB, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, f0, nf,
+                                                      total_bins, n_classes, count_labels, out);
+      AV_HIP_CHECK(hipGetLastError());
+    }
+    return;
+  }
+  const long long tab_bytes = 4LL * n_classes * total_bins;
+  const int grid = av::stream_grid(n, HB, 8, 2048);
+  if (mode != 2 && tab_bytes <= 64 * 1024) {
+    int replicas = (int)std::min<long long>(HB / AV_WAVE, (64 * 1024) / tab_bytes);
+    replicas = std::max(1, replicas);
+    hist_lds_kernel<<<grid, HB, tab_bytes * replicas, stream>>>(codes, ld, n, labels, d_bins, d_offs,
+                                                               nfeat, total_bins, n_classes,
+                                                               count_labels, replicas, out);
+  } else {
+    hist_global_kernel<<<grid, HB, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, nfeat,
+                                                total_bins, n_classes, count_labels, out);
+  }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void pair_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
+                    const int* d_bins, const int* d_pairs, const long long* d_poff, int n_pairs,
+                    int max_tab, int n_classes, unsigned long long* out, hipStream_t stream) {
+  if (n <= 0 || n_pairs <= 0) return;
+  const long long tab_bytes = 4LL * max_tab;
+  if (tab_bytes > 160 * 1024) throw std::runtime_error("pair_histogram: table exceeds LDS");
+  int replicas = (int)std::max<long long>(1, std::min<long long>(HB / AV_WAVE, (64 * 1024) / tab_bytes));
+  const int rows_blocks = std::max(1, std::min(1024, (int)((n + HB * 16 - 1) / (HB * 16))));
+  const int gx = std::max(1, std::min(rows_blocks, std::max(1, 2048 / n_pairs)));
+  dim3 grid(gx, n_pairs);
+  pair_hist_kernel<<<grid, HB, tab_bytes * replicas, stream>>>(codes, ld, n, labels, d_bins, d_pairs,
+                                                              d_poff, n_classes, replicas, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void bigram_histogram(const int16_t* states, long long n, int L, const uint8_t* labels,
+                      int n_classes, int S, unsigned long long* out, hipStream_t stream) {
+  if (n <= 0 || L < 2) return;
+  const long long tab_bytes = 4LL * n_classes * S * S;
+  int replicas = 0;
+  if (tab_bytes <= 64 * 1024)
+    replicas = (int)std::max<long long>(1, std::min<long long>(HB / AV_WAVE, (64 * 1024) / tab_bytes));
+  const int grid = av::stream_grid(n * (L - 1), HB, 8, 2048);
+  bigram_kernel<<<grid, HB, replicas ? tab_bytes * replicas : 0, stream>>>(states, n, L, labels,
+                                                                           n_classes, S, replicas, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void class_moments(const float* x, long long ld, long long n, int nfeat, const uint8_t* labels,
+                   int n_classes, double* part, int nblocks, double* out, hipStream_t stream) {
+  if (n <= 0 || nfeat <= 0) return;
+  for (int c0 = 0; c0 < n_classes; c0 += MC) {
+    const int nc = std::min(MC, n_classes - c0);
+    moments_partial_kernel<<<nblocks, HB, 0, stream>>>(x, ld, n, nfeat, labels, c0, nc, n_classes,
+                                                        part);
+    AV_HIP_CHECK(hipGetLastError());
+  }
+  const int len = n_classes * nfeat * 3;
+  moments_reduce_kernel<<<(len + 255) / 256, 256, 0, stream>>>(part, nblocks, len, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int moments_blocks(long long n) { return av::stream_grid(n, HB, 16, 1024); }
+
+}  // namespace avk

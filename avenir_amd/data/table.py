@@ -1,0 +1,289 @@
+"""Columnar, schema-encoded tables (layer N3 of SURVEY.md §7.1).
+
+A ``Table`` is the device-resident form of a CSV file described by a ``FeatureSchema``:
+
+* ``codes``   uint8 ``[Fb, ld]`` — binned features (categorical dictionary codes, or int/double
+  bucketized by ``bucketWidth``), feature-major (SoA) with ``ld`` a multiple of 16 so the HIP
+  kernels stream 16 rows per 128-bit load.  Unknown / missing values are coded 255.
+* ``numeric`` float32 ``[Fn, ld]`` — continuous (un-bucketized) numeric features.
+* ``labels``  uint8 ``[ld]`` — class attribute codes (255 = unknown).
+* ``ids``     list of record id strings (when the schema has an id field).
+
+Rows can be loaded as one contiguous shard per rank (``rank``/``world``) — the replacement for
+Hadoop input splits: every rank reads only its own byte range of the file.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..utils.schema import FeatureField, FeatureSchema
+
+CAT, BUCKET, FLOAT, INT = 0, 1, 2, 3
+MISSING = 255
+
+
+def pad16(n: int) -> int:
+    return max(16, ((n + 15) // 16) * 16)
+
+
+@dataclass
+class Table:
+    schema: FeatureSchema | None
+    n: int
+    codes: torch.Tensor                      # uint8 [Fb, ld]
+    binned_fields: list[FeatureField]
+    numeric: torch.Tensor                    # float32 [Fn, ld]
+    numeric_fields: list[FeatureField]
+    labels: torch.Tensor | None = None       # uint8 [ld]
+    class_field: FeatureField | None = None
+    ids: list[str] | None = None
+    lines: list[str] | None = None
+    row_offset: int = 0                      # global index of row 0 (sharded loads)
+    meta: dict = field(default_factory=dict)
+
+    # -- geometry ---------------------------------------------------------------------------------
+    @property
+    def ld(self) -> int:
+        return int(self.codes.shape[1]) if self.codes.numel() else pad16(self.n)
+
+    @property
+    def bins(self) -> list[int]:
+        return [f.num_bins for f in self.binned_fields]
+
+    @property
+    def offsets(self) -> list[int]:
+        out, o = [], 0
+        for b in self.bins:
+            out.append(o)
+            o += b
+        return out
+
+    @property
+    def total_bins(self) -> int:
+        return int(sum(self.bins))
+
+    @property
+    def n_classes(self) -> int:
+        return len(self.class_field.cardinality) if self.class_field is not None else 1
+
+    @property
+    def device(self) -> torch.device:
+        return self.codes.device
+
+    def to(self, device) -> "Table":
+        dev = torch.device(device)
+        return Table(self.schema, self.n, self.codes.to(dev), self.binned_fields,
+                     self.numeric.to(dev), self.numeric_fields,
+                     None if self.labels is None else self.labels.to(dev), self.class_field,
+                     self.ids, self.lines, self.row_offset, dict(self.meta))
+
+    def slice_rows(self, start: int, end: int) -> "Table":
+        """Row range [start, end) as a new table (copies into a fresh 16-aligned layout)."""
+        end = min(end, self.n)
+        m = max(0, end - start)
+        ld = pad16(m)
+        codes = torch.full((self.codes.shape[0], ld), MISSING, dtype=torch.uint8, device=self.device)
+        codes[:, :m] = self.codes[:, start:end]
+        num = torch.zeros((self.numeric.shape[0], ld), dtype=torch.float32, device=self.device)
+        num[:, :m] = self.numeric[:, start:end]
+        lab = None
+        if self.labels is not None:
+            lab = torch.full((ld,), MISSING, dtype=torch.uint8, device=self.device)
+            lab[:m] = self.labels[start:end]
+        return Table(self.schema, m, codes, self.binned_fields, num, self.numeric_fields, lab,
+                     self.class_field, self.ids[start:end] if self.ids else None,
+                     self.lines[start:end] if self.lines else None, self.row_offset + start,
+                     dict(self.meta))
+
+    def select_rows(self, idx: torch.Tensor) -> "Table":
+        idx = idx.to(self.device).long()
+        m = int(idx.numel())
+        ld = pad16(m)
+        codes = torch.full((self.codes.shape[0], ld), MISSING, dtype=torch.uint8, device=self.device)
+        codes[:, :m] = self.codes[:, idx]
+        num = torch.zeros((self.numeric.shape[0], ld), dtype=torch.float32, device=self.device)
+        num[:, :m] = self.numeric[:, idx]
+        lab = None
+        if self.labels is not None:
+            lab = torch.full((ld,), MISSING, dtype=torch.uint8, device=self.device)
+            lab[:m] = self.labels[idx]
+        il = idx.cpu().tolist()
+        return Table(self.schema, m, codes, self.binned_fields, num, self.numeric_fields, lab,
+                     self.class_field, [self.ids[i] for i in il] if self.ids else None,
+                     [self.lines[i] for i in il] if self.lines else None, 0, dict(self.meta))
+
+    def label_values(self) -> list[str]:
+        if self.class_field is None or self.labels is None:
+            return []
+        card = self.class_field.cardinality
+        return [card[c] if c < len(card) else "" for c in self.labels[: self.n].cpu().tolist()]
+
+    def dense_features(self, one_hot: bool = False) -> torch.Tensor:
+        """[n, D] float32 feature matrix (numeric as-is, binned as code or one-hot) in schema order."""
+        cols = []
+        fields = sorted([(f.ordinal, "b", i) for i, f in enumerate(self.binned_fields)] +
+                        [(f.ordinal, "n", i) for i, f in enumerate(self.numeric_fields)])
+        for _, kind, i in fields:
+            if kind == "n":
+                cols.append(self.numeric[i, : self.n].unsqueeze(1))
+            else:
+                c = self.codes[i, : self.n].long()
+                if one_hot:
+                    b = self.binned_fields[i].num_bins
+                    oh = torch.zeros((self.n, b), dtype=torch.float32, device=self.device)
+                    ok = c < b
+                    oh[ok.nonzero().squeeze(1), c[ok]] = 1.0
+                    cols.append(oh)
+                else:
+                    cols.append(c.float().unsqueeze(1))
+        if not cols:
+            return torch.zeros((self.n, 0), device=self.device)
+        return torch.cat(cols, dim=1)
+
+
+# ------------------------------------------------------------------------------------------------
+def _spec_for(f: FeatureField) -> tuple:
+    if f.is_categorical:
+        return (f.ordinal, CAT, list(f.cardinality or []), 1.0, 0, 254)
+    if f.is_bucketed:
+        return (f.ordinal, BUCKET, [], float(f.bucket_width), f.bucket_offset, min(254, f.num_bins - 1))
+    return (f.ordinal, FLOAT, [], 1.0, 0, 254)
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced row range of ``rank`` (first ``n % world`` ranks get one extra row)."""
+    base, rem = divmod(n, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
+             world: int = 1, device: str | torch.device = "cpu", keep_lines: bool = False,
+             skip_header: bool = False, nthreads: int = 8, feature_ordinals: Sequence[int] | None = None,
+             class_ordinal: int | None = None) -> Table:
+    """Parse ``path`` into a ``Table`` (this rank's shard) with the native K1 parser."""
+    feats = [f for f in schema.feature_fields
+             if feature_ordinals is None or f.ordinal in set(feature_ordinals)]
+    if feature_ordinals is not None:
+        # allow selecting non-"feature" fields explicitly
+        have = {f.ordinal for f in feats}
+        feats += [schema.find_field_by_ordinal(o) for o in feature_ordinals if o not in have]
+        feats.sort(key=lambda f: f.ordinal)
+    cls_f = (schema.find_field_by_ordinal(class_ordinal) if class_ordinal is not None
+             else schema.find_class_attr_field())
+    binned = [f for f in feats if f.is_binned]
+    numeric = [f for f in feats if not f.is_binned and f.is_numeric]
+    C = _native.host()
+    if C is not None:
+        csv = C.CsvFile(str(path), delim[0] if delim else ",", skip_header, nthreads)
+        total = csv.num_rows()
+        r0, r1 = shard_range(total, rank, world)
+        specs = [_spec_for(f) for f in binned] + [_spec_for(f) for f in numeric]
+        if cls_f is not None:
+            if not cls_f.cardinality:
+                cls_f.cardinality = csv.distinct(cls_f.ordinal, 255)
+            specs.append(_spec_for(cls_f))
+        cols, _bad = csv.parse(specs, r0, r1)
+        n = r1 - r0
+        ld = pad16(n)
+        codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned
+                 else torch.zeros((0, ld), dtype=torch.uint8))
+        numc = cols[len(binned): len(binned) + len(numeric)]
+        num = torch.zeros((len(numeric), ld), dtype=torch.float32)
+        for i, c in enumerate(numc):
+            num[i, :n] = c
+        labels = cols[-1][:ld].clone() if cls_f is not None else None
+        ids = None
+        idf = schema.id_field
+        lines = None
+        if keep_lines or idf is not None:
+            lines_all = csv.lines(r0, r1)
+            if idf is not None:
+                ids = [ln.split(delim)[idf.ordinal] if ln else "" for ln in lines_all]
+            if keep_lines:
+                lines = lines_all
+    else:  # pure-Python fallback (slow; only when the native module is unavailable)
+        with open(path) as fh:
+            all_lines = [ln.rstrip("\r\n") for ln in fh if ln.strip()]
+        if skip_header:
+            all_lines = all_lines[1:]
+        r0, r1 = shard_range(len(all_lines), rank, world)
+        rows = [ln.split(delim) for ln in all_lines[r0:r1]]
+        n = len(rows)
+        ld = pad16(n)
+        codes = torch.full((len(binned), ld), MISSING, dtype=torch.uint8)
+        for j, f in enumerate(binned):
+            codes[j, :n] = torch.tensor([_encode_py(f, r[f.ordinal] if f.ordinal < len(r) else "")
+                                         for r in rows], dtype=torch.uint8)
+        num = torch.zeros((len(numeric), ld), dtype=torch.float32)
+        for j, f in enumerate(numeric):
+            num[j, :n] = torch.tensor([_float(r[f.ordinal]) if f.ordinal < len(r) else math.nan
+                                       for r in rows])
+        labels = None
+        if cls_f is not None:
+            if not cls_f.cardinality:
+                seen: dict[str, None] = {}
+                for r in rows:
+                    seen.setdefault(r[cls_f.ordinal].strip(), None)
+                cls_f.cardinality = list(seen)
+            labels = torch.full((ld,), MISSING, dtype=torch.uint8)
+            labels[:n] = torch.tensor([_encode_py(cls_f, r[cls_f.ordinal]) for r in rows],
+                                      dtype=torch.uint8)
+        idf = schema.id_field
+        ids = [r[idf.ordinal] for r in rows] if idf is not None else None
+        lines = all_lines[r0:r1] if keep_lines else None
+    t = Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, lines, r0)
+    return t.to(device) if str(device) != "cpu" else t
+
+
+def _float(s: str) -> float:
+    try:
+        return float(s)
+    except ValueError:
+        return math.nan
+
+
+def _encode_py(f: FeatureField, s: str) -> int:
+    s = s.strip()
+    if f.is_categorical:
+        try:
+            return f.cardinality.index(s)
+        except ValueError:
+            return MISSING
+    v = _float(s)
+    if math.isnan(v):
+        return MISSING
+    b = int(math.floor(v / f.bucket_width)) - f.bucket_offset
+    return b if 0 <= b < min(255, f.num_bins) else MISSING
+
+
+def from_arrays(schema: FeatureSchema, columns: dict[int, Sequence], device="cpu") -> Table:
+    """Build a Table from in-memory columns keyed by ordinal (strings or numbers)."""
+    feats = schema.feature_fields
+    cls_f = schema.find_class_attr_field()
+    binned = [f for f in feats if f.is_binned]
+    numeric = [f for f in feats if not f.is_binned and f.is_numeric]
+    n = len(next(iter(columns.values())))
+    ld = pad16(n)
+    codes = torch.full((len(binned), ld), MISSING, dtype=torch.uint8)
+    for j, f in enumerate(binned):
+        codes[j, :n] = torch.tensor([_encode_py(f, str(v)) for v in columns[f.ordinal]],
+                                    dtype=torch.uint8)
+    num = torch.zeros((len(numeric), ld), dtype=torch.float32)
+    for j, f in enumerate(numeric):
+        num[j, :n] = torch.tensor(np.asarray(columns[f.ordinal], dtype=np.float32))
+    labels = None
+    if cls_f is not None and cls_f.ordinal in columns:
+        labels = torch.full((ld,), MISSING, dtype=torch.uint8)
+        labels[:n] = torch.tensor([_encode_py(cls_f, str(v)) for v in columns[cls_f.ordinal]],
+                                  dtype=torch.uint8)
+    idf = schema.id_field
+    ids = [str(v) for v in columns[idf.ordinal]] if idf is not None and idf.ordinal in columns else None
+    return Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids).to(device)

@@ -1,0 +1,345 @@
+"""Naive Bayes: distributed training + batched inference (the first end-to-end slice).
+
+Reference components (behaviour, not code):
+
+* ``BayesianDistribution`` (MR) — per record x feature emits ``(class, featOrd, bin) -> 1`` and
+  ``(class, featOrd) -> (1, v, v^2)`` for continuous features; the reducer writes feature
+  posterior, class prior and feature prior lines (``J/bayesian/BayesianDistribution.java:137-178,
+  :263-327``).  Here: ONE fused K2 histogram launch per rank over the device-resident columns,
+  one deterministic moments launch, then ONE all-reduce of the ``[C, TB]`` counts and the
+  ``[C, Fc, 3]`` moments over RCCL.
+* ``BayesianModel`` / ``FeaturePosterior`` — probability tables (``J/bayesian/BayesianModel.java:
+  50-74, :217-233``).  Here: log-probability tensors staged in LDS by the inference kernel.
+* ``BayesianPredictor`` (map-only) — ``P(f|c) P(c) / P(f)`` in integer percent, default (max) or
+  cost-based arbitration, optional "classified/ambiguous" margin, Validation counters
+  (``J/bayesian/BayesianPredictor.java:227-421``).  Here: one inference kernel launch that also
+  accumulates the confusion matrix; counters are all-reduced once.
+
+The reference's text model layout is kept for interchange: ``class,featOrd,bin,count`` (feature
+posterior), ``class,,,count`` (class prior), ``,featOrd,bin,count`` (feature prior),
+``class,featOrd,,mean,stdDev`` / ``,featOrd,,mean,stdDev`` (continuous).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from pathlib import Path
+
+import torch
+
+from .. import _native
+from ..data.table import Table
+from ..ops import histogram as H
+from ..parallel.comm import Comm, get_comm
+from ..utils.metrics import ConfusionMatrix, Counters
+from ..utils.schema import FeatureSchema
+
+_LOG_FLOOR = math.log(1e-12)
+
+
+@dataclass
+class NBPrediction:
+    pred: torch.Tensor           # int32 [n] predicted class code
+    prob: torch.Tensor | None    # float32 [n, C] posterior (normalised) or reference ratio
+    confusion: torch.Tensor | None  # int64 [C, C] (actual, predicted)
+
+
+class NaiveBayes:
+    def __init__(self, schema: FeatureSchema | None = None, laplace: float = 0.0,
+                 comm: Comm | None = None):
+        self.schema = schema
+        self.laplace = float(laplace)
+        self.comm = comm
+        self.counts: torch.Tensor | None = None      # int64 [C, TB]
+        self.class_n: torch.Tensor | None = None     # int64 [C]
+        self.moments: torch.Tensor | None = None     # f64 [C, Fc, 3]
+        self.bins: list[int] = []
+        self.binned_ordinals: list[int] = []
+        self.numeric_ordinals: list[int] = []
+        self.class_values: list[str] = []
+        self.counters = Counters()
+        self._tables: dict | None = None
+
+    # ----------------------------------------------------------------------------------------
+    # training
+    # ----------------------------------------------------------------------------------------
+    def fit(self, t: Table, reduce: bool = True) -> "NaiveBayes":
+        """Count on this rank's shard, then all-reduce across ranks."""
+        comm = self.comm or get_comm()
+        self.bins = t.bins
+        self.binned_ordinals = [f.ordinal for f in t.binned_fields]
+        self.numeric_ordinals = [f.ordinal for f in t.numeric_fields]
+        self.class_values = list(t.class_field.cardinality) if t.class_field else ["_"]
+        C = t.n_classes
+        # one fused launch: [C, TB] feature counts + a class-count column (no host sync)
+        both = H.class_histogram(t.codes, t.n, self.bins, t.labels, C, count_labels=True)
+        moments = H.class_moments(t.numeric, t.n, t.labels, C)
+        if reduce and comm.is_distributed:
+            comm.all_reduce(both)
+            if moments.numel():
+                comm.all_reduce(moments)
+        self._both = both
+        self.counts, self.class_n = both[:, :-1], both[:, -1]
+        self.moments = moments
+        self._tables = None
+        return self
+
+    def partial_fit(self, t: Table) -> "NaiveBayes":
+        """Accumulate more data (streaming / out-of-core).  Call ``reduce()`` once at the end."""
+        if self.counts is None:
+            return self.fit(t, reduce=False)
+        H.class_histogram(t.codes, t.n, self.bins, t.labels, t.n_classes, out=self._both,
+                          count_labels=True)
+        self.moments += H.class_moments(t.numeric, t.n, t.labels, t.n_classes)
+        self._tables = None
+        return self
+
+    def reduce(self) -> "NaiveBayes":
+        comm = self.comm or get_comm()
+        if comm.is_distributed:
+            comm.all_reduce(self._both)
+            if self.moments.numel():
+                comm.all_reduce(self.moments)
+        self._tables = None
+        return self
+
+    # ----------------------------------------------------------------------------------------
+    # probability tables
+    # ----------------------------------------------------------------------------------------
+    @property
+    def n_classes(self) -> int:
+        return int(self.counts.shape[0])
+
+    def class_counts(self) -> torch.Tensor:
+        """Records per class (the class prior counts)."""
+        return self.class_n
+
+    def tables(self, device=None) -> dict:
+        if self._tables is not None and (device is None or self._tables["logp"].device == torch.device(device)):
+            return self._tables
+        dev = torch.device(device) if device is not None else self.counts.device
+        cnt = self.counts.double().to(dev)
+        C, TB = cnt.shape
+        a = self.laplace
+        logp = torch.empty((C, TB), dtype=torch.float64, device=dev)
+        logfp = torch.empty((TB,), dtype=torch.float64, device=dev)
+        o = 0
+        for b in self.bins:
+            blk = cnt[:, o:o + b] + a
+            logp[:, o:o + b] = torch.log(blk / blk.sum(1, keepdim=True).clamp_min(1e-300))
+            pri = cnt[:, o:o + b].sum(0) + a
+            logfp[o:o + b] = torch.log(pri / pri.sum().clamp_min(1e-300))
+            o += b
+        logp = torch.nan_to_num(logp, nan=_LOG_FLOOR).clamp_min(_LOG_FLOOR)
+        logfp = torch.nan_to_num(logfp, nan=_LOG_FLOOR).clamp_min(_LOG_FLOOR)
+        cc = self.class_counts().double().to(dev)
+        logprior = torch.log((cc / cc.sum().clamp_min(1)).clamp_min(1e-300)).clamp_min(_LOG_FLOOR)
+        # Gaussian parameters of continuous features (sample std, like the reference reducer)
+        m = self.moments.to(dev)
+        n_, s_, q_ = m[..., 0], m[..., 1], m[..., 2]
+        mean = s_ / n_.clamp_min(1)
+        var = ((q_ - n_ * mean * mean) / (n_ - 1).clamp_min(1)).clamp_min(1e-12)
+        std = var.sqrt()
+        pn, ps, pq = n_.sum(0), s_.sum(0), q_.sum(0)
+        pmean = ps / pn.clamp_min(1)
+        pstd = ((pq - pn * pmean * pmean) / (pn - 1).clamp_min(1)).clamp_min(1e-12).sqrt()
+        half_log_2pi = 0.5 * math.log(2 * math.pi)
+        self._tables = {
+            "logp": logp.float().contiguous(), "logfp": logfp.float().contiguous(),
+            "logprior": logprior.float().contiguous(),
+            "gmean": mean.float().contiguous(), "ginvstd": (1.0 / std).float().contiguous(),
+            "glognorm": (-torch.log(std) - half_log_2pi).float().contiguous(),
+            "pmean": pmean.float().contiguous(), "pinvstd": (1.0 / pstd).float().contiguous(),
+            "plognorm": (-torch.log(pstd) - half_log_2pi).float().contiguous(),
+        }
+        return self._tables
+
+    # ----------------------------------------------------------------------------------------
+    # inference
+    # ----------------------------------------------------------------------------------------
+    def predict(self, t: Table, ref_scale: bool = False, with_prob: bool = True,
+                validate: bool = True) -> NBPrediction:
+        tb = self.tables(t.device)
+        C = self.n_classes
+        n = t.n
+        offs = H._dev_i32(t.offsets, t.device)
+        pred = torch.empty((max(n, 1),), dtype=torch.int32, device=t.device)
+        post = torch.empty((max(n, 1), C), dtype=torch.float32, device=t.device) if with_prob else None
+        conf = (torch.zeros((C, C), dtype=torch.int64, device=t.device)
+                if validate and t.labels is not None else None)
+        has_x = t.numeric.shape[0] > 0
+        if t.device.type == "cuda":
+            _native.C().nb_predict(t.codes, n, offs, tb["logp"], tb["logfp"],
+                                   t.numeric if has_x else None,
+                                   tb["gmean"] if has_x else None, tb["ginvstd"] if has_x else None,
+                                   tb["glognorm"] if has_x else None, tb["pmean"] if has_x else None,
+                                   tb["pinvstd"] if has_x else None, tb["plognorm"] if has_x else None,
+                                   tb["logprior"], bool(ref_scale), post, pred, t.labels, conf)
+        else:
+            self._predict_ref(t, tb, ref_scale, post, pred, conf)
+        return NBPrediction(pred[:n], None if post is None else post[:n], conf)
+
+    def _predict_ref(self, t: Table, tb: dict, ref_scale: bool, post, pred, conf) -> None:
+        n, C = t.n, self.n_classes
+        s = tb["logprior"].view(1, C).expand(n, C).clone()
+        lfp = torch.zeros(n)
+        o = 0
+        for f, b in enumerate(self.bins):
+            v = t.codes[f, :n].long()
+            ok = v < b
+            vv = torch.where(ok, v, torch.zeros_like(v)) + o
+            s += torch.where(ok.unsqueeze(1), tb["logp"][:, vv].T, torch.zeros(1))
+            lfp += torch.where(ok, tb["logfp"][vv], torch.zeros(1))
+            o += b
+        if t.numeric.shape[0]:
+            x = t.numeric[:, :n].T  # [n, Fc]
+            z = (x.unsqueeze(1) - tb["gmean"].unsqueeze(0)) * tb["ginvstd"].unsqueeze(0)
+            s += (tb["glognorm"].unsqueeze(0) - 0.5 * z * z).sum(2)
+            zp = (x - tb["pmean"]) * tb["pinvstd"]
+            lfp += (tb["plognorm"] - 0.5 * zp * zp).sum(1)
+        pred[:n] = torch.argmax(s, 1).int()
+        if post is not None:
+            post[:n] = torch.exp(s - lfp.unsqueeze(1)) if ref_scale else torch.softmax(s, 1)
+        if conf is not None:
+            a = t.labels[:n].long()
+            ok = a < C
+            conf += torch.bincount(a[ok] * C + pred[:n].long()[ok], minlength=C * C).view(C, C)
+
+    def validation_counters(self, conf: torch.Tensor, comm: Comm | None = None,
+                            pos_class: int = 1) -> Counters:
+        """Reference "Validation" counter group from an (all-reduced) confusion matrix."""
+        comm = comm or self.comm or get_comm()
+        conf = conf.clone()
+        if comm.is_distributed:
+            comm.all_reduce(conf)
+        c = conf.cpu()
+        cm = ConfusionMatrix(self.class_values[0], self.class_values[min(pos_class, len(self.class_values) - 1)])
+        if c.shape[0] >= 2:
+            cm.add_counts(tp=int(c[pos_class, pos_class]), fp=int(c[:, pos_class].sum() - c[pos_class, pos_class]),
+                          tn=int(c.sum() - c[pos_class, :].sum() - c[:, pos_class].sum() + c[pos_class, pos_class]),
+                          fn=int(c[pos_class, :].sum() - c[pos_class, pos_class]))
+        cm.to_counters(self.counters)
+        self.counters.set("Validation", "Correct", int(torch.diag(c).sum()))
+        self.counters.set("Validation", "Incorrect", int(c.sum() - torch.diag(c).sum()))
+        return self.counters
+
+    @staticmethod
+    def arbitrate_cost(prob_pct: torch.Tensor, fp_cost: float, fn_cost: float, pos: int = 1) -> torch.Tensor:
+        """Cost-based arbitration (``J/util/CostBasedArbitrator.java:50-64``): predict positive when
+        the expected cost of a false negative exceeds that of a false positive."""
+        pos_p = prob_pct[:, pos].float()
+        neg_p = prob_pct[:, 1 - pos].float()
+        return (pos_p * fn_cost > neg_p * fp_cost).int() * pos + (pos_p * fn_cost <= neg_p * fp_cost).int() * (1 - pos)
+
+    # ----------------------------------------------------------------------------------------
+    # reference text model I/O
+    # ----------------------------------------------------------------------------------------
+    def model_lines(self, delim: str = ",") -> list[str]:
+        schema = self.schema
+        cnt = self.counts.cpu()
+        lines: list[str] = []
+        o = 0
+        for f, (ordn, b) in enumerate(zip(self.binned_ordinals, self.bins)):
+            field = schema.find_field_by_ordinal(ordn) if schema else None
+            for c, cv in enumerate(self.class_values):
+                for k in range(b):
+                    v = int(cnt[c, o + k])
+                    if v:
+                        lab = field.bin_label(k) if field else str(k)
+                        lines.append(delim.join([cv, str(ordn), lab, str(v)]))
+            for k in range(b):
+                v = int(cnt[:, o + k].sum())
+                if v:
+                    lab = field.bin_label(k) if field else str(k)
+                    lines.append(delim.join(["", str(ordn), lab, str(v)]))
+            o += b
+        cc = self.class_counts().cpu()
+        for c, cv in enumerate(self.class_values):
+            lines.append(delim.join([cv, "", "", str(int(cc[c]))]))
+        if self.numeric_ordinals:
+            m = self.moments.cpu()
+            for j, ordn in enumerate(self.numeric_ordinals):
+                for c, cv in enumerate(self.class_values):
+                    n_, s_, q_ = (float(x) for x in m[c, j])
+                    mean = s_ / max(n_, 1)
+                    std = math.sqrt(max(q_ - n_ * mean * mean, 0) / max(n_ - 1, 1))
+                    lines.append(delim.join([cv, str(ordn), "", f"{mean:.6g}", f"{std:.6g}"]))
+                n_, s_, q_ = (float(x) for x in m[:, j].sum(0))
+                mean = s_ / max(n_, 1)
+                std = math.sqrt(max(q_ - n_ * mean * mean, 0) / max(n_ - 1, 1))
+                lines.append(delim.join(["", str(ordn), "", f"{mean:.6g}", f"{std:.6g}"]))
+        return lines
+
+    def save_model(self, path: str | Path, delim: str = ",") -> None:
+        Path(path).write_text("\n".join(self.model_lines(delim)) + "\n")
+
+    @classmethod
+    def load_model(cls, path: str | Path, schema: FeatureSchema, delim: str = ",",
+                   comm: Comm | None = None, device="cpu") -> "NaiveBayes":
+        """Load a reference-format model (ours or the Java job's ``part-r-00000``)."""
+        nb = cls(schema, comm=comm)
+        cls_f = schema.find_class_attr_field()
+        nb.class_values = list(cls_f.cardinality)
+        feats = schema.feature_fields
+        binned = [f for f in feats if f.is_binned]
+        numeric = [f for f in feats if not f.is_binned and f.is_numeric]
+        nb.bins = [f.num_bins for f in binned]
+        nb.binned_ordinals = [f.ordinal for f in binned]
+        nb.numeric_ordinals = [f.ordinal for f in numeric]
+        offs = {}
+        o = 0
+        for f in binned:
+            offs[f.ordinal] = (o, f)
+            o += f.num_bins
+        C = len(nb.class_values)
+        counts = torch.zeros((C, o), dtype=torch.int64)
+        moments = torch.zeros((C, len(numeric), 3), dtype=torch.float64)
+        cprior = torch.zeros(C, dtype=torch.int64)
+        num_idx = {f.ordinal: j for j, f in enumerate(numeric)}
+        for line in Path(path).read_text().splitlines():
+            if not line.strip():
+                continue
+            it = line.split(delim)
+            while len(it) < 5:
+                it.append("")
+            if it[0] == "":
+                continue  # feature prior lines are derivable from the posteriors
+            c = nb.class_values.index(it[0])
+            if it[1] == "" and it[2] == "":
+                cprior[c] += int(it[3])
+                continue
+            ordn = int(it[1])
+            if it[2] != "":
+                base, f = offs[ordn]
+                if f.is_categorical:
+                    k = f.cardinality.index(it[2])
+                else:
+                    k = int(it[2]) - f.bucket_offset
+                counts[c, base + k] += int(it[3])
+            else:
+                j = num_idx[ordn]
+                mean, std = float(it[3]), float(it[4])
+                nc = float(cprior[c]) or 1.0
+                moments[c, j] = torch.tensor([nc, mean * nc, (std * std) * (nc - 1) + nc * mean * mean],
+                                             dtype=torch.float64)
+        # fix up moment counts now that all class priors are known
+        for c in range(C):
+            nc = float(cprior[c])
+            if nc > 0 and moments.shape[1]:
+                mean = moments[c, :, 1] / moments[c, :, 0].clamp_min(1)
+                var = (moments[c, :, 2] - moments[c, :, 0] * mean * mean) / (moments[c, :, 0] - 1).clamp_min(1)
+                moments[c, :, 0] = nc
+                moments[c, :, 1] = mean * nc
+                moments[c, :, 2] = var * (nc - 1) + nc * mean * mean
+        nb._both = torch.cat([counts, cprior.view(C, 1)], 1).to(device)
+        nb.counts, nb.class_n = nb._both[:, :-1], nb._both[:, -1]
+        nb.moments = moments.to(device)
+        return nb
+
+
+def _label_counts(t: Table, C: int) -> torch.Tensor:
+    if t.labels is None:
+        return torch.tensor([t.n], dtype=torch.int64, device=t.device)
+    lab = t.labels[: t.n]
+    lab = lab[lab < C].long()
+    return torch.bincount(lab, minlength=C)[:C].to(torch.int64)

@@ -1,0 +1,143 @@
+"""Counting ops (K2/K3/K4/moments).  GPU tensors -> hand-written HIP kernels (``_C``);
+CPU tensors -> the PyTorch reference implementation of the same op (golden oracle)."""
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+
+from .. import _native
+
+
+_CONST_CACHE: dict = {}
+
+
+def _dev_i32(vals: Sequence[int], device) -> torch.Tensor:
+    """Small int32 metadata tensors, cached per (values, device) so repeated launches do not pay a
+    host->device copy (and its implicit synchronisation) every call."""
+    key = (tuple(int(v) for v in vals), str(device))
+    t = _CONST_CACHE.get(key)
+    if t is None:
+        if len(_CONST_CACHE) > 4096:
+            _CONST_CACHE.clear()
+        t = torch.tensor(list(key[0]), dtype=torch.int32, device=device)
+        _CONST_CACHE[key] = t
+    return t
+
+
+def class_histogram(codes: torch.Tensor, n: int, bins: Sequence[int], labels: torch.Tensor | None,
+                    n_classes: int, out: torch.Tensor | None = None, mode: int = 0,
+                    count_labels: bool = False) -> torch.Tensor:
+    """Class-conditional histogram ``out[c, off_f + b]`` (int64 ``[C, sum(bins)]``; with
+    ``count_labels`` an extra last column holds the per-class record counts, fused in the same
+    pass so no host synchronisation is needed).
+
+    ``codes`` uint8 ``[F, ld]`` (feature-major), codes >= bins[f] (e.g. 255) are skipped;
+    ``labels`` uint8 ``[>= n]`` or None (then C = 1).  ``mode``: 0 auto (packed byte-counter fast
+    path when C*bins <= 16), 1 LDS path, 2 global-atomic path (for tests).
+    """
+    F = codes.shape[0]
+    bins = [int(b) for b in bins]
+    assert len(bins) == F, "bins length must equal number of feature rows"
+    tb = sum(bins) + (1 if count_labels else 0)
+    C = int(n_classes) if labels is not None else 1
+    if out is None:
+        out = torch.zeros((C, tb), dtype=torch.int64, device=codes.device)
+    if (F == 0 and not count_labels) or n == 0:
+        return out
+    if codes.is_cuda:
+        offs = [0] * F
+        for f in range(1, F):
+            offs[f] = offs[f - 1] + bins[f - 1]
+        _native.C().class_histogram(codes.contiguous(), int(n),
+                                    None if labels is None else labels.contiguous(),
+                                    _dev_i32(bins, codes.device), _dev_i32(offs, codes.device),
+                                    bins, tb, C, out, int(mode), bool(count_labels))
+        return out
+    # --- CPU reference ---
+    lab = labels[:n].long() if labels is not None else torch.zeros(n, dtype=torch.long)
+    if count_labels:
+        ok = lab < C
+        out[:, tb - 1] += torch.bincount(lab[ok], minlength=C)[:C]
+    o = 0
+    for f, b in enumerate(bins):
+        v = codes[f, :n].long()
+        ok = (v < b) & (lab < C)
+        idx = lab[ok] * b + v[ok]
+        out[:, o:o + b] += torch.bincount(idx, minlength=C * b).view(C, b)
+        o += b
+    return out
+
+
+def pair_histogram(codes: torch.Tensor, n: int, bins: Sequence[int],
+                   pairs: Sequence[tuple[int, int]], labels: torch.Tensor | None,
+                   n_classes: int) -> list[torch.Tensor]:
+    """Joint histograms for feature pairs: list of int64 ``[C, B_a, B_b]`` tensors."""
+    bins = [int(b) for b in bins]
+    C = int(n_classes) if labels is not None else 1
+    sizes = [C * bins[a] * bins[b] for a, b in pairs]
+    if not pairs:
+        return []
+    if codes.is_cuda:
+        offs = [0] * len(pairs)
+        for i in range(1, len(pairs)):
+            offs[i] = offs[i - 1] + sizes[i - 1]
+        flat = torch.zeros(sum(sizes), dtype=torch.int64, device=codes.device)
+        pt = torch.tensor([list(p) for p in pairs], dtype=torch.int32, device=codes.device)
+        po = torch.tensor(offs, dtype=torch.int64, device=codes.device)
+        _native.C().pair_histogram(codes.contiguous(), int(n),
+                                   None if labels is None else labels.contiguous(),
+                                   _dev_i32(bins, codes.device), pt, po, max(sizes), C, flat)
+        return [flat[o:o + s].view(C, bins[a], bins[b]) for o, s, (a, b) in zip(offs, sizes, pairs)]
+    lab = labels[:n].long() if labels is not None else torch.zeros(n, dtype=torch.long)
+    res = []
+    for a, b in pairs:
+        va, vb = codes[a, :n].long(), codes[b, :n].long()
+        ok = (va < bins[a]) & (vb < bins[b]) & (lab < C)
+        idx = (lab[ok] * bins[a] + va[ok]) * bins[b] + vb[ok]
+        res.append(torch.bincount(idx, minlength=C * bins[a] * bins[b]).view(C, bins[a], bins[b]))
+    return res
+
+
+def bigram_histogram(states: torch.Tensor, n_states: int, labels: torch.Tensor | None = None,
+                     n_classes: int = 1) -> torch.Tensor:
+    """Markov transition counts ``[C, S, S]`` from int16 state sequences ``[N, L]`` (negative =
+    padding)."""
+    C = int(n_classes) if labels is not None else 1
+    S = int(n_states)
+    out = torch.zeros((C, S, S), dtype=torch.int64, device=states.device)
+    if states.numel() == 0 or states.shape[1] < 2:
+        return out
+    if states.is_cuda:
+        _native.C().bigram_histogram(states.to(torch.int16).contiguous(),
+                                     None if labels is None else labels.contiguous(), C, S, out)
+        return out
+    a = states[:, :-1].long()
+    b = states[:, 1:].long()
+    lab = (labels[: states.shape[0]].long() if labels is not None
+           else torch.zeros(states.shape[0], dtype=torch.long)).unsqueeze(1).expand_as(a)
+    ok = (a >= 0) & (b >= 0) & (a < S) & (b < S) & (lab < C)
+    idx = (lab[ok] * S + a[ok]) * S + b[ok]
+    out += torch.bincount(idx, minlength=C * S * S).view(C, S, S)
+    return out
+
+
+def class_moments(x: torch.Tensor, n: int, labels: torch.Tensor | None, n_classes: int) -> torch.Tensor:
+    """``[C, F, 3]`` float64 (count, sum, sum of squares) per class and continuous feature."""
+    C = int(n_classes) if labels is not None else 1
+    F = x.shape[0]
+    if F == 0 or n == 0:
+        return torch.zeros((C, F, 3), dtype=torch.float64, device=x.device)
+    if x.is_cuda:
+        return _native.C().class_moments(x.float().contiguous(), int(n),
+                                         None if labels is None else labels.contiguous(), C)
+    lab = labels[:n].long() if labels is not None else torch.zeros(n, dtype=torch.long)
+    xv = x[:, :n].double()
+    out = torch.zeros((C, F, 3), dtype=torch.float64)
+    for c in range(C):
+        m = lab == c
+        xc = xv[:, m]
+        out[c, :, 0] = float(m.sum())
+        out[c, :, 1] = xc.sum(1)
+        out[c, :, 2] = (xc * xc).sum(1)
+    return out

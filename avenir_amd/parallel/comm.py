@@ -1,0 +1,268 @@
+"""Collective communication layer (N4): RCCL over xGMI via ``torch.distributed``.
+
+Every shuffle / broadcast / collect of the reference maps onto one of these ops (SURVEY.md
+§2.24, §2.26):
+
+* Hadoop combiner + reducer sum, Spark ``reduceByKey`` on dense keys  -> ``all_reduce`` (sum)
+* HDFS side files read in every mapper's ``setup()``, Spark ``broadcast`` -> ``broadcast``
+* Spark ``collect``/``collectAsMap``, cascade-SVM support vectors     -> ``all_gather_v``
+* key-partitioned shuffles (joins, group-by-entity)                   -> ``all_to_all_v``
+* bucket-pair replication for all-pairs similarity                    -> ``ring_pass``
+
+One process per GPU; backend ``nccl`` (== RCCL on ROCm) for GPU tensors, ``gloo`` on CPU (tests,
+CI).  With world size 1 every op is a no-op, so single-GPU code paths are the same code.
+
+Design notes for xGMI (7 point-to-point links per MI355X): the payloads here are small dense count
+tensors (KB..tens of MB), so ops are issued ONCE per model/iteration on coalesced flat buffers
+(``all_reduce_coalesced``) rather than per key; RCCL picks its one-shot/tree algorithms for small
+messages and multi-ring for large ones.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import os
+import time
+from contextlib import contextmanager
+from typing import Any, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..utils import logging as alog
+
+_COMM: "Comm | None" = None
+
+
+class CollectiveTimeout(RuntimeError):
+    pass
+
+
+class Comm:
+    def __init__(self, backend: str | None = None, timeout_s: float | None = None,
+                 device: str | None = None):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device == "cuda":
+            n = torch.cuda.device_count()
+            torch.cuda.set_device(self.local_rank % max(1, n))
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            self.device = torch.device("cpu")
+        self.timeout_s = float(timeout_s or os.environ.get("AVENIR_COMM_TIMEOUT", "600"))
+        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        self._owns_pg = False
+        if self.world > 1 and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            kw = {}
+            if self.backend == "nccl":
+                kw["device_id"] = self.device
+            dist.init_process_group(self.backend, rank=self.rank, world_size=self.world,
+                                    timeout=_dt.timedelta(seconds=self.timeout_s), **kw)
+            self._owns_pg = True
+        if dist.is_initialized():
+            self.world = dist.get_world_size()
+            self.rank = dist.get_rank()
+        self.stats = {"calls": 0, "bytes": 0, "seconds": 0.0}
+
+    # ------------------------------------------------------------------------------------------
+    @property
+    def is_distributed(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def _account(self, t: torch.Tensor, t0: float) -> None:
+        self.stats["calls"] += 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+        self.stats["seconds"] += time.perf_counter() - t0
+
+    def _prep(self, t: torch.Tensor) -> tuple[torch.Tensor, bool]:
+        """gloo only handles CPU tensors, RCCL only GPU tensors: move if needed."""
+        if self.backend == "gloo" and t.is_cuda:
+            return t.cpu(), True
+        return t, False
+
+    # ------------------------------------------------------------------------------------------
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place all-reduce (sum|max|min|prod); returns ``t``."""
+        if not self.is_distributed:
+            return t
+        t0 = time.perf_counter()
+        x, moved = self._prep(t)
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+               "prod": dist.ReduceOp.PRODUCT}[op]
+        dist.all_reduce(x, op=rop)
+        if moved:
+            t.copy_(x)
+        self._account(t, t0)
+        return t
+
+    def all_reduce_coalesced(self, tensors: Sequence[torch.Tensor], op: str = "sum") -> None:
+        """All-reduce several tensors of one dtype with a single collective (flat buffer)."""
+        if not self.is_distributed or not tensors:
+            return
+        by_dtype: dict[torch.dtype, list[torch.Tensor]] = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for ts in by_dtype.values():
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            self.all_reduce(flat, op)
+            o = 0
+            for t in ts:
+                k = t.numel()
+                t.copy_(flat[o:o + k].view_as(t))
+                o += k
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if not self.is_distributed:
+            return t
+        t0 = time.perf_counter()
+        x, moved = self._prep(t)
+        dist.broadcast(x, src)
+        if moved:
+            t.copy_(x)
+        self._account(t, t0)
+        return t
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.is_distributed:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src)
+        return box[0]
+
+    def all_gather_object(self, obj: Any) -> list[Any]:
+        if not self.is_distributed:
+            return [obj]
+        out: list[Any] = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Equal-shape all-gather -> [world, *t.shape]."""
+        if not self.is_distributed:
+            return t.unsqueeze(0)
+        x, moved = self._prep(t.contiguous())
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x)
+        return out.to(t.device) if moved else out
+
+    def all_gather_v(self, t: torch.Tensor) -> torch.Tensor:
+        """Variable-length all-gather along dim 0 (RCCL has no AllGatherV: exchange counts,
+        pad to the max, all-gather, strip)."""
+        if not self.is_distributed:
+            return t
+        n = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
+        counts = self.all_gather(n).view(-1).tolist()
+        m = max(counts)
+        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        g = self.all_gather(pad)
+        return torch.cat([g[r, : counts[r]] for r in range(self.world)], dim=0)
+
+    def all_to_all_v(self, chunks: list[torch.Tensor]) -> list[torch.Tensor]:
+        """Send ``chunks[r]`` to rank r; receive one tensor from every rank (dim-0 variable)."""
+        if not self.is_distributed:
+            return [chunks[0]]
+        dev = chunks[0].device
+        sizes = torch.tensor([c.shape[0] for c in chunks], dtype=torch.long, device=dev)
+        recv_sizes = torch.empty_like(sizes)
+        if self.backend == "gloo":
+            # gloo lacks all_to_all: emulate with all_gather_v of (dest, payload)
+            allsizes = self.all_gather(sizes)  # [world(src), world(dst)]
+            flat = torch.cat(chunks, dim=0)
+            g = self.all_gather_v(flat)
+            out, o = [], 0
+            for src in range(self.world):
+                row = allsizes[src].tolist()
+                start = o + sum(row[: self.rank])
+                out.append(g[start:start + row[self.rank]])
+                o += sum(row)
+            return out
+        dist.all_to_all_single(recv_sizes, sizes)
+        tail = tuple(chunks[0].shape[1:])
+        send = torch.cat(chunks, dim=0)
+        recv = torch.empty((int(recv_sizes.sum()),) + tail, dtype=send.dtype, device=dev)
+        dist.all_to_all_single(recv, send, recv_sizes.tolist(), sizes.tolist())
+        return list(torch.split(recv, recv_sizes.tolist()))
+
+    def ring_pass(self, t: torch.Tensor) -> torch.Tensor:
+        """Send ``t`` to rank+1 and receive from rank-1 (systolic all-pairs schedule).  Shapes may
+        differ between ranks: the dim-0 length travels first."""
+        if not self.is_distributed:
+            return t
+        nxt, prv = (self.rank + 1) % self.world, (self.rank - 1) % self.world
+        x, moved = self._prep(t.contiguous())
+        n_out = torch.tensor([x.shape[0]], dtype=torch.long, device=x.device)
+        n_in = torch.empty_like(n_out)
+        reqs = [dist.isend(n_out, nxt), dist.irecv(n_in, prv)]
+        for r in reqs:
+            r.wait()
+        recv = torch.empty((int(n_in.item()),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        reqs = [dist.isend(x, nxt), dist.irecv(recv, prv)]
+        for r in reqs:
+            r.wait()
+        return recv.to(t.device) if moved else recv
+
+    def barrier(self) -> None:
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def reduce_max_scalar(self, v: float) -> float:
+        if not self.is_distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        self.all_reduce(t, "max")
+        return float(t.item())
+
+    def shutdown(self) -> None:
+        if self._owns_pg and dist.is_initialized():
+            dist.destroy_process_group()
+            self._owns_pg = False
+
+
+def get_comm(**kw) -> Comm:
+    global _COMM
+    if _COMM is None:
+        _COMM = Comm(**kw)
+    return _COMM
+
+
+def set_comm(c: Comm | None) -> None:
+    global _COMM
+    _COMM = c
+
+
+@contextmanager
+def timed_collective(name: str, warn_s: float = 30.0):
+    """Watchdog-style timing of a collective phase: logs a warning when a phase is slow (a hung
+    peer shows up here long before RCCL's own timeout fires)."""
+    t0 = time.perf_counter()
+    yield
+    dt = time.perf_counter() - t0
+    if dt > warn_s:
+        alog.get_logger("comm").warning("collective %s took %.1fs", name, dt)
+
+
+def maybe_inject_fault(iteration: int, rank: int | None = None) -> None:
+    """Env-driven fault injection for recovery tests: when
+    ``AVMI_FAULT_RANK`` == this rank and ``AVMI_FAULT_ITER`` == iteration, raise."""
+    fr = os.environ.get("AVMI_FAULT_RANK")
+    fi = os.environ.get("AVMI_FAULT_ITER")
+    if fr is None or fi is None:
+        return
+    r = rank if rank is not None else int(os.environ.get("RANK", "0"))
+    if int(fr) == r and int(fi) == iteration:
+        mode = os.environ.get("AVMI_FAULT_MODE", "raise")
+        if mode == "exit":
+            os._exit(17)
+        raise RuntimeError(f"injected fault at rank {r} iteration {iteration}")

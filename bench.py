@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: distributed Naive Bayes training throughput (rows/s, whole job).
+
+BASELINE.json names no metric (the reference publishes no numbers), so the
+headline is the one BASELINE.md lists first and SURVEY.md §7.3 names as the minimum end-to-end
+slice: Naive Bayes churn-model training (``BayesianDistribution``) on the ``resource/churn.json``
+schema — 5 categorical features, 2 classes.
+
+One step = one complete training pass over this rank's shard: the fused K2 class-conditional
+histogram (HIP, packed byte counters) + class counts over ``rows_per_gpu`` records, ONE RCCL
+all-reduce of the [C, TB+1] count table, and the model finalisation (log-probability tables for
+the predictor).  Weak scaling: every GPU owns ``rows_per_gpu`` synthetic records (same
+distributions as the reference's ``usage.rb``), generated on device before timing.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows-per-gpu R]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--predict", action="store_true", help="also time batched inference")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+              file=sys.stderr)
+
+    from avenir_amd.data.synth import CHURN_SCHEMA, churn_device
+    from avenir_amd.data.table import Table
+    from avenir_amd.models.bayes import NaiveBayes
+    from avenir_amd.parallel.comm import get_comm
+    from avenir_amd.utils.schema import FeatureSchema
+
+    comm = get_comm()
+    dev = comm.device
+    if dev.type != "cuda":
+        print("[bench] no GPU visible: running on CPU with a tiny problem", file=sys.stderr)
+        args.rows_per_gpu = min(args.rows_per_gpu, 1 << 16)
+    n = int(args.rows_per_gpu)
+    schema = FeatureSchema.from_json(CHURN_SCHEMA)
+    codes, labels = churn_device(n, seed=1234 + comm.rank, device=dev)
+    feats = schema.feature_fields
+    table = Table(schema, n, codes, feats, torch.zeros((0, codes.shape[1]), device=dev), [],
+                  labels, schema.find_class_attr_field())
+    nb = NaiveBayes(schema, comm=comm)
+
+    def step():
+        nb.fit(table)
+        nb.tables()
+
+    for _ in range(args.warmup):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = comm.reduce_max_scalar(dt)
+
+    # sanity: the model must have counted every record of every rank in the last step
+    total_rows = int(nb.class_n.sum().item())
+    assert total_rows == n * comm.world, (total_rows, n * comm.world)
+
+    ms = dt * 1000.0 / args.steps
+    rows_per_s = n * comm.world * args.steps / dt
+    bytes_per_row = codes.shape[0] + 1  # 5 feature codes + 1 label byte
+    extra = {"ms_per_step": ms, "hbm_gbps_per_gpu": n * bytes_per_row / (ms / 1000.0) / 1e9}
+    if args.predict:
+        pr_n = min(n, 1 << 26)
+        sub = Table(schema, pr_n, codes[:, : ((pr_n + 15) // 16) * 16].contiguous(), feats,
+                    torch.zeros((0, 16), device=dev), [], labels[: ((pr_n + 15) // 16) * 16].contiguous(),
+                    schema.find_class_attr_field())
+        nb.predict(sub, with_prob=True)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(5):
+            nb.predict(sub, with_prob=True)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        extra["predict_rows_per_s_per_gpu"] = pr_n * 5 / (time.perf_counter() - t1)
+
+    if comm.rank == 0:
+        out = {
+            "metric": "naive_bayes_train_rows_per_s",
+            "value": rows_per_s,
+            "unit": "rows/s",
+            "n_gpus": comm.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8-codes/int64-counts (exact integer counting)",
+            "data": "synthetic (device-generated, resource/usage.rb distributions)",
+            "config": {
+                "model": "NaiveBayes(resource/churn.json: 5 categorical features, 2 classes)",
+                "global_batch": n * comm.world,
+                "rows_per_gpu": n,
+                "seq_len": None,
+                "parallelism": f"dp{comm.world}",
+            },
+            "extra": extra,
+        }
+        print(json.dumps(out))
+    comm.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

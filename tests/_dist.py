@@ -1,0 +1,54 @@
+"""Helpers to run multi-rank (gloo, CPU) tests in-process via torch.multiprocessing."""
+from __future__ import annotations
+
+import os
+import socket
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, args, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    try:
+        from avenir_amd.parallel import comm as C
+        C.set_comm(None)
+        c = C.get_comm(device="cpu", backend="gloo")
+        res = fn(rank, world, *args)
+        q.put((rank, "ok", res))
+        c.barrier()
+        c.shutdown()
+    except Exception:  # noqa: BLE001
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def run_world(fn, world: int, *args, timeout: float = 120.0):
+    """Run ``fn(rank, world, *args)`` on ``world`` gloo ranks; return results ordered by rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, status, res = q.get(timeout=timeout)
+            if status != "ok":
+                raise AssertionError(f"rank {rank} failed:\n{res}")
+            out[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return [out[r] for r in range(world)]

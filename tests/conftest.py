@@ -1,0 +1,41 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+REF = "/root/reference"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture
+def ref_resource():
+    def _p(name):
+        p = os.path.join(REF, "resource", name)
+        if not os.path.exists(p):
+            pytest.skip(f"reference resource {name} not mounted")
+        return p
+    return _p
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture
+def cuda():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    return torch.device("cuda")
