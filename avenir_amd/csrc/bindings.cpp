@@ -4,16 +4,19 @@
 // shape must never reach a hand-written kernel), fetches the current HIP stream of the tensor's
 // device, and calls the torch-free launcher in csrc/kernels/*.hip.
 #include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "avenir_kernels.h"
 #include "avenir_host.h"
 
 namespace {
 
+// PyTorch-ROCm exposes HIP devices as device type "cuda": use its masquerading guard/stream.
+using DevGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
+
 hipStream_t cur_stream(const at::Tensor& t) {
-  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 #define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
@@ -65,7 +68,7 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
     TORCH_CHECK(labels->numel() >= n, "labels shorter than n");
     lab = labels->data_ptr<uint8_t>();
   }
-  c10::hip::HIPGuard g(codes.device());
+  DevGuard g(codes.device());
   avk::class_histogram(codes.data_ptr<uint8_t>(), ld, n, lab, bins.data_ptr<int>(),
                        offs.data_ptr<int>(), hb.data(), (int)F, (int)total_bins, (int)n_classes,
                        count_labels ? 1 : 0,
@@ -96,7 +99,7 @@ void pair_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at::
     TORCH_CHECK(labels->numel() >= n, "labels shorter than n");
     lab = labels->data_ptr<uint8_t>();
   }
-  c10::hip::HIPGuard g(codes.device());
+  DevGuard g(codes.device());
   avk::pair_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, lab, bins.data_ptr<int>(),
                       pairs.data_ptr<int>(), reinterpret_cast<const long long*>(poff.data_ptr<int64_t>()), (int)pairs.size(0),
                       (int)max_tab, (int)n_classes,
@@ -120,7 +123,7 @@ void bigram_histogram(const at::Tensor& states, const c10::optional<at::Tensor>&
     TORCH_CHECK(labels->numel() >= states.size(0), "labels shorter than N");
     lab = labels->data_ptr<uint8_t>();
   }
-  c10::hip::HIPGuard g(states.device());
+  DevGuard g(states.device());
   avk::bigram_histogram(states.data_ptr<int16_t>(), states.size(0), (int)states.size(1), lab,
                         (int)n_classes, (int)S,
                         reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()),
@@ -140,7 +143,7 @@ at::Tensor class_moments(const at::Tensor& x, int64_t n, const c10::optional<at:
     lab = labels->data_ptr<uint8_t>();
   }
   const int64_t F = x.size(0);
-  c10::hip::HIPGuard g(x.device());
+  DevGuard g(x.device());
   auto opts = x.options().dtype(at::kDouble);
   auto out = at::zeros({n_classes, F, 3}, opts);
   const int nb = avk::moments_blocks(n);
@@ -208,7 +211,7 @@ void nb_predict(const at::Tensor& codes, int64_t n, const at::Tensor& offs, cons
     lab = labels->data_ptr<uint8_t>();
     conf = reinterpret_cast<unsigned long long*>(confusion->data_ptr<int64_t>());
   }
-  c10::hip::HIPGuard g(codes.device());
+  DevGuard g(codes.device());
   avk::nb_predict(codes.data_ptr<uint8_t>(), codes.size(1), n, (int)codes.size(0),
                   offs.data_ptr<int>(), logp.data_ptr<float>(), ptr_or_null<float>(logfp), TB,
                   ptr_or_null<float>(x), ldx, ncont, ptr_or_null<float>(gmean),

@@ -161,6 +161,200 @@ __global__ __launch_bounds__(HB) void hist_packed_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Class-split byte counters (fastest path: every bins[f] <= 7 and C <= 4).
+//
+// Per lane and per (class, feature) one u64 holds 8 byte counters indexed by the feature code.
+// The class of a row is turned into C 0/1 masks ONCE per row and shared by all features; a
+// feature byte then costs one bfe (shift amount 8*(code&7) precomputed SWAR for 4 rows) plus C
+// fused `v_lshl_add_u64` (acc += x_c << s).  A missing code (255) lands in byte 7, which is never a
+// valid bin (bins <= 7), so no validity test is needed in the hot loop — and byte 0..7 of the
+// first feature sum to the class's record count for free.
+// Every 15 tiles the byte counters are widened into per-lane 16-bit counters (no cross-lane
+// traffic); the 64-lane reduction happens once at the end (or every 256 flushes).
+// ---------------------------------------------------------------------------------------------
+template <int NF, int C>
+__global__ __launch_bounds__(HB) void hist_split_kernel(
+    const uint8_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const int* __restrict__ bins, const int* __restrict__ offs, int f0, int nfeat, int total_bins,
+    int count_labels, unsigned long long* __restrict__ out) {
+  constexpr int TAB = NF * C * 8;
+  constexpr int WPB = HB / AV_WAVE;
+  __shared__ unsigned int s_tab[WPB * TAB];  // one private slice per wave: plain stores, no atomics
+  for (int i = threadIdx.x; i < WPB * TAB; i += HB) s_tab[i] = 0;
+  __syncthreads();
+  unsigned int* my_tab = s_tab + av::wave_id() * TAB;
+
+  const uint4* col[NF];
+#pragma unroll
+  for (int k = 0; k < NF; ++k)
+    col[k] = reinterpret_cast<const uint4*>(codes + (long long)(f0 + k) * ld);
+  const uint4* lab = reinterpret_cast<const uint4*>(labels);
+
+  unsigned long long a8[C][NF], ae[C][NF], ao[C][NF];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int k = 0; k < NF; ++k) { a8[c][k] = 0; ae[c][k] = 0; ao[c][k] = 0; }
+
+  const unsigned long long M = 0x00FF00FF00FF00FFull;
+  auto widen = [&]() {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        ae[c][k] += a8[c][k] & M;
+        ao[c][k] += (a8[c][k] >> 8) & M;
+        a8[c][k] = 0;
+      }
+  };
+  auto reduce_to_lds = [&]() {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        {
+          const unsigned long long e = av::wave_sum_u64(ae[c][k]);
+          const unsigned long long o = av::wave_sum_u64(ao[c][k]);
+          // lane l < 8 owns byte counter l: even bytes come from e, odd bytes from o
+          const int l = av::lane_id();
+          const unsigned long long src = (l & 1) ? o : e;
+          const unsigned val = (unsigned)((src >> (16 * ((l >> 1) & 3))) & 0xFFFFu);
+          if (l < 8) my_tab[(k * C + c) * 8 + l] += val;
+        }
+        ae[c][k] = 0;
+        ao[c][k] = 0;
+      }
+  };
+
+  const long long nvec = n >> 4;
+  const long long ntiles = (nvec + AV_WAVE - 1) / AV_WAVE;
+  const int wpb = HB / AV_WAVE;
+  const long long gw = (long long)blockIdx.x * wpb + av::wave_id();
+  const long long nw = (long long)gridDim.x * wpb;
+  int since_flush = 0, flushes = 0;
+  for (long long t = gw; t < ntiles; t += nw) {
+    const long long v = t * AV_WAVE + av::lane_id();
+    if (v < nvec) {
+      const uint4 cl4 = (C > 1) ? lab[v] : make_uint4(0, 0, 0, 0);
+      uint4 x4[NF];
+#pragma unroll
+      for (int k = 0; k < NF; ++k)
+        x4[k] = col[k][v];
+      const unsigned cw[4] = {cl4.x, cl4.y, cl4.z, cl4.w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        // shift amounts 8*(code & 7) for 4 rows at once (SWAR, no carries)
+        unsigned sw[NF];
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+          const unsigned xw = (w == 0) ? x4[k].x : (w == 1) ? x4[k].y : (w == 2) ? x4[k].z : x4[k].w;
+          sw[k] = (xw & 0x07070707u) << 3;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          unsigned long long xc[C];
+          if (C == 1) {
+            xc[0] = 1ull;
+          } else {
+            const unsigned cb = (cw[w] >> (8 * j)) & 0xFFu;
+#pragma unroll
+            for (int c = 0; c < C; ++c) xc[c] = (cb == (unsigned)c) ? 1ull : 0ull;
+          }
+#pragma unroll
+          for (int k = 0; k < NF; ++k) {
+            const unsigned sh = (sw[k] >> (8 * j)) & 0xFFu;
+#pragma unroll
+            for (int c = 0; c < C; ++c) a8[c][k] += xc[c] << sh;
+          }
+        }
+      }
+    }
+    if (++since_flush == FLUSH_EVERY) {  // wave-uniform
+      widen();
+      since_flush = 0;
+      if (++flushes == 256) {  // 16-bit per-lane counters: 256 * 240 < 65536
+        reduce_to_lds();
+        flushes = 0;
+      }
+    }
+  }
+  widen();
+  reduce_to_lds();
+
+  // tail rows (n % 16): block 0, scalar LDS atomics
+  if (blockIdx.x == 0) {
+    for (long long r = nvec * 16 + threadIdx.x; r < n; r += HB) {
+      const unsigned c = (C > 1) ? labels[r] : 0u;
+      if (c >= (unsigned)C) continue;
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        const unsigned v = codes[(long long)(f0 + k) * ld + r];
+        atomicAdd(&s_tab[(k * C + c) * 8 + (v & 7u)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TAB; i += HB) {
+    unsigned long long tot = 0;
+#pragma unroll
+    for (int w = 0; w < WPB; ++w) tot += s_tab[w * TAB + i];
+    s_tab[i] = (unsigned)tot;  // slice 0 now holds the block total (each i owned by one thread)
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TAB; i += HB) {
+    const int k = i / (C * 8), c = (i / 8) % C, b = i % 8;
+    const unsigned v = s_tab[i];
+    if (v && b < bins[f0 + k])
+      atomicAdd(&out[(long long)c * total_bins + offs[f0 + k] + b], (unsigned long long)v);
+  }
+  if (count_labels && f0 == 0 && threadIdx.x < C) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s += s_tab[(0 * C + threadIdx.x) * 8 + b];
+    if (s) atomicAdd(&out[(long long)threadIdx.x * total_bins + total_bins - 1], s);
+  }
+}
+
+template <int C, int NF>
+void launch_split_nf(int grid, const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
+                     const int* d_bins, const int* d_offs, int f0, int total_bins, int count_labels,
+                     unsigned long long* out, hipStream_t stream) {
+  hist_split_kernel<NF, C><<<grid, HB, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, f0, NF,
+                                                   total_bins, count_labels, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+template <int C>
+void launch_split(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
+                  const int* d_bins, const int* d_offs, int nfeat, int total_bins, int count_labels,
+                  unsigned long long* out, hipStream_t stream) {
+  const long long nvec = n >> 4;
+  const int grid = av::stream_grid(std::max(1LL, nvec), HB, 4, 2048);
+  constexpr int MAXF = (C <= 2) ? 8 : 4;
+  for (int f0 = 0; f0 < nfeat; f0 += MAXF) {
+    const int nf = std::min(MAXF, nfeat - f0);
+#define AV_SPLIT(K) launch_split_nf<C, K>(grid, codes, ld, n, labels, d_bins, d_offs, f0, total_bins, count_labels, out, stream)
+    switch (nf) {
+      case 1: AV_SPLIT(1); break;
+      case 2: AV_SPLIT(2); break;
+      case 3: AV_SPLIT(3); break;
+      case 4: AV_SPLIT(4); break;
+      default:
+        if constexpr (MAXF == 8) {
+          switch (nf) {
+            case 5: AV_SPLIT(5); break;
+            case 6: AV_SPLIT(6); break;
+            case 7: AV_SPLIT(7); break;
+            default: AV_SPLIT(8); break;
+          }
+        }
+    }
+#undef AV_SPLIT
+  }
+}
+
 // General path: LDS-privatised table with R replicas (one per wave when it fits) so that lanes of
 // different waves never contend; replicas are summed once per block.
 __global__ __launch_bounds__(HB) void hist_lds_kernel(
@@ -361,7 +555,20 @@ void class_histogram(const uint8_t* codes, long long ld, long long n, const uint
   for (int f = 0; f < nfeat; ++f) max_cb = std::max(max_cb, n_classes * h_bins[f]);
   const bool aligned = (ld % 16 == 0) && ((uintptr_t)codes % 16 == 0) &&
                        (labels == nullptr || (uintptr_t)labels % 16 == 0);
-  if (mode == 0 && max_cb <= 16 && n_classes <= 16 && aligned && nfeat > 0) {
+  int max_b = 0;
+  for (int f = 0; f < nfeat; ++f) max_b = std::max(max_b, h_bins[f]);
+  if (mode == 0 && aligned && nfeat > 0 && max_b <= 7 && n_classes <= 4) {
+    const uint8_t* lab = n_classes > 1 ? labels : nullptr;
+    if (n_classes > 1 && labels == nullptr) n_classes = 1;
+    switch (n_classes) {
+      case 1: launch_split<1>(codes, ld, n, lab, d_bins, d_offs, nfeat, total_bins, count_labels, out, stream); break;
+      case 2: launch_split<2>(codes, ld, n, lab, d_bins, d_offs, nfeat, total_bins, count_labels, out, stream); break;
+      case 3: launch_split<3>(codes, ld, n, lab, d_bins, d_offs, nfeat, total_bins, count_labels, out, stream); break;
+      default: launch_split<4>(codes, ld, n, lab, d_bins, d_offs, nfeat, total_bins, count_labels, out, stream); break;
+    }
+    return;
+  }
+  if ((mode == 0 || mode == 3) && max_cb <= 16 && n_classes <= 16 && aligned && nfeat > 0) {
     const long long nvec = n >> 4;
     const int grid = av::stream_grid(std::max(1LL, nvec), HB, 4, 2048);
     for (int f0 = 0; f0 < nfeat; f0 += 8) {

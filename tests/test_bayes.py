@@ -125,7 +125,10 @@ def _random_codes(n, bins, C, seed=0, missing_frac=0.01):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bins,C,mode", [
-    (100_003, [4, 3, 3, 3, 5], 2, 0),          # packed fast path, ragged tail
+    (100_003, [4, 3, 3, 3, 5], 2, 0),          # class-split fast path, ragged tail
+    (100_003, [4, 3, 3, 3, 5], 2, 3),          # packed-idx path
+    (33_333, [7, 1, 2], 4, 0),                 # class-split C=4
+    (33_335, [7, 6, 2, 5, 3, 3, 1, 2, 4, 7], 1, 0),  # class-split C=1, two groups
     (1 << 20, [2, 8, 4, 2, 3, 5, 7, 1, 2], 2, 0),  # > 8 features -> two feature groups
     (50_000, [17, 30, 9], 3, 0),               # LDS path (C*B > 16)
     (50_000, [4, 3], 2, 1),                    # forced LDS path
@@ -133,8 +136,8 @@ def _random_codes(n, bins, C, seed=0, missing_frac=0.01):
 ])
 def test_class_histogram_gpu(cuda, n, bins, C, mode):
     codes, lab = _random_codes(n, bins, C, seed=n)
-    ref = H.class_histogram(codes, n, bins, lab, C)
-    got = H.class_histogram(codes.to(cuda), n, bins, lab.to(cuda), C, mode=mode)
+    ref = H.class_histogram(codes, n, bins, lab, C, count_labels=True)
+    got = H.class_histogram(codes.to(cuda), n, bins, lab.to(cuda), C, mode=mode, count_labels=True)
     assert torch.equal(got.cpu(), ref)
 
 
