@@ -221,8 +221,144 @@ void nb_predict(const at::Tensor& codes, int64_t n, const at::Tensor& offs, cons
                   ptr_or_null<float>(post), pred.data_ptr<int>(), lab, conf, cur_stream(codes));
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// trees (K7/K8)
+// ---------------------------------------------------------------------------------------------
+static void check_codes(const at::Tensor& codes, int64_t n) {
+  CHECK_DEV(codes);
+  CHECK_DTYPE(codes, at::kByte);
+  TORCH_CHECK(codes.dim() == 2 && n <= codes.size(1), "codes must be [F, ld>=n]");
+}
+
+void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels,
+                    const at::Tensor& node, const c10::optional<at::Tensor>& weight,
+                    const at::Tensor& bins, const at::Tensor& offs, int64_t total_bins,
+                    int64_t n_classes, int64_t n_nodes, at::Tensor& hist) {
+  check_codes(codes, n);
+  CHECK_DEV(labels);
+  CHECK_DTYPE(labels, at::kByte);
+  CHECK_DEV(node);
+  CHECK_DTYPE(node, at::kInt);
+  TORCH_CHECK(labels.numel() >= n && node.numel() >= n, "labels/node too short");
+  CHECK_DEV(bins);
+  CHECK_DEV(offs);
+  TORCH_CHECK(bins.numel() == codes.size(0) && offs.numel() == codes.size(0), "bins/offs != F");
+  CHECK_DEV(hist);
+  CHECK_DTYPE(hist, at::kLong);
+  TORCH_CHECK(hist.numel() == n_nodes * n_classes * total_bins, "hist must be [A, C, TB]");
+  const uint8_t* w = nullptr;
+  if (weight.has_value() && weight->defined()) {
+    CHECK_DEV((*weight));
+    CHECK_DTYPE((*weight), at::kByte);
+    TORCH_CHECK(weight->numel() >= n, "weight too short");
+    w = weight->data_ptr<uint8_t>();
+  }
+  DevGuard g(codes.device());
+  avk::node_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, labels.data_ptr<uint8_t>(),
+                      node.data_ptr<int>(), w, bins.data_ptr<int>(), offs.data_ptr<int>(),
+                      (int)codes.size(0), (int)total_bins, (int)n_classes, (int)n_nodes,
+                      reinterpret_cast<unsigned long long*>(hist.data_ptr<int64_t>()), cur_stream(codes));
+}
+
+void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& node,
+                         const at::Tensor& g, const at::Tensor& h, const at::Tensor& bins,
+                         const at::Tensor& offs, int64_t total_bins, int64_t n_nodes, at::Tensor& out) {
+  check_codes(codes, n);
+  CHECK_DEV(node);
+  CHECK_DTYPE(node, at::kInt);
+  CHECK_DEV(g);
+  CHECK_DTYPE(g, at::kFloat);
+  CHECK_DEV(h);
+  CHECK_DTYPE(h, at::kFloat);
+  TORCH_CHECK(node.numel() >= n && g.numel() >= n && h.numel() >= n, "node/g/h too short");
+  CHECK_DEV(out);
+  CHECK_DTYPE(out, at::kLong);
+  TORCH_CHECK(out.numel() == n_nodes * total_bins * 2, "out must be [A, TB, 2]");
+  DevGuard gd(codes.device());
+  avk::node_grad_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, node.data_ptr<int>(),
+                           g.data_ptr<float>(), h.data_ptr<float>(), bins.data_ptr<int>(),
+                           offs.data_ptr<int>(), (int)codes.size(0), (int)total_bins, (int)n_nodes,
+                           reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(codes));
+}
+
+void tree_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::Tensor& split_feat,
+                 const at::Tensor& segmap, const at::Tensor& child_of) {
+  check_codes(codes, n);
+  CHECK_DEV(node);
+  CHECK_DTYPE(node, at::kInt);
+  TORCH_CHECK(node.numel() >= n, "node too short");
+  CHECK_DEV(split_feat);
+  CHECK_DTYPE(split_feat, at::kInt);
+  CHECK_DEV(segmap);
+  CHECK_DTYPE(segmap, at::kShort);
+  CHECK_DEV(child_of);
+  CHECK_DTYPE(child_of, at::kInt);
+  const int64_t A = split_feat.numel();
+  TORCH_CHECK(segmap.dim() == 2 && segmap.size(0) == A, "segmap must be [A, max_bins]");
+  TORCH_CHECK(child_of.dim() == 2 && child_of.size(0) == A, "child_of must be [A, max_seg]");
+  auto sf = split_feat.cpu();
+  for (int64_t a = 0; a < A; ++a)
+    TORCH_CHECK(sf.data_ptr<int>()[a] < codes.size(0), "split feature out of range");
+  DevGuard g(codes.device());
+  avk::tree_assign(codes.data_ptr<uint8_t>(), codes.size(1), n, node.data_ptr<int>(),
+                   split_feat.data_ptr<int>(), segmap.data_ptr<int16_t>(), (int)segmap.size(1),
+                   child_of.data_ptr<int>(), (int)child_of.size(1), cur_stream(codes));
+}
+
+void tree_predict(const at::Tensor& codes, int64_t n, const at::Tensor& feat, const at::Tensor& seg_base,
+                  const at::Tensor& segmap, const at::Tensor& child_base, const at::Tensor& child,
+                  const at::Tensor& leaf_idx, const at::Tensor& values, const at::Tensor& tree_root,
+                  const c10::optional<at::Tensor>& tree_w, int64_t mode, at::Tensor& out) {
+  check_codes(codes, n);
+  for (const at::Tensor* t : {&feat, &seg_base, &child_base, &child, &leaf_idx, &tree_root}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kInt);
+  }
+  CHECK_DEV(segmap);
+  CHECK_DTYPE(segmap, at::kShort);
+  CHECK_DEV(values);
+  CHECK_DTYPE(values, at::kFloat);
+  CHECK_DEV(out);
+  CHECK_DTYPE(out, at::kFloat);
+  TORCH_CHECK(values.dim() == 2, "values must be [L, V]");
+  const int V = (int)values.size(1);
+  TORCH_CHECK(out.numel() >= n * V, "out too short");
+  const int K = (int)feat.numel();
+  TORCH_CHECK(seg_base.numel() == K && child_base.numel() == K && leaf_idx.numel() == K,
+              "node arrays must have equal length");
+  // host-side structural validation (the kernel trusts these indices)
+  auto fc = feat.cpu(), sc = seg_base.cpu(), cb = child_base.cpu(), lc = leaf_idx.cpu(), ch = child.cpu(),
+       tr = tree_root.cpu();
+  for (int k = 0; k < K; ++k) {
+    const int f = fc.data_ptr<int>()[k];
+    TORCH_CHECK(f < codes.size(0), "tree feature out of range");
+    TORCH_CHECK(lc.data_ptr<int>()[k] >= 0 && lc.data_ptr<int>()[k] < values.size(0), "leaf idx range");
+    if (f >= 0) {
+      TORCH_CHECK(sc.data_ptr<int>()[k] >= 0 && sc.data_ptr<int>()[k] < segmap.size(0), "seg_base range");
+      TORCH_CHECK(cb.data_ptr<int>()[k] >= 0 && cb.data_ptr<int>()[k] < ch.numel(), "child_base range");
+    }
+  }
+  for (int64_t i = 0; i < ch.numel(); ++i) TORCH_CHECK(ch.data_ptr<int>()[i] < K, "child index range");
+  for (int64_t i = 0; i < tr.numel(); ++i)
+    TORCH_CHECK(tr.data_ptr<int>()[i] >= 0 && tr.data_ptr<int>()[i] < K, "tree root range");
+  const float* tw = nullptr;
+  if (tree_w.has_value() && tree_w->defined()) {
+    CHECK_DEV((*tree_w));
+    TORCH_CHECK(tree_w->numel() == tree_root.numel(), "tree_w length");
+    tw = tree_w->data_ptr<float>();
+  }
+  DevGuard g(codes.device());
+  avk::tree_predict(codes.data_ptr<uint8_t>(), codes.size(1), n, feat.data_ptr<int>(),
+                    seg_base.data_ptr<int>(), segmap.data_ptr<int16_t>(), (int)segmap.size(1),
+                    child_base.data_ptr<int>(), child.data_ptr<int>(), leaf_idx.data_ptr<int>(),
+                    values.data_ptr<float>(), V, tree_root.data_ptr<int>(), tw, (int)tree_root.numel(),
+                    (int)mode, out.data_ptr<float>(), cur_stream(codes));
+}
+
 // ---------------------------------------------------------------------------------------------
 // host runtime
+
 // ---------------------------------------------------------------------------------------------
 // specs: list of (ordinal, kind, vocab, bucket_width, bucket_offset, max_code).  Returns one
 // CPU tensor per spec: uint8 [ld] for CAT/BUCKET (ld = n rounded up to 16, padding = 255),
@@ -295,6 +431,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bigram_histogram", &bigram_histogram);
   m.def("class_moments", &class_moments);
   m.def("nb_predict", &nb_predict);
+  m.def("node_histogram", &node_histogram);
+  m.def("node_grad_histogram", &node_grad_histogram);
+  m.def("tree_assign", &tree_assign);
+  m.def("tree_predict", &tree_predict);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

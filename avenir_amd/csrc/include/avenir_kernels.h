@@ -30,4 +30,20 @@ void nb_predict(const uint8_t* codes, long long ld, long long n, int nfeat, cons
                 const float* logprior, int C, int ref_scale, float* post, int* pred,
                 const uint8_t* labels, unsigned long long* confusion, hipStream_t stream);
 
+// ---- tree.hip (K7/K8) -----------------------------------------------------------------------
+void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
+                    const int* node, const uint8_t* weight, const int* bins, const int* offs,
+                    int nfeat, int total_bins, int n_classes, int n_nodes, unsigned long long* hist,
+                    hipStream_t stream);
+void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const int* node,
+                         const float* g, const float* h, const int* bins, const int* offs, int nfeat,
+                         int total_bins, int n_nodes, long long* out, hipStream_t stream);
+void tree_assign(const uint8_t* codes, long long ld, long long n, int* node, const int* split_feat,
+                 const short* segmap, int max_bins, const int* child_of, int max_seg,
+                 hipStream_t stream);
+void tree_predict(const uint8_t* codes, long long ld, long long n, const int* feat, const int* seg_base,
+                  const short* segmap, int max_bins, const int* child_base, const int* child,
+                  const int* leaf_idx, const float* values, int V, const int* tree_root,
+                  const float* tree_w, int n_trees, int mode, float* out, hipStream_t stream);
+
 }  // namespace avk

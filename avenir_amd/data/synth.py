@@ -103,8 +103,6 @@ CALL_HANGUP_SCHEMA = {
         {"name": "id", "ordinal": 0, "id": True, "dataType": "string"},
         {"name": "customer type", "ordinal": 1, "dataType": "categorical", "feature": True,
          "maxSplit": 2, "cardinality": ["business", "residence"]},
-        {"name": "area code", "ordinal": 2, "dataType": "categorical", "feature": False,
-         "cardinality": ["408", "650", "415", "510", "925"]},
         {"name": "issue", "ordinal": 3, "dataType": "categorical", "feature": True, "maxSplit": 2,
          "cardinality": ["internet", "cable", "billing", "other"]},
         {"name": "time of day", "ordinal": 4, "dataType": "categorical", "feature": True,

@@ -167,8 +167,17 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
 def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
              world: int = 1, device: str | torch.device = "cpu", keep_lines: bool = False,
              skip_header: bool = False, nthreads: int = 8, feature_ordinals: Sequence[int] | None = None,
-             class_ordinal: int | None = None) -> Table:
-    """Parse ``path`` into a ``Table`` (this rank's shard) with the native K1 parser."""
+             class_ordinal: int | None = None, raw_numeric: bool = False) -> Table:
+    """Parse ``path`` into a ``Table`` (this rank's shard) with the native K1 parser.
+
+    ``raw_numeric``: keep int/double features as raw float columns even when the schema gives a
+    ``bucketWidth`` (the tree builders bin them by their own split points)."""
+    if raw_numeric:
+        import copy
+        schema = copy.deepcopy(schema)
+        for f in schema.fields:
+            if f.is_numeric:
+                f.bucket_width = None
     feats = [f for f in schema.feature_fields
              if feature_ordinals is None or f.ordinal in set(feature_ordinals)]
     if feature_ordinals is not None:

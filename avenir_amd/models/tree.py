@@ -1,0 +1,970 @@
+"""Decision trees, random forests and gradient-boosted trees on the GPU.
+
+Reference behaviour (``J/tree``, ``J/model``, ``P/supv/rf.py``, ``P/supv/gbt.py``):
+
+* ``DecisionTreeBuilder`` grows a tree level by level (one Hadoop job per level).  Candidate splits
+  come from ``SplitManager``: numeric attributes split at multiples of ``splitScanInterval`` between
+  ``min`` and ``max`` into up to ``maxSplit`` segments (``SplitManager.java:256-330``), categorical
+  attributes are partitioned into 2..``maxSplit`` value groups (``:405-522``).  Each parent keeps
+  the split with the minimum population-weighted entropy / gini of its children (``best``) or a
+  random one among the top ``dtb.top.split.count`` (``randomAmongTop``)
+  (``DecisionTreeBuilder.java:499-616``); ``DecisionPathStoppingStrategy`` stops a path by
+  ``maxDepth`` / ``minInfoGain`` / ``minPopulation`` (``:57-70``); attributes per path are chosen
+  ``all`` / ``notUsedYet`` / ``randomAll`` / ``randomNotUsedYet`` (``:365-381``); sub-sampling is
+  ``withReplace`` / ``withoutReplace`` / ``none``.  The model is a JSON ``DecisionPathList``.
+* ``DecisionTreeModel`` predicts with the first matching path (``DecisionTreeModel.java:56-93``);
+  ``EnsemblePredictiveModel`` is a weighted majority vote (``EnsemblePredictiveModel.java:69-110``).
+
+MI355X design: a level = ONE histogram kernel pass (``node_hist``: class counts per frontier node x
+fine bin, where every candidate split of every attribute is a grouping of fine bins), split scoring
+for all nodes x all candidate splits as batched tensor math on the device, and ONE row-assignment
+kernel pass.  Data-parallel across ranks: the [A, C, TB] histogram is all-reduced once per level,
+so every rank takes identical decisions (shared seeded RNG) and moves its own rows.
+
+Documented divergence: the reference's multi-point numeric split emits an unbounded ``le`` for its
+last interior segment (``SplitManager.java:620-660``, the segments then overlap); here every segment
+is bounded (``attr le p2 p1`` = ``p1 < x <= p2``), which is what the predicate evaluation intends.
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import math
+import random
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Sequence
+
+import numpy as np
+import torch
+
+from ..data.table import MISSING, Table, pad16
+from ..ops import tree_ops as T
+from ..parallel.comm import Comm, get_comm
+from ..utils.schema import FeatureField, FeatureSchema
+
+ROOT = "$root"
+
+
+# ================================================================================================
+# Split space: per-attribute fine-bin encoding + candidate splits
+# ================================================================================================
+@dataclass
+class Split:
+    segmap: list[int]          # fine bin -> segment
+    n_seg: int
+    predicates: list[str]      # predicate string per segment (reference syntax)
+
+
+@dataclass
+class FeatureSplits:
+    field: FeatureField
+    kind: str                          # "cat" | "num"
+    points: list[float] = field(default_factory=list)   # numeric split points (fine-bin edges)
+    splits: list[Split] = field(default_factory=list)
+    binary: bool = False               # binary threshold splits scored by prefix sums
+
+    @property
+    def n_bins(self) -> int:
+        return len(self.field.cardinality) if self.kind == "cat" else len(self.points) + 1
+
+    def encode(self, t: Table) -> torch.Tensor:
+        """uint8 [ld] fine-bin codes of this attribute for table ``t`` (255 = missing)."""
+        f = self.field
+        if self.kind == "cat":
+            j = [x.ordinal for x in t.binned_fields].index(f.ordinal)
+            return t.codes[j]
+        # numeric: need the raw column
+        names = [x.ordinal for x in t.numeric_fields]
+        if f.ordinal in names:
+            x = t.numeric[names.index(f.ordinal)]
+            pts = torch.tensor(self.points, dtype=torch.float32, device=x.device)
+            b = torch.bucketize(x, pts, right=False)  # P[b-1] < x <= P[b]
+            b = torch.where(torch.isnan(x), torch.full_like(b, MISSING), b)
+            return b.clamp_max(MISSING).to(torch.uint8)
+        j = [x.ordinal for x in t.binned_fields].index(f.ordinal)
+        # bucketized column (bucketWidth): map bucket centre to fine bins (approximate)
+        c = t.codes[j].long()
+        lo = (c + f.bucket_offset).float() * f.bucket_width
+        pts = torch.tensor(self.points, dtype=torch.float32, device=c.device)
+        b = torch.bucketize(lo, pts, right=False)
+        return torch.where(c >= MISSING, torch.full_like(b, MISSING), b).to(torch.uint8)
+
+    def pred_value(self, v: float) -> str:
+        if self.field.is_integer or float(v).is_integer():
+            return str(int(round(v)))
+        return repr(float(v))
+
+
+def _set_partitions(values: list[str], k: int):
+    """All partitions of ``values`` into exactly ``k`` non-empty groups (restricted growth strings),
+    in a canonical order."""
+    n = len(values)
+
+    def rec(i, assign, m):
+        if i == n:
+            if m == k:
+                yield list(assign)
+            return
+        if n - i < k - m:  # not enough elements left to open the remaining groups
+            return
+        for g in range(min(m + 1, k)):
+            assign.append(g)
+            yield from rec(i + 1, assign, max(m, g + 1))
+            assign.pop()
+
+    yield from rec(0, [], 0)
+
+
+def categorical_splits(field: FeatureField, max_split: int | None = None, cap: int = 4096) -> list[Split]:
+    card = list(field.cardinality)
+    ms = max(2, max_split or field.max_split or 2)
+    out = []
+    for k in range(2, min(ms, len(card)) + 1):
+        for assign in _set_partitions(card, k):
+            groups = [[card[i] for i in range(len(card)) if assign[i] == g] for g in range(k)]
+            preds = [f"{field.ordinal} in {':'.join(gv)}" for gv in groups]
+            out.append(Split(list(assign), k, preds))
+            if len(out) >= cap:
+                return out
+    return out
+
+
+def numeric_points(field: FeatureField, values: torch.Tensor | None = None, max_bins: int = 32) -> list[float]:
+    """Split points: multiples of splitScanInterval in (min, max) (reference), else data quantiles."""
+    if field.min is not None and field.max is not None and field.split_scan_interval:
+        lo, hi, step = field.min, field.max, field.split_scan_interval
+        if int((hi - lo) / step) == 0:
+            step = (hi - lo) / 2
+        pts, p = [], lo + step
+        while p < hi - 1e-12:
+            pts.append(p)
+            p += step
+        return pts
+    if values is None:
+        raise ValueError(f"field {field.name}: no min/max/splitScanInterval and no data for quantiles")
+    v = values[~torch.isnan(values)].float()
+    if v.numel() == 0:
+        return []
+    qs = torch.linspace(0, 1, max_bins + 1, device=v.device)[1:-1]
+    if v.numel() > 1 << 24:
+        v = v[torch.randperm(v.numel(), device=v.device)[: 1 << 24]]
+    pts = torch.unique(torch.quantile(v, qs)).cpu().tolist()
+    return [float(p) for p in pts]
+
+
+def numeric_splits(fs: FeatureSplits, max_split: int | None = None, cap: int = 4096) -> list[Split]:
+    P = fs.points
+    ms = max(2, max_split or fs.field.max_split or 2)
+    out = []
+    for m in range(1, ms):
+        for combo in itertools.combinations(range(len(P)), m):
+            pts = [P[i] for i in combo]
+            # fine bin b covers (P[b-1], P[b]]: segment = #chosen points <= P[b-1]
+            segmap = []
+            for b in range(len(P) + 1):
+                segmap.append(0 if b == 0 else sum(1 for i in combo if i <= b - 1))
+            o = fs.field.ordinal
+            pv = [fs.pred_value(p) for p in pts]
+            preds = [f"{o} le {pv[0]}"]
+            for i in range(1, len(pv)):
+                preds.append(f"{o} le {pv[i]} {pv[i - 1]}")
+            preds.append(f"{o} gt {pv[-1]}")
+            out.append(Split(segmap, m + 1, preds))
+            if len(out) >= cap:
+                return out
+    return out
+
+
+def build_split_space(schema: FeatureSchema, t: Table | None = None, attrs: Sequence[int] | None = None,
+                      binary: bool = False, max_bins: int = 32) -> list[FeatureSplits]:
+    """Candidate-split space over the feature attributes (reference SplitManager semantics, or
+    binary threshold splits over ordered fine bins when ``binary``)."""
+    out = []
+    for f in schema.feature_fields:
+        if attrs is not None and f.ordinal not in attrs:
+            continue
+        if f.is_categorical:
+            fs = FeatureSplits(f, "cat", binary=binary)
+            if not binary:
+                fs.splits = categorical_splits(f)
+        elif f.is_numeric:
+            vals = None
+            if t is not None:
+                names = [x.ordinal for x in t.numeric_fields]
+                if f.ordinal in names:
+                    vals = t.numeric[names.index(f.ordinal), : t.n]
+            if binary or not (f.min is not None and f.max is not None and f.split_scan_interval):
+                pts = numeric_points(FeatureField(f.name, f.ordinal, f.data_type), vals, max_bins)
+            else:
+                pts = numeric_points(f, vals, max_bins)
+            fs = FeatureSplits(f, "num", points=pts, binary=binary)
+            if not binary:
+                fs.splits = numeric_splits(fs)
+        else:
+            continue
+        if fs.n_bins > 254:
+            raise ValueError(f"attribute {f.name}: {fs.n_bins} fine bins > 254")
+        out.append(fs)
+    return out
+
+
+def _with_total_row(codes: torch.Tensor, n: int) -> torch.Tensor:
+    tot = torch.full((1, codes.shape[1]), MISSING, dtype=torch.uint8, device=codes.device)
+    tot[0, :n] = 0
+    return torch.cat([codes, tot], 0)
+
+
+def encode_for_tree(space: list[FeatureSplits], t: Table) -> torch.Tensor:
+    ld = t.ld
+    codes = torch.full((len(space), ld), MISSING, dtype=torch.uint8, device=t.device)
+    for i, fs in enumerate(space):
+        c = fs.encode(t)
+        codes[i, : c.shape[0]] = c[:ld]
+    codes[:, t.n:] = MISSING
+    return codes
+
+
+# ================================================================================================
+# impurity
+# ================================================================================================
+def impurity(counts: torch.Tensor, algorithm: str) -> torch.Tensor:
+    """Entropy (base 2) or gini over the last dim of class counts (InfoContentStat.processStat)."""
+    tot = counts.sum(-1, keepdim=True).double()
+    p = counts.double() / tot.clamp_min(1)
+    if algorithm == "entropy":
+        return -(torch.where(p > 0, p * torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))).sum(-1)
+    if algorithm in ("giniIndex", "gini"):
+        return 1.0 - (p * p).sum(-1)
+    raise ValueError(f"unsupported split algorithm {algorithm}")
+
+
+# ================================================================================================
+# tree structure
+# ================================================================================================
+@dataclass
+class Node:
+    predicates: list[str]
+    population: int
+    info: float
+    class_pr: list[float]
+    depth: int
+    stopped: bool = False
+    feature: int = -1            # index into the split space (internal nodes)
+    split: int = -1              # index of the chosen split
+    segmap: list[int] | None = None
+    children: list[int] = field(default_factory=list)   # per segment: node index or -1
+    used_attrs: frozenset = frozenset()
+
+    @property
+    def is_leaf(self) -> bool:
+        return self.feature < 0
+
+
+class DecisionTree:
+    """A built tree: node list (index 0 = root) + its split space and class values."""
+
+    def __init__(self, nodes: list[Node], space: list[FeatureSplits], class_values: list[str]):
+        self.nodes = nodes
+        self.space = space
+        self.class_values = class_values
+
+    # -- reference JSON (DecisionPathList) ---------------------------------------------------------
+    def to_decision_paths(self, total_population: int | None = None) -> dict:
+        paths = []
+        for nd in self.nodes:
+            if not nd.is_leaf:
+                continue
+            preds = [{"attribute": 0, "predicateStr": ROOT, "operator": None, "valueInt": 0,
+                      "valueDbl": 0.0, "categoricalValues": None, "otherBoundInt": None,
+                      "otherBoundDbl": None}]
+            for ps in nd.predicates:
+                preds.append(_predicate_obj(ps, self._field_of(ps)))
+            cp = {cv: p for cv, p in zip(self.class_values, nd.class_pr)}
+            maj = max(cp.values()) if cp else 0.0
+            mino = 1.0 - maj
+            conf = min(maj / mino, 100.0) if mino > 0 else 100.0
+            d = {"stopped": nd.stopped or True, "classValPr": cp, "infoContent": nd.info,
+                 "predicates": preds, "population": nd.population,
+                 "outputClassVal": max(cp, key=cp.get) if cp else "", "confidence": conf}
+            if total_population:
+                d["support"] = nd.population / total_population
+            paths.append(d)
+        return {"decisionPaths": paths}
+
+    def _field_of(self, ps: str) -> FeatureField:
+        o = int(ps.split()[0])
+        for fs in self.space:
+            if fs.field.ordinal == o:
+                return fs.field
+        raise KeyError(o)
+
+    def save_json(self, path: str | Path, total_population: int | None = None) -> None:
+        Path(path).write_text(json.dumps(self.to_decision_paths(total_population), indent=1))
+
+    # -- native compact format ---------------------------------------------------------------------
+    def state(self) -> dict:
+        return {
+            "class_values": self.class_values,
+            "space": [{"ordinal": fs.field.ordinal, "kind": fs.kind, "points": fs.points,
+                       "binary": fs.binary} for fs in self.space],
+            "nodes": [{"predicates": n.predicates, "population": n.population, "info": n.info,
+                       "class_pr": n.class_pr, "depth": n.depth, "stopped": n.stopped,
+                       "feature": n.feature, "split": n.split, "segmap": n.segmap,
+                       "children": n.children} for n in self.nodes],
+        }
+
+    @classmethod
+    def from_state(cls, st: dict, schema: FeatureSchema) -> "DecisionTree":
+        space = [FeatureSplits(schema.find_field_by_ordinal(s["ordinal"]), s["kind"], list(s["points"]),
+                               binary=s.get("binary", False)) for s in st["space"]]
+        nodes = [Node(n["predicates"], n["population"], n["info"], n["class_pr"], n["depth"], n["stopped"],
+                      n["feature"], n["split"], n["segmap"], n["children"]) for n in st["nodes"]]
+        return cls(nodes, space, st["class_values"])
+
+    # -- rules ---------------------------------------------------------------------------------
+    def rules(self) -> list[tuple[str, str, float]]:
+        """(predicate conjunction, class, probability) per leaf."""
+        out = []
+        for nd in self.nodes:
+            if nd.is_leaf:
+                k = int(np.argmax(nd.class_pr)) if nd.class_pr else 0
+                out.append((" and ".join([ROOT] + nd.predicates), self.class_values[k], nd.class_pr[k]))
+        return out
+
+
+def _predicate_obj(ps: str, f: FeatureField) -> dict:
+    it = ps.split()
+    d = {"attribute": int(it[0]), "predicateStr": ps, "operator": it[1], "valueInt": 0, "valueDbl": 0.0,
+         "categoricalValues": None, "otherBoundInt": None, "otherBoundDbl": None}
+    if it[1] == "in":
+        d["categoricalValues"] = it[2].split(":")
+    elif f.is_integer:
+        d["valueInt"] = int(float(it[2]))
+        if len(it) > 3:
+            d["otherBoundInt"] = int(float(it[3]))
+    else:
+        d["valueDbl"] = float(it[2])
+        if len(it) > 3:
+            d["otherBoundDbl"] = float(it[3])
+    return d
+
+
+# ================================================================================================
+# builder
+# ================================================================================================
+@dataclass
+class TreeParams:
+    algorithm: str = "giniIndex"                  # entropy | giniIndex
+    stopping: str = "maxDepth"                    # maxDepth | minInfoGain | minPopulation
+    max_depth: int = 3
+    min_info_gain: float = 0.0
+    min_population: int = 1
+    attr_selection: str = "notUsedYet"            # all | notUsedYet | randomAll | randomNotUsedYet
+    random_attr_count: int = 3
+    split_selection: str = "best"                 # best | randomAmongTop
+    top_split_count: int = 3
+    sub_sampling: str = "none"                    # none | withReplace | withoutReplace
+    sampling_rate: float = 100.0                  # percent, withoutReplace
+    seed: int = 0
+    binary: bool = False                          # binary threshold splits (RF / sklearn style)
+    max_bins: int = 32
+
+    @classmethod
+    def from_config(cls, cfg) -> "TreeParams":
+        """From a ``dtb.``-prefixed JobConfig (reference keys, R/detr.properties)."""
+        p = cls()
+        p.algorithm = cfg.get_str("split.algorithm", p.algorithm)
+        p.stopping = cfg.get_str("path.stopping.strategy", "minInfoGain")
+        if p.stopping == "maxDepth":
+            p.max_depth = cfg.get_int("max.depth.limit")
+        elif p.stopping == "minInfoGain":
+            p.min_info_gain = cfg.get_float("min.info.gain.limit")
+        elif p.stopping == "minPopulation":
+            p.min_population = cfg.get_int("min.population.limit")
+        p.attr_selection = cfg.get_str("split.attribute.selection.strategy", p.attr_selection)
+        p.random_attr_count = cfg.get_int("random.split.set.size", p.random_attr_count)
+        p.split_selection = cfg.get_str("split.select.strategy", p.split_selection)
+        p.top_split_count = cfg.get_int("top.split.count", p.top_split_count)
+        p.sub_sampling = cfg.get_str("sub.sampling.strategy", p.sub_sampling)
+        p.sampling_rate = cfg.get_float("sub.sampling.rate", p.sampling_rate)
+        p.seed = cfg.get_int("random.seed", p.seed)
+        return p
+
+
+class DecisionTreeBuilder:
+    """Level-wise GPU tree builder (data parallel over ranks)."""
+
+    def __init__(self, schema: FeatureSchema, params: TreeParams | None = None, comm: Comm | None = None,
+                 space: list[FeatureSplits] | None = None):
+        self.schema = schema
+        self.p = params or TreeParams()
+        self.comm = comm
+        self.space = space
+        self.level_times: list[float] = []
+
+    # -- helpers -------------------------------------------------------------------------------
+    def _weights(self, t: Table, rng_seed: int) -> torch.Tensor | None:
+        p = self.p
+        if p.sub_sampling == "none":
+            return None
+        comm = self.comm or get_comm()
+        g = torch.Generator(device=t.device)
+        g.manual_seed(rng_seed * 1000003 + comm.rank)
+        if p.sub_sampling == "withReplace":
+            w = torch.poisson(torch.ones(t.ld, device=t.device), generator=g).clamp_max(255)
+        elif p.sub_sampling == "withoutReplace":
+            w = (torch.rand(t.ld, generator=g, device=t.device) * 100.0 < p.sampling_rate).float()
+        else:
+            raise ValueError(f"unknown sub sampling strategy {p.sub_sampling}")
+        w[t.n:] = 0
+        return w.to(torch.uint8)
+
+    def _candidate_attrs(self, nd: Node, F: int, rng: random.Random) -> list[int]:
+        s = self.p.attr_selection
+        allf = list(range(F))
+        if s == "all":
+            return allf
+        remaining = [f for f in allf if f not in nd.used_attrs] or allf
+        if s == "notUsedYet":
+            return remaining
+        if s == "randomAll":
+            return sorted(rng.sample(allf, min(self.p.random_attr_count, F)))
+        if s == "randomNotUsedYet":
+            return sorted(rng.sample(remaining, min(self.p.random_attr_count, len(remaining))))
+        raise ValueError(f"unknown attribute selection strategy {s}")
+
+    def _should_stop(self, pop: int, info: float, parent_info: float, depth: int) -> bool:
+        p = self.p
+        if p.stopping == "maxDepth":
+            return depth >= p.max_depth
+        if p.stopping == "minInfoGain":
+            return (parent_info - info) < p.min_info_gain
+        if p.stopping == "minPopulation":
+            return pop < p.min_population
+        raise ValueError(f"invalid stopping strategy {p.stopping}")
+
+    # -- build ---------------------------------------------------------------------------------
+    def fit(self, t: Table, tree_seed: int | None = None, codes: torch.Tensor | None = None) -> DecisionTree:
+        import time
+        comm = self.comm or get_comm()
+        p = self.p
+        seed = p.seed if tree_seed is None else tree_seed
+        rng = random.Random(seed)  # identical on every rank
+        if self.space is None:
+            self.space = build_split_space(self.schema, t, binary=p.binary, max_bins=p.max_bins)
+        space = self.space
+        if codes is None:
+            codes = encode_for_tree(space, t)
+        # one constant extra row (code 0 for every real row): its single bin is the node total
+        codes = _with_total_row(codes, t.n)
+        F = len(space)
+        bins = [fs.n_bins for fs in space] + [1]
+        offs = list(itertools.accumulate([0] + bins[:-1]))
+        C = t.n_classes
+        dev = t.device
+        labels = t.labels
+        weight = self._weights(t, seed)
+
+        # segment-assignment tensors per feature (explicit splits)
+        seg_tensors = []
+        for fs in space:
+            if fs.binary:
+                seg_tensors.append(None)
+                continue
+            S = len(fs.splits)
+            G = max((s.n_seg for s in fs.splits), default=1)
+            M = torch.zeros((S, G, fs.n_bins), dtype=torch.float64)
+            for si, sp in enumerate(fs.splits):
+                for b, g in enumerate(sp.segmap):
+                    M[si, g, b] = 1.0
+            seg_tensors.append(M.to(dev))
+
+        node = torch.full((t.ld,), -1, dtype=torch.int32, device=dev)
+        node[: t.n] = 0
+        # root
+        root_hist = T.node_histogram(codes, t.n, labels, node, weight, bins, C, 1)
+        if comm.is_distributed:
+            comm.all_reduce(root_hist)
+        rc = root_hist[0, :, offs[F]]
+        pop = int(rc.sum())
+        root = Node([], pop, float(impurity(rc.unsqueeze(0), p.algorithm)[0]),
+                    (rc.double() / max(pop, 1)).tolist(), depth=1)
+        nodes = [root]
+        frontier = [0]  # global node indices of the active frontier (local index = position)
+        while frontier:
+            t0 = time.perf_counter()
+            A = len(frontier)
+            hist = T.node_histogram(codes, t.n, labels, node, weight, bins, C, A)  # [A, C, TB]
+            if comm.is_distributed:
+                comm.all_reduce(hist)
+            hist_t = hist.transpose(1, 2).double()  # [A, TB, C]
+            # ---- score every candidate split of every attribute, all nodes at once ----
+            cand_masks = torch.zeros((A, F), dtype=torch.bool)
+            for a, gi in enumerate(frontier):
+                for f in self._candidate_attrs(nodes[gi], F, rng):
+                    cand_masks[a, f] = True
+            cand_masks = cand_masks.to(dev)
+            score_blocks, index = [], []  # index: (feature, split id)
+            for f, fs in enumerate(space):
+                hb = hist_t[:, offs[f]: offs[f] + bins[f], :]     # [A, B, C]
+                if fs.binary:
+                    left = torch.cumsum(hb, 1)[:, :-1, :]          # [A, B-1, C]
+                    tot = hb.sum(1, keepdim=True)
+                    right = tot - left
+                    seg = torch.stack([left, right], 2)            # [A, S, 2, C]
+                    ns = seg.shape[1]
+                else:
+                    M = seg_tensors[f]
+                    if M.shape[0] == 0:
+                        continue
+                    seg = torch.einsum("sgb,abc->asgc", M, hb)      # [A, S, G, C]
+                    ns = M.shape[0]
+                cnt = seg.sum(-1)                                   # [A, S, G]
+                stat = impurity(seg, p.algorithm)                   # [A, S, G]
+                wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)   # [A, S]
+                nonempty = (cnt > 0).sum(-1) >= 2                   # a split must separate rows
+                wavg = torch.where(nonempty & cand_masks[:, f:f + 1], wavg,
+                                   torch.full_like(wavg, math.inf))
+                score_blocks.append(wavg)
+                index.extend((f, s) for s in range(ns))
+            if not score_blocks:
+                break
+            scores = torch.cat(score_blocks, 1)                     # [A, S_total]
+            if p.split_selection == "randomAmongTop":
+                k = min(p.top_split_count, scores.shape[1])
+                top = torch.topk(scores, k, dim=1, largest=False).indices.cpu()
+                topv = torch.gather(scores, 1, top.to(dev)).cpu()
+                choice = []
+                for a in range(A):
+                    fin = [i for i in range(k) if math.isfinite(float(topv[a, i]))]
+                    choice.append(int(top[a, rng.choice(fin)]) if fin else -1)
+                best = torch.tensor(choice)
+                best_val = torch.tensor([float(scores[a, c]) if c >= 0 else math.inf
+                                         for a, c in enumerate(choice)])
+            else:
+                best_val, best = scores.min(1)
+                best, best_val = best.cpu(), best_val.cpu()
+            # segment counts of the chosen splits, one gather per node
+            seg_counts = []
+            for a in range(A):
+                if not math.isfinite(float(best_val[a])):
+                    seg_counts.append(None)
+                    continue
+                f, s = index[int(best[a])]
+                hb = hist_t[a, offs[f]: offs[f] + bins[f], :]
+                if space[f].binary:
+                    left = hb[: s + 1].sum(0)
+                    seg_counts.append(torch.stack([left, hb.sum(0) - left]))
+                else:
+                    seg_counts.append(torch.einsum("gb,bc->gc", seg_tensors[f][s], hb))
+            seg_counts = [None if x is None else x.round().long().cpu() for x in seg_counts]
+            # ---- create children ----
+            new_frontier: list[int] = []
+            max_bins = max(bins)
+            max_seg = 2
+            for a in range(A):
+                if seg_counts[a] is not None:
+                    max_seg = max(max_seg, seg_counts[a].shape[0])
+            split_feat = torch.full((A,), -1, dtype=torch.int32)
+            segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
+            child_of = torch.full((A, max_seg), -1, dtype=torch.int32)
+            for a, gi in enumerate(frontier):
+                nd = nodes[gi]
+                sc = seg_counts[a]
+                if sc is None:
+                    nd.stopped = True
+                    continue
+                f, s = index[int(best[a])]
+                fs = space[f]
+                if fs.binary:
+                    sm = [0 if b <= s else 1 for b in range(fs.n_bins)]
+                    pv = fs.points[s] if fs.kind == "num" else s
+                    o = fs.field.ordinal
+                    if fs.kind == "num":
+                        preds = [f"{o} le {fs.pred_value(pv)}", f"{o} gt {fs.pred_value(pv)}"]
+                    else:
+                        card = fs.field.cardinality
+                        preds = [f"{o} in {':'.join(card[: s + 1])}", f"{o} in {':'.join(card[s + 1:])}"]
+                else:
+                    sp = fs.splits[s]
+                    sm, preds = sp.segmap, sp.predicates
+                nd.feature, nd.split, nd.segmap = f, s, list(sm)
+                nd.children = []
+                split_feat[a] = f
+                segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
+                for g in range(sc.shape[0]):
+                    cnt = sc[g]
+                    pop = int(cnt.sum())
+                    if pop == 0:
+                        nd.children.append(-1)
+                        continue
+                    info = float(impurity(cnt.unsqueeze(0), p.algorithm)[0])
+                    depth = nd.depth + 1
+                    stop = self._should_stop(pop, info, nd.info, depth) or info == 0.0
+                    child = Node(nd.predicates + [preds[g]], pop, info, (cnt.double() / pop).tolist(),
+                                 depth, stopped=stop, used_attrs=nd.used_attrs | {f})
+                    ci = len(nodes)
+                    nodes.append(child)
+                    nd.children.append(ci)
+                    if not stop:
+                        child_of[a, g] = len(new_frontier)
+                        new_frontier.append(ci)
+            T.tree_assign(codes, t.n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
+            frontier = new_frontier
+            self.level_times.append(time.perf_counter() - t0)
+        cls = t.class_field.cardinality if t.class_field else ["_"]
+        return DecisionTree(nodes, space, list(cls))
+
+
+# ================================================================================================
+# inference (ModelPredictor / DecisionTreeModel / EnsemblePredictiveModel)
+# ================================================================================================
+def flatten_forest(trees: Sequence[DecisionTree], device, weights: Sequence[float] | None = None,
+                   value_fn=None) -> dict:
+    """Concatenate trees into the flat int32/int16/float32 arrays of ``tree_predict``.  All trees
+    must share one split space (same encoded code rows)."""
+    feat, seg_base, child_base, leaf_idx, child, segrows, values, roots = [], [], [], [], [], [], [], []
+    max_bins = max((fs.n_bins for fs in trees[0].space), default=1)
+    for tr in trees:
+        base = len(feat)
+        roots.append(base)
+        for nd in tr.nodes:
+            if nd.is_leaf or not nd.children:
+                feat.append(-1)
+                seg_base.append(0)
+                child_base.append(0)
+            else:
+                feat.append(nd.feature)
+                seg_base.append(len(segrows))
+                row = [-1] * max_bins
+                for b, g in enumerate(nd.segmap):
+                    row[b] = g
+                segrows.append(row)
+                child_base.append(len(child))
+                child.extend([c + base if c >= 0 else -1 for c in nd.children])
+            leaf_idx.append(len(values))
+            values.append(value_fn(nd) if value_fn else nd.class_pr)
+    if not segrows:
+        segrows = [[-1] * max_bins]
+    if not child:
+        child = [-1]
+    dev = torch.device(device)
+    out = {
+        "feat": torch.tensor(feat, dtype=torch.int32, device=dev),
+        "seg_base": torch.tensor(seg_base, dtype=torch.int32, device=dev),
+        "segmap": torch.tensor(segrows, dtype=torch.int16, device=dev),
+        "child_base": torch.tensor(child_base, dtype=torch.int32, device=dev),
+        "child": torch.tensor(child, dtype=torch.int32, device=dev),
+        "leaf_idx": torch.tensor(leaf_idx, dtype=torch.int32, device=dev),
+        "values": torch.tensor(values, dtype=torch.float32, device=dev),
+        "tree_root": torch.tensor(roots, dtype=torch.int32, device=dev),
+    }
+    if weights is not None:
+        out["tree_w"] = torch.tensor(list(weights), dtype=torch.float32, device=dev)
+    return out
+
+
+class TreeEnsemble:
+    """Prediction over one or more trees (DecisionTreeModel; EnsemblePredictiveModel when more than
+    one tree: weighted majority vote, optional minimum odds ratio -> ambiguous)."""
+
+    def __init__(self, trees: Sequence[DecisionTree], weights: Sequence[float] | None = None):
+        self.trees = list(trees)
+        self.weights = list(weights) if weights is not None else None
+        self._flat: dict | None = None
+
+    @property
+    def class_values(self) -> list[str]:
+        return self.trees[0].class_values
+
+    def encode(self, t: Table) -> torch.Tensor:
+        return encode_for_tree(self.trees[0].space, t)
+
+    def flat(self, device) -> dict:
+        if self._flat is None or self._flat["feat"].device != torch.device(device):
+            self._flat = flatten_forest(self.trees, device, self.weights)
+        return self._flat
+
+    def predict_proba(self, t: Table, codes: torch.Tensor | None = None) -> torch.Tensor:
+        codes = self.encode(t) if codes is None else codes
+        out = T.tree_predict(codes, t.n, self.flat(t.device), mode=0)
+        tw = sum(self.weights) if self.weights else len(self.trees)
+        return out / tw
+
+    def predict_votes(self, t: Table, codes: torch.Tensor | None = None) -> torch.Tensor:
+        codes = self.encode(t) if codes is None else codes
+        return T.tree_predict(codes, t.n, self.flat(t.device), mode=1)
+
+    def predict(self, t: Table, min_odds_ratio: float | None = None) -> torch.Tensor:
+        """Class index per row; with an ensemble, majority vote (-1 = ambiguous when the top/second
+        vote ratio is below ``min_odds_ratio``)."""
+        if len(self.trees) == 1:
+            return self.predict_proba(t).argmax(1)
+        votes = self.predict_votes(t)
+        top2 = torch.topk(votes, min(2, votes.shape[1]), dim=1)
+        pred = top2.indices[:, 0]
+        if min_odds_ratio is not None and votes.shape[1] > 1:
+            ratio = top2.values[:, 0] / top2.values[:, 1].clamp_min(1e-9)
+            pred = torch.where(ratio < min_odds_ratio, torch.full_like(pred, -1), pred)
+        return pred
+
+
+# ================================================================================================
+# random forest (P/supv/rf.py parity: sklearn-style RF, and R/rafo.sh reference RF)
+# ================================================================================================
+class RandomForest:
+    def __init__(self, schema: FeatureSchema, n_trees: int = 10, params: TreeParams | None = None,
+                 max_features: str | int = "sqrt", comm: Comm | None = None, tree_parallel: bool = False):
+        self.schema = schema
+        self.n_trees = n_trees
+        base = params or TreeParams(binary=True, stopping="maxDepth", max_depth=8,
+                                    sub_sampling="withReplace", attr_selection="randomAll")
+        self.params = base
+        self.max_features = max_features
+        self.comm = comm
+        self.tree_parallel = tree_parallel
+        self.trees: list[DecisionTree] = []
+
+    def _k(self, F: int) -> int:
+        mf = self.max_features
+        if isinstance(mf, int):
+            return max(1, min(F, mf))
+        if mf == "sqrt":
+            return max(1, int(math.sqrt(F)))
+        if mf == "log2":
+            return max(1, int(math.log2(F)))
+        if mf in ("all", None, "auto"):
+            return F
+        return max(1, int(float(mf) * F))
+
+    def fit(self, t: Table) -> "RandomForest":
+        comm = self.comm or get_comm()
+        space = build_split_space(self.schema, t, binary=self.params.binary, max_bins=self.params.max_bins)
+        codes = encode_for_tree(space, t)
+        import copy
+        my_trees = range(self.n_trees)
+        if self.tree_parallel and comm.is_distributed:
+            my_trees = range(comm.rank, self.n_trees, comm.world)
+        trees = []
+        for i in my_trees:
+            p = copy.copy(self.params)
+            p.random_attr_count = self._k(len(space))
+            p.seed = self.params.seed * 7919 + i
+            b = DecisionTreeBuilder(self.schema, p, comm=_LocalComm() if self.tree_parallel else comm,
+                                    space=space)
+            trees.append(b.fit(t, tree_seed=p.seed, codes=codes))
+        if self.tree_parallel and comm.is_distributed:
+            states = comm.all_gather_object([tr.state() for tr in trees])
+            allt = {}
+            for r, sts in enumerate(states):
+                for j, st in enumerate(sts):
+                    allt[r + j * comm.world] = DecisionTree.from_state(st, self.schema)
+            trees = [allt[i] for i in sorted(allt)]
+        self.trees = trees
+        return self
+
+    def ensemble(self) -> TreeEnsemble:
+        return TreeEnsemble(self.trees)
+
+    def predict_proba(self, t: Table) -> torch.Tensor:
+        return self.ensemble().predict_proba(t)
+
+    def predict(self, t: Table) -> torch.Tensor:
+        return self.predict_proba(t).argmax(1)
+
+
+class _LocalComm:
+    """Single-rank stand-in used for tree-parallel forests (each rank grows whole trees)."""
+    is_distributed = False
+    world = 1
+    rank = 0
+
+
+# ================================================================================================
+# gradient boosted trees (P/supv/gbt.py parity: sklearn GradientBoostingClassifier, deviance loss)
+# ================================================================================================
+@dataclass
+class GBTParams:
+    n_estimators: int = 120
+    learning_rate: float = 0.12
+    max_depth: int = 3
+    min_samples_leaf: int = 1
+    subsample: float = 1.0
+    l2: float = 0.0
+    max_bins: int = 64
+    seed: int = 0
+
+
+@dataclass
+class _RegNode:
+    value: float
+    feature: int = -1
+    threshold_bin: int = -1
+    children: list[int] = field(default_factory=list)
+    depth: int = 0
+
+
+class GradientBoostedTrees:
+    """Histogram GBT: per stage one regression tree per class on (g, h) with Newton leaves.
+    Every level = one ``node_grad_hist`` pass (exact fixed-point sums) + one ``tree_assign`` pass."""
+
+    def __init__(self, schema: FeatureSchema, params: GBTParams | None = None, comm: Comm | None = None):
+        self.schema = schema
+        self.p = params or GBTParams()
+        self.comm = comm
+        self.space: list[FeatureSplits] | None = None
+        self.stages: list[list[DecisionTree]] = []
+        self.init: torch.Tensor | None = None
+        self.n_classes = 2
+        self.train_loss: list[float] = []
+
+    def _tree(self, codes, n, g, h, bins, dev) -> DecisionTree:
+        comm = self.comm or get_comm()
+        p = self.p
+        offs = list(itertools.accumulate([0] + bins[:-1]))
+        node = torch.full((codes.shape[1],), -1, dtype=torch.int32, device=dev)
+        node[:n] = 0
+        nodes = [Node([], n, 0.0, [0.0], depth=0)]
+        values = [0.0]
+        frontier = [0]
+        G_root = None
+        for depth in range(p.max_depth + 1):
+            A = len(frontier)
+            hist = T.node_grad_histogram(codes, n, node, g, h, bins, A)   # [A, TB, 2] f64
+            if comm.is_distributed:
+                comm.all_reduce(hist)
+            tot = hist[:, offs[-1], :]            # the constant total row's single bin
+            G, H = tot[:, 0], tot[:, 1]
+            if G_root is None:
+                G_root = G
+            leaf_val = (-G / (H + p.l2).clamp_min(1e-12)).cpu().tolist()
+            for a, gi in enumerate(frontier):
+                values[gi] = leaf_val[a]
+            if depth == p.max_depth:
+                break
+            best_gain = torch.full((A,), -math.inf, dtype=torch.float64, device=dev)
+            best_f = torch.full((A,), -1, dtype=torch.long, device=dev)
+            best_b = torch.full((A,), -1, dtype=torch.long, device=dev)
+            parent = (G * G / (H + p.l2).clamp_min(1e-12))
+            for f, b in enumerate(bins[:-1]):
+                hb = hist[:, offs[f]: offs[f] + b, :]
+                left = torch.cumsum(hb, 1)[:, :-1, :]
+                ft = hb.sum(1, keepdim=True)
+                right = ft - left
+                gl, hl, gr, hr = left[..., 0], left[..., 1], right[..., 0], right[..., 1]
+                gain = gl * gl / (hl + p.l2).clamp_min(1e-12) + gr * gr / (hr + p.l2).clamp_min(1e-12) \
+                    - parent.unsqueeze(1)
+                ok = (hl > 1e-12) & (hr > 1e-12)
+                gain = torch.where(ok, gain, torch.full_like(gain, -math.inf))
+                if gain.shape[1] == 0:
+                    continue
+                gv, gb = gain.max(1)
+                upd = gv > best_gain
+                best_gain = torch.where(upd, gv, best_gain)
+                best_f = torch.where(upd, torch.full_like(best_f, f), best_f)
+                best_b = torch.where(upd, gb, best_b)
+            bg, bf, bb = best_gain.cpu().tolist(), best_f.cpu().tolist(), best_b.cpu().tolist()
+            max_bins = max(bins)
+            split_feat = torch.full((A,), -1, dtype=torch.int32)
+            segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
+            child_of = torch.full((A, 2), -1, dtype=torch.int32)
+            new_frontier = []
+            for a, gi in enumerate(frontier):
+                if bf[a] < 0 or not math.isfinite(bg[a]) or bg[a] <= 1e-12:
+                    continue
+                f, thr = bf[a], bb[a]
+                sm = [0 if x <= thr else 1 for x in range(bins[f])]
+                nd = nodes[gi]
+                nd.feature, nd.split, nd.segmap = f, thr, sm
+                split_feat[a] = f
+                segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
+                nd.children = []
+                for s in range(2):
+                    ci = len(nodes)
+                    nodes.append(Node([], 0, 0.0, [0.0], depth=nd.depth + 1))
+                    values.append(0.0)
+                    nd.children.append(ci)
+                    child_of[a, s] = len(new_frontier)
+                    new_frontier.append(ci)
+            if not new_frontier:
+                break
+            T.tree_assign(codes, n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
+            frontier = new_frontier
+        for i, nd in enumerate(nodes):
+            nd.class_pr = [values[i]]
+        return DecisionTree(nodes, self.space, ["value"])
+
+    def fit(self, t: Table) -> "GradientBoostedTrees":
+        comm = self.comm or get_comm()
+        p = self.p
+        self.space = build_split_space(self.schema, t, binary=True, max_bins=p.max_bins)
+        codes = encode_for_tree(self.space, t)
+        codes = _with_total_row(codes, t.n)
+        bins = [fs.n_bins for fs in self.space] + [1]
+        n, dev = t.n, t.device
+        C = t.n_classes
+        self.n_classes = C
+        y = t.labels[:n].long().clamp_max(C - 1)
+        K = 1 if C == 2 else C
+        cnt = torch.bincount(y, minlength=C).double()
+        if comm.is_distributed:
+            comm.all_reduce(cnt)
+        prior = (cnt / cnt.sum()).clamp(1e-12, 1 - 1e-12)
+        if K == 1:
+            self.init = torch.log(prior[1] / prior[0]).view(1).float()
+        else:
+            self.init = torch.log(prior).float()
+        F = self.init.to(dev).view(1, K).expand(n, K).clone()
+        Y = torch.nn.functional.one_hot(y, C).float() if K > 1 else y.float().view(n, 1)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(p.seed + 17 * comm.rank)
+        for _ in range(p.n_estimators):
+            if K == 1:
+                pr = torch.sigmoid(F)
+            else:
+                pr = torch.softmax(F, 1)
+            grad = pr - Y
+            hess = (pr * (1 - pr)).clamp_min(1e-6)
+            if p.subsample < 1.0:
+                m = (torch.rand(n, generator=gen, device=dev) < p.subsample).float().view(n, 1)
+                grad, hess = grad * m, hess * m
+            stage = []
+            for k in range(K):
+                g = torch.zeros(codes.shape[1], device=dev)
+                h = torch.zeros(codes.shape[1], device=dev)
+                g[:n], h[:n] = grad[:, k], hess[:, k]
+                tr = self._tree(codes, n, g, h, bins, dev)
+                flat = flatten_forest([tr], dev, value_fn=lambda nd: nd.class_pr)
+                F[:, k] += p.learning_rate * T.tree_predict(codes, n, flat, mode=0)[:, 0]
+                stage.append(tr)
+            self.stages.append(stage)
+            if K == 1:
+                loss = torch.nn.functional.binary_cross_entropy_with_logits(F[:, 0], Y[:, 0])
+            else:
+                loss = torch.nn.functional.cross_entropy(F, y)
+            self.train_loss.append(float(loss))
+        self._flat = None
+        return self
+
+    def decision_function(self, t: Table) -> torch.Tensor:
+        codes = encode_for_tree(self.space, t)
+        K = 1 if self.n_classes == 2 else self.n_classes
+        F = self.init.to(t.device).view(1, K).expand(t.n, K).clone()
+        for k in range(K):
+            trees = [st[k] for st in self.stages]
+            if not trees:
+                continue
+            flat = flatten_forest(trees, t.device, value_fn=lambda nd: nd.class_pr)
+            F[:, k] += self.p.learning_rate * T.tree_predict(codes, t.n, flat, mode=0)[:, 0]
+        return F
+
+    def predict_proba(self, t: Table) -> torch.Tensor:
+        F = self.decision_function(t)
+        if F.shape[1] == 1:
+            p1 = torch.sigmoid(F[:, 0])
+            return torch.stack([1 - p1, p1], 1)
+        return torch.softmax(F, 1)
+
+    def predict(self, t: Table) -> torch.Tensor:
+        return self.predict_proba(t).argmax(1)
