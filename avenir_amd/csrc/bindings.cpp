@@ -357,6 +357,47 @@ void tree_predict(const at::Tensor& codes, int64_t n, const at::Tensor& feat, co
 }
 
 // ---------------------------------------------------------------------------------------------
+// distance / kNN / clustering (K9/K11)
+// ---------------------------------------------------------------------------------------------
+py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t q_base, int64_t r_base,
+                   bool exclude_self, int64_t splits) {
+  CHECK_DEV(Q);
+  CHECK_DTYPE(Q, at::kFloat);
+  CHECK_DEV(R);
+  CHECK_DTYPE(R, at::kFloat);
+  TORCH_CHECK(Q.dim() == 2 && R.dim() == 2 && Q.size(1) == R.size(1), "Q [M,D], R [N,D] required");
+  TORCH_CHECK(k >= 1 && k <= 32, "k must be in [1,32]");
+  const int64_t M = Q.size(0), N = R.size(0), D = Q.size(1);
+  TORCH_CHECK(D >= 1, "D must be >= 1");
+  if (splits <= 0) {
+    const int64_t qb = (M + 63) / 64;
+    splits = std::max<int64_t>(1, std::min<int64_t>((N + 63) / 64, (2048 + qb - 1) / qb));
+  }
+  auto od = at::empty({M, k}, Q.options());
+  auto oi = at::empty({M, k}, Q.options().dtype(at::kLong));
+  DevGuard g(Q.device());
+  avk::knn_topk(Q.data_ptr<float>(), M, R.data_ptr<float>(), N, (int)D, (int)k, q_base, r_base,
+                exclude_self ? 1 : 0, od.data_ptr<float>(), reinterpret_cast<long long*>(oi.data_ptr<int64_t>()),
+                (int)splits, cur_stream(Q));
+  return py::make_tuple(od, oi, splits);
+}
+
+py::tuple cluster_accumulate(const at::Tensor& X, const at::Tensor& assign, int64_t K) {
+  CHECK_DEV(X);
+  CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(assign);
+  CHECK_DTYPE(assign, at::kInt);
+  TORCH_CHECK(X.dim() == 2 && assign.numel() == X.size(0), "X [N,D], assign [N]");
+  auto sums = at::zeros({K, X.size(1)}, X.options().dtype(at::kDouble));
+  auto counts = at::zeros({K}, X.options().dtype(at::kLong));
+  DevGuard g(X.device());
+  avk::cluster_accumulate(X.data_ptr<float>(), X.size(0), (int)X.size(1), assign.data_ptr<int>(), (int)K,
+                          sums.data_ptr<double>(),
+                          reinterpret_cast<unsigned long long*>(counts.data_ptr<int64_t>()), cur_stream(X));
+  return py::make_tuple(sums, counts);
+}
+
+// ---------------------------------------------------------------------------------------------
 // host runtime
 
 // ---------------------------------------------------------------------------------------------
@@ -435,6 +476,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("node_grad_histogram", &node_grad_histogram);
   m.def("tree_assign", &tree_assign);
   m.def("tree_predict", &tree_predict);
+  m.def("knn_topk", &knn_topk);
+  m.def("cluster_accumulate", &cluster_accumulate);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -1,0 +1,232 @@
+// K9 / K11: pairwise distance + fused top-k on MFMA, and cluster accumulation (CDNA4, gfx950).
+//
+// Replaces the reference's all-pairs distance stage (the external sifarish SameTypeSimilarity job
+// driven by resource/knn.sh, and spark RecordSimilarity's bucket-pair replication,
+// S/similarity/RecordSimilarity.scala:80-188) followed by a secondary-sort top-k reducer
+// (J/knn/NearestNeighbor.java:317-406, S/similarity/NearestRecords.scala:97-125): the N x M distance
+// matrix is never materialised.  k-means assignment (J/cluster/KmeansCluster.java:154-172) is the
+// k = 1 case of the same kernel.
+//
+// Block = 256 threads = 4 waves, a 64-query x 64-reference tile per step.  Each wave computes a
+// 32 x 32 block of dot products with the exact f32-input MFMA v_mfma_f32_32x32x2_f32 (bit-exact
+// fmaf chain; on gfx950 it runs at the f32 vector rate and leaves the VALU free for the top-k), the
+// tile is turned into squared distances ||q||^2 + ||r||^2 - 2 q.r in LDS, then 4 threads per query
+// scan 16 candidates each against a private register-resident sorted top-K (insertion is rare once
+// the list has warmed up), and the 4 partial lists are merged at the end.
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+constexpr int KT = 256;   // threads
+constexpr int BQ = 64;    // queries per block
+constexpr int BR = 64;    // references per tile
+constexpr int KC = 32;    // feature chunk staged in LDS (multiple of 2: MFMA K = 2)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int K>
+__device__ __forceinline__ void topk_insert(float (&bd)[K], int (&bi)[K], float d, int j) {
+  if (d < bd[K - 1]) {
+    bd[K - 1] = d;
+    bi[K - 1] = j;
+#pragma unroll
+    for (int s = K - 1; s > 0; --s) {
+      if (bd[s] < bd[s - 1]) {
+        const float td = bd[s]; bd[s] = bd[s - 1]; bd[s - 1] = td;
+        const int ti = bi[s]; bi[s] = bi[s - 1]; bi[s - 1] = ti;
+      }
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(KT) void knn_mfma_kernel(
+    const float* __restrict__ Q, long long M, const float* __restrict__ R, long long N, int D,
+    long long r_per_split, long long q_index_base, long long r_index_base, int exclude_self,
+    float* __restrict__ out_d, long long* __restrict__ out_i, int kk) {
+  __shared__ float sQ[BQ][KC + 1];
+  __shared__ float sR[BR][KC + 1];
+  __shared__ float sD[BQ][BR + 1];
+  __shared__ float sqn[BQ], srn[BR];
+  __shared__ float mD[BQ][4][K];
+  __shared__ int mI[BQ][4][K];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wq = wave >> 1, wr = wave & 1;
+  const long long q0 = (long long)blockIdx.x * BQ;
+  const long long rb = (long long)blockIdx.y * r_per_split;
+  const long long re = min(N, rb + r_per_split);
+
+  // query norms (once)
+  if (tid < BQ) {
+    float s = 0.f;
+    const long long q = q0 + tid;
+    if (q < M)
+      for (int d = 0; d < D; ++d) {
+        const float v = Q[q * D + d];
+        s = fmaf(v, v, s);
+      }
+    sqn[tid] = s;
+  }
+
+  float bd[K];
+  int bi[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
+  const int my_q = tid >> 2, part = tid & 3;
+
+  for (long long r0 = rb; r0 < re; r0 += BR) {
+    __syncthreads();
+    if (tid < BR) {
+      float s = 0.f;
+      const long long r = r0 + tid;
+      if (r < re)
+        for (int d = 0; d < D; ++d) {
+          const float v = R[r * D + d];
+          s = fmaf(v, v, s);
+        }
+      srn[tid] = s;
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    for (int d0 = 0; d0 < D; d0 += KC) {
+      __syncthreads();
+      for (int e = tid; e < BQ * KC; e += KT) {
+        const int row = e / KC, c = e % KC;
+        const long long q = q0 + row;
+        sQ[row][c] = (q < M && d0 + c < D) ? Q[q * D + d0 + c] : 0.f;
+        const long long r = r0 + row;
+        sR[row][c] = (r < re && d0 + c < D) ? R[r * D + d0 + c] : 0.f;
+      }
+      __syncthreads();
+      const int li = lane & 31, lk = lane >> 5;
+#pragma unroll
+      for (int k = 0; k < KC; k += 2) {
+        const float a = sQ[wq * 32 + li][k + lk];   // A[i = lane&31][k = lane>>5]
+        const float b = sR[wr * 32 + li][k + lk];   // B[k = lane>>5][j = lane&31]
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      }
+    }
+    // accumulator -> squared distances in LDS (C/D map: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5))
+    {
+      const int col = lane & 31;
+      const long long rj = r0 + wr * 32 + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int qi = wq * 32 + row;
+        float dist = sqn[qi] + srn[wr * 32 + col] - 2.f * acc[r];
+        dist = fmaxf(dist, 0.f);
+        const long long gq = q0 + qi;
+        if (rj >= re || gq >= M) dist = INFINITY;
+        if (exclude_self && (q_index_base + gq) == (r_index_base + rj)) dist = INFINITY;
+        sD[qi][wr * 32 + col] = dist;
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int c = 0; c < 16; ++c) {
+      const int j = part * 16 + c;
+      topk_insert<K>(bd, bi, sD[my_q][j], (int)(r0 - rb) + j);
+    }
+  }
+  // merge the 4 partial lists of each query
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    mD[my_q][part][s] = bd[s];
+    mI[my_q][part][s] = bi[s];
+  }
+  __syncthreads();
+  if (part == 0) {
+    const long long gq = q0 + my_q;
+    if (gq < M) {
+      int p[4] = {0, 0, 0, 0};
+      for (int s = 0; s < kk; ++s) {
+        int best = 0;
+        float bv = INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float v = p[w] < K ? mD[my_q][w][p[w]] : INFINITY;
+          if (v < bv) { bv = v; best = w; }
+        }
+        const int li = p[best] < K ? mI[my_q][best][p[best]] : -1;
+        out_d[gq * kk + s] = bv;
+        out_i[gq * kk + s] = (li >= 0 && bv < INFINITY) ? (r_index_base + rb + li) : -1;
+        p[best]++;
+      }
+    }
+  }
+}
+
+// Cluster accumulation: sums[k][d] (f64) and counts[k] of the rows assigned to cluster k.
+// LDS-privatised (K*D doubles per block when it fits), flushed once per block.
+__global__ __launch_bounds__(KT) void cluster_accum_kernel(const float* __restrict__ X, long long N, int D,
+                                                           const int* __restrict__ assign, int Kc,
+                                                           double* __restrict__ sums,
+                                                           unsigned long long* __restrict__ counts,
+                                                           int use_lds) {
+  extern __shared__ __attribute__((aligned(16))) double s_sum[];
+  unsigned int* s_cnt = reinterpret_cast<unsigned int*>(s_sum + (use_lds ? Kc * D : 0));
+  if (use_lds) {
+    for (int i = threadIdx.x; i < Kc * D; i += KT) s_sum[i] = 0.0;
+    for (int i = threadIdx.x; i < Kc; i += KT) s_cnt[i] = 0;
+    __syncthreads();
+  }
+  const long long stride = (long long)gridDim.x * KT;
+  for (long long r = (long long)blockIdx.x * KT + threadIdx.x; r < N; r += stride) {
+    const int k = assign[r];
+    if (k < 0 || k >= Kc) continue;
+    if (use_lds) {
+      atomicAdd(&s_cnt[k], 1u);
+      for (int d = 0; d < D; ++d) atomicAdd(&s_sum[k * D + d], (double)X[r * D + d]);
+    } else {
+      atomicAdd(&counts[k], 1ull);
+      for (int d = 0; d < D; ++d) atomicAdd(&sums[(long long)k * D + d], (double)X[r * D + d]);
+    }
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < Kc * D; i += KT)
+      if (s_sum[i] != 0.0) atomicAdd(&sums[i], s_sum[i]);
+    for (int i = threadIdx.x; i < Kc; i += KT)
+      if (s_cnt[i]) atomicAdd(&counts[i], (unsigned long long)s_cnt[i]);
+  }
+}
+
+}  // namespace
+
+namespace avk {
+
+void knn_topk(const float* Q, long long M, const float* R, long long N, int D, int k,
+              long long q_index_base, long long r_index_base, int exclude_self, float* out_d,
+              long long* out_i, int splits, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  const long long per = ((N + splits - 1) / splits + BR - 1) / BR * BR;
+  dim3 grid((unsigned)((M + BQ - 1) / BQ), (unsigned)splits);
+#define AV_KNN(KK)                                                                                \
+  knn_mfma_kernel<KK><<<grid, KT, 0, stream>>>(Q, M, R, N, D, per, q_index_base, r_index_base,    \
+                                               exclude_self, out_d, reinterpret_cast<long long*>(out_i), k)
+  if (k <= 1) AV_KNN(1);
+  else if (k <= 4) AV_KNN(4);
+  else if (k <= 8) AV_KNN(8);
+  else if (k <= 16) AV_KNN(16);
+  else if (k <= 32) AV_KNN(32);
+  else throw std::runtime_error("knn_topk: k > 32 not supported by the fused kernel");
+#undef AV_KNN
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void cluster_accumulate(const float* X, long long N, int D, const int* assign, int K, double* sums,
+                        unsigned long long* counts, hipStream_t stream) {
+  if (N <= 0) return;
+  const size_t lds = (size_t)K * D * sizeof(double) + (size_t)K * sizeof(unsigned);
+  const int use_lds = lds <= 64 * 1024 ? 1 : 0;
+  cluster_accum_kernel<<<av::stream_grid(N, KT, 8, 2048), KT, use_lds ? lds : 0, stream>>>(
+      X, N, D, assign, K, sums, counts, use_lds);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace avk

@@ -1,0 +1,154 @@
+"""Distance ops (K9/K11): fused MFMA distance + top-k, ring-pass distributed kNN, cluster sums,
+and the mixed-type record encoding that turns schema records into a euclidean space."""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from ..data.table import MISSING, Table
+
+_MFMA_METRICS = ("euclidean", "sqeuclidean", "cosine")
+
+
+def _cpu_topk(Q, R, k, metric, p, exclude_self, q_base, r_base, chunk=4096):
+    ds, ix = [], []
+    for s in range(0, Q.shape[0], chunk):
+        q = Q[s:s + chunk]
+        if metric in ("sqeuclidean", "euclidean"):
+            d = torch.cdist(q.double(), R.double()) ** 2
+        elif metric == "cosine":
+            qn = torch.nn.functional.normalize(q.double(), dim=1)
+            rn = torch.nn.functional.normalize(R.double(), dim=1)
+            d = (1 - qn @ rn.T).clamp_min(0)
+        elif metric == "manhattan":
+            d = torch.cdist(q.double(), R.double(), p=1)
+        elif metric == "minkowski":
+            d = torch.cdist(q.double(), R.double(), p=p)
+        else:
+            raise ValueError(f"unknown metric {metric}")
+        if exclude_self:
+            qi = torch.arange(s, s + q.shape[0], device=d.device).view(-1, 1) + q_base
+            ri = torch.arange(R.shape[0], device=d.device).view(1, -1) + r_base
+            d = torch.where(qi == ri, torch.full_like(d, math.inf), d)
+        kk = min(k, R.shape[0])
+        v, i = torch.topk(d, kk, dim=1, largest=False)
+        if kk < k:
+            v = torch.cat([v, torch.full((v.shape[0], k - kk), math.inf, dtype=v.dtype, device=v.device)], 1)
+            i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)
+        i = torch.where(torch.isinf(v), torch.full_like(i, -1), i + r_base)
+        ds.append(v.float())
+        ix.append(i)
+    return torch.cat(ds), torch.cat(ix)
+
+
+def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: float = 2.0,
+        exclude_self: bool = False, q_base: int = 0, r_base: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+    """k nearest references of every query: (dist float32 [M, k] ascending, idx int64 [M, k]);
+    idx = -1 / dist = inf when fewer than k candidates.  ``sqeuclidean`` returns squared distances,
+    ``cosine`` returns 1 - cos."""
+    Q = Q.float().contiguous()
+    R = R.float().contiguous()
+    if Q.is_cuda and metric in _MFMA_METRICS and k <= 32:
+        if metric == "cosine":
+            Qn = torch.nn.functional.normalize(Q, dim=1)
+            Rn = torch.nn.functional.normalize(R, dim=1)
+            d, i, _ = _native.C().knn_topk(Qn, Rn, int(k), int(q_base), int(r_base), bool(exclude_self), 0)
+            return d * 0.5, i
+        d, i, _ = _native.C().knn_topk(Q, R, int(k), int(q_base), int(r_base), bool(exclude_self), 0)
+        return (d.sqrt() if metric == "euclidean" else d), i
+    d, i = _cpu_topk(Q, R, k, "sqeuclidean" if metric == "euclidean" else metric, p, exclude_self,
+                     q_base, r_base)
+    return (d.sqrt() if metric == "euclidean" else d), i
+
+
+def merge_topk(d1, i1, d2, i2, k):
+    d = torch.cat([d1, d2], 1)
+    i = torch.cat([i1, i2], 1)
+    v, j = torch.topk(d, k, dim=1, largest=False)
+    return v, torch.gather(i, 1, j)
+
+
+def distributed_knn(Q: torch.Tensor, R: torch.Tensor, k: int, comm, metric: str = "euclidean",
+                    r_base: int = 0, q_base: int = 0, exclude_self: bool = False):
+    """Systolic all-pairs kNN: every rank keeps its query shard and passes its reference shard
+    around the ring (``Comm.ring_pass``) — no bucket-pair replication.  ``r_base``
+    is this rank's global index offset of R."""
+    if not comm.is_distributed:
+        return knn(Q, R, k, metric, exclude_self=exclude_self, q_base=q_base, r_base=r_base)
+    best_d = torch.full((Q.shape[0], k), math.inf, device=Q.device)
+    best_i = torch.full((Q.shape[0], k), -1, dtype=torch.long, device=Q.device)
+    cur, cur_base = R, torch.tensor([r_base], dtype=torch.long, device=Q.device)
+    for step in range(comm.world):
+        d, i = knn(Q, cur, k, metric, exclude_self=exclude_self, q_base=q_base, r_base=int(cur_base.item()))
+        best_d, best_i = merge_topk(best_d, best_i, d, i, k)
+        if step + 1 < comm.world:
+            cur = comm.ring_pass(cur)
+            cur_base = comm.ring_pass(cur_base)
+    return best_d, best_i
+
+
+def pairwise(Q: torch.Tensor, R: torch.Tensor, metric: str = "euclidean", p: float = 2.0) -> torch.Tensor:
+    """Full distance matrix (for small problems / outputs that need every pair)."""
+    if metric in ("euclidean", "sqeuclidean"):
+        d = torch.cdist(Q.float(), R.float())
+        return d * d if metric == "sqeuclidean" else d
+    if metric == "cosine":
+        return 1 - torch.nn.functional.normalize(Q.float(), dim=1) @ torch.nn.functional.normalize(R.float(), dim=1).T
+    if metric == "manhattan":
+        return torch.cdist(Q.float(), R.float(), p=1)
+    if metric == "minkowski":
+        return torch.cdist(Q.float(), R.float(), p=p)
+    if metric == "jaccard":
+        a, b = (Q > 0).float(), (R > 0).float()
+        inter = a @ b.T
+        union = a.sum(1, keepdim=True) + b.sum(1).unsqueeze(0) - inter
+        return 1 - inter / union.clamp_min(1e-12)
+    raise ValueError(metric)
+
+
+def cluster_accumulate(X: torch.Tensor, assign: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-cluster feature sums (f64 [K, D]) and counts (int64 [K]) of the assigned rows."""
+    if X.is_cuda:
+        return _native.C().cluster_accumulate(X.float().contiguous(), assign.int().contiguous(), int(K))
+    a = assign.long()
+    ok = (a >= 0) & (a < K)
+    sums = torch.zeros((K, X.shape[1]), dtype=torch.float64)
+    sums.index_add_(0, a[ok], X[ok].double())
+    counts = torch.bincount(a[ok], minlength=K)[:K].long()
+    return sums, counts
+
+
+def encode_mixed(t: Table, weights: dict[int, float] | None = None, ranges: dict[int, tuple] | None = None) -> torch.Tensor:
+    """Dense [n, D] float32 embedding whose squared euclidean distance equals the mixed-type record
+    distance: numeric attributes contribute w * ((x - y) / range)^2, categorical attributes
+    w * [x != y] (one-hot scaled by sqrt(w / 2)).  Bucketed attributes are treated as ordinal."""
+    cols = []
+    n = t.n
+    for j, f in enumerate(t.numeric_fields):
+        w = (weights or {}).get(f.ordinal, f.weight)
+        x = t.numeric[j, :n]
+        if ranges and f.ordinal in ranges:
+            lo, hi = ranges[f.ordinal]
+        elif f.min is not None and f.max is not None:
+            lo, hi = f.min, f.max
+        else:
+            lo, hi = float(torch.nan_to_num(x).min()), float(torch.nan_to_num(x).max())
+        rng = max(hi - lo, 1e-12)
+        cols.append(((torch.nan_to_num(x) - lo) / rng * math.sqrt(w)).unsqueeze(1))
+    for j, f in enumerate(t.binned_fields):
+        w = (weights or {}).get(f.ordinal, f.weight)
+        c = t.codes[j, :n].long()
+        if f.is_categorical:
+            b = f.num_bins
+            oh = torch.zeros((n, b), dtype=torch.float32, device=t.device)
+            ok = c < b
+            oh[torch.nonzero(ok).squeeze(1), c[ok]] = math.sqrt(w / 2.0)
+            cols.append(oh)
+        else:
+            b = max(f.num_bins - 1, 1)
+            cols.append((torch.where(c >= MISSING, torch.zeros_like(c), c).float() / b * math.sqrt(w)).unsqueeze(1))
+    if not cols:
+        return torch.zeros((n, 0), device=t.device)
+    return torch.cat(cols, 1).contiguous()

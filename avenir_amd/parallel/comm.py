@@ -149,8 +149,9 @@ class Comm:
         if not self.is_distributed:
             return t.unsqueeze(0)
         x, moved = self._prep(t.contiguous())
-        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        dist.all_gather_into_tensor(out, x)
+        flat = torch.empty((self.world * x.numel(),), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(flat, x.reshape(-1))
+        out = flat.view((self.world,) + tuple(x.shape))
         return out.to(t.device) if moved else out
 
     def all_gather_v(self, t: torch.Tensor) -> torch.Tensor:

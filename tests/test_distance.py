@@ -1,0 +1,154 @@
+"""Distance / kNN / k-means / similarity tests (CPU oracles + gpu numerics)."""
+import math
+
+import pytest
+import torch
+
+from avenir_amd.data import synth
+from avenir_amd.models.cluster import KMeans, categorical_modes, dbscan, hopkins
+from avenir_amd.models.knn import NearestNeighbor
+from avenir_amd.models.similarity import NearestRecords, RecordSimilarity, top_matches_by_class
+from avenir_amd.ops import distance as D
+
+from _dist import run_world
+
+
+def _brute(Q, R, k):
+    d = torch.cdist(Q.double(), R.double())
+    v, i = torch.topk(d, k, dim=1, largest=False)
+    return v.float(), i
+
+
+def test_knn_cpu_matches_bruteforce():
+    g = torch.Generator().manual_seed(0)
+    Q, R = torch.randn(50, 7, generator=g), torch.randn(300, 7, generator=g)
+    d, i = D.knn(Q, R, 5)
+    bd, bi = _brute(Q, R, 5)
+    assert torch.allclose(d, bd, atol=1e-5) and torch.equal(i, bi)
+    d2, i2 = D.knn(R[:40], R, 3, exclude_self=True)
+    assert not bool((i2 == torch.arange(40).view(-1, 1)).any())
+
+
+def test_knn_classifier_and_kernels():
+    x, y = synth.supervised(1200, 5, 2, seed=1)
+    nn_ = NearestNeighbor(k=7, kernel="gaussian", kernel_param=300.0).fit(x[:1000], y[:1000], 2)
+    r = nn_.predict(x[1000:])
+    assert float((r.pred == y[1000:]).float().mean()) > 0.85
+    live = r.class_scores.sum(1) > 0
+    assert bool(live.any())
+    assert torch.allclose(r.class_prob[live].sum(1), torch.full((int(live.sum()),), 100.0), atol=1e-3)
+    for kern in ("none", "linearMultiplicative", "linearAdditive"):
+        r2 = NearestNeighbor(k=5, kernel=kern).fit(x[:1000], y[:1000], 2).predict(x[1000:])
+        assert r2.pred.shape == (200,)
+    reg = NearestNeighbor(k=5, regression="average").fit(x[:1000], y[:1000].float() * 10, 2).predict(x[1000:1010])
+    assert reg.pred.shape == (10,)
+
+
+def test_kmeans_recovers_blobs():
+    g = torch.Generator().manual_seed(3)
+    centers = torch.tensor([[0.0, 0.0], [10.0, 10.0], [-10.0, 8.0]])
+    lab = torch.randint(0, 3, (3000,), generator=g)
+    X = centers[lab] + 0.5 * torch.randn(3000, 2, generator=g)
+    km = KMeans([2, 3, 4, 5], n_init=2, seed=1).fit(X)
+    C = km.best[3].centroids
+    for c in centers:
+        assert float(((C - c) ** 2).sum(1).min()) < 0.1
+    assert km.knuckle_k() == 3
+    pred = km.predict(X, 3)
+    # purity
+    agree = 0
+    for k in range(3):
+        m = pred == k
+        agree += int(torch.bincount(lab[m], minlength=3).max())
+    assert agree / 3000 > 0.99
+
+
+def _rank_kmeans(rank, world, X):
+    from avenir_amd.parallel.comm import get_comm
+    n = X.shape[0]
+    s, e = rank * n // world, (rank + 1) * n // world
+    km = KMeans(3, seed=5, comm=get_comm()).fit(X[s:e])
+    return km.best[3].centroids, km.best[3].sse
+
+
+def test_kmeans_world_size_equivalence():
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(2000, 3, generator=g) + torch.randint(0, 3, (2000, 1), generator=g) * 6.0
+    ref = KMeans(3, seed=5).fit(X)
+    res = run_world(_rank_kmeans, 2, X)
+    for C, sse in res:
+        assert sse == pytest.approx(ref.best[3].sse, rel=1e-4)
+
+
+def test_distributed_knn_ring():
+    g = torch.Generator().manual_seed(5)
+    R = torch.randn(400, 4, generator=g)
+    Q = torch.randn(30, 4, generator=g)
+    res = run_world(_rank_knn, 2, Q, R)
+    bd, bi = _brute(Q, R, 4)
+    for d, i in res:
+        assert torch.equal(i, bi) and torch.allclose(d, bd, atol=1e-5)
+
+
+def _rank_knn(rank, world, Q, R):
+    from avenir_amd.parallel.comm import get_comm
+    n = R.shape[0]
+    s, e = rank * n // world, (rank + 1) * n // world
+    return D.distributed_knn(Q, R[s:e].contiguous(), 4, get_comm(), r_base=s)
+
+
+def test_similarity_helpers():
+    g = torch.Generator().manual_seed(6)
+    X = torch.randn(100, 3, generator=g)
+    y = torch.randint(0, 2, (100,), generator=g)
+    d, i = top_matches_by_class(X, y, 3)
+    ok = i >= 0
+    assert bool((y[i[ok]] == y.view(-1, 1).expand_as(i)[ok]).all())
+    d2, i2 = top_matches_by_class(X, y, 3, same_class=False)
+    assert bool((y[i2[i2 >= 0]] != y.view(-1, 1).expand_as(i2)[i2 >= 0]).all())
+    pairs = list(RecordSimilarity().all_pairs(X[:10]))
+    assert sum(p[0].numel() for p in pairs) == 45
+    nd, ni = NearestRecords(k=2, max_distance=0.5)(X)
+    assert bool((nd[ni >= 0] <= 0.5).all())
+
+
+def test_dbscan_and_hopkins():
+    g = torch.Generator().manual_seed(7)
+    X = torch.cat([torch.randn(100, 2, generator=g) * 0.2, torch.randn(100, 2, generator=g) * 0.2 + 5])
+    lab = dbscan(X, eps=0.5, min_samples=4)
+    assert int(lab.max()) == 1
+    assert hopkins(X, 50) > 0.8
+
+
+def test_categorical_modes():
+    codes = torch.full((2, 16), 255, dtype=torch.uint8)
+    codes[0, :6] = torch.tensor([0, 0, 1, 2, 2, 2], dtype=torch.uint8)
+    codes[1, :6] = torch.tensor([1, 1, 0, 0, 0, 1], dtype=torch.uint8)
+    m = categorical_modes(codes, 6, [3, 2], torch.tensor([0, 0, 0, 1, 1, 1]), 2)
+    assert m.tolist() == [[0, 1], [2, 0]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,Dm,k", [(1000, 5000, 16, 5), (77, 3001, 3, 1), (513, 1000, 70, 32),
+                                       (4096, 20000, 33, 8)])
+def test_knn_mfma_gpu(cuda, M, N, Dm, k):
+    g = torch.Generator().manual_seed(M)
+    Q, R = torch.randn(M, Dm, generator=g), torch.randn(N, Dm, generator=g)
+    d, i = D.knn(Q.to(cuda), R.to(cuda), k)
+    bd, bi = _brute(Q, R, k)
+    assert torch.allclose(d.cpu(), bd, atol=2e-3, rtol=1e-4)
+    agree = float((i.cpu() == bi).float().mean())
+    assert agree > 0.995
+    d2, i2 = D.knn(R[:300].to(cuda), R.to(cuda), 4, exclude_self=True)
+    assert not bool((i2.cpu() == torch.arange(300).view(-1, 1)).any())
+
+
+@pytest.mark.gpu
+def test_kmeans_gpu_matches_cpu(cuda):
+    g = torch.Generator().manual_seed(8)
+    X = torch.randn(20000, 6, generator=g) + torch.randint(0, 4, (20000, 1), generator=g) * 5.0
+    kc = KMeans(4, seed=2, max_iter=50).fit(X)
+    kg = KMeans(4, seed=2, max_iter=50).fit(X.to(cuda))
+    assert kg.best[4].sse == pytest.approx(kc.best[4].sse, rel=1e-3)
+    s, c = D.cluster_accumulate(X.to(cuda), torch.randint(0, 4, (20000,), generator=g).int().to(cuda), 4)
+    assert int(c.sum()) == 20000
