@@ -373,8 +373,8 @@ py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t 
     const int64_t qb = (M + 63) / 64;
     splits = std::max<int64_t>(1, std::min<int64_t>((N + 63) / 64, (2048 + qb - 1) / qb));
   }
-  auto od = at::empty({M, k}, Q.options());
-  auto oi = at::empty({M, k}, Q.options().dtype(at::kLong));
+  auto od = at::empty({splits, M, k}, Q.options());
+  auto oi = at::empty({splits, M, k}, Q.options().dtype(at::kLong));
   DevGuard g(Q.device());
   avk::knn_topk(Q.data_ptr<float>(), M, R.data_ptr<float>(), N, (int)D, (int)k, q_base, r_base,
                 exclude_self ? 1 : 0, od.data_ptr<float>(), reinterpret_cast<long long*>(oi.data_ptr<int64_t>()),

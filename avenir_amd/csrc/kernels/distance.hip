@@ -142,6 +142,9 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   __syncthreads();
   if (part == 0) {
     const long long gq = q0 + my_q;
+    // each reference split writes its own [M][kk] slab (merged by the caller)
+    out_d += (long long)blockIdx.y * M * kk;
+    out_i += (long long)blockIdx.y * M * kk;
     if (gq < M) {
       int p[4] = {0, 0, 0, 0};
       for (int s = 0; s < kk; ++s) {

@@ -52,11 +52,18 @@ def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: 
     R = R.float().contiguous()
     if Q.is_cuda and metric in _MFMA_METRICS and k <= 32:
         if metric == "cosine":
-            Qn = torch.nn.functional.normalize(Q, dim=1)
-            Rn = torch.nn.functional.normalize(R, dim=1)
-            d, i, _ = _native.C().knn_topk(Qn, Rn, int(k), int(q_base), int(r_base), bool(exclude_self), 0)
+            Q = torch.nn.functional.normalize(Q, dim=1)
+            R = torch.nn.functional.normalize(R, dim=1)
+        d, i, splits = _native.C().knn_topk(Q, R, int(k), int(q_base), int(r_base), bool(exclude_self), 0)
+        if splits > 1:  # merge the per-split top-k slabs [S, M, k] -> [M, k]
+            d = d.permute(1, 0, 2).reshape(Q.shape[0], -1)
+            i = i.permute(1, 0, 2).reshape(Q.shape[0], -1)
+            d, j = torch.topk(d, int(k), dim=1, largest=False)
+            i = torch.gather(i, 1, j)
+        else:
+            d, i = d[0], i[0]
+        if metric == "cosine":
             return d * 0.5, i
-        d, i, _ = _native.C().knn_topk(Q, R, int(k), int(q_base), int(r_base), bool(exclude_self), 0)
         return (d.sqrt() if metric == "euclidean" else d), i
     d, i = _cpu_topk(Q, R, k, "sqeuclidean" if metric == "euclidean" else metric, p, exclude_self,
                      q_base, r_base)
