@@ -398,6 +398,50 @@ py::tuple cluster_accumulate(const at::Tensor& X, const at::Tensor& assign, int6
 }
 
 // ---------------------------------------------------------------------------------------------
+// sequences (K14/K15)
+// ---------------------------------------------------------------------------------------------
+py::tuple viterbi(const at::Tensor& obs, const at::Tensor& logA, const at::Tensor& logB,
+                  const at::Tensor& logpi, int64_t mode) {
+  CHECK_DEV(obs);
+  CHECK_DTYPE(obs, at::kShort);
+  TORCH_CHECK(obs.dim() == 2, "obs must be [N, T]");
+  for (const at::Tensor* t : {&logA, &logB, &logpi}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  const int64_t S = logA.size(0), O = logB.size(1);
+  TORCH_CHECK(logA.dim() == 2 && logA.size(1) == S, "logA must be [S, S]");
+  TORCH_CHECK(logB.dim() == 2 && logB.size(0) == S, "logB must be [S, O]");
+  TORCH_CHECK(logpi.numel() == S, "logpi must be [S]");
+  TORCH_CHECK(S >= 1 && S <= 192, "1 <= S <= 192");
+  const int64_t N = obs.size(0), T = obs.size(1);
+  auto opts = obs.options();
+  auto path = at::empty({N, T}, opts);
+  auto score = at::empty({N}, logA.options());
+  at::Tensor bp = mode == 0 ? at::empty({N, T, S}, opts) : at::empty({1}, opts);
+  DevGuard g(obs.device());
+  avk::viterbi(obs.data_ptr<int16_t>(), N, (int)T, (int)S, (int)O, logA.data_ptr<float>(),
+               logB.data_ptr<float>(), logpi.data_ptr<float>(), (int)mode, bp.data_ptr<int16_t>(),
+               path.data_ptr<int16_t>(), score.data_ptr<float>(), cur_stream(obs));
+  return py::make_tuple(path, score);
+}
+
+at::Tensor markov_logodds(const at::Tensor& states, const at::Tensor& lr) {
+  CHECK_DEV(states);
+  CHECK_DTYPE(states, at::kShort);
+  TORCH_CHECK(states.dim() == 2, "states must be [N, L]");
+  CHECK_DEV(lr);
+  CHECK_DTYPE(lr, at::kFloat);
+  TORCH_CHECK(lr.dim() == 2 && lr.size(0) == lr.size(1), "lr must be [S, S]");
+  TORCH_CHECK(lr.size(0) <= 200, "S <= 200");
+  auto out = at::empty({states.size(0)}, lr.options());
+  DevGuard g(states.device());
+  avk::markov_logodds(states.data_ptr<int16_t>(), states.size(0), (int)states.size(1), lr.data_ptr<float>(),
+                      (int)lr.size(0), out.data_ptr<float>(), cur_stream(states));
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
 // host runtime
 
 // ---------------------------------------------------------------------------------------------
@@ -478,6 +522,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("tree_predict", &tree_predict);
   m.def("knn_topk", &knn_topk);
   m.def("cluster_accumulate", &cluster_accumulate);
+  m.def("viterbi", &viterbi);
+  m.def("markov_logodds", &markov_logodds);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -53,4 +53,10 @@ void knn_topk(const float* Q, long long M, const float* R, long long N, int D, i
 void cluster_accumulate(const float* X, long long N, int D, const int* assign, int K, double* sums,
                         unsigned long long* counts, hipStream_t stream);
 
+// ---- sequence.hip (K14/K15) ----------------------------------------------------------------
+void viterbi(const short* obs, long long n, int T, int S, int O, const float* logA, const float* logB,
+             const float* logpi, int mode, short* bp, short* path, float* score, hipStream_t stream);
+void markov_logodds(const short* states, long long n, int L, const float* lr, int S, float* out,
+                    hipStream_t stream);
+
 }  // namespace avk
