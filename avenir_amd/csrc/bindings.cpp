@@ -442,6 +442,52 @@ at::Tensor markov_logodds(const at::Tensor& states, const at::Tensor& lr) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// association mining (K17)
+// ---------------------------------------------------------------------------------------------
+at::Tensor itemset_support(const at::Tensor& P, const at::Tensor& items, const at::Tensor& cand_prefix,
+                           const at::Tensor& cand_item) {
+  CHECK_DEV(P);
+  CHECK_DTYPE(P, at::kLong);
+  CHECK_DEV(items);
+  CHECK_DTYPE(items, at::kLong);
+  CHECK_DEV(cand_prefix);
+  CHECK_DTYPE(cand_prefix, at::kInt);
+  CHECK_DEV(cand_item);
+  CHECK_DTYPE(cand_item, at::kInt);
+  TORCH_CHECK(P.dim() == 2 && items.dim() == 2 && P.size(1) == items.size(1), "P [F,W], items [I,W]");
+  TORCH_CHECK(cand_prefix.numel() == cand_item.numel(), "candidate arrays differ in length");
+  const int64_t M = cand_prefix.numel();
+  if (M) {
+    TORCH_CHECK(cand_prefix.min().item<int>() >= 0 && cand_prefix.max().item<int>() < P.size(0),
+                "cand_prefix out of range");
+    TORCH_CHECK(cand_item.min().item<int>() >= 0 && cand_item.max().item<int>() < items.size(0),
+                "cand_item out of range");
+  }
+  auto sup = at::zeros({M}, P.options());
+  DevGuard g(P.device());
+  avk::itemset_support(reinterpret_cast<const unsigned long long*>(P.data_ptr<int64_t>()), (int)P.size(1),
+                       reinterpret_cast<const unsigned long long*>(items.data_ptr<int64_t>()),
+                       cand_prefix.data_ptr<int>(), cand_item.data_ptr<int>(), (int)M,
+                       reinterpret_cast<unsigned long long*>(sup.data_ptr<int64_t>()), cur_stream(P));
+  return sup;
+}
+
+at::Tensor build_bitsets(const at::Tensor& tx, const at::Tensor& item, int64_t n_tx, int64_t n_items) {
+  CHECK_DEV(tx);
+  CHECK_DTYPE(tx, at::kLong);
+  CHECK_DEV(item);
+  CHECK_DTYPE(item, at::kInt);
+  TORCH_CHECK(tx.numel() == item.numel(), "tx/item length mismatch");
+  const int64_t W = (n_tx + 63) / 64;
+  auto bits = at::zeros({n_items, std::max<int64_t>(W, 1)}, tx.options());
+  DevGuard g(tx.device());
+  avk::build_bitsets(reinterpret_cast<const long long*>(tx.data_ptr<int64_t>()), item.data_ptr<int>(),
+                     tx.numel(), (int)std::max<int64_t>(W, 1), (int)n_items,
+                     reinterpret_cast<unsigned long long*>(bits.data_ptr<int64_t>()), cur_stream(tx));
+  return bits;
+}
+
+// ---------------------------------------------------------------------------------------------
 // host runtime
 
 // ---------------------------------------------------------------------------------------------
@@ -524,6 +570,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cluster_accumulate", &cluster_accumulate);
   m.def("viterbi", &viterbi);
   m.def("markov_logodds", &markov_logodds);
+  m.def("itemset_support", &itemset_support);
+  m.def("build_bitsets", &build_bitsets);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

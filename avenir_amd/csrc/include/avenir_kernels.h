@@ -59,4 +59,11 @@ void viterbi(const short* obs, long long n, int T, int S, int O, const float* lo
 void markov_logodds(const short* states, long long n, int L, const float* lr, int S, float* out,
                     hipStream_t stream);
 
+// ---- assoc.hip (K17) -----------------------------------------------------------------------
+void itemset_support(const unsigned long long* P, int W, const unsigned long long* items,
+                     const int* cand_prefix, const int* cand_item, int M, unsigned long long* support,
+                     hipStream_t stream);
+void build_bitsets(const long long* tx, const int* item, long long n, int W, int n_items,
+                   unsigned long long* bits, hipStream_t stream);
+
 }  // namespace avk
