@@ -488,6 +488,50 @@ at::Tensor build_bitsets(const at::Tensor& tx, const at::Tensor& item, int64_t n
 }
 
 // ---------------------------------------------------------------------------------------------
+// bandits (K20)
+// ---------------------------------------------------------------------------------------------
+at::Tensor bandit_select(int64_t algo, int64_t batch, const at::Tensor& trials, const at::Tensor& rsum,
+                         const at::Tensor& probs, const at::Tensor& hist, double bin_width,
+                         const at::Tensor& fparam, const at::Tensor& iparam, at::Tensor& gstate,
+                         at::Tensor& istate, at::Tensor& epochs, int64_t seed, int64_t round) {
+  CHECK_DEV(trials);
+  CHECK_DTYPE(trials, at::kInt);
+  TORCH_CHECK(trials.dim() == 2, "trials must be [G, A]");
+  const int64_t G = trials.size(0), A = trials.size(1);
+  TORCH_CHECK(A >= 1 && A <= 64, "1 <= arms <= 64");
+  CHECK_DEV(rsum);
+  CHECK_DTYPE(rsum, at::kFloat);
+  CHECK_DEV(probs);
+  CHECK_DTYPE(probs, at::kFloat);
+  CHECK_DEV(hist);
+  CHECK_DTYPE(hist, at::kInt);
+  TORCH_CHECK(rsum.sizes() == trials.sizes() && probs.sizes() == trials.sizes(), "rsum/probs shape");
+  TORCH_CHECK(hist.dim() == 3 && hist.size(0) == G && hist.size(1) == A, "hist must be [G, A, NB]");
+  CHECK_DEV(fparam);
+  CHECK_DTYPE(fparam, at::kFloat);
+  CHECK_DEV(iparam);
+  CHECK_DTYPE(iparam, at::kInt);
+  TORCH_CHECK(fparam.numel() >= 8 && iparam.numel() >= 8, "param vectors need 8 entries");
+  CHECK_DEV(gstate);
+  CHECK_DTYPE(gstate, at::kFloat);
+  CHECK_DEV(istate);
+  CHECK_DTYPE(istate, at::kInt);
+  CHECK_DEV(epochs);
+  CHECK_DTYPE(epochs, at::kInt);
+  TORCH_CHECK(gstate.numel() == G * 4 && istate.numel() == G * 4 && epochs.sizes() == trials.sizes(),
+              "state shapes");
+  TORCH_CHECK(batch >= 1, "batch >= 1");
+  auto out = at::empty({G, batch}, trials.options());
+  DevGuard g(trials.device());
+  avk::bandit_select((int)algo, (int)G, (int)A, (int)batch, trials.data_ptr<int>(), rsum.data_ptr<float>(),
+                     probs.data_ptr<float>(), reinterpret_cast<const unsigned*>(hist.data_ptr<int>()),
+                     (int)hist.size(2), (float)bin_width, fparam.data_ptr<float>(), iparam.data_ptr<int>(),
+                     gstate.data_ptr<float>(), istate.data_ptr<int>(), epochs.data_ptr<int>(),
+                     (unsigned long long)seed, (unsigned long long)round, out.data_ptr<int>(), cur_stream(trials));
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
 // host runtime
 
 // ---------------------------------------------------------------------------------------------
@@ -572,6 +616,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("markov_logodds", &markov_logodds);
   m.def("itemset_support", &itemset_support);
   m.def("build_bitsets", &build_bitsets);
+  m.def("bandit_select", &bandit_select);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -66,4 +66,10 @@ void itemset_support(const unsigned long long* P, int W, const unsigned long lon
 void build_bitsets(const long long* tx, const int* item, long long n, int W, int n_items,
                    unsigned long long* bits, hipStream_t stream);
 
+// ---- bandit.hip (K20) ----------------------------------------------------------------------
+void bandit_select(int algo, int G, int A, int batch, const int* trials, const float* rsum, const float* probs,
+                   const unsigned* hist, int nb, float bin_width, const float* fparam, const int* iparam,
+                   float* gstate, int* istate, int* epochs, unsigned long long seed, unsigned long long round,
+                   int* out, hipStream_t stream);
+
 }  // namespace avk
