@@ -532,6 +532,75 @@ at::Tensor bandit_select(int64_t algo, int64_t batch, const at::Tensor& trials, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// samplers (K21)
+// ---------------------------------------------------------------------------------------------
+at::Tensor sample(int64_t dist, int64_t n, const at::Tensor& params, const c10::optional<at::Tensor>& table,
+                  int64_t seed, int64_t offset) {
+  CHECK_DEV(params);
+  CHECK_DTYPE(params, at::kFloat);
+  TORCH_CHECK(params.numel() >= 3, "params needs 3 entries");
+  TORCH_CHECK(n >= 0, "n >= 0");
+  const float* tp = nullptr;
+  int nb = 0;
+  if (table.has_value() && table->defined()) {
+    CHECK_DEV((*table));
+    CHECK_DTYPE((*table), at::kFloat);
+    TORCH_CHECK(table->numel() >= 1, "empty CDF table");
+    tp = table->data_ptr<float>();
+    nb = (int)table->numel();
+  }
+  TORCH_CHECK(dist != 9 || tp != nullptr, "table sampler needs a CDF");
+  auto out = at::empty({n}, params.options());
+  DevGuard g(params.device());
+  avk::sample((int)dist, n, params.data_ptr<float>(), tp, nb, (unsigned long long)seed, (unsigned long long)offset,
+              out.data_ptr<float>(), cur_stream(params));
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+// optimisation (K22)
+// ---------------------------------------------------------------------------------------------
+void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict, bool swap, at::Tensor& sol,
+               at::Tensor& cur_cost, at::Tensor& best_sol, at::Tensor& best_cost, int64_t iters, double t0,
+               double cool, int64_t interval, bool geometric, int64_t max_retry, int64_t seed, int64_t offset,
+               at::Tensor& stats) {
+  CHECK_DEV(cost);
+  CHECK_DTYPE(cost, at::kFloat);
+  TORCH_CHECK(cost.dim() == 2 && cost.size(1) >= 2, "cost must be [L, V>=2]");
+  const int64_t L = cost.size(0), V = cost.size(1);
+  TORCH_CHECK(V <= 32767 && L <= 512, "V or L too large (L <= 512: the [L][64] solution tile lives in LDS)");
+  CHECK_DEV(sol);
+  CHECK_DTYPE(sol, at::kShort);
+  TORCH_CHECK(sol.dim() == 2 && sol.size(1) == L, "sol must be [P, L]");
+  const int64_t P = sol.size(0);
+  TORCH_CHECK(sol.min().item<int>() >= 0 && sol.max().item<int>() < V, "solution values out of range");
+  CHECK_DEV(best_sol);
+  CHECK_DTYPE(best_sol, at::kShort);
+  TORCH_CHECK(best_sol.sizes() == sol.sizes(), "best_sol shape");
+  for (at::Tensor* t : {&cur_cost, &best_cost}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+    TORCH_CHECK(t->numel() == P, "cost vectors must be [P]");
+  }
+  CHECK_DEV(stats);
+  CHECK_DTYPE(stats, at::kLong);
+  TORCH_CHECK(stats.numel() >= 3, "stats needs 3 entries");
+  const uint8_t* cf = nullptr;
+  if (conflict.has_value() && conflict->defined()) {
+    CHECK_DEV((*conflict));
+    CHECK_DTYPE((*conflict), at::kByte);
+    TORCH_CHECK(conflict->dim() == 2 && conflict->size(0) == L && conflict->size(1) == L, "conflict [L, L]");
+    cf = conflict->data_ptr<uint8_t>();
+  }
+  DevGuard g(cost.device());
+  avk::sa_assign(cost.data_ptr<float>(), (int)L, (int)V, cf, swap ? 1 : 0, sol.data_ptr<int16_t>(), cur_cost.data_ptr<float>(),
+                 best_sol.data_ptr<int16_t>(), best_cost.data_ptr<float>(), (int)P, (int)iters, (float)t0,
+                 (float)cool, (int)interval, geometric ? 1 : 0, (int)max_retry, (unsigned long long)seed,
+                 (unsigned long long)offset, reinterpret_cast<unsigned long long*>(stats.data_ptr<int64_t>()),
+                 cur_stream(cost));
+}
+
+// ---------------------------------------------------------------------------------------------
 // host runtime
 
 // ---------------------------------------------------------------------------------------------
@@ -617,6 +686,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("itemset_support", &itemset_support);
   m.def("build_bitsets", &build_bitsets);
   m.def("bandit_select", &bandit_select);
+  m.def("sample", &sample);
+  m.def("sa_assign", &sa_assign);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

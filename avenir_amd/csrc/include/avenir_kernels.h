@@ -72,4 +72,14 @@ void bandit_select(int algo, int G, int A, int batch, const int* trials, const f
                    float* gstate, int* istate, int* epochs, unsigned long long seed, unsigned long long round,
                    int* out, hipStream_t stream);
 
+// ---- sampler.hip (K21) ---------------------------------------------------------------------
+void sample(int dist, long long n, const float* params, const float* table, int nbins, unsigned long long seed,
+            unsigned long long offset, float* out, hipStream_t stream);
+
+// ---- optim.hip (K22) -----------------------------------------------------------------------
+void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
+               short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
+               int geometric, int max_retry, unsigned long long seed, unsigned long long offset,
+               unsigned long long* stats, hipStream_t stream);
+
 }  // namespace avk

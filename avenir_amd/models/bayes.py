@@ -205,6 +205,27 @@ class NaiveBayes:
             ok = a < C
             conf += torch.bincount(a[ok] * C + pred[:n].long()[ok], minlength=C * C).view(C, C)
 
+    def feature_loglik(self, t: Table) -> tuple[torch.Tensor, torch.Tensor]:
+        """Per-row, per-feature, per-class log-likelihood terms ``[n, Fcat + Fnum, C]`` and class
+        log-priors — the decomposition the feature-subset optimiser scores subsets with (a subset's
+        posterior score is the masked sum over the feature axis)."""
+        tb = self.tables(t.device)
+        n, C = t.n, self.n_classes
+        cols = []
+        o = 0
+        for f, b in enumerate(self.bins):
+            v = t.codes[f, :n].long()
+            ok = v < b
+            vv = torch.where(ok, v, torch.zeros_like(v)) + o
+            cols.append(torch.where(ok.unsqueeze(1), tb["logp"][:, vv].T, torch.zeros((), device=t.device)))
+            o += b
+        if t.numeric.shape[0]:
+            x = t.numeric[:, :n].T
+            z = (x.unsqueeze(1) - tb["gmean"].unsqueeze(0)) * tb["ginvstd"].unsqueeze(0)   # [n, C, Fc]
+            g = tb["glognorm"].unsqueeze(0) - 0.5 * z * z
+            cols.extend(g[:, :, j] for j in range(g.shape[2]))
+        return torch.stack(cols, 1), tb["logprior"]
+
     def validation_counters(self, conf: torch.Tensor, comm: Comm | None = None,
                             pos_class: int = 1) -> Counters:
         """Reference "Validation" counter group from an (all-reduced) confusion matrix."""
