@@ -601,6 +601,70 @@ void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict
 }
 
 // ---------------------------------------------------------------------------------------------
+// generalised linear models (K13)
+// ---------------------------------------------------------------------------------------------
+at::Tensor glm_gradient(const at::Tensor& X, int64_t n, const at::Tensor& y, const c10::optional<at::Tensor>& sw,
+                        const at::Tensor& w, int64_t mode, const c10::optional<at::Tensor>& hw) {
+  CHECK_DEV(X);
+  CHECK_DTYPE(X, at::kFloat);
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous(), "X must be contiguous [D, ld]");
+  const int64_t D = X.size(0), ld = X.size(1);
+  TORCH_CHECK(D == 4 || D == 8 || D == 16 || D == 32, "D must be padded to 4/8/16/32");
+  TORCH_CHECK(ld % 16 == 0 && n >= 0 && n <= ld, "ld must be a multiple of 16 and >= n");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 logistic, 1 squared, 2 hinge");
+  CHECK_DEV(y);
+  CHECK_DTYPE(y, at::kFloat);
+  TORCH_CHECK(y.is_contiguous() && y.numel() >= ld, "y must cover ld rows");
+  CHECK_DEV(w);
+  CHECK_DTYPE(w, at::kFloat);
+  TORCH_CHECK(w.is_contiguous() && w.numel() == D, "w must be [D]");
+  const float* swp = nullptr;
+  if (sw.has_value() && sw->defined()) {
+    CHECK_DEV((*sw));
+    CHECK_DTYPE((*sw), at::kFloat);
+    TORCH_CHECK(sw->is_contiguous() && sw->numel() >= ld, "sw must cover ld rows");
+    swp = sw->data_ptr<float>();
+  }
+  float* hwp = nullptr;
+  if (hw.has_value() && hw->defined()) {
+    CHECK_DEV((*hw));
+    CHECK_DTYPE((*hw), at::kFloat);
+    TORCH_CHECK(hw->is_contiguous() && hw->numel() >= n, "hw must cover n rows");
+    hwp = hw->data_ptr<float>();
+  }
+  DevGuard g(X.device());
+  const int grid = avk::glm_grid(n);
+  auto partial = at::empty({grid, D + 1}, X.options().dtype(at::kDouble));
+  avk::glm_grad(X.data_ptr<float>(), ld, n, (int)D, y.data_ptr<float>(), swp, w.data_ptr<float>(), (int)mode,
+                partial.data_ptr<double>(), grid, hwp, cur_stream(X));
+  return partial.sum(0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// SMO kernel SVM (K12)
+// ---------------------------------------------------------------------------------------------
+at::Tensor smo_solve(const at::Tensor& K, const at::Tensor& y, const at::Tensor& diag, at::Tensor& alpha,
+                     at::Tensor& G, double C, double eps, int64_t max_iter) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&K, &y, &diag, &alpha, &G}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+    TORCH_CHECK(t->is_contiguous(), "SMO tensors must be contiguous");
+  }
+  TORCH_CHECK(K.dim() == 3 && K.size(1) == K.size(2), "K must be [B, N, N]");
+  const int64_t B = K.size(0), N = K.size(1);
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&y, &diag, &alpha, &G})
+    TORCH_CHECK(t->dim() == 2 && t->size(0) == B && t->size(1) == N, "SMO vectors must be [B, N]");
+  TORCH_CHECK(N < (1LL << 31) / 2, "N too large");
+  TORCH_CHECK(C > 0 && eps > 0 && max_iter >= 0, "bad SMO parameters");
+  DevGuard g(K.device());
+  auto iters = at::zeros({B}, K.options().dtype(at::kInt));
+  avk::smo_solve(K.data_ptr<float>(), y.data_ptr<float>(), diag.data_ptr<float>(), alpha.data_ptr<float>(),
+                 G.data_ptr<float>(), (int)B, (int)N, (float)C, (float)eps, (int)max_iter, iters.data_ptr<int>(),
+                 cur_stream(K));
+  return iters;
+}
+
+// ---------------------------------------------------------------------------------------------
 // host runtime
 
 // ---------------------------------------------------------------------------------------------
@@ -688,6 +752,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bandit_select", &bandit_select);
   m.def("sample", &sample);
   m.def("sa_assign", &sa_assign);
+  m.def("glm_gradient", &glm_gradient);
+  m.def("smo_solve", &smo_solve);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -82,4 +82,13 @@ void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swa
                int geometric, int max_retry, unsigned long long seed, unsigned long long offset,
                unsigned long long* stats, hipStream_t stream);
 
+// ---- linear.hip (K13) ----------------------------------------------------------------------
+int glm_grid(long long n);
+void glm_grad(const float* X, long long ld, long long n, int D, const float* y, const float* sw, const float* w,
+              int mode, double* partial, int grid, float* hw, hipStream_t stream);
+
+// ---- svm.hip (K12) -------------------------------------------------------------------------
+void smo_solve(const float* K, const float* y, const float* diag, float* alpha, float* G, int B, int N, float C,
+               float eps, int max_iter, int* iters, hipStream_t stream);
+
 }  // namespace avk

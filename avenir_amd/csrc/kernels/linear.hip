@@ -1,0 +1,122 @@
+// K13: fused generalised-linear-model gradient (CDNA4, gfx950).
+//
+// Reference: LogisticRegressor.aggregate (J/regress/LogisticRegressor.java:61-73) computes, per
+// record, sigma(w.x) and accumulates x * (y - sigma) — one mapper pass per Hadoop job
+// (J/regress/LogisticRegressionJob.java:143-195).  Here ONE pass over the column-major feature
+// matrix X [D, ld] (the framework's SoA layout: a wave's loads of one feature are contiguous) yields
+//   g = sum_i sw_i * x_i * e_i        (e = y - sigma(z) | y - z | hinge subgradient y*[y z < 1])
+//   loss = sum_i sw_i * l_i           (logistic NLL | squared/2 | hinge)
+//   h_i = sw_i * sigma'(z_i)          (optional per-row curvature, for the Newton/IRLS Hessian GEMM)
+// Each lane owns VEC consecutive rows (vector loads), keeps w and its gradient partials in
+// registers, and the block reduces through wave DPP sums + LDS into one double partial row;
+// partial rows are summed on device (deterministic: no float atomics).
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ float softplus(float z) {
+  return z > 0.f ? z + log1pf(__expf(-z)) : log1pf(__expf(z));
+}
+
+template <int D, int VEC>
+__global__ __launch_bounds__(256) void glm_grad_kernel(const float* __restrict__ X, long long ld, long long n,
+                                                       const float* __restrict__ y, const float* __restrict__ sw,
+                                                       const float* __restrict__ w, int mode,
+                                                       double* __restrict__ partial, float* __restrict__ hw) {
+  typedef float vf __attribute__((ext_vector_type(VEC)));
+  __shared__ float red[4][D + 1];
+  float wr[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) wr[k] = w[k];
+  float g[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) g[k] = 0.f;
+  float loss = 0.f;
+  const long long nq = (n + VEC - 1) / VEC;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < nq; q += stride) {
+    const long long r0 = q * VEC;
+    vf xv[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xv[k] = *reinterpret_cast<const vf*>(X + (long long)k * ld + r0);
+    const vf yv = *reinterpret_cast<const vf*>(y + r0);
+    vf sv;
+    if (sw) sv = *reinterpret_cast<const vf*>(sw + r0);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      if (r0 + v >= n) break;
+      float z = 0.f;
+#pragma unroll
+      for (int k = 0; k < D; ++k) z = fmaf(wr[k], xv[k][v], z);
+      const float yy = yv[v];
+      const float s = sw ? sv[v] : 1.f;
+      float e, l, h;
+      if (mode == 0) {
+        const float p = 1.f / (1.f + __expf(-z));
+        e = yy - p;
+        l = softplus(z) - yy * z;
+        h = p * (1.f - p);
+      } else if (mode == 1) {
+        e = yy - z;
+        l = 0.5f * e * e;
+        h = 1.f;
+      } else {
+        const float m = yy * z;
+        e = m < 1.f ? yy : 0.f;
+        l = fmaxf(0.f, 1.f - m);
+        h = 0.f;
+      }
+      e *= s;
+#pragma unroll
+      for (int k = 0; k < D; ++k) g[k] = fmaf(xv[k][v], e, g[k]);
+      loss = fmaf(l, s, loss);
+      if (hw) hw[r0 + v] = h * s;
+    }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const float t = av::wave_sum(g[k]);
+    if (lane == 0) red[wid][k] = t;
+  }
+  {
+    const float t = av::wave_sum(loss);
+    if (lane == 0) red[wid][D] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x <= D) {
+    double acc = 0.0;
+    for (int q = 0; q < 4; ++q) acc += (double)red[q][threadIdx.x];
+    partial[(long long)blockIdx.x * (D + 1) + threadIdx.x] = acc;
+  }
+}
+
+template <int D, int VEC>
+void launch_glm(const float* X, long long ld, long long n, const float* y, const float* sw, const float* w, int mode,
+                double* partial, int grid, float* hw, hipStream_t stream) {
+  glm_grad_kernel<D, VEC><<<grid, 256, 0, stream>>>(X, ld, n, y, sw, w, mode, partial, hw);
+}
+
+}  // namespace
+
+namespace avk {
+
+int glm_grid(long long n) {
+  const long long nq = (n + 3) / 4;
+  return av::stream_grid(nq, 256, 4, 2048);
+}
+
+void glm_grad(const float* X, long long ld, long long n, int D, const float* y, const float* sw, const float* w,
+              int mode, double* partial, int grid, float* hw, hipStream_t stream) {
+  switch (D) {
+    case 4: launch_glm<4, 4>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
+    case 8: launch_glm<8, 4>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
+    case 16: launch_glm<16, 4>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
+    case 32: launch_glm<32, 2>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
+    default: throw std::runtime_error("glm_grad: D must be 4, 8, 16 or 32");
+  }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace avk

@@ -1,0 +1,221 @@
+"""Linear models (K13 fused GLM gradient), regression, Fisher discriminant, kernel SVM (K12 SMO)."""
+import numpy as np
+import pytest
+import torch
+
+from avenir_amd.models.linear import (DenseSoA, ElasticNet, LinearRegression, LinearSVM, LogisticRegression,
+                                      MODE_HINGE, MODE_LOGISTIC, MODE_SQUARED, fisher_discriminant, fisher_lines,
+                                      glm_gradient)
+from avenir_amd.models.svm import CascadeSVM, SVC, kernel_matrix, smo_batch, smo_reference
+from tests._dist import run_world
+
+
+def _logit_data(n=4000, d=5, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn((n, d), generator=g)
+    w = torch.linspace(-1.5, 1.5, d)
+    p = torch.sigmoid(X @ w + 0.3)
+    y = (torch.rand(n, generator=g) < p).long()
+    return X, y, w
+
+
+def _glm_oracle(X, y, w, mode, sw=None):
+    Xd = torch.cat([torch.ones(X.shape[0], 1), X], 1).double()
+    z = Xd @ w.double()
+    yy = y.double()
+    s = sw.double() if sw is not None else torch.ones_like(yy)
+    if mode == MODE_LOGISTIC:
+        p = torch.sigmoid(z)
+        e, l = yy - p, -(yy * torch.log(p) + (1 - yy) * torch.log(1 - p))
+    elif mode == MODE_SQUARED:
+        e = yy - z
+        l = 0.5 * e * e
+    else:
+        e = torch.where(yy * z < 1, yy, torch.zeros_like(yy))
+        l = (1 - yy * z).clamp_min(0)
+    return Xd.T @ (e * s), (l * s).sum()
+
+
+@pytest.mark.parametrize("mode", [MODE_LOGISTIC, MODE_SQUARED, MODE_HINGE])
+def test_glm_gradient_cpu(mode):
+    X, y, _ = _logit_data(1000, 6)
+    yv = y.float() if mode != MODE_HINGE else (2.0 * y - 1)
+    data = DenseSoA(X)
+    w = torch.randn(7) * 0.3
+    sw = torch.rand(1000)
+    g, loss, _ = glm_gradient(data, data.vec(yv), w, mode, data.vec(sw))
+    rg, rl = _glm_oracle(X, yv, w, mode, sw)
+    assert torch.allclose(g[:7].double(), rg, rtol=1e-6, atol=1e-6)
+    assert float(loss) == pytest.approx(float(rl), rel=1e-6)
+
+
+def test_logistic_regression_newton_and_gd():
+    X, y, w = _logit_data(20000, 4)
+    m = LogisticRegression(solver="newton", max_iter=20).fit(X, y)
+    assert torch.allclose(m.coef[1:].float(), w, atol=0.1)
+    assert float(m.coef[0]) == pytest.approx(0.3, abs=0.1)
+    acc = float((m.predict(X) == y).float().mean())
+    assert acc > 0.7
+    gd = LogisticRegression(solver="gd", lr=2.0, max_iter=300, criteria="iterLimit", tol=0.0).fit(X, y)
+    assert torch.allclose(gd.coef.float(), m.coef.float(), atol=0.05)
+    assert gd.losses[-1] <= gd.losses[0]
+    assert len(gd.coefficient_lines()) == 301
+
+
+def test_logistic_coefficient_file(tmp_path):
+    X, y, _ = _logit_data(3000, 3)
+    m = LogisticRegression(max_iter=5, criteria="iterLimit").fit(X, y)
+    p = tmp_path / "coeff.txt"
+    m.save_coefficients(p)
+    assert len(p.read_text().splitlines()) == 6
+    m2 = LogisticRegression.load_coefficients(p)
+    assert torch.allclose(m2.coef, m.coef.cpu())
+    # convergence criteria stop early
+    m3 = LogisticRegression(max_iter=50, criteria="allBelowThreshold", threshold=0.5).fit(X, y)
+    assert len(m3.history) < 50
+
+
+def _dist_logit(rank, world):
+    X, y, _ = _logit_data(8000, 4, seed=3)
+    lo, hi = rank * 4000, (rank + 1) * 4000
+    m = LogisticRegression(max_iter=15).fit(X[lo:hi], y[lo:hi])
+    return m.coef.tolist()
+
+
+def test_logistic_data_parallel_matches_single():
+    res = run_world(_dist_logit, 2)
+    X, y, _ = _logit_data(8000, 4, seed=3)
+    single = LogisticRegression(max_iter=15).fit(X, y).coef
+    assert np.allclose(res[0], res[1])
+    assert np.allclose(res[0], single.tolist(), atol=1e-6)
+
+
+def test_linear_and_elastic_net():
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn((5000, 6), generator=g)
+    w = torch.tensor([2.0, 0.0, -1.0, 0.0, 0.5, 3.0])
+    y = X @ w + 1.0 + 0.1 * torch.randn(5000, generator=g)
+    lr = LinearRegression().fit(X, y)
+    assert torch.allclose(lr.coef[1:].float(), w, atol=0.01) and float(lr.coef[0]) == pytest.approx(1.0, abs=0.01)
+    assert lr.score(X, y) > 0.99
+    en = ElasticNet(alpha=0.05, l1_ratio=0.9).fit(X, y)
+    # sparse-ish solution: small coefficients shrink to 0
+    assert abs(float(en.coef[2])) < 0.05 and abs(float(en.coef[4])) < 0.05
+    assert float(en.coef[6]) == pytest.approx(3.0, abs=0.2)
+    # pure ridge limit equals closed form
+    en0 = ElasticNet(alpha=0.01, l1_ratio=0.0, max_iter=5000, tol=1e-12).fit(X, y)
+    Xc = X.double() - X.double().mean(0)
+    yc = y.double() - y.double().mean()
+    ridge = torch.linalg.solve(Xc.T @ Xc + 0.01 * 5000 * torch.eye(6, dtype=torch.float64), Xc.T @ yc)
+    assert torch.allclose(en0.coef[1:], ridge, atol=1e-5)
+
+
+def test_linear_svm_hinge():
+    g = torch.Generator().manual_seed(2)
+    X = torch.randn((4000, 3), generator=g)
+    y = ((X @ torch.tensor([1.0, -2.0, 0.5])) > 0.2).long()
+    m = LinearSVM(lam=1e-3, max_iter=300).fit(X, y)
+    assert float((m.predict(X) == y).float().mean()) > 0.97
+
+
+def test_fisher_discriminant():
+    g = torch.Generator().manual_seed(0)
+    x0 = torch.randn((3000, 2), generator=g) + torch.tensor([0.0, 5.0])
+    x1 = torch.randn((1000, 2), generator=g) * 2 + torch.tensor([4.0, 5.5])
+    x = torch.cat([x0, x1])
+    lab = torch.cat([torch.zeros(3000), torch.ones(1000)]).long()
+    r = fisher_discriminant(x, lab)
+    m0, m1 = x0.double().mean(0), x1.double().mean(0)
+    v0, v1 = x0.double().var(0, unbiased=False), x1.double().var(0, unbiased=False)
+    pooled = (v0 * 3000 + v1 * 1000) / 4000
+    lo = np.log(3.0)
+    disc = (m0 + m1) / 2 - lo * pooled / (m0 - m1)
+    assert torch.allclose(r[:, 0], torch.full((2,), lo, dtype=torch.float64))
+    assert torch.allclose(r[:, 1], pooled) and torch.allclose(r[:, 2], disc)
+    assert fisher_lines(r)[0].startswith("0,")
+
+
+def _blobs(n=300, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    r = torch.rand(n, generator=g) * 6.28
+    inner = torch.stack([torch.cos(r), torch.sin(r)], 1) * 1.0 + 0.1 * torch.randn(n, 2, generator=g)
+    outer = torch.stack([torch.cos(r), torch.sin(r)], 1) * 3.0 + 0.1 * torch.randn(n, 2, generator=g)
+    X = torch.cat([inner, outer])
+    y = torch.cat([torch.zeros(n), torch.ones(n)]).long()
+    return X, y
+
+
+def test_smo_reference_kkt():
+    X, y = _blobs(80)
+    K = kernel_matrix(X, X, "rbf", 0.5).double().numpy()
+    ys = np.where(y.numpy() == 1, 1.0, -1.0)
+    a, G, it = smo_reference(K, ys, C=1.0, eps=1e-4)
+    assert abs((a * ys).sum()) < 1e-6                # equality constraint
+    assert (a >= -1e-9).all() and (a <= 1 + 1e-9).all()
+    assert it > 0
+
+
+def test_svc_rbf_and_multiclass():
+    X, y = _blobs(150)
+    m = SVC(kernel="rbf", C=1.0, gamma=0.5).fit(X, y)
+    assert float((m.predict(X) == y).float().mean()) > 0.98
+    assert 0 < len(m.support_indexes()) < X.shape[0]
+    lin = SVC(kernel="linear", C=1.0).fit(X, y)
+    assert float((lin.predict(X) == y).float().mean()) < 0.8     # not linearly separable
+    g = torch.Generator().manual_seed(4)
+    centers = torch.tensor([[0.0, 0.0], [4.0, 0.0], [0.0, 4.0]])
+    lab = torch.randint(0, 3, (300,), generator=g)
+    Xm = centers[lab] + 0.5 * torch.randn(300, 2, generator=g)
+    mc = SVC(kernel="poly", degree=2, gamma=0.5, coef0=1.0, C=2.0).fit(Xm, lab)
+    assert float((mc.predict(Xm) == lab).float().mean()) > 0.97
+
+
+def test_cascade_svm():
+    X, y = _blobs(200, seed=5)
+    perm = torch.randperm(400, generator=torch.Generator().manual_seed(0))
+    X, y = X[perm], y[perm]
+    c = CascadeSVM(shards=4, kernel="rbf", gamma=0.5, C=1.0).fit(X, y)
+    assert float((c.predict(X) == y).float().mean()) > 0.98
+    assert c.n_cascade_sv < 400
+
+
+@pytest.mark.gpu
+def test_glm_kernel_matches_oracle(cuda):
+    for d in (3, 7, 15, 31):
+        X, y, _ = _logit_data(100_003, d, seed=d)
+        data = DenseSoA(X, device=cuda)
+        w = torch.randn(d + 1) * 0.3
+        sw = torch.rand(100_003)
+        for mode in (MODE_LOGISTIC, MODE_SQUARED, MODE_HINGE):
+            yv = y.float() if mode != MODE_HINGE else (2.0 * y - 1)
+            g, loss, h = glm_gradient(data, data.vec(yv), w, mode, data.vec(sw), want_h=True)
+            rg, rl = _glm_oracle(X, yv, w, mode, sw)
+            assert torch.allclose(g[: d + 1].cpu(), rg, rtol=1e-4, atol=1e-2), (d, mode)
+            assert float(loss) == pytest.approx(float(rl), rel=1e-4)
+            assert h.shape[0] == 100_003
+
+
+@pytest.mark.gpu
+def test_logistic_regression_gpu(cuda):
+    X, y, w = _logit_data(200_000, 8)
+    m = LogisticRegression(max_iter=20).fit(X.to(cuda), y.to(cuda))
+    ref = LogisticRegression(max_iter=20).fit(X, y)
+    assert torch.allclose(m.coef.cpu(), ref.coef, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_smo_kernel_matches_reference(cuda):
+    X, y = _blobs(400, seed=2)
+    ys = torch.where(y == 1, 1.0, -1.0)
+    K = kernel_matrix(X, X, "rbf", 0.5)
+    Kb = torch.stack([K, K])
+    yb = torch.stack([ys, -ys])
+    ag, rg, itg = smo_batch(Kb.to(cuda), yb.to(cuda), 1.0, 1e-3)
+    ac, rc, itc = smo_batch(Kb, yb, 1.0, 1e-3)
+    # same optimum: decision values agree
+    fg = (ag.cpu() * yb) @ K - rg.cpu().view(-1, 1)
+    fc = (ac * yb) @ K - rc.view(-1, 1)
+    assert torch.allclose(fg, fc, atol=5e-3)
+    assert (itg.cpu() > 0).all()
+    m = SVC(kernel="rbf", gamma=0.5).fit(X.to(cuda), y.to(cuda))
+    assert float((m.predict(X.to(cuda)).cpu() == y).float().mean()) > 0.98
