@@ -1,0 +1,132 @@
+"""Neural models: MLP (layer spec, graphs), LSTM, autoencoder, RBM imputation, DQN pricing."""
+import pytest
+import torch
+
+from avenir_amd.nn import (AutoEncoder, DQNAgent, FeedForwardNetwork, LstmNetwork, PolicyServer, PricingEnv,
+                           RestrictedBoltzmannMachine, parse_layer_spec)
+from avenir_amd.utils.config import Configuration
+
+
+def _xor_data(n=2000, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand((n, 2), generator=g) * 2 - 1
+    y = ((x[:, 0] * x[:, 1]) > 0).long()
+    return x, y
+
+
+def test_layer_spec():
+    s = parse_layer_spec("8:relu:true:false:0.1,4:tanh:true:true:0,1:none:false:false:0", 5)
+    kinds = [type(m).__name__ for m in s]
+    assert kinds == ["Linear", "BatchNorm1d", "ReLU", "Dropout", "Linear", "Tanh", "BatchNorm1d", "Linear"]
+    with pytest.raises(ValueError):
+        parse_layer_spec("8:relu", 3)
+
+
+def test_mlp_classifier_and_checkpoint(tmp_path):
+    x, y = _xor_data()
+    m = FeedForwardNetwork("16:relu:false:false:0,16:relu:false:false:0,2:none:false:false:0", 2, loss="ce",
+                           optimizer="adam", lr=0.01, batch_size=64, num_iter=60, device="cpu")
+    m.fit(x, y, track_interval=10)
+    acc = m.evaluate_model(x, y, "accuracy")
+    assert acc > 0.95
+    assert m.errors[-1] < m.errors[0]
+    p = tmp_path / "mlp.pt"
+    m.save(p)
+    m2 = FeedForwardNetwork("16:relu:false:false:0,16:relu:false:false:0,2:none:false:false:0", 2, loss="ce",
+                            device="cpu")
+    m2.restore(p)
+    assert torch.equal(m2.predict(x, "binary"), m.predict(x, "binary"))
+
+
+def test_mlp_from_config(tmp_path):
+    rows = []
+    g = torch.Generator().manual_seed(1)
+    X = torch.rand((500, 3), generator=g)
+    t = X @ torch.tensor([1.0, -2.0, 0.5]) + 0.3
+    for i in range(500):
+        rows.append(f"id{i},{X[i, 0]:.5f},{X[i, 1]:.5f},{X[i, 2]:.5f},{t[i]:.5f}")
+    f = tmp_path / "train.csv"
+    f.write_text("\n".join(rows))
+    conf = Configuration({"train.data.fields": "1,2,3,4", "train.data.feature.fields": "0,1,2",
+                          "train.data.out.fields": "3", "train.layer.data": "8:relu:false:false:0,1:none:false:false:0",
+                          "train.optimizer": "adam", "train.opt.learning.rate": "0.01", "train.batch.size": "32",
+                          "train.num.iterations": "80", "train.lossFn": "mse", "common.device": "cpu"}, {})
+    m = FeedForwardNetwork.from_config(conf)
+    x, y = m.prep_data(f)
+    assert x.shape == (500, 3) and y.shape == (500, 1)
+    m.fit(x, y)
+    assert m.evaluate_model(x, y, "rmse") < 0.15
+
+
+def test_lstm_seq_to_one_and_seq():
+    g = torch.Generator().manual_seed(0)
+    n, S = 600, 5
+    seq = torch.rand((n, S * 1), generator=g)
+    y = (seq.sum(1) > S / 2).float()
+    m = LstmNetwork(1, 16, 1, seq_len=S, batch_size=32, out_activation="sigmoid", loss="bce", lr=0.01, num_iter=40,
+                    device="cpu")
+    x = m.to_sequences(seq)
+    m.fit(x, y)
+    acc = float((m.predict(x, "binary") == y.long()).float().mean())
+    assert acc > 0.9
+    ms = LstmNetwork(1, 8, 1, seq_len=S, out_sequence=True, out_activation=None, lr=0.01, num_iter=5, device="cpu")
+    out = ms.predict(ms.to_sequences(seq))
+    assert out.shape == (n, S, 1)
+
+
+def test_autoencoder_anomaly():
+    g = torch.Generator().manual_seed(0)
+    z = torch.randn((2000, 2), generator=g)
+    A = torch.randn((2, 8), generator=g)
+    x = z @ A + 0.01 * torch.randn((2000, 8), generator=g)
+    ae = AutoEncoder(8, [4, 2], ["tanh", None], ["tanh", None], lr=0.01, batch_size=128, num_iter=60, device="cpu")
+    ae.fit(x)
+    assert ae.losses[-1] < ae.losses[0] * 0.2
+    assert ae.encode(x).shape == (2000, 2)
+    out = torch.randn((20, 8), generator=g) * 3
+    assert float(ae.reconstruction_error(out).mean()) > 3 * float(ae.reconstruction_error(x).mean())
+
+
+def test_rbm_imputation():
+    g = torch.Generator().manual_seed(0)
+    # two binary prototypes with noise
+    proto = torch.tensor([[1, 1, 1, 1, 0, 0, 0, 0], [0, 0, 0, 0, 1, 1, 1, 1]], dtype=torch.float32)
+    lab = torch.randint(0, 2, (1000,), generator=g)
+    x = proto[lab]
+    flip = torch.rand(x.shape, generator=g) < 0.03
+    x = torch.where(flip, 1 - x, x)
+    rbm = RestrictedBoltzmannMachine(8, 6, lr=0.05, batch_size=10, num_iter=20, device="cpu").fit(x)
+    miss = torch.zeros_like(x, dtype=torch.bool)
+    miss[:, 0] = True
+    miss[:, 5] = True
+    imp = rbm.impute(x, miss, n_iter=60)
+    truth = proto[lab]
+    acc = float((imp[:, [0, 5]] == truth[:, [0, 5]]).float().mean())
+    assert acc > 0.9
+
+
+def test_dqn_pricing_learns():
+    env = PricingEnv(64, device="cpu", seed=0)
+    s = env.reset()
+    assert s.shape == (64, 41)
+    agent = DQNAgent(env, lr=0.002, gamma=0.8, batch=256, hiddens=(64, 64), eps_decay_steps=300, target_sync=50)
+    base = agent.evaluate()
+    agent.train(iterations=25)
+    after = agent.evaluate()
+    assert after > base * 0.98     # learned policy is at least as good as the initial greedy policy
+    srv = PolicyServer(agent)
+    prices = srv.get_price(env.reset()[:3])
+    assert len(prices) == 3 and all(400 <= p < 500 for p in prices)
+
+
+@pytest.mark.gpu
+def test_mlp_graph_capture_on_gpu(cuda):
+    x, y = _xor_data(4096)
+    m = FeedForwardNetwork("32:relu:false:false:0,32:relu:false:false:0,2:none:false:false:0", 2, loss="ce",
+                           optimizer="adam", lr=0.01, batch_size=256, num_iter=40, device="cuda", graph=True)
+    m.fit(x, y)
+    assert m.evaluate_model(x, y, "accuracy") > 0.95
+    lstm = LstmNetwork(1, 16, 1, seq_len=5, batch_size=64, loss="bce", lr=0.01, num_iter=5, device="cuda")
+    seq = torch.rand((256, 5))
+    lstm.fit(lstm.to_sequences(seq), (seq.sum(1) > 2.5).float())
+    assert lstm.predict(lstm.to_sequences(seq)).device.type == "cuda"
