@@ -1,0 +1,137 @@
+"""Text: preprocessing, n-grams, tf-idf (vs sklearn oracle), summarisers, LDA, word2vec, text NB."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from avenir_amd.text import (BiGram, DocSentences, Doc2Vec, LatentDirichletAllocation, LatentSemSumm,
+                             NonNegMatFactSumm, SumBasicSumm, TermFreqSumm, TextNaiveBayes, TextPreProcessor,
+                             TextRankSumm, TfIdf, Vocabulary, Word2Vec, WordVectorContainer, doc_term_matrix, nmf,
+                             pagerank, porter_stem, split_sentences, tfidf_matrix)
+
+DOC = ("The GPU accelerates matrix multiplication for deep learning workloads. "
+       "Matrix cores on the accelerator perform fused multiply add operations at high throughput. "
+       "Bananas are a popular fruit rich in potassium and eaten around the world. "
+       "Memory bandwidth limits many deep learning kernels that are not compute bound. "
+       "Fruit markets sell bananas, apples and oranges every single morning. "
+       "Kernel fusion reduces memory traffic by keeping intermediate tiles in local memory. "
+       "The weather today is sunny with a light breeze from the west.")
+
+
+def test_porter_stemmer_known_words():
+    cases = {"caresses": "caress", "ponies": "poni", "running": "run", "relational": "relat", "happiness": "happi",
+             "generalization": "gener", "hopping": "hop", "filing": "file", "agreed": "agre", "sky": "sky"}
+    for w, s in cases.items():
+        assert porter_stem(w) == s, w
+
+
+def test_preprocessor_pipeline():
+    pp = TextPreProcessor()
+    t = pp.denoiseText("<p>Hello [note] world &amp; friends</p>")
+    assert "note" not in t and "&" in t
+    toks = pp.tokenize(pp.replaceContractions("I can't run 3 miles, it's 100 degrees!"))
+    n = pp.normalize(toks)
+    assert "cannot" not in n and "three" in n and "one hundred" in n and "miles" in n
+    assert pp.removeShortWords(["a", "abc"], 2) == ["abc"]
+    assert pp.removeLowFreqWords(["a", "a", "b"], 1) == ["a", "a"]
+    assert pp.lemmatizeWords(["cats", "ponies"]) == ["cat", "pony"]
+
+
+def test_ngrams_and_tfidf_vs_sklearn():
+    from sklearn.feature_extraction.text import TfidfVectorizer
+    docs = [["gpu", "matrix", "gpu"], ["matrix", "memory"], ["banana", "fruit", "fruit", "gpu"]]
+    bg = BiGram()
+    for d in docs:
+        bg.countDocNGrams(d)
+    assert bg.counts["gpu matrix"] == 1 and bg.getVocabSize() == 6
+    vocab = Vocabulary(docs)
+    X = doc_term_matrix(docs, vocab)
+    W = tfidf_matrix(X).numpy()
+    sk = TfidfVectorizer(analyzer=lambda d: d, vocabulary=vocab.words).fit_transform(docs).toarray()
+    assert np.allclose(W, sk, atol=1e-6)
+    tf = TfIdf(None, True)
+    for d in docs:
+        tf.countDocWords(d)
+    assert tf.getCount("gpu") == 3
+    v = tf.getVector(["gpu", "memory"], True, True)
+    assert float(v.sum()) == pytest.approx(1.0)
+
+
+def test_sentences_and_summarizers():
+    assert len(split_sentences(DOC)) == 7
+    ds = DocSentences(text=DOC, min_length=5)
+    assert len(ds.getSentences()) == 7
+    for S in (TermFreqSumm(size=3), SumBasicSumm(size=3), LatentSemSumm(num_topics=2, size=3),
+              NonNegMatFactSumm(num_topics=2, size=3), TextRankSumm(size=3), TextRankSumm(size=3, diversify=True)):
+        out = S.summarize(text=DOC)
+        assert len(out) == 3
+        sents = split_sentences(DOC)
+        pos = [sents.index(s) for s, _ in out]
+        assert pos == sorted(pos)           # document order
+    assert len(TermFreqSumm(size=50, by_count=False).summarize(text=DOC)) == 3
+
+
+def test_nmf_and_pagerank():
+    g = torch.Generator().manual_seed(0)
+    W0, H0 = torch.rand((30, 3), generator=g), torch.rand((3, 20), generator=g)
+    W, H = nmf(W0 @ H0, 3, iters=500)
+    assert float(((W @ H) - W0 @ H0).norm() / (W0 @ H0).norm()) < 0.05
+    S = torch.tensor([[0, 1, 1], [1, 0, 0], [1, 0, 0]], dtype=torch.float64)
+    r = pagerank(S)
+    assert float(r.sum()) == pytest.approx(1.0) and int(r.argmax()) == 0
+
+
+def _topic_corpus(n=300, seed=0):
+    rnd = random.Random(seed)
+    topics = [["gpu", "kernel", "memory", "matrix", "cache", "tile"],
+              ["banana", "apple", "fruit", "orange", "market", "juice"],
+              ["rain", "sunny", "weather", "wind", "cloud", "storm"]]
+    docs, labels = [], []
+    for i in range(n):
+        t = rnd.randrange(3)
+        docs.append([rnd.choice(topics[t]) for _ in range(20)])
+        labels.append(t)
+    return docs, labels, topics
+
+
+def test_lda_recovers_topics():
+    docs, labels, topics = _topic_corpus()
+    lda = LatentDirichletAllocation(3, iters=30, seed=1).fit(docs)
+    found = [set(w for w, _ in lda.top_terms(k, 6)) for k in range(3)]
+    for t in topics:
+        assert max(len(set(t) & f) for f in found) >= 5
+    th = lda.doc_topic()
+    assert torch.allclose(th.sum(1), torch.ones(len(docs), dtype=th.dtype))
+    assert lda.transform(docs[:5]).shape == (5, 3)
+
+
+def test_word2vec_and_doc2vec(tmp_path):
+    docs, labels, topics = _topic_corpus(400)
+    w2v = Word2Vec(dim=16, window=3, epochs=5, batch=2048, seed=0).fit(docs)
+    sim = dict(w2v.most_similar("gpu", 5))
+    assert len(set(sim) & set(topics[0])) >= 4
+    p = tmp_path / "w2v.safetensors"
+    w2v.save(p)
+    w2 = Word2Vec.load(p)
+    assert torch.allclose(w2.vector("gpu"), w2v.vector("gpu"))
+    d2v = Doc2Vec(dim=16, epochs=10, seed=0).fit(docs)
+    D = d2v.doc_vectors()
+    D = D - D.mean(0)                       # remove the corpus-frequency direction
+    D = D / D.norm(dim=1, keepdim=True)
+    same = [(D[i] @ D[j]).item() for i in range(20) for j in range(20) if i != j and labels[i] == labels[j]]
+    diff = [(D[i] @ D[j]).item() for i in range(20) for j in range(20) if labels[i] != labels[j]]
+    assert np.mean(same) > np.mean(diff) + 0.2
+
+
+def test_text_nb_and_similarity():
+    docs, labels, _ = _topic_corpus(300, seed=3)
+    nb = TextNaiveBayes().fit(docs[:200], labels[:200])
+    assert nb.accuracy(docs[200:], labels[200:]) > 0.97
+    wc = WordVectorContainer()
+    for d in docs[:6]:
+        wc.addWords(d)
+    S = wc.getPairWiseSimilarity()
+    assert S.shape == (6, 6) and torch.allclose(S.diagonal(), torch.ones(6))
+    J = wc.withSimilarityAlgo("jaccard").getInterSetSimilarity(True, False, 3)
+    assert J.shape == (3, 3)
