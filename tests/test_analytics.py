@@ -1,0 +1,168 @@
+"""Analytics: DataExplorer (vs scipy/numpy oracles), PCA (vs sklearn), streaming PCA, time series,
+ICE / LIME."""
+import math
+
+import numpy as np
+import pytest
+import torch
+from scipy import stats
+
+from avenir_amd.analytics import (PCA, DataExplorer, IncrementalPCA, LimeTabular, PrincipalCompState,
+                                  TimeSeriesGenerator, individual_conditional_expectation, partial_dependence)
+
+
+@pytest.fixture
+def dx():
+    rng = np.random.default_rng(0)
+    d = DataExplorer()
+    d.addListNumericData(rng.normal(5, 2, 2000), "a")
+    d.addListNumericData(rng.normal(5.3, 2, 2000), "b")
+    d.addListNumericData(rng.gamma(2, 2, 2000), "g")
+    d.addCatListData(list(rng.choice(["x", "y", "z"], 2000)), "c")
+    d.addCatListData(list(rng.choice(["p", "q"], 2000)), "c2")
+    return d
+
+
+def test_stats_and_distributions(dx):
+    x = dx.getNumericData("g").numpy()
+    s = dx.getStats("g")
+    assert s["length"] == 2000 and s["mean"] == pytest.approx(x.mean())
+    assert s["std"] == pytest.approx(x.std()) and s["skew"] == pytest.approx(stats.skew(x), rel=1e-6)
+    assert s["kurtosis"] == pytest.approx(stats.kurtosis(x), rel=1e-6)
+    f = dx.getFreqDistr("g", 10)
+    r = stats.relfreq(x, numbins=10)
+    assert np.allclose(f["frequency"], r.frequency, atol=1e-9) and f["lowLimit"] == pytest.approx(r.lowerlimit)
+    assert dx.getPercentile("g", 3.0)["percentile"] == pytest.approx(stats.percentileofscore(x, 3.0))
+    assert dx.getValueAtPercentile("g", 50)["value"] == pytest.approx(np.median(x))
+    assert dx.getEntropy("g")["entropy"] > 0 and dx.getMutualInfo("a", "b")["mutInfo"] >= 0
+    assert dx.isMonotonicallyChanging([1, 2, 3])["monotonic increasing"]
+    assert dx.getCatUniqueValueCounts("c")["counts"][0] > 600
+
+
+def test_correlations_and_tests(dx):
+    a, b = dx.getNumericData("a").numpy(), dx.getNumericData("b").numpy()
+    assert dx.getPearsonCorr("a", "b")["stat"] == pytest.approx(stats.pearsonr(a, b)[0], abs=1e-9)
+    assert dx.getPearsonCorr("a", "b")["pvalue"] == pytest.approx(stats.pearsonr(a, b)[1], rel=1e-6)
+    assert dx.getSpearmanRankCorr("a", "b")["stat"] == pytest.approx(stats.spearmanr(a, b)[0], abs=1e-9)
+    ks = dx.testTwoSampleKs("a", "b")
+    assert ks["stat"] == pytest.approx(stats.ks_2samp(a, b).statistic)
+    for m in ("testTwoSampleStudent", "testTwoSampleMw", "testTwoSampleKw", "testTwoSampleVarLevene",
+              "testTwoSampleVarBartlet", "testTwoSampleScaleAb", "testTwoSampleCvm", "testTwoSampleMedMood",
+              "testTwoSampleAnderson", "testTwoSampleVarFk", "testTwoSampleScaleMood"):
+        r = getattr(dx, m)("a", "b")
+        assert "stat" in r
+    for m in ("testNormalJarqBera", "testNormalShapWilk", "testNormalDagast", "testSkew"):
+        assert getattr(dx, m)("a")["pvalue"] is not None
+    assert dx.testNormalJarqBera("g")["pvalue"] < 1e-6
+    ct = dx.getConTab("c", "c2")
+    assert ct["table"].sum() == 2000
+    assert 0 <= dx.getChiSqCorr("c", "c2")["pvalue"] <= 1
+    same = dx.testTwoSampleZk("a", "a")
+    diff = dx.testTwoSampleZk("a", "g")
+    assert same["pvalue"] > 0.3 and diff["pvalue"] < 0.05
+    assert dx.testTwoSampleZc("a", "g")["pvalue"] < 0.05 and dx.testTwoSampleZa("a", "g")["pvalue"] < 0.05
+
+
+def test_time_series_methods():
+    d = DataExplorer()
+    gen = TimeSeriesGenerator(1000, interval_s=3600, seed=1)
+    s = gen.gen(base=10, trend=0.01, day=[3.0], noise_sd=0.5)[0]
+    d.addListNumericData(s.numpy(), "ts")
+    tr = d.getTrend("ts")
+    assert tr["coeff"][0] == pytest.approx(0.01, abs=0.002)
+    comp = d.getTimeSeriesComponents("ts", "additive", 24)
+    assert comp["seasonalAmp"] == pytest.approx(3.0, rel=0.15)
+    ac = d.getAutoCorr("ts", 30)["autoCorr"]
+    assert ac[0] == pytest.approx(1.0) and ac[24] > ac[12]
+    pac = d.getParAutoCorr("ts", 5)["partAutoCorr"]
+    assert len(pac) == 6
+    ar = gen.ar([0.7], noise_sd=1.0)[0]
+    d.addListNumericData(ar.numpy(), "ar")
+    assert d.getAutoCorr("ar", 2)["autoCorr"][1] == pytest.approx(0.7, abs=0.08)
+    assert d.testStationaryAdf("ar")["stationary"]
+    rw = gen.rw(5.0, 1.0)[0]
+    d.addListNumericData(rw.numpy(), "rw")
+    assert not d.testStationaryKpss("rw")["stationary"]
+    ft = d.getFourierTransform("ts")
+    assert len(ft["amplitude"]) == len(ft["frequency"])
+    so, mask = gen.aol(s, 2.0)
+    assert 5 < int(mask.sum()) < 40
+    assert len(gen.to_lines(s.view(1, -1))) == 1000
+
+
+def test_regressions_and_outliers():
+    rng = np.random.default_rng(2)
+    x = rng.uniform(0, 10, 300)
+    y = 2 * x + 1 + rng.normal(0, 0.1, 300)
+    y[:10] += 50      # outliers
+    d = DataExplorer()
+    d.addListNumericData(x, "x")
+    d.addListNumericData(y, "y")
+    ts = d.fitTheilSenRobustLinearReg("x", "y")
+    assert ts["slope"] == pytest.approx(2.0, abs=0.05)
+    sg = d.fitSiegelRobustLinearReg("x", "y")
+    assert sg["slope"] == pytest.approx(2.0, abs=0.05)
+    pts = rng.normal(0, 1, (500, 2))
+    pts[:5] += 8
+    d.addListNumericData(pts[:, 0], "p0")
+    d.addListNumericData(pts[:, 1], "p1")
+    for m in ("getOutliersWithKnnDistance", "getOutliersWithLocalFactor", "getOutliersWithCovarDeterminant"):
+        out = set(getattr(d, m)(["p0", "p1"], contamination=0.01)["outliers"].tolist())
+        assert {0, 1, 2, 3, 4} <= out
+
+
+def test_save_restore(tmp_path, dx):
+    dx.addNote("a", "normal data")
+    dx.save(tmp_path / "ws")
+    d2 = DataExplorer()
+    d2.restore(tmp_path / "ws")
+    assert d2.getNotes("a") == ["normal data"] and d2.getCatData("c") == dx.getCatData("c")
+    assert torch.equal(d2.getNumericData("g"), dx.getNumericData("g"))
+
+
+def test_pca_vs_sklearn():
+    from sklearn.decomposition import PCA as SKPCA
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(1000, 5)) @ rng.normal(size=(5, 5))
+    p = PCA(3).fit(torch.tensor(X))
+    sk = SKPCA(3).fit(X)
+    assert np.allclose(p.explained_variance_.numpy(), sk.explained_variance_, rtol=1e-8)
+    assert np.allclose(np.abs(p.components_.numpy()), np.abs(sk.components_), atol=1e-8)
+    Z = p.transform(torch.tensor(X))
+    assert np.allclose(np.abs(Z.numpy()), np.abs(sk.transform(X)), atol=1e-6)
+
+
+def test_incremental_pca_tracks_dominant_direction():
+    g = torch.Generator().manual_seed(0)
+    D = 4
+    u = torch.tensor([1.0, 1.0, 0.0, 0.0]) / math.sqrt(2)
+    streams = {}
+    for k in range(3):
+        z = torch.randn((2000, 1), generator=g) * 3
+        streams[f"k{k}"] = z * u + 0.05 * torch.randn((2000, D), generator=g)
+    ip = IncrementalPCA(D, init_hidden=1, forget=0.99)
+    st = ip.update(streams)
+    for k in streams:
+        w = st[k].components[0]
+        assert abs(float(w @ u.double()) / float(w.norm())) > 0.99
+    lines = st["k0"].serialize()
+    back = PrincipalCompState.load(lines)
+    assert back.num_hidden == st["k0"].num_hidden and back.count == 2000
+
+
+def test_ice_and_lime():
+    w = torch.tensor([2.0, -1.0, 0.0])
+    model = lambda X: torch.sigmoid(X @ w)
+    X = torch.randn((5, 3), generator=torch.Generator().manual_seed(0))
+    grid, pred = individual_conditional_expectation(model, X, 0, "float", 1.0, 10)
+    assert grid.shape == (5, 11) and pred.shape == (5, 11)
+    assert bool((pred[:, 1:] >= pred[:, :-1]).all())          # monotone in feature 0
+    pd = partial_dependence(model, X, 1, torch.linspace(-2, 2, 5))
+    assert pd.shape[0] == 5
+    lime = LimeTabular(torch.randn((1000, 3), generator=torch.Generator().manual_seed(1)), ["a", "b", "c"])
+    proba = lambda P: torch.stack([1 - model(P), model(P)], 1)
+    e = lime.explain(torch.zeros(3), proba, label=1, num_samples=4000)
+    names = [n for n, _ in e["explanation"]]
+    assert names[0] == "a" and names[-1] == "c"
+    coefs = dict(e["explanation"])
+    assert coefs["a"] > 0 > coefs["b"]
