@@ -5,7 +5,7 @@ exploratory analytics).
 
 Layers: ``utils`` (config, schema, logging, metrics, checkpoint, tracing),
 ``data`` (CSV -> device columns), ``parallel`` (RCCL collectives), ``ops`` (HIP kernel wrappers),
-``models`` (estimators), ``cli`` and ``serving`` (surfaces).
+``models`` (estimators), ``optimize``, ``nn``, ``text``, ``analytics``, ``cli`` and ``serve`` (surfaces).
 """
 __version__ = "0.1.0"
 
