@@ -267,3 +267,49 @@ def maybe_inject_fault(iteration: int, rank: int | None = None) -> None:
         if mode == "exit":
             os._exit(17)
         raise RuntimeError(f"injected fault at rank {r} iteration {iteration}")
+
+
+class Watchdog:
+    """Failure detector for long collective phases: the training / iteration loop
+    calls ``beat()``; if no beat arrives within ``timeout_s`` the watchdog logs the stall and
+    (``abort=True``) terminates this rank with exit code 75 so ``torchrun --max-restarts`` can
+    relaunch the job, which then resumes from its last iteration checkpoint.  RCCL's own async
+    error handling (``TORCH_NCCL_ASYNC_ERROR_HANDLING=1``, set here if unset) aborts a hung
+    communicator from inside the process group as a second line of defence."""
+
+    def __init__(self, timeout_s: float = 300.0, abort: bool = True, on_stall=None):
+        import threading
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        self.timeout_s, self.abort, self.on_stall = timeout_s, abort, on_stall
+        self._last = time.monotonic()
+        self._stop = threading.Event()
+        self.stalled = False
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def beat(self) -> None:
+        self._last = time.monotonic()
+
+    def _run(self):
+        while not self._stop.wait(min(1.0, self.timeout_s / 4)):
+            if time.monotonic() - self._last > self.timeout_s:
+                self.stalled = True
+                alog.get_logger("comm").error("watchdog: no progress for %.0fs", self.timeout_s)
+                if self.on_stall is not None:
+                    self.on_stall()
+                if self.abort:
+                    os._exit(75)
+                return
+
+    def stop(self) -> None:
+        self._stop.set()
+
+
+def health_check(comm: "Comm | None" = None) -> bool:
+    """One tiny all-reduce that every rank must answer: True when the world is healthy."""
+    comm = comm or get_comm()
+    if not comm.is_distributed:
+        return True
+    t = torch.ones(1, device=comm.device if comm.backend == "nccl" else "cpu")
+    comm.all_reduce(t)
+    return int(t.item()) == comm.world

@@ -173,3 +173,46 @@ def perf_metric(metric: str, actual: Sequence, pred: Sequence, pos: int = 1):
         n = int(max(max(actual), max(pred))) + 1
         return confusion(torch.as_tensor(actual), torch.as_tensor(pred), n)
     raise ValueError(f"unknown metric {metric}")
+
+
+class MetricsRegistry:
+    """Counters (grouped, reference names), gauges and fixed-bucket histograms; ``snapshot()`` is a
+    JSON-able dict, ``all_reduce`` sums counters / histograms and maxes gauges across ranks."""
+
+    def __init__(self, buckets: Sequence[float] = (0.1, 0.5, 1, 5, 10, 50, 100, 500, 1000)):
+        self.counters = Counters()
+        self.gauges: dict[str, float] = {}
+        self.buckets = list(buckets)
+        self.hists: dict[str, list[int]] = {}
+
+    def gauge(self, name: str, value: float) -> None:
+        self.gauges[name] = float(value)
+
+    def observe(self, name: str, value: float) -> None:
+        h = self.hists.setdefault(name, [0] * (len(self.buckets) + 1))
+        i = next((k for k, b in enumerate(self.buckets) if value <= b), len(self.buckets))
+        h[i] += 1
+
+    def snapshot(self) -> dict:
+        return {"counters": self.counters.as_dict(), "gauges": dict(self.gauges),
+                "histograms": {k: {"buckets": self.buckets, "counts": v} for k, v in self.hists.items()}}
+
+    def all_reduce(self, comm) -> None:
+        self.counters.all_reduce(comm)
+        dev = comm.device if comm.backend == "nccl" else "cpu"
+        names = comm.broadcast_object(sorted(self.hists))
+        if names:
+            t = torch.tensor([self.hists.get(n, [0] * (len(self.buckets) + 1)) for n in names], device=dev)
+            comm.all_reduce(t)
+            self.hists = {n: row for n, row in zip(names, t.tolist())}
+        gnames = comm.broadcast_object(sorted(self.gauges))
+        if gnames:
+            g = torch.tensor([self.gauges.get(n, float("-inf")) for n in gnames], dtype=torch.float64, device=dev)
+            comm.all_reduce(g, op="max")
+            self.gauges = dict(zip(gnames, g.tolist()))
+
+    def dumps(self) -> str:
+        return json.dumps(self.snapshot(), indent=1, sort_keys=True)
+
+
+METRICS = MetricsRegistry()

@@ -1,0 +1,105 @@
+"""Infrastructure: checkpoint container (CRC, safetensors compatibility), resume after an injected
+fault, tracing, metrics registry, watchdog, health check."""
+import os
+
+import pytest
+import torch
+
+from avenir_amd.parallel.comm import Watchdog, health_check, maybe_inject_fault
+from avenir_amd.utils import checkpoint as C
+from avenir_amd.utils.metrics import MetricsRegistry
+from avenir_amd.utils.tracing import Tracer
+from tests._dist import run_world
+
+
+def test_container_roundtrip_and_safetensors(tmp_path):
+    t = {"w": torch.randn(3, 4), "counts": torch.arange(10, dtype=torch.int64), "flag": torch.tensor([True, False]),
+         "empty": torch.zeros(0)}
+    p = tmp_path / "a.ckpt"
+    C.save(p, t, {"algorithm": "test", "iteration": 3})
+    back, meta = C.load(p)
+    assert meta == {"algorithm": "test", "iteration": 3}
+    for k in t:
+        assert torch.equal(back[k], t[k])
+    from safetensors.torch import load_file
+    st = load_file(str(p))
+    assert torch.equal(st["w"], t["w"])
+    raw = bytearray(p.read_bytes())
+    raw[-5] ^= 0xFF                                  # corrupt tensor bytes
+    p.write_bytes(bytes(raw))
+    with pytest.raises(IOError):
+        C.load(p)
+
+
+def test_resume_after_injected_fault(tmp_path, monkeypatch):
+    ck = C.IterationCheckpointer(tmp_path, "kmeans")
+    calls = []
+
+    def step(it, st):
+        calls.append(it)
+        maybe_inject_fault(it, rank=0)
+        return {"x": st["x"] + 1}
+    monkeypatch.setenv("AVMI_FAULT_RANK", "0")
+    monkeypatch.setenv("AVMI_FAULT_ITER", "4")
+    # the fault fires once: clear the env after the first failure via a counting wrapper
+    fired = {"n": 0}
+
+    def step_once(it, st):
+        if it == 4 and fired["n"] == 0:
+            fired["n"] += 1
+            return step(it, st)
+        if fired["n"]:
+            monkeypatch.delenv("AVMI_FAULT_RANK", raising=False)
+        return step(it, st)
+    out = C.run_with_recovery(step_once, 8, {"x": torch.zeros(2)}, ck)
+    assert torch.equal(out["x"], torch.full((2,), 8.0))
+    assert calls == [0, 1, 2, 3, 4, 4, 5, 6, 7]          # iterations 0-3 were not redone
+    nxt, t, meta = ck.resume()
+    assert nxt == 8 and meta["algorithm"] == "kmeans"
+
+
+def test_tracer_and_metrics():
+    tr = Tracer().enable()
+    with tr.range("gemm", nbytes=1e6, flops=2e9):
+        torch.randn(256, 256) @ torch.randn(256, 256)
+    with tr.range("gemm"):
+        pass
+    r = tr.report()
+    assert r["gemm"]["calls"] == 2 and "GB_per_s" in r["gemm"] and "TFLOP_per_s" in r["gemm"]
+    m = MetricsRegistry()
+    m.counters.incr("Validation", "TruePositive", 3)
+    m.gauge("hbm_gbps", 4500.0)
+    m.observe("latency_ms", 0.3)
+    m.observe("latency_ms", 7)
+    s = m.snapshot()
+    assert s["counters"]["Validation"]["TruePositive"] == 3 and sum(s["histograms"]["latency_ms"]["counts"]) == 2
+
+
+def test_watchdog_detects_stall():
+    hit = []
+    w = Watchdog(timeout_s=0.3, abort=False, on_stall=lambda: hit.append(1))
+    import time
+    time.sleep(1.2)
+    assert w.stalled and hit
+    w.stop()
+    w2 = Watchdog(timeout_s=5, abort=False)
+    w2.beat()
+    assert not w2.stalled
+    w2.stop()
+
+
+def _metrics_world(rank, world):
+    from avenir_amd.parallel.comm import get_comm
+    m = MetricsRegistry()
+    m.counters.incr("Validation", "Correct", rank + 1)
+    m.gauge("g", float(rank))
+    m.observe("lat", 1.0)
+    m.all_reduce(get_comm())
+    return health_check(), m.snapshot()
+
+
+def test_distributed_metrics_and_health():
+    res = run_world(_metrics_world, 2)
+    ok, snap = res[0]
+    assert ok and snap["counters"]["Validation"]["Correct"] == 3 and snap["gauges"]["g"] == 1.0
+    assert sum(snap["histograms"]["lat"]["counts"]) == 2
