@@ -664,6 +664,29 @@ at::Tensor smo_solve(const at::Tensor& K, const at::Tensor& y, const at::Tensor&
   return iters;
 }
 
+std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,
+                                    int64_t extent, double laplace, double log_floor) {
+  CHECK_DEV(counts);
+  CHECK_DTYPE(counts, at::kLong);
+  TORCH_CHECK(counts.dim() == 2 && counts.is_contiguous(), "counts must be contiguous [C, TB+1]");
+  CHECK_DEV(offs);
+  CHECK_DTYPE(offs, at::kInt);
+  CHECK_DEV(bins);
+  CHECK_DTYPE(bins, at::kInt);
+  const int64_t C = counts.size(0), TB = counts.size(1) - 1, F = bins.numel();
+  TORCH_CHECK(offs.numel() == F && F >= 1 && TB >= 1, "offs/bins mismatch");
+  // extent = offs[F-1] + bins[F-1], computed on the host by the caller (no device sync here, so
+  // the call is HIP-graph capturable)
+  TORCH_CHECK(extent <= TB, "bins exceed count table");
+  DevGuard g(counts.device());
+  auto o = counts.options().dtype(at::kFloat);
+  auto logp = at::empty({C, TB}, o), logfp = at::empty({TB}, o), logprior = at::empty({C}, o);
+  avk::nb_finalize(reinterpret_cast<const long long*>(counts.data_ptr<int64_t>()), (int)C, (int)TB, offs.data_ptr<int>(), bins.data_ptr<int>(), (int)F,
+                   (float)laplace, (float)log_floor, logp.data_ptr<float>(), logfp.data_ptr<float>(),
+                   logprior.data_ptr<float>(), cur_stream(counts));
+  return {logp, logfp, logprior};
+}
+
 // ---------------------------------------------------------------------------------------------
 // host runtime
 
@@ -754,6 +777,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sa_assign", &sa_assign);
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);
+  m.def("nb_finalize", &nb_finalize);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -91,4 +91,8 @@ void glm_grad(const float* X, long long ld, long long n, int D, const float* y, 
 void smo_solve(const float* K, const float* y, const float* diag, float* alpha, float* G, int B, int N, float C,
                float eps, int max_iter, int* iters, hipStream_t stream);
 
+// ---- bayes.hip: model finalisation -----------------------------------------------------------
+void nb_finalize(const long long* counts, int C, int TB, const int* offs, const int* bins, int F, float laplace,
+                 float log_floor, float* logp, float* logfp, float* logprior, hipStream_t stream);
+
 }  // namespace avk

@@ -176,3 +176,14 @@ def test_nb_predict_gpu_matches_cpu(cuda, tmp_path):
     ref_c = nb.predict(t, ref_scale=True)
     ref_g = nbg.predict(tg, ref_scale=True)
     assert torch.allclose(ref_g.prob.cpu(), ref_c.prob, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_nb_finalize_kernel_matches_cpu(cuda, tmp_path):
+    _, t = _churn_table(tmp_path, 5000, seed=4)
+    for laplace in (0.0, 1.0):
+        nbc = NaiveBayes(t.schema, laplace=laplace).fit(t)
+        nbg = NaiveBayes(t.schema, laplace=laplace).fit(t.to(cuda))
+        tc, tg = nbc.tables(), nbg.tables()
+        for k in ("logp", "logfp", "logprior"):
+            assert torch.allclose(tg[k].cpu(), tc[k].float(), atol=1e-5), (k, laplace)
