@@ -1,0 +1,106 @@
+"""Additive time-series forecaster with changepoints, seasonality and holidays.
+
+Reference: ``ProphetForcaster`` (P/unsupv/profo.py:35-286) wraps fbprophet (piecewise-linear trend
+with changepoints, Fourier seasonalities, holiday effects; train / validate / save / forecast).
+fbprophet is not available, so this is a compact re-implementation of the same additive model
+solved as ONE regularised least-squares problem on the device (MAP estimate with a Laplace-like
+L1 prior on changepoint deltas approximated by ridge, no MCMC / uncertainty sampling):
+
+    y(t) = k t + m + sum_j delta_j (t - s_j)_+ + sum_seasons Fourier(t) + sum_h beta_h 1[t in h]
+
+Forecast parity with fbprophet is unpinned.  Save/load use the framework container format.
+"""
+from __future__ import annotations
+
+import math
+from typing import Sequence
+
+import torch
+
+DAY = 86400.0
+
+
+class AdditiveForecaster:
+    def __init__(self, n_changepoints: int = 25, changepoint_range: float = 0.8, changepoint_prior: float = 0.05,
+                 yearly: int = 10, weekly: int = 3, daily: int = 0, seasonality_prior: float = 10.0,
+                 holidays: dict[str, Sequence[float]] | None = None, holiday_window_s: float = DAY, device="cpu"):
+        self.ncp, self.cpr, self.cp_prior = n_changepoints, changepoint_range, changepoint_prior
+        self.seas = [(365.25 * DAY, yearly), (7 * DAY, weekly), (DAY, daily)]
+        self.s_prior = seasonality_prior
+        self.holidays = {k: list(v) for k, v in (holidays or {}).items()}
+        self.hw = holiday_window_s
+        self.device = torch.device(device)
+
+    def _design(self, t: torch.Tensor) -> torch.Tensor:
+        ts = (t - self.t0) / self.scale_t                       # scaled time in [0, 1] over training
+        cols = [ts, torch.ones_like(ts)]
+        for s in self.cps:
+            cols.append((ts - s).clamp_min(0))
+        for period, order in self.seas:
+            for k in range(1, order + 1):
+                ang = 2 * math.pi * k * t / period
+                cols += [torch.sin(ang), torch.cos(ang)]
+        for name, days in self.holidays.items():
+            d = torch.tensor(days, dtype=torch.float64, device=t.device)
+            cols.append(((t.view(-1, 1) - d.view(1, -1)).abs() < self.hw).any(1).double())
+        return torch.stack(cols, 1)
+
+    def fit(self, t, y) -> "AdditiveForecaster":
+        t = torch.as_tensor(t, dtype=torch.float64, device=self.device)
+        y = torch.as_tensor(y, dtype=torch.float64, device=self.device)
+        self.t0, self.scale_t = float(t.min()), float(t.max() - t.min()) or 1.0
+        self.y_scale = float(y.abs().max()) or 1.0
+        self.cps = torch.linspace(0, self.cpr, self.ncp + 2, dtype=torch.float64)[1:-1].tolist() if self.ncp else []
+        X = self._design(t)
+        ys = y / self.y_scale
+        # priors: changepoint deltas ~ N(0, cp_prior^2), seasonal / holiday ~ N(0, s_prior^2)
+        reg = torch.zeros(X.shape[1], dtype=torch.float64, device=self.device)
+        reg[2:2 + len(self.cps)] = 1.0 / self.cp_prior ** 2
+        reg[2 + len(self.cps):] = 1.0 / self.s_prior ** 2
+        # MAP: data term weighted by 1/sigma^2 (sigma from a weakly regularised first pass), so the
+        # priors act relative to the observation noise as in the Bayesian model
+        eye = 1e-9 * torch.eye(X.shape[1], dtype=torch.float64, device=self.device)
+        XtX, Xty = X.T @ X, X.T @ ys
+        b0 = torch.linalg.solve(XtX + 1e-6 * torch.diag(reg) + eye, Xty)
+        s2 = float(((ys - X @ b0) ** 2).mean()) + 1e-12
+        self.beta = torch.linalg.solve(XtX / s2 + torch.diag(reg) + eye, Xty / s2)
+        resid = ys - X @ self.beta
+        self.sigma = float(resid.std()) * self.y_scale
+        return self
+
+    def predict(self, t) -> dict[str, torch.Tensor]:
+        t = torch.as_tensor(t, dtype=torch.float64, device=self.device)
+        X = self._design(t)
+        yhat = (X @ self.beta) * self.y_scale
+        nt = 2 + len(self.cps)
+        trend = (X[:, :nt] @ self.beta[:nt]) * self.y_scale
+        return {"yhat": yhat, "trend": trend, "seasonal": yhat - trend,
+                "yhat_lower": yhat - 1.96 * self.sigma, "yhat_upper": yhat + 1.96 * self.sigma}
+
+    def future_times(self, periods: int, freq_s: float = DAY, last: float | None = None) -> torch.Tensor:
+        start = last if last is not None else self.t0 + self.scale_t
+        return start + freq_s * torch.arange(1, periods + 1, dtype=torch.float64, device=self.device)
+
+    def validate(self, t, y) -> dict[str, float]:
+        p = self.predict(t)["yhat"]
+        y = torch.as_tensor(y, dtype=torch.float64, device=self.device)
+        e = p - y
+        return {"rmse": float((e * e).mean().sqrt()), "mae": float(e.abs().mean()),
+                "mape": float((e.abs() / y.abs().clamp_min(1e-12)).mean() * 100)}
+
+    def save(self, path):
+        from ..utils import checkpoint as C
+        C.save(path, {"beta": self.beta}, {"t0": self.t0, "scale_t": self.scale_t, "y_scale": self.y_scale,
+                                           "cps": self.cps, "sigma": self.sigma, "seas": self.seas,
+                                           "holidays": self.holidays, "hw": self.hw})
+
+    @classmethod
+    def load(cls, path, device="cpu"):
+        from ..utils import checkpoint as C
+        t, m = C.load(path, device)
+        f = cls(device=device)
+        f.beta = t["beta"].double()
+        f.t0, f.scale_t, f.y_scale, f.cps, f.sigma = m["t0"], m["scale_t"], m["y_scale"], m["cps"], m["sigma"]
+        f.seas = [tuple(s) for s in m["seas"]]
+        f.holidays, f.hw = m["holidays"], m["hw"]
+        return f

@@ -587,3 +587,60 @@ class EnsemblePredictiveModel:
             ratio = top2[:, 0] / top2[:, 1].clamp_min(1e-12)
             out = torch.where(ratio >= self.min_odds, out, torch.full_like(out, -1))
         return out
+
+
+class DeterministicPredictiveModel(PredictiveModel):
+    """Label-only predictor (J/model/DeterministicPredictiveModel.java:41-49)."""
+
+    def predict(self, X, actual=None):
+        pred = torch.as_tensor(np.asarray(self.model.predict(X))).long().view(-1)
+        if self.error_counting and actual is not None:
+            a = torch.as_tensor(np.asarray(actual)).long()
+            self.total += len(a)
+            self.errors += int((pred != a).sum())
+            self.fp += int(((pred == 1) & (a == 0)).sum())
+            self.fn += int(((pred == 0) & (a == 1)).sum())
+        return pred
+
+
+class ModelPredictor:
+    """Decision-tree model predictor (J/model/ModelPredictor.java:49-254): one or more tree models
+    (decision-path JSON or native state); several models form a voting ensemble; output modes
+    ``withRecord`` (record + prediction), ``withKId`` (id + prediction), ``withActualClassAttr``
+    (id + actual + prediction); error rate reported at the end.  Batched inference = the K8
+    forest kernel over all trees at once."""
+
+    def __init__(self, trees: list, schema: FeatureSchema, output_mode: str = "withRecord", delim: str = ",",
+                 min_odds_ratio: float | None = None):
+        self.ens = T.TreeEnsemble(trees)
+        self.schema, self.mode, self.delim, self.min_odds = schema, output_mode, delim, min_odds_ratio
+        self.errors = self.total = 0
+
+    @classmethod
+    def from_state_files(cls, paths, schema: FeatureSchema, **kw):
+        import json as _json
+        trees = [T.DecisionTree.from_state(_json.loads(Path(p).read_text()), schema) for p in paths]
+        return cls(trees, schema, **kw)
+
+    def predict_lines(self, t: Table) -> list[str]:
+        pred = self.ens.predict(t, self.min_odds).cpu().tolist()
+        vals = self.ens.class_values
+        ids = t.ids or [str(i) for i in range(t.n)]
+        act = t.labels[: t.n].cpu().tolist() if t.labels is not None else None
+        out = []
+        d = self.delim
+        for i, p in enumerate(pred):
+            pv = vals[p] if 0 <= p < len(vals) else "ambiguous"
+            if act is not None and act[i] < len(vals):
+                self.total += 1
+                self.errors += int(vals[act[i]] != pv)
+            if self.mode == "withKId":
+                out.append(f"{ids[i]}{d}{pv}")
+            elif self.mode == "withActualClassAttr":
+                out.append(f"{ids[i]}{d}{vals[act[i]] if act is not None else ''}{d}{pv}")
+            else:
+                out.append(f"{t.lines[i] if t.lines else ids[i]}{d}{pv}")
+        return out
+
+    def error_rate(self) -> float:
+        return self.errors / max(self.total, 1)

@@ -257,3 +257,92 @@ class CascadeSVM:
 
     def decision_function(self, X):
         return self.model.decision_function(X)
+
+
+class OneClassSVM:
+    """nu one-class SVM (Schölkopf et al.; P/app/ocsvm.py uses sklearn's OneClassSVM) on the same
+    K12 SMO kernel: all labels +1, linear term 0, box [0, 1] with sum(alpha) = nu * n (LIBSVM's
+    scaling), initial alphas = the first nu*n points and gradient G = K alpha."""
+
+    def __init__(self, kernel: str = "rbf", nu: float = 0.1, gamma: float | str = "scale", degree: int = 3,
+                 coef0: float = 0.0, eps: float = 1e-3, max_iter: int = 1_000_000):
+        self.kernel, self.nu, self.gamma, self.degree, self.coef0 = kernel, nu, gamma, degree, coef0
+        self.eps, self.max_iter = eps, max_iter
+
+    def fit(self, X) -> "OneClassSVM":
+        X = torch.as_tensor(X).float()
+        n = X.shape[0]
+        self.g = SVC(gamma=self.gamma)._gamma(X) if not isinstance(self.gamma, (int, float)) else float(self.gamma)
+        K = kernel_matrix(X, X, self.kernel, self.g, self.degree, self.coef0)
+        m = self.nu * n
+        k = int(m)
+        alpha = torch.zeros(n, dtype=torch.float32, device=X.device)
+        alpha[:k] = 1.0
+        if k < n:
+            alpha[k] = m - k
+        G = (K @ alpha).contiguous()
+        y = torch.ones(n, dtype=torch.float32, device=X.device)
+        if X.device.type == "cuda":
+            a = alpha.view(1, -1).contiguous()
+            g = G.view(1, -1).contiguous()
+            Kc = K.unsqueeze(0).contiguous()
+            diag = torch.diagonal(Kc, dim1=1, dim2=2).contiguous()
+            _native.C().smo_solve(Kc, y.view(1, -1).contiguous(), diag, a, g, 1.0, float(self.eps), int(self.max_iter))
+            alpha, G = a[0], g[0]
+        else:
+            alpha, G = _smo_from(K.double().numpy(), np.ones(n), alpha.double().numpy(), G.double().numpy(), 1.0,
+                                 self.eps, self.max_iter)
+            alpha, G = torch.from_numpy(alpha).float(), torch.from_numpy(G).float()
+        self.rho = _rho(alpha.view(1, -1), G.view(1, -1), y.view(1, -1).cpu() if alpha.device.type == "cpu"
+                        else y.view(1, -1), 1.0)[0]
+        sv = alpha > 0
+        self.sv_X, self.coef = X[sv], alpha[sv]
+        return self
+
+    def decision_function(self, X):
+        X = torch.as_tensor(X).float().to(self.sv_X.device)
+        Kx = kernel_matrix(self.sv_X, X, self.kernel, self.g, self.degree, self.coef0)
+        return self.coef @ Kx - self.rho
+
+    def predict(self, X):
+        return torch.where(self.decision_function(X) >= 0, 1, -1)
+
+
+def _smo_from(K, y, alpha, G, C, eps, max_iter):
+    """Host SMO continuing from a given (alpha, G) — same selection / update as smo_reference."""
+    N = y.size
+    QD = np.diag(K).copy()
+    for _ in range(max_iter):
+        up = np.where(y > 0, alpha < C, alpha > 0)
+        low = np.where(y > 0, alpha > 0, alpha < C)
+        if not up.any():
+            break
+        v = np.where(up, -y * G, -np.inf)
+        i = int(np.argmax(v))
+        gmax = v[i]
+        yg = np.where(low, y * G, -np.inf)
+        gmax2 = yg.max()
+        bd = gmax + yg
+        a = np.where(QD[i] + QD - 2 * K[i] > 0, QD[i] + QD - 2 * K[i], 1e-12)
+        gain = np.where(low & (bd > 0), bd * bd / a, -np.inf)
+        j = int(np.argmax(gain))
+        if gmax + gmax2 < eps or not np.isfinite(gain[j]):
+            break
+        oi, oj = alpha[i], alpha[j]
+        quad = max(QD[i] + QD[j] - 2 * K[i, j], 1e-12)
+        delta = (G[i] - G[j]) / quad          # y_i == y_j == 1
+        s = oi + oj
+        ai, aj = oi - delta, oj + delta
+        if s > C:
+            if ai > C:
+                ai, aj = C, s - C
+        elif aj < 0:
+            aj, ai = 0.0, s
+        if s > C:
+            if aj > C:
+                aj, ai = C, s - C
+        elif ai < 0:
+            ai, aj = 0.0, s
+        alpha[i], alpha[j] = ai, aj
+        G += K[i] * (ai - oi) + K[j] * (aj - oj)
+    return alpha, G

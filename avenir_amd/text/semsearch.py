@@ -1,0 +1,114 @@
+"""Semantic document search over token / sentence embeddings.
+
+Reference: ``ssearch.py`` (P/app/ssearch.py:32-346) embeds documents with spaCy-transformers BERT
+and compares a query with nine document-similarity algorithms: token max, token avg-max, token
+max-avg, token avg, token median, sentence avg, sentence median, sentence max, plus whole-document
+average.  spaCy / BERT are not available, so embeddings come from any encoder (our
+:class:`~avenir_amd.text.models.Word2Vec`, an external model's vectors, or hashing vectors);
+the similarity algorithms are implemented exactly as batched device reductions: all
+query-token x document-token cosine similarities of the whole corpus are ONE GEMM, followed by
+segmented max / mean / median reductions per document.
+"""
+from __future__ import annotations
+
+from typing import Callable, Sequence
+
+import torch
+
+from .preprocess import clean_tokens, split_sentences
+
+ALGOS = ("tokenMax", "tokenAvMax", "tokenMaxAv", "tokenAv", "tokenMed", "sentAv", "sentMed", "sentMax", "docAv")
+
+
+def _norm(x):
+    return x / x.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+
+
+class SemanticSearch:
+    def __init__(self, embed_tokens: Callable[[Sequence[str]], torch.Tensor], device="cpu"):
+        """``embed_tokens(list of tokens) -> [n, d]`` embedding matrix."""
+        self.embed = embed_tokens
+        self.device = torch.device(device)
+        self.docs: list[str] = []
+        self.tok_emb: list[torch.Tensor] = []
+        self.sent_emb: list[torch.Tensor] = []
+
+    def add(self, text: str):
+        toks = clean_tokens(text)
+        e = torch.as_tensor(self.embed(toks)).float().to(self.device) if toks else torch.zeros((0, 1))
+        self.tok_emb.append(_norm(e))
+        sents = [clean_tokens(s) for s in split_sentences(text)]
+        se = [torch.as_tensor(self.embed(s)).float().mean(0) for s in sents if s]
+        self.sent_emb.append(_norm(torch.stack(se).to(self.device)) if se else e[:0])
+        self.docs.append(text)
+        return self
+
+    def _flat(self, embs):
+        lens = torch.tensor([e.shape[0] for e in embs], device=self.device)
+        cat = torch.cat([e for e in embs if e.shape[0]], 0)
+        seg = torch.repeat_interleave(torch.arange(len(embs), device=self.device), lens)
+        return cat, seg, lens
+
+    def scores(self, query: str, algo: str = "tokenAvMax") -> torch.Tensor:
+        """Similarity of the query to every document: [n_docs]."""
+        qt = clean_tokens(query)
+        q = _norm(torch.as_tensor(self.embed(qt)).float().to(self.device))          # [m, d]
+        if algo.startswith("sent"):
+            cat, seg, lens = self._flat(self.sent_emb)
+            qv = _norm(q.mean(0, keepdim=True))
+            s = (cat @ qv.T).view(-1)                                               # [S]
+            return self._segment(s, seg, lens, {"sentAv": "mean", "sentMed": "median", "sentMax": "max"}[algo])
+        if algo == "docAv":
+            cat, seg, lens = self._flat(self.tok_emb)
+            D = torch.zeros((len(self.docs), cat.shape[1]), device=self.device).index_add_(0, seg, cat)
+            return (_norm(D) @ _norm(q.mean(0, keepdim=True)).T).view(-1)
+        cat, seg, lens = self._flat(self.tok_emb)
+        S = q @ cat.T                                                               # [m, T] one GEMM
+        nd = len(self.docs)
+        if algo == "tokenMax":
+            return self._segment(S.max(0).values, seg, lens, "max")
+        if algo == "tokenAvMax":     # per query token: max over doc tokens; then average
+            mx = torch.full((S.shape[0], nd), -2.0, device=self.device).scatter_reduce(
+                1, seg.view(1, -1).expand_as(S), S, "amax", include_self=True)
+            return mx.mean(0)
+        if algo == "tokenMaxAv":     # per query token: mean over doc tokens; then max
+            sm = torch.zeros((S.shape[0], nd), device=self.device).index_add_(1, seg, S)
+            return (sm / lens.clamp_min(1).view(1, -1)).max(0).values
+        if algo == "tokenAv":
+            return self._segment(S.mean(0), seg, lens, "mean")
+        if algo == "tokenMed":
+            return self._segment(S.median(0).values, seg, lens, "median")
+        raise ValueError(f"unknown algorithm {algo}")
+
+    def _segment(self, v, seg, lens, how):
+        nd = len(self.docs)
+        if how == "max":
+            return torch.full((nd,), -2.0, device=self.device).scatter_reduce(0, seg, v, "amax", include_self=True)
+        if how == "mean":
+            return torch.zeros(nd, device=self.device).index_add_(0, seg, v) / lens.clamp_min(1)
+        out = torch.empty(nd, device=self.device)
+        o = 0
+        for i, L in enumerate(lens.tolist()):
+            out[i] = v[o:o + L].median() if L else -2.0
+            o += L
+        return out
+
+    def search(self, query: str, algo: str = "tokenAvMax", top: int = 5) -> list[tuple[int, float]]:
+        s = self.scores(query, algo)
+        idx = torch.argsort(s, descending=True)[:top].tolist()
+        return [(i, float(s[i])) for i in idx]
+
+
+def hashing_embedder(dim: int = 256, seed: int = 0):
+    """Deterministic random-projection token vectors (a stand-in encoder when no trained model is
+    available): each token hashes to a fixed gaussian vector."""
+    import hashlib
+
+    def emb(tokens):
+        out = []
+        for t in tokens:
+            h = int(hashlib.md5(f"{seed}:{t}".encode()).hexdigest()[:8], 16)
+            g = torch.Generator().manual_seed(h)
+            out.append(torch.randn(dim, generator=g))
+        return torch.stack(out) if out else torch.zeros((0, dim))
+    return emb
