@@ -181,3 +181,32 @@ def test_misc_helpers():
     assert M.terms_hyp_space([2, 3], 2) == 3 * 4 * 2
     assert M.disjunctive_hyp_space([2, 2, 2], 2, 3, 1) == 8 * 2
     assert M.conjunctive_hyp_space_ln([2, 2], 2, 2) == pytest.approx(4 * math.log(2) + math.log(2))
+
+
+def test_score_model_generator(tmp_path):
+    from avenir_amd.data.generators import class_conditional, loan_approval
+    from avenir_amd.models.bayes import NaiveBayes
+    m = loan_approval()
+    cols, label, score = m.generate(20000, seed=1)
+    assert 0.2 < float(label.float().mean()) < 0.8
+    assert float(cols["income"].min()) >= 50 and float(cols["income"].max()) <= 160
+    lines = m.lines(500, seed=2)
+    assert len(lines) == 500 and lines[0].count(",") == 12
+    # the generated data is learnable: NB over the schema beats the majority rate
+    f = tmp_path / "loan.csv"
+    f.write_text("\n".join(m.lines(5000, seed=3)) + "\n")
+    sch = m.schema("approved")
+    for fd in sch["fields"]:
+        if fd.get("dataType") == "int":
+            fd["bucketWidth"] = max(1, int((fd["max"] or 100) - (fd["min"] or 0)) // 10) if fd["max"] else 5
+            fd["min"] = fd["min"] or 0
+            fd["max"] = fd["max"] or 60
+    t = load_csv(f, FeatureSchema.from_json(sch))
+    nb = NaiveBayes(t.schema).fit(t)
+    r = nb.predict(t)
+    acc = float((r.pred.long() == t.labels[: t.n].long()).float().mean())
+    maj = max(float(t.labels[: t.n].float().mean()), 1 - float(t.labels[: t.n].float().mean()))
+    assert acc > maj + 0.05
+    cols2, y = class_conditional([60, 40], {"status": [("cat", ["m", "s"], [100, 20]), ("cat", ["m", "s"], [20, 100])],
+                                            "income": [("num", 120, 10), ("num", 80, 10)]}, 4000)
+    assert float(cols2["income"][y == 0].mean()) > float(cols2["income"][y == 1].mean()) + 30
