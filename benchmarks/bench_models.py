@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""End-to-end model training / inference throughput on one GPU (JSON line per model).
+
+    python benchmarks/bench_models.py --only rf,gbt,kmeans,logit,svm,knn,sa,mlp
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def timed(fn, reps=1):
+    fn()                                  # warm-up (compiles / caches)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, out
+
+
+def _numeric_table(n, d, seed=0, classes=2):
+    from avenir_amd.data.table import Table, pad16
+    from avenir_amd.models.supervised import array_schema
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    X = torch.randn((d, pad16(n)), device="cuda", generator=g)
+    w = torch.randn(d, device="cuda", generator=g)
+    y = ((w @ X[:, :n]) + 0.5 * torch.randn(n, device="cuda", generator=g) > 0).to(torch.uint8)
+    lab = torch.full((pad16(n),), 255, dtype=torch.uint8, device="cuda")
+    lab[:n] = y
+    schema = array_schema(d, [0, 1])
+    t = Table(schema, n, torch.zeros((0, pad16(n)), dtype=torch.uint8, device="cuda"), [], X,
+              schema.feature_fields, lab, schema.find_class_attr_field())
+    return t
+
+
+def bench_rf(a):
+    from avenir_amd.models.tree import RandomForest, TreeParams
+    n, d = a.rows, 16
+    t = _numeric_table(n, d)
+    for trees, depth in ((10, 8),):
+        p = TreeParams(binary=True, stopping="maxDepth", max_depth=depth, sub_sampling="withReplace",
+                       attr_selection="randomAll", max_bins=32)
+        sec, rf = timed(lambda: RandomForest(t.schema, trees, p, "sqrt").fit(t))
+        emit(model="random_forest", rows=n, features=d, trees=trees, depth=depth, seconds=sec,
+             rows_x_trees_per_s=n * trees / sec)
+        ps, _ = timed(lambda: rf.predict_proba(t), 3)
+        emit(model="random_forest_predict", rows=n, trees=trees, seconds=ps, rows_per_s=n / ps)
+
+
+def bench_gbt(a):
+    from avenir_amd.models.tree import GBTParams, GradientBoostedTrees
+    n, d = a.rows, 16
+    t = _numeric_table(n, d, 1)
+    p = GBTParams(n_estimators=50, learning_rate=0.1, max_depth=4, max_bins=64)
+    sec, _ = timed(lambda: GradientBoostedTrees(t.schema, p).fit(t))
+    emit(model="gbt", rows=n, features=d, rounds=50, depth=4, seconds=sec, rows_x_rounds_per_s=n * 50 / sec)
+
+
+def bench_kmeans(a):
+    from avenir_amd.models.cluster import KMeans
+    n, d, k = a.rows, 16, 16
+    X = torch.randn((n, d), device="cuda")
+    sec, km = timed(lambda: KMeans(k, n_init=1, max_iter=20, tol=0).fit(X))
+    it = km.best[k].iterations
+    emit(model="kmeans", rows=n, dim=d, k=k, iterations=it, seconds=sec, rows_x_iters_per_s=n * it / sec)
+
+
+def bench_logit(a):
+    from avenir_amd.models.linear import LogisticRegression
+    n, d = a.rows * 4, 15
+    X = torch.randn((n, d), device="cuda")
+    y = (X[:, 0] - X[:, 1] > 0).float()
+    sec, m = timed(lambda: LogisticRegression(max_iter=10, criteria="iterLimit", tol=0).fit(X, y))
+    emit(model="logistic_regression_newton", rows=n, features=d, iterations=10, seconds=sec,
+         rows_x_iters_per_s=n * 10 / sec)
+
+
+def bench_svm(a):
+    from avenir_amd.models.svm import SVC
+    n = 16384
+    X = torch.randn((n, 8), device="cuda")
+    y = (X[:, 0] * X[:, 1] > 0).long()
+    sec, m = timed(lambda: SVC("rbf", C=1.0, gamma=0.5).fit(X, y))
+    emit(model="svm_rbf_smo", rows=n, seconds=sec, iterations=m.iters, support_vectors=len(m.support_))
+
+
+def bench_knn(a):
+    from avenir_amd.models.knn import NearestNeighbor
+    n, d = 1 << 20, 16
+    X = torch.randn((n, d), device="cuda")
+    y = (X[:, 0] > 0).long()
+    Q = torch.randn((1 << 16, d), device="cuda")
+    nn = NearestNeighbor(k=10).fit(X, y, 2)
+    sec, _ = timed(lambda: nn.predict(Q))
+    emit(model="knn_classify", train_rows=n, queries=Q.shape[0], dim=d, k=10, seconds=sec,
+         pairs_per_s=n * Q.shape[0] / sec)
+
+
+def bench_sa(a):
+    from avenir_amd.optimize import AssignmentDomain, SimulatedAnnealing
+    g = torch.Generator().manual_seed(0)
+    d = AssignmentDomain(torch.rand((64, 16), generator=g) * 100,
+                         (torch.rand((64, 64), generator=g) < 0.05)).to("cuda")
+    sec, r = timed(lambda: SimulatedAnnealing(d, n_chains=1 << 16, iters=1000, t0=5.0).run())
+    emit(model="simulated_annealing_chains", chains=1 << 16, iters=1000, seconds=sec,
+         moves_per_s=(1 << 16) * 1000 / sec, best_cost=r.best_cost)
+
+
+def bench_mlp(a):
+    from avenir_amd.nn import FeedForwardNetwork
+    n = 1 << 18
+    X = torch.randn((n, 16), device="cuda")
+    y = (X[:, 0] * X[:, 1] > 0).long()
+    for graph in (False, True):
+        m = FeedForwardNetwork("64:relu:false:false:0,64:relu:false:false:0,2:none:false:false:0", 16, loss="ce",
+                               optimizer="adam", lr=1e-3, batch_size=1024, num_iter=1, device="cuda", graph=graph)
+        sec, _ = timed(lambda: m.fit(X, y, num_iter=2))
+        emit(model="mlp_train", graph=graph, rows=n, batch=1024, epochs=2, seconds=sec,
+             steps_per_s=2 * (n // 1024) / sec)
+
+
+BENCHES = {"rf": bench_rf, "gbt": bench_gbt, "kmeans": bench_kmeans, "logit": bench_logit, "svm": bench_svm,
+           "knn": bench_knn, "sa": bench_sa, "mlp": bench_mlp}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--rows", type=int, default=1 << 24)
+    a = ap.parse_args()
+    for name, fn in BENCHES.items():
+        if a.only and name not in a.only.split(","):
+            continue
+        try:
+            fn(a)
+        except Exception as e:  # noqa: BLE001
+            emit(model=name, error=f"{type(e).__name__}: {e}")
+
+
+if __name__ == "__main__":
+    main()
