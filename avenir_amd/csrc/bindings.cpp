@@ -687,6 +687,25 @@ std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& 
   return {logp, logfp, logprior};
 }
 
+at::Tensor weighted_gram(const at::Tensor& X, int64_t n, int64_t D, const c10::optional<at::Tensor>& h) {
+  CHECK_DEV(X);
+  CHECK_DTYPE(X, at::kFloat);
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && X.size(0) >= D && D >= 1 && D <= 32, "X [>=D, ld], D <= 32");
+  TORCH_CHECK(n >= 0 && n <= X.size(1), "n exceeds ld");
+  const float* hp = nullptr;
+  if (h.has_value() && h->defined()) {
+    CHECK_DEV((*h));
+    CHECK_DTYPE((*h), at::kFloat);
+    TORCH_CHECK(h->is_contiguous() && h->numel() >= n, "h must cover n rows");
+    hp = h->data_ptr<float>();
+  }
+  DevGuard g(X.device());
+  const int grid = avk::gram_grid(n);
+  auto partial = at::empty({(int64_t)grid * 4, 32, 32}, X.options());
+  avk::weighted_gram(X.data_ptr<float>(), X.size(1), n, (int)D, hp, partial.data_ptr<float>(), grid, cur_stream(X));
+  return partial.to(at::kDouble).sum(0).narrow(0, 0, D).narrow(1, 0, D);
+}
+
 // ---------------------------------------------------------------------------------------------
 // host runtime
 
@@ -778,6 +797,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);
   m.def("nb_finalize", &nb_finalize);
+  m.def("weighted_gram", &weighted_gram);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -95,4 +95,8 @@ void smo_solve(const float* K, const float* y, const float* diag, float* alpha, 
 void nb_finalize(const long long* counts, int C, int TB, const int* offs, const int* bins, int F, float laplace,
                  float log_floor, float* logp, float* logfp, float* logprior, hipStream_t stream);
 
+int gram_grid(long long n);
+void weighted_gram(const float* X, long long ld, long long n, int D, const float* h, float* partial, int grid,
+                   hipStream_t stream);
+
 }  // namespace avk

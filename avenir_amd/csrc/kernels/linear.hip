@@ -92,6 +92,47 @@ __global__ __launch_bounds__(256) void glm_grad_kernel(const float* __restrict__
   }
 }
 
+// Weighted Gram matrix G = sum_i h_i x_i x_i^T for D <= 32 (Newton / IRLS Hessian, ridge
+// normal equations) on the matrix cores: each wave stages a 32-feature x 64-row tile of the
+// column-major X in LDS (coalesced 256-B feature rows), then issues 32
+// v_mfma_f32_32x32x2_f32 with A[i][k] = h_k x_k[i], B[k][j] = x_k[j] (k = row).  Each wave keeps
+// its own 32x32 accumulator across all its tiles and writes it once; partials are summed in fp64
+// on the device.  Replaces a skinny [D, n] x [n, D] library GEMM (K = n) that hipBLASLt rejects.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256) void gram_mfma_kernel(const float* __restrict__ X, long long ld, long long n, int D,
+                                                        const float* __restrict__ h, float* __restrict__ partial) {
+  __shared__ float tile[4][32][65];  // per wave: [feature][row] (+1 pad against bank conflicts)
+  __shared__ float hs[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long ntiles = (n + 63) / 64;
+  const long long gw = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (long long t = gw; t < ntiles; t += nw) {
+    const long long row = t * 64 + lane;
+    const bool ok = row < n;
+    hs[w][lane] = ok ? (h ? h[row] : 1.f) : 0.f;
+    for (int i = 0; i < 32; ++i) tile[w][i][lane] = (ok && i < D) ? X[(long long)i * ld + row] : 0.f;
+    __builtin_amdgcn_s_waitcnt(0);  // LDS writes of this wave visible to its own lanes (wave-private tile)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 8
+    for (int kk = 0; kk < 32; ++kk) {
+      const int r = 2 * kk + (lane >> 5);
+      const float xv = tile[w][lane & 31][r];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv * hs[w][r], xv, acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  float* out = partial + gw * 1024;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    out[row * 32 + (lane & 31)] = acc[r];
+  }
+}
+
 template <int D, int VEC>
 void launch_glm(const float* X, long long ld, long long n, const float* y, const float* sw, const float* w, int mode,
                 double* partial, int grid, float* hw, hipStream_t stream) {
@@ -116,6 +157,15 @@ void glm_grad(const float* X, long long ld, long long n, int D, const float* y, 
     case 32: launch_glm<32, 2>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
     default: throw std::runtime_error("glm_grad: D must be 4, 8, 16 or 32");
   }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int gram_grid(long long n) { return av::stream_grid((n + 63) / 64, 4, 1, 1024); }
+
+void weighted_gram(const float* X, long long ld, long long n, int D, const float* h, float* partial, int grid,
+                   hipStream_t stream) {
+  if (D > 32) throw std::runtime_error("weighted_gram: D must be <= 32");
+  gram_mfma_kernel<<<grid, 256, 0, stream>>>(X, ld, n, D, h, partial);
   AV_HIP_CHECK(hipGetLastError());
 }
 

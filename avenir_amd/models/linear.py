@@ -137,8 +137,11 @@ class LogisticRegression:
             g = g[:D].double().clone()
             buf = torch.cat([g, loss.view(1).double()])
             if self.solver == "newton":
-                Xr = data.X[:D, : data.n]
-                H = (Xr * h.view(1, -1)) @ Xr.T                                   # [D, D] GEMM
+                if data.device.type == "cuda" and D <= 32:
+                    H = _native.C().weighted_gram(data.X, data.n, D, h.contiguous())   # MFMA Gram
+                else:
+                    Xr = data.X[:D, : data.n]
+                    H = (Xr * h.view(1, -1)) @ Xr.T                               # [D, D] GEMM
                 buf = torch.cat([buf, H.double().reshape(-1)])
             if comm.is_distributed:
                 buf = comm.all_reduce(buf)

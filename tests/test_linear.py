@@ -184,13 +184,16 @@ def test_glm_kernel_matches_oracle(cuda):
     for d in (3, 7, 15, 31):
         X, y, _ = _logit_data(100_003, d, seed=d)
         data = DenseSoA(X, device=cuda)
-        w = torch.randn(d + 1) * 0.3
-        sw = torch.rand(100_003)
+        gen = torch.Generator().manual_seed(100 + d)
+        w = torch.randn(d + 1, generator=gen) * 0.3
+        sw = torch.rand(100_003, generator=gen)
         for mode in (MODE_LOGISTIC, MODE_SQUARED, MODE_HINGE):
             yv = y.float() if mode != MODE_HINGE else (2.0 * y - 1)
             g, loss, h = glm_gradient(data, data.vec(yv), w, mode, data.vec(sw), want_h=True)
             rg, rl = _glm_oracle(X, yv, w, mode, sw)
-            assert torch.allclose(g[: d + 1].cpu(), rg, rtol=1e-4, atol=1e-2), (d, mode)
+            # hinge: rows with y z within float rounding of the margin may flip their indicator
+            rtol = 1e-3 if mode == MODE_HINGE else 1e-4
+            assert torch.allclose(g[: d + 1].cpu(), rg, rtol=rtol, atol=1e-2), (d, mode)
             assert float(loss) == pytest.approx(float(rl), rel=1e-4)
             assert h.shape[0] == 100_003
 
@@ -219,3 +222,20 @@ def test_smo_kernel_matches_reference(cuda):
     assert (itg.cpu() > 0).all()
     m = SVC(kernel="rbf", gamma=0.5).fit(X.to(cuda), y.to(cuda))
     assert float((m.predict(X.to(cuda)).cpu() == y).float().mean()) > 0.98
+
+
+@pytest.mark.gpu
+def test_weighted_gram_mfma(cuda):
+    from avenir_amd import _native
+    for d, n in ((5, 1000), (16, 100_003), (32, 4097)):
+        g = torch.Generator().manual_seed(d)
+        X = torch.randn((d, n), generator=g)
+        h = torch.rand(n, generator=g)
+        ld = ((n + 15) // 16) * 16
+        Xp = torch.zeros((d, ld))
+        Xp[:, :n] = X
+        G = _native.C().weighted_gram(Xp.to(cuda), n, d, h.to(cuda)).cpu()
+        ref = (X.double() * h.double()) @ X.double().T
+        assert torch.allclose(G, ref, rtol=1e-4, atol=1e-3 * n ** 0.5), (d, n)
+        G1 = _native.C().weighted_gram(Xp.to(cuda), n, d, None).cpu()
+        assert torch.allclose(G1, X.double() @ X.double().T, rtol=1e-4, atol=1e-3 * n ** 0.5)
