@@ -99,4 +99,9 @@ int gram_grid(long long n);
 void weighted_gram(const float* X, long long ld, long long n, int D, const float* h, float* partial, int grid,
                    hipStream_t stream);
 
+// ---- cluster.hip (K16) ---------------------------------------------------------------------
+int kmeans_grid(long long n);
+void kmeans_step(const float* X, long long n, int D, const float* C, int k, int* assign, float* partial,
+                 double* sse_partial, int grid, hipStream_t stream);
+
 }  // namespace avk

@@ -19,6 +19,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from .. import _native
 from ..ops import distance as dist
 from ..parallel.comm import Comm, get_comm
 
@@ -75,15 +76,40 @@ class KMeans:
             C = comm.broadcast(C.contiguous(), 0)
         return C.contiguous()
 
+    def _step(self, X: torch.Tensor, Xp: torch.Tensor | None, C: torch.Tensor, k: int):
+        """One Lloyd pass -> (sums f64 [k, D], counts [k], sse f64 [1]).  GPU: the fused K16 kernel
+        (assignment + SSE + partial sums, data read once); CPU: distance + accumulate oracle."""
+        if Xp is not None:
+            D = X.shape[1]
+            Cp = torch.zeros((k, Xp.shape[1]), dtype=torch.float32, device=X.device)
+            Cp[:, :D] = C
+            sums, counts, sse, _ = _native.C().kmeans_step(Xp, Cp.contiguous(), False)
+            return sums[:, :D].contiguous(), counts.round().long(), sse.view(1)
+        d, idx = dist.knn(X, C, 1, "sqeuclidean")
+        sums, counts = dist.cluster_accumulate(X, idx[:, 0].int(), k)
+        return sums, counts, d[:, 0].double().sum().view(1)
+
+    @staticmethod
+    def _padded(X: torch.Tensor, k: int) -> torch.Tensor | None:
+        if not X.is_cuda or not _native.available():
+            return None
+        D = X.shape[1]
+        Dp = next((p for p in (2, 4, 8, 16, 32, 64) if p >= D), None)
+        if Dp is None or k * (2 * Dp + 2) * 4 > 64 * 1024:
+            return None
+        if Dp == D:
+            return X
+        Xp = torch.zeros((X.shape[0], Dp), dtype=torch.float32, device=X.device)
+        Xp[:, :D] = X
+        return Xp
+
     def _run(self, X: torch.Tensor, k: int, seed: int) -> KMeansRun:
         comm = self.comm or get_comm()
         C = self._init_centroids(X, k, seed)
         run = KMeansRun(k, seed, C)
+        Xp = self._padded(X, k)
         for it in range(self.max_iter):
-            d, idx = dist.knn(X, C, 1, "sqeuclidean")
-            assign = idx[:, 0].int()
-            sums, counts = dist.cluster_accumulate(X, assign, k)
-            sse = d[:, 0].double().sum().view(1)
+            sums, counts, sse = self._step(X, Xp, C, k)
             if comm.is_distributed:
                 comm.all_reduce(sums)
                 comm.all_reduce(counts)
@@ -96,9 +122,7 @@ class KMeans:
             if move <= self.tol:
                 run.converged = True
                 break
-        d, idx = dist.knn(X, C, 1, "sqeuclidean")
-        sse = d[:, 0].double().sum().view(1)
-        sums, counts = dist.cluster_accumulate(X, idx[:, 0].int(), k)
+        sums, counts, sse = self._step(X, Xp, C, k)
         if comm.is_distributed:
             comm.all_reduce(sse)
             comm.all_reduce(counts)

@@ -480,6 +480,22 @@ class DecisionTreeBuilder:
                     M[si, g, b] = 1.0
             seg_tensors.append(M.to(dev))
 
+        # binary-threshold features are scored together: one segmented cumsum over their bins
+        bin_f = [f for f, fs in enumerate(space) if fs.binary]
+        if bin_f:
+            bcols = torch.cat([torch.arange(offs[f], offs[f] + bins[f]) for f in bin_f]).to(dev)
+            bfeat = torch.cat([torch.full((bins[f],), f, dtype=torch.long) for f in bin_f]).to(dev)
+            # position of each bin's feature start / end inside the gathered block
+            starts, pos = [], 0
+            for f in bin_f:
+                starts.append(pos)
+                pos += bins[f]
+            bstart = torch.cat([torch.full((bins[f],), st, dtype=torch.long) for f, st in zip(bin_f, starts)]).to(dev)
+            bend = torch.cat([torch.full((bins[f],), st + bins[f] - 1, dtype=torch.long)
+                              for f, st in zip(bin_f, starts)]).to(dev)
+            bthr = torch.cat([torch.arange(bins[f]) for f in bin_f]).to(dev)      # threshold index within feature
+            bvalid = bthr < torch.cat([torch.full((bins[f],), bins[f] - 1) for f in bin_f]).to(dev)
+
         node = torch.full((t.ld,), -1, dtype=torch.int32, device=dev)
         node[: t.n] = 0
         # root
@@ -506,14 +522,24 @@ class DecisionTreeBuilder:
                     cand_masks[a, f] = True
             cand_masks = cand_masks.to(dev)
             score_blocks, index = [], []  # index: (feature, split id)
+            if bin_f:
+                hb = hist_t[:, bcols, :]                                    # [A, NB, C]
+                cs = torch.cumsum(hb, 1)
+                base = torch.where((bstart > 0).view(1, -1, 1), cs[:, (bstart - 1).clamp_min(0), :],
+                                   torch.zeros_like(cs))
+                left = cs - base
+                right = cs[:, bend, :] - base - left
+                bseg = torch.stack([left, right], 2)                        # [A, NB, 2, C]
+                cnt = bseg.sum(-1)
+                stat = impurity(bseg, p.algorithm)
+                wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)
+                ok = ((cnt > 0).sum(-1) >= 2) & bvalid.view(1, -1) & cand_masks[:, bfeat]
+                score_blocks.append(torch.where(ok, wavg, torch.full_like(wavg, math.inf)))
+                index.extend(zip(bfeat.tolist(), bthr.tolist()))
             for f, fs in enumerate(space):
                 hb = hist_t[:, offs[f]: offs[f] + bins[f], :]     # [A, B, C]
                 if fs.binary:
-                    left = torch.cumsum(hb, 1)[:, :-1, :]          # [A, B-1, C]
-                    tot = hb.sum(1, keepdim=True)
-                    right = tot - left
-                    seg = torch.stack([left, right], 2)            # [A, S, 2, C]
-                    ns = seg.shape[1]
+                    continue
                 else:
                     M = seg_tensors[f]
                     if M.shape[0] == 0:
@@ -545,20 +571,22 @@ class DecisionTreeBuilder:
             else:
                 best_val, best = scores.min(1)
                 best, best_val = best.cpu(), best_val.cpu()
-            # segment counts of the chosen splits, one gather per node
-            seg_counts = []
+            # segment counts of the chosen splits (binary: one gather for every node, one copy)
+            seg_counts: list = [None] * A
+            bvals = best_val.tolist()
+            bidx = best.tolist()
+            bin_rows = [a for a in range(A) if math.isfinite(bvals[a]) and space[index[bidx[a]][0]].binary]
+            if bin_rows:
+                ra = torch.tensor(bin_rows, device=dev)
+                cols = torch.tensor([bidx[a] for a in bin_rows], device=dev)       # position in the binary block
+                ch = bseg[ra, cols].round().long().cpu()                          # [R, 2, C]
+                for j, a in enumerate(bin_rows):
+                    seg_counts[a] = ch[j]
             for a in range(A):
-                if not math.isfinite(float(best_val[a])):
-                    seg_counts.append(None)
-                    continue
-                f, s = index[int(best[a])]
-                hb = hist_t[a, offs[f]: offs[f] + bins[f], :]
-                if space[f].binary:
-                    left = hb[: s + 1].sum(0)
-                    seg_counts.append(torch.stack([left, hb.sum(0) - left]))
-                else:
-                    seg_counts.append(torch.einsum("gb,bc->gc", seg_tensors[f][s], hb))
-            seg_counts = [None if x is None else x.round().long().cpu() for x in seg_counts]
+                if math.isfinite(bvals[a]) and seg_counts[a] is None:
+                    f, s = index[bidx[a]]
+                    hb = hist_t[a, offs[f]: offs[f] + bins[f], :]
+                    seg_counts[a] = torch.einsum("gb,bc->gc", seg_tensors[f][s], hb).round().long().cpu()
             # ---- create children ----
             new_frontier: list[int] = []
             max_bins = max(bins)
@@ -843,28 +871,22 @@ class GradientBoostedTrees:
                 values[gi] = leaf_val[a]
             if depth == p.max_depth:
                 break
-            best_gain = torch.full((A,), -math.inf, dtype=torch.float64, device=dev)
-            best_f = torch.full((A,), -1, dtype=torch.long, device=dev)
-            best_b = torch.full((A,), -1, dtype=torch.long, device=dev)
             parent = (G * G / (H + p.l2).clamp_min(1e-12))
-            for f, b in enumerate(bins[:-1]):
-                hb = hist[:, offs[f]: offs[f] + b, :]
-                left = torch.cumsum(hb, 1)[:, :-1, :]
-                ft = hb.sum(1, keepdim=True)
-                right = ft - left
-                gl, hl, gr, hr = left[..., 0], left[..., 1], right[..., 0], right[..., 1]
-                gain = gl * gl / (hl + p.l2).clamp_min(1e-12) + gr * gr / (hr + p.l2).clamp_min(1e-12) \
-                    - parent.unsqueeze(1)
-                ok = (hl > 1e-12) & (hr > 1e-12)
-                gain = torch.where(ok, gain, torch.full_like(gain, -math.inf))
-                if gain.shape[1] == 0:
-                    continue
-                gv, gb = gain.max(1)
-                upd = gv > best_gain
-                best_gain = torch.where(upd, gv, best_gain)
-                best_f = torch.where(upd, torch.full_like(best_f, f), best_f)
-                best_b = torch.where(upd, gb, best_b)
-            bg, bf, bb = best_gain.cpu().tolist(), best_f.cpu().tolist(), best_b.cpu().tolist()
+            # all thresholds of all features at once: segmented cumsum over the feature bins
+            sc = self._scan
+            cs = torch.cumsum(hist[:, : sc["nb"], :], 1)                          # [A, NB, 2]
+            base = torch.where((sc["start"] > 0).view(1, -1, 1), cs[:, (sc["start"] - 1).clamp_min(0), :],
+                               torch.zeros_like(cs))
+            left = cs - base
+            right = cs[:, sc["end"], :] - base - left
+            gl, hl, gr, hr = left[..., 0], left[..., 1], right[..., 0], right[..., 1]
+            gain = gl * gl / (hl + p.l2).clamp_min(1e-12) + gr * gr / (hr + p.l2).clamp_min(1e-12) \
+                - parent.unsqueeze(1)
+            ok = (hl > 1e-12) & (hr > 1e-12) & sc["valid"].view(1, -1)
+            gain = torch.where(ok, gain, torch.full_like(gain, -math.inf))
+            best_gain, best_pos = gain.max(1)
+            sel = torch.stack([best_gain, sc["feat"][best_pos].double(), sc["thr"][best_pos].double()]).cpu()
+            bg, bf, bb = sel[0].tolist(), [int(v) for v in sel[1].tolist()], [int(v) for v in sel[2].tolist()]
             max_bins = max(bins)
             split_feat = torch.full((A,), -1, dtype=torch.int32)
             segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
@@ -903,6 +925,17 @@ class GradientBoostedTrees:
         codes = _with_total_row(codes, t.n)
         bins = [fs.n_bins for fs in self.space] + [1]
         n, dev = t.n, t.device
+        # static index tensors of the vectorised threshold scan (features are contiguous in the histogram)
+        fb = bins[:-1]
+        offs0 = list(itertools.accumulate([0] + fb[:-1]))
+        self._scan = {
+            "nb": sum(fb),
+            "feat": torch.cat([torch.full((b,), f, dtype=torch.long) for f, b in enumerate(fb)]).to(dev),
+            "thr": torch.cat([torch.arange(b) for b in fb]).to(dev),
+            "start": torch.cat([torch.full((b,), o, dtype=torch.long) for o, b in zip(offs0, fb)]).to(dev),
+            "end": torch.cat([torch.full((b,), o + b - 1, dtype=torch.long) for o, b in zip(offs0, fb)]).to(dev),
+            "valid": torch.cat([torch.arange(b) < b - 1 for b in fb]).to(dev),
+        }
         C = t.n_classes
         self.n_classes = C
         y = t.labels[:n].long().clamp_max(C - 1)

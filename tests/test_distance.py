@@ -152,3 +152,32 @@ def test_kmeans_gpu_matches_cpu(cuda):
     assert kg.best[4].sse == pytest.approx(kc.best[4].sse, rel=1e-3)
     s, c = D.cluster_accumulate(X.to(cuda), torch.randint(0, 4, (20000,), generator=g).int().to(cuda), 4)
     assert int(c.sum()) == 20000
+
+
+@pytest.mark.gpu
+def test_kmeans_step_kernel_matches_oracle(cuda):
+    from avenir_amd import _native
+    from avenir_amd.models.cluster import KMeans
+    for D, k in ((2, 3), (16, 16), (5, 40)):
+        g = torch.Generator().manual_seed(D + k)
+        X = torch.randn((50_000, D), generator=g)
+        C = torch.randn((k, D), generator=g)
+        Dp = next(p for p in (2, 4, 8, 16, 32, 64) if p >= D)
+        Xp = torch.zeros((X.shape[0], Dp))
+        Xp[:, :D] = X
+        Cp = torch.zeros((k, Dp))
+        Cp[:, :D] = C
+        sums, counts, sse, assign = _native.C().kmeans_step(Xp.to(cuda), Cp.to(cuda), True)
+        d2 = torch.cdist(X.double(), C.double()) ** 2
+        ref_a = d2.argmin(1)
+        agree = float((assign.cpu().long() == ref_a).float().mean())
+        assert agree > 0.999
+        a = assign.cpu().long()
+        ref_sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, a, X.double())
+        assert torch.allclose(sums.cpu()[:, :D], ref_sums, atol=1e-2, rtol=1e-4)
+        assert torch.equal(counts.cpu().round().long(), torch.bincount(a, minlength=k))
+        assert float(sse) == pytest.approx(float(d2.gather(1, a.view(-1, 1)).sum()), rel=1e-4)
+    X = torch.randn((20_000, 3), generator=torch.Generator().manual_seed(1))
+    cpu = KMeans(4, n_init=1, max_iter=10, seed=3).fit(X)
+    gpu = KMeans(4, n_init=1, max_iter=10, seed=3).fit(X.to(cuda))
+    assert gpu.best[4].sse == pytest.approx(cpu.best[4].sse, rel=1e-3)
