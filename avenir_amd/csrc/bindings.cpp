@@ -706,27 +706,36 @@ at::Tensor weighted_gram(const at::Tensor& X, int64_t n, int64_t D, const c10::o
   return partial.to(at::kDouble).sum(0).narrow(0, 0, D).narrow(1, 0, D);
 }
 
-std::vector<at::Tensor> kmeans_step(const at::Tensor& X, const at::Tensor& C, bool want_assign) {
+std::vector<at::Tensor> kmeans_step(const at::Tensor& X, const at::Tensor& C, const std::vector<int64_t>& ks,
+                                    bool want_assign) {
   CHECK_DEV(X);
   CHECK_DTYPE(X, at::kFloat);
   CHECK_DEV(C);
   CHECK_DTYPE(C, at::kFloat);
-  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && C.dim() == 2 && C.is_contiguous(), "X [n, D], C [k, D] contiguous");
-  const int64_t n = X.size(0), D = X.size(1), k = C.size(0);
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && C.dim() == 2 && C.is_contiguous(), "X [n, D], C [K, D] contiguous");
+  const int64_t n = X.size(0), D = X.size(1), K = C.size(0), R = (int64_t)ks.size();
   TORCH_CHECK(C.size(1) == D, "centroid dimension mismatch");
   TORCH_CHECK(D == 2 || D == 4 || D == 8 || D == 16 || D == 32 || D == 64, "D must be padded to 2/4/8/16/32/64");
-  TORCH_CHECK(k >= 1 && k * (2 * D + 2) * 4 <= 64 * 1024, "k * D too large for the LDS-resident kernel");
+  TORCH_CHECK(R >= 1 && R <= 16, "1..16 runs per launch");
+  std::vector<int> off(R + 1, 0);
+  for (int64_t r = 0; r < R; ++r) {
+    TORCH_CHECK(ks[r] >= 1, "every run needs k >= 1");
+    off[r + 1] = off[r] + (int)ks[r];
+  }
+  TORCH_CHECK(off[R] == K, "sum(ks) must equal the number of centroid rows");
+  TORCH_CHECK(K * (2 * D + 2) * 4 <= 64 * 1024, "total centroids * D too large for the LDS-resident kernel");
   DevGuard g(X.device());
+  auto roff = at::tensor(std::vector<int>(off.begin(), off.end()), at::TensorOptions().dtype(at::kInt)).to(X.device());
   const int grid = avk::kmeans_grid(n);
-  auto partial = at::empty({grid, k, D + 1}, X.options());
-  auto ssep = at::empty({grid}, X.options().dtype(at::kDouble));
+  auto partial = at::empty({grid, K, D + 1}, X.options());
+  auto ssep = at::empty({grid, R}, X.options().dtype(at::kDouble));
   at::Tensor assign;
-  if (want_assign) assign = at::empty({n}, X.options().dtype(at::kInt));
-  avk::kmeans_step(X.data_ptr<float>(), n, (int)D, C.data_ptr<float>(), (int)k,
+  if (want_assign) assign = at::empty({R, n}, X.options().dtype(at::kInt));
+  avk::kmeans_step(X.data_ptr<float>(), n, (int)D, C.data_ptr<float>(), roff.data_ptr<int>(), (int)R, (int)K,
                    want_assign ? assign.data_ptr<int>() : nullptr, partial.data_ptr<float>(), ssep.data_ptr<double>(),
                    grid, cur_stream(X));
-  auto tot = partial.to(at::kDouble).sum(0);  // [k, D + 1]
-  return {tot.narrow(1, 0, D), tot.select(1, D), ssep.sum(), want_assign ? assign : at::Tensor()};
+  auto tot = partial.to(at::kDouble).sum(0);  // [K, D + 1]
+  return {tot.narrow(1, 0, D), tot.select(1, D), ssep.sum(0), want_assign ? assign : at::Tensor()};
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -101,7 +101,7 @@ void weighted_gram(const float* X, long long ld, long long n, int D, const float
 
 // ---- cluster.hip (K16) ---------------------------------------------------------------------
 int kmeans_grid(long long n);
-void kmeans_step(const float* X, long long n, int D, const float* C, int k, int* assign, float* partial,
-                 double* sse_partial, int grid, hipStream_t stream);
+void kmeans_step(const float* X, long long n, int D, const float* C, const int* roff, int R, int K, int* assign,
+                 float* partial, double* sse_partial, int grid, hipStream_t stream);
 
 }  // namespace avk

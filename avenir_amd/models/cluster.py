@@ -76,26 +76,34 @@ class KMeans:
             C = comm.broadcast(C.contiguous(), 0)
         return C.contiguous()
 
-    def _step(self, X: torch.Tensor, Xp: torch.Tensor | None, C: torch.Tensor, k: int):
-        """One Lloyd pass -> (sums f64 [k, D], counts [k], sse f64 [1]).  GPU: the fused K16 kernel
-        (assignment + SSE + partial sums, data read once); CPU: distance + accumulate oracle."""
+    def _step(self, X: torch.Tensor, Xp: torch.Tensor | None, Cs: list[torch.Tensor]):
+        """One Lloyd pass for a GROUP of runs -> per run (sums f64 [k, D], counts [k], sse f64 [1]).
+        GPU: ONE launch of the fused K16 kernel for all runs (data read once); CPU: oracle."""
         if Xp is not None:
             D = X.shape[1]
-            Cp = torch.zeros((k, Xp.shape[1]), dtype=torch.float32, device=X.device)
-            Cp[:, :D] = C
-            sums, counts, sse, _ = _native.C().kmeans_step(Xp, Cp.contiguous(), False)
-            return sums[:, :D].contiguous(), counts.round().long(), sse.view(1)
-        d, idx = dist.knn(X, C, 1, "sqeuclidean")
-        sums, counts = dist.cluster_accumulate(X, idx[:, 0].int(), k)
-        return sums, counts, d[:, 0].double().sum().view(1)
+            ks = [c.shape[0] for c in Cs]
+            Cp = torch.zeros((sum(ks), Xp.shape[1]), dtype=torch.float32, device=X.device)
+            Cp[:, :D] = torch.cat(Cs)
+            sums, counts, sse, _ = _native.C().kmeans_step(Xp, Cp.contiguous(), ks, False)
+            out, o = [], 0
+            for r, k in enumerate(ks):
+                out.append((sums[o:o + k, :D].contiguous(), counts[o:o + k].round().long(), sse[r:r + 1]))
+                o += k
+            return out
+        res = []
+        for C in Cs:
+            d, idx = dist.knn(X, C, 1, "sqeuclidean")
+            sums, counts = dist.cluster_accumulate(X, idx[:, 0].int(), C.shape[0])
+            res.append((sums, counts, d[:, 0].double().sum().view(1)))
+        return res
 
     @staticmethod
-    def _padded(X: torch.Tensor, k: int) -> torch.Tensor | None:
+    def _padded(X: torch.Tensor) -> torch.Tensor | None:
         if not X.is_cuda or not _native.available():
             return None
         D = X.shape[1]
         Dp = next((p for p in (2, 4, 8, 16, 32, 64) if p >= D), None)
-        if Dp is None or k * (2 * Dp + 2) * 4 > 64 * 1024:
+        if Dp is None:
             return None
         if Dp == D:
             return X
@@ -103,41 +111,75 @@ class KMeans:
         Xp[:, :D] = X
         return Xp
 
-    def _run(self, X: torch.Tensor, k: int, seed: int) -> KMeansRun:
-        comm = self.comm or get_comm()
-        C = self._init_centroids(X, k, seed)
-        run = KMeansRun(k, seed, C)
-        Xp = self._padded(X, k)
-        for it in range(self.max_iter):
-            sums, counts, sse = self._step(X, Xp, C, k)
-            if comm.is_distributed:
-                comm.all_reduce(sums)
-                comm.all_reduce(counts)
-                comm.all_reduce(sse)
-            newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1).view(-1, 1), C.double()).float()
-            move = float(((newC - C) ** 2).sum(1).sqrt().max())
-            C = newC
-            run.history.append(float(sse))
-            run.iterations = it + 1
-            if move <= self.tol:
-                run.converged = True
-                break
-        sums, counts, sse = self._step(X, Xp, C, k)
-        if comm.is_distributed:
-            comm.all_reduce(sse)
-            comm.all_reduce(counts)
-        run.centroids, run.sse, run.counts = C, float(sse), counts
-        return run
+    def _groups(self, specs: list[tuple[int, int]], Dp: int | None) -> list[list[int]]:
+        """Pack runs into launch groups: <= 16 runs and total centroids within the LDS budget."""
+        groups, cur, tot = [], [], 0
+        cap = (64 * 1024) // (4 * (2 * Dp + 2)) if Dp else 1 << 30
+        for i, (k, _) in enumerate(specs):
+            if Dp is not None and k > cap:
+                raise ValueError(f"k={k} too large for the LDS-resident k-means kernel at D={Dp}")
+            if cur and (len(cur) == 16 or tot + k > cap or Dp is None):
+                groups.append(cur)
+                cur, tot = [], 0
+            cur.append(i)
+            tot += k
+        if cur:
+            groups.append(cur)
+        return groups
 
     def fit(self, X: torch.Tensor) -> "KMeans":
+        """All (k, init) runs advance together (S/cluster/KmeansCluster.scala keys by
+        (numClusters, initGroup)): one kernel launch per iteration per group of runs."""
+        comm = self.comm or get_comm()
         X = X.float().contiguous()
-        self.runs = []
-        for k in self.ks:
-            for r in range(self.n_init):
-                run = self._run(X, k, self.seed * 1009 + k * 31 + r)
-                self.runs.append(run)
-                if k not in self.best or run.sse < self.best[k].sse:
-                    self.best[k] = run
+        Xp = self._padded(X)
+        specs = [(k, self.seed * 1009 + k * 31 + r) for k in self.ks for r in range(self.n_init)]
+        runs = [KMeansRun(k, sd, self._init_centroids(X, k, sd)) for k, sd in specs]
+        self.best = {}
+        for grp in self._groups(specs, Xp.shape[1] if Xp is not None else None):
+            active = list(grp)
+            for it in range(self.max_iter):
+                res = self._step(X, Xp, [runs[i].centroids for i in active])
+                if comm.is_distributed:
+                    flat = torch.cat([torch.cat([s.view(-1), c.double().view(-1), e]) for s, c, e in res])
+                    flat = comm.all_reduce(flat)
+                    o, red = 0, []
+                    for s, c, e in res:
+                        a, b = s.numel(), c.numel()
+                        red.append((flat[o:o + a].view_as(s), flat[o + a:o + a + b].round().long(),
+                                    flat[o + a + b:o + a + b + 1]))
+                        o += a + b + 1
+                    res = red
+                moves = []
+                for i, (sums, counts, sse) in zip(active, res):
+                    C = runs[i].centroids
+                    newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1).view(-1, 1),
+                                       C.double()).float()
+                    moves.append(((newC - C) ** 2).sum(1).sqrt().max())
+                    runs[i].centroids = newC
+                    runs[i].history.append(sse)
+                    runs[i].iterations = it + 1
+                mv = torch.stack(moves).cpu().tolist()          # one host sync per iteration per group
+                still = []
+                for i, m in zip(active, mv):
+                    if m <= self.tol:
+                        runs[i].converged = True
+                    else:
+                        still.append(i)
+                active = still
+                if not active:
+                    break
+            final = self._step(X, Xp, [runs[i].centroids for i in grp])
+            for i, (sums, counts, sse) in zip(grp, final):
+                if comm.is_distributed:
+                    sse = comm.all_reduce(sse)
+                    counts = comm.all_reduce(counts)
+                runs[i].sse, runs[i].counts = float(sse), counts
+                runs[i].history = [float(h) for h in runs[i].history]
+        self.runs = runs
+        for r in runs:
+            if r.k not in self.best or r.sse < self.best[r.k].sse:
+                self.best[r.k] = r
         return self
 
     @property

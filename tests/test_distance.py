@@ -167,7 +167,8 @@ def test_kmeans_step_kernel_matches_oracle(cuda):
         Xp[:, :D] = X
         Cp = torch.zeros((k, Dp))
         Cp[:, :D] = C
-        sums, counts, sse, assign = _native.C().kmeans_step(Xp.to(cuda), Cp.to(cuda), True)
+        sums, counts, sse, assign = _native.C().kmeans_step(Xp.to(cuda), Cp.to(cuda), [k], True)
+        assign = assign[0]
         d2 = torch.cdist(X.double(), C.double()) ** 2
         ref_a = d2.argmin(1)
         agree = float((assign.cpu().long() == ref_a).float().mean())
@@ -178,6 +179,17 @@ def test_kmeans_step_kernel_matches_oracle(cuda):
         assert torch.equal(counts.cpu().round().long(), torch.bincount(a, minlength=k))
         assert float(sse) == pytest.approx(float(d2.gather(1, a.view(-1, 1)).sum()), rel=1e-4)
     X = torch.randn((20_000, 3), generator=torch.Generator().manual_seed(1))
-    cpu = KMeans(4, n_init=1, max_iter=10, seed=3).fit(X)
-    gpu = KMeans(4, n_init=1, max_iter=10, seed=3).fit(X.to(cuda))
-    assert gpu.best[4].sse == pytest.approx(cpu.best[4].sse, rel=1e-3)
+    cpu = KMeans([3, 4, 5], n_init=2, max_iter=10, seed=3).fit(X)
+    gpu = KMeans([3, 4, 5], n_init=2, max_iter=10, seed=3).fit(X.to(cuda))     # 6 runs, one launch / iter
+    for k in (3, 4, 5):
+        assert gpu.best[k].sse == pytest.approx(cpu.best[k].sse, rel=1e-3)
+    # multi-run launch equals single-run launches
+    C1 = torch.randn((3, 4), generator=torch.Generator().manual_seed(5))
+    C2 = torch.randn((7, 4), generator=torch.Generator().manual_seed(6))
+    X4 = torch.randn((30_000, 4), generator=torch.Generator().manual_seed(7)).to(cuda)
+    s_all, c_all, e_all, a_all = _native.C().kmeans_step(X4, torch.cat([C1, C2]).to(cuda), [3, 7], True)
+    s1, c1, e1, a1 = _native.C().kmeans_step(X4, C1.to(cuda), [3], True)
+    s2, c2, e2, a2 = _native.C().kmeans_step(X4, C2.to(cuda), [7], True)
+    assert torch.equal(a_all[0], a1[0]) and torch.equal(a_all[1], a2[0])
+    assert torch.allclose(s_all, torch.cat([s1, s2]), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(e_all, torch.cat([e1, e2]), rtol=1e-6)
