@@ -57,7 +57,9 @@ class KMeans:
         g.manual_seed(seed)
         # sample up to 64k points overall for seeding
         m = min(X.shape[0], max(1, 65536 // max(comm.world, 1)))
-        sel = torch.randperm(X.shape[0], generator=g)[:m].to(X.device)
+        # sample without a full permutation of the data (O(m), not O(n)); duplicates are harmless
+        sel = (torch.randperm(X.shape[0], generator=g)[:m] if X.shape[0] <= 4 * m
+               else torch.randint(0, X.shape[0], (m,), generator=g)).to(X.device)
         S = X[sel].float()
         if comm.is_distributed:
             S = comm.all_gather_v(S)
@@ -267,7 +269,7 @@ def hopkins(X: torch.Tensor, sample: int = 100, seed: int = 0) -> float:
     n = X.shape[0]
     m = min(sample, n - 1)
     X = X.float()
-    idx = torch.randperm(n, generator=g)[:m].to(X.device)
+    idx = (torch.randperm(n, generator=g)[:m] if n <= 4 * m else torch.randint(0, n, (m,), generator=g)).to(X.device)
     lo, hi = X.min(0).values, X.max(0).values
     U = lo + (hi - lo) * torch.rand((m, X.shape[1]), generator=g).to(X.device)
     ud, _ = dist.knn(U, X, 1, "euclidean")
