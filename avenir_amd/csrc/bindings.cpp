@@ -706,36 +706,162 @@ at::Tensor weighted_gram(const at::Tensor& X, int64_t n, int64_t D, const c10::o
   return partial.to(at::kDouble).sum(0).narrow(0, 0, D).narrow(1, 0, D);
 }
 
-std::vector<at::Tensor> kmeans_step(const at::Tensor& X, const at::Tensor& C, const std::vector<int64_t>& ks,
-                                    bool want_assign) {
-  CHECK_DEV(X);
-  CHECK_DTYPE(X, at::kFloat);
-  CHECK_DEV(C);
-  CHECK_DTYPE(C, at::kFloat);
-  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && C.dim() == 2 && C.is_contiguous(), "X [n, D], C [K, D] contiguous");
-  const int64_t n = X.size(0), D = X.size(1), K = C.size(0), R = (int64_t)ks.size();
-  TORCH_CHECK(C.size(1) == D, "centroid dimension mismatch");
+// k-means (K16).  Centroids in pair layout C2 [Kp/2, D, 2] (every run padded to an even count),
+// norms Cn [Kp] (+inf for padding), run offsets roff [R + 1] (device copy + host copy h_roff).
+std::vector<at::Tensor> kmeans_assign(const at::Tensor& X, const at::Tensor& C2, const at::Tensor& Cn,
+                                      const at::Tensor& roff, const std::vector<int64_t>& h_roff, bool want_assign) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &C2, &Cn}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  CHECK_DEV(roff);
+  CHECK_DTYPE(roff, at::kInt);
+  TORCH_CHECK(X.dim() == 2, "X must be [n, D]");
+  const int64_t n = X.size(0), D = X.size(1), R = (int64_t)h_roff.size() - 1;
   TORCH_CHECK(D == 2 || D == 4 || D == 8 || D == 16 || D == 32 || D == 64, "D must be padded to 2/4/8/16/32/64");
   TORCH_CHECK(R >= 1 && R <= 16, "1..16 runs per launch");
-  std::vector<int> off(R + 1, 0);
-  for (int64_t r = 0; r < R; ++r) {
-    TORCH_CHECK(ks[r] >= 1, "every run needs k >= 1");
-    off[r + 1] = off[r] + (int)ks[r];
-  }
-  TORCH_CHECK(off[R] == K, "sum(ks) must equal the number of centroid rows");
-  TORCH_CHECK(K * (2 * D + 2) * 4 <= 64 * 1024, "total centroids * D too large for the LDS-resident kernel");
+  TORCH_CHECK(roff.numel() == R + 1, "roff must have R + 1 entries");
+  TORCH_CHECK(h_roff[0] == 0, "roff[0] must be 0");
+  for (int64_t r = 0; r < R; ++r)
+    TORCH_CHECK(h_roff[r + 1] >= h_roff[r] + 2 && h_roff[r + 1] % 2 == 0, "every run needs an even count >= 2");
+  const int64_t K = h_roff[R];
+  TORCH_CHECK(K <= 4096, "at most 4096 centroids per launch");
+  TORCH_CHECK(C2.numel() == K * D && Cn.numel() == K, "C2 must hold Kp * D values and Cn Kp norms");
   DevGuard g(X.device());
-  auto roff = at::tensor(std::vector<int>(off.begin(), off.end()), at::TensorOptions().dtype(at::kInt)).to(X.device());
   const int grid = avk::kmeans_grid(n);
   auto partial = at::empty({grid, K, D + 1}, X.options());
   auto ssep = at::empty({grid, R}, X.options().dtype(at::kDouble));
   at::Tensor assign;
   if (want_assign) assign = at::empty({R, n}, X.options().dtype(at::kInt));
-  avk::kmeans_step(X.data_ptr<float>(), n, (int)D, C.data_ptr<float>(), roff.data_ptr<int>(), (int)R, (int)K,
-                   want_assign ? assign.data_ptr<int>() : nullptr, partial.data_ptr<float>(), ssep.data_ptr<double>(),
-                   grid, cur_stream(X));
-  auto tot = partial.to(at::kDouble).sum(0);  // [K, D + 1]
-  return {tot.narrow(1, 0, D), tot.select(1, D), ssep.sum(0), want_assign ? assign : at::Tensor()};
+  avk::kmeans_assign(X.data_ptr<float>(), n, (int)D, C2.data_ptr<float>(), Cn.data_ptr<float>(), roff.data_ptr<int>(),
+                     (int)R, (int)K, want_assign ? assign.data_ptr<int>() : nullptr, partial.data_ptr<float>(),
+                     ssep.data_ptr<double>(), grid, cur_stream(X));
+  return {partial, ssep, want_assign ? assign : at::Tensor()};
+}
+
+// -> fp64 [K * (D + 1) + R]: per centroid (sums[D], count), then per-run SSE
+at::Tensor kmeans_reduce(const at::Tensor& partial, const at::Tensor& ssep) {
+  CHECK_DEV(partial);
+  CHECK_DTYPE(partial, at::kFloat);
+  CHECK_DEV(ssep);
+  CHECK_DTYPE(ssep, at::kDouble);
+  TORCH_CHECK(partial.dim() == 3 && ssep.dim() == 2 && ssep.size(0) == partial.size(0), "partial [G, K, D+1], ssep [G, R]");
+  const int64_t G = partial.size(0), K = partial.size(1), D = partial.size(2) - 1, R = ssep.size(1);
+  auto out = at::empty({K * (D + 1) + R}, ssep.options());
+  DevGuard g(partial.device());
+  avk::kmeans_reduce(partial.data_ptr<float>(), ssep.data_ptr<double>(), (int)G, (int)K, (int)D, (int)R,
+                     out.data_ptr<double>(), cur_stream(partial));
+  return out;
+}
+
+// updates C2 / Cn in place; returns the per-run maximum centroid movement (float [R])
+at::Tensor kmeans_update(const at::Tensor& flat, at::Tensor& C2, at::Tensor& Cn, const at::Tensor& run_of,
+                         const at::Tensor& frozen, int64_t D) {
+  CHECK_DEV(flat);
+  CHECK_DTYPE(flat, at::kDouble);
+  CHECK_DEV(C2);
+  CHECK_DTYPE(C2, at::kFloat);
+  CHECK_DEV(Cn);
+  CHECK_DTYPE(Cn, at::kFloat);
+  CHECK_DEV(run_of);
+  CHECK_DTYPE(run_of, at::kInt);
+  CHECK_DEV(frozen);
+  CHECK_DTYPE(frozen, at::kByte);
+  const int64_t K = Cn.numel(), R = frozen.numel();
+  TORCH_CHECK(K % 2 == 0 && C2.numel() == K * D && run_of.numel() == K, "layout mismatch");
+  TORCH_CHECK(R >= 1 && R <= 16 && flat.numel() == K * (D + 1) + R, "flat must be [K * (D + 1) + R]");
+  auto moves = at::empty({R}, C2.options());
+  DevGuard g(C2.device());
+  avk::kmeans_update(flat.data_ptr<double>(), (int)K, (int)D, (int)R, run_of.data_ptr<int>(), frozen.data_ptr<uint8_t>(),
+                     C2.data_ptr<float>(), Cn.data_ptr<float>(), moves.data_ptr<float>(), cur_stream(C2));
+  return moves;
+}
+
+// ---------------------------------------------------------------------------------------------
+// sequence mining (K5 / K16 / K19)
+
+// Returns (keys int64 [U], counts int64 [U]); key = (len << 58) | (group * group_mul + packed).
+// The table starts at `cap` slots and doubles while the kernel reports that it filled up.
+py::tuple ngram_count(const at::Tensor& states, int64_t S, int64_t min_len, int64_t max_len,
+                      const c10::optional<at::Tensor>& group, int64_t group_mul, int64_t cap) {
+  CHECK_DEV(states);
+  CHECK_DTYPE(states, at::kShort);
+  TORCH_CHECK(states.dim() == 2, "states must be [N, L]");
+  TORCH_CHECK(S >= 1 && S < 32767, "1 <= S < 32767");
+  TORCH_CHECK(min_len >= 1 && max_len >= min_len && max_len <= 63, "1 <= min_len <= max_len <= 63");
+  const int64_t N = states.size(0), L = states.size(1);
+  const int* gp = nullptr;
+  if (group.has_value() && group->defined()) {
+    CHECK_DEV((*group));
+    CHECK_DTYPE((*group), at::kInt);
+    TORCH_CHECK(group->numel() == N, "group must be [N]");
+    gp = group->data_ptr<int>();
+  }
+  TORCH_CHECK(cap >= 1024 && (cap & (cap - 1)) == 0, "cap must be a power of two >= 1024");
+  DevGuard g(states.device());
+  auto dev = states.options();
+  for (;;) {
+    auto keys = at::full({cap}, -1, dev.dtype(at::kLong));
+    auto counts = at::zeros({cap}, dev.dtype(at::kInt));
+    auto flag = at::zeros({1}, dev.dtype(at::kInt));
+    avk::ngram_count(states.data_ptr<int16_t>(), N, (int)L, (int)S, (int)min_len, (int)max_len, gp,
+                     (unsigned long long)group_mul, reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()),
+                     reinterpret_cast<unsigned*>(counts.data_ptr<int>()), (unsigned long long)cap,
+                     flag.data_ptr<int>(), cur_stream(states));
+    if (flag.item<int>() != 0) {
+      TORCH_CHECK(cap < (1LL << 30), "ngram_count: more than 2^30 distinct n-grams");
+      cap *= 2;
+      continue;
+    }
+    auto ok = at::empty({cap}, dev.dtype(at::kLong));
+    auto oc = at::empty({cap}, dev.dtype(at::kLong));
+    auto nout = at::zeros({1}, dev.dtype(at::kLong));
+    avk::hash_compact(reinterpret_cast<const unsigned long long*>(keys.data_ptr<int64_t>()),
+                      reinterpret_cast<const unsigned*>(counts.data_ptr<int>()), (unsigned long long)cap,
+                      reinterpret_cast<long long*>(ok.data_ptr<int64_t>()), reinterpret_cast<long long*>(oc.data_ptr<int64_t>()),
+                      reinterpret_cast<unsigned long long*>(nout.data_ptr<int64_t>()), cur_stream(states));
+    const int64_t U = nout.item<int64_t>();
+    return py::make_tuple(ok.narrow(0, 0, U), oc.narrow(0, 0, U));
+  }
+}
+
+// P fp64 [S, S]; w1, w2 fp64 [B, ldw]; steps int32 [B] (each < ldw) -> out fp64 [B, 2, S, S]
+at::Tensor uniformization(const at::Tensor& P, const at::Tensor& w1, const at::Tensor& w2, const at::Tensor& steps,
+                          const std::vector<int64_t>& h_steps) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&P, &w1, &w2}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kDouble);
+  }
+  CHECK_DEV(steps);
+  CHECK_DTYPE(steps, at::kInt);
+  const int64_t S = P.size(0);
+  TORCH_CHECK(P.dim() == 2 && P.size(1) == S && S >= 1 && S <= 64, "P must be [S, S], S <= 64");
+  TORCH_CHECK(w1.dim() == 2 && w1.sizes() == w2.sizes(), "w1, w2 must be [B, ldw]");
+  const int64_t B = w1.size(0), ldw = w1.size(1);
+  TORCH_CHECK(steps.numel() == B && (int64_t)h_steps.size() == B, "steps must be [B]");
+  for (int64_t s : h_steps) TORCH_CHECK(s >= 0 && s < ldw, "steps[b] must be in [0, ldw)");
+  auto out = at::empty({B, 2, S, S}, P.options());
+  DevGuard g(P.device());
+  avk::uniformization(P.data_ptr<double>(), (int)S, w1.data_ptr<double>(), w2.data_ptr<double>(), steps.data_ptr<int>(),
+                      (int)ldw, (int)B, out.data_ptr<double>(), cur_stream(P));
+  return out;
+}
+
+// A int32 [n, Wa], B int32 [m, Wb] window ids (negative = invalid) -> int32 [n, m] match counts
+at::Tensor dot_matrix(const at::Tensor& A, const at::Tensor& B) {
+  CHECK_DEV(A);
+  CHECK_DTYPE(A, at::kInt);
+  CHECK_DEV(B);
+  CHECK_DTYPE(B, at::kInt);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "A [n, Wa], B [m, Wb]");
+  const int64_t n = A.size(0), m = B.size(0);
+  TORCH_CHECK(n < (1LL << 20) && m < (1LL << 31), "too many sequences");
+  auto hits = at::empty({n, m}, A.options());
+  if (n == 0 || m == 0) return hits;
+  DevGuard g(A.device());
+  avk::dot_matrix(A.data_ptr<int>(), (int)n, (int)A.size(1), B.data_ptr<int>(), (int)m, (int)B.size(1),
+                  hits.data_ptr<int>(), cur_stream(A));
+  return hits;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -830,7 +956,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_solve", &smo_solve);
   m.def("nb_finalize", &nb_finalize);
   m.def("weighted_gram", &weighted_gram);
-  m.def("kmeans_step", &kmeans_step);
+  m.def("kmeans_assign", &kmeans_assign);
+  m.def("kmeans_reduce", &kmeans_reduce);
+  m.def("kmeans_update", &kmeans_update);
+  m.def("ngram_count", &ngram_count);
+  m.def("uniformization", &uniformization);
+  m.def("dot_matrix", &dot_matrix);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

@@ -101,7 +101,21 @@ void weighted_gram(const float* X, long long ld, long long n, int D, const float
 
 // ---- cluster.hip (K16) ---------------------------------------------------------------------
 int kmeans_grid(long long n);
-void kmeans_step(const float* X, long long n, int D, const float* C, const int* roff, int R, int K, int* assign,
-                 float* partial, double* sse_partial, int grid, hipStream_t stream);
+void kmeans_assign(const float* X, long long n, int D, const float* C2, const float* Cn, const int* roff, int R, int K,
+                   int* assign, float* partial, double* sse_partial, int grid, hipStream_t stream);
+void kmeans_reduce(const float* partial, const double* sse_partial, int grid, int K, int D, int R, double* out,
+                   hipStream_t stream);
+void kmeans_update(const double* flat, int K, int D, int R, const int* run_of, const unsigned char* frozen, float* C2,
+                   float* Cn, float* moves, hipStream_t stream);
+
+// seqmine.hip (K5 n-gram hash counts, K16 uniformisation, K19 dot-matrix matching)
+void ngram_count(const short* st, long long n, int L, int S, int min_len, int max_len, const int* group,
+                 unsigned long long group_mul, unsigned long long* keys, unsigned* counts, unsigned long long cap,
+                 int* overflow, hipStream_t stream);
+void hash_compact(const unsigned long long* keys, const unsigned* counts, unsigned long long cap, long long* out_keys,
+                  long long* out_counts, unsigned long long* n_out, hipStream_t stream);
+void uniformization(const double* P, int S, const double* w1, const double* w2, const int* steps, int ldw, int B,
+                    double* out, hipStream_t stream);
+void dot_matrix(const int* A, int n, int Wa, const int* B, int m, int Wb, int* hits, hipStream_t stream);
 
 }  // namespace avk

@@ -1,18 +1,36 @@
 // K16: fused k-means Lloyd step for MANY k-means runs at once — assignment + SSE + centroid
-// partial sums in ONE pass over the data (CDNA4, gfx950).
+// partial sums in ONE pass over the data, then a deterministic device reduction and a device
+// centroid update, so an iteration is three launches and one 4-byte-per-run host read
+// (CDNA4, gfx950).
 //
 // Reference: KmeansCluster (J/cluster/KmeansCluster.java, one MR job per iteration: mapper
-// assigns each record to its nearest centroid, reducer averages) and the Spark job that runs many
-// (numClusters, initGroup) instances keyed by group (S/cluster/KmeansCluster.scala:103-156).
+// assigns each record to its nearest centroid (ClusterMapper.map :154-172), reducer averages
+// (ClusterReducer.reduce :233-297)) and the Spark job that runs many (numClusters, initGroup)
+// instances keyed by group (S/cluster/KmeansCluster.scala:103-156).
 //
-// Design: the centroids of all R runs (concatenated [K_total][D], run r owns rows
-// [roff[r], roff[r+1])) and their squared norms live in LDS; each lane owns one data row at a time,
-// keeps it in registers (float4 loads), computes ||c||^2 - 2 x.c against every centroid from LDS
-// broadcast reads, takes the per-run argmin, and adds the row into the per-workgroup LDS
-// accumulator of the winning centroid of every run ([K_total][D+1], f32 ds_add; the last column
-// counts).  The data is read ONCE per iteration for all runs; workgroup partials are summed in
-// fp64 on the device.  D in {2,4,8,16,32,64} (host pads with zeros), R <= 16,
-// K_total * (2D + 2) floats <= 64 KiB.
+// Centroid layout ("pair layout"): the centroids of all R runs are concatenated, every run padded
+// to an even count with dummy centroids (norm = +inf, never chosen), and stored interleaved in
+// pairs: C2[j/2][d][j&1].  That lets one v_pk_fma_f32 score a row against TWO centroids, with the
+// centroid pair arriving as one 64-bit SGPR operand (wave-uniform -> scalar loads, constant cache).
+//
+// kmeans_mfma_kernel: each lane owns one data row of a 64-row wave tile (the next tile's row is
+// prefetched into registers while the current one is scored), keeps it in registers and scores it
+// against every centroid pair of every run with packed FMAs.  The per-run argmin goes to a
+// wave-private LDS strip and the centroid partial sums become a GEMM on the matrix cores:
+//     sums[c][d] += sum_r onehot[c][r] * x[r][d]
+// issued as v_mfma_f32_16x16x4_f32 with A = one-hot(assignments) (16 centroids x 4 rows) and
+// B = the staged row tile (4 rows x 16 dims), accumulating in registers over the wave's rows.
+// Counts are one LDS integer atomic per row and run.  Workgroup partials [grid, K, D + 1].
+// kmeans_step_kernel (fallback, more than 16 centroid x dim blocks of 16): centroids and
+// accumulators in LDS, per-row ds_add.
+// kmeans_reduce_kernel: fixed-order fp64 sum of the workgroup partials (deterministic).
+// kmeans_update_kernel: new centroids (mean, or unchanged when empty / run frozen), their norms,
+// and the per-run maximum centroid movement (the reference's convergence test).
+// D in {2,4,8,16,32,64} (host pads with zeros), R <= 16 runs per launch.
+//
+// Measured (MI355X, 16.7 M rows x 16 dims, k = 16): 384 us per pass; the same kernel with the
+// scoring and the MFMAs removed streams the data in 182 us (5.9 TB/s), so the pass is bound by the
+// f32 scoring VALU work (16 packed FMAs + argmin per centroid pair per row), not by HBM.
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -20,12 +38,55 @@ namespace {
 
 constexpr int KB = 256;
 constexpr int MAX_RUNS = 16;  // per-run SSE lives in (statically indexed) registers
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float pair_at(const float* C2, int D, int j, int d) {
+  return C2[(long long)(j >> 1) * 2 * D + 2 * d + (j & 1)];
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(const float* __restrict__ X, long long row, bool ok, float (&x)[D]) {
+  if constexpr (D % 4 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 4) {
+      const float4 v = ok ? *reinterpret_cast<const float4*>(X + row * D + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[d] = v.x; x[d + 1] = v.y; x[d + 2] = v.z; x[d + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = ok ? X[row * D + d] : 0.f;
+  }
+}
+
+// Score x against the pair-layout centroids [j0, j1) (both even): best squared distance - ||x||^2.
+// Two packed-FMA chains (even / odd dims) so consecutive FMAs do not depend on each other.
+template <int D>
+__device__ __forceinline__ void score_run(const float (&x)[D], const float* __restrict__ C2,
+                                          const float* __restrict__ Cn, int j0, int j1, float& best, int& bj) {
+  best = INFINITY;
+  bj = j0;
+  for (int j = j0; j < j1; j += 2) {
+    const f32x2* c = reinterpret_cast<const f32x2*>(C2 + (long long)j * D);  // wave-uniform: s_load
+    const f32x2 cn = *reinterpret_cast<const f32x2*>(Cn + j);
+    f32x2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < D; d += 2) {
+      a0 = __builtin_elementwise_fma((f32x2){x[d], x[d]}, c[d], a0);
+      if (d + 1 < D) a1 = __builtin_elementwise_fma((f32x2){x[d + 1], x[d + 1]}, c[d + 1], a1);
+    }
+    const f32x2 acc = a0 + a1;
+    const float d0 = cn.x - 2.f * acc.x, d1 = cn.y - 2.f * acc.y;
+    if (d0 < best) { best = d0; bj = j; }
+    if (d1 < best) { best = d1; bj = j + 1; }
+  }
+}
 
 template <int D>
 __global__ __launch_bounds__(KB) void kmeans_step_kernel(const float* __restrict__ X, long long n,
-                                                         const float* __restrict__ C, const int* __restrict__ roff,
-                                                         int R, int* __restrict__ assign,
-                                                         float* __restrict__ partial,
+                                                         const float* __restrict__ C2, const float* __restrict__ Cn,
+                                                         const int* __restrict__ roff, int R,
+                                                         int* __restrict__ assign, float* __restrict__ partial,
                                                          double* __restrict__ sse_partial) {
   extern __shared__ float lds[];
   __shared__ int s_off[MAX_RUNS + 1];
@@ -36,14 +97,9 @@ __global__ __launch_bounds__(KB) void kmeans_step_kernel(const float* __restrict
   float* cen = lds;                 // [K][D]
   float* cnorm = cen + K * D;       // [K]
   float* acc = cnorm + K;           // [K][D + 1]
-  for (int i = threadIdx.x; i < K * D; i += KB) cen[i] = C[i];
+  for (int i = threadIdx.x; i < K * D; i += KB) cen[i] = pair_at(C2, D, i / D, i % D);
+  for (int i = threadIdx.x; i < K; i += KB) cnorm[i] = Cn[i];
   for (int i = threadIdx.x; i < K * (D + 1); i += KB) acc[i] = 0.f;
-  __syncthreads();
-  for (int j = threadIdx.x; j < K; j += KB) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s = fmaf(cen[j * D + d], cen[j * D + d], s);
-    cnorm[j] = s;
-  }
   __syncthreads();
   double sse[MAX_RUNS];
 #pragma unroll
@@ -51,16 +107,7 @@ __global__ __launch_bounds__(KB) void kmeans_step_kernel(const float* __restrict
   const long long stride = (long long)gridDim.x * KB;
   for (long long row = (long long)blockIdx.x * KB + threadIdx.x; row < n; row += stride) {
     float x[D];
-    if constexpr (D % 4 == 0) {
-#pragma unroll
-      for (int d = 0; d < D; d += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(X + row * D + d);
-        x[d] = v.x; x[d + 1] = v.y; x[d + 2] = v.z; x[d + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int d = 0; d < D; ++d) x[d] = X[row * D + d];
-    }
+    load_row<D>(X, row, true, x);
     float xn = 0.f;
 #pragma unroll
     for (int d = 0; d < D; ++d) xn = fmaf(x[d], x[d], xn);
@@ -100,6 +147,213 @@ __global__ __launch_bounds__(KB) void kmeans_step_kernel(const float* __restrict
   }
 }
 
+template <int D, int KBLK>
+__global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict__ X, long long n,
+                                                         const float* __restrict__ C2, const float* __restrict__ Cn,
+                                                         const int* __restrict__ roff, int R, int K,
+                                                         int* __restrict__ assign, float* __restrict__ partial,
+                                                         double* __restrict__ sse_partial) {
+  constexpr int DP = D < 16 ? 16 : D;  // staged row width (zero padded to one 16-wide block)
+  constexpr int DB = DP / 16;
+  extern __shared__ float lds[];
+  float* xs_all = lds;                                                 // [4 waves][64][DP]
+  int* asg_all = reinterpret_cast<int*>(xs_all + 4 * 64 * DP);         // [4 waves][64][R]
+  unsigned* cnt = reinterpret_cast<unsigned*>(asg_all + 4 * 64 * R);   // [K]
+  float* red = reinterpret_cast<float*>(cnt + K);                      // [K][D]
+  __shared__ double sred[4][MAX_RUNS];
+  for (int i = threadIdx.x; i < K; i += KB) cnt[i] = 0u;
+  for (int i = threadIdx.x; i < K * D; i += KB) red[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* xs = xs_all + w * 64 * DP;
+  int* asg = asg_all + w * 64 * R;
+  // A operand: lane l supplies A[i = l & 15][k = l >> 4] of centroid block cb
+  // (centroid ids as floats are exact; -1 never matches an assignment: centroid lanes past K)
+  float a_centf[KBLK];
+  int a_runc[KBLK];
+#pragma unroll
+  for (int cb = 0; cb < KBLK; ++cb) {
+    const int c = cb * 16 + (lane & 15);
+    int rr = -1;
+    for (int r = 0; r < R; ++r)
+      if (c >= roff[r] && c < roff[r + 1]) rr = r;
+    a_centf[cb] = rr >= 0 ? (float)c : -2.f;
+    a_runc[cb] = rr >= 0 ? rr : 0;
+  }
+  f32x4 acc[2][KBLK][DB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int cb = 0; cb < KBLK; ++cb)
+#pragma unroll
+      for (int db = 0; db < DB; ++db) acc[h][cb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double sse[MAX_RUNS];
+#pragma unroll
+  for (int r = 0; r < MAX_RUNS; ++r) sse[r] = 0.0;
+  const long long ntiles = (n + 63) / 64;
+  const long long gw = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
+  float xnext[D];
+  if (gw < ntiles) load_row<D>(X, gw * 64 + lane, gw * 64 + lane < n, xnext);
+  for (long long t = gw; t < ntiles; t += nw) {
+    const long long row = t * 64 + lane;
+    const bool ok = row < n;
+    float x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = xnext[d];
+    {  // prefetch the next tile's row: its HBM latency hides behind this tile's scoring
+      const long long nrow = (t + nw) * 64 + lane;
+      if (t + nw < ntiles) load_row<D>(X, nrow, nrow < n, xnext);
+    }
+    float xn = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) xn = fmaf(x[d], x[d], xn);
+#pragma unroll
+    for (int r = 0; r < MAX_RUNS; ++r) {
+      if (r >= R) break;
+      const int j0 = __builtin_amdgcn_readfirstlane(roff[r]), j1 = __builtin_amdgcn_readfirstlane(roff[r + 1]);
+      float best;
+      int bj;
+      score_run<D>(x, C2, Cn, j0, j1, best, bj);
+      if (ok) {
+        if (assign) assign[(long long)r * n + row] = bj - j0;
+        sse[r] += (double)fmaxf(best + xn, 0.f);
+        atomicAdd(&cnt[bj], 1u);
+      }
+      asg[lane * R + r] = ok ? bj : -1;
+    }
+    float xp[DP];  // zero-padded copy (compile-time indices: stays in registers)
+#pragma unroll
+    for (int d = 0; d < DP; ++d) xp[d] = d < D ? x[d < D ? d : 0] : 0.f;
+#pragma unroll
+    for (int d = 0; d < DP; d += 4)
+      *reinterpret_cast<float4*>(xs + lane * DP + d) = make_float4(xp[d], xp[d + 1], xp[d + 2], xp[d + 3]);
+    // wave-private strip: LDS executes one wave's instructions in order, so the reads below see
+    // these writes without a waitcnt (a full s_waitcnt(0) here would also drain the prefetch)
+    __builtin_amdgcn_wave_barrier();
+    // 16 MFMA k-steps of 4 rows; operands of 4 steps are read from LDS back to back (one wait),
+    // and even / odd steps feed two accumulator sets so consecutive MFMAs are independent
+#pragma unroll
+    for (int s0 = 0; s0 < 16; s0 += 4) {
+      float a[4][KBLK], b[4][DB];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 4 * (s0 + q) + (lane >> 4);
+#pragma unroll
+        for (int cb = 0; cb < KBLK; ++cb) a[q][cb] = (float)asg[rr * R + a_runc[cb]];
+#pragma unroll
+        for (int db = 0; db < DB; ++db) b[q][db] = xs[rr * DP + db * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int cb = 0; cb < KBLK; ++cb) {
+          const float av = a[q][cb] == a_centf[cb] ? 1.f : 0.f;
+#pragma unroll
+          for (int db = 0; db < DB; ++db)
+            acc[q & 1][cb][db] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[q][db], acc[q & 1][cb][db], 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // combine the 4 waves' accumulators in LDS: lane holds D[i = 4 (l >> 4) + q][j = l & 15]
+#pragma unroll
+  for (int cb = 0; cb < KBLK; ++cb)
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = cb * 16 + 4 * (lane >> 4) + q, d = db * 16 + (lane & 15);
+        if (c < K && d < D) atomicAdd(&red[c * D + d], acc[0][cb][db][q] + acc[1][cb][db][q]);
+      }
+#pragma unroll
+  for (int r = 0; r < MAX_RUNS; ++r) {
+    if (r >= R) break;
+    const double v = av::wave_sum(sse[r]);
+    if (lane == 0) sred[w][r] = v;
+  }
+  __syncthreads();
+  float* out = partial + (long long)blockIdx.x * K * (D + 1);
+  for (int i = threadIdx.x; i < K * (D + 1); i += KB) {
+    const int c = i / (D + 1), d = i - c * (D + 1);
+    out[i] = d < D ? red[c * D + d] : (float)cnt[c];
+  }
+  for (int r = threadIdx.x; r < R; r += KB) {
+    double s = 0.0;
+    for (int q = 0; q < 4; ++q) s += sred[q][r];
+    sse_partial[(long long)blockIdx.x * R + r] = s;
+  }
+}
+
+// out[o] = sum_g partial[g][o] (o < KD1) and out[KD1 + r] = sum_g ssep[g][r]: 16 outputs x 64
+// grid slices per workgroup (4 independent partial sums per lane keep 4 loads in flight), slices
+// combined in a fixed order: deterministic.
+constexpr int RD_O = 16, RD_S = 64;
+__global__ __launch_bounds__(RD_O * RD_S) void kmeans_reduce_kernel(const float* __restrict__ partial,
+                                                                    const double* __restrict__ ssep, int grid,
+                                                                    int KD1, int R, double* __restrict__ out) {
+  __shared__ double red[RD_S][RD_O];
+  const int oi = threadIdx.x % RD_O, sl = threadIdx.x / RD_O;
+  const int o = blockIdx.x * RD_O + oi;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (o < KD1) {
+    int g = sl;
+    for (; g + 3 * RD_S < grid; g += 4 * RD_S) {
+      s0 += (double)partial[(long long)g * KD1 + o];
+      s1 += (double)partial[(long long)(g + RD_S) * KD1 + o];
+      s2 += (double)partial[(long long)(g + 2 * RD_S) * KD1 + o];
+      s3 += (double)partial[(long long)(g + 3 * RD_S) * KD1 + o];
+    }
+    for (; g < grid; g += RD_S) s0 += (double)partial[(long long)g * KD1 + o];
+  } else if (o < KD1 + R) {
+    for (int g = sl; g < grid; g += RD_S) s0 += ssep[(long long)g * R + (o - KD1)];
+  }
+  red[sl][oi] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (sl == 0 && o < KD1 + R) {
+    double t = 0.0;
+    for (int q = 0; q < RD_S; ++q) t += red[q][oi];
+    out[o] = t;
+  }
+}
+
+__global__ __launch_bounds__(1024) void kmeans_update_kernel(const double* __restrict__ flat, int K, int D, int R,
+                                                             const int* __restrict__ run_of,
+                                                             const unsigned char* __restrict__ frozen,
+                                                             float* __restrict__ C2, float* __restrict__ Cn,
+                                                             float* __restrict__ moves) {
+  extern __shared__ float mv2[];  // [K]
+  __shared__ unsigned mx[MAX_RUNS];
+  for (int c = threadIdx.x; c < K; c += 1024) mv2[c] = 0.f;
+  if (threadIdx.x < MAX_RUNS) mx[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * D; i += 1024) {
+    const int c = i / D, d = i - c * D;
+    const int r = run_of[c];
+    if (r < 0 || frozen[r]) continue;
+    const double cnt = flat[(long long)c * (D + 1) + D];
+    float* p = C2 + (long long)(c >> 1) * 2 * D + 2 * d + (c & 1);
+    const float old = *p;
+    const float nw = cnt > 0.0 ? (float)(flat[(long long)c * (D + 1) + d] / cnt) : old;
+    *p = nw;
+    const float df = nw - old;
+    atomicAdd(&mv2[c], df * df);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < K; c += 1024) {
+    const int r = run_of[c];
+    if (r < 0 || frozen[r]) continue;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) {
+      const float v = C2[(long long)(c >> 1) * 2 * D + 2 * d + (c & 1)];
+      s = fmaf(v, v, s);
+    }
+    Cn[c] = s;
+    atomicMax(&mx[r], __float_as_uint(sqrtf(mv2[c])));  // non-negative floats order like their bits
+  }
+  __syncthreads();
+  if (threadIdx.x < R) moves[threadIdx.x] = __uint_as_float(mx[threadIdx.x]);
+}
+
 }  // namespace
 
 namespace avk {
@@ -110,20 +364,62 @@ int kmeans_grid(long long n) {
   return (int)std::max(256LL, std::min(g, 4096LL));
 }
 
-void kmeans_step(const float* X, long long n, int D, const float* C, const int* roff, int R, int K, int* assign,
-                 float* partial, double* sse_partial, int grid, hipStream_t stream) {
-  if (R < 1 || R > MAX_RUNS) throw std::runtime_error("kmeans_step: 1 <= runs <= 16");
+void kmeans_assign(const float* X, long long n, int D, const float* C2, const float* Cn, const int* roff, int R, int K,
+                   int* assign, float* partial, double* sse_partial, int grid, hipStream_t stream) {
+  if (R < 1 || R > MAX_RUNS) throw std::runtime_error("kmeans_assign: 1 <= runs <= 16");
+  if (K & 1) throw std::runtime_error("kmeans_assign: padded centroid count must be even");
+  const int DP = D < 16 ? 16 : D;
+  int KBt = 1;
+  while (KBt * 16 < K) KBt *= 2;
+  if (KBt * (DP / 16) <= 16) {
+    const size_t lds = sizeof(float) * (4 * 64 * (size_t)DP + 4 * 64 * (size_t)R + K + (size_t)K * D);
+    if (lds > 160 * 1024) throw std::runtime_error("kmeans_assign: LDS budget exceeded");
+#define AVK_KMM(DD, KK)                                                                                       \
+  if (D == DD && KBt == KK) {                                                                                 \
+    if (lds > 64 * 1024)                                                                                      \
+      AV_HIP_CHECK(hipFuncSetAttribute((const void*)kmeans_mfma_kernel<DD, KK>,                               \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                \
+    kmeans_mfma_kernel<DD, KK><<<grid, KB, lds, stream>>>(X, n, C2, Cn, roff, R, K, assign, partial, sse_partial); \
+    AV_HIP_CHECK(hipGetLastError());                                                                          \
+    return;                                                                                                   \
+  }
+    AVK_KMM(2, 1) AVK_KMM(2, 2) AVK_KMM(2, 4) AVK_KMM(2, 8) AVK_KMM(2, 16)
+    AVK_KMM(4, 1) AVK_KMM(4, 2) AVK_KMM(4, 4) AVK_KMM(4, 8) AVK_KMM(4, 16)
+    AVK_KMM(8, 1) AVK_KMM(8, 2) AVK_KMM(8, 4) AVK_KMM(8, 8) AVK_KMM(8, 16)
+    AVK_KMM(16, 1) AVK_KMM(16, 2) AVK_KMM(16, 4) AVK_KMM(16, 8) AVK_KMM(16, 16)
+    AVK_KMM(32, 1) AVK_KMM(32, 2) AVK_KMM(32, 4) AVK_KMM(32, 8)
+    AVK_KMM(64, 1) AVK_KMM(64, 2) AVK_KMM(64, 4)
+#undef AVK_KMM
+    throw std::runtime_error("kmeans_assign: D must be 2, 4, 8, 16, 32 or 64");
+  }
   const size_t lds = sizeof(float) * ((size_t)K * D + K + (size_t)K * (D + 1));
-  if (lds > 64 * 1024) throw std::runtime_error("kmeans_step: total centroids * D too large for LDS");
+  if (lds > 64 * 1024) throw std::runtime_error("kmeans_assign: total centroids * D too large for LDS");
   switch (D) {
-#define AVK_KM(DD)                                                                                          \
-  case DD:                                                                                                  \
-    kmeans_step_kernel<DD><<<grid, KB, lds, stream>>>(X, n, C, roff, R, assign, partial, sse_partial); \
+#define AVK_KM(DD)                                                                                                \
+  case DD:                                                                                                        \
+    kmeans_step_kernel<DD><<<grid, KB, lds, stream>>>(X, n, C2, Cn, roff, R, assign, partial, sse_partial); \
     break;
     AVK_KM(2) AVK_KM(4) AVK_KM(8) AVK_KM(16) AVK_KM(32) AVK_KM(64)
 #undef AVK_KM
-    default: throw std::runtime_error("kmeans_step: D must be 2, 4, 8, 16, 32 or 64");
+    default: throw std::runtime_error("kmeans_assign: D must be 2, 4, 8, 16, 32 or 64");
   }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void kmeans_reduce(const float* partial, const double* sse_partial, int grid, int K, int D, int R, double* out,
+                   hipStream_t stream) {
+  const int KD1 = K * (D + 1);
+  const int blocks = (KD1 + R + RD_O - 1) / RD_O;
+  kmeans_reduce_kernel<<<blocks, RD_O * RD_S, 0, stream>>>(partial, sse_partial, grid, KD1, R, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void kmeans_update(const double* flat, int K, int D, int R, const int* run_of, const unsigned char* frozen, float* C2,
+                   float* Cn, float* moves, hipStream_t stream) {
+  if (R < 1 || R > MAX_RUNS) throw std::runtime_error("kmeans_update: 1 <= runs <= 16");
+  const size_t lds = sizeof(float) * (size_t)K;
+  if (lds > 64 * 1024) throw std::runtime_error("kmeans_update: too many centroids");
+  kmeans_update_kernel<<<1, 1024, lds, stream>>>(flat, K, D, R, run_of, frozen, C2, Cn, moves);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -8,9 +8,10 @@ numeric means + categorical modes, movement / status / SSE, :57-297), ``S/cluste
 :103-172), ``S/cluster/KMeansPlusPlusCluster.scala`` (commons-math k-means++), ``P/unsupv/cluster.py``
 (sklearn kmeans / agglomerative / dbscan, Hopkins statistic), ``J/cluster/AgglomerativeGraphical.java``.
 
-MI355X: assignment is the k = 1 case of the fused MFMA distance + top-k kernel, the update is one
-LDS-privatised accumulation kernel, and ONE all-reduce of [K, D] sums + [K] counts per iteration
-replaces the shuffle; the convergence test runs on device.
+MI355X: a group of up to 16 runs shares ONE pass over the data per iteration (K16: packed-FMA
+scoring against SGPR-resident centroid pairs, one-hot x rows on the matrix cores for the partial
+sums), a deterministic device reduction, ONE all-reduce of the flat [K (D+1) + R] statistics
+replaces the shuffle, and the centroid update + movement test run on the device.
 """
 from __future__ import annotations
 
@@ -34,6 +35,58 @@ class KMeansRun:
     counts: torch.Tensor | None = None
     converged: bool = False
     history: list = field(default_factory=list)
+
+
+class _PairLayout:
+    """Device state of one launch group in the K16 pair layout: runs padded to an even centroid
+    count (padding centroids have norm +inf and are never chosen), stored as C2 [Kp/2, Dp, 2]."""
+
+    def __init__(self, Cs: list[torch.Tensor], Dp: int):
+        dev = Cs[0].device
+        self.ks = [c.shape[0] for c in Cs]
+        self.h_roff = [0]
+        for k in self.ks:
+            self.h_roff.append(self.h_roff[-1] + k + (k & 1))
+        K = self.h_roff[-1]
+        self.K, self.Dp = K, Dp
+        Cf = torch.zeros((K, Dp), dtype=torch.float32, device=dev)
+        self.Cn = torch.full((K,), math.inf, dtype=torch.float32, device=dev)
+        run_of = torch.full((K,), -1, dtype=torch.int32)
+        for r, C in enumerate(Cs):
+            o, k = self.h_roff[r], self.ks[r]
+            Cf[o:o + k, :C.shape[1]] = C.float()
+            self.Cn[o:o + k] = (C.float() ** 2).sum(1)
+            run_of[o:o + k] = r
+        self.C2 = Cf.view(K // 2, 2, Dp).transpose(1, 2).contiguous()
+        self.run_of = run_of.to(dev)
+        self.roff = torch.tensor(self.h_roff, dtype=torch.int32, device=dev)
+
+    def centroids(self, r: int, D: int) -> torch.Tensor:
+        Cf = self.C2.transpose(1, 2).reshape(self.K, self.Dp)
+        o = self.h_roff[r]
+        return Cf[o:o + self.ks[r], :D].contiguous()
+
+    def stats(self, flat: torch.Tensor, r: int, D: int):
+        """(sums f64 [k, D], counts f64 [k], sse f64 scalar) of run r from the reduced vector."""
+        blk = flat[: self.K * (self.Dp + 1)].view(self.K, self.Dp + 1)
+        o, k = self.h_roff[r], self.ks[r]
+        return blk[o:o + k, :D], blk[o:o + k, self.Dp], flat[self.K * (self.Dp + 1) + r]
+
+
+def kmeans_step(X: torch.Tensor, Cs: list[torch.Tensor], want_assign: bool = False):
+    """One fused K16 Lloyd pass of several runs over ``X`` (GPU, D padded to 2/4/8/16/32/64):
+    per run (sums f64 [k, D], counts f64 [k], sse f64, assignment int32 [n] or None)."""
+    Dp = X.shape[1]
+    lay = _PairLayout(Cs, Dp)
+    C = _native.C()
+    partial, ssep, assign = C.kmeans_assign(X.float().contiguous(), lay.C2, lay.Cn, lay.roff, lay.h_roff,
+                                            want_assign)
+    flat = C.kmeans_reduce(partial, ssep)
+    out = []
+    for r in range(len(Cs)):
+        sums, counts, sse = lay.stats(flat, r, Dp)
+        out.append((sums, counts, sse, assign[r] if want_assign else None))
+    return out
 
 
 class KMeans:
@@ -66,32 +119,23 @@ class KMeans:
         if self.init == "random":
             C = S[torch.randperm(S.shape[0], generator=g)[:k].to(S.device)]
         else:
-            first = int(torch.randint(0, S.shape[0], (1,), generator=g))
-            C = S[first:first + 1]
-            d2 = ((S - C) ** 2).sum(1)
-            for _ in range(1, k):
-                p = (d2 / d2.sum().clamp_min(1e-30)).double().cpu()
-                nxt = int(torch.multinomial(p, 1, generator=g)) if float(p.sum()) > 0 else 0
-                C = torch.cat([C, S[nxt:nxt + 1]])
-                d2 = torch.minimum(d2, ((S - S[nxt]) ** 2).sum(1))
+            # D^2 sampling by inverse CDF on the device: no host round trip per centre
+            u = torch.rand(k, generator=g, dtype=torch.float64)
+            m = S.shape[0]
+            idx = [torch.full((1,), min(int(float(u[0]) * m), m - 1), dtype=torch.long, device=S.device)]
+            d2 = ((S - S.index_select(0, idx[0])) ** 2).sum(1).double()
+            for i in range(1, k):
+                cum = torch.cumsum(d2, 0)
+                nxt = torch.searchsorted(cum, (cum[-1:] * float(u[i])), right=True).clamp_max(m - 1)
+                idx.append(nxt)
+                d2 = torch.minimum(d2, ((S - S.index_select(0, nxt)) ** 2).sum(1).double())
+            C = S.index_select(0, torch.cat(idx))
         if comm.is_distributed:
             C = comm.broadcast(C.contiguous(), 0)
         return C.contiguous()
 
-    def _step(self, X: torch.Tensor, Xp: torch.Tensor | None, Cs: list[torch.Tensor]):
-        """One Lloyd pass for a GROUP of runs -> per run (sums f64 [k, D], counts [k], sse f64 [1]).
-        GPU: ONE launch of the fused K16 kernel for all runs (data read once); CPU: oracle."""
-        if Xp is not None:
-            D = X.shape[1]
-            ks = [c.shape[0] for c in Cs]
-            Cp = torch.zeros((sum(ks), Xp.shape[1]), dtype=torch.float32, device=X.device)
-            Cp[:, :D] = torch.cat(Cs)
-            sums, counts, sse, _ = _native.C().kmeans_step(Xp, Cp.contiguous(), ks, False)
-            out, o = [], 0
-            for r, k in enumerate(ks):
-                out.append((sums[o:o + k, :D].contiguous(), counts[o:o + k].round().long(), sse[r:r + 1]))
-                o += k
-            return out
+    def _step(self, X: torch.Tensor, Cs: list[torch.Tensor]):
+        """CPU oracle of one Lloyd pass -> per run (sums f64 [k, D], counts [k], sse f64 [1])."""
         res = []
         for C in Cs:
             d, idx = dist.knn(X, C, 1, "sqeuclidean")
@@ -114,24 +158,30 @@ class KMeans:
         return Xp
 
     def _groups(self, specs: list[tuple[int, int]], Dp: int | None) -> list[list[int]]:
-        """Pack runs into launch groups: <= 16 runs and total centroids within the LDS budget."""
+        """Pack runs into launch groups: <= 16 runs and at most as many padded centroids as one
+        launch holds (the kernel picks its MFMA or LDS variant from the group's size); CPU: one run
+        per group."""
         groups, cur, tot = [], [], 0
-        cap = (64 * 1024) // (4 * (2 * Dp + 2)) if Dp else 1 << 30
+        # MFMA variant: <= 16 blocks of 16 centroids x 16 dims; LDS variant: K (2 Dp + 2) floats <= 64 KiB
+        cap = max(256 // max(1, Dp // 16), (65536 // (8 * Dp + 8)) & ~1) if Dp else 1 << 30
         for i, (k, _) in enumerate(specs):
-            if Dp is not None and k > cap:
-                raise ValueError(f"k={k} too large for the LDS-resident k-means kernel at D={Dp}")
-            if cur and (len(cur) == 16 or tot + k > cap or Dp is None):
+            kp = k + (k & 1)
+            if kp > cap:
+                raise ValueError(f"k={k} exceeds the {cap} centroids one k-means launch holds at D={Dp}")
+            if cur and (len(cur) == 16 or tot + kp > cap or Dp is None):
                 groups.append(cur)
                 cur, tot = [], 0
             cur.append(i)
-            tot += k
+            tot += kp
         if cur:
             groups.append(cur)
         return groups
 
     def fit(self, X: torch.Tensor) -> "KMeans":
         """All (k, init) runs advance together (S/cluster/KmeansCluster.scala keys by
-        (numClusters, initGroup)): one kernel launch per iteration per group of runs."""
+        (numClusters, initGroup)).  GPU: per iteration ONE fused assignment launch for a group of
+        runs, one reduction launch, one RCCL all-reduce of the flat [K (D+1) + R] statistics when
+        distributed, one update launch and a 4-byte-per-run host read of the centroid movement."""
         comm = self.comm or get_comm()
         X = X.float().contiguous()
         Xp = self._padded(X)
@@ -139,50 +189,93 @@ class KMeans:
         runs = [KMeansRun(k, sd, self._init_centroids(X, k, sd)) for k, sd in specs]
         self.best = {}
         for grp in self._groups(specs, Xp.shape[1] if Xp is not None else None):
-            active = list(grp)
-            for it in range(self.max_iter):
-                res = self._step(X, Xp, [runs[i].centroids for i in active])
-                if comm.is_distributed:
-                    flat = torch.cat([torch.cat([s.view(-1), c.double().view(-1), e]) for s, c, e in res])
-                    flat = comm.all_reduce(flat)
-                    o, red = 0, []
-                    for s, c, e in res:
-                        a, b = s.numel(), c.numel()
-                        red.append((flat[o:o + a].view_as(s), flat[o + a:o + a + b].round().long(),
-                                    flat[o + a + b:o + a + b + 1]))
-                        o += a + b + 1
-                    res = red
-                moves = []
-                for i, (sums, counts, sse) in zip(active, res):
-                    C = runs[i].centroids
-                    newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1).view(-1, 1),
-                                       C.double()).float()
-                    moves.append(((newC - C) ** 2).sum(1).sqrt().max())
-                    runs[i].centroids = newC
-                    runs[i].history.append(sse)
-                    runs[i].iterations = it + 1
-                mv = torch.stack(moves).cpu().tolist()          # one host sync per iteration per group
-                still = []
-                for i, m in zip(active, mv):
-                    if m <= self.tol:
-                        runs[i].converged = True
-                    else:
-                        still.append(i)
-                active = still
-                if not active:
-                    break
-            final = self._step(X, Xp, [runs[i].centroids for i in grp])
-            for i, (sums, counts, sse) in zip(grp, final):
-                if comm.is_distributed:
-                    sse = comm.all_reduce(sse)
-                    counts = comm.all_reduce(counts)
-                runs[i].sse, runs[i].counts = float(sse), counts
-                runs[i].history = [float(h) for h in runs[i].history]
+            if Xp is not None:
+                self._fit_gpu_group(X.shape[1], Xp, [runs[i] for i in grp], comm)
+            else:
+                self._fit_cpu_group(X, [runs[i] for i in grp], comm)
         self.runs = runs
         for r in runs:
             if r.k not in self.best or r.sse < self.best[r.k].sse:
                 self.best[r.k] = r
         return self
+
+    def _fit_gpu_group(self, D: int, Xp: torch.Tensor, grp: list[KMeansRun], comm) -> None:
+        C = _native.C()
+        lay = _PairLayout([r.centroids for r in grp], Xp.shape[1])
+        R = len(grp)
+        frozen_h = [0] * R
+        frozen = torch.zeros(R, dtype=torch.uint8, device=Xp.device)
+        hist: list[tuple[int, torch.Tensor]] = []
+        for it in range(self.max_iter):
+            partial, ssep, _ = C.kmeans_assign(Xp, lay.C2, lay.Cn, lay.roff, lay.h_roff, False)
+            flat = C.kmeans_reduce(partial, ssep)
+            if comm.is_distributed:
+                flat = comm.all_reduce(flat)
+            moves = C.kmeans_update(flat, lay.C2, lay.Cn, lay.run_of, frozen, lay.Dp)
+            hist.append((it, flat[-R:]))
+            mv = moves.cpu().tolist()                  # the one host sync of the iteration
+            changed = False
+            for r, run in enumerate(grp):
+                if frozen_h[r]:
+                    continue
+                run.iterations = it + 1
+                if mv[r] <= self.tol:
+                    run.converged = True
+                    frozen_h[r] = 1
+                    changed = True
+            if all(frozen_h):
+                break
+            if changed:
+                frozen.copy_(torch.tensor(frozen_h, dtype=torch.uint8))
+        sse_hist = torch.stack([h for _, h in hist]).cpu()
+        for r, run in enumerate(grp):
+            run.history = [float(sse_hist[i, r]) for i in range(run.iterations)]
+            run.centroids = lay.centroids(r, D)
+        partial, ssep, _ = C.kmeans_assign(Xp, lay.C2, lay.Cn, lay.roff, lay.h_roff, False)
+        flat = C.kmeans_reduce(partial, ssep)
+        if comm.is_distributed:
+            flat = comm.all_reduce(flat)
+        for r, run in enumerate(grp):
+            _, counts, sse = lay.stats(flat, r, D)
+            run.sse, run.counts = float(sse), counts.round().long()
+
+    def _fit_cpu_group(self, X: torch.Tensor, grp: list[KMeansRun], comm) -> None:
+        active = list(range(len(grp)))
+        for it in range(self.max_iter):
+            res = self._step(X, [grp[i].centroids for i in active])
+            if comm.is_distributed:
+                flat = torch.cat([torch.cat([s.view(-1), c.double().view(-1), e]) for s, c, e in res])
+                flat = comm.all_reduce(flat)
+                o, red = 0, []
+                for s_, c, e in res:
+                    a, b = s_.numel(), c.numel()
+                    red.append((flat[o:o + a].view_as(s_), flat[o + a:o + a + b].round().long(),
+                                flat[o + a + b:o + a + b + 1]))
+                    o += a + b + 1
+                res = red
+            still = []
+            for i, (sums, counts, sse) in zip(active, res):
+                run = grp[i]
+                Cc = run.centroids
+                newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1).view(-1, 1),
+                                   Cc.double()).float()
+                mv = float(((newC - Cc) ** 2).sum(1).sqrt().max())
+                run.centroids = newC
+                run.history.append(float(sse))
+                run.iterations = it + 1
+                if mv <= self.tol:
+                    run.converged = True
+                else:
+                    still.append(i)
+            active = still
+            if not active:
+                break
+        final = self._step(X, [r.centroids for r in grp])
+        for run, (sums, counts, sse) in zip(grp, final):
+            if comm.is_distributed:
+                sse = comm.all_reduce(sse)
+                counts = comm.all_reduce(counts)
+            run.sse, run.counts = float(sse), counts
 
     @property
     def cluster_centers_(self) -> torch.Tensor:

@@ -326,28 +326,37 @@ class ContTimeStateTransitionStats:
         S = Q.shape[0]
         self.P = torch.eye(S, dtype=torch.float64, device=Q.device) + self.Q / max(self.lam, 1e-300)
 
-    def _powers(self, t: float) -> tuple[torch.Tensor, torch.Tensor]:
+    def _weights(self, t: float) -> tuple[int, torch.Tensor, torch.Tensor]:
+        """Truncation L = 4 + 6 sqrt(lt) + lt and the Poisson weights w_k and tails P(N > k)."""
         lt = self.lam * t
         L = int(4 + 6 * math.sqrt(lt) + lt)
-        S = self.P.shape[0]
-        pw = [torch.eye(S, dtype=torch.float64, device=self.P.device)]
-        for _ in range(L):
-            pw.append(pw[-1] @ self.P)
-        k = torch.arange(L + 1, dtype=torch.float64, device=self.P.device)
-        logpois = -lt + k * math.log(max(lt, 1e-300)) - torch.lgamma(k + 1)
-        return torch.stack(pw), torch.exp(logpois)
+        k = torch.arange(L + 1, dtype=torch.float64)
+        w = torch.exp(-lt + k * math.log(max(lt, 1e-300)) - torch.lgamma(k + 1))
+        tail = (1.0 - torch.cumsum(w, 0)).clamp_min(0)
+        return L, w, tail
+
+    def sums(self, times: list[float]) -> tuple[torch.Tensor, torch.Tensor]:
+        """For every t: (future-state probabilities [S, S], expected dwell times [S, S]) from ONE
+        batched power-chain launch (K16); P^k is never materialised in HBM."""
+        ws = [self._weights(t) for t in times]
+        ldw = max(L for L, _, _ in ws) + 1
+        w1 = torch.zeros((len(times), ldw), dtype=torch.float64)
+        w2 = torch.zeros_like(w1)
+        for b, (L, w, tail) in enumerate(ws):
+            w1[b, : L + 1] = w
+            w2[b, : L + 1] = tail
+        dev = self.P.device
+        A, B = SO.uniformization_sums(self.P, w1.to(dev), w2.to(dev), [L for L, _, _ in ws])
+        return A, B / self.lam
 
     def future_state_prob(self, t: float) -> torch.Tensor:
         """[S, S]: P(X(t) = j | X(0) = i) = sum_k Poisson(k; lt) (P^k)_ij."""
-        pw, w = self._powers(t)
-        return (w.view(-1, 1, 1) * pw).sum(0)
+        return self.sums([t])[0][0]
 
     def state_dwell_time(self, t: float) -> torch.Tensor:
         """[S, S]: expected time spent in j over [0, t] starting in i
         = (1/lambda) sum_k P(N > k) (P^k)_ij, N ~ Poisson(lt)."""
-        pw, w = self._powers(t)
-        tail = (1.0 - torch.cumsum(w, 0)).clamp_min(0)
-        return (tail.view(-1, 1, 1) * pw).sum(0) / self.lam
+        return self.sums([t])[1][0]
 
     def transition_count(self, t: float) -> torch.Tensor:
         """[S, S, S]: expected number of i->j transitions over [0, t] from start state s
@@ -401,16 +410,14 @@ def dot_matrix_similarity(A: torch.Tensor, B: torch.Tensor, window: int = 3) -> 
     by the number of windows.  A [n, L], B [m, L'] int (negative = padding)."""
     wa = A.long().unfold(1, window, 1)      # [n, La, w]
     wb = B.long().unfold(1, window, 1)      # [m, Lb, w]
-    base = int(max(int(A.max()), int(B.max())) + 2)
-    pw = base ** torch.arange(window - 1, -1, -1, device=A.device)
-    ka = ((wa + 1) * pw).sum(-1)
-    kb = ((wb + 1) * pw).sum(-1)
     va = (wa >= 0).all(-1)
     vb = (wb >= 0).all(-1)
-    ka = torch.where(va, ka, torch.full_like(ka, -1))
-    kb = torch.where(vb, kb, torch.full_like(kb, -2))
-    eq = (ka.unsqueeze(1).unsqueeze(3) == kb.unsqueeze(0).unsqueeze(2))   # [n, m, La, Lb]
-    hits = eq.sum((2, 3)).double()
+    # dense window ids shared by both sides (exact: no hashing), -1 for windows with padding
+    allw = torch.cat([wa.reshape(-1, window), wb.reshape(-1, window)])
+    _, inv = torch.unique(allw, dim=0, return_inverse=True)
+    ida = torch.where(va, inv[: wa.shape[0] * wa.shape[1]].view(va.shape), torch.full_like(va, -1, dtype=torch.long))
+    idb = torch.where(vb, inv[wa.shape[0] * wa.shape[1]:].view(vb.shape), torch.full_like(vb, -1, dtype=torch.long))
+    hits = SO.dot_matrix_hits(ida.to(torch.int32), idb.to(torch.int32)).double()
     denom = (va.sum(1).view(-1, 1) * vb.sum(1).view(1, -1)).clamp_min(1).double().sqrt()
     return hits / denom
 

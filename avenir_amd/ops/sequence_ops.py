@@ -1,4 +1,5 @@
-"""Sequence ops (K14/K15, n-gram counting): GPU -> HIP kernels; CPU -> PyTorch references."""
+"""Sequence ops (K14/K15 Viterbi / log-odds, K5 n-grams, K16 uniformisation, K19 dot matrix):
+GPU -> HIP kernels; CPU -> PyTorch references."""
 from __future__ import annotations
 
 import torch
@@ -70,11 +71,38 @@ def markov_logodds(states: torch.Tensor, log_ratio: torch.Tensor) -> torch.Tenso
 def ngram_counts(states: torch.Tensor, n_states: int, min_len: int = 2, max_len: int = 5,
                  group: torch.Tensor | None = None) -> dict[int, tuple[torch.Tensor, torch.Tensor]]:
     """Count every contiguous sub-sequence of length min_len..max_len (ProbabilisticSuffixTree
-    counting).  n-grams are packed into int64 keys (base n_states + 1, group id in the high bits)
-    and counted with a device radix sort (torch.unique).  Returns {length: (keys, counts)}."""
-    s = states.long()
-    N, L = s.shape
+    counting, J/markov/ProbabilisticSuffixTreeGenerator.java:140-194).  n-grams are packed into
+    int64 keys (base n_states + 1, group id in the high bits).  GPU: one pass of the K5 hash-count
+    kernel for all lengths (LDS-privatised table, global open addressing); CPU: per-length device
+    sort (torch.unique).  Returns {length: (sorted keys, counts)}."""
+    N, L = states.shape
     base = n_states + 1
+    gmul = base ** max_len
+    if group is not None:
+        gmax = int(group.max()) + 1 if group.numel() else 1
+        if gmul * gmax >= (1 << 58):
+            raise ValueError("n-gram key space (groups x (S+1)^max_len) exceeds 2^58")
+    elif gmul >= (1 << 58):
+        raise ValueError("n-gram key space (S+1)^max_len exceeds 2^58")
+    if states.is_cuda:
+        st = states.to(torch.int16).contiguous()
+        g = group.to(torch.int32).contiguous() if group is not None else None
+        windows = sum(max(0, L - k + 1) for k in range(min_len, max_len + 1)) * N
+        space = sum(base ** k for k in range(min_len, max_len + 1)) * (gmax if group is not None else 1)
+        cap = 1 << max(10, int(2 * min(windows, space) + 1).bit_length())
+        keys, counts = _native.C().ngram_count(st, n_states, min_len, max_len, g, gmul, min(cap, 1 << 30))
+        keys, order = torch.sort(keys)
+        counts = counts[order]
+        ln = keys >> 58
+        keys = keys & ((1 << 58) - 1)
+        out = {}
+        for k in range(min_len, max_len + 1):
+            if k > L:
+                break
+            m = ln == k
+            out[k] = (keys[m], counts[m])
+        return out
+    s = states.long()
     out = {}
     for k in range(min_len, max_len + 1):
         if k > L:
@@ -86,10 +114,46 @@ def ngram_counts(states: torch.Tensor, n_states: int, min_len: int = 2, max_len:
             ok &= (col >= 0) & (col < n_states)
             key = key * base + col.clamp_min(0)
         if group is not None:
-            key = key + group.long().view(-1, 1) * (base ** max_len)
+            key = key + group.long().view(-1, 1) * gmul
         keys, counts = torch.unique(key[ok], return_counts=True)
         out[k] = (keys, counts)
     return out
+
+
+def uniformization_sums(P: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor,
+                        steps: list[int]) -> tuple[torch.Tensor, torch.Tensor]:
+    """A_b = sum_{k<=steps[b]} w1[b,k] P^k and B_b = sum w2[b,k] P^k for B problems sharing one
+    S x S matrix (S <= 64): the K16 power-chain kernel on GPU (P^k never leaves LDS), repeated
+    fp64 matmuls on CPU.  w1, w2 [B, ldw] with ldw > max(steps)."""
+    P = P.double().contiguous()
+    w1 = w1.double().contiguous()
+    w2 = w2.double().contiguous()
+    if P.is_cuda:
+        st = torch.tensor(steps, dtype=torch.int32, device=P.device)
+        out = _native.C().uniformization(P, w1, w2, st, [int(s) for s in steps])
+        return out[:, 0], out[:, 1]
+    S = P.shape[0]
+    A = torch.zeros((len(steps), S, S), dtype=torch.float64)
+    B = torch.zeros_like(A)
+    for b, L in enumerate(steps):
+        cur = torch.eye(S, dtype=torch.float64)
+        for k in range(L + 1):
+            if k:
+                cur = cur @ P
+            A[b] += w1[b, k] * cur
+            B[b] += w2[b, k] * cur
+    return A, B
+
+
+def dot_matrix_hits(ida: torch.Tensor, idb: torch.Tensor) -> torch.Tensor:
+    """hits[i, j] = #{(p, q): ida[i, p] == idb[j, q] >= 0} (K19 on GPU).  Inputs are int32 window
+    ids (negative = invalid window)."""
+    if ida.is_cuda:
+        return _native.C().dot_matrix(ida.to(torch.int32).contiguous(), idb.to(torch.int32).contiguous())
+    a = ida.long()
+    b = torch.where(idb.long() < 0, torch.full_like(idb.long(), -2), idb.long())
+    eq = a.unsqueeze(1).unsqueeze(3) == b.unsqueeze(0).unsqueeze(2)
+    return eq.sum((2, 3)).to(torch.int32)
 
 
 def decode_ngram(key: int, k: int, n_states: int, max_len: int | None = None) -> tuple[int, list[int]]:

@@ -156,19 +156,17 @@ def test_kmeans_gpu_matches_cpu(cuda):
 
 @pytest.mark.gpu
 def test_kmeans_step_kernel_matches_oracle(cuda):
-    from avenir_amd import _native
-    from avenir_amd.models.cluster import KMeans
-    for D, k in ((2, 3), (16, 16), (5, 40)):
+    from avenir_amd.models.cluster import KMeans, kmeans_step
+    # (D, k): MFMA variant with 1, 2 and 4 centroid blocks, odd k (pair padding), D padding,
+    # and a group large enough for the LDS fallback variant (k 300 at D 16: 32 centroid blocks)
+    for D, k in ((2, 3), (16, 16), (5, 40), (33, 7), (16, 300)):
         g = torch.Generator().manual_seed(D + k)
         X = torch.randn((50_000, D), generator=g)
         C = torch.randn((k, D), generator=g)
         Dp = next(p for p in (2, 4, 8, 16, 32, 64) if p >= D)
         Xp = torch.zeros((X.shape[0], Dp))
         Xp[:, :D] = X
-        Cp = torch.zeros((k, Dp))
-        Cp[:, :D] = C
-        sums, counts, sse, assign = _native.C().kmeans_step(Xp.to(cuda), Cp.to(cuda), [k], True)
-        assign = assign[0]
+        sums, counts, sse, assign = kmeans_step(Xp.to(cuda), [C.to(cuda)], True)[0]
         d2 = torch.cdist(X.double(), C.double()) ** 2
         ref_a = d2.argmin(1)
         agree = float((assign.cpu().long() == ref_a).float().mean())
@@ -183,13 +181,14 @@ def test_kmeans_step_kernel_matches_oracle(cuda):
     gpu = KMeans([3, 4, 5], n_init=2, max_iter=10, seed=3).fit(X.to(cuda))     # 6 runs, one launch / iter
     for k in (3, 4, 5):
         assert gpu.best[k].sse == pytest.approx(cpu.best[k].sse, rel=1e-3)
+        assert len(gpu.best[k].history) == gpu.best[k].iterations
     # multi-run launch equals single-run launches
-    C1 = torch.randn((3, 4), generator=torch.Generator().manual_seed(5))
-    C2 = torch.randn((7, 4), generator=torch.Generator().manual_seed(6))
+    C1 = torch.randn((3, 4), generator=torch.Generator().manual_seed(5)).to(cuda)
+    C2 = torch.randn((7, 4), generator=torch.Generator().manual_seed(6)).to(cuda)
     X4 = torch.randn((30_000, 4), generator=torch.Generator().manual_seed(7)).to(cuda)
-    s_all, c_all, e_all, a_all = _native.C().kmeans_step(X4, torch.cat([C1, C2]).to(cuda), [3, 7], True)
-    s1, c1, e1, a1 = _native.C().kmeans_step(X4, C1.to(cuda), [3], True)
-    s2, c2, e2, a2 = _native.C().kmeans_step(X4, C2.to(cuda), [7], True)
-    assert torch.equal(a_all[0], a1[0]) and torch.equal(a_all[1], a2[0])
-    assert torch.allclose(s_all, torch.cat([s1, s2]), rtol=1e-5, atol=1e-3)
-    assert torch.allclose(e_all, torch.cat([e1, e2]), rtol=1e-6)
+    both = kmeans_step(X4, [C1, C2], True)
+    one = kmeans_step(X4, [C1], True) + kmeans_step(X4, [C2], True)
+    for (s_a, c_a, e_a, a_a), (s_b, c_b, e_b, a_b) in zip(both, one):
+        assert torch.equal(a_a, a_b) and torch.equal(c_a, c_b)
+        assert torch.allclose(s_a, s_b, rtol=1e-5, atol=1e-3)
+        assert float(e_a) == pytest.approx(float(e_b), rel=1e-6)

@@ -150,3 +150,52 @@ def test_sequence_kernels_gpu(cuda):
         fc = dec.log_likelihood(obs)
         fg = dec.log_likelihood(obs.to(cuda)).cpu()
         assert torch.allclose(fc, fg, rtol=1e-4, atol=1e-3)
+
+
+def test_ctmc_batched_sums_and_dot_matrix_oracle():
+    Q = torch.tensor([[-0.5, 0.3, 0.2], [0.1, -0.4, 0.3], [0.2, 0.2, -0.4]], dtype=torch.float64)
+    stats = M.ContTimeStateTransitionStats(Q)
+    A, B = stats.sums([0.5, 2.0, 7.0])
+    for b, t in enumerate([0.5, 2.0, 7.0]):
+        assert torch.allclose(A[b], torch.linalg.matrix_exp(Q * t), atol=1e-8)
+        assert torch.allclose(B[b].sum(1), torch.full((3,), t, dtype=torch.float64), atol=1e-6)
+    ida = torch.tensor([[0, 1, 2, -1], [3, 3, 0, 1]], dtype=torch.int32)
+    idb = torch.tensor([[1, 1, 9], [-1, -1, -1]], dtype=torch.int32)
+    assert SO.dot_matrix_hits(ida, idb).tolist() == [[2, 0], [2, 0]]
+
+
+@pytest.mark.gpu
+def test_seqmine_kernels_gpu(cuda):
+    # K5: n-gram hash counting (hot short n-grams collide in the LDS table; many distinct long ones)
+    gen = torch.Generator().manual_seed(0)
+    for S, N, L, lo, hi in ((4, 20000, 24, 2, 5), (40, 3000, 50, 1, 4)):
+        st = torch.randint(0, S, (N, L), generator=gen, dtype=torch.int16)
+        st[::5, L - 7:] = -1
+        st[3::11, 4] = -1
+        grp = torch.randint(0, 3, (N,), generator=gen, dtype=torch.int32)
+        for g in (None, grp):
+            ref = SO.ngram_counts(st, S, lo, hi, g)
+            got = SO.ngram_counts(st.to(cuda), S, lo, hi, None if g is None else g.to(cuda))
+            assert sorted(ref) == sorted(got)
+            for k in ref:
+                assert torch.equal(ref[k][0], got[k][0].cpu()) and torch.equal(ref[k][1], got[k][1].cpu())
+    # K16: uniformisation power chain against matrix_exp / the CPU chain
+    rng = np.random.default_rng(1)
+    for S in (3, 17, 64):
+        R = torch.tensor(rng.uniform(0.05, 1.0, (S, S)))
+        R.fill_diagonal_(0)
+        Q = R - torch.diag(R.sum(1))
+        cpu = M.ContTimeStateTransitionStats(Q)
+        gpu = M.ContTimeStateTransitionStats(Q.to(cuda))
+        ts = [0.1, 1.0, 3.0]
+        Ac, Bc = cpu.sums(ts)
+        Ag, Bg = gpu.sums(ts)
+        assert torch.allclose(Ac, Ag.cpu(), atol=1e-10) and torch.allclose(Bc, Bg.cpu(), atol=1e-9)
+        assert torch.allclose(Ag[1].cpu(), torch.linalg.matrix_exp(Q), atol=1e-8)
+    # K19: dot-matrix window matching, window ids longer than one LDS chunk
+    for n, m, Wa, Wb in ((37, 50, 20, 33), (20, 18, 300, 270)):
+        ida = torch.randint(-1, 40, (n, Wa), generator=gen, dtype=torch.int32)
+        idb = torch.randint(-1, 40, (m, Wb), generator=gen, dtype=torch.int32)
+        assert torch.equal(SO.dot_matrix_hits(ida, idb), SO.dot_matrix_hits(ida.to(cuda), idb.to(cuda)).cpu())
+    A = torch.randint(0, 4, (64, 40), generator=gen)
+    assert torch.allclose(M.dot_matrix_similarity(A, A[:9], 3), M.dot_matrix_similarity(A.to(cuda), A[:9].to(cuda), 3).cpu())
