@@ -728,7 +728,7 @@ std::vector<at::Tensor> kmeans_assign(const at::Tensor& X, const at::Tensor& C2,
   TORCH_CHECK(K <= 4096, "at most 4096 centroids per launch");
   TORCH_CHECK(C2.numel() == K * D && Cn.numel() == K, "C2 must hold Kp * D values and Cn Kp norms");
   DevGuard g(X.device());
-  const int grid = avk::kmeans_grid(n);
+  const int grid = avk::kmeans_grid(n, (int)D, (int)K, (int)R);
   auto partial = at::empty({grid, K, D + 1}, X.options());
   auto ssep = at::empty({grid, R}, X.options().dtype(at::kDouble));
   at::Tensor assign;

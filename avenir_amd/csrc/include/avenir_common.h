@@ -121,6 +121,11 @@ __device__ __forceinline__ u4 philox_draw(uint64_t seed, uint64_t offset, uint64
   return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// Workgroups of `kernel` (block threads, lds dynamic bytes) resident on the whole device at once
+// (occupancy x CUs).  A grid-stride kernel launched with more workgroups than this runs a second,
+// partial round at lower occupancy; host/runtime.cpp.
+int resident_blocks(const void* kernel, int block, size_t lds);
+
 // Grid sizing for memory-bound streaming kernels: enough waves to fill 256 CUs several times
 // over, capped so the tail is short (Guideline 11).
 inline int stream_grid(long long work_items, int block, int per_thread = 1, int cap = 2048) {

@@ -100,7 +100,7 @@ void weighted_gram(const float* X, long long ld, long long n, int D, const float
                    hipStream_t stream);
 
 // ---- cluster.hip (K16) ---------------------------------------------------------------------
-int kmeans_grid(long long n);
+int kmeans_grid(long long n, int D, int K, int R);
 void kmeans_assign(const float* X, long long n, int D, const float* C2, const float* Cn, const int* roff, int R, int K,
                    int* assign, float* partial, double* sse_partial, int grid, hipStream_t stream);
 void kmeans_reduce(const float* partial, const double* sse_partial, int grid, int K, int D, int R, double* out,

@@ -354,35 +354,22 @@ __global__ __launch_bounds__(1024) void kmeans_update_kernel(const double* __res
   if (threadIdx.x < R) moves[threadIdx.x] = __uint_as_float(mx[threadIdx.x]);
 }
 
-}  // namespace
+// Kernel variant for (D, K, R): the MFMA kernel when its accumulators fit (<= 16 blocks of 16
+// centroids x 16 dims), else the LDS kernel.  Returns nullptr when neither fits.
+struct KmVariant {
+  const void* fn;
+  size_t lds;
+  bool mfma;
+};
 
-namespace avk {
-
-int kmeans_grid(long long n) {
-  // ~16K rows per workgroup, between 256 and 4096 workgroups
-  long long g = (n + 16383) / 16384;
-  return (int)std::max(256LL, std::min(g, 4096LL));
-}
-
-void kmeans_assign(const float* X, long long n, int D, const float* C2, const float* Cn, const int* roff, int R, int K,
-                   int* assign, float* partial, double* sse_partial, int grid, hipStream_t stream) {
-  if (R < 1 || R > MAX_RUNS) throw std::runtime_error("kmeans_assign: 1 <= runs <= 16");
-  if (K & 1) throw std::runtime_error("kmeans_assign: padded centroid count must be even");
+KmVariant km_variant(int D, int K, int R) {
   const int DP = D < 16 ? 16 : D;
   int KBt = 1;
   while (KBt * 16 < K) KBt *= 2;
   if (KBt * (DP / 16) <= 16) {
     const size_t lds = sizeof(float) * (4 * 64 * (size_t)DP + 4 * 64 * (size_t)R + K + (size_t)K * D);
-    if (lds > 160 * 1024) throw std::runtime_error("kmeans_assign: LDS budget exceeded");
-#define AVK_KMM(DD, KK)                                                                                       \
-  if (D == DD && KBt == KK) {                                                                                 \
-    if (lds > 64 * 1024)                                                                                      \
-      AV_HIP_CHECK(hipFuncSetAttribute((const void*)kmeans_mfma_kernel<DD, KK>,                               \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                \
-    kmeans_mfma_kernel<DD, KK><<<grid, KB, lds, stream>>>(X, n, C2, Cn, roff, R, K, assign, partial, sse_partial); \
-    AV_HIP_CHECK(hipGetLastError());                                                                          \
-    return;                                                                                                   \
-  }
+#define AVK_KMM(DD, KK) \
+  if (D == DD && KBt == KK) return {(const void*)kmeans_mfma_kernel<DD, KK>, lds, true};
     AVK_KMM(2, 1) AVK_KMM(2, 2) AVK_KMM(2, 4) AVK_KMM(2, 8) AVK_KMM(2, 16)
     AVK_KMM(4, 1) AVK_KMM(4, 2) AVK_KMM(4, 4) AVK_KMM(4, 8) AVK_KMM(4, 16)
     AVK_KMM(8, 1) AVK_KMM(8, 2) AVK_KMM(8, 4) AVK_KMM(8, 8) AVK_KMM(8, 16)
@@ -390,20 +377,51 @@ void kmeans_assign(const float* X, long long n, int D, const float* C2, const fl
     AVK_KMM(32, 1) AVK_KMM(32, 2) AVK_KMM(32, 4) AVK_KMM(32, 8)
     AVK_KMM(64, 1) AVK_KMM(64, 2) AVK_KMM(64, 4)
 #undef AVK_KMM
-    throw std::runtime_error("kmeans_assign: D must be 2, 4, 8, 16, 32 or 64");
+    return {nullptr, 0, true};
   }
   const size_t lds = sizeof(float) * ((size_t)K * D + K + (size_t)K * (D + 1));
-  if (lds > 64 * 1024) throw std::runtime_error("kmeans_assign: total centroids * D too large for LDS");
   switch (D) {
-#define AVK_KM(DD)                                                                                                \
-  case DD:                                                                                                        \
-    kmeans_step_kernel<DD><<<grid, KB, lds, stream>>>(X, n, C2, Cn, roff, R, assign, partial, sse_partial); \
-    break;
-    AVK_KM(2) AVK_KM(4) AVK_KM(8) AVK_KM(16) AVK_KM(32) AVK_KM(64)
-#undef AVK_KM
-    default: throw std::runtime_error("kmeans_assign: D must be 2, 4, 8, 16, 32 or 64");
+    case 2: return {(const void*)kmeans_step_kernel<2>, lds, false};
+    case 4: return {(const void*)kmeans_step_kernel<4>, lds, false};
+    case 8: return {(const void*)kmeans_step_kernel<8>, lds, false};
+    case 16: return {(const void*)kmeans_step_kernel<16>, lds, false};
+    case 32: return {(const void*)kmeans_step_kernel<32>, lds, false};
+    case 64: return {(const void*)kmeans_step_kernel<64>, lds, false};
+    default: return {nullptr, 0, false};
   }
-  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+namespace avk {
+
+int kmeans_grid(long long n, int D, int K, int R) {
+  // ~16K rows per workgroup, between 256 and 4096 workgroups, but never more than are resident at
+  // once (a second partial round of workgroups runs at lower occupancy)
+  long long g = std::max(256LL, std::min((n + 16383) / 16384, 4096LL));
+  const KmVariant v = km_variant(D, K, R);
+  if (v.fn && v.lds <= 160 * 1024) {
+    if (v.lds > 64 * 1024)
+      AV_HIP_CHECK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
+    g = std::min<long long>(g, av::resident_blocks(v.fn, KB, v.lds));
+  }
+  return (int)g;
+}
+
+void kmeans_assign(const float* X, long long n, int D, const float* C2, const float* Cn, const int* roff, int R, int K,
+                   int* assign, float* partial, double* sse_partial, int grid, hipStream_t stream) {
+  if (R < 1 || R > MAX_RUNS) throw std::runtime_error("kmeans_assign: 1 <= runs <= 16");
+  if (K & 1) throw std::runtime_error("kmeans_assign: padded centroid count must be even");
+  const KmVariant v = km_variant(D, K, R);
+  if (!v.fn) throw std::runtime_error("kmeans_assign: D must be 2, 4, 8, 16, 32 or 64");
+  if (v.lds > (v.mfma ? 160 : 64) * 1024) throw std::runtime_error("kmeans_assign: LDS budget exceeded");
+  if (v.lds > 64 * 1024)
+    AV_HIP_CHECK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
+  void* args[] = {(void*)&X, (void*)&n, (void*)&C2, (void*)&Cn, (void*)&roff, (void*)&R, (void*)&K,
+                  (void*)&assign, (void*)&partial, (void*)&sse_partial};
+  void* args_lds[] = {(void*)&X, (void*)&n, (void*)&C2, (void*)&Cn, (void*)&roff, (void*)&R,
+                      (void*)&assign, (void*)&partial, (void*)&sse_partial};
+  AV_HIP_CHECK(hipLaunchKernel(v.fn, dim3(grid), dim3(KB), v.mfma ? args : args_lds, v.lds, stream));
 }
 
 void kmeans_reduce(const float* partial, const double* sse_partial, int grid, int K, int D, int R, double* out,

@@ -142,6 +142,19 @@ def test_class_histogram_gpu(cuda, n, bins, C, mode):
 
 
 @pytest.mark.gpu
+def test_class_histogram_gpu_skewed_long_run(cuda):
+    """Every row in ONE bin and class over 2^28 rows: each lane's 16-bit counters grow past what a
+    64-lane sum of 16-bit fields can hold, so the kernel must widen before the cross-lane sum."""
+    n = 1 << 28
+    codes = torch.ones((2, n), dtype=torch.uint8, device=cuda)
+    codes[1] = 2
+    lab = torch.zeros(n, dtype=torch.uint8, device=cuda)
+    got = H.class_histogram(codes, n, [4, 3], lab, 2, count_labels=True).cpu()
+    assert int(got[0, 1]) == n and int(got[0, 4 + 2]) == n and int(got[0, -1]) == n
+    assert int(got.sum()) == 3 * n
+
+
+@pytest.mark.gpu
 def test_pair_bigram_moments_gpu(cuda):
     n, bins, C = 70_001, [4, 6, 3], 3
     codes, lab = _random_codes(n, bins, C, seed=1)
