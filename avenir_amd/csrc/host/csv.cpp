@@ -202,10 +202,11 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
             if ((int)fields.size() > max_ord) break;
           }
         }
+        bool short_row = false;
         for (int o = 0; o <= max_ord; ++o) {
           if (by_ord[o].empty()) continue;
           const bool have = o < (int)fields.size();
-          if (!have) ++bad[t];
+          short_row |= !have;
           for (int si : by_ord[o]) {
             const ColSpec& sp = specs[si];
             switch (sp.kind) {
@@ -241,6 +242,7 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
             }
           }
         }
+        if (short_row) ++bad[t];
       }
     });
   }
