@@ -26,6 +26,9 @@ hipStream_t cur_stream(const at::Tensor& t) {
   CHECK_CUDA(t);     \
   CHECK_CONTIG(t)
 
+// vector loads in the kernels need the base address aligned (a sliced view may not be)
+bool aligned(const at::Tensor& t, int bytes) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes == 0; }
+
 template <typename T>
 T* ptr_or_null(const c10::optional<at::Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
@@ -240,7 +243,10 @@ void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels
   CHECK_DTYPE(labels, at::kByte);
   CHECK_DEV(node);
   CHECK_DTYPE(node, at::kInt);
-  TORCH_CHECK(labels.numel() >= n && node.numel() >= n, "labels/node too short");
+  const int64_t n4 = (n + 3) / 4 * 4;  // the kernels read whole 4-row quads
+  TORCH_CHECK(labels.numel() >= n4 && node.numel() >= n4, "labels/node must cover n rounded up to 4");
+  TORCH_CHECK(codes.size(1) % 4 == 0, "codes leading dimension must be a multiple of 4");
+  TORCH_CHECK(aligned(node, 16) && aligned(labels, 4) && aligned(codes, 4), "node / labels / codes misaligned");
   CHECK_DEV(bins);
   CHECK_DEV(offs);
   TORCH_CHECK(bins.numel() == codes.size(0) && offs.numel() == codes.size(0), "bins/offs != F");
@@ -251,7 +257,7 @@ void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels
   if (weight.has_value() && weight->defined()) {
     CHECK_DEV((*weight));
     CHECK_DTYPE((*weight), at::kByte);
-    TORCH_CHECK(weight->numel() >= n, "weight too short");
+    TORCH_CHECK(weight->numel() >= n4 && aligned(*weight, 4), "weight must cover n rounded up to 4, 4-byte aligned");
     w = weight->data_ptr<uint8_t>();
   }
   DevGuard g(codes.device());
@@ -271,7 +277,10 @@ void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& n
   CHECK_DTYPE(g, at::kFloat);
   CHECK_DEV(h);
   CHECK_DTYPE(h, at::kFloat);
-  TORCH_CHECK(node.numel() >= n && g.numel() >= n && h.numel() >= n, "node/g/h too short");
+  const int64_t n4 = (n + 3) / 4 * 4;  // the kernel reads whole 4-row quads
+  TORCH_CHECK(node.numel() >= n4 && g.numel() >= n4 && h.numel() >= n4, "node/g/h must cover n rounded up to 4");
+  TORCH_CHECK(codes.size(1) % 4 == 0, "codes leading dimension must be a multiple of 4");
+  TORCH_CHECK(aligned(node, 16) && aligned(g, 16) && aligned(h, 16) && aligned(codes, 4), "node / g / h / codes misaligned");
   CHECK_DEV(out);
   CHECK_DTYPE(out, at::kLong);
   TORCH_CHECK(out.numel() == n_nodes * total_bins * 2, "out must be [A, TB, 2]");

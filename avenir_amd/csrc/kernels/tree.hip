@@ -18,6 +18,12 @@ namespace {
 
 constexpr int TB_THREADS = 256;
 
+// Both histogram kernels give each lane 4 consecutive rows per step: the node ids / labels / weights
+// / gradients of the 4 rows and, for a chunk of 8 features, the 8 x 4 codes are fetched with wide
+// loads before any LDS atomic is issued, so the HBM latency of a step is paid once instead of once
+// per feature (the first version loaded one byte per feature and waited on each).
+constexpr int FCH = 8;  // features whose codes are in flight together
+
 // hist layout: [A][C][TB] uint64; node ids are LOCAL indices of the active frontier (-1 = skip).
 // Each block owns a contiguous range of nodes [a0, a0 + na) held in LDS (uint32), so rows of other
 // nodes are skipped; grid.y walks node chunks.
@@ -32,18 +38,38 @@ __global__ __launch_bounds__(TB_THREADS) void node_hist_kernel(
   const int per_node = n_classes * total_bins;
   for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) s_h[i] = 0;
   __syncthreads();
+  const long long nq = (n + 3) >> 2;  // 4-row quads (ld is a multiple of 16: quads never cross it)
   const long long stride = (long long)gridDim.x * TB_THREADS;
-  for (long long r = (long long)blockIdx.x * TB_THREADS + threadIdx.x; r < n; r += stride) {
-    const int a = node[r] - a0;
-    if (a < 0 || a >= na) continue;
-    const unsigned c = labels[r];
-    if (c >= (unsigned)n_classes) continue;
-    const unsigned w = weight ? weight[r] : 1u;
-    if (w == 0) continue;
-    unsigned int* h = s_h + a * per_node + c * total_bins;
-    for (int f = 0; f < nfeat; ++f) {
-      const unsigned v = codes[(long long)f * ld + r];
-      if (v < (unsigned)bins[f]) atomicAdd(&h[offs[f] + v], w);
+  for (long long q = (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < nq; q += stride) {
+    const long long r0 = q * 4;
+    const int4 nd4 = *reinterpret_cast<const int4*>(node + r0);
+    const uchar4 lb4 = *reinterpret_cast<const uchar4*>(labels + r0);
+    const uchar4 w4 = weight ? *reinterpret_cast<const uchar4*>(weight + r0) : make_uchar4(1, 1, 1, 1);
+    int a[4] = {nd4.x - a0, nd4.y - a0, nd4.z - a0, nd4.w - a0};
+    const unsigned c[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
+    const unsigned w[4] = {w4.x, w4.y, w4.z, w4.w};
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = r0 + j < n && a[j] >= 0 && a[j] < na && c[j] < (unsigned)n_classes && w[j] != 0;
+      if (!ok) a[j] = -1;
+      any |= ok;
+    }
+    if (!any) continue;
+    for (int f0 = 0; f0 < nfeat; f0 += FCH) {
+      uchar4 v4[FCH];
+#pragma unroll
+      for (int k = 0; k < FCH; ++k)
+        if (f0 + k < nfeat) v4[k] = *reinterpret_cast<const uchar4*>(codes + (long long)(f0 + k) * ld + r0);
+#pragma unroll
+      for (int k = 0; k < FCH; ++k) {
+        if (f0 + k >= nfeat) break;
+        const unsigned B = (unsigned)bins[f0 + k], o = (unsigned)offs[f0 + k];
+        const unsigned v[4] = {v4[k].x, v4[k].y, v4[k].z, v4[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (a[j] >= 0 && v[j] < B) atomicAdd(&s_h[a[j] * per_node + c[j] * total_bins + o + v[j]], w[j]);
+      }
     }
   }
   __syncthreads();
@@ -66,20 +92,44 @@ __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
   const int per_node = total_bins * 2;
   for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) s_g[i] = 0;
   __syncthreads();
+  const long long nq = (n + 3) >> 2;
   const long long stride = (long long)gridDim.x * TB_THREADS;
   const float S = 16777216.0f;
-  for (long long r = (long long)blockIdx.x * TB_THREADS + threadIdx.x; r < n; r += stride) {
-    const int a = node[r] - a0;
-    if (a < 0 || a >= na) continue;
-    const long long gi = __float2ll_rn(g[r] * S);
-    const long long hi = __float2ll_rn(h[r] * S);
-    long long* base = s_g + a * per_node;
-    for (int f = 0; f < nfeat; ++f) {
-      const unsigned v = codes[(long long)f * ld + r];
-      if (v < (unsigned)bins[f]) {
-        const int b = offs[f] + v;
-        atomicAdd((unsigned long long*)&base[2 * b], (unsigned long long)gi);
-        atomicAdd((unsigned long long*)&base[2 * b + 1], (unsigned long long)hi);
+  for (long long q = (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < nq; q += stride) {
+    const long long r0 = q * 4;
+    const int4 nd4 = *reinterpret_cast<const int4*>(node + r0);
+    int a[4] = {nd4.x - a0, nd4.y - a0, nd4.z - a0, nd4.w - a0};
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = r0 + j < n && a[j] >= 0 && a[j] < na;
+      if (!ok) a[j] = -1;
+      any |= ok;
+    }
+    if (!any) continue;
+    const float4 g4 = *reinterpret_cast<const float4*>(g + r0);
+    const float4 h4 = *reinterpret_cast<const float4*>(h + r0);
+    const long long gi[4] = {__float2ll_rn(g4.x * S), __float2ll_rn(g4.y * S), __float2ll_rn(g4.z * S),
+                             __float2ll_rn(g4.w * S)};
+    const long long hi[4] = {__float2ll_rn(h4.x * S), __float2ll_rn(h4.y * S), __float2ll_rn(h4.z * S),
+                             __float2ll_rn(h4.w * S)};
+    for (int f0 = 0; f0 < nfeat; f0 += FCH) {
+      uchar4 v4[FCH];
+#pragma unroll
+      for (int k = 0; k < FCH; ++k)
+        if (f0 + k < nfeat) v4[k] = *reinterpret_cast<const uchar4*>(codes + (long long)(f0 + k) * ld + r0);
+#pragma unroll
+      for (int k = 0; k < FCH; ++k) {
+        if (f0 + k >= nfeat) break;
+        const unsigned B = (unsigned)bins[f0 + k], o = (unsigned)offs[f0 + k];
+        const unsigned v[4] = {v4[k].x, v4[k].y, v4[k].z, v4[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (a[j] >= 0 && v[j] < B) {
+            long long* base = s_g + a[j] * per_node + 2 * (o + v[j]);
+            atomicAdd((unsigned long long*)&base[0], (unsigned long long)gi[j]);
+            atomicAdd((unsigned long long*)&base[1], (unsigned long long)hi[j]);
+          }
       }
     }
   }
@@ -156,6 +206,10 @@ __global__ __launch_bounds__(TB_THREADS) void tree_predict_kernel(
 
 namespace avk {
 
+// LDS per workgroup for the node tables: 32 KiB keeps 4+ workgroups per CU (measured better than
+// 64 KiB even though more node chunks re-read the rows).
+static long long tree_lds_budget() { return 32 * 1024; }
+
 void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
                     const int* node, const uint8_t* weight, const int* bins, const int* offs,
                     int nfeat, int total_bins, int n_classes, int n_nodes, unsigned long long* hist,
@@ -163,9 +217,9 @@ void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8
   if (n <= 0 || n_nodes <= 0) return;
   const long long per_node_bytes = 4LL * n_classes * total_bins;
   if (per_node_bytes > 64 * 1024) throw std::runtime_error("node_histogram: per-node table exceeds LDS");
-  const int npc = (int)std::max<long long>(1, std::min<long long>(n_nodes, (64 * 1024) / per_node_bytes));
+  const int npc = (int)std::max<long long>(1, std::min<long long>(n_nodes, tree_lds_budget() / per_node_bytes));
   const int chunks = (n_nodes + npc - 1) / npc;
-  const int gx = std::max(1, std::min(av::stream_grid(n, TB_THREADS, 8, 2048), std::max(64, 4096 / chunks)));
+  const int gx = std::max(1, std::min(av::stream_grid((n + 3) / 4, TB_THREADS, 2, 2048), std::max(64, 4096 / chunks)));
   dim3 grid(gx, chunks);
   node_hist_kernel<<<grid, TB_THREADS, per_node_bytes * npc, stream>>>(
       codes, ld, n, labels, node, weight, bins, offs, nfeat, total_bins, n_classes, npc, n_nodes, hist);
@@ -178,9 +232,9 @@ void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const 
   if (n <= 0 || n_nodes <= 0) return;
   const long long per_node_bytes = 16LL * total_bins;
   if (per_node_bytes > 64 * 1024) throw std::runtime_error("node_grad_histogram: table exceeds LDS");
-  const int npc = (int)std::max<long long>(1, std::min<long long>(n_nodes, (64 * 1024) / per_node_bytes));
+  const int npc = (int)std::max<long long>(1, std::min<long long>(n_nodes, tree_lds_budget() / per_node_bytes));
   const int chunks = (n_nodes + npc - 1) / npc;
-  const int gx = std::max(1, std::min(av::stream_grid(n, TB_THREADS, 8, 2048), std::max(64, 4096 / chunks)));
+  const int gx = std::max(1, std::min(av::stream_grid((n + 3) / 4, TB_THREADS, 2, 2048), std::max(64, 4096 / chunks)));
   dim3 grid(gx, chunks);
   node_grad_hist_kernel<<<grid, TB_THREADS, per_node_bytes * npc, stream>>>(
       codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, out);

@@ -508,12 +508,10 @@ class DecisionTreeBuilder:
                     (rc.double() / max(pop, 1)).tolist(), depth=1)
         nodes = [root]
         frontier = [0]  # global node indices of the active frontier (local index = position)
+        hist = root_hist  # [A, C, TB] of the frontier; later levels: built + derived by subtraction
         while frontier:
             t0 = time.perf_counter()
             A = len(frontier)
-            hist = T.node_histogram(codes, t.n, labels, node, weight, bins, C, A)  # [A, C, TB]
-            if comm.is_distributed:
-                comm.all_reduce(hist)
             hist_t = hist.transpose(1, 2).double()  # [A, TB, C]
             # ---- score every candidate split of every attribute, all nodes at once ----
             cand_masks = torch.zeros((A, F), dtype=torch.bool)
@@ -589,6 +587,7 @@ class DecisionTreeBuilder:
                     seg_counts[a] = torch.einsum("gb,bc->gc", seg_tensors[f][s], hb).round().long().cpu()
             # ---- create children ----
             new_frontier: list[int] = []
+            derived: list[tuple[int, int, list[int]]] = []   # (global child, parent slot, built sibling gis)
             max_bins = max(bins)
             max_seg = 2
             for a in range(A):
@@ -621,6 +620,7 @@ class DecisionTreeBuilder:
                 nd.children = []
                 split_feat[a] = f
                 segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
+                kids = []
                 for g in range(sc.shape[0]):
                     cnt = sc[g]
                     pop = int(cnt.sum())
@@ -635,11 +635,37 @@ class DecisionTreeBuilder:
                     ci = len(nodes)
                     nodes.append(child)
                     nd.children.append(ci)
-                    if not stop:
+                    kids.append((g, ci, pop, stop))
+                # histogram subtraction: when every row of the parent lands in a frontier child, the
+                # most populated child's histogram is the parent's minus its built siblings'
+                live = [k for k in kids if not k[3]]
+                whole = sum(k[2] for k in kids) == nd.population and len(live) == len(kids) and len(live) >= 2
+                heavy = max(live, key=lambda k: k[2])[1] if whole else -1
+                for g, ci, _, stop in kids:
+                    if not stop and ci != heavy:
                         child_of[a, g] = len(new_frontier)
                         new_frontier.append(ci)
+                if heavy >= 0:
+                    derived.append((heavy, a, [ci for _, ci, _, _ in live if ci != heavy]))
+            # derived children take the ids after the built ones: the histogram pass skips their rows
+            slot = {ci: k for k, ci in enumerate(new_frontier)}
+            m = len(new_frontier)
+            for j, (ci, a, _) in enumerate(derived):
+                g = nodes[frontier[a]].children.index(ci)
+                child_of[a, g] = m + j
             T.tree_assign(codes, t.n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
-            frontier = new_frontier
+            if new_frontier or derived:
+                hs = T.node_histogram(codes, t.n, labels, node, weight, bins, C, m)   # built children only
+                if comm.is_distributed:
+                    comm.all_reduce(hs)
+                parts = [hs]
+                for ci, a, sibs in derived:
+                    dh = hist[a].clone()
+                    for sg in sibs:
+                        dh -= hs[slot[sg]]
+                    parts.append(dh.unsqueeze(0))
+                hist = torch.cat(parts) if len(parts) > 1 else hs
+            frontier = new_frontier + [ci for ci, _, _ in derived]
             self.level_times.append(time.perf_counter() - t0)
         cls = t.class_field.cardinality if t.class_field else ["_"]
         return DecisionTree(nodes, space, list(cls))
@@ -848,6 +874,10 @@ class GradientBoostedTrees:
         self.train_loss: list[float] = []
 
     def _tree(self, codes, n, g, h, bins, dev) -> DecisionTree:
+        """One regression tree on (g, h).  Per level ONE histogram pass over the rows, and only for
+        the lighter child of every split: the heavier sibling's histogram is the parent's minus the
+        lighter one (exact: the sums are fixed point), and the last level's leaf values come from
+        the split scan itself, so a depth-d tree costs d - 1 half-size passes plus the root pass."""
         comm = self.comm or get_comm()
         p = self.p
         offs = list(itertools.accumulate([0] + bins[:-1]))
@@ -856,24 +886,23 @@ class GradientBoostedTrees:
         nodes = [Node([], n, 0.0, [0.0], depth=0)]
         values = [0.0]
         frontier = [0]
-        G_root = None
-        for depth in range(p.max_depth + 1):
-            A = len(frontier)
-            hist = T.node_grad_histogram(codes, n, node, g, h, bins, A)   # [A, TB, 2] f64
+
+        def grad_hist(A):
+            hh = T.node_grad_histogram(codes, n, node, g, h, bins, A)   # [A, TB, 2] f64
             if comm.is_distributed:
-                comm.all_reduce(hist)
+                comm.all_reduce(hh)
+            return hh
+
+        hist = grad_hist(1)
+        tot = hist[:, offs[-1], :]
+        values[0] = float(-tot[0, 0] / (tot[0, 1] + p.l2).clamp_min(1e-12))
+        sc = self._scan
+        for depth in range(p.max_depth):
+            A = len(frontier)
             tot = hist[:, offs[-1], :]            # the constant total row's single bin
             G, H = tot[:, 0], tot[:, 1]
-            if G_root is None:
-                G_root = G
-            leaf_val = (-G / (H + p.l2).clamp_min(1e-12)).cpu().tolist()
-            for a, gi in enumerate(frontier):
-                values[gi] = leaf_val[a]
-            if depth == p.max_depth:
-                break
             parent = (G * G / (H + p.l2).clamp_min(1e-12))
             # all thresholds of all features at once: segmented cumsum over the feature bins
-            sc = self._scan
             cs = torch.cumsum(hist[:, : sc["nb"], :], 1)                          # [A, NB, 2]
             base = torch.where((sc["start"] > 0).view(1, -1, 1), cs[:, (sc["start"] - 1).clamp_min(0), :],
                                torch.zeros_like(cs))
@@ -885,13 +914,22 @@ class GradientBoostedTrees:
             ok = (hl > 1e-12) & (hr > 1e-12) & sc["valid"].view(1, -1)
             gain = torch.where(ok, gain, torch.full_like(gain, -math.inf))
             best_gain, best_pos = gain.max(1)
-            sel = torch.stack([best_gain, sc["feat"][best_pos].double(), sc["thr"][best_pos].double()]).cpu()
+            bi = best_pos.view(-1, 1)
+            cgl, chl = gl.gather(1, bi)[:, 0], hl.gather(1, bi)[:, 0]
+            cgr, chr_ = gr.gather(1, bi)[:, 0], hr.gather(1, bi)[:, 0]
+            # a parent whose split feature is missing on some rows drops them: subtraction invalid
+            exact = (chl + chr_) == H
+            sel = torch.stack([best_gain, sc["feat"][best_pos].double(), sc["thr"][best_pos].double(),
+                               -cgl / (chl + p.l2).clamp_min(1e-12), -cgr / (chr_ + p.l2).clamp_min(1e-12),
+                               (chl <= chr_).double(), exact.double()]).cpu()
             bg, bf, bb = sel[0].tolist(), [int(v) for v in sel[1].tolist()], [int(v) for v in sel[2].tolist()]
+            vl, vr, lighter_left, ex = sel[3].tolist(), sel[4].tolist(), sel[5].tolist(), sel[6].tolist()
             max_bins = max(bins)
+            last = depth + 1 == p.max_depth
             split_feat = torch.full((A,), -1, dtype=torch.int32)
             segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
             child_of = torch.full((A, 2), -1, dtype=torch.int32)
-            new_frontier = []
+            expand = []                                  # (frontier slot, left id, right id)
             for a, gi in enumerate(frontier):
                 if bf[a] < 0 or not math.isfinite(bg[a]) or bg[a] <= 1e-12:
                     continue
@@ -902,17 +940,32 @@ class GradientBoostedTrees:
                 split_feat[a] = f
                 segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
                 nd.children = []
-                for s in range(2):
+                for s_, v in ((0, vl[a]), (1, vr[a])):
                     ci = len(nodes)
                     nodes.append(Node([], 0, 0.0, [0.0], depth=nd.depth + 1))
-                    values.append(0.0)
+                    values.append(v)
                     nd.children.append(ci)
-                    child_of[a, s] = len(new_frontier)
-                    new_frontier.append(ci)
-            if not new_frontier:
-                break
+                expand.append((a, nd.children[0], nd.children[1]))
+            if not expand or last:
+                break                                    # children are leaves: values already set
+            m = len(expand)
+            subtract = all(ex[a] > 0.5 for a, _, _ in expand)
+            # frontier order: lighter children (ids 0..m-1) first, heavier siblings (m..2m-1) after
+            light, heavy = [], []
+            for k, (a, cl, cr) in enumerate(expand):
+                lt_left = lighter_left[a] > 0.5
+                child_of[a, 0 if lt_left else 1] = k
+                child_of[a, 1 if lt_left else 0] = m + k
+                light.append(cl if lt_left else cr)
+                heavy.append(cr if lt_left else cl)
             T.tree_assign(codes, n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
-            frontier = new_frontier
+            if subtract:
+                hs = grad_hist(m)                                        # lighter children only
+                pa = torch.tensor([a for a, _, _ in expand], dtype=torch.long, device=dev)
+                hist = torch.cat([hs, hist[pa] - hs])
+            else:
+                hist = grad_hist(2 * m)
+            frontier = light + heavy
         for i, nd in enumerate(nodes):
             nd.class_pr = [values[i]]
         return DecisionTree(nodes, self.space, ["value"])

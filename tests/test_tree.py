@@ -256,3 +256,28 @@ def test_forest_and_gbt_gpu(cuda):
     gb = GradientBoostedTrees(schema, GBTParams(n_estimators=10, max_depth=3)).fit(tg)
     gbc = GradientBoostedTrees(schema, GBTParams(n_estimators=10, max_depth=3)).fit(t)
     assert torch.allclose(gb.predict_proba(tg).cpu(), gbc.predict_proba(t), atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_node_histogram_kernels_match_oracle(cuda):
+    """Raw K9 kernels against the CPU oracle: ragged n (not a multiple of the 4-row quads), rows of
+    other frontier nodes / left nodes (-1) / nodes past the chunk, zero weights, missing codes."""
+    from avenir_amd.ops import tree_ops as TO
+    g = torch.Generator().manual_seed(5)
+    n, ld = 100_003, 100_016
+    bins = [5, 9, 2, 17, 3, 8, 4, 11, 6, 1]
+    codes = torch.full((len(bins), ld), 255, dtype=torch.uint8)
+    for f, b in enumerate(bins):
+        codes[f, :n] = torch.randint(0, b + 1, (n,), generator=g).to(torch.uint8)   # b = missing
+    A = 37
+    node = torch.randint(-1, A + 3, (ld,), generator=g, dtype=torch.int32)
+    labels = torch.randint(0, 3, (ld,), generator=g).to(torch.uint8)
+    weight = torch.randint(0, 3, (ld,), generator=g).to(torch.uint8)
+    ref = TO.node_histogram(codes, n, labels, node, weight, bins, 3, A)
+    got = TO.node_histogram(codes.to(cuda), n, labels.to(cuda), node.to(cuda), weight.to(cuda), bins, 3, A)
+    assert torch.equal(got.cpu(), ref)
+    gr = torch.randn(ld, generator=g)
+    hs = torch.rand(ld, generator=g)
+    ref = TO.node_grad_histogram(codes, n, node, gr, hs, bins, A)
+    got = TO.node_grad_histogram(codes.to(cuda), n, node.to(cuda), gr.to(cuda), hs.to(cuda), bins, A)
+    assert torch.equal(got.cpu(), ref)
