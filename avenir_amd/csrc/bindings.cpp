@@ -939,6 +939,76 @@ std::string format_rows(py::object prefix, const at::Tensor& cols, std::vector<i
                           delim.empty() ? ',' : delim[0], nthreads);
 }
 
+// ---------------------------------------------------------------------------------------------
+// K27 LSTM recurrence.  Fragments are packed by avenir_amd/ops/rnn.py (pack_whh): wfrag holds
+// [NW, 4, KS, 64, 8] bf16 (forward), wfragT [NW, 4KS, 64, 8] bf16 (backward); NW = 2 KS.
+int64_t lstm_ks(int64_t H) {
+  TORCH_CHECK(H >= 1 && H <= 128, "fused LSTM supports hidden sizes 1..128");
+  return H <= 32 ? 1 : (H <= 64 ? 2 : 4);  // padded hidden size HP = 32 KS in {32, 64, 128}
+}
+
+void check_opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char* name) {
+  if (!t.has_value() || !t->defined()) return;
+  TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kFloat, name,
+              " must be a contiguous fp32 GPU tensor");
+  TORCH_CHECK(t->numel() == numel, name, " has the wrong size");
+}
+
+std::vector<at::Tensor> lstm_forward(const at::Tensor& xw, const at::Tensor& wfrag,
+                                     const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
+                                     int64_t H, bool save_gates) {
+  CHECK_DEV(xw);
+  CHECK_DTYPE(xw, at::kFloat);
+  TORCH_CHECK(xw.dim() == 3 && xw.size(2) == 4 * H, "xw must be [B, T, 4H]");
+  const int64_t B = xw.size(0), T = xw.size(1), KS = lstm_ks(H);
+  TORCH_CHECK(B >= 1 && T >= 1 && B * T * 4 * H < (1LL << 40), "bad LSTM sizes");
+  CHECK_DEV(wfrag);
+  CHECK_DTYPE(wfrag, at::kBFloat16);
+  TORCH_CHECK(wfrag.numel() == 2 * KS * 4 * KS * 64 * 8, "wfrag must be [NW, 4, KS, 64, 8]");
+  TORCH_CHECK(aligned(wfrag, 16), "wfrag must be 16-byte aligned");
+  check_opt_f32(h0, B * H, "h0");
+  check_opt_f32(c0, B * H, "c0");
+  DevGuard g(xw.device());
+  auto hseq = at::empty({B, T, H}, xw.options()), cseq = at::empty({B, T, H}, xw.options());
+  at::Tensor gates;
+  if (save_gates) gates = at::empty({B, T, 4 * H}, xw.options());
+  const int RT = avk::lstm_row_tiles(B, (int)KS);
+  avk::lstm_fwd(xw.data_ptr<float>(), wfrag.data_ptr(), ptr_or_null<float>(h0), ptr_or_null<float>(c0), (int)B,
+                (int)T, (int)H, (int)KS, RT, hseq.data_ptr<float>(), cseq.data_ptr<float>(),
+                save_gates ? gates.data_ptr<float>() : nullptr, cur_stream(xw));
+  if (save_gates) return {hseq, cseq, gates};
+  return {hseq, cseq};
+}
+
+std::vector<at::Tensor> lstm_backward(const at::Tensor& dhseq, const at::Tensor& gates, const at::Tensor& cseq,
+                                      const c10::optional<at::Tensor>& c0, const c10::optional<at::Tensor>& dhn,
+                                      const c10::optional<at::Tensor>& dcn, const at::Tensor& wfragT, int64_t H) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&dhseq, &gates, &cseq}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(dhseq.dim() == 3 && dhseq.size(2) == H, "dhseq must be [B, T, H]");
+  const int64_t B = dhseq.size(0), T = dhseq.size(1), KS = lstm_ks(H);
+  TORCH_CHECK(cseq.sizes() == dhseq.sizes(), "cseq must be [B, T, H]");
+  TORCH_CHECK(gates.dim() == 3 && gates.size(0) == B && gates.size(1) == T && gates.size(2) == 4 * H,
+              "gates must be [B, T, 4H]");
+  CHECK_DEV(wfragT);
+  CHECK_DTYPE(wfragT, at::kBFloat16);
+  TORCH_CHECK(wfragT.numel() == 2 * KS * 4 * KS * 64 * 8, "wfragT must be [NW, 4KS, 64, 8]");
+  TORCH_CHECK(aligned(wfragT, 16), "wfragT must be 16-byte aligned");
+  check_opt_f32(c0, B * H, "c0");
+  check_opt_f32(dhn, B * H, "dhn");
+  check_opt_f32(dcn, B * H, "dcn");
+  DevGuard g(dhseq.device());
+  auto dz = at::empty({B, T, 4 * H}, dhseq.options());
+  auto dh0 = at::empty({B, H}, dhseq.options()), dc0 = at::empty({B, H}, dhseq.options());
+  const int RT = avk::lstm_row_tiles(B, (int)KS);
+  avk::lstm_bwd(dhseq.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), ptr_or_null<float>(c0),
+                ptr_or_null<float>(dhn), ptr_or_null<float>(dcn), wfragT.data_ptr(), (int)B, (int)T, (int)H, (int)KS,
+                RT, dz.data_ptr<float>(), dh0.data_ptr<float>(), dc0.data_ptr<float>(), cur_stream(dhseq));
+  return {dz, dh0, dc0};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -971,6 +1041,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("ngram_count", &ngram_count);
   m.def("uniformization", &uniformization);
   m.def("dot_matrix", &dot_matrix);
+  m.def("lstm_ks", &lstm_ks);
+  m.def("lstm_forward", &lstm_forward);
+  m.def("lstm_backward", &lstm_backward);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',

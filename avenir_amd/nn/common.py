@@ -99,7 +99,9 @@ def _cfg(conf, key, default):
     return conf.get_string(key)[0]
 
 
-def pick_device(name: str | None = None) -> torch.device:
+def pick_device(name: "str | torch.device | None" = None) -> torch.device:
+    if isinstance(name, torch.device):
+        return name
     if name in (None, "", "auto"):
         return torch.device("cuda" if torch.cuda.is_available() else "cpu")
     if name.startswith("cuda") and not torch.cuda.is_available():

@@ -1,8 +1,9 @@
 """LSTM sequence models (``LstmNetwork``, P/supv/lstm.py:42-378).
 
 Rows hold one flattened sequence ``seq_len x input_size`` (+ optional target column); the model is
-``nn.LSTM`` (MIOpen RNN kernels on ROCm) + Linear + optional output activation, seq-to-one
-(last step) or seq-to-seq.  Differences from the reference, all deliberate:
+``ops.rnn.FusedLSTM`` (K27: one persistent HIP kernel launch per layer for the whole recurrence,
+forward and backward; same parameter names as ``nn.LSTM``) + Linear + optional output
+activation, seq-to-one (last step) or seq-to-seq.  Differences from the reference, all deliberate:
 * batches are formed by ONE reshape + gather on the device instead of a per-element Python loop
   (lstm.py:187-218);
 * the initial hidden state is created on the model's device (the reference makes it on the CPU,
@@ -15,6 +16,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..ops.rnn import FusedLSTM
 from .common import (_cfg, create_activation, create_loss, load_checkpoint, optimizer_from_config, pick_device,
                      save_checkpoint, scale_data)
 
@@ -28,8 +30,9 @@ class LstmNetwork(torch.nn.Module):
         self.input_size, self.hidden_size, self.output_size = input_size, hidden_size, output_size
         self.num_layers, self.seq_len, self.batch_size = num_layers, seq_len, batch_size
         self.out_seq, self.grad_clip, self.num_iter = out_sequence, grad_clip, num_iter
-        self.lstm = torch.nn.LSTM(input_size, hidden_size, num_layers, batch_first=True,
-                                  dropout=dropout if num_layers > 1 else 0.0)
+        # K27 fused LSTM (persistent HIP recurrence kernel on the GPU); nn.LSTM-compatible state dict
+        self.lstm = FusedLSTM(input_size, hidden_size, num_layers, batch_first=True,
+                              dropout=dropout if num_layers > 1 else 0.0)
         self.linear = torch.nn.Linear(hidden_size, output_size)
         self.out_act = create_activation(out_activation)
         self.loss_name = loss

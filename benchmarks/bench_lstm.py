@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""K27 fused LSTM vs PyTorch-ROCm nn.LSTM (MIOpen) — training step and inference on one MI355X.
+
+Configs: the reference's contact-tracing LSTM (R/lstm_ct.properties: input 5, hidden 100, 2
+layers, seq_len 5, 1000 sequences from R/viral_infection_prediction_with_lstm_tutorial.txt:14) and
+two larger batch/sequence shapes.  A training step = forward + CE loss + backward + Adam on the
+whole model (LSTM + linear head).  Prints one JSON line per (config, implementation).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from avenir_amd.ops.rnn import FusedLSTM  # noqa: E402
+
+CONFIGS = [
+    dict(name="reference_ct", B=1000, T=5, I=5, H=100, L=2, O=2),
+    dict(name="b8k_t16_h64", B=8192, T=16, I=32, H=64, L=2, O=2),
+    dict(name="b64k_t32_h128", B=65536, T=32, I=16, H=128, L=2, O=2),
+]
+
+
+class Net(torch.nn.Module):
+    def __init__(self, lstm, H, O):
+        super().__init__()
+        self.lstm = lstm
+        self.head = torch.nn.Linear(H, O)
+
+    def forward(self, x):
+        out, _ = self.lstm(x)
+        return self.head(out[:, -1])
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(steps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / steps
+
+
+def run(cfg, impl, steps, warmup):
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    B, T, I, H, L, O = (cfg[k] for k in "BTIHLO")
+    ref = torch.nn.LSTM(I, H, L, batch_first=True)
+    if impl == "fused":
+        lstm = FusedLSTM(I, H, L)
+        lstm.load_state_dict(ref.state_dict())
+    else:
+        lstm = ref
+    net = Net(lstm, H, O).to(dev)
+    opt = torch.optim.Adam(net.parameters(), lr=2e-3)
+    x = torch.randn(B, T, I, device=dev)
+    y = torch.randint(0, O, (B,), device=dev)
+    lossf = torch.nn.CrossEntropyLoss()
+    losses = []
+
+    def train_step():
+        opt.zero_grad(set_to_none=True)
+        loss = lossf(net(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.detach())
+
+    def infer():
+        with torch.no_grad():
+            net(x)
+
+    ms_train = timed(train_step, steps, warmup)
+    ms_inf = timed(infer, steps, warmup)
+    flops = 2 * B * T * 4 * H * (I + H) * L  # forward GEMM flops (input + recurrent)
+    return {"bench": "lstm", "config": cfg["name"], "impl": impl, "B": B, "T": T, "I": I, "H": H, "L": L,
+            "train_ms": ms_train, "infer_ms": ms_inf,
+            "train_seq_per_s": B / (ms_train * 1e-3), "infer_seq_per_s": B / (ms_inf * 1e-3),
+            "fwd_tflops": flops / (ms_inf * 1e-3) / 1e12,
+            "loss_first": float(losses[0]), "loss_last": float(losses[-1])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--configs", default="all")
+    args = ap.parse_args()
+    names = None if args.configs == "all" else set(args.configs.split(","))
+    for cfg in CONFIGS:
+        if names and cfg["name"] not in names:
+            continue
+        res = {}
+        for impl in ("fused", "miopen"):
+            res[impl] = run(cfg, impl, args.steps, args.warmup)
+            print(json.dumps(res[impl]), flush=True)
+        print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"],
+                          "train_x": res["miopen"]["train_ms"] / res["fused"]["train_ms"],
+                          "infer_x": res["miopen"]["infer_ms"] / res["fused"]["infer_ms"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,100 @@
+"""K27 fused LSTM: fragment packing (CPU), nn.LSTM parity of the module (CPU), HIP kernels vs the
+fp32 oracle (GPU)."""
+import pytest
+import torch
+
+from avenir_amd.ops import rnn
+
+
+@pytest.mark.parametrize("H", [20, 64, 100])
+def test_pack_whh_fragment_maps(H):
+    torch.manual_seed(0)
+    W = torch.randn(4 * H, H)
+    fwd, bwd = rnn.pack_whh(W, H)
+    HP = rnn.padded_hidden(H)
+    KS, NW = HP // 32, HP // 16
+    assert fwd.shape == (NW, 4, KS, 4, 16, 8) and bwd.shape == (NW, 4 * KS, 4, 16, 8)
+    fwd = fwd.float().reshape(NW, 4, KS, 64, 8)
+    bwd = bwd.float().reshape(NW, 4 * KS, 64, 8)
+    Wb = W.to(torch.bfloat16).float()
+
+    def w_at(r, c):  # padded W_hh element, rows gate-major
+        g, u = divmod(r, HP)
+        return Wb[g * H + u, c].item() if (u < H and c < H) else 0.0
+
+    g_ = torch.Generator().manual_seed(1)
+    for _ in range(200):
+        w, g, ks, lane, j = (int(torch.randint(0, n, (1,), generator=g_)) for n in (NW, 4, KS, 64, 8))
+        col, q = lane & 15, lane >> 4
+        assert fwd[w, g, ks, lane, j].item() == w_at(g * HP + 16 * w + col, 32 * ks + 8 * q + j)
+        s = int(torch.randint(0, 4 * KS, (1,), generator=g_))
+        gg, kk = divmod(s, KS)
+        assert bwd[w, s, lane, j].item() == w_at(gg * HP + 32 * kk + 8 * q + j, 16 * w + col)
+
+
+def test_fused_lstm_module_matches_torch_lstm_cpu():
+    torch.manual_seed(0)
+    ref = torch.nn.LSTM(6, 10, 2, batch_first=True)
+    mine = rnn.FusedLSTM(6, 10, 2)
+    mine.load_state_dict(ref.state_dict())
+    x = torch.randn(5, 7, 6)
+    h0, c0 = torch.randn(2, 5, 10), torch.randn(2, 5, 10)
+    o1, (h1, c1) = ref(x, (h0, c0))
+    o2, (h2, c2) = mine(x, (h0, c0))
+    torch.testing.assert_close(o2, o1, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(h2, h1, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(c2, c1, atol=1e-5, rtol=1e-5)
+    (o1.square().sum() + c1.sum()).backward()
+    (o2.square().sum() + c2.sum()).backward()
+    for (n, p1), p2 in zip(ref.named_parameters(), mine.parameters()):
+        torch.testing.assert_close(p2.grad, p1.grad, atol=1e-4, rtol=1e-4, msg=n)
+
+
+def _oracle(x, w_ih, w_hh, b, h0, c0):
+    x, w_ih, w_hh, b = (t.detach().double().requires_grad_() for t in (x, w_ih, w_hh, b))
+    h0 = h0.detach().double().requires_grad_()
+    c0 = c0.detach().double().requires_grad_()
+    hs, (h, c) = rnn.lstm_reference(x, w_ih, w_hh, b, h0, c0)
+    return (x, w_ih, w_hh, b, h0, c0), hs, h, c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,I,H", [(37, 5, 3, 20), (1000, 5, 8, 100), (9000, 6, 16, 64), (20000, 3, 4, 128)])
+def test_fused_lstm_kernels_vs_fp32_oracle(cuda, B, T, I, H):
+    torch.manual_seed(B)
+    k = 1.0 / H ** 0.5
+    x = torch.randn(B, T, I, device=cuda)
+    w_ih = (torch.rand(4 * H, I, device=cuda) * 2 - 1) * k
+    w_hh = (torch.rand(4 * H, H, device=cuda) * 2 - 1) * k
+    b = (torch.rand(4 * H, device=cuda) * 2 - 1) * k
+    h0 = torch.randn(B, H, device=cuda) * 0.5
+    c0 = torch.randn(B, H, device=cuda) * 0.5
+    leaves = [t.clone().requires_grad_() for t in (x, w_ih, w_hh, b, h0, c0)]
+    hs, h, c = rnn.lstm_layer(*leaves)
+    assert hs.shape == (B, T, H)
+    ins, hs_r, h_r, c_r = _oracle(x, w_ih, w_hh, b, h0, c0)
+    # bf16 recurrent operands, fp32 accumulation / gate math
+    assert (hs.double() - hs_r).abs().max().item() < 2e-2
+    assert (c.double() - c_r).abs().max().item() < 3e-2
+    gy = torch.randn_like(hs)
+    gc = torch.randn_like(c)
+    (hs * gy).sum().backward(retain_graph=True)
+    (c * gc).sum().backward()
+    ((hs_r * gy.double()).sum() + (c_r * gc.double()).sum()).backward()
+    for name, mine, ref in zip(["x", "w_ih", "w_hh", "b", "h0", "c0"], leaves, ins):
+        g1, g2 = mine.grad.double(), ref.grad
+        rel = (g1 - g2).norm() / g2.norm().clamp_min(1e-12)
+        assert rel.item() < 3e-2, (name, rel.item())
+
+
+@pytest.mark.gpu
+def test_fused_lstm_network_trains(cuda):
+    from avenir_amd.nn.sequence import LstmNetwork
+    torch.manual_seed(0)
+    n, T = 4096, 5
+    x = torch.rand(n, T, 1, device=cuda)
+    y = (x.sum(dim=(1, 2)) > T / 2).float()
+    net = LstmNetwork(1, 100, 1, num_layers=2, seq_len=T, batch_size=256, lr=0.01, num_iter=60, device=cuda)
+    assert isinstance(net.lstm, rnn.FusedLSTM)
+    net.fit(x, y)
+    assert net.losses[-1] < 0.6 * net.losses[0]
