@@ -940,10 +940,11 @@ std::string format_rows(py::object prefix, const at::Tensor& cols, std::vector<i
 }
 
 // ---------------------------------------------------------------------------------------------
-// K27 LSTM recurrence.  Fragments are packed by avenir_amd/ops/rnn.py (pack_whh): wfrag holds
-// [NW, 4, KS, 64, 8] bf16 (forward), wfragT [NW, 4KS, 64, 8] bf16 (backward); NW = 2 KS.
+// K27 LSTM recurrence.  Fragments are packed by avenir_amd/ops/rnn.py (pack_weights): wfrag holds
+// [NW, 4, KS+IS, 64, 8] bf16 (forward, [W_hh | W_ih]), wfragT [NW, 4KS, 64, 8] bf16 (backward,
+// W_hhᵀ); NW = 2 KS.
 int64_t lstm_ks(int64_t H) {
-  TORCH_CHECK(H >= 1 && H <= 128, "fused LSTM supports hidden sizes 1..128");
+  TORCH_CHECK(H >= 1 && H <= 128, "fused LSTM supports hidden and input sizes 1..128");
   return H <= 32 ? 1 : (H <= 64 ? 2 : 4);  // padded hidden size HP = 32 KS in {32, 64, 128}
 }
 
@@ -954,44 +955,60 @@ void check_opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char
   TORCH_CHECK(t->numel() == numel, name, " has the wrong size");
 }
 
-std::vector<at::Tensor> lstm_forward(const at::Tensor& xw, const at::Tensor& wfrag,
+// x [B, T, I] fp32; wfrag [NW, 4, KS+IS, 64, 8] bf16 ([W_hh | W_ih]); bias [4HP] fp32 kernel order.
+// Returns hseq [B,T,H], cseq [B,T,HP] (+ gates [B,T,4HP] bf16, hx [B,T,HP+IP] bf16 when training).
+std::vector<at::Tensor> lstm_forward(const at::Tensor& x, const at::Tensor& wfrag, const at::Tensor& bias,
                                      const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
-                                     int64_t H, bool save_gates) {
-  CHECK_DEV(xw);
-  CHECK_DTYPE(xw, at::kFloat);
-  TORCH_CHECK(xw.dim() == 3 && xw.size(2) == 4 * H, "xw must be [B, T, 4H]");
-  const int64_t B = xw.size(0), T = xw.size(1), KS = lstm_ks(H);
-  TORCH_CHECK(B >= 1 && T >= 1 && B * T * 4 * H < (1LL << 40), "bad LSTM sizes");
+                                     int64_t H, bool training) {
+  const int64_t KS = lstm_ks(H), HP = 32 * KS;
+  CHECK_DEV(x);
+  CHECK_DTYPE(x, at::kFloat);
+  TORCH_CHECK(x.dim() == 3, "x must be [B, T, I]");
+  const int64_t B = x.size(0), T = x.size(1), I = x.size(2);
+  const int64_t IS = lstm_ks(I), IP = 32 * IS, KT = KS + IS;
+  TORCH_CHECK(B >= 1 && T >= 1, "empty LSTM input");
   CHECK_DEV(wfrag);
   CHECK_DTYPE(wfrag, at::kBFloat16);
-  TORCH_CHECK(wfrag.numel() == 2 * KS * 4 * KS * 64 * 8, "wfrag must be [NW, 4, KS, 64, 8]");
+  TORCH_CHECK(wfrag.numel() == 2 * KS * 4 * KT * 64 * 8, "wfrag must be [NW, 4, KS+IS, 64, 8]");
   TORCH_CHECK(aligned(wfrag, 16), "wfrag must be 16-byte aligned");
+  CHECK_DEV(bias);
+  CHECK_DTYPE(bias, at::kFloat);
+  TORCH_CHECK(bias.numel() == 4 * HP, "bias must be [4HP] (kernel order)");
   check_opt_f32(h0, B * H, "h0");
   check_opt_f32(c0, B * H, "c0");
-  DevGuard g(xw.device());
-  auto hseq = at::empty({B, T, H}, xw.options()), cseq = at::empty({B, T, H}, xw.options());
-  at::Tensor gates;
-  if (save_gates) gates = at::empty({B, T, 4 * H}, xw.options());
+  DevGuard g(x.device());
+  auto f32 = x.options();
+  auto bf = x.options().dtype(at::kBFloat16);
+  auto hseq = at::empty({B, T, H}, f32), cseq = at::empty({B, T, HP}, f32);
+  at::Tensor gates, hx;
+  if (training) {
+    gates = at::empty({B, T, 4 * HP}, bf);
+    hx = at::empty({B, T, HP + IP}, bf);
+  }
   const int RT = avk::lstm_row_tiles(B, (int)KS);
-  avk::lstm_fwd(xw.data_ptr<float>(), wfrag.data_ptr(), ptr_or_null<float>(h0), ptr_or_null<float>(c0), (int)B,
-                (int)T, (int)H, (int)KS, RT, hseq.data_ptr<float>(), cseq.data_ptr<float>(),
-                save_gates ? gates.data_ptr<float>() : nullptr, cur_stream(xw));
-  if (save_gates) return {hseq, cseq, gates};
+  avk::lstm_fwd(x.data_ptr<float>(), (int)I, (int)IS, wfrag.data_ptr(), bias.data_ptr<float>(), ptr_or_null<float>(h0),
+                ptr_or_null<float>(c0), (int)B, (int)T, (int)H, (int)KS, RT, hseq.data_ptr<float>(),
+                cseq.data_ptr<float>(), training ? reinterpret_cast<unsigned short*>(gates.data_ptr()) : nullptr,
+                training ? reinterpret_cast<unsigned short*>(hx.data_ptr()) : nullptr, cur_stream(x));
+  if (training) return {hseq, cseq, gates, hx};
   return {hseq, cseq};
 }
 
 std::vector<at::Tensor> lstm_backward(const at::Tensor& dhseq, const at::Tensor& gates, const at::Tensor& cseq,
                                       const c10::optional<at::Tensor>& c0, const c10::optional<at::Tensor>& dhn,
                                       const c10::optional<at::Tensor>& dcn, const at::Tensor& wfragT, int64_t H) {
+  const int64_t KS = lstm_ks(H), HP = 32 * KS;
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&dhseq, &gates, &cseq}) {
     CHECK_DEV((*t));
-    CHECK_DTYPE((*t), at::kFloat);
+    CHECK_DTYPE((*t), t == &gates ? at::kBFloat16 : at::kFloat);
+    TORCH_CHECK(aligned(*t, 16), "LSTM backward inputs must be 16-byte aligned");
   }
   TORCH_CHECK(dhseq.dim() == 3 && dhseq.size(2) == H, "dhseq must be [B, T, H]");
-  const int64_t B = dhseq.size(0), T = dhseq.size(1), KS = lstm_ks(H);
-  TORCH_CHECK(cseq.sizes() == dhseq.sizes(), "cseq must be [B, T, H]");
-  TORCH_CHECK(gates.dim() == 3 && gates.size(0) == B && gates.size(1) == T && gates.size(2) == 4 * H,
-              "gates must be [B, T, 4H]");
+  const int64_t B = dhseq.size(0), T = dhseq.size(1);
+  TORCH_CHECK(cseq.dim() == 3 && cseq.size(0) == B && cseq.size(1) == T && cseq.size(2) == HP,
+              "cseq must be [B, T, HP]");
+  TORCH_CHECK(gates.dim() == 3 && gates.size(0) == B && gates.size(1) == T && gates.size(2) == 4 * HP,
+              "gates must be [B, T, 4HP]");
   CHECK_DEV(wfragT);
   CHECK_DTYPE(wfragT, at::kBFloat16);
   TORCH_CHECK(wfragT.numel() == 2 * KS * 4 * KS * 64 * 8, "wfragT must be [NW, 4KS, 64, 8]");
@@ -1000,12 +1017,14 @@ std::vector<at::Tensor> lstm_backward(const at::Tensor& dhseq, const at::Tensor&
   check_opt_f32(dhn, B * H, "dhn");
   check_opt_f32(dcn, B * H, "dcn");
   DevGuard g(dhseq.device());
-  auto dz = at::empty({B, T, 4 * H}, dhseq.options());
+  auto dz = at::empty({B, T, 4 * HP}, dhseq.options().dtype(at::kBFloat16));
   auto dh0 = at::empty({B, H}, dhseq.options()), dc0 = at::empty({B, H}, dhseq.options());
   const int RT = avk::lstm_row_tiles(B, (int)KS);
-  avk::lstm_bwd(dhseq.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), ptr_or_null<float>(c0),
-                ptr_or_null<float>(dhn), ptr_or_null<float>(dcn), wfragT.data_ptr(), (int)B, (int)T, (int)H, (int)KS,
-                RT, dz.data_ptr<float>(), dh0.data_ptr<float>(), dc0.data_ptr<float>(), cur_stream(dhseq));
+  avk::lstm_bwd(dhseq.data_ptr<float>(), reinterpret_cast<const unsigned short*>(gates.data_ptr()),
+                cseq.data_ptr<float>(), ptr_or_null<float>(c0), ptr_or_null<float>(dhn), ptr_or_null<float>(dcn),
+                wfragT.data_ptr(), (int)B, (int)T, (int)H, (int)KS, RT,
+                reinterpret_cast<unsigned short*>(dz.data_ptr()), dh0.data_ptr<float>(), dc0.data_ptr<float>(),
+                cur_stream(dhseq));
   return {dz, dh0, dc0};
 }
 

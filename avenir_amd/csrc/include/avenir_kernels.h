@@ -119,12 +119,14 @@ void uniformization(const double* P, int S, const double* w1, const double* w2, 
 void dot_matrix(const int* A, int n, int Wa, const int* B, int m, int Wb, int* hits, hipStream_t stream);
 
 // ---- rnn.hip (K27 persistent LSTM recurrence, bf16 MFMA) -------------------------------------
-// KS = HP / 32 (HP = hidden size padded to 32, <= 128), RT = 16-row tiles per workgroup.
+// KS = HP / 32 (HP = hidden size padded to 32, 64 or 128), IS = IP / 32 likewise for the layer
+// input size, RT = 16-sequence tiles per workgroup.
 int lstm_row_tiles(long long B, int KS);
-void lstm_fwd(const float* xw, const void* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
-              int RT, float* hseq, float* cseq, float* gates, hipStream_t stream);
-void lstm_bwd(const float* dhseq, const float* gates, const float* cseq, const float* c0, const float* dhn,
-              const float* dcn, const void* wfragT, int B, int T, int H, int KS, int RT, float* dz, float* dh0,
-              float* dc0, hipStream_t stream);
+void lstm_fwd(const float* x, int I, int IS, const void* wfrag, const float* bias, const float* h0, const float* c0,
+              int B, int T, int H, int KS, int RT, float* hseq, float* cseq, unsigned short* gates, unsigned short* hx,
+              hipStream_t stream);
+void lstm_bwd(const float* dhseq, const unsigned short* gates, const float* cseq, const float* c0, const float* dhn,
+              const float* dcn, const void* wfragT, int B, int T, int H, int KS, int RT, unsigned short* dz,
+              float* dh0, float* dc0, hipStream_t stream);
 
 }  // namespace avk

@@ -3,17 +3,20 @@
 The reference's only GPU-addressable model is the PyTorch LSTM of ``LstmNetwork``
 (P/supv/lstm.py:42-378, SURVEY.md §3.5: hidden 100, 2 layers, seq_len 5).  On MI355X the split is:
 
-* ``x·W_ihᵀ + b_ih + b_hh`` for every timestep at once — one hipBLASLt GEMM (K = input size);
-* the sequential recurrence — ONE launch of ``lstm_fwd_kernel`` (csrc/kernels/rnn.hip): each
-  workgroup carries 16–64 sequences through all timesteps with W_hh resident in VGPRs as bf16
-  MFMA fragments and the cell state in registers (no per-timestep launches);
-* backward — ONE launch of ``lstm_bwd_kernel`` for the dz / dh / dc recurrence, then the weight
-  gradients ``Σ_t dz_tᵀ h_{t-1}``, ``dzᵀ x`` and ``dx = dz·W_ih`` as GEMMs over all B·T rows.
+* forward — ONE launch of ``lstm_fwd_kernel`` per layer (csrc/kernels/rnn.hip): each workgroup
+  carries 16–32 sequences through all timesteps with [W_hh | W_ih] resident in VGPRs as bf16 MFMA
+  fragments, the cell state in registers and the input projection fused into the recurrent
+  product (no per-timestep launches, no B·T·4H projection tensor);
+* backward — ONE launch of ``lstm_bwd_kernel`` for the dz / dh / dc recurrence, then ONE GEMM
+  ``dzᵀ·hx`` over all B·T rows for dW_hh, dW_ih and db together (``hx`` = the forward's MFMA
+  B-operand rows [h_{t-1} | x_t | 1]) and one GEMM for ``dx = dz·W_ih``.
 
-Numerics: the recurrent product runs in bf16 with fp32 accumulation (gate math, cell state and
-all outputs fp32), i.e. the usual mixed-precision LSTM; ``lstm_reference`` is the fp32 oracle.
-Hidden sizes above 128 (beyond the register-resident design) use PyTorch's MIOpen LSTM on the
-GPU; that is the only non-kernel path and it is selected by shape, never by a missing extension.
+Numerics (mixed precision): GEMM operands and the B·T·4H-sized intermediates (xw, saved gates,
+gate gradients) are bf16 with fp32 accumulation; gate math, the cell state, h outputs and the
+weight gradients are fp32.  ``lstm_reference`` is the fp32 oracle.
+Hidden or input sizes above 128 (beyond the register-resident design) use PyTorch's MIOpen LSTM
+on the GPU; that is the only non-kernel path and it is selected by shape, never by a missing
+extension.
 """
 from __future__ import annotations
 
@@ -30,25 +33,24 @@ def padded_hidden(H: int) -> int:
     return 32 if H <= 32 else (64 if H <= 64 else 128)
 
 
-def _pad_whh(w_hh: torch.Tensor, H: int) -> torch.Tensor:
-    HP = padded_hidden(H)
-    wp = torch.zeros((4, HP, HP), device=w_hh.device, dtype=torch.float32)
-    wp[:, :H, :H] = w_hh.detach().float().view(4, H, H)
-    return wp
+def pack_weights(w_ih: torch.Tensor, w_hh: torch.Tensor, H: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """(W_ih [4H, I], W_hh [4H, H]) -> bf16 MFMA A-fragments (forward [NW,4,KS+IS,4,16,8], backward
+    [NW,4KS,4,16,8]).
 
-
-def pack_whh(w_hh: torch.Tensor, H: int) -> tuple[torch.Tensor, torch.Tensor]:
-    """W_hh [4H, H] -> (forward fragments [NW,4,KS,64,8], backward fragments [NW,4KS,64,8]) in bf16.
-
-    Forward B-operand of v_mfma_f32_16x16x32_bf16 for wave w, gate g, k-step ks: lane q*16+col,
-    element j holds W_hh[g*H + 16w + col, 32ks + 8q + j].  Backward (dh = dz·W_hh, k over the 4·HP
-    gate rows): lane q*16+col, element j of k-step s holds W_hh[g*H + 32(s%KS) + 8q + j, 16w + col]
-    with g = s // KS.
+    The kernels compute transposed products (zᵀ = [W_hh | W_ih]·[h; x]ᵀ, dhᵀ = W_hhᵀ·dzᵀ), so these
+    are the A-operands of v_mfma_f32_16x16x32_bf16.  Forward, wave w, gate g, k-step ks: lane
+    q*16+col, element j holds Wcat[g*H + 16w + col, 32ks + 8q + j] where Wcat = [W_hh (HP cols) |
+    W_ih (IP cols)].  Backward (k over the 4·HP gate rows): lane q*16+col, element j of k-step s
+    holds W_hh[g*H + 32(s%KS) + 8q + j, 16w + col] with g = s // KS.  Padding is zero.
     """
-    HP = padded_hidden(H)
-    KS, NW = HP // 32, HP // 16
-    wp = _pad_whh(w_hh, H)
-    fwd = wp.view(4, NW, 16, KS, 4, 8).permute(1, 0, 3, 4, 2, 5).contiguous()
+    I = w_ih.shape[1]
+    HP, IP = padded_hidden(H), padded_hidden(I)
+    KS, NW, KT = HP // 32, HP // 16, (HP + IP) // 32
+    wcat = torch.zeros((4, HP, HP + IP), device=w_hh.device, dtype=torch.float32)
+    wcat[:, :H, :H] = w_hh.detach().float().view(4, H, H)
+    wcat[:, :H, HP:HP + I] = w_ih.detach().float().view(4, H, I)
+    fwd = wcat.view(4, NW, 16, KT, 4, 8).permute(1, 0, 3, 4, 2, 5)
+    wp = wcat[:, :, :HP].contiguous()
     bwd = wp.view(4, KS, 4, 8, NW, 16).permute(4, 0, 1, 2, 5, 3).contiguous().view(NW, 4 * KS, 4, 16, 8)
     return fwd.to(torch.bfloat16).contiguous(), bwd.to(torch.bfloat16).contiguous()
 
@@ -74,47 +76,111 @@ def lstm_reference(x, w_ih, w_hh, b=None, h0=None, c0=None):
     return torch.stack(outs, 1), (h, c)
 
 
+_ORDER_CACHE: dict = {}
+
+
+def kernel_gate_order(H: int, device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Kernel column order of the 4·HP gate columns: kc = 64·w + 16·g + i for unit u = 16·w + i.
+
+    Returns (valid_kc, torch_row, inv): ``valid_kc`` are the kernel columns of real units,
+    ``torch_row`` the matching row g·H + u of W_ih / W_hh / b, and ``inv[g·H + u]`` the kernel
+    column of every torch row (for gathering gradients back)."""
+    key = (H, str(device))
+    if key not in _ORDER_CACHE:
+        HP = padded_hidden(H)
+        kc = torch.arange(4 * HP)
+        w, g, i = kc // 64, (kc % 64) // 16, kc % 16
+        u = 16 * w + i
+        ok = u < H
+        valid_kc = kc[ok]
+        torch_row = (g * H + u)[ok]
+        inv = torch.empty(4 * H, dtype=torch.long)
+        inv[torch_row] = valid_kc
+        _ORDER_CACHE[key] = tuple(t.to(device) for t in (valid_kc, torch_row, inv))
+    return _ORDER_CACHE[key]
+
+
+def to_kernel_order(w: torch.Tensor, H: int) -> torch.Tensor:
+    """[4H, ...] gate-major rows (torch.nn.LSTM order) -> [4HP, ...] kernel order, padded with 0."""
+    valid_kc, torch_row, _ = kernel_gate_order(H, w.device)
+    out = w.new_zeros((4 * padded_hidden(H),) + tuple(w.shape[1:]))
+    out[valid_kc] = w[torch_row]
+    return out
+
+
+class _FragCache:
+    """Packed weight fragments keyed on the weights' (storage, version): inference re-uses them
+    across calls, training re-packs once per optimizer step (the forward's pack serves the
+    backward).  Inside a HIP-graph capture the pack is always recorded, so replays re-pack."""
+
+    def __init__(self, size: int = 16):
+        self.size, self.d = size, {}
+
+    def get(self, w_ih: torch.Tensor, w_hh: torch.Tensor, H: int):
+        if torch.cuda.is_current_stream_capturing():
+            return pack_weights(w_ih, w_hh, H)
+        key = (w_ih.data_ptr(), w_ih._version, tuple(w_ih.shape), w_hh.data_ptr(), w_hh._version, H)
+        hit = self.d.get(key)
+        if hit is None:
+            if len(self.d) >= self.size:
+                self.d.pop(next(iter(self.d)))
+            hit = self.d[key] = pack_weights(w_ih, w_hh, H)
+        return hit
+
+
+_frags = _FragCache()
+
+
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> fp32 GEMM (hipBLASLt, fp32 accumulate and output)."""
+    return torch.mm(a, b, out_dtype=torch.float32)
+
+
 class _LstmLayer(torch.autograd.Function):
+    """One layer: forward = ONE kernel launch (input projection fused into the recurrence); backward
+    = one kernel launch + one GEMM for all weight and bias gradients (dzᵀ·hx) + one GEMM for dx.
+    The B·T·4H-sized tensors (saved gates, dz) and hx are bf16; cell state, h outputs and the
+    weight gradients are fp32."""
+
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b, h0, c0):
         B, T, I = x.shape
         H = w_hh.shape[1]
-        mod = _native.C()
-        x2 = x.reshape(B * T, I)
-        if b is not None:
-            xw = torch.addmm(b.unsqueeze(0), x2, w_ih.t())
-        else:
-            xw = x2 @ w_ih.t()
-        xw = xw.view(B, T, 4 * H)
-        frag, frag_t = pack_whh(w_hh, H)
+        HP = padded_hidden(H)
+        frag, frag_t = _frags.get(w_ih, w_hh, H)
+        bias = to_kernel_order(b.detach().float(), H) if b is not None else x.new_zeros(4 * HP)
         need = any(ctx.needs_input_grad)
-        outs = mod.lstm_forward(xw, frag, h0, c0, H, bool(need))
+        outs = _native.C().lstm_forward(x, frag, bias, h0, c0, H, bool(need))
         hseq, cseq = outs[0], outs[1]
         if need:
-            ctx.save_for_backward(x, w_ih, w_hh, hseq, cseq, outs[2], h0, c0, frag_t)
-        ctx.has_b = b is not None
-        return hseq, hseq[:, -1], cseq[:, -1]
+            w_ih_k = to_kernel_order(w_ih.detach(), H).to(torch.bfloat16)    # [4HP, I] for dx
+            ctx.save_for_backward(w_ih_k, cseq, outs[2], outs[3], c0, frag_t)
+        ctx.has_b, ctx.dims = b is not None, (B, T, I, H)
+        return hseq, hseq[:, -1], cseq[:, -1, :H]
 
     @staticmethod
     def backward(ctx, dhseq, dhn, dcn):
-        x, w_ih, w_hh, hseq, cseq, gates, h0, c0, frag_t = ctx.saved_tensors
-        B, T, I = x.shape
-        H = w_hh.shape[1]
+        w_ih_k, cseq, gates, hx, c0, frag_t = ctx.saved_tensors
+        B, T, I, H = ctx.dims
+        HP, IP = padded_hidden(H), padded_hidden(I)
+        _, _, inv = kernel_gate_order(H, cseq.device)
         if dhseq is None:
-            dhseq = torch.zeros_like(hseq)
+            dhseq = cseq.new_zeros(B, T, H)
         dz, dh0, dc0 = _native.C().lstm_backward(dhseq.contiguous(), gates, cseq, c0,
                                                  None if dhn is None else dhn.contiguous(),
                                                  None if dcn is None else dcn.contiguous(), frag_t, H)
-        dz2 = dz.view(B * T, 4 * H)
-        dx = (dz2 @ w_ih).view(B, T, I) if ctx.needs_input_grad[0] else None
-        dw_ih = dz2.t() @ x.reshape(B * T, I) if ctx.needs_input_grad[1] else None
-        dw_hh = None
-        if ctx.needs_input_grad[2]:
-            first = h0.unsqueeze(1) if h0 is not None else hseq.new_zeros(B, 1, H)
-            hprev = torch.cat([first, hseq[:, :-1]], 1).reshape(B * T, H)
-            dw_hh = dz2.t() @ hprev
-        db = dz2.sum(0) if ctx.has_b and ctx.needs_input_grad[3] else None
-        return (dx, dw_ih, dw_hh, db, dh0 if h0 is not None else None, dc0 if c0 is not None else None)
+        dz2 = dz.view(B * T, 4 * HP)                                 # bf16, kernel order
+        dx = _mm_f32(dz2, w_ih_k).view(B, T, I) if ctx.needs_input_grad[0] else None
+        dw_ih = dw_hh = db = None
+        if any(ctx.needs_input_grad[1:4]):
+            dwcat = _mm_f32(dz2.t(), hx.view(B * T, HP + IP)).index_select(0, inv)   # [4H, HP+IP]
+            dw_hh = dwcat[:, :H].contiguous()
+            dw_ih = dwcat[:, HP:HP + I].contiguous()
+            if ctx.has_b:
+                # hx carries a ones column at HP + I when the input is narrower than its padding
+                db = dwcat[:, HP + I].contiguous() if I < IP else dz2.sum(0, dtype=torch.float32).index_select(0, inv)
+        need = ctx.needs_input_grad
+        return dx, dw_ih, dw_hh, db, (dh0 if need[4] else None), (dc0 if need[5] else None)
 
 
 def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None):
@@ -124,7 +190,7 @@ def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None):
     CPU tensors run the fp32 reference.
     """
     H = w_hh.shape[1]
-    if x.is_cuda and H <= MAX_FUSED_HIDDEN:
+    if x.is_cuda and H <= MAX_FUSED_HIDDEN and x.shape[-1] <= MAX_FUSED_HIDDEN:
         x = x.float().contiguous()
         h0 = None if h0 is None else h0.float().contiguous()
         c0 = None if c0 is None else c0.float().contiguous()
@@ -169,7 +235,8 @@ class FusedLSTM(torch.nn.Module):
 
     def forward(self, x, hx=None):
         H, L = self.hidden_size, self.num_layers
-        if x.is_cuda and H > MAX_FUSED_HIDDEN:   # beyond the register-resident kernel: MIOpen
+        if x.is_cuda and (H > MAX_FUSED_HIDDEN or self.input_size > MAX_FUSED_HIDDEN):
+            # beyond the register-resident kernel: MIOpen
             if hx is None:
                 z = x.new_zeros(L, x.shape[0], H)
                 hx = (z, z)

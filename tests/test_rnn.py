@@ -6,30 +6,34 @@ import torch
 from avenir_amd.ops import rnn
 
 
-@pytest.mark.parametrize("H", [20, 64, 100])
-def test_pack_whh_fragment_maps(H):
+@pytest.mark.parametrize("H,I", [(20, 5), (64, 64), (100, 100), (37, 128)])
+def test_pack_weights_fragment_maps(H, I):
     torch.manual_seed(0)
-    W = torch.randn(4 * H, H)
-    fwd, bwd = rnn.pack_whh(W, H)
-    HP = rnn.padded_hidden(H)
-    KS, NW = HP // 32, HP // 16
-    assert fwd.shape == (NW, 4, KS, 4, 16, 8) and bwd.shape == (NW, 4 * KS, 4, 16, 8)
-    fwd = fwd.float().reshape(NW, 4, KS, 64, 8)
+    Whh, Wih = torch.randn(4 * H, H), torch.randn(4 * H, I)
+    fwd, bwd = rnn.pack_weights(Wih, Whh, H)
+    HP, IP = rnn.padded_hidden(H), rnn.padded_hidden(I)
+    KS, NW, KT = HP // 32, HP // 16, (HP + IP) // 32
+    assert fwd.shape == (NW, 4, KT, 4, 16, 8) and bwd.shape == (NW, 4 * KS, 4, 16, 8)
+    fwd = fwd.float().reshape(NW, 4, KT, 64, 8)
     bwd = bwd.float().reshape(NW, 4 * KS, 64, 8)
-    Wb = W.to(torch.bfloat16).float()
+    Hb, Ib = Whh.to(torch.bfloat16).float(), Wih.to(torch.bfloat16).float()
 
-    def w_at(r, c):  # padded W_hh element, rows gate-major
+    def wcat(r, c):  # padded [W_hh | W_ih] element, rows gate-major
         g, u = divmod(r, HP)
-        return Wb[g * H + u, c].item() if (u < H and c < H) else 0.0
+        if u >= H:
+            return 0.0
+        if c < HP:
+            return Hb[g * H + u, c].item() if c < H else 0.0
+        return Ib[g * H + u, c - HP].item() if c - HP < I else 0.0
 
     g_ = torch.Generator().manual_seed(1)
-    for _ in range(200):
-        w, g, ks, lane, j = (int(torch.randint(0, n, (1,), generator=g_)) for n in (NW, 4, KS, 64, 8))
+    for _ in range(300):
+        w, g, ks, lane, j = (int(torch.randint(0, n, (1,), generator=g_)) for n in (NW, 4, KT, 64, 8))
         col, q = lane & 15, lane >> 4
-        assert fwd[w, g, ks, lane, j].item() == w_at(g * HP + 16 * w + col, 32 * ks + 8 * q + j)
+        assert fwd[w, g, ks, lane, j].item() == wcat(g * HP + 16 * w + col, 32 * ks + 8 * q + j)
         s = int(torch.randint(0, 4 * KS, (1,), generator=g_))
         gg, kk = divmod(s, KS)
-        assert bwd[w, s, lane, j].item() == w_at(gg * HP + 32 * kk + 8 * q + j, 16 * w + col)
+        assert bwd[w, s, lane, j].item() == wcat(gg * HP + 32 * kk + 8 * q + j, 16 * w + col)
 
 
 def test_fused_lstm_module_matches_torch_lstm_cpu():
@@ -59,7 +63,8 @@ def _oracle(x, w_ih, w_hh, b, h0, c0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,T,I,H", [(37, 5, 3, 20), (1000, 5, 8, 100), (9000, 6, 16, 64), (20000, 3, 4, 128)])
+@pytest.mark.parametrize("B,T,I,H", [(37, 5, 3, 20), (50, 4, 3, 37), (1000, 5, 8, 100), (9000, 6, 16, 64), (20000, 3, 4, 128),
+                                     (3000, 4, 64, 48), (700, 3, 128, 128), (500, 2, 100, 64)])
 def test_fused_lstm_kernels_vs_fp32_oracle(cuda, B, T, I, H):
     torch.manual_seed(B)
     k = 1.0 / H ** 0.5
@@ -98,3 +103,18 @@ def test_fused_lstm_network_trains(cuda):
     assert isinstance(net.lstm, rnn.FusedLSTM)
     net.fit(x, y)
     assert net.losses[-1] < 0.6 * net.losses[0]
+
+
+@pytest.mark.parametrize("H", [20, 64, 100, 128])
+def test_kernel_gate_order_roundtrip(H):
+    HP = rnn.padded_hidden(H)
+    w = torch.randn(4 * H, 3)
+    k = rnn.to_kernel_order(w, H)
+    assert k.shape == (4 * HP, 3)
+    for kc in range(4 * HP):
+        wv, g, i = kc // 64, (kc % 64) // 16, kc % 16
+        u = 16 * wv + i
+        expect = w[g * H + u] if u < H else torch.zeros(3)
+        assert torch.equal(k[kc], expect)
+    _, _, inv = rnn.kernel_gate_order(H, w.device)
+    assert torch.equal(k.index_select(0, inv), w)
