@@ -166,14 +166,22 @@ def load_checkpoint(path, model: torch.nn.Module, optimizer: torch.optim.Optimiz
 class GraphedStep:
     """Capture ``step_fn(x, y) -> loss`` (forward + backward + optimiser step) into one HIP graph
     for fixed-shape batches; ``__call__`` copies the batch into static buffers and replays.  Falls
-    back to eager execution on CPU or when capture is disabled."""
+    back to eager execution on CPU or when capture is disabled.
+
+    Capture needs a few eager warm-up steps (allocator pools, lazily created optimiser state).
+    When ``model`` / ``optimizer`` are given, their state is restored afterwards — parameters and
+    buffers to the pre-warm-up values, optimiser state tensors to their initial zeros (step
+    counts 0) — so the warm-up does not count as training.  Restoration is in place, so the
+    addresses captured in the graph stay valid."""
 
     def __init__(self, step_fn: Callable, x_example: torch.Tensor, y_example: torch.Tensor, enabled: bool = True,
-                 warmup: int = 3):
+                 warmup: int = 3, model: torch.nn.Module | None = None,
+                 optimizer: torch.optim.Optimizer | None = None):
         self.fn = step_fn
         self.enabled = enabled and x_example.is_cuda
         self.graph = None
         if self.enabled:
+            snap = [t.detach().clone() for t in _state_tensors(model)] if model is not None else None
             self.sx = x_example.clone()
             self.sy = y_example.clone()
             s = torch.cuda.Stream()
@@ -185,6 +193,15 @@ class GraphedStep:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self.sloss = self.fn(self.sx, self.sy)
+            with torch.no_grad():
+                if snap is not None:
+                    for t, v in zip(_state_tensors(model), snap):
+                        t.copy_(v)
+                if optimizer is not None:
+                    for st in optimizer.state.values():
+                        for v in st.values():
+                            if torch.is_tensor(v):
+                                v.zero_()
 
     def __call__(self, x, y):
         if self.graph is None:
@@ -193,3 +210,7 @@ class GraphedStep:
         self.sy.copy_(y, non_blocking=True)
         self.graph.replay()
         return self.sloss
+
+
+def _state_tensors(model: torch.nn.Module):
+    return [p for p in model.parameters()] + [b for b in model.buffers()]

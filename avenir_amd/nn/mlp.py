@@ -138,7 +138,8 @@ class FeedForwardNetwork(torch.nn.Module):
             xb = x[perm[: nb * bs]].view(nb, bs, -1)
             yb = y[perm[: nb * bs]].view((nb, bs) + tuple(y.shape[1:]))
             if step is None:
-                step = GraphedStep(self._step, xb[0], yb[0], enabled=use_graph)
+                step = GraphedStep(self._step, xb[0], yb[0], enabled=use_graph, model=self,
+                                   optimizer=self.optimizer)
             tot = torch.zeros((), device=self.device)
             for b in range(nb):
                 tot += step(xb[b], yb[b])

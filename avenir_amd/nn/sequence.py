@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from ..ops.rnn import FusedLSTM
-from .common import (_cfg, create_activation, create_loss, load_checkpoint, optimizer_from_config, pick_device,
+from .common import (GraphedStep, _cfg, create_activation, create_loss, load_checkpoint, optimizer_from_config, pick_device,
                      save_checkpoint, scale_data)
 
 
@@ -25,7 +25,7 @@ class LstmNetwork(torch.nn.Module):
     def __init__(self, input_size: int, hidden_size: int, output_size: int, num_layers: int = 1, seq_len: int = 1,
                  batch_size: int = 32, out_sequence: bool = False, out_activation: str | None = "sigmoid",
                  dropout: float = 0.0, loss: str = "mse", optimizer: str = "adam", lr: float = 1e-3,
-                 grad_clip: float = 5.0, num_iter: int = 100, device=None, conf=None):
+                 grad_clip: float = 5.0, num_iter: int = 100, device=None, conf=None, graph: bool = True):
         super().__init__()
         self.input_size, self.hidden_size, self.output_size = input_size, hidden_size, output_size
         self.num_layers, self.seq_len, self.batch_size = num_layers, seq_len, batch_size
@@ -40,7 +40,9 @@ class LstmNetwork(torch.nn.Module):
         self.device = pick_device(device)
         self.to(self.device)
         cfg = conf if conf is not None else {"train.optimizer": optimizer, "train.opt.learning.rate": lr}
-        self.optimizer = optimizer_from_config(self.parameters(), cfg)
+        self.use_graph = graph
+        self.optimizer = optimizer_from_config(self.parameters(), cfg,
+                                               capturable=self.device.type == "cuda" and graph)
         self.conf = conf
         self.losses: list[float] = []
 
@@ -93,30 +95,39 @@ class LstmNetwork(torch.nn.Module):
             return y.long().view(-1)
         return y.float().view(y.shape[0], -1) if not self.out_seq else y.float()
 
+    def _step(self, x, tgt):
+        self.optimizer.zero_grad(set_to_none=False)
+        out = self(x)
+        if self.out_seq and self.loss_name in ("ce", "nll"):
+            out = out.reshape(-1, out.shape[-1])
+        loss = self.loss_fn(out, tgt)
+        loss.backward()
+        if self.grad_clip:
+            torch.nn.utils.clip_grad_norm_(self.parameters(), self.grad_clip, foreach=True)
+        self.optimizer.step()
+        return loss.detach()
+
     def fit(self, x: torch.Tensor, y: torch.Tensor, num_iter: int | None = None, seed: int = 0) -> "LstmNetwork":
+        """``num_iter`` epochs of shuffled fixed-size mini-batches.  On the GPU the whole step
+        (fused-LSTM forward, loss, backward, clipping, optimiser) is one captured HIP graph."""
         x = x.to(self.device).float()
-        y = y.to(self.device)
+        tgt = self._target(y.to(self.device))
         n = x.shape[0]
         bs = min(self.batch_size, n)
         nb = max(n // bs, 1)
         g = torch.Generator().manual_seed(seed)
         self.train()
+        step = None
         for _ in range(num_iter if num_iter is not None else self.num_iter):
-            perm = torch.randperm(n, generator=g).to(self.device)
+            perm = torch.randperm(n, generator=g).to(self.device)[: nb * bs]
+            xb = x[perm].view((nb, bs) + tuple(x.shape[1:]))
+            yb = tgt[perm].view((nb, bs) + tuple(tgt.shape[1:]))
+            if step is None:
+                step = GraphedStep(self._step, xb[0], yb[0], enabled=self.use_graph and self.device.type == "cuda",
+                                   model=self, optimizer=self.optimizer)
             tot = torch.zeros((), device=self.device)
             for b in range(nb):
-                idx = perm[b * bs:(b + 1) * bs]
-                self.optimizer.zero_grad()
-                out = self(x[idx])
-                tgt = self._target(y[idx])
-                if self.out_seq and self.loss_name in ("ce", "nll"):
-                    out = out.reshape(-1, out.shape[-1])
-                loss = self.loss_fn(out, tgt)
-                loss.backward()
-                if self.grad_clip:
-                    torch.nn.utils.clip_grad_norm_(self.parameters(), self.grad_clip)
-                self.optimizer.step()
-                tot += loss.detach()
+                tot += step(xb[b], yb[b])
             self.losses.append(float(tot) / nb)
         self.eval()
         return self

@@ -17,6 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from avenir_amd.nn.common import GraphedStep  # noqa: E402
 from avenir_amd.ops.rnn import FusedLSTM  # noqa: E402
 
 CONFIGS = [
@@ -55,13 +56,14 @@ def run(cfg, impl, steps, warmup):
     dev = torch.device("cuda")
     B, T, I, H, L, O = (cfg[k] for k in "BTIHLO")
     ref = torch.nn.LSTM(I, H, L, batch_first=True)
-    if impl == "fused":
+    if impl.startswith("fused"):
         lstm = FusedLSTM(I, H, L)
         lstm.load_state_dict(ref.state_dict())
     else:
         lstm = ref
     net = Net(lstm, H, O).to(dev)
-    opt = torch.optim.Adam(net.parameters(), lr=2e-3)
+    graph = impl.endswith("graph")
+    opt = torch.optim.Adam(net.parameters(), lr=2e-3, capturable=graph)
     x = torch.randn(B, T, I, device=dev)
     y = torch.randint(0, O, (B,), device=dev)
     lossf = torch.nn.CrossEntropyLoss()
@@ -78,6 +80,18 @@ def run(cfg, impl, steps, warmup):
         with torch.no_grad():
             net(x)
 
+    if graph:   # whole step (forward, loss, backward, Adam) as one HIP graph
+        def step_fn(xx, yy):
+            opt.zero_grad(set_to_none=False)
+            loss = lossf(net(xx), yy)
+            loss.backward()
+            opt.step()
+            return loss.detach()
+        gs = GraphedStep(step_fn, x, y, model=net, optimizer=opt)
+
+        def train_step():
+            losses.append(gs(x, y).clone())
+
     ms_train = timed(train_step, steps, warmup)
     ms_inf = timed(infer, steps, warmup)
     flops = 2 * B * T * 4 * H * (I + H) * L  # forward GEMM flops (input + recurrent)
@@ -93,7 +107,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--configs", default="all")
-    ap.add_argument("--impls", default="fused,miopen")
+    ap.add_argument("--impls", default="fused,fused_graph,miopen")
     args = ap.parse_args()
     names = None if args.configs == "all" else set(args.configs.split(","))
     for cfg in CONFIGS:
@@ -103,10 +117,12 @@ def main():
         for impl in args.impls.split(","):
             res[impl] = run(cfg, impl, args.steps, args.warmup)
             print(json.dumps(res[impl]), flush=True)
-        if len(res) == 2:
-            print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"],
-                              "train_x": res["miopen"]["train_ms"] / res["fused"]["train_ms"],
-                              "infer_x": res["miopen"]["infer_ms"] / res["fused"]["infer_ms"]}), flush=True)
+        if "miopen" in res:
+            for impl in res:
+                if impl != "miopen":
+                    print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"], "impl": impl,
+                                      "train_x": res["miopen"]["train_ms"] / res[impl]["train_ms"],
+                                      "infer_x": res["miopen"]["infer_ms"] / res[impl]["infer_ms"]}), flush=True)
 
 
 if __name__ == "__main__":

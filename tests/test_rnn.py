@@ -118,3 +118,24 @@ def test_kernel_gate_order_roundtrip(H):
         assert torch.equal(k[kc], expect)
     _, _, inv = rnn.kernel_gate_order(H, w.device)
     assert torch.equal(k.index_select(0, inv), w)
+
+
+@pytest.mark.gpu
+def test_lstm_network_graph_matches_eager(cuda):
+    """The captured HIP-graph train step (warm-up state restored) trains exactly like eager."""
+    from avenir_amd.nn.sequence import LstmNetwork
+    torch.manual_seed(0)
+    x = torch.rand(512, 5, 3, device=cuda)
+    y = (x.sum(dim=(1, 2)) > 7.5).float()
+    nets = []
+    for graph in (False, True):
+        torch.manual_seed(1)
+        net = LstmNetwork(3, 40, 1, num_layers=2, seq_len=5, batch_size=128, lr=0.01, num_iter=4, device=cuda,
+                          graph=graph)
+        # same optimiser arithmetic on both sides (capturable Adam keeps its step count on device)
+        net.optimizer = torch.optim.Adam(net.parameters(), lr=0.01, capturable=True)
+        net.fit(x, y)
+        nets.append(net)
+    torch.testing.assert_close(torch.tensor(nets[1].losses), torch.tensor(nets[0].losses), rtol=1e-4, atol=1e-5)
+    for p0, p1 in zip(nets[0].parameters(), nets[1].parameters()):
+        torch.testing.assert_close(p1, p0, rtol=1e-4, atol=1e-5)
