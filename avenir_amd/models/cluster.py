@@ -119,16 +119,23 @@ class KMeans:
         if self.init == "random":
             C = S[torch.randperm(S.shape[0], generator=g)[:k].to(S.device)]
         else:
-            # D^2 sampling by inverse CDF on the device: no host round trip per centre
-            u = torch.rand(k, generator=g, dtype=torch.float64)
+            # greedy k-means++ (Arthur & Vassilvitskii 2007, as scikit-learn): per centre draw
+            # L = 2 + ln k candidates by D^2 inverse-CDF sampling and keep the one that lowers the
+            # potential most; all on the device, no host round trip per centre
+            L = 2 + int(math.log(max(k, 2)))
+            u = torch.rand((k, L), generator=g, dtype=torch.float64)
             m = S.shape[0]
-            idx = [torch.full((1,), min(int(float(u[0]) * m), m - 1), dtype=torch.long, device=S.device)]
+            idx = [torch.full((1,), min(int(float(u[0, 0]) * m), m - 1), dtype=torch.long, device=S.device)]
             d2 = ((S - S.index_select(0, idx[0])) ** 2).sum(1).double()
+            uu = u.to(S.device)
             for i in range(1, k):
                 cum = torch.cumsum(d2, 0)
-                nxt = torch.searchsorted(cum, (cum[-1:] * float(u[i])), right=True).clamp_max(m - 1)
-                idx.append(nxt)
-                d2 = torch.minimum(d2, ((S - S.index_select(0, nxt)) ** 2).sum(1).double())
+                cand = torch.searchsorted(cum, cum[-1:] * uu[i], right=True).clamp_max(m - 1)   # [L]
+                dc = torch.cdist(S.index_select(0, cand).double(), S.double()).square()       # [L, m]
+                pot = torch.minimum(dc, d2.unsqueeze(0))                                     # [L, m]
+                best = pot.sum(1).argmin().view(1)
+                idx.append(cand.index_select(0, best))
+                d2 = pot.index_select(0, best)[0]
             C = S.index_select(0, torch.cat(idx))
         if comm.is_distributed:
             C = comm.broadcast(C.contiguous(), 0)

@@ -505,7 +505,7 @@ class DecisionTreeBuilder:
         rc = root_hist[0, :, offs[F]]
         pop = int(rc.sum())
         root = Node([], pop, float(impurity(rc.unsqueeze(0), p.algorithm)[0]),
-                    (rc.double() / max(pop, 1)).tolist(), depth=1)
+                    (rc.double() / max(pop, 1)).tolist(), depth=0)   # depth = #predicates on the path
         nodes = [root]
         frontier = [0]  # global node indices of the active frontier (local index = position)
         hist = root_hist  # [A, C, TB] of the frontier; later levels: built + derived by subtraction
@@ -628,7 +628,7 @@ class DecisionTreeBuilder:
                         nd.children.append(-1)
                         continue
                     info = float(impurity(cnt.unsqueeze(0), p.algorithm)[0])
-                    depth = nd.depth + 1
+                    depth = nd.depth + 1   # parentPredicates.size() + 1 (DecisionTreeBuilder.java:606)
                     stop = self._should_stop(pop, info, nd.info, depth) or info == 0.0
                     child = Node(nd.predicates + [preds[g]], pop, info, (cnt.double() / pop).tolist(),
                                  depth, stopped=stop, used_attrs=nd.used_attrs | {f})
