@@ -278,6 +278,28 @@ def _markov(args):
     _write(args, m.model_lines(cfg.field_delim_out))
 
 
+@job("genData", "tutorial fixture generator: --name <P/app script> --gen-args a,b,c [--seed s] (data/fixtures.py)")
+def _gen_data(args):
+    from .data.fixtures import FIXTURES
+
+    def num(v):
+        for t in (int, float):
+            try:
+                return t(v)
+            except ValueError:
+                pass
+        return v
+    if args.name not in FIXTURES:
+        raise SystemExit(f"unknown fixture {args.name}; one of {', '.join(sorted(FIXTURES))}")
+    gargs = [num(v) for v in args.gen_args.split(",")] if args.gen_args else []
+    out = FIXTURES[args.name](*gargs, seed=args.seed)
+    lines = out[0] if isinstance(out, tuple) else out
+    if args.output:
+        _write(args, lines)
+    else:
+        sys.stdout.write("\n".join(lines) + "\n")
+
+
 @job("wordCount", "word count sanity job")
 def _wc(args):
     from collections import Counter
@@ -388,6 +410,8 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--name")
     ap.add_argument("--port", type=int, default=5000)
     ap.add_argument("--k")
+    ap.add_argument("--gen-args", help="comma-separated generator arguments (genData)")
+    ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args(argv)
     if args.list or not args.job:
         for n, (_, h) in sorted(JOBS.items()):
