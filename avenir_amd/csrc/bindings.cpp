@@ -673,6 +673,29 @@ at::Tensor smo_solve(const at::Tensor& K, const at::Tensor& y, const at::Tensor&
   return iters;
 }
 
+// Working-set sub-problems: Kws [B, Q, Q], yws / aws / gws [B, Q], gap [B]; aws updated in place.
+at::Tensor smo_ws_solve(const at::Tensor& Kws, const at::Tensor& yws, at::Tensor& aws, const at::Tensor& gws,
+                        const at::Tensor& gap, double C, double eps, int64_t max_iter) {
+  const int64_t Q = avk::smo_ws_size();
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Kws, &yws, &aws, &gws, &gap}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(Kws.dim() == 3 && Kws.size(1) == Q && Kws.size(2) == Q, "Kws must be [B, Q, Q] with Q = ", Q);
+  const int64_t B = Kws.size(0);
+  TORCH_CHECK(aligned(Kws, 16), "Kws must be 16-byte aligned");
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&yws, &aws, &gws})
+    TORCH_CHECK(t->dim() == 2 && t->size(0) == B && t->size(1) == Q, "working-set vectors must be [B, Q]");
+  TORCH_CHECK(gap.numel() == B, "gap must be [B]");
+  TORCH_CHECK(C > 0 && eps > 0 && max_iter >= 0, "bad SMO parameters");
+  DevGuard g(Kws.device());
+  auto iters = at::zeros({B}, Kws.options().dtype(at::kInt));
+  avk::smo_ws_solve(Kws.data_ptr<float>(), yws.data_ptr<float>(), aws.data_ptr<float>(), gws.data_ptr<float>(),
+                    gap.data_ptr<float>(), (int)B, (float)C, (float)eps, (int)max_iter, iters.data_ptr<int>(),
+                    cur_stream(Kws));
+  return iters;
+}
+
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,
                                     int64_t extent, double laplace, double log_floor) {
   CHECK_DEV(counts);
@@ -1052,6 +1075,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sa_assign", &sa_assign);
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);
+  m.def("smo_ws_solve", &smo_ws_solve);
+  m.def("smo_ws_size", &avk::smo_ws_size);
   m.def("nb_finalize", &nb_finalize);
   m.def("weighted_gram", &weighted_gram);
   m.def("kmeans_assign", &kmeans_assign);

@@ -24,11 +24,37 @@ namespace av {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
+// ---- wave-wide reductions on DPP + v_readlane (no LDS traffic) ---------------------------------
+// Steps 1 and 2 are quad_perm swaps, 4 and 8 are row rotations inside each 16-lane row (all VALU
+// DPP moves, a few cycles each); the four row results are then combined from v_readlane into a
+// wave-uniform value.  __shfl_xor lowers to ds_bpermute (an LDS-pipe round trip per step), which
+// dominated latency-bound loops such as the SMO step (smo_ws_kernel).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+template <typename Op>
+__device__ __forceinline__ float wave_reduce_f(float v, Op op) {
+  v = op(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_f<0x124>(v));  // row_ror:4
+  v = op(v, dpp_f<0x128>(v));  // row_ror:8
+  return op(op(lane_f(v, 0), lane_f(v, 16)), op(lane_f(v, 32), lane_f(v, 48)));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+template <>
+__device__ __forceinline__ float wave_sum<float>(float v) {
+  return wave_reduce_f(v, [](float a, float b) { return a + b; });
 }
 
 template <typename T>
@@ -40,6 +66,10 @@ __device__ __forceinline__ T wave_max(T v) {
   }
   return v;
 }
+template <>
+__device__ __forceinline__ float wave_max<float>(float v) {
+  return wave_reduce_f(v, [](float a, float b) { return fmaxf(a, b); });
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
@@ -50,24 +80,32 @@ __device__ __forceinline__ T wave_min(T v) {
   }
   return v;
 }
+template <>
+__device__ __forceinline__ float wave_min<float>(float v) {
+  return wave_reduce_f(v, [](float a, float b) { return fminf(a, b); });
+}
 
-// (value, index) argmax over the wave; ties -> lowest index (deterministic).
-__device__ __forceinline__ void wave_argmax(float& v, int& idx) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float w = __shfl_xor(v, o, 64);
-    int j = __shfl_xor(idx, o, 64);
-    if (w > v || (w == v && j < idx)) { v = w; idx = j; }
-  }
+// (value, index) argmax / argmin over the wave; ties -> lowest index (deterministic).  The result
+// is wave-uniform.
+template <bool MAX>
+__device__ __forceinline__ void wave_arg_step(float& v, int& i, float v2, int i2) {
+  if ((MAX ? v2 > v : v2 < v) || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
-__device__ __forceinline__ void wave_argmin(float& v, int& idx) {
+template <bool MAX>
+__device__ __forceinline__ void wave_arg(float& v, int& idx) {
+  wave_arg_step<MAX>(v, idx, dpp_f<0xB1>(v), dpp_i<0xB1>(idx));
+  wave_arg_step<MAX>(v, idx, dpp_f<0x4E>(v), dpp_i<0x4E>(idx));
+  wave_arg_step<MAX>(v, idx, dpp_f<0x124>(v), dpp_i<0x124>(idx));
+  wave_arg_step<MAX>(v, idx, dpp_f<0x128>(v), dpp_i<0x128>(idx));
+  float r = lane_f(v, 0);
+  int ri = __builtin_amdgcn_readlane(idx, 0);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float w = __shfl_xor(v, o, 64);
-    int j = __shfl_xor(idx, o, 64);
-    if (w < v || (w == v && j < idx)) { v = w; idx = j; }
-  }
+  for (int l = 16; l < 64; l += 16) wave_arg_step<MAX>(r, ri, lane_f(v, l), __builtin_amdgcn_readlane(idx, l));
+  v = r;
+  idx = ri;
 }
+__device__ __forceinline__ void wave_argmax(float& v, int& idx) { wave_arg<true>(v, idx); }
+__device__ __forceinline__ void wave_argmin(float& v, int& idx) { wave_arg<false>(v, idx); }
 
 // 64-bit wave sum built from two 32-bit shuffles per step.
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {

@@ -90,6 +90,9 @@ void glm_grad(const float* X, long long ld, long long n, int D, const float* y, 
 // ---- svm.hip (K12) -------------------------------------------------------------------------
 void smo_solve(const float* K, const float* y, const float* diag, float* alpha, float* G, int B, int N, float C,
                float eps, int max_iter, int* iters, hipStream_t stream);
+int smo_ws_size();
+void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
+                  float eps, int max_iter, int* iters, hipStream_t stream);
 
 // ---- bayes.hip: model finalisation -----------------------------------------------------------
 void nb_finalize(const long long* counts, int C, int TB, const int* offs, const int* bins, int F, float laplace,

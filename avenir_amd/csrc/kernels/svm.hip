@@ -159,6 +159,119 @@ __global__ __launch_bounds__(SMO_THREADS) void smo_kernel(const float* __restric
   if (threadIdx.x == 0) iters[b] = it;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Working-set (decomposition) SMO inner solver: ONE wavefront per problem solves the Q-variable
+// sub-problem of a working set chosen on the device (top violators of the whole problem, see
+// models/svm.py::smo_decomposition) with the Q x Q kernel block resident in LDS (64 KB for Q=128).
+// Every reduction is a 64-lane shuffle (no barriers), so one SMO step costs a few hundred
+// cycles instead of the block-wide scans of smo_kernel over all N; the O(N) work moves to the
+// outer loop as one top-k and one batched GEMV per Q-variable step.
+//   Kws [B][Q][Q], yws [B][Q] (0 = unused slot), aws [B][Q] in/out, gws [B][Q] (gradient of the
+//   full problem restricted to the working set), gap [B] (global violation; the local
+//   tolerance is max(eps, 0.1 gap)).
+constexpr int WS_Q = 128;
+
+__global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Kall, const float* __restrict__ yall,
+                                                    float* __restrict__ aall, const float* __restrict__ gall,
+                                                    const float* __restrict__ gap, float C, float eps, int max_iter,
+                                                    int* __restrict__ iters) {
+  constexpr int Q = WS_Q, E = Q / 64;
+  __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float* Kb = Kall + (long long)b * Q * Q;
+  for (int e = lane; e < Q * Q / 4; e += 64)
+    reinterpret_cast<float4*>(&Ks[0][0])[e] = reinterpret_cast<const float4*>(Kb)[e];
+  float y[E], a[E], g[E], qd[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = lane + 64 * e;
+    y[e] = yall[b * Q + t];
+    a[e] = aall[b * Q + t];
+    g[e] = gall[b * Q + t];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int e = 0; e < E; ++e) qd[e] = Ks[lane + 64 * e][lane + 64 * e];
+  const float epsl = fmaxf(eps, 0.1f * gap[b]);
+  constexpr int NONE = 0x7fffffff;
+  int it = 0;
+  for (; it < max_iter; ++it) {
+    float gmax = -INFINITY;
+    int gi = NONE;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const bool up = y[e] > 0.f ? a[e] < C : (y[e] < 0.f && a[e] > 0.f);
+      const float v = -y[e] * g[e];
+      if (up && v > gmax) { gmax = v; gi = lane + 64 * e; }
+    }
+    av::wave_argmax(gmax, gi);
+    if (gi == NONE) break;
+    const int i = gi;
+    const float Kii = Ks[i][i];
+    float best = -INFINITY, gmax2 = -INFINITY;
+    int bj = NONE;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int t = lane + 64 * e;
+      const bool low = y[e] > 0.f ? a[e] > 0.f : (y[e] < 0.f && a[e] < C);
+      if (!low) continue;
+      const float yg = y[e] * g[e];
+      gmax2 = fmaxf(gmax2, yg);
+      const float bd = gmax + yg;
+      if (bd > 0.f) {
+        float q = Kii + qd[e] - 2.f * Ks[i][t];
+        q = q > 0.f ? q : TAU;
+        const float gain = bd * bd / q;
+        if (gain > best) { best = gain; bj = t; }
+      }
+    }
+    gmax2 = av::wave_max(gmax2);
+    av::wave_argmax(best, bj);
+    if (gmax + gmax2 < epsl || bj == NONE) break;
+    const int j = bj;
+    // fetch the pair's state from its owner lanes (slot index is wave-uniform)
+    const int si = i >> 6, sj = j >> 6;
+    float yi = 0.f, ai = 0.f, gi_ = 0.f, yj = 0.f, aj = 0.f, gj = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (e == si) { yi = __shfl(y[e], i & 63, 64); ai = __shfl(a[e], i & 63, 64); gi_ = __shfl(g[e], i & 63, 64); }
+      if (e == sj) { yj = __shfl(y[e], j & 63, 64); aj = __shfl(a[e], j & 63, 64); gj = __shfl(g[e], j & 63, 64); }
+    }
+    const float oi = ai, oj = aj;
+    float quad = Kii + Ks[j][j] - 2.f * Ks[i][j];
+    quad = quad > 0.f ? quad : TAU;
+    if (yi != yj) {
+      const float delta = (-gi_ - gj) / quad, diff = ai - aj;
+      ai += delta;
+      aj += delta;
+      if (diff > 0.f) { if (aj < 0.f) { aj = 0.f; ai = diff; } }
+      else if (ai < 0.f) { ai = 0.f; aj = -diff; }
+      if (diff > 0.f) { if (ai > C) { ai = C; aj = C - diff; } }
+      else if (aj > C) { aj = C; ai = C + diff; }
+    } else {
+      const float delta = (gi_ - gj) / quad, sum = ai + aj;
+      ai -= delta;
+      aj += delta;
+      if (sum > C) { if (ai > C) { ai = C; aj = sum - C; } }
+      else if (aj < 0.f) { aj = 0.f; ai = sum; }
+      if (sum > C) { if (aj > C) { aj = C; ai = sum - C; } }
+      else if (ai < 0.f) { ai = 0.f; aj = sum; }
+    }
+    const float di = (ai - oi) * yi, dj = (aj - oj) * yj;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int t = lane + 64 * e;
+      if (t == i) a[e] = ai;
+      if (t == j) a[e] = aj;
+      g[e] += y[e] * (Ks[i][t] * di + Ks[j][t] * dj);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) aall[b * Q + lane + 64 * e] = a[e];
+  if (lane == 0) iters[b] = it;
+}
+
 }  // namespace
 
 namespace avk {
@@ -167,6 +280,15 @@ void smo_solve(const float* K, const float* y, const float* diag, float* alpha, 
                float eps, int max_iter, int* iters, hipStream_t stream) {
   if (B <= 0 || N <= 0) return;
   smo_kernel<<<B, SMO_THREADS, 0, stream>>>(K, y, diag, alpha, G, N, C, eps, max_iter, iters);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int smo_ws_size() { return WS_Q; }
+
+void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
+                  float eps, int max_iter, int* iters, hipStream_t stream) {
+  if (B <= 0) return;
+  smo_ws_kernel<<<B, 64, 0, stream>>>(Kws, yws, aws, gws, gap, C, eps, max_iter, iters);
   AV_HIP_CHECK(hipGetLastError());
 }
 

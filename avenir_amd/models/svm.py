@@ -40,15 +40,16 @@ def kernel_matrix(A: torch.Tensor, B: torch.Tensor, kernel: str = "rbf", gamma: 
     raise ValueError(f"unknown kernel {kernel}")
 
 
-def smo_reference(K: np.ndarray, y: np.ndarray, C: float, eps: float = 1e-3, max_iter: int = 100000):
-    """Host SMO with the same working-set selection and update as ``smo_kernel``.
-    Returns (alpha, G, iterations)."""
+def smo_reference(K: np.ndarray, y: np.ndarray, C: float, eps: float = 1e-3, max_iter: int = 100000,
+                  alpha0: np.ndarray | None = None, G0: np.ndarray | None = None):
+    """Host SMO with the same working-set selection and update as ``smo_kernel`` (and, from a
+    given (alpha0, G0), as the working-set kernel ``smo_ws_kernel``).  Returns (alpha, G, iterations)."""
     K = np.asarray(K, np.float64)
     y = np.asarray(y, np.float64)
     N = y.size
     valid = y != 0
-    alpha = np.zeros(N)
-    G = np.where(valid, -1.0, 0.0)
+    alpha = np.zeros(N) if alpha0 is None else np.asarray(alpha0, np.float64).copy()
+    G = np.where(valid, -1.0, 0.0) if G0 is None else np.asarray(G0, np.float64).copy()
     QD = np.diag(K).copy()
     it = 0
     for it in range(max_iter):
@@ -124,9 +125,128 @@ def _rho(alpha: torch.Tensor, G: torch.Tensor, y: torch.Tensor, C: float) -> tor
     return torch.where(nf > 0, sf / nf.clamp_min(1), (ub + lb) / 2)
 
 
-def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_iter: int = 1_000_000):
-    """Solve B SVM duals: K [B, N, N], y [B, N] in {-1, 0 (padding), +1}.  Returns (alpha, rho, iters)."""
+class _WorkingSetSMO:
+    """State and one outer step of the working-set solver, written with static shapes so that a
+    block of steps can be captured as one HIP graph (see ``smo_decomposition``)."""
+
+    def __init__(self, K, y, C, eps, inner_iter, Q):
+        self.K, self.C, self.eps, self.inner_iter = K, float(C), float(eps), int(inner_iter)
+        B, N = y.shape
+        dev = K.device
+        self.gpu = dev.type == "cuda"
+        self.B, self.N, self.Q, self.h = B, N, Q, min(Q // 2, N)
+        self.yf = y.float().contiguous()
+        self.yp = torch.cat([self.yf, torch.zeros((B, 1), device=dev)], 1)     # slot N = unused
+        self.alpha = torch.zeros((B, N + 1), device=dev)
+        self.G = torch.where(self.yp != 0, -torch.ones_like(self.yp), torch.zeros_like(self.yp))
+        self.rows = torch.arange(B, device=dev)
+        self.inner_total = torch.zeros(B, dtype=torch.long, device=dev)
+        self.gap = torch.full((B,), float("inf"), device=dev)
+        self.ninf = torch.tensor(-float("inf"), device=dev)
+
+    def refresh_gap(self):
+        a, g, yf = self.alpha[:, :self.N], self.G[:, :self.N], self.yf
+        up = (yf > 0) & (a < self.C) | (yf < 0) & (a > 0)
+        low = (yf > 0) & (a > 0) | (yf < 0) & (a < self.C)
+        vu = torch.where(up, -yf * g, self.ninf)
+        vl = torch.where(low, yf * g, self.ninf)
+        self.gap.copy_(vu.max(1).values + vl.max(1).values)
+        return vu, vl
+
+    def step(self):
+        B, N, Q, h, dev = self.B, self.N, self.Q, self.h, self.K.device
+        vu, vl = self.refresh_gap()
+        vu_v, iu = torch.topk(vu, h, 1)
+        vl_v, il = torch.topk(vl, h, 1)
+        ws = torch.cat([iu, il], 1)
+        ok = torch.cat([vu_v > -float("inf"), (vl_v > -float("inf")) & ~(il.unsqueeze(2) == iu.unsqueeze(1)).any(2)], 1)
+        if ws.shape[1] < Q:                                                    # N < Q/2: pad the set
+            pad = Q - ws.shape[1]
+            ws = torch.cat([ws, torch.zeros((B, pad), dtype=ws.dtype, device=dev)], 1)
+            ok = torch.cat([ok, torch.zeros((B, pad), dtype=torch.bool, device=dev)], 1)
+        wsg = torch.where(ok, ws, torch.zeros_like(ws))
+        yws = (self.yp.gather(1, wsg) * ok).contiguous()
+        aws = self.alpha.gather(1, wsg).contiguous()
+        gws = self.G.gather(1, wsg).contiguous()
+        Kws = self.K[self.rows.view(-1, 1, 1), wsg.unsqueeze(2), wsg.unsqueeze(1)].float().contiguous()
+        a_old = aws.clone()
+        gap = torch.where(torch.isfinite(self.gap), self.gap, torch.zeros_like(self.gap)).contiguous()
+        if self.gpu:
+            it = _native.C().smo_ws_solve(Kws, yws, aws, gws, gap, self.C, self.eps, self.inner_iter)
+        else:
+            its = []
+            for b in range(B):
+                an, _, ib = smo_reference(Kws[b].double().numpy(), yws[b].double().numpy(), self.C,
+                                          max(self.eps, 0.1 * float(gap[b])), self.inner_iter,
+                                          aws[b].double().numpy(), gws[b].double().numpy())
+                aws[b] = torch.from_numpy(an).float()
+                its.append(ib)
+            it = torch.tensor(its)
+        self.inner_total += it.to(dev).long()
+        dA = (aws - a_old) * yws
+        self.alpha.scatter_(1, torch.where(ok, ws, torch.full_like(ws, N)), torch.where(ok, aws, torch.zeros_like(aws)))
+        Krows = self.K[self.rows.view(-1, 1), wsg].float()                     # [B, Q, N]
+        self.G[:, :N] += self.yf * torch.bmm(dA.unsqueeze(1), Krows).squeeze(1)
+
+
+def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_outer: int = 100_000,
+                      inner_iter: int = 2048, check_every: int = 16, Q: int | None = None, graph: bool = True):
+    """Working-set SMO for B problems (K [B, N, N], y [B, N] in {-1, 0, +1}).
+
+    Each outer step picks the Q/2 largest violators of the "up" set and the Q/2 largest of the
+    "low" set (the maximal violating pair is always among them), solves that Q-variable
+    sub-problem to a relaxed tolerance max(eps, 0.1 gap) — on the GPU in ``smo_ws_kernel``, one
+    wavefront per problem with the Q x Q kernel block in LDS — and applies the alpha changes to
+    the full gradient with one batched GEMV.  On the GPU ``check_every`` steps are one captured
+    HIP graph (static shapes; steps after convergence are no-ops because the sub-problem solver
+    stops at once), and the host reads the global violation gap once per replay.  Stops when
+    the gap < eps.  Returns (alpha, G, outer steps, inner steps).
+    """
+    Q = Q or (_native.C().smo_ws_size() if K.device.type == "cuda" else 128)
+    st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q)
+    outer = 0
+    if st.gpu and graph:
+        st.step()                                # eager warm-up: allocator pool, kernel caches
+        outer = 1
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(check_every):
+                    st.step()
+                st.refresh_gap()
+        torch.cuda.current_stream().wait_stream(s)
+        # capture records without executing: replay the block until converged
+        while outer < max_outer:
+            st.refresh_gap()
+            if bool((~(st.gap >= eps)).all()):
+                break
+            g.replay()
+            outer += check_every
+    else:
+        while outer < max_outer:
+            st.refresh_gap()
+            if outer % check_every == 0 and bool((~(st.gap >= eps)).all()):
+                break
+            st.step()
+            outer += 1
+    N = st.N
+    return st.alpha[:, :N].contiguous(), st.G[:, :N].contiguous(), outer, st.inner_total
+
+
+WS_MIN_N = 4096   # above this the working-set solver beats the single-workgroup full SMO (bench_svm.py)
+
+
+def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_iter: int = 1_000_000,
+              solver: str = "auto"):
+    """Solve B SVM duals: K [B, N, N], y [B, N] in {-1, 0 (padding), +1}.  Returns (alpha, rho, iters).
+    ``solver``: "full" (one persistent workgroup runs plain SMO over all N), "ws" (working-set
+    decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N)."""
     B, N = y.shape
+    if solver == "ws" or (solver == "auto" and K.device.type == "cuda" and N > WS_MIN_N):
+        alpha, G, outer, inner = smo_decomposition(K, y, C, eps, inner_iter=2048)
+        return alpha, _rho(alpha, G, y.float(), C), inner.int()
     if K.device.type == "cuda":
         Kc = K.float().contiguous()
         yc = y.float().contiguous()

@@ -239,3 +239,37 @@ def test_weighted_gram_mfma(cuda):
         assert torch.allclose(G, ref, rtol=1e-4, atol=1e-3 * n ** 0.5), (d, n)
         G1 = _native.C().weighted_gram(Xp.to(cuda), n, d, None).cpu()
         assert torch.allclose(G1, X.double() @ X.double().T, rtol=1e-4, atol=1e-3 * n ** 0.5)
+
+
+def _svm_dual(a, y, K):
+    a, y = a.double(), y.double()
+    return float(0.5 * (a * y) @ K.double() @ (a * y) - a.sum())
+
+
+def test_smo_working_set_cpu_matches_full():
+    from avenir_amd.models.svm import kernel_matrix, smo_decomposition, smo_reference
+    torch.manual_seed(0)
+    X = torch.randn(300, 4)
+    y = torch.where(X[:, 0] * X[:, 1] > 0, 1.0, -1.0)
+    K = kernel_matrix(X, X, "rbf", 0.5)
+    a_ref, _, _ = smo_reference(K.double().numpy(), y.double().numpy(), 1.0, 1e-4)
+    a, G, outer, inner = smo_decomposition(K.unsqueeze(0), y.view(1, -1), 1.0, 1e-4, Q=64)
+    assert outer > 1
+    assert abs(_svm_dual(a[0], y, K) - _svm_dual(torch.from_numpy(a_ref), y, K)) < 1e-4 * abs(_svm_dual(a[0], y, K))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [700, 3000])
+def test_smo_working_set_gpu_matches_full(cuda, N):
+    from avenir_amd.models.svm import kernel_matrix, smo_batch
+    torch.manual_seed(N)
+    X = torch.randn(N, 6, device=cuda)
+    y = torch.where(X[:, 0] * X[:, 1] + 0.3 * X[:, 2] > 0, 1.0, -1.0)
+    K = kernel_matrix(X, X, "rbf", 0.4).unsqueeze(0).contiguous()
+    af, rf, _ = smo_batch(K, y.view(1, -1), 1.0, 1e-3, solver="full")
+    aw, rw, _ = smo_batch(K, y.view(1, -1), 1.0, 1e-3, solver="ws")
+    df, dw = _svm_dual(af[0], y, K[0]), _svm_dual(aw[0], y, K[0])
+    assert abs(df - dw) < 2e-4 * abs(df)
+    ff = (af[0] * y) @ K[0] - rf[0]
+    fw = (aw[0] * y) @ K[0] - rw[0]
+    assert (torch.sign(ff) == torch.sign(fw)).float().mean() > 0.995
