@@ -79,6 +79,45 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
                        cur_stream(codes));
 }
 
+// K2 over row-packed records: words int16 [>= n] (bit layout from shifts / widths), bins / offs
+// int32 [F] (device), out int64 [C][TB] (accumulated into).
+void class_histogram_rowpacked(const at::Tensor& words, int64_t n, std::vector<int64_t> shifts,
+                               std::vector<int64_t> widths, int64_t label_shift, int64_t label_width,
+                               const at::Tensor& bins, const at::Tensor& offs, int64_t total_bins, int64_t n_classes,
+                               at::Tensor& out, bool count_labels) {
+  CHECK_DEV(words);
+  CHECK_DTYPE(words, at::kShort);
+  TORCH_CHECK(words.dim() == 1 && n >= 0 && n <= words.numel(), "words must be [>= n]");
+  TORCH_CHECK(aligned(words, 16), "words must be 16-byte aligned");
+  const int64_t F = (int64_t)shifts.size();
+  TORCH_CHECK(F >= 1 && F <= 8 && (int64_t)widths.size() == F, "1..8 packed fields");
+  std::vector<int> sh(F), wd(F);
+  int64_t used = 0;
+  for (int64_t k = 0; k < F; ++k) {
+    TORCH_CHECK(widths[k] >= 1 && widths[k] <= 3 && shifts[k] >= 0 && shifts[k] + widths[k] <= 16,
+                "packed field must be 1..3 bits inside 16");
+    sh[k] = (int)shifts[k];
+    wd[k] = (int)widths[k];
+    used = std::max<int64_t>(used, shifts[k] + widths[k]);
+  }
+  TORCH_CHECK(n_classes >= 1 && n_classes <= 2, "row-packed histogram supports 1 or 2 classes");
+  TORCH_CHECK(n_classes == 1 || (label_width == n_classes && label_shift >= 0 && label_shift + label_width <= 16),
+              "the class must be C one-hot bits inside the 16-bit record");
+  CHECK_DEV(bins);
+  CHECK_DTYPE(bins, at::kInt);
+  CHECK_DEV(offs);
+  CHECK_DTYPE(offs, at::kInt);
+  TORCH_CHECK(bins.numel() == F && offs.numel() == F, "bins / offs must have F entries");
+  CHECK_DEV(out);
+  CHECK_DTYPE(out, at::kLong);
+  TORCH_CHECK(out.numel() == n_classes * total_bins, "out must be [C * TB]");
+  DevGuard g(words.device());
+  avk::class_histogram_rowpacked(reinterpret_cast<const uint16_t*>(words.data_ptr()), n, sh.data(), wd.data(), (int)F,
+                                 (int)label_shift, (int)label_width, bins.data_ptr<int>(), offs.data_ptr<int>(),
+                                 (int)total_bins, (int)n_classes, count_labels ? 1 : 0,
+                                 reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(words));
+}
+
 void pair_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at::Tensor>& labels,
                     const at::Tensor& bins, const at::Tensor& pairs, const at::Tensor& poff,
                     int64_t max_tab, int64_t n_classes, at::Tensor& out) {
@@ -1057,6 +1096,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "avenir_amd native kernels (HIP/CDNA4 gfx950) and host runtime";
   m.def("class_histogram", &class_histogram);
   m.def("pair_histogram", &pair_histogram);
+  m.def("class_histogram_rowpacked", &class_histogram_rowpacked);
   m.def("bigram_histogram", &bigram_histogram);
   m.def("class_moments", &class_moments);
   m.def("nb_predict", &nb_predict);

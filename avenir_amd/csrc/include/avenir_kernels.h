@@ -21,6 +21,11 @@ void bigram_histogram(const int16_t* states, long long n, int L, const uint8_t* 
 void class_moments(const float* x, long long ld, long long n, int nfeat, const uint8_t* labels,
                    int n_classes, double* part, int nblocks, double* out, hipStream_t stream);
 int moments_blocks(long long n);
+// K2 on row-packed records: one uint16 word per record, field k at bit h_shift[k] (1..3 bits,
+// all-ones = missing), class at label_shift.
+void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_shift, const int* h_width, int nfeat,
+                               int label_shift, int label_width, const int* d_bins, const int* d_offs, int total_bins,
+                               int n_classes, int count_labels, unsigned long long* out, hipStream_t stream);
 
 // ---- bayes.hip ----------------------------------------------------------------------------
 void nb_predict(const uint8_t* codes, long long ld, long long n, int nfeat, const int* offs,

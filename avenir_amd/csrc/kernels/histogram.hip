@@ -133,6 +133,7 @@ __global__ __launch_bounds__(HB) void hist_packed_kernel(
 
   // tail rows (n % 16) — block 0 only, scalar
   if (blockIdx.x == 0) {
+    __syncthreads();  // slice 0 is final before the tail's atomics land in it
     for (long long r = nvec * 16 + threadIdx.x; r < n; r += HB) {
       const unsigned c = labels ? labels[r] : 0u;
 #pragma unroll
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(HB) void hist_split_kernel(
 
   // tail rows (n % 16): block 0, scalar LDS atomics
   if (blockIdx.x == 0) {
+    __syncthreads();  // slice 0 is final before the tail's atomics land in it
     for (long long r = nvec * 16 + threadIdx.x; r < n; r += HB) {
       const unsigned c = (C > 1) ? labels[r] : 0u;
       if (c >= (unsigned)C) continue;
@@ -362,6 +364,187 @@ void launch_split(const uint8_t* codes, long long ld, long long n, const uint8_t
     }
 #undef AV_SPLIT
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2, row-packed layout: every record is ONE 16-bit word holding all of its categorical codes
+// and its class (field k at bit sh[k], width w[k] <= 3 bits, the all-ones value of a field being
+// its missing code, never a valid bin; for C = 2 the class is two one-hot bits at lsh, both clear
+// for an unknown class).  For low-cardinality schemas such as R/churn.json (5 features of 3-5
+// values + a binary class = 14 bits) this is 2 bytes per record instead of F + 1 = 6 bytes of
+// byte-per-code columns.
+//
+// At 2 B/record the pass is ALU-bound unless a record costs < ~30 VALU ops, so the counting uses
+// only full-rate 32-bit ops (a 64-bit variable shift per (record, feature, class) — the byte-
+// counter-in-u64 scheme — measured 1.48 ms per 2^30 records, slower than the 6 B/record columns):
+// per lane and (class, feature) one u32 of eight 4-bit counters indexed by the code; a record
+// costs, per feature, one v_bfe_u32 + one shift for the nibble offset and one v_lshl_add_u32 per
+// class (acc += is_class << 4*code), the class masks being two more bfe's.
+// After every tile (8 records per lane, <= 8 per nibble) the nibbles are spread into two u32 of
+// byte counters (even / odd codes); every 31 tiles (<= 248 per byte) those are widened into
+// 16-bit lane fields; after 256 widenings (<= 63488) or at the end the fields are summed across
+// the wave into the wave's private LDS slice.
+// ---------------------------------------------------------------------------------------------
+struct RowPackSpec {
+  int sh[8];  // bit offset of feature k
+  int w[8];   // bit width of feature k (1..3)
+  int lsh;    // first of the C one-hot class bits (C >= 2)
+};
+
+template <int NF, int C>
+__global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __restrict__ words, long long n,
+                                                          RowPackSpec spec, const int* __restrict__ bins,
+                                                          const int* __restrict__ offs, int total_bins,
+                                                          int count_labels, unsigned long long* __restrict__ out) {
+  constexpr int TAB = NF * C * 8;
+  constexpr int WPB = HB / AV_WAVE;
+  constexpr int FLUSH = 31;  // 31 tiles x 8 records = 248 increments per byte counter at most
+  __shared__ unsigned int s_tab[WPB * TAB];
+  for (int i = threadIdx.x; i < WPB * TAB; i += HB) s_tab[i] = 0;
+  __syncthreads();
+  unsigned int* my_tab = s_tab + av::wave_id() * TAB;
+  const uint4* w4 = reinterpret_cast<const uint4*>(words);
+
+  unsigned a4[C][NF], be[C][NF], bo[C][NF], w16[C][NF][4];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int k = 0; k < NF; ++k) {
+      a4[c][k] = 0;
+      be[c][k] = 0;
+      bo[c][k] = 0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) w16[c][k][m] = 0;
+    }
+  const unsigned N4 = 0x0F0F0F0Fu, B8 = 0x00FF00FFu;
+  auto spread = [&]() __attribute__((always_inline)) {  // nibbles -> bytes: be byte j = code 2j, bo byte j = code 2j + 1
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        be[c][k] += a4[c][k] & N4;
+        bo[c][k] += (a4[c][k] >> 4) & N4;
+        a4[c][k] = 0;
+      }
+  };
+  auto widen = [&]() __attribute__((always_inline)) {  // bytes -> 16-bit fields: w16[0] codes {0, 4}, [1] {2, 6}, [2] {1, 5}, [3] {3, 7}
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        w16[c][k][0] += be[c][k] & B8;
+        w16[c][k][1] += (be[c][k] >> 8) & B8;
+        w16[c][k][2] += bo[c][k] & B8;
+        w16[c][k][3] += (bo[c][k] >> 8) & B8;
+        be[c][k] = 0;
+        bo[c][k] = 0;
+      }
+  };
+  auto reduce_to_lds = [&]() __attribute__((always_inline)) {  // lane l < 8 owns code l
+    const int l = av::lane_id();
+    const int r = l & 3, mi = ((r & 1) << 1) | (r >> 1), half = (l >> 2) & 1;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        unsigned sel = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const unsigned lo = av::wave_sum(w16[c][k][m] & 0xFFFFu);
+          const unsigned hi = av::wave_sum(w16[c][k][m] >> 16);
+          if (m == mi) sel = half ? hi : lo;
+          w16[c][k][m] = 0;
+        }
+        if (l < 8) my_tab[(k * C + c) * 8 + l] += sel;
+      }
+  };
+
+  const long long nvec = n >> 3;  // 8 records per 16-byte load
+  const long long ntiles = (nvec + AV_WAVE - 1) / AV_WAVE;
+  const long long gw = (long long)blockIdx.x * WPB + av::wave_id();
+  const long long nw = (long long)gridDim.x * WPB;
+  int since_flush = 0, flushes = 0;
+  // one tile of loads always in flight ahead of the tile being counted (the counting is ~30 VALU
+  // ops per record, so a wave that only loads after counting leaves HBM idle)
+  long long v = gw * AV_WAVE + av::lane_id();
+  uint4 qn = (gw < ntiles && v < nvec) ? w4[v] : make_uint4(0u, 0u, 0u, 0u);
+  for (long long t = gw; t < ntiles; t += nw) {
+    const uint4 q = qn;
+    const bool have = v < nvec;
+    v += nw * AV_WAVE;
+    if (t + nw < ntiles && v < nvec) qn = w4[v];
+    if (have) {
+      const unsigned dw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const unsigned d = dw[h >> 1];
+        const int o = 16 * (h & 1);  // record h sits in bits [o, o + 16) of its dword
+        unsigned x[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          x[c] = C == 1 ? 1u : __builtin_amdgcn_ubfe(d, (unsigned)(spec.lsh + o + c), 1u);
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+          const unsigned s4 = __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]) << 2;
+#pragma unroll
+          for (int c = 0; c < C; ++c) a4[c][k] += x[c] << s4;
+        }
+      }
+    }
+    spread();
+    if (++since_flush == FLUSH) {  // wave-uniform
+      widen();
+      since_flush = 0;
+      if (++flushes == 256) {
+        reduce_to_lds();
+        flushes = 0;
+      }
+    }
+  }
+  widen();
+  reduce_to_lds();
+
+  if (blockIdx.x == 0) {  // tail records (n % 8), once every wave's slice is final
+    __syncthreads();
+    for (long long r = nvec * 8 + threadIdx.x; r < n; r += HB) {
+      const unsigned w = words[r];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        if (C > 1 && !__builtin_amdgcn_ubfe(w, (unsigned)(spec.lsh + c), 1u)) continue;
+#pragma unroll
+        for (int k = 0; k < NF; ++k)
+          atomicAdd(&s_tab[(k * C + c) * 8 + __builtin_amdgcn_ubfe(w, (unsigned)spec.sh[k], (unsigned)spec.w[k])], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TAB; i += HB) {
+    unsigned long long tot = 0;
+#pragma unroll
+    for (int w = 0; w < WPB; ++w) tot += s_tab[w * TAB + i];
+    s_tab[i] = (unsigned)tot;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TAB; i += HB) {
+    const int k = i / (C * 8), c = (i / 8) % C, b = i % 8;
+    const unsigned v = s_tab[i];
+    if (v && b < bins[k]) atomicAdd(&out[(long long)c * total_bins + offs[k] + b], (unsigned long long)v);
+  }
+  if (count_labels && threadIdx.x < C) {  // every record of a class has exactly one feature-0 code
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) sum += s_tab[(0 * C + threadIdx.x) * 8 + b];
+    if (sum) atomicAdd(&out[(long long)threadIdx.x * total_bins + total_bins - 1], sum);
+  }
+}
+
+template <int NF, int C>
+void launch_rowpack(const uint16_t* words, long long n, const RowPackSpec& spec, const int* bins, const int* offs,
+                    int total_bins, int count_labels, unsigned long long* out, hipStream_t stream) {
+  static const int res = av::resident_blocks((const void*)hist_rowpack_kernel<NF, C>, HB, 0);
+  const int grid = std::min(av::stream_grid(std::max(1LL, n >> 3), HB, 4, 4096), res);
+  hist_rowpack_kernel<NF, C><<<grid, HB, 0, stream>>>(words, n, spec, bins, offs, total_bins, count_labels, out);
+  AV_HIP_CHECK(hipGetLastError());
 }
 
 // General path: LDS-privatised table with R replicas (one per wave when it fits) so that lanes of
@@ -656,5 +839,35 @@ void class_moments(const float* x, long long ld, long long n, int nfeat, const u
 }
 
 int moments_blocks(long long n) { return av::stream_grid(n, HB, 16, 1024); }
+
+void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_shift, const int* h_width, int nfeat,
+                               int label_shift, int label_width, const int* d_bins, const int* d_offs, int total_bins,
+                               int n_classes, int count_labels, unsigned long long* out, hipStream_t stream) {
+  if (n <= 0 || nfeat <= 0) return;
+  if (nfeat > 8 || n_classes < 1 || n_classes > 2) throw std::runtime_error("row-packed histogram: F <= 8, C <= 2");
+  RowPackSpec spec{};
+  for (int k = 0; k < nfeat; ++k) {
+    if (h_width[k] < 1 || h_width[k] > 3) throw std::runtime_error("row-packed histogram: field widths 1..3 bits");
+    spec.sh[k] = h_shift[k];
+    spec.w[k] = h_width[k];
+  }
+  if (n_classes > 1 && label_width != n_classes)
+    throw std::runtime_error("row-packed histogram: the class is C one-hot bits");
+  spec.lsh = n_classes > 1 ? label_shift : 0;
+#define AV_RP(NF)                                                                                          \
+  (n_classes == 1 ? launch_rowpack<NF, 1>(words, n, spec, d_bins, d_offs, total_bins, count_labels, out, stream) \
+                  : launch_rowpack<NF, 2>(words, n, spec, d_bins, d_offs, total_bins, count_labels, out, stream))
+  switch (nfeat) {
+    case 1: AV_RP(1); break;
+    case 2: AV_RP(2); break;
+    case 3: AV_RP(3); break;
+    case 4: AV_RP(4); break;
+    case 5: AV_RP(5); break;
+    case 6: AV_RP(6); break;
+    case 7: AV_RP(7); break;
+    default: AV_RP(8); break;
+  }
+#undef AV_RP
+}
 
 }  // namespace avk

@@ -47,6 +47,7 @@ class Table:
     lines: list[str] | None = None
     row_offset: int = 0                      # global index of row 0 (sharded loads)
     meta: dict = field(default_factory=dict)
+    rowpack: object | None = None            # ops.histogram.RowPacked (see pack_rows)
 
     # -- geometry ---------------------------------------------------------------------------------
     @property
@@ -76,6 +77,14 @@ class Table:
     @property
     def device(self) -> torch.device:
         return self.codes.device
+
+    def pack_rows(self) -> "Table":
+        """Attach the 16-bit row-packed form of the binned codes + class
+        (``ops.histogram.pack_rows``) when the schema fits; Naive Bayes training then streams
+        2 bytes per record instead of one byte per code column.  No-op when it does not fit."""
+        from ..ops.histogram import pack_rows
+        self.rowpack = pack_rows(self.codes, self.n, self.bins, self.labels, self.n_classes)
+        return self
 
     def to(self, device) -> "Table":
         dev = torch.device(device)

@@ -73,7 +73,11 @@ class NaiveBayes:
         self.class_values = list(t.class_field.cardinality) if t.class_field else ["_"]
         C = t.n_classes
         # one fused launch: [C, TB] feature counts + a class-count column (no host sync)
-        both = H.class_histogram(t.codes, t.n, self.bins, t.labels, C, count_labels=True)
+        rp = self._packed(t)
+        if rp is not None:
+            both = H.class_histogram_packed(rp, count_labels=True)
+        else:
+            both = H.class_histogram(t.codes, t.n, self.bins, t.labels, C, count_labels=True)
         moments = H.class_moments(t.numeric, t.n, t.labels, C)
         if reduce and comm.is_distributed:
             comm.all_reduce(both)
@@ -85,12 +89,23 @@ class NaiveBayes:
         self._tables = None
         return self
 
+    def _packed(self, t: Table):
+        """The table's row-packed records when they describe exactly these rows and bins."""
+        rp = getattr(t, "rowpack", None)
+        if rp is not None and rp.n == t.n and rp.n_classes == t.n_classes and rp.bins == self.bins:
+            return rp
+        return None
+
     def partial_fit(self, t: Table) -> "NaiveBayes":
         """Accumulate more data (streaming / out-of-core).  Call ``reduce()`` once at the end."""
         if self.counts is None:
             return self.fit(t, reduce=False)
-        H.class_histogram(t.codes, t.n, self.bins, t.labels, t.n_classes, out=self._both,
-                          count_labels=True)
+        rp = self._packed(t)
+        if rp is not None:
+            H.class_histogram_packed(rp, out=self._both, count_labels=True)
+        else:
+            H.class_histogram(t.codes, t.n, self.bins, t.labels, t.n_classes, out=self._both,
+                              count_labels=True)
         self.moments += H.class_moments(t.numeric, t.n, t.labels, t.n_classes)
         self._tables = None
         return self

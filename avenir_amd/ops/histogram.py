@@ -2,6 +2,7 @@
 CPU tensors -> the PyTorch reference implementation of the same op (golden oracle)."""
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Sequence
 
 import torch
@@ -67,6 +68,114 @@ def class_histogram(codes: torch.Tensor, n: int, bins: Sequence[int], labels: to
         out[:, o:o + b] += torch.bincount(idx, minlength=C * b).view(C, b)
         o += b
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# row-packed records: every categorical code of a record and its class in ONE 16-bit word
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class RowPacked:
+    """Records packed one 16-bit word each (``pack_rows``): feature k's code in bits
+    [shifts[k], shifts[k] + widths[k]) (its all-ones value = missing code); for C = 2 the class
+    as two one-hot bits at label_shift (bit c set = class c, none set = unknown class)."""
+    words: torch.Tensor      # int16 [>= n], numel a multiple of 8 (16-byte vector loads)
+    n: int
+    bins: list[int]
+    shifts: list[int]
+    widths: list[int]
+    label_shift: int
+    label_width: int         # 0: no class field (C = 1)
+    n_classes: int
+
+
+def rowpack_layout(bins: Sequence[int], n_classes: int):
+    """(shifts, widths, label_shift, label_width) of the 16-bit record, or None when the schema
+    does not fit: at most 8 features of at most 7 values (bit_length(b) bits, so the all-ones
+    value >= b is free for 'missing') and 1 or 2 classes (C = 2: two one-hot class bits)."""
+    bins = [int(b) for b in bins]
+    C = int(n_classes)
+    if not bins or len(bins) > 8 or C < 1 or C > 2 or min(bins) < 1 or max(bins) > 7:
+        return None
+    widths = [b.bit_length() for b in bins]
+    shifts, s = [], 0
+    for w in widths:
+        shifts.append(s)
+        s += w
+    lw = 2 if C == 2 else 0
+    if s + lw > 16:
+        return None
+    return shifts, widths, s, lw
+
+
+def pack_rows(codes: torch.Tensor, n: int, bins: Sequence[int], labels: torch.Tensor | None,
+              n_classes: int) -> RowPacked | None:
+    """Pack ``codes`` uint8 [F, >= n] (+ ``labels``) into one 16-bit word per record, on the
+    tensors' device; None when ``rowpack_layout`` refuses the schema.  Codes >= bins[k] and
+    labels >= C become the field's all-ones value, which every consumer skips — exactly the
+    records the column histogram skips, so the counts are identical."""
+    bins = [int(b) for b in bins]
+    C = int(n_classes) if labels is not None else 1
+    if labels is not None and C == 1:
+        return None                      # a 1-class label column still filters rows: keep columns
+    lay = rowpack_layout(bins, C)
+    if lay is None or codes.shape[0] != len(bins):
+        return None
+    shifts, widths, lsh, lw = lay
+    w = torch.zeros(max(8, (n + 7) // 8 * 8), dtype=torch.int32, device=codes.device)
+    body = w[:n]
+    for k, (b, s, wd) in enumerate(zip(bins, shifts, widths)):
+        v = codes[k, :n].to(torch.int32)
+        body |= torch.where(v < b, v, torch.full_like(v, (1 << wd) - 1)) << s
+    if lw:
+        v = labels[:n].to(torch.int32)
+        body |= torch.where(v < C, 1 << v.clamp_max(C - 1), torch.zeros_like(v)) << lsh
+    words = torch.where(w >= 32768, w - 65536, w).to(torch.int16)
+    return RowPacked(words, int(n), bins, shifts, widths, lsh, lw, C)
+
+
+def unpack_rows(rp: RowPacked) -> tuple[torch.Tensor, torch.Tensor | None]:
+    """Inverse of ``pack_rows``: (codes uint8 [F, pad16(n)], labels uint8 [pad16(n)] or None),
+    missing / unknown values as 255."""
+    n = rp.n
+    ld = max(16, (n + 15) // 16 * 16)
+    w = rp.words[:n].to(torch.int32) & 0xFFFF
+    codes = torch.full((len(rp.bins), ld), 255, dtype=torch.uint8, device=w.device)
+    for k, (b, s, wd) in enumerate(zip(rp.bins, rp.shifts, rp.widths)):
+        v = (w >> s) & ((1 << wd) - 1)
+        codes[k, :n] = torch.where(v < b, v, torch.full_like(v, 255)).to(torch.uint8)
+    labels = None
+    if rp.label_width:
+        labels = torch.full((ld,), 255, dtype=torch.uint8, device=w.device)
+        v = (w >> rp.label_shift) & ((1 << rp.label_width) - 1)
+        cls = torch.full_like(v, 255)                                     # one-hot class bits
+        for c in range(rp.n_classes):
+            cls = torch.where(v == (1 << c), torch.full_like(v, c), cls)
+        labels[:n] = cls.to(torch.uint8)
+    return codes, labels
+
+
+def class_histogram_packed(rp: RowPacked, out: torch.Tensor | None = None,
+                           count_labels: bool = False) -> torch.Tensor:
+    """``class_histogram`` over row-packed records (same ``[C, sum(bins) (+1)]`` int64 result).
+    GPU: the K2 row-packed kernel streams 2 bytes per record (8 records per 16-byte load)
+    instead of F + 1 bytes of code columns; CPU: unpack + the column reference."""
+    C = rp.n_classes
+    tb = sum(rp.bins) + (1 if count_labels else 0)
+    if out is None:
+        out = torch.zeros((C, tb), dtype=torch.int64, device=rp.words.device)
+    if rp.n == 0:
+        return out
+    if rp.words.is_cuda:
+        offs = [0] * len(rp.bins)
+        for f in range(1, len(rp.bins)):
+            offs[f] = offs[f - 1] + rp.bins[f - 1]
+        dev = rp.words.device
+        _native.C().class_histogram_rowpacked(rp.words, int(rp.n), rp.shifts, rp.widths, rp.label_shift,
+                                              rp.label_width, _dev_i32(rp.bins, dev),
+                                              _dev_i32(offs, dev), tb, C, out, bool(count_labels))
+        return out
+    codes, labels = unpack_rows(rp)
+    return class_histogram(codes, rp.n, rp.bins, labels, C, out=out, count_labels=count_labels)
 
 
 def pair_histogram(codes: torch.Tensor, n: int, bins: Sequence[int],

@@ -12,7 +12,10 @@ all-reduce of the [C, TB+1] count table, and the model finalisation (log-probabi
 the predictor).  Weak scaling: every GPU owns ``rows_per_gpu`` synthetic records (same
 distributions as the reference's ``usage.rb``), generated on device before timing.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows-per-gpu R]
+The records are held on device as one 16-bit word per record (5 codes + class, ``--layout
+rowpacked``, packed once at load time; lossless) or as uint8 code columns (``--layout columns``).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows-per-gpu R] [--layout L]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -33,6 +36,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 30)
     ap.add_argument("--predict", action="store_true", help="also time batched inference")
+    ap.add_argument("--layout", choices=["rowpacked", "columns"], default="rowpacked",
+                    help="device layout of the encoded records: one 16-bit word per record "
+                         "(2 B/record) or one uint8 column per feature + label (6 B/record)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -57,6 +63,15 @@ def main() -> int:
     feats = schema.feature_fields
     table = Table(schema, n, codes, feats, torch.zeros((0, codes.shape[1]), device=dev), [],
                   labels, schema.find_class_attr_field())
+    bytes_per_row = codes.shape[0] + 1  # 5 feature codes + 1 label byte
+    if args.layout == "rowpacked":
+        # lossless re-encoding done once at load time, like the dictionary encoding itself
+        table.pack_rows()
+        if table.rowpack is None:
+            print("[bench] schema does not fit 16-bit records: using code columns", file=sys.stderr)
+            args.layout = "columns"
+        else:
+            bytes_per_row = 2
     nb = NaiveBayes(schema, comm=comm)
 
     def step():
@@ -87,8 +102,7 @@ def main() -> int:
 
     ms = dt * 1000.0 / args.steps
     rows_per_s = n * comm.world * args.steps / dt
-    bytes_per_row = codes.shape[0] + 1  # 5 feature codes + 1 label byte
-    extra = {"ms_per_step": ms, "hbm_gbps_per_gpu": n * bytes_per_row / (ms / 1000.0) / 1e9}
+    extra = {"layout": args.layout, "ms_per_step": ms, "hbm_gbps_per_gpu": n * bytes_per_row / (ms / 1000.0) / 1e9}
     if args.predict:
         pr_n = min(n, 1 << 26)
         sub = Table(schema, pr_n, codes[:, : ((pr_n + 15) // 16) * 16].contiguous(), feats,
@@ -116,7 +130,8 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "uint8-codes/int64-counts (exact integer counting)",
+            "dtype": ("uint16 row-packed categorical records (2 B/record, lossless)/int64 counts (exact)"
+                      if args.layout == "rowpacked" else "uint8-codes/int64-counts (exact integer counting)"),
             "data": "synthetic (device-generated, resource/usage.rb distributions)",
             "config": {
                 "model": "NaiveBayes(resource/churn.json: 5 categorical features, 2 classes)",

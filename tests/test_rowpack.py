@@ -1,0 +1,121 @@
+"""Row-packed categorical records (one 16-bit word per record) for the class histogram that
+Naive Bayes training runs on: bit layout rules, lossless pack/unpack, CPU and HIP counts equal
+to the byte-per-code column histogram (including missing codes and unknown classes), and the
+Naive Bayes model trained from the packed form equal to the one trained from columns."""
+import pytest
+import torch
+
+from avenir_amd.data.synth import CHURN_SCHEMA, churn_device
+from avenir_amd.data.table import Table
+from avenir_amd.models.bayes import NaiveBayes
+from avenir_amd.ops import histogram as H
+from avenir_amd.utils.schema import FeatureSchema
+
+gpu = pytest.mark.gpu
+
+
+def _random_codes(n, bins, C, seed=0, missing=0.05):
+    g = torch.Generator().manual_seed(seed)
+    F = len(bins)
+    ld = max(16, (n + 15) // 16 * 16)
+    codes = torch.full((F, ld), 255, dtype=torch.uint8)
+    for k, b in enumerate(bins):
+        v = torch.randint(0, b, (n,), generator=g)
+        v[torch.rand(n, generator=g) < missing] = 255
+        codes[k, :n] = v.to(torch.uint8)
+    labels = torch.full((ld,), 255, dtype=torch.uint8)
+    lab = torch.randint(0, C, (n,), generator=g)
+    lab[torch.rand(n, generator=g) < missing] = 255
+    labels[:n] = lab.to(torch.uint8)
+    return codes, labels
+
+
+def test_layout_rules():
+    assert H.rowpack_layout([4, 3, 3, 3, 5], 2) == ([0, 3, 5, 7, 9], [3, 2, 2, 2, 3], 12, 2)
+    assert H.rowpack_layout([1, 2, 3], 1) == ([0, 1, 3], [1, 2, 2], 5, 0)
+    assert H.rowpack_layout([8], 2) is None              # 8 values + a missing code need 4 bits
+    assert H.rowpack_layout([7] * 5, 2) is None          # 15 + 2 bits > 16
+    assert H.rowpack_layout([3] * 9, 1) is None          # more than 8 fields
+    assert H.rowpack_layout([3, 3], 3) is None           # more than 2 classes
+
+
+def test_pack_unpack_lossless():
+    bins = [4, 3, 3, 3, 5]
+    n = 1001
+    codes, labels = _random_codes(n, bins, 2, seed=1)
+    rp = H.pack_rows(codes, n, bins, labels, 2)
+    assert rp is not None and rp.words.dtype == torch.int16 and rp.words.numel() % 8 == 0
+    c2, l2 = H.unpack_rows(rp)
+    ok = codes[:, :n] < torch.tensor(bins, dtype=torch.uint8).view(-1, 1)
+    assert torch.equal(torch.where(ok, codes[:, :n], torch.full_like(codes[:, :n], 255)), c2[:, :n])
+    lok = labels[:n] < 2
+    assert torch.equal(torch.where(lok, labels[:n], torch.full_like(labels[:n], 255)), l2[:n])
+
+
+def test_packed_histogram_cpu_matches_columns():
+    bins = [4, 3, 3, 3, 5]
+    n = 3333
+    codes, labels = _random_codes(n, bins, 2, seed=2)
+    ref = H.class_histogram(codes, n, bins, labels, 2, count_labels=True)
+    rp = H.pack_rows(codes, n, bins, labels, 2)
+    assert torch.equal(ref, H.class_histogram_packed(rp, count_labels=True))
+
+
+def test_table_pack_rows_and_bayes_cpu():
+    schema = FeatureSchema.from_json(CHURN_SCHEMA)
+    n = 5000
+    codes, labels = churn_device(n, seed=7, device="cpu")
+    t = Table(schema, n, codes, schema.feature_fields, torch.zeros((0, codes.shape[1])), [], labels,
+              schema.find_class_attr_field())
+    a = NaiveBayes(schema).fit(t)
+    t.pack_rows()
+    assert t.rowpack is not None and t.rowpack.n == n
+    b = NaiveBayes(schema).fit(t)
+    assert torch.equal(a.counts, b.counts) and torch.equal(a.class_n, b.class_n)
+
+
+@gpu
+@pytest.mark.parametrize("n", [1, 7, 8, 63, 4097, 1 << 20])
+@pytest.mark.parametrize("C", [1, 2])
+def test_packed_histogram_gpu_matches_columns(n, C):
+    bins = [4, 3, 3, 3, 5] if C == 2 else [7, 1, 2, 3, 4, 5]
+    codes, labels = _random_codes(n, bins, C, seed=n)
+    codes, labels = codes.cuda(), labels.cuda()
+    lab = labels if C == 2 else None
+    ref = H.class_histogram(codes, n, bins, lab, C, count_labels=True)
+    rp = H.pack_rows(codes, n, bins, lab, C)
+    assert rp is not None
+    got = H.class_histogram_packed(rp, count_labels=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ref.cpu(), got.cpu())
+
+
+@gpu
+def test_packed_histogram_gpu_long_uniform_run():
+    """2^28 identical records: every lane's byte counters go through many flush windows, so a
+    counter overflow shows up as a wrong count."""
+    n = 1 << 28
+    bins = [4, 3, 3, 3, 5]
+    word = 2 | (1 << 3) | (0 << 5) | (2 << 7) | (4 << 9) | (2 << 12)      # class 1 = one-hot bit 13
+    words = torch.full((n,), word, dtype=torch.int16, device="cuda")
+    rp = H.RowPacked(words, n, bins, *H.rowpack_layout(bins, 2), 2)
+    got = H.class_histogram_packed(rp, count_labels=True).cpu()
+    exp = torch.zeros_like(got)
+    for o, v in zip([0, 4, 7, 10, 13], [2, 1, 0, 2, 4]):
+        exp[1, o + v] = n
+    exp[1, -1] = n
+    assert torch.equal(got, exp)
+
+
+@gpu
+def test_bayes_packed_equals_columns_gpu():
+    schema = FeatureSchema.from_json(CHURN_SCHEMA)
+    n = (1 << 22) + 5
+    codes, labels = churn_device(n, seed=11, device="cuda")
+    t = Table(schema, n, codes, schema.feature_fields, torch.zeros((0, codes.shape[1]), device="cuda"), [],
+              labels, schema.find_class_attr_field())
+    a = NaiveBayes(schema).fit(t)
+    t.pack_rows()
+    assert t.rowpack is not None
+    b = NaiveBayes(schema).fit(t)
+    assert torch.equal(a.counts.cpu(), b.counts.cpu()) and torch.equal(a.class_n.cpu(), b.class_n.cpu())
