@@ -368,34 +368,46 @@ void launch_split(const uint8_t* codes, long long ld, long long n, const uint8_t
 
 // ---------------------------------------------------------------------------------------------
 // K2, row-packed layout: every record is ONE 16-bit word holding all of its categorical codes
-// and its class (field k at bit sh[k], width w[k] <= 3 bits, the all-ones value of a field being
-// its missing code, never a valid bin; for C = 2 the class is two one-hot bits at lsh, both clear
-// for an unknown class).  For low-cardinality schemas such as R/churn.json (5 features of 3-5
-// values + a binary class = 14 bits) this is 2 bytes per record instead of F + 1 = 6 bytes of
-// byte-per-code columns.
+// and its class (field k at bit sh[k], width w[k] <= 3 bits; a field that has missing values
+// keeps its all-ones value as the missing code, never a valid bin; for C = 2 the class is two
+// one-hot bits at lsh, both clear for an unknown class).  For low-cardinality schemas such as
+// R/churn.json (5 features of 3-5 values + a binary class = 13 bits) this is 2 bytes per record
+// instead of F + 1 = 6 bytes of byte-per-code columns.
 //
-// At 2 B/record the pass is ALU-bound unless a record costs < ~30 VALU ops, so the counting uses
-// only full-rate 32-bit ops (a 64-bit variable shift per (record, feature, class) — the byte-
-// counter-in-u64 scheme — measured 1.48 ms per 2^30 records, slower than the 6 B/record columns):
-// per lane and (class, feature) one u32 of eight 4-bit counters indexed by the code; a record
-// costs, per feature, one v_bfe_u32 + one shift for the nibble offset and one v_lshl_add_u32 per
-// class (acc += is_class << 4*code), the class masks being two more bfe's.
-// After every tile (8 records per lane, <= 8 per nibble) the nibbles are spread into two u32 of
-// byte counters (even / odd codes); every 31 tiles (<= 248 per byte) those are widened into
-// 16-bit lane fields; after 256 widenings (<= 63488) or at the end the fields are summed across
-// the wave into the wave's private LDS slice.
+// At 2 B/record the pass is ALU-bound unless a record costs < ~15 VALU ops (one wave64 VALU op
+// per ~4 cycles per SIMD measured), so the counting uses only full-rate 32-bit ops (the byte-
+// counter-in-u64 scheme, one 64-bit variable shift per (record, feature, class), measured
+// 1.48 ms per 2^30 records — slower than the 6 B/record columns):
+//  * per lane, one u32 of eight 4-bit counters per accumulator, incremented with ONE
+//    v_lshl_add_u32 (acc += valid << 4*slot);
+//  * the NM leading features (C = 2, width <= 2: at most 4 codes) merge class and code into one
+//    slot 4c + code, so they cost one increment per record instead of one per class; the other
+//    features keep one accumulator per class (acc_c += is_class_c << 4*code);
+//  * after every tile (8 records per lane, <= 8 per nibble) the nibbles are spread into two u32
+//    of byte counters (even / odd slots); every 31 tiles (<= 248 per byte) those are widened into
+//    16-bit lane fields; after 256 widenings (<= 63488) or at the end the fields are summed
+//    across the wave into the wave's private LDS slice [feature][class][code];
+//  * the next tile's 16-byte load is issued before the current tile is counted.
 // ---------------------------------------------------------------------------------------------
 struct RowPackSpec {
-  int sh[8];  // bit offset of feature k
+  int sh[8];  // bit offset of feature k (kernel order: class-merged features first)
   int w[8];   // bit width of feature k (1..3)
   int lsh;    // first of the C one-hot class bits (C >= 2)
 };
 
-template <int NF, int C>
+// acc += x << s as ONE v_lshl_add_u32: left to itself the compiler turns the chain of 8 record
+// increments into v_lshlrev_b32 + v_add3_u32 trees (1.5 ops per increment instead of 1)
+__device__ __forceinline__ void lshl_add_u32(unsigned& acc, unsigned x, unsigned s) {
+  asm("v_lshl_add_u32 %0, %1, %2, %0" : "+v"(acc) : "v"(x), "v"(s));
+}
+
+template <int NF, int C, int NM>
 __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __restrict__ words, long long n,
                                                           RowPackSpec spec, const int* __restrict__ bins,
                                                           const int* __restrict__ offs, int total_bins,
                                                           int count_labels, unsigned long long* __restrict__ out) {
+  static_assert(NM == 0 || C == 2, "class-merged slots need C == 2");
+  constexpr int NA = NM + C * (NF - NM);  // accumulators per lane; separate (k, c) -> NM + (k - NM) * C + c
   constexpr int TAB = NF * C * 8;
   constexpr int WPB = HB / AV_WAVE;
   constexpr int FLUSH = 31;  // 31 tiles x 8 records = 248 increments per byte counter at most
@@ -405,58 +417,57 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
   unsigned int* my_tab = s_tab + av::wave_id() * TAB;
   const uint4* w4 = reinterpret_cast<const uint4*>(words);
 
-  unsigned a4[C][NF], be[C][NF], bo[C][NF], w16[C][NF][4];
+  unsigned a4[NA], be[NA], bo[NA], w16[NA][4];
 #pragma unroll
-  for (int c = 0; c < C; ++c)
+  for (int j = 0; j < NA; ++j) {
+    a4[j] = 0;
+    be[j] = 0;
+    bo[j] = 0;
 #pragma unroll
-    for (int k = 0; k < NF; ++k) {
-      a4[c][k] = 0;
-      be[c][k] = 0;
-      bo[c][k] = 0;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) w16[c][k][m] = 0;
-    }
+    for (int m = 0; m < 4; ++m) w16[j][m] = 0;
+  }
   const unsigned N4 = 0x0F0F0F0Fu, B8 = 0x00FF00FFu;
-  auto spread = [&]() __attribute__((always_inline)) {  // nibbles -> bytes: be byte j = code 2j, bo byte j = code 2j + 1
+  auto spread = [&]() __attribute__((always_inline)) {  // nibbles -> bytes: be byte i = slot 2i, bo = 2i + 1
 #pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int k = 0; k < NF; ++k) {
-        be[c][k] += a4[c][k] & N4;
-        bo[c][k] += (a4[c][k] >> 4) & N4;
-        a4[c][k] = 0;
-      }
+    for (int j = 0; j < NA; ++j) {
+      be[j] += a4[j] & N4;
+      bo[j] += (a4[j] >> 4) & N4;
+      a4[j] = 0;
+    }
   };
-  auto widen = [&]() __attribute__((always_inline)) {  // bytes -> 16-bit fields: w16[0] codes {0, 4}, [1] {2, 6}, [2] {1, 5}, [3] {3, 7}
+  auto widen = [&]() __attribute__((always_inline)) {  // -> 16-bit: [0] slots {0,4}, [1] {2,6}, [2] {1,5}, [3] {3,7}
 #pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int k = 0; k < NF; ++k) {
-        w16[c][k][0] += be[c][k] & B8;
-        w16[c][k][1] += (be[c][k] >> 8) & B8;
-        w16[c][k][2] += bo[c][k] & B8;
-        w16[c][k][3] += (bo[c][k] >> 8) & B8;
-        be[c][k] = 0;
-        bo[c][k] = 0;
-      }
+    for (int j = 0; j < NA; ++j) {
+      w16[j][0] += be[j] & B8;
+      w16[j][1] += (be[j] >> 8) & B8;
+      w16[j][2] += bo[j] & B8;
+      w16[j][3] += (bo[j] >> 8) & B8;
+      be[j] = 0;
+      bo[j] = 0;
+    }
   };
-  auto reduce_to_lds = [&]() __attribute__((always_inline)) {  // lane l < 8 owns code l
+  auto reduce_to_lds = [&]() __attribute__((always_inline)) {  // lane l < 8 owns slot l
     const int l = av::lane_id();
     const int r = l & 3, mi = ((r & 1) << 1) | (r >> 1), half = (l >> 2) & 1;
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+    for (int j = 0; j < NA; ++j) {
+      unsigned sel = 0;
 #pragma unroll
-      for (int k = 0; k < NF; ++k) {
-        unsigned sel = 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const unsigned lo = av::wave_sum(w16[c][k][m] & 0xFFFFu);
-          const unsigned hi = av::wave_sum(w16[c][k][m] >> 16);
-          if (m == mi) sel = half ? hi : lo;
-          w16[c][k][m] = 0;
-        }
-        if (l < 8) my_tab[(k * C + c) * 8 + l] += sel;
+      for (int m = 0; m < 4; ++m) {
+        const unsigned lo = av::wave_sum(w16[j][m] & 0xFFFFu);
+        const unsigned hi = av::wave_sum(w16[j][m] >> 16);
+        if (m == mi) sel = half ? hi : lo;
+        w16[j][m] = 0;
       }
+      int dst;
+      if (j < NM) {
+        dst = (j * C + (l >> 2)) * 8 + (l & 3);  // slot 4c + code
+      } else {
+        const int k = NM + (j - NM) / C, c = (j - NM) % C;
+        dst = (k * C + c) * 8 + l;
+      }
+      if (l < 8) my_tab[dst] += sel;
+    }
   };
 
   const long long nvec = n >> 3;  // 8 records per 16-byte load
@@ -464,8 +475,6 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
   const long long gw = (long long)blockIdx.x * WPB + av::wave_id();
   const long long nw = (long long)gridDim.x * WPB;
   int since_flush = 0, flushes = 0;
-  // one tile of loads always in flight ahead of the tile being counted (the counting is ~30 VALU
-  // ops per record, so a wave that only loads after counting leaves HBM idle)
   long long v = gw * AV_WAVE + av::lane_id();
   uint4 qn = (gw < ntiles && v < nvec) ? w4[v] : make_uint4(0u, 0u, 0u, 0u);
   for (long long t = gw; t < ntiles; t += nw) {
@@ -483,11 +492,20 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
 #pragma unroll
         for (int c = 0; c < C; ++c)
           x[c] = C == 1 ? 1u : __builtin_amdgcn_ubfe(d, (unsigned)(spec.lsh + o + c), 1u);
+        unsigned valid = 0, c16 = 0;
+        if (NM > 0) {
+          valid = x[0] | x[C - 1];  // known class
+          c16 = x[C - 1] << 4;      // class 1: slot + 4 = nibble shift + 16
+        }
 #pragma unroll
         for (int k = 0; k < NF; ++k) {
-          const unsigned s4 = __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]) << 2;
+          const unsigned code = __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]);
+          if (k < NM) {
+            lshl_add_u32(a4[k], valid, (code << 2) | c16);
+          } else {
 #pragma unroll
-          for (int c = 0; c < C; ++c) a4[c][k] += x[c] << s4;
+            for (int c = 0; c < C; ++c) lshl_add_u32(a4[NM + (k - NM) * C + c], x[c], code << 2);
+          }
         }
       }
     }
@@ -527,8 +545,8 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
   __syncthreads();
   for (int i = threadIdx.x; i < TAB; i += HB) {
     const int k = i / (C * 8), c = (i / 8) % C, b = i % 8;
-    const unsigned v = s_tab[i];
-    if (v && b < bins[k]) atomicAdd(&out[(long long)c * total_bins + offs[k] + b], (unsigned long long)v);
+    const unsigned cnt = s_tab[i];
+    if (cnt && b < bins[k]) atomicAdd(&out[(long long)c * total_bins + offs[k] + b], (unsigned long long)cnt);
   }
   if (count_labels && threadIdx.x < C) {  // every record of a class has exactly one feature-0 code
     unsigned long long sum = 0;
@@ -538,13 +556,40 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
   }
 }
 
-template <int NF, int C>
-void launch_rowpack(const uint16_t* words, long long n, const RowPackSpec& spec, const int* bins, const int* offs,
-                    int total_bins, int count_labels, unsigned long long* out, hipStream_t stream) {
-  static const int res = av::resident_blocks((const void*)hist_rowpack_kernel<NF, C>, HB, 0);
-  const int grid = std::min(av::stream_grid(std::max(1LL, n >> 3), HB, 4, 4096), res);
-  hist_rowpack_kernel<NF, C><<<grid, HB, 0, stream>>>(words, n, spec, bins, offs, total_bins, count_labels, out);
+struct RowPackLaunch {
+  const uint16_t* words;
+  long long n;
+  RowPackSpec spec;
+  const int* bins;
+  const int* offs;
+  int total_bins, count_labels;
+  unsigned long long* out;
+  hipStream_t stream;
+};
+
+template <int NF, int C, int NM>
+void launch_rowpack(const RowPackLaunch& a) {
+  static const int res = av::resident_blocks((const void*)hist_rowpack_kernel<NF, C, NM>, HB, 0);
+  const int grid = std::min(av::stream_grid(std::max(1LL, a.n >> 3), HB, 4, 4096), res);
+  hist_rowpack_kernel<NF, C, NM><<<grid, HB, 0, a.stream>>>(a.words, a.n, a.spec, a.bins, a.offs, a.total_bins,
+                                                            a.count_labels, a.out);
   AV_HIP_CHECK(hipGetLastError());
+}
+
+template <int NF, int NM>
+void launch_rowpack_c2(int nm, const RowPackLaunch& a) {
+  if constexpr (NM > NF) {
+    throw std::runtime_error("row-packed histogram: bad merged-feature count");
+  } else {
+    if (nm == NM) launch_rowpack<NF, 2, NM>(a);
+    else launch_rowpack_c2<NF, NM + 1>(nm, a);
+  }
+}
+
+template <int NF>
+void launch_rowpack_nf(int n_classes, int nm, const RowPackLaunch& a) {
+  if (n_classes == 1) launch_rowpack<NF, 1, 0>(a);
+  else launch_rowpack_c2<NF, 0>(nm, a);
 }
 
 // General path: LDS-privatised table with R replicas (one per wave when it fits) so that lanes of
@@ -854,20 +899,20 @@ void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_
   if (n_classes > 1 && label_width != n_classes)
     throw std::runtime_error("row-packed histogram: the class is C one-hot bits");
   spec.lsh = n_classes > 1 ? label_shift : 0;
-#define AV_RP(NF)                                                                                          \
-  (n_classes == 1 ? launch_rowpack<NF, 1>(words, n, spec, d_bins, d_offs, total_bins, count_labels, out, stream) \
-                  : launch_rowpack<NF, 2>(words, n, spec, d_bins, d_offs, total_bins, count_labels, out, stream))
+  int nm = 0;  // leading features whose (class, code) share one slot (kernel order puts them first)
+  if (n_classes == 2)
+    while (nm < nfeat && h_width[nm] <= 2) ++nm;
+  const RowPackLaunch a{words, n, spec, d_bins, d_offs, total_bins, count_labels, out, stream};
   switch (nfeat) {
-    case 1: AV_RP(1); break;
-    case 2: AV_RP(2); break;
-    case 3: AV_RP(3); break;
-    case 4: AV_RP(4); break;
-    case 5: AV_RP(5); break;
-    case 6: AV_RP(6); break;
-    case 7: AV_RP(7); break;
-    default: AV_RP(8); break;
+    case 1: launch_rowpack_nf<1>(n_classes, nm, a); break;
+    case 2: launch_rowpack_nf<2>(n_classes, nm, a); break;
+    case 3: launch_rowpack_nf<3>(n_classes, nm, a); break;
+    case 4: launch_rowpack_nf<4>(n_classes, nm, a); break;
+    case 5: launch_rowpack_nf<5>(n_classes, nm, a); break;
+    case 6: launch_rowpack_nf<6>(n_classes, nm, a); break;
+    case 7: launch_rowpack_nf<7>(n_classes, nm, a); break;
+    default: launch_rowpack_nf<8>(n_classes, nm, a); break;
   }
-#undef AV_RP
 }
 
 }  // namespace avk

@@ -88,15 +88,20 @@ class RowPacked:
     n_classes: int
 
 
-def rowpack_layout(bins: Sequence[int], n_classes: int):
+def rowpack_layout(bins: Sequence[int], n_classes: int, missing: Sequence[bool] | None = None):
     """(shifts, widths, label_shift, label_width) of the 16-bit record, or None when the schema
-    does not fit: at most 8 features of at most 7 values (bit_length(b) bits, so the all-ones
-    value >= b is free for 'missing') and 1 or 2 classes (C = 2: two one-hot class bits)."""
+    does not fit: at most 8 features of at most 3 bits and 1 or 2 classes (C = 2: two one-hot
+    class bits).  A feature with missing values takes bit_length(b) bits so its all-ones value
+    (>= b) is free for 'missing'; one without (``missing[k]`` False) only bit_length(b - 1)."""
     bins = [int(b) for b in bins]
     C = int(n_classes)
-    if not bins or len(bins) > 8 or C < 1 or C > 2 or min(bins) < 1 or max(bins) > 7:
+    if missing is None:
+        missing = [True] * len(bins)
+    if not bins or len(bins) > 8 or C < 1 or C > 2 or min(bins) < 1:
         return None
-    widths = [b.bit_length() for b in bins]
+    widths = [max(1, (b if m else b - 1).bit_length()) for b, m in zip(bins, missing)]
+    if max(widths) > 3:
+        return None
     shifts, s = [], 0
     for w in widths:
         shifts.append(s)
@@ -117,8 +122,12 @@ def pack_rows(codes: torch.Tensor, n: int, bins: Sequence[int], labels: torch.Te
     C = int(n_classes) if labels is not None else 1
     if labels is not None and C == 1:
         return None                      # a 1-class label column still filters rows: keep columns
-    lay = rowpack_layout(bins, C)
-    if lay is None or codes.shape[0] != len(bins):
+    if codes.shape[0] != len(bins):
+        return None
+    # data-adaptive widths: a feature without missing codes needs no all-ones 'missing' value
+    missing = [bool((codes[k, :n] >= b).any()) for k, b in enumerate(bins)] if n else [False] * len(bins)
+    lay = rowpack_layout(bins, C, missing)
+    if lay is None:
         return None
     shifts, widths, lsh, lw = lay
     w = torch.zeros(max(8, (n + 7) // 8 * 8), dtype=torch.int32, device=codes.device)
@@ -169,10 +178,15 @@ def class_histogram_packed(rp: RowPacked, out: torch.Tensor | None = None,
         offs = [0] * len(rp.bins)
         for f in range(1, len(rp.bins)):
             offs[f] = offs[f - 1] + rp.bins[f - 1]
+        # kernel order: features of <= 2 bits first (for C = 2 they share one counter per record
+        # across both classes); output columns stay in schema order through offs
+        order = sorted(range(len(rp.bins)), key=lambda k: (C == 2 and rp.widths[k] > 2, k))
         dev = rp.words.device
-        _native.C().class_histogram_rowpacked(rp.words, int(rp.n), rp.shifts, rp.widths, rp.label_shift,
-                                              rp.label_width, _dev_i32(rp.bins, dev),
-                                              _dev_i32(offs, dev), tb, C, out, bool(count_labels))
+        _native.C().class_histogram_rowpacked(rp.words, int(rp.n), [rp.shifts[k] for k in order],
+                                              [rp.widths[k] for k in order], rp.label_shift, rp.label_width,
+                                              _dev_i32([rp.bins[k] for k in order], dev),
+                                              _dev_i32([offs[k] for k in order], dev), tb, C, out,
+                                              bool(count_labels))
         return out
     codes, labels = unpack_rows(rp)
     return class_histogram(codes, rp.n, rp.bins, labels, C, out=out, count_labels=count_labels)

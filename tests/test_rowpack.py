@@ -37,6 +37,9 @@ def test_layout_rules():
     assert H.rowpack_layout([7] * 5, 2) is None          # 15 + 2 bits > 16
     assert H.rowpack_layout([3] * 9, 1) is None          # more than 8 fields
     assert H.rowpack_layout([3, 3], 3) is None           # more than 2 classes
+    # data-adaptive: no missing values -> bit_length(b - 1) bits
+    assert H.rowpack_layout([4, 3, 3, 3, 5], 2, [False] * 5) == ([0, 2, 4, 6, 8], [2, 2, 2, 2, 3], 11, 2)
+    assert H.rowpack_layout([8, 1], 1, [False, False]) == ([0, 3], [3, 1], 4, 0)
 
 
 def test_pack_unpack_lossless():
@@ -77,9 +80,12 @@ def test_table_pack_rows_and_bayes_cpu():
 @gpu
 @pytest.mark.parametrize("n", [1, 7, 8, 63, 4097, 1 << 20])
 @pytest.mark.parametrize("C", [1, 2])
-def test_packed_histogram_gpu_matches_columns(n, C):
+@pytest.mark.parametrize("missing", [0.05, 0.0])
+def test_packed_histogram_gpu_matches_columns(n, C, missing):
+    """With missing codes churn's fields are 3/2/2/2/3 bits (3 class-merged), without 2/2/2/2/3
+    (4 merged); C = 1 has no merging."""
     bins = [4, 3, 3, 3, 5] if C == 2 else [7, 1, 2, 3, 4, 5]
-    codes, labels = _random_codes(n, bins, C, seed=n)
+    codes, labels = _random_codes(n, bins, C, seed=n, missing=missing)
     codes, labels = codes.cuda(), labels.cuda()
     lab = labels if C == 2 else None
     ref = H.class_histogram(codes, n, bins, lab, C, count_labels=True)
@@ -99,6 +105,7 @@ def test_packed_histogram_gpu_long_uniform_run():
     word = 2 | (1 << 3) | (0 << 5) | (2 << 7) | (4 << 9) | (2 << 12)      # class 1 = one-hot bit 13
     words = torch.full((n,), word, dtype=torch.int16, device="cuda")
     rp = H.RowPacked(words, n, bins, *H.rowpack_layout(bins, 2), 2)
+    assert rp.widths == [3, 2, 2, 2, 3]
     got = H.class_histogram_packed(rp, count_labels=True).cpu()
     exp = torch.zeros_like(got)
     for o, v in zip([0, 4, 7, 10, 13], [2, 1, 0, 2, 4]):
