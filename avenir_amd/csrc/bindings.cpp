@@ -474,6 +474,68 @@ py::tuple viterbi(const at::Tensor& obs, const at::Tensor& logA, const at::Tenso
   return py::make_tuple(path, score);
 }
 
+at::Tensor viterbi_chunks(const at::Tensor& obs, const at::Tensor& logA, const at::Tensor& logB,
+                          const at::Tensor& logpi, int64_t n, int64_t obs_div, const c10::optional<at::Tensor>& bp) {
+  CHECK_DEV(obs);
+  CHECK_DTYPE(obs, at::kShort);
+  TORCH_CHECK(obs.dim() == 2, "obs must be [rows, T]");
+  for (const at::Tensor* t : {&logA, &logB, &logpi}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  const int64_t S = logA.size(0), O = logB.size(1), T = obs.size(1);
+  TORCH_CHECK(logA.dim() == 2 && logA.size(1) == S, "logA must be [S, S]");
+  TORCH_CHECK(logB.dim() == 2 && logB.size(0) == S, "logB must be [S, O]");
+  TORCH_CHECK(logpi.dim() == 2 && logpi.size(1) == S && logpi.size(0) >= 1, "logpi must be [rows, S]");
+  TORCH_CHECK(S >= 1 && S <= 192, "1 <= S <= 192");
+  TORCH_CHECK(n >= 0 && obs_div >= 1 && (n == 0 || (n - 1) / obs_div < obs.size(0)),
+              "obs has fewer rows than n / obs_div");
+  auto delta = at::empty({n, S}, logA.options());
+  short* bpp = nullptr;
+  if (bp.has_value() && bp->defined()) {
+    CHECK_DEV((*bp));
+    CHECK_DTYPE((*bp), at::kShort);
+    TORCH_CHECK(bp->numel() == n * T * S, "bp must be [n, T, S]");
+    bpp = bp->data_ptr<int16_t>();
+  }
+  DevGuard g(obs.device());
+  avk::viterbi_chunks(obs.data_ptr<int16_t>(), n, obs_div, (int)T, (int)S, (int)O, logA.data_ptr<float>(),
+                      logB.data_ptr<float>(), logpi.data_ptr<float>(), logpi.size(0), bpp, delta.data_ptr<float>(),
+                      cur_stream(obs));
+  return delta;
+}
+
+void viterbi_backtrack(const at::Tensor& bp, const at::Tensor& lens, const at::Tensor& ends, int64_t per_chunk,
+                       const c10::optional<at::Tensor>& first, const c10::optional<at::Tensor>& path) {
+  CHECK_DEV(bp);
+  CHECK_DTYPE(bp, at::kShort);
+  TORCH_CHECK(bp.dim() == 3, "bp must be [P, T, S]");
+  const int64_t P = bp.size(0), T = bp.size(1), S = bp.size(2);
+  CHECK_DEV(lens);
+  CHECK_DTYPE(lens, at::kInt);
+  CHECK_DEV(ends);
+  CHECK_DTYPE(ends, at::kInt);
+  TORCH_CHECK(lens.numel() == P, "lens must be [P]");
+  TORCH_CHECK(per_chunk >= 1 && ends.numel() == P * per_chunk, "ends must be [P * per_chunk]");
+  int* fp = nullptr;
+  short* pp = nullptr;
+  if (first.has_value() && first->defined()) {
+    CHECK_DEV((*first));
+    CHECK_DTYPE((*first), at::kInt);
+    TORCH_CHECK(first->numel() == P * per_chunk, "first must be [P * per_chunk]");
+    fp = first->data_ptr<int>();
+  }
+  if (path.has_value() && path->defined()) {
+    CHECK_DEV((*path));
+    CHECK_DTYPE((*path), at::kShort);
+    TORCH_CHECK(per_chunk == 1 && path->numel() == P * T, "path needs one track per chunk and [P, T]");
+    pp = path->data_ptr<int16_t>();
+  }
+  DevGuard g(bp.device());
+  avk::viterbi_backtrack(bp.data_ptr<int16_t>(), lens.data_ptr<int>(), ends.data_ptr<int>(), P * per_chunk,
+                         (int)per_chunk, (int)T, (int)S, fp, pp, cur_stream(bp));
+}
+
 at::Tensor markov_logodds(const at::Tensor& states, const at::Tensor& lr) {
   CHECK_DEV(states);
   CHECK_DTYPE(states, at::kShort);
@@ -1107,6 +1169,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("knn_topk", &knn_topk);
   m.def("cluster_accumulate", &cluster_accumulate);
   m.def("viterbi", &viterbi);
+  m.def("viterbi_chunks", &viterbi_chunks);
+  m.def("viterbi_backtrack", &viterbi_backtrack);
   m.def("markov_logodds", &markov_logodds);
   m.def("itemset_support", &itemset_support);
   m.def("build_bitsets", &build_bitsets);

@@ -61,6 +61,13 @@ void cluster_accumulate(const float* X, long long N, int D, const int* assign, i
 // ---- sequence.hip (K14/K15) ----------------------------------------------------------------
 void viterbi(const short* obs, long long n, int T, int S, int O, const float* logA, const float* logB,
              const float* logpi, int mode, short* bp, short* path, float* score, hipStream_t stream);
+// chunked Viterbi pieces: n runs (run k reads observation row k / obs_div, starts from logpi row
+// k % pi_mod), optional back-pointers [n, T, S], final delta vectors [n, S]
+void viterbi_chunks(const short* obs, long long n, long long obs_div, int T, int S, int O, const float* logA,
+                    const float* logB, const float* logpi, long long pi_mod, short* bp, float* delta_out,
+                    hipStream_t stream);
+void viterbi_backtrack(const short* bp, const int* lens, const int* ends, long long ntracks, int per_chunk, int T,
+                       int S, int* first, short* path, hipStream_t stream);
 void markov_logodds(const short* states, long long n, int L, const float* lr, int S, float* out,
                     hipStream_t stream);
 

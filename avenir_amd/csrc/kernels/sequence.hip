@@ -17,20 +17,34 @@ namespace {
 
 constexpr int VT = 256;  // 4 waves -> 4 sequences per block
 
+struct ViterbiArgs {
+  const short* obs;    // [rows, T] observations, a negative value ends the sequence
+  long long n;         // sequences, one wavefront each
+  long long obs_div;   // sequence s reads observation row s / obs_div
+  long long pi_mod;    // sequence s starts from logpi row s % pi_mod
+  int T, S, O, mode;   // mode 0 Viterbi (max-plus), 1 forward (log-sum-exp)
+  const float* logA;   // [S, S]
+  const float* logB;   // [S, O]
+  const float* logpi;  // [pi_mod, S]
+  short* bp;           // [n, T, S] back-pointers, or null
+  short* path;         // [n, T] decoded path (needs bp), or null
+  float* score;        // [n], or null
+  float* delta_out;    // [n, S] final delta vector, or null
+};
+
 template <int QS>
-__global__ __launch_bounds__(VT) void viterbi_kernel(const short* __restrict__ obs, long long n, int T, int S,
-                                                     int O, const float* __restrict__ logA,
-                                                     const float* __restrict__ logB,
-                                                     const float* __restrict__ logpi, int mode,
-                                                     short* __restrict__ bp, short* __restrict__ path,
-                                                     float* __restrict__ score) {
+__global__ __launch_bounds__(VT) void viterbi_kernel(const ViterbiArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sA[];  // [S][S]
-  for (int i = threadIdx.x; i < S * S; i += VT) sA[i] = logA[i];
+  const int S = a.S, T = a.T, O = a.O, mode = a.mode;
+  for (int i = threadIdx.x; i < S * S; i += VT) sA[i] = a.logA[i];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const long long seq = (long long)blockIdx.x * (VT / 64) + (threadIdx.x >> 6);
-  if (seq >= n) return;  // wave-uniform exit (after the only block barrier)
-  const short* ob = obs + seq * T;
+  if (seq >= a.n) return;  // wave-uniform exit (after the only block barrier)
+  const short* ob = a.obs + (seq / a.obs_div) * T;
+  const float* logpi = a.logpi + (seq % a.pi_mod) * S;
+  const float* logB = a.logB;
+  short* bp = a.bp;
   float delta[QS];
 #pragma unroll
   for (int q = 0; q < QS; ++q) {
@@ -90,10 +104,17 @@ __global__ __launch_bounds__(VT) void viterbi_kernel(const short* __restrict__ o
       const int j = lane + 64 * q;
       if (j < S) {
         delta[q] = nd[q] + logB[(long long)j * O + ot];
-        if (mode == 0) bp[(seq * T + t) * S + j] = arg[q];
+        if (bp) bp[(seq * T + t) * S + j] = arg[q];
       }
     }
     ++len;
+  }
+  if (a.delta_out) {
+#pragma unroll
+    for (int q = 0; q < QS; ++q) {
+      const int j = lane + 64 * q;
+      if (j < S) a.delta_out[seq * S + j] = delta[q];
+    }
   }
   // final: best state (Viterbi) or log-sum-exp (forward)
   float best = -INFINITY;
@@ -106,15 +127,17 @@ __global__ __launch_bounds__(VT) void viterbi_kernel(const short* __restrict__ o
   if (mode == 0) {
     av::wave_argmax(best, barg);
     if (lane == 0) {
-      score[seq] = best;
-      short* pth = path + seq * T;
-      for (int t = len; t < T; ++t) pth[t] = -1;
-      if (len > 0) {
-        int s = barg;
-        pth[len - 1] = (short)s;
-        for (int t = len - 1; t > 0; --t) {
-          s = bp[(seq * T + t) * S + s];
-          pth[t - 1] = (short)s;
+      if (a.score) a.score[seq] = best;
+      if (a.path) {
+        short* pth = a.path + seq * T;
+        for (int t = len; t < T; ++t) pth[t] = -1;
+        if (len > 0) {
+          int s = barg;
+          pth[len - 1] = (short)s;
+          for (int t = len - 1; t > 0; --t) {
+            s = bp[(seq * T + t) * S + s];
+            pth[t - 1] = (short)s;
+          }
         }
       }
     }
@@ -128,8 +151,53 @@ __global__ __launch_bounds__(VT) void viterbi_kernel(const short* __restrict__ o
       if (j < S && delta[q] > -INFINITY) s += __expf(delta[q] - m);
     }
     s = av::wave_sum(s);
-    if (lane == 0) score[seq] = (len > 0 && m > -INFINITY) ? m + __logf(s) : -INFINITY;
+    if (lane == 0 && a.score) a.score[seq] = (len > 0 && m > -INFINITY) ? m + __logf(s) : -INFINITY;
   }
+}
+
+// Chunked-Viterbi back-tracking (sequence_ops.viterbi_long): thread k follows the back-pointers
+// of chunk k / per_chunk from state ends[k] at the chunk's last position down to position 0,
+// writing the state reached there (first[k]: the chunk's end -> start map) and / or the path.
+__global__ __launch_bounds__(256) void viterbi_backtrack_kernel(const short* __restrict__ bp,
+                                                                const int* __restrict__ lens,
+                                                                const int* __restrict__ ends, long long ntracks,
+                                                                int per_chunk, int T, int S, int* __restrict__ first,
+                                                                short* __restrict__ path) {
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k >= ntracks) return;
+  const long long c = k / per_chunk;
+  const int len = min(max(lens[c], 0), T);
+  int s = min(max(ends[k], 0), S - 1);
+  const short* b = bp + c * (long long)T * S;
+  short* p = path ? path + c * (long long)T : nullptr;
+  if (p)
+    for (int t = len; t < T; ++t) p[t] = -1;
+  if (len == 0) {
+    if (first) first[k] = -1;
+    return;
+  }
+  if (p) p[len - 1] = (short)s;
+  for (int t = len - 1; t > 0; --t) {
+    s = b[(long long)t * S + s];
+    if (p) p[t - 1] = (short)s;
+  }
+  if (first) first[k] = s;
+}
+
+void launch_viterbi(const ViterbiArgs& a, hipStream_t stream) {
+  if (a.n <= 0 || a.T <= 0) return;
+  if ((size_t)a.S * a.S * sizeof(float) > 160 * 1024) throw std::runtime_error("viterbi: S too large for LDS");
+  const unsigned grid = (unsigned)((a.n + 3) / 4);
+  const size_t lds = (size_t)a.S * a.S * sizeof(float);
+  if (a.S <= 64)
+    viterbi_kernel<1><<<grid, VT, lds, stream>>>(a);
+  else if (a.S <= 128)
+    viterbi_kernel<2><<<grid, VT, lds, stream>>>(a);
+  else if (a.S <= 192)
+    viterbi_kernel<3><<<grid, VT, lds, stream>>>(a);
+  else
+    throw std::runtime_error("viterbi: more than 192 states not supported");
+  AV_HIP_CHECK(hipGetLastError());
 }
 
 __global__ __launch_bounds__(256) void markov_logodds_kernel(const short* __restrict__ st, long long n, int L,
@@ -159,18 +227,23 @@ namespace avk {
 
 void viterbi(const short* obs, long long n, int T, int S, int O, const float* logA, const float* logB,
              const float* logpi, int mode, short* bp, short* path, float* score, hipStream_t stream) {
-  if (n <= 0 || T <= 0) return;
-  if ((size_t)S * S * sizeof(float) > 160 * 1024) throw std::runtime_error("viterbi: S too large for LDS");
-  const unsigned grid = (unsigned)((n + 3) / 4);
-  const size_t lds = (size_t)S * S * sizeof(float);
-  if (S <= 64)
-    viterbi_kernel<1><<<grid, VT, lds, stream>>>(obs, n, T, S, O, logA, logB, logpi, mode, bp, path, score);
-  else if (S <= 128)
-    viterbi_kernel<2><<<grid, VT, lds, stream>>>(obs, n, T, S, O, logA, logB, logpi, mode, bp, path, score);
-  else if (S <= 192)
-    viterbi_kernel<3><<<grid, VT, lds, stream>>>(obs, n, T, S, O, logA, logB, logpi, mode, bp, path, score);
-  else
-    throw std::runtime_error("viterbi: more than 192 states not supported");
+  const ViterbiArgs a{obs, n, 1, 1, T, S, O, mode, logA, logB, logpi,
+                      mode == 0 ? bp : nullptr, mode == 0 ? path : nullptr, score, nullptr};
+  launch_viterbi(a, stream);
+}
+
+void viterbi_chunks(const short* obs, long long n, long long obs_div, int T, int S, int O, const float* logA,
+                    const float* logB, const float* logpi, long long pi_mod, short* bp, float* delta_out,
+                    hipStream_t stream) {
+  const ViterbiArgs a{obs, n, obs_div, pi_mod, T, S, O, 0, logA, logB, logpi, bp, nullptr, nullptr, delta_out};
+  launch_viterbi(a, stream);
+}
+
+void viterbi_backtrack(const short* bp, const int* lens, const int* ends, long long ntracks, int per_chunk, int T,
+                       int S, int* first, short* path, hipStream_t stream) {
+  if (ntracks <= 0 || T <= 0) return;
+  viterbi_backtrack_kernel<<<(unsigned)((ntracks + 255) / 256), 256, 0, stream>>>(bp, lens, ends, ntracks, per_chunk,
+                                                                                  T, S, first, path);
   AV_HIP_CHECK(hipGetLastError());
 }
 

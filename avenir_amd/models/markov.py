@@ -221,6 +221,12 @@ class ViterbiDecoder:
         lA, lB, lp = self.hmm.log_params(obs.device)
         return SO.viterbi(obs, lA, lB, lp)
 
+    def decode_long(self, obs: torch.Tensor, chunk: int = 1024, comm=None) -> tuple[torch.Tensor, float]:
+        """One long sequence (this rank's segment of it when distributed) by the chunked
+        max-plus scan of ``sequence_ops.viterbi_long``: (path, best log score)."""
+        lA, lB, lp = self.hmm.log_params(obs.device)
+        return SO.viterbi_long(obs, lA, lB, lp, chunk=chunk, comm=comm)
+
     def log_likelihood(self, obs: torch.Tensor) -> torch.Tensor:
         lA, lB, lp = self.hmm.log_params(obs.device)
         return SO.viterbi(obs, lA, lB, lp, forward=True)[1]
