@@ -679,6 +679,206 @@ def id_list(n: int, size: int, seed=0) -> list[str]:
     return list(ids(rng_of(seed), n, size))
 
 
+# ---------------------------------------------------------------------------------------------
+# resource/*.rb generators and transforms.  lib/util.rb is not part of the reference, so its
+# samplers follow their use in the scripts: NumericalFieldRange(lo..hi, w, ...) = a range picked
+# by weight, then a uniform integer inside it; CategoricalField(v, w, ...) = a value picked by
+# weight; IdGenerator.generate(k) = a random k-token id.
+# ---------------------------------------------------------------------------------------------
+def _ranges(rng, spec: Sequence[tuple[tuple[int, int], float]], n: int) -> np.ndarray:
+    lo = np.array([r[0] for r, _ in spec], dtype=np.int64)
+    hi = np.array([r[1] for r, _ in spec], dtype=np.int64)
+    w = np.array([w for _, w in spec], dtype=np.float64)
+    k = rng.choice(len(spec), size=n, p=w / w.sum())
+    return rng.integers(lo[k], hi[k] + 1)
+
+
+def hosp_readmit(n: int, seed=0) -> list[str]:
+    """Hospital readmission (resource/hosp_readmit.rb): id, age, weight, height, employment,
+    family status, diet, exercise, follow-up, smoking, alcohol, readmitted (Y/N) with probability
+    20 % plus the script's risk increments.  (The script's follow-up 'average' branch tests the
+    misspelt 'avearge' and never fires; kept.)"""
+    rng = rng_of(seed)
+    pid = ids(rng, n, 12)
+    age = _ranges(rng, [((10, 20), 2), ((21, 30), 3), ((31, 40), 6), ((41, 50), 10), ((51, 60), 14),
+                        ((61, 70), 19), ((71, 80), 25), ((81, 90), 21)], n)
+    wt = _ranges(rng, [((130, 140), 9), ((141, 150), 13), ((151, 160), 16), ((161, 170), 20), ((171, 180), 23),
+                       ((181, 190), 20), ((191, 200), 17), ((201, 211), 14), ((211, 220), 10), ((221, 230), 7),
+                       ((231, 240), 5), ((241, 250), 3)], n)
+    ht = _ranges(rng, [((50, 55), 9), ((56, 60), 12), ((61, 65), 16), ((66, 70), 23), ((71, 75), 14)], n)
+    p = 20 + np.select([age > 80, age > 70, age > 60], [10, 5, 3], 0)
+    p += np.where((wt > 200) & (ht < 70), 5, np.where((wt > 180) & (ht < 60), 3, 0))
+    emp = _cat(rng, ["employed", "unemployed", "retired"], [10, 1, 3], n)
+    emp = np.where((age > 68) & (rng.integers(0, 10, n) < 8), "retired", emp)
+    p += np.select([emp == "unemployed", emp == "retired"], [6, 4], 0)
+    fam = _cat(rng, ["alone", "with partner"], [10, 15], n)
+    p += np.where(fam == "alone", 9, 0)
+    diet = _cat(rng, ["average", "poor", "good"], [10, 4, 2], n)
+    diet = np.where((emp == "unemployed") & (rng.integers(0, 10, n) < 7), "poor", diet)
+    p += np.select([diet == "poor", diet == "average"], [4, 2], 0)
+    ex = _cat(rng, ["average", "low", "high"], [10, 12, 4], n)
+    p += np.select([ex == "low", ex == "average"], [3, 1], 0)
+    fu = _cat(rng, ["average", "low", "high"], [10, 14, 3], n)
+    p += np.where(fu == "low", 8, 0)
+    smoking = _cat(rng, ["non smoker", "smoker"], [10, 3], n)
+    p += np.where(smoking == "smoker", 6, 0)
+    alcohol = _cat(rng, ["average", "low", "high"], [10, 16, 4], n)
+    p += np.select([alcohol == "high", alcohol == "average"], [5, 2], 0)
+    readmit = np.where(rng.integers(0, 100, n) < p, "Y", "N")
+    return _rows(_s(pid), _s(age), _s(wt), _s(ht), _s(emp), _s(fam), _s(diet), _s(ex), _s(fu), _s(smoking),
+                 _s(alcohol), _s(readmit))
+
+
+def disease(n: int, seed=0) -> list[str]:
+    """Disease risk (resource/disease.rb): id, age 20-79, race, weight 120-239, diet, family
+    history, domestic life, status Yes/No with risk 15 % scaled by age band, race, diet, family
+    history and living alone (capped at 99 %)."""
+    rng = rng_of(seed)
+    pid = ids(rng, n, 12)
+    age = 20 + rng.integers(0, 60, n)
+    race = _cat(rng, ["EUA", "AFA", "LAA", "ASA"], [10, 3, 1, 1], n)
+    weight = 120 + rng.integers(0, 120, n)
+    diet = _cat(rng, ["LF", "REG", "HF"], [2, 8, 4], n)
+    fam = _cat(rng, ["NFH", "FH"], [5, 1], n)
+    dom = _cat(rng, ["S", "DP"], [2, 4], n)
+    pr = 15.0 * np.select([age < 40, age < 50, age < 60, age < 70], [1.0, 1.05, 1.15, 1.4], 1.5)
+    pr *= np.select([race == "AFA", race == "ASA", race == "LAA"], [1.2, 0.9, 0.95], 1.0)
+    pr *= np.where(diet == "HF", 1.15, 1.0) * np.where(fam == "FH", 1.2, 1.0) * np.where(dom == "S", 1.2, 1.0)
+    pr = np.minimum(pr, 99)
+    status = np.where(rng.integers(0, 100, n) < pr, "Yes", "No")
+    return _rows(_s(pid), _s(age), _s(race), _s(weight), _s(diet), _s(fam), _s(dom), _s(status))
+
+
+EVENT_STATES = ["SL", "SS", "SM", "ML", "MS", "MM", "LL", "LS", "LM"]
+
+
+def event_seq(n: int, seed=0) -> list[str]:
+    """Customer event sequences (resource/event_seq.rb): 5-24 events from 9 states; after each
+    event, with probability 0.3, a burst of 1-3 events from the same first-letter group (the
+    script's first two members of the group)."""
+    rng = rng_of(seed)
+    cid = ids(rng, n, 10)
+    ne = 5 + rng.integers(0, 20, n)
+    B = int(ne.sum())
+    base = rng.integers(0, 9, B)
+    blen = np.where(rng.integers(0, 10, B) < 3, 1 + rng.integers(0, 3, B), 0)
+    rep = np.repeat(np.arange(B), 1 + blen)
+    first = np.r_[0, np.cumsum(1 + blen)[:-1]]
+    pos = np.arange(len(rep)) - first[rep]
+    ev = np.where(pos == 0, base[rep], (base[rep] // 3) * 3 + rng.integers(0, 2, len(rep)))
+    per_cust = np.bincount(np.repeat(np.arange(n), ne), weights=1 + blen, minlength=n).astype(np.int64)
+    names = np.asarray(EVENT_STATES)[ev]
+    cuts = np.r_[0, np.cumsum(per_cust)]
+    return [f"{cid[i]}," + ",".join(names[cuts[i]:cuts[i + 1]]) for i in range(n)]
+
+
+def buy_xaction(cust_count: int, days: int, visitor_percent: float, seed=0, start_date: str = "2013-01-01",
+                start_xid: int = DEFAULT_END) -> list[str]:
+    """Purchase transactions (resource/buy_xaction.rb): every day visitor_percent x customers x
+    U(85, 115) % transactions by customers drawn with replacement; a first purchase is 40-219,
+    later ones depend on the days since and the amount of the customer's previous purchase.
+    Rows: customer id, transaction id, date, amount.  Vectorised per day; repeat picks of a
+    customer within a day are applied in pick order (rank rounds)."""
+    rng = rng_of(seed)
+    cids = ids(rng, cust_count, 10)
+    last_day = np.full(cust_count, -1, dtype=np.int64)
+    last_amt = np.zeros(cust_count, dtype=np.int64)
+    day0 = np.datetime64(start_date, "D")
+    out, xid = [], start_xid
+    for d in range(days):
+        m = int(visitor_percent * cust_count * (85 + rng.integers(0, 30)) / 100)
+        pick = rng.integers(0, cust_count, m)
+        order = np.argsort(pick, kind="stable")
+        sp = pick[order]
+        grp_start = np.r_[0, np.flatnonzero(np.diff(sp)) + 1]
+        rank_sorted = np.arange(m) - np.repeat(grp_start, np.diff(np.r_[grp_start, m]))
+        rank = np.empty(m, dtype=np.int64)
+        rank[order] = rank_sorted
+        amt = np.zeros(m, dtype=np.int64)
+        for r in range(int(rank.max()) + 1 if m else 0):
+            sel = np.flatnonzero(rank == r)
+            c = pick[sel]
+            k = len(sel)
+            gap = d - last_day[c]
+            la = last_amt[c]
+            a = np.where(la < 40, 50 + rng.integers(0, 20, k) - 10, 30 + rng.integers(0, 10, k) - 5)
+            a = np.where(gap >= 30, np.where(la < 80, 100 + rng.integers(0, 40, k) - 20,
+                                             60 + rng.integers(0, 20, k) - 10), a)
+            a = np.where(gap >= 60, np.where(la < 150, 180 + rng.integers(0, 60, k) - 30,
+                                             120 + rng.integers(0, 40, k) - 20), a)
+            a = np.where(last_day[c] < 0, 40 + rng.integers(0, 180, k), a)
+            amt[sel] = a
+            last_day[c] = d
+            last_amt[c] = a
+        date = str(day0 + d)
+        out.extend(f"{cids[c]},{xid + 1 + i},{date},{a}" for i, (c, a) in enumerate(zip(pick, amt)))
+        xid += m
+    return out
+
+
+def _xaction_state(prev_date, prev_amt, date, amt, short_days: int) -> str:
+    dd = (date - prev_date).astype(np.int64)
+    d = np.where(dd < short_days, "S", np.where(dd < 60, "M", "L"))
+    a = np.where(prev_amt < 0.9 * amt, "L", np.where(prev_amt < 1.1 * amt, "E", "G"))
+    return np.char.add(d, a)
+
+
+def _group_xactions(lines: Sequence[str]) -> dict[str, tuple[np.ndarray, np.ndarray]]:
+    hist: dict[str, list] = {}
+    for ln in lines:
+        it = ln.strip().split(",")
+        hist.setdefault(it[0], []).append((it[2], it[3]))
+    return {c: (np.array([np.datetime64(d, "D") for d, _ in h]), np.array([int(a) for _, a in h]))
+            for c, h in hist.items()}
+
+
+def xaction_seq(xaction_lines: Sequence[str]) -> list[str]:
+    """Transaction -> state sequence per customer (resource/xaction_seq.rb): a state per pair of
+    consecutive purchases, days gap S < 15 <= M < 60 <= L and amount change L / E / G at +-10 %;
+    customers with more than one state."""
+    out = []
+    for c, (dates, amts) in _group_xactions(xaction_lines).items():
+        if len(dates) < 2:
+            continue
+        seq = _xaction_state(dates[:-1], amts[:-1], dates[1:], amts[1:], 15)
+        if len(seq) > 1:
+            out.append(f"{c}," + ",".join(seq))
+    return out
+
+
+def xaction_state(history_lines: Sequence[str]) -> list[str]:
+    """Per-customer history rows ``cid,date,amt,date,amt,...`` -> state sequences
+    (resource/xaction_state.rb; gap thresholds 30 / 60 days), for rows with >= 2 purchases."""
+    out = []
+    for ln in history_lines:
+        it = ln.strip().split(",")
+        if len(it) < 5:
+            continue
+        dates = np.array([np.datetime64(x, "D") for x in it[1::2]])
+        amts = np.array([int(x) for x in it[2::2]])
+        seq = _xaction_state(dates[:-1], amts[:-1], dates[1:], amts[1:], 30)
+        out.append(f"{it[0]}," + ",".join(seq))
+    return out
+
+
+MARK_STATES = ["SL", "SE", "SG", "ML", "ME", "MG", "LL", "LE", "LG"]
+
+
+def mark_plan(xaction_lines: Sequence[str], model_rows: Sequence[Sequence[int]]) -> list[str]:
+    """Next marketing date per customer (resource/mark_plan.rb): the last purchase-pair state
+    (gap thresholds 30 / 60) -> most likely next state in the 9 x 9 transition count model ->
+    last purchase date + 15 / 45 / 90 days.  Rows ``cid, date`` as the script prints them."""
+    model = np.asarray(model_rows, dtype=np.int64)
+    out = []
+    for c, (dates, amts) in _group_xactions(xaction_lines).items():
+        if len(dates) < 2:
+            continue
+        last = str(_xaction_state(dates[-2:-1], amts[-2:-1], dates[-1:], amts[-1:], 30)[0])
+        nxt = MARK_STATES[int(np.argmax(model[MARK_STATES.index(last)]))]
+        out.append(f"{c}, {dates[-1] + {'S': 15, 'M': 45, 'L': 90}[nxt[0]]}")
+    return out
+
+
 FIXTURES: dict[str, Callable] = {
     "advt": advt, "atm_xaction": atm_xaction, "call_hangup": call_hangup, "cs_escalate": cs_escalate,
     "cust_seg": cust_seg, "cust_value": cust_value, "elearn": elearn,
@@ -687,4 +887,6 @@ FIXTURES: dict[str, Callable] = {
     "prot_seq": prot_seq, "prsale": prsale_stats, "ranproj": ranproj, "retarget": retarget,
     "sales_lead": sales_lead, "supplier": supplier, "telecom_churn": telecom_churn,
     "visit_history": visit_history, "lat_long": lat_long, "id_gen": id_list,
+    # resource/*.rb
+    "hosp_readmit": hosp_readmit, "disease": disease, "event_seq": event_seq, "buy_xaction": buy_xaction,
 }

@@ -28,6 +28,10 @@ CASES = {
     "telecom_churn": ((400, 30, 5), 7),
     "visit_history": ((100, 30), None),
     "lat_long": ((50, 37.0, -122.0, 38.0, -121.0), 2),
+    "hosp_readmit": ((400,), 12),
+    "disease": ((400,), 8),
+    "event_seq": ((100,), None),
+    "buy_xaction": ((50, 20, 0.3), 4),
     "id_gen": ((20, 12), 1),
 }
 
@@ -94,3 +98,38 @@ def test_price_opt_revenue_peaks():
     for revs in by.values():
         k = int(np.argmax(revs))
         assert all(revs[i] <= revs[i + 1] + 40 for i in range(k))   # rises to the peak (up to jitter)
+
+
+def test_ruby_generators_rates_and_pipeline():
+    rows = [r.split(",") for r in F.hosp_readmit(20000, seed=1)]
+    low = np.mean([r[11] == "Y" for r in rows if r[8] == "low"])
+    high = np.mean([r[11] == "Y" for r in rows if r[8] == "high"])
+    assert 0.05 < high < low < 0.9                      # low follow-up adds 8 points of risk
+    d = [r.split(",") for r in F.disease(20000, seed=2)]
+    young = np.mean([r[7] == "Yes" for r in d if int(r[1]) < 40])
+    old = np.mean([r[7] == "Yes" for r in d if int(r[1]) >= 70])
+    assert young < old
+    ev = F.event_seq(200, seed=3)
+    assert all(len(e.split(",")) >= 6 and set(e.split(",")[1:]) <= set(F.EVENT_STATES) for e in ev)
+    xs = F.buy_xaction(40, 120, 0.5, seed=4)
+    by = {}
+    for ln in xs:
+        c, _, date, amt = ln.split(",")
+        by.setdefault(c, []).append((np.datetime64(date), int(amt)))
+    for h in by.values():                               # the script's amount rules
+        assert 40 <= h[0][1] <= 219
+        for (d0, a0), (d1, a1) in zip(h, h[1:]):
+            gap = int((d1 - d0).astype(int))
+            if gap < 30:
+                assert (40 <= a1 <= 59) if a0 < 40 else (25 <= a1 <= 34)
+    seqs = F.xaction_seq(xs)
+    assert seqs and all(set(s.split(",")[1:]) <= set(F.MARK_STATES) for s in seqs)
+    hist = [c + "," + ",".join(f"{d},{a}" for d, a in h) for c, h in by.items()]
+    st = F.xaction_state(hist)
+    assert len(st) == sum(len(h) >= 2 for h in by.values())
+    model = np.eye(9, dtype=int) * 5 + 1
+    plan = F.mark_plan(xs, model)
+    assert len(plan) == sum(len(h) >= 2 for h in by.values())
+    c, date = plan[0].split(", ")
+    last = by[c][-1][0]
+    assert int((np.datetime64(date) - last).astype(int)) in (15, 45, 90)
