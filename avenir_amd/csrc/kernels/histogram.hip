@@ -370,7 +370,7 @@ void launch_split(const uint8_t* codes, long long ld, long long n, const uint8_t
 // K2, row-packed layout: every record is ONE 16-bit word holding all of its categorical codes
 // and its class (field k at bit sh[k], width w[k] <= 3 bits; a field that has missing values
 // keeps its all-ones value as the missing code, never a valid bin; for C = 2 the class is two
-// one-hot bits at lsh, both clear for an unknown class).  For low-cardinality schemas such as
+// one-hot bits 0-1, both clear for an unknown class, and the fields follow from bit 2).  For low-cardinality schemas such as
 // R/churn.json (5 features of 3-5 values + a binary class = 13 bits) this is 2 bytes per record
 // instead of F + 1 = 6 bytes of byte-per-code columns.
 //
@@ -426,6 +426,9 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
 #pragma unroll
     for (int m = 0; m < 4; ++m) w16[j][m] = 0;
   }
+  unsigned m4[NF];  // C = 2: (4 * code) field mask of both records of a dword
+#pragma unroll
+  for (int k = 0; k < NF; ++k) m4[k] = (((1u << spec.w[k]) - 1u) << 2) * 0x00010001u;
   const unsigned N4 = 0x0F0F0F0Fu, B8 = 0x00FF00FFu;
   auto spread = [&]() __attribute__((always_inline)) {  // nibbles -> bytes: be byte i = slot 2i, bo = 2i + 1
 #pragma unroll
@@ -484,27 +487,41 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
     if (t + nw < ntiles && v < nvec) qn = w4[v];
     if (have) {
       const unsigned dw[4] = {q.x, q.y, q.z, q.w};
+      if (C == 1) {
 #pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const unsigned d = dw[h >> 1];
-        const int o = 16 * (h & 1);  // record h sits in bits [o, o + 16) of its dword
-        unsigned x[C];
+        for (int h = 0; h < 8; ++h) {
+          const unsigned d = dw[h >> 1];
+          const int o = 16 * (h & 1);  // record h sits in bits [o, o + 16) of its dword
 #pragma unroll
-        for (int c = 0; c < C; ++c)
-          x[c] = C == 1 ? 1u : __builtin_amdgcn_ubfe(d, (unsigned)(spec.lsh + o + c), 1u);
-        unsigned valid = 0, c16 = 0;
-        if (NM > 0) {
-          valid = x[0] | x[C - 1];  // known class
-          c16 = x[C - 1] << 4;      // class 1: slot + 4 = nibble shift + 16
+          for (int k = 0; k < NF; ++k)
+            lshl_add_u32(a4[k], 1u, __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]) << 2);
         }
+      } else {
+        // two records per dword: class one-hot bits at 0-1 / 16-17 and every field at bit >= 2,
+        // so (d >> (sh - 2)) & mask puts 4 * code of both records at bits 2-4 / 18-20 in two ops
+        // (v_lshl_add_u32 reads only bits [4:0] of its shift operand)
 #pragma unroll
-        for (int k = 0; k < NF; ++k) {
-          const unsigned code = __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]);
-          if (k < NM) {
-            lshl_add_u32(a4[k], valid, (code << 2) | c16);
-          } else {
+        for (int h = 0; h < 4; ++h) {
+          const unsigned d = dw[h];
+          const unsigned x0a = d & 1u, x1a = __builtin_amdgcn_ubfe(d, 1u, 1u);
+          const unsigned x0b = __builtin_amdgcn_ubfe(d, 16u, 1u), x1b = __builtin_amdgcn_ubfe(d, 17u, 1u);
+          const unsigned va = x0a | x1a, vb = x0b | x1b;  // known class
+          const unsigned c16 = (d << 3) & 0x00100010u;    // class 1: slot + 4 = nibble shift + 16
 #pragma unroll
-            for (int c = 0; c < C; ++c) lshl_add_u32(a4[NM + (k - NM) * C + c], x[c], code << 2);
+          for (int k = 0; k < NF; ++k) {
+            const unsigned t = (d >> (unsigned)(spec.sh[k] - 2)) & m4[k];
+            if (k < NM) {
+              const unsigned sm = t | c16;
+              lshl_add_u32(a4[k], va, sm);
+              lshl_add_u32(a4[k], vb, sm >> 16);
+            } else {
+              const int j = NM + (k - NM) * C;
+              const unsigned tb = t >> 16;
+              lshl_add_u32(a4[j], x0a, t);
+              lshl_add_u32(a4[j + 1], x1a, t);
+              lshl_add_u32(a4[j], x0b, tb);
+              lshl_add_u32(a4[j + 1], x1b, tb);
+            }
           }
         }
       }
@@ -896,8 +913,10 @@ void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_
     spec.sh[k] = h_shift[k];
     spec.w[k] = h_width[k];
   }
-  if (n_classes > 1 && label_width != n_classes)
-    throw std::runtime_error("row-packed histogram: the class is C one-hot bits");
+  if (n_classes > 1 && (label_width != n_classes || label_shift != 0))
+    throw std::runtime_error("row-packed histogram: the class is C one-hot bits at bit 0");
+  for (int k = 0; k < nfeat; ++k)
+    if (n_classes > 1 && h_shift[k] < 2) throw std::runtime_error("row-packed histogram: fields start at bit 2");
   spec.lsh = n_classes > 1 ? label_shift : 0;
   int nm = 0;  // leading features whose (class, code) share one slot (kernel order puts them first)
   if (n_classes == 2)

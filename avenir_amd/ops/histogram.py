@@ -102,14 +102,14 @@ def rowpack_layout(bins: Sequence[int], n_classes: int, missing: Sequence[bool] 
     widths = [max(1, (b if m else b - 1).bit_length()) for b, m in zip(bins, missing)]
     if max(widths) > 3:
         return None
-    shifts, s = [], 0
+    lw = 2 if C == 2 else 0            # C = 2: class bits 0-1, the fields from bit 2
+    shifts, s = [], lw
     for w in widths:
         shifts.append(s)
         s += w
-    lw = 2 if C == 2 else 0
-    if s + lw > 16:
+    if s > 16:
         return None
-    return shifts, widths, s, lw
+    return shifts, widths, 0 if lw else s, lw
 
 
 def pack_rows(codes: torch.Tensor, n: int, bins: Sequence[int], labels: torch.Tensor | None,

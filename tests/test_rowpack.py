@@ -31,14 +31,14 @@ def _random_codes(n, bins, C, seed=0, missing=0.05):
 
 
 def test_layout_rules():
-    assert H.rowpack_layout([4, 3, 3, 3, 5], 2) == ([0, 3, 5, 7, 9], [3, 2, 2, 2, 3], 12, 2)
+    assert H.rowpack_layout([4, 3, 3, 3, 5], 2) == ([2, 5, 7, 9, 11], [3, 2, 2, 2, 3], 0, 2)
     assert H.rowpack_layout([1, 2, 3], 1) == ([0, 1, 3], [1, 2, 2], 5, 0)
     assert H.rowpack_layout([8], 2) is None              # 8 values + a missing code need 4 bits
     assert H.rowpack_layout([7] * 5, 2) is None          # 15 + 2 bits > 16
     assert H.rowpack_layout([3] * 9, 1) is None          # more than 8 fields
     assert H.rowpack_layout([3, 3], 3) is None           # more than 2 classes
     # data-adaptive: no missing values -> bit_length(b - 1) bits
-    assert H.rowpack_layout([4, 3, 3, 3, 5], 2, [False] * 5) == ([0, 2, 4, 6, 8], [2, 2, 2, 2, 3], 11, 2)
+    assert H.rowpack_layout([4, 3, 3, 3, 5], 2, [False] * 5) == ([2, 4, 6, 8, 10], [2, 2, 2, 2, 3], 0, 2)
     assert H.rowpack_layout([8, 1], 1, [False, False]) == ([0, 3], [3, 1], 4, 0)
 
 
@@ -102,7 +102,7 @@ def test_packed_histogram_gpu_long_uniform_run():
     counter overflow shows up as a wrong count."""
     n = 1 << 28
     bins = [4, 3, 3, 3, 5]
-    word = 2 | (1 << 3) | (0 << 5) | (2 << 7) | (4 << 9) | (2 << 12)      # class 1 = one-hot bit 13
+    word = (1 << 1) | (2 << 2) | (1 << 5) | (0 << 7) | (2 << 9) | (4 << 11)      # class 1 = one-hot bit 1
     words = torch.full((n,), word, dtype=torch.int16, device="cuda")
     rp = H.RowPacked(words, n, bins, *H.rowpack_layout(bins, 2), 2)
     assert rp.widths == [3, 2, 2, 2, 3]
