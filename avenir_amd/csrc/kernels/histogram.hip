@@ -478,56 +478,66 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
   const long long gw = (long long)blockIdx.x * WPB + av::wave_id();
   const long long nw = (long long)gridDim.x * WPB;
   int since_flush = 0, flushes = 0;
-  long long v = gw * AV_WAVE + av::lane_id();
-  uint4 qn = (gw < ntiles && v < nvec) ? w4[v] : make_uint4(0u, 0u, 0u, 0u);
-  for (long long t = gw; t < ntiles; t += nw) {
-    const uint4 q = qn;
-    const bool have = v < nvec;
-    v += nw * AV_WAVE;
-    if (t + nw < ntiles && v < nvec) qn = w4[v];
-    if (have) {
-      const unsigned dw[4] = {q.x, q.y, q.z, q.w};
-      if (C == 1) {
+  // two tiles per iteration, and the next iteration's two 16-byte loads in flight while these
+  // are counted (counting costs ~22 VALU ops per record, so loads must run well ahead)
+  auto count = [&](const uint4 q) __attribute__((always_inline)) {
+    const unsigned dw[4] = {q.x, q.y, q.z, q.w};
+    if (C == 1) {
 #pragma unroll
-        for (int h = 0; h < 8; ++h) {
-          const unsigned d = dw[h >> 1];
-          const int o = 16 * (h & 1);  // record h sits in bits [o, o + 16) of its dword
+      for (int h = 0; h < 8; ++h) {
+        const unsigned d = dw[h >> 1];
+        const int o = 16 * (h & 1);  // record h sits in bits [o, o + 16) of its dword
 #pragma unroll
-          for (int k = 0; k < NF; ++k)
-            lshl_add_u32(a4[k], 1u, __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]) << 2);
-        }
-      } else {
-        // two records per dword: class one-hot bits at 0-1 / 16-17 and every field at bit >= 2,
-        // so (d >> (sh - 2)) & mask puts 4 * code of both records at bits 2-4 / 18-20 in two ops
-        // (v_lshl_add_u32 reads only bits [4:0] of its shift operand)
+        for (int k = 0; k < NF; ++k)
+          lshl_add_u32(a4[k], 1u, __builtin_amdgcn_ubfe(d, (unsigned)(spec.sh[k] + o), (unsigned)spec.w[k]) << 2);
+      }
+    } else {
+      // two records per dword: class one-hot bits at 0-1 / 16-17 and every field at bit >= 2,
+      // so (d >> (sh - 2)) & mask puts 4 * code of both records at bits 2-4 / 18-20 in two ops
+      // (v_lshl_add_u32 reads only bits [4:0] of its shift operand)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const unsigned d = dw[h];
-          const unsigned x0a = d & 1u, x1a = __builtin_amdgcn_ubfe(d, 1u, 1u);
-          const unsigned x0b = __builtin_amdgcn_ubfe(d, 16u, 1u), x1b = __builtin_amdgcn_ubfe(d, 17u, 1u);
-          const unsigned va = x0a | x1a, vb = x0b | x1b;  // known class
-          const unsigned c16 = (d << 3) & 0x00100010u;    // class 1: slot + 4 = nibble shift + 16
+      for (int h = 0; h < 4; ++h) {
+        const unsigned d = dw[h];
+        const unsigned x0a = d & 1u, x1a = __builtin_amdgcn_ubfe(d, 1u, 1u);
+        const unsigned x0b = __builtin_amdgcn_ubfe(d, 16u, 1u), x1b = __builtin_amdgcn_ubfe(d, 17u, 1u);
+        const unsigned va = x0a | x1a, vb = x0b | x1b;  // known class
+        const unsigned c16 = (d << 3) & 0x00100010u;    // class 1: slot + 4 = nibble shift + 16
 #pragma unroll
-          for (int k = 0; k < NF; ++k) {
-            const unsigned t = (d >> (unsigned)(spec.sh[k] - 2)) & m4[k];
-            if (k < NM) {
-              const unsigned sm = t | c16;
-              lshl_add_u32(a4[k], va, sm);
-              lshl_add_u32(a4[k], vb, sm >> 16);
-            } else {
-              const int j = NM + (k - NM) * C;
-              const unsigned tb = t >> 16;
-              lshl_add_u32(a4[j], x0a, t);
-              lshl_add_u32(a4[j + 1], x1a, t);
-              lshl_add_u32(a4[j], x0b, tb);
-              lshl_add_u32(a4[j + 1], x1b, tb);
-            }
+        for (int k = 0; k < NF; ++k) {
+          const unsigned t = (d >> (unsigned)(spec.sh[k] - 2)) & m4[k];
+          if (k < NM) {
+            const unsigned sm = t | c16;
+            lshl_add_u32(a4[k], va, sm);
+            lshl_add_u32(a4[k], vb, sm >> 16);
+          } else {
+            const int j = NM + (k - NM) * C;
+            const unsigned tb = t >> 16;
+            lshl_add_u32(a4[j], x0a, t);
+            lshl_add_u32(a4[j + 1], x1a, t);
+            lshl_add_u32(a4[j], x0b, tb);
+            lshl_add_u32(a4[j + 1], x1b, tb);
           }
         }
       }
     }
+    };
+  const long long vstride = nw * AV_WAVE;
+  long long v = gw * AV_WAVE + av::lane_id();
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  uint4 qa = (gw < ntiles && v < nvec) ? w4[v] : z4;
+  uint4 qb = (gw + nw < ntiles && v + vstride < nvec) ? w4[v + vstride] : z4;
+  for (long long t = gw; t < ntiles; t += 2 * nw) {
+    const uint4 q0 = qa, q1 = qb;
+    const bool h0 = v < nvec, h1 = t + nw < ntiles && v + vstride < nvec;
+    v += 2 * vstride;
+    if (t + 2 * nw < ntiles && v < nvec) qa = w4[v];
+    if (t + 3 * nw < ntiles && v + vstride < nvec) qb = w4[v + vstride];
+    if (h0) count(q0);
     spread();
-    if (++since_flush == FLUSH) {  // wave-uniform
+    if (h1) count(q1);
+    spread();
+    since_flush += 2;
+    if (since_flush >= FLUSH - 1) {  // wave-uniform; <= 30 tiles x 8 records per byte counter
       widen();
       since_flush = 0;
       if (++flushes == 256) {
