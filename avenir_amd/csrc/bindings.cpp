@@ -797,6 +797,51 @@ at::Tensor smo_ws_solve(const at::Tensor& Kws, const at::Tensor& yws, at::Tensor
   return iters;
 }
 
+void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tensor& y, double C, int64_t h,
+                   at::Tensor& ws, at::Tensor& ok, at::Tensor& gap) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&alpha, &G, &y, &gap}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
+  const int64_t B = y.size(0), N = y.size(1);
+  TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
+              "alpha / G must be [B, >= N]");
+  TORCH_CHECK(h >= 1 && h <= 64 && N >= 1 && N <= (1 << 18), "1 <= h <= 64, 1 <= N <= 2^18");
+  CHECK_DEV(ws);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DEV(ok);
+  CHECK_DTYPE(ok, at::kBool);
+  TORCH_CHECK(ws.numel() == B * 2 * h && ok.numel() == B * 2 * h && gap.numel() == B, "ws / ok [B, 2h], gap [B]");
+  DevGuard g(y.device());
+  avk::smo_ws_select(alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)N,
+                     (int)alpha.size(1), (float)C, (int)h, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()),
+                     ok.data_ptr<bool>(), gap.data_ptr<float>(), cur_stream(y));
+}
+
+void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& dA, const at::Tensor& ok,
+                   const at::Tensor& y, at::Tensor& G) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&K, &dA, &y, &G}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
+  const int64_t B = y.size(0), N = y.size(1);
+  TORCH_CHECK(K.dim() == 3 && K.size(0) == B && K.size(1) == N && K.size(2) == N, "K must be [B, N, N]");
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == B && G.size(1) >= N, "G must be [B, >= N]");
+  CHECK_DEV(ws);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DEV(ok);
+  CHECK_DTYPE(ok, at::kBool);
+  TORCH_CHECK(ws.dim() == 2 && ws.size(0) == B && ws.size(1) <= avk::smo_ws_size() && dA.sizes() == ws.sizes() &&
+                  ok.sizes() == ws.sizes(),
+              "ws / dA / ok must be [B, Q <= ", avk::smo_ws_size(), "]");
+  DevGuard g(y.device());
+  avk::smo_ws_update(K.data_ptr<float>(), reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()),
+                     dA.data_ptr<float>(), ok.data_ptr<bool>(), y.data_ptr<float>(), G.data_ptr<float>(), (int)B,
+                     (int)N, (int)G.size(1), (int)ws.size(1), cur_stream(y));
+}
+
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,
                                     int64_t extent, double laplace, double log_floor) {
   CHECK_DEV(counts);
@@ -1180,6 +1225,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);
   m.def("smo_ws_solve", &smo_ws_solve);
+  m.def("smo_ws_select", &smo_ws_select);
+  m.def("smo_ws_update", &smo_ws_update);
   m.def("smo_ws_size", &avk::smo_ws_size);
   m.def("nb_finalize", &nb_finalize);
   m.def("weighted_gram", &weighted_gram);

@@ -102,6 +102,11 @@ void glm_grad(const float* X, long long ld, long long n, int D, const float* y, 
 // ---- svm.hip (K12) -------------------------------------------------------------------------
 void smo_solve(const float* K, const float* y, const float* diag, float* alpha, float* G, int B, int N, float C,
                float eps, int max_iter, int* iters, hipStream_t stream);
+// working-set selection (gap, top-h up / low violators, duplicate mask) and gradient update
+void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
+                   long long* ws, bool* ok, float* gap, hipStream_t stream);
+void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
+                   int B, int N, int ldag, int Q, hipStream_t stream);
 int smo_ws_size();
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream);

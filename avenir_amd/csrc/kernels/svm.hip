@@ -272,6 +272,180 @@ __global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Ka
   if (lane == 0) iters[b] = it;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Working-set selection and gradient update for smo_decomposition, one launch each per outer
+// step (they replace ~25 small torch ops: the violation values, two top-k sorts, the
+// duplicate mask, the [B, Q, N] row gather and the batched GEMV).
+//
+// smo_ws_select_kernel: one 1024-thread workgroup per problem.  The "up" / "low" violation
+// values are recomputed from (alpha, G, y) in every pass (N floats x 3 from L2); the gap is
+// max(up) + max(low); the h largest of each set are found by an exact 4-pass 8-bit radix select
+// on order-preserving float keys (LDS histogram), collected with LDS counters, and written in
+// ascending index order (deterministic working sets).  A low-set index already in the up set is
+// masked out (ok = 0), as in the torch path.
+// smo_ws_update_kernel: G[n] += y[n] * sum_q dA[q] K[ws[q], n], one thread per n, the Q
+// (index, dA) pairs in LDS, K rows read coalesced.
+// ---------------------------------------------------------------------------------------------
+constexpr int SEL_T = 1024;
+
+__device__ __forceinline__ float ws_violation(int which, float y, float a, float g, float C) {
+  if (which == 0) {
+    const bool up = y > 0.f ? a < C : (y < 0.f && a > 0.f);
+    return up ? -y * g : -INFINITY;
+  }
+  const bool low = y > 0.f ? a > 0.f : (y < 0.f && a < C);
+  return low ? y * g : -INFINITY;
+}
+
+__device__ __forceinline__ unsigned order_key(float f) {  // monotone float -> uint
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <typename T, typename Op>
+__device__ T block_reduce(T v, T* red, Op op) {  // all SEL_T threads; red has >= 17 slots
+  constexpr int NW = SEL_T / 64;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T r = red[0];
+    for (int i = 1; i < NW; ++i) r = op(r, red[i]);
+    red[NW] = r;
+  }
+  __syncthreads();
+  const T r = red[NW];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __restrict__ alpha,
+                                                              const float* __restrict__ G,
+                                                              const float* __restrict__ y, int N, int ldag, float C,
+                                                              int h, long long* __restrict__ ws,
+                                                              bool* __restrict__ ok, float* __restrict__ gap) {
+  extern __shared__ unsigned in_up[];  // [(N + 31) / 32] bitmap of the selected up set
+  __shared__ unsigned hist[256];
+  __shared__ float redf[17];
+  __shared__ unsigned redu[17];
+  __shared__ unsigned s_prefix, s_mask, s_krem, s_gt, s_eq;
+  __shared__ int pick[2][64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* ab = alpha + (long long)b * ldag;
+  const float* gb = G + (long long)b * ldag;
+  const float* yb = y + (long long)b * N;
+  const int words = (N + 31) / 32;
+  for (int i = tid; i < words; i += SEL_T) in_up[i] = 0;
+
+  float mu = -INFINITY, ml = -INFINITY;
+  for (int n = tid; n < N; n += SEL_T) {
+    const float yn = yb[n], an = ab[n], gn = gb[n];
+    mu = fmaxf(mu, ws_violation(0, yn, an, gn, C));
+    ml = fmaxf(ml, ws_violation(1, yn, an, gn, C));
+  }
+  auto fmax_op = [](float p, float q) { return fmaxf(p, q); };
+  auto add_op = [](unsigned p, unsigned q) { return p + q; };
+  mu = block_reduce(mu, redf, fmax_op);
+  ml = block_reduce(ml, redf, fmax_op);
+  if (tid == 0) gap[b] = mu + ml;
+
+  int npick[2] = {0, 0};
+  for (int which = 0; which < 2; ++which) {
+    unsigned e = 0;
+    for (int n = tid; n < N; n += SEL_T) e += ws_violation(which, yb[n], ab[n], gb[n], C) > -INFINITY ? 1u : 0u;
+    e = block_reduce(e, redu, add_op);
+    const unsigned k = e < (unsigned)h ? e : (unsigned)h;
+    npick[which] = (int)k;
+    if (k == 0) continue;  // block-uniform
+    if (tid == 0) { s_prefix = 0; s_mask = 0; s_krem = k; }
+    for (int d = 3; d >= 0; --d) {
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      const unsigned prefix = s_prefix, mask = s_mask;
+      for (int n = tid; n < N; n += SEL_T) {
+        const float v = ws_violation(which, yb[n], ab[n], gb[n], C);
+        if (v > -INFINITY) {
+          const unsigned key = order_key(v);
+          if ((key & mask) == prefix) atomicAdd(&hist[(key >> (8 * d)) & 255u], 1u);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {  // the digit holding the krem-th largest key
+        unsigned cum = 0, krem = s_krem;
+        for (int dg = 255; dg >= 0; --dg) {
+          if (cum + hist[dg] >= krem) {
+            s_prefix = prefix | ((unsigned)dg << (8 * d));
+            s_mask = mask | (255u << (8 * d));
+            s_krem = krem - cum;
+            break;
+          }
+          cum += hist[dg];
+        }
+        s_gt = 0;
+        s_eq = 0;
+      }
+      __syncthreads();
+    }
+    const unsigned T = s_prefix, krem = s_krem, ngt = k - krem;  // keys > T: exactly ngt of them
+    for (int n = tid; n < N; n += SEL_T) {
+      const float v = ws_violation(which, yb[n], ab[n], gb[n], C);
+      if (v > -INFINITY) {
+        const unsigned key = order_key(v);
+        if (key > T) {
+          pick[which][atomicAdd(&s_gt, 1u)] = n;
+        } else if (key == T) {
+          const unsigned s2 = atomicAdd(&s_eq, 1u);
+          if (s2 < krem) pick[which][ngt + s2] = n;
+        }
+      }
+    }
+    __syncthreads();
+    if (which == 0 && tid < (int)k) atomicOr(&in_up[pick[0][tid] >> 5], 1u << (pick[0][tid] & 31));
+    __syncthreads();
+  }
+  // ascending index order within each half; unused slots -> (0, not ok)
+  if (tid < 2 * h) {
+    const int which = tid / h, slot = tid % h, np = npick[which];
+    long long* wsb = ws + (long long)b * 2 * h + which * h;
+    bool* okb = ok + (long long)b * 2 * h + which * h;
+    if (slot < np) {
+      const int n = pick[which][slot];
+      int rank = 0;
+      for (int j = 0; j < np; ++j) rank += pick[which][j] < n ? 1 : 0;
+      wsb[rank] = n;
+      okb[rank] = which == 0 || !((in_up[n >> 5] >> (n & 31)) & 1u);
+    } else {
+      wsb[slot] = 0;
+      okb[slot] = false;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
+                                                            const float* __restrict__ dA, const bool* __restrict__ ok,
+                                                            const float* __restrict__ y, float* __restrict__ G, int N,
+                                                            int ldag, int Q) {
+  __shared__ long long s_ws[WS_Q];
+  __shared__ float s_d[WS_Q];
+  const int b = blockIdx.y;
+  for (int q = threadIdx.x; q < Q; q += 256) {
+    const bool o = ok[(long long)b * Q + q];
+    s_ws[q] = o ? ws[(long long)b * Q + q] : 0;
+    s_d[q] = o ? dA[(long long)b * Q + q] : 0.f;
+  }
+  __syncthreads();
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const float* Kb = K + (long long)b * N * N;
+  float acc = 0.f;
+  for (int q = 0; q < Q; ++q)
+    if (s_d[q] != 0.f) acc += s_d[q] * Kb[s_ws[q] * N + n];  // s_d is block-uniform: no divergence
+  G[(long long)b * ldag + n] += y[(long long)b * N + n] * acc;
+}
+
 }  // namespace
 
 namespace avk {
@@ -289,6 +463,21 @@ void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* g
                   float eps, int max_iter, int* iters, hipStream_t stream) {
   if (B <= 0) return;
   smo_ws_kernel<<<B, 64, 0, stream>>>(Kws, yws, aws, gws, gap, C, eps, max_iter, iters);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
+                   long long* ws, bool* ok, float* gap, hipStream_t stream) {
+  if (B <= 0) return;
+  const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
+  smo_ws_select_kernel<<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
+                   int B, int N, int ldag, int Q, hipStream_t stream) {
+  if (B <= 0 || N <= 0) return;
+  smo_ws_update_kernel<<<dim3((N + 255) / 256, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q);
   AV_HIP_CHECK(hipGetLastError());
 }
 

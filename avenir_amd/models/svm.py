@@ -129,7 +129,7 @@ class _WorkingSetSMO:
     """State and one outer step of the working-set solver, written with static shapes so that a
     block of steps can be captured as one HIP graph (see ``smo_decomposition``)."""
 
-    def __init__(self, K, y, C, eps, inner_iter, Q):
+    def __init__(self, K, y, C, eps, inner_iter, Q, fused=True):
         self.K, self.C, self.eps, self.inner_iter = K, float(C), float(eps), int(inner_iter)
         B, N = y.shape
         dev = K.device
@@ -143,6 +143,12 @@ class _WorkingSetSMO:
         self.inner_total = torch.zeros(B, dtype=torch.long, device=dev)
         self.gap = torch.full((B,), float("inf"), device=dev)
         self.ninf = torch.tensor(-float("inf"), device=dev)
+        # fused selection / update kernels (one launch each instead of ~25 torch ops per step)
+        self.fused = (fused and self.gpu and K.dtype == torch.float32 and K.is_contiguous() and N <= (1 << 18)
+                      and Q == 128)
+        if self.fused:
+            self.ws_buf = torch.zeros((B, Q), dtype=torch.long, device=dev)
+            self.ok_buf = torch.zeros((B, Q), dtype=torch.bool, device=dev)
 
     def refresh_gap(self):
         a, g, yf = self.alpha[:, :self.N], self.G[:, :self.N], self.yf
@@ -155,15 +161,20 @@ class _WorkingSetSMO:
 
     def step(self):
         B, N, Q, h, dev = self.B, self.N, self.Q, self.h, self.K.device
-        vu, vl = self.refresh_gap()
-        vu_v, iu = torch.topk(vu, h, 1)
-        vl_v, il = torch.topk(vl, h, 1)
-        ws = torch.cat([iu, il], 1)
-        ok = torch.cat([vu_v > -float("inf"), (vl_v > -float("inf")) & ~(il.unsqueeze(2) == iu.unsqueeze(1)).any(2)], 1)
-        if ws.shape[1] < Q:                                                    # N < Q/2: pad the set
-            pad = Q - ws.shape[1]
-            ws = torch.cat([ws, torch.zeros((B, pad), dtype=ws.dtype, device=dev)], 1)
-            ok = torch.cat([ok, torch.zeros((B, pad), dtype=torch.bool, device=dev)], 1)
+        if self.fused:
+            _native.C().smo_ws_select(self.alpha, self.G, self.yf, self.C, Q // 2, self.ws_buf, self.ok_buf, self.gap)
+            ws, ok = self.ws_buf, self.ok_buf
+        else:
+            vu, vl = self.refresh_gap()
+            vu_v, iu = torch.topk(vu, h, 1)
+            vl_v, il = torch.topk(vl, h, 1)
+            ws = torch.cat([iu, il], 1)
+            ok = torch.cat([vu_v > -float("inf"),
+                            (vl_v > -float("inf")) & ~(il.unsqueeze(2) == iu.unsqueeze(1)).any(2)], 1)
+            if ws.shape[1] < Q:                                                # N < Q/2: pad the set
+                pad = Q - ws.shape[1]
+                ws = torch.cat([ws, torch.zeros((B, pad), dtype=ws.dtype, device=dev)], 1)
+                ok = torch.cat([ok, torch.zeros((B, pad), dtype=torch.bool, device=dev)], 1)
         wsg = torch.where(ok, ws, torch.zeros_like(ws))
         yws = (self.yp.gather(1, wsg) * ok).contiguous()
         aws = self.alpha.gather(1, wsg).contiguous()
@@ -185,12 +196,16 @@ class _WorkingSetSMO:
         self.inner_total += it.to(dev).long()
         dA = (aws - a_old) * yws
         self.alpha.scatter_(1, torch.where(ok, ws, torch.full_like(ws, N)), torch.where(ok, aws, torch.zeros_like(aws)))
-        Krows = self.K[self.rows.view(-1, 1), wsg].float()                     # [B, Q, N]
-        self.G[:, :N] += self.yf * torch.bmm(dA.unsqueeze(1), Krows).squeeze(1)
+        if self.fused:
+            _native.C().smo_ws_update(self.K, ws, dA.contiguous(), ok, self.yf, self.G)
+        else:
+            Krows = self.K[self.rows.view(-1, 1), wsg].float()                 # [B, Q, N]
+            self.G[:, :N] += self.yf * torch.bmm(dA.unsqueeze(1), Krows).squeeze(1)
 
 
 def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_outer: int = 100_000,
-                      inner_iter: int = 2048, check_every: int = 16, Q: int | None = None, graph: bool = True):
+                      inner_iter: int = 2048, check_every: int = 16, Q: int | None = None, graph: bool = True,
+                      fused: bool = True):
     """Working-set SMO for B problems (K [B, N, N], y [B, N] in {-1, 0, +1}).
 
     Each outer step picks the Q/2 largest violators of the "up" set and the Q/2 largest of the
@@ -200,10 +215,12 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     the full gradient with one batched GEMV.  On the GPU ``check_every`` steps are one captured
     HIP graph (static shapes; steps after convergence are no-ops because the sub-problem solver
     stops at once), and the host reads the global violation gap once per replay.  Stops when
-    the gap < eps.  Returns (alpha, G, outer steps, inner steps).
+    the gap < eps.  ``fused`` (GPU, float32 K, N <= 2^18): the working-set selection and the
+    gradient update are one kernel each (``smo_ws_select`` / ``smo_ws_update``) instead of ~25
+    torch ops.  Returns (alpha, G, outer steps, inner steps).
     """
     Q = Q or (_native.C().smo_ws_size() if K.device.type == "cuda" else 128)
-    st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q)
+    st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused)
     outer = 0
     if st.gpu and graph:
         st.step()                                # eager warm-up: allocator pool, kernel caches

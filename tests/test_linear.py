@@ -273,3 +273,52 @@ def test_smo_working_set_gpu_matches_full(cuda, N):
     ff = (af[0] * y) @ K[0] - rf[0]
     fw = (aw[0] * y) @ K[0] - rw[0]
     assert (torch.sign(ff) == torch.sign(fw)).float().mean() > 0.995
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [40, 1000, 70000])
+def test_smo_ws_select_matches_topk(cuda, N):
+    """Fused working-set selection == gap + top-h up / low violator sets of the torch path."""
+    from avenir_amd import _native
+    torch.manual_seed(N)
+    B, h, Cc = 3, 64, 1.0
+    y = torch.where(torch.rand(B, N, device=cuda) > 0.5, 1.0, -1.0)
+    alpha = torch.zeros(B, N + 1, device=cuda)
+    alpha[:, :N] = torch.rand(B, N, device=cuda).clamp(0.2, 0.8) * (torch.rand(B, N, device=cuda) > 0.3) * Cc
+    alpha[:, :N] = torch.where(torch.rand(B, N, device=cuda) > 0.9, torch.full_like(y, Cc), alpha[:, :N])
+    G = torch.randn(B, N + 1, device=cuda)
+    ws = torch.zeros(B, 2 * h, dtype=torch.long, device=cuda)
+    ok = torch.zeros(B, 2 * h, dtype=torch.bool, device=cuda)
+    gap = torch.zeros(B, device=cuda)
+    _native.C().smo_ws_select(alpha, G, y, Cc, h, ws, ok, gap)
+    a, g = alpha[:, :N], G[:, :N]
+    up = (y > 0) & (a < Cc) | (y < 0) & (a > 0)
+    low = (y > 0) & (a > 0) | (y < 0) & (a < Cc)
+    vu = torch.where(up, -y * g, torch.full_like(g, -float("inf")))
+    vl = torch.where(low, y * g, torch.full_like(g, -float("inf")))
+    assert torch.allclose(gap, vu.max(1).values + vl.max(1).values)
+    for b in range(B):
+        for half, v in ((0, vu[b]), (1, vl[b])):
+            k = min(h, int(torch.isfinite(v).sum()))
+            exp = set(torch.topk(v, k).indices.tolist())
+            sl = slice(half * h, half * h + k)
+            got = ws[b, sl].tolist()
+            assert set(got) == exp and got == sorted(got)
+            assert not ok[b, half * h + k:(half + 1) * h].any()
+        iu = set(ws[b, :h][ok[b, :h]].tolist())
+        for i, o in zip(ws[b, h:].tolist(), ok[b, h:].tolist()):
+            if o:
+                assert i not in iu
+
+
+@pytest.mark.gpu
+def test_smo_decomposition_fused_matches_torch_path(cuda):
+    from avenir_amd.models.svm import kernel_matrix, smo_decomposition
+    torch.manual_seed(5)
+    X = torch.randn(5000, 6, device=cuda)
+    y = torch.where(X[:, 0] * X[:, 1] > 0, 1.0, -1.0)
+    K = kernel_matrix(X, X, "rbf", 0.5).unsqueeze(0).contiguous()
+    a1, _, o1, _ = smo_decomposition(K, y.view(1, -1), 1.0, 1e-3, fused=True)
+    a0, _, o0, _ = smo_decomposition(K, y.view(1, -1), 1.0, 1e-3, fused=False)
+    d1, d0 = _svm_dual(a1[0], y, K[0]), _svm_dual(a0[0], y, K[0])
+    assert abs(d1 - d0) < 2e-4 * abs(d0)
