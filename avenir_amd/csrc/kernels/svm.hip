@@ -208,7 +208,12 @@ __global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Ka
     av::wave_argmax(gmax, gi);
     if (gi == NONE) break;
     const int i = gi;
-    const float Kii = Ks[i][i];
+    // i / j are wave-uniform: their per-lane state comes over with v_readlane (a few cycles)
+    // instead of ds_bpermute shuffles (an LDS round trip each)
+    float Kii = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (e == (i >> 6)) Kii = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qd[e]), i & 63));
     float best = -INFINITY, gmax2 = -INFINITY;
     int bj = NONE;
 #pragma unroll
@@ -232,14 +237,15 @@ __global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Ka
     const int j = bj;
     // fetch the pair's state from its owner lanes (slot index is wave-uniform)
     const int si = i >> 6, sj = j >> 6;
-    float yi = 0.f, ai = 0.f, gi_ = 0.f, yj = 0.f, aj = 0.f, gj = 0.f;
+    float yi = 0.f, ai = 0.f, gi_ = 0.f, yj = 0.f, aj = 0.f, gj = 0.f, Kjj = 0.f;
+    auto rdl = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      if (e == si) { yi = __shfl(y[e], i & 63, 64); ai = __shfl(a[e], i & 63, 64); gi_ = __shfl(g[e], i & 63, 64); }
-      if (e == sj) { yj = __shfl(y[e], j & 63, 64); aj = __shfl(a[e], j & 63, 64); gj = __shfl(g[e], j & 63, 64); }
+      if (e == si) { yi = rdl(y[e], i & 63); ai = rdl(a[e], i & 63); gi_ = rdl(g[e], i & 63); }
+      if (e == sj) { yj = rdl(y[e], j & 63); aj = rdl(a[e], j & 63); gj = rdl(g[e], j & 63); Kjj = rdl(qd[e], j & 63); }
     }
     const float oi = ai, oj = aj;
-    float quad = Kii + Ks[j][j] - 2.f * Ks[i][j];
+    float quad = Kii + Kjj - 2.f * Ks[i][j];
     quad = quad > 0.f ? quad : TAU;
     if (yi != yj) {
       const float delta = (-gi_ - gj) / quad, diff = ai - aj;
