@@ -819,6 +819,35 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
                      ok.data_ptr<bool>(), gap.data_ptr<float>(), cur_stream(y));
 }
 
+void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& ok, at::Tensor& alpha,
+                        const at::Tensor& G, const at::Tensor& y, const at::Tensor& gap, double C, double eps,
+                        int64_t max_iter, at::Tensor& dA, at::Tensor& inner_total) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&K, &alpha, &G, &y, &gap, &dA}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
+  const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
+  TORCH_CHECK(K.dim() == 3 && K.size(0) == B && K.size(1) == N && K.size(2) == N, "K must be [B, N, N]");
+  TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
+              "alpha / G must be [B, >= N]");
+  CHECK_DEV(ws);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DEV(ok);
+  CHECK_DTYPE(ok, at::kBool);
+  CHECK_DEV(inner_total);
+  CHECK_DTYPE(inner_total, at::kLong);
+  TORCH_CHECK(ws.numel() == B * Q && ok.numel() == B * Q && dA.numel() == B * Q, "ws / ok / dA must be [B, ", Q, "]");
+  TORCH_CHECK(gap.numel() == B && inner_total.numel() == B, "gap / inner_total must be [B]");
+  TORCH_CHECK(C > 0 && eps > 0 && max_iter >= 0, "bad SMO parameters");
+  DevGuard g(y.device());
+  avk::smo_ws_solve_fused(K.data_ptr<float>(), (int)N, reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()),
+                          ok.data_ptr<bool>(), alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(),
+                          (int)alpha.size(1), gap.data_ptr<float>(), (int)B, (float)C, (float)eps, (int)max_iter,
+                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
+                          cur_stream(y));
+}
+
 void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& dA, const at::Tensor& ok,
                    const at::Tensor& y, at::Tensor& G) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&K, &dA, &y, &G}) {
@@ -1227,6 +1256,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_ws_solve", &smo_ws_solve);
   m.def("smo_ws_select", &smo_ws_select);
   m.def("smo_ws_update", &smo_ws_update);
+  m.def("smo_ws_solve_fused", &smo_ws_solve_fused);
   m.def("smo_ws_size", &avk::smo_ws_size);
   m.def("nb_finalize", &nb_finalize);
   m.def("weighted_gram", &weighted_gram);

@@ -107,6 +107,9 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
                    long long* ws, bool* ok, float* gap, hipStream_t stream);
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                    int B, int N, int ldag, int Q, hipStream_t stream);
+void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
+                        const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
+                        long long* inner_total, hipStream_t stream);
 int smo_ws_size();
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream);

@@ -171,29 +171,11 @@ __global__ __launch_bounds__(SMO_THREADS) void smo_kernel(const float* __restric
 //   tolerance is max(eps, 0.1 gap)).
 constexpr int WS_Q = 128;
 
-__global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Kall, const float* __restrict__ yall,
-                                                    float* __restrict__ aall, const float* __restrict__ gall,
-                                                    const float* __restrict__ gap, float C, float eps, int max_iter,
-                                                    int* __restrict__ iters) {
-  constexpr int Q = WS_Q, E = Q / 64;
-  __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
-  const int b = blockIdx.x, lane = threadIdx.x;
-  const float* Kb = Kall + (long long)b * Q * Q;
-  for (int e = lane; e < Q * Q / 4; e += 64)
-    reinterpret_cast<float4*>(&Ks[0][0])[e] = reinterpret_cast<const float4*>(Kb)[e];
-  float y[E], a[E], g[E], qd[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int t = lane + 64 * e;
-    y[e] = yall[b * Q + t];
-    a[e] = aall[b * Q + t];
-    g[e] = gall[b * Q + t];
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int e = 0; e < E; ++e) qd[e] = Ks[lane + 64 * e][lane + 64 * e];
-  const float epsl = fmaxf(eps, 0.1f * gap[b]);
+// The SMO iterations of one Q-variable sub-problem, run by ONE wavefront: lane l owns variables
+// l + 64e; the Q x Q kernel block is in LDS.  Returns the iteration count.
+template <int E>
+__device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (&a)[E], float (&g)[E],
+                           const float (&qd)[E], float C, float epsl, int max_iter, int lane) {
   constexpr int NONE = 0x7fffffff;
   int it = 0;
   for (; it < max_iter; ++it) {
@@ -273,11 +255,88 @@ __global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Ka
       g[e] += y[e] * (Ks[i][t] * di + Ks[j][t] * dj);
     }
   }
+  return it;
+}
+
+__global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Kall, const float* __restrict__ yall,
+                                                    float* __restrict__ aall, const float* __restrict__ gall,
+                                                    const float* __restrict__ gap, float C, float eps, int max_iter,
+                                                    int* __restrict__ iters) {
+  constexpr int Q = WS_Q, E = Q / 64;
+  __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float* Kb = Kall + (long long)b * Q * Q;
+  for (int e = lane; e < Q * Q / 4; e += 64)
+    reinterpret_cast<float4*>(&Ks[0][0])[e] = reinterpret_cast<const float4*>(Kb)[e];
+  float y[E], a[E], g[E], qd[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = lane + 64 * e;
+    y[e] = yall[b * Q + t];
+    a[e] = aall[b * Q + t];
+    g[e] = gall[b * Q + t];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int e = 0; e < E; ++e) qd[e] = Ks[lane + 64 * e][lane + 64 * e];
+  const float epsl = fmaxf(eps, 0.1f * gap[b]);
+  const int it = ws_smo_loop<E>(Ks, y, a, g, qd, C, epsl, max_iter, lane);
 #pragma unroll
   for (int e = 0; e < E; ++e) aall[b * Q + lane + 64 * e] = a[e];
   if (lane == 0) iters[b] = it;
 }
 
+
+// smo_ws_solve_fused_kernel: the sub-problem solve with its gathers and scatters folded in: the
+// workgroup's 4 waves gather K[ws, ws] into LDS, wave 0 loads (y, alpha, G) of the working set,
+// runs ws_smo_loop, scatters the new alphas, writes dA = (alpha_new - alpha_old) y for the
+// gradient update and adds its iteration count to inner_total.
+__global__ __launch_bounds__(256) void smo_ws_solve_fused_kernel(const float* __restrict__ K, int N,
+                                                                 const long long* __restrict__ ws,
+                                                                 const bool* __restrict__ ok, float* __restrict__ alpha,
+                                                                 const float* __restrict__ G, const float* __restrict__ yv,
+                                                                 int ldag, const float* __restrict__ gap, float C,
+                                                                 float eps, int max_iter, float* __restrict__ dA,
+                                                                 long long* __restrict__ inner_total) {
+  constexpr int Q = WS_Q, E = Q / 64;
+  __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
+  __shared__ long long s_ws[Q];
+  __shared__ int s_ok[Q];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  for (int q = tid; q < Q; q += 256) {
+    const bool o = ok[(long long)b * Q + q];
+    s_ok[q] = o ? 1 : 0;
+    s_ws[q] = o ? ws[(long long)b * Q + q] : 0;
+  }
+  __syncthreads();
+  const float* Kb = K + (long long)b * N * N;
+  for (int e = tid; e < Q * Q; e += 256) Ks[e / Q][e % Q] = Kb[s_ws[e / Q] * N + s_ws[e % Q]];
+  __syncthreads();
+  if (tid >= 64) return;  // wave 0 solves; no block barrier follows
+  const int lane = tid;
+  float y[E], a[E], g[E], qd[E], a0[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = lane + 64 * e;
+    const long long n = s_ws[t];
+    y[e] = s_ok[t] ? yv[(long long)b * N + n] : 0.f;
+    a[e] = alpha[(long long)b * ldag + n];
+    g[e] = G[(long long)b * ldag + n];
+    a0[e] = a[e];
+    qd[e] = Ks[t][t];
+  }
+  float gp = gap[b];
+  if (!isfinite(gp)) gp = 0.f;
+  const int it = ws_smo_loop<E>(Ks, y, a, g, qd, C, fmaxf(eps, 0.1f * gp), max_iter, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = lane + 64 * e;
+    if (s_ok[t]) alpha[(long long)b * ldag + s_ws[t]] = a[e];
+    dA[(long long)b * Q + t] = (a[e] - a0[e]) * y[e];
+  }
+  if (lane == 0) inner_total[b] += it;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Working-set selection and gradient update for smo_decomposition, one launch each per outer
@@ -484,6 +543,15 @@ void smo_ws_update(const float* K, const long long* ws, const float* dA, const b
                    int B, int N, int ldag, int Q, hipStream_t stream) {
   if (B <= 0 || N <= 0) return;
   smo_ws_update_kernel<<<dim3((N + 255) / 256, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
+                        const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
+                        long long* inner_total, hipStream_t stream) {
+  if (B <= 0) return;
+  smo_ws_solve_fused_kernel<<<B, 256, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
+                                                   inner_total);
   AV_HIP_CHECK(hipGetLastError());
 }
 

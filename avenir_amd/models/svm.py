@@ -149,6 +149,7 @@ class _WorkingSetSMO:
         if self.fused:
             self.ws_buf = torch.zeros((B, Q), dtype=torch.long, device=dev)
             self.ok_buf = torch.zeros((B, Q), dtype=torch.bool, device=dev)
+            self.dA_buf = torch.zeros((B, Q), device=dev)
 
     def refresh_gap(self):
         a, g, yf = self.alpha[:, :self.N], self.G[:, :self.N], self.yf
@@ -161,20 +162,23 @@ class _WorkingSetSMO:
 
     def step(self):
         B, N, Q, h, dev = self.B, self.N, self.Q, self.h, self.K.device
-        if self.fused:
-            _native.C().smo_ws_select(self.alpha, self.G, self.yf, self.C, Q // 2, self.ws_buf, self.ok_buf, self.gap)
-            ws, ok = self.ws_buf, self.ok_buf
-        else:
-            vu, vl = self.refresh_gap()
-            vu_v, iu = torch.topk(vu, h, 1)
-            vl_v, il = torch.topk(vl, h, 1)
-            ws = torch.cat([iu, il], 1)
-            ok = torch.cat([vu_v > -float("inf"),
-                            (vl_v > -float("inf")) & ~(il.unsqueeze(2) == iu.unsqueeze(1)).any(2)], 1)
-            if ws.shape[1] < Q:                                                # N < Q/2: pad the set
-                pad = Q - ws.shape[1]
-                ws = torch.cat([ws, torch.zeros((B, pad), dtype=ws.dtype, device=dev)], 1)
-                ok = torch.cat([ok, torch.zeros((B, pad), dtype=torch.bool, device=dev)], 1)
+        if self.fused:  # three launches: select, solve (gathers / scatter folded in), gradient update
+            C_ = _native.C()
+            C_.smo_ws_select(self.alpha, self.G, self.yf, self.C, Q // 2, self.ws_buf, self.ok_buf, self.gap)
+            C_.smo_ws_solve_fused(self.K, self.ws_buf, self.ok_buf, self.alpha, self.G, self.yf, self.gap, self.C,
+                                  self.eps, self.inner_iter, self.dA_buf, self.inner_total)
+            C_.smo_ws_update(self.K, self.ws_buf, self.dA_buf, self.ok_buf, self.yf, self.G)
+            return
+        vu, vl = self.refresh_gap()
+        vu_v, iu = torch.topk(vu, h, 1)
+        vl_v, il = torch.topk(vl, h, 1)
+        ws = torch.cat([iu, il], 1)
+        ok = torch.cat([vu_v > -float("inf"),
+                        (vl_v > -float("inf")) & ~(il.unsqueeze(2) == iu.unsqueeze(1)).any(2)], 1)
+        if ws.shape[1] < Q:                                                # N < Q/2: pad the set
+            pad = Q - ws.shape[1]
+            ws = torch.cat([ws, torch.zeros((B, pad), dtype=ws.dtype, device=dev)], 1)
+            ok = torch.cat([ok, torch.zeros((B, pad), dtype=torch.bool, device=dev)], 1)
         wsg = torch.where(ok, ws, torch.zeros_like(ws))
         yws = (self.yp.gather(1, wsg) * ok).contiguous()
         aws = self.alpha.gather(1, wsg).contiguous()
