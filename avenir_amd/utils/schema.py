@@ -127,6 +127,18 @@ class FeatureSchema:
         if isinstance(obj, (str, Path)):
             p = Path(obj)
             obj = json.loads(p.read_text()) if p.exists() else json.loads(str(obj))
+        if "fields" not in obj and isinstance(obj.get("entity"), dict):
+            # sifarish / similarity format (e.g. resource/elearnActivity.json):
+            # {"distAlgorithm": ..., "entity": {"name": ..., "fields": [...]}}; every field that is
+            # neither the id nor the "classAttribute" is a feature
+            ent = obj["entity"]
+            fields = [FeatureField.from_json(d) for d in ent.get("fields", [])]
+            for f in fields:
+                if not f.id and not f.extra.get("classAttribute", False):
+                    f.feature = True
+            extra = {k: v for k, v in obj.items() if k != "entity"}
+            extra["entityName"] = ent.get("name")
+            return cls(fields, extra)
         fields = [FeatureField.from_json(d) for d in obj.get("fields", [])]
         return cls(fields, {k: v for k, v in obj.items() if k != "fields"})
 
@@ -142,6 +154,9 @@ class FeatureSchema:
 
     # -- chombo FeatureSchema API --------------------------------------------------------------
     def find_class_attr_field(self) -> FeatureField | None:
+        for f in self.fields:  # explicit "classAttribute": true (sifarish entity schemas)
+            if f.extra.get("classAttribute", False):
+                return f
         for f in self.fields:
             if not f.id and not f.feature and f.data_type != "string":
                 return f

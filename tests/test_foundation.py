@@ -109,3 +109,20 @@ def test_metrics():
     assert (cm.tp, cm.fp, cm.tn, cm.fn) == (1, 1, 1, 1) and cm.accuracy == 50
     assert math.isclose(roc_auc([0, 0, 1, 1], [0.1, 0.4, 0.35, 0.8]), 0.75)
     assert perf_metric("acc", [1, 0, 1], [1, 1, 1]) == pytest.approx(2 / 3)
+
+
+def test_schema_entity_format_with_class_attribute():
+    """sifarish-style schema (resource/elearnActivity.json layout): fields under "entity", every
+    non-id non-class field a feature, the class marked by "classAttribute"."""
+    from avenir_amd.utils.schema import FeatureSchema
+    d = {"distAlgorithm": "euclidean", "numericDiffThreshold": 0.2,
+         "entity": {"name": "studentActivity", "fields": [
+             {"name": "studentID", "ordinal": 0, "id": True, "dataType": "string"},
+             {"name": "contentTime", "ordinal": 1, "dataType": "int", "min": 0, "max": 600},
+             {"name": "emailCount", "ordinal": 2, "dataType": "int", "min": 0, "max": 20},
+             {"name": "status", "ordinal": 3, "dataType": "categorical", "classAttribute": True,
+              "cardinality": ["pass", "fail"]}]}}
+    s = FeatureSchema.from_json(d)
+    assert [f.name for f in s.feature_fields] == ["contentTime", "emailCount"]
+    assert s.find_class_attr_field().name == "status"
+    assert s.extra["entityName"] == "studentActivity" and s.extra["distAlgorithm"] == "euclidean"
