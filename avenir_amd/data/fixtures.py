@@ -263,9 +263,10 @@ def cust_value(n: int, seed=0) -> list[str]:
     return _rows(ids(rng, n, 8), gender, zc, fq, value)
 
 
-def elearn(n: int, seed=0) -> list[str]:
+def elearn(n: int, seed=0, as_int: bool = False) -> list[str]:
     """E-learning activity with a failure probability built from per-feature thresholds
-    (P/app/elearn.py:26-105).  Rows: user id, 9 activity features, P/F."""
+    (P/app/elearn.py:26-105).  Rows: user id, 9 activity features, P/F.  The script prints the
+    features as floats; ``as_int`` rounds them to the int fields of resource/elearnActivity.json."""
     rng = rng_of(seed)
     spec = [(300, 100), (80, 40), (40, 20), (10, 6), (50, 30), (60, 40), (100, 60), (60, 40), (12, 8)]
     f = [_tnorm(rng, m, s, n) for m, s in spec]
@@ -284,6 +285,8 @@ def elearn(n: int, seed=0) -> list[str]:
     p += np.where(f[8] < 4, 8, 0)
     status = np.where(rng.integers(0, 101, n) < p, "F", "P")
     uid = 1000000 + rng.integers(0, 1000001, n)
+    if as_int:
+        return _rows(_s(uid), *[_s(np.rint(c).astype(np.int64)) for c in f], status)
     return _rows(_s(uid), *[[repr(float(v)) for v in c] for c in f], status)
 
 

@@ -133,3 +133,8 @@ def test_ruby_generators_rates_and_pipeline():
     c, date = plan[0].split(", ")
     last = by[c][-1][0]
     assert int((np.datetime64(date) - last).astype(int)) in (15, 45, 90)
+
+
+def test_elearn_int_fields_for_entity_schema():
+    rows = [r.split(",") for r in F.elearn(50, seed=3, as_int=True)]
+    assert all(len(r) == 11 and all(v.lstrip("-").isdigit() for v in r[1:10]) and r[10] in "PF" for r in rows)
