@@ -278,6 +278,25 @@ def _markov(args):
     _write(args, m.model_lines(cfg.field_delim_out))
 
 
+@job("viterbiStatePredictor", "HMM state sequence per observation sequence (J/markov/ViterbiStatePredictor.java); --model <HMM lines>")
+def _viterbi(args):
+    """Rows ``id,obs,obs,...`` -> ``id,state,state,...`` (a token outside the model's observations
+    ends the sequence).  vsp.skip.field.count (default 1) leading fields are copied through."""
+    from .models.markov import HiddenMarkovModel, ViterbiDecoder
+    cfg = _cfg(args, "vsp.")
+    d = cfg.field_delim_in
+    skip = cfg.get_int("skip.field.count", 1)
+    hmm = HiddenMarkovModel.from_lines(_lines(args.model), d)
+    rows = [l.split(d) for l in _lines(args.input)]
+    oi = {o: i for i, o in enumerate(hmm.observations)}
+    obs = torch.full((len(rows), max([len(r) - skip for r in rows] + [1])), -1, dtype=torch.int16)
+    for r, row in enumerate(rows):
+        for j, tok in enumerate(row[skip:]):
+            obs[r, j] = oi.get(tok, -1)
+    paths = ViterbiDecoder(hmm).decode_labels(obs.to(_device(args)))
+    _write(args, [d.join(row[:skip] + p) for row, p in zip(rows, paths)])
+
+
 @job("genData", "tutorial fixture generator: --name <P/app script> --gen-args a,b,c [--seed s] (data/fixtures.py)")
 def _gen_data(args):
     from .data.fixtures import FIXTURES
