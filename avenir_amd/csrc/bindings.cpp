@@ -42,7 +42,8 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
                      int64_t total_bins, int64_t n_classes, at::Tensor& out, int64_t mode,
                      bool count_labels) {
   CHECK_DEV(codes);
-  CHECK_DTYPE(codes, at::kByte);
+  const bool wide = codes.scalar_type() == at::kUInt16;
+  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8 or uint16");
   TORCH_CHECK(codes.dim() == 2, "codes must be [F, ld]");
   const int64_t F = codes.size(0), ld = codes.size(1);
   TORCH_CHECK(n <= ld, "n exceeds codes leading dimension");
@@ -58,7 +59,8 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
   int64_t sum_bins = 0;
   std::vector<int> hb(F);
   for (int64_t f = 0; f < F; ++f) {
-    TORCH_CHECK(h_bins[f] > 0 && h_bins[f] <= 255, "bins per feature must be in [1,255]");
+    TORCH_CHECK(h_bins[f] > 0 && h_bins[f] <= (wide ? 65535 : 255),
+                wide ? "bins per feature must be in [1,65535]" : "bins per feature must be in [1,255]");
     hb[f] = (int)h_bins[f];
     sum_bins += h_bins[f];
   }
@@ -72,6 +74,13 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
     lab = labels->data_ptr<uint8_t>();
   }
   DevGuard g(codes.device());
+  if (wide) {
+    avk::class_histogram_wide(reinterpret_cast<const uint16_t*>(codes.data_ptr()), ld, n, lab, bins.data_ptr<int>(),
+                              offs.data_ptr<int>(), (int)F, (int)total_bins, (int)n_classes, count_labels ? 1 : 0,
+                              reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), (int)mode,
+                              cur_stream(codes));
+    return;
+  }
   avk::class_histogram(codes.data_ptr<uint8_t>(), ld, n, lab, bins.data_ptr<int>(),
                        offs.data_ptr<int>(), hb.data(), (int)F, (int)total_bins, (int)n_classes,
                        count_labels ? 1 : 0,
@@ -673,7 +682,7 @@ at::Tensor sample(int64_t dist, int64_t n, const at::Tensor& params, const c10::
 void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict, bool swap, at::Tensor& sol,
                at::Tensor& cur_cost, at::Tensor& best_sol, at::Tensor& best_cost, int64_t iters, double t0,
                double cool, int64_t interval, bool geometric, int64_t max_retry, int64_t seed, int64_t offset,
-               at::Tensor& stats) {
+               at::Tensor& stats, int64_t it_begin, double temp_start) {
   CHECK_DEV(cost);
   CHECK_DTYPE(cost, at::kFloat);
   TORCH_CHECK(cost.dim() == 2 && cost.size(1) >= 2, "cost must be [L, V>=2]");
@@ -694,7 +703,7 @@ void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict
   }
   CHECK_DEV(stats);
   CHECK_DTYPE(stats, at::kLong);
-  TORCH_CHECK(stats.numel() >= 3, "stats needs 3 entries");
+  TORCH_CHECK(stats.numel() >= 4, "stats needs 4 entries (3 counters + hand-off temperature)");
   const uint8_t* cf = nullptr;
   if (conflict.has_value() && conflict->defined()) {
     CHECK_DEV((*conflict));
@@ -706,7 +715,8 @@ void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict
   avk::sa_assign(cost.data_ptr<float>(), (int)L, (int)V, cf, swap ? 1 : 0, sol.data_ptr<int16_t>(), cur_cost.data_ptr<float>(),
                  best_sol.data_ptr<int16_t>(), best_cost.data_ptr<float>(), (int)P, (int)iters, (float)t0,
                  (float)cool, (int)interval, geometric ? 1 : 0, (int)max_retry, (unsigned long long)seed,
-                 (unsigned long long)offset, reinterpret_cast<unsigned long long*>(stats.data_ptr<int64_t>()),
+                 (unsigned long long)offset, (int)it_begin, (float)temp_start,
+                 reinterpret_cast<unsigned long long*>(stats.data_ptr<int64_t>()),
                  cur_stream(cost));
 }
 
@@ -1089,6 +1099,7 @@ py::tuple csv_parse(avh::CsvFile& f, py::list specs_py, int64_t row_begin, int64
     s.bucket_width = t[3].cast<double>();
     s.bucket_offset = t[4].cast<int>();
     s.max_code = t[5].cast<int>();
+    if (t.size() > 6) s.wide = t[6].cast<bool>();
     TORCH_CHECK(s.ordinal >= 0, "negative ordinal");
     if (s.kind == avh::BUCKET) TORCH_CHECK(s.bucket_width > 0, "bucket width must be > 0");
     specs.push_back(std::move(s));
@@ -1101,7 +1112,9 @@ py::tuple csv_parse(avh::CsvFile& f, py::list specs_py, int64_t row_begin, int64
   std::vector<void*> ptrs;
   for (auto& s : specs) {
     at::Tensor t;
-    if (s.kind == avh::CAT || s.kind == avh::BUCKET)
+    if ((s.kind == avh::CAT || s.kind == avh::BUCKET) && s.wide)
+      t = at::full({std::max<int64_t>(ld, 16)}, 65535, at::TensorOptions().dtype(at::kUInt16));
+    else if (s.kind == avh::CAT || s.kind == avh::BUCKET)
       t = at::full({std::max<int64_t>(ld, 16)}, 255, at::TensorOptions().dtype(at::kByte));
     else if (s.kind == avh::FLOAT)
       t = at::empty({n}, at::TensorOptions().dtype(at::kFloat));
@@ -1271,7 +1284,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_backward", &lstm_backward);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
-      .def(py::init<const std::string&, char, bool, int>(), py::arg("path"), py::arg("delim") = ',',
+      .def(py::init<const std::string&, const std::string&, bool, int>(), py::arg("path"), py::arg("delim") = ",",
            py::arg("skip_header") = false, py::arg("nthreads") = 8)
       .def("num_rows", &avh::CsvFile::num_rows)
       .def("max_fields", &avh::CsvFile::max_fields)

@@ -76,28 +76,37 @@ inline int64_t parse_int(std::string_view s, bool* ok) {
 
 struct CatLookup {
   std::vector<std::string> vocab;
-  std::unordered_map<std::string_view, uint8_t> map;
-  explicit CatLookup(const std::vector<std::string>& v) : vocab(v) {
-    if (vocab.size() > 255) throw std::runtime_error("categorical cardinality > 255 not supported");
-    for (size_t i = 0; i < vocab.size(); ++i) map.emplace(std::string_view(vocab[i]), (uint8_t)i);
+  std::unordered_map<std::string_view, uint16_t> map;
+  explicit CatLookup(const std::vector<std::string>& v, bool wide) : vocab(v) {
+    const size_t cap = wide ? 65535 : 255;
+    if (vocab.size() > cap)
+      throw std::runtime_error("categorical cardinality " + std::to_string(vocab.size()) + " exceeds the " +
+                               std::to_string(cap) + "-value code width");
+    for (size_t i = 0; i < vocab.size(); ++i) map.emplace(std::string_view(vocab[i]), (uint16_t)i);
   }
-  inline uint8_t code(std::string_view s) const {
+  // dictionary code, 65535 when unknown
+  inline uint16_t code(std::string_view s) const {
     s = trim(s);
     if (vocab.size() <= 8) {
       for (size_t i = 0; i < vocab.size(); ++i)
         if (s.size() == vocab[i].size() && std::memcmp(s.data(), vocab[i].data(), s.size()) == 0)
-          return (uint8_t)i;
-      return 255;
+          return (uint16_t)i;
+      return 65535;
     }
     auto it = map.find(s);
-    return it == map.end() ? 255 : it->second;
+    return it == map.end() ? 65535 : it->second;
   }
 };
 
+inline void store_code(void* out, int64_t r, bool wide, uint32_t code) {
+  if (wide) static_cast<uint16_t*>(out)[r] = (uint16_t)(code > 65535 ? 65535 : code);
+  else static_cast<uint8_t*>(out)[r] = (uint8_t)(code > 255 ? 255 : code);
+}
+
 }  // namespace
 
-CsvFile::CsvFile(const std::string& path, char delim, bool skip_header, int nthreads)
-    : delim_(delim), nthreads_(std::max(1, nthreads)) {
+CsvFile::CsvFile(const std::string& path, const std::string& delim, bool skip_header, int nthreads)
+    : delim_(delim.empty() ? std::string(",") : delim), nthreads_(std::max(1, nthreads)) {
   fd_ = ::open(path.c_str(), O_RDONLY);
   if (fd_ < 0) throw std::runtime_error("cannot open " + path);
   struct stat st;
@@ -115,6 +124,33 @@ CsvFile::CsvFile(const std::string& path, char delim, bool skip_header, int nthr
 CsvFile::~CsvFile() {
   if (data_) munmap(const_cast<char*>(data_), size_);
   if (fd_ >= 0) ::close(fd_);
+}
+
+void CsvFile::split(const char* p, const char* e, std::vector<std::string_view>& out, int max_fields) const {
+  out.clear();
+  const char* s = p;
+  if (delim_.size() == 1) {
+    const char d = delim_[0];
+    for (const char* q = p; q <= e; ++q) {
+      if (q == e || *q == d) {
+        out.emplace_back(s, (size_t)(q - s));
+        s = q + 1;
+        if (max_fields >= 0 && (int)out.size() >= max_fields) return;
+      }
+    }
+    return;
+  }
+  const size_t dl = delim_.size();
+  const char* q = p;
+  while (true) {
+    const char* hit = nullptr;
+    for (const char* c = q; c + dl <= e; ++c)
+      if (*c == delim_[0] && std::memcmp(c, delim_.data(), dl) == 0) { hit = c; break; }
+    if (!hit) { out.emplace_back(s, (size_t)(e - s)); return; }
+    out.emplace_back(s, (size_t)(hit - s));
+    if (max_fields >= 0 && (int)out.size() >= max_fields) return;
+    s = q = hit + dl;
+  }
 }
 
 void CsvFile::index_lines(bool skip_header) {
@@ -142,7 +178,13 @@ void CsvFile::index_lines(bool skip_header) {
           st[t].push_back((int64_t)p);
           en[t].push_back((int64_t)qe);
           int nf = 1;
-          for (size_t k = p; k < qe; ++k) nf += (data_[k] == delim_);
+          if (delim_.size() == 1) {
+            for (size_t k = p; k < qe; ++k) nf += (data_[k] == delim_[0]);
+          } else {
+            std::vector<std::string_view> f;
+            split(data_ + p, data_ + qe, f, -1);
+            nf = (int)f.size();
+          }
           mf[t] = std::max(mf[t], nf);
         }
         p = q + 1;
@@ -175,7 +217,7 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
   std::vector<std::unique_ptr<CatLookup>> cats(specs.size());
   int max_ord = 0;
   for (size_t i = 0; i < specs.size(); ++i) {
-    if (specs[i].kind == CAT) cats[i] = std::make_unique<CatLookup>(specs[i].vocab);
+    if (specs[i].kind == CAT) cats[i] = std::make_unique<CatLookup>(specs[i].vocab, specs[i].wide);
     max_ord = std::max(max_ord, specs[i].ordinal);
   }
   // ordinal -> list of spec indices
@@ -193,15 +235,7 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
       for (int64_t r = r0; r < r1; ++r) {
         const char* p = data_ + line_start_[base + r];
         const char* e = data_ + line_end_[base + r];
-        fields.clear();
-        const char* s = p;
-        for (const char* q = p; q <= e; ++q) {
-          if (q == e || *q == delim_) {
-            fields.emplace_back(s, (size_t)(q - s));
-            s = q + 1;
-            if ((int)fields.size() > max_ord) break;
-          }
-        }
+        split(p, e, fields, max_ord + 1);
         bool short_row = false;
         for (int o = 0; o <= max_ord; ++o) {
           if (by_ord[o].empty()) continue;
@@ -211,20 +245,20 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
             const ColSpec& sp = specs[si];
             switch (sp.kind) {
               case CAT: {
-                static_cast<uint8_t*>(outs[si])[r] = have ? cats[si]->code(fields[o]) : 255;
+                store_code(outs[si], r, sp.wide, have ? cats[si]->code(fields[o]) : 65535u);
                 break;
               }
               case BUCKET: {
-                uint8_t c = 255;
+                uint32_t c = 65535u;
                 if (have) {
                   const double v = parse_double(fields[o]);
                   if (!std::isnan(v)) {
                     // the reference uses integer division: Integer.parseInt(v) / bucketWidth
                     const long long b = (long long)std::floor(v / sp.bucket_width) - sp.bucket_offset;
-                    if (b >= 0 && b <= sp.max_code) c = (uint8_t)b;
+                    if (b >= 0 && b <= sp.max_code) c = (uint32_t)b;
                   }
                 }
-                static_cast<uint8_t*>(outs[si])[r] = c;
+                store_code(outs[si], r, sp.wide, c);
                 break;
               }
               case FLOAT: {
@@ -256,23 +290,14 @@ std::vector<std::string> CsvFile::distinct(int ordinal, size_t limit) {
   std::vector<std::string> out;
   std::unordered_map<std::string, int> seen;
   const int64_t n = num_rows();
+  std::vector<std::string_view> f;
   for (int64_t r = 0; r < n; ++r) {
-    std::string_view line(data_ + line_start_[r], (size_t)(line_end_[r] - line_start_[r]));
-    int f = 0;
-    size_t s = 0;
-    for (size_t q = 0; q <= line.size(); ++q) {
-      if (q == line.size() || line[q] == delim_) {
-        if (f == ordinal) {
-          std::string v(trim(line.substr(s, q - s)));
-          if (seen.emplace(v, 1).second) {
-            out.push_back(v);
-            if (out.size() >= limit) return out;
-          }
-          break;
-        }
-        ++f;
-        s = q + 1;
-      }
+    split(data_ + line_start_[r], data_ + line_end_[r], f, ordinal + 1);
+    if ((int)f.size() <= ordinal) continue;
+    std::string v(trim(f[ordinal]));
+    if (seen.emplace(v, 1).second) {
+      out.push_back(v);
+      if (out.size() >= limit) return out;
     }
   }
   return out;
@@ -281,17 +306,10 @@ std::vector<std::string> CsvFile::distinct(int ordinal, size_t limit) {
 std::vector<std::string> CsvFile::column_strings(int ordinal) {
   const int64_t n = num_rows();
   std::vector<std::string> out(n);
+  std::vector<std::string_view> f;
   for (int64_t r = 0; r < n; ++r) {
-    std::string_view line(data_ + line_start_[r], (size_t)(line_end_[r] - line_start_[r]));
-    int f = 0;
-    size_t s = 0;
-    for (size_t q = 0; q <= line.size(); ++q) {
-      if (q == line.size() || line[q] == delim_) {
-        if (f == ordinal) { out[r] = std::string(trim(line.substr(s, q - s))); break; }
-        ++f;
-        s = q + 1;
-      }
-    }
+    split(data_ + line_start_[r], data_ + line_end_[r], f, ordinal + 1);
+    if ((int)f.size() > ordinal) out[r] = std::string(trim(f[ordinal]));
   }
   return out;
 }

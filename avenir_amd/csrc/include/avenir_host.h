@@ -26,12 +26,15 @@ struct ColSpec {
   std::vector<std::string> vocab;  // CAT: known values, code = index (255 = unknown)
   double bucket_width = 1.0;       // BUCKET: code = (int)(v / width) - offset
   int bucket_offset = 0;
-  int max_code = 254;              // BUCKET: codes > max_code -> 255
+  int max_code = 254;              // BUCKET: codes > max_code -> missing
+  bool wide = false;               // CAT/BUCKET: uint16 codes (missing = 65535) for > 255 values
 };
 
 class CsvFile {
  public:
-  CsvFile(const std::string& path, char delim, bool skip_header, int nthreads);
+  // ``delim``: one character (fast path) or a multi-character literal separator (e.g. ",," of
+  // the reference's REST record lists).
+  CsvFile(const std::string& path, const std::string& delim, bool skip_header, int nthreads);
   ~CsvFile();
   int64_t num_rows() const { return (int64_t)line_start_.size(); }
   int max_fields() const { return max_fields_; }
@@ -49,10 +52,12 @@ class CsvFile {
 
  private:
   void index_lines(bool skip_header);
+  // split [p, e) at the delimiter into at most max_fields fields (all when max_fields < 0)
+  void split(const char* p, const char* e, std::vector<std::string_view>& out, int max_fields) const;
   const char* data_ = nullptr;
   size_t size_ = 0;
   int fd_ = -1;
-  char delim_;
+  std::string delim_;
   int nthreads_;
   int max_fields_ = 0;
   std::vector<int64_t> line_start_;

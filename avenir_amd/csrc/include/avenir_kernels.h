@@ -13,6 +13,10 @@ void class_histogram(const uint8_t* codes, long long ld, long long n, const uint
                      const int* d_bins, const int* d_offs, const int* h_bins, int nfeat,
                      int total_bins, int n_classes, int count_labels, unsigned long long* out,
                      int mode, hipStream_t stream);
+// ---- wide.hip: uint16 codes (> 255 values per field) -------------------------------------------
+void class_histogram_wide(const uint16_t* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins,
+                          const int* d_offs, int nfeat, int total_bins, int n_classes, int count_labels,
+                          unsigned long long* out, int mode, hipStream_t stream);
 void pair_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
                     const int* d_bins, const int* d_pairs, const long long* d_poff, int n_pairs,
                     int max_tab, int n_classes, unsigned long long* out, hipStream_t stream);
@@ -92,7 +96,7 @@ void sample(int dist, long long n, const float* params, const float* table, int 
 void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
                short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
                int geometric, int max_retry, unsigned long long seed, unsigned long long offset,
-               unsigned long long* stats, hipStream_t stream);
+               int it_begin, float temp_start, unsigned long long* stats, hipStream_t stream);
 
 // ---- linear.hip (K13) ----------------------------------------------------------------------
 int glm_grid(long long n);

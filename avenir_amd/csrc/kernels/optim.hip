@@ -31,7 +31,8 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
     const float* __restrict__ cost, int L, int V, const uint8_t* __restrict__ conflict, int swap,
     short* __restrict__ sol, float* __restrict__ cur_cost, short* __restrict__ best_sol,
     float* __restrict__ best_cost, int P, int iters, float t0, float cool, int interval, int geometric,
-    int max_retry, unsigned long long seed, unsigned long long offset, unsigned long long* __restrict__ stats) {
+    int max_retry, unsigned long long seed, unsigned long long offset, int it_begin, float temp_start,
+    unsigned long long* __restrict__ stats) {
   extern __shared__ short lds_sol[];
   const int lane = threadIdx.x;
   const int p = blockIdx.x * 64 + lane;
@@ -43,10 +44,12 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
   short* bs = best_sol + (long long)p * L;
   float c = cur_cost[p];
   float bc = best_cost[p];
-  float temp = t0;
+  // resumable: a run split into segments [it_begin, it_begin + iters) draws the same Philox counters
+  // and follows the same cooling schedule as one uninterrupted launch
+  float temp = temp_start;
   unsigned long long acc_better = 0, acc_worse = 0, rejected = 0;
   const float invL = 1.f / (float)L;
-  for (int it = 0; it < iters; ++it) {
+  for (int it = it_begin; it < it_begin + iters; ++it) {
     int pos = -1, nv = 0, old = 0, j2 = -1;
     for (int tr = 0; tr <= max_retry; ++tr) {
       const av::u4 r = av::philox_draw(seed, offset + (unsigned long long)it * (max_retry + 1) + tr,
@@ -94,6 +97,7 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
   cur_cost[p] = c;
   best_cost[p] = bc;
   if (stats) {
+    if (p == 0) stats[3] = (unsigned long long)__float_as_uint(temp);  // segment hand-off temperature
     atomicAdd(&stats[0], acc_better);
     atomicAdd(&stats[1], acc_worse);
     atomicAdd(&stats[2], rejected);
@@ -107,12 +111,12 @@ namespace avk {
 void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
                short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
                int geometric, int max_retry, unsigned long long seed, unsigned long long offset,
-               unsigned long long* stats, hipStream_t stream) {
+               int it_begin, float temp_start, unsigned long long* stats, hipStream_t stream) {
   if (P <= 0 || iters <= 0) return;
   const size_t lds = (size_t)L * 64 * sizeof(short);
   sa_assign_kernel<<<(P + 63) / 64, 64, lds, stream>>>(cost, L, V, conflict, swap, sol, cur_cost, best_sol,
                                                        best_cost, P, iters, t0, cool, interval, geometric, max_retry,
-                                                       seed, offset, stats);
+                                                       seed, offset, it_begin, temp_start, stats);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -35,7 +35,7 @@ static void test_csv(const std::string& dir) {
       f << i << "," << (i % 101 == 0 ? "mauve" : colors[i % 3]) << "," << (i % 50) << "," << (i * 0.5) << "\n";
     }
   }
-  avh::CsvFile csv(path, ',', true, 8);
+  avh::CsvFile csv(path, ",", true, 8);
   CHECK(csv.num_rows() == n);
   std::vector<avh::ColSpec> specs(3);
   specs[0].ordinal = 1; specs[0].kind = avh::CAT; specs[0].vocab = {"red", "green", "blue"};

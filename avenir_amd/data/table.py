@@ -4,7 +4,10 @@ A ``Table`` is the device-resident form of a CSV file described by a ``FeatureSc
 
 * ``codes``   uint8 ``[Fb, ld]`` — binned features (categorical dictionary codes, or int/double
   bucketized by ``bucketWidth``), feature-major (SoA) with ``ld`` a multiple of 16 so the HIP
-  kernels stream 16 rows per 128-bit load.  Unknown / missing values are coded 255.
+  kernels stream 16 rows per 128-bit load.  Unknown / missing values are coded 255.  When any
+  binned field has more than 255 values (the reference keys categoricals by raw string, so
+  high-cardinality fields such as supplier / product ids are legal) the table is *wide*: codes are
+  uint16 with 65535 = missing, counted by the K2w kernel (``wide.hip``).
 * ``numeric`` float32 ``[Fn, ld]`` — continuous (un-bucketized) numeric features.
 * ``labels``  uint8 ``[ld]`` — class attribute codes (255 = unknown).
 * ``ids``     list of record id strings (when the schema has an id field).
@@ -27,6 +30,42 @@ from ..utils.schema import FeatureField, FeatureSchema
 
 CAT, BUCKET, FLOAT, INT = 0, 1, 2, 3
 MISSING = 255
+MISSING16 = 65535
+
+
+def missing_code(codes: torch.Tensor) -> int:
+    """The 'missing / unknown' code of a code tensor (255 for uint8, 65535 for wide uint16)."""
+    return MISSING16 if codes.dtype == torch.uint16 else MISSING
+
+
+def needs_wide(fields) -> bool:
+    return any(f.num_bins > 255 for f in fields)
+
+
+_ESCAPED_LITERALS = {r"\t": "\t", r"\|": "|", r"\.": ".", r"\\": "\\", r"\$": "$", r"\^": "^"}
+
+
+def _literal(delim: str) -> str | None:
+    """The literal separator a ``field.delim.regex`` value denotes, or None for a real regex."""
+    import re
+    if delim in _ESCAPED_LITERALS:
+        return _ESCAPED_LITERALS[delim]
+    return delim if delim and re.escape(delim) == delim else None
+
+
+def split_regex(delim: str):
+    """A splitter for the reference's ``field.delim.regex`` (Java ``String.split(regex)``): plain
+    ``str.split`` for a literal separator (one or several characters, e.g. the ``,,`` of the REST
+    record lists), a compiled regex otherwise."""
+    import re
+    lit = _literal(delim)
+    if lit is not None:
+        return lambda s: s.split(lit)
+    return re.compile(delim).split
+
+
+def _is_regex(delim: str) -> bool:
+    return _literal(delim or ",") is None
 
 
 def pad16(n: int) -> int:
@@ -67,6 +106,14 @@ class Table:
         return out
 
     @property
+    def missing(self) -> int:
+        return missing_code(self.codes)
+
+    @property
+    def wide(self) -> bool:
+        return self.codes.dtype == torch.uint16
+
+    @property
     def total_bins(self) -> int:
         return int(sum(self.bins))
 
@@ -98,7 +145,7 @@ class Table:
         end = min(end, self.n)
         m = max(0, end - start)
         ld = pad16(m)
-        codes = torch.full((self.codes.shape[0], ld), MISSING, dtype=torch.uint8, device=self.device)
+        codes = torch.full((self.codes.shape[0], ld), self.missing, dtype=self.codes.dtype, device=self.device)
         codes[:, :m] = self.codes[:, start:end]
         num = torch.zeros((self.numeric.shape[0], ld), dtype=torch.float32, device=self.device)
         num[:, :m] = self.numeric[:, start:end]
@@ -115,7 +162,7 @@ class Table:
         idx = idx.to(self.device).long()
         m = int(idx.numel())
         ld = pad16(m)
-        codes = torch.full((self.codes.shape[0], ld), MISSING, dtype=torch.uint8, device=self.device)
+        codes = torch.full((self.codes.shape[0], ld), self.missing, dtype=self.codes.dtype, device=self.device)
         codes[:, :m] = self.codes[:, idx]
         num = torch.zeros((self.numeric.shape[0], ld), dtype=torch.float32, device=self.device)
         num[:, :m] = self.numeric[:, idx]
@@ -158,12 +205,13 @@ class Table:
 
 
 # ------------------------------------------------------------------------------------------------
-def _spec_for(f: FeatureField) -> tuple:
+def _spec_for(f: FeatureField, wide: bool = False) -> tuple:
+    top = 65534 if wide else 254
     if f.is_categorical:
-        return (f.ordinal, CAT, list(f.cardinality or []), 1.0, 0, 254)
+        return (f.ordinal, CAT, list(f.cardinality or []), 1.0, 0, top, wide)
     if f.is_bucketed:
-        return (f.ordinal, BUCKET, [], float(f.bucket_width), f.bucket_offset, min(254, f.num_bins - 1))
-    return (f.ordinal, FLOAT, [], 1.0, 0, 254)
+        return (f.ordinal, BUCKET, [], float(f.bucket_width), f.bucket_offset, min(top, f.num_bins - 1), wide)
+    return (f.ordinal, FLOAT, [], 1.0, 0, top, False)
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -196,14 +244,26 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         feats.sort(key=lambda f: f.ordinal)
     cls_f = (schema.find_field_by_ordinal(class_ordinal) if class_ordinal is not None
              else schema.find_class_attr_field())
+    C = _native.host()
+    use_native = C is not None and not _is_regex(delim)
+    csv = C.CsvFile(str(path), _literal(delim or ","), skip_header, nthreads) if use_native else None
+    # categorical fields without a schema cardinality: dictionary in first-seen order over the
+    # WHOLE file (identical on every rank), any size (uint16 codes above 255 values)
+    for f in feats:
+        if f.is_categorical and not f.cardinality:
+            if csv is not None:
+                f.cardinality = csv.distinct(f.ordinal, 65535)
+            else:
+                f.cardinality = _distinct_py(path, f.ordinal, delim, skip_header)
     binned = [f for f in feats if f.is_binned]
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
-    C = _native.host()
-    if C is not None:
-        csv = C.CsvFile(str(path), delim[0] if delim else ",", skip_header, nthreads)
+    wide = needs_wide(binned)
+    miss = MISSING16 if wide else MISSING
+    cdt = torch.uint16 if wide else torch.uint8
+    if csv is not None:
         total = csv.num_rows()
         r0, r1 = shard_range(total, rank, world)
-        specs = [_spec_for(f) for f in binned] + [_spec_for(f) for f in numeric]
+        specs = [_spec_for(f, wide) for f in binned] + [_spec_for(f) for f in numeric]
         if cls_f is not None:
             if not cls_f.cardinality:
                 cls_f.cardinality = csv.distinct(cls_f.ordinal, 255)
@@ -212,7 +272,7 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         n = r1 - r0
         ld = pad16(n)
         codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned
-                 else torch.zeros((0, ld), dtype=torch.uint8))
+                 else torch.zeros((0, ld), dtype=cdt))
         numc = cols[len(binned): len(binned) + len(numeric)]
         num = torch.zeros((len(numeric), ld), dtype=torch.float32)
         for i, c in enumerate(numc):
@@ -224,22 +284,23 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         if keep_lines or idf is not None:
             lines_all = csv.lines(r0, r1)
             if idf is not None:
-                ids = [ln.split(delim)[idf.ordinal] if ln else "" for ln in lines_all]
+                ids = csv.column_strings(idf.ordinal)[r0:r1]
             if keep_lines:
                 lines = lines_all
-    else:  # pure-Python fallback (slow; only when the native module is unavailable)
+    else:  # pure-Python path: regex delimiters, or no native module
         with open(path) as fh:
             all_lines = [ln.rstrip("\r\n") for ln in fh if ln.strip()]
         if skip_header:
             all_lines = all_lines[1:]
         r0, r1 = shard_range(len(all_lines), rank, world)
-        rows = [ln.split(delim) for ln in all_lines[r0:r1]]
+        splitter = split_regex(delim or ",")
+        rows = [splitter(ln) for ln in all_lines[r0:r1]]
         n = len(rows)
         ld = pad16(n)
-        codes = torch.full((len(binned), ld), MISSING, dtype=torch.uint8)
+        codes = torch.full((len(binned), ld), miss, dtype=cdt)
         for j, f in enumerate(binned):
-            codes[j, :n] = torch.tensor([_encode_py(f, r[f.ordinal] if f.ordinal < len(r) else "")
-                                         for r in rows], dtype=torch.uint8)
+            codes[j, :n] = torch.tensor([_encode_py(f, r[f.ordinal] if f.ordinal < len(r) else "", miss)
+                                         for r in rows], dtype=torch.int32).to(cdt)
         num = torch.zeros((len(numeric), ld), dtype=torch.float32)
         for j, f in enumerate(numeric):
             num[j, :n] = torch.tensor([_float(r[f.ordinal]) if f.ordinal < len(r) else math.nan
@@ -261,6 +322,19 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
     return t.to(device) if str(device) != "cpu" else t
 
 
+def _distinct_py(path, ordinal: int, delim: str, skip_header: bool) -> list[str]:
+    split = split_regex(delim or ",")
+    seen: dict[str, None] = {}
+    with open(path) as fh:
+        for i, ln in enumerate(fh):
+            if (skip_header and i == 0) or not ln.strip():
+                continue
+            r = split(ln.rstrip("\r\n"))
+            if ordinal < len(r):
+                seen.setdefault(r[ordinal].strip(), None)
+    return list(seen)
+
+
 def _float(s: str) -> float:
     try:
         return float(s)
@@ -268,18 +342,18 @@ def _float(s: str) -> float:
         return math.nan
 
 
-def _encode_py(f: FeatureField, s: str) -> int:
+def _encode_py(f: FeatureField, s: str, missing: int = MISSING) -> int:
     s = s.strip()
     if f.is_categorical:
         try:
             return f.cardinality.index(s)
         except ValueError:
-            return MISSING
+            return missing
     v = _float(s)
     if math.isnan(v):
-        return MISSING
+        return missing
     b = int(math.floor(v / f.bucket_width)) - f.bucket_offset
-    return b if 0 <= b < min(255, f.num_bins) else MISSING
+    return b if 0 <= b < min(missing, f.num_bins) else missing
 
 
 def from_arrays(schema: FeatureSchema, columns: dict[int, Sequence], device="cpu") -> Table:
@@ -290,10 +364,14 @@ def from_arrays(schema: FeatureSchema, columns: dict[int, Sequence], device="cpu
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
     n = len(next(iter(columns.values())))
     ld = pad16(n)
-    codes = torch.full((len(binned), ld), MISSING, dtype=torch.uint8)
+    wide = needs_wide(binned)
+    miss = MISSING16 if wide else MISSING
+    codes = torch.full((len(binned), ld), miss, dtype=torch.uint16 if wide else torch.uint8)
     for j, f in enumerate(binned):
-        codes[j, :n] = torch.tensor([_encode_py(f, str(v)) for v in columns[f.ordinal]],
-                                    dtype=torch.uint8)
+        lut = {v: i for i, v in enumerate(f.cardinality)} if f.is_categorical else None
+        vals = ([lut.get(str(v).strip(), miss) for v in columns[f.ordinal]] if lut is not None
+                else [_encode_py(f, str(v), miss) for v in columns[f.ordinal]])
+        codes[j, :n] = torch.tensor(vals, dtype=torch.int32).to(codes.dtype)
     num = torch.zeros((len(numeric), ld), dtype=torch.float32)
     for j, f in enumerate(numeric):
         num[j, :n] = torch.tensor(np.asarray(columns[f.ordinal], dtype=np.float32))

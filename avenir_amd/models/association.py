@@ -19,6 +19,7 @@ import torch
 
 from .. import _native
 from ..parallel.comm import Comm, get_comm
+from ..utils.resilience import IterationLoop, RecoveryConfig
 
 
 def _popcount64(x: torch.Tensor) -> torch.Tensor:
@@ -70,10 +71,12 @@ class FrequentItemsets:
 
 
 class Apriori:
-    def __init__(self, support_threshold: float = 0.1, max_len: int = 5, comm: Comm | None = None):
+    def __init__(self, support_threshold: float = 0.1, max_len: int = 5, comm: Comm | None = None,
+                 recovery: RecoveryConfig | None = None):
         self.threshold = support_threshold
         self.max_len = max_len
         self.comm = comm
+        self.recovery = recovery        # per-level checkpoint / resume (utils/resilience)
 
     def fit_transactions(self, transactions: list[list[str]], device="cpu", tx_base: int = 0,
                          items: list[str] | None = None) -> FrequentItemsets:
@@ -114,44 +117,73 @@ class Apriori:
         levels = {1: freq}
         P = bits[[s[0][0] for s in freq]] if freq else bits[:0]
         k = 1
+        lp = IterationLoop("apriori", self.recovery, comm, device=bits.device)
+        _, st, meta = lp.restore(bits.device)
+        if st is not None:                  # resume after level ``meta['k']``: rebuild the level
+            k = int(meta["k"])              # lists and the prefix bitsets of the last level
+            levels = {}
+            for j in range(1, k + 1):
+                if f"l{j}_sets" not in st:
+                    continue
+                sets_t, sup_t = st[f"l{j}_sets"].tolist(), st[f"l{j}_sup"].tolist()
+                levels[j] = [(tuple(a), b) for a, b in zip(sets_t, sup_t)]
+            freq = levels.get(k, [])
+            P = bits[[s[-1] for s, _ in freq]] if freq else bits[:0]
+            if freq:
+                idx = torch.tensor([s for s, _ in freq], dtype=torch.long, device=bits.device)
+                for c in range(k - 1):
+                    P = P & bits[idx[:, c]]
         while freq and k < self.max_len:
             k += 1
-            sets = [s for s, _ in freq]
-            setidx = {s: j for j, s in enumerate(sets)}
-            cp, ci, cands = [], [], []
-            # join (k-1)-sets sharing their first k-2 items; prune by the Apriori property
-            by_pref: dict[tuple, list[int]] = {}
-            for j, s in enumerate(sets):
-                by_pref.setdefault(s[:-1], []).append(j)
-            for grp in by_pref.values():
-                for a, b in itertools.combinations(grp, 2):
-                    sa, sb = sets[a], sets[b]
-                    cand = sa + (sb[-1],) if sa[-1] < sb[-1] else sb + (sa[-1],)
-                    if any(sub not in setidx for sub in itertools.combinations(cand, k - 1)):
-                        continue
-                    base = a if sa[-1] < sb[-1] else b
-                    cp.append(base)
-                    ci.append(cand[-1])
-                    cands.append(cand)
-            if not cands:
-                break
-            dev = bits.device
-            cpt = torch.tensor(cp, dtype=torch.int32, device=dev)
-            cit = torch.tensor(ci, dtype=torch.int32, device=dev)
-            sup = itemset_support(P, bits, cpt, cit)
-            if comm.is_distributed:
-                comm.all_reduce(sup)
-            sup_l = sup.cpu().tolist()
-            keep = [m for m in range(len(cands)) if sup_l[m] > min_count]
-            freq = [(cands[m], sup_l[m]) for m in keep]
-            if freq:
-                kt = torch.tensor(keep, dtype=torch.long, device=dev)
-                P = P[cpt.long()[kt]] & bits[cit.long()[kt]]
-                order = sorted(range(len(freq)), key=lambda m: freq[m][0])
-                freq = [freq[m] for m in order]
-                P = P[torch.tensor(order, dtype=torch.long, device=dev)]
-                levels[k] = freq
+            with lp.step(k):
+                sets = [s for s, _ in freq]
+                setidx = {s: j for j, s in enumerate(sets)}
+                cp, ci, cands = [], [], []
+                # join (k-1)-sets sharing their first k-2 items; prune by the Apriori property
+                by_pref: dict[tuple, list[int]] = {}
+                for j, s in enumerate(sets):
+                    by_pref.setdefault(s[:-1], []).append(j)
+                for grp in by_pref.values():
+                    for a, b in itertools.combinations(grp, 2):
+                        sa, sb = sets[a], sets[b]
+                        cand = sa + (sb[-1],) if sa[-1] < sb[-1] else sb + (sa[-1],)
+                        if any(sub not in setidx for sub in itertools.combinations(cand, k - 1)):
+                            continue
+                        base = a if sa[-1] < sb[-1] else b
+                        cp.append(base)
+                        ci.append(cand[-1])
+                        cands.append(cand)
+                if not cands:
+                    break
+                dev = bits.device
+                cpt = torch.tensor(cp, dtype=torch.int32, device=dev)
+                cit = torch.tensor(ci, dtype=torch.int32, device=dev)
+                sup = itemset_support(P, bits, cpt, cit)
+                if comm.is_distributed:
+                    comm.all_reduce(sup)
+                sup_l = sup.cpu().tolist()
+                keep = [m for m in range(len(cands)) if sup_l[m] > min_count]
+                freq = [(cands[m], sup_l[m]) for m in keep]
+                if freq:
+                    kt = torch.tensor(keep, dtype=torch.long, device=dev)
+                    P = P[cpt.long()[kt]] & bits[cit.long()[kt]]
+                    order = sorted(range(len(freq)), key=lambda m: freq[m][0])
+                    freq = [freq[m] for m in order]
+                    P = P[torch.tensor(order, dtype=torch.long, device=dev)]
+                    levels[k] = freq
+            if lp.enabled:
+                lp.commit(k, _levels_state(levels), {"k": k})
+        lp.close()
         return FrequentItemsets(items, levels, N)
+
+
+def _levels_state(levels) -> dict[str, torch.Tensor]:
+    out = {}
+    for j, lv in levels.items():
+        out[f"l{j}_sets"] = (torch.tensor([e[0] for e in lv], dtype=torch.long) if lv
+                             else torch.zeros((0, j), dtype=torch.long))
+        out[f"l{j}_sup"] = torch.tensor([e[1] for e in lv], dtype=torch.long)
+    return out
 
 
 def association_rules(fi: FrequentItemsets, conf_threshold: float = 0.5, min_len: int = 2):

@@ -198,28 +198,29 @@ class NaiveBayes:
         conf = (torch.zeros((C, C), dtype=torch.int64, device=t.device)
                 if validate and t.labels is not None else None)
         has_x = t.numeric.shape[0] > 0
-        if t.device.type == "cuda":
+        if t.device.type == "cuda" and not t.wide:
             _native.C().nb_predict(t.codes, n, offs, tb["logp"], tb["logfp"],
                                    t.numeric if has_x else None,
                                    tb["gmean"] if has_x else None, tb["ginvstd"] if has_x else None,
                                    tb["glognorm"] if has_x else None, tb["pmean"] if has_x else None,
                                    tb["pinvstd"] if has_x else None, tb["plognorm"] if has_x else None,
                                    tb["logprior"], bool(ref_scale), post, pred, t.labels, conf)
-        else:
+        else:   # CPU oracle; also wide (uint16-code) tables on the GPU, as batched torch gathers
             self._predict_ref(t, tb, ref_scale, post, pred, conf)
         return NBPrediction(pred[:n], None if post is None else post[:n], conf)
 
     def _predict_ref(self, t: Table, tb: dict, ref_scale: bool, post, pred, conf) -> None:
         n, C = t.n, self.n_classes
         s = tb["logprior"].view(1, C).expand(n, C).clone()
-        lfp = torch.zeros(n)
+        lfp = torch.zeros(n, device=s.device)
+        zero = torch.zeros(1, device=s.device)
         o = 0
         for f, b in enumerate(self.bins):
             v = t.codes[f, :n].long()
             ok = v < b
             vv = torch.where(ok, v, torch.zeros_like(v)) + o
-            s += torch.where(ok.unsqueeze(1), tb["logp"][:, vv].T, torch.zeros(1))
-            lfp += torch.where(ok, tb["logfp"][vv], torch.zeros(1))
+            s += torch.where(ok.unsqueeze(1), tb["logp"][:, vv].T, zero)
+            lfp += torch.where(ok, tb["logfp"][vv], zero)
             o += b
         if t.numeric.shape[0]:
             x = t.numeric[:, :n].T  # [n, Fc]

@@ -23,6 +23,7 @@ import torch
 from .. import _native
 from ..ops import distance as dist
 from ..parallel.comm import Comm, get_comm
+from ..utils.resilience import IterationLoop, RecoveryConfig
 
 
 @dataclass
@@ -91,7 +92,8 @@ def kmeans_step(X: torch.Tensor, Cs: list[torch.Tensor], want_assign: bool = Fal
 
 class KMeans:
     def __init__(self, n_clusters: int | list[int] = 3, n_init: int = 1, max_iter: int = 300,
-                 tol: float = 1e-4, init: str = "k-means++", seed: int = 0, comm: Comm | None = None):
+                 tol: float = 1e-4, init: str = "k-means++", seed: int = 0, comm: Comm | None = None,
+                 recovery: RecoveryConfig | None = None):
         self.ks = [n_clusters] if isinstance(n_clusters, int) else list(n_clusters)
         self.n_init = n_init
         self.max_iter = max_iter
@@ -99,6 +101,7 @@ class KMeans:
         self.init = init
         self.seed = seed
         self.comm = comm
+        self.recovery = recovery           # checkpoint / resume per Lloyd iteration (utils/resilience)
         self.runs: list[KMeansRun] = []
         self.best: dict[int, KMeansRun] = {}
 
@@ -195,32 +198,48 @@ class KMeans:
         specs = [(k, self.seed * 1009 + k * 31 + r) for k in self.ks for r in range(self.n_init)]
         runs = [KMeansRun(k, sd, self._init_centroids(X, k, sd)) for k, sd in specs]
         self.best = {}
-        for grp in self._groups(specs, Xp.shape[1] if Xp is not None else None):
-            if Xp is not None:
-                self._fit_gpu_group(X.shape[1], Xp, [runs[i] for i in grp], comm)
-            else:
-                self._fit_cpu_group(X, [runs[i] for i in grp], comm)
+        for gi, grp in enumerate(self._groups(specs, Xp.shape[1] if Xp is not None else None)):
+            with IterationLoop(f"kmeans.g{gi}", self.recovery, comm, device=X.device) as lp:
+                if Xp is not None:
+                    self._fit_gpu_group(X.shape[1], Xp, [runs[i] for i in grp], comm, lp)
+                else:
+                    self._fit_cpu_group(X, [runs[i] for i in grp], comm, lp)
         self.runs = runs
         for r in runs:
             if r.k not in self.best or r.sse < self.best[r.k].sse:
                 self.best[r.k] = r
         return self
 
-    def _fit_gpu_group(self, D: int, Xp: torch.Tensor, grp: list[KMeansRun], comm) -> None:
+    def _fit_gpu_group(self, D: int, Xp: torch.Tensor, grp: list[KMeansRun], comm,
+                       lp: IterationLoop) -> None:
         C = _native.C()
         lay = _PairLayout([r.centroids for r in grp], Xp.shape[1])
         R = len(grp)
         frozen_h = [0] * R
         frozen = torch.zeros(R, dtype=torch.uint8, device=Xp.device)
         hist: list[tuple[int, torch.Tensor]] = []
-        for it in range(self.max_iter):
-            partial, ssep, _ = C.kmeans_assign(Xp, lay.C2, lay.Cn, lay.roff, lay.h_roff, False)
-            flat = C.kmeans_reduce(partial, ssep)
-            if comm.is_distributed:
-                flat = comm.all_reduce(flat)
-            moves = C.kmeans_update(flat, lay.C2, lay.Cn, lay.run_of, frozen, lay.Dp)
-            hist.append((it, flat[-R:]))
-            mv = moves.cpu().tolist()                  # the one host sync of the iteration
+        it0, st, _ = lp.restore(Xp.device)
+        if st is not None:                              # resume: centroids, status, SSE history
+            lay.C2.copy_(st["C2"])
+            lay.Cn.copy_(st["Cn"])
+            frozen_h = [int(v) for v in st["frozen"].tolist()]
+            frozen.copy_(st["frozen"])
+            hist = [(i, st["hist"][i]) for i in range(st["hist"].shape[0])]
+            for r, run in enumerate(grp):
+                run.iterations = int(st["iters"][r])
+                run.converged = bool(frozen_h[r])
+        nbytes = float(Xp.numel() * 4)
+        for it in range(it0, self.max_iter):
+            if all(frozen_h):
+                break
+            with lp.step(it, nbytes=nbytes):
+                partial, ssep, _ = C.kmeans_assign(Xp, lay.C2, lay.Cn, lay.roff, lay.h_roff, False)
+                flat = C.kmeans_reduce(partial, ssep)
+                if comm.is_distributed:
+                    flat = comm.all_reduce(flat)
+                moves = C.kmeans_update(flat, lay.C2, lay.Cn, lay.run_of, frozen, lay.Dp)
+                hist.append((it, flat[-R:]))
+                mv = moves.cpu().tolist()                  # the one host sync of the iteration
             changed = False
             for r, run in enumerate(grp):
                 if frozen_h[r]:
@@ -230,11 +249,13 @@ class KMeans:
                     run.converged = True
                     frozen_h[r] = 1
                     changed = True
-            if all(frozen_h):
-                break
             if changed:
                 frozen.copy_(torch.tensor(frozen_h, dtype=torch.uint8))
-        sse_hist = torch.stack([h for _, h in hist]).cpu()
+            if lp.enabled:
+                lp.commit(it, {"C2": lay.C2, "Cn": lay.Cn, "frozen": frozen,
+                               "iters": torch.tensor([r.iterations for r in grp]),
+                               "hist": torch.stack([h for _, h in hist])})
+        sse_hist = torch.stack([h for _, h in hist]).cpu() if hist else torch.zeros((0, R), dtype=torch.float64)
         for r, run in enumerate(grp):
             run.history = [float(sse_hist[i, r]) for i in range(run.iterations)]
             run.centroids = lay.centroids(r, D)
@@ -246,10 +267,21 @@ class KMeans:
             _, counts, sse = lay.stats(flat, r, D)
             run.sse, run.counts = float(sse), counts.round().long()
 
-    def _fit_cpu_group(self, X: torch.Tensor, grp: list[KMeansRun], comm) -> None:
+    def _fit_cpu_group(self, X: torch.Tensor, grp: list[KMeansRun], comm, lp: IterationLoop) -> None:
         active = list(range(len(grp)))
-        for it in range(self.max_iter):
-            res = self._step(X, [grp[i].centroids for i in active])
+        it0, st, _ = lp.restore(X.device)
+        if st is not None:
+            for r, run in enumerate(grp):
+                run.centroids = st[f"c{r}"].to(X.device)
+                run.iterations = int(st["iters"][r])
+                run.converged = bool(st["done"][r])
+                run.history = st[f"h{r}"].tolist()
+            active = [r for r in range(len(grp)) if not grp[r].converged]
+        for it in range(it0, self.max_iter):
+            if not active:
+                break
+            with lp.step(it):
+                res = self._step(X, [grp[i].centroids for i in active])
             if comm.is_distributed:
                 flat = torch.cat([torch.cat([s.view(-1), c.double().view(-1), e]) for s, c, e in res])
                 flat = comm.all_reduce(flat)
@@ -275,8 +307,12 @@ class KMeans:
                 else:
                     still.append(i)
             active = still
-            if not active:
-                break
+            if lp.enabled:
+                state = {f"c{r}": run.centroids for r, run in enumerate(grp)}
+                state.update({f"h{r}": torch.tensor(run.history, dtype=torch.float64) for r, run in enumerate(grp)})
+                state["iters"] = torch.tensor([run.iterations for run in grp])
+                state["done"] = torch.tensor([run.converged for run in grp])
+                lp.commit(it, state)
         final = self._step(X, [r.centroids for r in grp])
         for run, (sums, counts, sse) in zip(grp, final):
             if comm.is_distributed:

@@ -306,12 +306,13 @@ def apply_encoding(t: Table, enc: dict[int, dict[str, float]], default: float = 
     for j, f in enumerate(t.binned_fields):
         if f.ordinal not in enc:
             continue
-        lut = torch.full((256,), default, dtype=torch.float32, device=t.device)
-        for k in range(f.num_bins):
-            lab = f.bin_label(k)
-            if lab in enc[f.ordinal]:
-                lut[k] = enc[f.ordinal][lab]
-        cols.append(lut[t.codes[j, : t.n].long()])
+        # one slot per code incl. the missing code (255, or 65535 for wide tables)
+        lut = torch.full((t.missing + 1,), default, dtype=torch.float64)
+        e = enc[f.ordinal]
+        ks = [k for k in range(f.num_bins) if f.bin_label(k) in e]
+        if ks:
+            lut[torch.tensor(ks)] = torch.tensor([e[f.bin_label(k)] for k in ks], dtype=torch.float64)
+        cols.append(lut.float().to(t.device)[t.codes[j, : t.n].long()])
     return torch.stack(cols, 1) if cols else torch.zeros((t.n, 0), device=t.device)
 
 
@@ -330,8 +331,9 @@ def leave_one_out_encoding(t: Table, target: torch.Tensor, noise: float = 0.0, r
     gmean = gsum / gcnt
     for j, f in enumerate(t.binned_fields):
         c = t.codes[j, :n].long()
-        s = torch.zeros(256, dtype=torch.float64, device=y.device).index_add_(0, c, y)
-        k = torch.zeros(256, dtype=torch.float64, device=y.device).index_add_(0, c, torch.ones_like(y))
+        m = t.missing + 1
+        s = torch.zeros(m, dtype=torch.float64, device=y.device).index_add_(0, c, y)
+        k = torch.zeros(m, dtype=torch.float64, device=y.device).index_add_(0, c, torch.ones_like(y))
         _reduce(comm, s, k)
         v = (s[c] - y + reg * gmean) / (k[c] - 1 + reg).clamp_min(1e-12)
         if noise > 0:

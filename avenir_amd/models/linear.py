@@ -29,6 +29,7 @@ import torch
 
 from .. import _native
 from ..parallel.comm import Comm, get_comm
+from ..utils.resilience import IterationLoop, RecoveryConfig
 
 MODE_LOGISTIC, MODE_SQUARED, MODE_HINGE = 0, 1, 2
 
@@ -114,8 +115,9 @@ def _converged(prev: torch.Tensor, cur: torch.Tensor, criteria: str, threshold: 
 class LogisticRegression:
     def __init__(self, solver: str = "newton", lr: float = 1.0, max_iter: int = 25, l2: float = 0.0,
                  intercept: bool = True, criteria: str = "averageBelowThreshold", threshold: float = 0.01,
-                 tol: float = 1e-8, comm: Comm | None = None):
+                 tol: float = 1e-8, comm: Comm | None = None, recovery: RecoveryConfig | None = None):
         self.solver, self.lr, self.max_iter, self.l2 = solver, lr, max_iter, l2
+        self.recovery = recovery
         self.intercept, self.criteria, self.threshold, self.tol = intercept, criteria, threshold, tol
         self.comm = comm
         self.coef: torch.Tensor | None = None
@@ -132,37 +134,58 @@ class LogisticRegression:
         n_tot = float(comm.all_reduce(n_tot)) if comm.is_distributed else float(n_tot)
         w = torch.zeros((D,), dtype=torch.float64, device=data.device) if self.coef is None else self.coef.double().clone()
         self.history = [w.tolist()]
-        for it in range(self.max_iter):
-            g, loss, h = glm_gradient(data, yy, w.float(), MODE_LOGISTIC, sw, want_h=self.solver == "newton")
-            g = g[:D].double().clone()
-            buf = torch.cat([g, loss.view(1).double()])
-            if self.solver == "newton":
-                if data.device.type == "cuda" and D <= 32:
-                    H = _native.C().weighted_gram(data.X, data.n, D, h.contiguous())   # MFMA Gram
-                else:
-                    Xr = data.X[:D, : data.n]
-                    H = (Xr * h.view(1, -1)) @ Xr.T                               # [D, D] GEMM
-                buf = torch.cat([buf, H.double().reshape(-1)])
-            if comm.is_distributed:
-                buf = comm.all_reduce(buf)
-            g, loss = buf[:D], float(buf[D])
-            if self.l2:
-                g = g - self.l2 * w * n_tot
-                loss += 0.5 * self.l2 * n_tot * float((w * w).sum())
-            self.losses.append(loss / n_tot)
-            prev = w.clone()
-            if self.solver == "newton":
-                H = buf[D + 1:].view(D, D) + (self.l2 * n_tot + 1e-9 * n_tot) * torch.eye(D, dtype=torch.float64, device=w.device)
-                w = w + torch.linalg.solve(H, g)
-            else:
-                w = w + self.lr * g / n_tot
-            self.history.append(w.tolist())
-            if float(g.abs().max()) / n_tot < self.tol:
+        lp = IterationLoop("logistic", self.recovery, comm, device=data.device)
+        it0, st, _ = lp.restore(data.device)
+        if st is not None:       # the coefficient history is the reference's per-iteration state file
+            self.history = st["history"].tolist()
+            self.losses = st["losses"].tolist()
+            w = st["history"][-1].to(data.device)
+            if bool(st["done"]):
+                it0 = self.max_iter
+        for it in range(it0, self.max_iter):
+            with lp.step(it, nbytes=float(data.X.numel() * 4)):
+                w, stop = self._iterate(data, yy, sw, w, D, n_tot, comm)
+            if lp.enabled:
+                lp.commit(it, {"history": torch.tensor(self.history, dtype=torch.float64),
+                               "losses": torch.tensor(self.losses, dtype=torch.float64),
+                               "done": torch.tensor(stop)})
+            if stop:
                 break
-            if self.criteria != "iterLimit" and _converged(prev, w, self.criteria, self.threshold):
-                break
+        lp.close()
         self.coef = w
         return self
+
+    def _iterate(self, data, yy, sw, w, D, n_tot, comm):
+        """One gradient / Newton iteration -> (new weights, converged)."""
+        g, loss, h = glm_gradient(data, yy, w.float(), MODE_LOGISTIC, sw, want_h=self.solver == "newton")
+        g = g[:D].double().clone()
+        buf = torch.cat([g, loss.view(1).double()])
+        if self.solver == "newton":
+            if data.device.type == "cuda" and D <= 32:
+                H = _native.C().weighted_gram(data.X, data.n, D, h.contiguous())   # MFMA Gram
+            else:
+                Xr = data.X[:D, : data.n]
+                H = (Xr * h.view(1, -1)) @ Xr.T                               # [D, D] GEMM
+            buf = torch.cat([buf, H.double().reshape(-1)])
+        if comm.is_distributed:
+            buf = comm.all_reduce(buf)
+        g, loss = buf[:D], float(buf[D])
+        if self.l2:
+            g = g - self.l2 * w * n_tot
+            loss += 0.5 * self.l2 * n_tot * float((w * w).sum())
+        self.losses.append(loss / n_tot)
+        prev = w.clone()
+        if self.solver == "newton":
+            H = buf[D + 1:].view(D, D) + (self.l2 * n_tot + 1e-9 * n_tot) * torch.eye(D, dtype=torch.float64, device=w.device)
+            w = w + torch.linalg.solve(H, g)
+        else:
+            w = w + self.lr * g / n_tot
+        self.history.append(w.tolist())
+        if float(g.abs().max()) / n_tot < self.tol:
+            return w, True
+        if self.criteria != "iterLimit" and _converged(prev, w, self.criteria, self.threshold):
+            return w, True
+        return w, False
 
     def decision_function(self, X) -> torch.Tensor:
         data = X if isinstance(X, DenseSoA) else DenseSoA(X, self.intercept, device=self.coef.device)

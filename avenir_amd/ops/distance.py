@@ -155,7 +155,7 @@ def encode_mixed(t: Table, weights: dict[int, float] | None = None, ranges: dict
             cols.append(oh)
         else:
             b = max(f.num_bins - 1, 1)
-            cols.append((torch.where(c >= MISSING, torch.zeros_like(c), c).float() / b * math.sqrt(w)).unsqueeze(1))
+            cols.append((torch.where(c >= t.missing, torch.zeros_like(c), c).float() / b * math.sqrt(w)).unsqueeze(1))
     if not cols:
         return torch.zeros((n, 0), device=t.device)
     return torch.cat(cols, 1).contiguous()

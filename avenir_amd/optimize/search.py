@@ -32,6 +32,7 @@ import torch
 from .. import _native
 from ..ops.random import philox4x32, u32_to_unit
 from ..parallel.comm import Comm, get_comm
+from ..utils.resilience import IterationLoop, RecoveryConfig
 from .domain import AssignmentDomain, SearchDomain
 
 
@@ -68,8 +69,11 @@ class SimulatedAnnealing:
     def __init__(self, domain: SearchDomain, n_chains: int = 8, iters: int = 300, t0: float = 30.0,
                  cooling: float = 0.99, geometric: bool = True, interval: int = 2, step: int = 1,
                  max_retry: int = 3, seed: int = 0, locally_optimize: bool = False, local_iters: int = 50,
-                 comm: Comm | None = None, use_kernel: bool | None = None):
+                 comm: Comm | None = None, use_kernel: bool | None = None,
+                 recovery: RecoveryConfig | None = None, segment: int | None = None):
         self.domain = domain
+        self.recovery = recovery        # checkpoint / resume (utils/resilience)
+        self.segment = segment          # moves per checkpointed segment (default iters / 10)
         self.n_chains, self.iters, self.t0, self.cooling = n_chains, iters, t0, cooling
         self.geometric, self.interval, self.step, self.max_retry = geometric, interval, step, max_retry
         self.seed, self.locally_optimize, self.local_iters = seed, locally_optimize, local_iters
@@ -99,22 +103,64 @@ class SimulatedAnnealing:
         cost = d.evaluate(sol)
         kernel_ok = isinstance(d, AssignmentDomain) and self.step == 1 and d.L <= 512
         use_kernel = kernel_ok if self.use_kernel is None else (self.use_kernel and kernel_ok)
-        if use_kernel:
-            best, bc, stats = sa_assign(d, sol, cost, self.iters, self.t0, self.cooling, self.interval,
-                                        self.geometric, self.max_retry, seed, 0)
-        else:
-            best, bc, stats = self._generic(sol, cost, gen)
+        with IterationLoop("simulatedAnnealing", self.recovery, comm, sharded=True, device=d.device) as lp:
+            if use_kernel and not lp.enabled:
+                best, bc, stats = sa_assign(d, sol, cost, self.iters, self.t0, self.cooling, self.interval,
+                                            self.geometric, self.max_retry, seed, 0)
+            elif use_kernel:
+                best, bc, stats = self._segmented(lp, sol, cost, seed)
+            else:
+                best, bc, stats = self._generic(sol, cost, gen, lp)
         if self.locally_optimize:
             best, bc = local_focussed(d, best, bc, self.local_iters, gen)
         b, c = _global_best(comm, bc, best)
         return OptResult(b, c, bc, best, stats=stats)
 
-    def _generic(self, sol, cost, gen):
+    def _segmented(self, lp: IterationLoop, sol, cost, seed):
+        """Kernel path under checkpointing: the run is split into segments of ``segment`` moves
+        (one launch each, same Philox counters and cooling schedule as one launch); every segment
+        commits the chains' current / best solutions, temperature and counters (one file per
+        rank: chains are rank-local)."""
+        d = self.domain
+        seg = max(1, self.segment or -(-self.iters // 10))
+        best = bc = temp = None
+        stats = {"better": 0, "worse_accepted": 0, "rejected": 0}
+        b0 = 0
+        _, st, meta = lp.restore(d.device)
+        if st is not None:
+            sol, cost, best, bc = st["sol"], st["cost"], st["best"], st["best_cost"]
+            temp, b0, stats = float(meta["temp"]), int(meta["moves"]), dict(meta["stats"])
+        for b in range(b0, self.iters, seg):
+            n = min(seg, self.iters - b)
+            with lp.step(b // seg):
+                best, bc, s, sol, cost, temp = sa_assign(d, sol, cost, n, self.t0, self.cooling, self.interval,
+                                                         self.geometric, self.max_retry, seed, 0, it_begin=b,
+                                                         temp_start=temp, best=best, best_cost=bc,
+                                                         return_state=True)
+            for k in stats:
+                stats[k] += s[k]
+            lp.commit(b // seg, {"sol": sol, "cost": cost, "best": best, "best_cost": bc},
+                      {"temp": temp, "moves": b + n, "stats": stats}, force=True)
+        if best is None:                       # resumed after the last segment
+            best, bc = st["best"], st["best_cost"]
+        return best, bc, stats
+
+    def _generic(self, sol, cost, gen, lp: IterationLoop | None = None):
         d = self.domain
         best, bc = sol.clone(), cost.clone()
         temp = self.t0
         stats = {"better": 0, "worse_accepted": 0, "rejected": 0}
-        for it in range(self.iters):
+        it0 = 0
+        if lp is not None:
+            it0, st, meta = lp.restore(d.device)
+            if st is not None:
+                sol, cost, best, bc = st["sol"], st["cost"], st["best"], st["best_cost"]
+                gen.set_state(st["rng"])
+                temp, stats = float(meta["temp"]), dict(meta["stats"])
+        for it in range(it0, self.iters):
+            if lp is not None:
+                with lp.step(it):
+                    pass
             cand, _ = d.mutate(sol, self.step, gen, self.max_retry)
             cc = d.evaluate(cand)
             delta = cc - cost
@@ -130,47 +176,67 @@ class SimulatedAnnealing:
             bc = torch.minimum(bc, cost)
             if self.interval > 0 and (it + 1) % self.interval == 0:
                 temp = temp * self.cooling if self.geometric else max(self.t0 - (it + 1) * self.cooling, 1e-12)
+            if lp is not None and lp.enabled:
+                lp.commit(it, {"sol": sol, "cost": cost, "best": best, "best_cost": bc, "rng": gen.get_state()},
+                          {"temp": temp, "stats": stats})
         return best, bc, stats
 
 
 def sa_assign(d: AssignmentDomain, sol: torch.Tensor, cost: torch.Tensor, iters: int, t0: float, cool: float,
-              interval: int, geometric: bool, max_retry: int, seed: int, offset: int):
+              interval: int, geometric: bool, max_retry: int, seed: int, offset: int, it_begin: int = 0,
+              temp_start: float | None = None, best: torch.Tensor | None = None, best_cost: torch.Tensor | None = None,
+              return_state: bool = False):
     """Run ``sol.shape[0]`` SA chains over an assignment domain: K22 kernel on GPU, the bit-exact
-    numpy mirror (same Philox stream, float32 arithmetic) on CPU.  Returns (best_sol, best_cost, stats)."""
+    numpy mirror (same Philox stream, float32 arithmetic) on CPU.  Returns (best_sol, best_cost, stats)
+    or, with ``return_state``, also (current_sol, current_cost, temperature) so a run split into
+    segments [it_begin, it_begin + iters) (checkpoint / resume) equals one uninterrupted launch."""
+    ts = float(t0 if temp_start is None else temp_start)
     if sol.device.type == "cuda":
         s16 = sol.to(torch.int16).contiguous()
         cur = cost.float().contiguous().clone()
-        best = s16.clone()
-        bc = cur.clone()
-        st = torch.zeros(3, dtype=torch.long, device=sol.device)
+        bsol = s16.clone() if best is None else best.to(torch.int16).contiguous().clone()
+        bc = cur.clone() if best_cost is None else best_cost.float().contiguous().clone()
+        st = torch.zeros(4, dtype=torch.long, device=sol.device)
         _native.C().sa_assign(d.cost_table, None if d.conflict is None else d.conflict.to(torch.uint8).contiguous(),
-                              bool(d.swap_moves), s16, cur, best, bc, int(iters), float(t0), float(cool),
-                              int(interval), bool(geometric), int(max_retry), int(seed), int(offset), st)
+                              bool(d.swap_moves), s16, cur, bsol, bc, int(iters), float(t0), float(cool),
+                              int(interval), bool(geometric), int(max_retry), int(seed), int(offset), st,
+                              int(it_begin), ts)
         s = st.tolist()
-        return best.long(), bc, {"better": s[0], "worse_accepted": s[1], "rejected": s[2]}
-    b, c, s = sa_assign_reference(d.cost_table.numpy(), None if d.conflict is None else d.conflict.numpy(),
-                                  d.swap_moves, sol.numpy(), cost.float().numpy(), iters, t0, cool, interval,
-                                  geometric, max_retry, seed, offset)
+        stats = {"better": s[0], "worse_accepted": s[1], "rejected": s[2]}
+        if return_state:
+            temp = float(np.array([s[3]], dtype=np.uint32).view(np.float32)[0]) if iters > 0 else ts
+            return bsol.long(), bc, stats, s16.long(), cur, temp
+        return bsol.long(), bc, stats
+    out = sa_assign_reference(d.cost_table.numpy(), None if d.conflict is None else d.conflict.numpy(),
+                              d.swap_moves, sol.numpy(), cost.float().numpy(), iters, t0, cool, interval,
+                              geometric, max_retry, seed, offset, it_begin, ts,
+                              None if best is None else best.numpy(), None if best_cost is None else best_cost.float().numpy())
+    b, c, s, cs, cc, temp = out
+    if return_state:
+        return (torch.from_numpy(b).long(), torch.from_numpy(c), s, torch.from_numpy(cs).long(),
+                torch.from_numpy(cc), float(temp))
     return torch.from_numpy(b).long(), torch.from_numpy(c), s
 
 
-def sa_assign_reference(cost, conflict, swap, sol, cur, iters, t0, cool, interval, geometric, max_retry, seed, offset):
-    """Host mirror of ``sa_assign_kernel`` (optim.hip), vectorised over chains."""
+def sa_assign_reference(cost, conflict, swap, sol, cur, iters, t0, cool, interval, geometric, max_retry, seed, offset,
+                        it_begin=0, temp_start=None, best=None, best_cost=None):
+    """Host mirror of ``sa_assign_kernel`` (optim.hip), vectorised over chains.  Returns
+    (best, best_cost, stats, current_sol, current_cost, temperature)."""
     cost = np.asarray(cost, np.float32)
     L, V = cost.shape
     sol = np.array(sol, dtype=np.int64)
     P = sol.shape[0]
     c = np.array(cur, dtype=np.float32)
-    bc = c.copy()
-    best = sol.copy()
+    bc = c.copy() if best_cost is None else np.array(best_cost, dtype=np.float32)
+    best = sol.copy() if best is None else np.array(best, dtype=np.int64)
     rows = np.arange(P)
     idx = np.arange(P, dtype=np.uint64)
     ar = np.arange(L)
     invL = np.float32(1.0 / L)
-    temp = np.float32(t0)
+    temp = np.float32(t0 if temp_start is None else temp_start)
     st = [0, 0, 0]
     R = max_retry + 1
-    for it in range(iters):
+    for it in range(it_begin, it_begin + iters):
         pending = np.ones(P, bool)
         pos = np.full(P, -1)
         nv = np.zeros(P, np.int64)
@@ -228,7 +294,8 @@ def sa_assign_reference(cost, conflict, swap, sol, cur, iters, t0, cool, interva
         bc = np.where(imp, c, bc)
         if interval > 0 and (it + 1) % interval == 0:
             temp = np.float32(temp * np.float32(cool)) if geometric else np.float32(max(t0 - (it + 1) * cool, 1e-12))
-    return best, bc.astype(np.float32), {"better": st[0], "worse_accepted": st[1], "rejected": st[2]}
+    return (best, bc.astype(np.float32), {"better": st[0], "worse_accepted": st[1], "rejected": st[2]},
+            sol, c.astype(np.float32), temp)
 
 
 def local_focussed(d: SearchDomain, sols: torch.Tensor, costs: torch.Tensor, n_iter: int, gen=None):
@@ -272,8 +339,10 @@ class GeneticAlgorithm:
 
     def __init__(self, domain: SearchDomain, islands: int = 4, pool: int = 10, mating: int = 5, replacement: int = 5,
                  generations: int = 100, purge_first: bool = True, mutate_children: bool = True,
-                 migrate_every: int = 0, seed: int = 0, comm: Comm | None = None):
+                 migrate_every: int = 0, seed: int = 0, comm: Comm | None = None,
+                 recovery: RecoveryConfig | None = None):
         self.d = domain
+        self.recovery = recovery        # per-generation checkpoint / resume (utils/resilience)
         self.I, self.Pp, self.m, self.r, self.G = islands, pool, mating, replacement, generations
         self.purge_first, self.mutate_children, self.migrate_every = purge_first, mutate_children, migrate_every
         self.seed, self.comm = seed, comm
@@ -295,41 +364,56 @@ class GeneticAlgorithm:
         pop, cost = pop.view(I, Pp, L), cost.view(I, Pp)
         history = []
         ii = torch.arange(I, device=d.device).view(-1, 1)
-        for g in range(self.G):
-            order = cost.argsort(1)
-            pop, cost = pop[ii, order], cost[ii, order]
-            history.append(float(cost[:, 0].min()))
-            # children: 2x oversampled pairs from the mating list, first r valid per island
-            npair = self.r
-            a = (torch.rand((I, npair), generator=gen, device=d.device) * self.m).long().clamp_max(self.m - 1)
-            b = (torch.rand((I, npair), generator=gen, device=d.device) * (self.m - 1)).long().clamp_max(max(self.m - 2, 0))
-            b = b + (b >= a).long()
-            pa, pb = pop[ii, a].view(-1, L), pop[ii, b.clamp_max(Pp - 1)].view(-1, L)
-            c1, c2 = d.crossover(pa, pb, gen)
-            kids = torch.cat([c1.view(I, npair, L), c2.view(I, npair, L)], 1).view(-1, L)
-            if self.mutate_children:
-                kids, _ = d.mutate(kids, 1, gen)
-            kc = d.evaluate(kids).view(I, 2 * npair)
-            kids = kids.view(I, 2 * npair, L)
-            ko = kc.argsort(1)[:, : self.r]                              # best r children (valid first)
-            kids, kc = kids[ii, ko], kc[ii, ko]
-            if self.purge_first:
-                pop = torch.cat([pop[:, : Pp - self.r], kids], 1)
-                cost = torch.cat([cost[:, : Pp - self.r], kc], 1)
-            else:
-                allp, allc = torch.cat([pop, kids], 1), torch.cat([cost, kc], 1)
-                o = allc.argsort(1)[:, :Pp]
-                pop, cost = allp[ii, o], allc[ii, o]
-            if self.migrate_every and I > 1 and (g + 1) % self.migrate_every == 0:
-                bi = cost.argmin(1)
-                elite, ec = pop[ii.view(-1), bi], cost[ii.view(-1), bi]
-                wi = cost.argmax(1)
-                pop[ii.view(-1), wi] = elite.roll(1, 0)
-                cost[ii.view(-1), wi] = ec.roll(1, 0)
+        lp = IterationLoop("geneticAlgorithm", self.recovery, comm, sharded=True, device=d.device)
+        g0, st, meta = lp.restore(d.device)
+        if st is not None:                  # islands are rank-local: one checkpoint per rank
+            pop, cost = st["pop"], st["cost"]
+            gen.set_state(st["rng"])
+            history = list(meta["history"])
+        for g in range(g0, self.G):
+            with lp.step(g):
+                pop, cost = self._generation(g, pop, cost, gen, history, ii)
+            if lp.enabled:
+                lp.commit(g, {"pop": pop, "cost": cost, "rng": gen.get_state()}, {"history": history})
+        lp.close()
         bi = cost.argmin(1)
         bs, bc = pop[ii.view(-1), bi], cost[ii.view(-1), bi]
         b, c = _global_best(comm, bc, bs)
         return OptResult(b, c, bc, bs, history)
+
+    def _generation(self, g, pop, cost, gen, history, ii):
+        d, I, Pp, L = self.d, self.I, self.Pp, self.d.L
+        order = cost.argsort(1)
+        pop, cost = pop[ii, order], cost[ii, order]
+        history.append(float(cost[:, 0].min()))
+        # children: 2x oversampled pairs from the mating list, first r valid per island
+        npair = self.r
+        a = (torch.rand((I, npair), generator=gen, device=d.device) * self.m).long().clamp_max(self.m - 1)
+        b = (torch.rand((I, npair), generator=gen, device=d.device) * (self.m - 1)).long().clamp_max(max(self.m - 2, 0))
+        b = b + (b >= a).long()
+        pa, pb = pop[ii, a].view(-1, L), pop[ii, b.clamp_max(Pp - 1)].view(-1, L)
+        c1, c2 = d.crossover(pa, pb, gen)
+        kids = torch.cat([c1.view(I, npair, L), c2.view(I, npair, L)], 1).view(-1, L)
+        if self.mutate_children:
+            kids, _ = d.mutate(kids, 1, gen)
+        kc = d.evaluate(kids).view(I, 2 * npair)
+        kids = kids.view(I, 2 * npair, L)
+        ko = kc.argsort(1)[:, : self.r]                              # best r children (valid first)
+        kids, kc = kids[ii, ko], kc[ii, ko]
+        if self.purge_first:
+            pop = torch.cat([pop[:, : Pp - self.r], kids], 1)
+            cost = torch.cat([cost[:, : Pp - self.r], kc], 1)
+        else:
+            allp, allc = torch.cat([pop, kids], 1), torch.cat([cost, kc], 1)
+            o = allc.argsort(1)[:, :Pp]
+            pop, cost = allp[ii, o], allc[ii, o]
+        if self.migrate_every and I > 1 and (g + 1) % self.migrate_every == 0:
+            bi = cost.argmin(1)
+            elite, ec = pop[ii.view(-1), bi], cost[ii.view(-1), bi]
+            wi = cost.argmax(1)
+            pop[ii.view(-1), wi] = elite.roll(1, 0)
+            cost[ii.view(-1), wi] = ec.roll(1, 0)
+        return pop, cost
 
 
 class EvolutionaryOptimizer:

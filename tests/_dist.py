@@ -52,3 +52,37 @@ def run_world(fn, world: int, *args, timeout: float = 120.0):
             if p.is_alive():
                 p.kill()
     return [out[r] for r in range(world)]
+
+
+def _worker_env(rank, world, port, fn, args, q, env):
+    os.environ.update(env or {})
+    _worker(rank, world, port, fn, args, q)
+
+
+def run_world_outcome(fn, world: int, *args, env: dict | None = None, timeout: float = 120.0):
+    """Like ``run_world`` but tolerant of failing ranks (fault-injection tests): returns
+    ``(results_by_rank, errors_by_rank, exitcodes)``; every rank process is fresh (spawn)."""
+    import queue as _queue
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker_env, args=(r, world, port, fn, args, q, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, errs = {}, {}
+    import time as _t
+    deadline = _t.monotonic() + timeout
+    while len(res) + len(errs) < world and _t.monotonic() < deadline:
+        try:
+            rank, status, payload = q.get(timeout=1.0)
+        except _queue.Empty:
+            if all(not p.is_alive() for p in procs) and q.empty():
+                break
+            continue
+        (res if status == "ok" else errs)[rank] = payload
+    for p in procs:
+        p.join(timeout=10)
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=10)
+    return res, errs, [p.exitcode for p in procs]

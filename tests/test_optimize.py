@@ -70,7 +70,7 @@ def test_sa_reference_consistent():
     assert ok.all()
     cost = d.cost(sol)
     best, bc, st = sa_assign_reference(d.cost_table.numpy(), d.conflict.numpy(), True, sol.numpy(), cost.numpy(),
-                                       400, 5.0, 0.98, 2, True, 3, 11, 0)
+                                       400, 5.0, 0.98, 2, True, 3, 11, 0)[:3]
     bt = torch.from_numpy(best)
     # incremental cost bookkeeping agrees with a full re-evaluation; best solutions are valid
     assert torch.allclose(d.cost(bt), torch.from_numpy(bc), atol=1e-3)
@@ -244,7 +244,7 @@ def test_sa_kernel_matches_reference(cuda):
     sol, ok = d.random(256, torch.Generator().manual_seed(9))
     cost = d.cost(sol)
     rb, rc, rs = sa_assign_reference(d.cost_table.numpy(), d.conflict.numpy(), True, sol.numpy(), cost.numpy(),
-                                     300, 4.0, 0.98, 3, True, 3, 1234, 0)
+                                     300, 4.0, 0.98, 3, True, 3, 1234, 0)[:3]
     dg = d.to(cuda)
     gb, gc, gs = sa_assign(dg, sol.to(cuda), cost.to(cuda), 300, 4.0, 0.98, 3, True, 3, 1234, 0)
     same = (gb.cpu().numpy() == rb).all(1)
@@ -262,3 +262,34 @@ def test_sa_kernel_task_schedule(cuda, task_domain):
     r = SimulatedAnnealing(d, n_chains=4096, iters=500, t0=2.0, cooling=0.98, interval=4).run()
     assert r.best.device.type == "cuda"
     assert r.best_cost == pytest.approx(lb, abs=1e-3)
+
+
+def _sa_segments(d, sol, cost, seg, total=300):
+    """Run ``total`` SA moves as segments of ``seg`` moves chained through the returned state."""
+    best = bc = None
+    temp = None
+    cur, cc = sol, cost
+    for b in range(0, total, seg):
+        best, bc, _, cur, cc, temp = sa_assign(d, cur, cc, min(seg, total - b), 4.0, 0.98, 3, True, 3, 1234, 0,
+                                               it_begin=b, temp_start=temp, best=best, best_cost=bc,
+                                               return_state=True)
+    return best, bc
+
+
+def test_sa_segments_equal_one_run():
+    d = _random_assignment(L=20, V=8, seed=5)
+    sol, _ = d.random(64, torch.Generator().manual_seed(2))
+    cost = d.cost(sol)
+    b1, c1 = _sa_segments(d, sol, cost, 300)
+    b2, c2 = _sa_segments(d, sol, cost, 70)
+    assert torch.equal(b1, b2) and torch.equal(c1, c2)
+
+
+@pytest.mark.gpu
+def test_sa_kernel_segments_equal_one_run(cuda):
+    d = _random_assignment(L=40, V=12, seed=7).to(cuda)
+    sol, _ = d.random(256, torch.Generator(device=cuda).manual_seed(9))
+    cost = d.cost(sol)
+    b1, c1 = _sa_segments(d, sol, cost, 300)
+    b2, c2 = _sa_segments(d, sol, cost, 64)
+    assert torch.equal(b1, b2) and torch.equal(c1, c2)
