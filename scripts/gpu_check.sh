@@ -6,7 +6,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 echo "== pytest -m gpu"
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread 2>&1 | tee gpurun_out/pytest_gpu.log
+timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread 2>&1 | tee gpurun_out/pytest_gpu.log
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log
 echo "== bench"

@@ -137,4 +137,9 @@ def test_wide_encoding_gpu_matches_cpu(cuda, tmp_path):
     assert a.keys() == b.keys()
     for k in a:
         da, db = dict(a[k]), dict(b[k])
-        assert all(abs(da[v] - db[v]) < 1e-9 or (math.isnan(da[v]) and math.isnan(db[v])) for v in db)
+        # odds ratios are +inf where a value never occurs with the negative class: compare with
+        # equality first (inf == inf), then relatively, then NaN-to-NaN
+        assert all(da[v] == db[v] or math.isclose(da[v], db[v], rel_tol=1e-12)
+                   or (math.isnan(da[v]) and math.isnan(db[v])) for v in db)
+    cg = H.class_histogram(tg.codes, tg.n, tg.bins, tg.labels, tg.n_classes)
+    assert torch.equal(cg.cpu(), H.class_histogram(t.codes, t.n, t.bins, t.labels, t.n_classes))
