@@ -1081,6 +1081,33 @@ at::Tensor dot_matrix(const at::Tensor& A, const at::Tensor& B) {
   return hits;
 }
 
+// K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
+// are joined with every row whose (k-1)-prefix equals their (k-1)-suffix -> int32 [M, k+1].
+at::Tensor gsp_join(const at::Tensor& X, int64_t lo, int64_t hi) {
+  CHECK_DEV(X);
+  CHECK_DTYPE(X, at::kInt);
+  TORCH_CHECK(X.dim() == 2 && X.size(1) >= 2, "X [N, k], k >= 2");
+  const int64_t N = X.size(0), k = X.size(1);
+  TORCH_CHECK(N < (1LL << 31) && 0 <= lo && lo <= hi && hi <= N, "bad left range");
+  const int64_t n = hi - lo;
+  auto opt = X.options();
+  if (n == 0) return at::empty({0, k + 1}, opt);
+  DevGuard g(X.device());
+  auto start = at::empty({n}, opt);
+  auto len = at::empty({n}, opt);
+  avk::gsp_count(X.data_ptr<int>(), (int)N, (int)k, (int)lo, (int)hi, start.data_ptr<int>(), len.data_ptr<int>(),
+                 cur_stream(X));
+  auto len64 = len.to(at::kLong);
+  auto incl = at::cumsum(len64, 0);
+  const int64_t M = incl[n - 1].item<int64_t>();
+  auto offs = (incl - len64).contiguous();
+  auto out = at::empty({M, k + 1}, opt);
+  if (M > 0)
+    avk::gsp_emit(X.data_ptr<int>(), (int)k, (int)lo, (int)hi, start.data_ptr<int>(), len.data_ptr<int>(),
+                  reinterpret_cast<const long long*>(offs.data_ptr<int64_t>()), out.data_ptr<int>(), cur_stream(X));
+  return out;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host runtime
 
@@ -1279,6 +1306,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("ngram_count", &ngram_count);
   m.def("uniformization", &uniformization);
   m.def("dot_matrix", &dot_matrix);
+  m.def("gsp_join", &gsp_join);
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);

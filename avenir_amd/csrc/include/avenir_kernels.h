@@ -145,6 +145,11 @@ void uniformization(const double* P, int S, const double* w1, const double* w2, 
                     double* out, hipStream_t stream);
 void dot_matrix(const int* A, int n, int Wa, const int* B, int m, int Wb, int* hits, hipStream_t stream);
 
+// gsp.hip (K18 GSP candidate self-join over a lexicographically sorted [N, k] sequence matrix)
+void gsp_count(const int* X, int N, int k, int lo, int hi, int* seg_start, int* seg_len, hipStream_t stream);
+void gsp_emit(const int* X, int k, int lo, int hi, const int* seg_start, const int* seg_len, const long long* offs,
+              int* out, hipStream_t stream);
+
 // ---- rnn.hip (K27 persistent LSTM recurrence, bf16 MFMA) -------------------------------------
 // KS = HP / 32 (HP = hidden size padded to 32, 64 or 128), IS = IP / 32 likewise for the layer
 // input size, RT = 16-sequence tiles per workgroup.

@@ -1,0 +1,280 @@
+"""Shared plumbing of the CLI jobs: registry, config, sharded text input, rank-aware output.
+
+Every reference job is launched as ``<class> -Dconf.path=<props> in out`` (Hadoop) or
+``<object> in out <hocon>`` (Spark, ``getCommandLineArgs(args, 3)``, e.g.
+S/util/LinearMapper.scala:40-99).  Here a job is a function ``fn(ctx)`` registered under the
+reference's job name; ``ctx`` (a :class:`JobContext`) carries the typed config (``.properties``
+with the job's key prefix, or the HOCON app block), the input shard of this rank and the output
+writer.
+
+Distributed semantics (one process per GPU under ``torchrun``; RCCL collectives):
+
+* map-only jobs (predictors, samplers, transforms) read a contiguous block of the input lines
+  per rank and write their own ``part-NNNNN`` file (Hadoop's one-file-per-mapper) when the output
+  is a directory, or gather their lines to rank 0 (rank order) when it is a single file;
+* reducing jobs (models, statistics) build dense partial tensors per rank, all-reduce them once
+  and write from rank 0 only.
+"""
+from __future__ import annotations
+
+import json
+import sys
+from collections import Counter
+from pathlib import Path
+from typing import Callable, Iterable, Sequence
+
+import torch
+
+JOBS: dict[str, tuple[Callable, str]] = {}
+
+
+def job(name: str, help_: str, aliases: Sequence[str] = ()):
+    def deco(fn):
+        JOBS[name] = (fn, help_)
+        for a in aliases:
+            JOBS[a] = (fn, f"alias of {name}")
+        return fn
+    return deco
+
+
+def parse_defines(defs: Sequence[str] | None) -> dict[str, str]:
+    """``-D key=value`` overrides (Hadoop's generic ``-D`` option)."""
+    out = {}
+    for d in defs or []:
+        if "=" not in d:
+            raise SystemExit(f"-D expects key=value, got {d!r}")
+        k, v = d.split("=", 1)
+        out[k.strip()] = v
+    return out
+
+
+class JobContext:
+    """Per-job view of the CLI arguments: config, device, communicator, I/O helpers."""
+
+    def __init__(self, args, prefix: str = "", app: str | None = None):
+        from ..parallel.comm import get_comm
+        from ..utils.config import JobConfig
+        self.args = args
+        app = getattr(args, "app", None) or app
+        if getattr(args, "config", None):
+            if str(args.config).endswith(".conf") and app is None:
+                # a HOCON file with a block named after the job (the Spark appName)
+                from ..utils.config import read_hocon
+                if getattr(args, "job", None) in read_hocon(args.config):
+                    app = args.job
+            self.cfg = JobConfig.from_file(args.config, prefix, app if str(args.config).endswith(".conf") else None)
+        else:
+            self.cfg = JobConfig({}, prefix)
+        self.cfg.update(parse_defines(getattr(args, "define", None)))
+        self.comm = get_comm()
+        dev = getattr(args, "device", None)
+        self.device = torch.device(dev) if dev else torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+    # -- config shortcuts ---------------------------------------------------------------------
+    def __getattr__(self, name):
+        # cfg.get_int / get_str / ... reachable as ctx.get_int(...)
+        if name.startswith("get") or name == "has":
+            return getattr(self.cfg, name)
+        raise AttributeError(name)
+
+    @property
+    def delim_in(self) -> str:
+        return self.cfg.get_str("field.delim.regex", None) or self.cfg.get_str("field.delim.in", None) or ","
+
+    @property
+    def delim_out(self) -> str:
+        return self.cfg.get_str("field.delim.out", None) or self.cfg.get_str("field.delim", None) or ","
+
+    @property
+    def split(self) -> Callable[[str], list[str]]:
+        from ..data.table import split_regex
+        return split_regex(self.delim_in)
+
+    def path(self, key: str | None = None, arg: str | None = None, default=None) -> str:
+        """A side-file path: the CLI flag ``arg`` if given, else config ``key`` (made relative to the
+        config file's directory when it does not exist as given)."""
+        v = getattr(self.args, arg, None) if arg else None
+        if not v and key is not None:
+            v = self.cfg.get_str(key, default)
+        if v is None:
+            raise SystemExit(f"missing path: --{arg or ''} / {self.cfg.prefix}{key}")
+        p = Path(v)
+        if not p.exists() and getattr(self.args, "config", None):
+            alt = Path(self.args.config).parent / v
+            if alt.exists():
+                return str(alt)
+        return str(p)
+
+    def schema(self, key: str = "feature.schema.file.path"):
+        from ..utils.schema import FeatureSchema
+        p = getattr(self.args, "schema", None) or self.cfg.get_str(key, None)
+        if not p:
+            for k in ("feature.schema.file.path", "schema.file.path"):
+                p = p or self.cfg.get_str(k, None)
+        if not p:
+            raise SystemExit("a feature schema is required (--schema or *.schema.file.path)")
+        return FeatureSchema.from_json(Path(self.path(None, None, p) if not Path(p).exists() else p))
+
+    def adhoc_schema(self, cat_ords, class_ord: int | None = None, num_ords=()):
+        """A schema built from config ordinals (jobs whose reference reads ordinals, not a schema
+        file): categorical features with dictionaries discovered from the data, optional numeric
+        features and class attribute."""
+        from ..utils.schema import FeatureField, FeatureSchema
+        fields = [FeatureField(f"f{o}", o, "categorical", feature=True) for o in cat_ords]
+        fields += [FeatureField(f"f{o}", o, "double", feature=True) for o in num_ords]
+        if class_ord is not None:
+            fields.append(FeatureField(f"f{class_ord}", class_ord, "categorical", extra={"classAttribute": True}))
+        return FeatureSchema(fields)
+
+    # -- input --------------------------------------------------------------------------------
+    def all_lines(self, path: str | None = None) -> list[str]:
+        return read_lines(path or self.args.input)
+
+    def lines(self, path: str | None = None, shard: bool = True) -> list[str]:
+        """This rank's contiguous block of the input lines (all lines when not distributed)."""
+        ls = self.all_lines(path)
+        if not shard or not self.comm.is_distributed:
+            return ls
+        from ..data.table import shard_range
+        a, b = shard_range(len(ls), self.comm.rank, self.comm.world)
+        return ls[a:b]
+
+    def rows(self, path: str | None = None, shard: bool = True, keep_empty: bool = True) -> list[list[str]]:
+        sp = self.split
+        return [sp(l) for l in self.lines(path, shard)]
+
+    def table(self, raw_numeric: bool = False, path: str | None = None, schema=None, shard: bool = True):
+        from ..data.table import load_csv
+        comm = self.comm
+        path = str(path or self.args.input)
+        files = input_files(path)
+        if len(files) != 1:
+            # a Hadoop-style directory of part files (or a comma list): one concatenated file
+            import tempfile
+            tmp = tempfile.NamedTemporaryFile("w", suffix=".csv", delete=False)
+            for f in files:
+                txt = f.read_text()
+                tmp.write(txt if txt.endswith("\n") or not txt else txt + "\n")
+            tmp.close()
+            path = tmp.name
+        else:
+            path = str(files[0])
+        return load_csv(path, schema or self.schema(), self.delim_in,
+                        rank=comm.rank if shard else 0, world=comm.world if shard else 1,
+                        device=self.device, keep_lines=True, raw_numeric=raw_numeric)
+
+    # -- collectives on host objects ------------------------------------------------------------
+    def union(self, items: Iterable) -> list:
+        """Sorted union of a set of hashable keys over all ranks (shared vocabulary)."""
+        s = set(items)
+        if self.comm.is_distributed:
+            for part in self.comm.all_gather_object(sorted(s, key=str)):
+                s.update(part)
+        return sorted(s, key=str)
+
+    def sum_counts(self, c: Counter | dict) -> Counter:
+        """Merge a host ``Counter`` over ranks (sparse string-keyed reductions)."""
+        out = Counter(c)
+        if self.comm.is_distributed:
+            out = Counter()
+            for part in self.comm.all_gather_object(dict(c)):
+                out.update(part)
+        return out
+
+    def all_reduce(self, *ts: torch.Tensor) -> None:
+        if self.comm.is_distributed:
+            self.comm.all_reduce_coalesced(list(ts))
+
+    def gather_lines(self, lines: list[str]) -> list[str]:
+        if not self.comm.is_distributed:
+            return lines
+        out = []
+        for part in self.comm.all_gather_object(lines):
+            out += part
+        return out
+
+    @property
+    def is_root(self) -> bool:
+        return self.comm.rank == 0
+
+    # -- output -------------------------------------------------------------------------------
+    def _target(self, out: str | None = None) -> tuple[Path, bool]:
+        p = Path(out or self.args.output)
+        is_dir = p.is_dir() or (p.suffix == "" and not p.exists())
+        return p, is_dir
+
+    def emit(self, lines: list[str], out: str | None = None) -> Path | None:
+        """Map-side output: per-rank part file into a directory, or rank-ordered single file."""
+        p, is_dir = self._target(out)
+        if is_dir:
+            p.mkdir(parents=True, exist_ok=True)
+            t = p / f"part-{self.comm.rank:05d}"
+            _write_text(t, lines)
+            return t
+        lines = self.gather_lines(lines)
+        if self.is_root:
+            _write_text(p, lines)
+            return p
+        return None
+
+    def emit_root(self, lines: list[str], out: str | None = None, name: str = "part-00000") -> Path | None:
+        """Reduce-side output: rank 0 writes the (already reduced) result."""
+        if not self.is_root:
+            return None
+        p, is_dir = self._target(out)
+        if is_dir:
+            p.mkdir(parents=True, exist_ok=True)
+            p = p / name
+        _write_text(p, lines)
+        return p
+
+    def emit_json(self, obj, out: str | None = None) -> None:
+        if self.is_root:
+            p = Path(out or self.args.output)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_text(json.dumps(obj, indent=1))
+
+    def report(self, obj: dict) -> None:
+        """Counters / summary line on stdout (Hadoop job counters)."""
+        if self.is_root:
+            print(json.dumps(obj, default=str), flush=True)
+
+
+def _write_text(p: Path, lines: list[str]) -> None:
+    p.parent.mkdir(parents=True, exist_ok=True)
+    p.write_text("\n".join(lines) + ("\n" if lines else ""))
+
+
+def read_lines(path: str | Sequence[str]) -> list[str]:
+    """Non-empty lines of a file, or of every visible file of a directory (sorted, Hadoop part
+    files), or of a comma-separated list of those (``FileInputFormat.addInputPaths``)."""
+    paths = [path] if isinstance(path, (str, Path)) else list(path)
+    out: list[str] = []
+    for ps in paths:
+        for one in str(ps).split(",") if not Path(str(ps)).exists() else [str(ps)]:
+            p = Path(one)
+            files = (sorted(f for f in p.iterdir() if f.is_file() and not f.name.startswith((".", "_")))
+                     if p.is_dir() else [p])
+            for f in files:
+                out += [l for l in f.read_text().splitlines() if l.strip()]
+    return out
+
+
+def input_files(path: str) -> list[Path]:
+    """The files behind an input path (comma list / directory / file)."""
+    out = []
+    for one in str(path).split(","):
+        p = Path(one)
+        out += (sorted(f for f in p.iterdir() if f.is_file() and not f.name.startswith((".", "_")))
+                if p.is_dir() else [p])
+    return out
+
+
+def fmt(x: float, prec: int = 3) -> str:
+    """``BasicUtils.formatDouble(x, prec)``."""
+    return f"{x:.{prec}f}"
+
+
+def die(msg: str) -> None:
+    print(msg, file=sys.stderr)
+    raise SystemExit(2)

@@ -1,0 +1,573 @@
+"""Core jobs: Naive Bayes, trees, kNN, logistic regression, MI, encodings, Apriori, SMOTE, KS,
+Markov, Viterbi, fixtures, SA, k-means, bandits, classifier / serving drivers.
+
+Reference drivers: R/detr.sh, R/rafo.sh, R/knn.sh, R/carm.sh, R/hica.sh, R/fit.sh, R/ovsa.sh,
+R/ks.sh, R/conv.sh, R/opt.sh, R/wc.sh and the P/app classifier drivers.
+"""
+from __future__ import annotations
+
+import json
+import math
+import sys
+from pathlib import Path
+
+import torch
+
+from .common import JobContext, job
+
+
+# ================================================================================================
+# Bayesian / trees / kNN / linear
+# ================================================================================================
+@job("bayesianDistribution", "naive Bayes training (J/bayesian/BayesianDistribution.java): CSV -> model lines")
+def nb_train(args):
+    """``bad.tabular.input=false`` selects the text mode (``mapText``, :186-195): every line is
+    ``text<delim>class`` and the word tokens are the bins of one text feature (ordinal 1)."""
+    from ..models.bayes import NaiveBayes
+    ctx = JobContext(args, "bad.")
+    if not ctx.get_bool("tabular.input", True):
+        from ..models.bayes import TextNaiveBayesModel
+        m = TextNaiveBayesModel.fit_lines(ctx.lines(), ctx.split, ctx, ctx.get_int("class.field.ordinal", 1),
+                                          ctx.get_int("text.field.ordinal", 0))
+        ctx.emit_root(m.model_lines(ctx.delim_out))
+        return
+    t = ctx.table()
+    nb = NaiveBayes(t.schema).fit(t)
+    ctx.emit_root(nb.model_lines(ctx.delim_out))
+
+
+@job("bayesianPredictor", "naive Bayes prediction (J/bayesian/BayesianPredictor.java): CSV + model -> record,class,prob")
+def nb_predict(args):
+    """Output modes: ``record,predClass,prob`` (default), or with ``bap.output.feature.prob.only``
+    ``id,featurePriorProb,cls0,p0,cls1,p1,...,actualClass`` (:271-285; the stage that feeds the
+    class-conditioned kNN of R/knn.sh)."""
+    from ..models.bayes import NaiveBayes
+    ctx = JobContext(args, "bap.")
+    if not ctx.get_bool("tabular.input", True):
+        from ..models.bayes import TextNaiveBayesModel
+        m = TextNaiveBayesModel.load(ctx.path("bayesian.model.file.path", "model"), ctx.split)
+        to = ctx.get_int("text.field.ordinal", 0)
+        rows = ctx.rows()
+        pred, prob = m.predict([r[to] for r in rows])
+        d = ctx.delim_out
+        ctx.emit([f"{d.join(r)}{d}{m.classes[p]}{d}{int(round(100 * q))}" for r, p, q in zip(rows, pred, prob)])
+        return
+    t = ctx.table()
+    nb = NaiveBayes.load_model(ctx.path("bayesian.model.file.path", "model"), t.schema)
+    vals = t.class_field.cardinality if t.class_field else None
+    d = ctx.delim_out
+    if ctx.get_bool("output.feature.prob.only", False):
+        fp, post = nb.feature_probs(t)
+        ids = t.ids if t.ids is not None else [ln.split(",")[0] for ln in t.lines]
+        lab = t.labels[: t.n].long().cpu().tolist() if t.labels is not None else [0] * t.n
+        fp, post = fp.cpu().tolist(), post.cpu().tolist()
+        lines = []
+        for i in range(t.n):
+            parts = [ids[i], f"{fp[i]:.6g}"]
+            for c, v in enumerate(nb.class_values):
+                parts += [v, f"{post[i][c]:.6g}"]
+            parts.append(vals[lab[i]] if vals and lab[i] < len(vals) else "")
+            lines.append(d.join(parts))
+        ctx.emit(lines)
+        return
+    r = nb.predict(t)
+    pred = r.pred.cpu().tolist()
+    prob = r.prob.max(1).values.cpu().tolist() if r.prob is not None else [1.0] * len(pred)
+    ctx.emit([f"{t.lines[i]}{d}{vals[p] if vals else p}{d}{prob[i]:.3f}" for i, p in enumerate(pred)])
+    if r.confusion is not None:
+        conf = r.confusion.clone()
+        ctx.all_reduce(conf)
+        ctx.report({"confusion": conf.cpu().tolist()})
+
+
+@job("decisionTree", "decision tree (J/tree/DecisionTreeBuilder.java, dtb.* keys) -> decision path JSON")
+def dec_tree(args):
+    """Whole tree in one call (decision-path JSON to ``--output``), or — with
+    ``dtb.decision.file.path.out`` — ONE LEVEL per call like the reference's MR iteration
+    (R/detr.sh decTree / mvDecFiles, :713-725): the current paths are read from
+    ``dtb.decision.file.path.in`` (absent = root), the tree is grown one level deeper and written to
+    ``decision.file.path.out``; the records, each prefixed by the predicates of its path
+    (``dtb.dec.path.delim``), go to ``--output``.  Each level's JSON is the resume point."""
+    from ..models.tree import DecisionPathModel, DecisionTreeBuilder, TreeParams
+    ctx = JobContext(args, "dtb.")
+    t = ctx.table(raw_numeric=True)
+    p = TreeParams.from_config(ctx.cfg)
+    n = torch.tensor([t.n])
+    ctx.all_reduce(n)
+    out_path = ctx.get_str("decision.file.path.out", None)
+    if not out_path:
+        tree = DecisionTreeBuilder(t.schema, p, comm=ctx.comm).fit(t)
+        ctx.emit_json(tree.to_decision_paths(int(n)))
+        return
+    in_path = ctx.get_str("decision.file.path.in", None)
+    depth = 0
+    if in_path and Path(in_path).exists():
+        prev = json.loads(Path(in_path).read_text())
+        depth = max((len(dp["predicates"]) - 1 for dp in prev["decisionPaths"]), default=0)
+    limit = p.max_depth if p.stopping == "maxDepth" else 10 ** 6
+    level = min(depth + 1, limit)
+    p.stopping, p.max_depth = "maxDepth", level
+    tree = DecisionTreeBuilder(t.schema, p, comm=ctx.comm).fit(t)
+    js = tree.to_decision_paths(int(n))
+    if ctx.is_root:
+        Path(out_path).parent.mkdir(parents=True, exist_ok=True)
+        Path(out_path).write_text(json.dumps(js, indent=1))
+    grown = max((len(dp["predicates"]) - 1 for dp in js["decisionPaths"]), default=0)
+    rows = [ln.split(ctx.delim_in) if len(ctx.delim_in) == 1 else ctx.split(ln) for ln in t.lines]
+    _, first = DecisionPathModel(js).predict_proba_rows(rows)
+    pd = ctx.get_str("dec.path.delim", ";")
+    d = ctx.delim_out
+    paths = [pd.join(pr["predicateStr"] for pr in dp["predicates"]) for dp in js["decisionPaths"]]
+    ctx.emit([f"{paths[int(j)] if int(j) >= 0 else '$root'}{d}{ln}" for ln, j in zip(t.lines, first.tolist())])
+    ctx.report({"level": grown, "done": grown <= depth or grown >= limit})
+
+
+@job("randomForest", "random forest of decision trees (R/rafo.sh) -> one JSON per tree")
+def rafo(args):
+    from ..models.tree import RandomForest, TreeParams
+    ctx = JobContext(args, "dtb.")
+    t = ctx.table(raw_numeric=True)
+    p = TreeParams.from_config(ctx.cfg)
+    p.sub_sampling = ctx.get_str("sub.sampling.strategy", "withReplace")
+    rf = RandomForest(t.schema, ctx.get_int("num.trees", 10), p, ctx.get_str("max.features", "sqrt")).fit(t)
+    if ctx.is_root:
+        out = Path(args.output)
+        out.mkdir(parents=True, exist_ok=True)
+        for i, tr in enumerate(rf.trees):
+            (out / f"tree_{i}.json").write_text(json.dumps(tr.to_decision_paths(t.n)))
+
+
+@job("knnClassifier", "kNN classification with the fused distance+top-k kernel: --input test --train train CSV")
+def knn(args):
+    """Both sets are sharded over ranks; the training shards circulate around the ring
+    (``distributed_knn``) so every rank classifies only its own query shard."""
+    from ..models.knn import NearestNeighbor
+    ctx = JobContext(args, "nen.")
+    schema = ctx.schema()
+    tr = ctx.table(raw_numeric=True, path=args.train, schema=schema)
+    te = ctx.table(raw_numeric=True, schema=schema)
+    Xtr, Xte = tr.dense_features(one_hot=True), te.dense_features(one_hot=True)
+    lo, hi = Xtr.min(0).values, Xtr.max(0).values
+    if ctx.comm.is_distributed:
+        ctx.comm.all_reduce(lo, "min")
+        ctx.comm.all_reduce(hi, "max")
+    scale = (hi - lo).clamp_min(1e-12)
+    nn = NearestNeighbor.from_config(ctx.cfg).fit((Xtr - lo) / scale, tr.labels[: tr.n].long(), tr.n_classes,
+                                                  index_base=tr.row_offset)
+    res = nn.predict((Xte - lo) / scale, q_base=te.row_offset)
+    vals = te.class_field.cardinality
+    d = ctx.delim_out
+    ctx.emit([f"{te.lines[i]}{d}{vals[p]}" for i, p in enumerate(res.pred.cpu().tolist())])
+
+
+@job("logisticRegression", "logistic regression (J/regress/LogisticRegressionJob.java): CSV -> coefficient lines per iteration")
+def logit(args):
+    from ..models.linear import LogisticRegression
+    ctx = JobContext(args, "lor.")
+    t = ctx.table(raw_numeric=True)
+    X = t.dense_features()
+    m = LogisticRegression(solver=ctx.get_str("solver", "newton"), max_iter=ctx.get_int("iteration.limit", 10),
+                           criteria=ctx.get_str("convergence.criteria", "iterLimit"),
+                           threshold=ctx.get_float("convergence.threshold", 5.0))
+    pos = ctx.get_str("positive.class.value", None)
+    vals = t.class_field.cardinality
+    y = (t.labels[: t.n].long() == (vals.index(pos) if pos in vals else 1)).float()
+    m.fit(X, y)
+    ctx.emit_root(m.coefficient_lines(ctx.delim_out))
+
+
+# ================================================================================================
+# exploration / encoding / sampling
+# ================================================================================================
+@job("mutualInformation", "mutual information feature scores (J/explore/MutualInformation.java, mut.* keys)")
+def mi(args):
+    """One class histogram + all pair histograms (K2/K3), one all-reduce; the scores of
+    ``mut.mutual.info.score.algorithms``; with ``mut.feature.class.cond.dstr.sep.output`` the
+    feature class-conditional distribution is written to
+    ``mut.feature.class.distr.output.file.path`` (the input of categoricalClassAffinity, R/carm.sh)."""
+    from ..models.explore import MutualInformation
+    ctx = JobContext(args, "mut.")
+    t = ctx.table()
+    m = MutualInformation(comm=ctx.comm)
+    m.fit(t)
+    alg = ctx.get_str("mutual.info.score.algorithms", "mutual.info.maximization").split(",")
+    lines = []
+    fns = {"mutual.info.maximization": m.mim, "mutual.info.selection": m.mifs, "joint.mutual.info": m.jmi,
+           "double.input.symmetrical.relevance": m.disr, "min.redundancy.max.relevance": m.mrmr}
+    for a in alg:
+        if a in fns:
+            lines.append(a)
+            lines += [f"{f},{s:.6f}" for f, s in fns[a]()]
+    ctx.emit_root(lines)
+    if ctx.get_bool("feature.class.cond.dstr.sep.output", False):
+        ctx.emit_root(m.class_conditional_lines(t, ctx.delim_out), ctx.get_str("feature.class.distr.output.file.path"))
+
+
+@job("categoricalClassAffinity", "class affinity of categorical values (J/explore/CategoricalClassAffinity.java, cca.*)")
+def caff(args):
+    """Input: the feature class-conditional distribution file of mutualInformation
+    (``featOrd,classVal,featVal,prob``, R/carm.sh), or — with a schema — the raw records (the
+    distribution is then computed here by the K2 class histogram).  For each strategy of
+    ``cca.affinity.strategy`` (oddsRatio, distrDiff, minRisk, klDiff): an ``algorithm: <s>`` line,
+    then ``featOrd,value,score`` per feature sorted by descending score (:189-258)."""
+    ctx = JobContext(args, "cca.")
+    strategies = ctx.get_list("affinity.strategy", "oddsRatio")
+    pos = ctx.get_str("pos.class.attr.value", None) or ctx.get_str("positive.class.value", None)
+    d = ctx.delim_out
+    has_schema = bool(getattr(args, "schema", None) or ctx.has("feature.schema.file.path"))
+    lines = []
+    if has_schema:
+        from ..models.explore import class_affinity
+        t = ctx.table()
+        pc = t.class_field.cardinality.index(pos) if pos in (t.class_field.cardinality or []) else 0
+        for sname in strategies:
+            res = class_affinity(t, sname, pos_class=pc, comm=ctx.comm)
+            lines.append(f"algorithm: {sname}")
+            lines += [f"{o}{d}{v}{d}{s!r}" for o, vals in res.items() for v, s in vals]
+        ctx.emit_root(lines)
+        return
+    pos_d, neg_d = {}, {}
+    feats = []
+    for r in ctx.rows(shard=False):
+        if len(r) < 4:
+            continue
+        o = int(r[0])
+        if o not in feats:
+            feats.append(o)
+        (pos_d if r[1] == pos else neg_d).setdefault(o, {})[r[2]] = float(r[3])
+    for sname in strategies:
+        lines.append(f"algorithm: {sname}")
+        for o in feats:
+            pdist, ndist = pos_d.get(o, {}), neg_d.get(o, {})
+            vals = list(pdist)
+            p = torch.tensor([pdist[v] for v in vals], dtype=torch.float64)
+            q = torch.tensor([ndist.get(v, 0.0) for v in vals], dtype=torch.float64)
+            if sname == "oddsRatio":
+                sc = (p / (1 - p)) / (q / (1 - q))
+            elif sname == "distrDiff":
+                sc = p - q
+            elif sname == "minRisk":
+                sc = p * (1 - q)
+            elif sname == "klDiff":
+                sc = p * torch.log(p / q)
+            else:
+                raise SystemExit(f"unknown affinity strategy {sname}")
+            order = sorted(range(len(vals)), key=lambda i: -float(sc[i]) if not math.isnan(float(sc[i])) else math.inf)
+            lines += [f"{o}{d}{vals[i]}{d}{float(sc[i])!r}" for i in order]
+    ctx.emit_root(lines)
+
+
+@job("categoricalContinuousEncoding", "supervised ratio / weight-of-evidence encoding (R/hica.sh, J/explore/CategoricalContinuousEncoding.java)")
+def hica(args):
+    """Reference keys ``coe.cat.attribute.ordinals``, ``coe.class.attr.ordinal``,
+    ``coe.pos.class.attr.value``, ``coe.encoding.strategy``, ``coe.output.scale`` (schema-less; the
+    dictionaries of the categorical fields are discovered, any cardinality — uint16 codes above 255
+    values), or a feature schema.  Output ``attr,value,encodedInt`` (:204-230)."""
+    from ..models.explore import supervised_encoding
+    ctx = JobContext(args, "coe.")
+    if ctx.has("cat.attribute.ordinals"):
+        schema = ctx.adhoc_schema(ctx.get_int_list("cat.attribute.ordinals"), ctx.get_int("class.attr.ordinal"))
+        t = ctx.table(schema=schema)
+    else:
+        ctx.cfg.prefix = "cce."
+        t = ctx.table()
+    pos = ctx.get_str("pos.class.attr.value", None)
+    vals = t.class_field.cardinality
+    pc = vals.index(pos) if pos in vals else 1
+    enc = supervised_encoding(t, ctx.get_str("encoding.strategy", "supervisedRatio"), ctx.get_int("output.scale", 1000),
+                              pos_class=pc, comm=ctx.comm)
+    d = ctx.delim_out
+    ctx.emit_root([f"{o}{d}{v}{d}{int(s)}" for o, m in enc.items() for v, s in m.items()])
+
+
+@job("frequentItemsApriori", "Apriori frequent item sets (R/fit.sh): one transaction per line")
+def apriori(args):
+    from ..models.association import Apriori
+    ctx = JobContext(args, "fia.")
+    skip = ctx.get_int("skip.field.count", 1)
+    rows = ctx.rows()
+    base = 0
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        base = shard_range(len(ctx.all_lines()), ctx.comm.rank, ctx.comm.world)[0]
+    ap = Apriori(ctx.get_float("support.threshold", 0.1), ctx.get_int("max.item.set.length", 4))
+    fi = ap.fit_transactions([r[skip:] for r in rows], device=ctx.device, tx_base=base)
+    d = ctx.delim_out
+    lines = [d.join(names) + f"{d}{sup:.6f}" for k in range(1, ap.max_len + 1) for names, sup in fi.as_names(k)]
+    ctx.emit_root(lines)
+
+
+@job("classBasedOverSampler", "SMOTE over-sampling of the minority class (R/ovsa.sh, J/explore/ClassBasedOverSampler.java)")
+def smote(args):
+    """Two input forms.  With ``cbos.rec.len`` (the reference): every line is a minority record
+    followed by its same-class neighbours (topMatchesByClass compact output), each ``rec.len``
+    fields; ``cbos.over.sampling.multiplier`` synthetic records per line interpolate the numeric
+    fields of the record and a neighbour picked uniformly or exponentially
+    (``cbos.neighbor.sampling.distr``) and take categorical values from either (:125-200) — all
+    lines of the shard at once as ``[n, M, rec.len]`` tensors.  Without it: the neighbourhoods are
+    computed here by the fused kNN kernel over the schema's features."""
+    from ..models.sampling import smote as _smote
+    ctx = JobContext(args, "cbos.")
+    if ctx.has("rec.len"):
+        return _smote_from_neighbors(ctx)
+    t = ctx.table(raw_numeric=True)
+    X = t.dense_features()
+    y = t.labels[: t.n].long()
+    minority = int(torch.bincount(y).argmin())
+    n_new = int((y != minority).sum() - (y == minority).sum())
+    Xn, _ = _smote(X, y, minority, max(n_new, 0), ctx.get_int("neighbor.count", 5), seed=ctx.comm.rank)
+    vals = t.class_field.cardinality
+    d = ctx.delim_out
+    ctx.emit([d.join(f"{v:.4f}" for v in row) + f"{d}{vals[minority]}" for row in Xn.cpu().tolist()])
+
+
+def _smote_from_neighbors(ctx: JobContext) -> None:
+    import random
+    L = ctx.get_int("rec.len")
+    mult = ctx.get_int("over.sampling.multiplier")
+    distr = ctx.get_str("neighbor.sampling.distr", "uniform")
+    prec = ctx.get_int("output.precision", 3)
+    schema = ctx.schema("feature.schema.file.path")
+    rows = [r for r in ctx.rows() if len(r) >= 2 * L]
+    if not rows:
+        ctx.emit([])
+        return
+    M = max((len(r) - L) // L for r in rows)
+    n = len(rows)
+    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + 7919 * ctx.comm.rank)
+    nnb = torch.tensor([(len(r) - L) // L for r in rows], dtype=torch.long)
+    if distr == "exponential":
+        mean = ctx.get_float("exp.distr.mean")
+        e = -mean * torch.log(torch.rand((n, mult), generator=g, dtype=torch.float64).clamp_min(1e-12))
+        pick = (torch.round(e).long() - 1).clamp_min(0)
+        pick = torch.minimum(pick, (nnb - 1).view(-1, 1))
+    else:
+        pick = (torch.rand((n, mult), generator=g, dtype=torch.float64) * nnb.view(-1, 1)).long()
+    gap = torch.rand((n, mult), generator=g, dtype=torch.float64)
+    coin = torch.rand((n, mult), generator=g) < 0.5
+    fields = {f.ordinal: f for f in schema.fields}
+    num_cols = [i for i in range(L) if i in fields and fields[i].feature and fields[i].is_numeric]
+    src = torch.tensor([[float(r[i]) for i in num_cols] for r in rows], dtype=torch.float64)
+    nb = torch.zeros((n, M, len(num_cols)), dtype=torch.float64)
+    for a, r in enumerate(rows):
+        for m in range((len(r) - L) // L):
+            nb[a, m] = torch.tensor([float(r[L + m * L + i]) for i in num_cols], dtype=torch.float64)
+    tgt = nb[torch.arange(n).view(-1, 1), pick]                      # [n, mult, F]
+    new = src.unsqueeze(1) + (tgt - src.unsqueeze(1)) * gap.unsqueeze(2)
+    d = ctx.delim_out
+    rnd = random.Random(ctx.get_int("random.seed", 0) + ctx.comm.rank)
+    out = []
+    for a, r in enumerate(rows):
+        for j in range(mult):
+            nrec = r[L + int(pick[a, j]) * L: L + int(pick[a, j]) * L + L]
+            rec = list(r[:L])
+            for i in range(L):
+                f = fields.get(i)
+                if f is None:
+                    continue
+                if f.id:
+                    s = list(r[i] + nrec[i])
+                    rnd.shuffle(s)
+                    rec[i] = "".join(s)[: len(r[i])]
+                elif f.feature and f.is_categorical:
+                    rec[i] = r[i] if coin[a, j] else nrec[i]
+            for c, i in enumerate(num_cols):
+                v = float(new[a, j, c])
+                rec[i] = str(int(v)) if fields[i].is_integer else f"{v:.{prec}f}"
+            out.append(d.join(rec))
+    ctx.emit(out)
+
+
+@job("kolmogorovSmirnovModelDrift", "KS drift between reference and current distributions (S/explore/KolmogorovSmirnovModelDrift.scala)")
+def ks(args):
+    from ..models.explore import kolmogorov_smirnov_drift, numeric_histogram
+    ctx = JobContext(args, "ksd.")
+    if not getattr(args, "train", None):
+        from .pipeline_stages import ks_from_distr
+        return ks_from_distr(ctx)
+    col = ctx.get_int("attr.ordinal", 0)
+    sp = ctx.split
+    ref = torch.tensor([float(sp(l)[col]) for l in ctx.all_lines(args.train)], dtype=torch.float64)
+    cur = torch.tensor([float(sp(l)[col]) for l in ctx.all_lines()], dtype=torch.float64)
+    bw = ctx.get_float("bin.width", float((ref.max() - ref.min()) / 50 or 1))
+    lo = float(min(ref.min(), cur.min()))
+    nb = int((float(max(ref.max(), cur.max())) - lo) / bw) + 1
+    stat, crit, drift = kolmogorov_smirnov_drift(numeric_histogram(ref, bw, lo, nb), numeric_histogram(cur, bw, lo, nb))
+    ctx.emit_root([f"{col},{stat:.6f},{crit:.6f},{drift}"])
+
+
+# ================================================================================================
+# sequences / Markov
+# ================================================================================================
+@job("markovStateTransitionModel", "Markov transition probabilities per class (R/conv.sh, J/markov/MarkovStateTransitionModel.java)")
+def markov(args):
+    """Compact rows ``id,[class],s1,s2,...`` (MR and Spark compact format), or the Spark long format
+    (``mst.input.format=long``: ``id,seq,state`` rows grouped by id and ordered by seq,
+    S/sequence/MarkovStateTransitionModel.scala:202-225)."""
+    from ..models.markov import MarkovStateTransitionModel
+    ctx = JobContext(args, "mst.")
+    states = ctx.get_list("model.states", None) or ctx.get_list("state.list")
+    skip = ctx.get_int("skip.field.count", 1)
+    cls_ord = ctx.get_int("class.label.field.ord", ctx.get_int("class.label.field.ordinal", -1))
+    rows = ctx.rows()
+    if ctx.get_str("input.format", "compact") == "long":
+        from collections import defaultdict
+        id_ord, seq_ord, st_ord = (ctx.get_int("id.field.ordinal", 0), ctx.get_int("seq.field.ordinal", 1),
+                                   ctx.get_int("state.field.ordinal", 2))
+        g = defaultdict(list)
+        for r in ctx.rows(shard=False):
+            g[r[id_ord]].append((float(r[seq_ord]), r[st_ord]))
+        rows = [[k] + [s for _, s in sorted(v)] for k, v in sorted(g.items())]
+        if ctx.comm.is_distributed:
+            from ..data.table import shard_range
+            a, b = shard_range(len(rows), ctx.comm.rank, ctx.comm.world)
+            rows = rows[a:b]
+        skip, cls_ord = 1, -1
+    seqs = [r[skip:] if cls_ord < 0 else [v for i, v in enumerate(r) if i >= skip and i != cls_ord] for r in rows]
+    m = MarkovStateTransitionModel(states, scale=ctx.get_int("trans.prob.scale", 1000), comm=ctx.comm)
+    enc = m.encode(seqs)
+    labels = None
+    if cls_ord >= 0:
+        cl = ctx.get_list("class.labels", None) or ctx.union(r[cls_ord] for r in rows)
+        m.class_labels = cl
+        labels = torch.tensor([cl.index(r[cls_ord]) for r in rows])
+    m.fit(enc, labels)
+    ctx.emit_root(m.model_lines(ctx.delim_out))
+
+
+@job("viterbiStatePredictor", "HMM state sequence per observation sequence (J/markov/ViterbiStatePredictor.java); --model <HMM lines>")
+def viterbi(args):
+    """Rows ``id,obs,obs,...`` -> ``id,state,state,...``: ``vsp.id.field.ordinal`` (default 0) is
+    written first, the observations start after ``vsp.skip.field.count`` (default 1) fields; with
+    ``vsp.output.state.only=false`` each token is ``obs<sub.field.delim>state``.  The model file is
+    always split on ',' (:94-142).  A token outside the model's observations ends the sequence."""
+    from ..models.markov import HiddenMarkovModel, ViterbiDecoder
+    ctx = JobContext(args, "vsp.")
+    skip = ctx.get_int("skip.field.count", 1)
+    id_ord = ctx.get_int("id.field.ordinal", 0)
+    state_only = ctx.get_bool("output.state.only", True)
+    sub = ctx.get_str("sub.field.delim", ":")
+    hmm = HiddenMarkovModel.from_lines(ctx.all_lines(ctx.path("hmm.model.path", "model")), ",")
+    rows = ctx.rows()
+    oi = {o: i for i, o in enumerate(hmm.observations)}
+    obs = torch.full((len(rows), max([len(r) - skip for r in rows] + [1])), -1, dtype=torch.int16)
+    for r, row in enumerate(rows):
+        for j, tok in enumerate(row[skip:]):
+            obs[r, j] = oi.get(tok, -1)
+    paths = ViterbiDecoder(hmm).decode_labels(obs.to(ctx.device))
+    d = ctx.delim_out
+    out = []
+    for row, p in zip(rows, paths):
+        toks = p if state_only else [f"{o}{sub}{s}" for o, s in zip(row[skip:], p)]
+        out.append(d.join([row[id_ord]] + toks))
+    ctx.emit(out)
+
+
+@job("genData", "tutorial fixture generator: --name <P/app script> --gen-args a,b,c [--seed s] (data/fixtures.py)")
+def gen_data(args):
+    from ..data.fixtures import FIXTURES
+
+    def num(v):
+        for t in (int, float):
+            try:
+                return t(v)
+            except ValueError:
+                pass
+        return v
+    if args.name not in FIXTURES:
+        raise SystemExit(f"unknown fixture {args.name}; one of {', '.join(sorted(FIXTURES))}")
+    gargs = [num(v) for v in args.gen_args.split(",")] if args.gen_args else []
+    out = FIXTURES[args.name](*gargs, seed=args.seed)
+    lines = out[0] if isinstance(out, tuple) else out
+    if args.output:
+        JobContext(args).emit_root(lines)
+    else:
+        sys.stdout.write("\n".join(lines) + "\n")
+
+
+@job("wordCount", "word count (J/text/WordCounter.java, S/sanity/WordCount.scala)")
+def wc(args):
+    from collections import Counter
+    ctx = JobContext(args)
+    c = ctx.sum_counts(Counter(w for l in ctx.lines() for w in l.split()))
+    ctx.emit_root([f"{w},{n}" for w, n in sorted(c.items())])
+
+
+# ================================================================================================
+# optimisation / clustering / bandits
+# ================================================================================================
+@job("simulatedAnnealing", "SA over a task-schedule domain (R/opt.conf block simulatedAnnealing)")
+def sa(args):
+    from ..optimize import SimulatedAnnealing, TaskScheduleSearch
+    ctx = JobContext(args, app="simulatedAnnealing")
+    dom_file = ctx.path("domain.callback.config.file", "domain")
+    d = TaskScheduleSearch.from_json(dom_file, ctx.device)
+    r = SimulatedAnnealing.from_config(d, ctx.cfg).run()
+    o = ctx.get_str("field.delim.out", ",")
+    lines = [f"{d.format_solution(s)}{o}{c:.6f}" for s, c in zip(r.solutions.tolist(), r.costs.tolist())]
+    lines.sort(key=lambda l: float(l.rsplit(o, 1)[1]))
+    ctx.emit_root(lines)
+    ctx.report({"best_cost": r.best_cost, **r.stats})
+
+
+@job("kmeansCluster", "k-means over numeric columns (S/cluster/KmeansCluster.scala); --k list; knuckle-point k")
+def kmeans(args):
+    from ..models.cluster import KMeans
+    ctx = JobContext(args, "kmc.")
+    cols = ctx.get_int_list("attr.ordinals", "0")
+    X = torch.tensor([[float(r[c]) for c in cols] for r in ctx.rows()], device=ctx.device)
+    ks = [int(k) for k in (args.k or ctx.get_str("num.clusters", "3")).split(",")]
+    km = KMeans(ks, n_init=ctx.get_int("num.init.groups", 3), max_iter=ctx.get_int("max.iterations", 100)).fit(X)
+    lines = []
+    for k in ks:
+        run = km.best[k]
+        lines += [f"{k},{i}," + ",".join(f"{v:.4f}" for v in c) for i, c in enumerate(run.centroids.cpu().tolist())]
+        lines.append(f"{k},sse,{run.sse:.4f}")
+    if len(ks) > 2:
+        lines.append(f"knuckle,{km.knuckle_k()}")
+    ctx.emit_root(lines)
+
+
+@job("multiArmBandit", "batch bandit per group (S/reinforce/MultiArmBandit.scala): rewards in, actions out")
+def mab(args):
+    from ..models.bandit import BanditBank
+    ctx = JobContext(args, app="multiArmBandit")
+    actions = ctx.get_list("action.list")
+    rows = ctx.rows(shard=False)                # group, action, reward
+    groups = sorted({r[0] for r in rows})
+    bank = BanditBank(ctx.get_str("learner.type", "upperConfidenceBoundOne"), actions, len(groups),
+                      dict(ctx.cfg.values), device=ctx.device)
+    if rows:
+        gi = torch.tensor([groups.index(r[0]) for r in rows])
+        ai = torch.tensor([actions.index(r[1]) for r in rows])
+        rw = torch.tensor([float(r[2]) for r in rows])
+        bank.set_rewards(gi, ai, rw)
+    acts = bank.next_actions().cpu()
+    ctx.emit_root([f"{g}," + ",".join(actions[a] for a in acts[i].tolist()) for i, g in enumerate(groups)])
+
+
+# ================================================================================================
+# python-side drivers and services
+# ================================================================================================
+@job("classifier", "config-driven classifier (P/supv drivers): --kind rf|gbt|svm|lr --mode train|trainValidate|validate|...")
+def classifier(args):
+    from ..models import supervised as SV
+    cls = {"rf": SV.RandomForest, "gbt": SV.GradientBoostedTrees, "svm": SV.SupportVectorMachine,
+           "lr": SV.LogisticRegressionDiscriminant}[args.kind]
+    c = cls(args.config, device=args.device)
+    mode = args.mode or c.getMode()
+    res = {"training": c.train, "train": c.train, "trainValidate": c.trainValidate,
+           "trainValidateSearch": c.trainValidateSearch, "validate": c.validate, "predict": c.predict,
+           "predictProb": c.predictProb, "autoTrain": c.autoTrain}[mode]()
+    if isinstance(res, torch.Tensor):
+        res = res.cpu().tolist()
+    print(json.dumps(res, default=str))
+
+
+@job("serve", "REST prediction service (P/app/rfsvc.py etc.): --kind rf|gbt|svm|lr --config props --port P [--name rf]")
+def serve(args):
+    from ..serve import PredictionServer, classifier_factory
+    srv = PredictionServer()
+    srv.register_lazy(args.name or args.kind, classifier_factory(args.kind, args.config))
+    print(f"serving /{args.name or args.kind}/predict on 127.0.0.1:{args.port}", flush=True)
+    srv.serve(args.port)

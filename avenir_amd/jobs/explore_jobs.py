@@ -1,0 +1,640 @@
+"""Exploration, encoding, sampling and feature-relevance jobs (J/explore/*, S/explore/*, S/util/*).
+
+Counting jobs build a dense per-rank tensor (contingency tables, class counts, moments) with the
+device histogram kernels, all-reduce it once over RCCL and write from rank 0 (the reference's
+combiner + single reducer); record-wise jobs (samplers, encoders, mappers) transform their input
+shard and write one part file per rank (the reference's map-only jobs).
+"""
+from __future__ import annotations
+
+import math
+from collections import Counter, defaultdict
+
+import torch
+
+from .common import JobContext, fmt, job
+
+
+def _schema_or_none(ctx: JobContext, key: str):
+    try:
+        return ctx.schema(key)
+    except SystemExit:
+        return None
+
+
+def _pairs(spec: str) -> list[tuple[int, int]]:
+    """``a:b,c:d`` (chombo ``assertIntPairListConfigParam``)."""
+    return [tuple(int(x) for x in p.split(":")) for p in spec.split(",") if p.strip()]
+
+
+# ================================================================================================
+# categorical / numerical correlation
+# ================================================================================================
+def _contingency_job(ctx: JobContext, src_key: str, dst_key: str, stat_fn) -> None:
+    """Shared driver of CramerCorrelation / HeterogeneityReductionCorrelation
+    (J/explore/CategoricalCorrelation.java:52-209): one multi-pair 2-D histogram launch (K3) per
+    rank, ONE all-reduce of every contingency table, ``srcName,dstName,stat`` lines."""
+    from ..models.explore import ContingencyStats
+    from ..ops import histogram as H
+    schema = ctx.schema("feature.schema.file.path")
+    src = ctx.get_int_list(src_key)
+    dst = ctx.get_int_list(dst_key)
+    pairs = [(s, d) for s in src for d in dst if s != d]
+    ords = sorted({o for p in pairs for o in p})
+    t = ctx.table(schema=_with_features(schema, ords))
+    pos = {f.ordinal: j for j, f in enumerate(t.binned_fields)}
+    tabs = H.pair_histogram(t.codes, t.n, t.bins, [(pos[a], pos[b]) for a, b in pairs], None, 1)
+    tabs = [tb[0].clone() for tb in tabs]
+    ctx.all_reduce(*tabs)
+    d = ctx.delim_out
+    lines = []
+    for (a, b), tb in zip(pairs, tabs):
+        fa, fb = schema.find_field_by_ordinal(a), schema.find_field_by_ordinal(b)
+        lines.append(f"{fa.name}{d}{fb.name}{d}{stat_fn(ContingencyStats(tb))}")
+    ctx.emit_root(lines)
+
+
+def _with_features(schema, ords):
+    """A copy of the schema whose feature set is exactly ``ords`` (class attribute dropped)."""
+    import copy
+    s = copy.deepcopy(schema)
+    for f in s.fields:
+        f.feature = f.ordinal in set(ords)
+        if f.ordinal in set(ords):
+            f.class_attr = False
+    return s
+
+
+@job("cramerCorrelation", "Cramer index per categorical attribute pair (J/explore/CramerCorrelation.java, crc.*)")
+def cramer(args):
+    ctx = JobContext(args, "crc.")
+    _contingency_job(ctx, "source.attributes", "dest.attributes", lambda c: c.cramer_index())
+
+
+@job("heterogeneityReductionCorrelation",
+     "concentration (gini) / uncertainty coefficient per attribute pair (J/explore/HeterogeneityReductionCorrelation.java)")
+def hetero(args):
+    ctx = JobContext(args, "cac.")
+    alg = ctx.cfg.values.get("hrc.heterogeneity.algorithm", "gini")
+    _contingency_job(ctx, "first.set.attributes", "second.set..attributes" if ctx.has("second.set..attributes")
+                     else "second.set.attributes",
+                     (lambda c: c.concentration_coeff()) if alg == "gini" else (lambda c: c.uncertainty_coeff()))
+
+
+@job("numericalCorrelation", "Pearson correlation of attribute pairs (J/explore/NumericalCorrelation.java, nuc.*)")
+def numcorr(args):
+    """``nuc.attr.pairs=a:b,...``; means/std-devs come from ``nuc.stats.file.path`` (chombo
+    NumericalAttrStats lines ``attr,...,mean,...,stdDev``) when given, else from the same pass (one
+    fused moments reduction: counts, sums and the cross-product GEMM, one all-reduce)."""
+    ctx = JobContext(args, "nuc.")
+    pairs = _pairs(ctx.get_str("attr.pairs"))
+    ords = sorted({o for p in pairs for o in p})
+    rows = ctx.rows()
+    X = torch.tensor([[float(r[o]) for o in ords] for r in rows], dtype=torch.float64, device=ctx.device)
+    n = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=ctx.device)
+    s = X.sum(0)
+    G = X.T @ X
+    ctx.all_reduce(n, s, G)
+    mean = s / n
+    cov = G / n - mean.view(-1, 1) * mean.view(1, -1)
+    sd = cov.diag().clamp_min(1e-300).sqrt()
+    if ctx.has("stats.file.path"):
+        st = {}
+        for l in ctx.all_lines(ctx.path("stats.file.path")):
+            p = ctx.split(l)
+            st[int(p[0])] = float(p[-1])
+        sd = torch.tensor([st.get(o, float(sd[i])) for i, o in enumerate(ords)], dtype=torch.float64, device=ctx.device)
+    ix = {o: i for i, o in enumerate(ords)}
+    d = ctx.delim_out
+    ctx.emit_root([f"{a}{d}{b}{d}{float(cov[ix[a], ix[b]] / (sd[ix[a]] * sd[ix[b]]))}" for a, b in pairs])
+
+
+# ================================================================================================
+# rules
+# ================================================================================================
+@job("ruleEvaluator", "confidence and support of named rules rue.rule.<name>=<cond> > <class> (J/explore/RuleEvaluator.java)")
+def rule_evaluator(args):
+    """Each rule's antecedent is evaluated column-wise over the shard (``utils/rules.py``), the
+    per-rule class counts are one ``[R, C]`` tensor, all-reduced once; output
+    ``name,confidence,support`` with ``rue.conf.strategy`` confAccuracy | confEntropy
+    (:231-268; support divides by ``rue.data.size`` when given, else by the global record count)."""
+    from ..utils.rules import ColumnCache, rules_from_config
+    ctx = JobContext(args, "rue.")
+    rules = rules_from_config(ctx.cfg)
+    cls_ord = ctx.get_int("class.attr.ord")
+    classes = ctx.get_list("class.values", None)
+    rows = ctx.rows(keep_empty=True)
+    cols = ColumnCache(rows, ctx.device)
+    if not classes:
+        classes = ctx.union(r[cls_ord] for r in rows)
+    ci = {c: i for i, c in enumerate(classes)}
+    lab = torch.tensor([ci.get(r[cls_ord], -1) for r in rows], dtype=torch.long, device=ctx.device)
+    C, R = len(classes), len(rules)
+    counts = torch.zeros((R, C), dtype=torch.float64, device=ctx.device)
+    for k, (name, rexp) in enumerate(rules.items()):
+        m = rexp.evaluate(cols) & (lab >= 0)
+        counts[k] = torch.bincount(lab[m], minlength=C)[:C].double()
+    n = torch.tensor([float(len(rows))], dtype=torch.float64, device=ctx.device)
+    ctx.all_reduce(counts, n)
+    size = ctx.get_int("data.size", None) or int(n)
+    strat = ctx.get_str("conf.strategy", "confAccuracy")
+    d = ctx.delim_out
+    lines = []
+    for k, (name, rexp) in enumerate(rules.items()):
+        tot = float(counts[k].sum())
+        cons = ci.get(rexp.consequent, 0)
+        if strat == "confEntropy":
+            p1 = float(counts[k, cons]) / max(tot, 1)
+            p2 = float(counts[k, cons ^ 1]) / max(tot, 1) if C > 1 else 0.0
+            ent = sum(p * math.log(p) for p in (p1, p2) if p > 0)
+            conf = ent / math.log(2) + 1.0
+        else:
+            conf = float(counts[k, cons]) / max(tot, 1)
+        lines.append(f"{name}{d}{fmt(conf)}{d}{fmt(tot / max(size, 1))}")
+    ctx.emit_root(lines)
+
+
+# ================================================================================================
+# feature relevance / neighbourhoods
+# ================================================================================================
+@job("reliefFeatureRelevance", "Relief feature relevance (J/explore/ReliefFeatureRelevance.java, ffr.* / S FeatureRelevanceByRelief)",
+     aliases=("featureRelevanceByRelief",))
+def relief_job(args):
+    """Two input forms:
+
+    * ``ffr.neighborhood.file.path`` given (MR form): records keyed by ``ffr.id.ord`` plus a
+      neighbourhood file of ``srcId,srcClass,trgClass,trgId,...`` lines (ClassBasedNeighborhood);
+      every (src, trg) pair adds -|diff| on a hit and +|diff| on a miss, normalised by the
+      attribute range, divided by the pair count;
+    * otherwise: the neighbourhoods are computed here with the fused kNN kernel (nearest hit and
+      miss per record, ``ffr.neighbor.count``), over the schema's feature attributes.
+
+    Output ``attrOrd,score`` (3 decimals)."""
+    from ..models.sampling import relief
+    ctx = JobContext(args, "ffr.")
+    attrs = ctx.get_int_list("attr.ordinals", None)
+    schema = _schema_or_none(ctx, "attr.schema.file.path")
+    d = ctx.delim_out
+    if ctx.has("neighborhood.file.path"):
+        id_ord = ctx.get_int("id.ord")
+        recs = {r[id_ord]: r for r in ctx.rows(shard=False)}
+        pairs = []
+        for l in ctx.all_lines(ctx.path("neighborhood.file.path")):
+            p = ctx.split(l)
+            for trg in p[3:]:
+                if p[0] in recs and trg in recs:
+                    pairs.append((p[0], trg, p[1] == p[2]))
+        if ctx.comm.is_distributed:
+            from ..data.table import shard_range
+            a, b = shard_range(len(pairs), ctx.comm.rank, ctx.comm.world)
+            pairs = pairs[a:b]
+        score = torch.zeros(len(attrs), dtype=torch.float64)
+        for j, o in enumerate(attrs):
+            f = schema.find_field_by_ordinal(o) if schema else None
+            if f is not None and f.is_categorical:
+                diff = torch.tensor([float(recs[s][o] != recs[t][o]) for s, t, _ in pairs], dtype=torch.float64)
+            else:
+                rng = (f.max - f.min) if f is not None and f.max is not None and f.min is not None else 1.0
+                diff = torch.tensor([abs(float(recs[s][o]) - float(recs[t][o])) / rng for s, t, _ in pairs],
+                                    dtype=torch.float64)
+            sign = torch.tensor([-1.0 if hit else 1.0 for _, _, hit in pairs], dtype=torch.float64)
+            score[j] = (diff * sign).sum() if pairs else 0.0
+        npairs = torch.tensor([float(len(pairs))], dtype=torch.float64)
+        ctx.all_reduce(score, npairs)
+        ctx.emit_root([f"{o}{d}{fmt(float(score[j]) / max(float(npairs), 1))}" for j, o in enumerate(attrs)])
+        return
+    t = ctx.table(raw_numeric=True, schema=schema)
+    X = t.dense_features()
+    ords = [f.ordinal for f in t.binned_fields] + [f.ordinal for f in t.numeric_fields]
+    s = relief(X, t.labels[: t.n].long(), ctx.get_int("neighbor.count", 1))
+    keep = attrs or ords
+    ctx.emit_root([f"{o}{d}{fmt(float(s[ords.index(o)]))}" for o in keep if o in ords])
+
+
+@job("topMatchesByClass", "same-class nearest neighbours from pair distances (J/explore/TopMatchesByClass.java, tmc.*)")
+def top_matches(args):
+    """Input: ``srcId,trgId,srcRec...,trgRec...,rank`` (recordSimilarity with record output), or
+    ``srcId,trgId,rank`` when ``tmc.include.rec.in.output=false``.  Both directions of every
+    same-class pair are ranked per source (a device segmented sort on (src, rank)); the top
+    ``tmc.top.match.count`` (or all within ``tmc.top.match.distance``) are written per source, one
+    line per neighbour or one compact line (``tmc.compact.output``).  The reference's reducer stops
+    one short of ``top.match.count`` (``++count >= topMatchCount``); here exactly that many are
+    kept."""
+    ctx = JobContext(args, "tmc.")
+    cls_ord = ctx.get_int("class.attr.ord")
+    filt = ctx.get_str("filer.class.value", None)
+    inc_rec = ctx.get_bool("include.rec.in.output", True)
+    by_count = ctx.get_bool("nearest.by.count", True)
+    by_dist = ctx.get_bool("nearest.by.distance", False)
+    topn = ctx.get_int("top.match.count", 10) if by_count else None
+    maxd = ctx.get_int("top.match.distance", 200) if (by_dist or not by_count) else None
+    compact = ctx.get_bool("compact.output", False)
+    inc_cls = ctx.get_bool("include.class.in.output", True)
+    rows = ctx.rows(shard=False)
+    src, trg, rank, cls = [], [], [], []
+    recs = {}
+    for r in rows:
+        L = (len(r) - 3) // 2
+        s_id, t_id = r[0], r[1]
+        s_rec, t_rec = r[2:2 + L], r[2 + L:2 + 2 * L]
+        sc, tc = s_rec[cls_ord], t_rec[cls_ord]
+        if sc != tc or (filt is not None and sc != filt):
+            continue
+        recs[s_id], recs[t_id] = s_rec, t_rec
+        rk = int(float(r[-1]))
+        src += [s_id, t_id]
+        trg += [t_id, s_id]
+        rank += [rk, rk]
+        cls += [sc, sc]
+    ids = sorted(recs)
+    ii = {v: i for i, v in enumerate(ids)}
+    if not src:
+        ctx.emit_root([])
+        return
+    S = torch.tensor([ii[x] for x in src])
+    Tt = torch.tensor([ii[x] for x in trg])
+    Rk = torch.tensor(rank)
+    order = torch.argsort(Rk, stable=True)
+    order = order[torch.argsort(S[order], stable=True)]
+    S, Tt, Rk = S[order], Tt[order], Rk[order]
+    first = torch.ones_like(S, dtype=torch.bool)
+    first[1:] = S[1:] != S[:-1]
+    start = torch.cummax(torch.where(first, torch.arange(len(S)), torch.zeros_like(S)), 0).values
+    pos = torch.arange(len(S)) - start
+    keep = torch.ones_like(S, dtype=torch.bool)
+    if topn is not None:
+        keep &= pos < topn
+    if maxd is not None:
+        keep &= Rk <= maxd
+    d = ctx.delim_out
+    out = defaultdict(list)
+    for s, t in zip(S[keep].tolist(), Tt[keep].tolist()):
+        out[s].append(d.join(recs[ids[t]]) if inc_rec else ids[t])
+    lines = []
+    clsmap = dict(zip(src, cls))
+    for s in sorted(out):
+        head = d.join(recs[ids[s]]) if inc_rec else ids[s]
+        if inc_cls:
+            head += d + clsmap[ids[s]]
+        if compact:
+            lines.append(d.join([head] + out[s]))
+        else:
+            lines += [f"{head}{d}{x}" for x in out[s]]
+    ctx.emit_root(lines)
+
+
+# ================================================================================================
+# samplers
+# ================================================================================================
+@job("underSamplingBalancer", "class-balancing under-sampling (J/explore/UnderSamplingBalancer.java, usb.*)")
+def undersampling(args):
+    """Keeps a record of a class with global count n_c with probability min_c / n_c (the class
+    counts are all-reduced first, instead of the reference's per-mapper warm-up batch estimate)."""
+    ctx = JobContext(args, "usb.")
+    lines = ctx.lines()
+    cls_ord = ctx.get_int("class.attr.ord")
+    sp = ctx.split
+    vals = ctx.union(sp(l)[cls_ord] for l in lines)
+    y = torch.tensor([vals.index(sp(l)[cls_ord]) for l in lines], dtype=torch.long)
+    C = torch.bincount(y, minlength=len(vals)).double()
+    ctx.all_reduce(C)
+    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + 7919 * ctx.comm.rank)
+    minc = float(C[C > 0].min())
+    keep = torch.rand(len(lines), generator=g) < (minc / C.clamp_min(1))[y]
+    ctx.emit([l for l, k in zip(lines, keep.tolist()) if k])
+
+
+@job("baggingSampler", "bootstrap resampling within batches (J/explore/BaggingSampler.java, bas.batch.size)")
+def bagging(args):
+    from ..models.sampling import bagging_indices
+    ctx = JobContext(args, "bas.")
+    lines = ctx.lines()
+    idx = bagging_indices(len(lines), ctx.get_int("batch.size", 10000), seed=ctx.get_int("random.seed", 0) + ctx.comm.rank)
+    ctx.emit([lines[i] for i in idx.tolist()])
+
+
+@job("adaBoostError", "weighted misclassification error (J/explore/AdaBoostError.java, abe.*)")
+def adaboost_error(args):
+    ctx = JobContext(args, "abe.")
+    rows = ctx.rows()
+    po, ao, bo = (ctx.get_int("pred.class.attr.ord"), ctx.get_int("actual.class.attr.ord"),
+                  ctx.get_int("boost.attr.ord"))
+    wrong = torch.tensor([float(r[po] != r[ao]) for r in rows], dtype=torch.float64)
+    w = torch.tensor([float(r[bo]) for r in rows], dtype=torch.float64)
+    acc = torch.stack([(wrong * w).sum(), torch.tensor(float(len(rows)), dtype=torch.float64)])
+    ctx.all_reduce(acc)
+    err = float(acc[0]) if ctx.get_bool("weight.normalized", False) else float(acc[0]) / max(float(acc[1]), 1)
+    ctx.emit_root([f"error={fmt(err, ctx.get_int('output.precision', 6))}"])
+
+
+@job("adaBoostUpdate", "boost weight update from the error file (J/explore/AdaBoostUpdate.java, abu.*)")
+def adaboost_update(args):
+    ctx = JobContext(args, "abu.")
+    err = float(ctx.all_lines(ctx.path("error.file.path"))[0].split("=")[1])
+    alpha = 0.5 * math.log((1.0 - err) / err) if 0 < err < 1 else 0.0
+    po, ao, bo = (ctx.get_int("pred.class.attr.ord"), ctx.get_int("actual.class.attr.ord"),
+                  ctx.get_int("boost.attr.ord"))
+    prec = int(ctx.cfg.values.get("abe.output.precision", 6))
+    init = ctx.get_float("intial.weight", 1.0)
+    rows = ctx.rows()
+    w = torch.tensor([float(r[bo]) for r in rows], dtype=torch.float64)
+    wrong = torch.tensor([r[po] != r[ao] for r in rows])
+    nw = w * torch.exp(torch.where(wrong, torch.full_like(w, alpha), torch.full_like(w, -alpha))) if err < 0.5 \
+        else torch.full_like(w, init)
+    d = ctx.delim_out
+    out = []
+    for r, v in zip(rows, nw.tolist()):
+        r = list(r)
+        r[bo] = fmt(v, prec)
+        out.append(d.join(r))
+    ctx.emit(out)
+
+
+# ================================================================================================
+# split generation (tree building blocks)
+# ================================================================================================
+@job("classPartitionGenerator", "candidate splits with gain ratio per attribute (J/explore/ClassPartitionGenerator.java, cpg.*)",
+     aliases=("splitGenerator",))
+def class_partition(args):
+    """One split-histogram launch over all attributes' candidate splits (K2 over tree-binned
+    codes), all-reduced, then every split's stat from one batched ``[S, G, C]`` contraction.
+    ``cpg.split.attributes`` restricts the attributes; ``cpg.at.root`` emits the root info only."""
+    from ..models.splitstat import class_partition_stats, info_content
+    ctx = JobContext(args, "cpg.")
+    t = ctx.table(raw_numeric=True)
+    alg = ctx.get_str("split.algorithm", "giniIndex")
+    d = ctx.delim_out
+    if ctx.get_bool("at.root", False):
+        C = t.n_classes
+        cnt = torch.bincount(t.labels[: t.n].long().cpu(), minlength=C)[:C].double()
+        ctx.all_reduce(cnt)
+        ctx.emit_root([f"$root{d}{float(info_content(cnt, alg)):.6f}"])
+        return
+    attrs = ctx.get_int_list("split.attributes", None)
+    st = class_partition_stats(t, alg, attrs, comm=ctx.comm)
+    ctx.emit_root([f"{s['attr']}{d}{s['key']}{d}{s['gain_ratio']:.6f}" for s in st])
+
+
+# ================================================================================================
+# encodings / mappers
+# ================================================================================================
+def java_hash(s: str) -> int:
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+def fnv_hash(s: str) -> int:
+    h = 0x811C9DC5
+    for b in s.encode():
+        h ^= b
+        h = (h * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
+@job("categoricalFeatureHashingEncoding", "hashing-trick encoding (S/explore/CategoricalFeatureHashingEncoding.scala)")
+def feature_hashing_job(args):
+    """Index hash = Java ``String.hashCode`` mod ``encoding.size``, sign = FNV-1a parity; the vector
+    replaces the categorical fields at ``encoding.vecOffset`` among the remaining fields.  Values
+    are hashed once per distinct value, the [n, size] encoding is one scatter-add."""
+    ctx = JobContext(args, app="categoricalFeatureHashingEncoding")
+    cat = ctx.get_int_list("cat.fieldOrdinals")
+    size = ctx.get_int("encoding.size")
+    rows = ctx.rows()
+    n = len(rows)
+    vocab: dict[str, int] = {}
+    codes = torch.tensor([[vocab.setdefault(r[o], len(vocab)) for o in cat] for r in rows], dtype=torch.long).view(n, -1)
+    inv = sorted(vocab, key=vocab.get)
+    idx = torch.tensor([abs(java_hash(v)) % size for v in inv], dtype=torch.long)
+    sgn = torch.tensor([1 if fnv_hash(v) % 2 == 1 else -1 for v in inv], dtype=torch.long)
+    enc = torch.zeros((n, size), dtype=torch.long)
+    if n and inv:
+        enc.scatter_add_(1, idx[codes], sgn[codes])
+    rem = [i for i in range(len(rows[0]) if rows else 0) if i not in set(cat)]
+    off = ctx.get_int("encoding.vecOffset", len(rem))
+    d = ctx.delim_out
+    out = []
+    for r, e in zip(rows, enc.tolist()):
+        other = [r[i] for i in rem]
+        out.append(d.join(other[:off] + [str(v) for v in e] + other[off:]))
+    ctx.emit(out)
+
+
+@job("categoricalLeaveOneOutEncoding", "leave-one-out target encoding (S/explore/CategoricalLeaveOneOutEncoding.scala)")
+def loo_encoding(args):
+    """Training set: per (field, value) (count, sum of the +1/-1 target) is all-reduced and saved to
+    ``target.stat.file.path`` as ``field,value,count,sum``; each value is encoded as
+    ``(sum - y) / (count - 1 + reg) * (1 + N(0, rand.std.dev))``.  Validation / test set: the saved
+    stats are loaded and ``sum / (count + reg)`` is used (:66-136)."""
+    ctx = JobContext(args, app="categoricalLeaveOneOutEncoding")
+    cat = ctx.get_int_list("cat.field.ordinals")
+    cls_ord = ctx.get_int("class.field.ordinal")
+    pos = ctx.get_str("class.pos.val", None)
+    reg = ctx.get_float("regularization.factor", 10.0)
+    sd = ctx.get_float("rand.std.dev", 0.3)
+    prec = ctx.get_int("ouput.precision", 3)
+    train = ctx.get_bool("train.data.set", True)
+    stat_path = ctx.get_str("target.stat.file.path", None)
+    rows = ctx.rows()
+    yv = torch.tensor([(1.0 if r[cls_ord] == pos else -1.0) if pos is not None else float(r[cls_ord]) for r in rows],
+                      dtype=torch.float64)
+    keys = ctx.union((o, r[o]) for r in rows for o in cat)
+    ki = {k: i for i, k in enumerate(keys)}
+    K = len(keys)
+    if train:
+        cnt = torch.zeros(K, dtype=torch.float64)
+        sm = torch.zeros(K, dtype=torch.float64)
+        for j, o in enumerate(cat):
+            kk = torch.tensor([ki[(o, r[o])] for r in rows], dtype=torch.long)
+            cnt.index_add_(0, kk, torch.ones_like(yv))
+            sm.index_add_(0, kk, yv)
+        ctx.all_reduce(cnt, sm)
+        if stat_path and ctx.is_root:
+            from pathlib import Path
+            Path(stat_path).parent.mkdir(parents=True, exist_ok=True)
+            Path(stat_path).write_text("\n".join(f"{o}{ctx.delim_out}{v}{ctx.delim_out}{int(cnt[i])}{ctx.delim_out}{int(sm[i])}"
+                                                 for i, (o, v) in enumerate(keys)) + "\n")
+        stats = {k: (float(cnt[i]), float(sm[i])) for k, i in ki.items()}
+    else:
+        stats = {}
+        for l in ctx.all_lines(stat_path):
+            p = ctx.split(l)
+            stats[(int(p[0]), p[1])] = (float(p[2]), float(p[3]))
+    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + ctx.comm.rank)
+    out = []
+    d = ctx.delim_out
+    enc = {}
+    for o in cat:
+        c = torch.tensor([stats[(o, r[o])][0] for r in rows], dtype=torch.float64)
+        s = torch.tensor([stats[(o, r[o])][1] for r in rows], dtype=torch.float64)
+        if train:
+            noise = 1.0 + (torch.randn(len(rows), generator=g, dtype=torch.float64) * sd).clamp(-3 * sd, 3 * sd)
+            enc[o] = ((s - yv) / (c - 1 + reg) * noise).tolist()
+        else:
+            enc[o] = (s / (c + reg)).tolist()
+    for i, r in enumerate(rows):
+        r = list(r)
+        for o in cat:
+            r[o] = fmt(enc[o][i], prec)
+        out.append(d.join(r))
+    ctx.emit(out)
+
+
+@job("binaryDummyVariableGenerator", "one-hot (binary dummy) expansion of categorical fields (S/util/BinaryDummyVariableGenerator.scala)")
+def binary_dummy_job(args):
+    ctx = JobContext(args, app="binaryDummyVariableGenerator")
+    cat = ctx.get_int_list("cat.field.ordinals")
+    tv, fv = ctx.get_str("true.value", "1"), ctx.get_str("false.value", "0")
+    ci = ctx.get_bool("case.insensitive", False)
+    rows = ctx.rows()
+    uniq = {}
+    for o in cat:
+        u = ctx.cfg.get_list(f"fieldUniqueValues.{o}", None)
+        if u is None:
+            u = ctx.union(r[o] for r in rows)
+        uniq[o] = [x.lower() for x in u] if ci else u
+    d = ctx.delim_out
+    out = []
+    for r in rows:
+        parts = []
+        for i, v in enumerate(r):
+            if i in uniq:
+                vv = v.lower() if ci else v
+                parts += [tv if vv == u else fv for u in uniq[i]]
+            else:
+                parts.append(v)
+        out.append(d.join(parts))
+    ctx.emit(out)
+
+
+@job("linearMapper", "linear transform of numeric fields y = M x (S/util/LinearMapper.scala)")
+def linear_mapper(args):
+    """``trans.matrix.path`` rows of M (comma separated); output ``ids, y..., retained fields``;
+    the transform of the whole shard is one GEMM on the device."""
+    ctx = JobContext(args, app="linearMapper")
+    ids = ctx.get_int_list("id.field.ordinals", [])
+    q = ctx.get_int_list("quant.field.ordinals")
+    ret = ctx.get_int_list("retained.field.ordinals", [])
+    prec = ctx.get_int("output.precision", 3)
+    M = torch.tensor([[float(x) for x in l.split(",")] for l in ctx.all_lines(ctx.path("trans.matrix.path"))],
+                     dtype=torch.float64, device=ctx.device)
+    rows = ctx.rows()
+    X = torch.tensor([[float(r[o]) for o in q] for r in rows], dtype=torch.float64, device=ctx.device).view(len(rows), len(q))
+    Y = (X @ M.T).cpu().tolist()
+    d = ctx.delim_out
+    ctx.emit([d.join([r[o] for o in ids] + [fmt(v, prec) for v in y] + [r[o] for o in ret]) for r, y in zip(rows, Y)])
+
+
+@job("incrementalPrincipalComponent", "streaming PCA per key with persisted state (S/explore/IncrementalPrincipalComponent.scala)")
+def incremental_pca(args):
+    """Records ``id...,x1..xD`` grouped by key; the state file (``state.filePath``) of the previous
+    run is loaded when it exists and written back (PrincipalCompState text blocks); all keys are
+    updated together by the batched GHA recursion of ``analytics/pca.py``."""
+    from pathlib import Path
+    from ..analytics.pca import IncrementalPCA, PrincipalCompState
+    ctx = JobContext(args, app="incrementalPrincipalComponent")
+    ids = ctx.get_int_list("id.field.ordinals")
+    q = ctx.get_int_list("quant.field.ordinals")
+    prec = ctx.get_int("output.precision", 3)
+    groups = defaultdict(list)
+    for r in ctx.rows(shard=False):
+        groups[":".join(r[o] for o in ids)].append([float(r[o]) for o in q])
+    keys = sorted(groups)
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
+        keys = keys[a:b]
+    ipca = IncrementalPCA(len(q), forget=ctx.get_float("forget.factor", 0.96),
+                          low_energy=ctx.get_float("energy.lowThreshold", 0.95),
+                          high_energy=ctx.get_float("energy.highThreshold", 0.98), device=ctx.device)
+    sp = ctx.get_str("state.filePath", None)
+    d = ctx.delim_out
+    if sp and Path(sp).exists():
+        blk = ctx.all_lines(sp)
+        i = 0
+        while i < len(blk):
+            nh = int(blk[i].split(d)[2])
+            st = PrincipalCompState.load(blk[i:i + 3 + nh], d)
+            ipca.states[st.key] = st
+            i += 3 + nh
+    states = ipca.update({k: torch.tensor(groups[k], dtype=torch.float64) for k in keys})
+    lines = [l for k in keys for l in states[k].serialize(d, prec)]
+    lines = ctx.gather_lines(lines)
+    if sp and ctx.is_root:
+        Path(sp).parent.mkdir(parents=True, exist_ok=True)
+        Path(sp).write_text("\n".join(lines) + "\n")
+    ctx.emit_root(lines)
+
+
+@job("individualConditionalExpectation", "ICE curves by grid expansion + in-process batched model inference (S/interpret/IndividualConditionalExpectation.scala)")
+def ice_job(args):
+    """Input ``key...,x1..xD``; ``ice.feature.ordinal`` (feature index within x) is varied over
+    ``ice.feature.values``; the reference HTTP-POSTs every grid batch to a prediction service, here
+    the model (``--kind`` + ``--config``, the P/supv classifier drivers) scores the whole expanded
+    grid in one batched call.  Output ``key...,value,prediction`` sorted by prediction per key
+    (descending by default)."""
+    from ..models import supervised as SV
+    ctx = JobContext(args, app="individualConditionalExpectation")
+    kl = ctx.get_int("data.keyLen")
+    feat = ctx.get_int("feature.ordinal")
+    vals = ctx.get_float_list("feature.values")
+    desc = ctx.get_bool("prediction.sortDescending", True)
+    prec = ctx.get_int("output.precision", 3)
+    cls = {"rf": SV.RandomForest, "gbt": SV.GradientBoostedTrees, "svm": SV.SupportVectorMachine,
+           "lr": SV.LogisticRegressionDiscriminant}[args.kind]
+    model = cls(ctx.get_str("model.config", None) or args.model, device=args.device)
+    model.train()
+    rows = ctx.rows()
+    X = torch.tensor([[float(v) for v in r[kl:]] for r in rows], dtype=torch.float64)
+    G = X.repeat_interleave(len(vals), 0)
+    G[:, feat] = torch.tensor(vals, dtype=torch.float64).repeat(len(rows))
+    p = model.predictProb(G.numpy())
+    p = torch.as_tensor(p)
+    p = p[:, -1] if p.dim() == 2 else p
+    p = p.view(len(rows), len(vals))
+    d = ctx.delim_out
+    out = []
+    for i, r in enumerate(rows):
+        order = sorted(range(len(vals)), key=lambda j: float(p[i, j]), reverse=desc)
+        out += [d.join(r[:kl] + [f"{vals[j]:g}", fmt(float(p[i, j]), prec)]) for j in order]
+    ctx.emit(out)
+
+
+# ================================================================================================
+# discriminant analysis / SVM
+# ================================================================================================
+@job("fisherDiscriminant", "univariate Fisher discriminant per attribute, binary class (J/discriminant/FisherDiscriminant.java)")
+def fisher(args):
+    from ..models.linear import fisher_discriminant, fisher_lines
+    ctx = JobContext(args, "fid.")
+    t = ctx.table(raw_numeric=True)
+    X = t.dense_features()
+    r = fisher_discriminant(X, t.labels[: t.n].long(), comm=ctx.comm)
+    ords = [f.ordinal for f in t.binned_fields] + [f.ordinal for f in t.numeric_fields]
+    d = ctx.delim_out
+    ctx.emit_root([d.join([str(o)] + l.split(",")[1:]) for o, l in zip(ords, fisher_lines(r.cpu()))])
+
+
+@job("supportVectorMachine", "cascade SVM: per-rank SMO, all-gather of support vectors, final SMO (J/discriminant/SupportVectorMachine.java)")
+def svm_job(args):
+    """Output: one line per final support vector ``alpha,classValue,x...`` then ``bias,<b>``
+    (decision f(x) = sum alpha_i y_i K(x_i, x) + b)."""
+    from ..models.svm import CascadeSVM
+    ctx = JobContext(args, "svm.")
+    t = ctx.table(raw_numeric=True)
+    X = t.dense_features().float()
+    y = t.labels[: t.n].long()
+    pos = ctx.get_str("positive.class.value", None)
+    vals = t.class_field.cardinality
+    pi = vals.index(pos) if pos in vals else 1
+    yb = (y == pi).long()
+    m = CascadeSVM(comm=ctx.comm, C=ctx.get_float("penalty.factor", 1.0), kernel=ctx.get_str("kernel.type", "linear"),
+                   gamma=ctx.get_float("kernel.param", 1.0)).fit(X, yb)
+    d = ctx.delim_out
+    sv = m.model
+    coef = sv.dual_coef[0].cpu().tolist()
+    lines = [d.join([f"{abs(a):.6f}", vals[pi] if a > 0 else vals[1 - pi]] + [f"{v:.6f}" for v in x])
+             for a, x in zip(coef, sv.sv_X.cpu().tolist())]
+    lines.append(f"bias{d}{-float(sv.rho[0]):.6f}")
+    ctx.emit_root(lines)

@@ -1,0 +1,667 @@
+"""Association, clustering, nearest-neighbour pipeline, model-prediction, batch-bandit, similarity
+and population-optimiser jobs (J/association, J/cluster, J/knn, J/model, J/tree/DataPartitioner,
+J/reinforce batch bandits, S/similarity, S/cluster/KMeansPlusPlusCluster, S/optimize)."""
+from __future__ import annotations
+
+import itertools
+import json
+import math
+from collections import defaultdict
+from pathlib import Path
+
+import torch
+
+from .common import JobContext, fmt, job
+
+
+# ================================================================================================
+# association rules
+# ================================================================================================
+@job("associationRuleMiner", "rules antecedent -> consequent from frequent item sets (J/association/AssociationRuleMiner.java, arm.*)")
+def rule_miner(args):
+    """Input: frequent item-set lines ``item,...,support`` (frequentItemsApriori output, all
+    lengths).  Every proper subset (size <= ``arm.max.ante.size``) of a set is an antecedent;
+    confidence = support(set) / support(antecedent); lines ``a,b -> c`` when above
+    ``arm.conf.threshold`` (:111-196)."""
+    ctx = JobContext(args, "arm.")
+    max_ante = ctx.get_int("max.ante.size", 3)
+    thr = ctx.get_float("conf.threshold")
+    sup = {}
+    for r in ctx.rows(shard=False):
+        sup[tuple(r[:-1])] = float(r[-1])
+    items = sorted(sup)
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(items), ctx.comm.rank, ctx.comm.world)
+        items = items[a:b]
+    out = []
+    for s in items:
+        if len(s) < 2:
+            continue
+        for k in range(1, min(max_ante, len(s) - 1) + 1):
+            for ante in itertools.combinations(s, k):
+                sa = sup.get(ante)
+                if sa is None:
+                    sa = sup.get(tuple(sorted(ante)))
+                if not sa:
+                    continue
+                if sup[s] / sa > thr:
+                    cons = [x for x in s if x not in ante]
+                    out.append(",".join(ante) + " -> " + ",".join(cons))
+    out = ctx.gather_lines(out)
+    ctx.emit_root(out)
+
+
+@job("infrequentItemMarker", "replace items outside the frequent 1-item sets by a marker (J/association/InfrequentItemMarker.java, iim.*)")
+def infrequent_marker(args):
+    ctx = JobContext(args, "iim.")
+    skip = ctx.get_int("skip.field.count", 1)
+    marker = ctx.get_str("infreq.item.marker", "*")
+    freq = set()
+    for r in ctx.rows(ctx.path("item.set.file.path", "model"), shard=False):
+        if len(r) == 2 or ctx.get_int("item.set.length", 1) == 1:
+            freq.add(r[0])
+    d = ctx.delim_out
+    ctx.emit([d.join(r[:skip] + [x if x in freq else marker for x in r[skip:]]) for r in ctx.rows()])
+
+
+# ================================================================================================
+# clustering
+# ================================================================================================
+@job("entityDistanceStore", "build the memory-mapped entity-distance store from pair distances (J/util/EntityDistanceMapFileAccessor.java)")
+def distance_store(args):
+    """Input either ``entity,e1:d1,e2:d2,...`` lines or ``e1,e2,dist`` pair lines
+    (``eds.pair.input=true``, e.g. sameTypeSimilarity / recordSimilarity output)."""
+    from ..utils.distance_store import EntityDistanceStore
+    ctx = JobContext(args, "eds.")
+    lines = ctx.all_lines()
+    if ctx.get_bool("pair.input", False):
+        rows = [ctx.split(l) for l in lines]
+        EntityDistanceStore.write_pairs([r[0] for r in rows], [r[1] for r in rows], [float(r[2]) for r in rows],
+                                        args.output)
+    else:
+        EntityDistanceStore.write_text(lines, args.output, ctx.delim_in if len(ctx.delim_in) == 1 else ",",
+                                       ctx.get_str("sub.field.delim", ":"))
+
+
+@job("agglomerativeGraphical", "greedy edge-weighted clustering over a persisted distance store (J/cluster/AgglomerativeGraphical.java, agg.*)")
+def agglomerative(args):
+    """Entities (first field of each input line) join the cluster with the best new average edge
+    weight above ``agg.min.av.edge.weight.threshold`` (``agg.distance.scale`` turns distances into
+    similarities); the store is ``agg.distance.store.path`` (entityDistanceStore output).  Output:
+    ``clusterIndex,member,...,avgEdgeWeight``."""
+    from ..utils.distance_store import EntityDistanceStore, agglomerative_graphical
+    ctx = JobContext(args, "agg.")
+    store = EntityDistanceStore(ctx.path("distance.store.path", "model"))
+    ents = [r[0] for r in ctx.rows(shard=False)]
+    scale = ctx.get_float("distance.scale", None)
+    cl = agglomerative_graphical(store, ents, ctx.get_float("min.av.edge.weight.threshold"), scale)
+    d = ctx.delim_out
+    ctx.emit_root([d.join([str(i)] + m + [repr(w)]) for i, (m, w) in enumerate(cl)])
+
+
+@job("kMeansPlusPlusCluster", "k-means++ per key group and per k, knuckle-point k (S/cluster/KMeansPlusPlusCluster.scala)")
+def kmeanspp(args):
+    """Records ``key..,x1..xD`` grouped by ``id.fieldOrdinals``; for every group and every k of
+    ``num.clusters`` a D^2-seeded k-means (``num.clustGroup`` restarts, ``num.iter`` Lloyd steps) runs
+    batched on the device; output per group: ``key..,k,sse`` lines and ``key..,knuckle,k``; the
+    centroids go to ``cluster.outputPath`` as ``key..,k,i,c..``."""
+    from ..models.cluster import KMeans
+    ctx = JobContext(args, app="kMeansPlusPlusCluster")
+    kords = ctx.get_int_list("id.fieldOrdinals", []) if ctx.get_str("id.fieldOrdinals", "") else []
+    ks = ctx.get_int_list("num.clusters")
+    prec = ctx.get_int("output.precision", 3)
+    attrs = ctx.get_int_list("attr.ordinals", None)
+    groups = defaultdict(list)
+    for r in ctx.rows(shard=False):
+        cols = attrs or [i for i in range(len(r)) if i not in kords]
+        groups[tuple(r[o] for o in kords)].append([float(r[c]) for c in cols])
+    keys = sorted(groups)
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
+        keys = keys[a:b]
+    d = ctx.delim_out
+    out, cents = [], []
+    from ..parallel.comm import Comm
+    local = _LocalComm()
+    for k in keys:
+        X = torch.tensor(groups[k], dtype=torch.float32, device=ctx.device)
+        kk = [c for c in ks if c <= X.shape[0]]
+        km = KMeans(kk, n_init=ctx.get_int("num.clustGroup", 10), max_iter=ctx.get_int("num.iter", 10),
+                    init="k-means++", comm=local).fit(X)
+        for c in kk:
+            run = km.best[c]
+            out.append(d.join(list(k) + [str(c), fmt(run.sse, prec)]))
+            cents += [d.join(list(k) + [str(c), str(i)] + [fmt(v, prec) for v in cc])
+                      for i, cc in enumerate(run.centroids.cpu().tolist())]
+        if len(kk) > 2:
+            out.append(d.join(list(k) + ["knuckle", str(km.knuckle_k())]))
+    ctx.emit(out)
+    cp = ctx.get_str("cluster.outputPath", None)
+    if cp:
+        ctx.emit(cents, cp)
+
+
+class _LocalComm:
+    """Single-process view: per-key models are independent (no cross-rank reduction)."""
+    world, rank, is_distributed, is_root = 1, 0, False, True
+
+    def all_reduce(self, t, op="sum"):
+        return t
+
+    def all_reduce_coalesced(self, ts, op="sum"):
+        return None
+
+    def barrier(self):
+        return None
+
+
+# ================================================================================================
+# nearest-neighbour pipeline (R/knn.sh)
+# ================================================================================================
+@job("sameTypeSimilarity", "mixed-type all-pairs distances between a training and a test set (sifarish SameTypeSimilarity, R/knn.sh computeDistance)")
+def same_type_similarity(args):
+    """Both sets (``--train`` and ``--input``; or one input with ``sts.base.set.split.prefix``
+    file-name prefixes) are encoded with the schema's mixed-type distance (numeric range-scaled,
+    categorical mismatch, field weights) into a euclidean embedding, and the distances of every
+    (train, test) pair are one device GEMM per block.  Output (``sts.output.id.first``):
+    ``trainId,testId,dist*scale,trainClass,testClass`` — the layout the NearestNeighbor mapper
+    and FeatureCondProbJoiner read (J/knn/NearestNeighbor.java:130-183).  ``sts.top.match.count``
+    keeps only the k nearest train records per test record (fused distance + top-k kernel)."""
+    from ..ops.distance import encode_mixed, knn, pairwise
+    ctx = JobContext(args, "sts.")
+    schema = ctx.schema("same.schema.file.path")
+    if args.train:
+        tr_path, te_path = args.train, args.input
+    else:
+        from .common import input_files
+        pref = ctx.get_str("base.set.split.prefix", "tr")
+        files = input_files(args.input)
+        tr_path = ",".join(str(f) for f in files if f.name.startswith(pref))
+        te_path = ",".join(str(f) for f in files if not f.name.startswith(pref))
+    tr = ctx.table(path=tr_path, schema=schema, shard=False, raw_numeric=True)
+    te = ctx.table(path=te_path, schema=schema, raw_numeric=True)
+    ranges = {}
+    for j, f in enumerate(tr.numeric_fields):
+        x = torch.cat([tr.numeric[j, : tr.n], te.numeric[j, : te.n].to(tr.numeric.device)])
+        lo, hi = torch.nan_to_num(x).min(), torch.nan_to_num(x).max()
+        if ctx.comm.is_distributed:
+            lo, hi = lo.clone().view(1), hi.clone().view(1)
+            ctx.comm.all_reduce(lo, "min")
+            ctx.comm.all_reduce(hi, "max")
+        ranges[f.ordinal] = (float(f.min) if f.min is not None else float(lo), float(f.max) if f.max is not None else float(hi))
+    A = encode_mixed(tr, ranges=ranges)
+    B = encode_mixed(te, ranges=ranges)
+    nf = max(1, len(tr.numeric_fields) + len(tr.binned_fields))
+    scale = ctx.get_float("distance.scale", 1000.0)
+    topk = ctx.get_int("top.match.count", 0)
+    cls_tr = tr.label_values() if tr.labels is not None else [""] * tr.n
+    cls_te = te.label_values() if te.labels is not None else [""] * te.n
+    id_tr = tr.ids or [str(i) for i in range(tr.n)]
+    id_te = te.ids or [str(i + te.row_offset) for i in range(te.n)]
+    d = ctx.delim_out
+    out = []
+    if topk > 0:
+        dist, idx = knn(B, A, topk, "euclidean")
+        dist = (dist / math.sqrt(nf) * scale).round().long().cpu().tolist()
+        for q, (dr, ir) in enumerate(zip(dist, idx.cpu().tolist())):
+            for dd, i in zip(dr, ir):
+                if i >= 0:
+                    out.append(d.join([id_tr[i], id_te[q], str(dd), cls_tr[i], cls_te[q]]))
+    else:
+        for s in range(0, te.n, 4096):
+            D = (pairwise(B[s:s + 4096], A) / math.sqrt(nf) * scale).round().long().cpu()
+            for q in range(D.shape[0]):
+                row = D[q].tolist()
+                out += [d.join([id_tr[i], id_te[s + q], str(row[i]), cls_tr[i], cls_te[s + q]]) for i in range(tr.n)]
+    ctx.emit(out)
+
+
+@job("featureCondProbJoiner", "join NB feature posteriors of training records onto distance pairs (J/knn/FeatureCondProbJoiner.java, fcb.*)")
+def cond_prob_joiner(args):
+    """Input: the distance pairs and the ``bayesianPredictor`` prob-only files (file name prefix
+    ``fcb.feature.cond.prob.split.prefix``).  Output per pair:
+    ``testId,testClass,trainId,distance,trainClass,trainClassPostProb`` (:153-178)."""
+    from .common import input_files
+    ctx = JobContext(args, "fcb.")
+    pref = ctx.get_str("feature.cond.prob.split.prefix", "condProb")
+    files = input_files(args.input)
+    if args.model:
+        files += input_files(args.model)
+    prob_files = [f for f in files if f.name.startswith(pref)]
+    pair_files = [f for f in files if not f.name.startswith(pref)]
+    sp = ctx.split
+    post = {}
+    for f in prob_files:
+        for l in f.read_text().splitlines():
+            if not l.strip():
+                continue
+            p = sp(l)
+            cls = p[-1]
+            for i in range(2, len(p) - 1, 2):
+                if p[i] == cls:
+                    post[p[0]] = (cls, p[i + 1])
+                    break
+    d = ctx.delim_out
+    lines = [l for f in pair_files for l in f.read_text().splitlines() if l.strip()]
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(lines), ctx.comm.rank, ctx.comm.world)
+        lines = lines[a:b]
+    out = []
+    for l in lines:
+        p = sp(l)
+        if p[0] in post:
+            c, pr = post[p[0]]
+            out.append(d.join([p[1], p[4], p[0], p[2], c, pr]))
+    ctx.emit(out)
+
+
+@job("nearestNeighbor", "kNN from precomputed distance pairs (J/knn/NearestNeighbor.java, nen.*; R/knn.sh knnClassifier)")
+def nearest_neighbor(args):
+    """Input pairs ``trainId,testId,dist,trainClass[,testClass]`` or, class-conditioned, the
+    joiner's ``testId,testClass,trainId,dist,trainClass,postProb``.  Per test record the
+    ``nen.top.match.count`` nearest (device segmented sort on (test, distance)) are scored by the
+    kernel function of ``models/knn.NearestNeighbor`` (none / linearMultiplicative / linearAdditive
+    / gaussian, optional inverse-distance and class-conditional weights) and classified (max score,
+    decision threshold or cost-based).  Output ``testId[,cls,score...][,actual],predicted``
+    (:317-406); ``Validation`` counters on stdout."""
+    from ..models.knn import NearestNeighbor
+    ctx = JobContext(args, "nen.")
+    val = ctx.get_bool("validation.mode", True)
+    ccw = ctx.get_bool("class.condtion.weighted", False) or ctx.get_bool("class.condition.weighted", False)
+    k = ctx.get_int("top.match.count", 10)
+    out_distr = ctx.get_bool("output.class.distr", False)
+    rows = ctx.rows(shard=False)
+    if ccw:
+        te_id = [r[0] for r in rows]
+        te_cls = [r[1] for r in rows]
+        dist = [float(r[3]) for r in rows]
+        tr_cls = [r[4] for r in rows]
+        w = [float(r[5]) for r in rows]
+    else:
+        te_id = [r[1] for r in rows]
+        dist = [float(r[2]) for r in rows]
+        tr_cls = [r[3] for r in rows]
+        te_cls = [r[4] if len(r) > 4 else "" for r in rows]
+        w = None
+    classes = ctx.get_list("class.attribute.values", None) or sorted(set(tr_cls))
+    ci = {c: i for i, c in enumerate(classes)}
+    tests = sorted(set(te_id))
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(tests), ctx.comm.rank, ctx.comm.world)
+        mine = set(tests[a:b])
+        sel = [i for i, t in enumerate(te_id) if t in mine]
+        tests = tests[a:b]
+    else:
+        sel = list(range(len(rows)))
+    ti = {t: i for i, t in enumerate(tests)}
+    T = torch.tensor([ti[te_id[i]] for i in sel], dtype=torch.long)
+    Dv = torch.tensor([dist[i] for i in sel], dtype=torch.float64)
+    Cv = torch.tensor([ci[tr_cls[i]] for i in sel], dtype=torch.long)
+    order = torch.argsort(Dv, stable=True)
+    order = order[torch.argsort(T[order], stable=True)]
+    T, Dv, Cv = T[order], Dv[order], Cv[order]
+    Wv = torch.tensor([w[sel[i]] for i in order.tolist()], dtype=torch.float64) if w is not None else None
+    first = torch.ones_like(T, dtype=torch.bool)
+    first[1:] = T[1:] != T[:-1]
+    start = torch.cummax(torch.where(first, torch.arange(len(T)), torch.zeros_like(T)), 0).values
+    rank = torch.arange(len(T)) - start
+    keep = rank < k
+    nn = NearestNeighbor.from_config(ctx.cfg)
+    nt, C = len(tests), len(classes)
+    dk = torch.full((nt, k), math.inf, dtype=torch.float32)
+    ck = torch.zeros((nt, k), dtype=torch.long)
+    dk[T[keep], rank[keep]] = (Dv[keep] / 1000.0).float()     # distances are scaled by 1000 upstream
+    ck[T[keep], rank[keep]] = Cv[keep]
+    s = nn._kernel_scores(dk)
+    if Wv is not None:
+        wk = torch.zeros((nt, k), dtype=torch.float32)
+        wk[T[keep], rank[keep]] = Wv[keep].float()
+        s = s * wk
+    scores = torch.zeros((nt, C), dtype=torch.float32).scatter_add_(1, ck, s.float())
+    pred = scores.argmax(1)
+    if nn.decision_threshold > 0 and C == 2:
+        ratio = scores[:, 1] / scores[:, 0].clamp_min(1e-12)
+        pred = (ratio > nn.decision_threshold).long()
+    actual = {}
+    for i in sel:
+        actual[te_id[i]] = te_cls[i]
+    d = ctx.delim_out
+    out = []
+    correct = 0
+    for t, name in enumerate(tests):
+        parts = [name]
+        if out_distr:
+            for c in range(C):
+                parts += [classes[c], f"{float(scores[t, c]):g}"]
+        if val:
+            parts.append(actual[name])
+        pv = classes[int(pred[t])]
+        parts.append(pv)
+        correct += int(val and actual[name] == pv)
+        out.append(d.join(parts))
+    ctx.emit(out)
+    if val:
+        acc = torch.tensor([float(correct), float(len(tests))])
+        ctx.all_reduce(acc)
+        ctx.report({"Validation": {"Correct": int(acc[0]), "Incorrect": int(acc[1] - acc[0])}})
+
+
+# ================================================================================================
+# model prediction / data partitioning
+# ================================================================================================
+@job("modelPredictor", "decision-tree model (ensemble) predictor (J/model/ModelPredictor.java, mop.*)")
+def model_predictor(args):
+    """``mop.model.dir.path`` + ``mop.model.file.names`` (decision-path JSON or native tree state
+    files; several = weighted voting ensemble), ``mop.output.mode`` withRecord | withKId |
+    withActualClassAttr; the error rate goes to ``map.error.rate.file.path`` when given."""
+    from ..models.tree import DecisionPathModel
+    ctx = JobContext(args, "mop.")
+    mdir = Path(ctx.path("model.dir.path", "model"))
+    names = ctx.get_list("model.file.names", None) or sorted(p.name for p in mdir.glob("*.json"))
+    models = [DecisionPathModel(json.loads((mdir / n).read_text())) for n in names]
+    weights = ctx.get_float_list("ensemble.memeber.weights", None) or [1.0] * len(models)
+    classes = sorted({c for m in models for c in m.class_values})
+    rows = ctx.rows()
+    votes = torch.zeros((len(rows), len(classes)), dtype=torch.float64)
+    for m, w in zip(models, weights):
+        pr, _ = m.predict_proba_rows(rows)
+        idx = torch.tensor([classes.index(c) for c in m.class_values], dtype=torch.long)
+        win = idx[pr.argmax(1)]
+        votes.scatter_add_(1, win.view(-1, 1), torch.full((len(rows), 1), float(w), dtype=torch.float64))
+    pred = votes.argmax(1).tolist()
+    mode = ctx.get_str("output.mode", "withRecord")
+    id_o = ctx.get_int("rec.id.ordinal", 0)
+    co = ctx.get_int("rec.class.attr.ordinal", ctx.get_int("class.attr.ord", -1))
+    d = ctx.delim_out
+    out, errors, total = [], 0, 0
+    for r, p in zip(rows, pred):
+        pv = classes[p]
+        if co >= 0 and co < len(r):
+            total += 1
+            errors += int(r[co] != pv)
+        if mode == "withKId":
+            out.append(f"{r[id_o]}{d}{pv}")
+        elif mode == "withActualClassAttr":
+            out.append(f"{r[id_o]}{d}{r[co]}{d}{pv}")
+        else:
+            out.append(f"{d.join(r)}{d}{pv}")
+    ctx.emit(out)
+    err = torch.tensor([float(errors), float(total)])
+    ctx.all_reduce(err)
+    rate = float(err[0]) / max(float(err[1]), 1)
+    ep = ctx.cfg.values.get("map.error.rate.file.path")
+    if ep and ctx.is_root:
+        Path(ep).parent.mkdir(parents=True, exist_ok=True)
+        Path(ep).write_text(f"errorRate={rate:.6f}\n")
+    ctx.report({"errorRate": rate})
+
+
+@job("dataPartitioner", "partition records by the best (or random top) split of classPartitionGenerator (J/tree/DataPartitioner.java, dap.*)")
+def data_partitioner(args):
+    """Split candidates ``attr,splitKey,stat`` from ``dap.split.path``; ``dap.split.selection.strategy``
+    best (max stat) or randomAmongTop (``dap.num.top.splits``); records are routed by the split's
+    segment index (the K bucketize op) into ``<out>/split=<attr>/segment=<j>/part-NNNNN``."""
+    from ..models.splitstat import parse_split_key
+    ctx = JobContext(args, "dap.")
+    schema = ctx.schema()
+    cands = [ctx.split(l) for l in ctx.all_lines(ctx.path("split.path", "model"))]
+    cands.sort(key=lambda p: -float(p[-1]))
+    strat = ctx.get_str("split.selection.strategy", "best")
+    if strat == "best":
+        pick = cands[0]
+    else:
+        g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0))
+        pick = cands[int(torch.randint(0, min(ctx.get_int("num.top.splits", 5), len(cands)), (1,), generator=g))]
+    attr = int(pick[0])
+    key = ",".join(pick[1:-1]) if len(pick) > 3 else pick[1]
+    f = schema.find_field_by_ordinal(attr)
+    rows = ctx.rows()
+    if f.is_categorical:
+        groups = parse_split_key(key, "cat")
+        lut = {v: j for j, g in enumerate(groups) for v in g}
+        seg = [lut.get(r[attr], len(groups) - 1) for r in rows]
+    else:
+        pts = torch.tensor(parse_split_key(key, "num"), dtype=torch.float64)
+        x = torch.tensor([float(r[attr]) for r in rows], dtype=torch.float64)
+        seg = torch.bucketize(x, pts, right=False).tolist()
+    d = ctx.delim_out
+    by = defaultdict(list)
+    for r, s in zip(rows, seg):
+        by[s].append(d.join(r))
+    base = Path(args.output) / f"split={attr}"
+    for s, ls in sorted(by.items()):
+        p = base / f"segment={s}"
+        p.mkdir(parents=True, exist_ok=True)
+        (p / f"part-{ctx.comm.rank:05d}").write_text("\n".join(ls) + "\n")
+    ctx.report({"split": attr, "key": key, "segments": len(by)})
+
+
+# ================================================================================================
+# batch bandits (MR map-only, per group)
+# ================================================================================================
+def _batch_bandit(args, prefix: str, strategy_fn):
+    from ..models.bandit import batch_select
+    ctx = JobContext(args, prefix)
+    rows = ctx.rows(shard=False)
+    co, ro = ctx.get_int("count.ordinal", 2), ctx.get_int("reward.ordinal", 3)
+    groups = sorted({r[0] for r in rows})
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(groups), ctx.comm.rank, ctx.comm.world)
+        groups = groups[a:b]
+    gi = {g: i for i, g in enumerate(groups)}
+    items = defaultdict(list)
+    for r in rows:
+        if r[0] in gi:
+            items[r[0]].append((r[1], float(r[co]) if co >= 0 else 0.0, float(r[ro]) if ro >= 0 else 0.0))
+    I = max([len(v) for v in items.values()] + [1])
+    G = len(groups)
+    cnt = torch.zeros((G, I), dtype=torch.float64)
+    rew = torch.full((G, I), 0.0, dtype=torch.float64)
+    valid = torch.zeros((G, I), dtype=torch.bool)
+    for g, lst in items.items():
+        for j, (_, c, w) in enumerate(lst):
+            cnt[gi[g], j], rew[gi[g], j], valid[gi[g], j] = c, w * max(c, 1.0) if ctx.get_bool("reward.is.mean", True) else w, True
+    bs = {}
+    cp = ctx.get_str("group.item.count.path", None)
+    if cp and Path(cp).exists():
+        for l in ctx.all_lines(cp):
+            p = ctx.split(l)
+            bs[p[0]] = int(p[1])
+    glob = ctx.get_int("global.batch.size", 1)
+    rnd = ctx.get_int("current.round.num", 1)
+    kmax = max([bs.get(g, glob) for g in groups] + [1])
+    sel = strategy_fn(ctx, cnt, rew, valid, kmax, rnd, batch_select)
+    d = ctx.delim_out
+    out = []
+    for g in groups:
+        k = min(bs.get(g, glob), len(items[g]))
+        for j in sel[gi[g], :k].tolist():
+            if j < len(items[g]):
+                out.append(f"{g}{d}{items[g][j][0]}")
+    ctx.emit(out)
+
+
+def _mask(score, valid):
+    return torch.where(valid, score, torch.full_like(score, -math.inf))
+
+
+@job("greedyRandomBandit", "epsilon-greedy / Auer greedy batch selection per group (J/reinforce/GreedyRandomBandit.java)")
+def greedy_random_bandit(args):
+    def fn(ctx, cnt, rew, valid, k, rnd, batch_select):
+        alg = ctx.get_str("prob.reduction.algorithm", "linear")
+        strat = {"linear": "linear", "logLinear": "logLinear", "auerGreedy": "auerGreedy"}.get(alg, "linear")
+        sel = batch_select(cnt, _mask(rew, valid).nan_to_num(neginf=-1e30), k, strat, rnd,
+                           epsilon=ctx.get_float("random.selection.prob", 0.5), seed=ctx.get_int("random.seed", 0))
+        return sel
+    _batch_bandit(args, "", fn)
+
+
+@job("auerDeterministic", "deterministic UCB1 batch selection per group (J/reinforce/AuerDeterministic.java)")
+def auer_det(args):
+    def fn(ctx, cnt, rew, valid, k, rnd, batch_select):
+        cnt = torch.where(valid, cnt, torch.full_like(cnt, 1e30))
+        return batch_select(cnt, rew, k, "auerDeterministic", rnd)
+    _batch_bandit(args, "", fn)
+
+
+@job("softMaxBandit", "softmax batch selection per group (J/reinforce/SoftMaxBandit.java)")
+def softmax_bandit(args):
+    def fn(ctx, cnt, rew, valid, k, rnd, batch_select):
+        rew = torch.where(valid, rew, torch.full_like(rew, -1e30))
+        return batch_select(cnt.clamp_min(1), rew, k, "softMax", rnd, temp=ctx.get_float("temp.constant", 1.0),
+                            seed=ctx.get_int("random.seed", 0))
+    _batch_bandit(args, "", fn)
+
+
+@job("randomFirstGreedyBandit", "explore-first then greedy batch selection (J/reinforce/RandomFirstGreedyBandit.java)")
+def random_first_bandit(args):
+    def fn(ctx, cnt, rew, valid, k, rnd, batch_select):
+        from ..models.bandit import pac_exploration_count
+        I = int(valid.sum(1).max())
+        if ctx.get_str("exploration.count.strategy", "simple") == "pac":
+            ex = pac_exploration_count(I, ctx.get_float("pac.reward.diff", 0.2), ctx.get_float("pac.prob.diff", 0.2))
+        else:
+            ex = ctx.get_int("exploration.count.factor", 2) * I
+        ex = max(1, ex // max(k, 1))
+        rew = torch.where(valid, rew, torch.full_like(rew, -1e30))
+        return batch_select(cnt.clamp_min(1), rew, k, "randomFirst", rnd, explore_count=ex, seed=ctx.get_int("random.seed", 0))
+    _batch_bandit(args, "", fn)
+
+
+# ================================================================================================
+# record similarity
+# ================================================================================================
+def _numeric_matrix(ctx, rows, ords):
+    return torch.tensor([[float(r[o]) for o in ords] for r in rows], dtype=torch.float32, device=ctx.device)
+
+
+@job("recordSimilarity", "all-pairs record distances, optionally between two sets (S/similarity/RecordSimilarity.scala, chombo RecordSimilarity)")
+def record_similarity(args):
+    """Numeric fields ``attr.ordinals`` (range-normalised), ids at ``id.ordinal``; distances of all
+    pairs (i < j within one set, or every (base, other) pair with ``--train``) are a tiled device
+    GEMM; the pair loop runs in ``ring`` order over the ranks' shards.  Output
+    ``id1,id2,[rec1,rec2,]dist*scale`` (``output.record``), pairs above ``dist.threshold``
+    dropped."""
+    from ..ops.distance import pairwise
+    ctx = JobContext(args, "resi.", app="recordSimilarity")
+    ords = ctx.get_int_list("attr.ordinals")
+    idc = ctx.get_int("id.ordinal", 0)
+    scale = ctx.get_float("distance.scale", 1000.0)
+    thr = ctx.get_float("dist.threshold", math.inf)
+    out_rec = ctx.get_bool("output.record", False)
+    rows = ctx.rows(shard=False)
+    other = ctx.rows(args.train, shard=False) if args.train else None
+    allx = _numeric_matrix(ctx, rows + (other or []), ords)
+    lo, hi = allx.min(0).values, allx.max(0).values
+    rng = (hi - lo).clamp_min(1e-12)
+    A = (_numeric_matrix(ctx, rows, ords) - lo) / rng
+    B = (_numeric_matrix(ctx, other, ords) - lo) / rng if other else A
+    Brows = other or rows
+    from ..data.table import shard_range
+    a, b = shard_range(len(rows), ctx.comm.rank, ctx.comm.world)
+    d = ctx.delim_out
+    out = []
+    nf = math.sqrt(max(len(ords), 1))
+    for s in range(a, b, 2048):
+        e = min(b, s + 2048)
+        D = (pairwise(A[s:e], B) / nf * scale).round().long().cpu()
+        for q in range(e - s):
+            i = s + q
+            js = range(i + 1, len(Brows)) if other is None else range(len(Brows))
+            row = D[q].tolist()
+            for j in js:
+                if row[j] <= thr:
+                    parts = [rows[i][idc], Brows[j][idc]]
+                    if out_rec:
+                        parts += rows[i] + Brows[j]
+                    out.append(d.join(parts + [str(row[j])]))
+    ctx.emit(out)
+
+
+@job("groupedRecordSimilarity", "pairwise distances within each group (S/similarity/GroupedRecordSimilarity.scala)")
+def grouped_similarity(args):
+    from ..ops.distance import pairwise
+    ctx = JobContext(args, app="groupedRecordSimilarity")
+    kords = ctx.get_int_list("group.field.ordinals", None) or ctx.get_int_list("key.field.ordinals")
+    ords = ctx.get_int_list("attr.ordinals")
+    idc = ctx.get_int("id.ordinal", 0)
+    prec = ctx.get_int("output.precision", 3)
+    g = defaultdict(list)
+    for r in ctx.rows(shard=False):
+        g[tuple(r[o] for o in kords)].append(r)
+    keys = sorted(g)
+    from ..data.table import shard_range
+    a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
+    d = ctx.delim_out
+    out = []
+    for k in keys[a:b]:
+        rows = g[k]
+        X = _numeric_matrix(ctx, rows, ords)
+        D = pairwise(X, X).cpu().tolist()
+        for i in range(len(rows)):
+            for j in range(i + 1, len(rows)):
+                out.append(d.join(list(k) + [rows[i][idc], rows[j][idc], fmt(D[i][j], prec)]))
+    ctx.emit(out)
+
+
+@job("nearestRecords", "per record the top-k nearest from pair distances, by count or distance (S/similarity/NearestRecords.scala)")
+def nearest_records(args):
+    """Pair rows ``id1,id2,...,dist`` (both directions considered); per first record the nearest
+    ``neighbor.count`` (or all within ``neighbor.dist.threshold``), output ``id,n1,n2,...``."""
+    ctx = JobContext(args, app="nearestRecords")
+    k = ctx.get_int("neighbor.count", 5)
+    thr = ctx.get_float("neighbor.dist.threshold", math.inf)
+    nb = defaultdict(list)
+    for r in ctx.rows(shard=False):
+        dd = float(r[-1])
+        nb[r[0]].append((dd, r[1]))
+        nb[r[1]].append((dd, r[0]))
+    keys = sorted(nb)
+    from ..data.table import shard_range
+    a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
+    d = ctx.delim_out
+    ctx.emit([d.join([x] + [y for dd, y in sorted(nb[x])[:k] if dd <= thr]) for x in keys[a:b]])
+
+
+# ================================================================================================
+# population optimisers (Spark)
+# ================================================================================================
+def _domain(ctx):
+    from ..optimize import TaskScheduleSearch
+    return TaskScheduleSearch.from_json(ctx.path("domain.callback.config.file", "domain"), ctx.device)
+
+
+@job("geneticAlgorithm", "island-model GA over a task-schedule domain (S/optimize/GeneticAlgorithm.scala)")
+def genetic(args):
+    from ..optimize.search import GeneticAlgorithm
+    ctx = JobContext(args, app="geneticAlgorithm")
+    d = _domain(ctx)
+    pop = ctx.get_int("population.size", 16)
+    ga = GeneticAlgorithm(d, islands=ctx.get_int("num.optimizers", 4), pool=pop, mating=max(2, pop // 2),
+                          replacement=max(1, pop // 2), generations=ctx.get_int("num.generations", 100),
+                          seed=ctx.get_int("random.seed", 0), comm=ctx.comm)
+    r = ga.run()
+    o = ctx.delim_out
+    lines = [f"{d.format_solution(s)}{o}{c:.6f}" for s, c in zip(r.solutions.tolist(), r.costs.tolist())]
+    ctx.emit_root(sorted(lines, key=lambda l: float(l.rsplit(o, 1)[1])))
+    ctx.report({"best_cost": r.best_cost})
+
+
+@job("randomSearch", "random multi-start search + local search around the best (S/optimize/RandomSearch.scala)")
+def random_search(args):
+    from ..optimize.search import RandomSearch
+    ctx = JobContext(args, app="randomSearch")
+    d = _domain(ctx)
+    rs = RandomSearch(d, n=ctx.get_int("max.num.iterations", 100) * ctx.get_int("num.optimizers", 4),
+                      local="focussed" if ctx.get_bool("locally.optimize", False) else None,
+                      seed=ctx.get_int("random.seed", 0), comm=ctx.comm)
+    r = rs.run()
+    o = ctx.delim_out
+    lines = [f"{d.format_solution(s)}{o}{c:.6f}" for s, c in zip(r.solutions.tolist(), r.costs.tolist())]
+    ctx.emit_root(lines)
+    ctx.report({"best_cost": r.best_cost})

@@ -257,6 +257,25 @@ class NaiveBayes:
             cols.extend(g[:, :, j] for j in range(g.shape[2]))
         return torch.stack(cols, 1), tb["logprior"]
 
+    def feature_probs(self, t: Table) -> tuple[torch.Tensor, torch.Tensor]:
+        """(feature prior probability P(f) [n], feature posterior P(f|c) [n, C]) per record — the
+        ``bap.output.feature.prob.only`` output (BayesianPredictor.java:271-285, BayesianModel
+        ``getFeaturePriorProb`` / ``getFeaturePostProb``: products over the features)."""
+        terms, _ = self.feature_loglik(t)                       # [n, F, C]
+        tb = self.tables(t.device)
+        n = t.n
+        lfp = torch.zeros(n, device=t.device)
+        o = 0
+        for f, b in enumerate(self.bins):
+            v = t.codes[f, :n].long()
+            ok = v < b
+            lfp += torch.where(ok, tb["logfp"][torch.where(ok, v, torch.zeros_like(v)) + o], torch.zeros((), device=t.device))
+            o += b
+        if t.numeric.shape[0]:
+            zp = (t.numeric[:, :n].T - tb["pmean"]) * tb["pinvstd"]
+            lfp += (tb["plognorm"] - 0.5 * zp * zp).sum(1)
+        return torch.exp(lfp.double()), torch.exp(terms.double().sum(1))
+
     def validation_counters(self, conf: torch.Tensor, comm: Comm | None = None,
                             pos_class: int = 1) -> Counters:
         """Reference "Validation" counter group from an (all-reduced) confusion matrix."""
@@ -395,3 +414,106 @@ def _label_counts(t: Table, C: int) -> torch.Tensor:
     lab = t.labels[: t.n]
     lab = lab[lab < C].long()
     return torch.bincount(lab, minlength=C)[:C].to(torch.int64)
+
+
+# ================================================================================================
+# text mode (BayesianDistribution.mapText, J/bayesian/BayesianDistribution.java:186-195)
+# ================================================================================================
+# Lucene StandardAnalyzer's English stop set (the tokenizer the reference uses)
+_STOP = frozenset("a an and are as at be but by for if in into is it no not of on or such that the their then "
+                  "there these they this to was will with".split())
+
+
+def tokenize(text: str) -> list[str]:
+    """Lower-case alphanumeric tokens minus the analyzer's stop words."""
+    import re
+    return [w for w in re.findall(r"[a-z0-9]+", text.lower()) if w not in _STOP]
+
+
+class TextNaiveBayesModel:
+    """Multinomial NB over word tokens: the text is one feature (ordinal 1 in the model lines) whose
+    bins are the tokens.  Training counts are one ``[C, V]`` bincount over a vocabulary shared by all
+    ranks, all-reduced once; lines keep the tabular model layout (``class,1,token,count``,
+    ``class,,,docCount``, ``,1,token,count``)."""
+
+    FEATURE_ORDINAL = 1
+
+    def __init__(self, classes: list[str], vocab: list[str], counts: torch.Tensor, docs: torch.Tensor):
+        self.classes, self.vocab = classes, vocab
+        self.counts, self.docs = counts, docs          # int64 [C, V], int64 [C]
+
+    @classmethod
+    def fit_lines(cls, lines: list[str], split, ctx, class_ord: int = 1, text_ord: int = 0) -> "TextNaiveBayesModel":
+        rows = [split(l) for l in lines]
+        toks = [tokenize(r[text_ord]) for r in rows]
+        classes = ctx.union(r[class_ord] for r in rows)
+        vocab = ctx.union(w for ts in toks for w in ts)
+        ci = {c: i for i, c in enumerate(classes)}
+        vi = {w: i for i, w in enumerate(vocab)}
+        C, V = len(classes), len(vocab)
+        cl = torch.tensor([ci[r[class_ord]] for r in rows], dtype=torch.long)
+        flat_c = torch.repeat_interleave(cl, torch.tensor([len(t) for t in toks], dtype=torch.long))
+        flat_w = torch.tensor([vi[w] for t in toks for w in t], dtype=torch.long)
+        dev = ctx.device
+        counts = torch.bincount((flat_c * V + flat_w).to(dev), minlength=C * V)[: C * V].view(C, V)
+        docs = torch.bincount(cl.to(dev), minlength=C)[:C]
+        ctx.all_reduce(counts, docs)
+        return cls(classes, vocab, counts, docs)
+
+    def model_lines(self, delim: str = ",") -> list[str]:
+        f = self.FEATURE_ORDINAL
+        cnt = self.counts.cpu()
+        out = []
+        for c, cv in enumerate(self.classes):
+            for w in torch.nonzero(cnt[c]).view(-1).tolist():
+                out.append(f"{cv}{delim}{f}{delim}{self.vocab[w]}{delim}{int(cnt[c, w])}")
+        for c, cv in enumerate(self.classes):
+            out.append(f"{cv}{delim}{delim}{delim}{int(self.docs[c])}")
+        tot = cnt.sum(0)
+        for w in torch.nonzero(tot).view(-1).tolist():
+            out.append(f"{delim}{f}{delim}{self.vocab[w]}{delim}{int(tot[w])}")
+        return out
+
+    @classmethod
+    def load(cls, path, split) -> "TextNaiveBayesModel":
+        from ..jobs.common import read_lines
+        post: dict[tuple[str, str], int] = {}
+        docs: dict[str, int] = {}
+        for l in read_lines(path):
+            p = split(l)
+            if p[0] and p[1] and p[2]:
+                post[(p[0], p[2])] = int(float(p[3]))
+            elif p[0] and not p[1]:
+                docs[p[0]] = int(float(p[3]))
+        classes = sorted(docs)
+        vocab = sorted({w for _, w in post})
+        ci = {c: i for i, c in enumerate(classes)}
+        vi = {w: i for i, w in enumerate(vocab)}
+        counts = torch.zeros((len(classes), len(vocab)), dtype=torch.long)
+        for (c, w), n in post.items():
+            counts[ci[c], vi[w]] = n
+        return cls(classes, vocab, counts, torch.tensor([docs[c] for c in classes], dtype=torch.long))
+
+    def predict(self, texts: list[str], alpha: float = 1.0) -> tuple[list[int], list[float]]:
+        """Multinomial NB with Laplace smoothing: argmax_c log P(c) + sum_w n_w log P(w|c); the
+        bag-of-words matrix times the log-probability table is one GEMM."""
+        vi = {w: i for i, w in enumerate(self.vocab)}
+        C, V = self.counts.shape
+        dev = self.counts.device
+        rows, cols = [], []
+        for i, t in enumerate(texts):
+            for w in tokenize(t):
+                if w in vi:
+                    rows.append(i)
+                    cols.append(vi[w])
+        bow = torch.zeros((len(texts), V), dtype=torch.float64, device=dev)
+        if rows:
+            bow.index_put_((torch.tensor(rows, device=dev), torch.tensor(cols, device=dev)),
+                           torch.ones(len(rows), dtype=torch.float64, device=dev), accumulate=True)
+        cnt = self.counts.double()
+        logp = torch.log((cnt + alpha) / (cnt.sum(1, keepdim=True) + alpha * V))
+        prior = torch.log(self.docs.double() / self.docs.sum().clamp_min(1)).to(dev)
+        s = bow @ logp.T + prior
+        p = torch.softmax(s, 1)
+        best = p.max(1)
+        return best.indices.tolist(), best.values.tolist()

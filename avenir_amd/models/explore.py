@@ -75,6 +75,7 @@ class MutualInformation:
         for x in pc:
             pcs.append(flat[o:o + x.numel()].view(x.shape).double())
             o += x.numel()
+        self.class_feature_counts = fc                     # [C, TB + 1] (last column: class counts)
         cls_cnt = fc[:, -1]
         total = cls_cnt.sum()
         pc_ = cls_cnt / total
@@ -116,6 +117,23 @@ class MutualInformation:
         return res
 
     # -- greedy feature scores (MutualInformationScore) ------------------------------------------
+    def class_conditional_lines(self, t: Table, delim: str = ",") -> list[str]:
+        """``featOrd,classVal,featVal,P(featVal|class)`` lines — the feature class-conditional
+        distribution output (MutualInformation.java:560-583) that CategoricalClassAffinity reads."""
+        fc = self.class_feature_counts
+        cls_vals = t.label_values_all() if hasattr(t, "label_values_all") else t.class_field.cardinality
+        out, off = [], 0
+        for f in t.binned_fields:
+            b = f.num_bins
+            for c, cv in enumerate(cls_vals):
+                n = float(fc[c, -1])
+                for k in range(b):
+                    cnt = float(fc[c, off + k])
+                    if cnt > 0 and n > 0:
+                        out.append(f"{f.ordinal}{delim}{cv}{delim}{f.bin_label(k)}{delim}{cnt / n!r}")
+            off += b
+        return out
+
     def mim(self) -> list[tuple[int, float]]:
         return sorted(self.result.feature_class.items(), key=lambda kv: -kv[1])
 

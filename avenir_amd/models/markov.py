@@ -195,14 +195,77 @@ class HiddenMarkovModelBuilder:
                 obs[r, j], st[r, j] = oi.get(o, -1), si.get(s, -1)
         return obs, st
 
-    def fit(self, obs: torch.Tensor, st: torch.Tensor) -> HiddenMarkovModel:
+    def counts(self, obs: torch.Tensor, st: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """This rank's (transition [S, S], emission [S, O], initial [S]) counts (int64)."""
         S, O = len(self.states), len(self.observations)
         trans = H.bigram_histogram(st, S)[0]
         s, o = st.long(), obs.long()
         ok = (s >= 0) & (o >= 0) & (s < S) & (o < O)
         emit = torch.bincount((s[ok] * O + o[ok]), minlength=S * O)[: S * O].view(S, O)
-        first = s[:, 0]
+        first = s[:, 0] if s.shape[1] else s.new_zeros(0)
         init = torch.bincount(first[(first >= 0) & (first < S)], minlength=S)[:S]
+        return trans.long(), emit.long().to(trans.device), init.long().to(trans.device)
+
+    def partially_tagged_counts(self, rows: list[list[str]], window: list[int]):
+        """Partially tagged sequences (HiddenMarkovModelBuilder.java:174-260): state tokens sit
+        among the observations; each state's emission counts are spread over the observations to
+        its left and right within a boundary, weighted by ``window[k]`` at distance k+1 (last
+        weight repeated).  Boundaries reproduce the reference's integer arithmetic exactly,
+        including its operator precedence (``s_i - s_{i-1} / 2``).  The (state, obs, weight)
+        triples of all rows become one scatter-add."""
+        S, O = len(self.states), len(self.observations)
+        si = {s: i for i, s in enumerate(self.states)}
+        oi = {o: i for i, o in enumerate(self.observations)}
+        ts, to, tw, tr_a, tr_b, init = [], [], [], [], [], []
+        wl = len(window)
+        for items in rows:
+            idx = [i for i, tok in enumerate(items) if tok in si]
+            if not idx:
+                continue
+            init.append(si[items[idx[0]]])
+            n = len(items)
+            for i, p in enumerate(idx):
+                lw = rw = 0
+                if i > 0:
+                    lw = p - idx[i - 1] // 2
+                    lb = p - lw
+                else:
+                    lb = -1
+                if i < len(idx) - 1:
+                    rw = idx[i + 1] - p // 2
+                    rb = p + rw
+                else:
+                    rb = -1
+                if lb == -1 and rb != -1:
+                    lb = max(p - rw, 0)
+                elif rb == -1 and lb != -1:
+                    rb = min(p + lw, n - 1)
+                elif lb == -1 and rb == -1:
+                    lb = p // 2
+                    rb = p + (n - 1 - p) // 2
+                st = si[items[p]]
+                for k, j in enumerate(range(p - 1, lb - 1, -1)):
+                    if j < 0 or j >= n:
+                        continue
+                    if items[j] in oi:
+                        ts.append(st), to.append(oi[items[j]]), tw.append(window[min(k, wl - 1)])
+                for k, j in enumerate(range(p + 1, rb + 1)):
+                    if j < 0 or j >= n:
+                        continue
+                    if items[j] in oi:
+                        ts.append(st), to.append(oi[items[j]]), tw.append(window[min(k, wl - 1)])
+            for a, b in zip(idx[:-1], idx[1:]):
+                tr_a.append(si[items[a]]), tr_b.append(si[items[b]])
+        emit = torch.zeros(S * O, dtype=torch.long).index_add_(
+            0, torch.tensor(ts, dtype=torch.long) * O + torch.tensor(to, dtype=torch.long),
+            torch.tensor(tw, dtype=torch.long)).view(S, O)
+        trans = torch.bincount(torch.tensor(tr_a, dtype=torch.long) * S + torch.tensor(tr_b, dtype=torch.long),
+                               minlength=S * S)[: S * S].view(S, S)
+        ini = torch.bincount(torch.tensor(init, dtype=torch.long), minlength=S)[:S]
+        return trans, emit, ini
+
+    def fit(self, obs: torch.Tensor, st: torch.Tensor) -> HiddenMarkovModel:
+        trans, emit, init = self.counts(obs, st)
         comm = self.comm or get_comm()
         if comm.is_distributed:
             for x in (trans, emit, init):
@@ -321,6 +384,30 @@ class StateTransitionRate:
         self.Q = Q
         return Q
 
+    def fit_grouped(self, key: torch.Tensor, time_ms: torch.Tensor, state: torch.Tensor, n_keys: int,
+                    unit_ms: float = 3600_000.0) -> torch.Tensor:
+        """One rate matrix per key ``[G, S, S]`` (StateTransitionRate.scala:91-167): sort by
+        (key, time), transitions between consecutive events of a key, dwell time of the source
+        state in ``unit_ms`` units; off-diagonal q_ij = n_ij / T_i, q_ii = -sum_j q_ij (rows of
+        unvisited states stay zero)."""
+        k, t, s = key.long(), time_ms.long(), state.long()
+        order = torch.argsort(t, stable=True)
+        order = order[torch.argsort(k[order], stable=True)]
+        k, t, s = k[order], t[order].double(), s[order]
+        same = k[1:] == k[:-1]
+        g, a, b = k[:-1][same], s[:-1][same], s[1:][same]
+        dt = (t[1:] - t[:-1])[same] / unit_ms
+        S, G = self.S, n_keys
+        n = torch.zeros(G * S * S, dtype=torch.float64, device=s.device).index_add_(
+            0, (g * S + a) * S + b, torch.ones_like(dt)).view(G, S, S)
+        dwell = torch.zeros(G * S, dtype=torch.float64, device=s.device).index_add_(0, g * S + a, dt).view(G, S)
+        Q = torch.where(dwell.unsqueeze(2) > 0, n / dwell.clamp_min(1e-300).unsqueeze(2), torch.zeros_like(n))
+        eye = torch.eye(S, dtype=torch.bool, device=s.device)
+        off = Q.masked_fill(eye, 0.0).sum(2)
+        Q = torch.where(eye, -off.unsqueeze(2).expand_as(Q), Q)
+        self.Q = Q
+        return Q
+
 
 class ContTimeStateTransitionStats:
     """Uniformisation: P = I + Q/lambda, powers P^0..P^L with L = 4 + 6 sqrt(lambda t) + lambda t
@@ -408,6 +495,29 @@ def gsp_candidates(freq: list[tuple[int, ...]]) -> list[tuple[int, ...]]:
         for b in by_prefix.get(a[1:], []):
             out.add(a + (b[-1],))
     return sorted(out)
+
+
+def gsp_candidates_device(seqs: list[tuple[str, ...]], device="cpu", comm: Comm | None = None) -> list[tuple[str, ...]]:
+    """GSP k+1 candidates of a set of frequent k-sequences of string tokens, on the device
+    (``SO.gsp_join``); distributed: each rank joins its shard of left sequences against all of
+    them and rank 0 receives the union (sorted, unique)."""
+    comm = comm or get_comm()
+    seqs = sorted(set(seqs))
+    if not seqs:
+        return []
+    k = len(seqs[0])
+    vocab = sorted({t for s in seqs for t in s})
+    ti = {t: i for i, t in enumerate(vocab)}
+    X = torch.tensor([[ti[t] for t in s] for s in seqs], dtype=torch.int32, device=device)
+    lo, hi = 0, X.shape[0]
+    if comm.is_distributed:
+        from ..data.table import shard_range
+        lo, hi = shard_range(X.shape[0], comm.rank, comm.world)
+    C = SO.gsp_join(X, lo, hi)
+    if comm.is_distributed:
+        C = comm.all_gather_v(C.cpu() if comm.backend == "gloo" else C)
+    C = torch.unique(C.cpu(), dim=0) if C.numel() else C.cpu().view(0, k + 1)
+    return [tuple(vocab[i] for i in row) for row in C.tolist()]
 
 
 def dot_matrix_similarity(A: torch.Tensor, B: torch.Tensor, window: int = 3) -> torch.Tensor:

@@ -83,7 +83,7 @@ def parse_split_key(key: str, kind: str):
 
 
 def class_partition_stats(t: Table, algorithm: str = "entropy", attrs: Sequence[int] | None = None,
-                          max_bins: int = 32) -> list[dict]:
+                          max_bins: int = 32, comm=None) -> list[dict]:
     """Score every candidate split of every attribute (ClassPartitionGenerator).
 
     Returns dicts {attr, key, stat, gain, gain_ratio, counts [G, C]} sorted by attribute then
@@ -93,7 +93,10 @@ def class_partition_stats(t: Table, algorithm: str = "entropy", attrs: Sequence[
     codes = T.encode_for_tree(space, t)
     bins = [fs.n_bins for fs in space]
     C = t.n_classes
-    hist = H.class_histogram(codes, t.n, bins, t.labels, C, count_labels=True).cpu()   # [C, TB + 1]
+    hist = H.class_histogram(codes, t.n, bins, t.labels, C, count_labels=True)          # [C, TB + 1]
+    if comm is not None and comm.is_distributed:
+        comm.all_reduce(hist)
+    hist = hist.cpu()
     parent_counts = hist[:, -1].double()
     parent = float(info_content(parent_counts, "entropy" if algorithm == "entropy" else "giniIndex")) \
         if algorithm in ("entropy", "giniIndex", "gini") else 0.0

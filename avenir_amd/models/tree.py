@@ -333,6 +333,67 @@ class DecisionTree:
         return out
 
 
+class DecisionPathModel:
+    """Inference straight from the reference's decision-path JSON (J/tree/DecisionTreeModel.java:
+    56-144): a record takes the first path whose predicates all hold.  Predicates (``ord le v``,
+    ``ord le v lower``, ``ord gt v``, ``ord in a:b``) are evaluated column-wise over all records
+    (one tensor comparison per distinct predicate), the path matches are one ``[N, P]`` boolean
+    matrix, and the first matching path per record is an argmax."""
+
+    def __init__(self, js: dict):
+        self.paths = js["decisionPaths"]
+        self.class_values = sorted({c for p in self.paths for c in p.get("classValPr", {})})
+
+    def _pred(self, cols, ps: str) -> torch.Tensor:
+        it = ps.split()
+        o, op = int(it[0]), it[1]
+        if op == "in":
+            c, vocab = cols.codes(o)
+            ids = [vocab[v] for v in it[2].split(":") if v in vocab]
+            return torch.isin(c, torch.tensor(ids, dtype=torch.long)) if ids else torch.zeros_like(c, dtype=torch.bool)
+        x = cols.numeric(o)
+        v = float(it[2])
+        if op == "le":
+            m = x <= v
+            if len(it) > 3:
+                m &= x > float(it[3])
+            return m
+        if op == "gt":
+            m = x > v
+            if len(it) > 3:
+                m &= x <= float(it[3])
+            return m
+        if op == "lt":
+            return x < v
+        if op == "ge":
+            return x >= v
+        raise ValueError(f"unknown predicate operator in {ps!r}")
+
+    def predict_proba_rows(self, rows) -> tuple[torch.Tensor, torch.Tensor]:
+        """(class probabilities [N, C] of the matched path, matched path index [N] (-1 = none))."""
+        from ..utils.rules import ColumnCache
+        cols = ColumnCache(rows)
+        n, P = len(rows), len(self.paths)
+        M = torch.ones((n, P), dtype=torch.bool)
+        cache: dict[str, torch.Tensor] = {}
+        for j, p in enumerate(self.paths):
+            for pr in p["predicates"]:
+                ps = pr["predicateStr"]
+                if ps == ROOT:
+                    continue
+                if ps not in cache:
+                    cache[ps] = self._pred(cols, ps)
+                M[:, j] &= cache[ps]
+        any_ = M.any(1)
+        first = torch.where(any_, M.int().argmax(1), torch.full((n,), -1, dtype=torch.long))
+        ci = {c: i for i, c in enumerate(self.class_values)}
+        tab = torch.zeros((P + 1, len(ci)), dtype=torch.float64)
+        for j, p in enumerate(self.paths):
+            for c, v in p.get("classValPr", {}).items():
+                tab[j, ci[c]] = float(v)
+        return tab[torch.where(first >= 0, first, torch.full_like(first, P))], first
+
+
 def _predicate_obj(ps: str, f: FeatureField) -> dict:
     it = ps.split()
     d = {"attribute": int(it[0]), "predicateStr": ps, "operator": it[1], "valueInt": 0, "valueDbl": 0.0,

@@ -335,6 +335,33 @@ def dot_matrix_hits(ida: torch.Tensor, idb: torch.Tensor) -> torch.Tensor:
     return eq.sum((2, 3)).to(torch.int32)
 
 
+def gsp_join(X: torch.Tensor, lo: int = 0, hi: int | None = None) -> torch.Tensor:
+    """GSP candidate self-join (K18): X int [N, k] token-id rows; left rows [lo, hi) of the
+    lexicographically sorted unique rows are joined with every row b whose b[:-1] equals their
+    a[1:], giving a ++ b[-1].  Returns int32 [M, k+1] (left-row order, partners in sorted order)."""
+    X = torch.unique(X.to(torch.int32), dim=0) if X.numel() else X.to(torch.int32)
+    N, k = X.shape
+    hi = N if hi is None else hi
+    if X.is_cuda:
+        return _native.C().gsp_join(X.contiguous(), int(lo), int(hi))
+    if N == 0 or hi <= lo:
+        return torch.zeros((0, k + 1), dtype=torch.int32)
+    # oracle: dense ids of the (k-1)-grams, partners found by searchsorted over sorted prefix ids
+    both = torch.cat([X[:, :-1], X[:, 1:]])
+    _, inv = torch.unique(both, dim=0, return_inverse=True)
+    pid, sid = inv[:N], inv[N:]
+    order = torch.argsort(pid, stable=True)
+    ps = pid[order]
+    a = torch.arange(lo, hi)
+    s = torch.searchsorted(ps, sid[a], right=False)
+    e = torch.searchsorted(ps, sid[a], right=True)
+    cnt = e - s
+    left = torch.repeat_interleave(a, cnt)
+    base = torch.repeat_interleave(s - torch.cumsum(cnt, 0) + cnt, cnt)
+    right = order[base + torch.arange(int(cnt.sum()))]
+    return torch.cat([X[left], X[right, -1:]], 1)
+
+
 def decode_ngram(key: int, k: int, n_states: int, max_len: int | None = None) -> tuple[int, list[int]]:
     base = n_states + 1
     grp = 0
