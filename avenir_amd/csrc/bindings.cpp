@@ -1081,6 +1081,158 @@ at::Tensor dot_matrix(const at::Tensor& A, const at::Tensor& B) {
   return hits;
 }
 
+// ---- device-resident forest builder (forest.hip) ---------------------------------------------
+// codes uint8 [F][ld], lab/wt uint8 [ld] on the device.  Work lists (slot/node int32, start int64,
+// len int32, bases int64) are HOST tensors: they are bound-checked here on the CPU and copied to the
+// device by the binding, so no chunk outside the row buffer can reach a kernel and no D2H read is
+// needed for the check.
+static const long long* i64p(const at::Tensor& t) { return reinterpret_cast<const long long*>(t.data_ptr<int64_t>()); }
+
+static void check_host_items(const at::Tensor& node, const at::Tensor& start, const at::Tensor& len, int64_t ld,
+                             int64_t n_nodes) {
+  TORCH_CHECK(!node.is_cuda() && !start.is_cuda() && !len.is_cuda(), "work lists are host tensors");
+  CHECK_DTYPE(node, at::kInt);
+  CHECK_DTYPE(start, at::kLong);
+  CHECK_DTYPE(len, at::kInt);
+  const int64_t n = node.numel();
+  TORCH_CHECK(start.numel() == n && len.numel() == n, "work list arrays differ in length");
+  const auto node_c = node.contiguous(), start_c = start.contiguous(), len_c = len.contiguous();
+  const int* nd = node_c.data_ptr<int>();
+  const int64_t* st = start_c.data_ptr<int64_t>();
+  const int* ln = len_c.data_ptr<int>();
+  for (int64_t i = 0; i < n; ++i) {
+    TORCH_CHECK(nd[i] >= 0 && nd[i] < n_nodes, "work item node / slot out of range");
+    TORCH_CHECK(st[i] >= 0 && ln[i] >= 0 && st[i] + ln[i] <= ld, "work item outside the row buffer");
+  }
+}
+
+static at::Tensor to_dev(const at::Tensor& t, const at::Tensor& like) {
+  return t.contiguous().to(like.device(), /*non_blocking=*/true);
+}
+
+void forest_hist(const at::Tensor& codes, const at::Tensor& lab, const at::Tensor& wt, const at::Tensor& slot,
+                 const at::Tensor& start, const at::Tensor& len, const at::Tensor& bins, const at::Tensor& offs,
+                 int64_t TB, int64_t C, at::Tensor& hist) {
+  CHECK_DEV(codes); CHECK_DTYPE(codes, at::kByte);
+  CHECK_DEV(lab); CHECK_DTYPE(lab, at::kByte);
+  CHECK_DEV(wt); CHECK_DTYPE(wt, at::kByte);
+  CHECK_DEV(hist); CHECK_DTYPE(hist, at::kLong);
+  CHECK_DEV(bins); CHECK_DEV(offs);
+  const int64_t ld = codes.size(1), F = codes.size(0), n = slot.numel();
+  TORCH_CHECK(lab.numel() >= ld && wt.numel() >= ld, "label / weight columns shorter than the code rows");
+  TORCH_CHECK(bins.numel() == F && offs.numel() == F, "bins / offs per feature");
+  TORCH_CHECK(hist.dim() == 3 && hist.size(1) == C && hist.size(2) == TB, "hist [A, C, TB]");
+  check_host_items(slot, start, len, ld, hist.size(0));
+  if (n == 0) return;
+  auto d_slot = to_dev(slot, codes), d_start = to_dev(start, codes), d_len = to_dev(len, codes);
+  DevGuard g(codes.device());
+  avk::forest_hist(codes.data_ptr<uint8_t>(), ld, lab.data_ptr<uint8_t>(), wt.data_ptr<uint8_t>(),
+                   d_slot.data_ptr<int>(), i64p(d_start), d_len.data_ptr<int>(), (int)n, bins.data_ptr<int>(),
+                   offs.data_ptr<int>(), (int)F, (int)TB, (int)C,
+                   reinterpret_cast<unsigned long long*>(hist.data_ptr<int64_t>()), cur_stream(codes));
+}
+
+// X float32 [F, ldx] (rows 0..n), edges float32 concatenated (<= 254 per feature), eoff int32 [F+1]
+// (host tensor, checked here) -> uint8 [F, ldo] codes (rows >= n untouched).
+void bucketize_u8(const at::Tensor& X, int64_t n, const at::Tensor& edges, const at::Tensor& eoff, at::Tensor& out) {
+  CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(edges); CHECK_DTYPE(edges, at::kFloat);
+  CHECK_DEV(out); CHECK_DTYPE(out, at::kByte);
+  TORCH_CHECK(!eoff.is_cuda(), "eoff is a host tensor");
+  CHECK_DTYPE(eoff, at::kInt);
+  const int64_t F = X.size(0);
+  TORCH_CHECK(eoff.numel() == F + 1 && out.size(0) == F && n <= X.size(1) && n <= out.size(1), "shapes");
+  const auto eo = eoff.contiguous();
+  const int* e = eo.data_ptr<int>();
+  TORCH_CHECK(e[0] == 0 && e[F] == edges.numel(), "edge offsets");
+  for (int64_t f = 0; f < F; ++f) TORCH_CHECK(e[f + 1] >= e[f] && e[f + 1] - e[f] <= 254, "at most 254 edges per feature");
+  if (n == 0 || F == 0) return;
+  auto d_eoff = eo.to(X.device());
+  DevGuard g(X.device());
+  avk::bucketize_u8(X.data_ptr<float>(), X.size(1), n, (int)F, edges.data_ptr<float>(), d_eoff.data_ptr<int>(),
+                    out.data_ptr<uint8_t>(), out.size(1), cur_stream(X));
+}
+
+std::vector<at::Tensor> forest_split(const at::Tensor& hist, const at::Tensor& fmask, const at::Tensor& bins,
+                                     const at::Tensor& offs, int64_t algo, int64_t topk, const at::Tensor& rnd) {
+  CHECK_DEV(hist); CHECK_DTYPE(hist, at::kLong);
+  CHECK_DEV(fmask); CHECK_DTYPE(fmask, at::kByte);
+  CHECK_DEV(rnd); CHECK_DTYPE(rnd, at::kFloat);
+  const int64_t A = hist.size(0), C = hist.size(1), TB = hist.size(2), F = bins.numel();
+  TORCH_CHECK(fmask.size(0) == A && fmask.size(1) == F && rnd.numel() >= A, "fmask [A, F], rnd [A]");
+  TORCH_CHECK(C <= 16, "forest_split: at most 16 classes");
+  auto io = hist.options().dtype(at::kInt), fo = hist.options().dtype(at::kFloat);
+  auto feat = at::empty({A}, io), thr = at::empty({A}, io);
+  auto score = at::empty({A}, fo), imp = at::empty({A}, fo);
+  auto left = at::empty({A, C}, hist.options());
+  if (A > 0) {
+    DevGuard g(hist.device());
+    avk::forest_split(reinterpret_cast<const long long*>(hist.data_ptr<int64_t>()), fmask.data_ptr<uint8_t>(),
+                      bins.data_ptr<int>(), offs.data_ptr<int>(), (int)F, (int)TB, (int)C, (int)algo, (int)topk,
+                      rnd.data_ptr<float>(), (int)A, feat.data_ptr<int>(), thr.data_ptr<int>(), score.data_ptr<float>(),
+                      imp.data_ptr<float>(), reinterpret_cast<long long*>(left.data_ptr<int64_t>()), cur_stream(hist));
+  }
+  return {feat, thr, score, imp, left};
+}
+
+at::Tensor forest_part_count(const at::Tensor& codes, const at::Tensor& node, const at::Tensor& start,
+                             const at::Tensor& len, const at::Tensor& feat, const at::Tensor& thr) {
+  CHECK_DEV(codes); CHECK_DTYPE(codes, at::kByte);
+  CHECK_DEV(feat); CHECK_DTYPE(feat, at::kInt);
+  CHECK_DEV(thr); CHECK_DTYPE(thr, at::kInt);
+  check_host_items(node, start, len, codes.size(1), feat.numel());
+  auto out = at::zeros({node.numel()}, feat.options());
+  if (node.numel()) {
+    auto d_node = to_dev(node, codes), d_start = to_dev(start, codes), d_len = to_dev(len, codes);
+    DevGuard g(codes.device());
+    avk::forest_part_count(codes.data_ptr<uint8_t>(), codes.size(1), d_node.data_ptr<int>(), i64p(d_start),
+                           d_len.data_ptr<int>(), (int)node.numel(), feat.data_ptr<int>(), thr.data_ptr<int>(),
+                           out.data_ptr<int>(), cur_stream(codes));
+  }
+  return out;
+}
+
+void forest_part_scatter(const at::Tensor& codes, const at::Tensor& lab, const at::Tensor& wt, at::Tensor& dcodes,
+                         at::Tensor& dlab, at::Tensor& dwt, const at::Tensor& node, const at::Tensor& start,
+                         const at::Tensor& len, const at::Tensor& left_base, const at::Tensor& right_base,
+                         const at::Tensor& item_left, const at::Tensor& feat, const at::Tensor& thr) {
+  CHECK_DEV(codes); CHECK_DTYPE(codes, at::kByte);
+  CHECK_DEV(dcodes); CHECK_DTYPE(dcodes, at::kByte);
+  CHECK_DEV(lab); CHECK_DEV(wt); CHECK_DEV(dlab); CHECK_DEV(dwt);
+  TORCH_CHECK(!item_left.is_cuda(), "item_left (forest_part_count output) is a host tensor");
+  CHECK_DTYPE(item_left, at::kInt);
+  CHECK_DEV(feat); CHECK_DEV(thr);
+  TORCH_CHECK(dcodes.sizes() == codes.sizes() && dlab.numel() == lab.numel() && dwt.numel() == wt.numel(),
+              "destination buffers must match the source");
+  const int64_t ld = codes.size(1);
+  check_host_items(node, start, len, ld, feat.numel());
+  TORCH_CHECK(!left_base.is_cuda() && !right_base.is_cuda(), "bases are host tensors");
+  CHECK_DTYPE(left_base, at::kLong);
+  CHECK_DTYPE(right_base, at::kLong);
+  const int64_t n = node.numel();
+  TORCH_CHECK(left_base.numel() == n && right_base.numel() == n && item_left.numel() == n, "one base per work item");
+  {  // every chunk's destinations stay inside the buffer: [lb, lb + left) and [rb, rb + len - left)
+    const auto lb_c = left_base.contiguous(), rb_c = right_base.contiguous(), len_c = len.contiguous();
+    const auto il_c = item_left.contiguous();
+    const int64_t* lb = lb_c.data_ptr<int64_t>();
+    const int64_t* rb = rb_c.data_ptr<int64_t>();
+    const int* ln = len_c.data_ptr<int>();
+    const int* il = il_c.data_ptr<int>();
+    for (int64_t i = 0; i < n; ++i)
+      TORCH_CHECK(il[i] >= 0 && il[i] <= ln[i] && lb[i] >= 0 && rb[i] >= 0 && lb[i] + il[i] <= ld &&
+                      rb[i] + (ln[i] - il[i]) <= ld,
+                  "forest_part_scatter: destination outside the row buffer");
+  }
+  if (n == 0) return;
+  auto d_node = to_dev(node, codes), d_start = to_dev(start, codes), d_len = to_dev(len, codes);
+  auto d_lb = to_dev(left_base, codes), d_rb = to_dev(right_base, codes);
+  DevGuard g(codes.device());
+  avk::forest_part_scatter(codes.data_ptr<uint8_t>(), lab.data_ptr<uint8_t>(), wt.data_ptr<uint8_t>(),
+                           dcodes.data_ptr<uint8_t>(), dlab.data_ptr<uint8_t>(), dwt.data_ptr<uint8_t>(), ld,
+                           (int)codes.size(0), d_node.data_ptr<int>(), i64p(d_start), d_len.data_ptr<int>(), (int)n,
+                           i64p(d_lb), i64p(d_rb), feat.data_ptr<int>(), thr.data_ptr<int>(), cur_stream(codes));
+}
+
 // K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
 // are joined with every row whose (k-1)-prefix equals their (k-1)-suffix -> int32 [M, k+1].
 at::Tensor gsp_join(const at::Tensor& X, int64_t lo, int64_t hi) {
@@ -1307,6 +1459,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("uniformization", &uniformization);
   m.def("dot_matrix", &dot_matrix);
   m.def("gsp_join", &gsp_join);
+  m.def("forest_hist", &forest_hist);
+  m.def("bucketize_u8", &bucketize_u8);
+  m.def("forest_split", &forest_split);
+  m.def("forest_part_count", &forest_part_count);
+  m.def("forest_part_scatter", &forest_part_scatter);
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);

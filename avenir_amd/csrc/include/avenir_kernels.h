@@ -145,6 +145,23 @@ void uniformization(const double* P, int S, const double* w1, const double* w2, 
                     double* out, hipStream_t stream);
 void dot_matrix(const int* A, int n, int Wa, const int* B, int m, int Wb, int* hits, hipStream_t stream);
 
+// forest.hip (device-resident forest builder: chunk histograms, K6/K7 split scoring, partitioning)
+void bucketize_u8(const float* X, long long ldx, long long n, int F, const float* edges, const int* eoff, uint8_t* out,
+                  long long ldo, hipStream_t stream);
+void forest_hist(const uint8_t* codes, long long ld, const uint8_t* lab, const uint8_t* wt, const int* item_slot,
+                 const long long* item_start, const int* item_len, int n_items, const int* bins, const int* offs,
+                 int nfeat, int TB, int C, unsigned long long* hist, hipStream_t stream);
+void forest_split(const long long* hist, const uint8_t* fmask, const int* bins, const int* offs, int nfeat, int TB,
+                  int C, int algo, int topk, const float* rnd, int A, int* feat, int* thr, float* score, float* imp,
+                  long long* left, hipStream_t stream);
+void forest_part_count(const uint8_t* codes, long long ld, const int* item_node, const long long* item_start,
+                       const int* item_len, int n_items, const int* feat, const int* thr, int* item_left,
+                       hipStream_t stream);
+void forest_part_scatter(const uint8_t* codes, const uint8_t* lab, const uint8_t* wt, uint8_t* dcodes, uint8_t* dlab,
+                         uint8_t* dwt, long long ld, int nfeat, const int* item_node, const long long* item_start,
+                         const int* item_len, int n_items, const long long* left_base, const long long* right_base,
+                         const int* feat, const int* thr, hipStream_t stream);
+
 // gsp.hip (K18 GSP candidate self-join over a lexicographically sorted [N, k] sequence matrix)
 void gsp_count(const int* X, int N, int k, int lo, int hi, int* seg_start, int* seg_len, hipStream_t stream);
 void gsp_emit(const int* X, int k, int lo, int hi, const int* seg_start, const int* seg_len, const long long* offs,

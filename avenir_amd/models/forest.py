@@ -1,0 +1,351 @@
+"""Device-resident random-forest builder: all trees grow together, level-synchronously, with their
+bootstrap rows partitioned in HBM (kernels and design notes in ``csrc/kernels/forest.hip``).
+
+Reference: random forest = ``DecisionTreeBuilder`` repeated per tree with sub-sampling and random
+attribute subsets (J/tree/DecisionTreeBuilder.java:137-193 sampling, :365-381 attribute selection,
+:499-616 expandTree, R/rafo.sh), each level one MapReduce job.  Per level here, for ALL trees:
+
+1. histogram of the smaller child of every split (one chunked launch over contiguous segments;
+   the larger child = parent - sibling, one batched tensor op); all-reduced when data-parallel;
+2. K6/K7 split scoring of every frontier node (one launch; random feature subsets as masks drawn
+   by one device RNG call; ``best`` or ``randomAmongTop``);
+3. stopping rules (maxDepth / minPopulation / minInfoGain / pure) as tensor ops;
+4. ONE device->host copy: decisions + per-chunk left-row counts;
+5. numpy (vectorised, no per-node Python loop) child segments, build/derive slots, next work lists;
+6. stable partition of every splitting node's rows into [left | right] (double buffer).
+
+The trees come back as :class:`models.tree.DecisionTree` (same predicates, decision-path JSON,
+flattening for the K8 inference kernel).  Binary threshold splits over the split space's ordered
+fine bins (numeric and categorical), like ``TreeParams(binary=True)``.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..data.table import Table
+from ..ops import forest_ops as FO
+from ..parallel.comm import Comm, get_comm
+from ..utils.schema import FeatureSchema
+from . import tree as T
+
+
+@dataclass
+class _Frontier:
+    node: np.ndarray      # global node id (into the node table)
+    start: np.ndarray     # int64 local row offset of the node's segment in the buffer
+    count: np.ndarray     # int64 local row count
+    depth: np.ndarray     # int64
+
+
+class ForestBuilder:
+    """Grow ``n_trees`` binary-split trees at once.
+
+    ``params``: a :class:`models.tree.TreeParams` (algorithm, stopping, max_depth,
+    min_population, min_info_gain, attr_selection + random_attr_count, split_selection +
+    top_split_count, sub_sampling + sampling_rate, seed, max_bins).  ``comm``: data-parallel over
+    row shards (histograms all-reduced per level); ``tree_parallel`` distributes whole trees over
+    ranks instead (no per-level collective)."""
+
+    def __init__(self, schema: FeatureSchema, n_trees: int, params: T.TreeParams, comm: Comm | None = None,
+                 chunk: int | None = None):
+        self.schema = schema
+        self.n_trees = n_trees
+        self.p = params
+        self.comm = comm
+        self.chunk = chunk
+        self.level_times: list[float] = []
+        self.stats: dict = {}
+
+    # ------------------------------------------------------------------------------------------
+    def _weights(self, n: int, ld: int, dev, tree_ids: list[int]) -> torch.Tensor:
+        """uint8 [T, n] bootstrap multiplicities (Poisson(1) = with replacement), Bernoulli
+        (without replacement, rate %), or ones."""
+        comm = self.comm or get_comm()
+        p = self.p
+        Tn = len(tree_ids)
+        if p.sub_sampling == "none":
+            return torch.ones((Tn, n), dtype=torch.uint8, device=dev)
+        out = torch.empty((Tn, n), dtype=torch.uint8, device=dev)
+        for j, t in enumerate(tree_ids):
+            g = torch.Generator(device=dev)
+            g.manual_seed((p.seed * 7919 + t) * 1000003 + comm.rank)
+            if p.sub_sampling == "withReplace":
+                out[j] = torch.poisson(torch.ones(n, device=dev), generator=g).clamp_max(255).to(torch.uint8)
+            elif p.sub_sampling == "withoutReplace":
+                out[j] = (torch.rand(n, generator=g, device=dev) * 100.0 < p.sampling_rate).to(torch.uint8)
+            else:
+                raise ValueError(f"unknown sub sampling strategy {p.sub_sampling}")
+        return out
+
+    def _chunks(self, node_idx: np.ndarray, start: np.ndarray, count: np.ndarray, chunk: int):
+        """Split segments into <= chunk-row work items: (item node index, item start, item len)."""
+        nch = np.maximum(1, -(-count // chunk))
+        item_node = np.repeat(node_idx, nch)
+        first = np.repeat(np.cumsum(nch) - nch, nch)
+        k = np.arange(item_node.size) - first
+        seg_start = np.repeat(start, nch)
+        seg_cnt = np.repeat(count, nch)
+        istart = seg_start + k * chunk
+        ilen = np.clip(seg_cnt - k * chunk, 0, chunk)
+        return item_node.astype(np.int32), istart.astype(np.int64), ilen.astype(np.int32), nch
+
+    def _mask(self, A: int, F: int, gen: torch.Generator, dev) -> torch.Tensor:
+        p = self.p
+        if p.attr_selection in ("all", "notUsedYet") or A == 0:
+            return torch.ones((A, F), dtype=torch.uint8, device=dev)
+        k = max(1, min(p.random_attr_count, F))
+        r = torch.rand((A, F), generator=gen, device=dev)
+        idx = torch.topk(r, k, dim=1, largest=False).indices
+        m = torch.zeros((A, F), dtype=torch.uint8, device=dev)
+        m.scatter_(1, idx, 1)
+        return m
+
+    # ------------------------------------------------------------------------------------------
+    def fit(self, t: Table, space: list | None = None, codes: torch.Tensor | None = None,
+            tree_ids: list[int] | None = None, weights: torch.Tensor | None = None) -> list[T.DecisionTree]:
+        """``weights``: optional explicit uint8 [T, n] bootstrap multiplicities (tests)."""
+        comm = self.comm or get_comm()
+        p = self.p
+        dev = t.device
+        if space is None:
+            space = T.build_split_space(self.schema, t, binary=True, max_bins=p.max_bins)
+        if codes is None:
+            codes = T.encode_for_tree(space, t)
+        n = t.n
+        F = len(space)
+        bins = [fs.n_bins for fs in space]
+        offs = list(np.cumsum([0] + bins[:-1]))
+        TB = sum(bins) + 1
+        C = t.n_classes
+        algo = 1 if p.algorithm == "entropy" else 0
+        topk = p.top_split_count if p.split_selection == "randomAmongTop" else 1
+        tree_ids = list(range(self.n_trees)) if tree_ids is None else tree_ids
+        Tn = len(tree_ids)
+        bins_d = torch.tensor(bins, dtype=torch.int32, device=dev)
+        offs_d = torch.tensor(offs, dtype=torch.int32, device=dev)
+        t0 = time.perf_counter()
+
+        # ---- per-tree bootstrap row buffers (one gather) ----------------------------------
+        w = self._weights(n, t.ld, dev, tree_ids) if weights is None else weights.to(dev, torch.uint8)  # [T, n]
+        keep = w > 0
+        cnt_t = keep.sum(1)
+        rows = torch.nonzero(keep.view(-1)).view(-1)               # flat (tree, row) ids, tree-major
+        src_row = rows % n
+        R = int(rows.numel())
+        ldb = max(16, R)
+        cb = torch.empty((F, ldb), dtype=torch.uint8, device=dev)
+        cb[:, :R] = codes[:, :n].index_select(1, src_row)
+        lb = torch.empty(ldb, dtype=torch.uint8, device=dev)
+        lb[:R] = t.labels[:n].to(dev).index_select(0, src_row)
+        wb = torch.zeros(ldb, dtype=torch.uint8, device=dev)
+        wb[:R] = w.view(-1)[rows]
+        del rows, src_row, keep, w
+        cb2, lb2, wb2 = torch.empty_like(cb), torch.empty_like(lb), torch.zeros_like(wb)
+        cnt_h = cnt_t.cpu().numpy().astype(np.int64)
+        starts_h = np.concatenate([[0], np.cumsum(cnt_h)[:-1]]).astype(np.int64)
+        chunk = self.chunk or int(max(2048, min(65536, R // 4096 if R else 2048)))
+
+        # ---- node table (host, numpy growing arrays) ---------------------------------------
+        cap = 1024
+        tbl = {k: np.zeros(cap, dtype=np.int64) for k in ("tree", "depth", "feat", "thr", "left", "right", "parent")}
+        tbl["counts"] = np.zeros((cap, C), dtype=np.int64)
+        tbl["imp"] = np.zeros(cap, dtype=np.float64)
+        for k in ("feat", "thr", "left", "right", "parent"):
+            tbl[k][:] = -1
+        n_nodes = 0
+
+        def add_nodes(tree, depth, parent, counts):
+            nonlocal n_nodes, cap
+            m = len(tree)
+            while n_nodes + m > cap:
+                for k in tbl:
+                    a = tbl[k]
+                    b = np.zeros((cap * 2,) + a.shape[1:], dtype=a.dtype)
+                    if k in ("feat", "thr", "left", "right", "parent"):
+                        b[:] = -1
+                    b[:cap] = a
+                    tbl[k] = b
+                cap *= 2
+            ids = np.arange(n_nodes, n_nodes + m)
+            tbl["tree"][ids], tbl["depth"][ids], tbl["parent"][ids] = tree, depth, parent
+            tbl["counts"][ids] = counts
+            n_nodes += m
+            return ids
+
+        # ---- root histograms ---------------------------------------------------------------
+        root_ids = add_nodes(np.arange(Tn), np.zeros(Tn, np.int64), np.full(Tn, -1), np.zeros((Tn, C), np.int64))
+        fr = _Frontier(root_ids, starts_h.copy(), cnt_h.copy(), np.zeros(Tn, np.int64))
+        hist = torch.zeros((Tn, C, TB), dtype=torch.int64, device=dev)
+        inode, istart, ilen, _ = self._chunks(np.arange(Tn), fr.start, fr.count, chunk)
+        FO.forest_hist(cb, lb, wb, inode, istart, ilen, bins_d, offs_d, bins, TB, C, hist)
+        if comm.is_distributed:
+            comm.all_reduce(hist)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(p.seed * 1000003 + 17)
+        level = 0
+        n_hist_rows = int(fr.count.sum())
+        while fr.node.size:
+            tl = time.perf_counter()
+            A = fr.node.size
+            fmask = self._mask(A, F, gen, dev)
+            rnd = torch.rand(A, generator=gen, device=dev)
+            feat, thr, score, imp, left = FO.forest_split(hist, fmask, bins_d, offs_d, bins, algo, topk, rnd)
+            tot = hist[:, :, TB - 1]
+            pop = tot.sum(1).double()
+            depth_d = torch.as_tensor(fr.depth, device=dev)
+            stop = ~torch.isfinite(score) | (imp <= 0)
+            if p.stopping == "maxDepth":
+                stop |= depth_d >= p.max_depth
+            elif p.stopping == "minPopulation":
+                stop |= pop < p.min_population
+            elif p.stopping == "minInfoGain":
+                stop |= (imp.double() - score.double()) < p.min_info_gain
+            feat_eff = torch.where(stop, torch.full_like(feat, -1), feat).int().contiguous()
+            thr = thr.int().contiguous()
+            inode, istart, ilen, nch = self._chunks(np.arange(A), fr.start, fr.count, chunk)
+            # last level (every child at max depth): children are leaves, rows need no partition
+            last = p.stopping == "maxDepth" and bool((fr.depth + 1 >= p.max_depth).all())
+            item_left = (torch.zeros(inode.size, dtype=torch.int32) if last
+                         else FO.forest_part_count(cb, inode, istart, ilen, feat_eff, thr))
+            # ---- the ONE host copy of the level ----
+            pack = [feat_eff.cpu(), thr.cpu(), left.cpu(), tot.cpu(), imp.double().cpu(), item_left.cpu()]
+            f_h, t_h, l_h, tot_h, imp_h, il_h = [x.numpy() for x in pack]
+            ids = fr.node
+            tbl["counts"][ids] = tot_h
+            tbl["imp"][ids] = imp_h
+            split = f_h >= 0
+            if not split.any():
+                break
+            # per-node local left / right row counts from the chunk counts
+            il_h = il_h.astype(np.int64)
+            ends = np.cumsum(nch)
+            first = ends - nch
+            csum = np.concatenate([[0], np.cumsum(il_h)])
+            nleft = csum[ends] - csum[first]
+            nright = fr.count - nleft
+            sp = np.nonzero(split)[0]
+            tbl["feat"][ids[sp]] = f_h[sp]
+            tbl["thr"][ids[sp]] = t_h[sp]
+            lc = l_h[sp]
+            rc = tot_h[sp] - lc
+            d1 = fr.depth[sp] + 1
+            kids = add_nodes(np.repeat(tbl["tree"][ids[sp]], 2), np.repeat(d1, 2), np.repeat(ids[sp], 2),
+                             np.stack([lc, rc], 1).reshape(-1, C))
+            lk, rk = kids[0::2], kids[1::2]
+            tbl["left"][ids[sp]], tbl["right"][ids[sp]] = lk, rk
+            # ---- next frontier: children that can still split -------------------------------
+            ch_node = np.stack([lk, rk], 1).reshape(-1)
+            ch_start = np.stack([fr.start[sp], fr.start[sp] + nleft[sp]], 1).reshape(-1)
+            ch_count = np.stack([nleft[sp], nright[sp]], 1).reshape(-1)
+            ch_depth = np.repeat(d1, 2)
+            ch_w = np.stack([lc.sum(1), rc.sum(1)], 1).reshape(-1)          # global weighted populations
+            ch_pure = (np.stack([lc, rc], 1).reshape(-1, C) > 0).sum(1) <= 1
+            go = (ch_w >= 2) & ~ch_pure
+            if p.stopping == "maxDepth":
+                go &= ch_depth < p.max_depth
+            elif p.stopping == "minPopulation":
+                go &= ch_w >= p.min_population
+            if last:
+                go[:] = False
+            # partition: only the rows of nodes with a continuing child move (leaf rows are done)
+            need = np.zeros(A, dtype=bool)
+            need[sp] = go.reshape(-1, 2).any(1)
+            if need.any():
+                item_right = ilen.astype(np.int64) - il_h
+                rsum = np.concatenate([[0], np.cumsum(item_right)])
+                owner = inode.astype(np.int64)
+                lbase = fr.start[owner] + (csum[:-1] - csum[first[owner]])
+                rbase = fr.start[owner] + nleft[owner] + (rsum[:-1] - rsum[first[owner]])
+                fs_h = np.where(need, f_h, -1).astype(np.int32)
+                feat_sc = torch.from_numpy(fs_h).to(dev) if need.sum() < sp.size else feat_eff
+                FO.forest_part_scatter(cb, lb, wb, cb2, lb2, wb2, inode, istart, ilen, lbase, rbase, il_h, feat_sc,
+                                       thr)
+                cb, cb2, lb, lb2, wb, wb2 = cb2, cb, lb2, lb, wb2, wb
+            parent_slot = np.repeat(sp, 2)
+            sib = np.arange(ch_node.size) ^ 1
+            both = go & go[sib]
+            # of a live pair the lighter child is built, the heavier derived (ties: left built)
+            lighter = np.where(np.arange(ch_node.size) % 2 == 0, ch_w <= ch_w[sib], ch_w < ch_w[sib])
+            build = go & (~both | lighter)
+            derive = go & both & ~lighter
+            order = np.concatenate([np.nonzero(build)[0], np.nonzero(derive)[0]])
+            nb = int(build.sum())
+            newA = order.size
+            slot_of = np.full(ch_node.size, -1, np.int64)
+            slot_of[order] = np.arange(newA)
+            hist_new = torch.zeros((newA, C, TB), dtype=torch.int64, device=dev)
+            bidx = order[:nb]
+            if nb:
+                inode2, istart2, ilen2, _ = self._chunks(np.arange(nb), ch_start[bidx], ch_count[bidx], chunk)
+                FO.forest_hist(cb, lb, wb, inode2, istart2, ilen2, bins_d, offs_d, bins, TB, C, hist_new)
+                n_hist_rows += int(ch_count[bidx].sum())
+            if comm.is_distributed and newA:
+                comm.all_reduce(hist_new)
+            if newA > nb:
+                didx = order[nb:]
+                ps = torch.as_tensor(parent_slot[didx], device=dev)
+                ss = torch.as_tensor(slot_of[sib[didx]], device=dev)
+                hist_new[nb:] = hist[ps] - hist_new[ss]
+            hist = hist_new
+            fr = _Frontier(ch_node[order], ch_start[order], ch_count[order], ch_depth[order])
+            level += 1
+            self.level_times.append(time.perf_counter() - tl)
+        self.stats = {"rows_buffered": R, "levels": level, "nodes": n_nodes, "hist_rows": n_hist_rows,
+                      "chunk": chunk, "seconds": time.perf_counter() - t0}
+        return self._to_trees(tbl, n_nodes, Tn, space, t)
+
+    # ------------------------------------------------------------------------------------------
+    def _to_trees(self, tbl, n_nodes, Tn, space, t: Table) -> list[T.DecisionTree]:
+        cls = list(t.class_field.cardinality) if t.class_field else ["_"]
+        algo = self.p.algorithm
+        trees = []
+        tree_of = tbl["tree"][:n_nodes]
+        cnts = tbl["counts"][:n_nodes].astype(np.float64)
+        pops = cnts.sum(1)
+        pr_all = cnts / np.maximum(pops, 1.0)[:, None]
+        if algo == "entropy":
+            with np.errstate(divide="ignore", invalid="ignore"):
+                info_all = -np.where(pr_all > 0, pr_all * np.log2(np.where(pr_all > 0, pr_all, 1.0)), 0.0).sum(1)
+        else:
+            info_all = 1.0 - (pr_all * pr_all).sum(1)
+        info_all = np.where(pops > 0, info_all, 0.0)
+        for ti in range(Tn):
+            gids = np.nonzero(tree_of == ti)[0]
+            local = {int(g): i for i, g in enumerate(gids)}
+            nodes: list[T.Node] = []
+            preds_of: dict[int, list[str]] = {}
+            used_of: dict[int, frozenset] = {}
+            for g in gids.tolist():
+                par = int(tbl["parent"][g])
+                if par < 0:
+                    preds, used = [], frozenset()
+                else:
+                    fs = space[int(tbl["feat"][par])]
+                    s = int(tbl["thr"][par])
+                    o = fs.field.ordinal
+                    if fs.kind == "num":
+                        pv = fs.pred_value(fs.points[s])
+                        pr = f"{o} le {pv}" if int(tbl["left"][par]) == g else f"{o} gt {pv}"
+                    else:
+                        card = fs.field.cardinality
+                        pr = (f"{o} in {':'.join(card[: s + 1])}" if int(tbl["left"][par]) == g
+                              else f"{o} in {':'.join(card[s + 1:])}")
+                    preds = preds_of[par] + [pr]
+                    used = used_of[par] | {int(tbl["feat"][par])}
+                preds_of[g], used_of[g] = preds, used
+                nd = T.Node(preds, int(pops[g]), float(info_all[g]), pr_all[g].tolist(), int(tbl["depth"][g]),
+                            stopped=int(tbl["feat"][g]) < 0, used_attrs=used)
+                f = int(tbl["feat"][g])
+                if f >= 0:
+                    thr = int(tbl["thr"][g])
+                    nd.feature, nd.split = f, thr
+                    nd.segmap = [0 if b <= thr else 1 for b in range(space[f].n_bins)]
+                    nd.children = [local[int(tbl["left"][g])], local[int(tbl["right"][g])]]
+                nodes.append(nd)
+            trees.append(T.DecisionTree(nodes, space, cls))
+        return trees

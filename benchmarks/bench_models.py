@@ -54,7 +54,7 @@ def bench_rf(a):
                        attr_selection="randomAll", max_bins=32)
         sec, rf = timed(lambda: RandomForest(t.schema, trees, p, "sqrt").fit(t))
         emit(model="random_forest", rows=n, features=d, trees=trees, depth=depth, seconds=sec,
-             rows_x_trees_per_s=n * trees / sec)
+             rows_x_trees_per_s=n * trees / sec, build=getattr(rf, "build_stats", None))
         ps, _ = timed(lambda: rf.predict_proba(t), 3)
         emit(model="random_forest_predict", rows=n, trees=trees, seconds=ps, rows_per_s=n / ps)
 

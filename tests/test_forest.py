@@ -1,0 +1,184 @@
+"""Device-resident forest builder (models/forest.py, csrc/kernels/forest.hip): equivalence with the
+level-wise DecisionTreeBuilder, the kernels against their PyTorch oracles, data-parallel
+bit-exactness, and GPU == CPU."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from avenir_amd.data import synth
+from avenir_amd.data.table import load_csv
+from avenir_amd.models import tree as T
+from avenir_amd.models.forest import ForestBuilder
+from avenir_amd.ops import forest_ops as FO
+from avenir_amd.utils.schema import FeatureSchema
+from tests._dist import run_world
+
+
+def _table(tmp_path, n=3000, seed=2, device="cpu"):
+    p = tmp_path / "h.csv"
+    p.write_text("\n".join(synth.call_hangup_lines(n, seed=seed)) + "\n")
+    schema = FeatureSchema.from_json(synth.CALL_HANGUP_SCHEMA)
+    return schema, load_csv(p, schema, raw_numeric=True, device=device)
+
+
+def _paths(tree):
+    return sorted(json.dumps([x["predicates"], x["population"]]) for x in tree.to_decision_paths()["decisionPaths"])
+
+
+@pytest.mark.parametrize("alg", ["giniIndex", "entropy"])
+def test_single_tree_equals_levelwise_builder(tmp_path, alg):
+    schema, t = _table(tmp_path)
+    prm = T.TreeParams(algorithm=alg, binary=True, stopping="maxDepth", max_depth=5, attr_selection="all",
+                       sub_sampling="none")
+    old = T.DecisionTreeBuilder(schema, prm).fit(t)
+    new = ForestBuilder(schema, 1, prm).fit(t)[0]
+    assert _paths(old) == _paths(new)
+
+
+def test_forest_oracle_ops_consistency(tmp_path):
+    """Every row lands in exactly one leaf of each tree; leaf populations add up to the bootstrap weight."""
+    schema, t = _table(tmp_path, 2000, 5)
+    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=6, attr_selection="randomAll", random_attr_count=2,
+                       sub_sampling="withReplace", seed=4)
+    fb = ForestBuilder(schema, 4, prm)
+    trees = fb.fit(t)
+    for tr in trees:
+        root = tr.nodes[0]
+        leaves = [nd for nd in tr.nodes if nd.is_leaf]
+        assert sum(nd.population for nd in leaves) == root.population
+        for nd in tr.nodes:
+            if not nd.is_leaf:
+                assert sum(tr.nodes[c].population for c in nd.children) == nd.population
+    acc = float((T.TreeEnsemble(trees).predict(t).cpu() == t.labels[: t.n].long()).float().mean())
+    assert acc > 0.6
+
+
+def test_random_among_top_and_min_population(tmp_path):
+    schema, t = _table(tmp_path, 1500, 6)
+    prm = T.TreeParams(binary=True, stopping="minPopulation", min_population=100, attr_selection="all",
+                       split_selection="randomAmongTop", top_split_count=3, sub_sampling="none", seed=1)
+    tr = ForestBuilder(schema, 2, prm).fit(t)
+    for x in tr:
+        for nd in x.nodes:
+            if not nd.is_leaf:
+                assert nd.population >= 100
+
+
+def _dp_worker(rank, world, rows, sj):
+    from avenir_amd.data.table import from_arrays  # noqa: F401
+    import tempfile
+    import os
+    schema = FeatureSchema.from_json(sj)
+    d = tempfile.mkdtemp()
+    p = os.path.join(d, "h.csv")
+    open(p, "w").write("\n".join(rows) + "\n")
+    from avenir_amd.parallel.comm import get_comm
+    t = load_csv(p, schema, raw_numeric=True, rank=rank, world=world)
+    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=5, attr_selection="all", sub_sampling="none")
+    # split points must be global: build the space from the full file on every rank
+    full = load_csv(p, schema, raw_numeric=True)
+    space = T.build_split_space(schema, full, binary=True, max_bins=prm.max_bins)
+    codes = T.encode_for_tree(space, t)
+    trees = ForestBuilder(schema, 2, prm, comm=get_comm()).fit(t, space=space, codes=codes)
+    return [_paths(x) for x in trees]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_bit_exact(tmp_path, world):
+    rows = synth.call_hangup_lines(2400, seed=9)
+    ref = run_world(_dp_worker, 1, rows, synth.CALL_HANGUP_SCHEMA)[0]
+    got = run_world(_dp_worker, world, rows, synth.CALL_HANGUP_SCHEMA)
+    for g in got:
+        assert g == ref
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: kernels vs oracles, whole forest GPU == CPU
+# ---------------------------------------------------------------------------------------------
+def _rand_buffers(F=6, R=5000, B=8, C=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    codes = torch.randint(0, B + 1, (F, R), generator=g, dtype=torch.uint8)   # B = missing code
+    lab = torch.randint(0, C, (R,), generator=g, dtype=torch.uint8)
+    wt = torch.randint(0, 4, (R,), generator=g, dtype=torch.uint8)
+    return codes, lab, wt, [B] * F
+
+
+@pytest.mark.gpu
+def test_forest_kernels_match_oracles(cuda):
+    codes, lab, wt, bins = _rand_buffers()
+    F, R = codes.shape
+    C, TB = 3, sum(bins) + 1
+    offs = list(np.cumsum([0] + bins[:-1]))
+    bd, od = torch.tensor(bins, dtype=torch.int32), torch.tensor(offs, dtype=torch.int32)
+    slot = [0, 1, 1, 2, 0]
+    start = [0, 1000, 1800, 3000, 4100]
+    ln = [1000, 800, 1, 1100, 900]
+    h_c = torch.zeros((3, C, TB), dtype=torch.int64)
+    FO.forest_hist(codes, lab, wt, slot, start, ln, bd, od, bins, TB, C, h_c)
+    h_g = torch.zeros((3, C, TB), dtype=torch.int64, device=cuda)
+    FO.forest_hist(codes.to(cuda), lab.to(cuda), wt.to(cuda), slot, start, ln, bd.to(cuda), od.to(cuda), bins, TB, C,
+                   h_g)
+    assert torch.equal(h_g.cpu(), h_c)
+    m = torch.ones((3, F), dtype=torch.uint8)
+    m[1, 2] = 0
+    rnd = torch.tensor([0.1, 0.7, 0.4])
+    for algo in (0, 1):
+        for topk in (1, 3):
+            rc = FO.forest_split(h_c, m, bd, od, bins, algo, topk, rnd)
+            rg = FO.forest_split(h_g, m.to(cuda), bd.to(cuda), od.to(cuda), bins, algo, topk, rnd.to(cuda))
+            assert torch.equal(rg[0].cpu(), rc[0]) and torch.equal(rg[1].cpu(), rc[1])
+            assert torch.allclose(rg[2].cpu(), rc[2], rtol=1e-6) and torch.equal(rg[4].cpu(), rc[4])
+    feat = torch.tensor([2, -1, 4], dtype=torch.int32)
+    thr = torch.tensor([3, 0, 5], dtype=torch.int32)
+    node = [0, 0, 2, 1]
+    st, ln = [0, 1500, 3000, 2000], [1500, 1500, 2000, 1000]
+    lc = FO.forest_part_count(codes, node, st, ln, feat, thr)
+    lg = FO.forest_part_count(codes.to(cuda), node, st, ln, feat.to(cuda), thr.to(cuda))
+    assert torch.equal(lg.cpu(), lc)
+    # bases: node 0 segment [0, 3000) two chunks, node 2 segment [3000, 5000)
+    nl0 = int(lc[0] + lc[1])
+    lbase = [0, int(lc[0]), 3000, 2000]
+    rbase = [nl0, nl0 + (1500 - int(lc[0])), 3000 + int(lc[2]), 2000]
+    outs = []
+    for dev in ("cpu", cuda):
+        dc, dl, dw = torch.zeros_like(codes).to(dev), torch.zeros_like(lab).to(dev), torch.zeros_like(wt).to(dev)
+        FO.forest_part_scatter(codes.to(dev), lab.to(dev), wt.to(dev), dc, dl, dw, node, st, ln, lbase, rbase, lc,
+                               feat.to(dev), thr.to(dev))
+        outs.append((dc.cpu(), dl.cpu(), dw.cpu()))
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+    # stability: the left part of node 0 is its rows with code <= 3 in original order
+    sel = torch.nonzero(codes[2, :3000].long() <= 3).view(-1)
+    assert torch.equal(outs[0][0][:, :nl0], codes[:, sel])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,sel", [("giniIndex", "best"), ("entropy", "randomAmongTop")])
+def test_forest_gpu_equals_cpu(cuda, tmp_path, alg, sel):
+    schema, t = _table(tmp_path, 20000, 3)
+    tg = t.to(cuda)
+    prm = T.TreeParams(algorithm=alg, binary=True, stopping="maxDepth", max_depth=7, attr_selection="all",
+                       split_selection=sel, top_split_count=2, sub_sampling="none")
+    g = torch.Generator().manual_seed(1)
+    w = torch.poisson(torch.ones((3, t.n)), generator=g).clamp_max(255).to(torch.uint8)
+    space = T.build_split_space(schema, t, binary=True, max_bins=prm.max_bins)
+    cpu = ForestBuilder(schema, 3, prm).fit(t, space=space, weights=w)
+    gpu = ForestBuilder(schema, 3, prm).fit(tg, space=space, weights=w)
+    if sel == "best":
+        for a, b in zip(cpu, gpu):
+            assert _paths(a) == _paths(b)
+    else:   # random picks use the device RNG: same structure statistics only
+        assert all(len(b.nodes) > 10 for b in gpu)
+
+
+@pytest.mark.gpu
+def test_bucketize_kernel_matches_torch(cuda, tmp_path):
+    schema, t = _table(tmp_path, 5000, 8)
+    tg = t.to(cuda)
+    tg.numeric[0, 7] = float("nan")
+    t.numeric[0, 7] = float("nan")
+    space = T.build_split_space(schema, t, binary=True, max_bins=32)
+    c_cpu = T.encode_for_tree(space, t)
+    c_gpu = T.encode_for_tree(space, tg)
+    assert torch.equal(c_gpu.cpu(), c_cpu)
