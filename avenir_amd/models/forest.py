@@ -40,6 +40,25 @@ class _Frontier:
     start: np.ndarray     # int64 local row offset of the node's segment in the buffer
     count: np.ndarray     # int64 local row count
     depth: np.ndarray     # int64
+    key: np.ndarray       # int64 holding a uint32 per-node random key (see _h32)
+
+
+_M32 = 0xFFFFFFFF
+
+
+def _h32(x):
+    """32-bit integer mixer (two multiply-xorshift rounds) on int64 arrays / tensors holding uint32
+    values; every product stays below 2^59, so numpy, torch CPU and torch GPU agree bit for bit."""
+    x = x & _M32
+    x = (((x >> 16) ^ x) * 0x45D9F3B) & _M32
+    x = (((x >> 16) ^ x) * 0x45D9F3B) & _M32
+    return (x >> 16) ^ x
+
+
+def _child_keys(key: np.ndarray) -> np.ndarray:
+    """Keys of the (left, right) children, interleaved: a node's random stream depends only on the
+    seed, its tree id and its path, never on which other trees / ranks grow alongside it."""
+    return np.stack([_h32(key ^ 0x5BD1E995), _h32(key ^ 0x1B873593)], 1).reshape(-1)
 
 
 class ForestBuilder:
@@ -94,12 +113,15 @@ class ForestBuilder:
         ilen = np.clip(seg_cnt - k * chunk, 0, chunk)
         return item_node.astype(np.int32), istart.astype(np.int64), ilen.astype(np.int32), nch
 
-    def _mask(self, A: int, F: int, gen: torch.Generator, dev) -> torch.Tensor:
+    def _mask(self, A: int, F: int, key: torch.Tensor, dev) -> torch.Tensor:
+        """Random feature subset per node from its key: the k features with the smallest
+        h32(key ^ f * golden) (ties broken by feature index)."""
         p = self.p
         if p.attr_selection in ("all", "notUsedYet") or A == 0:
             return torch.ones((A, F), dtype=torch.uint8, device=dev)
         k = max(1, min(p.random_attr_count, F))
-        r = torch.rand((A, F), generator=gen, device=dev)
+        fk = (torch.arange(F, device=dev, dtype=torch.int64) * 0x9E3779B9) & _M32
+        r = _h32(key.view(-1, 1) ^ fk.view(1, -1)) * F + torch.arange(F, device=dev).view(1, -1)
         idx = torch.topk(r, k, dim=1, largest=False).indices
         m = torch.zeros((A, F), dtype=torch.uint8, device=dev)
         m.scatter_(1, idx, 1)
@@ -126,6 +148,8 @@ class ForestBuilder:
         topk = p.top_split_count if p.split_selection == "randomAmongTop" else 1
         tree_ids = list(range(self.n_trees)) if tree_ids is None else tree_ids
         Tn = len(tree_ids)
+        if Tn == 0:        # tree-parallel with more ranks than trees
+            return []
         bins_d = torch.tensor(bins, dtype=torch.int32, device=dev)
         offs_d = torch.tensor(offs, dtype=torch.int32, device=dev)
         t0 = time.perf_counter()
@@ -179,21 +203,21 @@ class ForestBuilder:
 
         # ---- root histograms ---------------------------------------------------------------
         root_ids = add_nodes(np.arange(Tn), np.zeros(Tn, np.int64), np.full(Tn, -1), np.zeros((Tn, C), np.int64))
-        fr = _Frontier(root_ids, starts_h.copy(), cnt_h.copy(), np.zeros(Tn, np.int64))
+        root_key = _h32((np.int64(p.seed) * 1000003 + 7) ^ (np.asarray(tree_ids, np.int64) * 2654435761))
+        fr = _Frontier(root_ids, starts_h.copy(), cnt_h.copy(), np.zeros(Tn, np.int64), root_key)
         hist = torch.zeros((Tn, C, TB), dtype=torch.int64, device=dev)
         inode, istart, ilen, _ = self._chunks(np.arange(Tn), fr.start, fr.count, chunk)
         FO.forest_hist(cb, lb, wb, inode, istart, ilen, bins_d, offs_d, bins, TB, C, hist)
         if comm.is_distributed:
             comm.all_reduce(hist)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(p.seed * 1000003 + 17)
         level = 0
         n_hist_rows = int(fr.count.sum())
         while fr.node.size:
             tl = time.perf_counter()
             A = fr.node.size
-            fmask = self._mask(A, F, gen, dev)
-            rnd = torch.rand(A, generator=gen, device=dev)
+            key_d = torch.as_tensor(fr.key, device=dev)
+            fmask = self._mask(A, F, key_d, dev)
+            rnd = (_h32(key_d ^ 0x2545F491).double() / 4294967296.0).float()
             feat, thr, score, imp, left = FO.forest_split(hist, fmask, bins_d, offs_d, bins, algo, topk, rnd)
             tot = hist[:, :, TB - 1]
             pop = tot.sum(1).double()
@@ -292,7 +316,8 @@ class ForestBuilder:
                 ss = torch.as_tensor(slot_of[sib[didx]], device=dev)
                 hist_new[nb:] = hist[ps] - hist_new[ss]
             hist = hist_new
-            fr = _Frontier(ch_node[order], ch_start[order], ch_count[order], ch_depth[order])
+            ch_key = _child_keys(fr.key[sp])
+            fr = _Frontier(ch_node[order], ch_start[order], ch_count[order], ch_depth[order], ch_key[order])
             level += 1
             self.level_times.append(time.perf_counter() - tl)
         self.stats = {"rows_buffered": R, "levels": level, "nodes": n_nodes, "hist_rows": n_hist_rows,

@@ -80,19 +80,32 @@ def merge_topk(d1, i1, d2, i2, k):
 def distributed_knn(Q: torch.Tensor, R: torch.Tensor, k: int, comm, metric: str = "euclidean",
                     r_base: int = 0, q_base: int = 0, exclude_self: bool = False):
     """Systolic all-pairs kNN: every rank keeps its query shard and passes its reference shard
-    around the ring (``Comm.ring_pass``) — no bucket-pair replication.  ``r_base``
-    is this rank's global index offset of R."""
+    around the ring — no bucket-pair replication.  The shard sizes are exchanged
+    ONCE up front (one all-gather), so every hop's receive buffer and global index base are known on
+    the host; the send/receive of the NEXT shard is posted (``Comm.ring_pass_start``) before the
+    fused distance + top-k of the current one, so the transfer over xGMI overlaps the compute.
+    ``r_base`` is this rank's global index offset of R (kept for the single-rank path)."""
     if not comm.is_distributed:
         return knn(Q, R, k, metric, exclude_self=exclude_self, q_base=q_base, r_base=r_base)
     best_d = torch.full((Q.shape[0], k), math.inf, device=Q.device)
     best_i = torch.full((Q.shape[0], k), -1, dtype=torch.long, device=Q.device)
-    cur, cur_base = R, torch.tensor([r_base], dtype=torch.long, device=Q.device)
-    for step in range(comm.world):
-        d, i = knn(Q, cur, k, metric, exclude_self=exclude_self, q_base=q_base, r_base=int(cur_base.item()))
+    n = torch.tensor([R.shape[0]], dtype=torch.long, device=Q.device)
+    sizes = comm.all_gather(n).view(-1).tolist()
+    bases = [0]
+    for c in sizes[:-1]:
+        bases.append(bases[-1] + c)
+    cur = R.contiguous()
+    W, me = comm.world, comm.rank
+    for step in range(W):
+        owner = (me - step) % W                 # whose shard ``cur`` is
+        pending = None
+        if step + 1 < W:
+            src = (me - step - 1) % W
+            pending = comm.ring_pass_start(cur, sizes[src])
+        d, i = knn(Q, cur, k, metric, exclude_self=exclude_self, q_base=q_base, r_base=bases[owner])
         best_d, best_i = merge_topk(best_d, best_i, d, i, k)
-        if step + 1 < comm.world:
-            cur = comm.ring_pass(cur)
-            cur_base = comm.ring_pass(cur_base)
+        if pending is not None:
+            cur = comm.ring_pass_finish(pending)
     return best_d, best_i
 
 

@@ -39,7 +39,7 @@ class CollectiveTimeout(RuntimeError):
 
 class Comm:
     def __init__(self, backend: str | None = None, timeout_s: float | None = None,
-                 device: str | None = None):
+                 device: str | None = None, port: int | None = None):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
@@ -56,7 +56,9 @@ class Comm:
         self._owns_pg = False
         if self.world > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29533")
+            # torchrun exports MASTER_PORT; AVENIR_MASTER_PORT (or Comm(port=...)) overrides the
+            # fallback used when a job starts its own ranks
+            os.environ.setdefault("MASTER_PORT", str(port or os.environ.get("AVENIR_MASTER_PORT", "29533")))
             kw = {}
             if self.backend == "nccl":
                 kw["device_id"] = self.device
@@ -210,6 +212,24 @@ class Comm:
         for r in reqs:
             r.wait()
         return recv.to(t.device) if moved else recv
+
+    def ring_pass_start(self, t: torch.Tensor, recv_rows: int):
+        """Post the send of ``t`` to rank+1 and the receive of ``recv_rows`` rows (same trailing
+        shape / dtype) from rank-1; returns a handle for :meth:`ring_pass_finish`.  Issued as one
+        batched P2P group (``batch_isend_irecv``: no send/recv ordering deadlock on RCCL) so the
+        caller can compute while the transfer is in flight."""
+        nxt, prv = (self.rank + 1) % self.world, (self.rank - 1) % self.world
+        x, moved = self._prep(t.contiguous())
+        recv = torch.empty((int(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        ops = [dist.P2POp(dist.isend, x, nxt), dist.P2POp(dist.irecv, recv, prv)]
+        reqs = dist.batch_isend_irecv(ops)
+        return reqs, recv, x, (t.device if moved else None)
+
+    def ring_pass_finish(self, handle) -> torch.Tensor:
+        reqs, recv, _keepalive, dev = handle
+        for r in reqs:
+            r.wait()
+        return recv.to(dev) if dev is not None else recv
 
     def barrier(self) -> None:
         if self.is_distributed:

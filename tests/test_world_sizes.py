@@ -1,0 +1,162 @@
+"""Multi-rank equivalence at world sizes 1, 2, 4 and 8 (gloo, CPU processes): every distributed
+model trained on row shards must give the single-process result — counts bit-exact, floats within
+tolerance.  One spawn per world size runs all models."""
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from _dist import run_world
+from avenir_amd.data import synth
+
+
+def _data():
+    d = tempfile.mkdtemp(prefix="avmi_ws_")
+    churn = os.path.join(d, "churn.csv")
+    synth.write_churn(churn, 3001, seed=5)
+    hang = os.path.join(d, "hangup.csv")
+    with open(hang, "w") as fh:
+        fh.write("\n".join(synth.call_hangup_lines(2003, seed=8)) + "\n")
+    rng = np.random.default_rng(7)
+    seqs = [[str(x) for x in rng.integers(0, 4, 12)] for _ in range(401)]
+    tagged = [[f"{'ab'[int(s) % 2]}:{'HL'[int(s) // 2]}" for s in row] for row in seqs]
+    tx = [sorted({f"i{int(v)}" for v in rng.integers(0, 9, 5)}) for _ in range(503)]
+    return churn, hang, seqs, tagged, tx
+
+
+def _shard(xs, rank, world):
+    n = len(xs)
+    return xs[rank * n // world:(rank + 1) * n // world]
+
+
+def _all_models(rank, world, churn, hang, seqs, tagged, tx):
+    from avenir_amd.data.table import load_csv
+    from avenir_amd.models import tree as T
+    from avenir_amd.models.association import Apriori
+    from avenir_amd.models.bayes import NaiveBayes
+    from avenir_amd.models.cluster import KMeans
+    from avenir_amd.models.explore import MutualInformation, categorical_correlation
+    from avenir_amd.models.forest import ForestBuilder
+    from avenir_amd.models.linear import LogisticRegression
+    from avenir_amd.models.markov import (HiddenMarkovModelBuilder, MarkovStateTransitionModel,
+                                          ProbabilisticSuffixTree)
+    from avenir_amd.ops import distance as D
+    from avenir_amd.ops import sequence_ops as SO
+    from avenir_amd.parallel.comm import get_comm
+    from avenir_amd.utils.schema import FeatureSchema
+    comm = get_comm()
+    out = {}
+    # ---- counting models: bit-exact -----------------------------------------------------------
+    cs = FeatureSchema.from_json(synth.CHURN_SCHEMA)
+    t = load_csv(churn, cs, rank=rank, world=world)
+    nb = NaiveBayes(cs, comm=comm).fit(t)
+    out["nb"] = (nb.counts.tolist(), nb.class_n.tolist())
+    mi = MutualInformation(comm=comm)
+    r = mi.fit(t)
+    out["mi"] = sorted((k, round(v, 12)) for k, v in r.feature_class.items())
+    out["cramer"] = sorted((k, round(v, 12)) for k, v in categorical_correlation(t, comm=comm).items())
+    m = MarkovStateTransitionModel(["0", "1", "2", "3"], comm=comm)
+    m.fit(m.encode(_shard(seqs, rank, world)))
+    out["markov"] = m.counts.tolist()
+    hb = HiddenMarkovModelBuilder(["H", "L"], ["a", "b"], comm=comm)
+    ob, st = hb.encode(_shard(tagged, rank, world))
+    hmm = hb.fit(ob, st)
+    out["hmm"] = (hmm.A.tolist(), hmm.B.tolist(), hmm.pi.tolist())
+    pst = ProbabilisticSuffixTree(4, 3).fit(m.encode(_shard(seqs, rank, world)), comm=comm)
+    out["pst"] = [(tok, ch.count) for tok, ch in sorted(pst.root.children.items())]
+    fi = Apriori(0.08, max_len=3, comm=comm).fit_transactions(_shard(tx, rank, world))
+    out["apriori"] = sorted((tuple(fi.items[i] for i in s), c) for lvl in fi.levels.values() for s, c in lvl)
+    # ---- trees: level-wise builder (data parallel), forest data-parallel and tree-parallel ----
+    hs = FeatureSchema.from_json(synth.CALL_HANGUP_SCHEMA)
+    th = load_csv(hang, hs, rank=rank, world=world, raw_numeric=True)
+    full = load_csv(hang, hs, raw_numeric=True)
+    tr = T.DecisionTreeBuilder(hs, T.TreeParams(max_depth=3), comm=comm).fit(th)
+    out["tree"] = [(n.predicates, n.population) for n in tr.nodes]
+    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=4, attr_selection="all", sub_sampling="none")
+    space = T.build_split_space(hs, full, binary=True, max_bins=32)
+    fb = ForestBuilder(hs, 2, prm, comm=comm).fit(th, space=space, codes=T.encode_for_tree(space, th))
+    out["forest_dp"] = [[(n.predicates, n.population) for n in x.nodes] for x in fb]
+    rf = T.RandomForest(hs, 6, T.TreeParams(binary=True, stopping="maxDepth", max_depth=4,
+                                            sub_sampling="withReplace", attr_selection="randomAll", seed=3),
+                        "sqrt", comm=comm, tree_parallel=True).fit(full)
+    out["forest_tp"] = [[(n.predicates, n.population) for n in x.nodes] for x in rf.trees]
+    # ---- float models: tolerance ------------------------------------------------------------
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(2000, 3, generator=g) + torch.randint(0, 3, (2000, 1), generator=g) * 6.0
+    km = KMeans(3, seed=5, comm=comm).fit(_shard(X, rank, world))
+    out["kmeans"] = float(km.best[3].sse)
+    w = torch.tensor([1.0, -2.0, 0.5])
+    y = ((X @ w + 2.0 * torch.randn(2000, generator=g)) > 0).double()     # non-separable: finite optimum
+    lr = LogisticRegression(max_iter=10).fit(_shard(X, rank, world), _shard(y, rank, world))
+    out["logit"] = lr.coef.tolist()
+    Q = torch.randn(64, 3, generator=g)
+    lo = rank * 2000 // world
+    d, i = D.distributed_knn(Q, _shard(X, rank, world).contiguous(), 5, comm, r_base=lo)
+    out["knn"] = (d.tolist(), i.tolist())
+    # ---- sequence parallel Viterbi -----------------------------------------------------------
+    gh = torch.Generator().manual_seed(9)
+    norm = lambda mm: torch.log(mm / mm.sum(-1, keepdim=True))
+    lA = norm(torch.rand(5, 5, generator=gh, dtype=torch.float64) + 0.05)
+    lB = norm(torch.rand(5, 4, generator=gh, dtype=torch.float64) + 0.05)
+    lp = norm(torch.rand(5, generator=gh, dtype=torch.float64) + 0.05)
+    obs = torch.randint(0, 4, (1601,), generator=gh).to(torch.int16)
+    path, score = SO.viterbi_long(_shard(obs, rank, world), lA, lB, lp, chunk=64)
+    out["viterbi"] = (path.tolist(), round(float(score), 6))
+    return out
+
+
+@pytest.fixture(scope="module")
+def reference():
+    args = _data()
+    return args, run_world(_all_models, 1, *args, timeout=300)[0]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_world_size_equivalence(reference, world):
+    args, ref = reference
+    res = run_world(_all_models, world, *args, timeout=600)
+    for r, got in enumerate(res):
+        for key in ("nb", "mi", "cramer", "markov", "hmm", "pst", "apriori", "tree", "forest_dp", "forest_tp"):
+            assert got[key] == ref[key], f"rank {r}/{world}: {key} differs"
+        assert got["kmeans"] == pytest.approx(ref["kmeans"], rel=1e-5)
+        assert np.allclose(got["logit"], ref["logit"], rtol=1e-7, atol=1e-9)
+        assert np.allclose(got["knn"][0], ref["knn"][0], atol=1e-5)
+        assert got["knn"][1] == ref["knn"][1]
+        assert got["viterbi"][1] == pytest.approx(ref["viterbi"][1], rel=1e-9)
+    # Viterbi is sequence-parallel: the rank segments concatenate to the single-rank path
+    assert sum((g["viterbi"][0] for g in res), []) == ref["viterbi"][0]
+
+
+def _cli_ranks(rank, world, data, schema, model, out_dir, out_file):
+    from avenir_amd.cli import main
+    from avenir_amd.parallel import comm as C
+    assert main(["bayesianPredictor", "-i", data, "-o", out_dir, "--schema", schema, "--model", model,
+                 "--device", "cpu"]) == 0
+    C.get_comm().barrier()
+    assert main(["bayesianPredictor", "-i", data, "-o", out_file, "--schema", schema, "--model", model,
+                 "--device", "cpu"]) == 0
+    return rank
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cli_map_output_per_rank(tmp_path, world):
+    """Map-side CLI jobs under several ranks: one part file per rank in a directory output, or the
+    rank-ordered lines gathered into a single file; either way every input row appears once."""
+    from avenir_amd.cli import main
+    data, schema = tmp_path / "churn.csv", tmp_path / "churn.json"
+    synth.write_churn(data, 1001, seed=2, schema_path=schema)
+    model = tmp_path / "nb.txt"
+    assert main(["bayesianDistribution", "-i", str(data), "-o", str(model), "--schema", str(schema),
+                 "--device", "cpu"]) == 0
+    out_dir, out_file = tmp_path / "pred", tmp_path / "pred.txt"
+    run_world(_cli_ranks, world, str(data), str(schema), str(model), str(out_dir), str(out_file))
+    parts = sorted(out_dir.glob("part-*"))
+    assert len(parts) == world
+    rows = [l for p in parts for l in p.read_text().splitlines() if l]
+    src = [l for l in data.read_text().splitlines() if l]
+    assert [r.rsplit(",", 2)[0] for r in rows] == src
+    single = [l for l in out_file.read_text().splitlines() if l]
+    assert single == rows
