@@ -1120,6 +1120,7 @@ void forest_hist(const at::Tensor& codes, const at::Tensor& lab, const at::Tenso
   CHECK_DEV(bins); CHECK_DEV(offs);
   const int64_t ld = codes.size(1), F = codes.size(0), n = slot.numel();
   TORCH_CHECK(lab.numel() >= ld && wt.numel() >= ld, "label / weight columns shorter than the code rows");
+  TORCH_CHECK(ld % 8 == 0, "row buffers must be padded to a multiple of 8 rows (8-byte lane loads)");
   TORCH_CHECK(bins.numel() == F && offs.numel() == F, "bins / offs per feature");
   TORCH_CHECK(hist.dim() == 3 && hist.size(1) == C && hist.size(2) == TB, "hist [A, C, TB]");
   check_host_items(slot, start, len, ld, hist.size(0));
@@ -1181,6 +1182,7 @@ at::Tensor forest_part_count(const at::Tensor& codes, const at::Tensor& node, co
   CHECK_DEV(feat); CHECK_DTYPE(feat, at::kInt);
   CHECK_DEV(thr); CHECK_DTYPE(thr, at::kInt);
   check_host_items(node, start, len, codes.size(1), feat.numel());
+  TORCH_CHECK(codes.size(1) % 8 == 0, "row buffers must be padded to a multiple of 8 rows");
   auto out = at::zeros({node.numel()}, feat.options());
   if (node.numel()) {
     auto d_node = to_dev(node, codes), d_start = to_dev(start, codes), d_len = to_dev(len, codes);
@@ -1206,6 +1208,7 @@ void forest_part_scatter(const at::Tensor& codes, const at::Tensor& lab, const a
               "destination buffers must match the source");
   const int64_t ld = codes.size(1);
   check_host_items(node, start, len, ld, feat.numel());
+  TORCH_CHECK(ld % 8 == 0 && lab.numel() >= ld && wt.numel() >= ld, "row buffers padded to a multiple of 8 rows");
   TORCH_CHECK(!left_base.is_cuda() && !right_base.is_cuda(), "bases are host tensors");
   CHECK_DTYPE(left_base, at::kLong);
   CHECK_DTYPE(right_base, at::kLong);

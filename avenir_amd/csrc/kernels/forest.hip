@@ -34,8 +34,28 @@ constexpr int FB_THREADS = 256;
 constexpr int FB_MAXC = 16;  // classes handled in registers by the split kernel
 
 // ------------------------------------------------------------------------------------------------
-// histogram of chunks: hist[slot][c][TB] += w for every (feature bin) + the node total at TB-1
+// Row-buffer access pattern shared by the three streaming kernels: a chunk [start, start + len) is
+// walked in tiles of 8 * 256 rows starting at start rounded DOWN to 8; lane t owns the 8
+// consecutive rows [base + 8t, base + 8t + 8) and fetches every column of them with one aligned
+// 8-byte load (a wave reads 512 contiguous bytes per column per instruction instead of 64); rows
+// outside the chunk are masked.  The buffers are padded to a multiple of 16 rows (checked by the
+// binding), so the rounded-up tail of the last chunk stays inside them.
 // ------------------------------------------------------------------------------------------------
+constexpr int RPT = 8;                    // rows per lane per tile
+constexpr int RTILE = RPT * FB_THREADS;   // 2048 rows per tile
+
+__device__ __forceinline__ unsigned valid_mask(long long r0, long long start, long long end) {
+  unsigned m = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) m |= (unsigned)(r0 + j >= start && r0 + j < end) << j;
+  return m;
+}
+
+__device__ __forceinline__ unsigned byte_of(const uint2& v, int j) {
+  return ((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xFFu;
+}
+
+// histogram of chunks: hist[slot][c][TB] += w for every (feature bin) + the node total at TB-1
 __global__ __launch_bounds__(FB_THREADS) void forest_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, const uint8_t* __restrict__ lab, const uint8_t* __restrict__ wt,
     const int* __restrict__ item_slot, const long long* __restrict__ item_start, const int* __restrict__ item_len,
@@ -47,18 +67,33 @@ __global__ __launch_bounds__(FB_THREADS) void forest_hist_kernel(
   for (int i = threadIdx.x; i < per; i += FB_THREADS) s_h[i] = 0;
   __syncthreads();
   const long long start = item_start[item];
-  const int len = item_len[item];
-  for (int i = threadIdx.x; i < len; i += FB_THREADS) {
-    const long long r = start + i;
-    const unsigned c = lab[r];
-    const unsigned w = wt[r];
-    if (c >= (unsigned)C || w == 0) continue;
-    unsigned int* row = s_h + c * TB;
-    for (int f = 0; f < nfeat; ++f) {
-      const unsigned v = codes[(long long)f * ld + r];
-      if (v < (unsigned)bins[f]) atomicAdd(&row[offs[f] + v], w);
+  const long long end = start + item_len[item];
+  for (long long base = start & ~7LL; base < end; base += RTILE) {
+    const long long r0 = base + RPT * threadIdx.x;
+    unsigned m = valid_mask(r0, start, end);
+    if (!m) continue;
+    const uint2 lv = *reinterpret_cast<const uint2*>(lab + r0);
+    const uint2 wv = *reinterpret_cast<const uint2*>(wt + r0);
+    unsigned c8[RPT], w8[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      c8[j] = byte_of(lv, j);
+      w8[j] = byte_of(wv, j);
+      if (c8[j] >= (unsigned)C || w8[j] == 0) m &= ~(1u << j);
     }
-    atomicAdd(&row[TB - 1], w);
+    if (!m) continue;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j)
+      if (m >> j & 1) atomicAdd(&s_h[c8[j] * TB + TB - 1], w8[j]);
+    for (int f = 0; f < nfeat; ++f) {
+      const uint2 cv = *reinterpret_cast<const uint2*>(codes + (long long)f * ld + r0);
+      const unsigned B = (unsigned)bins[f], o = (unsigned)offs[f];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const unsigned v = byte_of(cv, j);
+        if ((m >> j & 1) && v < B) atomicAdd(&s_h[c8[j] * TB + o + v], w8[j]);
+      }
+    }
   }
   __syncthreads();
   unsigned long long* dst = hist + (long long)item_slot[item] * per;
@@ -194,10 +229,14 @@ __global__ __launch_bounds__(FB_THREADS) void forest_split_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// partition: count rows going left / right per chunk of a splitting node's segment
+// partition: count rows going left per chunk of a splitting node's segment
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool goes_left(const uint8_t* codes, long long ld, long long r, int f, int thr) {
-  return (int)codes[(long long)f * ld + r] <= thr;  // missing codes (>= bins) are > thr: right
+// left bits of the 8 rows (code <= thr; missing codes >= bins are > thr: right)
+__device__ __forceinline__ unsigned left_bits(const uint2& cv, int thr) {
+  unsigned b = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) b |= (unsigned)((int)byte_of(cv, j) <= thr) << j;
+  return b;
 }
 
 __global__ __launch_bounds__(FB_THREADS) void forest_part_count_kernel(
@@ -212,27 +251,33 @@ __global__ __launch_bounds__(FB_THREADS) void forest_part_count_kernel(
   const int f = feat[a];
   const int t = thr[a];
   const long long start = item_start[item];
-  const int len = item_len[item];
+  const long long end = start + item_len[item];
   int cnt = 0;
-  if (f >= 0)
-    for (int i = threadIdx.x; i < len; i += FB_THREADS) cnt += goes_left(codes, ld, start + i, f, t) ? 1 : 0;
+  if (f >= 0) {
+    const uint8_t* col = codes + (long long)f * ld;
+    for (long long base = start & ~7LL; base < end; base += RTILE) {
+      const long long r0 = base + RPT * threadIdx.x;
+      const unsigned m = valid_mask(r0, start, end);
+      if (m) cnt += __popc(left_bits(*reinterpret_cast<const uint2*>(col + r0), t) & m);
+    }
+  }
   cnt = av::wave_sum(cnt);
   if (av::lane_id() == 0 && cnt) atomicAdd(&s_cnt, cnt);
   __syncthreads();
   if (threadIdx.x == 0) item_left[item] = s_cnt;
 }
 
-// Stable scatter: rows of a chunk keep their order within the left / right part.
+// Stable scatter of a splitting node's rows into [left rows | right rows] (order kept within each).
 //
-// A tile of 1024 rows (4 per lane, strided so every wave load is 64 contiguous bytes) is ranked
-// with wave ballots (4 sub-passes of 256 rows, LDS prefix over the 4 waves), then every column of
-// the tile is STAGED in LDS in partitioned order ([left rows | right rows], F + 2 columns x 1 KiB),
-// and written out as two contiguous runs per column with aligned dword stores (byte stores only
-// for the unaligned head / tail of a run).  The first version stored every byte of every row at its
-// destination individually (~1.1 TB/s); the runs of consecutive tiles abut, and a dword is only
-// written when the run owns all four of its bytes, so tiles never clobber each other.
-constexpr int PT = 4;
-constexpr int TILE = FB_THREADS * PT;
+// Per 2048-row tile: every lane ranks its 8 rows (popcounts of the left / right bits), one wave
+// inclusive scan of the packed (left | right << 16) counts + an LDS prefix over the 4 waves gives
+// each row its position in the tile's partitioned order; then the columns are moved in groups of
+// SG: aligned 8-byte loads, bytes dropped into an LDS stage at their partitioned position, and the
+// stage written out as two contiguous runs per column (left run at lb, right run at rb) with
+// aligned dword stores (byte stores only for a run's unaligned head / tail; a dword is written
+// only when the run owns all 4 of its bytes, so abutting runs of consecutive tiles never clobber
+// each other).
+constexpr int SG = 6;  // columns staged per group: SG * 2 KiB of LDS
 
 __device__ __forceinline__ void write_run(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int n) {
   const int head = min(n, (int)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3));
@@ -252,67 +297,72 @@ __global__ __launch_bounds__(FB_THREADS) void forest_part_scatter_kernel(
     const int* __restrict__ item_node, const long long* __restrict__ item_start, const int* __restrict__ item_len,
     const long long* __restrict__ left_base, const long long* __restrict__ right_base, const int* __restrict__ feat,
     const int* __restrict__ thr) {
-  extern __shared__ uint8_t s_stage[];  // [(nfeat + 2)][TILE]
-  __shared__ int s_wl[FB_THREADS / AV_WAVE], s_wr[FB_THREADS / AV_WAVE];
+  __shared__ uint8_t s_stage[SG][RTILE];
+  __shared__ int s_wtot[FB_THREADS / AV_WAVE];
   const int item = blockIdx.x;
   const int a = item_node[item];
   const int f = feat[a];
   if (f < 0) return;  // uniform over the block: no barrier is skipped by part of it
   const int t = thr[a];
   const long long start = item_start[item];
-  const int len = item_len[item];
+  const long long end = start + item_len[item];
   const int ncol = nfeat + 2;
   long long lb = left_base[item], rb = right_base[item];
   const int lane = av::lane_id(), wave = av::wave_id();
-  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int t0 = 0; t0 < len; t0 += TILE) {
-    int pos[PT];
-    bool isl[PT];
-    int nl = 0, nr = 0;
+  const uint8_t* scol = codes + (long long)f * ld;
+  for (long long base = start & ~7LL; base < end; base += RTILE) {
+    const long long r0 = base + RPT * threadIdx.x;
+    const unsigned m = valid_mask(r0, start, end);
+    const unsigned lbits = m ? (left_bits(*reinterpret_cast<const uint2*>(scol + r0), t) & m) : 0u;
+    const unsigned rbits = m & ~lbits;
+    // packed inclusive scan over the wave: low 16 bits left counts, high 16 bits right counts
+    const int mine = __popc(lbits) | (__popc(rbits) << 16);
+    int inc = mine;
 #pragma unroll
-    for (int j = 0; j < PT; ++j) {
-      const int i = t0 + j * FB_THREADS + threadIdx.x;
-      const bool valid = i < len;
-      const bool left = valid && goes_left(codes, ld, start + i, f, t);
-      const bool right = valid && !left;
-      const unsigned long long bl = __ballot(left), br = __ballot(right);
-      if (lane == 0) {
-        s_wl[wave] = __popcll(bl);
-        s_wr[wave] = __popcll(br);
+    for (int o = 1; o < AV_WAVE; o <<= 1) {
+      const int y = __shfl_up(inc, o, AV_WAVE);
+      if (lane >= o) inc += y;
+    }
+    if (lane == AV_WAVE - 1) s_wtot[wave] = inc;
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int w = 0; w < FB_THREADS / AV_WAVE; ++w) {
+      if (w < wave) before += s_wtot[w];
+      tot += s_wtot[w];
+    }
+    const int excl = before + inc - mine;
+    const int nl = tot & 0xFFFF, nr = tot >> 16;
+    int pl = excl & 0xFFFF, pr = nl + (excl >> 16);
+    short pos[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      pos[j] = -1;
+      if (lbits >> j & 1) pos[j] = (short)(pl++);
+      else if (rbits >> j & 1) pos[j] = (short)(pr++);
+    }
+    for (int g0 = 0; g0 < ncol; g0 += SG) {
+      const int ng = min(SG, ncol - g0);
+      for (int g = 0; g < ng; ++g) {
+        const int k = g0 + g;
+        const uint8_t* src = k < nfeat ? codes + (long long)k * ld : (k == nfeat ? lab : wt);
+        if (m) {
+          const uint2 v = *reinterpret_cast<const uint2*>(src + r0);
+#pragma unroll
+          for (int j = 0; j < RPT; ++j)
+            if (pos[j] >= 0) s_stage[g][pos[j]] = (uint8_t)byte_of(v, j);
+        }
       }
       __syncthreads();
-      int ol = 0, orr = 0, tl = 0, tr = 0;
-      for (int w = 0; w < FB_THREADS / AV_WAVE; ++w) {
-        if (w < wave) {
-          ol += s_wl[w];
-          orr += s_wr[w];
-        }
-        tl += s_wl[w];
-        tr += s_wr[w];
+      for (int g = 0; g < ng; ++g) {
+        const int k = g0 + g;
+        uint8_t* dst = k < nfeat ? dcodes + (long long)k * ld : (k == nfeat ? dlab : dwt);
+        write_run(dst + lb, s_stage[g], nl);
+        write_run(dst + rb, s_stage[g] + nl, nr);
       }
-      isl[j] = left;
-      pos[j] = !valid ? -1 : (left ? nl + ol + __popcll(bl & below) : nr + orr + __popcll(br & below));
-      nl += tl;
-      nr += tr;
-      __syncthreads();  // s_wl / s_wr are rewritten by the next sub-pass
-    }
-    // stage every column in partitioned order: [0, nl) left rows, [nl, nl + nr) right rows
-    for (int k = 0; k < ncol; ++k) {
-      const uint8_t* src = k < nfeat ? codes + (long long)k * ld : (k == nfeat ? lab : wt);
-      uint8_t* st = s_stage + k * TILE;
-#pragma unroll
-      for (int j = 0; j < PT; ++j)
-        if (pos[j] >= 0) st[isl[j] ? pos[j] : nl + pos[j]] = src[start + t0 + j * FB_THREADS + threadIdx.x];
-    }
-    __syncthreads();
-    for (int k = 0; k < ncol; ++k) {
-      uint8_t* dst = k < nfeat ? dcodes + (long long)k * ld : (k == nfeat ? dlab : dwt);
-      write_run(dst + lb, s_stage + k * TILE, nl);
-      write_run(dst + rb, s_stage + k * TILE + nl, nr);
+      __syncthreads();  // the stage (and s_wtot, on the last group) is rewritten next
     }
     lb += nl;
     rb += nr;
-    __syncthreads();  // the stage is rewritten by the next tile
   }
 }
 
@@ -392,9 +442,7 @@ void forest_part_scatter(const uint8_t* codes, const uint8_t* lab, const uint8_t
                          const int* item_len, int n_items, const long long* left_base, const long long* right_base,
                          const int* feat, const int* thr, hipStream_t stream) {
   if (n_items <= 0) return;
-  const size_t lds = (size_t)(nfeat + 2) * TILE;
-  if (lds > 64 * 1024) throw std::runtime_error("forest_part_scatter: more than 62 features");
-  forest_part_scatter_kernel<<<n_items, FB_THREADS, lds, stream>>>(codes, lab, wt, dcodes, dlab, dwt, ld, nfeat,
+  forest_part_scatter_kernel<<<n_items, FB_THREADS, 0, stream>>>(codes, lab, wt, dcodes, dlab, dwt, ld, nfeat,
                                                                   item_node, item_start, item_len, left_base,
                                                                   right_base, feat, thr);
   AV_HIP_CHECK(hipGetLastError());

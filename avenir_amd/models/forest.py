@@ -161,7 +161,7 @@ class ForestBuilder:
         rows = torch.nonzero(keep.view(-1)).view(-1)               # flat (tree, row) ids, tree-major
         src_row = rows % n
         R = int(rows.numel())
-        ldb = max(16, R)
+        ldb = max(16, (R + 15) // 16 * 16)        # 8-byte lane loads need a multiple of 8 rows
         cb = torch.empty((F, ldb), dtype=torch.uint8, device=dev)
         cb[:, :R] = codes[:, :n].index_select(1, src_row)
         lb = torch.empty(ldb, dtype=torch.uint8, device=dev)
@@ -212,13 +212,17 @@ class ForestBuilder:
             comm.all_reduce(hist)
         level = 0
         n_hist_rows = int(fr.count.sum())
+        from ..parallel.comm import maybe_inject_fault
+        from ..utils.tracing import TRACER
         while fr.node.size:
             tl = time.perf_counter()
+            maybe_inject_fault(level, comm.rank)            # env-driven fault injection per level
             A = fr.node.size
             key_d = torch.as_tensor(fr.key, device=dev)
             fmask = self._mask(A, F, key_d, dev)
             rnd = (_h32(key_d ^ 0x2545F491).double() / 4294967296.0).float()
-            feat, thr, score, imp, left = FO.forest_split(hist, fmask, bins_d, offs_d, bins, algo, topk, rnd)
+            with TRACER.range("forest.split", 0.0, float(A) * sum(bins) * C * 8, dev):
+                feat, thr, score, imp, left = FO.forest_split(hist, fmask, bins_d, offs_d, bins, algo, topk, rnd)
             tot = hist[:, :, TB - 1]
             pop = tot.sum(1).double()
             depth_d = torch.as_tensor(fr.depth, device=dev)
@@ -287,8 +291,9 @@ class ForestBuilder:
                 rbase = fr.start[owner] + nleft[owner] + (rsum[:-1] - rsum[first[owner]])
                 fs_h = np.where(need, f_h, -1).astype(np.int32)
                 feat_sc = torch.from_numpy(fs_h).to(dev) if need.sum() < sp.size else feat_eff
-                FO.forest_part_scatter(cb, lb, wb, cb2, lb2, wb2, inode, istart, ilen, lbase, rbase, il_h, feat_sc,
-                                       thr)
+                with TRACER.range("forest.partition", 2.0 * int(fr.count[need].sum()) * (F + 2), 0.0, dev):
+                    FO.forest_part_scatter(cb, lb, wb, cb2, lb2, wb2, inode, istart, ilen, lbase, rbase, il_h,
+                                           feat_sc, thr)
                 cb, cb2, lb, lb2, wb, wb2 = cb2, cb, lb2, lb, wb2, wb
             parent_slot = np.repeat(sp, 2)
             sib = np.arange(ch_node.size) ^ 1
@@ -306,7 +311,8 @@ class ForestBuilder:
             bidx = order[:nb]
             if nb:
                 inode2, istart2, ilen2, _ = self._chunks(np.arange(nb), ch_start[bidx], ch_count[bidx], chunk)
-                FO.forest_hist(cb, lb, wb, inode2, istart2, ilen2, bins_d, offs_d, bins, TB, C, hist_new)
+                with TRACER.range("forest.hist", float(ch_count[bidx].sum()) * (F + 2), 0.0, dev):
+                    FO.forest_hist(cb, lb, wb, inode2, istart2, ilen2, bins_d, offs_d, bins, TB, C, hist_new)
                 n_hist_rows += int(ch_count[bidx].sum())
             if comm.is_distributed and newA:
                 comm.all_reduce(hist_new)

@@ -951,10 +951,12 @@ class GradientBoostedTrees:
     """Histogram GBT: per stage one regression tree per class on (g, h) with Newton leaves.
     Every level = one ``node_grad_hist`` pass (exact fixed-point sums) + one ``tree_assign`` pass."""
 
-    def __init__(self, schema: FeatureSchema, params: GBTParams | None = None, comm: Comm | None = None):
+    def __init__(self, schema: FeatureSchema, params: GBTParams | None = None, comm: Comm | None = None,
+                 recovery=None):
         self.schema = schema
         self.p = params or GBTParams()
         self.comm = comm
+        self.recovery = recovery          # per-round checkpoint / resume (utils/resilience)
         self.space: list[FeatureSplits] | None = None
         self.stages: list[list[DecisionTree]] = []
         self.init: torch.Tensor | None = None
@@ -1093,31 +1095,52 @@ class GradientBoostedTrees:
         Y = torch.nn.functional.one_hot(y, C).float() if K > 1 else y.float().view(n, 1)
         gen = torch.Generator(device=dev)
         gen.manual_seed(p.seed + 17 * comm.rank)
-        for _ in range(p.n_estimators):
-            if K == 1:
-                pr = torch.sigmoid(F)
-            else:
-                pr = torch.softmax(F, 1)
-            grad = pr - Y
-            hess = (pr * (1 - pr)).clamp_min(1e-6)
-            if p.subsample < 1.0:
-                m = (torch.rand(n, generator=gen, device=dev) < p.subsample).float().view(n, 1)
-                grad, hess = grad * m, hess * m
-            stage = []
-            for k in range(K):
-                g = torch.zeros(codes.shape[1], device=dev)
-                h = torch.zeros(codes.shape[1], device=dev)
-                g[:n], h[:n] = grad[:, k], hess[:, k]
-                tr = self._tree(codes, n, g, h, bins, dev)
-                flat = flatten_forest([tr], dev, value_fn=lambda nd: nd.class_pr)
-                F[:, k] += p.learning_rate * T.tree_predict(codes, n, flat, mode=0)[:, 0]
-                stage.append(tr)
-            self.stages.append(stage)
-            if K == 1:
-                loss = torch.nn.functional.binary_cross_entropy_with_logits(F[:, 0], Y[:, 0])
-            else:
-                loss = torch.nn.functional.cross_entropy(F, y)
-            self.train_loss.append(float(loss))
+        # one boosting round = one resumable iteration: the raw scores F (this rank's rows) and the
+        # subsample RNG state go to a per-rank checkpoint, the trees (identical on every rank) ride
+        # along as JSON metadata (utils/resilience.IterationLoop)
+        from ..utils.resilience import IterationLoop
+        lp = IterationLoop("gbt", self.recovery, comm, sharded=True, device=dev)
+        r0, st, meta = lp.restore(dev)
+        if st is not None:
+            F = st["F"].to(dev)
+            gen.set_state(st["rng"].cpu())
+            self.stages = [[DecisionTree.from_state(x, self.schema) for x in stage] for stage in meta["stages"]]
+            for stage in self.stages:
+                for tr in stage:
+                    tr.space = self.space
+            self.train_loss = list(meta["train_loss"])
+        nbytes = float(codes.numel()) * max(1, p.max_depth)
+        for rnd in range(r0, p.n_estimators):
+            with lp.step(rnd, nbytes=nbytes):
+                if K == 1:
+                    pr = torch.sigmoid(F)
+                else:
+                    pr = torch.softmax(F, 1)
+                grad = pr - Y
+                hess = (pr * (1 - pr)).clamp_min(1e-6)
+                if p.subsample < 1.0:
+                    m = (torch.rand(n, generator=gen, device=dev) < p.subsample).float().view(n, 1)
+                    grad, hess = grad * m, hess * m
+                stage = []
+                for k in range(K):
+                    g = torch.zeros(codes.shape[1], device=dev)
+                    h = torch.zeros(codes.shape[1], device=dev)
+                    g[:n], h[:n] = grad[:, k], hess[:, k]
+                    tr = self._tree(codes, n, g, h, bins, dev)
+                    flat = flatten_forest([tr], dev, value_fn=lambda nd: nd.class_pr)
+                    F[:, k] += p.learning_rate * T.tree_predict(codes, n, flat, mode=0)[:, 0]
+                    stage.append(tr)
+                self.stages.append(stage)
+                if K == 1:
+                    loss = torch.nn.functional.binary_cross_entropy_with_logits(F[:, 0], Y[:, 0])
+                else:
+                    loss = torch.nn.functional.cross_entropy(F, y)
+                self.train_loss.append(float(loss))
+            if lp.enabled:
+                lp.commit(rnd, {"F": F, "rng": gen.get_state()},
+                          {"stages": [[tr.state() for tr in stage] for stage in self.stages],
+                           "train_loss": self.train_loss})
+        lp.close()
         self._flat = None
         return self
 

@@ -67,8 +67,22 @@ def _annealing(rank, world, ckdir):
     return r.costs.tolist(), r.solutions.tolist()
 
 
-@pytest.mark.parametrize("fn", [_kmeans, _logistic, _apriori, _genetic, _annealing],
-                         ids=["kmeans", "logistic", "apriori", "genetic", "annealing"])
+def _gbt(rank, world, ckdir):
+    from avenir_amd.models.supervised import array_schema, array_table
+    from avenir_amd.models.tree import GBTParams, GradientBoostedTrees
+    from avenir_amd.utils.resilience import RecoveryConfig
+    g = torch.Generator().manual_seed(11 + rank)
+    X = torch.randn(600, 4, generator=g)
+    y = ((X[:, 0] - X[:, 1] + 0.5 * torch.randn(600, generator=g)) > 0).long()
+    schema = array_schema(4, [0, 1])
+    t = array_table(X, y, schema)
+    m = GradientBoostedTrees(schema, GBTParams(n_estimators=8, max_depth=3, subsample=0.7, max_bins=16),
+                             recovery=RecoveryConfig(ckdir)).fit(t)
+    return m.train_loss, m.decision_function(t).tolist()
+
+
+@pytest.mark.parametrize("fn", [_kmeans, _logistic, _apriori, _genetic, _annealing, _gbt],
+                         ids=["kmeans", "logistic", "apriori", "genetic", "annealing", "gbt"])
 def test_fault_then_fresh_resume_equals_uninterrupted(tmp_path, fn):
     clean, errs, codes = run_world_outcome(fn, 2, str(tmp_path / "clean"))
     assert not errs and codes == [0, 0], errs
