@@ -396,7 +396,7 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   __shared__ unsigned hist[256];
   __shared__ float redf[17];
   __shared__ unsigned redu[17];
-  __shared__ unsigned s_prefix, s_mask, s_krem, s_gt, s_eq;
+  __shared__ unsigned s_prefix, s_mask, s_krem, s_gt;
   __shared__ int pick[2][64];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float* ab = alpha + (long long)b * ldag;
@@ -450,22 +450,43 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
           cum += hist[dg];
         }
         s_gt = 0;
-        s_eq = 0;
+
       }
       __syncthreads();
     }
     const unsigned T = s_prefix, krem = s_krem, ngt = k - krem;  // keys > T: exactly ngt of them
-    for (int n = tid; n < N; n += SEL_T) {
-      const float v = ws_violation(which, yb[n], ab[n], gb[n], C);
-      if (v > -INFINITY) {
-        const unsigned key = order_key(v);
-        if (key > T) {
-          pick[which][atomicAdd(&s_gt, 1u)] = n;
-        } else if (key == T) {
-          const unsigned s2 = atomicAdd(&s_eq, 1u);
-          if (s2 < krem) pick[which][ngt + s2] = n;
+    // keys > T are all taken (their slots are re-sorted by index below); among the keys == T the
+    // krem SMALLEST indices are taken: the rows are walked in index order, SEL_T at a time, and a
+    // block prefix count of the ties (wave ballots + per-wave totals) ranks each tie — the working
+    // set no longer depends on the order of LDS atomics (first outer step: every violator ties).
+    unsigned eq_base = 0;  // ties seen in earlier SEL_T blocks (block-uniform)
+    const int lane = tid & 63, wv = tid >> 6;
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int n0 = 0; n0 < N; n0 += SEL_T) {
+      const int n = n0 + tid;
+      bool eq = false;
+      if (n < N) {
+        const float v = ws_violation(which, yb[n], ab[n], gb[n], C);
+        if (v > -INFINITY) {
+          const unsigned key = order_key(v);
+          if (key > T) pick[which][atomicAdd(&s_gt, 1u)] = n;
+          eq = key == T;
         }
       }
+      const unsigned long long bal = __ballot(eq);
+      if (lane == 0) redu[wv] = (unsigned)__popcll(bal);
+      __syncthreads();
+      unsigned before = eq_base, tot = 0;
+      for (int w = 0; w < SEL_T / 64; ++w) {
+        if (w < wv) before += redu[w];
+        tot += redu[w];
+      }
+      if (eq) {
+        const unsigned r = before + (unsigned)__popcll(bal & below);
+        if (r < krem) pick[which][ngt + r] = n;
+      }
+      eq_base += tot;
+      __syncthreads();  // redu is rewritten by the next block of rows
     }
     __syncthreads();
     if (which == 0 && tid < (int)k) atomicOr(&in_up[pick[0][tid] >> 5], 1u << (pick[0][tid] & 31));

@@ -263,10 +263,18 @@ def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max
               solver: str = "auto"):
     """Solve B SVM duals: K [B, N, N], y [B, N] in {-1, 0 (padding), +1}.  Returns (alpha, rho, iters).
     ``solver``: "full" (one persistent workgroup runs plain SMO over all N), "ws" (working-set
-    decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N)."""
+    decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N).
+
+    ``max_iter`` bounds the two-variable SMO steps on every path: the full solver counts them
+    directly; the working-set solver runs at most ``max(1, max_iter // inner_iter)`` outer steps of
+    at most ``inner_iter`` sub-problem steps each.  ``iters`` is the number of two-variable steps
+    taken per problem in both cases (for the working-set path: the inner steps summed over the
+    outer steps)."""
     B, N = y.shape
     if solver == "ws" or (solver == "auto" and K.device.type == "cuda" and N > WS_MIN_N):
-        alpha, G, outer, inner = smo_decomposition(K, y, C, eps, inner_iter=2048)
+        inner_iter = min(2048, max(1, max_iter))
+        alpha, G, outer, inner = smo_decomposition(K, y, C, eps, max_outer=max(1, max_iter // inner_iter),
+                                                   inner_iter=inner_iter)
         return alpha, _rho(alpha, G, y.float(), C), inner.int()
     if K.device.type == "cuda":
         Kc = K.float().contiguous()
