@@ -1482,6 +1482,17 @@ PYBIND11_MODULE(_C, m) {
       .def("lines", &avh::CsvFile::lines)
       .def("parse", &csv_parse, py::arg("specs"), py::arg("row_begin") = 0, py::arg("row_end") = -1);
   m.def("format_rows", &format_rows);
+  m.def("write_coded_csv", [](const std::string& path, const at::Tensor& codes, int64_t n,
+                              std::vector<std::vector<std::string>> vocab, std::string id_prefix, std::string delim,
+                              int nthreads) {
+    TORCH_CHECK(!codes.is_cuda() && codes.scalar_type() == at::kByte && codes.dim() == 2,
+                "codes must be a CPU uint8 [ncol, ld] tensor");
+    TORCH_CHECK((int64_t)vocab.size() == codes.size(0) && n <= codes.size(1), "one vocabulary per column");
+    auto c = codes.contiguous();
+    py::gil_scoped_release rel;
+    return avh::write_coded_csv(path, c.data_ptr<uint8_t>(), (int)c.size(0), c.size(1), n, vocab, id_prefix,
+                                delim.empty() ? ',' : delim[0], nthreads);
+  });
   py::class_<avh::SpscRing>(m, "SpscRing")
       .def(py::init<size_t, int>())
       .def("push", [](avh::SpscRing& r, std::vector<int64_t> rec) {

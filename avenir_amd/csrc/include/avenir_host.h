@@ -94,4 +94,8 @@ void write_container(const std::string& path, const std::string& header_json,
 std::string read_container_header(const std::string& path, uint64_t* data_offset);
 uint32_t crc32(const void* data, size_t n, uint32_t seed = 0);
 
+int64_t write_coded_csv(const std::string& path, const uint8_t* codes, int ncol, int64_t ld, int64_t n,
+                        const std::vector<std::vector<std::string>>& vocab, const std::string& id_prefix,
+                        char delim, int nthreads);
+
 }  // namespace avh
