@@ -1236,6 +1236,40 @@ void forest_part_scatter(const at::Tensor& codes, const at::Tensor& lab, const a
                            i64p(d_lb), i64p(d_rb), feat.data_ptr<int>(), thr.data_ptr<int>(), cur_stream(codes));
 }
 
+// Bootstrap row buffers of ``keys.numel()`` trees over the first n rows of codes [F, ld] / lab:
+// returns (codes [F, ldb], labels [ldb], weights [ldb], rows per tree (host int64)), tree-major.
+std::vector<at::Tensor> forest_bootstrap(const at::Tensor& codes, const at::Tensor& lab, int64_t n,
+                                         const at::Tensor& keys, int64_t row_off, int64_t mode, int64_t rate32) {
+  CHECK_DEV(codes); CHECK_DTYPE(codes, at::kByte);
+  CHECK_DEV(lab); CHECK_DTYPE(lab, at::kByte);
+  CHECK_DEV(keys); CHECK_DTYPE(keys, at::kLong);
+  TORCH_CHECK(codes.dim() == 2 && codes.is_contiguous() && lab.is_contiguous() && keys.is_contiguous(),
+              "contiguous codes [F, ld], labels, keys");
+  const int64_t ld = codes.size(1), F = codes.size(0), T = keys.numel();
+  TORCH_CHECK(ld % 8 == 0 && 0 <= n && n <= ld && lab.numel() >= ld, "row buffers padded to a multiple of 8 rows");
+  TORCH_CHECK(0 <= mode && mode <= 2 && 0 <= rate32 && rate32 <= 0xFFFFFFFFLL && row_off >= 0, "bad sampling mode");
+  TORCH_CHECK(T > 0 && T < 65536, "1..65535 trees");
+  const int64_t tiles = std::max<int64_t>(1, (n + 2047) / 2048);
+  auto iopt = codes.options().dtype(at::kInt);
+  auto tile_cnt = at::zeros({T, tiles}, iopt);
+  DevGuard g(codes.device());
+  auto keysu = reinterpret_cast<const unsigned long long*>(keys.data_ptr<int64_t>());
+  avk::forest_boot_count(keysu, (int)T, n, row_off, (int)mode, (unsigned)rate32, tile_cnt.data_ptr<int>(),
+                         cur_stream(codes));
+  auto flat = tile_cnt.view({-1}).to(at::kLong);
+  auto incl = flat.cumsum(0);
+  auto tile_off = (incl - flat).contiguous();
+  auto per_tree = tile_cnt.sum(1, false, at::kLong).cpu();
+  const int64_t R = per_tree.sum().item<int64_t>();
+  const int64_t ldb = std::max<int64_t>(16, (R + 15) / 16 * 16);
+  auto bopt = codes.options();
+  auto cb = at::empty({F, ldb}, bopt), lb = at::empty({ldb}, bopt), wb = at::zeros({ldb}, bopt);
+  avk::forest_boot_scatter(codes.data_ptr<uint8_t>(), ld, (int)F, lab.data_ptr<uint8_t>(), keysu, (int)T, n, row_off,
+                           (int)mode, (unsigned)rate32, i64p(tile_off), cb.data_ptr<uint8_t>(), lb.data_ptr<uint8_t>(),
+                           wb.data_ptr<uint8_t>(), ldb, cur_stream(codes));
+  return {cb, lb, wb, per_tree};
+}
+
 // K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
 // are joined with every row whose (k-1)-prefix equals their (k-1)-suffix -> int32 [M, k+1].
 at::Tensor gsp_join(const at::Tensor& X, int64_t lo, int64_t hi) {
@@ -1467,6 +1501,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("forest_split", &forest_split);
   m.def("forest_part_count", &forest_part_count);
   m.def("forest_part_scatter", &forest_part_scatter);
+  m.def("forest_bootstrap", &forest_bootstrap);
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);

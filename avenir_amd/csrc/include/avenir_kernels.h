@@ -157,6 +157,12 @@ void forest_split(const long long* hist, const uint8_t* fmask, const int* bins, 
 void forest_part_count(const uint8_t* codes, long long ld, const int* item_node, const long long* item_start,
                        const int* item_len, int n_items, const int* feat, const int* thr, int* item_left,
                        hipStream_t stream);
+void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
+                       unsigned rate32, int* tile_cnt, hipStream_t stream);
+void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,
+                         const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
+                         unsigned rate32, const long long* tile_off, uint8_t* dcodes, uint8_t* dlab, uint8_t* dwt,
+                         long long ldb, hipStream_t stream);
 void forest_part_scatter(const uint8_t* codes, const uint8_t* lab, const uint8_t* wt, uint8_t* dcodes, uint8_t* dlab,
                          uint8_t* dwt, long long ld, int nfeat, const int* item_node, const long long* item_start,
                          const int* item_len, int n_items, const long long* left_base, const long long* right_base,

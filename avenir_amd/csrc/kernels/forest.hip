@@ -367,6 +367,131 @@ __global__ __launch_bounds__(FB_THREADS) void forest_part_scatter_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Bootstrap row buffers.  The multiplicity of (tree, global row) is a pure function of the tree key
+// and the row index (splitmix64 -> 32 uniform bits -> Poisson(1) by inverse CDF, Bernoulli(rate) or
+// 1), so the sample is the same on any device and any number of ranks (rows are keyed by their
+// GLOBAL index).  Two passes over grid (row tiles, trees): count the kept rows per tile, then, after
+// a scan of the tile counts, write every kept row's codes / label / weight compacted into the
+// tree-major buffers through the same LDS stage + aligned run writes as the partition.
+// ------------------------------------------------------------------------------------------------
+__constant__ unsigned kPoisson1Cdf[12] = {1580030168u, 3160060337u, 3950075421u, 4213413783u,
+                                          4279248373u, 4292415291u, 4294609777u, 4294923276u,
+                                          4294962463u, 4294966817u, 4294967252u, 4294967292u};
+
+__device__ __forceinline__ unsigned boot_weight(unsigned long long key, unsigned long long row, int mode,
+                                                unsigned rate32) {
+  if (mode == 0) return 1u;
+  unsigned long long z = key + row * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  const unsigned u = (unsigned)(z >> 32);
+  if (mode == 2) return u < rate32 ? 1u : 0u;
+  unsigned k = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) k += u >= kPoisson1Cdf[i] ? 1u : 0u;
+  return k;
+}
+
+// weights of this lane's 8 rows packed one byte each (rows >= n weigh 0)
+__device__ __forceinline__ unsigned long long boot_weights8(unsigned long long key, long long row_off, long long r0,
+                                                            long long n, int mode, unsigned rate32) {
+  unsigned long long w = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (r0 + j < n) w |= (unsigned long long)boot_weight(key, (unsigned long long)(row_off + r0 + j), mode, rate32)
+                         << (8 * j);
+  return w;
+}
+
+__device__ __forceinline__ unsigned nonzero_bytes(unsigned long long w) {
+  unsigned b = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) b |= (unsigned)((w >> (8 * j) & 0xFF) != 0) << j;
+  return b;
+}
+
+__device__ __forceinline__ int block_excl_scan(int mine, int* s_wtot, int& tot) {
+  const int lane = av::lane_id(), wave = av::wave_id();
+  int inc = mine;
+#pragma unroll
+  for (int o = 1; o < AV_WAVE; o <<= 1) {
+    const int y = __shfl_up(inc, o, AV_WAVE);
+    if (lane >= o) inc += y;
+  }
+  if (lane == AV_WAVE - 1) s_wtot[wave] = inc;
+  __syncthreads();
+  int before = 0;
+  tot = 0;
+  for (int w = 0; w < FB_THREADS / AV_WAVE; ++w) {
+    if (w < wave) before += s_wtot[w];
+    tot += s_wtot[w];
+  }
+  return before + inc - mine;
+}
+
+__global__ __launch_bounds__(FB_THREADS) void forest_boot_count_kernel(const unsigned long long* __restrict__ keys,
+                                                                       long long n, long long row_off, int mode,
+                                                                       unsigned rate32, int* __restrict__ tile_cnt) {
+  __shared__ int s_wtot[FB_THREADS / AV_WAVE];
+  const int tree = blockIdx.y;
+  const long long r0 = (long long)blockIdx.x * RTILE + RPT * threadIdx.x;
+  const unsigned long long w = boot_weights8(keys[tree], row_off, r0, n, mode, rate32);
+  int tot;
+  block_excl_scan(__popc(nonzero_bytes(w)), s_wtot, tot);
+  if (threadIdx.x == 0) tile_cnt[(long long)tree * gridDim.x + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(FB_THREADS) void forest_boot_scatter_kernel(
+    const uint8_t* __restrict__ codes, long long ld, int nfeat, const uint8_t* __restrict__ lab,
+    const unsigned long long* __restrict__ keys, long long n, long long row_off, int mode, unsigned rate32,
+    const long long* __restrict__ tile_off, uint8_t* __restrict__ dcodes, uint8_t* __restrict__ dlab,
+    uint8_t* __restrict__ dwt, long long ldb) {
+  __shared__ uint8_t s_stage[SG][RTILE];
+  __shared__ int s_wtot[FB_THREADS / AV_WAVE];
+  const int tree = blockIdx.y;
+  const long long r0 = (long long)blockIdx.x * RTILE + RPT * threadIdx.x;
+  const unsigned long long w = boot_weights8(keys[tree], row_off, r0, n, mode, rate32);
+  const unsigned keep = nonzero_bytes(w);
+  int tot;
+  int p = block_excl_scan(__popc(keep), s_wtot, tot);
+  if (tot == 0) return;  // uniform over the block
+  short pos[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) pos[j] = (keep >> j & 1) ? (short)(p++) : (short)-1;
+  const long long out = tile_off[(long long)tree * gridDim.x + blockIdx.x];
+  const bool any = r0 < n;
+  const int ncol = nfeat + 2;
+  for (int g0 = 0; g0 < ncol; g0 += SG) {
+    const int ng = min(SG, ncol - g0);
+    for (int g = 0; g < ng; ++g) {
+      const int k = g0 + g;
+      if (!any || !keep) continue;
+      unsigned long long v;
+      if (k < nfeat) {
+        const uint2 x = *reinterpret_cast<const uint2*>(codes + (long long)k * ld + r0);
+        v = (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+      } else if (k == nfeat) {
+        const uint2 x = *reinterpret_cast<const uint2*>(lab + r0);
+        v = (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+      } else {
+        v = w;
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j)
+        if (pos[j] >= 0) s_stage[g][pos[j]] = (uint8_t)(v >> (8 * j));
+    }
+    __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+      const int k = g0 + g;
+      uint8_t* dst = k < nfeat ? dcodes + (long long)k * ldb : (k == nfeat ? dlab : dwt);
+      write_run(dst + out, s_stage[g], tot);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Fused fine-bin encoding of all numeric columns: out[f][r] = #{edges of f < x} (bin b covers
 // (P[b-1], P[b]]), 255 for NaN.  One launch for every feature instead of one torch.bucketize
 // (int64 intermediates) per feature.  grid = (row blocks, F); the feature's edges sit in LDS.
@@ -445,6 +570,27 @@ void forest_part_scatter(const uint8_t* codes, const uint8_t* lab, const uint8_t
   forest_part_scatter_kernel<<<n_items, FB_THREADS, 0, stream>>>(codes, lab, wt, dcodes, dlab, dwt, ld, nfeat,
                                                                   item_node, item_start, item_len, left_base,
                                                                   right_base, feat, thr);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+
+void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
+                       unsigned rate32, int* tile_cnt, hipStream_t stream) {
+  if (n <= 0 || ntrees <= 0) return;
+  const long long tiles = (n + RTILE - 1) / RTILE;
+  forest_boot_count_kernel<<<dim3((unsigned)tiles, ntrees), FB_THREADS, 0, stream>>>(keys, n, row_off, mode, rate32,
+                                                                                    tile_cnt);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,
+                         const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
+                         unsigned rate32, const long long* tile_off, uint8_t* dcodes, uint8_t* dlab, uint8_t* dwt,
+                         long long ldb, hipStream_t stream) {
+  if (n <= 0 || ntrees <= 0) return;
+  const long long tiles = (n + RTILE - 1) / RTILE;
+  forest_boot_scatter_kernel<<<dim3((unsigned)tiles, ntrees), FB_THREADS, 0, stream>>>(
+      codes, ld, nfeat, lab, keys, n, row_off, mode, rate32, tile_off, dcodes, dlab, dwt, ldb);
   AV_HIP_CHECK(hipGetLastError());
 }
 

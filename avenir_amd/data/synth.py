@@ -97,6 +97,21 @@ def churn_device(n: int, seed: int = 0, device="cuda", ld: int | None = None):
     return codes, labels
 
 
+def write_churn_native(path: str | Path, n: int, seed: int = 0, nthreads: int = 8) -> int:
+    """Write ``n`` churn records as CSV through the native multi-threaded writer
+    (``avh::write_coded_csv``): the ``churn_device`` distributions sampled on the host, ids
+    ``C<row>``.  Used for the ingest-inclusive benchmark (10^8-row files in seconds).
+    Returns the bytes written."""
+    from .. import _native
+    C = _native.host()
+    if C is None or not hasattr(C, "write_coded_csv"):
+        raise RuntimeError("write_churn_native needs the native host module (avenir_amd._C)")
+    codes, labels = churn_device(n, seed=seed, device="cpu")
+    cols = torch.cat([codes, labels[None]], 0).contiguous()
+    vocab = [list(f["cardinality"]) for f in CHURN_SCHEMA["fields"][1:7]]
+    return int(C.write_coded_csv(str(path), cols, n, vocab, "C", ",", nthreads))
+
+
 # ----------------------------------------------------------------------------------------------
 CALL_HANGUP_SCHEMA = {
     "fields": [

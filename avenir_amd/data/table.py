@@ -221,6 +221,37 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < rem else 0)
 
 
+class LazyColumn(Sequence):
+    """A string column of the native CSV file (e.g. the record ids), materialised as Python
+    strings on first access: training jobs over 10^8 records never touch the ids, and building
+    them eagerly cost more than parsing the file."""
+
+    def __init__(self, csv, ordinal: int, r0: int, r1: int):
+        self._csv, self._ord, self._r0, self._r1 = csv, ordinal, r0, r1
+        self._vals: list[str] | None = None
+
+    def _get(self) -> list[str]:
+        if self._vals is None:
+            self._vals = self._csv.column_strings(self._ord)[self._r0:self._r1]
+            self._csv = None
+        return self._vals
+
+    def __len__(self) -> int:
+        return self._r1 - self._r0
+
+    def __bool__(self) -> bool:
+        return self._r1 > self._r0
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __eq__(self, other):
+        return list(self._get()) == list(other)
+
+
 def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
              world: int = 1, device: str | torch.device = "cpu", keep_lines: bool = False,
              skip_header: bool = False, nthreads: int = 8, feature_ordinals: Sequence[int] | None = None,
@@ -281,12 +312,10 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         ids = None
         idf = schema.id_field
         lines = None
-        if keep_lines or idf is not None:
-            lines_all = csv.lines(r0, r1)
-            if idf is not None:
-                ids = csv.column_strings(idf.ordinal)[r0:r1]
-            if keep_lines:
-                lines = lines_all
+        if idf is not None:
+            ids = LazyColumn(csv, idf.ordinal, r0, r1)
+        if keep_lines:
+            lines = csv.lines(r0, r1)
     else:  # pure-Python path: regex delimiters, or no native module
         with open(path) as fh:
             all_lines = [ln.rstrip("\r\n") for ln in fh if ln.strip()]

@@ -81,25 +81,29 @@ class ForestBuilder:
         self.stats: dict = {}
 
     # ------------------------------------------------------------------------------------------
-    def _weights(self, n: int, ld: int, dev, tree_ids: list[int]) -> torch.Tensor:
-        """uint8 [T, n] bootstrap multiplicities (Poisson(1) = with replacement), Bernoulli
-        (without replacement, rate %), or ones."""
-        comm = self.comm or get_comm()
+    def _boot_keys(self, tree_ids: list[int]) -> np.ndarray:
+        """One 64-bit bootstrap key per tree from (seed, tree id): the sample of a tree depends on
+        nothing else (not the rank, the device or the world size — rows are keyed globally)."""
         p = self.p
-        Tn = len(tree_ids)
-        if p.sub_sampling == "none":
-            return torch.ones((Tn, n), dtype=torch.uint8, device=dev)
-        out = torch.empty((Tn, n), dtype=torch.uint8, device=dev)
-        for j, t in enumerate(tree_ids):
-            g = torch.Generator(device=dev)
-            g.manual_seed((p.seed * 7919 + t) * 1000003 + comm.rank)
-            if p.sub_sampling == "withReplace":
-                out[j] = torch.poisson(torch.ones(n, device=dev), generator=g).clamp_max(255).to(torch.uint8)
-            elif p.sub_sampling == "withoutReplace":
-                out[j] = (torch.rand(n, generator=g, device=dev) * 100.0 < p.sampling_rate).to(torch.uint8)
-            else:
-                raise ValueError(f"unknown sub sampling strategy {p.sub_sampling}")
-        return out
+        k = (np.asarray(tree_ids, dtype=np.uint64) + np.uint64(1)) * np.uint64(0xD1B54A32D192ED03)
+        with np.errstate(over="ignore"):
+            k ^= np.uint64((p.seed * 1000003 + 17) & 0xFFFFFFFFFFFFFFFF)
+        return k.view(np.int64)
+
+    def _weights(self, n: int, row_off: int, tree_ids: list[int]) -> np.ndarray:
+        """uint8 [T, n] bootstrap multiplicities of this rank's rows (host; the builder draws them
+        on the device inside ``forest_bootstrap``): Poisson(1) = with replacement, Bernoulli
+        (without replacement, rate %), or ones."""
+        mode, rate32 = self._boot_mode()
+        rows = np.arange(row_off, row_off + n, dtype=np.int64)
+        return np.stack([FO.boot_weights(int(k), rows, mode, rate32) for k in self._boot_keys(tree_ids)])
+
+    def _boot_mode(self) -> tuple[int, int]:
+        p = self.p
+        if p.sub_sampling not in FO.BOOT_MODES:
+            raise ValueError(f"unknown sub sampling strategy {p.sub_sampling}")
+        rate32 = int(min(max(p.sampling_rate, 0.0), 100.0) / 100.0 * 4294967296.0)
+        return FO.BOOT_MODES[p.sub_sampling], min(rate32, 0xFFFFFFFF)
 
     def _chunks(self, node_idx: np.ndarray, start: np.ndarray, count: np.ndarray, chunk: int):
         """Split segments into <= chunk-row work items: (item node index, item start, item len)."""
@@ -155,20 +159,26 @@ class ForestBuilder:
         t0 = time.perf_counter()
 
         # ---- per-tree bootstrap row buffers (one gather) ----------------------------------
-        w = self._weights(n, t.ld, dev, tree_ids) if weights is None else weights.to(dev, torch.uint8)  # [T, n]
-        keep = w > 0
-        cnt_t = keep.sum(1)
-        rows = torch.nonzero(keep.view(-1)).view(-1)               # flat (tree, row) ids, tree-major
-        src_row = rows % n
-        R = int(rows.numel())
-        ldb = max(16, (R + 15) // 16 * 16)        # 8-byte lane loads need a multiple of 8 rows
-        cb = torch.empty((F, ldb), dtype=torch.uint8, device=dev)
-        cb[:, :R] = codes[:, :n].index_select(1, src_row)
-        lb = torch.empty(ldb, dtype=torch.uint8, device=dev)
-        lb[:R] = t.labels[:n].to(dev).index_select(0, src_row)
-        wb = torch.zeros(ldb, dtype=torch.uint8, device=dev)
-        wb[:R] = w.view(-1)[rows]
-        del rows, src_row, keep, w
+        if weights is None:        # fused on-device draw + compaction (one pass per tree tile)
+            mode, rate32 = self._boot_mode()
+            cb, lb, wb, cnt_t = FO.forest_bootstrap(codes.contiguous(), t.labels.to(dev).contiguous(), n,
+                                                    self._boot_keys(tree_ids), t.row_offset, mode, rate32)
+            R = int(cnt_t.sum())
+        else:
+            w = weights.to(dev, torch.uint8)                        # [T, n] explicit multiplicities
+            keep = w > 0
+            cnt_t = keep.sum(1)
+            rows = torch.nonzero(keep.view(-1)).view(-1)            # flat (tree, row) ids, tree-major
+            src_row = rows % n
+            R = int(rows.numel())
+            ldb = max(16, (R + 15) // 16 * 16)    # 8-byte lane loads need a multiple of 8 rows
+            cb = torch.empty((F, ldb), dtype=torch.uint8, device=dev)
+            cb[:, :R] = codes[:, :n].index_select(1, src_row)
+            lb = torch.empty(ldb, dtype=torch.uint8, device=dev)
+            lb[:R] = t.labels[:n].to(dev).index_select(0, src_row)
+            wb = torch.zeros(ldb, dtype=torch.uint8, device=dev)
+            wb[:R] = w.view(-1)[rows]
+            del rows, src_row, keep, w
         cb2, lb2, wb2 = torch.empty_like(cb), torch.empty_like(lb), torch.zeros_like(wb)
         cnt_h = cnt_t.cpu().numpy().astype(np.int64)
         starts_h = np.concatenate([[0], np.cumsum(cnt_h)[:-1]]).astype(np.int64)
@@ -345,38 +355,60 @@ class ForestBuilder:
         else:
             info_all = 1.0 - (pr_all * pr_all).sum(1)
         info_all = np.where(pops > 0, info_all, 0.0)
+        # host-side node assembly over plain lists (numpy scalar access per node dominated):
+        # predicate strings and segment maps are shared per (feature, threshold)
+        par_l = tbl["parent"][:n_nodes].tolist()
+        feat_l = tbl["feat"][:n_nodes].tolist()
+        thr_l = tbl["thr"][:n_nodes].tolist()
+        left_l = tbl["left"][:n_nodes].tolist()
+        right_l = tbl["right"][:n_nodes].tolist()
+        depth_l = tbl["depth"][:n_nodes].tolist()
+        pops_l = pops.astype(np.int64).tolist()
+        info_l = info_all.tolist()
+        pr_l = pr_all.tolist()
+        pred_cache: dict[tuple[int, int], tuple[str, str]] = {}
+        seg_cache: dict[tuple[int, int], list[int]] = {}
+
+        def preds_for(f: int, s: int) -> tuple[str, str]:
+            key = (f, s)
+            if key not in pred_cache:
+                fs = space[f]
+                o = fs.field.ordinal
+                if fs.kind == "num":
+                    pv = fs.pred_value(fs.points[s])
+                    pred_cache[key] = (f"{o} le {pv}", f"{o} gt {pv}")
+                else:
+                    card = fs.field.cardinality
+                    pred_cache[key] = (f"{o} in {':'.join(card[: s + 1])}", f"{o} in {':'.join(card[s + 1:])}")
+            return pred_cache[key]
+
+        order = np.argsort(tree_of[:n_nodes], kind="stable")
+        bounds = np.searchsorted(tree_of[:n_nodes][order], np.arange(Tn + 1))
         for ti in range(Tn):
-            gids = np.nonzero(tree_of == ti)[0]
-            local = {int(g): i for i, g in enumerate(gids)}
+            gids = order[bounds[ti]:bounds[ti + 1]].tolist()
+            local = {g: i for i, g in enumerate(gids)}
             nodes: list[T.Node] = []
             preds_of: dict[int, list[str]] = {}
             used_of: dict[int, frozenset] = {}
-            for g in gids.tolist():
-                par = int(tbl["parent"][g])
+            for g in gids:
+                par = par_l[g]
                 if par < 0:
                     preds, used = [], frozenset()
                 else:
-                    fs = space[int(tbl["feat"][par])]
-                    s = int(tbl["thr"][par])
-                    o = fs.field.ordinal
-                    if fs.kind == "num":
-                        pv = fs.pred_value(fs.points[s])
-                        pr = f"{o} le {pv}" if int(tbl["left"][par]) == g else f"{o} gt {pv}"
-                    else:
-                        card = fs.field.cardinality
-                        pr = (f"{o} in {':'.join(card[: s + 1])}" if int(tbl["left"][par]) == g
-                              else f"{o} in {':'.join(card[s + 1:])}")
-                    preds = preds_of[par] + [pr]
-                    used = used_of[par] | {int(tbl["feat"][par])}
+                    lp, rp = preds_for(feat_l[par], thr_l[par])
+                    preds = preds_of[par] + [lp if left_l[par] == g else rp]
+                    used = used_of[par] | {feat_l[par]}
                 preds_of[g], used_of[g] = preds, used
-                nd = T.Node(preds, int(pops[g]), float(info_all[g]), pr_all[g].tolist(), int(tbl["depth"][g]),
-                            stopped=int(tbl["feat"][g]) < 0, used_attrs=used)
-                f = int(tbl["feat"][g])
+                f = feat_l[g]
+                nd = T.Node(preds, pops_l[g], info_l[g], pr_l[g], depth_l[g], stopped=f < 0, used_attrs=used)
                 if f >= 0:
-                    thr = int(tbl["thr"][g])
+                    thr = thr_l[g]
                     nd.feature, nd.split = f, thr
-                    nd.segmap = [0 if b <= thr else 1 for b in range(space[f].n_bins)]
-                    nd.children = [local[int(tbl["left"][g])], local[int(tbl["right"][g])]]
+                    sm = seg_cache.get((f, thr))
+                    if sm is None:
+                        sm = seg_cache[(f, thr)] = [0 if b <= thr else 1 for b in range(space[f].n_bins)]
+                    nd.segmap = sm
+                    nd.children = [local[left_l[g]], local[right_l[g]]]
                 nodes.append(nd)
             trees.append(T.DecisionTree(nodes, space, cls))
         return trees

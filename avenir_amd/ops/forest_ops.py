@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
 from .. import _native
@@ -20,6 +21,53 @@ def _i32(x):
 
 def _i64(x):
     return torch.as_tensor(x, dtype=torch.int64)
+
+
+POISSON1_CDF = np.array([1580030168, 3160060337, 3950075421, 4213413783, 4279248373, 4292415291, 4294609777,
+                         4294923276, 4294962463, 4294966817, 4294967252, 4294967292], dtype=np.uint64)
+BOOT_MODES = {"none": 0, "withReplace": 1, "withoutReplace": 2}
+
+
+def boot_weights(key: int, rows: np.ndarray, mode: int, rate32: int) -> np.ndarray:
+    """Bootstrap multiplicity of each global row for one tree key (the kernel's ``boot_weight``):
+    splitmix64(key + row * golden) -> high 32 bits u -> Poisson(1) by inverse CDF (mode 1),
+    u < rate32 (mode 2) or 1 (mode 0).  uint8."""
+    if mode == 0:
+        return np.ones(rows.shape, np.uint8)
+    with np.errstate(over="ignore"):
+        z = np.uint64(key & 0xFFFFFFFFFFFFFFFF) + rows.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    u = z >> np.uint64(32)
+    if mode == 2:
+        return (u < np.uint64(rate32)).astype(np.uint8)
+    return (u[:, None] >= POISSON1_CDF[None, :]).sum(1).astype(np.uint8)
+
+
+def forest_bootstrap(codes, lab, n: int, keys, row_off: int, mode: int, rate32: int):
+    """Per-tree bootstrap row buffers: the kept rows (multiplicity > 0) of every tree, tree-major,
+    compacted into (codes [F, ldb], labels [ldb], weights [ldb]) plus the host int64 row count
+    per tree.  ``keys`` int64 [T] (one per tree); rows are keyed by ``row_off + r`` (global)."""
+    keys = torch.as_tensor(keys, dtype=torch.int64)
+    if codes.is_cuda:
+        cb, lb, wb, per = _native.C().forest_bootstrap(codes.contiguous(), lab.contiguous(), int(n),
+                                                       keys.to(codes.device), int(row_off), int(mode), int(rate32))
+        return cb, lb, wb, per
+    rows = np.arange(row_off, row_off + n, dtype=np.int64)
+    ws = [boot_weights(int(k), rows, mode, rate32) for k in keys.tolist()]
+    idx = [np.nonzero(w)[0] for w in ws]
+    R = int(sum(i.size for i in idx))
+    ldb = max(16, (R + 15) // 16 * 16)
+    F = codes.shape[0]
+    cb = torch.empty((F, ldb), dtype=torch.uint8)
+    lb = torch.empty(ldb, dtype=torch.uint8)
+    wb = torch.zeros(ldb, dtype=torch.uint8)
+    sel = torch.from_numpy(np.concatenate(idx) if idx else np.zeros(0, np.int64))
+    cb[:, :R] = codes[:, :n].index_select(1, sel)
+    lb[:R] = lab[:n].index_select(0, sel)
+    wb[:R] = torch.from_numpy(np.concatenate([w[i] for w, i in zip(ws, idx)]) if idx else np.zeros(0, np.uint8))
+    return cb, lb, wb, torch.tensor([i.size for i in idx], dtype=torch.int64)
 
 
 def forest_hist(codes, lab, wt, slot, start, length, bins_d, offs_d, bins, TB: int, C: int, hist) -> None:

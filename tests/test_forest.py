@@ -76,7 +76,9 @@ def _dp_worker(rank, world, rows, sj):
     open(p, "w").write("\n".join(rows) + "\n")
     from avenir_amd.parallel.comm import get_comm
     t = load_csv(p, schema, raw_numeric=True, rank=rank, world=world)
-    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=5, attr_selection="all", sub_sampling="none")
+    # bootstrap rows are keyed by their global index, so the bagged forest is world-size invariant
+    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=5, attr_selection="all",
+                       sub_sampling="withReplace", seed=3)
     # split points must be global: build the space from the full file on every rank
     full = load_csv(p, schema, raw_numeric=True)
     space = T.build_split_space(schema, full, binary=True, max_bins=prm.max_bins)
@@ -92,6 +94,33 @@ def test_data_parallel_bit_exact(tmp_path, world):
     got = run_world(_dp_worker, world, rows, synth.CALL_HANGUP_SCHEMA)
     for g in got:
         assert g == ref
+
+
+def test_bootstrap_weights_distribution():
+    rows = np.arange(10, 200010, dtype=np.int64)
+    w = FO.boot_weights(12345, rows, 1, 0)
+    assert abs(w.mean() - 1.0) < 0.01 and abs((w == 0).mean() - np.exp(-1)) < 0.005
+    assert abs((w == 2).mean() - np.exp(-1) / 2) < 0.005 and w.max() < 13
+    b = FO.boot_weights(777, rows, 2, int(0.3 * 2**32))
+    assert abs(b.mean() - 0.3) < 0.005 and set(np.unique(b)) <= {0, 1}
+    assert (FO.boot_weights(1, rows, 0, 0) == 1).all()
+    # keyed by global row: a shard's weights are the matching slice of the whole
+    assert np.array_equal(FO.boot_weights(12345, rows[500:900], 1, 0), w[500:900])
+
+
+def test_bootstrap_buffers_cpu():
+    codes, lab, _, _ = _rand_buffers(F=3, R=1000)
+    keys = [11, -5, 2**62 + 3]
+    cb, lb, wb, per = FO.forest_bootstrap(codes, lab, 997, keys, 40, 1, 0)
+    off = 0
+    for k, c in zip(keys, per.tolist()):
+        w = FO.boot_weights(k, np.arange(40, 1037), 1, 0)
+        idx = np.nonzero(w)[0]
+        assert c == idx.size
+        assert torch.equal(cb[:, off:off + c], codes[:, torch.from_numpy(idx)])
+        assert torch.equal(lb[off:off + c], lab[torch.from_numpy(idx)])
+        assert np.array_equal(wb[off:off + c].numpy(), w[idx])
+        off += c
 
 
 # ---------------------------------------------------------------------------------------------
@@ -170,6 +199,34 @@ def test_forest_gpu_equals_cpu(cuda, tmp_path, alg, sel):
             assert _paths(a) == _paths(b)
     else:   # random picks use the device RNG: same structure statistics only
         assert all(len(b.nodes) > 10 for b in gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,mode", [(5000, 1), (4093, 1), (20000, 2), (3001, 0), (7, 1)])
+def test_bootstrap_kernel_matches_oracle(cuda, n, mode):
+    codes, lab, _, _ = _rand_buffers(F=5, R=((n + 15) // 16) * 16, seed=n)
+    keys = [3, 99, -17, 2**40]
+    rate = int(0.37 * 2**32)
+    c = FO.forest_bootstrap(codes, lab, n, keys, 1234, mode, rate)
+    g = FO.forest_bootstrap(codes.to(cuda), lab.to(cuda), n, keys, 1234, mode, rate)
+    assert torch.equal(c[3], g[3].cpu())
+    R = int(c[3].sum())
+    assert torch.equal(c[0][:, :R], g[0][:, :R].cpu())
+    assert torch.equal(c[1][:R], g[1][:R].cpu())
+    assert torch.equal(c[2][:R], g[2][:R].cpu())
+
+
+@pytest.mark.gpu
+def test_bagged_forest_gpu_equals_cpu(cuda, tmp_path):
+    """Default (device-drawn) bootstrap: the GPU forest is the CPU forest."""
+    schema, t = _table(tmp_path, 30000, 4)
+    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=6, attr_selection="all",
+                       sub_sampling="withReplace", seed=8)
+    space = T.build_split_space(schema, t, binary=True, max_bins=prm.max_bins)
+    cpu = ForestBuilder(schema, 4, prm).fit(t, space=space)
+    gpu = ForestBuilder(schema, 4, prm).fit(t.to(cuda), space=space)
+    for a, b in zip(cpu, gpu):
+        assert _paths(a) == _paths(b)
 
 
 @pytest.mark.gpu
