@@ -417,13 +417,14 @@ void tree_predict(const at::Tensor& codes, int64_t n, const at::Tensor& feat, co
 // distance / kNN / clustering (K9/K11)
 // ---------------------------------------------------------------------------------------------
 py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t q_base, int64_t r_base,
-                   bool exclude_self, int64_t splits) {
+                   bool exclude_self, int64_t splits, int64_t metric, double p) {
   CHECK_DEV(Q);
   CHECK_DTYPE(Q, at::kFloat);
   CHECK_DEV(R);
   CHECK_DTYPE(R, at::kFloat);
   TORCH_CHECK(Q.dim() == 2 && R.dim() == 2 && Q.size(1) == R.size(1), "Q [M,D], R [N,D] required");
-  TORCH_CHECK(k >= 1 && k <= 32, "k must be in [1,32]");
+  TORCH_CHECK(k >= 1 && k <= 64, "k must be in [1,64]");
+  TORCH_CHECK(metric >= 0 && metric <= 2 && (metric != 2 || p > 0), "metric 0 (sq euclidean), 1 (L1), 2 (Lp, p > 0)");
   const int64_t M = Q.size(0), N = R.size(0), D = Q.size(1);
   TORCH_CHECK(D >= 1, "D must be >= 1");
   if (splits <= 0) {
@@ -435,7 +436,7 @@ py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t 
   DevGuard g(Q.device());
   avk::knn_topk(Q.data_ptr<float>(), M, R.data_ptr<float>(), N, (int)D, (int)k, q_base, r_base,
                 exclude_self ? 1 : 0, od.data_ptr<float>(), reinterpret_cast<long long*>(oi.data_ptr<int64_t>()),
-                (int)splits, cur_stream(Q));
+                (int)splits, (int)metric, (float)p, cur_stream(Q));
   return py::make_tuple(od, oi, splits);
 }
 

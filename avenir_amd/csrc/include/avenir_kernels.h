@@ -58,7 +58,7 @@ void tree_predict(const uint8_t* codes, long long ld, long long n, const int* fe
 // ---- distance.hip (K9/K11) -----------------------------------------------------------------
 void knn_topk(const float* Q, long long M, const float* R, long long N, int D, int k,
               long long q_index_base, long long r_index_base, int exclude_self, float* out_d,
-              long long* out_i, int splits, hipStream_t stream);
+              long long* out_i, int splits, int metric, float p, hipStream_t stream);
 void cluster_accumulate(const float* X, long long N, int D, const int* assign, int K, double* sums,
                         unsigned long long* counts, hipStream_t stream);
 

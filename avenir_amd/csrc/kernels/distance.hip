@@ -7,7 +7,8 @@
 // matrix is never materialised.  k-means assignment (J/cluster/KmeansCluster.java:154-172) is the
 // k = 1 case of the same kernel.
 //
-// Block = 256 threads = 4 waves, a 64-query x 64-reference tile per step.  Each wave computes a
+// Block = 256 threads = 4 waves, a 64-query x 64-reference tile per step (L1 / Lp metrics: the same
+// tile on the VALU, 4 x 4 distances per thread).  Each wave computes a
 // 32 x 32 block of dot products with the exact f32-input MFMA v_mfma_f32_32x32x2_f32 (bit-exact
 // fmaf chain; on gfx950 it runs at the f32 vector rate and leaves the VALU free for the top-k), the
 // tile is turned into squared distances ||q||^2 + ||r||^2 - 2 q.r in LDS, then 4 threads per query
@@ -40,17 +41,34 @@ __device__ __forceinline__ void topk_insert(float (&bd)[K], int (&bi)[K], float 
   }
 }
 
-template <int K>
+// LDS carve (dynamic, 16-byte aligned): the main loop's Q / R feature chunks, the distance tile and
+// the norms, and — aliased over them once the scan is done — the per-query merge lists.  Aliasing
+// keeps a K <= 32 block at 66 KB (2 blocks per CU) and lets K = 64 fit at all (132 KB).
+constexpr int LDS_SQ = 0;
+constexpr int LDS_SR = LDS_SQ + BQ * (KC + 1) * 4;
+constexpr int LDS_SD = LDS_SR + BR * (KC + 1) * 4;
+constexpr int LDS_QN = LDS_SD + BQ * (BR + 1) * 4;
+constexpr int LDS_RN = LDS_QN + BQ * 4;
+constexpr int LDS_MAIN = LDS_RN + BR * 4;
+__host__ __device__ constexpr int knn_lds_bytes(int K) {
+  return LDS_MAIN > BQ * 4 * K * 8 ? LDS_MAIN : BQ * 4 * K * 8;
+}
+
+// MET: 0 = squared euclidean on MFMA (||q||^2 + ||r||^2 - 2 q.r), 1 = L1 (VALU), 2 = sum |q - r|^p
+// (VALU; the caller takes the p-th root of the selected values — the order is the same).
+template <int K, int MET>
 __global__ __launch_bounds__(KT) void knn_mfma_kernel(
     const float* __restrict__ Q, long long M, const float* __restrict__ R, long long N, int D,
     long long r_per_split, long long q_index_base, long long r_index_base, int exclude_self,
-    float* __restrict__ out_d, long long* __restrict__ out_i, int kk) {
-  __shared__ float sQ[BQ][KC + 1];
-  __shared__ float sR[BR][KC + 1];
-  __shared__ float sD[BQ][BR + 1];
-  __shared__ float sqn[BQ], srn[BR];
-  __shared__ float mD[BQ][4][K];
-  __shared__ int mI[BQ][4][K];
+    float* __restrict__ out_d, long long* __restrict__ out_i, int kk, float pw) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float(*sQ)[KC + 1] = reinterpret_cast<float(*)[KC + 1]>(smem + LDS_SQ);
+  float(*sR)[KC + 1] = reinterpret_cast<float(*)[KC + 1]>(smem + LDS_SR);
+  float(*sD)[BR + 1] = reinterpret_cast<float(*)[BR + 1]>(smem + LDS_SD);
+  float* sqn = reinterpret_cast<float*>(smem + LDS_QN);
+  float* srn = reinterpret_cast<float*>(smem + LDS_RN);
+  float(*mD)[4][K] = reinterpret_cast<float(*)[4][K]>(smem);
+  int(*mI)[4][K] = reinterpret_cast<int(*)[4][K]>(smem + BQ * 4 * K * 4);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -59,8 +77,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   const long long rb = (long long)blockIdx.y * r_per_split;
   const long long re = min(N, rb + r_per_split);
 
-  // query norms (once)
-  if (tid < BQ) {
+  if (MET == 0 && tid < BQ) {  // query norms (once)
     float s = 0.f;
     const long long q = q0 + tid;
     if (q < M)
@@ -79,7 +96,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
 
   for (long long r0 = rb; r0 < re; r0 += BR) {
     __syncthreads();
-    if (tid < BR) {
+    if (MET == 0 && tid < BR) {
       float s = 0.f;
       const long long r = r0 + tid;
       if (r < re)
@@ -89,9 +106,10 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         }
       srn[tid] = s;
     }
-    f32x16 acc;
+    f32x16 acc;  // MET 0: the wave's 32 x 32 MFMA block; MET 1/2: this thread's 4 x 4 block
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const int tq = tid >> 4, tr = tid & 15;  // VALU block: queries tq + 16 a, references tr + 16 b
     for (int d0 = 0; d0 < D; d0 += KC) {
       __syncthreads();
       for (int e = tid; e < BQ * KC; e += KT) {
@@ -102,16 +120,34 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         sR[row][c] = (r < re && d0 + c < D) ? R[r * D + d0 + c] : 0.f;
       }
       __syncthreads();
-      const int li = lane & 31, lk = lane >> 5;
+      if constexpr (MET == 0) {
+        const int li = lane & 31, lk = lane >> 5;
 #pragma unroll
-      for (int k = 0; k < KC; k += 2) {
-        const float a = sQ[wq * 32 + li][k + lk];   // A[i = lane&31][k = lane>>5]
-        const float b = sR[wr * 32 + li][k + lk];   // B[k = lane>>5][j = lane&31]
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        for (int k = 0; k < KC; k += 2) {
+          const float a = sQ[wq * 32 + li][k + lk];   // A[i = lane&31][k = lane>>5]
+          const float b = sR[wr * 32 + li][k + lk];   // B[k = lane>>5][j = lane&31]
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+      } else {
+        // zero-padded features contribute |0 - 0| = 0, so no tail guard is needed
+        for (int c = 0; c < KC; ++c) {
+          float qa[4], rv[4];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) qa[a] = sQ[tq + 16 * a][c];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) rv[b] = sR[tr + 16 * b][c];
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const float df = fabsf(qa[a] - rv[b]);
+              acc[a * 4 + b] += (MET == 1) ? df : __powf(df, pw);
+            }
+        }
       }
     }
-    // accumulator -> squared distances in LDS (C/D map: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5))
-    {
+    if constexpr (MET == 0) {
+      // accumulator -> squared distances in LDS (C/D map: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5))
       const int col = lane & 31;
       const long long rj = r0 + wr * 32 + col;
 #pragma unroll
@@ -125,6 +161,18 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         if (exclude_self && (q_index_base + gq) == (r_index_base + rj)) dist = INFINITY;
         sD[qi][wr * 32 + col] = dist;
       }
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int qi = tq + 16 * a, rj = tr + 16 * b;
+          const long long gq = q0 + qi, gr = r0 + rj;
+          float dist = acc[a * 4 + b];
+          if (gr >= re || gq >= M) dist = INFINITY;
+          if (exclude_self && (q_index_base + gq) == (r_index_base + gr)) dist = INFINITY;
+          sD[qi][rj] = dist;
+        }
     }
     __syncthreads();
 #pragma unroll 4
@@ -133,6 +181,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       topk_insert<K>(bd, bi, sD[my_q][j], (int)(r0 - rb) + j);
     }
   }
+  __syncthreads();  // the merge lists alias the tiles
   // merge the 4 partial lists of each query
 #pragma unroll
   for (int s = 0; s < K; ++s) {
@@ -205,20 +254,30 @@ namespace avk {
 
 void knn_topk(const float* Q, long long M, const float* R, long long N, int D, int k,
               long long q_index_base, long long r_index_base, int exclude_self, float* out_d,
-              long long* out_i, int splits, hipStream_t stream) {
+              long long* out_i, int splits, int metric, float p, hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
   const long long per = ((N + splits - 1) / splits + BR - 1) / BR * BR;
   dim3 grid((unsigned)((M + BQ - 1) / BQ), (unsigned)splits);
-#define AV_KNN(KK)                                                                                \
-  knn_mfma_kernel<KK><<<grid, KT, 0, stream>>>(Q, M, R, N, D, per, q_index_base, r_index_base,    \
-                                               exclude_self, out_d, reinterpret_cast<long long*>(out_i), k)
-  if (k <= 1) AV_KNN(1);
-  else if (k <= 4) AV_KNN(4);
-  else if (k <= 8) AV_KNN(8);
-  else if (k <= 16) AV_KNN(16);
-  else if (k <= 32) AV_KNN(32);
-  else throw std::runtime_error("knn_topk: k > 32 not supported by the fused kernel");
-#undef AV_KNN
+  auto launch = [&](auto kern, int K) {
+    const int lds = knn_lds_bytes(K);
+    AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    kern<<<grid, KT, lds, stream>>>(Q, M, R, N, D, per, q_index_base, r_index_base, exclude_self, out_d,
+                                    reinterpret_cast<long long*>(out_i), k, p);
+  };
+#define AV_KNN_MET(MET)                                                  \
+  if (k <= 1) launch(knn_mfma_kernel<1, MET>, 1);                        \
+  else if (k <= 4) launch(knn_mfma_kernel<4, MET>, 4);                   \
+  else if (k <= 8) launch(knn_mfma_kernel<8, MET>, 8);                   \
+  else if (k <= 16) launch(knn_mfma_kernel<16, MET>, 16);                \
+  else if (k <= 32) launch(knn_mfma_kernel<32, MET>, 32);                \
+  else if (k <= 64) launch(knn_mfma_kernel<64, MET>, 64);                \
+  else throw std::runtime_error("knn_topk: k > 64 not supported by the fused kernel");
+  if (metric == 0) { AV_KNN_MET(0) }
+  else if (metric == 1) { AV_KNN_MET(1) }
+  else if (metric == 2) { AV_KNN_MET(2) }
+  else throw std::runtime_error("knn_topk: unknown metric");
+#undef AV_KNN_MET
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -18,6 +18,7 @@ Hadoop input splits: every rank reads only its own byte range of the file.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Sequence
@@ -254,7 +255,7 @@ class LazyColumn(Sequence):
 
 def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
              world: int = 1, device: str | torch.device = "cpu", keep_lines: bool = False,
-             skip_header: bool = False, nthreads: int = 8, feature_ordinals: Sequence[int] | None = None,
+             skip_header: bool = False, nthreads: int | None = None, feature_ordinals: Sequence[int] | None = None,
              class_ordinal: int | None = None, raw_numeric: bool = False) -> Table:
     """Parse ``path`` into a ``Table`` (this rank's shard) with the native K1 parser.
 
@@ -277,6 +278,8 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
              else schema.find_class_attr_field())
     C = _native.host()
     use_native = C is not None and not _is_regex(delim)
+    if nthreads is None:    # parse threads: the machine's cores, capped at a GPU box's CPU share
+        nthreads = max(1, min(16, os.cpu_count() or 8))
     csv = C.CsvFile(str(path), _literal(delim or ","), skip_header, nthreads) if use_native else None
     # categorical fields without a schema cardinality: dictionary in first-seen order over the
     # WHOLE file (identical on every rank), any size (uint16 codes above 255 values)

@@ -10,6 +10,7 @@ from .. import _native
 from ..data.table import MISSING, Table
 
 _MFMA_METRICS = ("euclidean", "sqeuclidean", "cosine")
+_KMAX = 64          # largest k of the fused kernel (register-resident sorted lists)
 
 
 def _cpu_topk(Q, R, k, metric, p, exclude_self, q_base, r_base, chunk=4096):
@@ -47,14 +48,22 @@ def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: 
         exclude_self: bool = False, q_base: int = 0, r_base: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
     """k nearest references of every query: (dist float32 [M, k] ascending, idx int64 [M, k]);
     idx = -1 / dist = inf when fewer than k candidates.  ``sqeuclidean`` returns squared distances,
-    ``cosine`` returns 1 - cos."""
+    ``cosine`` returns 1 - cos.  On the GPU every metric with k <= 64 runs the fused distance +
+    top-k kernel (K9); larger k use chunked device distance blocks + ``torch.topk``."""
     Q = Q.float().contiguous()
     R = R.float().contiguous()
-    if Q.is_cuda and metric in _MFMA_METRICS and k <= 32:
+    if metric == "minkowski" and p == 2.0:
+        metric = "euclidean"
+    elif metric == "minkowski" and p == 1.0:
+        metric = "manhattan"
+    kmet = {"euclidean": 0, "sqeuclidean": 0, "cosine": 0, "manhattan": 1, "minkowski": 2}.get(metric)
+    if Q.is_cuda and kmet is not None and k <= _KMAX:
+        # fused tile distance + top-k: MFMA dot products (euclidean family) or VALU |q - r|^p
         if metric == "cosine":
             Q = torch.nn.functional.normalize(Q, dim=1)
             R = torch.nn.functional.normalize(R, dim=1)
-        d, i, splits = _native.C().knn_topk(Q, R, int(k), int(q_base), int(r_base), bool(exclude_self), 0)
+        d, i, splits = _native.C().knn_topk(Q, R, int(k), int(q_base), int(r_base), bool(exclude_self), 0,
+                                            kmet, float(p))
         if splits > 1:  # merge the per-split top-k slabs [S, M, k] -> [M, k]
             d = d.permute(1, 0, 2).reshape(Q.shape[0], -1)
             i = i.permute(1, 0, 2).reshape(Q.shape[0], -1)
@@ -64,6 +73,8 @@ def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: 
             d, i = d[0], i[0]
         if metric == "cosine":
             return d * 0.5, i
+        if metric == "minkowski":
+            return d.pow(1.0 / p), i
         return (d.sqrt() if metric == "euclidean" else d), i
     d, i = _cpu_topk(Q, R, k, "sqeuclidean" if metric == "euclidean" else metric, p, exclude_self,
                      q_base, r_base)

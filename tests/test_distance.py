@@ -144,6 +144,26 @@ def test_knn_mfma_gpu(cuda, M, N, Dm, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("metric,p,k", [("manhattan", 1.0, 5), ("minkowski", 3.0, 7), ("euclidean", 2.0, 50),
+                                        ("manhattan", 1.0, 64), ("minkowski", 1.5, 1), ("cosine", 2.0, 40)])
+def test_knn_metrics_and_large_k_gpu(cuda, metric, p, k):
+    """L1 / Lp on the VALU tile and k up to 64 in the fused kernel, against a float64 oracle."""
+    g = torch.Generator().manual_seed(k)
+    Q, R = torch.randn(700, 19, generator=g), torch.randn(4003, 19, generator=g)
+    d, i = D.knn(Q.to(cuda), R.to(cuda), k, metric=metric, p=p)
+    if metric == "cosine":
+        ref = 1 - torch.nn.functional.normalize(Q.double(), dim=1) @ torch.nn.functional.normalize(R.double(), dim=1).T
+    else:
+        ref = torch.cdist(Q.double(), R.double(), p=p)
+    bd, bi = torch.topk(ref, k, dim=1, largest=False)
+    assert torch.allclose(d.cpu().double(), bd, atol=2e-3, rtol=1e-4)
+    agree = float((i.cpu() == bi).float().mean())
+    assert agree > 0.99
+    d2, i2 = D.knn(R[:200].to(cuda), R.to(cuda), 3, metric=metric, p=p, exclude_self=True)
+    assert not bool((i2.cpu() == torch.arange(200).view(-1, 1)).any())
+
+
+@pytest.mark.gpu
 def test_kmeans_gpu_matches_cpu(cuda):
     g = torch.Generator().manual_seed(8)
     X = torch.randn(20000, 6, generator=g) + torch.randint(0, 4, (20000, 1), generator=g) * 5.0
