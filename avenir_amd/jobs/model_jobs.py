@@ -567,19 +567,21 @@ def record_similarity(args):
     d = ctx.delim_out
     out = []
     nf = math.sqrt(max(len(ords), 1))
+    nB = len(Brows)
     for s in range(a, b, 2048):
         e = min(b, s + 2048)
-        D = (pairwise(A[s:e], B) / nf * scale).round().long().cpu()
-        for q in range(e - s):
+        D = (pairwise(A[s:e], B) / nf * scale).round().long()
+        keep = D <= thr if math.isfinite(thr) else torch.ones_like(D, dtype=torch.bool)
+        if other is None:   # upper triangle: j > i
+            keep &= torch.arange(nB, device=D.device).view(1, -1) > torch.arange(s, e, device=D.device).view(-1, 1)
+        qi, jj = torch.nonzero(keep, as_tuple=True)          # row-major: (i, j) ascending
+        vals = D[qi, jj].tolist()
+        for q, j, v in zip(qi.tolist(), jj.tolist(), vals):
             i = s + q
-            js = range(i + 1, len(Brows)) if other is None else range(len(Brows))
-            row = D[q].tolist()
-            for j in js:
-                if row[j] <= thr:
-                    parts = [rows[i][idc], Brows[j][idc]]
-                    if out_rec:
-                        parts += rows[i] + Brows[j]
-                    out.append(d.join(parts + [str(row[j])]))
+            parts = [rows[i][idc], Brows[j][idc]]
+            if out_rec:
+                parts += rows[i] + Brows[j]
+            out.append(d.join(parts + [str(v)]))
     ctx.emit(out)
 
 
@@ -599,13 +601,16 @@ def grouped_similarity(args):
     a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
     d = ctx.delim_out
     out = []
-    for k in keys[a:b]:
-        rows = g[k]
-        X = _numeric_matrix(ctx, rows, ords)
-        D = pairwise(X, X).cpu().tolist()
-        for i in range(len(rows)):
-            for j in range(i + 1, len(rows)):
-                out.append(d.join(list(k) + [rows[i][idc], rows[j][idc], fmt(D[i][j], prec)]))
+    # all of this rank's groups in one batched pass (GroupedRecordSimilarity.pairs)
+    from ..models.similarity import GroupedRecordSimilarity
+    mine = [(gi, r) for gi, k in enumerate(keys[a:b]) for r in g[k]]
+    if mine:
+        X = _numeric_matrix(ctx, [r for _, r in mine], ords)
+        gid = torch.tensor([gi for gi, _ in mine], dtype=torch.long, device=X.device)
+        ii, jj, dd = GroupedRecordSimilarity().pairs(X, gid)
+        for i, j, v in zip(ii.tolist(), jj.tolist(), dd.tolist()):
+            gi, ri = mine[i]
+            out.append(d.join(list(keys[a + gi]) + [ri[idc], mine[j][1][idc], fmt(v, prec)]))
     ctx.emit(out)
 
 

@@ -52,11 +52,72 @@ class NearestRecords:
 
 
 class GroupedRecordSimilarity:
+    """Pairwise distances within each key group, all groups at once: records are sorted by group,
+    groups are bucketed by size (powers of two) and each bucket is ONE batched distance launch over
+    a zero-padded [groups, L, D] block — no per-group loop, whatever the number of groups."""
+
     def __init__(self, metric: str = "euclidean"):
         self.metric = metric
 
+    def pairs(self, X: torch.Tensor, groups: torch.Tensor):
+        """Every within-group pair i < j (original row indices): (i, j, distance) tensors, ordered
+        by group then (i, j)."""
+        n = X.shape[0]
+        dev = X.device
+        groups = groups.to(dev)
+        order = torch.argsort(groups, stable=True)
+        g_sorted = groups[order]
+        _, counts = torch.unique_consecutive(g_sorted, return_counts=True)
+        starts = torch.cumsum(counts, 0) - counts
+        cnt_h = counts.cpu()
+        out_i, out_j, out_d, out_key = [], [], [], []
+        G = int(cnt_h.numel())
+        if n == 0 or G == 0:
+            e = torch.zeros(0, dtype=torch.long, device=dev)
+            return e, e, torch.zeros(0, device=dev)
+        lvl = torch.ceil(torch.log2(cnt_h.clamp_min(1).double())).long()
+        for L2 in torch.unique(lvl).tolist():
+            gsel = torch.nonzero(lvl == L2).view(-1)
+            L = 1 << int(L2)
+            if L < 2:
+                continue                                           # singleton groups: no pairs
+            gd = gsel.to(dev)
+            pos = torch.arange(L, device=dev)
+            valid = pos.view(1, -1) < counts[gd].view(-1, 1)          # [Gb, L]
+            src = (starts[gd].view(-1, 1) + pos.view(1, -1)).clamp_max(n - 1)
+            rows = order[src]                                         # [Gb, L] original row ids
+            B = X[rows] * valid.unsqueeze(-1)
+            Dm = self._batched(B)                                     # [Gb, L, L]
+            ii, jj = torch.triu_indices(L, L, 1, device=dev)
+            ok = valid[:, ii] & valid[:, jj]                          # [Gb, P]
+            gb, pidx = torch.nonzero(ok, as_tuple=True)
+            out_i.append(rows[gb, ii[pidx]])
+            out_j.append(rows[gb, jj[pidx]])
+            out_d.append(Dm[gb, ii[pidx], jj[pidx]])
+            out_key.append(gd[gb] * (n + 1) + starts[gd[gb]])         # stable group order
+        if not out_i:
+            e = torch.zeros(0, dtype=torch.long, device=dev)
+            return e, e, torch.zeros(0, device=dev)
+        i, j, d, key = torch.cat(out_i), torch.cat(out_j), torch.cat(out_d), torch.cat(out_key)
+        # group order, then (i, j) in the group's sorted-row order
+        rank = torch.empty(n, dtype=torch.long, device=dev)
+        rank[order] = torch.arange(n, device=dev)
+        o = torch.argsort(rank[i] * (n + 1) + rank[j])
+        return i[o], j[o], d[o]
+
+    def _batched(self, B: torch.Tensor) -> torch.Tensor:
+        if self.metric in ("euclidean", "sqeuclidean"):
+            d = torch.cdist(B, B)
+            return d * d if self.metric == "sqeuclidean" else d
+        if self.metric == "manhattan":
+            return torch.cdist(B, B, p=1)
+        if self.metric == "cosine":
+            nb = torch.nn.functional.normalize(B, dim=-1)
+            return 1 - nb @ nb.transpose(1, 2)
+        raise ValueError(f"unknown metric {self.metric}")
+
     def __call__(self, X: torch.Tensor, groups: torch.Tensor) -> dict[int, torch.Tensor]:
-        """Full distance matrix per group id."""
+        """Full distance matrix per group id (small outputs; ``pairs`` is the bulk path)."""
         out = {}
         for g in torch.unique(groups).tolist():
             idx = torch.nonzero(groups == g).squeeze(1)

@@ -212,3 +212,40 @@ def test_kmeans_step_kernel_matches_oracle(cuda):
         assert torch.equal(a_a, a_b) and torch.equal(c_a, c_b)
         assert torch.allclose(s_a, s_b, rtol=1e-5, atol=1e-3)
         assert float(e_a) == pytest.approx(float(e_b), rel=1e-6)
+
+
+def _grouped_oracle(X, groups):
+    out = []
+    for g in sorted(set(groups.tolist())):
+        idx = [i for i in range(len(groups)) if int(groups[i]) == g]
+        for a in range(len(idx)):
+            for b in range(a + 1, len(idx)):
+                out.append((idx[a], idx[b], float(torch.dist(X[idx[a]].double(), X[idx[b]].double()))))
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_grouped_similarity_batched_equals_per_group(seed):
+    from avenir_amd.models.similarity import GroupedRecordSimilarity
+    g = torch.Generator().manual_seed(seed)
+    sizes = [1, 2, 3, 5, 8, 9, 17, 1, 33, 4]
+    groups = torch.cat([torch.full((s,), 7 * k + 3) for k, s in enumerate(sizes)])
+    perm = torch.randperm(groups.numel(), generator=g)
+    groups = groups[perm]
+    X = torch.randn(groups.numel(), 4, generator=g)
+    i, j, d = GroupedRecordSimilarity().pairs(X, groups)
+    ref = _grouped_oracle(X, groups)
+    assert [(a, b) for a, b, _ in ref] == list(zip(i.tolist(), j.tolist()))
+    assert torch.allclose(d.double(), torch.tensor([v for _, _, v in ref], dtype=torch.float64), atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_grouped_similarity_gpu(cuda):
+    from avenir_amd.models.similarity import GroupedRecordSimilarity
+    g = torch.Generator().manual_seed(3)
+    groups = torch.randint(0, 500, (6000,), generator=g)
+    X = torch.randn(6000, 5, generator=g)
+    ic, jc, dc = GroupedRecordSimilarity().pairs(X, groups)
+    ig, jg, dg = GroupedRecordSimilarity().pairs(X.to(cuda), groups.to(cuda))
+    assert torch.equal(ic, ig.cpu()) and torch.equal(jc, jg.cpu())
+    assert torch.allclose(dc, dg.cpu(), atol=1e-4)
