@@ -1271,6 +1271,43 @@ std::vector<at::Tensor> forest_bootstrap(const at::Tensor& codes, const at::Tens
   return {cb, lb, wb, per_tree};
 }
 
+// K27: Y = act(X W^T + b) and its backward epilogue (dZ = dY * act'(Y), db = colsum dZ).
+at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b, int64_t act) {
+  CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
+  TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "X [M, K], W [N, K]");
+  TORCH_CHECK(act >= 0 && act <= 5, "activation code 0..5");
+  TORCH_CHECK(X.size(0) < (1LL << 31) && W.size(0) < (1LL << 31) && X.size(1) < (1LL << 31), "dims < 2^31");
+  auto Xc = X.contiguous(), Wc = W.contiguous();
+  at::Tensor bc;
+  if (b.has_value() && b->defined()) {
+    CHECK_DEV((*b)); CHECK_DTYPE((*b), at::kFloat);
+    TORCH_CHECK(b->numel() == W.size(0), "bias [N]");
+    bc = b->contiguous();
+  }
+  auto Y = at::empty({X.size(0), W.size(0)}, X.options());
+  DevGuard g(X.device());
+  avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), bc.defined() ? bc.data_ptr<float>() : nullptr,
+                      Y.data_ptr<float>(), (int)X.size(0), (int)W.size(0), (int)X.size(1), (int)act, cur_stream(X));
+  return Y;
+}
+
+std::vector<at::Tensor> linear_act_bwd(const at::Tensor& dY, const at::Tensor& Y, int64_t act) {
+  CHECK_DEV(dY); CHECK_DTYPE(dY, at::kFloat);
+  CHECK_DEV(Y); CHECK_DTYPE(Y, at::kFloat);
+  TORCH_CHECK(dY.sizes() == Y.sizes() && Y.dim() == 2, "dY and Y [M, N]");
+  TORCH_CHECK(act >= 0 && act <= 5, "activation code 0..5");
+  const int M = (int)Y.size(0), N = (int)Y.size(1);
+  auto dYc = dY.contiguous(), Yc = Y.contiguous();
+  auto dZ = at::empty_like(Yc);
+  auto part = at::empty({std::max(1, avk::linear_act_bwd_blocks(M)), N}, Y.options());
+  DevGuard g(Y.device());
+  if (M == 0) part.zero_();
+  avk::linear_act_bwd(dYc.data_ptr<float>(), Yc.data_ptr<float>(), dZ.data_ptr<float>(), part.data_ptr<float>(), M,
+                      N, (int)act, cur_stream(Y));
+  return {dZ, part.sum(0)};
+}
+
 // K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
 // are joined with every row whose (k-1)-prefix equals their (k-1)-suffix -> int32 [M, k+1].
 at::Tensor gsp_join(const at::Tensor& X, int64_t lo, int64_t hi) {
@@ -1503,6 +1540,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("forest_part_count", &forest_part_count);
   m.def("forest_part_scatter", &forest_part_scatter);
   m.def("forest_bootstrap", &forest_bootstrap);
+  m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0);
+  m.def("linear_act_bwd", &linear_act_bwd);
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);

@@ -157,6 +157,12 @@ void forest_split(const long long* hist, const uint8_t* fmask, const int* bins, 
 void forest_part_count(const uint8_t* codes, long long ld, const int* item_node, const long long* item_start,
                        const int* item_len, int n_items, const int* feat, const int* thr, int* item_left,
                        hipStream_t stream);
+// K27 fused Linear + bias + activation (mlp.hip)
+void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
+                    hipStream_t stream);
+int linear_act_bwd_blocks(int M);
+void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
+                    hipStream_t stream);
 void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
                        unsigned rate32, int* tile_cnt, hipStream_t stream);
 void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,

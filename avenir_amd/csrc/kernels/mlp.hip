@@ -1,0 +1,143 @@
+// K27: fused Linear + bias + activation for the feed-forward network (FeedForwardNetwork,
+// P/supv/tnn.py:100-145 builds Linear -> activation pairs; torch runs them as an addmm followed by
+// a separate activation kernel, i.e. the [M, N] pre-activation makes a full HBM round trip).
+//
+// Forward  Y = act(X W^T + b):  X [M, K] row-major, W [N, K] row-major (torch Linear layout).
+//   Block = 256 threads = 4 waves over a 64 x 64 output tile; each wave owns a 32 x 32 quarter and
+//   accumulates it with the exact-f32 MFMA v_mfma_f32_32x32x2_f32 (same rounding as an fmaf chain)
+//   over K chunks of 32 staged in LDS (rows padded to 33 floats: the column-of-rows reads of the
+//   A / B operands hit 32 distinct banks).  Bias and activation are applied to the accumulator in
+//   registers and Y is stored once.
+// Backward dZ = dY * act'(Y), db = colsum(dZ): one pass over dY / Y (the derivative is taken from
+//   the stored output, so no pre-activation tensor is kept), per-block column partials reduced on
+//   the host side of the op; dX = dZ W and dW = dZ^T X are plain GEMMs (hipBLASLt).
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+constexpr int MT = 256;  // threads
+constexpr int TM = 64;   // output rows per block
+constexpr int TN = 64;   // output cols per block
+constexpr int KC = 32;   // K chunk in LDS
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// act codes: 0 identity, 1 relu, 2 sigmoid, 3 tanh, 4 leaky relu (0.01), 5 elu (alpha 1)
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  switch (act) {
+    case 1: return fmaxf(z, 0.f);
+    case 2: return 1.f / (1.f + expf(-z));
+    case 3: return tanhf(z);
+    case 4: return z > 0.f ? z : 0.01f * z;
+    case 5: return z > 0.f ? z : expm1f(z);
+    default: return z;
+  }
+}
+
+// derivative expressed through the output y = act(z)
+__device__ __forceinline__ float act_grad_from_y(float y, int act) {
+  switch (act) {
+    case 1: return y > 0.f ? 1.f : 0.f;
+    case 2: return y * (1.f - y);
+    case 3: return 1.f - y * y;
+    case 4: return y > 0.f ? 1.f : 0.01f;
+    case 5: return y > 0.f ? 1.f : y + 1.f;
+    default: return 1.f;
+  }
+}
+
+__global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W,
+                                                             const float* __restrict__ b, float* __restrict__ Y,
+                                                             int M, int N, int K, int act) {
+  __shared__ float sX[TM][KC + 1];
+  __shared__ float sW[TN][KC + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const long long m0 = (long long)blockIdx.y * TM;
+  const int n0 = blockIdx.x * TN;
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    __syncthreads();
+    for (int e = tid; e < TM * KC; e += MT) {
+      const int row = e / KC, c = e % KC;
+      const long long m = m0 + row;
+      const int n = n0 + row, k = k0 + c;
+      sX[row][c] = (m < M && k < K) ? X[m * K + k] : 0.f;
+      sW[row][c] = (n < N && k < K) ? W[(long long)n * K + k] : 0.f;
+    }
+    __syncthreads();
+    const int li = lane & 31, lk = lane >> 5;
+#pragma unroll
+    for (int k = 0; k < KC; k += 2) {
+      const float a = sX[wm * 32 + li][k + lk];  // A[i = lane&31][k = lane>>5]
+      const float w = sW[wn * 32 + li][k + lk];  // B[k = lane>>5][j = lane&31]
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+    }
+  }
+  // epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  const int col = n0 + wn * 32 + (lane & 31);
+  if (col >= N) return;
+  const float bias = b ? b[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const long long row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row < M) Y[row * N + col] = act_fwd(acc[r] + bias, act);
+  }
+}
+
+// dZ = dY * act'(Y); partial[blockIdx.y][n] = sum over this block's rows of dZ[., n]
+constexpr int BR_ROWS = 256;
+__global__ __launch_bounds__(MT) void linear_act_bwd_kernel(const float* __restrict__ dY, const float* __restrict__ Y,
+                                                             float* __restrict__ dZ, float* __restrict__ partial,
+                                                             int M, int N, int act) {
+  __shared__ float s[MT / 64][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const long long r0 = (long long)blockIdx.y * BR_ROWS;
+  float acc = 0.f;
+  if (n < N) {
+    for (int i = rg; i < BR_ROWS; i += MT / 64) {
+      const long long m = r0 + i;
+      if (m >= M) break;
+      const long long o = m * N + n;
+      const float g = dY[o] * act_grad_from_y(Y[o], act);
+      dZ[o] = g;
+      acc += g;
+    }
+  }
+  s[rg][c] = acc;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < MT / 64; ++j) t += s[j][c];
+    partial[(long long)blockIdx.y * N + n] = t;
+  }
+}
+
+}  // namespace
+
+namespace avk {
+
+void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
+                    hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
+  linear_act_fwd_kernel<<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int linear_act_bwd_blocks(int M) { return (M + BR_ROWS - 1) / BR_ROWS; }
+
+void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
+                    hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)linear_act_bwd_blocks(M));
+  linear_act_bwd_kernel<<<grid, MT, 0, stream>>>(dY, Y, dZ, partial, M, N, act);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace avk

@@ -23,7 +23,25 @@ from .common import (GraphedStep, _cfg, create_activation, create_loss, load_che
                      optimizer_from_config, pick_device, save_checkpoint, scale_data)
 
 
-def parse_layer_spec(spec: str, n_in: int) -> torch.nn.Sequential:
+class FusedLinear(torch.nn.Linear):
+    """``Linear`` followed by an activation, run as the K27 fused kernel on the GPU
+    (``ops.mlp_ops.linear_act``).  Same parameter names as ``torch.nn.Linear``, so checkpoints keep
+    the reference's ``layers.<i>.weight`` keys; the activation's slot in the Sequential holds an
+    ``Identity``."""
+
+    def __init__(self, n_in: int, n_out: int, act: str):
+        super().__init__(n_in, n_out)
+        self.act = act
+
+    def forward(self, x):
+        from ..ops.mlp_ops import linear_act
+        return linear_act(x, self.weight, self.bias, self.act)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", act={self.act}"
+
+
+def parse_layer_spec(spec: str, n_in: int, fuse: bool = True) -> torch.nn.Sequential:
     layers: list[torch.nn.Module] = []
     ninp = n_in
     for ld in spec.split(","):
@@ -43,7 +61,13 @@ def parse_layer_spec(spec: str, n_in: int) -> torch.nn.Sequential:
                 if act is not None:
                     layers.append(act)
         elif act is not None:
-            layers.append(act)
+            from ..ops.mlp_ops import ACT_CODES
+            if fuse and act_s in ACT_CODES:
+                # Linear + activation -> one fused kernel; Identity keeps the module indices
+                layers[-1] = FusedLinear(ninp, nunit, act_s)
+                layers.append(torch.nn.Identity())
+            else:
+                layers.append(act)
         if dpr > 0:
             layers.append(torch.nn.Dropout(dpr))
         ninp = nunit

@@ -1,0 +1,57 @@
+"""K27 fused Linear + bias + activation (csrc/kernels/mlp.hip) as an autograd op.
+
+``linear_act(x, W, b, act)`` = ``act(x @ W.T + b)``.  On the GPU the forward is ONE MFMA kernel with
+the bias and activation applied in the accumulator epilogue (torch: addmm + a separate activation
+pass over [M, N]); the backward is one fused pass computing ``dZ = dY * act'(Y)`` and the bias
+gradient from the stored output, then two library GEMMs (hipBLASLt) for ``dX`` and ``dW``.  CPU
+tensors run the plain PyTorch composition (the numerics oracle of the GPU tests).
+
+Reference: FeedForwardNetwork layer construction, P/supv/tnn.py:100-145.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+ACT_CODES = {None: 0, "none": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leakyRelu": 4, "elu": 5}
+
+
+def _act_torch(z: torch.Tensor, code: int) -> torch.Tensor:
+    if code == 1:
+        return torch.relu(z)
+    if code == 2:
+        return torch.sigmoid(z)
+    if code == 3:
+        return torch.tanh(z)
+    if code == 4:
+        return torch.nn.functional.leaky_relu(z, 0.01)
+    if code == 5:
+        return torch.nn.functional.elu(z)
+    return z
+
+
+class _LinearAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b, code):
+        C = _native.C()
+        y = C.linear_act_fwd(x, W, b, code)
+        ctx.save_for_backward(x, W, y)
+        ctx.code = code
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, y = ctx.saved_tensors
+        dz, db = _native.C().linear_act_bwd(gy.contiguous(), y, ctx.code)
+        gx = dz @ W if ctx.needs_input_grad[0] else None
+        gW = dz.t() @ x if ctx.needs_input_grad[1] else None
+        return gx, gW, (db if ctx.has_b else None), None
+
+
+def linear_act(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: str | int | None) -> torch.Tensor:
+    code = act if isinstance(act, int) else ACT_CODES[act]
+    if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2:
+        return _LinearAct.apply(x.contiguous(), W, b, code)
+    return _act_torch(torch.nn.functional.linear(x, W, b), code)

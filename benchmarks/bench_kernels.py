@@ -165,8 +165,26 @@ def bench_sampler(args):
         emit(kernel="sample", dist=name, n=n, ms=med, samples_per_s=n / (med / 1e3), gbps=n * 4 / (med / 1e3) / 1e9)
 
 
+def bench_mlp(args):
+    """K27 fused Linear+bias+act vs torch (addmm + activation), forward and forward+backward."""
+    from avenir_amd.ops.mlp_ops import linear_act
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for M, K, N in ((65536, 64, 64), (65536, 256, 256), (8192, 32, 16)):
+        x = torch.randn((M, K), device="cuda", generator=g, requires_grad=True)
+        W = torch.randn((N, K), device="cuda", generator=g, requires_grad=True)
+        b = torch.randn((N,), device="cuda", generator=g, requires_grad=True)
+        gy = torch.randn((M, N), device="cuda", generator=g)
+        for name, fn in (("fused", lambda: linear_act(x, W, b, "relu")),
+                         ("torch", lambda: torch.relu(torch.nn.functional.linear(x, W, b)))):
+            with torch.no_grad():
+                fwd, _ = timeit(fn, iters=20)
+            fb, _ = timeit(lambda: fn().backward(gy), iters=20)
+            emit(kernel="linear_relu", variant=name, M=M, K=K, N=N, fwd_ms=fwd, fwd_bwd_ms=fb,
+                 fwd_tflops=2.0 * M * K * N / (fwd / 1e3) / 1e12)
+
+
 BENCHES = {"hist": bench_hist, "nbpred": bench_nb_predict, "glm": bench_glm, "smo": bench_smo, "sa": bench_sa,
-           "knn": bench_knn, "sample": bench_sampler}
+           "knn": bench_knn, "sample": bench_sampler, "mlp": bench_mlp}
 
 
 def main():

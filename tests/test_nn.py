@@ -130,3 +130,46 @@ def test_mlp_graph_capture_on_gpu(cuda):
     seq = torch.rand((256, 5))
     lstm.fit(lstm.to_sequences(seq), (seq.sum(1) > 2.5).float())
     assert lstm.predict(lstm.to_sequences(seq)).device.type == "cuda"
+
+
+def test_fused_layer_spec_keeps_indices():
+    s = parse_layer_spec("8:relu:false:false:0,4:sigmoid:false:false:0.2,1:none:false:false:0", 5)
+    kinds = [type(m).__name__ for m in s]
+    assert kinds == ["FusedLinear", "Identity", "FusedLinear", "Identity", "Dropout", "Linear"]
+    ref = parse_layer_spec("8:relu:false:false:0,4:sigmoid:false:false:0.2,1:none:false:false:0", 5, fuse=False)
+    assert list(s.state_dict().keys()) == list(ref.state_dict().keys())
+    ref.load_state_dict(s.state_dict())
+    s.eval(), ref.eval()
+    x = torch.randn(7, 5)
+    assert torch.allclose(s(x), ref(x), atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh", "leakyRelu", "elu"])
+@pytest.mark.parametrize("M,K,N", [(37, 5, 3), (300, 64, 130), (1025, 33, 64)])
+def test_linear_act_kernel_matches_torch(cuda, act, M, K, N):
+    from avenir_amd.ops.mlp_ops import _act_torch, ACT_CODES, linear_act
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g, dtype=torch.float64)
+    W = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
+    b = torch.randn(N, generator=g, dtype=torch.float64)
+    gy = torch.randn(M, N, generator=g, dtype=torch.float64)
+    xr, Wr, br = (t.clone().requires_grad_() for t in (x, W, b))
+    yr = _act_torch(torch.nn.functional.linear(xr, Wr, br), ACT_CODES[act])
+    yr.backward(gy)
+    xg, Wg, bg = (t.float().to(cuda).requires_grad_() for t in (x, W, b))
+    yg = linear_act(xg, Wg, bg, act)
+    yg.backward(gy.float().to(cuda))
+    assert torch.allclose(yg.detach().cpu().double(), yr.detach(), atol=1e-4, rtol=1e-4)
+    for a, r in ((xg.grad, xr.grad), (Wg.grad, Wr.grad), (bg.grad, br.grad)):
+        assert torch.allclose(a.cpu().double(), r, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_mlp_fused_trains_on_gpu(cuda):
+    x, y = _xor_data()
+    m = FeedForwardNetwork("16:relu:false:false:0,16:tanh:false:false:0,2:none:false:false:0", 2, loss="ce",
+                           optimizer="adam", lr=0.01, batch_size=64, num_iter=60, device=cuda)
+    assert any(type(l).__name__ == "FusedLinear" for l in m.layers)
+    m.fit(x, y)
+    assert m.evaluate_model(x, y, "accuracy") > 0.95
