@@ -77,16 +77,10 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   const long long rb = (long long)blockIdx.y * r_per_split;
   const long long re = min(N, rb + r_per_split);
 
-  if (MET == 0 && tid < BQ) {  // query norms (once)
-    float s = 0.f;
-    const long long q = q0 + tid;
-    if (q < M)
-      for (int d = 0; d < D; ++d) {
-        const float v = Q[q * D + d];
-        s = fmaf(v, v, s);
-      }
-    sqn[tid] = s;
-  }
+  // Norms are accumulated from the LDS-staged chunks (threads 0..63: reference rows, 64..127:
+  // query rows on the first reference tile), in the same d order as a plain fmaf loop; a direct
+  // per-thread loop over D global loads serialised one memory latency per feature per tile.
+  float qn_acc = 0.f;
 
   float bd[K];
   int bi[K];
@@ -96,16 +90,8 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
 
   for (long long r0 = rb; r0 < re; r0 += BR) {
     __syncthreads();
-    if (MET == 0 && tid < BR) {
-      float s = 0.f;
-      const long long r = r0 + tid;
-      if (r < re)
-        for (int d = 0; d < D; ++d) {
-          const float v = R[r * D + d];
-          s = fmaf(v, v, s);
-        }
-      srn[tid] = s;
-    }
+    const bool first_tile = r0 == rb;
+    float rn_acc = 0.f;
     f32x16 acc;  // MET 0: the wave's 32 x 32 MFMA block; MET 1/2: this thread's 4 x 4 block
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -121,6 +107,13 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       }
       __syncthreads();
       if constexpr (MET == 0) {
+        if (tid < BR) {
+#pragma unroll 8
+          for (int c = 0; c < KC; ++c) rn_acc = fmaf(sR[tid][c], sR[tid][c], rn_acc);
+        } else if (first_tile && tid < BR + BQ) {
+#pragma unroll 8
+          for (int c = 0; c < KC; ++c) qn_acc = fmaf(sQ[tid - BR][c], sQ[tid - BR][c], qn_acc);
+        }
         const int li = lane & 31, lk = lane >> 5;
 #pragma unroll
         for (int k = 0; k < KC; k += 2) {
@@ -147,6 +140,9 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       }
     }
     if constexpr (MET == 0) {
+      if (tid < BR) srn[tid] = rn_acc;
+      else if (first_tile && tid < BR + BQ) sqn[tid - BR] = qn_acc;
+      __syncthreads();
       // accumulator -> squared distances in LDS (C/D map: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5))
       const int col = lane & 31;
       const long long rj = r0 + wr * 32 + col;

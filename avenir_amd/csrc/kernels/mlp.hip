@@ -47,6 +47,61 @@ __device__ __forceinline__ float act_grad_from_y(float y, int act) {
   }
 }
 
+// One K chunk of the X and W tiles held in registers (8 floats of each per thread): loaded for
+// chunk c+1 while the MFMAs of chunk c run, then dropped into LDS.  VEC: 16-byte loads (K % 4 == 0).
+template <bool VEC>
+struct ChunkRegs {
+  float x[8], w[8];
+  __device__ __forceinline__ void load(const float* __restrict__ X, const float* __restrict__ W, long long m0, int n0,
+                                       int k0, int M, int N, int K) {
+    const int tid = threadIdx.x;
+    if constexpr (VEC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int e4 = tid + MT * i, row = e4 >> 3, c = (e4 & 7) * 4;
+        const long long m = m0 + row;
+        const int n = n0 + row, k = k0 + c;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+        if (m < M && k < K) a = *reinterpret_cast<const float4*>(X + m * K + k);
+        if (n < N && k < K) b = *reinterpret_cast<const float4*>(W + (long long)n * K + k);
+        x[4 * i] = a.x; x[4 * i + 1] = a.y; x[4 * i + 2] = a.z; x[4 * i + 3] = a.w;
+        w[4 * i] = b.x; w[4 * i + 1] = b.y; w[4 * i + 2] = b.z; w[4 * i + 3] = b.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = tid + MT * i, row = e / KC, c = e % KC;
+        const long long m = m0 + row;
+        const int n = n0 + row, k = k0 + c;
+        x[i] = (m < M && k < K) ? X[m * K + k] : 0.f;
+        w[i] = (n < N && k < K) ? W[(long long)n * K + k] : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float (*sX)[KC + 1], float (*sW)[KC + 1]) const {
+    const int tid = threadIdx.x;
+    if constexpr (VEC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int e4 = tid + MT * i, row = e4 >> 3, c = (e4 & 7) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sX[row][c + j] = x[4 * i + j];
+          sW[row][c + j] = w[4 * i + j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = tid + MT * i, row = e / KC, c = e % KC;
+        sX[row][c] = x[i];
+        sW[row][c] = w[i];
+      }
+    }
+  }
+};
+
+template <bool VEC>
 __global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W,
                                                              const float* __restrict__ b, float* __restrict__ Y,
                                                              int M, int N, int K, int act) {
@@ -59,16 +114,13 @@ __global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restr
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  ChunkRegs<VEC> pre;
+  pre.load(X, W, m0, n0, 0, M, N, K);
   for (int k0 = 0; k0 < K; k0 += KC) {
+    __syncthreads();  // previous chunk's MFMA reads are done
+    pre.store(sX, sW);
     __syncthreads();
-    for (int e = tid; e < TM * KC; e += MT) {
-      const int row = e / KC, c = e % KC;
-      const long long m = m0 + row;
-      const int n = n0 + row, k = k0 + c;
-      sX[row][c] = (m < M && k < K) ? X[m * K + k] : 0.f;
-      sW[row][c] = (n < N && k < K) ? W[(long long)n * K + k] : 0.f;
-    }
-    __syncthreads();
+    if (k0 + KC < K) pre.load(X, W, m0, n0, k0 + KC, M, N, K);  // in flight during the MFMAs
     const int li = lane & 31, lk = lane >> 5;
 #pragma unroll
     for (int k = 0; k < KC; k += 2) {
@@ -126,7 +178,10 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
                     hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
   dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
-  linear_act_fwd_kernel<<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act);
+  const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(W) % 16 == 0);
+  if (vec) linear_act_fwd_kernel<true><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act);
+  else linear_act_fwd_kernel<false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act);
   AV_HIP_CHECK(hipGetLastError());
 }
 
