@@ -564,6 +564,32 @@ def classifier(args):
     print(json.dumps(res, default=str))
 
 
+@job("autoSupervisedLearning", "TPE search over classifiers and their hyper-parameters (P/app/autosupv.py): "
+     "--gen-args maxEvals,clf:config[:prob],...", aliases=("autosupv",))
+def auto_supervised_learning(args):
+    """``autosupv.py maxEvals rf:rf.properties[:p] gbt:gbt.properties[:p] ...``: each classifier's
+    ``train.search.params`` defines its branch of the space; TPE minimises ``trainValidate()``.
+    Prints the best assignment (hyperopt form: label -> index / value) and its loss."""
+    from ..models import supervised as SV
+    from ..optimize.tpe import auto_supervised
+    items = [v for v in (args.gen_args or "").split(",") if v]
+    if len(items) < 2:
+        raise SystemExit("autoSupervisedLearning needs --gen-args maxEvals,clf:config[:prob],...")
+    max_evals = int(items[0])
+    kinds = {"rf": SV.RandomForest, "gbt": SV.GradientBoostedTrees, "svm": SV.SupportVectorMachine,
+             "lr": SV.LogisticRegressionDiscriminant}
+    clfs, probs = {}, []
+    for it in items[1:]:
+        parts = it.split(":")
+        if parts[0] not in kinds:
+            raise ValueError("unsupported classifier")
+        clfs[parts[0]] = kinds[parts[0]](parts[1], device=args.device)
+        if len(parts) == 3:
+            probs.append(float(parts[2]))
+    best, loss, t = auto_supervised(clfs, max_evals, probs or None, seed=args.seed or 0)
+    print(json.dumps({"best": best, "loss": loss, "evals": len(t.trials)}, default=str))
+
+
 @job("serve", "REST prediction service (P/app/rfsvc.py etc.): --kind rf|gbt|svm|lr --config props --port P [--name rf]")
 def serve(args):
     from ..serve import PredictionServer, classifier_factory

@@ -112,3 +112,43 @@ def hashing_embedder(dim: int = 256, seed: int = 0):
             out.append(torch.randn(dim, generator=g))
         return torch.stack(out) if out else torch.zeros((0, dim))
     return emb
+
+
+def corpus_embedder(docs: Sequence[str], dim: int = 100, epochs: int = 10, window: int = 5, device="cpu",
+                    seed: int = 0):
+    """Document embedder trained on the corpus itself: skip-gram Word2Vec (negative sampling, on
+    ``device``) over the cleaned sentences of ``docs``; tokens outside its vocabulary fall back to
+    scaled hashing vectors.  Stands in for ssearch.py's spaCy-transformers BERT encoder
+    (P/app/ssearch.py:184-186), which needs pretrained weights this environment cannot fetch —
+    parity unpinned; the tests check retrieval quality on a seeded topical corpus instead."""
+    from .models import Word2Vec
+    sents = [clean_tokens(s) for d in docs for s in split_sentences(d)]
+    sents = [s for s in sents if s]
+    w2v = Word2Vec(dim=dim, window=window, epochs=epochs, seed=seed, device=device).fit(sents)
+    fallback = hashing_embedder(dim, seed)
+    W = w2v.W
+    scale = float(W.norm(dim=1).mean()) if W.numel() else 1.0
+
+    def emb(tokens):
+        if not tokens:
+            return torch.zeros((0, dim), device=W.device)
+        idx = [w2v.vocab.index.get(t, -1) for t in tokens]
+        out = torch.empty((len(tokens), dim), device=W.device)
+        known = [k for k, i in enumerate(idx) if i >= 0]
+        if known:
+            out[known] = W[torch.tensor([idx[k] for k in known], device=W.device)]
+        unk = [k for k, i in enumerate(idx) if i < 0]
+        if unk:
+            v = fallback([tokens[k] for k in unk]).to(W.device)
+            out[unk] = v / v.norm(dim=1, keepdim=True).clamp_min(1e-12) * scale
+        return out
+    emb.model = w2v
+    return emb
+
+
+def search_corpus(docs: Sequence[str], dim: int = 100, epochs: int = 10, device="cpu", seed: int = 0) -> SemanticSearch:
+    """A :class:`SemanticSearch` over ``docs`` with the corpus-trained embedder."""
+    ss = SemanticSearch(corpus_embedder(docs, dim, epochs, device=device, seed=seed), device=device)
+    for d in docs:
+        ss.add(d)
+    return ss

@@ -210,3 +210,25 @@ def test_score_model_generator(tmp_path):
     cols2, y = class_conditional([60, 40], {"status": [("cat", ["m", "s"], [100, 20]), ("cat", ["m", "s"], [20, 100])],
                                             "income": [("num", 120, 10), ("num", 80, 10)]}, 4000)
     assert float(cols2["income"][y == 0].mean()) > float(cols2["income"][y == 1].mean()) + 30
+
+
+def test_corpus_embedder_retrieval():
+    """Corpus-trained embedder (parity unpinned vs ssearch.py's BERT): queries made of topic words
+    retrieve documents of that topic."""
+    import random as _r
+    from avenir_amd.text.semsearch import search_corpus
+    rng = _r.Random(4)
+    topics = [[f"{p}{i}" for i in range(12)] for p in ("gpu", "fruit", "storm")]
+    docs, lab = [], []
+    for k in range(45):
+        t = k % 3
+        sents = [" ".join(rng.choice(topics[t]) for _ in range(8)) + "." for _ in range(4)]
+        docs.append(" ".join(sents))
+        lab.append(t)
+    ss = search_corpus(docs, dim=32, epochs=15, seed=1)
+    for t in range(3):
+        q = " ".join(topics[t][:3])
+        for algo in ("tokenAvMax", "docAv", "sentAv"):
+            top = ss.search(q, algo, top=5)
+            prec = sum(lab[i] == t for i, _ in top) / 5
+            assert prec >= 0.8, (t, algo, prec)
