@@ -413,6 +413,48 @@ void tree_predict(const at::Tensor& codes, int64_t n, const at::Tensor& feat, co
                     (int)mode, out.data_ptr<float>(), cur_stream(codes));
 }
 
+// Binary-split forest inference from LDS (forest_predict_bin_kernel).  nodes int32 [K, 2] packed
+// records (see tree.hip); validated on the host: feature / child ranges, leaves marked 255.
+void forest_predict_bin(const at::Tensor& codes, int64_t n, const at::Tensor& nodes, const at::Tensor& values,
+                        const at::Tensor& tree_root, const c10::optional<at::Tensor>& tree_w, int64_t mode,
+                        at::Tensor& out) {
+  check_codes(codes, n);
+  CHECK_DEV(nodes); CHECK_DTYPE(nodes, at::kInt);
+  CHECK_DEV(values); CHECK_DTYPE(values, at::kFloat);
+  CHECK_DEV(tree_root); CHECK_DTYPE(tree_root, at::kInt);
+  CHECK_DEV(out); CHECK_DTYPE(out, at::kFloat);
+  TORCH_CHECK(nodes.dim() == 2 && nodes.size(1) == 2 && nodes.is_contiguous(), "nodes [K, 2] int32");
+  const int64_t K = nodes.size(0);
+  TORCH_CHECK(K > 0 && K <= 65535 && values.dim() == 2 && values.size(0) == K, "values [K, V], K <= 65535");
+  const int V = (int)values.size(1);
+  TORCH_CHECK(V >= 1 && V <= 8 && out.numel() >= n * V, "1..8 outputs per row");
+  const int F = (int)codes.size(0);
+  TORCH_CHECK(F <= 255, "at most 255 features");
+  TORCH_CHECK(avk::forest_predict_bin_lds((int)K, F) <= 160 * 1024, "forest too large for the LDS kernel");
+  auto nc = nodes.cpu(), rc = tree_root.cpu();
+  const int* nd = nc.data_ptr<int>();
+  for (int64_t k = 0; k < K; ++k) {
+    const unsigned x = (unsigned)nd[2 * k], y = (unsigned)nd[2 * k + 1];
+    const unsigned f = x & 0xFF;
+    if (f == 0xFF) continue;
+    TORCH_CHECK((int)f < F && (y & 0xFFFF) < K && (y >> 16) < K, "forest node out of range");
+  }
+  for (int64_t t = 0; t < rc.numel(); ++t)
+    TORCH_CHECK(rc.data_ptr<int>()[t] >= 0 && rc.data_ptr<int>()[t] < K, "tree root out of range");
+  const float* tw = nullptr;
+  if (tree_w.has_value() && tree_w->defined()) {
+    CHECK_DEV((*tree_w)); CHECK_DTYPE((*tree_w), at::kFloat);
+    TORCH_CHECK(tree_w->numel() == tree_root.numel(), "one weight per tree");
+    tw = tree_w->data_ptr<float>();
+  }
+  auto vc = values.contiguous();
+  DevGuard g(codes.device());
+  avk::forest_predict_bin(codes.data_ptr<uint8_t>(), codes.size(1), n, F,
+                          reinterpret_cast<const uint2*>(nodes.data_ptr<int>()), (int)K, vc.data_ptr<float>(), V,
+                          tree_root.data_ptr<int>(), tw, (int)tree_root.numel(), (int)mode, out.data_ptr<float>(),
+                          cur_stream(codes));
+}
+
 // ---------------------------------------------------------------------------------------------
 // distance / kNN / clustering (K9/K11)
 // ---------------------------------------------------------------------------------------------
@@ -1540,6 +1582,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("forest_part_count", &forest_part_count);
   m.def("forest_part_scatter", &forest_part_scatter);
   m.def("forest_bootstrap", &forest_bootstrap);
+  m.def("forest_predict_bin", &forest_predict_bin);
   m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0);
   m.def("linear_act_bwd", &linear_act_bwd);
   m.def("lstm_ks", &lstm_ks);

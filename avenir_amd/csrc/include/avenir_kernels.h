@@ -163,6 +163,10 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
 int linear_act_bwd_blocks(int M);
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream);
+long long forest_predict_bin_lds(int n_nodes, int nfeat);
+void forest_predict_bin(const uint8_t* codes, long long ld, long long n, int nfeat, const uint2* nodes, int n_nodes,
+                        const float* values, int V, const int* tree_root, const float* tree_w, int n_trees, int mode,
+                        float* out, hipStream_t stream);
 void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
                        unsigned rate32, int* tile_cnt, hipStream_t stream);
 void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,

@@ -88,42 +88,67 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
   const int my_q = tid >> 2, part = tid & 3;
 
+  // A query block whose features fit one chunk is staged once; reference chunks are prefetched
+  // into registers one step ahead (the global loads of the next chunk / tile are in flight during
+  // the MFMAs and the top-k scan of the current one).
+  const bool q_once = D <= KC;
+  const int nchunk = (D + KC - 1) / KC;
+  float pr[BR * KC / KT];
+  auto load_r = [&](long long rr0, int dd0) {
+#pragma unroll
+    for (int i = 0; i < BR * KC / KT; ++i) {
+      const int e = tid + KT * i, row = e / KC, c = e % KC;
+      const long long r = rr0 + row;
+      pr[i] = (r < re && dd0 + c < D) ? R[r * D + dd0 + c] : 0.f;
+    }
+  };
+  if (q_once)
+    for (int e = tid; e < BQ * KC; e += KT) {
+      const int row = e / KC, c = e % KC;
+      const long long q = q0 + row;
+      sQ[row][c] = (q < M && c < D) ? Q[q * D + c] : 0.f;
+    }
+  if (rb < re) load_r(rb, 0);
   for (long long r0 = rb; r0 < re; r0 += BR) {
-    __syncthreads();
     const bool first_tile = r0 == rb;
     float rn_acc = 0.f;
     f32x16 acc;  // MET 0: the wave's 32 x 32 MFMA block; MET 1/2: this thread's 4 x 4 block
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     const int tq = tid >> 4, tr = tid & 15;  // VALU block: queries tq + 16 a, references tr + 16 b
-    for (int d0 = 0; d0 < D; d0 += KC) {
-      __syncthreads();
-      for (int e = tid; e < BQ * KC; e += KT) {
-        const int row = e / KC, c = e % KC;
-        const long long q = q0 + row;
-        sQ[row][c] = (q < M && d0 + c < D) ? Q[q * D + d0 + c] : 0.f;
-        const long long r = r0 + row;
-        sR[row][c] = (r < re && d0 + c < D) ? R[r * D + d0 + c] : 0.f;
+    for (int ci = 0; ci < nchunk; ++ci) {
+      const int d0 = ci * KC;
+      const int kend = min(KC, D - d0);
+      __syncthreads();  // previous chunk's (and tile's) LDS reads are done
+      if (!q_once)
+        for (int e = tid; e < BQ * KC; e += KT) {
+          const int row = e / KC, c = e % KC;
+          const long long q = q0 + row;
+          sQ[row][c] = (q < M && d0 + c < D) ? Q[q * D + d0 + c] : 0.f;
+        }
+#pragma unroll
+      for (int i = 0; i < BR * KC / KT; ++i) {
+        const int e = tid + KT * i;
+        sR[e / KC][e % KC] = pr[i];
       }
       __syncthreads();
+      if (ci + 1 < nchunk) load_r(r0, d0 + KC);
+      else if (r0 + BR < re) load_r(r0 + BR, 0);
       if constexpr (MET == 0) {
         if (tid < BR) {
-#pragma unroll 8
-          for (int c = 0; c < KC; ++c) rn_acc = fmaf(sR[tid][c], sR[tid][c], rn_acc);
+          for (int c = 0; c < kend; ++c) rn_acc = fmaf(sR[tid][c], sR[tid][c], rn_acc);
         } else if (first_tile && tid < BR + BQ) {
-#pragma unroll 8
-          for (int c = 0; c < KC; ++c) qn_acc = fmaf(sQ[tid - BR][c], sQ[tid - BR][c], qn_acc);
+          for (int c = 0; c < kend; ++c) qn_acc = fmaf(sQ[tid - BR][c], sQ[tid - BR][c], qn_acc);
         }
         const int li = lane & 31, lk = lane >> 5;
-#pragma unroll
-        for (int k = 0; k < KC; k += 2) {
+        const int kend2 = (kend + 1) & ~1;  // zero-padded odd tail
+        for (int k = 0; k < kend2; k += 2) {
           const float a = sQ[wq * 32 + li][k + lk];   // A[i = lane&31][k = lane>>5]
           const float b = sR[wr * 32 + li][k + lk];   // B[k = lane>>5][j = lane&31]
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
         }
       } else {
-        // zero-padded features contribute |0 - 0| = 0, so no tail guard is needed
-        for (int c = 0; c < KC; ++c) {
+        for (int c = 0; c < kend; ++c) {
           float qa[4], rv[4];
 #pragma unroll
           for (int a = 0; a < 4; ++a) qa[a] = sQ[tq + 16 * a][c];

@@ -202,6 +202,62 @@ __global__ __launch_bounds__(TB_THREADS) void tree_predict_kernel(
   }
 }
 
+
+// Binary-split forests (every internal node: code <= thr -> left, else right; the ForestBuilder /
+// binary DecisionTreeBuilder output): the node table of ALL trees sits in LDS as 8-byte records
+//   x = feat | thr << 8 | n_bins << 16   (feat 255 = leaf),   y = left | right << 16  (global ids)
+// and every thread first copies its row's F codes (coalesced column loads) into an LDS row slot,
+// so the traversal is LDS-only; per-tree node values (read once per tree at the stopping node)
+// come from global memory and the V outputs accumulate in registers, written once per row.
+// A code >= n_bins (missing / unseen) stops the walk at that node, as in tree_predict_kernel.
+constexpr int FPB_MAXV = 8;
+__global__ __launch_bounds__(TB_THREADS) void forest_predict_bin_kernel(
+    const uint8_t* __restrict__ codes, long long ld, long long n, int nfeat, const uint2* __restrict__ nodes,
+    int n_nodes, const float* __restrict__ values, int V, const int* __restrict__ tree_root,
+    const float* __restrict__ tree_w, int n_trees, int mode, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fp_smem[];
+  uint2* s_nodes = reinterpret_cast<uint2*>(fp_smem);
+  uint8_t* s_row = fp_smem + (size_t)n_nodes * sizeof(uint2) + threadIdx.x * nfeat;
+  for (int i = threadIdx.x; i < n_nodes; i += TB_THREADS) s_nodes[i] = nodes[i];
+  __syncthreads();
+  const long long stride = (long long)gridDim.x * TB_THREADS;
+  for (long long r = (long long)blockIdx.x * TB_THREADS + threadIdx.x; r < n; r += stride) {
+    for (int f = 0; f < nfeat; ++f) s_row[f] = codes[(long long)f * ld + r];
+    float acc[FPB_MAXV];
+#pragma unroll
+    for (int j = 0; j < FPB_MAXV; ++j) acc[j] = 0.f;
+    for (int t = 0; t < n_trees; ++t) {
+      int k = tree_root[t];
+      for (int guard = 0; guard < 256; ++guard) {
+        const uint2 nd = s_nodes[k];
+        const unsigned f = nd.x & 0xFF;
+        if (f == 0xFF) break;
+        const unsigned v = s_row[f];
+        if (v >= ((nd.x >> 16) & 0xFF)) break;
+        k = (int)(v <= ((nd.x >> 8) & 0xFF) ? (nd.y & 0xFFFF) : (nd.y >> 16));
+      }
+      const float* val = values + (long long)k * V;
+      const float w = tree_w ? tree_w[t] : 1.f;
+      if (mode == 0) {
+#pragma unroll
+        for (int j = 0; j < FPB_MAXV; ++j)
+          if (j < V) acc[j] += w * val[j];
+      } else {
+        int best = 0;
+        float bv = val[0];
+        for (int j = 1; j < V; ++j)
+          if (val[j] > bv) { bv = val[j]; best = j; }
+#pragma unroll
+        for (int j = 0; j < FPB_MAXV; ++j)
+          if (j == best) acc[j] += w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FPB_MAXV; ++j)
+      if (j < V) out[r * V + j] += acc[j];
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -258,6 +314,24 @@ void tree_predict(const uint8_t* codes, long long ld, long long n, const int* fe
   tree_predict_kernel<<<av::stream_grid(n, TB_THREADS, 2, 8192), TB_THREADS, 0, stream>>>(
       codes, ld, n, feat, seg_base, segmap, max_bins, child_base, child, leaf_idx, values, V,
       tree_root, tree_w, n_trees, mode, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+
+long long forest_predict_bin_lds(int n_nodes, int nfeat) {
+  return (long long)n_nodes * 8 + (long long)TB_THREADS * nfeat;
+}
+
+void forest_predict_bin(const uint8_t* codes, long long ld, long long n, int nfeat, const uint2* nodes, int n_nodes,
+                        const float* values, int V, const int* tree_root, const float* tree_w, int n_trees, int mode,
+                        float* out, hipStream_t stream) {
+  if (n <= 0 || n_trees <= 0) return;
+  const long long lds = forest_predict_bin_lds(n_nodes, nfeat);
+  if (lds > 160 * 1024 || V > FPB_MAXV) throw std::runtime_error("forest_predict_bin: forest too large for LDS");
+  AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(forest_predict_bin_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  forest_predict_bin_kernel<<<av::stream_grid(n, TB_THREADS, 1, 4096), TB_THREADS, (size_t)lds, stream>>>(
+      codes, ld, n, nfeat, nodes, n_nodes, values, V, tree_root, tree_w, n_trees, mode, out);
   AV_HIP_CHECK(hipGetLastError());
 }
 

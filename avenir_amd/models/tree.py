@@ -792,7 +792,35 @@ def flatten_forest(trees: Sequence[DecisionTree], device, weights: Sequence[floa
     }
     if weights is not None:
         out["tree_w"] = torch.tensor(list(weights), dtype=torch.float32, device=dev)
+    bn = _binary_nodes(trees)
+    if bn is not None:
+        out["bin_nodes"] = torch.tensor(bn, dtype=torch.int64).to(torch.int32).to(dev)
     return out
+
+
+def _binary_nodes(trees: Sequence[DecisionTree]) -> list | None:
+    """Packed [K, 2] records of ``forest_predict_bin_kernel`` when every internal node is a
+    threshold split (segments 0..0 1..1 over the feature's bins, two children) and the forest fits
+    the record fields (features < 255, bins <= 255, < 65536 nodes); None otherwise."""
+    recs = []
+    for tr in trees:
+        base = len(recs)
+        for nd in tr.nodes:
+            if nd.is_leaf or not nd.children:
+                recs.append([0xFF, 0])
+                continue
+            nb = tr.space[nd.feature].n_bins
+            sm = list(nd.segmap)
+            thr = sum(1 for g in sm if g == 0) - 1
+            if (len(nd.children) != 2 or min(nd.children) < 0 or nd.feature >= 255 or nb > 255 or thr < 0
+                    or sm != [0] * (thr + 1) + [1] * (len(sm) - thr - 1) or len(sm) != nb):
+                return None
+            left, right = nd.children[0] + base, nd.children[1] + base
+            recs.append([nd.feature | (thr << 8) | (nb << 16), left | (right << 16)])
+    if len(recs) > 65535:
+        return None
+    # int32 view of the unsigned record words
+    return [[x - (1 << 32) if x >= (1 << 31) else x for x in r] for r in recs]
 
 
 class TreeEnsemble:

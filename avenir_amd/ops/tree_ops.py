@@ -102,6 +102,12 @@ def tree_predict(codes: torch.Tensor, n: int, forest: dict, mode: int = 0) -> to
     out = torch.zeros((max(n, 1), V), dtype=torch.float32, device=codes.device)
     if n == 0:
         return out[:0]
+    if codes.is_cuda and "bin_nodes" in forest and V <= 8 and codes.shape[0] <= 255 and \
+            forest["bin_nodes"].shape[0] * 8 + 256 * codes.shape[0] <= 160 * 1024:
+        # threshold-split forests: node table of all trees in LDS, register accumulation
+        _native.C().forest_predict_bin(codes, int(n), forest["bin_nodes"], forest["values"], forest["tree_root"],
+                                       forest.get("tree_w"), int(mode), out)
+        return out[:n]
     if codes.is_cuda:
         _native.C().tree_predict(codes, int(n), forest["feat"], forest["seg_base"], forest["segmap"],
                                  forest["child_base"], forest["child"], forest["leaf_idx"],

@@ -239,3 +239,26 @@ def test_bucketize_kernel_matches_torch(cuda, tmp_path):
     c_cpu = T.encode_for_tree(space, t)
     c_gpu = T.encode_for_tree(space, tg)
     assert torch.equal(c_gpu.cpu(), c_cpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_binary_forest_predict_kernel(cuda, tmp_path, mode):
+    """LDS binary-forest inference == generic tree_predict kernel == CPU traversal (incl. missing codes)."""
+    from avenir_amd.ops import tree_ops as TO
+    schema, t = _table(tmp_path, 6000, 11)
+    prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=7, attr_selection="all",
+                       sub_sampling="withReplace", seed=2)
+    space = T.build_split_space(schema, t, binary=True, max_bins=prm.max_bins)
+    trees = ForestBuilder(schema, 5, prm).fit(t, space=space)
+    codes = T.encode_for_tree(space, t).clone()
+    codes[1, ::7] = 255                                     # missing values stop the walk
+    flat_c = T.flatten_forest(trees, "cpu", weights=[1.0, 0.5, 2.0, 1.0, 1.5])
+    assert "bin_nodes" in flat_c
+    ref = TO.tree_predict(codes, t.n, flat_c, mode=mode)
+    flat_g = T.flatten_forest(trees, cuda, weights=[1.0, 0.5, 2.0, 1.0, 1.5])
+    got = TO.tree_predict(codes.to(cuda), t.n, flat_g, mode=mode)
+    generic = dict(flat_g)
+    generic.pop("bin_nodes")
+    gen = TO.tree_predict(codes.to(cuda), t.n, generic, mode=mode)
+    assert torch.allclose(got.cpu(), ref, atol=1e-5) and torch.allclose(gen.cpu(), ref, atol=1e-5)
