@@ -26,6 +26,22 @@ constexpr int KC = 32;    // feature chunk staged in LDS (multiple of 2: MFMA K 
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+template <int N>
+__device__ __forceinline__ float sq_norm(const float* __restrict__ row, float acc) {
+#pragma unroll
+  for (int c = 0; c < N; ++c) acc = fmaf(row[c], row[c], acc);
+  return acc;
+}
+
+// A[i = lane&31][k = lane>>5] from the query row, B[k = lane>>5][j = lane&31] from the reference row
+template <int N>
+__device__ __forceinline__ f32x16 mfma_chunk(const float* __restrict__ qrow, const float* __restrict__ rrow, int lk,
+                                             f32x16 acc) {
+#pragma unroll
+  for (int k = 0; k < N; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qrow[k + lk], rrow[k + lk], acc, 0, 0, 0);
+  return acc;
+}
+
 template <int K>
 __device__ __forceinline__ void topk_insert(float (&bd)[K], int (&bi)[K], float d, int j) {
   if (d < bd[K - 1]) {
@@ -135,18 +151,17 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       if (ci + 1 < nchunk) load_r(r0, d0 + KC);
       else if (r0 + BR < re) load_r(r0 + BR, 0);
       if constexpr (MET == 0) {
+        // fully unrolled over a half or a whole chunk (zero-padded features add exact zeros):
+        // all LDS operand reads issue ahead of the back-to-back MFMAs
+        const bool half = kend <= KC / 2;
         if (tid < BR) {
-          for (int c = 0; c < kend; ++c) rn_acc = fmaf(sR[tid][c], sR[tid][c], rn_acc);
+          rn_acc = half ? sq_norm<KC / 2>(sR[tid], rn_acc) : sq_norm<KC>(sR[tid], rn_acc);
         } else if (first_tile && tid < BR + BQ) {
-          for (int c = 0; c < kend; ++c) qn_acc = fmaf(sQ[tid - BR][c], sQ[tid - BR][c], qn_acc);
+          qn_acc = half ? sq_norm<KC / 2>(sQ[tid - BR], qn_acc) : sq_norm<KC>(sQ[tid - BR], qn_acc);
         }
         const int li = lane & 31, lk = lane >> 5;
-        const int kend2 = (kend + 1) & ~1;  // zero-padded odd tail
-        for (int k = 0; k < kend2; k += 2) {
-          const float a = sQ[wq * 32 + li][k + lk];   // A[i = lane&31][k = lane>>5]
-          const float b = sR[wr * 32 + li][k + lk];   // B[k = lane>>5][j = lane&31]
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-        }
+        if (half) acc = mfma_chunk<KC / 2>(sQ[wq * 32 + li], sR[wr * 32 + li], lk, acc);
+        else acc = mfma_chunk<KC>(sQ[wq * 32 + li], sR[wr * 32 + li], lk, acc);
       } else {
         for (int c = 0; c < kend; ++c) {
           float qa[4], rv[4];

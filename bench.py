@@ -20,6 +20,8 @@ CSV parsing and packing are NOT in the timed steps (the headline is the on-devic
 * ``columns_rows_per_s_per_gpu`` — the same training step over the uint8 code columns.
 * ``ingest`` (1 GPU by default, ``--ingest-rows``) — the end-to-end job time for a CSV file of
   ``2^26`` records written beforehand: native K1 parse -> device -> fit -> model text lines.
+* ``rccl_all_reduce`` (more than one GPU) — all-reduce latency at 8 KB and bus bandwidth at
+  1 MB / 64 MB over the job's GPUs.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows-per-gpu R] [--layout L]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -43,6 +45,26 @@ def _timed(fn, dev) -> float:
     if dev.type == "cuda":
         torch.cuda.synchronize()
     return time.perf_counter() - t0
+
+
+def _allreduce_probe(comm, dev) -> list:
+    """RCCL all-reduce over this job's GPUs (outside the timed steps): latency of a KB-scale
+    count-table-sized message and bus bandwidth (algbw x 2(n-1)/n) at 1 MB and 64 MB."""
+    import torch.distributed as dist
+    out = []
+    W = comm.world
+    for nbytes, iters in ((8 << 10, 50), (1 << 20, 20), (64 << 20, 10)):
+        x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+        for _ in range(3):
+            dist.all_reduce(x)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier()
+        t = _timed(lambda: [dist.all_reduce(x) for _ in range(iters)], dev) / iters
+        t = comm.reduce_max_scalar(t)
+        alg = nbytes / t / 1e9
+        out.append({"bytes": nbytes, "us": t * 1e6, "algbw_GBps": alg, "busbw_GBps": alg * 2 * (W - 1) / W})
+    return out
 
 
 def _ingest(rows: int, schema, dev, comm) -> dict:
@@ -93,6 +115,8 @@ def main() -> int:
     ap.add_argument("--layout", choices=["rowpacked", "columns"], default="rowpacked",
                     help="device layout of the encoded records: one 16-bit word per record "
                          "(2 B/record) or one uint8 column per feature + label (6 B/record)")
+    ap.add_argument("--probe-allreduce", action="store_true",
+                    help="run the all-reduce probe on any device (it runs by default on >1 GPU)")
     ap.add_argument("--ingest-rows", type=int, default=-1,
                     help="rows of the ingest-inclusive CSV measurement (0 = skip; default 2^26 on "
                          "a single GPU, skipped on more)")
@@ -168,6 +192,11 @@ def main() -> int:
         extra["columns_rows_per_s_per_gpu"] = n * k / t1
         extra["columns_hbm_gbps_per_gpu"] = n * (codes.shape[0] + 1) * k / t1 / 1e9
         table.rowpack = rp
+    if comm.world > 1 and (dev.type == "cuda" or args.probe_allreduce):
+        try:
+            extra["rccl_all_reduce"] = _allreduce_probe(comm, dev)
+        except Exception as e:      # a probe failure must not lose the measured headline
+            extra["rccl_all_reduce"] = {"error": repr(e)}
     ingest_rows = args.ingest_rows if args.ingest_rows >= 0 else ((1 << 26) if comm.world == 1 else 0)
     if ingest_rows > 0 and (dev.type == "cuda" or args.ingest_rows > 0):
         extra["ingest"] = _ingest(ingest_rows, schema, dev, comm)

@@ -58,6 +58,9 @@ def main(root):
                 der["lds_bank_conflict_cycles_per_lds_inst"] = per.get("SQ_LDS_BANK_CONFLICT", 0) / per["SQ_INSTS_LDS"]
             if t and per.get("GRBM_GUI_ACTIVE"):
                 der["effective_clock_GHz"] = per["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
+                # SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves: x4 / (1024 SIMDs x the
+                # kernel's cycles per XCD) = fraction of SIMD cycles issuing VALU (1.0 = issue-bound)
+                der["valu_busy_per_simd"] = per.get("SQ_ACTIVE_INST_VALU", 0) * 4 / (1024 * per["GRBM_GUI_ACTIVE"] / 8)
             if t and per.get("SQ_VALU_MFMA_BUSY_CYCLES") and per.get("GRBM_GUI_ACTIVE"):
                 # MFMA busy cycles summed over 1024 SIMDs vs the kernel's active cycles per XCD
                 der["mfma_busy_frac"] = per["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * per["GRBM_GUI_ACTIVE"] / 8)
