@@ -102,7 +102,10 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   int bi[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
-  const int my_q = tid >> 2, part = tid & 3;
+  // top-k owner of each (query, partial list): MET 0 takes candidates straight from the MFMA
+  // accumulator (lane = one query column, 16 reference rows), the VALU metrics from the sD tile
+  const int my_q = MET == 0 ? (wq * 32 + (lane & 31)) : (tid >> 2);
+  const int part = MET == 0 ? (wr * 2 + (lane >> 5)) : (tid & 3);
 
   // A query block whose features fit one chunk is staged once; reference chunks are prefetched
   // into registers one step ahead (the global loads of the next chunk / tile are in flight during
@@ -151,8 +154,9 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       if (ci + 1 < nchunk) load_r(r0, d0 + KC);
       else if (r0 + BR < re) load_r(r0 + BR, 0);
       if constexpr (MET == 0) {
-        // fully unrolled over a half or a whole chunk (zero-padded features add exact zeros):
-        // all LDS operand reads issue ahead of the back-to-back MFMAs
+        // norms over a half or a whole chunk; the MFMA chain always covers the whole (zero-padded)
+        // chunk: a second, half-length unrolled chain cost more in VGPRs / occupancy than the
+        // skipped MFMAs saved (measured at D = 16 and 32)
         const bool half = kend <= KC / 2;
         if (tid < BR) {
           rn_acc = half ? sq_norm<KC / 2>(sR[tid], rn_acc) : sq_norm<KC>(sR[tid], rn_acc);
@@ -160,8 +164,9 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
           qn_acc = half ? sq_norm<KC / 2>(sQ[tid - BR], qn_acc) : sq_norm<KC>(sQ[tid - BR], qn_acc);
         }
         const int li = lane & 31, lk = lane >> 5;
-        if (half) acc = mfma_chunk<KC / 2>(sQ[wq * 32 + li], sR[wr * 32 + li], lk, acc);
-        else acc = mfma_chunk<KC>(sQ[wq * 32 + li], sR[wr * 32 + li], lk, acc);
+        // A = references (rows of the 32 x 32 block), B = queries (columns): each lane's 16
+        // accumulators are 16 reference distances of ONE query
+        acc = mfma_chunk<KC>(sR[wr * 32 + li], sQ[wq * 32 + li], lk, acc);
       } else {
         for (int c = 0; c < kend; ++c) {
           float qa[4], rv[4];
@@ -183,19 +188,18 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       if (tid < BR) srn[tid] = rn_acc;
       else if (first_tile && tid < BR + BQ) sqn[tid - BR] = qn_acc;
       __syncthreads();
-      // accumulator -> squared distances in LDS (C/D map: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5))
-      const int col = lane & 31;
-      const long long rj = r0 + wr * 32 + col;
-#pragma unroll
+      // accumulator -> distances -> this lane's top-k, no LDS round trip
+      // (C/D map: col = lane&31 = query, row = (r&3) + 8(r>>2) + 4(lane>>5) = reference)
+      const float qn = sqn[my_q];
+      const long long gq = q0 + my_q;
+#pragma unroll 2
       for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int qi = wq * 32 + row;
-        float dist = sqn[qi] + srn[wr * 32 + col] - 2.f * acc[r];
-        dist = fmaxf(dist, 0.f);
-        const long long gq = q0 + qi;
-        if (rj >= re || gq >= M) dist = INFINITY;
-        if (exclude_self && (q_index_base + gq) == (r_index_base + rj)) dist = INFINITY;
-        sD[qi][wr * 32 + col] = dist;
+        const int rj = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const long long gr = r0 + rj;
+        float dist = fmaxf(qn + srn[rj] - 2.f * acc[r], 0.f);
+        if (gr >= re || gq >= M) dist = INFINITY;
+        if (exclude_self && (q_index_base + gq) == (r_index_base + gr)) dist = INFINITY;
+        topk_insert<K>(bd, bi, dist, (int)(r0 - rb) + rj);
       }
     } else {
 #pragma unroll
@@ -210,11 +214,13 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
           sD[qi][rj] = dist;
         }
     }
-    __syncthreads();
+    if constexpr (MET != 0) {
+      __syncthreads();
 #pragma unroll 4
-    for (int c = 0; c < 16; ++c) {
-      const int j = part * 16 + c;
-      topk_insert<K>(bd, bi, sD[my_q][j], (int)(r0 - rb) + j);
+      for (int c = 0; c < 16; ++c) {
+        const int j = part * 16 + c;
+        topk_insert<K>(bd, bi, sD[my_q][j], (int)(r0 - rb) + j);
+      }
     }
   }
   __syncthreads();  // the merge lists alias the tiles

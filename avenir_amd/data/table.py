@@ -28,6 +28,7 @@ import torch
 
 from .. import _native
 from ..utils.schema import FeatureField, FeatureSchema
+from ..utils.tracing import traced
 
 CAT, BUCKET, FLOAT, INT = 0, 1, 2, 3
 MISSING = 255
@@ -253,6 +254,7 @@ class LazyColumn(Sequence):
         return list(self._get()) == list(other)
 
 
+@traced("data.load_csv", nbytes=lambda path, *a, **k: os.path.getsize(path))
 def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
              world: int = 1, device: str | torch.device = "cpu", keep_lines: bool = False,
              skip_header: bool = False, nthreads: int | None = None, feature_ordinals: Sequence[int] | None = None,

@@ -34,6 +34,7 @@ from ..ops import histogram as H
 from ..parallel.comm import Comm, get_comm
 from ..utils.metrics import ConfusionMatrix, Counters
 from ..utils.schema import FeatureSchema
+from ..utils.tracing import traced
 
 _LOG_FLOOR = math.log(1e-12)
 
@@ -64,6 +65,7 @@ class NaiveBayes:
     # ----------------------------------------------------------------------------------------
     # training
     # ----------------------------------------------------------------------------------------
+    @traced("nb.fit", nbytes=lambda self, t, *a, **k: t.n * (t.codes.shape[0] + 1), device=lambda self, t, *a, **k: t.device)
     def fit(self, t: Table, reduce: bool = True) -> "NaiveBayes":
         """Count on this rank's shard, then all-reduce across ranks."""
         comm = self.comm or get_comm()
@@ -187,6 +189,7 @@ class NaiveBayes:
     # ----------------------------------------------------------------------------------------
     # inference
     # ----------------------------------------------------------------------------------------
+    @traced("nb.predict", nbytes=lambda self, t, *a, **k: t.n * (t.codes.shape[0] + 1), device=lambda self, t, *a, **k: t.device)
     def predict(self, t: Table, ref_scale: bool = False, with_prob: bool = True,
                 validate: bool = True) -> NBPrediction:
         tb = self.tables(t.device)

@@ -21,6 +21,7 @@ import torch
 
 from .. import _native
 from ..parallel.comm import Comm, get_comm
+from ..utils.tracing import traced
 
 
 def kernel_matrix(A: torch.Tensor, B: torch.Tensor, kernel: str = "rbf", gamma: float = 1.0, degree: int = 3,
@@ -259,6 +260,7 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
 WS_MIN_N = 4096   # above this the working-set solver beats the single-workgroup full SMO (bench_svm.py)
 
 
+@traced("svm.smo", nbytes=lambda K, *a, **k: K.numel() * K.element_size(), device=lambda K, *a, **k: K.device)
 def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_iter: int = 1_000_000,
               solver: str = "auto"):
     """Solve B SVM duals: K [B, N, N], y [B, N] in {-1, 0 (padding), +1}.  Returns (alpha, rho, iters).

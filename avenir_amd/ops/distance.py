@@ -8,6 +8,7 @@ import torch
 
 from .. import _native
 from ..data.table import MISSING, Table
+from ..utils.tracing import traced
 
 _MFMA_METRICS = ("euclidean", "sqeuclidean", "cosine")
 _KMAX = 64          # largest k of the fused kernel (register-resident sorted lists)
@@ -44,6 +45,7 @@ def _cpu_topk(Q, R, k, metric, p, exclude_self, q_base, r_base, chunk=4096):
     return torch.cat(ds), torch.cat(ix)
 
 
+@traced("knn", flops=lambda Q, R, *a, **k: 2.0 * Q.shape[0] * R.shape[0] * Q.shape[1], device=lambda Q, *a, **k: Q.device)
 def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: float = 2.0,
         exclude_self: bool = False, q_base: int = 0, r_base: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
     """k nearest references of every query: (dist float32 [M, k] ascending, idx int64 [M, k]);

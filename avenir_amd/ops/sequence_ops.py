@@ -6,8 +6,10 @@ import numpy as np
 import torch
 
 from .. import _native
+from ..utils.tracing import traced
 
 
+@traced("viterbi", nbytes=lambda obs, *a, **k: obs.numel() * obs.element_size(), device=lambda obs, *a, **k: obs.device)
 def viterbi(obs: torch.Tensor, logA: torch.Tensor, logB: torch.Tensor, logpi: torch.Tensor,
             forward: bool = False) -> tuple[torch.Tensor | None, torch.Tensor]:
     """Batched log-space Viterbi (path int16 [N, T], -1 padded; score [N]) or, with ``forward``,

@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from ..utils import logging as alog
+from ..utils.tracing import traced
 
 _COMM: "Comm | None" = None
 
@@ -91,6 +92,7 @@ class Comm:
         return t, False
 
     # ------------------------------------------------------------------------------------------
+    @traced("comm.all_reduce", nbytes=lambda self, t, *a, **k: t.numel() * t.element_size(), device=lambda self, t, *a, **k: t.device)
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         """In-place all-reduce (sum|max|min|prod); returns ``t``."""
         if not self.is_distributed:
@@ -146,6 +148,7 @@ class Comm:
         dist.all_gather_object(out, obj)
         return out
 
+    @traced("comm.all_gather", nbytes=lambda self, t, *a, **k: t.numel() * t.element_size() * self.world, device=lambda self, t, *a, **k: t.device)
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Equal-shape all-gather -> [world, *t.shape]."""
         if not self.is_distributed:

@@ -91,6 +91,29 @@ def trace(name: str, nbytes: float = 0.0, flops: float = 0.0, device=None):
     return TRACER.range(name, nbytes, flops, device)
 
 
+def traced(name: str, nbytes=None, flops=None, device=None):
+    """Decorator form: ``@traced("nb.fit", nbytes=lambda self, t, *a, **k: t.n * 6)``.  The byte /
+    FLOP callables and ``device`` (a callable too) see the call's arguments; disabled tracing
+    costs one attribute check per call."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(*args, **kw):
+            if not TRACER.enabled:
+                return fn(*args, **kw)
+            try:
+                nb = float(nbytes(*args, **kw)) if nbytes else 0.0
+                fl = float(flops(*args, **kw)) if flops else 0.0
+                dv = device(*args, **kw) if device else None
+            except Exception:
+                nb, fl, dv = 0.0, 0.0, None
+            with TRACER.range(name, nb, fl, dv):
+                return fn(*args, **kw)
+        return wrapper
+    return deco
+
+
 @contextlib.contextmanager
 def torch_profile(path: str | None = None, cuda: bool | None = None):
     """torch.profiler wrapper for the NN paths; writes a Chrome trace when ``path`` is given."""

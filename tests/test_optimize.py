@@ -261,7 +261,10 @@ def test_sa_kernel_task_schedule(cuda, task_domain):
     lb = float(d.cost_table.min(1).values.mean())
     r = SimulatedAnnealing(d, n_chains=4096, iters=500, t0=2.0, cooling=0.98, interval=4).run()
     assert r.best.device.type == "cuda"
-    assert r.best_cost == pytest.approx(lb, abs=1e-3)
+    # the per-task minimum ignores the employee conflicts, so it bounds the optimum from below
+    assert lb - 1e-3 <= r.best_cost <= lb * 1.01
+    assert float(d.cost(r.best.view(1, -1))[0]) == pytest.approx(r.best_cost, rel=1e-5)
+    assert bool(d.valid(r.best.view(1, -1))[0])
 
 
 def _sa_segments(d, sol, cost, seg, total=300):
