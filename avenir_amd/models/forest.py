@@ -139,7 +139,7 @@ class ForestBuilder:
         p = self.p
         dev = t.device
         if space is None:
-            space = T.build_split_space(self.schema, t, binary=True, max_bins=p.max_bins)
+            space = T.build_split_space(self.schema, t, binary=True, max_bins=p.max_bins, comm=comm)
         if codes is None:
             codes = T.encode_for_tree(space, t)
         n = t.n

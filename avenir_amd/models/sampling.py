@@ -107,21 +107,61 @@ class AdaBoost:
 def relief(X: torch.Tensor, y: torch.Tensor, k: int = 1, ranges: torch.Tensor | None = None,
            comm: Comm | None = None) -> torch.Tensor:
     """Relief feature relevance [D]: sum over records of (miss diff - hit diff) / n, diffs normalised
-    by the attribute range."""
+    by the attribute range.  With row shards on several ranks the neighbours are searched over ALL
+    ranks' records (one all-gather of the shard, as TopMatchesByClass joins every pair) and the
+    ranges are global, so the score equals the single-process one."""
+    comm = comm or get_comm()
     X = X.float()
-    rng = (X.max(0).values - X.min(0).values) if ranges is None else ranges.float().to(X.device)
+    dist_mode = comm.is_distributed
+    if dist_mode:
+        dev = comm.device if comm.backend == "nccl" else torch.device("cpu")
+        Xa = comm.all_gather_v(X.to(dev)).to(X.device)
+        ya = comm.all_gather_v(y.to(dev).long()).to(X.device)
+        sizes = comm.all_gather(torch.tensor([X.shape[0]], dtype=torch.long, device=dev)).view(-1).tolist()
+        base = int(sum(sizes[:comm.rank]))
+    else:
+        Xa, ya, base = X, y, 0
+    rng = (Xa.max(0).values - Xa.min(0).values) if ranges is None else ranges.float().to(X.device)
     rng = rng.clamp_min(1e-12)
-    _, hit = top_matches_by_class(X, y, k, same_class=True)
-    _, miss = top_matches_by_class(X, y, k, same_class=False)
+    if dist_mode:
+        hit, miss = _global_matches(X, y.long(), Xa, ya, base, k)
+    else:
+        _, hit = top_matches_by_class(X, y, k, same_class=True)
+        _, miss = top_matches_by_class(X, y, k, same_class=False)
     score = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
     for j in range(k):
         h, m = hit[:, j], miss[:, j]
         okh, okm = h >= 0, m >= 0
-        score -= ((X[okh] - X[h[okh]]).abs() / rng).double().sum(0)
-        score += ((X[okm] - X[m[okm]]).abs() / rng).double().sum(0)
+        score -= ((X[okh] - Xa[h[okh]]).abs() / rng).double().sum(0)
+        score += ((X[okm] - Xa[m[okm]]).abs() / rng).double().sum(0)
     n = torch.tensor([float(X.shape[0] * k)], dtype=torch.float64, device=X.device)
-    comm = comm or get_comm()
-    if comm.is_distributed:
+    if dist_mode:
         comm.all_reduce(score)
         comm.all_reduce(n)
     return (score / n).float()
+
+
+def _global_matches(X, y, Xa, ya, base: int, k: int):
+    """Nearest same-class (hits, self excluded by global id) and other-class (misses) records of
+    this rank's rows among all records: global row ids [n, k] (-1 when fewer)."""
+    from ..ops import distance as dist
+    n = X.shape[0]
+    hit = torch.full((n, k), -1, dtype=torch.long, device=X.device)
+    miss = torch.full((n, k), -1, dtype=torch.long, device=X.device)
+    for c in torch.unique(ya).tolist():
+        qi = torch.nonzero(y == c).squeeze(1)
+        if qi.numel() == 0:
+            continue
+        ri = torch.nonzero(ya == c).squeeze(1)
+        if ri.numel():
+            _, i = dist.knn(X[qi], Xa[ri], min(k + 1, ri.numel()))
+            gi = torch.where(i >= 0, ri[i.clamp_min(0)], i)
+            keep = (gi != (qi + base).view(-1, 1)) & (gi >= 0)                  # drop self
+            slot = keep.long().cumsum(1) - 1
+            rr, cc = torch.nonzero(keep & (slot < k), as_tuple=True)
+            hit[qi[rr], slot[rr, cc]] = gi[rr, cc]
+        ro = torch.nonzero(ya != c).squeeze(1)
+        if ro.numel():
+            _, i = dist.knn(X[qi], Xa[ro], k)
+            miss[qi] = torch.where(i >= 0, ro[i.clamp_min(0)], i)
+    return hit, miss

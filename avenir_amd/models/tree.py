@@ -179,10 +179,13 @@ def numeric_splits(fs: FeatureSplits, max_split: int | None = None, cap: int = 4
 
 
 def build_split_space(schema: FeatureSchema, t: Table | None = None, attrs: Sequence[int] | None = None,
-                      binary: bool = False, max_bins: int = 32) -> list[FeatureSplits]:
+                      binary: bool = False, max_bins: int = 32, comm=None) -> list[FeatureSplits]:
     """Candidate-split space over the feature attributes (reference SplitManager semantics, or
-    binary threshold splits over ordered fine bins when ``binary``)."""
+    binary threshold splits over ordered fine bins when ``binary``).  With ``comm`` distributed and
+    row shards, data-quantile split points come from the values of ALL ranks (one all-gather per
+    numeric column of at most 2^20 / world sampled values each), so every rank bins identically."""
     out = []
+    gather = comm is not None and comm.is_distributed
     for f in schema.feature_fields:
         if attrs is not None and f.ordinal not in attrs:
             continue
@@ -196,6 +199,9 @@ def build_split_space(schema: FeatureSchema, t: Table | None = None, attrs: Sequ
                 names = [x.ordinal for x in t.numeric_fields]
                 if f.ordinal in names:
                     vals = t.numeric[names.index(f.ordinal), : t.n]
+                    if gather and (binary or not (f.min is not None and f.max is not None
+                                                  and f.split_scan_interval)):
+                        vals = _gather_sample(vals, comm)
             if binary or not (f.min is not None and f.max is not None and f.split_scan_interval):
                 pts = numeric_points(FeatureField(f.name, f.ordinal, f.data_type), vals, max_bins)
             else:
@@ -209,6 +215,14 @@ def build_split_space(schema: FeatureSchema, t: Table | None = None, attrs: Sequ
             raise ValueError(f"attribute {f.name}: {fs.n_bins} fine bins > 254")
         out.append(fs)
     return out
+
+
+def _gather_sample(vals: torch.Tensor, comm) -> torch.Tensor:
+    """This rank's column values (strided to <= 2^20 / world when larger) gathered from all ranks."""
+    cap = max(1, (1 << 20) // comm.world)
+    v = vals[:: (vals.numel() + cap - 1) // cap] if vals.numel() > cap else vals
+    dev = comm.device if comm.backend == "nccl" else torch.device("cpu")
+    return comm.all_gather_v(v.float().contiguous().to(dev)).to(vals.device)
 
 
 def _with_total_row(codes: torch.Tensor, n: int) -> torch.Tensor:
@@ -528,7 +542,7 @@ class DecisionTreeBuilder:
         seed = p.seed if tree_seed is None else tree_seed
         rng = random.Random(seed)  # identical on every rank
         if self.space is None:
-            self.space = build_split_space(self.schema, t, binary=p.binary, max_bins=p.max_bins)
+            self.space = build_split_space(self.schema, t, binary=p.binary, max_bins=p.max_bins, comm=comm)
         space = self.space
         if codes is None:
             codes = encode_for_tree(space, t)
@@ -898,7 +912,9 @@ class RandomForest:
 
     def fit(self, t: Table) -> "RandomForest":
         comm = self.comm or get_comm()
-        space = build_split_space(self.schema, t, binary=self.params.binary, max_bins=self.params.max_bins)
+        # tree-parallel ranks hold every row; data-parallel ranks bin on globally gathered samples
+        space = build_split_space(self.schema, t, binary=self.params.binary, max_bins=self.params.max_bins,
+                                  comm=None if self.tree_parallel else comm)
         codes = encode_for_tree(space, t)
         import copy
         my_trees = range(self.n_trees)
@@ -1091,7 +1107,7 @@ class GradientBoostedTrees:
     def fit(self, t: Table) -> "GradientBoostedTrees":
         comm = self.comm or get_comm()
         p = self.p
-        self.space = build_split_space(self.schema, t, binary=True, max_bins=p.max_bins)
+        self.space = build_split_space(self.schema, t, binary=True, max_bins=p.max_bins, comm=comm)
         codes = encode_for_tree(self.space, t)
         codes = _with_total_row(codes, t.n)
         bins = [fs.n_bins for fs in self.space] + [1]

@@ -96,6 +96,20 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx):
     lo = rank * 2000 // world
     d, i = D.distributed_knn(Q, _shard(X, rank, world).contiguous(), 5, comm, r_base=lo)
     out["knn"] = (d.tolist(), i.tolist())
+    # ---- cascade SVM (same global shard partition at every world size), Relief, GBT -----------
+    from avenir_amd.models.sampling import relief
+    from avenir_amd.models.svm import CascadeSVM
+    gs = torch.Generator().manual_seed(12)
+    Xs = torch.randn(640, 2, generator=gs)
+    ys = (Xs[:, 0] * Xs[:, 1] > 0).long()
+    cs_ = CascadeSVM(shards=8 // world, comm=comm, gamma=0.5, C=1.0).fit(_shard(Xs, rank, world), _shard(ys, rank, world))
+    probe = torch.randn(64, 2, generator=gs)
+    out["cascade"] = (cs_.n_cascade_sv, cs_.decision_function(probe).tolist())
+    Xr = torch.randn(600, 5, generator=gs)
+    yr = ((Xr[:, 0] + 0.5 * Xr[:, 3]) > 0).long()
+    out["relief"] = relief(_shard(Xr, rank, world), _shard(yr, rank, world), k=2, comm=comm).tolist()
+    gbt = T.GradientBoostedTrees(hs, T.GBTParams(n_estimators=6, max_depth=3, max_bins=32), comm=comm).fit(th)
+    out["gbt"] = gbt.decision_function(full).tolist()
     # ---- sequence parallel Viterbi -----------------------------------------------------------
     gh = torch.Generator().manual_seed(9)
     norm = lambda mm: torch.log(mm / mm.sum(-1, keepdim=True))
@@ -126,6 +140,10 @@ def test_world_size_equivalence(reference, world):
         assert np.allclose(got["knn"][0], ref["knn"][0], atol=1e-5)
         assert got["knn"][1] == ref["knn"][1]
         assert got["viterbi"][1] == pytest.approx(ref["viterbi"][1], rel=1e-9)
+        assert got["cascade"][0] == ref["cascade"][0]
+        assert np.allclose(got["cascade"][1], ref["cascade"][1], atol=1e-5)
+        assert np.allclose(got["relief"], ref["relief"], rtol=1e-6, atol=1e-7)
+        assert np.allclose(got["gbt"], ref["gbt"], rtol=1e-6, atol=1e-6)
     # Viterbi is sequence-parallel: the rank segments concatenate to the single-rank path
     assert sum((g["viterbi"][0] for g in res), []) == ref["viterbi"][0]
 
