@@ -178,3 +178,36 @@ def test_cli_map_output_per_rank(tmp_path, world):
     assert [r.rsplit(",", 2)[0] for r in rows] == src
     single = [l for l in out_file.read_text().splitlines() if l]
     assert single == rows
+
+
+def _domain():
+    from avenir_amd.optimize.domain import AssignmentDomain
+    g = torch.Generator().manual_seed(21)
+    cost = torch.rand((20, 8), generator=g) * 100
+    conf = torch.rand((20, 20), generator=g) < 0.12
+    return AssignmentDomain(cost, conf | conf.T, invalid_cost=1e3)
+
+
+def _optimisers(rank, world, seed):
+    from avenir_amd.optimize.search import GeneticAlgorithm, SimulatedAnnealing
+    from avenir_amd.parallel.comm import get_comm
+    comm = get_comm()
+    sa = SimulatedAnnealing(_domain(), n_chains=16, iters=200, t0=5.0, cooling=0.97, seed=seed, comm=comm).run()
+    ga = GeneticAlgorithm(_domain(), islands=2, pool=12, mating=6, replacement=6, generations=15, seed=seed,
+                          comm=comm).run()
+    return float(sa.best_cost), float(ga.best_cost)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_optimiser_islands_equal_independent_runs(world):
+    """SA chains / GA islands are rank-local (the reference runs independent optimisers per Spark
+    partition): the W-rank result is the best of W single-process runs seeded as those ranks."""
+    got = run_world(_optimisers, world, 5)
+    from avenir_amd.optimize.search import GeneticAlgorithm, SimulatedAnnealing
+    sa_ref = min(float(SimulatedAnnealing(_domain(), n_chains=16, iters=200, t0=5.0, cooling=0.97,
+                                          seed=5 + 1_000_003 * r).run().best_cost) for r in range(world))
+    ga_ref = min(float(GeneticAlgorithm(_domain(), islands=2, pool=12, mating=6, replacement=6, generations=15,
+                                        seed=5 + 7919 * r).run().best_cost) for r in range(world))
+    for sa_c, ga_c in got:
+        assert sa_c == pytest.approx(sa_ref, rel=1e-6)
+        assert ga_c == pytest.approx(ga_ref, rel=1e-6)
