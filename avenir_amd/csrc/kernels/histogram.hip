@@ -18,6 +18,9 @@
 // reduces them with 64-lane shuffles (64*240 < 2^16) and lane 0 adds into an LDS table.
 // This keeps the kernel at the HBM roofline even with 2 classes (where a plain atomic
 // histogram would serialise on a handful of hot addresses).
+#include <cstdlib>
+#include <string>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -583,6 +586,72 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K2 joint variant for row-packed records of at most 15 bits: every record is ONE LDS atomic into
+// the block's 2^bits joint table (record value -> count); the class-conditional marginals are
+// taken from that table once per block (2^bits entries x F fields, LDS atomics into a [C][TB]
+// table) and flushed with one global atomic per non-zero count.  Per record this is one
+// ds_add_u32 instead of ~22 VALU ops (hist_rowpack_kernel), so the pass is no longer VALU-issue
+// bound.  The record words are the same as pack_rows'.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(HB) void hist_joint_kernel(const uint16_t* __restrict__ words, long long n, int nbits,
+                                                        RowPackSpec spec, int nfeat, int n_classes,
+                                                        const int* __restrict__ bins, const int* __restrict__ offs,
+                                                        int total_bins, int count_labels,
+                                                        unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned int s_joint[];
+  unsigned int* s_small = s_joint + (1 << nbits);  // [C][total_bins]
+  const int J = 1 << nbits;
+  const unsigned mask = (unsigned)J - 1u;
+  for (int i = threadIdx.x; i < J + n_classes * total_bins; i += HB) s_joint[i] = 0;
+  __syncthreads();
+  const uint4* w4 = reinterpret_cast<const uint4*>(words);
+  const long long nvec = n >> 3;
+  const long long stride = (long long)gridDim.x * HB;
+  long long v = (long long)blockIdx.x * HB + threadIdx.x;
+  uint4 q = v < nvec ? w4[v] : make_uint4(0u, 0u, 0u, 0u);
+  for (; v < nvec; v += stride) {
+    const uint4 cur = q;
+    if (v + stride < nvec) q = w4[v + stride];  // next vector in flight while this one is counted
+    const unsigned dw[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      atomicAdd(&s_joint[dw[h] & mask], 1u);
+      atomicAdd(&s_joint[(dw[h] >> 16) & mask], 1u);
+    }
+  }
+  if (blockIdx.x == 0)
+    for (long long r = nvec * 8 + threadIdx.x; r < n; r += HB) atomicAdd(&s_joint[words[r] & mask], 1u);
+  __syncthreads();
+  for (int j = threadIdx.x; j < J; j += HB) {
+    const unsigned cnt = s_joint[j];
+    if (!cnt) continue;
+    int c = 0;
+    if (n_classes > 1) {
+      const unsigned lb = __builtin_amdgcn_ubfe((unsigned)j, (unsigned)spec.lsh, (unsigned)n_classes);
+      if (lb == 1u) c = 0;
+      else if (lb == 2u) c = 1;
+      else continue;  // unknown class: not counted (as in the column histogram)
+    }
+    unsigned int* row = s_small + c * total_bins;
+    for (int k = 0; k < nfeat; ++k) {
+      const int code = (int)__builtin_amdgcn_ubfe((unsigned)j, (unsigned)spec.sh[k], (unsigned)spec.w[k]);
+      if (code < bins[k]) atomicAdd(&row[offs[k] + code], cnt);
+    }
+    if (count_labels) atomicAdd(&row[total_bins - 1], cnt);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_classes * total_bins; i += HB) {
+    const unsigned cnt = s_small[i];
+    if (cnt) atomicAdd(&out[i], (unsigned long long)cnt);
+  }
+}
+
+int hist_joint_lds(int nbits, int n_classes, int total_bins) {
+  return (int)(sizeof(unsigned) * ((size_t(1) << nbits) + (size_t)n_classes * total_bins));
+}
+
 struct RowPackLaunch {
   const uint16_t* words;
   long long n;
@@ -931,6 +1000,24 @@ void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_
   int nm = 0;  // leading features whose (class, code) share one slot (kernel order puts them first)
   if (n_classes == 2)
     while (nm < nfeat && h_width[nm] <= 2) ++nm;
+  // records of <= 15 bits: one LDS atomic per record into the joint table (AVMI_ROWPACK_KERNEL=nibble
+  // keeps the VALU nibble-counter kernel)
+  int nbits = n_classes > 1 ? label_shift + label_width : 1;
+  for (int k = 0; k < nfeat; ++k) nbits = std::max(nbits, h_shift[k] + h_width[k]);
+  const char* kenv = std::getenv("AVMI_ROWPACK_KERNEL");
+  const bool force_nibble = kenv && std::string(kenv) == "nibble";
+  const int jlds = hist_joint_lds(nbits, n_classes, total_bins);
+  if (!force_nibble && nbits <= 15 && jlds <= 136 * 1024) {
+    if (jlds > 64 * 1024)
+      AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_joint_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, jlds));
+    const int res = av::resident_blocks((const void*)hist_joint_kernel, HB, (size_t)jlds);
+    const int grid = std::max(1, std::min(av::stream_grid(std::max(1LL, n >> 3), HB, 4, 4096), res));
+    hist_joint_kernel<<<grid, HB, (size_t)jlds, stream>>>(words, n, nbits, spec, nfeat, n_classes, d_bins, d_offs,
+                                                          total_bins, count_labels, out);
+    AV_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const RowPackLaunch a{words, n, spec, d_bins, d_offs, total_bins, count_labels, out, stream};
   switch (nfeat) {
     case 1: launch_rowpack_nf<1>(n_classes, nm, a); break;

@@ -126,3 +126,22 @@ def test_bayes_packed_equals_columns_gpu():
     assert t.rowpack is not None
     b = NaiveBayes(schema).fit(t)
     assert torch.equal(a.counts.cpu(), b.counts.cpu()) and torch.equal(a.class_n.cpu(), b.class_n.cpu())
+
+
+@gpu
+@pytest.mark.parametrize("missing", [False, True])
+def test_joint_and_nibble_rowpack_kernels_agree(monkeypatch, missing):
+    """Records of <= 15 bits go through the joint-table kernel (one LDS atomic per record); the
+    nibble-counter kernel (AVMI_ROWPACK_KERNEL=nibble) must give the same counts, and both equal
+    the column histogram."""
+    n = (1 << 21) + 13
+    bins = [4, 3, 3, 3, 5]
+    codes, labels = _random_codes(n, bins, 2, seed=3, missing=missing)
+    codes, labels = codes.cuda(), labels.cuda()
+    ref = H.class_histogram(codes, n, bins, labels, 2, count_labels=True).cpu()
+    rp = H.pack_rows(codes, n, bins, labels, 2)
+    monkeypatch.delenv("AVMI_ROWPACK_KERNEL", raising=False)
+    joint = H.class_histogram_packed(rp, count_labels=True).cpu()
+    monkeypatch.setenv("AVMI_ROWPACK_KERNEL", "nibble")
+    nib = H.class_histogram_packed(rp, count_labels=True).cpu()
+    assert torch.equal(joint, ref) and torch.equal(nib, ref)
