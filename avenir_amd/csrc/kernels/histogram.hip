@@ -595,6 +595,11 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
 // ds_add_u32 instead of ~22 VALU ops (hist_rowpack_kernel), so the pass is no longer VALU-issue
 // bound.  The record words are the same as pack_rows'.
 // ---------------------------------------------------------------------------------------------
+// Record value -> LDS slot: the low 6 bits (the LDS bank) XOR-folded with bits 6-11 and 12-17, so
+// the bank depends on every field, not only on the class bits and the first fields (which take few
+// distinct values); bits >= 6 are unchanged, so the map is a bijection and its own inverse.
+__device__ __forceinline__ unsigned joint_slot(unsigned j) { return j ^ ((j >> 6) & 63u) ^ ((j >> 12) & 63u); }
+
 __global__ __launch_bounds__(HB) void hist_joint_kernel(const uint16_t* __restrict__ words, long long n, int nbits,
                                                         RowPackSpec spec, int nfeat, int n_classes,
                                                         const int* __restrict__ bins, const int* __restrict__ offs,
@@ -617,16 +622,17 @@ __global__ __launch_bounds__(HB) void hist_joint_kernel(const uint16_t* __restri
     const unsigned dw[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      atomicAdd(&s_joint[dw[h] & mask], 1u);
-      atomicAdd(&s_joint[(dw[h] >> 16) & mask], 1u);
+      atomicAdd(&s_joint[joint_slot(dw[h] & mask)], 1u);
+      atomicAdd(&s_joint[joint_slot((dw[h] >> 16) & mask)], 1u);
     }
   }
   if (blockIdx.x == 0)
-    for (long long r = nvec * 8 + threadIdx.x; r < n; r += HB) atomicAdd(&s_joint[words[r] & mask], 1u);
+    for (long long r = nvec * 8 + threadIdx.x; r < n; r += HB) atomicAdd(&s_joint[joint_slot(words[r] & mask)], 1u);
   __syncthreads();
-  for (int j = threadIdx.x; j < J; j += HB) {
-    const unsigned cnt = s_joint[j];
+  for (int p = threadIdx.x; p < J; p += HB) {
+    const unsigned cnt = s_joint[p];
     if (!cnt) continue;
+    const int j = (int)joint_slot((unsigned)p);  // the slot map is its own inverse
     int c = 0;
     if (n_classes > 1) {
       const unsigned lb = __builtin_amdgcn_ubfe((unsigned)j, (unsigned)spec.lsh, (unsigned)n_classes);

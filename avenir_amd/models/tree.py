@@ -186,8 +186,17 @@ def build_split_space(schema: FeatureSchema, t: Table | None = None, attrs: Sequ
     numeric column of at most 2^20 / world sampled values each), so every rank bins identically."""
     out = []
     gather = comm is not None and comm.is_distributed
+    pre = _batched_points(schema, t, attrs, binary, max_bins) if (t is not None and not gather) else {}
     for f in schema.feature_fields:
         if attrs is not None and f.ordinal not in attrs:
+            continue
+        if f.ordinal in pre:
+            fs = FeatureSplits(f, "num", points=pre[f.ordinal], binary=binary)
+            if not binary:
+                fs.splits = numeric_splits(fs)
+            if fs.n_bins > 254:
+                raise ValueError(f"attribute {f.name}: {fs.n_bins} fine bins > 254")
+            out.append(fs)
             continue
         if f.is_categorical:
             fs = FeatureSplits(f, "cat", binary=binary)
@@ -215,6 +224,26 @@ def build_split_space(schema: FeatureSchema, t: Table | None = None, attrs: Sequ
             raise ValueError(f"attribute {f.name}: {fs.n_bins} fine bins > 254")
         out.append(fs)
     return out
+
+
+def _batched_points(schema, t: Table, attrs, binary: bool, max_bins: int) -> dict[int, list[float]]:
+    """Quantile split points of every data-quantile numeric feature in ONE batched quantile over a
+    stacked [F, m] sample (one sort launch instead of one per column); identical to
+    ``numeric_points`` per column.  Columns with NaNs are left to the per-column path."""
+    names = [x.ordinal for x in t.numeric_fields]
+    fields = [f for f in schema.feature_fields
+              if (attrs is None or f.ordinal in attrs) and f.is_numeric and f.ordinal in names
+              and (binary or not (f.min is not None and f.max is not None and f.split_scan_interval))]
+    if len(fields) < 2 or t.n == 0:
+        return {}
+    V = t.numeric[[names.index(f.ordinal) for f in fields], : t.n].float()
+    if bool(torch.isnan(V).any()):
+        return {}
+    if V.shape[1] > 1 << 20:
+        V = V[:, :: (V.shape[1] + (1 << 20) - 1) >> 20]
+    qs = torch.linspace(0, 1, max_bins + 1, device=V.device)[1:-1]
+    Q = torch.quantile(V, qs, dim=1).t().contiguous().cpu()           # [F, nq]
+    return {f.ordinal: [float(p) for p in torch.unique(Q[i]).tolist()] for i, f in enumerate(fields)}
 
 
 def _gather_sample(vals: torch.Tensor, comm) -> torch.Tensor:
