@@ -127,6 +127,54 @@ void class_histogram_rowpacked(const at::Tensor& words, int64_t n, std::vector<i
                                  reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(words));
 }
 
+// Dense B-bit record stream from the 16-bit row-packed words (32 records per B dwords).
+at::Tensor pack_dense(const at::Tensor& words, int64_t n, int64_t B) {
+  CHECK_DEV(words);
+  CHECK_DTYPE(words, at::kShort);
+  TORCH_CHECK(words.dim() == 1 && n >= 0 && n <= words.numel(), "words must be [>= n]");
+  TORCH_CHECK(B >= 4 && B <= 15, "4..15 bits per record");
+  auto dense = at::zeros({std::max<int64_t>(1, avk::dense_words(n, (int)B))}, words.options().dtype(at::kInt));
+  DevGuard g(words.device());
+  avk::pack_dense(reinterpret_cast<const uint16_t*>(words.data_ptr()), n, (int)B,
+                  reinterpret_cast<uint32_t*>(dense.data_ptr<int>()), cur_stream(words));
+  return dense;
+}
+
+void class_histogram_dense(const at::Tensor& dense, int64_t n, int64_t B, std::vector<int64_t> shifts,
+                           std::vector<int64_t> widths, int64_t label_shift, int64_t label_width, const at::Tensor& bins,
+                           const at::Tensor& offs, int64_t total_bins, int64_t n_classes, at::Tensor& out,
+                           bool count_labels) {
+  CHECK_DEV(dense);
+  CHECK_DTYPE(dense, at::kInt);
+  TORCH_CHECK(B >= 4 && B <= 15 && n >= 0 && dense.numel() >= avk::dense_words(n, (int)B), "dense stream too short");
+  const int64_t F = (int64_t)shifts.size();
+  TORCH_CHECK(F >= 1 && F <= 8 && (int64_t)widths.size() == F, "1..8 packed fields");
+  std::vector<int> sh(F), wd(F);
+  for (int64_t k = 0; k < F; ++k) {
+    TORCH_CHECK(widths[k] >= 1 && widths[k] <= 8 && shifts[k] >= 0 && shifts[k] + widths[k] <= B,
+                "packed field outside the record");
+    sh[k] = (int)shifts[k];
+    wd[k] = (int)widths[k];
+  }
+  TORCH_CHECK(n_classes >= 1 && n_classes <= 2, "1 or 2 classes");
+  CHECK_DEV(bins); CHECK_DTYPE(bins, at::kInt);
+  CHECK_DEV(offs); CHECK_DTYPE(offs, at::kInt);
+  TORCH_CHECK(bins.numel() == F && offs.numel() == F, "bins / offs must have F entries");
+  {
+    auto bc = bins.cpu(), oc = offs.cpu();
+    for (int64_t k = 0; k < F; ++k)
+      TORCH_CHECK(oc.data_ptr<int>()[k] >= 0 && oc.data_ptr<int>()[k] + bc.data_ptr<int>()[k] <= total_bins,
+                  "feature bins outside the table");
+  }
+  CHECK_DEV(out); CHECK_DTYPE(out, at::kLong);
+  TORCH_CHECK(out.numel() == n_classes * total_bins, "out must be [C * TB]");
+  DevGuard g(dense.device());
+  avk::class_histogram_dense(reinterpret_cast<const uint32_t*>(dense.data_ptr<int>()), n, (int)B, sh.data(), wd.data(),
+                             (int)F, (int)label_shift, (int)label_width, bins.data_ptr<int>(), offs.data_ptr<int>(),
+                             (int)total_bins, (int)n_classes, count_labels ? 1 : 0,
+                             reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(dense));
+}
+
 void pair_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at::Tensor>& labels,
                     const at::Tensor& bins, const at::Tensor& pairs, const at::Tensor& poff,
                     int64_t max_tab, int64_t n_classes, at::Tensor& out) {
@@ -1542,6 +1590,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("class_histogram", &class_histogram);
   m.def("pair_histogram", &pair_histogram);
   m.def("class_histogram_rowpacked", &class_histogram_rowpacked);
+  m.def("pack_dense", &pack_dense);
+  m.def("class_histogram_dense", &class_histogram_dense);
   m.def("bigram_histogram", &bigram_histogram);
   m.def("class_moments", &class_moments);
   m.def("nb_predict", &nb_predict);

@@ -167,6 +167,13 @@ long long forest_predict_bin_lds(int n_nodes, int nfeat);
 void forest_predict_bin(const uint8_t* codes, long long ld, long long n, int nfeat, const uint2* nodes, int n_nodes,
                         const float* values, int V, const int* tree_root, const float* tree_w, int n_trees, int mode,
                         float* out, hipStream_t stream);
+// dense B-bit record streams (histogram.hip)
+long long dense_words(long long n, int B);
+void pack_dense(const uint16_t* words, long long n, int B, uint32_t* dense, hipStream_t stream);
+void class_histogram_dense(const uint32_t* dense, long long n, int B, const int* h_shift, const int* h_width,
+                           int nfeat, int label_shift, int label_width, const int* d_bins, const int* d_offs,
+                           int total_bins, int n_classes, int count_labels, unsigned long long* out,
+                           hipStream_t stream);
 void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
                        unsigned rate32, int* tile_cnt, hipStream_t stream);
 void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,

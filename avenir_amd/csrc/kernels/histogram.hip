@@ -654,6 +654,91 @@ __global__ __launch_bounds__(HB) void hist_joint_kernel(const uint16_t* __restri
   }
 }
 
+
+// Dense variant: records of B bits packed back to back, 32 records per B dwords (a lane's group),
+// so a 2^30-record churn table (B = 13) streams 1.63 B/record instead of 2.  Each lane loads its
+// group's B dwords (consecutive lanes read consecutive groups) and extracts the 32 records at
+// compile-time bit offsets (one v_bfe, or v_alignbit across a dword boundary).  Records at index
+// >= n (the last group's padding) are skipped.
+template <int B>
+__global__ __launch_bounds__(HB) void hist_joint_dense_kernel(const uint32_t* __restrict__ dense, long long n,
+                                                              RowPackSpec spec, int nfeat, int n_classes,
+                                                              const int* __restrict__ bins,
+                                                              const int* __restrict__ offs, int total_bins,
+                                                              int count_labels, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned int s_joint[];
+  constexpr int J = 1 << B;
+  constexpr unsigned M = (unsigned)J - 1u;
+  unsigned int* s_small = s_joint + J;
+  for (int i = threadIdx.x; i < J + n_classes * total_bins; i += HB) s_joint[i] = 0;
+  __syncthreads();
+  const long long groups = (n + 31) >> 5;
+  const long long stride = (long long)gridDim.x * HB;
+  for (long long g = (long long)blockIdx.x * HB + threadIdx.x; g < groups; g += stride) {
+    uint32_t d[B + 1];
+    const uint32_t* src = dense + g * B;
+#pragma unroll
+    for (int i = 0; i < B; ++i) d[i] = src[i];
+    d[B] = 0;
+    const long long left = n - (g << 5);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int bit = k * B, i = bit >> 5, sh = bit & 31;
+      unsigned r;
+      if (sh + B <= 32) r = __builtin_amdgcn_ubfe(d[i], (unsigned)sh, (unsigned)B);
+      else r = __builtin_amdgcn_alignbit(d[i + 1], d[i], (unsigned)sh) & M;
+      if (left >= 32 || k < left) atomicAdd(&s_joint[joint_slot(r)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < J; p += HB) {
+    const unsigned cnt = s_joint[p];
+    if (!cnt) continue;
+    const int j = (int)joint_slot((unsigned)p);
+    int c = 0;
+    if (n_classes > 1) {
+      const unsigned lb = __builtin_amdgcn_ubfe((unsigned)j, (unsigned)spec.lsh, (unsigned)n_classes);
+      if (lb == 1u) c = 0;
+      else if (lb == 2u) c = 1;
+      else continue;
+    }
+    unsigned int* row = s_small + c * total_bins;
+    for (int kf = 0; kf < nfeat; ++kf) {
+      const int code = (int)__builtin_amdgcn_ubfe((unsigned)j, (unsigned)spec.sh[kf], (unsigned)spec.w[kf]);
+      if (code < bins[kf]) atomicAdd(&row[offs[kf] + code], cnt);
+    }
+    if (count_labels) atomicAdd(&row[total_bins - 1], cnt);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_classes * total_bins; i += HB) {
+    const unsigned cnt = s_small[i];
+    if (cnt) atomicAdd(&out[i], (unsigned long long)cnt);
+  }
+}
+
+// dense[g * B + i]: record k of group g at bits [k B, k B + B) of the group's B dwords
+__global__ __launch_bounds__(HB) void pack_dense_kernel(const uint16_t* __restrict__ words, long long n, int B,
+                                                        uint32_t* __restrict__ dense) {
+  const long long groups = (n + 31) >> 5;
+  const long long stride = (long long)gridDim.x * HB;
+  for (long long g = (long long)blockIdx.x * HB + threadIdx.x; g < groups; g += stride) {
+    uint32_t d[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) d[i] = 0;
+    for (int k = 0; k < 32; ++k) {
+      const long long r = (g << 5) + k;
+      const uint32_t v = r < n ? ((uint32_t)words[r] & ((1u << B) - 1u)) : 0u;
+      const int bit = k * B, i = bit >> 5, sh = bit & 31;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {  // register-indexed writes unrolled (no scratch)
+        if (q == i) d[q] |= v << sh;
+        if (q == i + 1 && sh + B > 32) d[q] |= v >> (32 - sh);
+      }
+    }
+    for (int i = 0; i < B; ++i) dense[g * B + i] = d[i];
+  }
+}
+
 int hist_joint_lds(int nbits, int n_classes, int total_bins) {
   return (int)(sizeof(unsigned) * ((size_t(1) << nbits) + (size_t)n_classes * total_bins));
 }
@@ -1034,6 +1119,58 @@ void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_
     case 6: launch_rowpack_nf<6>(n_classes, nm, a); break;
     case 7: launch_rowpack_nf<7>(n_classes, nm, a); break;
     default: launch_rowpack_nf<8>(n_classes, nm, a); break;
+  }
+}
+
+
+long long dense_words(long long n, int B) { return ((n + 31) >> 5) * (long long)B; }
+
+void pack_dense(const uint16_t* words, long long n, int B, uint32_t* dense, hipStream_t stream) {
+  if (n <= 0) return;
+  if (B < 1 || B > 15) throw std::runtime_error("pack_dense: 1..15 bits per record");
+  pack_dense_kernel<<<av::stream_grid((n + 31) >> 5, HB, 1, 4096), HB, 0, stream>>>(words, n, B, dense);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+template <int B>
+static void launch_joint_dense(const uint32_t* dense, long long n, const RowPackSpec& spec, int nfeat, int n_classes,
+                               const int* bins, const int* offs, int total_bins, int count_labels,
+                               unsigned long long* out, hipStream_t stream) {
+  const int lds = hist_joint_lds(B, n_classes, total_bins);
+  if (lds > 64 * 1024)
+    AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_joint_dense_kernel<B>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  const int res = av::resident_blocks((const void*)hist_joint_dense_kernel<B>, HB, (size_t)lds);
+  const int grid = std::max(1, std::min(av::stream_grid(std::max(1LL, (n + 31) >> 5), HB, 1, 8192), res));
+  hist_joint_dense_kernel<B><<<grid, HB, (size_t)lds, stream>>>(dense, n, spec, nfeat, n_classes, bins, offs,
+                                                                 total_bins, count_labels, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void class_histogram_dense(const uint32_t* dense, long long n, int B, const int* h_shift, const int* h_width,
+                           int nfeat, int label_shift, int label_width, const int* d_bins, const int* d_offs,
+                           int total_bins, int n_classes, int count_labels, unsigned long long* out,
+                           hipStream_t stream) {
+  if (n <= 0 || nfeat <= 0) return;
+  if (nfeat > 8 || n_classes < 1 || n_classes > 2) throw std::runtime_error("dense histogram: F <= 8, C <= 2");
+  if (n_classes > 1 && (label_width != n_classes || label_shift != 0))
+    throw std::runtime_error("dense histogram: the class is C one-hot bits at bit 0");
+  RowPackSpec spec{};
+  int need = n_classes > 1 ? label_width : 1;
+  for (int k = 0; k < nfeat; ++k) {
+    spec.sh[k] = h_shift[k];
+    spec.w[k] = h_width[k];
+    need = std::max(need, h_shift[k] + h_width[k]);
+  }
+  spec.lsh = n_classes > 1 ? label_shift : 0;
+  if (need > B) throw std::runtime_error("dense histogram: fields exceed the record width");
+  switch (B) {
+#define AV_DENSE(BB) \
+  case BB: launch_joint_dense<BB>(dense, n, spec, nfeat, n_classes, d_bins, d_offs, total_bins, count_labels, out, stream); break;
+    AV_DENSE(4) AV_DENSE(5) AV_DENSE(6) AV_DENSE(7) AV_DENSE(8) AV_DENSE(9) AV_DENSE(10) AV_DENSE(11)
+    AV_DENSE(12) AV_DENSE(13) AV_DENSE(14) AV_DENSE(15)
+#undef AV_DENSE
+    default: throw std::runtime_error("dense histogram: 4..15 bits per record");
   }
 }
 

@@ -2,6 +2,8 @@
 CPU tensors -> the PyTorch reference implementation of the same op (golden oracle)."""
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import Sequence
 
@@ -86,6 +88,15 @@ class RowPacked:
     label_shift: int
     label_width: int         # 0: no class field (C = 1)
     n_classes: int
+    dense: torch.Tensor | None = None   # GPU: the same records as a dense B-bit stream (pack_dense)
+    bits: int = 16                      # B: bits per record actually used
+
+    def ensure_dense(self) -> "RowPacked":
+        """Attach the dense B-bit stream (32 records per B dwords, 1.6 B/record for churn) the
+        joint-table kernel streams instead of the 16-bit words; GPU only, B in 4..15."""
+        if self.dense is None and self.words.is_cuda and 4 <= self.bits <= 15 and self.n > 0:
+            self.dense = _native.C().pack_dense(self.words, int(self.n), int(self.bits))
+        return self
 
 
 def rowpack_layout(bins: Sequence[int], n_classes: int, missing: Sequence[bool] | None = None):
@@ -139,7 +150,8 @@ def pack_rows(codes: torch.Tensor, n: int, bins: Sequence[int], labels: torch.Te
         v = labels[:n].to(torch.int32)
         body |= torch.where(v < C, 1 << v.clamp_max(C - 1), torch.zeros_like(v)) << lsh
     words = torch.where(w >= 32768, w - 65536, w).to(torch.int16)
-    return RowPacked(words, int(n), bins, shifts, widths, lsh, lw, C)
+    bits = max([s + wd for s, wd in zip(shifts, widths)] + [lsh + lw])
+    return RowPacked(words, int(n), bins, shifts, widths, lsh, lw, C, bits=bits).ensure_dense()
 
 
 def unpack_rows(rp: RowPacked) -> tuple[torch.Tensor, torch.Tensor | None]:
@@ -182,6 +194,13 @@ def class_histogram_packed(rp: RowPacked, out: torch.Tensor | None = None,
         # across both classes); output columns stay in schema order through offs
         order = sorted(range(len(rp.bins)), key=lambda k: (C == 2 and rp.widths[k] > 2, k))
         dev = rp.words.device
+        kind = os.environ.get("AVMI_ROWPACK_KERNEL", "dense")
+        if kind == "dense" and rp.dense is not None:
+            # dense B-bit records, one LDS atomic per record into the joint table
+            _native.C().class_histogram_dense(rp.dense, int(rp.n), int(rp.bits), list(rp.shifts), list(rp.widths),
+                                              rp.label_shift, rp.label_width, _dev_i32(rp.bins, dev),
+                                              _dev_i32(offs, dev), tb, C, out, bool(count_labels))
+            return out
         _native.C().class_histogram_rowpacked(rp.words, int(rp.n), [rp.shifts[k] for k in order],
                                               [rp.widths[k] for k in order], rp.label_shift, rp.label_width,
                                               _dev_i32([rp.bins[k] for k in order], dev),

@@ -129,19 +129,21 @@ def test_bayes_packed_equals_columns_gpu():
 
 
 @gpu
-@pytest.mark.parametrize("missing", [False, True])
-def test_joint_and_nibble_rowpack_kernels_agree(monkeypatch, missing):
-    """Records of <= 15 bits go through the joint-table kernel (one LDS atomic per record); the
-    nibble-counter kernel (AVMI_ROWPACK_KERNEL=nibble) must give the same counts, and both equal
-    the column histogram."""
-    n = (1 << 21) + 13
-    bins = [4, 3, 3, 3, 5]
-    codes, labels = _random_codes(n, bins, 2, seed=3, missing=missing)
+@pytest.mark.parametrize("n,C,missing", [((1 << 21) + 13, 2, 0.0), ((1 << 21) + 13, 2, 0.05), (1000, 2, 0.0),
+                                         (77777, 1, 0.0), (31, 2, 0.05)])
+def test_dense_joint_and_nibble_rowpack_kernels_agree(monkeypatch, n, C, missing):
+    """Dense B-bit records (default), 16-bit words through the joint-table kernel
+    (AVMI_ROWPACK_KERNEL=joint) and the nibble-counter kernel (=nibble) give the column counts."""
+    bins = [4, 3, 3, 3, 5] if C == 2 else [7, 1, 2, 3]
+    codes, labels = _random_codes(n, bins, C, seed=n, missing=missing)
     codes, labels = codes.cuda(), labels.cuda()
-    ref = H.class_histogram(codes, n, bins, labels, 2, count_labels=True).cpu()
-    rp = H.pack_rows(codes, n, bins, labels, 2)
-    monkeypatch.delenv("AVMI_ROWPACK_KERNEL", raising=False)
-    joint = H.class_histogram_packed(rp, count_labels=True).cpu()
-    monkeypatch.setenv("AVMI_ROWPACK_KERNEL", "nibble")
-    nib = H.class_histogram_packed(rp, count_labels=True).cpu()
-    assert torch.equal(joint, ref) and torch.equal(nib, ref)
+    lab = labels if C == 2 else None
+    ref = H.class_histogram(codes, n, bins, lab, C, count_labels=True).cpu()
+    rp = H.pack_rows(codes, n, bins, lab, C)
+    assert rp.dense is not None and rp.dense.numel() == ((n + 31) // 32) * rp.bits
+    res = {}
+    for kind in ("dense", "joint", "nibble"):
+        monkeypatch.setenv("AVMI_ROWPACK_KERNEL", kind)
+        res[kind] = H.class_histogram_packed(rp, count_labels=True).cpu()
+    for kind, got in res.items():
+        assert torch.equal(got, ref), kind
