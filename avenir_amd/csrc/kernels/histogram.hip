@@ -598,7 +598,9 @@ __global__ __launch_bounds__(HB) void hist_rowpack_kernel(const uint16_t* __rest
 // Record value -> LDS slot: the low 6 bits (the LDS bank) XOR-folded with bits 6-11 and 12-17, so
 // the bank depends on every field, not only on the class bits and the first fields (which take few
 // distinct values); bits >= 6 are unchanged, so the map is a bijection and its own inverse.
-__device__ __forceinline__ unsigned joint_slot(unsigned j) { return j ^ ((j >> 6) & 63u) ^ ((j >> 12) & 63u); }
+__device__ __forceinline__ unsigned joint_slot(unsigned j) {
+  return j ^ __builtin_amdgcn_ubfe(j, 6u, 6u) ^ __builtin_amdgcn_ubfe(j, 12u, 6u);  // 2 v_bfe + v_xor3
+}
 
 __global__ __launch_bounds__(HB) void hist_joint_kernel(const uint16_t* __restrict__ words, long long n, int nbits,
                                                         RowPackSpec spec, int nfeat, int n_classes,
@@ -681,13 +683,18 @@ __global__ __launch_bounds__(HB) void hist_joint_dense_kernel(const uint32_t* __
     for (int i = 0; i < B; ++i) d[i] = src[i];
     d[B] = 0;
     const long long left = n - (g << 5);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
+    auto rec = [&](int k) __attribute__((always_inline)) -> unsigned {
       const int bit = k * B, i = bit >> 5, sh = bit & 31;
-      unsigned r;
-      if (sh + B <= 32) r = __builtin_amdgcn_ubfe(d[i], (unsigned)sh, (unsigned)B);
-      else r = __builtin_amdgcn_alignbit(d[i + 1], d[i], (unsigned)sh) & M;
-      if (left >= 32 || k < left) atomicAdd(&s_joint[joint_slot(r)], 1u);
+      if (sh + B <= 32) return __builtin_amdgcn_ubfe(d[i], (unsigned)sh, (unsigned)B);
+      return __builtin_amdgcn_alignbit(d[i + 1], d[i], (unsigned)sh) & M;
+    };
+    if (left >= 32) {  // every group but the last: no per-record predicate
+#pragma unroll
+      for (int k = 0; k < 32; ++k) atomicAdd(&s_joint[joint_slot(rec(k))], 1u);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        if (k < left) atomicAdd(&s_joint[joint_slot(rec(k))], 1u);
     }
   }
   __syncthreads();

@@ -6,14 +6,16 @@ headline is the one BASELINE.md lists first and SURVEY.md §7.3 names as the min
 slice: Naive Bayes churn-model training (``BayesianDistribution``) on the ``resource/churn.json``
 schema — 5 categorical features, 2 classes.
 
-One step = one complete training pass over this rank's shard: the fused K2 class-conditional
-histogram (HIP, packed byte counters) + class counts over ``rows_per_gpu`` records, ONE RCCL
+One step = one complete training pass over this rank's shard: the K2 class-conditional histogram
+(HIP joint-table kernel: one LDS atomic per record, marginals per block) + class counts over
+``rows_per_gpu`` records, ONE RCCL
 all-reduce of the [C, TB+1] count table, and the model finalisation (log-probability tables for
 the predictor).  Weak scaling: every GPU owns ``rows_per_gpu`` synthetic records (same
 distributions as the reference's ``usage.rb``), generated on device before timing.
 
-The records are held on device as one 16-bit word per record (5 codes + class, ``--layout
-rowpacked``, packed once at load time; lossless) or as uint8 code columns (``--layout columns``).
+The records are held on device packed once at load time, losslessly (``--layout rowpacked``: the
+5 codes + one-hot class of a record in 13 bits, streamed as a dense 13-bit record stream; the
+16-bit word form is kept too) or as uint8 code columns (``--layout columns``).
 CSV parsing and packing are NOT in the timed steps (the headline is the on-device training pass);
 ``extra`` reports them separately:
 
@@ -152,7 +154,8 @@ def main() -> int:
             print("[bench] schema does not fit 16-bit records: using code columns", file=sys.stderr)
             args.layout = "columns"
         else:
-            bytes_per_row = 2
+            rp = table.rowpack
+            bytes_per_row = rp.bits / 8.0 if getattr(rp, "dense", None) is not None else 2
     nb = NaiveBayes(schema, comm=comm)
 
     def step():
@@ -227,7 +230,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("uint16 row-packed categorical records (2 B/record, lossless)/int64 counts (exact)"
+            "dtype": (f"row-packed categorical records ({bytes_per_row * 8:g}-bit records, lossless)/int64 counts (exact)"
                       if args.layout == "rowpacked" else "uint8-codes/int64-counts (exact integer counting)"),
             "data": "synthetic (device-generated, resource/usage.rb distributions)",
             "config": {

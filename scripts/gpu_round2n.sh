@@ -1,0 +1,8 @@
+#!/bin/bash
+set -eo pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_rowpack.py tests/test_bayes.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r2n_tests.log 2>&1
+timeout -k 10 300 python -u bench.py --ingest-rows 0 > gpurun_out/r2n_bench.log 2>&1
+PMC_TARGETS="rowpack" bash scripts/gpu_pmc.sh > gpurun_out/r2n_pmc.log 2>&1
+tail -2 gpurun_out/r2n_tests.log; cat gpurun_out/r2n_bench.log
