@@ -662,8 +662,11 @@ __global__ __launch_bounds__(HB) void hist_joint_kernel(const uint16_t* __restri
 // group's B dwords (consecutive lanes read consecutive groups) and extracts the 32 records at
 // compile-time bit offsets (one v_bfe, or v_alignbit across a dword boundary).  Records at index
 // >= n (the last group's padding) are skipped.
-template <int B>
-__global__ __launch_bounds__(HB) void hist_joint_dense_kernel(const uint32_t* __restrict__ dense, long long n,
+// R replicas of the joint table, interleaved (slot * R + lane % R): lanes of different residues
+// never share a bank, which divides the LDS atomic conflicts of random records by about R; NT
+// threads per block keep enough waves per CU when the replicated table limits blocks per CU.
+template <int B, int R, int NT>
+__global__ __launch_bounds__(NT) void hist_joint_dense_kernel(const uint32_t* __restrict__ dense, long long n,
                                                               RowPackSpec spec, int nfeat, int n_classes,
                                                               const int* __restrict__ bins,
                                                               const int* __restrict__ offs, int total_bins,
@@ -671,12 +674,13 @@ __global__ __launch_bounds__(HB) void hist_joint_dense_kernel(const uint32_t* __
   extern __shared__ __attribute__((aligned(16))) unsigned int s_joint[];
   constexpr int J = 1 << B;
   constexpr unsigned M = (unsigned)J - 1u;
-  unsigned int* s_small = s_joint + J;
-  for (int i = threadIdx.x; i < J + n_classes * total_bins; i += HB) s_joint[i] = 0;
+  unsigned int* s_small = s_joint + J * R;
+  for (int i = threadIdx.x; i < J * R + n_classes * total_bins; i += NT) s_joint[i] = 0;
+  const unsigned rep = threadIdx.x & (R - 1);
   __syncthreads();
   const long long groups = (n + 31) >> 5;
-  const long long stride = (long long)gridDim.x * HB;
-  for (long long g = (long long)blockIdx.x * HB + threadIdx.x; g < groups; g += stride) {
+  const long long stride = (long long)gridDim.x * NT;
+  for (long long g = (long long)blockIdx.x * NT + threadIdx.x; g < groups; g += stride) {
     uint32_t d[B + 1];
     const uint32_t* src = dense + g * B;
 #pragma unroll
@@ -690,16 +694,18 @@ __global__ __launch_bounds__(HB) void hist_joint_dense_kernel(const uint32_t* __
     };
     if (left >= 32) {  // every group but the last: no per-record predicate
 #pragma unroll
-      for (int k = 0; k < 32; ++k) atomicAdd(&s_joint[joint_slot(rec(k))], 1u);
+      for (int k = 0; k < 32; ++k) atomicAdd(&s_joint[joint_slot(rec(k)) * R + rep], 1u);
     } else {
 #pragma unroll
       for (int k = 0; k < 32; ++k)
-        if (k < left) atomicAdd(&s_joint[joint_slot(rec(k))], 1u);
+        if (k < left) atomicAdd(&s_joint[joint_slot(rec(k)) * R + rep], 1u);
     }
   }
   __syncthreads();
-  for (int p = threadIdx.x; p < J; p += HB) {
-    const unsigned cnt = s_joint[p];
+  for (int p = threadIdx.x; p < J; p += NT) {
+    unsigned cnt = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) cnt += s_joint[p * R + r];
     if (!cnt) continue;
     const int j = (int)joint_slot((unsigned)p);
     int c = 0;
@@ -717,7 +723,7 @@ __global__ __launch_bounds__(HB) void hist_joint_dense_kernel(const uint32_t* __
     if (count_labels) atomicAdd(&row[total_bins - 1], cnt);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n_classes * total_bins; i += HB) {
+  for (int i = threadIdx.x; i < n_classes * total_bins; i += NT) {
     const unsigned cnt = s_small[i];
     if (cnt) atomicAdd(&out[i], (unsigned long long)cnt);
   }
@@ -1139,19 +1145,35 @@ void pack_dense(const uint16_t* words, long long n, int B, uint32_t* dense, hipS
   AV_HIP_CHECK(hipGetLastError());
 }
 
+template <int B, int R, int NT>
+static void launch_joint_dense_r(const uint32_t* dense, long long n, const RowPackSpec& spec, int nfeat, int n_classes,
+                                 const int* bins, const int* offs, int total_bins, int count_labels,
+                                 unsigned long long* out, hipStream_t stream) {
+  const int lds = (int)(sizeof(unsigned) * ((size_t)R * (size_t(1) << B) + (size_t)n_classes * total_bins));
+  if (lds > 160 * 1024) throw std::runtime_error("dense histogram: replicated table exceeds LDS");
+  auto kern = hist_joint_dense_kernel<B, R, NT>;
+  if (lds > 64 * 1024)
+    AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     lds));
+  const int res = av::resident_blocks((const void*)kern, NT, (size_t)lds);
+  const int grid = std::max(1, std::min(av::stream_grid(std::max(1LL, (n + 31) >> 5), NT, 1, 8192), res));
+  kern<<<grid, NT, (size_t)lds, stream>>>(dense, n, spec, nfeat, n_classes, bins, offs, total_bins, count_labels, out);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+// replicas: AVMI_JOINT_REPLICAS (1, 2 or 4), else the most that fit 128 KiB of LDS
 template <int B>
 static void launch_joint_dense(const uint32_t* dense, long long n, const RowPackSpec& spec, int nfeat, int n_classes,
                                const int* bins, const int* offs, int total_bins, int count_labels,
                                unsigned long long* out, hipStream_t stream) {
-  const int lds = hist_joint_lds(B, n_classes, total_bins);
-  if (lds > 64 * 1024)
-    AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_joint_dense_kernel<B>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  const int res = av::resident_blocks((const void*)hist_joint_dense_kernel<B>, HB, (size_t)lds);
-  const int grid = std::max(1, std::min(av::stream_grid(std::max(1LL, (n + 31) >> 5), HB, 1, 8192), res));
-  hist_joint_dense_kernel<B><<<grid, HB, (size_t)lds, stream>>>(dense, n, spec, nfeat, n_classes, bins, offs,
-                                                                 total_bins, count_labels, out);
-  AV_HIP_CHECK(hipGetLastError());
+  int R = (B <= 13) ? 4 : (B == 14 ? 2 : 1);
+  if (const char* e = std::getenv("AVMI_JOINT_REPLICAS")) R = std::atoi(e);
+  if (R >= 4 && B <= 13)
+    launch_joint_dense_r<B, 4, 1024>(dense, n, spec, nfeat, n_classes, bins, offs, total_bins, count_labels, out, stream);
+  else if (R >= 2 && B <= 14)
+    launch_joint_dense_r<B, 2, 512>(dense, n, spec, nfeat, n_classes, bins, offs, total_bins, count_labels, out, stream);
+  else
+    launch_joint_dense_r<B, 1, HB>(dense, n, spec, nfeat, n_classes, bins, offs, total_bins, count_labels, out, stream);
 }
 
 void class_histogram_dense(const uint32_t* dense, long long n, int B, const int* h_shift, const int* h_width,

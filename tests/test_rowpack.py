@@ -145,5 +145,9 @@ def test_dense_joint_and_nibble_rowpack_kernels_agree(monkeypatch, n, C, missing
     for kind in ("dense", "joint", "nibble"):
         monkeypatch.setenv("AVMI_ROWPACK_KERNEL", kind)
         res[kind] = H.class_histogram_packed(rp, count_labels=True).cpu()
+    monkeypatch.setenv("AVMI_ROWPACK_KERNEL", "dense")
+    for r in (1, 2, 4):          # replicated joint tables
+        monkeypatch.setenv("AVMI_JOINT_REPLICAS", str(r))
+        res[f"dense-r{r}"] = H.class_histogram_packed(rp, count_labels=True).cpu()
     for kind, got in res.items():
         assert torch.equal(got, ref), kind
