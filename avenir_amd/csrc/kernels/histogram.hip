@@ -677,6 +677,9 @@ __global__ __launch_bounds__(NT) void hist_joint_dense_kernel(const uint32_t* __
   unsigned int* s_small = s_joint + J * R;
   for (int i = threadIdx.x; i < J * R + n_classes * total_bins; i += NT) s_joint[i] = 0;
   const unsigned rep = threadIdx.x & (R - 1);
+  // xorshift slot map j ^ (j >> S), S = the bank bits left to the record (5 - log2 R): the bank then
+  // depends on two groups of fields; a bijection, inverted below by xor-ing all shifts of S
+  constexpr int S = R == 4 ? 3 : (R == 2 ? 4 : 5);
   __syncthreads();
   const long long groups = (n + 31) >> 5;
   const long long stride = (long long)gridDim.x * NT;
@@ -694,11 +697,17 @@ __global__ __launch_bounds__(NT) void hist_joint_dense_kernel(const uint32_t* __
     };
     if (left >= 32) {  // every group but the last: no per-record predicate
 #pragma unroll
-      for (int k = 0; k < 32; ++k) atomicAdd(&s_joint[joint_slot(rec(k)) * R + rep], 1u);
+      for (int k = 0; k < 32; ++k) {
+        const unsigned r = rec(k);
+        atomicAdd(&s_joint[(r ^ (r >> S)) * R + rep], 1u);
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < 32; ++k)
-        if (k < left) atomicAdd(&s_joint[joint_slot(rec(k)) * R + rep], 1u);
+        if (k < left) {
+        const unsigned r = rec(k);
+        atomicAdd(&s_joint[(r ^ (r >> S)) * R + rep], 1u);
+      }
     }
   }
   __syncthreads();
@@ -707,7 +716,10 @@ __global__ __launch_bounds__(NT) void hist_joint_dense_kernel(const uint32_t* __
 #pragma unroll
     for (int r = 0; r < R; ++r) cnt += s_joint[p * R + r];
     if (!cnt) continue;
-    const int j = (int)joint_slot((unsigned)p);
+    unsigned ju = (unsigned)p;
+#pragma unroll
+    for (int t = S; t < B; t += S) ju ^= (unsigned)p >> t;
+    const int j = (int)ju;
     int c = 0;
     if (n_classes > 1) {
       const unsigned lb = __builtin_amdgcn_ubfe((unsigned)j, (unsigned)spec.lsh, (unsigned)n_classes);
