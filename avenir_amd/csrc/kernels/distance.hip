@@ -57,17 +57,20 @@ __device__ __forceinline__ void topk_insert(float (&bd)[K], int (&bi)[K], float 
   }
 }
 
-// LDS carve (dynamic, 16-byte aligned): the main loop's Q / R feature chunks, the distance tile and
-// the norms, and — aliased over them once the scan is done — the per-query merge lists.  Aliasing
-// keeps a K <= 32 block at 66 KB (2 blocks per CU) and lets K = 64 fit at all (132 KB).
-constexpr int LDS_SQ = 0;
-constexpr int LDS_SR = LDS_SQ + BQ * (KC + 1) * 4;
-constexpr int LDS_SD = LDS_SR + BR * (KC + 1) * 4;
-constexpr int LDS_QN = LDS_SD + BQ * (BR + 1) * 4;
-constexpr int LDS_RN = LDS_QN + BQ * 4;
-constexpr int LDS_MAIN = LDS_RN + BR * 4;
-__host__ __device__ constexpr int knn_lds_bytes(int K) {
-  return LDS_MAIN > BQ * 4 * K * 8 ? LDS_MAIN : BQ * 4 * K * 8;
+// LDS carve (dynamic, 16-byte aligned): the query block (all D features when D <= QRES, so it is
+// staged once per block; else one KC chunk), the reference chunk, the distance tile (VALU
+// metrics) and the norms, and — aliased over them once the scan is done — the per-query merge
+// lists.  qstride = the query rows' LDS stride in floats (padded by one against bank conflicts).
+constexpr int QRES = 256;
+__host__ __device__ inline int knn_qstride(int D) { return (D <= QRES ? ((D + KC - 1) / KC) * KC : KC) + 1; }
+// the distance tile sD exists only for the VALU metrics (MET != 0 scans it for the top-k)
+__host__ __device__ inline int knn_off_sr(int qs) { return BQ * qs * 4; }
+__host__ __device__ inline int knn_off_sd(int qs) { return knn_off_sr(qs) + BR * (KC + 1) * 4; }
+__host__ __device__ inline int knn_off_qn(int qs, int met) { return knn_off_sd(qs) + (met ? BQ * (BR + 1) * 4 : 0); }
+__host__ __device__ inline int knn_off_rn(int qs, int met) { return knn_off_qn(qs, met) + BQ * 4; }
+__host__ __device__ inline int knn_lds_bytes(int K, int D, int met) {
+  const int main = knn_off_rn(knn_qstride(D), met) + BR * 4;
+  return main > BQ * 4 * K * 8 ? main : BQ * 4 * K * 8;
 }
 
 // MET: 0 = squared euclidean on MFMA (||q||^2 + ||r||^2 - 2 q.r), 1 = L1 (VALU), 2 = sum |q - r|^p
@@ -78,11 +81,12 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
     long long r_per_split, long long q_index_base, long long r_index_base, int exclude_self,
     float* __restrict__ out_d, long long* __restrict__ out_i, int kk, float pw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float(*sQ)[KC + 1] = reinterpret_cast<float(*)[KC + 1]>(smem + LDS_SQ);
-  float(*sR)[KC + 1] = reinterpret_cast<float(*)[KC + 1]>(smem + LDS_SR);
-  float(*sD)[BR + 1] = reinterpret_cast<float(*)[BR + 1]>(smem + LDS_SD);
-  float* sqn = reinterpret_cast<float*>(smem + LDS_QN);
-  float* srn = reinterpret_cast<float*>(smem + LDS_RN);
+  const int qs = knn_qstride(D);
+  float* sQ = reinterpret_cast<float*>(smem);  // row i at sQ + i * qs
+  float(*sR)[KC + 1] = reinterpret_cast<float(*)[KC + 1]>(smem + knn_off_sr(qs));
+  float(*sD)[BR + 1] = reinterpret_cast<float(*)[BR + 1]>(smem + knn_off_sd(qs));
+  float* sqn = reinterpret_cast<float*>(smem + knn_off_qn(qs, MET));
+  float* srn = reinterpret_cast<float*>(smem + knn_off_rn(qs, MET));
   float(*mD)[4][K] = reinterpret_cast<float(*)[4][K]>(smem);
   int(*mI)[4][K] = reinterpret_cast<int(*)[4][K]>(smem + BQ * 4 * K * 4);
 
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   // A query block whose features fit one chunk is staged once; reference chunks are prefetched
   // into registers one step ahead (the global loads of the next chunk / tile are in flight during
   // the MFMAs and the top-k scan of the current one).
-  const bool q_once = D <= KC;
+  const bool q_once = D <= QRES;  // the whole query block resident in LDS
   const int nchunk = (D + KC - 1) / KC;
   float pr[BR * KC / KT];
   auto load_r = [&](long long rr0, int dd0) {
@@ -121,12 +125,14 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       pr[i] = (r < re && dd0 + c < D) ? R[r * D + dd0 + c] : 0.f;
     }
   };
-  if (q_once)
-    for (int e = tid; e < BQ * KC; e += KT) {
-      const int row = e / KC, c = e % KC;
+  if (q_once) {
+    const int qc = qs - 1;
+    for (int e = tid; e < BQ * qc; e += KT) {
+      const int row = e / qc, c = e % qc;
       const long long q = q0 + row;
-      sQ[row][c] = (q < M && c < D) ? Q[q * D + c] : 0.f;
+      sQ[row * qs + c] = (q < M && c < D) ? Q[q * D + c] : 0.f;
     }
+  }
   if (rb < re) load_r(rb, 0);
   for (long long r0 = rb; r0 < re; r0 += BR) {
     const bool first_tile = r0 == rb;
@@ -143,8 +149,9 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         for (int e = tid; e < BQ * KC; e += KT) {
           const int row = e / KC, c = e % KC;
           const long long q = q0 + row;
-          sQ[row][c] = (q < M && d0 + c < D) ? Q[q * D + d0 + c] : 0.f;
+          sQ[row * qs + c] = (q < M && d0 + c < D) ? Q[q * D + d0 + c] : 0.f;
         }
+      const int qo = q_once ? d0 : 0;  // this chunk's column offset in the query rows
 #pragma unroll
       for (int i = 0; i < BR * KC / KT; ++i) {
         const int e = tid + KT * i;
@@ -161,17 +168,18 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         if (tid < BR) {
           rn_acc = half ? sq_norm<KC / 2>(sR[tid], rn_acc) : sq_norm<KC>(sR[tid], rn_acc);
         } else if (first_tile && tid < BR + BQ) {
-          qn_acc = half ? sq_norm<KC / 2>(sQ[tid - BR], qn_acc) : sq_norm<KC>(sQ[tid - BR], qn_acc);
+          qn_acc = half ? sq_norm<KC / 2>(sQ + (tid - BR) * qs + qo, qn_acc)
+                        : sq_norm<KC>(sQ + (tid - BR) * qs + qo, qn_acc);
         }
         const int li = lane & 31, lk = lane >> 5;
         // A = references (rows of the 32 x 32 block), B = queries (columns): each lane's 16
         // accumulators are 16 reference distances of ONE query
-        acc = mfma_chunk<KC>(sR[wr * 32 + li], sQ[wq * 32 + li], lk, acc);
+        acc = mfma_chunk<KC>(sR[wr * 32 + li], sQ + (wq * 32 + li) * qs + qo, lk, acc);
       } else {
         for (int c = 0; c < kend; ++c) {
           float qa[4], rv[4];
 #pragma unroll
-          for (int a = 0; a < 4; ++a) qa[a] = sQ[tq + 16 * a][c];
+          for (int a = 0; a < 4; ++a) qa[a] = sQ[(tq + 16 * a) * qs + qo + c];
 #pragma unroll
           for (int b = 0; b < 4; ++b) rv[b] = sR[tr + 16 * b][c];
 #pragma unroll
@@ -301,7 +309,8 @@ void knn_topk(const float* Q, long long M, const float* R, long long N, int D, i
   const long long per = ((N + splits - 1) / splits + BR - 1) / BR * BR;
   dim3 grid((unsigned)((M + BQ - 1) / BQ), (unsigned)splits);
   auto launch = [&](auto kern, int K) {
-    const int lds = knn_lds_bytes(K);
+    const int lds = knn_lds_bytes(K, D, metric);
+    if (lds > 160 * 1024) throw std::runtime_error("knn_topk: LDS carve exceeds 160 KiB");
     AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     kern<<<grid, KT, lds, stream>>>(Q, M, R, N, D, per, q_index_base, r_index_base, exclude_self, out_d,

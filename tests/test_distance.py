@@ -130,7 +130,8 @@ def test_categorical_modes():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,Dm,k", [(1000, 5000, 16, 5), (77, 3001, 3, 1), (513, 1000, 70, 32),
-                                       (4096, 20000, 33, 8)])
+                                       (4096, 20000, 33, 8), (257, 2000, 200, 10), (100, 1500, 300, 5),
+                                       (130, 999, 256, 64)])
 def test_knn_mfma_gpu(cuda, M, N, Dm, k):
     g = torch.Generator().manual_seed(M)
     Q, R = torch.randn(M, Dm, generator=g), torch.randn(N, Dm, generator=g)
