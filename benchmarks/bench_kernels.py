@@ -148,7 +148,7 @@ def bench_sa(args):
 def bench_knn(args):
     from avenir_amd.ops import distance as Dm
     g = torch.Generator(device="cuda").manual_seed(0)
-    for M, R, D in ((65536, 65536, 16), (16384, 1 << 20, 32)):
+    for M, R, D in ((65536, 65536, 16), (16384, 1 << 20, 32), (16384, 1 << 18, 64), (16384, 1 << 18, 256)):
         Q = torch.randn((M, D), device="cuda", generator=g)
         Rt = torch.randn((R, D), device="cuda", generator=g)
         med, _ = timeit(lambda: Dm.knn(Q, Rt, 10), iters=5, warmup=1)
