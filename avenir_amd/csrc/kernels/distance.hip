@@ -198,16 +198,28 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       __syncthreads();
       // accumulator -> distances -> this lane's top-k, no LDS round trip
       // (C/D map: col = lane&31 = query, row = (r&3) + 8(r>>2) + 4(lane>>5) = reference)
-      const float qn = sqn[my_q];
       const long long gq = q0 + my_q;
+      const float qn = gq < M ? sqn[my_q] : INFINITY;  // padded query rows never insert
+      const int jb = (int)(r0 - rb) + wr * 32 + 4 * (lane >> 5);
+      if (r0 + BR <= re && !exclude_self) {
+        // full tile, no self exclusion (uniform): 3 VALU ops + one compare per candidate
 #pragma unroll 2
-      for (int r = 0; r < 16; ++r) {
-        const int rj = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const long long gr = r0 + rj;
-        float dist = fmaxf(qn + srn[rj] - 2.f * acc[r], 0.f);
-        if (gr >= re || gq >= M) dist = INFINITY;
-        if (exclude_self && (q_index_base + gq) == (r_index_base + gr)) dist = INFINITY;
-        topk_insert<K>(bd, bi, dist, (int)(r0 - rb) + rj);
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const float dist = fmaxf(fmaf(-2.f, acc[r], qn + srn[wr * 32 + 4 * (lane >> 5) + ro]), 0.f);
+          topk_insert<K>(bd, bi, dist, jb + ro);
+        }
+      } else {
+#pragma unroll 2
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const int rj = wr * 32 + 4 * (lane >> 5) + ro;
+          const long long gr = r0 + rj;
+          float dist = fmaxf(fmaf(-2.f, acc[r], qn + srn[rj]), 0.f);
+          if (gr >= re) dist = INFINITY;
+          if (exclude_self && (q_index_base + gq) == (r_index_base + gr)) dist = INFINITY;
+          topk_insert<K>(bd, bi, dist, jb + ro);
+        }
       }
     } else {
 #pragma unroll
