@@ -387,6 +387,11 @@ __device__ T block_reduce(T v, T* red, Op op) {  // all SEL_T threads; red has >
   return r;
 }
 
+// PER > 0: every thread caches the up / low violations of its PER rows in registers once, and the
+// 13 passes of the selection (max, counts, 4 radix digits, ties, for both sides) read registers
+// instead of re-reading alpha / G / y from global memory each pass (latency-bound at one
+// workgroup).  PER = 0: no cache (any N).
+template <int PER>
 __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __restrict__ alpha,
                                                               const float* __restrict__ G,
                                                               const float* __restrict__ y, int N, int ldag, float C,
@@ -404,12 +409,32 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   const float* yb = y + (long long)b * N;
   const int words = (N + 31) / 32;
   for (int i = tid; i < words; i += SEL_T) in_up[i] = 0;
+  float cu[PER > 0 ? PER : 1], cl[PER > 0 ? PER : 1];
+  if constexpr (PER > 0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int n = tid + i * SEL_T;
+      cu[i] = n < N ? ws_violation(0, yb[n], ab[n], gb[n], C) : -INFINITY;
+      cl[i] = n < N ? ws_violation(1, yb[n], ab[n], gb[n], C) : -INFINITY;
+    }
+  }
+  // violation of row n = tid + i * SEL_T on side `which`
+  auto viol = [&](int which, int i, int n) -> float {
+    if constexpr (PER > 0) {
+      float v = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        if (j == i) v = which ? cl[j] : cu[j];
+      return v;
+    } else {
+      return ws_violation(which, yb[n], ab[n], gb[n], C);
+    }
+  };
 
   float mu = -INFINITY, ml = -INFINITY;
-  for (int n = tid; n < N; n += SEL_T) {
-    const float yn = yb[n], an = ab[n], gn = gb[n];
-    mu = fmaxf(mu, ws_violation(0, yn, an, gn, C));
-    ml = fmaxf(ml, ws_violation(1, yn, an, gn, C));
+  for (int i = 0, n = tid; n < N; ++i, n += SEL_T) {
+    mu = fmaxf(mu, viol(0, i, n));
+    ml = fmaxf(ml, viol(1, i, n));
   }
   auto fmax_op = [](float p, float q) { return fmaxf(p, q); };
   auto add_op = [](unsigned p, unsigned q) { return p + q; };
@@ -420,7 +445,7 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   int npick[2] = {0, 0};
   for (int which = 0; which < 2; ++which) {
     unsigned e = 0;
-    for (int n = tid; n < N; n += SEL_T) e += ws_violation(which, yb[n], ab[n], gb[n], C) > -INFINITY ? 1u : 0u;
+    for (int i = 0, n = tid; n < N; ++i, n += SEL_T) e += viol(which, i, n) > -INFINITY ? 1u : 0u;
     e = block_reduce(e, redu, add_op);
     const unsigned k = e < (unsigned)h ? e : (unsigned)h;
     npick[which] = (int)k;
@@ -430,8 +455,8 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
       if (tid < 256) hist[tid] = 0;
       __syncthreads();
       const unsigned prefix = s_prefix, mask = s_mask;
-      for (int n = tid; n < N; n += SEL_T) {
-        const float v = ws_violation(which, yb[n], ab[n], gb[n], C);
+      for (int i = 0, n = tid; n < N; ++i, n += SEL_T) {
+        const float v = viol(which, i, n);
         if (v > -INFINITY) {
           const unsigned key = order_key(v);
           if ((key & mask) == prefix) atomicAdd(&hist[(key >> (8 * d)) & 255u], 1u);
@@ -462,11 +487,11 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
     unsigned eq_base = 0;  // ties seen in earlier SEL_T blocks (block-uniform)
     const int lane = tid & 63, wv = tid >> 6;
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int n0 = 0; n0 < N; n0 += SEL_T) {
+    for (int n0 = 0, i = 0; n0 < N; n0 += SEL_T, ++i) {
       const int n = n0 + tid;
       bool eq = false;
       if (n < N) {
-        const float v = ws_violation(which, yb[n], ab[n], gb[n], C);
+        const float v = viol(which, i, n);
         if (v > -INFINITY) {
           const unsigned key = order_key(v);
           if (key > T) pick[which][atomicAdd(&s_gt, 1u)] = n;
@@ -556,7 +581,10 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
                    long long* ws, bool* ok, float* gap, hipStream_t stream) {
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
-  smo_ws_select_kernel<<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  const int per = (N + SEL_T - 1) / SEL_T;
+  if (per <= 8) smo_ws_select_kernel<8><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  else if (per <= 16) smo_ws_select_kernel<16><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  else smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -250,9 +250,16 @@ class ForestBuilder:
             last = p.stopping == "maxDepth" and bool((fr.depth + 1 >= p.max_depth).all())
             item_left = (torch.zeros(inode.size, dtype=torch.int32) if last
                          else FO.forest_part_count(cb, inode, istart, ilen, feat_eff, thr))
-            # ---- the ONE host copy of the level ----
-            pack = [feat_eff.cpu(), thr.cpu(), left.cpu(), tot.cpu(), imp.double().cpu(), item_left.cpu()]
-            f_h, t_h, l_h, tot_h, imp_h, il_h = [x.numpy() for x in pack]
+            # ---- the ONE host copy of the level: every per-node result packed as int64 words ----
+            parts = [feat_eff.long().view(-1), thr.long().view(-1), left.long().reshape(-1), tot.long().reshape(-1),
+                     imp.double().view(torch.int64).view(-1), item_left.to(dev).long().view(-1)]
+            sizes = [x.numel() for x in parts]
+            flat = torch.cat(parts).cpu().numpy()
+            segs = np.split(flat, np.cumsum(sizes)[:-1])
+            f_h, t_h = segs[0], segs[1]
+            l_h, tot_h = segs[2].reshape(A, C), segs[3].reshape(A, C)
+            imp_h = segs[4].view(np.float64)
+            il_h = segs[5]
             ids = fr.node
             tbl["counts"][ids] = tot_h
             tbl["imp"][ids] = imp_h
