@@ -332,6 +332,7 @@ void knn_topk(const float* Q, long long M, const float* R, long long N, int D, i
   if (k <= 1) launch(knn_mfma_kernel<1, MET>, 1);                        \
   else if (k <= 4) launch(knn_mfma_kernel<4, MET>, 4);                   \
   else if (k <= 8) launch(knn_mfma_kernel<8, MET>, 8);                   \
+  else if (k <= 10) launch(knn_mfma_kernel<10, MET>, 10);                \
   else if (k <= 16) launch(knn_mfma_kernel<16, MET>, 16);                \
   else if (k <= 32) launch(knn_mfma_kernel<32, MET>, 32);                \
   else if (k <= 64) launch(knn_mfma_kernel<64, MET>, 64);                \

@@ -1,0 +1,9 @@
+#!/bin/bash
+set -eo pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_distance.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r2s_tests.log 2>&1
+timeout -k 10 300 python -u benchmarks/bench_kernels.py --only knn > gpurun_out/r2s_knn.log 2>&1
+timeout -k 10 300 python -u benchmarks/rf_phases.py > gpurun_out/r2s_rf.log 2>&1
+timeout -k 10 600 python -u benchmarks/bench_vs_reference.py --only nb,rf,knn > gpurun_out/r2s_vsref.log 2>&1
+tail -2 gpurun_out/r2s_tests.log; cat gpurun_out/r2s_knn.log gpurun_out/r2s_rf.log; grep '^{' gpurun_out/r2s_vsref.log
