@@ -463,19 +463,36 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
         }
       }
       __syncthreads();
-      if (tid == 0) {  // the digit holding the krem-th largest key
-        unsigned cum = 0, krem = s_krem;
-        for (int dg = 255; dg >= 0; --dg) {
-          if (cum + hist[dg] >= krem) {
-            s_prefix = prefix | ((unsigned)dg << (8 * d));
-            s_mask = mask | (255u << (8 * d));
-            s_krem = krem - cum;
-            break;
-          }
-          cum += hist[dg];
+      if (tid < 64) {  // the digit holding the krem-th largest key: one wave scans the 256 bins
+        const int l = tid;
+        unsigned c[4], sum = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {  // lane l holds digits 255 - 4l .. 252 - 4l (descending)
+          c[t] = hist[255 - (4 * l + t)];
+          sum += c[t];
         }
-        s_gt = 0;
-
+        unsigned inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned y = __shfl_up(inc, o, 64);
+          if (l >= o) inc += y;
+        }
+        const unsigned krem = s_krem, excl = inc - sum;
+        if (excl < krem && krem <= inc) {  // exactly one lane
+          unsigned cum = excl;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (cum + c[t] >= krem) {
+              const unsigned dg = 255u - (unsigned)(4 * l + t);
+              s_prefix = prefix | (dg << (8 * d));
+              s_mask = mask | (255u << (8 * d));
+              s_krem = krem - cum;
+              break;
+            }
+            cum += c[t];
+          }
+        }
+        if (l == 0) s_gt = 0;
       }
       __syncthreads();
     }

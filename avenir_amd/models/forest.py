@@ -345,7 +345,16 @@ class ForestBuilder:
             self.level_times.append(time.perf_counter() - tl)
         self.stats = {"rows_buffered": R, "levels": level, "nodes": n_nodes, "hist_rows": n_hist_rows,
                       "chunk": chunk, "seconds": time.perf_counter() - t0}
-        return self._to_trees(tbl, n_nodes, Tn, space, t)
+        # thousands of small node objects: keep the cyclic GC from pausing in the middle (a gen-2
+        # pass over every live object cost 50-100 ms here, more than the whole device build)
+        import gc
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            return self._to_trees(tbl, n_nodes, Tn, space, t)
+        finally:
+            if was:
+                gc.enable()
 
     # ------------------------------------------------------------------------------------------
     def _to_trees(self, tbl, n_nodes, Tn, space, t: Table) -> list[T.DecisionTree]:
