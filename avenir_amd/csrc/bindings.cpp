@@ -1078,7 +1078,7 @@ at::Tensor kmeans_update(const at::Tensor& flat, at::Tensor& C2, at::Tensor& Cn,
   const int64_t K = Cn.numel(), R = frozen.numel();
   TORCH_CHECK(K % 2 == 0 && C2.numel() == K * D && run_of.numel() == K, "layout mismatch");
   TORCH_CHECK(R >= 1 && R <= 16 && flat.numel() == K * (D + 1) + R, "flat must be [K * (D + 1) + R]");
-  auto moves = at::empty({R}, C2.options());
+  auto moves = at::empty({2 * R}, C2.options());  // [max shift per run | total squared shift per run]
   DevGuard g(C2.device());
   avk::kmeans_update(flat.data_ptr<double>(), (int)K, (int)D, (int)R, run_of.data_ptr<int>(), frozen.data_ptr<uint8_t>(),
                      C2.data_ptr<float>(), Cn.data_ptr<float>(), moves.data_ptr<float>(), cur_stream(C2));

@@ -323,8 +323,12 @@ __global__ __launch_bounds__(1024) void kmeans_update_kernel(const double* __res
                                                              float* __restrict__ moves) {
   extern __shared__ float mv2[];  // [K]
   __shared__ unsigned mx[MAX_RUNS];
+  __shared__ float ss[MAX_RUNS];  // per run: sum over centroids of the squared shift (sklearn's tol)
   for (int c = threadIdx.x; c < K; c += 1024) mv2[c] = 0.f;
-  if (threadIdx.x < MAX_RUNS) mx[threadIdx.x] = 0u;
+  if (threadIdx.x < MAX_RUNS) {
+    mx[threadIdx.x] = 0u;
+    ss[threadIdx.x] = 0.f;
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < K * D; i += 1024) {
     const int c = i / D, d = i - c * D;
@@ -349,9 +353,13 @@ __global__ __launch_bounds__(1024) void kmeans_update_kernel(const double* __res
     }
     Cn[c] = s;
     atomicMax(&mx[r], __float_as_uint(sqrtf(mv2[c])));  // non-negative floats order like their bits
+    atomicAdd(&ss[r], mv2[c]);
   }
   __syncthreads();
-  if (threadIdx.x < R) moves[threadIdx.x] = __uint_as_float(mx[threadIdx.x]);
+  if (threadIdx.x < R) {
+    moves[threadIdx.x] = __uint_as_float(mx[threadIdx.x]);  // max centroid shift (Java criterion)
+    moves[R + threadIdx.x] = ss[threadIdx.x];               // total squared shift
+  }
 }
 
 // Kernel variant for (D, K, R): the MFMA kernel when its accumulators fit (<= 16 blocks of 16

@@ -93,11 +93,18 @@ def kmeans_step(X: torch.Tensor, Cs: list[torch.Tensor], want_assign: bool = Fal
 class KMeans:
     def __init__(self, n_clusters: int | list[int] = 3, n_init: int = 1, max_iter: int = 300,
                  tol: float = 1e-4, init: str = "k-means++", seed: int = 0, comm: Comm | None = None,
-                 recovery: RecoveryConfig | None = None):
+                 recovery: RecoveryConfig | None = None, tol_mode: str = "shift"):
         self.ks = [n_clusters] if isinstance(n_clusters, int) else list(n_clusters)
         self.n_init = n_init
         self.max_iter = max_iter
         self.tol = tol
+        # "shift": a run converges when every centroid moves <= tol (J/cluster/ClusterData.java:
+        # movement > centroidShiftThreshold keeps a cluster active); "sklearn": when the summed
+        # squared centroid shift <= tol x the mean per-feature variance of the data (P/unsupv/
+        # cluster.py uses scikit-learn's KMeans and its tol)
+        if tol_mode not in ("shift", "sklearn"):
+            raise ValueError(f"unknown tol_mode {tol_mode}")
+        self.tol_mode = tol_mode
         self.init = init
         self.seed = seed
         self.comm = comm
@@ -194,6 +201,7 @@ class KMeans:
         distributed, one update launch and a 4-byte-per-run host read of the centroid movement."""
         comm = self.comm or get_comm()
         X = X.float().contiguous()
+        self._tol_eff = self._effective_tol(X, comm)
         Xp = self._padded(X)
         specs = [(k, self.seed * 1009 + k * 31 + r) for k in self.ks for r in range(self.n_init)]
         runs = [KMeansRun(k, sd, self._init_centroids(X, k, sd)) for k, sd in specs]
@@ -209,6 +217,24 @@ class KMeans:
             if r.k not in self.best or r.sse < self.best[r.k].sse:
                 self.best[r.k] = r
         return self
+
+    def _effective_tol(self, X: torch.Tensor, comm) -> float:
+        if self.tol_mode == "shift":
+            return self.tol
+        # global mean of per-feature variances (sums / squares / count all-reduced)
+        st = torch.stack([X.double().sum(0), (X.double() ** 2).sum(0)])
+        n = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=X.device)
+        if comm.is_distributed:
+            comm.all_reduce(st)
+            comm.all_reduce(n)
+        mean = st[0] / n
+        var = (st[1] / n - mean * mean).clamp_min(0)
+        return float(var.mean()) * self.tol
+
+    def _converged(self, max_shift: float, sq_shift: float) -> bool:
+        if self.tol_mode == "shift":
+            return max_shift <= self.tol
+        return sq_shift <= self._tol_eff
 
     def _fit_gpu_group(self, D: int, Xp: torch.Tensor, grp: list[KMeansRun], comm,
                        lp: IterationLoop) -> None:
@@ -245,7 +271,7 @@ class KMeans:
                 if frozen_h[r]:
                     continue
                 run.iterations = it + 1
-                if mv[r] <= self.tol:
+                if self._converged(mv[r], mv[R + r]):
                     run.converged = True
                     frozen_h[r] = 1
                     changed = True
@@ -298,11 +324,12 @@ class KMeans:
                 Cc = run.centroids
                 newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1).view(-1, 1),
                                    Cc.double()).float()
-                mv = float(((newC - Cc) ** 2).sum(1).sqrt().max())
+                sh2 = ((newC - Cc) ** 2).sum(1)
+                mv, sq = float(sh2.sqrt().max()), float(sh2.sum())
                 run.centroids = newC
                 run.history.append(float(sse))
                 run.iterations = it + 1
-                if mv <= self.tol:
+                if self._converged(mv, sq):
                     run.converged = True
                 else:
                     still.append(i)

@@ -130,7 +130,7 @@ def bench_kmeans(a):
     centers = torch.randn((k, d), device="cuda", generator=g) * 4
     X = centers[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randn((n, d), device="cuda",
                                                                                       generator=g)
-    g_s, km = gpu_time(lambda: KMeans(k, n_init=inits, max_iter=it, tol=1e-4).fit(X))
+    g_s, km = gpu_time(lambda: KMeans(k, n_init=inits, max_iter=it, tol=1e-4, tol_mode="sklearn").fit(X))
     run = km.best[k]
     xn = X.cpu().numpy()
     c_s, sk = cpu_time(lambda: SKKMeans(k, n_init=inits, max_iter=it, tol=1e-4, random_state=0).fit(xn))

@@ -250,3 +250,18 @@ def test_grouped_similarity_gpu(cuda):
     ig, jg, dg = GroupedRecordSimilarity().pairs(X.to(cuda), groups.to(cuda))
     assert torch.equal(ic, ig.cpu()) and torch.equal(jc, jg.cpu())
     assert torch.allclose(dc, dg.cpu(), atol=1e-4)
+
+
+def test_kmeans_sklearn_tolerance_mode():
+    """tol_mode='sklearn': converged when the summed squared centroid shift <= tol x the mean
+    feature variance (scikit-learn's rule, P/unsupv/cluster.py); 'shift' keeps the Java
+    per-centroid movement threshold.  The relative rule stops no later than the absolute one."""
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(4000, 3, generator=g) * 3 + torch.randint(0, 5, (4000, 1), generator=g) * 4.0
+    a = KMeans(5, seed=1, tol=1e-4, tol_mode="shift").fit(X)
+    b = KMeans(5, seed=1, tol=1e-4, tol_mode="sklearn").fit(X)
+    assert b.best[5].iterations <= a.best[5].iterations
+    assert b._tol_eff == pytest.approx(1e-4 * float(X.double().var(0, unbiased=False).mean()), rel=1e-9)
+    assert b.best[5].sse == pytest.approx(a.best[5].sse, rel=1e-2)
+    with pytest.raises(ValueError):
+        KMeans(3, tol_mode="bogus")
