@@ -292,7 +292,8 @@ __global__ __launch_bounds__(64) void smo_ws_kernel(const float* __restrict__ Ka
 // workgroup's 4 waves gather K[ws, ws] into LDS, wave 0 loads (y, alpha, G) of the working set,
 // runs ws_smo_loop, scatters the new alphas, writes dA = (alpha_new - alpha_old) y for the
 // gradient update and adds its iteration count to inner_total.
-__global__ __launch_bounds__(256) void smo_ws_solve_fused_kernel(const float* __restrict__ K, int N,
+constexpr int SOLVE_T = 1024;  // all 16 waves gather the Q x Q block (memory parallelism), wave 0 solves
+__global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float* __restrict__ K, int N,
                                                                  const long long* __restrict__ ws,
                                                                  const bool* __restrict__ ok, float* __restrict__ alpha,
                                                                  const float* __restrict__ G, const float* __restrict__ yv,
@@ -304,14 +305,27 @@ __global__ __launch_bounds__(256) void smo_ws_solve_fused_kernel(const float* __
   __shared__ long long s_ws[Q];
   __shared__ int s_ok[Q];
   const int b = blockIdx.x, tid = threadIdx.x;
-  for (int q = tid; q < Q; q += 256) {
+  for (int q = tid; q < Q; q += SOLVE_T) {
     const bool o = ok[(long long)b * Q + q];
     s_ok[q] = o ? 1 : 0;
     s_ws[q] = o ? ws[(long long)b * Q + q] : 0;
   }
   __syncthreads();
   const float* Kb = K + (long long)b * N * N;
-  for (int e = tid; e < Q * Q; e += 256) Ks[e / Q][e % Q] = Kb[s_ws[e / Q] * N + s_ws[e % Q]];
+  // scattered 4-byte gathers from the N x N kernel matrix: 16 per thread, all issued before the
+  // LDS stores (latency-bound otherwise)
+  constexpr int PER = Q * Q / SOLVE_T;
+  float kv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + i * SOLVE_T;
+    kv[i] = Kb[s_ws[e / Q] * N + s_ws[e % Q]];
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + i * SOLVE_T;
+    Ks[e / Q][e % Q] = kv[i];
+  }
   __syncthreads();
   if (tid >= 64) return;  // wave 0 solves; no block barrier follows
   const int lane = tid;
@@ -616,7 +630,7 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
                         long long* inner_total, hipStream_t stream) {
   if (B <= 0) return;
-  smo_ws_solve_fused_kernel<<<B, 256, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
+  smo_ws_solve_fused_kernel<<<B, SOLVE_T, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
                                                    inner_total);
   AV_HIP_CHECK(hipGetLastError());
 }
