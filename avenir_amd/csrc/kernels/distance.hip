@@ -7,13 +7,16 @@
 // matrix is never materialised.  k-means assignment (J/cluster/KmeansCluster.java:154-172) is the
 // k = 1 case of the same kernel.
 //
-// Block = 256 threads = 4 waves, a 64-query x 64-reference tile per step (L1 / Lp metrics: the same
-// tile on the VALU, 4 x 4 distances per thread).  Each wave computes a
+// Block = 256 threads = 4 waves, a 64-query x 64-reference tile per step.  Each wave computes a
 // 32 x 32 block of dot products with the exact f32-input MFMA v_mfma_f32_32x32x2_f32 (bit-exact
-// fmaf chain; on gfx950 it runs at the f32 vector rate and leaves the VALU free for the top-k), the
-// tile is turned into squared distances ||q||^2 + ||r||^2 - 2 q.r in LDS, then 4 threads per query
-// scan 16 candidates each against a private register-resident sorted top-K (insertion is rare once
-// the list has warmed up), and the 4 partial lists are merged at the end.
+// fmaf chain), references as the A operand and queries as the B operand, so each lane's 16
+// accumulators are 16 reference distances of ONE query: ||q||^2 + ||r||^2 - 2 q.r goes straight
+// from the accumulators into that lane's register-resident sorted top-K (insertion is rare once
+// the list has warmed up) — no LDS distance tile, no barrier before the scan.  The query block
+// stays in LDS for D <= 256; reference chunks are register-prefetched one step ahead.  The four
+// partial lists of a query (2 waves x 2 lane halves) are merged at the end in LDS aliased over the
+// tiles.  L1 / Lp metrics run the same tile on the VALU (4 x 4 distances per thread) through an
+// LDS distance tile scanned by 4 threads per query.
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
