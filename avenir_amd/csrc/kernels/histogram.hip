@@ -9,6 +9,11 @@
 //     J/explore/CramerCorrelation.java:162-182).
 // K4  Markov bigram histogram  out[c][s][s']  (J/markov/MarkovStateTransitionModel.java:116-133).
 //
+// Row-packed records (all codes + one-hot class of a record in <= 15 bits): hist_joint_dense_kernel
+// counts each record with ONE LDS atomic into the block's joint table (dense B-bit record stream,
+// 1.63 B/record for churn) and takes the class-conditional marginals once per block — the NB
+// training headline; hist_joint_kernel / hist_rowpack_kernel are the 16-bit-word variants.
+//
 // Data layout (SoA, feature-major): codes are uint8 [F][ld] with ld % 16 == 0, so every lane
 // streams 16 rows per 128-bit load.  A code is either < bins[f] or the missing sentinel 255.
 //

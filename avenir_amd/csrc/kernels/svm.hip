@@ -358,7 +358,8 @@ __global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float
 // duplicate mask, the [B, Q, N] row gather and the batched GEMV).
 //
 // smo_ws_select_kernel: one 1024-thread workgroup per problem.  The "up" / "low" violation
-// values are recomputed from (alpha, G, y) in every pass (N floats x 3 from L2); the gap is
+// values are computed from (alpha, G, y) once into registers (N <= 16384; else every pass re-reads
+// them from L2); the gap is
 // max(up) + max(low); the h largest of each set are found by an exact 4-pass 8-bit radix select
 // on order-preserving float keys (LDS histogram), collected with LDS counters, and written in
 // ascending index order (deterministic working sets).  A low-set index already in the up set is
