@@ -1,3 +1,9 @@
+#include <cstring>
+#include <thread>
+#include <unistd.h>
+#include <sys/stat.h>
+#include <sys/mman.h>
+#include <fcntl.h>
 // pybind11 bindings for avenir_amd._C — the only translation unit that includes torch.
 //
 // Each binding validates device / dtype / contiguity / shape on the host BEFORE launching (a bad
@@ -1398,6 +1404,206 @@ std::vector<at::Tensor> linear_act_bwd(const at::Tensor& dY, const at::Tensor& Y
   return {dZ, part.sum(0)};
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1 on the device (csv.hip): upload the file through a ring of pinned staging buffers (host
+// copies from the page cache overlap the DMA of the previous slot), index the lines and parse
+// every column on the GPU.  specs: the host parser's tuples (ordinal, kind, vocab, bucket_width,
+// bucket_offset, max_code, wide); kinds CAT / BUCKET / FLOAT.  Returns (columns, rows, short rows).
+#define BIND_HIP_CHECK(expr)                                                         \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    TORCH_CHECK(_e == hipSuccess, #expr, " failed: ", hipGetErrorString(_e));        \
+  } while (0)
+
+static uint32_t fnv1a_fold(const std::string& v) {
+  uint32_t h = 2166136261u;
+  for (unsigned char c : v) h = (h ^ c) * 16777619u;
+  return h ^ (h >> 15);
+}
+
+py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std::string& delim, bool skip_header,
+                           int64_t rank, int64_t world, const at::Tensor& like) {
+  CHECK_DEV(like);
+  TORCH_CHECK(delim.size() == 1, "device CSV parse: single-character delimiter");
+  int fd = ::open(path.c_str(), O_RDONLY);
+  TORCH_CHECK(fd >= 0, "cannot open ", path);
+  struct stat st;
+  TORCH_CHECK(fstat(fd, &st) == 0, "cannot stat ", path);
+  const int64_t size = (int64_t)st.st_size;
+  const int64_t padded = std::max<int64_t>(16, (size + 15) / 16 * 16);
+  auto dopt = like.options().dtype(at::kByte);
+  auto dev = at::empty({padded}, dopt);
+  DevGuard g(like.device());
+  hipStream_t stream = cur_stream(like);
+  if (padded > size) BIND_HIP_CHECK(hipMemsetAsync(dev.data_ptr<uint8_t>() + size, 0, padded - size, stream));
+  if (size > 0) {
+    const char* map = static_cast<const char*>(mmap(nullptr, (size_t)size, PROT_READ, MAP_PRIVATE, fd, 0));
+    TORCH_CHECK(map != MAP_FAILED, "mmap failed for ", path);
+    madvise(const_cast<char*>(map), (size_t)size, MADV_SEQUENTIAL);
+    constexpr int SLOTS = 4;
+    constexpr int64_t SLOT = 64LL << 20;
+    static void* ring[SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+    static hipEvent_t done[SLOTS];
+    if (!ring[0])
+      for (int i = 0; i < SLOTS; ++i) {
+        BIND_HIP_CHECK(hipHostMalloc(&ring[i], SLOT, hipHostMallocDefault));
+        BIND_HIP_CHECK(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+      }
+    int64_t k = 0;
+    for (int64_t off = 0; off < size; off += SLOT, ++k) {
+      const int slot = (int)(k % SLOTS);
+      const int64_t len = std::min(SLOT, size - off);
+      if (k >= SLOTS) BIND_HIP_CHECK(hipEventSynchronize(done[slot]));  // the slot's last DMA is done
+      {  // page cache -> pinned slot with 4 threads
+        std::vector<std::thread> th;
+        const int T = 4;
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t] {
+            const int64_t a = len * t / T, b = len * (t + 1) / T;
+            std::memcpy(static_cast<char*>(ring[slot]) + a, map + off + a, (size_t)(b - a));
+          });
+        for (auto& x : th) x.join();
+      }
+      BIND_HIP_CHECK(hipMemcpyAsync(dev.data_ptr<uint8_t>() + off, ring[slot], (size_t)len, hipMemcpyHostToDevice,
+                                  stream));
+      BIND_HIP_CHECK(hipEventRecord(done[slot], stream));
+    }
+    munmap(const_cast<char*>(map), (size_t)size);
+  }
+  ::close(fd);
+  // ---- line index ----
+  const int64_t nch = std::max<int64_t>(1, avk::csv_chunks(size));
+  auto counts = at::zeros({nch}, like.options().dtype(at::kInt));
+  avk::csv_newline_counts(dev.data_ptr<uint8_t>(), size, reinterpret_cast<unsigned*>(counts.data_ptr<int>()), stream);
+  auto c64 = counts.to(at::kLong);
+  auto incl = c64.cumsum(0);
+  auto offsets = (incl - c64).contiguous();
+  const int64_t nl = size > 0 ? incl[-1].item<int64_t>() : 0;
+  uint8_t last = '\n';
+  if (size > 0) BIND_HIP_CHECK(hipMemcpy(&last, dev.data_ptr<uint8_t>() + size - 1, 1, hipMemcpyDeviceToHost));
+  const bool tail = size > 0 && last != '\n';
+  auto pos = at::empty({nl + (tail ? 1 : 0)}, like.options().dtype(at::kLong));
+  if (nl) avk::csv_newline_positions(dev.data_ptr<uint8_t>(), size, reinterpret_cast<long long*>(offsets.data_ptr<int64_t>()),
+                                     reinterpret_cast<long long*>(pos.data_ptr<int64_t>()), stream);
+  if (tail) pos.narrow(0, nl, 1).fill_(size);
+  auto starts = at::cat({at::zeros({1}, pos.options()), pos.narrow(0, 0, std::max<int64_t>(0, pos.numel() - 1)) + 1});
+  starts = starts.narrow(0, 0, pos.numel());
+  auto ends = pos;
+  // blank lines (empty after dropping a trailing CR) are skipped, as in the host parser
+  if (pos.numel()) {
+    auto lens = ends - starts;
+    auto lastc = dev.index({(ends - 1).clamp_min(0)}).to(at::kLong);
+    auto eff = lens - ((lastc == '\r') & (lens > 0)).to(at::kLong);
+    auto keep = eff > 0;
+    if (!keep.all().item<bool>()) {
+      auto idx = at::nonzero(keep).view({-1});
+      starts = starts.index({idx});
+      ends = ends.index({idx});
+    }
+  }
+  if (skip_header && starts.numel()) {
+    starts = starts.narrow(0, 1, starts.numel() - 1);
+    ends = ends.narrow(0, 1, ends.numel() - 1);
+  }
+  const int64_t total = starts.numel();
+  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
+  // this rank's contiguous balanced row range (data/table.py shard_range)
+  const int64_t base = total / world, rem = total % world;
+  const int64_t row_begin = rank * base + std::min(rank, rem);
+  const int64_t n = base + (rank < rem ? 1 : 0);
+  starts = starts.narrow(0, row_begin, n).contiguous();
+  ends = ends.narrow(0, row_begin, n).contiguous();
+  // ---- specs, vocabulary tables, outputs ----
+  const int64_t ld = std::max<int64_t>(16, (n + 15) / 16 * 16);
+  struct HostSpec {
+    int ordinal, kind, wide, max_code, bucket_offset, tab_off, tab_mask, vbase;
+    double bucket_width;
+    unsigned long long out;
+  };
+  TORCH_CHECK(avk::csv_devspec_bytes() == (int)sizeof(HostSpec), "DevSpec layout mismatch");
+  std::vector<HostSpec> hs;
+  std::vector<int> tabs, voff, vlen;
+  std::string vbytes;
+  std::vector<at::Tensor> outs;
+  std::vector<std::pair<int, int>> order;  // (ordinal, spec index) to sort by ordinal
+  int idx = 0;
+  for (auto item : specs_py) {
+    auto t = item.cast<py::tuple>();
+    HostSpec sp{};
+    sp.ordinal = t[0].cast<int>();
+    sp.kind = t[1].cast<int>();
+    auto vocab = t[2].cast<std::vector<std::string>>();
+    sp.bucket_width = t[3].cast<double>();
+    sp.bucket_offset = t[4].cast<int>();
+    sp.max_code = t[5].cast<int>();
+    sp.wide = t.size() > 6 && t[6].cast<bool>() ? 1 : 0;
+    TORCH_CHECK(sp.ordinal >= 0 && sp.kind >= 0 && sp.kind <= 2, "device CSV parse: CAT / BUCKET / FLOAT columns");
+    if (sp.kind == 1) TORCH_CHECK(sp.bucket_width > 0, "bucket width must be > 0");
+    at::Tensor o;
+    if (sp.kind == 2) {
+      o = at::empty({std::max<int64_t>(n, 1)}, like.options().dtype(at::kFloat));
+    } else {
+      o = sp.wide ? at::full({ld}, 65535, like.options().dtype(at::kUInt16)) : at::full({ld}, 255, dopt);
+    }
+    sp.out = reinterpret_cast<unsigned long long>(o.data_ptr());
+    if (sp.kind == 0) {
+      TORCH_CHECK(vocab.size() <= (sp.wide ? 65535u : 255u), "categorical cardinality exceeds the code width");
+      size_t sz = 16;
+      while (sz < 2 * vocab.size()) sz <<= 1;
+      sp.tab_off = (int)tabs.size();
+      sp.tab_mask = (int)sz - 1;
+      sp.vbase = (int)voff.size();
+      tabs.resize(tabs.size() + sz, -1);
+      for (size_t i = 0; i < vocab.size(); ++i) {
+        uint32_t h = fnv1a_fold(vocab[i]) & (uint32_t)(sz - 1);
+        bool dup = false;
+        while (tabs[sp.tab_off + h] >= 0) {
+          if (vocab[(size_t)tabs[sp.tab_off + h]] == vocab[i]) { dup = true; break; }
+          h = (h + 1) & (uint32_t)(sz - 1);
+        }
+        if (!dup) tabs[sp.tab_off + h] = (int)i;
+      }
+      for (auto& v : vocab) {
+        voff.push_back((int)vbytes.size());
+        vlen.push_back((int)v.size());
+        vbytes += v;
+      }
+    }
+    hs.push_back(sp);
+    outs.push_back(o);
+    order.push_back({sp.ordinal, idx++});
+  }
+  TORCH_CHECK(hs.size() <= 32, "device CSV parse: at most 32 columns");
+  std::stable_sort(order.begin(), order.end());
+  std::vector<HostSpec> sorted;
+  int max_ord = 0;
+  for (auto& pr : order) {
+    sorted.push_back(hs[(size_t)pr.second]);
+    max_ord = std::max(max_ord, pr.first);
+  }
+  auto hopt = at::TensorOptions().dtype(at::kByte);
+  auto spec_h = at::empty({(int64_t)(sorted.size() * sizeof(HostSpec))}, hopt);
+  if (!sorted.empty()) std::memcpy(spec_h.data_ptr<uint8_t>(), sorted.data(), sorted.size() * sizeof(HostSpec));
+  auto to_i32 = [&](const std::vector<int>& v) {
+    auto t = at::empty({(int64_t)std::max<size_t>(1, v.size())}, at::TensorOptions().dtype(at::kInt));
+    if (!v.empty()) std::memcpy(t.data_ptr<int>(), v.data(), v.size() * sizeof(int));
+    return t.to(like.device());
+  };
+  auto spec_d = spec_h.to(like.device());
+  auto tabs_d = to_i32(tabs), voff_d = to_i32(voff), vlen_d = to_i32(vlen);
+  auto vb_h = at::empty({(int64_t)std::max<size_t>(1, vbytes.size())}, hopt);
+  if (!vbytes.empty()) std::memcpy(vb_h.data_ptr<uint8_t>(), vbytes.data(), vbytes.size());
+  auto vb_d = vb_h.to(like.device());
+  auto bad = at::zeros({1}, like.options().dtype(at::kLong));
+  avk::csv_parse_rows(dev.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(starts.data_ptr<int64_t>()),
+                      reinterpret_cast<const long long*>(ends.data_ptr<int64_t>()), n, delim[0], spec_d.data_ptr<uint8_t>(),
+                      (int)sorted.size(), max_ord, tabs_d.data_ptr<int>(), voff_d.data_ptr<int>(), vlen_d.data_ptr<int>(),
+                      vb_d.data_ptr<uint8_t>(), reinterpret_cast<unsigned long long*>(bad.data_ptr<int64_t>()), stream);
+  py::list cols;
+  for (auto& o : outs) cols.append(o);
+  return py::make_tuple(cols, n, bad, total, row_begin);
+}
+
 // K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
 // are joined with every row whose (k-1)-prefix equals their (k-1)-suffix -> int32 [M, k+1].
 at::Tensor gsp_join(const at::Tensor& X, int64_t lo, int64_t hi) {
@@ -1632,6 +1838,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("forest_part_count", &forest_part_count);
   m.def("forest_part_scatter", &forest_part_scatter);
   m.def("forest_bootstrap", &forest_bootstrap);
+  m.def("csv_parse_device", &csv_parse_device);
   m.def("forest_predict_bin", &forest_predict_bin);
   m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0);
   m.def("linear_act_bwd", &linear_act_bwd);

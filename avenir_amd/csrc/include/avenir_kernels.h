@@ -174,6 +174,15 @@ void class_histogram_dense(const uint32_t* dense, long long n, int B, const int*
                            int nfeat, int label_shift, int label_width, const int* d_bins, const int* d_offs,
                            int total_bins, int n_classes, int count_labels, unsigned long long* out,
                            hipStream_t stream);
+// K1 device CSV parse (csv.hip)
+long long csv_chunks(long long size);
+void csv_newline_counts(const uint8_t* bytes, long long size, unsigned* counts, hipStream_t stream);
+void csv_newline_positions(const uint8_t* bytes, long long size, const long long* offsets, long long* pos,
+                           hipStream_t stream);
+void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long long* ends, long long n, char delim,
+                    const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
+                    const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream);
+int csv_devspec_bytes();
 void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
                        unsigned rate32, int* tile_cnt, hipStream_t stream);
 void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,

@@ -1,0 +1,250 @@
+// K1 on the device: schema-driven CSV -> columnar encode.
+//
+// The reference parses every record with String.split + schema lookups inside each mapper
+// (e.g. J/bayesian/BayesianDistribution.java mapper); the host path here is the multi-threaded
+// mmap parser (csrc/host/csv.cpp).  For large files bound for the GPU the raw bytes are uploaded
+// once and parsed where they will be used:
+//   1. csv_nl_count_kernel   : newlines per 64 KiB chunk (16-byte loads, SWAR byte compare);
+//   2. (device exclusive scan of the chunk counts);
+//   3. csv_nl_pos_kernel     : every newline's byte offset, in order (block scan of per-thread
+//                              counts inside each chunk);
+//   4. csv_parse_kernel      : one thread per record walks its fields once and writes every
+//                              schema column: dictionary codes (FNV-1a open-addressing table per
+//                              field, verified against the vocabulary bytes), bucket codes, floats.
+// Field semantics match the host parser exactly (trim of spaces / tabs / CR, the same decimal
+// accumulation in double, integer-division buckets, 'missing' for unknown values / short rows).
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+constexpr int CT = 256;              // threads per block
+constexpr long long CHUNK = 1 << 16;  // bytes per counting chunk (one block each)
+
+__device__ __forceinline__ unsigned zero_bytes(unsigned x) {  // high bit of each zero byte of x
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
+__global__ __launch_bounds__(CT) void csv_nl_count_kernel(const uint8_t* __restrict__ bytes, long long size,
+                                                          unsigned* __restrict__ counts) {
+  const long long c0 = (long long)blockIdx.x * CHUNK;
+  const long long c1 = min(size, c0 + CHUNK);
+  unsigned cnt = 0;
+  // 16-byte vectors (the buffer is padded to a multiple of 16 and 16-byte aligned)
+  for (long long v = c0 + 16LL * threadIdx.x; v < c1; v += 16LL * CT) {
+    const uint4 q = *reinterpret_cast<const uint4*>(bytes + v);
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+    const int valid = (int)min(16LL, c1 - v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unsigned m = zero_bytes(w[i] ^ 0x0A0A0A0Au);
+      const int lim = valid - 4 * i;  // bytes of this word inside the file
+      if (lim < 4) m &= lim <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - lim)));
+      cnt += __popc(m);
+    }
+  }
+  cnt = av::wave_sum(cnt);
+  __shared__ unsigned part[CT / 64];
+  if (av::lane_id() == 0) part[av::wave_id()] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t = 0;
+    for (int w = 0; w < CT / 64; ++w) t += part[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(CT) void csv_nl_pos_kernel(const uint8_t* __restrict__ bytes, long long size,
+                                                        const long long* __restrict__ offsets,
+                                                        long long* __restrict__ pos) {
+  __shared__ unsigned s_wtot[CT / 64];
+  const long long c0 = (long long)blockIdx.x * CHUNK;
+  const long long c1 = min(size, c0 + CHUNK);
+  long long out = offsets[blockIdx.x];
+  const int lane = av::lane_id(), wave = av::wave_id();
+  for (long long base = c0; base < c1; base += 16LL * CT) {
+    const long long v = base + 16LL * threadIdx.x;
+    unsigned bits = 0;  // bit i: byte v + i is a newline
+    if (v < c1) {
+      const uint4 q = *reinterpret_cast<const uint4*>(bytes + v);
+      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned m = zero_bytes(w[i] ^ 0x0A0A0A0Au);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if ((m >> (8 * b + 7)) & 1u) bits |= 1u << (4 * i + b);
+      }
+      const int valid = (int)min(16LL, c1 - v);
+      if (valid < 16) bits &= (1u << valid) - 1u;
+    }
+    const unsigned mine = __popc(bits);
+    unsigned inc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wtot[wave] = inc;
+    __syncthreads();
+    unsigned before = 0, tot = 0;
+    for (int w = 0; w < CT / 64; ++w) {
+      if (w < wave) before += s_wtot[w];
+      tot += s_wtot[w];
+    }
+    long long o = out + before + inc - mine;
+    while (bits) {
+      const int b = __ffs(bits) - 1;
+      pos[o++] = v + b;
+      bits &= bits - 1u;
+    }
+    out += tot;
+    __syncthreads();  // s_wtot is rewritten by the next step
+  }
+}
+
+struct DevSpec {
+  int ordinal, kind, wide, max_code;
+  int bucket_offset, tab_off, tab_mask, vbase;  // vbase: global index of the field's first vocab entry
+  double bucket_width;
+  unsigned long long out;  // device address of the output column
+};
+
+__device__ __forceinline__ bool is_space(uint8_t c) { return c == ' ' || c == '\t' || c == '\r'; }
+
+// the host parser's decimal accumulation (csrc/host/csv.cpp parse_double), NaN on garbage / empty
+__device__ double dev_parse_double(const uint8_t* p, const uint8_t* e) {
+  bool neg = false;
+  if (p < e && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
+  double v = 0.0;
+  int digits = 0;
+  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++digits; }
+  if (p < e && *p == '.') {
+    ++p;
+    double scale = 0.1;
+    while (p < e && *p >= '0' && *p <= '9') { v += (*p - '0') * scale; scale *= 0.1; ++p; ++digits; }
+  }
+  if (digits == 0) return __longlong_as_double(0x7ff8000000000000LL);
+  if (p < e && (*p == 'e' || *p == 'E')) {
+    ++p;
+    bool eneg = false;
+    if (p < e && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
+    int ex = 0;
+    while (p < e && *p >= '0' && *p <= '9') { ex = ex * 10 + (*p - '0'); ++p; }
+    v *= pow(10.0, eneg ? -ex : ex);
+  }
+  if (p != e) return __longlong_as_double(0x7ff8000000000000LL);
+  return neg ? -v : v;
+}
+
+__global__ __launch_bounds__(CT) void csv_parse_kernel(const uint8_t* __restrict__ bytes,
+                                                       const long long* __restrict__ starts,
+                                                       const long long* __restrict__ ends, long long n, char delim,
+                                                       const DevSpec* __restrict__ specs, int nspecs, int max_ord,
+                                                       const int* __restrict__ tabs, const int* __restrict__ voff,
+                                                       const int* __restrict__ vlen, const uint8_t* __restrict__ vbytes,
+                                                       unsigned long long* __restrict__ short_rows) {
+  __shared__ DevSpec s_spec[32];
+  for (int i = threadIdx.x; i < nspecs; i += CT) s_spec[i] = specs[i];
+  __syncthreads();
+  unsigned bad = 0;
+  const long long stride = (long long)gridDim.x * CT;
+  for (long long r = (long long)blockIdx.x * CT + threadIdx.x; r < n; r += stride) {
+    const uint8_t* p = bytes + starts[r];
+    const uint8_t* e = bytes + ends[r];
+    int o = 0, si = 0;  // specs are sorted by ordinal
+    const uint8_t* a = p;
+    bool short_row = false;
+    while (o <= max_ord && si < nspecs) {
+      const uint8_t* q = a;
+      while (q < e && *q != (uint8_t)delim) ++q;
+      while (si < nspecs && s_spec[si].ordinal == o) {
+        const DevSpec& sp = s_spec[si];
+        const uint8_t* f0 = a;
+        const uint8_t* f1 = q;
+        while (f0 < f1 && is_space(*f0)) ++f0;
+        while (f1 > f0 && is_space(f1[-1])) --f1;
+        unsigned code = 65535u;
+        if (sp.kind == 0) {  // CAT
+          unsigned h = 2166136261u;
+          for (const uint8_t* c = f0; c < f1; ++c) h = (h ^ *c) * 16777619u;
+          h ^= h >> 15;
+          unsigned slot = h & (unsigned)sp.tab_mask;
+          const int len = (int)(f1 - f0);
+          while (true) {
+            const int ci = tabs[sp.tab_off + slot];  // the field's code, -1 = empty slot
+            if (ci < 0) break;
+            const int gi = sp.vbase + ci;
+            if (vlen[gi] == len) {
+              const uint8_t* vb = vbytes + voff[gi];
+              int k = 0;
+              while (k < len && vb[k] == f0[k]) ++k;
+              if (k == len) { code = (unsigned)ci; break; }
+            }
+            slot = (slot + 1) & (unsigned)sp.tab_mask;
+          }
+        } else if (sp.kind == 1) {  // BUCKET: the reference's integer division
+          const double v = dev_parse_double(f0, f1);
+          if (!isnan(v)) {
+            const long long b = (long long)floor(v / sp.bucket_width) - sp.bucket_offset;
+            if (b >= 0 && b <= sp.max_code) code = (unsigned)b;
+          }
+        } else {  // FLOAT
+          reinterpret_cast<float*>(sp.out)[r] = (float)dev_parse_double(f0, f1);
+        }
+        if (sp.kind != 2) {
+          if (sp.wide) reinterpret_cast<uint16_t*>(sp.out)[r] = (uint16_t)min(code, 65535u);
+          else reinterpret_cast<uint8_t*>(sp.out)[r] = (uint8_t)min(code, 255u);
+        }
+        ++si;
+      }
+      ++o;
+      if (q >= e) break;
+      a = q + 1;
+    }
+    for (; si < nspecs; ++si) {  // fields beyond the end of the row: missing
+      short_row = true;
+      const DevSpec& sp = s_spec[si];
+      if (sp.kind == 2) reinterpret_cast<float*>(sp.out)[r] = __int_as_float(0x7fc00000);
+      else if (sp.wide) reinterpret_cast<uint16_t*>(sp.out)[r] = 65535;
+      else reinterpret_cast<uint8_t*>(sp.out)[r] = 255;
+    }
+    bad += short_row ? 1u : 0u;
+  }
+  bad = av::wave_sum(bad);
+  if (av::lane_id() == 0 && bad) atomicAdd(short_rows, (unsigned long long)bad);
+}
+
+}  // namespace
+
+namespace avk {
+
+long long csv_chunks(long long size) { return (size + CHUNK - 1) / CHUNK; }
+
+void csv_newline_counts(const uint8_t* bytes, long long size, unsigned* counts, hipStream_t stream) {
+  if (size <= 0) return;
+  csv_nl_count_kernel<<<(unsigned)csv_chunks(size), CT, 0, stream>>>(bytes, size, counts);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void csv_newline_positions(const uint8_t* bytes, long long size, const long long* offsets, long long* pos,
+                           hipStream_t stream) {
+  if (size <= 0) return;
+  csv_nl_pos_kernel<<<(unsigned)csv_chunks(size), CT, 0, stream>>>(bytes, size, offsets, pos);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long long* ends, long long n, char delim,
+                    const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
+                    const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream) {
+  if (n <= 0 || nspecs <= 0) return;
+  if (nspecs > 32) throw std::runtime_error("csv_parse_rows: at most 32 parsed columns");
+  csv_parse_kernel<<<av::stream_grid(n, CT, 1, 8192), CT, 0, stream>>>(
+      bytes, starts, ends, n, delim, reinterpret_cast<const DevSpec*>(specs), nspecs, max_ord, tabs, voff, vlen,
+      vbytes, short_rows);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int csv_devspec_bytes() { return (int)sizeof(DevSpec); }
+
+}  // namespace avk

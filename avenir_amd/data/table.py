@@ -229,12 +229,15 @@ class LazyColumn(Sequence):
     them eagerly cost more than parsing the file."""
 
     def __init__(self, csv, ordinal: int, r0: int, r1: int):
+        """``csv``: a native CsvFile, or a zero-argument factory of one (the device parser keeps
+        no host index, so the host one is only built if the strings are ever asked for)."""
         self._csv, self._ord, self._r0, self._r1 = csv, ordinal, r0, r1
         self._vals: list[str] | None = None
 
     def _get(self) -> list[str]:
         if self._vals is None:
-            self._vals = self._csv.column_strings(self._ord)[self._r0:self._r1]
+            csv = self._csv() if callable(self._csv) else self._csv
+            self._vals = csv.column_strings(self._ord)[self._r0:self._r1]
             self._csv = None
         return self._vals
 
@@ -282,6 +285,14 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
     use_native = C is not None and not _is_regex(delim)
     if nthreads is None:    # parse threads: the machine's cores, capped at a GPU box's CPU share
         nthreads = max(1, min(16, os.cpu_count() or 8))
+    dev = torch.device(device)
+    if (use_native and dev.type == "cuda" and not keep_lines and len(_literal(delim or ",")) == 1
+            and hasattr(C, "csv_parse_device") and os.path.getsize(path) >= _GPU_CSV_MIN_BYTES
+            and all(f.cardinality or not f.is_categorical for f in feats)
+            and (cls_f is None or cls_f.cardinality)):
+        t = _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads)
+        if t is not None:
+            return t
     csv = C.CsvFile(str(path), _literal(delim or ","), skip_header, nthreads) if use_native else None
     # categorical fields without a schema cardinality: dictionary in first-seen order over the
     # WHOLE file (identical on every rank), any size (uint16 codes above 255 values)
@@ -354,6 +365,40 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         lines = all_lines[r0:r1] if keep_lines else None
     t = Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, lines, r0)
     return t.to(device) if str(device) != "cpu" else t
+
+
+_GPU_CSV_MIN_BYTES = int(os.environ.get("AVMI_GPU_CSV_MIN_BYTES", str(32 << 20)))
+
+
+def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads):
+    """K1 on the GPU (csrc/kernels/csv.hip): upload the file, index lines and parse the schema's
+    columns on the device; same codes as the host parser.  None when a column kind needs the host
+    path (raw int64 columns)."""
+    binned = [f for f in feats if f.is_binned]
+    numeric = [f for f in feats if not f.is_binned and f.is_numeric]
+    wide = needs_wide(binned)
+    specs = [_spec_for(f, wide) for f in binned] + [_spec_for(f) for f in numeric]
+    if cls_f is not None:
+        specs.append(_spec_for(cls_f))
+    if any(sp[1] not in (CAT, BUCKET, FLOAT) for sp in specs):
+        return None
+    like = torch.empty(0, device=dev)
+    cols, n, _bad, _total, r0 = C.csv_parse_device(str(path), specs, _literal(delim or ","), skip_header,
+                                                   int(rank), int(world), like)
+    ld = pad16(n)
+    cdt = torch.uint16 if wide else torch.uint8
+    codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned
+             else torch.zeros((0, ld), dtype=cdt, device=dev))
+    num = torch.zeros((len(numeric), ld), dtype=torch.float32, device=dev)
+    for i, c in enumerate(cols[len(binned): len(binned) + len(numeric)]):
+        num[i, :n] = c[:n]
+    labels = cols[-1][:ld] if cls_f is not None else None
+    idf = schema.id_field
+    ids = None
+    if idf is not None:
+        lit = _literal(delim or ",")
+        ids = LazyColumn(lambda: C.CsvFile(str(path), lit, skip_header, nthreads), idf.ordinal, r0, r0 + n)
+    return Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, None, r0)
 
 
 def _distinct_py(path, ordinal: int, delim: str, skip_header: bool) -> list[str]:

@@ -99,8 +99,11 @@ def _ingest(rows: int, schema, dev, comm) -> dict:
         out["model_lines_s"] = _timed(lambda: lines.extend(nb.model_lines()), dev)
         assert int(nb.class_n.sum().item()) == rows
         total = out["load_s"] + out["fit_s"] + out["model_lines_s"]
+        from avenir_amd.data import table as _tb
         out.update(rows=rows, file_bytes=nbytes, total_s=total, rows_per_s=rows / total,
-                   parse_gbps=nbytes / out["load_s"] / 1e9, model_lines=len(lines))
+                   parse_gbps=nbytes / out["load_s"] / 1e9, model_lines=len(lines),
+                   parser="device (K1 csv.hip)" if dev.type == "cuda" and nbytes >= _tb._GPU_CSV_MIN_BYTES
+                   else "host (csrc/host/csv.cpp)")
         return out
     finally:
         if os.path.exists(path):
