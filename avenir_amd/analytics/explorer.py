@@ -7,10 +7,12 @@ regressions, outlier scores, trend/seasonality) runs as torch reductions on the 
 the long tail of classical hypothesis tests delegates the p-value to scipy.stats on the host (the
 reference does the same); Zhang's tests use device permutation sampling.
 
-Differences: plotting methods return the data that would be plotted (no display here);
-``save``/``restore`` write JSON + .npz (no pickle); isolation-forest / one-class-SVM outlier
-detectors are replaced by kNN-distance and LOF scores computed with the K6 distance kernel path
-and a Mahalanobis (min-covariance-style) score — parity unpinned.
+Differences: plotting methods render with matplotlib's Agg backend into ``plot_dir`` (PNG files,
+one per call) when it is set and otherwise only return the plotted data (no display here);
+``save``/``restore`` write JSON + .npz (no pickle).  The isolation-forest outliers use
+``models/outlier.py`` (level-synchronous device trees) and the one-class-SVM outliers the K12 SMO
+kernel (``models/svm.py::OneClassSVM``); both agree with scikit-learn statistically (random draws
+differ).  kNN-distance, LOF and Mahalanobis scores are extra detectors.
 """
 from __future__ import annotations
 
@@ -30,7 +32,9 @@ def _np(x):
 
 
 class DataExplorer:
-    def __init__(self, verbose: bool = False, device="cpu"):
+    def __init__(self, verbose: bool = False, device="cpu", plot_dir: str | None = None):
+        self.plot_dir = plot_dir
+        self._nplots = 0
         self.data: dict[str, tuple[str, object]] = {}
         self.notes: dict[str, list[str]] = {}
         self.verbose = verbose
@@ -81,12 +85,72 @@ class DataExplorer:
         for c, n in zip(cols, names):
             self._add(n, "cat", [r[c] for r in rows])
 
-    def addDataFrameData(self, df, *names):
-        for n in (names or df.columns):
+    def addDataFrameData(self, df, *columns):
+        """``addDataFrameData(df, numeric, *columns)`` as in the reference (``numeric`` True for
+        numeric, False for binary; columns = indexes followed by names, or names), or
+        ``addDataFrameData(df, *names)`` which infers numeric vs categorical per column."""
+        if columns and isinstance(columns[0], (bool, np.bool_)):
+            numeric, cols = bool(columns[0]), list(columns[1:])
+            for name, col in self._df_columns(df, cols):
+                arr = col.to_numpy()
+                if numeric:
+                    assert self.inferDataType(arr) in ("binary", "integer", "float"), "data is not numeric"
+                else:
+                    assert self.inferDataType(arr) == "binary", "data is not binary"
+                self._add(str(name), "num" if numeric else "bin", arr)
+            return
+        for n in (columns or df.columns):
             kind = "cat" if df[n].dtype == object else "num"
             self._add(str(n), kind, df[n].tolist() if kind == "cat" else df[n].to_numpy())
 
-    addDataFrameNumericData = addDataFrameData
+    @staticmethod
+    def _df_columns(df, cols):
+        """(name, column) pairs for 'indexes followed by names' or plain column names."""
+        if cols and isinstance(cols[0], (int, np.integer)):
+            k = len(cols) // 2
+            for ci, name in zip(cols[:k], cols[k:]):
+                assert ci < len(df.columns), f"col index {ci} outside range"
+                yield name, df.iloc[:, ci]
+        else:
+            for c in cols:
+                yield c, df[c]
+
+    def addDataFrameNumericData(self, df, *columns):
+        self.addDataFrameData(df, True, *columns)
+
+    def addDataFrameBinaryData(self, df, *columns):
+        self.addDataFrameData(df, False, *columns)
+
+    def addDataFrameCatData(self, df, *columns):
+        for name, col in self._df_columns(df, list(columns)):
+            self._add(str(name), "cat", [str(v) for v in col.tolist()])
+
+    @staticmethod
+    def _read_df(path, cols):
+        import pandas as pd
+        return pd.read_csv(path, header=None if cols and isinstance(cols[0], (int, np.integer)) else 0)
+
+    def addFileData(self, path, numeric, *columns):
+        """Reference form: ``addFileData(path, numeric, *columns)`` through a pandas frame (a
+        header row when the columns are given by name)."""
+        if not isinstance(numeric, (bool, np.bool_)):     # older form: numeric columns only
+            return self.addFileNumericData(path, numeric, *columns)
+        self.addDataFrameData(self._read_df(path, list(columns)), bool(numeric), *columns)
+
+    def queryDataFrameData(self, df, *columns):
+        """Inferred data type of each column: binary / integer / float / categorical / mixed."""
+        return {"columns and data types": [(str(n), self.inferDataType(c.to_numpy()))
+                                           for n, c in self._df_columns(df, list(columns))]}
+
+    def queryFileData(self, path, *columns):
+        return self.queryDataFrameData(self._read_df(path, list(columns)), *columns)
+
+    def loadCatFloatDataFrame(self, ds1, ds2):
+        """A frame with the categorical data set in column 0 and the numeric one in column 1."""
+        import pandas as pd
+        a, b = self.getCatData(ds1), _np(self.getNumericData(ds2))
+        a, b = self.ensureSameSize([a, b])
+        return pd.DataFrame({0: a, 1: b})
 
     def remData(self, name):
         self.data.pop(name, None)
@@ -102,7 +166,39 @@ class DataExplorer:
         return sorted(self.data)
 
     def getDataType(self, name):
-        return self.data[name][0]
+        """Workspace kind (num / bin / cat) of a data set name, or the inferred type of an array."""
+        if isinstance(name, str) and name in self.data:
+            return self.data[name][0]
+        return self.inferDataType(name)
+
+    @staticmethod
+    def inferDataType(col) -> str:
+        """binary / integer / float / categorical / mixed, the reference's order of checks."""
+        a = np.asarray(col, dtype=object).ravel()
+        if a.size == 0:
+            return "mixed"
+        nums = [isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool) for v in a]
+        if all(nums):
+            f = a.astype(np.float64)
+            if np.all((f == 0) | (f == 1)):
+                return "binary"
+            if np.all(np.floor(f) == f):
+                return "integer"
+            return "float"
+        if all(isinstance(v, str) for v in a):
+            return "categorical"
+        return "mixed"
+
+    def print(self, ds):
+        """First 50 values of a data set (and its size); returned as well as printed when verbose."""
+        kind, v = self.data[ds]
+        vals = v[:50] if kind == "cat" else _np(v[:50]).tolist()
+        n = len(v) if kind == "cat" else int(v.numel())
+        if self.verbose:
+            print(f"size {n}")
+            print("showing first 50 elements")
+            print(vals)
+        return {"size": n, "head": vals}
 
     def getNumericData(self, ds) -> torch.Tensor:
         if isinstance(ds, str):
@@ -325,7 +421,19 @@ class DataExplorer:
         thr = torch.quantile(sc, 1 - contamination)
         return {"scores": _np(sc), "outliers": _np((sc > thr).nonzero().view(-1))}
 
-    getOutliersWithIsoForest = getOutliersWithKnnDistance
+    def _outlier_result(self, X, is_out):
+        m = _np(is_out).astype(bool)
+        Xn = _np(X)
+        return {"numOutliers": int(m.sum()), "outliers": Xn[m], "dataWithoutOutliers": Xn[~m],
+                "outlierIndexes": np.nonzero(m)[0]}
+
+    def getOutliersWithIsoForest(self, contamination, *dsl, seed: int = 0):
+        """Isolation forest over the named numeric data sets (P/mlextra/daexp.py:921-941)."""
+        from ..models.outlier import IsolationForest
+        assert 0 <= contamination <= 0.5, "contamination outside valid range"
+        X = self._matrix(dsl)
+        iso = IsolationForest(contamination=contamination if contamination > 0 else "auto", seed=seed)
+        return self._outlier_result(X, iso.fit_predict(X) == -1)
 
     def getOutliersWithLocalFactor(self, dss, k: int = 10, contamination: float = 0.05):
         """Local outlier factor from the k-NN graph (reachability distances)."""
@@ -348,7 +456,13 @@ class DataExplorer:
         thr = torch.quantile(md, 1 - contamination)
         return {"scores": _np(md), "outliers": _np((md > thr).nonzero().view(-1))}
 
-    getOutliersWithSupVecMach = getOutliersWithCovarDeterminant
+    def getOutliersWithSupVecMach(self, nu, *dsl):
+        """One-class SVM (RBF, gamma 'scale') outliers (P/mlextra/daexp.py:965-985)."""
+        from ..models.svm import OneClassSVM
+        assert 0 <= nu <= 0.5, "error upper bound outside valid range"
+        X = self._matrix(dsl)
+        svm = OneClassSVM(nu=nu).fit(X)
+        return self._outlier_result(X, svm.predict(X) == -1)
 
     # ------------------------------------------------------------------------------------------
     # correlation
@@ -628,3 +742,112 @@ class DataExplorer:
     def ensureSameSize(self, dlist):
         m = min(len(d) for d in dlist)
         return [d[:m] for d in dlist]
+
+    # ------------------------------------------------------------------------------------------
+    # plots (P/mlextra/daexp.py:488-560, 1080-1090, 1230-1300): Agg-rendered PNGs in plot_dir
+    # ------------------------------------------------------------------------------------------
+    def _render(self, tag: str, draw) -> str | None:
+        """Run ``draw(ax)`` on a fresh Agg figure and save it as ``<plot_dir>/<n>_<tag>.png``;
+        nothing is drawn without a plot_dir (or without matplotlib)."""
+        if not self.plot_dir:
+            return None
+        try:
+            import matplotlib
+            matplotlib.use("Agg")
+            import matplotlib.pyplot as plt
+        except ImportError:
+            return None
+        Path(self.plot_dir).mkdir(parents=True, exist_ok=True)
+        fig, ax = plt.subplots()
+        try:
+            draw(ax)
+            self._nplots += 1
+            path = str(Path(self.plot_dir) / f"{self._nplots:03d}_{tag}.png")
+            fig.savefig(path)
+        finally:
+            plt.close(fig)
+        return path
+
+    def plot(self, ds, yscale=None):
+        y = _np(self.getNumericData(ds))
+
+        def draw(ax):
+            ax.plot(y)
+            if yscale:
+                ax.set_yscale(yscale)
+        return {"data": y, "file": self._render("plot", draw)}
+
+    def plotZoomed(self, ds, beg, end, yscale=None):
+        y = _np(self.getNumericData(ds))[beg:end]
+
+        def draw(ax):
+            ax.plot(np.arange(beg, beg + len(y)), y)
+            if yscale:
+                ax.set_yscale(yscale)
+        return {"data": y, "file": self._render("zoomed", draw)}
+
+    def scatterPlot(self, ds1, ds2):
+        a, b = self.ensureSameSize([_np(self.getNumericData(ds1)), _np(self.getNumericData(ds2))])
+        x = np.arange(1, len(a) + 1)
+
+        def draw(ax):
+            ax.scatter(x, a, color="red")
+            ax.scatter(x, b, color="blue")
+        return {"data": (a, b), "file": self._render("scatter", draw)}
+
+    def plotHist(self, ds, cumulative=False, density=False, nbins=20):
+        x = self.getNumericData(ds).double()
+        lo, hi = float(x.min()), float(x.max())
+        cnt = torch.histc(x, bins=nbins, min=lo, max=hi if hi > lo else lo + 1.0)
+        edges = np.linspace(lo, hi if hi > lo else lo + 1.0, nbins + 1)
+        h = _np(cnt)
+        if density:
+            h = h / max(h.sum() * (edges[1] - edges[0]), 1e-300)
+        if cumulative:
+            h = np.cumsum(h)
+
+        def draw(ax):
+            ax.stairs(h, edges, fill=True)
+        return {"counts": h, "edges": edges, "file": self._render("hist", draw)}
+
+    def plotRegFit(self, x, y, slope, intercept):
+        x, y = np.asarray(x, dtype=np.float64), np.asarray(y, dtype=np.float64)
+
+        def draw(ax):
+            ax.plot(x, y, "b.")
+            ax.plot(x, intercept + slope * x, "r-")
+        return {"fit": intercept + slope * x, "file": self._render("regfit", draw)}
+
+    def _bars(self, tag, vals, alpha_band=None):
+        def draw(ax):
+            ax.stem(np.arange(len(vals)), vals)
+            if alpha_band is not None:
+                ax.axhline(alpha_band, ls="--")
+                ax.axhline(-alpha_band, ls="--")
+        return self._render(tag, draw)
+
+    def plotAutoCorr(self, ds, lags, alpha=0.05, diffOrder=0):
+        """Autocorrelation bars with the +-z/sqrt(n) band (the reference's statsmodels plot_acf)."""
+        x = self.getNumericData(ds)
+        if diffOrder > 0:
+            for _ in range(diffOrder):
+                x = x[1:] - x[:-1]
+            ds = x
+        ac = self.getAutoCorr(ds, lags)["autoCorr"]
+        band = self._z(alpha) / math.sqrt(max(int(x.numel()), 1))
+        return {"autoCorr": ac, "file": self._bars("acf", ac, band)}
+
+    def plotParAcf(self, ds, lags, alpha=0.05):
+        pac = self.getParAutoCorr(ds, lags)
+        vals = np.asarray(pac["partAutoCorr"])
+        band = self._z(alpha) / math.sqrt(max(int(self.getNumericData(ds).numel()), 1))
+        return {"partAutoCorr": vals, "file": self._bars("pacf", vals, band)}
+
+    def plotCrossCorr(self, ds1, ds2, normed=True, lags=10):
+        cc = self.getCrossCorr(ds1, ds2, lags)["crossCorr"]
+        return {"crossCorr": cc, "file": self._bars("xcorr", cc)}
+
+    @staticmethod
+    def _z(alpha):
+        from scipy.stats import norm
+        return float(norm.ppf(1 - alpha / 2))
