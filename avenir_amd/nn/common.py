@@ -80,9 +80,22 @@ def _cfg(conf, key, default):
     """Read ``key`` from a reference-style Configuration (value, is_default) or a dict."""
     if conf is None:
         return default
-    if isinstance(conf, dict):
-        v = conf.get(key, default)
-        return default if v in (None, "_") else v
+    if isinstance(conf, dict) or hasattr(conf, "values") and not hasattr(conf, "defaults"):
+        # a plain dict, or a CLI JobConfig (.properties strings): typed like the default
+        vals = conf if isinstance(conf, dict) else conf.values
+        v = vals.get(key, default)
+        if v in (None, "_"):
+            return default
+        if isinstance(v, str) and default is not None and not isinstance(default, str):
+            if isinstance(default, bool):
+                return v.strip().lower() == "true"
+            if isinstance(default, int):
+                return int(v)
+            if isinstance(default, float):
+                return float(v)
+            if isinstance(default, list):
+                return [float(x) for x in v.split(",")]
+        return v
     if key not in conf.defaults:
         conf.defaults[key] = (default, None)
         conf.configs.setdefault(key, "_")

@@ -70,9 +70,9 @@ class Tracer:
             sec = a["ms"] / 1e3
             r = {"calls": a["calls"], "total_ms": round(a["ms"], 4), "mean_ms": round(a["ms"] / a["calls"], 4)}
             if a["bytes"] and sec > 0:
-                r["GB_per_s"] = round(a["bytes"] / sec / 1e9, 2)
+                r["GB_per_s"] = float(f"{a['bytes'] / sec / 1e9:.4g}")
             if a["flops"] and sec > 0:
-                r["TFLOP_per_s"] = round(a["flops"] / sec / 1e12, 3)
+                r["TFLOP_per_s"] = float(f"{a['flops'] / sec / 1e12:.4g}")
             out[name] = r
         return out
 
