@@ -149,7 +149,7 @@ at::Tensor pack_dense(const at::Tensor& words, int64_t n, int64_t B) {
 void class_histogram_dense(const at::Tensor& dense, int64_t n, int64_t B, std::vector<int64_t> shifts,
                            std::vector<int64_t> widths, int64_t label_shift, int64_t label_width, const at::Tensor& bins,
                            const at::Tensor& offs, int64_t total_bins, int64_t n_classes, at::Tensor& out,
-                           bool count_labels) {
+                           bool count_labels, std::vector<int64_t> bins_host, std::vector<int64_t> offs_host) {
   CHECK_DEV(dense);
   CHECK_DTYPE(dense, at::kInt);
   TORCH_CHECK(B >= 4 && B <= 15 && n >= 0 && dense.numel() >= avk::dense_words(n, (int)B), "dense stream too short");
@@ -166,12 +166,13 @@ void class_histogram_dense(const at::Tensor& dense, int64_t n, int64_t B, std::v
   CHECK_DEV(bins); CHECK_DTYPE(bins, at::kInt);
   CHECK_DEV(offs); CHECK_DTYPE(offs, at::kInt);
   TORCH_CHECK(bins.numel() == F && offs.numel() == F, "bins / offs must have F entries");
-  {
-    auto bc = bins.cpu(), oc = offs.cpu();
-    for (int64_t k = 0; k < F; ++k)
-      TORCH_CHECK(oc.data_ptr<int>()[k] >= 0 && oc.data_ptr<int>()[k] + bc.data_ptr<int>()[k] <= total_bins,
-                  "feature bins outside the table");
-  }
+  // the table bounds are checked on the host copies of bins / offs (the caller's cached device
+  // tensors hold the same values): reading the device tensors back here would be a blocking
+  // copy that drains the stream and serialises every training step with the host
+  TORCH_CHECK((int64_t)bins_host.size() == F && (int64_t)offs_host.size() == F, "bins_host / offs_host: F entries");
+  for (int64_t k = 0; k < F; ++k)
+    TORCH_CHECK(offs_host[k] >= 0 && bins_host[k] >= 1 && offs_host[k] + bins_host[k] <= total_bins,
+                "feature bins outside the table");
   CHECK_DEV(out); CHECK_DTYPE(out, at::kLong);
   TORCH_CHECK(out.numel() == n_classes * total_bins, "out must be [C * TB]");
   DevGuard g(dense.device());
@@ -534,6 +535,48 @@ py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t 
                 exclude_self ? 1 : 0, od.data_ptr<float>(), reinterpret_cast<long long*>(oi.data_ptr<int64_t>()),
                 (int)splits, (int)metric, (float)p, cur_stream(Q));
   return py::make_tuple(od, oi, splits);
+}
+
+
+py::tuple knn_vote(const at::Tensor& d, const at::Tensor& idx, const at::Tensor& ys,
+                   const c10::optional<at::Tensor>& post, int64_t C, int64_t kern, double kparam, double scale,
+                   double kscale, bool invdist, double thr, int64_t pos) {
+  CHECK_DEV(d);
+  CHECK_DTYPE(d, at::kFloat);
+  CHECK_DEV(idx);
+  CHECK_DTYPE(idx, at::kLong);
+  CHECK_DEV(ys);
+  CHECK_DTYPE(ys, at::kLong);
+  TORCH_CHECK(d.dim() == 2 && idx.sizes() == d.sizes() && d.is_contiguous() && idx.is_contiguous(),
+              "d / idx must be contiguous [M, k]");
+  TORCH_CHECK(ys.dim() == 1 && ys.is_contiguous(), "ys must be contiguous [R]");
+  TORCH_CHECK(C >= 1 && C <= 64, "knn_vote: 1 <= C <= 64");
+  TORCH_CHECK(kern >= 0 && kern <= 3, "kern 0 none, 1 linearMultiplicative, 2 linearAdditive, 3 gaussian");
+  int post_mode = 0;
+  const float* pp = nullptr;
+  if (post.has_value() && post->defined()) {
+    CHECK_DEV((*post));
+    CHECK_DTYPE((*post), at::kFloat);
+    TORCH_CHECK(post->is_contiguous() && post->size(0) == ys.size(0) &&
+                (post->dim() == 1 || (post->dim() == 2 && post->size(1) == C)), "post must be [R] or [R, C]");
+    post_mode = post->dim() == 1 ? 1 : 2;
+    pp = post->data_ptr<float>();
+  }
+  // every neighbour index must address ys / post (the kernel reads them unchecked)
+  const int64_t M = d.size(0), k = d.size(1);
+  if (M > 0 && k > 0) {
+    TORCH_CHECK(idx.max().item<int64_t>() < ys.size(0), "knn_vote: neighbour index outside the label vector");
+  }
+  auto scores = at::empty({M, C}, d.options());
+  auto prob = at::empty({M, C}, d.options());
+  auto pred = at::empty({M}, d.options().dtype(at::kLong));
+  DevGuard g(d.device());
+  avk::knn_vote(d.data_ptr<float>(), reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()), M, (int)k,
+                reinterpret_cast<const long long*>(ys.data_ptr<int64_t>()), pp, post_mode, (int)C, (int)kern,
+                (float)kparam, (float)scale, (float)kscale, invdist ? 1 : 0, (float)thr, (int)pos,
+                scores.data_ptr<float>(), prob.data_ptr<float>(), reinterpret_cast<long long*>(pred.data_ptr<int64_t>()),
+                cur_stream(d));
+  return py::make_tuple(scores, prob, pred);
 }
 
 py::tuple cluster_accumulate(const at::Tensor& X, const at::Tensor& assign, int64_t K) {
@@ -1806,6 +1849,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("tree_assign", &tree_assign);
   m.def("tree_predict", &tree_predict);
   m.def("knn_topk", &knn_topk);
+  m.def("knn_vote", &knn_vote);
   m.def("cluster_accumulate", &cluster_accumulate);
   m.def("viterbi", &viterbi);
   m.def("viterbi_chunks", &viterbi_chunks);

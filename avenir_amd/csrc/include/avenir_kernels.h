@@ -59,6 +59,9 @@ void tree_predict(const uint8_t* codes, long long ld, long long n, const int* fe
 void knn_topk(const float* Q, long long M, const float* R, long long N, int D, int k,
               long long q_index_base, long long r_index_base, int exclude_self, float* out_d,
               long long* out_i, int splits, int metric, float p, hipStream_t stream);
+void knn_vote(const float* dist, const long long* idx, long long M, int k, const long long* ys,
+              const float* post, int post_mode, int C, int kern, float kparam, float scale, float kscale,
+              int invdist, float thr, int pos, float* scores, float* prob, long long* pred, hipStream_t stream);
 void cluster_accumulate(const float* X, long long N, int D, const int* assign, int K, double* sums,
                         unsigned long long* counts, hipStream_t stream);
 

@@ -313,6 +313,74 @@ __global__ __launch_bounds__(KT) void cluster_accum_kernel(const float* __restri
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K10: kernel-weighted class vote over each query's k neighbours (J/knn/Neighborhood.java:150-218,
+// NearestNeighbor's class-conditional weighting).  One thread per query; the per-class sums live
+// in CMAX registers (the class is matched with an unrolled compare, no dynamic register index), so
+// scores, percent probabilities and the decision come out of one pass over the [M, k] lists.
+// kern: 0 none, 1 linearMultiplicative, 2 linearAdditive, 3 gaussian.  post_mode: 0 none,
+// 1 one posterior per training record, 2 [R, C] posterior (the neighbour's own class column).
+// ---------------------------------------------------------------------------------------------
+constexpr int VOTE_T = 256;
+
+template <int CMAX>
+__global__ __launch_bounds__(VOTE_T) void knn_vote_kernel(
+    const float* __restrict__ dist, const long long* __restrict__ idx, long long M, int k,
+    const long long* __restrict__ ys, const float* __restrict__ post, int post_mode, int C, int kern,
+    float kparam, float scale, float kscale, int invdist, float thr, int pos,
+    float* __restrict__ scores, float* __restrict__ prob, long long* __restrict__ pred) {
+  const long long q = (long long)blockIdx.x * VOTE_T + threadIdx.x;
+  if (q >= M) return;
+  float acc[CMAX];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
+  const float* dq = dist + q * k;
+  const long long* iq = idx + q * k;
+  for (int j = 0; j < k; ++j) {
+    const long long i = iq[j];
+    const float d = dq[j];
+    if (i < 0 || isinf(d)) continue;
+    const float ds = d * scale;
+    float s;
+    if (kern == 0) s = 1.f;
+    else if (kern == 1) s = ds == 0.f ? 2.f * kscale : kscale / fmaxf(ds, 1e-9f);
+    else if (kern == 2) s = kscale - ds;
+    else { const float t = ds / kparam; s = kscale * __expf(-0.5f * t * t); }
+    if (invdist) s = s / fmaxf(ds, 1.f);
+    const long long y = ys[i];
+    const int c = (int)(y < 0 ? 0 : (y >= C ? C - 1 : y));
+    if (post_mode == 1) s *= post[i];
+    else if (post_mode == 2) s *= post[i * C + c];
+#pragma unroll
+    for (int cc = 0; cc < CMAX; ++cc) acc[cc] += (cc == c) ? s : 0.f;
+  }
+  float total = 0.f;
+  int best = 0;
+  float bv = acc[0];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) {
+    if (c < C) {
+      total += acc[c];
+      if (acc[c] > bv) { bv = acc[c]; best = c; }
+    }
+  }
+  float* sq = scores + q * C;
+  float* pq = prob + q * C;
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) {
+    if (c < C) {
+      sq[c] = acc[c];
+      pq[c] = total > 0.f ? acc[c] * 100.f / total : 0.f;
+    }
+  }
+  if (thr > 0.f && C == 2) {
+    const float a = pos ? acc[1] : acc[0], b = pos ? acc[0] : acc[1];
+    best = a / fmaxf(b, 1e-12f) > thr ? pos : 1 - pos;
+  }
+  pred[q] = best;
+}
+
 }  // namespace
 
 namespace avk {
@@ -345,6 +413,25 @@ void knn_topk(const float* Q, long long M, const float* R, long long N, int D, i
   else if (metric == 2) { AV_KNN_MET(2) }
   else throw std::runtime_error("knn_topk: unknown metric");
 #undef AV_KNN_MET
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+
+void knn_vote(const float* dist, const long long* idx, long long M, int k, const long long* ys,
+              const float* post, int post_mode, int C, int kern, float kparam, float scale, float kscale,
+              int invdist, float thr, int pos, float* scores, float* prob, long long* pred, hipStream_t stream) {
+  if (M <= 0) return;
+  const unsigned grid = (unsigned)((M + VOTE_T - 1) / VOTE_T);
+#define AV_VOTE(CM) knn_vote_kernel<CM><<<grid, VOTE_T, 0, stream>>>(dist, idx, M, k, ys, post, post_mode, C, kern, \
+      kparam, scale, kscale, invdist, thr, pos, scores, prob, pred)
+  if (C <= 2) AV_VOTE(2);
+  else if (C <= 4) AV_VOTE(4);
+  else if (C <= 8) AV_VOTE(8);
+  else if (C <= 16) AV_VOTE(16);
+  else if (C <= 32) AV_VOTE(32);
+  else if (C <= 64) AV_VOTE(64);
+  else throw std::runtime_error("knn_vote: more than 64 classes");
+#undef AV_VOTE
   AV_HIP_CHECK(hipGetLastError());
 }
 

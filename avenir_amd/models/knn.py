@@ -20,11 +20,13 @@ from dataclasses import dataclass
 
 import torch
 
+from .. import _native
 from ..ops import distance as dist
 from ..parallel.comm import Comm, get_comm
 from ..utils.metrics import ConfusionMatrix, Counters
 
 KERNEL_SCALE = 1000.0
+_VOTE_KERNELS = {"none": 0, "linearMultiplicative": 1, "linearAdditive": 2, "gaussian": 3}
 
 
 @dataclass
@@ -139,11 +141,23 @@ class NearestNeighbor:
                 raise ValueError(f"unknown regression method {self.regression}")
             return KnnResult(pred, None, None, idx, d)
         C = self.n_classes
+        kern = _VOTE_KERNELS.get(self.kernel)
+        if Q.is_cuda and C <= 64 and kern is not None and (
+                not self.class_cond_weighted or (ps is not None and (ps.dim() == 1 or ps.shape[1] == C))):
+            # K10: one launch for kernel weights, class-conditional weights, class sums, percent
+            # probabilities and the decision (knn_vote_kernel in distance.hip)
+            post = ps.float().contiguous() if self.class_cond_weighted else None
+            scores, prob, pred = _native.C().knn_vote(
+                d.float().contiguous(), idx.contiguous(), ys.long().contiguous(), post, int(C), kern,
+                float(self.kernel_param), float(self.scale), float(KERNEL_SCALE),
+                bool(self.inverse_distance_weighted),
+                float(self.decision_threshold) if C == 2 else -1.0, int(self.positive_class))
+            return KnnResult(pred, scores, prob, idx, d)
         s = self._kernel_scores(d) * valid
         if self.class_cond_weighted:
             if ps is None:
                 raise ValueError("class conditional weighting needs feature posterior probabilities")
-            s = s * ps[gi].float().gather(1, ny.long().unsqueeze(2)).squeeze(2) if ps.dim() == 2 and ps.shape[1] == C \
+            s = s * ps[gi].float().gather(2, ny.long().clamp(0, C - 1).unsqueeze(2)).squeeze(2) if ps.dim() == 2 and ps.shape[1] == C \
                 else s * ps[gi].float()
         scores = torch.zeros((Q.shape[0], C), dtype=torch.float32, device=Q.device)
         scores.scatter_add_(1, ny.long().clamp(0, C - 1), s.float())

@@ -199,7 +199,8 @@ def class_histogram_packed(rp: RowPacked, out: torch.Tensor | None = None,
             # dense B-bit records, one LDS atomic per record into the joint table
             _native.C().class_histogram_dense(rp.dense, int(rp.n), int(rp.bits), list(rp.shifts), list(rp.widths),
                                               rp.label_shift, rp.label_width, _dev_i32(rp.bins, dev),
-                                              _dev_i32(offs, dev), tb, C, out, bool(count_labels))
+                                              _dev_i32(offs, dev), tb, C, out, bool(count_labels),
+                                              list(rp.bins), offs)
             return out
         _native.C().class_histogram_rowpacked(rp.words, int(rp.n), [rp.shifts[k] for k in order],
                                               [rp.widths[k] for k in order], rp.label_shift, rp.label_width,

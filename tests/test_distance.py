@@ -265,3 +265,50 @@ def test_kmeans_sklearn_tolerance_mode():
     assert b.best[5].sse == pytest.approx(a.best[5].sse, rel=1e-2)
     with pytest.raises(ValueError):
         KMeans(3, tol_mode="bogus")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kern,C,ccw,thr", [("none", 2, False, -1.0), ("gaussian", 2, True, -1.0),
+                                            ("linearMultiplicative", 5, False, -1.0),
+                                            ("linearAdditive", 2, False, 1.5), ("gaussian", 37, True, -1.0)])
+def test_knn_vote_kernel_matches_torch_vote(cuda, kern, C, ccw, thr):
+    """K10 knn_vote_kernel (one launch) == the torch vote on the same neighbour lists, including
+    class-conditional weights ([R] and [R, C] posteriors) and the decision-threshold rule."""
+    g = torch.Generator().manual_seed(C)
+    X = torch.randn(3000, 8, generator=g)
+    y = torch.randint(0, C, (3000,), generator=g)
+    post = torch.rand(3000, C, generator=g) if C > 2 else torch.rand(3000, generator=g)
+    m = NearestNeighbor(k=9, kernel=kern, kernel_param=300.0, class_cond_weighted=ccw,
+                        inverse_distance_weighted=(kern == "none"), decision_threshold=thr)
+    m.fit(X.to(cuda), y.to(cuda), C, feature_post_prob=post.to(cuda) if ccw else None)
+    got = m.predict(X[:500].to(cuda), exclude_self=True)
+    # torch vote: same object with the kernel path disabled (an unknown-to-K10 kernel name forces it)
+    import avenir_amd.models.knn as K
+    saved = dict(K._VOTE_KERNELS)
+    K._VOTE_KERNELS.clear()
+    try:
+        ref = m.predict(X[:500].to(cuda), exclude_self=True)
+    finally:
+        K._VOTE_KERNELS.update(saved)
+    assert torch.equal(got.neighbors, ref.neighbors)
+    assert torch.allclose(got.class_scores, ref.class_scores, rtol=1e-5, atol=1e-3)
+    assert torch.allclose(got.class_prob, ref.class_prob, rtol=1e-5, atol=1e-3)
+    close = (ref.class_scores.topk(2, 1).values.diff(dim=1).abs().squeeze(1) > 1e-3 * ref.class_scores.abs().max())
+    assert torch.equal(got.pred.long()[close], ref.pred.long()[close])
+
+
+def test_knn_class_cond_weight_per_class_posterior():
+    """[R, C] posteriors weight each neighbour by ITS OWN class column (torch vote path)."""
+    g = torch.Generator().manual_seed(5)
+    C, k = 6, 4
+    X = torch.randn(400, 5, generator=g)
+    y = torch.randint(0, C, (400,), generator=g)
+    post = torch.rand(400, C, generator=g)
+    m = NearestNeighbor(k=k, class_cond_weighted=True).fit(X, y, C, feature_post_prob=post)
+    r = m.predict(X[:50], exclude_self=True)
+    exp = torch.zeros(50, C)
+    for q in range(50):
+        for j in range(k):
+            i = int(r.neighbors[q, j])
+            exp[q, y[i]] += post[i, y[i]]
+    assert torch.allclose(r.class_scores, exp, atol=1e-5)
