@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 from dataclasses import dataclass
 from pathlib import Path
 
@@ -37,6 +38,18 @@ from ..utils.schema import FeatureSchema
 from ..utils.tracing import traced
 
 _LOG_FLOOR = math.log(1e-12)
+# AVMI_NB_OVERLAP=0 keeps the multi-GPU all-reduce on the caller's stream
+_OVERLAP_REDUCE = os.environ.get("AVMI_NB_OVERLAP", "1") != "0"
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(device: torch.device):
+    """One side stream per device for the model-reduce work of multi-GPU fits."""
+    key = torch.device(device).index
+    st = _SIDE_STREAMS.get(key)
+    if st is None:
+        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return st
 
 
 @dataclass
@@ -61,6 +74,72 @@ class NaiveBayes:
         self.class_values: list[str] = []
         self.counters = Counters()
         self._tables: dict | None = None
+        self._ready = None            # event after the side-stream all-reduce / finalize (GPU, >1 rank)
+        self._side = None
+
+    # The model tensors are read through properties: when the all-reduce of a multi-GPU fit runs on
+    # the side stream, the first read on another stream waits for it (see _reduce_on_side_stream).
+    @property
+    def counts(self):
+        self._wait()
+        return self._counts
+
+    @counts.setter
+    def counts(self, v):
+        self._counts = v
+
+    @property
+    def class_n(self):
+        self._wait()
+        return self._class_n
+
+    @class_n.setter
+    def class_n(self, v):
+        self._class_n = v
+
+    @property
+    def moments(self):
+        self._wait()
+        return self._moments
+
+    @moments.setter
+    def moments(self, v):
+        self._moments = v
+
+    def _wait(self) -> None:
+        """Make the current stream wait for a pending side-stream reduce / finalize, and mark the
+        model tensors as used on it (the caching allocator must not recycle them early)."""
+        ev = self.__dict__.get("_ready")
+        if ev is None:
+            return
+        self._ready = None
+        cur = torch.cuda.current_stream(self._both.device)
+        cur.wait_event(ev)
+        ts = [self._both, self._moments] + (list(self._tables.values()) if self._tables else [])
+        for t in ts:
+            if t is not None and t.is_cuda and t.numel():
+                t.record_stream(cur)
+
+    def _reduce_on_side_stream(self, comm: Comm, both: torch.Tensor, moments: torch.Tensor) -> None:
+        """Multi-GPU fit on the GPU: the RCCL all-reduce (and later the finalize of tables()) is
+        issued on a per-device side stream that waits for this step's histogram, so the caller's
+        stream is free to start the NEXT histogram while the collective runs — the collective
+        overlaps compute instead of sitting between steps.  Any read of the model (properties,
+        tables consumers, predict) waits on the recorded event first."""
+        main = torch.cuda.current_stream(both.device)
+        side = _side_stream(both.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            comm.all_reduce(both)
+            if moments.numel():
+                comm.all_reduce(moments)
+        both.record_stream(side)
+        if moments.numel():
+            moments.record_stream(side)
+        self._side = side
+        ev = torch.cuda.Event()
+        ev.record(side)
+        self._ready = ev
 
     # ----------------------------------------------------------------------------------------
     # training
@@ -81,14 +160,31 @@ class NaiveBayes:
         else:
             both = H.class_histogram(t.codes, t.n, self.bins, t.labels, C, count_labels=True)
         moments = H.class_moments(t.numeric, t.n, t.labels, C)
+        self._ready, self._side = None, None
         if reduce and comm.is_distributed:
-            comm.all_reduce(both)
-            if moments.numel():
-                comm.all_reduce(moments)
+            if both.is_cuda and _OVERLAP_REDUCE and comm.backend != "gloo":
+                self._reduce_on_side_stream(comm, both, moments)
+            else:
+                comm.all_reduce(both)
+                if moments.numel():
+                    comm.all_reduce(moments)
         self._both = both
         self.counts, self.class_n = both[:, :-1], both[:, -1]
         self.moments = moments
         self._tables = None
+        if both.is_cuda and self.bins:
+            # the model IS the tables: one fused finalize launch, queued behind the counts (on the
+            # side stream when the all-reduce runs there, so it never blocks the caller's stream)
+            if self._ready is not None:
+                ev = self._ready
+                with torch.cuda.stream(self._side):
+                    self._side.wait_event(ev)
+                    self._tables_impl(None)
+                ev2 = torch.cuda.Event()
+                ev2.record(self._side)
+                self._ready = ev2
+            else:
+                self._tables_impl(None)
         return self
 
     def _packed(self, t: Table):
@@ -133,8 +229,14 @@ class NaiveBayes:
         return self.class_n
 
     def tables(self, device=None) -> dict:
+        """Log-probability tables (cached; a GPU fit computes them eagerly — see fit)."""
         if self._tables is not None and (device is None or self._tables["logp"].device == torch.device(device)):
+            self._wait()
             return self._tables
+        self._wait()
+        return self._tables_impl(device)
+
+    def _tables_impl(self, device=None) -> dict:
         dev = torch.device(device) if device is not None else self.counts.device
         a = self.laplace
         if dev.type == "cuda" and self._both is not None and self._both.device == dev and self.bins:

@@ -162,8 +162,10 @@ def main() -> int:
     nb = NaiveBayes(schema, comm=comm)
 
     def step():
+        # one training step = count + (multi-GPU) all-reduce + fused finalize into the log-prob
+        # tables; a GPU fit builds the tables itself, and with >1 rank the all-reduce + finalize
+        # run on a side stream that overlaps the next step's histogram (models/bayes.py)
         nb.fit(table)
-        nb.tables()
 
     for _ in range(args.warmup):
         step()

@@ -200,3 +200,45 @@ def test_nb_finalize_kernel_matches_cpu(cuda, tmp_path):
         tc, tg = nbc.tables(), nbg.tables()
         for k in ("logp", "logfp", "logprior"):
             assert torch.allclose(tg[k].cpu(), tc[k].float(), atol=1e-5), (k, laplace)
+
+
+class _DoublingComm:
+    """Stand-in for a 2-rank RCCL communicator on one GPU: all_reduce doubles in place on the
+    CURRENT stream (like RCCL, which orders itself after the caller's stream), so the side-stream
+    reduce / finalize ordering of NaiveBayes.fit is exercised without a second GPU."""
+    is_distributed = True
+    backend = "nccl"
+    rank, world = 0, 2
+
+    def all_reduce(self, t, op="sum"):
+        torch.cuda._sleep(2_000_000)          # a slow collective: exposes missing waits
+        t.add_(t.clone())
+        return t
+
+
+@pytest.mark.gpu
+def test_nb_side_stream_reduce_ordering(cuda):
+    from avenir_amd.data.synth import CHURN_SCHEMA, churn_device
+    from avenir_amd.data.table import Table
+    from avenir_amd.utils.schema import FeatureSchema
+    schema = FeatureSchema.from_json(CHURN_SCHEMA)
+    n = 1 << 20
+    codes, labels = churn_device(n, seed=3, device=cuda)
+    t = Table(schema, n, codes, schema.feature_fields, torch.zeros((0, codes.shape[1]), device=cuda), [],
+              labels, schema.find_class_attr_field())
+    t.pack_rows()
+    single = NaiveBayes(schema).fit(t)
+    ref_counts = single.counts.clone() * 2
+    ref_tables = {k: v.clone() for k, v in single.tables().items()}
+    nb = NaiveBayes(schema, comm=_DoublingComm())
+    for _ in range(3):                         # back-to-back fits, reads only at the end
+        nb.fit(t)
+    assert torch.equal(nb.counts, ref_counts)  # property read waits for the side stream
+    tb = nb.tables()
+    for k in ("logp", "logfp", "logprior"):
+        assert torch.allclose(tb[k], ref_tables[k], atol=1e-6), k
+    nb.fit(t)
+    pr = nb.predict(t)                         # predict on the main stream waits too
+    sp = single.predict(t)
+    assert torch.equal(pr.pred, sp.pred)
+    assert int(nb.class_n.sum()) == 2 * n
