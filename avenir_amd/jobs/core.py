@@ -586,8 +586,12 @@ def auto_supervised_learning(args):
         clfs[parts[0]] = kinds[parts[0]](parts[1], device=args.device)
         if len(parts) == 3:
             probs.append(float(parts[2]))
-    best, loss, t = auto_supervised(clfs, max_evals, probs or None, seed=args.seed or 0)
-    print(json.dumps({"best": best, "loss": loss, "evals": len(t.trials)}, default=str))
+    from ..parallel.comm import get_comm
+    comm = get_comm()
+    # under torchrun every rank trains one proposal of each TPE batch on its own GPU
+    best, loss, t = auto_supervised(clfs, max_evals, probs or None, seed=args.seed or 0, comm=comm)
+    if comm.rank == 0:
+        print(json.dumps({"best": best, "loss": loss, "evals": len(t.trials)}, default=str))
 
 
 @job("serve", "REST prediction service (P/app/rfsvc.py etc.): --kind rf|gbt|svm|lr --config props --port P [--name rf]")

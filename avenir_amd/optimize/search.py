@@ -601,7 +601,8 @@ class BayesianOptimizer:
 # hyper-parameter search (P/supv/pasearch.py)
 # ================================================================================================
 def parameter_search(space: dict[str, Sequence], score_fn: Callable[[dict], float], strategy: str = "random",
-                     n_iter: int = 20, seed: int = 0, t0: float = 1.0, cooling: float = 0.9) -> tuple[dict, float, list]:
+                     n_iter: int = 20, seed: int = 0, t0: float = 1.0, cooling: float = 0.9,
+                     comm: Comm | None = None) -> tuple[dict, float, list]:
     """Search a discrete hyper-parameter grid minimising ``score_fn(params)``.
 
     ``guided``: coordinate-wise sweeps (GuidedParameterSearch); ``random``: random grid points
@@ -633,8 +634,16 @@ def parameter_search(space: dict[str, Sequence], score_fn: Callable[[dict], floa
                     hist.append(best)
     elif strategy == "random":
         cur, best = None, float("inf")
-        for _ in range(n_iter):
-            cand = [int(rng.integers(len(space[n]))) for n in names]
+        cands = [[int(rng.integers(len(space[n]))) for n in names] for _ in range(n_iter)]
+        if comm is not None and comm.is_distributed:
+            # the candidates are independent, so every rank trains its share (one
+            # trial per GPU) and the scores are all-gathered; the walk below then reads the cache
+            todo = sorted({tuple(c) for c in cands}, key=lambda c: cands.index(list(c)))
+            mine = {c: float(score_fn({n: space[n][i] for n, i in zip(names, c)}))
+                    for c in todo[comm.rank::comm.world]}
+            for part in comm.all_gather_object(mine):
+                cache.update(part)
+        for cand in cands:
             s = ev(cand)
             if s < best:
                 best, cur = s, cand

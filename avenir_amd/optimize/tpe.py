@@ -202,12 +202,31 @@ class TPE:
         return assign
 
     # -- driver -----------------------------------------------------------------------------------
-    def minimize(self, fn: Callable[[Any], float], max_evals: int) -> tuple[Any, float]:
-        for _ in range(max_evals):
-            a = self.suggest()
-            v = _materialise(self.space, a)
-            loss = float(fn(v))
-            self.trials.append(Trial(a, loss, v))
+    def minimize(self, fn: Callable[[Any], float], max_evals: int, batch: int | None = None,
+                 comm=None) -> tuple[Any, float]:
+        """Sequential TPE (batch 1), or batches of ``batch`` proposals drawn from the same
+        posterior and evaluated concurrently: with a distributed ``comm`` every rank draws the
+        same batch (identical RNG and trial history), evaluates proposal ``rank`` on its own GPU
+        and the losses are all-gathered, so all ranks keep one trial list (one trial
+        per GPU).  ``batch`` defaults to the world size."""
+        world = comm.world if comm is not None and comm.is_distributed else 1
+        rank = comm.rank if world > 1 else 0
+        batch = max(1, int(batch or world))
+        done = 0
+        while done < max_evals:
+            nb = min(batch, max_evals - done)
+            props = [self.suggest() for _ in range(nb)]
+            vals = [_materialise(self.space, a) for a in props]
+            if world > 1:
+                mine = {i: float(fn(vals[i])) for i in range(rank, nb, world)}
+                losses: dict = {}
+                for part in comm.all_gather_object(mine):
+                    losses.update(part)
+            else:
+                losses = {i: float(fn(v)) for i, v in enumerate(vals)}
+            for i in range(nb):
+                self.trials.append(Trial(props[i], losses[i], vals[i]))
+            done += nb
         best = min(self.trials, key=lambda t: t.loss)
         return best.value, best.loss
 
@@ -216,9 +235,10 @@ class TPE:
         return dict(min(self.trials, key=lambda t: t.loss).assign)
 
 
-def fmin(fn: Callable[[Any], float], space, max_evals: int, seed: int = 0, **kw) -> tuple[dict, TPE]:
+def fmin(fn: Callable[[Any], float], space, max_evals: int, seed: int = 0, batch: int | None = None,
+         comm=None, **kw) -> tuple[dict, TPE]:
     t = TPE(space, seed=seed, **kw)
-    t.minimize(fn, max_evals)
+    t.minimize(fn, max_evals, batch=batch, comm=comm)
     return t.best_assignment(), t
 
 
@@ -252,7 +272,8 @@ def classifier_space(config, name: str) -> dict:
     return {"model": name, "param": params}
 
 
-def auto_supervised(classifiers: dict, max_evals: int, probs: Sequence[float] | None = None, seed: int = 0):
+def auto_supervised(classifiers: dict, max_evals: int, probs: Sequence[float] | None = None, seed: int = 0,
+                    comm=None):
     """Pick the classifier and its hyper-parameters minimising ``trainValidate()`` by TPE
     (autosupv.py:124-137).  ``classifiers``: name -> BaseClassifier.  Returns (best assignment,
     best loss, the TPE object with every trial)."""
@@ -265,5 +286,5 @@ def auto_supervised(classifiers: dict, max_evals: int, probs: Sequence[float] | 
             clf.setConfigParam(k, str(v))
         return clf.trainValidate()
 
-    best, t = fmin(evaluate, space, max_evals, seed=seed)
+    best, t = fmin(evaluate, space, max_evals, seed=seed, comm=comm)
     return best, min(tr.loss for tr in t.trials), t

@@ -4,6 +4,7 @@ optimiser behaviour on objectives with known optima and the conditional (tree) s
 import json
 
 import numpy as np
+import pytest
 
 from avenir_amd.optimize import tpe
 
@@ -67,3 +68,43 @@ def test_autosupv_cli(tmp_path, capsys):
                  "--device", "cpu"]) == 0
     out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert out["evals"] == 8 and 0 <= out["loss"] < 0.3 and "classifier" in out["best"]
+
+
+def _tpe_ranks(rank, world, max_evals):
+    from avenir_amd.optimize.search import parameter_search
+    from avenir_amd.optimize.tpe import choice, fmin, uniform
+    from avenir_amd.parallel.comm import get_comm
+    comm = get_comm()
+    evaluated = []
+
+    def loss(v):
+        evaluated.append(v)
+        return (v["x"] - 0.3) ** 2 + (0.0 if v["kind"] == "b" else 0.5)
+    space = {"x": uniform("x", -2.0, 2.0), "kind": choice("kind", ["a", "b", "c"])}
+    best, t = fmin(loss, space, max_evals, seed=7, comm=comm, n_startup=8)
+    ps_evals = []
+
+    def score(p):
+        ps_evals.append(p)
+        return abs(p["a"] - 3) + abs(p["b"] - 1)
+    pbest, pscore, _ = parameter_search({"a": list(range(8)), "b": list(range(4))}, score, "random",
+                                        n_iter=12, seed=3, comm=comm)
+    return best, [tr.loss for tr in t.trials], len(evaluated), pbest, pscore, len(ps_evals)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tpe_and_random_search_trial_parallel(world):
+    """SURVEY P8: every rank evaluates its share of each TPE batch / of the random candidates;
+    the result equals the single-process run with the same batch size, and no trial is evaluated
+    twice across ranks."""
+    from _dist import run_world
+    from avenir_amd.optimize.tpe import choice, fmin, uniform
+    res = run_world(_tpe_ranks, world, 24, timeout=300)
+    space = {"x": uniform("x", -2.0, 2.0), "kind": choice("kind", ["a", "b", "c"])}
+    ref_best, ref_t = fmin(lambda v: (v["x"] - 0.3) ** 2 + (0.0 if v["kind"] == "b" else 0.5), space, 24,
+                           seed=7, batch=world, n_startup=8)
+    for best, losses, _, pbest, pscore, _ in res:
+        assert best == ref_best and losses == [tr.loss for tr in ref_t.trials]
+        assert pbest == res[0][3] and pscore == res[0][4]
+    assert sum(r[2] for r in res) == 24                    # each TPE proposal trained once
+    assert sum(r[5] for r in res) <= 12                    # random candidates split, duplicates once
