@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import os
+import pickle
 import socket
 import traceback
 
@@ -24,7 +25,9 @@ def _worker(rank, world, port, fn, args, q):
         C.set_comm(None)
         c = C.get_comm(device="cpu", backend="gloo")
         res = fn(rank, world, *args)
-        q.put((rank, "ok", res))
+        # pickled by value here: the queue's default tensor pickler shares storage by fd, which
+        # breaks when this rank exits before the parent has received it (connection reset)
+        q.put((rank, "ok", pickle.dumps(res)))
         c.barrier()
         c.shutdown()
     except Exception:  # noqa: BLE001
@@ -45,7 +48,7 @@ def run_world(fn, world: int, *args, timeout: float = 120.0):
             rank, status, res = q.get(timeout=timeout)
             if status != "ok":
                 raise AssertionError(f"rank {rank} failed:\n{res}")
-            out[rank] = res
+            out[rank] = pickle.loads(res)
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -79,7 +82,7 @@ def run_world_outcome(fn, world: int, *args, env: dict | None = None, timeout: f
             if all(not p.is_alive() for p in procs) and q.empty():
                 break
             continue
-        (res if status == "ok" else errs)[rank] = payload
+        (res if status == "ok" else errs)[rank] = pickle.loads(payload) if status == "ok" else payload
     for p in procs:
         p.join(timeout=10)
         if p.is_alive():
