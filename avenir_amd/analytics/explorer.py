@@ -315,19 +315,19 @@ class DataExplorer:
         return {"unique values": [k for k, _ in c], "counts": [v for _, v in c]}
 
     def getStats(self, ds, nextreme: int = 5):
+        from ..ops.encode_ops import column_moments, moments_dict
         x = self.getNumericData(ds).double()
         n = x.numel()
-        m = x.mean()
-        d = x - m
-        sd = d.pow(2).mean().sqrt()
+        mo = moments_dict(column_moments(x)[0])  # K26: moments in two streaming passes
         u, c = torch.unique(x, return_counts=True)
+        xs = torch.sort(x).values
         med = torch.quantile(x, 0.5)
-        return {"length": n, "min": float(x.min()), "max": float(x.max()),
-                "n smallest": _np(torch.sort(x).values[:nextreme]).tolist(),
-                "n largest": _np(torch.sort(x, descending=True).values[:nextreme]).tolist(),
-                "mean": float(m), "median": float(med), "mode": float(u[c.argmax()]), "mode count": int(c.max()),
-                "std": float(sd), "skew": float(d.pow(3).mean() / sd ** 3),
-                "kurtosis": float(d.pow(4).mean() / sd ** 4 - 3), "mad": float((x - med).abs().median() * 1.4826)}
+        return {"length": n, "min": mo["min"], "max": mo["max"],
+                "n smallest": _np(xs[:nextreme]).tolist(),
+                "n largest": _np(xs.flip(0)[:nextreme]).tolist(),
+                "mean": mo["mean"], "median": float(med), "mode": float(u[c.argmax()]), "mode count": int(c.max()),
+                "std": mo["std"], "skew": mo["skew"],
+                "kurtosis": mo["kurtosis"], "mad": float((x - med).abs().median() * 1.4826)}
 
     def getNullCount(self, ds):
         x = self.getNumericData(ds)

@@ -1674,6 +1674,90 @@ at::Tensor gsp_join(const at::Tensor& X, int64_t lo, int64_t hi) {
   return out;
 }
 
+// K26 column moments of a column-major [F, ld] float32 / float64 matrix over its first n rows.
+// Returns double [F, 8]: count (non-NaN), sum, min, max, m2, m3, m4 (central power sums / count),
+// mean.  Two streaming passes; partials reduced with a fixed-shape sum (reproducible).
+at::Tensor col_moments(const at::Tensor& X, int64_t n) {
+  CHECK_DEV(X);
+  TORCH_CHECK(X.dim() == 2 && n >= 1 && n <= X.size(1), "X [F, ld], 1 <= n <= ld");
+  const bool f32 = X.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || X.scalar_type() == at::kDouble, "X must be float32 or float64");
+  const int64_t F = X.size(0), ld = X.size(1);
+  TORCH_CHECK(F >= 1 && F < 65536, "1 <= F < 65536 columns");
+  if (f32) TORCH_CHECK(ld % 4 == 0 && aligned(X, 16), "float32 X needs ld % 4 == 0 and 16-byte alignment");
+  DevGuard g(X.device());
+  const int nb = avk::col_moments_blocks(n, (int)F);
+  auto opt = X.options().dtype(at::kDouble);
+  auto p0 = at::empty({F, nb, 4}, opt);
+  auto p1 = at::empty({F, nb, 4}, opt);
+  auto st = cur_stream(X);
+  if (f32) avk::col_moments_f32(X.data_ptr<float>(), n, ld, (int)F, 0, nullptr, p0.data_ptr<double>(), st);
+  else avk::col_moments_f64(X.data_ptr<double>(), n, ld, (int)F, 0, nullptr, p0.data_ptr<double>(), st);
+  auto cnt = p0.select(2, 0).sum(1), sm = p0.select(2, 1).sum(1);
+  auto lo = std::get<0>(p0.select(2, 2).min(1)), hi = std::get<0>(p0.select(2, 3).max(1));
+  auto mean = (sm / cnt.clamp_min(1.0)).contiguous();
+  if (f32) avk::col_moments_f32(X.data_ptr<float>(), n, ld, (int)F, 1, mean.data_ptr<double>(), p1.data_ptr<double>(), st);
+  else avk::col_moments_f64(X.data_ptr<double>(), n, ld, (int)F, 1, mean.data_ptr<double>(), p1.data_ptr<double>(), st);
+  auto c1 = cnt.clamp_min(1.0);
+  auto m2 = p1.select(2, 0).sum(1) / c1, m3 = p1.select(2, 1).sum(1) / c1, m4 = p1.select(2, 2).sum(1) / c1;
+  return at::stack({cnt, sm, lo, hi, m2, m3, m4, mean}, 1);
+}
+
+// K23 leave-one-out statistics: codes [F, ld] uint8 (m = 256) or uint16 (m = 65536), y double [n]
+// -> (sum double [F, m], count int32 [F, m]) over the first n rows.
+py::tuple loo_stats(const at::Tensor& codes, int64_t n, const at::Tensor& y) {
+  CHECK_DEV(codes);
+  CHECK_DEV(y);
+  CHECK_DTYPE(y, at::kDouble);
+  const bool wide = codes.scalar_type() == at::kUInt16;
+  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8 or uint16");
+  TORCH_CHECK(codes.dim() == 2 && n >= 0 && n <= codes.size(1) && y.numel() >= n, "codes [F, ld], y [>= n]");
+  const int64_t F = codes.size(0), m = wide ? 65536 : 256;
+  TORCH_CHECK(F >= 1 && F < 65536, "1 <= F < 65536 columns");
+  DevGuard g(codes.device());
+  auto sum = at::zeros({F, m}, y.options());
+  auto cnt = at::zeros({F, m}, codes.options().dtype(at::kInt));
+  if (n > 0)
+    avk::loo_stats(codes.data_ptr(), wide, codes.size(1), n, (int)F, y.data_ptr<double>(), sum.data_ptr<double>(),
+                   reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), cur_stream(codes));
+  return py::make_tuple(sum, cnt);
+}
+
+// K23 leave-one-out apply -> float32 [n, F] (row-major); noise double [F, n] uniforms or undefined.
+at::Tensor loo_apply(const at::Tensor& codes, int64_t n, const at::Tensor& y, const at::Tensor& sum,
+                     const at::Tensor& cnt, const at::Tensor& gmean, double reg,
+                     const c10::optional<at::Tensor>& noise, double amp) {
+  CHECK_DEV(codes);
+  CHECK_DEV(y);
+  CHECK_DEV(sum);
+  CHECK_DEV(cnt);
+  CHECK_DEV(gmean);
+  CHECK_DTYPE(y, at::kDouble);
+  CHECK_DTYPE(sum, at::kDouble);
+  CHECK_DTYPE(cnt, at::kInt);
+  CHECK_DTYPE(gmean, at::kDouble);
+  const bool wide = codes.scalar_type() == at::kUInt16;
+  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8 or uint16");
+  const int64_t F = codes.size(0), m = wide ? 65536 : 256;
+  TORCH_CHECK(codes.dim() == 2 && n >= 0 && n <= codes.size(1) && y.numel() >= n, "codes [F, ld], y [>= n]");
+  TORCH_CHECK(sum.numel() == F * m && cnt.numel() == F * m && gmean.numel() >= 1, "stats tables [F, m]");
+  TORCH_CHECK((n + 255) / 256 < (1LL << 31), "too many rows");
+  const double* nz = nullptr;
+  if (noise.has_value() && noise->defined()) {
+    CHECK_DEV((*noise));
+    CHECK_DTYPE((*noise), at::kDouble);
+    TORCH_CHECK(noise->numel() == F * n, "noise [F, n]");
+    nz = noise->data_ptr<double>();
+  }
+  DevGuard g(codes.device());
+  auto out = at::empty({n, F}, y.options().dtype(at::kFloat));
+  if (n > 0)
+    avk::loo_apply(codes.data_ptr(), wide, codes.size(1), n, (int)F, y.data_ptr<double>(), sum.data_ptr<double>(),
+                   reinterpret_cast<const unsigned*>(cnt.data_ptr<int>()), gmean.data_ptr<double>(), reg, nz, amp,
+                   out.data_ptr<float>(), cur_stream(codes));
+  return out;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host runtime
 
@@ -1876,6 +1960,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("uniformization", &uniformization);
   m.def("dot_matrix", &dot_matrix);
   m.def("gsp_join", &gsp_join);
+  m.def("col_moments", &col_moments);
+  m.def("loo_stats", &loo_stats);
+  m.def("loo_apply", &loo_apply, py::arg("codes"), py::arg("n"), py::arg("y"), py::arg("sum"), py::arg("cnt"),
+        py::arg("gmean"), py::arg("reg"), py::arg("noise") = py::none(), py::arg("amp") = 0.0);
   m.def("forest_hist", &forest_hist);
   m.def("bucketize_u8", &bucketize_u8);
   m.def("forest_split", &forest_split);

@@ -202,6 +202,18 @@ void gsp_count(const int* X, int N, int k, int lo, int hi, int* seg_start, int* 
 void gsp_emit(const int* X, int k, int lo, int hi, const int* seg_start, const int* seg_len, const long long* offs,
               int* out, hipStream_t stream);
 
+// encode.hip (K26 column moments, K23 leave-one-out target encoding)
+int col_moments_blocks(long long n, int F);
+void col_moments_f32(const float* X, long long n, long long ld, int F, int pass, const double* mean, double* part,
+                     hipStream_t stream);
+void col_moments_f64(const double* X, long long n, long long ld, int F, int pass, const double* mean, double* part,
+                     hipStream_t stream);
+void loo_stats(const void* codes, bool wide, long long ld, long long n, int F, const double* y, double* sum,
+               unsigned* cnt, hipStream_t stream);
+void loo_apply(const void* codes, bool wide, long long ld, long long n, int F, const double* y, const double* sum,
+               const unsigned* cnt, const double* gmean, double reg, const double* noise, double amp, float* out,
+               hipStream_t stream);
+
 // ---- rnn.hip (K27 persistent LSTM recurrence, bf16 MFMA) -------------------------------------
 // KS = HP / 32 (HP = hidden size padded to 32, 64 or 128), IS = IP / 32 likewise for the layer
 // input size, RT = 16-sequence tiles per workgroup.

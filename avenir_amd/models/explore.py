@@ -338,38 +338,67 @@ def leave_one_out_encoding(t: Table, target: torch.Tensor, noise: float = 0.0, r
                            seed: int = 0, comm: Comm | None = None) -> torch.Tensor:
     """Leave-one-out target mean per categorical value (S/explore/CategoricalLeaveOneOutEncoding):
     (sum_v - y_i + reg * global_mean) / (count_v - 1 + reg), optional multiplicative noise."""
+    from ..ops import encode_ops as E
     n = t.n
-    y = target[:n].double()
+    y = target[:n].double().to(t.codes.device)
     g = torch.Generator(device="cpu")
     g.manual_seed(seed)
-    cols = []
     gsum = y.sum().view(1)
     gcnt = torch.tensor([float(n)], dtype=torch.float64, device=y.device)
-    _reduce(comm, gsum, gcnt)
-    gmean = gsum / gcnt
-    for j, f in enumerate(t.binned_fields):
-        c = t.codes[j, :n].long()
-        m = t.missing + 1
-        s = torch.zeros(m, dtype=torch.float64, device=y.device).index_add_(0, c, y)
-        k = torch.zeros(m, dtype=torch.float64, device=y.device).index_add_(0, c, torch.ones_like(y))
-        _reduce(comm, s, k)
-        v = (s[c] - y + reg * gmean) / (k[c] - 1 + reg).clamp_min(1e-12)
-        if noise > 0:
-            v = v * (1 + noise * (2 * torch.rand(n, generator=g).to(v.device).double() - 1))
-        cols.append(v.float())
-    return torch.stack(cols, 1)
+    nf = len(t.binned_fields)
+    codes = t.codes[:nf]
+    s, k = E.loo_stats(codes, n, y)  # K23: per (column, value) target sums and counts
+    _reduce(comm, gsum, gcnt, s, k)
+    # one uniform stream per column, drawn in column order from the seeded host generator
+    u = torch.stack([torch.rand(n, generator=g) for _ in range(nf)]).double() if noise > 0 else None
+    return E.loo_apply(codes, n, y, s, k, gsum / gcnt, reg=reg, noise=u, amp=float(noise))
+
+
+def _hash_slot(j: int, v: str, size: int, signed: bool) -> tuple[int, float]:
+    h = int.from_bytes(hashlib.md5(f"{j}:{v}".encode()).digest()[:8], "little")
+    return h % size, (-1.0 if (signed and (h >> 63) & 1) else 1.0)
 
 
 def feature_hashing(values: Sequence[Sequence[str]], size: int, signed: bool = True) -> torch.Tensor:
     """Hashing trick over categorical strings (index hash + sign hash), [n, size]
-    (S/explore/CategoricalFeatureHashingEncoding.scala:107-119)."""
-    out = torch.zeros((len(values), size), dtype=torch.float32)
-    for i, row in enumerate(values):
+    (S/explore/CategoricalFeatureHashingEncoding.scala:107-119).  Each distinct (column, value) is
+    hashed once; the rows are then one vectorised scatter-add."""
+    cache: dict[tuple[int, str], int] = {}
+    slots, signs, keys = [], [], []
+    for row in values:
         for j, v in enumerate(row):
-            h = int.from_bytes(hashlib.md5(f"{j}:{v}".encode()).digest()[:8], "little")
-            idx = h % size
-            sgn = -1.0 if (signed and (h >> 63) & 1) else 1.0
-            out[i, idx] += sgn
+            key = (j, v)
+            u = cache.get(key)
+            if u is None:
+                u = cache[key] = len(slots)
+                idx, sg = _hash_slot(j, v, size, signed)
+                slots.append(idx)
+                signs.append(sg)
+            keys.append(u)
+    out = torch.zeros((len(values), size), dtype=torch.float32)
+    if not keys:
+        return out
+    lens = torch.tensor([len(r) for r in values])
+    rows = torch.repeat_interleave(torch.arange(len(values)), lens)
+    k = torch.tensor(keys)
+    return out.index_put_((rows, torch.tensor(slots)[k]), torch.tensor(signs, dtype=torch.float32)[k],
+                          accumulate=True)
+
+
+def feature_hashing_table(t: Table, size: int, signed: bool = True) -> torch.Tensor:
+    """``feature_hashing`` of a Table's categorical columns on its device: every dictionary value
+    is hashed once on the host into a per-column (slot, sign) lookup table, the [n, size] matrix is
+    built by one gather + scatter-add over the resident codes (no per-record host work)."""
+    cats = [(j, f) for j, f in enumerate(t.binned_fields) if f.is_categorical]
+    out = torch.zeros((t.n, size), dtype=torch.float32, device=t.device)
+    rows = torch.arange(t.n, device=t.device)
+    for pos, (j, f) in enumerate(cats):
+        lut_i = torch.zeros(t.missing + 1, dtype=torch.long)
+        lut_s = torch.zeros(t.missing + 1, dtype=torch.float32)  # missing code contributes 0
+        for k, v in enumerate(f.cardinality):
+            lut_i[k], lut_s[k] = _hash_slot(pos, v, size, signed)
+        c = t.codes[j, : t.n].long()
+        out.index_put_((rows, lut_i.to(t.device)[c]), lut_s.to(t.device)[c], accumulate=True)
     return out
 
 

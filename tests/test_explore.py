@@ -79,6 +79,12 @@ def test_supervised_encodings(tmp_path):
     assert dummy.shape[1] == 18 and int(dummy.sum()) == 2000 * 5
     fh = E.feature_hashing([["a", "b"], ["a", "c"]], 16)
     assert fh.shape == (2, 16) and float(fh.abs().sum()) == 4
+    # Table / device variant == the string API over the same categorical values
+    cats = [f for f in t.binned_fields if f.is_categorical]
+    strs = [[f.bin_label(int(t.codes[j, i])) for j, f in enumerate(t.binned_fields) if f.is_categorical]
+            for i in range(t.n)]
+    assert torch.equal(E.feature_hashing_table(t, 32), E.feature_hashing(strs, 32))
+    assert len(cats) == len(strs[0])
 
 
 def test_numerical_correlation():
