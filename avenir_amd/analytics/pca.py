@@ -122,6 +122,13 @@ class IncrementalPCA:
         for k, key in enumerate(keys):
             X[k, : lens[k]] = torch.as_tensor(streams[key], dtype=torch.float64, device=dev)
         hidx = torch.arange(H, device=dev).view(1, -1)
+        if dev.type == "cuda" and D <= 64 and K:
+            # K24 (pca.hip): one wave per key runs its whole stream in one launch
+            from .. import _native
+            nh32 = nh.int()
+            _native.C().spirit_update(X, lens.int(), W, E, he, ve, cnt, nh32, float(self.lam), float(self.lo),
+                                      float(self.hi))
+            nh, T = nh32.long(), 0
         for t in range(T):
             live = (lens > t)
             x = X[:, t].clone()                                           # [K, D]

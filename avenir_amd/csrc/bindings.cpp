@@ -1758,6 +1758,34 @@ at::Tensor loo_apply(const at::Tensor& codes, int64_t n, const at::Tensor& y, co
   return out;
 }
 
+// K24 streaming PCA: advances every key's state (W [K, H, D], E / he [K, H], ve / cnt [K], nh int32
+// [K]) over its stream X [K, T, D] (first lens[k] records), in place.
+void spirit_update(const at::Tensor& X, const at::Tensor& lens, at::Tensor W, at::Tensor E, at::Tensor he,
+                   at::Tensor ve, at::Tensor cnt, at::Tensor nh, double lam, double lo, double hi) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &W, &E, &he, &ve, &cnt}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kDouble);
+  }
+  CHECK_DEV(lens);
+  CHECK_DEV(nh);
+  CHECK_DTYPE(lens, at::kInt);
+  CHECK_DTYPE(nh, at::kInt);
+  TORCH_CHECK(X.dim() == 3 && W.dim() == 3, "X [K, T, D], W [K, H, D]");
+  const int64_t K = X.size(0), T = X.size(1), D = X.size(2), H = W.size(1);
+  TORCH_CHECK(D >= 1 && D <= 64 && H >= 1 && H <= D, "spirit kernel: 1 <= H <= D <= 64");
+  TORCH_CHECK(W.size(0) == K && W.size(2) == D && E.numel() == K * H && he.numel() == K * H && ve.numel() == K &&
+                  cnt.numel() == K && nh.numel() == K && lens.numel() == K, "state shapes");
+  if (K == 0) return;
+  // host copies bound-check the per-key lengths and unit counts before the launch
+  auto lh = lens.cpu(), nhh = nh.cpu();
+  TORCH_CHECK(lh.min().item<int>() >= 0 && lh.max().item<int>() <= T, "lens in [0, T]");
+  TORCH_CHECK(nhh.min().item<int>() >= 1 && nhh.max().item<int>() <= H, "nh in [1, H]");
+  DevGuard g(X.device());
+  avk::spirit_update(X.data_ptr<double>(), (int)K, (int)T, (int)D, (int)H, lens.data_ptr<int>(), W.data_ptr<double>(),
+                     E.data_ptr<double>(), he.data_ptr<double>(), ve.data_ptr<double>(), cnt.data_ptr<double>(),
+                     nh.data_ptr<int>(), lam, lo, hi, cur_stream(X));
+}
+
 // ---------------------------------------------------------------------------------------------
 // host runtime
 
@@ -1960,6 +1988,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("uniformization", &uniformization);
   m.def("dot_matrix", &dot_matrix);
   m.def("gsp_join", &gsp_join);
+  m.def("spirit_update", &spirit_update);
   m.def("col_moments", &col_moments);
   m.def("loo_stats", &loo_stats);
   m.def("loo_apply", &loo_apply, py::arg("codes"), py::arg("n"), py::arg("y"), py::arg("sum"), py::arg("cnt"),

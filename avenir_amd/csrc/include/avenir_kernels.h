@@ -214,6 +214,10 @@ void loo_apply(const void* codes, bool wide, long long ld, long long n, int F, c
                const unsigned* cnt, const double* gmean, double reg, const double* noise, double amp, float* out,
                hipStream_t stream);
 
+// pca.hip (K24 streaming PCA, one wave per key; D <= 64, H <= D)
+void spirit_update(const double* X, int K, int T, int D, int H, const int* lens, double* W, double* E, double* he,
+                   double* ve, double* cnt, int* nh, double lam, double lo, double hi, hipStream_t stream);
+
 // ---- rnn.hip (K27 persistent LSTM recurrence, bf16 MFMA) -------------------------------------
 // KS = HP / 32 (HP = hidden size padded to 32, 64 or 128), IS = IP / 32 likewise for the layer
 // input size, RT = 16-sequence tiles per workgroup.

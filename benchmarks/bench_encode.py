@@ -1,7 +1,11 @@
 """Throughput of the K26 column-moments and K23 leave-one-out kernels (encode.hip) on one GPU,
 with the equivalent PyTorch-op chains as the comparison; one JSON line per case."""
 import json
+import os
+import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 

@@ -3,7 +3,7 @@
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_encode_ops.py tests/test_wide.py -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/enc_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_encode_ops.py tests/test_wide.py tests/test_analytics.py -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/enc_tests.log 2>&1
 rc=$?; tail -15 gpurun_out/enc_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u benchmarks/bench_encode.py > gpurun_out/enc_bench.log 2>&1 || exit $?
 cat gpurun_out/enc_bench.log

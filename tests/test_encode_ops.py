@@ -102,3 +102,23 @@ def test_explorer_getstats_gpu(cuda):
     a, b = dc.getStats("x"), dg.getStats("x")
     for key in ("mean", "std", "skew", "kurtosis", "min", "max", "median"):
         assert math.isclose(a[key], b[key], rel_tol=1e-9), key
+
+
+@pytest.mark.gpu
+def test_incremental_pca_kernel_matches_cpu(cuda):
+    """K24 spirit_kernel (one wave per key) == the torch recurrence on the CPU, across two update
+    calls (state carried), keys of different lengths and unit growth / shrink."""
+    from avenir_amd.analytics import IncrementalPCA
+    g = torch.Generator().manual_seed(5)
+    D = 12
+    mix = torch.randn(D, D, generator=g, dtype=torch.float64)
+    streams = [{f"k{j}": (torch.randn(40 + 7 * j, D, generator=g, dtype=torch.float64) * torch.linspace(3, 0.1, D,
+                dtype=torch.float64)) @ mix for j in range(5)} for _ in range(2)]
+    a, b = IncrementalPCA(D, init_hidden=1, forget=0.97), IncrementalPCA(D, init_hidden=1, forget=0.97, device=cuda)
+    for s in streams:
+        sa, sb = a.update(s), b.update(s)
+    for key in sa:
+        assert sa[key].num_hidden == sb[key].num_hidden and sa[key].count == sb[key].count
+        assert torch.allclose(sa[key].components, sb[key].components.cpu(), rtol=1e-8, atol=1e-9)
+        assert all(math.isclose(x, y, rel_tol=1e-8, abs_tol=1e-12)
+                   for x, y in zip(sa[key].hidden_unit_energy, sb[key].hidden_unit_energy))
