@@ -94,6 +94,10 @@ class IncrementalPCA:
                  low_energy: float = 0.95, high_energy: float = 0.98, device="cpu"):
         self.D, self.H0 = dimension, init_hidden
         self.Hmax = max_hidden or dimension
+        if not 1 <= self.Hmax <= dimension:
+            raise ValueError(f"max_hidden must be in [1, dimension={dimension}], got {self.Hmax}")
+        if not 1 <= init_hidden <= self.Hmax:
+            raise ValueError(f"init_hidden must be in [1, max_hidden={self.Hmax}], got {init_hidden}")
         self.lam, self.lo, self.hi = forget, low_energy, high_energy
         self.device = torch.device(device)
         self.states: dict[str, PrincipalCompState] = {}
@@ -122,7 +126,7 @@ class IncrementalPCA:
         for k, key in enumerate(keys):
             X[k, : lens[k]] = torch.as_tensor(streams[key], dtype=torch.float64, device=dev)
         hidx = torch.arange(H, device=dev).view(1, -1)
-        if dev.type == "cuda" and D <= 64 and K:
+        if dev.type == "cuda" and D <= 64 and H <= D and K:
             # K24 (pca.hip): one wave per key runs its whole stream in one launch
             from .. import _native
             nh32 = nh.int()

@@ -60,4 +60,6 @@ def main(argv: list[str] | None = None) -> int:
 
 
 if __name__ == "__main__":
+    from . import freeze_startup_objects
+    freeze_startup_objects()
     sys.exit(main())

@@ -1,4 +1,8 @@
 #include <cstring>
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <unistd.h>
 #include <sys/stat.h>
@@ -1458,6 +1462,33 @@ std::vector<at::Tensor> linear_act_bwd(const at::Tensor& dY, const at::Tensor& Y
     TORCH_CHECK(_e == hipSuccess, #expr, " failed: ", hipGetErrorString(_e));        \
   } while (0)
 
+// Pinned staging ring of the device uploads: one per device index (events belong to the device
+// that was current when they were created), each behind a mutex so concurrent loads from several
+// threads never share a slot; a call waits for every slot's last DMA before reusing it.
+constexpr int SLOTS = 4;
+constexpr int64_t SLOT = 64LL << 20;
+struct StagingRing {
+  std::mutex mu;
+  void* buf[SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t done[SLOTS];
+};
+
+static StagingRing& staging_ring(int device) {
+  static std::mutex reg_mu;
+  static std::map<int, std::unique_ptr<StagingRing>> rings;
+  std::lock_guard<std::mutex> g(reg_mu);
+  auto& r = rings[device];
+  if (!r) {
+    r = std::make_unique<StagingRing>();
+    for (int i = 0; i < SLOTS; ++i) {
+      BIND_HIP_CHECK(hipHostMalloc(&r->buf[i], SLOT, hipHostMallocDefault));
+      BIND_HIP_CHECK(hipEventCreateWithFlags(&r->done[i], hipEventDisableTiming));
+      BIND_HIP_CHECK(hipEventRecord(r->done[i], nullptr));  // completed: the first wait returns at once
+    }
+  }
+  return *r;
+}
+
 static uint32_t fnv1a_fold(const std::string& v) {
   uint32_t h = 2166136261u;
   for (unsigned char c : v) h = (h ^ c) * 16777619u;
@@ -1483,15 +1514,12 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
     const char* map = static_cast<const char*>(mmap(nullptr, (size_t)size, PROT_READ, MAP_PRIVATE, fd, 0));
     TORCH_CHECK(map != MAP_FAILED, "mmap failed for ", path);
     madvise(const_cast<char*>(map), (size_t)size, MADV_SEQUENTIAL);
-    constexpr int SLOTS = 4;
-    constexpr int64_t SLOT = 64LL << 20;
-    static void* ring[SLOTS] = {nullptr, nullptr, nullptr, nullptr};
-    static hipEvent_t done[SLOTS];
-    if (!ring[0])
-      for (int i = 0; i < SLOTS; ++i) {
-        BIND_HIP_CHECK(hipHostMalloc(&ring[i], SLOT, hipHostMallocDefault));
-        BIND_HIP_CHECK(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
-      }
+    StagingRing& R = staging_ring(like.device().index());
+    std::lock_guard<std::mutex> hold(R.mu);  // one upload at a time per device ring
+    void** ring = R.buf;
+    hipEvent_t* done = R.done;
+    // a previous call's last DMAs may still read the slots (they ran on that call's stream)
+    for (int i = 0; i < SLOTS; ++i) BIND_HIP_CHECK(hipEventSynchronize(done[i]));
     int64_t k = 0;
     for (int64_t off = 0; off < size; off += SLOT, ++k) {
       const int slot = (int)(k % SLOTS);
@@ -1855,6 +1883,256 @@ std::string format_rows(py::object prefix, const at::Tensor& cols, std::vector<i
                           delim.empty() ? ',' : delim[0], nthreads);
 }
 
+// TextShard tokenizer (records.cpp): returns (off int64 [L+1], codes int32 [T], sub int32 [T] or None,
+// nums float64 [T] or None, vocab list[str]).
+py::tuple text_tokenize(avh::TextShard& sh, const std::string& delims, const std::string& sub_delim,
+                        const std::string& modes, const std::string& tail_mode, bool trim, bool want_nums) {
+  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1, "sub_delim: 0/1 char, tail_mode: 1 char");
+  for (char c : modes + tail_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
+  avh::TokenSpec sp;
+  sp.delims = delims.empty() ? std::string(",") : delims;
+  sp.sub_delim = sub_delim.empty() ? 0 : sub_delim[0];
+  sp.modes = modes;
+  sp.tail_mode = tail_mode[0];
+  sp.trim = trim;
+  const int64_t L = sh.num_lines();
+  int64_t T;
+  {
+    py::gil_scoped_release rel;
+    T = sh.count_tokens(sp);
+  }
+  auto o = at::TensorOptions();
+  auto off = at::empty({L + 1}, o.dtype(at::kLong));
+  auto codes = at::empty({T}, o.dtype(at::kInt));
+  at::Tensor sub, nums;
+  if (sp.sub_delim) sub = at::empty({T}, o.dtype(at::kInt));
+  if (want_nums) nums = at::empty({T}, o.dtype(at::kDouble));
+  {
+    py::gil_scoped_release rel;
+    sh.tokenize(off.data_ptr<int64_t>(), codes.data_ptr<int32_t>(), sub.defined() ? sub.data_ptr<int32_t>() : nullptr,
+                nums.defined() ? nums.data_ptr<double>() : nullptr);
+  }
+  py::object subo = sub.defined() ? py::cast(sub) : py::none();
+  py::object numo = nums.defined() ? py::cast(nums) : py::none();
+  return py::make_tuple(off, codes, subo, numo, sh.vocab());
+}
+
+std::vector<std::string> text_field_strings(const avh::TextShard& sh, const at::Tensor& line, const at::Tensor& field) {
+  TORCH_CHECK(!line.is_cuda() && !field.is_cuda() && line.numel() == field.numel(), "CPU line / field index tensors");
+  auto l = line.to(at::kLong).contiguous();
+  auto f = field.to(at::kInt).contiguous();
+  py::gil_scoped_release rel;
+  return sh.field_strings(l.data_ptr<int64_t>(), f.data_ptr<int32_t>(), l.numel());
+}
+
+// K1 device tokenizer (records.hip): this rank's byte range is uploaded through the pinned staging
+// ring and tokenized on the GPU.  Same result as TextShard.tokenize (codes in first-occurrence
+// order, the same vocabulary).  Returns (off, codes, sub | None, nums | None, vocab, stats) with the
+// tensors on ``like``'s device, or None when the exactness check found a hash collision (the
+// caller then uses the host tokenizer).
+py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, int64_t world,
+                                const std::string& delims_in, const std::string& sub_delim, const std::string& modes,
+                                const std::string& tail_mode, bool trim, bool want_nums, const at::Tensor& like) {
+  CHECK_DEV(like);
+  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && modes.size() <= 64, "bad tokenizer options");
+  for (char c : modes + tail_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
+  const std::string delims = delims_in.empty() ? std::string(",") : delims_in;
+  const char sd = sub_delim.empty() ? 0 : sub_delim[0];
+  DevGuard g(like.device());
+  hipStream_t stream = cur_stream(like);
+  auto t0 = std::chrono::steady_clock::now();
+  std::unique_ptr<avh::ByteShard> sh;
+  {
+    py::gil_scoped_release rel;
+    sh = std::make_unique<avh::ByteShard>(paths, rank, world, false);
+  }
+  // ---- upload: segments streamed through the ring, each newline-terminated ----
+  const auto& segs = sh->segments();
+  int64_t size = 0;
+  for (auto& sg : segs) size += sg.len + ((sg.len > 0 && sg.p[sg.len - 1] != '\n') ? 1 : 0);
+  const int64_t padded = std::max<int64_t>(16, (size + 15) / 16 * 16);
+  auto dopt = like.options().dtype(at::kByte);
+  auto dev = at::empty({padded}, dopt);
+  if (padded > size) BIND_HIP_CHECK(hipMemsetAsync(dev.data_ptr<uint8_t>() + size, 0, padded - size, stream));
+  {
+    py::gil_scoped_release rel;
+    struct Piece { const char* p; int64_t len; };
+    static const char nl = '\n';
+    std::vector<Piece> pieces;
+    for (auto& sg : segs) {
+      if (sg.len <= 0) continue;
+      pieces.push_back({sg.p, sg.len});
+      if (sg.p[sg.len - 1] != '\n') pieces.push_back({&nl, 1});
+    }
+    StagingRing& R = staging_ring(like.device().index());
+    std::lock_guard<std::mutex> hold(R.mu);
+    for (int i = 0; i < SLOTS; ++i) BIND_HIP_CHECK(hipEventSynchronize(R.done[i]));
+    int64_t out = 0, k = 0;
+    size_t pi = 0;
+    int64_t pofs = 0;
+    while (out < size) {
+      const int slot = (int)(k % SLOTS);
+      if (k >= SLOTS) BIND_HIP_CHECK(hipEventSynchronize(R.done[slot]));
+      // fill the slot from the piece list (parallel memcpy of each run)
+      int64_t fill = 0;
+      char* dst = static_cast<char*>(R.buf[slot]);
+      while (fill < SLOT && pi < pieces.size()) {
+        const int64_t n = std::min(SLOT - fill, pieces[pi].len - pofs);
+        const char* src = pieces[pi].p + pofs;
+        const int T = n >= (8 << 20) ? 8 : 1;
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t)
+          th.emplace_back([&, t] {
+            const int64_t a = n * t / T, b = n * (t + 1) / T;
+            std::memcpy(dst + fill + a, src + a, (size_t)(b - a));
+          });
+        std::memcpy(dst + fill, src, (size_t)(n / T));
+        for (auto& x : th) x.join();
+        fill += n;
+        pofs += n;
+        if (pofs == pieces[pi].len) { ++pi; pofs = 0; }
+      }
+      BIND_HIP_CHECK(hipMemcpyAsync(dev.data_ptr<uint8_t>() + out, R.buf[slot], (size_t)fill, hipMemcpyHostToDevice,
+                                    stream));
+      BIND_HIP_CHECK(hipEventRecord(R.done[slot], stream));
+      out += fill;
+      ++k;
+    }
+  }
+  sh.reset();
+  auto t1 = std::chrono::steady_clock::now();
+  const uint8_t* bytes = dev.data_ptr<uint8_t>();
+  auto lopt = like.options().dtype(at::kLong);
+  auto iopt = like.options().dtype(at::kInt);
+  // ---- newline index -> raw lines (every segment ends with '\n') ----
+  const int64_t nch = std::max<int64_t>(1, avk::csv_chunks(size));
+  auto counts = at::zeros({nch}, iopt);
+  avk::csv_newline_counts(bytes, size, reinterpret_cast<unsigned*>(counts.data_ptr<int>()), stream);
+  auto c64 = counts.to(at::kLong);
+  auto incl = c64.cumsum(0);
+  auto coff = (incl - c64).contiguous();
+  const int64_t nraw = size > 0 ? incl[-1].item<int64_t>() : 0;
+  auto pos = at::empty({std::max<int64_t>(1, nraw)}, lopt);
+  if (nraw) avk::csv_newline_positions(bytes, size, reinterpret_cast<long long*>(coff.data_ptr<int64_t>()),
+                                       reinterpret_cast<long long*>(pos.data_ptr<int64_t>()), stream);
+  auto ls = at::empty({std::max<int64_t>(1, nraw)}, lopt), le = at::empty_like(ls);
+  auto nt = at::zeros({std::max<int64_t>(1, nraw)}, iopt);
+  avk::rec_lines(bytes, reinterpret_cast<const long long*>(pos.data_ptr<int64_t>()), nraw, delims.data(),
+                 (int)delims.size(), reinterpret_cast<long long*>(ls.data_ptr<int64_t>()),
+                 reinterpret_cast<long long*>(le.data_ptr<int64_t>()), nt.data_ptr<int>(), stream);
+  ls = ls.narrow(0, 0, nraw);
+  le = le.narrow(0, 0, nraw);
+  nt = nt.narrow(0, 0, nraw);
+  if (nraw && !(nt > 0).all().item<bool>()) {  // drop blank lines
+    auto idx = at::nonzero(nt > 0).view({-1});
+    ls = ls.index({idx});
+    le = le.index({idx});
+    nt = nt.index({idx});
+  }
+  ls = ls.contiguous();
+  le = le.contiguous();
+  const int64_t L = ls.numel();
+  auto off = at::zeros({L + 1}, lopt);
+  if (L) off.narrow(0, 1, L).copy_(nt.to(at::kLong).cumsum(0));
+  const int64_t T = L ? off[L].item<int64_t>() : 0;
+  // ---- tokens + dictionary table ----
+  auto cap_for = [](int64_t n) {
+    int64_t c = 1024;
+    while (c < 2 * n) c <<= 1;
+    return c;
+  };
+  const int64_t tdict = T * (sd ? 2 : 1);
+  int64_t cap = std::min<int64_t>(cap_for(tdict), 1LL << 24);
+  auto tslot = at::empty({std::max<int64_t>(1, T)}, iopt);
+  auto th2 = at::empty({std::max<int64_t>(1, T)}, iopt);
+  at::Tensor tsub, th2s, nums;
+  if (sd) {
+    tsub = at::empty({std::max<int64_t>(1, T)}, iopt);
+    th2s = at::empty({std::max<int64_t>(1, T)}, iopt);
+  }
+  if (want_nums) nums = at::empty({std::max<int64_t>(1, T)}, like.options().dtype(at::kDouble));
+  at::Tensor keys, h2tab, first;
+  auto ctr = at::zeros({2}, iopt);  // inserted, overflow
+  while (true) {
+    keys = at::zeros({cap}, lopt);
+    h2tab = at::empty({cap}, iopt);
+    first = at::full({cap}, -1, lopt);  // all ones = EMPTY_FIRST
+    ctr.zero_();
+    avk::rec_tokens(bytes, reinterpret_cast<const long long*>(ls.data_ptr<int64_t>()),
+                    reinterpret_cast<const long long*>(le.data_ptr<int64_t>()),
+                    reinterpret_cast<const long long*>(off.data_ptr<int64_t>()), L, delims.data(), (int)delims.size(),
+                    modes.data(), (int)modes.size(), tail_mode[0], sd, trim,
+                    reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()),
+                    reinterpret_cast<unsigned*>(h2tab.data_ptr<int>()),
+                    reinterpret_cast<unsigned long long*>(first.data_ptr<int64_t>()), (unsigned long long)(cap - 1),
+                    tslot.data_ptr<int>(), reinterpret_cast<unsigned*>(th2.data_ptr<int>()),
+                    sd ? tsub.data_ptr<int>() : nullptr, sd ? reinterpret_cast<unsigned*>(th2s.data_ptr<int>()) : nullptr,
+                    want_nums ? nums.data_ptr<double>() : nullptr, reinterpret_cast<unsigned*>(ctr.data_ptr<int>()),
+                    reinterpret_cast<unsigned*>(ctr.data_ptr<int>()) + 1, stream);
+    const bool over = ctr[1].item<int>() != 0;
+    if (!over) break;
+    TORCH_CHECK(cap < (1LL << 31), "device tokenizer: dictionary table exceeds 2^31 slots");
+    cap <<= 2;  // more distinct values than the table holds at load 1/2: retry with a 4x table
+  }
+  // ---- dense codes in first-occurrence order ----
+  auto used = at::nonzero(first != -1).view({-1});
+  const int64_t D = used.numel();
+  auto focc = first.index({used});
+  // first-occurrence keys are unique and non-negative as int64 (< 2^62), so a signed sort orders them
+  auto order = std::get<1>(focc.sort());
+  auto occ = focc.index({order}).contiguous();
+  auto slot_code = at::full({cap}, -1, iopt);
+  slot_code.index_put_({used.index({order})}, at::arange(D, iopt));
+  auto mism = at::zeros({1}, iopt);
+  auto codes = at::empty({std::max<int64_t>(1, T)}, iopt);
+  avk::rec_codes(tslot.data_ptr<int>(), reinterpret_cast<const unsigned*>(th2.data_ptr<int>()), T,
+                 slot_code.data_ptr<int>(), reinterpret_cast<const unsigned*>(h2tab.data_ptr<int>()),
+                 codes.data_ptr<int>(), reinterpret_cast<unsigned*>(mism.data_ptr<int>()), stream);
+  at::Tensor subc;
+  if (sd) {
+    subc = at::empty({std::max<int64_t>(1, T)}, iopt);
+    avk::rec_codes(tsub.data_ptr<int>(), reinterpret_cast<const unsigned*>(th2s.data_ptr<int>()), T,
+                   slot_code.data_ptr<int>(), reinterpret_cast<const unsigned*>(h2tab.data_ptr<int>()),
+                   subc.data_ptr<int>(), reinterpret_cast<unsigned*>(mism.data_ptr<int>()), stream);
+  }
+  // ---- vocabulary bytes ----
+  auto vstart = at::empty({std::max<int64_t>(1, D)}, lopt);
+  auto vlen = at::empty({std::max<int64_t>(1, D)}, iopt);
+  avk::rec_vocab(bytes, reinterpret_cast<const long long*>(ls.data_ptr<int64_t>()),
+                 reinterpret_cast<const long long*>(le.data_ptr<int64_t>()),
+                 reinterpret_cast<const long long*>(off.data_ptr<int64_t>()), L,
+                 reinterpret_cast<const unsigned long long*>(occ.data_ptr<int64_t>()), D, delims.data(),
+                 (int)delims.size(), sd, trim, reinterpret_cast<long long*>(vstart.data_ptr<int64_t>()),
+                 vlen.data_ptr<int>(), stream);
+  auto vl64 = vlen.narrow(0, 0, D).to(at::kLong);
+  auto vincl = vl64.cumsum(0);
+  auto vout = (vincl - vl64).contiguous();
+  const int64_t VB = D ? vincl[-1].item<int64_t>() : 0;
+  auto vbytes = at::empty({std::max<int64_t>(1, VB)}, dopt);
+  avk::rec_gather(bytes, reinterpret_cast<const long long*>(vstart.data_ptr<int64_t>()), vlen.data_ptr<int>(),
+                  reinterpret_cast<const long long*>(vout.data_ptr<int64_t>()), D, vbytes.data_ptr<uint8_t>(), stream);
+  if (mism.item<int>() != 0) return py::none();  // a 64-bit hash collision: let the host path decide
+  auto vb_h = vbytes.narrow(0, 0, VB).cpu();
+  auto vo_h = vout.cpu();
+  auto vl_h = vl64.cpu();
+  std::vector<std::string> vocab((size_t)D);
+  {
+    const char* b = reinterpret_cast<const char*>(vb_h.data_ptr<uint8_t>());
+    const int64_t* o = vo_h.data_ptr<int64_t>();
+    const int64_t* n = vl_h.data_ptr<int64_t>();
+    for (int64_t r = 0; r < D; ++r) vocab[(size_t)r].assign(b + o[r], (size_t)n[r]);
+  }
+  auto t2 = std::chrono::steady_clock::now();
+  py::dict stats;
+  stats["bytes"] = size;
+  stats["upload_s"] = std::chrono::duration<double>(t1 - t0).count();
+  stats["tokenize_s"] = std::chrono::duration<double>(t2 - t1).count();
+  stats["table_slots"] = cap;
+  py::object subo = sd ? py::cast(subc.narrow(0, 0, T)) : py::none();
+  py::object numo = want_nums ? py::cast(nums.narrow(0, 0, T)) : py::none();
+  return py::make_tuple(off, codes.narrow(0, 0, T), subo, numo, vocab, stats);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K27 LSTM recurrence.  Fragments are packed by avenir_amd/ops/rnn.py (pack_weights): wfrag holds
 // [NW, 4, KS+IS, 64, 8] bf16 (forward, [W_hh | W_ih]), wfragT [NW, 4KS, 64, 8] bf16 (backward,
@@ -2010,6 +2288,13 @@ PYBIND11_MODULE(_C, m) {
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, const std::string&, bool, int>(), py::arg("path"), py::arg("delim") = ",",
            py::arg("skip_header") = false, py::arg("nthreads") = 8)
+      .def(py::init([](std::vector<std::string> paths, int64_t rank, int64_t world, std::string delim, bool skip_header,
+                       int nthreads) {
+             py::gil_scoped_release rel;
+             return new avh::CsvFile(paths, rank, world, delim, skip_header, nthreads);
+           }),
+           py::arg("paths"), py::arg("rank"), py::arg("world"), py::arg("delim") = ",", py::arg("skip_header") = false,
+           py::arg("nthreads") = 8)
       .def("num_rows", &avh::CsvFile::num_rows)
       .def("max_fields", &avh::CsvFile::max_fields)
       .def("distinct", &avh::CsvFile::distinct)
@@ -2017,6 +2302,23 @@ PYBIND11_MODULE(_C, m) {
       .def("line", &avh::CsvFile::line)
       .def("lines", &avh::CsvFile::lines)
       .def("parse", &csv_parse, py::arg("specs"), py::arg("row_begin") = 0, py::arg("row_end") = -1);
+  py::class_<avh::TextShard>(m, "TextShard")
+      .def(py::init([](std::vector<std::string> paths, int64_t rank, int64_t world, int nthreads, bool skip_header) {
+             py::gil_scoped_release rel;
+             return new avh::TextShard(paths, rank, world, nthreads, skip_header);
+           }),
+           py::arg("paths"), py::arg("rank") = 0, py::arg("world") = 1, py::arg("nthreads") = 8,
+           py::arg("skip_header") = false)
+      .def("num_lines", &avh::TextShard::num_lines)
+      .def("bytes_read", &avh::TextShard::bytes_read)
+      .def("total_bytes", &avh::TextShard::total_bytes)
+      .def("lines", &avh::TextShard::lines)
+      .def("tokenize", &text_tokenize, py::arg("delims") = ",", py::arg("sub_delim") = "", py::arg("modes") = "",
+           py::arg("tail_mode") = "d", py::arg("trim") = false, py::arg("want_nums") = false)
+      .def("field_strings", &text_field_strings);
+  m.def("text_tokenize_device", &text_tokenize_device, py::arg("paths"), py::arg("rank"), py::arg("world"),
+        py::arg("delims") = ",", py::arg("sub_delim") = "", py::arg("modes") = "", py::arg("tail_mode") = "d",
+        py::arg("trim") = false, py::arg("want_nums") = false, py::arg("like"));
   m.def("format_rows", &format_rows);
   m.def("write_coded_csv", [](const std::string& path, const at::Tensor& codes, int64_t n,
                               std::vector<std::vector<std::string>> vocab, std::string id_prefix, std::string delim,

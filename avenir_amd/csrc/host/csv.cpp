@@ -145,8 +145,18 @@ CsvFile::CsvFile(const std::string& path, const std::string& delim, bool skip_he
   index_lines(skip_header);
 }
 
+CsvFile::CsvFile(const std::vector<std::string>& paths, int64_t rank, int64_t world, const std::string& delim,
+                 bool skip_header, int nthreads)
+    : delim_(delim.empty() ? std::string(",") : delim), nthreads_(std::max(1, nthreads)) {
+  ByteShard sh(paths, rank, world);
+  owned_.resize((size_t)(sh.bytes() + (int64_t)sh.segments().size()) + 16, 0);
+  size_ = (size_t)sh.copy_to(owned_.data(), true);
+  data_ = owned_.data();
+  index_lines(skip_header && rank == 0);
+}
+
 CsvFile::~CsvFile() {
-  if (data_) munmap(const_cast<char*>(data_), size_);
+  if (data_ && owned_.empty()) munmap(const_cast<char*>(data_), size_);
   if (fd_ >= 0) ::close(fd_);
 }
 

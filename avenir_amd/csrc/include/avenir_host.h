@@ -30,8 +30,40 @@ struct ColSpec {
   bool wide = false;               // CAT/BUCKET: uint16 codes (missing = 65535) for > 255 values
 };
 
+// Rank ``rank``'s byte range of the concatenated ``paths`` as memory-mapped segments of whole lines
+// (a line belongs to the range holding its first byte; one segment per file touched).  Only the
+// rank's own pages are mapped and faulted in (MAP_POPULATE over the segment).
+class ByteShard {
+ public:
+  struct Segment {
+    const char* p;
+    int64_t len;
+    void* map;
+    size_t map_len;
+  };
+  // populate: fault the pages in at map time (host tokenizer); the device upload faults them in
+  // from its parallel copy threads instead
+  ByteShard(const std::vector<std::string>& paths, int64_t rank, int64_t world, bool populate = true);
+  ~ByteShard();
+  ByteShard(const ByteShard&) = delete;
+  ByteShard& operator=(const ByteShard&) = delete;
+  const std::vector<Segment>& segments() const { return segs_; }
+  int64_t bytes() const { return bytes_; }
+  int64_t total_bytes() const { return total_bytes_; }
+  // concatenate the segments into dst (a '\n' after a segment lacking one when ``terminate``);
+  // dst needs bytes() + segments().size() bytes; returns the bytes written
+  int64_t copy_to(char* dst, bool terminate) const;
+
+ private:
+  std::vector<Segment> segs_;
+  int64_t bytes_ = 0, total_bytes_ = 0;
+};
+
 class CsvFile {
  public:
+  // byte-range shard of several files (records.cpp read_byte_shard): no bytes of other ranks are read
+  CsvFile(const std::vector<std::string>& paths, int64_t rank, int64_t world, const std::string& delim,
+          bool skip_header, int nthreads);
   // ``delim``: one character (fast path) or a multi-character literal separator (e.g. ",," of
   // the reference's REST record lists).
   CsvFile(const std::string& path, const std::string& delim, bool skip_header, int nthreads);
@@ -57,11 +89,54 @@ class CsvFile {
   const char* data_ = nullptr;
   size_t size_ = 0;
   int fd_ = -1;
+  std::vector<char> owned_;  // the byte-shard buffer (empty for a mapped file)
   std::string delim_;
   int nthreads_;
   int max_fields_ = 0;
   std::vector<int64_t> line_start_;
   std::vector<int64_t> line_end_;
+};
+
+// Tokenizer options of TextShard: ``delims`` — every listed character separates fields; per field
+// index a mode ('d' dictionary code, 'n' parsed double, 'x' nothing) from ``modes``, ``tail_mode``
+// beyond it; ``sub_delim`` (0 = none) splits a 'd' token once more into (code, sub code);
+// ``trim`` strips spaces / tabs around fields (the reference's String.split does not).
+struct TokenSpec {
+  std::string delims = ",";
+  char sub_delim = 0;
+  std::string modes;
+  char tail_mode = 'd';
+  bool trim = false;
+};
+
+// K1 for non-schema layouts (records.cpp): this rank's byte range of the concatenated input files
+// (a line belongs to the rank whose range holds its first byte), its non-blank lines, and a CSR
+// token table with a shard-wide first-occurrence dictionary.
+class TextShard {
+ public:
+  TextShard(const std::vector<std::string>& paths, int64_t rank, int64_t world, int nthreads, bool skip_header);
+  int64_t num_lines() const { return (int64_t)ls_.size(); }
+  int64_t bytes_read() const { return bytes_.bytes(); }
+  int64_t total_bytes() const { return bytes_.total_bytes(); }
+  const ByteShard& byte_shard() const { return bytes_; }
+  std::vector<std::string> lines(int64_t begin, int64_t end) const;
+  // pass 1: number of tokens under ``spec``; pass 2 fills off [L + 1], codes [T] (-1 for non-'d'
+  // fields) and, when non-null, sub [T] (-1 without a sub-delimiter) and nums [T] (NaN for non-'n').
+  int64_t count_tokens(const TokenSpec& spec);
+  void tokenize(int64_t* off, int32_t* codes, int32_t* sub, double* nums);
+  const std::vector<std::string>& vocab() const { return vocab_; }
+  // raw text of field ``field[i]`` of line ``line[i]`` (empty when the line is shorter)
+  std::vector<std::string> field_strings(const int64_t* line, const int32_t* field, int64_t n) const;
+
+ private:
+  void index_lines(bool skip_header);
+  ByteShard bytes_;
+  int nthreads_;
+  std::vector<const char*> ls_, le_;
+  TokenSpec spec_;
+  uint8_t sep_[256] = {0};
+  std::vector<int64_t> tok_lines_, tok_cnt_;
+  std::vector<std::string> vocab_;
 };
 
 // Format rows of numeric columns to CSV text quickly (multi-threaded).  prefix: optional per-row

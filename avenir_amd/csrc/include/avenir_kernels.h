@@ -186,6 +186,21 @@ void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long lo
                     const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
                     const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream);
 int csv_devspec_bytes();
+// K1 device tokenizer for non-schema record layouts (records.hip)
+void rec_lines(const uint8_t* bytes, const long long* nlpos, long long nraw, const char* delims, int ndelims,
+               long long* lstart, long long* lend, int* ntok, hipStream_t stream);
+void rec_tokens(const uint8_t* bytes, const long long* lstart, const long long* lend, const long long* off, long long L,
+                const char* delims, int ndelims, const char* modes, int nmodes, char tail_mode, char sub_delim,
+                bool trim, unsigned long long* keys, unsigned* h2tab, unsigned long long* first,
+                unsigned long long mask, int* tslot, unsigned* th2, int* tsub, unsigned* th2sub, double* nums,
+                unsigned* inserted, unsigned* overflow, hipStream_t stream);
+void rec_codes(const int* tslot, const unsigned* th2, long long T, const int* slot_code, const unsigned* h2tab,
+               int* codes, unsigned* mismatch, hipStream_t stream);
+void rec_vocab(const uint8_t* bytes, const long long* lstart, const long long* lend, const long long* off, long long L,
+               const unsigned long long* occ, long long D, const char* delims, int ndelims, char sub_delim, bool trim,
+               long long* vstart, int* vlen, hipStream_t stream);
+void rec_gather(const uint8_t* bytes, const long long* vstart, const int* vlen, const long long* vout, long long D,
+                uint8_t* out, hipStream_t stream);
 void forest_boot_count(const unsigned long long* keys, int ntrees, long long n, long long row_off, int mode,
                        unsigned rate32, int* tile_cnt, hipStream_t stream);
 void forest_boot_scatter(const uint8_t* codes, long long ld, int nfeat, const uint8_t* lab,

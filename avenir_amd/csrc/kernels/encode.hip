@@ -10,7 +10,11 @@
 //   fixed-shape reduction, so the result is bit-reproducible run to run (no float atomics).
 //   NaN entries are skipped (the reference's null handling).
 //
-// K23 leave-one-out target encoding (S/explore/CategoricalLeaveOneOutEncoding.scala:80-118):
+// K23 leave-one-out target encoding.  The kernel formula is a superset: with gmean = 0, amp = 1 and
+//   u = (z + 1) / 2 it is S/explore/CategoricalLeaveOneOutEncoding.scala:110-125
+//   ((posSum - y) / (count - 1 + reg) * (1 + z), z truncated Gaussian; models/explore.py
+//   leave_one_out_encoding(formula="reference")); gmean != 0 is the "smoothed" variant, not in the
+//   reference.
 //   loo_stats_kernel: per (column, code) target sum and count.  uint8 codes: a block privatises
 //     the 256-slot table in LDS (fp64 ds_add + u32 counters), then flushes the touched slots with
 //     global atomics; uint16 ("wide", > 255 values) codes go to global atomics directly.

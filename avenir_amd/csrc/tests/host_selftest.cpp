@@ -115,11 +115,60 @@ static void test_format_and_container(const std::string& dir) {
   std::remove(path.c_str());
 }
 
+// byte-range shards over two files: every line lands on exactly one rank whatever the world size,
+// the tokens of the union equal the world-1 tokens, and the dictionaries agree in merged order
+static void test_text_shards(const std::string& dir) {
+  const std::string p1 = dir + "/shard_a.txt", p2 = dir + "/shard_b.txt";
+  const char* st[] = {"L", "M", "H", "LL", "MMM"};
+  int nlines = 0;
+  {
+    std::ofstream a(p1), b(p2);
+    for (int i = 0; i < 20000; ++i) {
+      std::ofstream& f = i < 12000 ? a : b;
+      if (i % 501 == 0) { f << "   \n"; continue; }  // blank lines are dropped
+      f << "id" << i;
+      for (int k = 0; k < 1 + i % 7; ++k) f << "," << st[(i + k) % 5] << ":" << (k % 2 ? "x" : "y");
+      if (i != 19999) f << (i % 3 ? "\n" : "\r\n");  // the last line has no newline
+      ++nlines;
+    }
+  }
+  avh::TokenSpec spec;
+  spec.sub_delim = ':';
+  spec.modes = "x";
+  avh::TextShard whole({p1, p2}, 0, 1, 8, false);
+  CHECK(whole.num_lines() == nlines);
+  const int64_t T1 = whole.count_tokens(spec);
+  std::vector<int64_t> off1(whole.num_lines() + 1);
+  std::vector<int32_t> c1(T1), s1(T1);
+  whole.tokenize(off1.data(), c1.data(), s1.data(), nullptr);
+  for (int world : {2, 3, 8}) {
+    int64_t lines = 0, toks = 0;
+    for (int r = 0; r < world; ++r) {
+      avh::TextShard sh({p1, p2}, r, world, 3, false);
+      const int64_t T = sh.count_tokens(spec);
+      std::vector<int64_t> off(sh.num_lines() + 1);
+      std::vector<int32_t> c(T), s(T);
+      sh.tokenize(off.data(), c.data(), s.data(), nullptr);
+      for (int64_t k = 0; k < T; ++k) {
+        if (c[k] < 0) { CHECK(c1[toks + k] < 0); continue; }
+        CHECK(sh.vocab()[(size_t)c[k]] == whole.vocab()[(size_t)c1[toks + k]]);
+        CHECK(sh.vocab()[(size_t)s[k]] == whole.vocab()[(size_t)s1[toks + k]]);
+      }
+      lines += sh.num_lines();
+      toks += T;
+    }
+    CHECK(lines == nlines && toks == T1);
+  }
+  std::remove(p1.c_str());
+  std::remove(p2.c_str());
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
   test_csv(dir);
   test_ring();
   test_format_and_container(dir);
+  test_text_shards(dir);
   std::printf("OK\n");
   return 0;
 }

@@ -1,0 +1,279 @@
+"""Record tables for the reference's non-schema text layouts.
+
+The reference's sequence, transaction, tagged-token, pair-distance and event jobs split every line
+with ``String.split`` and look the tokens up in HashMaps inside their mappers (state sequences
+J/markov/MarkovStateTransitionModel.java:116-133, transactions
+J/association/FrequentItemsApriori.java:133-196, ``obs:state`` tokens
+J/markov/HiddenMarkovModelBuilder.java:136-260, pair-distance rows
+J/explore/TopMatchesByClass.java:133-211 and J/knn/NearestNeighbor.java:130-183, time-stamped
+events S/markov/StateTransitionRate.scala:91-167).
+
+Here :func:`read_records` turns a rank's byte range of the input (a file, a Hadoop-style directory
+of part files, or a comma list of those) into a :class:`Records` CSR table in ONE native pass:
+
+* every rank reads only its own byte range (a line belongs to the rank whose range holds its first
+  byte, as Hadoop's input splits); blank lines are dropped, a trailing CR is removed;
+* every field is a token: a dictionary code (first-occurrence order), a parsed double, or nothing,
+  by a per-field mode string (``'d'`` / ``'n'`` / ``'x'``, ``tail_mode`` beyond it); a
+  sub-delimiter splits each dictionary token once more (``obs:state`` -> code, sub code);
+* on a GPU the bytes are uploaded once and tokenized by the K1 device kernels
+  (``csrc/kernels/records.hip``); on the host by the multi-threaded ``TextShard``
+  (``csrc/host/records.cpp``).  Both give identical tables;
+* with several ranks the dictionaries are merged once (all-gather of the vocabularies, rank order:
+  the merged order is the global first-occurrence order, so codes do not depend on the world
+  size) and the local codes remapped on the device.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Sequence
+
+import torch
+
+from .. import _native
+
+#: bytes of a shard below which a GPU job tokenizes on the host and copies the table over
+DEVICE_MIN_BYTES = int(os.environ.get("AVMI_GPU_RECORDS_MIN_BYTES", str(4 << 20)))
+
+
+def input_paths(path: str | Path | Sequence) -> list[str]:
+    """The files behind an input: a file, a directory of part files (sorted, hidden and ``_``
+    files skipped) or a comma-separated list of those (``FileInputFormat.addInputPaths``)."""
+    items = [path] if isinstance(path, (str, Path)) else list(path)
+    out: list[str] = []
+    for it in items:
+        parts = [str(it)] if Path(str(it)).exists() else str(it).split(",")
+        for one in parts:
+            p = Path(one)
+            if p.is_dir():
+                out += [str(f) for f in sorted(p.iterdir()) if f.is_file() and not f.name.startswith((".", "_"))]
+            else:
+                out.append(str(p))
+    return out
+
+
+def _threads() -> int:
+    return max(1, min(16, os.cpu_count() or 8))
+
+
+@dataclass
+class Records:
+    """CSR token table of one rank's lines.
+
+    ``off`` int64 [L+1] token offsets per line; ``codes`` int32 [T] dictionary codes (-1 for
+    non-dictionary fields); ``sub`` int32 [T] sub-delimiter codes (-1 when absent) or None;
+    ``nums`` float64 [T] (NaN for non-numeric fields) or None; ``vocab`` the dictionary strings;
+    ``line_base`` the global index of this rank's first line."""
+    off: torch.Tensor
+    codes: torch.Tensor
+    sub: torch.Tensor | None
+    nums: torch.Tensor | None
+    vocab: list[str]
+    line_base: int = 0
+    stats: dict = field(default_factory=dict)
+    _shard: object = None
+
+    @property
+    def n_lines(self) -> int:
+        return self.off.numel() - 1
+
+    @property
+    def n_tokens(self) -> int:
+        return self.codes.numel()
+
+    @property
+    def device(self) -> torch.device:
+        return self.codes.device
+
+    def lens(self) -> torch.Tensor:
+        return self.off[1:] - self.off[:-1]
+
+    def width(self) -> int | None:
+        """The common number of fields of every line, or None when lines differ."""
+        if self.n_lines == 0:
+            return 0
+        ln = self.lens()
+        w = int(ln[0])
+        return w if bool((ln == w).all()) else None
+
+    def line_of_token(self) -> torch.Tensor:
+        """int64 [T]: the line index of every token."""
+        return torch.repeat_interleave(torch.arange(self.n_lines, device=self.device), self.lens())
+
+    def index(self, values: Sequence[str]) -> torch.Tensor:
+        """int32 [V]: dictionary code -> position in ``values`` (-1 when absent)."""
+        pos = {v: i for i, v in enumerate(values)}
+        return torch.tensor([pos.get(w, -1) for w in self.vocab] or [0], dtype=torch.int32, device=self.device)[
+            : len(self.vocab)]
+
+    def map_codes(self, codes: torch.Tensor, values: Sequence[str]) -> torch.Tensor:
+        """``codes`` (dictionary codes, -1 = none) translated to positions in ``values`` (-1)."""
+        lut = self.index(values)
+        if lut.numel() == 0:
+            return torch.full_like(codes, -1)
+        return torch.where(codes >= 0, lut[codes.clamp_min(0).long()], torch.full_like(codes, -1))
+
+    def field(self, j: int, numeric: bool = False) -> torch.Tensor:
+        """Codes (or values) of field ``j`` of every line; -1 (NaN) for lines with fewer fields.
+        Negative ``j`` counts from the end of each line."""
+        src = self.nums if numeric else self.codes
+        if src is None:
+            raise ValueError("no numeric tokens were parsed (read_records(numeric=...))")
+        lens = self.lens()
+        idx = (self.off[1:] + j) if j < 0 else (self.off[:-1] + j)
+        ok = (idx >= self.off[:-1]) & (idx < self.off[1:]) & (lens > 0)
+        fill = float("nan") if numeric else -1
+        if src.numel() == 0:
+            return torch.full((self.n_lines,), fill, dtype=src.dtype, device=self.device)
+        vals = src[idx.clamp(0, max(0, src.numel() - 1))]
+        return torch.where(ok, vals, torch.full_like(vals, fill))
+
+    def dense(self, width: int, numeric: bool = False) -> torch.Tensor:
+        """[L, width] view of the tokens of fixed-width lines."""
+        src = self.nums if numeric else self.codes
+        return src.view(self.n_lines, width)
+
+    def strings(self, codes: torch.Tensor | Sequence[int]) -> list[str]:
+        v = self.vocab
+        cs = codes.tolist() if isinstance(codes, torch.Tensor) else list(codes)
+        return [v[c] if c >= 0 else "" for c in cs]
+
+    def lines(self) -> list[str]:
+        """The raw text of this rank's lines (host shard only; re-read for device tables)."""
+        if self._shard is None:
+            raise RuntimeError("raw lines are only kept by host-tokenized tables")
+        return self._shard.lines(0, self.n_lines)
+
+    def to(self, device) -> "Records":
+        mv = lambda t: None if t is None else t.to(device)
+        return Records(mv(self.off), mv(self.codes), mv(self.sub), mv(self.nums), self.vocab, self.line_base,
+                       self.stats, self._shard)
+
+
+# ------------------------------------------------------------------------------------------------
+def read_records(path, *, comm=None, delims: str = ",", sub_delim: str = "", modes: str = "", tail_mode: str = "d",
+                 trim: bool = False, numeric: bool = False, device="cpu", skip_header: bool = False,
+                 shard: bool = True) -> Records:
+    """This rank's :class:`Records` of ``path`` (see the module docstring).  ``comm``: the job's
+    communicator (byte-range shard + dictionary merge when distributed); ``shard=False`` reads the
+    whole input on every rank (side files)."""
+    paths = input_paths(path)
+    dist = comm is not None and comm.is_distributed and shard
+    rank, world = (comm.rank, comm.world) if dist else (0, 1)
+    dev = torch.device(device)
+    C = _native.host()
+    rec = None
+    if C is not None:
+        if dev.type == "cuda" and hasattr(C, "text_tokenize_device") and not skip_header:
+            total = sum(os.path.getsize(p) for p in paths)
+            if total // world >= DEVICE_MIN_BYTES:
+                r = C.text_tokenize_device(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric,
+                                           torch.empty(0, device=dev))
+                if r is not None:
+                    off, codes, sub, nums, vocab, stats = r
+                    rec = Records(off, codes, sub, nums, list(vocab), stats=dict(stats, path="device"))
+        if rec is None:
+            sh = C.TextShard(paths, rank, world, _threads(), skip_header)
+            off, codes, sub, nums, vocab = sh.tokenize(delims, sub_delim, modes, tail_mode, trim, numeric)
+            rec = Records(off, codes, sub, nums, list(vocab), stats={"path": "host", "bytes": sh.bytes_read()},
+                          _shard=sh)
+            if dev.type != "cpu":
+                rec = rec.to(dev)
+    else:
+        rec = _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header)
+        rec = rec.to(dev) if dev.type != "cpu" else rec
+    if dist:
+        _merge_vocab(rec, comm)
+    return rec
+
+
+def _merge_vocab(rec: Records, comm) -> None:
+    """Global dictionary = the rank-ordered union of the shard dictionaries (= global first
+    occurrence); local codes are remapped on their device; ``line_base`` from the line counts."""
+    parts = comm.all_gather_object((rec.vocab, rec.n_lines))
+    glob: dict[str, int] = {}
+    for voc, _ in parts:
+        for w in voc:
+            if w not in glob:
+                glob[w] = len(glob)
+    rec.line_base = sum(n for _, n in parts[: comm.rank])
+    if rec.vocab:
+        lut = torch.tensor([glob[w] for w in rec.vocab], dtype=torch.int32, device=rec.device)
+        remap = lambda c: torch.where(c >= 0, lut[c.clamp_min(0).long()], c)
+        rec.codes = remap(rec.codes)
+        if rec.sub is not None:
+            rec.sub = remap(rec.sub)
+    rec.vocab = list(glob)
+
+
+def _py_lines(paths, rank: int, world: int, skip_header: bool) -> list[str]:
+    """Pure-Python twin of the native byte-range shard: non-blank lines whose first byte lies in
+    this rank's range of the concatenated files."""
+    total = sum(os.path.getsize(p) for p in paths)
+    lo, hi = total * rank // world, total * (rank + 1) // world
+    out: list[str] = []
+    base = 0
+    for p in paths:
+        raw = Path(p).read_bytes()
+        start = 0
+        while start < len(raw):
+            nl = raw.find(b"\n", start)
+            end = len(raw) if nl < 0 else nl
+            if lo <= base + start < hi:
+                ln = raw[start:end].decode()
+                ln = ln[:-1] if ln.endswith("\r") else ln
+                if ln.strip(" \t\r\v\f"):
+                    out.append(ln)
+            start = end + 1
+        base += len(raw)
+    if skip_header and rank == 0 and out:
+        out = out[1:]
+    return out
+
+
+def _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header) -> Records:
+    """Pure-Python twin of the native tokenizers (used when the extension is not built)."""
+    import math
+    import re
+    lines = _py_lines(paths, rank, world, skip_header)
+    sep = "[" + re.escape(delims or ",") + "]"
+    vocab: dict[str, int] = {}
+    off, codes, sub, nums = [0], [], [], []
+    for ln in lines:
+        fields = re.split(sep, ln)
+        for f, tok in enumerate(fields):
+            m = modes[f] if f < len(modes) else tail_mode
+            if trim:
+                tok = tok.strip(" \t\r\v\f")
+            c, s, v = -1, -1, math.nan
+            if m == "d":
+                a, b = (tok.split(sub_delim, 1) + [None])[:2] if sub_delim else (tok, None)
+                c = vocab.setdefault(a, len(vocab))
+                if b is not None:
+                    s = vocab.setdefault(b, len(vocab))
+            elif m == "n":
+                try:
+                    v = float(tok.strip(" \t\r\v\f"))
+                except ValueError:
+                    v = math.nan
+            codes.append(c)
+            sub.append(s)
+            nums.append(v)
+        off.append(len(codes))
+    return Records(torch.tensor(off, dtype=torch.int64), torch.tensor(codes, dtype=torch.int32),
+                   torch.tensor(sub, dtype=torch.int32) if sub_delim else None,
+                   torch.tensor(nums, dtype=torch.float64) if numeric else None, list(vocab), stats={"path": "python"})
+
+
+def shard_lines(path, comm=None, shard: bool = True, skip_header: bool = False) -> list[str]:
+    """This rank's non-blank lines of ``path`` (byte-range shard; all lines with ``shard=False``)."""
+    paths = input_paths(path)
+    dist = comm is not None and comm.is_distributed and shard
+    rank, world = (comm.rank, comm.world) if dist else (0, 1)
+    C = _native.host()
+    if C is not None:
+        sh = C.TextShard(paths, rank, world, _threads(), skip_header)
+        return sh.lines(0, sh.num_lines())
+    return _py_lines(paths, rank, world, skip_header)

@@ -257,12 +257,19 @@ class LazyColumn(Sequence):
         return list(self._get()) == list(other)
 
 
-@traced("data.load_csv", nbytes=lambda path, *a, **k: os.path.getsize(path))
-def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
+def _nbytes(path) -> int:
+    return sum(os.path.getsize(p) for p in path) if isinstance(path, (list, tuple)) else os.path.getsize(path)
+
+
+@traced("data.load_csv", nbytes=lambda path, *a, **k: _nbytes(path))
+def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *, rank: int = 0,
              world: int = 1, device: str | torch.device = "cpu", keep_lines: bool = False,
              skip_header: bool = False, nthreads: int | None = None, feature_ordinals: Sequence[int] | None = None,
              class_ordinal: int | None = None, raw_numeric: bool = False) -> Table:
     """Parse ``path`` into a ``Table`` (this rank's shard) with the native K1 parser.
+
+    ``path`` may be a list of files (a Hadoop part-file directory): they are read as one byte
+    stream by the native parser, without a temporary concatenated copy.
 
     ``raw_numeric``: keep int/double features as raw float columns even when the schema gives a
     ``bucketWidth`` (the tree builders bin them by their own split points)."""
@@ -281,19 +288,26 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         feats.sort(key=lambda f: f.ordinal)
     cls_f = (schema.find_field_by_ordinal(class_ordinal) if class_ordinal is not None
              else schema.find_class_attr_field())
+    multi = isinstance(path, (list, tuple))
+    if multi and len(path) == 1:
+        path, multi = path[0], False
     C = _native.host()
     use_native = C is not None and not _is_regex(delim)
     if nthreads is None:    # parse threads: the machine's cores, capped at a GPU box's CPU share
         nthreads = max(1, min(16, os.cpu_count() or 8))
     dev = torch.device(device)
-    if (use_native and dev.type == "cuda" and not keep_lines and len(_literal(delim or ",")) == 1
+    if (use_native and not multi and dev.type == "cuda" and not keep_lines and len(_literal(delim or ",")) == 1
             and hasattr(C, "csv_parse_device") and os.path.getsize(path) >= _GPU_CSV_MIN_BYTES
             and all(f.cardinality or not f.is_categorical for f in feats)
             and (cls_f is None or cls_f.cardinality)):
         t = _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads)
         if t is not None:
             return t
-    csv = C.CsvFile(str(path), _literal(delim or ","), skip_header, nthreads) if use_native else None
+    if use_native:
+        csv = (C.CsvFile([str(p) for p in path], 0, 1, _literal(delim or ","), skip_header, nthreads) if multi
+               else C.CsvFile(str(path), _literal(delim or ","), skip_header, nthreads))
+    else:
+        csv = None
     # categorical fields without a schema cardinality: dictionary in first-seen order over the
     # WHOLE file (identical on every rank), any size (uint16 codes above 255 values)
     for f in feats:
@@ -301,7 +315,7 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
             if csv is not None:
                 f.cardinality = csv.distinct(f.ordinal, 65535)
             else:
-                f.cardinality = _distinct_py(path, f.ordinal, delim, skip_header)
+                f.cardinality = _distinct_py(_py_lines_of(path, skip_header), f.ordinal, delim)
     binned = [f for f in feats if f.is_binned]
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
     wide = needs_wide(binned)
@@ -333,10 +347,7 @@ def load_csv(path: str | Path, schema: FeatureSchema, delim: str = ",", *, rank:
         if keep_lines:
             lines = csv.lines(r0, r1)
     else:  # pure-Python path: regex delimiters, or no native module
-        with open(path) as fh:
-            all_lines = [ln.rstrip("\r\n") for ln in fh if ln.strip()]
-        if skip_header:
-            all_lines = all_lines[1:]
+        all_lines = _py_lines_of(path, skip_header)
         r0, r1 = shard_range(len(all_lines), rank, world)
         splitter = split_regex(delim or ",")
         rows = [splitter(ln) for ln in all_lines[r0:r1]]
@@ -401,16 +412,22 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     return Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, None, r0)
 
 
-def _distinct_py(path, ordinal: int, delim: str, skip_header: bool) -> list[str]:
+def _py_lines_of(path, skip_header: bool) -> list[str]:
+    """Non-blank lines of one file or a list of files (pure-Python path)."""
+    out: list[str] = []
+    for p in (path if isinstance(path, (list, tuple)) else [path]):
+        with open(p) as fh:
+            out += [ln.rstrip("\r\n") for ln in fh if ln.strip()]
+    return out[1:] if skip_header else out
+
+
+def _distinct_py(lines: list[str], ordinal: int, delim: str) -> list[str]:
     split = split_regex(delim or ",")
     seen: dict[str, None] = {}
-    with open(path) as fh:
-        for i, ln in enumerate(fh):
-            if (skip_header and i == 0) or not ln.strip():
-                continue
-            r = split(ln.rstrip("\r\n"))
-            if ordinal < len(r):
-                seen.setdefault(r[ordinal].strip(), None)
+    for ln in lines:
+        r = split(ln)
+        if ordinal < len(r):
+            seen.setdefault(r[ordinal].strip(), None)
     return list(seen)
 
 

@@ -128,38 +128,48 @@ class JobContext:
 
     # -- input --------------------------------------------------------------------------------
     def all_lines(self, path: str | None = None) -> list[str]:
-        return read_lines(path or self.args.input)
+        """Every non-blank line of ``path`` (side files read whole by every rank)."""
+        from ..data.records import shard_lines
+        return shard_lines(path or self.args.input, None, shard=False)
 
     def lines(self, path: str | None = None, shard: bool = True) -> list[str]:
-        """This rank's contiguous block of the input lines (all lines when not distributed)."""
-        ls = self.all_lines(path)
-        if not shard or not self.comm.is_distributed:
-            return ls
-        from ..data.table import shard_range
-        a, b = shard_range(len(ls), self.comm.rank, self.comm.world)
-        return ls[a:b]
+        """This rank's lines: the native byte-range shard of the input (a rank reads only the bytes of
+        its range; a line belongs to the rank whose range holds its first byte).  All lines when
+        ``shard=False`` or not distributed."""
+        from ..data.records import shard_lines
+        return shard_lines(path or self.args.input, self.comm, shard=shard)
 
     def rows(self, path: str | None = None, shard: bool = True, keep_empty: bool = True) -> list[list[str]]:
         sp = self.split
         return [sp(l) for l in self.lines(path, shard)]
+
+    def records(self, path: str | None = None, shard: bool = True, **kw):
+        """This rank's CSR token table of the input (data/records.py): one native pass (device
+        tokenizer on a GPU), dictionary merged over ranks.  ``kw``: modes / tail_mode / sub_delim /
+        numeric / trim / delims (default: the job's literal field delimiter)."""
+        from ..data.records import read_records
+        from ..data.table import _literal
+        if "delims" not in kw:
+            lit = _literal(self.delim_in)
+            if lit is None or len(lit) != 1:
+                raise SystemExit(f"native record input needs a one-character field delimiter, got {self.delim_in!r}")
+            kw["delims"] = lit
+        return read_records(path or self.args.input, comm=self.comm, device=self.device, shard=shard, **kw)
+
+    def line_base(self, n_local: int) -> int:
+        """Global index of this rank's first line (exclusive scan of the line counts)."""
+        if not self.comm.is_distributed:
+            return 0
+        counts = self.comm.all_gather_object(int(n_local))
+        return int(sum(counts[: self.comm.rank]))
 
     def table(self, raw_numeric: bool = False, path: str | None = None, schema=None, shard: bool = True):
         from ..data.table import load_csv
         comm = self.comm
         path = str(path or self.args.input)
         files = input_files(path)
-        if len(files) != 1:
-            # a Hadoop-style directory of part files (or a comma list): one concatenated file
-            import tempfile
-            tmp = tempfile.NamedTemporaryFile("w", suffix=".csv", delete=False)
-            for f in files:
-                txt = f.read_text()
-                tmp.write(txt if txt.endswith("\n") or not txt else txt + "\n")
-            tmp.close()
-            path = tmp.name
-        else:
-            path = str(files[0])
-        return load_csv(path, schema or self.schema(), self.delim_in,
+        src = [str(f) for f in files] if len(files) != 1 else str(files[0])
+        return load_csv(src, schema or self.schema(), self.delim_in,
                         rank=comm.rank if shard else 0, world=comm.world if shard else 1,
                         device=self.device, keep_lines=True, raw_numeric=raw_numeric)
 

@@ -335,10 +335,21 @@ def apply_encoding(t: Table, enc: dict[int, dict[str, float]], default: float = 
 
 
 def leave_one_out_encoding(t: Table, target: torch.Tensor, noise: float = 0.0, reg: float = 0.0,
-                           seed: int = 0, comm: Comm | None = None) -> torch.Tensor:
-    """Leave-one-out target mean per categorical value (S/explore/CategoricalLeaveOneOutEncoding):
-    (sum_v - y_i + reg * global_mean) / (count_v - 1 + reg), optional multiplicative noise."""
+                           seed: int = 0, comm: Comm | None = None, formula: str = "reference") -> torch.Tensor:
+    """Leave-one-out target encoding per categorical value, on the K23 kernels.
+
+    ``formula="reference"`` (default) is S/explore/CategoricalLeaveOneOutEncoding.scala:110-125:
+    ``(sum_v - y_i) / (count_v - 1 + reg) * (1 + z)`` with ``z ~ N(0, noise)`` truncated at 3 sd
+    (the ``categoricalLeaveOneOutEncoding`` job uses the same function).
+    ``formula="smoothed"`` is a deliberate variant that is NOT in the reference: the prior
+    ``reg * global_mean`` is added to the numerator (shrinkage towards the global mean) and the
+    noise is uniform ``1 + noise * (2u - 1)``.
+
+    The kernel computes ``(s - y + reg * g) / (k - 1 + reg) * (1 + amp * (2u - 1))``; the
+    reference formula is the case ``g = 0``, ``amp = 1``, ``u = (z + 1) / 2``."""
     from ..ops import encode_ops as E
+    if formula not in ("reference", "smoothed"):
+        raise ValueError(f"formula must be 'reference' or 'smoothed', got {formula!r}")
     n = t.n
     y = target[:n].double().to(t.codes.device)
     g = torch.Generator(device="cpu")
@@ -349,9 +360,19 @@ def leave_one_out_encoding(t: Table, target: torch.Tensor, noise: float = 0.0, r
     codes = t.codes[:nf]
     s, k = E.loo_stats(codes, n, y)  # K23: per (column, value) target sums and counts
     _reduce(comm, gsum, gcnt, s, k)
-    # one uniform stream per column, drawn in column order from the seeded host generator
-    u = torch.stack([torch.rand(n, generator=g) for _ in range(nf)]).double() if noise > 0 else None
-    return E.loo_apply(codes, n, y, s, k, gsum / gcnt, reg=reg, noise=u, amp=float(noise))
+    u = None
+    if noise > 0:
+        # one stream per column, drawn in column order from the seeded host generator
+        if formula == "reference":
+            z = torch.stack([(torch.randn(n, generator=g, dtype=torch.float64) * noise).clamp(-3 * noise, 3 * noise)
+                             for _ in range(nf)])
+            u, amp = (z + 1.0) / 2.0, 1.0
+        else:
+            u, amp = torch.stack([torch.rand(n, generator=g) for _ in range(nf)]).double(), float(noise)
+    else:
+        amp = 0.0
+    gmean = torch.zeros(1, dtype=torch.float64, device=y.device) if formula == "reference" else gsum / gcnt
+    return E.loo_apply(codes, n, y, s, k, gmean, reg=reg, noise=u, amp=amp)
 
 
 def _hash_slot(j: int, v: str, size: int, signed: bool) -> tuple[int, float]:

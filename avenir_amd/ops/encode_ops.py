@@ -24,7 +24,7 @@ def column_moments(X: torch.Tensor, n: int | None = None) -> torch.Tensor:
     sums divided by the count."""
     X2 = X.view(1, -1) if X.dim() == 1 else X
     n = X2.shape[1] if n is None else int(n)
-    if X2.is_cuda:
+    if X2.is_cuda and n > 0:
         if X2.dtype not in (torch.float32, torch.float64):
             X2 = X2.double()
         if X2.dtype == torch.float32 and (X2.shape[1] % 4 or X2.data_ptr() % 16 or not X2.is_contiguous()):

@@ -132,12 +132,14 @@ def main() -> int:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
               file=sys.stderr)
 
+    import avenir_amd
     from avenir_amd.data.synth import CHURN_SCHEMA, churn_device
     from avenir_amd.data.table import Table
     from avenir_amd.models.bayes import NaiveBayes
     from avenir_amd.parallel.comm import get_comm
     from avenir_amd.utils.schema import FeatureSchema
 
+    avenir_amd.freeze_startup_objects()
     comm = get_comm()
     dev = comm.device
     if dev.type != "cuda":

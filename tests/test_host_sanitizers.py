@@ -1,6 +1,6 @@
 """Native host runtime under sanitizers.
 
-The CSV encoder, SPSC ring, row formatter and checkpoint container are compiled together with a
+The CSV encoder, byte-range text shards + tokenizer, SPSC ring, row formatter and checkpoint container are compiled together with a
 C++ self-test (avenir_amd/csrc/tests/host_selftest.cpp) twice: with AddressSanitizer +
 UndefinedBehaviorSanitizer and with ThreadSanitizer (the ring is exercised by a producer and a
 consumer thread, the CSV parser and formatter by 8 worker threads).  GPU-side sanitizers are not
@@ -15,7 +15,7 @@ import pytest
 
 ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "avenir_amd", "csrc")
 SOURCES = [os.path.join(ROOT, "tests", "host_selftest.cpp"), os.path.join(ROOT, "host", "csv.cpp"),
-           os.path.join(ROOT, "host", "ring_ckpt.cpp")]
+           os.path.join(ROOT, "host", "ring_ckpt.cpp"), os.path.join(ROOT, "host", "records.cpp")]
 
 
 def _build_and_run(tmp_path, flags: list[str], env_extra: dict[str, str]) -> None:
