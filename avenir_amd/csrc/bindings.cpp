@@ -1932,8 +1932,10 @@ std::vector<std::string> text_field_strings(const avh::TextShard& sh, const at::
 // caller then uses the host tokenizer).
 py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, int64_t world,
                                 const std::string& delims_in, const std::string& sub_delim, const std::string& modes,
-                                const std::string& tail_mode, bool trim, bool want_nums, const at::Tensor& like) {
+                                const std::string& tail_mode, bool trim, bool want_nums, const at::Tensor& like,
+                                int64_t max_initial_slots) {
   CHECK_DEV(like);
+  TORCH_CHECK(max_initial_slots >= 1024, "max_initial_slots >= 1024");
   TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && modes.size() <= 64, "bad tokenizer options");
   for (char c : modes + tail_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
   const std::string delims = delims_in.empty() ? std::string(",") : delims_in;
@@ -2042,7 +2044,7 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
     return c;
   };
   const int64_t tdict = T * (sd ? 2 : 1);
-  int64_t cap = std::min<int64_t>(cap_for(tdict), 1LL << 24);
+  int64_t cap = std::min<int64_t>(cap_for(tdict), max_initial_slots);
   auto tslot = at::empty({std::max<int64_t>(1, T)}, iopt);
   auto th2 = at::empty({std::max<int64_t>(1, T)}, iopt);
   at::Tensor tsub, th2s, nums;
@@ -2131,6 +2133,59 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
   py::object subo = sd ? py::cast(subc.narrow(0, 0, T)) : py::none();
   py::object numo = want_nums ? py::cast(nums.narrow(0, 0, T)) : py::none();
   return py::make_tuple(off, codes.narrow(0, 0, T), subo, numo, vocab, stats);
+}
+
+// format_columns(cols, n, delim, nthreads) -> bytes.  cols: ("s", list[str], idx int32) |
+// ("f", float64, prec) | ("i", int64) | ("c", literal) | ("g", literal glued without a delimiter) |
+// ("l", list[str], idx int32, off int64 [n+1]).
+py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& delim, int nthreads) {
+  std::vector<avh::FmtCol> cols;
+  std::vector<std::unique_ptr<std::vector<std::string>>> tables;
+  std::vector<at::Tensor> keep;
+  for (auto item : cols_py) {
+    auto t = item.cast<py::tuple>();
+    const std::string kind = t[0].cast<std::string>();
+    avh::FmtCol c;
+    auto cpu_tensor = [&](py::handle h, at::ScalarType st, int64_t len, const char* what) {
+      auto x = h.cast<at::Tensor>().to(at::kCPU).to(st).contiguous();
+      TORCH_CHECK(x.numel() >= len, "format_columns: ", what, " column shorter than required");
+      keep.push_back(x);
+      return x;
+    };
+    if (kind == "s" || kind == "l") {
+      tables.push_back(std::make_unique<std::vector<std::string>>(t[1].cast<std::vector<std::string>>()));
+      c.table = tables.back().get();
+      if (kind == "s") {
+        c.kind = avh::FmtCol::STR;
+        c.idx = cpu_tensor(t[2], at::kInt, n, "string").data_ptr<int32_t>();
+      } else {
+        c.kind = avh::FmtCol::LIST;
+        auto off = cpu_tensor(t[3], at::kLong, n + 1, "list offsets");
+        const int64_t m = n ? off.data_ptr<int64_t>()[n] : 0;
+        c.idx = cpu_tensor(t[2], at::kInt, m, "list").data_ptr<int32_t>();
+        c.off = off.data_ptr<int64_t>();
+      }
+    } else if (kind == "f") {
+      c.kind = avh::FmtCol::F64;
+      c.dv = cpu_tensor(t[1], at::kDouble, n, "float").data_ptr<double>();
+      c.prec = t.size() > 2 ? t[2].cast<int>() : 6;
+    } else if (kind == "i") {
+      c.kind = avh::FmtCol::I64;
+      c.iv = cpu_tensor(t[1], at::kLong, n, "int").data_ptr<int64_t>();
+    } else if (kind == "c" || kind == "g") {
+      c.kind = kind == "c" ? avh::FmtCol::LIT : avh::FmtCol::GLUE;
+      c.lit = t[1].cast<std::string>();
+    } else {
+      TORCH_CHECK(false, "format_columns: unknown column kind ", kind);
+    }
+    cols.push_back(std::move(c));
+  }
+  std::string out;
+  {
+    py::gil_scoped_release rel;
+    out = avh::format_columns(cols, n, delim, nthreads);
+  }
+  return py::bytes(out);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2318,7 +2373,10 @@ PYBIND11_MODULE(_C, m) {
       .def("field_strings", &text_field_strings);
   m.def("text_tokenize_device", &text_tokenize_device, py::arg("paths"), py::arg("rank"), py::arg("world"),
         py::arg("delims") = ",", py::arg("sub_delim") = "", py::arg("modes") = "", py::arg("tail_mode") = "d",
-        py::arg("trim") = false, py::arg("want_nums") = false, py::arg("like"));
+        py::arg("trim") = false, py::arg("want_nums") = false, py::arg("like"),
+        py::arg("max_initial_slots") = 1LL << 24);
+  m.def("format_columns", &format_columns_py, py::arg("cols"), py::arg("n"), py::arg("delim") = ",",
+        py::arg("nthreads") = 8);
   m.def("format_rows", &format_rows);
   m.def("write_coded_csv", [](const std::string& path, const at::Tensor& codes, int64_t n,
                               std::vector<std::vector<std::string>> vocab, std::string id_prefix, std::string delim,

@@ -144,6 +144,23 @@ class TextShard {
 std::string format_rows(const std::vector<std::string>* prefix, const double* cols, int ncol,
                         int64_t n, const std::vector<int>& precision, char delim, int nthreads);
 
+// One output column of format_columns: STR = table[idx[r]], F64 = dv[r] ("%.*f", prec < 0: "%g"),
+// I64 = iv[r], LIT = a constant, LIST = table[idx[j]] for j in [off[r], off[r+1]) (delimited, nothing
+// when empty), GLUE = a constant appended with no delimiter (brackets).  An index outside the table
+// writes an empty field.
+struct FmtCol {
+  enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5 };
+  int kind = STR;
+  const std::vector<std::string>* table = nullptr;
+  const int32_t* idx = nullptr;
+  const double* dv = nullptr;
+  int prec = 6;
+  const int64_t* iv = nullptr;
+  const int64_t* off = nullptr;
+  std::string lit;
+};
+std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads);
+
 // Lock-free SPSC ring of fixed-size int64 records.
 class SpscRing {
  public:

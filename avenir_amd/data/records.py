@@ -135,6 +135,41 @@ class Records:
         src = self.nums if numeric else self.codes
         return src.view(self.n_lines, width)
 
+    def padded(self, codes: torch.Tensor | None = None, start: int = 0, drop: Sequence[int] = (), fill: int = -1,
+               min_len: int = 0, dtype=torch.int16) -> tuple[torch.Tensor, torch.Tensor]:
+        """Per-line token rows as a padded ``[L, W]`` matrix: the tokens at field positions
+        ``>= start`` except ``drop`` (e.g. a class field inside a sequence), left-aligned, ``fill``
+        beyond each line's end.  ``codes`` defaults to the dictionary codes (any per-token int
+        tensor, e.g. mapped states).  Returns (matrix, kept-token count per line).  Fixed-width
+        tables are a strided column selection; ragged ones one scatter."""
+        src = self.codes if codes is None else codes
+        L = self.n_lines
+        w = self.width()
+        dropset = {d for d in drop if d >= start}
+        if w is not None:
+            cols = [j for j in range(start, w) if j not in dropset]
+            cnt = torch.full((L,), len(cols), dtype=torch.int64, device=self.device)
+            if not cols or L == 0:
+                return torch.full((L, max(min_len, len(cols))), fill, dtype=dtype, device=self.device), cnt
+            M = src.view(L, w)[:, torch.tensor(cols, device=self.device)]
+            if len(cols) < min_len:
+                M = torch.cat([M, torch.full((L, min_len - len(cols)), fill, dtype=M.dtype, device=self.device)], 1)
+            return M.to(dtype), cnt
+        tl = self.line_of_token()
+        pos = torch.arange(self.n_tokens, device=self.device) - self.off[:-1][tl]
+        keep = pos >= start
+        for d in dropset:
+            keep &= pos != d
+        cs = torch.cumsum(keep.long(), 0)
+        before = torch.cat([torch.zeros(1, dtype=torch.long, device=self.device), cs])[self.off[:-1]]
+        cnt = torch.cat([torch.zeros(1, dtype=torch.long, device=self.device), cs])[self.off[1:]] - before
+        W = max(min_len, int(cnt.max()) if L else 0)
+        M = torch.full((L, W), fill, dtype=dtype, device=self.device)
+        if W and bool(keep.any()):
+            newpos = cs - 1 - before[tl]
+            M[tl[keep], newpos[keep]] = src[keep].to(dtype)
+        return M, cnt
+
     def strings(self, codes: torch.Tensor | Sequence[int]) -> list[str]:
         v = self.vocab
         cs = codes.tolist() if isinstance(codes, torch.Tensor) else list(codes)
@@ -277,3 +312,123 @@ def shard_lines(path, comm=None, shard: bool = True, skip_header: bool = False) 
         sh = C.TextShard(paths, rank, world, _threads(), skip_header)
         return sh.lines(0, sh.num_lines())
     return _py_lines(paths, rank, world, skip_header)
+
+
+def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
+    """Output text of ``n`` rows assembled column by column (native, multi-threaded):
+    ``("s", table, idx)`` string-table lookups, ``("f", values, prec)`` numbers (prec < 0: ``%g``),
+    ``("i", ints)``, ``("c", literal)``, ``("g", literal)`` glued on without a delimiter,
+    ``("l", table, idx, off)`` a variable-length list of table strings per row (CSR).  Every row
+    ends with a newline."""
+    C = _native.host()
+    if C is not None:
+        return C.format_columns(cols, int(n), delim, _threads())
+    rows = [[] for _ in range(n)]
+    glue_pre = [""] * n
+    for c in cols:
+        k = c[0]
+        if k == "g":
+            for r in range(n):
+                if rows[r]:
+                    rows[r][-1] += c[1]
+                else:
+                    glue_pre[r] += c[1]
+            continue
+        if k == "s":
+            tab, idx = c[1], c[2].tolist()
+            for r in range(n):
+                rows[r].append(tab[idx[r]] if 0 <= idx[r] < len(tab) else "")
+        elif k == "f":
+            vals, prec = c[1].tolist(), (c[2] if len(c) > 2 else 6)
+            for r in range(n):
+                v = vals[r]
+                rows[r].append("NaN" if v != v else (f"{v:.{prec}f}" if prec >= 0 else f"{v:g}"))
+        elif k == "i":
+            vals = c[1].tolist()
+            for r in range(n):
+                rows[r].append(str(int(vals[r])))
+        elif k == "c":
+            for r in range(n):
+                rows[r].append(c[1])
+        elif k == "l":
+            tab, idx, off = c[1], c[2].tolist(), c[3].tolist()
+            for r in range(n):
+                rows[r] += [tab[i] if 0 <= i < len(tab) else "" for i in idx[off[r]:off[r + 1]]]
+        else:
+            raise ValueError(f"unknown column kind {k!r}")
+    out = []
+    for r in range(n):
+        if rows[r]:
+            rows[r][0] = glue_pre[r] + rows[r][0]
+            out.append(delim.join(rows[r]) + "\n")
+        else:
+            out.append(glue_pre[r] + "\n")
+    return "".join(out).encode()
+
+
+# ------------------------------------------------------------------------------------------------
+# keyed (reduce-side) helpers: the MapReduce shuffle as one all-to-all
+def sorted_keys(rec: Records, codes: torch.Tensor, comm=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """The distinct dictionary codes of ``codes`` over all ranks, ordered by their strings (the
+    reducer key order of the reference), and a [V] lookup code -> position in that order (-1).
+    Presence is one all-reduce of a [V] byte mask; the string sort runs once on the host."""
+    import numpy as np
+    V = len(rec.vocab)
+    dev = codes.device
+    present = torch.zeros(max(1, V), dtype=torch.uint8, device=dev)
+    c = codes[codes >= 0].long()
+    if c.numel():
+        present[c] = 1
+    if comm is not None and comm.is_distributed:
+        comm.all_reduce(present, "max")
+    idx = torch.nonzero(present[:V]).view(-1).cpu()
+    if idx.numel():
+        order = np.argsort(np.array([rec.vocab[i] for i in idx.tolist()]), kind="stable")
+        keys = idx[torch.from_numpy(order.astype(np.int64))]
+    else:
+        keys = idx
+    pos = torch.full((max(1, V),), -1, dtype=torch.int64)
+    pos[keys] = torch.arange(keys.numel())
+    return keys.to(dev), pos[:V].to(dev)
+
+
+def owner_of(pos: torch.Tensor, n_keys: int, world: int) -> torch.Tensor:
+    """Rank owning sorted key position ``pos`` when the keys are cut into contiguous balanced
+    blocks (data/table.shard_range): the rank-ordered concatenation of the owners' outputs is the
+    global key order, so outputs do not depend on the world size."""
+    base, rem = divmod(n_keys, world)
+    starts = torch.tensor([r * base + min(r, rem) for r in range(world)], dtype=torch.int64, device=pos.device)
+    return (torch.searchsorted(starts, pos.long(), right=True) - 1).clamp_min(0)
+
+
+def shuffle(comm, owner: torch.Tensor, cols: list[torch.Tensor]) -> list[torch.Tensor]:
+    """Send every row (``cols`` share dim 0) to rank ``owner[row]`` with one all-to-all; the
+    received rows come in source-rank order, each source's rows in their original order, so a
+    stable sort downstream sees the global input order.  float64 columns travel bit-exact."""
+    if comm is None or not comm.is_distributed:
+        return cols
+    kinds = [c.dtype for c in cols]
+    packed = torch.stack([c.view(torch.int64) if c.dtype == torch.float64 else c.long() for c in cols], 1) \
+        if cols else torch.zeros((owner.numel(), 0), dtype=torch.int64, device=owner.device)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=comm.world).tolist()
+    chunks = list(torch.split(packed[order], counts))
+    recv = torch.cat(comm.all_to_all_v(chunks), 0)
+    out = []
+    for j, dt in enumerate(kinds):
+        col = recv[:, j].contiguous()
+        out.append(col.view(torch.float64) if dt == torch.float64 else col.to(dt))
+    return out
+
+
+def numeric_lut(vocab: list[str], device) -> torch.Tensor:
+    """float64 [V]: the number each dictionary string parses to (NaN otherwise) — numeric fields
+    tokenized as dictionary entries (ranks, small integer fields)."""
+    import numpy as np
+    out = np.full(max(1, len(vocab)), np.nan)
+    for i, v in enumerate(vocab):
+        try:
+            out[i] = float(v)
+        except ValueError:
+            pass
+    return torch.from_numpy(out[: len(vocab)]).to(device)

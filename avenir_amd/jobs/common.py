@@ -227,6 +227,35 @@ class JobContext:
             return p
         return None
 
+    def emit_text(self, text: bytes, out: str | None = None) -> Path | None:
+        """Map-side output of pre-formatted text (data/records.format_lines): this rank's part file
+        into a directory, or the rank-ordered concatenation written by rank 0."""
+        p, is_dir = self._target(out)
+        if is_dir:
+            p.mkdir(parents=True, exist_ok=True)
+            t = p / f"part-{self.comm.rank:05d}"
+            t.write_bytes(text)
+            return t
+        if self.comm.is_distributed:
+            text = b"".join(self.comm.all_gather_object(text))
+        if self.is_root:
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(text)
+            return p
+        return None
+
+    def emit_root_text(self, text: bytes, out: str | None = None, name: str = "part-00000") -> Path | None:
+        """Reduce-side output of pre-formatted text: rank 0 writes it."""
+        if not self.is_root:
+            return None
+        p, is_dir = self._target(out)
+        if is_dir:
+            p.mkdir(parents=True, exist_ok=True)
+            p = p / name
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(text)
+        return p
+
     def emit_root(self, lines: list[str], out: str | None = None, name: str = "part-00000") -> Path | None:
         """Reduce-side output: rank 0 writes the (already reduced) result."""
         if not self.is_root:

@@ -282,16 +282,18 @@ def hica(args):
 
 @job("frequentItemsApriori", "Apriori frequent item sets (R/fit.sh): one transaction per line")
 def apriori(args):
+    from ..data.table import _literal
     from ..models.association import Apriori
     ctx = JobContext(args, "fia.")
     skip = ctx.get_int("skip.field.count", 1)
-    rows = ctx.rows()
-    base = 0
-    if ctx.comm.is_distributed:
-        from ..data.table import shard_range
-        base = shard_range(len(ctx.all_lines()), ctx.comm.rank, ctx.comm.world)[0]
-    ap = Apriori(ctx.get_float("support.threshold", 0.1), ctx.get_int("max.item.set.length", 4))
-    fi = ap.fit_transactions([r[skip:] for r in rows], device=ctx.device, tx_base=base)
+    ap = Apriori(ctx.get_float("support.threshold", 0.1), ctx.get_int("max.item.set.length", 4), comm=ctx.comm)
+    lit = _literal(ctx.delim_in)
+    if lit is not None and len(lit) == 1:
+        # native transaction ingest: this rank's byte range -> (transaction, item) pairs -> device bit rows
+        fi = ap.fit_records(ctx.records(modes="x" * skip), skip)
+    else:
+        rows = ctx.rows()
+        fi = ap.fit_transactions([r[skip:] for r in rows], device=ctx.device)
     d = ctx.delim_out
     lines = [d.join(names) + f"{d}{sup:.6f}" for k in range(1, ap.max_len + 1) for names, sup in fi.as_names(k)]
     ctx.emit_root(lines)
@@ -403,13 +405,47 @@ def ks(args):
 def markov(args):
     """Compact rows ``id,[class],s1,s2,...`` (MR and Spark compact format), or the Spark long format
     (``mst.input.format=long``: ``id,seq,state`` rows grouped by id and ordered by seq,
-    S/sequence/MarkovStateTransitionModel.scala:202-225)."""
-    from ..models.markov import MarkovStateTransitionModel
+    S/sequence/MarkovStateTransitionModel.scala:202-225).
+
+    Compact rows go through the native record path (J/markov/MarkovStateTransitionModel.java:116-133
+    splits and looks up every token in its mapper): this rank's byte range is tokenized once (on
+    the GPU when there is one), states and class labels are dictionary lookups on the device, the
+    sequences a padded [N, L] state matrix for the K4 bigram kernel, and the [C, S, S] counts are
+    all-reduced once."""
+    from ..data.table import _literal
     ctx = JobContext(args, "mst.")
+    lit = _literal(ctx.delim_in)
+    if ctx.get_str("input.format", "compact") == "long" or lit is None or len(lit) != 1:
+        return _markov_rows(ctx)
+    from ..models.markov import MarkovStateTransitionModel
     states = ctx.get_list("model.states", None) or ctx.get_list("state.list")
     skip = ctx.get_int("skip.field.count", 1)
     cls_ord = ctx.get_int("class.label.field.ord", ctx.get_int("class.label.field.ordinal", -1))
-    rows = ctx.rows()
+    modes = "".join("d" if i == cls_ord else "x" for i in range(max(skip, cls_ord + 1)))
+    rec = ctx.records(modes=modes)
+    st = rec.map_codes(rec.codes, states)
+    seqs, _ = rec.padded(st, start=skip, drop=(cls_ord,) if cls_ord >= 0 else ())
+    m = MarkovStateTransitionModel(states, scale=ctx.get_int("trans.prob.scale", 1000), comm=ctx.comm)
+    labels = None
+    if cls_ord >= 0:
+        lc = rec.field(cls_ord)
+        present = torch.unique(lc[lc >= 0]).tolist()
+        cl = ctx.get_list("class.labels", None) or ctx.union(rec.vocab[c] for c in present)
+        if len(cl) > 254:
+            raise SystemExit("markovStateTransitionModel: at most 254 class labels")
+        m.class_labels = cl
+        labels = rec.map_codes(lc, cl)
+        labels = torch.where(labels >= 0, labels, torch.full_like(labels, 255)).to(torch.uint8)
+    m.fit(seqs, labels)
+    ctx.emit_root(m.model_lines(ctx.delim_out))
+
+
+def _markov_rows(ctx: JobContext):
+    """Long-format input (and regex delimiters): the row-list path."""
+    from ..models.markov import MarkovStateTransitionModel
+    states = ctx.get_list("model.states", None) or ctx.get_list("state.list")
+    skip = ctx.get_int("skip.field.count", 1)
+    cls_ord = ctx.get_int("class.label.field.ord", ctx.get_int("class.label.field.ordinal", -1))
     if ctx.get_str("input.format", "compact") == "long":
         from collections import defaultdict
         id_ord, seq_ord, st_ord = (ctx.get_int("id.field.ordinal", 0), ctx.get_int("seq.field.ordinal", 1),
@@ -423,6 +459,8 @@ def markov(args):
             a, b = shard_range(len(rows), ctx.comm.rank, ctx.comm.world)
             rows = rows[a:b]
         skip, cls_ord = 1, -1
+    else:
+        rows = ctx.rows()
     seqs = [r[skip:] if cls_ord < 0 else [v for i, v in enumerate(r) if i >= skip and i != cls_ord] for r in rows]
     m = MarkovStateTransitionModel(states, scale=ctx.get_int("trans.prob.scale", 1000), comm=ctx.comm)
     enc = m.encode(seqs)

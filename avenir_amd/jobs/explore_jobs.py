@@ -230,6 +230,17 @@ def top_matches(args):
     maxd = ctx.get_int("top.match.distance", 200) if (by_dist or not by_count) else None
     compact = ctx.get_bool("compact.output", False)
     inc_cls = ctx.get_bool("include.class.in.output", True)
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    if lit is not None and len(lit) == 1:
+        rec = ctx.records()
+        W = rec.width()
+        if ctx.comm.is_distributed:
+            W = ctx.comm.all_gather_object(W)
+            W = W[0] if all(w == W[0] or w == 0 for w in W) else None
+            W = W if W != 0 else None
+        if W is not None and W >= 5 and (W - 3) % 2 == 0:
+            return _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact, inc_cls)
     rows = ctx.rows(shard=False)
     src, trg, rank, cls = [], [], [], []
     recs = {}
@@ -281,6 +292,95 @@ def top_matches(args):
         else:
             lines += [f"{head}{d}{x}" for x in out[s]]
     ctx.emit_root(lines)
+
+
+def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact, inc_cls):
+    """topMatchesByClass on the native record table: same-class pairs both ways, shuffled to the
+    rank owning the source entity (entities in string order, contiguous blocks per rank: the
+    reference's reducer key order), a device segmented sort on (source, rank) with the global
+    input order as tie-break, and the output assembled by the native formatter."""
+    from ..data.records import format_lines, numeric_lut, owner_of, shuffle, sorted_keys
+    comm = ctx.comm
+    dev = rec.device
+    Lr = (W - 3) // 2
+    M = rec.codes.view(rec.n_lines, W).long()
+    sc, tc = M[:, 2 + cls_ord], M[:, 2 + Lr + cls_ord]
+    ok = sc == tc
+    if filt is not None:
+        fc = rec.vocab.index(filt) if filt in rec.vocab else -2
+        ok &= sc == fc
+    rnum = numeric_lut(rec.vocab, dev)
+    rk = torch.trunc(rnum[M[:, W - 1].clamp_min(0)]) if len(rec.vocab) else torch.zeros(rec.n_lines, device=dev)
+    rk = torch.nan_to_num(rk, nan=float(2 ** 62)).long()
+    Mo = M[ok]
+    rko = rk[ok]
+    seq = (torch.nonzero(ok).view(-1) + rec.line_base) * 2
+    # both directions: (s -> t) then (t -> s), interleaved in input order via the sequence number
+    src = torch.cat([Mo[:, 0], Mo[:, 1]])
+    trg = torch.cat([Mo[:, 1], Mo[:, 0]])
+    srec = torch.cat([Mo[:, 2:2 + Lr], Mo[:, 2 + Lr:2 + 2 * Lr]])
+    trec = torch.cat([Mo[:, 2 + Lr:2 + 2 * Lr], Mo[:, 2:2 + Lr]])
+    sq = torch.cat([seq, seq + 1])
+    rr = torch.cat([rko, rko])
+    keys, pos = sorted_keys(rec, src, comm)
+    E = keys.numel()
+    if E == 0:
+        ctx.emit_root([])
+        return
+    spos = pos[src]
+    owner = owner_of(spos, E, comm.world) if comm.is_distributed else torch.zeros_like(spos)
+    cols = [spos, trg, rr, sq] + [srec[:, j] for j in range(Lr)] + [trec[:, j] for j in range(Lr)]
+    cols = shuffle(comm, owner, cols)
+    spos, trg, rr, sq = cols[:4]
+    srec = torch.stack(cols[4:4 + Lr], 1) if Lr else None
+    trec = torch.stack(cols[4 + Lr:], 1) if Lr else None
+    # (source, rank, input order) sort
+    o = torch.argsort(sq, stable=True)
+    o = o[torch.argsort(rr[o], stable=True)]
+    o = o[torch.argsort(spos[o], stable=True)]
+    spos, trg, rr = spos[o], trg[o], rr[o]
+    srec, trec = srec[o], trec[o]
+    n = spos.numel()
+    first = torch.ones(n, dtype=torch.bool, device=dev)
+    if n > 1:
+        first[1:] = spos[1:] != spos[:-1]
+    idx = torch.arange(n, device=dev)
+    start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
+    rank_in = idx - start
+    keep = torch.ones(n, dtype=torch.bool, device=dev)
+    if topn is not None:
+        keep &= rank_in < topn
+    if maxd is not None:
+        keep &= rr <= maxd
+    head_cols = (srec if inc_rec else keys[spos].view(-1, 1))
+    tail_cols = (trec if inc_rec else trg.view(-1, 1))
+    voc = rec.vocab
+    d = ctx.delim_out
+    if compact:
+        heads = torch.nonzero(first).view(-1)
+        kept = keep.long()
+        cnt = torch.zeros(heads.numel(), dtype=torch.long, device=dev).index_add_(
+            0, torch.cumsum(first.long(), 0)[keep] - 1, kept[keep])
+        has = cnt > 0
+        heads, cnt = heads[has], cnt[has]
+        tails = tail_cols[keep]
+        off = torch.zeros(cnt.numel() + 1, dtype=torch.long, device=dev)
+        off[1:] = torch.cumsum(cnt * tails.shape[1], 0)
+        hc = head_cols[heads]
+        cols_f = [("s", voc, hc[:, j].int().cpu()) for j in range(hc.shape[1])]
+        if inc_cls:
+            cols_f.append(("s", voc, srec[heads][:, cls_ord].int().cpu()))
+        cols_f.append(("l", voc, tails.reshape(-1).int().cpu(), off.cpu()))
+        text = format_lines(cols_f, heads.numel(), d)
+    else:
+        hc, tcs = head_cols[keep], tail_cols[keep]
+        cols_f = [("s", voc, hc[:, j].int().cpu()) for j in range(hc.shape[1])]
+        if inc_cls:
+            cols_f.append(("s", voc, srec[keep][:, cls_ord].int().cpu()))
+        cols_f += [("s", voc, tcs[:, j].int().cpu()) for j in range(tcs.shape[1])]
+        text = format_lines(cols_f, hc.shape[0], d)
+    # every rank's part is already in global source order: rank-ordered concatenation
+    ctx.emit_text(text)
 
 
 # ================================================================================================

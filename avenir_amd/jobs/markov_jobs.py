@@ -20,21 +20,39 @@ def hmm_builder(args):
     emission weights spread left/right by ``hmmb.window.function`` (:174-260).  Counts of the three
     tables are all-reduced once; output: states, observations, S transition rows, S emission rows,
     the initial-state row (integer rows scaled by ``hmmb.trans.prob.scale``)."""
+    from ..data.table import _literal
     from ..models.markov import HiddenMarkovModel, HiddenMarkovModelBuilder, normalize_rows
     ctx = JobContext(args, "hmmb.")
     states = ctx.get_list("model.states")
     observations = ctx.get_list("model.observations")
     scale = ctx.get_int("trans.prob.scale", 1000)
-    rows = ctx.rows()
     b = HiddenMarkovModelBuilder(states, observations, comm=ctx.comm)
+    lit = _literal(ctx.delim_in)
+    native = lit is not None and len(lit) == 1
     if ctx.get_bool("partially.tagged", False):
         win = ctx.get_int_list("window.function")
-        trans, emit, init = b.partially_tagged_counts(rows, win)
+        if native:   # every field of the row, states and observations by dictionary lookup
+            rec = ctx.records()
+            trans, emit, init = b.partially_tagged_counts_tokens(
+                rec.off, rec.map_codes(rec.codes, states), rec.map_codes(rec.codes, observations), win)
+        else:
+            trans, emit, init = b.partially_tagged_counts(ctx.rows(), win)
     else:
         skip = ctx.get_int("skip.field.count", 0)
         sub = ctx.get_str("sub.field.delim", ":")
-        tagged = [r[skip:] for r in rows if len(r) >= skip + 2]
-        obs, st = b.encode(tagged, sub)
+        if native and len(sub) == 1:
+            # obs:state tokens split natively (code, sub code); rows with >= 2 tagged tokens
+            rec = ctx.records(modes="x" * skip, sub_delim=sub)
+            st_tok = (rec.map_codes(rec.sub, states) if rec.sub is not None
+                      else torch.full_like(rec.codes, -1))
+            obs, n = rec.padded(rec.map_codes(rec.codes, observations), start=skip)
+            st, _ = rec.padded(st_tok, start=skip)
+            keep = n >= 2
+            if not bool(keep.all()):
+                obs, st = obs[keep], st[keep]
+        else:
+            tagged = [r[skip:] for r in ctx.rows() if len(r) >= skip + 2]
+            obs, st = b.encode(tagged, sub)
         trans, emit, init = b.counts(obs, st)
     ctx.all_reduce(trans, emit, init)
     A = normalize_rows(trans, scale)
@@ -246,6 +264,10 @@ def state_transition_rate(args):
     unit = ctx.get_str("rate.time.unit", "hour")
     in_unit = ctx.get_str("input.time.unit", "ms")
     prec = ctx.get_int("trans.rate.output.precision", 6)
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    if lit is not None and len(lit) == 1 and 1 <= len(kords) <= 2 and to not in kords and so not in kords:
+        return _state_transition_rate_native(ctx, kords, to, so, states, unit, in_unit, prec)
     rows = ctx.rows(shard=False)
     keys = sorted({tuple(r[o] for o in kords) for r in rows})
     ki = {k: i for i, k in enumerate(keys)}
@@ -260,6 +282,54 @@ def state_transition_rate(args):
     for i, k in enumerate(keys):
         out.append("(" + d.join(list(k) + [f"{v:.{prec}f}" for v in Q[i].reshape(-1).tolist()]) + ")")
     ctx.emit_root(out)
+
+
+def _state_transition_rate_native(ctx, kords, to, so, states, unit, in_unit, prec):
+    """stateTransitionRate on the native record table: events shuffled to the rank owning their
+    key (keys in string order, contiguous blocks per rank), then one segmented device pass per
+    rank (StateTransitionRate.fit_grouped) and the native formatter for ``(key,q00,q01,...)``."""
+    import numpy as np
+    from ..data.records import format_lines, owner_of, shuffle
+    from ..data.table import shard_range
+    from ..models.markov import StateTransitionRate
+    comm = ctx.comm
+    top = max(list(kords) + [to, so]) + 1
+    modes = "".join("n" if i == to else ("d" if (i in kords or i == so) else "x") for i in range(top))
+    rec = ctx.records(modes=modes, tail_mode="x", numeric=True)
+    dev = rec.device
+    V = max(1, len(rec.vocab))
+    kc = [rec.field(o).long() for o in kords]
+    tm_raw = rec.field(to, numeric=True)
+    st = rec.map_codes(rec.field(so), states).long()
+    ok = (st >= 0) & ~torch.isnan(tm_raw)
+    for c in kc:
+        ok &= c >= 0
+    comp = kc[0] if len(kc) == 1 else kc[0] * V + kc[1]
+    comp, st = comp[ok], st[ok]
+    mult = 1000 if in_unit == "sec" else 1
+    tm = torch.trunc(tm_raw[ok]).long() * mult
+    # global key set in string-tuple order
+    loc = torch.unique(comp)
+    allk = comm.all_gather_v(loc) if comm.is_distributed else loc
+    allk = torch.unique(allk).cpu()
+    parts = [allk] if len(kc) == 1 else [allk // V, allk % V]
+    strs = [np.array([rec.vocab[i] for i in p.tolist()]) for p in parts]
+    order = (np.lexsort(tuple(reversed(strs))) if allk.numel() else np.zeros(0, np.int64)).astype(np.int64)
+    order_t = torch.from_numpy(order)
+    G = allk.numel()
+    rank_of = torch.empty(G, dtype=torch.long)
+    rank_of[order_t] = torch.arange(G)
+    kpos = rank_of.to(dev)[torch.searchsorted(allk.to(dev), comp)] if comp.numel() else comp
+    owner = owner_of(kpos, G, comm.world) if comm.is_distributed else torch.zeros_like(kpos)
+    kpos, tm, st = shuffle(comm, owner, [kpos, tm, st])
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    Q = StateTransitionRate(len(states)).fit_grouped(kpos - a, tm, st, b - a, _MS[unit])
+    skeys = allk[order_t][a:b]
+    key_parts = [skeys] if len(kc) == 1 else [skeys // V, skeys % V]
+    cols = [("g", "(")] + [("s", rec.vocab, p.int()) for p in key_parts]
+    Qc = Q.reshape(b - a, -1).double().cpu()
+    cols += [("f", Qc[:, j].contiguous(), prec) for j in range(Qc.shape[1])] + [("g", ")")]
+    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
 
 
 @job("contTimeStateTransitionStats", "CTMC statistics by uniformisation: stateDwellTime | StateTransitionCount | futureStateProb (S/markov/ContTimeStateTransitionStats.scala)")

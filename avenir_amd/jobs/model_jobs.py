@@ -273,6 +273,15 @@ def nearest_neighbor(args):
     ccw = ctx.get_bool("class.condtion.weighted", False) or ctx.get_bool("class.condition.weighted", False)
     k = ctx.get_int("top.match.count", 10)
     out_distr = ctx.get_bool("output.class.distr", False)
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    if lit is not None and len(lit) == 1:
+        rec = ctx.records(modes="ddxndn" if ccw else "xdnd", tail_mode="d", numeric=True)
+        W = rec.width()
+        widths = ctx.comm.all_gather_object(W) if ctx.comm.is_distributed else [W]
+        ok_w = {w for w in widths if w not in (0, None)}
+        if len(ok_w) <= 1 and None not in widths and (ok_w <= ({6} if ccw else {4, 5})):
+            return _nearest_neighbor_native(ctx, rec, next(iter(ok_w), 6 if ccw else 4), ccw, val, k, out_distr)
     rows = ctx.rows(shard=False)
     if ccw:
         te_id = [r[0] for r in rows]
@@ -317,6 +326,7 @@ def nearest_neighbor(args):
     dk[T[keep], rank[keep]] = (Dv[keep] / 1000.0).float()     # distances are scaled by 1000 upstream
     ck[T[keep], rank[keep]] = Cv[keep]
     s = nn._kernel_scores(dk)
+    s = torch.where(torch.isfinite(dk), s, torch.zeros_like(s))   # empty neighbour slots do not vote
     if Wv is not None:
         wk = torch.zeros((nt, k), dtype=torch.float32)
         wk[T[keep], rank[keep]] = Wv[keep].float()
@@ -346,6 +356,104 @@ def nearest_neighbor(args):
     ctx.emit(out)
     if val:
         acc = torch.tensor([float(correct), float(len(tests))])
+        ctx.all_reduce(acc)
+        ctx.report({"Validation": {"Correct": int(acc[0]), "Incorrect": int(acc[1] - acc[0])}})
+
+
+def _nearest_neighbor_native(ctx, rec, W, ccw, val, k, out_distr):
+    """nearestNeighbor on the native record table: candidate pairs shuffled to the rank owning the
+    test record (test ids in string order, contiguous blocks: the reducer key order), a device
+    segmented sort on (test, distance) with the global input order as tie-break, the kernel-weighted
+    vote of models/knn.NearestNeighbor as [tests, k] tensors, and the native formatter for the
+    output (J/knn/NearestNeighbor.java:317-406)."""
+    from ..data.records import format_lines, owner_of, shuffle, sorted_keys
+    from ..models.knn import NearestNeighbor
+    comm = ctx.comm
+    dev = rec.device
+    n = rec.n_lines
+    Cd = rec.codes.view(n, W).long() if n else rec.codes.view(0, W).long()
+    Nd = rec.nums.view(n, W) if n else rec.nums.view(0, W)
+    if ccw:
+        te, te_c, dist, tr_c, w = Cd[:, 0], Cd[:, 1], Nd[:, 3], Cd[:, 4], Nd[:, 5]
+    else:
+        te, dist, tr_c = Cd[:, 1], Nd[:, 2], Cd[:, 3]
+        te_c = Cd[:, 4] if W > 4 else torch.full_like(te, -1)
+        w = None
+    classes = ctx.get_list("class.attribute.values", None)
+    if classes is None:
+        present = torch.unique(tr_c[tr_c >= 0]).tolist()
+        classes = ctx.union(rec.vocab[c] for c in present)
+    C = len(classes)
+    ci = rec.index(classes).long() if len(rec.vocab) else torch.zeros(0, dtype=torch.long, device=dev)
+    cls_idx = ci[tr_c.clamp_min(0)] if n and ci.numel() else torch.full_like(tr_c, -1)
+    keys, pos = sorted_keys(rec, te, comm)
+    E = keys.numel()
+    tpos = pos[te] if n else te
+    seq = torch.arange(n, device=dev) + rec.line_base
+    owner = owner_of(tpos, E, comm.world) if comm.is_distributed else torch.zeros_like(tpos)
+    cols = [tpos, dist, cls_idx, te_c, seq] + ([w] if w is not None else [])
+    cols = shuffle(comm, owner, cols)
+    tpos, dist, cls_idx, te_c, seq = cols[:5]
+    w = cols[5] if len(cols) > 5 else None
+    # this rank's tests: the contiguous block of sorted positions it owns
+    from ..data.table import shard_range
+    a, b = shard_range(E, comm.rank, comm.world) if comm.is_distributed else (0, E)
+    nt = b - a
+    t = tpos - a
+    o = torch.argsort(seq, stable=True)
+    o = o[torch.argsort(dist[o], stable=True)]
+    o = o[torch.argsort(t[o], stable=True)]
+    t, dist, cls_idx, te_c, seq = t[o], dist[o], cls_idx[o], te_c[o], seq[o]
+    w = w[o] if w is not None else None
+    m = t.numel()
+    first = torch.ones(m, dtype=torch.bool, device=dev)
+    if m > 1:
+        first[1:] = t[1:] != t[:-1]
+    idx = torch.arange(m, device=dev)
+    start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
+    rank = idx - start
+    keep = (rank < k) & (cls_idx >= 0)      # neighbours of an unknown class do not vote
+    nn = NearestNeighbor.from_config(ctx.cfg)
+    dk = torch.full((nt, k), math.inf, dtype=torch.float32, device=dev)
+    ck = torch.zeros((nt, k), dtype=torch.long, device=dev)
+    dk[t[keep], rank[keep]] = (dist[keep] / 1000.0).float()   # distances are scaled by 1000 upstream
+    ck[t[keep], rank[keep]] = cls_idx[keep]
+    s = nn._kernel_scores(dk)
+    s = torch.where(torch.isfinite(dk), s, torch.zeros_like(s))   # empty neighbour slots do not vote
+    if w is not None:
+        wk = torch.zeros((nt, k), dtype=torch.float32, device=dev)
+        wk[t[keep], rank[keep]] = w[keep].float()
+        s = s * wk
+    scores = torch.zeros((nt, max(C, 1)), dtype=torch.float32, device=dev).scatter_add_(1, ck, s.float())
+    pred = scores.argmax(1)
+    if nn.decision_threshold > 0 and C == 2:
+        ratio = scores[:, 1] / scores[:, 0].clamp_min(1e-12)
+        pred = (ratio > nn.decision_threshold).long()
+    # actual class of a test: its last candidate row in input order
+    last = torch.full((nt,), -1, dtype=torch.long, device=dev)
+    if m:
+        last.scatter_reduce_(0, t, seq, "amax")
+        at = torch.full((nt,), -1, dtype=torch.long, device=dev)
+        hit = seq == last[t]
+        at[t[hit]] = te_c[hit]
+    else:
+        at = torch.full((nt,), -1, dtype=torch.long, device=dev)
+    names = keys[a:b]
+    voc = rec.vocab
+    cols_f = [("s", voc, names.int().cpu())]
+    if out_distr:
+        sc = scores.double().cpu()
+        for c in range(C):
+            cols_f += [("c", classes[c]), ("f", sc[:, c].contiguous(), -1)]
+    if val:
+        cols_f.append(("s", voc, at.int().cpu()))
+    cols_f.append(("s", list(classes), pred.int().cpu()))
+    ctx.emit_text(format_lines(cols_f, nt, ctx.delim_out))
+    if val:
+        av = rec.index(classes).long()
+        act_cls = torch.where(at >= 0, av[at.clamp_min(0)] if av.numel() else at, torch.full_like(at, -2))
+        correct = float((act_cls == pred).sum())
+        acc = torch.tensor([correct, float(nt)], dtype=torch.float64)
         ctx.all_reduce(acc)
         ctx.report({"Validation": {"Correct": int(acc[0]), "Incorrect": int(acc[1] - acc[0])}})
 

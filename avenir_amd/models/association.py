@@ -38,12 +38,10 @@ def build_bitsets(tx: torch.Tensor, item: torch.Tensor, n_tx: int, n_items: int)
     W = max(1, (n_tx + 63) // 64)
     bits = torch.zeros((n_items, W), dtype=torch.int64)
     ok = (item >= 0) & (item < n_items) & (tx >= 0) & (tx < n_tx)
-    for t, i in zip(tx[ok].tolist(), item[ok].tolist()):
-        w, b = divmod(t, 64)
-        val = 1 << b
-        if val >= 1 << 63:
-            val -= 1 << 64
-        bits[i, w] |= val
+    # distinct (item, tx) pairs: adding distinct powers of two is OR (two's-complement wrap at bit 63)
+    key = torch.unique(item[ok].long() * n_tx + tx[ok].long())
+    i, t = key // n_tx, key % n_tx
+    bits.view(-1).index_add_(0, i * W + t // 64, torch.bitwise_left_shift(torch.ones_like(t), t % 64))
     return bits
 
 
@@ -97,6 +95,21 @@ class Apriori:
         bits = build_bitsets(torch.tensor(tx, dtype=torch.long, device=dev),
                              torch.tensor(it, dtype=torch.int32, device=dev), len(transactions), len(items))
         return self.fit_bitsets(bits, len(transactions), items)
+
+    def fit_records(self, rec, skip: int = 0) -> FrequentItemsets:
+        """Transactions from a CSR record table (data/records.py) whose first ``skip`` fields were
+        tokenized as 'x' (transaction ids), so every dictionary entry is an item and the (merged)
+        dictionary is the global item set.  Items are ordered by name (as ``fit_transactions``);
+        (transaction, item) pairs go straight from the token table to the device bit rows."""
+        items = sorted(rec.vocab)
+        order = {v: k for k, v in enumerate(items)}
+        dev = rec.device
+        lut = torch.tensor([order[v] for v in rec.vocab] or [0], dtype=torch.int32, device=dev)
+        ok = rec.codes >= 0
+        tx = rec.line_of_token()[ok]
+        it = lut[rec.codes[ok].long()] if len(rec.vocab) else rec.codes[ok]
+        bits = build_bitsets(tx, it, rec.n_lines, len(items))
+        return self.fit_bitsets(bits, rec.n_lines, items)
 
     def fit_bitsets(self, bits: torch.Tensor, n_tx: int, items: list[str]) -> FrequentItemsets:
         comm = self.comm or get_comm()

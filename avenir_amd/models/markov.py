@@ -264,6 +264,61 @@ class HiddenMarkovModelBuilder:
         ini = torch.bincount(torch.tensor(init, dtype=torch.long), minlength=S)[:S]
         return trans, emit, ini
 
+    def partially_tagged_counts_tokens(self, off: torch.Tensor, st_tok: torch.Tensor, ob_tok: torch.Tensor,
+                                       window: list[int]):
+        """:meth:`partially_tagged_counts` over a CSR token table on its device: ``off`` [L+1]
+        line offsets, ``st_tok`` / ``ob_tok`` [T] state / observation index of every token (-1
+        when the token is not one).  The per-state left / right emission windows are expanded
+        into (state, observation, weight) triples with one ``repeat_interleave`` and scattered
+        once; no per-line Python loop (same integer boundary arithmetic as the list version)."""
+        S, O = len(self.states), len(self.observations)
+        dev = st_tok.device
+        L = off.numel() - 1
+        lens = off[1:] - off[:-1]
+        tl = torch.repeat_interleave(torch.arange(L, device=dev), lens)
+        pos = torch.arange(st_tok.numel(), device=dev) - off[:-1][tl]
+        ks = torch.nonzero(st_tok >= 0).view(-1)
+        z = torch.zeros(0, dtype=torch.long, device=dev)
+        if ks.numel() == 0:
+            return (torch.zeros((S, S), dtype=torch.long, device=dev), torch.zeros((S, O), dtype=torch.long, device=dev),
+                    torch.zeros(S, dtype=torch.long, device=dev))
+        ln, p, sv = tl[ks], pos[ks], st_tok[ks].long()
+        nn = lens[ln]
+        f = torch.zeros(1, dtype=torch.bool, device=dev)
+        prev_same = torch.cat([f, ln[1:] == ln[:-1]])
+        next_same = torch.cat([ln[1:] == ln[:-1], f])
+        p_prev = torch.cat([z.new_zeros(1), p[:-1]])
+        p_next = torch.cat([p[1:], z.new_zeros(1)])
+        neg = torch.full_like(p, -1)
+        lw = torch.where(prev_same, p - torch.div(p_prev, 2, rounding_mode="floor"), torch.zeros_like(p))
+        lb = torch.where(prev_same, p - lw, neg)
+        rw = torch.where(next_same, p_next - torch.div(p, 2, rounding_mode="floor"), torch.zeros_like(p))
+        rb = torch.where(next_same, p + rw, neg)
+        c1 = (lb == -1) & (rb != -1)
+        c2 = (rb == -1) & (lb != -1)
+        c3 = (lb == -1) & (rb == -1)
+        lb = torch.where(c1, (p - rw).clamp_min(0), lb)
+        rb = torch.where(c2, torch.minimum(p + lw, nn - 1), rb)
+        lb = torch.where(c3, torch.div(p, 2, rounding_mode="floor"), lb)
+        rb = torch.where(c3, p + torch.div(nn - 1 - p, 2, rounding_mode="floor"), rb)
+        n_left = (p - lb.clamp_min(0)).clamp_min(0)
+        n_right = (torch.minimum(rb, nn - 1) - p).clamp_min(0)
+        tot = n_left + n_right
+        rep = torch.repeat_interleave(torch.arange(ks.numel(), device=dev), tot)
+        start = torch.cumsum(tot, 0) - tot
+        t = torch.arange(rep.numel(), device=dev) - start[rep]
+        left = t < n_left[rep]
+        j = torch.where(left, p[rep] - 1 - t, p[rep] + 1 + (t - n_left[rep]))
+        k = torch.where(left, t, t - n_left[rep])
+        w = torch.tensor(window, dtype=torch.long, device=dev)[k.clamp_max(len(window) - 1)]
+        ob = ob_tok[off[:-1][ln[rep]] + j].long()
+        ok = ob >= 0
+        emit = torch.zeros(S * O, dtype=torch.long, device=dev).index_add_(0, sv[rep][ok] * O + ob[ok], w[ok]).view(S, O)
+        a, b = sv[:-1][prev_same[1:]], sv[1:][prev_same[1:]]
+        trans = torch.bincount(a * S + b, minlength=S * S)[: S * S].view(S, S)
+        ini = torch.bincount(sv[~prev_same], minlength=S)[:S]
+        return trans, emit, ini
+
     def fit(self, obs: torch.Tensor, st: torch.Tensor) -> HiddenMarkovModel:
         trans, emit, init = self.counts(obs, st)
         comm = self.comm or get_comm()

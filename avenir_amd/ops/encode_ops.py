@@ -21,15 +21,20 @@ MOMENT_FIELDS = ("count", "sum", "min", "max", "m2", "m3", "m4", "mean")
 def column_moments(X: torch.Tensor, n: int | None = None) -> torch.Tensor:
     """double [F, 8] = (count, sum, min, max, m2, m3, m4, mean) of each row of a column-major
     [F, ld] (or 1-D) matrix over its first ``n`` entries; NaNs are skipped, m_k are central power
-    sums divided by the count."""
+    sums divided by the count.  A column without values (n == 0 or all NaN) has count 0, sum 0
+    and NaN for every other statistic, on both devices."""
     X2 = X.view(1, -1) if X.dim() == 1 else X
     n = X2.shape[1] if n is None else int(n)
-    if X2.is_cuda and n > 0:
+    if n == 0:
+        out = torch.full((X2.shape[0], 8), float("nan"), dtype=torch.float64, device=X2.device)
+        out[:, :2] = 0.0
+        return out
+    if X2.is_cuda:
         if X2.dtype not in (torch.float32, torch.float64):
             X2 = X2.double()
         if X2.dtype == torch.float32 and (X2.shape[1] % 4 or X2.data_ptr() % 16 or not X2.is_contiguous()):
             X2 = X2.double()
-        return _native.C().col_moments(X2.contiguous(), n)
+        return _empty_as_nan(_native.C().col_moments(X2.contiguous(), n))
     x = X2[:, :n].double()
     ok = ~torch.isnan(x)
     cnt = ok.sum(1).double()
@@ -41,7 +46,17 @@ def column_moments(X: torch.Tensor, n: int | None = None) -> torch.Tensor:
     mean = sm / c1
     d = torch.where(ok, x - mean[:, None], torch.zeros_like(x))
     d2 = d * d
-    return torch.stack([cnt, sm, lo, hi, d2.sum(1) / c1, (d2 * d).sum(1) / c1, (d2 * d2).sum(1) / c1, mean], 1)
+    return _empty_as_nan(torch.stack([cnt, sm, lo, hi, d2.sum(1) / c1, (d2 * d).sum(1) / c1, (d2 * d2).sum(1) / c1,
+                                      mean], 1))
+
+
+def _empty_as_nan(m: torch.Tensor) -> torch.Tensor:
+    empty = m[:, 0] == 0
+    if bool(empty.any()):
+        m = m.clone()
+        m[empty, 2:] = float("nan")
+        m[empty, 1] = 0.0
+    return m
 
 
 def moments_dict(row: torch.Tensor) -> dict[str, float]:

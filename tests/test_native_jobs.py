@@ -1,0 +1,149 @@
+"""The six text-layout jobs on native record ingest.
+
+Each job runs twice on the same seeded data: through the native record path (one-character
+delimiter) and through the row-list path (the same delimiter written as the regex ``[,]``, which
+the native path does not take) — outputs must be identical.  At world 3 (gloo ranks, byte-range
+shards, dictionary merge, all-to-all key shuffle) the output must equal world 1.  GPU: the same
+jobs on a device table (device tokenizer) against the CPU run."""
+from __future__ import annotations
+
+import random
+from pathlib import Path
+
+import pytest
+import torch
+
+from avenir_amd.cli import main
+from avenir_amd.data import records as R
+from avenir_amd.data import synth_text as S
+
+from _dist import run_world
+
+
+def _lines(p):
+    p = Path(p)
+    if p.is_dir():
+        return [l for f in sorted(p.iterdir()) if f.is_file() for l in f.read_text().splitlines() if l.strip()]
+    return [l for l in p.read_text().splitlines() if l.strip()]
+
+
+def _ragged_sequences(path, n, seed):
+    rnd = random.Random(seed)
+    st = S.STATES + ["BAD"]
+    with open(path, "w") as f:
+        for i in range(n):
+            toks = [rnd.choice(st) for _ in range(rnd.randint(1, 12))]
+            f.write(f"c{i},{rnd.choice('TF')}," + ",".join(toks) + "\n")
+            if i % 50 == 0:
+                f.write("\n")
+
+
+def _partial(path, n, seed):
+    rnd = random.Random(seed)
+    with open(path, "w") as f:
+        for i in range(n):
+            f.write(",".join(rnd.choice(["a", "b", "c", "d", "S", "T", "U"]) for _ in range(rnd.randint(1, 14))) + "\n")
+
+
+CASES = {
+    # name: (job, writer, props text)
+    "mst": ("markovStateTransitionModel", lambda p: _ragged_sequences(p, 3000, 1),
+            "mst.model.states=" + ",".join(S.STATES) + "\nmst.skip.field.count=1\nmst.class.label.field.ord=1\n"
+            "mst.trans.prob.scale=1000\n"),
+    "mst1": ("markovStateTransitionModel", lambda p: S.state_sequences(p, 4000, classes=None, seed=2),
+             "mst.model.states=" + ",".join(S.STATES) + "\nmst.skip.field.count=1\n"),
+    "hmm": ("hiddenMarkovModelBuilder", lambda p: S.tagged_sequences(p, 3000, seed=3),
+            "hmmb.model.states=S,T,U\nhmmb.model.observations=a,b,c,d\nhmmb.skip.field.count=1\n"
+            "hmmb.trans.prob.scale=1000\n"),
+    "hmmp": ("hiddenMarkovModelBuilder", lambda p: _partial(p, 3000, 4),
+             "hmmb.model.states=S,T,U\nhmmb.model.observations=a,b,c,d\nhmmb.partially.tagged=true\n"
+             "hmmb.window.function=4,2,1\n"),
+    "apriori": ("frequentItemsApriori", lambda p: S.transactions(p, 3000, n_items=60, per_tx=5, seed=5),
+                "fia.support.threshold=0.02\nfia.max.item.set.length=3\nfia.skip.field.count=1\n"),
+    "tmc": ("topMatchesByClass", lambda p: S.match_pairs(p, 6000, 300, seed=6),
+            "tmc.class.attr.ord=1\ntmc.top.match.count=4\n"),
+    "tmcc": ("topMatchesByClass", lambda p: S.match_pairs(p, 6000, 300, seed=7),
+             "tmc.class.attr.ord=1\ntmc.top.match.count=3\ntmc.compact.output=true\n"
+             "tmc.include.class.in.output=false\ntmc.include.rec.in.output=false\n"),
+    "nen": ("nearestNeighbor", lambda p: S.knn_pairs(p, 200, 16, n_train=500, seed=8),
+            "nen.top.match.count=5\nnen.kernel.function=none\nnen.validation.mode=true\n"
+            "nen.output.class.distr=true\n"),
+    "str": ("stateTransitionRate", lambda p: S.events(p, 5000, n_keys=40, seed=9), None),
+}
+
+
+def _props(tmp, name, text, regex=False):
+    if name == "str":
+        p = tmp / "str.conf"
+        p.write_text("stateTransitionRate {\n field.delim.in = \"" + ("[,]" if regex else ",") + "\"\n"
+                     " key.field.ordinals = [0]\n time.field.ordinal = 1\n state.field.ordinal = 2\n"
+                     " state.values = [A,B,C,D]\n rate.time.unit = hour\n}\n")
+        return p
+    p = tmp / f"{name}{'_re' if regex else ''}.properties"
+    p.write_text(text + ("field.delim.regex=[,]\n" if regex else "field.delim.regex=,\n"))
+    return p
+
+
+def _run(job, data, out, cfg, device="cpu"):
+    args = [job, "-i", str(data), "-o", str(out), "-c", str(cfg), "--device", device]
+    if job == "stateTransitionRate":
+        args += ["--app", "stateTransitionRate"]
+    assert main(args) == 0
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_native_equals_row_path(tmp_path, name):
+    job, writer, text = CASES[name]
+    data = tmp_path / "data.txt"
+    writer(data)
+    _run(job, data, tmp_path / "native.txt", _props(tmp_path, name, text))
+    _run(job, data, tmp_path / "rows.txt", _props(tmp_path, name, text, regex=True))
+    got, ref = _lines(tmp_path / "native.txt"), _lines(tmp_path / "rows.txt")
+    assert got and got == ref
+
+
+def _world_job(rank, world, job, data, out, cfg):
+    args = [job, "-i", data, "-o", out, "-c", cfg, "--device", "cpu"]
+    if job == "stateTransitionRate":
+        args += ["--app", "stateTransitionRate"]
+    assert main(args) == 0
+    return True
+
+
+@pytest.mark.parametrize("name", ["mst", "hmmp", "apriori", "tmc", "nen", "str"])
+def test_native_jobs_world_invariant(tmp_path, name):
+    job, writer, text = CASES[name]
+    data = tmp_path / "data.txt"
+    writer(data)
+    cfg = _props(tmp_path, name, text)
+    _run(job, data, tmp_path / "w1.txt", cfg)
+    run_world(_world_job, 3, job, str(data), str(tmp_path / "w3.txt"), str(cfg), timeout=300)
+    assert _lines(tmp_path / "w3.txt") == _lines(tmp_path / "w1.txt")
+
+
+def _byte_ranges(rank, world, data):
+    from avenir_amd.parallel.comm import get_comm
+    rec = R.read_records(data, comm=get_comm())
+    return rec.stats["bytes"], rec.n_lines
+
+
+def test_each_rank_reads_only_its_byte_range(tmp_path):
+    data = tmp_path / "seq.txt"
+    nbytes = S.state_sequences(data, 4000, seed=11)
+    res = run_world(_byte_ranges, 4, str(data))
+    assert sum(b for b, _ in res) == nbytes            # no byte is read twice
+    assert all(b < nbytes / 4 * 1.05 for b, _ in res)  # every rank reads about its quarter
+    assert sum(n for _, n in res) == 4000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_native_jobs_on_gpu_equal_cpu(tmp_path, name, monkeypatch):
+    job, writer, text = CASES[name]
+    data = tmp_path / "data.txt"
+    writer(data)
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)   # small files through the device tokenizer too
+    cfg = _props(tmp_path, name, text)
+    _run(job, data, tmp_path / "gpu.txt", cfg, device="cuda")
+    _run(job, data, tmp_path / "cpu.txt", cfg)
+    assert _lines(tmp_path / "gpu.txt") == _lines(tmp_path / "cpu.txt")

@@ -1,0 +1,201 @@
+"""Native record ingest (data/records.py, csrc/host/records.cpp, csrc/kernels/records.hip).
+
+CPU: the native TextShard tokenizer against its pure-Python twin, byte-range shards at several
+world sizes (every line on exactly one rank; merged dictionaries = world-1 dictionary), and the
+JobContext line shards.  GPU: the device tokenizer against the host tokenizer (codes, sub codes,
+numbers, vocabulary), sharded and whole."""
+from __future__ import annotations
+
+import math
+import random
+
+import pytest
+import torch
+
+from avenir_amd import _native
+from avenir_amd.data import records as R
+
+from _dist import run_world
+
+
+def _write(tmp_path, n=3000, seed=0, crlf=True, name="rec.txt"):
+    rnd = random.Random(seed)
+    st = ["L", "M", "H", "LL", "hm", "x y"]
+    lines = []
+    for i in range(n):
+        toks = [f"{rnd.choice(st)}:{rnd.choice('abc')}" for _ in range(rnd.randint(1, 9))]
+        lines.append(f"id{i},{rnd.random() * 100:.3f}," + ",".join(toks))
+        if i % 97 == 0:
+            lines.append("  \t ")
+    txt = "".join(l + ("\r\n" if crlf and i % 3 == 0 else "\n") for i, l in enumerate(lines))
+    p = tmp_path / name
+    p.write_text(txt.rstrip("\n"))   # last line without a newline
+    return p
+
+
+SPECS = [dict(), dict(sub_delim=":"), dict(modes="xn", numeric=True), dict(modes="dn", sub_delim=":", numeric=True,
+                                                                              trim=True)]
+
+
+def _py(paths, rank=0, world=1, **kw):
+    return R._read_records_py(paths, rank, world, kw.get("delims", ","), kw.get("sub_delim", ""), kw.get("modes", ""),
+                              kw.get("tail_mode", "d"), kw.get("trim", False), kw.get("numeric", False), False)
+
+
+def _same(a, b):
+    assert a.vocab == b.vocab
+    assert torch.equal(a.off.cpu(), b.off.cpu())
+    assert torch.equal(a.codes.cpu(), b.codes.cpu())
+    assert (a.sub is None) == (b.sub is None)
+    if a.sub is not None:
+        assert torch.equal(a.sub.cpu(), b.sub.cpu())
+    if a.nums is not None:
+        assert torch.allclose(a.nums.cpu(), b.nums.cpu(), equal_nan=True)
+
+
+@pytest.mark.skipif(not _native.available(), reason="native extension not built")
+@pytest.mark.parametrize("spec", SPECS)
+def test_native_tokenizer_matches_python(tmp_path, spec):
+    p = _write(tmp_path)
+    _same(R.read_records(str(p), **spec), _py([str(p)], **spec))
+
+
+@pytest.mark.skipif(not _native.available(), reason="native extension not built")
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_byte_range_shards_partition_lines(tmp_path, world):
+    a = _write(tmp_path, n=2000, seed=1, name="part-00000")
+    _write(tmp_path, n=1500, seed=2, name="part-00001")
+    whole = R.shard_lines(str(tmp_path))
+    C = _native.C()
+    parts, bytes_read = [], 0
+    for r in range(world):
+        sh = C.TextShard([str(tmp_path / "part-00000"), str(tmp_path / "part-00001")], r, world, 4, False)
+        parts += sh.lines(0, sh.num_lines())
+        bytes_read += sh.bytes_read()
+        # the python twin makes the same ownership decision
+        assert sh.lines(0, sh.num_lines()) == R._py_lines([str(tmp_path / "part-00000"),
+                                                           str(tmp_path / "part-00001")], r, world, False)
+    assert parts == whole
+    # every byte is read by exactly one rank (plus nothing else)
+    assert bytes_read == a.stat().st_size + (tmp_path / "part-00001").stat().st_size
+
+
+def _rank_records(rank, world, path):
+    from avenir_amd.parallel.comm import get_comm
+    rec = R.read_records(path, comm=get_comm(), sub_delim=":", modes="xn", numeric=True)
+    return rec.line_base, rec.n_lines, rec.vocab, rec.codes.tolist(), rec.sub.tolist()
+
+
+@pytest.mark.skipif(not _native.available(), reason="native extension not built")
+def test_merged_dictionary_is_world_invariant(tmp_path):
+    p = _write(tmp_path, n=4000, seed=3)
+    one = R.read_records(str(p), sub_delim=":", modes="xn", numeric=True)
+    res = run_world(_rank_records, 4, str(p))
+    codes, subs, base = [], [], 0
+    for lb, n, voc, c, s in res:
+        assert voc == one.vocab          # the merged dictionary is the world-1 dictionary
+        assert lb == base
+        base += n
+        codes += c
+        subs += s
+    assert base == one.n_lines
+    assert codes == one.codes.tolist() and subs == one.sub.tolist()
+
+
+def test_records_helpers(tmp_path):
+    p = tmp_path / "f.txt"
+    p.write_text("a,1.5,x\nb,2,y,z\n\nc,bad,x\n")
+    rec = R.read_records(str(p), modes="dn", numeric=True)
+    assert rec.n_lines == 3 and rec.width() is None
+    assert rec.strings(rec.field(0)) == ["a", "b", "c"]
+    f1 = rec.field(1, numeric=True)
+    assert f1[0] == 1.5 and f1[1] == 2 and math.isnan(float(f1[2]))
+    assert rec.strings(rec.field(-1)) == ["x", "z", "x"]
+    assert rec.field(3).tolist() == [-1, rec.vocab.index("z"), -1]
+    assert rec.map_codes(rec.field(0), ["c", "a"]).tolist() == [1, -1, 0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", SPECS)
+@pytest.mark.parametrize("world", [1, 3])
+def test_device_tokenizer_matches_host(tmp_path, cuda, spec, world):
+    p = _write(tmp_path, n=20000, seed=4)
+    C = _native.C()
+    for r in range(world):
+        out = C.text_tokenize_device([str(p)], r, world, ",", spec.get("sub_delim", ""), spec.get("modes", ""), "d",
+                                     spec.get("trim", False), spec.get("numeric", False), torch.empty(0, device=cuda))
+        assert out is not None
+        off, codes, sub, nums, vocab, stats = out
+        assert codes.is_cuda and off.is_cuda
+        sh = C.TextShard([str(p)], r, world, 4, False)
+        hoff, hcodes, hsub, hnums, hvocab = sh.tokenize(",", spec.get("sub_delim", ""), spec.get("modes", ""), "d",
+                                                        spec.get("trim", False), spec.get("numeric", False))
+        _same(R.Records(off, codes, sub, nums, list(vocab)), R.Records(hoff, hcodes, hsub, hnums, list(hvocab)))
+
+
+@pytest.mark.gpu
+def test_device_tokenizer_large_vocab_and_table_growth(tmp_path, cuda, monkeypatch):
+    # 300k distinct ids + a small vocabulary; a 1024-slot first table forces the retry path
+    p = tmp_path / "ids.txt"
+    rnd = random.Random(5)
+    p.write_text("\n".join(f"u{i * 7919 % 1000003},{rnd.choice('ABCD')},{i % 13}" for i in range(300_000)) + "\n")
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
+    dev = R.read_records(str(p), device=cuda, modes="ddn", numeric=True)
+    assert dev.stats.get("path") == "device"
+    host = R.read_records(str(p), modes="ddn", numeric=True)
+    _same(dev, host)
+    off, codes, sub, nums, vocab, stats = _native.C().text_tokenize_device(
+        [str(p)], 0, 1, ",", "", "ddn", "d", False, True, torch.empty(0, device=cuda), 1024)
+    assert stats["table_slots"] >= 2 * len(host.vocab)
+    _same(R.Records(off, codes, sub, nums, list(vocab)), host)
+
+
+@pytest.mark.gpu
+def test_device_csv_ring_two_threads(tmp_path, cuda):
+    """concurrent device CSV loads must not share staging slots."""
+    import threading
+    from avenir_amd.data import table as T
+    from avenir_amd.data.table import load_csv
+    from avenir_amd.utils.schema import FeatureSchema
+    schema = FeatureSchema.from_json({"fields": [
+        {"name": "id", "ordinal": 0, "dataType": "string", "id": True},
+        {"name": "a", "ordinal": 1, "dataType": "categorical", "feature": True, "cardinality": ["x", "y", "z"]},
+        {"name": "c", "ordinal": 2, "dataType": "categorical", "cardinality": ["0", "1"]}]})
+    paths = []
+    for k in range(2):
+        p = tmp_path / f"t{k}.csv"
+        rnd = random.Random(k)
+        p.write_text("\n".join(f"r{i},{rnd.choice('xyz')},{rnd.randint(0, 1)}" for i in range(400_000)) + "\n")
+        paths.append(p)
+    old = T._GPU_CSV_MIN_BYTES
+    T._GPU_CSV_MIN_BYTES = 1
+    try:
+        res = [None, None]
+
+        def load(k):
+            res[k] = load_csv(str(paths[k]), schema, ",", device=cuda)
+
+        th = [threading.Thread(target=load, args=(k,)) for k in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        T._GPU_CSV_MIN_BYTES = old
+    for k in range(2):
+        ref = load_csv(str(paths[k]), schema, ",")
+        assert torch.equal(res[k].codes[:, : ref.n].cpu(), ref.codes[:, : ref.n])
+        assert torch.equal(res[k].labels[: ref.n].cpu(), ref.labels[: ref.n])
+
+
+@pytest.mark.gpu
+def test_col_moments_empty_matches_cpu(cuda):
+    """an empty column behaves the same on both devices."""
+    from avenir_amd.ops import encode_ops as E
+    x = torch.zeros(2, 0)
+    a = E.column_moments(x)
+    b = E.column_moments(x.to(cuda)).cpu()
+    assert torch.equal(a[:, 0], b[:, 0])
+    assert torch.allclose(a, b, equal_nan=True)
+    y = torch.full((1, 100), float("nan"))
+    assert torch.allclose(E.column_moments(y), E.column_moments(y.to(cuda)).cpu(), equal_nan=True)
