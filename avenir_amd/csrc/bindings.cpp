@@ -1886,15 +1886,18 @@ std::string format_rows(py::object prefix, const at::Tensor& cols, std::vector<i
 // TextShard tokenizer (records.cpp): returns (off int64 [L+1], codes int32 [T], sub int32 [T] or None,
 // nums float64 [T] or None, vocab list[str]).
 py::tuple text_tokenize(avh::TextShard& sh, const std::string& delims, const std::string& sub_delim,
-                        const std::string& modes, const std::string& tail_mode, bool trim, bool want_nums) {
-  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1, "sub_delim: 0/1 char, tail_mode: 1 char");
-  for (char c : modes + tail_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
+                        const std::string& modes, const std::string& tail_mode, bool trim, bool want_nums,
+                        const std::string& last_mode) {
+  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && last_mode.size() <= 1,
+              "sub_delim / last_mode: 0/1 char, tail_mode: 1 char");
+  for (char c : modes + tail_mode + last_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
   avh::TokenSpec sp;
   sp.delims = delims.empty() ? std::string(",") : delims;
   sp.sub_delim = sub_delim.empty() ? 0 : sub_delim[0];
   sp.modes = modes;
   sp.tail_mode = tail_mode[0];
   sp.trim = trim;
+  sp.last_mode = last_mode.empty() ? 0 : last_mode[0];
   const int64_t L = sh.num_lines();
   int64_t T;
   {
@@ -1933,11 +1936,12 @@ std::vector<std::string> text_field_strings(const avh::TextShard& sh, const at::
 py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, int64_t world,
                                 const std::string& delims_in, const std::string& sub_delim, const std::string& modes,
                                 const std::string& tail_mode, bool trim, bool want_nums, const at::Tensor& like,
-                                int64_t max_initial_slots) {
+                                int64_t max_initial_slots, const std::string& last_mode) {
   CHECK_DEV(like);
   TORCH_CHECK(max_initial_slots >= 1024, "max_initial_slots >= 1024");
-  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && modes.size() <= 64, "bad tokenizer options");
-  for (char c : modes + tail_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
+  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && modes.size() <= 64 && last_mode.size() <= 1,
+              "bad tokenizer options");
+  for (char c : modes + tail_mode + last_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
   const std::string delims = delims_in.empty() ? std::string(",") : delims_in;
   const char sd = sub_delim.empty() ? 0 : sub_delim[0];
   DevGuard g(like.device());
@@ -2063,7 +2067,7 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
     avk::rec_tokens(bytes, reinterpret_cast<const long long*>(ls.data_ptr<int64_t>()),
                     reinterpret_cast<const long long*>(le.data_ptr<int64_t>()),
                     reinterpret_cast<const long long*>(off.data_ptr<int64_t>()), L, delims.data(), (int)delims.size(),
-                    modes.data(), (int)modes.size(), tail_mode[0], sd, trim,
+                    modes.data(), (int)modes.size(), tail_mode[0], sd, trim, last_mode.empty() ? 0 : last_mode[0],
                     reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()),
                     reinterpret_cast<unsigned*>(h2tab.data_ptr<int>()),
                     reinterpret_cast<unsigned long long*>(first.data_ptr<int64_t>()), (unsigned long long)(cap - 1),
@@ -2130,6 +2134,10 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
   stats["upload_s"] = std::chrono::duration<double>(t1 - t0).count();
   stats["tokenize_s"] = std::chrono::duration<double>(t2 - t1).count();
   stats["table_slots"] = cap;
+  // the dictionary bytes stay on the device too (string-order sorts of keys run there)
+  stats["vbytes"] = vbytes.narrow(0, 0, std::max<int64_t>(VB, 0));
+  stats["voff"] = vout;
+  stats["vlen"] = vl64;
   py::object subo = sd ? py::cast(subc.narrow(0, 0, T)) : py::none();
   py::object numo = want_nums ? py::cast(nums.narrow(0, 0, T)) : py::none();
   return py::make_tuple(off, codes.narrow(0, 0, T), subo, numo, vocab, stats);
@@ -2141,6 +2149,7 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
 py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& delim, int nthreads) {
   std::vector<avh::FmtCol> cols;
   std::vector<std::unique_ptr<std::vector<std::string>>> tables;
+  std::map<PyObject*, const std::vector<std::string>*> table_of;
   std::vector<at::Tensor> keep;
   for (auto item : cols_py) {
     auto t = item.cast<py::tuple>();
@@ -2153,8 +2162,13 @@ py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& deli
       return x;
     };
     if (kind == "s" || kind == "l") {
-      tables.push_back(std::make_unique<std::vector<std::string>>(t[1].cast<std::vector<std::string>>()));
-      c.table = tables.back().get();
+      PyObject* key = t[1].ptr();  // one conversion per distinct table object
+      auto hit = table_of.find(key);
+      if (hit == table_of.end()) {
+        tables.push_back(std::make_unique<std::vector<std::string>>(t[1].cast<std::vector<std::string>>()));
+        hit = table_of.emplace(key, tables.back().get()).first;
+      }
+      c.table = hit->second;
       if (kind == "s") {
         c.kind = avh::FmtCol::STR;
         c.idx = cpu_tensor(t[2], at::kInt, n, "string").data_ptr<int32_t>();
@@ -2369,12 +2383,13 @@ PYBIND11_MODULE(_C, m) {
       .def("total_bytes", &avh::TextShard::total_bytes)
       .def("lines", &avh::TextShard::lines)
       .def("tokenize", &text_tokenize, py::arg("delims") = ",", py::arg("sub_delim") = "", py::arg("modes") = "",
-           py::arg("tail_mode") = "d", py::arg("trim") = false, py::arg("want_nums") = false)
+           py::arg("tail_mode") = "d", py::arg("trim") = false, py::arg("want_nums") = false,
+           py::arg("last_mode") = "")
       .def("field_strings", &text_field_strings);
   m.def("text_tokenize_device", &text_tokenize_device, py::arg("paths"), py::arg("rank"), py::arg("world"),
         py::arg("delims") = ",", py::arg("sub_delim") = "", py::arg("modes") = "", py::arg("tail_mode") = "d",
         py::arg("trim") = false, py::arg("want_nums") = false, py::arg("like"),
-        py::arg("max_initial_slots") = 1LL << 24);
+        py::arg("max_initial_slots") = 1LL << 24, py::arg("last_mode") = "");
   m.def("format_columns", &format_columns_py, py::arg("cols"), py::arg("n"), py::arg("delim") = ",",
         py::arg("nthreads") = 8);
   m.def("format_rows", &format_rows);

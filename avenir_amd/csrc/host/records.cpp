@@ -335,7 +335,7 @@ void TextShard::tokenize(int64_t* off, int32_t* codes, int32_t* sub, double* num
         while (true) {
           const char* q = p;
           while (q < e && !sep_[(uint8_t)*q]) ++q;
-          const char m = f < nm ? sp.modes[(size_t)f] : sp.tail_mode;
+          const char m = (q >= e && sp.last_mode) ? sp.last_mode : (f < nm ? sp.modes[(size_t)f] : sp.tail_mode);
           const char* a = p;
           const char* b = q;
           if (sp.trim) {

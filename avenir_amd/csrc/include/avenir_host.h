@@ -107,6 +107,7 @@ struct TokenSpec {
   std::string modes;
   char tail_mode = 'd';
   bool trim = false;
+  char last_mode = 0;  // the mode of every line's LAST field (0: by position like the others)
 };
 
 // K1 for non-schema layouts (records.cpp): this rank's byte range of the concatenated input files

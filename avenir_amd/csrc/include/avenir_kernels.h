@@ -191,7 +191,7 @@ void rec_lines(const uint8_t* bytes, const long long* nlpos, long long nraw, con
                long long* lstart, long long* lend, int* ntok, hipStream_t stream);
 void rec_tokens(const uint8_t* bytes, const long long* lstart, const long long* lend, const long long* off, long long L,
                 const char* delims, int ndelims, const char* modes, int nmodes, char tail_mode, char sub_delim,
-                bool trim, unsigned long long* keys, unsigned* h2tab, unsigned long long* first,
+                bool trim, char last_mode, unsigned long long* keys, unsigned* h2tab, unsigned long long* first,
                 unsigned long long mask, int* tslot, unsigned* th2, int* tsub, unsigned* th2sub, double* nums,
                 unsigned* inserted, unsigned* overflow, hipStream_t stream);
 void rec_codes(const int* tslot, const unsigned* th2, long long T, const int* slot_code, const unsigned* h2tab,

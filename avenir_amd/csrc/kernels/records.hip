@@ -36,7 +36,7 @@ struct TokArgs {
   unsigned sep[8];         // 256-bit separator set
   unsigned char modes[64];  // per field index: 'd' / 'n' / 'x'
   int nmodes;
-  unsigned char tail_mode, sub_delim, trim, pad;
+  unsigned char tail_mode, sub_delim, trim, last_mode;  // last_mode: mode of every line's last field (0: none)
 };
 
 __device__ __forceinline__ bool is_sep(const TokArgs& a, uint8_t c) { return (a.sep[c >> 5] >> (c & 31)) & 1u; }
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(RT) void rec_tokens_kernel(
     while (true) {
       const uint8_t* q = p;
       while (q < e && !is_sep(a, *q)) ++q;
-      const unsigned char m = f < a.nmodes ? a.modes[f] : a.tail_mode;
+      const unsigned char m = (q >= e && a.last_mode) ? a.last_mode : (f < a.nmodes ? a.modes[f] : a.tail_mode);
       const uint8_t* s0 = p;
       const uint8_t* s1 = q;
       if (a.trim) {
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(RT) void rec_gather_kernel(const uint8_t* __restric
 }
 
 TokArgs make_args(const char* delims, int ndelims, const char* modes, int nmodes, char tail_mode, char sub_delim,
-                  bool trim) {
+                  bool trim, char last_mode = 0) {
   TokArgs a{};
   if (nmodes > 64) throw std::runtime_error("device tokenizer: at most 64 per-field modes");
   for (int i = 0; i < ndelims; ++i) {
@@ -292,6 +292,7 @@ TokArgs make_args(const char* delims, int ndelims, const char* modes, int nmodes
   a.tail_mode = (unsigned char)tail_mode;
   a.sub_delim = (unsigned char)sub_delim;
   a.trim = trim ? 1 : 0;
+  a.last_mode = (unsigned char)last_mode;
   return a;
 }
 
@@ -309,11 +310,11 @@ void rec_lines(const uint8_t* bytes, const long long* nlpos, long long nraw, con
 
 void rec_tokens(const uint8_t* bytes, const long long* lstart, const long long* lend, const long long* off, long long L,
                 const char* delims, int ndelims, const char* modes, int nmodes, char tail_mode, char sub_delim,
-                bool trim, unsigned long long* keys, unsigned* h2tab, unsigned long long* first,
+                bool trim, char last_mode, unsigned long long* keys, unsigned* h2tab, unsigned long long* first,
                 unsigned long long mask, int* tslot, unsigned* th2, int* tsub, unsigned* th2sub, double* nums,
                 unsigned* inserted, unsigned* overflow, hipStream_t stream) {
   if (L <= 0) return;
-  const TokArgs a = make_args(delims, ndelims, modes, nmodes, tail_mode, sub_delim, trim);
+  const TokArgs a = make_args(delims, ndelims, modes, nmodes, tail_mode, sub_delim, trim, last_mode);
   rec_tokens_kernel<<<av::stream_grid(L, RT, 1, 8192), RT, 0, stream>>>(bytes, lstart, lend, off, L, a, keys, h2tab,
                                                                          first, mask, tslot, th2, tsub, th2sub, nums,
                                                                          inserted, overflow);

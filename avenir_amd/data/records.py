@@ -74,6 +74,9 @@ class Records:
     line_base: int = 0
     stats: dict = field(default_factory=dict)
     _shard: object = None
+    #: the dictionary's bytes on the device (device tokenizer, single shard): vbytes uint8, voff /
+    #: vlen int64 per entry — string-order sorts of keys then run on the device
+    vbytes: tuple | None = None
 
     @property
     def n_lines(self) -> int:
@@ -190,10 +193,11 @@ class Records:
 # ------------------------------------------------------------------------------------------------
 def read_records(path, *, comm=None, delims: str = ",", sub_delim: str = "", modes: str = "", tail_mode: str = "d",
                  trim: bool = False, numeric: bool = False, device="cpu", skip_header: bool = False,
-                 shard: bool = True) -> Records:
+                 shard: bool = True, last_mode: str = "") -> Records:
     """This rank's :class:`Records` of ``path`` (see the module docstring).  ``comm``: the job's
     communicator (byte-range shard + dictionary merge when distributed); ``shard=False`` reads the
-    whole input on every rank (side files)."""
+    whole input on every rank (side files); ``last_mode``: the mode of every line's last field
+    (e.g. ``'n'`` for a trailing rank / distance of any line width)."""
     paths = input_paths(path)
     dist = comm is not None and comm.is_distributed and shard
     rank, world = (comm.rank, comm.world) if dist else (0, 1)
@@ -205,19 +209,21 @@ def read_records(path, *, comm=None, delims: str = ",", sub_delim: str = "", mod
             total = sum(os.path.getsize(p) for p in paths)
             if total // world >= DEVICE_MIN_BYTES:
                 r = C.text_tokenize_device(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric,
-                                           torch.empty(0, device=dev))
+                                           torch.empty(0, device=dev), 1 << 24, last_mode)
                 if r is not None:
                     off, codes, sub, nums, vocab, stats = r
-                    rec = Records(off, codes, sub, nums, list(vocab), stats=dict(stats, path="device"))
+                    vb = (stats.pop("vbytes"), stats.pop("voff"), stats.pop("vlen"))
+                    rec = Records(off, codes, sub, nums, list(vocab), stats=dict(stats, path="device"), vbytes=vb)
         if rec is None:
             sh = C.TextShard(paths, rank, world, _threads(), skip_header)
-            off, codes, sub, nums, vocab = sh.tokenize(delims, sub_delim, modes, tail_mode, trim, numeric)
+            off, codes, sub, nums, vocab = sh.tokenize(delims, sub_delim, modes, tail_mode, trim, numeric, last_mode)
             rec = Records(off, codes, sub, nums, list(vocab), stats={"path": "host", "bytes": sh.bytes_read()},
                           _shard=sh)
             if dev.type != "cpu":
                 rec = rec.to(dev)
     else:
-        rec = _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header)
+        rec = _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header,
+                               last_mode)
         rec = rec.to(dev) if dev.type != "cpu" else rec
     if dist:
         _merge_vocab(rec, comm)
@@ -234,6 +240,7 @@ def _merge_vocab(rec: Records, comm) -> None:
             if w not in glob:
                 glob[w] = len(glob)
     rec.line_base = sum(n for _, n in parts[: comm.rank])
+    rec.vbytes = None     # the merged dictionary's entries no longer match the shard's bytes
     if rec.vocab:
         lut = torch.tensor([glob[w] for w in rec.vocab], dtype=torch.int32, device=rec.device)
         remap = lambda c: torch.where(c >= 0, lut[c.clamp_min(0).long()], c)
@@ -268,7 +275,8 @@ def _py_lines(paths, rank: int, world: int, skip_header: bool) -> list[str]:
     return out
 
 
-def _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header) -> Records:
+def _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header,
+                     last_mode: str = "") -> Records:
     """Pure-Python twin of the native tokenizers (used when the extension is not built)."""
     import math
     import re
@@ -279,7 +287,7 @@ def _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, tr
     for ln in lines:
         fields = re.split(sep, ln)
         for f, tok in enumerate(fields):
-            m = modes[f] if f < len(modes) else tail_mode
+            m = last_mode if (last_mode and f == len(fields) - 1) else (modes[f] if f < len(modes) else tail_mode)
             if trim:
                 tok = tok.strip(" \t\r\v\f")
             c, s, v = -1, -1, math.nan
@@ -368,11 +376,58 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
 
 # ------------------------------------------------------------------------------------------------
 # keyed (reduce-side) helpers: the MapReduce shuffle as one all-to-all
+_KEY_BYTES = 7          # bytes per non-negative int64 sort word
+_KEY_WORDS = 3         # strings up to 21 bytes sort on the device
+
+
+def _pack_words(b: torch.Tensor, lens: torch.Tensor) -> list[torch.Tensor]:
+    """[n, 21] uint8 (zero padded) -> 3 int64 words, most significant first (big-endian 7-byte
+    groups: non-negative, so signed order = byte order = code-point order of UTF-8 text)."""
+    out = []
+    for w in range(_KEY_WORDS):
+        v = torch.zeros(b.shape[0], dtype=torch.int64, device=b.device)
+        for j in range(_KEY_BYTES):
+            v = v * 256 + b[:, w * _KEY_BYTES + j].long()
+        out.append(v)
+    return out
+
+
+def _string_order(rec: Records, idx: torch.Tensor) -> torch.Tensor | None:
+    """Permutation sorting dictionary entries ``idx`` by their strings, on ``idx``'s device, or
+    None when an entry is longer than 21 bytes (the caller then sorts on the host)."""
+    dev = idx.device
+    W = _KEY_BYTES * _KEY_WORDS
+    if rec.vbytes is not None and rec.vbytes[0].device == dev:
+        vb, vo, vl = rec.vbytes
+        lens = vl[idx]
+        if lens.numel() and int(lens.max()) > W:
+            return None
+        j = torch.arange(W, device=dev)
+        pos = (vo[idx].view(-1, 1) + j).clamp_max(max(0, vb.numel() - 1))
+        b = torch.where(j < lens.view(-1, 1), vb[pos] if vb.numel() else torch.zeros_like(pos, dtype=torch.uint8),
+                        torch.zeros((), dtype=torch.uint8, device=dev))
+    else:
+        enc = [rec.vocab[i].encode() for i in idx.tolist()]
+        if enc and max(len(e) for e in enc) > W:
+            return None
+        import numpy as np
+        arr = np.zeros((len(enc), W), dtype=np.uint8)
+        for r, e in enumerate(enc):
+            arr[r, : len(e)] = np.frombuffer(e, dtype=np.uint8)
+        b = torch.from_numpy(arr).to(dev)
+        lens = None
+    words = _pack_words(b, lens)
+    order = torch.arange(idx.numel(), device=dev)
+    for w in reversed(words):       # LSD: stable sorts from the least significant word
+        order = order[torch.argsort(w[order], stable=True)]
+    return order
+
+
 def sorted_keys(rec: Records, codes: torch.Tensor, comm=None) -> tuple[torch.Tensor, torch.Tensor]:
     """The distinct dictionary codes of ``codes`` over all ranks, ordered by their strings (the
     reducer key order of the reference), and a [V] lookup code -> position in that order (-1).
-    Presence is one all-reduce of a [V] byte mask; the string sort runs once on the host."""
-    import numpy as np
+    Presence is one all-reduce of a [V] byte mask; the string order comes from packed byte keys
+    sorted on the device (a host string sort only for entries longer than 21 bytes)."""
     V = len(rec.vocab)
     dev = codes.device
     present = torch.zeros(max(1, V), dtype=torch.uint8, device=dev)
@@ -381,15 +436,16 @@ def sorted_keys(rec: Records, codes: torch.Tensor, comm=None) -> tuple[torch.Ten
         present[c] = 1
     if comm is not None and comm.is_distributed:
         comm.all_reduce(present, "max")
-    idx = torch.nonzero(present[:V]).view(-1).cpu()
-    if idx.numel():
-        order = np.argsort(np.array([rec.vocab[i] for i in idx.tolist()]), kind="stable")
-        keys = idx[torch.from_numpy(order.astype(np.int64))]
-    else:
-        keys = idx
-    pos = torch.full((max(1, V),), -1, dtype=torch.int64)
-    pos[keys] = torch.arange(keys.numel())
-    return keys.to(dev), pos[:V].to(dev)
+    idx = torch.nonzero(present[:V]).view(-1)
+    order = _string_order(rec, idx) if idx.numel() else idx
+    if order is None:
+        import numpy as np
+        o = np.argsort(np.array([rec.vocab[i] for i in idx.tolist()]), kind="stable")
+        order = torch.from_numpy(o.astype(np.int64)).to(dev)
+    keys = idx[order]
+    pos = torch.full((max(1, V),), -1, dtype=torch.int64, device=dev)
+    pos[keys] = torch.arange(keys.numel(), device=dev)
+    return keys, pos[:V]
 
 
 def owner_of(pos: torch.Tensor, n_keys: int, world: int) -> torch.Tensor:

@@ -233,7 +233,7 @@ def top_matches(args):
     from ..data.table import _literal
     lit = _literal(ctx.delim_in)
     if lit is not None and len(lit) == 1:
-        rec = ctx.records()
+        rec = ctx.records(last_mode="n", numeric=True)     # the trailing rank parsed as a number
         W = rec.width()
         if ctx.comm.is_distributed:
             W = ctx.comm.all_gather_object(W)
@@ -299,7 +299,7 @@ def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact
     rank owning the source entity (entities in string order, contiguous blocks per rank: the
     reference's reducer key order), a device segmented sort on (source, rank) with the global
     input order as tie-break, and the output assembled by the native formatter."""
-    from ..data.records import format_lines, numeric_lut, owner_of, shuffle, sorted_keys
+    from ..data.records import format_lines, owner_of, shuffle, sorted_keys
     comm = ctx.comm
     dev = rec.device
     Lr = (W - 3) // 2
@@ -309,9 +309,7 @@ def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact
     if filt is not None:
         fc = rec.vocab.index(filt) if filt in rec.vocab else -2
         ok &= sc == fc
-    rnum = numeric_lut(rec.vocab, dev)
-    rk = torch.trunc(rnum[M[:, W - 1].clamp_min(0)]) if len(rec.vocab) else torch.zeros(rec.n_lines, device=dev)
-    rk = torch.nan_to_num(rk, nan=float(2 ** 62)).long()
+    rk = torch.nan_to_num(torch.trunc(rec.field(-1, numeric=True)), nan=float(2 ** 62)).long()
     Mo = M[ok]
     rko = rk[ok]
     seq = (torch.nonzero(ok).view(-1) + rec.line_base) * 2

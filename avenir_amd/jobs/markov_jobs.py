@@ -308,6 +308,8 @@ def _state_transition_rate_native(ctx, kords, to, so, states, unit, in_unit, pre
     comp, st = comp[ok], st[ok]
     mult = 1000 if in_unit == "sec" else 1
     tm = torch.trunc(tm_raw[ok]).long() * mult
+    if len(kc) == 1:
+        return _str_single_key(ctx, rec, comp, tm, st, states, unit, prec)
     # global key set in string-tuple order
     loc = torch.unique(comp)
     allk = comm.all_gather_v(loc) if comm.is_distributed else loc
@@ -328,6 +330,25 @@ def _state_transition_rate_native(ctx, kords, to, so, states, unit, in_unit, pre
     key_parts = [skeys] if len(kc) == 1 else [skeys // V, skeys % V]
     cols = [("g", "(")] + [("s", rec.vocab, p.int()) for p in key_parts]
     Qc = Q.reshape(b - a, -1).double().cpu()
+    cols += [("f", Qc[:, j].contiguous(), prec) for j in range(Qc.shape[1])] + [("g", ")")]
+    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
+
+
+def _str_single_key(ctx, rec, key, tm, st, states, unit, prec):
+    """One key field: keys in string order by the device packed-key sort (data/records.sorted_keys)."""
+    from ..data.records import format_lines, owner_of, shuffle, sorted_keys
+    from ..data.table import shard_range
+    from ..models.markov import StateTransitionRate
+    comm = ctx.comm
+    keys, pos = sorted_keys(rec, key, comm)
+    G = keys.numel()
+    kpos = pos[key]
+    owner = owner_of(kpos, G, comm.world) if comm.is_distributed else torch.zeros_like(kpos)
+    kpos, tm, st = shuffle(comm, owner, [kpos, tm, st])
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    Q = StateTransitionRate(len(states)).fit_grouped(kpos - a, tm, st, b - a, _MS[unit])
+    Qc = Q.reshape(b - a, -1).double().cpu()
+    cols = [("g", "("), ("s", rec.vocab, keys[a:b].int().cpu())]
     cols += [("f", Qc[:, j].contiguous(), prec) for j in range(Qc.shape[1])] + [("g", ")")]
     ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
 

@@ -54,6 +54,9 @@ class Comm:
             self.device = torch.device("cpu")
         self.timeout_s = float(timeout_s or os.environ.get("AVENIR_COMM_TIMEOUT", "600"))
         self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        # the process group's real backend; ``backend`` picks the algorithmic path (equal except in
+        # the RCCL emulation of tests: see emulated_rccl)
+        self.pg_backend = self.backend
         self._owns_pg = False
         if self.world > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -69,7 +72,18 @@ class Comm:
         if dist.is_initialized():
             self.world = dist.get_world_size()
             self.rank = dist.get_rank()
+            self.pg_backend = dist.get_backend()
         self.stats = {"calls": 0, "bytes": 0, "seconds": 0.0}
+
+    @classmethod
+    def emulated_rccl(cls, device: str | None = None, **kw) -> "Comm":
+        """A communicator that takes every RCCL-only code path (``backend == "nccl"``: side-stream
+        overlap of the NB all-reduce, device-resident collective buffers) while its process group
+        is gloo — so those paths run in multi-process tests on a CPU host or on ONE GPU shared by
+        several ranks.  Tensors cross the gloo group through host copies (``_prep``)."""
+        c = cls(backend="gloo", device=device, **kw)
+        c.backend = "nccl"
+        return c
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -87,7 +101,7 @@ class Comm:
 
     def _prep(self, t: torch.Tensor) -> tuple[torch.Tensor, bool]:
         """gloo only handles CPU tensors, RCCL only GPU tensors: move if needed."""
-        if self.backend == "gloo" and t.is_cuda:
+        if self.pg_backend == "gloo" and t.is_cuda:
             return t.cpu(), True
         return t, False
 
@@ -173,30 +187,25 @@ class Comm:
         return torch.cat([g[r, : counts[r]] for r in range(self.world)], dim=0)
 
     def all_to_all_v(self, chunks: list[torch.Tensor]) -> list[torch.Tensor]:
-        """Send ``chunks[r]`` to rank r; receive one tensor from every rank (dim-0 variable)."""
+        """Send ``chunks[r]`` to rank r; receive one tensor from every rank (dim-0 variable): one
+        all-to-all of the row counts, one ``all_to_all_single`` of the payload (RCCL over xGMI on
+        GPUs; gloo runs the same call on host copies)."""
         if not self.is_distributed:
             return [chunks[0]]
         dev = chunks[0].device
-        sizes = torch.tensor([c.shape[0] for c in chunks], dtype=torch.long, device=dev)
-        recv_sizes = torch.empty_like(sizes)
-        if self.backend == "gloo":
-            # gloo lacks all_to_all: emulate with all_gather_v of (dest, payload)
-            allsizes = self.all_gather(sizes)  # [world(src), world(dst)]
-            flat = torch.cat(chunks, dim=0)
-            g = self.all_gather_v(flat)
-            out, o = [], 0
-            for src in range(self.world):
-                row = allsizes[src].tolist()
-                start = o + sum(row[: self.rank])
-                out.append(g[start:start + row[self.rank]])
-                o += sum(row)
-            return out
-        dist.all_to_all_single(recv_sizes, sizes)
         tail = tuple(chunks[0].shape[1:])
-        send = torch.cat(chunks, dim=0)
-        recv = torch.empty((int(recv_sizes.sum()),) + tail, dtype=send.dtype, device=dev)
-        dist.all_to_all_single(recv, send, recv_sizes.tolist(), sizes.tolist())
-        return list(torch.split(recv, recv_sizes.tolist()))
+        send, moved = self._prep(torch.cat(chunks, dim=0).contiguous())
+        sizes = torch.tensor([c.shape[0] for c in chunks], dtype=torch.long, device=send.device)
+        recv_sizes = torch.empty_like(sizes)
+        t0 = time.perf_counter()
+        dist.all_to_all_single(recv_sizes, sizes)
+        rs = recv_sizes.tolist()
+        recv = torch.empty((int(sum(rs)),) + tail, dtype=send.dtype, device=send.device)
+        dist.all_to_all_single(recv, send, rs, sizes.tolist())
+        self._account(recv, t0)
+        if moved:
+            recv = recv.to(dev)
+        return list(torch.split(recv, rs))
 
     def ring_pass(self, t: torch.Tensor) -> torch.Tensor:
         """Send ``t`` to rank+1 and receive from rank-1 (systolic all-pairs schedule).  Shapes may
@@ -236,7 +245,7 @@ class Comm:
 
     def barrier(self) -> None:
         if self.is_distributed:
-            if self.backend == "nccl":
+            if self.pg_backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
@@ -244,7 +253,7 @@ class Comm:
     def reduce_max_scalar(self, v: float) -> float:
         if not self.is_distributed:
             return v
-        t = torch.tensor([v], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        t = torch.tensor([v], dtype=torch.float64, device=self.device if self.pg_backend == "nccl" else "cpu")
         self.all_reduce(t, "max")
         return float(t.item())
 

@@ -12,8 +12,13 @@ rounds, SA / GA generations, Apriori levels) runs inside an ``IterationLoop``:
 
 * ``restore()`` returns the last committed iteration's tensors from
   ``<dir>/<algo>.ckpt`` (the CRC-checked container of ``utils/checkpoint``), so a job started
-  fresh after a crash — new processes, possibly a different world size — continues where the
-  previous one stopped and produces the same result as an uninterrupted run;
+  fresh after a crash — new processes — continues where the previous one stopped and produces the
+  same result as an uninterrupted run.  Replicated state (rank 0 writes it; k-means, logistic
+  regression, Apriori) resumes at any world size: it does not depend on the sharding, and every
+  rank loads the same file.  Sharded state (``<algo>.rank<r>.ckpt`` per rank; GBT, SA chains, GA
+  islands) is only valid at the world size that wrote it: ``restore()`` checks the recorded world
+  size and the set of rank files on every rank and refuses a resume at a different world size
+  with :class:`WorldSizeMismatch` instead of letting some ranks resume and others start over;
 * ``step(it)`` wraps one iteration: it beats the ``Watchdog`` (a stalled collective aborts the rank
   with exit code 75 so ``torchrun --max-restarts`` relaunches it), runs the env-driven fault
   injector (``AVMI_FAULT_RANK`` / ``AVMI_FAULT_ITER`` / ``AVMI_FAULT_MODE``) and opens a tracer
@@ -55,6 +60,10 @@ class RecoveryConfig:
                    float(wd) if wd else None)
 
 
+class WorldSizeMismatch(RuntimeError):
+    """A sharded checkpoint was written at a different world size than the resuming job's."""
+
+
 class IterationLoop:
     """Checkpoint / resume + watchdog + fault injection + tracing around one iterative algorithm.
 
@@ -90,13 +99,39 @@ class IterationLoop:
     def restore(self, device=None) -> tuple[int, dict | None, dict | None]:
         """(next_iteration, tensors, meta) of the last committed iteration, or (0, None, None)."""
         p = self.path
-        if p is None or not self.cfg.resume or not p.exists():
+        if p is None or not self.cfg.resume:
+            return 0, None, None
+        if self.sharded:
+            self._check_shard_set()
+        if not p.exists():
             return 0, None, None
         t, m = ckpt.load(p, device or self.device or "cpu")
         if m.get("algorithm") != self.algo:
             raise IOError(f"checkpoint {p} belongs to {m.get('algorithm')!r}, not {self.algo!r}")
+        if self.sharded and int(m.get("world_size", self.comm.world)) != self.comm.world:
+            raise WorldSizeMismatch(f"sharded checkpoint {p} was written at world size {m.get('world_size')}; "
+                                    f"resuming at world size {self.comm.world} would mix resumed and fresh ranks "
+                                    f"(re-run at world size {m.get('world_size')} or clear {self.cfg.directory})")
         self.restored_from = int(m["iteration"])
         return self.restored_from + 1, t, m
+
+    def _check_shard_set(self) -> None:
+        """Every rank sees the same directory: the rank files present must be exactly ranks
+        0..world-1 (or none).  A world-2 checkpoint resumed at world 4 (ranks 2, 3 without a file)
+        or at world 1 (an orphaned rank-1 file) is refused on every rank alike."""
+        d = Path(self.cfg.directory)
+        found = set()
+        pre = f"{self.algo}.rank"
+        if d.is_dir():
+            for f in d.iterdir():
+                if f.name.startswith(pre) and f.name.endswith(".ckpt"):
+                    mid = f.name[len(pre):-len(".ckpt")]
+                    if mid.isdigit():
+                        found.add(int(mid))
+        if found and found != set(range(self.comm.world)):
+            raise WorldSizeMismatch(f"sharded checkpoint of {self.algo!r} has rank files {sorted(found)}; this job "
+                                    f"runs {self.comm.world} ranks (re-run at world size {max(found) + 1} or clear "
+                                    f"{self.cfg.directory})")
 
     @contextlib.contextmanager
     def step(self, it: int, nbytes: float = 0.0, flops: float = 0.0):

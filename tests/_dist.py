@@ -17,13 +17,28 @@ def free_port() -> int:
     return p
 
 
+def _make_comm(kind: str):
+    """``gloo:cpu`` (default), ``gloo:cuda`` (device tensors over a gloo group: ranks share the
+    GPU), ``rccl-emul:cpu`` / ``rccl-emul:cuda`` (Comm.emulated_rccl: the RCCL-only code paths
+    over a gloo group)."""
+    from avenir_amd.parallel import comm as C
+    be, dev = (kind.split(":") + ["cpu"])[:2]
+    c = C.Comm.emulated_rccl(device=dev) if be == "rccl-emul" else C.Comm(backend="gloo", device=dev)
+    if dev == "cuda":   # every rank on the one visible GPU
+        import torch
+        torch.cuda.set_device(0)
+        c.device = torch.device("cuda", 0)
+    C.set_comm(c)
+    return c
+
+
 def _worker(rank, world, port, fn, args, q):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     try:
         from avenir_amd.parallel import comm as C
         C.set_comm(None)
-        c = C.get_comm(device="cpu", backend="gloo")
+        c = _make_comm(os.environ.get("AVMI_TEST_COMM", "gloo:cpu"))
         res = fn(rank, world, *args)
         # pickled by value here: the queue's default tensor pickler shares storage by fd, which
         # breaks when this rank exits before the parent has received it (connection reset)
@@ -34,12 +49,14 @@ def _worker(rank, world, port, fn, args, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def run_world(fn, world: int, *args, timeout: float = 120.0):
-    """Run ``fn(rank, world, *args)`` on ``world`` gloo ranks; return results ordered by rank."""
+def run_world(fn, world: int, *args, timeout: float = 120.0, comm: str = "gloo:cpu"):
+    """Run ``fn(rank, world, *args)`` on ``world`` ranks (``comm``: see _make_comm); return the
+    results ordered by rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_env, args=(r, world, port, fn, args, q, {"AVMI_TEST_COMM": comm}))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = {}

@@ -199,3 +199,26 @@ def test_col_moments_empty_matches_cpu(cuda):
     assert torch.allclose(a, b, equal_nan=True)
     y = torch.full((1, 100), float("nan"))
     assert torch.allclose(E.column_moments(y), E.column_moments(y.to(cuda)).cpu(), equal_nan=True)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_sorted_keys_string_order(tmp_path, dev, monkeypatch):
+    """Reducer key order = Python string order, from packed byte keys (device gather when the
+    device tokenizer kept the dictionary bytes), including multi-byte UTF-8 and > 21-byte keys."""
+    rnd = random.Random(9)
+    alpha = "aAbZ09_é€"
+    keys = {"".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 8))) for _ in range(3000)}
+    keys |= {"k" * 20, "k" * 21, "k" * 20 + "a"}
+    p = tmp_path / "k.txt"
+    p.write_text("\n".join(f"{k},x" for k in sorted(keys, key=lambda _: rnd.random())) + "\n", encoding="utf-8")
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
+    rec = R.read_records(str(p), device=dev, modes="dx")
+    ks, pos = R.sorted_keys(rec, rec.field(0))
+    got = rec.strings(ks)
+    assert got == sorted(k for k in keys if k)  or got == sorted(keys)
+    short = {k for k in keys if len(k.encode()) <= 21}
+    p2 = tmp_path / "k2.txt"
+    p2.write_text("\n".join(f"{k},x" for k in short) + "\n", encoding="utf-8")
+    rec2 = R.read_records(str(p2), device=dev, modes="dx")
+    ks2, _ = R.sorted_keys(rec2, rec2.field(0))
+    assert rec2.strings(ks2) == sorted(short)

@@ -94,3 +94,26 @@ def test_fault_then_fresh_resume_equals_uninterrupted(tmp_path, fn):
     resumed, errs, codes = run_world_outcome(fn, 2, ck)   # fresh processes, same checkpoint dir
     assert not errs and codes == [0, 0], errs
     assert resumed == clean
+
+
+@pytest.mark.parametrize("new_world", [1, 4])
+def test_sharded_resume_at_other_world_size_refused(tmp_path, new_world):
+    """a world-2 sharded checkpoint (GA islands) resumed at world 1 or 4 raises
+    WorldSizeMismatch on every rank instead of silently mixing resumed and fresh ranks."""
+    ck = str(tmp_path / "faulty")
+    res, errs, codes = run_world_outcome(_genetic, 2, ck, env=FAULT, timeout=90)
+    assert codes[1] == 17
+    assert sorted(p.name for p in (tmp_path / "faulty").glob("*.ckpt")) == [
+        "geneticAlgorithm.rank0.ckpt", "geneticAlgorithm.rank1.ckpt"]
+    res, errs, codes = run_world_outcome(_genetic, new_world, ck, timeout=90)
+    assert not res and len(errs) == new_world
+    assert all("WorldSizeMismatch" in e for e in errs.values()), errs
+
+
+def test_replicated_resume_at_other_world_size(tmp_path):
+    """Replicated state (Apriori levels, written by rank 0) resumes at a different world size."""
+    ck = str(tmp_path / "faulty")
+    run_world_outcome(_apriori, 2, ck, env=FAULT, timeout=90)
+    assert (tmp_path / "faulty" / "apriori.ckpt").exists()
+    res, errs, codes = run_world_outcome(_apriori, 4, ck, timeout=90)
+    assert not errs and codes == [0] * 4, errs

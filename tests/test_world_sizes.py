@@ -32,7 +32,7 @@ def _shard(xs, rank, world):
     return xs[rank * n // world:(rank + 1) * n // world]
 
 
-def _all_models(rank, world, churn, hang, seqs, tagged, tx):
+def _all_models(rank, world, churn, hang, seqs, tagged, tx, dev="cpu"):
     from avenir_amd.data.table import load_csv
     from avenir_amd.models import tree as T
     from avenir_amd.models.association import Apriori
@@ -51,7 +51,7 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx):
     out = {}
     # ---- counting models: bit-exact -----------------------------------------------------------
     cs = FeatureSchema.from_json(synth.CHURN_SCHEMA)
-    t = load_csv(churn, cs, rank=rank, world=world)
+    t = load_csv(churn, cs, rank=rank, world=world, device=dev)
     nb = NaiveBayes(cs, comm=comm).fit(t)
     out["nb"] = (nb.counts.tolist(), nb.class_n.tolist())
     mi = MutualInformation(comm=comm)
@@ -59,20 +59,21 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx):
     out["mi"] = sorted((k, round(v, 12)) for k, v in r.feature_class.items())
     out["cramer"] = sorted((k, round(v, 12)) for k, v in categorical_correlation(t, comm=comm).items())
     m = MarkovStateTransitionModel(["0", "1", "2", "3"], comm=comm)
-    m.fit(m.encode(_shard(seqs, rank, world)))
+    m.fit(m.encode(_shard(seqs, rank, world)).to(dev))
     out["markov"] = m.counts.tolist()
     hb = HiddenMarkovModelBuilder(["H", "L"], ["a", "b"], comm=comm)
     ob, st = hb.encode(_shard(tagged, rank, world))
+    ob, st = ob.to(dev), st.to(dev)
     hmm = hb.fit(ob, st)
     out["hmm"] = (hmm.A.tolist(), hmm.B.tolist(), hmm.pi.tolist())
-    pst = ProbabilisticSuffixTree(4, 3).fit(m.encode(_shard(seqs, rank, world)), comm=comm)
+    pst = ProbabilisticSuffixTree(4, 3).fit(m.encode(_shard(seqs, rank, world)).to(dev), comm=comm)
     out["pst"] = [(tok, ch.count) for tok, ch in sorted(pst.root.children.items())]
-    fi = Apriori(0.08, max_len=3, comm=comm).fit_transactions(_shard(tx, rank, world))
+    fi = Apriori(0.08, max_len=3, comm=comm).fit_transactions(_shard(tx, rank, world), device=dev)
     out["apriori"] = sorted((tuple(fi.items[i] for i in s), c) for lvl in fi.levels.values() for s, c in lvl)
     # ---- trees: level-wise builder (data parallel), forest data-parallel and tree-parallel ----
     hs = FeatureSchema.from_json(synth.CALL_HANGUP_SCHEMA)
-    th = load_csv(hang, hs, rank=rank, world=world, raw_numeric=True)
-    full = load_csv(hang, hs, raw_numeric=True)
+    th = load_csv(hang, hs, rank=rank, world=world, raw_numeric=True, device=dev)
+    full = load_csv(hang, hs, raw_numeric=True, device=dev)
     tr = T.DecisionTreeBuilder(hs, T.TreeParams(max_depth=3), comm=comm).fit(th)
     out["tree"] = [(n.predicates, n.population) for n in tr.nodes]
     prm = T.TreeParams(binary=True, stopping="maxDepth", max_depth=4, attr_selection="all", sub_sampling="none")
@@ -86,15 +87,15 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx):
     # ---- float models: tolerance ------------------------------------------------------------
     g = torch.Generator().manual_seed(4)
     X = torch.randn(2000, 3, generator=g) + torch.randint(0, 3, (2000, 1), generator=g) * 6.0
-    km = KMeans(3, seed=5, comm=comm).fit(_shard(X, rank, world))
+    km = KMeans(3, seed=5, comm=comm).fit(_shard(X, rank, world).to(dev))
     out["kmeans"] = float(km.best[3].sse)
     w = torch.tensor([1.0, -2.0, 0.5])
     y = ((X @ w + 2.0 * torch.randn(2000, generator=g)) > 0).double()     # non-separable: finite optimum
-    lr = LogisticRegression(max_iter=10).fit(_shard(X, rank, world), _shard(y, rank, world))
+    lr = LogisticRegression(max_iter=10).fit(_shard(X, rank, world).to(dev), _shard(y, rank, world).to(dev))
     out["logit"] = lr.coef.tolist()
     Q = torch.randn(64, 3, generator=g)
     lo = rank * 2000 // world
-    d, i = D.distributed_knn(Q, _shard(X, rank, world).contiguous(), 5, comm, r_base=lo)
+    d, i = D.distributed_knn(Q.to(dev), _shard(X, rank, world).contiguous().to(dev), 5, comm, r_base=lo)
     out["knn"] = (d.tolist(), i.tolist())
     # ---- cascade SVM (same global shard partition at every world size), Relief, GBT -----------
     from avenir_amd.models.sampling import relief
@@ -102,12 +103,13 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx):
     gs = torch.Generator().manual_seed(12)
     Xs = torch.randn(640, 2, generator=gs)
     ys = (Xs[:, 0] * Xs[:, 1] > 0).long()
-    cs_ = CascadeSVM(shards=8 // world, comm=comm, gamma=0.5, C=1.0).fit(_shard(Xs, rank, world), _shard(ys, rank, world))
+    cs_ = CascadeSVM(shards=8 // world, comm=comm, gamma=0.5, C=1.0).fit(_shard(Xs, rank, world).to(dev),
+                                                                       _shard(ys, rank, world).to(dev))
     probe = torch.randn(64, 2, generator=gs)
-    out["cascade"] = (cs_.n_cascade_sv, cs_.decision_function(probe).tolist())
+    out["cascade"] = (cs_.n_cascade_sv, cs_.decision_function(probe.to(dev)).tolist())
     Xr = torch.randn(600, 5, generator=gs)
     yr = ((Xr[:, 0] + 0.5 * Xr[:, 3]) > 0).long()
-    out["relief"] = relief(_shard(Xr, rank, world), _shard(yr, rank, world), k=2, comm=comm).tolist()
+    out["relief"] = relief(_shard(Xr, rank, world).to(dev), _shard(yr, rank, world).to(dev), k=2, comm=comm).tolist()
     gbt = T.GradientBoostedTrees(hs, T.GBTParams(n_estimators=6, max_depth=3, max_bins=32), comm=comm).fit(th)
     out["gbt"] = gbt.decision_function(full).tolist()
     # ---- sequence parallel Viterbi -----------------------------------------------------------
@@ -117,7 +119,7 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx):
     lB = norm(torch.rand(5, 4, generator=gh, dtype=torch.float64) + 0.05)
     lp = norm(torch.rand(5, generator=gh, dtype=torch.float64) + 0.05)
     obs = torch.randint(0, 4, (1601,), generator=gh).to(torch.int16)
-    path, score = SO.viterbi_long(_shard(obs, rank, world), lA, lB, lp, chunk=64)
+    path, score = SO.viterbi_long(_shard(obs, rank, world).to(dev), lA.to(dev), lB.to(dev), lp.to(dev), chunk=64)
     out["viterbi"] = (path.tolist(), round(float(score), 6))
     return out
 
@@ -128,10 +130,7 @@ def reference():
     return args, run_world(_all_models, 1, *args, timeout=300)[0]
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_world_size_equivalence(reference, world):
-    args, ref = reference
-    res = run_world(_all_models, world, *args, timeout=600)
+def _compare(res, ref, world):
     for r, got in enumerate(res):
         for key in ("nb", "mi", "cramer", "markov", "hmm", "pst", "apriori", "tree", "forest_dp", "forest_tp"):
             assert got[key] == ref[key], f"rank {r}/{world}: {key} differs"
@@ -146,6 +145,33 @@ def test_world_size_equivalence(reference, world):
         assert np.allclose(got["gbt"], ref["gbt"], rtol=1e-6, atol=1e-6)
     # Viterbi is sequence-parallel: the rank segments concatenate to the single-rank path
     assert sum((g["viterbi"][0] for g in res), []) == ref["viterbi"][0]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_world_size_equivalence(reference, world):
+    args, ref = reference
+    res = run_world(_all_models, world, *args, timeout=600)
+    _compare(res, ref, world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_world_size_equivalence_emulated_rccl(reference, world):
+    """The RCCL-only code paths (backend == "nccl": device collective buffers, all_to_all_single,
+    batched P2P ring) over a gloo group on the CPU."""
+    args, ref = reference
+    _compare(run_world(_all_models, world, *args, timeout=600, comm="rccl-emul:cpu"), ref, world)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("comm", ["gloo:cuda", "rccl-emul:cuda"])
+def test_world_size_equivalence_device_tensors(comm):
+    """Every model of the set with DEVICE tensors at world 2 and 4: separate rank processes sharing
+    cuda:0 (the HIP kernels under row sharding, the _prep copy path, and with rccl-emul the NB
+    side-stream all-reduce overlap), against the same set at world 1 on the device."""
+    args = _data()
+    ref = run_world(_all_models, 1, *args, "cuda", timeout=600, comm=comm)[0]
+    for world in (2, 4):
+        _compare(run_world(_all_models, world, *args, "cuda", timeout=600, comm=comm), ref, world)
 
 
 def _cli_ranks(rank, world, data, schema, model, out_dir, out_file):
