@@ -565,46 +565,104 @@ class DecisionTreeBuilder:
 
     # -- build ---------------------------------------------------------------------------------
     def fit(self, t: Table, tree_seed: int | None = None, codes: torch.Tensor | None = None) -> DecisionTree:
-        import time
+        """One tree over this rank's rows (``sub.sampling`` weights from a seeded generator)."""
         comm = self.comm or get_comm()
         p = self.p
         seed = p.seed if tree_seed is None else tree_seed
-        rng = random.Random(seed)  # identical on every rank
         if self.space is None:
             self.space = build_split_space(self.schema, t, binary=p.binary, max_bins=p.max_bins, comm=comm)
-        space = self.space
         if codes is None:
-            codes = encode_for_tree(space, t)
-        # one constant extra row (code 0 for every real row): its single bin is the node total
-        codes = _with_total_row(codes, t.n)
+            codes = encode_for_tree(self.space, t)
+        node0 = torch.full((t.ld,), -1, dtype=torch.int32, device=t.device)
+        node0[: t.n] = 0
+        cls = list(t.class_field.cardinality) if t.class_field else ["_"]
+        return self._grow(_with_total_row(codes, t.n), t.n, t.labels, self._weights(t, seed), node0,
+                          [random.Random(seed)], t.n_classes, cls)[0]
+
+    def fit_many(self, t: Table, seeds: Sequence[int], codes: torch.Tensor | None = None) -> list[DecisionTree]:
+        """Several trees at once (a random forest with the reference's split semantics: multi-way
+        numeric splits, categorical set partitions, ``notUsedYet`` / ``randomNotUsedYet``): every
+        tree's bootstrap sample is a contiguous block of one row buffer (forest.hip bootstrap kernels:
+        multiplicity = f(seed, tree, GLOBAL row), so samples do not depend on the device or the
+        world size), every level of ALL trees is one histogram launch, one scoring pass and one
+        host copy.  Tree i uses ``seeds[i]`` for its bootstrap and its attribute / split draws, so
+        it equals the tree a one-tree build with that seed and sample would give."""
+        from ..ops import forest_ops as FO
+        comm = self.comm or get_comm()
+        p = self.p
+        if self.space is None:
+            self.space = build_split_space(self.schema, t, binary=p.binary, max_bins=p.max_bins, comm=comm)
+        if codes is None:
+            codes = encode_for_tree(self.space, t)
+        if p.sub_sampling not in FO.BOOT_MODES:
+            raise ValueError(f"unknown sub sampling strategy {p.sub_sampling}")
+        mode = FO.BOOT_MODES[p.sub_sampling]
+        rate32 = min(int(min(max(p.sampling_rate, 0.0), 100.0) / 100.0 * 4294967296.0), 0xFFFFFFFF)
+        keys = np.asarray([((s * 1000003 + 17) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF for s in seeds],
+                          dtype=np.uint64).view(np.int64)
+        dev = t.device
+        cb, lb, wb, cnt = FO.forest_bootstrap(codes.contiguous(), t.labels.to(dev).contiguous(), t.n, keys,
+                                              t.row_offset, mode, rate32)
+        cnt_h = [int(x) for x in cnt.tolist()]
+        R = sum(cnt_h)
+        node0 = torch.full((cb.shape[1],), -1, dtype=torch.int32, device=dev)
+        if R:
+            node0[:R] = torch.repeat_interleave(torch.arange(len(seeds), dtype=torch.int32, device=dev),
+                                                torch.tensor(cnt_h, device=dev))
+        cls = list(t.class_field.cardinality) if t.class_field else ["_"]
+        return self._grow(_with_total_row(cb, R), R, lb, wb, node0, [random.Random(s) for s in seeds],
+                          t.n_classes, cls)
+
+    def _grow(self, codes: torch.Tensor, n: int, labels: torch.Tensor, weight: torch.Tensor | None,
+              node: torch.Tensor, rngs: list, C: int, cls: list[str]) -> list[DecisionTree]:
+        """Level-wise growth of ``len(rngs)`` trees whose rows are marked by ``node`` (row -> root
+        slot = tree index, -1 = unused).  Per level, for every frontier node of every tree: ONE
+        histogram launch (children whose parent is fully covered are derived by subtraction), the
+        scores of every candidate split of every attribute as batched device tensor math, the
+        segment counts of the chosen (or top-k) splits gathered on the device, and ONE host copy.
+        The host then only creates node objects."""
+        import time
+        comm = self.comm or get_comm()
+        p = self.p
+        space = self.space
         F = len(space)
         bins = [fs.n_bins for fs in space] + [1]
         offs = list(itertools.accumulate([0] + bins[:-1]))
-        C = t.n_classes
-        dev = t.device
-        labels = t.labels
-        weight = self._weights(t, seed)
+        TBt = offs[F] + 1
+        dev = codes.device
+        NT = len(rngs)
 
-        # segment-assignment tensors per feature (explicit splits)
-        seg_tensors = []
-        for fs in space:
-            if fs.binary:
-                seg_tensors.append(None)
-                continue
+        # ---- explicit (multi-way / categorical partition) splits of every feature, once ----------
+        nb_f = [f for f, fs in enumerate(space) if not fs.binary and len(fs.splits)]
+        Gmax = max([s.n_seg for f in nb_f for s in space[f].splits] + [2])
+        Bmax = max([space[f].n_bins for f in nb_f] + [1])
+        seg_tensors = {}
+        nb_rows = []                              # (feature, split) of every explicit split, in order
+        for f in nb_f:
+            fs = space[f]
             S = len(fs.splits)
-            G = max((s.n_seg for s in fs.splits), default=1)
-            M = torch.zeros((S, G, fs.n_bins), dtype=torch.float64)
+            M = torch.zeros((S, Gmax, fs.n_bins), dtype=torch.float64)
             for si, sp in enumerate(fs.splits):
                 for b, g in enumerate(sp.segmap):
                     M[si, g, b] = 1.0
-            seg_tensors.append(M.to(dev))
+            seg_tensors[f] = M.to(dev)
+            nb_rows += [(f, s) for s in range(S)]
+        if nb_rows:
+            # per explicit split: its [Gmax, Bmax] segment map and the histogram column of each bin
+            # (TBt = an all-zero column appended for the padding bins)
+            allseg = torch.zeros((len(nb_rows), Gmax, Bmax), dtype=torch.float64)
+            splitcol = torch.full((len(nb_rows), Bmax), TBt, dtype=torch.long)
+            for r, (f, s) in enumerate(nb_rows):
+                B = space[f].n_bins
+                allseg[r, :, :B] = seg_tensors[f][s].cpu()
+                splitcol[r, :B] = torch.arange(offs[f], offs[f] + B)
+            allseg, splitcol = allseg.to(dev), splitcol.to(dev)
 
         # binary-threshold features are scored together: one segmented cumsum over their bins
         bin_f = [f for f, fs in enumerate(space) if fs.binary]
         if bin_f:
             bcols = torch.cat([torch.arange(offs[f], offs[f] + bins[f]) for f in bin_f]).to(dev)
             bfeat = torch.cat([torch.full((bins[f],), f, dtype=torch.long) for f in bin_f]).to(dev)
-            # position of each bin's feature start / end inside the gathered block
             starts, pos = [], 0
             for f in bin_f:
                 starts.append(pos)
@@ -614,31 +672,34 @@ class DecisionTreeBuilder:
                               for f, st in zip(bin_f, starts)]).to(dev)
             bthr = torch.cat([torch.arange(bins[f]) for f in bin_f]).to(dev)      # threshold index within feature
             bvalid = bthr < torch.cat([torch.full((bins[f],), bins[f] - 1) for f in bin_f]).to(dev)
+        NBc = int(bcols.numel()) if bin_f else 0
+        # score column -> (feature, split): binary block first, then the explicit splits
+        index: list[tuple[int, int]] = (list(zip(bfeat.tolist(), bthr.tolist())) if bin_f else []) + nb_rows
 
-        node = torch.full((t.ld,), -1, dtype=torch.int32, device=dev)
-        node[: t.n] = 0
-        # root
-        root_hist = T.node_histogram(codes, t.n, labels, node, weight, bins, C, 1)
+        # ---- roots: one histogram launch for every tree ------------------------------------------
+        hist = T.node_histogram(codes, n, labels, node, weight, bins, C, NT)
         if comm.is_distributed:
-            comm.all_reduce(root_hist)
-        rc = root_hist[0, :, offs[F]]
-        pop = int(rc.sum())
-        root = Node([], pop, float(impurity(rc.unsqueeze(0), p.algorithm)[0]),
-                    (rc.double() / max(pop, 1)).tolist(), depth=0)   # depth = #predicates on the path
-        nodes = [root]
-        frontier = [0]  # global node indices of the active frontier (local index = position)
-        hist = root_hist  # [A, C, TB] of the frontier; later levels: built + derived by subtraction
+            comm.all_reduce(hist)
+        rc_all = hist[:, :, offs[F]].cpu()
+        nodes: list[Node] = []
+        tree_of: list[int] = []
+        for ti in range(NT):
+            rc = rc_all[ti]
+            pop = int(rc.sum())
+            nodes.append(Node([], pop, float(impurity(rc.unsqueeze(0), p.algorithm)[0]),
+                              (rc.double() / max(pop, 1)).tolist(), depth=0))   # depth = #predicates
+            tree_of.append(ti)
+        frontier = list(range(NT))   # global node indices; position = histogram slot
         while frontier:
             t0 = time.perf_counter()
             A = len(frontier)
-            hist_t = hist.transpose(1, 2).double()  # [A, TB, C]
-            # ---- score every candidate split of every attribute, all nodes at once ----
-            cand_masks = torch.zeros((A, F), dtype=torch.bool)
+            hist_t = hist.transpose(1, 2).double()                     # [A, TB, C]
+            # ---- candidate attributes (per-tree RNG streams, frontier order) ----
+            cand = np.zeros((A, F), dtype=bool)
             for a, gi in enumerate(frontier):
-                for f in self._candidate_attrs(nodes[gi], F, rng):
-                    cand_masks[a, f] = True
-            cand_masks = cand_masks.to(dev)
-            score_blocks, index = [], []  # index: (feature, split id)
+                cand[a, self._candidate_attrs(nodes[gi], F, rngs[tree_of[gi]])] = True
+            cand_masks = torch.from_numpy(cand).to(dev)
+            score_blocks = []
             if bin_f:
                 hb = hist_t[:, bcols, :]                                    # [A, NB, C]
                 cs = torch.cumsum(hb, 1)
@@ -652,114 +713,108 @@ class DecisionTreeBuilder:
                 wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)
                 ok = ((cnt > 0).sum(-1) >= 2) & bvalid.view(1, -1) & cand_masks[:, bfeat]
                 score_blocks.append(torch.where(ok, wavg, torch.full_like(wavg, math.inf)))
-                index.extend(zip(bfeat.tolist(), bthr.tolist()))
-            for f, fs in enumerate(space):
-                hb = hist_t[:, offs[f]: offs[f] + bins[f], :]     # [A, B, C]
-                if fs.binary:
-                    continue
-                else:
-                    M = seg_tensors[f]
-                    if M.shape[0] == 0:
-                        continue
-                    seg = torch.einsum("sgb,abc->asgc", M, hb)      # [A, S, G, C]
-                    ns = M.shape[0]
-                cnt = seg.sum(-1)                                   # [A, S, G]
-                stat = impurity(seg, p.algorithm)                   # [A, S, G]
-                wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)   # [A, S]
-                nonempty = (cnt > 0).sum(-1) >= 2                   # a split must separate rows
-                wavg = torch.where(nonempty & cand_masks[:, f:f + 1], wavg,
-                                   torch.full_like(wavg, math.inf))
-                score_blocks.append(wavg)
-                index.extend((f, s) for s in range(ns))
+            for f in nb_f:
+                hb = hist_t[:, offs[f]: offs[f] + bins[f], :]               # [A, B, C]
+                seg = torch.einsum("sgb,abc->asgc", seg_tensors[f], hb)     # [A, S, G, C]
+                cnt = seg.sum(-1)
+                stat = impurity(seg, p.algorithm)
+                wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)     # [A, S]
+                nonempty = (cnt > 0).sum(-1) >= 2                           # a split must separate rows
+                score_blocks.append(torch.where(nonempty & cand_masks[:, f:f + 1], wavg,
+                                                torch.full_like(wavg, math.inf)))
             if not score_blocks:
                 break
-            scores = torch.cat(score_blocks, 1)                     # [A, S_total]
-            if p.split_selection == "randomAmongTop":
-                k = min(p.top_split_count, scores.shape[1])
-                top = torch.topk(scores, k, dim=1, largest=False).indices.cpu()
-                topv = torch.gather(scores, 1, top.to(dev)).cpu()
-                choice = []
-                for a in range(A):
-                    fin = [i for i in range(k) if math.isfinite(float(topv[a, i]))]
-                    choice.append(int(top[a, rng.choice(fin)]) if fin else -1)
-                best = torch.tensor(choice)
-                best_val = torch.tensor([float(scores[a, c]) if c >= 0 else math.inf
-                                         for a, c in enumerate(choice)])
+            scores = torch.cat(score_blocks, 1)                             # [A, S_total]
+            k = min(p.top_split_count, scores.shape[1]) if p.split_selection == "randomAmongTop" else 1
+            if k == 1:
+                tv, ti_ = scores.min(1)
+                top, topv = ti_.view(A, 1), tv.view(A, 1)
             else:
-                best_val, best = scores.min(1)
-                best, best_val = best.cpu(), best_val.cpu()
-            # segment counts of the chosen splits (binary: one gather for every node, one copy)
-            seg_counts: list = [None] * A
-            bvals = best_val.tolist()
-            bidx = best.tolist()
-            bin_rows = [a for a in range(A) if math.isfinite(bvals[a]) and space[index[bidx[a]][0]].binary]
-            if bin_rows:
-                ra = torch.tensor(bin_rows, device=dev)
-                cols = torch.tensor([bidx[a] for a in bin_rows], device=dev)       # position in the binary block
-                ch = bseg[ra, cols].round().long().cpu()                          # [R, 2, C]
-                for j, a in enumerate(bin_rows):
-                    seg_counts[a] = ch[j]
+                top = torch.topk(scores, k, dim=1, largest=False).indices
+                topv = torch.gather(scores, 1, top)
+            # segment class counts of every top candidate, on the device: [A, k, Gmax', C]
+            G2 = max(Gmax, 2)
+            segc = torch.zeros((A, k, G2, C), dtype=torch.float64, device=dev)
+            if bin_f:
+                isb = top < NBc
+                bsel = bseg[torch.arange(A, device=dev).view(-1, 1).expand(A, k), top.clamp_max(NBc - 1)]
+                segc[:, :, :2] = torch.where(isb.view(A, k, 1, 1), bsel, segc[:, :, :2])
+            if nb_rows:
+                isn = top >= NBc
+                r = (top - NBc).clamp(0, len(nb_rows) - 1)
+                hpad = torch.cat([hist_t, torch.zeros((A, 1, C), dtype=hist_t.dtype, device=dev)], 1)
+                cols = splitcol[r]                                          # [A, k, Bmax]
+                hsel = torch.gather(hpad, 1, cols.view(A, -1, 1).expand(-1, -1, C)).view(A, k, Bmax, C)
+                nsel = torch.einsum("akgb,akbc->akgc", allseg[r], hsel)
+                segc[:, :, :Gmax] = torch.where(isn.view(A, k, 1, 1), nsel, segc[:, :, :Gmax])
+            # ---- the ONE host copy of the level ----
+            flat = torch.cat([top.double().view(-1), topv.double().view(-1), segc.round().view(-1)]).cpu()
+            top_h = flat[: A * k].long().view(A, k).tolist()
+            topv_h = flat[A * k: 2 * A * k].view(A, k).tolist()
+            segc_h = flat[2 * A * k:].view(A, k, G2, C).long()
+            # ---- choose (randomAmongTop: per-tree RNG among the finite top-k) ----
+            pick = [-1] * A
             for a in range(A):
-                if math.isfinite(bvals[a]) and seg_counts[a] is None:
-                    f, s = index[bidx[a]]
-                    hb = hist_t[a, offs[f]: offs[f] + bins[f], :]
-                    seg_counts[a] = torch.einsum("gb,bc->gc", seg_tensors[f][s], hb).round().long().cpu()
+                if k == 1:
+                    pick[a] = 0 if math.isfinite(topv_h[a][0]) else -1
+                else:
+                    fin = [i for i in range(k) if math.isfinite(topv_h[a][i])]
+                    pick[a] = rngs[tree_of[frontier[a]]].choice(fin) if fin else -1
             # ---- create children ----
             new_frontier: list[int] = []
             derived: list[tuple[int, int, list[int]]] = []   # (global child, parent slot, built sibling gis)
             max_bins = max(bins)
-            max_seg = 2
-            for a in range(A):
-                if seg_counts[a] is not None:
-                    max_seg = max(max_seg, seg_counts[a].shape[0])
+            max_seg = G2
             split_feat = torch.full((A,), -1, dtype=torch.int32)
             segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
             child_of = torch.full((A, max_seg), -1, dtype=torch.int32)
             for a, gi in enumerate(frontier):
                 nd = nodes[gi]
-                sc = seg_counts[a]
-                if sc is None:
+                if pick[a] < 0:
                     nd.stopped = True
                     continue
-                f, s = index[int(best[a])]
+                f, s = index[top_h[a][pick[a]]]
                 fs = space[f]
                 if fs.binary:
                     sm = [0 if b <= s else 1 for b in range(fs.n_bins)]
-                    pv = fs.points[s] if fs.kind == "num" else s
                     o = fs.field.ordinal
                     if fs.kind == "num":
-                        preds = [f"{o} le {fs.pred_value(pv)}", f"{o} gt {fs.pred_value(pv)}"]
+                        pv = fs.pred_value(fs.points[s])
+                        preds = [f"{o} le {pv}", f"{o} gt {pv}"]
                     else:
                         card = fs.field.cardinality
                         preds = [f"{o} in {':'.join(card[: s + 1])}", f"{o} in {':'.join(card[s + 1:])}"]
+                    ng = 2
                 else:
                     sp = fs.splits[s]
-                    sm, preds = sp.segmap, sp.predicates
+                    sm, preds, ng = sp.segmap, sp.predicates, sp.n_seg
+                sc = segc_h[a, pick[a], :ng]
                 nd.feature, nd.split, nd.segmap = f, s, list(sm)
                 nd.children = []
                 split_feat[a] = f
                 segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
                 kids = []
-                for g in range(sc.shape[0]):
-                    cnt = sc[g]
-                    pop = int(cnt.sum())
+                for g in range(ng):
+                    cntg = sc[g]
+                    pop = int(cntg.sum())
                     if pop == 0:
                         nd.children.append(-1)
                         continue
-                    info = float(impurity(cnt.unsqueeze(0), p.algorithm)[0])
+                    info = float(impurity(cntg.unsqueeze(0), p.algorithm)[0])
                     depth = nd.depth + 1   # parentPredicates.size() + 1 (DecisionTreeBuilder.java:606)
                     stop = self._should_stop(pop, info, nd.info, depth) or info == 0.0
-                    child = Node(nd.predicates + [preds[g]], pop, info, (cnt.double() / pop).tolist(),
+                    child = Node(nd.predicates + [preds[g]], pop, info, (cntg.double() / pop).tolist(),
                                  depth, stopped=stop, used_attrs=nd.used_attrs | {f})
                     ci = len(nodes)
                     nodes.append(child)
+                    tree_of.append(tree_of[gi])
                     nd.children.append(ci)
                     kids.append((g, ci, pop, stop))
                 # histogram subtraction: when every row of the parent lands in a frontier child, the
                 # most populated child's histogram is the parent's minus its built siblings'
-                live = [k for k in kids if not k[3]]
-                whole = sum(k[2] for k in kids) == nd.population and len(live) == len(kids) and len(live) >= 2
-                heavy = max(live, key=lambda k: k[2])[1] if whole else -1
+                live = [kk for kk in kids if not kk[3]]
+                whole = sum(kk[2] for kk in kids) == nd.population and len(live) == len(kids) and len(live) >= 2
+                heavy = max(live, key=lambda kk: kk[2])[1] if whole else -1
                 for g, ci, _, stop in kids:
                     if not stop and ci != heavy:
                         child_of[a, g] = len(new_frontier)
@@ -767,27 +822,42 @@ class DecisionTreeBuilder:
                 if heavy >= 0:
                     derived.append((heavy, a, [ci for _, ci, _, _ in live if ci != heavy]))
             # derived children take the ids after the built ones: the histogram pass skips their rows
-            slot = {ci: k for k, ci in enumerate(new_frontier)}
+            slot = {ci: j for j, ci in enumerate(new_frontier)}
             m = len(new_frontier)
             for j, (ci, a, _) in enumerate(derived):
                 g = nodes[frontier[a]].children.index(ci)
                 child_of[a, g] = m + j
-            T.tree_assign(codes, t.n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
+            T.tree_assign(codes, n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
             if new_frontier or derived:
-                hs = T.node_histogram(codes, t.n, labels, node, weight, bins, C, m)   # built children only
+                hs = T.node_histogram(codes, n, labels, node, weight, bins, C, m)   # built children only
                 if comm.is_distributed:
                     comm.all_reduce(hs)
                 parts = [hs]
-                for ci, a, sibs in derived:
-                    dh = hist[a].clone()
-                    for sg in sibs:
-                        dh -= hs[slot[sg]]
-                    parts.append(dh.unsqueeze(0))
+                if derived:
+                    pa = torch.tensor([a for _, a, _ in derived], device=dev)
+                    dh = hist[pa].clone()
+                    for j, (ci, a, sibs) in enumerate(derived):
+                        for sg in sibs:
+                            dh[j] -= hs[slot[sg]]
+                    parts.append(dh)
                 hist = torch.cat(parts) if len(parts) > 1 else hs
             frontier = new_frontier + [ci for ci, _, _ in derived]
             self.level_times.append(time.perf_counter() - t0)
-        cls = t.class_field.cardinality if t.class_field else ["_"]
-        return DecisionTree(nodes, space, list(cls))
+        # ---- split the node list into one DecisionTree per tree (children re-indexed) ----
+        per_tree: list[list[int]] = [[] for _ in range(NT)]
+        for g, ti in enumerate(tree_of):
+            per_tree[ti].append(g)
+        out = []
+        for ti in range(NT):
+            gids = per_tree[ti]
+            local = {g: j for j, g in enumerate(gids)}
+            tn = []
+            for g in gids:
+                nd = nodes[g]
+                nd.children = [local[c] if c >= 0 else -1 for c in nd.children]
+                tn.append(nd)
+            out.append(DecisionTree(tn, space, list(cls)))
+        return out
 
 
 # ================================================================================================
@@ -959,13 +1029,15 @@ class RandomForest:
             trees = fb.fit(t, space=space, codes=codes, tree_ids=list(my_trees))
             self.build_stats = fb.stats
             my_trees = []
-        for i in my_trees:
+        if list(my_trees):
+            # the reference's split semantics (multi-way numeric, categorical partitions,
+            # notUsedYet): every tree of this rank grown together by the level-wise builder
             p = copy.copy(self.params)
             p.random_attr_count = self._k(len(space))
-            p.seed = self.params.seed * 7919 + i
             b = DecisionTreeBuilder(self.schema, p, comm=_LocalComm() if self.tree_parallel else comm,
                                     space=space)
-            trees.append(b.fit(t, tree_seed=p.seed, codes=codes))
+            trees = b.fit_many(t, [self.params.seed * 7919 + i for i in my_trees], codes=codes)
+            self.build_stats = {"levels": len(b.level_times), "seconds": sum(b.level_times)}
         if self.tree_parallel and comm.is_distributed:
             states = comm.all_gather_object([tr.state() for tr in trees])
             allt = {}

@@ -281,3 +281,44 @@ def test_node_histogram_kernels_match_oracle(cuda):
     ref = TO.node_grad_histogram(codes, n, node, gr, hs, bins, A)
     got = TO.node_grad_histogram(codes.to(cuda), n, node.to(cuda), gr.to(cuda), hs.to(cuda), bins, A)
     assert torch.equal(got.cpu(), ref)
+
+
+# ------------------------------------------------------------------------------------------------
+# batched reference-semantics forest (DecisionTreeBuilder.fit_many)
+def _tree_sig(tr):
+    return [(n.predicates, n.population, n.children) for n in tr.nodes]
+
+
+REF_PARAMS = dict(stopping="maxDepth", max_depth=3, sub_sampling="withReplace", attr_selection="randomNotUsedYet",
+                  random_attr_count=3, split_selection="randomAmongTop", top_split_count=3)
+
+
+def test_fit_many_equals_one_tree_builds(tmp_path):
+    """Every tree of a batched build equals the tree built alone with its seed (the batch shares
+    launches, not random streams), multi-way numeric + categorical partition splits."""
+    _, schema, t = _hangup(tmp_path, 4000, seed=3)
+    for f in schema.feature_fields:
+        f.max_split = 3                        # up to 3-way splits (SplitManager maxSplit)
+    seeds = [11, 12, 13, 14]
+    many = DecisionTreeBuilder(schema, TreeParams(**REF_PARAMS)).fit_many(t, seeds)
+    for s, tr in zip(seeds, many):
+        one = DecisionTreeBuilder(schema, TreeParams(**REF_PARAMS)).fit_many(t, [s])[0]
+        assert _tree_sig(tr) == _tree_sig(one)
+    assert any(len(n.children) > 2 for tr in many for n in tr.nodes)   # multi-way splits occur
+
+
+def test_reference_forest_uses_batched_builder(tmp_path):
+    _, schema, t = _hangup(tmp_path, 3000, seed=4)
+    rf = RandomForest(schema, 5, TreeParams(**REF_PARAMS), "all").fit(t)
+    assert len(rf.trees) == 5 and rf.build_stats["levels"] >= 1
+    assert float((rf.predict(t) == t.labels[: t.n].long()).float().mean()) > 0.6
+
+
+@pytest.mark.gpu
+def test_fit_many_gpu_equals_cpu(cuda, tmp_path):
+    _, schema, t = _hangup(tmp_path, 60_000, seed=5)
+    for extra in ({}, {"algorithm": "entropy", "split_selection": "best", "attr_selection": "notUsedYet"}):
+        prm = dict(REF_PARAMS, **extra)
+        cpu = DecisionTreeBuilder(schema, TreeParams(**prm)).fit_many(t, [1, 2, 3])
+        gpu = DecisionTreeBuilder(schema, TreeParams(**prm)).fit_many(t.to(cuda), [1, 2, 3])
+        assert [_tree_sig(x) for x in gpu] == [_tree_sig(x) for x in cpu]

@@ -84,6 +84,11 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx, dev="cpu"):
                                             sub_sampling="withReplace", attr_selection="randomAll", seed=3),
                         "sqrt", comm=comm, tree_parallel=True).fit(full)
     out["forest_tp"] = [[(n.predicates, n.population) for n in x.nodes] for x in rf.trees]
+    # reference split semantics (multi-way numeric, categorical partitions, notUsedYet), data parallel
+    rr = T.RandomForest(hs, 3, T.TreeParams(stopping="maxDepth", max_depth=3, sub_sampling="withReplace",
+                                            attr_selection="randomNotUsedYet", random_attr_count=3, seed=5),
+                        "all", comm=comm).fit(th)
+    out["forest_ref"] = [[(n.predicates, n.population) for n in x.nodes] for x in rr.trees]
     # ---- float models: tolerance ------------------------------------------------------------
     g = torch.Generator().manual_seed(4)
     X = torch.randn(2000, 3, generator=g) + torch.randint(0, 3, (2000, 1), generator=g) * 6.0
@@ -130,15 +135,16 @@ def reference():
     return args, run_world(_all_models, 1, *args, timeout=300)[0]
 
 
-def _compare(res, ref, world):
+def _compare(res, ref, world, score_rel=1e-9):
     for r, got in enumerate(res):
-        for key in ("nb", "mi", "cramer", "markov", "hmm", "pst", "apriori", "tree", "forest_dp", "forest_tp"):
+        for key in ("nb", "mi", "cramer", "markov", "hmm", "pst", "apriori", "tree", "forest_dp", "forest_tp",
+                    "forest_ref"):
             assert got[key] == ref[key], f"rank {r}/{world}: {key} differs"
         assert got["kmeans"] == pytest.approx(ref["kmeans"], rel=1e-5)
         assert np.allclose(got["logit"], ref["logit"], rtol=1e-7, atol=1e-9)
         assert np.allclose(got["knn"][0], ref["knn"][0], atol=1e-5)
         assert got["knn"][1] == ref["knn"][1]
-        assert got["viterbi"][1] == pytest.approx(ref["viterbi"][1], rel=1e-9)
+        assert got["viterbi"][1] == pytest.approx(ref["viterbi"][1], rel=score_rel)
         assert got["cascade"][0] == ref["cascade"][0]
         assert np.allclose(got["cascade"][1], ref["cascade"][1], atol=1e-5)
         assert np.allclose(got["relief"], ref["relief"], rtol=1e-6, atol=1e-7)
@@ -171,7 +177,8 @@ def test_world_size_equivalence_device_tensors(comm):
     args = _data()
     ref = run_world(_all_models, 1, *args, "cuda", timeout=600, comm=comm)[0]
     for world in (2, 4):
-        _compare(run_world(_all_models, world, *args, "cuda", timeout=600, comm=comm), ref, world)
+        # the device Viterbi scan accumulates in fp32 per chunk: the score depends on the chunking
+        _compare(run_world(_all_models, world, *args, "cuda", timeout=600, comm=comm), ref, world, score_rel=1e-6)
 
 
 def _cli_ranks(rank, world, data, schema, model, out_dir, out_file):
