@@ -376,7 +376,8 @@ void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels
 
 void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& node,
                          const at::Tensor& g, const at::Tensor& h, const at::Tensor& bins,
-                         const at::Tensor& offs, int64_t total_bins, int64_t n_nodes, at::Tensor& out) {
+                         const at::Tensor& offs, int64_t total_bins, int64_t n_nodes, at::Tensor& out,
+                         bool even_only) {
   check_codes(codes, n);
   CHECK_DEV(node);
   CHECK_DTYPE(node, at::kInt);
@@ -395,7 +396,52 @@ void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& n
   avk::node_grad_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, node.data_ptr<int>(),
                            g.data_ptr<float>(), h.data_ptr<float>(), bins.data_ptr<int>(),
                            offs.data_ptr<int>(), (int)codes.size(0), (int)total_bins, (int)n_nodes,
-                           reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(codes));
+                           even_only ? 1 : 0, reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(codes));
+}
+
+// Device GBT round pieces (gbt.hip).  F: [ld, K] float32 raw scores (row-major), y uint8 labels.
+void gbt_grad(const at::Tensor& F, int64_t k, const at::Tensor& y, int64_t n, int64_t row_off, int64_t seed,
+              int64_t rate32, at::Tensor& g, at::Tensor& h, const c10::optional<at::Tensor>& loss) {
+  CHECK_DEV(F); CHECK_DTYPE(F, at::kFloat);
+  CHECK_DEV(y); CHECK_DTYPE(y, at::kByte);
+  CHECK_DEV(g); CHECK_DTYPE(g, at::kFloat);
+  CHECK_DEV(h); CHECK_DTYPE(h, at::kFloat);
+  TORCH_CHECK(F.dim() == 2 && F.is_contiguous() && F.size(0) >= n, "F must be a contiguous [>= n, K] tensor");
+  const int64_t K = F.size(1);
+  TORCH_CHECK(k >= 0 && k < K && K >= 1 && K <= 255, "bad class index");
+  TORCH_CHECK(y.numel() >= n && g.numel() >= n && h.numel() >= n, "y / g / h shorter than n");
+  TORCH_CHECK(rate32 >= 0 && rate32 <= 0xFFFFFFFFLL, "rate32 is a uint32");
+  double* lp = nullptr;
+  if (loss.has_value() && loss->defined()) {
+    CHECK_DEV((*loss)); CHECK_DTYPE((*loss), at::kDouble);
+    TORCH_CHECK(loss->numel() >= 1, "loss slot");
+    lp = loss->data_ptr<double>();
+  }
+  DevGuard gd(F.device());
+  avk::gbt_grad(F.data_ptr<float>(), (int)K, (int)k, y.data_ptr<uint8_t>(), n, row_off, (unsigned long long)seed,
+                (unsigned)rate32, g.data_ptr<float>(), h.data_ptr<float>(), lp, cur_stream(F));
+}
+
+void gbt_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::Tensor& feat, const at::Tensor& thr,
+                const at::Tensor& value, const at::Tensor& bins, int64_t level, bool last, double lr, at::Tensor& F,
+                int64_t k) {
+  check_codes(codes, n);
+  CHECK_DEV(node); CHECK_DTYPE(node, at::kInt);
+  CHECK_DEV(feat); CHECK_DTYPE(feat, at::kInt);
+  CHECK_DEV(thr); CHECK_DTYPE(thr, at::kInt);
+  CHECK_DEV(value); CHECK_DTYPE(value, at::kDouble);
+  CHECK_DEV(bins); CHECK_DTYPE(bins, at::kInt);
+  CHECK_DEV(F); CHECK_DTYPE(F, at::kFloat);
+  TORCH_CHECK(level >= 0 && level < 24, "level out of range");
+  const int64_t H = (2LL << level) - 1 + (2LL << level);   // heap entries up to the next level
+  TORCH_CHECK(feat.numel() >= H && thr.numel() >= H && value.numel() >= H, "heap arrays too short for the level");
+  TORCH_CHECK(node.numel() >= n && F.dim() == 2 && F.is_contiguous() && F.size(0) >= n, "node / F shapes");
+  TORCH_CHECK(k >= 0 && k < F.size(1), "bad class index");
+  TORCH_CHECK(bins.numel() >= codes.size(0) - 1, "bins per feature");
+  DevGuard gd(codes.device());
+  avk::gbt_assign(codes.data_ptr<uint8_t>(), codes.size(1), n, node.data_ptr<int>(), feat.data_ptr<int>(),
+                  thr.data_ptr<int>(), value.data_ptr<double>(), bins.data_ptr<int>(), (int)level, last ? 1 : 0,
+                  (float)lr, F.data_ptr<float>(), (int)F.size(1), (int)k, cur_stream(codes));
 }
 
 void tree_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::Tensor& split_feat,
@@ -2304,7 +2350,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("class_moments", &class_moments);
   m.def("nb_predict", &nb_predict);
   m.def("node_histogram", &node_histogram);
-  m.def("node_grad_histogram", &node_grad_histogram);
+  m.def("node_grad_histogram", &node_grad_histogram, py::arg("codes"), py::arg("n"), py::arg("node"), py::arg("g"),
+        py::arg("h"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_nodes"), py::arg("out"),
+        py::arg("even_only") = false);
+  m.def("gbt_grad", &gbt_grad);
+  m.def("gbt_assign", &gbt_assign);
   m.def("tree_assign", &tree_assign);
   m.def("tree_predict", &tree_predict);
   m.def("knn_topk", &knn_topk);

@@ -46,7 +46,7 @@ void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8
                     hipStream_t stream);
 void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const int* node,
                          const float* g, const float* h, const int* bins, const int* offs, int nfeat,
-                         int total_bins, int n_nodes, long long* out, hipStream_t stream);
+                         int total_bins, int n_nodes, int even_only, long long* out, hipStream_t stream);
 void tree_assign(const uint8_t* codes, long long ld, long long n, int* node, const int* split_feat,
                  const short* segmap, int max_bins, const int* child_of, int max_seg,
                  hipStream_t stream);
@@ -186,6 +186,12 @@ void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long lo
                     const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
                     const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream);
 int csv_devspec_bytes();
+// device GBT round (gbt.hip)
+void gbt_grad(const float* F, int K, int k, const uint8_t* y, long long n, long long row_off, unsigned long long seed,
+              unsigned rate32, float* g, float* h, double* loss, hipStream_t stream);
+void gbt_assign(const uint8_t* codes, long long ld, long long n, int* node, const int* feat, const int* thr,
+                const double* value, const int* bins, int level, int last, float lr, float* F, int K, int k,
+                hipStream_t stream);
 // K1 device tokenizer for non-schema record layouts (records.hip)
 void rec_lines(const uint8_t* bytes, const long long* nlpos, long long nraw, const char* delims, int ndelims,
                long long* lstart, long long* lend, int* ntok, hipStream_t stream);

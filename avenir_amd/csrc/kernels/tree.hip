@@ -84,7 +84,7 @@ __global__ __launch_bounds__(TB_THREADS) void node_hist_kernel(
 __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, long long n, const int* __restrict__ node,
     const float* __restrict__ g, const float* __restrict__ h, const int* __restrict__ bins,
-    const int* __restrict__ offs, int nfeat, int total_bins, int nodes_per_chunk, int n_nodes,
+    const int* __restrict__ offs, int nfeat, int total_bins, int nodes_per_chunk, int n_nodes, int even_only,
     long long* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) long long s_g[];
   const int a0 = blockIdx.y * nodes_per_chunk;
@@ -98,10 +98,13 @@ __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
   for (long long q = (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < nq; q += stride) {
     const long long r0 = q * 4;
     const int4 nd4 = *reinterpret_cast<const int4*>(node + r0);
-    int a[4] = {nd4.x - a0, nd4.y - a0, nd4.z - a0, nd4.w - a0};
+    int a[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
     bool any = false;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      // even_only (GBT sibling subtraction): only rows of even (left) slots, counted at slot / 2
+      if (even_only) a[j] = (a[j] < 0 || (a[j] & 1)) ? -1 : (a[j] >> 1);
+      a[j] = a[j] < 0 ? -1 : a[j] - a0;
       const bool ok = r0 + j < n && a[j] >= 0 && a[j] < na;
       if (!ok) a[j] = -1;
       any |= ok;
@@ -284,7 +287,7 @@ void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8
 
 void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const int* node,
                          const float* g, const float* h, const int* bins, const int* offs, int nfeat,
-                         int total_bins, int n_nodes, long long* out, hipStream_t stream) {
+                         int total_bins, int n_nodes, int even_only, long long* out, hipStream_t stream) {
   if (n <= 0 || n_nodes <= 0) return;
   const long long per_node_bytes = 16LL * total_bins;
   if (per_node_bytes > 64 * 1024) throw std::runtime_error("node_grad_histogram: table exceeds LDS");
@@ -293,7 +296,7 @@ void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const 
   const int gx = std::max(1, std::min(av::stream_grid((n + 3) / 4, TB_THREADS, 2, 2048), std::max(64, 4096 / chunks)));
   dim3 grid(gx, chunks);
   node_grad_hist_kernel<<<grid, TB_THREADS, per_node_bytes * npc, stream>>>(
-      codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, out);
+      codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, even_only, out);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import itertools
 import json
+import os
 import math
 import random
 from dataclasses import dataclass, field
@@ -1094,7 +1095,16 @@ class _RegNode:
 
 class GradientBoostedTrees:
     """Histogram GBT: per stage one regression tree per class on (g, h) with Newton leaves.
-    Every level = one ``node_grad_hist`` pass (exact fixed-point sums) + one ``tree_assign`` pass."""
+
+    Device-resident rounds (csrc/kernels/gbt.hip): every tree of depth D lives in static heap
+    arrays (slot s of a level has children 2s / 2s+1), so a tree build is a fixed sequence of launches
+    — per level one ``node_grad_hist`` pass (exact fixed-point sums; from level 1 only the left
+    children, right = parent - left), the threshold scan as batched tensor math, and one
+    ``gbt_assign`` pass that also adds ``lr * leaf value`` to the raw scores of rows reaching a
+    leaf (no separate inference pass).  On a GPU that sequence is captured once in a HIP graph and
+    replayed per tree; the per-round gradient kernel computes the previous round's training loss on
+    the device.  Nothing is copied to the host until the fit ends (one copy of every tree), except
+    when per-round checkpoints are written."""
 
     def __init__(self, schema: FeatureSchema, params: GBTParams | None = None, comm: Comm | None = None,
                  recovery=None):
@@ -1107,39 +1117,41 @@ class GradientBoostedTrees:
         self.init: torch.Tensor | None = None
         self.n_classes = 2
         self.train_loss: list[float] = []
+        self.graph_used = False
 
-    def _tree(self, codes, n, g, h, bins, dev) -> DecisionTree:
-        """One regression tree on (g, h).  Per level ONE histogram pass over the rows, and only for
-        the lighter child of every split: the heavier sibling's histogram is the parent's minus the
-        lighter one (exact: the sums are fixed point), and the last level's leaf values come from
-        the split scan itself, so a depth-d tree costs d - 1 half-size passes plus the root pass."""
-        comm = self.comm or get_comm()
+    # ------------------------------------------------------------------------------------------
+    def _build_tree(self, st: dict, k: int) -> None:
+        """One regression tree for class ``k`` from the gradients in st["g"][k], st["h"][k]: writes
+        the heap arrays st["feat"], st["thr"], st["val"] and updates the raw scores.  Static shapes
+        and device-only work (graph-capturable)."""
         p = self.p
-        offs = list(itertools.accumulate([0] + bins[:-1]))
-        node = torch.full((codes.shape[1],), -1, dtype=torch.int32, device=dev)
+        comm = self.comm or get_comm()
+        codes, n, bins, sc = st["codes"], st["n"], st["bins"], self._scan
+        node, g, h = st["node"], st["g"][k], st["h"][k]
+        feat, thr, val = st["feat"], st["thr"], st["val"]
+        tb_tot = st["offs"][-1]
+        feat.fill_(-1)
+        thr.zero_()
+        val.zero_()
         node[:n] = 0
-        nodes = [Node([], n, 0.0, [0.0], depth=0)]
-        values = [0.0]
-        frontier = [0]
 
-        def grad_hist(A):
-            hh = T.node_grad_histogram(codes, n, node, g, h, bins, A)   # [A, TB, 2] f64
+        def grad_hist(A, even):
+            hh = T.node_grad_histogram(codes, n, node, g, h, bins, A, even_only=even, bins_d=st["bins_d"],
+                                       offs_d=st["offs_d"])
             if comm.is_distributed:
                 comm.all_reduce(hh)
             return hh
 
-        hist = grad_hist(1)
-        tot = hist[:, offs[-1], :]
-        values[0] = float(-tot[0, 0] / (tot[0, 1] + p.l2).clamp_min(1e-12))
-        sc = self._scan
-        for depth in range(p.max_depth):
-            A = len(frontier)
-            tot = hist[:, offs[-1], :]            # the constant total row's single bin
+        hist = grad_hist(1, False)
+        D = p.max_depth
+        for lvl in range(D):
+            A = 1 << lvl
+            hb, hc = A - 1, 2 * A - 1
+            tot = hist[:, tb_tot, :]
             G, H = tot[:, 0], tot[:, 1]
-            parent = (G * G / (H + p.l2).clamp_min(1e-12))
-            # all thresholds of all features at once: segmented cumsum over the feature bins
-            # (scanned along the contiguous last dim: a middle-dim scan of this [A, NB, 2] tensor
-            # ran as a 140 us outer-dim scan kernel, the top GBT cost per level)
+            if lvl == 0:
+                val[0:1] = -G / (H + p.l2).clamp_min(1e-12)
+            parent = G * G / (H + p.l2).clamp_min(1e-12)
             cs = torch.cumsum(hist[:, : sc["nb"], :].transpose(1, 2).contiguous(), 2).transpose(1, 2)  # [A, NB, 2]
             base = torch.where((sc["start"] > 0).view(1, -1, 1), cs[:, (sc["start"] - 1).clamp_min(0), :],
                                torch.zeros_like(cs))
@@ -1154,70 +1166,78 @@ class GradientBoostedTrees:
             bi = best_pos.view(-1, 1)
             cgl, chl = gl.gather(1, bi)[:, 0], hl.gather(1, bi)[:, 0]
             cgr, chr_ = gr.gather(1, bi)[:, 0], hr.gather(1, bi)[:, 0]
-            # a parent whose split feature is missing on some rows drops them: subtraction invalid
-            exact = (chl + chr_) == H
-            sel = torch.stack([best_gain, sc["feat"][best_pos].double(), sc["thr"][best_pos].double(),
-                               -cgl / (chl + p.l2).clamp_min(1e-12), -cgr / (chr_ + p.l2).clamp_min(1e-12),
-                               (chl <= chr_).double(), exact.double()]).cpu()
-            bg, bf, bb = sel[0].tolist(), [int(v) for v in sel[1].tolist()], [int(v) for v in sel[2].tolist()]
-            vl, vr, lighter_left, ex = sel[3].tolist(), sel[4].tolist(), sel[5].tolist(), sel[6].tolist()
-            max_bins = max(bins)
-            last = depth + 1 == p.max_depth
-            split_feat = torch.full((A,), -1, dtype=torch.int32)
-            segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
-            child_of = torch.full((A, 2), -1, dtype=torch.int32)
-            expand = []                                  # (frontier slot, left id, right id)
-            for a, gi in enumerate(frontier):
-                if bf[a] < 0 or not math.isfinite(bg[a]) or bg[a] <= 1e-12:
-                    continue
-                f, thr = bf[a], bb[a]
-                sm = [0 if x <= thr else 1 for x in range(bins[f])]
-                nd = nodes[gi]
-                nd.feature, nd.split, nd.segmap = f, thr, sm
-                split_feat[a] = f
-                segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
-                nd.children = []
-                for s_, v in ((0, vl[a]), (1, vr[a])):
-                    ci = len(nodes)
-                    nodes.append(Node([], 0, 0.0, [0.0], depth=nd.depth + 1))
-                    values.append(v)
-                    nd.children.append(ci)
-                expand.append((a, nd.children[0], nd.children[1]))
-            if not expand or last:
-                break                                    # children are leaves: values already set
-            m = len(expand)
-            subtract = all(ex[a] > 0.5 for a, _, _ in expand)
-            # frontier order: lighter children (ids 0..m-1) first, heavier siblings (m..2m-1) after
-            light, heavy = [], []
-            for k, (a, cl, cr) in enumerate(expand):
-                lt_left = lighter_left[a] > 0.5
-                child_of[a, 0 if lt_left else 1] = k
-                child_of[a, 1 if lt_left else 0] = m + k
-                light.append(cl if lt_left else cr)
-                heavy.append(cr if lt_left else cl)
-            T.tree_assign(codes, n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
-            if subtract:
-                hs = grad_hist(m)                                        # lighter children only
-                pa = torch.tensor([a for a, _, _ in expand], dtype=torch.long, device=dev)
-                hist = torch.cat([hs, hist[pa] - hs])
+            split = torch.isfinite(best_gain) & (best_gain > 1e-12)
+            feat[hb:hb + A] = torch.where(split, sc["feat"][best_pos], torch.full_like(best_pos, -1)).int()
+            thr[hb:hb + A] = sc["thr"][best_pos].int()
+            vl = -cgl / (chl + p.l2).clamp_min(1e-12)
+            vr = -cgr / (chr_ + p.l2).clamp_min(1e-12)
+            val[hc:hc + 2 * A] = torch.where(split.view(-1, 1), torch.stack([vl, vr], 1),
+                                             torch.zeros_like(torch.stack([vl, vr], 1))).view(-1)
+            last = lvl + 1 == D
+            T.gbt_assign(codes, n, node, feat, thr, val, st["bins_t"], lvl, last, p.learning_rate, st["F"], k)
+            if last:
+                break
+            if st["subtract"]:
+                hl_ = grad_hist(A, True)                     # left children (even slots) only
+                hist = torch.stack([hl_, hist - hl_], 1).view(2 * A, *hist.shape[1:])
             else:
-                hist = grad_hist(2 * m)
-            frontier = light + heavy
-        for i, nd in enumerate(nodes):
-            nd.class_pr = [values[i]]
-        return DecisionTree(nodes, self.space, ["value"])
+                hist = grad_hist(2 * A, False)
+
+    def _trees_from_heaps(self, feat, thr, val) -> list[list[DecisionTree]]:
+        """Host DecisionTrees from the [R, K, heap] arrays (nodes reachable from the root only)."""
+        R, K, Hn = feat.shape
+        bins = [fs.n_bins for fs in self.space]
+        fl, tl, vl = feat.tolist(), thr.tolist(), val.tolist()
+        seg_cache: dict[tuple[int, int], list[int]] = {}
+        stages = []
+        for r in range(R):
+            stage = []
+            for k in range(K):
+                fr, trr, vr = fl[r][k], tl[r][k], vl[r][k]
+                nodes: list[Node] = []
+                idx_of = {0: 0}
+                order = [0]
+                nodes.append(Node([], 0, 0.0, [vr[0]], depth=0))
+                q = 0
+                while q < len(order):
+                    i = order[q]
+                    q += 1
+                    f = fr[i]
+                    if f < 0 or 2 * i + 2 >= Hn:
+                        continue
+                    # heap children of i: level l = floor(log2(i + 1)); slot s = i - (2^l - 1)
+                    lvl = (i + 1).bit_length() - 1
+                    s = i - ((1 << lvl) - 1)
+                    cl = (2 << lvl) - 1 + 2 * s
+                    nd = nodes[idx_of[i]]
+                    th = trr[i]
+                    sm = seg_cache.get((f, th))
+                    if sm is None:
+                        sm = seg_cache[(f, th)] = [0 if b <= th else 1 for b in range(bins[f])]
+                    nd.feature, nd.split, nd.segmap = f, th, sm
+                    nd.children = []
+                    for c in (cl, cl + 1):
+                        idx_of[c] = len(nodes)
+                        nd.children.append(len(nodes))
+                        nodes.append(Node([], 0, 0.0, [vr[c]], depth=nd.depth + 1))
+                        order.append(c)
+                stage.append(DecisionTree(nodes, self.space, ["value"]))
+            stages.append(stage)
+        return stages
 
     def fit(self, t: Table) -> "GradientBoostedTrees":
         comm = self.comm or get_comm()
         p = self.p
+        if p.max_depth < 1 or p.max_depth > 16:
+            raise ValueError("GBT max_depth must be in 1..16")
         self.space = build_split_space(self.schema, t, binary=True, max_bins=p.max_bins, comm=comm)
-        codes = encode_for_tree(self.space, t)
-        codes = _with_total_row(codes, t.n)
+        codes = _with_total_row(encode_for_tree(self.space, t), t.n)
         bins = [fs.n_bins for fs in self.space] + [1]
         n, dev = t.n, t.device
-        # static index tensors of the vectorised threshold scan (features are contiguous in the histogram)
+        ld = codes.shape[1]
         fb = bins[:-1]
         offs0 = list(itertools.accumulate([0] + fb[:-1]))
+        offs = list(itertools.accumulate([0] + bins[:-1]))
         self._scan = {
             "nb": sum(fb),
             "feat": torch.cat([torch.full((b,), f, dtype=torch.long) for f, b in enumerate(fb)]).to(dev),
@@ -1233,63 +1253,101 @@ class GradientBoostedTrees:
         cnt = torch.bincount(y, minlength=C).double()
         if comm.is_distributed:
             comm.all_reduce(cnt)
+        n_total = float(cnt.sum())
         prior = (cnt / cnt.sum()).clamp(1e-12, 1 - 1e-12)
-        if K == 1:
-            self.init = torch.log(prior[1] / prior[0]).view(1).float()
-        else:
-            self.init = torch.log(prior).float()
-        F = self.init.to(dev).view(1, K).expand(n, K).clone()
-        Y = torch.nn.functional.one_hot(y, C).float() if K > 1 else y.float().view(n, 1)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(p.seed + 17 * comm.rank)
-        # one boosting round = one resumable iteration: the raw scores F (this rank's rows) and the
-        # subsample RNG state go to a per-rank checkpoint, the trees (identical on every rank) ride
-        # along as JSON metadata (utils/resilience.IterationLoop)
+        self.init = (torch.log(prior[1] / prior[0]).view(1) if K == 1 else torch.log(prior)).float()
+        Hn = (2 << p.max_depth) - 1
+        R = p.n_estimators
+        missing = bool((codes[:-1, :n] == MISSING).any()) if n else False
+        if comm.is_distributed:
+            mt = torch.tensor([float(missing)])
+            comm.all_reduce(mt, "max")
+            missing = bool(mt[0] > 0)
+        y8 = torch.zeros(ld, dtype=torch.uint8, device=dev)
+        y8[:n] = y.to(torch.uint8)
+        st = {
+            "codes": codes, "n": n, "bins": bins, "offs": offs,
+            "bins_d": torch.tensor(bins, dtype=torch.int32, device=dev),
+            "offs_d": torch.tensor(offs, dtype=torch.int32, device=dev),
+            "bins_t": torch.tensor(fb, dtype=torch.int32, device=dev),
+            "node": torch.full((ld,), -1, dtype=torch.int32, device=dev),
+            "g": torch.zeros((K, ld), dtype=torch.float32, device=dev),
+            "h": torch.zeros((K, ld), dtype=torch.float32, device=dev),
+            "feat": torch.full((Hn,), -1, dtype=torch.int32, device=dev),
+            "thr": torch.zeros(Hn, dtype=torch.int32, device=dev),
+            "val": torch.zeros(Hn, dtype=torch.float64, device=dev),
+            "F": self.init.to(dev).view(1, K).expand(ld, K).contiguous(),
+            "subtract": not missing,
+        }
+        feat_all = torch.full((R, K, Hn), -1, dtype=torch.int32, device=dev)
+        thr_all = torch.zeros((R, K, Hn), dtype=torch.int32, device=dev)
+        val_all = torch.zeros((R, K, Hn), dtype=torch.float64, device=dev)
+        loss_all = torch.zeros(R + 1, dtype=torch.float64, device=dev)
+        rate32 = 0xFFFFFFFF if p.subsample >= 1.0 else int(max(0.0, p.subsample) * 4294967296.0)
+        # one boosting round = one resumable iteration (per-rank F, trees in the metadata)
         from ..utils.resilience import IterationLoop
         lp = IterationLoop("gbt", self.recovery, comm, sharded=True, device=dev)
-        r0, st, meta = lp.restore(dev)
-        if st is not None:
-            F = st["F"].to(dev)
-            gen.set_state(st["rng"].cpu())
-            self.stages = [[DecisionTree.from_state(x, self.schema) for x in stage] for stage in meta["stages"]]
-            for stage in self.stages:
-                for tr in stage:
-                    tr.space = self.space
-            self.train_loss = list(meta["train_loss"])
-        nbytes = float(codes.numel()) * max(1, p.max_depth)
-        for rnd in range(r0, p.n_estimators):
-            with lp.step(rnd, nbytes=nbytes):
-                if K == 1:
-                    pr = torch.sigmoid(F)
-                else:
-                    pr = torch.softmax(F, 1)
-                grad = pr - Y
-                hess = (pr * (1 - pr)).clamp_min(1e-6)
-                if p.subsample < 1.0:
-                    m = (torch.rand(n, generator=gen, device=dev) < p.subsample).float().view(n, 1)
-                    grad, hess = grad * m, hess * m
-                stage = []
+        r0, ck, meta = lp.restore(dev)
+        if ck is not None:
+            st["F"].copy_(ck["F"].to(dev))
+            feat_all[:r0], thr_all[:r0], val_all[:r0] = ck["feat"].to(dev), ck["thr"].to(dev), ck["val"].to(dev)
+            loss_all[:r0] = ck["loss"].to(dev)[:r0]     # this rank's own partial sums
+        use_graph = (dev.type == "cuda" and not comm.is_distributed and not lp.enabled
+                     and os.environ.get("AVMI_GBT_GRAPH", "1") != "0")
+        graphs: dict[int, Any] = {}
+
+        def tree(k):
+            if not use_graph:
+                self._build_tree(st, k)
+                return
+            if k not in graphs:
+                # warm up on a side stream (allocator pools, kernel selection), then capture
+                s_ = torch.cuda.Stream(device=dev)
+                s_.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(s_):
+                    Fsave = st["F"].clone()
+                    self._build_tree(st, k)
+                    st["F"].copy_(Fsave)
+                torch.cuda.current_stream(dev).wait_stream(s_)
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    self._build_tree(st, k)
+                graphs[k] = gr
+            graphs[k].replay()
+
+        seed_base = (p.seed * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
+        for rnd in range(r0, R):
+            with lp.step(rnd, nbytes=float(codes.numel()) * p.max_depth):
+                rseed = (seed_base ^ (rnd * 0xD1B54A32D192ED03)) & 0x7FFFFFFFFFFFFFFF
+                for k in range(K):       # all gradients from the round's starting scores
+                    T.gbt_grad(st["F"], k, y8, n, t.row_offset, rseed, rate32, st["g"][k], st["h"][k],
+                               loss_all[rnd:rnd + 1] if k == 0 else None)
                 for k in range(K):
-                    g = torch.zeros(codes.shape[1], device=dev)
-                    h = torch.zeros(codes.shape[1], device=dev)
-                    g[:n], h[:n] = grad[:, k], hess[:, k]
-                    tr = self._tree(codes, n, g, h, bins, dev)
-                    flat = flatten_forest([tr], dev, value_fn=lambda nd: nd.class_pr)
-                    F[:, k] += p.learning_rate * T.tree_predict(codes, n, flat, mode=0)[:, 0]
-                    stage.append(tr)
-                self.stages.append(stage)
-                if K == 1:
-                    loss = torch.nn.functional.binary_cross_entropy_with_logits(F[:, 0], Y[:, 0])
-                else:
-                    loss = torch.nn.functional.cross_entropy(F, y)
-                self.train_loss.append(float(loss))
+                    tree(k)
+                    feat_all[rnd, k].copy_(st["feat"])
+                    thr_all[rnd, k].copy_(st["thr"])
+                    val_all[rnd, k].copy_(st["val"])
             if lp.enabled:
-                lp.commit(rnd, {"F": F, "rng": gen.get_state()},
-                          {"stages": [[tr.state() for tr in stage] for stage in self.stages],
-                           "train_loss": self.train_loss})
-        lp.close()
+                lp.commit(rnd, {"F": st["F"], "feat": feat_all[:rnd + 1], "thr": thr_all[:rnd + 1],
+                                "val": val_all[:rnd + 1], "loss": loss_all[:rnd + 1]},
+                          {"train_loss": self._losses(loss_all, rnd + 1, st, y8, n, t, n_total, comm)})
+        self.graph_used = bool(graphs)
+        self.train_loss = self._losses(loss_all, R, st, y8, n, t, n_total, comm)
+        self.stages = self._trees_from_heaps(feat_all.cpu(), thr_all.cpu(), val_all.cpu())
         self._flat = None
         return self
+
+    def _losses(self, loss_all, upto, st, y8, n, t, n_total, comm) -> list[float]:
+        """train_loss[r] = mean deviance after round r: round r+1's gradient pass measured it; the
+        last one is measured here.  One host copy."""
+        last = torch.zeros(1, dtype=torch.float64, device=loss_all.device)
+        K = st["F"].shape[1]
+        gs = torch.zeros_like(st["g"][0])
+        T.gbt_grad(st["F"], 0, y8, n, t.row_offset, 0, 0xFFFFFFFF, gs, torch.zeros_like(gs), last)
+        tot = torch.cat([loss_all[1:upto], last])
+        if comm.is_distributed:
+            comm.all_reduce(tot)
+        return (tot / max(n_total, 1.0)).tolist()
 
     def decision_function(self, t: Table) -> torch.Tensor:
         codes = encode_for_tree(self.space, t)

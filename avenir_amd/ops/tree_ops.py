@@ -46,19 +46,26 @@ def node_histogram(codes: torch.Tensor, n: int, labels: torch.Tensor, node: torc
 
 
 def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torch.Tensor,
-                        h: torch.Tensor, bins: Sequence[int], n_nodes: int) -> torch.Tensor:
-    """Exact fixed-point (2^-24) sums of gradient and hessian per (node, bin): float64 [A, TB, 2]."""
+                        h: torch.Tensor, bins: Sequence[int], n_nodes: int, even_only: bool = False,
+                        bins_d: torch.Tensor | None = None, offs_d: torch.Tensor | None = None) -> torch.Tensor:
+    """Exact fixed-point (2^-24) sums of gradient and hessian per (node, bin): float64 [A, TB, 2].
+    ``even_only``: only rows of even node ids, counted at id / 2 (the left children of a level, for
+    sibling subtraction).  ``bins_d`` / ``offs_d``: cached device copies of the bin tables."""
     bins = [int(b) for b in bins]
     tb = sum(bins)
     if codes.is_cuda:
         out = torch.zeros((n_nodes, tb, 2), dtype=torch.int64, device=codes.device)
         if n and n_nodes:
             _native.C().node_grad_histogram(codes, int(n), node, g.float().contiguous(),
-                                            h.float().contiguous(), _dev_i32(bins, codes.device),
-                                            _dev_i32(_offs(bins), codes.device), tb, int(n_nodes), out)
+                                            h.float().contiguous(),
+                                            bins_d if bins_d is not None else _dev_i32(bins, codes.device),
+                                            offs_d if offs_d is not None else _dev_i32(_offs(bins), codes.device),
+                                            tb, int(n_nodes), out, bool(even_only))
         return out.double() / _GRAD_SCALE
     out = torch.zeros((n_nodes, tb, 2), dtype=torch.int64)
     nd = node[:n].long()
+    if even_only:
+        nd = torch.where((nd >= 0) & (nd % 2 == 0), nd // 2, torch.full_like(nd, -1))
     gi = torch.round(g[:n].float() * _GRAD_SCALE).long()
     hi = torch.round(h[:n].float() * _GRAD_SCALE).long()
     ok_r = (nd >= 0) & (nd < n_nodes)
@@ -70,6 +77,76 @@ def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torc
         flat.index_add_(0, base, gi[ok])
         flat.index_add_(0, base + 1, hi[ok])
     return out.double() / _GRAD_SCALE
+
+
+def gbt_grad(F: torch.Tensor, k: int, y: torch.Tensor, n: int, row_off: int, seed: int, rate32: int,
+             g: torch.Tensor, h: torch.Tensor, loss: torch.Tensor | None = None) -> None:
+    """In place: g, h = gradient / hessian of the deviance loss for class ``k`` (sigmoid when
+    ``F`` has one column, softmax otherwise) at the raw scores ``F`` [>= n, K]; rows outside the
+    counter-hash subsample (``rate32`` / 2^32, keyed by ``seed`` and the GLOBAL row) get 0;
+    ``loss`` (when given) += the summed loss of the current scores (gbt.hip)."""
+    if F.is_cuda:
+        _native.C().gbt_grad(F, int(k), y, int(n), int(row_off), int(seed) & 0x7FFFFFFFFFFFFFFF, int(rate32), g, h,
+                             loss)
+        return
+    K = F.shape[1]
+    f = F[:n].double()
+    yl = y[:n].long()
+    if K == 1:
+        p = torch.sigmoid(f[:, 0])
+        target = yl.double()
+        lv = f[:, 0].clamp_min(0) - f[:, 0] * target + torch.log1p(torch.exp(-f[:, 0].abs()))
+    else:
+        lse = torch.logsumexp(f, 1)
+        p = torch.exp(f[:, k] - lse)
+        target = (yl == k).double()
+        lv = lse - f.gather(1, yl.clamp_max(K - 1).view(-1, 1))[:, 0]
+    gr = (p - target).float()
+    hr = (p * (1 - p)).float().clamp_min(1e-6)
+    if rate32 != 0xFFFFFFFF:
+        rows = torch.arange(row_off, row_off + n, dtype=torch.int64)
+        u = _mix32((int(seed) & 0xFFFFFFFFFFFFFFFF), rows)
+        keep = u < rate32
+        gr, hr = torch.where(keep, gr, torch.zeros_like(gr)), torch.where(keep, hr, torch.zeros_like(hr))
+    g[:n], h[:n] = gr, hr
+    if loss is not None:
+        loss += lv.sum()
+
+
+def _mix32(seed: int, rows: torch.Tensor) -> torch.Tensor:
+    """splitmix64 finaliser of seed + row * golden, high 32 bits (gbt.hip mix32), via numpy uint64."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + rows.numpy().astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return torch.from_numpy((z >> np.uint64(32)).astype(np.int64))
+
+
+def gbt_assign(codes: torch.Tensor, n: int, node: torch.Tensor, feat: torch.Tensor, thr: torch.Tensor,
+               value: torch.Tensor, bins_t: torch.Tensor, level: int, last: bool, lr: float, F: torch.Tensor,
+               k: int) -> None:
+    """In place: rows of slot s at ``level`` (heap index 2^level - 1 + s) move to child 2s / 2s+1
+    by ``code <= thr``; rows reaching a leaf (no split, missing code, or the last level) add
+    ``lr * value[leaf]`` to ``F[:, k]`` and leave (node = -1)."""
+    if codes.is_cuda:
+        _native.C().gbt_assign(codes, int(n), node, feat, thr, value, bins_t, int(level), bool(last), float(lr), F,
+                               int(k))
+        return
+    hb, hc = (1 << level) - 1, (2 << level) - 1
+    s = node[:n].long()
+    act = s >= 0
+    i = (hb + s).clamp_min(0)
+    f = feat.long()[i]
+    fc = f.clamp_min(0)
+    c = codes[fc, torch.arange(n)].long()
+    has = act & (f >= 0) & (c < bins_t.long()[fc])
+    child = 2 * s + (c > thr.long()[i]).long()
+    leaf_val = torch.where(has & last, value[(hc + child).clamp_min(0).clamp_max(value.numel() - 1)], value[i])
+    finish = act & (~has | last)
+    F[:n, k] += torch.where(finish, (lr * leaf_val.float()), torch.zeros_like(F[:n, k]))
+    node[:n] = torch.where(act & has & (not last), child, torch.full_like(s, -1)).to(node.dtype)
 
 
 def tree_assign(codes: torch.Tensor, n: int, node: torch.Tensor, split_feat: torch.Tensor,

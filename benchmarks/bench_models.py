@@ -63,9 +63,30 @@ def bench_gbt(a):
     from avenir_amd.models.tree import GBTParams, GradientBoostedTrees
     n, d = a.rows, 16
     t = _numeric_table(n, d, 1)
-    p = GBTParams(n_estimators=50, learning_rate=0.1, max_depth=4, max_bins=64)
-    sec, _ = timed(lambda: GradientBoostedTrees(t.schema, p).fit(t))
-    emit(model="gbt", rows=n, features=d, rounds=50, depth=4, seconds=sec, rows_x_rounds_per_s=n * 50 / sec)
+    for rounds, depth in ((120, 3), (50, 4)):
+        p = GBTParams(n_estimators=rounds, learning_rate=0.1, max_depth=depth, max_bins=64)
+        sec, m = timed(lambda: GradientBoostedTrees(t.schema, p).fit(t))
+        acc = float((m.predict(t) == t.labels[:n].long()).float().mean())
+        emit(model="gbt", rows=n, features=d, rounds=rounds, depth=depth, seconds=sec, ms_per_round=1e3 * sec / rounds,
+             rows_x_rounds_per_s=n * rounds / sec, graph=m.graph_used, train_acc=acc,
+             loss_first_last=[m.train_loss[0], m.train_loss[-1]])
+
+
+def bench_rf_ref(a):
+    """Random forest with the reference's split semantics (explicit multi-point numeric splits up to
+    maxSplit, randomNotUsedYet attributes, randomAmongTop): all trees in one batched level-wise build."""
+    from avenir_amd.models.tree import RandomForest, TreeParams
+    n, d = a.rows, 16
+    t = _numeric_table(n, d, 2)
+    for f in t.schema.feature_fields:
+        f.max_split = 3
+    p = TreeParams(binary=False, stopping="maxDepth", max_depth=5, sub_sampling="withReplace",
+                   attr_selection="randomNotUsedYet", random_attr_count=4, split_selection="randomAmongTop",
+                   top_split_count=3, max_bins=8)
+    sec, rf = timed(lambda: RandomForest(t.schema, 10, p, "all").fit(t))
+    acc = float((rf.predict(t) == t.labels[:n].long()).float().mean())
+    emit(model="random_forest_reference_splits", rows=n, features=d, trees=10, depth=5, max_split=3, seconds=sec,
+         rows_x_trees_per_s=n * 10 / sec, train_acc=acc, build=getattr(rf, "build_stats", None))
 
 
 def bench_kmeans(a):
@@ -131,7 +152,7 @@ def bench_mlp(a):
              steps_per_s=2 * (n // 1024) / sec)
 
 
-BENCHES = {"rf": bench_rf, "gbt": bench_gbt, "kmeans": bench_kmeans, "logit": bench_logit, "svm": bench_svm,
+BENCHES = {"rf": bench_rf, "rf_ref": bench_rf_ref, "gbt": bench_gbt, "kmeans": bench_kmeans, "logit": bench_logit, "svm": bench_svm,
            "knn": bench_knn, "sa": bench_sa, "mlp": bench_mlp}
 
 
