@@ -399,6 +399,53 @@ void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& n
                            even_only ? 1 : 0, reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(codes));
 }
 
+// K25 re-sampling (resample.hip)
+at::Tensor resample_uniform(int64_t seed, int64_t stream, int64_t base, int64_t n, const at::Tensor& like) {
+  CHECK_DEV(like);
+  TORCH_CHECK(n >= 0 && base >= 0, "bad range");
+  auto out = at::empty({n}, like.options().dtype(at::kFloat));
+  DevGuard gd(like.device());
+  avk::resample_uniform((unsigned long long)seed, (unsigned long long)stream, base, n, out.data_ptr<float>(),
+                        cur_stream(like));
+  return out;
+}
+
+std::vector<at::Tensor> smote(const at::Tensor& X, const at::Tensor& Xn, const at::Tensor& nn,
+                              const c10::optional<at::Tensor>& Cs, const c10::optional<at::Tensor>& Cn, int64_t mult,
+                              int64_t gbase, int64_t seed, bool exponential, double exp_mean) {
+  CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(Xn); CHECK_DTYPE(Xn, at::kFloat);
+  CHECK_DEV(nn); CHECK_DTYPE(nn, at::kInt);
+  TORCH_CHECK(X.dim() == 2 && Xn.dim() == 3 && X.is_contiguous() && Xn.is_contiguous() && nn.is_contiguous(),
+              "X [m, D], Xn [m, k, D] contiguous");
+  const int64_t m = X.size(0), D = X.size(1), k = Xn.size(1);
+  TORCH_CHECK(Xn.size(0) == m && Xn.size(2) == D && nn.numel() == m && mult >= 0 && k >= 1, "shape mismatch");
+  TORCH_CHECK(m * std::max<int64_t>(mult, 1) < (1LL << 40), "too many synthetic rows");
+  // every neighbour count must be <= k (the kernel indexes Xn[r, pick < nn[r]])
+  if (m) TORCH_CHECK(nn.max().item<int>() <= k && nn.min().item<int>() >= 0, "neighbour counts must be in [0, k]");
+  int64_t Dc = 0;
+  const int* cs = nullptr;
+  const int* cn = nullptr;
+  if (Cs.has_value() && Cs->defined()) {
+    TORCH_CHECK(Cn.has_value() && Cn->defined(), "categorical neighbours missing");
+    CHECK_DEV((*Cs)); CHECK_DTYPE((*Cs), at::kInt);
+    CHECK_DEV((*Cn)); CHECK_DTYPE((*Cn), at::kInt);
+    Dc = Cs->size(1);
+    TORCH_CHECK(Cs->dim() == 2 && Cs->size(0) == m && Cn->dim() == 3 && Cn->size(0) == m && Cn->size(1) == k &&
+                Cn->size(2) == Dc && Cs->is_contiguous() && Cn->is_contiguous(), "Cs [m, Dc], Cn [m, k, Dc]");
+    cs = Cs->data_ptr<int>();
+    cn = Cn->data_ptr<int>();
+  }
+  auto outX = at::empty({m * mult, D}, X.options());
+  auto outC = at::empty({m * mult, Dc}, X.options().dtype(at::kInt));
+  auto pick = at::empty({m * mult}, X.options().dtype(at::kInt));
+  DevGuard gd(X.device());
+  avk::smote(X.data_ptr<float>(), Xn.data_ptr<float>(), nn.data_ptr<int>(), cs, cn, m, (int)k, (int)D, (int)Dc,
+             (int)mult, gbase, (unsigned long long)seed, exponential ? 1 : 0, (float)exp_mean, outX.data_ptr<float>(),
+             Dc ? outC.data_ptr<int>() : nullptr, pick.data_ptr<int>(), cur_stream(X));
+  return {outX, outC, pick};
+}
+
 // Device GBT round pieces (gbt.hip).  F: [ld, K] float32 raw scores (row-major), y uint8 labels.
 void gbt_grad(const at::Tensor& F, int64_t k, const at::Tensor& y, int64_t n, int64_t row_off, int64_t seed,
               int64_t rate32, at::Tensor& g, at::Tensor& h, const c10::optional<at::Tensor>& loss) {
@@ -2354,6 +2401,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("h"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_nodes"), py::arg("out"),
         py::arg("even_only") = false);
   m.def("gbt_grad", &gbt_grad);
+  m.def("resample_uniform", &resample_uniform);
+  m.def("smote", &smote);
   m.def("gbt_assign", &gbt_assign);
   m.def("tree_assign", &tree_assign);
   m.def("tree_predict", &tree_predict);

@@ -186,6 +186,12 @@ void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long lo
                     const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
                     const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream);
 int csv_devspec_bytes();
+// K25 re-sampling (resample.hip)
+void resample_uniform(unsigned long long seed, unsigned long long stream, long long base, long long n, float* out,
+                      hipStream_t st);
+void smote(const float* X, const float* Xn, const int* nn, const int* Cs, const int* Cn, long long m, int k, int D,
+           int Dc, int mult, long long gbase, unsigned long long seed, int exponential, float exp_mean, float* outX,
+           int* outC, int* outPick, hipStream_t st);
 // device GBT round (gbt.hip)
 void gbt_grad(const float* F, int K, int k, const uint8_t* y, long long n, long long row_off, unsigned long long seed,
               unsigned rate32, float* g, float* h, double* loss, hipStream_t stream);

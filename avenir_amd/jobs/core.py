@@ -315,53 +315,77 @@ def smote(args):
     t = ctx.table(raw_numeric=True)
     X = t.dense_features()
     y = t.labels[: t.n].long()
-    minority = int(torch.bincount(y).argmin())
-    n_new = int((y != minority).sum() - (y == minority).sum())
-    Xn, _ = _smote(X, y, minority, max(n_new, 0), ctx.get_int("neighbor.count", 5), seed=ctx.comm.rank)
+    cnt = torch.bincount(y, minlength=t.n_classes).double()
+    ctx.all_reduce(cnt)                                       # global class counts
+    present = torch.nonzero(cnt > 0).view(-1)
+    minority = int(present[cnt[present].argmin()])
+    n_new = int(cnt.sum() - 2 * cnt[minority])                # majority total - minority
+    Xn, _ = _smote(X, y, minority, max(n_new, 0), ctx.get_int("neighbor.count", 5),
+                   seed=ctx.get_int("random.seed", 0), comm=ctx.comm)
     vals = t.class_field.cardinality
     d = ctx.delim_out
     ctx.emit([d.join(f"{v:.4f}" for v in row) + f"{d}{vals[minority]}" for row in Xn.cpu().tolist()])
 
 
 def _smote_from_neighbors(ctx: JobContext) -> None:
+    """ClassBasedOverSampler.map (:125-200) on topMatchesByClass compact lines: record + up to M
+    neighbour records of ``rec.len`` fields.  Every line's ``over.sampling.multiplier`` synthetic
+    records come from the K25 SMOTE kernel (Philox draws keyed by the GLOBAL line index and copy:
+    neighbour pick uniform / exponential, gap, categorical coin), so the output does not depend on
+    the world size; the id field shuffles the two ids' characters with a generator seeded by the
+    same key."""
     import random
+    from ..ops import resample_ops as RS
     L = ctx.get_int("rec.len")
     mult = ctx.get_int("over.sampling.multiplier")
     distr = ctx.get_str("neighbor.sampling.distr", "uniform")
     prec = ctx.get_int("output.precision", 3)
     schema = ctx.schema("feature.schema.file.path")
-    rows = [r for r in ctx.rows() if len(r) >= 2 * L]
+    seed = ctx.get_int("random.seed", 0)
+    all_rows = ctx.rows()
+    base = ctx.line_base(len(all_rows))
+    keep_i = [i for i, r in enumerate(all_rows) if len(r) >= 2 * L]
+    rows = [all_rows[i] for i in keep_i]
     if not rows:
         ctx.emit([])
         return
     M = max((len(r) - L) // L for r in rows)
     n = len(rows)
-    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + 7919 * ctx.comm.rank)
-    nnb = torch.tensor([(len(r) - L) // L for r in rows], dtype=torch.long)
-    if distr == "exponential":
-        mean = ctx.get_float("exp.distr.mean")
-        e = -mean * torch.log(torch.rand((n, mult), generator=g, dtype=torch.float64).clamp_min(1e-12))
-        pick = (torch.round(e).long() - 1).clamp_min(0)
-        pick = torch.minimum(pick, (nnb - 1).view(-1, 1))
-    else:
-        pick = (torch.rand((n, mult), generator=g, dtype=torch.float64) * nnb.view(-1, 1)).long()
-    gap = torch.rand((n, mult), generator=g, dtype=torch.float64)
-    coin = torch.rand((n, mult), generator=g) < 0.5
     fields = {f.ordinal: f for f in schema.fields}
     num_cols = [i for i in range(L) if i in fields and fields[i].feature and fields[i].is_numeric]
-    src = torch.tensor([[float(r[i]) for i in num_cols] for r in rows], dtype=torch.float64)
-    nb = torch.zeros((n, M, len(num_cols)), dtype=torch.float64)
+    nnb = torch.tensor([(len(r) - L) // L for r in rows], dtype=torch.int32)
+    src = torch.tensor([[float(r[i]) for i in num_cols] for r in rows], dtype=torch.float32).view(n, len(num_cols))
+    nb = torch.zeros((n, M, len(num_cols)), dtype=torch.float32)
     for a, r in enumerate(rows):
         for m in range((len(r) - L) // L):
-            nb[a, m] = torch.tensor([float(r[L + m * L + i]) for i in num_cols], dtype=torch.float64)
-    tgt = nb[torch.arange(n).view(-1, 1), pick]                      # [n, mult, F]
-    new = src.unsqueeze(1) + (tgt - src.unsqueeze(1)) * gap.unsqueeze(2)
+            nb[a, m] = torch.tensor([float(r[L + m * L + i]) for i in num_cols], dtype=torch.float32)
+    # categorical coin: source codes 0, neighbour codes 1 -> the kernel's choice per synthetic record
+    Cs = torch.zeros((n, 1), dtype=torch.int32)
+    Cn = torch.ones((n, M, 1), dtype=torch.int32)
+    gidx = torch.tensor([base + i for i in keep_i], dtype=torch.long)
+    dev = ctx.device
+    outs = []
+    # the kernel keys draws by (gbase + r) * mult + j with contiguous r: run per contiguous run of lines
+    runs, start = [], 0
+    for a in range(1, n + 1):
+        if a == n or int(gidx[a]) != int(gidx[a - 1]) + 1:
+            runs.append((start, a))
+            start = a
+    newX, newC, pick = [], [], []
+    for a0, a1 in runs:
+        x, c, pk = RS.smote_rows(src[a0:a1].to(dev), nb[a0:a1].to(dev), nnb[a0:a1].to(dev), Cs[a0:a1].to(dev),
+                                 Cn[a0:a1].to(dev), mult, int(gidx[a0]), seed, distr == "exponential",
+                                 ctx.get_float("exp.distr.mean", 1.0))
+        newX.append(x.cpu())
+        newC.append(c.cpu())
+        pick.append(pk.cpu())
+    newX, newC, pick = torch.cat(newX), torch.cat(newC), torch.cat(pick)
     d = ctx.delim_out
-    rnd = random.Random(ctx.get_int("random.seed", 0) + ctx.comm.rank)
-    out = []
     for a, r in enumerate(rows):
         for j in range(mult):
-            nrec = r[L + int(pick[a, j]) * L: L + int(pick[a, j]) * L + L]
+            o = a * mult + j
+            pj = max(int(pick[o]), 0)
+            nrec = r[L + pj * L: L + pj * L + L]
             rec = list(r[:L])
             for i in range(L):
                 f = fields.get(i)
@@ -369,15 +393,15 @@ def _smote_from_neighbors(ctx: JobContext) -> None:
                     continue
                 if f.id:
                     s = list(r[i] + nrec[i])
-                    rnd.shuffle(s)
+                    random.Random((seed * 1000003 + int(gidx[a])) * 131 + j).shuffle(s)
                     rec[i] = "".join(s)[: len(r[i])]
                 elif f.feature and f.is_categorical:
-                    rec[i] = r[i] if coin[a, j] else nrec[i]
+                    rec[i] = r[i] if int(newC[o, 0]) == 0 else nrec[i]
             for c, i in enumerate(num_cols):
-                v = float(new[a, j, c])
+                v = float(newX[o, c])
                 rec[i] = str(int(v)) if fields[i].is_integer else f"{v:.{prec}f}"
-            out.append(d.join(rec))
-    ctx.emit(out)
+            outs.append(d.join(rec))
+    ctx.emit(outs)
 
 
 @job("kolmogorovSmirnovModelDrift", "KS drift between reference and current distributions (S/explore/KolmogorovSmirnovModelDrift.scala)")

@@ -387,28 +387,43 @@ def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact
 @job("underSamplingBalancer", "class-balancing under-sampling (J/explore/UnderSamplingBalancer.java, usb.*)")
 def undersampling(args):
     """Keeps a record of a class with global count n_c with probability min_c / n_c (the class
-    counts are all-reduced first, instead of the reference's per-mapper warm-up batch estimate)."""
+    counts are all-reduced first, instead of the reference's per-mapper warm-up batch estimate);
+    the draw of record g is the K25 Philox stream at the GLOBAL record index, so the kept set does
+    not depend on the world size (models/sampling.undersample)."""
+    from ..models.sampling import undersample
     ctx = JobContext(args, "usb.")
     lines = ctx.lines()
     cls_ord = ctx.get_int("class.attr.ord")
     sp = ctx.split
     vals = ctx.union(sp(l)[cls_ord] for l in lines)
-    y = torch.tensor([vals.index(sp(l)[cls_ord]) for l in lines], dtype=torch.long)
-    C = torch.bincount(y, minlength=len(vals)).double()
-    ctx.all_reduce(C)
-    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + 7919 * ctx.comm.rank)
-    minc = float(C[C > 0].min())
-    keep = torch.rand(len(lines), generator=g) < (minc / C.clamp_min(1))[y]
+    vi = {v: i for i, v in enumerate(vals)}
+    y = torch.tensor([vi[sp(l)[cls_ord]] for l in lines], dtype=torch.long)
+    keep = undersample(y, seed=ctx.get_int("random.seed", 0), comm=ctx.comm)
     ctx.emit([l for l, k in zip(lines, keep.tolist()) if k])
 
 
 @job("baggingSampler", "bootstrap resampling within batches (J/explore/BaggingSampler.java, bas.batch.size)")
 def bagging(args):
+    """Output slot g (global record order) copies record b0 + floor(u(seed, g) * batch) of its batch
+    (models/sampling.bagging_indices, K25 Philox at the global index): the same records whatever
+    the world size; picks that another rank holds (batches crossing a shard boundary) are fetched
+    with one object all-gather of the requests and one of the answers."""
     from ..models.sampling import bagging_indices
     ctx = JobContext(args, "bas.")
     lines = ctx.lines()
-    idx = bagging_indices(len(lines), ctx.get_int("batch.size", 10000), seed=ctx.get_int("random.seed", 0) + ctx.comm.rank)
-    ctx.emit([lines[i] for i in idx.tolist()])
+    comm = ctx.comm
+    sizes = comm.all_gather_object(len(lines)) if comm.is_distributed else [len(lines)]
+    base, total = sum(sizes[: comm.rank]), sum(sizes)
+    idx = bagging_indices(len(lines), ctx.get_int("batch.size", 10000), seed=ctx.get_int("random.seed", 0),
+                          base=base, total=total).tolist()
+    remote = sorted({i for i in idx if not base <= i < base + len(lines)})
+    got = {}
+    if comm.is_distributed:
+        reqs = comm.all_gather_object(remote)
+        mine = {i: lines[i - base] for r in reqs for i in r if base <= i < base + len(lines)}
+        for part in comm.all_gather_object(mine):
+            got.update(part)
+    ctx.emit([lines[i - base] if base <= i < base + len(lines) else got[i] for i in idx])
 
 
 @job("adaBoostError", "weighted misclassification error (J/explore/AdaBoostError.java, abe.*)")

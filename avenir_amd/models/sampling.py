@@ -22,33 +22,74 @@ from ..parallel.comm import Comm, get_comm
 from .similarity import top_matches_by_class
 
 
+def _row_base(n: int, comm) -> tuple[int, list[int]]:
+    """(global index of this rank's first row, every rank's row count)."""
+    if comm is None or not comm.is_distributed:
+        return 0, [n]
+    sizes = [int(x) for x in comm.all_gather_object(int(n))]
+    return sum(sizes[: comm.rank]), sizes
+
+
 def smote(X: torch.Tensor, y: torch.Tensor, minority: int, n_new: int, k: int = 5, seed: int = 0,
-          cat_cols: torch.Tensor | None = None, pick: str = "uniform") -> tuple[torch.Tensor, torch.Tensor]:
-    """Return (new_X [n_new, D], new_cat [n_new, Fc] or None) for the minority class."""
-    g = torch.Generator(device="cpu")
-    g.manual_seed(seed)
+          cat_cols: torch.Tensor | None = None, pick: str = "uniform", exp_mean: float = 1.0,
+          comm: Comm | None = None) -> tuple[torch.Tensor, torch.Tensor | None]:
+    """SMOTE over this rank's rows (ClassBasedOverSampler, J/explore/ClassBasedOverSampler.java:
+    125-200): ``n_new`` synthetic minority records over ALL ranks.  Minority record g (global order)
+    seeds ``n_new // m + (g < n_new % m)`` synthetic records; its k same-class neighbours are found
+    among every rank's minority records (distributed_knn ring, no all-gather of X) and their rows
+    fetched by id; pick / gap / categorical coin come from the K25 kernel's Philox draws keyed by
+    (seed, record, copy).  The rank-ordered concatenation of the outputs does not depend on the world
+    size.  Returns (new_X [*, D], new_cat [*, Fc] or None)."""
+    from ..ops import resample_ops as RS
+    comm = comm or get_comm()
+    dist_mode = comm.is_distributed
     idx = torch.nonzero(y == minority).squeeze(1)
-    Xm = X[idx].float()
-    _, nb = dist.knn(Xm, Xm, min(k, max(1, Xm.shape[0] - 1)), "euclidean", exclude_self=True)
-    src = torch.randint(0, Xm.shape[0], (n_new,), generator=g).to(X.device)
-    col = torch.randint(0, nb.shape[1], (n_new,), generator=g).to(X.device)
-    nbr = nb[src, col].clamp_min(0)
-    gap = torch.rand((n_new, 1), generator=g).to(X.device)
-    newX = Xm[src] + gap * (Xm[nbr] - Xm[src])
-    newC = None
+    Xm = X[idx].float().contiguous()
+    m_loc = Xm.shape[0]
+    gbase, sizes = _row_base(m_loc, comm if dist_mode else None)
+    m = sum(sizes)
+    D = X.shape[1]
+    if m == 0 or n_new <= 0:
+        return X.new_zeros((0, D)).float(), (None if cat_cols is None else cat_cols.new_zeros((0, cat_cols.shape[1])))
+    kk = max(1, min(k, m - 1))
+    gid = torch.arange(gbase, gbase + m_loc, device=X.device)
+    _, nb = dist.distributed_knn(Xm, Xm, kk + 1, comm if dist_mode else _SelfComm(), r_ids=gid)
+    keep = (nb != gid.view(-1, 1)) & (nb >= 0)                              # drop self
+    slot = keep.long().cumsum(1) - 1
+    nbk = torch.full((m_loc, kk), -1, dtype=torch.long, device=X.device)
+    rr, cc = torch.nonzero(keep & (slot < kk), as_tuple=True)
+    nbk[rr, slot[rr, cc]] = nb[rr, cc]
+    nn = (nbk >= 0).sum(1).int()
+    tables = [Xm] + ([cat_cols[idx].int().contiguous()] if cat_cols is not None else [])
+    if dist_mode:
+        fetched = comm.fetch_rows(nbk.view(-1), tables, gbase, sizes)
+    else:
+        fetched = [t[nbk.view(-1).clamp_min(0)] for t in tables]
+    Xn = fetched[0].view(m_loc, kk, D).contiguous()
+    Cs = Cn = None
     if cat_cols is not None:
-        Cm = cat_cols[idx]
-        if pick == "exponential":
-            u = torch.rand(n_new, generator=g).to(X.device)
-            take_src = (-torch.log(u.clamp_min(1e-12))) < 1.0
-        else:
-            take_src = torch.rand(n_new, generator=g).to(X.device) < 0.5
-        newC = torch.where(take_src.unsqueeze(1), Cm[src], Cm[nbr])
-    return newX, newC
+        Cs = tables[1]
+        Cn = fetched[1].view(m_loc, kk, -1).contiguous()
+    mult = -(-n_new // m)
+    newX, newC, _ = RS.smote_rows(Xm, Xn, nn, Cs, Cn, mult, gbase, seed, pick == "exponential", exp_mean)
+    # record g keeps copies j < n_new // m + (g < n_new % m)
+    gi = torch.arange(gbase, gbase + m_loc, device=newX.device).repeat_interleave(mult)
+    j = torch.arange(mult, device=newX.device).repeat(m_loc)
+    take = j < (n_new // m + (gi < n_new % m).long())
+    return newX[take], (newC[take] if cat_cols is not None else None)
+
+
+class _SelfComm:
+    is_distributed = False
+    world = 1
+    rank = 0
 
 
 def undersample(y: torch.Tensor, seed: int = 0, comm: Comm | None = None) -> torch.Tensor:
-    """Boolean keep-mask balancing classes down to the minority count (global counts)."""
+    """Boolean keep-mask balancing classes down to the minority count: record g of class c is kept
+    when u(seed, g) < min_count / count_c (global counts; K25 Philox keyed by the GLOBAL record
+    index, so the mask does not depend on the world size)."""
+    from ..ops import resample_ops as RS
     comm = comm or get_comm()
     C = int(y.max()) + 1 if y.numel() else 1
     cnt = torch.bincount(y.long(), minlength=C).double()
@@ -58,23 +99,28 @@ def undersample(y: torch.Tensor, seed: int = 0, comm: Comm | None = None) -> tor
         if int(C2) > C:
             cnt = torch.cat([cnt, torch.zeros(int(C2) - C, dtype=cnt.dtype, device=cnt.device)])
         comm.all_reduce(cnt)
-    minc = float(cnt[cnt > 0].min())
-    keep_p = (minc / cnt.clamp_min(1))[y.long()]
-    g = torch.Generator(device="cpu")
-    g.manual_seed(seed + 7919 * comm.rank)
-    return torch.rand(y.shape[0], generator=g).to(y.device) < keep_p
+    base, _ = _row_base(y.shape[0], comm)
+    minc = float(cnt[cnt > 0].min()) if bool((cnt > 0).any()) else 0.0
+    keep_p = (minc / cnt.clamp_min(1))[y.long()].float()
+    u = RS.uniform(seed, RS.STREAM_UNDERSAMPLE, base, y.shape[0], y.device).to(y.device)
+    return u <= keep_p
 
 
-def bagging_indices(n: int, batch_size: int | None = None, seed: int = 0) -> torch.Tensor:
-    """Bootstrap indices (with replacement) drawn within consecutive batches."""
-    g = torch.Generator(device="cpu")
-    g.manual_seed(seed)
-    bs = batch_size or n
-    out = []
-    for s in range(0, n, bs):
-        m = min(bs, n - s)
-        out.append(s + torch.randint(0, m, (m,), generator=g))
-    return torch.cat(out) if out else torch.zeros(0, dtype=torch.long)
+def bagging_indices(n: int, batch_size: int | None = None, seed: int = 0, base: int = 0,
+                    total: int | None = None, device="cpu") -> torch.Tensor:
+    """Bootstrap positions (with replacement) drawn within consecutive batches of the GLOBAL record
+    order (BaggingSampler, J/explore/BaggingSampler.java:117-122): output slot g of batch
+    [b0, b1) takes record b0 + floor(u(seed, g) * (b1 - b0)).  Slots [base, base + n) of ``total``
+    records; returns GLOBAL record ids (a rank fetches the ones it does not hold)."""
+    from ..ops import resample_ops as RS
+    total = n if total is None else total
+    bs = batch_size or total
+    g = torch.arange(base, base + n, dtype=torch.long)
+    b0 = (g // bs) * bs
+    b1 = torch.clamp(b0 + bs, max=total)
+    u = RS.uniform(seed, RS.STREAM_BAGGING, base, n, "cpu").double()
+    pick = b0 + torch.minimum((u * (b1 - b0).double()).long(), (b1 - b0 - 1).clamp_min(0))
+    return pick.to(device)
 
 
 class AdaBoost:
@@ -106,62 +152,56 @@ class AdaBoost:
 
 def relief(X: torch.Tensor, y: torch.Tensor, k: int = 1, ranges: torch.Tensor | None = None,
            comm: Comm | None = None) -> torch.Tensor:
-    """Relief feature relevance [D]: sum over records of (miss diff - hit diff) / n, diffs normalised
-    by the attribute range.  With row shards on several ranks the neighbours are searched over ALL
-    ranks' records (one all-gather of the shard, as TopMatchesByClass joins every pair) and the
-    ranges are global, so the score equals the single-process one."""
+    """Relief feature relevance [D]: sum over records of (miss diff - hit diff) / (n k), diffs
+    normalised by the attribute range (J/explore/ReliefFeatureRelevance.java:119-232).  Sharded:
+    the hits (nearest same-class, self excluded) and misses (nearest other-class) of this rank's
+    rows are searched over ALL ranks' records by the distributed_knn ring (class subsets travel
+    with their global ids), the neighbour rows are fetched by id with two all-to-alls, and the
+    ranges are one min / max all-reduce — no rank ever holds more than its shard plus n*k fetched
+    rows (the previous design all-gathered X)."""
     comm = comm or get_comm()
-    X = X.float()
+    X = X.float().contiguous()
+    y = y.long()
     dist_mode = comm.is_distributed
-    if dist_mode:
-        dev = comm.device if comm.backend == "nccl" else torch.device("cpu")
-        Xa = comm.all_gather_v(X.to(dev)).to(X.device)
-        ya = comm.all_gather_v(y.to(dev).long()).to(X.device)
-        sizes = comm.all_gather(torch.tensor([X.shape[0]], dtype=torch.long, device=dev)).view(-1).tolist()
-        base = int(sum(sizes[:comm.rank]))
+    cm = comm if dist_mode else _SelfComm()
+    base, sizes = _row_base(X.shape[0], comm if dist_mode else None)
+    if ranges is None:
+        lo = X.min(0).values if X.shape[0] else torch.full((X.shape[1],), float("inf"), device=X.device)
+        hi = X.max(0).values if X.shape[0] else torch.full((X.shape[1],), float("-inf"), device=X.device)
+        if dist_mode:
+            comm.all_reduce(lo, "min")
+            comm.all_reduce(hi, "max")
+        rng = hi - lo
     else:
-        Xa, ya, base = X, y, 0
-    rng = (Xa.max(0).values - Xa.min(0).values) if ranges is None else ranges.float().to(X.device)
+        rng = ranges.float().to(X.device)
     rng = rng.clamp_min(1e-12)
+    C = torch.tensor([float(int(y.max()) + 1 if y.numel() else 0)], device=X.device)
     if dist_mode:
-        hit, miss = _global_matches(X, y.long(), Xa, ya, base, k)
-    else:
-        _, hit = top_matches_by_class(X, y, k, same_class=True)
-        _, miss = top_matches_by_class(X, y, k, same_class=False)
-    score = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
-    for j in range(k):
-        h, m = hit[:, j], miss[:, j]
-        okh, okm = h >= 0, m >= 0
-        score -= ((X[okh] - Xa[h[okh]]).abs() / rng).double().sum(0)
-        score += ((X[okm] - Xa[m[okm]]).abs() / rng).double().sum(0)
-    n = torch.tensor([float(X.shape[0] * k)], dtype=torch.float64, device=X.device)
-    if dist_mode:
-        comm.all_reduce(score)
-        comm.all_reduce(n)
-    return (score / n).float()
-
-
-def _global_matches(X, y, Xa, ya, base: int, k: int):
-    """Nearest same-class (hits, self excluded by global id) and other-class (misses) records of
-    this rank's rows among all records: global row ids [n, k] (-1 when fewer)."""
-    from ..ops import distance as dist
+        comm.all_reduce(C, "max")
     n = X.shape[0]
+    gid = torch.arange(base, base + n, device=X.device)
     hit = torch.full((n, k), -1, dtype=torch.long, device=X.device)
     miss = torch.full((n, k), -1, dtype=torch.long, device=X.device)
-    for c in torch.unique(ya).tolist():
+    for c in range(int(C.item())):          # every rank walks the same classes (collective ring)
         qi = torch.nonzero(y == c).squeeze(1)
-        if qi.numel() == 0:
-            continue
-        ri = torch.nonzero(ya == c).squeeze(1)
-        if ri.numel():
-            _, i = dist.knn(X[qi], Xa[ri], min(k + 1, ri.numel()))
-            gi = torch.where(i >= 0, ri[i.clamp_min(0)], i)
-            keep = (gi != (qi + base).view(-1, 1)) & (gi >= 0)                  # drop self
-            slot = keep.long().cumsum(1) - 1
-            rr, cc = torch.nonzero(keep & (slot < k), as_tuple=True)
-            hit[qi[rr], slot[rr, cc]] = gi[rr, cc]
-        ro = torch.nonzero(ya != c).squeeze(1)
-        if ro.numel():
-            _, i = dist.knn(X[qi], Xa[ro], k)
-            miss[qi] = torch.where(i >= 0, ro[i.clamp_min(0)], i)
-    return hit, miss
+        oi = torch.nonzero(y != c).squeeze(1)
+        _, hh = dist.distributed_knn(X[qi], X[qi], k + 1, cm, r_ids=gid[qi])
+        keep = (hh != gid[qi].view(-1, 1)) & (hh >= 0)
+        slot = keep.long().cumsum(1) - 1
+        rr, cc = torch.nonzero(keep & (slot < k), as_tuple=True)
+        hit[qi[rr], slot[rr, cc]] = hh[rr, cc]
+        _, mm = dist.distributed_knn(X[qi], X[oi], k, cm, r_ids=gid[oi])
+        miss[qi] = mm
+    if dist_mode:
+        Xh, Xmiss = (comm.fetch_rows(hit.view(-1), [X], base, sizes)[0].view(n, k, -1),
+                     comm.fetch_rows(miss.view(-1), [X], base, sizes)[0].view(n, k, -1))
+    else:
+        Xh, Xmiss = X[hit.clamp_min(0)], X[miss.clamp_min(0)]
+    dh = ((X.unsqueeze(1) - Xh).abs() / rng).double() * (hit >= 0).unsqueeze(2)
+    dm = ((X.unsqueeze(1) - Xmiss).abs() / rng).double() * (miss >= 0).unsqueeze(2)
+    score = (dm.sum((0, 1)) - dh.sum((0, 1)))
+    cnt = torch.tensor([float(n * k)], dtype=torch.float64, device=X.device)
+    if dist_mode:
+        comm.all_reduce(score)
+        comm.all_reduce(cnt)
+    return (score / cnt).float()

@@ -90,14 +90,28 @@ def merge_topk(d1, i1, d2, i2, k):
     return v, torch.gather(i, 1, j)
 
 
+def _merge_topk_by_id(d1, i1, d2, i2, k):
+    """merge_topk with ties broken by the smaller global id (order-independent)."""
+    d = torch.cat([d1, d2], 1)
+    i = torch.cat([i1, i2], 1)
+    o = torch.argsort(torch.where(i >= 0, i, torch.full_like(i, 1 << 62)), dim=1, stable=True)
+    d, i = torch.gather(d, 1, o), torch.gather(i, 1, o)
+    o = torch.argsort(d, dim=1, stable=True)[:, :k]
+    return torch.gather(d, 1, o), torch.gather(i, 1, o)
+
+
 def distributed_knn(Q: torch.Tensor, R: torch.Tensor, k: int, comm, metric: str = "euclidean",
-                    r_base: int = 0, q_base: int = 0, exclude_self: bool = False):
+                    r_base: int = 0, q_base: int = 0, exclude_self: bool = False, r_ids: torch.Tensor | None = None):
     """Systolic all-pairs kNN: every rank keeps its query shard and passes its reference shard
     around the ring — no bucket-pair replication.  The shard sizes are exchanged
     ONCE up front (one all-gather), so every hop's receive buffer and global index base are known on
     the host; the send/receive of the NEXT shard is posted (``Comm.ring_pass_start``) before the
     fused distance + top-k of the current one, so the transfer over xGMI overlaps the compute.
-    ``r_base`` is this rank's global index offset of R (kept for the single-rank path)."""
+    ``r_base`` is this rank's global index offset of R (kept for the single-rank path).
+    ``r_ids``: explicit global ids of R's rows (e.g. a class subset of a shard); they travel around
+    the ring with the rows and are what the result indexes (``exclude_self`` not supported then)."""
+    if r_ids is not None:
+        return _distributed_knn_ids(Q, R, r_ids.long(), k, comm, metric)
     if not comm.is_distributed:
         return knn(Q, R, k, metric, exclude_self=exclude_self, q_base=q_base, r_base=r_base)
     best_d = torch.full((Q.shape[0], k), math.inf, device=Q.device)
@@ -119,6 +133,34 @@ def distributed_knn(Q: torch.Tensor, R: torch.Tensor, k: int, comm, metric: str 
         best_d, best_i = merge_topk(best_d, best_i, d, i, k)
         if pending is not None:
             cur = comm.ring_pass_finish(pending)
+    return best_d, best_i
+
+
+def _distributed_knn_ids(Q, R, ids, k, comm, metric):
+    """distributed_knn over reference rows carrying explicit global ids (ring of (rows, ids))."""
+    best_d = torch.full((Q.shape[0], k), math.inf, device=Q.device)
+    best_i = torch.full((Q.shape[0], k), -1, dtype=torch.long, device=Q.device)
+    W, me = comm.world, comm.rank
+    sizes = [R.shape[0]]
+    if comm.is_distributed:
+        sizes = comm.all_gather(torch.tensor([R.shape[0]], dtype=torch.long, device=Q.device)).view(-1).tolist()
+    cur, cur_ids = R.contiguous(), ids.contiguous()
+    for step in range(W):
+        pending = None
+        if step + 1 < W:
+            src = (me - step - 1) % W
+            pending = (comm.ring_pass_start(cur, sizes[src]), comm.ring_pass_start(cur_ids, sizes[src]))
+        if cur.shape[0] and Q.shape[0]:
+            d, i = knn(Q, cur, min(k, cur.shape[0]), metric)
+            gi = torch.where(i >= 0, cur_ids[i.clamp_min(0)], i)
+            if d.shape[1] < k:
+                pad = k - d.shape[1]
+                d = torch.cat([d, torch.full((d.shape[0], pad), math.inf, device=d.device)], 1)
+                gi = torch.cat([gi, torch.full((gi.shape[0], pad), -1, dtype=gi.dtype, device=gi.device)], 1)
+            best_d, best_i = _merge_topk_by_id(best_d, best_i, d, gi, k)
+        if pending is not None:
+            cur = comm.ring_pass_finish(pending[0])
+            cur_ids = comm.ring_pass_finish(pending[1])
     return best_d, best_i
 
 

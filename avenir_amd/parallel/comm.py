@@ -207,6 +207,38 @@ class Comm:
             recv = recv.to(dev)
         return list(torch.split(recv, rs))
 
+    def fetch_rows(self, gids: torch.Tensor, tables: list[torch.Tensor], base: int, sizes: list[int]) -> list[torch.Tensor]:
+        """Rows ``gids`` (global row ids; -1 = none -> zeros) of row-sharded ``tables`` (this rank holds
+        global rows [base, base + len)), ``sizes`` = every rank's row count.  Two all-to-alls (the
+        requests, then the rows) instead of an all-gather of every table: O(requested rows)."""
+        dev = gids.device
+        g = gids.long().view(-1)
+        if not self.is_distributed:
+            li = (g - base).clamp(0, max(0, tables[0].shape[0] - 1)) if tables and tables[0].shape[0] else g.clamp_min(0)
+            out = []
+            for t in tables:
+                v = t[li] if t.shape[0] else torch.zeros((g.numel(),) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+                out.append(torch.where((g >= 0).view((-1,) + (1,) * (t.dim() - 1)), v, torch.zeros_like(v)))
+            return out
+        starts = torch.tensor([sum(sizes[:r]) for r in range(self.world)], dtype=torch.long, device=dev)
+        owner = (torch.searchsorted(starts, g.clamp_min(0), right=True) - 1).clamp_min(0)
+        owner = torch.where(g >= 0, owner, torch.full_like(owner, self.rank))
+        order = torch.argsort(owner, stable=True)
+        counts = torch.bincount(owner, minlength=self.world).tolist()
+        req = self.all_to_all_v(list(torch.split(g[order], counts)))          # ids others want from me
+        want = torch.cat(req) if req else torch.zeros(0, dtype=torch.long, device=dev)
+        li = (want - base).clamp(0, max(0, tables[0].shape[0] - 1))
+        back_counts = [r.shape[0] for r in req]
+        out = []
+        for t in tables:
+            v = t[li] if t.shape[0] else torch.zeros((want.numel(),) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+            v = torch.where((want >= 0).view((-1,) + (1,) * (t.dim() - 1)), v, torch.zeros_like(v))
+            got = torch.cat(self.all_to_all_v(list(torch.split(v, back_counts))))  # in my request order
+            res = torch.empty_like(got)
+            res[order] = got
+            out.append(res)
+        return out
+
     def ring_pass(self, t: torch.Tensor) -> torch.Tensor:
         """Send ``t`` to rank+1 and receive from rank-1 (systolic all-pairs schedule).  Shapes may
         differ between ranks: the dim-0 length travels first."""
