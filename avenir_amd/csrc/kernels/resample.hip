@@ -61,8 +61,11 @@ __global__ __launch_bounds__(RS_T) void smote_kernel(const float* __restrict__ X
     const float* src = X + r * D;
     const float* nb = cnt > 0 ? Xn + (r * k + pick) * D : src;
     float* dst = outX + o * D;
-    // no contraction into an FMA: the host twin rounds the product and the sum separately
-    for (int c = 0; c < D; ++c) dst[c] = __fadd_rn(src[c], __fmul_rn(gap, __fsub_rn(nb[c], src[c])));
+    {
+      // no contraction into an FMA: the host twin rounds the product and the sum separately
+#pragma clang fp contract(off)
+      for (int c = 0; c < D; ++c) dst[c] = src[c] + gap * (nb[c] - src[c]);
+    }
     if (Dc > 0) {
       const bool take_src = (d.z >> 31) != 0;
       const int* cs = Cs + r * Dc;

@@ -23,33 +23,36 @@ def rule_miner(args):
     lengths).  Every proper subset (size <= ``arm.max.ante.size``) of a set is an antecedent;
     confidence = support(set) / support(antecedent); lines ``a,b -> c`` when above
     ``arm.conf.threshold`` (:111-196)."""
+    from ..models.association import FrequentItemsets, association_rules
     ctx = JobContext(args, "arm.")
     max_ante = ctx.get_int("max.ante.size", 3)
     thr = ctx.get_float("conf.threshold")
     sup = {}
     for r in ctx.rows(shard=False):
         sup[tuple(r[:-1])] = float(r[-1])
-    items = sorted(sup)
-    if ctx.comm.is_distributed:
-        from ..data.table import shard_range
-        a, b = shard_range(len(items), ctx.comm.rank, ctx.comm.world)
-        items = items[a:b]
-    out = []
-    for s in items:
-        if len(s) < 2:
-            continue
-        for k in range(1, min(max_ante, len(s) - 1) + 1):
-            for ante in itertools.combinations(s, k):
-                sa = sup.get(ante)
-                if sa is None:
-                    sa = sup.get(tuple(sorted(ante)))
-                if not sa:
-                    continue
-                if sup[s] / sa > thr:
-                    cons = [x for x in s if x not in ante]
-                    out.append(",".join(ante) + " -> " + ",".join(cons))
-    out = ctx.gather_lines(out)
-    ctx.emit_root(out)
+    # the sets as item-id rows (ids in name order; every row sorted) with float supports: the
+    # antecedent joins and confidences run on the device (models/association.association_rules)
+    names = sorted({x for s_ in sup for x in s_})
+    nid = {v: i for i, v in enumerate(names)}
+    by_len: dict[int, list] = {}
+    for s_, v in sup.items():
+        by_len.setdefault(len(s_), []).append((sorted(nid[x] for x in s_), v))
+    dev = ctx.device
+    sets, sups = {}, {}
+    for k, lst in by_len.items():
+        lst.sort()
+        sets[k] = torch.tensor([e[0] for e in lst], dtype=torch.long, device=dev)
+        sups[k] = torch.tensor([e[1] for e in lst], dtype=torch.float64, device=dev)
+    fi = FrequentItemsets(names, None, 1, sets, sups)
+    rules = association_rules(fi, thr, min_len=2, max_ante=max_ante)
+    # the reference's order: sets in name order, antecedent size, combination
+    keyed = []
+    for ante, cons, _, _ in rules:
+        full = tuple(sorted(ante + cons))
+        pos = tuple(full.index(x) for x in ante)
+        keyed.append(((full, len(ante), pos), ",".join(ante) + " -> " + ",".join(cons)))
+    keyed.sort(key=lambda e: e[0])
+    ctx.emit_root([line for _, line in keyed])
 
 
 @job("infrequentItemMarker", "replace items outside the frequent 1-item sets by a marker (J/association/InfrequentItemMarker.java, iim.*)")

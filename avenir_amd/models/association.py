@@ -13,7 +13,7 @@ MI355X: transactions become item bit rows ([I, T/64] uint64, built on device), e
 from __future__ import annotations
 
 import itertools
-from dataclasses import dataclass
+import math
 
 import torch
 
@@ -22,14 +22,12 @@ from ..parallel.comm import Comm, get_comm
 from ..utils.resilience import IterationLoop, RecoveryConfig
 
 
+_POP8 = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64)
+
+
 def _popcount64(x: torch.Tensor) -> torch.Tensor:
-    """CPU popcount of int64 words (reference path)."""
-    v = x.clone()
-    c = torch.zeros_like(v)
-    for _ in range(64):
-        c += v & 1
-        v = torch.bitwise_right_shift(v, 1) & 0x7FFFFFFFFFFFFFFF
-    return c
+    """CPU popcount of int64 words (reference path): a 256-entry byte table over the 8 bytes."""
+    return _POP8[x.contiguous().view(torch.uint8).long()].view(*x.shape, 8).sum(-1)
 
 
 def build_bitsets(tx: torch.Tensor, item: torch.Tensor, n_tx: int, n_items: int) -> torch.Tensor:
@@ -49,14 +47,38 @@ def itemset_support(P: torch.Tensor, items: torch.Tensor, cand_prefix: torch.Ten
                     cand_item: torch.Tensor) -> torch.Tensor:
     if P.is_cuda:
         return _native.C().itemset_support(P, items, cand_prefix.int().contiguous(), cand_item.int().contiguous())
-    return _popcount64(P[cand_prefix.long()] & items[cand_item.long()]).sum(1)
+    out = torch.empty(cand_prefix.numel(), dtype=torch.int64)
+    step = max(1, (1 << 22) // max(1, P.shape[1]))             # bounded temporaries
+    for a in range(0, cand_prefix.numel(), step):
+        b = min(cand_prefix.numel(), a + step)
+        out[a:b] = _popcount64(P[cand_prefix[a:b].long()] & items[cand_item[a:b].long()]).sum(1)
+    return out
 
 
-@dataclass
 class FrequentItemsets:
-    items: list[str]
-    levels: dict[int, list[tuple[tuple[int, ...], int]]]   # k -> [(itemset as item ids, support count)]
-    n_transactions: int
+    """Frequent item sets per length: ``sets[k]`` int64 [N_k, k] item ids (rows sorted
+    lexicographically, items ascending within a row) and ``sups[k]`` int64 [N_k] support counts, on
+    the device that mined them; ``levels`` is the list view ({k: [(item-id tuple, count)]})."""
+
+    def __init__(self, items: list[str], levels: dict | None = None, n_transactions: int = 0,
+                 sets: dict | None = None, sups: dict | None = None):
+        self.items = items
+        self.n_transactions = n_transactions
+        self.sets: dict[int, torch.Tensor] = dict(sets or {})
+        self.sups: dict[int, torch.Tensor] = dict(sups or {})
+        if levels is not None:
+            for k, lv in levels.items():
+                self.sets[k] = (torch.tensor([e[0] for e in lv], dtype=torch.long) if lv
+                                else torch.zeros((0, k), dtype=torch.long))
+                self.sups[k] = torch.tensor([e[1] for e in lv], dtype=torch.long)
+        self._levels = None
+
+    @property
+    def levels(self) -> dict[int, list[tuple[tuple[int, ...], int]]]:
+        if self._levels is None:
+            self._levels = {k: [(tuple(a), int(b)) for a, b in zip(self.sets[k].tolist(), self.sups[k].tolist())]
+                            for k in sorted(self.sets)}
+        return self._levels
 
     def support(self, itemset: tuple[int, ...]) -> int | None:
         for s, c in self.levels.get(len(itemset), []):
@@ -66,6 +88,71 @@ class FrequentItemsets:
 
     def as_names(self, k: int) -> list[tuple[list[str], float]]:
         return [([self.items[i] for i in s], c / self.n_transactions) for s, c in self.levels.get(k, [])]
+
+
+def _set_keys(S: torch.Tensor, base: int) -> torch.Tensor:
+    """Order-preserving int64 key of every row (item ids ascending): exact mixed radix ``base``
+    when base^k < 2^62, else a 64-bit polynomial hash (membership is then verified row-wise)."""
+    k = S.shape[1]
+    key = torch.zeros(S.shape[0], dtype=torch.long, device=S.device)
+    if k * math.log2(max(base, 2)) < 62:
+        for j in range(k):
+            key = key * base + S[:, j]
+        return key
+    for j in range(k):
+        key = key * 1000003 + S[:, j] + 1
+        key = key ^ (key >> 29)
+    return key
+
+
+def _lookup(S: torch.Tensor, Q: torch.Tensor, base: int) -> torch.Tensor:
+    """Row index of every row of ``Q`` in the row set ``S`` (-1 when absent), exact."""
+    if S.shape[0] == 0 or Q.shape[0] == 0:
+        return torch.full((Q.shape[0],), -1, dtype=torch.long, device=Q.device)
+    ks = _set_keys(S, base)
+    order = torch.argsort(ks)
+    kss = ks[order]
+    kq = _set_keys(Q, base)
+    pos = torch.searchsorted(kss, kq).clamp_max(kss.numel() - 1)
+    row = order[pos]
+    hit = (kss[pos] == kq) & (S[row] == Q).all(1)
+    return torch.where(hit, row, torch.full_like(row, -1))
+
+
+def candidates(S: torch.Tensor, n_items: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Apriori candidate generation on the device (S/association/FrequentItemsApriori.scala:222-262):
+    the frequent (k-1)-sets ``S`` [N, k-1] (sorted rows) joined with every later row of the same
+    (k-2)-prefix group — a segmented expansion, the K18 self-join pattern — then every candidate
+    whose other (k-1)-subsets are not all frequent is pruned by an exact sorted-key lookup.
+    Returns (prefix row a [M], candidates [M, k]) in lexicographic order."""
+    N, km1 = S.shape
+    dev = S.device
+    if N < 2:
+        return torch.zeros(0, dtype=torch.long, device=dev), torch.zeros((0, km1 + 1), dtype=torch.long, device=dev)
+    if km1 == 1:
+        gstart = torch.zeros(N, dtype=torch.long, device=dev)
+        gend = torch.full((N,), N, dtype=torch.long, device=dev)
+    else:
+        pre = S[:, :-1]
+        new = torch.ones(N, dtype=torch.bool, device=dev)
+        new[1:] = (pre[1:] != pre[:-1]).any(1)
+        gid = torch.cumsum(new.long(), 0) - 1
+        starts = torch.nonzero(new).view(-1)
+        ends = torch.cat([starts[1:], torch.tensor([N], device=dev)])
+        gend = ends[gid]
+    cnt = gend - torch.arange(N, device=dev) - 1                 # later rows of the same group
+    a = torch.repeat_interleave(torch.arange(N, device=dev), cnt)
+    first = torch.cumsum(cnt, 0) - cnt
+    b = a + 1 + (torch.arange(a.numel(), device=dev) - first[a])
+    cand = torch.cat([S[a], S[b][:, -1:]], 1)
+    if km1 >= 2 and cand.shape[0]:
+        ok = torch.ones(cand.shape[0], dtype=torch.bool, device=dev)
+        k = km1 + 1
+        for drop in range(k - 2):                # subsets without item `drop` (the last two are S[b], S[a])
+            sub = torch.cat([cand[:, :drop], cand[:, drop + 1:]], 1)
+            ok &= _lookup(S, sub, n_items) >= 0
+        a, cand = a[ok], cand[ok]
+    return a, cand
 
 
 class Apriori:
@@ -112,111 +199,118 @@ class Apriori:
         return self.fit_bitsets(bits, rec.n_lines, items)
 
     def fit_bitsets(self, bits: torch.Tensor, n_tx: int, items: list[str]) -> FrequentItemsets:
+        """Level-wise mining with every level on the device: candidate join + prune
+        (:func:`candidates`), ONE support kernel (AND + popcount of the (k-1)-prefix bit rows with
+        the last item's row, K17), the support vector all-reduced across transaction shards, and a
+        device filter.  The host sees only the level sizes (and the sets at the end)."""
         comm = self.comm or get_comm()
-        total = torch.tensor([n_tx], dtype=torch.int64, device=bits.device)
+        dev = bits.device
+        total = torch.tensor([n_tx], dtype=torch.int64, device=dev)
         if comm.is_distributed:
             comm.all_reduce(total)
         N = int(total)
         min_count = self.threshold * N
         I = bits.shape[0]
-        ones = torch.full((1, bits.shape[1]), -1, dtype=torch.int64, device=bits.device)
+        ones = torch.full((1, bits.shape[1]), -1, dtype=torch.int64, device=dev)
         # level 1: support of every item = popcount(ones & item row)
-        sup = itemset_support(ones, bits, torch.zeros(I, dtype=torch.int32, device=bits.device),
-                              torch.arange(I, dtype=torch.int32, device=bits.device))
+        sup = itemset_support(ones, bits, torch.zeros(I, dtype=torch.int32, device=dev),
+                              torch.arange(I, dtype=torch.int32, device=dev))
         if comm.is_distributed:
             comm.all_reduce(sup)
-        sup_l = sup.cpu().tolist()
-        freq = [((i,), sup_l[i]) for i in range(I) if sup_l[i] > min_count]
-        levels = {1: freq}
-        P = bits[[s[0][0] for s in freq]] if freq else bits[:0]
+        keep = torch.nonzero(sup > min_count).view(-1)
+        sets = {1: keep.view(-1, 1)}
+        sups = {1: sup[keep].long()}
+        S = sets[1]
+        P = bits[keep]
         k = 1
-        lp = IterationLoop("apriori", self.recovery, comm, device=bits.device)
-        _, st, meta = lp.restore(bits.device)
+        lp = IterationLoop("apriori", self.recovery, comm, device=dev)
+        _, st, meta = lp.restore(dev)
         if st is not None:                  # resume after level ``meta['k']``: rebuild the level
-            k = int(meta["k"])              # lists and the prefix bitsets of the last level
-            levels = {}
+            k = int(meta["k"])              # tensors and the prefix bitsets of the last level
+            sets, sups = {}, {}
             for j in range(1, k + 1):
-                if f"l{j}_sets" not in st:
-                    continue
-                sets_t, sup_t = st[f"l{j}_sets"].tolist(), st[f"l{j}_sup"].tolist()
-                levels[j] = [(tuple(a), b) for a, b in zip(sets_t, sup_t)]
-            freq = levels.get(k, [])
-            P = bits[[s[-1] for s, _ in freq]] if freq else bits[:0]
-            if freq:
-                idx = torch.tensor([s for s, _ in freq], dtype=torch.long, device=bits.device)
-                for c in range(k - 1):
-                    P = P & bits[idx[:, c]]
-        while freq and k < self.max_len:
+                if f"l{j}_sets" in st:
+                    sets[j], sups[j] = st[f"l{j}_sets"].to(dev).long(), st[f"l{j}_sup"].to(dev).long()
+            S = sets.get(k, torch.zeros((0, k), dtype=torch.long, device=dev))
+            P = bits[S[:, -1]] if S.shape[0] else bits[:0]
+            for c in range(k - 1):
+                P = P & bits[S[:, c]]
+        while S.shape[0] and k < self.max_len:
             k += 1
             with lp.step(k):
-                sets = [s for s, _ in freq]
-                setidx = {s: j for j, s in enumerate(sets)}
-                cp, ci, cands = [], [], []
-                # join (k-1)-sets sharing their first k-2 items; prune by the Apriori property
-                by_pref: dict[tuple, list[int]] = {}
-                for j, s in enumerate(sets):
-                    by_pref.setdefault(s[:-1], []).append(j)
-                for grp in by_pref.values():
-                    for a, b in itertools.combinations(grp, 2):
-                        sa, sb = sets[a], sets[b]
-                        cand = sa + (sb[-1],) if sa[-1] < sb[-1] else sb + (sa[-1],)
-                        if any(sub not in setidx for sub in itertools.combinations(cand, k - 1)):
-                            continue
-                        base = a if sa[-1] < sb[-1] else b
-                        cp.append(base)
-                        ci.append(cand[-1])
-                        cands.append(cand)
-                if not cands:
+                a, cand = candidates(S, I)
+                if cand.shape[0] == 0:
                     break
-                dev = bits.device
-                cpt = torch.tensor(cp, dtype=torch.int32, device=dev)
-                cit = torch.tensor(ci, dtype=torch.int32, device=dev)
-                sup = itemset_support(P, bits, cpt, cit)
+                sup = itemset_support(P, bits, a.int(), cand[:, -1].int())
                 if comm.is_distributed:
                     comm.all_reduce(sup)
-                sup_l = sup.cpu().tolist()
-                keep = [m for m in range(len(cands)) if sup_l[m] > min_count]
-                freq = [(cands[m], sup_l[m]) for m in keep]
-                if freq:
-                    kt = torch.tensor(keep, dtype=torch.long, device=dev)
-                    P = P[cpt.long()[kt]] & bits[cit.long()[kt]]
-                    order = sorted(range(len(freq)), key=lambda m: freq[m][0])
-                    freq = [freq[m] for m in order]
-                    P = P[torch.tensor(order, dtype=torch.long, device=dev)]
-                    levels[k] = freq
+                keep = torch.nonzero(sup > min_count).view(-1)
+                if keep.numel() == 0:
+                    break
+                S = cand[keep]
+                P = P[a[keep]] & bits[cand[keep, -1]]
+                sets[k], sups[k] = S, sup[keep].long()
             if lp.enabled:
-                lp.commit(k, _levels_state(levels), {"k": k})
+                lp.commit(k, _levels_state(sets, sups), {"k": k})
         lp.close()
-        return FrequentItemsets(items, levels, N)
+        return FrequentItemsets(items, None, N, sets, sups)
 
 
-def _levels_state(levels) -> dict[str, torch.Tensor]:
+def _levels_state(sets, sups) -> dict[str, torch.Tensor]:
     out = {}
-    for j, lv in levels.items():
-        out[f"l{j}_sets"] = (torch.tensor([e[0] for e in lv], dtype=torch.long) if lv
-                             else torch.zeros((0, j), dtype=torch.long))
-        out[f"l{j}_sup"] = torch.tensor([e[1] for e in lv], dtype=torch.long)
+    for j in sets:
+        out[f"l{j}_sets"] = sets[j].cpu()
+        out[f"l{j}_sup"] = sups[j].cpu()
     return out
 
 
-def association_rules(fi: FrequentItemsets, conf_threshold: float = 0.5, min_len: int = 2):
-    """(antecedent names, consequent names, support, confidence) for every rule above threshold."""
-    sup = {s: c for lvl in fi.levels.values() for s, c in lvl}
+def association_rules(fi: FrequentItemsets, conf_threshold: float = 0.5, min_len: int = 2,
+                      max_ante: int | None = None):
+    """(antecedent names, consequent names, support, confidence) of every rule above the threshold
+    (J/association/AssociationRuleMiner.java:111-196): per set length k and antecedent size r, the
+    C(k, r) antecedents of all sets are gathered as one [N_k, C, r] tensor, their supports joined
+    from level r by an exact sorted-key lookup, and the confidences filtered on the device; the
+    host formats only the surviving rules (ordered by set, antecedent size, combination)."""
     out = []
-    for k, lvl in fi.levels.items():
+    I = max(1, len(fi.items))
+    for k in sorted(fi.sets):
         if k < min_len:
             continue
-        for s, c in lvl:
-            for r in range(1, k):
-                for ante in itertools.combinations(s, r):
-                    a = sup.get(ante)
-                    if not a:
-                        continue
-                    conf = c / a
-                    if conf > conf_threshold:
-                        cons = tuple(x for x in s if x not in ante)
-                        out.append(([fi.items[i] for i in ante], [fi.items[i] for i in cons],
-                                    c / fi.n_transactions, conf))
+        S, cs = fi.sets[k], fi.sups[k]
+        if S.shape[0] == 0:
+            continue
+        dev = S.device
+        found = []            # (set idx, r, combo idx, ante cols, cons cols, conf)
+        for r in range(1, k if max_ante is None else min(k, max_ante + 1)):
+            if r not in fi.sets:
+                continue
+            combos = list(itertools.combinations(range(k), r))
+            cidx = torch.tensor(combos, dtype=torch.long, device=dev)                 # [C, r]
+            ante = S[:, cidx]                                                            # [N, C, r]
+            row = _lookup(fi.sets[r], ante.reshape(-1, r), I).view(S.shape[0], len(combos))
+            sa = torch.where(row >= 0, fi.sups[r][row.clamp_min(0)], torch.zeros_like(row))
+            conf = cs.view(-1, 1).double() / torch.where(sa > 0, sa.double(), torch.ones_like(sa, dtype=torch.float64))
+            ok = (row >= 0) & (sa > 0) & (conf > conf_threshold)
+            si, ci = torch.nonzero(ok, as_tuple=True)
+            if si.numel():
+                found.append((si, torch.full_like(si, r), ci, conf[si, ci]))
+        if not found:
+            continue
+        si = torch.cat([f[0] for f in found])
+        rr = torch.cat([f[1] for f in found])
+        ci = torch.cat([f[2] for f in found])
+        cf = torch.cat([f[3] for f in found])
+        key = (si * (k + 1) + rr) * (1 << 20) + ci
+        o = torch.argsort(key)
+        sets_l = S.tolist()
+        sup_l = cs.tolist()
+        combo_cache = {r: list(itertools.combinations(range(k), r)) for r in range(1, k)}
+        for s_, r_, c_, f_ in zip(si[o].tolist(), rr[o].tolist(), ci[o].tolist(), cf[o].tolist()):
+            ids = sets_l[s_]
+            pos = combo_cache[r_][c_]
+            ante = [fi.items[ids[p]] for p in pos]
+            cons = [fi.items[ids[p]] for p in range(k) if p not in pos]
+            out.append((ante, cons, sup_l[s_] / fi.n_transactions, f_))
     return out
 
 

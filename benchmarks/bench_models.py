@@ -89,6 +89,32 @@ def bench_rf_ref(a):
          rows_x_trees_per_s=n * 10 / sec, train_acc=acc, build=getattr(rf, "build_stats", None))
 
 
+def bench_apriori(a):
+    """Apriori with device candidate generation / pruning / support (models/association.py): the
+    tutorial case (resource/freq_items_apriori_tutorial.txt: 50,000 items, 3 seeded triplets,
+    2,000 transactions, support 0.1) and 10^6 transactions x 10^4 items (Zipf items)."""
+    import tempfile
+    from avenir_amd.data import fixtures, synth_text
+    from avenir_amd.data.records import read_records
+    from avenir_amd.models.association import Apriori, association_rules
+    d = tempfile.mkdtemp()
+    cases = []
+    p1 = f"{d}/tut.txt"
+    with open(p1, "w") as fh:
+        fh.write("\n".join(fixtures.freq_items(50000, 3, 2000, seed=1)) + "\n")
+    cases.append(("tutorial_50k_items_2k_tx", p1, 2, 0.1, 4))
+    p2 = f"{d}/big.txt"
+    synth_text.transactions(p2, 1_000_000, n_items=10_000, per_tx=12, seed=2)
+    cases.append(("1M_tx_10k_items", p2, 1, 0.002, 4))
+    for name, path, skip, sup, ml in cases:
+        rec = read_records(path, device="cuda", modes="x" * skip)
+        torch.cuda.synchronize()
+        sec, fi = timed(lambda: Apriori(sup, ml).fit_records(rec, skip))
+        rs, rules = timed(lambda: association_rules(fi, 0.5))
+        emit(model="apriori", case=name, transactions=rec.n_lines, items=len(rec.vocab), support=sup,
+             seconds=sec, levels={k: int(v.shape[0]) for k, v in fi.sets.items()}, rules=len(rules), rules_seconds=rs)
+
+
 def bench_kmeans(a):
     from avenir_amd.models.cluster import KMeans
     n, d, k = a.rows, 16, 16
@@ -152,7 +178,7 @@ def bench_mlp(a):
              steps_per_s=2 * (n // 1024) / sec)
 
 
-BENCHES = {"rf": bench_rf, "rf_ref": bench_rf_ref, "gbt": bench_gbt, "kmeans": bench_kmeans, "logit": bench_logit, "svm": bench_svm,
+BENCHES = {"rf": bench_rf, "rf_ref": bench_rf_ref, "gbt": bench_gbt, "apriori": bench_apriori, "kmeans": bench_kmeans, "logit": bench_logit, "svm": bench_svm,
            "knn": bench_knn, "sa": bench_sa, "mlp": bench_mlp}
 
 
