@@ -52,8 +52,9 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
                      int64_t total_bins, int64_t n_classes, at::Tensor& out, int64_t mode,
                      bool count_labels) {
   CHECK_DEV(codes);
-  const bool wide = codes.scalar_type() == at::kUInt16;
-  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8 or uint16");
+  const bool huge = codes.scalar_type() == at::kInt;
+  const bool wide = huge || codes.scalar_type() == at::kUInt16;
+  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8, uint16 or int32");
   TORCH_CHECK(codes.dim() == 2, "codes must be [F, ld]");
   const int64_t F = codes.size(0), ld = codes.size(1);
   TORCH_CHECK(n <= ld, "n exceeds codes leading dimension");
@@ -69,12 +70,13 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
   int64_t sum_bins = 0;
   std::vector<int> hb(F);
   for (int64_t f = 0; f < F; ++f) {
-    TORCH_CHECK(h_bins[f] > 0 && h_bins[f] <= (wide ? 65535 : 255),
-                wide ? "bins per feature must be in [1,65535]" : "bins per feature must be in [1,255]");
+    const int64_t cap = huge ? 0x7FFFFFFE : (wide ? 65535 : 255);
+    TORCH_CHECK(h_bins[f] > 0 && h_bins[f] <= cap, "bins per feature must be in [1, ", cap, "]");
     hb[f] = (int)h_bins[f];
     sum_bins += h_bins[f];
   }
   TORCH_CHECK(sum_bins + (count_labels ? 1 : 0) <= total_bins, "sum(bins) > total_bins");
+  TORCH_CHECK(n_classes * total_bins < (1LL << 31), "histogram table exceeds 2^31 slots");
   TORCH_CHECK(n_classes >= 1 && n_classes <= 255, "n_classes must be in [1,255]");
   const uint8_t* lab = nullptr;
   if (labels.has_value() && labels->defined()) {
@@ -84,6 +86,13 @@ void class_histogram(const at::Tensor& codes, int64_t n, const c10::optional<at:
     lab = labels->data_ptr<uint8_t>();
   }
   DevGuard g(codes.device());
+  if (huge) {
+    avk::class_histogram_i32(codes.data_ptr<int>(), ld, n, lab, bins.data_ptr<int>(), offs.data_ptr<int>(), (int)F,
+                             (int)total_bins, (int)n_classes, count_labels ? 1 : 0,
+                             reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), (int)mode,
+                             cur_stream(codes));
+    return;
+  }
   if (wide) {
     avk::class_histogram_wide(reinterpret_cast<const uint16_t*>(codes.data_ptr()), ld, n, lab, bins.data_ptr<int>(),
                               offs.data_ptr<int>(), (int)F, (int)total_bins, (int)n_classes, count_labels ? 1 : 0,
@@ -325,6 +334,87 @@ void nb_predict(const at::Tensor& codes, int64_t n, const at::Tensor& offs, cons
   avk::nb_predict(codes.data_ptr<uint8_t>(), codes.size(1), n, (int)codes.size(0),
                   offs.data_ptr<int>(), logp.data_ptr<float>(), ptr_or_null<float>(logfp), TB,
                   ptr_or_null<float>(x), ldx, ncont, ptr_or_null<float>(gmean),
+                  ptr_or_null<float>(ginvstd), ptr_or_null<float>(glognorm),
+                  ptr_or_null<float>(pmean), ptr_or_null<float>(pinvstd),
+                  ptr_or_null<float>(plognorm), logprior.data_ptr<float>(), C, ref_scale ? 1 : 0,
+                  ptr_or_null<float>(post), pred.data_ptr<int>(), lab, conf, cur_stream(codes));
+}
+
+// Wide tables: codes uint8 / uint16 / int32 [F, ld], bins int32 [F] (device), logpT [TB, C] (transposed).
+void nb_predict_wide(const at::Tensor& codes, int64_t n, const at::Tensor& offs, const at::Tensor& bins,
+                     const at::Tensor& logpT,
+                const c10::optional<at::Tensor>& logfp, const c10::optional<at::Tensor>& x,
+                const c10::optional<at::Tensor>& gmean, const c10::optional<at::Tensor>& ginvstd,
+                const c10::optional<at::Tensor>& glognorm, const c10::optional<at::Tensor>& pmean,
+                const c10::optional<at::Tensor>& pinvstd, const c10::optional<at::Tensor>& plognorm,
+                const at::Tensor& logprior, bool ref_scale, const c10::optional<at::Tensor>& post,
+                at::Tensor& pred, const c10::optional<at::Tensor>& labels,
+                const c10::optional<at::Tensor>& confusion) {
+  CHECK_DEV(codes);
+  TORCH_CHECK(codes.scalar_type() == at::kByte || codes.scalar_type() == at::kUInt16 ||
+                  codes.scalar_type() == at::kInt, "codes must be uint8, uint16 or int32");
+  TORCH_CHECK(codes.dim() == 2 && n <= codes.size(1) && codes.is_contiguous(), "codes must be [F, ld>=n]");
+  CHECK_DEV(logpT);
+  CHECK_DTYPE(logpT, at::kFloat);
+  TORCH_CHECK(logpT.dim() == 2 && logpT.is_contiguous(), "logpT must be [TB, C]");
+  const int TB = (int)logpT.size(0), C = (int)logpT.size(1);
+  TORCH_CHECK(C >= 1 && C <= avk::nb_predict_wide_max_classes(), "nb_predict_wide: 1..32 classes");
+  CHECK_DEV(bins);
+  CHECK_DTYPE(bins, at::kInt);
+  TORCH_CHECK(bins.numel() == codes.size(0), "bins must be [F]");
+  {
+    // every valid code indexes inside the table: offs[f] + bins[f] <= TB
+    auto hb = bins.cpu(), ho = offs.cpu();
+    for (int64_t f = 0; f < codes.size(0); ++f)
+      TORCH_CHECK(ho.data_ptr<int>()[f] >= 0 && hb.data_ptr<int>()[f] >= 0 &&
+                      (int64_t)ho.data_ptr<int>()[f] + hb.data_ptr<int>()[f] <= TB, "offs/bins exceed the table");
+  }
+  CHECK_DEV(offs);
+  CHECK_DTYPE(offs, at::kInt);
+  TORCH_CHECK(offs.numel() == codes.size(0), "offs must be [F]");
+  CHECK_DEV(logprior);
+  CHECK_DTYPE(logprior, at::kFloat);
+  TORCH_CHECK(logprior.numel() == C, "logprior must be [C]");
+  CHECK_DEV(pred);
+  CHECK_DTYPE(pred, at::kInt);
+  TORCH_CHECK(pred.numel() >= n, "pred too short");
+  int ncont = 0;
+  long long ldx = 0;
+  if (x.has_value() && x->defined()) {
+    CHECK_DEV((*x));
+    CHECK_DTYPE((*x), at::kFloat);
+    TORCH_CHECK(x->dim() == 2 && n <= x->size(1), "x must be [Fc, ld>=n]");
+    ncont = (int)x->size(0);
+    ldx = x->size(1);
+    TORCH_CHECK(gmean.has_value() && gmean->numel() == (int64_t)C * ncont, "gmean must be [C,Fc]");
+    TORCH_CHECK(ginvstd.has_value() && ginvstd->numel() == (int64_t)C * ncont, "ginvstd");
+    TORCH_CHECK(glognorm.has_value() && glognorm->numel() == (int64_t)C * ncont, "glognorm");
+    if (ref_scale)
+      TORCH_CHECK(pmean.has_value() && pinvstd.has_value() && plognorm.has_value(),
+                  "feature-prior Gaussian params required with ref_scale");
+  }
+  if (ref_scale) TORCH_CHECK(logfp.has_value() && logfp->numel() == TB, "logfp must be [TB]");
+  if (post.has_value() && post->defined()) {
+    CHECK_DEV((*post));
+    TORCH_CHECK(post->numel() >= n * C, "post too short");
+  }
+  const uint8_t* lab = nullptr;
+  unsigned long long* conf = nullptr;
+  if (confusion.has_value() && confusion->defined()) {
+    TORCH_CHECK(labels.has_value() && labels->defined(), "confusion requires labels");
+    CHECK_DEV((*labels));
+    CHECK_DTYPE((*labels), at::kByte);
+    TORCH_CHECK(labels->numel() >= n, "labels too short");
+    CHECK_DEV((*confusion));
+    CHECK_DTYPE((*confusion), at::kLong);
+    TORCH_CHECK(confusion->numel() == (int64_t)C * C, "confusion must be [C,C]");
+    lab = labels->data_ptr<uint8_t>();
+    conf = reinterpret_cast<unsigned long long*>(confusion->data_ptr<int64_t>());
+  }
+  DevGuard g(codes.device());
+  avk::nb_predict_wide(codes.data_ptr(), (int)codes.element_size(), codes.size(1), n, (int)codes.size(0),
+                       offs.data_ptr<int>(), bins.data_ptr<int>(), logpT.data_ptr<float>(), ptr_or_null<float>(logfp),
+                       ptr_or_null<float>(x), ldx, ncont, ptr_or_null<float>(gmean),
                   ptr_or_null<float>(ginvstd), ptr_or_null<float>(glognorm),
                   ptr_or_null<float>(pmean), ptr_or_null<float>(pinvstd),
                   ptr_or_null<float>(plognorm), logprior.data_ptr<float>(), C, ref_scale ? 1 : 0,
@@ -854,7 +944,7 @@ at::Tensor bandit_select(int64_t algo, int64_t batch, const at::Tensor& trials, 
   CHECK_DTYPE(trials, at::kInt);
   TORCH_CHECK(trials.dim() == 2, "trials must be [G, A]");
   const int64_t G = trials.size(0), A = trials.size(1);
-  TORCH_CHECK(A >= 1 && A <= 64, "1 <= arms <= 64");
+  TORCH_CHECK(A >= 1 && A <= 1024, "1 <= arms <= 1024");
   CHECK_DEV(rsum);
   CHECK_DTYPE(rsum, at::kFloat);
   CHECK_DEV(probs);
@@ -966,7 +1056,8 @@ at::Tensor glm_gradient(const at::Tensor& X, int64_t n, const at::Tensor& y, con
   CHECK_DTYPE(X, at::kFloat);
   TORCH_CHECK(X.dim() == 2 && X.is_contiguous(), "X must be contiguous [D, ld]");
   const int64_t D = X.size(0), ld = X.size(1);
-  TORCH_CHECK(D == 4 || D == 8 || D == 16 || D == 32, "D must be padded to 4/8/16/32");
+  TORCH_CHECK(D == 4 || D == 8 || D == 16 || D == 32 || (D > 32 && D <= 256),
+              "D must be padded to 4/8/16/32 or lie in (32, 256]");
   TORCH_CHECK(ld % 16 == 0 && n >= 0 && n <= ld, "ld must be a multiple of 16 and >= n");
   TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 logistic, 1 squared, 2 hinge");
   CHECK_DEV(y);
@@ -1088,11 +1179,13 @@ void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Ten
   TORCH_CHECK(gap.numel() == B && inner_total.numel() == B, "gap / inner_total must be [B]");
   TORCH_CHECK(C > 0 && eps > 0 && max_iter >= 0, "bad SMO parameters");
   DevGuard g(y.device());
+  // gathered K[ws, ws] blocks (graph capture: from the capture's private pool)
+  auto Kws = at::empty({B, Q, Q}, K.options());
   avk::smo_ws_solve_fused(K.data_ptr<float>(), (int)N, reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()),
                           ok.data_ptr<bool>(), alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(),
                           (int)alpha.size(1), gap.data_ptr<float>(), (int)B, (float)C, (float)eps, (int)max_iter,
                           dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
-                          cur_stream(y));
+                          Kws.data_ptr<float>(), cur_stream(y));
 }
 
 void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& dA, const at::Tensor& ok,
@@ -1144,7 +1237,7 @@ std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& 
 at::Tensor weighted_gram(const at::Tensor& X, int64_t n, int64_t D, const c10::optional<at::Tensor>& h) {
   CHECK_DEV(X);
   CHECK_DTYPE(X, at::kFloat);
-  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && X.size(0) >= D && D >= 1 && D <= 32, "X [>=D, ld], D <= 32");
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && X.size(0) >= D && D >= 1 && D <= 1024, "X [>=D, ld], D <= 1024");
   TORCH_CHECK(n >= 0 && n <= X.size(1), "n exceeds ld");
   const float* hp = nullptr;
   if (h.has_value() && h->defined()) {
@@ -1154,10 +1247,26 @@ at::Tensor weighted_gram(const at::Tensor& X, int64_t n, int64_t D, const c10::o
     hp = h->data_ptr<float>();
   }
   DevGuard g(X.device());
-  const int grid = avk::gram_grid(n);
-  auto partial = at::empty({(int64_t)grid * 4, 32, 32}, X.options());
+  if (D <= 32) {
+    const int grid = avk::gram_grid(n);
+    auto partial = at::empty({(int64_t)grid * 4, 32, 32}, X.options());
+    avk::weighted_gram(X.data_ptr<float>(), X.size(1), n, (int)D, hp, partial.data_ptr<float>(), grid, cur_stream(X));
+    return partial.to(at::kDouble).sum(0).narrow(0, 0, D).narrow(1, 0, D);
+  }
+  // block pairs: keep the total work-group count (and the partial buffer) near the D <= 32 launch
+  const int64_t nb = (D + 31) / 32, npairs = nb * (nb + 1) / 2;
+  const int grid = (int)std::max<int64_t>(8, avk::gram_grid(n) / npairs);
+  auto partial = at::empty({(int64_t)grid * 4, npairs, 32, 32}, X.options());
   avk::weighted_gram(X.data_ptr<float>(), X.size(1), n, (int)D, hp, partial.data_ptr<float>(), grid, cur_stream(X));
-  return partial.to(at::kDouble).sum(0).narrow(0, 0, D).narrow(1, 0, D);
+  auto blocks = partial.to(at::kDouble).sum(0);  // [npairs, 32, 32]
+  auto G = at::zeros({nb * 32, nb * 32}, blocks.options());
+  int64_t p = 0;
+  for (int64_t bi = 0; bi < nb; ++bi)
+    for (int64_t bj = bi; bj < nb; ++bj, ++p) {
+      G.narrow(0, bi * 32, 32).narrow(1, bj * 32, 32).copy_(blocks[p]);
+      if (bj != bi) G.narrow(0, bj * 32, 32).narrow(1, bi * 32, 32).copy_(blocks[p].t());
+    }
+  return G.narrow(0, 0, D).narrow(1, 0, D).contiguous();
 }
 
 // k-means (K16).  Centroids in pair layout C2 [Kp/2, D, 2] (every run padded to an even count),
@@ -1700,7 +1809,9 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
     sp.bucket_width = t[3].cast<double>();
     sp.bucket_offset = t[4].cast<int>();
     sp.max_code = t[5].cast<int>();
-    sp.wide = t.size() > 6 && t[6].cast<bool>() ? 1 : 0;
+    const int width = t.size() > 6 ? t[6].cast<int>() : 0;
+    TORCH_CHECK(width <= 1, "device CSV parse: int32 codes take the host parser");
+    sp.wide = width >= 1 ? 1 : 0;
     TORCH_CHECK(sp.ordinal >= 0 && sp.kind >= 0 && sp.kind <= 2, "device CSV parse: CAT / BUCKET / FLOAT columns");
     if (sp.kind == 1) TORCH_CHECK(sp.bucket_width > 0, "bucket width must be > 0");
     at::Tensor o;
@@ -1826,20 +1937,29 @@ at::Tensor col_moments(const at::Tensor& X, int64_t n) {
 
 // K23 leave-one-out statistics: codes [F, ld] uint8 (m = 256) or uint16 (m = 65536), y double [n]
 // -> (sum double [F, m], count int32 [F, m]) over the first n rows.
-py::tuple loo_stats(const at::Tensor& codes, int64_t n, const at::Tensor& y) {
+static int64_t loo_slots(const at::Tensor& codes, int64_t slots) {
+  if (codes.scalar_type() == at::kInt) {
+    TORCH_CHECK(slots >= 2 && slots <= (1LL << 30), "int32 codes: slots (max code + 2) in [2, 2^30]");
+    return slots;
+  }
+  TORCH_CHECK(codes.scalar_type() == at::kUInt16 || codes.scalar_type() == at::kByte,
+              "codes must be uint8, uint16 or int32");
+  return codes.scalar_type() == at::kUInt16 ? 65536 : 256;
+}
+
+py::tuple loo_stats(const at::Tensor& codes, int64_t n, const at::Tensor& y, int64_t slots) {
   CHECK_DEV(codes);
   CHECK_DEV(y);
   CHECK_DTYPE(y, at::kDouble);
-  const bool wide = codes.scalar_type() == at::kUInt16;
-  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8 or uint16");
   TORCH_CHECK(codes.dim() == 2 && n >= 0 && n <= codes.size(1) && y.numel() >= n, "codes [F, ld], y [>= n]");
-  const int64_t F = codes.size(0), m = wide ? 65536 : 256;
+  const int64_t F = codes.size(0), m = loo_slots(codes, slots);
+  const int cb = (int)codes.element_size();
   TORCH_CHECK(F >= 1 && F < 65536, "1 <= F < 65536 columns");
   DevGuard g(codes.device());
   auto sum = at::zeros({F, m}, y.options());
   auto cnt = at::zeros({F, m}, codes.options().dtype(at::kInt));
   if (n > 0)
-    avk::loo_stats(codes.data_ptr(), wide, codes.size(1), n, (int)F, y.data_ptr<double>(), sum.data_ptr<double>(),
+    avk::loo_stats(codes.data_ptr(), cb, (int)m, codes.size(1), n, (int)F, y.data_ptr<double>(), sum.data_ptr<double>(),
                    reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), cur_stream(codes));
   return py::make_tuple(sum, cnt);
 }
@@ -1847,7 +1967,7 @@ py::tuple loo_stats(const at::Tensor& codes, int64_t n, const at::Tensor& y) {
 // K23 leave-one-out apply -> float32 [n, F] (row-major); noise double [F, n] uniforms or undefined.
 at::Tensor loo_apply(const at::Tensor& codes, int64_t n, const at::Tensor& y, const at::Tensor& sum,
                      const at::Tensor& cnt, const at::Tensor& gmean, double reg,
-                     const c10::optional<at::Tensor>& noise, double amp) {
+                     const c10::optional<at::Tensor>& noise, double amp, int64_t slots) {
   CHECK_DEV(codes);
   CHECK_DEV(y);
   CHECK_DEV(sum);
@@ -1857,9 +1977,8 @@ at::Tensor loo_apply(const at::Tensor& codes, int64_t n, const at::Tensor& y, co
   CHECK_DTYPE(sum, at::kDouble);
   CHECK_DTYPE(cnt, at::kInt);
   CHECK_DTYPE(gmean, at::kDouble);
-  const bool wide = codes.scalar_type() == at::kUInt16;
-  TORCH_CHECK(wide || codes.scalar_type() == at::kByte, "codes must be uint8 or uint16");
-  const int64_t F = codes.size(0), m = wide ? 65536 : 256;
+  const int64_t F = codes.size(0), m = loo_slots(codes, slots);
+  const int cb = (int)codes.element_size();
   TORCH_CHECK(codes.dim() == 2 && n >= 0 && n <= codes.size(1) && y.numel() >= n, "codes [F, ld], y [>= n]");
   TORCH_CHECK(sum.numel() == F * m && cnt.numel() == F * m && gmean.numel() >= 1, "stats tables [F, m]");
   TORCH_CHECK((n + 255) / 256 < (1LL << 31), "too many rows");
@@ -1873,7 +1992,7 @@ at::Tensor loo_apply(const at::Tensor& codes, int64_t n, const at::Tensor& y, co
   DevGuard g(codes.device());
   auto out = at::empty({n, F}, y.options().dtype(at::kFloat));
   if (n > 0)
-    avk::loo_apply(codes.data_ptr(), wide, codes.size(1), n, (int)F, y.data_ptr<double>(), sum.data_ptr<double>(),
+    avk::loo_apply(codes.data_ptr(), cb, (int)m, codes.size(1), n, (int)F, y.data_ptr<double>(), sum.data_ptr<double>(),
                    reinterpret_cast<const unsigned*>(cnt.data_ptr<int>()), gmean.data_ptr<double>(), reg, nz, amp,
                    out.data_ptr<float>(), cur_stream(codes));
   return out;
@@ -1925,7 +2044,12 @@ py::tuple csv_parse(avh::CsvFile& f, py::list specs_py, int64_t row_begin, int64
     s.bucket_width = t[3].cast<double>();
     s.bucket_offset = t[4].cast<int>();
     s.max_code = t[5].cast<int>();
-    if (t.size() > 6) s.wide = t[6].cast<bool>();
+    if (t.size() > 6) {  // code width: 0 / False uint8, 1 / True uint16, 2 int32 (CAT only)
+      const int w = t[6].cast<int>();
+      s.wide = w >= 1;
+      s.huge = w >= 2;
+      TORCH_CHECK(!s.huge || s.kind == avh::CAT, "int32 codes are for categorical columns");
+    }
     TORCH_CHECK(s.ordinal >= 0, "negative ordinal");
     if (s.kind == avh::BUCKET) TORCH_CHECK(s.bucket_width > 0, "bucket width must be > 0");
     specs.push_back(std::move(s));
@@ -1938,7 +2062,9 @@ py::tuple csv_parse(avh::CsvFile& f, py::list specs_py, int64_t row_begin, int64
   std::vector<void*> ptrs;
   for (auto& s : specs) {
     at::Tensor t;
-    if ((s.kind == avh::CAT || s.kind == avh::BUCKET) && s.wide)
+    if (s.kind == avh::CAT && s.huge)
+      t = at::full({std::max<int64_t>(ld, 16)}, 0x7FFFFFFF, at::TensorOptions().dtype(at::kInt));
+    else if ((s.kind == avh::CAT || s.kind == avh::BUCKET) && s.wide)
       t = at::full({std::max<int64_t>(ld, 16)}, 65535, at::TensorOptions().dtype(at::kUInt16));
     else if (s.kind == avh::CAT || s.kind == avh::BUCKET)
       t = at::full({std::max<int64_t>(ld, 16)}, 255, at::TensorOptions().dtype(at::kByte));
@@ -2396,6 +2522,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bigram_histogram", &bigram_histogram);
   m.def("class_moments", &class_moments);
   m.def("nb_predict", &nb_predict);
+  m.def("nb_predict_wide", &nb_predict_wide);
   m.def("node_histogram", &node_histogram);
   m.def("node_grad_histogram", &node_grad_histogram, py::arg("codes"), py::arg("n"), py::arg("node"), py::arg("g"),
         py::arg("h"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_nodes"), py::arg("out"),
@@ -2436,9 +2563,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gsp_join", &gsp_join);
   m.def("spirit_update", &spirit_update);
   m.def("col_moments", &col_moments);
-  m.def("loo_stats", &loo_stats);
+  m.def("loo_stats", &loo_stats, py::arg("codes"), py::arg("n"), py::arg("y"), py::arg("slots") = -1);
   m.def("loo_apply", &loo_apply, py::arg("codes"), py::arg("n"), py::arg("y"), py::arg("sum"), py::arg("cnt"),
-        py::arg("gmean"), py::arg("reg"), py::arg("noise") = py::none(), py::arg("amp") = 0.0);
+        py::arg("gmean"), py::arg("reg"), py::arg("noise") = py::none(), py::arg("amp") = 0.0,
+        py::arg("slots") = -1);
   m.def("forest_hist", &forest_hist);
   m.def("bucketize_u8", &bucketize_u8);
   m.def("forest_split", &forest_split);

@@ -86,8 +86,8 @@ struct CatLookup {
     for (size_t i = 0; i < n; ++i) h = (h ^ (uint8_t)p[i]) * 16777619u;
     return h ^ (h >> 15);
   }
-  explicit CatLookup(const std::vector<std::string>& v, bool wide) : vocab(v) {
-    const size_t cap = wide ? 65535 : 255;
+  explicit CatLookup(const std::vector<std::string>& v, bool wide, bool huge) : vocab(v) {
+    const size_t cap = huge ? 0x7FFFFFFEu : (wide ? 65535 : 255);
     if (vocab.size() > cap)
       throw std::runtime_error("categorical cardinality " + std::to_string(vocab.size()) + " exceeds the " +
                                std::to_string(cap) + "-value code width");
@@ -106,22 +106,24 @@ struct CatLookup {
       if (!dup) slot[h] = (int32_t)i;
     }
   }
-  // dictionary code, 65535 when unknown
-  inline uint16_t code(std::string_view s) const {
+  // dictionary code, kUnknown when unknown (store_code clamps it to the column's missing code)
+  static constexpr uint32_t kUnknown = 0xFFFFFFFFu;
+  inline uint32_t code(std::string_view s) const {
     s = trim(s);
     uint32_t h = hash(s.data(), s.size()) & mask;
     while (true) {
       const int32_t i = slot[h];
-      if (i < 0) return 65535;
+      if (i < 0) return kUnknown;
       const std::string& v = vocab[(size_t)i];
-      if (v.size() == s.size() && std::memcmp(v.data(), s.data(), s.size()) == 0) return (uint16_t)i;
+      if (v.size() == s.size() && std::memcmp(v.data(), s.data(), s.size()) == 0) return (uint32_t)i;
       h = (h + 1) & mask;
     }
   }
 };
 
-inline void store_code(void* out, int64_t r, bool wide, uint32_t code) {
-  if (wide) static_cast<uint16_t*>(out)[r] = (uint16_t)(code > 65535 ? 65535 : code);
+inline void store_code(void* out, int64_t r, const ColSpec& sp, uint32_t code) {
+  if (sp.huge) static_cast<int32_t*>(out)[r] = (int32_t)(code > 0x7FFFFFFFu ? 0x7FFFFFFFu : code);
+  else if (sp.wide) static_cast<uint16_t*>(out)[r] = (uint16_t)(code > 65535 ? 65535 : code);
   else static_cast<uint8_t*>(out)[r] = (uint8_t)(code > 255 ? 255 : code);
 }
 
@@ -278,7 +280,7 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
   std::vector<std::unique_ptr<CatLookup>> cats(specs.size());
   int max_ord = 0;
   for (size_t i = 0; i < specs.size(); ++i) {
-    if (specs[i].kind == CAT) cats[i] = std::make_unique<CatLookup>(specs[i].vocab, specs[i].wide);
+    if (specs[i].kind == CAT) cats[i] = std::make_unique<CatLookup>(specs[i].vocab, specs[i].wide, specs[i].huge);
     max_ord = std::max(max_ord, specs[i].ordinal);
   }
   // ordinal -> list of spec indices
@@ -299,10 +301,10 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
         const ColSpec& sp = specs[si];
         switch (sp.kind) {
           case CAT:
-            store_code(outs[si], r, sp.wide, have ? cats[si]->code(fv) : 65535u);
+            store_code(outs[si], r, sp, have ? cats[si]->code(fv) : CatLookup::kUnknown);
             break;
           case BUCKET: {
-            uint32_t c = 65535u;
+            uint32_t c = CatLookup::kUnknown;
             if (have) {
               const double v = parse_double(fv);
               if (!std::isnan(v)) {
@@ -311,7 +313,7 @@ int64_t CsvFile::parse(const std::vector<ColSpec>& specs, const std::vector<void
                 if (b >= 0 && b <= sp.max_code) c = (uint32_t)b;
               }
             }
-            store_code(outs[si], r, sp.wide, c);
+            store_code(outs[si], r, sp, c);
             break;
           }
           case FLOAT:

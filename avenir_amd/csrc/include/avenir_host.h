@@ -28,6 +28,7 @@ struct ColSpec {
   int bucket_offset = 0;
   int max_code = 254;              // BUCKET: codes > max_code -> missing
   bool wide = false;               // CAT/BUCKET: uint16 codes (missing = 65535) for > 255 values
+  bool huge = false;               // CAT: int32 codes (missing = INT32_MAX) for > 65534 values
 };
 
 // Rank ``rank``'s byte range of the concatenated ``paths`` as memory-mapped segments of whole lines

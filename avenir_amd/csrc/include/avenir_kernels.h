@@ -17,6 +17,9 @@ void class_histogram(const uint8_t* codes, long long ld, long long n, const uint
 void class_histogram_wide(const uint16_t* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins,
                           const int* d_offs, int nfeat, int total_bins, int n_classes, int count_labels,
                           unsigned long long* out, int mode, hipStream_t stream);
+void class_histogram_i32(const int* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins,
+                          const int* d_offs, int nfeat, int total_bins, int n_classes, int count_labels,
+                          unsigned long long* out, int mode, hipStream_t stream);
 void pair_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
                     const int* d_bins, const int* d_pairs, const long long* d_poff, int n_pairs,
                     int max_tab, int n_classes, unsigned long long* out, hipStream_t stream);
@@ -32,6 +35,12 @@ void class_histogram_rowpacked(const uint16_t* words, long long n, const int* h_
                                int n_classes, int count_labels, unsigned long long* out, hipStream_t stream);
 
 // ---- bayes.hip ----------------------------------------------------------------------------
+int nb_predict_wide_max_classes();
+void nb_predict_wide(const void* codes, int code_bytes, long long ld, long long n, int nfeat, const int* offs,
+                     const int* bins, const float* logpT, const float* logfp, const float* x, long long ldx, int ncont,
+                     const float* gmean, const float* ginvstd, const float* glognorm, const float* pmean,
+                     const float* pinvstd, const float* plognorm, const float* logprior, int C, int ref_scale,
+                     float* post, int* pred, const uint8_t* labels, unsigned long long* confusion, hipStream_t stream);
 void nb_predict(const uint8_t* codes, long long ld, long long n, int nfeat, const int* offs,
                 const float* logp, const float* logfp, int total_bins, const float* x, long long ldx,
                 int ncont, const float* gmean, const float* ginvstd, const float* glognorm,
@@ -116,7 +125,7 @@ void smo_ws_update(const float* K, const long long* ws, const float* dA, const b
                    int B, int N, int ldag, int Q, hipStream_t stream);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
-                        long long* inner_total, hipStream_t stream);
+                        long long* inner_total, float* Kws, hipStream_t stream);
 int smo_ws_size();
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream);
@@ -235,9 +244,9 @@ void col_moments_f32(const float* X, long long n, long long ld, int F, int pass,
                      hipStream_t stream);
 void col_moments_f64(const double* X, long long n, long long ld, int F, int pass, const double* mean, double* part,
                      hipStream_t stream);
-void loo_stats(const void* codes, bool wide, long long ld, long long n, int F, const double* y, double* sum,
+void loo_stats(const void* codes, int code_bytes, int m, long long ld, long long n, int F, const double* y, double* sum,
                unsigned* cnt, hipStream_t stream);
-void loo_apply(const void* codes, bool wide, long long ld, long long n, int F, const double* y, const double* sum,
+void loo_apply(const void* codes, int code_bytes, int m, long long ld, long long n, int F, const double* y, const double* sum,
                const unsigned* cnt, const double* gmean, double reg, const double* noise, double amp, float* out,
                hipStream_t stream);
 

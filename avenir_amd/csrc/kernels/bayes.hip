@@ -96,6 +96,87 @@ __global__ __launch_bounds__(PB) void nb_predict_kernel(
   }
 }
 
+// Wide tables (uint16 / int32 codes: categoricals beyond 255 values).  The [C][TB] table no longer
+// fits LDS (10^5-value fields), so the model is read through L2 in the transposed layout
+// logpT [TB][C]: one record-feature gather fetches the C class terms of its value from one
+// contiguous run (one cache line for C <= 32), and the per-class scores live in registers
+// (compile-time unrolled over NBW_MAXC with a C guard, so no scratch).  Codes >= bins[f] (missing
+// or unknown) contribute nothing, as in the CPU oracle.
+constexpr int NBW_MAXC = 32;
+
+template <typename CT>
+__global__ __launch_bounds__(PB) void nb_predict_wide_kernel(
+    const CT* __restrict__ codes, long long ld, long long n, int nfeat, const int* __restrict__ offs,
+    const int* __restrict__ bins, const float* __restrict__ logpT /*[TB][C]*/, const float* __restrict__ logfp,
+    const float* __restrict__ x, long long ldx, int ncont, const float* __restrict__ gmean,
+    const float* __restrict__ ginvstd, const float* __restrict__ glognorm, const float* __restrict__ pmean,
+    const float* __restrict__ pinvstd, const float* __restrict__ plognorm, const float* __restrict__ logprior, int C,
+    int ref_scale, float* __restrict__ post, int* __restrict__ pred, const uint8_t* __restrict__ labels,
+    unsigned long long* __restrict__ confusion) {
+  __shared__ unsigned s_conf[NBW_MAXC * NBW_MAXC];
+  if (confusion)
+    for (int i = threadIdx.x; i < C * C; i += PB) s_conf[i] = 0;
+  __syncthreads();
+  const long long stride = (long long)gridDim.x * PB;
+  for (long long r = (long long)blockIdx.x * PB + threadIdx.x; r < n; r += stride) {
+    float s[NBW_MAXC];
+#pragma unroll
+    for (int c = 0; c < NBW_MAXC; ++c) s[c] = c < C ? logprior[c] : -INFINITY;
+    float lfp = 0.f;
+    for (int f = 0; f < nfeat; ++f) {
+      const unsigned v = (unsigned)codes[(long long)f * ld + r];
+      if (v >= (unsigned)bins[f]) continue;
+      const long long idx = (long long)offs[f] + v;
+      const float* row = logpT + idx * C;
+#pragma unroll
+      for (int c = 0; c < NBW_MAXC; ++c)
+        if (c < C) s[c] += row[c];
+      if (ref_scale) lfp += logfp[idx];
+    }
+    for (int j = 0; j < ncont; ++j) {
+      const float xv = x[(long long)j * ldx + r];
+#pragma unroll
+      for (int c = 0; c < NBW_MAXC; ++c)
+        if (c < C) {
+          const float z = (xv - gmean[c * ncont + j]) * ginvstd[c * ncont + j];
+          s[c] += glognorm[c * ncont + j] - 0.5f * z * z;
+        }
+      if (ref_scale) {
+        const float z = (xv - pmean[j]) * pinvstd[j];
+        lfp += plognorm[j] - 0.5f * z * z;
+      }
+    }
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int c = 0; c < NBW_MAXC; ++c)
+      if (c < C && s[c] > best) { best = s[c]; arg = c; }
+    pred[r] = arg;
+    if (post) {
+      float sub = lfp;
+      if (!ref_scale) {
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < NBW_MAXC; ++c)
+          if (c < C) se += __expf(s[c] - best);
+        sub = best + __logf(se);
+      }
+#pragma unroll
+      for (int c = 0; c < NBW_MAXC; ++c)
+        if (c < C) post[r * C + c] = __expf(s[c] - sub);
+    }
+    if (confusion) {
+      const unsigned a = labels[r];
+      if (a < (unsigned)C) atomicAdd(&s_conf[a * C + arg], 1u);
+    }
+  }
+  if (confusion) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * C; i += PB)
+      if (s_conf[i]) atomicAdd(&confusion[i], (unsigned long long)s_conf[i]);
+  }
+}
+
 // Model finalisation: [C, TB+1] int64 counts (last column = class counts) -> float log tables.
 // One workgroup per feature (+1 for the class prior); fp64 sums, floor at log_floor.  Replaces
 // ~40 tiny torch launches in the training step (BayesianDistribution reducer + the predictor's
@@ -181,6 +262,44 @@ void nb_predict(const uint8_t* codes, long long ld, long long n, int nfeat, cons
                                                ldx, ncont, gmean, ginvstd, glognorm, pmean, pinvstd,
                                                plognorm, logprior, C, ref_scale, post, pred, labels,
                                                confusion);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+template <typename CT>
+static void nb_predict_wide_t(const CT* codes, long long ld, long long n, int nfeat, const int* offs, const int* bins,
+                              const float* logpT, const float* logfp, const float* x, long long ldx, int ncont,
+                              const float* gmean, const float* ginvstd, const float* glognorm, const float* pmean,
+                              const float* pinvstd, const float* plognorm, const float* logprior, int C,
+                              int ref_scale, float* post, int* pred, const uint8_t* labels,
+                              unsigned long long* confusion, hipStream_t stream) {
+  const int grid = av::stream_grid(n, PB, 4, 4096);
+  nb_predict_wide_kernel<CT><<<grid, PB, 0, stream>>>(codes, ld, n, nfeat, offs, bins, logpT, logfp, x, ldx, ncont,
+                                                      gmean, ginvstd, glognorm, pmean, pinvstd, plognorm, logprior, C,
+                                                      ref_scale, post, pred, labels, confusion);
+}
+
+int nb_predict_wide_max_classes() { return NBW_MAXC; }
+
+void nb_predict_wide(const void* codes, int code_bytes, long long ld, long long n, int nfeat, const int* offs,
+                     const int* bins, const float* logpT, const float* logfp, const float* x, long long ldx, int ncont,
+                     const float* gmean, const float* ginvstd, const float* glognorm, const float* pmean,
+                     const float* pinvstd, const float* plognorm, const float* logprior, int C, int ref_scale,
+                     float* post, int* pred, const uint8_t* labels, unsigned long long* confusion,
+                     hipStream_t stream) {
+  if (n <= 0) return;
+  if (C < 1 || C > NBW_MAXC) throw std::runtime_error("nb_predict_wide: 1..32 classes");
+  if (code_bytes == 4)
+    nb_predict_wide_t<int>(static_cast<const int*>(codes), ld, n, nfeat, offs, bins, logpT, logfp, x, ldx, ncont, gmean,
+                           ginvstd, glognorm, pmean, pinvstd, plognorm, logprior, C, ref_scale, post, pred, labels,
+                           confusion, stream);
+  else if (code_bytes == 2)
+    nb_predict_wide_t<uint16_t>(static_cast<const uint16_t*>(codes), ld, n, nfeat, offs, bins, logpT, logfp, x, ldx,
+                                ncont, gmean, ginvstd, glognorm, pmean, pinvstd, plognorm, logprior, C, ref_scale,
+                                post, pred, labels, confusion, stream);
+  else
+    nb_predict_wide_t<uint8_t>(static_cast<const uint8_t*>(codes), ld, n, nfeat, offs, bins, logpT, logfp, x, ldx,
+                               ncont, gmean, ginvstd, glognorm, pmean, pinvstd, plognorm, logprior, C, ref_scale, post,
+                               pred, labels, confusion, stream);
   AV_HIP_CHECK(hipGetLastError());
 }
 

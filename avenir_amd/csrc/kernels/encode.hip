@@ -17,14 +17,16 @@
 //   reference.
 //   loo_stats_kernel: per (column, code) target sum and count.  uint8 codes: a block privatises
 //     the 256-slot table in LDS (fp64 ds_add + u32 counters), then flushes the touched slots with
-//     global atomics; uint16 ("wide", > 255 values) codes go to global atomics directly.
+//     global atomics; uint16 ("wide", > 255 values) and int32 (> 65,534 values) codes go to global
+//     atomics directly.
 //   loo_apply_kernel: out[i, j] = (sum[c] - y_i + reg * gmean) / max(cnt[c] - 1 + reg, 1e-12)
 //     (x (1 + amp * (2u - 1)) with the caller's uniforms u [F, n], one stream per column), fused gather + formula + layout
 //     change: a block stages a [Fc, 256] code tile (columns contiguous, coalesced reads) in LDS and
 //     writes the row-major [256, Fc] output tile with consecutive lanes on consecutive floats.
 //
 // Index safety: every load is inside [0, n) of its column; code values index tables of m slots
-// with m = 256 (uint8) or 65536 (uint16), so any code value is in range by construction.
+// with m = 256 (uint8) or 65536 (uint16), so any code value is in range by construction; int32
+// codes (> 65,534 values) are clamped to the last slot m - 1 (missing / out of range).
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -123,7 +125,7 @@ constexpr int LOO_THREADS = 256;
 template <typename CT>
 __global__ __launch_bounds__(LOO_THREADS) void loo_stats_kernel(const CT* __restrict__ codes, long long ld, long long n,
                                                                 const double* __restrict__ y, double* __restrict__ sum,
-                                                                unsigned* __restrict__ cnt) {
+                                                                unsigned* __restrict__ cnt, int m) {
   const int f = blockIdx.y;
   const CT* col = codes + (long long)f * ld;
   const long long stride = (long long)gridDim.x * LOO_THREADS;
@@ -145,15 +147,17 @@ __global__ __launch_bounds__(LOO_THREADS) void loo_stats_kernel(const CT* __rest
       atomicAdd(&cnt[(long long)f * 256 + threadIdx.x], k);
     }
   } else {
+    const unsigned top = (unsigned)(m - 1);  // the missing / out-of-range slot
     for (long long i = (long long)blockIdx.x * LOO_THREADS + threadIdx.x; i < n; i += stride) {
-      const long long c = (long long)f * 65536 + col[i];
+      const unsigned v = (unsigned)col[i];
+      const long long c = (long long)f * m + (v < top ? v : top);
       atomicAdd(&sum[c], y[i]);
       atomicAdd(&cnt[c], 1u);
     }
   }
 }
 
-constexpr int LOO_TILE_F = 32;  // columns per tile -> [32][256] uint16 = 16 KB of LDS
+constexpr int LOO_TILE_F = 32;  // columns per tile -> [32][256] u32 = 32 KB of LDS
 
 template <typename CT>
 __global__ __launch_bounds__(LOO_THREADS) void loo_apply_kernel(const CT* __restrict__ codes, long long ld, long long n,
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(LOO_THREADS) void loo_apply_kernel(const CT* __rest
                                                                 const double* __restrict__ gmean, double reg,
                                                                 const double* __restrict__ noise, double amp,
                                                                 float* __restrict__ out) {
-  __shared__ unsigned short tile[LOO_TILE_F][LOO_THREADS];
+  __shared__ unsigned tile[LOO_TILE_F][LOO_THREADS];
   __shared__ double ys[LOO_THREADS];
   const long long r0 = (long long)blockIdx.x * LOO_THREADS;
   const int f0 = blockIdx.y * LOO_TILE_F;
@@ -172,7 +176,11 @@ __global__ __launch_bounds__(LOO_THREADS) void loo_apply_kernel(const CT* __rest
   const int t = threadIdx.x;
   if (t < rows) {
     ys[t] = y[r0 + t];
-    for (int j = 0; j < fc; ++j) tile[j][t] = (unsigned short)codes[(long long)(f0 + j) * ld + r0 + t];
+    const unsigned top = (unsigned)(m - 1);
+    for (int j = 0; j < fc; ++j) {
+      const unsigned v = (unsigned)codes[(long long)(f0 + j) * ld + r0 + t];
+      tile[j][t] = v < top ? v : top;
+    }
   }
   __syncthreads();
   const double gm = reg * gmean[0];
@@ -222,24 +230,28 @@ static int loo_blocks(long long n, int F) {
   return (int)(b < 1 ? 1 : b);
 }
 
-void loo_stats(const void* codes, bool wide, long long ld, long long n, int F, const double* y, double* sum,
+void loo_stats(const void* codes, int code_bytes, int m, long long ld, long long n, int F, const double* y, double* sum,
                unsigned* cnt, hipStream_t stream) {
   const dim3 grid(loo_blocks(n, F), F);
-  if (wide)
+  if (code_bytes == 4)
+    loo_stats_kernel<int><<<grid, LOO_THREADS, 0, stream>>>(static_cast<const int*>(codes), ld, n, y, sum, cnt, m);
+  else if (code_bytes == 2)
     loo_stats_kernel<unsigned short><<<grid, LOO_THREADS, 0, stream>>>(static_cast<const unsigned short*>(codes), ld, n,
-                                                                       y, sum, cnt);
+                                                                       y, sum, cnt, m);
   else
     loo_stats_kernel<unsigned char><<<grid, LOO_THREADS, 0, stream>>>(static_cast<const unsigned char*>(codes), ld, n,
-                                                                      y, sum, cnt);
+                                                                      y, sum, cnt, m);
   AV_HIP_CHECK(hipGetLastError());
 }
 
-void loo_apply(const void* codes, bool wide, long long ld, long long n, int F, const double* y, const double* sum,
-               const unsigned* cnt, const double* gmean, double reg, const double* noise, double amp, float* out,
-               hipStream_t stream) {
+void loo_apply(const void* codes, int code_bytes, int m, long long ld, long long n, int F, const double* y,
+               const double* sum, const unsigned* cnt, const double* gmean, double reg, const double* noise, double amp,
+               float* out, hipStream_t stream) {
   const dim3 grid((unsigned)((n + LOO_THREADS - 1) / LOO_THREADS), (F + LOO_TILE_F - 1) / LOO_TILE_F);
-  const int m = wide ? 65536 : 256;
-  if (wide)
+  if (code_bytes == 4)
+    loo_apply_kernel<int><<<grid, LOO_THREADS, 0, stream>>>(static_cast<const int*>(codes), ld, n, F, y, sum, cnt, m,
+                                                            gmean, reg, noise, amp, out);
+  else if (code_bytes == 2)
     loo_apply_kernel<unsigned short><<<grid, LOO_THREADS, 0, stream>>>(
         static_cast<const unsigned short*>(codes), ld, n, F, y, sum, cnt, m, gmean, reg, noise, amp, out);
   else

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(FB_THREADS) void forest_split_kernel(
         chosen[nk++] = bf;
       }
       if (nk > 0) {
-        int j = (int)(rnd[a] * nk);
+        int j = (int)((double)rnd[a] * nk);  // fp64 product, as the host twin
         pick = chosen[j < nk ? j : nk - 1];
       }
     }

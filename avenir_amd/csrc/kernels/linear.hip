@@ -133,6 +133,134 @@ __global__ __launch_bounds__(256) void gram_mfma_kernel(const float* __restrict_
   }
 }
 
+// D > 32: the Gram matrix in 32 x 32 blocks.  blockIdx.y enumerates the upper-triangular block
+// pairs (bi <= bj); each wave stages the 32-feature x 64-row tiles of feature blocks bi and bj
+// and accumulates G[bi, bj] = sum_k h_k x_k[bi] x_k[bj]^T with the same MFMA as above.  Partials
+// per (wave, pair) are summed in fp64 on the device and mirrored into the lower triangle.
+__global__ __launch_bounds__(256) void gram_mfma_pair_kernel(const float* __restrict__ X, long long ld, long long n,
+                                                             int D, int nb, const float* __restrict__ h,
+                                                             float* __restrict__ partial) {
+  __shared__ float tile[4][2][32][65];
+  __shared__ float hs[4][64];
+  int p = blockIdx.y, bi = 0;
+  while (p >= nb - bi) { p -= nb - bi; ++bi; }
+  const int bj = bi + p;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long ntiles = (n + 63) / 64;
+  const long long gw = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
+  const int sb = bi == bj ? 0 : 1;  // diagonal pairs read one tile twice
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (long long t = gw; t < ntiles; t += nw) {
+    const long long row = t * 64 + lane;
+    const bool ok = row < n;
+    hs[w][lane] = ok ? (h ? h[row] : 1.f) : 0.f;
+    for (int i = 0; i < 32; ++i) {
+      const int fa = bi * 32 + i, fb = bj * 32 + i;
+      tile[w][0][i][lane] = (ok && fa < D) ? X[(long long)fa * ld + row] : 0.f;
+      if (sb) tile[w][1][i][lane] = (ok && fb < D) ? X[(long long)fb * ld + row] : 0.f;
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // wave-private tiles: own LDS writes visible to own lanes
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 8
+    for (int kk = 0; kk < 32; ++kk) {
+      const int r = 2 * kk + (lane >> 5);
+      const float xa = tile[w][0][lane & 31][r];
+      const float xb = tile[w][sb][lane & 31][r];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa * hs[w][r], xb, acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  float* out = partial + (gw * gridDim.y + blockIdx.y) * 1024;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    out[row * 32 + (lane & 31)] = acc[r];
+  }
+}
+
+// D in (32, 256]: the same one-pass gradient with the feature loop tiled through LDS.  A block
+// walks row tiles of TR = 128 rows (grid-stride): the [D, TR] tile of the column-major X is staged
+// in LDS with coalesced 512-B feature-row segments, two threads per row compute z = w.x over the
+// tile (half the features each, one shuffle to combine), the loss and e = sw * f(z) (e to LDS),
+// then thread k < D accumulates g_k += sum_r X[k, r] e_r from LDS in a register across all the
+// block's tiles.  X is read from HBM exactly once; per-block partials are summed on the device.
+constexpr int TR = 128;
+constexpr int TDMAX = 256;
+
+__global__ __launch_bounds__(256) void glm_grad_tiled_kernel(const float* __restrict__ X, long long ld, long long n,
+                                                             int D, const float* __restrict__ y,
+                                                             const float* __restrict__ sw, const float* __restrict__ w,
+                                                             int mode, double* __restrict__ partial,
+                                                             float* __restrict__ hw) {
+  // dynamic LDS sized by D (D * 129 floats: 52 KB at D = 100, so several blocks share a CU)
+  extern __shared__ float smem[];
+  float* tile = smem;                      // [D][TR + 1]
+  float* ws_ = tile + D * (TR + 1);        // [D]
+  float* es = ws_ + D;                     // [TR]
+  float* red = es + TR;                    // [4]
+  const int t = threadIdx.x;
+  for (int k = t; k < D; k += 256) ws_[k] = w[k];
+  float gk = 0.f, loss = 0.f;
+  const long long ntile = (n + TR - 1) / TR;
+  const int half = (D + 1) / 2;
+  for (long long tt = blockIdx.x; tt < ntile; tt += gridDim.x) {
+    const long long r0 = tt * TR;
+    __syncthreads();  // the previous tile's tile[] / es[] reads are done
+    // stage: thread t loads rows (t & 127) of features k = 2j + (t >> 7)
+    for (int k = t >> 7; k < D; k += 2) {
+      const long long r = r0 + (t & (TR - 1));
+      tile[k * (TR + 1) + (t & (TR - 1))] = r < n ? X[(long long)k * ld + r] : 0.f;
+    }
+    __syncthreads();
+    // z: rows r = t >> 1, the feature half (t & 1)
+    const int rr = t >> 1, hsel = t & 1;
+    float z = 0.f;
+    const int k0 = hsel ? half : 0, k1 = hsel ? D : half;
+    for (int k = k0; k < k1; ++k) z = fmaf(ws_[k], tile[k * (TR + 1) + rr], z);
+    z += __shfl_xor(z, 1, 64);
+    if (hsel == 0) {
+      const long long r = r0 + rr;
+      float e = 0.f;
+      if (r < n) {
+        const float yy = y[r];
+        const float s = sw ? sw[r] : 1.f;
+        float l, h;
+        if (mode == 0) {
+          const float p = 1.f / (1.f + __expf(-z));
+          e = yy - p;
+          l = softplus(z) - yy * z;
+          h = p * (1.f - p);
+        } else if (mode == 1) {
+          e = yy - z;
+          l = 0.5f * e * e;
+          h = 1.f;
+        } else {
+          const float m = yy * z;
+          e = m < 1.f ? yy : 0.f;
+          l = fmaxf(0.f, 1.f - m);
+          h = 0.f;
+        }
+        e *= s;
+        loss = fmaf(l, s, loss);
+        if (hw) hw[r] = h * s;
+      }
+      es[rr] = e;
+    }
+    __syncthreads();
+    if (t < D) {
+#pragma unroll 8
+      for (int r = 0; r < TR; ++r) gk = fmaf(tile[t * (TR + 1) + r], es[r], gk);
+    }
+  }
+  const float lw = av::wave_sum(loss);
+  if ((t & 63) == 0) red[t >> 6] = lw;
+  __syncthreads();
+  if (t < D) partial[(long long)blockIdx.x * (D + 1) + t] = (double)gk;
+  if (t == 0) partial[(long long)blockIdx.x * (D + 1) + D] = (double)red[0] + red[1] + red[2] + red[3];
+}
+
 template <int D, int VEC>
 void launch_glm(const float* X, long long ld, long long n, const float* y, const float* sw, const float* w, int mode,
                 double* partial, int grid, float* hw, hipStream_t stream) {
@@ -155,7 +283,13 @@ void glm_grad(const float* X, long long ld, long long n, int D, const float* y, 
     case 8: launch_glm<8, 4>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
     case 16: launch_glm<16, 4>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
     case 32: launch_glm<32, 2>(X, ld, n, y, sw, w, mode, partial, grid, hw, stream); break;
-    default: throw std::runtime_error("glm_grad: D must be 4, 8, 16 or 32");
+    default:
+      if (D > 32 && D <= TDMAX) {
+        const size_t lds = sizeof(float) * ((size_t)D * (TR + 1) + D + TR + 4);
+        glm_grad_tiled_kernel<<<grid, 256, lds, stream>>>(X, ld, n, D, y, sw, w, mode, partial, hw);
+        break;
+      }
+      throw std::runtime_error("glm_grad: D must be 4, 8, 16, 32 or in (32, 256]");
   }
   AV_HIP_CHECK(hipGetLastError());
 }
@@ -164,8 +298,12 @@ int gram_grid(long long n) { return av::stream_grid((n + 63) / 64, 4, 1, 1024); 
 
 void weighted_gram(const float* X, long long ld, long long n, int D, const float* h, float* partial, int grid,
                    hipStream_t stream) {
-  if (D > 32) throw std::runtime_error("weighted_gram: D must be <= 32");
-  gram_mfma_kernel<<<grid, 256, 0, stream>>>(X, ld, n, D, h, partial);
+  if (D <= 32) {
+    gram_mfma_kernel<<<grid, 256, 0, stream>>>(X, ld, n, D, h, partial);
+  } else {
+    const int nb = (D + 31) / 32;
+    gram_mfma_pair_kernel<<<dim3(grid, nb * (nb + 1) / 2), 256, 0, stream>>>(X, ld, n, D, nb, h, partial);
+  }
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -352,6 +352,65 @@ __global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float
   if (lane == 0) inner_total[b] += it;
 }
 
+// smo_ws_gather_kernel: K[ws, ws] of every problem into a contiguous [B, Q, Q] block, one
+// workgroup per (row p, problem): the Q x Q scattered 4-byte reads are spread over Q * B
+// workgroups (all CUs) instead of being issued by the one CU that then solves.
+__global__ __launch_bounds__(WS_Q) void smo_ws_gather_kernel(const float* __restrict__ K, int N,
+                                                             const long long* __restrict__ ws,
+                                                             const bool* __restrict__ ok, float* __restrict__ Kws) {
+  constexpr int Q = WS_Q;
+  const int b = blockIdx.y, p = blockIdx.x, q = threadIdx.x;
+  const long long* wb = ws + (long long)b * Q;
+  const bool* ob = ok + (long long)b * Q;
+  const long long rp = ob[p] ? wb[p] : 0, cq = ob[q] ? wb[q] : 0;  // < N (select writes n < N)
+  Kws[((long long)b * Q + p) * Q + q] = K[(long long)b * N * N + rp * N + cq];
+}
+
+// smo_ws_solve_kernel: one wavefront per problem: the gathered Q x Q block into LDS (coalesced
+// 16-byte loads), then the sub-problem solve, the alpha scatter, dA and the iteration count.
+__global__ __launch_bounds__(64) void smo_ws_solve_kernel(const float* __restrict__ Kws,
+                                                          const long long* __restrict__ ws,
+                                                          const bool* __restrict__ ok, float* __restrict__ alpha,
+                                                          const float* __restrict__ G, const float* __restrict__ yv,
+                                                          int N, int ldag, const float* __restrict__ gap, float C,
+                                                          float eps, int max_iter, float* __restrict__ dA,
+                                                          long long* __restrict__ inner_total) {
+  constexpr int Q = WS_Q, E = Q / 64;
+  __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float4* src = reinterpret_cast<const float4*>(Kws + (long long)b * Q * Q);
+  float4* dst = reinterpret_cast<float4*>(&Ks[0][0]);
+#pragma unroll 8
+  for (int e = lane; e < Q * Q / 4; e += 64) dst[e] = src[e];
+  float y[E], a[E], g[E], qd[E], a0[E];
+  bool okv[E];
+  long long wsv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = lane + 64 * e;
+    okv[e] = ok[(long long)b * Q + t];
+    wsv[e] = okv[e] ? ws[(long long)b * Q + t] : 0;
+    y[e] = okv[e] ? yv[(long long)b * N + wsv[e]] : 0.f;
+    a[e] = alpha[(long long)b * ldag + wsv[e]];
+    g[e] = G[(long long)b * ldag + wsv[e]];
+    a0[e] = a[e];
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // wave-private LDS block: own writes visible to own lanes
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int e = 0; e < E; ++e) qd[e] = Ks[lane + 64 * e][lane + 64 * e];
+  float gp = gap[b];
+  if (!isfinite(gp)) gp = 0.f;
+  const int it = ws_smo_loop<E>(Ks, y, a, g, qd, C, fmaxf(eps, 0.1f * gp), max_iter, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = lane + 64 * e;
+    if (okv[e]) alpha[(long long)b * ldag + wsv[e]] = a[e];
+    dA[(long long)b * Q + t] = (a[e] - a0[e]) * y[e];
+  }
+  if (lane == 0) inner_total[b] += it;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Working-set selection and gradient update for smo_decomposition, one launch each per outer
 // step (they replace ~25 small torch ops: the violation values, two top-k sorts, the
@@ -470,11 +529,28 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
       if (tid < 256) hist[tid] = 0;
       __syncthreads();
       const unsigned prefix = s_prefix, mask = s_mask;
-      for (int i = 0, n = tid; n < N; ++i, n += SEL_T) {
-        const float v = viol(which, i, n);
-        if (v > -INFINITY) {
-          const unsigned key = order_key(v);
-          if ((key & mask) == prefix) atomicAdd(&hist[(key >> (8 * d)) & 255u], 1u);
+      for (int i = 0, n0 = 0; n0 < N; ++i, n0 += SEL_T) {
+        const int n = n0 + tid;
+        bool act = false;
+        unsigned dg = 0;
+        if (n < N) {
+          const float v = viol(which, i, n);
+          if (v > -INFINITY) {
+            const unsigned key = order_key(v);
+            act = (key & mask) == prefix;
+            dg = (key >> (8 * d)) & 255u;
+          }
+        }
+        // leader aggregation: the lanes sharing the first active lane's digit add with ONE atomic
+        // (ties are the common case — every violator ties on the first outer step — and
+        // same-address LDS atomics serialise)
+        const unsigned long long am = __ballot(act);
+        if (am) {
+          const int lead = __ffsll((long long)am) - 1;
+          const unsigned d0 = (unsigned)__builtin_amdgcn_readlane((int)dg, lead);
+          const unsigned long long same = __ballot(act && dg == d0);
+          if ((tid & 63) == lead) atomicAdd(&hist[d0], (unsigned)__popcll(same));
+          else if (act && dg != d0) atomicAdd(&hist[dg], 1u);
         }
       }
       __syncthreads();
@@ -567,26 +643,55 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   }
 }
 
+// G[n] += y[n] * sum_q dA[q] K[ws[q], n].  A workgroup owns 64 consecutive columns n; its 4 waves
+// split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into quarters, each lane
+// streams its column of those K rows (coalesced, 8 loads in flight), and the 4 partials are added
+// in a fixed order (deterministic).  Grid (N / 64, B): >= 128 workgroups at N = 8192.
 __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
                                                             const float* __restrict__ dA, const bool* __restrict__ ok,
                                                             const float* __restrict__ y, float* __restrict__ G, int N,
                                                             int ldag, int Q) {
   __shared__ long long s_ws[WS_Q];
   __shared__ float s_d[WS_Q];
-  const int b = blockIdx.y;
-  for (int q = threadIdx.x; q < Q; q += 256) {
-    const bool o = ok[(long long)b * Q + q];
-    s_ws[q] = o ? ws[(long long)b * Q + q] : 0;
-    s_d[q] = o ? dA[(long long)b * Q + q] : 0.f;
+  __shared__ float red[4][64];
+  __shared__ int s_cnt;
+  const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w == 0) {
+    int base = 0;
+    for (int q0 = 0; q0 < Q; q0 += 64) {
+      const int q = q0 + lane;
+      float d = 0.f;
+      long long r = 0;
+      if (q < Q && ok[(long long)b * Q + q]) {
+        d = dA[(long long)b * Q + q];
+        r = ws[(long long)b * Q + q];
+      }
+      const bool nz = d != 0.f;
+      const unsigned long long bal = __ballot(nz);
+      const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+      if (nz) {
+        const int k = base + (int)__popcll(bal & below);
+        s_ws[k] = r;
+        s_d[k] = d;
+      }
+      base += (int)__popcll(bal);
+    }
+    if (lane == 0) s_cnt = base;
   }
   __syncthreads();
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  const float* Kb = K + (long long)b * N * N;
+  const int cnt = s_cnt, per = (cnt + 3) / 4;
+  const int q0 = w * per, q1 = min(cnt, q0 + per);
+  const int n = blockIdx.x * 64 + lane;
   float acc = 0.f;
-  for (int q = 0; q < Q; ++q)
-    if (s_d[q] != 0.f) acc += s_d[q] * Kb[s_ws[q] * N + n];  // s_d is block-uniform: no divergence
-  G[(long long)b * ldag + n] += y[(long long)b * N + n] * acc;
+  if (n < N) {
+    const float* Kb = K + (long long)b * N * N + n;
+#pragma unroll 8
+    for (int q = q0; q < q1; ++q) acc += s_d[q] * Kb[s_ws[q] * N];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && n < N)
+    G[(long long)b * ldag + n] += y[(long long)b * N + n] * (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
 }
 
 }  // namespace
@@ -623,16 +728,23 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                    int B, int N, int ldag, int Q, hipStream_t stream) {
   if (B <= 0 || N <= 0) return;
-  smo_ws_update_kernel<<<dim3((N + 255) / 256, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q);
+  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q);
   AV_HIP_CHECK(hipGetLastError());
 }
 
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
-                        long long* inner_total, hipStream_t stream) {
+                        long long* inner_total, float* Kws, hipStream_t stream) {
   if (B <= 0) return;
-  smo_ws_solve_fused_kernel<<<B, SOLVE_T, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
-                                                   inner_total);
+  if (Kws) {  // spread gather (Q x B workgroups) + one-wave solve
+    smo_ws_gather_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(K, N, ws, ok, Kws);
+    AV_HIP_CHECK(hipGetLastError());
+    smo_ws_solve_kernel<<<B, 64, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, max_iter, dA,
+                                              inner_total);
+  } else {
+    smo_ws_solve_fused_kernel<<<B, SOLVE_T, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
+                                                         inner_total);
+  }
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -3,8 +3,9 @@
 // The reference keys every categorical by its raw string, so a field may hold any number of
 // values (e.g. the supplier / product ids of the high-cardinality `hica` driver,
 // J/explore/CategoricalContinuousEncoding.java:116-137, S/explore/CategoricalLeaveOneOutEncoding.scala:80).
-// Tables whose binned fields exceed 255 values carry uint16 codes [F, ld] (65535 = missing); this
-// kernel counts them.
+// Tables whose binned fields exceed 255 values carry uint16 codes [F, ld] (65535 = missing), and
+// beyond 65,534 values int32 codes (INT32_MAX = missing); these kernels count both (templated on the
+// code type; the unsigned compare against bins[f] skips missing codes).
 //
 // Layout: counters are u32 slots c * TB + off_f + code.  When the whole [C, TB] table fits in LDS
 // (<= 36 K counters = 144 KiB of the 160 KiB per CU) each workgroup privatises it: one 1024-thread
@@ -21,8 +22,9 @@ namespace {
 constexpr int kWideThreads = 1024;
 constexpr int kLdsSlots = 36 * 1024;
 
+template <typename CT>
 __global__ __launch_bounds__(kWideThreads) void hist_wide_lds_kernel(
-    const uint16_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const CT* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
     const int* __restrict__ bins, const int* __restrict__ offs, int nfeat, int total_bins, int n_classes,
     int count_labels, unsigned long long* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned int s_tab[];
@@ -36,8 +38,9 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_lds_kernel(
     unsigned int* row = s_tab + c * total_bins;
     if (count_labels) atomicAdd(&row[total_bins - 1], 1u);
     for (int f = 0; f < nfeat; ++f) {
-      const int v = (int)codes[(long long)f * ld + r];  // coalesced: consecutive lanes, consecutive rows
-      if (v < bins[f]) atomicAdd(&row[offs[f] + v], 1u);
+      // coalesced: consecutive lanes, consecutive rows; unsigned compare skips the missing code
+      const unsigned v = (unsigned)codes[(long long)f * ld + r];
+      if (v < (unsigned)bins[f]) atomicAdd(&row[offs[f] + v], 1u);
     }
   }
   __syncthreads();
@@ -47,8 +50,9 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_lds_kernel(
   }
 }
 
+template <typename CT>
 __global__ __launch_bounds__(256) void hist_wide_global_kernel(
-    const uint16_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
+    const CT* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
     const int* __restrict__ bins, const int* __restrict__ offs, int nfeat, int total_bins, int n_classes,
     int count_labels, unsigned long long* __restrict__ out) {
   const long long stride = (long long)gridDim.x * 256;
@@ -58,8 +62,8 @@ __global__ __launch_bounds__(256) void hist_wide_global_kernel(
     unsigned long long* row = out + (long long)c * total_bins;
     if (count_labels) atomicAdd(&row[total_bins - 1], 1ull);
     for (int f = 0; f < nfeat; ++f) {
-      const int v = (int)codes[(long long)f * ld + r];
-      if (v < bins[f]) atomicAdd(&row[offs[f] + v], 1ull);
+      const unsigned v = (unsigned)codes[(long long)f * ld + r];
+      if (v < (unsigned)bins[f]) atomicAdd(&row[(long long)offs[f] + v], 1ull);
     }
   }
 }
@@ -78,31 +82,46 @@ int num_cus() {
 
 namespace avk {
 
-void class_histogram_wide(const uint16_t* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins,
-                          const int* d_offs, int nfeat, int total_bins, int n_classes, int count_labels,
-                          unsigned long long* out, int mode, hipStream_t stream) {
+template <typename CT>
+void hist_wide(const CT* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins, const int* d_offs,
+               int nfeat, int total_bins, int n_classes, int count_labels, unsigned long long* out, int mode,
+               hipStream_t stream) {
   if (n <= 0) return;
   const long long slots = (long long)n_classes * total_bins;
   if (mode != 2 && slots <= kLdsSlots) {
     const size_t lds = (size_t)slots * sizeof(unsigned int);
     static bool attr = false;
     if (!attr) {
-      AV_HIP_CHECK(hipFuncSetAttribute((const void*)hist_wide_lds_kernel,
+      AV_HIP_CHECK(hipFuncSetAttribute((const void*)hist_wide_lds_kernel<CT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSlots * 4));
       attr = true;
     }
     // one block per CU (the table takes most of the LDS), never more blocks than row tiles
     const long long tiles = (n + kWideThreads - 1) / kWideThreads;
     const int grid = (int)std::min<long long>(tiles, (long long)num_cus());
-    hist_wide_lds_kernel<<<grid, kWideThreads, lds, stream>>>(codes, ld, n, labels, d_bins, d_offs, nfeat,
-                                                              total_bins, n_classes, count_labels, out);
+    hist_wide_lds_kernel<CT><<<grid, kWideThreads, lds, stream>>>(codes, ld, n, labels, d_bins, d_offs, nfeat,
+                                                                  total_bins, n_classes, count_labels, out);
   } else {
     const long long tiles = (n + 255) / 256;
     const int grid = (int)std::min<long long>(tiles, (long long)num_cus() * 8);
-    hist_wide_global_kernel<<<grid, 256, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, nfeat, total_bins,
-                                                      n_classes, count_labels, out);
+    hist_wide_global_kernel<CT><<<grid, 256, 0, stream>>>(codes, ld, n, labels, d_bins, d_offs, nfeat, total_bins,
+                                                          n_classes, count_labels, out);
   }
   AV_HIP_CHECK(hipGetLastError());
+}
+
+void class_histogram_wide(const uint16_t* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins,
+                          const int* d_offs, int nfeat, int total_bins, int n_classes, int count_labels,
+                          unsigned long long* out, int mode, hipStream_t stream) {
+  hist_wide<uint16_t>(codes, ld, n, labels, d_bins, d_offs, nfeat, total_bins, n_classes, count_labels, out, mode,
+                      stream);
+}
+
+// int32 codes (categoricals beyond 65,534 values; missing = INT32_MAX)
+void class_histogram_i32(const int* codes, long long ld, long long n, const uint8_t* labels, const int* d_bins,
+                         const int* d_offs, int nfeat, int total_bins, int n_classes, int count_labels,
+                         unsigned long long* out, int mode, hipStream_t stream) {
+  hist_wide<int>(codes, ld, n, labels, d_bins, d_offs, nfeat, total_bins, n_classes, count_labels, out, mode, stream);
 }
 
 }  // namespace avk

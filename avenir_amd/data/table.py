@@ -7,7 +7,8 @@ A ``Table`` is the device-resident form of a CSV file described by a ``FeatureSc
   kernels stream 16 rows per 128-bit load.  Unknown / missing values are coded 255.  When any
   binned field has more than 255 values (the reference keys categoricals by raw string, so
   high-cardinality fields such as supplier / product ids are legal) the table is *wide*: codes are
-  uint16 with 65535 = missing, counted by the K2w kernel (``wide.hip``).
+  uint16 with 65535 = missing, counted by the K2w kernel (``wide.hip``); beyond 65,534 values the
+  codes are int32 with INT32_MAX = missing (same kernel, int32 instantiation).
 * ``numeric`` float32 ``[Fn, ld]`` — continuous (un-bucketized) numeric features.
 * ``labels``  uint8 ``[ld]`` — class attribute codes (255 = unknown).
 * ``ids``     list of record id strings (when the schema has an id field).
@@ -33,15 +34,33 @@ from ..utils.tracing import traced
 CAT, BUCKET, FLOAT, INT = 0, 1, 2, 3
 MISSING = 255
 MISSING16 = 65535
+MISSING32 = 2**31 - 1
+_MISSING_OF = {torch.uint8: MISSING, torch.uint16: MISSING16, torch.int32: MISSING32}
 
 
 def missing_code(codes: torch.Tensor) -> int:
-    """The 'missing / unknown' code of a code tensor (255 for uint8, 65535 for wide uint16)."""
-    return MISSING16 if codes.dtype == torch.uint16 else MISSING
+    """The 'missing / unknown' code of a code tensor (255 uint8, 65535 uint16, INT32_MAX int32)."""
+    return _MISSING_OF.get(codes.dtype, MISSING)
 
 
 def needs_wide(fields) -> bool:
     return any(f.num_bins > 255 for f in fields)
+
+
+def code_width(fields) -> int:
+    """0: uint8 codes, 1: uint16 (> 255 values), 2: int32 (> 65,534 values in some field)."""
+    top = max((f.num_bins for f in fields), default=0)
+    return 2 if top > 65534 else (1 if top > 255 else 0)
+
+
+_CODE_DTYPE = (torch.uint8, torch.uint16, torch.int32)
+
+
+def code_slots(codes: torch.Tensor, bins) -> int:
+    """Per-column table size for code-indexed lookups: every valid code plus one missing slot."""
+    if codes.dtype == torch.int32:
+        return max([int(b) for b in bins] + [1]) + 1
+    return 65536 if codes.dtype == torch.uint16 else 256
 
 
 _ESCAPED_LITERALS = {r"\t": "\t", r"\|": "|", r"\.": ".", r"\\": "\\", r"\$": "$", r"\^": "^"}
@@ -113,7 +132,8 @@ class Table:
 
     @property
     def wide(self) -> bool:
-        return self.codes.dtype == torch.uint16
+        """Codes wider than a byte (uint16, or int32 beyond 65,534 values)."""
+        return self.codes.dtype != torch.uint8
 
     @property
     def total_bins(self) -> int:
@@ -207,13 +227,18 @@ class Table:
 
 
 # ------------------------------------------------------------------------------------------------
-def _spec_for(f: FeatureField, wide: bool = False) -> tuple:
-    top = 65534 if wide else 254
+def _spec_for(f: FeatureField, width: int = 0) -> tuple:
+    """Native parse spec; ``width`` 0 uint8, 1 uint16, 2 int32 codes (categoricals only; buckets
+    stay <= uint16)."""
+    width = int(width)
+    top = (MISSING32 - 1) if width == 2 else (65534 if width else 254)
     if f.is_categorical:
-        return (f.ordinal, CAT, list(f.cardinality or []), 1.0, 0, top, wide)
+        return (f.ordinal, CAT, list(f.cardinality or []), 1.0, 0, top, width)
     if f.is_bucketed:
-        return (f.ordinal, BUCKET, [], float(f.bucket_width), f.bucket_offset, min(top, f.num_bins - 1), wide)
-    return (f.ordinal, FLOAT, [], 1.0, 0, top, False)
+        w = min(width, 1)
+        return (f.ordinal, BUCKET, [], float(f.bucket_width), f.bucket_offset,
+                min(65534 if w else 254, f.num_bins - 1), w)
+    return (f.ordinal, FLOAT, [], 1.0, 0, top, 0)
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -313,18 +338,18 @@ def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *
     for f in feats:
         if f.is_categorical and not f.cardinality:
             if csv is not None:
-                f.cardinality = csv.distinct(f.ordinal, 65535)
+                f.cardinality = csv.distinct(f.ordinal, MISSING32 - 1)
             else:
                 f.cardinality = _distinct_py(_py_lines_of(path, skip_header), f.ordinal, delim)
     binned = [f for f in feats if f.is_binned]
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
-    wide = needs_wide(binned)
-    miss = MISSING16 if wide else MISSING
-    cdt = torch.uint16 if wide else torch.uint8
+    width = code_width(binned)
+    cdt = _CODE_DTYPE[width]
+    miss = _MISSING_OF[cdt]
     if csv is not None:
         total = csv.num_rows()
         r0, r1 = shard_range(total, rank, world)
-        specs = [_spec_for(f, wide) for f in binned] + [_spec_for(f) for f in numeric]
+        specs = [_spec_for(f, width) for f in binned] + [_spec_for(f) for f in numeric]
         if cls_f is not None:
             if not cls_f.cardinality:
                 cls_f.cardinality = csv.distinct(cls_f.ordinal, 255)
@@ -332,8 +357,12 @@ def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *
         cols, _bad = csv.parse(specs, r0, r1)
         n = r1 - r0
         ld = pad16(n)
-        codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned
-                 else torch.zeros((0, ld), dtype=cdt))
+        codes = (torch.stack([c[:ld].to(cdt) if c.dtype != cdt else c[:ld] for c in cols[: len(binned)]])
+                 if binned else torch.zeros((0, ld), dtype=cdt))
+        if binned and cdt == torch.int32:     # uint16 bucket columns: their missing code -> INT32_MAX
+            for j, c in enumerate(cols[: len(binned)]):
+                if c.dtype == torch.uint16:
+                    codes[j][codes[j] == MISSING16] = MISSING32
         numc = cols[len(binned): len(binned) + len(numeric)]
         num = torch.zeros((len(numeric), ld), dtype=torch.float32)
         for i, c in enumerate(numc):
@@ -355,8 +384,14 @@ def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *
         ld = pad16(n)
         codes = torch.full((len(binned), ld), miss, dtype=cdt)
         for j, f in enumerate(binned):
-            codes[j, :n] = torch.tensor([_encode_py(f, r[f.ordinal] if f.ordinal < len(r) else "", miss)
-                                         for r in rows], dtype=torch.int32).to(cdt)
+            if f.is_categorical:     # dictionary lookup (first occurrence wins, as the native parser)
+                lut: dict[str, int] = {}
+                for i, v in enumerate(f.cardinality):
+                    lut.setdefault(v, i)
+                vals = [lut.get(r[f.ordinal].strip(), miss) if f.ordinal < len(r) else miss for r in rows]
+            else:
+                vals = [_encode_py(f, r[f.ordinal] if f.ordinal < len(r) else "", miss) for r in rows]
+            codes[j, :n] = torch.tensor(vals, dtype=torch.int64).to(cdt)
         num = torch.zeros((len(numeric), ld), dtype=torch.float32)
         for j, f in enumerate(numeric):
             num[j, :n] = torch.tensor([_float(r[f.ordinal]) if f.ordinal < len(r) else math.nan
@@ -387,8 +422,11 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     path (raw int64 columns)."""
     binned = [f for f in feats if f.is_binned]
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
-    wide = needs_wide(binned)
-    specs = [_spec_for(f, wide) for f in binned] + [_spec_for(f) for f in numeric]
+    width = code_width(binned)
+    if width > 1:
+        return None                          # int32 codes: the host parser
+    wide = width == 1
+    specs = [_spec_for(f, width) for f in binned] + [_spec_for(f) for f in numeric]
     if cls_f is not None:
         specs.append(_spec_for(cls_f))
     if any(sp[1] not in (CAT, BUCKET, FLOAT) for sp in specs):
@@ -460,14 +498,14 @@ def from_arrays(schema: FeatureSchema, columns: dict[int, Sequence], device="cpu
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
     n = len(next(iter(columns.values())))
     ld = pad16(n)
-    wide = needs_wide(binned)
-    miss = MISSING16 if wide else MISSING
-    codes = torch.full((len(binned), ld), miss, dtype=torch.uint16 if wide else torch.uint8)
+    cdt = _CODE_DTYPE[code_width(binned)]
+    miss = _MISSING_OF[cdt]
+    codes = torch.full((len(binned), ld), miss, dtype=cdt)
     for j, f in enumerate(binned):
         lut = {v: i for i, v in enumerate(f.cardinality)} if f.is_categorical else None
         vals = ([lut.get(str(v).strip(), miss) for v in columns[f.ordinal]] if lut is not None
                 else [_encode_py(f, str(v), miss) for v in columns[f.ordinal]])
-        codes[j, :n] = torch.tensor(vals, dtype=torch.int32).to(codes.dtype)
+        codes[j, :n] = torch.tensor(vals, dtype=torch.int64).to(codes.dtype)
     num = torch.zeros((len(numeric), ld), dtype=torch.float32)
     for j, f in enumerate(numeric):
         num[j, :n] = torch.tensor(np.asarray(columns[f.ordinal], dtype=np.float32))

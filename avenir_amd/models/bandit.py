@@ -182,12 +182,16 @@ class BanditBank:
         gst, ist, ep = self.gstate.cpu().numpy(), self.istate.cpu().numpy(), self.epochs.cpu().numpy()
         out = np.zeros((G, batch), dtype=np.int32)
         code = self.code
+        # arm k on lane k % 64, slot k // 64; E slots (a power of two, as the kernel's template)
+        E = 1
+        while E * 64 < A:
+            E *= 2
         for g in range(G):
             n = trials[g].astype(np.int64)
             mean = np.where(n > 0, rsum[g] / np.maximum(n, 1), 0.0).astype(np.float32)
             total = int(n.sum())
             for b in range(batch):
-                idx = np.uint64((g * batch + b) * 64) + np.arange(64, dtype=np.uint64)
+                idx = np.uint64((g * batch + b) * E * 64) + np.arange(E * 64, dtype=np.uint64)
                 x, y, _, _ = philox4x32(self.seed, self.round, idx)
                 u_lane, v_lane = u32_to_unit(x), u32_to_unit(y)
                 u_a, u_b = float(u32_to_unit(x[:1])[0]), float(u32_to_unit(y[:1])[0])

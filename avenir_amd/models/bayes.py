@@ -310,7 +310,17 @@ class NaiveBayes:
                                    tb["glognorm"] if has_x else None, tb["pmean"] if has_x else None,
                                    tb["pinvstd"] if has_x else None, tb["plognorm"] if has_x else None,
                                    tb["logprior"], bool(ref_scale), post, pred, t.labels, conf)
-        else:   # CPU oracle; also wide (uint16-code) tables on the GPU, as batched torch gathers
+        elif t.device.type == "cuda" and C <= 32:
+            # wide (uint16 / int32 code) tables: transposed model read through L2 (bayes.hip)
+            if "logpT" not in tb:
+                tb["logpT"] = tb["logp"].T.contiguous()
+            _native.C().nb_predict_wide(t.codes.contiguous(), n, offs, H._dev_i32(t.bins, t.device), tb["logpT"],
+                                        tb["logfp"], t.numeric if has_x else None,
+                                        tb["gmean"] if has_x else None, tb["ginvstd"] if has_x else None,
+                                        tb["glognorm"] if has_x else None, tb["pmean"] if has_x else None,
+                                        tb["pinvstd"] if has_x else None, tb["plognorm"] if has_x else None,
+                                        tb["logprior"], bool(ref_scale), post, pred, t.labels, conf)
+        else:   # CPU oracle (and > 32 classes on the GPU, as batched torch gathers)
             self._predict_ref(t, tb, ref_scale, post, pred, conf)
         return NBPrediction(pred[:n], None if post is None else post[:n], conf)
 

@@ -324,13 +324,15 @@ def apply_encoding(t: Table, enc: dict[int, dict[str, float]], default: float = 
     for j, f in enumerate(t.binned_fields):
         if f.ordinal not in enc:
             continue
-        # one slot per code incl. the missing code (255, or 65535 for wide tables)
-        lut = torch.full((t.missing + 1,), default, dtype=torch.float64)
+        # one slot per code incl. the missing code (255 / 65535; int32 codes clamp into the last slot)
+        m = min(t.missing + 1, f.num_bins + 1)
+        lut = torch.full((max(m, t.missing + 1) if t.codes.dtype != torch.int32 else m,), default,
+                         dtype=torch.float64)
         e = enc[f.ordinal]
         ks = [k for k in range(f.num_bins) if f.bin_label(k) in e]
         if ks:
             lut[torch.tensor(ks)] = torch.tensor([e[f.bin_label(k)] for k in ks], dtype=torch.float64)
-        cols.append(lut.float().to(t.device)[t.codes[j, : t.n].long()])
+        cols.append(lut.float().to(t.device)[t.codes[j, : t.n].long().clamp(max=lut.numel() - 1)])
     return torch.stack(cols, 1) if cols else torch.zeros((t.n, 0), device=t.device)
 
 
@@ -358,7 +360,8 @@ def leave_one_out_encoding(t: Table, target: torch.Tensor, noise: float = 0.0, r
     gcnt = torch.tensor([float(n)], dtype=torch.float64, device=y.device)
     nf = len(t.binned_fields)
     codes = t.codes[:nf]
-    s, k = E.loo_stats(codes, n, y)  # K23: per (column, value) target sums and counts
+    from ..data.table import code_slots
+    s, k = E.loo_stats(codes, n, y, code_slots(codes, t.bins[:nf]))  # K23: per (column, value) sums, counts
     _reduce(comm, gsum, gcnt, s, k)
     u = None
     if noise > 0:

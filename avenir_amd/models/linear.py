@@ -80,7 +80,7 @@ def glm_gradient(data: DenseSoA, y: torch.Tensor, w: torch.Tensor, mode: int, sw
     """(g [Dp] f64 = sum sw*x*e, loss f64, h [n] or None) — K13 on GPU, fp64 torch on CPU."""
     wp = torch.zeros((data.Dp,), dtype=torch.float32, device=data.device)
     wp[: w.numel()] = w.to(data.device, torch.float32)
-    if data.device.type == "cuda" and data.Dp <= 32:
+    if data.device.type == "cuda" and data.Dp <= 256:      # K13 (tiled through LDS above 32)
         hw = torch.empty((max(data.n, 1),), dtype=torch.float32, device=data.device) if want_h else None
         out = _native.C().glm_gradient(data.X, data.n, y, sw, wp, int(mode), hw)
         return out[:-1], out[-1], (hw[: data.n] if want_h else None)
@@ -161,8 +161,8 @@ class LogisticRegression:
         g = g[:D].double().clone()
         buf = torch.cat([g, loss.view(1).double()])
         if self.solver == "newton":
-            if data.device.type == "cuda" and D <= 32:
-                H = _native.C().weighted_gram(data.X, data.n, D, h.contiguous())   # MFMA Gram
+            if data.device.type == "cuda" and D <= 1024:
+                H = _native.C().weighted_gram(data.X, data.n, D, h.contiguous())   # MFMA Gram (32x32 blocks)
             else:
                 Xr = data.X[:D, : data.n]
                 H = (Xr * h.view(1, -1)) @ Xr.T                               # [D, D] GEMM

@@ -70,18 +70,29 @@ def moments_dict(row: torch.Tensor) -> dict[str, float]:
             "kurtosis": m4 / sd ** 4 - 3 if sd > 0 else float("nan")}
 
 
-def _slots(codes: torch.Tensor) -> int:
+def _slots(codes: torch.Tensor, slots: int | None = None) -> int:
+    if codes.dtype == torch.int32:
+        if slots is None:
+            raise ValueError("int32 codes need slots = max code + 2 (data.table.code_slots)")
+        return int(slots)
     return 65536 if codes.dtype == torch.uint16 else 256
 
 
-def loo_stats(codes: torch.Tensor, n: int, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+def _clamped(codes: torch.Tensor, n: int, m: int) -> torch.Tensor:
+    """Codes as int64 with every value >= m - 1 (missing, out of range) in the last slot."""
+    return codes[:, :n].long().clamp(max=m - 1)
+
+
+def loo_stats(codes: torch.Tensor, n: int, y: torch.Tensor, slots: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """Per (column, code) target sum (double [F, m]) and count (int32 [F, m]) over ``n`` rows of
-    ``codes`` [F, ld] (uint8: m = 256, uint16: m = 65536)."""
+    ``codes`` [F, ld] (uint8: m = 256, uint16: m = 65536, int32: m = ``slots``; codes >= m - 1 are
+    counted in slot m - 1)."""
     y = y[:n].double().contiguous()
+    m = _slots(codes, slots)
     if codes.is_cuda:
-        return tuple(_native.C().loo_stats(codes.contiguous(), int(n), y))
-    F, m = codes.shape[0], _slots(codes)
-    c = codes[:, :n].long() + torch.arange(F).view(-1, 1) * m
+        return tuple(_native.C().loo_stats(codes.contiguous(), int(n), y, m if codes.dtype == torch.int32 else -1))
+    F = codes.shape[0]
+    c = _clamped(codes, n, m) + torch.arange(F).view(-1, 1) * m
     s = torch.zeros(F * m, dtype=torch.float64).index_add_(0, c.reshape(-1), y.repeat(F))
     k = torch.zeros(F * m, dtype=torch.int64).index_add_(0, c.reshape(-1), torch.ones(F * n, dtype=torch.int64))
     return s.view(F, m), k.view(F, m).int()
@@ -96,11 +107,13 @@ def loo_apply(codes: torch.Tensor, n: int, y: torch.Tensor, s: torch.Tensor, k: 
     if codes.is_cuda:
         nz = noise[:, :n].double().contiguous().to(codes.device) if noise is not None else None
         return _native.C().loo_apply(codes.contiguous(), int(n), y, s.double().contiguous(), k.int().contiguous(),
-                                     gm.to(codes.device), float(reg), nz, float(amp))
+                                     gm.to(codes.device), float(reg), nz, float(amp),
+                                     int(s.shape[1]) if codes.dtype == torch.int32 else -1)
     F = codes.shape[0]
     cols = []
+    cl = _clamped(codes, n, int(s.shape[1]))
     for j in range(F):
-        c = codes[j, :n].long()
+        c = cl[j]
         v = (s[j, c] - y + reg * gm) / (k[j, c].double() - 1 + reg).clamp_min(1e-12)
         if noise is not None:
             v = v * (1 + amp * (2 * noise[j, :n].double() - 1))

@@ -104,19 +104,30 @@ def _impurity(cnt: torch.Tensor, tot: torch.Tensor, algo: int) -> torch.Tensor:
 
 
 def forest_split(hist, fmask, bins_d, offs_d, bins, algo: int, topk: int, rnd):
-    """Per node: (feature, threshold, weighted child impurity, node impurity, left class counts)."""
-    if hist.is_cuda:
+    """Per node: (feature, threshold, weighted child impurity, node impurity, left class counts).
+
+    GPU with <= 16 classes: the fused K6/K7 kernel (forest.hip).  Otherwise the batched tensor
+    twin below, on the histogram's own device (no per-node host loop, any class count)."""
+    if hist.is_cuda and hist.shape[1] <= 16:
         return _native.C().forest_split(hist, fmask, bins_d, offs_d, int(algo), int(topk), rnd)
+    return _forest_split_tensor(hist, fmask, bins, algo, topk, rnd)
+
+
+def _forest_split_tensor(hist, fmask, bins, algo: int, topk: int, rnd):
     A, C, TB = hist.shape
+    dev = hist.device
     F = len(bins)
     h = hist.double()
     tot = h[:, :, TB - 1]                                              # [A, C]
     ntot = tot.sum(1)
-    best = torch.full((A, F), math.inf, dtype=torch.float64)
-    bthr = torch.full((A, F), -1, dtype=torch.int64)
-    o = 0
+    best = torch.full((A, F), math.inf, dtype=torch.float64, device=dev)
+    bthr = torch.full((A, F), -1, dtype=torch.int64, device=dev)
+    offs = [0]
+    for b in bins[:-1]:
+        offs.append(offs[-1] + b)
     for f, B in enumerate(bins):
         if B >= 2:
+            o = offs[f]
             cs = torch.cumsum(h[:, :, o:o + B - 1], 2).transpose(1, 2)   # [A, B-1, C] left counts
             nl = cs.sum(-1)
             nr = ntot.unsqueeze(1) - nl
@@ -124,30 +135,35 @@ def forest_split(hist, fmask, bins_d, offs_d, bins, algo: int, topk: int, rnd):
             s = (nl * _impurity(cs, nl, algo) + nr * _impurity(right, nr, algo)) / ntot.clamp_min(1e-300).unsqueeze(1)
             s = torch.where((nl > 0) & (nr > 0), s, torch.full_like(s, math.inf))
             v, i = s.min(1)                                             # first minimum
-            ok = fmask[:, f].bool()
+            ok = fmask[:, f].to(dev).bool()
             best[:, f] = torch.where(ok, v, torch.full_like(v, math.inf))
             bthr[:, f] = torch.where(ok & torch.isfinite(v), i, torch.full_like(i, -1))
-        o += B
-    feat = torch.full((A,), -1, dtype=torch.int32)
-    thr = torch.full((A,), -1, dtype=torch.int32)
-    score = torch.full((A,), math.inf, dtype=torch.float32)
-    left = torch.zeros((A, C), dtype=torch.int64)
-    offs = [0]
-    for b in bins[:-1]:
-        offs.append(offs[-1] + b)
-    for a in range(A):
-        row = best[a]
-        if topk <= 1:
-            v, f = row.min(0)
-            pick = int(f) if math.isfinite(float(v)) else -1
-        else:
-            order = sorted([f for f in range(F) if math.isfinite(float(row[f]))], key=lambda f: (float(row[f]), f))
-            chosen = order[: min(topk, 32)]
-            pick = chosen[min(int(float(rnd[a]) * len(chosen)), len(chosen) - 1)] if chosen else -1
-        if pick >= 0:
-            t = int(bthr[a, pick])
-            feat[a], thr[a], score[a] = pick, t, float(row[pick])
-            left[a] = hist[a, :, offs[pick]: offs[pick] + t + 1].sum(1)
+    fin = torch.isfinite(best)
+    if topk <= 1:
+        v, pick = best.min(1)                                           # first minimum feature
+        has = torch.isfinite(v)
+    else:
+        # stable sort by (score, feature): the random choice among the top min(topk, 32) features
+        order = torch.sort(best, dim=1, stable=True).indices
+        kk = torch.clamp(fin.sum(1), max=min(int(topk), 32))
+        has = kk > 0
+        j = (rnd[:A].to(dev).double() * kk.double()).long()
+        j = torch.minimum(j, (kk - 1).clamp_min(0))
+        pick = order.gather(1, j.view(-1, 1)).view(-1)
+    pick = torch.where(has, pick, torch.zeros_like(pick))
+    t = bthr.gather(1, pick.view(-1, 1)).view(-1)
+    sc = best.gather(1, pick.view(-1, 1)).view(-1)
+    feat = torch.where(has, pick, torch.full_like(pick, -1)).int()
+    thr = torch.where(has, t, torch.full_like(t, -1)).int()
+    score = torch.where(has, sc, torch.full_like(sc, math.inf)).float()
+    # left counts = class histogram of the chosen feature's bins 0..thr (exact int64 prefix sums)
+    offs_t = torch.tensor(offs, dtype=torch.int64, device=dev)
+    cum = torch.cumsum(hist.long(), 2)                                  # [A, C, TB]
+    o = offs_t[pick]
+    hi = (o + t.clamp_min(0)).view(-1, 1, 1).expand(A, C, 1)
+    lo = (o - 1).clamp_min(0).view(-1, 1, 1).expand(A, C, 1)
+    left = cum.gather(2, hi).squeeze(2) - torch.where((o > 0).view(-1, 1), cum.gather(2, lo).squeeze(2), 0)
+    left = torch.where(has.view(-1, 1), left, torch.zeros_like(left))
     imp = _impurity(tot, ntot, algo).float()
     return feat, thr, score, imp, left
 

@@ -83,3 +83,42 @@ def test_bandit_kernel_matches_reference(cuda, algo):
     gpu_bank, gpu_picks = _run(algo, cuda, groups=64, rounds=rounds, seed=3)
     agree = float((cpu_picks == gpu_picks).float().mean())
     assert agree > 0.97, (algo, agree)
+
+
+def _run_many(algo, device="cpu", A=100, groups=8, rounds=120, seed=0):
+    p = torch.linspace(0.05, 0.6, A)
+    p[37] = 0.95                                            # the best arm sits in the second slot
+    bank = BanditBank(algo, [f"a{i}" for i in range(A)], groups, CFG[algo], device=device, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    picks = []
+    for _ in range(rounds):
+        act = bank.next_actions(1)[:, 0].cpu().long()
+        picks.append(act)
+        r = (torch.rand(groups, generator=g) < p[act]).float()
+        bank.set_rewards(torch.arange(groups), act, r)
+    return bank, torch.stack(picks)
+
+
+@pytest.mark.parametrize("algo", ["upperConfidenceBoundOne", "thompsonSampler", "randomGreedy"])
+def test_hundred_arm_bandit(algo):
+    """> 64 arms: arms spread over E = 2 lane slots (bandit.hip) — every arm is reachable, and the
+    learners that converge within 400 rounds at 100 arms move to better arms (UCB1 still explores)."""
+    _, picks = _run_many(algo, rounds=400)
+    assert int(picks.max()) >= 64 and int(picks.min()) >= 0
+    assert len(set(picks.reshape(-1).tolist())) > 90                # min.trial visits every arm
+    if algo != "upperConfidenceBoundOne":
+        p = torch.linspace(0.05, 0.6, 100)
+        p[37] = 0.95
+        assert float(p[picks[-100:]].mean()) > 0.42, algo
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", sorted(ALGOS))
+@pytest.mark.parametrize("A", [100, 1000])
+def test_many_arm_bandit_kernel_matches_reference(cuda, algo, A):
+    if algo == "exponentialWeightExpert":
+        pytest.skip("expert advice matrix is [experts, arms]; covered at 4 arms")
+    _, cpu_picks = _run_many(algo, "cpu", A=A, groups=32, rounds=20, seed=3)
+    _, gpu_picks = _run_many(algo, cuda, A=A, groups=32, rounds=20, seed=3)
+    agree = float((cpu_picks == gpu_picks).float().mean())
+    assert agree > 0.97, (algo, A, agree)

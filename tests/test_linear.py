@@ -181,7 +181,7 @@ def test_cascade_svm():
 
 @pytest.mark.gpu
 def test_glm_kernel_matches_oracle(cuda):
-    for d in (3, 7, 15, 31):
+    for d in (3, 7, 15, 31, 40, 99, 200):      # > 32: the LDS-tiled kernel
         X, y, _ = _logit_data(100_003, d, seed=d)
         data = DenseSoA(X, device=cuda)
         gen = torch.Generator().manual_seed(100 + d)
@@ -207,6 +207,15 @@ def test_logistic_regression_gpu(cuda):
 
 
 @pytest.mark.gpu
+def test_logistic_regression_wide_gpu(cuda):
+    """D = 100 features (101 with the intercept): tiled K13 gradient + blocked MFMA Newton Hessian."""
+    X, y, w = _logit_data(300_000, 100, seed=4)
+    m = LogisticRegression(max_iter=8).fit(X.to(cuda), y.to(cuda))
+    ref = LogisticRegression(max_iter=8).fit(X, y)
+    assert torch.allclose(m.coef.cpu(), ref.coef, atol=2e-3)
+
+
+@pytest.mark.gpu
 def test_smo_kernel_matches_reference(cuda):
     X, y = _blobs(400, seed=2)
     ys = torch.where(y == 1, 1.0, -1.0)
@@ -227,7 +236,7 @@ def test_smo_kernel_matches_reference(cuda):
 @pytest.mark.gpu
 def test_weighted_gram_mfma(cuda):
     from avenir_amd import _native
-    for d, n in ((5, 1000), (16, 100_003), (32, 4097)):
+    for d, n in ((5, 1000), (16, 100_003), (32, 4097), (33, 5000), (100, 100_003), (250, 20_011)):
         g = torch.Generator().manual_seed(d)
         X = torch.randn((d, n), generator=g)
         h = torch.rand(n, generator=g)

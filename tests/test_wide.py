@@ -143,3 +143,85 @@ def test_wide_encoding_gpu_matches_cpu(cuda, tmp_path):
                    or (math.isnan(da[v]) and math.isnan(db[v])) for v in db)
     cg = H.class_histogram(tg.codes, tg.n, tg.bins, tg.labels, tg.n_classes)
     assert torch.equal(cg.cpu(), H.class_histogram(t.codes, t.n, t.bins, t.labels, t.n_classes))
+
+
+# ---------------------------------------------------------------------------------------------
+# > 65,534 values: int32 codes (INT32_MAX = missing), same kernels (int32 instantiations)
+# ---------------------------------------------------------------------------------------------
+HUGE = 100_000
+
+
+def test_huge_categorical_table_and_encodings(tmp_path):
+    data, sp, lines = _write(tmp_path, n=150_000, nv=HUGE, seed=2)
+    t = load_csv(data, FeatureSchema.from_json(sp), ",")
+    assert t.codes.dtype == torch.int32 and t.wide and t.missing == 2**31 - 1
+    sup_f = t.binned_fields[0]
+    assert sup_f.num_bins > 65535
+    # codes round-trip to the raw strings (first-seen dictionary order)
+    for i in (0, 5, 149_999):
+        assert sup_f.cardinality[int(t.codes[0, i])] == lines[i].split(",")[1]
+    enc = supervised_encoding(t, "supervisedRatio", 1000, pos_class=1)
+    cnt = _oracle_counts(lines)
+    for v in list(cnt)[:200]:
+        neg, pos = cnt[v]
+        assert enc[1][v] == math.trunc(pos * 1000 / (pos + neg))
+    X = apply_encoding(t, enc)
+    assert float(X[7, 0]) == enc[1][lines[7].split(",")[1]]
+    y = (t.labels[: t.n] == 1).double()
+    loo = leave_one_out_encoding(t, y)
+    sums = collections.defaultdict(float)
+    cnts = collections.defaultdict(int)
+    for ln in lines:
+        r = ln.split(",")
+        sums[r[1]] += r[3] == "T"
+        cnts[r[1]] += 1
+    for i in (0, 17, 123_456):
+        r = lines[i].split(",")
+        exp = (sums[r[1]] - float(r[3] == "T")) / max(cnts[r[1]] - 1, 1e-12)
+        assert abs(float(loo[i, 0]) - exp) < 1e-5
+    # the pure-Python parser (regex delimiter) gives the same int32 table
+    t2 = load_csv(data, FeatureSchema.from_json(sp), ",+")
+    assert t2.codes.dtype == torch.int32 and torch.equal(t2.codes[:, : t2.n], t.codes[:, : t.n])
+
+
+def test_huge_categorical_naive_bayes_cpu(tmp_path):
+    from avenir_amd.models.bayes import NaiveBayes
+    data, sp, _ = _write(tmp_path, n=150_000, nv=HUGE, seed=3)
+    t = load_csv(data, FeatureSchema.from_json(sp), ",")
+    assert t.codes.dtype == torch.int32
+    nb = NaiveBayes().fit(t)
+    p = nb.predict(t)
+    assert p.pred.shape[0] == t.n and float(p.prob.sum(1).mean()) == pytest.approx(1.0, rel=1e-4)
+
+
+@pytest.mark.gpu
+def test_huge_categorical_gpu_matches_cpu(cuda, tmp_path):
+    from avenir_amd.models.bayes import NaiveBayes
+    data, sp, _ = _write(tmp_path, n=400_000, nv=HUGE, seed=4)
+    t = load_csv(data, FeatureSchema.from_json(sp), ",")
+    tg = load_csv(data, FeatureSchema.from_json(sp), ",", device=cuda)
+    assert tg.codes.dtype == torch.int32 and torch.equal(tg.codes.cpu(), t.codes)
+    for mode in (0, 2):
+        assert torch.equal(H.class_histogram(tg.codes, tg.n, tg.bins, tg.labels, 2, mode=mode).cpu(),
+                           H.class_histogram(t.codes, t.n, t.bins, t.labels, 2))
+    assert supervised_encoding(tg, "supervisedRatio") == supervised_encoding(t, "supervisedRatio")
+    y = (t.labels[: t.n] == 1).double()
+    assert torch.allclose(leave_one_out_encoding(tg, y.to(cuda)).cpu(), leave_one_out_encoding(t, y))
+    pc = NaiveBayes().fit(t).predict(t)
+    pg = NaiveBayes().fit(tg).predict(tg)                  # nb_predict_wide, int32 instantiation
+    assert torch.equal(pg.pred.cpu(), pc.pred)
+    assert torch.allclose(pg.prob.cpu(), pc.prob, atol=1e-5)
+    assert torch.equal(pg.confusion.cpu(), pc.confusion)
+
+
+@pytest.mark.gpu
+def test_wide_naive_bayes_predict_kernel(cuda, tmp_path):
+    """uint16-code tables take the wide NB kernel on the GPU (previously a torch fallback)."""
+    from avenir_amd.models.bayes import NaiveBayes
+    data, sp, _ = _write(tmp_path)
+    t = load_csv(data, FeatureSchema.from_json(sp), ",")
+    tg = t.to(cuda)
+    pc = NaiveBayes().fit(t).predict(t)
+    pg = NaiveBayes().fit(tg).predict(tg)
+    assert torch.equal(pg.pred.cpu(), pc.pred)
+    assert torch.allclose(pg.prob.cpu(), pc.prob, atol=1e-5)

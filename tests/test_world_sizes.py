@@ -141,7 +141,8 @@ def _compare(res, ref, world, score_rel=1e-9):
                     "forest_ref"):
             assert got[key] == ref[key], f"rank {r}/{world}: {key} differs"
         assert got["kmeans"] == pytest.approx(ref["kmeans"], rel=1e-5)
-        assert np.allclose(got["logit"], ref["logit"], rtol=1e-7, atol=1e-9)
+        # device: the fp32 K13 gradient partials depend on the row sharding (fp64 across ranks)
+        assert np.allclose(got["logit"], ref["logit"], rtol=max(1e-7, score_rel * 2), atol=1e-9)
         assert np.allclose(got["knn"][0], ref["knn"][0], atol=1e-5)
         assert got["knn"][1] == ref["knn"][1]
         assert got["viterbi"][1] == pytest.approx(ref["viterbi"][1], rel=score_rel)
