@@ -581,6 +581,62 @@ void gbt_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::
                   (float)lr, F.data_ptr<float>(), (int)F.size(1), (int)k, cur_stream(codes));
 }
 
+// One GBT level's split scoring (gbt.hip gbt_split_kernel).  Either `hist` [A, TB, 2] int64, or
+// `parent` / `left` [A / 2, TB, 2] (sibling subtraction); `out_hist` [A, TB, 2] or None receives the
+// level's histogram.  Scan tables: int32 [nb] (pvalid uint8).  Heap arrays feat / thr int32, val f64.
+void gbt_split(const c10::optional<at::Tensor>& hist, const c10::optional<at::Tensor>& parent,
+               const c10::optional<at::Tensor>& left, const c10::optional<at::Tensor>& out_hist, int64_t A,
+               int64_t tot, const at::Tensor& pfeat, const at::Tensor& pthr, const at::Tensor& pstart,
+               const at::Tensor& pend, const at::Tensor& pvalid, double l2, double scale, int64_t level,
+               at::Tensor& feat, at::Tensor& thr, at::Tensor& val) {
+  const bool has_h = hist.has_value() && hist->defined();
+  const at::Tensor& ref = has_h ? *hist : *left;
+  TORCH_CHECK(has_h || (parent.has_value() && parent->defined() && left.has_value() && left->defined()),
+              "gbt_split: hist, or parent + left");
+  CHECK_DEV(ref);
+  CHECK_DTYPE(ref, at::kLong);
+  TORCH_CHECK(ref.dim() == 3 && ref.size(2) == 2 && ref.is_contiguous(), "histograms must be [nodes, TB, 2]");
+  const int64_t TB = ref.size(1);
+  if (has_h) {
+    TORCH_CHECK(hist->size(0) == A, "hist must have A nodes");
+  } else {
+    TORCH_CHECK(A % 2 == 0 && left->size(0) == A / 2 && parent->sizes() == left->sizes() && parent->is_contiguous() &&
+                    parent->scalar_type() == at::kLong,
+                "parent / left must be [A / 2, TB, 2] int64");
+  }
+  long long* oh = nullptr;
+  if (out_hist.has_value() && out_hist->defined()) {
+    TORCH_CHECK(out_hist->scalar_type() == at::kLong && out_hist->is_contiguous() && out_hist->size(0) == A &&
+                    out_hist->size(1) == TB && out_hist->size(2) == 2,
+                "out_hist must be [A, TB, 2] int64");
+    oh = reinterpret_cast<long long*>(out_hist->data_ptr<int64_t>());
+  }
+  const int64_t nb = pfeat.numel();
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&pfeat, &pthr, &pstart, &pend}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kInt);
+    TORCH_CHECK(t->numel() == nb, "scan tables must have nb entries");
+  }
+  CHECK_DTYPE(pvalid, at::kByte);
+  TORCH_CHECK(pvalid.numel() == nb && nb < TB && tot >= 0 && tot < TB, "scan tables / total bin");
+  // (no host read-back of the scan tables: this runs inside captured graphs; the kernel clamps
+  // every table-derived index into [p, nb))
+  CHECK_DTYPE(feat, at::kInt);
+  CHECK_DTYPE(thr, at::kInt);
+  CHECK_DTYPE(val, at::kDouble);
+  TORCH_CHECK(level >= 0 && level < 24 && A == (1LL << level), "A must be 2^level");
+  const int64_t hb = A - 1, hc = 2 * A - 1;
+  TORCH_CHECK(feat.numel() >= hc && thr.numel() >= hc && val.numel() >= hc + 2 * A, "heap arrays too short");
+  DevGuard gd(ref.device());
+  using ll = const long long*;
+  avk::gbt_split(has_h ? reinterpret_cast<ll>(hist->data_ptr<int64_t>()) : nullptr,
+                 has_h ? nullptr : reinterpret_cast<ll>(parent->data_ptr<int64_t>()),
+                 has_h ? nullptr : reinterpret_cast<ll>(left->data_ptr<int64_t>()), oh, (int)A, (int)TB, (int)tot, pfeat.data_ptr<int>(),
+                 pthr.data_ptr<int>(), pstart.data_ptr<int>(), pend.data_ptr<int>(), pvalid.data_ptr<uint8_t>(),
+                 (int)nb, l2, 1.0 / scale, (int)hb, (int)hc, level == 0 ? 1 : 0, feat.data_ptr<int>(),
+                 thr.data_ptr<int>(), val.data_ptr<double>(), cur_stream(ref));
+}
+
 void tree_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::Tensor& split_feat,
                  const at::Tensor& segmap, const at::Tensor& child_of) {
   check_codes(codes, n);
@@ -2528,6 +2584,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("h"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_nodes"), py::arg("out"),
         py::arg("even_only") = false);
   m.def("gbt_grad", &gbt_grad);
+  m.def("gbt_split", &gbt_split);
   m.def("resample_uniform", &resample_uniform);
   m.def("smote", &smote);
   m.def("gbt_assign", &gbt_assign);

@@ -204,6 +204,10 @@ void smote(const float* X, const float* Xn, const int* nn, const int* Cs, const 
 // device GBT round (gbt.hip)
 void gbt_grad(const float* F, int K, int k, const uint8_t* y, long long n, long long row_off, unsigned long long seed,
               unsigned rate32, float* g, float* h, double* loss, hipStream_t stream);
+void gbt_split(const long long* hist, const long long* parent, const long long* left, long long* out_hist, int A,
+               int TB, int tot, const int* pfeat, const int* pthr, const int* pstart, const int* pend,
+               const unsigned char* pvalid, int nb, double l2, double invS, int hb, int hc, int level0, int* feat,
+               int* thr, double* val, hipStream_t stream);
 void gbt_assign(const uint8_t* codes, long long ld, long long n, int* node, const int* feat, const int* thr,
                 const double* value, const int* bins, int level, int last, float lr, float* F, int K, int k,
                 hipStream_t stream);

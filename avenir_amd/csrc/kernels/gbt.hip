@@ -99,9 +99,113 @@ __global__ __launch_bounds__(GT) void gbt_assign_kernel(const uint8_t* __restric
   }
 }
 
+// Split scoring of one level, one workgroup per node (replaces ~25 small tensor ops per level):
+//   * the node's [TB][2] fixed-point (g, h) histogram: given (level 0 / no subtraction), or built
+//     from the parent level's histogram and the left-children histogram (odd slot = parent - left,
+//     exact in int64) and written out as the next level's parent;
+//   * per feature, the exact int64 prefix over its bins (one thread per feature);
+//   * gain = gl^2 / max(hl + l2, 1e-12) + gr^2 / max(hr + l2, 1e-12) - parent over every threshold
+//     position (fp64, no FMA contraction, the expression order of the host twin in models/tree.py),
+//     argmax with ties to the lowest position;
+//   * the node's feature / threshold and its two children's Newton values into the heap.
+// Positions p < nb are the features' bins in histogram order (pstart / pend: the feature's first
+// and last bin, pvalid: p < pend); bin `tot` is the node total (the all-rows extra feature).
+constexpr int GS_T = 256;
+
+__global__ __launch_bounds__(GS_T) void gbt_split_kernel(const long long* __restrict__ hist,
+                                                         const long long* __restrict__ parent,
+                                                         const long long* __restrict__ left,
+                                                         long long* __restrict__ out_hist, int TB, int tot,
+                                                         const int* __restrict__ pfeat, const int* __restrict__ pthr,
+                                                         const int* __restrict__ pstart, const int* __restrict__ pend,
+                                                         const unsigned char* __restrict__ pvalid, int nb, double l2,
+                                                         double invS, int hb, int hc, int level0,
+                                                         int* __restrict__ feat, int* __restrict__ thr,
+                                                         double* __restrict__ val) {
+#pragma clang fp contract(off)
+  extern __shared__ long long gs_smem[];
+  long long* sh = gs_smem;            // [TB][2]
+  long long* cs = gs_smem + 2 * TB;   // [nb][2] per-feature prefix sums
+  __shared__ double bg[GS_T / 64];
+  __shared__ int bp[GS_T / 64];
+  const int a = blockIdx.x, tid = threadIdx.x;
+  const long long w2 = 2LL * TB;
+  for (int i = tid; i < 2 * TB; i += GS_T) {
+    long long v;
+    if (hist) {
+      v = hist[a * w2 + i];
+    } else {
+      const long long l = left[(long long)(a >> 1) * w2 + i];
+      v = (a & 1) ? parent[(long long)(a >> 1) * w2 + i] - l : l;
+    }
+    sh[i] = v;
+    if (out_hist) out_hist[a * w2 + i] = v;
+  }
+  __syncthreads();
+  for (int p = tid; p < nb; p += GS_T) {
+    if (pstart[p] != p) continue;  // one thread per feature
+    const int e = min(max(pend[p], p), nb - 1);
+    long long g = 0, h = 0;
+    for (int q = p; q <= e; ++q) {
+      g += sh[2 * q];
+      h += sh[2 * q + 1];
+      cs[2 * q] = g;
+      cs[2 * q + 1] = h;
+    }
+  }
+  __syncthreads();
+  const double G = (double)sh[2 * tot] * invS, H = (double)sh[2 * tot + 1] * invS;
+  const double par = G * G / fmax(H + l2, 1e-12);
+  double best = -INFINITY;
+  int bpos = 0x7fffffff;
+  for (int p = tid; p < nb; p += GS_T) {
+    const int e = min(max(pend[p], p), nb - 1);
+    const double gl = (double)cs[2 * p] * invS, hl = (double)cs[2 * p + 1] * invS;
+    const double gr = (double)(cs[2 * e] - cs[2 * p]) * invS, hr = (double)(cs[2 * e + 1] - cs[2 * p + 1]) * invS;
+    double gain = -INFINITY;
+    if (hl > 1e-12 && hr > 1e-12 && pvalid[p]) gain = gl * gl / fmax(hl + l2, 1e-12) + gr * gr / fmax(hr + l2, 1e-12) - par;
+    if (gain > best) { best = gain; bpos = p; }  // p ascends per thread: the first maximum stays
+  }
+  // block argmax, ties -> lowest position
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o, 64);
+    const int op = __shfl_xor(bpos, o, 64);
+    if (ob > best || (ob == best && op < bpos)) { best = ob; bpos = op; }
+  }
+  if ((tid & 63) == 0) { bg[tid >> 6] = best; bp[tid >> 6] = bpos; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < GS_T / 64; ++w)
+      if (bg[w] > best || (bg[w] == best && bp[w] < bpos)) { best = bg[w]; bpos = bp[w]; }
+    const bool split = isfinite(best) && best > 1e-12;
+    const int p = bpos < nb ? bpos : 0;
+    feat[hb + a] = split ? pfeat[p] : -1;
+    thr[hb + a] = pthr[p];
+    const int e = min(max(pend[p], p), nb - 1);
+    const double gl = (double)cs[2 * p] * invS, hl = (double)cs[2 * p + 1] * invS;
+    const double gr = (double)(cs[2 * e] - cs[2 * p]) * invS, hr = (double)(cs[2 * e + 1] - cs[2 * p + 1]) * invS;
+    val[hc + 2 * a] = split ? -gl / fmax(hl + l2, 1e-12) : 0.0;
+    val[hc + 2 * a + 1] = split ? -gr / fmax(hr + l2, 1e-12) : 0.0;
+    if (level0) val[0] = -G / fmax(H + l2, 1e-12);
+  }
+}
+
 }  // namespace
 
 namespace avk {
+
+void gbt_split(const long long* hist, const long long* parent, const long long* left, long long* out_hist, int A,
+               int TB, int tot, const int* pfeat, const int* pthr, const int* pstart, const int* pend,
+               const unsigned char* pvalid, int nb, double l2, double invS, int hb, int hc, int level0, int* feat,
+               int* thr, double* val, hipStream_t stream) {
+  if (A <= 0) return;
+  const size_t lds = sizeof(long long) * 2 * ((size_t)TB + nb);
+  if (lds > 160 * 1024) throw std::runtime_error("gbt_split: histogram exceeds LDS");
+  gbt_split_kernel<<<A, GS_T, lds, stream>>>(hist, parent, left, out_hist, TB, tot, pfeat, pthr, pstart, pend, pvalid,
+                                             nb, l2, invS, hb, hc, level0, feat, thr, val);
+  AV_HIP_CHECK(hipGetLastError());
+}
 
 void gbt_grad(const float* F, int K, int k, const uint8_t* y, long long n, long long row_off, unsigned long long seed,
               unsigned rate32, float* g, float* h, double* loss, hipStream_t stream) {

@@ -1142,8 +1142,11 @@ class GradientBoostedTrees:
                 comm.all_reduce(hh)
             return hh
 
-        hist = grad_hist(1, False)
         D = p.max_depth
+        if codes.is_cuda:
+            self._build_tree_device(st, k, grad_hist_raw=lambda A, even: self._grad_hist_raw(st, comm, g, h, A, even))
+            return
+        hist = grad_hist(1, False)
         for lvl in range(D):
             A = 1 << lvl
             hb, hc = A - 1, 2 * A - 1
@@ -1182,6 +1185,39 @@ class GradientBoostedTrees:
                 hist = torch.stack([hl_, hist - hl_], 1).view(2 * A, *hist.shape[1:])
             else:
                 hist = grad_hist(2 * A, False)
+
+    @staticmethod
+    def _grad_hist_raw(st, comm, g, h, A, even):
+        hh = T.node_grad_histogram(st["codes"], st["n"], st["node"], g, h, st["bins"], A, even_only=even,
+                                   bins_d=st["bins_d"], offs_d=st["offs_d"], raw=True)
+        if comm.is_distributed:
+            comm.all_reduce(hh)               # exact int64 fixed point
+        return hh
+
+    def _build_tree_device(self, st: dict, k: int, grad_hist_raw) -> None:
+        """GPU levels: raw fixed-point histograms -> ONE split-scoring launch per level
+        (gbt_split_kernel: sibling subtraction, prefix sums, gains, argmax, heap writes) -> the
+        assign / leaf-update launch.  Same results as the tensor scan of ``_build_tree``."""
+        p = self.p
+        codes, n, sc = st["codes"], st["n"], self._scan
+        node, feat, thr, val = st["node"], st["feat"], st["thr"], st["val"]
+        tot = st["offs"][-1]
+        D = p.max_depth
+        hist, parent, left = grad_hist_raw(1, False), None, None
+        for lvl in range(D):
+            A = 1 << lvl
+            last = lvl + 1 == D
+            keep = st["subtract"] and not last          # this level's histogram is the next one's parent
+            out_h = torch.empty((A, hist.shape[1] if hist is not None else left.shape[1], 2), dtype=torch.int64,
+                                device=codes.device) if keep else None
+            T.gbt_split(hist, parent, left, out_h, A, tot, sc, p.l2, lvl, feat, thr, val)
+            T.gbt_assign(codes, n, node, feat, thr, val, st["bins_t"], lvl, last, p.learning_rate, st["F"], k)
+            if last:
+                break
+            if st["subtract"]:
+                hist, parent, left = None, out_h, grad_hist_raw(A, True)
+            else:
+                hist, parent, left = grad_hist_raw(2 * A, False), None, None
 
     def _trees_from_heaps(self, feat, thr, val) -> list[list[DecisionTree]]:
         """Host DecisionTrees from the [R, K, heap] arrays (nodes reachable from the root only)."""
@@ -1246,6 +1282,9 @@ class GradientBoostedTrees:
             "end": torch.cat([torch.full((b,), o + b - 1, dtype=torch.long) for o, b in zip(offs0, fb)]).to(dev),
             "valid": torch.cat([torch.arange(b) < b - 1 for b in fb]).to(dev),
         }
+        sc = self._scan
+        sc.update({"feat_i": sc["feat"].int(), "thr_i": sc["thr"].int(), "start_i": sc["start"].int(),
+                   "end_i": sc["end"].int(), "valid_u8": sc["valid"].to(torch.uint8)})
         C = t.n_classes
         self.n_classes = C
         y = t.labels[:n].long().clamp_max(C - 1)

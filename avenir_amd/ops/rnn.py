@@ -15,8 +15,12 @@ Numerics (mixed precision): GEMM operands and the B·T·4H-sized intermediates (
 gate gradients) are bf16 with fp32 accumulation; gate math, the cell state, h outputs and the
 weight gradients are fp32.  ``lstm_reference`` is the fp32 oracle.
 Hidden or input sizes above 128 (beyond the register-resident design) use PyTorch's MIOpen LSTM
-on the GPU; that is the only non-kernel path and it is selected by shape, never by a missing
-extension.
+on the GPU; that path is selected by shape, never by a missing extension.
+
+``FusedLSTM(precision="fp32")`` keeps the reference's numerics end to end (P/supv/lstm.py trains
+an fp32 ``nn.LSTM``): every op in fp32, on MIOpen's fp32 LSTM on the GPU.  The default
+``precision="bf16"`` is the fused mixed-precision kernel above; ``tests/test_rnn.py`` checks its
+training loss curve against an fp32 ``nn.LSTM`` from the same initialisation.
 """
 from __future__ import annotations
 
@@ -204,10 +208,13 @@ class FusedLSTM(torch.nn.Module):
     dicts load either way.  ``forward(x, (h0, c0)) -> (out, (h_n, c_n))``."""
 
     def __init__(self, input_size: int, hidden_size: int, num_layers: int = 1, bias: bool = True,
-                 batch_first: bool = True, dropout: float = 0.0):
+                 batch_first: bool = True, dropout: float = 0.0, precision: str = "bf16"):
         super().__init__()
         if not batch_first:
             raise ValueError("FusedLSTM is batch-first")
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' (fused mixed-precision kernel) or 'fp32', got {precision!r}")
+        self.precision = precision
         self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
         self.bias, self.dropout, self.batch_first = bias, float(dropout), True
         H = hidden_size
@@ -235,8 +242,8 @@ class FusedLSTM(torch.nn.Module):
 
     def forward(self, x, hx=None):
         H, L = self.hidden_size, self.num_layers
-        if x.is_cuda and (H > MAX_FUSED_HIDDEN or self.input_size > MAX_FUSED_HIDDEN):
-            # beyond the register-resident kernel: MIOpen
+        if x.is_cuda and (H > MAX_FUSED_HIDDEN or self.input_size > MAX_FUSED_HIDDEN or self.precision == "fp32"):
+            # beyond the register-resident kernel, or fp32 numerics requested: MIOpen (fp32)
             if hx is None:
                 z = x.new_zeros(L, x.shape[0], H)
                 hx = (z, z)

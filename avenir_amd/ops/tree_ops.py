@@ -47,7 +47,8 @@ def node_histogram(codes: torch.Tensor, n: int, labels: torch.Tensor, node: torc
 
 def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torch.Tensor,
                         h: torch.Tensor, bins: Sequence[int], n_nodes: int, even_only: bool = False,
-                        bins_d: torch.Tensor | None = None, offs_d: torch.Tensor | None = None) -> torch.Tensor:
+                        bins_d: torch.Tensor | None = None, offs_d: torch.Tensor | None = None,
+                        raw: bool = False) -> torch.Tensor:
     """Exact fixed-point (2^-24) sums of gradient and hessian per (node, bin): float64 [A, TB, 2].
     ``even_only``: only rows of even node ids, counted at id / 2 (the left children of a level, for
     sibling subtraction).  ``bins_d`` / ``offs_d``: cached device copies of the bin tables."""
@@ -61,7 +62,7 @@ def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torc
                                             bins_d if bins_d is not None else _dev_i32(bins, codes.device),
                                             offs_d if offs_d is not None else _dev_i32(_offs(bins), codes.device),
                                             tb, int(n_nodes), out, bool(even_only))
-        return out.double() / _GRAD_SCALE
+        return out if raw else out.double() / _GRAD_SCALE
     out = torch.zeros((n_nodes, tb, 2), dtype=torch.int64)
     nd = node[:n].long()
     if even_only:
@@ -76,7 +77,18 @@ def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torc
         base = (nd[ok] * tb + o + v[ok]) * 2
         flat.index_add_(0, base, gi[ok])
         flat.index_add_(0, base + 1, hi[ok])
-    return out.double() / _GRAD_SCALE
+    return out if raw else out.double() / _GRAD_SCALE
+
+
+def gbt_split(hist, parent, left, out_hist, A: int, tot: int, scan: dict, l2: float, level: int,
+              feat, thr, val) -> None:
+    """One GBT level's split scoring on the device (gbt.hip gbt_split_kernel): raw int64 fixed-point
+    histograms in (``hist`` [A, TB, 2], or ``parent`` / ``left`` [A/2, TB, 2] for sibling
+    subtraction), heap feat / thr / val out; ``out_hist`` receives the level's histogram.  The
+    host twin is the tensor scan in models/tree.py GradientBoostedTrees._build_tree."""
+    _native.C().gbt_split(hist, parent, left, out_hist, int(A), int(tot), scan["feat_i"], scan["thr_i"],
+                          scan["start_i"], scan["end_i"], scan["valid_u8"], float(l2), _GRAD_SCALE, int(level),
+                          feat, thr, val)
 
 
 def gbt_grad(F: torch.Tensor, k: int, y: torch.Tensor, n: int, row_off: int, seed: int, rate32: int,

@@ -62,9 +62,14 @@ def run(cfg, impl, steps, warmup):
     else:
         lstm = ref
     net = Net(lstm, H, O).to(dev)
+    # miopen_bf16: the whole model in bf16 on MIOpen — the like-for-like precision comparison for
+    # the fused kernel's bf16 GEMM operands (miopen = fp32, the reference's numerics)
+    xdt = torch.bfloat16 if impl == "miopen_bf16" else torch.float32
+    if impl == "miopen_bf16":
+        net = net.to(torch.bfloat16)
     graph = impl.endswith("graph")
     opt = torch.optim.Adam(net.parameters(), lr=2e-3, capturable=graph)
-    x = torch.randn(B, T, I, device=dev)
+    x = torch.randn(B, T, I, device=dev, dtype=xdt)
     y = torch.randint(0, O, (B,), device=dev)
     lossf = torch.nn.CrossEntropyLoss()
     losses = []
@@ -107,7 +112,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--configs", default="all")
-    ap.add_argument("--impls", default="fused,fused_graph,miopen")
+    ap.add_argument("--impls", default="fused,fused_graph,miopen,miopen_bf16")
     args = ap.parse_args()
     names = None if args.configs == "all" else set(args.configs.split(","))
     for cfg in CONFIGS:
@@ -117,12 +122,14 @@ def main():
         for impl in args.impls.split(","):
             res[impl] = run(cfg, impl, args.steps, args.warmup)
             print(json.dumps(res[impl]), flush=True)
-        if "miopen" in res:
+        for base in ("miopen", "miopen_bf16"):      # fp32 (reference numerics) and like-for-like bf16
+            if base not in res:
+                continue
             for impl in res:
-                if impl != "miopen":
-                    print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"], "impl": impl,
-                                      "train_x": res["miopen"]["train_ms"] / res[impl]["train_ms"],
-                                      "infer_x": res["miopen"]["infer_ms"] / res[impl]["infer_ms"]}), flush=True)
+                if impl.startswith("fused"):
+                    print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"], "impl": impl, "vs": base,
+                                      "train_x": res[base]["train_ms"] / res[impl]["train_ms"],
+                                      "infer_x": res[base]["infer_ms"] / res[impl]["infer_ms"]}), flush=True)
 
 
 if __name__ == "__main__":
