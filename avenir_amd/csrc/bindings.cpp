@@ -467,7 +467,7 @@ void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels
 void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& node,
                          const at::Tensor& g, const at::Tensor& h, const at::Tensor& bins,
                          const at::Tensor& offs, int64_t total_bins, int64_t n_nodes, at::Tensor& out,
-                         bool even_only) {
+                         bool even_only, int64_t tot_slot, double scale) {
   check_codes(codes, n);
   CHECK_DEV(node);
   CHECK_DTYPE(node, at::kInt);
@@ -482,11 +482,14 @@ void node_grad_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& n
   CHECK_DEV(out);
   CHECK_DTYPE(out, at::kLong);
   TORCH_CHECK(out.numel() == n_nodes * total_bins * 2, "out must be [A, TB, 2]");
+  TORCH_CHECK(tot_slot >= -1 && tot_slot < total_bins, "tot_slot out of range");
+  TORCH_CHECK(scale > 0 && scale <= 65536.0, "scale must be in (0, 2^16]");
   DevGuard gd(codes.device());
   avk::node_grad_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, node.data_ptr<int>(),
                            g.data_ptr<float>(), h.data_ptr<float>(), bins.data_ptr<int>(),
                            offs.data_ptr<int>(), (int)codes.size(0), (int)total_bins, (int)n_nodes,
-                           even_only ? 1 : 0, reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(codes));
+                           even_only ? 1 : 0, (int)tot_slot, (float)scale,
+                           reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(codes));
 }
 
 // K25 re-sampling (resample.hip)
@@ -1215,7 +1218,7 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
 
 void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& ok, at::Tensor& alpha,
                         const at::Tensor& G, const at::Tensor& y, const at::Tensor& gap, double C, double eps,
-                        int64_t max_iter, at::Tensor& dA, at::Tensor& inner_total) {
+                        int64_t max_iter, at::Tensor& dA, at::Tensor& inner_total, double rel_tol) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&K, &alpha, &G, &y, &gap, &dA}) {
     CHECK_DEV((*t));
     CHECK_DTYPE((*t), at::kFloat);
@@ -1241,7 +1244,7 @@ void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Ten
                           ok.data_ptr<bool>(), alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(),
                           (int)alpha.size(1), gap.data_ptr<float>(), (int)B, (float)C, (float)eps, (int)max_iter,
                           dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
-                          Kws.data_ptr<float>(), cur_stream(y));
+                          Kws.data_ptr<float>(), (float)rel_tol, cur_stream(y));
 }
 
 void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& dA, const at::Tensor& ok,
@@ -2000,7 +2003,12 @@ static int64_t loo_slots(const at::Tensor& codes, int64_t slots) {
   }
   TORCH_CHECK(codes.scalar_type() == at::kUInt16 || codes.scalar_type() == at::kByte,
               "codes must be uint8, uint16 or int32");
-  return codes.scalar_type() == at::kUInt16 ? 65536 : 256;
+  if (codes.scalar_type() == at::kUInt16) {
+    // uint16: the table may be cut to the used values (codes >= slots - 1 land in the last slot)
+    TORCH_CHECK(slots <= 0 || (slots >= 2 && slots <= 65536), "uint16 codes: slots in [2, 65536]");
+    return slots > 0 ? slots : 65536;
+  }
+  return 256;
 }
 
 py::tuple loo_stats(const at::Tensor& codes, int64_t n, const at::Tensor& y, int64_t slots) {
@@ -2582,7 +2590,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("node_histogram", &node_histogram);
   m.def("node_grad_histogram", &node_grad_histogram, py::arg("codes"), py::arg("n"), py::arg("node"), py::arg("g"),
         py::arg("h"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_nodes"), py::arg("out"),
-        py::arg("even_only") = false);
+        py::arg("even_only") = false, py::arg("tot_slot") = -1, py::arg("scale") = 65536.0);
   m.def("gbt_grad", &gbt_grad);
   m.def("gbt_split", &gbt_split);
   m.def("resample_uniform", &resample_uniform);
@@ -2607,7 +2615,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_ws_solve", &smo_ws_solve);
   m.def("smo_ws_select", &smo_ws_select);
   m.def("smo_ws_update", &smo_ws_update);
-  m.def("smo_ws_solve_fused", &smo_ws_solve_fused);
+  m.def("smo_ws_solve_fused", &smo_ws_solve_fused, py::arg("K"), py::arg("ws"), py::arg("ok"), py::arg("alpha"),
+        py::arg("G"), py::arg("y"), py::arg("gap"), py::arg("C"), py::arg("eps"), py::arg("max_iter"), py::arg("dA"),
+        py::arg("inner_total"), py::arg("rel_tol") = 0.1);
   m.def("smo_ws_size", &avk::smo_ws_size);
   m.def("nb_finalize", &nb_finalize);
   m.def("weighted_gram", &weighted_gram);

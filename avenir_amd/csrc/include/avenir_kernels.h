@@ -55,7 +55,7 @@ void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8
                     hipStream_t stream);
 void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const int* node,
                          const float* g, const float* h, const int* bins, const int* offs, int nfeat,
-                         int total_bins, int n_nodes, int even_only, long long* out, hipStream_t stream);
+                         int total_bins, int n_nodes, int even_only, int tot_slot, float scale, long long* out, hipStream_t stream);
 void tree_assign(const uint8_t* codes, long long ld, long long n, int* node, const int* split_feat,
                  const short* segmap, int max_bins, const int* child_of, int max_seg,
                  hipStream_t stream);
@@ -125,7 +125,7 @@ void smo_ws_update(const float* K, const long long* ws, const float* dA, const b
                    int B, int N, int ldag, int Q, hipStream_t stream);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
-                        long long* inner_total, float* Kws, hipStream_t stream);
+                        long long* inner_total, float* Kws, float rel_tol, hipStream_t stream);
 int smo_ws_size();
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream);

@@ -157,6 +157,46 @@ __global__ __launch_bounds__(LOO_THREADS) void loo_stats_kernel(const CT* __rest
   }
 }
 
+// Wide codes (uint16 / int32) whose per-column table fits LDS (m slots x (fp64 sum + u32 count)
+// <= 144 KiB, i.e. up to ~12 k values): 1024-thread blocks privatise the column's table in LDS
+// (native ds_add_f64), then flush only the touched slots with global atomics — one atomic pair
+// per (block, value) instead of per row.
+constexpr int LOO_WIDE_T = 1024;
+constexpr size_t LOO_WIDE_LDS = 144 * 1024;
+
+template <typename CT>
+__global__ __launch_bounds__(LOO_WIDE_T) void loo_stats_lds_kernel(const CT* __restrict__ codes, long long ld,
+                                                                   long long n, const double* __restrict__ y,
+                                                                   double* __restrict__ sum,
+                                                                   unsigned* __restrict__ cnt, int m) {
+  extern __shared__ double s_dyn[];
+  double* s_sum = s_dyn;
+  unsigned* s_cnt = reinterpret_cast<unsigned*>(s_dyn + m);
+  const int f = blockIdx.y;
+  const CT* col = codes + (long long)f * ld;
+  for (int i = threadIdx.x; i < m; i += LOO_WIDE_T) {
+    s_sum[i] = 0.0;
+    s_cnt[i] = 0u;
+  }
+  __syncthreads();
+  const unsigned top = (unsigned)(m - 1);
+  const long long stride = (long long)gridDim.x * LOO_WIDE_T;
+  for (long long i = (long long)blockIdx.x * LOO_WIDE_T + threadIdx.x; i < n; i += stride) {
+    const unsigned v = (unsigned)col[i];
+    const unsigned c = v < top ? v : top;
+    atomicAdd(&s_sum[c], y[i]);
+    atomicAdd(&s_cnt[c], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += LOO_WIDE_T) {
+    const unsigned k = s_cnt[i];
+    if (k) {
+      atomicAdd(&sum[(long long)f * m + i], s_sum[i]);
+      atomicAdd(&cnt[(long long)f * m + i], k);
+    }
+  }
+}
+
 constexpr int LOO_TILE_F = 32;  // columns per tile -> [32][256] u32 = 32 KB of LDS
 
 template <typename CT>
@@ -232,6 +272,29 @@ static int loo_blocks(long long n, int F) {
 
 void loo_stats(const void* codes, int code_bytes, int m, long long ld, long long n, int F, const double* y, double* sum,
                unsigned* cnt, hipStream_t stream) {
+  const size_t wide_lds = (size_t)m * (sizeof(double) + sizeof(unsigned));
+  if (code_bytes >= 2 && wide_lds <= LOO_WIDE_LDS) {
+    static bool attr = false;
+    if (!attr) {
+      AV_HIP_CHECK(hipFuncSetAttribute((const void*)loo_stats_lds_kernel<int>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LOO_WIDE_LDS));
+      AV_HIP_CHECK(hipFuncSetAttribute((const void*)loo_stats_lds_kernel<unsigned short>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LOO_WIDE_LDS));
+      attr = true;
+    }
+    // >= 16 rows per thread so the table zero + flush is amortised; <= 256 blocks per column
+    long long gx = n / (LOO_WIDE_T * 16);
+    gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+    const dim3 wgrid((unsigned)gx, F);
+    if (code_bytes == 4)
+      loo_stats_lds_kernel<int><<<wgrid, LOO_WIDE_T, wide_lds, stream>>>(static_cast<const int*>(codes), ld, n, y, sum,
+                                                                        cnt, m);
+    else
+      loo_stats_lds_kernel<unsigned short><<<wgrid, LOO_WIDE_T, wide_lds, stream>>>(
+          static_cast<const unsigned short*>(codes), ld, n, y, sum, cnt, m);
+    AV_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const dim3 grid(loo_blocks(n, F), F);
   if (code_bytes == 4)
     loo_stats_kernel<int><<<grid, LOO_THREADS, 0, stream>>>(static_cast<const int*>(codes), ld, n, y, sum, cnt, m);

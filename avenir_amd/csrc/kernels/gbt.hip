@@ -64,9 +64,17 @@ __global__ __launch_bounds__(GT) void gbt_grad_kernel(const float* __restrict__ 
     acc += (double)lr_loss;
   }
   if (loss) {
-    // per-wave sum, one atomic per wave (the loss is a report, not part of the model)
+    // block sum, ONE atomic per block (the loss is a report, not part of the model; one atomic per
+    // wave serialised ~260 k same-address atomics at 16.7 M rows)
+    __shared__ double red[GT / 64];
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (av::lane_id() == 0) atomicAdd(loss, acc);
+    if (av::lane_id() == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int w = 0; w < GT / 64; ++w) s += red[w];
+      atomicAdd(loss, s);
+    }
   }
 }
 
@@ -109,7 +117,8 @@ __global__ __launch_bounds__(GT) void gbt_assign_kernel(const uint8_t* __restric
 //     argmax with ties to the lowest position;
 //   * the node's feature / threshold and its two children's Newton values into the heap.
 // Positions p < nb are the features' bins in histogram order (pstart / pend: the feature's first
-// and last bin, pvalid: p < pend); bin `tot` is the node total (the all-rows extra feature).
+// and last bin, pvalid: p < pend); slot `tot` holds the rows whose feature-0 code is missing, so
+// feature 0's bins + `tot` are the node total (node_grad_hist_kernel tot_slot).
 constexpr int GS_T = 256;
 
 __global__ __launch_bounds__(GS_T) void gbt_split_kernel(const long long* __restrict__ hist,
@@ -154,7 +163,9 @@ __global__ __launch_bounds__(GS_T) void gbt_split_kernel(const long long* __rest
     }
   }
   __syncthreads();
-  const double G = (double)sh[2 * tot] * invS, H = (double)sh[2 * tot + 1] * invS;
+  // node total = feature 0's bins (positions 0..pend[0]) + the slot of rows missing feature 0
+  const int e0 = min(max(pend[0], 0), nb - 1);
+  const double G = (double)(cs[2 * e0] + sh[2 * tot]) * invS, H = (double)(cs[2 * e0 + 1] + sh[2 * tot + 1]) * invS;
   const double par = G * G / fmax(H + l2, 1e-12);
   double best = -INFINITY;
   int bpos = 0x7fffffff;

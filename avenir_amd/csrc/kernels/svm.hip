@@ -171,6 +171,33 @@ __global__ __launch_bounds__(SMO_THREADS) void smo_kernel(const float* __restric
 //   tolerance is max(eps, 0.1 gap)).
 constexpr int WS_Q = 128;
 
+// (value, index) argmax with ties to the lowest index AND a plain max of a second value, in one
+// DPP pass: the three chains are independent, so their DPP moves issue back to back.
+__device__ __forceinline__ void wave_argmax_and_max(float& v, int& idx, float& m) {
+#define AV_ARGMAX_MAX_STEP(CTRL)                                \
+  {                                                             \
+    const float v2 = av::dpp_f<CTRL>(v), m2 = av::dpp_f<CTRL>(m); \
+    const int i2 = av::dpp_i<CTRL>(idx);                        \
+    av::wave_arg_step<true>(v, idx, v2, i2);                    \
+    m = fmaxf(m, m2);                                           \
+  }
+  AV_ARGMAX_MAX_STEP(0xB1)
+  AV_ARGMAX_MAX_STEP(0x4E)
+  AV_ARGMAX_MAX_STEP(0x124)
+  AV_ARGMAX_MAX_STEP(0x128)
+#undef AV_ARGMAX_MAX_STEP
+  float r = av::lane_f(v, 0), rm = av::lane_f(m, 0);
+  int ri = __builtin_amdgcn_readlane(idx, 0);
+#pragma unroll
+  for (int l = 16; l < 64; l += 16) {
+    av::wave_arg_step<true>(r, ri, av::lane_f(v, l), __builtin_amdgcn_readlane(idx, l));
+    rm = fmaxf(rm, av::lane_f(m, l));
+  }
+  v = r;
+  idx = ri;
+  m = rm;
+}
+
 // The SMO iterations of one Q-variable sub-problem, run by ONE wavefront: lane l owns variables
 // l + 64e; the Q x Q kernel block is in LDS.  Returns the iteration count.
 template <int E>
@@ -209,12 +236,13 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       if (bd > 0.f) {
         float q = Kii + qd[e] - 2.f * Ks[i][t];
         q = q > 0.f ? q : TAU;
-        const float gain = bd * bd / q;
+        // selection only: the hardware reciprocal (one instruction) instead of an IEEE divide;
+        // the two-variable update below keeps exact division
+        const float gain = bd * bd * __builtin_amdgcn_rcpf(q);
         if (gain > best) { best = gain; bj = t; }
       }
     }
-    gmax2 = av::wave_max(gmax2);
-    av::wave_argmax(best, bj);
+    wave_argmax_and_max(best, bj, gmax2);
     if (gmax + gmax2 < epsl || bj == NONE) break;
     const int j = bj;
     // fetch the pair's state from its owner lanes (slot index is wave-uniform)
@@ -368,20 +396,23 @@ __global__ __launch_bounds__(WS_Q) void smo_ws_gather_kernel(const float* __rest
 
 // smo_ws_solve_kernel: one wavefront per problem: the gathered Q x Q block into LDS (coalesced
 // 16-byte loads), then the sub-problem solve, the alpha scatter, dA and the iteration count.
-__global__ __launch_bounds__(64) void smo_ws_solve_kernel(const float* __restrict__ Kws,
+constexpr int WSS_T = 256;  // 4 waves stage the K block, wave 0 solves
+__global__ __launch_bounds__(WSS_T) void smo_ws_solve_kernel(const float* __restrict__ Kws,
                                                           const long long* __restrict__ ws,
                                                           const bool* __restrict__ ok, float* __restrict__ alpha,
                                                           const float* __restrict__ G, const float* __restrict__ yv,
                                                           int N, int ldag, const float* __restrict__ gap, float C,
-                                                          float eps, int max_iter, float* __restrict__ dA,
-                                                          long long* __restrict__ inner_total) {
+                                                          float eps, float rel_tol, int max_iter,
+                                                          float* __restrict__ dA, long long* __restrict__ inner_total) {
   constexpr int Q = WS_Q, E = Q / 64;
   __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
   const int b = blockIdx.x, lane = threadIdx.x;
   const float4* src = reinterpret_cast<const float4*>(Kws + (long long)b * Q * Q);
   float4* dst = reinterpret_cast<float4*>(&Ks[0][0]);
-#pragma unroll 8
-  for (int e = lane; e < Q * Q / 4; e += 64) dst[e] = src[e];
+#pragma unroll 4
+  for (int e = threadIdx.x; e < Q * Q / 4; e += WSS_T) dst[e] = src[e];
+  __syncthreads();
+  if (threadIdx.x >= 64) return;  // wave 0 solves; no barrier follows
   float y[E], a[E], g[E], qd[E], a0[E];
   bool okv[E];
   long long wsv[E];
@@ -395,13 +426,11 @@ __global__ __launch_bounds__(64) void smo_ws_solve_kernel(const float* __restric
     g[e] = G[(long long)b * ldag + wsv[e]];
     a0[e] = a[e];
   }
-  __builtin_amdgcn_s_waitcnt(0);  // wave-private LDS block: own writes visible to own lanes
-  __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int e = 0; e < E; ++e) qd[e] = Ks[lane + 64 * e][lane + 64 * e];
   float gp = gap[b];
   if (!isfinite(gp)) gp = 0.f;
-  const int it = ws_smo_loop<E>(Ks, y, a, g, qd, C, fmaxf(eps, 0.1f * gp), max_iter, lane);
+  const int it = ws_smo_loop<E>(Ks, y, a, g, qd, C, fmaxf(eps, rel_tol * gp), max_iter, lane);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int t = lane + 64 * e;
@@ -477,6 +506,7 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   __shared__ unsigned redu[17];
   __shared__ unsigned s_prefix, s_mask, s_krem, s_gt;
   __shared__ int pick[2][64];
+  __shared__ unsigned wcnt[PER > 0 ? PER : 1][SEL_T / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float* ab = alpha + (long long)b * ldag;
   const float* gb = G + (long long)b * ldag;
@@ -595,7 +625,42 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
     unsigned eq_base = 0;  // ties seen in earlier SEL_T blocks (block-uniform)
     const int lane = tid & 63, wv = tid >> 6;
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int n0 = 0, i = 0; n0 < N; n0 += SEL_T, ++i) {
+    if constexpr (PER > 0) {
+      // register-cached rows: all PER chunks' tie ballots at once, ONE barrier for the per-(chunk,
+      // wave) counts, then every tie ranks itself (index order = chunk-major, then thread)
+      unsigned long long bal[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int n = i * SEL_T + tid;
+        bool eq = false;
+        if (n < N) {
+          const float v = viol(which, i, n);
+          if (v > -INFINITY) {
+            const unsigned key = order_key(v);
+            if (key > T) pick[which][atomicAdd(&s_gt, 1u)] = n;
+            eq = key == T;
+          }
+        }
+        bal[i] = __ballot(eq);
+        if (lane == 0) wcnt[i][wv] = (unsigned)__popcll(bal[i]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        unsigned before = eq_base, tot = 0;
+        for (int w = 0; w < SEL_T / 64; ++w) {
+          const unsigned c = wcnt[i][w];
+          if (w < wv) before += c;
+          tot += c;
+        }
+        if ((bal[i] >> lane) & 1ull) {
+          const unsigned r = before + (unsigned)__popcll(bal[i] & below);
+          if (r < krem) pick[which][ngt + r] = i * SEL_T + tid;
+        }
+        eq_base += tot;
+      }
+    }
+    for (int n0 = 0, i = 0; PER == 0 && n0 < N; n0 += SEL_T, ++i) {
       const int n = n0 + tid;
       bool eq = false;
       if (n < N) {
@@ -734,13 +799,13 @@ void smo_ws_update(const float* K, const long long* ws, const float* dA, const b
 
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
-                        long long* inner_total, float* Kws, hipStream_t stream) {
+                        long long* inner_total, float* Kws, float rel_tol, hipStream_t stream) {
   if (B <= 0) return;
   if (Kws) {  // spread gather (Q x B workgroups) + one-wave solve
     smo_ws_gather_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(K, N, ws, ok, Kws);
     AV_HIP_CHECK(hipGetLastError());
-    smo_ws_solve_kernel<<<B, 64, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, max_iter, dA,
-                                              inner_total);
+    smo_ws_solve_kernel<<<B, WSS_T, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, rel_tol, max_iter,
+                                                 dA, inner_total);
   } else {
     smo_ws_solve_fused_kernel<<<B, SOLVE_T, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
                                                          inner_total);

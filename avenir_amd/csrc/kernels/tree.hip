@@ -79,22 +79,29 @@ __global__ __launch_bounds__(TB_THREADS) void node_hist_kernel(
   }
 }
 
-// Gradient-boosting histogram: per (node, bin) exact fixed-point sums of g and h (scale 2^24),
-// accumulated as int64 in LDS (ds_add_u64 is exact and order-independent).  out: [A][TB][2].
+// Gradient-boosting histogram: per (node, bin) exact fixed-point sums of g and h (scale S = 2^16 per
+// row, round to nearest; inputs |g| <= 1, 0 <= h <= 1 — deviance gradients / hessians).  ONE 64-bit LDS atomic per (row, feature): the slot holds
+// (h_q << 32) + g_q (g_q sign-extended), whose wrapping 64-bit sum is (sum h_q << 32) + sum g_q as
+// long as |sum g_q| < 2^31 — guaranteed because a block scans at most 2^14 rows (the host sizes
+// the grid) and |g_q| <= 2^16; sum h_q < 2^32 likewise (h <= 1/4).  The flush splits the two sums
+// and adds them to the int64 output [A][TB][2] (exact, order-independent).
+// tot_slot >= 0: rows whose feature-0 code is missing (>= bins[0]) go to that slot, so feature 0's
+// bins + tot_slot hold the node total (no separate all-rows feature).
+constexpr long long GH_MAX_ROWS_PER_BLOCK = 1LL << 14;
+
 __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, long long n, const int* __restrict__ node,
     const float* __restrict__ g, const float* __restrict__ h, const int* __restrict__ bins,
     const int* __restrict__ offs, int nfeat, int total_bins, int nodes_per_chunk, int n_nodes, int even_only,
-    long long* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) long long s_g[];
+    int tot_slot, float S, long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_p[];
   const int a0 = blockIdx.y * nodes_per_chunk;
   const int na = min(nodes_per_chunk, n_nodes - a0);
-  const int per_node = total_bins * 2;
-  for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) s_g[i] = 0;
+  const int per_node = total_bins;
+  for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) s_p[i] = 0ull;
   __syncthreads();
   const long long nq = (n + 3) >> 2;
   const long long stride = (long long)gridDim.x * TB_THREADS;
-  const float S = 16777216.0f;
   for (long long q = (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < nq; q += stride) {
     const long long r0 = q * 4;
     const int4 nd4 = *reinterpret_cast<const int4*>(node + r0);
@@ -112,10 +119,13 @@ __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
     if (!any) continue;
     const float4 g4 = *reinterpret_cast<const float4*>(g + r0);
     const float4 h4 = *reinterpret_cast<const float4*>(h + r0);
-    const long long gi[4] = {__float2ll_rn(g4.x * S), __float2ll_rn(g4.y * S), __float2ll_rn(g4.z * S),
-                             __float2ll_rn(g4.w * S)};
-    const long long hi[4] = {__float2ll_rn(h4.x * S), __float2ll_rn(h4.y * S), __float2ll_rn(h4.z * S),
-                             __float2ll_rn(h4.w * S)};
+    const float gv[4] = {g4.x, g4.y, g4.z, g4.w}, hv[4] = {h4.x, h4.y, h4.z, h4.w};
+    unsigned long long pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long gq = __float2ll_rn(gv[j] * S), hq = __float2ll_rn(hv[j] * S);
+      pk[j] = ((unsigned long long)hq << 32) + (unsigned long long)gq;
+    }
     for (int f0 = 0; f0 < nfeat; f0 += FCH) {
       uchar4 v4[FCH];
 #pragma unroll
@@ -126,20 +136,26 @@ __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
         if (f0 + k >= nfeat) break;
         const unsigned B = (unsigned)bins[f0 + k], o = (unsigned)offs[f0 + k];
         const unsigned v[4] = {v4[k].x, v4[k].y, v4[k].z, v4[k].w};
+        const bool tot_here = f0 + k == 0 && tot_slot >= 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (a[j] >= 0 && v[j] < B) {
-            long long* base = s_g + a[j] * per_node + 2 * (o + v[j]);
-            atomicAdd((unsigned long long*)&base[0], (unsigned long long)gi[j]);
-            atomicAdd((unsigned long long*)&base[1], (unsigned long long)hi[j]);
-          }
+        for (int j = 0; j < 4; ++j) {
+          if (a[j] < 0) continue;
+          const int slot = v[j] < B ? (int)(o + v[j]) : (tot_here ? tot_slot : -1);
+          if (slot >= 0) atomicAdd(&s_p[a[j] * per_node + slot], pk[j]);
+        }
       }
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) {
-    const long long v = s_g[i];
-    if (v) atomicAdd((unsigned long long*)&out[(long long)a0 * per_node + i], (unsigned long long)v);
+    const unsigned long long v = s_p[i];
+    if (v) {
+      const long long gs = (long long)(int)(unsigned)(v & 0xFFFFFFFFull);
+      const long long hs = (long long)((v - (unsigned long long)gs) >> 32);
+      long long* o = out + ((long long)a0 * per_node + i) * 2;
+      if (gs) atomicAdd((unsigned long long*)&o[0], (unsigned long long)gs);
+      if (hs) atomicAdd((unsigned long long*)&o[1], (unsigned long long)hs);
+    }
   }
 }
 
@@ -287,16 +303,23 @@ void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8
 
 void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const int* node,
                          const float* g, const float* h, const int* bins, const int* offs, int nfeat,
-                         int total_bins, int n_nodes, int even_only, long long* out, hipStream_t stream) {
+                         int total_bins, int n_nodes, int even_only, int tot_slot, float scale, long long* out,
+                         hipStream_t stream) {
   if (n <= 0 || n_nodes <= 0) return;
-  const long long per_node_bytes = 16LL * total_bins;
+  if (scale > 65536.0f) throw std::runtime_error("node_grad_histogram: scale must be <= 2^16 (packed sums)");
+  const long long per_node_bytes = 8LL * total_bins;
   if (per_node_bytes > 64 * 1024) throw std::runtime_error("node_grad_histogram: table exceeds LDS");
   const int npc = (int)std::max<long long>(1, std::min<long long>(n_nodes, tree_lds_budget() / per_node_bytes));
   const int chunks = (n_nodes + npc - 1) / npc;
-  const int gx = std::max(1, std::min(av::stream_grid((n + 3) / 4, TB_THREADS, 2, 2048), std::max(64, 4096 / chunks)));
-  dim3 grid(gx, chunks);
+  long long gx = std::max(1, std::min(av::stream_grid((n + 3) / 4, TB_THREADS, 2, 2048), std::max(64, 4096 / chunks)));
+  // packed 32-bit partial sums: at most GH_MAX_ROWS_PER_BLOCK rows scanned per block
+  const long long quads_per_block = GH_MAX_ROWS_PER_BLOCK / 4;
+  const long long min_gx = ((n + 3) / 4 + quads_per_block - 1) / quads_per_block;
+  gx = std::max(gx, min_gx);
+  if (gx > 0x7fffffffLL) throw std::runtime_error("node_grad_histogram: too many rows");
+  dim3 grid((unsigned)gx, chunks);
   node_grad_hist_kernel<<<grid, TB_THREADS, per_node_bytes * npc, stream>>>(
-      codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, even_only, out);
+      codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, even_only, tot_slot, scale, out);
   AV_HIP_CHECK(hipGetLastError());
 }
 

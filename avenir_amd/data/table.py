@@ -58,9 +58,9 @@ _CODE_DTYPE = (torch.uint8, torch.uint16, torch.int32)
 
 def code_slots(codes: torch.Tensor, bins) -> int:
     """Per-column table size for code-indexed lookups: every valid code plus one missing slot."""
-    if codes.dtype == torch.int32:
+    if codes.dtype in (torch.int32, torch.uint16):
         return max([int(b) for b in bins] + [1]) + 1
-    return 65536 if codes.dtype == torch.uint16 else 256
+    return 256
 
 
 _ESCAPED_LITERALS = {r"\t": "\t", r"\|": "|", r"\.": ".", r"\\": "\\", r"\$": "$", r"\^": "^"}

@@ -130,8 +130,9 @@ class _WorkingSetSMO:
     """State and one outer step of the working-set solver, written with static shapes so that a
     block of steps can be captured as one HIP graph (see ``smo_decomposition``)."""
 
-    def __init__(self, K, y, C, eps, inner_iter, Q, fused=True):
+    def __init__(self, K, y, C, eps, inner_iter, Q, fused=True, rel_tol=0.1):
         self.K, self.C, self.eps, self.inner_iter = K, float(C), float(eps), int(inner_iter)
+        self.rel_tol = float(rel_tol)
         B, N = y.shape
         dev = K.device
         self.gpu = dev.type == "cuda"
@@ -167,7 +168,7 @@ class _WorkingSetSMO:
             C_ = _native.C()
             C_.smo_ws_select(self.alpha, self.G, self.yf, self.C, Q // 2, self.ws_buf, self.ok_buf, self.gap)
             C_.smo_ws_solve_fused(self.K, self.ws_buf, self.ok_buf, self.alpha, self.G, self.yf, self.gap, self.C,
-                                  self.eps, self.inner_iter, self.dA_buf, self.inner_total)
+                                  self.eps, self.inner_iter, self.dA_buf, self.inner_total, self.rel_tol)
             C_.smo_ws_update(self.K, self.ws_buf, self.dA_buf, self.ok_buf, self.yf, self.G)
             return
         vu, vl = self.refresh_gap()
@@ -210,7 +211,7 @@ class _WorkingSetSMO:
 
 def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_outer: int = 100_000,
                       inner_iter: int = 2048, check_every: int = 16, Q: int | None = None, graph: bool = True,
-                      fused: bool = True):
+                      fused: bool = True, rel_tol: float | None = None):
     """Working-set SMO for B problems (K [B, N, N], y [B, N] in {-1, 0, +1}).
 
     Each outer step picks the Q/2 largest violators of the "up" set and the Q/2 largest of the
@@ -225,7 +226,10 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     torch ops.  Returns (alpha, G, outer steps, inner steps).
     """
     Q = Q or (_native.C().smo_ws_size() if K.device.type == "cuda" else 128)
-    st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused)
+    if rel_tol is None:   # sub-problem tolerance max(eps, rel_tol * gap) of the fused GPU solver
+        import os
+        rel_tol = float(os.environ.get("AVMI_SMO_REL_TOL", "0.1"))
+    st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused, rel_tol)
     outer = 0
     if st.gpu and graph:
         st.step()                                # eager warm-up: allocator pool, kernel caches
@@ -239,9 +243,10 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
                     st.step()
                 st.refresh_gap()
         torch.cuda.current_stream().wait_stream(s)
-        # capture records without executing: replay the block until converged
+        # capture records without executing: replay the block until converged (the captured block
+        # ends with refresh_gap, so the gap read after a replay is current)
+        st.refresh_gap()
         while outer < max_outer:
-            st.refresh_gap()
             if bool((~(st.gap >= eps)).all()):
                 break
             g.replay()

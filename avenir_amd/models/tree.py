@@ -1137,7 +1137,7 @@ class GradientBoostedTrees:
 
         def grad_hist(A, even):
             hh = T.node_grad_histogram(codes, n, node, g, h, bins, A, even_only=even, bins_d=st["bins_d"],
-                                       offs_d=st["offs_d"])
+                                       offs_d=st["offs_d"], tot_slot=tb_tot)
             if comm.is_distributed:
                 comm.all_reduce(hh)
             return hh
@@ -1150,7 +1150,8 @@ class GradientBoostedTrees:
         for lvl in range(D):
             A = 1 << lvl
             hb, hc = A - 1, 2 * A - 1
-            tot = hist[:, tb_tot, :]
+            # node total: feature 0's bins + the slot of rows missing feature 0 (tot_slot)
+            tot = hist[:, : bins[0], :].sum(1) + hist[:, tb_tot, :]
             G, H = tot[:, 0], tot[:, 1]
             if lvl == 0:
                 val[0:1] = -G / (H + p.l2).clamp_min(1e-12)
@@ -1189,7 +1190,7 @@ class GradientBoostedTrees:
     @staticmethod
     def _grad_hist_raw(st, comm, g, h, A, even):
         hh = T.node_grad_histogram(st["codes"], st["n"], st["node"], g, h, st["bins"], A, even_only=even,
-                                   bins_d=st["bins_d"], offs_d=st["offs_d"], raw=True)
+                                   bins_d=st["bins_d"], offs_d=st["offs_d"], raw=True, tot_slot=st["offs"][-1])
         if comm.is_distributed:
             comm.all_reduce(hh)               # exact int64 fixed point
         return hh
@@ -1267,7 +1268,8 @@ class GradientBoostedTrees:
         if p.max_depth < 1 or p.max_depth > 16:
             raise ValueError("GBT max_depth must be in 1..16")
         self.space = build_split_space(self.schema, t, binary=True, max_bins=p.max_bins, comm=comm)
-        codes = _with_total_row(encode_for_tree(self.space, t), t.n)
+        codes = encode_for_tree(self.space, t)
+        # + one slot: rows missing feature 0 (feature 0's bins + it = the node total)
         bins = [fs.n_bins for fs in self.space] + [1]
         n, dev = t.n, t.device
         ld = codes.shape[1]
@@ -1297,7 +1299,7 @@ class GradientBoostedTrees:
         self.init = (torch.log(prior[1] / prior[0]).view(1) if K == 1 else torch.log(prior)).float()
         Hn = (2 << p.max_depth) - 1
         R = p.n_estimators
-        missing = bool((codes[:-1, :n] == MISSING).any()) if n else False
+        missing = bool((codes[:, :n] == MISSING).any()) if n else False
         if comm.is_distributed:
             mt = torch.tensor([float(missing)])
             comm.all_reduce(mt, "max")

@@ -75,7 +75,9 @@ def _slots(codes: torch.Tensor, slots: int | None = None) -> int:
         if slots is None:
             raise ValueError("int32 codes need slots = max code + 2 (data.table.code_slots)")
         return int(slots)
-    return 65536 if codes.dtype == torch.uint16 else 256
+    if codes.dtype == torch.uint16:
+        return int(slots) if slots is not None else 65536
+    return 256
 
 
 def _clamped(codes: torch.Tensor, n: int, m: int) -> torch.Tensor:
@@ -85,12 +87,12 @@ def _clamped(codes: torch.Tensor, n: int, m: int) -> torch.Tensor:
 
 def loo_stats(codes: torch.Tensor, n: int, y: torch.Tensor, slots: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """Per (column, code) target sum (double [F, m]) and count (int32 [F, m]) over ``n`` rows of
-    ``codes`` [F, ld] (uint8: m = 256, uint16: m = 65536, int32: m = ``slots``; codes >= m - 1 are
-    counted in slot m - 1)."""
+    ``codes`` [F, ld] (uint8: m = 256, uint16: m = ``slots`` or 65536, int32: m = ``slots``; codes
+    >= m - 1 are counted in slot m - 1)."""
     y = y[:n].double().contiguous()
     m = _slots(codes, slots)
     if codes.is_cuda:
-        return tuple(_native.C().loo_stats(codes.contiguous(), int(n), y, m if codes.dtype == torch.int32 else -1))
+        return tuple(_native.C().loo_stats(codes.contiguous(), int(n), y, m if codes.dtype != torch.uint8 else -1))
     F = codes.shape[0]
     c = _clamped(codes, n, m) + torch.arange(F).view(-1, 1) * m
     s = torch.zeros(F * m, dtype=torch.float64).index_add_(0, c.reshape(-1), y.repeat(F))
@@ -108,7 +110,7 @@ def loo_apply(codes: torch.Tensor, n: int, y: torch.Tensor, s: torch.Tensor, k: 
         nz = noise[:, :n].double().contiguous().to(codes.device) if noise is not None else None
         return _native.C().loo_apply(codes.contiguous(), int(n), y, s.double().contiguous(), k.int().contiguous(),
                                      gm.to(codes.device), float(reg), nz, float(amp),
-                                     int(s.shape[1]) if codes.dtype == torch.int32 else -1)
+                                     int(s.shape[1]) if codes.dtype != torch.uint8 else -1)
     F = codes.shape[0]
     cols = []
     cl = _clamped(codes, n, int(s.shape[1]))

@@ -8,7 +8,9 @@ import torch
 from .. import _native
 from .histogram import _dev_i32
 
-_GRAD_SCALE = float(1 << 24)
+# fixed-point scale of the GBT gradient histograms: 2^-16 per row (node_grad_hist_kernel packs the
+# g and h sums of a block into one 64-bit LDS word)
+_GRAD_SCALE = float(1 << 16)
 
 
 def _offs(bins: Sequence[int]) -> list[int]:
@@ -48,10 +50,12 @@ def node_histogram(codes: torch.Tensor, n: int, labels: torch.Tensor, node: torc
 def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torch.Tensor,
                         h: torch.Tensor, bins: Sequence[int], n_nodes: int, even_only: bool = False,
                         bins_d: torch.Tensor | None = None, offs_d: torch.Tensor | None = None,
-                        raw: bool = False) -> torch.Tensor:
-    """Exact fixed-point (2^-24) sums of gradient and hessian per (node, bin): float64 [A, TB, 2].
-    ``even_only``: only rows of even node ids, counted at id / 2 (the left children of a level, for
-    sibling subtraction).  ``bins_d`` / ``offs_d``: cached device copies of the bin tables."""
+                        raw: bool = False, tot_slot: int = -1) -> torch.Tensor:
+    """Exact fixed-point (2^-16 per row) sums of gradient and hessian per (node, bin): float64
+    [A, TB, 2] (int64 raw sums with ``raw``).  ``even_only``: only rows of even node ids, counted at
+    id / 2 (the left children of a level, for sibling subtraction).  ``tot_slot``: rows whose
+    feature-0 code is missing are counted in that bin (feature 0 + it = the node total).
+    ``bins_d`` / ``offs_d``: cached device copies of the bin tables."""
     bins = [int(b) for b in bins]
     tb = sum(bins)
     if codes.is_cuda:
@@ -61,7 +65,7 @@ def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torc
                                             h.float().contiguous(),
                                             bins_d if bins_d is not None else _dev_i32(bins, codes.device),
                                             offs_d if offs_d is not None else _dev_i32(_offs(bins), codes.device),
-                                            tb, int(n_nodes), out, bool(even_only))
+                                            tb, int(n_nodes), out, bool(even_only), int(tot_slot), _GRAD_SCALE)
         return out if raw else out.double() / _GRAD_SCALE
     out = torch.zeros((n_nodes, tb, 2), dtype=torch.int64)
     nd = node[:n].long()
@@ -71,12 +75,17 @@ def node_grad_histogram(codes: torch.Tensor, n: int, node: torch.Tensor, g: torc
     hi = torch.round(h[:n].float() * _GRAD_SCALE).long()
     ok_r = (nd >= 0) & (nd < n_nodes)
     flat = out.view(-1)
-    for f, (b, o) in enumerate(zip(bins, _offs(bins))):
+    for f, (b, o) in enumerate(zip(bins[: codes.shape[0]], _offs(bins))):
         v = codes[f, :n].long()
         ok = ok_r & (v < b)
         base = (nd[ok] * tb + o + v[ok]) * 2
         flat.index_add_(0, base, gi[ok])
         flat.index_add_(0, base + 1, hi[ok])
+        if f == 0 and tot_slot >= 0:
+            miss = ok_r & (v >= b)
+            base = (nd[miss] * tb + tot_slot) * 2
+            flat.index_add_(0, base, gi[miss])
+            flat.index_add_(0, base + 1, hi[miss])
     return out if raw else out.double() / _GRAD_SCALE
 
 

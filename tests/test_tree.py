@@ -276,11 +276,20 @@ def test_node_histogram_kernels_match_oracle(cuda):
     ref = TO.node_histogram(codes, n, labels, node, weight, bins, 3, A)
     got = TO.node_histogram(codes.to(cuda), n, labels.to(cuda), node.to(cuda), weight.to(cuda), bins, 3, A)
     assert torch.equal(got.cpu(), ref)
-    gr = torch.randn(ld, generator=g)
+    gr = torch.randn(ld, generator=g).clamp(-1, 1)          # GBT gradients: |g| <= 1, 0 <= h <= 1
     hs = torch.rand(ld, generator=g)
     ref = TO.node_grad_histogram(codes, n, node, gr, hs, bins, A)
     got = TO.node_grad_histogram(codes.to(cuda), n, node.to(cuda), gr.to(cuda), hs.to(cuda), bins, A)
     assert torch.equal(got.cpu(), ref)
+    # packed-sum extremes (every row at |g| = 1, h = 1 in one node), the total slot, left children only
+    bt = bins + [1]
+    for gv, even, ts in ((1.0, False, sum(bins)), (-1.0, True, sum(bins)), (0.5, False, -1)):
+        gg, hh = torch.full((ld,), gv), torch.ones(ld)
+        nd = torch.zeros(ld, dtype=torch.int32) if not even else node.abs() % 4
+        ref = TO.node_grad_histogram(codes, n, nd, gg, hh, bt, A, even_only=even, tot_slot=ts)
+        got = TO.node_grad_histogram(codes.to(cuda), n, nd.to(cuda), gg.to(cuda), hh.to(cuda), bt, A,
+                                     even_only=even, tot_slot=ts)
+        assert torch.equal(got.cpu(), ref), (gv, even, ts)
 
 
 # ------------------------------------------------------------------------------------------------
