@@ -480,23 +480,20 @@ class DataExplorer:
         return {"stat": r, "pvalue": float(2 * stats.t.sf(abs(t), n - 2))}
 
     def _rank(self, x):
-        # average ranks for ties
-        o = torch.argsort(x)
-        r = torch.empty_like(x)
-        r[o] = torch.arange(1, x.numel() + 1, dtype=x.dtype, device=x.device)
-        u, inv = torch.unique(x, return_inverse=True)
-        s = torch.zeros(u.numel(), dtype=x.dtype, device=x.device).index_add_(0, inv, r)
-        c = torch.bincount(inv, minlength=u.numel()).to(x.dtype)
-        return (s / c)[inv]
+        """Average ranks over ties (K26 rank_avg kernel on the GPU)."""
+        from ..ops.stats_ops import rank_avg
+        return rank_avg(x)[0]
 
     def getSpearmanRankCorr(self, ds1, ds2, sigLev=0.05):
-        x, y = self.getNumericData(ds1).double(), self.getNumericData(ds2).double()
-        return self.getPearsonCorr(self._rank(x), self._rank(y))
+        from ..ops.stats_ops import spearman
+        rho, p = spearman(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": rho, "pvalue": p}
 
     def getKendalRankCorr(self, ds1, ds2, sigLev=0.05):
-        from scipy import stats
-        r = stats.kendalltau(_np(self.getNumericData(ds1)), _np(self.getNumericData(ds2)))
-        return {"stat": float(r[0]), "pvalue": float(r[1])}
+        """tau-b from exact device pair counts (K26 kendall_pairs) + tie terms of the ranks."""
+        from ..ops.stats_ops import kendall_tau_b
+        tau, p = kendall_tau_b(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": tau, "pvalue": p}
 
     def getPointBiserialCorr(self, ds1, ds2, sigLev=0.05):
         return self.getPearsonCorr(ds1, ds2)
@@ -643,16 +640,19 @@ class DataExplorer:
         return {"stat": d, "pvalue": float(stats.ks_2samp(_np(a), _np(b)).pvalue)}
 
     def testTwoSampleMw(self, ds1, ds2, sigLev=0.05):
-        from scipy import stats
-        return self._two(stats.mannwhitneyu, ds1, ds2)
+        """U from device rank sums of the merged sample (K26 rank_avg), scipy's p-value formula."""
+        from ..ops.stats_ops import mann_whitney_u
+        u, p = mann_whitney_u(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": u, "pvalue": p}
 
     def testTwoSampleWilcox(self, ds1, ds2, sigLev=0.05):
         from scipy import stats
         return self._two(stats.wilcoxon, ds1, ds2)
 
     def testTwoSampleKw(self, ds1, ds2, sigLev=0.05):
-        from scipy import stats
-        return self._two(stats.kruskal, ds1, ds2)
+        from ..ops.stats_ops import kruskal_h
+        h, p = kruskal_h(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": h, "pvalue": p}
 
     def testTwoSampleFriedman(self, ds1, ds2, ds3, sigLev=0.05):
         from scipy import stats

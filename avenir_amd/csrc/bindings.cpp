@@ -640,6 +640,117 @@ void gbt_split(const c10::optional<at::Tensor>& hist, const c10::optional<at::Te
                  thr.data_ptr<int>(), val.data_ptr<double>(), cur_stream(ref));
 }
 
+// K26 rank statistics (stats.hip).  sorted / perm: torch.sort of the sample (ascending);
+// group int32 [n] (original order) or None.  Returns (ranks f64 [n], tie terms f64 [4], group rank
+// sums f64 [n_groups]).
+py::tuple rank_avg(const at::Tensor& sorted, const at::Tensor& perm, const c10::optional<at::Tensor>& group,
+                   int64_t n_groups) {
+  CHECK_DEV(sorted);
+  CHECK_DTYPE(sorted, at::kDouble);
+  CHECK_DEV(perm);
+  CHECK_DTYPE(perm, at::kLong);
+  TORCH_CHECK(sorted.dim() == 1 && sorted.is_contiguous() && perm.sizes() == sorted.sizes() && perm.is_contiguous(),
+              "sorted / perm must be contiguous [n]");
+  const int64_t n = sorted.numel();
+  const int* gp = nullptr;
+  if (group.has_value() && group->defined()) {
+    CHECK_DEV((*group));
+    CHECK_DTYPE((*group), at::kInt);
+    TORCH_CHECK(group->numel() == n && group->is_contiguous(), "group must be [n]");
+    TORCH_CHECK(n_groups >= 1 && n_groups < (1 << 20), "n_groups in [1, 2^20)");
+    gp = group->data_ptr<int>();
+  }
+  auto o = sorted.options();
+  auto ranks = at::empty({n}, o), tie = at::zeros({4}, o), gsum = at::zeros({std::max<int64_t>(n_groups, 1)}, o);
+  DevGuard gd(sorted.device());
+  avk::rank_avg(sorted.data_ptr<double>(), reinterpret_cast<const long long*>(perm.data_ptr<int64_t>()), n, gp,
+                (int)n_groups, ranks.data_ptr<double>(), tie.data_ptr<double>(), gsum.data_ptr<double>(),
+                cur_stream(sorted));
+  return py::make_tuple(ranks, tie, gsum);
+}
+
+// Kendall pair counts of (x, y) f64 [n]: int64 [5] = concordant, discordant, x-only ties, y-only
+// ties, ties in both.
+at::Tensor kendall_pairs(const at::Tensor& x, const at::Tensor& y) {
+  CHECK_DEV(x);
+  CHECK_DTYPE(x, at::kDouble);
+  CHECK_DEV(y);
+  CHECK_DTYPE(y, at::kDouble);
+  TORCH_CHECK(x.dim() == 1 && x.is_contiguous() && y.sizes() == x.sizes() && y.is_contiguous(), "x, y must be [n]");
+  TORCH_CHECK(x.numel() <= (1LL << 24), "kendall_pairs: n <= 2^24");
+  auto out = at::zeros({5}, x.options().dtype(at::kLong));
+  DevGuard gd(x.device());
+  avk::kendall_pairs(x.data_ptr<double>(), y.data_ptr<double>(), x.numel(),
+                     reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(x));
+  return out;
+}
+
+// K28 text kernels (text.hip)
+void tfidf_rows(const at::Tensor& crow, const at::Tensor& col, at::Tensor& val, const at::Tensor& idf, bool sublinear,
+                int64_t norm) {
+  CHECK_DEV(crow); CHECK_DTYPE(crow, at::kLong);
+  CHECK_DEV(col); CHECK_DTYPE(col, at::kLong);
+  CHECK_DEV(val); CHECK_DTYPE(val, at::kFloat);
+  CHECK_DEV(idf); CHECK_DTYPE(idf, at::kFloat);
+  TORCH_CHECK(crow.dim() == 1 && crow.numel() >= 1 && col.numel() == val.numel() && val.is_contiguous() &&
+                  col.is_contiguous() && crow.is_contiguous(), "CSR arrays");
+  TORCH_CHECK(norm >= 0 && norm <= 2, "norm: 0 none, 1 l1, 2 l2");
+  const int64_t nnz = col.numel();
+  if (nnz) {
+    // column ids index idf; row pointers must be monotone within [0, nnz] (one host check per call:
+    // TF-IDF is built once per corpus)
+    TORCH_CHECK(col.min().item<int64_t>() >= 0 && col.max().item<int64_t>() < idf.numel(), "column id out of range");
+  }
+  TORCH_CHECK(crow[0].item<int64_t>() == 0 && crow[-1].item<int64_t>() == nnz, "crow must span [0, nnz]");
+  DevGuard gd(val.device());
+  avk::tfidf_rows(reinterpret_cast<const long long*>(crow.data_ptr<int64_t>()),
+                  reinterpret_cast<const long long*>(col.data_ptr<int64_t>()), val.data_ptr<float>(),
+                  idf.data_ptr<float>(), crow.numel() - 1, sublinear ? 1 : 0, (int)norm, cur_stream(val));
+}
+
+py::tuple pagerank(const at::Tensor& P, double d, int64_t iters, double tol) {
+  CHECK_DEV(P);
+  CHECK_DTYPE(P, at::kDouble);
+  TORCH_CHECK(P.dim() == 2 && P.size(0) == P.size(1) && P.is_contiguous(), "P must be contiguous [n, n]");
+  TORCH_CHECK(P.size(0) <= avk::pagerank_max_n(), "pagerank: n <= ", avk::pagerank_max_n());
+  const int n = (int)P.size(0);
+  auto r = at::empty({n}, P.options());
+  auto it = at::zeros({1}, P.options().dtype(at::kInt));
+  DevGuard gd(P.device());
+  avk::pagerank(P.data_ptr<double>(), n, d, (int)iters, tol, r.data_ptr<double>(), it.data_ptr<int>(), cur_stream(P));
+  return py::make_tuple(r, it);
+}
+
+void sgns_step(at::Tensor& Win, at::Tensor& Wout, const at::Tensor& centre, const at::Tensor& context,
+               const at::Tensor& aprob, const at::Tensor& alias, int64_t neg, double lr, int64_t base, int64_t total,
+               int64_t seed, int64_t step) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Win, &Wout, &aprob}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+    TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
+  }
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&centre, &context, &alias}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kInt);
+    TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
+  }
+  TORCH_CHECK(Win.dim() == 2 && Wout.dim() == 2 && Win.size(1) == Wout.size(1), "Win [Rin, d], Wout [V, d]");
+  const int64_t V = Wout.size(0), dim = Win.size(1);
+  TORCH_CHECK(aprob.numel() == V && alias.numel() == V, "alias table must have V entries");
+  TORCH_CHECK(centre.numel() == context.numel(), "centre / context lengths");
+  TORCH_CHECK(neg >= 0 && neg <= 64, "0 <= neg <= 64");
+  // ids index the tables: bounds checked on the host copies (one check per epoch-sized batch)
+  if (centre.numel()) {
+    TORCH_CHECK(centre.min().item<int>() >= 0 && centre.max().item<int>() < Win.size(0), "centre id out of range");
+    TORCH_CHECK(context.min().item<int>() >= 0 && context.max().item<int>() < V, "context id out of range");
+    TORCH_CHECK(alias.min().item<int>() >= 0 && alias.max().item<int>() < V, "alias id out of range");
+  }
+  DevGuard gd(Win.device());
+  avk::sgns_step(Win.data_ptr<float>(), Wout.data_ptr<float>(), (int)dim, centre.data_ptr<int>(), context.data_ptr<int>(),
+                 centre.numel(), aprob.data_ptr<float>(), alias.data_ptr<int>(), (int)V, (int)neg, (float)lr, base,
+                 std::max<int64_t>(total, 1), (unsigned long long)seed, (unsigned long long)step, cur_stream(Win));
+}
+
 void tree_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::Tensor& split_feat,
                  const at::Tensor& segmap, const at::Tensor& child_of) {
   check_codes(codes, n);
@@ -2593,6 +2704,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("even_only") = false, py::arg("tot_slot") = -1, py::arg("scale") = 65536.0);
   m.def("gbt_grad", &gbt_grad);
   m.def("gbt_split", &gbt_split);
+  m.def("rank_avg", &rank_avg);
+  m.def("tfidf_rows", &tfidf_rows);
+  m.def("pagerank", &pagerank);
+  m.def("sgns_step", &sgns_step);
+  m.def("kendall_pairs", &kendall_pairs);
   m.def("resample_uniform", &resample_uniform);
   m.def("smote", &smote);
   m.def("gbt_assign", &gbt_assign);

@@ -269,4 +269,18 @@ void lstm_bwd(const float* dhseq, const unsigned short* gates, const float* cseq
               const float* dcn, const void* wfragT, int B, int T, int H, int KS, int RT, unsigned short* dz,
               float* dh0, float* dc0, hipStream_t stream);
 
+// stats.hip (K26 rank statistics)
+void rank_avg(const double* sorted, const long long* perm, long long n, const int* group, int n_groups, double* ranks,
+              double* tie, double* gsum, hipStream_t stream);
+void kendall_pairs(const double* x, const double* y, long long n, unsigned long long* out, hipStream_t stream);
+
+// text.hip (K28)
+void tfidf_rows(const long long* crow, const long long* col, float* val, const float* idf, long long n_rows,
+                int sublinear, int norm, hipStream_t stream);
+int pagerank_max_n();
+void pagerank(const double* P, int n, double d, int iters, double tol, double* r, int* it, hipStream_t stream);
+void sgns_step(float* Win, float* Wout, int dim, const int* centre, const int* context, long long n_pairs,
+               const float* aprob, const int* alias, int V, int neg, float lr0, long long base, long long total,
+               unsigned long long seed, unsigned long long step, hipStream_t stream);
+
 }  // namespace avk

@@ -1,0 +1,182 @@
+// K28 text kernels for CDNA4 (gfx950): TF-IDF rows, TextRank power iteration, skip-gram negative
+// sampling.
+//
+// Reference: python/text/preprocess.py:380-524 (TfIdf / term-frequency vectors, host Counters),
+// python/text/summ.py TextRank (networkx pagerank over a sentence-similarity graph) and
+// python/text/wv.py:36-153 (gensim word2vec / doc2vec).
+//   * tfidf_rows_kernel : one wavefront per document row of the CSR count matrix: w = tf * idf[col]
+//     (tf = count or 1 + ln count), then the row's L2 (or L1) norm as a wave reduction and the
+//     normalised weights written in place — one pass instead of densify + 4 tensor ops.
+//   * pagerank_kernel   : the whole power iteration in ONE persistent workgroup: r lives in LDS,
+//     every iteration is a column sweep of the row-stochastic matrix (thread j owns columns
+//     j, j + 1024, ... — consecutive threads read consecutive addresses of a row), and the L1
+//     change is reduced on the device, so there is no host synchronisation per iteration.
+//   * sgns_kernel       : one wavefront per (centre, context) pair: the context and `neg` negatives
+//     drawn on the device (Philox keyed by (seed, step, pair) + an alias table of the unigram^0.75
+//     noise distribution), dot products as wave reductions, the logistic gradients, and the
+//     updates applied Hogwild-style with float atomics (the standard GPU word2vec scheme); d <= 256
+//     (each lane owns d / 64 coordinates).  PV-DBOW (doc2vec) is the same kernel with the document
+//     matrix as the centre table.
+// Index safety: CSR column ids < V (checked by the binding), alias indices < V, pair ids < V / D.
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void tfidf_rows_kernel(const long long* __restrict__ crow,
+                                                         const long long* __restrict__ col, float* __restrict__ val,
+                                                         const float* __restrict__ idf, long long n_rows, int sublinear,
+                                                         int norm) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const long long b = crow[row], e = crow[row + 1];
+  float acc = 0.f;
+  for (long long k = b + lane; k < e; k += 64) {
+    const float tf = sublinear ? log1pf(val[k]) : val[k];
+    const float w = tf * idf[col[k]];
+    val[k] = w;
+    acc += norm == 2 ? w * w : fabsf(w);
+  }
+  if (norm == 0) return;
+  acc = av::wave_sum(acc);
+  const float s = norm == 2 ? sqrtf(acc) : acc;
+  const float inv = 1.f / fmaxf(s, 1e-12f);
+  for (long long k = b + lane; k < e; k += 64) val[k] *= inv;
+}
+
+constexpr int PR_T = 1024;
+constexpr int PR_MAXN = 8192;  // r (fp64) in LDS
+
+__global__ __launch_bounds__(PR_T) void pagerank_kernel(const double* __restrict__ P, int n, double d, int iters,
+                                                        double tol, double* __restrict__ r_out,
+                                                        int* __restrict__ it_out) {
+  __shared__ double r[PR_MAXN];
+  __shared__ double red[PR_T / 64];
+  const int tid = threadIdx.x;
+  for (int j = tid; j < n; j += PR_T) r[j] = 1.0 / n;
+  __syncthreads();
+  constexpr int PER = PR_MAXN / PR_T;
+  double nr[PER];
+  int it = 0;
+  for (; it < iters; ++it) {
+    double diff = 0.0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int j = tid + q * PR_T;
+      nr[q] = 0.0;
+      if (j < n) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += P[(long long)i * n + j] * r[i];
+        nr[q] = (1.0 - d) / n + d * s;
+        diff += fabs(nr[q] - r[j]);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) diff += __shfl_xor(diff, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = diff;
+    __syncthreads();  // every r[i] read of this iteration is done
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int j = tid + q * PR_T;
+      if (j < n) r[j] = nr[q];
+    }
+    double tot = 0.0;
+    for (int w = 0; w < PR_T / 64; ++w) tot += red[w];
+    __syncthreads();  // r updated; red reusable
+    if (tot < tol) { ++it; break; }
+  }
+  for (int j = tid; j < n; j += PR_T) r_out[j] = r[j];
+  if (tid == 0) *it_out = it;
+}
+
+// alias table: prob[V] (float), alias[V] (int); draw: k = u1 * V, take k if u2 < prob[k] else alias[k]
+template <int DV>
+__global__ __launch_bounds__(256) void sgns_kernel(float* __restrict__ Win, float* __restrict__ Wout,
+                                                   const int* __restrict__ centre, const int* __restrict__ context,
+                                                   long long n_pairs, const float* __restrict__ aprob,
+                                                   const int* __restrict__ alias, int V, int neg, float lr0,
+                                                   long long base, long long total, unsigned long long seed,
+                                                   unsigned long long step) {
+  const long long pr = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pr >= n_pairs) return;
+  // word2vec's linear decay over all pairs of all epochs
+  const float lr = lr0 * fmaxf(1e-4f, 1.f - (float)(base + pr) / (float)total);
+  const int lane = threadIdx.x & 63;
+  const int c = centre[pr];
+  float* wc = Win + (long long)c * (DV * 64);
+  float v[DV], grad[DV];
+#pragma unroll
+  for (int k = 0; k < DV; ++k) {
+    v[k] = wc[lane + 64 * k];
+    grad[k] = 0.f;
+  }
+  for (int t = 0; t <= neg; ++t) {
+    int o;
+    float label;
+    if (t == 0) {
+      o = context[pr];
+      label = 1.f;
+    } else {
+      // the same draw on every lane (wave-uniform counter): no broadcast needed
+      const av::u4 rr = av::philox_draw(seed, step, (unsigned long long)(pr * 64 + t));
+      int k = (int)(av::u32_to_unit(rr.x) * (float)V);
+      k = k >= V ? V - 1 : k;
+      o = av::u32_to_unit(rr.y) < aprob[k] ? k : alias[k];
+      label = 0.f;
+    }
+    float* wo = Wout + (long long)o * (DV * 64);
+    float u[DV], dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < DV; ++k) {
+      u[k] = wo[lane + 64 * k];
+      dot += u[k] * v[k];
+    }
+    dot = av::wave_sum(dot);
+    const float sig = 1.f / (1.f + __expf(-dot));
+    const float g = (label - sig) * lr;
+#pragma unroll
+    for (int k = 0; k < DV; ++k) {
+      grad[k] += g * u[k];
+      atomicAdd(&wo[lane + 64 * k], g * v[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < DV; ++k) atomicAdd(&wc[lane + 64 * k], grad[k]);
+}
+
+}  // namespace
+
+namespace avk {
+
+void tfidf_rows(const long long* crow, const long long* col, float* val, const float* idf, long long n_rows,
+                int sublinear, int norm, hipStream_t stream) {
+  if (n_rows <= 0) return;
+  tfidf_rows_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, stream>>>(crow, col, val, idf, n_rows, sublinear, norm);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int pagerank_max_n() { return PR_MAXN; }
+
+void pagerank(const double* P, int n, double d, int iters, double tol, double* r, int* it, hipStream_t stream) {
+  if (n <= 0) return;
+  if (n > PR_MAXN) throw std::runtime_error("pagerank: n exceeds the LDS-resident vector");
+  pagerank_kernel<<<1, PR_T, 0, stream>>>(P, n, d, iters, tol, r, it);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void sgns_step(float* Win, float* Wout, int dim, const int* centre, const int* context, long long n_pairs,
+               const float* aprob, const int* alias, int V, int neg, float lr0, long long base, long long total,
+               unsigned long long seed, unsigned long long step, hipStream_t stream) {
+  if (n_pairs <= 0) return;
+  const unsigned grid = (unsigned)((n_pairs + 3) / 4);
+  switch (dim) {
+    case 64: sgns_kernel<1><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
+    case 128: sgns_kernel<2><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
+    case 192: sgns_kernel<3><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
+    case 256: sgns_kernel<4><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
+    default: throw std::runtime_error("sgns_step: padded dim must be 64, 128, 192 or 256");
+  }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace avk

@@ -263,6 +263,7 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
 
 
 WS_MIN_N = 4096   # above this the working-set solver beats the single-workgroup full SMO (bench_svm.py)
+LAST_SOLVE: dict = {}   # outer-step count of the last working-set solve (benchmarks / diagnostics)
 
 
 @traced("svm.smo", nbytes=lambda K, *a, **k: K.numel() * K.element_size(), device=lambda K, *a, **k: K.device)
@@ -273,15 +274,17 @@ def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max
     decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N).
 
     ``max_iter`` bounds the two-variable SMO steps on every path: the full solver counts them
-    directly; the working-set solver runs at most ``max(1, max_iter // inner_iter)`` outer steps of
-    at most ``inner_iter`` sub-problem steps each.  ``iters`` is the number of two-variable steps
+    directly; the working-set solver runs at most ``max(1, max_iter // 64)`` outer steps of at most
+    ``inner_iter`` sub-problem steps each (a sub-problem takes tens of steps, so a cap of
+    ``max_iter // inner_iter`` outer steps stopped large problems before convergence).  ``iters`` is the number of two-variable steps
     taken per problem in both cases (for the working-set path: the inner steps summed over the
     outer steps)."""
     B, N = y.shape
     if solver == "ws" or (solver == "auto" and K.device.type == "cuda" and N > WS_MIN_N):
         inner_iter = min(2048, max(1, max_iter))
-        alpha, G, outer, inner = smo_decomposition(K, y, C, eps, max_outer=max(1, max_iter // inner_iter),
+        alpha, G, outer, inner = smo_decomposition(K, y, C, eps, max_outer=max(1, max_iter // 64),
                                                    inner_iter=inner_iter)
+        LAST_SOLVE.update(solver="ws", outer=outer)
         return alpha, _rho(alpha, G, y.float(), C), inner.int()
     if K.device.type == "cuda":
         Kc = K.float().contiguous()

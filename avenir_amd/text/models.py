@@ -186,11 +186,20 @@ class NonNegMatFactSumm(LatentSemSumm):
         return W
 
 
+PAGERANK_KERNEL_MAX_N = 2048   # one persistent workgroup sweeps P per iteration: fine up to ~2k nodes
+
+
 def pagerank(S: torch.Tensor, d: float = 0.85, iters: int = 100, tol: float = 1e-10) -> torch.Tensor:
-    """Weighted pagerank by power iteration on a similarity matrix (dangling rows -> uniform)."""
+    """Weighted pagerank by power iteration on a similarity matrix (dangling rows -> uniform).
+    GPU, n <= 2048: the whole iteration in one persistent kernel (text.hip pagerank_kernel, no host
+    synchronisation per iteration); otherwise tensor GEMVs."""
     n = S.shape[0]
     out = S.sum(1, keepdim=True)
     P = torch.where(out > 0, S / out.clamp_min(1e-300), torch.full_like(S, 1.0 / n))
+    if S.is_cuda and 0 < n <= PAGERANK_KERNEL_MAX_N:
+        from .. import _native
+        r, _ = _native.C().pagerank(P.double().contiguous(), float(d), int(iters), float(tol))
+        return r.to(S.dtype)
     r = torch.full((n,), 1.0 / n, dtype=S.dtype, device=S.device)
     for _ in range(iters):
         nr = (1 - d) / n + d * (P.T @ r)
@@ -307,21 +316,72 @@ def _row_mean_add(M: torch.Tensor, rows: torch.Tensor, upd: torch.Tensor, mean: 
     M += acc / cnt.unsqueeze(1)
 
 
+def _alias_table(p: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Vose's alias table of a discrete distribution (host, O(V)): (prob f32 [V], alias i32 [V])."""
+    import numpy as np
+    q = (p.double().cpu().numpy() * p.numel()).astype(np.float64)
+    V = q.size
+    prob, alias = np.ones(V), np.arange(V, dtype=np.int64)
+    small = [i for i in range(V) if q[i] < 1.0]
+    large = [i for i in range(V) if q[i] >= 1.0]
+    while small and large:
+        s, l = small.pop(), large.pop()
+        prob[s], alias[s] = q[s], l
+        q[l] -= 1.0 - q[s]
+        (small if q[l] < 1.0 else large).append(l)
+    return torch.tensor(prob, dtype=torch.float32), torch.tensor(alias, dtype=torch.int32)
+
+
+def _sgns_dim(d: int) -> int:
+    for p in (64, 128, 192, 256):
+        if d <= p:
+            return p
+    return 0
+
+
 class Word2Vec:
+    """Skip-gram with negative sampling.  GPU with dim <= 256: one ``sgns_step`` launch per epoch
+    (text.hip: a wavefront per pair, device negatives from an alias table, Hogwild float atomics,
+    word2vec's linear rate decay from ``kernel_lr``); CPU: batched tensor SGD with per-row averaged
+    updates (rate ``lr``)."""
+
     def __init__(self, dim: int = 100, window: int = 5, negative: int = 5, min_count: int = 1, epochs: int = 5,
-                 lr: float = 0.5, batch: int = 4096, seed: int = 0, device="cpu"):
+                 lr: float = 0.5, batch: int = 4096, seed: int = 0, device="cpu", kernel_lr: float = 0.025):
         self.dim, self.window, self.negative, self.min_count = dim, window, negative, min_count
         self.epochs, self.lr, self.batch, self.seed, self.device = epochs, lr, batch, seed, torch.device(device)
+        self.kernel_lr = kernel_lr
 
     def _pairs(self, ids: list[list[int]]):
+        """(centre, context) of every in-sentence window pair, vectorised over the flat corpus."""
+        flat = torch.tensor([w for s in ids for w in s], dtype=torch.long)
+        sent = torch.tensor([k for k, s in enumerate(ids) for _ in s], dtype=torch.long)
         cen, ctx = [], []
-        for s in ids:
-            for i, w in enumerate(s):
-                for j in range(max(0, i - self.window), min(len(s), i + self.window + 1)):
-                    if j != i:
-                        cen.append(w)
-                        ctx.append(s[j])
-        return torch.tensor(cen, dtype=torch.long), torch.tensor(ctx, dtype=torch.long)
+        for off in range(1, self.window + 1):
+            ok = sent[off:] == sent[:-off] if flat.numel() > off else torch.zeros(0, dtype=torch.bool)
+            a, b = flat[:-off][ok], flat[off:][ok]
+            cen += [a, b]
+            ctx += [b, a]
+        if not cen:
+            return torch.zeros(0, dtype=torch.long), torch.zeros(0, dtype=torch.long)
+        return torch.cat(cen), torch.cat(ctx)
+
+    def _use_kernel(self) -> bool:
+        return self.device.type == "cuda" and _sgns_dim(self.dim) > 0
+
+    def _fit_kernel(self, Win: torch.Tensor, Wout: torch.Tensor, cen: torch.Tensor, ctx: torch.Tensor) -> None:
+        """Epochs of device SGNS: Win [R, dp] / Wout [V, dp] zero-padded beyond ``dim`` (padding
+        coordinates stay zero: their gradients are products with zeros)."""
+        from .. import _native
+        aprob, alias = _alias_table(self.noise)
+        aprob, alias = aprob.to(self.device), alias.to(self.device)
+        g = torch.Generator(device=self.device).manual_seed(self.seed)
+        cen, ctx = cen.to(self.device).int(), ctx.to(self.device).int()
+        n = cen.numel()
+        for ep in range(self.epochs):
+            perm = torch.randperm(n, device=self.device, generator=g)
+            _native.C().sgns_step(Win, Wout, cen[perm].contiguous(), ctx[perm].contiguous(), aprob, alias,
+                                  int(self.negative), float(self.kernel_lr), ep * n, self.epochs * n,
+                                  int(self.seed), ep)
 
     def fit(self, sentences: Sequence[Sequence[str]]) -> "Word2Vec":
         self.vocab = Vocabulary(sentences, self.min_count)
@@ -333,6 +393,14 @@ class Word2Vec:
         g = torch.Generator(device=self.device).manual_seed(self.seed)
         self.W = ((torch.rand((V, self.dim), device=self.device, generator=g) - 0.5) / self.dim)
         self.C = torch.zeros((V, self.dim), device=self.device)
+        if self._use_kernel():
+            dp = _sgns_dim(self.dim)
+            Win = torch.zeros((V, dp), device=self.device)
+            Win[:, : self.dim] = self.W
+            Wout = torch.zeros((V, dp), device=self.device)
+            self._fit_kernel(Win, Wout, cen, ctx)
+            self.W, self.C = Win[:, : self.dim].contiguous(), Wout[:, : self.dim].contiguous()
+            return self
         cen, ctx = cen.to(self.device), ctx.to(self.device)
         n = cen.numel()
         total = self.epochs * max(1, (n + self.batch - 1) // self.batch)
@@ -401,6 +469,15 @@ class Doc2Vec(Word2Vec):
         g = torch.Generator(device=self.device).manual_seed(self.seed)
         self.D = ((torch.rand((D, self.dim), device=self.device, generator=g) - 0.5) / self.dim)
         self.C = torch.zeros((V, self.dim), device=self.device)
+        if self._use_kernel():      # PV-DBOW = SGNS with the document table as the centre table
+            dp = _sgns_dim(self.dim)
+            Din = torch.zeros((D, dp), device=self.device)
+            Din[:, : self.dim] = self.D
+            Wout = torch.zeros((V, dp), device=self.device)
+            self._fit_kernel(Din, Wout, doc, word)
+            self.D, self.C = Din[:, : self.dim].contiguous(), Wout[:, : self.dim].contiguous()
+            self.W = self.C
+            return self
         n = doc.numel()
         for ep in range(self.epochs):
             perm = torch.randperm(n, device=self.device, generator=g)

@@ -479,8 +479,27 @@ def doc_term_matrix(docs: Sequence[Sequence[str]], vocab: Vocabulary, device="cp
                                    torch.tensor(val, dtype=torch.float32), size=(len(docs), len(vocab))).to(device)
 
 
+def tfidf_csr(counts: torch.Tensor, smooth: bool = True, sublinear: bool = False, norm: str | None = "l2"):
+    """Sparse CSR TF-IDF [D, V] from a CSR count matrix on the GPU: document frequencies by one
+    bincount of the column ids, then ONE ``tfidf_rows`` launch (text.hip: a wavefront per row
+    weights its entries and normalises them in place)."""
+    from .. import _native
+    D, V = counts.shape
+    crow, col = counts.crow_indices().contiguous(), counts.col_indices().contiguous()
+    val = counts.values().float().clone().contiguous()
+    df = torch.bincount(col, minlength=V).float()
+    idf = (torch.log((1 + D) / (1 + df)) + 1 if smooth else torch.log(D / df.clamp_min(1)) + 1).float().contiguous()
+    _native.C().tfidf_rows(crow, col, val, idf, bool(sublinear), {None: 0, "l1": 1, "l2": 2}[norm])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return torch.sparse_csr_tensor(crow, col, val, size=(D, V))
+
+
 def tfidf_matrix(counts: torch.Tensor, smooth: bool = True, sublinear: bool = False, norm: str | None = "l2"):
-    """Dense TF-IDF [D, V] from a (sparse or dense) count matrix: idf = ln((1+D)/(1+df)) + 1."""
+    """Dense TF-IDF [D, V] from a (sparse or dense) count matrix: idf = ln((1+D)/(1+df)) + 1.
+    Sparse CSR input on the GPU goes through the K28 row kernel (``tfidf_csr``)."""
+    if counts.is_sparse_csr and counts.is_cuda:
+        return tfidf_csr(counts, smooth, sublinear, norm).to_dense()
     X = counts.to_dense() if counts.is_sparse_csr or counts.is_sparse else counts
     D = X.shape[0]
     df = (X > 0).sum(0).float()

@@ -135,3 +135,50 @@ def test_text_nb_and_similarity():
     assert S.shape == (6, 6) and torch.allclose(S.diagonal(), torch.ones(6))
     J = wc.withSimilarityAlgo("jaccard").getInterSetSimilarity(True, False, 3)
     assert J.shape == (3, 3)
+
+
+# ------------------------------------------------------------------------------------------------
+# K28 kernels (text.hip): TF-IDF rows, persistent pagerank, SGNS word2vec / doc2vec
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_tfidf_kernel_matches_sklearn(cuda):
+    from sklearn.feature_extraction.text import TfidfVectorizer
+    docs, _, _ = _topic_corpus(200, seed=5)
+    docs[3] = []                                            # an empty document row
+    vocab = Vocabulary(docs)
+    X = doc_term_matrix(docs, vocab, device=cuda)
+    for norm in ("l2", "l1", None):
+        for sub in (False, True):
+            W = tfidf_matrix(X, sublinear=sub, norm=norm).cpu().numpy()
+            sk = TfidfVectorizer(analyzer=lambda d: d, vocabulary=vocab.words, norm=norm,
+                                 sublinear_tf=sub).fit_transform(docs).toarray()
+            assert np.allclose(W, sk, atol=1e-6), (norm, sub)
+
+
+@pytest.mark.gpu
+def test_pagerank_kernel_matches_tensor_path(cuda):
+    g = torch.Generator().manual_seed(2)
+    for n in (3, 130, 1500):
+        S = torch.rand((n, n), generator=g, dtype=torch.float64)
+        S[:, 1] = 0
+        S[1, :] = 0                                         # a dangling node
+        S.fill_diagonal_(0)
+        ref = pagerank(S)
+        got = pagerank(S.to(cuda)).cpu()
+        assert torch.allclose(got, ref, rtol=1e-10, atol=1e-13), n
+
+
+@pytest.mark.gpu
+def test_word2vec_and_doc2vec_kernel(cuda):
+    docs, labels, topics = _topic_corpus(400)
+    w2v = Word2Vec(dim=16, window=3, epochs=5, seed=0, device=cuda).fit(docs)
+    assert w2v.W.shape[1] == 16
+    sim = dict(w2v.most_similar("gpu", 5))
+    assert len(set(sim) & set(topics[0])) >= 4
+    d2v = Doc2Vec(dim=16, epochs=10, seed=0, device=cuda).fit(docs)
+    D = d2v.doc_vectors().cpu()
+    D = D - D.mean(0)
+    D = D / D.norm(dim=1, keepdim=True)
+    same = [(D[i] @ D[j]).item() for i in range(20) for j in range(20) if i != j and labels[i] == labels[j]]
+    diff = [(D[i] @ D[j]).item() for i in range(20) for j in range(20) if labels[i] != labels[j]]
+    assert np.mean(same) > np.mean(diff) + 0.2
