@@ -685,6 +685,36 @@ at::Tensor kendall_pairs(const at::Tensor& x, const at::Tensor& y) {
   return out;
 }
 
+// Mixed-type kNN (distance.hip): Qn [nq, Dn] / Rn [nr, Dn] f32 scaled numerics, Qc / Rc int32 codes
+// (-1 = missing), wc f32 [Dc].  Returns (dist f32 [nq, k], idx int64 [nq, k]).
+py::tuple mixed_knn(const at::Tensor& Qn, const at::Tensor& Qc, const at::Tensor& Rn, const at::Tensor& Rc,
+                    const at::Tensor& wc, int64_t k, int64_t r_base) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Qn, &Rn, &wc}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+    TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
+  }
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Qc, &Rc}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kInt);
+    TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
+  }
+  TORCH_CHECK(Qn.dim() == 2 && Rn.dim() == 2 && Qc.dim() == 2 && Rc.dim() == 2, "2-D inputs");
+  const int64_t nq = Qn.size(0), nr = Rn.size(0), Dn = Qn.size(1), Dc = Qc.size(1);
+  TORCH_CHECK(Qc.size(0) == nq && Rc.size(0) == nr && Rn.size(1) == Dn && Rc.size(1) == Dc && wc.numel() == Dc,
+              "shape mismatch");
+  TORCH_CHECK(Dn <= avk::mixed_knn_max_dims() && Dc <= avk::mixed_knn_max_dims() && k >= 1 && k <= 32,
+              "mixed_knn: <= 32 numeric and <= 32 categorical columns, 1 <= k <= 32");
+  TORCH_CHECK(nr < (1LL << 31), "too many reference rows");
+  auto d = at::empty({nq, k}, Qn.options());
+  auto i = at::empty({nq, k}, Qn.options().dtype(at::kLong));
+  DevGuard gd(Qn.device());
+  avk::mixed_knn(Qn.data_ptr<float>(), Qc.data_ptr<int>(), nq, Rn.data_ptr<float>(), Rc.data_ptr<int>(), nr, (int)Dn,
+                 (int)Dc, wc.data_ptr<float>(), (int)k, r_base, d.data_ptr<float>(),
+                 reinterpret_cast<long long*>(i.data_ptr<int64_t>()), cur_stream(Qn));
+  return py::make_tuple(d, i);
+}
+
 // K28 text kernels (text.hip)
 void tfidf_rows(const at::Tensor& crow, const at::Tensor& col, at::Tensor& val, const at::Tensor& idf, bool sublinear,
                 int64_t norm) {
@@ -721,10 +751,13 @@ py::tuple pagerank(const at::Tensor& P, double d, int64_t iters, double tol) {
   return py::make_tuple(r, it);
 }
 
-void sgns_step(at::Tensor& Win, at::Tensor& Wout, const at::Tensor& centre, const at::Tensor& context,
-               const at::Tensor& aprob, const at::Tensor& alias, int64_t neg, double lr, int64_t base, int64_t total,
-               int64_t seed, int64_t step) {
-  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Win, &Wout, &aprob}) {
+// One SGNS mini-batch: gradients of every pair into gIn / gOut (+ per-row counts cIn / cOut), then
+// the rows move by their mean update (gIn for the centre table summed when mean_in is false).
+// The caller checks id ranges once per fit (pairs / alias are built from the vocabulary).
+void sgns_step(at::Tensor& Win, at::Tensor& Wout, at::Tensor& gIn, at::Tensor& gOut, at::Tensor& cIn, at::Tensor& cOut,
+               const at::Tensor& centre, const at::Tensor& context, const at::Tensor& aprob, const at::Tensor& alias,
+               int64_t neg, double lr, bool mean_in, int64_t seed, int64_t step) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Win, &Wout, &gIn, &gOut, &cIn, &cOut, &aprob}) {
     CHECK_DEV((*t));
     CHECK_DTYPE((*t), at::kFloat);
     TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
@@ -735,20 +768,18 @@ void sgns_step(at::Tensor& Win, at::Tensor& Wout, const at::Tensor& centre, cons
     TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
   }
   TORCH_CHECK(Win.dim() == 2 && Wout.dim() == 2 && Win.size(1) == Wout.size(1), "Win [Rin, d], Wout [V, d]");
+  TORCH_CHECK(gIn.sizes() == Win.sizes() && gOut.sizes() == Wout.sizes() && cIn.numel() == Win.size(0) &&
+                  cOut.numel() == Wout.size(0), "gradient / count buffers must match the tables");
   const int64_t V = Wout.size(0), dim = Win.size(1);
   TORCH_CHECK(aprob.numel() == V && alias.numel() == V, "alias table must have V entries");
   TORCH_CHECK(centre.numel() == context.numel(), "centre / context lengths");
   TORCH_CHECK(neg >= 0 && neg <= 64, "0 <= neg <= 64");
-  // ids index the tables: bounds checked on the host copies (one check per epoch-sized batch)
-  if (centre.numel()) {
-    TORCH_CHECK(centre.min().item<int>() >= 0 && centre.max().item<int>() < Win.size(0), "centre id out of range");
-    TORCH_CHECK(context.min().item<int>() >= 0 && context.max().item<int>() < V, "context id out of range");
-    TORCH_CHECK(alias.min().item<int>() >= 0 && alias.max().item<int>() < V, "alias id out of range");
-  }
   DevGuard gd(Win.device());
-  avk::sgns_step(Win.data_ptr<float>(), Wout.data_ptr<float>(), (int)dim, centre.data_ptr<int>(), context.data_ptr<int>(),
-                 centre.numel(), aprob.data_ptr<float>(), alias.data_ptr<int>(), (int)V, (int)neg, (float)lr, base,
-                 std::max<int64_t>(total, 1), (unsigned long long)seed, (unsigned long long)step, cur_stream(Win));
+  avk::sgns_step(Win.data_ptr<float>(), Wout.data_ptr<float>(), gIn.data_ptr<float>(), gOut.data_ptr<float>(),
+                 cIn.data_ptr<float>(), cOut.data_ptr<float>(), (int)dim, Win.size(0), centre.data_ptr<int>(),
+                 context.data_ptr<int>(), centre.numel(), aprob.data_ptr<float>(), alias.data_ptr<int>(), (int)V,
+                 (int)neg, (float)lr, mean_in ? 1 : 0, (unsigned long long)seed, (unsigned long long)step,
+                 cur_stream(Win));
 }
 
 void tree_assign(const at::Tensor& codes, int64_t n, at::Tensor& node, const at::Tensor& split_feat,
@@ -2706,6 +2737,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbt_split", &gbt_split);
   m.def("rank_avg", &rank_avg);
   m.def("tfidf_rows", &tfidf_rows);
+  m.def("mixed_knn", &mixed_knn);
   m.def("pagerank", &pagerank);
   m.def("sgns_step", &sgns_step);
   m.def("kendall_pairs", &kendall_pairs);

@@ -269,6 +269,11 @@ void lstm_bwd(const float* dhseq, const unsigned short* gates, const float* cseq
               const float* dcn, const void* wfragT, int B, int T, int H, int KS, int RT, unsigned short* dz,
               float* dh0, float* dc0, hipStream_t stream);
 
+// distance.hip: mixed-type kNN without one-hot expansion
+int mixed_knn_max_dims();
+void mixed_knn(const float* Qn, const int* Qc, long long nq, const float* Rn, const int* Rc, long long nr, int Dn,
+               int Dc, const float* wc, int k, long long r_base, float* out_d, long long* out_i, hipStream_t stream);
+
 // stats.hip (K26 rank statistics)
 void rank_avg(const double* sorted, const long long* perm, long long n, const int* group, int n_groups, double* ranks,
               double* tie, double* gsum, hipStream_t stream);
@@ -279,8 +284,8 @@ void tfidf_rows(const long long* crow, const long long* col, float* val, const f
                 int sublinear, int norm, hipStream_t stream);
 int pagerank_max_n();
 void pagerank(const double* P, int n, double d, int iters, double tol, double* r, int* it, hipStream_t stream);
-void sgns_step(float* Win, float* Wout, int dim, const int* centre, const int* context, long long n_pairs,
-               const float* aprob, const int* alias, int V, int neg, float lr0, long long base, long long total,
-               unsigned long long seed, unsigned long long step, hipStream_t stream);
+void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, float* cOut, int dim, long long rows_in,
+               const int* centre, const int* context, long long n_pairs, const float* aprob, const int* alias, int V,
+               int neg, float lr, int mean_in, unsigned long long seed, unsigned long long step, hipStream_t stream);
 
 }  // namespace avk

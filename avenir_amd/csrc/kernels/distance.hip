@@ -381,6 +381,72 @@ __global__ __launch_bounds__(VOTE_T) void knn_vote_kernel(
   pred[q] = best;
 }
 
+// Mixed-type record distance without one-hot expansion: numeric columns
+// pre-scaled by sqrt(w) / range contribute squared differences, categorical columns contribute
+// w on a code mismatch, w / 2 when exactly one side is missing (-1) and 0 when both are — exactly
+// the squared euclidean distance of ops.distance.encode_mixed's scaled one-hot embedding, so
+// results match the MFMA path, but the width is the number of columns, not of categorical values.
+// One thread per query (features in registers), 256 reference rows per LDS stage (all threads read
+// the same row: broadcast), top-k in registers; returns euclidean distances.
+constexpr int MX_T = 256;
+constexpr int MX_MAXD = 32;
+
+template <int K>
+__global__ __launch_bounds__(MX_T) void mixed_knn_kernel(const float* __restrict__ Qn, const int* __restrict__ Qc,
+                                                         long long nq, const float* __restrict__ Rn,
+                                                         const int* __restrict__ Rc, long long nr, int Dn, int Dc,
+                                                         const float* __restrict__ wc, int k, long long r_base,
+                                                         float* __restrict__ out_d, long long* __restrict__ out_i) {
+  __shared__ float sRn[MX_T * MX_MAXD];
+  __shared__ int sRc[MX_T * MX_MAXD];
+  __shared__ float sw[MX_MAXD];
+  const int tid = threadIdx.x;
+  const long long q = (long long)blockIdx.x * MX_T + tid;
+  if (tid < Dc) sw[tid] = wc[tid];
+  float qn[MX_MAXD];
+  int qc[MX_MAXD];
+#pragma unroll
+  for (int f = 0; f < MX_MAXD; ++f) {
+    qn[f] = (q < nq && f < Dn) ? Qn[q * Dn + f] : 0.f;
+    qc[f] = (q < nq && f < Dc) ? Qc[q * Dc + f] : -1;
+  }
+  float bd[K];
+  int bi[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
+  for (long long r0 = 0; r0 < nr; r0 += MX_T) {
+    const int rows = (int)min((long long)MX_T, nr - r0);
+    __syncthreads();  // the previous stage's reads are done
+    for (int e = tid; e < rows * Dn; e += MX_T) sRn[e] = Rn[r0 * Dn + e];
+    for (int e = tid; e < rows * Dc; e += MX_T) sRc[e] = Rc[r0 * Dc + e];
+    __syncthreads();
+    if (q >= nq) continue;
+    for (int j = 0; j < rows; ++j) {
+      float d = 0.f;
+#pragma unroll
+      for (int f = 0; f < MX_MAXD; ++f)
+        if (f < Dn) {
+          const float t = qn[f] - sRn[j * Dn + f];
+          d = fmaf(t, t, d);
+        }
+#pragma unroll
+      for (int f = 0; f < MX_MAXD; ++f)
+        if (f < Dc) {
+          const int a = qc[f], b = sRc[j * Dc + f];
+          const float w = sw[f];
+          d += (a < 0 && b < 0) ? 0.f : ((a < 0 || b < 0) ? 0.5f * w : (a != b ? w : 0.f));
+        }
+      topk_insert<K>(bd, bi, d, (int)(r0 + j));
+    }
+  }
+  if (q >= nq) return;
+  for (int s = 0; s < k; ++s) {
+    const bool ok = s < K && bi[s] >= 0;
+    out_d[q * k + s] = ok ? sqrtf(fmaxf(bd[s], 0.f)) : INFINITY;
+    out_i[q * k + s] = ok ? (long long)bi[s] + r_base : -1;
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -432,6 +498,22 @@ void knn_vote(const float* dist, const long long* idx, long long M, int k, const
   else if (C <= 64) AV_VOTE(64);
   else throw std::runtime_error("knn_vote: more than 64 classes");
 #undef AV_VOTE
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int mixed_knn_max_dims() { return MX_MAXD; }
+
+void mixed_knn(const float* Qn, const int* Qc, long long nq, const float* Rn, const int* Rc, long long nr, int Dn,
+               int Dc, const float* wc, int k, long long r_base, float* out_d, long long* out_i, hipStream_t stream) {
+  if (nq <= 0) return;
+  if (Dn > MX_MAXD || Dc > MX_MAXD || k < 1 || k > 32) throw std::runtime_error("mixed_knn: dims <= 32, 1 <= k <= 32");
+  const unsigned grid = (unsigned)((nq + MX_T - 1) / MX_T);
+#define AV_MX(KK) mixed_knn_kernel<KK><<<grid, MX_T, 0, stream>>>(Qn, Qc, nq, Rn, Rc, nr, Dn, Dc, wc, k, r_base, out_d, out_i)
+  if (k <= 4) AV_MX(4);
+  else if (k <= 8) AV_MX(8);
+  else if (k <= 16) AV_MX(16);
+  else AV_MX(32);
+#undef AV_MX
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -712,6 +712,189 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
 // split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into quarters, each lane
 // streams its column of those K rows (coalesced, 8 loads in flight), and the 4 partials are added
 // in a fixed order (deterministic).  Grid (N / 64, B): >= 128 workgroups at N = 8192.
+// Register-cached variant (N <= PER * 1024) with both sides (up / low) selected TOGETHER: one
+// combined reduction for the two maxima and the two candidate counts, then every radix digit pass
+// builds the two 256-bin histograms in the same sweep and two waves scan them in parallel, and the
+// tie ranking of both sides shares one barrier — 12 barriers per launch instead of ~40 (the
+// selection is latency-bound at one workgroup).  Same working set as smo_ws_select_kernel.
+template <int PER>
+__global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __restrict__ alpha,
+                                                               const float* __restrict__ G,
+                                                               const float* __restrict__ y, int N, int ldag, float C,
+                                                               int h, long long* __restrict__ ws,
+                                                               bool* __restrict__ ok, float* __restrict__ gap) {
+  extern __shared__ unsigned in_up[];
+  __shared__ unsigned hist[2][256];
+  __shared__ float redf[2][SEL_T / 64];
+  __shared__ unsigned redu[2][SEL_T / 64];
+  __shared__ unsigned s_prefix[2], s_mask[2], s_krem[2], s_gt[2];
+  __shared__ int pick[2][64];
+  __shared__ unsigned wcnt[2][PER][SEL_T / 64];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* ab = alpha + (long long)b * ldag;
+  const float* gb = G + (long long)b * ldag;
+  const float* yb = y + (long long)b * N;
+  const int words = (N + 31) / 32;
+  for (int i = tid; i < words; i += SEL_T) in_up[i] = 0;
+  float cv[2][PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int n = tid + i * SEL_T;
+    cv[0][i] = n < N ? ws_violation(0, yb[n], ab[n], gb[n], C) : -INFINITY;
+    cv[1][i] = n < N ? ws_violation(1, yb[n], ab[n], gb[n], C) : -INFINITY;
+  }
+  // ---- maxima and candidate counts of both sides: one barrier ---------------------------------
+  float m[2] = {-INFINITY, -INFINITY};
+  unsigned e[2] = {0u, 0u};
+#pragma unroll
+  for (int w = 0; w < 2; ++w)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      m[w] = fmaxf(m[w], cv[w][i]);
+      e[w] += cv[w][i] > -INFINITY ? 1u : 0u;
+    }
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    for (int o = 32; o > 0; o >>= 1) {
+      m[w] = fmaxf(m[w], __shfl_xor(m[w], o, 64));
+      e[w] += __shfl_xor(e[w], o, 64);
+    }
+    if (lane == 0) { redf[w][wv] = m[w]; redu[w][wv] = e[w]; }
+  }
+  if (tid < 2) { s_prefix[tid] = 0; s_mask[tid] = 0; }
+  __syncthreads();
+  unsigned k[2];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    float mm = -INFINITY;
+    unsigned ee = 0;
+    for (int q = 0; q < SEL_T / 64; ++q) { mm = fmaxf(mm, redf[w][q]); ee += redu[w][q]; }
+    m[w] = mm;
+    k[w] = ee < (unsigned)h ? ee : (unsigned)h;
+  }
+  if (tid == 0) gap[b] = m[0] + m[1];
+  if (tid < 2) s_krem[tid] = k[tid];
+  // ---- 4 radix digit passes, both sides per pass ------------------------------------------------
+  for (int d = 3; d >= 0; --d) {
+    if (tid < 512) hist[tid >> 8][tid & 255] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      if (k[w] == 0) continue;  // block-uniform
+      const unsigned prefix = s_prefix[w], mask = s_mask[w];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const float v = cv[w][i];
+        bool act = false;
+        unsigned dg = 0;
+        if (v > -INFINITY) {
+          const unsigned key = order_key(v);
+          act = (key & mask) == prefix;
+          dg = (key >> (8 * d)) & 255u;
+        }
+        const unsigned long long am = __ballot(act);
+        if (am) {
+          const int lead = __ffsll((long long)am) - 1;
+          const unsigned d0 = (unsigned)__builtin_amdgcn_readlane((int)dg, lead);
+          const unsigned long long same = __ballot(act && dg == d0);
+          if (lane == lead) atomicAdd(&hist[w][d0], (unsigned)__popcll(same));
+          else if (act && dg != d0) atomicAdd(&hist[w][dg], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (wv < 2 && k[wv] > 0) {  // wave w scans side w's 256 bins
+      const int w = wv, l = lane;
+      const unsigned prefix = s_prefix[w], mask = s_mask[w];
+      unsigned c[4], sum = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        c[t] = hist[w][255 - (4 * l + t)];
+        sum += c[t];
+      }
+      unsigned inc = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned yv = __shfl_up(inc, o, 64);
+        if (l >= o) inc += yv;
+      }
+      const unsigned krem = s_krem[w], excl = inc - sum;
+      if (excl < krem && krem <= inc) {
+        unsigned cum = excl;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (cum + c[t] >= krem) {
+            const unsigned dg = 255u - (unsigned)(4 * l + t);
+            s_prefix[w] = prefix | (dg << (8 * d));
+            s_mask[w] = mask | (255u << (8 * d));
+            s_krem[w] = krem - cum;
+            break;
+          }
+          cum += c[t];
+        }
+      }
+      if (l == 0) s_gt[w] = 0;
+    }
+    __syncthreads();
+  }
+  // ---- keys above the threshold, and ties by ascending index, both sides: one barrier ----------
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  unsigned long long bal[2][PER];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const unsigned T = s_prefix[w];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      bool eq = false;
+      if (k[w] > 0 && cv[w][i] > -INFINITY) {
+        const unsigned key = order_key(cv[w][i]);
+        if (key > T) pick[w][atomicAdd(&s_gt[w], 1u)] = i * SEL_T + tid;
+        eq = key == T;
+      }
+      bal[w][i] = __ballot(eq);
+      if (lane == 0) wcnt[w][i][wv] = (unsigned)__popcll(bal[w][i]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const unsigned krem = s_krem[w], ngt = k[w] - krem;
+    unsigned eq_base = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      unsigned before = eq_base, tot = 0;
+      for (int q = 0; q < SEL_T / 64; ++q) {
+        const unsigned c = wcnt[w][i][q];
+        if (q < wv) before += c;
+        tot += c;
+      }
+      if ((bal[w][i] >> lane) & 1ull) {
+        const unsigned r = before + (unsigned)__popcll(bal[w][i] & below);
+        if (r < krem) pick[w][ngt + r] = i * SEL_T + tid;
+      }
+      eq_base += tot;
+    }
+  }
+  __syncthreads();
+  if (tid < (int)k[0]) atomicOr(&in_up[pick[0][tid] >> 5], 1u << (pick[0][tid] & 31));
+  __syncthreads();
+  if (tid < 2 * h) {
+    const int which = tid / h, slot = tid % h, np = (int)k[which];
+    long long* wsb = ws + (long long)b * 2 * h + which * h;
+    bool* okb = ok + (long long)b * 2 * h + which * h;
+    if (slot < np) {
+      const int n = pick[which][slot];
+      int rank = 0;
+      for (int j = 0; j < np; ++j) rank += pick[which][j] < n ? 1 : 0;
+      wsb[rank] = n;
+      okb[rank] = which == 0 || !((in_up[n >> 5] >> (n & 31)) & 1u);
+    } else {
+      wsb[slot] = 0;
+      okb[slot] = false;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
                                                             const float* __restrict__ dA, const bool* __restrict__ ok,
                                                             const float* __restrict__ y, float* __restrict__ G, int N,
@@ -784,7 +967,9 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   const int per = (N + SEL_T - 1) / SEL_T;
-  if (per <= 8) smo_ws_select_kernel<8><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
+  if (per <= 4) smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  else if (per <= 8) smo_ws_select2_kernel<8><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   else if (per <= 16) smo_ws_select_kernel<16><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   else smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   AV_HIP_CHECK(hipGetLastError());

@@ -5,18 +5,19 @@
 // python/text/summ.py TextRank (networkx pagerank over a sentence-similarity graph) and
 // python/text/wv.py:36-153 (gensim word2vec / doc2vec).
 //   * tfidf_rows_kernel : one wavefront per document row of the CSR count matrix: w = tf * idf[col]
-//     (tf = count or 1 + ln count), then the row's L2 (or L1) norm as a wave reduction and the
+//     (tf = count, or 1 + ln count when sublinear — scikit-learn's sublinear_tf), then the row's L2 (or L1) norm as a wave reduction and the
 //     normalised weights written in place — one pass instead of densify + 4 tensor ops.
 //   * pagerank_kernel   : the whole power iteration in ONE persistent workgroup: r lives in LDS,
 //     every iteration is a column sweep of the row-stochastic matrix (thread j owns columns
 //     j, j + 1024, ... — consecutive threads read consecutive addresses of a row), and the L1
 //     change is reduced on the device, so there is no host synchronisation per iteration.
-//   * sgns_kernel       : one wavefront per (centre, context) pair: the context and `neg` negatives
-//     drawn on the device (Philox keyed by (seed, step, pair) + an alias table of the unigram^0.75
-//     noise distribution), dot products as wave reductions, the logistic gradients, and the
-//     updates applied Hogwild-style with float atomics (the standard GPU word2vec scheme); d <= 256
-//     (each lane owns d / 64 coordinates).  PV-DBOW (doc2vec) is the same kernel with the document
-//     matrix as the centre table.
+//   * sgns_grad_kernel / sgns_apply_kernel : one wavefront per (centre, context) pair of a
+//     mini-batch: the context and `neg` negatives drawn on the device (Philox keyed by (seed, step,
+//     pair) + an alias table of the unigram^0.75 noise distribution), dot products as wave
+//     reductions, the logistic gradients accumulated per row with float atomics; the apply pass
+//     moves each touched row by the mean of its updates (the tensor path's averaged SGD);
+//     d <= 256 (each lane owns d / 64 coordinates).  PV-DBOW (doc2vec) is the same pair kernel
+//     with the document matrix as the centre table (summed, not averaged: few rows per doc).
 // Index safety: CSR column ids < V (checked by the binding), alias indices < V, pair ids < V / D.
 #include "avenir_common.h"
 #include "avenir_kernels.h"
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(256) void tfidf_rows_kernel(const long long* __rest
   const long long b = crow[row], e = crow[row + 1];
   float acc = 0.f;
   for (long long k = b + lane; k < e; k += 64) {
-    const float tf = sublinear ? log1pf(val[k]) : val[k];
+    const float tf = sublinear ? (val[k] > 0.f ? 1.f + logf(val[k]) : 0.f) : val[k];
     const float w = tf * idf[col[k]];
     val[k] = w;
     acc += norm == 2 ? w * w : fabsf(w);
@@ -89,21 +90,25 @@ __global__ __launch_bounds__(PR_T) void pagerank_kernel(const double* __restrict
   if (tid == 0) *it_out = it;
 }
 
-// alias table: prob[V] (float), alias[V] (int); draw: k = u1 * V, take k if u2 < prob[k] else alias[k]
+// alias table: prob[V] (float), alias[V] (int); draw: k = u1 * V, take k if u2 < prob[k] else alias[k].
+// One mini-batch: every pair's gradients are ADDED into gIn / gOut with per-row counts (float
+// atomics); sgns_apply_kernel then moves each touched row by the MEAN of its updates.  A device
+// batch touches a frequent word many times, and summing those steps (Hogwild over thousands of
+// concurrent waves) diverges on small vocabularies; the mean keeps the step size independent of the
+// batch size — the same update as the tensor path of text/models.py.
 template <int DV>
-__global__ __launch_bounds__(256) void sgns_kernel(float* __restrict__ Win, float* __restrict__ Wout,
-                                                   const int* __restrict__ centre, const int* __restrict__ context,
-                                                   long long n_pairs, const float* __restrict__ aprob,
-                                                   const int* __restrict__ alias, int V, int neg, float lr0,
-                                                   long long base, long long total, unsigned long long seed,
-                                                   unsigned long long step) {
+__global__ __launch_bounds__(256) void sgns_grad_kernel(const float* __restrict__ Win, const float* __restrict__ Wout,
+                                                        float* __restrict__ gIn, float* __restrict__ gOut,
+                                                        float* __restrict__ cIn, float* __restrict__ cOut,
+                                                        const int* __restrict__ centre, const int* __restrict__ context,
+                                                        long long n_pairs, const float* __restrict__ aprob,
+                                                        const int* __restrict__ alias, int V, int neg, float lr,
+                                                        unsigned long long seed, unsigned long long step) {
   const long long pr = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pr >= n_pairs) return;
-  // word2vec's linear decay over all pairs of all epochs
-  const float lr = lr0 * fmaxf(1e-4f, 1.f - (float)(base + pr) / (float)total);
   const int lane = threadIdx.x & 63;
   const int c = centre[pr];
-  float* wc = Win + (long long)c * (DV * 64);
+  const float* wc = Win + (long long)c * (DV * 64);
   float v[DV], grad[DV];
 #pragma unroll
   for (int k = 0; k < DV; ++k) {
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(256) void sgns_kernel(float* __restrict__ Win, floa
       o = av::u32_to_unit(rr.y) < aprob[k] ? k : alias[k];
       label = 0.f;
     }
-    float* wo = Wout + (long long)o * (DV * 64);
+    const float* wo = Wout + (long long)o * (DV * 64);
     float u[DV], dot = 0.f;
 #pragma unroll
     for (int k = 0; k < DV; ++k) {
@@ -132,16 +137,34 @@ __global__ __launch_bounds__(256) void sgns_kernel(float* __restrict__ Win, floa
       dot += u[k] * v[k];
     }
     dot = av::wave_sum(dot);
-    const float sig = 1.f / (1.f + __expf(-dot));
-    const float g = (label - sig) * lr;
+    const float g = (label - 1.f / (1.f + __expf(-dot))) * lr;
+    float* go = gOut + (long long)o * (DV * 64);
 #pragma unroll
     for (int k = 0; k < DV; ++k) {
       grad[k] += g * u[k];
-      atomicAdd(&wo[lane + 64 * k], g * v[k]);
+      atomicAdd(&go[lane + 64 * k], g * v[k]);
+    }
+    if (lane == 0) atomicAdd(&cOut[o], 1.f);
+  }
+  float* gc = gIn + (long long)c * (DV * 64);
+#pragma unroll
+  for (int k = 0; k < DV; ++k) atomicAdd(&gc[lane + 64 * k], grad[k]);
+  if (lane == 0) atomicAdd(&cIn[c], 1.f);
+}
+
+// W[r] += g[r] / max(count[r], 1) (mean_in: the centre table of doc2vec sums instead), g -> 0
+__global__ __launch_bounds__(256) void sgns_apply_kernel(float* __restrict__ W, float* __restrict__ g,
+                                                         const float* __restrict__ cnt, long long rows, int dp,
+                                                         int mean) {
+  const long long total = rows * dp;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
+    const float gv = g[i];
+    if (gv != 0.f) {
+      W[i] += mean ? gv / fmaxf(cnt[i / dp], 1.f) : gv;
+      g[i] = 0.f;
     }
   }
-#pragma unroll
-  for (int k = 0; k < DV; ++k) atomicAdd(&wc[lane + 64 * k], grad[k]);
 }
 
 }  // namespace
@@ -164,18 +187,26 @@ void pagerank(const double* P, int n, double d, int iters, double tol, double* r
   AV_HIP_CHECK(hipGetLastError());
 }
 
-void sgns_step(float* Win, float* Wout, int dim, const int* centre, const int* context, long long n_pairs,
-               const float* aprob, const int* alias, int V, int neg, float lr0, long long base, long long total,
-               unsigned long long seed, unsigned long long step, hipStream_t stream) {
+void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, float* cOut, int dim, long long rows_in,
+               const int* centre, const int* context, long long n_pairs, const float* aprob, const int* alias, int V,
+               int neg, float lr, int mean_in, unsigned long long seed, unsigned long long step, hipStream_t stream) {
   if (n_pairs <= 0) return;
   const unsigned grid = (unsigned)((n_pairs + 3) / 4);
+#define AV_SG(DV) sgns_grad_kernel<DV><<<grid, 256, 0, stream>>>(Win, Wout, gIn, gOut, cIn, cOut, centre, context, \
+      n_pairs, aprob, alias, V, neg, lr, seed, step)
   switch (dim) {
-    case 64: sgns_kernel<1><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
-    case 128: sgns_kernel<2><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
-    case 192: sgns_kernel<3><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
-    case 256: sgns_kernel<4><<<grid, 256, 0, stream>>>(Win, Wout, centre, context, n_pairs, aprob, alias, V, neg, lr0, base, total, seed, step); break;
+    case 64: AV_SG(1); break;
+    case 128: AV_SG(2); break;
+    case 192: AV_SG(3); break;
+    case 256: AV_SG(4); break;
     default: throw std::runtime_error("sgns_step: padded dim must be 64, 128, 192 or 256");
   }
+#undef AV_SG
+  AV_HIP_CHECK(hipGetLastError());
+  sgns_apply_kernel<<<av::stream_grid(rows_in * dim, 256, 4, 4096), 256, 0, stream>>>(Win, gIn, cIn, rows_in, dim,
+                                                                                       mean_in);
+  AV_HIP_CHECK(hipGetLastError());
+  sgns_apply_kernel<<<av::stream_grid((long long)V * dim, 256, 4, 4096), 256, 0, stream>>>(Wout, gOut, cOut, V, dim, 1);
   AV_HIP_CHECK(hipGetLastError());
 }
 

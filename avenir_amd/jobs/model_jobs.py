@@ -172,7 +172,7 @@ def same_type_similarity(args):
     ``trainId,testId,dist*scale,trainClass,testClass`` — the layout the NearestNeighbor mapper
     and FeatureCondProbJoiner read (J/knn/NearestNeighbor.java:130-183).  ``sts.top.match.count``
     keeps only the k nearest train records per test record (fused distance + top-k kernel)."""
-    from ..ops.distance import encode_mixed, knn, pairwise
+    from ..ops.distance import encode_mixed, knn, knn_mixed, pairwise, split_mixed
     ctx = JobContext(args, "sts.")
     schema = ctx.schema("same.schema.file.path")
     if args.train:
@@ -194,11 +194,16 @@ def same_type_similarity(args):
             ctx.comm.all_reduce(lo, "min")
             ctx.comm.all_reduce(hi, "max")
         ranges[f.ordinal] = (float(f.min) if f.min is not None else float(lo), float(f.max) if f.max is not None else float(hi))
-    A = encode_mixed(tr, ranges=ranges)
-    B = encode_mixed(te, ranges=ranges)
     nf = max(1, len(tr.numeric_fields) + len(tr.binned_fields))
-    scale = ctx.get_float("distance.scale", 1000.0)
     topk = ctx.get_int("top.match.count", 0)
+    onehot = sum(f.num_bins for f in tr.binned_fields if f.is_categorical)
+    # wide categoricals: the column-wise mixed kernel instead of a one-hot embedding (GPU top-k)
+    use_mixed = (0 < topk <= 32 and tr.device.type == "cuda" and onehot > 64
+                 and len(tr.numeric_fields) + len(tr.binned_fields) <= 32)
+    if not use_mixed:
+        A = encode_mixed(tr, ranges=ranges)
+        B = encode_mixed(te, ranges=ranges)
+    scale = ctx.get_float("distance.scale", 1000.0)
     cls_tr = tr.label_values() if tr.labels is not None else [""] * tr.n
     cls_te = te.label_values() if te.labels is not None else [""] * te.n
     id_tr = tr.ids or [str(i) for i in range(tr.n)]
@@ -206,7 +211,12 @@ def same_type_similarity(args):
     d = ctx.delim_out
     out = []
     if topk > 0:
-        dist, idx = knn(B, A, topk, "euclidean")
+        if use_mixed:
+            An, Ac, wc = split_mixed(tr, ranges=ranges)
+            Bn, Bc, _ = split_mixed(te, ranges=ranges)
+            dist, idx = knn_mixed(Bn, Bc, An, Ac, wc, topk)
+        else:
+            dist, idx = knn(B, A, topk, "euclidean")
         dist = (dist / math.sqrt(nf) * scale).round().long().cpu().tolist()
         for q, (dr, ir) in enumerate(zip(dist, idx.cpu().tolist())):
             for dd, i in zip(dr, ir):

@@ -195,6 +195,55 @@ def cluster_accumulate(X: torch.Tensor, assign: torch.Tensor, K: int) -> tuple[t
     return sums, counts
 
 
+def split_mixed(t: Table, weights: dict[int, float] | None = None, ranges: dict[int, tuple] | None = None):
+    """The mixed-type distance's columns without one-hot expansion: (numeric f32 [n, Dn] scaled by
+    sqrt(w) / range — bucketed attributes as ordinals, as in ``encode_mixed`` —, categorical codes
+    int32 [n, Dc] with -1 for missing, categorical weights f32 [Dc])."""
+    enc_num, cats, wcat = [], [], []
+    n = t.n
+    num_only = Table(t.schema, t.n, t.codes[:0], [], t.numeric, t.numeric_fields, t.labels, t.class_field)
+    if t.numeric_fields:
+        enc_num.append(encode_mixed(num_only, weights, ranges))
+    for j, f in enumerate(t.binned_fields):
+        w = (weights or {}).get(f.ordinal, f.weight)
+        c = t.codes[j, :n].long()
+        if f.is_categorical:
+            cats.append(torch.where(c < f.num_bins, c, torch.full_like(c, -1)).int())
+            wcat.append(float(w))
+        else:
+            b = max(f.num_bins - 1, 1)
+            enc_num.append((torch.where(c >= t.missing, torch.zeros_like(c), c).float() / b * math.sqrt(w)).unsqueeze(1))
+    num = torch.cat(enc_num, 1).contiguous() if enc_num else torch.zeros((n, 0), device=t.device)
+    cat = torch.stack(cats, 1).contiguous() if cats else torch.zeros((n, 0), dtype=torch.int32, device=t.device)
+    return num, cat, torch.tensor(wcat, dtype=torch.float32, device=t.device)
+
+
+def knn_mixed(Qn, Qc, Rn, Rc, wc, k: int, r_base: int = 0):
+    """k nearest references under the mixed-type distance (``split_mixed`` columns): euclidean
+    distances f32 [nq, k] (+inf / -1 for missing slots) and global indices.  GPU: one
+    ``mixed_knn_kernel`` launch; CPU: the same arithmetic on the one-hot embedding's terms."""
+    k = int(k)
+    if Qn.is_cuda:
+        return tuple(_native.C().mixed_knn(Qn.float().contiguous(), Qc.int().contiguous(), Rn.float().contiguous(),
+                                           Rc.int().contiguous(), wc.float().contiguous(), k, int(r_base)))
+    nq, nr = Qn.shape[0], Rn.shape[0]
+    out_d = torch.full((nq, k), math.inf)
+    out_i = torch.full((nq, k), -1, dtype=torch.long)
+    for s in range(0, nq, 1024):
+        q, qc = Qn[s:s + 1024].float(), Qc[s:s + 1024].long()
+        d2 = torch.cdist(q, Rn.float()) ** 2 if Qn.shape[1] else torch.zeros((q.shape[0], nr))
+        for f in range(Qc.shape[1]):
+            a, b = qc[:, f].view(-1, 1), Rc[:, f].long().view(1, -1)
+            w = float(wc[f])
+            d2 = d2 + torch.where((a < 0) & (b < 0), 0.0, torch.where((a < 0) | (b < 0), 0.5 * w,
+                                                                      torch.where(a != b, w, 0.0)))
+        kk = min(k, nr)
+        v, i = torch.topk(d2, kk, dim=1, largest=False, sorted=True)
+        out_d[s:s + 1024, :kk] = v.clamp_min(0).sqrt()
+        out_i[s:s + 1024, :kk] = i + r_base
+    return out_d, out_i
+
+
 def encode_mixed(t: Table, weights: dict[int, float] | None = None, ranges: dict[int, tuple] | None = None) -> torch.Tensor:
     """Dense [n, D] float32 embedding whose squared euclidean distance equals the mixed-type record
     distance: numeric attributes contribute w * ((x - y) / range)^2, categorical attributes

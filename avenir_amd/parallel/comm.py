@@ -16,6 +16,14 @@ Design notes for xGMI (7 point-to-point links per MI355X): the payloads here are
 tensors (KB..tens of MB), so ops are issued ONCE per model/iteration on coalesced flat buffers
 (``all_reduce_coalesced``) rather than per key; RCCL picks its one-shot/tree algorithms for small
 messages and multi-ring for large ones.
+
+One-shot small-message all-reduce: on a fully connected xGMI node every GPU has a
+direct link to every peer, so for KB-scale count tables a single all-gather (each rank's table to
+every peer in ONE step) followed by a local sum replaces the 2(n-1)-step ring of reduce-scatter +
+all-gather.  ``all_reduce(..., algo="oneshot")`` (or ``AVMI_SMALL_ALLREDUCE=oneshot`` for sum
+reductions up to ``AVMI_ONESHOT_MAX_BYTES``, default 64 KiB) takes that path; the local reduction
+runs in rank order, so the result is also bit-identical on every rank and run (fp32 / fp64 sums
+included).  ``bench.py`` reports both latencies on multi-GPU runs.
 """
 from __future__ import annotations
 
@@ -32,6 +40,8 @@ from ..utils import logging as alog
 from ..utils.tracing import traced
 
 _COMM: "Comm | None" = None
+_ONESHOT_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "") == "oneshot"
+_ONESHOT_MAX_BYTES = int(os.environ.get("AVMI_ONESHOT_MAX_BYTES", str(64 << 10)))
 
 
 class CollectiveTimeout(RuntimeError):
@@ -107,10 +117,16 @@ class Comm:
 
     # ------------------------------------------------------------------------------------------
     @traced("comm.all_reduce", nbytes=lambda self, t, *a, **k: t.numel() * t.element_size(), device=lambda self, t, *a, **k: t.device)
-    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        """In-place all-reduce (sum|max|min|prod); returns ``t``."""
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", algo: str | None = None) -> torch.Tensor:
+        """In-place all-reduce (sum|max|min|prod); returns ``t``.  ``algo``: None (library
+        collective, or the env-selected small-message path), "ring" (library), "oneshot"
+        (all-gather + rank-ordered local reduction)."""
         if not self.is_distributed:
             return t
+        if algo is None and op == "sum" and _ONESHOT_ENV and t.numel() * t.element_size() <= _ONESHOT_MAX_BYTES:
+            algo = "oneshot"
+        if algo == "oneshot":
+            return self._all_reduce_oneshot(t, op)
         t0 = time.perf_counter()
         x, moved = self._prep(t)
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
@@ -118,6 +134,28 @@ class Comm:
         dist.all_reduce(x, op=rop)
         if moved:
             t.copy_(x)
+        self._account(t, t0)
+        return t
+
+    def _all_reduce_oneshot(self, t: torch.Tensor, op: str) -> torch.Tensor:
+        """One all-gather of every rank's buffer, then the reduction over ranks in rank order."""
+        t0 = time.perf_counter()
+        g = self.all_gather(t.contiguous())                       # [world, *t.shape]
+        if op == "sum":
+            r = g[0].clone()
+            for k in range(1, self.world):
+                r += g[k]
+        elif op == "max":
+            r = g.amax(0)
+        elif op == "min":
+            r = g.amin(0)
+        elif op == "prod":
+            r = g[0].clone()
+            for k in range(1, self.world):
+                r *= g[k]
+        else:
+            raise ValueError(op)
+        t.copy_(r)
         self._account(t, t0)
         return t
 

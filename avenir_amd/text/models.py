@@ -340,16 +340,15 @@ def _sgns_dim(d: int) -> int:
 
 
 class Word2Vec:
-    """Skip-gram with negative sampling.  GPU with dim <= 256: one ``sgns_step`` launch per epoch
-    (text.hip: a wavefront per pair, device negatives from an alias table, Hogwild float atomics,
-    word2vec's linear rate decay from ``kernel_lr``); CPU: batched tensor SGD with per-row averaged
-    updates (rate ``lr``)."""
+    """Skip-gram with negative sampling, mini-batch SGD with per-row averaged updates (rate
+    ``lr``, linear decay).  GPU with dim <= 256: per batch one ``sgns_step`` (text.hip: a
+    wavefront per pair, device negatives from an alias table, gradient accumulation + mean apply);
+    CPU: the same batches as tensor ops."""
 
     def __init__(self, dim: int = 100, window: int = 5, negative: int = 5, min_count: int = 1, epochs: int = 5,
-                 lr: float = 0.5, batch: int = 4096, seed: int = 0, device="cpu", kernel_lr: float = 0.025):
+                 lr: float = 0.5, batch: int = 4096, seed: int = 0, device="cpu"):
         self.dim, self.window, self.negative, self.min_count = dim, window, negative, min_count
         self.epochs, self.lr, self.batch, self.seed, self.device = epochs, lr, batch, seed, torch.device(device)
-        self.kernel_lr = kernel_lr
 
     def _pairs(self, ids: list[list[int]]):
         """(centre, context) of every in-sentence window pair, vectorised over the flat corpus."""
@@ -368,20 +367,37 @@ class Word2Vec:
     def _use_kernel(self) -> bool:
         return self.device.type == "cuda" and _sgns_dim(self.dim) > 0
 
-    def _fit_kernel(self, Win: torch.Tensor, Wout: torch.Tensor, cen: torch.Tensor, ctx: torch.Tensor) -> None:
-        """Epochs of device SGNS: Win [R, dp] / Wout [V, dp] zero-padded beyond ``dim`` (padding
-        coordinates stay zero: their gradients are products with zeros)."""
+    def _fit_kernel(self, Win: torch.Tensor, Wout: torch.Tensor, cen: torch.Tensor, ctx: torch.Tensor,
+                    mean_in: bool = True, decay_per_batch: bool = True) -> None:
+        """Epochs of device SGNS mini-batches (the tensor path's batches, rate and averaged
+        updates): Win [R, dp] / Wout [V, dp] zero-padded beyond ``dim`` (padding coordinates stay
+        zero: their gradients are products with zeros)."""
         from .. import _native
+        V = Wout.shape[0]
         aprob, alias = _alias_table(self.noise)
         aprob, alias = aprob.to(self.device), alias.to(self.device)
         g = torch.Generator(device=self.device).manual_seed(self.seed)
-        cen, ctx = cen.to(self.device).int(), ctx.to(self.device).int()
         n = cen.numel()
+        if n:   # ids index the tables: checked once per fit
+            assert int(cen.min()) >= 0 and int(cen.max()) < Win.shape[0] and int(ctx.min()) >= 0 and int(ctx.max()) < V
+        cen, ctx = cen.to(self.device).int(), ctx.to(self.device).int()
+        gIn, gOut = torch.zeros_like(Win), torch.zeros_like(Wout)
+        cIn = torch.zeros(Win.shape[0], device=self.device)
+        cOut = torch.zeros(V, device=self.device)
+        nb = max(1, (n + self.batch - 1) // self.batch)
+        total, step = self.epochs * nb, 0
+        C = _native.C()
         for ep in range(self.epochs):
             perm = torch.randperm(n, device=self.device, generator=g)
-            _native.C().sgns_step(Win, Wout, cen[perm].contiguous(), ctx[perm].contiguous(), aprob, alias,
-                                  int(self.negative), float(self.kernel_lr), ep * n, self.epochs * n,
-                                  int(self.seed), ep)
+            c_ep, o_ep = cen[perm].contiguous(), ctx[perm].contiguous()
+            lr_ep = self.lr * (1 - ep / self.epochs)
+            for b in range(0, n, self.batch):
+                lr = self.lr * max(1e-4, 1 - step / total) if decay_per_batch else lr_ep
+                C.sgns_step(Win, Wout, gIn, gOut, cIn, cOut, c_ep[b:b + self.batch], o_ep[b:b + self.batch],
+                            aprob, alias, int(self.negative), float(lr), bool(mean_in), int(self.seed), step)
+                cIn.zero_()
+                cOut.zero_()
+                step += 1
 
     def fit(self, sentences: Sequence[Sequence[str]]) -> "Word2Vec":
         self.vocab = Vocabulary(sentences, self.min_count)
@@ -474,7 +490,7 @@ class Doc2Vec(Word2Vec):
             Din = torch.zeros((D, dp), device=self.device)
             Din[:, : self.dim] = self.D
             Wout = torch.zeros((V, dp), device=self.device)
-            self._fit_kernel(Din, Wout, doc, word)
+            self._fit_kernel(Din, Wout, doc, word, mean_in=False, decay_per_batch=False)
             self.D, self.C = Din[:, : self.dim].contiguous(), Wout[:, : self.dim].contiguous()
             self.W = self.C
             return self

@@ -504,7 +504,7 @@ def tfidf_matrix(counts: torch.Tensor, smooth: bool = True, sublinear: bool = Fa
     D = X.shape[0]
     df = (X > 0).sum(0).float()
     idf = torch.log((1 + D) / (1 + df)) + 1 if smooth else torch.log(D / df.clamp_min(1)) + 1
-    tf = torch.log1p(X) if sublinear else X
+    tf = torch.where(X > 0, 1 + torch.log(X.clamp_min(1e-30)), torch.zeros_like(X)) if sublinear else X
     W = tf * idf
     if norm == "l2":
         W = W / W.norm(dim=1, keepdim=True).clamp_min(1e-12)

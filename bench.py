@@ -66,6 +66,15 @@ def _allreduce_probe(comm, dev) -> list:
         t = comm.reduce_max_scalar(t)
         alg = nbytes / t / 1e9
         out.append({"bytes": nbytes, "us": t * 1e6, "algbw_GBps": alg, "busbw_GBps": alg * 2 * (W - 1) / W})
+    # one-shot small-message path (all-gather + rank-ordered local sum) at the count-table size
+    for nbytes, iters in ((8 << 10, 50), (64 << 10, 50)):
+        x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+        for _ in range(3):
+            comm.all_reduce(x, algo="oneshot")
+        comm.barrier()
+        t = _timed(lambda: [comm.all_reduce(x, algo="oneshot") for _ in range(iters)], dev) / iters
+        t = comm.reduce_max_scalar(t)
+        out.append({"bytes": nbytes, "algo": "oneshot", "us": t * 1e6})
     return out
 
 

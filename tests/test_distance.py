@@ -1,6 +1,8 @@
 """Distance / kNN / k-means / similarity tests (CPU oracles + gpu numerics)."""
 import math
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -312,3 +314,51 @@ def test_knn_class_cond_weight_per_class_posterior():
             i = int(r.neighbors[q, j])
             exp[q, y[i]] += post[i, y[i]]
     assert torch.allclose(r.class_scores, exp, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------------------------
+# mixed-type distance without one-hot expansion (distance.hip mixed_knn_kernel)
+# ---------------------------------------------------------------------------------------------
+def _mixed_table(n, seed, device="cpu", card=300):
+    from avenir_amd.data.table import from_arrays
+    from avenir_amd.utils.schema import FeatureSchema
+    rng = np.random.default_rng(seed)
+    sj = {"fields": [
+        {"name": "x", "ordinal": 0, "dataType": "double", "feature": True, "weight": 1.0},
+        {"name": "z", "ordinal": 1, "dataType": "double", "feature": True, "weight": 0.5},
+        {"name": "c", "ordinal": 2, "dataType": "categorical", "feature": True, "weight": 2.0,
+         "cardinality": [f"v{i}" for i in range(card)]},
+        {"name": "e", "ordinal": 3, "dataType": "categorical", "feature": True, "cardinality": ["a", "b", "c"]}]}
+    cols = {0: rng.normal(size=n).round(3), 1: rng.uniform(0, 5, n).round(3),
+            2: [f"v{v}" if v < card else "zz" for v in rng.integers(0, card + 5, n)],   # some unknown values
+            3: [("a", "b", "c")[v] for v in rng.integers(0, 3, n)]}
+    return from_arrays(FeatureSchema.from_json(sj), cols, device=device)
+
+
+def test_split_mixed_equals_onehot_embedding_distances():
+    from avenir_amd.ops.distance import encode_mixed, knn, knn_mixed, split_mixed
+    tr, te = _mixed_table(500, 1), _mixed_table(80, 2)
+    ranges = {0: (-4.0, 4.0), 1: (0.0, 5.0)}
+    A, B = encode_mixed(tr, ranges=ranges), encode_mixed(te, ranges=ranges)
+    An, Ac, wc = split_mixed(tr, ranges=ranges)
+    Bn, Bc, _ = split_mixed(te, ranges=ranges)
+    assert Ac.shape[1] == 2 and A.shape[1] > 300          # the one-hot width the kernel avoids
+    d1, i1 = knn(B, A, 7, "euclidean")
+    d2, i2 = knn_mixed(Bn, Bc, An, Ac, wc, 7)
+    assert torch.allclose(d1, d2, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_mixed_knn_kernel_matches_cpu(cuda):
+    from avenir_amd.ops.distance import knn_mixed, split_mixed
+    tr, te = _mixed_table(3000, 3), _mixed_table(700, 4)
+    ranges = {0: (-4.0, 4.0), 1: (0.0, 5.0)}
+    An, Ac, wc = split_mixed(tr, ranges=ranges)
+    Bn, Bc, _ = split_mixed(te, ranges=ranges)
+    for k in (1, 5, 20):
+        dc, ic = knn_mixed(Bn, Bc, An, Ac, wc, k)
+        dg, ig = knn_mixed(Bn.to(cuda), Bc.to(cuda), An.to(cuda), Ac.to(cuda), wc.to(cuda), k, r_base=0)
+        assert torch.allclose(dg.cpu(), dc, atol=1e-5)
+        # neighbour sets agree wherever distances are not tied
+        ok = (dc[:, 1:] - dc[:, :-1]).abs().min(1).values > 1e-4 if k > 1 else torch.ones(dc.shape[0], dtype=torch.bool)
+        assert torch.equal(ig.cpu()[ok], ic[ok])
