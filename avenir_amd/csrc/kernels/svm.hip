@@ -839,20 +839,19 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
   }
   // ---- keys above the threshold, and ties by ascending index, both sides: one barrier ----------
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  unsigned long long bal[2][PER];
+  // the tie flags are recomputed in the ranking pass (cheap) rather than kept: registers for
+  // PER = 32 (N = 32768)
+  auto is_tie = [&](int w, int i) -> bool {
+    return k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) == s_prefix[w];
+  };
 #pragma unroll
   for (int w = 0; w < 2; ++w) {
     const unsigned T = s_prefix[w];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      bool eq = false;
-      if (k[w] > 0 && cv[w][i] > -INFINITY) {
-        const unsigned key = order_key(cv[w][i]);
-        if (key > T) pick[w][atomicAdd(&s_gt[w], 1u)] = i * SEL_T + tid;
-        eq = key == T;
-      }
-      bal[w][i] = __ballot(eq);
-      if (lane == 0) wcnt[w][i][wv] = (unsigned)__popcll(bal[w][i]);
+      if (k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) > T) pick[w][atomicAdd(&s_gt[w], 1u)] = i * SEL_T + tid;
+      const unsigned long long bal = __ballot(is_tie(w, i));
+      if (lane == 0) wcnt[w][i][wv] = (unsigned)__popcll(bal);
     }
   }
   __syncthreads();
@@ -868,8 +867,10 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
         if (q < wv) before += c;
         tot += c;
       }
-      if ((bal[w][i] >> lane) & 1ull) {
-        const unsigned r = before + (unsigned)__popcll(bal[w][i] & below);
+      const bool tie = is_tie(w, i);
+      const unsigned long long bal = __ballot(tie);
+      if (tie) {
+        const unsigned r = before + (unsigned)__popcll(bal & below);
         if (r < krem) pick[w][ngt + r] = i * SEL_T + tid;
       }
       eq_base += tot;
@@ -970,7 +971,8 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   if (per <= 4) smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   else if (per <= 8) smo_ws_select2_kernel<8><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
-  else if (per <= 16) smo_ws_select_kernel<16><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  else if (per <= 16) smo_ws_select2_kernel<16><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  else if (per <= 32) smo_ws_select2_kernel<32><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   else smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
   AV_HIP_CHECK(hipGetLastError());
 }

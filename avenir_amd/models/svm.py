@@ -228,7 +228,7 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     Q = Q or (_native.C().smo_ws_size() if K.device.type == "cuda" else 128)
     if rel_tol is None:   # sub-problem tolerance max(eps, rel_tol * gap) of the fused GPU solver
         import os
-        rel_tol = float(os.environ.get("AVMI_SMO_REL_TOL", "0.1"))
+        rel_tol = float(os.environ.get("AVMI_SMO_REL_TOL", "0.3"))
     st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused, rel_tol)
     outer = 0
     if st.gpu and graph:
