@@ -1353,9 +1353,15 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
   CHECK_DTYPE(ok, at::kBool);
   TORCH_CHECK(ws.numel() == B * 2 * h && ok.numel() == B * 2 * h && gap.numel() == B, "ws / ok [B, 2h], gap [B]");
   DevGuard g(y.device());
+  // two-level selection scratch: per (problem, part, side) local candidates and counts (inside a
+  // graph capture these come from the capture's private pool)
+  const int64_t parts = avk::smo_ws_select_parts((int)N);
+  auto cand = at::empty({B, parts, 2, h}, y.options().dtype(at::kInt));
+  auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
   avk::smo_ws_select(alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)N,
                      (int)alpha.size(1), (float)C, (int)h, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()),
-                     ok.data_ptr<bool>(), gap.data_ptr<float>(), cur_stream(y));
+                     ok.data_ptr<bool>(), gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(),
+                     cur_stream(y));
 }
 
 void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& ok, at::Tensor& alpha,

@@ -120,7 +120,8 @@ void smo_solve(const float* K, const float* y, const float* diag, float* alpha, 
                float eps, int max_iter, int* iters, hipStream_t stream);
 // working-set selection (gap, top-h up / low violators, duplicate mask) and gradient update
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
-                   long long* ws, bool* ok, float* gap, hipStream_t stream);
+                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, hipStream_t stream);
+int smo_ws_select_parts(int N);
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                    int B, int N, int ldag, int Q, hipStream_t stream);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,

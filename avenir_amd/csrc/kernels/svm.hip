@@ -171,89 +171,84 @@ __global__ __launch_bounds__(SMO_THREADS) void smo_kernel(const float* __restric
 //   tolerance is max(eps, 0.1 gap)).
 constexpr int WS_Q = 128;
 
-// (value, index) argmax with ties to the lowest index AND a plain max of a second value, in one
-// DPP pass: the three chains are independent, so their DPP moves issue back to back.
-__device__ __forceinline__ void wave_argmax_and_max(float& v, int& idx, float& m) {
-#define AV_ARGMAX_MAX_STEP(CTRL)                                \
-  {                                                             \
-    const float v2 = av::dpp_f<CTRL>(v), m2 = av::dpp_f<CTRL>(m); \
-    const int i2 = av::dpp_i<CTRL>(idx);                        \
-    av::wave_arg_step<true>(v, idx, v2, i2);                    \
-    m = fmaxf(m, m2);                                           \
-  }
-  AV_ARGMAX_MAX_STEP(0xB1)
-  AV_ARGMAX_MAX_STEP(0x4E)
-  AV_ARGMAX_MAX_STEP(0x124)
-  AV_ARGMAX_MAX_STEP(0x128)
-#undef AV_ARGMAX_MAX_STEP
-  float r = av::lane_f(v, 0), rm = av::lane_f(m, 0);
-  int ri = __builtin_amdgcn_readlane(idx, 0);
-#pragma unroll
-  for (int l = 16; l < 64; l += 16) {
-    av::wave_arg_step<true>(r, ri, av::lane_f(v, l), __builtin_amdgcn_readlane(idx, l));
-    rm = fmaxf(rm, av::lane_f(m, l));
-  }
-  v = r;
-  idx = ri;
-  m = rm;
+__device__ __forceinline__ unsigned order_key(float f) {  // monotone float -> uint
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Wave max of u32 keys: 4 DPP max steps + the 4 row results over v_readlane (uniform result).
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+  v = max(v, (unsigned)av::dpp_i<0xB1>((int)v));
+  v = max(v, (unsigned)av::dpp_i<0x4E>((int)v));
+  v = max(v, (unsigned)av::dpp_i<0x124>((int)v));
+  v = max(v, (unsigned)av::dpp_i<0x128>((int)v));
+  const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0), b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+  const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+  return max(max(a, b), max(c, d));
+}
+
+__device__ __forceinline__ float order_key_inv(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
 
 // The SMO iterations of one Q-variable sub-problem, run by ONE wavefront: lane l owns variables
-// l + 64e; the Q x Q kernel block is in LDS.  Returns the iteration count.
+// t = l + 64e; the Q x Q kernel block is in LDS.  Returns the iteration count.
+//
+// Every VALU instruction of a wave64 costs >= 4 cycles and the loop is one dependent chain, so the
+// instruction count IS the iteration time.  The two argmax selections are therefore packed u32
+// max reductions: the order-preserving key of the value with its low 7 bits replaced by
+// (127 - t) — ties (and values within 2^-16 relative) go to the lowest variable — one DPP chain
+// each instead of a (value, index) pair chain; the exact values for the stopping test come from
+// the owner lane (i's violation) or from a plain max of exact keys (the low-set maximum).
 template <int E>
 __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (&a)[E], float (&g)[E],
                            const float (&qd)[E], float C, float epsl, int max_iter, int lane) {
-  constexpr int NONE = 0x7fffffff;
+  static_assert(E * 64 <= 128, "7-bit variable codes");
+  auto rdl = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
   int it = 0;
   for (; it < max_iter; ++it) {
-    float gmax = -INFINITY;
-    int gi = NONE;
+    unsigned ku = 0u;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const bool up = y[e] > 0.f ? a[e] < C : (y[e] < 0.f && a[e] > 0.f);
-      const float v = -y[e] * g[e];
-      if (up && v > gmax) { gmax = v; gi = lane + 64 * e; }
+      const unsigned kk = (order_key(-y[e] * g[e]) & ~0x7Fu) | (127u - (unsigned)(lane + 64 * e));
+      ku = up ? max(ku, kk) : ku;
     }
-    av::wave_argmax(gmax, gi);
-    if (gi == NONE) break;
-    const int i = gi;
-    // i / j are wave-uniform: their per-lane state comes over with v_readlane (a few cycles)
-    // instead of ds_bpermute shuffles (an LDS round trip each)
-    float Kii = 0.f;
+    ku = wave_max_u32(ku);
+    if (ku == 0u) break;
+    const int i = 127 - (int)(ku & 0x7Fu);
+    // i's state from its owner lane (the slot index is wave-uniform)
+    const int si = i >> 6;
+    float yi = 0.f, ai = 0.f, gi_ = 0.f, Kii = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (e == (i >> 6)) Kii = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qd[e]), i & 63));
-    float best = -INFINITY, gmax2 = -INFINITY;
-    int bj = NONE;
+      if (e == si) { yi = rdl(y[e], i & 63); ai = rdl(a[e], i & 63); gi_ = rdl(g[e], i & 63); Kii = rdl(qd[e], i & 63); }
+    const float gmax = -yi * gi_;
+    unsigned kj = 0u, km = 0u;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int t = lane + 64 * e;
       const bool low = y[e] > 0.f ? a[e] > 0.f : (y[e] < 0.f && a[e] < C);
-      if (!low) continue;
       const float yg = y[e] * g[e];
-      gmax2 = fmaxf(gmax2, yg);
       const float bd = gmax + yg;
-      if (bd > 0.f) {
-        float q = Kii + qd[e] - 2.f * Ks[i][t];
-        q = q > 0.f ? q : TAU;
-        // selection only: the hardware reciprocal (one instruction) instead of an IEEE divide;
-        // the two-variable update below keeps exact division
-        const float gain = bd * bd * __builtin_amdgcn_rcpf(q);
-        if (gain > best) { best = gain; bj = t; }
-      }
+      float q = Kii + qd[e] - 2.f * Ks[i][t];
+      q = q > 0.f ? q : TAU;
+      // selection only: the hardware reciprocal instead of an IEEE divide (the update keeps it)
+      const float gain = bd * bd * __builtin_amdgcn_rcpf(q);
+      const unsigned kg = (order_key(gain) & ~0x7Fu) | (127u - (unsigned)t);
+      kj = (low && bd > 0.f) ? max(kj, kg) : kj;
+      km = low ? max(km, order_key(yg)) : km;
     }
-    wave_argmax_and_max(best, bj, gmax2);
-    if (gmax + gmax2 < epsl || bj == NONE) break;
-    const int j = bj;
-    // fetch the pair's state from its owner lanes (slot index is wave-uniform)
-    const int si = i >> 6, sj = j >> 6;
-    float yi = 0.f, ai = 0.f, gi_ = 0.f, yj = 0.f, aj = 0.f, gj = 0.f, Kjj = 0.f;
-    auto rdl = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+    kj = wave_max_u32(kj);
+    km = wave_max_u32(km);
+    const float gmax2 = km ? order_key_inv(km) : -INFINITY;
+    if (gmax + gmax2 < epsl || kj == 0u) break;
+    const int j = 127 - (int)(kj & 0x7Fu);
+    const int sj = j >> 6;
+    float yj = 0.f, aj = 0.f, gj = 0.f, Kjj = 0.f;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      if (e == si) { yi = rdl(y[e], i & 63); ai = rdl(a[e], i & 63); gi_ = rdl(g[e], i & 63); }
+    for (int e = 0; e < E; ++e)
       if (e == sj) { yj = rdl(y[e], j & 63); aj = rdl(a[e], j & 63); gj = rdl(g[e], j & 63); Kjj = rdl(qd[e], j & 63); }
-    }
     const float oi = ai, oj = aj;
     float quad = Kii + Kjj - 2.f * Ks[i][j];
     quad = quad > 0.f ? quad : TAU;
@@ -466,10 +461,6 @@ __device__ __forceinline__ float ws_violation(int which, float y, float a, float
   return low ? y * g : -INFINITY;
 }
 
-__device__ __forceinline__ unsigned order_key(float f) {  // monotone float -> uint
-  const unsigned u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
 
 template <typename T, typename Op>
 __device__ T block_reduce(T v, T* red, Op op) {  // all SEL_T threads; red has >= 17 slots
@@ -708,41 +699,62 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   }
 }
 
-// G[n] += y[n] * sum_q dA[q] K[ws[q], n].  A workgroup owns 64 consecutive columns n; its 4 waves
-// split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into quarters, each lane
-// streams its column of those K rows (coalesced, 8 loads in flight), and the 4 partials are added
-// in a fixed order (deterministic).  Grid (N / 64, B): >= 128 workgroups at N = 8192.
-// Register-cached variant (N <= PER * 1024) with both sides (up / low) selected TOGETHER: one
-// combined reduction for the two maxima and the two candidate counts, then every radix digit pass
-// builds the two 256-bin histograms in the same sweep and two waves scan them in parallel, and the
-// tie ranking of both sides shares one barrier — 12 barriers per launch instead of ~40 (the
-// selection is latency-bound at one workgroup).  Same working set as smo_ws_select_kernel.
-template <int PER>
-__global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __restrict__ alpha,
-                                                               const float* __restrict__ G,
-                                                               const float* __restrict__ y, int N, int ldag, float C,
-                                                               int h, long long* __restrict__ ws,
-                                                               bool* __restrict__ ok, float* __restrict__ gap) {
-  extern __shared__ unsigned in_up[];
+// Register-cached selection with both sides (up / low) selected TOGETHER: one combined reduction
+// for the two maxima and the two candidate counts, then every radix digit pass builds the two
+// 256-bin histograms in the same sweep and two waves scan them in parallel, and the tie ranking of
+// both sides shares one barrier — 12 barriers per launch instead of ~40 (the selection is
+// latency-bound at one workgroup).  Same working set as smo_ws_select_kernel.
+//
+// Element sources (position pos = i * SEL_T + tid, positions ascend with the row index, so tie
+// ranking by position = by index):
+//   RangeSrc — rows [n0, n1) of the problem (single level, or one part of a two-level selection);
+//   CandSrc  — the parts' local top-h candidates concatenated in part order (second level).
+// Two-level selection (N > 4096): each part of 2048 / 4096 / 8192 rows (the smallest whose
+// candidates fit one workgroup) keeps its local top h per side (the global top h, ties to the
+// lowest index, is contained in the union), then ONE workgroup of 256..1024 threads selects over
+// the parts x h candidates — the parts run on different CUs with 2..8 register rows per thread.
+struct RangeSrc {
+  int n0, n1;
+  __device__ int row(int, int pos) const { const int n = n0 + pos; return n < n1 ? n : -1; }
+};
+struct CandSrc {
+  const int* cand;  // [parts][2][h] local picks (ascending row index), this problem
+  const int* cnt;   // [parts][2]
+  int parts, h;
+  __device__ int row(int w, int pos) const {
+    for (int q = 0; q < parts; ++q) {
+      const int c = cnt[q * 2 + w];
+      if (pos < c) return cand[(q * 2 + w) * h + pos];
+      pos -= c;
+    }
+    return -1;
+  }
+};
+
+template <int PER, bool PARTIAL, int NT, class Src>
+__device__ void ws_select2_body(const Src& src, const float* __restrict__ ab, const float* __restrict__ gb,
+                                const float* __restrict__ yb, int N, float C, int h, long long* __restrict__ wsb,
+                                bool* __restrict__ okb, float* __restrict__ gapb, int* __restrict__ cand_out,
+                                int* __restrict__ cnt_out, unsigned* in_up) {
   __shared__ unsigned hist[2][256];
-  __shared__ float redf[2][SEL_T / 64];
-  __shared__ unsigned redu[2][SEL_T / 64];
+  __shared__ float redf[2][NT / 64];
+  __shared__ unsigned redu[2][NT / 64];
   __shared__ unsigned s_prefix[2], s_mask[2], s_krem[2], s_gt[2];
   __shared__ int pick[2][64];
-  __shared__ unsigned wcnt[2][PER][SEL_T / 64];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const float* ab = alpha + (long long)b * ldag;
-  const float* gb = G + (long long)b * ldag;
-  const float* yb = y + (long long)b * N;
-  const int words = (N + 31) / 32;
-  for (int i = tid; i < words; i += SEL_T) in_up[i] = 0;
+  __shared__ unsigned wcnt[2][PER][NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (!PARTIAL)
+    for (int i = tid; i < (N + 31) / 32; i += NT) in_up[i] = 0;
   float cv[2][PER];
+  int rid[2][PER];  // row of each register slot (the candidate source is walked once)
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int n = tid + i * SEL_T;
-    cv[0][i] = n < N ? ws_violation(0, yb[n], ab[n], gb[n], C) : -INFINITY;
-    cv[1][i] = n < N ? ws_violation(1, yb[n], ab[n], gb[n], C) : -INFINITY;
-  }
+  for (int w = 0; w < 2; ++w)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int n = src.row(w, i * NT + tid);
+      rid[w][i] = n;
+      cv[w][i] = n >= 0 ? ws_violation(w, yb[n], ab[n], gb[n], C) : -INFINITY;
+    }
   // ---- maxima and candidate counts of both sides: one barrier ---------------------------------
   float m[2] = {-INFINITY, -INFINITY};
   unsigned e[2] = {0u, 0u};
@@ -768,15 +780,15 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
   for (int w = 0; w < 2; ++w) {
     float mm = -INFINITY;
     unsigned ee = 0;
-    for (int q = 0; q < SEL_T / 64; ++q) { mm = fmaxf(mm, redf[w][q]); ee += redu[w][q]; }
+    for (int q = 0; q < NT / 64; ++q) { mm = fmaxf(mm, redf[w][q]); ee += redu[w][q]; }
     m[w] = mm;
     k[w] = ee < (unsigned)h ? ee : (unsigned)h;
   }
-  if (tid == 0) gap[b] = m[0] + m[1];
+  if (!PARTIAL && tid == 0) *gapb = m[0] + m[1];
   if (tid < 2) s_krem[tid] = k[tid];
   // ---- 4 radix digit passes, both sides per pass ------------------------------------------------
   for (int d = 3; d >= 0; --d) {
-    if (tid < 512) hist[tid >> 8][tid & 255] = 0;
+    for (int q = tid; q < 512; q += NT) hist[q >> 8][q & 255] = 0;
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
@@ -837,10 +849,9 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
     }
     __syncthreads();
   }
-  // ---- keys above the threshold, and ties by ascending index, both sides: one barrier ----------
+  // ---- keys above the threshold, and ties by ascending position, both sides: one barrier -------
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // the tie flags are recomputed in the ranking pass (cheap) rather than kept: registers for
-  // PER = 32 (N = 32768)
+  // tie flags are recomputed in the ranking pass (cheap) rather than kept in registers
   auto is_tie = [&](int w, int i) -> bool {
     return k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) == s_prefix[w];
   };
@@ -849,7 +860,8 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
     const unsigned T = s_prefix[w];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      if (k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) > T) pick[w][atomicAdd(&s_gt[w], 1u)] = i * SEL_T + tid;
+      if (k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) > T)
+        pick[w][atomicAdd(&s_gt[w], 1u)] = rid[w][i];
       const unsigned long long bal = __ballot(is_tie(w, i));
       if (lane == 0) wcnt[w][i][wv] = (unsigned)__popcll(bal);
     }
@@ -862,7 +874,7 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       unsigned before = eq_base, tot = 0;
-      for (int q = 0; q < SEL_T / 64; ++q) {
+      for (int q = 0; q < NT / 64; ++q) {
         const unsigned c = wcnt[w][i][q];
         if (q < wv) before += c;
         tot += c;
@@ -871,31 +883,95 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
       const unsigned long long bal = __ballot(tie);
       if (tie) {
         const unsigned r = before + (unsigned)__popcll(bal & below);
-        if (r < krem) pick[w][ngt + r] = i * SEL_T + tid;
+        if (r < krem) pick[w][ngt + r] = rid[w][i];
       }
       eq_base += tot;
     }
   }
   __syncthreads();
+  if (PARTIAL) {
+    // local picks in ascending row order + counts (the second level concatenates the parts)
+    if (tid < 2 * h) {
+      const int which = tid / h, slot = tid % h, np = (int)k[which];
+      if (slot < np) {
+        const int n = pick[which][slot];
+        int rank = 0;
+        for (int j = 0; j < np; ++j) rank += pick[which][j] < n ? 1 : 0;
+        cand_out[which * h + rank] = n;
+      }
+    }
+    if (tid < 2) cnt_out[tid] = (int)k[tid];
+    return;
+  }
   if (tid < (int)k[0]) atomicOr(&in_up[pick[0][tid] >> 5], 1u << (pick[0][tid] & 31));
   __syncthreads();
   if (tid < 2 * h) {
     const int which = tid / h, slot = tid % h, np = (int)k[which];
-    long long* wsb = ws + (long long)b * 2 * h + which * h;
-    bool* okb = ok + (long long)b * 2 * h + which * h;
+    long long* wsw = wsb + which * h;
+    bool* okw = okb + which * h;
     if (slot < np) {
       const int n = pick[which][slot];
       int rank = 0;
       for (int j = 0; j < np; ++j) rank += pick[which][j] < n ? 1 : 0;
-      wsb[rank] = n;
-      okb[rank] = which == 0 || !((in_up[n >> 5] >> (n & 31)) & 1u);
+      wsw[rank] = n;
+      okw[rank] = which == 0 || !((in_up[n >> 5] >> (n & 31)) & 1u);
     } else {
-      wsb[slot] = 0;
-      okb[slot] = false;
+      wsw[slot] = 0;
+      okw[slot] = false;
     }
   }
 }
 
+// single level: one workgroup per problem over all N rows
+template <int PER>
+__global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __restrict__ alpha,
+                                                               const float* __restrict__ G,
+                                                               const float* __restrict__ y, int N, int ldag, float C,
+                                                               int h, long long* __restrict__ ws,
+                                                               bool* __restrict__ ok, float* __restrict__ gap) {
+  extern __shared__ unsigned in_up[];
+  const int b = blockIdx.x;
+  ws_select2_body<PER, false, SEL_T>(RangeSrc{0, N}, alpha + (long long)b * ldag, G + (long long)b * ldag,
+                                     y + (long long)b * N, N, C, h, ws + (long long)b * 2 * h,
+                                     ok + (long long)b * 2 * h, gap + b, nullptr, nullptr, in_up);
+}
+
+// two levels: part p of problem b = rows [p * chunk, (p + 1) * chunk), chunk = PER * SEL_T
+template <int PER>
+__global__ __launch_bounds__(SEL_T) void smo_ws_select_part_kernel(const float* __restrict__ alpha,
+                                                                   const float* __restrict__ G,
+                                                                   const float* __restrict__ y, int N, int ldag,
+                                                                   float C, int h, int parts, int* __restrict__ cand,
+                                                                   int* __restrict__ cnt) {
+  const int b = blockIdx.y, p = blockIdx.x;
+  const int n0 = p * PER * SEL_T, n1 = min(N, n0 + PER * SEL_T);
+  ws_select2_body<PER, true, SEL_T>(RangeSrc{n0, n1}, alpha + (long long)b * ldag, G + (long long)b * ldag,
+                                    y + (long long)b * N, N, C, h, nullptr, nullptr, nullptr,
+                                    cand + ((long long)b * parts + p) * 2 * h, cnt + ((long long)b * parts + p) * 2,
+                                    nullptr);
+}
+
+// merge: one workgroup of NT >= parts * h threads over the concatenated candidates
+template <int NT>
+__global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __restrict__ alpha,
+                                                                 const float* __restrict__ G,
+                                                                 const float* __restrict__ y, int N, int ldag, float C,
+                                                                 int h, int parts, const int* __restrict__ cand,
+                                                                 const int* __restrict__ cnt,
+                                                                 long long* __restrict__ ws, bool* __restrict__ ok,
+                                                                 float* __restrict__ gap) {
+  extern __shared__ unsigned in_up[];
+  const int b = blockIdx.x;
+  const CandSrc src{cand + (long long)b * parts * 2 * h, cnt + (long long)b * parts * 2, parts, h};
+  ws_select2_body<1, false, NT>(src, alpha + (long long)b * ldag, G + (long long)b * ldag, y + (long long)b * N, N, C,
+                                h, ws + (long long)b * 2 * h, ok + (long long)b * 2 * h, gap + b, nullptr, nullptr,
+                                in_up);
+}
+
+// G[n] += y[n] * sum_q dA[q] K[ws[q], n].  A workgroup owns 64 consecutive columns n; its 4 waves
+// split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into quarters, each lane
+// streams its column of those K rows (coalesced, 8 loads in flight), and the 4 partials are added
+// in a fixed order (deterministic).  Grid (N / 64, B): >= 128 workgroups at N = 8192.
 __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
                                                             const float* __restrict__ dA, const bool* __restrict__ ok,
                                                             const float* __restrict__ y, float* __restrict__ G, int N,
@@ -963,17 +1039,49 @@ void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* g
   AV_HIP_CHECK(hipGetLastError());
 }
 
+// parts of 2048 / 4096 / 8192 rows: the smallest whose candidates (parts x h per side) fit a
+// 512-thread merge, else a 1024-thread one
+static int select_part_per(int N, int h) {
+  for (int cap : {512, SEL_T})
+    for (int per = 2; per <= 8; per *= 2) {
+      const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
+      if (parts * h <= cap) return per;
+    }
+  return 0;
+}
+
+int smo_ws_select_parts(int N) {
+  const int per = select_part_per(N, 64);
+  return per ? (N + per * SEL_T - 1) / (per * SEL_T) : 1;
+}
+
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
-                   long long* ws, bool* ok, float* gap, hipStream_t stream) {
+                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, hipStream_t stream) {
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
-  const int per = (N + SEL_T - 1) / SEL_T;
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
-  if (per <= 4) smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
-  else if (per <= 8) smo_ws_select2_kernel<8><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
-  else if (per <= 16) smo_ws_select2_kernel<16><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
-  else if (per <= 32) smo_ws_select2_kernel<32><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
-  else smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  const int per = select_part_per(N, 64);
+  if (N <= 4 * SEL_T) {
+    smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  } else if (cand && per) {
+    // two levels: parts on separate CUs, then one merge over <= parts x h candidates per side
+    const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
+    const dim3 pg(parts, B);
+    if (per == 2) smo_ws_select_part_kernel<2><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt);
+    else if (per == 4) smo_ws_select_part_kernel<4><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt);
+    else smo_ws_select_part_kernel<8><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt);
+    AV_HIP_CHECK(hipGetLastError());
+    const int m = parts * h;
+    if (m <= 256)
+      smo_ws_select_merge_kernel<256><<<B, 256, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap);
+    else if (m <= 512)
+      smo_ws_select_merge_kernel<512><<<B, 512, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap);
+    else
+      smo_ws_select_merge_kernel<1024><<<B, 1024, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok,
+                                                                 gap);
+  } else {
+    smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+  }
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -285,7 +285,7 @@ def test_smo_working_set_gpu_matches_full(cuda, N):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [40, 1000, 5000, 12000, 70000])
+@pytest.mark.parametrize("N", [40, 1000, 5000, 12000, 40000, 70000])
 def test_smo_ws_select_matches_topk(cuda, N):
     """Fused working-set selection == gap + top-h up / low violator sets of the torch path."""
     from avenir_amd import _native
