@@ -55,7 +55,10 @@ __device__ __forceinline__ unsigned byte_of(const uint2& v, int j) {
   return ((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xFFu;
 }
 
-// histogram of chunks: hist[slot][c][TB] += w for every (feature bin) + the node total at TB-1
+// histogram of chunks: hist[slot][c][TB] += w for every (feature bin) + the node total at TB-1.
+// The node total is NOT a per-row atomic (every row of a class hit the same LDS word: the main
+// source of LDS conflicts): feature 0's missing codes go to the TB-1 word, and at the flush each
+// class adds its feature-0 bins to it (every counted row is in exactly one of those words).
 __global__ __launch_bounds__(FB_THREADS) void forest_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, const uint8_t* __restrict__ lab, const uint8_t* __restrict__ wt,
     const int* __restrict__ item_slot, const long long* __restrict__ item_start, const int* __restrict__ item_len,
@@ -82,18 +85,30 @@ __global__ __launch_bounds__(FB_THREADS) void forest_hist_kernel(
       if (c8[j] >= (unsigned)C || w8[j] == 0) m &= ~(1u << j);
     }
     if (!m) continue;
+    if (nfeat == 0) {
 #pragma unroll
-    for (int j = 0; j < RPT; ++j)
-      if (m >> j & 1) atomicAdd(&s_h[c8[j] * TB + TB - 1], w8[j]);
+      for (int j = 0; j < RPT; ++j)
+        if (m >> j & 1) atomicAdd(&s_h[c8[j] * TB + TB - 1], w8[j]);
+    }
     for (int f = 0; f < nfeat; ++f) {
       const uint2 cv = *reinterpret_cast<const uint2*>(codes + (long long)f * ld + r0);
       const unsigned B = (unsigned)bins[f], o = (unsigned)offs[f];
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
         const unsigned v = byte_of(cv, j);
-        if ((m >> j & 1) && v < B) atomicAdd(&s_h[c8[j] * TB + o + v], w8[j]);
+        if (m >> j & 1) {
+          if (v < B) atomicAdd(&s_h[c8[j] * TB + o + v], w8[j]);
+          else if (f == 0) atomicAdd(&s_h[c8[j] * TB + TB - 1], w8[j]);  // missing: total word
+        }
       }
     }
+  }
+  __syncthreads();
+  if (nfeat > 0 && threadIdx.x < C) {  // node total = feature 0's bins + its missing rows
+    const int c = threadIdx.x, B0 = bins[0], o0 = offs[0];
+    unsigned t = s_h[c * TB + TB - 1];
+    for (int v = 0; v < B0; ++v) t += s_h[c * TB + o0 + v];
+    s_h[c * TB + TB - 1] = t;
   }
   __syncthreads();
   unsigned long long* dst = hist + (long long)item_slot[item] * per;

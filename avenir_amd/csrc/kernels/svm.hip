@@ -177,11 +177,17 @@ __device__ __forceinline__ unsigned order_key(float f) {  // monotone float -> u
 }
 
 // Wave max of u32 keys: 4 DPP max steps + the 4 row results over v_readlane (uniform result).
+// (old = 0, bound_ctrl: 0 is the identity of an unsigned max, so the DPP move folds into
+// v_max_u32_dpp — no separate v_mov + wait state per step)
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_max_step(unsigned v) {
+  return max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
-  v = max(v, (unsigned)av::dpp_i<0xB1>((int)v));
-  v = max(v, (unsigned)av::dpp_i<0x4E>((int)v));
-  v = max(v, (unsigned)av::dpp_i<0x124>((int)v));
-  v = max(v, (unsigned)av::dpp_i<0x128>((int)v));
+  v = dpp_max_step<0xB1>(v);
+  v = dpp_max_step<0x4E>(v);
+  v = dpp_max_step<0x124>(v);
+  v = dpp_max_step<0x128>(v);
   const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0), b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
   const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
   return max(max(a, b), max(c, d));
@@ -210,7 +216,8 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
     unsigned ku = 0u;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const bool up = y[e] > 0.f ? a[e] < C : (y[e] < 0.f && a[e] > 0.f);
+      // branch-free set membership (bitwise on the compare masks: no exec-mask branches)
+      const bool up = ((y[e] > 0.f) & (a[e] < C)) | ((y[e] < 0.f) & (a[e] > 0.f));
       const unsigned kk = (order_key(-y[e] * g[e]) & ~0x7Fu) | (127u - (unsigned)(lane + 64 * e));
       ku = up ? max(ku, kk) : ku;
     }
@@ -228,14 +235,15 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int t = lane + 64 * e;
-      const bool low = y[e] > 0.f ? a[e] > 0.f : (y[e] < 0.f && a[e] < C);
+      const bool low = ((y[e] > 0.f) & (a[e] > 0.f)) | ((y[e] < 0.f) & (a[e] < C));
       const float yg = y[e] * g[e];
       const float bd = gmax + yg;
       float q = Kii + qd[e] - 2.f * Ks[i][t];
       q = q > 0.f ? q : TAU;
-      // selection only: the hardware reciprocal instead of an IEEE divide (the update keeps it)
+      // selection only: the hardware reciprocal instead of an IEEE divide; gain >= 0, so its raw
+      // bits already order like the value
       const float gain = bd * bd * __builtin_amdgcn_rcpf(q);
-      const unsigned kg = (order_key(gain) & ~0x7Fu) | (127u - (unsigned)t);
+      const unsigned kg = (__float_as_uint(gain) & ~0x7Fu) | (127u - (unsigned)t);
       kj = (low && bd > 0.f) ? max(kj, kg) : kj;
       km = low ? max(km, order_key(yg)) : km;
     }
@@ -252,8 +260,15 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
     const float oi = ai, oj = aj;
     float quad = Kii + Kjj - 2.f * Ks[i][j];
     quad = quad > 0.f ? quad : TAU;
+    // num / quad: hardware reciprocal + one residual correction (within an ulp of the IEEE
+    // quotient, 4 instructions instead of the 13-instruction divide sequence)
+    auto qdiv = [quad](float num) {
+      const float r = __builtin_amdgcn_rcpf(quad);
+      const float d0 = num * r;
+      return fmaf(r, fmaf(-quad, d0, num), d0);
+    };
     if (yi != yj) {
-      const float delta = (-gi_ - gj) / quad, diff = ai - aj;
+      const float delta = qdiv(-gi_ - gj), diff = ai - aj;
       ai += delta;
       aj += delta;
       if (diff > 0.f) { if (aj < 0.f) { aj = 0.f; ai = diff; } }
@@ -261,7 +276,7 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       if (diff > 0.f) { if (ai > C) { ai = C; aj = C - diff; } }
       else if (aj > C) { aj = C; ai = C + diff; }
     } else {
-      const float delta = (gi_ - gj) / quad, sum = ai + aj;
+      const float delta = qdiv(gi_ - gj), sum = ai + aj;
       ai -= delta;
       aj += delta;
       if (sum > C) { if (ai > C) { ai = C; aj = sum - C; } }
