@@ -231,6 +231,8 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
         rel_tol = float(os.environ.get("AVMI_SMO_REL_TOL", "0.3"))
     st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused, rel_tol)
     outer = 0
+    import os
+    graph = graph and os.environ.get("AVMI_SMO_GRAPH", "1") != "0"
     if st.gpu and graph:
         st.step()                                # eager warm-up: allocator pool, kernel caches
         outer = 1
