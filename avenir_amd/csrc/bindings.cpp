@@ -1361,7 +1361,7 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
   avk::smo_ws_select(alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)N,
                      (int)alpha.size(1), (float)C, (int)h, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()),
                      ok.data_ptr<bool>(), gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(),
-                     cur_stream(y));
+                     -INFINITY, cur_stream(y));
 }
 
 void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& ok, at::Tensor& alpha,
@@ -1415,7 +1415,46 @@ void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& 
   DevGuard g(y.device());
   avk::smo_ws_update(K.data_ptr<float>(), reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()),
                      dA.data_ptr<float>(), ok.data_ptr<bool>(), y.data_ptr<float>(), G.data_ptr<float>(), (int)B,
-                     (int)N, (int)G.size(1), (int)ws.size(1), cur_stream(y));
+                     (int)N, (int)G.size(1), (int)ws.size(1), nullptr, -INFINITY, cur_stream(y));
+}
+
+// The whole working-set solve in one call (avk::smo_ws_run): state tensors as in the per-step
+// bindings above; returns the number of outer steps enqueued.
+int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const at::Tensor& y, double C, double eps,
+                   int64_t inner_iter, double rel_tol, int64_t max_outer, int64_t check_every, at::Tensor& ws,
+                   at::Tensor& ok, at::Tensor& dA, at::Tensor& inner_total, at::Tensor& gap) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&K, &alpha, &G, &y, &gap, &dA}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
+  const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
+  TORCH_CHECK(N >= 1 && N <= (1 << 18), "1 <= N <= 2^18");
+  TORCH_CHECK(K.dim() == 3 && K.size(0) == B && K.size(1) == N && K.size(2) == N, "K must be [B, N, N]");
+  TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
+              "alpha / G must be [B, >= N]");
+  CHECK_DEV(ws);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DEV(ok);
+  CHECK_DTYPE(ok, at::kBool);
+  CHECK_DEV(inner_total);
+  CHECK_DTYPE(inner_total, at::kLong);
+  TORCH_CHECK(ws.numel() == B * Q && ok.numel() == B * Q && dA.numel() == B * Q, "ws / ok / dA must be [B, ", Q, "]");
+  TORCH_CHECK(gap.numel() == B && inner_total.numel() == B, "gap / inner_total must be [B]");
+  TORCH_CHECK(C > 0 && eps > 0 && inner_iter >= 0, "bad SMO parameters");
+  DevGuard g(y.device());
+  const int64_t parts = avk::smo_ws_select_parts((int)N);
+  auto cand = at::empty({B, parts, 2, Q / 2}, y.options().dtype(at::kInt));
+  auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
+  auto Kws = at::empty({B, Q, Q}, K.options());
+  auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
+  return avk::smo_ws_run(K.data_ptr<float>(), (int)N, alpha.data_ptr<float>(), G.data_ptr<float>(),
+                         y.data_ptr<float>(), (int)B, (int)alpha.size(1), (float)C, (float)eps, (int)inner_iter,
+                         (float)rel_tol, max_outer, (int)check_every,
+                         reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
+                         dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
+                         gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
+                         host_gap.data_ptr<float>(), cur_stream(y));
 }
 
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,
@@ -2769,6 +2808,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_ws_solve", &smo_ws_solve);
   m.def("smo_ws_select", &smo_ws_select);
   m.def("smo_ws_update", &smo_ws_update);
+  m.def("smo_ws_run", &smo_ws_run);
   m.def("smo_ws_solve_fused", &smo_ws_solve_fused, py::arg("K"), py::arg("ws"), py::arg("ok"), py::arg("alpha"),
         py::arg("G"), py::arg("y"), py::arg("gap"), py::arg("C"), py::arg("eps"), py::arg("max_iter"), py::arg("dA"),
         py::arg("inner_total"), py::arg("rel_tol") = 0.1);

@@ -171,6 +171,16 @@ __global__ __launch_bounds__(SMO_THREADS) void smo_kernel(const float* __restric
 //   tolerance is max(eps, 0.1 gap)).
 constexpr int WS_Q = 128;
 
+// Converged-problem early exit shared by every kernel of an outer step: once the violation gap of
+// problem b (written by the previous step's selection) is below the stopping tolerance, that step's
+// sub-problem solve took zero iterations (its local violation <= gap < eps) and changed nothing, so
+// the selection, gather, solve and update of every later step are no-ops and return at once.  This
+// lets the host queue steps ahead of the convergence test (smo_ws_run) at ~no cost.
+// (skip = -inf disables it; a NaN gap counts as converged, as in the host test.)
+__device__ __forceinline__ bool ws_done(const float* gap, int b, float skip) {
+  return gap != nullptr && skip > -INFINITY && !(gap[b] >= skip);
+}
+
 __device__ __forceinline__ unsigned order_key(float f) {  // monotone float -> uint
   const unsigned u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -232,13 +242,15 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       if (e == si) { yi = rdl(y[e], i & 63); ai = rdl(a[e], i & 63); gi_ = rdl(g[e], i & 63); Kii = rdl(qd[e], i & 63); }
     const float gmax = -yi * gi_;
     unsigned kj = 0u, km = 0u;
+    float kit[E];  // row i of the block, kept for K[i][j] (a readlane) and the gradient update
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int t = lane + 64 * e;
+      kit[e] = Ks[i][t];
       const bool low = ((y[e] > 0.f) & (a[e] > 0.f)) | ((y[e] < 0.f) & (a[e] < C));
       const float yg = y[e] * g[e];
       const float bd = gmax + yg;
-      float q = Kii + qd[e] - 2.f * Ks[i][t];
+      float q = Kii + qd[e] - 2.f * kit[e];
       q = q > 0.f ? q : TAU;
       // selection only: the hardware reciprocal instead of an IEEE divide; gain >= 0, so its raw
       // bits already order like the value
@@ -258,7 +270,11 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
     for (int e = 0; e < E; ++e)
       if (e == sj) { yj = rdl(y[e], j & 63); aj = rdl(a[e], j & 63); gj = rdl(g[e], j & 63); Kjj = rdl(qd[e], j & 63); }
     const float oi = ai, oj = aj;
-    float quad = Kii + Kjj - 2.f * Ks[i][j];
+    float kij = 0.f;  // K[i][j] from the owner lane of the cached row (no LDS round trip)
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (e == sj) kij = rdl(kit[e], j & 63);
+    float quad = Kii + Kjj - 2.f * kij;
     quad = quad > 0.f ? quad : TAU;
     // num / quad: hardware reciprocal + one residual correction (within an ulp of the IEEE
     // quotient, 4 instructions instead of the 13-instruction divide sequence)
@@ -267,22 +283,27 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       const float d0 = num * r;
       return fmaf(r, fmaf(-quad, d0, num), d0);
     };
-    if (yi != yj) {
-      const float delta = qdiv(-gi_ - gj), diff = ai - aj;
-      ai += delta;
-      aj += delta;
-      if (diff > 0.f) { if (aj < 0.f) { aj = 0.f; ai = diff; } }
-      else if (ai < 0.f) { ai = 0.f; aj = -diff; }
-      if (diff > 0.f) { if (ai > C) { ai = C; aj = C - diff; } }
-      else if (aj > C) { aj = C; ai = C + diff; }
-    } else {
-      const float delta = qdiv(gi_ - gj), sum = ai + aj;
-      ai -= delta;
-      aj += delta;
-      if (sum > C) { if (ai > C) { ai = C; aj = sum - C; } }
-      else if (aj < 0.f) { aj = 0.f; ai = sum; }
-      if (sum > C) { if (aj > C) { aj = C; ai = sum - C; } }
-      else if (ai < 0.f) { ai = 0.f; aj = sum; }
+    // LIBSVM's two-variable update and box clipping, both label cases evaluated with selects
+    // (wave-uniform values: no branches in the dependent chain)
+    const bool opp = yi != yj;
+    const float delta = qdiv(opp ? -gi_ - gj : gi_ - gj);
+    {
+      // opposite labels: ai - aj = diff is kept; same labels: ai + aj = sum is kept
+      const float diff = ai - aj, sum = ai + aj;
+      float pi = opp ? ai + delta : ai - delta, pj = aj + delta;
+      // first clip
+      const bool dpos = diff > 0.f, spos = sum > C;
+      const bool c1 = opp ? (dpos ? pj < 0.f : pi < 0.f) : (spos ? pi > C : pj < 0.f);
+      const float ci = opp ? (dpos ? diff : 0.f) : (spos ? C : sum);
+      const float cj = opp ? (dpos ? 0.f : -diff) : (spos ? sum - C : 0.f);
+      pi = c1 ? ci : pi;
+      pj = c1 ? cj : pj;
+      // second clip
+      const bool c2 = opp ? (dpos ? pi > C : pj > C) : (spos ? pj > C : pi < 0.f);
+      const float di_ = opp ? (dpos ? C : C + diff) : (spos ? sum - C : 0.f);
+      const float dj_ = opp ? (dpos ? C - diff : C) : (spos ? C : sum);
+      ai = c2 ? di_ : pi;
+      aj = c2 ? dj_ : pj;
     }
     const float di = (ai - oi) * yi, dj = (aj - oj) * yj;
 #pragma unroll
@@ -290,7 +311,7 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       const int t = lane + 64 * e;
       if (t == i) a[e] = ai;
       if (t == j) a[e] = aj;
-      g[e] += y[e] * (Ks[i][t] * di + Ks[j][t] * dj);
+      g[e] += y[e] * (kit[e] * di + Ks[j][t] * dj);
     }
   }
   return it;
@@ -395,9 +416,11 @@ __global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float
 // workgroups (all CUs) instead of being issued by the one CU that then solves.
 __global__ __launch_bounds__(WS_Q) void smo_ws_gather_kernel(const float* __restrict__ K, int N,
                                                              const long long* __restrict__ ws,
-                                                             const bool* __restrict__ ok, float* __restrict__ Kws) {
+                                                             const bool* __restrict__ ok, float* __restrict__ Kws,
+                                                             const float* __restrict__ gap, float skip) {
   constexpr int Q = WS_Q;
   const int b = blockIdx.y, p = blockIdx.x, q = threadIdx.x;
+  if (ws_done(gap, b, skip)) return;
   const long long* wb = ws + (long long)b * Q;
   const bool* ob = ok + (long long)b * Q;
   const long long rp = ob[p] ? wb[p] : 0, cq = ob[q] ? wb[q] : 0;  // < N (select writes n < N)
@@ -417,6 +440,10 @@ __global__ __launch_bounds__(WSS_T) void smo_ws_solve_kernel(const float* __rest
   constexpr int Q = WS_Q, E = Q / 64;
   __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
   const int b = blockIdx.x, lane = threadIdx.x;
+  if (ws_done(gap, b, eps)) {  // converged: zero iterations, alpha unchanged, dA = 0
+    for (int t = threadIdx.x; t < Q; t += WSS_T) dA[(long long)b * Q + t] = 0.f;
+    return;
+  }
   const float4* src = reinterpret_cast<const float4*>(Kws + (long long)b * Q * Q);
   float4* dst = reinterpret_cast<float4*>(&Ks[0][0]);
 #pragma unroll 4
@@ -477,6 +504,7 @@ __device__ __forceinline__ float ws_violation(int which, float y, float a, float
 }
 
 
+
 template <typename T, typename Op>
 __device__ T block_reduce(T v, T* red, Op op) {  // all SEL_T threads; red has >= 17 slots
   constexpr int NW = SEL_T / 64;
@@ -505,7 +533,8 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
                                                               const float* __restrict__ G,
                                                               const float* __restrict__ y, int N, int ldag, float C,
                                                               int h, long long* __restrict__ ws,
-                                                              bool* __restrict__ ok, float* __restrict__ gap) {
+                                                              bool* __restrict__ ok, float* __restrict__ gap,
+                                                              float skip) {
   extern __shared__ unsigned in_up[];  // [(N + 31) / 32] bitmap of the selected up set
   __shared__ unsigned hist[256];
   __shared__ float redf[17];
@@ -514,6 +543,7 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_kernel(const float* __res
   __shared__ int pick[2][64];
   __shared__ unsigned wcnt[PER > 0 ? PER : 1][SEL_T / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
+  if (ws_done(gap, b, skip)) return;
   const float* ab = alpha + (long long)b * ldag;
   const float* gb = G + (long long)b * ldag;
   const float* yb = y + (long long)b * N;
@@ -943,9 +973,11 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select2_kernel(const float* __re
                                                                const float* __restrict__ G,
                                                                const float* __restrict__ y, int N, int ldag, float C,
                                                                int h, long long* __restrict__ ws,
-                                                               bool* __restrict__ ok, float* __restrict__ gap) {
+                                                               bool* __restrict__ ok, float* __restrict__ gap,
+                                                               float skip) {
   extern __shared__ unsigned in_up[];
   const int b = blockIdx.x;
+  if (ws_done(gap, b, skip)) return;
   ws_select2_body<PER, false, SEL_T>(RangeSrc{0, N}, alpha + (long long)b * ldag, G + (long long)b * ldag,
                                      y + (long long)b * N, N, C, h, ws + (long long)b * 2 * h,
                                      ok + (long long)b * 2 * h, gap + b, nullptr, nullptr, in_up);
@@ -957,8 +989,10 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_part_kernel(const float* 
                                                                    const float* __restrict__ G,
                                                                    const float* __restrict__ y, int N, int ldag,
                                                                    float C, int h, int parts, int* __restrict__ cand,
-                                                                   int* __restrict__ cnt) {
+                                                                   int* __restrict__ cnt, const float* __restrict__ gap,
+                                                                   float skip) {
   const int b = blockIdx.y, p = blockIdx.x;
+  if (ws_done(gap, b, skip)) return;
   const int n0 = p * PER * SEL_T, n1 = min(N, n0 + PER * SEL_T);
   ws_select2_body<PER, true, SEL_T>(RangeSrc{n0, n1}, alpha + (long long)b * ldag, G + (long long)b * ldag,
                                     y + (long long)b * N, N, C, h, nullptr, nullptr, nullptr,
@@ -974,9 +1008,10 @@ __global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __
                                                                  int h, int parts, const int* __restrict__ cand,
                                                                  const int* __restrict__ cnt,
                                                                  long long* __restrict__ ws, bool* __restrict__ ok,
-                                                                 float* __restrict__ gap) {
+                                                                 float* __restrict__ gap, float skip) {
   extern __shared__ unsigned in_up[];
   const int b = blockIdx.x;
+  if (ws_done(gap, b, skip)) return;  // every thread reads gap[b] before thread 0 rewrites it (after a barrier)
   const CandSrc src{cand + (long long)b * parts * 2 * h, cnt + (long long)b * parts * 2, parts, h};
   ws_select2_body<1, false, NT>(src, alpha + (long long)b * ldag, G + (long long)b * ldag, y + (long long)b * N, N, C,
                                 h, ws + (long long)b * 2 * h, ok + (long long)b * 2 * h, gap + b, nullptr, nullptr,
@@ -990,12 +1025,13 @@ __global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __
 __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
                                                             const float* __restrict__ dA, const bool* __restrict__ ok,
                                                             const float* __restrict__ y, float* __restrict__ G, int N,
-                                                            int ldag, int Q) {
+                                                            int ldag, int Q, const float* __restrict__ gap, float skip) {
   __shared__ long long s_ws[WS_Q];
   __shared__ float s_d[WS_Q];
   __shared__ float red[4][64];
   __shared__ int s_cnt;
   const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (ws_done(gap, b, skip)) return;
   if (w == 0) {
     int base = 0;
     for (int q0 = 0; q0 < Q; q0 += 64) {
@@ -1071,39 +1107,41 @@ int smo_ws_select_parts(int N) {
 }
 
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
-                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, hipStream_t stream) {
+                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream) {
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
   if (N <= 4 * SEL_T) {
-    smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+    smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap, skip);
   } else if (cand && per) {
     // two levels: parts on separate CUs, then one merge over <= parts x h candidates per side
     const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
     const dim3 pg(parts, B);
-    if (per == 2) smo_ws_select_part_kernel<2><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt);
-    else if (per == 4) smo_ws_select_part_kernel<4><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt);
-    else smo_ws_select_part_kernel<8><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt);
+    if (per == 2) smo_ws_select_part_kernel<2><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, gap, skip);
+    else if (per == 4) smo_ws_select_part_kernel<4><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, gap, skip);
+    else smo_ws_select_part_kernel<8><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, gap, skip);
     AV_HIP_CHECK(hipGetLastError());
     const int m = parts * h;
     if (m <= 256)
-      smo_ws_select_merge_kernel<256><<<B, 256, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap);
+      smo_ws_select_merge_kernel<256><<<B, 256, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap,
+                                                                skip);
     else if (m <= 512)
-      smo_ws_select_merge_kernel<512><<<B, 512, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap);
+      smo_ws_select_merge_kernel<512><<<B, 512, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap,
+                                                                skip);
     else
       smo_ws_select_merge_kernel<1024><<<B, 1024, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok,
-                                                                 gap);
+                                                                 gap, skip);
   } else {
-    smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap);
+    smo_ws_select_kernel<0><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap, skip);
   }
   AV_HIP_CHECK(hipGetLastError());
 }
 
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
-                   int B, int N, int ldag, int Q, hipStream_t stream) {
+                   int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream) {
   if (B <= 0 || N <= 0) return;
-  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q);
+  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q, gap, skip);
   AV_HIP_CHECK(hipGetLastError());
 }
 
@@ -1112,7 +1150,7 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
                         long long* inner_total, float* Kws, float rel_tol, hipStream_t stream) {
   if (B <= 0) return;
   if (Kws) {  // spread gather (Q x B workgroups) + one-wave solve
-    smo_ws_gather_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(K, N, ws, ok, Kws);
+    smo_ws_gather_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(K, N, ws, ok, Kws, gap, eps);
     AV_HIP_CHECK(hipGetLastError());
     smo_ws_solve_kernel<<<B, WSS_T, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, rel_tol, max_iter,
                                                  dA, inner_total);
@@ -1121,6 +1159,48 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
                                                          inner_total);
   }
   AV_HIP_CHECK(hipGetLastError());
+}
+
+// The whole working-set solve driven from the host without Python or graph capture: blocks of
+// `check_every` outer steps (select, gather, solve, update = 5 launches each, ~25 us of host time
+// against ~65 us of GPU time per step, so the queue never drains) are enqueued back to back; after
+// each block the gaps are copied into pinned host memory behind an event, and the host tests the
+// PREVIOUS block's gaps while the current one runs.  Steps queued past convergence are no-ops
+// (ws_done), so the one-block look-behind costs a few microseconds of empty launches instead of a
+// pipeline drain per test.  Returns the number of outer steps enqueued.
+long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
+                     float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
+                     bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
+                     float* host_gap, hipStream_t stream) {
+  if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
+  const int Q = WS_Q, h = WS_Q / 2;
+  check_every = check_every < 1 ? 1 : check_every;
+  hipEvent_t ev[2];
+  for (auto& e : ev) AV_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  long long outer = 0;
+  for (long long blk = 0; outer < max_outer; ++blk) {
+    const long long n = std::min<long long>(check_every, max_outer - outer);
+    for (long long s = 0; s < n; ++s) {
+      smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream);
+      smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws, rel_tol,
+                         stream);
+      smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);
+    }
+    outer += n;
+    float* hg = host_gap + (blk & 1) * B;
+    AV_HIP_CHECK(hipMemcpyAsync(hg, gap, sizeof(float) * B, hipMemcpyDeviceToHost, stream));
+    AV_HIP_CHECK(hipEventRecord(ev[blk & 1], stream));
+    if (blk >= 1) {
+      AV_HIP_CHECK(hipEventSynchronize(ev[(blk - 1) & 1]));
+      const float* pg = host_gap + ((blk - 1) & 1) * B;
+      bool done = true;
+      for (int b = 0; b < B; ++b) done = done && !(pg[b] >= eps);
+      if (done) break;
+    }
+  }
+  AV_HIP_CHECK(hipStreamSynchronize(stream));
+  for (auto& e : ev) AV_HIP_CHECK(hipEventDestroy(e));
+  return outer;
 }
 
 }  // namespace avk

@@ -218,10 +218,12 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     "low" set (the maximal violating pair is always among them), solves that Q-variable
     sub-problem to a relaxed tolerance max(eps, 0.1 gap) — on the GPU in ``smo_ws_kernel``, one
     wavefront per problem with the Q x Q kernel block in LDS — and applies the alpha changes to
-    the full gradient with one batched GEMV.  On the GPU ``check_every`` steps are one captured
-    HIP graph (static shapes; steps after convergence are no-ops because the sub-problem solver
-    stops at once), and the host reads the global violation gap once per replay.  Stops when
-    the gap < eps.  ``fused`` (GPU, float32 K, N <= 2^18): the working-set selection and the
+    the full gradient with one batched GEMV.  On the GPU with the fused kernels the whole loop runs
+    in C++ (``smo_ws_run``: blocks of 8 steps queued back to back, the gap of the previous block
+    tested while the next one runs, steps past convergence are no-op launches); otherwise (or with
+    AVMI_SMO_LOOP=graph) ``check_every`` steps are one captured HIP graph (static shapes; steps
+    after convergence are no-ops because the sub-problem solver stops at once), and the host reads
+    the global violation gap once per replay.  Stops when the gap < eps.  ``fused`` (GPU, float32 K, N <= 2^18): the working-set selection and the
     gradient update are one kernel each (``smo_ws_select`` / ``smo_ws_update``) instead of ~25
     torch ops.  Returns (alpha, G, outer steps, inner steps).
     """
@@ -232,8 +234,14 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused, rel_tol)
     outer = 0
     import os
-    graph = graph and os.environ.get("AVMI_SMO_GRAPH", "1") != "0"
-    if st.gpu and graph:
+    mode = os.environ.get("AVMI_SMO_LOOP", "native")   # native | graph | eager
+    if st.fused and graph and mode == "native":
+        # the step loop in C++ (smo_ws_run): no capture, no per-step Python; queued steps past
+        # convergence are no-op launches
+        outer = int(_native.C().smo_ws_run(K, st.alpha, st.G, st.yf, st.C, st.eps, st.inner_iter, st.rel_tol,
+                                           int(max_outer), 8, st.ws_buf, st.ok_buf, st.dA_buf, st.inner_total,
+                                           st.gap))
+    elif st.gpu and graph and mode != "eager":
         st.step()                                # eager warm-up: allocator pool, kernel caches
         outer = 1
         s = torch.cuda.Stream()
