@@ -646,8 +646,10 @@ class DataExplorer:
         return {"stat": u, "pvalue": p}
 
     def testTwoSampleWilcox(self, ds1, ds2, sigLev=0.05):
-        from scipy import stats
-        return self._two(stats.wilcoxon, ds1, ds2)
+        """Signed-rank statistic from device ranks of |x - y| (K26 rank_avg), scipy's formulas."""
+        from ..ops.stats_ops import wilcoxon_signed_rank
+        w, p = wilcoxon_signed_rank(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": w, "pvalue": p}
 
     def testTwoSampleKw(self, ds1, ds2, sigLev=0.05):
         from ..ops.stats_ops import kruskal_h
@@ -664,9 +666,10 @@ class DataExplorer:
         return self._two(stats.epps_singleton_2samp, ds1, ds2)
 
     def testTwoSampleAnderson(self, ds1, ds2, sigLev=0.05):
-        from scipy import stats
-        r = stats.anderson_ksamp([_np(self.getNumericData(ds1)), _np(self.getNumericData(ds2))])
-        return {"stat": float(r.statistic), "pvalue": float(r.significance_level)}
+        """k-sample Anderson-Darling (midrank) with the A2 sums on the samples' device."""
+        from ..ops.stats_ops import anderson_ksamp
+        a2, _, p = anderson_ksamp(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": a2, "pvalue": p}
 
     def testTwoSampleScaleAb(self, ds1, ds2, sigLev=0.05):
         from scipy import stats
@@ -694,9 +697,10 @@ class DataExplorer:
         return {"stat": float(r[0]), "pvalue": float(r[1])}
 
     def testTwoSampleCvm(self, ds1, ds2, sigLev=0.05):
-        from scipy import stats
-        r = stats.cramervonmises_2samp(_np(self.getNumericData(ds1)), _np(self.getNumericData(ds2)))
-        return {"stat": float(r.statistic), "pvalue": float(r.pvalue)}
+        """Two-sample Cramer-von Mises from device pooled ranks (K26 rank_avg)."""
+        from ..ops.stats_ops import cvm_2samp
+        t, p = cvm_2samp(self.getNumericData(ds1), self.getNumericData(ds2))
+        return {"stat": t, "pvalue": p}
 
     # Zhang (2002, 2006) likelihood-ratio EDF tests with device permutation p-values
     def _zhang(self, ds1, ds2, kind: str, nperm: int = 500, seed: int = 0):

@@ -1361,7 +1361,7 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
   avk::smo_ws_select(alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)N,
                      (int)alpha.size(1), (float)C, (int)h, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()),
                      ok.data_ptr<bool>(), gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(),
-                     -INFINITY, cur_stream(y));
+                     -INFINITY, nullptr, cur_stream(y));
 }
 
 void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& ok, at::Tensor& alpha,
@@ -1418,6 +1418,23 @@ void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& 
                      (int)N, (int)G.size(1), (int)ws.size(1), nullptr, -INFINITY, cur_stream(y));
 }
 
+// exp(-gamma |a_i - b_j|^2) [na, nb] float32 in one pass (d <= 64)
+at::Tensor rbf_matrix(const at::Tensor& A, const at::Tensor& B, double gamma) {
+  CHECK_DEV(A);
+  CHECK_DEV(B);
+  CHECK_DTYPE(A, at::kFloat);
+  CHECK_DTYPE(B, at::kFloat);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1) && A.size(1) >= 1 && A.size(1) <= 64,
+              "A [na, d], B [nb, d], 1 <= d <= 64");
+  TORCH_CHECK(A.size(0) < (1LL << 31) / 64 && B.size(0) < (1LL << 31) / 64, "too many rows");
+  DevGuard g(A.device());
+  const auto Ac = A.contiguous(), Bc = B.contiguous();
+  auto K = at::empty({A.size(0), B.size(0)}, A.options());
+  avk::rbf_matrix(Ac.data_ptr<float>(), Bc.data_ptr<float>(), (int)A.size(0), (int)B.size(0), (int)A.size(1),
+                  (float)gamma, K.data_ptr<float>(), cur_stream(A));
+  return K;
+}
+
 // The whole working-set solve in one call (avk::smo_ws_run): state tensors as in the per-step
 // bindings above; returns the number of outer steps enqueued.
 int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const at::Tensor& y, double C, double eps,
@@ -1448,13 +1465,15 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
   auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
   auto Kws = at::empty({B, Q, Q}, K.options());
   auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
+  auto ticket = at::zeros({B}, y.options().dtype(at::kInt));  // fused two-level selection (zeroed once)
   return avk::smo_ws_run(K.data_ptr<float>(), (int)N, alpha.data_ptr<float>(), G.data_ptr<float>(),
                          y.data_ptr<float>(), (int)B, (int)alpha.size(1), (float)C, (float)eps, (int)inner_iter,
                          (float)rel_tol, max_outer, (int)check_every,
                          reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
                          gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
-                         host_gap.data_ptr<float>(), cur_stream(y));
+                         host_gap.data_ptr<float>(), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()),
+                         cur_stream(y));
 }
 
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,
@@ -2809,6 +2828,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_ws_select", &smo_ws_select);
   m.def("smo_ws_update", &smo_ws_update);
   m.def("smo_ws_run", &smo_ws_run);
+  m.def("rbf_matrix", &rbf_matrix);
   m.def("smo_ws_solve_fused", &smo_ws_solve_fused, py::arg("K"), py::arg("ws"), py::arg("ok"), py::arg("alpha"),
         py::arg("G"), py::arg("y"), py::arg("gap"), py::arg("C"), py::arg("eps"), py::arg("max_iter"), py::arg("dA"),
         py::arg("inner_total"), py::arg("rel_tol") = 0.1);

@@ -203,6 +203,22 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
   return max(max(a, b), max(c, d));
 }
 
+// two independent wave maxima with their DPP steps interleaved (each step's VGPR hazard is covered by
+// the other chain's instruction instead of an s_nop)
+__device__ __forceinline__ void wave_max2_u32(unsigned& u, unsigned& v) {
+  u = dpp_max_step<0xB1>(u);
+  v = dpp_max_step<0xB1>(v);
+  u = dpp_max_step<0x4E>(u);
+  v = dpp_max_step<0x4E>(v);
+  u = dpp_max_step<0x124>(u);
+  v = dpp_max_step<0x124>(v);
+  u = dpp_max_step<0x128>(u);
+  v = dpp_max_step<0x128>(v);
+  auto rl = [](unsigned x, int l) { return (unsigned)__builtin_amdgcn_readlane((int)x, l); };
+  u = max(max(rl(u, 0), rl(u, 16)), max(rl(u, 32), rl(u, 48)));
+  v = max(max(rl(v, 0), rl(v, 16)), max(rl(v, 32), rl(v, 48)));
+}
+
 __device__ __forceinline__ float order_key_inv(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
@@ -259,8 +275,7 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       kj = (low && bd > 0.f) ? max(kj, kg) : kj;
       km = low ? max(km, order_key(yg)) : km;
     }
-    kj = wave_max_u32(kj);
-    km = wave_max_u32(km);
+    wave_max2_u32(kj, km);
     const float gmax2 = km ? order_key_inv(km) : -INFINITY;
     if (gmax + gmax2 < epsl || kj == 0u) break;
     const int j = 127 - (int)(kj & 0x7Fu);
@@ -444,25 +459,29 @@ __global__ __launch_bounds__(WSS_T) void smo_ws_solve_kernel(const float* __rest
     for (int t = threadIdx.x; t < Q; t += WSS_T) dA[(long long)b * Q + t] = 0.f;
     return;
   }
+  // wave 0's working-set state (dependent ws -> y / alpha / G loads) is issued BEFORE the block
+  // staging so that its latency overlaps the copy
+  float y[E], a[E], g[E], qd[E], a0[E];
+  bool okv[E];
+  long long wsv[E];
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int t = lane + 64 * e;
+      okv[e] = ok[(long long)b * Q + t];
+      wsv[e] = okv[e] ? ws[(long long)b * Q + t] : 0;
+      y[e] = okv[e] ? yv[(long long)b * N + wsv[e]] : 0.f;
+      a[e] = alpha[(long long)b * ldag + wsv[e]];
+      g[e] = G[(long long)b * ldag + wsv[e]];
+      a0[e] = a[e];
+    }
+  }
   const float4* src = reinterpret_cast<const float4*>(Kws + (long long)b * Q * Q);
   float4* dst = reinterpret_cast<float4*>(&Ks[0][0]);
 #pragma unroll 4
   for (int e = threadIdx.x; e < Q * Q / 4; e += WSS_T) dst[e] = src[e];
   __syncthreads();
   if (threadIdx.x >= 64) return;  // wave 0 solves; no barrier follows
-  float y[E], a[E], g[E], qd[E], a0[E];
-  bool okv[E];
-  long long wsv[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int t = lane + 64 * e;
-    okv[e] = ok[(long long)b * Q + t];
-    wsv[e] = okv[e] ? ws[(long long)b * Q + t] : 0;
-    y[e] = okv[e] ? yv[(long long)b * N + wsv[e]] : 0.f;
-    a[e] = alpha[(long long)b * ldag + wsv[e]];
-    g[e] = G[(long long)b * ldag + wsv[e]];
-    a0[e] = a[e];
-  }
 #pragma unroll
   for (int e = 0; e < E; ++e) qd[e] = Ks[lane + 64 * e][lane + 64 * e];
   float gp = gap[b];
@@ -1000,6 +1019,42 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_part_kernel(const float* 
                                     nullptr);
 }
 
+// Both levels in ONE launch: every part selects its local candidates as above, and the LAST part
+// workgroup of a problem to finish (a ticket counter; each part publishes its candidates with a
+// device-scope fence first, so the other XCDs' L2 lines are written back before the ticket moves)
+// runs the merge over all parts' candidates and re-arms the ticket.  No workgroup waits on another
+// (no spinning, any residency), and the merge launch with its dispatch gap per outer step is gone.
+template <int PER>
+__global__ __launch_bounds__(SEL_T) void smo_ws_select_fused_kernel(const float* __restrict__ alpha,
+                                                                    const float* __restrict__ G,
+                                                                    const float* __restrict__ y, int N, int ldag,
+                                                                    float C, int h, int parts, int* __restrict__ cand,
+                                                                    int* __restrict__ cnt, long long* __restrict__ ws,
+                                                                    bool* __restrict__ ok, float* __restrict__ gap,
+                                                                    float skip, unsigned* __restrict__ ticket) {
+  extern __shared__ unsigned in_up[];
+  __shared__ int s_last;
+  const int b = blockIdx.y, p = blockIdx.x;
+  if (ws_done(gap, b, skip)) return;  // block-uniform; every part of problem b returns alike
+  const int n0 = p * PER * SEL_T, n1 = min(N, n0 + PER * SEL_T);
+  int* cb = cand + (long long)b * parts * 2 * h;
+  int* nb = cnt + (long long)b * parts * 2;
+  ws_select2_body<PER, true, SEL_T>(RangeSrc{n0, n1}, alpha + (long long)b * ldag, G + (long long)b * ldag,
+                                    y + (long long)b * N, N, C, h, nullptr, nullptr, nullptr, cb + p * 2 * h,
+                                    nb + p * 2, nullptr);
+  __threadfence();  // release this part's candidates
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&ticket[b], 1u) == (unsigned)(parts - 1);
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // acquire the other parts' candidates
+  const CandSrc src{cb, nb, parts, h};
+  ws_select2_body<1, false, SEL_T>(src, alpha + (long long)b * ldag, G + (long long)b * ldag, y + (long long)b * N, N,
+                                   C, h, ws + (long long)b * 2 * h, ok + (long long)b * 2 * h, gap + b, nullptr,
+                                   nullptr, in_up);
+  if (threadIdx.x == 0) atomicExch(&ticket[b], 0u);  // re-arm for the next outer step
+}
+
 // merge: one workgroup of NT >= parts * h threads over the concatenated candidates
 template <int NT>
 __global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __restrict__ alpha,
@@ -1070,9 +1125,73 @@ __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restr
     G[(long long)b * ldag + n] += y[(long long)b * N + n] * (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
 }
 
+// RBF kernel matrix K[i][j] = exp(-gamma * |a_i - b_j|^2) in ONE pass for d <= 64: a 64 x 64
+// output tile per workgroup, the 64 rows of A and of B staged in LDS (zero-padded to DP), each of the
+// 256 threads computes a 4 x 4 block from the squared DIFFERENCES (no |a|^2 + |b|^2 - 2ab
+// cancellation) and writes it as 4 row segments (16 threads x 16 B contiguous per row).  The
+// GEMM + five elementwise passes of the tensor formula become one write-bound pass (N = 32 768:
+// 4 GB written once instead of ~14 passes over 4 GB temporaries).
+template <int DP>
+__global__ __launch_bounds__(256) void rbf_matrix_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                         int na, int nb, int d, float gamma, float* __restrict__ K) {
+  __shared__ float sa[64][DP + 1], sb[64][DP + 1];
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64, tid = threadIdx.x;
+  for (int e = tid; e < 64 * DP; e += 256) {
+    const int r = e / DP, k = e % DP;
+    sa[r][k] = (i0 + r < na && k < d) ? A[(long long)(i0 + r) * d + k] : 0.f;
+    sb[r][k] = (j0 + r < nb && k < d) ? B[(long long)(j0 + r) * d + k] : 0.f;
+  }
+  __syncthreads();
+  const int tx = tid & 15, ty = tid >> 4;
+  float acc[4][4] = {};
+#pragma unroll 4
+  for (int k = 0; k < DP; ++k) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) av[r] = sa[ty * 4 + r][k];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bv[c] = sb[tx * 4 + c][k];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float df = av[r] - bv[c];
+        acc[r][c] = fmaf(df, df, acc[r][c]);
+      }
+  }
+  const int jc = j0 + tx * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + ty * 4 + r;
+    if (i >= na) continue;
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = expf(-gamma * acc[r][c]);
+    float* dst = K + (long long)i * nb + jc;
+    if ((nb & 3) == 0 && jc + 3 < nb) {
+      *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (jc + c < nb) dst[c] = o[c];
+    }
+  }
+}
+
 }  // namespace
 
 namespace avk {
+
+void rbf_matrix(const float* A, const float* B, int na, int nb, int d, float gamma, float* K, hipStream_t stream) {
+  if (na <= 0 || nb <= 0) return;
+  const dim3 grid((nb + 63) / 64, (na + 63) / 64);
+  if (d <= 8) rbf_matrix_kernel<8><<<grid, 256, 0, stream>>>(A, B, na, nb, d, gamma, K);
+  else if (d <= 16) rbf_matrix_kernel<16><<<grid, 256, 0, stream>>>(A, B, na, nb, d, gamma, K);
+  else if (d <= 32) rbf_matrix_kernel<32><<<grid, 256, 0, stream>>>(A, B, na, nb, d, gamma, K);
+  else if (d <= 64) rbf_matrix_kernel<64><<<grid, 256, 0, stream>>>(A, B, na, nb, d, gamma, K);
+  else throw std::runtime_error("rbf_matrix: d <= 64");
+  AV_HIP_CHECK(hipGetLastError());
+}
 
 void smo_solve(const float* K, const float* y, const float* diag, float* alpha, float* G, int B, int N, float C,
                float eps, int max_iter, int* iters, hipStream_t stream) {
@@ -1107,13 +1226,24 @@ int smo_ws_select_parts(int N) {
 }
 
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
-                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream) {
+                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, unsigned* ticket,
+                   hipStream_t stream) {
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
   if (N <= 4 * SEL_T) {
     smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap, skip);
+  } else if (cand && per && ticket) {
+    // two levels in one launch (the last part to finish merges)
+    const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
+    const dim3 pg(parts, B);
+#define AV_SF(P) smo_ws_select_fused_kernel<P><<<pg, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, \
+      cnt, ws, ok, gap, skip, ticket)
+    if (per == 2) AV_SF(2);
+    else if (per == 4) AV_SF(4);
+    else AV_SF(8);
+#undef AV_SF
   } else if (cand && per) {
     // two levels: parts on separate CUs, then one merge over <= parts x h candidates per side
     const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
@@ -1171,7 +1301,7 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, hipStream_t stream) {
+                     float* host_gap, unsigned* ticket, hipStream_t stream) {
   if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
   const int Q = WS_Q, h = WS_Q / 2;
   check_every = check_every < 1 ? 1 : check_every;
@@ -1181,7 +1311,7 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
   for (long long blk = 0; outer < max_outer; ++blk) {
     const long long n = std::min<long long>(check_every, max_outer - outer);
     for (long long s = 0; s < n; ++s) {
-      smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream);
+      smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, ticket, stream);
       smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws, rel_tol,
                          stream);
       smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);

@@ -151,3 +151,124 @@ def kruskal_h(*samples) -> tuple[float, float]:
         return float("nan"), float("nan")
     h /= tc
     return h, float(stats.chi2.sf(h, len(xs) - 1))
+
+
+def wilcoxon_signed_rank(x, y) -> tuple[float, float]:
+    """(statistic, two-sided p) as scipy.stats.wilcoxon(x, y) (zero_method "wilcox", no continuity
+    correction, method auto).  The ranks of |x - y| over the non-zero differences and the positive
+    / negative rank sums come from ONE rank_avg launch (group = sign); the tie term feeds the
+    normal approximation.  Samples of <= 50 pairs (where scipy uses exact or permutation nulls)
+    are delegated to scipy on those few values."""
+    from scipy import stats
+    x, y = _dev(x), _dev(y).to(_dev(x).device)
+    if x.numel() != y.numel():
+        raise ValueError("wilcoxon: x and y must have the same length")
+    n_all = x.numel()
+    if n_all <= 50:
+        r = stats.wilcoxon(x.cpu().numpy(), y.cpu().numpy())
+        return float(r.statistic), float(r.pvalue)
+    d = x - y
+    d = d[d != 0]
+    n = d.numel()
+    if n == 0:
+        return 0.0, float("nan")
+    _, tie, gs = rank_avg(d.abs(), (d > 0).to(torch.int32), 2)
+    r_minus, r_plus = (float(v) for v in gs.tolist())
+    mn = n * (n + 1.0) * 0.25
+    se = math.sqrt((n * (n + 1.0) * (2.0 * n + 1.0) - float(tie[0]) / 2.0) / 24.0)
+    z = (r_plus - mn) / se if se > 0 else float("nan")
+    p = float(2 * stats.norm.sf(abs(z))) if math.isfinite(z) else float("nan")
+    return min(r_plus, r_minus), min(1.0, p)
+
+
+def cvm_2samp(x, y) -> tuple[float, float]:
+    """(T, p) as scipy.stats.cramervonmises_2samp (method auto: asymptotic above 20 values per
+    sample, else scipy's exact null on the host values).  Pooled ranks from one rank_avg launch;
+    the ranks of each sample in ascending order are its pooled ranks sorted."""
+    from scipy import stats
+    x, y = _dev(x), _dev(y).to(_dev(x).device)
+    nx, ny = x.numel(), y.numel()
+    if nx < 2 or ny < 2:
+        raise ValueError("x and y must contain at least two observations.")
+    if max(nx, ny) <= 20:
+        r = stats.cramervonmises_2samp(x.cpu().numpy(), y.cpu().numpy())
+        return float(r.statistic), float(r.pvalue)
+    r, _, _ = rank_avg(torch.cat([x, y]))
+    rx = torch.sort(r[:nx]).values
+    ry = torch.sort(r[nx:]).values
+    dev = r.device
+    u = (nx * ((rx - torch.arange(1, nx + 1, device=dev, dtype=torch.float64)) ** 2).sum()
+         + ny * ((ry - torch.arange(1, ny + 1, device=dev, dtype=torch.float64)) ** 2).sum())
+    u = float(u)
+    k, N = nx * ny, nx + ny
+    t = u / (k * N) - (4 * k - 1) / (6 * N)
+    et = (1 + 1 / N) / 6
+    vt = (N + 1) * (4 * k * N - 3 * (nx ** 2 + ny ** 2) - 2 * k) / (45 * N ** 2 * 4 * k)
+    tn = 1 / 6 + (t - et) / math.sqrt(45 * vt)
+    if tn < 0.003:
+        return t, 1.0
+    from scipy.stats._hypotests import _cdf_cvm_inf
+    return t, max(0.0, 1.0 - float(_cdf_cvm_inf(tn)))
+
+
+def anderson_ksamp(*samples) -> tuple[float, list[float], float]:
+    """(standardised A2, critical values, significance level) as scipy.stats.anderson_ksamp
+    (midrank variant, Scholz & Stephens 1987).  The A2akN sum runs on the samples' device: one sort of
+    the pooled sample, its distinct values, and per sample one sort and two searchsorted passes; the
+    normalisation and the p-value interpolation are host formulas on N and k."""
+    import warnings
+
+    import numpy as np
+    xs = [_dev(s) for s in samples]
+    k = len(xs)
+    if k < 2:
+        raise ValueError("anderson_ksamp needs at least two samples")
+    dev = xs[0].device
+    xs = [s.to(dev) for s in xs]
+    n = [s.numel() for s in xs]
+    if min(n) == 0:
+        raise ValueError("anderson_ksamp encountered sample without observations")
+    Z = torch.sort(torch.cat(xs)).values
+    N = Z.numel()
+    Zs = torch.unique_consecutive(Z)
+    if Zs.numel() < 2:
+        raise ValueError("anderson_ksamp needs more than one distinct observation")
+    left = torch.searchsorted(Z, Zs, right=False).double()
+    lj = torch.searchsorted(Z, Zs, right=True).double() - left
+    Bj = left + lj / 2.0
+    den = Bj * (N - Bj) - N * lj / 4.0
+    a2 = torch.zeros((), dtype=torch.float64, device=dev)
+    for s, ni in zip(xs, n):
+        ss = torch.sort(s).values
+        r = torch.searchsorted(ss, Zs, right=True).double()
+        f = r - torch.searchsorted(ss, Zs, right=False).double()
+        M = r - f / 2.0
+        a2 = a2 + (lj / N * (N * M - Bj * ni) ** 2 / den).sum() / ni
+    A2kN = float(a2) * (N - 1.0) / N
+    # normalisation (scipy.stats.anderson_ksamp)
+    H = sum(1.0 / v for v in n)
+    hs_cs = np.cumsum(1.0 / np.arange(N - 1, 1, -1))
+    h = hs_cs[-1] + 1
+    g = (hs_cs / np.arange(2, N)).sum()
+    a = (4 * g - 6) * (k - 1) + (10 - 6 * g) * H
+    b = (2 * g - 4) * k ** 2 + 8 * h * k + (2 * g - 14 * h - 4) * H - 8 * h + 4 * g - 6
+    c = (6 * h + 2 * g - 2) * k ** 2 + (4 * h - 4 * g + 6) * k + (2 * h - 6) * H + 4 * h
+    d = (2 * h + 6) * k ** 2 - 4 * h * k
+    sigmasq = (a * N ** 3 + b * N ** 2 + c * N + d) / ((N - 1.0) * (N - 2.0) * (N - 3.0))
+    m = k - 1
+    A2 = (A2kN - m) / math.sqrt(sigmasq)
+    b0 = np.array([0.675, 1.281, 1.645, 1.96, 2.326, 2.573, 3.085])
+    b1 = np.array([-0.245, 0.25, 0.678, 1.149, 1.822, 2.364, 3.615])
+    b2 = np.array([-0.105, -0.305, -0.362, -0.391, -0.396, -0.345, -0.154])
+    critical = b0 + b1 / math.sqrt(m) + b2 / m
+    sig = np.array([0.25, 0.1, 0.05, 0.025, 0.01, 0.005, 0.001])
+    if A2 < critical.min():
+        p = float(sig.max())
+        warnings.warn(f"p-value capped: true value larger than {p}.", stacklevel=2)
+    elif A2 > critical.max():
+        p = float(sig.min())
+        warnings.warn(f"p-value floored: true value smaller than {p}.", stacklevel=2)
+    else:
+        pf = np.polyfit(critical, np.log(sig), 2)
+        p = float(math.exp(np.polyval(pf, A2)))
+    return float(A2), critical.tolist(), p

@@ -27,3 +27,42 @@ def test_smo_batch_respects_max_iter(cuda):
     K, y = _problem(device=cuda)
     alpha, rho, iters = S.smo_batch(K, y, 1.0, 1e-6, max_iter=4096)
     assert int(iters.max()) <= 4096
+
+
+def _gap(alpha, G, y, C=1.0):
+    up = (y > 0) & (alpha < C) | (y < 0) & (alpha > 0)
+    low = (y > 0) & (alpha > 0) | (y < 0) & (alpha < C)
+    ninf = torch.tensor(-float("inf"), device=y.device)
+    return (torch.where(up, -y * G, ninf).max(1).values + torch.where(low, y * G, ninf).max(1).values)
+
+
+@pytest.mark.gpu
+def test_native_loop_matches_graph_loop_and_batches(cuda, monkeypatch):
+    """smo_ws_run (C++ step loop, converged steps as no-op launches) takes exactly the steps of the
+    graph-replay loop; in a batch the earlier-converging problem is frozen by the early exits, so
+    every problem's solution equals its single-problem solve."""
+    K1, y1 = _problem(N=6000, seed=1, device=cuda)
+    K2, y2 = _problem(N=6000, seed=2, device=cuda)
+    monkeypatch.setenv("AVMI_SMO_LOOP", "graph")
+    ag, gg, _, ig = S.smo_decomposition(K1, y1, 1.0, 1e-3)
+    monkeypatch.setenv("AVMI_SMO_LOOP", "native")
+    an, gn, _, inn = S.smo_decomposition(K1, y1, 1.0, 1e-3)
+    torch.cuda.synchronize()
+    assert torch.equal(an, ag) and torch.equal(gn, gg) and torch.equal(inn, ig)
+    assert float(_gap(an, gn, y1)[0]) < 1e-3
+    a2, g2, _, _ = S.smo_decomposition(K2, y2, 1.0, 1e-3)
+    Kb = torch.cat([K1, K2]).contiguous()
+    ab, gb, _, _ = S.smo_decomposition(Kb, torch.cat([y1, y2]), 1.0, 1e-3)
+    assert torch.equal(ab[0], an[0]) and torch.equal(ab[1], a2[0])
+    assert torch.equal(gb[1], g2[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("na,nb,d", [(200, 130, 3), (64, 64, 8), (517, 301, 20), (100, 257, 64)])
+def test_rbf_matrix_kernel_matches_fp64(cuda, na, nb, d):
+    g = torch.Generator().manual_seed(na + d)
+    A, B = torch.randn(na, d, generator=g), torch.randn(nb, d, generator=g)
+    ref = torch.exp(-0.3 * torch.cdist(A.double(), B.double()) ** 2)
+    got = S.kernel_matrix(A.to(cuda), B.to(cuda), "rbf", 0.3).cpu().double()
+    assert got.shape == (na, nb)
+    assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
