@@ -1356,12 +1356,12 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
   // two-level selection scratch: per (problem, part, side) local candidates and counts (inside a
   // graph capture these come from the capture's private pool)
   const int64_t parts = avk::smo_ws_select_parts((int)N);
-  auto cand = at::empty({B, parts, 2, h}, y.options().dtype(at::kInt));
+  auto cand = at::empty({2, B, parts, 2, h}, y.options().dtype(at::kInt));  // rows, then float values
   auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
   avk::smo_ws_select(alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)N,
                      (int)alpha.size(1), (float)C, (int)h, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()),
                      ok.data_ptr<bool>(), gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(),
-                     -INFINITY, nullptr, cur_stream(y));
+                     -INFINITY, cur_stream(y));
 }
 
 void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& ok, at::Tensor& alpha,
@@ -1461,19 +1461,17 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
   TORCH_CHECK(C > 0 && eps > 0 && inner_iter >= 0, "bad SMO parameters");
   DevGuard g(y.device());
   const int64_t parts = avk::smo_ws_select_parts((int)N);
-  auto cand = at::empty({B, parts, 2, Q / 2}, y.options().dtype(at::kInt));
+  auto cand = at::empty({2, B, parts, 2, Q / 2}, y.options().dtype(at::kInt));  // rows, then float values
   auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
   auto Kws = at::empty({B, Q, Q}, K.options());
   auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
-  auto ticket = at::zeros({B}, y.options().dtype(at::kInt));  // fused two-level selection (zeroed once)
   return avk::smo_ws_run(K.data_ptr<float>(), (int)N, alpha.data_ptr<float>(), G.data_ptr<float>(),
                          y.data_ptr<float>(), (int)B, (int)alpha.size(1), (float)C, (float)eps, (int)inner_iter,
                          (float)rel_tol, max_outer, (int)check_every,
                          reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
                          gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
-                         host_gap.data_ptr<float>(), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()),
-                         cur_stream(y));
+                         host_gap.data_ptr<float>(), cur_stream(y));
 }
 
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,

@@ -120,15 +120,14 @@ void smo_solve(const float* K, const float* y, const float* diag, float* alpha, 
                float eps, int max_iter, int* iters, hipStream_t stream);
 // working-set selection (gap, top-h up / low violators, duplicate mask) and gradient update
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
-                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, unsigned* ticket,
-                   hipStream_t stream);
+                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream);
 int smo_ws_select_parts(int N);
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                    int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream);
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, unsigned* ticket, hipStream_t stream);
+                     float* host_gap, hipStream_t stream);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
                         long long* inner_total, float* Kws, float rel_tol, hipStream_t stream);

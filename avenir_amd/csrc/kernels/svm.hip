@@ -799,12 +799,13 @@ template <int PER, bool PARTIAL, int NT, class Src>
 __device__ void ws_select2_body(const Src& src, const float* __restrict__ ab, const float* __restrict__ gb,
                                 const float* __restrict__ yb, int N, float C, int h, long long* __restrict__ wsb,
                                 bool* __restrict__ okb, float* __restrict__ gapb, int* __restrict__ cand_out,
-                                int* __restrict__ cnt_out, unsigned* in_up) {
+                                int* __restrict__ cnt_out, unsigned* in_up, float* __restrict__ candv_out = nullptr) {
   __shared__ unsigned hist[2][256];
   __shared__ float redf[2][NT / 64];
   __shared__ unsigned redu[2][NT / 64];
   __shared__ unsigned s_prefix[2], s_mask[2], s_krem[2], s_gt[2];
   __shared__ int pick[2][64];
+  __shared__ float pickv[2][64];  // the picks' violation values (PARTIAL: handed to the merge)
   __shared__ unsigned wcnt[2][PER][NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (!PARTIAL)
@@ -924,8 +925,11 @@ __device__ void ws_select2_body(const Src& src, const float* __restrict__ ab, co
     const unsigned T = s_prefix[w];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      if (k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) > T)
-        pick[w][atomicAdd(&s_gt[w], 1u)] = rid[w][i];
+      if (k[w] > 0 && cv[w][i] > -INFINITY && order_key(cv[w][i]) > T) {
+        const unsigned slot = atomicAdd(&s_gt[w], 1u);
+        pick[w][slot] = rid[w][i];
+        pickv[w][slot] = cv[w][i];
+      }
       const unsigned long long bal = __ballot(is_tie(w, i));
       if (lane == 0) wcnt[w][i][wv] = (unsigned)__popcll(bal);
     }
@@ -947,7 +951,10 @@ __device__ void ws_select2_body(const Src& src, const float* __restrict__ ab, co
       const unsigned long long bal = __ballot(tie);
       if (tie) {
         const unsigned r = before + (unsigned)__popcll(bal & below);
-        if (r < krem) pick[w][ngt + r] = rid[w][i];
+        if (r < krem) {
+          pick[w][ngt + r] = rid[w][i];
+          pickv[w][ngt + r] = cv[w][i];
+        }
       }
       eq_base += tot;
     }
@@ -962,6 +969,7 @@ __device__ void ws_select2_body(const Src& src, const float* __restrict__ ab, co
         int rank = 0;
         for (int j = 0; j < np; ++j) rank += pick[which][j] < n ? 1 : 0;
         cand_out[which * h + rank] = n;
+        if (candv_out) candv_out[which * h + rank] = pickv[which][slot];
       }
     }
     if (tid < 2) cnt_out[tid] = (int)k[tid];
@@ -1008,51 +1016,15 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_select_part_kernel(const float* 
                                                                    const float* __restrict__ G,
                                                                    const float* __restrict__ y, int N, int ldag,
                                                                    float C, int h, int parts, int* __restrict__ cand,
-                                                                   int* __restrict__ cnt, const float* __restrict__ gap,
-                                                                   float skip) {
+                                                                   int* __restrict__ cnt, float* __restrict__ candv,
+                                                                   const float* __restrict__ gap, float skip) {
   const int b = blockIdx.y, p = blockIdx.x;
   if (ws_done(gap, b, skip)) return;
   const int n0 = p * PER * SEL_T, n1 = min(N, n0 + PER * SEL_T);
   ws_select2_body<PER, true, SEL_T>(RangeSrc{n0, n1}, alpha + (long long)b * ldag, G + (long long)b * ldag,
                                     y + (long long)b * N, N, C, h, nullptr, nullptr, nullptr,
                                     cand + ((long long)b * parts + p) * 2 * h, cnt + ((long long)b * parts + p) * 2,
-                                    nullptr);
-}
-
-// Both levels in ONE launch: every part selects its local candidates as above, and the LAST part
-// workgroup of a problem to finish (a ticket counter; each part publishes its candidates with a
-// device-scope fence first, so the other XCDs' L2 lines are written back before the ticket moves)
-// runs the merge over all parts' candidates and re-arms the ticket.  No workgroup waits on another
-// (no spinning, any residency), and the merge launch with its dispatch gap per outer step is gone.
-template <int PER>
-__global__ __launch_bounds__(SEL_T) void smo_ws_select_fused_kernel(const float* __restrict__ alpha,
-                                                                    const float* __restrict__ G,
-                                                                    const float* __restrict__ y, int N, int ldag,
-                                                                    float C, int h, int parts, int* __restrict__ cand,
-                                                                    int* __restrict__ cnt, long long* __restrict__ ws,
-                                                                    bool* __restrict__ ok, float* __restrict__ gap,
-                                                                    float skip, unsigned* __restrict__ ticket) {
-  extern __shared__ unsigned in_up[];
-  __shared__ int s_last;
-  const int b = blockIdx.y, p = blockIdx.x;
-  if (ws_done(gap, b, skip)) return;  // block-uniform; every part of problem b returns alike
-  const int n0 = p * PER * SEL_T, n1 = min(N, n0 + PER * SEL_T);
-  int* cb = cand + (long long)b * parts * 2 * h;
-  int* nb = cnt + (long long)b * parts * 2;
-  ws_select2_body<PER, true, SEL_T>(RangeSrc{n0, n1}, alpha + (long long)b * ldag, G + (long long)b * ldag,
-                                    y + (long long)b * N, N, C, h, nullptr, nullptr, nullptr, cb + p * 2 * h,
-                                    nb + p * 2, nullptr);
-  __threadfence();  // release this part's candidates
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&ticket[b], 1u) == (unsigned)(parts - 1);
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // acquire the other parts' candidates
-  const CandSrc src{cb, nb, parts, h};
-  ws_select2_body<1, false, SEL_T>(src, alpha + (long long)b * ldag, G + (long long)b * ldag, y + (long long)b * N, N,
-                                   C, h, ws + (long long)b * 2 * h, ok + (long long)b * 2 * h, gap + b, nullptr,
-                                   nullptr, in_up);
-  if (threadIdx.x == 0) atomicExch(&ticket[b], 0u);  // re-arm for the next outer step
+                                    nullptr, candv + ((long long)b * parts + p) * 2 * h);
 }
 
 // merge: one workgroup of NT >= parts * h threads over the concatenated candidates
@@ -1073,17 +1045,95 @@ __global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __
                                 in_up);
 }
 
-// G[n] += y[n] * sum_q dA[q] K[ws[q], n].  A workgroup owns 64 consecutive columns n; its 4 waves
-// split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into quarters, each lane
-// streams its column of those K rows (coalesced, 8 loads in flight), and the 4 partials are added
-// in a fixed order (deterministic).  Grid (N / 64, B): >= 128 workgroups at N = 8192.
-__global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
+// Rank merge of the parts' candidates (replaces the radix merge for the two-level path): the
+// parts hand over (row, violation) pairs, so every candidate's 64-bit key (order_key(v) << 32 |
+// ~row: larger = more violating, ties to the lower row — the same order as the radix selection)
+// is known without touching alpha / G again.  Thread t ranks candidate t % M of side t / M by
+// counting the larger keys of its side (two keys per 16-byte LDS broadcast read, no barriers
+// inside); rank < h is selected, the selected rows are put in ascending order by a 64-entry count,
+// and the low side's rows already chosen on the up side are marked unused.  3 barriers instead of
+// ~14.  NT = 2M threads (M = parts x h candidate slots per side, <= 512).
+template <int NT>
+__global__ __launch_bounds__(NT) void smo_ws_merge_rank_kernel(int h, int parts, const int* __restrict__ cand,
+                                                               const int* __restrict__ cnt,
+                                                               const float* __restrict__ candv,
+                                                               long long* __restrict__ ws, bool* __restrict__ ok,
+                                                               float* __restrict__ gap, float skip) {
+  constexpr int M = NT / 2;
+  __shared__ __attribute__((aligned(16))) unsigned long long key[2][M];
+  __shared__ int sel[2][64];
+  __shared__ float s_max[2];
+  __shared__ int s_cnt[2];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (ws_done(gap, b, skip)) return;
+  const int w = tid / M, c = tid % M;
+  const int* cb = cand + (long long)b * parts * 2 * h;
+  const float* vb = candv + (long long)b * parts * 2 * h;
+  const int* nb = cnt + (long long)b * parts * 2;
+  int row = -1;
+  float val = -INFINITY;
+  if (c < parts * h) {
+    const int q = c / h, s = c % h;
+    if (s < nb[q * 2 + w]) {
+      row = cb[(q * 2 + w) * h + s];
+      val = vb[(q * 2 + w) * h + s];
+    }
+  }
+  const unsigned long long mk = row >= 0 ? ((unsigned long long)order_key(val) << 32) | (unsigned)(~row) : 0ull;
+  key[w][c] = mk;
+  if (tid < 2) {
+    int n = 0;
+    for (int q = 0; q < parts; ++q) n += nb[q * 2 + tid];
+    s_cnt[tid] = n < h ? n : h;
+    s_max[tid] = -INFINITY;
+  }
+  __syncthreads();
+  const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(&key[w][0]);
+  int rank = 0;
+#pragma unroll 8
+  for (int e = 0; e < M / 2; ++e) {
+    const ulonglong2 kk = kp[e];
+    rank += (kk.x > mk ? 1 : 0) + (kk.y > mk ? 1 : 0);
+  }
+  if (mk != 0ull && rank < h) {
+    sel[w][rank] = row;
+    if (rank == 0) s_max[w] = val;
+  }
+  __syncthreads();
+  if (tid == 0) gap[b] = s_max[0] + s_max[1];
+  if (tid < 2 * h) {
+    const int ww = tid / h, slot = tid % h, np = s_cnt[ww];
+    long long* wsw = ws + (long long)b * 2 * h + ww * h;
+    bool* okw = ok + (long long)b * 2 * h + ww * h;
+    if (slot < np) {
+      const int n = sel[ww][slot];
+      int pos = 0;
+      for (int j = 0; j < np; ++j) pos += sel[ww][j] < n ? 1 : 0;
+      bool dup = false;
+      if (ww == 1)
+        for (int j = 0; j < s_cnt[0]; ++j) dup |= sel[0][j] == n;
+      wsw[pos] = n;
+      okw[pos] = !dup;
+    } else {
+      wsw[slot] = 0;
+      okw[slot] = false;
+    }
+  }
+}
+
+// G[n] += y[n] * sum_q dA[q] K[ws[q], n].  A workgroup owns 64 consecutive columns n; its 16 waves
+// split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into sixteenths, each lane
+// streams its column of those <= 8 K rows (coalesced, all loads in flight at once), and the 16
+// partials are added in a fixed order (deterministic).  Grid (N / 64, B): >= 128 workgroups at
+// N = 8192.  (16 waves rather than 4: the per-wave row chain is the latency, 5.6 -> ~3 us.)
+constexpr int UPD_T = 1024;
+__global__ __launch_bounds__(UPD_T) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
                                                             const float* __restrict__ dA, const bool* __restrict__ ok,
                                                             const float* __restrict__ y, float* __restrict__ G, int N,
                                                             int ldag, int Q, const float* __restrict__ gap, float skip) {
   __shared__ long long s_ws[WS_Q];
   __shared__ float s_d[WS_Q];
-  __shared__ float red[4][64];
+  __shared__ float red[UPD_T / 64][64];
   __shared__ int s_cnt;
   const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (ws_done(gap, b, skip)) return;
@@ -1110,7 +1160,8 @@ __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restr
     if (lane == 0) s_cnt = base;
   }
   __syncthreads();
-  const int cnt = s_cnt, per = (cnt + 3) / 4;
+  constexpr int NW = UPD_T / 64;
+  const int cnt = s_cnt, per = (cnt + NW - 1) / NW;
   const int q0 = w * per, q1 = min(cnt, q0 + per);
   const int n = blockIdx.x * 64 + lane;
   float acc = 0.f;
@@ -1121,8 +1172,12 @@ __global__ __launch_bounds__(256) void smo_ws_update_kernel(const float* __restr
   }
   red[w][lane] = acc;
   __syncthreads();
-  if (w == 0 && n < N)
-    G[(long long)b * ldag + n] += y[(long long)b * N + n] * (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+  if (w == 0 && n < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += red[k][lane];
+    G[(long long)b * ldag + n] += y[(long long)b * N + n] * s;
+  }
 }
 
 // RBF kernel matrix K[i][j] = exp(-gamma * |a_i - b_j|^2) in ONE pass for d <= 64: a 64 x 64
@@ -1209,6 +1264,12 @@ void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* g
   AV_HIP_CHECK(hipGetLastError());
 }
 
+// "0" / "false" in the environment turns an optional fast path off (A/B measurements)
+static bool env_off(const char* name) {
+  const char* v = std::getenv(name);
+  return v && (v[0] == '0' || v[0] == 'f' || v[0] == 'F' || v[0] == 'n' || v[0] == 'N');
+}
+
 // parts of 2048 / 4096 / 8192 rows: the smallest whose candidates (parts x h per side) fit a
 // 512-thread merge, else a 1024-thread one
 static int select_part_per(int N, int h) {
@@ -1225,34 +1286,36 @@ int smo_ws_select_parts(int N) {
   return per ? (N + per * SEL_T - 1) / (per * SEL_T) : 1;
 }
 
+// cand: [B][parts][2][h] rows followed by [B][parts][2][h] float violation values (candv)
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
-                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, unsigned* ticket,
-                   hipStream_t stream) {
+                   long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream) {
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
   if (N <= 4 * SEL_T) {
     smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap, skip);
-  } else if (cand && per && ticket) {
-    // two levels in one launch (the last part to finish merges)
-    const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
-    const dim3 pg(parts, B);
-#define AV_SF(P) smo_ws_select_fused_kernel<P><<<pg, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, \
-      cnt, ws, ok, gap, skip, ticket)
-    if (per == 2) AV_SF(2);
-    else if (per == 4) AV_SF(4);
-    else AV_SF(8);
-#undef AV_SF
   } else if (cand && per) {
     // two levels: parts on separate CUs, then one merge over <= parts x h candidates per side
     const int parts = (N + per * SEL_T - 1) / (per * SEL_T);
     const dim3 pg(parts, B);
-    if (per == 2) smo_ws_select_part_kernel<2><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, gap, skip);
-    else if (per == 4) smo_ws_select_part_kernel<4><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, gap, skip);
-    else smo_ws_select_part_kernel<8><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, gap, skip);
+    float* candv = reinterpret_cast<float*>(cand + (long long)B * parts * 2 * h);
+#define AV_SP(P) smo_ws_select_part_kernel<P><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, \
+      candv, gap, skip)
+    if (per == 2) AV_SP(2);
+    else if (per == 4) AV_SP(4);
+    else AV_SP(8);
+#undef AV_SP
     AV_HIP_CHECK(hipGetLastError());
     const int m = parts * h;
+    // rank merge up to 256 candidates per side (N <= 8192: 7.0 us against 10.4 us for the radix
+    // merge, profiles/r3_svm_v6_kernel_stats.txt); beyond that its O(M^2) LDS reads stop paying
+    if (m <= 256 && !env_off("AVMI_SMO_RANK_MERGE")) {
+      if (m <= 128) smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      else smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      AV_HIP_CHECK(hipGetLastError());
+      return;
+    }
     if (m <= 256)
       smo_ws_select_merge_kernel<256><<<B, 256, lds, stream>>>(alpha, G, y, N, ldag, C, h, parts, cand, cnt, ws, ok, gap,
                                                                 skip);
@@ -1271,7 +1334,7 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                    int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream) {
   if (B <= 0 || N <= 0) return;
-  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), 256, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q, gap, skip);
+  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), UPD_T, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q, gap, skip);
   AV_HIP_CHECK(hipGetLastError());
 }
 
@@ -1301,21 +1364,42 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, unsigned* ticket, hipStream_t stream) {
+                     float* host_gap, hipStream_t caller) {
   if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
   const int Q = WS_Q, h = WS_Q / 2;
   check_every = check_every < 1 ? 1 : check_every;
   hipEvent_t ev[2];
   for (auto& e : ev) AV_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  long long outer = 0;
-  for (long long blk = 0; outer < max_outer; ++blk) {
-    const long long n = std::min<long long>(check_every, max_outer - outer);
+  // a private stream ordered after the caller's work (the caller's may be the null stream, which
+  // cannot be captured); the caller's stream is synchronised at the end anyway
+  hipStream_t stream = nullptr;
+  AV_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  AV_HIP_CHECK(hipEventRecord(ev[1], caller));
+  AV_HIP_CHECK(hipStreamWaitEvent(stream, ev[1], 0));
+  auto enqueue = [&](long long n) {
     for (long long s = 0; s < n; ++s) {
-      smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, ticket, stream);
+      smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream);
       smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws, rel_tol,
                          stream);
       smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);
     }
+  };
+  // One block of steps captured once as a HIP graph (a few microseconds of host time per block
+  // instead of five launches per step); the capture records without executing.
+  hipGraphExec_t exec = nullptr;
+  if (!env_off("AVMI_SMO_RUN_GRAPH") && max_outer >= check_every) {
+    hipGraph_t graph = nullptr;
+    AV_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    enqueue(check_every);
+    AV_HIP_CHECK(hipStreamEndCapture(stream, &graph));
+    AV_HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    AV_HIP_CHECK(hipGraphDestroy(graph));
+  }
+  long long outer = 0;
+  for (long long blk = 0; outer < max_outer; ++blk) {
+    const long long n = std::min<long long>(check_every, max_outer - outer);
+    if (exec && n == check_every) AV_HIP_CHECK(hipGraphLaunch(exec, stream));
+    else enqueue(n);
     outer += n;
     float* hg = host_gap + (blk & 1) * B;
     AV_HIP_CHECK(hipMemcpyAsync(hg, gap, sizeof(float) * B, hipMemcpyDeviceToHost, stream));
@@ -1329,6 +1413,8 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
     }
   }
   AV_HIP_CHECK(hipStreamSynchronize(stream));
+  AV_HIP_CHECK(hipStreamDestroy(stream));
+  if (exec) AV_HIP_CHECK(hipGraphExecDestroy(exec));
   for (auto& e : ev) AV_HIP_CHECK(hipEventDestroy(e));
   return outer;
 }
