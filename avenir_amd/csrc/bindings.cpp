@@ -1373,7 +1373,9 @@ void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Ten
   }
   TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
   const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
-  TORCH_CHECK(K.dim() == 3 && K.size(0) == B && K.size(1) == N && K.size(2) == N, "K must be [B, N, N]");
+  TORCH_CHECK(K.dim() == 3 && (K.size(0) == B || K.size(0) == 1) && K.size(1) == N && K.size(2) == N,
+              "K must be [B or 1 (shared by all problems), N, N]");
+  const long long kbs = K.size(0) == 1 ? 0LL : (long long)N * N;
   TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
               "alpha / G must be [B, >= N]");
   CHECK_DEV(ws);
@@ -1392,7 +1394,7 @@ void smo_ws_solve_fused(const at::Tensor& K, const at::Tensor& ws, const at::Ten
                           ok.data_ptr<bool>(), alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(),
                           (int)alpha.size(1), gap.data_ptr<float>(), (int)B, (float)C, (float)eps, (int)max_iter,
                           dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
-                          Kws.data_ptr<float>(), (float)rel_tol, cur_stream(y));
+                          Kws.data_ptr<float>(), (float)rel_tol, kbs, cur_stream(y));
 }
 
 void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& dA, const at::Tensor& ok,
@@ -1403,7 +1405,9 @@ void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& 
   }
   TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
   const int64_t B = y.size(0), N = y.size(1);
-  TORCH_CHECK(K.dim() == 3 && K.size(0) == B && K.size(1) == N && K.size(2) == N, "K must be [B, N, N]");
+  TORCH_CHECK(K.dim() == 3 && (K.size(0) == B || K.size(0) == 1) && K.size(1) == N && K.size(2) == N,
+              "K must be [B or 1 (shared by all problems), N, N]");
+  const long long kbs = K.size(0) == 1 ? 0LL : (long long)N * N;
   TORCH_CHECK(G.dim() == 2 && G.size(0) == B && G.size(1) >= N, "G must be [B, >= N]");
   CHECK_DEV(ws);
   CHECK_DTYPE(ws, at::kLong);
@@ -1415,7 +1419,7 @@ void smo_ws_update(const at::Tensor& K, const at::Tensor& ws, const at::Tensor& 
   DevGuard g(y.device());
   avk::smo_ws_update(K.data_ptr<float>(), reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()),
                      dA.data_ptr<float>(), ok.data_ptr<bool>(), y.data_ptr<float>(), G.data_ptr<float>(), (int)B,
-                     (int)N, (int)G.size(1), (int)ws.size(1), nullptr, -INFINITY, cur_stream(y));
+                     (int)N, (int)G.size(1), (int)ws.size(1), nullptr, -INFINITY, kbs, cur_stream(y));
 }
 
 // exp(-gamma |a_i - b_j|^2) [na, nb] float32 in one pass (d <= 64)
@@ -1447,7 +1451,9 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
   TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
   const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
   TORCH_CHECK(N >= 1 && N <= (1 << 18), "1 <= N <= 2^18");
-  TORCH_CHECK(K.dim() == 3 && K.size(0) == B && K.size(1) == N && K.size(2) == N, "K must be [B, N, N]");
+  TORCH_CHECK(K.dim() == 3 && (K.size(0) == B || K.size(0) == 1) && K.size(1) == N && K.size(2) == N,
+              "K must be [B or 1 (shared by all problems), N, N]");
+  const long long kbs = K.size(0) == 1 ? 0LL : (long long)N * N;
   TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
               "alpha / G must be [B, >= N]");
   CHECK_DEV(ws);
@@ -1471,7 +1477,7 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
                          reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
                          gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
-                         host_gap.data_ptr<float>(), cur_stream(y));
+                         host_gap.data_ptr<float>(), kbs, cur_stream(y));
 }
 
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,

@@ -123,14 +123,14 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
                    long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream);
 int smo_ws_select_parts(int N);
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
-                   int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream);
+                   int B, int N, int ldag, int Q, const float* gap, float skip, long long kbs, hipStream_t stream);
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, hipStream_t stream);
+                     float* host_gap, long long kbs, hipStream_t stream);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
-                        long long* inner_total, float* Kws, float rel_tol, hipStream_t stream);
+                        long long* inner_total, float* Kws, float rel_tol, long long kbs, hipStream_t stream);
 int smo_ws_size();
 void rbf_matrix(const float* A, const float* B, int na, int nb, int d, float gamma, float* K, hipStream_t stream);
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,

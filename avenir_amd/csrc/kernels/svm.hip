@@ -373,7 +373,7 @@ __global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float
                                                                  const float* __restrict__ G, const float* __restrict__ yv,
                                                                  int ldag, const float* __restrict__ gap, float C,
                                                                  float eps, int max_iter, float* __restrict__ dA,
-                                                                 long long* __restrict__ inner_total) {
+                                                                 long long* __restrict__ inner_total, long long kbs) {
   constexpr int Q = WS_Q, E = Q / 64;
   __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
   __shared__ long long s_ws[Q];
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float
     s_ws[q] = o ? ws[(long long)b * Q + q] : 0;
   }
   __syncthreads();
-  const float* Kb = K + (long long)b * N * N;
+  const float* Kb = K + b * kbs;
   // scattered 4-byte gathers from the N x N kernel matrix: 16 per thread, all issued before the
   // LDS stores (latency-bound otherwise)
   constexpr int PER = Q * Q / SOLVE_T;
@@ -432,14 +432,14 @@ __global__ __launch_bounds__(SOLVE_T) void smo_ws_solve_fused_kernel(const float
 __global__ __launch_bounds__(WS_Q) void smo_ws_gather_kernel(const float* __restrict__ K, int N,
                                                              const long long* __restrict__ ws,
                                                              const bool* __restrict__ ok, float* __restrict__ Kws,
-                                                             const float* __restrict__ gap, float skip) {
+                                                             const float* __restrict__ gap, float skip, long long kbs) {
   constexpr int Q = WS_Q;
   const int b = blockIdx.y, p = blockIdx.x, q = threadIdx.x;
   if (ws_done(gap, b, skip)) return;
   const long long* wb = ws + (long long)b * Q;
   const bool* ob = ok + (long long)b * Q;
   const long long rp = ob[p] ? wb[p] : 0, cq = ob[q] ? wb[q] : 0;  // < N (select writes n < N)
-  Kws[((long long)b * Q + p) * Q + q] = K[(long long)b * N * N + rp * N + cq];
+  Kws[((long long)b * Q + p) * Q + q] = K[b * kbs + rp * N + cq];
 }
 
 // smo_ws_solve_kernel: one wavefront per problem: the gathered Q x Q block into LDS (coalesced
@@ -1130,7 +1130,8 @@ constexpr int UPD_T = 1024;
 __global__ __launch_bounds__(UPD_T) void smo_ws_update_kernel(const float* __restrict__ K, const long long* __restrict__ ws,
                                                             const float* __restrict__ dA, const bool* __restrict__ ok,
                                                             const float* __restrict__ y, float* __restrict__ G, int N,
-                                                            int ldag, int Q, const float* __restrict__ gap, float skip) {
+                                                            int ldag, int Q, const float* __restrict__ gap, float skip,
+                                                            long long kbs) {
   __shared__ long long s_ws[WS_Q];
   __shared__ float s_d[WS_Q];
   __shared__ float red[UPD_T / 64][64];
@@ -1166,7 +1167,7 @@ __global__ __launch_bounds__(UPD_T) void smo_ws_update_kernel(const float* __res
   const int n = blockIdx.x * 64 + lane;
   float acc = 0.f;
   if (n < N) {
-    const float* Kb = K + (long long)b * N * N + n;
+    const float* Kb = K + b * kbs + n;
 #pragma unroll 8
     for (int q = q0; q < q1; ++q) acc += s_d[q] * Kb[s_ws[q] * N];
   }
@@ -1332,24 +1333,24 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
 }
 
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
-                   int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream) {
+                   int B, int N, int ldag, int Q, const float* gap, float skip, long long kbs, hipStream_t stream) {
   if (B <= 0 || N <= 0) return;
-  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), UPD_T, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q, gap, skip);
+  smo_ws_update_kernel<<<dim3((N + 63) / 64, B), UPD_T, 0, stream>>>(K, ws, dA, ok, y, G, N, ldag, Q, gap, skip, kbs);
   AV_HIP_CHECK(hipGetLastError());
 }
 
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
-                        long long* inner_total, float* Kws, float rel_tol, hipStream_t stream) {
+                        long long* inner_total, float* Kws, float rel_tol, long long kbs, hipStream_t stream) {
   if (B <= 0) return;
   if (Kws) {  // spread gather (Q x B workgroups) + one-wave solve
-    smo_ws_gather_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(K, N, ws, ok, Kws, gap, eps);
+    smo_ws_gather_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(K, N, ws, ok, Kws, gap, eps, kbs);
     AV_HIP_CHECK(hipGetLastError());
     smo_ws_solve_kernel<<<B, WSS_T, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, rel_tol, max_iter,
                                                  dA, inner_total);
   } else {
     smo_ws_solve_fused_kernel<<<B, SOLVE_T, 0, stream>>>(K, N, ws, ok, alpha, G, y, ldag, gap, C, eps, max_iter, dA,
-                                                         inner_total);
+                                                         inner_total, kbs);
   }
   AV_HIP_CHECK(hipGetLastError());
 }
@@ -1364,7 +1365,7 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, hipStream_t caller) {
+                     float* host_gap, long long kbs, hipStream_t caller) {
   if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
   const int Q = WS_Q, h = WS_Q / 2;
   check_every = check_every < 1 ? 1 : check_every;
@@ -1380,8 +1381,8 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
     for (long long s = 0; s < n; ++s) {
       smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream);
       smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws, rel_tol,
-                         stream);
-      smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);
+                         kbs, stream);
+      smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, kbs, stream);
     }
   };
   // One block of steps captured once as a HIP graph (a few microseconds of host time per block

@@ -151,6 +151,8 @@ class _WorkingSetSMO:
         # fused selection / update kernels (one launch each instead of ~25 torch ops per step)
         self.fused = (fused and self.gpu and K.dtype == torch.float32 and K.is_contiguous() and N <= (1 << 18)
                       and Q == 128)
+        if K.shape[0] == 1 and B > 1 and not self.fused:   # one shared K: a broadcast view for indexing
+            self.K = K.expand(B, -1, -1)
         if self.fused:
             self.ws_buf = torch.zeros((B, Q), dtype=torch.long, device=dev)
             self.ok_buf = torch.zeros((B, Q), dtype=torch.bool, device=dev)
@@ -282,7 +284,9 @@ LAST_SOLVE: dict = {}   # outer-step count of the last working-set solve (benchm
 @traced("svm.smo", nbytes=lambda K, *a, **k: K.numel() * K.element_size(), device=lambda K, *a, **k: K.device)
 def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_iter: int = 1_000_000,
               solver: str = "auto"):
-    """Solve B SVM duals: K [B, N, N], y [B, N] in {-1, 0 (padding), +1}.  Returns (alpha, rho, iters).
+    """Solve B SVM duals: K [B, N, N] (or [1, N, N] shared by all B problems — one-vs-rest classes
+    — which the working-set kernels read in place instead of B copies), y [B, N] in {-1, 0 (padding),
+    +1}.  Returns (alpha, rho, iters).
     ``solver``: "full" (one persistent workgroup runs plain SMO over all N), "ws" (working-set
     decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N).
 
@@ -299,6 +303,8 @@ def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max
                                                    inner_iter=inner_iter)
         LAST_SOLVE.update(solver="ws", outer=outer)
         return alpha, _rho(alpha, G, y.float(), C), inner.int()
+    if K.shape[0] == 1 and B > 1:
+        K = K.expand(B, -1, -1)
     if K.device.type == "cuda":
         Kc = K.float().contiguous()
         yc = y.float().contiguous()
@@ -355,9 +361,8 @@ class SVC:
             ys = torch.where(y == self.classes[1], 1.0, -1.0).view(1, -1)
         else:
             ys = torch.stack([torch.where(y == c, 1.0, -1.0) for c in self.classes])
-        B = ys.shape[0]
-        Kb = K.unsqueeze(0).expand(B, -1, -1).contiguous() if B > 1 else K.unsqueeze(0)
-        alpha, rho, iters = smo_batch(Kb, ys.to(X.device), self.C, self.eps, self.max_iter)
+        # one K for all one-vs-rest problems (smo_batch broadcasts it where a solver needs copies)
+        alpha, rho, iters = smo_batch(K.unsqueeze(0), ys.to(X.device), self.C, self.eps, self.max_iter)
         self.iters = iters.tolist()
         sv = (alpha > 0).any(0)
         self.support_ = sv.nonzero().view(-1)

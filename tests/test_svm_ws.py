@@ -66,3 +66,18 @@ def test_rbf_matrix_kernel_matches_fp64(cuda, na, nb, d):
     got = S.kernel_matrix(A.to(cuda), B.to(cuda), "rbf", 0.3).cpu().double()
     assert got.shape == (na, nb)
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_shared_kernel_matrix_batch_equals_copies(cuda):
+    """One-vs-rest problems read ONE [1, N, N] kernel matrix in place (batch stride 0) and get the
+    same duals as with B materialised copies."""
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(5000, 3, generator=g)
+    cls = (X[:, 0] > 0.5).long() + (X[:, 1] > 0).long()
+    ys = torch.stack([torch.where(cls == c, 1.0, -1.0) for c in range(3)]).to(cuda)
+    K = S.kernel_matrix(X.to(cuda), X.to(cuda), "rbf", 0.5).unsqueeze(0).contiguous()
+    a1, r1, i1 = S.smo_batch(K, ys, 1.0, 1e-3, solver="ws")
+    a3, r3, i3 = S.smo_batch(K.expand(3, -1, -1).contiguous(), ys, 1.0, 1e-3, solver="ws")
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a3) and torch.equal(i1, i3) and torch.allclose(r1, r3)
