@@ -59,16 +59,21 @@ __device__ __forceinline__ unsigned byte_of(const uint2& v, int j) {
 // The node total is NOT a per-row atomic (every row of a class hit the same LDS word: the main
 // source of LDS conflicts): feature 0's missing codes go to the TB-1 word, and at the flush each
 // class adds its feature-0 bins to it (every counted row is in exactly one of those words).
+// The LDS table is replicated `rep` times (1..8, as many as fit): lane l adds into replica
+// l % rep, so lanes of one wave whose rows share a (class, bin) word — the common case with few
+// classes and skewed bins — hit different words; the replica stride is odd, so the copies of a
+// word sit in different banks.  The replicas are summed before the flush.
 __global__ __launch_bounds__(FB_THREADS) void forest_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, const uint8_t* __restrict__ lab, const uint8_t* __restrict__ wt,
     const int* __restrict__ item_slot, const long long* __restrict__ item_start, const int* __restrict__ item_len,
     const int* __restrict__ bins, const int* __restrict__ offs, int nfeat, int TB, int C,
-    unsigned long long* __restrict__ hist) {
-  extern __shared__ unsigned int s_h[];
+    unsigned long long* __restrict__ hist, int rep) {
+  extern __shared__ unsigned int s_all[];
   const int item = blockIdx.x;
-  const int per = C * TB;
-  for (int i = threadIdx.x; i < per; i += FB_THREADS) s_h[i] = 0;
+  const int per = C * TB, stride = per | 1;
+  for (int i = threadIdx.x; i < rep * stride; i += FB_THREADS) s_all[i] = 0;
   __syncthreads();
+  unsigned* s_h = s_all + (threadIdx.x & (rep - 1)) * stride;  // this lane's replica
   const long long start = item_start[item];
   const long long end = start + item_len[item];
   for (long long base = start & ~7LL; base < end; base += RTILE) {
@@ -104,6 +109,15 @@ __global__ __launch_bounds__(FB_THREADS) void forest_hist_kernel(
     }
   }
   __syncthreads();
+  s_h = s_all;
+  if (rep > 1) {  // replicas -> replica 0
+    for (int i = threadIdx.x; i < per; i += FB_THREADS) {
+      unsigned t = s_all[i];
+      for (int r = 1; r < rep; ++r) t += s_all[r * stride + i];
+      s_all[i] = t;
+    }
+    __syncthreads();
+  }
   if (nfeat > 0 && threadIdx.x < C) {  // node total = feature 0's bins + its missing rows
     const int c = threadIdx.x, B0 = bins[0], o0 = offs[0];
     unsigned t = s_h[c * TB + TB - 1];
@@ -550,10 +564,19 @@ void forest_hist(const uint8_t* codes, long long ld, const uint8_t* lab, const u
                  const long long* item_start, const int* item_len, int n_items, const int* bins, const int* offs,
                  int nfeat, int TB, int C, unsigned long long* hist, hipStream_t stream) {
   if (n_items <= 0) return;
-  const size_t lds = sizeof(unsigned) * (size_t)C * TB;
-  if (lds > 64 * 1024) throw std::runtime_error("forest_hist: class x bin table exceeds LDS");
+  const size_t stride = ((size_t)C * TB) | 1;
+  if (sizeof(unsigned) * stride > 64 * 1024) throw std::runtime_error("forest_hist: class x bin table exceeds LDS");
+  int rep = 8;  // replicas that fit 32 KB (keeps several workgroups per CU)
+  while (rep > 1 && sizeof(unsigned) * stride * rep > 32 * 1024) rep >>= 1;
+  const char* e = std::getenv("AVMI_FOREST_HIST_REP");
+  if (e && *e) {
+    const int r = std::atoi(e);
+    if (r == 1 || r == 2 || r == 4 || r == 8) rep = r;
+  }
+  if (sizeof(unsigned) * stride * rep > 64 * 1024) rep = 1;
+  const size_t lds = sizeof(unsigned) * stride * rep;
   forest_hist_kernel<<<n_items, FB_THREADS, lds, stream>>>(codes, ld, lab, wt, item_slot, item_start, item_len, bins,
-                                                            offs, nfeat, TB, C, hist);
+                                                            offs, nfeat, TB, C, hist, rep);
   AV_HIP_CHECK(hipGetLastError());
 }
 
