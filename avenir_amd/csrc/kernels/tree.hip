@@ -93,13 +93,17 @@ __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, long long n, const int* __restrict__ node,
     const float* __restrict__ g, const float* __restrict__ h, const int* __restrict__ bins,
     const int* __restrict__ offs, int nfeat, int total_bins, int nodes_per_chunk, int n_nodes, int even_only,
-    int tot_slot, float S, long long* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long s_p[];
+    int tot_slot, float S, long long* __restrict__ out, int rep) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_all[];
   const int a0 = blockIdx.y * nodes_per_chunk;
   const int na = min(nodes_per_chunk, n_nodes - a0);
   const int per_node = total_bins;
-  for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) s_p[i] = 0ull;
+  // rep replicas of the table (lane l adds into replica l % rep; odd stride: a word's copies sit in
+  // different banks), summed before the flush — fewer same-word atomics from one wave
+  const int rstride = (nodes_per_chunk * per_node) | 1;
+  for (int i = threadIdx.x; i < rep * rstride; i += TB_THREADS) s_all[i] = 0ull;
   __syncthreads();
+  unsigned long long* s_p = s_all + (threadIdx.x & (rep - 1)) * rstride;
   const long long nq = (n + 3) >> 2;
   const long long stride = (long long)gridDim.x * TB_THREADS;
   for (long long q = (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < nq; q += stride) {
@@ -148,7 +152,8 @@ __global__ __launch_bounds__(TB_THREADS) void node_grad_hist_kernel(
   }
   __syncthreads();
   for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) {
-    const unsigned long long v = s_p[i];
+    unsigned long long v = s_all[i];
+    for (int r = 1; r < rep; ++r) v += s_all[r * rstride + i];  // wrapping packed sums add exactly
     if (v) {
       const long long gs = (long long)(int)(unsigned)(v & 0xFFFFFFFFull);
       const long long hs = (long long)((v - (unsigned long long)gs) >> 32);
@@ -318,8 +323,18 @@ void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const 
   gx = std::max(gx, min_gx);
   if (gx > 0x7fffffffLL) throw std::runtime_error("node_grad_histogram: too many rows");
   dim3 grid((unsigned)gx, chunks);
-  node_grad_hist_kernel<<<grid, TB_THREADS, per_node_bytes * npc, stream>>>(
-      codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, even_only, tot_slot, scale, out);
+  // table replicas (opt-in, AVMI_GBT_HIST_REP=2|4): unlike the forest's 32-bit class counts they
+  // do not pay for the 64-bit packed sums — GBT 120 x depth 3 at 16.7 M rows: 137 ms with one
+  // table, 139-140 ms with 2 or 4 (profiles/r3_gbt_hist_replicas_ab.txt)
+  const long long rbytes = 8LL * ((npc * (long long)total_bins) | 1);
+  int rep = 1;
+  const char* e = std::getenv("AVMI_GBT_HIST_REP");
+  if (e && *e) {
+    const int r = std::atoi(e);
+    if ((r == 1 || r == 2 || r == 4) && rbytes * r <= 64 * 1024) rep = r;
+  }
+  node_grad_hist_kernel<<<grid, TB_THREADS, rbytes * rep, stream>>>(
+      codes, ld, n, node, g, h, bins, offs, nfeat, total_bins, npc, n_nodes, even_only, tot_slot, scale, out, rep);
   AV_HIP_CHECK(hipGetLastError());
 }
 
