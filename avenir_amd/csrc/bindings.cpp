@@ -709,9 +709,14 @@ py::tuple mixed_knn(const at::Tensor& Qn, const at::Tensor& Qc, const at::Tensor
   auto d = at::empty({nq, k}, Qn.options());
   auto i = at::empty({nq, k}, Qn.options().dtype(at::kLong));
   DevGuard gd(Qn.device());
+  const int splits = avk::mixed_knn_splits(nq, nr);
+  const int64_t KK = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 32;
+  auto pd = at::empty({splits, nq, KK}, Qn.options());
+  auto pi = at::empty({splits, nq, KK}, Qn.options().dtype(at::kInt));
   avk::mixed_knn(Qn.data_ptr<float>(), Qc.data_ptr<int>(), nq, Rn.data_ptr<float>(), Rc.data_ptr<int>(), nr, (int)Dn,
                  (int)Dc, wc.data_ptr<float>(), (int)k, r_base, d.data_ptr<float>(),
-                 reinterpret_cast<long long*>(i.data_ptr<int64_t>()), cur_stream(Qn));
+                 reinterpret_cast<long long*>(i.data_ptr<int64_t>()), pd.data_ptr<float>(), pi.data_ptr<int>(), splits,
+                 cur_stream(Qn));
   return py::make_tuple(d, i);
 }
 

@@ -277,8 +277,10 @@ void lstm_bwd(const float* dhseq, const unsigned short* gates, const float* cseq
 
 // distance.hip: mixed-type kNN without one-hot expansion
 int mixed_knn_max_dims();
+int mixed_knn_splits(long long nq, long long nr);
 void mixed_knn(const float* Qn, const int* Qc, long long nq, const float* Rn, const int* Rc, long long nr, int Dn,
-               int Dc, const float* wc, int k, long long r_base, float* out_d, long long* out_i, hipStream_t stream);
+               int Dc, const float* wc, int k, long long r_base, float* out_d, long long* out_i, float* part_d,
+               int* part_i, int splits, hipStream_t stream);
 
 // stats.hip (K26 rank statistics)
 void rank_avg(const double* sorted, const long long* perm, long long n, const int* group, int n_groups, double* ranks,

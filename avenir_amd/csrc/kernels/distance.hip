@@ -386,60 +386,131 @@ __global__ __launch_bounds__(VOTE_T) void knn_vote_kernel(
 // w on a code mismatch, w / 2 when exactly one side is missing (-1) and 0 when both are — exactly
 // the squared euclidean distance of ops.distance.encode_mixed's scaled one-hot embedding, so
 // results match the MFMA path, but the width is the number of columns, not of categorical values.
-// One thread per query (features in registers), 256 reference rows per LDS stage (all threads read
-// the same row: broadcast), top-k in registers; returns euclidean distances.
+//
+// The categorical part is folded like the one-hot norms: sum_f w_f/2 ([a_f >= 0] + [b_f >= 0])
+// - sum_f w_f [a_f == b_f >= 0], i.e. a per-query constant + a per-reference constant (computed
+// once per LDS stage) - one compare-and-add per column.  One thread per query (features in
+// registers, column counts padded to DN / DC at compile time: padded numerics are 0 on both sides,
+// padded codes never match), 256 reference rows per LDS stage read as 16-byte broadcasts, top-k in
+// registers.  The references are split over gridDim.y so that a launch has >= 1024 workgroups
+// (a few thousand queries alone fill less than a third of the chip); mixed_knn_merge_kernel merges
+// the splits' lists (ties to the lower reference index, as within a split).
 constexpr int MX_T = 256;
 constexpr int MX_MAXD = 32;
 
-template <int K>
+template <int K, int DN, int DC>
 __global__ __launch_bounds__(MX_T) void mixed_knn_kernel(const float* __restrict__ Qn, const int* __restrict__ Qc,
                                                          long long nq, const float* __restrict__ Rn,
                                                          const int* __restrict__ Rc, long long nr, int Dn, int Dc,
-                                                         const float* __restrict__ wc, int k, long long r_base,
-                                                         float* __restrict__ out_d, long long* __restrict__ out_i) {
-  __shared__ float sRn[MX_T * MX_MAXD];
-  __shared__ int sRc[MX_T * MX_MAXD];
-  __shared__ float sw[MX_MAXD];
+                                                         const float* __restrict__ wc, long long per,
+                                                         float* __restrict__ part_d, int* __restrict__ part_i) {
+  constexpr int DNS = DN > 0 ? DN : 4, DCS = DC > 0 ? DC : 4;
+  __shared__ __attribute__((aligned(16))) float sRn[MX_T][DNS];
+  __shared__ __attribute__((aligned(16))) int sRc[MX_T][DCS];
+  __shared__ float sK[MX_T];
   const int tid = threadIdx.x;
   const long long q = (long long)blockIdx.x * MX_T + tid;
-  if (tid < Dc) sw[tid] = wc[tid];
-  float qn[MX_MAXD];
-  int qc[MX_MAXD];
+  const long long rs = (long long)blockIdx.y * per, re = min(nr, rs + per);
+  float w[DCS];
 #pragma unroll
-  for (int f = 0; f < MX_MAXD; ++f) {
-    qn[f] = (q < nq && f < Dn) ? Qn[q * Dn + f] : 0.f;
-    qc[f] = (q < nq && f < Dc) ? Qc[q * Dc + f] : -1;
+  for (int f = 0; f < DCS; ++f) w[f] = f < Dc ? wc[f] : 0.f;
+  float qn[DNS];
+  int qa[DCS];
+  float qconst = 0.f;
+#pragma unroll
+  for (int f = 0; f < DNS; ++f) qn[f] = (q < nq && f < Dn) ? Qn[q * Dn + f] : 0.f;
+#pragma unroll
+  for (int f = 0; f < DCS; ++f) {
+    const int a = (q < nq && f < Dc) ? Qc[q * Dc + f] : -1;
+    qconst += a >= 0 ? 0.5f * w[f] : 0.f;
+    qa[f] = a >= 0 ? a : -2;  // a missing query code matches nothing
   }
   float bd[K];
   int bi[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
-  for (long long r0 = 0; r0 < nr; r0 += MX_T) {
-    const int rows = (int)min((long long)MX_T, nr - r0);
+  for (long long r0 = rs; r0 < re; r0 += MX_T) {
+    const int rows = (int)min((long long)MX_T, re - r0);
     __syncthreads();  // the previous stage's reads are done
-    for (int e = tid; e < rows * Dn; e += MX_T) sRn[e] = Rn[r0 * Dn + e];
-    for (int e = tid; e < rows * Dc; e += MX_T) sRc[e] = Rc[r0 * Dc + e];
+    if (DN > 0)
+      for (int e = tid; e < MX_T * DN; e += MX_T) {
+        const int j = e / DN, f = e % DN;
+        sRn[j][f] = (j < rows && f < Dn) ? Rn[(r0 + j) * Dn + f] : 0.f;
+      }
+    if (DC > 0)
+      for (int e = tid; e < MX_T * DC; e += MX_T) {
+        const int j = e / DC, f = e % DC;
+        sRc[j][f] = (j < rows && f < Dc) ? Rc[(r0 + j) * Dc + f] : -1;
+      }
+    __syncthreads();
+    if (DC > 0) {  // per-reference constant: w/2 per present code
+      float c = 0.f;
+#pragma unroll
+      for (int f = 0; f < DC; ++f) c += sRc[tid][f] >= 0 ? 0.5f * w[f] : 0.f;
+      sK[tid] = c;
+    } else {
+      sK[tid] = 0.f;
+    }
     __syncthreads();
     if (q >= nq) continue;
     for (int j = 0; j < rows; ++j) {
       float d = 0.f;
+      if (DN > 0) {
 #pragma unroll
-      for (int f = 0; f < MX_MAXD; ++f)
-        if (f < Dn) {
-          const float t = qn[f] - sRn[j * Dn + f];
-          d = fmaf(t, t, d);
+        for (int f = 0; f < DN; f += 4) {
+          const float4 r = *reinterpret_cast<const float4*>(&sRn[j][f]);
+          const float t0 = qn[f] - r.x, t1 = qn[f + 1] - r.y, t2 = qn[f + 2] - r.z, t3 = qn[f + 3] - r.w;
+          d = fmaf(t0, t0, d);
+          d = fmaf(t1, t1, d);
+          d = fmaf(t2, t2, d);
+          d = fmaf(t3, t3, d);
         }
+      }
+      if (DC > 0) {
+        float m = 0.f;
 #pragma unroll
-      for (int f = 0; f < MX_MAXD; ++f)
-        if (f < Dc) {
-          const int a = qc[f], b = sRc[j * Dc + f];
-          const float w = sw[f];
-          d += (a < 0 && b < 0) ? 0.f : ((a < 0 || b < 0) ? 0.5f * w : (a != b ? w : 0.f));
+        for (int f = 0; f < DC; f += 4) {
+          const int4 r = *reinterpret_cast<const int4*>(&sRc[j][f]);
+          m += qa[f] == r.x ? w[f] : 0.f;
+          m += qa[f + 1] == r.y ? w[f + 1] : 0.f;
+          m += qa[f + 2] == r.z ? w[f + 2] : 0.f;
+          m += qa[f + 3] == r.w ? w[f + 3] : 0.f;
         }
+        d += (qconst + sK[j]) - m;
+      }
       topk_insert<K>(bd, bi, d, (int)(r0 + j));
     }
   }
   if (q >= nq) return;
+  const long long o = ((long long)blockIdx.y * nq + q) * K;
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    part_d[o + s] = bd[s];
+    part_i[o + s] = bi[s];
+  }
+}
+
+// per query: the splits' sorted lists, in split (= reference index) order, into the final top-k
+template <int K>
+__global__ __launch_bounds__(MX_T) void mixed_knn_merge_kernel(const float* __restrict__ part_d,
+                                                               const int* __restrict__ part_i, long long nq,
+                                                               int splits, int k, long long r_base,
+                                                               float* __restrict__ out_d,
+                                                               long long* __restrict__ out_i) {
+  const long long q = (long long)blockIdx.x * MX_T + threadIdx.x;
+  if (q >= nq) return;
+  float bd[K];
+  int bi[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
+  for (int sp = 0; sp < splits; ++sp) {
+    const long long o = ((long long)sp * nq + q) * K;
+    for (int s = 0; s < K; ++s) {
+      const int i = part_i[o + s];
+      if (i < 0) break;  // a split's list is sorted: the rest is empty
+      topk_insert<K>(bd, bi, part_d[o + s], i);
+    }
+  }
   for (int s = 0; s < k; ++s) {
     const bool ok = s < K && bi[s] >= 0;
     out_d[q * k + s] = ok ? sqrtf(fmaxf(bd[s], 0.f)) : INFINITY;
@@ -503,17 +574,39 @@ void knn_vote(const float* dist, const long long* idx, long long M, int k, const
 
 int mixed_knn_max_dims() { return MX_MAXD; }
 
+// reference splits: enough workgroups for the chip (>= 1024), each split >= 4096 references
+int mixed_knn_splits(long long nq, long long nr) {
+  const long long gx = (nq + MX_T - 1) / MX_T;
+  long long s = (1024 + gx - 1) / gx;
+  s = std::min(s, std::max(1LL, nr / 4096));
+  return (int)std::max(1LL, std::min(s, 64LL));
+}
+
 void mixed_knn(const float* Qn, const int* Qc, long long nq, const float* Rn, const int* Rc, long long nr, int Dn,
-               int Dc, const float* wc, int k, long long r_base, float* out_d, long long* out_i, hipStream_t stream) {
+               int Dc, const float* wc, int k, long long r_base, float* out_d, long long* out_i, float* part_d,
+               int* part_i, int splits, hipStream_t stream) {
   if (nq <= 0) return;
   if (Dn > MX_MAXD || Dc > MX_MAXD || k < 1 || k > 32) throw std::runtime_error("mixed_knn: dims <= 32, 1 <= k <= 32");
-  const unsigned grid = (unsigned)((nq + MX_T - 1) / MX_T);
-#define AV_MX(KK) mixed_knn_kernel<KK><<<grid, MX_T, 0, stream>>>(Qn, Qc, nq, Rn, Rc, nr, Dn, Dc, wc, k, r_base, out_d, out_i)
-  if (k <= 4) AV_MX(4);
-  else if (k <= 8) AV_MX(8);
-  else if (k <= 16) AV_MX(16);
-  else AV_MX(32);
-#undef AV_MX
+  const long long per = std::max(1LL, (nr + splits - 1) / splits);
+  const dim3 grid((unsigned)((nq + MX_T - 1) / MX_T), (unsigned)splits);
+  const int KK = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 32;
+  const int DNP = Dn == 0 ? 0 : Dn <= 4 ? 4 : Dn <= 8 ? 8 : Dn <= 16 ? 16 : 32;
+  const int DCP = Dc == 0 ? 0 : Dc <= 4 ? 4 : Dc <= 8 ? 8 : Dc <= 16 ? 16 : 32;
+#define AV_MX3(KK_, DN_, DC_) \
+  if (KK == KK_ && DNP == DN_ && DCP == DC_) \
+    mixed_knn_kernel<KK_, DN_, DC_><<<grid, MX_T, 0, stream>>>(Qn, Qc, nq, Rn, Rc, nr, Dn, Dc, wc, per, part_d, part_i);
+#define AV_MXD(KK_, DN_) AV_MX3(KK_, DN_, 0) AV_MX3(KK_, DN_, 4) AV_MX3(KK_, DN_, 8) AV_MX3(KK_, DN_, 16) AV_MX3(KK_, DN_, 32)
+#define AV_MXK(KK_) AV_MXD(KK_, 0) AV_MXD(KK_, 4) AV_MXD(KK_, 8) AV_MXD(KK_, 16) AV_MXD(KK_, 32)
+  AV_MXK(4) AV_MXK(8) AV_MXK(16) AV_MXK(32)
+#undef AV_MXK
+#undef AV_MXD
+#undef AV_MX3
+  AV_HIP_CHECK(hipGetLastError());
+  const unsigned mg = (unsigned)((nq + MX_T - 1) / MX_T);
+#define AV_MM(KK_) \
+  if (KK == KK_) mixed_knn_merge_kernel<KK_><<<mg, MX_T, 0, stream>>>(part_d, part_i, nq, splits, k, r_base, out_d, out_i);
+  AV_MM(4) AV_MM(8) AV_MM(16) AV_MM(32)
+#undef AV_MM
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -49,9 +49,52 @@ def rank_avg(x: torch.Tensor, group: torch.Tensor | None = None, n_groups: int =
     return ranks, tie, gs
 
 
-def kendall_counts(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-    """int64 [5]: concordant, discordant, tied in x only, tied in y only, tied in both (pairs i < j)."""
+KENDALL_PAIRS_MAX_N = 1 << 15   # above: the O(n log^2 n) merge count beats the O(n^2) pair kernel
+
+
+def _tie_pairs(v: torch.Tensor) -> torch.Tensor:
+    """sum over runs of equal values (v sorted; rows of a 2-D v) of t (t - 1) / 2."""
+    _, c = torch.unique_consecutive(v, dim=0, return_counts=True)
+    c = c.long()
+    return (c * (c - 1) // 2).sum()
+
+
+def _kendall_merge_counts(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Knight's method on the device: order by (x, y), count the strict inversions of the y sequence
+    level by level (blocks of 2s: every right-half value's count of larger left-half values by one
+    batched searchsorted, then the blocks sorted for the next level) — the discordant pairs, since
+    pairs tied in x are ordered by y and never inverted.  Tie pairs from run lengths; concordant =
+    all - discordant - tied.  O(n log^2 n) work in log2 n launches of sort + searchsorted."""
+    n = x.numel()
+    o = torch.sort(y, stable=True).indices
+    o = o[torch.sort(x[o], stable=True).indices]
+    xs, ys = x[o], y[o]
+    m = 1 << max(0, (n - 1).bit_length())
+    cur = torch.cat([ys, torch.full((m - n,), float("inf"), dtype=ys.dtype, device=ys.device)])
+    inv = torch.zeros((), dtype=torch.int64, device=x.device)
+    s = 1
+    while s < m:
+        blk = cur.view(-1, 2, s)
+        L, R = blk[:, 0, :].contiguous(), blk[:, 1, :].contiguous()
+        inv += (s - torch.searchsorted(L, R, right=True)).sum()
+        cur = torch.sort(cur.view(-1, 2 * s), dim=1).values.view(-1)
+        s *= 2
+    both = _tie_pairs(torch.stack([xs, ys], 1))
+    tx = _tie_pairs(xs)
+    ty = _tie_pairs(torch.sort(y).values)
+    tot = torch.tensor(n * (n - 1) // 2, dtype=torch.int64, device=x.device)
+    tx_only, ty_only = tx - both, ty - both
+    return torch.stack([tot - inv - tx_only - ty_only - both, inv, tx_only, ty_only, both])
+
+
+def kendall_counts(x: torch.Tensor, y: torch.Tensor, method: str = "auto") -> torch.Tensor:
+    """int64 [5]: concordant, discordant, tied in x only, tied in y only, tied in both (pairs i < j).
+    ``method``: "pairs" (GPU: the exact all-pairs kernel; CPU: tiled tensor comparisons), "merge"
+    (sort-based inversion count) or "auto" (pairs up to KENDALL_PAIRS_MAX_N values on the GPU and
+    4096 on the CPU, merge above)."""
     x, y = _dev(x), _dev(y).to(_dev(x).device)
+    if method == "merge" or (method == "auto" and x.numel() > (KENDALL_PAIRS_MAX_N if x.is_cuda else 4096)):
+        return _kendall_merge_counts(x, y)
     if x.is_cuda:
         return _native.C().kendall_pairs(x, y)
     n = x.numel()

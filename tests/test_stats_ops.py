@@ -138,3 +138,21 @@ def test_explorer_two_sample_edf_tests():
 def test_edf_and_signed_rank_tests_on_device(cuda):
     x, y = _samples(5000, seed=7)
     _edf_checks(x, y, cuda)
+
+
+@pytest.mark.parametrize("ties", [True, False])
+def test_kendall_merge_count_equals_pair_count(ties):
+    x, y = _samples(3000, seed=9, ties=ties)
+    a = S.kendall_counts(torch.tensor(x), torch.tensor(y), method="pairs")
+    b = S.kendall_counts(torch.tensor(x), torch.tensor(y), method="merge")
+    assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_kendall_merge_count_on_device(cuda):
+    x, y = _samples(100_000, seed=10)
+    g = S.kendall_counts(torch.tensor(x, device=cuda), torch.tensor(y, device=cuda), method="merge")
+    c = S.kendall_counts(torch.tensor(x), torch.tensor(y), method="merge")
+    assert torch.equal(g.cpu(), c)
+    small = S.kendall_counts(torch.tensor(x[:20000], device=cuda), torch.tensor(y[:20000], device=cuda), method="pairs")
+    assert torch.equal(small.cpu(), S.kendall_counts(torch.tensor(x[:20000]), torch.tensor(y[:20000]), method="merge"))
