@@ -761,7 +761,9 @@ py::tuple pagerank(const at::Tensor& P, double d, int64_t iters, double tol) {
 // The caller checks id ranges once per fit (pairs / alias are built from the vocabulary).
 void sgns_step(at::Tensor& Win, at::Tensor& Wout, at::Tensor& gIn, at::Tensor& gOut, at::Tensor& cIn, at::Tensor& cOut,
                const at::Tensor& centre, const at::Tensor& context, const at::Tensor& aprob, const at::Tensor& alias,
-               int64_t neg, double lr, bool mean_in, int64_t seed, int64_t step) {
+               int64_t neg, double lr, bool mean_in, int64_t seed, int64_t step, const c10::optional<at::Tensor>& hot,
+               const c10::optional<at::Tensor>& gOutHot, const c10::optional<at::Tensor>& gInHot,
+               const c10::optional<at::Tensor>& cIn_next, const c10::optional<at::Tensor>& cOut_next) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&Win, &Wout, &gIn, &gOut, &cIn, &cOut, &aprob}) {
     CHECK_DEV((*t));
     CHECK_DTYPE((*t), at::kFloat);
@@ -773,9 +775,37 @@ void sgns_step(at::Tensor& Win, at::Tensor& Wout, at::Tensor& gIn, at::Tensor& g
     TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
   }
   TORCH_CHECK(Win.dim() == 2 && Wout.dim() == 2 && Win.size(1) == Wout.size(1), "Win [Rin, d], Wout [V, d]");
-  TORCH_CHECK(gIn.sizes() == Win.sizes() && gOut.sizes() == Wout.sizes() && cIn.numel() == Win.size(0) &&
-                  cOut.numel() == Wout.size(0), "gradient / count buffers must match the tables");
-  const int64_t V = Wout.size(0), dim = Win.size(1);
+  const int64_t V = Wout.size(0), dim = Win.size(1), R = avk::sgns_hot_replicas();
+  // hot rows: hot int32 [V] (slot in [0, H) or -1), gOutHot [R, H, d]; gInHot [R, H, d] or None (the
+  // centre table shares the word ids: word2vec); the counts carry R x H extra entries after the rows
+  int64_t H = 0;
+  if (hot) {
+    CHECK_DEV((*hot));
+    CHECK_DTYPE((*hot), at::kInt);
+    TORCH_CHECK(hot->numel() == V && gOutHot && gOutHot->dim() == 3 && gOutHot->size(0) == R &&
+                    gOutHot->size(2) == dim && gOutHot->is_contiguous(), "hot [V], gOutHot [R, H, d]");
+    CHECK_DTYPE((*gOutHot), at::kFloat);
+    H = gOutHot->size(1);  // slots outside [0, H) are treated as cold by the kernels (no host sync here)
+    if (gInHot) {
+      CHECK_DTYPE((*gInHot), at::kFloat);
+      TORCH_CHECK(gInHot->sizes() == gOutHot->sizes() && gInHot->is_contiguous() && Win.size(0) == V,
+                  "gInHot like gOutHot, centre table over the same ids");
+    }
+  }
+  const int64_t extra_in = (hot && gInHot) ? R * H : 0, extra_out = hot ? R * H : 0;
+  // ping-pong counts: the buffers of the next batch, cleared by this batch's apply pass
+  const at::Tensor* cin_n = cIn_next ? &*cIn_next : nullptr;
+  const at::Tensor* cout_n = cOut_next ? &*cOut_next : nullptr;
+  for (const at::Tensor* t : {cin_n, cout_n})
+    if (t) {
+      CHECK_DEV((*t));
+      CHECK_DTYPE((*t), at::kFloat);
+      TORCH_CHECK(t->is_contiguous(), "contiguous tensors required");
+    }
+  TORCH_CHECK((!cin_n || cin_n->numel() == cIn.numel()) && (!cout_n || cout_n->numel() == cOut.numel()),
+              "next count buffers must match the current ones");
+  TORCH_CHECK(gIn.sizes() == Win.sizes() && gOut.sizes() == Wout.sizes() && cIn.numel() == Win.size(0) + extra_in &&
+                  cOut.numel() == Wout.size(0) + extra_out, "gradient / count buffers must match the tables");
   TORCH_CHECK(aprob.numel() == V && alias.numel() == V, "alias table must have V entries");
   TORCH_CHECK(centre.numel() == context.numel(), "centre / context lengths");
   TORCH_CHECK(neg >= 0 && neg <= 64, "0 <= neg <= 64");
@@ -784,6 +814,9 @@ void sgns_step(at::Tensor& Win, at::Tensor& Wout, at::Tensor& gIn, at::Tensor& g
                  cIn.data_ptr<float>(), cOut.data_ptr<float>(), (int)dim, Win.size(0), centre.data_ptr<int>(),
                  context.data_ptr<int>(), centre.numel(), aprob.data_ptr<float>(), alias.data_ptr<int>(), (int)V,
                  (int)neg, (float)lr, mean_in ? 1 : 0, (unsigned long long)seed, (unsigned long long)step,
+                 hot ? hot->data_ptr<int>() : nullptr, (int)H, hot ? gOutHot->data_ptr<float>() : nullptr,
+                 (hot && gInHot) ? gInHot->data_ptr<float>() : nullptr, cin_n ? cin_n->data_ptr<float>() : nullptr,
+                 cin_n ? cin_n->numel() : 0, cout_n ? cout_n->data_ptr<float>() : nullptr, cout_n ? cout_n->numel() : 0,
                  cur_stream(Win));
 }
 
@@ -2812,7 +2845,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("tfidf_rows", &tfidf_rows);
   m.def("mixed_knn", &mixed_knn);
   m.def("pagerank", &pagerank);
-  m.def("sgns_step", &sgns_step);
+  m.def("sgns_hot_replicas", &avk::sgns_hot_replicas);
+  m.def("sgns_step", &sgns_step, py::arg("Win"), py::arg("Wout"), py::arg("gIn"), py::arg("gOut"), py::arg("cIn"),
+        py::arg("cOut"), py::arg("centre"), py::arg("context"), py::arg("aprob"), py::arg("alias"), py::arg("neg"),
+        py::arg("lr"), py::arg("mean_in"), py::arg("seed"), py::arg("step"), py::arg("hot") = py::none(),
+        py::arg("gOutHot") = py::none(), py::arg("gInHot") = py::none(), py::arg("cIn_next") = py::none(),
+        py::arg("cOut_next") = py::none());
   m.def("kendall_pairs", &kendall_pairs);
   m.def("resample_uniform", &resample_uniform);
   m.def("smote", &smote);

@@ -292,8 +292,11 @@ void tfidf_rows(const long long* crow, const long long* col, float* val, const f
                 int sublinear, int norm, hipStream_t stream);
 int pagerank_max_n();
 void pagerank(const double* P, int n, double d, int iters, double tol, double* r, int* it, hipStream_t stream);
+int sgns_hot_replicas();
 void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, float* cOut, int dim, long long rows_in,
                const int* centre, const int* context, long long n_pairs, const float* aprob, const int* alias, int V,
-               int neg, float lr, int mean_in, unsigned long long seed, unsigned long long step, hipStream_t stream);
+               int neg, float lr, int mean_in, unsigned long long seed, unsigned long long step, const int* hot, int H,
+               float* gOutHot, float* gInHot, float* cIn_next, long long n_cin, float* cOut_next, long long n_cout,
+               hipStream_t stream);
 
 }  // namespace avk

@@ -90,6 +90,13 @@ __global__ __launch_bounds__(PR_T) void pagerank_kernel(const double* __restrict
   if (tid == 0) *it_out = it;
 }
 
+// Hot rows: the negatives follow unigram^0.75 and the contexts / centres the unigram itself, so a
+// few frequent words collect most of a batch's gradient atomics, all on the same addresses (the
+// grad kernel was 82 % of an epoch, serialised on them).  Rows with hot[row] = s >= 0 (the H most
+// probable words) accumulate instead into SG_R replicas [SG_R][H][dp] chosen by the pair index,
+// counts likewise after the table's rows; the apply pass folds the replicas back (and zeroes them).
+constexpr int SG_R = 16;
+
 // alias table: prob[V] (float), alias[V] (int); draw: k = u1 * V, take k if u2 < prob[k] else alias[k].
 // One mini-batch: every pair's gradients are ADDED into gIn / gOut with per-row counts (float
 // atomics); sgns_apply_kernel then moves each touched row by the MEAN of its updates.  A device
@@ -103,10 +110,13 @@ __global__ __launch_bounds__(256) void sgns_grad_kernel(const float* __restrict_
                                                         const int* __restrict__ centre, const int* __restrict__ context,
                                                         long long n_pairs, const float* __restrict__ aprob,
                                                         const int* __restrict__ alias, int V, int neg, float lr,
-                                                        unsigned long long seed, unsigned long long step) {
+                                                        unsigned long long seed, unsigned long long step,
+                                                        const int* __restrict__ hot, int H, float* __restrict__ gOutHot,
+                                                        float* __restrict__ gInHot, long long rows_in) {
   const long long pr = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pr >= n_pairs) return;
   const int lane = threadIdx.x & 63;
+  const int rep = (int)(pr & (SG_R - 1));
   const int c = centre[pr];
   const float* wc = Win + (long long)c * (DV * 64);
   float v[DV], grad[DV];
@@ -138,30 +148,54 @@ __global__ __launch_bounds__(256) void sgns_grad_kernel(const float* __restrict_
     }
     dot = av::wave_sum(dot);
     const float g = (label - 1.f / (1.f + __expf(-dot))) * lr;
-    float* go = gOut + (long long)o * (DV * 64);
+    int hs = hot ? hot[o] : -1;
+    hs = hs < H ? hs : -1;
+    float* go = hs >= 0 ? gOutHot + (long long)(rep * H + hs) * (DV * 64) : gOut + (long long)o * (DV * 64);
 #pragma unroll
     for (int k = 0; k < DV; ++k) {
       grad[k] += g * u[k];
       atomicAdd(&go[lane + 64 * k], g * v[k]);
     }
-    if (lane == 0) atomicAdd(&cOut[o], 1.f);
+    if (lane == 0) atomicAdd(&cOut[hs >= 0 ? (long long)V + rep * H + hs : (long long)o], 1.f);
   }
-  float* gc = gIn + (long long)c * (DV * 64);
+  int hc = (hot && gInHot) ? hot[c] : -1;
+  hc = hc < H ? hc : -1;
+  float* gc = hc >= 0 ? gInHot + (long long)(rep * H + hc) * (DV * 64) : gIn + (long long)c * (DV * 64);
 #pragma unroll
   for (int k = 0; k < DV; ++k) atomicAdd(&gc[lane + 64 * k], grad[k]);
-  if (lane == 0) atomicAdd(&cIn[c], 1.f);
+  if (lane == 0) atomicAdd(&cIn[hc >= 0 ? rows_in + rep * H + hc : (long long)c], 1.f);
 }
 
-// W[r] += g[r] / max(count[r], 1) (mean_in: the centre table of doc2vec sums instead), g -> 0
+// W[r] += g[r] / max(count[r], 1) (mean_in: the centre table of doc2vec sums instead), g -> 0;
+// hot rows (hot[r] = s >= 0, gHot != null) first fold their SG_R replicas (zeroing them) and
+// counts (stored after the table's rows; zeroed by the caller with the counts)
 __global__ __launch_bounds__(256) void sgns_apply_kernel(float* __restrict__ W, float* __restrict__ g,
                                                          const float* __restrict__ cnt, long long rows, int dp,
-                                                         int mean) {
+                                                         int mean, const int* __restrict__ hot, int H,
+                                                         float* __restrict__ gHot, float* __restrict__ zero_next,
+                                                         long long n_zero) {
   const long long total = rows * dp;
   const long long stride = (long long)gridDim.x * 256;
+  // the other count buffer (ping-pong: the previous batch's, no longer read) is cleared for the next
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; zero_next && i < n_zero; i += stride)
+    zero_next[i] = 0.f;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
-    const float gv = g[i];
+    const long long r = i / dp;
+    float gv = g[i];
+    float cv = cnt[r];
+    const int hs = (hot && gHot) ? hot[r] : -1;
+    if (hs >= 0 && hs < H) {
+      const int col = (int)(i - r * dp);
+#pragma unroll 4
+      for (int q = 0; q < SG_R; ++q) {
+        float* p = gHot + (long long)(q * H + hs) * dp + col;
+        gv += *p;
+        *p = 0.f;
+        cv += cnt[rows + q * H + hs];
+      }
+    }
     if (gv != 0.f) {
-      W[i] += mean ? gv / fmaxf(cnt[i / dp], 1.f) : gv;
+      W[i] += mean ? gv / fmaxf(cv, 1.f) : gv;
       g[i] = 0.f;
     }
   }
@@ -187,13 +221,17 @@ void pagerank(const double* P, int n, double d, int iters, double tol, double* r
   AV_HIP_CHECK(hipGetLastError());
 }
 
+int sgns_hot_replicas() { return SG_R; }
+
 void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, float* cOut, int dim, long long rows_in,
                const int* centre, const int* context, long long n_pairs, const float* aprob, const int* alias, int V,
-               int neg, float lr, int mean_in, unsigned long long seed, unsigned long long step, hipStream_t stream) {
+               int neg, float lr, int mean_in, unsigned long long seed, unsigned long long step, const int* hot, int H,
+               float* gOutHot, float* gInHot, float* cIn_next, long long n_cin, float* cOut_next, long long n_cout,
+               hipStream_t stream) {
   if (n_pairs <= 0) return;
   const unsigned grid = (unsigned)((n_pairs + 3) / 4);
 #define AV_SG(DV) sgns_grad_kernel<DV><<<grid, 256, 0, stream>>>(Win, Wout, gIn, gOut, cIn, cOut, centre, context, \
-      n_pairs, aprob, alias, V, neg, lr, seed, step)
+      n_pairs, aprob, alias, V, neg, lr, seed, step, hot, H, gOutHot, gInHot, rows_in)
   switch (dim) {
     case 64: AV_SG(1); break;
     case 128: AV_SG(2); break;
@@ -204,9 +242,12 @@ void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, flo
 #undef AV_SG
   AV_HIP_CHECK(hipGetLastError());
   sgns_apply_kernel<<<av::stream_grid(rows_in * dim, 256, 4, 4096), 256, 0, stream>>>(Win, gIn, cIn, rows_in, dim,
-                                                                                       mean_in);
+                                                                                       mean_in, hot, H, gInHot,
+                                                                                       cIn_next, n_cin);
   AV_HIP_CHECK(hipGetLastError());
-  sgns_apply_kernel<<<av::stream_grid((long long)V * dim, 256, 4, 4096), 256, 0, stream>>>(Wout, gOut, cOut, V, dim, 1);
+  sgns_apply_kernel<<<av::stream_grid((long long)V * dim, 256, 4, 4096), 256, 0, stream>>>(Wout, gOut, cOut, V, dim, 1,
+                                                                                           hot, H, gOutHot, cOut_next,
+                                                                                           n_cout);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -382,8 +382,17 @@ class Word2Vec:
             assert int(cen.min()) >= 0 and int(cen.max()) < Win.shape[0] and int(ctx.min()) >= 0 and int(ctx.max()) < V
         cen, ctx = cen.to(self.device).int(), ctx.to(self.device).int()
         gIn, gOut = torch.zeros_like(Win), torch.zeros_like(Wout)
-        cIn = torch.zeros(Win.shape[0], device=self.device)
-        cOut = torch.zeros(V, device=self.device)
+        # hot rows (sgns kernels): the H most probable noise words accumulate into R replicas
+        R = _native.C().sgns_hot_replicas()
+        H = min(V, 256)
+        hot = torch.full((V,), -1, dtype=torch.int32, device=self.device)
+        hot[torch.topk(self.noise, H).indices] = torch.arange(H, dtype=torch.int32, device=self.device)
+        words_in = mean_in and Win.shape[0] == V        # word2vec: the centre table is over word ids
+        gOutHot = torch.zeros((R, H, Wout.shape[1]), device=self.device)
+        gInHot = torch.zeros_like(gOutHot) if words_in else None
+        # ping-pong count buffers: a batch's apply pass clears the other pair for the next batch
+        cIns = [torch.zeros(Win.shape[0] + (R * H if words_in else 0), device=self.device) for _ in range(2)]
+        cOuts = [torch.zeros(V + R * H, device=self.device) for _ in range(2)]
         nb = max(1, (n + self.batch - 1) // self.batch)
         total, step = self.epochs * nb, 0
         C = _native.C()
@@ -393,10 +402,11 @@ class Word2Vec:
             lr_ep = self.lr * (1 - ep / self.epochs)
             for b in range(0, n, self.batch):
                 lr = self.lr * max(1e-4, 1 - step / total) if decay_per_batch else lr_ep
-                C.sgns_step(Win, Wout, gIn, gOut, cIn, cOut, c_ep[b:b + self.batch], o_ep[b:b + self.batch],
-                            aprob, alias, int(self.negative), float(lr), bool(mean_in), int(self.seed), step)
-                cIn.zero_()
-                cOut.zero_()
+                cur, nxt = step & 1, (step + 1) & 1
+                C.sgns_step(Win, Wout, gIn, gOut, cIns[cur], cOuts[cur], c_ep[b:b + self.batch],
+                            o_ep[b:b + self.batch], aprob, alias, int(self.negative), float(lr), bool(mean_in),
+                            int(self.seed), step, hot=hot, gOutHot=gOutHot, gInHot=gInHot, cIn_next=cIns[nxt],
+                            cOut_next=cOuts[nxt])
                 step += 1
 
     def fit(self, sentences: Sequence[Sequence[str]]) -> "Word2Vec":
