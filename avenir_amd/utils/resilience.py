@@ -103,6 +103,10 @@ class IterationLoop:
             return 0, None, None
         if self.sharded:
             self._check_shard_set()
+            # no rank may commit its first shard while another is still listing the directory
+            # (a fast rank's fresh rank<r>.ckpt would read as a foreign partial shard set)
+            if self.comm.world > 1:
+                self.comm.barrier()
         if not p.exists():
             return 0, None, None
         t, m = ckpt.load(p, device or self.device or "cpu")
