@@ -1,3 +1,5 @@
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <chrono>
 #include <map>
@@ -1980,7 +1982,33 @@ struct StagingRing {
   std::mutex mu;
   void* buf[SLOTS] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done[SLOTS];
+  hipStream_t side = nullptr;   // second DMA queue (AVMI_UPLOAD_STREAMS=2, default): odd slots copy on it
+  hipEvent_t side_done = nullptr;
 };
+
+static int upload_streams() {  // default 2 (measured 30.6 -> 32.7 GB/s at 16 threads)
+  const char* e = std::getenv("AVMI_UPLOAD_STREAMS");
+  return (e && std::atoi(e) == 1) ? 1 : 2;
+}
+
+// DMA of slot k: on ``main`` or (two-queue mode, odd k) on the ring's side stream.
+static void ring_dma(StagingRing& R, int slot, int64_t k, uint8_t* dst, int64_t len, hipStream_t main, int ns) {
+  hipStream_t s = main;
+  if (ns == 2 && (k & 1)) {
+    if (!R.side) BIND_HIP_CHECK(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
+    s = R.side;
+  }
+  BIND_HIP_CHECK(hipMemcpyAsync(dst, R.buf[slot], (size_t)len, hipMemcpyHostToDevice, s));
+  BIND_HIP_CHECK(hipEventRecord(R.done[slot], s));
+}
+
+// the caller's stream waits for every side-stream copy of this upload
+static void ring_join(StagingRing& R, hipStream_t main) {
+  if (!R.side) return;
+  if (!R.side_done) BIND_HIP_CHECK(hipEventCreateWithFlags(&R.side_done, hipEventDisableTiming));
+  BIND_HIP_CHECK(hipEventRecord(R.side_done, R.side));
+  BIND_HIP_CHECK(hipStreamWaitEvent(main, R.side_done, 0));
+}
 
 static StagingRing& staging_ring(int device) {
   static std::mutex reg_mu;
@@ -1996,6 +2024,40 @@ static StagingRing& staging_ring(int device) {
     }
   }
   return *r;
+}
+
+// Host threads filling one staging slot (AVMI_UPLOAD_THREADS, default 16, 1..32; MI355X box:
+// 8 -> 16 threads took the 2.5 GB churn CSV load from 0.10 to 0.08 s, profiles/r3_csv_upload_sweep.jsonl).
+static int upload_threads() {
+  const char* e = std::getenv("AVMI_UPLOAD_THREADS");
+  const int t = e ? std::atoi(e) : 16;
+  return std::max(1, std::min(t, 32));
+}
+
+// AVMI_UPLOAD_MODE=mmap: copy from a mapping of the file (page faults on every source page);
+// default pread: each thread reads its part of the slot straight into the pinned buffer.
+static bool upload_pread() {
+  const char* e = std::getenv("AVMI_UPLOAD_MODE");
+  return !(e && std::string(e) == "mmap");
+}
+
+// bytes [off, off + len) of fd into dst with T threads; pread may return short counts
+static void pread_parallel(int fd, char* dst, int64_t off, int64_t len, int T) {
+  std::vector<std::thread> th;
+  std::atomic<bool> bad{false};
+  auto part = [&](int t) {
+    int64_t a = len * t / T;
+    const int64_t b = len * (t + 1) / T;
+    while (a < b) {
+      const ssize_t r = ::pread(fd, dst + a, (size_t)(b - a), (off_t)(off + a));
+      if (r <= 0) { bad = true; return; }
+      a += r;
+    }
+  };
+  for (int t = 1; t < T; ++t) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+  TORCH_CHECK(!bad, "pread failed during the device upload");
 }
 
 static uint32_t fnv1a_fold(const std::string& v) {
@@ -2020,9 +2082,16 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
   hipStream_t stream = cur_stream(like);
   if (padded > size) BIND_HIP_CHECK(hipMemsetAsync(dev.data_ptr<uint8_t>() + size, 0, padded - size, stream));
   if (size > 0) {
-    const char* map = static_cast<const char*>(mmap(nullptr, (size_t)size, PROT_READ, MAP_PRIVATE, fd, 0));
-    TORCH_CHECK(map != MAP_FAILED, "mmap failed for ", path);
-    madvise(const_cast<char*>(map), (size_t)size, MADV_SEQUENTIAL);
+    py::gil_scoped_release rel;
+    const bool use_pread = upload_pread();
+    const int T = upload_threads();
+    const int NS = upload_streams();
+    const char* map = nullptr;
+    if (!use_pread) {
+      map = static_cast<const char*>(mmap(nullptr, (size_t)size, PROT_READ, MAP_PRIVATE, fd, 0));
+      TORCH_CHECK(map != MAP_FAILED, "mmap failed for ", path);
+      madvise(const_cast<char*>(map), (size_t)size, MADV_SEQUENTIAL);
+    }
     StagingRing& R = staging_ring(like.device().index());
     std::lock_guard<std::mutex> hold(R.mu);  // one upload at a time per device ring
     void** ring = R.buf;
@@ -2034,9 +2103,10 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
       const int slot = (int)(k % SLOTS);
       const int64_t len = std::min(SLOT, size - off);
       if (k >= SLOTS) BIND_HIP_CHECK(hipEventSynchronize(done[slot]));  // the slot's last DMA is done
-      {  // page cache -> pinned slot with 4 threads
+      if (use_pread) {  // page cache -> pinned slot, T threads, no source page faults
+        pread_parallel(fd, static_cast<char*>(ring[slot]), off, len, T);
+      } else {
         std::vector<std::thread> th;
-        const int T = 4;
         for (int t = 0; t < T; ++t)
           th.emplace_back([&, t] {
             const int64_t a = len * t / T, b = len * (t + 1) / T;
@@ -2044,11 +2114,10 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
           });
         for (auto& x : th) x.join();
       }
-      BIND_HIP_CHECK(hipMemcpyAsync(dev.data_ptr<uint8_t>() + off, ring[slot], (size_t)len, hipMemcpyHostToDevice,
-                                  stream));
-      BIND_HIP_CHECK(hipEventRecord(done[slot], stream));
+      ring_dma(R, slot, k, dev.data_ptr<uint8_t>() + off, len, stream, NS);
     }
-    munmap(const_cast<char*>(map), (size_t)size);
+    ring_join(R, stream);
+    if (map) munmap(const_cast<char*>(map), (size_t)size);
   }
   ::close(fd);
   // ---- line index ----
@@ -2504,6 +2573,7 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
     StagingRing& R = staging_ring(like.device().index());
     std::lock_guard<std::mutex> hold(R.mu);
     for (int i = 0; i < SLOTS; ++i) BIND_HIP_CHECK(hipEventSynchronize(R.done[i]));
+    const int NS = upload_streams();
     int64_t out = 0, k = 0;
     size_t pi = 0;
     int64_t pofs = 0;
@@ -2516,7 +2586,7 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
       while (fill < SLOT && pi < pieces.size()) {
         const int64_t n = std::min(SLOT - fill, pieces[pi].len - pofs);
         const char* src = pieces[pi].p + pofs;
-        const int T = n >= (8 << 20) ? 8 : 1;
+        const int T = n >= (8 << 20) ? upload_threads() : 1;
         std::vector<std::thread> th;
         for (int t = 1; t < T; ++t)
           th.emplace_back([&, t] {
@@ -2529,12 +2599,11 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
         pofs += n;
         if (pofs == pieces[pi].len) { ++pi; pofs = 0; }
       }
-      BIND_HIP_CHECK(hipMemcpyAsync(dev.data_ptr<uint8_t>() + out, R.buf[slot], (size_t)fill, hipMemcpyHostToDevice,
-                                    stream));
-      BIND_HIP_CHECK(hipEventRecord(R.done[slot], stream));
+      ring_dma(R, slot, k, dev.data_ptr<uint8_t>() + out, fill, stream, NS);
       out += fill;
       ++k;
     }
+    ring_join(R, stream);
   }
   sh.reset();
   auto t1 = std::chrono::steady_clock::now();

@@ -101,6 +101,10 @@ def _ingest(rows: int, schema, dev, comm) -> dict:
         def load():
             nonlocal t
             t = load_csv(path, schema, device=dev, rank=0, world=1)
+        # the first load of a process also allocates the pinned staging ring (one-time, reported
+        # apart); the job rate is a full re-parse + upload of the file on a warm process
+        out["first_load_s"] = _timed(load, dev)
+        t = None
         out["load_s"] = _timed(load, dev)
         nb = NaiveBayes(schema)
         out["fit_s"] = _timed(lambda: nb.fit(t), dev)
