@@ -723,26 +723,28 @@ py::tuple mixed_knn(const at::Tensor& Qn, const at::Tensor& Qc, const at::Tensor
 }
 
 // K28 text kernels (text.hip)
-void tfidf_rows(const at::Tensor& crow, const at::Tensor& col, at::Tensor& val, const at::Tensor& idf, bool sublinear,
-                int64_t norm) {
+// K28 TF-IDF (text.hip): val (float counts, contiguous) is weighted and normalised in place;
+// returns the document frequencies.  Index checks run on the device; one status read per call.
+at::Tensor tfidf_csr(const at::Tensor& crow, const at::Tensor& col, at::Tensor& val, int64_t V, bool smooth,
+                     bool sublinear, int64_t norm) {
   CHECK_DEV(crow); CHECK_DTYPE(crow, at::kLong);
   CHECK_DEV(col); CHECK_DTYPE(col, at::kLong);
   CHECK_DEV(val); CHECK_DTYPE(val, at::kFloat);
-  CHECK_DEV(idf); CHECK_DTYPE(idf, at::kFloat);
   TORCH_CHECK(crow.dim() == 1 && crow.numel() >= 1 && col.numel() == val.numel() && val.is_contiguous() &&
                   col.is_contiguous() && crow.is_contiguous(), "CSR arrays");
   TORCH_CHECK(norm >= 0 && norm <= 2, "norm: 0 none, 1 l1, 2 l2");
-  const int64_t nnz = col.numel();
-  if (nnz) {
-    // column ids index idf; row pointers must be monotone within [0, nnz] (one host check per call:
-    // TF-IDF is built once per corpus)
-    TORCH_CHECK(col.min().item<int64_t>() >= 0 && col.max().item<int64_t>() < idf.numel(), "column id out of range");
-  }
-  TORCH_CHECK(crow[0].item<int64_t>() == 0 && crow[-1].item<int64_t>() == nnz, "crow must span [0, nnz]");
+  TORCH_CHECK(V >= 1, "vocabulary size >= 1");
   DevGuard gd(val.device());
-  avk::tfidf_rows(reinterpret_cast<const long long*>(crow.data_ptr<int64_t>()),
-                  reinterpret_cast<const long long*>(col.data_ptr<int64_t>()), val.data_ptr<float>(),
-                  idf.data_ptr<float>(), crow.numel() - 1, sublinear ? 1 : 0, (int)norm, cur_stream(val));
+  auto df = at::zeros({V}, val.options().dtype(at::kInt));
+  auto status = at::zeros({1}, val.options().dtype(at::kInt));
+  avk::tfidf_csr(reinterpret_cast<const long long*>(crow.data_ptr<int64_t>()),
+                 reinterpret_cast<const long long*>(col.data_ptr<int64_t>()), val.data_ptr<float>(),
+                 crow.numel() - 1, col.numel(), V, smooth ? 1 : 0, sublinear ? 1 : 0, (int)norm,
+                 df.data_ptr<int>(), status.data_ptr<int>(), cur_stream(val));
+  const int st = status.item<int>();
+  TORCH_CHECK(!(st & 1), "tfidf: column id out of range [0, ", V, ")");
+  TORCH_CHECK(!(st & 2), "tfidf: row pointers must be monotone within [0, nnz]");
+  return df;
 }
 
 py::tuple pagerank(const at::Tensor& P, double d, int64_t iters, double tol) {
@@ -2911,7 +2913,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbt_grad", &gbt_grad);
   m.def("gbt_split", &gbt_split);
   m.def("rank_avg", &rank_avg);
-  m.def("tfidf_rows", &tfidf_rows);
+  m.def("tfidf_csr", &tfidf_csr);
   m.def("mixed_knn", &mixed_knn);
   m.def("pagerank", &pagerank);
   m.def("sgns_hot_replicas", &avk::sgns_hot_replicas);

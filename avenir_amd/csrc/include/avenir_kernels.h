@@ -288,8 +288,10 @@ void rank_avg(const double* sorted, const long long* perm, long long n, const in
 void kendall_pairs(const double* x, const double* y, long long n, unsigned long long* out, hipStream_t stream);
 
 // text.hip (K28)
-void tfidf_rows(const long long* crow, const long long* col, float* val, const float* idf, long long n_rows,
-                int sublinear, int norm, hipStream_t stream);
+// TF-IDF of a CSR count matrix in place: document frequencies (df, V zeroed ints) then the
+// weighted, normalised rows; status bit 1 = column id out of range, 2 = bad row pointers
+void tfidf_csr(const long long* crow, const long long* col, float* val, long long n_rows, long long nnz, long long V,
+               int smooth, int sublinear, int norm, int* df, int* status, hipStream_t stream);
 int pagerank_max_n();
 void pagerank(const double* P, int n, double d, int iters, double tol, double* r, int* it, hipStream_t stream);
 int sgns_hot_replicas();

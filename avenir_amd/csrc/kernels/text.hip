@@ -4,9 +4,17 @@
 // Reference: python/text/preprocess.py:380-524 (TfIdf / term-frequency vectors, host Counters),
 // python/text/summ.py TextRank (networkx pagerank over a sentence-similarity graph) and
 // python/text/wv.py:36-153 (gensim word2vec / doc2vec).
-//   * tfidf_rows_kernel : one wavefront per document row of the CSR count matrix: w = tf * idf[col]
-//     (tf = count, or 1 + ln count when sublinear — scikit-learn's sublinear_tf), then the row's L2 (or L1) norm as a wave reduction and the
-//     normalised weights written in place — one pass instead of densify + 4 tensor ops.
+//   * tfidf_df_kernel   : document frequencies of a CSR count matrix (every column id once per row):
+//     a workgroup counts a chunk of <= 65,535 entries into an LDS table of 16-bit counters (two per
+//     word, 65,536 ids per 128 KB window, up to 4 windows re-reading the L2-resident chunk) and
+//     flushes one global atomic per non-zero bin, so a hot word costs one atomic per chunk instead
+//     of one per document (a global-atomic bincount serialises every occurrence on one address);
+//     ids past the windows use global atomics.
+//   * tfidf_rows_kernel : one wavefront per document row: w = tf * idf(df[col]) with the idf formula
+//     inline (smooth: ln((1+D)/(1+df)) + 1, else ln(D/df) + 1; tf = count, or 1 + ln count when
+//     sublinear — scikit-learn's sublinear_tf), then the row's L2 (or L1) norm as a wave reduction and
+//     the normalised weights written in place.  Both kernels check their indices on the device and
+//     raise a status bit instead of touching memory out of range; the binding reads it once.
 //   * pagerank_kernel   : the whole power iteration in ONE persistent workgroup: r lives in LDS,
 //     every iteration is a column sweep of the row-stochastic matrix (thread j owns columns
 //     j, j + 1024, ... — consecutive threads read consecutive addresses of a row), and the L1
@@ -19,23 +27,76 @@
 //     d <= 256 (each lane owns d / 64 coordinates).  PV-DBOW (doc2vec) is the same pair kernel
 //     with the document matrix as the centre table (summed, not averaged: few rows per doc).
 // Index safety: CSR column ids < V (checked by the binding), alias indices < V, pair ids < V / D.
+#include <algorithm>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
 namespace {
 
+constexpr int DF_T = 512;
+constexpr int DF_WIN = 65536;            // column ids per LDS window: two 16-bit counters per word (128 KB)
+constexpr int DF_CHUNK = 65535;          // nnz per chunk: a 16-bit counter cannot carry into its neighbour
+constexpr int DF_MAX_WIN = 4;            // ids >= 4 * 65536 are counted with global atomics
+
+__global__ __launch_bounds__(DF_T) void tfidf_df_kernel(const long long* __restrict__ col, long long nnz, long long V,
+                                                        int* __restrict__ df, int* __restrict__ status) {
+  __shared__ unsigned h[DF_WIN / 2];
+  const int nwin = (int)min<long long>((V + DF_WIN - 1) / DF_WIN, DF_MAX_WIN);
+  const long long lds_end = (long long)nwin * DF_WIN;
+  int bad = 0;
+  for (long long c0 = (long long)blockIdx.x * DF_CHUNK; c0 < nnz; c0 += (long long)gridDim.x * DF_CHUNK) {
+    const long long c1 = min(nnz, c0 + DF_CHUNK);
+    for (int w = 0; w < nwin; ++w) {
+      for (int i = threadIdx.x; i < DF_WIN / 2; i += DF_T) h[i] = 0u;
+      __syncthreads();
+      const long long lo = (long long)w * DF_WIN, hi = lo + DF_WIN;
+      for (long long k = c0 + threadIdx.x; k < c1; k += DF_T) {
+        const long long c = col[k];
+        if (c < 0 || c >= V) {
+          bad = 1;                        // never counted
+        } else if (c >= lo && c < hi) {
+          const int b = (int)(c - lo);
+          atomicAdd(&h[b >> 1], 1u << ((b & 1) * 16));
+        } else if (w == 0 && c >= lds_end) {  // ids past the LDS windows, once
+          atomicAdd(df + c, 1);
+        }
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < DF_WIN / 2; i += DF_T) {
+        const unsigned v = h[i];
+        if (v & 0xFFFFu) atomicAdd(df + lo + 2 * i, (int)(v & 0xFFFFu));
+        if (v >> 16) atomicAdd(df + lo + 2 * i + 1, (int)(v >> 16));
+      }
+      __syncthreads();
+    }
+  }
+  if (bad) atomicOr(status, 1);
+}
+
 __global__ __launch_bounds__(256) void tfidf_rows_kernel(const long long* __restrict__ crow,
                                                          const long long* __restrict__ col, float* __restrict__ val,
-                                                         const float* __restrict__ idf, long long n_rows, int sublinear,
-                                                         int norm) {
+                                                         const int* __restrict__ df, long long n_rows, long long nnz,
+                                                         long long V, float n_docs, int smooth, int sublinear, int norm,
+                                                         int* __restrict__ status) {
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_rows) return;
   const int lane = threadIdx.x & 63;
   const long long b = crow[row], e = crow[row + 1];
+  if (b < 0 || e > nnz || b > e) {
+    if (lane == 0) atomicOr(status, 2);
+    return;
+  }
   float acc = 0.f;
   for (long long k = b + lane; k < e; k += 64) {
+    const long long c = col[k];
     const float tf = sublinear ? (val[k] > 0.f ? 1.f + logf(val[k]) : 0.f) : val[k];
-    const float w = tf * idf[col[k]];
+    float idf = 0.f;
+    if (c >= 0 && c < V) {
+      const float d = (float)df[c];
+      idf = smooth ? logf((1.f + n_docs) / (1.f + d)) + 1.f : logf(n_docs / fmaxf(d, 1.f)) + 1.f;
+    }
+    const float w = tf * idf;
     val[k] = w;
     acc += norm == 2 ? w * w : fabsf(w);
   }
@@ -205,10 +266,16 @@ __global__ __launch_bounds__(256) void sgns_apply_kernel(float* __restrict__ W, 
 
 namespace avk {
 
-void tfidf_rows(const long long* crow, const long long* col, float* val, const float* idf, long long n_rows,
-                int sublinear, int norm, hipStream_t stream) {
+void tfidf_csr(const long long* crow, const long long* col, float* val, long long n_rows, long long nnz, long long V,
+               int smooth, int sublinear, int norm, int* df, int* status, hipStream_t stream) {
+  if (nnz > 0) {
+    const long long blocks = std::min<long long>(1024, (nnz + DF_CHUNK - 1) / DF_CHUNK);
+    tfidf_df_kernel<<<(unsigned)blocks, DF_T, 0, stream>>>(col, nnz, V, df, status);
+    AV_HIP_CHECK(hipGetLastError());
+  }
   if (n_rows <= 0) return;
-  tfidf_rows_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, stream>>>(crow, col, val, idf, n_rows, sublinear, norm);
+  tfidf_rows_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, stream>>>(crow, col, val, df, n_rows, nnz, V,
+                                                                      (float)n_rows, smooth, sublinear, norm, status);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -480,16 +480,14 @@ def doc_term_matrix(docs: Sequence[Sequence[str]], vocab: Vocabulary, device="cp
 
 
 def tfidf_csr(counts: torch.Tensor, smooth: bool = True, sublinear: bool = False, norm: str | None = "l2"):
-    """Sparse CSR TF-IDF [D, V] from a CSR count matrix on the GPU: document frequencies by one
-    bincount of the column ids, then ONE ``tfidf_rows`` launch (text.hip: a wavefront per row
-    weights its entries and normalises them in place)."""
+    """Sparse CSR TF-IDF [D, V] from a CSR count matrix on the GPU: two K28 launches (text.hip):
+    document frequencies by an LDS-privatised count of the column ids, then a wavefront per row
+    weights its entries (idf inline) and normalises them in place; index checks on the device."""
     from .. import _native
     D, V = counts.shape
     crow, col = counts.crow_indices().contiguous(), counts.col_indices().contiguous()
     val = counts.values().float().clone().contiguous()
-    df = torch.bincount(col, minlength=V).float()
-    idf = (torch.log((1 + D) / (1 + df)) + 1 if smooth else torch.log(D / df.clamp_min(1)) + 1).float().contiguous()
-    _native.C().tfidf_rows(crow, col, val, idf, bool(sublinear), {None: 0, "l1": 1, "l2": 2}[norm])
+    _native.C().tfidf_csr(crow, col, val, int(V), bool(smooth), bool(sublinear), {None: 0, "l1": 1, "l2": 2}[norm])
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         return torch.sparse_csr_tensor(crow, col, val, size=(D, V))

@@ -156,6 +156,37 @@ def test_tfidf_kernel_matches_sklearn(cuda):
 
 
 @pytest.mark.gpu
+def test_tfidf_csr_large_vocab_and_range_checks(cuda):
+    """Zipf columns over V > 32768 (LDS-counted hot ids + global-atomic tail) against sklearn's
+    TfidfTransformer, smooth and unsmoothed idf; out-of-range ids fail loudly."""
+    import scipy.sparse as sp
+    from sklearn.feature_extraction.text import TfidfTransformer
+
+    from avenir_amd.text.preprocess import tfidf_csr
+    rng = np.random.default_rng(3)
+    D, V, per = 3000, 40000, 50
+    cols = np.minimum(rng.zipf(1.3, size=D * per) - 1, V - 1)
+    M = sp.csr_matrix((np.ones(D * per, dtype=np.float32), (np.repeat(np.arange(D), per), cols)), shape=(D, V))
+    M.sum_duplicates()
+    G = torch.sparse_csr_tensor(torch.tensor(M.indptr, dtype=torch.long), torch.tensor(M.indices, dtype=torch.long),
+                                torch.tensor(M.data), size=(D, V)).to(cuda)
+    for smooth in (True, False):
+        for sub in (False, True):
+            W = tfidf_csr(G, smooth=smooth, sublinear=sub).to_dense().cpu().numpy()
+            sk = TfidfTransformer(smooth_idf=smooth, sublinear_tf=sub).fit_transform(M).toarray()
+            assert np.allclose(W, sk, atol=1e-6), (smooth, sub)
+    from avenir_amd import _native
+    col = G.col_indices().clone()
+    col[7] = V + 5
+    with pytest.raises(RuntimeError, match="column id out of range"):
+        _native.C().tfidf_csr(G.crow_indices(), col, G.values().clone(), V, True, False, 2)
+    crow = G.crow_indices().clone()
+    crow[5] = crow[6] + 1                                   # a row pointer past its successor
+    with pytest.raises(RuntimeError, match="row pointers"):
+        _native.C().tfidf_csr(crow, G.col_indices(), G.values().clone(), V, True, False, 2)
+
+
+@pytest.mark.gpu
 def test_pagerank_kernel_matches_tensor_path(cuda):
     g = torch.Generator().manual_seed(2)
     for n in (3, 130, 1500):
