@@ -2,6 +2,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -684,6 +685,26 @@ at::Tensor kendall_pairs(const at::Tensor& x, const at::Tensor& y) {
   DevGuard gd(x.device());
   avk::kendall_pairs(x.data_ptr<double>(), y.data_ptr<double>(), x.numel(),
                      reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(x));
+  return out;
+}
+
+// Strict inversions of y f64 [n] (Knight's Kendall discordant count when y is ordered by (x, y)):
+// int64 [1] on the device, no host synchronisation.
+at::Tensor inversion_count(const at::Tensor& y) {
+  CHECK_DEV(y);
+  CHECK_DTYPE(y, at::kDouble);
+  TORCH_CHECK(y.dim() == 1, "y must be [n]");
+  DevGuard gd(y.device());
+  const int64_t n = y.numel();
+  auto out = at::zeros({1}, y.options().dtype(at::kLong));
+  if (n <= 1) return out;
+  int64_t m = avk::inv_merge_block();
+  while (m < n) m <<= 1;
+  auto a = at::full({m}, std::numeric_limits<double>::infinity(), y.options());
+  a.narrow(0, 0, n).copy_(y);
+  auto tmp = at::empty({m}, y.options());
+  avk::inversions(a.data_ptr<double>(), tmp.data_ptr<double>(), m,
+                  reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(y));
   return out;
 }
 
@@ -2923,6 +2944,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gOutHot") = py::none(), py::arg("gInHot") = py::none(), py::arg("cIn_next") = py::none(),
         py::arg("cOut_next") = py::none());
   m.def("kendall_pairs", &kendall_pairs);
+  m.def("inversion_count", &inversion_count);
   m.def("resample_uniform", &resample_uniform);
   m.def("smote", &smote);
   m.def("gbt_assign", &gbt_assign);

@@ -286,6 +286,10 @@ void mixed_knn(const float* Qn, const int* Qc, long long nq, const float* Rn, co
 void rank_avg(const double* sorted, const long long* perm, long long n, const int* group, int n_groups, double* ranks,
               double* tie, double* gsum, hipStream_t stream);
 void kendall_pairs(const double* x, const double* y, long long n, unsigned long long* out, hipStream_t stream);
+// strict inversions of a[0, m) by merge-path merges (m a power of two >= inv_merge_block(), pad
+// with +inf); a / tmp clobbered, returns the one holding the sorted values; inv (u64) += count
+int inv_merge_block();
+double* inversions(double* a, double* tmp, long long m, unsigned long long* inv, hipStream_t stream);
 
 // text.hip (K28)
 // TF-IDF of a CSR count matrix in place: document frequencies (df, V zeroed ints) then the

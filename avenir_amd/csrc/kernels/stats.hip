@@ -16,8 +16,19 @@
 //     discordant, x-tied, y-tied and both-tied pairs in registers (u32 per thread, at most 256
 //     pairs per tile), reduced per workgroup and added to u64 totals — exact integer counts,
 //     O(n^2) work spread over (n / 256)^2 / 2 workgroups.
-// Index safety: binary searches stay in [0, n); perm[i] < n is the caller's permutation of 0..n-1;
+//   * inv_merge_local_kernel / inv_merge_level_kernel : strict inversions of a sequence (Knight's
+//     Kendall count: y ordered by (x, y)) by a bottom-up merge sort whose merges are merge-path
+//     rank computations: a left-run element lands at its index + #(right < v), a right-run element
+//     at its index + #(left <= v) and contributes #(left > v) inversions.  Runs up to 1,024 values
+//     are merged inside one workgroup in LDS (10 levels, one launch), longer runs one launch per
+//     level; counts are wave-reduced into one u64.  O(n log^2 n) work in 1 + log2(n / 1024) launches
+//     (the tensor path was a batched sort + searchsorted per level).
+// Index safety: binary searches stay in [0, n); merge levels work on m = a power of two >= 1024
+// values (padded with +inf by the caller), so every run and its partner lie inside [0, m); perm[i] < n is the caller's permutation of 0..n-1;
 // group ids >= n_groups are ignored; pair tiles only touch rows / columns < n.
+#include <algorithm>
+#include <stdexcept>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -159,6 +170,85 @@ __global__ __launch_bounds__(KT) void kendall_pairs_kernel(const double* __restr
   }
 }
 
+constexpr int IM_T = 1024;
+
+__device__ __forceinline__ int lb_run(const double* v, int n, double key) {   // #(v < key)
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int ub_run(const double* v, int n, double key) {   // #(v <= key)
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] <= key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void inv_add(unsigned long long c, unsigned long long* inv) {
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(inv, c);
+}
+
+// every 1,024-value block of in, sorted through runs of 1, 2, ..., 512 in LDS -> out
+__global__ __launch_bounds__(IM_T) void inv_merge_local_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                               unsigned long long* __restrict__ inv) {
+  __shared__ double buf[2][IM_T];
+  const long long base = (long long)blockIdx.x * IM_T;
+  const int t = threadIdx.x;
+  buf[0][t] = in[base + t];
+  __syncthreads();
+  unsigned long long c = 0;
+  int cur = 0;
+  for (int s = 1; s < IM_T; s <<= 1) {
+    const double* src = buf[cur];
+    const int p = t & ~(2 * s - 1), w = t - p;
+    const double v = src[t];
+    int pos;
+    if (w < s) {
+      pos = w + lb_run(src + p + s, s, v);
+    } else {
+      const int u = ub_run(src + p, s, v);
+      pos = (w - s) + u;
+      c += (unsigned long long)(s - u);
+    }
+    buf[cur ^ 1][p + pos] = v;
+    cur ^= 1;
+    __syncthreads();
+  }
+  out[base + t] = buf[cur][t];
+  inv_add(c, inv);
+}
+
+// one merge level of runs of s (>= 1,024) values: in -> out, m values in all
+__global__ __launch_bounds__(256) void inv_merge_level_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                              long long m, long long s,
+                                                              unsigned long long* __restrict__ inv) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  unsigned long long c = 0;
+  if (i < m) {
+    const long long p = i & ~(2 * s - 1), w = i - p;
+    const double v = in[i];
+    long long pos;
+    if (w < s) {
+      pos = w + lower_bound_d(in + p + s, s, v);
+    } else {
+      const long long u = upper_bound_d(in + p, s, v);
+      pos = (w - s) + u;
+      c = (unsigned long long)(s - u);
+    }
+    out[p + pos] = v;
+  }
+  inv_add(c, inv);
+}
+
 }  // namespace
 
 namespace avk {
@@ -178,6 +268,24 @@ void kendall_pairs(const double* x, const double* y, long long n, unsigned long 
   if (tiles > 0x7fffffffLL) throw std::runtime_error("kendall_pairs: n too large");
   kendall_pairs_kernel<<<(unsigned)tiles, KT, 0, stream>>>(x, y, n, (int)nt, out);
   AV_HIP_CHECK(hipGetLastError());
+}
+
+int inv_merge_block() { return IM_T; }
+
+// strict inversions of a[0, m) (m a power of two >= IM_T); a and tmp are clobbered.  Returns the
+// buffer holding the sorted sequence (a or tmp).
+double* inversions(double* a, double* tmp, long long m, unsigned long long* inv, hipStream_t stream) {
+  if (m < IM_T || (m & (m - 1))) throw std::runtime_error("inversions: m must be a power of two >= 1024");
+  inv_merge_local_kernel<<<(unsigned)(m / IM_T), IM_T, 0, stream>>>(a, tmp, inv);
+  AV_HIP_CHECK(hipGetLastError());
+  double* src = tmp;
+  double* dst = a;
+  for (long long s = IM_T; s < m; s <<= 1) {
+    inv_merge_level_kernel<<<(unsigned)((m + 255) / 256), 256, 0, stream>>>(src, dst, m, s, inv);
+    AV_HIP_CHECK(hipGetLastError());
+    std::swap(src, dst);
+  }
+  return src;
 }
 
 }  // namespace avk

@@ -64,21 +64,26 @@ def _kendall_merge_counts(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     level by level (blocks of 2s: every right-half value's count of larger left-half values by one
     batched searchsorted, then the blocks sorted for the next level) — the discordant pairs, since
     pairs tied in x are ordered by y and never inverted.  Tie pairs from run lengths; concordant =
-    all - discordant - tied.  O(n log^2 n) work in log2 n launches of sort + searchsorted."""
+    all - discordant - tied.  O(n log^2 n) work: on the GPU the merge-path kernels of stats.hip
+    (1 + log2(n / 1024) launches), on the CPU a batched sort + searchsorted per level."""
     n = x.numel()
     o = torch.sort(y, stable=True).indices
     o = o[torch.sort(x[o], stable=True).indices]
     xs, ys = x[o], y[o]
-    m = 1 << max(0, (n - 1).bit_length())
-    cur = torch.cat([ys, torch.full((m - n,), float("inf"), dtype=ys.dtype, device=ys.device)])
-    inv = torch.zeros((), dtype=torch.int64, device=x.device)
-    s = 1
-    while s < m:
-        blk = cur.view(-1, 2, s)
-        L, R = blk[:, 0, :].contiguous(), blk[:, 1, :].contiguous()
-        inv += (s - torch.searchsorted(L, R, right=True)).sum()
-        cur = torch.sort(cur.view(-1, 2 * s), dim=1).values.view(-1)
-        s *= 2
+    if ys.is_cuda:
+        # stats.hip merge-path kernels: runs <= 1024 merged in LDS, then one launch per level
+        inv = _native.C().inversion_count(ys.double().contiguous())[0]
+    else:
+        m = 1 << max(0, (n - 1).bit_length())
+        cur = torch.cat([ys, torch.full((m - n,), float("inf"), dtype=ys.dtype, device=ys.device)])
+        inv = torch.zeros((), dtype=torch.int64, device=x.device)
+        s = 1
+        while s < m:
+            blk = cur.view(-1, 2, s)
+            L, R = blk[:, 0, :].contiguous(), blk[:, 1, :].contiguous()
+            inv += (s - torch.searchsorted(L, R, right=True)).sum()
+            cur = torch.sort(cur.view(-1, 2 * s), dim=1).values.view(-1)
+            s *= 2
     both = _tie_pairs(torch.stack([xs, ys], 1))
     tx = _tie_pairs(xs)
     ty = _tie_pairs(torch.sort(y).values)

@@ -156,3 +156,8 @@ def test_kendall_merge_count_on_device(cuda):
     assert torch.equal(g.cpu(), c)
     small = S.kendall_counts(torch.tensor(x[:20000], device=cuda), torch.tensor(y[:20000], device=cuda), method="pairs")
     assert torch.equal(small.cpu(), S.kendall_counts(torch.tensor(x[:20000]), torch.tensor(y[:20000]), method="merge"))
+    # the merge-path kernels at sizes around the 1,024-value LDS block, against the all-pairs kernel
+    for n in (2, 3, 1000, 1024, 1025, 2048, 5000):
+        gx, gy = torch.tensor(x[:n], device=cuda), torch.tensor(y[:n], device=cuda)
+        assert torch.equal(S.kendall_counts(gx, gy, method="merge").cpu(),
+                           S.kendall_counts(gx, gy, method="pairs").cpu()), n
