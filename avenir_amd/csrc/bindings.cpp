@@ -2269,10 +2269,11 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
   if (!vbytes.empty()) std::memcpy(vb_h.data_ptr<uint8_t>(), vbytes.data(), vbytes.size());
   auto vb_d = vb_h.to(like.device());
   auto bad = at::zeros({1}, like.options().dtype(at::kLong));
-  avk::csv_parse_rows(dev.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(starts.data_ptr<int64_t>()),
+  avk::csv_parse_rows(dev.data_ptr<uint8_t>(), dev.numel(), reinterpret_cast<const long long*>(starts.data_ptr<int64_t>()),
                       reinterpret_cast<const long long*>(ends.data_ptr<int64_t>()), n, delim[0], spec_d.data_ptr<uint8_t>(),
                       (int)sorted.size(), max_ord, tabs_d.data_ptr<int>(), voff_d.data_ptr<int>(), vlen_d.data_ptr<int>(),
-                      vb_d.data_ptr<uint8_t>(), reinterpret_cast<unsigned long long*>(bad.data_ptr<int64_t>()), stream);
+                      vb_d.data_ptr<uint8_t>(), (int)tabs_d.numel(), (int)vlen_d.numel(), (int)vbytes.size(),
+                      reinterpret_cast<unsigned long long*>(bad.data_ptr<int64_t>()), stream);
   py::list cols;
   for (auto& o : outs) cols.append(o);
   return py::make_tuple(cols, n, bad, total, row_begin);

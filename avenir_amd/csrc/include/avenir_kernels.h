@@ -197,9 +197,10 @@ long long csv_chunks(long long size);
 void csv_newline_counts(const uint8_t* bytes, long long size, unsigned* counts, hipStream_t stream);
 void csv_newline_positions(const uint8_t* bytes, long long size, const long long* offsets, long long* pos,
                            hipStream_t stream);
-void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long long* ends, long long n, char delim,
-                    const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
-                    const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream);
+void csv_parse_rows(const uint8_t* bytes, long long size_padded, const long long* starts, const long long* ends,
+                    long long n, char delim, const void* specs, int nspecs, int max_ord, const int* tabs,
+                    const int* voff, const int* vlen, const uint8_t* vbytes, int ntab, int nvoc, int nvb,
+                    unsigned long long* short_rows, hipStream_t stream);
 int csv_devspec_bytes();
 // K25 re-sampling (resample.hip)
 void resample_uniform(unsigned long long seed, unsigned long long stream, long long base, long long n, float* out,

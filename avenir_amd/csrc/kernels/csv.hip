@@ -8,9 +8,11 @@
 //   2. (device exclusive scan of the chunk counts);
 //   3. csv_nl_pos_kernel     : every newline's byte offset, in order (block scan of per-thread
 //                              counts inside each chunk);
-//   4. csv_parse_kernel      : one thread per record walks its fields once and writes every
-//                              schema column: dictionary codes (FNV-1a open-addressing table per
-//                              field, verified against the vocabulary bytes), bucket codes, floats.
+//   4. csv_parse_kernel      : tiles of 256 consecutive records; the tile's bytes are staged in
+//                              LDS by 16-byte loads (and dictionaries up to 16 KB copied to LDS), then one thread per record walks its fields
+//                              once and writes every schema column: dictionary codes (FNV-1a
+//                              open-addressing table per field, verified against the vocabulary
+//                              bytes), bucket codes, floats.
 // Field semantics match the host parser exactly (trim of spaces / tabs / CR, the same decimal
 // accumulation in double, integer-division buckets, 'missing' for unknown values / short rows).
 #include "avenir_common.h"
@@ -137,79 +139,124 @@ __device__ double dev_parse_double(const uint8_t* p, const uint8_t* e) {
   return neg ? -v : v;
 }
 
-__global__ __launch_bounds__(CT) void csv_parse_kernel(const uint8_t* __restrict__ bytes,
+constexpr int PT_BYTES = 32 * 1024;  // LDS tile of the block's line bytes
+constexpr int PD_BYTES = 16 * 1024;  // LDS copy of the dictionaries (probe table, lengths, offsets, bytes)
+
+// one record: p..e its bytes (LDS tile or global), r its output row
+__device__ __forceinline__ bool parse_record(const uint8_t* p, const uint8_t* e, long long r, char delim,
+                                             const DevSpec* s_spec, int nspecs, int max_ord,
+                                             const int* __restrict__ tabs, const int* __restrict__ voff,
+                                             const int* __restrict__ vlen, const uint8_t* __restrict__ vbytes) {
+  int o = 0, si = 0;  // specs are sorted by ordinal
+  const uint8_t* a = p;
+  while (o <= max_ord && si < nspecs) {
+    const uint8_t* q = a;
+    while (q < e && *q != (uint8_t)delim) ++q;
+    while (si < nspecs && s_spec[si].ordinal == o) {
+      const DevSpec& sp = s_spec[si];
+      const uint8_t* f0 = a;
+      const uint8_t* f1 = q;
+      while (f0 < f1 && is_space(*f0)) ++f0;
+      while (f1 > f0 && is_space(f1[-1])) --f1;
+      unsigned code = 65535u;
+      if (sp.kind == 0) {  // CAT
+        unsigned h = 2166136261u;
+        for (const uint8_t* c = f0; c < f1; ++c) h = (h ^ *c) * 16777619u;
+        h ^= h >> 15;
+        unsigned slot = h & (unsigned)sp.tab_mask;
+        const int len = (int)(f1 - f0);
+        while (true) {
+          const int ci = tabs[sp.tab_off + slot];  // the field's code, -1 = empty slot
+          if (ci < 0) break;
+          const int gi = sp.vbase + ci;
+          if (vlen[gi] == len) {
+            const uint8_t* vb = vbytes + voff[gi];
+            int k = 0;
+            while (k < len && vb[k] == f0[k]) ++k;
+            if (k == len) { code = (unsigned)ci; break; }
+          }
+          slot = (slot + 1) & (unsigned)sp.tab_mask;
+        }
+      } else if (sp.kind == 1) {  // BUCKET: the reference's integer division
+        const double v = dev_parse_double(f0, f1);
+        if (!isnan(v)) {
+          const long long b = (long long)floor(v / sp.bucket_width) - sp.bucket_offset;
+          if (b >= 0 && b <= sp.max_code) code = (unsigned)b;
+        }
+      } else {  // FLOAT
+        reinterpret_cast<float*>(sp.out)[r] = (float)dev_parse_double(f0, f1);
+      }
+      if (sp.kind != 2) {
+        if (sp.wide) reinterpret_cast<uint16_t*>(sp.out)[r] = (uint16_t)min(code, 65535u);
+        else reinterpret_cast<uint8_t*>(sp.out)[r] = (uint8_t)min(code, 255u);
+      }
+      ++si;
+    }
+    ++o;
+    if (q >= e) break;
+    a = q + 1;
+  }
+  const bool short_row = si < nspecs;
+  for (; si < nspecs; ++si) {  // fields beyond the end of the row: missing
+    const DevSpec& sp = s_spec[si];
+    if (sp.kind == 2) reinterpret_cast<float*>(sp.out)[r] = __int_as_float(0x7fc00000);
+    else if (sp.wide) reinterpret_cast<uint16_t*>(sp.out)[r] = 65535;
+    else reinterpret_cast<uint8_t*>(sp.out)[r] = 255;
+  }
+  return short_row;
+}
+
+// A tile of CT consecutive records per step: their byte span (rows are in file order) is staged
+// into LDS with 16-byte coalesced loads, then every thread walks its own record in LDS (the
+// per-thread byte walk was a stream of uncoalesced global byte loads); spans above the tile size
+// are walked in global memory.  The byte buffer is padded to a multiple of 16.
+__global__ __launch_bounds__(CT) void csv_parse_kernel(const uint8_t* __restrict__ bytes, long long size_padded,
                                                        const long long* __restrict__ starts,
                                                        const long long* __restrict__ ends, long long n, char delim,
                                                        const DevSpec* __restrict__ specs, int nspecs, int max_ord,
                                                        const int* __restrict__ tabs, const int* __restrict__ voff,
                                                        const int* __restrict__ vlen, const uint8_t* __restrict__ vbytes,
+                                                       int ntab, int nvoc, int nvb,
                                                        unsigned long long* __restrict__ short_rows) {
   __shared__ DevSpec s_spec[32];
+  __shared__ __attribute__((aligned(16))) uint8_t tile[PT_BYTES];
+  __shared__ __attribute__((aligned(16))) int dict[PD_BYTES / 4];
   for (int i = threadIdx.x; i < nspecs; i += CT) s_spec[i] = specs[i];
-  __syncthreads();
+  // small dictionaries (every schema of the reference's examples) are probed in LDS: the probe
+  // chain tabs -> vlen -> voff -> vbytes was four dependent global loads per categorical field
+  const bool dict_lds = 4LL * ntab + 8LL * nvoc + nvb <= PD_BYTES;
+  int* l_tabs = dict;
+  int* l_vlen = dict + ntab;
+  int* l_voff = l_vlen + nvoc;
+  uint8_t* l_vb = reinterpret_cast<uint8_t*>(l_voff + nvoc);
+  if (dict_lds) {
+    for (int i = threadIdx.x; i < ntab; i += CT) l_tabs[i] = tabs[i];
+    for (int i = threadIdx.x; i < nvoc; i += CT) { l_vlen[i] = vlen[i]; l_voff[i] = voff[i]; }
+    for (int i = threadIdx.x; i < nvb; i += CT) l_vb[i] = vbytes[i];
+  }
   unsigned bad = 0;
-  const long long stride = (long long)gridDim.x * CT;
-  for (long long r = (long long)blockIdx.x * CT + threadIdx.x; r < n; r += stride) {
-    const uint8_t* p = bytes + starts[r];
-    const uint8_t* e = bytes + ends[r];
-    int o = 0, si = 0;  // specs are sorted by ordinal
-    const uint8_t* a = p;
-    bool short_row = false;
-    while (o <= max_ord && si < nspecs) {
-      const uint8_t* q = a;
-      while (q < e && *q != (uint8_t)delim) ++q;
-      while (si < nspecs && s_spec[si].ordinal == o) {
-        const DevSpec& sp = s_spec[si];
-        const uint8_t* f0 = a;
-        const uint8_t* f1 = q;
-        while (f0 < f1 && is_space(*f0)) ++f0;
-        while (f1 > f0 && is_space(f1[-1])) --f1;
-        unsigned code = 65535u;
-        if (sp.kind == 0) {  // CAT
-          unsigned h = 2166136261u;
-          for (const uint8_t* c = f0; c < f1; ++c) h = (h ^ *c) * 16777619u;
-          h ^= h >> 15;
-          unsigned slot = h & (unsigned)sp.tab_mask;
-          const int len = (int)(f1 - f0);
-          while (true) {
-            const int ci = tabs[sp.tab_off + slot];  // the field's code, -1 = empty slot
-            if (ci < 0) break;
-            const int gi = sp.vbase + ci;
-            if (vlen[gi] == len) {
-              const uint8_t* vb = vbytes + voff[gi];
-              int k = 0;
-              while (k < len && vb[k] == f0[k]) ++k;
-              if (k == len) { code = (unsigned)ci; break; }
-            }
-            slot = (slot + 1) & (unsigned)sp.tab_mask;
-          }
-        } else if (sp.kind == 1) {  // BUCKET: the reference's integer division
-          const double v = dev_parse_double(f0, f1);
-          if (!isnan(v)) {
-            const long long b = (long long)floor(v / sp.bucket_width) - sp.bucket_offset;
-            if (b >= 0 && b <= sp.max_code) code = (unsigned)b;
-          }
-        } else {  // FLOAT
-          reinterpret_cast<float*>(sp.out)[r] = (float)dev_parse_double(f0, f1);
-        }
-        if (sp.kind != 2) {
-          if (sp.wide) reinterpret_cast<uint16_t*>(sp.out)[r] = (uint16_t)min(code, 65535u);
-          else reinterpret_cast<uint8_t*>(sp.out)[r] = (uint8_t)min(code, 255u);
-        }
-        ++si;
-      }
-      ++o;
-      if (q >= e) break;
-      a = q + 1;
+  for (long long r0 = (long long)blockIdx.x * CT; r0 < n; r0 += (long long)gridDim.x * CT) {
+    const long long r1 = min(n, r0 + CT);
+    const long long lo = starts[r0] & ~15LL;
+    const long long hi = min(size_padded, (ends[r1 - 1] + 15) & ~15LL);
+    const bool staged = hi - lo <= PT_BYTES;
+    __syncthreads();  // s_spec written / the previous tile fully parsed
+    if (staged) {
+      for (long long v = lo + 16LL * threadIdx.x; v < hi; v += 16LL * CT)
+        *reinterpret_cast<uint4*>(tile + (v - lo)) = *reinterpret_cast<const uint4*>(bytes + v);
     }
-    for (; si < nspecs; ++si) {  // fields beyond the end of the row: missing
-      short_row = true;
-      const DevSpec& sp = s_spec[si];
-      if (sp.kind == 2) reinterpret_cast<float*>(sp.out)[r] = __int_as_float(0x7fc00000);
-      else if (sp.wide) reinterpret_cast<uint16_t*>(sp.out)[r] = 65535;
-      else reinterpret_cast<uint8_t*>(sp.out)[r] = 255;
+    __syncthreads();
+    const long long r = r0 + threadIdx.x;
+    if (r < r1) {
+      const long long b = starts[r], e = ends[r];
+      bool sr;
+      if (staged && b >= lo && e <= hi && dict_lds)
+        sr = parse_record(tile + (b - lo), tile + (e - lo), r, delim, s_spec, nspecs, max_ord, l_tabs, l_voff, l_vlen,
+                          l_vb);
+      else
+        sr = parse_record(bytes + b, bytes + e, r, delim, s_spec, nspecs, max_ord, tabs, voff, vlen, vbytes);
+      bad += sr ? 1u : 0u;
     }
-    bad += short_row ? 1u : 0u;
   }
   bad = av::wave_sum(bad);
   if (av::lane_id() == 0 && bad) atomicAdd(short_rows, (unsigned long long)bad);
@@ -234,14 +281,16 @@ void csv_newline_positions(const uint8_t* bytes, long long size, const long long
   AV_HIP_CHECK(hipGetLastError());
 }
 
-void csv_parse_rows(const uint8_t* bytes, const long long* starts, const long long* ends, long long n, char delim,
-                    const void* specs, int nspecs, int max_ord, const int* tabs, const int* voff, const int* vlen,
-                    const uint8_t* vbytes, unsigned long long* short_rows, hipStream_t stream) {
+void csv_parse_rows(const uint8_t* bytes, long long size_padded, const long long* starts, const long long* ends,
+                    long long n, char delim, const void* specs, int nspecs, int max_ord, const int* tabs,
+                    const int* voff, const int* vlen, const uint8_t* vbytes, int ntab, int nvoc, int nvb,
+                    unsigned long long* short_rows, hipStream_t stream) {
   if (n <= 0 || nspecs <= 0) return;
   if (nspecs > 32) throw std::runtime_error("csv_parse_rows: at most 32 parsed columns");
+  if (size_padded % 16) throw std::runtime_error("csv_parse_rows: the byte buffer must be padded to 16");
   csv_parse_kernel<<<av::stream_grid(n, CT, 1, 8192), CT, 0, stream>>>(
-      bytes, starts, ends, n, delim, reinterpret_cast<const DevSpec*>(specs), nspecs, max_ord, tabs, voff, vlen,
-      vbytes, short_rows);
+      bytes, size_padded, starts, ends, n, delim, reinterpret_cast<const DevSpec*>(specs), nspecs, max_ord, tabs, voff, vlen,
+      vbytes, ntab, nvoc, nvb, short_rows);
   AV_HIP_CHECK(hipGetLastError());
 }
 

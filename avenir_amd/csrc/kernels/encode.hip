@@ -274,14 +274,11 @@ void loo_stats(const void* codes, int code_bytes, int m, long long ld, long long
                unsigned* cnt, hipStream_t stream) {
   const size_t wide_lds = (size_t)m * (sizeof(double) + sizeof(unsigned));
   if (code_bytes >= 2 && wide_lds <= LOO_WIDE_LDS) {
-    static bool attr = false;
-    if (!attr) {
-      AV_HIP_CHECK(hipFuncSetAttribute((const void*)loo_stats_lds_kernel<int>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LOO_WIDE_LDS));
-      AV_HIP_CHECK(hipFuncSetAttribute((const void*)loo_stats_lds_kernel<unsigned short>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LOO_WIDE_LDS));
-      attr = true;
-    }
+    // set on every call: the attribute belongs to the current device (no process-wide cache)
+    AV_HIP_CHECK(hipFuncSetAttribute((const void*)loo_stats_lds_kernel<int>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LOO_WIDE_LDS));
+    AV_HIP_CHECK(hipFuncSetAttribute((const void*)loo_stats_lds_kernel<unsigned short>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LOO_WIDE_LDS));
     // >= 16 rows per thread so the table zero + flush is amortised; <= 256 blocks per column
     long long gx = n / (LOO_WIDE_T * 16);
     gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);

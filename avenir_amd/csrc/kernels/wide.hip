@@ -68,13 +68,10 @@ __global__ __launch_bounds__(256) void hist_wide_global_kernel(
   }
 }
 
-int num_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    AV_HIP_CHECK(hipGetDevice(&dev));
-    AV_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+int num_cus() {  // of the current device, queried per call (a host attribute read)
+  int dev = 0, cus = 0;
+  AV_HIP_CHECK(hipGetDevice(&dev));
+  AV_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   return cus;
 }
 
@@ -90,12 +87,9 @@ void hist_wide(const CT* codes, long long ld, long long n, const uint8_t* labels
   const long long slots = (long long)n_classes * total_bins;
   if (mode != 2 && slots <= kLdsSlots) {
     const size_t lds = (size_t)slots * sizeof(unsigned int);
-    static bool attr = false;
-    if (!attr) {
-      AV_HIP_CHECK(hipFuncSetAttribute((const void*)hist_wide_lds_kernel<CT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSlots * 4));
-      attr = true;
-    }
+    // set on every call: the attribute belongs to the current device (no process-wide cache)
+    AV_HIP_CHECK(hipFuncSetAttribute((const void*)hist_wide_lds_kernel<CT>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSlots * 4));
     // one block per CU (the table takes most of the LDS), never more blocks than row tiles
     const long long tiles = (n + kWideThreads - 1) / kWideThreads;
     const int grid = (int)std::min<long long>(tiles, (long long)num_cus());

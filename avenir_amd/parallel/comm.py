@@ -334,9 +334,18 @@ class Comm:
 
 
 def get_comm(**kw) -> Comm:
+    """The process's communicator.  ``AVENIR_COMM_BACKEND`` = gloo / nccl / rccl-emul overrides the
+    default backend (rccl-emul: the RCCL code paths over a gloo group, so several ranks can share
+    one GPU in a rehearsal of a multi-GPU run)."""
     global _COMM
     if _COMM is None:
-        _COMM = Comm(**kw)
+        be = os.environ.get("AVENIR_COMM_BACKEND", "")
+        if be == "rccl-emul" and "backend" not in kw:
+            _COMM = Comm.emulated_rccl(**kw)
+        else:
+            if be in ("gloo", "nccl"):
+                kw.setdefault("backend", be)
+            _COMM = Comm(**kw)
     return _COMM
 
 
