@@ -2122,9 +2122,11 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
     // a previous call's last DMAs may still read the slots (they ran on that call's stream)
     for (int i = 0; i < SLOTS; ++i) BIND_HIP_CHECK(hipEventSynchronize(done[i]));
     int64_t k = 0;
-    for (int64_t off = 0; off < size; off += SLOT, ++k) {
+    // pieces grow 8, 16, 32, 64 MB: the first DMA starts after an 8 MB fill instead of a 64 MB one
+    int64_t len = 0;
+    for (int64_t off = 0; off < size; off += len, ++k) {
       const int slot = (int)(k % SLOTS);
-      const int64_t len = std::min(SLOT, size - off);
+      len = std::min(std::min(SLOT, (int64_t)(8LL << 20) << std::min<int64_t>(k, 3)), size - off);
       if (k >= SLOTS) BIND_HIP_CHECK(hipEventSynchronize(done[slot]));  // the slot's last DMA is done
       if (use_pread) {  // page cache -> pinned slot, T threads, no source page faults
         pread_parallel(fd, static_cast<char*>(ring[slot]), off, len, T);
@@ -2607,8 +2609,9 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
       // fill the slot from the piece list (parallel memcpy of each run)
       int64_t fill = 0;
       char* dst = static_cast<char*>(R.buf[slot]);
-      while (fill < SLOT && pi < pieces.size()) {
-        const int64_t n = std::min(SLOT - fill, pieces[pi].len - pofs);
+      const int64_t cap = std::min(SLOT, (int64_t)(8LL << 20) << std::min<int64_t>(k, 3));  // 8, 16, 32, 64 MB
+      while (fill < cap && pi < pieces.size()) {
+        const int64_t n = std::min(cap - fill, pieces[pi].len - pofs);
         const char* src = pieces[pi].p + pofs;
         const int T = n >= (8 << 20) ? upload_threads() : 1;
         std::vector<std::thread> th;
