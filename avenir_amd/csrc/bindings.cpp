@@ -1985,6 +1985,46 @@ std::vector<at::Tensor> linear_act_bwd(const at::Tensor& dY, const at::Tensor& Y
   return {dZ, part.sum(0)};
 }
 
+// K27 fused backward of Y = act(X W^T + b): returns (dX | None, dW, db).  dW / db come from the
+// fused weight-gradient kernel (dZ formed in-tile), dX = dZ W through the forward MFMA kernel
+// (identity activation, W^T as its [K, N] operand).
+py::tuple linear_act_backward(const at::Tensor& dY, const at::Tensor& Y, const at::Tensor& X, const at::Tensor& W,
+                              int64_t act, bool need_dx) {
+  CHECK_DEV(dY); CHECK_DTYPE(dY, at::kFloat);
+  CHECK_DEV(Y); CHECK_DTYPE(Y, at::kFloat);
+  CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
+  TORCH_CHECK(Y.dim() == 2 && dY.sizes() == Y.sizes() && X.dim() == 2 && W.dim() == 2, "dY, Y [M, N], X [M, K], W [N, K]");
+  TORCH_CHECK(X.size(0) == Y.size(0) && W.size(0) == Y.size(1) && W.size(1) == X.size(1), "shape mismatch");
+  TORCH_CHECK(act >= 0 && act <= 5, "activation code 0..5");
+  TORCH_CHECK(X.size(0) < (1LL << 31) && W.size(0) < (1LL << 31) && X.size(1) < (1LL << 31), "dims < 2^31");
+  const int M = (int)Y.size(0), N = (int)Y.size(1), K = (int)X.size(1);
+  auto dYc = dY.contiguous(), Yc = Y.contiguous(), Xc = X.contiguous();
+  DevGuard g(Y.device());
+  const int S = avk::linear_act_wgrad_slices(M, N, K);
+  const int64_t E = (int64_t)N * K + N;
+  auto pW = at::empty({S, E}, Y.options());
+  auto tmp = at::empty({(S + 63) / 64, E}, Y.options());
+  auto outv = at::empty({E}, Y.options());
+  auto dW = outv.narrow(0, 0, (int64_t)N * K).view({N, K});
+  auto db = outv.narrow(0, (int64_t)N * K, N);
+  at::Tensor dZ;
+  if (need_dx) dZ = at::empty({M, N}, Y.options());
+  if (M == 0) {
+    outv.zero_();
+    return py::make_tuple(need_dx ? py::cast(at::zeros({0, K}, X.options())) : py::none(), dW, db);
+  }
+  hipStream_t st = cur_stream(Y);
+  avk::linear_act_wgrad(dYc.data_ptr<float>(), Yc.data_ptr<float>(), Xc.data_ptr<float>(),
+                        need_dx ? dZ.data_ptr<float>() : nullptr, pW.data_ptr<float>(), tmp.data_ptr<float>(),
+                        outv.data_ptr<float>(), M, N, K, (int)act, st);
+  if (!need_dx) return py::make_tuple(py::none(), dW, db);
+  auto Wt = W.t().contiguous();  // [K, N]
+  auto dX = at::empty({M, K}, X.options());
+  avk::linear_act_fwd(dZ.data_ptr<float>(), Wt.data_ptr<float>(), nullptr, dX.data_ptr<float>(), M, K, N, 0, st);
+  return py::make_tuple(dX, dW, db);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1 on the device (csv.hip): upload the file through a ring of pinned staging buffers (host
 // copies from the page cache overlap the DMA of the previous slot), index the lines and parse
@@ -3002,6 +3042,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("forest_predict_bin", &forest_predict_bin);
   m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0);
   m.def("linear_act_bwd", &linear_act_bwd);
+  m.def("linear_act_backward", &linear_act_backward);
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);

@@ -181,6 +181,12 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
 int linear_act_bwd_blocks(int M);
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream);
+// out [N*K + N] = (dW = dZ^T X row-major [N, K], db = colsum dZ) with dZ = dY * act'(Y) fused (dZ
+// written when non-null); pW [S, N*K + N] slice partials, tmp [ceil(S / 64), N*K + N],
+// S = linear_act_wgrad_slices(M, N, K)
+int linear_act_wgrad_slices(int M, int N, int K);
+void linear_act_wgrad(const float* dY, const float* Y, const float* X, float* dZ, float* pW, float* tmp, float* out,
+                      int M, int N, int K, int act, hipStream_t stream);
 long long forest_predict_bin_lds(int n_nodes, int nfeat);
 void forest_predict_bin(const uint8_t* codes, long long ld, long long n, int nfeat, const uint2* nodes, int n_nodes,
                         const float* values, int V, const int* tree_root, const float* tree_w, int n_trees, int mode,

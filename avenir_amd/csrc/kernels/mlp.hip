@@ -11,6 +11,8 @@
 // Backward dZ = dY * act'(Y), db = colsum(dZ): one pass over dY / Y (the derivative is taken from
 //   the stored output, so no pre-activation tensor is kept), per-block column partials reduced on
 //   the host side of the op; dX = dZ W and dW = dZ^T X are plain GEMMs (hipBLASLt).
+#include <algorithm>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -170,6 +172,114 @@ __global__ __launch_bounds__(MT) void linear_act_bwd_kernel(const float* __restr
   }
 }
 
+// Weight gradient with the activation derivative fused in: dW = dZ^T X, db = colsum(dZ), dZ =
+// dY * act'(Y) computed while the tile is staged (and written once, by the k-tile-0 blocks, for the
+// dX GEMM).  Block = 4 waves over a 64 (n) x 64 (k) tile of dW and one slice of rows of M; chunks of
+// 32 rows of dZ and X go through LDS and feed v_mfma_f32_32x32x2_f32 with m as the contraction
+// index; every slice writes a partial tile, summed in a fixed order by linear_act_wgrad_reduce_kernel
+// (deterministic).  The library GEMM this replaces (dZ^T X with M = 65,536 rows reduced inside a
+// couple of output tiles) ran at ~2.5 TFLOP/s.
+constexpr int MC = 32;
+constexpr int WPT = (MC * 64) / MT;  // elements of each staged array per thread and chunk
+
+struct WgradRegs {  // one chunk of dY, Y (n-tile columns) and X (k-tile columns) in flight
+  float dy[WPT], y[WPT], x[WPT];
+  __device__ __forceinline__ void load(const float* __restrict__ dY, const float* __restrict__ Y,
+                                       const float* __restrict__ X, long long m0, long long r1, int n0, int k0, int N,
+                                       int K) {
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int e = threadIdx.x + MT * i, row = e >> 6, c = e & 63;
+      const long long m = m0 + row;
+      const int n = n0 + c, k = k0 + c;
+      const bool okz = m < r1 && n < N;
+      dy[i] = okz ? dY[m * N + n] : 0.f;
+      y[i] = okz ? Y[m * N + n] : 0.f;
+      x[i] = (m < r1 && k < K) ? X[m * K + k] : 0.f;
+    }
+  }
+};
+
+__global__ __launch_bounds__(MT) void linear_act_wgrad_kernel(const float* __restrict__ dY, const float* __restrict__ Y,
+                                                               const float* __restrict__ X, float* __restrict__ dZ,
+                                                               float* __restrict__ pW, int M, int N, int K,
+                                                               int rows_per_slice, int act) {
+  __shared__ float sZ[MC][TN + 1];
+  __shared__ float sX[MC][TN + 1];
+  __shared__ float sB[MT / 64][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const long long sl = blockIdx.z;
+  const long long r0 = sl * rows_per_slice, r1 = min((long long)M, r0 + rows_per_slice);
+  const bool lead = blockIdx.y == 0;
+  const long long row_stride = (long long)N * K + N;  // dW partial then db partial
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  float bacc = 0.f;  // column tid & 63 of this thread's rows
+  const int li = lane & 31, lm = lane >> 5;
+  WgradRegs pre;
+  if (r0 < r1) pre.load(dY, Y, X, r0, r1, n0, k0, N, K);
+  for (long long m0 = r0; m0 < r1; m0 += MC) {
+    __syncthreads();  // the previous chunk's MFMA reads are done
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int e = tid + MT * i, row = e >> 6, c = e & 63;
+      const float z = pre.dy[i] * act_grad_from_y(pre.y[i], act);  // 0 outside the tile (dy = 0)
+      if (lead && dZ && m0 + row < r1 && n0 + c < N) dZ[(m0 + row) * N + n0 + c] = z;
+      sZ[row][c] = z;
+      bacc += z;
+      sX[row][c] = pre.x[i];
+    }
+    __syncthreads();
+    if (m0 + MC < r1) pre.load(dY, Y, X, m0 + MC, r1, n0, k0, N, K);  // in flight during the MFMAs
+#pragma unroll
+    for (int mm = 0; mm < MC; mm += 2) {
+      const float a = sZ[mm + lm][wn * 32 + li];  // A[i = n][k = m]
+      const float b = sX[mm + lm][wk * 32 + li];  // B[k = m][j = k]
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+  }
+  const int col = k0 + wk * 32 + (lane & 31);
+  if (col < K) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (n < N) pW[sl * row_stride + (long long)n * K + col] = acc[r];
+    }
+  }
+  if (lead) {  // bias partial in the tail of the slice row
+    sB[wave][lane] = bacc;
+    __syncthreads();
+    if (wave == 0 && n0 + lane < N)
+      pW[sl * row_stride + (long long)N * K + n0 + lane] = sB[0][lane] + sB[1][lane] + sB[2][lane] + sB[3][lane];
+  }
+}
+
+// out[y][e] = sum of in[s][e] over slices s in [y * span, (y + 1) * span), e < E: a block = 64
+// elements x 16 slice groups, the group sums combined in a fixed order (deterministic).  Two passes
+// (span 64, then the rest) keep every thread's serial chain short at any slice count.
+constexpr int RG = 16;
+__global__ __launch_bounds__(64 * RG) void slice_sum_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                            int S, int span, long long E) {
+  __shared__ float sw[RG][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + c;
+  const int s0 = blockIdx.y * span, s1 = min(S, s0 + span);
+  float t = 0.f;
+  if (e < E)
+    for (int s = s0 + g; s < s1; s += RG) t += in[(long long)s * E + e];
+  sw[g][c] = t;
+  __syncthreads();
+  if (g == 0 && e < E) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < RG; ++k) a += sw[k][c];
+    out[(long long)blockIdx.y * E + e] = a;
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -192,6 +302,32 @@ void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, 
   if (M <= 0 || N <= 0) return;
   dim3 grid((unsigned)((N + 63) / 64), (unsigned)linear_act_bwd_blocks(M));
   linear_act_bwd_kernel<<<grid, MT, 0, stream>>>(dY, Y, dZ, partial, M, N, act);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+// slices of M for the weight gradient: about 512 blocks over the (n, k) tiles, >= 256 rows each
+int linear_act_wgrad_slices(int M, int N, int K) {  // ~1024 blocks, >= 64 rows per slice
+  const long long tiles = (long long)((N + 63) / 64) * ((K + 63) / 64);
+  long long S = std::max(1LL, 1024 / std::max(1LL, tiles));
+  S = std::min(S, std::max(1LL, ((long long)M + 63) / 64));
+  return (int)S;
+}
+
+void linear_act_wgrad(const float* dY, const float* Y, const float* X, float* dZ, float* pW, float* tmp, float* out,
+                      int M, int N, int K, int act, hipStream_t stream) {
+  if (N <= 0 || K <= 0) return;
+  const int S = linear_act_wgrad_slices(M, N, K);
+  int rows = (int)((((long long)M + S - 1) / S + MC - 1) / MC * MC);
+  if (rows < MC) rows = MC;
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((K + 63) / 64), (unsigned)S);
+  linear_act_wgrad_kernel<<<grid, MT, 0, stream>>>(dY, Y, X, dZ, pW, M, N, K, rows, act);
+  AV_HIP_CHECK(hipGetLastError());
+  const long long E = (long long)N * K + N;
+  const unsigned ex = (unsigned)((E + 63) / 64);
+  const int S2 = (S + 63) / 64;
+  slice_sum_kernel<<<dim3(ex, (unsigned)S2), 64 * RG, 0, stream>>>(pW, tmp, S, 64, E);
+  AV_HIP_CHECK(hipGetLastError());
+  slice_sum_kernel<<<dim3(ex, 1), 64 * RG, 0, stream>>>(tmp, out, S2, S2, E);
   AV_HIP_CHECK(hipGetLastError());
 }
 

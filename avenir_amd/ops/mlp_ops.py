@@ -2,8 +2,11 @@
 
 ``linear_act(x, W, b, act)`` = ``act(x @ W.T + b)``.  On the GPU the forward is ONE MFMA kernel with
 the bias and activation applied in the accumulator epilogue (torch: addmm + a separate activation
-pass over [M, N]); the backward is one fused pass computing ``dZ = dY * act'(Y)`` and the bias
-gradient from the stored output, then two library GEMMs (hipBLASLt) for ``dX`` and ``dW``.  CPU
+pass over [M, N]).  The backward is one MFMA kernel forming ``dZ = dY * act'(Y)`` in its tiles and
+reducing ``dW = dZ^T X`` and the bias gradient over row slices (a fixed-order slice sum after it),
+then ``dX = dZ W`` on the forward MFMA kernel (layers up to 64 x 64; the library GEMM for ``dW``
+reduced all M rows inside one or two output tiles).  Wider layers: one fused ``dZ`` + bias-gradient
+pass, then two hipBLASLt GEMMs.  CPU
 tensors run the plain PyTorch composition (the numerics oracle of the GPU tests).
 
 Reference: FeedForwardNetwork layer construction, P/supv/tnn.py:100-145.
@@ -13,6 +16,11 @@ from __future__ import annotations
 import torch
 
 from .. import _native
+
+# layers up to this width (both N and K) take the fused weight-gradient backward (one 64 x 64 dW
+# tile per row slice: the reference's networks, e.g. R/tnn_bo.properties 8-wide); wider layers re-read
+# their inputs per tile there and use the fused dZ pass + hipBLASLt GEMMs instead
+FUSED_BWD_MAX = 64
 
 ACT_CODES = {None: 0, "none": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leakyRelu": 4, "elu": 5}
 
@@ -44,6 +52,11 @@ class _LinearAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, W, y = ctx.saved_tensors
+        N, K = W.shape
+        if N <= FUSED_BWD_MAX and K <= FUSED_BWD_MAX:
+            gx, gW, db = _native.C().linear_act_backward(gy.contiguous(), y, x, W, ctx.code,
+                                                         bool(ctx.needs_input_grad[0]))
+            return gx, (gW if ctx.needs_input_grad[1] else None), (db if ctx.has_b else None), None
         dz, db = _native.C().linear_act_bwd(gy.contiguous(), y, ctx.code)
         gx = dz @ W if ctx.needs_input_grad[0] else None
         gW = dz.t() @ x if ctx.needs_input_grad[1] else None

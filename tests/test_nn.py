@@ -147,7 +147,7 @@ def test_fused_layer_spec_keeps_indices():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh", "leakyRelu", "elu"])
-@pytest.mark.parametrize("M,K,N", [(37, 5, 3), (300, 64, 130), (1025, 33, 64)])
+@pytest.mark.parametrize("M,K,N", [(37, 5, 3), (300, 64, 130), (1025, 33, 64), (20000, 48, 64), (20000, 200, 96)])
 def test_linear_act_kernel_matches_torch(cuda, act, M, K, N):
     from avenir_amd.ops.mlp_ops import _act_torch, ACT_CODES, linear_act
     g = torch.Generator().manual_seed(M + N)
@@ -164,6 +164,40 @@ def test_linear_act_kernel_matches_torch(cuda, act, M, K, N):
     assert torch.allclose(yg.detach().cpu().double(), yr.detach(), atol=1e-4, rtol=1e-4)
     for a, r in ((xg.grad, xr.grad), (Wg.grad, Wr.grad), (bg.grad, br.grad)):
         assert torch.allclose(a.cpu().double(), r, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_linear_act_backward_without_input_grad(cuda):
+    """First layer of a network: no dX; dW / db from the fused weight-gradient kernel alone."""
+    from avenir_amd.ops.mlp_ops import linear_act
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(5000, 16, generator=g)
+    W = torch.randn(48, 16, generator=g) / 4
+    b = torch.randn(48, generator=g)
+    gy = torch.randn(5000, 48, generator=g)
+    Wr, br = W.double().requires_grad_(), b.double().requires_grad_()
+    torch.tanh(torch.nn.functional.linear(x.double(), Wr, br)).backward(gy.double())
+    Wg, bg = W.to(cuda).requires_grad_(), b.to(cuda).requires_grad_()
+    linear_act(x.to(cuda), Wg, bg, "tanh").backward(gy.to(cuda))
+    assert torch.allclose(Wg.grad.cpu().double(), Wr.grad, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(bg.grad.cpu().double(), br.grad, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_wgrad_kernel_multi_tile(cuda):
+    """The fused weight-gradient binding on a multi-tile layer (N, K > 64, not dispatched by
+    linear_act) against float64 torch."""
+    from avenir_amd import _native
+    g = torch.Generator().manual_seed(6)
+    M, K, N = 9000, 130, 96
+    x, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / 10
+    y = torch.sigmoid(x @ W.t())
+    gy = torch.randn(M, N, generator=g)
+    dz = gy.double() * y.double() * (1 - y.double())
+    gx, gW, db = _native.C().linear_act_backward(gy.to(cuda), y.to(cuda), x.to(cuda), W.to(cuda), 2, True)
+    assert torch.allclose(gW.cpu().double(), dz.t() @ x.double(), atol=2e-3, rtol=1e-3)
+    assert torch.allclose(db.cpu().double(), dz.sum(0), atol=2e-3, rtol=1e-3)
+    assert torch.allclose(gx.cpu().double(), dz @ W.double(), atol=2e-3, rtol=1e-3)
 
 
 @pytest.mark.gpu
