@@ -88,7 +88,14 @@ def test_bandit_kernel_matches_reference(cuda, algo):
 def _run_many(algo, device="cpu", A=100, groups=8, rounds=120, seed=0):
     p = torch.linspace(0.05, 0.6, A)
     p[37] = 0.95                                            # the best arm sits in the second slot
-    bank = BanditBank(algo, [f"a{i}" for i in range(A)], groups, CFG[algo], device=device, seed=seed)
+    experts = None
+    if algo == "exponentialWeightExpert":                   # 8 experts, each favouring a band of arms
+        eg = torch.Generator().manual_seed(11)
+        experts = torch.rand((8, A), generator=eg) + 0.05
+        experts[3, 30:45] += 4.0
+        experts = experts / experts.sum(1, keepdim=True)
+    bank = BanditBank(algo, [f"a{i}" for i in range(A)], groups, CFG[algo], device=device, seed=seed,
+                      experts=experts)
     g = torch.Generator().manual_seed(seed)
     picks = []
     for _ in range(rounds):
@@ -116,8 +123,6 @@ def test_hundred_arm_bandit(algo):
 @pytest.mark.parametrize("algo", sorted(ALGOS))
 @pytest.mark.parametrize("A", [100, 1000])
 def test_many_arm_bandit_kernel_matches_reference(cuda, algo, A):
-    if algo == "exponentialWeightExpert":
-        pytest.skip("expert advice matrix is [experts, arms]; covered at 4 arms")
     _, cpu_picks = _run_many(algo, "cpu", A=A, groups=32, rounds=20, seed=3)
     _, gpu_picks = _run_many(algo, cuda, A=A, groups=32, rounds=20, seed=3)
     agree = float((cpu_picks == gpu_picks).float().mean())
