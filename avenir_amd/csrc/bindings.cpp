@@ -781,6 +781,35 @@ py::tuple pagerank(const at::Tensor& P, double d, int64_t iters, double tol) {
   return py::make_tuple(r, it);
 }
 
+// Weighted pagerank for any n on several workgroups per iteration (no host sync per iteration):
+// (r [n], iterations [1]).
+py::tuple pagerank_multi(const at::Tensor& P, double d, int64_t iters, double tol) {
+  CHECK_DEV(P);
+  CHECK_DTYPE(P, at::kDouble);
+  TORCH_CHECK(P.dim() == 2 && P.size(0) == P.size(1) && P.is_contiguous(), "P must be contiguous [n, n]");
+  TORCH_CHECK(P.size(0) < (1LL << 31) && iters >= 0 && iters < (1LL << 30), "pagerank: n < 2^31");
+  const int64_t n = P.size(0);
+  DevGuard gd(P.device());
+  auto buf = at::empty({2, n}, P.options());
+  buf[0].fill_(1.0 / (double)std::max<int64_t>(n, 1));
+  auto partial = at::empty({(n + avk::pagerank_multi_rows() - 1) / avk::pagerank_multi_rows(), n}, P.options());
+  auto dpart = at::empty({(n + 255) / 256}, P.options());
+  auto state = at::zeros({2}, P.options().dtype(at::kInt));
+  // batches of 8 iterations, one host read of the flag per batch: a converged run stops enqueueing
+  // (the early-exit launches of a whole up-front enqueue cost more than the work at small n)
+  auto state_h = at::empty({2}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+  int it = 0;
+  for (int64_t k0 = 0; k0 < iters; k0 += 8) {
+    const int64_t k1 = std::min<int64_t>(iters, k0 + 8);
+    avk::pagerank_multi(P.data_ptr<double>(), (int)n, d, (int)k0, (int)k1, tol, buf.data_ptr<double>(),
+                        partial.data_ptr<double>(), dpart.data_ptr<double>(), state.data_ptr<int>(), cur_stream(P));
+    state_h.copy_(state);
+    it = state_h[1].item<int>();
+    if (state_h[0].item<int>()) break;
+  }
+  return py::make_tuple(buf[it & 1].clone(), state.narrow(0, 1, 1).clone());
+}
+
 // One SGNS mini-batch: gradients of every pair into gIn / gOut (+ per-row counts cIn / cOut), then
 // the rows move by their mean update (gIn for the centre table summed when mean_in is false).
 // The caller checks id ranges once per fit (pairs / alias are built from the vocabulary).
@@ -2981,6 +3010,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("tfidf_csr", &tfidf_csr);
   m.def("mixed_knn", &mixed_knn);
   m.def("pagerank", &pagerank);
+  m.def("pagerank_multi", &pagerank_multi);
   m.def("sgns_hot_replicas", &avk::sgns_hot_replicas);
   m.def("sgns_step", &sgns_step, py::arg("Win"), py::arg("Wout"), py::arg("gIn"), py::arg("gOut"), py::arg("cIn"),
         py::arg("cOut"), py::arg("centre"), py::arg("context"), py::arg("aprob"), py::arg("alias"), py::arg("neg"),

@@ -303,6 +303,10 @@ double* inversions(double* a, double* tmp, long long m, unsigned long long* inv,
 // weighted, normalised rows; status bit 1 = column id out of range, 2 = bad row pointers
 void tfidf_csr(const long long* crow, const long long* col, float* val, long long n_rows, long long nnz, long long V,
                int smooth, int sublinear, int norm, int* df, int* status, hipStream_t stream);
+// multi-workgroup power iteration (any n): see text.hip; result in buf[state[1] & 1]
+int pagerank_multi_rows();
+void pagerank_multi(const double* P, int n, double d, int k0, int k1, double tol, double* buf, double* partial,
+                    double* dpart, int* state, hipStream_t stream);
 int pagerank_max_n();
 void pagerank(const double* P, int n, double d, int iters, double tol, double* r, int* it, hipStream_t stream);
 int sgns_hot_replicas();

@@ -151,6 +151,65 @@ __global__ __launch_bounds__(PR_T) void pagerank_kernel(const double* __restrict
   if (tid == 0) *it_out = it;
 }
 
+// Multi-workgroup power iteration for graphs above the single-workgroup size: per iteration
+//   pr_partial_kernel  : column sums of P[rows of chunk y, j] * r[i] (r chunk staged in LDS), one
+//                        partial per (row chunk, column) — every CU streams a slab of P;
+//   pr_finalize_kernel : nr[j] = (1 - d) / n + d * sum_y partial[y][j] (fixed order), per-block
+//                        L1 change partials;
+//   pr_status_kernel   : one block sums the change partials (fixed order) and raises the done flag
+//                        at the first iteration under tol.
+// Every kernel returns at once once the flag is up, so the host enqueues all iterations without a
+// synchronisation per iteration and reads the iteration count once at the end.
+constexpr int PRM_T = 256;
+constexpr int PRM_ROWS = 256;
+
+__global__ __launch_bounds__(PRM_T) void pr_partial_kernel(const double* __restrict__ P, const double* __restrict__ r,
+                                                           double* __restrict__ partial, int n,
+                                                           const int* __restrict__ done) {
+  if (*done) return;
+  __shared__ double rs[PRM_ROWS];
+  const int j = blockIdx.x * PRM_T + threadIdx.x;
+  const int i0 = blockIdx.y * PRM_ROWS, i1 = min(n, i0 + PRM_ROWS);
+  for (int i = i0 + threadIdx.x; i < i1; i += PRM_T) rs[i - i0] = r[i];
+  __syncthreads();
+  if (j >= n) return;
+  double s = 0.0;
+  for (int i = i0; i < i1; ++i) s += P[(long long)i * n + j] * rs[i - i0];
+  partial[(long long)blockIdx.y * n + j] = s;
+}
+
+__global__ __launch_bounds__(PRM_T) void pr_finalize_kernel(const double* __restrict__ partial, int R,
+                                                            const double* __restrict__ r, double* __restrict__ nr,
+                                                            int n, double d, double* __restrict__ dpart,
+                                                            const int* __restrict__ done) {
+  if (*done) return;
+  __shared__ double red[PRM_T / 64];
+  const int j = blockIdx.x * PRM_T + threadIdx.x;
+  double diff = 0.0;
+  if (j < n) {
+    double s = 0.0;
+    for (int y = 0; y < R; ++y) s += partial[(long long)y * n + j];
+    const double v = (1.0 - d) / n + d * s;
+    nr[j] = v;
+    diff = fabs(v - r[j]);
+  }
+  for (int o = 32; o > 0; o >>= 1) diff += __shfl_xor(diff, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = diff;
+  __syncthreads();
+  if (threadIdx.x == 0) dpart[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(64) void pr_status_kernel(const double* __restrict__ dpart, int nb, double tol, int k,
+                                                       int* __restrict__ done, int* __restrict__ it_out) {
+  if (*done) return;
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int b = 0; b < nb; ++b) t += dpart[b];
+    *it_out = k + 1;
+    if (t < tol) *done = 1;
+  }
+}
+
 // Hot rows: the negatives follow unigram^0.75 and the contexts / centres the unigram itself, so a
 // few frequent words collect most of a batch's gradient atomics, all on the same addresses (the
 // grad kernel was 82 % of an epoch, serialised on them).  Rows with hot[row] = s >= 0 (the H most
@@ -315,6 +374,25 @@ void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, flo
   sgns_apply_kernel<<<av::stream_grid((long long)V * dim, 256, 4, 4096), 256, 0, stream>>>(Wout, gOut, cOut, V, dim, 1,
                                                                                            hot, H, gOutHot, cOut_next,
                                                                                            n_cout);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+int pagerank_multi_rows() { return PRM_ROWS; }
+
+// Iterations [k0, k1).  buf: 2 x n (buf[0] = the start vector, filled by the caller), partial:
+// ceil(n / 256) x n, dpart: ceil(n / 256), state: 2 ints zeroed before the first batch (done,
+// iterations).  The result is in buf[iterations & 1].
+void pagerank_multi(const double* P, int n, double d, int k0, int k1, double tol, double* buf, double* partial,
+                    double* dpart, int* state, hipStream_t stream) {
+  if (n <= 0) return;
+  const int nb = (n + PRM_T - 1) / PRM_T, R = (n + PRM_ROWS - 1) / PRM_ROWS;
+  for (int k = k0; k < k1; ++k) {
+    const double* r = buf + (long long)(k & 1) * n;
+    double* nr = buf + (long long)((k + 1) & 1) * n;
+    pr_partial_kernel<<<dim3((unsigned)nb, (unsigned)R), PRM_T, 0, stream>>>(P, r, partial, n, state);
+    pr_finalize_kernel<<<(unsigned)nb, PRM_T, 0, stream>>>(partial, R, r, nr, n, d, dpart, state);
+    pr_status_kernel<<<1, 64, 0, stream>>>(dpart, nb, tol, k, state, state + 1);
+  }
   AV_HIP_CHECK(hipGetLastError());
 }
 

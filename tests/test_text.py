@@ -200,6 +200,28 @@ def test_pagerank_kernel_matches_tensor_path(cuda):
 
 
 @pytest.mark.gpu
+def test_pagerank_multi_workgroup(cuda):
+    """Graphs above the one-workgroup size (and the multi-workgroup kernels at small n, incl. an
+    iteration cap hit before convergence) against the tensor path, iteration counts included."""
+    from avenir_amd import _native
+    g = torch.Generator().manual_seed(3)
+    for n, iters, tol in ((3, 100, 1e-10), (300, 100, 1e-10), (700, 4, 1e-10), (3000, 100, 1e-10)):
+        S = torch.rand((n, n), generator=g, dtype=torch.float64)
+        S[:, 1] = 0
+        S[1, :] = 0
+        S.fill_diagonal_(0)
+        ref = pagerank(S, iters=iters, tol=tol)
+        out = S.sum(1, keepdim=True)
+        P = torch.where(out > 0, S / out.clamp_min(1e-300), torch.full_like(S, 1.0 / n))
+        r, it = _native.C().pagerank_multi(P.to(cuda).contiguous(), 0.85, iters, tol)
+        r1, it1 = _native.C().pagerank(P.to(cuda).contiguous(), 0.85, iters, tol) if n <= 8192 else (r, it)
+        assert torch.allclose(r.cpu(), ref, rtol=1e-10, atol=1e-13), n
+        assert int(it) == int(it1), (n, int(it), int(it1))
+        if n > 2048:
+            assert torch.allclose(pagerank(S.to(cuda), iters=iters, tol=tol).cpu(), ref, rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.gpu
 def test_word2vec_and_doc2vec_kernel(cuda):
     docs, labels, topics = _topic_corpus(400)
     w2v = Word2Vec(dim=16, window=3, epochs=5, seed=0, device=cuda).fit(docs)
