@@ -139,6 +139,8 @@ def kendall_tau_b(x, y) -> tuple[float, float]:
     from scipy import stats
     x, y = _dev(x), _dev(y).to(_dev(x).device)
     n = x.numel()
+    if bool(torch.isnan(x).any() | torch.isnan(y).any()):
+        return float("nan"), float("nan")          # scipy's nan_policy="propagate"
     cnt = kendall_counts(x, y).tolist()
     con, dis = cnt[0], cnt[1]
     _, tx, _ = rank_avg(x)

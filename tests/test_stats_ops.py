@@ -49,6 +49,14 @@ def test_rank_statistics_match_scipy(ties):
     assert h == pytest.approx(ref.statistic, rel=1e-10) and p == pytest.approx(ref.pvalue, rel=1e-6)
 
 
+def test_kendall_nan_propagates():
+    x, y = _samples(50, seed=1)
+    x[7] = np.nan
+    tau, p = S.kendall_tau_b(torch.tensor(x), torch.tensor(y))
+    ref = stats.kendalltau(x, y)
+    assert np.isnan(tau) and np.isnan(p) and np.isnan(ref.statistic)
+
+
 def test_small_samples_use_exact_paths():
     x = np.array([3.1, 1.2, 5.5, 4.0, 2.2, 9.1, 7.3])
     y = np.array([2.0, 1.0, 6.0, 3.0, 2.5, 8.0, 9.0])
