@@ -270,8 +270,8 @@ def top_matches(args):
     S, Tt, Rk = S[order], Tt[order], Rk[order]
     first = torch.ones_like(S, dtype=torch.bool)
     first[1:] = S[1:] != S[:-1]
-    start = torch.cummax(torch.where(first, torch.arange(len(S)), torch.zeros_like(S)), 0).values
-    pos = torch.arange(len(S)) - start
+    from ..data.records import segment_rank
+    pos = segment_rank(first)
     keep = torch.ones_like(S, dtype=torch.bool)
     if topn is not None:
         keep &= pos < topn
@@ -342,9 +342,8 @@ def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact
     first = torch.ones(n, dtype=torch.bool, device=dev)
     if n > 1:
         first[1:] = spos[1:] != spos[:-1]
-    idx = torch.arange(n, device=dev)
-    start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
-    rank_in = idx - start
+    from ..data.records import segment_rank
+    rank_in = segment_rank(first)
     keep = torch.ones(n, dtype=torch.bool, device=dev)
     if topn is not None:
         keep &= rank_in < topn

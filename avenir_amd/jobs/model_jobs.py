@@ -329,8 +329,8 @@ def nearest_neighbor(args):
     Wv = torch.tensor([w[sel[i]] for i in order.tolist()], dtype=torch.float64) if w is not None else None
     first = torch.ones_like(T, dtype=torch.bool)
     first[1:] = T[1:] != T[:-1]
-    start = torch.cummax(torch.where(first, torch.arange(len(T)), torch.zeros_like(T)), 0).values
-    rank = torch.arange(len(T)) - start
+    from ..data.records import segment_rank
+    rank = segment_rank(first)
     keep = rank < k
     nn = NearestNeighbor.from_config(ctx.cfg)
     nt, C = len(tests), len(classes)
@@ -422,9 +422,8 @@ def _nearest_neighbor_native(ctx, rec, W, ccw, val, k, out_distr):
     first = torch.ones(m, dtype=torch.bool, device=dev)
     if m > 1:
         first[1:] = t[1:] != t[:-1]
-    idx = torch.arange(m, device=dev)
-    start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
-    rank = idx - start
+    from ..data.records import segment_rank
+    rank = segment_rank(first)
     keep = (rank < k) & (cls_idx >= 0)      # neighbours of an unknown class do not vote
     nn = NearestNeighbor.from_config(ctx.cfg)
     dk = torch.full((nt, k), math.inf, dtype=torch.float32, device=dev)
