@@ -2229,16 +2229,19 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
   if (nl) avk::csv_newline_positions(dev.data_ptr<uint8_t>(), size, reinterpret_cast<long long*>(offsets.data_ptr<int64_t>()),
                                      reinterpret_cast<long long*>(pos.data_ptr<int64_t>()), stream);
   if (tail) pos.narrow(0, nl, 1).fill_(size);
-  auto starts = at::cat({at::zeros({1}, pos.options()), pos.narrow(0, 0, std::max<int64_t>(0, pos.numel() - 1)) + 1});
-  starts = starts.narrow(0, 0, pos.numel());
-  auto ends = pos;
-  // blank lines (empty after dropping a trailing CR) are skipped, as in the host parser
-  if (pos.numel()) {
-    auto lens = ends - starts;
-    auto lastc = dev.index({(ends - 1).clamp_min(0)}).to(at::kLong);
-    auto eff = lens - ((lastc == '\r') & (lens > 0)).to(at::kLong);
-    auto keep = eff > 0;
-    if (!keep.all().item<bool>()) {
+  // line bounds + blank-line flags in one pass; blank lines (empty after dropping a trailing CR)
+  // are skipped, as in the host parser (compaction only when some exist)
+  const int64_t nlines = pos.numel();
+  auto starts = at::empty({nlines}, pos.options());
+  auto ends = at::empty({nlines}, pos.options());
+  if (nlines) {
+    auto keep = at::empty({nlines}, pos.options().dtype(at::kByte));
+    auto blank = at::zeros({1}, pos.options());
+    avk::csv_line_bounds(dev.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(pos.data_ptr<int64_t>()), nlines,
+                         reinterpret_cast<long long*>(starts.data_ptr<int64_t>()),
+                         reinterpret_cast<long long*>(ends.data_ptr<int64_t>()), keep.data_ptr<uint8_t>(),
+                         reinterpret_cast<unsigned long long*>(blank.data_ptr<int64_t>()), stream);
+    if (blank.item<int64_t>() > 0) {
       auto idx = at::nonzero(keep).view({-1});
       starts = starts.index({idx});
       ends = ends.index({idx});

@@ -203,6 +203,10 @@ long long csv_chunks(long long size);
 void csv_newline_counts(const uint8_t* bytes, long long size, unsigned* counts, hipStream_t stream);
 void csv_newline_positions(const uint8_t* bytes, long long size, const long long* offsets, long long* pos,
                            hipStream_t stream);
+// per line: starts / ends (line i ends at pos[i]), keep = not blank (CR-only lines are blank),
+// *blank += blank lines
+void csv_line_bounds(const uint8_t* bytes, const long long* pos, long long nl, long long* starts, long long* ends,
+                     uint8_t* keep, unsigned long long* blank, hipStream_t stream);
 void csv_parse_rows(const uint8_t* bytes, long long size_padded, const long long* starts, const long long* ends,
                     long long n, char delim, const void* specs, int nspecs, int max_ord, const int* tabs,
                     const int* voff, const int* vlen, const uint8_t* vbytes, int ntab, int nvoc, int nvb,
