@@ -1,6 +1,8 @@
 #include <atomic>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <chrono>
 #include <limits>
 #include <map>
@@ -2133,11 +2135,68 @@ static bool upload_pread() {
   return !(e && std::string(e) == "mmap");
 }
 
+// Persistent host workers for the staging fills (a fill of 64 MB used to spawn and join 16 threads,
+// ~15 us each, for every slot).  run(T, fn) calls fn(0..T-1), part 0 on the caller, and returns when
+// all parts are done.  The pool is never destroyed (no join at interpreter exit).
+class FillPool {
+ public:
+  static FillPool& get() {  // a forked child has none of the parent's workers: it gets its own pool
+    static std::mutex m;
+    static FillPool* p = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> g(m);
+    if (!p || owner != ::getpid()) {
+      p = new FillPool();
+      owner = ::getpid();
+    }
+    return *p;
+  }
+  void run(int T, const std::function<void(int)>& fn) {
+    std::unique_lock<std::mutex> call(call_mu_);  // one parallel fill at a time
+    while ((int)workers_.size() < T - 1) workers_.emplace_back([this, id = (int)workers_.size() + 1] { loop(id); });
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn_ = &fn;
+      parts_ = T;
+      pending_ = T - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= parts_) continue;
+        f = fn_;
+      }
+      (*f)(id);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int parts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
 // bytes [off, off + len) of fd into dst with T threads; pread may return short counts
 static void pread_parallel(int fd, char* dst, int64_t off, int64_t len, int T) {
-  std::vector<std::thread> th;
   std::atomic<bool> bad{false};
-  auto part = [&](int t) {
+  std::function<void(int)> part = [&](int t) {
     int64_t a = len * t / T;
     const int64_t b = len * (t + 1) / T;
     while (a < b) {
@@ -2146,9 +2205,7 @@ static void pread_parallel(int fd, char* dst, int64_t off, int64_t len, int T) {
       a += r;
     }
   };
-  for (int t = 1; t < T; ++t) th.emplace_back(part, t);
-  part(0);
-  for (auto& x : th) x.join();
+  FillPool::get().run(T, part);
   TORCH_CHECK(!bad, "pread failed during the device upload");
 }
 
@@ -2686,14 +2743,12 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
         const int64_t n = std::min(cap - fill, pieces[pi].len - pofs);
         const char* src = pieces[pi].p + pofs;
         const int T = n >= (8 << 20) ? upload_threads() : 1;
-        std::vector<std::thread> th;
-        for (int t = 1; t < T; ++t)
-          th.emplace_back([&, t] {
-            const int64_t a = n * t / T, b = n * (t + 1) / T;
-            std::memcpy(dst + fill + a, src + a, (size_t)(b - a));
-          });
-        std::memcpy(dst + fill, src, (size_t)(n / T));
-        for (auto& x : th) x.join();
+        std::function<void(int)> part = [&](int t) {
+          const int64_t a = n * t / T, b = n * (t + 1) / T;
+          std::memcpy(dst + fill + a, src + a, (size_t)(b - a));
+        };
+        if (T > 1) FillPool::get().run(T, part);
+        else part(0);
         fill += n;
         pofs += n;
         if (pofs == pieces[pi].len) { ++pi; pofs = 0; }
