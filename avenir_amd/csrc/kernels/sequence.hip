@@ -10,6 +10,8 @@
 // K15  Markov-chain log-odds classifier: sum over transitions of log(A0[s,s'] / A1[s,s']) with the
 //      [S, S] log-ratio table in LDS, one thread per sequence
 //      (J/markov/MarkovModelClassifier.java:127-150).
+#include <cstdlib>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -155,6 +157,86 @@ __global__ __launch_bounds__(VT) void viterbi_kernel(const ViterbiArgs a) {
   }
 }
 
+// Small state spaces (S <= SP <= 32): 64 / SP sequences share one wavefront, lane group g owns
+// sequence g and lane j of the group state j (the one-sequence-per-wave kernel left 56 of 64 lanes
+// idle at S = 8).  prev[i] comes from the group's lane i by a shuffle; a group whose sequence ended
+// keeps its delta and stops counting; the wave leaves the time loop when no group is active.
+template <int SP>
+__global__ __launch_bounds__(VT) void viterbi_small_kernel(const ViterbiArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sA[];  // [S][S]
+  constexpr int G = 64 / SP;
+  const int S = a.S, T = a.T, O = a.O, mode = a.mode;
+  for (int i = threadIdx.x; i < S * S; i += VT) sA[i] = a.logA[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, grp = lane / SP, j = lane % SP, base = grp * SP;
+  const long long seq = ((long long)blockIdx.x * (VT / 64) + (threadIdx.x >> 6)) * G + grp;
+  const bool live = seq < a.n;
+  const bool js = live && j < S;
+  const short* ob = a.obs + (live ? (seq / a.obs_div) * T : 0);
+  const float* logpi = a.logpi + (live ? (seq % a.pi_mod) * S : 0);
+  const float* logB = a.logB;
+  short* bp = a.bp;
+  const int o0 = live ? ob[0] : -1;
+  float delta = (js && o0 >= 0 && o0 < O) ? logpi[j] + logB[(long long)j * O + o0] : -INFINITY;
+  int len = (live && o0 >= 0) ? 1 : 0;
+  bool act = live;
+  for (int t = 1; t < T; ++t) {
+    const int ot = act ? ob[t] : -1;
+    if (ot < 0 || ot >= O) act = false;
+    if (!__any(act)) break;
+    float nd = -INFINITY, se = 0.f;
+    short arg = 0;
+    for (int i = 0; i < S; ++i) {
+      const float prev = __shfl(delta, base + i, 64);
+      const float v = prev + (j < S ? sA[i * S + (j < S ? j : 0)] : 0.f);
+      if (mode == 0) {
+        if (v > nd) { nd = v; arg = (short)i; }
+      } else {
+        if (v > nd) { se = se * __expf(nd - v) + 1.f; nd = v; }
+        else if (v > -INFINITY) se += __expf(v - nd);
+      }
+    }
+    if (mode != 0) nd = (nd > -INFINITY) ? nd + __logf(se) : -INFINITY;
+    if (act && j < S) {
+      delta = nd + logB[(long long)j * O + ot];
+      if (bp) bp[(seq * T + t) * S + j] = arg;
+    }
+    if (act) ++len;
+  }
+  if (a.delta_out && js) a.delta_out[seq * S + j] = delta;
+  float best = js ? delta : -INFINITY;
+  int barg = js ? j : 0;
+#pragma unroll
+  for (int o = SP / 2; o > 0; o >>= 1) {  // group argmax, ties -> lowest state (as wave_argmax)
+    const float v2 = __shfl_xor(best, o, 64);
+    const int i2 = __shfl_xor(barg, o, 64);
+    if (v2 > best || (v2 == best && i2 < barg)) { best = v2; barg = i2; }
+  }
+  if (mode == 0) {
+    if (live && j == 0) {
+      if (a.score) a.score[seq] = best;
+      if (a.path) {
+        short* pth = a.path + seq * T;
+        for (int t = len; t < T; ++t) pth[t] = -1;
+        if (len > 0) {
+          int st = barg;
+          pth[len - 1] = (short)st;
+          for (int t = len - 1; t > 0; --t) {
+            st = bp[(seq * T + t) * S + st];
+            pth[t - 1] = (short)st;
+          }
+        }
+      }
+    }
+  } else {
+    float m = best;  // group max (best is the group's max after the argmax reduction)
+    float e = (js && delta > -INFINITY) ? __expf(delta - m) : 0.f;
+#pragma unroll
+    for (int o = SP / 2; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+    if (live && j == 0 && a.score) a.score[seq] = (len > 0 && m > -INFINITY) ? m + __logf(e) : -INFINITY;
+  }
+}
+
 // Chunked-Viterbi back-tracking (sequence_ops.viterbi_long): thread k follows the back-pointers
 // of chunk k / per_chunk from state ends[k] at the chunk's last position down to position 0,
 // writing the state reached there (first[k]: the chunk's end -> start map) and / or the path.
@@ -184,12 +266,24 @@ __global__ __launch_bounds__(256) void viterbi_backtrack_kernel(const short* __r
   if (first) first[k] = s;
 }
 
+static bool small_off() {  // AVMI_VITERBI_SMALL=0: one sequence per wavefront at any S (A/B switch)
+  const char* e = std::getenv("AVMI_VITERBI_SMALL");
+  return e && e[0] == '0';
+}
+
 void launch_viterbi(const ViterbiArgs& a, hipStream_t stream) {
   if (a.n <= 0 || a.T <= 0) return;
   if ((size_t)a.S * a.S * sizeof(float) > 160 * 1024) throw std::runtime_error("viterbi: S too large for LDS");
   const unsigned grid = (unsigned)((a.n + 3) / 4);
   const size_t lds = (size_t)a.S * a.S * sizeof(float);
-  if (a.S <= 64)
+  if (a.S <= 32 && !small_off()) {  // several sequences per wavefront
+    const int sp = a.S <= 8 ? 8 : (a.S <= 16 ? 16 : 32);
+    const long long per_block = (VT / 64) * (64 / sp);
+    const unsigned g2 = (unsigned)((a.n + per_block - 1) / per_block);
+    if (sp == 8) viterbi_small_kernel<8><<<g2, VT, lds, stream>>>(a);
+    else if (sp == 16) viterbi_small_kernel<16><<<g2, VT, lds, stream>>>(a);
+    else viterbi_small_kernel<32><<<g2, VT, lds, stream>>>(a);
+  } else if (a.S <= 64)
     viterbi_kernel<1><<<grid, VT, lds, stream>>>(a);
   else if (a.S <= 128)
     viterbi_kernel<2><<<grid, VT, lds, stream>>>(a);
