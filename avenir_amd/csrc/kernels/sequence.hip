@@ -315,6 +315,37 @@ __global__ __launch_bounds__(256) void markov_logodds_kernel(const short* __rest
   }
 }
 
+// Tiled variant: 256 sequences' states staged in LDS by coalesced 2-byte loads (row stride L + 1
+// shorts), then every thread walks its own sequence from LDS; the plain kernel's per-thread walk
+// touched 64 different rows per load instruction.
+__global__ __launch_bounds__(256) void markov_logodds_tiled_kernel(const short* __restrict__ st, long long n, int L,
+                                                                    const float* __restrict__ lr, int S,
+                                                                    float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sL[];
+  short* tile = reinterpret_cast<short*>(sL + S * S);
+  const int LP = L + 1;
+  for (int i = threadIdx.x; i < S * S; i += 256) sL[i] = lr[i];
+  for (long long r0 = (long long)blockIdx.x * 256; r0 < n; r0 += (long long)gridDim.x * 256) {
+    const int rows = (int)min(256LL, n - r0);
+    __syncthreads();  // lr staged / the previous tile fully walked
+    const short* src = st + r0 * L;
+    for (int e = threadIdx.x; e < rows * L; e += 256) tile[(e / L) * LP + e % L] = src[e];
+    __syncthreads();
+    if (threadIdx.x < rows) {
+      const short* s = tile + threadIdx.x * LP;
+      float acc = 0.f;
+      int a = s[0];
+      for (int j = 1; j < L; ++j) {
+        const int b = s[j];
+        if (a < 0 || b < 0 || a >= S || b >= S) break;
+        acc += sL[a * S + b];
+        a = b;
+      }
+      out[r0 + threadIdx.x] = acc;
+    }
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -344,8 +375,13 @@ void viterbi_backtrack(const short* bp, const int* lens, const int* ends, long l
 void markov_logodds(const short* states, long long n, int L, const float* lr, int S, float* out,
                     hipStream_t stream) {
   if (n <= 0) return;
-  markov_logodds_kernel<<<av::stream_grid(n, 256, 2, 4096), 256, (size_t)S * S * sizeof(float), stream>>>(
-      states, n, L, lr, S, out);
+  const size_t tiled = (size_t)S * S * sizeof(float) + (size_t)256 * (L + 1) * sizeof(short);
+  const char* e = std::getenv("AVMI_LOGODDS_TILED");
+  if (tiled <= 64 * 1024 && !(e && e[0] == '0'))
+    markov_logodds_tiled_kernel<<<av::stream_grid(n, 256, 1, 4096), 256, tiled, stream>>>(states, n, L, lr, S, out);
+  else
+    markov_logodds_kernel<<<av::stream_grid(n, 256, 2, 4096), 256, (size_t)S * S * sizeof(float), stream>>>(
+        states, n, L, lr, S, out);
   AV_HIP_CHECK(hipGetLastError());
 }
 
