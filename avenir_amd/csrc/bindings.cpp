@@ -2378,36 +2378,45 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
     outs.push_back(o);
     order.push_back({sp.ordinal, idx++});
   }
-  TORCH_CHECK(hs.size() <= 32, "device CSV parse: at most 32 columns");
   std::stable_sort(order.begin(), order.end());
-  std::vector<HostSpec> sorted;
-  int max_ord = 0;
-  for (auto& pr : order) {
-    sorted.push_back(hs[(size_t)pr.second]);
-    max_ord = std::max(max_ord, pr.first);
-  }
   auto hopt = at::TensorOptions().dtype(at::kByte);
-  auto spec_h = at::empty({(int64_t)(sorted.size() * sizeof(HostSpec))}, hopt);
-  if (!sorted.empty()) std::memcpy(spec_h.data_ptr<uint8_t>(), sorted.data(), sorted.size() * sizeof(HostSpec));
   auto to_i32 = [&](const std::vector<int>& v) {
     auto t = at::empty({(int64_t)std::max<size_t>(1, v.size())}, at::TensorOptions().dtype(at::kInt));
     if (!v.empty()) std::memcpy(t.data_ptr<int>(), v.data(), v.size() * sizeof(int));
     return t.to(like.device());
   };
-  auto spec_d = spec_h.to(like.device());
   auto tabs_d = to_i32(tabs), voff_d = to_i32(voff), vlen_d = to_i32(vlen);
   auto vb_h = at::empty({(int64_t)std::max<size_t>(1, vbytes.size())}, hopt);
   if (!vbytes.empty()) std::memcpy(vb_h.data_ptr<uint8_t>(), vbytes.data(), vbytes.size());
   auto vb_d = vb_h.to(like.device());
   auto bad = at::zeros({1}, like.options().dtype(at::kLong));
-  avk::csv_parse_rows(dev.data_ptr<uint8_t>(), dev.numel(), reinterpret_cast<const long long*>(starts.data_ptr<int64_t>()),
-                      reinterpret_cast<const long long*>(ends.data_ptr<int64_t>()), n, delim[0], spec_d.data_ptr<uint8_t>(),
-                      (int)sorted.size(), max_ord, tabs_d.data_ptr<int>(), voff_d.data_ptr<int>(), vlen_d.data_ptr<int>(),
-                      vb_d.data_ptr<uint8_t>(), (int)tabs_d.numel(), (int)vlen_d.numel(), (int)vbytes.size(),
-                      reinterpret_cast<unsigned long long*>(bad.data_ptr<int64_t>()), stream);
+  auto bad_scratch = at::zeros({1}, like.options().dtype(at::kLong));
+  // wide schemas in passes of up to 64 columns (ordinal order): each pass walks a row only up to
+  // its last column; short rows are counted by the pass holding the largest ordinal
+  constexpr size_t GROUP = 64;
+  const size_t ng = (order.size() + GROUP - 1) / GROUP;
+  for (size_t g0 = 0; g0 < order.size(); g0 += GROUP) {
+    std::vector<HostSpec> sorted;
+    int max_ord = 0;
+    for (size_t k = g0; k < std::min(order.size(), g0 + GROUP); ++k) {
+      sorted.push_back(hs[(size_t)order[k].second]);
+      max_ord = std::max(max_ord, order[k].first);
+    }
+    auto spec_h = at::empty({(int64_t)(sorted.size() * sizeof(HostSpec))}, hopt);
+    std::memcpy(spec_h.data_ptr<uint8_t>(), sorted.data(), sorted.size() * sizeof(HostSpec));
+    auto spec_d = spec_h.to(like.device());
+    const bool last_group = g0 / GROUP == ng - 1;
+    avk::csv_parse_rows(dev.data_ptr<uint8_t>(), dev.numel(), reinterpret_cast<const long long*>(starts.data_ptr<int64_t>()),
+                        reinterpret_cast<const long long*>(ends.data_ptr<int64_t>()), n, delim[0], spec_d.data_ptr<uint8_t>(),
+                        (int)sorted.size(), max_ord, tabs_d.data_ptr<int>(), voff_d.data_ptr<int>(), vlen_d.data_ptr<int>(),
+                        vb_d.data_ptr<uint8_t>(), (int)tabs_d.numel(), (int)vlen_d.numel(), (int)vbytes.size(),
+                        reinterpret_cast<unsigned long long*>((last_group ? bad : bad_scratch).data_ptr<int64_t>()),
+                        stream);
+  }
   py::list cols;
   for (auto& o : outs) cols.append(o);
-  return py::make_tuple(cols, n, bad, total, row_begin);
+  // the rows' byte spans in the file (raw-line output of the jobs: data/lines.py)
+  return py::make_tuple(cols, n, bad, total, row_begin, starts, ends);
 }
 
 // K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
@@ -2943,6 +2952,16 @@ py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& deli
     } else if (kind == "c" || kind == "g") {
       c.kind = kind == "c" ? avh::FmtCol::LIT : avh::FmtCol::GLUE;
       c.lit = t[1].cast<std::string>();
+    } else if (kind == "r" || kind == "rf" || kind == "rt") {
+      // raw input lines: (kind, owner, addr int64 [n], len int64 [n], [field,] from_delims); the
+      // owner (a CsvFile / TextShard / mapping) keeps the bytes alive for the call
+      TORCH_CHECK(!t[1].is_none(), "format_columns: raw line column without its owner");
+      c.kind = kind == "r" ? avh::FmtCol::RAW : (kind == "rf" ? avh::FmtCol::FIELD : avh::FmtCol::TAIL);
+      c.raddr = cpu_tensor(t[2], at::kLong, n, "line address").data_ptr<int64_t>();
+      c.rlen = cpu_tensor(t[3], at::kLong, n, "line length").data_ptr<int64_t>();
+      size_t k = 4;
+      if (kind != "r") c.field = t[k++].cast<int>();
+      if (t.size() > k) c.from_delims = t[k].cast<std::string>();
     } else {
       TORCH_CHECK(false, "format_columns: unknown column kind ", kind);
     }
@@ -2954,6 +2973,39 @@ py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& deli
     out = avh::format_columns(cols, n, delim, nthreads);
   }
   return py::bytes(out);
+}
+
+// pack_spans(addr int64 [n], len int64 [n], nthreads) -> (bytes uint8 [sum len], off int64 [n + 1]):
+// the lines behind byte spans (data/lines.py) copied into one contiguous buffer — the payload that
+// travels around the ring of the all-pairs similarity jobs.  Rows are split over the threads.
+py::tuple pack_spans(const at::Tensor& addr_in, const at::Tensor& len_in, int nthreads) {
+  auto addr = addr_in.to(at::kCPU).to(at::kLong).contiguous();
+  auto len = len_in.to(at::kCPU).to(at::kLong).contiguous();
+  TORCH_CHECK(addr.numel() == len.numel(), "pack_spans: address / length size mismatch");
+  const int64_t n = addr.numel();
+  auto off = at::empty({n + 1}, at::kLong);
+  int64_t* o = off.data_ptr<int64_t>();
+  const int64_t* a = addr.data_ptr<int64_t>();
+  const int64_t* l = len.data_ptr<int64_t>();
+  o[0] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    TORCH_CHECK(l[i] >= 0, "pack_spans: negative length");
+    o[i + 1] = o[i] + l[i];
+  }
+  auto bytes = at::empty({std::max<int64_t>(o[n], 1)}, at::kByte);
+  uint8_t* dst = bytes.data_ptr<uint8_t>();
+  {
+    py::gil_scoped_release rel;
+    const int T = n < 65536 ? 1 : std::max(1, std::min(nthreads, 64));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        for (int64_t i = n * t / T; i < n * (t + 1) / T; ++i)
+          if (l[i]) std::memcpy(dst + o[i], reinterpret_cast<const void*>(a[i]), (size_t)l[i]);
+      });
+    for (auto& x : th) x.join();
+  }
+  return py::make_tuple(bytes.narrow(0, 0, o[n]), off);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3151,6 +3203,13 @@ PYBIND11_MODULE(_C, m) {
       .def("column_strings", &avh::CsvFile::column_strings)
       .def("line", &avh::CsvFile::line)
       .def("lines", &avh::CsvFile::lines)
+      .def("line_spans", [](const avh::CsvFile& f, int64_t b, int64_t e) {
+        b = std::max<int64_t>(0, b);
+        e = std::max(b, std::min<int64_t>(f.num_rows(), e));
+        auto addr = at::empty({e - b}, at::kLong), len = at::empty({e - b}, at::kLong);
+        f.line_spans(b, e, addr.data_ptr<int64_t>(), len.data_ptr<int64_t>());
+        return py::make_tuple(addr, len);
+      })
       .def("parse", &csv_parse, py::arg("specs"), py::arg("row_begin") = 0, py::arg("row_end") = -1);
   py::class_<avh::TextShard>(m, "TextShard")
       .def(py::init([](std::vector<std::string> paths, int64_t rank, int64_t world, int nthreads, bool skip_header) {
@@ -3163,6 +3222,11 @@ PYBIND11_MODULE(_C, m) {
       .def("bytes_read", &avh::TextShard::bytes_read)
       .def("total_bytes", &avh::TextShard::total_bytes)
       .def("lines", &avh::TextShard::lines)
+      .def("line_spans", [](const avh::TextShard& sh) {
+        auto addr = at::empty({sh.num_lines()}, at::kLong), len = at::empty({sh.num_lines()}, at::kLong);
+        sh.line_spans(addr.data_ptr<int64_t>(), len.data_ptr<int64_t>());
+        return py::make_tuple(addr, len);
+      })
       .def("tokenize", &text_tokenize, py::arg("delims") = ",", py::arg("sub_delim") = "", py::arg("modes") = "",
            py::arg("tail_mode") = "d", py::arg("trim") = false, py::arg("want_nums") = false,
            py::arg("last_mode") = "")
@@ -3174,6 +3238,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("format_columns", &format_columns_py, py::arg("cols"), py::arg("n"), py::arg("delim") = ",",
         py::arg("nthreads") = 8);
   m.def("format_rows", &format_rows);
+  m.def("pack_spans", &pack_spans, py::arg("addr"), py::arg("len"), py::arg("nthreads") = 16);
   m.def("write_coded_csv", [](const std::string& path, const at::Tensor& codes, int64_t n,
                               std::vector<std::vector<std::string>> vocab, std::string id_prefix, std::string delim,
                               int nthreads) {

@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "avenir_host.h"
+#include "avenir_numparse.h"
 
 namespace avh {
 
@@ -25,33 +26,15 @@ inline std::string_view trim(std::string_view s) {
   return s;
 }
 
-// Fast decimal parser: [+-]digits[.digits][(e|E)[+-]digits]; NaN on garbage / empty.
+// Decimal parser (avenir_numparse.h, shared with the device K1 kernels): correctly rounded,
+// strtod for the rare fields beyond the exact fast path; NaN on garbage / empty.
 inline double parse_double(std::string_view s) {
   s = trim(s);
-  if (s.empty()) return std::nan("");
-  const char* p = s.data();
-  const char* e = p + s.size();
-  bool neg = false;
-  if (*p == '+' || *p == '-') { neg = (*p == '-'); ++p; }
-  double v = 0;
-  int digits = 0;
-  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++digits; }
-  if (p < e && *p == '.') {
-    ++p;
-    double scale = 0.1;
-    while (p < e && *p >= '0' && *p <= '9') { v += (*p - '0') * scale; scale *= 0.1; ++p; ++digits; }
-  }
-  if (digits == 0) return std::nan("");
-  if (p < e && (*p == 'e' || *p == 'E')) {
-    ++p;
-    bool eneg = false;
-    if (p < e && (*p == '+' || *p == '-')) { eneg = (*p == '-'); ++p; }
-    int ex = 0;
-    while (p < e && *p >= '0' && *p <= '9') { ex = ex * 10 + (*p - '0'); ++p; }
-    v *= std::pow(10.0, eneg ? -ex : ex);
-  }
-  if (p != e) return std::nan("");
-  return neg ? -v : v;
+  bool slow = false;
+  const double v = avnum::parse_decimal(s.data(), s.data() + s.size(), &slow);
+  if (!slow) return v;
+  const std::string z(s);
+  return std::strtod(z.c_str(), nullptr);
 }
 
 inline int64_t parse_int(std::string_view s, bool* ok) {
@@ -405,6 +388,16 @@ std::vector<std::string> CsvFile::lines(int64_t b, int64_t e) const {
   for (int64_t i = b; i < e; ++i)
     out.emplace_back(data_ + line_start_[i], (size_t)(line_end_[i] - line_start_[i]));
   return out;
+}
+
+void CsvFile::line_spans(int64_t b, int64_t e, int64_t* addr, int64_t* len) const {
+  b = std::max<int64_t>(0, b);
+  e = std::min<int64_t>(num_rows(), e);
+  const int64_t base = (int64_t)reinterpret_cast<uintptr_t>(data_);
+  for (int64_t i = b; i < e; ++i) {
+    addr[i - b] = base + line_start_[(size_t)i];
+    len[i - b] = line_end_[(size_t)i] - line_start_[(size_t)i];
+  }
 }
 
 std::string format_rows(const std::vector<std::string>* prefix, const double* cols, int ncol,

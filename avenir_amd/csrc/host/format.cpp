@@ -3,9 +3,12 @@
 // reference's reducers write one Text line per record through Hadoop's TextOutputFormat; jobs here
 // produce millions of output lines per rank (neighbour lists, per-entity predictions), which Python
 // string joins would spend seconds on.
+#include <charconv>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <stdexcept>
+#include <array>
 #include <thread>
 
 #include "avenir_host.h"
@@ -14,9 +17,67 @@ namespace avh {
 
 namespace {
 
+// Python's repr(float): the shortest digit string that round-trips (std::to_chars), written in
+// fixed notation for decimal exponents -4 <= e < 16 and as d.ddde[+-]XX otherwise.
+inline void put_pyrepr(std::string& s, double v) {
+  if (std::isnan(v)) {
+    s += "nan";
+    return;
+  }
+  if (std::isinf(v)) {
+    s += v < 0 ? "-inf" : "inf";
+    return;
+  }
+  char buf[40];
+  auto res = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+  const char* p = buf;
+  const char* end = res.ptr;
+  if (*p == '-') {
+    s.push_back('-');
+    ++p;
+  }
+  char dig[24];
+  int nd = 0;
+  const char* q = p;
+  for (; q < end && *q != 'e'; ++q)
+    if (*q != '.') dig[nd++] = *q;
+  int ex = 0;  // to_chars does not terminate the buffer: parse the exponent up to ``end``
+  bool eneg = false;
+  for (const char* c = q + 1; c < end; ++c) {
+    if (*c == '-') eneg = true;
+    else if (*c >= '0' && *c <= '9') ex = ex * 10 + (*c - '0');
+  }
+  if (eneg) ex = -ex;
+  if (ex >= -4 && ex < 16) {
+    if (ex >= 0) {
+      for (int i = 0; i <= ex; ++i) s.push_back(i < nd ? dig[i] : '0');
+      s.push_back('.');
+      if (nd > ex + 1) s.append(dig + ex + 1, (size_t)(nd - ex - 1));
+      else s.push_back('0');
+    } else {
+      s += "0.";
+      s.append((size_t)(-ex - 1), '0');
+      s.append(dig, (size_t)nd);
+    }
+    return;
+  }
+  s.push_back(dig[0]);
+  if (nd > 1) {
+    s.push_back('.');
+    s.append(dig + 1, (size_t)(nd - 1));
+  }
+  char eb[8];
+  const int el = snprintf(eb, sizeof eb, "e%c%02d", ex < 0 ? '-' : '+', ex < 0 ? -ex : ex);
+  s.append(eb, (size_t)el);
+}
+
 inline void put_double(std::string& s, double v, int prec) {
   char buf[64];
   int len;
+  if (prec == -2) {
+    put_pyrepr(s, v);
+    return;
+  }
   if (std::isnan(v)) {
     s += "NaN";
     return;
@@ -32,6 +93,55 @@ inline void put_int(std::string& s, int64_t v) {
   s.append(buf, (size_t)len);
 }
 
+// [a, e) of field ``f`` of the line [p, p + n) split at any character with sep[c] set (f < 0:
+// counted from the end); false when the line has fewer fields
+inline bool field_span(const char* p, int64_t n, int f, const uint8_t* sep, const char** a, const char** e) {
+  const char* end = p + n;
+  if (f >= 0) {
+    const char* s = p;
+    for (int k = 0; k < f; ++k) {
+      while (s < end && !sep[(uint8_t)*s]) ++s;
+      if (s >= end) return false;
+      ++s;
+    }
+    const char* t = s;
+    while (t < end && !sep[(uint8_t)*t]) ++t;
+    *a = s;
+    *e = t;
+    return true;
+  }
+  const char* t = end;
+  for (int k = -1; k > f; --k) {
+    while (t > p && !sep[(uint8_t)t[-1]]) --t;
+    if (t <= p) return false;
+    --t;
+  }
+  const char* s = t;
+  while (s > p && !sep[(uint8_t)s[-1]]) --s;
+  *a = s;
+  *e = t;
+  return true;
+}
+
+// append [p, p + n) with every separator character replaced by ``delim`` (copied as is when the
+// only separator is the delimiter itself)
+inline void put_rejoined(std::string& s, const char* p, int64_t n, const uint8_t* sep, bool same,
+                         const std::string& delim) {
+  if (same) {
+    s.append(p, (size_t)n);
+    return;
+  }
+  const char* end = p + n;
+  const char* a = p;
+  for (const char* c = p; c < end; ++c)
+    if (sep[(uint8_t)*c]) {
+      s.append(a, (size_t)(c - a));
+      s += delim;
+      a = c + 1;
+    }
+  s.append(a, (size_t)(end - a));
+}
+
 }  // namespace
 
 std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads) {
@@ -39,6 +149,16 @@ std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std
     if ((c.kind == FmtCol::STR || c.kind == FmtCol::LIST) && (!c.table || !c.idx))
       throw std::runtime_error("format_columns: string column without table / index");
     if (c.kind == FmtCol::LIST && !c.off) throw std::runtime_error("format_columns: list column without offsets");
+    if ((c.kind == FmtCol::RAW || c.kind == FmtCol::FIELD || c.kind == FmtCol::TAIL) && (!c.raddr || !c.rlen))
+      throw std::runtime_error("format_columns: line column without spans");
+  }
+  // per column: separator table of the raw-line kinds, and whether re-joining changes nothing
+  std::vector<std::array<uint8_t, 256>> seps(cols.size());
+  std::vector<char> same(cols.size(), 0);
+  for (size_t k = 0; k < cols.size(); ++k) {
+    seps[k].fill(0);
+    for (char ch : cols[k].from_delims) seps[k][(uint8_t)ch] = 1;
+    same[k] = cols[k].from_delims.empty() || cols[k].from_delims == delim;
   }
   const int T = n < 16384 ? 1 : std::max(1, nthreads);
   std::vector<std::string> parts(T);
@@ -52,7 +172,8 @@ std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std
         s.reserve((size_t)(r1 - r0) * (8 * cols.size() + 8));
         for (int64_t r = r0; r < r1; ++r) {
           bool first = true;
-          for (const auto& c : cols) {
+          for (size_t ci = 0; ci < cols.size(); ++ci) {
+            const auto& c = cols[ci];
             if (c.kind == FmtCol::GLUE) {
               s += c.lit;
               continue;
@@ -84,6 +205,23 @@ std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std
               case FmtCol::LIT:
                 s += c.lit;
                 break;
+              case FmtCol::RAW:
+                put_rejoined(s, reinterpret_cast<const char*>(c.raddr[r]), c.rlen[r], seps[ci].data(), same[ci],
+                             delim);
+                break;
+              case FmtCol::FIELD: {
+                const char *a, *e;
+                if (field_span(reinterpret_cast<const char*>(c.raddr[r]), c.rlen[r], c.field, seps[ci].data(), &a, &e))
+                  s.append(a, (size_t)(e - a));
+                break;
+              }
+              case FmtCol::TAIL: {
+                const char* p = reinterpret_cast<const char*>(c.raddr[r]);
+                const char *a, *e;
+                if (field_span(p, c.rlen[r], c.field, seps[ci].data(), &a, &e))
+                  put_rejoined(s, a, (int64_t)(p + c.rlen[r] - a), seps[ci].data(), false, delim);
+                break;
+              }
               default:
                 break;
             }

@@ -29,6 +29,7 @@
 #include <thread>
 
 #include "avenir_host.h"
+#include "avenir_numparse.h"
 
 namespace avh {
 
@@ -36,32 +37,16 @@ namespace {
 
 inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
-// decimal parser shared with csv.cpp semantics (NaN on garbage / empty)
+// decimal parser shared with csv.cpp and the device tokenizer (avenir_numparse.h: correctly
+// rounded; strtod for the rare fields beyond the exact fast path), NaN on garbage / empty
 inline double parse_num(const char* p, const char* e) {
   while (p < e && is_ws(*p)) ++p;
   while (e > p && is_ws(e[-1])) --e;
-  if (p == e) return std::nan("");
-  bool neg = false;
-  if (*p == '+' || *p == '-') { neg = (*p == '-'); ++p; }
-  double v = 0;
-  int digits = 0;
-  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++digits; }
-  if (p < e && *p == '.') {
-    ++p;
-    double scale = 0.1;
-    while (p < e && *p >= '0' && *p <= '9') { v += (*p - '0') * scale; scale *= 0.1; ++p; ++digits; }
-  }
-  if (digits == 0) return std::nan("");
-  if (p < e && (*p == 'e' || *p == 'E')) {
-    ++p;
-    bool eneg = false;
-    if (p < e && (*p == '+' || *p == '-')) { eneg = (*p == '-'); ++p; }
-    int ex = 0;
-    while (p < e && *p >= '0' && *p <= '9') { ex = ex * 10 + (*p - '0'); ++p; }
-    v *= std::pow(10.0, eneg ? -ex : ex);
-  }
-  if (p != e) return std::nan("");
-  return neg ? -v : v;
+  bool slow = false;
+  const double v = avnum::parse_decimal(p, e, &slow);
+  if (!slow) return v;
+  const std::string s(p, e);
+  return std::strtod(s.c_str(), nullptr);
 }
 
 // 64-bit hash of a short byte string in 8-byte words (a partial last word is loaded whole and
@@ -288,6 +273,13 @@ std::vector<std::string> TextShard::lines(int64_t b, int64_t e) const {
   out.reserve((size_t)std::max<int64_t>(0, e - b));
   for (int64_t i = b; i < e; ++i) out.emplace_back(ls_[(size_t)i], (size_t)(le_[(size_t)i] - ls_[(size_t)i]));
   return out;
+}
+
+void TextShard::line_spans(int64_t* addr, int64_t* len) const {
+  for (size_t i = 0; i < ls_.size(); ++i) {
+    addr[i] = (int64_t)reinterpret_cast<uintptr_t>(ls_[i]);
+    len[i] = (int64_t)(le_[i] - ls_[i]);
+  }
 }
 
 int64_t TextShard::count_tokens(const TokenSpec& spec) {

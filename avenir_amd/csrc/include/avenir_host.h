@@ -82,6 +82,8 @@ class CsvFile {
   std::vector<std::string> column_strings(int ordinal);
   std::string line(int64_t i) const;
   std::vector<std::string> lines(int64_t begin, int64_t end) const;
+  // absolute address and byte length of lines [begin, end) (valid while the CsvFile lives)
+  void line_spans(int64_t begin, int64_t end, int64_t* addr, int64_t* len) const;
 
  private:
   void index_lines(bool skip_header);
@@ -122,6 +124,8 @@ class TextShard {
   int64_t total_bytes() const { return bytes_.total_bytes(); }
   const ByteShard& byte_shard() const { return bytes_; }
   std::vector<std::string> lines(int64_t begin, int64_t end) const;
+  // absolute address and byte length of every line (valid while the TextShard lives)
+  void line_spans(int64_t* addr, int64_t* len) const;
   // pass 1: number of tokens under ``spec``; pass 2 fills off [L + 1], codes [T] (-1 for non-'d'
   // fields) and, when non-null, sub [T] (-1 without a sub-delimiter) and nums [T] (NaN for non-'n').
   int64_t count_tokens(const TokenSpec& spec);
@@ -146,12 +150,16 @@ class TextShard {
 std::string format_rows(const std::vector<std::string>* prefix, const double* cols, int ncol,
                         int64_t n, const std::vector<int>& precision, char delim, int nthreads);
 
-// One output column of format_columns: STR = table[idx[r]], F64 = dv[r] ("%.*f", prec < 0: "%g"),
-// I64 = iv[r], LIT = a constant, LIST = table[idx[j]] for j in [off[r], off[r+1]) (delimited, nothing
-// when empty), GLUE = a constant appended with no delimiter (brackets).  An index outside the table
-// writes an empty field.
+// One output column of format_columns: STR = table[idx[r]], F64 = dv[r] ("%.*f"; prec -1: "%g",
+// prec -2: Python's repr, the shortest round-trip digits), I64 = iv[r], LIT = a constant, LIST =
+// table[idx[j]] for j in [off[r], off[r+1]) (delimited, nothing when empty), GLUE = a constant
+// appended with no delimiter (brackets), RAW = the input line at raddr[r] (rlen[r] bytes) with every
+// character of ``from_delims`` replaced by the output delimiter (no replacement when empty), FIELD =
+// field ``field`` of that line split at any character of ``from_delims`` (negative: from the end;
+// empty when the line is shorter), TAIL = the fields ``field``.. of the line re-joined with the
+// output delimiter.  An index outside the table writes an empty field.
 struct FmtCol {
-  enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5 };
+  enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5, RAW = 6, FIELD = 7, TAIL = 8 };
   int kind = STR;
   const std::vector<std::string>* table = nullptr;
   const int32_t* idx = nullptr;
@@ -160,6 +168,10 @@ struct FmtCol {
   const int64_t* iv = nullptr;
   const int64_t* off = nullptr;
   std::string lit;
+  const int64_t* raddr = nullptr;
+  const int64_t* rlen = nullptr;
+  int field = 0;
+  std::string from_delims;
 };
 std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads);
 

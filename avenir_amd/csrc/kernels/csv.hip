@@ -17,6 +17,8 @@
 // accumulation in double, integer-division buckets, 'missing' for unknown values / short rows).
 #include "avenir_common.h"
 #include "avenir_kernels.h"
+#define AVNUM_HD __device__
+#include "avenir_numparse.h"
 
 namespace {
 
@@ -136,31 +138,14 @@ struct DevSpec {
 
 __device__ __forceinline__ bool is_space(uint8_t c) { return c == ' ' || c == '\t' || c == '\r'; }
 
-// the host parser's decimal accumulation (csrc/host/csv.cpp parse_double), NaN on garbage / empty
+// the host parser's decimal conversion (csrc/host/csv.cpp parse_double, avenir_numparse.h), NaN on
+// garbage / empty; [p, e) is trimmed by the caller
 __device__ double dev_parse_double(const uint8_t* p, const uint8_t* e) {
-  bool neg = false;
-  if (p < e && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
-  double v = 0.0;
-  int digits = 0;
-  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++digits; }
-  if (p < e && *p == '.') {
-    ++p;
-    double scale = 0.1;
-    while (p < e && *p >= '0' && *p <= '9') { v += (*p - '0') * scale; scale *= 0.1; ++p; ++digits; }
-  }
-  if (digits == 0) return __longlong_as_double(0x7ff8000000000000LL);
-  if (p < e && (*p == 'e' || *p == 'E')) {
-    ++p;
-    bool eneg = false;
-    if (p < e && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
-    int ex = 0;
-    while (p < e && *p >= '0' && *p <= '9') { ex = ex * 10 + (*p - '0'); ++p; }
-    v *= pow(10.0, eneg ? -ex : ex);
-  }
-  if (p != e) return __longlong_as_double(0x7ff8000000000000LL);
-  return neg ? -v : v;
+  bool slow;
+  return avnum::parse_decimal(reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(e), &slow);
 }
 
+constexpr int CSV_MAX_SPECS = 64;  // columns per parse pass (the host splits wider schemas)
 constexpr int PT_BYTES = 32 * 1024;  // LDS tile of the block's line bytes
 constexpr int PD_BYTES = 16 * 1024;  // LDS copy of the dictionaries (probe table, lengths, offsets, bytes)
 
@@ -240,7 +225,7 @@ __global__ __launch_bounds__(CT) void csv_parse_kernel(const uint8_t* __restrict
                                                        const int* __restrict__ vlen, const uint8_t* __restrict__ vbytes,
                                                        int ntab, int nvoc, int nvb,
                                                        unsigned long long* __restrict__ short_rows) {
-  __shared__ DevSpec s_spec[32];
+  __shared__ DevSpec s_spec[CSV_MAX_SPECS];
   __shared__ __attribute__((aligned(16))) uint8_t tile[PT_BYTES];
   __shared__ __attribute__((aligned(16))) int dict[PD_BYTES / 4];
   for (int i = threadIdx.x; i < nspecs; i += CT) s_spec[i] = specs[i];
@@ -315,7 +300,7 @@ void csv_parse_rows(const uint8_t* bytes, long long size_padded, const long long
                     const int* voff, const int* vlen, const uint8_t* vbytes, int ntab, int nvoc, int nvb,
                     unsigned long long* short_rows, hipStream_t stream) {
   if (n <= 0 || nspecs <= 0) return;
-  if (nspecs > 32) throw std::runtime_error("csv_parse_rows: at most 32 parsed columns");
+  if (nspecs > CSV_MAX_SPECS) throw std::runtime_error("csv_parse_rows: at most 64 parsed columns per pass");
   if (size_padded % 16) throw std::runtime_error("csv_parse_rows: the byte buffer must be padded to 16");
   csv_parse_kernel<<<av::stream_grid(n, CT, 1, 8192), CT, 0, stream>>>(
       bytes, size_padded, starts, ends, n, delim, reinterpret_cast<const DevSpec*>(specs), nspecs, max_ord, tabs, voff, vlen,

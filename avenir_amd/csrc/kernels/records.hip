@@ -26,6 +26,8 @@
 // with a larger table); token indices are < off[L] by construction.
 #include "avenir_common.h"
 #include "avenir_kernels.h"
+#define AVNUM_HD __device__
+#include "avenir_numparse.h"
 
 namespace {
 
@@ -65,33 +67,13 @@ __device__ __forceinline__ unsigned hash32(const uint8_t* p, int n) {
   return h ^ (h >> 13);
 }
 
-// host parse_num semantics (records.cpp): trim, [+-]digits[.digits][e[+-]digits], NaN otherwise
+// host parse_num semantics (records.cpp, avenir_numparse.h): trim, [+-]digits[.digits][e[+-]digits],
+// correctly rounded on the fast path, NaN otherwise
 __device__ double parse_num(const uint8_t* p, const uint8_t* e) {
   while (p < e && is_ws(*p)) ++p;
   while (e > p && is_ws(e[-1])) --e;
-  const double nan = __longlong_as_double(0x7ff8000000000000LL);
-  if (p == e) return nan;
-  bool neg = false;
-  if (*p == '+' || *p == '-') { neg = *p == '-'; ++p; }
-  double v = 0.0;
-  int digits = 0;
-  while (p < e && *p >= '0' && *p <= '9') { v = v * 10 + (*p - '0'); ++p; ++digits; }
-  if (p < e && *p == '.') {
-    ++p;
-    double scale = 0.1;
-    while (p < e && *p >= '0' && *p <= '9') { v += (*p - '0') * scale; scale *= 0.1; ++p; ++digits; }
-  }
-  if (digits == 0) return nan;
-  if (p < e && (*p == 'e' || *p == 'E')) {
-    ++p;
-    bool eneg = false;
-    if (p < e && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
-    int ex = 0;
-    while (p < e && *p >= '0' && *p <= '9') { ex = ex * 10 + (*p - '0'); ++p; }
-    v *= pow(10.0, eneg ? -ex : ex);
-  }
-  if (p != e) return nan;
-  return neg ? -v : v;
+  bool slow;
+  return avnum::parse_decimal(reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(e), &slow);
 }
 
 __global__ __launch_bounds__(RT) void rec_lines_kernel(const uint8_t* __restrict__ bytes,

@@ -54,8 +54,9 @@ __global__ __launch_bounds__(VT) void viterbi_kernel(const ViterbiArgs a) {
     const int o0 = ob[0];
     delta[q] = (j < S && o0 >= 0 && o0 < O) ? logpi[j] + logB[(long long)j * O + o0] : -INFINITY;
   }
-  int len = (ob[0] >= 0) ? 1 : 0;
-  for (int t = 1; t < T; ++t) {
+  // an invalid first observation ends the sequence before it starts (len 0, as the host oracle)
+  int len = (ob[0] >= 0 && ob[0] < O) ? 1 : 0;
+  for (int t = 1; len > 0 && t < T; ++t) {
     const int ot = ob[t];
     if (ot < 0 || ot >= O) break;  // wave-uniform (all lanes read the same word)
     float nd[QS];
@@ -178,8 +179,8 @@ __global__ __launch_bounds__(VT) void viterbi_small_kernel(const ViterbiArgs a) 
   short* bp = a.bp;
   const int o0 = live ? ob[0] : -1;
   float delta = (js && o0 >= 0 && o0 < O) ? logpi[j] + logB[(long long)j * O + o0] : -INFINITY;
-  int len = (live && o0 >= 0) ? 1 : 0;
-  bool act = live;
+  int len = (live && o0 >= 0 && o0 < O) ? 1 : 0;
+  bool act = len > 0;  // an invalid first observation: an empty sequence
   for (int t = 1; t < T; ++t) {
     const int ot = act ? ob[t] : -1;
     if (ot < 0 || ot >= O) act = false;

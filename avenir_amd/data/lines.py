@@ -1,0 +1,166 @@
+"""Input lines kept as byte spans, not Python strings (VERDICT r3 "lines kept as byte offsets").
+
+Map-side jobs of the reference echo the input record in their output (``record,predClass,prob`` of
+J/bayesian/BayesianPredictor.java:271-285, the ``withRecord`` mode of J/model/ModelPredictor.java,
+the ``$path;record`` lines of the decision-tree level step) or copy fields of it (the id of
+J/markov/ViterbiStatePredictor.java:114-142 and J/markov/MarkovModelClassifier.java:127-150).  A
+Python string per input line costs more than the GPU kernels of those jobs at 10^7+ records, so a
+:class:`LineSpans` holds, per line of a rank's shard, the absolute address and byte length of the
+line inside memory that the native parser already has (the mapped CSV file, a byte shard, or a
+mapping of the file the device parser uploaded) plus the object that owns that memory.  The native
+formatter (``data/records.format_lines`` kinds ``r`` / ``rf`` / ``rt``) copies the bytes straight
+into the output; Python strings are only built when a caller indexes or iterates.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+
+class LineSpans(Sequence):
+    """Byte spans of a shard's lines.  ``owner`` keeps the memory alive; ``addr`` / ``lens`` int64
+    tensors (CPU, or any device: moved to the host on first use)."""
+
+    def __init__(self, owner, addr: torch.Tensor, lens: torch.Tensor, strings: list[str] | None = None):
+        self._owner = owner
+        self._addr = addr
+        self._lens = lens
+        self._strings = strings
+
+    # -- constructors -----------------------------------------------------------------------------
+    @classmethod
+    def from_csv(cls, csv, r0: int, r1: int) -> "LineSpans":
+        """Rows [r0, r1) of a native ``CsvFile``."""
+        addr, lens = csv.line_spans(int(r0), int(r1))
+        return cls(csv, addr, lens)
+
+    @classmethod
+    def from_shard(cls, shard) -> "LineSpans":
+        """Every line of a native ``TextShard`` (records.py host tokenizer)."""
+        addr, lens = shard.line_spans()
+        return cls(shard, addr, lens)
+
+    @classmethod
+    def from_file(cls, path: str, starts: torch.Tensor, ends: torch.Tensor) -> "LineSpans":
+        """Lines at byte offsets [starts, ends) of ``path`` (e.g. the device CSV parser's row
+        bounds, still on the GPU): the file is mapped read-only on the host, the offsets become
+        addresses when a formatter first needs them."""
+        return _FileSpans(path, starts, ends)
+
+    @classmethod
+    def from_strings(cls, lines: list[str]) -> "LineSpans":
+        """Python strings (pure-Python fallback paths): encoded once into one buffer."""
+        enc = [ln.encode() for ln in lines]
+        buf = ctypes.create_string_buffer(b"".join(enc) or b"\0")
+        lens = torch.tensor([len(e) for e in enc], dtype=torch.int64)
+        base = ctypes.addressof(buf)
+        addr = base + torch.cumsum(lens, 0) - lens
+        return cls(buf, addr, lens, list(lines))
+
+    @classmethod
+    def from_packed(cls, buf: torch.Tensor, off: torch.Tensor) -> "LineSpans":
+        """Lines packed by :meth:`pack` (e.g. received from another rank): ``buf`` uint8, ``off``
+        int64 [n + 1]."""
+        buf, off = buf.cpu().contiguous(), off.cpu().long()
+        base = buf.data_ptr() if buf.numel() else 0
+        return cls(buf, base + off[:-1], off[1:] - off[:-1])
+
+    def pack(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """The lines copied into one buffer: (uint8 [bytes], int64 offsets [n + 1]) — a payload
+        that can travel through collectives (native multi-threaded copy)."""
+        from .. import _native
+        owner, a, n = self.spans()
+        C = _native.host()
+        if C is not None and hasattr(C, "pack_spans"):
+            return C.pack_spans(a, n)
+        enc = [ctypes.string_at(x, m) for x, m in zip(a.tolist(), n.tolist())]
+        off = torch.zeros(len(enc) + 1, dtype=torch.int64)
+        if enc:
+            off[1:] = torch.cumsum(torch.tensor([len(e) for e in enc], dtype=torch.int64), 0)
+        return torch.frombuffer(bytearray(b"".join(enc) or b"\0"), dtype=torch.uint8)[: int(off[-1])].clone(), off
+
+    # -- spans --------------------------------------------------------------------------------------
+    def spans(self) -> tuple[object, torch.Tensor, torch.Tensor]:
+        """(owner, addr int64 CPU, len int64 CPU)."""
+        if self._addr.device.type != "cpu":
+            self._addr, self._lens = self._addr.cpu(), self._lens.cpu()
+        return self._owner, self._addr, self._lens
+
+    def column(self, kind: str = "r", field: int | None = None, delims: str = "") -> tuple:
+        """A ``format_lines`` column: the whole line (``r``; ``delims`` re-joined with the output
+        delimiter), field ``field`` (``rf``), or the fields from ``field`` on (``rt``)."""
+        owner, a, n = self.spans()
+        if kind == "r":
+            return ("r", owner, a, n, delims)
+        return (kind, owner, a, n, int(field), delims)
+
+    def __len__(self) -> int:
+        return int(self._lens.numel())
+
+    def _str(self, i: int) -> str:
+        _, a, n = self.spans()
+        return ctypes.string_at(int(a[i]), int(n[i])).decode()
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            owner, a, n = self._owner, self._addr, self._lens
+            return LineSpans(owner, a[i], n[i], self._strings[i] if self._strings is not None else None)
+        if isinstance(i, torch.Tensor):
+            return self.select(i)
+        if self._strings is not None:
+            return self._strings[i]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        return self._str(i)
+
+    def select(self, idx: torch.Tensor) -> "LineSpans":
+        """The lines at ``idx`` (int64 indexes or a bool mask), in that order."""
+        owner, a, n = self.spans()
+        idx = idx.cpu()
+        strings = None
+        if self._strings is not None:
+            il = torch.nonzero(idx).view(-1).tolist() if idx.dtype == torch.bool else idx.tolist()
+            strings = [self._strings[j] for j in il]
+        return LineSpans(owner, a[idx], n[idx], strings)
+
+    def tolist(self) -> list[str]:
+        if self._strings is None:
+            _, a, n = self.spans()
+            self._strings = [ctypes.string_at(x, m).decode() for x, m in zip(a.tolist(), n.tolist())]
+        return self._strings
+
+    def __iter__(self):
+        return iter(self.tolist())
+
+    def __eq__(self, other):
+        return self.tolist() == list(other)
+
+
+class _FileSpans(LineSpans):
+    """LineSpans over a read-only mapping of a file, created on first use."""
+
+    def __init__(self, path: str, starts: torch.Tensor, ends: torch.Tensor):
+        super().__init__(None, starts, ends - starts)
+        self._path = path
+        self._mapped = False
+
+    def spans(self):
+        if not self._mapped:
+            import numpy as np
+            mm = np.memmap(self._path, dtype=np.uint8, mode="r") if self._lens.numel() else np.zeros(1, np.uint8)
+            base = int(mm.ctypes.data)
+            self._owner = mm
+            self._addr = self._addr.cpu() + base
+            self._lens = self._lens.cpu()
+            self._mapped = True
+        return super().spans()
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            owner, a, n = self.spans()
+            return LineSpans(owner, a[i], n[i])
+        return super().__getitem__(i)

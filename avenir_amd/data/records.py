@@ -77,6 +77,9 @@ class Records:
     #: the dictionary's bytes on the device (device tokenizer, single shard): vbytes uint8, voff /
     #: vlen int64 per entry — string-order sorts of keys then run on the device
     vbytes: tuple | None = None
+    #: (paths, rank, world, skip_header) of the shard, to re-index its raw lines on demand
+    _src: tuple | None = None
+    _spans: object = None
 
     @property
     def n_lines(self) -> int:
@@ -179,15 +182,34 @@ class Records:
         return [v[c] if c >= 0 else "" for c in cs]
 
     def lines(self) -> list[str]:
-        """The raw text of this rank's lines (host shard only; re-read for device tables)."""
-        if self._shard is None:
-            raise RuntimeError("raw lines are only kept by host-tokenized tables")
-        return self._shard.lines(0, self.n_lines)
+        """The raw text of this rank's lines as Python strings (prefer :meth:`line_spans`)."""
+        return self.line_spans().tolist()
+
+    def line_spans(self):
+        """This rank's raw lines as byte spans (data/lines.LineSpans) for the native formatter:
+        the host tokenizer's shard, or — for a device-tokenized table — a host line index of the
+        same byte range built on first use (one multi-threaded newline scan, no tokenizing)."""
+        from .lines import LineSpans
+        if self._spans is None:
+            if self._shard is None and self._src is not None:
+                paths, rank, world, skip = self._src
+                C = _native.host()
+                if C is not None:
+                    self._shard = C.TextShard(paths, rank, world, _threads(), skip)
+                else:
+                    self._spans = LineSpans.from_strings(_py_lines(paths, rank, world, skip))
+            if self._spans is None:
+                if self._shard is None:
+                    raise RuntimeError("raw lines are not available for this table")
+                self._spans = LineSpans.from_shard(self._shard)
+            if len(self._spans) != self.n_lines:
+                raise RuntimeError("line index does not match the token table")
+        return self._spans
 
     def to(self, device) -> "Records":
         mv = lambda t: None if t is None else t.to(device)
         return Records(mv(self.off), mv(self.codes), mv(self.sub), mv(self.nums), self.vocab, self.line_base,
-                       self.stats, self._shard)
+                       self.stats, self._shard, _src=self._src, _spans=self._spans)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -225,6 +247,7 @@ def read_records(path, *, comm=None, delims: str = ",", sub_delim: str = "", mod
         rec = _read_records_py(paths, rank, world, delims, sub_delim, modes, tail_mode, trim, numeric, skip_header,
                                last_mode)
         rec = rec.to(dev) if dev.type != "cpu" else rec
+    rec._src = (paths, rank, world, skip_header)
     if dist:
         _merge_vocab(rec, comm)
     return rec
@@ -326,8 +349,10 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
     """Output text of ``n`` rows assembled column by column (native, multi-threaded):
     ``("s", table, idx)`` string-table lookups, ``("f", values, prec)`` numbers (prec < 0: ``%g``),
     ``("i", ints)``, ``("c", literal)``, ``("g", literal)`` glued on without a delimiter,
-    ``("l", table, idx, off)`` a variable-length list of table strings per row (CSR).  Every row
-    ends with a newline."""
+    ``("l", table, idx, off)`` a variable-length list of table strings per row (CSR), and the raw
+    input line kinds of ``data/lines.LineSpans.column``: ``("r", ...)`` the line, ``("rf", ...)``
+    one of its fields, ``("rt", ...)`` its fields from one on.  ``prec`` -2 writes Python's
+    ``repr`` of the value.  Every row ends with a newline."""
     C = _native.host()
     if C is not None:
         return C.format_columns(cols, int(n), delim, _threads())
@@ -350,7 +375,8 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
             vals, prec = c[1].tolist(), (c[2] if len(c) > 2 else 6)
             for r in range(n):
                 v = vals[r]
-                rows[r].append("NaN" if v != v else (f"{v:.{prec}f}" if prec >= 0 else f"{v:g}"))
+                rows[r].append(repr(v) if prec == -2 else
+                               ("NaN" if v != v else (f"{v:.{prec}f}" if prec >= 0 else f"{v:g}")))
         elif k == "i":
             vals = c[1].tolist()
             for r in range(n):
@@ -362,6 +388,24 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
             tab, idx, off = c[1], c[2].tolist(), c[3].tolist()
             for r in range(n):
                 rows[r] += [tab[i] if 0 <= i < len(tab) else "" for i in idx[off[r]:off[r + 1]]]
+        elif k in ("r", "rf", "rt"):
+            import ctypes
+            import re
+            a, ln = c[2].tolist(), c[3].tolist()
+            fld = c[4] if k != "r" else 0
+            dl = c[5] if k != "r" else (c[4] if len(c) > 4 else "")
+            sp = re.compile("[" + re.escape(dl) + "]") if dl else None
+            for r in range(n):
+                txt = ctypes.string_at(a[r], ln[r]).decode()
+                if k == "r":
+                    rows[r].append(sp.sub(delim, txt) if sp else txt)
+                    continue
+                parts = sp.split(txt) if sp else [txt]
+                if k == "rf":
+                    ok = -len(parts) <= fld < len(parts)
+                    rows[r].append(parts[fld] if ok else "")
+                else:
+                    rows[r].append(delim.join(parts[fld:]) if fld < len(parts) else "")
         else:
             raise ValueError(f"unknown column kind {k!r}")
     out = []

@@ -100,6 +100,19 @@ def tagged_sequences(path, n: int, seq_len: int = 8, obs=("a", "b", "c", "d"), s
     return _write(path, cols)
 
 
+def observation_sequences(path, n: int, seq_len: int = 8, obs=("a", "b", "c", "d"), states=("S", "T", "U"),
+                          seed: int = 0) -> int:
+    """``id,o1,...,oL``: the observations of ``tagged_sequences`` without their state tags
+    (viterbiStatePredictor input)."""
+    rng = np.random.default_rng(seed)
+    cols = [_id("s", np.arange(n), 9)]
+    st = rng.integers(0, len(states), n)
+    for _ in range(seq_len):
+        cols.append(_pick(list(obs), (st + rng.integers(0, 2, n)) % len(obs)))
+        st = np.where(rng.random(n) < 0.3, rng.integers(0, len(states), n), st)
+    return _write(path, cols)
+
+
 def match_pairs(path, n_pairs: int, n_entities: int, classes=("A", "B"), seed: int = 0) -> int:
     """``src,trg,srcId,srcClass,trgId,trgClass,rank`` (record = id, class; tmc.class.attr.ord=1)."""
     rng = np.random.default_rng(seed)
@@ -135,7 +148,7 @@ def events(path, n: int, n_keys: int = 100000, states=("A", "B", "C", "D"), seed
     return _write(path, [_id("k", key, len(str(n_keys - 1))), _digits(t, 13), _pick(list(states), st)])
 
 
-FORMATS = {"mst": state_sequences, "apriori": transactions, "hmm": tagged_sequences, "tmc": match_pairs,
+FORMATS = {"obs": observation_sequences, "mst": state_sequences, "apriori": transactions, "hmm": tagged_sequences, "tmc": match_pairs,
            "nen": knn_pairs, "str": events}
 
 

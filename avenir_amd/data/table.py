@@ -195,7 +195,7 @@ class Table:
         il = idx.cpu().tolist()
         return Table(self.schema, m, codes, self.binned_fields, num, self.numeric_fields, lab,
                      self.class_field, [self.ids[i] for i in il] if self.ids else None,
-                     [self.lines[i] for i in il] if self.lines else None, 0, dict(self.meta))
+                     _select_lines(self.lines, idx, il), 0, dict(self.meta))
 
     def label_values(self) -> list[str]:
         if self.class_field is None or self.labels is None:
@@ -224,6 +224,15 @@ class Table:
         if not cols:
             return torch.zeros((self.n, 0), device=self.device)
         return torch.cat(cols, dim=1)
+
+
+def _select_lines(lines, idx: torch.Tensor, il: list[int]):
+    if not lines:
+        return None
+    from .lines import LineSpans
+    if isinstance(lines, LineSpans):
+        return lines.select(idx)
+    return [lines[i] for i in il]
 
 
 # ------------------------------------------------------------------------------------------------
@@ -321,11 +330,12 @@ def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *
     if nthreads is None:    # parse threads: the machine's cores, capped at a GPU box's CPU share
         nthreads = max(1, min(16, os.cpu_count() or 8))
     dev = torch.device(device)
-    if (use_native and not multi and dev.type == "cuda" and not keep_lines and len(_literal(delim or ",")) == 1
+    if (use_native and not multi and dev.type == "cuda" and len(_literal(delim or ",")) == 1
             and hasattr(C, "csv_parse_device") and os.path.getsize(path) >= _GPU_CSV_MIN_BYTES
             and all(f.cardinality or not f.is_categorical for f in feats)
             and (cls_f is None or cls_f.cardinality)):
-        t = _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads)
+        t = _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads,
+                             keep_lines)
         if t is not None:
             return t
     if use_native:
@@ -373,8 +383,9 @@ def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *
         lines = None
         if idf is not None:
             ids = LazyColumn(csv, idf.ordinal, r0, r1)
-        if keep_lines:
-            lines = csv.lines(r0, r1)
+        if keep_lines:   # byte spans into the mapped file, strings only on demand (data/lines.py)
+            from .lines import LineSpans
+            lines = LineSpans.from_csv(csv, r0, r1)
     else:  # pure-Python path: regex delimiters, or no native module
         all_lines = _py_lines_of(path, skip_header)
         r0, r1 = shard_range(len(all_lines), rank, world)
@@ -408,18 +419,24 @@ def load_csv(path: str | Path | list, schema: FeatureSchema, delim: str = ",", *
                                       dtype=torch.uint8)
         idf = schema.id_field
         ids = [r[idf.ordinal] for r in rows] if idf is not None else None
-        lines = all_lines[r0:r1] if keep_lines else None
-    t = Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, lines, r0)
+        lines = None
+        if keep_lines:
+            from .lines import LineSpans
+            lines = LineSpans.from_strings(all_lines[r0:r1])
+    t = Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, lines, r0,
+              meta={"parser": "host" if csv is not None else "python"})
     return t.to(device) if str(device) != "cpu" else t
 
 
 _GPU_CSV_MIN_BYTES = int(os.environ.get("AVMI_GPU_CSV_MIN_BYTES", str(32 << 20)))
 
 
-def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads):
+def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feats, cls_f, nthreads,
+                     keep_lines: bool = False):
     """K1 on the GPU (csrc/kernels/csv.hip): upload the file, index lines and parse the schema's
-    columns on the device; same codes as the host parser.  None when a column kind needs the host
-    path (raw int64 columns)."""
+    columns on the device (in passes of up to 64 columns); same codes as the host parser.  None when
+    a column kind needs the host path (int32 codes).  ``keep_lines``: the rows' byte spans in the
+    file (from the device line index) as a lazy data/lines.LineSpans."""
     binned = [f for f in feats if f.is_binned]
     numeric = [f for f in feats if not f.is_binned and f.is_numeric]
     width = code_width(binned)
@@ -432,8 +449,8 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     if any(sp[1] not in (CAT, BUCKET, FLOAT) for sp in specs):
         return None
     like = torch.empty(0, device=dev)
-    cols, n, _bad, _total, r0 = C.csv_parse_device(str(path), specs, _literal(delim or ","), skip_header,
-                                                   int(rank), int(world), like)
+    cols, n, _bad, _total, r0, starts, ends = C.csv_parse_device(str(path), specs, _literal(delim or ","),
+                                                                 skip_header, int(rank), int(world), like)
     ld = pad16(n)
     cdt = torch.uint16 if wide else torch.uint8
     codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned
@@ -447,7 +464,11 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     if idf is not None:
         lit = _literal(delim or ",")
         ids = LazyColumn(lambda: C.CsvFile(str(path), lit, skip_header, nthreads), idf.ordinal, r0, r0 + n)
-    return Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, None, r0)
+    lines = None
+    if keep_lines:
+        from .lines import LineSpans
+        lines = LineSpans.from_file(str(path), starts, ends)
+    return Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, lines, r0, meta={"parser": "device"})
 
 
 def _py_lines_of(path, skip_header: bool) -> list[str]:

@@ -52,32 +52,43 @@ def nb_predict(args):
         d = ctx.delim_out
         ctx.emit([f"{d.join(r)}{d}{m.classes[p]}{d}{int(round(100 * q))}" for r, p, q in zip(rows, pred, prob)])
         return
+    from ..data.records import format_lines
     t = ctx.table()
     nb = NaiveBayes.load_model(ctx.path("bayesian.model.file.path", "model"), t.schema)
     vals = t.class_field.cardinality if t.class_field else None
     d = ctx.delim_out
+    lit = _single_delim(ctx)
     if ctx.get_bool("output.feature.prob.only", False):
+        # id,featurePriorProb,cls0,p0,cls1,p1,...,actualClass: columns straight from the device
+        # results and the raw line bytes (the id field), one native formatting pass
         fp, post = nb.feature_probs(t)
-        ids = t.ids if t.ids is not None else [ln.split(",")[0] for ln in t.lines]
-        lab = t.labels[: t.n].long().cpu().tolist() if t.labels is not None else [0] * t.n
-        fp, post = fp.cpu().tolist(), post.cpu().tolist()
-        lines = []
-        for i in range(t.n):
-            parts = [ids[i], f"{fp[i]:.6g}"]
-            for c, v in enumerate(nb.class_values):
-                parts += [v, f"{post[i][c]:.6g}"]
-            parts.append(vals[lab[i]] if vals and lab[i] < len(vals) else "")
-            lines.append(d.join(parts))
-        ctx.emit(lines)
+        idf = t.schema.id_field
+        cols = [t.lines.column("rf", idf.ordinal if idf is not None else 0, lit if idf is not None else ",")]
+        cols.append(("f", fp.double().cpu(), -1))
+        pc = post.double().cpu()
+        for c, v in enumerate(nb.class_values):
+            cols += [("c", v), ("f", pc[:, c].contiguous(), -1)]
+        lab = t.labels[: t.n].int().cpu() if t.labels is not None else torch.full((t.n,), -1, dtype=torch.int32)
+        cols.append(("s", list(vals or []), lab))
+        ctx.emit_text(format_lines(cols, t.n, d))
         return
     r = nb.predict(t)
-    pred = r.pred.cpu().tolist()
-    prob = r.prob.max(1).values.cpu().tolist() if r.prob is not None else [1.0] * len(pred)
-    ctx.emit([f"{t.lines[i]}{d}{vals[p] if vals else p}{d}{prob[i]:.3f}" for i, p in enumerate(pred)])
+    prob = r.prob.max(1).values if r.prob is not None else torch.ones(t.n, device=r.pred.device)
+    pred = r.pred.int().cpu()
+    cols = [t.lines.column("r"), ("s", list(vals), pred) if vals else ("i", pred.long()),
+            ("f", prob.double().cpu(), 3)]
+    ctx.emit_text(format_lines(cols, t.n, d))
     if r.confusion is not None:
         conf = r.confusion.clone()
         ctx.all_reduce(conf)
         ctx.report({"confusion": conf.cpu().tolist()})
+
+
+def _single_delim(ctx) -> str:
+    """The one-character literal input delimiter (raw-line field extraction), else ','."""
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    return lit if lit is not None and len(lit) == 1 else ","
 
 
 @job("decisionTree", "decision tree (J/tree/DecisionTreeBuilder.java, dtb.* keys) -> decision path JSON")
@@ -113,12 +124,15 @@ def dec_tree(args):
         Path(out_path).parent.mkdir(parents=True, exist_ok=True)
         Path(out_path).write_text(json.dumps(js, indent=1))
     grown = max((len(dp["predicates"]) - 1 for dp in js["decisionPaths"]), default=0)
-    rows = [ln.split(ctx.delim_in) if len(ctx.delim_in) == 1 else ctx.split(ln) for ln in t.lines]
-    _, first = DecisionPathModel(js).predict_proba_rows(rows)
+    # every record prefixed by the predicates of the path it takes: the paths are evaluated
+    # column-wise on the table's device, the lines formatted natively from their byte spans
+    from ..data.records import format_lines
+    from ..models.tree import TableColumns
+    _, first = DecisionPathModel(js).predict_proba_cols(TableColumns(t))
     pd = ctx.get_str("dec.path.delim", ";")
-    d = ctx.delim_out
-    paths = [pd.join(pr["predicateStr"] for pr in dp["predicates"]) for dp in js["decisionPaths"]]
-    ctx.emit([f"{paths[int(j)] if int(j) >= 0 else '$root'}{d}{ln}" for ln, j in zip(t.lines, first.tolist())])
+    paths = [pd.join(pr["predicateStr"] for pr in dp["predicates"]) for dp in js["decisionPaths"]] + ["$root"]
+    first = torch.where(first >= 0, first, torch.full_like(first, len(paths) - 1)).int().cpu()
+    ctx.emit_text(format_lines([("s", paths, first), t.lines.column("r")], t.n, ctx.delim_out))
     ctx.report({"level": grown, "done": grown <= depth or grown >= limit})
 
 
@@ -155,9 +169,9 @@ def knn(args):
     nn = NearestNeighbor.from_config(ctx.cfg).fit((Xtr - lo) / scale, tr.labels[: tr.n].long(), tr.n_classes,
                                                   index_base=tr.row_offset)
     res = nn.predict((Xte - lo) / scale, q_base=te.row_offset)
+    from ..data.records import format_lines
     vals = te.class_field.cardinality
-    d = ctx.delim_out
-    ctx.emit([f"{te.lines[i]}{d}{vals[p]}" for i, p in enumerate(res.pred.cpu().tolist())])
+    ctx.emit_text(format_lines([te.lines.column("r"), ("s", list(vals), res.pred.int().cpu())], te.n, ctx.delim_out))
 
 
 @job("logisticRegression", "logistic regression (J/regress/LogisticRegressionJob.java): CSV -> coefficient lines per iteration")
@@ -510,12 +524,38 @@ def viterbi(args):
     state_only = ctx.get_bool("output.state.only", True)
     sub = ctx.get_str("sub.field.delim", ":")
     hmm = HiddenMarkovModel.from_lines(ctx.all_lines(ctx.path("hmm.model.path", "model")), ",")
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _viterbi_rows(ctx, hmm, skip, id_ord, state_only, sub)
+    from ..data.records import format_lines
+    # native path: this rank's byte range tokenized once (observation tokens by dictionary), the
+    # padded [N, L] observation matrix built on the device, the K-Viterbi kernel, and the output
+    # formatted from the decoded state ids and the raw id field — no per-token Python
+    rec = ctx.records(modes="x" * skip)
+    obs, _ = rec.padded(rec.map_codes(rec.codes, hmm.observations), start=skip, min_len=1)
+    path, _ = ViterbiDecoder(hmm).decode(obs.to(ctx.device))
+    ok = path >= 0
+    cnt = ok.sum(1).long()
+    off = torch.cat([cnt.new_zeros(1), torch.cumsum(cnt, 0)]).cpu()
+    S = len(hmm.states)
+    if state_only:
+        table, idx = hmm.states, path[ok]
+    else:   # obs<sub>state tokens: one table entry per (observation, state) pair
+        table = [f"{o}{sub}{st}" for o in hmm.observations for st in hmm.states]
+        idx = obs.to(path.device).long()[ok] * S + path[ok]
+    cols = [rec.line_spans().column("rf", id_ord, lit), ("l", table, idx.int().cpu(), off)]
+    ctx.emit_text(format_lines(cols, rec.n_lines, ctx.delim_out))
+
+
+def _viterbi_rows(ctx, hmm, skip, id_ord, state_only, sub):
+    """Regex delimiters: the split-row path."""
+    from ..models.markov import ViterbiDecoder
     rows = ctx.rows()
     oi = {o: i for i, o in enumerate(hmm.observations)}
-    obs = torch.full((len(rows), max([len(r) - skip for r in rows] + [1])), -1, dtype=torch.int16)
-    for r, row in enumerate(rows):
-        for j, tok in enumerate(row[skip:]):
-            obs[r, j] = oi.get(tok, -1)
+    L = max([len(r) - skip for r in rows] + [1])
+    obs = torch.tensor([[oi.get(t, -1) for t in r[skip:]] + [-1] * (L - len(r[skip:])) for r in rows],
+                       dtype=torch.int16).view(len(rows), L)
     paths = ViterbiDecoder(hmm).decode_labels(obs.to(ctx.device))
     d = ctx.delim_out
     out = []

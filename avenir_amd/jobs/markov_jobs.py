@@ -83,13 +83,36 @@ def mmc(args):
     cls_ord = ctx.get_int("class.label.field.ord", -1)
     thr = ctx.get_float("log.odds.threshold", 0.0)
     clf = MarkovModelClassifier(mats[labels[0]], mats[labels[1]], labels, thr)
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _mmc_rows(ctx, clf, states, labels, skip, id_ord, val, cls_ord, thr)
+    from ..data.records import format_lines
+    # native path: state tokens by dictionary lookup, the padded [N, L] state matrix on the device
+    # (class field dropped when it sits among the states), the K15 gather-sum kernel, and the
+    # output from the raw id / class fields and the device results
+    rec = ctx.records(modes="x" * skip)
+    keep = rec.lens() >= skip + 2
+    X, _ = rec.padded(rec.map_codes(rec.codes, states), start=skip, drop=(cls_ord,) if cls_ord >= skip else (),
+                      min_len=1)
+    X = X[keep]
+    lo = clf.log_odds(X.to(ctx.device)).double()
+    pred = (lo <= thr).int().cpu()       # 0 -> labels[0] (log-odds above the threshold)
+    spans = rec.line_spans().select(keep.cpu())
+    cols = [spans.column("rf", id_ord, lit)]
+    if val:
+        cols.append(spans.column("rf", cls_ord, lit))
+    cols += [("s", list(labels[:2]), pred), ("f", lo.cpu(), -2)]
+    ctx.emit_text(format_lines(cols, int(keep.sum()), ctx.delim_out))
+
+
+def _mmc_rows(ctx, clf, states, labels, skip, id_ord, val, cls_ord, thr):
+    """Regex delimiters: the split-row path."""
     rows = [r for r in ctx.rows() if len(r) >= skip + 2]
     si = {s: i for i, s in enumerate(states)}
-    L = max([len(r) - skip for r in rows] + [1])
-    X = torch.full((len(rows), L), -1, dtype=torch.int16)
-    for i, r in enumerate(rows):
-        toks = [v for j, v in enumerate(r[skip:], skip) if j != cls_ord] if cls_ord >= skip else r[skip:]
-        X[i, : len(toks)] = torch.tensor([si.get(v, -1) for v in toks], dtype=torch.int16)
+    toks = [[v for j, v in enumerate(r[skip:], skip) if j != cls_ord] if cls_ord >= skip else r[skip:] for r in rows]
+    L = max([len(t) for t in toks] + [1])
+    X = torch.tensor([[si.get(v, -1) for v in t] + [-1] * (L - len(t)) for t in toks], dtype=torch.int16).view(-1, L)
     lo = clf.log_odds(X.to(ctx.device)).double().cpu()
     d = ctx.delim_out
     out = []
@@ -105,27 +128,206 @@ def mmc(args):
 # ================================================================================================
 @job("probabilisticSuffixTreeGenerator", "counts of all sub-sequences of length 2..L per partition/class (J/markov/ProbabilisticSuffixTreeGenerator.java, pstg.*)")
 def pstg(args):
-    """Each row's tokens (after ``pstg.skip.field.count``) are mapped to a shared vocabulary; every
-    window of width 2..``pstg.max.seq.length`` is one row of an int64 key tensor (prefix id x
-    token digits), counted by a device sort + unique; counts are merged across ranks; one line per
-    distinct n-gram ``ids..,[class],tok..,count`` plus the ``$`` root count per prefix (:140-305).
-    ``pstg.input.format.sequential=false`` reads one token per record (field ``pstg.data.field.ordinal``)
-    with a sliding window per id."""
+    """Counts of every window of width 2..``pstg.max.seq.length`` of the token fields, per prefix
+    (``pstg.id.field.ordinals`` fields + the ``pstg.class.label.field.ord`` label), plus the
+    ``<root symbol>`` count per prefix (the number of windows), one line each:
+    ``ids..,[class],tok..,count`` in key order (:140-305).  As in the reference the class field adds
+    one to ``pstg.skip.field.count`` (:118-122).  ``pstg.input.format.sequential=false`` reads one
+    token per record (``pstg.data.field.ordinal``) and slides a window of the last L tokens per
+    prefix over the records in input order.
+
+    Native path (one-character delimiter): the rank's byte range is tokenized once; the K5 hash
+    count kernel (``ops/sequence_ops.ngram_counts``, LDS-privatised open addressing) counts all
+    widths of all rows in one pass with the prefix as the group id; the decoded (prefix, n-gram,
+    count) rows of all ranks are merged on rank 0, ordered by string ranks and formatted natively."""
+    from ..data.table import _literal
     ctx = JobContext(args, "pstg.")
     skip = ctx.get_int("skip.field.count", 0)
     cls_ord = ctx.get_int("class.label.field.ord", -1)
+    if cls_ord >= 0:
+        skip += 1
     L = ctx.get_int("max.seq.length", 5)
     root = ctx.get_str("tree.root.symbol", "$")
     id_ords = ctx.get_int_list("id.field.ordinals", [])
+    pref_ords = list(id_ords) + ([cls_ord] if cls_ord >= 0 else [])
+    sequential = ctx.get_bool("input.format.sequential", True)
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _pstg_rows(ctx, skip, cls_ord, L, root, id_ords, sequential)
+    if sequential:
+        rec = ctx.records(modes="".join("d" if i in pref_ords else "x" for i in range(skip)))
+        keep = rec.lens() >= skip + 2
+        T, _ = rec.padded(start=skip, dtype=torch.int32)
+        T = T[keep]
+        P = (torch.stack([rec.field(o) for o in pref_ords], 1)[keep] if pref_ords
+             else torch.zeros((T.shape[0], 0), dtype=torch.int32, device=T.device))
+    else:
+        dfo = ctx.get_int("data.field.ordinal")
+        top = max(pref_ords + [dfo]) + 1
+        rec = ctx.records(modes="".join("d" if (i in pref_ords or i == dfo) else "x" for i in range(top)),
+                          tail_mode="x")
+        T, P = _stream_windows(ctx, rec, pref_ords, dfo, L)
+    rows = _ngram_rows(T, P, L, streaming=not sequential)
+    _emit_pst(ctx, rec, rows, len(pref_ords), L, root)
+
+
+def _stream_windows(ctx, rec, pref_ords, dfo, L):
+    """Non-sequential input: every record adds its token to the window of its prefix; each full
+    window (the last L tokens) is one row of ``T`` [W, L] whose prefixes of width 2..L are
+    counted.  Records are shuffled to the rank owning their prefix (all-to-all, input order kept:
+    rows arrive in source-rank order, each source's rows in file order), then grouped by a stable
+    sort on the device."""
+    from ..data.records import segment_rank, shuffle
+    dev = rec.device
+    tok = rec.field(dfo).long()
+    P = (torch.stack([rec.field(o) for o in pref_ords], 1).long() if pref_ords
+         else torch.zeros((rec.n_lines, 0), dtype=torch.long, device=dev))
+    ok = (tok >= 0) & ((P >= 0).all(1) if pref_ords else torch.ones_like(tok, dtype=torch.bool))
+    tok, P = tok[ok], P[ok]
+    comm = ctx.comm
+    if comm.is_distributed:
+        h = torch.zeros_like(tok)
+        for j in range(P.shape[1]):
+            h = (h * 1000003 + P[:, j]) % (1 << 40)
+        cols = shuffle(comm, h % comm.world, [tok] + [P[:, j] for j in range(P.shape[1])])
+        tok = cols[0]
+        P = torch.stack(cols[1:], 1) if P.shape[1] else torch.zeros((tok.numel(), 0), dtype=torch.long, device=dev)
+    if tok.numel() == 0:
+        return torch.zeros((0, L), dtype=torch.int32, device=dev), P[:0]
+    if P.shape[1]:
+        _, g = torch.unique(P, dim=0, return_inverse=True)
+    else:
+        g = torch.zeros_like(tok)
+    order = torch.argsort(g, stable=True)
+    gs, ts = g[order], tok[order]
+    first = torch.ones_like(gs, dtype=torch.bool)
+    first[1:] = gs[1:] != gs[:-1]
+    pos = segment_rank(first)
+    n_g = torch.bincount(gs)
+    # a window is complete at every record with pos >= L - 1; it starts at that record - (L - 1)
+    end = torch.nonzero(pos >= L - 1).view(-1)
+    start = end - (L - 1)
+    T = ts[start.view(-1, 1) + torch.arange(L, device=dev).view(1, -1)].int()
+    Pw = P[order][start].int()
+    del n_g
+    return T, Pw
+
+
+def _ngram_rows(T: torch.Tensor, P: torch.Tensor, L: int, streaming: bool) -> torch.Tensor:
+    """int64 [U, k + L + 2] rows ``prefix codes.., token codes.. (-1 padded), is_root, count`` of
+    this rank: the windows of width 2..L of every row of ``T`` (dictionary codes, -1 padding;
+    with ``streaming`` only the windows starting at column 0) counted per prefix row of ``P``."""
+    from ..ops import sequence_ops as SO
+    dev = T.device
+    k = P.shape[1]
+    N = T.shape[0]
+    empty = torch.zeros((0, k + L + 2), dtype=torch.long, device=dev)
+    if N == 0:
+        return empty
+    valid = T >= 0
+    uv = torch.unique(T[valid])                          # the token codes in use -> dense 0..S-1
+    S = uv.numel()
+    dense = torch.where(valid, torch.searchsorted(uv, T.clamp_min(0)), torch.full_like(T, -1)).int()
+    if k:
+        gk, ginv = torch.unique(P.long(), dim=0, return_inverse=True)
+    else:
+        gk, ginv = torch.zeros((1, 0), dtype=torch.long, device=dev), torch.zeros(N, dtype=torch.long, device=dev)
+    base = S + 1
+    out = []
+    if streaming:
+        counts = {}
+        for w in range(2, min(L, T.shape[1]) + 1):
+            win = dense[:, :w].long()
+            okw = (win >= 0).all(1)
+            key = ginv.clone()
+            for j in range(w):
+                key = key * base + win[:, j].clamp_min(0)
+            keys, cnt = torch.unique(key[okw], return_counts=True)
+            counts[w] = (keys % (base ** w), keys // (base ** w), cnt)
+    else:
+        gmul = base ** L
+        if gmul * max(1, gk.shape[0]) >= (1 << 58):
+            raise SystemExit("probabilisticSuffixTreeGenerator: (tokens + 1)^max.seq.length x prefixes exceeds the "
+                             "2^58 n-gram key space")
+        res = SO.ngram_counts(dense, S, 2, L, group=ginv if k else None)
+        counts = {w: (kk % gmul, kk // gmul, cc) for w, (kk, cc) in res.items()}
+    for w, (packed, grp, cnt) in counts.items():
+        toks = torch.full((packed.numel(), L), -1, dtype=torch.long, device=dev)
+        rem = packed.clone()
+        for j in range(w - 1, -1, -1):
+            toks[:, j] = uv[(rem % base)]
+            rem = rem // base
+        out.append(torch.cat([gk[grp], toks, torch.zeros_like(cnt).view(-1, 1), cnt.long().view(-1, 1)], 1))
+    if not out:
+        return empty
+    rows = torch.cat(out, 0)
+    # the root line of every prefix: the number of its windows
+    g_all = torch.cat([grp for _, grp, _ in counts.values()])
+    c_all = torch.cat([cnt.long() for _, _, cnt in counts.values()])
+    rc = torch.zeros(gk.shape[0], dtype=torch.long, device=dev).index_add_(0, g_all, c_all)
+    live = rc > 0
+    rroot = torch.cat([gk[live], torch.full((int(live.sum()), L), -1, dtype=torch.long, device=dev),
+                       torch.ones((int(live.sum()), 1), dtype=torch.long, device=dev), rc[live].view(-1, 1)], 1)
+    return torch.cat([rows, rroot], 0)
+
+
+def _emit_pst(ctx, rec, rows: torch.Tensor, k: int, L: int, root: str) -> None:
+    """Merge every rank's (prefix, n-gram, count) rows on rank 0 (sum per distinct key), order them
+    as the reference's sorted Tuple keys (string order field by field, a shorter key first, the
+    root symbol compared as a string) and write them with the native formatter."""
+    import bisect
+
+    import numpy as np
+    from ..data.records import format_lines, sorted_keys
+    comm = ctx.comm
+    if comm.is_distributed:
+        dev = comm.device if comm.backend == "nccl" else torch.device("cpu")
+        rows = comm.all_gather_v(rows.to(dev))
+    if not ctx.is_root:
+        return
+    rows = rows.cpu()
+    if rows.numel() == 0:
+        ctx.emit_root_text(b"")
+        return
+    key, inv = torch.unique(rows[:, :-1], dim=0, return_inverse=True)
+    cnt = torch.zeros(key.shape[0], dtype=torch.long).index_add_(0, inv, rows[:, -1])
+    codes = key[:, : k + L]
+    is_root = key[:, k + L].bool()
+    used = torch.unique(codes[codes >= 0])
+    keys_sorted, pos = sorted_keys(rec, used.to(rec.device) if rec.device.type != "cpu" else used)
+    keys_sorted, pos = keys_sorted.cpu(), pos.cpu()
+    vocab = rec.vocab
+    # rank of the root symbol among the used strings (it only meets tokens, at the first token slot)
+    nless = bisect.bisect_left(range(keys_sorted.numel()), root, key=lambda i: vocab[int(keys_sorted[i])])
+    rk = torch.where(codes >= 0, 2 * pos[codes.clamp_min(0)] + 2, torch.zeros_like(codes))
+    rk[is_root, k] = 2 * nless + 1
+    order = np.lexsort(tuple(rk[:, j].numpy() for j in range(k + L - 1, -1, -1)))
+    order = torch.from_numpy(order.astype(np.int64))
+    codes, is_root, cnt = codes[order], is_root[order], cnt[order]
+    # compact string table of the used codes (+ the root symbol)
+    tab = [vocab[int(c)] for c in keys_sorted.tolist()] + [root]
+    lut = torch.full((len(vocab) + 1,), -1, dtype=torch.int32)
+    lut[keys_sorted] = torch.arange(keys_sorted.numel(), dtype=torch.int32)
+    ci = torch.where(codes >= 0, lut[codes.clamp_min(0)], torch.full_like(codes, -1, dtype=torch.int32).int()).int()
+    tk = ci[:, k:].clone()
+    tk[is_root, 0] = len(tab) - 1
+    n_tok = (tk >= 0).sum(1)
+    off = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(n_tok, 0)])
+    cols = [("s", tab, ci[:, j].contiguous()) for j in range(k)]
+    cols += [("l", tab, tk[tk >= 0].contiguous(), off), ("i", cnt)]
+    ctx.emit_root_text(format_lines(cols, int(cnt.numel()), ctx.delim_out))
+
+
+def _pstg_rows(ctx, skip, cls_ord, L, root, id_ords, sequential):
+    """Regex delimiters: split rows, then the same counting as the native path."""
     seqs: list[tuple[tuple, list[str]]] = []
-    if ctx.get_bool("input.format.sequential", True):
+    if sequential:
         for r in ctx.rows():
             if len(r) < skip + 2:
                 continue
             pref = tuple(r[o] for o in id_ords) + ((r[cls_ord],) if cls_ord >= 0 else ())
             seqs.append((pref, r[skip:]))
     else:
-        # streaming windows per id: a window of the last L tokens emits prefixes of width 2..L
         dfo = ctx.get_int("data.field.ordinal")
         wins = defaultdict(list)
         for r in ctx.rows(shard=False):
@@ -135,60 +337,33 @@ def pstg(args):
             if len(w) > L:
                 w.pop(0)
             if len(w) == L:
-                seqs.append((pref, list(w[:L]) + ["\x00stream"]))
-    counts = ngram_counts(ctx, seqs, L, streaming=not ctx.get_bool("input.format.sequential", True))
+                seqs.append((pref, list(w)))
+        if ctx.comm.rank != 0:
+            seqs = []
+    counts = ngram_counts(ctx, seqs, L, streaming=not sequential, root=root)
     d = ctx.delim_out
     ctx.emit_root([d.join(list(k) + [str(c)]) for k, c in sorted(counts.items())] if ctx.is_root else [])
 
 
-def ngram_counts(ctx: JobContext, seqs, L: int, streaming: bool = False) -> dict[tuple, int]:
-    """{(prefix.., tok..): count} and {(prefix.., '$'): root count} for all windows of width 2..L."""
-    vocab = ctx.union({t for _, s in seqs for t in s if t != "\x00stream"})
+def ngram_counts(ctx: JobContext, seqs, L: int, streaming: bool = False, root: str = "$") -> dict[tuple, int]:
+    """{(prefix.., tok..): count} and {(prefix.., root): root count} for all windows of width 2..L
+    (split-row path; ``streaming``: only the windows at the start of each row)."""
+    vocab = ctx.union({t for _, s in seqs for t in s})
     prefs = ctx.union({p for p, _ in seqs})
-    ti = {t: i + 1 for i, t in enumerate(vocab)}      # 0 = padding
+    ti = {t: i for i, t in enumerate(vocab)}
     pi = {p: i for i, p in enumerate(prefs)}
-    V = len(vocab) + 1
     out: dict[tuple, int] = {}
-    if not seqs:
-        seqs = []
     maxlen = max([len(s) for _, s in seqs] + [2])
-    T = torch.zeros((len(seqs), maxlen), dtype=torch.long)
-    P = torch.tensor([pi[p] for p, _ in seqs], dtype=torch.long)
-    for i, (_, s) in enumerate(seqs):
-        toks = [ti[t] for t in s if t != "\x00stream"]
-        T[i, : len(toks)] = torch.tensor(toks, dtype=torch.long)
-    T = T.to(ctx.device)
-    P = P.to(ctx.device)
-    root = torch.zeros(len(prefs), dtype=torch.long, device=ctx.device)
-    digits = max(1, math.ceil(math.log2(V + 1)))
-    for w in range(2, L + 1):
-        if T.shape[1] < w or T.shape[0] == 0:
-            keys, cnt = torch.zeros(0, dtype=torch.long), torch.zeros(0, dtype=torch.long)
-        else:
-            win = T.unfold(1, w, 1)                                   # [n, nw, w]
-            if streaming:
-                win = win[:, :1]                                     # one prefix window per stream step
-            ok = (win > 0).all(-1)
-            key = P.view(-1, 1).expand_as(ok)
-            for j in range(w):
-                key = key * (1 << digits) + win[..., j]
-            keys, cnt = torch.unique(key[ok], return_counts=True)
-            root.index_add_(0, P.view(-1, 1).expand_as(ok)[ok], torch.ones_like(key[ok]))
-        if ctx.comm.is_distributed:
-            ks = ctx.comm.all_gather_v(keys.cpu())
-            cs = ctx.comm.all_gather_v(cnt.cpu())
-            keys, inv = torch.unique(ks, return_inverse=True)
-            cnt = torch.zeros_like(keys).index_add_(0, inv, cs)
-        for k, c in zip(keys.cpu().tolist(), cnt.cpu().tolist()):
-            toks = []
-            for _ in range(w):
-                toks.append(vocab[(k & ((1 << digits) - 1)) - 1])
-                k >>= digits
-            out[tuple(prefs[k]) + tuple(reversed(toks))] = c
-    ctx.all_reduce(root)
-    for p, c in zip(prefs, root.cpu().tolist()):
-        if c:
-            out[tuple(p) + ("$",)] = c
+    T = torch.tensor([[ti[t] for t in s] + [-1] * (maxlen - len(s)) for _, s in seqs], dtype=torch.int32)
+    T = T.view(len(seqs), maxlen)
+    P = torch.tensor([pi[p] for p, _ in seqs], dtype=torch.int32).view(-1, 1)
+    rows = _ngram_rows(T.to(ctx.device), P.to(ctx.device), L, streaming)
+    if ctx.comm.is_distributed:
+        dev = ctx.comm.device if ctx.comm.backend == "nccl" else torch.device("cpu")
+        rows = ctx.comm.all_gather_v(rows.to(dev))
+    for r in rows.cpu().tolist():
+        key = prefs[r[0]] + ((root,) if r[1 + L] else tuple(vocab[t] for t in r[1:1 + L] if t >= 0))
+        out[key] = out.get(key, 0) + r[-1]
     return out
 
 
@@ -304,6 +479,14 @@ def _state_transition_rate_native(ctx, kords, to, so, states, unit, in_unit, pre
     ok = (st >= 0) & ~torch.isnan(tm_raw)
     for c in kc:
         ok &= c >= 0
+    # an event with an unknown state or an unparsable time stamp is an error, as in the row path
+    # and the reference (DoubleTable.add fails): dropping it would splice its neighbours into a
+    # transition that never happened.  Counted over all ranks so every rank stops together.
+    bad = torch.tensor([int((~ok).sum())], dtype=torch.long, device=dev)
+    ctx.all_reduce(bad)
+    if int(bad):
+        raise SystemExit(f"stateTransitionRate: {int(bad)} event(s) with a state outside state.values, "
+                         f"a missing key or an unparsable time stamp")
     comp = kc[0] if len(kc) == 1 else kc[0] * V + kc[1]
     comp, st = comp[ok], st[ok]
     mult = 1000 if in_unit == "sec" else 1

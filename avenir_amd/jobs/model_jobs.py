@@ -485,6 +485,76 @@ def model_predictor(args):
     models = [DecisionPathModel(json.loads((mdir / n).read_text())) for n in names]
     weights = ctx.get_float_list("ensemble.memeber.weights", None) or [1.0] * len(models)
     classes = sorted({c for m in models for c in m.class_values})
+    mode = ctx.get_str("output.mode", "withRecord")
+    id_o = ctx.get_int("rec.id.ordinal", 0)
+    co = ctx.get_int("rec.class.attr.ordinal", ctx.get_int("class.attr.ord", -1))
+    from ..data.table import _literal
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _model_predictor_rows(ctx, models, weights, classes, mode, id_o, co)
+    from ..data.records import format_lines, numeric_lut
+    from ..utils.rules import RecordColumns
+    # native path: the predicate fields are tokenized once ('d' for categorical sets and the class,
+    # 'n' for thresholds), every model's paths are evaluated column-wise on the device, and the
+    # output comes from the raw line bytes + the vote winners
+    cat, num = set(), set()
+    for m in models:
+        for pth in m.paths:
+            for pr in pth["predicates"]:
+                it = pr["predicateStr"].split()
+                if len(it) >= 3 and it[0].lstrip("-").isdigit():
+                    (cat if it[1] == "in" else num).add(int(it[0]))
+    dict_ords = cat | ({co} if co >= 0 else set())
+    top = max(list(cat | num) + [co, 0]) + 1
+    modes = "".join("d" if i in dict_ords else ("n" if i in num else "x") for i in range(top))
+    rec = ctx.records(modes=modes, tail_mode="x", numeric=True, trim=True)
+    cols_src = RecordColumns(rec)
+    both = num & dict_ords
+    if both:   # a field used as a category and as a number: its numbers from the dictionary strings
+        lut = numeric_lut(rec.vocab, rec.device)
+        plain = cols_src.numeric
+        cols_src.numeric = lambda o: (torch.where(rec.field(o) >= 0, lut[rec.field(o).long().clamp_min(0)],
+                                                  torch.full((rec.n_lines,), float("nan"), dtype=torch.float64,
+                                                             device=rec.device))
+                                      if o in both else plain(o))
+    n = rec.n_lines
+    votes = torch.zeros((n, len(classes)), dtype=torch.float64, device=rec.device)
+    for m, w in zip(models, weights):
+        pr, _ = m.predict_proba_cols(cols_src)
+        idx = torch.tensor([classes.index(c) for c in m.class_values], dtype=torch.long, device=rec.device)
+        win = idx[pr.argmax(1)]
+        votes.scatter_add_(1, win.view(-1, 1), torch.full((n, 1), float(w), dtype=torch.float64, device=rec.device))
+    pred = votes.argmax(1)
+    spans = rec.line_spans()
+    pcol = ("s", list(classes), pred.int().cpu())
+    if mode == "withKId":
+        cols = [spans.column("rf", id_o, lit), pcol]
+    elif mode == "withActualClassAttr":
+        cols = [spans.column("rf", id_o, lit), spans.column("rf", co, lit), pcol]
+    else:
+        cols = [spans.column("r", delims=lit), pcol]
+    ctx.emit_text(format_lines(cols, n, ctx.delim_out))
+    if co >= 0:
+        has = rec.lens() > co
+        actual = rec.map_codes(rec.field(co), classes).long()
+        err = torch.tensor([float(((actual != pred) & has).sum()), float(has.sum())], dtype=torch.float64)
+    else:
+        err = torch.zeros(2, dtype=torch.float64)
+    _report_error_rate(ctx, err)
+
+
+def _report_error_rate(ctx, err: torch.Tensor) -> None:
+    ctx.all_reduce(err)
+    rate = float(err[0]) / max(float(err[1]), 1)
+    ep = ctx.cfg.values.get("map.error.rate.file.path")
+    if ep and ctx.is_root:
+        Path(ep).parent.mkdir(parents=True, exist_ok=True)
+        Path(ep).write_text(f"errorRate={rate:.6f}\n")
+    ctx.report({"errorRate": rate})
+
+
+def _model_predictor_rows(ctx, models, weights, classes, mode, id_o, co):
+    """Regex delimiters: the split-row path."""
     rows = ctx.rows()
     votes = torch.zeros((len(rows), len(classes)), dtype=torch.float64)
     for m, w in zip(models, weights):
@@ -493,16 +563,13 @@ def model_predictor(args):
         win = idx[pr.argmax(1)]
         votes.scatter_add_(1, win.view(-1, 1), torch.full((len(rows), 1), float(w), dtype=torch.float64))
     pred = votes.argmax(1).tolist()
-    mode = ctx.get_str("output.mode", "withRecord")
-    id_o = ctx.get_int("rec.id.ordinal", 0)
-    co = ctx.get_int("rec.class.attr.ordinal", ctx.get_int("class.attr.ord", -1))
     d = ctx.delim_out
     out, errors, total = [], 0, 0
     for r, p in zip(rows, pred):
         pv = classes[p]
         if co >= 0 and co < len(r):
             total += 1
-            errors += int(r[co] != pv)
+            errors += int(r[co].strip() != pv)
         if mode == "withKId":
             out.append(f"{r[id_o]}{d}{pv}")
         elif mode == "withActualClassAttr":
@@ -510,14 +577,7 @@ def model_predictor(args):
         else:
             out.append(f"{d.join(r)}{d}{pv}")
     ctx.emit(out)
-    err = torch.tensor([float(errors), float(total)])
-    ctx.all_reduce(err)
-    rate = float(err[0]) / max(float(err[1]), 1)
-    ep = ctx.cfg.values.get("map.error.rate.file.path")
-    if ep and ctx.is_root:
-        Path(ep).parent.mkdir(parents=True, exist_ok=True)
-        Path(ep).write_text(f"errorRate={rate:.6f}\n")
-    ctx.report({"errorRate": rate})
+    _report_error_rate(ctx, torch.tensor([float(errors), float(total)], dtype=torch.float64))
 
 
 @job("dataPartitioner", "partition records by the best (or random top) split of classPartitionGenerator (J/tree/DataPartitioner.java, dap.*)")
@@ -656,19 +716,116 @@ def random_first_bandit(args):
 # ================================================================================================
 # record similarity
 # ================================================================================================
+@job("recordSimilarity", "all-pairs record distances, optionally between two sets (S/similarity/RecordSimilarity.scala, chombo RecordSimilarity)")
+def record_similarity(args):
+    """Numeric fields ``attr.ordinals`` (range-normalised over both sets), ids at ``id.ordinal``;
+    distances of all pairs (i < j within one set, or every (base, other) pair with ``--train``)
+    scaled by ``distance.scale`` and rounded; pairs above ``dist.threshold`` dropped.  Output
+    ``id1,id2,[rec1,rec2,]dist`` (``output.record``), in (i, j) order.
+
+    Data-parallel (the reference replicates every record into ``num.buckets`` bucket pairs,
+    S/similarity/RecordSimilarity.scala:80-150): every rank reads only its byte range of each set;
+    its base rows stay put while the other set's row blocks — numeric columns plus the raw line
+    bytes — travel around the ring (``Comm.ring_iter``: the next block's transfer is posted before
+    the distance tiles of the current one run on the device).  Each rank writes the pairs of its own
+    base rows, sorted by (i, j), so the rank-ordered output equals the single-rank one."""
+    from ..data.table import _literal
+    ctx = JobContext(args, "resi.", app="recordSimilarity")
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _record_similarity_rows(ctx, args)
+    from ..data.lines import LineSpans
+    from ..data.records import format_lines
+    from ..ops.distance import pairwise
+    ords = ctx.get_int_list("attr.ordinals")
+    idc = ctx.get_int("id.ordinal", 0)
+    scale = ctx.get_float("distance.scale", 1000.0)
+    thr = ctx.get_float("dist.threshold", math.inf)
+    out_rec = ctx.get_bool("output.record", False)
+    comm = ctx.comm
+    top = max(list(ords) + [idc]) + 1
+    modes = "".join("n" if i in ords else "x" for i in range(top))
+    rA = ctx.records(modes=modes, tail_mode="x", numeric=True)
+    rB = ctx.records(args.train, modes=modes, tail_mode="x", numeric=True) if args.train else None
+    dev = ctx.device
+    num = lambda r: (torch.stack([r.field(o, numeric=True) for o in ords], 1).float().to(dev) if r.n_lines
+                     else torch.zeros((0, len(ords)), dtype=torch.float32, device=dev))
+    XA = num(rA)
+    XB = num(rB) if rB is not None else XA
+    both = torch.cat([XA, XB]) if rB is not None else XA
+    big = torch.full((len(ords),), float("inf"), device=dev)
+    lo = torch.where(torch.isnan(both), big, both).amin(0) if both.shape[0] else big.clone()
+    hi = torch.where(torch.isnan(both), -big, both).amax(0) if both.shape[0] else -big
+    if comm.is_distributed:
+        comm.all_reduce(lo, "min")
+        comm.all_reduce(hi, "max")
+    rng = (hi - lo).clamp_min(1e-12)
+    A = (XA - lo) / rng
+    B = (XB - lo) / rng if rB is not None else A
+    spA = rA.line_spans()
+    spB = rB.line_spans() if rB is not None else spA
+    a_base = rA.line_base
+    b_rec = rB if rB is not None else rA
+    nB = torch.tensor([b_rec.n_lines], dtype=torch.long)
+    ctx.all_reduce(nB)
+    NB = int(nB)
+    bbuf, boff = spB.pack()
+    cdev = comm.device if (comm.is_distributed and comm.pg_backend == "nccl") else torch.device("cpu")
+    payload = [B.to(cdev), torch.tensor([b_rec.line_base], dtype=torch.long, device=cdev), bbuf.to(cdev),
+               boff.to(cdev)]
+    nf = math.sqrt(max(len(ords), 1))
+    tile = max(1, min(4096, (1 << 26) // max(1, NB // max(1, comm.world))))
+    I, J, Dv, H = [], [], [], []
+    blocks = []
+    for h, (owner, (Bc, bbase, bb, bo)) in enumerate(comm.ring_iter(payload)):
+        Bc = Bc.to(dev)
+        b0 = int(bbase.cpu()[0]) if bbase.numel() else 0
+        blocks.append(LineSpans.from_packed(bb, bo))
+        nb = Bc.shape[0]
+        for s in range(0, A.shape[0], tile):
+            e = min(A.shape[0], s + tile)
+            if nb == 0:
+                break
+            D = torch.round(pairwise(A[s:e], Bc) / nf * scale)
+            keep = D <= thr if math.isfinite(thr) else torch.ones_like(D, dtype=torch.bool)
+            if rB is None:   # upper triangle of the global index: j > i
+                keep &= (torch.arange(b0, b0 + nb, device=dev).view(1, -1)
+                         > torch.arange(a_base + s, a_base + e, device=dev).view(-1, 1))
+            qi, jj = torch.nonzero(keep, as_tuple=True)
+            if qi.numel():
+                I.append(qi + s)
+                J.append(jj + b0)
+                Dv.append(D[qi, jj].long())
+                H.append(torch.full_like(jj, h) * (1 << 40) + jj)
+    if I:
+        I, J, Dv, H = torch.cat(I), torch.cat(J), torch.cat(Dv), torch.cat(H)
+        order = torch.argsort(I * max(1, NB) + J)
+        I, Dv, H = I[order].cpu(), Dv[order].cpu(), H[order].cpu()
+    else:
+        I = Dv = H = torch.zeros(0, dtype=torch.long)
+    # the B side of every pair: its hop's received line block, row jj
+    hop, jl = H >> 40, H & ((1 << 40) - 1)
+    hop_base = torch.tensor([0] + [len(b) for b in blocks], dtype=torch.long).cumsum(0)
+    addr = torch.cat([b.spans()[1] for b in blocks]) if blocks else torch.zeros(0, dtype=torch.long)
+    lens = torch.cat([b.spans()[2] for b in blocks]) if blocks else torch.zeros(0, dtype=torch.long)
+    gi = hop_base[:-1][hop] + jl if hop.numel() else hop
+    spJ = LineSpans(blocks, addr[gi], lens[gi])
+    spI = spA.select(I)
+    cols = [spI.column("rf", idc, lit), spJ.column("rf", idc, lit)]
+    if out_rec:
+        cols += [spI.column("r", delims=lit), spJ.column("r", delims=lit)]
+    cols.append(("i", Dv))
+    ctx.emit_text(format_lines(cols, int(I.numel()), ctx.delim_out))
+
+
 def _numeric_matrix(ctx, rows, ords):
     return torch.tensor([[float(r[o]) for o in ords] for r in rows], dtype=torch.float32, device=ctx.device)
 
 
-@job("recordSimilarity", "all-pairs record distances, optionally between two sets (S/similarity/RecordSimilarity.scala, chombo RecordSimilarity)")
-def record_similarity(args):
-    """Numeric fields ``attr.ordinals`` (range-normalised), ids at ``id.ordinal``; distances of all
-    pairs (i < j within one set, or every (base, other) pair with ``--train``) are a tiled device
-    GEMM; the pair loop runs in ``ring`` order over the ranks' shards.  Output
-    ``id1,id2,[rec1,rec2,]dist*scale`` (``output.record``), pairs above ``dist.threshold``
-    dropped."""
+def _record_similarity_rows(ctx, args):
+    """Regex delimiters: the split-row path (every rank reads both sets, computes its block of
+    base rows)."""
     from ..ops.distance import pairwise
-    ctx = JobContext(args, "resi.", app="recordSimilarity")
     ords = ctx.get_int_list("attr.ordinals")
     idc = ctx.get_int("id.ordinal", 0)
     scale = ctx.get_float("distance.scale", 1000.0)
@@ -690,12 +847,12 @@ def record_similarity(args):
     nB = len(Brows)
     for s in range(a, b, 2048):
         e = min(b, s + 2048)
-        D = (pairwise(A[s:e], B) / nf * scale).round().long()
+        D = torch.round(pairwise(A[s:e], B) / nf * scale)
         keep = D <= thr if math.isfinite(thr) else torch.ones_like(D, dtype=torch.bool)
         if other is None:   # upper triangle: j > i
             keep &= torch.arange(nB, device=D.device).view(1, -1) > torch.arange(s, e, device=D.device).view(-1, 1)
         qi, jj = torch.nonzero(keep, as_tuple=True)          # row-major: (i, j) ascending
-        vals = D[qi, jj].tolist()
+        vals = D[qi, jj].long().tolist()
         for q, j, v in zip(qi.tolist(), jj.tolist(), vals):
             i = s + q
             parts = [rows[i][idc], Brows[j][idc]]

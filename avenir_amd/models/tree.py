@@ -409,7 +409,8 @@ class DecisionPathModel:
         if op == "in":
             c, vocab = cols.codes(o)
             ids = [vocab[v] for v in it[2].split(":") if v in vocab]
-            return torch.isin(c, torch.tensor(ids, dtype=torch.long)) if ids else torch.zeros_like(c, dtype=torch.bool)
+            return (torch.isin(c, torch.tensor(ids, dtype=torch.long, device=c.device)) if ids
+                    else torch.zeros_like(c, dtype=torch.bool))
         x = cols.numeric(o)
         v = float(it[2])
         if op == "le":
@@ -431,9 +432,16 @@ class DecisionPathModel:
     def predict_proba_rows(self, rows) -> tuple[torch.Tensor, torch.Tensor]:
         """(class probabilities [N, C] of the matched path, matched path index [N] (-1 = none))."""
         from ..utils.rules import ColumnCache
-        cols = ColumnCache(rows)
-        n, P = len(rows), len(self.paths)
-        M = torch.ones((n, P), dtype=torch.bool)
+        return self.predict_proba_cols(ColumnCache(rows))
+
+    def predict_proba_cols(self, cols) -> tuple[torch.Tensor, torch.Tensor]:
+        """:meth:`predict_proba_rows` over a column source with ``n``, ``device``, ``codes(o)`` ->
+        (codes, {value: code}) and ``numeric(o)`` -> float64 values: ``utils.rules.ColumnCache``
+        (split rows), :class:`TableColumns` (a schema Table) or ``RecordColumns`` (a native token
+        table) — the last two keep every step on the table's device."""
+        n, P = cols.n, len(self.paths)
+        dev = cols.device
+        M = torch.ones((n, P), dtype=torch.bool, device=dev)
         cache: dict[str, torch.Tensor] = {}
         for j, p in enumerate(self.paths):
             for pr in p["predicates"]:
@@ -444,13 +452,34 @@ class DecisionPathModel:
                     cache[ps] = self._pred(cols, ps)
                 M[:, j] &= cache[ps]
         any_ = M.any(1)
-        first = torch.where(any_, M.int().argmax(1), torch.full((n,), -1, dtype=torch.long))
+        first = torch.where(any_, M.int().argmax(1), torch.full((n,), -1, dtype=torch.long, device=dev))
         ci = {c: i for i, c in enumerate(self.class_values)}
         tab = torch.zeros((P + 1, len(ci)), dtype=torch.float64)
         for j, p in enumerate(self.paths):
             for c, v in p.get("classValPr", {}).items():
                 tab[j, ci[c]] = float(v)
-        return tab[torch.where(first >= 0, first, torch.full_like(first, P))], first
+        return tab.to(dev)[torch.where(first >= 0, first, torch.full_like(first, P))], first
+
+
+class TableColumns:
+    """Column source of :meth:`DecisionPathModel.predict_proba_cols` over a schema Table (loaded
+    with ``raw_numeric``): categorical codes with the schema dictionary, numeric columns widened to
+    float64 — the predicate thresholds the builder writes come from the same float32 columns."""
+
+    def __init__(self, t: Table):
+        self.t, self.n, self.device = t, t.n, t.device
+
+    def codes(self, o: int):
+        for j, f in enumerate(self.t.binned_fields):
+            if f.ordinal == o:
+                return self.t.codes[j, : self.n].long(), {v: i for i, v in enumerate(f.cardinality or [])}
+        raise KeyError(f"field {o} is not a binned field of the table")
+
+    def numeric(self, o: int) -> torch.Tensor:
+        for j, f in enumerate(self.t.numeric_fields):
+            if f.ordinal == o:
+                return self.t.numeric[j, : self.n].double()
+        raise KeyError(f"field {o} is not a numeric field of the table")
 
 
 def _predicate_obj(ps: str, f: FeatureField) -> dict:

@@ -23,8 +23,9 @@ def viterbi(obs: torch.Tensor, logA: torch.Tensor, logB: torch.Tensor, logpi: to
     S = logA.shape[0]
     lA, lB, lp = logA.double(), logB.double(), logpi.double()
     ob = obs.long()
-    valid = ob >= 0
+    valid = (ob >= 0) & (ob < lB.shape[1])      # an out-of-range observation ends the sequence too
     lens = torch.where(valid.all(1), torch.full((N,), T), (~valid).int().argmax(1))
+    ob = torch.where(valid, ob, torch.zeros_like(ob))
     o0 = ob[:, 0].clamp_min(0)
     delta = lp.view(1, S) + lB[:, o0].T
     bps = []
@@ -40,19 +41,21 @@ def viterbi(obs: torch.Tensor, logA: torch.Tensor, logB: torch.Tensor, logpi: to
         act = (t < lens).view(N, 1)
         delta = torch.where(act, nd, delta)
         bps.append(bp)
+    empty = lens == 0                              # an invalid first observation: no path, score -inf
     if forward:
-        return None, torch.logsumexp(delta, 1).float()
+        ll = torch.logsumexp(delta, 1)
+        return None, torch.where(empty, torch.full_like(ll, float("-inf")), ll).float()
     score, s = delta.max(1)
+    score = torch.where(empty, torch.full_like(score, float("-inf")), score)
+    # backtrack all rows at once: path[L-1] = argmax, path[t] = bp_{t+1}[path[t+1]] for t < L-1
     path = torch.full((N, T), -1, dtype=torch.int16)
-    for r in range(N):
-        L = int(lens[r])
-        if L == 0:
-            continue
-        st = int(s[r])
-        path[r, L - 1] = st
-        for t in range(L - 1, 0, -1):
-            st = int(bps[t - 1][r, st])
-            path[r, t - 1] = st
+    rows = torch.arange(N)
+    nxt = s.clone()
+    for t in range(T - 1, -1, -1):
+        st = s if t == T - 1 else torch.where(t == lens - 1, s, bps[t][rows, nxt])
+        st = torch.where(t < lens, st, torch.full_like(st, -1))
+        path[:, t] = st.to(torch.int16)
+        nxt = st.clamp_min(0)
     return path, score.float()
 
 
@@ -255,7 +258,8 @@ def ngram_counts(states: torch.Tensor, n_states: int, min_len: int = 2, max_len:
     counting, J/markov/ProbabilisticSuffixTreeGenerator.java:140-194).  n-grams are packed into
     int64 keys (base n_states + 1, group id in the high bits).  GPU: one pass of the K5 hash-count
     kernel for all lengths (LDS-privatised table, global open addressing); CPU: per-length device
-    sort (torch.unique).  Returns {length: (sorted keys, counts)}."""
+    sort (torch.unique; also on a GPU when the states do not fit the kernel's int16).  Returns
+    {length: (sorted keys, counts)}."""
     N, L = states.shape
     base = n_states + 1
     gmul = base ** max_len
@@ -265,7 +269,7 @@ def ngram_counts(states: torch.Tensor, n_states: int, min_len: int = 2, max_len:
             raise ValueError("n-gram key space (groups x (S+1)^max_len) exceeds 2^58")
     elif gmul >= (1 << 58):
         raise ValueError("n-gram key space (S+1)^max_len exceeds 2^58")
-    if states.is_cuda:
+    if states.is_cuda and n_states < 32767:
         st = states.to(torch.int16).contiguous()
         g = group.to(torch.int32).contiguous() if group is not None else None
         windows = sum(max(0, L - k + 1) for k in range(min_len, max_len + 1)) * N

@@ -164,7 +164,8 @@ def kendall_tau_b(x, y) -> tuple[float, float]:
 
 def mann_whitney_u(a, b) -> tuple[float, float]:
     """(U of the first sample, two-sided p) as scipy.stats.mannwhitneyu (continuity correction,
-    method auto: exact for tie-free samples of <= 8 values each)."""
+    method auto = scipy's ``_mwu_choose_method``: the exact null for tie-free samples unless BOTH
+    hold more than 8 values)."""
     from scipy import stats
     a, b = _dev(a), _dev(b).to(_dev(a).device)
     n1, n2 = a.numel(), b.numel()
@@ -174,7 +175,7 @@ def mann_whitney_u(a, b) -> tuple[float, float]:
     r1 = float(gs[0])
     u1 = r1 - n1 * (n1 + 1) / 2.0
     t3 = float(tie[0])
-    if n1 <= 8 and n2 <= 8 and t3 == 0:
+    if (n1 <= 8 or n2 <= 8) and t3 == 0:
         return u1, float(stats.mannwhitneyu(a.cpu().numpy(), b.cpu().numpy()).pvalue)
     u2 = n1 * n2 - u1
     u = max(u1, u2)

@@ -313,6 +313,31 @@ class Comm:
             r.wait()
         return recv.to(dev) if dev is not None else recv
 
+    def ring_iter(self, tensors: list[torch.Tensor]):
+        """Systolic ring over every rank's block: yields ``(owner, block)`` W times, starting with
+        this rank's own ``tensors`` (a list sharing dim 0 per tensor, any dtypes), then the blocks of
+        rank-1, rank-2, ... .  The block sizes are exchanged once up front; the transfer of the
+        next block (``ring_pass_start``, one batched P2P group per tensor) is posted BEFORE the
+        current block is yielded, so the caller's compute on it overlaps the xGMI transfer.  With
+        world size 1: the own block once."""
+        if not self.is_distributed:
+            yield self.rank, tensors
+            return
+        W, me = self.world, self.rank
+        n = torch.tensor([t.shape[0] for t in tensors], dtype=torch.long,
+                         device=self.device if self.pg_backend == "nccl" else "cpu")
+        sizes = self.all_gather(n).view(W, -1).tolist()
+        cur = [t.contiguous() for t in tensors]
+        for step in range(W):
+            owner = (me - step) % W
+            pend = None
+            if step + 1 < W:
+                src = (me - step - 1) % W
+                pend = [self.ring_pass_start(t, sizes[src][k]) for k, t in enumerate(cur)]
+            yield owner, cur
+            if pend is not None:
+                cur = [self.ring_pass_finish(h) for h in pend]
+
     def barrier(self) -> None:
         if self.is_distributed:
             if self.pg_backend == "nccl":

@@ -89,6 +89,26 @@ class RuleExpression:
         return self.evaluate(ColumnCache(rows, device))
 
 
+class RecordColumns:
+    """ColumnCache's interface over a native token table (data/records.Records): ``codes(o)`` are
+    the table's dictionary codes of field ``o`` (read with mode 'd', trimmed), ``numeric(o)`` its
+    parsed doubles (mode 'n'), both on the table's device; no Python string per record."""
+
+    def __init__(self, rec):
+        self.rec, self.n, self.device = rec, rec.n_lines, rec.device
+        self._vocab: dict[str, int] | None = None
+
+    def numeric(self, o: int) -> torch.Tensor:
+        return self.rec.field(o, numeric=True)
+
+    def codes(self, o: int):
+        if self._vocab is None:
+            self._vocab = {}
+            for i, v in enumerate(self.rec.vocab):
+                self._vocab.setdefault(v, i)
+        return self.rec.field(o).long(), self._vocab
+
+
 class ColumnCache:
     """Lazily tensorised columns of a list of split records."""
 

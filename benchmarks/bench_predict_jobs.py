@@ -1,0 +1,125 @@
+"""End-to-end (file -> output file) timings of the prediction / sequence jobs that moved onto
+native input and output in round 4: viterbiStatePredictor,
+markovModelClassifier, probabilisticSuffixTreeGenerator (K5), bayesianPredictor, decisionTree
+level mode, modelPredictor.  Each job runs in-process on ``--records`` records (default 2^24) of a
+synthetic file of its reference layout; models are trained once beforehand (untimed); the best
+of ``--reps`` runs is reported as records/s, one JSON line per job.
+
+    python benchmarks/bench_predict_jobs.py [--records N] [--jobs vit,mmc,...] [--out file]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from avenir_amd.cli import main as cli  # noqa: E402
+from avenir_amd.data import synth  # noqa: E402
+from avenir_amd.data import synth_text as S  # noqa: E402
+
+
+def _run(args):
+    assert cli([str(a) for a in args]) == 0
+
+
+def _props(d, name, text):
+    p = os.path.join(d, name)
+    with open(p, "w") as fh:
+        fh.write(text)
+    return p
+
+
+def setup(job: str, d: str, n: int, dev: str):
+    """(argv without -o, input path) for ``job``; trains its model (untimed)."""
+    if job == "vit":
+        tagged = os.path.join(d, "tagged.txt")
+        S.tagged_sequences(tagged, min(n, 1 << 20), seed=3)
+        cfg = _props(d, "hmm.properties", "hmmb.model.states=S,T,U\nhmmb.model.observations=a,b,c,d\n"
+                                          "hmmb.skip.field.count=1\nhmmb.trans.prob.scale=1000\n")
+        model = os.path.join(d, "hmm.txt")
+        _run(["hiddenMarkovModelBuilder", "-i", tagged, "-o", model, "-c", cfg, "--device", dev])
+        data = os.path.join(d, "obs.txt")
+        S.observation_sequences(data, n, seed=4)
+        return ["viterbiStatePredictor", "-i", data, "--model", model, "-c",
+                _props(d, "vit.properties", "vsp.skip.field.count=1\n")], data
+    if job in ("mmc", "pst"):
+        data = os.path.join(d, "seq.txt")
+        if not os.path.exists(data):
+            S.state_sequences(data, n, seed=5)
+        if job == "pst":
+            return ["probabilisticSuffixTreeGenerator", "-i", data, "-c",
+                    _props(d, "pst.properties", "pstg.skip.field.count=1\npstg.class.label.field.ord=1\n"
+                                                "pstg.max.seq.length=5\n")], data
+        cfg = _props(d, "mmc.properties", "mst.model.states=" + ",".join(S.STATES) + "\nmst.skip.field.count=2\n"
+                     "mst.class.label.field.ord=1\nmst.class.labels=T,F\nmmc.class.labels=T,F\n"
+                     "mmc.skip.field.count=2\nmmc.validation.mode=true\nmmc.class.label.field.ord=1\n")
+        model = os.path.join(d, "mm.txt")
+        _run(["markovStateTransitionModel", "-i", data, "-o", model, "-c", cfg, "--device", dev])
+        return ["markovModelClassifier", "-i", data, "--model", model, "-c", cfg], data
+    data, schema = os.path.join(d, "churn.csv"), os.path.join(d, "churn.json")
+    if not os.path.exists(data):
+        synth.write_churn_native(data, n, seed=6)
+        with open(schema, "w") as fh:
+            json.dump(synth.CHURN_SCHEMA, fh)
+    if job == "nbp":
+        model = os.path.join(d, "nb.txt")
+        _run(["bayesianDistribution", "-i", data, "-o", model, "--schema", schema, "--device", dev])
+        return ["bayesianPredictor", "-i", data, "--schema", schema, "--model", model], data
+    if job == "detr":
+        return ["decisionTree", "-i", data, "--schema", schema, "-c",
+                _props(d, "detr.properties", "dtb.split.algorithm=giniIndex\ndtb.path.stopping.strategy=maxDepth\n"
+                       f"dtb.max.depth.limit=3\ndtb.decision.file.path.out={os.path.join(d, 'dp.json')}\n")], data
+    if job == "mop":
+        forest = os.path.join(d, "forest")
+        cfg = _props(d, "mop.properties", f"dtb.feature.schema.file.path={schema}\ndtb.split.algorithm=giniIndex\n"
+                     "dtb.path.stopping.strategy=maxDepth\ndtb.max.depth.limit=4\ndtb.num.trees=5\n"
+                     f"mop.model.dir.path={forest}\nmop.output.mode=withActualClassAttr\nmop.rec.id.ordinal=0\n"
+                     "mop.rec.class.attr.ordinal=6\n")
+        _run(["randomForest", "-i", data, "-o", forest, "-c", cfg, "--device", dev])
+        return ["modelPredictor", "-i", data, "-c", cfg], data
+    raise SystemExit(f"unknown job {job}")
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=1 << 24)
+    ap.add_argument("--jobs", default="vit,mmc,pst,nbp,detr,mop")
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    d = tempfile.mkdtemp(prefix="avmi_pred_")
+    for job in args.jobs.split(","):
+        argv, data = setup(job, d, args.records, dev)
+        out = os.path.join(d, f"{job}.out")
+        best = None
+        for _ in range(args.reps):
+            if dev == "cuda":
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _run(argv + ["-o", out, "--device", dev])
+            if dev == "cuda":
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        with open(out if os.path.isfile(out) else os.path.join(out, "part-00000"), "rb") as fh:
+            n_out = sum(1 for _ in fh)
+        rec = {"bench": "predict_job", "job": argv[0], "records": args.records, "device": dev,
+               "bytes": os.path.getsize(data), "seconds": round(best, 4), "records_per_s": args.records / best,
+               "output_lines": n_out}
+        print(json.dumps(rec), flush=True)
+        if args.out:
+            with open(args.out, "a") as fh:
+                fh.write(json.dumps(rec) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -49,3 +49,58 @@ def test_device_csv_edge_cases(cuda, tmp_path, monkeypatch):
     schema = FeatureSchema.from_json(synth.CALL_HANGUP_SCHEMA)
     _compare(p, schema, skip_header=True)
     _compare(p, schema, skip_header=True, raw_numeric=True)
+
+
+def _wide_file(path, n_rows, n_cols=80, seed=0):
+    """``id,c1..c{n_cols-1},class``: categorical / bucketed int / float columns in turn."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    cols = [np.char.add("r", np.arange(n_rows).astype(str))]
+    fields = [{"name": "id", "ordinal": 0, "id": True, "dataType": "string"}]
+    for j in range(1, n_cols):
+        k = j % 3
+        if k == 0:
+            cols.append(np.array(["aa", "bb", "cc", "dd"])[rng.integers(0, 4, n_rows)])
+            fields.append({"name": f"c{j}", "ordinal": j, "dataType": "categorical", "feature": True,
+                           "cardinality": ["aa", "bb", "cc", "dd"]})
+        elif k == 1:
+            cols.append(rng.integers(0, 100, n_rows).astype(str))
+            fields.append({"name": f"c{j}", "ordinal": j, "dataType": "int", "feature": True, "bucketWidth": 10,
+                           "min": 0, "max": 99})
+        else:
+            cols.append(np.char.mod("%.3f", rng.normal(size=n_rows)))
+            fields.append({"name": f"c{j}", "ordinal": j, "dataType": "double", "feature": True})
+    cols.append(np.array(["T", "F"])[rng.integers(0, 2, n_rows)])
+    fields.append({"name": "cls", "ordinal": n_cols, "dataType": "categorical", "classAttribute": True,
+                   "cardinality": ["T", "F"]})
+    with open(path, "w") as f:
+        for a in range(0, n_rows, 20000):
+            rows = [",".join(c[i] for c in cols) for i in range(a, min(n_rows, a + 20000))]
+            f.write("\n".join(rows) + "\n")
+    return FeatureSchema.from_json({"fields": fields})
+
+
+def test_wide_schema_host_parse_keeps_line_spans(tmp_path):
+    """The host parser on an 80-column schema; lines kept as byte spans equal the file's lines."""
+    p = tmp_path / "wide.csv"
+    schema = _wide_file(p, 3000)
+    t = TB.load_csv(p, schema, keep_lines=True)
+    assert t.n == 3000 and t.meta["parser"] == "host" and len(t.binned_fields) > 32
+    assert t.lines.tolist() == p.read_text().splitlines()
+    sub = t.select_rows(torch.tensor([5, 2, 2999]))
+    assert list(sub.lines) == [p.read_text().splitlines()[i] for i in (5, 2, 2999)]
+
+
+@pytest.mark.gpu
+def test_device_csv_wide_schema_over_32mb(cuda, tmp_path):
+    """> 32 parsed columns used to throw inside csv_parse_device.  80 columns, a file
+    above the 32 MB device threshold: the device parse (passes of <= 64 columns) equals the host
+    parse, reports parser='device', and its line spans equal the host lines."""
+    p = tmp_path / "wide.csv"
+    schema = _wide_file(p, 110_000)
+    assert os.path.getsize(p) >= TB._GPU_CSV_MIN_BYTES
+    cpu, gpu = _compare(p, schema, keep_lines=True)
+    assert gpu.meta.get("parser") == "device"
+    assert gpu.codes.shape[0] + gpu.numeric.shape[0] >= 79
+    assert gpu.lines[:100].tolist() == cpu.lines[:100].tolist()
+    assert gpu.lines[-3:].tolist() == cpu.lines[-3:].tolist() and len(gpu.lines) == len(cpu.lines)

@@ -357,7 +357,7 @@ def test_markov_classifier_and_pst(tmp_path):
     res = [l.split(",") for l in lines(out)]
     acc = sum(r[1] == r[2] for r in res) / len(res)
     assert acc > 0.8
-    cfg2 = props(tmp_path, "pst.properties", "pstg.skip.field.count=2\npstg.max.seq.length=3\n"
+    cfg2 = props(tmp_path, "pst.properties", "pstg.skip.field.count=1\npstg.max.seq.length=3\n"
                  "pstg.class.label.field.ord=1\n")
     out2 = tmp_path / "pst.txt"
     run("probabilisticSuffixTreeGenerator", "-i", data, "-o", out2, "-c", cfg2)

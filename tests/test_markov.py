@@ -142,11 +142,15 @@ def test_sequence_kernels_gpu(cuda):
         hmm = M.HiddenMarkovModel([str(i) for i in range(S)], [str(i) for i in range(O)], A, B, pi)
         obs = torch.tensor(rng.integers(0, O, (300, 25)), dtype=torch.int16)
         obs[5, 10:] = -1
+        obs[6, 0] = -1                      # an invalid first observation: an empty path
+        obs[7, 3] = O                       # an out-of-range observation ends the sequence
         dec = M.ViterbiDecoder(hmm)
         pc, sc = dec.decode(obs)
         pg, sg = M.ViterbiDecoder(hmm).decode(obs.to(cuda))
         assert torch.allclose(sc, sg.cpu(), rtol=1e-4, atol=1e-3)
         assert float((pc == pg.cpu()).float().mean()) > 0.999
+        assert bool((pg[6] == -1).all()) and bool((pc[6] == -1).all())
+        assert bool((pg[7, 3:] == -1).all()) and bool((pg[7, :3] >= 0).all())
         fc = dec.log_likelihood(obs)
         fg = dec.log_likelihood(obs.to(cuda)).cpu()
         assert torch.allclose(fc, fg, rtol=1e-4, atol=1e-3)

@@ -102,6 +102,18 @@ def test_native_equals_row_path(tmp_path, name):
     assert got and got == ref
 
 
+@pytest.mark.parametrize("regex", [False, True])
+def test_state_transition_rate_unknown_state_raises(tmp_path, regex):
+    """An event outside ``state.values`` stops both paths (the reference's DoubleTable.add fails);
+    the native path used to drop it and splice a transition that never happened."""
+    data = tmp_path / "ev.txt"
+    S.events(data, 400, n_keys=5, seed=3)
+    with open(data, "a") as f:
+        f.write("k1,1600000000000123,Z\n")
+    with pytest.raises((SystemExit, KeyError)):
+        _run("stateTransitionRate", data, tmp_path / "o.txt", _props(tmp_path, "str", None, regex=regex))
+
+
 def _world_job(rank, world, job, data, out, cfg):
     args = [job, "-i", data, "-o", out, "-c", cfg, "--device", "cpu"]
     if job == "stateTransitionRate":

@@ -222,3 +222,82 @@ def test_sorted_keys_string_order(tmp_path, dev, monkeypatch):
     rec2 = R.read_records(str(p2), device=dev, modes="dx")
     ks2, _ = R.sorted_keys(rec2, rec2.field(0))
     assert rec2.strings(ks2) == sorted(short)
+
+
+_NUM_TOKENS = ["0.3", "0.1", "-0.7", "123.456", "1e-5", "2.5E+3", "000.0625", ".5", "5.", "9007199254740993",
+               "0.30000000000000004", "1.7976931348623157e308", "4.9e-324", "123456789012345678901234.5",
+               "3.141592653589793238", "1e", "--1", "1.2.3", "", " 42 ", "7e22", "1e23", "0.000000000000000000001"]
+
+
+def _num_file(tmp_path, reps=1):
+    p = tmp_path / "nums.txt"
+    p.write_text("".join(f"r{i},{t}\n" for i in range(reps) for t in _NUM_TOKENS))
+    return p
+
+
+def _py_float(t):
+    try:
+        v = float(t.strip(" \t\r\v\f"))
+    except ValueError:
+        return math.nan
+    return v if t.strip()[-1:].isdigit() or t.strip().endswith(".") else math.nan
+
+
+@pytest.mark.skipif(not _native.available(), reason="native extension not built")
+def test_numeric_tokens_are_correctly_rounded(tmp_path):
+    """the native decimal parser rounded on every fractional digit ("0.3" ->
+    0.30000000000000004).  Native host tokens now equal Python's float() bit for bit (and the
+    pure-Python twin), including the strtod fallback beyond the exact fast path."""
+    p = _num_file(tmp_path)
+    nat = R.read_records(str(p), modes="xn", numeric=True).field(1, numeric=True).tolist()
+    py = _py(str(p) and [str(p)], modes="xn", numeric=True).field(1, numeric=True).tolist()
+    want = [_py_float(t) for t in _NUM_TOKENS]
+    for t, a, b, w in zip(_NUM_TOKENS, nat, py, want):
+        if math.isnan(w):
+            assert math.isnan(a), t
+            continue
+        assert a == w and b == w, (t, a, b, w)
+
+
+@pytest.mark.gpu
+def test_device_numeric_tokens_match_host(tmp_path, cuda, monkeypatch):
+    """The device tokenizer shares the parser: identical bits on the fast path (every token of up
+    to 15 significant digits and |exponent| <= 22)."""
+    p = _num_file(tmp_path, reps=400)
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
+    dev = R.read_records(str(p), device=cuda, modes="xn", numeric=True)
+    assert dev.stats.get("path") == "device"
+    host = R.read_records(str(p), modes="xn", numeric=True)
+    a, b = dev.field(1, numeric=True).cpu(), host.field(1, numeric=True)
+    fast = torch.tensor([len(t.strip().lstrip("+-").replace(".", "").lstrip("0")) <= 15 and "e" not in t.lower()
+                         for t in _NUM_TOKENS] * 400)
+    assert torch.equal(torch.isnan(a), torch.isnan(b))
+    ok = fast & ~torch.isnan(b)
+    assert torch.equal(a[ok], b[ok])
+
+
+def test_format_lines_pyrepr_and_raw_kinds(tmp_path):
+    """``prec=-2`` is Python's repr (shortest round trip); ``r`` / ``rf`` / ``rt`` copy raw line
+    bytes (whole, one field, fields from one on) — native and pure-Python formatter agree."""
+    import random as _r
+    from avenir_amd.data.lines import LineSpans
+    rnd = _r.Random(1)
+    v = torch.tensor([0.1 + 0.2, -0.0, 1e16, 1.5e-5, 123.0, 1e-4, 5e-324, float("inf"), float("nan")]
+                     + [rnd.uniform(-1, 1) * 10 ** rnd.randint(-25, 25) for _ in range(500)], dtype=torch.float64)
+    got = R.format_lines([("f", v, -2)], v.numel()).decode().split()
+    assert got == [repr(x) for x in v.tolist()]
+    p = tmp_path / "l.txt"
+    p.write_text("a,b,c\nd|e,f\n\ng\n")
+    sh = _native.C().TextShard([str(p)], 0, 1, 2, False) if _native.available() else None
+    spans = LineSpans.from_shard(sh) if sh is not None else LineSpans.from_strings(["a,b,c", "d|e,f", "g"])
+    assert spans.tolist() == ["a,b,c", "d|e,f", "g"] and spans[1] == "d|e,f" and len(spans) == 3
+    cols = [spans.column("rf", 1, ",|"), spans.column("rf", -1, ","), spans.column("rt", 1, ",|"),
+            spans.column("r", delims=",")]
+    want = "b;c;b;c;a;b;c\ne;f;e;f;d|e;f\n;g;;g\n"
+    assert R.format_lines(cols, 3, ";").decode() == want
+    C = _native.host
+    try:
+        _native.host = lambda: None          # the pure-Python twin
+        assert R.format_lines(cols, 3, ";").decode() == want
+    finally:
+        _native.host = C

@@ -68,6 +68,16 @@ def test_small_samples_use_exact_paths():
     assert u == pytest.approx(ref.statistic) and p == pytest.approx(ref.pvalue)
 
 
+@pytest.mark.parametrize("n1,n2", [(5, 200), (200, 8), (9, 9)])
+def test_mann_whitney_unbalanced_matches_scipy_method_choice(n1, n2):
+    """scipy's method='auto' takes the exact null when either tie-free sample has <= 8 values."""
+    rng = np.random.default_rng(n1 * 1000 + n2)
+    a, b = rng.normal(size=n1), rng.normal(size=n2) + 0.1
+    u, p = S.mann_whitney_u(torch.tensor(a), torch.tensor(b))
+    ref = stats.mannwhitneyu(a, b)
+    assert u == pytest.approx(ref.statistic) and p == pytest.approx(ref.pvalue, rel=1e-9)
+
+
 def test_explorer_uses_rank_kernels():
     from avenir_amd.analytics.explorer import DataExplorer
     x, y = _samples(400, seed=3)
