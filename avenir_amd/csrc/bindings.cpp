@@ -2924,7 +2924,7 @@ py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& deli
       keep.push_back(x);
       return x;
     };
-    if (kind == "s" || kind == "l") {
+    if (kind == "s" || kind == "l" || kind == "lp") {
       PyObject* key = t[1].ptr();  // one conversion per distinct table object
       auto hit = table_of.find(key);
       if (hit == table_of.end()) {
@@ -2935,11 +2935,18 @@ py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& deli
       if (kind == "s") {
         c.kind = avh::FmtCol::STR;
         c.idx = cpu_tensor(t[2], at::kInt, n, "string").data_ptr<int32_t>();
-      } else {
+      } else if (kind == "l") {
         c.kind = avh::FmtCol::LIST;
         auto off = cpu_tensor(t[3], at::kLong, n + 1, "list offsets");
         const int64_t m = n ? off.data_ptr<int64_t>()[n] : 0;
         c.idx = cpu_tensor(t[2], at::kInt, m, "list").data_ptr<int32_t>();
+        c.off = off.data_ptr<int64_t>();
+      } else {  // ("lp", table, idx int32 [m], ints int64 [m], off int64 [n + 1])
+        c.kind = avh::FmtCol::PAIRS;
+        auto off = cpu_tensor(t[4], at::kLong, n + 1, "list offsets");
+        const int64_t m = n ? off.data_ptr<int64_t>()[n] : 0;
+        c.idx = cpu_tensor(t[2], at::kInt, m, "list").data_ptr<int32_t>();
+        c.iv = cpu_tensor(t[3], at::kLong, m, "pair list ints").data_ptr<int64_t>();
         c.off = off.data_ptr<int64_t>();
       }
     } else if (kind == "f") {

@@ -146,9 +146,11 @@ inline void put_rejoined(std::string& s, const char* p, int64_t n, const uint8_t
 
 std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads) {
   for (const auto& c : cols) {
-    if ((c.kind == FmtCol::STR || c.kind == FmtCol::LIST) && (!c.table || !c.idx))
+    if ((c.kind == FmtCol::STR || c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) && (!c.table || !c.idx))
       throw std::runtime_error("format_columns: string column without table / index");
-    if (c.kind == FmtCol::LIST && !c.off) throw std::runtime_error("format_columns: list column without offsets");
+    if ((c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) && !c.off)
+      throw std::runtime_error("format_columns: list column without offsets");
+    if (c.kind == FmtCol::PAIRS && !c.iv) throw std::runtime_error("format_columns: pair list without integers");
     if ((c.kind == FmtCol::RAW || c.kind == FmtCol::FIELD || c.kind == FmtCol::TAIL) && (!c.raddr || !c.rlen))
       throw std::runtime_error("format_columns: line column without spans");
   }
@@ -178,13 +180,17 @@ std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std
               s += c.lit;
               continue;
             }
-            if (c.kind == FmtCol::LIST) {
+            if (c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) {
               const int64_t a = c.off[r], b = c.off[r + 1];
               for (int64_t j = a; j < b; ++j) {
                 if (!first) s += delim;
                 first = false;
                 const int32_t k = c.idx[j];
                 if (k >= 0 && (size_t)k < c.table->size()) s += (*c.table)[(size_t)k];
+                if (c.kind == FmtCol::PAIRS) {
+                  s += delim;
+                  put_int(s, c.iv[j]);
+                }
               }
               continue;
             }

@@ -157,9 +157,11 @@ std::string format_rows(const std::vector<std::string>* prefix, const double* co
 // character of ``from_delims`` replaced by the output delimiter (no replacement when empty), FIELD =
 // field ``field`` of that line split at any character of ``from_delims`` (negative: from the end;
 // empty when the line is shorter), TAIL = the fields ``field``.. of the line re-joined with the
-// output delimiter.  An index outside the table writes an empty field.
+// output delimiter, PAIRS = LIST with an integer iv[j] after every string (``w,count,w,count``).
+// An index outside the table writes an empty field.
 struct FmtCol {
-  enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5, RAW = 6, FIELD = 7, TAIL = 8 };
+  enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5, RAW = 6, FIELD = 7, TAIL = 8,
+                    PAIRS = 9 };
   int kind = STR;
   const std::vector<std::string>* table = nullptr;
   const int32_t* idx = nullptr;

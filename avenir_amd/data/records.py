@@ -349,7 +349,8 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
     """Output text of ``n`` rows assembled column by column (native, multi-threaded):
     ``("s", table, idx)`` string-table lookups, ``("f", values, prec)`` numbers (prec < 0: ``%g``),
     ``("i", ints)``, ``("c", literal)``, ``("g", literal)`` glued on without a delimiter,
-    ``("l", table, idx, off)`` a variable-length list of table strings per row (CSR), and the raw
+    ``("l", table, idx, off)`` a variable-length list of table strings per row (CSR),
+    ``("lp", table, idx, ints, off)`` the same with an integer after every string, and the raw
     input line kinds of ``data/lines.LineSpans.column``: ``("r", ...)`` the line, ``("rf", ...)``
     one of its fields, ``("rt", ...)`` its fields from one on.  ``prec`` -2 writes Python's
     ``repr`` of the value.  Every row ends with a newline."""
@@ -388,6 +389,11 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
             tab, idx, off = c[1], c[2].tolist(), c[3].tolist()
             for r in range(n):
                 rows[r] += [tab[i] if 0 <= i < len(tab) else "" for i in idx[off[r]:off[r + 1]]]
+        elif k == "lp":
+            tab, idx, iv, off = c[1], c[2].tolist(), c[3].tolist(), c[4].tolist()
+            for r in range(n):
+                for j in range(off[r], off[r + 1]):
+                    rows[r] += [tab[idx[j]] if 0 <= idx[j] < len(tab) else "", str(int(iv[j]))]
         elif k in ("r", "rf", "rt"):
             import ctypes
             import re
@@ -490,6 +496,41 @@ def sorted_keys(rec: Records, codes: torch.Tensor, comm=None) -> tuple[torch.Ten
     pos = torch.full((max(1, V),), -1, dtype=torch.int64, device=dev)
     pos[keys] = torch.arange(keys.numel(), device=dev)
     return keys, pos[:V]
+
+
+def sorted_key_tuples(rec: Records, cols: list[torch.Tensor], comm=None):
+    """Composite keys of several dictionary-coded fields (``cols``: per field the codes of every
+    row, all rows valid) in the reference's reducer order — tuples of strings compared field by
+    field — over all ranks.  Returns (kpos int64 [n]: the global position of every row's key,
+    G: the number of distinct keys, key codes int64 [G, m] (host) in that order).  The field codes'
+    string ranks come from ONE device packed-key sort (``sorted_keys``); a key is the mixed-radix
+    number of its ranks, and the distinct keys of all ranks are one all-gather."""
+    dev = cols[0].device if cols else rec.device
+    m = len(cols)
+    n = cols[0].numel() if cols else 0
+    if m == 0:
+        return torch.zeros(n, dtype=torch.long, device=dev), 1, torch.zeros((1, 0), dtype=torch.long)
+    keys, pos = sorted_keys(rec, torch.cat([c.reshape(-1) for c in cols]), comm)
+    R = keys.numel() + 1
+    if R ** m >= (1 << 62):
+        raise ValueError("composite key space exceeds 2^62")
+    comp = torch.zeros(n, dtype=torch.long, device=dev)
+    for c in cols:
+        comp = comp * R + pos[c.long()]
+    loc = torch.unique(comp)
+    if comm is not None and comm.is_distributed:
+        cdev = comm.device if comm.pg_backend == "nccl" else torch.device("cpu")
+        allc = torch.unique(comm.all_gather_v(loc.to(cdev))).to(dev)
+    else:
+        allc = loc
+    kpos = torch.searchsorted(allc, comp)
+    digits, rem = [], allc.clone()
+    for _ in range(m):
+        digits.append(rem % R)
+        rem = rem // R
+    table = torch.stack([keys[d] for d in reversed(digits)], 1).cpu() if allc.numel() else \
+        torch.zeros((0, m), dtype=torch.long)
+    return kpos, int(allc.numel()), table
 
 
 def segment_rank(first: torch.Tensor) -> torch.Tensor:

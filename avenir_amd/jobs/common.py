@@ -27,6 +27,10 @@ import torch
 
 JOBS: dict[str, tuple[Callable, str]] = {}
 
+#: input bytes this process read through ``JobContext.records`` (per-rank byte-range evidence for
+#: the data-parallel tests; a Hadoop-style counter)
+IO_STATS = {"bytes_read": 0}
+
 
 def job(name: str, help_: str, aliases: Sequence[str] = ()):
     def deco(fn):
@@ -154,7 +158,9 @@ class JobContext:
             if lit is None or len(lit) != 1:
                 raise SystemExit(f"native record input needs a one-character field delimiter, got {self.delim_in!r}")
             kw["delims"] = lit
-        return read_records(path or self.args.input, comm=self.comm, device=self.device, shard=shard, **kw)
+        rec = read_records(path or self.args.input, comm=self.comm, device=self.device, shard=shard, **kw)
+        IO_STATS["bytes_read"] += int(rec.stats.get("bytes", 0))
+        return rec
 
     def line_base(self, n_local: int) -> int:
         """Global index of this rank's first line (exclusive scan of the line counts)."""

@@ -643,17 +643,55 @@ def event_time(args):
 @job("sequenceGenerator", "group records by key, ordered by a sequence field (S/sequence/SequenceGenerator.scala)")
 def seq_gen(args):
     """Output ``key..,v..,v..,...`` (the value fields of every record of the key in sequence
-    order); the ordering is the device segmented sort of ``models/markov.sequence_generator``."""
-    from ..models.markov import sequence_generator
+    order, ties in input order), keys in string order.  Native path: each rank reads its byte
+    range; records move to the rank owning their key (one all-to-all; keys in string order cut
+    into contiguous blocks, so the rank-ordered part files are the global order); one device sort
+    by (key, sequence) per rank and the native formatter."""
+    from ..data.table import _literal
     ctx = JobContext(args, app="sequenceGenerator")
     kords = ctx.get_int_list("id.field.ordinals")
     vords = ctx.get_int_list("val.field.ordinals")
     sf = ctx.get_int("seq.field")
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _seq_gen_rows(ctx, kords, vords, sf)
+    from ..data.records import format_lines, owner_of, shuffle, sorted_key_tuples
+    from ..data.table import shard_range
+    comm = ctx.comm
+    top = max(list(kords) + list(vords) + [sf]) + 1
+    modes = "".join("n" if i == sf else ("d" if (i in kords or i in vords) else "x") for i in range(top))
+    # the sequence field doubles as a value field: its number AND its dictionary string
+    rec = ctx.records(modes=modes, tail_mode="x", numeric=True)
+    if sf in vords:
+        rec2 = ctx.records(modes="".join("d" if i == sf else "x" for i in range(top)), tail_mode="x")
+        vcols = [rec2.field(o).long() if o == sf else rec.field(o).long() for o in vords]
+    else:
+        vcols = [rec.field(o).long() for o in vords]
+    kpos, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], comm)
+    seqv = torch.trunc(rec.field(sf, numeric=True)).long()
+    owner = owner_of(kpos, G, comm.world) if comm.is_distributed else torch.zeros_like(kpos)
+    cols = shuffle(comm, owner, [kpos, seqv] + vcols)
+    kp, sv, V = cols[0], cols[1], torch.stack(cols[2:], 1) if vcols else None
+    o = torch.argsort(sv, stable=True)
+    o = o[torch.argsort(kp[o], stable=True)]
+    kp = kp[o]
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    cnt = torch.bincount(kp - a, minlength=b - a) * len(vords) if b > a else torch.zeros(0, dtype=torch.long)
+    off = torch.cat([torch.zeros(1, dtype=torch.long, device=cnt.device), torch.cumsum(cnt, 0)]).cpu()
+    vals = V[o].reshape(-1).int().cpu() if V is not None else torch.zeros(0, dtype=torch.int32)
+    out = [("s", rec.vocab, ktab[a:b, j].int().contiguous()) for j in range(len(kords))]
+    out.append(("l", rec.vocab, vals, off))
+    ctx.emit_text(format_lines(out, b - a, ctx.delim_out))
+
+
+def _seq_gen_rows(ctx, kords, vords, sf):
+    """Regex delimiters: the split-row path."""
+    from ..models.markov import sequence_generator
     rows = ctx.rows(shard=False)
     keys = sorted({tuple(r[o] for o in kords) for r in rows})
     ki = {k: i for i, k in enumerate(keys)}
-    kk = torch.tensor([ki[tuple(r[o] for o in kords)] for r in rows])
-    sv = torch.tensor([int(float(r[sf])) for r in rows])
+    kk = torch.tensor([ki[tuple(r[o] for o in kords)] for r in rows], dtype=torch.long)
+    sv = torch.tensor([int(float(r[sf])) for r in rows], dtype=torch.long)
     ks, order, starts = sequence_generator(kk, sv, torch.arange(len(rows)))
     d = ctx.delim_out
     bounds = starts.tolist() + [len(rows)]
@@ -670,17 +708,61 @@ def seq_gen(args):
 @job("timeDelayEmbeddingModel", "histogram of symbol windows per key (S/sequence/TimeDelayEmbeddingModel.scala, appName markovChainPredictor)",
      aliases=("markovChainPredictor",))
 def time_delay(args):
-    """Per key, records ordered by ``seq.fieldOrd``; every full window of ``window.size`` symbols of
-    ``attr.ordinal`` is counted (device n-gram count); output ``key..,w1:w2:w3,count,...``."""
+    """Per key, records ordered by ``seq.fieldOrd`` (ties in input order); every full window of
+    ``window.size`` symbols of ``attr.ordinal`` is counted; output ``key..,w1:w2:w3,count,...``
+    (windows in string order), keys in string order.  Native path: byte-range reads, one
+    all-to-all to the key owners, windows gathered from the device sort and counted by one unique
+    over (key, window) codes."""
+    from ..data.table import _literal
     ctx = JobContext(args, app="markovChainPredictor")
     kords = ctx.get_int_list("id.fieldOrdinals", [])
     ao = ctx.get_int("attr.ordinal")
     so = ctx.get_int("seq.fieldOrd")
     w = ctx.get_int("window.size", 3)
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _time_delay_rows(ctx, kords, ao, so, w)
+    from ..data.records import format_lines, owner_of, segment_rank, shuffle, sorted_key_tuples
+    from ..data.table import shard_range
+    comm = ctx.comm
+    top = max(list(kords) + [ao, so]) + 1
+    modes = "".join("n" if i == so else ("d" if (i in kords or i == ao) else "x") for i in range(top))
+    rec = ctx.records(modes=modes, tail_mode="x", numeric=True)
+    kpos, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], comm)
+    owner = owner_of(kpos, G, comm.world) if comm.is_distributed else torch.zeros_like(kpos)
+    kp, sq, sym = shuffle(comm, owner, [kpos, rec.field(so, numeric=True), rec.field(ao).long()])
+    o = torch.argsort(sq, stable=True)
+    o = o[torch.argsort(kp[o], stable=True)]
+    kp, sym = kp[o], sym[o]
+    first = torch.ones_like(kp, dtype=torch.bool)
+    first[1:] = kp[1:] != kp[:-1]
+    end = torch.nonzero(segment_rank(first) >= w - 1).view(-1)
+    win = sym[end.view(-1, 1) - (w - 1) + torch.arange(w, device=sym.device).view(1, -1)]   # [n_win, w]
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    uwin, winv = torch.unique(win, dim=0, return_inverse=True) if win.numel() else (win, win[:, 0])
+    # window strings (few distinct): their string order decides the output order inside a key
+    wstr = [":".join(rec.vocab[c] for c in row) for row in uwin.cpu().tolist()]
+    wrank = torch.empty(len(wstr), dtype=torch.long)
+    wrank[torch.tensor(sorted(range(len(wstr)), key=wstr.__getitem__), dtype=torch.long)] = \
+        torch.arange(len(wstr), dtype=torch.long)
+    wr = wrank.to(win.device)[winv] if win.numel() else winv
+    key = (kp[end] - a) * max(1, len(wstr)) + wr
+    uk, cnt = torch.unique(key, return_counts=True)
+    kk, ww = uk // max(1, len(wstr)), uk % max(1, len(wstr))
+    per = torch.bincount(kk, minlength=b - a) if b > a else torch.zeros(0, dtype=torch.long)
+    off = torch.cat([torch.zeros(1, dtype=torch.long, device=per.device), torch.cumsum(per, 0)]).cpu()
+    wtab = sorted(wstr)
+    out = [("s", rec.vocab, ktab[a:b, j].int().contiguous()) for j in range(len(kords))]
+    out.append(("lp", wtab, ww.int().cpu(), cnt.long().cpu(), off))
+    ctx.emit_text(format_lines(out, b - a, ctx.delim_out))
+
+
+def _time_delay_rows(ctx, kords, ao, so, w):
+    """Regex delimiters: the split-row path."""
     g = defaultdict(list)
     for r in ctx.rows(shard=False):
         g[tuple(r[o] for o in kords)].append((float(r[so]), r[ao]))
-    seqs = [(k, [s for _, s in sorted(v)]) for k, v in sorted(g.items())]
+    seqs = [(k, [s for _, s in sorted(v, key=lambda e: e[0])]) for k, v in sorted(g.items())]
     if ctx.comm.is_distributed:
         from ..data.table import shard_range
         a, b = shard_range(len(seqs), ctx.comm.rank, ctx.comm.world)
@@ -689,20 +771,7 @@ def time_delay(args):
     out = []
     for k, s in seqs:
         c: dict[str, int] = defaultdict(int)
-        if len(s) >= w:
-            vocab = {t: i for i, t in enumerate(sorted(set(s)))}
-            inv = sorted(vocab, key=vocab.get)
-            T = torch.tensor([vocab[t] for t in s], dtype=torch.long, device=ctx.device)
-            win = T.unfold(0, w, 1)
-            key = torch.zeros(win.shape[0], dtype=torch.long, device=ctx.device)
-            for j in range(w):
-                key = key * len(vocab) + win[:, j]
-            u, cnt = torch.unique(key, return_counts=True)
-            for kk, cc in zip(u.cpu().tolist(), cnt.cpu().tolist()):
-                toks = []
-                for _ in range(w):
-                    toks.append(inv[kk % len(vocab)])
-                    kk //= len(vocab)
-                c[":".join(reversed(toks))] = cc
+        for i in range(len(s) - w + 1):
+            c[":".join(s[i:i + w])] += 1
         out.append(d.join(list(k) + [f"{x}{d}{c[x]}" for x in sorted(c)]))
     ctx.emit(out)

@@ -864,8 +864,44 @@ def _record_similarity_rows(ctx, args):
 
 @job("groupedRecordSimilarity", "pairwise distances within each group (S/similarity/GroupedRecordSimilarity.scala)")
 def grouped_similarity(args):
-    from ..ops.distance import pairwise
+    """Distances of every pair of records (i < j in input order) inside each group of
+    ``group.field.ordinals``; output ``key..,id_i,id_j,dist`` by group in key order.  Native path:
+    each rank reads its byte range; records move to the rank owning their group (one all-to-all,
+    groups in string order cut into contiguous blocks); every rank runs the batched in-group
+    distance launches of ``GroupedRecordSimilarity`` on its groups and writes them."""
+    from ..data.table import _literal
     ctx = JobContext(args, app="groupedRecordSimilarity")
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _grouped_similarity_rows(ctx)
+    from ..data.records import format_lines, owner_of, shuffle, sorted_key_tuples
+    from ..data.table import shard_range
+    from ..models.similarity import GroupedRecordSimilarity
+    kords = ctx.get_int_list("group.field.ordinals", None) or ctx.get_int_list("key.field.ordinals")
+    ords = ctx.get_int_list("attr.ordinals")
+    idc = ctx.get_int("id.ordinal", 0)
+    prec = ctx.get_int("output.precision", 3)
+    comm = ctx.comm
+    top = max(list(kords) + list(ords) + [idc]) + 1
+    modes = "".join("d" if (i in kords or i == idc) else ("n" if i in ords else "x") for i in range(top))
+    rec = ctx.records(modes=modes, tail_mode="x", numeric=True)
+    kpos, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], comm)
+    owner = owner_of(kpos, G, comm.world) if comm.is_distributed else torch.zeros_like(kpos)
+    cols = shuffle(comm, owner, [kpos, rec.field(idc).long()] + [rec.field(o, numeric=True) for o in ords])
+    kp, ids = cols[0], cols[1]
+    X = torch.stack(cols[2:], 1).float().to(ctx.device) if ords else torch.zeros((kp.numel(), 0), device=ctx.device)
+    a, _ = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    ii, jj, dd = GroupedRecordSimilarity().pairs(X, (kp - a).to(ctx.device))
+    ii, jj = ii.cpu(), jj.cpu()
+    kp_c, ids_c = kp.cpu(), ids.cpu().int()
+    out = [("s", rec.vocab, ktab[kp_c[ii], j].int().contiguous()) for j in range(len(kords))]
+    out += [("s", rec.vocab, ids_c[ii]), ("s", rec.vocab, ids_c[jj]), ("f", dd.double().cpu(), prec)]
+    ctx.emit_text(format_lines(out, int(ii.numel()), ctx.delim_out))
+
+
+def _grouped_similarity_rows(ctx):
+    """Regex delimiters: the split-row path (every rank reads the input, handles a block of groups)."""
+    from ..ops.distance import pairwise  # noqa: F401
     kords = ctx.get_int_list("group.field.ordinals", None) or ctx.get_int_list("key.field.ordinals")
     ords = ctx.get_int_list("attr.ordinals")
     idc = ctx.get_int("id.ordinal", 0)
@@ -878,7 +914,6 @@ def grouped_similarity(args):
     a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
     d = ctx.delim_out
     out = []
-    # all of this rank's groups in one batched pass (GroupedRecordSimilarity.pairs)
     from ..models.similarity import GroupedRecordSimilarity
     mine = [(gi, r) for gi, k in enumerate(keys[a:b]) for r in g[k]]
     if mine:
@@ -894,10 +929,47 @@ def grouped_similarity(args):
 @job("nearestRecords", "per record the top-k nearest from pair distances, by count or distance (S/similarity/NearestRecords.scala)")
 def nearest_records(args):
     """Pair rows ``id1,id2,...,dist`` (both directions considered); per first record the nearest
-    ``neighbor.count`` (or all within ``neighbor.dist.threshold``), output ``id,n1,n2,...``."""
+    ``neighbor.count`` (or all within ``neighbor.dist.threshold``), output ``id,n1,n2,...`` in id
+    order, neighbours by distance then id.  Native path: each rank reads its byte range, both
+    directions of every pair go to the rank owning the record (all-to-all), one device sort by
+    (record, distance, neighbour) per rank."""
+    from ..data.table import _literal
     ctx = JobContext(args, app="nearestRecords")
+    lit = _literal(ctx.delim_in)
     k = ctx.get_int("neighbor.count", 5)
     thr = ctx.get_float("neighbor.dist.threshold", math.inf)
+    if lit is None or len(lit) != 1:
+        return _nearest_records_rows(ctx, k, thr)
+    from ..data.records import format_lines, owner_of, segment_rank, shuffle, sorted_keys
+    from ..data.table import shard_range
+    comm = ctx.comm
+    rec = ctx.records(modes="dd", tail_mode="x", numeric=True, last_mode="n")
+    ok = rec.lens() >= 3
+    a_, b_, dist = rec.field(0)[ok].long(), rec.field(1)[ok].long(), rec.field(-1, numeric=True)[ok]
+    x = torch.cat([a_, b_])
+    y = torch.cat([b_, a_])
+    dd = torch.cat([dist, dist])
+    keys, pos = sorted_keys(rec, x, comm)
+    G = keys.numel()
+    xp, yp = pos[x], pos[y]
+    owner = owner_of(xp, G, comm.world) if comm.is_distributed else torch.zeros_like(xp)
+    xp, yp, dd = shuffle(comm, owner, [xp, yp, dd])
+    o = torch.argsort(yp, stable=True)
+    o = o[torch.argsort(dd[o], stable=True)]
+    o = o[torch.argsort(xp[o], stable=True)]
+    xp, yp, dd = xp[o], yp[o], dd[o]
+    first = torch.ones_like(xp, dtype=torch.bool)
+    first[1:] = xp[1:] != xp[:-1]
+    keep = (segment_rank(first) < k) & (dd <= thr)
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    cnt = torch.bincount((xp - a)[keep], minlength=b - a) if b > a else torch.zeros(0, dtype=torch.long)
+    off = torch.cat([torch.zeros(1, dtype=torch.long, device=cnt.device), torch.cumsum(cnt, 0)]).cpu()
+    kc = keys.cpu()
+    cols = [("s", rec.vocab, kc[a:b].int().contiguous()), ("l", rec.vocab, kc[yp[keep].cpu()].int(), off)]
+    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
+
+
+def _nearest_records_rows(ctx, k, thr):
     nb = defaultdict(list)
     for r in ctx.rows(shard=False):
         dd = float(r[-1])

@@ -1,0 +1,127 @@
+"""Data-parallel execution of the formerly rank-replicated jobs.
+
+Every job here reads only its rank's byte range of the input (checked through
+``jobs.common.IO_STATS``) and produces the same output at world 1, 2 and 4 (gloo ranks): the
+all-pairs similarity job through a ring of record blocks (``Comm.ring_iter``), the keyed jobs
+through one all-to-all shuffle by key (``data/records.shuffle``).  The native path also equals the
+split-row path (the same delimiter written as a regex)."""
+from __future__ import annotations
+
+import os
+import random
+from pathlib import Path
+
+import pytest
+
+from avenir_amd.cli import main
+from avenir_amd.jobs import common as JC
+
+from _dist import run_world
+
+
+def _lines(p):
+    p = Path(p)
+    if p.is_dir():
+        return [l for f in sorted(p.iterdir()) if f.is_file() for l in f.read_text().splitlines() if l.strip()]
+    return [l for l in p.read_text().splitlines() if l.strip()]
+
+
+def _points(path, n, seed, groups=None):
+    rnd = random.Random(seed)
+    with open(path, "w") as f:
+        for i in range(n):
+            g = f"g{rnd.randrange(groups)}," if groups else ""
+            f.write(f"{g}p{i:05d},{rnd.gauss(0, 1):.4f},{rnd.gauss(0, 1):.4f},{rnd.randint(0, 9)}\n")
+
+
+def _setup(tmp: Path, name: str):
+    """(argv without -o / -c, HOCON block text, input path)."""
+    if name.startswith("rs"):
+        data = tmp / "pts.csv"
+        _points(data, 700, 1)
+        argv = ["recordSimilarity", "-i", data]
+        if name == "rs_two":
+            other = tmp / "other.csv"
+            _points(other, 300, 2)
+            argv += ["--train", other]
+        extra = "  output.record = true\n" if name == "rs_rec" else ""
+        thr = "  dist.threshold = 150\n" if name != "rs_all" else ""
+        return argv, ("recordSimilarity {\n  attr.ordinals = [1,2,3]\n  id.ordinal = 0\n  distance.scale = 1000\n"
+                      + thr + extra + "}\n"), data
+    rnd = random.Random(sum(map(ord, name)))
+    if name == "gr":
+        data = tmp / "grp.csv"
+        _points(data, 900, 3, groups=23)
+        return (["groupedRecordSimilarity", "-i", data],
+                "groupedRecordSimilarity {\n  group.field.ordinals = [0]\n  attr.ordinals = [2,3]\n  id.ordinal = 1\n}\n",
+                data)
+    if name == "nr":
+        data = tmp / "pairs.csv"
+        with open(data, "w") as f:
+            for _ in range(3000):
+                a, b = rnd.randrange(400), rnd.randrange(400)
+                f.write(f"e{a},e{b},{rnd.randint(0, 50)}\n")
+        return (["nearestRecords", "-i", data],
+                "nearestRecords {\n  neighbor.count = 3\n  neighbor.dist.threshold = 40\n}\n", data)
+    if name == "sg":
+        data = tmp / "ev.csv"
+        with open(data, "w") as f:
+            for i in range(2500):
+                f.write(f"k{rnd.randrange(150)},{rnd.choice('ab')},{rnd.randint(0, 60)},v{i % 7},w{i % 5}\n")
+        return (["sequenceGenerator", "-i", data],
+                "sequenceGenerator {\n  id.field.ordinals = [0,1]\n  val.field.ordinals = [3,4]\n  seq.field = 2\n}\n",
+                data)
+    if name == "td":
+        data = tmp / "sym.csv"
+        with open(data, "w") as f:
+            for i in range(3000):
+                f.write(f"k{rnd.randrange(60)},{i * 7 % 1000},{rnd.choice(['L', 'M', 'H', 'HH'])}\n")
+        return (["timeDelayEmbeddingModel", "-i", data],
+                "markovChainPredictor {\n  id.fieldOrdinals = [0]\n  attr.ordinal = 2\n  seq.fieldOrd = 1\n"
+                "  window.size = 3\n}\n", data)
+    raise KeyError(name)
+
+
+def _conf(tmp, text, regex=False):
+    p = tmp / f"job{'_re' if regex else ''}.conf"
+    body = text.replace("{\n", "{\n  field.delim.in = \"" + ("[,]" if regex else ",") + "\"\n", 1)
+    p.write_text(body)
+    return p
+
+
+CASES = ["rs", "rs_all", "rs_two", "rs_rec", "gr", "nr", "sg", "td"]
+
+
+def _app(argv):
+    return ["--app", "markovChainPredictor" if argv[0] == "timeDelayEmbeddingModel" else argv[0]]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_native_equals_row_path(tmp_path, name):
+    argv, text, _ = _setup(tmp_path, name)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "n.txt"), "-c", str(_conf(tmp_path, text))]
+                + _app(argv) + ["--device", "cpu"]) == 0
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "r.txt"), "-c", str(_conf(tmp_path, text, True))]
+                + _app(argv) + ["--device", "cpu"]) == 0
+    got, ref = _lines(tmp_path / "n.txt"), _lines(tmp_path / "r.txt")
+    assert got and got == ref
+
+
+def _world(rank, world, argv, out, cfg):
+    JC.IO_STATS["bytes_read"] = 0
+    assert main(argv + ["-o", out, "-c", cfg, "--device", "cpu"]) == 0
+    return JC.IO_STATS["bytes_read"]
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("world", [2, 4])
+def test_world_invariant_and_byte_range_reads(tmp_path, name, world):
+    argv, text, data = _setup(tmp_path, name)
+    cfg = _conf(tmp_path, text)
+    args = [str(a) for a in argv] + _app(argv)
+    assert main(args + ["-o", str(tmp_path / "w1.txt"), "-c", str(cfg), "--device", "cpu"]) == 0
+    read = run_world(_world, world, args, str(tmp_path / f"w{world}.txt"), str(cfg), timeout=300)
+    assert _lines(tmp_path / f"w{world}.txt") == _lines(tmp_path / "w1.txt")
+    total = os.path.getsize(data) + (os.path.getsize(argv[argv.index("--train") + 1]) if "--train" in argv else 0)
+    assert sum(read) == total                      # every input byte read exactly once
+    assert max(read) <= total / world * 1.1 + 200  # each rank about its share
