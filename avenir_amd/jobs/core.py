@@ -632,20 +632,53 @@ def kmeans(args):
 
 @job("multiArmBandit", "batch bandit per group (S/reinforce/MultiArmBandit.scala): rewards in, actions out")
 def mab(args):
+    """Rows ``group,action,reward``; per group (string order) the learner's next action(s), output
+    ``group,action..``.  Native path: each rank reads its byte range and sends every reward row to
+    the rank owning its group (one all-to-all, input order kept); the bank spans ALL groups on
+    every rank, so the selection's Philox streams are keyed by the global group index and the
+    output does not depend on the world size; each rank writes its block of groups."""
+    from ..data.table import _literal
     from ..models.bandit import BanditBank
     ctx = JobContext(args, app="multiArmBandit")
     actions = ctx.get_list("action.list")
-    rows = ctx.rows(shard=False)                # group, action, reward
-    groups = sorted({r[0] for r in rows})
-    bank = BanditBank(ctx.get_str("learner.type", "upperConfidenceBoundOne"), actions, len(groups),
-                      dict(ctx.cfg.values), device=ctx.device)
-    if rows:
-        gi = torch.tensor([groups.index(r[0]) for r in rows])
-        ai = torch.tensor([actions.index(r[1]) for r in rows])
-        rw = torch.tensor([float(r[2]) for r in rows])
-        bank.set_rewards(gi, ai, rw)
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        rows = ctx.rows(shard=False)                # group, action, reward
+        groups = sorted({r[0] for r in rows})
+        bank = BanditBank(ctx.get_str("learner.type", "upperConfidenceBoundOne"), actions, len(groups),
+                          dict(ctx.cfg.values), device=ctx.device)
+        if rows:
+            gi = {g: i for i, g in enumerate(groups)}
+            bank.set_rewards(torch.tensor([gi[r[0]] for r in rows]), torch.tensor([actions.index(r[1]) for r in rows]),
+                             torch.tensor([float(r[2]) for r in rows]))
+        acts = bank.next_actions().cpu()
+        from ..data.table import shard_range
+        a, b = shard_range(len(groups), ctx.comm.rank, ctx.comm.world) if ctx.comm.is_distributed else (0, len(groups))
+        ctx.emit([f"{g}," + ",".join(actions[x] for x in acts[i].tolist()) for i, g in enumerate(groups) if a <= i < b])
+        return
+    from ..data.records import format_lines, owner_of, shuffle, sorted_keys
+    from ..data.table import shard_range
+    comm = ctx.comm
+    rec = ctx.records(modes="ddn", tail_mode="x", numeric=True)
+    g_code = rec.field(0)
+    act = rec.map_codes(rec.field(1), actions).long()
+    if bool((act < 0).any()):
+        raise SystemExit("multiArmBandit: an action outside action.list")
+    keys, pos = sorted_keys(rec, g_code, comm)
+    G = keys.numel()
+    gp = pos[g_code.long()]
+    owner = owner_of(gp, G, comm.world) if comm.is_distributed else torch.zeros_like(gp)
+    gp, act, rw = shuffle(comm, owner, [gp, act, rec.field(2, numeric=True)])
+    bank = BanditBank(ctx.get_str("learner.type", "upperConfidenceBoundOne"), actions, G, dict(ctx.cfg.values),
+                      device=ctx.device)
+    if gp.numel():
+        bank.set_rewards(gp, act, rw)
     acts = bank.next_actions().cpu()
-    ctx.emit_root([f"{g}," + ",".join(actions[a] for a in acts[i].tolist()) for i, g in enumerate(groups)])
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    nb = acts.shape[1]
+    cols = [("s", rec.vocab, keys[a:b].int().cpu()),
+            ("l", list(actions), acts[a:b].reshape(-1).int(), torch.arange(0, (b - a) * nb + 1, nb, dtype=torch.long))]
+    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
 
 
 # ================================================================================================

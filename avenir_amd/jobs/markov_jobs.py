@@ -372,20 +372,52 @@ def ngram_counts(ctx: JobContext, seqs, L: int, streaming: bool = False, root: s
 # ================================================================================================
 @job("candidateGenerationWithSelfJoin", "GSP k+1 candidate sequences by self-join on the (k-1)-overlap (J/sequence/CandidateGenerationWithSelfJoin.java, cgs.*)")
 def cgs(args):
-    """Rows hold a frequent k-sequence in their first ``cgs.item.set.length`` fields.  The join is
-    the device op of ``ops/sequence_ops.gsp_join`` (sort of the (k-1)-prefix ids + segmented
-    expansion kernel, K18); with several ranks each joins its shard of left sequences against the
-    full (all-gathered) right set, and the candidates are gathered to rank 0.  Every ordered pair
-    (a, b) with a[1:] == b[:-1] yields a + b[-1] (incl. a == b), which fixes two reference bugs
+    """Rows hold a frequent k-sequence in their first ``cgs.item.set.length`` fields.  Every ordered
+    pair (a, b) with a[1:] == b[:-1] yields a + b[-1] (incl. a == b), which fixes two reference bugs
     (pairs inside one hash bucket are never joined; the reverse join appends a token of the wrong
-    sequence, :243-276)."""
-    from ..models.markov import gsp_candidates_device
+    sequence, :243-276).  Native path: each rank reads its byte range; the (small) set of distinct
+    k-sequences is all-gathered as dictionary codes, ordered by the tokens' string ranks, and every
+    rank joins its block of left sequences against all of them on the device (``SO.gsp_join``,
+    K18); rank 0 writes the sorted union."""
+    from ..data.table import _literal
     ctx = JobContext(args, "cgs.")
     k = ctx.get_int("item.set.length")
-    seqs = [tuple(r[:k]) for r in ctx.rows(shard=False) if len(r) >= k]
-    cands = gsp_candidates_device(seqs, device=ctx.device, comm=ctx.comm)
-    d = ctx.delim_out
-    ctx.emit_root([d.join(c) for c in cands])
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        from ..models.markov import gsp_candidates_device
+        seqs = [tuple(r[:k]) for r in ctx.rows(shard=False) if len(r) >= k]
+        cands = gsp_candidates_device(seqs, device=ctx.device, comm=ctx.comm)
+        ctx.emit_root([ctx.delim_out.join(c) for c in cands])
+        return
+    from ..data.records import format_lines, sorted_keys
+    from ..data.table import shard_range
+    from ..ops import sequence_ops as SO
+    comm = ctx.comm
+    rec = ctx.records(modes="d" * k, tail_mode="x")
+    ok = rec.lens() >= k
+    S = torch.stack([rec.field(j)[ok].long() for j in range(k)], 1) if k else torch.zeros((0, 0), dtype=torch.long)
+    S = torch.unique(S, dim=0) if S.shape[0] else S
+    if comm.is_distributed:
+        cdev = comm.device if comm.pg_backend == "nccl" else torch.device("cpu")
+        S = comm.all_gather_v(S.to(cdev)).to(rec.device)
+        S = torch.unique(S, dim=0) if S.shape[0] else S
+    if S.shape[0] == 0:
+        ctx.emit_root_text(b"")
+        return
+    keys, pos = sorted_keys(rec, S.reshape(-1))          # token code -> string rank (every rank alike)
+    R = pos[S].int()
+    R = torch.unique(R, dim=0)                           # lexicographic = tuple-of-strings order
+    lo, hi = shard_range(R.shape[0], comm.rank, comm.world) if comm.is_distributed else (0, R.shape[0])
+    C = SO.gsp_join(R.to(ctx.device).contiguous(), lo, hi)
+    if comm.is_distributed:
+        cdev = comm.device if comm.pg_backend == "nccl" else torch.device("cpu")
+        C = comm.all_gather_v(C.to(cdev))
+    if not ctx.is_root:
+        return
+    C = torch.unique(C.cpu().long(), dim=0) if C.numel() else C.cpu().long().view(0, k + 1)
+    kc = keys.cpu()
+    cols = [("s", rec.vocab, kc[C[:, j]].int().contiguous()) for j in range(k + 1)]
+    ctx.emit_root_text(format_lines(cols, int(C.shape[0]), ctx.delim_out))
 
 
 @job("sequencePositionalCluster", "time-bounded event locality score over a sliding window (J/sequence/SequencePositionalCluster.java)")
@@ -588,20 +620,70 @@ def cont_time_stats(args):
 # ================================================================================================
 @job("dotMatrixMatching", "all-pairs dot-matrix window-match similarity of sequences (S/sequence/DotMatrixMatching.scala)")
 def dot_matrix(args):
-    """Rows ``id,tok,tok,...``; every pair (i < j) gets the window-match score of the K dot-matrix
-    kernel (sequences vs sequences, no bucket-pair replication); output ``id1,id2,score``."""
-    from ..models.markov import dot_matrix_similarity
+    """Rows ``id,tok,tok,...``; every pair (i < j) gets the window-match score of the K19
+    dot-matrix kernel; output ``id1,id2,score`` in (i, j) order.  Native path: each rank reads its
+    byte range; its sequences stay put while the other ranks' blocks (padded token-code rows + id
+    codes + global row base) travel around the ring (``Comm.ring_iter``, the next transfer posted
+    before the current block's kernel runs) — instead of the reference's bucket-pair replication
+    (S/sequence/DotMatrixMatching.scala:76-100)."""
+    from ..data.table import _literal
     ctx = JobContext(args, app="dotMatrixMatching")
     skip = ctx.get_int("skip.field.count", 1)
     w = ctx.get_int("window.size", 3)
     prec = ctx.get_int("output.precision", 3)
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _dot_matrix_rows(ctx, skip, w, prec)
+    from ..data.records import format_lines
+    from ..models.markov import dot_matrix_similarity
+    comm = ctx.comm
+    rec = ctx.records(modes="d" + "x" * max(0, skip - 1))
+    X, _ = rec.padded(start=skip, dtype=torch.long, min_len=w)
+    Lm = torch.tensor([X.shape[1]], dtype=torch.long)
+    if comm.is_distributed:
+        comm.all_reduce(Lm, "max")
+    L = int(Lm)
+    if X.shape[1] < L:
+        X = torch.cat([X, torch.full((X.shape[0], L - X.shape[1]), -1, dtype=X.dtype, device=X.device)], 1)
+    ids = rec.field(0).long()
+    base = rec.line_base
+    cdev = comm.device if (comm.is_distributed and comm.pg_backend == "nccl") else torch.device("cpu")
+    payload = [X.to(cdev), ids.to(cdev), torch.tensor([base], dtype=torch.long, device=cdev)]
+    dev = ctx.device
+    A = X.to(dev)
+    I, J, Sv, Jid = [], [], [], []
+    for _owner, (Bx, bid, bb) in comm.ring_iter(payload):
+        b0 = int(bb.cpu()[0]) if bb.numel() else 0
+        if Bx.shape[0] == 0 or A.shape[0] == 0:
+            continue
+        Sm = dot_matrix_similarity(A, Bx.to(dev), w)
+        keep = (torch.arange(b0, b0 + Bx.shape[0], device=Sm.device).view(1, -1)
+                > torch.arange(base, base + A.shape[0], device=Sm.device).view(-1, 1))
+        qi, jj = torch.nonzero(keep, as_tuple=True)
+        I.append(qi)
+        J.append(jj + b0)
+        Sv.append(Sm[qi, jj])
+        Jid.append(bid.to(Sm.device)[jj])
+    if I:
+        I, J, Sv, Jid = torch.cat(I), torch.cat(J), torch.cat(Sv), torch.cat(Jid)
+        o = torch.argsort(I * (1 << 40) + J)
+        I, Sv, Jid = I[o], Sv[o], Jid[o]
+    else:
+        I = Jid = torch.zeros(0, dtype=torch.long)
+        Sv = torch.zeros(0, dtype=torch.float64)
+    cols = [("s", rec.vocab, ids.to(I.device)[I].int().cpu()), ("s", rec.vocab, Jid.int().cpu()),
+            ("f", Sv.double().cpu(), prec)]
+    ctx.emit_text(format_lines(cols, int(I.numel()), ctx.delim_out))
+
+
+def _dot_matrix_rows(ctx, skip, w, prec):
+    """Regex delimiters: the split-row path (every rank reads the input, scores a block of rows)."""
+    from ..models.markov import dot_matrix_similarity
     rows = ctx.rows(shard=False)
     vocab = {}
     L = max([len(r) - skip for r in rows] + [w])
-    X = torch.full((len(rows), L), -1, dtype=torch.long)
-    for i, r in enumerate(rows):
-        X[i, : len(r) - skip] = torch.tensor([vocab.setdefault(t, len(vocab)) for t in r[skip:]], dtype=torch.long)
-    # each rank scores its block of query rows against all rows
+    X = torch.tensor([[vocab.setdefault(t, len(vocab)) for t in r[skip:]] + [-1] * (L - len(r) + skip) for r in rows],
+                     dtype=torch.long).view(len(rows), L)
     from ..data.table import shard_range
     a, b = shard_range(len(rows), ctx.comm.rank, ctx.comm.world)
     Sm = dot_matrix_similarity(X[a:b].to(ctx.device), X.to(ctx.device), w).cpu()

@@ -108,28 +108,24 @@ def kmeanspp(args):
     """Records ``key..,x1..xD`` grouped by ``id.fieldOrdinals``; for every group and every k of
     ``num.clusters`` a D^2-seeded k-means (``num.clustGroup`` restarts, ``num.iter`` Lloyd steps) runs
     batched on the device; output per group: ``key..,k,sse`` lines and ``key..,knuckle,k``; the
-    centroids go to ``cluster.outputPath`` as ``key..,k,i,c..``."""
+    centroids go to ``cluster.outputPath`` as ``key..,k,i,c..``.  Native path: each rank reads its
+    byte range and sends every record to the rank owning its group (one all-to-all; groups in
+    string order cut into contiguous blocks), which fits its groups."""
+    from ..data.table import _literal
     from ..models.cluster import KMeans
     ctx = JobContext(args, app="kMeansPlusPlusCluster")
     kords = ctx.get_int_list("id.fieldOrdinals", []) if ctx.get_str("id.fieldOrdinals", "") else []
     ks = ctx.get_int_list("num.clusters")
     prec = ctx.get_int("output.precision", 3)
     attrs = ctx.get_int_list("attr.ordinals", None)
-    groups = defaultdict(list)
-    for r in ctx.rows(shard=False):
-        cols = attrs or [i for i in range(len(r)) if i not in kords]
-        groups[tuple(r[o] for o in kords)].append([float(r[c]) for c in cols])
-    keys = sorted(groups)
-    if ctx.comm.is_distributed:
-        from ..data.table import shard_range
-        a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
-        keys = keys[a:b]
+    lit = _literal(ctx.delim_in)
+    groups = _kmeanspp_groups_native(ctx, kords, attrs) if lit is not None and len(lit) == 1 else \
+        _kmeanspp_groups_rows(ctx, kords, attrs)
     d = ctx.delim_out
     out, cents = [], []
-    from ..parallel.comm import Comm
     local = _LocalComm()
-    for k in keys:
-        X = torch.tensor(groups[k], dtype=torch.float32, device=ctx.device)
+    for k, X in groups:
+        X = X.to(ctx.device)
         kk = [c for c in ks if c <= X.shape[0]]
         km = KMeans(kk, n_init=ctx.get_int("num.clustGroup", 10), max_iter=ctx.get_int("num.iter", 10),
                     init="k-means++", comm=local).fit(X)
@@ -144,6 +140,54 @@ def kmeanspp(args):
     cp = ctx.get_str("cluster.outputPath", None)
     if cp:
         ctx.emit(cents, cp)
+
+
+def _kmeanspp_groups_native(ctx, kords, attrs):
+    """This rank's groups [(key strings, X float32 [n, D])] in key order, records in input order."""
+    from ..data.records import owner_of, shuffle, sorted_key_tuples
+    from ..data.table import shard_range
+    comm = ctx.comm
+    top = max(list(kords) + list(attrs or []) + [0]) + 1
+    if attrs:
+        modes = "".join("d" if i in kords else ("n" if i in attrs else "x") for i in range(top))
+        rec = ctx.records(modes=modes, tail_mode="x", numeric=True)
+        cols = list(attrs)
+    else:   # every non-key field is a coordinate (all lines as wide as the first one)
+        modes = "".join("d" if i in kords else "n" for i in range(top))
+        rec = ctx.records(modes=modes, tail_mode="n", numeric=True)
+        w = torch.tensor([rec.width() if rec.n_lines else 0], dtype=torch.long)
+        if comm.is_distributed:
+            comm.all_reduce(w, "max")
+        cols = [i for i in range(int(w)) if i not in kords]
+    kpos, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], comm)
+    owner = owner_of(kpos, G, comm.world) if comm.is_distributed else torch.zeros_like(kpos)
+    sh = shuffle(comm, owner, [kpos] + [rec.field(c, numeric=True) for c in cols])
+    kp = sh[0].cpu()
+    X = torch.stack(sh[1:], 1).float().cpu() if cols else torch.zeros((kp.numel(), 0))
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    o = torch.argsort(kp, stable=True)
+    kp, X = kp[o], X[o]
+    cnt = torch.bincount(kp - a, minlength=b - a).tolist() if b > a else []
+    out, s = [], 0
+    for g, c in enumerate(cnt):
+        key = tuple(rec.vocab[int(x)] for x in ktab[a + g].tolist())
+        out.append((key, X[s:s + c]))
+        s += c
+    return out
+
+
+def _kmeanspp_groups_rows(ctx, kords, attrs):
+    """Regex delimiters: the split-row path."""
+    groups = defaultdict(list)
+    for r in ctx.rows(shard=False):
+        cols = attrs or [i for i in range(len(r)) if i not in kords]
+        groups[tuple(r[o] for o in kords)].append([float(r[c]) for c in cols])
+    keys = sorted(groups)
+    if ctx.comm.is_distributed:
+        from ..data.table import shard_range
+        a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
+        keys = keys[a:b]
+    return [(k, torch.tensor(groups[k], dtype=torch.float32)) for k in keys]
 
 
 class _LocalComm:

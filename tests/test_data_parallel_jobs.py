@@ -79,20 +79,57 @@ def _setup(tmp: Path, name: str):
         return (["timeDelayEmbeddingModel", "-i", data],
                 "markovChainPredictor {\n  id.fieldOrdinals = [0]\n  attr.ordinal = 2\n  seq.fieldOrd = 1\n"
                 "  window.size = 3\n}\n", data)
+    if name == "dm":
+        data = tmp / "seqs.csv"
+        with open(data, "w") as f:
+            for i in range(160):
+                f.write(f"s{i}," + ",".join(rnd.choice("ABCD") for _ in range(rnd.randint(2, 12))) + "\n")
+        return (["dotMatrixMatching", "-i", data],
+                "dotMatrixMatching {\n  window.size = 3\n  output.precision = 4\n}\n", data)
+    if name == "cgs":
+        data = tmp / "freq.csv"
+        with open(data, "w") as f:
+            for _ in range(2000):
+                f.write(",".join(rnd.choice(["a", "b", "cc", "d", "e"]) for _ in range(3)) + ",0.1\n")
+        return ["candidateGenerationWithSelfJoin", "-i", data], "cgs.item.set.length=3\n", data
+    if name == "kpp":
+        data = tmp / "km.csv"
+        with open(data, "w") as f:
+            for i in range(1200):
+                g = rnd.randrange(7)
+                c = rnd.randrange(3)
+                f.write(f"g{g},{c * 4 + rnd.gauss(0, .3):.4f},{c * 3 + rnd.gauss(0, .3):.4f}\n")
+        return (["kMeansPlusPlusCluster", "-i", data],
+                "kMeansPlusPlusCluster {\n  id.fieldOrdinals = [0]\n  num.clusters = [2,3,4]\n  num.iter = 10\n"
+                "  num.clustGroup = 3\n}\n", data)
+    if name == "mab":
+        data = tmp / "rw.csv"
+        with open(data, "w") as f:
+            for _ in range(3000):
+                f.write(f"grp{rnd.randrange(40)},{rnd.choice(['a1', 'a2', 'a3'])},{rnd.randint(0, 100)}\n")
+        return (["multiArmBandit", "-i", data],
+                "multiArmBandit {\n  action.list = [a1,a2,a3]\n  learner.type = upperConfidenceBoundOne\n"
+                "  current.decision.round = 3\n}\n", data)
     raise KeyError(name)
 
 
 def _conf(tmp, text, regex=False):
+    if not text.lstrip().split("\n")[0].endswith("{"):      # a .properties job
+        p = tmp / f"job{'_re' if regex else ''}.properties"
+        p.write_text(text + ("field.delim.regex=[,]\n" if regex else "field.delim.regex=,\n"))
+        return p
     p = tmp / f"job{'_re' if regex else ''}.conf"
     body = text.replace("{\n", "{\n  field.delim.in = \"" + ("[,]" if regex else ",") + "\"\n", 1)
     p.write_text(body)
     return p
 
 
-CASES = ["rs", "rs_all", "rs_two", "rs_rec", "gr", "nr", "sg", "td"]
+CASES = ["rs", "rs_all", "rs_two", "rs_rec", "gr", "nr", "sg", "td", "dm", "cgs", "kpp", "mab"]
 
 
 def _app(argv):
+    if argv[0] == "candidateGenerationWithSelfJoin":
+        return []
     return ["--app", "markovChainPredictor" if argv[0] == "timeDelayEmbeddingModel" else argv[0]]
 
 
