@@ -2909,7 +2909,8 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
 // format_columns(cols, n, delim, nthreads) -> bytes.  cols: ("s", list[str], idx int32) |
 // ("f", float64, prec) | ("i", int64) | ("c", literal) | ("g", literal glued without a delimiter) |
 // ("l", list[str], idx int32, off int64 [n+1]).
-py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& delim, int nthreads) {
+py::object format_columns_impl(py::list cols_py, int64_t n, const std::string& delim, int nthreads,
+                               const std::string* path, bool append) {
   std::vector<avh::FmtCol> cols;
   std::vector<std::unique_ptr<std::vector<std::string>>> tables;
   std::map<PyObject*, const std::vector<std::string>*> table_of;
@@ -2974,12 +2975,30 @@ py::bytes format_columns_py(py::list cols_py, int64_t n, const std::string& deli
     }
     cols.push_back(std::move(c));
   }
+  if (path) {
+    int64_t w;
+    {
+      py::gil_scoped_release rel;
+      w = avh::format_columns_to_file(cols, n, delim, nthreads, *path, append);
+    }
+    return py::int_(w);
+  }
   std::string out;
   {
     py::gil_scoped_release rel;
     out = avh::format_columns(cols, n, delim, nthreads);
   }
   return py::bytes(out);
+}
+
+py::object format_columns_py(py::list cols_py, int64_t n, const std::string& delim, int nthreads) {
+  return format_columns_impl(cols_py, n, delim, nthreads, nullptr, false);
+}
+
+// format_columns_file(cols, n, delim, nthreads, path, append) -> bytes written (threads pwrite)
+py::object format_columns_file_py(py::list cols_py, int64_t n, const std::string& delim, int nthreads,
+                                  const std::string& path, bool append) {
+  return format_columns_impl(cols_py, n, delim, nthreads, &path, append);
 }
 
 // pack_spans(addr int64 [n], len int64 [n], nthreads) -> (bytes uint8 [sum len], off int64 [n + 1]):
@@ -3245,6 +3264,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("format_columns", &format_columns_py, py::arg("cols"), py::arg("n"), py::arg("delim") = ",",
         py::arg("nthreads") = 8);
   m.def("format_rows", &format_rows);
+  m.def("format_columns_file", &format_columns_file_py, py::arg("cols"), py::arg("n"), py::arg("delim"),
+        py::arg("nthreads"), py::arg("path"), py::arg("append") = false);
   m.def("pack_spans", &pack_spans, py::arg("addr"), py::arg("len"), py::arg("nthreads") = 16);
   m.def("write_coded_csv", [](const std::string& path, const at::Tensor& codes, int64_t n,
                               std::vector<std::vector<std::string>> vocab, std::string id_prefix, std::string delim,

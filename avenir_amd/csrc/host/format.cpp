@@ -9,6 +9,9 @@
 #include <cstring>
 #include <stdexcept>
 #include <array>
+#include <atomic>
+#include <fcntl.h>
+#include <unistd.h>
 #include <thread>
 
 #include "avenir_host.h"
@@ -72,7 +75,7 @@ inline void put_pyrepr(std::string& s, double v) {
 }
 
 inline void put_double(std::string& s, double v, int prec) {
-  char buf[64];
+  char buf[352];
   int len;
   if (prec == -2) {
     put_pyrepr(s, v);
@@ -82,15 +85,23 @@ inline void put_double(std::string& s, double v, int prec) {
     s += "NaN";
     return;
   }
-  if (prec >= 0) len = snprintf(buf, sizeof buf, "%.*f", prec, v);
-  else len = snprintf(buf, sizeof buf, "%g", v);  // Python's "{:g}"
-  s.append(buf, (size_t)len);
+  // std::to_chars with a precision formats exactly as printf's %.*f / %g (and several times faster)
+  auto res = prec >= 0 ? std::to_chars(buf, buf + sizeof buf, v, std::chars_format::fixed, prec)
+                       : std::to_chars(buf, buf + sizeof buf, v, std::chars_format::general, 6);  // "{:g}"
+  if (res.ec != std::errc()) {  // very large values at a high precision: printf into a heap buffer
+    len = snprintf(nullptr, 0, prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
+    std::string tmp((size_t)len + 1, '\0');
+    snprintf(tmp.data(), tmp.size(), prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
+    s.append(tmp.data(), (size_t)len);
+    return;
+  }
+  s.append(buf, (size_t)(res.ptr - buf));
 }
 
 inline void put_int(std::string& s, int64_t v) {
   char buf[24];
-  const int len = snprintf(buf, sizeof buf, "%lld", (long long)v);
-  s.append(buf, (size_t)len);
+  auto res = std::to_chars(buf, buf + sizeof buf, v);
+  s.append(buf, (size_t)(res.ptr - buf));
 }
 
 // [a, e) of field ``f`` of the line [p, p + n) split at any character with sep[c] set (f < 0:
@@ -144,7 +155,9 @@ inline void put_rejoined(std::string& s, const char* p, int64_t n, const uint8_t
 
 }  // namespace
 
-std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads) {
+// the rows split over ``nthreads`` threads, each formatting its block into its own buffer
+static std::vector<std::string> format_parts(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim,
+                                             int nthreads) {
   for (const auto& c : cols) {
     if ((c.kind == FmtCol::STR || c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) && (!c.table || !c.idx))
       throw std::runtime_error("format_columns: string column without table / index");
@@ -242,12 +255,56 @@ std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std
   for (auto& x : th) x.join();
   for (auto& e : err)
     if (!e.empty()) throw std::runtime_error(e);
+  return parts;
+}
+
+std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads) {
+  std::vector<std::string> parts = format_parts(cols, n, delim, nthreads);
   size_t tot = 0;
   for (auto& p : parts) tot += p.size();
   std::string out;
   out.reserve(tot);
   for (auto& p : parts) out += p;
   return out;
+}
+
+}  // namespace avh
+
+namespace avh {
+
+// format_columns straight into a file (created / truncated, or appended to): every thread formats
+// its block of rows, then writes it with pwrite at its offset — no concatenated copy, no Python
+// bytes object.  Returns the bytes written.
+int64_t format_columns_to_file(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads,
+                               const std::string& path, bool append) {
+  std::vector<std::string> parts = format_parts(cols, n, delim, nthreads);
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | (append ? 0 : O_TRUNC), 0644);
+  if (fd < 0) throw std::runtime_error("cannot open " + path + " for writing");
+  off_t base = 0;
+  if (append) base = ::lseek(fd, 0, SEEK_END);
+  std::vector<int64_t> off(parts.size() + 1, 0);
+  for (size_t t = 0; t < parts.size(); ++t) off[t + 1] = off[t] + (int64_t)parts[t].size();
+  std::vector<std::thread> th;
+  std::atomic<bool> bad{false};
+  for (size_t t = 0; t < parts.size(); ++t)
+    th.emplace_back([&, t] {
+      const char* p = parts[t].data();
+      int64_t left = (int64_t)parts[t].size(), at = base + off[t];
+      while (left > 0) {
+        const ssize_t w = ::pwrite(fd, p, (size_t)left, (off_t)at);
+        if (w <= 0) {
+          bad = true;
+          return;
+        }
+        p += w;
+        left -= w;
+        at += w;
+      }
+    });
+  for (auto& x : th) x.join();
+  ::close(fd);
+  if (bad) throw std::runtime_error("write failed: " + path);
+  return off.back();
 }
 
 }  // namespace avh

@@ -176,6 +176,8 @@ struct FmtCol {
   std::string from_delims;
 };
 std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads);
+int64_t format_columns_to_file(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads,
+                               const std::string& path, bool append);
 
 // Lock-free SPSC ring of fixed-size int64 records.
 class SpscRing {

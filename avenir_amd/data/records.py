@@ -345,7 +345,7 @@ def shard_lines(path, comm=None, shard: bool = True, skip_header: bool = False) 
     return _py_lines(paths, rank, world, skip_header)
 
 
-def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
+def format_lines(cols: list[tuple], n: int, delim: str = ",", path: str | None = None, append: bool = False):
     """Output text of ``n`` rows assembled column by column (native, multi-threaded):
     ``("s", table, idx)`` string-table lookups, ``("f", values, prec)`` numbers (prec < 0: ``%g``),
     ``("i", ints)``, ``("c", literal)``, ``("g", literal)`` glued on without a delimiter,
@@ -353,10 +353,19 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",") -> bytes:
     ``("lp", table, idx, ints, off)`` the same with an integer after every string, and the raw
     input line kinds of ``data/lines.LineSpans.column``: ``("r", ...)`` the line, ``("rf", ...)``
     one of its fields, ``("rt", ...)`` its fields from one on.  ``prec`` -2 writes Python's
-    ``repr`` of the value.  Every row ends with a newline."""
+    ``repr`` of the value.  Every row ends with a newline.  With ``path`` the text goes straight
+    into that file (threads pwrite their blocks; ``append`` adds to it) and the byte count is
+    returned instead of the bytes."""
     C = _native.host()
     if C is not None:
+        if path is not None:
+            return C.format_columns_file(cols, int(n), delim, _threads(), str(path), bool(append))
         return C.format_columns(cols, int(n), delim, _threads())
+    if path is not None:
+        data = format_lines(cols, n, delim)
+        with open(path, "ab" if append else "wb") as fh:
+            fh.write(data)
+        return len(data)
     rows = [[] for _ in range(n)]
     glue_pre = [""] * n
     for c in cols:

@@ -250,6 +250,35 @@ class JobContext:
             return p
         return None
 
+    def emit_columns(self, cols: list, n: int, out: str | None = None) -> Path | None:
+        """Map-side output of ``data/records.format_lines`` columns: this rank's part file into a
+        directory (or the whole file when not distributed) written straight from the native
+        formatter's threads; a single-file output of several ranks is gathered to rank 0."""
+        from ..data.records import format_lines
+        p, is_dir = self._target(out)
+        if is_dir or not self.comm.is_distributed:
+            if is_dir:
+                p.mkdir(parents=True, exist_ok=True)
+                p = p / f"part-{self.comm.rank:05d}"
+            else:
+                p.parent.mkdir(parents=True, exist_ok=True)
+            format_lines(cols, n, self.delim_out, path=str(p))
+            return p
+        return self.emit_text(format_lines(cols, n, self.delim_out), out)
+
+    def emit_root_columns(self, cols: list, n: int, out: str | None = None, name: str = "part-00000") -> Path | None:
+        """Reduce-side output of ``format_lines`` columns: rank 0 writes them."""
+        from ..data.records import format_lines
+        if not self.is_root:
+            return None
+        p, is_dir = self._target(out)
+        if is_dir:
+            p.mkdir(parents=True, exist_ok=True)
+            p = p / name
+        p.parent.mkdir(parents=True, exist_ok=True)
+        format_lines(cols, n, self.delim_out, path=str(p))
+        return p
+
     def emit_root_text(self, text: bytes, out: str | None = None, name: str = "part-00000") -> Path | None:
         """Reduce-side output of pre-formatted text: rank 0 writes it."""
         if not self.is_root:

@@ -70,14 +70,14 @@ def nb_predict(args):
             cols += [("c", v), ("f", pc[:, c].contiguous(), -1)]
         lab = t.labels[: t.n].int().cpu() if t.labels is not None else torch.full((t.n,), -1, dtype=torch.int32)
         cols.append(("s", list(vals or []), lab))
-        ctx.emit_text(format_lines(cols, t.n, d))
+        ctx.emit_columns(cols, t.n)
         return
     r = nb.predict(t)
     prob = r.prob.max(1).values if r.prob is not None else torch.ones(t.n, device=r.pred.device)
     pred = r.pred.int().cpu()
     cols = [t.lines.column("r"), ("s", list(vals), pred) if vals else ("i", pred.long()),
             ("f", prob.double().cpu(), 3)]
-    ctx.emit_text(format_lines(cols, t.n, d))
+    ctx.emit_columns(cols, t.n)
     if r.confusion is not None:
         conf = r.confusion.clone()
         ctx.all_reduce(conf)
@@ -132,7 +132,7 @@ def dec_tree(args):
     pd = ctx.get_str("dec.path.delim", ";")
     paths = [pd.join(pr["predicateStr"] for pr in dp["predicates"]) for dp in js["decisionPaths"]] + ["$root"]
     first = torch.where(first >= 0, first, torch.full_like(first, len(paths) - 1)).int().cpu()
-    ctx.emit_text(format_lines([("s", paths, first), t.lines.column("r")], t.n, ctx.delim_out))
+    ctx.emit_columns([("s", paths, first), t.lines.column("r")], t.n)
     ctx.report({"level": grown, "done": grown <= depth or grown >= limit})
 
 
@@ -171,7 +171,7 @@ def knn(args):
     res = nn.predict((Xte - lo) / scale, q_base=te.row_offset)
     from ..data.records import format_lines
     vals = te.class_field.cardinality
-    ctx.emit_text(format_lines([te.lines.column("r"), ("s", list(vals), res.pred.int().cpu())], te.n, ctx.delim_out))
+    ctx.emit_columns([te.lines.column("r"), ("s", list(vals), res.pred.int().cpu())], te.n)
 
 
 @job("logisticRegression", "logistic regression (J/regress/LogisticRegressionJob.java): CSV -> coefficient lines per iteration")
@@ -545,7 +545,7 @@ def viterbi(args):
         table = [f"{o}{sub}{st}" for o in hmm.observations for st in hmm.states]
         idx = obs.to(path.device).long()[ok] * S + path[ok]
     cols = [rec.line_spans().column("rf", id_ord, lit), ("l", table, idx.int().cpu(), off)]
-    ctx.emit_text(format_lines(cols, rec.n_lines, ctx.delim_out))
+    ctx.emit_columns(cols, rec.n_lines)
 
 
 def _viterbi_rows(ctx, hmm, skip, id_ord, state_only, sub):
@@ -678,7 +678,7 @@ def mab(args):
     nb = acts.shape[1]
     cols = [("s", rec.vocab, keys[a:b].int().cpu()),
             ("l", list(actions), acts[a:b].reshape(-1).int(), torch.arange(0, (b - a) * nb + 1, nb, dtype=torch.long))]
-    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
+    ctx.emit_columns(cols, b - a)
 
 
 # ================================================================================================

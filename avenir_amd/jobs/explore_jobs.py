@@ -368,16 +368,16 @@ def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact
         if inc_cls:
             cols_f.append(("s", voc, srec[heads][:, cls_ord].int().cpu()))
         cols_f.append(("l", voc, tails.reshape(-1).int().cpu(), off.cpu()))
-        text = format_lines(cols_f, heads.numel(), d)
+        n_out = heads.numel()
     else:
         hc, tcs = head_cols[keep], tail_cols[keep]
         cols_f = [("s", voc, hc[:, j].int().cpu()) for j in range(hc.shape[1])]
         if inc_cls:
             cols_f.append(("s", voc, srec[keep][:, cls_ord].int().cpu()))
         cols_f += [("s", voc, tcs[:, j].int().cpu()) for j in range(tcs.shape[1])]
-        text = format_lines(cols_f, hc.shape[0], d)
+        n_out = hc.shape[0]
     # every rank's part is already in global source order: rank-ordered concatenation
-    ctx.emit_text(text)
+    ctx.emit_columns(cols_f, n_out)
 
 
 # ================================================================================================

@@ -103,7 +103,7 @@ def mmc(args):
     if val:
         cols.append(spans.column("rf", cls_ord, lit))
     cols += [("s", list(labels[:2]), pred), ("f", lo.cpu(), -2)]
-    ctx.emit_text(format_lines(cols, int(keep.sum()), ctx.delim_out))
+    ctx.emit_columns(cols, int(keep.sum()))
 
 
 def _mmc_rows(ctx, clf, states, labels, skip, id_ord, val, cls_ord, thr):
@@ -315,7 +315,7 @@ def _emit_pst(ctx, rec, rows: torch.Tensor, k: int, L: int, root: str) -> None:
     off = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(n_tok, 0)])
     cols = [("s", tab, ci[:, j].contiguous()) for j in range(k)]
     cols += [("l", tab, tk[tk >= 0].contiguous(), off), ("i", cnt)]
-    ctx.emit_root_text(format_lines(cols, int(cnt.numel()), ctx.delim_out))
+    ctx.emit_root_columns(cols, int(cnt.numel()))
 
 
 def _pstg_rows(ctx, skip, cls_ord, L, root, id_ords, sequential):
@@ -417,7 +417,7 @@ def cgs(args):
     C = torch.unique(C.cpu().long(), dim=0) if C.numel() else C.cpu().long().view(0, k + 1)
     kc = keys.cpu()
     cols = [("s", rec.vocab, kc[C[:, j]].int().contiguous()) for j in range(k + 1)]
-    ctx.emit_root_text(format_lines(cols, int(C.shape[0]), ctx.delim_out))
+    ctx.emit_root_columns(cols, int(C.shape[0]))
 
 
 @job("sequencePositionalCluster", "time-bounded event locality score over a sliding window (J/sequence/SequencePositionalCluster.java)")
@@ -546,7 +546,7 @@ def _state_transition_rate_native(ctx, kords, to, so, states, unit, in_unit, pre
     cols = [("g", "(")] + [("s", rec.vocab, p.int()) for p in key_parts]
     Qc = Q.reshape(b - a, -1).double().cpu()
     cols += [("f", Qc[:, j].contiguous(), prec) for j in range(Qc.shape[1])] + [("g", ")")]
-    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
+    ctx.emit_columns(cols, b - a)
 
 
 def _str_single_key(ctx, rec, key, tm, st, states, unit, prec):
@@ -565,7 +565,7 @@ def _str_single_key(ctx, rec, key, tm, st, states, unit, prec):
     Qc = Q.reshape(b - a, -1).double().cpu()
     cols = [("g", "("), ("s", rec.vocab, keys[a:b].int().cpu())]
     cols += [("f", Qc[:, j].contiguous(), prec) for j in range(Qc.shape[1])] + [("g", ")")]
-    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
+    ctx.emit_columns(cols, b - a)
 
 
 @job("contTimeStateTransitionStats", "CTMC statistics by uniformisation: stateDwellTime | StateTransitionCount | futureStateProb (S/markov/ContTimeStateTransitionStats.scala)")
@@ -673,7 +673,7 @@ def dot_matrix(args):
         Sv = torch.zeros(0, dtype=torch.float64)
     cols = [("s", rec.vocab, ids.to(I.device)[I].int().cpu()), ("s", rec.vocab, Jid.int().cpu()),
             ("f", Sv.double().cpu(), prec)]
-    ctx.emit_text(format_lines(cols, int(I.numel()), ctx.delim_out))
+    ctx.emit_columns(cols, int(I.numel()))
 
 
 def _dot_matrix_rows(ctx, skip, w, prec):
@@ -763,7 +763,7 @@ def seq_gen(args):
     vals = V[o].reshape(-1).int().cpu() if V is not None else torch.zeros(0, dtype=torch.int32)
     out = [("s", rec.vocab, ktab[a:b, j].int().contiguous()) for j in range(len(kords))]
     out.append(("l", rec.vocab, vals, off))
-    ctx.emit_text(format_lines(out, b - a, ctx.delim_out))
+    ctx.emit_columns(out, b - a)
 
 
 def _seq_gen_rows(ctx, kords, vords, sf):
@@ -836,7 +836,7 @@ def time_delay(args):
     wtab = sorted(wstr)
     out = [("s", rec.vocab, ktab[a:b, j].int().contiguous()) for j in range(len(kords))]
     out.append(("lp", wtab, ww.int().cpu(), cnt.long().cpu(), off))
-    ctx.emit_text(format_lines(out, b - a, ctx.delim_out))
+    ctx.emit_columns(out, b - a)
 
 
 def _time_delay_rows(ctx, kords, ao, so, w):

@@ -504,7 +504,7 @@ def _nearest_neighbor_native(ctx, rec, W, ccw, val, k, out_distr):
     if val:
         cols_f.append(("s", voc, at.int().cpu()))
     cols_f.append(("s", list(classes), pred.int().cpu()))
-    ctx.emit_text(format_lines(cols_f, nt, ctx.delim_out))
+    ctx.emit_columns(cols_f, nt)
     if val:
         av = rec.index(classes).long()
         act_cls = torch.where(at >= 0, av[at.clamp_min(0)] if av.numel() else at, torch.full_like(at, -2))
@@ -577,7 +577,7 @@ def model_predictor(args):
         cols = [spans.column("rf", id_o, lit), spans.column("rf", co, lit), pcol]
     else:
         cols = [spans.column("r", delims=lit), pcol]
-    ctx.emit_text(format_lines(cols, n, ctx.delim_out))
+    ctx.emit_columns(cols, n)
     if co >= 0:
         has = rec.lens() > co
         actual = rec.map_codes(rec.field(co), classes).long()
@@ -668,28 +668,19 @@ def data_partitioner(args):
 # batch bandits (MR map-only, per group)
 # ================================================================================================
 def _batch_bandit(args, prefix: str, strategy_fn):
+    """Rows ``group,item,count,reward`` (ordinals ``count.ordinal`` / ``reward.ordinal``); per group
+    (string order) the selected batch of items, lines ``group,item``.  Native path: each rank
+    reads its byte range, rows go to the rank owning their group (one all-to-all; input order kept
+    inside a group), the dense [groups, items] state is one scatter, and the selection's draws are
+    keyed by the global group index (``batch_select(group_base=...)``), so the output does not
+    depend on the world size."""
+    from functools import partial
+    from ..data.table import _literal, shard_range
     from ..models.bandit import batch_select
     ctx = JobContext(args, prefix)
-    rows = ctx.rows(shard=False)
     co, ro = ctx.get_int("count.ordinal", 2), ctx.get_int("reward.ordinal", 3)
-    groups = sorted({r[0] for r in rows})
-    if ctx.comm.is_distributed:
-        from ..data.table import shard_range
-        a, b = shard_range(len(groups), ctx.comm.rank, ctx.comm.world)
-        groups = groups[a:b]
-    gi = {g: i for i, g in enumerate(groups)}
-    items = defaultdict(list)
-    for r in rows:
-        if r[0] in gi:
-            items[r[0]].append((r[1], float(r[co]) if co >= 0 else 0.0, float(r[ro]) if ro >= 0 else 0.0))
-    I = max([len(v) for v in items.values()] + [1])
-    G = len(groups)
-    cnt = torch.zeros((G, I), dtype=torch.float64)
-    rew = torch.full((G, I), 0.0, dtype=torch.float64)
-    valid = torch.zeros((G, I), dtype=torch.bool)
-    for g, lst in items.items():
-        for j, (_, c, w) in enumerate(lst):
-            cnt[gi[g], j], rew[gi[g], j], valid[gi[g], j] = c, w * max(c, 1.0) if ctx.get_bool("reward.is.mean", True) else w, True
+    mean_in = ctx.get_bool("reward.is.mean", True)
+    comm = ctx.comm
     bs = {}
     cp = ctx.get_str("group.item.count.path", None)
     if cp and Path(cp).exists():
@@ -698,13 +689,87 @@ def _batch_bandit(args, prefix: str, strategy_fn):
             bs[p[0]] = int(p[1])
     glob = ctx.get_int("global.batch.size", 1)
     rnd = ctx.get_int("current.round.num", 1)
+    lit = _literal(ctx.delim_in)
+    if lit is None or len(lit) != 1:
+        return _batch_bandit_rows(ctx, co, ro, mean_in, bs, glob, rnd, strategy_fn)
+    from ..data.records import format_lines, owner_of, segment_rank, shuffle, sorted_keys
+    top = max(2, co + 1, ro + 1)
+    modes = "dd" + "".join("n" if i in (co, ro) else "x" for i in range(2, top))
+    rec = ctx.records(modes=modes, tail_mode="x", numeric=True)
+    dev = rec.device
+    zero = torch.zeros(rec.n_lines, dtype=torch.float64, device=dev)
+    gcode, icode = rec.field(0).long(), rec.field(1).long()
+    c = rec.field(co, numeric=True) if co >= 0 else zero
+    w = rec.field(ro, numeric=True) if ro >= 0 else zero
+    keys, pos = sorted_keys(rec, gcode, comm)
+    G = keys.numel()
+    gp = pos[gcode]
+    owner = owner_of(gp, G, comm.world) if comm.is_distributed else torch.zeros_like(gp)
+    gp, ic, c, w = shuffle(comm, owner, [gp, icode, c, w])
+    o = torch.argsort(gp, stable=True)
+    gp, ic, c, w = gp[o], ic[o], c[o], w[o]
+    first = torch.ones_like(gp, dtype=torch.bool)
+    first[1:] = gp[1:] != gp[:-1]
+    j = segment_rank(first)
+    a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
+    Gl = b - a
+    nmax = torch.tensor([int(j.max()) + 1 if j.numel() else 1], dtype=torch.long)
+    gstr = [rec.vocab[int(x)] for x in keys[a:b].tolist()]
+    kv = torch.tensor([bs.get(g_, glob) for g_ in gstr], dtype=torch.long)
+    kmax = torch.tensor([int(kv.max()) if kv.numel() else 1], dtype=torch.long)
+    if comm.is_distributed:
+        comm.all_reduce(nmax, "max")
+        comm.all_reduce(kmax, "max")
+    I, kmax = int(nmax), max(1, int(kmax))
+    lg = (gp - a)
+    cnt = torch.zeros((Gl, I), dtype=torch.float64, device=dev)
+    rew = torch.zeros((Gl, I), dtype=torch.float64, device=dev)
+    valid = torch.zeros((Gl, I), dtype=torch.bool, device=dev)
+    items = torch.full((Gl, I), -1, dtype=torch.long, device=dev)
+    cnt[lg, j] = c
+    rew[lg, j] = w * c.clamp_min(1.0) if mean_in else w
+    valid[lg, j] = True
+    items[lg, j] = ic
+    ctx.global_max_items = I
+    sel = strategy_fn(ctx, cnt.cpu(), rew.cpu(), valid.cpu(), kmax, rnd, partial(batch_select, group_base=a))
+    n_items = valid.sum(1).cpu()
+    kk = torch.minimum(kv, n_items)
+    take = (torch.arange(sel.shape[1]).view(1, -1) < kk.view(-1, 1)) & (sel < n_items.view(-1, 1))
+    gi, si = torch.nonzero(take, as_tuple=True)
+    chosen = items.cpu()[gi, sel[gi, si]]
+    cols = [("s", rec.vocab, keys[a:b].cpu()[gi].int()), ("s", rec.vocab, chosen.int())]
+    ctx.emit_columns(cols, int(gi.numel()))
+
+
+def _batch_bandit_rows(ctx, co, ro, mean_in, bs, glob, rnd, strategy_fn):
+    """Regex delimiters: the split-row path (every rank reads the input, selects a block of groups)."""
+    from functools import partial
+    from ..data.table import shard_range
+    from ..models.bandit import batch_select
+    rows = ctx.rows(shard=False)
+    groups = sorted({r[0] for r in rows})
+    items = defaultdict(list)
+    for r in rows:
+        items[r[0]].append((r[1], float(r[co]) if co >= 0 else 0.0, float(r[ro]) if ro >= 0 else 0.0))
+    I = max([len(v) for v in items.values()] + [1])
     kmax = max([bs.get(g, glob) for g in groups] + [1])
-    sel = strategy_fn(ctx, cnt, rew, valid, kmax, rnd, batch_select)
+    a, b = shard_range(len(groups), ctx.comm.rank, ctx.comm.world) if ctx.comm.is_distributed else (0, len(groups))
+    groups = groups[a:b]
+    G = len(groups)
+    cnt = torch.tensor([[x[1] for x in items[g]] + [0.0] * (I - len(items[g])) for g in groups],
+                       dtype=torch.float64).view(G, I)
+    rw = torch.tensor([[x[2] for x in items[g]] + [0.0] * (I - len(items[g])) for g in groups],
+                      dtype=torch.float64).view(G, I)
+    rew = rw * cnt.clamp_min(1.0) if mean_in else rw
+    valid = torch.tensor([[True] * len(items[g]) + [False] * (I - len(items[g])) for g in groups],
+                         dtype=torch.bool).view(G, I)
+    ctx.global_max_items = I
+    sel = strategy_fn(ctx, cnt, rew, valid, kmax, rnd, partial(batch_select, group_base=a))
     d = ctx.delim_out
     out = []
-    for g in groups:
+    for gi_, g in enumerate(groups):
         k = min(bs.get(g, glob), len(items[g]))
-        for j in sel[gi[g], :k].tolist():
+        for j in sel[gi_, :k].tolist():
             if j < len(items[g]):
                 out.append(f"{g}{d}{items[g][j][0]}")
     ctx.emit(out)
@@ -746,7 +811,7 @@ def softmax_bandit(args):
 def random_first_bandit(args):
     def fn(ctx, cnt, rew, valid, k, rnd, batch_select):
         from ..models.bandit import pac_exploration_count
-        I = int(valid.sum(1).max())
+        I = getattr(ctx, "global_max_items", int(valid.sum(1).max()))   # over ALL groups (world-invariant)
         if ctx.get_str("exploration.count.strategy", "simple") == "pac":
             ex = pac_exploration_count(I, ctx.get_float("pac.reward.diff", 0.2), ctx.get_float("pac.prob.diff", 0.2))
         else:
@@ -859,7 +924,7 @@ def record_similarity(args):
     if out_rec:
         cols += [spI.column("r", delims=lit), spJ.column("r", delims=lit)]
     cols.append(("i", Dv))
-    ctx.emit_text(format_lines(cols, int(I.numel()), ctx.delim_out))
+    ctx.emit_columns(cols, int(I.numel()))
 
 
 def _numeric_matrix(ctx, rows, ords):
@@ -940,7 +1005,7 @@ def grouped_similarity(args):
     kp_c, ids_c = kp.cpu(), ids.cpu().int()
     out = [("s", rec.vocab, ktab[kp_c[ii], j].int().contiguous()) for j in range(len(kords))]
     out += [("s", rec.vocab, ids_c[ii]), ("s", rec.vocab, ids_c[jj]), ("f", dd.double().cpu(), prec)]
-    ctx.emit_text(format_lines(out, int(ii.numel()), ctx.delim_out))
+    ctx.emit_columns(out, int(ii.numel()))
 
 
 def _grouped_similarity_rows(ctx):
@@ -1010,7 +1075,7 @@ def nearest_records(args):
     off = torch.cat([torch.zeros(1, dtype=torch.long, device=cnt.device), torch.cumsum(cnt, 0)]).cpu()
     kc = keys.cpu()
     cols = [("s", rec.vocab, kc[a:b].int().contiguous()), ("l", rec.vocab, kc[yp[keep].cpu()].int(), off)]
-    ctx.emit_text(format_lines(cols, b - a, ctx.delim_out))
+    ctx.emit_columns(cols, b - a)
 
 
 def _nearest_records_rows(ctx, k, thr):

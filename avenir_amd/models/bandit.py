@@ -315,18 +315,25 @@ def _interval_ub(h: np.ndarray, bw: float, conf: float) -> float:
 # ================================================================================================
 def batch_select(counts: torch.Tensor, rewards: torch.Tensor, batch_size: int, strategy: str = "auerGreedy",
                  round_num: int = 1, epsilon: float = 0.1, temp: float = 1.0, explore_count: int = 0,
-                 seed: int = 0) -> torch.Tensor:
+                 seed: int = 0, group_base: int = 0) -> torch.Tensor:
     """Select ``batch_size`` distinct items per group from (count, total reward) state [G, I]:
     ``auerGreedy``/``auerDeterministic`` (UCB1 ranking), ``linear``/``logLinear`` eps-greedy
     (GreedyRandomBandit), ``softMax`` (SoftMaxBandit, sampling without replacement via Gumbel
     top-k), ``randomFirst`` (RandomFirstGreedyBandit: explore uniformly for the first
-    ``explore_count`` rounds, then exploit by mean reward)."""
+    ``explore_count`` rounds, then exploit by mean reward).  The random draws are counter-based
+    (Philox keyed by (seed + round, global group ``group_base + g``, item)), so a group's selection
+    does not depend on which other groups share the call — a rank's block of groups selects
+    exactly what a single process selects."""
     G, I = counts.shape
     n = counts.double()
     mean = torch.where(n > 0, rewards.double() / n.clamp_min(1), torch.zeros_like(n))
-    g = torch.Generator(device="cpu")
-    g.manual_seed(seed + round_num)
-    noise = torch.rand((G, I), generator=g, dtype=torch.float64).to(counts.device)
+    import numpy as np
+    from ..ops.random import philox4x32
+    idx = ((np.arange(G, dtype=np.uint64) + np.uint64(group_base))[:, None] * np.uint64(I)
+           + np.arange(I, dtype=np.uint64)[None, :]).reshape(-1)
+    x, y, _, _ = philox4x32(seed + round_num, 0, idx)
+    u = ((x.astype(np.uint64) << np.uint64(21)) | (y.astype(np.uint64) >> np.uint64(11))).astype(np.float64)
+    noise = torch.from_numpy((u + 0.5) / float(1 << 53)).view(G, I).to(counts.device)
     k = min(batch_size, I)
     if strategy in ("auerGreedy", "auerDeterministic"):
         tot = n.sum(1, keepdim=True).clamp_min(1)

@@ -110,6 +110,15 @@ def _setup(tmp: Path, name: str):
         return (["multiArmBandit", "-i", data],
                 "multiArmBandit {\n  action.list = [a1,a2,a3]\n  learner.type = upperConfidenceBoundOne\n"
                 "  current.decision.round = 3\n}\n", data)
+    if name in ("gb", "smb", "rfb"):
+        data = tmp / "state.csv"
+        with open(data, "w") as f:
+            for g in range(45):
+                for it in range(rnd.randint(1, 9)):
+                    f.write(f"grp{g},item{it},{rnd.randint(1, 30)},{rnd.random() * 5:.3f}\n")
+        job = {"gb": "greedyRandomBandit", "smb": "softMaxBandit", "rfb": "randomFirstGreedyBandit"}[name]
+        return ([job, "-i", data], "global.batch.size=2\ncurrent.round.num=3\ncount.ordinal=2\nreward.ordinal=3\n"
+                "random.selection.prob=0.3\nexploration.count.factor=1\n", data)
     raise KeyError(name)
 
 
@@ -124,11 +133,12 @@ def _conf(tmp, text, regex=False):
     return p
 
 
-CASES = ["rs", "rs_all", "rs_two", "rs_rec", "gr", "nr", "sg", "td", "dm", "cgs", "kpp", "mab"]
+CASES = ["rs", "rs_all", "rs_two", "rs_rec", "gr", "nr", "sg", "td", "dm", "cgs", "kpp", "mab", "gb", "smb", "rfb"]
 
 
 def _app(argv):
-    if argv[0] == "candidateGenerationWithSelfJoin":
+    if argv[0] in ("candidateGenerationWithSelfJoin", "greedyRandomBandit", "softMaxBandit",
+                   "randomFirstGreedyBandit"):
         return []
     return ["--app", "markovChainPredictor" if argv[0] == "timeDelayEmbeddingModel" else argv[0]]
 
