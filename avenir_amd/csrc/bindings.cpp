@@ -1571,7 +1571,131 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
                          reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
                          gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
-                         host_gap.data_ptr<float>(), kbs, cur_stream(y));
+                         host_gap.data_ptr<float>(), kbs, cur_stream(y), nullptr);
+}
+
+// implicit kernel source from X [B or 1, N, D] (or [N, D]) and its squared norms
+static avk::SvmKerX make_kerx(const at::Tensor& X, const at::Tensor& xn, int64_t B, int64_t N, int64_t kind,
+                              double gamma, double coef0, int64_t degree) {
+  CHECK_DEV(X);
+  CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(xn);
+  CHECK_DTYPE(xn, at::kFloat);
+  TORCH_CHECK(X.is_contiguous() && xn.is_contiguous(), "X / xn must be contiguous");
+  const bool batched = X.dim() == 3;
+  TORCH_CHECK((X.dim() == 2 && X.size(0) == N) || (batched && (X.size(0) == B || X.size(0) == 1) && X.size(1) == N),
+              "X must be [N, D] or [B or 1, N, D]");
+  const int64_t D = X.size(X.dim() - 1);
+  TORCH_CHECK(D >= 1 && D <= 65536, "1 <= D <= 65536");
+  TORCH_CHECK(xn.numel() == (batched ? X.size(0) : 1) * N, "xn must hold the squared norms of X's rows");
+  TORCH_CHECK(kind >= 0 && kind <= 3 && degree >= 0 && degree <= 16, "kernel kind 0..3, degree 0..16");
+  avk::SvmKerX k;
+  k.X = X.data_ptr<float>();
+  k.xn = xn.data_ptr<float>();
+  k.xbs = (batched && X.size(0) == B && B > 1) ? N : 0;
+  k.D = (int)D;
+  k.kind = (int)kind;
+  k.degree = (int)degree;
+  k.gamma = (float)gamma;
+  k.coef0 = (float)coef0;
+  return k;
+}
+
+// The working-set solve with the implicit kernel (no N x N matrix): K[ws, ws] and the gradient
+// updates are recomputed from X each outer step (avk::smo_ws_run with kx).
+int64_t smo_ws_run_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, double gamma, double coef0,
+                     int64_t degree, at::Tensor& alpha, at::Tensor& G, const at::Tensor& y, double C, double eps,
+                     int64_t inner_iter, double rel_tol, int64_t max_outer, int64_t check_every, at::Tensor& ws,
+                     at::Tensor& ok, at::Tensor& dA, at::Tensor& inner_total, at::Tensor& gap) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&alpha, &G, &y, &gap, &dA}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+  }
+  TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
+  const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
+  TORCH_CHECK(N >= 1 && N <= (1 << 18), "1 <= N <= 2^18");
+  const avk::SvmKerX k = make_kerx(X, xn, B, N, kind, gamma, coef0, degree);
+  TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
+              "alpha / G must be [B, >= N]");
+  CHECK_DEV(ws);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DEV(ok);
+  CHECK_DTYPE(ok, at::kBool);
+  CHECK_DEV(inner_total);
+  CHECK_DTYPE(inner_total, at::kLong);
+  TORCH_CHECK(ws.numel() == B * Q && ok.numel() == B * Q && dA.numel() == B * Q, "ws / ok / dA must be [B, ", Q, "]");
+  TORCH_CHECK(gap.numel() == B && inner_total.numel() == B, "gap / inner_total must be [B]");
+  TORCH_CHECK(C > 0 && eps > 0 && inner_iter >= 0, "bad SMO parameters");
+  DevGuard g(y.device());
+  const int64_t parts = avk::smo_ws_select_parts((int)N);
+  auto cand = at::empty({2, B, parts, 2, Q / 2}, y.options().dtype(at::kInt));
+  auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
+  auto Kws = at::empty({B, Q, Q}, y.options());
+  auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
+  return avk::smo_ws_run(nullptr, (int)N, alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B,
+                         (int)alpha.size(1), (float)C, (float)eps, (int)inner_iter, (float)rel_tol, max_outer,
+                         (int)check_every, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
+                         dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
+                         gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
+                         host_gap.data_ptr<float>(), 0, cur_stream(y), &k);
+}
+
+// one implicit-kernel gather (K[ws, ws] -> [B, Q, Q]) and one gradient update (tests / oracles)
+at::Tensor smo_ws_gather_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, double gamma, double coef0,
+                           int64_t degree, const at::Tensor& ws, const at::Tensor& ok, int64_t N) {
+  CHECK_DEV(ws);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DTYPE(ok, at::kBool);
+  const int64_t Q = avk::smo_ws_size(), B = ws.size(0);
+  TORCH_CHECK(ws.dim() == 2 && ws.size(1) == Q && ok.sizes() == ws.sizes(), "ws / ok must be [B, ", Q, "]");
+  TORCH_CHECK(ws.numel() == 0 || (ws.min().item<int64_t>() >= 0 && ws.max().item<int64_t>() < N), "ws out of range");
+  const avk::SvmKerX k = make_kerx(X, xn, B, N, kind, gamma, coef0, degree);
+  DevGuard g(ws.device());
+  auto Kws = at::zeros({B, Q, Q}, X.options());
+  avk::smo_ws_gather_x(k, reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
+                       Kws.data_ptr<float>(), (int)B, (int)N, nullptr, -INFINITY, cur_stream(ws));
+  return Kws;
+}
+
+void smo_ws_update_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, double gamma, double coef0,
+                     int64_t degree, const at::Tensor& ws, const at::Tensor& dA, const at::Tensor& ok,
+                     const at::Tensor& y, at::Tensor& G) {
+  CHECK_DEV(y);
+  CHECK_DTYPE(y, at::kFloat);
+  CHECK_DTYPE(G, at::kFloat);
+  CHECK_DTYPE(dA, at::kFloat);
+  CHECK_DTYPE(ws, at::kLong);
+  CHECK_DTYPE(ok, at::kBool);
+  const int64_t B = y.size(0), N = y.size(1);
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == B && G.size(1) >= N, "G must be [B, >= N]");
+  TORCH_CHECK(ws.dim() == 2 && ws.size(0) == B && ws.size(1) <= avk::smo_ws_size() && dA.sizes() == ws.sizes() &&
+                  ok.sizes() == ws.sizes(),
+              "ws / dA / ok must be [B, Q <= ", avk::smo_ws_size(), "]");
+  TORCH_CHECK(ws.numel() == 0 || (ws.min().item<int64_t>() >= 0 && ws.max().item<int64_t>() < N), "ws out of range");
+  const avk::SvmKerX k = make_kerx(X, xn, B, N, kind, gamma, coef0, degree);
+  DevGuard g(y.device());
+  avk::smo_ws_update_x(k, reinterpret_cast<const long long*>(ws.data_ptr<int64_t>()), dA.data_ptr<float>(),
+                       ok.data_ptr<bool>(), y.data_ptr<float>(), G.data_ptr<float>(), (int)B, (int)N, (int)G.size(1),
+                       (int)ws.size(1), nullptr, -INFINITY, cur_stream(y));
+}
+
+// K(A, B) [na, nb] through f32 MFMA for any d (kind 0 linear, 1 poly, 2 rbf, 3 sigmoid)
+at::Tensor svm_kernel_matrix(const at::Tensor& A, const at::Tensor& Bm, int64_t kind, double gamma, double coef0,
+                             int64_t degree) {
+  CHECK_DEV(A);
+  CHECK_DEV(Bm);
+  CHECK_DTYPE(A, at::kFloat);
+  CHECK_DTYPE(Bm, at::kFloat);
+  TORCH_CHECK(A.dim() == 2 && Bm.dim() == 2 && A.size(1) == Bm.size(1) && A.size(1) >= 1, "A [na, d], B [nb, d]");
+  TORCH_CHECK(A.size(0) < (1LL << 31) / 64 && Bm.size(0) < (1LL << 31) / 64, "too many rows");
+  DevGuard g(A.device());
+  const auto Ac = A.contiguous(), Bc = Bm.contiguous();
+  const auto an = (Ac * Ac).sum(1).contiguous(), bnrm = (Bc * Bc).sum(1).contiguous();
+  const avk::SvmKerX k = make_kerx(Ac, an, 1, A.size(0), kind, gamma, coef0, degree);
+  auto K = at::empty({A.size(0), Bm.size(0)}, A.options());
+  avk::svm_kernel_matrix_mfma(k, Bc.data_ptr<float>(), bnrm.data_ptr<float>(), (int)A.size(0), (int)Bm.size(0),
+                              K.data_ptr<float>(), cur_stream(A));
+  return K;
 }
 
 std::vector<at::Tensor> nb_finalize(const at::Tensor& counts, const at::Tensor& offs, const at::Tensor& bins,
@@ -3089,6 +3213,64 @@ std::vector<at::Tensor> lstm_forward(const at::Tensor& x, const at::Tensor& wfra
   return {hseq, cseq};
 }
 
+// fp32 recurrence (rnn_f32.hip): xw [B, T, 4HP] fp32 kernel order (input projection + biases);
+// wfrag [NW, 4, HP/4, 64] fp32.  Returns hseq [B,T,H], cseq [B,T,HP] (+ gates [B,T,4HP] fp32).
+std::vector<at::Tensor> lstm_forward_f32(const at::Tensor& xw, const at::Tensor& wfrag,
+                                         const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
+                                         int64_t H, bool training) {
+  const int64_t KS = lstm_ks(H), HP = 32 * KS;
+  CHECK_DEV(xw);
+  CHECK_DTYPE(xw, at::kFloat);
+  TORCH_CHECK(xw.dim() == 3 && xw.size(2) == 4 * HP && xw.is_contiguous(), "xw must be [B, T, 4HP] contiguous");
+  TORCH_CHECK(aligned(xw, 16), "xw must be 16-byte aligned");
+  const int64_t B = xw.size(0), T = xw.size(1);
+  TORCH_CHECK(B >= 1 && T >= 1, "empty LSTM input");
+  CHECK_DEV(wfrag);
+  CHECK_DTYPE(wfrag, at::kFloat);
+  TORCH_CHECK(wfrag.numel() == 2 * KS * 4 * (HP / 4) * 64, "wfrag must be [NW, 4, HP/4, 64]");
+  check_opt_f32(h0, B * H, "h0");
+  check_opt_f32(c0, B * H, "c0");
+  DevGuard g(xw.device());
+  auto f32 = xw.options();
+  auto hseq = at::empty({B, T, H}, f32), cseq = at::empty({B, T, HP}, f32);
+  at::Tensor gates;
+  if (training) gates = at::empty({B, T, 4 * HP}, f32);
+  avk::lstm_fwd_f32(xw.data_ptr<float>(), wfrag.data_ptr<float>(), ptr_or_null<float>(h0), ptr_or_null<float>(c0),
+                    (int)B, (int)T, (int)H, (int)KS, hseq.data_ptr<float>(), cseq.data_ptr<float>(),
+                    training ? gates.data_ptr<float>() : nullptr, cur_stream(xw));
+  if (training) return {hseq, cseq, gates};
+  return {hseq, cseq};
+}
+
+// fp32 backward recurrence: dz [B,T,4HP] fp32 (kernel order), dh0, dc0 [B,H]; wfragT [NW, HP, 64] fp32
+std::vector<at::Tensor> lstm_backward_f32(const at::Tensor& dhseq, const at::Tensor& gates, const at::Tensor& cseq,
+                                          const c10::optional<at::Tensor>& c0, const c10::optional<at::Tensor>& dhn,
+                                          const c10::optional<at::Tensor>& dcn, const at::Tensor& wfragT, int64_t H) {
+  const int64_t KS = lstm_ks(H), HP = 32 * KS;
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&dhseq, &gates, &cseq, &wfragT}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+    TORCH_CHECK(t->is_contiguous() && aligned(*t, 16), "LSTM backward inputs must be contiguous and 16-byte aligned");
+  }
+  TORCH_CHECK(dhseq.dim() == 3 && dhseq.size(2) == H, "dhseq must be [B, T, H]");
+  const int64_t B = dhseq.size(0), T = dhseq.size(1);
+  TORCH_CHECK(cseq.dim() == 3 && cseq.size(0) == B && cseq.size(1) == T && cseq.size(2) == HP,
+              "cseq must be [B, T, HP]");
+  TORCH_CHECK(gates.dim() == 3 && gates.size(0) == B && gates.size(1) == T && gates.size(2) == 4 * HP,
+              "gates must be [B, T, 4HP]");
+  TORCH_CHECK(wfragT.numel() == 2 * KS * HP * 64, "wfragT must be [NW, HP, 64]");
+  check_opt_f32(c0, B * H, "c0");
+  check_opt_f32(dhn, B * H, "dhn");
+  check_opt_f32(dcn, B * H, "dcn");
+  DevGuard g(dhseq.device());
+  auto dz = at::empty({B, T, 4 * HP}, dhseq.options());
+  auto dh0 = at::empty({B, H}, dhseq.options()), dc0 = at::empty({B, H}, dhseq.options());
+  avk::lstm_bwd_f32(dhseq.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), ptr_or_null<float>(c0),
+                    ptr_or_null<float>(dhn), ptr_or_null<float>(dcn), wfragT.data_ptr<float>(), (int)B, (int)T, (int)H,
+                    (int)KS, dz.data_ptr<float>(), dh0.data_ptr<float>(), dc0.data_ptr<float>(), cur_stream(dhseq));
+  return {dz, dh0, dc0};
+}
+
 std::vector<at::Tensor> lstm_backward(const at::Tensor& dhseq, const at::Tensor& gates, const at::Tensor& cseq,
                                       const c10::optional<at::Tensor>& c0, const c10::optional<at::Tensor>& dhn,
                                       const c10::optional<at::Tensor>& dcn, const at::Tensor& wfragT, int64_t H) {
@@ -3178,6 +3360,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_ws_select", &smo_ws_select);
   m.def("smo_ws_update", &smo_ws_update);
   m.def("smo_ws_run", &smo_ws_run);
+  m.def("smo_ws_run_x", &smo_ws_run_x);
+  m.def("smo_ws_gather_x", &smo_ws_gather_x);
+  m.def("smo_ws_update_x", &smo_ws_update_x);
+  m.def("svm_kernel_matrix", &svm_kernel_matrix);
   m.def("rbf_matrix", &rbf_matrix);
   m.def("smo_ws_solve_fused", &smo_ws_solve_fused, py::arg("K"), py::arg("ws"), py::arg("ok"), py::arg("alpha"),
         py::arg("G"), py::arg("y"), py::arg("gap"), py::arg("C"), py::arg("eps"), py::arg("max_iter"), py::arg("dA"),
@@ -3212,6 +3398,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);
+  m.def("lstm_forward_f32", &lstm_forward_f32);
+  m.def("lstm_backward_f32", &lstm_backward_f32);
 
   py::class_<avh::CsvFile>(m, "CsvFile")
       .def(py::init<const std::string&, const std::string&, bool, int>(), py::arg("path"), py::arg("delim") = ",",

@@ -124,10 +124,30 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
 int smo_ws_select_parts(int N);
 void smo_ws_update(const float* K, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                    int B, int N, int ldag, int Q, const float* gap, float skip, long long kbs, hipStream_t stream);
+// Implicit kernel source of the working-set solver: k(x_i, x_j) recomputed from the rows of X instead
+// of read from an N x N matrix (O(N D) memory).  Problem b uses rows X + b * xbs (xbs = 0: shared).
+struct SvmKerX {
+  const float* X;   // [B or 1][N][D] row-major
+  const float* xn;  // [B or 1][N] squared norms
+  long long xbs;    // problem stride in rows (0 or N)
+  int D;
+  int kind;         // 0 linear, 1 poly, 2 rbf, 3 sigmoid
+  int degree;
+  float gamma, coef0;
+};
+void smo_ws_gather_x(const SvmKerX& k, const long long* ws, const bool* ok, float* Kws, int B, int N, const float* gap,
+                     float skip, hipStream_t stream);
+void smo_ws_update_x(const SvmKerX& k, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
+                     int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream);
+// K [na, nb] = k(a_i, b_j) through f32 MFMA (v_mfma_f32_16x16x4_f32) for any d; a.X / a.xn are the
+// rows of A, Bx / bn those of B
+void svm_kernel_matrix_mfma(const SvmKerX& a, const float* Bx, const float* bn, int na, int nb, float* K,
+                            hipStream_t stream);
+// kx == nullptr: explicit K (kbs = problem stride); else the implicit source (K unused)
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, long long kbs, hipStream_t stream);
+                     float* host_gap, long long kbs, hipStream_t stream, const SvmKerX* kx = nullptr);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
                         long long* inner_total, float* Kws, float rel_tol, long long kbs, hipStream_t stream);
@@ -135,6 +155,13 @@ int smo_ws_size();
 void rbf_matrix(const float* A, const float* B, int na, int nb, int d, float gamma, float* K, hipStream_t stream);
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream);
+
+// ---- rnn_f32.hip (K27 fp32) ------------------------------------------------------------------
+void lstm_fwd_f32(const float* xw, const float* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
+                  float* hseq, float* cseq, float* gates, hipStream_t s);
+void lstm_bwd_f32(const float* dhseq, const float* gates, const float* cseq, const float* c0, const float* dhn,
+                  const float* dcn, const float* wfragT, int B, int T, int H, int KS, float* dz, float* dh0,
+                  float* dc0, hipStream_t s);
 
 // ---- bayes.hip: model finalisation -----------------------------------------------------------
 void nb_finalize(const long long* counts, int C, int TB, const int* offs, const int* bins, int F, float laplace,

@@ -1,0 +1,308 @@
+// K27 (fp32) — persistent fused LSTM recurrence on the f32 matrix cores, forward + backward.
+//
+// The fp32 twin of rnn.hip for the reference's numerics (P/supv/lstm.py:275-339 trains an fp32
+// torch.nn.LSTM): every product is v_mfma_f32_16x16x4_f32 — a k-ordered chain of f32 fmas, one
+// rounding per product, no reduced-precision operand — and every stored intermediate is fp32.
+//
+//   forward : z_t = xw_t + h_{t-1}·W_hhᵀ ; i,f,o = σ(z), g = tanh(z) ; c_t = f c_{t-1} + i g ;
+//             h_t = o tanh(c_t)
+//   backward: dz_t from (dh_t, dc_t, saved gates) ; dh_{t-1} = dz_t·W_hh ; dc_{t-1} = dc_t f
+//
+// Split (MI355X): the input projection xw = x·W_ihᵀ + b of ALL timesteps is one fp32 library GEMM
+// outside the kernel (fully parallel; with f32 operands the recurrent weights alone take HP VGPRs,
+// so [W_hh | W_ih] no longer both fit in registers as in the bf16 kernel).  Only the sequential
+// part lives here.  One workgroup owns RT tiles of 16 sequences for the whole sequence; wave w owns
+// hidden units [16w, 16w+16) of all four gates with its W_hh slice in VGPRs as f32 A-fragments
+// (lane l of k-step s: W[row 16w + (l&15)][k 4s + (l>>4)]), the cell state in VGPRs in the
+// accumulator layout (row = unit 4(l>>4) + r, column = sequence l&15 — the same C/D map as the bf16
+// kernel, so the gate math is shared), and the accumulators start from xw_t.  h_t goes through LDS
+// as fp32 (double-buffered, one barrier per step); the B operand of k-step s is one float per lane,
+// h[seq l&15][unit 4s + (l>>4)] (rows padded to HP + 1 floats: conflict-free).
+// Weight-gradient GEMMs (dzᵀ·h_{t-1}, dzᵀ·x, Σdz) and dx = dz·W_ih run as fp32 library GEMMs.
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  return copysignf((1.f - e) / (1.f + e), x);
+}
+
+// Layouts (kernel order of the 4·HP gate columns: kc = 64·w + 16·g + i for unit u = 16·w + i, gate g):
+//   xw     [B, T, 4HP] fp32, kernel order: x_t·W_ihᵀ + b_ih + b_hh (zero for padded units)
+//   wfrag  [NW][4][KS4][64] fp32: A-fragment of W_hh for (wave, gate, k-step of 4), KS4 = HP / 4
+//   h0, c0 [B, H] or null;  hseq [B, T, H], cseq [B, T, HP] fp32 out
+//   gates  [B, T, 4HP] fp32 post-activation (kernel order) out or null
+template <int KS, int RT>
+__global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __restrict__ xw,
+                                                                const float* __restrict__ wfrag,
+                                                                const float* __restrict__ h0,
+                                                                const float* __restrict__ c0, int B, int T, int H,
+                                                                float* __restrict__ hseq, float* __restrict__ cseq,
+                                                                float* __restrict__ gates) {
+  constexpr int HP = 32 * KS, KS4 = HP / 4, G4P = 4 * HP, NT = 128 * KS, LROW = HP + 1;
+  __shared__ float sbuf[2][RT * 16][LROW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col = lane & 15, quad = lane >> 4;
+  const int u0 = 16 * w + 4 * quad, kc0 = 64 * w + 4 * quad;
+  const long long row0 = (long long)blockIdx.x * (RT * 16);
+  const long long TG = (long long)T * G4P, THP = (long long)T * HP, TH = (long long)T * H;
+  const bool vec_h = (H & 3) == 0;
+
+  float wf[4][KS4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int s = 0; s < KS4; ++s) wf[g][s] = wfrag[((w * 4 + g) * KS4 + s) * 64 + lane];
+
+  int lrow[RT];
+  bool rok[RT];
+  f32x4 c[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int lr = rt * 16 + col;
+    rok[rt] = row0 + lr < B;
+    lrow[rt] = rok[rt] ? lr : (int)(B - 1 - row0);
+    const long long grow = row0 + lrow[rt];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = u0 + r < H;
+      c[rt][r] = (ok && c0) ? c0[grow * H + u0 + r] : 0.f;
+      sbuf[0][lr][u0 + r] = (ok && h0) ? h0[grow * H + u0 + r] : 0.f;
+    }
+  }
+  // xw_t of this lane's four units of every gate, prefetched one step ahead
+  f32x4 xn[RT][4];
+  auto load_xw = [&](int t) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const float* src = xw + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xn[rt][g] = *reinterpret_cast<const f32x4*>(src + 16 * g);
+    }
+  };
+  load_xw(0);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1;
+    f32x4 acc[RT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[rt][g] = xn[rt][g];
+    if (t + 1 < T) load_xw(t + 1);
+#pragma unroll
+    for (int s = 0; s < KS4; ++s)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const float hb = sbuf[cur][rt * 16 + col][4 * s + quad];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[rt][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[g][s], hb, acc[rt][g], 0, 0, 0);
+      }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      f32x4 ig, fg, gg, og, hn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ig[r] = sigm(acc[rt][0][r]);
+        fg[r] = sigm(acc[rt][1][r]);
+        gg[r] = tanh_(acc[rt][2][r]);
+        og[r] = sigm(acc[rt][3][r]);
+        c[rt][r] = fg[r] * c[rt][r] + ig[r] * gg[r];
+        hn[r] = og[r] * tanh_(c[rt][r]);
+        sbuf[cur ^ 1][rt * 16 + col][u0 + r] = hn[r];
+      }
+      if (rok[rt]) {
+        *reinterpret_cast<f32x4*>(cseq + lrow[rt] * THP + (long long)t * HP + u0 + row0 * THP) = c[rt];
+        float* hp = hseq + (row0 + lrow[rt]) * TH + (long long)t * H + u0;
+        if (vec_h) {
+          if (u0 < H) *reinterpret_cast<f32x4*>(hp) = hn;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (u0 + r < H) hp[r] = hn[r];
+        }
+        if (gates) {
+          float* gp = gates + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
+          *reinterpret_cast<f32x4*>(gp) = ig;
+          *reinterpret_cast<f32x4*>(gp + 16) = fg;
+          *reinterpret_cast<f32x4*>(gp + 32) = gg;
+          *reinterpret_cast<f32x4*>(gp + 48) = og;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dhseq [B, T, H]; gates [B, T, 4HP] fp32 kernel order; cseq [B, T, HP]; c0 / dhn / dcn [B, H] or null
+// wfragT [NW][4HP/4][64] fp32: A-fragment of W_hhᵀ for dhᵀ = W_hhᵀ·dzᵀ, k over the 4·HP gate rows
+//        gate-major (k = g·HP + u): lane l of k-step s holds W_hh[k = 4s + (l>>4)][unit 16w + (l&15)]
+// dz [B, T, 4HP] fp32 out (kernel order); dh0 / dc0 [B, H] out
+template <int KS, int RT>
+__global__ __launch_bounds__(128 * KS) void lstm_bwd_f32_kernel(
+    const float* __restrict__ dhseq, const float* __restrict__ gates, const float* __restrict__ cseq,
+    const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
+    const float* __restrict__ wfragT, int B, int T, int H, float* __restrict__ dz, float* __restrict__ dh0,
+    float* __restrict__ dc0) {
+  constexpr int HP = 32 * KS, G4P = 4 * HP, KB = G4P / 4, LZ = G4P + 1;
+  __shared__ float zbuf[RT * 16][LZ];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, quad = lane >> 4;
+  const int u0 = 16 * w + 4 * quad, kc0 = 64 * w + 4 * quad;
+  const long long row0 = (long long)blockIdx.x * (RT * 16);
+  const long long TG = (long long)T * G4P, THP = (long long)T * HP, TH = (long long)T * H;
+  const bool vec_h = (H & 3) == 0;
+
+  float wb[KB];
+#pragma unroll
+  for (int s = 0; s < KB; ++s) wb[s] = wfragT[(w * KB + s) * 64 + lane];
+
+  int lrow[RT];
+  bool rok[RT];
+  f32x4 dhr[RT], dcc[RT], cinit[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int lr = rt * 16 + col;
+    rok[rt] = row0 + lr < B;
+    lrow[rt] = rok[rt] ? lr : (int)(B - 1 - row0);
+    const long long grow = row0 + lrow[rt];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = u0 + r < H;
+      dhr[rt][r] = (ok && dhn) ? dhn[grow * H + u0 + r] : 0.f;
+      dcc[rt][r] = (ok && dcn) ? dcn[grow * H + u0 + r] : 0.f;
+      cinit[rt][r] = (ok && c0) ? c0[grow * H + u0 + r] : 0.f;
+    }
+  }
+  f32x4 pg[RT][4], pc[RT], pp[RT], pd[RT];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const long long grow = row0 + lrow[rt];
+      const float* gp = gates + grow * TG + (long long)t * G4P + kc0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pg[rt][g] = *reinterpret_cast<const f32x4*>(gp + 16 * g);
+      const float* cp = cseq + grow * THP + (long long)t * HP + u0;
+      pc[rt] = *reinterpret_cast<const f32x4*>(cp);
+      pp[rt] = t > 0 ? *reinterpret_cast<const f32x4*>(cp - HP) : cinit[rt];
+      const float* dp = dhseq + grow * TH + (long long)t * H + u0;
+      if (vec_h) {
+        pd[rt] = u0 < H ? *reinterpret_cast<const f32x4*>(dp) : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pd[rt][r] = u0 + r < H ? dp[r] : 0.f;
+      }
+    }
+  };
+  fetch(T - 1);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) dhr[rt] += pd[rt];
+  for (int t = T - 1; t >= 0; --t) {
+    f32x4 zi[RT], zf[RT], zg[RT], zo[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ig = pg[rt][0][r], fg = pg[rt][1][r], gg = pg[rt][2][r], og = pg[rt][3][r];
+        const float dh = dhr[rt][r];
+        const float tc = tanh_(pc[rt][r]);
+        const float dc = dcc[rt][r] + dh * og * (1.f - tc * tc);
+        zo[rt][r] = dh * tc * og * (1.f - og);
+        zi[rt][r] = dc * gg * ig * (1.f - ig);
+        zg[rt][r] = dc * ig * (1.f - gg * gg);
+        zf[rt][r] = dc * pp[rt][r] * fg * (1.f - fg);
+        dcc[rt][r] = dc * fg;
+      }
+    if (t > 0) {
+      fetch(t - 1);
+    } else {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) pd[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float* zr = &zbuf[rt * 16 + col][u0];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        zr[r] = zi[rt][r];
+        zr[HP + r] = zf[rt][r];
+        zr[2 * HP + r] = zg[rt][r];
+        zr[3 * HP + r] = zo[rt][r];
+      }
+      if (rok[rt]) {
+        float* zp = dz + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
+        *reinterpret_cast<f32x4*>(zp) = zi[rt];
+        *reinterpret_cast<f32x4*>(zp + 16) = zf[rt];
+        *reinterpret_cast<f32x4*>(zp + 32) = zg[rt];
+        *reinterpret_cast<f32x4*>(zp + 48) = zo[rt];
+      }
+    }
+    __syncthreads();
+    f32x4 acc[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KB; ++s)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[s], zbuf[rt * 16 + col][4 * s + quad], acc[rt], 0, 0, 0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) dhr[rt] = acc[rt] + pd[rt];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+    if (rok[rt]) {
+      const long long grow = row0 + lrow[rt];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (u0 + r < H) {
+          dh0[grow * H + u0 + r] = dhr[rt][r];
+          dc0[grow * H + u0 + r] = dcc[rt][r];
+        }
+    }
+}
+
+}  // namespace
+
+namespace avk {
+
+// RT = 1 throughout: the f32 weight fragments take HP (forward) / 4·HP/4 (backward) VGPRs per
+// lane, leaving no room for a second tile's accumulators at HP = 128.
+void lstm_fwd_f32(const float* xw, const float* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
+                  float* hseq, float* cseq, float* gates, hipStream_t s) {
+  const int grid = (B + 15) / 16;
+  switch (KS) {
+    case 1: lstm_fwd_f32_kernel<1, 1><<<grid, 128, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates); break;
+    case 2: lstm_fwd_f32_kernel<2, 1><<<grid, 256, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates); break;
+    case 4: lstm_fwd_f32_kernel<4, 1><<<grid, 512, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates); break;
+    default: throw std::runtime_error("lstm_fwd_f32: KS in {1, 2, 4}");
+  }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void lstm_bwd_f32(const float* dhseq, const float* gates, const float* cseq, const float* c0, const float* dhn,
+                  const float* dcn, const float* wfragT, int B, int T, int H, int KS, float* dz, float* dh0,
+                  float* dc0, hipStream_t s) {
+  const int grid = (B + 15) / 16;
+  switch (KS) {
+    case 1:
+      lstm_bwd_f32_kernel<1, 1><<<grid, 128, 0, s>>>(dhseq, gates, cseq, c0, dhn, dcn, wfragT, B, T, H, dz, dh0, dc0);
+      break;
+    case 2:
+      lstm_bwd_f32_kernel<2, 1><<<grid, 256, 0, s>>>(dhseq, gates, cseq, c0, dhn, dcn, wfragT, B, T, H, dz, dh0, dc0);
+      break;
+    case 4:
+      lstm_bwd_f32_kernel<4, 1><<<grid, 512, 0, s>>>(dhseq, gates, cseq, c0, dhn, dcn, wfragT, B, T, H, dz, dh0, dc0);
+      break;
+    default: throw std::runtime_error("lstm_bwd_f32: KS in {1, 2, 4}");
+  }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace avk

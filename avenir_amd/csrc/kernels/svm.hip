@@ -1234,6 +1234,259 @@ __global__ __launch_bounds__(256) void rbf_matrix_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Implicit kernel (avk::SvmKerX): the working-set solver recomputes the kernel values it needs
+// from the rows of X instead of reading an N x N matrix.  Per outer step it needs K[ws, ws]
+// (Q x Q, the sub-problem) and K[ws, :] (Q x N, the gradient update).  Recomputing the Q x N block
+// costs Q N D FMAs: at N = 262 144, D = 16, Q = 128 that is 0.5 GFLOP, ~10 us of VALU — less than
+// READING those 134 MB from an HBM row cache (27 us at 5 TB/s), so no cache is kept at all and
+// memory is O(N D): the N x N matrix (275 GB at N = 262 144) is never formed.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float kfun_dot(int kind, float dot, float ni, float nj, float gamma, float coef0, int deg) {
+  switch (kind) {
+    case 0:
+      return dot;
+    case 1: {
+      const float base = gamma * dot + coef0;
+      float r = 1.f;
+      for (int i = 0; i < deg; ++i) r *= base;
+      return r;
+    }
+    case 2:
+      return __expf(-gamma * fmaxf(ni + nj - 2.f * dot, 0.f));
+    default:
+      return tanhf(gamma * dot + coef0);
+  }
+}
+
+// K[ws_p, ws_q] of every problem: one workgroup per (p, problem), thread q; RBF from the squared
+// differences (no cancellation), the others from the dot product
+__global__ __launch_bounds__(WS_Q) void smo_ws_gather_x_kernel(const avk::SvmKerX k, const long long* __restrict__ ws,
+                                                               const bool* __restrict__ ok, float* __restrict__ Kws,
+                                                               int N, const float* __restrict__ gap, float skip) {
+  constexpr int Q = WS_Q;
+  const int b = blockIdx.y, p = blockIdx.x, q = threadIdx.x;
+  if (ws_done(gap, b, skip)) return;
+  const long long* wb = ws + (long long)b * Q;
+  const bool* ob = ok + (long long)b * Q;
+  const long long rp = ob[p] ? wb[p] : 0, rq = ob[q] ? wb[q] : 0;
+  const float* X = k.X + (long long)b * k.xbs * k.D;
+  const float* xp = X + rp * k.D;
+  const float* xq = X + rq * k.D;
+  float acc = 0.f;
+  if (k.kind == 2) {
+    for (int d = 0; d < k.D; ++d) {
+      const float df = xp[d] - xq[d];
+      acc = fmaf(df, df, acc);
+    }
+    Kws[((long long)b * Q + p) * Q + q] = __expf(-k.gamma * acc);
+    return;
+  }
+  for (int d = 0; d < k.D; ++d) acc = fmaf(xp[d], xq[d], acc);
+  Kws[((long long)b * Q + p) * Q + q] = kfun_dot(k.kind, acc, 0.f, 0.f, k.gamma, k.coef0, k.degree);
+}
+
+// compaction of the working set's non-zero (index, dA) pairs into LDS by wave 0 (q order)
+__device__ __forceinline__ void ws_compact(const long long* __restrict__ ws, const float* __restrict__ dA,
+                                           const bool* __restrict__ ok, int b, int Q, long long* s_ws, float* s_d,
+                                           int* s_cnt) {
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  for (int q0 = 0; q0 < Q; q0 += 64) {
+    const int q = q0 + lane;
+    float d = 0.f;
+    long long r = 0;
+    if (q < Q && ok[(long long)b * Q + q]) {
+      d = dA[(long long)b * Q + q];
+      r = ws[(long long)b * Q + q];
+    }
+    const bool nz = d != 0.f;
+    const unsigned long long bal = __ballot(nz);
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    if (nz) {
+      const int kk = base + (int)__popcll(bal & below);
+      s_ws[kk] = r;
+      s_d[kk] = d;
+    }
+    base += (int)__popcll(bal);
+  }
+  if (lane == 0) *s_cnt = base;
+}
+
+// G[n] += y[n] sum_q dA_q k(x_ws_q, x_n), D <= DP <= 64: one thread per column n, x_n in registers,
+// the (<= Q) working-set rows in LDS (every lane reads the same word: broadcast), RBF from squared
+// differences.  Grid (N / 256, B).
+constexpr int UPX_T = 256;
+template <int DP>
+__global__ __launch_bounds__(UPX_T) void smo_ws_update_x_kernel(const avk::SvmKerX k, const long long* __restrict__ ws,
+                                                                const float* __restrict__ dA, const bool* __restrict__ ok,
+                                                                const float* __restrict__ y, float* __restrict__ G, int N,
+                                                                int ldag, int Q, const float* __restrict__ gap,
+                                                                float skip) {
+  __shared__ long long s_ws[WS_Q];
+  __shared__ float s_d[WS_Q];
+  __shared__ float s_x[WS_Q][DP];
+  __shared__ int s_cnt;
+  const int b = blockIdx.y;
+  if (ws_done(gap, b, skip)) return;
+  if (threadIdx.x < 64) ws_compact(ws, dA, ok, b, Q, s_ws, s_d, &s_cnt);
+  __syncthreads();
+  const int cnt = s_cnt;
+  if (cnt == 0) return;
+  const int D = k.D;
+  const float* X = k.X + (long long)b * k.xbs * D;
+  for (int e = threadIdx.x; e < cnt * DP; e += UPX_T) {
+    const int q = e / DP, d = e % DP;
+    s_x[q][d] = d < D ? X[s_ws[q] * D + d] : 0.f;
+  }
+  __syncthreads();
+  const int n = blockIdx.x * UPX_T + threadIdx.x;
+  if (n >= N) return;
+  float xr[DP];
+#pragma unroll
+  for (int d = 0; d < DP; ++d) xr[d] = d < D ? X[(long long)n * D + d] : 0.f;
+  float acc = 0.f;
+  if (k.kind == 2) {
+    const float ng = -k.gamma;
+    for (int q = 0; q < cnt; ++q) {
+      float d2 = 0.f;
+#pragma unroll
+      for (int d = 0; d < DP; ++d) {
+        const float df = s_x[q][d] - xr[d];
+        d2 = fmaf(df, df, d2);
+      }
+      acc = fmaf(s_d[q], __expf(ng * d2), acc);
+    }
+  } else {
+    for (int q = 0; q < cnt; ++q) {
+      float dot = 0.f;
+#pragma unroll
+      for (int d = 0; d < DP; ++d) dot = fmaf(s_x[q][d], xr[d], dot);
+      acc = fmaf(s_d[q], kfun_dot(k.kind, dot, 0.f, 0.f, k.gamma, k.coef0, k.degree), acc);
+    }
+  }
+  G[(long long)b * ldag + n] += y[(long long)b * N + n] * acc;
+}
+
+// The same update for any D through f32 MFMA: the Q x 64 block of dot products of a workgroup (4
+// waves x 16 columns, 8 row tiles of 16 per wave) accumulates v_mfma_f32_16x16x4_f32 over D in LDS
+// chunks of 64 (working-set rows and the 64 column rows staged per chunk), then the epilogue maps
+// each dot product through the kernel, weights it by dA_q and reduces over q: the 4 rows a lane
+// holds per tile, then the 4 lane groups (xor-16 / xor-32 shuffles).  C/D map of 16x16x4:
+// col = lane & 15, row = 4 (lane >> 4) + reg.
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int UPM_T = 256, UPM_KC = 64;
+__global__ __launch_bounds__(UPM_T) void smo_ws_update_x_mfma_kernel(const avk::SvmKerX k,
+                                                                     const long long* __restrict__ ws,
+                                                                     const float* __restrict__ dA,
+                                                                     const bool* __restrict__ ok,
+                                                                     const float* __restrict__ y, float* __restrict__ G,
+                                                                     int N, int ldag, int Q,
+                                                                     const float* __restrict__ gap, float skip) {
+  __shared__ long long s_ws[WS_Q];
+  __shared__ float s_d[WS_Q];
+  __shared__ float s_nq[WS_Q];
+  __shared__ float s_a[WS_Q][UPM_KC + 1];
+  __shared__ float s_b[64][UPM_KC + 1];
+  __shared__ int s_cnt;
+  const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (ws_done(gap, b, skip)) return;
+  if (threadIdx.x < 64) ws_compact(ws, dA, ok, b, Q, s_ws, s_d, &s_cnt);
+  __syncthreads();
+  const int cnt = s_cnt;
+  if (cnt == 0) return;
+  const int D = k.D;
+  const float* X = k.X + (long long)b * k.xbs * D;
+  const float* xn = k.xn + (long long)b * k.xbs;
+  for (int q = threadIdx.x; q < WS_Q; q += UPM_T) {
+    s_nq[q] = q < cnt ? xn[s_ws[q]] : 0.f;
+    if (q >= cnt) s_d[q] = 0.f;
+  }
+  const int n0 = blockIdx.x * 64;
+  const int tiles = (cnt + 15) / 16;
+  f32x4 acc[WS_Q / 16];
+#pragma unroll
+  for (int t = 0; t < WS_Q / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < D; kc += UPM_KC) {
+    __syncthreads();  // the previous chunk is consumed
+    const int kw = min(UPM_KC, D - kc);
+    for (int e = threadIdx.x; e < tiles * 16 * UPM_KC; e += UPM_T) {
+      const int q = e / UPM_KC, d = e % UPM_KC;
+      s_a[q][d] = (q < cnt && d < kw) ? X[s_ws[q] * D + kc + d] : 0.f;
+    }
+    for (int e = threadIdx.x; e < 64 * UPM_KC; e += UPM_T) {
+      const int c = e / UPM_KC, d = e % UPM_KC;
+      s_b[c][d] = (n0 + c < N && d < kw) ? X[(long long)(n0 + c) * D + kc + d] : 0.f;
+    }
+    __syncthreads();
+    const int col = w * 16 + (lane & 15), kq = lane >> 4;
+    for (int kk = 0; kk < kw; kk += 4) {
+      const float bv = s_b[col][kk + kq];
+#pragma unroll
+      for (int t = 0; t < WS_Q / 16; ++t)
+        if (t < tiles) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(s_a[t * 16 + (lane & 15)][kk + kq], bv, acc[t], 0, 0, 0);
+    }
+  }
+  const int n = n0 + w * 16 + (lane & 15);
+  const float nn = n < N ? xn[n] : 0.f;
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < WS_Q / 16; ++t) {
+    if (t >= tiles) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = t * 16 + 4 * (lane >> 4) + r;
+      part = fmaf(s_d[q], kfun_dot(k.kind, acc[t][r], s_nq[q], nn, k.gamma, k.coef0, k.degree), part);
+    }
+  }
+  part += __shfl_xor(part, 16, 64);
+  part += __shfl_xor(part, 32, 64);
+  if (lane < 16 && n < N) G[(long long)b * ldag + n] += y[(long long)b * N + n] * part;
+}
+
+// K[i][j] = k(a_i, b_j) for any d by f32 MFMA: a 64 x 64 output tile per workgroup, wave w owns rows
+// 16w..16w+15 (4 column tiles of 16), D in LDS chunks of 64; the epilogue applies the kernel
+// (RBF from the norms) and writes 16-float row segments.
+__global__ __launch_bounds__(256) void kernel_matrix_mfma_kernel(const avk::SvmKerX a, const float* __restrict__ Bx,
+                                                                 const float* __restrict__ bn, int na, int nb,
+                                                                 float* __restrict__ K) {
+  __shared__ float sa[64][UPM_KC + 1], sb[64][UPM_KC + 1];
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int D = a.D;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < D; kc += UPM_KC) {
+    __syncthreads();
+    const int kw = min(UPM_KC, D - kc);
+    for (int e = threadIdx.x; e < 64 * UPM_KC; e += 256) {
+      const int r = e / UPM_KC, d = e % UPM_KC;
+      sa[r][d] = (i0 + r < na && d < kw) ? a.X[(long long)(i0 + r) * D + kc + d] : 0.f;
+      sb[r][d] = (j0 + r < nb && d < kw) ? Bx[(long long)(j0 + r) * D + kc + d] : 0.f;
+    }
+    __syncthreads();
+    const int kq = lane >> 4;
+    for (int kk = 0; kk < kw; kk += 4) {
+      const float av = sa[w * 16 + (lane & 15)][kk + kq];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sb[t * 16 + (lane & 15)][kk + kq],
+                                                                              acc[t], 0, 0, 0);
+    }
+  }
+  // acc[t][r]: row i = i0 + 16 w + 4 (lane >> 4) + r, column j = j0 + 16 t + (lane & 15)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = j0 + 16 * t + (lane & 15);
+    const float nj = j < nb ? bn[j] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 16 * w + 4 * (lane >> 4) + r;
+      if (i < na && j < nb)
+        K[(long long)i * nb + j] = kfun_dot(a.kind, acc[t][r], a.xn[i], nj, a.gamma, a.coef0, a.degree);
+    }
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -1257,6 +1510,38 @@ void smo_solve(const float* K, const float* y, const float* diag, float* alpha, 
 }
 
 int smo_ws_size() { return WS_Q; }
+
+void smo_ws_gather_x(const SvmKerX& k, const long long* ws, const bool* ok, float* Kws, int B, int N, const float* gap,
+                     float skip, hipStream_t stream) {
+  if (B <= 0) return;
+  smo_ws_gather_x_kernel<<<dim3(WS_Q, B), WS_Q, 0, stream>>>(k, ws, ok, Kws, N, gap, skip);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void smo_ws_update_x(const SvmKerX& k, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
+                     int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream) {
+  if (B <= 0 || N <= 0) return;
+  if (Q > WS_Q) throw std::runtime_error("smo_ws_update_x: Q <= 128");
+  if (k.D > 64 || std::getenv("AVMI_SVM_MFMA_UPDATE")) {
+    smo_ws_update_x_mfma_kernel<<<dim3((N + 63) / 64, B), UPM_T, 0, stream>>>(k, ws, dA, ok, y, G, N, ldag, Q, gap, skip);
+  } else {
+    const dim3 grid((N + UPX_T - 1) / UPX_T, B);
+#define AV_UX(DP) smo_ws_update_x_kernel<DP><<<grid, UPX_T, 0, stream>>>(k, ws, dA, ok, y, G, N, ldag, Q, gap, skip)
+    if (k.D <= 8) AV_UX(8);
+    else if (k.D <= 16) AV_UX(16);
+    else if (k.D <= 32) AV_UX(32);
+    else AV_UX(64);
+#undef AV_UX
+  }
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+void svm_kernel_matrix_mfma(const SvmKerX& a, const float* Bx, const float* bn, int na, int nb, float* K,
+                            hipStream_t stream) {
+  if (na <= 0 || nb <= 0) return;
+  kernel_matrix_mfma_kernel<<<dim3((nb + 63) / 64, (na + 63) / 64), 256, 0, stream>>>(a, Bx, bn, na, nb, K);
+  AV_HIP_CHECK(hipGetLastError());
+}
 
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream) {
@@ -1365,7 +1650,7 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, long long kbs, hipStream_t caller) {
+                     float* host_gap, long long kbs, hipStream_t caller, const SvmKerX* kx) {
   if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
   const int Q = WS_Q, h = WS_Q / 2;
   check_every = check_every < 1 ? 1 : check_every;
@@ -1380,6 +1665,14 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
   auto enqueue = [&](long long n) {
     for (long long s = 0; s < n; ++s) {
       smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream);
+      if (kx) {  // implicit kernel: K[ws, ws] and the gradient update from the rows of X
+        smo_ws_gather_x(*kx, ws, ok, Kws, B, N, gap, eps, stream);
+        smo_ws_solve_kernel<<<B, WSS_T, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, rel_tol,
+                                                     inner_iter, dA, inner_total);
+        AV_HIP_CHECK(hipGetLastError());
+        smo_ws_update_x(*kx, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);
+        continue;
+      }
       smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws, rel_tol,
                          kbs, stream);
       smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, kbs, stream);

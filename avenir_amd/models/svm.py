@@ -7,10 +7,16 @@ so the reference SVM cannot train at all), the cascade ``SupportVectorMachine`` 
 of support vectors), and the sklearn wrapper ``SupportVectorMachine`` (P/supv/svm.py:83-121:
 svc with linear / poly / rbf / sigmoid kernels, C, gamma).
 
-MI355X design: K = kernel(X X^T) is one GEMM + an elementwise epilogue; the whole SMO loop
-(second-order working-set selection, two-variable solve, gradient update) runs inside one
-persistent 1024-thread workgroup per problem (svm.hip), and B problems — one-vs-rest classes or
-cascade shards — are B workgroups of ONE launch.  The CPU path runs the same algorithm in numpy.
+MI355X design: small problems build K = kernel(X X^T) once (the fused RBF pass for d <= 64, f32
+MFMA for any other d / kernel) and run SMO inside one persistent workgroup per problem (svm.hip);
+larger ones run the working-set decomposition, either over that dense K or — above
+``DENSE_MAX_N`` rows, or when K would not fit — over an IMPLICIT kernel: every outer step
+recomputes the Q x Q sub-problem block and the Q x N gradient-update rows from the rows of X
+(``smo_ws_run_x``; VALU from squared differences for d <= 64, f32 MFMA beyond).  Recomputing those
+Q N D FMAs is cheaper than reading the same rows from an HBM row cache, so memory is O(N D):
+N = 262 144 x 16 needs ~30 MB instead of the 275 GB N x N matrix.  B problems — one-vs-rest
+classes or cascade shards — are B workgroups of ONE launch.  The CPU path runs the same algorithm
+in numpy.
 """
 from __future__ import annotations
 
@@ -24,13 +30,21 @@ from ..parallel.comm import Comm, get_comm
 from ..utils.tracing import traced
 
 
+KERNEL_KIND = {"linear": 0, "poly": 1, "rbf": 2, "sigmoid": 3}
+
+
 def kernel_matrix(A: torch.Tensor, B: torch.Tensor, kernel: str = "rbf", gamma: float = 1.0, degree: int = 3,
                   coef0: float = 0.0) -> torch.Tensor:
-    """K(A, B) [na, nb] float32 from one GEMM (RBF on the GPU with d <= 64: one fused pass of the
-    ``rbf_matrix`` kernel from squared differences)."""
+    """K(A, B) [na, nb] float32.  GPU: RBF with d <= 64 is one fused pass of the ``rbf_matrix``
+    kernel from squared differences; every other (kernel, d) is the f32-MFMA tile kernel
+    (``svm_kernel_matrix``, v_mfma_f32_16x16x4_f32) with the kernel applied in its epilogue.
+    CPU: one GEMM + the elementwise kernel."""
     A, B = A.float(), B.float()
-    if kernel == "rbf" and A.is_cuda and 1 <= A.shape[1] <= 64 and A.shape[0] and B.shape[0]:
-        return _native.C().rbf_matrix(A.contiguous(), B.contiguous(), float(gamma))
+    if A.is_cuda and A.shape[0] and B.shape[0] and kernel in KERNEL_KIND:
+        if kernel == "rbf" and 1 <= A.shape[1] <= 64:
+            return _native.C().rbf_matrix(A.contiguous(), B.contiguous(), float(gamma))
+        return _native.C().svm_kernel_matrix(A.contiguous(), B.contiguous(), KERNEL_KIND[kernel], float(gamma),
+                                             float(coef0), int(degree))
     dot = A @ B.T
     if kernel == "linear":
         return dot
@@ -42,6 +56,49 @@ def kernel_matrix(A: torch.Tensor, B: torch.Tensor, kernel: str = "rbf", gamma: 
         na, nb = (A * A).sum(1), (B * B).sum(1)
         return torch.exp(-gamma * (na.view(-1, 1) + nb.view(1, -1) - 2 * dot).clamp_min(0))
     raise ValueError(f"unknown kernel {kernel}")
+
+
+class ImplicitKernel:
+    """The kernel of B problems as the rows of X instead of an N x N matrix: X [N, D] (shared by all
+    problems) or [B, N, D] (one row set per problem, e.g. cascade shards), squared norms, kernel
+    parameters.  ``dense()`` materialises K for small problems and the CPU path."""
+
+    def __init__(self, X: torch.Tensor, kernel: str = "rbf", gamma: float = 1.0, coef0: float = 0.0, degree: int = 3):
+        self.X = X.float().contiguous()
+        self.xn = (self.X * self.X).sum(-1).contiguous()
+        self.kernel, self.kind = kernel, KERNEL_KIND[kernel]
+        self.gamma, self.coef0, self.degree = float(gamma), float(coef0), int(degree)
+
+    @property
+    def device(self) -> torch.device:
+        return self.X.device
+
+    @property
+    def N(self) -> int:
+        return int(self.X.shape[-2])
+
+    def dense(self) -> torch.Tensor:
+        """[B or 1, N, N]."""
+        Xs = self.X if self.X.dim() == 3 else self.X.unsqueeze(0)
+        return torch.stack([kernel_matrix(x, x, self.kernel, self.gamma, self.degree, self.coef0) for x in Xs])
+
+    def args(self) -> tuple:
+        return (self.X, self.xn, self.kind, self.gamma, self.coef0, self.degree)
+
+
+#: above this many rows (or when the dense matrices would not fit in free memory) the working-set
+#: solver runs on the implicit kernel
+DENSE_MAX_N = int(__import__("os").environ.get("AVMI_SVM_DENSE_MAX_N", "16384"))
+
+
+def use_implicit(n: int, n_mats: int, device) -> bool:
+    """Whether a problem of ``n`` rows (``n_mats`` dense N x N matrices) takes the implicit kernel."""
+    if torch.device(device).type != "cuda":
+        return False
+    if n > DENSE_MAX_N:
+        return True
+    free, _ = torch.cuda.mem_get_info(torch.device(device))
+    return 4.0 * n * n * n_mats > 0.5 * free
 
 
 def smo_reference(K: np.ndarray, y: np.ndarray, C: float, eps: float = 1e-3, max_iter: int = 100000,
@@ -236,6 +293,24 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     if rel_tol is None:   # sub-problem tolerance max(eps, rel_tol * gap) of the fused GPU solver
         import os
         rel_tol = float(os.environ.get("AVMI_SMO_REL_TOL", "0.3"))
+    if isinstance(K, ImplicitKernel):
+        if K.device.type != "cuda":
+            return smo_decomposition(K.dense(), y, C, eps, max_outer, inner_iter, check_every, Q, graph, fused,
+                                     rel_tol)
+        # the native loop over the implicit kernel: K[ws, ws] and the Q x N update rows from X
+        B, N = y.shape
+        dev = K.device
+        yf = y.float().contiguous()
+        alpha = torch.zeros((B, N + 1), device=dev)
+        G = torch.where(torch.cat([yf, torch.zeros((B, 1), device=dev)], 1) != 0, -1.0, 0.0).contiguous()
+        ws = torch.zeros((B, Q), dtype=torch.long, device=dev)
+        ok = torch.zeros((B, Q), dtype=torch.bool, device=dev)
+        dA = torch.zeros((B, Q), device=dev)
+        inner_total = torch.zeros(B, dtype=torch.long, device=dev)
+        gap = torch.full((B,), float("inf"), device=dev)
+        outer = int(_native.C().smo_ws_run_x(*K.args(), alpha, G, yf, float(C), float(eps), int(inner_iter),
+                                             float(rel_tol), int(max_outer), 8, ws, ok, dA, inner_total, gap))
+        return alpha[:, :N].contiguous(), G[:, :N].contiguous(), outer, inner_total
     st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused, rel_tol)
     outer = 0
     import os
@@ -285,18 +360,28 @@ LAST_SOLVE: dict = {}   # outer-step count of the last working-set solve (benchm
 def smo_batch(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1e-3, max_iter: int = 1_000_000,
               solver: str = "auto"):
     """Solve B SVM duals: K [B, N, N] (or [1, N, N] shared by all B problems — one-vs-rest classes
-    — which the working-set kernels read in place instead of B copies), y [B, N] in {-1, 0 (padding),
-    +1}.  Returns (alpha, rho, iters).
+    — which the working-set kernels read in place instead of B copies) or an :class:`ImplicitKernel`
+    (rows of X, no N x N matrix), y [B, N] in {-1, 0 (padding), +1}.  Returns (alpha, rho, iters).
     ``solver``: "full" (one persistent workgroup runs plain SMO over all N), "ws" (working-set
-    decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N).
+    decomposition, ``smo_decomposition``) or "auto" (ws on the GPU for N > WS_MIN_N, always for an
+    implicit kernel).
 
-    ``max_iter`` bounds the two-variable SMO steps on every path: the full solver counts them
-    directly; the working-set solver runs at most ``max(1, max_iter // 64)`` outer steps of at most
-    ``inner_iter`` sub-problem steps each (a sub-problem takes tens of steps, so a cap of
-    ``max_iter // inner_iter`` outer steps stopped large problems before convergence).  ``iters`` is the number of two-variable steps
-    taken per problem in both cases (for the working-set path: the inner steps summed over the
-    outer steps)."""
+    Iteration caps: the full solver stops after ``max_iter`` two-variable steps.  The working-set
+    solver stops after ``max(1, max_iter // 64)`` OUTER steps, each solving its sub-problem with
+    at most ``min(2048, max_iter)`` two-variable steps — so its total two-variable step count can
+    exceed ``max_iter`` (by up to 32x); ``max_iter`` is a bound on the outer work there, not on the
+    inner steps (a cap of ``max_iter // inner_iter`` outer steps stopped large problems before
+    convergence).  ``iters`` is the number of two-variable steps taken per problem in both cases
+    (for the working-set path: the inner steps summed over the outer steps)."""
     B, N = y.shape
+    if isinstance(K, ImplicitKernel):
+        if K.device.type != "cuda":      # CPU: the same solvers over the materialised matrix
+            return smo_batch(K.dense(), y, C, eps, max_iter, solver)
+        inner_iter = min(2048, max(1, max_iter))
+        alpha, G, outer, inner = smo_decomposition(K, y, C, eps, max_outer=max(1, max_iter // 64),
+                                                   inner_iter=inner_iter)
+        LAST_SOLVE.update(solver="ws-implicit", outer=outer)
+        return alpha, _rho(alpha, G, y.float(), C), inner.int()
     if solver == "ws" or (solver == "auto" and K.device.type == "cuda" and N > WS_MIN_N):
         inner_iter = min(2048, max(1, max_iter))
         alpha, G, outer, inner = smo_decomposition(K, y, C, eps, max_outer=max(1, max_iter // 64),
@@ -356,13 +441,17 @@ class SVC:
         y = torch.as_tensor(y, device=X.device).long().view(-1)
         self.classes = torch.unique(y).tolist()
         self.g = self._gamma(X)
-        K = kernel_matrix(X, X, self.kernel, self.g, self.degree, self.coef0)
+        if use_implicit(X.shape[0], 1, X.device):
+            K = ImplicitKernel(X, self.kernel, self.g, self.coef0, self.degree)
+        else:
+            K = kernel_matrix(X, X, self.kernel, self.g, self.degree, self.coef0)
         if len(self.classes) == 2:
             ys = torch.where(y == self.classes[1], 1.0, -1.0).view(1, -1)
         else:
             ys = torch.stack([torch.where(y == c, 1.0, -1.0) for c in self.classes])
         # one K for all one-vs-rest problems (smo_batch broadcasts it where a solver needs copies)
-        alpha, rho, iters = smo_batch(K.unsqueeze(0), ys.to(X.device), self.C, self.eps, self.max_iter)
+        alpha, rho, iters = smo_batch(K if isinstance(K, ImplicitKernel) else K.unsqueeze(0), ys.to(X.device),
+                                      self.C, self.eps, self.max_iter)
         self.iters = iters.tolist()
         sv = (alpha > 0).any(0)
         self.support_ = sv.nonzero().view(-1)
@@ -373,8 +462,13 @@ class SVC:
 
     def decision_function(self, X) -> torch.Tensor:
         X = torch.as_tensor(X).float().to(self.sv_X.device)
-        Kx = kernel_matrix(self.sv_X, X, self.kernel, self.g, self.degree, self.coef0)   # [nsv, n]
-        f = self.dual_coef @ Kx - self.rho.view(-1, 1)
+        # blocks of query rows: [nsv, block] kernel tiles stay bounded for any number of queries
+        blk = max(1, (1 << 28) // max(1, self.sv_X.shape[0]))
+        outs = []
+        for s in range(0, X.shape[0], blk):
+            Kx = kernel_matrix(self.sv_X, X[s:s + blk], self.kernel, self.g, self.degree, self.coef0)   # [nsv, n]
+            outs.append(self.dual_coef @ Kx - self.rho.view(-1, 1))
+        f = torch.cat(outs, 1) if outs else torch.zeros((self.dual_coef.shape[0], 0), device=X.device)
         return f[0] if f.shape[0] == 1 else f.T
 
     def predict(self, X) -> torch.Tensor:
@@ -410,13 +504,23 @@ class CascadeSVM:
         n = X.shape[0]
         S = max(1, min(self.shards, n))
         m = (n + S - 1) // S
-        Kb = torch.zeros((S, m, m), dtype=torch.float32, device=X.device)
         yb = torch.zeros((S, m), dtype=torch.float32, device=X.device)
         ys = torch.where(y == classes[1], 1.0, -1.0)
-        for s in range(S):
-            lo, hi = s * m, min(n, (s + 1) * m)
-            Kb[s, : hi - lo, : hi - lo] = kernel_matrix(X[lo:hi], X[lo:hi], base.kernel, g, base.degree, base.coef0)
-            yb[s, : hi - lo] = ys[lo:hi]
+        if use_implicit(m, S, X.device):
+            # every shard's rows as one padded [S, m, D] block: B problems of ONE implicit solve
+            Xb = torch.zeros((S, m, X.shape[1]), dtype=torch.float32, device=X.device)
+            for s in range(S):
+                lo, hi = s * m, min(n, (s + 1) * m)
+                Xb[s, : hi - lo] = X[lo:hi]
+                yb[s, : hi - lo] = ys[lo:hi]
+            Kb = ImplicitKernel(Xb, base.kernel, g, base.coef0, base.degree)
+        else:
+            Kb = torch.zeros((S, m, m), dtype=torch.float32, device=X.device)
+            for s in range(S):
+                lo, hi = s * m, min(n, (s + 1) * m)
+                Kb[s, : hi - lo, : hi - lo] = kernel_matrix(X[lo:hi], X[lo:hi], base.kernel, g, base.degree,
+                                                            base.coef0)
+                yb[s, : hi - lo] = ys[lo:hi]
         alpha, _, _ = smo_batch(Kb, yb, base.C, base.eps, base.max_iter)
         keep = torch.cat([(alpha[s, : min(n, (s + 1) * m) - s * m] > 0) for s in range(S)])
         Xs, yv = X[keep], y[keep]

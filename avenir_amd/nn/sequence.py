@@ -26,13 +26,14 @@ class LstmNetwork(torch.nn.Module):
                  batch_size: int = 32, out_sequence: bool = False, out_activation: str | None = "sigmoid",
                  dropout: float = 0.0, loss: str = "mse", optimizer: str = "adam", lr: float = 1e-3,
                  grad_clip: float = 5.0, num_iter: int = 100, device=None, conf=None, graph: bool = True,
-                 precision: str = "bf16"):
+                 precision: str = "fp32"):
         super().__init__()
         self.input_size, self.hidden_size, self.output_size = input_size, hidden_size, output_size
         self.num_layers, self.seq_len, self.batch_size = num_layers, seq_len, batch_size
         self.out_seq, self.grad_clip, self.num_iter = out_sequence, grad_clip, num_iter
         # K27 fused LSTM (persistent HIP recurrence kernel on the GPU); nn.LSTM-compatible state dict
-        # precision="fp32": the reference's fp32 numerics (MIOpen fp32 LSTM on the GPU)
+        # precision="fp32" (default): the reference's fp32 numerics on the fused fp32 kernels;
+        # "bf16": the mixed-precision kernels; "miopen": torch.lstm
         self.lstm = FusedLSTM(input_size, hidden_size, num_layers, batch_first=True,
                               dropout=dropout if num_layers > 1 else 0.0, precision=precision)
         self.linear = torch.nn.Linear(hidden_size, output_size)
@@ -59,7 +60,7 @@ class LstmNetwork(torch.nn.Module):
                    grad_clip=float(_cfg(conf, "train.grad.clip", 5.0)),
                    num_iter=_cfg(conf, "train.num.iterations", 500),
                    device=device or _cfg(conf, "common.device", "auto"), conf=conf,
-                   precision=str(_cfg(conf, "train.precision", "bf16")))
+                   precision=str(_cfg(conf, "train.precision", "fp32")))
 
     # -- data --------------------------------------------------------------------------------------
     def to_sequences(self, rows: torch.Tensor) -> torch.Tensor:

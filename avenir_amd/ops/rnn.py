@@ -17,10 +17,14 @@ weight gradients are fp32.  ``lstm_reference`` is the fp32 oracle.
 Hidden or input sizes above 128 (beyond the register-resident design) use PyTorch's MIOpen LSTM
 on the GPU; that path is selected by shape, never by a missing extension.
 
-``FusedLSTM(precision="fp32")`` keeps the reference's numerics end to end (P/supv/lstm.py trains
-an fp32 ``nn.LSTM``): every op in fp32, on MIOpen's fp32 LSTM on the GPU.  The default
-``precision="bf16"`` is the fused mixed-precision kernel above; ``tests/test_rnn.py`` checks its
-training loss curve against an fp32 ``nn.LSTM`` from the same initialisation.
+``precision="fp32"`` (the DEFAULT, the reference's numerics: P/supv/lstm.py trains an fp32
+``nn.LSTM``) runs the fp32 twin of the kernels (csrc/kernels/rnn_f32.hip): the recurrence on
+v_mfma_f32_16x16x4_f32 with W_hh resident in VGPRs as f32 fragments, every stored intermediate
+fp32, and the input projection x·W_ihᵀ + b of all timesteps as one fp32 GEMM ahead of it (the f32
+fragments of W_hh alone take HP VGPRs).  Backward: one fp32 recurrence launch + fp32 GEMMs for
+dW_hh = dzᵀ·h_{t-1}, dW_ih = dzᵀ·x, db = Σdz and dx = dz·W_ih.  ``precision="bf16"`` opts into the
+mixed-precision kernel above.  Both are checked against the fp32 oracle and ``nn.LSTM``
+(tests/test_rnn.py).
 """
 from __future__ import annotations
 
@@ -57,6 +61,20 @@ def pack_weights(w_ih: torch.Tensor, w_hh: torch.Tensor, H: int) -> tuple[torch.
     wp = wcat[:, :, :HP].contiguous()
     bwd = wp.view(4, KS, 4, 8, NW, 16).permute(4, 0, 1, 2, 5, 3).contiguous().view(NW, 4 * KS, 4, 16, 8)
     return fwd.to(torch.bfloat16).contiguous(), bwd.to(torch.bfloat16).contiguous()
+
+
+def pack_weights_f32(w_hh: torch.Tensor, H: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """W_hh [4H, H] -> fp32 A-fragments of v_mfma_f32_16x16x4_f32 (forward [NW, 4, HP/4, 64],
+    backward [NW, HP, 64]).  Forward, wave w, gate g, k-step s: lane q*16 + col holds
+    W_hh[g*H + 16w + col, 4s + q].  Backward (dhᵀ = W_hhᵀ·dzᵀ, k over the 4·HP gate rows gate-major,
+    k = g·HP + u): lane q*16 + col of k-step s holds W_hh[row of k = 4s + q, 16w + col].  Padding 0."""
+    HP = padded_hidden(H)
+    NW, KS4 = HP // 16, HP // 4
+    wp = torch.zeros((4, HP, HP), device=w_hh.device, dtype=torch.float32)
+    wp[:, :H, :H] = w_hh.detach().float().view(4, H, H)
+    fwd = wp.view(4, NW, 16, KS4, 4).permute(1, 0, 3, 4, 2).contiguous().view(NW, 4, KS4, 64)
+    bwd = wp.reshape(4 * HP, HP).view(HP, 4, NW, 16).permute(2, 0, 1, 3).contiguous().view(NW, HP, 64)
+    return fwd, bwd
 
 
 def lstm_cell_reference(x, h, c, w_ih, w_hh, b):
@@ -110,6 +128,27 @@ def to_kernel_order(w: torch.Tensor, H: int) -> torch.Tensor:
     out = w.new_zeros((4 * padded_hidden(H),) + tuple(w.shape[1:]))
     out[valid_kc] = w[torch_row]
     return out
+
+
+class _FragCacheF32:
+    """The fp32 fragments of W_hh, keyed like :class:`_FragCache`."""
+
+    def __init__(self, size: int = 16):
+        self.size, self.d = size, {}
+
+    def get(self, w_hh: torch.Tensor, H: int):
+        if torch.cuda.is_current_stream_capturing():
+            return pack_weights_f32(w_hh, H)
+        key = (w_hh.data_ptr(), w_hh._version, tuple(w_hh.shape), H)
+        hit = self.d.get(key)
+        if hit is None:
+            if len(self.d) >= self.size:
+                self.d.pop(next(iter(self.d)))
+            hit = self.d[key] = pack_weights_f32(w_hh, H)
+        return hit
+
+
+_frags_f32 = _FragCacheF32()
 
 
 class _FragCache:
@@ -187,17 +226,68 @@ class _LstmLayer(torch.autograd.Function):
         return dx, dw_ih, dw_hh, db, (dh0 if need[4] else None), (dc0 if need[5] else None)
 
 
-def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None):
+class _LstmLayerF32(torch.autograd.Function):
+    """One fp32 layer: forward = one fp32 GEMM (input projection of all timesteps, kernel gate
+    order) + ONE recurrence launch; backward = one recurrence launch + fp32 GEMMs for dx, dW_ih,
+    dW_hh and db."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b, h0, c0):
+        B, T, I = x.shape
+        H = w_hh.shape[1]
+        HP = padded_hidden(H)
+        frag, frag_t = _frags_f32.get(w_hh, H)
+        w_ih_k = to_kernel_order(w_ih.detach().float(), H)                      # [4HP, I]
+        bias = to_kernel_order(b.detach().float(), H) if b is not None else None
+        x2 = x.reshape(B * T, I)
+        xw = (torch.addmm(bias, x2, w_ih_k.t()) if bias is not None else x2 @ w_ih_k.t()).view(B, T, 4 * HP)
+        need = any(ctx.needs_input_grad)
+        outs = _native.C().lstm_forward_f32(xw.contiguous(), frag, h0, c0, H, bool(need))
+        hseq, cseq = outs[0], outs[1]
+        if need:
+            ctx.save_for_backward(x, w_ih_k, hseq, cseq, outs[2], h0, c0, frag_t)
+        ctx.has_b, ctx.dims = b is not None, (B, T, I, H)
+        return hseq, hseq[:, -1], cseq[:, -1, :H]
+
+    @staticmethod
+    def backward(ctx, dhseq, dhn, dcn):
+        x, w_ih_k, hseq, cseq, gates, h0, c0, frag_t = ctx.saved_tensors
+        B, T, I, H = ctx.dims
+        HP = padded_hidden(H)
+        _, _, inv = kernel_gate_order(H, cseq.device)
+        if dhseq is None:
+            dhseq = cseq.new_zeros(B, T, H)
+        dz, dh0, dc0 = _native.C().lstm_backward_f32(dhseq.contiguous(), gates, cseq, c0,
+                                                     None if dhn is None else dhn.contiguous(),
+                                                     None if dcn is None else dcn.contiguous(), frag_t, H)
+        dz2 = dz.view(B * T, 4 * HP)                                   # fp32, kernel order
+        need = ctx.needs_input_grad
+        dx = (dz2 @ w_ih_k).view(B, T, I) if need[0] else None
+        dw_ih = dw_hh = db = None
+        if need[1]:
+            dw_ih = (dz2.t() @ x.reshape(B * T, I)).index_select(0, inv)
+        if need[2]:
+            hprev = torch.cat([h0.view(B, 1, H) if h0 is not None else hseq.new_zeros(B, 1, H), hseq[:, :-1]], 1)
+            dw_hh = (dz2.t() @ hprev.reshape(B * T, H)).index_select(0, inv)
+        if need[3] and ctx.has_b:
+            db = dz2.sum(0).index_select(0, inv)
+        return dx, dw_ih, dw_hh, db, (dh0 if need[4] else None), (dc0 if need[5] else None)
+
+
+def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None, precision: str = "fp32"):
     """One batch-first LSTM layer: (hseq [B,T,H], h_T [B,H], c_T [B,H]).
 
-    GPU tensors with H <= 128 run the fused HIP kernels (raising if the extension is missing);
-    CPU tensors run the fp32 reference.
-    """
+    GPU tensors with H <= 128 run the fused HIP kernels (raising if the extension is missing):
+    ``precision="fp32"`` the fp32 recurrence (any input size: the input projection is a GEMM),
+    ``"bf16"`` the mixed-precision kernel (input size <= 128 too).  CPU tensors run the fp32
+    reference."""
     H = w_hh.shape[1]
-    if x.is_cuda and H <= MAX_FUSED_HIDDEN and x.shape[-1] <= MAX_FUSED_HIDDEN:
+    if x.is_cuda and H <= MAX_FUSED_HIDDEN and (precision == "fp32" or x.shape[-1] <= MAX_FUSED_HIDDEN):
         x = x.float().contiguous()
         h0 = None if h0 is None else h0.float().contiguous()
         c0 = None if c0 is None else c0.float().contiguous()
+        if precision == "fp32":
+            return _LstmLayerF32.apply(x, w_ih, w_hh, b, h0, c0)
         return _LstmLayer.apply(x, w_ih, w_hh, b, h0, c0)
     hseq, (h, c) = lstm_reference(x, w_ih, w_hh, b, h0, c0)
     return hseq, h, c
@@ -208,12 +298,13 @@ class FusedLSTM(torch.nn.Module):
     dicts load either way.  ``forward(x, (h0, c0)) -> (out, (h_n, c_n))``."""
 
     def __init__(self, input_size: int, hidden_size: int, num_layers: int = 1, bias: bool = True,
-                 batch_first: bool = True, dropout: float = 0.0, precision: str = "bf16"):
+                 batch_first: bool = True, dropout: float = 0.0, precision: str = "fp32"):
         super().__init__()
         if not batch_first:
             raise ValueError("FusedLSTM is batch-first")
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be 'bf16' (fused mixed-precision kernel) or 'fp32', got {precision!r}")
+        if precision not in ("bf16", "fp32", "miopen"):
+            raise ValueError(f"precision must be 'fp32' (fused fp32 kernels, default), 'bf16' (fused "
+                             f"mixed-precision kernel) or 'miopen' (torch.lstm), got {precision!r}")
         self.precision = precision
         self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
         self.bias, self.dropout, self.batch_first = bias, float(dropout), True
@@ -242,8 +333,9 @@ class FusedLSTM(torch.nn.Module):
 
     def forward(self, x, hx=None):
         H, L = self.hidden_size, self.num_layers
-        if x.is_cuda and (H > MAX_FUSED_HIDDEN or self.input_size > MAX_FUSED_HIDDEN or self.precision == "fp32"):
-            # beyond the register-resident kernel, or fp32 numerics requested: MIOpen (fp32)
+        if x.is_cuda and (H > MAX_FUSED_HIDDEN or self.precision == "miopen"
+                          or (self.precision == "bf16" and self.input_size > MAX_FUSED_HIDDEN)):
+            # beyond the register-resident kernels, or MIOpen requested (fp32)
             if hx is None:
                 z = x.new_zeros(L, x.shape[0], H)
                 hx = (z, z)
@@ -258,7 +350,8 @@ class FusedLSTM(torch.nn.Module):
                 b = getattr(self, f"bias_ih_l{l}") + getattr(self, f"bias_hh_l{l}")
             h0 = hx[0][l] if hx is not None else None
             c0 = hx[1][l] if hx is not None else None
-            out, h, c = lstm_layer(out, getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"), b, h0, c0)
+            out, h, c = lstm_layer(out, getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"), b, h0, c0,
+                                   self.precision)
             hs.append(h)
             cs.append(c)
             if self.dropout > 0 and self.training and l < L - 1:
