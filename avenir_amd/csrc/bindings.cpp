@@ -3213,6 +3213,51 @@ std::vector<at::Tensor> lstm_forward(const at::Tensor& x, const at::Tensor& wfra
   return {hseq, cseq};
 }
 
+// K7 split scoring (split.hip): hist int64 [A, C, TBt]; sp int32 [R, 6] (feature, column, bins,
+// segments, valid, segment-map offset); seg int8 segment maps; cand uint8 [A, F].  Returns the k best
+// splits per node (index, score) and their segment class counts [A, k, G2, C] / impurities [A, k, G2].
+std::vector<at::Tensor> ref_split_score(const at::Tensor& hist, const at::Tensor& sp, const at::Tensor& seg,
+                                        const at::Tensor& cand, int64_t algo, int64_t k, int64_t G2) {
+  CHECK_DEV(hist);
+  CHECK_DTYPE(hist, at::kLong);
+  CHECK_DEV(sp);
+  CHECK_DTYPE(sp, at::kInt);
+  CHECK_DEV(seg);
+  CHECK_DTYPE(seg, at::kChar);
+  CHECK_DEV(cand);
+  CHECK_DTYPE(cand, at::kByte);
+  TORCH_CHECK(hist.dim() == 3 && hist.is_contiguous(), "hist must be [A, C, TB] contiguous");
+  const int64_t A = hist.size(0), C = hist.size(1), TBt = hist.size(2), R = sp.size(0);
+  TORCH_CHECK(sp.dim() == 2 && sp.size(1) == 6 && sp.is_contiguous() && R >= 1, "sp must be [R >= 1, 6]");
+  TORCH_CHECK(cand.dim() == 2 && cand.size(0) == A && cand.is_contiguous(), "cand must be [A, F]");
+  TORCH_CHECK(C >= 1 && C <= 32 && k >= 1 && k <= R && G2 >= 2 && G2 <= 64 && (algo == 0 || algo == 1),
+              "1 <= C <= 32, 1 <= k <= R, 2 <= G2 <= 64, algo 0 (entropy) / 1 (gini)");
+  // host-side validation of the table against the histogram and the segment maps (no OOB reads)
+  auto sph = sp.cpu();
+  const int32_t* q = sph.data_ptr<int32_t>();
+  const int64_t F = cand.size(1);
+  for (int64_t r = 0; r < R; ++r) {
+    const int32_t* e = q + 6 * r;
+    TORCH_CHECK(e[0] >= 0 && e[0] < F && e[1] >= 0 && e[2] >= 1 && (int64_t)e[1] + e[2] <= TBt && e[3] >= 1 &&
+                    e[3] <= G2 && e[5] >= 0 && (int64_t)e[5] + e[2] <= seg.numel(),
+                "ref_split_score: split row ", r, " out of range");
+  }
+  DevGuard g(hist.device());
+  auto o = hist.options();
+  auto top = at::empty({A, k}, o);
+  auto topv = at::empty({A, k}, o.dtype(at::kDouble));
+  auto segc = at::empty({A, k, G2, C}, o.dtype(at::kDouble));
+  auto cinfo = at::empty({A, k, G2}, o.dtype(at::kDouble));
+  at::Tensor scratch;
+  if (R > 4096) scratch = at::empty({A, R}, o.dtype(at::kDouble));
+  avk::ref_split_score(reinterpret_cast<const long long*>(hist.data_ptr<int64_t>()), (int)A, (int)C, (int)TBt,
+                       sp.data_ptr<int32_t>(), seg.data_ptr<int8_t>(), (int)R, cand.data_ptr<uint8_t>(), (int)F,
+                       (int)algo, (int)k, (int)G2, reinterpret_cast<long long*>(top.data_ptr<int64_t>()),
+                       topv.data_ptr<double>(), segc.data_ptr<double>(), cinfo.data_ptr<double>(),
+                       R > 4096 ? scratch.data_ptr<double>() : nullptr, cur_stream(hist));
+  return {top, topv, segc, cinfo};
+}
+
 // fp32 recurrence (rnn_f32.hip): xw [B, T, 4HP] fp32 kernel order (input projection + biases);
 // wfrag [NW, 4, HP/4, 64] fp32.  Returns hseq [B,T,H], cseq [B,T,HP] (+ gates [B,T,4HP] fp32).
 std::vector<at::Tensor> lstm_forward_f32(const at::Tensor& xw, const at::Tensor& wfrag,
@@ -3399,6 +3444,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);
   m.def("lstm_forward_f32", &lstm_forward_f32);
+  m.def("ref_split_score", &ref_split_score);
   m.def("lstm_backward_f32", &lstm_backward_f32);
 
   py::class_<avh::CsvFile>(m, "CsvFile")

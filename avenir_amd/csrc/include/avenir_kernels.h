@@ -156,6 +156,11 @@ void rbf_matrix(const float* A, const float* B, int na, int nb, int d, float gam
 void smo_ws_solve(const float* Kws, const float* yws, float* aws, const float* gws, const float* gap, int B, float C,
                   float eps, int max_iter, int* iters, hipStream_t stream);
 
+// ---- split.hip (K7 reference-semantics split scoring) ------------------------------------------
+void ref_split_score(const long long* hist, int A, int C, int TBt, const int* sp, const signed char* seg, int R,
+                     const unsigned char* cand, int F, int algo, int k, int G2, long long* top, double* topv,
+                     double* segc, double* cinfo, double* scratch, hipStream_t stream);
+
 // ---- rnn_f32.hip (K27 fp32) ------------------------------------------------------------------
 void lstm_fwd_f32(const float* xw, const float* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
                   float* hseq, float* cseq, float* gates, hipStream_t s);

@@ -706,6 +706,26 @@ class DecisionTreeBuilder:
         # score column -> (feature, split): binary block first, then the explicit splits
         index: list[tuple[int, int]] = (list(zip(bfeat.tolist(), bthr.tolist())) if bin_f else []) + nb_rows
 
+        # K7 device scoring (csrc/kernels/split.hip): every candidate of ``index`` is a row of one split
+        # table — binary thresholds (the last one invalid) as two-segment maps, then the explicit
+        # splits — scored, ranked and expanded into segment counts / impurities on the device
+        use_k7 = (dev.type == "cuda" and os.environ.get("AVMI_TREE_K7", "1") != "0" and _native.C() is not None
+                  and hasattr(_native.C(), "ref_split_score") and C <= 32 and max(Gmax, 2) <= 64 and len(index) > 0)
+        if use_k7:
+            sp_rows, seg_bytes = [], []
+            for f, s_ in index:
+                fs = space[f]
+                if fs.binary:
+                    sm, ns, valid = [0 if b <= s_ else 1 for b in range(bins[f])], 2, int(s_ < bins[f] - 1)
+                else:
+                    sp_ = fs.splits[s_]
+                    sm, ns, valid = list(sp_.segmap), sp_.n_seg, 1
+                sp_rows.append([f, offs[f], bins[f], ns, valid, len(seg_bytes)])
+                seg_bytes += sm
+            k7_sp = torch.tensor(sp_rows, dtype=torch.int32, device=dev)
+            k7_seg = torch.tensor(seg_bytes, dtype=torch.int8, device=dev)
+            k7_algo = {"entropy": 0, "giniIndex": 1, "gini": 1}.get(p.algorithm)
+            use_k7 = k7_algo is not None
         # ---- roots: one histogram launch for every tree ------------------------------------------
         hist = T.node_histogram(codes, n, labels, node, weight, bins, C, NT)
         if comm.is_distributed:
@@ -729,59 +749,65 @@ class DecisionTreeBuilder:
             for a, gi in enumerate(frontier):
                 cand[a, self._candidate_attrs(nodes[gi], F, rngs[tree_of[gi]])] = True
             cand_masks = torch.from_numpy(cand).to(dev)
-            score_blocks = []
-            if bin_f:
-                hb = hist_t[:, bcols, :]                                    # [A, NB, C]
-                cs = torch.cumsum(hb, 1)
-                base = torch.where((bstart > 0).view(1, -1, 1), cs[:, (bstart - 1).clamp_min(0), :],
-                                   torch.zeros_like(cs))
-                left = cs - base
-                right = cs[:, bend, :] - base - left
-                bseg = torch.stack([left, right], 2)                        # [A, NB, 2, C]
-                cnt = bseg.sum(-1)
-                stat = impurity(bseg, p.algorithm)
-                wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)
-                ok = ((cnt > 0).sum(-1) >= 2) & bvalid.view(1, -1) & cand_masks[:, bfeat]
-                score_blocks.append(torch.where(ok, wavg, torch.full_like(wavg, math.inf)))
-            for f in nb_f:
-                hb = hist_t[:, offs[f]: offs[f] + bins[f], :]               # [A, B, C]
-                seg = torch.einsum("sgb,abc->asgc", seg_tensors[f], hb)     # [A, S, G, C]
-                cnt = seg.sum(-1)
-                stat = impurity(seg, p.algorithm)
-                wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)     # [A, S]
-                nonempty = (cnt > 0).sum(-1) >= 2                           # a split must separate rows
-                score_blocks.append(torch.where(nonempty & cand_masks[:, f:f + 1], wavg,
-                                                torch.full_like(wavg, math.inf)))
-            if not score_blocks:
-                break
-            scores = torch.cat(score_blocks, 1)                             # [A, S_total]
-            k = min(p.top_split_count, scores.shape[1]) if p.split_selection == "randomAmongTop" else 1
-            if k == 1:
-                tv, ti_ = scores.min(1)
-                top, topv = ti_.view(A, 1), tv.view(A, 1)
-            else:
-                top = torch.topk(scores, k, dim=1, largest=False).indices
-                topv = torch.gather(scores, 1, top)
-            # segment class counts of every top candidate, on the device: [A, k, Gmax', C]
             G2 = max(Gmax, 2)
-            segc = torch.zeros((A, k, G2, C), dtype=torch.float64, device=dev)
-            if bin_f:
-                isb = top < NBc
-                bsel = bseg[torch.arange(A, device=dev).view(-1, 1).expand(A, k), top.clamp_max(NBc - 1)]
-                segc[:, :, :2] = torch.where(isb.view(A, k, 1, 1), bsel, segc[:, :, :2])
-            if nb_rows:
-                isn = top >= NBc
-                r = (top - NBc).clamp(0, len(nb_rows) - 1)
-                hpad = torch.cat([hist_t, torch.zeros((A, 1, C), dtype=hist_t.dtype, device=dev)], 1)
-                cols = splitcol[r]                                          # [A, k, Bmax]
-                hsel = torch.gather(hpad, 1, cols.view(A, -1, 1).expand(-1, -1, C)).view(A, k, Bmax, C)
-                nsel = torch.einsum("akgb,akbc->akgc", allseg[r], hsel)
-                segc[:, :, :Gmax] = torch.where(isn.view(A, k, 1, 1), nsel, segc[:, :, :Gmax])
+            if use_k7:
+                k = min(p.top_split_count, len(index)) if p.split_selection == "randomAmongTop" else 1
+                top, topv, segc, cinfo = _native.C().ref_split_score(
+                    hist.contiguous(), k7_sp, k7_seg, cand_masks.to(torch.uint8).contiguous(), k7_algo, k, G2)
+            else:
+                score_blocks = []
+                if bin_f:
+                    hb = hist_t[:, bcols, :]                                    # [A, NB, C]
+                    cs = torch.cumsum(hb, 1)
+                    base = torch.where((bstart > 0).view(1, -1, 1), cs[:, (bstart - 1).clamp_min(0), :],
+                                       torch.zeros_like(cs))
+                    left = cs - base
+                    right = cs[:, bend, :] - base - left
+                    bseg = torch.stack([left, right], 2)                        # [A, NB, 2, C]
+                    cnt = bseg.sum(-1)
+                    stat = impurity(bseg, p.algorithm)
+                    wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)
+                    ok = ((cnt > 0).sum(-1) >= 2) & bvalid.view(1, -1) & cand_masks[:, bfeat]
+                    score_blocks.append(torch.where(ok, wavg, torch.full_like(wavg, math.inf)))
+                for f in nb_f:
+                    hb = hist_t[:, offs[f]: offs[f] + bins[f], :]               # [A, B, C]
+                    seg = torch.einsum("sgb,abc->asgc", seg_tensors[f], hb)     # [A, S, G, C]
+                    cnt = seg.sum(-1)
+                    stat = impurity(seg, p.algorithm)
+                    wavg = (stat * cnt).sum(-1) / cnt.sum(-1).clamp_min(1)     # [A, S]
+                    nonempty = (cnt > 0).sum(-1) >= 2                           # a split must separate rows
+                    score_blocks.append(torch.where(nonempty & cand_masks[:, f:f + 1], wavg,
+                                                    torch.full_like(wavg, math.inf)))
+                if not score_blocks:
+                    break
+                scores = torch.cat(score_blocks, 1)                             # [A, S_total]
+                k = min(p.top_split_count, scores.shape[1]) if p.split_selection == "randomAmongTop" else 1
+                # the k best by (score, index), as the device kernel ranks them
+                top = torch.sort(scores, dim=1, stable=True).indices[:, :k]
+                topv = torch.gather(scores, 1, top)
+                # segment class counts of every top candidate, on the device: [A, k, Gmax', C]
+                segc = torch.zeros((A, k, G2, C), dtype=torch.float64, device=dev)
+                if bin_f:
+                    isb = top < NBc
+                    bsel = bseg[torch.arange(A, device=dev).view(-1, 1).expand(A, k), top.clamp_max(NBc - 1)]
+                    segc[:, :, :2] = torch.where(isb.view(A, k, 1, 1), bsel, segc[:, :, :2])
+                if nb_rows:
+                    isn = top >= NBc
+                    r = (top - NBc).clamp(0, len(nb_rows) - 1)
+                    hpad = torch.cat([hist_t, torch.zeros((A, 1, C), dtype=hist_t.dtype, device=dev)], 1)
+                    cols = splitcol[r]                                          # [A, k, Bmax]
+                    hsel = torch.gather(hpad, 1, cols.view(A, -1, 1).expand(-1, -1, C)).view(A, k, Bmax, C)
+                    nsel = torch.einsum("akgb,akbc->akgc", allseg[r], hsel)
+                    segc[:, :, :Gmax] = torch.where(isn.view(A, k, 1, 1), nsel, segc[:, :, :Gmax])
+                cinfo = impurity(segc, p.algorithm)                             # [A, k, G2]
             # ---- the ONE host copy of the level ----
-            flat = torch.cat([top.double().view(-1), topv.double().view(-1), segc.round().view(-1)]).cpu()
+            flat = torch.cat([top.double().view(-1), topv.double().view(-1), segc.round().view(-1),
+                              cinfo.double().view(-1)]).cpu()
             top_h = flat[: A * k].long().view(A, k).tolist()
             topv_h = flat[A * k: 2 * A * k].view(A, k).tolist()
-            segc_h = flat[2 * A * k:].view(A, k, G2, C).long()
+            o3 = 2 * A * k + A * k * G2 * C
+            segc_h = flat[2 * A * k: o3].view(A, k, G2, C).long()
+            cinfo_h = flat[o3:].view(A, k, G2).tolist()
             # ---- choose (randomAmongTop: per-tree RNG among the finite top-k) ----
             pick = [-1] * A
             for a in range(A):
@@ -830,7 +856,7 @@ class DecisionTreeBuilder:
                     if pop == 0:
                         nd.children.append(-1)
                         continue
-                    info = float(impurity(cntg.unsqueeze(0), p.algorithm)[0])
+                    info = cinfo_h[a][pick[a]][g]                    # segment impurity from the device
                     depth = nd.depth + 1   # parentPredicates.size() + 1 (DecisionTreeBuilder.java:606)
                     stop = self._should_stop(pop, info, nd.info, depth) or info == 0.0
                     child = Node(nd.predicates + [preds[g]], pop, info, (cntg.double() / pop).tolist(),
