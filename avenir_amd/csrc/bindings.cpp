@@ -1304,7 +1304,7 @@ at::Tensor sample(int64_t dist, int64_t n, const at::Tensor& params, const c10::
 void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict, bool swap, at::Tensor& sol,
                at::Tensor& cur_cost, at::Tensor& best_sol, at::Tensor& best_cost, int64_t iters, double t0,
                double cool, int64_t interval, bool geometric, int64_t max_retry, int64_t seed, int64_t offset,
-               at::Tensor& stats, int64_t it_begin, double temp_start) {
+               at::Tensor& stats, int64_t it_begin, double temp_start, int64_t chain_base) {
   CHECK_DEV(cost);
   CHECK_DTYPE(cost, at::kFloat);
   TORCH_CHECK(cost.dim() == 2 && cost.size(1) >= 2, "cost must be [L, V>=2]");
@@ -1338,7 +1338,7 @@ void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict
                  best_sol.data_ptr<int16_t>(), best_cost.data_ptr<float>(), (int)P, (int)iters, (float)t0,
                  (float)cool, (int)interval, geometric ? 1 : 0, (int)max_retry, (unsigned long long)seed,
                  (unsigned long long)offset, (int)it_begin, (float)temp_start,
-                 reinterpret_cast<unsigned long long*>(stats.data_ptr<int64_t>()),
+                 reinterpret_cast<unsigned long long*>(stats.data_ptr<int64_t>()), (long long)chain_base,
                  cur_stream(cost));
 }
 

@@ -108,7 +108,8 @@ void sample(int dist, long long n, const float* params, const float* table, int 
 void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
                short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
                int geometric, int max_retry, unsigned long long seed, unsigned long long offset,
-               int it_begin, float temp_start, unsigned long long* stats, hipStream_t stream);
+               int it_begin, float temp_start, unsigned long long* stats, long long chain_base,
+               hipStream_t stream);
 
 // ---- linear.hip (K13) ----------------------------------------------------------------------
 int glm_grid(long long n);

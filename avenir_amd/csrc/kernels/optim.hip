@@ -32,11 +32,14 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
     short* __restrict__ sol, float* __restrict__ cur_cost, short* __restrict__ best_sol,
     float* __restrict__ best_cost, int P, int iters, float t0, float cool, int interval, int geometric,
     int max_retry, unsigned long long seed, unsigned long long offset, int it_begin, float temp_start,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, long long chain_base) {
   extern __shared__ short lds_sol[];
   const int lane = threadIdx.x;
   const int p = blockIdx.x * 64 + lane;
   const bool live = p < P;
+  // Philox stream of GLOBAL chain chain_base + p: a chain draws the same moves whichever rank
+  // (and launch) runs it, so chains can be re-dealt over a different world size on resume
+  const unsigned long long gp = (unsigned long long)(chain_base + p);
   short* s = lds_sol + lane;  // element j at s[j * 64]
   if (live)
     for (int j = 0; j < L; ++j) s[j * 64] = sol[(long long)p * L + j];
@@ -52,8 +55,7 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
   for (int it = it_begin; it < it_begin + iters; ++it) {
     int pos = -1, nv = 0, old = 0, j2 = -1;
     for (int tr = 0; tr <= max_retry; ++tr) {
-      const av::u4 r = av::philox_draw(seed, offset + (unsigned long long)it * (max_retry + 1) + tr,
-                                       (unsigned long long)p);
+      const av::u4 r = av::philox_draw(seed, offset + (unsigned long long)it * (max_retry + 1) + tr, gp);
       const int cp = min((int)(av::u32_to_unit(r.x) * (float)L), L - 1);
       int cv = min((int)(av::u32_to_unit(r.y) * (float)(V - 1)), V - 2);
       const int ov = s[cp * 64];
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
       float delta = cost[(long long)pos * V + nv] - cost[(long long)pos * V + old];
       if (j2 >= 0) delta += cost[(long long)j2 * V + old] - cost[(long long)j2 * V + nv];
       delta *= invL;
-      const av::u4 r2 = av::philox_draw(seed ^ 0x9e3779b97f4a7c15ull, offset + it, (unsigned long long)p);
+      const av::u4 r2 = av::philox_draw(seed ^ 0x9e3779b97f4a7c15ull, offset + it, gp);
       const bool accept = delta <= 0.f || av::u32_to_unit(r2.x) < __expf(-delta / fmaxf(temp, 1e-12f));
       if (accept) {
         c += delta;
@@ -111,12 +113,12 @@ namespace avk {
 void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
                short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
                int geometric, int max_retry, unsigned long long seed, unsigned long long offset,
-               int it_begin, float temp_start, unsigned long long* stats, hipStream_t stream) {
+               int it_begin, float temp_start, unsigned long long* stats, long long chain_base, hipStream_t stream) {
   if (P <= 0 || iters <= 0) return;
   const size_t lds = (size_t)L * 64 * sizeof(short);
   sa_assign_kernel<<<(P + 63) / 64, 64, lds, stream>>>(cost, L, V, conflict, swap, sol, cur_cost, best_sol,
                                                        best_cost, P, iters, t0, cool, interval, geometric, max_retry,
-                                                       seed, offset, it_begin, temp_start, stats);
+                                                       seed, offset, it_begin, temp_start, stats, chain_base);
   AV_HIP_CHECK(hipGetLastError());
 }
 

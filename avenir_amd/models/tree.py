@@ -1380,14 +1380,21 @@ class GradientBoostedTrees:
         val_all = torch.zeros((R, K, Hn), dtype=torch.float64, device=dev)
         loss_all = torch.zeros(R + 1, dtype=torch.float64, device=dev)
         rate32 = 0xFFFFFFFF if p.subsample >= 1.0 else int(max(0.0, p.subsample) * 4294967296.0)
-        # one boosting round = one resumable iteration (per-rank F, trees in the metadata)
+        # one boosting round = one resumable iteration.  The checkpoint is REPLICATED (rank 0 writes
+        # the trees and the global loss sums), so a job resumes at any world size: each rank replays
+        # the restored trees over its own rows to rebuild its raw scores (same gbt_assign launches
+        # in the same order as the original rounds: bit-identical F).
         from ..utils.resilience import IterationLoop
-        lp = IterationLoop("gbt", self.recovery, comm, sharded=True, device=dev)
+        lp = IterationLoop("gbt", self.recovery, comm, device=dev)
         r0, ck, meta = lp.restore(dev)
         if ck is not None:
-            st["F"].copy_(ck["F"].to(dev))
+            if tuple(ck["feat"].shape[1:]) != (K, Hn) or r0 > R:
+                raise ValueError(f"gbt checkpoint shape {tuple(ck['feat'].shape)} does not match this model "
+                                 f"(rounds {R}, classes {K}, heap {Hn})")
             feat_all[:r0], thr_all[:r0], val_all[:r0] = ck["feat"].to(dev), ck["thr"].to(dev), ck["val"].to(dev)
-            loss_all[:r0] = ck["loss"].to(dev)[:r0]     # this rank's own partial sums
+            if comm.rank == 0:                          # global sums: the final all-reduce adds zeros elsewhere
+                loss_all[:r0] = ck["loss"].to(dev)[:r0]
+            self._replay_scores(st, feat_all, thr_all, val_all, r0)
         use_graph = (dev.type == "cuda" and not comm.is_distributed and not lp.enabled
                      and os.environ.get("AVMI_GBT_GRAPH", "1") != "0")
         graphs: dict[int, Any] = {}
@@ -1424,14 +1431,28 @@ class GradientBoostedTrees:
                     thr_all[rnd, k].copy_(st["thr"])
                     val_all[rnd, k].copy_(st["val"])
             if lp.enabled:
-                lp.commit(rnd, {"F": st["F"], "feat": feat_all[:rnd + 1], "thr": thr_all[:rnd + 1],
-                                "val": val_all[:rnd + 1], "loss": loss_all[:rnd + 1]},
-                          {"train_loss": self._losses(loss_all, rnd + 1, st, y8, n, t, n_total, comm)})
+                gl = loss_all[:rnd + 1].clone()
+                if comm.is_distributed:
+                    comm.all_reduce(gl)
+                lp.commit(rnd, {"feat": feat_all[:rnd + 1], "thr": thr_all[:rnd + 1], "val": val_all[:rnd + 1],
+                                "loss": gl}, {"rows": n_total})
         self.graph_used = bool(graphs)
         self.train_loss = self._losses(loss_all, R, st, y8, n, t, n_total, comm)
         self.stages = self._trees_from_heaps(feat_all.cpu(), thr_all.cpu(), val_all.cpu())
         self._flat = None
         return self
+
+    def _replay_scores(self, st: dict, feat_all, thr_all, val_all, rounds: int) -> None:
+        """Raw scores of this rank's rows after ``rounds`` restored rounds: every tree's levels
+        re-run through ``gbt_assign`` exactly as the round that built it ran them."""
+        n, D, lr = st["n"], self.p.max_depth, self.p.learning_rate
+        K = st["F"].shape[1]
+        for rnd in range(rounds):
+            for k in range(K):
+                st["node"][:n] = 0
+                for lvl in range(D):
+                    T.gbt_assign(st["codes"], n, st["node"], feat_all[rnd, k], thr_all[rnd, k], val_all[rnd, k],
+                                 st["bins_t"], lvl, lvl + 1 == D, lr, st["F"], k)
 
     def _losses(self, loss_all, upto, st, y8, n, t, n_total, comm) -> list[float]:
         """train_loss[r] = mean deviance after round r: round r+1's gradient pass measured it; the

@@ -17,8 +17,10 @@ Reference behaviour:
 MI355X design: the population / the set of chains / the set of islands is the batch axis of
 device tensors.  Simulated annealing over an :class:`AssignmentDomain` runs entirely inside one
 K22 kernel launch (one chain per lane, solution tile in LDS); the other optimisers issue a few
-batched tensor ops per generation for ALL islands.  Across GPUs every rank runs its own chains /
-islands (seeded by rank) and the global best is one tiny all-gather.
+batched tensor ops per generation.  Chains and islands are indexed GLOBALLY (their random streams
+are keyed by global index, not by rank): rank r runs its block of them, the W-rank run equals one
+process running all of them, the global best is one tiny all-gather, and checkpoints re-deal the
+chains / islands over any world size on resume.
 """
 from __future__ import annotations
 
@@ -51,8 +53,12 @@ def _gen(device, seed: int) -> torch.Generator:
 
 
 def _global_best(comm: Comm, cost: torch.Tensor, sol: torch.Tensor) -> tuple[torch.Tensor, float]:
-    i = int(torch.argmin(cost))
-    c, s = cost[i:i + 1].float(), sol[i].long()
+    if cost.numel() == 0:                  # a rank left without chains / islands after a re-deal
+        c, s = torch.full((1,), math.inf, device=cost.device), torch.zeros(sol.shape[-1], dtype=torch.long,
+                                                                            device=sol.device)
+    else:
+        i = int(torch.argmin(cost))
+        c, s = cost[i:i + 1].float(), sol[i].long()
     if comm.is_distributed:
         dev = comm.device if comm.backend == "nccl" else torch.device("cpu")
         cs = comm.all_gather(c.to(dev)).view(-1)
@@ -94,56 +100,84 @@ class SimulatedAnnealing:
     def run(self, init: torch.Tensor | None = None) -> OptResult:
         comm = self.comm or get_comm()
         d = self.domain
-        seed = self.seed + 1_000_003 * comm.rank
-        gen = _gen(d.device, seed)
-        if init is None:
-            sol, _ = d.random(self.n_chains, gen)
-        else:
-            sol = init.to(d.device).long().clone()
-        cost = d.evaluate(sol)
         kernel_ok = isinstance(d, AssignmentDomain) and self.step == 1 and d.L <= 512
         use_kernel = kernel_ok if self.use_kernel is None else (self.use_kernel and kernel_ok)
-        with IterationLoop("simulatedAnnealing", self.recovery, comm, sharded=True, device=d.device) as lp:
-            if use_kernel and not lp.enabled:
-                best, bc, stats = sa_assign(d, sol, cost, self.iters, self.t0, self.cooling, self.interval,
-                                            self.geometric, self.max_retry, seed, 0)
-            elif use_kernel:
-                best, bc, stats = self._segmented(lp, sol, cost, seed)
-            else:
-                best, bc, stats = self._generic(sol, cost, gen, lp)
+        if use_kernel:
+            best, bc, stats, gen = self._run_kernel(comm, init)
+        else:
+            seed = self.seed + 1_000_003 * comm.rank
+            gen = _gen(d.device, seed)
+            sol = d.random(self.n_chains, gen)[0] if init is None else init.to(d.device).long().clone()
+            # generic path: one torch generator per rank drives every chain of the rank -> sharded
+            # state, resumable at the world size that wrote it
+            with IterationLoop("simulatedAnnealing.generic", self.recovery, comm, sharded=True,
+                               device=d.device) as lp:
+                best, bc, stats = self._generic(sol, d.evaluate(sol), gen, lp)
         if self.locally_optimize:
             best, bc = local_focussed(d, best, bc, self.local_iters, gen)
         b, c = _global_best(comm, bc, best)
         return OptResult(b, c, bc, best, stats=stats)
 
-    def _segmented(self, lp: IterationLoop, sol, cost, seed):
-        """Kernel path under checkpointing: the run is split into segments of ``segment`` moves
-        (one launch each, same Philox counters and cooling schedule as one launch); every segment
-        commits the chains' current / best solutions, temperature and counters (one file per
-        rank: chains are rank-local)."""
+    def _run_kernel(self, comm, init):
+        """K22 path.  Chains are GLOBAL: chain ``g`` draws Philox stream ``(seed, g)`` and starts from
+        row ``g`` of one population drawn from ``seed`` alone, rank ``r`` runs chains
+        ``[r * n_chains, (r + 1) * n_chains)``.  The W-rank result therefore equals one process
+        running ``W * n_chains`` chains, and the checkpoint (rank 0 writes every chain) resumes at
+        ANY world size: the restored chains are re-dealt by global index.  Under checkpointing the
+        run is split into segments of ``segment`` moves (one launch each, same Philox counters and
+        cooling schedule as one launch)."""
+        from ..data.table import shard_range
         d = self.domain
-        seg = max(1, self.segment or -(-self.iters // 10))
-        best = bc = temp = None
+        W, r = comm.world, comm.rank
+        gen = _gen(d.device, self.seed + 1_000_003 * r)          # local search only
         stats = {"better": 0, "worse_accepted": 0, "rejected": 0}
+        best = bc = temp = None
         b0 = 0
-        _, st, meta = lp.restore(d.device)
-        if st is not None:
-            sol, cost, best, bc = st["sol"], st["cost"], st["best"], st["best_cost"]
-            temp, b0, stats = float(meta["temp"]), int(meta["moves"]), dict(meta["stats"])
-        for b in range(b0, self.iters, seg):
-            n = min(seg, self.iters - b)
-            with lp.step(b // seg):
-                best, bc, s, sol, cost, temp = sa_assign(d, sol, cost, n, self.t0, self.cooling, self.interval,
-                                                         self.geometric, self.max_retry, seed, 0, it_begin=b,
-                                                         temp_start=temp, best=best, best_cost=bc,
-                                                         return_state=True)
-            for k in stats:
-                stats[k] += s[k]
-            lp.commit(b // seg, {"sol": sol, "cost": cost, "best": best, "best_cost": bc},
-                      {"temp": temp, "moves": b + n, "stats": stats}, force=True)
-        if best is None:                       # resumed after the last segment
-            best, bc = st["best"], st["best_cost"]
-        return best, bc, stats
+        with IterationLoop("simulatedAnnealing", self.recovery, comm, device=d.device) as lp:
+            _, st, meta = lp.restore(d.device)
+            if st is not None:
+                total = int(meta["chains"])
+                a, e = shard_range(total, r, W)
+                sol, cost, best, bc = (st[k][a:e].to(d.device) for k in ("sol", "cost", "best", "best_cost"))
+                temp, b0 = float(meta["temp"]), int(meta["moves"])
+                if r == 0:                                       # global counters: summed over ranks at the end
+                    stats = dict(meta["stats"])
+            else:
+                if init is None:
+                    total = self.n_chains * W
+                    sol = d.random(total, _gen(d.device, self.seed))[0][r * self.n_chains:(r + 1) * self.n_chains]
+                    a = r * self.n_chains
+                else:
+                    sol = init.to(d.device).long().clone()
+                    counts = comm.all_gather(torch.tensor([sol.shape[0]])).view(-1).tolist()
+                    total, a = sum(counts), sum(counts[:r])
+                cost = d.evaluate(sol)
+            seg = max(1, self.segment or -(-self.iters // 10)) if lp.enabled else max(1, self.iters)
+            for b in range(b0, self.iters, seg):
+                n = min(seg, self.iters - b)
+                with lp.step(b // seg):
+                    best, bc, s, sol, cost, temp = sa_assign(d, sol, cost, n, self.t0, self.cooling, self.interval,
+                                                             self.geometric, self.max_retry, self.seed, 0, it_begin=b,
+                                                             temp_start=temp, best=best, best_cost=bc,
+                                                             return_state=True, chain_base=a)
+                for k in stats:
+                    stats[k] += s[k]
+                if lp.enabled:
+                    full = [comm.all_gather_v(x.contiguous()) for x in (sol, cost, best, bc)]
+                    lp.commit(b // seg, dict(zip(("sol", "cost", "best", "best_cost"), full)),
+                              {"temp": temp, "moves": b + n, "stats": self._global_stats(comm, stats),
+                               "chains": total}, force=True)
+        if best is None:                                   # no moves at all
+            best, bc = sol.clone(), cost.clone()
+        return best.long(), bc, self._global_stats(comm, stats), gen
+
+    @staticmethod
+    def _global_stats(comm, stats: dict) -> dict:
+        if not comm.is_distributed:
+            return dict(stats)
+        v = torch.tensor([stats[k] for k in ("better", "worse_accepted", "rejected")], dtype=torch.float64)
+        comm.all_reduce(v)
+        return dict(zip(("better", "worse_accepted", "rejected"), (int(x) for x in v.tolist())))
 
     def _generic(self, sol, cost, gen, lp: IterationLoop | None = None):
         d = self.domain
@@ -185,11 +219,12 @@ class SimulatedAnnealing:
 def sa_assign(d: AssignmentDomain, sol: torch.Tensor, cost: torch.Tensor, iters: int, t0: float, cool: float,
               interval: int, geometric: bool, max_retry: int, seed: int, offset: int, it_begin: int = 0,
               temp_start: float | None = None, best: torch.Tensor | None = None, best_cost: torch.Tensor | None = None,
-              return_state: bool = False):
+              return_state: bool = False, chain_base: int = 0):
     """Run ``sol.shape[0]`` SA chains over an assignment domain: K22 kernel on GPU, the bit-exact
     numpy mirror (same Philox stream, float32 arithmetic) on CPU.  Returns (best_sol, best_cost, stats)
     or, with ``return_state``, also (current_sol, current_cost, temperature) so a run split into
-    segments [it_begin, it_begin + iters) (checkpoint / resume) equals one uninterrupted launch."""
+    segments [it_begin, it_begin + iters) (checkpoint / resume) equals one uninterrupted launch.
+    Row ``p`` is global chain ``chain_base + p``: its Philox stream does not depend on the launch."""
     ts = float(t0 if temp_start is None else temp_start)
     if sol.device.type == "cuda":
         s16 = sol.to(torch.int16).contiguous()
@@ -200,7 +235,7 @@ def sa_assign(d: AssignmentDomain, sol: torch.Tensor, cost: torch.Tensor, iters:
         _native.C().sa_assign(d.cost_table, None if d.conflict is None else d.conflict.to(torch.uint8).contiguous(),
                               bool(d.swap_moves), s16, cur, bsol, bc, int(iters), float(t0), float(cool),
                               int(interval), bool(geometric), int(max_retry), int(seed), int(offset), st,
-                              int(it_begin), ts)
+                              int(it_begin), ts, int(chain_base))
         s = st.tolist()
         stats = {"better": s[0], "worse_accepted": s[1], "rejected": s[2]}
         if return_state:
@@ -210,7 +245,8 @@ def sa_assign(d: AssignmentDomain, sol: torch.Tensor, cost: torch.Tensor, iters:
     out = sa_assign_reference(d.cost_table.numpy(), None if d.conflict is None else d.conflict.numpy(),
                               d.swap_moves, sol.numpy(), cost.float().numpy(), iters, t0, cool, interval,
                               geometric, max_retry, seed, offset, it_begin, ts,
-                              None if best is None else best.numpy(), None if best_cost is None else best_cost.float().numpy())
+                              None if best is None else best.numpy(), None if best_cost is None else best_cost.float().numpy(),
+                              chain_base)
     b, c, s, cs, cc, temp = out
     if return_state:
         return (torch.from_numpy(b).long(), torch.from_numpy(c), s, torch.from_numpy(cs).long(),
@@ -219,7 +255,7 @@ def sa_assign(d: AssignmentDomain, sol: torch.Tensor, cost: torch.Tensor, iters:
 
 
 def sa_assign_reference(cost, conflict, swap, sol, cur, iters, t0, cool, interval, geometric, max_retry, seed, offset,
-                        it_begin=0, temp_start=None, best=None, best_cost=None):
+                        it_begin=0, temp_start=None, best=None, best_cost=None, chain_base=0):
     """Host mirror of ``sa_assign_kernel`` (optim.hip), vectorised over chains.  Returns
     (best, best_cost, stats, current_sol, current_cost, temperature)."""
     cost = np.asarray(cost, np.float32)
@@ -230,7 +266,7 @@ def sa_assign_reference(cost, conflict, swap, sol, cur, iters, t0, cool, interva
     bc = c.copy() if best_cost is None else np.array(best_cost, dtype=np.float32)
     best = sol.copy() if best is None else np.array(best, dtype=np.int64)
     rows = np.arange(P)
-    idx = np.arange(P, dtype=np.uint64)
+    idx = np.arange(P, dtype=np.uint64) + np.uint64(chain_base)
     ar = np.arange(L)
     invL = np.float32(1.0 / L)
     temp = np.float32(t0 if temp_start is None else temp_start)
@@ -356,36 +392,79 @@ class GeneticAlgorithm:
                    **kw)
 
     def run(self) -> OptResult:
+        """Islands are GLOBAL: island ``g`` owns a generator seeded ``seed + 7919 g`` that draws its
+        initial pool and every crossover / mutation of that island, and rank ``r`` runs islands
+        ``[r * islands, (r + 1) * islands)``; migration is a ring over the global island order (one
+        all-gather of the elites).  So the W-rank run equals one process running ``W * islands``
+        islands, and the checkpoint — every island's pool, costs, history and generator state,
+        written by rank 0 — resumes at ANY world size by re-dealing the islands by global index."""
+        from ..data.table import shard_range
         comm = self.comm or get_comm()
-        d, I, Pp, L = self.d, self.I, self.Pp, self.d.L
-        gen = _gen(d.device, self.seed + 7919 * comm.rank)
-        pop, _ = d.random(I * Pp, gen)
-        cost = d.evaluate(pop)
-        pop, cost = pop.view(I, Pp, L), cost.view(I, Pp)
-        history = []
-        ii = torch.arange(I, device=d.device).view(-1, 1)
-        lp = IterationLoop("geneticAlgorithm", self.recovery, comm, sharded=True, device=d.device)
+        d, Pp, L = self.d, self.Pp, self.d.L
+        W, r = comm.world, comm.rank
+        lp = IterationLoop("geneticAlgorithm", self.recovery, comm, device=d.device)
         g0, st, meta = lp.restore(d.device)
-        if st is not None:                  # islands are rank-local: one checkpoint per rank
-            pop, cost = st["pop"], st["cost"]
-            gen.set_state(st["rng"])
-            history = list(meta["history"])
+        if st is not None:
+            total = int(meta["islands"])
+            a, e = shard_range(total, r, W)
+            pop, cost, hist = (st[k][a:e].to(d.device) for k in ("pop", "cost", "hist"))
+            gens = []
+            for i in range(a, e):
+                gg = _gen(d.device, 0)
+                gg.set_state(st["rng"][i].cpu().clone())
+                gens.append(gg)
+        else:
+            total, a, e = self.I * W, r * self.I, (r + 1) * self.I
+            gens = [_gen(d.device, self.seed + 7919 * i) for i in range(a, e)]
+            pop = torch.stack([d.random(Pp, gg)[0] for gg in gens]).view(e - a, Pp, L)
+            cost = d.evaluate(pop.view(-1, L)).view(e - a, Pp)
+            hist = torch.empty((e - a, 0), dtype=cost.dtype, device=d.device)
         for g in range(g0, self.G):
             with lp.step(g):
-                pop, cost = self._generation(g, pop, cost, gen, history, ii)
+                outs = [self._generation(pop[i:i + 1], cost[i:i + 1], gens[i]) for i in range(e - a)]
+                if outs:
+                    pop = torch.cat([o[0] for o in outs])
+                    cost = torch.cat([o[1] for o in outs])
+                    hist = torch.cat([hist, torch.cat([o[2] for o in outs]).view(-1, 1)], 1)
+                if self.migrate_every and total > 1 and (g + 1) % self.migrate_every == 0:
+                    pop, cost = self._migrate(comm, pop, cost, a, e)
             if lp.enabled:
-                lp.commit(g, {"pop": pop, "cost": cost, "rng": gen.get_state()}, {"history": history})
+                rng = torch.stack([gg.get_state() for gg in gens]) if gens else torch.empty((0, 1), dtype=torch.uint8)
+                full = [comm.all_gather_v(x.contiguous()) for x in (pop, cost, hist, rng)]
+                lp.commit(g, dict(zip(("pop", "cost", "hist", "rng"), full)), {"islands": total})
         lp.close()
+        ha = comm.all_gather_v(hist.contiguous()) if comm.is_distributed else hist
+        history = ha.min(0).values.tolist() if ha.shape[0] else []
+        ii = torch.arange(e - a, device=d.device)
         bi = cost.argmin(1)
-        bs, bc = pop[ii.view(-1), bi], cost[ii.view(-1), bi]
+        bs, bc = pop[ii, bi], cost[ii, bi]
         b, c = _global_best(comm, bc, bs)
         return OptResult(b, c, bc, bs, history)
 
-    def _generation(self, g, pop, cost, gen, history, ii):
-        d, I, Pp, L = self.d, self.I, self.Pp, self.d.L
+    @staticmethod
+    def _migrate(comm, pop, cost, a, e):
+        """Ring migration over the global islands: island g's elite replaces the worst member of
+        island g + 1 (mod the island count)."""
+        ii = torch.arange(e - a, device=pop.device)
+        bi = cost.argmin(1)
+        elite, ec = pop[ii, bi], cost[ii, bi]
+        ge, gc = comm.all_gather_v(elite.contiguous()), comm.all_gather_v(ec.contiguous())
+        ge, gc = ge.roll(1, 0)[a:e], gc.roll(1, 0)[a:e]
+        wi = cost.argmax(1)
+        pop, cost = pop.clone(), cost.clone()
+        pop[ii, wi] = ge.to(pop.device)
+        cost[ii, wi] = gc.to(cost.device)
+        return pop, cost
+
+    def _generation(self, pop, cost, gen):
+        """One generation of the islands in ``pop`` [I, pool, L] (all drawing from ``gen``).
+        Returns (pop, cost, best cost at the generation's start per island)."""
+        d, L = self.d, self.d.L
+        I, Pp = pop.shape[0], pop.shape[1]
+        ii = torch.arange(I, device=d.device).view(-1, 1)
         order = cost.argsort(1)
         pop, cost = pop[ii, order], cost[ii, order]
-        history.append(float(cost[:, 0].min()))
+        first = cost[:, 0].clone()
         # children: 2x oversampled pairs from the mating list, first r valid per island
         npair = self.r
         a = (torch.rand((I, npair), generator=gen, device=d.device) * self.m).long().clamp_max(self.m - 1)
@@ -407,13 +486,7 @@ class GeneticAlgorithm:
             allp, allc = torch.cat([pop, kids], 1), torch.cat([cost, kc], 1)
             o = allc.argsort(1)[:, :Pp]
             pop, cost = allp[ii, o], allc[ii, o]
-        if self.migrate_every and I > 1 and (g + 1) % self.migrate_every == 0:
-            bi = cost.argmin(1)
-            elite, ec = pop[ii.view(-1), bi], cost[ii.view(-1), bi]
-            wi = cost.argmax(1)
-            pop[ii.view(-1), wi] = elite.roll(1, 0)
-            cost[ii.view(-1), wi] = ec.roll(1, 0)
-        return pop, cost
+        return pop, cost, first
 
 
 class EvolutionaryOptimizer:

@@ -13,12 +13,16 @@ rounds, SA / GA generations, Apriori levels) runs inside an ``IterationLoop``:
 * ``restore()`` returns the last committed iteration's tensors from
   ``<dir>/<algo>.ckpt`` (the CRC-checked container of ``utils/checkpoint``), so a job started
   fresh after a crash — new processes — continues where the previous one stopped and produces the
-  same result as an uninterrupted run.  Replicated state (rank 0 writes it; k-means, logistic
-  regression, Apriori) resumes at any world size: it does not depend on the sharding, and every
-  rank loads the same file.  Sharded state (``<algo>.rank<r>.ckpt`` per rank; GBT, SA chains, GA
-  islands) is only valid at the world size that wrote it: ``restore()`` checks the recorded world
-  size and the set of rank files on every rank and refuses a resume at a different world size
-  with :class:`WorldSizeMismatch` instead of letting some ranks resume and others start over;
+  same result as an uninterrupted run.  Replicated state (rank 0 writes it) resumes at any world
+  size: k-means, logistic regression and Apriori state does not depend on the sharding; GBT
+  checkpoints its trees and global loss sums and every rank replays the trees over its own rows
+  to rebuild the raw scores; SA chains and GA islands are keyed by GLOBAL chain / island index
+  (their random streams too), so rank 0 checkpoints all of them and a resuming job re-deals them
+  over its own ranks.  Sharded state (``<algo>.rank<r>.ckpt`` per rank; SA over a generic domain,
+  whose torch generator is per rank) is only valid at the world size that wrote it: ``restore()``
+  checks the recorded world size and the set of rank files on every rank and refuses a resume at
+  a different world size with :class:`WorldSizeMismatch` instead of letting some ranks resume and
+  others start over;
 * ``step(it)`` wraps one iteration: it beats the ``Watchdog`` (a stalled collective aborts the rank
   with exit code 75 so ``torchrun --max-restarts`` relaunches it), runs the env-driven fault
   injector (``AVMI_FAULT_RANK`` / ``AVMI_FAULT_ITER`` / ``AVMI_FAULT_MODE``) and opens a tracer

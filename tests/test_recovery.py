@@ -51,9 +51,10 @@ def _genetic(rank, world, ckdir):
     from avenir_amd.optimize.search import GeneticAlgorithm
     from avenir_amd.utils.resilience import RecoveryConfig
     d = FunctionDomain([list(range(8))] * 6, lambda v: ((v - 3) ** 2).sum(1))
-    r = GeneticAlgorithm(d, islands=2, pool=12, mating=6, replacement=4, generations=10, seed=5,
-                         recovery=RecoveryConfig(ckdir)).run()
-    return r.history, r.costs.tolist()
+    # 4 global islands: 2 per rank at world 2, re-dealt 1 per rank at world 4 / 4 at world 1
+    r = GeneticAlgorithm(d, islands=4 // world, pool=12, mating=6, replacement=4, generations=10, seed=5,
+                         migrate_every=3, recovery=RecoveryConfig(ckdir)).run()
+    return r.history, r.best_cost, r.best.tolist()
 
 
 def _annealing(rank, world, ckdir):
@@ -62,27 +63,42 @@ def _annealing(rank, world, ckdir):
     from avenir_amd.utils.resilience import RecoveryConfig
     g = torch.Generator().manual_seed(3)
     d = AssignmentDomain(torch.rand(12, 6, generator=g))
-    r = SimulatedAnnealing(d, n_chains=16, iters=80, t0=2.0, seed=1, recovery=RecoveryConfig(ckdir),
+    r = SimulatedAnnealing(d, n_chains=32 // world, iters=80, t0=2.0, seed=1, recovery=RecoveryConfig(ckdir),
                            segment=10).run()
+    return r.best_cost, r.best.tolist(), r.stats
+
+
+def _annealing_generic(rank, world, ckdir):
+    """SA over a non-assignment domain: the torch-generator path, whose state is per rank."""
+    from avenir_amd.optimize.domain import FunctionDomain
+    from avenir_amd.optimize.search import SimulatedAnnealing
+    from avenir_amd.utils.resilience import RecoveryConfig
+    d = FunctionDomain([list(range(8))] * 6, lambda v: ((v - 3) ** 2).sum(1))
+    r = SimulatedAnnealing(d, n_chains=8, iters=12, t0=2.0, seed=1, recovery=RecoveryConfig(ckdir)).run()
     return r.costs.tolist(), r.solutions.tolist()
 
 
 def _gbt(rank, world, ckdir):
+    """One global data set, row-sharded over the ranks (global row offsets: the subsampling
+    stream is keyed by global row)."""
+    from avenir_amd.data.table import shard_range
     from avenir_amd.models.supervised import array_schema, array_table
     from avenir_amd.models.tree import GBTParams, GradientBoostedTrees
     from avenir_amd.utils.resilience import RecoveryConfig
-    g = torch.Generator().manual_seed(11 + rank)
-    X = torch.randn(600, 4, generator=g)
-    y = ((X[:, 0] - X[:, 1] + 0.5 * torch.randn(600, generator=g)) > 0).long()
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(1200, 4, generator=g)
+    y = ((X[:, 0] - X[:, 1] + 0.5 * torch.randn(1200, generator=g)) > 0).long()
     schema = array_schema(4, [0, 1])
-    t = array_table(X, y, schema)
+    lo, hi = shard_range(1200, rank, world)
+    t = array_table(X[lo:hi], y[lo:hi], schema)
+    t.row_offset = lo
     m = GradientBoostedTrees(schema, GBTParams(n_estimators=8, max_depth=3, subsample=0.7, max_bins=16),
                              recovery=RecoveryConfig(ckdir)).fit(t)
-    return m.train_loss, m.decision_function(t).tolist()
+    return m.train_loss, m.decision_function(array_table(X, y, schema)).view(-1).tolist()
 
 
-@pytest.mark.parametrize("fn", [_kmeans, _logistic, _apriori, _genetic, _annealing, _gbt],
-                         ids=["kmeans", "logistic", "apriori", "genetic", "annealing", "gbt"])
+@pytest.mark.parametrize("fn", [_kmeans, _logistic, _apriori, _genetic, _annealing, _annealing_generic, _gbt],
+                         ids=["kmeans", "logistic", "apriori", "genetic", "annealing", "annealing_generic", "gbt"])
 def test_fault_then_fresh_resume_equals_uninterrupted(tmp_path, fn):
     clean, errs, codes = run_world_outcome(fn, 2, str(tmp_path / "clean"))
     assert not errs and codes == [0, 0], errs
@@ -98,16 +114,48 @@ def test_fault_then_fresh_resume_equals_uninterrupted(tmp_path, fn):
 
 @pytest.mark.parametrize("new_world", [1, 4])
 def test_sharded_resume_at_other_world_size_refused(tmp_path, new_world):
-    """a world-2 sharded checkpoint (GA islands) resumed at world 1 or 4 raises
-    WorldSizeMismatch on every rank instead of silently mixing resumed and fresh ranks."""
+    """a world-2 sharded checkpoint (SA over a generic domain: one torch
+    generator per rank) resumed at world 1 or 4 raises WorldSizeMismatch on every rank instead of
+    silently mixing resumed and fresh ranks."""
     ck = str(tmp_path / "faulty")
-    res, errs, codes = run_world_outcome(_genetic, 2, ck, env=FAULT, timeout=90)
+    res, errs, codes = run_world_outcome(_annealing_generic, 2, ck, env=FAULT, timeout=90)
     assert codes[1] == 17
     assert sorted(p.name for p in (tmp_path / "faulty").glob("*.ckpt")) == [
-        "geneticAlgorithm.rank0.ckpt", "geneticAlgorithm.rank1.ckpt"]
-    res, errs, codes = run_world_outcome(_genetic, new_world, ck, timeout=90)
+        "simulatedAnnealing.generic.rank0.ckpt", "simulatedAnnealing.generic.rank1.ckpt"]
+    res, errs, codes = run_world_outcome(_annealing_generic, new_world, ck, timeout=90)
     assert not res and len(errs) == new_world
     assert all("WorldSizeMismatch" in e for e in errs.values()), errs
+
+
+def _close(a, b, tol):
+    if isinstance(a, (list, tuple)):
+        return len(a) == len(b) and all(_close(x, y, tol) for x, y in zip(a, b))
+    if isinstance(a, dict):
+        return a.keys() == b.keys() and all(_close(a[k], b[k], tol) for k in a)
+    if isinstance(a, float):
+        return abs(a - b) <= tol * max(1.0, abs(b))
+    return a == b
+
+
+@pytest.mark.parametrize("new_world", [1, 4])
+@pytest.mark.parametrize("fn", [_genetic, _annealing, _gbt], ids=["genetic", "annealing", "gbt"])
+def test_elastic_resume_at_other_world_size(tmp_path, fn, new_world):
+    """a world-2 run of a formerly rank-sharded algorithm (GA islands, SA chains,
+    GBT raw scores) is killed, then resumed at world 4 and at world 1 from the same checkpoint; the
+    result equals the uninterrupted world-2 run (GA / SA exactly: chains and islands are keyed by
+    global index; GBT within 1e-6: each rank replays the restored trees over its new row shard, and
+    only the float summation order of the histogram reduction changes with the world size)."""
+    clean, errs, codes = run_world_outcome(fn, 2, str(tmp_path / "clean"))
+    assert not errs and codes == [0, 0], errs
+    ck = str(tmp_path / "faulty")
+    res, errs, codes = run_world_outcome(fn, 2, ck, env=FAULT, timeout=90)
+    assert codes[1] == 17, (codes, errs)
+    assert len(res) < 2
+    resumed, errs, codes = run_world_outcome(fn, new_world, ck, timeout=120)
+    assert not errs and codes == [0] * new_world, errs
+    tol = 1e-6 if fn is _gbt else 0.0
+    for r in resumed.values():
+        assert _close(r, clean[0], tol), (r, clean[0])
 
 
 def test_replicated_resume_at_other_world_size(tmp_path):
