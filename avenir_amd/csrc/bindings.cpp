@@ -3399,6 +3399,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bandit_select", &bandit_select);
   m.def("sample", &sample);
   m.def("sa_assign", &sa_assign);
+  m.def("mixed_knn_max_dims", []() { return avk::mixed_knn_max_dims(); });
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);
   m.def("smo_ws_solve", &smo_ws_solve);

@@ -154,24 +154,58 @@ def rafo(args):
 @job("knnClassifier", "kNN classification with the fused distance+top-k kernel: --input test --train train CSV")
 def knn(args):
     """Both sets are sharded over ranks; the training shards circulate around the ring
-    (``distributed_knn``) so every rank classifies only its own query shard."""
+    (``distributed_knn``) so every rank classifies only its own query shard.  Distance: euclidean
+    over min-max scaled numeric attributes + one-hot categorical attributes.  With categorical /
+    bucketed attributes present (and at most 32 numeric + 32 categorical columns, k <= 32) the
+    one-hot matrix is never built: ``mixed_knn_kernel`` adds a mismatch weight of 2 per differing
+    category (1 against a missing value) — the one-hot squared distance — to the numeric terms."""
     from ..models.knn import NearestNeighbor
+    from ..ops.distance import mixed_knn_max_dims
     ctx = JobContext(args, "nen.")
     schema = ctx.schema()
     tr = ctx.table(raw_numeric=True, path=args.train, schema=schema)
     te = ctx.table(raw_numeric=True, schema=schema)
-    Xtr, Xte = tr.dense_features(one_hot=True), te.dense_features(one_hot=True)
-    lo, hi = Xtr.min(0).values, Xtr.max(0).values
+    nn = NearestNeighbor.from_config(ctx.cfg)
+    mx = mixed_knn_max_dims()
+    mixed = (bool(tr.binned_fields) and len(tr.numeric_fields) <= mx and len(tr.binned_fields) <= mx
+             and nn.k <= 32 and nn.metric == "euclidean")
+    if mixed:
+        Xtr, Xte = _numeric_block(tr), _numeric_block(te)
+        Ctr, Cte = _category_codes(tr), _category_codes(te)
+    else:
+        Xtr, Xte = tr.dense_features(one_hot=True), te.dense_features(one_hot=True)
+    lo, hi = Xtr.min(0).values if tr.n else Xtr.new_full((Xtr.shape[1],), math.inf), \
+        Xtr.max(0).values if tr.n else Xtr.new_full((Xtr.shape[1],), -math.inf)
     if ctx.comm.is_distributed:
         ctx.comm.all_reduce(lo, "min")
         ctx.comm.all_reduce(hi, "max")
     scale = (hi - lo).clamp_min(1e-12)
-    nn = NearestNeighbor.from_config(ctx.cfg).fit((Xtr - lo) / scale, tr.labels[: tr.n].long(), tr.n_classes,
-                                                  index_base=tr.row_offset)
-    res = nn.predict((Xte - lo) / scale, q_base=te.row_offset)
-    from ..data.records import format_lines
+    y = tr.labels[: tr.n].long()
+    if mixed:
+        wc = torch.full((Ctr.shape[1],), 2.0, device=Xtr.device)
+        nn.fit_mixed((Xtr - lo) / scale, Ctr, wc, y, tr.n_classes, index_base=tr.row_offset)
+        res = nn.predict((Xte - lo) / scale, q_base=te.row_offset, Qc=Cte)
+    else:
+        nn.fit((Xtr - lo) / scale, y, tr.n_classes, index_base=tr.row_offset)
+        res = nn.predict((Xte - lo) / scale, q_base=te.row_offset)
     vals = te.class_field.cardinality
     ctx.emit_columns([te.lines.column("r"), ("s", list(vals), res.pred.int().cpu())], te.n)
+
+
+def _numeric_block(t) -> torch.Tensor:
+    """[n, Dn] float32 numeric attributes of ``t`` in schema order."""
+    if not t.numeric_fields:
+        return torch.zeros((t.n, 0), device=t.device)
+    o = sorted(range(len(t.numeric_fields)), key=lambda i: t.numeric_fields[i].ordinal)
+    return t.numeric[o, : t.n].T.float().contiguous()
+
+
+def _category_codes(t) -> torch.Tensor:
+    """[n, Dc] int32 codes of the binned attributes (categorical and bucketed), -1 = missing."""
+    o = sorted(range(len(t.binned_fields)), key=lambda i: t.binned_fields[i].ordinal)
+    nb = torch.tensor([t.binned_fields[i].num_bins for i in o], device=t.device).view(1, -1)
+    c = t.codes[o, : t.n].T.long()
+    return torch.where(c < nb, c, torch.full_like(c, -1)).int().contiguous()
 
 
 @job("logisticRegression", "logistic regression (J/regress/LogisticRegressionJob.java): CSV -> coefficient lines per iteration")

@@ -77,6 +77,16 @@ class NearestNeighbor:
         self.n_classes = n_classes or (int(y.max()) + 1 if y.numel() else 1)
         self.post = feature_post_prob
         self.index_base = index_base
+        self.Xc = self.wc = None
+        return self
+
+    def fit_mixed(self, Xn: torch.Tensor, Xc: torch.Tensor, wc: torch.Tensor, y: torch.Tensor,
+                  n_classes: int | None = None, index_base: int = 0) -> "NearestNeighbor":
+        """Mixed-type training records: numeric block ``Xn`` [n, Dn] (already scaled), categorical
+        codes ``Xc`` int [n, Dc] (-1 missing) with per-column mismatch weights ``wc``.  Queries
+        then pass their own ``Qc``; distances run in ``mixed_knn_kernel`` (no one-hot matrix)."""
+        self.fit(Xn, y, n_classes, index_base=index_base)
+        self.Xc, self.wc = Xc.int().contiguous(), wc.float().contiguous()
         return self
 
     def _kernel_scores(self, d: torch.Tensor) -> torch.Tensor:
@@ -97,8 +107,13 @@ class NearestNeighbor:
             s = s / ds.clamp_min(1.0)
         return torch.where(torch.isinf(d), torch.zeros_like(s), s)
 
-    def kneighbors(self, Q: torch.Tensor, exclude_self: bool = False, q_base: int = 0):
+    def kneighbors(self, Q: torch.Tensor, exclude_self: bool = False, q_base: int = 0, Qc: torch.Tensor | None = None):
         comm = self.comm or get_comm()
+        if getattr(self, "Xc", None) is not None:
+            if Qc is None or exclude_self:
+                raise ValueError("mixed-type kNN needs the queries' categorical codes (and no exclude_self)")
+            return dist.distributed_knn_mixed(Q.float(), Qc, self.X, self.Xc, self.wc, self.k, comm,
+                                              r_base=self.index_base)
         if comm.is_distributed:
             # y / posterior of remote shards are gathered once (labels are tiny next to vectors)
             return dist.distributed_knn(Q.float(), self.X, self.k, comm, self.metric, r_base=self.index_base,
@@ -114,8 +129,9 @@ class NearestNeighbor:
         ps = comm.all_gather_v(self.post) if self.post is not None else None
         return ys, ps
 
-    def predict(self, Q: torch.Tensor, exclude_self: bool = False, q_base: int = 0) -> KnnResult:
-        d, idx = self.kneighbors(Q, exclude_self, q_base)
+    def predict(self, Q: torch.Tensor, exclude_self: bool = False, q_base: int = 0,
+                Qc: torch.Tensor | None = None) -> KnnResult:
+        d, idx = self.kneighbors(Q, exclude_self, q_base, Qc)
         ys, ps = self._global_labels()
         valid = idx >= 0
         gi = idx.clamp_min(0)

@@ -136,6 +136,42 @@ def distributed_knn(Q: torch.Tensor, R: torch.Tensor, k: int, comm, metric: str 
     return best_d, best_i
 
 
+def mixed_knn_max_dims() -> int:
+    """Largest numeric / categorical column count of the ``mixed_knn_kernel`` (and k <= 32)."""
+    try:
+        return int(_native.C().mixed_knn_max_dims())
+    except (AttributeError, RuntimeError, ImportError):
+        return 32
+
+
+def distributed_knn_mixed(Qn, Qc, Rn, Rc, wc, k: int, comm, r_base: int = 0):
+    """``knn_mixed`` with the reference shards travelling the ring (as ``distributed_knn``): the
+    numeric block and the categorical codes (bit-cast to float32) travel as ONE [nr, Dn + Dc]
+    buffer, the next shard's transfer is posted before the current shard's kernel."""
+    if not comm.is_distributed:
+        return knn_mixed(Qn, Qc, Rn, Rc, wc, k, r_base)
+    Dn = Rn.shape[1]
+    best_d = torch.full((Qn.shape[0], k), math.inf, device=Qn.device)
+    best_i = torch.full((Qn.shape[0], k), -1, dtype=torch.long, device=Qn.device)
+    sizes = comm.all_gather(torch.tensor([Rn.shape[0]], dtype=torch.long, device=Qn.device)).view(-1).tolist()
+    bases = [0]
+    for c in sizes[:-1]:
+        bases.append(bases[-1] + c)
+    cur = torch.cat([Rn.float(), Rc.int().contiguous().view(torch.float32)], 1).contiguous()
+    W, me = comm.world, comm.rank
+    for step in range(W):
+        owner = (me - step) % W
+        pending = None
+        if step + 1 < W:
+            pending = comm.ring_pass_start(cur, sizes[(me - step - 1) % W])
+        d, i = knn_mixed(Qn, Qc, cur[:, :Dn].contiguous(), cur[:, Dn:].contiguous().view(torch.int32), wc, k,
+                         bases[owner])
+        best_d, best_i = merge_topk(best_d, best_i, d, i.long(), k)
+        if pending is not None:
+            cur = comm.ring_pass_finish(pending)
+    return best_d, best_i
+
+
 def _distributed_knn_ids(Q, R, ids, k, comm, metric):
     """distributed_knn over reference rows carrying explicit global ids (ring of (rows, ids))."""
     best_d = torch.full((Q.shape[0], k), math.inf, device=Q.device)

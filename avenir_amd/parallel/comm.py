@@ -17,13 +17,16 @@ tensors (KB..tens of MB), so ops are issued ONCE per model/iteration on coalesce
 (``all_reduce_coalesced``) rather than per key; RCCL picks its one-shot/tree algorithms for small
 messages and multi-ring for large ones.
 
-One-shot small-message all-reduce: on a fully connected xGMI node every GPU has a
-direct link to every peer, so for KB-scale count tables a single all-gather (each rank's table to
-every peer in ONE step) followed by a local sum replaces the 2(n-1)-step ring of reduce-scatter +
-all-gather.  ``all_reduce(..., algo="oneshot")`` (or ``AVMI_SMALL_ALLREDUCE=oneshot`` for sum
-reductions up to ``AVMI_ONESHOT_MAX_BYTES``, default 64 KiB) takes that path; the local reduction
-runs in rank order, so the result is also bit-identical on every rank and run (fp32 / fp64 sums
-included).  ``bench.py`` reports both latencies on multi-GPU runs.
+Deterministic small-message all-reduce (``algo="oneshot"``; SURVEY §5.8 asks for a one-shot
+kernel, which this is NOT): the reduction is an all-gather of every rank's buffer followed by a
+local sum over ranks in rank order.  The all-gather is RCCL's own collective (its ring or direct
+algorithm, chosen by RCCL), so this path saves no communication steps over a library all-reduce;
+what it buys is a result that is bit-identical on every rank and every run (fp32 / fp64 sums
+included), at the price of ``world`` times the receive bytes.  ``all_reduce(..., algo="oneshot")``
+(or ``AVMI_SMALL_ALLREDUCE=oneshot`` for sum reductions up to ``AVMI_ONESHOT_MAX_BYTES``, default
+64 KiB) takes it; ``bench.py`` reports both latencies on multi-GPU runs.  A true one-shot P2P kernel
+(each GPU reading its peers' buffers over xGMI with device-side cross-process flags) is not
+provided: it cannot be validated on the single-GPU boxes available to this build.
 """
 from __future__ import annotations
 

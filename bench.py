@@ -66,7 +66,7 @@ def _allreduce_probe(comm, dev) -> list:
         t = comm.reduce_max_scalar(t)
         alg = nbytes / t / 1e9
         out.append({"bytes": nbytes, "us": t * 1e6, "algbw_GBps": alg, "busbw_GBps": alg * 2 * (W - 1) / W})
-    # one-shot small-message path (all-gather + rank-ordered local sum) at the count-table size
+    # deterministic small-message path (RCCL all-gather + rank-ordered local sum) at the count-table size
     for nbytes, iters in ((8 << 10, 50), (64 << 10, 50)):
         x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
         for _ in range(3):
@@ -74,7 +74,7 @@ def _allreduce_probe(comm, dev) -> list:
         comm.barrier()
         t = _timed(lambda: [comm.all_reduce(x, algo="oneshot") for _ in range(iters)], dev) / iters
         t = comm.reduce_max_scalar(t)
-        out.append({"bytes": nbytes, "algo": "oneshot", "us": t * 1e6})
+        out.append({"bytes": nbytes, "algo": "allgather_ordered_sum", "us": t * 1e6})
     return out
 
 
@@ -112,11 +112,11 @@ def _ingest(rows: int, schema, dev, comm) -> dict:
         out["model_lines_s"] = _timed(lambda: lines.extend(nb.model_lines()), dev)
         assert int(nb.class_n.sum().item()) == rows
         total = out["load_s"] + out["fit_s"] + out["model_lines_s"]
-        from avenir_amd.data import table as _tb
+        cold = out["first_load_s"] + out["fit_s"] + out["model_lines_s"]
         out.update(rows=rows, file_bytes=nbytes, total_s=total, rows_per_s=rows / total,
+                   cold_total_s=cold, cold_rows_per_s=rows / cold,
                    parse_gbps=nbytes / out["load_s"] / 1e9, model_lines=len(lines),
-                   parser="device (K1 csv.hip)" if dev.type == "cuda" and nbytes >= _tb._GPU_CSV_MIN_BYTES
-                   else "host (csrc/host/csv.cpp)")
+                   parser=str((getattr(t, "meta", None) or {}).get("parser", "unknown")))
         return out
     finally:
         if os.path.exists(path):

@@ -189,3 +189,52 @@ def test_native_predictors_gpu_equal_cpu(tmp_path, name, monkeypatch):
         assert [a.rsplit(",", 1)[0] for a in g] == [b.rsplit(",", 1)[0] for b in c]
     else:
         assert g == c
+
+
+def _knn_oracle_pair(device):
+    """Mixed-type kNN (numeric block + category codes) and the one-hot oracle on the same records."""
+    import torch
+    from avenir_amd.models.knn import NearestNeighbor
+    g = torch.Generator().manual_seed(4)
+    n, q = 1500, 400
+    Xn = torch.rand((n + q, 5), generator=g)
+    Xc = torch.randint(0, 4, (n + q, 3), generator=g).int()
+    Xc[::37, 1] = -1                                        # missing categories
+    oh = torch.cat([torch.nn.functional.one_hot(Xc[:, j].long().clamp_min(0), 4).float()
+                    * (Xc[:, j:j + 1] >= 0) for j in range(3)], 1)
+    y = (Xn[:, 0] + (Xc[:, 0] == 2).float() > 0.9).long()
+    wc = torch.full((3,), 2.0)
+    dev = torch.device(device)
+    m = NearestNeighbor(k=7).fit_mixed(Xn[:n].to(dev), Xc[:n].to(dev), wc.to(dev), y[:n].to(dev), 2)
+    o = NearestNeighbor(k=7).fit(torch.cat([Xn, oh], 1)[:n].to(dev), y[:n].to(dev), 2)
+    dm, _ = m.kneighbors(Xn[n:].to(dev), Qc=Xc[n:].to(dev))
+    do, _ = o.kneighbors(torch.cat([Xn, oh], 1)[n:].to(dev))
+    return dm.cpu(), do.cpu()
+
+
+def test_mixed_knn_equals_one_hot_oracle_cpu():
+    dm, do = _knn_oracle_pair("cpu")
+    assert (dm - do).abs().max() < 1e-4
+
+
+@pytest.mark.gpu
+def test_mixed_knn_equals_one_hot_oracle_gpu(cuda):
+    dm, do = _knn_oracle_pair(cuda)
+    assert (dm - do).abs().max() < 1e-3
+
+
+def test_knn_job_mixed_path_matches_one_hot_fallback(tmp_path, monkeypatch):
+    """knnClassifier with categorical attributes runs mixed_knn (no one-hot matrix); forcing the
+    one-hot fallback (column limit 0) gives the same predictions up to equidistant-neighbour ties."""
+    from avenir_amd.ops import distance as D
+    argv, text = _setup(tmp_path, "knn")
+    cfg = _cfg(tmp_path, text)
+    calls = []
+    real = D.distributed_knn_mixed
+    monkeypatch.setattr(D, "distributed_knn_mixed", lambda *a, **k: calls.append(1) or real(*a, **k))
+    _run(argv + ["-o", tmp_path / "mixed.txt", "-c", cfg, "--device", "cpu"])
+    assert calls, "the mixed-type path did not run"
+    monkeypatch.setattr(D, "mixed_knn_max_dims", lambda: 0)
+    _run(argv + ["-o", tmp_path / "onehot.txt", "-c", cfg, "--device", "cpu"])
+    a, b = _lines(tmp_path / "mixed.txt"), _lines(tmp_path / "onehot.txt")
+    assert len(a) == len(b) and sum(x != y for x, y in zip(a, b)) <= 0.03 * len(b)
