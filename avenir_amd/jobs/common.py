@@ -162,6 +162,36 @@ class JobContext:
         IO_STATS["bytes_read"] += int(rec.stats.get("bytes", 0))
         return rec
 
+    def native_delim(self) -> str | None:
+        """The job's field delimiter when it is one literal character (native tokenizers), else None."""
+        from ..data.table import _literal
+        lit = _literal(self.delim_in)
+        return lit if lit is not None and len(lit) == 1 else None
+
+    def try_records(self, path: str | None = None, shard: bool = True, **kw):
+        """:meth:`records` when the input delimiter is one literal character, else None (the job
+        then takes its split-row path)."""
+        if self.native_delim() is None:
+            return None
+        return self.records(path, shard=shard, **kw)
+
+    def numeric_matrix(self, ords, dtype=torch.float64, path: str | None = None, shard: bool = True, **kw):
+        """(X [n, len(ords)] on the job's device, Records or None): fields ``ords`` parsed as
+        numbers — natively (mode 'n' at those fields, the rest skipped; ``kw`` adds modes for other
+        fields, e.g. ``extra={0: 'd'}``) or, for a regex delimiter, from split rows (then the
+        second value is the row list)."""
+        ords = list(ords)
+        extra = dict(kw.pop("extra", {}))
+        rec = self.try_records(path, shard=shard, modes=field_modes({**{o: "n" for o in ords}, **extra}),
+                               tail_mode="x", numeric=True, **kw)
+        if rec is None:
+            rows = self.rows(path, shard)
+            X = torch.tensor([[float(r[o]) for o in ords] for r in rows], dtype=dtype).view(len(rows), len(ords))
+            return X.to(self.device), rows
+        if not ords:
+            return torch.zeros((rec.n_lines, 0), dtype=dtype, device=rec.device), rec
+        return torch.stack([rec.field(o, numeric=True) for o in ords], 1).to(dtype), rec
+
     def line_base(self, n_local: int) -> int:
         """Global index of this rank's first line (exclusive scan of the line counts)."""
         if not self.comm.is_distributed:
@@ -342,6 +372,27 @@ def input_files(path: str) -> list[Path]:
         out += (sorted(f for f in p.iterdir() if f.is_file() and not f.name.startswith((".", "_")))
                 if p.is_dir() else [p])
     return out
+
+
+def field_modes(spec: dict[int, str], default: str = "x") -> str:
+    """Per-field tokenizer mode string (``data/records.read_records``) from ``{field: mode}``."""
+    if not spec:
+        return ""
+    return "".join(spec.get(j, default) for j in range(max(spec) + 1))
+
+
+def field_columns(spans, width: int, delims: str, replace: dict | None = None, drop=()) -> list:
+    """``format_lines`` columns re-emitting fields ``0..width-1`` of each raw line (byte spans),
+    with ``replace[j]`` columns (one column or a list) in place of field j and ``drop`` removed."""
+    replace = replace or {}
+    cols = []
+    for j in range(width):
+        if j in replace:
+            r = replace[j]
+            cols += r if isinstance(r, list) else [r]
+        elif j not in drop:
+            cols.append(spans.column("rf", j, delims))
+    return cols
 
 
 def fmt(x: float, prec: int = 3) -> str:

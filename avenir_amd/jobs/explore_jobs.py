@@ -89,8 +89,7 @@ def numcorr(args):
     ctx = JobContext(args, "nuc.")
     pairs = _pairs(ctx.get_str("attr.pairs"))
     ords = sorted({o for p in pairs for o in p})
-    rows = ctx.rows()
-    X = torch.tensor([[float(r[o]) for o in ords] for r in rows], dtype=torch.float64, device=ctx.device)
+    X, _ = ctx.numeric_matrix(ords)
     n = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=ctx.device)
     s = X.sum(0)
     G = X.T @ X
@@ -118,23 +117,36 @@ def rule_evaluator(args):
     per-rule class counts are one ``[R, C]`` tensor, all-reduced once; output
     ``name,confidence,support`` with ``rue.conf.strategy`` confAccuracy | confEntropy
     (:231-268; support divides by ``rue.data.size`` when given, else by the global record count)."""
-    from ..utils.rules import ColumnCache, rules_from_config
+    from ..utils.rules import ColumnCache, RecordColumns, rule_field_modes, rules_from_config
+    from .common import field_modes
     ctx = JobContext(args, "rue.")
     rules = rules_from_config(ctx.cfg)
     cls_ord = ctx.get_int("class.attr.ord")
     classes = ctx.get_list("class.values", None)
-    rows = ctx.rows(keep_empty=True)
-    cols = ColumnCache(rows, ctx.device)
-    if not classes:
-        classes = ctx.union(r[cls_ord] for r in rows)
+    fm = rule_field_modes(rules.values(), {cls_ord: "d"})
+    rec = ctx.try_records(modes=field_modes(fm), tail_mode="x", numeric=True, trim=True)
+    if rec is not None:           # native: predicate fields tokenized once, rules evaluated on the device
+        cols = RecordColumns(rec, [o for o, m in fm.items() if m == "n"])
+        cc = rec.field(cls_ord)
+        if not classes:
+            classes = ctx.union(rec.strings(torch.unique(cc[cc >= 0])))
+        lab = rec.map_codes(cc, classes).long()
+        n_rows = rec.n_lines
+    else:
+        rows = ctx.rows(keep_empty=True)
+        cols = ColumnCache(rows, ctx.device)
+        if not classes:
+            classes = ctx.union(r[cls_ord] for r in rows)
+        ci = {c: i for i, c in enumerate(classes)}
+        lab = torch.tensor([ci.get(r[cls_ord], -1) for r in rows], dtype=torch.long, device=ctx.device)
+        n_rows = len(rows)
     ci = {c: i for i, c in enumerate(classes)}
-    lab = torch.tensor([ci.get(r[cls_ord], -1) for r in rows], dtype=torch.long, device=ctx.device)
     C, R = len(classes), len(rules)
     counts = torch.zeros((R, C), dtype=torch.float64, device=ctx.device)
     for k, (name, rexp) in enumerate(rules.items()):
         m = rexp.evaluate(cols) & (lab >= 0)
         counts[k] = torch.bincount(lab[m], minlength=C)[:C].double()
-    n = torch.tensor([float(len(rows))], dtype=torch.float64, device=ctx.device)
+    n = torch.tensor([float(n_rows)], dtype=torch.float64, device=ctx.device)
     ctx.all_reduce(counts, n)
     size = ctx.get_int("data.size", None) or int(n)
     strat = ctx.get_str("conf.strategy", "confAccuracy")
@@ -390,9 +402,19 @@ def undersampling(args):
     the draw of record g is the K25 Philox stream at the GLOBAL record index, so the kept set does
     not depend on the world size (models/sampling.undersample)."""
     from ..models.sampling import undersample
+    from .common import field_modes
     ctx = JobContext(args, "usb.")
-    lines = ctx.lines()
     cls_ord = ctx.get_int("class.attr.ord")
+    rec = ctx.try_records(modes=field_modes({cls_ord: "d"}), tail_mode="x")
+    if rec is not None:
+        cc = rec.field(cls_ord)
+        vals = ctx.union(rec.strings(torch.unique(cc[cc >= 0])))
+        y = rec.map_codes(cc, vals).long().cpu()
+        keep = undersample(y, seed=ctx.get_int("random.seed", 0), comm=ctx.comm).bool()
+        spans = rec.line_spans().select(keep)
+        ctx.emit_columns([spans.column("r")], len(spans))
+        return
+    lines = ctx.lines()
     sp = ctx.split
     vals = ctx.union(sp(l)[cls_ord] for l in lines)
     vi = {v: i for i, v in enumerate(vals)}
@@ -428,12 +450,10 @@ def bagging(args):
 @job("adaBoostError", "weighted misclassification error (J/explore/AdaBoostError.java, abe.*)")
 def adaboost_error(args):
     ctx = JobContext(args, "abe.")
-    rows = ctx.rows()
     po, ao, bo = (ctx.get_int("pred.class.attr.ord"), ctx.get_int("actual.class.attr.ord"),
                   ctx.get_int("boost.attr.ord"))
-    wrong = torch.tensor([float(r[po] != r[ao]) for r in rows], dtype=torch.float64)
-    w = torch.tensor([float(r[bo]) for r in rows], dtype=torch.float64)
-    acc = torch.stack([(wrong * w).sum(), torch.tensor(float(len(rows)), dtype=torch.float64)])
+    w, wrong, n_rows, _ = _boost_columns(ctx, po, ao, bo)
+    acc = torch.stack([(wrong.double() * w).sum(), torch.tensor(float(n_rows), dtype=torch.float64, device=w.device)])
     ctx.all_reduce(acc)
     err = float(acc[0]) if ctx.get_bool("weight.normalized", False) else float(acc[0]) / max(float(acc[1]), 1)
     ctx.emit_root([f"error={fmt(err, ctx.get_int('output.precision', 6))}"])
@@ -448,11 +468,18 @@ def adaboost_update(args):
                   ctx.get_int("boost.attr.ord"))
     prec = int(ctx.cfg.values.get("abe.output.precision", 6))
     init = ctx.get_float("intial.weight", 1.0)
-    rows = ctx.rows()
-    w = torch.tensor([float(r[bo]) for r in rows], dtype=torch.float64)
-    wrong = torch.tensor([r[po] != r[ao] for r in rows])
+    w, wrong, n_rows, src = _boost_columns(ctx, po, ao, bo)
     nw = w * torch.exp(torch.where(wrong, torch.full_like(w, alpha), torch.full_like(w, -alpha))) if err < 0.5 \
         else torch.full_like(w, init)
+    if not isinstance(src, list):         # native: the raw fields around the new weight
+        from .common import field_columns
+        width = src.width()
+        if width is None:
+            raise SystemExit("adaBoostUpdate: records of differing field counts")
+        spans = src.line_spans()
+        ctx.emit_columns(field_columns(spans, width, ctx.native_delim(), {bo: ("f", nw.cpu(), prec)}), n_rows)
+        return
+    rows = src
     d = ctx.delim_out
     out = []
     for r, v in zip(rows, nw.tolist()):
@@ -460,6 +487,18 @@ def adaboost_update(args):
         r[bo] = fmt(v, prec)
         out.append(d.join(r))
     ctx.emit(out)
+
+
+def _boost_columns(ctx, po, ao, bo):
+    """(boost weights f64, misclassified bool, record count, Records or the split rows)."""
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({po: "d", ao: "d", bo: "n"}), tail_mode="x", numeric=True)
+    if rec is not None:
+        return rec.field(bo, numeric=True).double(), rec.field(po) != rec.field(ao), rec.n_lines, rec
+    rows = ctx.rows()
+    w = torch.tensor([float(r[bo]) for r in rows], dtype=torch.float64)
+    wrong = torch.tensor([r[po] != r[ao] for r in rows], dtype=torch.bool)
+    return w, wrong, len(rows), rows
 
 
 # ================================================================================================
@@ -510,9 +549,32 @@ def feature_hashing_job(args):
     """Index hash = Java ``String.hashCode`` mod ``encoding.size``, sign = FNV-1a parity; the vector
     replaces the categorical fields at ``encoding.vecOffset`` among the remaining fields.  Values
     are hashed once per distinct value, the [n, size] encoding is one scatter-add."""
+    from .common import field_columns, field_modes
     ctx = JobContext(args, app="categoricalFeatureHashingEncoding")
     cat = ctx.get_int_list("cat.fieldOrdinals")
     size = ctx.get_int("encoding.size")
+    rec = ctx.try_records(modes=field_modes({o: "d" for o in cat}), tail_mode="x")
+    if rec is not None and rec.width() is not None:
+        # native: each distinct value hashed once (dictionary level), the [n, size] encoding one
+        # scatter-add on the device, the other fields re-emitted from the raw line bytes
+        n, width = rec.n_lines, rec.width()
+        codes = torch.stack([rec.field(o).long() for o in cat], 1) if cat else \
+            torch.zeros((n, 0), dtype=torch.long, device=rec.device)
+        idx = torch.tensor([abs(java_hash(v)) % size for v in rec.vocab] or [0], dtype=torch.long,
+                           device=rec.device)
+        sgn = torch.tensor([1 if fnv_hash(v) % 2 == 1 else -1 for v in rec.vocab] or [0], dtype=torch.long,
+                           device=rec.device)
+        enc = torch.zeros((n, size), dtype=torch.long, device=rec.device)
+        if n and rec.vocab and cat:
+            enc.scatter_add_(1, idx[codes.clamp_min(0)], sgn[codes.clamp_min(0)] * (codes >= 0))
+        rem = [i for i in range(width) if i not in set(cat)]
+        off = ctx.get_int("encoding.vecOffset", len(rem))
+        spans = rec.line_spans()
+        dl = ctx.native_delim()
+        other = [spans.column("rf", i, dl) for i in rem]
+        enc_h = enc.cpu()
+        ctx.emit_columns(other[:off] + [("i", enc_h[:, j]) for j in range(size)] + other[off:], n)
+        return
     rows = ctx.rows()
     n = len(rows)
     vocab: dict[str, int] = {}
@@ -548,6 +610,12 @@ def loo_encoding(args):
     prec = ctx.get_int("ouput.precision", 3)
     train = ctx.get_bool("train.data.set", True)
     stat_path = ctx.get_str("target.stat.file.path", None)
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({**{o: "d" for o in cat}, cls_ord: "d" if pos is not None else "n"}),
+                          tail_mode="x", numeric=pos is None)
+    if rec is not None and rec.width() is not None:
+        _loo_native(ctx, rec, cat, cls_ord, pos, reg, sd, prec, train, stat_path)
+        return
     rows = ctx.rows()
     yv = torch.tensor([(1.0 if r[cls_ord] == pos else -1.0) if pos is not None else float(r[cls_ord]) for r in rows],
                       dtype=torch.float64)
@@ -593,12 +661,85 @@ def loo_encoding(args):
     ctx.emit(out)
 
 
+def _loo_native(ctx, rec, cat, cls_ord, pos, reg, sd, prec, train, stat_path):
+    """categoricalLeaveOneOutEncoding on a native token table: per (field, dictionary code) count
+    and target sums as one [F, V] scatter-add + all-reduce, the encoding a gather, the output the
+    raw line bytes with the encoded fields replaced."""
+    from .common import field_columns
+    n, V, F = rec.n_lines, max(1, len(rec.vocab)), len(cat)
+    dev = rec.device
+    if pos is not None:
+        pc = rec.vocab.index(pos) if pos in rec.vocab else -2
+        yv = torch.where(rec.field(cls_ord) == pc, 1.0, -1.0).double()
+    else:
+        yv = rec.field(cls_ord, numeric=True).double()
+    codes = torch.stack([rec.field(o).long() for o in cat], 1) if F else torch.zeros((n, 0), dtype=torch.long, device=dev)
+    flat = (torch.arange(F, device=dev).view(1, -1) * V + codes.clamp_min(0)).view(-1)
+    if train:
+        cnt = torch.zeros(F * V, dtype=torch.float64, device=dev)
+        sm = torch.zeros(F * V, dtype=torch.float64, device=dev)
+        cnt.index_add_(0, flat, torch.ones(flat.numel(), dtype=torch.float64, device=dev))
+        sm.index_add_(0, flat, yv.view(-1, 1).expand(n, F).reshape(-1))
+        ctx.all_reduce(cnt, sm)
+        if stat_path and ctx.is_root:
+            from pathlib import Path
+            ch, sh = cnt.view(F, V).cpu(), sm.view(F, V).cpu()
+            d = ctx.delim_out
+            lines = []
+            for o in sorted(set(cat)):      # (field, value) keys in sorted order, as the row path's union
+                j = cat.index(o)
+                present = torch.nonzero(ch[j] > 0).view(-1).tolist()
+                for c in sorted(present, key=lambda c: rec.vocab[c]):
+                    lines.append(f"{o}{d}{rec.vocab[c]}{d}{int(ch[j, c])}{d}{int(sh[j, c])}")
+            Path(stat_path).parent.mkdir(parents=True, exist_ok=True)
+            Path(stat_path).write_text("\n".join(lines) + "\n")
+    else:
+        cnt = torch.zeros(F * V, dtype=torch.float64)
+        sm = torch.zeros(F * V, dtype=torch.float64)
+        vi = {v: i for i, v in enumerate(rec.vocab)}
+        fi = {o: j for j, o in enumerate(cat)}
+        for l in ctx.all_lines(stat_path):
+            p = ctx.split(l)
+            j, c = fi.get(int(p[0])), vi.get(p[1])
+            if j is not None and c is not None:
+                cnt[j * V + c], sm[j * V + c] = float(p[2]), float(p[3])
+        cnt, sm = cnt.to(dev), sm.to(dev)
+    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + ctx.comm.rank)
+    c_, s_ = cnt[flat].view(n, F), sm[flat].view(n, F)
+    rep = {}
+    for j, o in enumerate(cat):
+        if train:
+            noise = (1.0 + (torch.randn(n, generator=g, dtype=torch.float64) * sd).clamp(-3 * sd, 3 * sd)).to(dev)
+            e = (s_[:, j] - yv) / (c_[:, j] - 1 + reg) * noise
+        else:
+            e = s_[:, j] / (c_[:, j] + reg)
+        rep[o] = ("f", e.cpu(), prec)
+    ctx.emit_columns(field_columns(rec.line_spans(), rec.width(), ctx.native_delim(), rep), n)
+
+
 @job("binaryDummyVariableGenerator", "one-hot (binary dummy) expansion of categorical fields (S/util/BinaryDummyVariableGenerator.scala)")
 def binary_dummy_job(args):
     ctx = JobContext(args, app="binaryDummyVariableGenerator")
     cat = ctx.get_int_list("cat.field.ordinals")
     tv, fv = ctx.get_str("true.value", "1"), ctx.get_str("false.value", "0")
     ci = ctx.get_bool("case.insensitive", False)
+    from .common import field_columns, field_modes
+    rec = ctx.try_records(modes=field_modes({o: "d" for o in cat}), tail_mode="x")
+    if rec is not None and rec.width() is not None:
+        voc = [v.lower() for v in rec.vocab] if ci else rec.vocab
+        rep = {}
+        for o in cat:
+            c = rec.field(o)
+            u = ctx.cfg.get_list(f"fieldUniqueValues.{o}", None)
+            if u is None:
+                u = ctx.union(rec.strings(torch.unique(c[c >= 0])))
+            u = [x.lower() for x in u] if ci else u
+            ui = {x: i for i, x in enumerate(u)}
+            lut = torch.tensor([ui.get(v, -1) for v in voc] or [-1], dtype=torch.long, device=rec.device)
+            k = torch.where(c >= 0, lut[c.long().clamp_min(0)], torch.full_like(c.long(), -1)).cpu()
+            rep[o] = [("s", [fv, tv], (k == i).long()) for i in range(len(u))]
+        ctx.emit_columns(field_columns(rec.line_spans(), rec.width(), ctx.native_delim(), rep), rec.n_lines)
+        return
     rows = ctx.rows()
     uniq = {}
     for o in cat:
@@ -631,8 +772,15 @@ def linear_mapper(args):
     prec = ctx.get_int("output.precision", 3)
     M = torch.tensor([[float(x) for x in l.split(",")] for l in ctx.all_lines(ctx.path("trans.matrix.path"))],
                      dtype=torch.float64, device=ctx.device)
-    rows = ctx.rows()
-    X = torch.tensor([[float(r[o]) for o in q] for r in rows], dtype=torch.float64, device=ctx.device).view(len(rows), len(q))
+    X, src = ctx.numeric_matrix(q)
+    if not isinstance(src, list):      # native: one GEMM, ids / retained fields from the raw bytes
+        Y = (X @ M.T).cpu()
+        spans, dl = src.line_spans(), ctx.native_delim()
+        ctx.emit_columns([spans.column("rf", o, dl) for o in ids] + [("f", Y[:, j].contiguous(), prec)
+                                                                     for j in range(Y.shape[1])]
+                         + [spans.column("rf", o, dl) for o in ret], src.n_lines)
+        return
+    rows = src
     Y = (X @ M.T).cpu().tolist()
     d = ctx.delim_out
     ctx.emit([d.join([r[o] for o in ids] + [fmt(v, prec) for v in y] + [r[o] for o in ret]) for r, y in zip(rows, Y)])
@@ -649,14 +797,21 @@ def incremental_pca(args):
     ids = ctx.get_int_list("id.field.ordinals")
     q = ctx.get_int_list("quant.field.ordinals")
     prec = ctx.get_int("output.precision", 3)
-    groups = defaultdict(list)
-    for r in ctx.rows(shard=False):
-        groups[":".join(r[o] for o in ids)].append([float(r[o]) for o in q])
-    keys = sorted(groups)
-    if ctx.comm.is_distributed:
-        from ..data.table import shard_range
-        a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
-        keys = keys[a:b]
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({**{o: "d" for o in ids}, **{o: "n" for o in q}}), tail_mode="x",
+                          numeric=True)
+    if rec is not None:
+        keys, streams = _keyed_streams(ctx, rec, ids, q)
+    else:
+        groups = defaultdict(list)
+        for r in ctx.rows(shard=False):
+            groups[":".join(r[o] for o in ids)].append([float(r[o]) for o in q])
+        keys = sorted(groups)
+        if ctx.comm.is_distributed:
+            from ..data.table import shard_range
+            a, b = shard_range(len(keys), ctx.comm.rank, ctx.comm.world)
+            keys = keys[a:b]
+        streams = {k: torch.tensor(groups[k], dtype=torch.float64) for k in keys}
     ipca = IncrementalPCA(len(q), forget=ctx.get_float("forget.factor", 0.96),
                           low_energy=ctx.get_float("energy.lowThreshold", 0.95),
                           high_energy=ctx.get_float("energy.highThreshold", 0.98), device=ctx.device)
@@ -670,13 +825,35 @@ def incremental_pca(args):
             st = PrincipalCompState.load(blk[i:i + 3 + nh], d)
             ipca.states[st.key] = st
             i += 3 + nh
-    states = ipca.update({k: torch.tensor(groups[k], dtype=torch.float64) for k in keys})
+    states = ipca.update(streams)
     lines = [l for k in keys for l in states[k].serialize(d, prec)]
     lines = ctx.gather_lines(lines)
     if sp and ctx.is_root:
         Path(sp).parent.mkdir(parents=True, exist_ok=True)
         Path(sp).write_text("\n".join(lines) + "\n")
     ctx.emit_root(lines)
+
+
+def _keyed_streams(ctx, rec, key_ords, val_ords):
+    """(this rank's keys in order, {key: [n_k, D] float64 rows in input order}) of a native table:
+    byte-range shards, composite keys ranked in the reducer's order, rows shuffled to the rank that
+    owns their key (one all-to-all), grouped by a stable device sort."""
+    from ..data.records import owner_of, shuffle, sorted_key_tuples
+    comm = ctx.comm
+    kpos, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in key_ords], comm)
+    gidx = rec.line_base + torch.arange(rec.n_lines, device=rec.device)
+    vals = [rec.field(o, numeric=True).double() for o in val_ords]
+    if comm.is_distributed:
+        kpos, gidx, *vals = shuffle(comm, owner_of(kpos, G, comm.world), [kpos, gidx] + vals)
+    o1 = torch.argsort(gidx, stable=True)
+    o2 = torch.argsort(kpos[o1], stable=True)
+    order = o1[o2]
+    X = torch.stack(vals, 1)[order] if vals else torch.zeros((order.numel(), 0), dtype=torch.float64)
+    ks = kpos[order]
+    uk, cnt = torch.unique_consecutive(ks, return_counts=True)
+    names = [":".join(rec.vocab[c] for c in row) for row in ktab[uk.cpu()].tolist()]
+    parts = torch.split(X.cpu(), cnt.cpu().tolist())
+    return names, dict(zip(names, parts))
 
 
 @job("individualConditionalExpectation", "ICE curves by grid expansion + in-process batched model inference (S/interpret/IndividualConditionalExpectation.scala)")
@@ -697,6 +874,22 @@ def ice_job(args):
            "lr": SV.LogisticRegressionDiscriminant}[args.kind]
     model = cls(ctx.get_str("model.config", None) or args.model, device=args.device)
     model.train()
+    rec = ctx.try_records(modes="x" * kl, tail_mode="n", numeric=True)
+    if rec is not None and rec.width() is not None:
+        n, V = rec.n_lines, len(vals)
+        X = rec.nums.view(n, rec.width())[:, kl:].double().cpu()
+        G = X.repeat_interleave(V, 0)
+        G[:, feat] = torch.tensor(vals, dtype=torch.float64).repeat(n)
+        p = torch.as_tensor(model.predictProb(G.numpy()))
+        p = (p[:, -1] if p.dim() == 2 else p).double().view(n, V)
+        order = torch.sort(p, 1, descending=desc, stable=True).indices
+        rows_i = torch.arange(n).repeat_interleave(V)
+        spans, dl = rec.line_spans().select(rows_i), ctx.native_delim()
+        cols = [spans.column("rf", j, dl) for j in range(kl)]
+        vt = torch.tensor(vals, dtype=torch.float64)
+        cols += [("f", vt[order.reshape(-1)], -1), ("f", torch.gather(p, 1, order).reshape(-1), prec)]
+        ctx.emit_columns(cols, n * V)
+        return
     rows = ctx.rows()
     X = torch.tensor([[float(v) for v in r[kl:]] for r in rows], dtype=torch.float64)
     G = X.repeat_interleave(len(vals), 0)

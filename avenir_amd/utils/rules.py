@@ -89,26 +89,6 @@ class RuleExpression:
         return self.evaluate(ColumnCache(rows, device))
 
 
-class RecordColumns:
-    """ColumnCache's interface over a native token table (data/records.Records): ``codes(o)`` are
-    the table's dictionary codes of field ``o`` (read with mode 'd', trimmed), ``numeric(o)`` its
-    parsed doubles (mode 'n'), both on the table's device; no Python string per record."""
-
-    def __init__(self, rec):
-        self.rec, self.n, self.device = rec, rec.n_lines, rec.device
-        self._vocab: dict[str, int] | None = None
-
-    def numeric(self, o: int) -> torch.Tensor:
-        return self.rec.field(o, numeric=True)
-
-    def codes(self, o: int):
-        if self._vocab is None:
-            self._vocab = {}
-            for i, v in enumerate(self.rec.vocab):
-                self._vocab.setdefault(v, i)
-        return self.rec.field(o).long(), self._vocab
-
-
 class ColumnCache:
     """Lazily tensorised columns of a list of split records."""
 
@@ -153,6 +133,52 @@ class ColumnCache:
         lut = torch.tensor([{"gt": s > v, "ge": s >= v, "lt": s < v, "le": s <= v}[p.op] for s in inv],
                            dtype=torch.bool, device=c.device)
         return lut[c] if len(inv) else torch.zeros_like(c, dtype=torch.bool)
+
+
+class RecordColumns(ColumnCache):
+    """ColumnCache's interface over a native token table (data/records.Records): ``codes(o)`` are
+    the table's dictionary codes of field ``o`` (read with mode 'd', trimmed), ``numeric(o)`` its
+    parsed doubles — the table's own numbers for fields read with mode 'n' (``num_fields``), else
+    the numeric value of each dictionary string; everything stays on the table's device, no
+    Python string per record."""
+
+    def __init__(self, rec, num_fields=None):
+        self.rec, self.n, self.device = rec, rec.n_lines, rec.device
+        self.num_fields = None if num_fields is None else set(num_fields)
+        self._vocab: dict[str, int] | None = None
+        self._lut = None
+        self._num, self._codes = {}, {}
+
+    def numeric(self, o: int) -> torch.Tensor:
+        if self.rec.nums is not None and (self.num_fields is None or o in self.num_fields):
+            return self.rec.field(o, numeric=True)
+        if self._lut is None:
+            from ..data.records import numeric_lut
+            self._lut = numeric_lut(self.rec.vocab, self.device)
+        c = self.rec.field(o).long()
+        if self._lut.numel() == 0:
+            return torch.full(c.shape, math.nan, dtype=torch.float64, device=self.device)
+        return torch.where(c >= 0, self._lut[c.clamp_min(0)], torch.full(c.shape, math.nan, dtype=torch.float64,
+                                                                            device=self.device))
+
+    def codes(self, o: int):
+        if self._vocab is None:
+            self._vocab = {}
+            for i, v in enumerate(self.rec.vocab):
+                self._vocab.setdefault(v, i)
+        return self.rec.field(o).long(), self._vocab
+
+
+def rule_field_modes(rules, extra: dict | None = None) -> dict[int, str]:
+    """Tokenizer mode per field referenced by ``rules``: 'n' when every predicate on the field
+    compares numerically, else 'd' (``extra`` adds / overrides fields)."""
+    m: dict[int, str] = {}
+    for r in rules:
+        for p in r.predicates:
+            num = p.numeric and p.op in ("gt", "ge", "lt", "le", "eq", "ne")
+            m[p.ordinal] = "n" if num and m.get(p.ordinal, "n") == "n" else "d"
+    m.update(extra or {})
+    return m
 
 
 def rules_from_config(cfg, names_key: str = "rule.names", rule_prefix: str = "rule.",

@@ -1,0 +1,117 @@
+"""Record-wise exploration / encoding jobs on native input and output (no
+per-row Python in the jobs' main paths).
+
+Each job runs twice on the same data: the native path (one-character delimiter: the K1 token
+table, device columns, the native formatter writing raw line bytes) and the split-row path (the
+same delimiter as the regex ``[,]``) — outputs must be identical.  The keyed / data-parallel ones
+also run at world 2 (gloo ranks, byte-range shards) and must equal world 1."""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from avenir_amd.cli import main
+
+from _dist import run_world
+
+
+def _lines(p):
+    p = Path(p)
+    if p.is_dir():
+        return [l for f in sorted(p.iterdir()) if f.is_file() for l in f.read_text().splitlines() if l.strip()]
+    return [l for l in p.read_text().splitlines() if l.strip()]
+
+
+def _cat_rows(n=700, seed=3):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        a = rng.choice(["x", "y", "z", "Y"])
+        b = a if rng.random() < 0.7 else rng.choice(["x", "y", "z"])
+        c = rng.choice(["p", "q"])
+        cls = "T" if (a == "x" and rng.random() < 0.8) or rng.random() < 0.2 else "F"
+        rows.append(f"r{i},{a},{b},{c},{cls},{rng.random():.4f},{rng.normal():.5f}")
+    return rows
+
+
+def _setup(tmp: Path, name: str, regex: bool):
+    """(argv, config path) of case ``name`` with the literal or the regex delimiter."""
+    data = tmp / "d.csv"
+    data.write_text("\n".join(_cat_rows()) + "\n")
+    dl = "[,]" if regex else ","
+    tag = "re" if regex else "lit"
+    if name in ("hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca"):
+        num = tmp / "num.csv"
+        if not num.exists():
+            rng = np.random.default_rng(8)
+            num.write_text("\n".join(f"k{int(rng.integers(0, 9))},{rng.normal():.5f},{rng.normal():.5f},w{i}"
+                                     for i in range(900)) + "\n")
+        (tmp / "M.txt").write_text("1,1\n1,-1\n0.5,2\n")
+        stat = tmp / f"stat_{tag}.txt"
+        if name == "loo_test":
+            stat.write_text("1,x,100,20\n1,y,50,-10\n1,z,40,2\n1,Y,12,5\n2,x,70,7\n2,y,30,3\n2,z,10,-1\n2,Y,9,1\n")
+        block = {
+            "hash": ("categoricalFeatureHashingEncoding", "cat.fieldOrdinals = [1,3]\n encoding.size = 6\n"),
+            "loo": ("categoricalLeaveOneOutEncoding", f"cat.field.ordinals = [2,1]\n class.field.ordinal = 4\n"
+                    f' class.pos.val = "T"\n rand.std.dev = 0.2\n train.data.set = true\n'
+                    f' target.stat.file.path = "{stat}"\n'),
+            "loo_test": ("categoricalLeaveOneOutEncoding", f"cat.field.ordinals = [1,2]\n class.field.ordinal = 4\n"
+                         f' class.pos.val = "T"\n train.data.set = false\n target.stat.file.path = "{stat}"\n'),
+            "dummy": ("binaryDummyVariableGenerator", 'cat.field.ordinals = [1,3]\n true.value = "T"\n'),
+            "dummy_ci": ("binaryDummyVariableGenerator", "cat.field.ordinals = [1]\n case.insensitive = true\n"
+                         ' fieldUniqueValues.1 = ["x", "y"]\n'),
+            "lmap": ("linearMapper", f'id.field.ordinals = [3]\n quant.field.ordinals = [1,2]\n'
+                     f' retained.field.ordinals = [0]\n trans.matrix.path = "{tmp / "M.txt"}"\n output.precision = 4\n'),
+            "ipca": ("incrementalPrincipalComponent", "id.field.ordinals = [0]\n quant.field.ordinals = [1,2]\n"),
+        }[name]
+        conf = tmp / f"{name}_{tag}.conf"
+        conf.write_text(f'{block[0]} {{\n field.delim.in = "{dl}"\n {block[1]}}}\n')
+        inp = num if name in ("lmap", "ipca") else data
+        return [block[0], "-i", inp], conf
+    props = {
+        "nuc": ("numericalCorrelation", "nuc.attr.pairs=5:6,6:5\n"),
+        "rue": ("ruleEvaluator", "rue.rule.names=r1,r2,r3\nrue.rule.r1=1 eq x > T\n"
+                "rue.rule.r2=1 in y:z and 3 eq p > F\nrue.rule.r3=5 gt 0.5 and 6 le 0 > T\nrue.class.attr.ord=4\n"),
+        "usb": ("underSamplingBalancer", "usb.class.attr.ord=4\n"),
+        "abe": ("adaBoostError", "abe.pred.class.attr.ord=1\nabe.actual.class.attr.ord=2\nabe.boost.attr.ord=5\n"),
+    }
+    if name == "abu":
+        err = tmp / "err.txt"
+        err.write_text("error=0.3\n")
+        job, text = "adaBoostUpdate", (f"abu.pred.class.attr.ord=1\nabu.actual.class.attr.ord=2\nabu.boost.attr.ord=5\n"
+                                       f"abu.error.file.path={err}\nabe.output.precision=5\n")
+    else:
+        job, text = props[name]
+    cfg = tmp / f"{name}_{tag}.properties"
+    cfg.write_text(text + f"field.delim.regex={dl}\n")
+    return [job, "-i", data], cfg
+
+
+CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_native_equals_row_path(tmp_path, name):
+    argv, cfg = _setup(tmp_path, name, False)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "native"), "-c", str(cfg), "--device", "cpu"]) == 0
+    argv, cfg2 = _setup(tmp_path, name, True)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "rows"), "-c", str(cfg2), "--device", "cpu"]) == 0
+    got, ref = _lines(tmp_path / "native"), _lines(tmp_path / "rows")
+    assert got and got == ref
+    if name == "loo":
+        assert _lines(tmp_path / "stat_lit.txt") == _lines(tmp_path / "stat_re.txt")
+
+
+def _world(rank, world, argv, out, cfg):
+    assert main([str(a) for a in argv] + ["-o", out, "-c", cfg, "--device", "cpu"]) == 0
+    return True
+
+
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca"])
+def test_world2_equals_world1(tmp_path, name):
+    argv, cfg = _setup(tmp_path, name, False)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
+    run_world(_world, 2, [str(a) for a in argv], str(tmp_path / "w2"), str(cfg), timeout=300)
+    assert _lines(tmp_path / "w2") == _lines(tmp_path / "w1")
