@@ -460,9 +460,8 @@ def ks(args):
         from .pipeline_stages import ks_from_distr
         return ks_from_distr(ctx)
     col = ctx.get_int("attr.ordinal", 0)
-    sp = ctx.split
-    ref = torch.tensor([float(sp(l)[col]) for l in ctx.all_lines(args.train)], dtype=torch.float64)
-    cur = torch.tensor([float(sp(l)[col]) for l in ctx.all_lines()], dtype=torch.float64)
+    ref = ctx.numeric_matrix([col], path=args.train, shard=False)[0][:, 0].cpu()
+    cur = ctx.numeric_matrix([col], shard=False)[0][:, 0].cpu()
     bw = ctx.get_float("bin.width", float((ref.max() - ref.min()) / 50 or 1))
     lo = float(min(ref.min(), cur.min()))
     nb = int((float(max(ref.max(), cur.max())) - lo) / bw) + 1
@@ -651,7 +650,7 @@ def kmeans(args):
     from ..models.cluster import KMeans
     ctx = JobContext(args, "kmc.")
     cols = ctx.get_int_list("attr.ordinals", "0")
-    X = torch.tensor([[float(r[c]) for c in cols] for r in ctx.rows()], device=ctx.device)
+    X = ctx.numeric_matrix(cols, dtype=torch.float32)[0]
     ks = [int(k) for k in (args.k or ctx.get_str("num.clusters", "3")).split(",")]
     km = KMeans(ks, n_init=ctx.get_int("num.init.groups", 3), max_iter=ctx.get_int("max.iterations", 100)).fit(X)
     lines = []

@@ -437,9 +437,37 @@ def spc(args):
     thr = ctx.get_float("score.threshold")
     expr = ctx.get_str("cond.expression").replace("$0", str(q))
     rule = RuleExpression.from_condition(expr)
+    from ..utils.rules import RecordColumns, rule_field_modes
+    from .common import field_modes
+    fm = rule_field_modes([rule], {so: "n"})
+    rec = ctx.try_records(modes=field_modes(fm), tail_mode="x", numeric=True, trim=True)
+    if rec is not None:
+        # native: each rank tokenizes its byte range; the (time, condition) pairs of all ranks are
+        # one all-gather (16 bytes a record), every rank scores the global time order and writes
+        # the records of its own range
+        t_l = rec.field(so, numeric=True).double()
+        met_l = rule.evaluate(RecordColumns(rec, [o for o, m in fm.items() if m == "n"])).double()
+        comm = ctx.comm
+        pair = torch.stack([t_l, met_l], 1)
+        allp = comm.all_gather_v(pair.cpu()) if comm.is_distributed else pair.cpu()
+        score = _locality_scores(allp[:, 0], allp[:, 1], span)
+        base = rec.line_base
+        sc = score[base: base + rec.n_lines]
+        keep = sc > thr
+        spans, dl = rec.line_spans().select(keep), ctx.native_delim()
+        ctx.emit_columns([spans.column("rf", so, dl), spans.column("rf", q, dl), ("f", sc[keep], 3)], len(spans))
+        return
     rows = ctx.rows(shard=False)
     t = torch.tensor([float(r[so]) for r in rows], dtype=torch.float64)
     met = rule.evaluate_rows(rows).double()
+    score = _locality_scores(t, met, span)
+    d = ctx.delim_out
+    ctx.emit_root([f"{r[so]}{d}{r[q]}{d}{fmt(s)}" for r, s in zip(rows, score.tolist()) if s > thr])
+
+
+def _locality_scores(t: torch.Tensor, met: torch.Tensor, span: float) -> torch.Tensor:
+    """Fraction of condition-meeting events among the events of the trailing ``span`` (time
+    order, ties in input order) of every event."""
     order = torch.argsort(t, stable=True)
     ts, ms = t[order], met[order]
     cm = torch.cumsum(ms, 0)
@@ -449,8 +477,7 @@ def spc(args):
     met_in = cm - torch.where(lo > 0, cm[(lo - 1).clamp_min(0)], torch.zeros_like(cm))
     score = torch.zeros_like(t)
     score[order] = met_in / n_in
-    d = ctx.delim_out
-    ctx.emit_root([f"{r[so]}{d}{r[q]}{d}{fmt(s)}" for r, s in zip(rows, score.tolist()) if s > thr])
+    return score
 
 
 # ================================================================================================
@@ -589,6 +616,11 @@ def cont_time_stats(args):
         p = l.strip()[1:-1].split(d)
         rates[tuple(p[:kl])] = torch.tensor([float(x) for x in p[kl:kl + S * S]], dtype=torch.float64).view(S, S)
     si = {s: i for i, s in enumerate(states)}
+    from .common import field_modes
+    rec = ctx.try_records(modes="d" * (kl + 2), tail_mode="x")
+    if rec is not None:
+        _cont_time_native(ctx, rec, rates, kl, states, horizon, stat, targets)
+        return
     out = []
     cache = {}
     for r in ctx.rows():
@@ -613,6 +645,45 @@ def cont_time_stats(args):
             raise SystemExit(f"invalid state transition stats {stat}")
         out.append("(" + d.join(list(key) + [repr(v)]) + ")")
     ctx.emit(out)
+
+
+def _cont_time_native(ctx, rec, rates, kl, states, horizon, stat, targets):
+    """contTimeStateTransitionStats over a native token table: the stats of every distinct key
+    once (key level), every record's value one gather, output through the native formatter."""
+    from ..models.markov import ContTimeStateTransitionStats
+    S = len(states)
+    n = rec.n_lines
+    kc = torch.stack([rec.field(j).long() for j in range(kl)], 1) if kl else torch.zeros((n, 0), dtype=torch.long)
+    uk, inv = torch.unique(kc, dim=0, return_inverse=True) if n else (torch.zeros((0, kl), dtype=torch.long),
+                                                                      torch.zeros(0, dtype=torch.long))
+    P = torch.zeros((uk.shape[0], S, S), dtype=torch.float64)
+    Dw = torch.zeros((uk.shape[0], S, S), dtype=torch.float64)
+    Q = torch.zeros((uk.shape[0], S, S), dtype=torch.float64)
+    for u, codes in enumerate(uk.tolist()):
+        key = tuple(rec.vocab[c] for c in codes)
+        if key not in rates:
+            raise SystemExit(f"contTimeStateTransitionStats: no rate matrix for key {key}")
+        cs = ContTimeStateTransitionStats(rates[key].to(ctx.device))
+        A, B = cs.sums([horizon])
+        P[u], Dw[u], Q[u] = A[0].cpu(), B[0].cpu(), cs.Q.cpu()
+    i0 = rec.map_codes(rec.field(kl), states).long().cpu()
+    if bool((i0 < 0).any()):
+        raise SystemExit("contTimeStateTransitionStats: unknown initial state")
+    inv = inv.cpu()
+    if stat == "futureStateProb":
+        end = rec.map_codes(rec.field(kl + 1), states).long().cpu()
+        if bool((end < 0).any()):
+            raise SystemExit("futureStateProb needs an end state")
+        v = P[inv, i0, end]
+    elif stat == "stateDwellTime":
+        v = Dw[inv, i0, states.index(targets[0])]
+    elif stat == "StateTransitionCount":
+        a, b = states.index(targets[0]), states.index(targets[1])
+        v = Dw[inv, i0, a] * Q[inv, a, b]
+    else:
+        raise SystemExit(f"invalid state transition stats {stat}")
+    spans, dl = rec.line_spans(), ctx.native_delim()
+    ctx.emit_columns([("g", "(")] + [spans.column("rf", j, dl) for j in range(kl)] + [("f", v, -2), ("g", ")")], n)
 
 
 # ================================================================================================
@@ -704,6 +775,22 @@ def event_time(args):
     to = ctx.get_int("time.field.ordinal")
     res = ctx.get_str("time.resolution", "hourOfDay")
     gr = ctx.get_int("hour.granularity", 1)
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({**{o: "d" for o in kords}, to: "n"}), tail_mode="x", numeric=True)
+    if rec is not None:
+        from ..data.records import sorted_key_tuples
+        kpos, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], ctx.comm)
+        t = rec.field(to, numeric=True).long()
+        if res == "hourOfDay":
+            b, B = (t % 86400_000) // 3600_000 // gr, (24 + gr - 1) // gr
+        else:
+            b, B = ((t // 86400_000) + 4) % 7, 7
+        H = torch.zeros(G * B, dtype=torch.long, device=rec.device).index_add_(0, kpos * B + b, torch.ones_like(b))
+        ctx.all_reduce(H)
+        d = ctx.delim_out
+        ctx.emit_root([d.join([rec.vocab[c] for c in k] + [f"{j}:{int(c)}" for j, c in enumerate(h) if c])
+                       for k, h in zip(ktab.tolist(), H.view(G, B).tolist())])
+        return
     rows = ctx.rows()
     keys = ctx.union(tuple(r[o] for o in kords) for r in rows)
     ki = {k: i for i, k in enumerate(keys)}

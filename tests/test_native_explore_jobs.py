@@ -70,7 +70,32 @@ def _setup(tmp: Path, name: str, regex: bool):
         conf.write_text(f'{block[0]} {{\n field.delim.in = "{dl}"\n {block[1]}}}\n')
         inp = num if name in ("lmap", "ipca") else data
         return [block[0], "-i", inp], conf
+    if name in ("ctime", "etd"):
+        rng = np.random.default_rng(12)
+        ev = tmp / "ev.txt"
+        ev.write_text("\n".join(f"u{int(rng.integers(0, 7))},{int(rng.integers(0, 40 * 86400_000))},"
+                                f"{rng.choice(['F', 'P', 'L'])},{rng.choice(['F', 'P', 'L'])}" for _ in range(800)) + "\n")
+        rates = tmp / "rates.txt"
+        rates.write_text("\n".join("(" + ",".join([f"u{k}"] + [f"{v:.6f}" for v in
+                                                              (np.eye(3) * -3 + 1 + 0.1 * k).reshape(-1)]) + ")"
+                                   for k in range(7)) + "\n")
+        if name == "ctime":
+            block = ("contTimeStateTransitionStats", f'key.field.len = 1\n state.values = ["F", "P", "L"]\n'
+                     f' time.horizon = 2\n state.trans.file.path = "{rates}"\n state.trans.stat = "StateTransitionCount"\n'
+                     f' target.states = ["P", "L"]\n')
+            inp = tmp / "ct.txt"
+            inp.write_text("\n".join(",".join([l.split(",")[0]] + l.split(",")[2:]) for l in ev.read_text().split()))
+        else:
+            block = ("eventTimeDistribution", "id.field.ordinals = [0]\n time.field.ordinal = 1\n"
+                     ' time.resolution = "dayOfWeek"\n')
+            inp = ev
+        conf = tmp / f"{name}_{tag}.conf"
+        conf.write_text(f'{block[0]} {{\n field.delim.in = "{dl}"\n {block[1]}}}\n')
+        return [block[0], "-i", inp], conf
     props = {
+        "spc": ("sequencePositionalCluster", "quant.field.ordinal=6\nseq.num.field.ordinal=5\nwindow.time.span=0.05\n"
+                "score.threshold=0.55\ncond.expression=$0 gt 0\n"),
+        "kmc": ("kmeansCluster", "kmc.attr.ordinals=5,6\nkmc.num.clusters=2,3\nkmc.max.iterations=20\n"),
         "nuc": ("numericalCorrelation", "nuc.attr.pairs=5:6,6:5\n"),
         "rue": ("ruleEvaluator", "rue.rule.names=r1,r2,r3\nrue.rule.r1=1 eq x > T\n"
                 "rue.rule.r2=1 in y:z and 3 eq p > F\nrue.rule.r3=5 gt 0.5 and 6 le 0 > T\nrue.class.attr.ord=4\n"),
@@ -89,7 +114,8 @@ def _setup(tmp: Path, name: str, regex: bool):
     return [job, "-i", data], cfg
 
 
-CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca"]
+CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca", "spc",
+         "kmc", "ctime", "etd"]
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -109,7 +135,7 @@ def _world(rank, world, argv, out, cfg):
     return True
 
 
-@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca"])
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd"])
 def test_world2_equals_world1(tmp_path, name):
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
