@@ -11,7 +11,7 @@ from pathlib import Path
 
 import torch
 
-from .common import JobContext, fmt, job
+from .common import JobContext, field_modes, fmt, job
 
 
 # ================================================================================================
@@ -64,6 +64,18 @@ def infrequent_marker(args):
     for r in ctx.rows(ctx.path("item.set.file.path", "model"), shard=False):
         if len(r) == 2 or ctx.get_int("item.set.length", 1) == 1:
             freq.add(r[0])
+    rec = ctx.try_records(modes="x" * skip, tail_mode="d")
+    if rec is not None:
+        # native: the item tokens stay dictionary codes; the marker substitution is one table over
+        # the dictionary, the output a CSR string list behind the raw leading fields
+        tab = [v if v in freq else marker for v in rec.vocab]
+        spans, dl = rec.line_spans(), ctx.native_delim()
+        idx, cnt = rec.padded(start=skip, dtype=torch.int32)
+        off = torch.cat([torch.zeros(1, dtype=torch.long, device=cnt.device), torch.cumsum(cnt, 0)])
+        flat = idx[torch.arange(idx.shape[1], device=idx.device).view(1, -1) < cnt.view(-1, 1)]
+        ctx.emit_columns([spans.column("rf", j, dl) for j in range(skip)]
+                         + [("l", tab, flat.cpu(), off.cpu())], rec.n_lines)
+        return
     d = ctx.delim_out
     ctx.emit([d.join(r[:skip] + [x if x in freq else marker for x in r[skip:]]) for r in ctx.rows()])
 
@@ -643,6 +655,32 @@ def data_partitioner(args):
     attr = int(pick[0])
     key = ",".join(pick[1:-1]) if len(pick) > 3 else pick[1]
     f = schema.find_field_by_ordinal(attr)
+    rec = ctx.try_records(modes=field_modes({attr: "d" if f.is_categorical else "n"}), tail_mode="x",
+                          numeric=not f.is_categorical)
+    if rec is not None:
+        # native: the split field tokenized once, segments from one lookup / bucketize, every
+        # segment's lines written from their raw bytes by the native formatter
+        if f.is_categorical:
+            groups = parse_split_key(key, "cat")
+            lut = {v: j for j, g in enumerate(groups) for v in g}
+            tab = torch.tensor([lut.get(v, len(groups) - 1) for v in rec.vocab] or [0], dtype=torch.long)
+            c = rec.field(attr).long().cpu()
+            seg = torch.where(c >= 0, tab[c.clamp_min(0)], torch.full_like(c, len(groups) - 1))
+        else:
+            pts = torch.tensor(parse_split_key(key, "num"), dtype=torch.float64)
+            seg = torch.bucketize(rec.field(attr, numeric=True).double().cpu(), pts, right=False)
+        spans = rec.line_spans()
+        base = Path(args.output) / f"split={attr}"
+        segs = torch.unique(seg).tolist()
+        for sv in segs:
+            p = base / f"segment={sv}"
+            p.mkdir(parents=True, exist_ok=True)
+            sel = spans.select(seg == sv)
+            from ..data.records import format_lines
+            format_lines([sel.column("r", delims=ctx.native_delim())], len(sel), ctx.delim_out,
+                         path=str(p / f"part-{ctx.comm.rank:05d}"))
+        ctx.report({"split": attr, "key": key, "segments": len(segs)})
+        return
     rows = ctx.rows()
     if f.is_categorical:
         groups = parse_split_key(key, "cat")

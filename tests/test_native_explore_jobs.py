@@ -92,6 +92,16 @@ def _setup(tmp: Path, name: str, regex: bool):
         conf = tmp / f"{name}_{tag}.conf"
         conf.write_text(f'{block[0]} {{\n field.delim.in = "{dl}"\n {block[1]}}}\n')
         return [block[0], "-i", inp], conf
+    if name == "iim":
+        items = tmp / "items.txt"
+        rng = np.random.default_rng(2)
+        items.write_text("\n".join(f"t{i}," + ",".join(rng.choice(list("abcdefgh"), int(rng.integers(1, 6))))
+                                   for i in range(500)) + "\n")
+        fi = tmp / "fi.txt"
+        fi.write_text("a,0.4\nc,0.3\ne,0.2\n")
+        cfg = tmp / f"iim_{tag}.properties"
+        cfg.write_text(f"iim.item.set.file.path={fi}\niim.skip.field.count=1\nfield.delim.regex={dl}\n")
+        return ["infrequentItemMarker", "-i", items], cfg
     props = {
         "spc": ("sequencePositionalCluster", "quant.field.ordinal=6\nseq.num.field.ordinal=5\nwindow.time.span=0.05\n"
                 "score.threshold=0.55\ncond.expression=$0 gt 0\n"),
@@ -115,7 +125,7 @@ def _setup(tmp: Path, name: str, regex: bool):
 
 
 CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca", "spc",
-         "kmc", "ctime", "etd"]
+         "kmc", "ctime", "etd", "iim"]
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -135,7 +145,7 @@ def _world(rank, world, argv, out, cfg):
     return True
 
 
-@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd"])
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim"])
 def test_world2_equals_world1(tmp_path, name):
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
