@@ -3158,6 +3158,148 @@ py::tuple pack_spans(const at::Tensor& addr_in, const at::Tensor& len_in, int nt
   return py::make_tuple(bytes.narrow(0, 0, o[n]), off);
 }
 
+// smote_lines: the synthetic records of classBasedOverSampler (SMOTE) assembled natively from the
+// source lines (byte spans), the K25 kernel's outputs and the field kinds of one record block:
+// kind 0 copy the source field (class / non-feature), 1 id (the source id and the picked
+// neighbour's id scrambled, truncated to the source id's length), 2 integer feature (the kernel's
+// value truncated), 3 double feature (fixed, prec digits), 4 categorical feature (source or
+// neighbour field by the kernel's coin).  The scramble is a Fisher-Yates shuffle driven by a
+// splitmix64 stream keyed by (seed * 1000003 + global line) * 131 + copy (jobs/core.py mirrors it).
+namespace {
+inline uint64_t smx_next(uint64_t& x) {
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+}  // namespace
+
+py::tuple smote_lines(const at::Tensor& addr_in, const at::Tensor& len_in, int64_t L, const at::Tensor& kinds_in,
+                      const at::Tensor& numcol_in, const at::Tensor& newx_in, const at::Tensor& coin_in,
+                      const at::Tensor& pick_in, const at::Tensor& gidx_in, int64_t mult, int64_t seed, int64_t prec,
+                      const std::string& sep_in, const std::string& delim, int nthreads) {
+  auto addr = addr_in.to(at::kCPU).to(at::kLong).contiguous();
+  auto len = len_in.to(at::kCPU).to(at::kLong).contiguous();
+  auto kinds = kinds_in.to(at::kCPU).to(at::kInt).contiguous();
+  auto numcol = numcol_in.to(at::kCPU).to(at::kInt).contiguous();
+  auto newx = newx_in.to(at::kCPU).to(at::kFloat).contiguous();
+  auto coin = coin_in.to(at::kCPU).to(at::kInt).contiguous();
+  auto pick = pick_in.to(at::kCPU).to(at::kLong).contiguous();
+  auto gidx = gidx_in.to(at::kCPU).to(at::kLong).contiguous();
+  const int64_t n = addr.numel();
+  TORCH_CHECK(len.numel() == n && gidx.numel() == n, "smote_lines: one span and global index per line");
+  TORCH_CHECK(kinds.numel() == L && numcol.numel() == L && L >= 1, "smote_lines: kinds / numcol are [L]");
+  TORCH_CHECK(mult >= 0 && coin.numel() == n * mult && pick.numel() == n * mult, "smote_lines: [n * mult] draws");
+  const int64_t C = newx.dim() == 2 ? newx.size(1) : 0;
+  TORCH_CHECK(newx.dim() == 2 && newx.size(0) == n * mult, "smote_lines: newx [n * mult, C]");
+  TORCH_CHECK(sep_in.size() == 1, "smote_lines: one-character input delimiter");
+  const char sep = sep_in[0];
+  const int32_t* kd = kinds.data_ptr<int32_t>();
+  const int32_t* nc = numcol.data_ptr<int32_t>();
+  for (int64_t i = 0; i < L; ++i)
+    TORCH_CHECK(kd[i] >= 0 && kd[i] <= 4 && nc[i] < C && ((kd[i] != 2 && kd[i] != 3) || nc[i] >= 0),
+                "smote_lines: bad field kind / numeric column");
+  const int64_t* a = addr.data_ptr<int64_t>();
+  const int64_t* l = len.data_ptr<int64_t>();
+  const float* X = newx.data_ptr<float>();
+  const int32_t* cn = coin.data_ptr<int32_t>();
+  const int64_t* pk = pick.data_ptr<int64_t>();
+  const int64_t* gi = gidx.data_ptr<int64_t>();
+  const int T = n < 4096 ? 1 : std::max(1, std::min(nthreads, 64));
+  std::vector<std::string> parts((size_t)T);
+  std::vector<std::vector<int64_t>> lens((size_t)T);
+  {
+    py::gil_scoped_release rel;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        std::string& out = parts[(size_t)t];
+        std::vector<int64_t>& ol = lens[(size_t)t];
+        std::vector<std::pair<const char*, const char*>> fs;
+        std::string idb;
+        char num[64];
+        for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+          // field byte ranges of the source line
+          fs.clear();
+          const char* p = reinterpret_cast<const char*>(a[r]);
+          const char* e = p + l[r];
+          while (true) {
+            const char* q = static_cast<const char*>(std::memchr(p, sep, (size_t)(e - p)));
+            if (!q) q = e;
+            fs.emplace_back(p, q);
+            if (q >= e) break;
+            p = q + 1;
+          }
+          const int64_t F = (int64_t)fs.size();
+          for (int64_t j = 0; j < mult; ++j) {
+            const int64_t o = r * mult + j;
+            const int64_t pj = std::max<int64_t>(pk[o], 0);
+            const size_t start = out.size();
+            for (int64_t i = 0; i < L; ++i) {
+              if (i) out += delim;
+              const auto src = i < F ? fs[(size_t)i] : std::make_pair(e, e);
+              const int64_t ni = L + pj * L + i;
+              const auto nbr = ni < F ? fs[(size_t)ni] : std::make_pair(e, e);
+              switch (kd[i]) {
+                case 1: {
+                  idb.assign(src.first, src.second);
+                  idb.append(nbr.first, nbr.second);
+                  uint64_t x = ((uint64_t)seed * 1000003ull + (uint64_t)gi[r]) * 131ull + (uint64_t)j;
+                  for (int64_t k = (int64_t)idb.size() - 1; k > 0; --k) {
+                    const uint64_t z = smx_next(x) % (uint64_t)(k + 1);
+                    std::swap(idb[(size_t)k], idb[(size_t)z]);
+                  }
+                  out.append(idb.data(), (size_t)(src.second - src.first));
+                  break;
+                }
+                case 2: {
+                  const double v = (double)X[o * C + nc[i]];
+                  const int k = std::snprintf(num, sizeof num, "%lld", (long long)std::trunc(v));
+                  out.append(num, (size_t)k);
+                  break;
+                }
+                case 3: {
+                  const double v = (double)X[o * C + nc[i]];
+                  const int k = std::snprintf(num, sizeof num, "%.*f", (int)prec, v);
+                  out.append(num, (size_t)std::min<int>(k, (int)sizeof num - 1));
+                  break;
+                }
+                case 4: {
+                  const auto& f = cn[o] == 0 ? src : nbr;
+                  out.append(f.first, f.second);
+                  break;
+                }
+                default:
+                  out.append(src.first, src.second);
+              }
+            }
+            ol.push_back((int64_t)(out.size() - start));
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  int64_t tot = 0;
+  for (auto& s2 : parts) tot += (int64_t)s2.size();
+  auto bytes = at::empty({std::max<int64_t>(tot, 1)}, at::kByte);
+  auto off = at::empty({n * mult + 1}, at::kLong);
+  uint8_t* dst = bytes.data_ptr<uint8_t>();
+  int64_t* of = off.data_ptr<int64_t>();
+  int64_t at_b = 0, k = 0;
+  of[0] = 0;
+  for (int t = 0; t < T; ++t) {
+    std::memcpy(dst + at_b, parts[(size_t)t].data(), parts[(size_t)t].size());
+    at_b += (int64_t)parts[(size_t)t].size();
+    int64_t acc = of[k];
+    for (int64_t v : lens[(size_t)t]) {
+      acc += v;
+      of[++k] = acc;
+    }
+  }
+  return py::make_tuple(bytes.narrow(0, 0, tot), off);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K27 LSTM recurrence.  Fragments are packed by avenir_amd/ops/rnn.py (pack_weights): wfrag holds
 // [NW, 4, KS+IS, 64, 8] bf16 (forward, [W_hh | W_ih]), wfragT [NW, 4KS, 64, 8] bf16 (backward,
@@ -3399,6 +3541,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bandit_select", &bandit_select);
   m.def("sample", &sample);
   m.def("sa_assign", &sa_assign);
+  m.def("smote_lines", &smote_lines);
   m.def("mixed_knn_max_dims", []() { return avk::mixed_knn_max_dims(); });
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);

@@ -382,7 +382,6 @@ def _smote_from_neighbors(ctx: JobContext) -> None:
     neighbour pick uniform / exponential, gap, categorical coin), so the output does not depend on
     the world size; the id field shuffles the two ids' characters with a generator seeded by the
     same key."""
-    import random
     from ..ops import resample_ops as RS
     L = ctx.get_int("rec.len")
     mult = ctx.get_int("over.sampling.multiplier")
@@ -390,6 +389,10 @@ def _smote_from_neighbors(ctx: JobContext) -> None:
     prec = ctx.get_int("output.precision", 3)
     schema = ctx.schema("feature.schema.file.path")
     seed = ctx.get_int("random.seed", 0)
+    rec = ctx.try_records(tail_mode="n", numeric=True)
+    if rec is not None:
+        _smote_native(ctx, rec, L, mult, distr, prec, schema, seed)
+        return
     all_rows = ctx.rows()
     base = ctx.line_base(len(all_rows))
     keep_i = [i for i, r in enumerate(all_rows) if len(r) >= 2 * L]
@@ -440,9 +443,7 @@ def _smote_from_neighbors(ctx: JobContext) -> None:
                 if f is None:
                     continue
                 if f.id:
-                    s = list(r[i] + nrec[i])
-                    random.Random((seed * 1000003 + int(gidx[a])) * 131 + j).shuffle(s)
-                    rec[i] = "".join(s)[: len(r[i])]
+                    rec[i] = _scramble(r[i] + nrec[i], (seed * 1000003 + int(gidx[a])) * 131 + j)[: len(r[i])]
                 elif f.feature and f.is_categorical:
                     rec[i] = r[i] if int(newC[o, 0]) == 0 else nrec[i]
             for c, i in enumerate(num_cols):
@@ -450,6 +451,92 @@ def _smote_from_neighbors(ctx: JobContext) -> None:
                 rec[i] = str(int(v)) if fields[i].is_integer else f"{v:.{prec}f}"
             outs.append(d.join(rec))
     ctx.emit(outs)
+
+
+_M64 = (1 << 64) - 1
+
+
+def _scramble(s: str, key: int) -> str:
+    """The id scramble of ``smote_lines`` (bindings.cpp): Fisher-Yates over the bytes driven by a
+    splitmix64 stream seeded with ``key`` (mod 2^64)."""
+    b = bytearray(s.encode())
+    x = key & _M64
+    for k in range(len(b) - 1, 0, -1):
+        x = (x + 0x9E3779B97F4A7C15) & _M64
+        z = x
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+        z ^= z >> 31
+        r = z % (k + 1)
+        b[k], b[r] = b[r], b[k]
+    return b.decode(errors="replace")
+
+
+def _smote_native(ctx, rec, L, mult, distr, prec, schema, seed):
+    """classBasedOverSampler on a native token table (every field parsed as a number): source and
+    neighbour feature values are gathers from the token array, the K25 kernel draws the synthetic
+    values, and ``smote_lines`` assembles the output records from the raw line bytes."""
+    from .. import _native
+    from ..data.lines import LineSpans
+    from ..ops import resample_ops as RS
+    dev = ctx.device
+    lens = rec.lens()
+    keep = lens >= 2 * L
+    ki = torch.nonzero(keep).view(-1)
+    n = int(ki.numel())
+    if n == 0:
+        ctx.emit([])
+        return
+    fields = {f.ordinal: f for f in schema.fields}
+    num_cols = [i for i in range(L) if i in fields and fields[i].feature and fields[i].is_numeric]
+    kinds = []
+    for i in range(L):
+        f = fields.get(i)
+        if f is None or not (f.id or f.feature):
+            kinds.append(0)
+        elif f.id:
+            kinds.append(1)
+        elif i in num_cols:
+            kinds.append(2 if f.is_integer else 3)
+        elif f.is_categorical:
+            kinds.append(4)
+        else:
+            kinds.append(0)
+    base = rec.off[:-1][ki]
+    nnb = ((lens[ki] - L) // L).to(torch.int32)
+    M = int(nnb.max())
+    nums = rec.nums
+    cols = torch.tensor(num_cols, dtype=torch.long, device=base.device)
+    src = nums[base.view(-1, 1) + cols.view(1, -1)].float()
+    mm = torch.arange(M, device=base.device)
+    pos = base.view(-1, 1, 1) + L + (mm * L).view(1, -1, 1) + cols.view(1, 1, -1)
+    valid = (mm.view(1, -1) < nnb.view(-1, 1).long()).unsqueeze(2)
+    nb = torch.where(valid, nums[torch.where(valid, pos, base.view(-1, 1, 1))].float(), torch.zeros((), device=base.device))
+    Cs = torch.zeros((n, 1), dtype=torch.int32, device=base.device)
+    Cn = torch.ones((n, M, 1), dtype=torch.int32, device=base.device)
+    gidx = (rec.line_base + ki).long().cpu()
+    # the kernel keys draws by (gbase + r) * mult + j with contiguous r: one launch per run of
+    # consecutive kept lines
+    brk = torch.nonzero(gidx[1:] != gidx[:-1] + 1).view(-1) + 1
+    bounds = [0] + brk.tolist() + [n]
+    newX, newC, pick = [], [], []
+    for a0, a1 in zip(bounds[:-1], bounds[1:]):
+        x, c, pk = RS.smote_rows(src[a0:a1].to(dev), nb[a0:a1].to(dev), nnb[a0:a1].to(dev), Cs[a0:a1].to(dev),
+                                 Cn[a0:a1].to(dev), mult, int(gidx[a0]), seed, distr == "exponential",
+                                 ctx.get_float("exp.distr.mean", 1.0))
+        newX.append(x.cpu())
+        newC.append(c.cpu())
+        pick.append(pk.cpu())
+    newX, newC, pick = torch.cat(newX), torch.cat(newC), torch.cat(pick)
+    spans = rec.line_spans().select(ki.cpu())
+    _, addr, ln = spans.spans()
+    numcol = [num_cols.index(i) if i in num_cols else -1 for i in range(L)]
+    buf, off = _native.C().smote_lines(addr, ln, L, torch.tensor(kinds, dtype=torch.int32),
+                                       torch.tensor(numcol, dtype=torch.int32), newX.float(),
+                                       newC[:, 0].int().contiguous(), pick.long(), gidx, mult, seed, prec,
+                                       ctx.native_delim(), ctx.delim_out, 16)
+    out = LineSpans.from_packed(buf, off)
+    ctx.emit_columns([out.column("r")], len(out))
 
 
 @job("kolmogorovSmirnovModelDrift", "KS drift between reference and current distributions (S/explore/KolmogorovSmirnovModelDrift.scala)")

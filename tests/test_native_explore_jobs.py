@@ -92,6 +92,30 @@ def _setup(tmp: Path, name: str, regex: bool):
         conf = tmp / f"{name}_{tag}.conf"
         conf.write_text(f'{block[0]} {{\n field.delim.in = "{dl}"\n {block[1]}}}\n')
         return [block[0], "-i", inp], conf
+    if name in ("smote", "smote_exp"):
+        import json
+        rng = np.random.default_rng(21)
+        recs = [[f"id{i:04d}", f"{rng.random():.4f}", str(int(rng.integers(0, 50))), str(rng.choice(["u", "v", "w"])), "1"]
+                for i in range(300)]
+        lines = []
+        for i in range(300):
+            nbrs = rng.choice(300, int(rng.integers(1, 5)), replace=False)
+            lines.append(",".join(recs[i] + [x for j in nbrs for x in recs[j]]))
+        lines.append("short,1,2")                      # fewer than two records: skipped
+        inp = tmp / "nb.txt"
+        inp.write_text("\n".join(lines) + "\n")
+        sch = tmp / "sm.json"
+        sch.write_text(json.dumps({"fields": [
+            {"name": "id", "ordinal": 0, "id": True, "dataType": "string"},
+            {"name": "x", "ordinal": 1, "dataType": "double", "feature": True},
+            {"name": "k", "ordinal": 2, "dataType": "int", "feature": True},
+            {"name": "c", "ordinal": 3, "dataType": "categorical", "feature": True, "cardinality": ["u", "v", "w"]},
+            {"name": "cls", "ordinal": 4, "dataType": "categorical", "cardinality": ["0", "1"]}]}))
+        cfg = tmp / f"{name}_{tag}.properties"
+        cfg.write_text(f"cbos.rec.len=5\ncbos.over.sampling.multiplier=3\ncbos.feature.schema.file.path={sch}\n"
+                       f"cbos.neighbor.sampling.distr={'exponential' if name == 'smote_exp' else 'uniform'}\n"
+                       f"cbos.random.seed=7\nfield.delim.regex={dl}\n")
+        return ["classBasedOverSampler", "-i", inp], cfg
     if name == "iim":
         items = tmp / "items.txt"
         rng = np.random.default_rng(2)
@@ -125,7 +149,7 @@ def _setup(tmp: Path, name: str, regex: bool):
 
 
 CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca", "spc",
-         "kmc", "ctime", "etd", "iim"]
+         "kmc", "ctime", "etd", "iim", "smote", "smote_exp"]
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -145,7 +169,7 @@ def _world(rank, world, argv, out, cfg):
     return True
 
 
-@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim"])
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote"])
 def test_world2_equals_world1(tmp_path, name):
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
