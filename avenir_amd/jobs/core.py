@@ -13,6 +13,7 @@ from pathlib import Path
 
 import torch
 
+from .. import _native
 from .common import JobContext, job
 
 
@@ -711,6 +712,16 @@ def gen_data(args):
 def wc(args):
     from collections import Counter
     ctx = JobContext(args)
+    if _native.host() is not None:
+        # native: whitespace tokens of this rank's byte range as dictionary codes (merged over ranks,
+        # so the count vector is global after one all-reduce); only distinct words reach Python
+        rec = ctx.records(delims=" \t\r\v\f", tail_mode="d")
+        V = len(rec.vocab)
+        cnt = torch.bincount(rec.codes[rec.codes >= 0].long(), minlength=V)[:V] if V else torch.zeros(0, dtype=torch.long)
+        ctx.all_reduce(cnt)
+        ch = cnt.cpu().tolist()
+        ctx.emit_root([f"{w},{ch[i]}" for w, i in sorted((w, i) for i, w in enumerate(rec.vocab) if w and ch[i])])
+        return
     c = ctx.sum_counts(Counter(w for l in ctx.lines() for w in l.split()))
     ctx.emit_root([f"{w},{n}" for w, n in sorted(c.items())])
 

@@ -175,3 +175,23 @@ def test_world2_equals_world1(tmp_path, name):
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
     run_world(_world, 2, [str(a) for a in argv], str(tmp_path / "w2"), str(cfg), timeout=300)
     assert _lines(tmp_path / "w2") == _lines(tmp_path / "w1")
+
+
+def test_word_count_native_equals_counter(tmp_path):
+    from collections import Counter
+    rng = np.random.default_rng(5)
+    words = ["alpha", "beta", "gamma", "delta", "Zeta", "éta"]
+    text = "\n".join(" ".join(rng.choice(words, int(rng.integers(0, 9)))) + ("\t  x" if i % 7 == 0 else "")
+                     for i in range(2000)) + "\n"
+    inp = tmp_path / "t.txt"
+    inp.write_text(text)
+    ref = [f"{w},{n}" for w, n in sorted(Counter(w for l in text.splitlines() for w in l.split()).items())]
+    assert main(["wordCount", "-i", str(inp), "-o", str(tmp_path / "w1"), "--device", "cpu"]) == 0
+    assert _lines(tmp_path / "w1") == ref
+    run_world(_world_wc, 2, str(inp), str(tmp_path / "w2"), timeout=300)
+    assert _lines(tmp_path / "w2") == ref
+
+
+def _world_wc(rank, world, inp, out):
+    assert main(["wordCount", "-i", inp, "-o", out, "--device", "cpu"]) == 0
+    return True
