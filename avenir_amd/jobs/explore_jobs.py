@@ -187,6 +187,9 @@ def relief_job(args):
     attrs = ctx.get_int_list("attr.ordinals", None)
     schema = _schema_or_none(ctx, "attr.schema.file.path")
     d = ctx.delim_out
+    if ctx.has("neighborhood.file.path") and ctx.native_delim() is not None:
+        _relief_pairs_native(ctx, attrs, schema)
+        return
     if ctx.has("neighborhood.file.path"):
         id_ord = ctx.get_int("id.ord")
         recs = {r[id_ord]: r for r in ctx.rows(shard=False)}
@@ -221,6 +224,58 @@ def relief_job(args):
     s = relief(X, t.labels[: t.n].long(), ctx.get_int("neighbor.count", 1))
     keep = attrs or ords
     ctx.emit_root([f"{o}{d}{fmt(float(s[ords.index(o)]))}" for o in keep if o in ords])
+
+
+def _relief_pairs_native(ctx, attrs, schema):
+    """reliefFeatureRelevance (MR form) on token tables: the records (every rank reads them whole:
+    the join side) with the id as a dictionary code and the attributes as numbers / codes, the
+    neighbourhood file as this rank's byte range of dictionary tokens; pairs join the records by
+    code (one dictionary-level map between the two files), every attribute's signed differences are
+    one masked reduction, one all-reduce."""
+    from .common import field_modes
+    id_ord = ctx.get_int("id.ord")
+    cat = {o for o in attrs if schema is not None and schema.find_field_by_ordinal(o) is not None
+           and schema.find_field_by_ordinal(o).is_categorical}
+    recs = ctx.records(shard=False, modes=field_modes({id_ord: "d", **{o: ("d" if o in cat else "n") for o in attrs}}),
+                       tail_mode="x", numeric=True)
+    V = len(recs.vocab)
+    idc = recs.field(id_ord).long()
+    row_of = torch.full((max(V, 1),), -1, dtype=torch.long, device=recs.device)
+    if recs.n_lines:
+        row_of.scatter_reduce_(0, idc.clamp_min(0), torch.arange(recs.n_lines, device=recs.device), "amax")
+    nb = ctx.records(ctx.path("neighborhood.file.path"), tail_mode="d")
+    vi = {v: i for i, v in enumerate(recs.vocab)}
+    lut = torch.tensor([vi.get(v, -1) for v in nb.vocab] or [-1], dtype=torch.long, device=nb.device)
+    pad, cnt = nb.padded(dtype=torch.long)
+    dev = recs.device
+    score = torch.zeros(len(attrs), dtype=torch.float64, device=dev)
+    npairs = torch.zeros(1, dtype=torch.float64, device=dev)
+    if pad.shape[0] and pad.shape[1] > 3:
+        src, hit = pad[:, 0], pad[:, 1] == pad[:, 2]
+        trg = pad[:, 3:]
+        tv = torch.arange(trg.shape[1], device=pad.device).view(1, -1) < (cnt.view(-1, 1) - 3)
+        def to_row(c):
+            k = torch.where(c >= 0, lut[c.clamp_min(0)], torch.full_like(c, -1))
+            return torch.where(k >= 0, row_of[k.clamp_min(0)], torch.full_like(k, -1))
+        rs = to_row(src).view(-1, 1).expand_as(trg)
+        rt = to_row(trg)
+        ok = tv & (rs >= 0) & (rt >= 0)
+        rs, rt = rs[ok].to(dev), rt[ok].to(dev)
+        sign = torch.where(hit.view(-1, 1).expand_as(trg)[ok], -1.0, 1.0).double().to(dev)
+        npairs[0] = float(rs.numel())
+        for j, o in enumerate(attrs):
+            f = schema.find_field_by_ordinal(o) if schema else None
+            if o in cat:
+                c = recs.field(o)
+                diff = (c[rs] != c[rt]).double()
+            else:
+                rng = (f.max - f.min) if f is not None and f.max is not None and f.min is not None else 1.0
+                x = recs.field(o, numeric=True).double()
+                diff = (x[rs] - x[rt]).abs() / rng
+            score[j] = (diff * sign).sum()
+    ctx.all_reduce(score, npairs)
+    d = ctx.delim_out
+    ctx.emit_root([f"{o}{d}{fmt(float(score[j]) / max(float(npairs), 1))}" for j, o in enumerate(attrs)])
 
 
 @job("topMatchesByClass", "same-class nearest neighbours from pair distances (J/explore/TopMatchesByClass.java, tmc.*)")
@@ -431,8 +486,12 @@ def bagging(args):
     with one object all-gather of the requests and one of the answers."""
     from ..models.sampling import bagging_indices
     ctx = JobContext(args, "bas.")
-    lines = ctx.lines()
     comm = ctx.comm
+    rec = ctx.try_records(tail_mode="x")
+    if rec is not None:
+        _bagging_native(ctx, rec, bagging_indices)
+        return
+    lines = ctx.lines()
     sizes = comm.all_gather_object(len(lines)) if comm.is_distributed else [len(lines)]
     base, total = sum(sizes[: comm.rank]), sum(sizes)
     idx = bagging_indices(len(lines), ctx.get_int("batch.size", 10000), seed=ctx.get_int("random.seed", 0),
@@ -445,6 +504,44 @@ def bagging(args):
         for part in comm.all_gather_object(mine):
             got.update(part)
     ctx.emit([lines[i - base] if base <= i < base + len(lines) else got[i] for i in idx])
+
+
+def _bagging_native(ctx, rec, bagging_indices):
+    """baggingSampler on byte spans: picks this rank holds are span selections; picks of records
+    other ranks hold travel as one packed byte payload (all-gathered requests, each owner packs
+    the requested lines natively, one all-gather of the payloads)."""
+    from ..data.lines import LineSpans
+    comm = ctx.comm
+    spans = rec.line_spans()
+    n = len(spans)
+    sizes = comm.all_gather_object(n) if comm.is_distributed else [n]
+    base, total = sum(sizes[: comm.rank]), sum(sizes)
+    idx = bagging_indices(n, ctx.get_int("batch.size", 10000), seed=ctx.get_int("random.seed", 0), base=base,
+                          total=total).long()
+    local = (idx >= base) & (idx < base + n)
+    _, addr, ln = spans.spans()
+    out_a = torch.zeros(idx.numel(), dtype=torch.int64)
+    out_l = torch.zeros(idx.numel(), dtype=torch.int64)
+    li = (idx - base).clamp(0, max(n - 1, 0))
+    if n:
+        out_a[local], out_l[local] = addr[li[local]], ln[li[local]]
+    owners = [spans]
+    if comm.is_distributed:
+        req = torch.unique(comm.all_gather_v(torch.unique(idx[~local])))
+        mine = req[(req >= base) & (req < base + n)]
+        buf, off = spans.select(mine - base).pack()
+        g_idx = comm.all_gather_v(mine)
+        g_len = comm.all_gather_v(off[1:] - off[:-1])
+        g_buf = comm.all_gather_v(buf)
+        got = LineSpans.from_packed(g_buf, torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(g_len, 0)]))
+        owners.append(got)
+        rem = ~local
+        if bool(rem.any()):
+            j = torch.searchsorted(g_idx, idx[rem])
+            _, ga, gl = got.spans()
+            out_a[rem], out_l[rem] = ga[j], gl[j]
+    res = LineSpans(owners, out_a, out_l)
+    ctx.emit_columns([res.column("r", delims=ctx.native_delim())], len(res))
 
 
 @job("adaBoostError", "weighted misclassification error (J/explore/AdaBoostError.java, abe.*)")

@@ -116,6 +116,29 @@ def _setup(tmp: Path, name: str, regex: bool):
                        f"cbos.neighbor.sampling.distr={'exponential' if name == 'smote_exp' else 'uniform'}\n"
                        f"cbos.random.seed=7\nfield.delim.regex={dl}\n")
         return ["classBasedOverSampler", "-i", inp], cfg
+    if name == "relief":
+        import json
+        rng = np.random.default_rng(31)
+        recs = tmp / "recs.txt"
+        recs.write_text("\n".join(f"e{i},{rng.choice(['a', 'b'])},{rng.random():.3f},{rng.choice(['u', 'v'])}"
+                                   for i in range(200)) + "\n")
+        nbh = tmp / "nbh.txt"
+        nbh.write_text("\n".join(",".join([f"e{i}", str(rng.choice(['a', 'b'])), str(rng.choice(['a', 'b']))]
+                                          + [f"e{int(j)}" for j in rng.choice(210, 4)]) for i in range(200)) + "\n")
+        sch = tmp / "rl.json"
+        sch.write_text(json.dumps({"fields": [
+            {"name": "id", "ordinal": 0, "id": True, "dataType": "string"},
+            {"name": "c", "ordinal": 1, "dataType": "categorical", "feature": True, "cardinality": ["a", "b"]},
+            {"name": "x", "ordinal": 2, "dataType": "double", "feature": True, "min": 0, "max": 1},
+            {"name": "k", "ordinal": 3, "dataType": "categorical", "feature": True, "cardinality": ["u", "v"]}]}))
+        cfg = tmp / f"relief_{tag}.properties"
+        cfg.write_text(f"ffr.neighborhood.file.path={nbh}\nffr.id.ord=0\nffr.attr.ordinals=1,2,3\n"
+                       f"ffr.attr.schema.file.path={sch}\nfield.delim.regex={dl}\n")
+        return ["reliefFeatureRelevance", "-i", recs], cfg
+    if name == "bag":
+        cfg = tmp / f"bag_{tag}.properties"
+        cfg.write_text(f"bas.batch.size=64\nbas.random.seed=4\nfield.delim.regex={dl}\n")
+        return ["baggingSampler", "-i", data], cfg
     if name == "iim":
         items = tmp / "items.txt"
         rng = np.random.default_rng(2)
@@ -149,7 +172,7 @@ def _setup(tmp: Path, name: str, regex: bool):
 
 
 CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca", "spc",
-         "kmc", "ctime", "etd", "iim", "smote", "smote_exp"]
+         "kmc", "ctime", "etd", "iim", "smote", "smote_exp", "relief", "bag"]
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -169,7 +192,7 @@ def _world(rank, world, argv, out, cfg):
     return True
 
 
-@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote"])
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote", "relief", "bag"])
 def test_world2_equals_world1(tmp_path, name):
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
