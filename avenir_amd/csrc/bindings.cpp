@@ -2827,8 +2827,9 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
                                 int64_t max_initial_slots, const std::string& last_mode) {
   CHECK_DEV(like);
   TORCH_CHECK(max_initial_slots >= 1024, "max_initial_slots >= 1024");
-  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && modes.size() <= 64 && last_mode.size() <= 1,
-              "bad tokenizer options");
+  TORCH_CHECK(sub_delim.size() <= 1 && tail_mode.size() == 1 && last_mode.size() <= 1, "bad tokenizer options");
+  // the kernel argument block holds 64 per-field modes: wider mode strings take the host tokenizer
+  if (modes.size() > 64) return py::none();
   for (char c : modes + tail_mode + last_mode) TORCH_CHECK(c == 'd' || c == 'n' || c == 'x', "token modes are d / n / x");
   const std::string delims = delims_in.empty() ? std::string(",") : delims_in;
   const char sd = sub_delim.empty() ? 0 : sub_delim[0];

@@ -84,7 +84,29 @@ def setup(job: str, d: str, n: int, dev: str):
                      "mop.rec.class.attr.ordinal=6\n")
         _run(["randomForest", "-i", data, "-o", forest, "-c", cfg, "--device", dev])
         return ["modelPredictor", "-i", data, "-c", cfg], data
+    if job == "usb":
+        return ["underSamplingBalancer", "-i", data, "-c", _props(d, "usb.properties", "usb.class.attr.ord=6\n")], data
+    if job in ("hash", "dummy"):
+        block = ("categoricalFeatureHashingEncoding { cat.fieldOrdinals = [1,2,3]\n encoding.size = 8 }\n"
+                 if job == "hash" else "binaryDummyVariableGenerator { cat.field.ordinals = [1,4] }\n")
+        return [block.split()[0], "-i", data, "-c", _props(d, f"{job}.conf", block)], data
     raise SystemExit(f"unknown job {job}")
+
+
+def setup_rs(d: str, n: int):
+    """recordSimilarity on ``n`` records x 8 uniform dims: the all-pairs ring
+    with a distance threshold that keeps ~1e-4 of the pairs."""
+    import numpy as np
+    data = os.path.join(d, f"rs_{n}.csv")
+    rng = np.random.default_rng(3)
+    X = rng.random((n, 8))
+    with open(data, "w") as fh:
+        for i in range(0, n, 65536):
+            blk = X[i:i + 65536]
+            fh.write("\n".join(f"r{i + j}," + ",".join(f"{v:.5f}" for v in row) for j, row in enumerate(blk)) + "\n")
+    cfg = _props(d, "rs.properties", "resi.attr.ordinals=1,2,3,4,5,6,7,8\nresi.id.ordinal=0\n"
+                                     "resi.distance.scale=1000\nresi.dist.threshold=100\n")
+    return ["recordSimilarity", "-i", data, "-c", cfg], data
 
 
 def main() -> int:
@@ -92,12 +114,14 @@ def main() -> int:
     ap.add_argument("--records", type=int, default=1 << 24)
     ap.add_argument("--jobs", default="vit,mmc,pst,nbp,detr,mop")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--rs-records", type=int, default=1 << 17)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     d = tempfile.mkdtemp(prefix="avmi_pred_")
     for job in args.jobs.split(","):
-        argv, data = setup(job, d, args.records, dev)
+        n_rec = args.rs_records if job == "rs" else args.records
+        argv, data = setup_rs(d, n_rec) if job == "rs" else setup(job, d, args.records, dev)
         out = os.path.join(d, f"{job}.out")
         best = None
         for _ in range(args.reps):
@@ -109,11 +133,16 @@ def main() -> int:
                 torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
-        with open(out if os.path.isfile(out) else os.path.join(out, "part-00000"), "rb") as fh:
-            n_out = sum(1 for _ in fh)
-        rec = {"bench": "predict_job", "job": argv[0], "records": args.records, "device": dev,
-               "bytes": os.path.getsize(data), "seconds": round(best, 4), "records_per_s": args.records / best,
+        files = [out] if os.path.isfile(out) else [os.path.join(out, f) for f in sorted(os.listdir(out))]
+        n_out = 0
+        for fn in files:
+            with open(fn, "rb") as fh:
+                n_out += sum(1 for _ in fh)
+        rec = {"bench": "predict_job", "job": argv[0], "records": n_rec, "device": dev,
+               "bytes": os.path.getsize(data), "seconds": round(best, 4), "records_per_s": n_rec / best,
                "output_lines": n_out}
+        if job == "rs":
+            rec["pairs_per_s"] = n_rec * (n_rec - 1) / 2 / best
         print(json.dumps(rec), flush=True)
         if args.out:
             with open(args.out, "a") as fh:
