@@ -20,15 +20,36 @@ namespace avh {
 
 namespace {
 
+// Output cursor over a growable buffer: every row first reserves an upper bound of its bytes
+// (``ensure``), then the writers copy with plain pointer arithmetic — no per-append capacity check.
+struct Out {
+  std::string buf;
+  size_t pos = 0;
+  char* w = nullptr;
+  void ensure(size_t k) {
+    if (buf.size() - pos < k) {
+      buf.resize(std::max(buf.size() * 2, pos + k + (1u << 16)));
+    }
+    w = buf.data() + pos;
+  }
+  void commit() { pos = (size_t)(w - buf.data()); }
+  void put(const char* p, size_t n) {
+    std::memcpy(w, p, n);
+    w += n;
+  }
+  void put(char c) { *w++ = c; }
+};
+
 // Python's repr(float): the shortest digit string that round-trips (std::to_chars), written in
-// fixed notation for decimal exponents -4 <= e < 16 and as d.ddde[+-]XX otherwise.
-inline void put_pyrepr(std::string& s, double v) {
+// fixed notation for decimal exponents -4 <= e < 16 and as d.ddde[+-]XX otherwise.  <= 32 bytes.
+inline void put_pyrepr(Out& o, double v) {
   if (std::isnan(v)) {
-    s += "nan";
+    o.put("nan", 3);
     return;
   }
   if (std::isinf(v)) {
-    s += v < 0 ? "-inf" : "inf";
+    if (v < 0) o.put("-inf", 4);
+    else o.put("inf", 3);
     return;
   }
   char buf[40];
@@ -36,7 +57,7 @@ inline void put_pyrepr(std::string& s, double v) {
   const char* p = buf;
   const char* end = res.ptr;
   if (*p == '-') {
-    s.push_back('-');
+    o.put('-');
     ++p;
   }
   char dig[24];
@@ -53,56 +74,54 @@ inline void put_pyrepr(std::string& s, double v) {
   if (eneg) ex = -ex;
   if (ex >= -4 && ex < 16) {
     if (ex >= 0) {
-      for (int i = 0; i <= ex; ++i) s.push_back(i < nd ? dig[i] : '0');
-      s.push_back('.');
-      if (nd > ex + 1) s.append(dig + ex + 1, (size_t)(nd - ex - 1));
-      else s.push_back('0');
+      for (int i = 0; i <= ex; ++i) o.put(i < nd ? dig[i] : '0');
+      o.put('.');
+      if (nd > ex + 1) o.put(dig + ex + 1, (size_t)(nd - ex - 1));
+      else o.put('0');
     } else {
-      s += "0.";
-      s.append((size_t)(-ex - 1), '0');
-      s.append(dig, (size_t)nd);
+      o.put("0.", 2);
+      for (int i = 0; i < -ex - 1; ++i) o.put('0');
+      o.put(dig, (size_t)nd);
     }
     return;
   }
-  s.push_back(dig[0]);
+  o.put(dig[0]);
   if (nd > 1) {
-    s.push_back('.');
-    s.append(dig + 1, (size_t)(nd - 1));
+    o.put('.');
+    o.put(dig + 1, (size_t)(nd - 1));
   }
   char eb[8];
   const int el = snprintf(eb, sizeof eb, "e%c%02d", ex < 0 ? '-' : '+', ex < 0 ? -ex : ex);
-  s.append(eb, (size_t)el);
+  o.put(eb, (size_t)el);
 }
 
-inline void put_double(std::string& s, double v, int prec) {
-  char buf[352];
-  int len;
+constexpr size_t F64_BOUND = 352;  // fixed notation of the largest double at precision <= 15 + repr
+
+inline void put_double(Out& o, double v, int prec) {
   if (prec == -2) {
-    put_pyrepr(s, v);
+    put_pyrepr(o, v);
     return;
   }
   if (std::isnan(v)) {
-    s += "NaN";
+    o.put("NaN", 3);
     return;
   }
   // std::to_chars with a precision formats exactly as printf's %.*f / %g (and several times faster)
-  auto res = prec >= 0 ? std::to_chars(buf, buf + sizeof buf, v, std::chars_format::fixed, prec)
-                       : std::to_chars(buf, buf + sizeof buf, v, std::chars_format::general, 6);  // "{:g}"
-  if (res.ec != std::errc()) {  // very large values at a high precision: printf into a heap buffer
-    len = snprintf(nullptr, 0, prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
+  auto res = prec >= 0 ? std::to_chars(o.w, o.w + F64_BOUND, v, std::chars_format::fixed, prec)
+                       : std::to_chars(o.w, o.w + F64_BOUND, v, std::chars_format::general, 6);  // "{:g}"
+  if (res.ec != std::errc()) {  // beyond the bound (very large values at a high precision)
+    const int len = snprintf(nullptr, 0, prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
     std::string tmp((size_t)len + 1, '\0');
     snprintf(tmp.data(), tmp.size(), prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
-    s.append(tmp.data(), (size_t)len);
+    o.commit();
+    o.ensure((size_t)len + (1u << 20));  // the rest of the row: its bound was reserved before
+    o.put(tmp.data(), (size_t)len);
     return;
   }
-  s.append(buf, (size_t)(res.ptr - buf));
+  o.w = res.ptr;
 }
 
-inline void put_int(std::string& s, int64_t v) {
-  char buf[24];
-  auto res = std::to_chars(buf, buf + sizeof buf, v);
-  s.append(buf, (size_t)(res.ptr - buf));
-}
+inline void put_int(Out& o, int64_t v) { o.w = std::to_chars(o.w, o.w + 24, v).ptr; }
 
 // [a, e) of field ``f`` of the line [p, p + n) split at any character with sep[c] set (f < 0:
 // counted from the end); false when the line has fewer fields
@@ -136,22 +155,27 @@ inline bool field_span(const char* p, int64_t n, int f, const uint8_t* sep, cons
 
 // append [p, p + n) with every separator character replaced by ``delim`` (copied as is when the
 // only separator is the delimiter itself)
-inline void put_rejoined(std::string& s, const char* p, int64_t n, const uint8_t* sep, bool same,
-                         const std::string& delim) {
+inline void put_rejoined(Out& o, const char* p, int64_t n, const uint8_t* sep, bool same, const std::string& delim) {
   if (same) {
-    s.append(p, (size_t)n);
+    o.put(p, (size_t)n);
     return;
   }
   const char* end = p + n;
   const char* a = p;
   for (const char* c = p; c < end; ++c)
     if (sep[(uint8_t)*c]) {
-      s.append(a, (size_t)(c - a));
-      s += delim;
+      o.put(a, (size_t)(c - a));
+      o.put(delim.data(), delim.size());
       a = c + 1;
     }
-  s.append(a, (size_t)(end - a));
+  o.put(a, (size_t)(end - a));
 }
+
+struct Tab {
+  std::vector<const char*> p;
+  std::vector<uint32_t> n;
+  size_t maxlen = 0;
+};
 
 }  // namespace
 
@@ -167,13 +191,24 @@ static std::vector<std::string> format_parts(const std::vector<FmtCol>& cols, in
     if ((c.kind == FmtCol::RAW || c.kind == FmtCol::FIELD || c.kind == FmtCol::TAIL) && (!c.raddr || !c.rlen))
       throw std::runtime_error("format_columns: line column without spans");
   }
-  // per column: separator table of the raw-line kinds, and whether re-joining changes nothing
+  // per column: separator table of the raw-line kinds, whether re-joining changes nothing, and the
+  // string table as (pointer, length) pairs
   std::vector<std::array<uint8_t, 256>> seps(cols.size());
   std::vector<char> same(cols.size(), 0);
+  std::vector<Tab> tabs(cols.size());
+  const size_t dl = delim.size();
   for (size_t k = 0; k < cols.size(); ++k) {
     seps[k].fill(0);
     for (char ch : cols[k].from_delims) seps[k][(uint8_t)ch] = 1;
     same[k] = cols[k].from_delims.empty() || cols[k].from_delims == delim;
+    if (cols[k].table) {
+      Tab& t = tabs[k];
+      for (const auto& str : *cols[k].table) {
+        t.p.push_back(str.data());
+        t.n.push_back((uint32_t)str.size());
+        t.maxlen = std::max(t.maxlen, str.size());
+      }
+    }
   }
   const int T = n < 16384 ? 1 : std::max(1, nthreads);
   std::vector<std::string> parts(T);
@@ -183,70 +218,94 @@ static std::vector<std::string> format_parts(const std::vector<FmtCol>& cols, in
     th.emplace_back([&, t] {
       try {
         const int64_t r0 = n * t / T, r1 = n * (t + 1) / T;
-        std::string& s = parts[t];
-        s.reserve((size_t)(r1 - r0) * (8 * cols.size() + 8));
+        Out o;
+        o.buf.resize((size_t)(r1 - r0) * (8 * cols.size() + 8) + 4096);
         for (int64_t r = r0; r < r1; ++r) {
+          // upper bound of this row's bytes
+          size_t bound = 1;
+          for (size_t ci = 0; ci < cols.size(); ++ci) {
+            const auto& c = cols[ci];
+            switch (c.kind) {
+              case FmtCol::STR: bound += tabs[ci].maxlen + dl; break;
+              case FmtCol::LIST:
+              case FmtCol::PAIRS:
+                bound += (size_t)(c.off[r + 1] - c.off[r]) *
+                         (tabs[ci].maxlen + dl + (c.kind == FmtCol::PAIRS ? 24 + dl : 0));
+                break;
+              case FmtCol::F64: bound += F64_BOUND + dl; break;
+              case FmtCol::I64: bound += 24 + dl; break;
+              case FmtCol::LIT:
+              case FmtCol::GLUE: bound += c.lit.size() + dl; break;
+              default: bound += (size_t)c.rlen[r] * std::max<size_t>(dl, 1) + dl;
+            }
+          }
+          o.ensure(bound);
           bool first = true;
           for (size_t ci = 0; ci < cols.size(); ++ci) {
             const auto& c = cols[ci];
             if (c.kind == FmtCol::GLUE) {
-              s += c.lit;
+              o.put(c.lit.data(), c.lit.size());
               continue;
             }
             if (c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) {
+              const Tab& tb = tabs[ci];
               const int64_t a = c.off[r], b = c.off[r + 1];
               for (int64_t j = a; j < b; ++j) {
-                if (!first) s += delim;
+                if (!first) o.put(delim.data(), dl);
                 first = false;
                 const int32_t k = c.idx[j];
-                if (k >= 0 && (size_t)k < c.table->size()) s += (*c.table)[(size_t)k];
+                if (k >= 0 && (size_t)k < tb.p.size()) o.put(tb.p[(size_t)k], tb.n[(size_t)k]);
                 if (c.kind == FmtCol::PAIRS) {
-                  s += delim;
-                  put_int(s, c.iv[j]);
+                  o.put(delim.data(), dl);
+                  put_int(o, c.iv[j]);
                 }
               }
               continue;
             }
-            if (!first) s += delim;
+            if (!first) o.put(delim.data(), dl);
             first = false;
             switch (c.kind) {
               case FmtCol::STR: {
+                const Tab& tb = tabs[ci];
                 const int32_t k = c.idx[r];
-                if (k >= 0 && (size_t)k < c.table->size()) s += (*c.table)[(size_t)k];
+                if (k >= 0 && (size_t)k < tb.p.size()) o.put(tb.p[(size_t)k], tb.n[(size_t)k]);
                 break;
               }
               case FmtCol::F64:
-                put_double(s, c.dv[r], c.prec);
+                put_double(o, c.dv[r], c.prec);
                 break;
               case FmtCol::I64:
-                put_int(s, c.iv[r]);
+                put_int(o, c.iv[r]);
                 break;
               case FmtCol::LIT:
-                s += c.lit;
+                o.put(c.lit.data(), c.lit.size());
                 break;
               case FmtCol::RAW:
-                put_rejoined(s, reinterpret_cast<const char*>(c.raddr[r]), c.rlen[r], seps[ci].data(), same[ci],
+                put_rejoined(o, reinterpret_cast<const char*>(c.raddr[r]), c.rlen[r], seps[ci].data(), same[ci],
                              delim);
                 break;
               case FmtCol::FIELD: {
                 const char *a, *e;
                 if (field_span(reinterpret_cast<const char*>(c.raddr[r]), c.rlen[r], c.field, seps[ci].data(), &a, &e))
-                  s.append(a, (size_t)(e - a));
+                  o.put(a, (size_t)(e - a));
                 break;
               }
               case FmtCol::TAIL: {
                 const char* p = reinterpret_cast<const char*>(c.raddr[r]);
                 const char *a, *e;
                 if (field_span(p, c.rlen[r], c.field, seps[ci].data(), &a, &e))
-                  put_rejoined(s, a, (int64_t)(p + c.rlen[r] - a), seps[ci].data(), false, delim);
+                  put_rejoined(o, a, (int64_t)(p + c.rlen[r] - a), seps[ci].data(), false, delim);
                 break;
               }
               default:
                 break;
             }
           }
-          s.push_back('\n');
+          o.put('\n');
+          o.commit();
         }
+        o.buf.resize(o.pos);
+        parts[t] = std::move(o.buf);
       } catch (const std::exception& e) {
         err[t] = e.what();
       }
