@@ -57,15 +57,15 @@ def run(cfg, impl, steps, warmup):
     B, T, I, H, L, O = (cfg[k] for k in "BTIHLO")
     ref = torch.nn.LSTM(I, H, L, batch_first=True)
     if impl.startswith("fused"):
-        lstm = FusedLSTM(I, H, L)
+        lstm = FusedLSTM(I, H, L, precision="bf16" if "bf16" in impl else "fp32")
         lstm.load_state_dict(ref.state_dict())
     else:
         lstm = ref
     net = Net(lstm, H, O).to(dev)
     # miopen_bf16: the whole model in bf16 on MIOpen — the like-for-like precision comparison for
     # the fused kernel's bf16 GEMM operands (miopen = fp32, the reference's numerics)
-    xdt = torch.bfloat16 if impl == "miopen_bf16" else torch.float32
-    if impl == "miopen_bf16":
+    xdt = torch.bfloat16 if impl.startswith("miopen_bf16") else torch.float32
+    if impl.startswith("miopen_bf16"):
         net = net.to(torch.bfloat16)
     graph = impl.endswith("graph")
     opt = torch.optim.Adam(net.parameters(), lr=2e-3, capturable=graph)
@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--configs", default="all")
-    ap.add_argument("--impls", default="fused,fused_graph,miopen,miopen_bf16")
+    ap.add_argument("--impls", default="fused,fused_graph,fused_bf16,miopen,miopen_graph,miopen_bf16")
     args = ap.parse_args()
     names = None if args.configs == "all" else set(args.configs.split(","))
     for cfg in CONFIGS:
@@ -120,16 +120,22 @@ def main():
             continue
         res = {}
         for impl in args.impls.split(","):
-            res[impl] = run(cfg, impl, args.steps, args.warmup)
-            print(json.dumps(res[impl]), flush=True)
-        for base in ("miopen", "miopen_bf16"):      # fp32 (reference numerics) and like-for-like bf16
-            if base not in res:
+            try:
+                res[impl] = run(cfg, impl, args.steps, args.warmup)
+            except RuntimeError as e:        # e.g. a library LSTM that refuses graph capture
+                print(json.dumps({"bench": "lstm", "config": cfg["name"], "impl": impl, "error": str(e)[:200]}),
+                      flush=True)
+                res[impl] = None
                 continue
-            for impl in res:
-                if impl.startswith("fused"):
-                    print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"], "impl": impl, "vs": base,
-                                      "train_x": res[base]["train_ms"] / res[impl]["train_ms"],
-                                      "infer_x": res[base]["infer_ms"] / res[impl]["infer_ms"]}), flush=True)
+            print(json.dumps(res[impl]), flush=True)
+        # like-for-like pairs: eager vs eager and graph vs graph at fp32 (the reference's numerics),
+        # and the bf16 fused kernel vs bf16 MIOpen
+        for impl, base in (("fused", "miopen"), ("fused_graph", "miopen_graph"), ("fused_bf16", "miopen_bf16"),
+                           ("fused_graph", "miopen")):
+            if impl in res and base in res and res[base] and res[impl]:
+                print(json.dumps({"bench": "lstm_speedup", "config": cfg["name"], "impl": impl, "vs": base,
+                                  "train_x": res[base]["train_ms"] / res[impl]["train_ms"],
+                                  "infer_x": res[base]["infer_ms"] / res[impl]["infer_ms"]}), flush=True)
 
 
 if __name__ == "__main__":
