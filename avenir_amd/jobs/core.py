@@ -28,8 +28,9 @@ def nb_train(args):
     ctx = JobContext(args, "bad.")
     if not ctx.get_bool("tabular.input", True):
         from ..models.bayes import TextNaiveBayesModel
-        m = TextNaiveBayesModel.fit_lines(ctx.lines(), ctx.split, ctx, ctx.get_int("class.field.ordinal", 1),
-                                          ctx.get_int("text.field.ordinal", 0))
+        co, to = ctx.get_int("class.field.ordinal", 1), ctx.get_int("text.field.ordinal", 0)
+        m = TextNaiveBayesModel.fit_native(ctx, co, to) or TextNaiveBayesModel.fit_lines(ctx.lines(), ctx.split, ctx,
+                                                                                          co, to)
         ctx.emit_root(m.model_lines(ctx.delim_out))
         return
     t = ctx.table()
@@ -48,6 +49,20 @@ def nb_predict(args):
         from ..models.bayes import TextNaiveBayesModel
         m = TextNaiveBayesModel.load(ctx.path("bayesian.model.file.path", "model"), ctx.split)
         to = ctx.get_int("text.field.ordinal", 0)
+        got = TextNaiveBayesModel.word_tokens(ctx, ctx.get_int("class.field.ordinal", 1), to)
+        if got is not None:
+            # native: word ids of the shard's documents -> the model vocabulary (dictionary level),
+            # one bag-of-words GEMM, output from the raw line bytes
+            line, wid, uniq, _, fields = got
+            mi = {w: i for i, w in enumerate(m.vocab)}
+            lut = torch.tensor([mi.get(w, -1) for w in uniq] or [-1], dtype=torch.long)
+            mw = lut[wid] if wid.numel() else wid
+            k = mw >= 0
+            pred, prob = m.predict_bow(line[k], mw[k], fields.n_lines)
+            spans = fields.line_spans()
+            ctx.emit_columns([spans.column("r", delims=ctx.native_delim()), ("s", m.classes, pred.cpu()),
+                              ("i", torch.round(100 * prob.cpu()).long())], fields.n_lines)
+            return
         rows = ctx.rows()
         pred, prob = m.predict([r[to] for r in rows])
         d = ctx.delim_out

@@ -558,6 +558,26 @@ class TextNaiveBayesModel:
         self.counts, self.docs = counts, docs          # int64 [C, V], int64 [C]
 
     @classmethod
+    def fit_native(cls, ctx, class_ord: int = 1, text_ord: int = 0) -> "TextNaiveBayesModel | None":
+        """``fit_lines`` over native token tables (None when the layout needs the row path): one
+        ``[C, V]`` bincount of (class, word) over the shard's words, all-reduced; the vocabulary is
+        the global set of text words (the merged dictionary's lowered entries that occur)."""
+        got = cls.word_tokens(ctx, class_ord, text_ord)
+        if got is None:
+            return None
+        line, wid, uniq, ccode, fields = got
+        classes = ctx.union(fields.strings(torch.unique(ccode[ccode >= 0])))
+        cl = fields.map_codes(ccode, classes).long().cpu()
+        C, Vu = len(classes), len(uniq)
+        dev = ctx.device
+        counts = torch.bincount((cl[line] * Vu + wid).to(dev), minlength=C * Vu)[: C * Vu].view(C, Vu)
+        docs = torch.bincount(cl.to(dev), minlength=C)[:C]
+        ctx.all_reduce(counts, docs)
+        used = torch.nonzero(counts.sum(0) > 0).view(-1)
+        vocab = [uniq[i] for i in used.tolist()]
+        return cls(classes, vocab, counts[:, used], docs)
+
+    @classmethod
     def fit_lines(cls, lines: list[str], split, ctx, class_ord: int = 1, text_ord: int = 0) -> "TextNaiveBayesModel":
         rows = [split(l) for l in lines]
         toks = [tokenize(r[text_ord]) for r in rows]
@@ -613,22 +633,73 @@ class TextNaiveBayesModel:
         """Multinomial NB with Laplace smoothing: argmax_c log P(c) + sum_w n_w log P(w|c); the
         bag-of-words matrix times the log-probability table is one GEMM."""
         vi = {w: i for i, w in enumerate(self.vocab)}
-        C, V = self.counts.shape
-        dev = self.counts.device
         rows, cols = [], []
         for i, t in enumerate(texts):
             for w in tokenize(t):
                 if w in vi:
                     rows.append(i)
                     cols.append(vi[w])
-        bow = torch.zeros((len(texts), V), dtype=torch.float64, device=dev)
-        if rows:
-            bow.index_put_((torch.tensor(rows, device=dev), torch.tensor(cols, device=dev)),
-                           torch.ones(len(rows), dtype=torch.float64, device=dev), accumulate=True)
+        pred, prob = self.predict_bow(torch.tensor(rows, dtype=torch.long), torch.tensor(cols, dtype=torch.long),
+                                      len(texts), alpha)
+        return pred.tolist(), prob.tolist()
+
+    def predict_bow(self, rows: torch.Tensor, cols: torch.Tensor, n: int, alpha: float = 1.0):
+        """Class index and probability tensors of ``n`` documents given as (document, word id)
+        occurrence pairs (word ids into ``vocab``)."""
+        C, V = self.counts.shape
+        dev = self.counts.device
+        bow = torch.zeros((n, V), dtype=torch.float64, device=dev)
+        if rows.numel():
+            bow.index_put_((rows.to(dev), cols.to(dev)), torch.ones(rows.numel(), dtype=torch.float64, device=dev),
+                           accumulate=True)
         cnt = self.counts.double()
         logp = torch.log((cnt + alpha) / (cnt.sum(1, keepdim=True) + alpha * V))
         prior = torch.log(self.docs.double() / self.docs.sum().clamp_min(1)).to(dev)
         s = bow @ logp.T + prior
         p = torch.softmax(s, 1)
         best = p.max(1)
-        return best.indices.tolist(), best.values.tolist()
+        return best.indices, best.values
+
+    # -- native text tokens ---------------------------------------------------------------------
+    @staticmethod
+    def word_tokens(ctx, class_ord: int = 1, text_ord: int = 0):
+        """The ``tokenize`` words of every line's text field from native token tables, or None when
+        the layout is not ``text<delim>class`` with a one-character delimiter.  Returns (line of
+        every word token int64, lowered word id int64, lowered word strings, class codes per line,
+        class Records).  Two native passes over the shard: the fields (class codes), and the bytes
+        split at every non-alphanumeric byte (the text field's words are the tokens before the
+        class field's); case folding and stop words are dictionary-level."""
+        dl = ctx.native_delim()
+        if dl is None or text_ord != 0 or class_ord != 1 or dl.isalnum():
+            return None
+        fields = ctx.records(modes="xd", tail_mode="x")
+        ok = torch.tensor([float(fields.width() in (0, 2))])
+        if ctx.comm.is_distributed:
+            ctx.comm.all_reduce(ok, "min")          # every rank takes the same path
+        if not bool(ok[0] > 0):
+            return None
+        seps = "".join(chr(c) for c in range(1, 256) if not (chr(c).isascii() and chr(c).isalnum()))
+        words = ctx.records(delims=seps, tail_mode="d")
+        if words.n_lines != fields.n_lines:
+            return None
+        low = [w.lower() for w in words.vocab]
+        uniq = sorted(set(low))
+        ui = {w: i for i, w in enumerate(uniq)}
+        lut = torch.tensor([ui[w] if (w and w not in _STOP) else -1 for w in low] or [-1], dtype=torch.long)
+        # tokens of the class string (same split), per class code: they end every line
+        import re
+        cls = fields.field(1).long().cpu()
+        off = words.off.cpu()
+        lens = off[1:] - off[:-1]
+        # the class field's pieces: every separator inside it adds a (possibly empty) token, so
+        # count its separator-delimited pieces instead of its words
+        pieces = torch.tensor([len(re.split("[" + re.escape(seps) + "]", v)) for v in fields.vocab] or [1],
+                              dtype=torch.long)
+        text_len = lens - torch.where(cls >= 0, pieces[cls.clamp_min(0)], torch.zeros_like(cls))
+        codes = words.codes.long().cpu()
+        line = torch.repeat_interleave(torch.arange(words.n_lines), lens)
+        pos = torch.arange(codes.numel()) - off[:-1][line]
+        keep = pos < text_len[line]
+        wid = torch.where(codes >= 0, lut[codes.clamp_min(0)], torch.full_like(codes, -1))
+        keep &= wid >= 0
+        return line[keep], wid[keep], uniq, cls, fields

@@ -218,3 +218,46 @@ def test_word_count_native_equals_counter(tmp_path):
 def _world_wc(rank, world, inp, out):
     assert main(["wordCount", "-i", inp, "-o", out, "--device", "cpu"]) == 0
     return True
+
+
+def _docs(tmp, n=800, seed=9):
+    rng = np.random.default_rng(seed)
+    words = ["Cheap", "pills", "offer", "NOW", "meeting", "agenda", "Monday", "the", "a", "prize!", "win",
+             "project", "notes", "x2", "co-op", "É", "review."]
+    rows = []
+    for _ in range(n):
+        spam = rng.random() < 0.4
+        ws = rng.choice(words[:5] + words[8:11] if spam else words[4:], int(rng.integers(1, 9)))
+        rows.append(" ".join(ws) + ("," + ("spam" if spam else "ham-ok")))
+    p = tmp / "docs.txt"
+    p.write_text("\n".join(rows) + "\n")
+    q = tmp / "q.txt"
+    q.write_text("\n".join(" ".join(rng.choice(words, 4)) + ",?" for _ in range(300)) + "\n")
+    return p, q
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_text_nb_native_equals_row_path(tmp_path, world):
+    data, q = _docs(tmp_path)
+    outs = {}
+    for regex in (False, True):
+        dl = "[,]" if regex else ","
+        cfg = tmp_path / f"t{int(regex)}.properties"
+        cfg.write_text(f"bad.tabular.input=false\nbap.tabular.input=false\nfield.delim.regex={dl}\n")
+        model, out = tmp_path / f"m{int(regex)}.txt", tmp_path / f"p{int(regex)}"
+        if world == 1 or regex:
+            assert main(["bayesianDistribution", "-i", str(data), "-o", str(model), "-c", str(cfg), "--device", "cpu"]) == 0
+            assert main(["bayesianPredictor", "-i", str(q), "-o", str(out), "-c", str(cfg), "--model", str(model),
+                         "--device", "cpu"]) == 0
+        else:
+            run_world(_world_nb, 2, str(data), str(q), str(cfg), str(model), str(out), timeout=300)
+        outs[regex] = (_lines(model), _lines(out))
+    assert outs[False][0] and outs[False] == outs[True]
+
+
+def _world_nb(rank, world, data, q, cfg, model, out):
+    assert main(["bayesianDistribution", "-i", data, "-o", model, "-c", cfg, "--device", "cpu"]) == 0
+    from avenir_amd.parallel.comm import get_comm
+    get_comm().barrier()
+    assert main(["bayesianPredictor", "-i", q, "-o", out, "-c", cfg, "--model", model, "--device", "cpu"]) == 0
+    return True
