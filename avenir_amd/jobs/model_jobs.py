@@ -239,16 +239,20 @@ def same_type_similarity(args):
         files = input_files(args.input)
         tr_path = ",".join(str(f) for f in files if f.name.startswith(pref))
         te_path = ",".join(str(f) for f in files if not f.name.startswith(pref))
-    tr = ctx.table(path=tr_path, schema=schema, shard=False, raw_numeric=True)
+    # both sets are row-sharded; the training shards travel the ring (top-k) or are all-gathered
+    # once (all pairs); output columns come from the raw line bytes of both sets
+    tr = ctx.table(path=tr_path, schema=schema, raw_numeric=True)
     te = ctx.table(path=te_path, schema=schema, raw_numeric=True)
+    comm = ctx.comm
     ranges = {}
     for j, f in enumerate(tr.numeric_fields):
         x = torch.cat([tr.numeric[j, : tr.n], te.numeric[j, : te.n].to(tr.numeric.device)])
-        lo, hi = torch.nan_to_num(x).min(), torch.nan_to_num(x).max()
-        if ctx.comm.is_distributed:
-            lo, hi = lo.clone().view(1), hi.clone().view(1)
-            ctx.comm.all_reduce(lo, "min")
-            ctx.comm.all_reduce(hi, "max")
+        x = torch.nan_to_num(x)
+        lo = x.min().view(1) if x.numel() else torch.full((1,), math.inf, device=x.device)
+        hi = x.max().view(1) if x.numel() else torch.full((1,), -math.inf, device=x.device)
+        if comm.is_distributed:
+            comm.all_reduce(lo, "min")
+            comm.all_reduce(hi, "max")
         ranges[f.ordinal] = (float(f.min) if f.min is not None else float(lo), float(f.max) if f.max is not None else float(hi))
     nf = max(1, len(tr.numeric_fields) + len(tr.binned_fields))
     topk = ctx.get_int("top.match.count", 0)
@@ -256,35 +260,67 @@ def same_type_similarity(args):
     # wide categoricals: the column-wise mixed kernel instead of a one-hot embedding (GPU top-k)
     use_mixed = (0 < topk <= 32 and tr.device.type == "cuda" and onehot > 64
                  and len(tr.numeric_fields) + len(tr.binned_fields) <= 32)
-    if not use_mixed:
-        A = encode_mixed(tr, ranges=ranges)
-        B = encode_mixed(te, ranges=ranges)
     scale = ctx.get_float("distance.scale", 1000.0)
-    cls_tr = tr.label_values() if tr.labels is not None else [""] * tr.n
-    cls_te = te.label_values() if te.labels is not None else [""] * te.n
-    id_tr = tr.ids or [str(i) for i in range(tr.n)]
-    id_te = te.ids or [str(i + te.row_offset) for i in range(te.n)]
-    d = ctx.delim_out
-    out = []
+    idf = schema.id_field
+    dl = ctx.native_delim() or ","
+    cls_vals = list(te.class_field.cardinality) if te.class_field is not None else []
+    lab = lambda t: (t.labels[: t.n].long().cpu() if t.labels is not None else torch.full((t.n,), -1, dtype=torch.long))
+    # training rows' identity (line bytes + class codes) on every rank: one packed all-gather
+    from ..data.lines import LineSpans
+    tr_spans = _as_spans(tr)
+    tr_lab = lab(tr)
+    if comm.is_distributed:
+        buf, off = tr_spans.pack()
+        g_len = comm.all_gather_v(off[1:] - off[:-1])
+        tr_spans = LineSpans.from_packed(comm.all_gather_v(buf),
+                                         torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(g_len, 0)]))
+        tr_lab = comm.all_gather_v(tr_lab)
+    te_spans, te_lab = _as_spans(te), lab(te)
+    tr_base = tr.row_offset
+
+    def pair_columns(it, iq, dist):
+        """Output columns of pairs (global train row ``it``, local test row ``iq``)."""
+        tid = tr_spans.select(it).column("rf", idf.ordinal, dl) if idf is not None else ("i", it)
+        qid = te_spans.select(iq).column("rf", idf.ordinal, dl) if idf is not None else ("i", iq + te.row_offset)
+        return [tid, qid, ("i", dist), ("s", cls_vals, tr_lab[it]), ("s", cls_vals, te_lab[iq])]
+
     if topk > 0:
+        from ..ops.distance import distributed_knn, distributed_knn_mixed
         if use_mixed:
             An, Ac, wc = split_mixed(tr, ranges=ranges)
             Bn, Bc, _ = split_mixed(te, ranges=ranges)
-            dist, idx = knn_mixed(Bn, Bc, An, Ac, wc, topk)
+            dist, idx = distributed_knn_mixed(Bn, Bc, An, Ac, wc, topk, comm, r_base=tr_base)
         else:
-            dist, idx = knn(B, A, topk, "euclidean")
-        dist = (dist / math.sqrt(nf) * scale).round().long().cpu().tolist()
-        for q, (dr, ir) in enumerate(zip(dist, idx.cpu().tolist())):
-            for dd, i in zip(dr, ir):
-                if i >= 0:
-                    out.append(d.join([id_tr[i], id_te[q], str(dd), cls_tr[i], cls_te[q]]))
-    else:
-        for s in range(0, te.n, 4096):
-            D = (pairwise(B[s:s + 4096], A) / math.sqrt(nf) * scale).round().long().cpu()
-            for q in range(D.shape[0]):
-                row = D[q].tolist()
-                out += [d.join([id_tr[i], id_te[s + q], str(row[i]), cls_tr[i], cls_te[s + q]]) for i in range(tr.n)]
-    ctx.emit(out)
+            A, B = encode_mixed(tr, ranges=ranges), encode_mixed(te, ranges=ranges)
+            dist, idx = distributed_knn(B, A, topk, comm, "euclidean", r_base=tr_base)
+        dist = (dist / math.sqrt(nf) * scale).round().long().cpu()
+        idx = idx.cpu()
+        ok = idx >= 0
+        iq = torch.arange(idx.shape[0]).view(-1, 1).expand_as(idx)[ok]
+        ctx.emit_columns(pair_columns(idx[ok], iq, dist[ok]), int(ok.sum()))
+        return
+    from ..data.records import format_lines
+    A, B = encode_mixed(tr, ranges=ranges), encode_mixed(te, ranges=ranges)
+    if comm.is_distributed:
+        A = comm.all_gather_v(A.contiguous())
+    ntr = A.shape[0]
+    parts = []
+    step = max(1, (1 << 22) // max(ntr, 1))
+    for s0 in range(0, te.n, step):
+        D = (pairwise(B[s0:s0 + step], A) / math.sqrt(nf) * scale).round().long().cpu()
+        nq = D.shape[0]
+        it = torch.arange(ntr).repeat(nq)
+        iq = torch.arange(s0, s0 + nq).repeat_interleave(ntr)
+        parts.append(format_lines(pair_columns(it, iq, D.reshape(-1)), nq * ntr, ctx.delim_out))
+    ctx.emit_text(b"".join(parts))
+
+
+def _as_spans(t):
+    """A table's kept input lines as byte spans (data/lines.LineSpans)."""
+    from ..data.lines import LineSpans
+    if isinstance(t.lines, LineSpans):
+        return t.lines
+    return LineSpans.from_strings(list(t.lines or [""] * t.n))
 
 
 @job("featureCondProbJoiner", "join NB feature posteriors of training records onto distance pairs (J/knn/FeatureCondProbJoiner.java, fcb.*)")

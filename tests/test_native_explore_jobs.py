@@ -261,3 +261,29 @@ def _world_nb(rank, world, data, q, cfg, model, out):
     get_comm().barrier()
     assert main(["bayesianPredictor", "-i", q, "-o", out, "-c", cfg, "--model", model, "--device", "cpu"]) == 0
     return True
+
+
+def _sts_world(rank, world, argv, out):
+    assert main(argv + ["-o", out, "--device", "cpu"]) == 0
+    return True
+
+
+@pytest.mark.parametrize("topk", [0, 5])
+def test_same_type_similarity_world_invariant(tmp_path, topk):
+    """sameTypeSimilarity with both sets row-sharded (training shards on the ring for top-k, one
+    all-gather for all pairs): world 2 writes exactly the world-1 output."""
+    from avenir_amd.data.fixtures import FIXTURES
+    fix = Path(__file__).parent / "fixtures"
+    data = FIXTURES["elearn"](300, seed=7, as_int=True)
+    tr, te = tmp_path / "train.txt", tmp_path / "test.txt"
+    tr.write_text("\n".join(data[:200]) + "\n")
+    te.write_text("\n".join(data[200:]) + "\n")
+    props = tmp_path / "sts.properties"
+    props.write_text(f"sts.same.schema.file.path={fix / 'elearnActivity.json'}\nsts.distance.scale=1000\n"
+                     f"sts.top.match.count={topk}\n")
+    argv = ["sameTypeSimilarity", "-i", str(te), "--train", str(tr), "-c", str(props)]
+    assert main(argv + ["-o", str(tmp_path / "w1"), "--device", "cpu"]) == 0
+    w1 = _lines(tmp_path / "w1")
+    assert len(w1) == 100 * (topk or 200)
+    run_world(_sts_world, 2, argv, str(tmp_path / "w2"), timeout=300)
+    assert _lines(tmp_path / "w2") == w1

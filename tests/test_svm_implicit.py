@@ -110,13 +110,16 @@ def _dual(alpha, y, X, gamma):
 
 
 @pytest.mark.gpu
-def test_production_path_n8192_matches_fp64_dual_and_sklearn(cuda, monkeypatch):
-    """The implicit-kernel native loop (the path above DENSE_MAX_N rows) at N = 8192 x 16 RBF."""
+@pytest.mark.parametrize("path", ["implicit", "dense"])
+def test_production_path_n8192_matches_fp64_dual_and_sklearn(cuda, monkeypatch, path):
+    """The production working-set paths at N = 8192 x 16 RBF (native C++ outer loop, two-level
+    selection with the rank merge, graph-captured step blocks): the implicit kernel (rows from X,
+    the path above DENSE_MAX_N rows) and the dense kernel matrix."""
     from sklearn.svm import SVC as SKSVC
-    monkeypatch.setattr(S, "DENSE_MAX_N", 0)
+    monkeypatch.setattr(S, "DENSE_MAX_N", 0 if path == "implicit" else 1 << 30)
     X, y = _blobs(8192)
     m = S.SVC(kernel="rbf", C=1.0, gamma=0.05, eps=1e-3).fit(torch.tensor(X, device=cuda), torch.tensor(y, device=cuda))
-    assert S.LAST_SOLVE.get("solver") == "ws-implicit"
+    assert S.LAST_SOLVE.get("solver") == ("ws-implicit" if path == "implicit" else "ws")
     alpha = np.zeros(len(y))
     dc = m.dual_coef[0].double().cpu().numpy()
     alpha[m.support_.cpu().numpy()] = np.abs(dc)
