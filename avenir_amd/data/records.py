@@ -584,6 +584,27 @@ def shuffle(comm, owner: torch.Tensor, cols: list[torch.Tensor]) -> list[torch.T
     return out
 
 
+def shuffle_spans(comm, owner: torch.Tensor, spans):
+    """The line bytes behind ``spans`` sent along with :func:`shuffle` (same ``owner``): every
+    destination receives its lines in source-rank order, each source's lines in their original
+    order — aligned with the rows :func:`shuffle` delivers.  Returns a LineSpans over the
+    received bytes (one packed byte all-to-all plus one of the lengths)."""
+    from .lines import LineSpans
+    owner = owner.cpu()
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=comm.world).tolist()
+    buf, off = spans.select(order).pack()
+    lens = off[1:] - off[:-1]
+    bounds = [0]
+    for c in counts:
+        bounds.append(bounds[-1] + c)
+    byte_chunks = [buf[int(off[bounds[r]]):int(off[bounds[r + 1]])] for r in range(comm.world)]
+    len_chunks = [lens[bounds[r]:bounds[r + 1]] for r in range(comm.world)]
+    rb = torch.cat(comm.all_to_all_v(byte_chunks), 0) if comm.world else buf
+    rl = torch.cat(comm.all_to_all_v(len_chunks), 0)
+    return LineSpans.from_packed(rb, torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(rl, 0)]))
+
+
 def numeric_lut(vocab: list[str], device) -> torch.Tensor:
     """float64 [V]: the number each dictionary string parses to (NaN otherwise) — numeric fields
     tokenized as dictionary entries (ranks, small integer fields)."""

@@ -28,11 +28,12 @@ def normalizer(args):
     ords = ctx.get_int_list("num.attribute.ordinals")
     strat = ctx.get_str("normalizing.strategy", "minmax")
     prec = ctx.get_int("floating.precision", 3)
-    rows = ctx.rows()
-    X = torch.tensor([[float(r[o]) for o in ords] for r in rows], dtype=torch.float64).view(len(rows), len(ords))
-    st = torch.stack([torch.full((len(ords),), float(len(rows)), dtype=torch.float64), X.sum(0), (X * X).sum(0)])
-    mn = X.min(0).values if len(rows) else torch.full((len(ords),), math.inf, dtype=torch.float64)
-    mx = X.max(0).values if len(rows) else torch.full((len(ords),), -math.inf, dtype=torch.float64)
+    X, src = ctx.numeric_matrix(ords)
+    X = X.cpu()
+    nrow = X.shape[0]
+    st = torch.stack([torch.full((len(ords),), float(nrow), dtype=torch.float64), X.sum(0), (X * X).sum(0)])
+    mn = X.min(0).values if nrow else torch.full((len(ords),), math.inf, dtype=torch.float64)
+    mx = X.max(0).values if nrow else torch.full((len(ords),), -math.inf, dtype=torch.float64)
     ctx.all_reduce(st)
     if ctx.comm.is_distributed:
         ctx.comm.all_reduce(mn, "min")
@@ -47,6 +48,12 @@ def normalizer(args):
             Y = (Y - lo) / (hi - lo).clamp_min(1e-300)
     else:
         Y = (X - mn) / (mx - mn).clamp_min(1e-300)
+    if not isinstance(src, list):         # native: the raw fields around the normalised values
+        if _emit_replaced(ctx, src, {o: ("f", Y[:, j].contiguous(), prec) for j, o in enumerate(ords)}):
+            return
+        rows = ctx.rows()
+    else:
+        rows = src
     d = ctx.delim_out
     out = []
     for r, y in zip(rows, Y.tolist()):
@@ -64,8 +71,19 @@ def projection(args):
     from ..utils.rules import RuleExpression
     ctx = JobContext(args, "pro.")
     fields = ctx.get_int_list("projection.field")
-    rows = ctx.rows()
     flt = ctx.get_str("select.filter", None)
+    rule = RuleExpression.from_condition(flt, ctx.get_str("cond.delim", " and ")) if flt else None
+    from ..utils.rules import RecordColumns, rule_field_modes
+    from .common import field_modes
+    fm = rule_field_modes([rule] if rule else [])
+    rec = ctx.try_records(modes=field_modes(fm), tail_mode="x", numeric=True, trim=True)
+    if rec is not None:
+        keep = rule.evaluate(RecordColumns(rec, [o for o, m in fm.items() if m == "n"])).cpu() if rule else \
+            torch.ones(rec.n_lines, dtype=torch.bool)
+        spans, dl = rec.line_spans().select(keep), ctx.native_delim()
+        ctx.emit_columns([spans.column("rf", o, dl) for o in fields], len(spans))
+        return
+    rows = ctx.rows()
     keep = RuleExpression.from_condition(flt, ctx.get_str("cond.delim", " and ")).evaluate_rows(rows).tolist() \
         if flt else [True] * len(rows)
     d = ctx.delim_out
@@ -79,14 +97,18 @@ def temporal_filter(args):
     lo, hi = (float(x) for x in ctx.get_str("time.range").split(":"))
     mult = 1.0 if ctx.get_bool("time.stamp.in.mili", False) else 1000.0
     shift = ctx.get_float("time.zone.shift.hours", 0.0) * 3600.0
-    rows = ctx.rows()
-    t = torch.tensor([float(r[to]) for r in rows], dtype=torch.float64)
+    t, src = ctx.numeric_matrix([to])
+    t = t[:, 0].cpu()
     if mult == 1.0:
         t = t / 1000.0
     t = t + shift
-    keep = ((t >= lo) & (t <= hi)).tolist()
+    keep = (t >= lo) & (t <= hi)
+    if not isinstance(src, list):
+        spans = src.line_spans().select(keep)
+        ctx.emit_columns([spans.column("r", delims=ctx.native_delim())], len(spans))
+        return
     d = ctx.delim_out
-    ctx.emit([d.join(r) for r, k in zip(rows, keep) if k])
+    ctx.emit([d.join(r) for r, k in zip(src, keep.tolist()) if k])
 
 
 @job("transformer", "attribute transformers from a schema (chombo mr.Transformer, tra.*): keyValueTrans lookup")
@@ -119,6 +141,24 @@ def transformer(args):
                 else:
                     lut[q[0]] = q[1]
             luts[a["ordinal"]] = lut
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({a["ordinal"]: "d" for a in attrs}), tail_mode="x")
+    if rec is not None and rec.width() is not None:
+        # native: each attribute's lookup is one table over the dictionary; every target field is
+        # a string-table column, the other fields the raw bytes
+        rep_cols = {}
+        for a in attrs:
+            o = a["ordinal"]
+            lut = luts.get(o, {})
+            tab = [lut.get(w, w) for w in rec.vocab]
+            for t in a.get("targetFieldOrdinals", [o]):
+                rep_cols[t] = ("s", tab, rec.field(o).cpu())
+        width = max([rec.width()] + [t + 1 for t in rep_cols])
+        spans = rec.line_spans()
+        cols = [rep_cols[j] if j in rep_cols else (spans.column("rf", j, ctx.native_delim()) if j < rec.width()
+                                                  else ("c", "")) for j in range(width)]
+        ctx.emit_columns(cols, rec.n_lines)
+        return
     d = ctx.delim_out
     out = []
     for r in ctx.rows():
@@ -143,6 +183,28 @@ def unique_value_counter(args):
     ctx = JobContext(args, app="uniqueValueCounter")
     ords = ctx.get_int_list("cat.field.ordinals", None) or ctx.get_int_list("cat.fieldOrdinals")
     ci = ctx.get_bool("case.insensitive", False)
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({o: "d" for o in ords}), tail_mode="x")
+    if rec is not None:
+        # native: per field one bincount over the (globally merged) dictionary, one all-reduce
+        voc = [w.lower() for w in rec.vocab] if ci else rec.vocab
+        uv = sorted(set(voc))
+        ui = {w: i for i, w in enumerate(uv)}
+        lut = torch.tensor([ui[w] for w in voc] or [0], dtype=torch.long, device=rec.device)
+        U = max(1, len(uv))
+        C = torch.stack([torch.bincount(lut[c[c >= 0].long()], minlength=U)[:U] for c in
+                         (rec.field(o) for o in ords)]) if ords else torch.zeros((0, U), dtype=torch.long)
+        ctx.all_reduce(C)
+        with_counts = ctx.get_bool("count.values", False)
+        d = ctx.delim_out
+        out = []
+        for j, o in enumerate(ords):
+            parts = [str(o)]
+            for i in torch.nonzero(C[j] > 0).view(-1).tolist():
+                parts += [uv[i], str(int(C[j, i]))] if with_counts else [uv[i]]
+            out.append(d.join(parts))
+        ctx.emit_root(out)
+        return
     cnt = Counter()
     for r in ctx.rows():
         for o in ords:
@@ -169,6 +231,11 @@ def time_interval(args):
     kords = ctx.get_int_list("id.fieldOrdinals")
     to = ctx.get_int("time.fieldOrdinal")
     keep = ctx.get_bool("time.keepField", True)
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({**{o: "d" for o in kords}, to: "n"}), tail_mode="x", numeric=True)
+    if rec is not None:
+        _time_interval_native(ctx, rec, kords, to, keep)
+        return
     rows = ctx.rows(shard=False)
     keys = sorted({tuple(r[o] for o in kords) for r in rows})
     ki = {k: i for i, k in enumerate(keys)}
@@ -194,6 +261,51 @@ def time_interval(args):
     ctx.emit(out[a:b])
 
 
+def _time_interval_native(ctx, rec, kords, to, keep):
+    """timeIntervalGenerator over byte-range shards: every record (with its line bytes) moves to the
+    rank owning its key (keys in string order cut into contiguous blocks), one device sort by
+    (key, time, input order) there, intervals by one shifted difference."""
+    from ..data.records import owner_of, shuffle, shuffle_spans, sorted_key_tuples
+    comm = ctx.comm
+    kpos, G, _ = sorted_key_tuples(rec, [rec.field(o) for o in kords], comm)
+    t = rec.field(to, numeric=True).long()
+    gidx = rec.line_base + torch.arange(rec.n_lines, device=t.device)
+    spans = rec.line_spans()
+    if comm.is_distributed:
+        owner = owner_of(kpos, G, comm.world)
+        spans = shuffle_spans(comm, owner.cpu(), spans)
+        kpos, t, gidx = shuffle(comm, owner, [kpos, t, gidx])
+    o = torch.argsort(gidx, stable=True)
+    o = o[torch.argsort(t[o], stable=True)]
+    o = o[torch.argsort(kpos[o], stable=True)]
+    ks, ts = kpos[o], t[o]
+    dt = torch.zeros_like(ts)
+    if ts.numel() > 1:
+        dt[1:] = torch.where(ks[1:] == ks[:-1], ts[1:] - ts[:-1], torch.zeros_like(ts[1:]))
+    sel = spans.select(o.cpu())
+    dl = ctx.native_delim()
+    if keep:
+        cols = [sel.column("r", delims=dl), ("i", dt.cpu())]
+    else:
+        W = rec.width()
+        if W is None:
+            raise SystemExit("timeIntervalGenerator: records of differing field counts")
+        from .common import field_columns
+        cols = field_columns(sel, W, dl, {to: ("i", dt.cpu())})
+    ctx.emit_columns(cols, len(sel))
+
+
+def _emit_replaced(ctx, rec, replace: dict) -> bool:
+    """Emit every record with fields ``replace`` swapped for format columns (fixed-width tables);
+    False when the records differ in width (the caller takes its row path)."""
+    from .common import field_columns
+    W = rec.width()
+    if W is None:
+        return False
+    ctx.emit_columns(field_columns(rec.line_spans(), W, ctx.native_delim(), replace), rec.n_lines)
+    return True
+
+
 @job("numericalAttrDistrStats", "per-key fixed-width histograms of numeric attributes (chombo spark.explore.NumericalAttrDistrStats)")
 def num_distr_stats(args):
     """Per (id.fieldOrdinals key, attribute) a histogram of bin width ``attrBinWidth.<ord>``; one
@@ -203,6 +315,12 @@ def num_distr_stats(args):
     kords = ctx.get_int_list("id.fieldOrdinals", []) if ctx.has("id.fieldOrdinals") else []
     attrs = ctx.get_int_list("attr.ordinals")
     prec = ctx.get_int("output.precision", 3)
+    from .common import field_modes
+    rec = ctx.try_records(modes=field_modes({**{o: "d" for o in kords}, **{a: "n" for a in attrs}}), tail_mode="x",
+                          numeric=True)
+    if rec is not None:
+        _num_distr_native(ctx, rec, kords, attrs, prec)
+        return
     rows = ctx.rows()
     keys = ctx.union(tuple(r[o] for o in kords) for r in rows)
     ki = {k: i for i, k in enumerate(keys)}
@@ -233,6 +351,44 @@ def num_distr_stats(args):
             sd = math.sqrt(max(float(mom[i, 2]) / n - mean * mean, 0.0))
             bins = [f"{(j + int(lo)) * bw:g}{d}{c}" for j, c in enumerate(Hh[i].tolist()) if c]
             out.append(d.join(list(k) + [str(a), f"{bw:g}", str(int(n)), fmt(mean, prec), fmt(sd, prec)] + bins))
+    ctx.emit_root(out)
+
+
+def _num_distr_native(ctx, rec, kords, attrs, prec):
+    """numericalAttrDistrStats on a native token table: global key positions (string order), one
+    [G, B] histogram scatter-add and one moments scatter per attribute, all-reduced."""
+    from ..data.records import sorted_key_tuples
+    g, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], ctx.comm) if kords else \
+        (torch.zeros(rec.n_lines, dtype=torch.long, device=rec.device), 1, torch.zeros((1, 0), dtype=torch.long))
+    g = g.cpu()
+    keys = [tuple(rec.vocab[c] for c in row) for row in ktab.tolist()]
+    d = ctx.delim_out
+    out = []
+    for a in attrs:
+        bw = float(ctx.cfg.values.get(f"attrBinWidth.{a}", ctx.get_float("bin.width", 1.0)))
+        x = rec.field(a, numeric=True).double().cpu()
+        b = torch.floor(x / bw).long()
+        n = x.numel()
+        lo = torch.tensor([int(b.min()) if n else 0])
+        hi = torch.tensor([int(b.max()) if n else 0])
+        if ctx.comm.is_distributed:
+            ctx.comm.all_reduce(lo, "min")
+            ctx.comm.all_reduce(hi, "max")
+        B = int(hi - lo) + 1
+        Hh = torch.zeros(G * B, dtype=torch.long).index_add_(0, g * B + (b - int(lo)), torch.ones_like(b)).view(G, B)
+        mom = torch.zeros((G, 3), dtype=torch.float64)
+        mom[:, 0].index_add_(0, g, torch.ones_like(x))
+        mom[:, 1].index_add_(0, g, x)
+        mom[:, 2].index_add_(0, g, x * x)
+        ctx.all_reduce(Hh, mom)
+        for i, k in enumerate(keys):
+            cnt = float(mom[i, 0])
+            if cnt == 0:
+                continue
+            mean = float(mom[i, 1]) / cnt
+            sd = math.sqrt(max(float(mom[i, 2]) / cnt - mean * mean, 0.0))
+            bins = [f"{(j + int(lo)) * bw:g}{d}{c}" for j, c in enumerate(Hh[i].tolist()) if c]
+            out.append(d.join(list(k) + [str(a), f"{bw:g}", str(int(cnt)), fmt(mean, prec), fmt(sd, prec)] + bins))
     ctx.emit_root(out)
 
 

@@ -139,6 +139,50 @@ def _setup(tmp: Path, name: str, regex: bool):
         cfg = tmp / f"bag_{tag}.properties"
         cfg.write_text(f"bas.batch.size=64\nbas.random.seed=4\nfield.delim.regex={dl}\n")
         return ["baggingSampler", "-i", data], cfg
+    if name in ("nor", "pro", "tef", "tra"):
+        if name == "tef":
+            rng = np.random.default_rng(13)
+            ev = tmp / "tev.txt"
+            ev.write_text("\n".join(f"u{int(rng.integers(0, 7))},{int(rng.integers(0, 4000_000))},x" for _ in range(900))
+                          + "\n")
+            cfg = tmp / f"tef_{tag}.properties"
+            cfg.write_text(f"tef.time.stamp.field.ordinal=1\ntef.time.range=100:2000\ntef.time.stamp.in.mili=true\n"
+                           f"field.delim.regex={dl}\n")
+            return ["temporalFilter", "-i", ev], cfg
+        if name == "tra":
+            import json
+            enc = tmp / "enc.txt"
+            enc.write_text("1,x,10\n1,y,20\n3,p,P!\n")
+            sch = tmp / "tra.json"
+            sch.write_text(json.dumps({"fields": [
+                {"name": "a", "ordinal": 1, "transformers": ["keyValueTrans"], "targetFieldOrdinals": [1, 7]},
+                {"name": "c", "ordinal": 3, "transformers": ["keyValueTrans"]}]}))
+            tconf = tmp / "trans.conf"
+            tconf.write_text(f'transformers {{\n keyValueTrans {{\n  hdfsDataPath = "{enc}"\n  fieldDelim = ","\n }}\n}}\n')
+            cfg = tmp / f"tra_{tag}.properties"
+            cfg.write_text(f"tra.transformer.schema.file.path={sch}\ntra.transformer.config.file.path={tconf}\n"
+                           f"field.delim.regex={dl}\n")
+            return ["transformer", "-i", data], cfg
+        text = {"nor": "nor.num.attribute.ordinals=5,6\nnor.normalizing.strategy=zscore\nnor.force.unit.range=true\n"
+                       "nor.floating.precision=4\n",
+                "pro": "pro.projection.field=0,5,1\npro.select.filter=5 gt 0.5 and 1 in x:y\n"}[name]
+        cfg = tmp / f"{name}_{tag}.properties"
+        cfg.write_text(text + f"field.delim.regex={dl}\n")
+        return [{"nor": "normalizer", "pro": "projection"}[name], "-i", data], cfg
+    if name in ("uvc", "tig", "tig_rep", "nads"):
+        rng = np.random.default_rng(14)
+        ev = tmp / "tev2.txt"
+        ev.write_text("\n".join(f"u{int(rng.integers(0, 9))},{int(rng.integers(0, 400))},{rng.choice(['a', 'B', 'b'])}"
+                                f",{rng.random():.3f}" for _ in range(900)) + "\n")
+        block = {"uvc": ("uniqueValueCounter", "cat.field.ordinals = [1,3]\n count.values = true\n", data),
+                 "tig": ("timeIntervalGenerator", "id.fieldOrdinals = [0]\n time.fieldOrdinal = 1\n", ev),
+                 "tig_rep": ("timeIntervalGenerator", "id.fieldOrdinals = [0]\n time.fieldOrdinal = 1\n"
+                             " time.keepField = false\n", ev),
+                 "nads": ("numericalAttrDistrStats", "id.fieldOrdinals = [1]\n attr.ordinals = [5,6]\n"
+                          " attrBinWidth.5 = 0.1\n bin.width = 0.5\n", data)}[name]
+        conf = tmp / f"{name}_{tag}.conf"
+        conf.write_text(f'{block[0]} {{\n field.delim.in = "{dl}"\n {block[1]}}}\n')
+        return [block[0], "-i", block[2]], conf
     if name == "iim":
         items = tmp / "items.txt"
         rng = np.random.default_rng(2)
@@ -172,7 +216,7 @@ def _setup(tmp: Path, name: str, regex: bool):
 
 
 CASES = ["nuc", "rue", "usb", "abe", "abu", "hash", "loo", "loo_test", "dummy", "dummy_ci", "lmap", "ipca", "spc",
-         "kmc", "ctime", "etd", "iim", "smote", "smote_exp", "relief", "bag"]
+         "kmc", "ctime", "etd", "iim", "smote", "smote_exp", "relief", "bag", "nor", "pro", "tef", "tra", "uvc", "tig", "tig_rep", "nads"]
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -192,7 +236,7 @@ def _world(rank, world, argv, out, cfg):
     return True
 
 
-@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote", "relief", "bag"])
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote", "relief", "bag", "nor", "pro", "tef", "tra", "uvc", "tig", "tig_rep", "nads"])
 def test_world2_equals_world1(tmp_path, name):
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0
