@@ -331,3 +331,34 @@ def test_same_type_similarity_world_invariant(tmp_path, topk):
     assert len(w1) == 100 * (topk or 200)
     run_world(_sts_world, 2, argv, str(tmp_path / "w2"), timeout=300)
     assert _lines(tmp_path / "w2") == w1
+
+
+def _close_lines(a: list[str], b: list[str], rel=1e-4, abs_=2e-3):
+    """Line-by-line equality with numeric fields compared approximately (GPU float math)."""
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        if x == y:
+            continue
+        fx, fy = x.split(","), y.split(",")
+        assert len(fx) == len(fy), (x, y)
+        for u, v in zip(fx, fy):
+            if u != v:
+                assert abs(float(u) - float(v)) <= abs_ + rel * abs(float(v)), (x, y)
+
+
+GPU_CASES = ["rue", "usb", "abe", "abu", "hash", "loo_test", "dummy", "lmap", "spc", "ctime", "etd", "iim", "smote",
+             "relief", "bag", "nor", "pro", "tef", "tra", "uvc", "tig", "nads"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GPU_CASES)
+def test_native_jobs_gpu_equal_cpu(tmp_path, name, monkeypatch):
+    """The device tokenizer (forced on small files) + device kernels against the CPU run."""
+    from avenir_amd.data import records as R
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
+    argv, cfg = _setup(tmp_path, name, False)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "gpu"), "-c", str(cfg), "--device", "cuda"]) == 0
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "cpu"), "-c", str(cfg), "--device", "cpu"]) == 0
+    g, c = _lines(tmp_path / "gpu"), _lines(tmp_path / "cpu")
+    assert c
+    _close_lines(g, c)
