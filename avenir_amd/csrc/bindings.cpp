@@ -2893,6 +2893,10 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
     }
     ring_join(R, stream);
   }
+  // a shard inside ONE file: its lines can be addressed as file offsets (LineSpans.from_file), so
+  // the caller needs no host newline scan of the same bytes for raw-line output
+  const int seg_file = segs.size() == 1 ? segs[0].file : -1;
+  const int64_t seg_off = segs.size() == 1 ? segs[0].file_off : 0;
   sh.reset();
   auto t1 = std::chrono::steady_clock::now();
   const uint8_t* bytes = dev.data_ptr<uint8_t>();
@@ -3019,6 +3023,11 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
   auto t2 = std::chrono::steady_clock::now();
   py::dict stats;
   stats["bytes"] = size;
+  if (seg_file >= 0) {
+    stats["line_file"] = seg_file;
+    stats["line_starts"] = ls + seg_off;
+    stats["line_ends"] = le + seg_off;
+  }
   stats["upload_s"] = std::chrono::duration<double>(t1 - t0).count();
   stats["tokenize_s"] = std::chrono::duration<double>(t2 - t1).count();
   stats["table_slots"] = cap;

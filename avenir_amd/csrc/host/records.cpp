@@ -175,7 +175,7 @@ ByteShard::ByteShard(const std::vector<std::string>& paths, int64_t rank, int64_
         throw std::runtime_error("byte shard: mmap failed for " + paths[f]);
       }
       madvise(m, mlen, MADV_SEQUENTIAL);
-      segs_.push_back({static_cast<const char*>(m) + (a - ma), b - a, m, mlen});
+      segs_.push_back({static_cast<const char*>(m) + (a - ma), b - a, m, mlen, (int)f, a});
       bytes_ += b - a;
     }
     ::close(fd);

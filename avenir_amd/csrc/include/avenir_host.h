@@ -41,6 +41,8 @@ class ByteShard {
     int64_t len;
     void* map;
     size_t map_len;
+    int file = 0;          // index into the constructor's paths
+    int64_t file_off = 0;  // byte offset of p inside that file
   };
   // populate: fault the pages in at map time (host tokenizer); the device upload faults them in
   // from its parallel copy threads instead

@@ -80,6 +80,7 @@ class Records:
     #: (paths, rank, world, skip_header) of the shard, to re-index its raw lines on demand
     _src: tuple | None = None
     _spans: object = None
+    _file_lines: tuple | None = None    # (path, start, end byte offsets) of a device-tokenized shard
 
     @property
     def n_lines(self) -> int:
@@ -190,6 +191,9 @@ class Records:
         the host tokenizer's shard, or — for a device-tokenized table — a host line index of the
         same byte range built on first use (one multi-threaded newline scan, no tokenizing)."""
         from .lines import LineSpans
+        if self._spans is None and self._file_lines is not None:
+            path, starts, ends = self._file_lines
+            self._spans = LineSpans.from_file(path, starts, ends)
         if self._spans is None:
             if self._shard is None and self._src is not None:
                 paths, rank, world, skip = self._src
@@ -209,7 +213,7 @@ class Records:
     def to(self, device) -> "Records":
         mv = lambda t: None if t is None else t.to(device)
         return Records(mv(self.off), mv(self.codes), mv(self.sub), mv(self.nums), self.vocab, self.line_base,
-                       self.stats, self._shard, _src=self._src, _spans=self._spans)
+                       self.stats, self._shard, _src=self._src, _spans=self._spans, _file_lines=self._file_lines)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -235,7 +239,11 @@ def read_records(path, *, comm=None, delims: str = ",", sub_delim: str = "", mod
                 if r is not None:
                     off, codes, sub, nums, vocab, stats = r
                     vb = (stats.pop("vbytes"), stats.pop("voff"), stats.pop("vlen"))
+                    fl = None
+                    if "line_file" in stats:     # the shard lies in one file: lines as file offsets
+                        fl = (paths[int(stats.pop("line_file"))], stats.pop("line_starts"), stats.pop("line_ends"))
                     rec = Records(off, codes, sub, nums, list(vocab), stats=dict(stats, path="device"), vbytes=vb)
+                    rec._file_lines = fl
         if rec is None:
             sh = C.TextShard(paths, rank, world, _threads(), skip_header)
             off, codes, sub, nums, vocab = sh.tokenize(delims, sub_delim, modes, tail_mode, trim, numeric, last_mode)
