@@ -2540,7 +2540,8 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
   py::list cols;
   for (auto& o : outs) cols.append(o);
   // the rows' byte spans in the file (raw-line output of the jobs: data/lines.py)
-  return py::make_tuple(cols, n, bad, total, row_begin, starts, ends);
+  // plus the uploaded file bytes: the device output formatter (format.hip) copies raw lines from them
+  return py::make_tuple(cols, n, bad, total, row_begin, starts, ends, dev);
 }
 
 // K18 GSP self-join: X int32 [N, k] lexicographically sorted unique k-sequences; left rows [lo, hi)
@@ -3023,6 +3024,10 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
   auto t2 = std::chrono::steady_clock::now();
   py::dict stats;
   stats["bytes"] = size;
+  // the uploaded bytes and the lines' spans in them (device output formatter, format.hip)
+  stats["line_buf"] = dev;
+  stats["line_rel_starts"] = ls;
+  stats["line_rel_ends"] = le;
   if (seg_file >= 0) {
     stats["line_file"] = seg_file;
     stats["line_starts"] = ls + seg_off;
@@ -3133,6 +3138,154 @@ py::object format_columns_py(py::list cols_py, int64_t n, const std::string& del
 py::object format_columns_file_py(py::list cols_py, int64_t n, const std::string& delim, int nthreads,
                                   const std::string& path, bool append) {
   return format_columns_impl(cols_py, n, delim, nthreads, &path, append);
+}
+
+// format_device(cols, n, delim, path, append, nthreads, like) -> bytes written, or -1 when a value
+// needs the host formatter (a double outside the exact fixed-point fast path, a precision other
+// than 0..9): the rows are formatted on ``like``'s device (format.hip: length pass, device scan,
+// write pass), copied to pinned host memory once and written by ``nthreads`` pwrite threads.
+// Column tuples as format_columns, with device tensors; raw-line kinds read device line bytes:
+// ("dr" | "drf" | "drt", bytes uint8, start int64 [n], len int64 [n], [field,] from_delims).
+int64_t format_device(py::list cols_py, int64_t n, const std::string& delim, const std::string& path, bool append,
+                      int nthreads, const at::Tensor& like) {
+  CHECK_DEV(like);
+  DevGuard g(like.device());
+  hipStream_t stream = cur_stream(like);
+  auto dopt = like.options();
+  std::vector<avk::DevFmtCol> cols;
+  std::vector<at::Tensor> keep;
+  std::map<PyObject*, std::pair<at::Tensor, at::Tensor>> tables;
+  auto dev_tensor = [&](py::handle h, at::ScalarType st, int64_t len, const char* what) {
+    auto x = h.cast<at::Tensor>().to(like.device()).to(st).contiguous();
+    TORCH_CHECK(x.numel() >= len, "format_device: ", what, " column shorter than required");
+    keep.push_back(x);
+    return x;
+  };
+  auto upload_bytes = [&](const std::string& b) {
+    auto h = at::empty({std::max<int64_t>(1, (int64_t)b.size())}, at::kByte);
+    if (!b.empty()) std::memcpy(h.data_ptr<uint8_t>(), b.data(), b.size());
+    auto d = h.to(like.device());
+    keep.push_back(d);
+    return d;
+  };
+  for (auto item : cols_py) {
+    auto t = item.cast<py::tuple>();
+    const std::string kind = t[0].cast<std::string>();
+    avk::DevFmtCol c;
+    if (kind == "s" || kind == "l" || kind == "lp") {
+      PyObject* key = t[1].ptr();
+      auto hit = tables.find(key);
+      if (hit == tables.end()) {
+        auto strs = t[1].cast<std::vector<std::string>>();
+        std::string cat;
+        std::vector<int64_t> off(strs.size() + 1, 0);
+        for (size_t i = 0; i < strs.size(); ++i) {
+          cat += strs[i];
+          off[i + 1] = (int64_t)cat.size();
+        }
+        auto tb = upload_bytes(cat);
+        auto to = at::from_blob(off.data(), {(int64_t)off.size()}, at::kLong).to(like.device());
+        keep.push_back(to);
+        hit = tables.emplace(key, std::make_pair(tb, to)).first;
+      }
+      c.tbytes = hit->second.first.data_ptr<uint8_t>();
+      c.toff = hit->second.second.data_ptr<int64_t>();
+      c.tV = hit->second.second.numel() - 1;
+      if (kind == "s") {
+        c.kind = avk::DevFmtCol::STR;
+        c.idx = dev_tensor(t[2], at::kInt, n, "string").data_ptr<int32_t>();
+      } else {
+        const bool pairs = kind == "lp";
+        c.kind = pairs ? avk::DevFmtCol::PAIRS : avk::DevFmtCol::LIST;
+        auto off = dev_tensor(t[pairs ? 4 : 3], at::kLong, n + 1, "list offsets");
+        const int64_t m = n ? off[n].item<int64_t>() : 0;
+        c.idx = dev_tensor(t[2], at::kInt, m, "list").data_ptr<int32_t>();
+        if (pairs) c.iv = dev_tensor(t[3], at::kLong, m, "pair list ints").data_ptr<int64_t>();
+        c.off = off.data_ptr<int64_t>();
+      }
+    } else if (kind == "f") {
+      c.kind = avk::DevFmtCol::F64;
+      c.prec = t.size() > 2 ? t[2].cast<int>() : 6;
+      if (c.prec < 0 || c.prec > 9) return -1;  // %g / repr / long fractions: host formatter
+      c.dv = dev_tensor(t[1], at::kDouble, n, "float").data_ptr<double>();
+    } else if (kind == "i") {
+      c.kind = avk::DevFmtCol::I64;
+      c.iv = dev_tensor(t[1], at::kLong, n, "int").data_ptr<int64_t>();
+    } else if (kind == "c" || kind == "g") {
+      c.kind = kind == "c" ? avk::DevFmtCol::LIT : avk::DevFmtCol::GLUE;
+      const std::string lit = t[1].cast<std::string>();
+      c.lit = upload_bytes(lit).data_ptr<uint8_t>();
+      c.litlen = (int)lit.size();
+    } else if (kind == "dr" || kind == "drf" || kind == "drt") {
+      c.kind = kind == "dr" ? avk::DevFmtCol::RAW : (kind == "drf" ? avk::DevFmtCol::FIELD : avk::DevFmtCol::TAIL);
+      auto b = t[1].cast<at::Tensor>();
+      TORCH_CHECK(b.device() == like.device() && b.scalar_type() == at::kByte && b.is_contiguous(),
+                  "format_device: line bytes must be a contiguous uint8 tensor on the device");
+      keep.push_back(b);
+      c.lbytes = b.data_ptr<uint8_t>();
+      auto st = dev_tensor(t[2], at::kLong, n, "line start");
+      auto ln = dev_tensor(t[3], at::kLong, n, "line length");
+      c.lstart = st.data_ptr<int64_t>();
+      c.llen = ln.data_ptr<int64_t>();
+      size_t k = 4;
+      if (kind != "dr") c.field = t[k++].cast<int>();
+      const std::string fd = t.size() > k ? t[k].cast<std::string>() : std::string();
+      for (char ch : fd) c.sep[(uint8_t)ch >> 5] |= 1u << ((uint8_t)ch & 31);
+      c.same = fd.empty() || fd == delim;
+    } else {
+      return -1;   // a kind the device formatter does not handle
+    }
+    cols.push_back(c);
+  }
+  const int ncols = (int)cols.size();
+  auto dcols = at::empty({std::max<int64_t>(1, (int64_t)(ncols * sizeof(avk::DevFmtCol)))}, dopt.dtype(at::kByte));
+  if (ncols)
+    BIND_HIP_CHECK(hipMemcpyAsync(dcols.data_ptr(), cols.data(), ncols * sizeof(avk::DevFmtCol), hipMemcpyHostToDevice,
+                                  stream));
+  auto dl = upload_bytes(delim);
+  const auto* dc = reinterpret_cast<const avk::DevFmtCol*>(dcols.data_ptr());
+  auto len = at::empty({std::max<int64_t>(1, n)}, dopt.dtype(at::kLong));
+  auto bad = at::zeros({1}, dopt.dtype(at::kInt));
+  avk::format_rows_len(dc, ncols, n, dl.data_ptr<uint8_t>(), (int)delim.size(), len.data_ptr<int64_t>(),
+                       bad.data_ptr<int>(), stream);
+  if (bad.item<int>() != 0) return -1;
+  auto lens = len.narrow(0, 0, n);
+  auto cs = n ? lens.cumsum(0) : lens;
+  const int64_t total = n ? cs[n - 1].item<int64_t>() : 0;
+  auto start = (cs - lens).contiguous();
+  auto out = at::empty({std::max<int64_t>(1, total)}, dopt.dtype(at::kByte));
+  avk::format_rows_write(dc, ncols, n, dl.data_ptr<uint8_t>(), (int)delim.size(), start.data_ptr<int64_t>(),
+                         reinterpret_cast<char*>(out.data_ptr<uint8_t>()), stream);
+  auto host = at::empty({std::max<int64_t>(1, total)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  if (total)
+    BIND_HIP_CHECK(hipMemcpyAsync(host.data_ptr(), out.data_ptr(), (size_t)total, hipMemcpyDeviceToHost, stream));
+  BIND_HIP_CHECK(hipStreamSynchronize(stream));
+  {
+    py::gil_scoped_release rel;
+    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | (append ? 0 : O_TRUNC), 0644);
+    if (fd < 0) throw std::runtime_error("cannot open " + path + " for writing");
+    off_t base = append ? ::lseek(fd, 0, SEEK_END) : 0;
+    const int T = total < (16 << 20) ? 1 : std::max(1, std::min(nthreads, 32));
+    std::vector<std::thread> th;
+    std::atomic<bool> failed{false};
+    const char* src = reinterpret_cast<const char*>(host.data_ptr());
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        int64_t a = total * t / T, b = total * (t + 1) / T;
+        while (a < b) {
+          const ssize_t w = ::pwrite(fd, src + a, (size_t)(b - a), (off_t)(base + a));
+          if (w <= 0) {
+            failed = true;
+            return;
+          }
+          a += w;
+        }
+      });
+    for (auto& x : th) x.join();
+    ::close(fd);
+    if (failed) throw std::runtime_error("write failed: " + path);
+  }
+  return total;
 }
 
 // pack_spans(addr int64 [n], len int64 [n], nthreads) -> (bytes uint8 [sum len], off int64 [n + 1]):
@@ -3552,6 +3705,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", &sample);
   m.def("sa_assign", &sa_assign);
   m.def("smote_lines", &smote_lines);
+  m.def("format_device", &format_device);
   m.def("mixed_knn_max_dims", []() { return avk::mixed_knn_max_dims(); });
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);

@@ -353,4 +353,31 @@ void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, flo
                float* gOutHot, float* gInHot, float* cIn_next, long long n_cin, float* cOut_next, long long n_cout,
                hipStream_t stream);
 
+// ---- format.hip: output rows formatted on the device ------------------------------------------
+struct DevFmtCol {
+  enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5, RAW = 6, FIELD = 7, TAIL = 8,
+                    PAIRS = 9 };
+  int kind = STR;
+  int prec = 0;              // F64: fraction digits 0..9
+  int field = 0;             // FIELD / TAIL
+  int same = 0;              // RAW: the separators are the output delimiter (copy as is)
+  const int32_t* idx = nullptr;
+  const int64_t* off = nullptr;
+  const double* dv = nullptr;
+  const int64_t* iv = nullptr;
+  const uint8_t* tbytes = nullptr;  // string table bytes / offsets [tV + 1]
+  const int64_t* toff = nullptr;
+  int64_t tV = 0;
+  const uint8_t* lbytes = nullptr;  // line bytes, per-row start and length
+  const int64_t* lstart = nullptr;
+  const int64_t* llen = nullptr;
+  const uint8_t* lit = nullptr;
+  int litlen = 0;
+  uint32_t sep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+void format_rows_len(const DevFmtCol* cols, int ncols, int64_t n, const uint8_t* delim, int dl, int64_t* len, int* bad,
+                     hipStream_t stream);
+void format_rows_write(const DevFmtCol* cols, int ncols, int64_t n, const uint8_t* delim, int dl, const int64_t* start,
+                       char* out, hipStream_t stream);
+
 }  // namespace avk

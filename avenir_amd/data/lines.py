@@ -28,6 +28,9 @@ class LineSpans(Sequence):
         self._addr = addr
         self._lens = lens
         self._strings = strings
+        # device twin: (uploaded bytes uint8, line start int64, length int64) on the GPU — the same
+        # lines as the host spans, for the device output formatter (format.hip); None otherwise
+        self.dev: tuple | None = None
 
     # -- constructors -----------------------------------------------------------------------------
     @classmethod
@@ -90,11 +93,15 @@ class LineSpans(Sequence):
 
     def column(self, kind: str = "r", field: int | None = None, delims: str = "") -> tuple:
         """A ``format_lines`` column: the whole line (``r``; ``delims`` re-joined with the output
-        delimiter), field ``field`` (``rf``), or the fields from ``field`` on (``rt``)."""
+        delimiter), field ``field`` (``rf``), or the fields from ``field`` on (``rt``).  With a
+        device twin the column also carries the device form (``.dev``) for format.hip."""
         owner, a, n = self.spans()
-        if kind == "r":
-            return ("r", owner, a, n, delims)
-        return (kind, owner, a, n, int(field), delims)
+        col = _Col(("r", owner, a, n, delims) if kind == "r" else (kind, owner, a, n, int(field), delims))
+        if self.dev is not None:
+            buf, st, ln = self.dev
+            col.dev = (("d" + kind, buf, st, ln, delims) if kind == "r" else
+                       ("d" + kind, buf, st, ln, int(field), delims))
+        return col
 
     def __len__(self) -> int:
         return int(self._lens.numel())
@@ -125,7 +132,12 @@ class LineSpans(Sequence):
         if self._strings is not None:
             il = torch.nonzero(idx).view(-1).tolist() if idx.dtype == torch.bool else idx.tolist()
             strings = [self._strings[j] for j in il]
-        return LineSpans(owner, a[idx], n[idx], strings)
+        out = LineSpans(owner, a[idx], n[idx], strings)
+        if self.dev is not None:
+            buf, st, ln = self.dev
+            di = idx.to(st.device)
+            out.dev = (buf, st[di], ln[di])
+        return out
 
     def tolist(self) -> list[str]:
         if self._strings is None:
@@ -138,6 +150,11 @@ class LineSpans(Sequence):
 
     def __eq__(self, other):
         return self.tolist() == list(other)
+
+
+class _Col(tuple):
+    """A format column tuple that may carry its device form (``dev``)."""
+    dev = None
 
 
 class _FileSpans(LineSpans):

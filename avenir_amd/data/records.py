@@ -81,6 +81,7 @@ class Records:
     _src: tuple | None = None
     _spans: object = None
     _file_lines: tuple | None = None    # (path, start, end byte offsets) of a device-tokenized shard
+    _dev_lines: tuple | None = None     # (uploaded bytes, line starts, lengths) on the device
 
     @property
     def n_lines(self) -> int:
@@ -208,12 +209,15 @@ class Records:
                 self._spans = LineSpans.from_shard(self._shard)
             if len(self._spans) != self.n_lines:
                 raise RuntimeError("line index does not match the token table")
+            if self._dev_lines is not None and self._spans.dev is None:
+                self._spans.dev = self._dev_lines
         return self._spans
 
     def to(self, device) -> "Records":
         mv = lambda t: None if t is None else t.to(device)
         return Records(mv(self.off), mv(self.codes), mv(self.sub), mv(self.nums), self.vocab, self.line_base,
-                       self.stats, self._shard, _src=self._src, _spans=self._spans, _file_lines=self._file_lines)
+                       self.stats, self._shard, _src=self._src, _spans=self._spans, _file_lines=self._file_lines,
+                       _dev_lines=self._dev_lines)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -242,8 +246,10 @@ def read_records(path, *, comm=None, delims: str = ",", sub_delim: str = "", mod
                     fl = None
                     if "line_file" in stats:     # the shard lies in one file: lines as file offsets
                         fl = (paths[int(stats.pop("line_file"))], stats.pop("line_starts"), stats.pop("line_ends"))
+                    dl = (stats.pop("line_buf"), stats.pop("line_rel_starts"), stats.pop("line_rel_ends"))
                     rec = Records(off, codes, sub, nums, list(vocab), stats=dict(stats, path="device"), vbytes=vb)
                     rec._file_lines = fl
+                    rec._dev_lines = (dl[0], dl[1], dl[2] - dl[1])
         if rec is None:
             sh = C.TextShard(paths, rank, world, _threads(), skip_header)
             off, codes, sub, nums, vocab = sh.tokenize(delims, sub_delim, modes, tail_mode, trim, numeric, last_mode)
@@ -367,6 +373,11 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",", path: str | None =
     C = _native.host()
     if C is not None:
         if path is not None:
+            dcols = _device_columns(cols, n)
+            if dcols is not None:     # rows formatted on the GPU (format.hip), written by host threads
+                w = C.format_device(dcols[0], int(n), delim, str(path), bool(append), _threads(), dcols[1])
+                if w >= 0:
+                    return w
             return C.format_columns_file(cols, int(n), delim, _threads(), str(path), bool(append))
         return C.format_columns(cols, int(n), delim, _threads())
     if path is not None:
@@ -439,6 +450,43 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",", path: str | None =
         else:
             out.append(glue_pre[r] + "\n")
     return "".join(out).encode()
+
+
+#: rows from which ``format_lines`` formats on the GPU when every column is device-resident
+DEVICE_FORMAT_MIN_ROWS = int(os.environ.get("AVMI_DEVICE_FORMAT_MIN_ROWS", str(1 << 18)))
+
+
+def _device_columns(cols: list, n: int):
+    """(device column tuples, a device tensor) when every column can be formatted on the GPU
+    (tensors already on a GPU, raw-line columns with a device twin, literals, string tables), at
+    least one column is device data and ``n`` is large enough; else None."""
+    if n < DEVICE_FORMAT_MIN_ROWS or os.environ.get("AVMI_DEVICE_FORMAT", "1") == "0":
+        return None
+    out, like = [], None
+    for c in cols:
+        k = c[0]
+        if k in ("c", "g"):
+            out.append(c)
+            continue
+        if k in ("r", "rf", "rt"):
+            d = getattr(c, "dev", None)
+            if d is None:
+                return None
+            out.append(d)
+            like = d[1]
+            continue
+        if k == "f" and not (len(c) > 2 and 0 <= int(c[2]) <= 9):
+            return None
+        tens = {"s": [2], "l": [2, 3], "lp": [2, 3, 4], "f": [1], "i": [1]}.get(k)
+        if tens is None:
+            return None
+        for j in tens:
+            t = c[j]
+            if not (isinstance(t, torch.Tensor) and t.is_cuda):
+                return None
+            like = t
+        out.append(c)
+    return (out, like) if like is not None else None
 
 
 # ------------------------------------------------------------------------------------------------

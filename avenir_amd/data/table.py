@@ -449,8 +449,8 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     if any(sp[1] not in (CAT, BUCKET, FLOAT) for sp in specs):
         return None
     like = torch.empty(0, device=dev)
-    cols, n, _bad, _total, r0, starts, ends = C.csv_parse_device(str(path), specs, _literal(delim or ","),
-                                                                 skip_header, int(rank), int(world), like)
+    cols, n, _bad, _total, r0, starts, ends, fbytes = C.csv_parse_device(str(path), specs, _literal(delim or ","),
+                                                                         skip_header, int(rank), int(world), like)
     ld = pad16(n)
     cdt = torch.uint16 if wide else torch.uint8
     codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned
@@ -468,6 +468,7 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     if keep_lines:
         from .lines import LineSpans
         lines = LineSpans.from_file(str(path), starts, ends)
+        lines.dev = (fbytes, starts, ends - starts)      # the device formatter reads the uploaded bytes
     return Table(schema, n, codes, binned, num, numeric, labels, cls_f, ids, lines, r0, meta={"parser": "device"})
 
 

@@ -90,9 +90,9 @@ def nb_predict(args):
         return
     r = nb.predict(t)
     prob = r.prob.max(1).values if r.prob is not None else torch.ones(t.n, device=r.pred.device)
-    pred = r.pred.int().cpu()
+    pred = r.pred.int()          # device tensors: the device formatter writes the rows (format.hip)
     cols = [t.lines.column("r"), ("s", list(vals), pred) if vals else ("i", pred.long()),
-            ("f", prob.double().cpu(), 3)]
+            ("f", prob.double(), 3)]
     ctx.emit_columns(cols, t.n)
     if r.confusion is not None:
         conf = r.confusion.clone()
@@ -147,7 +147,7 @@ def dec_tree(args):
     _, first = DecisionPathModel(js).predict_proba_cols(TableColumns(t))
     pd = ctx.get_str("dec.path.delim", ";")
     paths = [pd.join(pr["predicateStr"] for pr in dp["predicates"]) for dp in js["decisionPaths"]] + ["$root"]
-    first = torch.where(first >= 0, first, torch.full_like(first, len(paths) - 1)).int().cpu()
+    first = torch.where(first >= 0, first, torch.full_like(first, len(paths) - 1)).int()
     ctx.emit_columns([("s", paths, first), t.lines.column("r")], t.n)
     ctx.report({"level": grown, "done": grown <= depth or grown >= limit})
 
@@ -205,7 +205,7 @@ def knn(args):
         nn.fit((Xtr - lo) / scale, y, tr.n_classes, index_base=tr.row_offset)
         res = nn.predict((Xte - lo) / scale, q_base=te.row_offset)
     vals = te.class_field.cardinality
-    ctx.emit_columns([te.lines.column("r"), ("s", list(vals), res.pred.int().cpu())], te.n)
+    ctx.emit_columns([te.lines.column("r"), ("s", list(vals), res.pred.int())], te.n)
 
 
 def _numeric_block(t) -> torch.Tensor:
@@ -673,14 +673,14 @@ def viterbi(args):
     path, _ = ViterbiDecoder(hmm).decode(obs.to(ctx.device))
     ok = path >= 0
     cnt = ok.sum(1).long()
-    off = torch.cat([cnt.new_zeros(1), torch.cumsum(cnt, 0)]).cpu()
+    off = torch.cat([cnt.new_zeros(1), torch.cumsum(cnt, 0)])
     S = len(hmm.states)
     if state_only:
         table, idx = hmm.states, path[ok]
     else:   # obs<sub>state tokens: one table entry per (observation, state) pair
         table = [f"{o}{sub}{st}" for o in hmm.observations for st in hmm.states]
         idx = obs.to(path.device).long()[ok] * S + path[ok]
-    cols = [rec.line_spans().column("rf", id_ord, lit), ("l", table, idx.int().cpu(), off)]
+    cols = [rec.line_spans().column("rf", id_ord, lit), ("l", table, idx.int(), off)]
     ctx.emit_columns(cols, rec.n_lines)
 
 

@@ -618,7 +618,7 @@ def model_predictor(args):
         votes.scatter_add_(1, win.view(-1, 1), torch.full((n, 1), float(w), dtype=torch.float64, device=rec.device))
     pred = votes.argmax(1)
     spans = rec.line_spans()
-    pcol = ("s", list(classes), pred.int().cpu())
+    pcol = ("s", list(classes), pred.int())
     if mode == "withKId":
         cols = [spans.column("rf", id_o, lit), pcol]
     elif mode == "withActualClassAttr":

@@ -356,6 +356,7 @@ def test_native_jobs_gpu_equal_cpu(tmp_path, name, monkeypatch):
     """The device tokenizer (forced on small files) + device kernels against the CPU run."""
     from avenir_amd.data import records as R
     monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
+    monkeypatch.setattr(R, "DEVICE_FORMAT_MIN_ROWS", 0)
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "gpu"), "-c", str(cfg), "--device", "cuda"]) == 0
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "cpu"), "-c", str(cfg), "--device", "cpu"]) == 0

@@ -176,6 +176,7 @@ def _close(a: list[str], b: list[str], rel=1e-4, abs_=2e-3):
 @pytest.mark.parametrize("name", CASES)
 def test_native_predictors_gpu_equal_cpu(tmp_path, name, monkeypatch):
     monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)        # device tokenizer on small files too
+    monkeypatch.setattr(R, "DEVICE_FORMAT_MIN_ROWS", 0)  # device output formatter too
     monkeypatch.setattr(TB, "_GPU_CSV_MIN_BYTES", 0)     # device CSV parser too
     argv, text = _setup(tmp_path, name)
     cfg = _cfg(tmp_path, text)
