@@ -89,6 +89,10 @@ def distance_store(args):
     (``eds.pair.input=true``, e.g. sameTypeSimilarity / recordSimilarity output)."""
     from ..utils.distance_store import EntityDistanceStore
     ctx = JobContext(args, "eds.")
+    if ctx.get_bool("pair.input", False) and ctx.native_delim() is not None:
+        rec = ctx.records(shard=False, modes="ddn", tail_mode="x", numeric=True)
+        EntityDistanceStore.write_codes(rec.field(0), rec.field(1), rec.field(2, numeric=True), rec.vocab, args.output)
+        return
     lines = ctx.all_lines()
     if ctx.get_bool("pair.input", False):
         rows = [ctx.split(l) for l in lines]

@@ -57,6 +57,43 @@ class EntityDistanceStore:
         return EntityDistanceStore.write_rows(rows, path)
 
     @staticmethod
+    def write_codes(src: "torch.Tensor", dst: "torch.Tensor", dist: "torch.Tensor", vocab: list[str], path: str | Path,
+                    symmetric: bool = True) -> "EntityDistanceStore":
+        """``write_pairs`` from dictionary codes (a native token table): entities are the vocabulary
+        entries that occur, in string order; the CSR rows come from one stable sort of the (row,
+        column) pairs — the same store as ``write_pairs`` without a Python object per pair."""
+        import torch
+        src, dst, dist = src.long().cpu(), dst.long().cpu(), dist.double().cpu()
+        if symmetric:
+            a = torch.stack([src, dst], 1).reshape(-1)
+            b = torch.stack([dst, src], 1).reshape(-1)
+            w = torch.stack([dist, dist], 1).reshape(-1)
+        else:
+            a, b, w = src, dst, dist
+        used = torch.zeros(max(1, len(vocab)), dtype=torch.bool)
+        used[a] = True
+        used[b] = True
+        ids = torch.nonzero(used).view(-1).tolist()
+        order = sorted(ids, key=lambda c: vocab[c])
+        ents = [vocab[c] for c in order]
+        rank = torch.full((max(1, len(vocab)),), -1, dtype=torch.long)
+        rank[torch.tensor(order, dtype=torch.long)] = torch.arange(len(order))
+        ra, rb = rank[a], rank[b]
+        o = torch.argsort(rb, stable=True)
+        o = o[torch.argsort(ra[o], stable=True)]
+        ra, rb, w = ra[o], rb[o], w[o]
+        indptr = torch.zeros(len(ents) + 1, dtype=torch.long)
+        if ra.numel():
+            indptr[1:] = torch.cumsum(torch.bincount(ra, minlength=len(ents)), 0)
+        p = Path(path)
+        p.mkdir(parents=True, exist_ok=True)
+        np.save(p / "indptr.npy", indptr.numpy())
+        np.save(p / "cols.npy", rb.numpy().astype(np.int64))
+        np.save(p / "vals.npy", w.numpy().astype(np.float64))
+        (p / "entities.json").write_text(json.dumps(ents))
+        return EntityDistanceStore(p)
+
+    @staticmethod
     def write_rows(rows: dict[str, list[tuple[str, float]]], path: str | Path) -> "EntityDistanceStore":
         p = Path(path)
         p.mkdir(parents=True, exist_ok=True)

@@ -363,3 +363,23 @@ def test_native_jobs_gpu_equal_cpu(tmp_path, name, monkeypatch):
     g, c = _lines(tmp_path / "gpu"), _lines(tmp_path / "cpu")
     assert c
     _close_lines(g, c)
+
+
+def test_distance_store_native_equals_python(tmp_path):
+    """entityDistanceStore from pair lines: the code-based CSR build equals write_pairs."""
+    import numpy as np
+    from avenir_amd.utils.distance_store import EntityDistanceStore
+    rng = np.random.default_rng(2)
+    pairs = [(f"e{int(rng.integers(0, 60))}", f"e{int(rng.integers(0, 60))}", float(rng.integers(1, 999)))
+             for _ in range(700)]
+    inp = tmp_path / "pairs.txt"
+    inp.write_text("\n".join(f"{a},{b},{int(d)}" for a, b, d in pairs) + "\n")
+    cfg = tmp_path / "eds.properties"
+    cfg.write_text("eds.pair.input=true\n")
+    assert main(["entityDistanceStore", "-i", str(inp), "-o", str(tmp_path / "native"), "-c", str(cfg),
+                 "--device", "cpu"]) == 0
+    EntityDistanceStore.write_pairs([a for a, _, _ in pairs], [b for _, b, _ in pairs], [d for _, _, d in pairs],
+                                    tmp_path / "py")
+    for f in ("indptr.npy", "cols.npy", "vals.npy"):
+        assert np.array_equal(np.load(tmp_path / "native" / f), np.load(tmp_path / "py" / f)), f
+    assert (tmp_path / "native" / "entities.json").read_text() == (tmp_path / "py" / "entities.json").read_text()
