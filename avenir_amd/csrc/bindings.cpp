@@ -3140,6 +3140,46 @@ py::object format_columns_file_py(py::list cols_py, int64_t n, const std::string
   return format_columns_impl(cols_py, n, delim, nthreads, &path, append);
 }
 
+// pairs_within(A f32 [nA, D], B f32 [nB, D], nf, scale, thr, tri, a_base, b_base) -> (I, J, dist):
+// the pairs with round(|a - b| / nf * scale) <= thr (j > i in global order when ``tri``), sorted by
+// (i, j).  Counts first into a buffer sized from an estimate, re-runs once when it overflows.
+py::tuple pairs_within(const at::Tensor& A, const at::Tensor& B, double nf, double scale, double thr, bool tri,
+                       int64_t a_base, int64_t b_base) {
+  CHECK_DEV(A);
+  CHECK_DEV(B);
+  CHECK_DTYPE(A, at::kFloat);
+  CHECK_DTYPE(B, at::kFloat);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1) && A.is_contiguous() && B.is_contiguous(),
+              "pairs_within: A [nA, D], B [nB, D] contiguous");
+  TORCH_CHECK(A.size(1) >= 1 && A.size(1) <= 64, "pairs_within: 1 <= D <= 64");
+  TORCH_CHECK(A.size(0) < (1LL << 31) && B.size(0) < (1LL << 31), "pairs_within: too many rows");
+  DevGuard g(A.device());
+  hipStream_t stream = cur_stream(A);
+  const int nA = (int)A.size(0), nB = (int)B.size(0), D = (int)A.size(1);
+  auto cnt = at::zeros({1}, A.options().dtype(at::kInt));
+  long long cap = std::max<long long>(1 << 20, ((long long)nA + nB) * 4);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    auto I = at::empty({cap}, A.options().dtype(at::kLong));
+    auto J = at::empty({cap}, A.options().dtype(at::kLong));
+    auto Dd = at::empty({cap}, A.options().dtype(at::kInt));
+    const long long found = avk::pairs_within(A.data_ptr<float>(), nA, B.data_ptr<float>(), nB, D, (float)nf,
+                                              (float)scale, (float)thr, tri ? 1 : 0, a_base, b_base,
+                                              cnt.data_ptr<int>(), cap,
+                                              reinterpret_cast<long long*>(I.data_ptr<int64_t>()),
+                                              reinterpret_cast<long long*>(J.data_ptr<int64_t>()), Dd.data_ptr<int>(),
+                                              stream);
+    TORCH_CHECK(found >= 0 && found < (1LL << 31) - 1, "pairs_within: pair count overflows int32");
+    if (found <= cap) {
+      auto i = I.narrow(0, 0, found), j = J.narrow(0, 0, found), d = Dd.narrow(0, 0, found);
+      auto order = (i * (int64_t)std::max(nB, 1) + j).argsort();
+      return py::make_tuple(i.index({order}), j.index({order}), d.index({order}).to(at::kLong));
+    }
+    cap = found;
+  }
+  TORCH_CHECK(false, "pairs_within: pair buffer overflow after resize");
+  return py::make_tuple();
+}
+
 // format_device(cols, n, delim, path, append, nthreads, like) -> bytes written, or -1 when a value
 // needs the host formatter (a double outside the exact fixed-point fast path, a precision other
 // than 0..9): the rows are formatted on ``like``'s device (format.hip: length pass, device scan,
@@ -3706,6 +3746,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sa_assign", &sa_assign);
   m.def("smote_lines", &smote_lines);
   m.def("format_device", &format_device);
+  m.def("pairs_within", &pairs_within);
   m.def("mixed_knn_max_dims", []() { return avk::mixed_knn_max_dims(); });
   m.def("glm_gradient", &glm_gradient);
   m.def("smo_solve", &smo_solve);

@@ -353,6 +353,10 @@ void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, flo
                float* gOutHot, float* gInHot, float* cIn_next, long long n_cin, float* cOut_next, long long n_cout,
                hipStream_t stream);
 
+// ---- distance.hip: threshold pairs (recordSimilarity) ----------------------------------------
+long long pairs_within(const float* A, int nA, const float* B, int nB, int D, float nf, float scale, float thr, int tri,
+                       long long a_base, long long b_base, int* cnt, long long cap, long long* outI, long long* outJ,
+                       int* outD, hipStream_t stream);
 // ---- format.hip: output rows formatted on the device ------------------------------------------
 struct DevFmtCol {
   enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5, RAW = 6, FIELD = 7, TAIL = 8,

@@ -518,6 +518,54 @@ __global__ __launch_bounds__(MX_T) void mixed_knn_merge_kernel(const float* __re
   }
 }
 
+
+// ---- pairs within a distance threshold (recordSimilarity) ---------------------------
+// The job keeps (i, j) pairs whose scaled, rounded euclidean distance round(sqrt(|a-b|^2) / nf *
+// scale) is at most ``thr`` (and j > i in global order for a self-join).  Instead of materialising
+// [tile, nB] distance blocks and compacting them with a sort / nonzero per tile, each workgroup
+// holds 64 A rows in LDS, each lane one B row in registers, and the kept pairs are appended with
+// one atomic per pair (the host sorts them by (i, j) afterwards: deterministic output).
+template <int DMAX>
+__global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restrict__ A, int nA,
+                                                           const float* __restrict__ B, int nB, int D, float nf,
+                                                           float scale, float thr, int tri, long long a_base,
+                                                           long long b_base, int* __restrict__ cnt, long long cap,
+                                                           long long* __restrict__ outI, long long* __restrict__ outJ,
+                                                           int* __restrict__ outD) {
+  __shared__ float As[64][DMAX + 1];
+  const int a0 = blockIdx.y * 64;
+  for (int e = threadIdx.x; e < 64 * D; e += 256) {
+    const int r = e / D, c = e - r * D;
+    As[r][c] = a0 + r < nA ? A[(long long)(a0 + r) * D + c] : 0.f;
+  }
+  __syncthreads();
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= nB) return;
+  float b[DMAX];
+#pragma unroll
+  for (int c = 0; c < DMAX; ++c) b[c] = c < D ? B[(long long)j * D + c] : 0.f;
+  const int na = min(64, nA - a0);
+  const long long gj = b_base + j;
+  for (int r = 0; r < na; ++r) {
+    if (tri && gj <= a_base + a0 + r) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < DMAX; ++c) {
+      const float d = As[r][c] - b[c];   // zero beyond D on both sides
+      s = fmaf(d, d, s);
+    }
+    const float dist = rintf(sqrtf(s) / nf * scale);   // torch.round: half to even
+    if (dist <= thr) {
+      const int k = atomicAdd(cnt, 1);
+      if ((long long)k < cap) {
+        outI[k] = a0 + r;
+        outJ[k] = j;
+        outD[k] = (int)dist;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -618,6 +666,30 @@ void cluster_accumulate(const float* X, long long N, int D, const int* assign, i
   cluster_accum_kernel<<<av::stream_grid(N, KT, 8, 2048), KT, use_lds ? lds : 0, stream>>>(
       X, N, D, assign, K, sums, counts, use_lds);
   AV_HIP_CHECK(hipGetLastError());
+}
+
+
+// pairs (i, j) with round(|a_i - b_j| / nf * scale) <= thr; returns the number found (the first
+// ``cap`` are written; the caller re-runs with a larger buffer when it exceeds cap)
+long long pairs_within(const float* A, int nA, const float* B, int nB, int D, float nf, float scale, float thr, int tri,
+                       long long a_base, long long b_base, int* cnt, long long cap, long long* outI, long long* outJ,
+                       int* outD, hipStream_t stream) {
+  if (nA <= 0 || nB <= 0) return 0;
+  if (D < 1 || D > 64) throw std::runtime_error("pairs_within: 1 <= D <= 64");
+  AV_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), stream));
+  const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((nA + 63) / 64));
+#define AV_PW(DM) \
+  pairs_within_kernel<DM><<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, tri, a_base, b_base, cnt, cap, outI, outJ, outD)
+  if (D <= 8) AV_PW(8);
+  else if (D <= 16) AV_PW(16);
+  else if (D <= 32) AV_PW(32);
+  else AV_PW(64);
+#undef AV_PW
+  AV_HIP_CHECK(hipGetLastError());
+  int h = 0;
+  AV_HIP_CHECK(hipMemcpyAsync(&h, cnt, sizeof(int), hipMemcpyDeviceToHost, stream));
+  AV_HIP_CHECK(hipStreamSynchronize(stream));
+  return h;
 }
 
 }  // namespace avk

@@ -6,11 +6,13 @@ from __future__ import annotations
 import itertools
 import json
 import math
+import os
 from collections import defaultdict
 from pathlib import Path
 
 import torch
 
+from .. import _native
 from .common import JobContext, field_modes, fmt, job
 
 
@@ -962,6 +964,8 @@ def record_similarity(args):
                boff.to(cdev)]
     nf = math.sqrt(max(len(ords), 1))
     tile = max(1, min(4096, (1 << 26) // max(1, NB // max(1, comm.world))))
+    fused = (dev.type == "cuda" and math.isfinite(thr) and 1 <= len(ords) <= 64
+             and os.environ.get("AVMI_RS_FUSED", "1") != "0")
     I, J, Dv, H = [], [], [], []
     blocks = []
     for h, (owner, (Bc, bbase, bb, bo)) in enumerate(comm.ring_iter(payload)):
@@ -969,6 +973,17 @@ def record_similarity(args):
         b0 = int(bbase.cpu()[0]) if bbase.numel() else 0
         blocks.append(LineSpans.from_packed(bb, bo))
         nb = Bc.shape[0]
+        if fused and nb and A.shape[0]:
+            # GPU: one fused distance + threshold + append launch per hop (distance.hip
+            # pairs_within_kernel), pairs sorted by (i, j) — no [tile, nB] distance blocks
+            qi, jj, dd = _native.C().pairs_within(A.contiguous(), Bc.float().contiguous(), nf, scale, thr, rB is None,
+                                                  int(a_base), int(b0))
+            if qi.numel():
+                I.append(qi)
+                J.append(jj + b0)
+                Dv.append(dd)
+                H.append(torch.full_like(jj, h) * (1 << 40) + jj)
+            continue
         for s in range(0, A.shape[0], tile):
             e = min(A.shape[0], s + tile)
             if nb == 0:

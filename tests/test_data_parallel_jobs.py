@@ -172,3 +172,30 @@ def test_world_invariant_and_byte_range_reads(tmp_path, name, world):
     total = os.path.getsize(data) + (os.path.getsize(argv[argv.index("--train") + 1]) if "--train" in argv else 0)
     assert sum(read) == total                      # every input byte read exactly once
     assert max(read) <= total / world * 1.1 + 200  # each rank about its share
+
+
+@pytest.mark.gpu
+def test_record_similarity_fused_kernel_matches_tiles(cuda, tmp_path, monkeypatch):
+    """recordSimilarity on the GPU: the fused threshold-pair kernel (pairs_within) against the
+    tiled torch path on the same device — same pairs, distances within one unit (sqrt-of-sum vs
+    the library cdist rounding at .5 boundaries), pairs at the threshold edge may differ."""
+    import numpy as np
+    from avenir_amd.cli import main
+    rng = np.random.default_rng(5)
+    X = rng.random((3000, 8))
+    data = tmp_path / "rs.csv"
+    data.write_text("\n".join(f"r{i}," + ",".join(f"{v:.5f}" for v in row) for i, row in enumerate(X)) + "\n")
+    cfg = tmp_path / "rs.properties"
+    cfg.write_text("resi.attr.ordinals=1,2,3,4,5,6,7,8\nresi.id.ordinal=0\nresi.distance.scale=1000\n"
+                   "resi.dist.threshold=120\n")
+    outs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("AVMI_RS_FUSED", fused)
+        out = tmp_path / f"o{fused}.txt"
+        assert main(["recordSimilarity", "-i", str(data), "-o", str(out), "-c", str(cfg), "--device", "cuda"]) == 0
+        outs[fused] = {tuple(l.split(",")[:2]): int(l.split(",")[2]) for l in out.read_text().split()}
+    a, b = outs["1"], outs["0"]
+    common = set(a) & set(b)
+    assert len(common) >= 0.99 * max(len(a), len(b)) and len(a) > 100
+    assert all(abs(a[k] - b[k]) <= 1 for k in common)
+    assert all(v >= 119 for k, v in a.items() if k not in b) and all(v >= 119 for k, v in b.items() if k not in a)

@@ -362,3 +362,30 @@ def test_mixed_knn_kernel_matches_cpu(cuda):
         # neighbour sets agree wherever distances are not tied
         ok = (dc[:, 1:] - dc[:, :-1]).abs().min(1).values > 1e-4 if k > 1 else torch.ones(dc.shape[0], dtype=torch.bool)
         assert torch.equal(ig.cpu()[ok], ic[ok])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [3, 8, 20, 64])
+def test_pairs_within_kernel_vs_fp64(cuda, D):
+    """distance.hip pairs_within_kernel: every pair with round(|a - b| / nf * scale) <= thr (and
+    j > i in global order for a self-join), sorted by (i, j), against an fp64 brute force."""
+    import math
+    from avenir_amd import _native
+    g = torch.Generator().manual_seed(D)
+    A, B = torch.rand(700, D, generator=g), torch.rand(900, D, generator=g)
+    nf, scale = math.sqrt(D), 1000.0
+    ref = torch.round(torch.cdist(A.double(), B.double()) / nf * scale)
+    thr = float(torch.quantile(ref.flatten(), 0.01))
+    for tri, a_base, b_base in ((False, 0, 0), (True, 100, 50)):
+        i, j, d = _native.C().pairs_within(A.to(cuda), B.to(cuda), nf, scale, thr, tri, a_base, b_base)
+        i, j, d = i.cpu(), j.cpu(), d.cpu()
+        keep = ref <= thr
+        if tri:
+            keep &= (torch.arange(900).view(1, -1) + b_base) > (torch.arange(700).view(-1, 1) + a_base)
+        ri, rj = torch.nonzero(keep, as_tuple=True)
+        got = set(zip(i.tolist(), j.tolist()))
+        exp = set(zip(ri.tolist(), rj.tolist()))
+        assert (i * 900 + j).diff().gt(0).all()                 # sorted by (i, j)
+        assert len(got ^ exp) <= 0.002 * len(exp) + 2           # fp32 vs fp64 at the threshold edge
+        for a, b, dd in zip(i.tolist()[:500], j.tolist()[:500], d.tolist()[:500]):
+            assert abs(dd - ref[a, b]) <= 1
