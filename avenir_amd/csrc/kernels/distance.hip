@@ -531,9 +531,9 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
                                                            float scale, float thr, int tri, long long a_base,
                                                            long long b_base, int* __restrict__ cnt, long long cap,
                                                            long long* __restrict__ outI, long long* __restrict__ outJ,
-                                                           int* __restrict__ outD) {
+                                                           int* __restrict__ outD, int a_row0) {
   __shared__ float As[64][DMAX + 1];
-  const int a0 = blockIdx.y * 64;
+  const int a0 = a_row0 + blockIdx.y * 64;
   for (int e = threadIdx.x; e < 64 * D; e += 256) {
     const int r = e / D, c = e - r * D;
     As[r][c] = a0 + r < nA ? A[(long long)(a0 + r) * D + c] : 0.f;
@@ -677,14 +677,20 @@ long long pairs_within(const float* A, int nA, const float* B, int nB, int D, fl
   if (nA <= 0 || nB <= 0) return 0;
   if (D < 1 || D > 64) throw std::runtime_error("pairs_within: 1 <= D <= 64");
   AV_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), stream));
-  const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((nA + 63) / 64));
-#define AV_PW(DM) \
-  pairs_within_kernel<DM><<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, tri, a_base, b_base, cnt, cap, outI, outJ, outD)
-  if (D <= 8) AV_PW(8);
-  else if (D <= 16) AV_PW(16);
-  else if (D <= 32) AV_PW(32);
-  else AV_PW(64);
+  // grid.y is capped at 65535 workgroups: A is covered in row chunks of 64 x 65535
+  const int CH = 64 * 65535;
+  for (int a_row0 = 0; a_row0 < nA; a_row0 += CH) {
+    const int rows = std::min(CH, nA - a_row0);
+    const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((rows + 63) / 64));
+#define AV_PW(DM)                                                                                                  \
+  pairs_within_kernel<DM><<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, tri, a_base, b_base, cnt, cap, \
+                                                    outI, outJ, outD, a_row0)
+    if (D <= 8) AV_PW(8);
+    else if (D <= 16) AV_PW(16);
+    else if (D <= 32) AV_PW(32);
+    else AV_PW(64);
 #undef AV_PW
+  }
   AV_HIP_CHECK(hipGetLastError());
   int h = 0;
   AV_HIP_CHECK(hipMemcpyAsync(&h, cnt, sizeof(int), hipMemcpyDeviceToHost, stream));
