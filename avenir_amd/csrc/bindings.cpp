@@ -3302,28 +3302,7 @@ int64_t format_device(py::list cols_py, int64_t n, const std::string& delim, con
   BIND_HIP_CHECK(hipStreamSynchronize(stream));
   {
     py::gil_scoped_release rel;
-    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | (append ? 0 : O_TRUNC), 0644);
-    if (fd < 0) throw std::runtime_error("cannot open " + path + " for writing");
-    off_t base = append ? ::lseek(fd, 0, SEEK_END) : 0;
-    const int T = total < (16 << 20) ? 1 : std::max(1, std::min(nthreads, 32));
-    std::vector<std::thread> th;
-    std::atomic<bool> failed{false};
-    const char* src = reinterpret_cast<const char*>(host.data_ptr());
-    for (int t = 0; t < T; ++t)
-      th.emplace_back([&, t] {
-        int64_t a = total * t / T, b = total * (t + 1) / T;
-        while (a < b) {
-          const ssize_t w = ::pwrite(fd, src + a, (size_t)(b - a), (off_t)(base + a));
-          if (w <= 0) {
-            failed = true;
-            return;
-          }
-          a += w;
-        }
-      });
-    for (auto& x : th) x.join();
-    ::close(fd);
-    if (failed) throw std::runtime_error("write failed: " + path);
+    avh::write_file_parallel(path, append, {{reinterpret_cast<const char*>(host.data_ptr()), total}}, nthreads);
   }
   return total;
 }

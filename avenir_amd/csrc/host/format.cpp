@@ -11,6 +11,8 @@
 #include <array>
 #include <atomic>
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <algorithm>
 #include <unistd.h>
 #include <thread>
 
@@ -334,36 +336,73 @@ namespace avh {
 // format_columns straight into a file (created / truncated, or appended to): every thread formats
 // its block of rows, then writes it with pwrite at its offset — no concatenated copy, no Python
 // bytes object.  Returns the bytes written.
-int64_t format_columns_to_file(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads,
-                               const std::string& path, bool append) {
-  std::vector<std::string> parts = format_parts(cols, n, delim, nthreads);
-  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | (append ? 0 : O_TRUNC), 0644);
+int64_t write_file_parallel(const std::string& path, bool append,
+                            const std::vector<std::pair<const char*, int64_t>>& parts, int nthreads) {
+  int64_t total = 0;
+  for (auto& p : parts) total += p.second;
+  const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | (append ? 0 : O_TRUNC), 0644);
   if (fd < 0) throw std::runtime_error("cannot open " + path + " for writing");
-  off_t base = 0;
-  if (append) base = ::lseek(fd, 0, SEEK_END);
-  std::vector<int64_t> off(parts.size() + 1, 0);
-  for (size_t t = 0; t < parts.size(); ++t) off[t + 1] = off[t] + (int64_t)parts[t].size();
-  std::vector<std::thread> th;
-  std::atomic<bool> bad{false};
-  for (size_t t = 0; t < parts.size(); ++t)
-    th.emplace_back([&, t] {
-      const char* p = parts[t].data();
-      int64_t left = (int64_t)parts[t].size(), at = base + off[t];
+  const off_t base = append ? ::lseek(fd, 0, SEEK_END) : 0;
+  bool done = false;
+  if (total >= (8 << 20)) {
+    // large outputs: size the file once and copy into a shared mapping from several threads —
+    // page-cache writes through write()/pwrite() serialise on the file's inode lock, page faults on
+    // a mapping do not
+    const int64_t page = (int64_t)sysconf(_SC_PAGESIZE);
+    const int64_t moff = (int64_t)base / page * page;
+    const size_t mlen = (size_t)(base + total - moff);
+    if (::ftruncate(fd, (off_t)(base + total)) == 0) {
+      void* m = ::mmap(nullptr, mlen, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)moff);
+      if (m != MAP_FAILED) {
+        char* dst = static_cast<char*>(m) + (base - moff);
+        std::vector<int64_t> off(parts.size() + 1, 0);
+        for (size_t k = 0; k < parts.size(); ++k) off[k + 1] = off[k] + parts[k].second;
+        const int T = std::max(1, std::min(nthreads, 32));
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t] {
+            // byte range [a, b) of the output, copied from the parts it overlaps
+            const int64_t a = total * t / T, b = total * (t + 1) / T;
+            size_t k = (size_t)(std::upper_bound(off.begin(), off.end(), a) - off.begin()) - 1;
+            for (int64_t x = a; x < b && k < parts.size(); ++k) {
+              const int64_t e = std::min(b, off[k + 1]);
+              if (e > x) std::memcpy(dst + x, parts[k].first + (x - off[k]), (size_t)(e - x));
+              x = std::max(x, e);
+            }
+          });
+        for (auto& x : th) x.join();
+        ::munmap(m, mlen);
+        done = true;
+      }
+    }
+  }
+  if (!done) {
+    int64_t at = base;
+    for (auto& p : parts) {
+      const char* q = p.first;
+      int64_t left = p.second;
       while (left > 0) {
-        const ssize_t w = ::pwrite(fd, p, (size_t)left, (off_t)at);
+        const ssize_t w = ::pwrite(fd, q, (size_t)left, (off_t)at);
         if (w <= 0) {
-          bad = true;
-          return;
+          ::close(fd);
+          throw std::runtime_error("write failed: " + path);
         }
-        p += w;
+        q += w;
         left -= w;
         at += w;
       }
-    });
-  for (auto& x : th) x.join();
+    }
+  }
   ::close(fd);
-  if (bad) throw std::runtime_error("write failed: " + path);
-  return off.back();
+  return total;
+}
+
+int64_t format_columns_to_file(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads,
+                               const std::string& path, bool append) {
+  std::vector<std::string> parts = format_parts(cols, n, delim, nthreads);
+  std::vector<std::pair<const char*, int64_t>> pv;
+  for (auto& p : parts) pv.emplace_back(p.data(), (int64_t)p.size());
+  return write_file_parallel(path, append, pv, nthreads);
 }
 
 }  // namespace avh

@@ -534,9 +534,9 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
                                                            int* __restrict__ outD, int a_row0) {
   __shared__ float As[64][DMAX + 1];
   const int a0 = a_row0 + blockIdx.y * 64;
-  for (int e = threadIdx.x; e < 64 * D; e += 256) {
-    const int r = e / D, c = e - r * D;
-    As[r][c] = a0 + r < nA ? A[(long long)(a0 + r) * D + c] : 0.f;
+  for (int e = threadIdx.x; e < 64 * DMAX; e += 256) {   // columns D..DMAX-1 zero (b[] is zero there too)
+    const int r = e / DMAX, c = e - r * DMAX;
+    As[r][c] = (a0 + r < nA && c < D) ? A[(long long)(a0 + r) * D + c] : 0.f;
   }
   __syncthreads();
   const int j = blockIdx.x * 256 + threadIdx.x;

@@ -29,7 +29,7 @@ constexpr int SP_LDS_DOUBLES = 12288;  // 96 KiB: node histogram in LDS when C *
 constexpr int SP_LDS_SCORES = 4096;    // split scores in LDS when R fits (else global scratch)
 
 __device__ __forceinline__ double impurity_of(const double* cnt, int C, int algo, double tot) {
-  if (tot <= 0.0) return 0.0;
+  if (tot <= 0.0) return algo == 0 ? 0.0 : 1.0;   // an empty segment: p = 0 (models/tree.py impurity)
   double s = 0.0;
   if (algo == 0) {  // entropy, base 2
     for (int c = 0; c < C; ++c) {

@@ -209,8 +209,8 @@ class Records:
                 self._spans = LineSpans.from_shard(self._shard)
             if len(self._spans) != self.n_lines:
                 raise RuntimeError("line index does not match the token table")
-            if self._dev_lines is not None and self._spans.dev is None:
-                self._spans.dev = self._dev_lines
+        if self._dev_lines is not None and self._spans.dev is None:
+            self._spans.dev = self._dev_lines
         return self._spans
 
     def to(self, device) -> "Records":

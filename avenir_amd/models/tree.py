@@ -39,6 +39,7 @@ from typing import Any, Sequence
 import numpy as np
 import torch
 
+from .. import _native
 from ..data.table import MISSING, Table, pad16
 from ..ops import tree_ops as T
 from ..parallel.comm import Comm, get_comm

@@ -30,6 +30,8 @@ from __future__ import annotations
 
 import math
 
+import weakref
+
 import torch
 
 from .. import _native
@@ -141,11 +143,15 @@ class _FragCacheF32:
             return pack_weights_f32(w_hh, H)
         key = (w_hh.data_ptr(), w_hh._version, tuple(w_hh.shape), H)
         hit = self.d.get(key)
-        if hit is None:
-            if len(self.d) >= self.size:
-                self.d.pop(next(iter(self.d)))
-            hit = self.d[key] = pack_weights_f32(w_hh, H)
-        return hit
+        # the entry must belong to THIS live tensor: a freed tensor's memory (same address, shape
+        # and version 0) may be re-used by a new one with different values
+        if hit is not None and hit[0]() is w_hh:
+            return hit[1]
+        if len(self.d) >= self.size:
+            self.d.pop(next(iter(self.d)))
+        frags = pack_weights_f32(w_hh, H)
+        self.d[key] = (weakref.ref(w_hh), frags)
+        return frags
 
 
 _frags_f32 = _FragCacheF32()
@@ -164,11 +170,13 @@ class _FragCache:
             return pack_weights(w_ih, w_hh, H)
         key = (w_ih.data_ptr(), w_ih._version, tuple(w_ih.shape), w_hh.data_ptr(), w_hh._version, H)
         hit = self.d.get(key)
-        if hit is None:
-            if len(self.d) >= self.size:
-                self.d.pop(next(iter(self.d)))
-            hit = self.d[key] = pack_weights(w_ih, w_hh, H)
-        return hit
+        if hit is not None and hit[0]() is w_ih and hit[1]() is w_hh:     # the same live tensors
+            return hit[2]
+        if len(self.d) >= self.size:
+            self.d.pop(next(iter(self.d)))
+        frags = pack_weights(w_ih, w_hh, H)
+        self.d[key] = (weakref.ref(w_ih), weakref.ref(w_hh), frags)
+        return frags
 
 
 _frags = _FragCache()

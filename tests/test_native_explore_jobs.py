@@ -339,7 +339,7 @@ def _close_lines(a: list[str], b: list[str], rel=1e-4, abs_=2e-3):
     for x, y in zip(a, b):
         if x == y:
             continue
-        fx, fy = x.split(","), y.split(",")
+        fx, fy = x.strip("()").split(","), y.strip("()").split(",")
         assert len(fx) == len(fy), (x, y)
         for u, v in zip(fx, fy):
             if u != v:
