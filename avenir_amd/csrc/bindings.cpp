@@ -3284,6 +3284,8 @@ int64_t format_device(py::list cols_py, int64_t n, const std::string& delim, con
                                   stream));
   auto dl = upload_bytes(delim);
   const auto* dc = reinterpret_cast<const avk::DevFmtCol*>(dcols.data_ptr());
+  const bool timing = std::getenv("AVMI_FORMAT_TIMING") != nullptr;
+  auto tp0 = std::chrono::steady_clock::now();
   auto len = at::empty({std::max<int64_t>(1, n)}, dopt.dtype(at::kLong));
   auto bad = at::zeros({1}, dopt.dtype(at::kInt));
   avk::format_rows_len(dc, ncols, n, dl.data_ptr<uint8_t>(), (int)delim.size(), len.data_ptr<int64_t>(),
@@ -3300,9 +3302,16 @@ int64_t format_device(py::list cols_py, int64_t n, const std::string& delim, con
   if (total)
     BIND_HIP_CHECK(hipMemcpyAsync(host.data_ptr(), out.data_ptr(), (size_t)total, hipMemcpyDeviceToHost, stream));
   BIND_HIP_CHECK(hipStreamSynchronize(stream));
+  auto tp1 = std::chrono::steady_clock::now();
   {
     py::gil_scoped_release rel;
     avh::write_file_parallel(path, append, {{reinterpret_cast<const char*>(host.data_ptr()), total}}, nthreads);
+  }
+  if (timing) {
+    auto tp2 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[format_device] rows %lld bytes %lld format+d2h %.4f s write %.4f s\n", (long long)n,
+                 (long long)total, std::chrono::duration<double>(tp1 - tp0).count(),
+                 std::chrono::duration<double>(tp2 - tp1).count());
   }
   return total;
 }

@@ -344,37 +344,35 @@ int64_t write_file_parallel(const std::string& path, bool append,
   if (fd < 0) throw std::runtime_error("cannot open " + path + " for writing");
   const off_t base = append ? ::lseek(fd, 0, SEEK_END) : 0;
   bool done = false;
-  if (total >= (8 << 20)) {
-    // large outputs: size the file once and copy into a shared mapping from several threads —
-    // page-cache writes through write()/pwrite() serialise on the file's inode lock, page faults on
-    // a mapping do not
-    const int64_t page = (int64_t)sysconf(_SC_PAGESIZE);
-    const int64_t moff = (int64_t)base / page * page;
-    const size_t mlen = (size_t)(base + total - moff);
-    if (::ftruncate(fd, (off_t)(base + total)) == 0) {
-      void* m = ::mmap(nullptr, mlen, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)moff);
-      if (m != MAP_FAILED) {
-        char* dst = static_cast<char*>(m) + (base - moff);
-        std::vector<int64_t> off(parts.size() + 1, 0);
-        for (size_t k = 0; k < parts.size(); ++k) off[k + 1] = off[k] + parts[k].second;
-        const int T = std::max(1, std::min(nthreads, 32));
-        std::vector<std::thread> th;
-        for (int t = 0; t < T; ++t)
-          th.emplace_back([&, t] {
-            // byte range [a, b) of the output, copied from the parts it overlaps
-            const int64_t a = total * t / T, b = total * (t + 1) / T;
-            size_t k = (size_t)(std::upper_bound(off.begin(), off.end(), a) - off.begin()) - 1;
-            for (int64_t x = a; x < b && k < parts.size(); ++k) {
-              const int64_t e = std::min(b, off[k + 1]);
-              if (e > x) std::memcpy(dst + x, parts[k].first + (x - off[k]), (size_t)(e - x));
-              x = std::max(x, e);
+  if (total >= (16 << 20) && nthreads > 1) {
+    // large outputs: byte ranges written by several threads (pwrite at their offsets)
+    std::vector<int64_t> off(parts.size() + 1, 0);
+    for (size_t k = 0; k < parts.size(); ++k) off[k + 1] = off[k] + parts[k].second;
+    const int T = std::max(1, std::min(nthreads, 16));
+    std::vector<std::thread> th;
+    std::atomic<bool> bad{false};
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const int64_t a = total * t / T, b = total * (t + 1) / T;
+        size_t k = (size_t)(std::upper_bound(off.begin(), off.end(), a) - off.begin()) - 1;
+        for (int64_t x = a; x < b && k < parts.size(); ++k) {
+          const int64_t e = std::min(b, off[k + 1]);
+          while (x < e) {
+            const ssize_t w = ::pwrite(fd, parts[k].first + (x - off[k]), (size_t)(e - x), (off_t)(base + x));
+            if (w <= 0) {
+              bad = true;
+              return;
             }
-          });
-        for (auto& x : th) x.join();
-        ::munmap(m, mlen);
-        done = true;
-      }
+            x += w;
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+    if (bad) {
+      ::close(fd);
+      throw std::runtime_error("write failed: " + path);
     }
+    done = true;
   }
   if (!done) {
     int64_t at = base;

@@ -180,8 +180,8 @@ struct FmtCol {
 std::string format_columns(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads);
 int64_t format_columns_to_file(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim, int nthreads,
                                const std::string& path, bool append);
-// write (or append) the concatenation of ``parts`` to ``path``: large outputs through a shared
-// mapping filled by several threads, small ones by pwrite; returns the bytes written
+// write (or append) the concatenation of ``parts`` to ``path``: large outputs as byte ranges
+// pwritten by several threads, small ones by one; returns the bytes written
 int64_t write_file_parallel(const std::string& path, bool append,
                             const std::vector<std::pair<const char*, int64_t>>& parts, int nthreads);
 

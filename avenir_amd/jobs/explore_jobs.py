@@ -464,7 +464,7 @@ def undersampling(args):
     if rec is not None:
         cc = rec.field(cls_ord)
         vals = ctx.union(rec.strings(torch.unique(cc[cc >= 0])))
-        y = rec.map_codes(cc, vals).long().cpu()
+        y = rec.map_codes(cc, vals).long()           # on the table's device: the Philox draws run there
         keep = undersample(y, seed=ctx.get_int("random.seed", 0), comm=ctx.comm).bool()
         spans = rec.line_spans().select(keep)
         ctx.emit_columns([spans.column("r")], len(spans))
@@ -574,7 +574,7 @@ def adaboost_update(args):
         if width is None:
             raise SystemExit("adaBoostUpdate: records of differing field counts")
         spans = src.line_spans()
-        ctx.emit_columns(field_columns(spans, width, ctx.native_delim(), {bo: ("f", nw.cpu(), prec)}), n_rows)
+        ctx.emit_columns(field_columns(spans, width, ctx.native_delim(), {bo: ("f", nw, prec)}), n_rows)
         return
     rows = src
     d = ctx.delim_out
@@ -669,8 +669,7 @@ def feature_hashing_job(args):
         spans = rec.line_spans()
         dl = ctx.native_delim()
         other = [spans.column("rf", i, dl) for i in rem]
-        enc_h = enc.cpu()
-        ctx.emit_columns(other[:off] + [("i", enc_h[:, j]) for j in range(size)] + other[off:], n)
+        ctx.emit_columns(other[:off] + [("i", enc[:, j]) for j in range(size)] + other[off:], n)
         return
     rows = ctx.rows()
     n = len(rows)
@@ -810,7 +809,7 @@ def _loo_native(ctx, rec, cat, cls_ord, pos, reg, sd, prec, train, stat_path):
             e = (s_[:, j] - yv) / (c_[:, j] - 1 + reg) * noise
         else:
             e = s_[:, j] / (c_[:, j] + reg)
-        rep[o] = ("f", e.cpu(), prec)
+        rep[o] = ("f", e, prec)
     ctx.emit_columns(field_columns(rec.line_spans(), rec.width(), ctx.native_delim(), rep), n)
 
 
@@ -833,7 +832,7 @@ def binary_dummy_job(args):
             u = [x.lower() for x in u] if ci else u
             ui = {x: i for i, x in enumerate(u)}
             lut = torch.tensor([ui.get(v, -1) for v in voc] or [-1], dtype=torch.long, device=rec.device)
-            k = torch.where(c >= 0, lut[c.long().clamp_min(0)], torch.full_like(c.long(), -1)).cpu()
+            k = torch.where(c >= 0, lut[c.long().clamp_min(0)], torch.full_like(c.long(), -1))
             rep[o] = [("s", [fv, tv], (k == i).long()) for i in range(len(u))]
         ctx.emit_columns(field_columns(rec.line_spans(), rec.width(), ctx.native_delim(), rep), rec.n_lines)
         return
@@ -871,7 +870,7 @@ def linear_mapper(args):
                      dtype=torch.float64, device=ctx.device)
     X, src = ctx.numeric_matrix(q)
     if not isinstance(src, list):      # native: one GEMM, ids / retained fields from the raw bytes
-        Y = (X @ M.T).cpu()
+        Y = X @ M.T
         spans, dl = src.line_spans(), ctx.native_delim()
         ctx.emit_columns([spans.column("rf", o, dl) for o in ids] + [("f", Y[:, j].contiguous(), prec)
                                                                      for j in range(Y.shape[1])]

@@ -29,11 +29,10 @@ def normalizer(args):
     strat = ctx.get_str("normalizing.strategy", "minmax")
     prec = ctx.get_int("floating.precision", 3)
     X, src = ctx.numeric_matrix(ords)
-    X = X.cpu()
-    nrow = X.shape[0]
-    st = torch.stack([torch.full((len(ords),), float(nrow), dtype=torch.float64), X.sum(0), (X * X).sum(0)])
-    mn = X.min(0).values if nrow else torch.full((len(ords),), math.inf, dtype=torch.float64)
-    mx = X.max(0).values if nrow else torch.full((len(ords),), -math.inf, dtype=torch.float64)
+    nrow, dv = X.shape[0], X.device
+    st = torch.stack([torch.full((len(ords),), float(nrow), dtype=torch.float64, device=dv), X.sum(0), (X * X).sum(0)])
+    mn = X.min(0).values if nrow else torch.full((len(ords),), math.inf, dtype=torch.float64, device=dv)
+    mx = X.max(0).values if nrow else torch.full((len(ords),), -math.inf, dtype=torch.float64, device=dv)
     ctx.all_reduce(st)
     if ctx.comm.is_distributed:
         ctx.comm.all_reduce(mn, "min")
@@ -152,7 +151,7 @@ def transformer(args):
             lut = luts.get(o, {})
             tab = [lut.get(w, w) for w in rec.vocab]
             for t in a.get("targetFieldOrdinals", [o]):
-                rep_cols[t] = ("s", tab, rec.field(o).cpu())
+                rep_cols[t] = ("s", tab, rec.field(o))
         width = max([rec.width()] + [t + 1 for t in rep_cols])
         spans = rec.line_spans()
         cols = [rep_cols[j] if j in rep_cols else (spans.column("rf", j, ctx.native_delim()) if j < rec.width()
@@ -285,13 +284,13 @@ def _time_interval_native(ctx, rec, kords, to, keep):
     sel = spans.select(o.cpu())
     dl = ctx.native_delim()
     if keep:
-        cols = [sel.column("r", delims=dl), ("i", dt.cpu())]
+        cols = [sel.column("r", delims=dl), ("i", dt)]
     else:
         W = rec.width()
         if W is None:
             raise SystemExit("timeIntervalGenerator: records of differing field counts")
         from .common import field_columns
-        cols = field_columns(sel, W, dl, {to: ("i", dt.cpu())})
+        cols = field_columns(sel, W, dl, {to: ("i", dt)})
     ctx.emit_columns(cols, len(sel))
 
 

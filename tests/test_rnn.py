@@ -168,7 +168,9 @@ def test_lstm_network_graph_matches_eager(cuda):
 @pytest.mark.gpu
 def test_fused_fp32_lstm_loss_curve_equals_nn_lstm(cuda):
     """The default fp32 fused kernels against an fp32 torch.nn.LSTM (MIOpen) from the same weights
-    and batches: the training loss curves agree at fp32 tolerance over all steps."""
+    and batches: the training loss curves agree at fp32 tolerance over all steps.  Plain SGD: Adam
+    divides by the running gradient RMS, which turns last-bit differences between two correct fp32
+    implementations into visibly different trajectories once the gradients become small."""
     from avenir_amd.nn.sequence import LstmNetwork
     torch.manual_seed(0)
     n, T = 2048, 5
@@ -184,12 +186,12 @@ def test_fused_fp32_lstm_loss_curve_equals_nn_lstm(cuda):
             ref = torch.nn.LSTM(2, 100, 2, batch_first=True).to(cuda)
             ref.load_state_dict(net.lstm.state_dict())
             net.lstm = ref
-        net.optimizer = torch.optim.Adam(net.parameters(), lr=0.005)
+        net.optimizer = torch.optim.SGD(net.parameters(), lr=2.0)
         torch.manual_seed(11)
         net.fit(x, y)
         curves[kind] = torch.tensor(net.losses)
     a, b = curves["fused"], curves["nn"]
-    assert a.shape == b.shape and b[-10:].mean() < 0.3 * b[0]
+    assert a.shape == b.shape and b[-10:].mean() < 0.6 * b[0]
     assert float(((a - b).abs() / b.abs()).max()) < 1e-3, (a, b)
     assert float(((a[:6] - b[:6]).abs() / b[:6].abs()).max()) < 1e-4, (a, b)
 
