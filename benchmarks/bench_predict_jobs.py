@@ -115,10 +115,11 @@ def main() -> int:
     ap.add_argument("--jobs", default="vit,mmc,pst,nbp,detr,mop")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--rs-records", type=int, default=1 << 17)
+    ap.add_argument("--dir", default=None, help="directory of the input / output files (default: a temp dir)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    d = tempfile.mkdtemp(prefix="avmi_pred_")
+    d = tempfile.mkdtemp(prefix="avmi_pred_", dir=args.dir)
     for job in args.jobs.split(","):
         n_rec = args.rs_records if job == "rs" else args.records
         argv, data = setup_rs(d, n_rec) if job == "rs" else setup(job, d, args.records, dev)
@@ -138,7 +139,7 @@ def main() -> int:
         for fn in files:
             with open(fn, "rb") as fh:
                 n_out += sum(1 for _ in fh)
-        rec = {"bench": "predict_job", "job": argv[0], "records": n_rec, "device": dev,
+        rec = {"bench": "predict_job", "job": argv[0], "records": n_rec, "device": dev, "dir": os.path.dirname(d),
                "bytes": os.path.getsize(data), "seconds": round(best, 4), "records_per_s": n_rec / best,
                "output_lines": n_out}
         if job == "rs":
@@ -147,6 +148,8 @@ def main() -> int:
         if args.out:
             with open(args.out, "a") as fh:
                 fh.write(json.dumps(rec) + "\n")
+    import shutil
+    shutil.rmtree(d, ignore_errors=True)
     return 0
 
 
