@@ -473,7 +473,7 @@ def _device_columns(cols: list, n: int):
             if d is None:
                 return None
             out.append(d)
-            like = d[1]
+            like = torch.empty(0, device=d[1].device)
             continue
         if k == "f" and not (len(c) > 2 and 0 <= int(c[2]) <= 9):
             return None
@@ -484,7 +484,7 @@ def _device_columns(cols: list, n: int):
             t = c[j]
             if not (isinstance(t, torch.Tensor) and t.is_cuda):
                 return None
-            like = t
+            like = torch.empty(0, device=t.device)
         out.append(c)
     return (out, like) if like is not None else None
 

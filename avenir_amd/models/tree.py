@@ -632,17 +632,20 @@ class DecisionTreeBuilder:
         keys = np.asarray([((s * 1000003 + 17) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF for s in seeds],
                           dtype=np.uint64).view(np.int64)
         dev = t.device
-        cb, lb, wb, cnt = FO.forest_bootstrap(codes.contiguous(), t.labels.to(dev).contiguous(), t.n, keys,
-                                              t.row_offset, mode, rate32)
+        # the node-total slot row rides along the bootstrap (a copy of the input's codes, not of the
+        # several-times larger bootstrap buffer)
+        cb, lb, wb, cnt = FO.forest_bootstrap(_with_total_row(codes, t.n).contiguous(), t.labels.to(dev).contiguous(),
+                                              t.n, keys, t.row_offset, mode, rate32)
         cnt_h = [int(x) for x in cnt.tolist()]
         R = sum(cnt_h)
+        cb[-1, R:] = MISSING
         node0 = torch.full((cb.shape[1],), -1, dtype=torch.int32, device=dev)
-        if R:
-            node0[:R] = torch.repeat_interleave(torch.arange(len(seeds), dtype=torch.int32, device=dev),
-                                                torch.tensor(cnt_h, device=dev))
+        a = 0
+        for i, c in enumerate(cnt_h):           # tree i's rows are one contiguous block
+            node0[a:a + c] = i
+            a += c
         cls = list(t.class_field.cardinality) if t.class_field else ["_"]
-        return self._grow(_with_total_row(cb, R), R, lb, wb, node0, [random.Random(s) for s in seeds],
-                          t.n_classes, cls)
+        return self._grow(cb, R, lb, wb, node0, [random.Random(s) for s in seeds], t.n_classes, cls)
 
     def _grow(self, codes: torch.Tensor, n: int, labels: torch.Tensor, weight: torch.Tensor | None,
               node: torch.Tensor, rngs: list, C: int, cls: list[str]) -> list[DecisionTree]:

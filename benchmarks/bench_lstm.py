@@ -122,7 +122,7 @@ def main():
         for impl in args.impls.split(","):
             try:
                 res[impl] = run(cfg, impl, args.steps, args.warmup)
-            except RuntimeError as e:        # e.g. a library LSTM that refuses graph capture
+            except Exception as e:           # e.g. a library LSTM that refuses graph capture
                 print(json.dumps({"bench": "lstm", "config": cfg["name"], "impl": impl, "error": str(e)[:200]}),
                       flush=True)
                 res[impl] = None

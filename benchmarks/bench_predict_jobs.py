@@ -123,9 +123,11 @@ def main() -> int:
     for job in args.jobs.split(","):
         n_rec = args.rs_records if job == "rs" else args.records
         argv, data = setup_rs(d, n_rec) if job == "rs" else setup(job, d, args.records, dev)
-        out = os.path.join(d, f"{job}.out")
         best = None
-        for _ in range(args.reps):
+        for rep in range(args.reps):
+            # a fresh output path per run (a job writes a new output; re-using one would time the
+            # truncation of the previous run's file)
+            out = os.path.join(d, f"{job}.{rep}.out")
             if dev == "cuda":
                 torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -134,6 +136,9 @@ def main() -> int:
                 torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
+            if rep + 1 < args.reps:
+                import shutil
+                shutil.rmtree(out, ignore_errors=True) if os.path.isdir(out) else os.remove(out)
         files = [out] if os.path.isfile(out) else [os.path.join(out, f) for f in sorted(os.listdir(out))]
         n_out = 0
         for fn in files:
@@ -145,6 +150,8 @@ def main() -> int:
         if job == "rs":
             rec["pairs_per_s"] = n_rec * (n_rec - 1) / 2 / best
         print(json.dumps(rec), flush=True)
+        for fn in files:
+            os.remove(fn)
         if args.out:
             with open(args.out, "a") as fh:
                 fh.write(json.dumps(rec) + "\n")
