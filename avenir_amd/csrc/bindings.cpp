@@ -439,7 +439,8 @@ static void check_codes(const at::Tensor& codes, int64_t n) {
 void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels,
                     const at::Tensor& node, const c10::optional<at::Tensor>& weight,
                     const at::Tensor& bins, const at::Tensor& offs, int64_t total_bins,
-                    int64_t n_classes, int64_t n_nodes, at::Tensor& hist) {
+                    int64_t n_classes, int64_t n_nodes, at::Tensor& hist,
+                    const c10::optional<at::Tensor>& node_rows) {
   check_codes(codes, n);
   CHECK_DEV(labels);
   CHECK_DTYPE(labels, at::kByte);
@@ -462,10 +463,17 @@ void node_histogram(const at::Tensor& codes, int64_t n, const at::Tensor& labels
     TORCH_CHECK(weight->numel() >= n4 && aligned(*weight, 4), "weight must cover n rounded up to 4, 4-byte aligned");
     w = weight->data_ptr<uint8_t>();
   }
+  const long long* nr = nullptr;  // per node [lo, hi) row range (the kernel clamps it to [0, n))
+  if (node_rows.has_value() && node_rows->defined()) {
+    CHECK_DEV((*node_rows));
+    CHECK_DTYPE((*node_rows), at::kLong);
+    TORCH_CHECK(node_rows->is_contiguous() && node_rows->numel() == 2 * n_nodes, "node_rows must be [A, 2]");
+    nr = reinterpret_cast<const long long*>(node_rows->data_ptr<int64_t>());
+  }
   DevGuard g(codes.device());
   avk::node_histogram(codes.data_ptr<uint8_t>(), codes.size(1), n, labels.data_ptr<uint8_t>(),
                       node.data_ptr<int>(), w, bins.data_ptr<int>(), offs.data_ptr<int>(),
-                      (int)codes.size(0), (int)total_bins, (int)n_classes, (int)n_nodes,
+                      (int)codes.size(0), (int)total_bins, (int)n_classes, (int)n_nodes, nr,
                       reinterpret_cast<unsigned long long*>(hist.data_ptr<int64_t>()), cur_stream(codes));
 }
 
@@ -3246,7 +3254,7 @@ int64_t format_device(py::list cols_py, int64_t n, const std::string& delim, con
     } else if (kind == "f") {
       c.kind = avk::DevFmtCol::F64;
       c.prec = t.size() > 2 ? t[2].cast<int>() : 6;
-      if (c.prec < 0 || c.prec > 9) return -1;  // %g / repr / long fractions: host formatter
+      if (c.prec != -2 && (c.prec < 0 || c.prec > 9)) return -1;  // %g / long fractions: host formatter
       c.dv = dev_tensor(t[1], at::kDouble, n, "float").data_ptr<double>();
     } else if (kind == "i") {
       c.kind = avk::DevFmtCol::I64;
@@ -3696,7 +3704,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("class_moments", &class_moments);
   m.def("nb_predict", &nb_predict);
   m.def("nb_predict_wide", &nb_predict_wide);
-  m.def("node_histogram", &node_histogram);
+  m.def("node_histogram", &node_histogram, py::arg("codes"), py::arg("n"), py::arg("labels"), py::arg("node"),
+        py::arg("weight"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_classes"),
+        py::arg("n_nodes"), py::arg("hist"), py::arg("node_rows") = py::none());
   m.def("node_grad_histogram", &node_grad_histogram, py::arg("codes"), py::arg("n"), py::arg("node"), py::arg("g"),
         py::arg("h"), py::arg("bins"), py::arg("offs"), py::arg("total_bins"), py::arg("n_nodes"), py::arg("out"),
         py::arg("even_only") = false, py::arg("tot_slot") = -1, py::arg("scale") = 65536.0);

@@ -51,8 +51,8 @@ void nb_predict(const uint8_t* codes, long long ld, long long n, int nfeat, cons
 // ---- tree.hip (K7/K8) -----------------------------------------------------------------------
 void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
                     const int* node, const uint8_t* weight, const int* bins, const int* offs,
-                    int nfeat, int total_bins, int n_classes, int n_nodes, unsigned long long* hist,
-                    hipStream_t stream);
+                    int nfeat, int total_bins, int n_classes, int n_nodes, const long long* node_rows,
+                    unsigned long long* hist, hipStream_t stream);
 void node_grad_histogram(const uint8_t* codes, long long ld, long long n, const int* node,
                          const float* g, const float* h, const int* bins, const int* offs, int nfeat,
                          int total_bins, int n_nodes, int even_only, int tot_slot, float scale, long long* out, hipStream_t stream);

@@ -111,6 +111,103 @@ __device__ __forceinline__ bool put_fixed(Sink& s, double v, int p) {
   return true;
 }
 
+// Python's repr(float) — the fewest significant digits that parse back to v, the nearest such
+// decimal, fixed notation for decimal exponents -4 <= x < 16 and d.ddde[+-]XX otherwise (the host
+// formatter's put_pyrepr, std::to_chars shortest) — by exact 128-bit integer arithmetic.
+// v = m 2^e (e <= -1); for k = 0, 1, .. 31 fraction digits, with 10^k = 5^k 2^k and s = -e - k:
+//   D = round(m 5^k / 2^s) (half to even), and D 10^-k round-trips iff it lies inside v's
+//   rounding interval:  (4m - 2) 5^k <= D 2^(s+2) <= (4m + 2) 5^k
+// (bounds included only for even m; the lower bound is (4m - 1) 5^k when m = 2^52 — the gap below
+// a power of two is half the gap above — and then D + 1 is tried too).  Every product stays below
+// 2^128 (m 5^31 < 2^125).  False outside that range (|v| >= 2^53, subnormals, values needing more
+// than 31 fraction digits): the host formatter takes over.
+__device__ __forceinline__ bool put_repr(Sink& s, double v) {
+  if (v != v) {
+    s.put("nan", 3);
+    return true;
+  }
+  const uint64_t bits = (uint64_t)__double_as_longlong(v);
+  const bool neg = bits >> 63;
+  const int be = (int)((bits >> 52) & 0x7ff);
+  const uint64_t frac = bits & ((1ull << 52) - 1);
+  if (be == 0x7ff) {
+    if (neg) s.put('-');
+    s.put("inf", 3);
+    return true;
+  }
+  if (be == 0 && frac == 0) {
+    if (neg) s.put('-');
+    s.put("0.0", 3);
+    return true;
+  }
+  if (be == 0) return false;  // subnormal
+  const uint64_t m = frac | (1ull << 52);
+  const int sh = 1075 - be;   // -e
+  if (sh < 1) return false;
+  const bool even = (m & 1ull) == 0, pow2 = frac == 0 && be > 1;
+  const unsigned __int128 one = 1;
+  unsigned __int128 p5 = 1;
+  uint64_t D = 0;
+  int k = 0;
+  bool found = false;
+  for (; k <= 31; ++k, p5 *= 5u) {
+    const int s2 = sh - k;
+    if (s2 > 125) continue;  // D would be 0
+    if (s2 < 1) return false;
+    const unsigned __int128 N = (unsigned __int128)m * p5;
+    unsigned __int128 q = N >> s2;
+    const unsigned __int128 r = N - (q << s2), half = one << (s2 - 1);
+    if (r > half || (r == half && (q & 1u))) ++q;
+    const unsigned __int128 hi = ((unsigned __int128)(4 * m + 2)) * p5;
+    const unsigned __int128 lo = ((unsigned __int128)(pow2 ? 4 * m - 1 : 4 * m - 2)) * p5;
+    for (int t = 0; t < (pow2 ? 2 : 1) && !found; ++t) {
+      const unsigned __int128 c = q + (unsigned)t;
+      if ((c >> 64) != 0) return false;
+      const unsigned __int128 L = c << (s2 + 2);
+      if (even ? (L >= lo && L <= hi) : (L > lo && L < hi)) {
+        D = (uint64_t)c;
+        found = true;
+      }
+    }
+    if (found) break;
+  }
+  if (!found || D == 0) return false;
+  // digits of D, trailing zeros dropped (k fraction digits: decimal exponent x = nd - 1 - k)
+  char b[24];
+  int nd = u64_digits(D, b);  // reversed: b[0] is the last digit
+  const int x = nd - 1 - k;
+  int z = 0;
+  while (z < nd - 1 && b[z] == '0') ++z;  // trailing zeros
+  const int sig = nd - z;                  // significant digits b[nd-1] .. b[z]
+  if (neg) s.put('-');
+  if (x >= -4 && x < 16) {
+    if (x >= 0) {
+      for (int i = 0; i <= x; ++i) s.put(i < sig ? b[nd - 1 - i] : '0');
+      s.put('.');
+      if (sig > x + 1)
+        for (int i = x + 1; i < sig; ++i) s.put(b[nd - 1 - i]);
+      else
+        s.put('0');
+    } else {
+      s.put("0.", 2);
+      for (int i = 0; i < -x - 1; ++i) s.put('0');
+      for (int i = 0; i < sig; ++i) s.put(b[nd - 1 - i]);
+    }
+    return true;
+  }
+  s.put(b[nd - 1]);
+  if (sig > 1) {
+    s.put('.');
+    for (int i = 1; i < sig; ++i) s.put(b[nd - 1 - i]);
+  }
+  s.put('e');
+  s.put(x < 0 ? '-' : '+');
+  const int ax = x < 0 ? -x : x;
+  if (ax < 10) s.put('0');
+  put_i64(s, ax);
+  return true;
+}
+
 // [a, e) of field f of the line (negative: from the end); false when the line is shorter
 __device__ __forceinline__ bool field_span(const uint8_t* p, int64_t n, int f, const uint32_t* sep, int64_t* a,
                                            int64_t* e) {
@@ -181,7 +278,7 @@ __device__ bool fmt_row(int64_t r, const avk::DevFmtCol* cols, int ncols, const 
     first = false;
     switch (c.kind) {
       case avk::DevFmtCol::STR: put_tab(s, c, c.idx[r]); break;
-      case avk::DevFmtCol::F64: ok &= put_fixed(s, c.dv[r], c.prec); break;
+      case avk::DevFmtCol::F64: ok &= c.prec == -2 ? put_repr(s, c.dv[r]) : put_fixed(s, c.dv[r], c.prec); break;
       case avk::DevFmtCol::I64: put_i64(s, c.iv[r]); break;
       case avk::DevFmtCol::LIT: s.put(c.lit, c.litlen); break;
       case avk::DevFmtCol::RAW:

@@ -31,16 +31,29 @@ __global__ __launch_bounds__(TB_THREADS) void node_hist_kernel(
     const uint8_t* __restrict__ codes, long long ld, long long n, const uint8_t* __restrict__ labels,
     const int* __restrict__ node, const uint8_t* __restrict__ weight, const int* __restrict__ bins,
     const int* __restrict__ offs, int nfeat, int total_bins, int n_classes, int nodes_per_chunk,
-    int n_nodes, unsigned long long* __restrict__ hist) {
+    int n_nodes, const long long* __restrict__ node_rows, unsigned long long* __restrict__ hist) {
   extern __shared__ __attribute__((aligned(16))) unsigned int s_h[];
   const int a0 = blockIdx.y * nodes_per_chunk;
   const int na = min(nodes_per_chunk, n_nodes - a0);
   const int per_node = n_classes * total_bins;
   for (int i = threadIdx.x; i < na * per_node; i += TB_THREADS) s_h[i] = 0;
+  // rows a chunk can hold: the union of its nodes' row ranges (a forest's trees are contiguous
+  // row blocks, so a chunk of one tree's nodes scans that tree's rows only)
+  long long lo = 0, hi = n;
+  if (node_rows) {
+    lo = n;
+    hi = 0;
+    for (int i = 0; i < na; ++i) {
+      lo = min(lo, node_rows[2 * (a0 + i)]);
+      hi = max(hi, node_rows[2 * (a0 + i) + 1]);
+    }
+    lo = max(lo, 0LL);
+    hi = min(hi, n);
+  }
   __syncthreads();
-  const long long nq = (n + 3) >> 2;  // 4-row quads (ld is a multiple of 16: quads never cross it)
+  const long long q1 = lo < hi ? (hi + 3) >> 2 : 0;  // 4-row quads (ld is a multiple of 16: quads never cross it)
   const long long stride = (long long)gridDim.x * TB_THREADS;
-  for (long long q = (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < nq; q += stride) {
+  for (long long q = (lo >> 2) + (long long)blockIdx.x * TB_THREADS + threadIdx.x; q < q1; q += stride) {
     const long long r0 = q * 4;
     const int4 nd4 = *reinterpret_cast<const int4*>(node + r0);
     const uchar4 lb4 = *reinterpret_cast<const uchar4*>(labels + r0);
@@ -292,8 +305,8 @@ static long long tree_lds_budget() { return 32 * 1024; }
 
 void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8_t* labels,
                     const int* node, const uint8_t* weight, const int* bins, const int* offs,
-                    int nfeat, int total_bins, int n_classes, int n_nodes, unsigned long long* hist,
-                    hipStream_t stream) {
+                    int nfeat, int total_bins, int n_classes, int n_nodes, const long long* node_rows,
+                    unsigned long long* hist, hipStream_t stream) {
   if (n <= 0 || n_nodes <= 0) return;
   const long long per_node_bytes = 4LL * n_classes * total_bins;
   if (per_node_bytes > 64 * 1024) throw std::runtime_error("node_histogram: per-node table exceeds LDS");
@@ -302,7 +315,7 @@ void node_histogram(const uint8_t* codes, long long ld, long long n, const uint8
   const int gx = std::max(1, std::min(av::stream_grid((n + 3) / 4, TB_THREADS, 2, 2048), std::max(64, 4096 / chunks)));
   dim3 grid(gx, chunks);
   node_hist_kernel<<<grid, TB_THREADS, per_node_bytes * npc, stream>>>(
-      codes, ld, n, labels, node, weight, bins, offs, nfeat, total_bins, n_classes, npc, n_nodes, hist);
+      codes, ld, n, labels, node, weight, bins, offs, nfeat, total_bins, n_classes, npc, n_nodes, node_rows, hist);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -475,7 +475,7 @@ def _device_columns(cols: list, n: int):
             out.append(d)
             like = torch.empty(0, device=d[1].device)
             continue
-        if k == "f" and not (len(c) > 2 and 0 <= int(c[2]) <= 9):
+        if k == "f" and not (len(c) > 2 and (0 <= int(c[2]) <= 9 or int(c[2]) == -2)):
             return None
         tens = {"s": [2], "l": [2, 3], "lp": [2, 3, 4], "f": [1], "i": [1]}.get(k)
         if tens is None:

@@ -97,12 +97,12 @@ def mmc(args):
                       min_len=1)
     X = X[keep]
     lo = clf.log_odds(X.to(ctx.device)).double()
-    pred = (lo <= thr).int().cpu()       # 0 -> labels[0] (log-odds above the threshold)
+    pred = (lo <= thr).int()             # 0 -> labels[0] (log-odds above the threshold)
     spans = rec.line_spans().select(keep.cpu())
     cols = [spans.column("rf", id_ord, lit)]
     if val:
         cols.append(spans.column("rf", cls_ord, lit))
-    cols += [("s", list(labels[:2]), pred), ("f", lo.cpu(), -2)]
+    cols += [("s", list(labels[:2]), pred), ("f", lo, -2)]     # device repr when the lines have a device twin
     ctx.emit_columns(cols, int(keep.sum()))
 
 

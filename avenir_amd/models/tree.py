@@ -645,17 +645,22 @@ class DecisionTreeBuilder:
             node0[a:a + c] = i
             a += c
         cls = list(t.class_field.cardinality) if t.class_field else ["_"]
-        return self._grow(cb, R, lb, wb, node0, [random.Random(s) for s in seeds], t.n_classes, cls)
+        starts = list(itertools.accumulate([0] + cnt_h))
+        return self._grow(cb, R, lb, wb, node0, [random.Random(s) for s in seeds], t.n_classes, cls,
+                          tree_rows=list(zip(starts[:-1], starts[1:])))
 
     def _grow(self, codes: torch.Tensor, n: int, labels: torch.Tensor, weight: torch.Tensor | None,
-              node: torch.Tensor, rngs: list, C: int, cls: list[str]) -> list[DecisionTree]:
+              node: torch.Tensor, rngs: list, C: int, cls: list[str],
+              tree_rows: list[tuple[int, int]] | None = None) -> list[DecisionTree]:
         """Level-wise growth of ``len(rngs)`` trees whose rows are marked by ``node`` (row -> root
         slot = tree index, -1 = unused).  Per level, for every frontier node of every tree: ONE
         histogram launch (children whose parent is fully covered are derived by subtraction), the
         scores of every candidate split of every attribute as batched device tensor math, the
         segment counts of the chosen (or top-k) splits gathered on the device, and ONE host copy.
-        The host then only creates node objects."""
+        The host then only creates node objects.  ``tree_rows``: tree i's rows are the block
+        [lo, hi) (fit_many's bootstrap layout), so each histogram chunk scans only its trees' rows."""
         import time
+        t_grow0 = time.perf_counter()
         comm = self.comm or get_comm()
         p = self.p
         space = self.space
@@ -731,18 +736,23 @@ class DecisionTreeBuilder:
             k7_algo = {"entropy": 0, "giniIndex": 1, "gini": 1}.get(p.algorithm)
             use_k7 = k7_algo is not None
         # ---- roots: one histogram launch for every tree ------------------------------------------
-        hist = T.node_histogram(codes, n, labels, node, weight, bins, C, NT)
+        def rows_of(gis):
+            if tree_rows is None:
+                return None
+            return torch.tensor([tree_rows[tree_of[g]] for g in gis], dtype=torch.long).to(dev, non_blocking=True)
+
+        tree_of: list[int] = list(range(NT))
+        hist = T.node_histogram(codes, n, labels, node, weight, bins, C, NT, rows_of(range(NT)))
         if comm.is_distributed:
             comm.all_reduce(hist)
         rc_all = hist[:, :, offs[F]].cpu()
+        self.root_time = time.perf_counter() - t_grow0
         nodes: list[Node] = []
-        tree_of: list[int] = []
         for ti in range(NT):
             rc = rc_all[ti]
             pop = int(rc.sum())
             nodes.append(Node([], pop, float(impurity(rc.unsqueeze(0), p.algorithm)[0]),
                               (rc.double() / max(pop, 1)).tolist(), depth=0))   # depth = #predicates
-            tree_of.append(ti)
         frontier = list(range(NT))   # global node indices; position = histogram slot
         while frontier:
             t0 = time.perf_counter()
@@ -889,7 +899,8 @@ class DecisionTreeBuilder:
                 child_of[a, g] = m + j
             T.tree_assign(codes, n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
             if new_frontier or derived:
-                hs = T.node_histogram(codes, n, labels, node, weight, bins, C, m)   # built children only
+                hs = T.node_histogram(codes, n, labels, node, weight, bins, C, m,   # built children only
+                                      rows_of(new_frontier))
                 if comm.is_distributed:
                     comm.all_reduce(hs)
                 parts = [hs]
@@ -1097,7 +1108,9 @@ class RandomForest:
             b = DecisionTreeBuilder(self.schema, p, comm=_LocalComm() if self.tree_parallel else comm,
                                     space=space)
             trees = b.fit_many(t, [self.params.seed * 7919 + i for i in my_trees], codes=codes)
-            self.build_stats = {"levels": len(b.level_times), "seconds": sum(b.level_times)}
+            self.build_stats = {"levels": len(b.level_times), "seconds": sum(b.level_times),
+                                "root_seconds": getattr(b, "root_time", None),
+                                "level_seconds": [round(x, 5) for x in b.level_times]}
         if self.tree_parallel and comm.is_distributed:
             states = comm.all_gather_object([tr.state() for tr in trees])
             allt = {}

@@ -23,8 +23,10 @@ def _offs(bins: Sequence[int]) -> list[int]:
 
 def node_histogram(codes: torch.Tensor, n: int, labels: torch.Tensor, node: torch.Tensor,
                    weight: torch.Tensor | None, bins: Sequence[int], n_classes: int,
-                   n_nodes: int) -> torch.Tensor:
-    """Class counts per (frontier node, class, fine bin): int64 ``[A, C, TB]``."""
+                   n_nodes: int, node_rows: torch.Tensor | None = None) -> torch.Tensor:
+    """Class counts per (frontier node, class, fine bin): int64 ``[A, C, TB]``.  ``node_rows``
+    (int64 ``[A, 2]``, optional): a [lo, hi) row range holding every row of each node (a forest's
+    trees are contiguous row blocks), so the kernel scans only those rows per node chunk."""
     bins = [int(b) for b in bins]
     tb = sum(bins)
     out = torch.zeros((n_nodes, n_classes, tb), dtype=torch.int64, device=codes.device)
@@ -33,7 +35,8 @@ def node_histogram(codes: torch.Tensor, n: int, labels: torch.Tensor, node: torc
     if codes.is_cuda:
         _native.C().node_histogram(codes, int(n), labels, node, weight, _dev_i32(bins, codes.device),
                                    _dev_i32(_offs(bins), codes.device), tb, int(n_classes),
-                                   int(n_nodes), out)
+                                   int(n_nodes), out,
+                                   None if node_rows is None else node_rows.to(codes.device, torch.long).contiguous())
         return out
     nd = node[:n].long()
     lab = labels[:n].long()

@@ -87,3 +87,28 @@ def test_format_lines_uses_device_twin(cuda, tmp_path, monkeypatch):
     monkeypatch.setenv("AVMI_DEVICE_FORMAT", "0")
     R.format_lines(cols, len(sel), ",", path=str(tmp_path / "h.txt"))
     assert (tmp_path / "d.txt").read_bytes() == (tmp_path / "h.txt").read_bytes()
+
+
+@pytest.mark.gpu
+def test_device_repr_equals_python(cuda, tmp_path):
+    """prec -2 (Python repr, the shortest round-trip digits) on the device: the same bytes as
+    ``repr`` for random magnitudes 1e-12 .. 1e15, powers of two and their neighbours, decimal
+    fractions, signed zero and the non-finite values; values outside the exact 128-bit path
+    (here 1e300) send the whole column to the host formatter (-1)."""
+    import math
+    g = torch.Generator().manual_seed(3)
+    n = 200000
+    x = torch.randn(n, generator=g, dtype=torch.float64) * 10 ** torch.randint(-12, 15, (n,), generator=g).double()
+    extra = [0.1, 0.2, 0.3, 1 / 3, 2 / 3, 1e-4, 1e-5, 9.999999999999999e-05, 1e15, 123456789.0, 0.5, 2.675, 1.005,
+             -0.0, 0.0, 4503599627370496.0, 12.0, 100.0, float("nan"), float("inf"), float("-inf")]
+    extra += [s * math.ldexp(1.0, k) for k in range(-40, 52) for s in (1, -1)]
+    extra += [math.nextafter(math.ldexp(1.0, k), d) for k in range(-40, 52) for d in (0.0, 1e308)]
+    extra += [i / 1000 for i in range(1, 5000)] + [-i / 7 for i in range(1, 5000)]
+    x = torch.cat([x, torch.tensor(extra, dtype=torch.float64)])
+    m = x.numel()
+    w, d = _dev([("f", x.to(cuda), -2)], m, ",", tmp_path, x.to(cuda))
+    assert w >= 0
+    want = "".join(repr(v) + "\n" for v in x.tolist()).encode()
+    assert d == want
+    big = torch.tensor([1.5, 1e300], dtype=torch.float64, device=cuda)
+    assert _dev([("f", big, -2)], 2, ",", tmp_path, big)[0] == -1
