@@ -28,6 +28,8 @@ class LineSpans(Sequence):
         self._addr = addr
         self._lens = lens
         self._strings = strings
+        # a selection whose host spans are built on first use: (parent LineSpans, CPU-able index)
+        self._pending: tuple | None = None
         # device twin: (uploaded bytes uint8, line start int64, length int64) on the GPU — the same
         # lines as the host spans, for the device output formatter (format.hip); None otherwise
         self.dev: tuple | None = None
@@ -87,6 +89,12 @@ class LineSpans(Sequence):
     # -- spans --------------------------------------------------------------------------------------
     def spans(self) -> tuple[object, torch.Tensor, torch.Tensor]:
         """(owner, addr int64 CPU, len int64 CPU)."""
+        if self._pending is not None:
+            parent, idx = self._pending
+            owner, a, n = parent.spans()
+            idx = idx.cpu()
+            self._owner, self._addr, self._lens = owner, a[idx], n[idx]
+            self._pending = None
         if self._addr.device.type != "cpu":
             self._addr, self._lens = self._addr.cpu(), self._lens.cpu()
         return self._owner, self._addr, self._lens
@@ -94,7 +102,15 @@ class LineSpans(Sequence):
     def column(self, kind: str = "r", field: int | None = None, delims: str = "") -> tuple:
         """A ``format_lines`` column: the whole line (``r``; ``delims`` re-joined with the output
         delimiter), field ``field`` (``rf``), or the fields from ``field`` on (``rt``).  With a
-        device twin the column also carries the device form (``.dev``) for format.hip."""
+        device twin the column also carries the device form (``.dev``) for format.hip, and its host
+        form is only built if the host formatter ends up writing it (``host_column``)."""
+        if self.dev is not None and self._strings is None:
+            buf, st, ln = self.dev
+            col = _Col((kind,))
+            col.dev = (("d" + kind, buf, st, ln, delims) if kind == "r" else
+                       ("d" + kind, buf, st, ln, int(field), delims))
+            col.src = (self, kind, field, delims)
+            return col
         owner, a, n = self.spans()
         col = _Col(("r", owner, a, n, delims) if kind == "r" else (kind, owner, a, n, int(field), delims))
         if self.dev is not None:
@@ -104,6 +120,8 @@ class LineSpans(Sequence):
         return col
 
     def __len__(self) -> int:
+        if self._pending is not None:
+            return int(self.dev[1].numel())
         return int(self._lens.numel())
 
     def _str(self, i: int) -> str:
@@ -112,7 +130,7 @@ class LineSpans(Sequence):
 
     def __getitem__(self, i):
         if isinstance(i, slice):
-            owner, a, n = self._owner, self._addr, self._lens
+            owner, a, n = self.spans()
             return LineSpans(owner, a[i], n[i], self._strings[i] if self._strings is not None else None)
         if isinstance(i, torch.Tensor):
             return self.select(i)
@@ -125,7 +143,15 @@ class LineSpans(Sequence):
         return self._str(i)
 
     def select(self, idx: torch.Tensor) -> "LineSpans":
-        """The lines at ``idx`` (int64 indexes or a bool mask), in that order."""
+        """The lines at ``idx`` (int64 indexes or a bool mask), in that order.  With a device twin
+        the selection runs on the device and the host spans follow on first use."""
+        if self.dev is not None and self._strings is None:
+            buf, st, ln = self.dev
+            di = idx.to(st.device)
+            out = LineSpans(None, self._addr[:0], self._lens[:0])
+            out._pending = (self, idx)
+            out.dev = (buf, st[di], ln[di])
+            return out
         owner, a, n = self.spans()
         idx = idx.cpu()
         strings = None
@@ -153,8 +179,21 @@ class LineSpans(Sequence):
 
 
 class _Col(tuple):
-    """A format column tuple that may carry its device form (``dev``)."""
+    """A format column tuple that may carry its device form (``dev``); a column whose host form is
+    still to be built holds only its kind plus ``src`` = (LineSpans, kind, field, delims)."""
     dev = None
+    src = None
+
+
+def host_column(c):
+    """The host form of a ``format_lines`` column (builds a deferred raw-line column)."""
+    if isinstance(c, _Col) and c.src is not None:
+        spans, kind, field, delims = c.src
+        owner, a, n = spans.spans()
+        col = _Col(("r", owner, a, n, delims) if kind == "r" else (kind, owner, a, n, int(field), delims))
+        col.dev = c.dev
+        return col
+    return c
 
 
 class _FileSpans(LineSpans):

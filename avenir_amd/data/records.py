@@ -33,6 +33,7 @@ from typing import Sequence
 import torch
 
 from .. import _native
+from .lines import host_column
 
 #: bytes of a shard below which a GPU job tokenizes on the host and copies the table over
 DEVICE_MIN_BYTES = int(os.environ.get("AVMI_GPU_RECORDS_MIN_BYTES", str(4 << 20)))
@@ -378,8 +379,10 @@ def format_lines(cols: list[tuple], n: int, delim: str = ",", path: str | None =
                 w = C.format_device(dcols[0], int(n), delim, str(path), bool(append), _threads(), dcols[1])
                 if w >= 0:
                     return w
-            return C.format_columns_file(cols, int(n), delim, _threads(), str(path), bool(append))
-        return C.format_columns(cols, int(n), delim, _threads())
+            return C.format_columns_file([host_column(c) for c in cols], int(n), delim, _threads(), str(path),
+                                         bool(append))
+        return C.format_columns([host_column(c) for c in cols], int(n), delim, _threads())
+    cols = [host_column(c) for c in cols]
     if path is not None:
         data = format_lines(cols, n, delim)
         with open(path, "ab" if append else "wb") as fh:

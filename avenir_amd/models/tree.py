@@ -442,18 +442,22 @@ class DecisionPathModel:
         table) — the last two keep every step on the table's device."""
         n, P = cols.n, len(self.paths)
         dev = cols.device
-        M = torch.ones((n, P), dtype=torch.bool, device=dev)
+        # the first matching path per record: paths visited last to first, each a chain of 1-D
+        # boolean ANDs and one select (no [N, P] match matrix: contiguous passes only)
         cache: dict[str, torch.Tensor] = {}
-        for j, p in enumerate(self.paths):
-            for pr in p["predicates"]:
+        first = torch.full((n,), P, dtype=torch.int32, device=dev)
+        for j in range(P - 1, -1, -1):
+            m = None
+            for pr in self.paths[j]["predicates"]:
                 ps = pr["predicateStr"]
                 if ps == ROOT:
                     continue
                 if ps not in cache:
                     cache[ps] = self._pred(cols, ps)
-                M[:, j] &= cache[ps]
-        any_ = M.any(1)
-        first = torch.where(any_, M.int().argmax(1), torch.full((n,), -1, dtype=torch.long, device=dev))
+                m = cache[ps].clone() if m is None else m.logical_and_(cache[ps])
+            first = torch.where(m, j, first) if m is not None else torch.full_like(first, j)
+        first = first.long()
+        first = torch.where(first < P, first, torch.full_like(first, -1))
         ci = {c: i for i, c in enumerate(self.class_values)}
         tab = torch.zeros((P + 1, len(ci)), dtype=torch.float64)
         for j, p in enumerate(self.paths):
