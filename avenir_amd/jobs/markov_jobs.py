@@ -6,6 +6,7 @@ import math
 from collections import defaultdict
 
 import torch
+from ..ops.encode_ops import unique_rows
 
 from .common import JobContext, fmt, job
 
@@ -195,7 +196,7 @@ def _stream_windows(ctx, rec, pref_ords, dfo, L):
     if tok.numel() == 0:
         return torch.zeros((0, L), dtype=torch.int32, device=dev), P[:0]
     if P.shape[1]:
-        _, g = torch.unique(P, dim=0, return_inverse=True)
+        _, g = unique_rows(P, True)
     else:
         g = torch.zeros_like(tok)
     order = torch.argsort(g, stable=True)
@@ -229,7 +230,7 @@ def _ngram_rows(T: torch.Tensor, P: torch.Tensor, L: int, streaming: bool) -> to
     S = uv.numel()
     dense = torch.where(valid, torch.searchsorted(uv, T.clamp_min(0)), torch.full_like(T, -1)).int()
     if k:
-        gk, ginv = torch.unique(P.long(), dim=0, return_inverse=True)
+        gk, ginv = unique_rows(P.long(), True)
     else:
         gk, ginv = torch.zeros((1, 0), dtype=torch.long, device=dev), torch.zeros(N, dtype=torch.long, device=dev)
     base = S + 1
@@ -289,7 +290,7 @@ def _emit_pst(ctx, rec, rows: torch.Tensor, k: int, L: int, root: str) -> None:
     if rows.numel() == 0:
         ctx.emit_root_text(b"")
         return
-    key, inv = torch.unique(rows[:, :-1], dim=0, return_inverse=True)
+    key, inv = unique_rows(rows[:, :-1], True)
     cnt = torch.zeros(key.shape[0], dtype=torch.long).index_add_(0, inv, rows[:, -1])
     codes = key[:, : k + L]
     is_root = key[:, k + L].bool()
@@ -396,17 +397,17 @@ def cgs(args):
     rec = ctx.records(modes="d" * k, tail_mode="x")
     ok = rec.lens() >= k
     S = torch.stack([rec.field(j)[ok].long() for j in range(k)], 1) if k else torch.zeros((0, 0), dtype=torch.long)
-    S = torch.unique(S, dim=0) if S.shape[0] else S
+    S = unique_rows(S) if S.shape[0] else S
     if comm.is_distributed:
         cdev = comm.device if comm.pg_backend == "nccl" else torch.device("cpu")
         S = comm.all_gather_v(S.to(cdev)).to(rec.device)
-        S = torch.unique(S, dim=0) if S.shape[0] else S
+        S = unique_rows(S) if S.shape[0] else S
     if S.shape[0] == 0:
         ctx.emit_root_text(b"")
         return
     keys, pos = sorted_keys(rec, S.reshape(-1))          # token code -> string rank (every rank alike)
     R = pos[S].int()
-    R = torch.unique(R, dim=0)                           # lexicographic = tuple-of-strings order
+    R = unique_rows(R)                           # lexicographic = tuple-of-strings order
     lo, hi = shard_range(R.shape[0], comm.rank, comm.world) if comm.is_distributed else (0, R.shape[0])
     C = SO.gsp_join(R.to(ctx.device).contiguous(), lo, hi)
     if comm.is_distributed:
@@ -414,7 +415,7 @@ def cgs(args):
         C = comm.all_gather_v(C.to(cdev))
     if not ctx.is_root:
         return
-    C = torch.unique(C.cpu().long(), dim=0) if C.numel() else C.cpu().long().view(0, k + 1)
+    C = unique_rows(C.cpu().long()) if C.numel() else C.cpu().long().view(0, k + 1)
     kc = keys.cpu()
     cols = [("s", rec.vocab, kc[C[:, j]].int().contiguous()) for j in range(k + 1)]
     ctx.emit_root_columns(cols, int(C.shape[0]))
@@ -654,7 +655,7 @@ def _cont_time_native(ctx, rec, rates, kl, states, horizon, stat, targets):
     S = len(states)
     n = rec.n_lines
     kc = torch.stack([rec.field(j).long() for j in range(kl)], 1) if kl else torch.zeros((n, 0), dtype=torch.long)
-    uk, inv = torch.unique(kc, dim=0, return_inverse=True) if n else (torch.zeros((0, kl), dtype=torch.long),
+    uk, inv = unique_rows(kc, True) if n else (torch.zeros((0, kl), dtype=torch.long),
                                                                       torch.zeros(0, dtype=torch.long))
     P = torch.zeros((uk.shape[0], S, S), dtype=torch.float64)
     Dw = torch.zeros((uk.shape[0], S, S), dtype=torch.float64)
@@ -908,7 +909,7 @@ def time_delay(args):
     end = torch.nonzero(segment_rank(first) >= w - 1).view(-1)
     win = sym[end.view(-1, 1) - (w - 1) + torch.arange(w, device=sym.device).view(1, -1)]   # [n_win, w]
     a, b = shard_range(G, comm.rank, comm.world) if comm.is_distributed else (0, G)
-    uwin, winv = torch.unique(win, dim=0, return_inverse=True) if win.numel() else (win, win[:, 0])
+    uwin, winv = unique_rows(win, True) if win.numel() else (win, win[:, 0])
     # window strings (few distinct): their string order decides the output order inside a key
     wstr = [":".join(rec.vocab[c] for c in row) for row in uwin.cpu().tolist()]
     wrank = torch.empty(len(wstr), dtype=torch.long)

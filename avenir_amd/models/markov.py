@@ -21,6 +21,7 @@ from dataclasses import dataclass, field
 from pathlib import Path
 
 import torch
+from ..ops.encode_ops import unique_rows
 
 from ..ops import histogram as H
 from ..ops import sequence_ops as SO
@@ -571,7 +572,7 @@ def gsp_candidates_device(seqs: list[tuple[str, ...]], device="cpu", comm: Comm 
     C = SO.gsp_join(X, lo, hi)
     if comm.is_distributed:
         C = comm.all_gather_v(C.cpu() if comm.backend == "gloo" else C)
-    C = torch.unique(C.cpu(), dim=0) if C.numel() else C.cpu().view(0, k + 1)
+    C = unique_rows(C.cpu()) if C.numel() else C.cpu().view(0, k + 1)
     return [tuple(vocab[i] for i in row) for row in C.tolist()]
 
 
@@ -585,7 +586,7 @@ def dot_matrix_similarity(A: torch.Tensor, B: torch.Tensor, window: int = 3) -> 
     vb = (wb >= 0).all(-1)
     # dense window ids shared by both sides (exact: no hashing), -1 for windows with padding
     allw = torch.cat([wa.reshape(-1, window), wb.reshape(-1, window)])
-    _, inv = torch.unique(allw, dim=0, return_inverse=True)
+    _, inv = unique_rows(allw, True)
     ida = torch.where(va, inv[: wa.shape[0] * wa.shape[1]].view(va.shape), torch.full_like(va, -1, dtype=torch.long))
     idb = torch.where(vb, inv[wa.shape[0] * wa.shape[1]:].view(vb.shape), torch.full_like(vb, -1, dtype=torch.long))
     hits = SO.dot_matrix_hits(ida.to(torch.int32), idb.to(torch.int32)).double()

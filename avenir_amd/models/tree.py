@@ -679,27 +679,29 @@ class DecisionTreeBuilder:
         nb_f = [f for f, fs in enumerate(space) if not fs.binary and len(fs.splits)]
         Gmax = max([s.n_seg for f in nb_f for s in space[f].splits] + [2])
         Bmax = max([space[f].n_bins for f in nb_f] + [1])
-        seg_tensors = {}
+        seg_np = {}
         nb_rows = []                              # (feature, split) of every explicit split, in order
         for f in nb_f:
             fs = space[f]
-            S = len(fs.splits)
-            M = torch.zeros((S, Gmax, fs.n_bins), dtype=torch.float64)
+            S, B = len(fs.splits), fs.n_bins
+            M = np.zeros((S, Gmax, B))
             for si, sp in enumerate(fs.splits):
-                for b, g in enumerate(sp.segmap):
-                    M[si, g, b] = 1.0
-            seg_tensors[f] = M.to(dev)
+                M[si, np.asarray(sp.segmap, dtype=np.int64), np.arange(len(sp.segmap))] = 1.0
+            seg_np[f] = M
             nb_rows += [(f, s) for s in range(S)]
+        seg_tensors = {f: torch.from_numpy(M).to(dev) for f, M in seg_np.items()}
         if nb_rows:
             # per explicit split: its [Gmax, Bmax] segment map and the histogram column of each bin
             # (TBt = an all-zero column appended for the padding bins)
-            allseg = torch.zeros((len(nb_rows), Gmax, Bmax), dtype=torch.float64)
-            splitcol = torch.full((len(nb_rows), Bmax), TBt, dtype=torch.long)
-            for r, (f, s) in enumerate(nb_rows):
-                B = space[f].n_bins
-                allseg[r, :, :B] = seg_tensors[f][s].cpu()
-                splitcol[r, :B] = torch.arange(offs[f], offs[f] + B)
-            allseg, splitcol = allseg.to(dev), splitcol.to(dev)
+            allseg = np.zeros((len(nb_rows), Gmax, Bmax))
+            splitcol = np.full((len(nb_rows), Bmax), TBt, dtype=np.int64)
+            r = 0
+            for f in nb_f:
+                S, B = seg_np[f].shape[0], space[f].n_bins
+                allseg[r:r + S, :, :B] = seg_np[f]
+                splitcol[r:r + S, :B] = np.arange(offs[f], offs[f] + B)
+                r += S
+            allseg, splitcol = torch.from_numpy(allseg).to(dev), torch.from_numpy(splitcol).to(dev)
 
         # binary-threshold features are scored together: one segmented cumsum over their bins
         bin_f = [f for f, fs in enumerate(space) if fs.binary]
@@ -824,7 +826,9 @@ class DecisionTreeBuilder:
             top_h = flat[: A * k].long().view(A, k).tolist()
             topv_h = flat[A * k: 2 * A * k].view(A, k).tolist()
             o3 = 2 * A * k + A * k * G2 * C
-            segc_h = flat[2 * A * k: o3].view(A, k, G2, C).long()
+            segc_np = flat[2 * A * k: o3].view(A, k, G2, C).numpy()
+            pop_h = segc_np.sum(-1).astype(np.int64).tolist()                       # [A][k][G2]
+            prob_h = (segc_np / np.maximum(segc_np.sum(-1, keepdims=True), 1)).tolist()
             cinfo_h = flat[o3:].view(A, k, G2).tolist()
             # ---- choose (randomAmongTop: per-tree RNG among the finite top-k) ----
             pick = [-1] * A
@@ -839,9 +843,9 @@ class DecisionTreeBuilder:
             derived: list[tuple[int, int, list[int]]] = []   # (global child, parent slot, built sibling gis)
             max_bins = max(bins)
             max_seg = G2
-            split_feat = torch.full((A,), -1, dtype=torch.int32)
-            segmap = torch.full((A, max_bins), -1, dtype=torch.int16)
-            child_of = torch.full((A, max_seg), -1, dtype=torch.int32)
+            split_feat = np.full((A,), -1, dtype=np.int32)
+            segmap = np.full((A, max_bins), -1, dtype=np.int16)
+            child_of = np.full((A, max_seg), -1, dtype=np.int32)
             for a, gi in enumerate(frontier):
                 nd = nodes[gi]
                 if pick[a] < 0:
@@ -862,22 +866,21 @@ class DecisionTreeBuilder:
                 else:
                     sp = fs.splits[s]
                     sm, preds, ng = sp.segmap, sp.predicates, sp.n_seg
-                sc = segc_h[a, pick[a], :ng]
+                pk = pick[a]
                 nd.feature, nd.split, nd.segmap = f, s, list(sm)
                 nd.children = []
                 split_feat[a] = f
-                segmap[a, : len(sm)] = torch.tensor(sm, dtype=torch.int16)
+                segmap[a, : len(sm)] = sm
                 kids = []
                 for g in range(ng):
-                    cntg = sc[g]
-                    pop = int(cntg.sum())
+                    pop = pop_h[a][pk][g]
                     if pop == 0:
                         nd.children.append(-1)
                         continue
-                    info = cinfo_h[a][pick[a]][g]                    # segment impurity from the device
+                    info = cinfo_h[a][pk][g]                         # segment impurity from the device
                     depth = nd.depth + 1   # parentPredicates.size() + 1 (DecisionTreeBuilder.java:606)
                     stop = self._should_stop(pop, info, nd.info, depth) or info == 0.0
-                    child = Node(nd.predicates + [preds[g]], pop, info, (cntg.double() / pop).tolist(),
+                    child = Node(nd.predicates + [preds[g]], pop, info, prob_h[a][pk][g],
                                  depth, stopped=stop, used_attrs=nd.used_attrs | {f})
                     ci = len(nodes)
                     nodes.append(child)
@@ -901,7 +904,8 @@ class DecisionTreeBuilder:
             for j, (ci, a, _) in enumerate(derived):
                 g = nodes[frontier[a]].children.index(ci)
                 child_of[a, g] = m + j
-            T.tree_assign(codes, n, node, split_feat.to(dev), segmap.to(dev), child_of.to(dev))
+            T.tree_assign(codes, n, node, torch.from_numpy(split_feat).to(dev), torch.from_numpy(segmap).to(dev),
+                          torch.from_numpy(child_of).to(dev))
             if new_frontier or derived:
                 hs = T.node_histogram(codes, n, labels, node, weight, bins, C, m,   # built children only
                                       rows_of(new_frontier))
@@ -911,9 +915,10 @@ class DecisionTreeBuilder:
                 if derived:
                     pa = torch.tensor([a for _, a, _ in derived], device=dev)
                     dh = hist[pa].clone()
-                    for j, (ci, a, sibs) in enumerate(derived):
-                        for sg in sibs:
-                            dh[j] -= hs[slot[sg]]
+                    jj = [j for j, (_, _, sibs) in enumerate(derived) for _ in sibs]
+                    ss = [slot[sg] for _, _, sibs in derived for sg in sibs]
+                    if jj:   # parent minus its built siblings, one scatter for the level
+                        dh.index_add_(0, torch.tensor(jj, device=dev), hs[torch.tensor(ss, device=dev)], alpha=-1)
                     parts.append(dh)
                 hist = torch.cat(parts) if len(parts) > 1 else hs
             frontier = new_frontier + [ci for ci, _, _ in derived]

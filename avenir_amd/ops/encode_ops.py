@@ -121,3 +121,33 @@ def loo_apply(codes: torch.Tensor, n: int, y: torch.Tensor, s: torch.Tensor, k: 
             v = v * (1 + amp * (2 * noise[j, :n].double() - 1))
         cols.append(v.float())
     return torch.stack(cols, 1) if cols else torch.zeros((n, 0))
+
+
+def unique_rows(X: torch.Tensor, return_inverse: bool = False):
+    """``torch.unique(X, dim=0)`` (rows in lexicographic order, optionally the inverse) for integer
+    rows.  When the per-column value ranges multiply to less than 2^62 the rows are packed into one
+    int64 key first, so the work is a 1-D sort instead of the row-wise unique (140 ms for
+    16.7 M x 2 rows on an MI355X against a few ms); otherwise the row-wise unique."""
+    if X.dim() != 2 or X.shape[0] == 0 or X.shape[1] == 0 or X.is_floating_point():
+        return torch.unique(X, dim=0, return_inverse=return_inverse)
+    Xl = X.long()
+    lo = Xl.min(0).values
+    span = (Xl.max(0).values - lo + 1).tolist()
+    total = 1
+    for s in span:
+        total *= int(s)
+    if total >= 1 << 62:
+        return torch.unique(X, dim=0, return_inverse=return_inverse)
+    key = torch.zeros(X.shape[0], dtype=torch.long, device=X.device)
+    for j, s in enumerate(span):                # first column most significant: lexicographic order
+        key = key * int(s) + (Xl[:, j] - lo[j])
+    if return_inverse:
+        uk, inv = torch.unique(key, return_inverse=True)
+    else:
+        uk, inv = torch.unique(key), None
+    cols = []
+    for j in range(len(span) - 1, -1, -1):
+        cols.append(uk % span[j] + lo[j])
+        uk = uk // span[j]
+    U = torch.stack(cols[::-1], 1).to(X.dtype)
+    return (U, inv) if return_inverse else U

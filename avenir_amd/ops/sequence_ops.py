@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+from .encode_ops import unique_rows
 
 from .. import _native
 from ..utils.tracing import traced
@@ -345,7 +346,7 @@ def gsp_join(X: torch.Tensor, lo: int = 0, hi: int | None = None) -> torch.Tenso
     """GSP candidate self-join (K18): X int [N, k] token-id rows; left rows [lo, hi) of the
     lexicographically sorted unique rows are joined with every row b whose b[:-1] equals their
     a[1:], giving a ++ b[-1].  Returns int32 [M, k+1] (left-row order, partners in sorted order)."""
-    X = torch.unique(X.to(torch.int32), dim=0) if X.numel() else X.to(torch.int32)
+    X = unique_rows(X.to(torch.int32)) if X.numel() else X.to(torch.int32)
     N, k = X.shape
     hi = N if hi is None else hi
     if X.is_cuda:
@@ -354,7 +355,7 @@ def gsp_join(X: torch.Tensor, lo: int = 0, hi: int | None = None) -> torch.Tenso
         return torch.zeros((0, k + 1), dtype=torch.int32)
     # oracle: dense ids of the (k-1)-grams, partners found by searchsorted over sorted prefix ids
     both = torch.cat([X[:, :-1], X[:, 1:]])
-    _, inv = torch.unique(both, dim=0, return_inverse=True)
+    _, inv = unique_rows(both, True)
     pid, sid = inv[:N], inv[N:]
     order = torch.argsort(pid, stable=True)
     ps = pid[order]

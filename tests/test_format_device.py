@@ -92,13 +92,15 @@ def test_format_lines_uses_device_twin(cuda, tmp_path, monkeypatch):
 @pytest.mark.gpu
 def test_device_repr_equals_python(cuda, tmp_path):
     """prec -2 (Python repr, the shortest round-trip digits) on the device: the same bytes as
-    ``repr`` for random magnitudes 1e-12 .. 1e15, powers of two and their neighbours, decimal
+    ``repr`` for random magnitudes 1e-10 .. 1e16, powers of two and their neighbours, decimal
     fractions, signed zero and the non-finite values; values outside the exact 128-bit path
     (here 1e300) send the whole column to the host formatter (-1)."""
     import math
     g = torch.Generator().manual_seed(3)
     n = 200000
-    x = torch.randn(n, generator=g, dtype=torch.float64) * 10 ** torch.randint(-12, 15, (n,), generator=g).double()
+    # |x| in [1e-10, 1e16): at most 31 fraction digits, the device path's whole range
+    sign = torch.where(torch.rand(n, generator=g) < 0.5, -1.0, 1.0).double()
+    x = sign * (0.1 + 9.9 * torch.rand(n, generator=g, dtype=torch.float64)) * 10.0 ** torch.randint(-9, 15, (n,), generator=g).double()
     extra = [0.1, 0.2, 0.3, 1 / 3, 2 / 3, 1e-4, 1e-5, 9.999999999999999e-05, 1e15, 123456789.0, 0.5, 2.675, 1.005,
              -0.0, 0.0, 4503599627370496.0, 12.0, 100.0, float("nan"), float("inf"), float("-inf")]
     extra += [s * math.ldexp(1.0, k) for k in range(-40, 52) for s in (1, -1)]
