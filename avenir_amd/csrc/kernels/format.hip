@@ -119,7 +119,8 @@ __device__ __forceinline__ bool put_fixed(Sink& s, double v, int p) {
 //   rounding interval:  (4m - 2) 5^k <= D 2^(s+2) <= (4m + 2) 5^k
 // (bounds included only for even m; the lower bound is (4m - 1) 5^k when m = 2^52 — the gap below
 // a power of two is half the gap above — and then D + 1 is tried too).  Every product stays below
-// 2^128 (m 5^31 < 2^125).  False outside that range (|v| >= 2^53, subnormals, values needing more
+// 2^128 (m 5^31 < 2^125); k = -e fraction digits are exact, so the loop ends by then.  False
+// outside that range (|v| >= 2^53, subnormals, values needing more
 // than 31 fraction digits): the host formatter takes over.
 __device__ __forceinline__ bool put_repr(Sink& s, double v) {
   if (v != v) {
@@ -143,7 +144,7 @@ __device__ __forceinline__ bool put_repr(Sink& s, double v) {
   if (be == 0) return false;  // subnormal
   const uint64_t m = frac | (1ull << 52);
   const int sh = 1075 - be;   // -e
-  if (sh < 1) return false;
+  if (sh < 0) return false;   // |v| >= 2^53
   const bool even = (m & 1ull) == 0, pow2 = frac == 0 && be > 1;
   const unsigned __int128 one = 1;
   unsigned __int128 p5 = 1;
@@ -153,11 +154,13 @@ __device__ __forceinline__ bool put_repr(Sink& s, double v) {
   for (; k <= 31; ++k, p5 *= 5u) {
     const int s2 = sh - k;
     if (s2 > 125) continue;  // D would be 0
-    if (s2 < 1) return false;
+    if (s2 < 0) return false;  // unreachable: k = -e digits are exact (s2 = 0)
     const unsigned __int128 N = (unsigned __int128)m * p5;
     unsigned __int128 q = N >> s2;
-    const unsigned __int128 r = N - (q << s2), half = one << (s2 - 1);
-    if (r > half || (r == half && (q & 1u))) ++q;
+    if (s2 > 0) {
+      const unsigned __int128 r = N - (q << s2), half = one << (s2 - 1);
+      if (r > half || (r == half && (q & 1u))) ++q;
+    }
     const unsigned __int128 hi = ((unsigned __int128)(4 * m + 2)) * p5;
     const unsigned __int128 lo = ((unsigned __int128)(pow2 ? 4 * m - 1 : 4 * m - 2)) * p5;
     for (int t = 0; t < (pow2 ? 2 : 1) && !found; ++t) {

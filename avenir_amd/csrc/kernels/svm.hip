@@ -1595,10 +1595,16 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
     AV_HIP_CHECK(hipGetLastError());
     const int m = parts * h;
     // rank merge up to 256 candidates per side (N <= 8192: 7.0 us against 10.4 us for the radix
-    // merge, profiles/r3_svm_v6_kernel_stats.txt); beyond that its O(M^2) LDS reads stop paying
-    if (m <= 256 && !env_off("AVMI_SMO_RANK_MERGE")) {
+    // merge, profiles/r3_svm_v6_kernel_stats.txt); 512 per side (N = 32768) is an A/B switch
+    // (AVMI_SMO_RANK_MERGE_MAX=512) until measured: its O(M^2) LDS reads double again
+    static const int rank_max = [] {
+      const char* e = std::getenv("AVMI_SMO_RANK_MERGE_MAX");
+      return e && std::atoi(e) >= 512 ? 512 : 256;
+    }();
+    if (m <= rank_max && !env_off("AVMI_SMO_RANK_MERGE")) {
       if (m <= 128) smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
-      else smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      else if (m <= 256) smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      else smo_ws_merge_rank_kernel<1024><<<B, 1024, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
       AV_HIP_CHECK(hipGetLastError());
       return;
     }

@@ -52,7 +52,7 @@ def bench_rf(a):
     for trees, depth in ((10, 8),):
         p = TreeParams(binary=True, stopping="maxDepth", max_depth=depth, sub_sampling="withReplace",
                        attr_selection="randomAll", max_bins=32)
-        sec, rf = timed(lambda: RandomForest(t.schema, trees, p, "sqrt").fit(t))
+        sec, rf = timed(lambda: RandomForest(t.schema, trees, p, "sqrt").fit(t), reps=3)
         emit(model="random_forest", rows=n, features=d, trees=trees, depth=depth, seconds=sec,
              rows_x_trees_per_s=n * trees / sec, build=getattr(rf, "build_stats", None))
         ps, _ = timed(lambda: rf.predict_proba(t), 3)
@@ -83,7 +83,7 @@ def bench_rf_ref(a):
     p = TreeParams(binary=False, stopping="maxDepth", max_depth=5, sub_sampling="withReplace",
                    attr_selection="randomNotUsedYet", random_attr_count=4, split_selection="randomAmongTop",
                    top_split_count=3, max_bins=8)
-    sec, rf = timed(lambda: RandomForest(t.schema, 10, p, "all").fit(t))
+    sec, rf = timed(lambda: RandomForest(t.schema, 10, p, "all").fit(t), reps=3)
     acc = float((rf.predict(t) == t.labels[:n].long()).float().mean())
     emit(model="random_forest_reference_splits", rows=n, features=d, trees=10, depth=5, max_split=3, seconds=sec,
          rows_x_trees_per_s=n * 10 / sec, train_acc=acc, build=getattr(rf, "build_stats", None))
