@@ -1045,6 +1045,135 @@ __global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __
                                 in_up);
 }
 
+// Wave max of u64 keys: the u32 DPP steps of wave_max_u32 on both halves (the pair compared as
+// one 64-bit value), the 4 row results over v_readlane; two independent maxima interleaved.
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_max64_step(unsigned long long v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTRL, 0xF, 0xF, true);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, true);
+  const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+  return o > v ? o : v;
+}
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ void wave_max2_u64(unsigned long long& u, unsigned long long& v) {
+  u = dpp_max64_step<0xB1>(u);
+  v = dpp_max64_step<0xB1>(v);
+  u = dpp_max64_step<0x4E>(u);
+  v = dpp_max64_step<0x4E>(v);
+  u = dpp_max64_step<0x124>(u);
+  v = dpp_max64_step<0x124>(v);
+  u = dpp_max64_step<0x128>(u);
+  v = dpp_max64_step<0x128>(v);
+  auto m4 = [](unsigned long long x) {
+    const unsigned long long a = readlane64(x, 0), b = readlane64(x, 16), c = readlane64(x, 32), d = readlane64(x, 48);
+    const unsigned long long ab = a > b ? a : b, cd = c > d ? c : d;
+    return ab > cd ? ab : cd;
+  };
+  u = m4(u);
+  v = m4(v);
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+  v = dpp_max64_step<0xB1>(v);
+  v = dpp_max64_step<0x4E>(v);
+  v = dpp_max64_step<0x124>(v);
+  v = dpp_max64_step<0x128>(v);
+  const unsigned long long a = readlane64(v, 0), b = readlane64(v, 16), c = readlane64(v, 32), d = readlane64(v, 48);
+  const unsigned long long ab = a > b ? a : b, cd = c > d ? c : d;
+  return ab > cd ? ab : cd;
+}
+
+// Register top-k part selection (two-level selection, first level): part p of problem b owns the
+// 64-row blocks p, p + parts, p + 2 parts, .. (block-cyclic: rows of one label or one cluster that
+// sit together in the input are spread over the parts), PER blocks per wave.  Every candidate is
+// one exact 64-bit key (order_key(violation) << 32 | ~row: larger = more violating, ties to the
+// lower row — the order of the radix selection and of the rank merge), so the selection is exact
+// and deterministic.  Each wave keeps its HP largest keys per side by HP wave-max steps (the owner
+// lane clears the winner), then waves 0 and 1 take the HP largest of the 16 waves' candidates of
+// side 0 / 1.  No radix passes and 2 barriers, against 12 for ws_select2_body.  The part's HP
+// candidates per side go to the rank merge; the global top h is exact whenever no part holds more
+// than HP of them (the host sizes HP to 2-4x a part's expected share of h; beyond that the working
+// set is a slightly different set of strong violators — any violating set keeps SMO convergent).
+template <int PER, int HP>
+__global__ __launch_bounds__(SEL_T) void smo_ws_topk_part_kernel(const float* __restrict__ alpha,
+                                                                 const float* __restrict__ G,
+                                                                 const float* __restrict__ y, int N, int ldag, float C,
+                                                                 int parts, int* __restrict__ cand,
+                                                                 int* __restrict__ cnt, float* __restrict__ candv,
+                                                                 const float* __restrict__ gap, float skip) {
+  static_assert(HP >= 4 && HP <= 64 && (16 * HP) % 64 == 0, "HP");
+  constexpr int NW = SEL_T / 64, R = NW * HP / 64;
+  __shared__ unsigned long long s_k[2][NW * HP];
+  const int b = blockIdx.y, p = blockIdx.x;
+  if (ws_done(gap, b, skip)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* ab = alpha + (long long)b * ldag;
+  const float* gb = G + (long long)b * ldag;
+  const float* yb = y + (long long)b * N;
+  unsigned long long key[2][PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const long long blk = (long long)(j * NW + wv) * parts + p;
+    const long long n = blk * 64 + lane;
+    key[0][j] = key[1][j] = 0ull;
+    if (n < N) {
+      const float yn = yb[n], an = ab[n], gn = gb[n];
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const float v = ws_violation(w, yn, an, gn, C);
+        if (v > -INFINITY) key[w][j] = ((unsigned long long)order_key(v) << 32) | (unsigned)~(unsigned)n;
+      }
+    }
+  }
+  for (int it = 0; it < HP; ++it) {  // the wave's HP largest per side
+    unsigned long long m0 = key[0][0], m1 = key[1][0];
+#pragma unroll
+    for (int j = 1; j < PER; ++j) {
+      m0 = key[0][j] > m0 ? key[0][j] : m0;
+      m1 = key[1][j] > m1 ? key[1][j] : m1;
+    }
+    wave_max2_u64(m0, m1);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {  // keys are unique (distinct rows); 0 = empty stays 0
+      if (key[0][j] == m0) key[0][j] = 0ull;
+      if (key[1][j] == m1) key[1][j] = 0ull;
+    }
+    if (lane == 0) {
+      s_k[0][wv * HP + it] = m0;
+      s_k[1][wv * HP + it] = m1;
+    }
+  }
+  __syncthreads();
+  if (wv >= 2) return;
+  const int w = wv;
+  unsigned long long c[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) c[r] = s_k[w][lane * R + r];
+  int* cb = cand + ((long long)b * parts + p) * 2 * HP + w * HP;
+  float* vb = candv + ((long long)b * parts + p) * 2 * HP + w * HP;
+  int np = 0;
+  for (int it = 0; it < HP; ++it) {
+    unsigned long long m = c[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) m = c[r] > m ? c[r] : m;
+    m = wave_max_u64(m);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (c[r] == m) c[r] = 0ull;
+    if (m == 0ull) break;  // wave-uniform: no further candidates
+    if (lane == 0) {
+      cb[it] = (int)~(unsigned)m;
+      vb[it] = order_key_inv((unsigned)(m >> 32));
+    }
+    ++np;
+  }
+  if (lane == 0) cnt[((long long)b * parts + p) * 2 + w] = np;
+}
+
 // Rank merge of the parts' candidates (replaces the radix merge for the two-level path): the
 // parts hand over (row, violation) pairs, so every candidate's 64-bit key (order_key(v) << 32 |
 // ~row: larger = more violating, ties to the lower row — the same order as the radix selection)
@@ -1054,7 +1183,7 @@ __global__ __launch_bounds__(NT) void smo_ws_select_merge_kernel(const float* __
 // and the low side's rows already chosen on the up side are marked unused.  3 barriers instead of
 // ~14.  NT = 2M threads (M = parts x h candidate slots per side, <= 512).
 template <int NT>
-__global__ __launch_bounds__(NT) void smo_ws_merge_rank_kernel(int h, int parts, const int* __restrict__ cand,
+__global__ __launch_bounds__(NT) void smo_ws_merge_rank_kernel(int h, int hp, int hs, int parts, const int* __restrict__ cand,
                                                                const int* __restrict__ cnt,
                                                                const float* __restrict__ candv,
                                                                long long* __restrict__ ws, bool* __restrict__ ok,
@@ -1067,16 +1196,16 @@ __global__ __launch_bounds__(NT) void smo_ws_merge_rank_kernel(int h, int parts,
   const int b = blockIdx.x, tid = threadIdx.x;
   if (ws_done(gap, b, skip)) return;
   const int w = tid / M, c = tid % M;
-  const int* cb = cand + (long long)b * parts * 2 * h;
-  const float* vb = candv + (long long)b * parts * 2 * h;
+  const int* cb = cand + (long long)b * parts * 2 * hs;
+  const float* vb = candv + (long long)b * parts * 2 * hs;
   const int* nb = cnt + (long long)b * parts * 2;
   int row = -1;
   float val = -INFINITY;
-  if (c < parts * h) {
-    const int q = c / h, s = c % h;
+  if (c < parts * hp) {  // part q's slot s (hp slots used of the stride hs)
+    const int q = c / hp, s = c % hp;
     if (s < nb[q * 2 + w]) {
-      row = cb[(q * 2 + w) * h + s];
-      val = vb[(q * 2 + w) * h + s];
+      row = cb[(q * 2 + w) * hs + s];
+      val = vb[(q * 2 + w) * hs + s];
     }
   }
   const unsigned long long mk = row >= 0 ? ((unsigned long long)order_key(val) << 32) | (unsigned)(~row) : 0ull;
@@ -1579,6 +1708,39 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
+  if (N > 4 * SEL_T && cand && per && !env_off("AVMI_SMO_TOPK") && h == 64) {
+    // register top-k parts + rank merge: 1 / 2 / 4 blocks of 64 rows per wave, HP = the power of
+    // two <= target / parts (target 128 candidates per side: the 256-thread merge)
+    static const int target = [] {
+      const char* e = std::getenv("AVMI_SMO_TOPK_M");
+      return e && std::atoi(e) >= 256 ? 256 : 128;
+    }();
+    const int tper = N <= 16 * 1024 ? 1 : (N <= 32 * 1024 ? 2 : 4);
+    const int tparts = (N + tper * SEL_T - 1) / (tper * SEL_T);
+    int hp = 64;
+    while (hp > 4 && tparts * hp > target) hp >>= 1;
+    const int old_parts = (N + per * SEL_T - 1) / (per * SEL_T);
+    if (tparts * hp <= target && tparts * hp >= h && tparts * hp <= old_parts * h) {
+      float* candv = reinterpret_cast<float*>(cand + (long long)B * old_parts * 2 * h);  // the allocation's layout
+      const dim3 pg(tparts, B);
+#define AV_TK(P, H) smo_ws_topk_part_kernel<P, H><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, tparts, cand, \
+      cnt, candv, gap, skip)
+#define AV_TKP(P) do { if (hp == 4) AV_TK(P, 4); else if (hp == 8) AV_TK(P, 8); else if (hp == 16) AV_TK(P, 16); \
+      else if (hp == 32) AV_TK(P, 32); else AV_TK(P, 64); } while (0)
+      if (tper == 1) AV_TKP(1);
+      else if (tper == 2) AV_TKP(2);
+      else AV_TKP(4);
+#undef AV_TKP
+#undef AV_TK
+      AV_HIP_CHECK(hipGetLastError());
+      if (tparts * hp <= 128)
+        smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, hp, hp, tparts, cand, cnt, candv, ws, ok, gap, skip);
+      else
+        smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, hp, hp, tparts, cand, cnt, candv, ws, ok, gap, skip);
+      AV_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if (N <= 4 * SEL_T) {
     smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap, skip);
   } else if (cand && per) {
@@ -1602,9 +1764,9 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
       return e && std::atoi(e) >= 512 ? 512 : 256;
     }();
     if (m <= rank_max && !env_off("AVMI_SMO_RANK_MERGE")) {
-      if (m <= 128) smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
-      else if (m <= 256) smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
-      else smo_ws_merge_rank_kernel<1024><<<B, 1024, 0, stream>>>(h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      if (m <= 128) smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, h, h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      else if (m <= 256) smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, h, h, parts, cand, cnt, candv, ws, ok, gap, skip);
+      else smo_ws_merge_rank_kernel<1024><<<B, 1024, 0, stream>>>(h, h, h, parts, cand, cnt, candv, ws, ok, gap, skip);
       AV_HIP_CHECK(hipGetLastError());
       return;
     }

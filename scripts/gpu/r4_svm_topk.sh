@@ -1,0 +1,9 @@
+# SVM: register top-k part selection (default) against the radix parts (AVMI_SMO_TOPK=0)
+set -o pipefail
+step() { "$@"; rc=$?; if [ $rc -gt 1 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
+step timeout -k 10 400 python -u -m pytest tests/test_svm_ws.py tests/test_svm_implicit.py tests/test_linear.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "svm or smo" > gpurun_out/r4_svm_topk_tests.log 2>&1
+step timeout -k 10 200 python -u benchmarks/bench_svm.py 8192,32768 ws > gpurun_out/r4_svm_topk.log 2>&1
+AVMI_SMO_TOPK_M=256 step timeout -k 10 200 python -u benchmarks/bench_svm.py 8192,32768 ws >> gpurun_out/r4_svm_topk.log 2>&1
+AVMI_SMO_TOPK=0 step timeout -k 10 200 python -u benchmarks/bench_svm.py 8192,32768 ws >> gpurun_out/r4_svm_topk.log 2>&1
+step timeout -k 10 300 python -u benchmarks/bench_vs_reference.py --only svm --svm-rows 8192 > gpurun_out/r4_svm_vsref.log 2>&1
+step timeout -k 10 300 python -u benchmarks/bench_vs_reference.py --only svm --svm-rows 32768 >> gpurun_out/r4_svm_vsref.log 2>&1
