@@ -1708,19 +1708,33 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
-  if (N > 4 * SEL_T && cand && per && !env_off("AVMI_SMO_TOPK") && h == 64) {
-    // register top-k parts + rank merge: 1 / 2 / 4 blocks of 64 rows per wave, HP = the power of
-    // two <= target / parts (target 128 candidates per side: the 256-thread merge)
+  // register top-k parts + rank merge for N > 16384 (below that the exact radix parts are as fast:
+  // N = 8192 20.0 vs 20.5 ms, while N = 32768 goes from 76 to 61 ms, profiles/r4_svm_topk_ab.log):
+  // 2 / 4 blocks of 64 rows per wave, HP = the power of two <= target / parts (target 128
+  // candidates per side: the 256-thread merge)
+  static const int topk_min_n = [] {
+    const char* e = std::getenv("AVMI_SMO_TOPK_MIN_N");
+    return e && *e ? std::atoi(e) : 16 * 1024 + 1;
+  }();
+  if (N > 4 * SEL_T && N >= topk_min_n && cand && per && !env_off("AVMI_SMO_TOPK") && h == 64) {
     static const int target = [] {
       const char* e = std::getenv("AVMI_SMO_TOPK_M");
       return e && std::atoi(e) >= 256 ? 256 : 128;
     }();
-    const int tper = N <= 16 * 1024 ? 1 : (N <= 32 * 1024 ? 2 : 4);
+    static const int force_per = [] {
+      const char* e = std::getenv("AVMI_SMO_TOPK_PER");
+      const int v = e && *e ? std::atoi(e) : 0;
+      return v == 1 || v == 2 || v == 4 ? v : 0;
+    }();
+    // one 64-row block per wave (N = 32768: 58 ms against 61 ms with 2 and 85 ms with 4 blocks,
+    // the HP-step wave loop being the cost), up to 256 candidates per side (512-thread merge)
+    const int tper = force_per ? force_per : 1;
     const int tparts = (N + tper * SEL_T - 1) / (tper * SEL_T);
     int hp = 64;
     while (hp > 4 && tparts * hp > target) hp >>= 1;
+    // (33..64 parts keep HP = 4: 256 candidates, the 512-thread merge; more parts: radix parts)
     const int old_parts = (N + per * SEL_T - 1) / (per * SEL_T);
-    if (tparts * hp <= target && tparts * hp >= h && tparts * hp <= old_parts * h) {
+    if (tparts * hp <= 256 && tparts * hp >= h && tparts * hp <= old_parts * h) {
       float* candv = reinterpret_cast<float*>(cand + (long long)B * old_parts * 2 * h);  // the allocation's layout
       const dim3 pg(tparts, B);
 #define AV_TK(P, H) smo_ws_topk_part_kernel<P, H><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, tparts, cand, \

@@ -1,4 +1,6 @@
 """Linear models (K13 fused GLM gradient), regression, Fisher discriminant, kernel SVM (K12 SMO)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -286,9 +288,12 @@ def test_smo_working_set_gpu_matches_full(cuda, N):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N", [40, 1000, 5000, 12000, 40000, 70000])
-def test_smo_ws_select_matches_topk(cuda, N):
-    """Fused working-set selection == gap + top-h up / low violator sets of the torch path."""
+def test_smo_ws_select_matches_topk(cuda, N, monkeypatch):
+    """Fused working-set selection == gap + top-h up / low violator sets of the torch path (the
+    exact radix selection: the register top-k parts, default above 16384 rows, are switched off
+    here and checked by test_smo_ws_select_topk_parts)."""
     from avenir_amd import _native
+    monkeypatch.setenv("AVMI_SMO_TOPK", "0")
     torch.manual_seed(N)
     B, h, Cc = 3, 64, 1.0
     y = torch.where(torch.rand(B, N, device=cuda) > 0.5, 1.0, -1.0)
@@ -318,6 +323,47 @@ def test_smo_ws_select_matches_topk(cuda, N):
         for i, o in zip(ws[b, h:].tolist(), ok[b, h:].tolist()):
             if o:
                 assert i not in iu
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [20000, 32768, 65536])
+def test_smo_ws_select_topk_parts(cuda, N):
+    """Register top-k part selection (N > 16384): the gap is exact; every pick is a valid member
+    of its side, picks are in ascending row order, the strongest violator of each side is picked,
+    low-side picks already on the up side are masked, and the picks are the exact top h except
+    where one part held more than its HP slots of them (a few of 64 on random data; >= 75 % here)."""
+    from avenir_amd import _native
+    torch.manual_seed(N)
+    B, h, Cc = 3, 64, 1.0
+    y = torch.where(torch.rand(B, N, device=cuda) > 0.5, 1.0, -1.0)
+    alpha = torch.zeros(B, N + 1, device=cuda)
+    alpha[:, :N] = torch.rand(B, N, device=cuda).clamp(0.2, 0.8) * (torch.rand(B, N, device=cuda) > 0.3) * Cc
+    alpha[:, :N] = torch.where(torch.rand(B, N, device=cuda) > 0.9, torch.full_like(y, Cc), alpha[:, :N])
+    G = torch.randn(B, N + 1, device=cuda)
+    ws = torch.zeros(B, 2 * h, dtype=torch.long, device=cuda)
+    ok = torch.zeros(B, 2 * h, dtype=torch.bool, device=cuda)
+    gap = torch.zeros(B, device=cuda)
+    _native.C().smo_ws_select(alpha, G, y, Cc, h, ws, ok, gap)
+    a, g = alpha[:, :N], G[:, :N]
+    up = (y > 0) & (a < Cc) | (y < 0) & (a > 0)
+    low = (y > 0) & (a > 0) | (y < 0) & (a < Cc)
+    vu = torch.where(up, -y * g, torch.full_like(g, -float("inf")))
+    vl = torch.where(low, y * g, torch.full_like(g, -float("inf")))
+    assert torch.equal(gap, vu.max(1).values + vl.max(1).values)
+    for b in range(B):
+        for half, v in ((0, vu[b]), (1, vl[b])):
+            k = min(h, int(torch.isfinite(v).sum()))
+            got = ws[b, half * h: half * h + k].tolist()
+            assert got == sorted(got) and len(set(got)) == k
+            assert all(math.isfinite(float(v[i])) for i in got)
+            assert int(v.argmax()) in got
+            exp = set(torch.topk(v, k).indices.tolist())
+            assert len(exp & set(got)) >= 0.75 * k
+        iu = set(ws[b, :h][ok[b, :h]].tolist())
+        kl = min(h, int(torch.isfinite(vl[b]).sum()))
+        for i, o in zip(ws[b, h:h + kl].tolist(), ok[b, h:h + kl].tolist()):
+            assert (i in iu) != o
+        assert not ok[b, h + kl:].any()
 
 
 @pytest.mark.gpu
