@@ -1730,8 +1730,14 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
     // the HP-step wave loop being the cost), up to 256 candidates per side (512-thread merge)
     const int tper = force_per ? force_per : 1;
     const int tparts = (N + tper * SEL_T - 1) / (tper * SEL_T);
+    static const int force_hp = [] {  // A/B: a fixed HP (4..64, power of two)
+      const char* e = std::getenv("AVMI_SMO_TOPK_HP");
+      const int v = e && *e ? std::atoi(e) : 0;
+      return v == 4 || v == 8 || v == 16 || v == 32 || v == 64 ? v : 0;
+    }();
     int hp = 64;
     while (hp > 4 && tparts * hp > target) hp >>= 1;
+    if (force_hp) hp = force_hp;
     // (33..64 parts keep HP = 4: 256 candidates, the 512-thread merge; more parts: radix parts)
     const int old_parts = (N + per * SEL_T - 1) / (per * SEL_T);
     if (tparts * hp <= 256 && tparts * hp >= h && tparts * hp <= old_parts * h) {
