@@ -232,6 +232,15 @@ __device__ __forceinline__ float order_key_inv(unsigned k) {
 // (127 - t) — ties (and values within 2^-16 relative) go to the lowest variable — one DPP chain
 // each instead of a (value, index) pair chain; the exact values for the stopping test come from
 // the owner lane (i's violation) or from a plain max of exact keys (the low-set maximum).
+// A wave-uniform value copied into a VGPR the compiler cannot prove uniform: the two-variable
+// update below then compiles to v_cndmask selects instead of ~20 scalar branches per iteration
+// (uniform compares of SGPR values become s_cbranch chains otherwise).
+__device__ __forceinline__ float as_divergent(float x) {
+  float r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 template <int E>
 __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (&a)[E], float (&g)[E],
                            const float (&qd)[E], float C, float epsl, int max_iter, int lane) {
@@ -252,10 +261,19 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
     const int i = 127 - (int)(ku & 0x7Fu);
     // i's state from its owner lane (the slot index is wave-uniform)
     const int si = i >> 6;
-    float yi = 0.f, ai = 0.f, gi_ = 0.f, Kii = 0.f;
+    float yi = rdl(y[0], i & 63), ai = rdl(a[0], i & 63), gi_ = rdl(g[0], i & 63), Kii = rdl(qd[0], i & 63);
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-      if (e == si) { yi = rdl(y[e], i & 63); ai = rdl(a[e], i & 63); gi_ = rdl(g[e], i & 63); Kii = rdl(qd[e], i & 63); }
+    for (int e = 1; e < E; ++e) {
+      const float y1 = rdl(y[e], i & 63), a1 = rdl(a[e], i & 63), g1 = rdl(g[e], i & 63), q1 = rdl(qd[e], i & 63);
+      yi = e == si ? y1 : yi;
+      ai = e == si ? a1 : ai;
+      gi_ = e == si ? g1 : gi_;
+      Kii = e == si ? q1 : Kii;
+    }
+    yi = as_divergent(yi);
+    ai = as_divergent(ai);
+    gi_ = as_divergent(gi_);
+    Kii = as_divergent(Kii);
     const float gmax = -yi * gi_;
     unsigned kj = 0u, km = 0u;
     float kit[E];  // row i of the block, kept for K[i][j] (a readlane) and the gradient update
@@ -280,15 +298,24 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
     if (gmax + gmax2 < epsl || kj == 0u) break;
     const int j = 127 - (int)(kj & 0x7Fu);
     const int sj = j >> 6;
-    float yj = 0.f, aj = 0.f, gj = 0.f, Kjj = 0.f;
+    float yj = rdl(y[0], j & 63), aj = rdl(a[0], j & 63), gj = rdl(g[0], j & 63), Kjj = rdl(qd[0], j & 63);
+    float kij = rdl(kit[0], j & 63);  // K[i][j] from the owner lane of the cached row (no LDS round trip)
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-      if (e == sj) { yj = rdl(y[e], j & 63); aj = rdl(a[e], j & 63); gj = rdl(g[e], j & 63); Kjj = rdl(qd[e], j & 63); }
+    for (int e = 1; e < E; ++e) {
+      const float y1 = rdl(y[e], j & 63), a1 = rdl(a[e], j & 63), g1 = rdl(g[e], j & 63), q1 = rdl(qd[e], j & 63);
+      const float k1 = rdl(kit[e], j & 63);
+      yj = e == sj ? y1 : yj;
+      aj = e == sj ? a1 : aj;
+      gj = e == sj ? g1 : gj;
+      Kjj = e == sj ? q1 : Kjj;
+      kij = e == sj ? k1 : kij;
+    }
+    yj = as_divergent(yj);
+    aj = as_divergent(aj);
+    gj = as_divergent(gj);
+    Kjj = as_divergent(Kjj);
+    kij = as_divergent(kij);
     const float oi = ai, oj = aj;
-    float kij = 0.f;  // K[i][j] from the owner lane of the cached row (no LDS round trip)
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-      if (e == sj) kij = rdl(kit[e], j & 63);
     float quad = Kii + Kjj - 2.f * kij;
     quad = quad > 0.f ? quad : TAU;
     // num / quad: hardware reciprocal + one residual correction (within an ulp of the IEEE
@@ -306,15 +333,17 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       // opposite labels: ai - aj = diff is kept; same labels: ai + aj = sum is kept
       const float diff = ai - aj, sum = ai + aj;
       float pi = opp ? ai + delta : ai - delta, pj = aj + delta;
-      // first clip
+      // first clip (conditions combined with bitwise ops: no short-circuit branches)
       const bool dpos = diff > 0.f, spos = sum > C;
-      const bool c1 = opp ? (dpos ? pj < 0.f : pi < 0.f) : (spos ? pi > C : pj < 0.f);
+      const bool c1 = (opp & dpos & (pj < 0.f)) | (opp & !dpos & (pi < 0.f)) | (!opp & spos & (pi > C)) |
+                      (!opp & !spos & (pj < 0.f));
       const float ci = opp ? (dpos ? diff : 0.f) : (spos ? C : sum);
       const float cj = opp ? (dpos ? 0.f : -diff) : (spos ? sum - C : 0.f);
       pi = c1 ? ci : pi;
       pj = c1 ? cj : pj;
       // second clip
-      const bool c2 = opp ? (dpos ? pi > C : pj > C) : (spos ? pj > C : pi < 0.f);
+      const bool c2 = (opp & dpos & (pi > C)) | (opp & !dpos & (pj > C)) | (!opp & spos & (pj > C)) |
+                      (!opp & !spos & (pi < 0.f));
       const float di_ = opp ? (dpos ? C : C + diff) : (spos ? sum - C : 0.f);
       const float dj_ = opp ? (dpos ? C - diff : C) : (spos ? C : sum);
       ai = c2 ? di_ : pi;
