@@ -1573,13 +1573,14 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
   auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
   auto Kws = at::empty({B, Q, Q}, K.options());
   auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
+  auto gap_next = at::empty({B}, y.options());
   return avk::smo_ws_run(K.data_ptr<float>(), (int)N, alpha.data_ptr<float>(), G.data_ptr<float>(),
                          y.data_ptr<float>(), (int)B, (int)alpha.size(1), (float)C, (float)eps, (int)inner_iter,
                          (float)rel_tol, max_outer, (int)check_every,
                          reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
                          gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
-                         host_gap.data_ptr<float>(), kbs, cur_stream(y), nullptr);
+                         host_gap.data_ptr<float>(), kbs, cur_stream(y), nullptr, gap_next.data_ptr<float>());
 }
 
 // implicit kernel source from X [B or 1, N, D] (or [N, D]) and its squared norms

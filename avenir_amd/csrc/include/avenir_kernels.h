@@ -148,7 +148,8 @@ void svm_kernel_matrix_mfma(const SvmKerX& a, const float* Bx, const float* bn, 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, long long kbs, hipStream_t stream, const SvmKerX* kx = nullptr);
+                     float* host_gap, long long kbs, hipStream_t stream, const SvmKerX* kx = nullptr,
+                     float* gap_next = nullptr);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
                         long long* inner_total, float* Kws, float rel_tol, long long kbs, hipStream_t stream);

@@ -480,10 +480,14 @@ __global__ __launch_bounds__(WSS_T) void smo_ws_solve_kernel(const float* __rest
                                                           const float* __restrict__ G, const float* __restrict__ yv,
                                                           int N, int ldag, const float* __restrict__ gap, float C,
                                                           float eps, float rel_tol, int max_iter,
-                                                          float* __restrict__ dA, long long* __restrict__ inner_total) {
+                                                          float* __restrict__ dA, long long* __restrict__ inner_total,
+                                                          float* __restrict__ gap_out = nullptr) {
   constexpr int Q = WS_Q, E = Q / 64;
   __shared__ __attribute__((aligned(16))) float Ks[Q][Q];
   const int b = blockIdx.x, lane = threadIdx.x;
+  // fused merge + gather: ``gap`` is this step's gap (written by the merge), published to the
+  // step's ``gap_out`` for the update and the next selection (the merge reads the previous one)
+  if (gap_out && threadIdx.x == 0) gap_out[b] = gap[b];
   if (ws_done(gap, b, eps)) {  // converged: zero iterations, alpha unchanged, dA = 0
     for (int t = threadIdx.x; t < Q; t += WSS_T) dA[(long long)b * Q + t] = 0.f;
     return;
@@ -1279,6 +1283,98 @@ __global__ __launch_bounds__(NT) void smo_ws_merge_rank_kernel(int h, int hp, in
   }
 }
 
+// The rank merge fused into the K[ws, ws] gather: every one of the Q x B gather workgroups repeats
+// the (small, deterministic) merge of the parts' candidates in LDS — identical in all of them —
+// and gathers its row p of the block; workgroup 0 also writes ws / ok and this step's gap into
+// ``gap_next`` (the previous step's gap in ``gap`` stays untouched for the other workgroups'
+// converged test; the solve publishes gap_next).  One launch and one dependent global round trip
+// less per outer step than merge + gather.
+template <int NT>
+__global__ __launch_bounds__(NT) void smo_ws_merge_gather_kernel(int h, int hp, int hs, int parts,
+                                                                 const int* __restrict__ cand,
+                                                                 const int* __restrict__ cnt,
+                                                                 const float* __restrict__ candv,
+                                                                 long long* __restrict__ ws, bool* __restrict__ ok,
+                                                                 const float* __restrict__ gap,
+                                                                 float* __restrict__ gap_next, float skip,
+                                                                 const float* __restrict__ K, int N, long long kbs,
+                                                                 float* __restrict__ Kws) {
+  constexpr int M = NT / 2, Q = WS_Q;
+  __shared__ __attribute__((aligned(16))) unsigned long long key[2][M];
+  __shared__ int sel[2][64];
+  __shared__ float s_max[2];
+  __shared__ int s_cnt[2];
+  __shared__ long long s_ws[Q];
+  __shared__ int s_ok[Q];
+  const int b = blockIdx.y, p = blockIdx.x, tid = threadIdx.x;
+  if (ws_done(gap, b, skip)) return;
+  const int w = tid / M, c = tid % M;
+  const int* cb = cand + (long long)b * parts * 2 * hs;
+  const float* vb = candv + (long long)b * parts * 2 * hs;
+  const int* nb = cnt + (long long)b * parts * 2;
+  int row = -1;
+  float val = -INFINITY;
+  if (c < parts * hp) {
+    const int q = c / hp, s = c % hp;
+    if (s < nb[q * 2 + w]) {
+      row = cb[(q * 2 + w) * hs + s];
+      val = vb[(q * 2 + w) * hs + s];
+    }
+  }
+  const unsigned long long mk = row >= 0 ? ((unsigned long long)order_key(val) << 32) | (unsigned)(~row) : 0ull;
+  key[w][c] = mk;
+  if (tid < 2) {
+    int n = 0;
+    for (int q = 0; q < parts; ++q) n += nb[q * 2 + tid];
+    s_cnt[tid] = n < h ? n : h;
+    s_max[tid] = -INFINITY;
+  }
+  __syncthreads();
+  const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(&key[w][0]);
+  int rank = 0;
+#pragma unroll 8
+  for (int e = 0; e < M / 2; ++e) {
+    const ulonglong2 kk = kp[e];
+    rank += (kk.x > mk ? 1 : 0) + (kk.y > mk ? 1 : 0);
+  }
+  if (mk != 0ull && rank < h) {
+    sel[w][rank] = row;
+    if (rank == 0) s_max[w] = val;
+  }
+  __syncthreads();
+  const float gnew = s_max[0] + s_max[1];
+  if (tid < 2 * h) {
+    const int ww = tid / h, slot = tid % h, np = s_cnt[ww];
+    if (slot < np) {
+      const int n = sel[ww][slot];
+      int pos = 0;
+      for (int j = 0; j < np; ++j) pos += sel[ww][j] < n ? 1 : 0;
+      bool dup = false;
+      if (ww == 1)
+        for (int j = 0; j < s_cnt[0]; ++j) dup |= sel[0][j] == n;
+      s_ws[ww * h + pos] = n;
+      s_ok[ww * h + pos] = dup ? 0 : 1;
+    } else {
+      s_ws[ww * h + slot] = 0;
+      s_ok[ww * h + slot] = 0;
+    }
+  }
+  __syncthreads();
+  if (p == 0) {
+    for (int q = tid; q < 2 * h; q += NT) {
+      ws[(long long)b * 2 * h + q] = s_ws[q];
+      ok[(long long)b * 2 * h + q] = s_ok[q] != 0;
+    }
+    if (tid == 0) gap_next[b] = gnew;
+  }
+  if (!(gnew >= skip) || p >= 2 * h) return;  // converged at this step: the solve and update skip too
+  const long long rp = s_ok[p] ? s_ws[p] : 0;
+  for (int q = tid; q < 2 * h; q += NT) {
+    const long long cq = s_ok[q] ? s_ws[q] : 0;
+    Kws[((long long)b * Q + p) * Q + q] = K[b * kbs + rp * N + cq];
+  }
+}
+
 // G[n] += y[n] * sum_q dA[q] K[ws[q], n].  A workgroup owns 64 consecutive columns n; its 16 waves
 // split the non-zero (ws, dA) pairs (compacted in q order by wave 0) into sixteenths, each lane
 // streams its column of those <= 8 K rows (coalesced, all loads in flight at once), and the 16
@@ -1730,9 +1826,26 @@ int smo_ws_select_parts(int N) {
   return per ? (N + per * SEL_T - 1) / (per * SEL_T) : 1;
 }
 
+// The rank merge of a two-level selection, when the caller launches it itself (fused with the gather)
+struct MergePlan {
+  int parts = 0, hp = 0, hs = 0, nt = 0;
+  const float* candv = nullptr;
+};
+
+static void select_impl(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
+                        long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream,
+                        MergePlan* plan);
+
 // cand: [B][parts][2][h] rows followed by [B][parts][2][h] float violation values (candv)
 void smo_ws_select(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
                    long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream) {
+  select_impl(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, skip, stream, nullptr);
+}
+
+static void select_impl(const float* alpha, const float* G, const float* y, int B, int N, int ldag, float C, int h,
+                        long long* ws, bool* ok, float* gap, int* cand, int* cnt, float skip, hipStream_t stream,
+                        MergePlan* plan) {
+  if (plan) *plan = MergePlan{};
   if (B <= 0) return;
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
@@ -1782,6 +1895,10 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
 #undef AV_TKP
 #undef AV_TK
       AV_HIP_CHECK(hipGetLastError());
+      if (plan) {
+        *plan = MergePlan{tparts, hp, hp, tparts * hp <= 128 ? 256 : 512, candv};
+        return;
+      }
       if (tparts * hp <= 128)
         smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, hp, hp, tparts, cand, cnt, candv, ws, ok, gap, skip);
       else
@@ -1813,6 +1930,10 @@ void smo_ws_select(const float* alpha, const float* G, const float* y, int B, in
       return e && std::atoi(e) >= 512 ? 512 : 256;
     }();
     if (m <= rank_max && !env_off("AVMI_SMO_RANK_MERGE")) {
+      if (plan) {
+        *plan = MergePlan{parts, h, h, m <= 128 ? 256 : (m <= 256 ? 512 : 1024), candv};
+        return;
+      }
       if (m <= 128) smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, h, h, parts, cand, cnt, candv, ws, ok, gap, skip);
       else if (m <= 256) smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, h, h, parts, cand, cnt, candv, ws, ok, gap, skip);
       else smo_ws_merge_rank_kernel<1024><<<B, 1024, 0, stream>>>(h, h, h, parts, cand, cnt, candv, ws, ok, gap, skip);
@@ -1867,8 +1988,10 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, long long kbs, hipStream_t caller, const SvmKerX* kx) {
+                     float* host_gap, long long kbs, hipStream_t caller, const SvmKerX* kx, float* gap_next) {
   if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
+  // merge fused into the gather (explicit K, a rank-merge selection, gap_next scratch given)
+  const bool fuse = gap_next && !kx && Kws && !env_off("AVMI_SMO_FUSED_GATHER");
   const int Q = WS_Q, h = WS_Q / 2;
   check_every = check_every < 1 ? 1 : check_every;
   hipEvent_t ev[2];
@@ -1879,8 +2002,31 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
   AV_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   AV_HIP_CHECK(hipEventRecord(ev[1], caller));
   AV_HIP_CHECK(hipStreamWaitEvent(stream, ev[1], 0));
+  if (fuse) AV_HIP_CHECK(hipMemcpyAsync(gap_next, gap, sizeof(float) * B, hipMemcpyDeviceToDevice, stream));
   auto enqueue = [&](long long n) {
     for (long long s = 0; s < n; ++s) {
+      if (fuse) {
+        MergePlan plan;
+        select_impl(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream, &plan);
+        if (plan.nt) {
+          const dim3 gg(Q, B);
+#define AV_MG(NT) smo_ws_merge_gather_kernel<NT><<<gg, NT, 0, stream>>>(h, plan.hp, plan.hs, plan.parts, cand, cnt, \
+      plan.candv, ws, ok, gap, gap_next, eps, K, N, kbs, Kws)
+          if (plan.nt == 256) AV_MG(256);
+          else if (plan.nt == 512) AV_MG(512);
+          else AV_MG(1024);
+#undef AV_MG
+          AV_HIP_CHECK(hipGetLastError());
+          smo_ws_solve_kernel<<<B, WSS_T, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap_next, C, eps, rel_tol,
+                                                       inner_iter, dA, inner_total, gap);
+          AV_HIP_CHECK(hipGetLastError());
+        } else {  // a selection without a separate merge (single level): unfused gather + solve
+          smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws,
+                             rel_tol, kbs, stream);
+        }
+        smo_ws_update(K, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, kbs, stream);
+        continue;
+      }
       smo_ws_select(alpha, G, y, B, N, ldag, C, h, ws, ok, gap, cand, cnt, eps, stream);
       if (kx) {  // implicit kernel: K[ws, ws] and the gradient update from the rows of X
         smo_ws_gather_x(*kx, ws, ok, Kws, B, N, gap, eps, stream);
