@@ -219,6 +219,37 @@ __device__ __forceinline__ void wave_max2_u32(unsigned& u, unsigned& v) {
   v = max(max(rl(v, 0), rl(v, 16)), max(rl(v, 32), rl(v, 48)));
 }
 
+// The same maxima finished with the gfx950 row swaps (v_permlane16_swap / v_permlane32_swap)
+// instead of 4 v_readlane + SALU max + broadcast: the result lands in every lane, 2 swaps + 2 max.
+__device__ __forceinline__ unsigned wave_max_u32_v(unsigned v) {
+  v = dpp_max_step<0xB1>(v);
+  v = dpp_max_step<0x4E>(v);
+  v = dpp_max_step<0x124>(v);
+  v = dpp_max_step<0x128>(v);
+  const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = max((unsigned)p16[0], (unsigned)p16[1]);
+  const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return max((unsigned)p32[0], (unsigned)p32[1]);
+}
+__device__ __forceinline__ void wave_max2_u32_v(unsigned& u, unsigned& v) {
+  u = dpp_max_step<0xB1>(u);
+  v = dpp_max_step<0xB1>(v);
+  u = dpp_max_step<0x4E>(u);
+  v = dpp_max_step<0x4E>(v);
+  u = dpp_max_step<0x124>(u);
+  v = dpp_max_step<0x124>(v);
+  u = dpp_max_step<0x128>(u);
+  v = dpp_max_step<0x128>(v);
+  const auto pu = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const auto pv = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  u = max((unsigned)pu[0], (unsigned)pu[1]);
+  v = max((unsigned)pv[0], (unsigned)pv[1]);
+  const auto qu = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const auto qv = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  u = max((unsigned)qu[0], (unsigned)qu[1]);
+  v = max((unsigned)qv[0], (unsigned)qv[1]);
+}
+
 __device__ __forceinline__ float order_key_inv(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
@@ -256,7 +287,7 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       const unsigned kk = (order_key(-y[e] * g[e]) & ~0x7Fu) | (127u - (unsigned)(lane + 64 * e));
       ku = up ? max(ku, kk) : ku;
     }
-    ku = wave_max_u32(ku);
+    ku = (unsigned)__builtin_amdgcn_readfirstlane((int)wave_max_u32_v(ku));
     if (ku == 0u) break;
     const int i = 127 - (int)(ku & 0x7Fu);
     // i's state from its owner lane (the slot index is wave-uniform)
@@ -293,7 +324,8 @@ __device__ int ws_smo_loop(const float (&Ks)[WS_Q][WS_Q], float (&y)[E], float (
       kj = (low && bd > 0.f) ? max(kj, kg) : kj;
       km = low ? max(km, order_key(yg)) : km;
     }
-    wave_max2_u32(kj, km);
+    wave_max2_u32_v(kj, km);
+    kj = (unsigned)__builtin_amdgcn_readfirstlane((int)kj);
     const float gmax2 = km ? order_key_inv(km) : -INFINITY;
     if (gmax + gmax2 < epsl || kj == 0u) break;
     const int j = 127 - (int)(kj & 0x7Fu);
