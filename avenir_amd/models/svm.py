@@ -324,15 +324,12 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
     elif st.gpu and graph and mode != "eager":
         st.step()                                # eager warm-up: allocator pool, kernel caches
         outer = 1
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(check_every):
-                    st.step()
-                st.refresh_gap()
-        torch.cuda.current_stream().wait_stream(s)
+        from ..utils.hipgraph import capturing
+        g = torch.cuda.CUDAGraph()
+        with capturing(g):
+            for _ in range(check_every):
+                st.step()
+            st.refresh_gap()
         # capture records without executing: replay the block until converged (the captured block
         # ends with refresh_gap, so the gap read after a replay is current)
         st.refresh_gap()

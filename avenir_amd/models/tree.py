@@ -1410,6 +1410,7 @@ class GradientBoostedTrees:
         # the trees and the global loss sums), so a job resumes at any world size: each rank replays
         # the restored trees over its own rows to rebuild its raw scores (same gbt_assign launches
         # in the same order as the original rounds: bit-identical F).
+        from ..utils.hipgraph import capturing
         from ..utils.resilience import IterationLoop
         lp = IterationLoop("gbt", self.recovery, comm, device=dev)
         r0, ck, meta = lp.restore(dev)
@@ -1439,7 +1440,7 @@ class GradientBoostedTrees:
                     st["F"].copy_(Fsave)
                 torch.cuda.current_stream(dev).wait_stream(s_)
                 gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr):
+                with capturing(gr):                  # no allocator flush per fit (utils/hipgraph.py)
                     self._build_tree(st, k)
                 graphs[k] = gr
             graphs[k].replay()

@@ -203,8 +203,9 @@ class GraphedStep:
                 for _ in range(warmup):
                     self.fn(self.sx, self.sy)
             torch.cuda.current_stream().wait_stream(s)
+            from ..utils.hipgraph import capturing
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with capturing(self.graph):
                 self.sloss = self.fn(self.sx, self.sy)
             with torch.no_grad():
                 if snap is not None:
