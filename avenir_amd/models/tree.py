@@ -1446,7 +1446,39 @@ class GradientBoostedTrees:
             graphs[k].replay()
 
         seed_base = (p.seed * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
-        for rnd in range(r0, R):
+        # Without subsampling a round does not depend on its index on the host side (the gradient's
+        # subsample seed is unused), so the WHOLE round — gradients, every class's tree, the heap
+        # copies into round slot rnd_dev (a device counter) and the loss — is one graph replayed
+        # once per round: 1 host launch per round instead of ~5 (launch-bound at 64 k rows: the
+        # fit's time follows host scheduling noise otherwise).  The first round runs eagerly
+        # (warm-up), the capture records without executing.
+        round_graph = None
+        if use_graph and rate32 == 0xFFFFFFFF and R - r0 >= 3 and os.environ.get("AVMI_GBT_ROUND_GRAPH", "1") != "0":
+            rnd_dev = torch.full((1,), r0, dtype=torch.long, device=dev)
+            loss_slot = torch.zeros(1, dtype=torch.float64, device=dev)
+
+            def round_body():
+                loss_slot.zero_()
+                for k in range(K):
+                    T.gbt_grad(st["F"], k, y8, n, t.row_offset, seed_base, rate32, st["g"][k], st["h"][k],
+                               loss_slot if k == 0 else None)
+                for k in range(K):
+                    self._build_tree(st, k)
+                    feat_all[:, k].index_copy_(0, rnd_dev, st["feat"].view(1, Hn))
+                    thr_all[:, k].index_copy_(0, rnd_dev, st["thr"].view(1, Hn))
+                    val_all[:, k].index_copy_(0, rnd_dev, st["val"].view(1, Hn))
+                loss_all.index_copy_(0, rnd_dev, loss_slot)
+                rnd_dev.add_(1)
+
+            with lp.step(r0, nbytes=float(codes.numel()) * p.max_depth):
+                round_body()
+            round_graph = torch.cuda.CUDAGraph()
+            with capturing(round_graph):
+                round_body()
+            for rnd in range(r0 + 1, R):
+                with lp.step(rnd, nbytes=float(codes.numel()) * p.max_depth):
+                    round_graph.replay()
+        for rnd in range(r0, R if round_graph is None else r0):
             with lp.step(rnd, nbytes=float(codes.numel()) * p.max_depth):
                 rseed = (seed_base ^ (rnd * 0xD1B54A32D192ED03)) & 0x7FFFFFFFFFFFFFFF
                 for k in range(K):       # all gradients from the round's starting scores
@@ -1463,7 +1495,7 @@ class GradientBoostedTrees:
                     comm.all_reduce(gl)
                 lp.commit(rnd, {"feat": feat_all[:rnd + 1], "thr": thr_all[:rnd + 1], "val": val_all[:rnd + 1],
                                 "loss": gl}, {"rows": n_total})
-        self.graph_used = bool(graphs)
+        self.graph_used = bool(graphs) or round_graph is not None
         self.train_loss = self._losses(loss_all, R, st, y8, n, t, n_total, comm)
         self.stages = self._trees_from_heaps(feat_all.cpu(), thr_all.cpu(), val_all.cpu())
         self._flat = None
