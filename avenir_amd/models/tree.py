@@ -1344,6 +1344,8 @@ class GradientBoostedTrees:
         return stages
 
     def fit(self, t: Table) -> "GradientBoostedTrees":
+        import time as _time
+        marks = [("start", _time.perf_counter())]
         comm = self.comm or get_comm()
         p = self.p
         if p.max_depth < 1 or p.max_depth > 16:
@@ -1446,6 +1448,10 @@ class GradientBoostedTrees:
             graphs[k].replay()
 
         seed_base = (p.seed * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
+        timing = os.environ.get("AVMI_GBT_TIMING") == "1" and dev.type == "cuda"
+        if timing:
+            torch.cuda.synchronize(dev)
+            marks.append(("setup", _time.perf_counter()))
         # Without subsampling a round does not depend on its index on the host side (the gradient's
         # subsample seed is unused), so the WHOLE round — gradients, every class's tree, the heap
         # copies into round slot rnd_dev (a device counter) and the loss — is one graph replayed
@@ -1472,9 +1478,15 @@ class GradientBoostedTrees:
 
             with lp.step(r0, nbytes=float(codes.numel()) * p.max_depth):
                 round_body()
+            if timing:
+                torch.cuda.synchronize(dev)
+                marks.append(("round0", _time.perf_counter()))
             round_graph = torch.cuda.CUDAGraph()
             with capturing(round_graph):
                 round_body()
+            if timing:
+                torch.cuda.synchronize(dev)
+                marks.append(("capture", _time.perf_counter()))
             for rnd in range(r0 + 1, R):
                 with lp.step(rnd, nbytes=float(codes.numel()) * p.max_depth):
                     round_graph.replay()
@@ -1496,9 +1508,17 @@ class GradientBoostedTrees:
                 lp.commit(rnd, {"feat": feat_all[:rnd + 1], "thr": thr_all[:rnd + 1], "val": val_all[:rnd + 1],
                                 "loss": gl}, {"rows": n_total})
         self.graph_used = bool(graphs) or round_graph is not None
+        if timing:
+            torch.cuda.synchronize(dev)
+            marks.append(("rounds", _time.perf_counter()))
         self.train_loss = self._losses(loss_all, R, st, y8, n, t, n_total, comm)
         self.stages = self._trees_from_heaps(feat_all.cpu(), thr_all.cpu(), val_all.cpu())
         self._flat = None
+        if timing:
+            marks.append(("trees", _time.perf_counter()))
+            import sys as _sys
+            _sys.stderr.write("[gbt_timing] " + " ".join(f"{a}={b - marks[i][1]:.4f}" for i, (a, b) in
+                                                         enumerate(marks[1:])) + "\n")
         return self
 
     def _replay_scores(self, st: dict, feat_all, thr_all, val_all, rounds: int) -> None:
