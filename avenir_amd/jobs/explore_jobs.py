@@ -399,10 +399,19 @@ def _top_matches_native(ctx, rec, W, cls_ord, filt, inc_rec, topn, maxd, compact
     spos, trg, rr, sq = cols[:4]
     srec = torch.stack(cols[4:4 + Lr], 1) if Lr else None
     trec = torch.stack(cols[4 + Lr:], 1) if Lr else None
-    # (source, rank, input order) sort
-    o = torch.argsort(sq, stable=True)
-    o = o[torch.argsort(rr[o], stable=True)]
-    o = o[torch.argsort(spos[o], stable=True)]
+    # (source, rank, input order) sort: ONE argsort of a packed int64 key when the three ranges fit
+    # 62 bits (the usual case: ~20 + ~10 + ~25 bits), else three stable passes
+    o = None
+    if sq.numel():
+        r_lo, r_hi = int(rr.min()), int(rr.max())
+        q_hi = int(sq.max())
+        bq, br = max(1, q_hi.bit_length()), max(1, (r_hi - r_lo).bit_length())
+        if max(1, E.bit_length()) + br + bq <= 62 and r_lo >= -(1 << 61):
+            o = torch.argsort((spos << (br + bq)) | ((rr - r_lo) << bq) | sq)
+    if o is None:
+        o = torch.argsort(sq, stable=True)
+        o = o[torch.argsort(rr[o], stable=True)]
+        o = o[torch.argsort(spos[o], stable=True)]
     spos, trg, rr = spos[o], trg[o], rr[o]
     srec, trec = srec[o], trec[o]
     n = spos.numel()
