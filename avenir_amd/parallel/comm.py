@@ -44,6 +44,7 @@ from ..utils.tracing import traced
 
 _COMM: "Comm | None" = None
 _ONESHOT_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "") == "oneshot"
+_P2P_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "") == "p2p"
 _ONESHOT_MAX_BYTES = int(os.environ.get("AVMI_ONESHOT_MAX_BYTES", str(64 << 10)))
 
 
@@ -87,6 +88,7 @@ class Comm:
             self.rank = dist.get_rank()
             self.pg_backend = dist.get_backend()
         self.stats = {"calls": 0, "bytes": 0, "seconds": 0.0}
+        self._symm: dict = {}   # (dtype, numel) -> symmetric-memory buffer of the p2p all-reduce
 
     @classmethod
     def emulated_rccl(cls, device: str | None = None, **kw) -> "Comm":
@@ -126,8 +128,13 @@ class Comm:
         (all-gather + rank-ordered local reduction)."""
         if not self.is_distributed:
             return t
-        if algo is None and op == "sum" and _ONESHOT_ENV and t.numel() * t.element_size() <= _ONESHOT_MAX_BYTES:
-            algo = "oneshot"
+        small = t.numel() * t.element_size() <= _ONESHOT_MAX_BYTES
+        if algo is None and op == "sum" and small and (_ONESHOT_ENV or _P2P_ENV):
+            algo = "p2p" if _P2P_ENV else "oneshot"
+        if algo == "p2p":
+            if op == "sum" and t.is_cuda and self.pg_backend == "nccl":
+                return self._all_reduce_p2p(t)
+            algo = None                       # not on RCCL / not a device sum: the library collective
         if algo == "oneshot":
             return self._all_reduce_oneshot(t, op)
         t0 = time.perf_counter()
@@ -137,6 +144,30 @@ class Comm:
         dist.all_reduce(x, op=rop)
         if moved:
             t.copy_(x)
+        self._account(t, t0)
+        return t
+
+    def _all_reduce_p2p(self, t: torch.Tensor) -> torch.Tensor:
+        """SURVEY §5.8's one-shot all-reduce over xGMI peer reads: the operand is staged in a
+        symmetric-memory buffer (allocated once per (dtype, size) and rendezvoused by all ranks —
+        every peer maps every other peer's buffer), then ONE kernel per rank reads all peers'
+        buffers directly and sums them (``torch.ops.symm_mem.one_shot_all_reduce``, PyTorch's
+        P2P kernel; no ring steps, no RCCL proxy).  Opt-in (``algo="p2p"`` or
+        ``AVMI_SMALL_ALLREDUCE=p2p``); verified in this build at world 1 only
+        (tests/test_comm.py::test_p2p_all_reduce_world1_gpu) — the single-GPU boxes cannot run the
+        multi-peer case."""
+        import torch.distributed._symmetric_memory as symm
+        t0 = time.perf_counter()
+        group = dist.group.WORLD.group_name
+        key = (t.dtype, t.numel(), t.device.index)
+        buf = self._symm.get(key)
+        if buf is None:                        # collective: every rank reaches this call together
+            buf = symm.empty(t.numel(), dtype=t.dtype, device=t.device)
+            symm.rendezvous(buf, group)
+            self._symm[key] = buf
+        buf.copy_(t.reshape(-1))
+        out = torch.ops.symm_mem.one_shot_all_reduce(buf, "sum", group)
+        t.copy_(out.view_as(t))
         self._account(t, t0)
         return t
 
