@@ -1882,13 +1882,14 @@ static void select_impl(const float* alpha, const float* G, const float* y, int 
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
-  // register top-k parts + rank merge for N > 16384 (below that the exact radix parts are as fast:
-  // N = 8192 20.0 vs 20.5 ms, while N = 32768 goes from 76 to 61 ms, profiles/r4_svm_topk_ab.log):
-  // 2 / 4 blocks of 64 rows per wave, HP = the power of two <= target / parts (target 128
-  // candidates per side: the 256-thread merge)
+  // register top-k parts + rank merge above 8192 rows, where the exact radix parts hand over more
+  // than the 256 candidates per side of the rank merge (the radix merge then costs ~12 us a step):
+  // N = 12000 28.5-29.1 -> 25.8-26.3 ms, 16384 37.0 -> 31.9 ms, 32768 76 -> 55 ms; at 8192 the
+  // exact radix parts are as fast (profiles/r4_svm_topk_ab.log, profiles/r4_svm_mid_ab.log).
+  // HP = the power of two <= target / parts (target 128 candidates per side: the 256-thread merge)
   static const int topk_min_n = [] {
     const char* e = std::getenv("AVMI_SMO_TOPK_MIN_N");
-    return e && *e ? std::atoi(e) : 16 * 1024 + 1;
+    return e && *e ? std::atoi(e) : 8 * 1024 + 1;
   }();
   if (N > 4 * SEL_T && N >= topk_min_n && cand && per && !env_off("AVMI_SMO_TOPK") && h == 64) {
     static const int target = [] {
