@@ -1157,22 +1157,25 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 // sit together in the input are spread over the parts), PER blocks per wave.  Every candidate is
 // one exact 64-bit key (order_key(violation) << 32 | ~row: larger = more violating, ties to the
 // lower row — the order of the radix selection and of the rank merge), so the selection is exact
-// and deterministic.  Each wave keeps its HP largest keys per side by HP wave-max steps (the owner
-// lane clears the winner), then waves 0 and 1 take the HP largest of the 16 waves' candidates of
-// side 0 / 1.  No radix passes and 2 barriers, against 12 for ws_select2_body.  The part's HP
+// and deterministic.  Each wave keeps its HW (<= 4) largest keys per side by HW wave-max steps (the
+// owner lane clears the winner), then waves 0 and 1 take the HP largest of the 16 waves' candidates
+// of side 0 / 1.  No radix passes and 2 barriers, against 12 for ws_select2_body.  The part's HP
 // candidates per side go to the rank merge; the global top h is exact whenever no part holds more
-// than HP of them (the host sizes HP to 2-4x a part's expected share of h; beyond that the working
-// set is a slightly different set of strong violators — any violating set keeps SMO convergent).
-template <int PER, int HP>
+// than HP of them and no 64-row block more than HW (the host sizes HP to 2-4x a part's expected
+// share of h; a block's expected share is 64 h / N < 1 here; beyond that the working set is a
+// slightly different set of strong violators — any violating set keeps SMO convergent).
+template <int PER, int HP, int HW = (HP < 4 ? HP : 4)>
 __global__ __launch_bounds__(SEL_T) void smo_ws_topk_part_kernel(const float* __restrict__ alpha,
                                                                  const float* __restrict__ G,
                                                                  const float* __restrict__ y, int N, int ldag, float C,
                                                                  int parts, int* __restrict__ cand,
                                                                  int* __restrict__ cnt, float* __restrict__ candv,
                                                                  const float* __restrict__ gap, float skip) {
-  static_assert(HP >= 4 && HP <= 64 && (16 * HP) % 64 == 0, "HP");
-  constexpr int NW = SEL_T / 64, R = NW * HP / 64;
-  __shared__ unsigned long long s_k[2][NW * HP];
+  // each wave keeps its HW largest keys per side (a 64-row block holds ~64 h / N of the global
+  // top h: far below HW = 4 at N > 4096), the workgroup the HP largest of those 16 x HW
+  static_assert(HP >= 4 && HP <= 64 && HW >= 1 && HW <= HP && (16 * HW) % 64 == 0, "HP / HW");
+  constexpr int NW = SEL_T / 64, R = NW * HW / 64;
+  __shared__ unsigned long long s_k[2][NW * HW];
   const int b = blockIdx.y, p = blockIdx.x;
   if (ws_done(gap, b, skip)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1194,7 +1197,7 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_topk_part_kernel(const float* __
       }
     }
   }
-  for (int it = 0; it < HP; ++it) {  // the wave's HP largest per side
+  for (int it = 0; it < HW; ++it) {  // the wave's HW largest per side
     unsigned long long m0 = key[0][0], m1 = key[1][0];
 #pragma unroll
     for (int j = 1; j < PER; ++j) {
@@ -1208,8 +1211,8 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_topk_part_kernel(const float* __
       if (key[1][j] == m1) key[1][j] = 0ull;
     }
     if (lane == 0) {
-      s_k[0][wv * HP + it] = m0;
-      s_k[1][wv * HP + it] = m1;
+      s_k[0][wv * HW + it] = m0;
+      s_k[1][wv * HW + it] = m1;
     }
   }
   __syncthreads();
@@ -1882,14 +1885,14 @@ static void select_impl(const float* alpha, const float* G, const float* y, int 
   const size_t lds = (size_t)((N + 31) / 32) * sizeof(unsigned);
   if (h > 64) throw std::runtime_error("smo_ws_select: h <= 64");
   const int per = select_part_per(N, 64);
-  // register top-k parts + rank merge above 8192 rows, where the exact radix parts hand over more
-  // than the 256 candidates per side of the rank merge (the radix merge then costs ~12 us a step):
-  // N = 12000 28.5-29.1 -> 25.8-26.3 ms, 16384 37.0 -> 31.9 ms, 32768 76 -> 55 ms; at 8192 the
-  // exact radix parts are as fast (profiles/r4_svm_topk_ab.log, profiles/r4_svm_mid_ab.log).
-  // HP = the power of two <= target / parts (target 128 candidates per side: the 256-thread merge)
+  // register top-k parts + rank merge for every two-level size (N > 4096), HW = 4 keys per wave and
+  // HP = the power of two <= target / parts per part (target 128 candidates per side: the
+  // 256-thread merge).  Against the exact radix parts: N = 8192 18.3-19.3 -> 17.2-18.4 ms, 12000
+  // 28.5-29.1 -> 23.4 ms, 16384 37.0 -> 31.2 ms, 32768 76 -> 54 ms (profiles/r4_svm_topk_ab.log,
+  // profiles/r4_svm_mid_ab.log, profiles/r4_svm_hw_ab.log).  AVMI_SMO_TOPK=0: the exact radix parts.
   static const int topk_min_n = [] {
     const char* e = std::getenv("AVMI_SMO_TOPK_MIN_N");
-    return e && *e ? std::atoi(e) : 8 * 1024 + 1;
+    return e && *e ? std::atoi(e) : 4 * 1024 + 1;
   }();
   if (N > 4 * SEL_T && N >= topk_min_n && cand && per && !env_off("AVMI_SMO_TOPK") && h == 64) {
     static const int target = [] {

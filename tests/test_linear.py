@@ -290,7 +290,7 @@ def test_smo_working_set_gpu_matches_full(cuda, N):
 @pytest.mark.parametrize("N", [40, 1000, 5000, 12000, 40000, 70000])
 def test_smo_ws_select_matches_topk(cuda, N, monkeypatch):
     """Fused working-set selection == gap + top-h up / low violator sets of the torch path (the
-    exact radix selection: the register top-k parts, default above 8192 rows, are switched off
+    exact radix selection: the register top-k parts, the default above 4096 rows, are switched off
     here and checked by test_smo_ws_select_topk_parts)."""
     from avenir_amd import _native
     monkeypatch.setenv("AVMI_SMO_TOPK", "0")
@@ -326,9 +326,9 @@ def test_smo_ws_select_matches_topk(cuda, N, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [12000, 20000, 32768, 65536])
+@pytest.mark.parametrize("N", [8192, 12000, 20000, 32768, 65536])
 def test_smo_ws_select_topk_parts(cuda, N):
-    """Register top-k part selection (N > 8192): the gap is exact; every pick is a valid member
+    """Register top-k part selection (N > 4096): the gap is exact; every pick is a valid member
     of its side, picks are in ascending row order, the strongest violator of each side is picked,
     low-side picks already on the up side are masked, and the picks are the exact top h except
     where one part held more than its HP slots of them (a few of 64 on random data; >= 75 % here)."""
