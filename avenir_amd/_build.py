@@ -6,7 +6,7 @@ Everything is compiled IN-TREE into ``avenir_amd/_C.so`` (one Python extension m
   include no torch headers, so they compile in seconds.
 * ``csrc/host/*.cpp``     -> host-only C++ runtime (CSV->columnar parser, config, ring buffer,
   checkpoint container).  Compiled with the same clang driver, no offload.
-* ``csrc/bindings.cpp``   -> the only TU that includes torch / pybind11.
+* ``csrc/bindings.cpp`` + ``csrc/bind_*.cpp`` -> the only TUs that include torch / pybind11.
 
 A ``build.ninja`` file is generated so rebuilds are incremental and parallel.  Run
 ``python -m avenir_amd._build`` (or ``__graft_entry__.build()``).
@@ -44,7 +44,7 @@ def _hipcc() -> str:
 def sources():
     kern = sorted((CSRC / "kernels").glob("*.hip"))
     host = sorted((CSRC / "host").glob("*.cpp"))
-    return kern, host, CSRC / "bindings.cpp"
+    return kern, host, [CSRC / "bindings.cpp"] + sorted(CSRC.glob("bind_*.cpp"))
 
 
 def write_ninja(debug: bool = False) -> Path:
@@ -99,9 +99,10 @@ def write_ninja(debug: bool = False) -> Path:
         o = BUILD / (s.stem + ".host.o")
         lines.append(f"build {o}: hcc {s}")
         objs.append(o)
-    ob = BUILD / "bindings.o"
-    lines.append(f"build {ob}: bcc {bind}")
-    objs.append(ob)
+    for s in bind:
+        ob = BUILD / (s.stem + ".o")
+        lines.append(f"build {ob}: bcc {s}")
+        objs.append(ob)
     lines.append(f"build {OUT}: link " + " ".join(str(o) for o in objs))
     lines.append(f"default {OUT}")
     nf = BUILD / "build.ninja"

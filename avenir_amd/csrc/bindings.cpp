@@ -3694,7 +3694,10 @@ std::vector<at::Tensor> lstm_backward(const at::Tensor& dhseq, const at::Tensor&
 
 }  // namespace
 
+void register_comm(py::module_& m);  // bind_comm.cpp
+
 PYBIND11_MODULE(_C, m) {
+  register_comm(m);
   m.doc() = "avenir_amd native kernels (HIP/CDNA4 gfx950) and host runtime";
   m.def("class_histogram", &class_histogram);
   m.def("pair_histogram", &pair_histogram);

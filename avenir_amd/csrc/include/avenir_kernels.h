@@ -385,4 +385,18 @@ void format_rows_len(const DevFmtCol* cols, int ncols, int64_t n, const uint8_t*
 void format_rows_write(const DevFmtCol* cols, int ncols, int64_t n, const uint8_t* delim, int dl, const int64_t* start,
                        char* out, hipStream_t stream);
 
+// ---- comm.hip: peer-mapped small-message all-reduce (one-shot / two-shot) --------------------
+constexpr int P2P_MAX_RANKS = 16;
+constexpr int P2P_MAX_BLOCKS = 64;
+enum P2PDtype { P2P_F32 = 0, P2P_F64 = 1, P2P_I32 = 2, P2P_I64 = 3 };
+struct P2PView {
+  void* data[P2P_MAX_RANKS];       // every rank's data region as mapped in this process
+  unsigned* flags[P2P_MAX_RANKS];  // every rank's flag array as mapped in this process
+  int* status;                     // this rank's status word
+  long long cap_bytes;             // bytes of ONE staging buffer (4 per data region)
+  int rank, world;
+};
+void p2p_all_reduce(void* x, long long n, int dtype, const P2PView& v, unsigned epoch, int two_shot,
+                    long long timeout_ticks, hipStream_t st);
+
 }  // namespace avk

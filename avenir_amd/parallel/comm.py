@@ -17,16 +17,23 @@ tensors (KB..tens of MB), so ops are issued ONCE per model/iteration on coalesce
 (``all_reduce_coalesced``) rather than per key; RCCL picks its one-shot/tree algorithms for small
 messages and multi-ring for large ones.
 
-Deterministic small-message all-reduce (``algo="oneshot"``; SURVEY §5.8 asks for a one-shot
-kernel, which this is NOT): the reduction is an all-gather of every rank's buffer followed by a
-local sum over ranks in rank order.  The all-gather is RCCL's own collective (its ring or direct
-algorithm, chosen by RCCL), so this path saves no communication steps over a library all-reduce;
-what it buys is a result that is bit-identical on every rank and every run (fp32 / fp64 sums
-included), at the price of ``world`` times the receive bytes.  ``all_reduce(..., algo="oneshot")``
-(or ``AVMI_SMALL_ALLREDUCE=oneshot`` for sum reductions up to ``AVMI_ONESHOT_MAX_BYTES``, default
-64 KiB) takes it; ``bench.py`` reports both latencies on multi-GPU runs.  A true one-shot P2P kernel
-(each GPU reading its peers' buffers over xGMI with device-side cross-process flags) is not
-provided: it cannot be validated on the single-GPU boxes available to this build.
+Deterministic small-message all-reduce, two variants, both bit-identical on every rank and run:
+
+* ``algo="p2p"``: the hand-written peer-mapped kernels of ``csrc/kernels/comm.hip``
+  (``parallel/p2p.py``).  Each rank stages its operand in an IPC-exported buffer; ONE kernel per
+  rank waits on per-block epoch flags raised by its peers and sums every peer's staging in rank
+  order (one-shot up to 256 KiB, reduce-scatter + all-gather through result stagings above, up to
+  the 8 MiB staging capacity; larger messages take the library collective).  No ring steps, no
+  proxy thread.  Device sums of float32 / float64 / int32 / int64 only; other cases fall back to
+  the library collective.  Tested with 2 and 4 processes sharing one GPU
+  (tests/test_p2p_allreduce.py) — the multi-process path through the same code a multi-GPU node
+  takes over xGMI.
+* ``algo="oneshot"``: an all-gather of every rank's buffer (RCCL's collective) followed by a local
+  sum in rank order; any reduction op, any device.
+
+``AVMI_SMALL_ALLREDUCE=p2p|oneshot`` routes sum reductions up to ``AVMI_ONESHOT_MAX_BYTES``
+(default 64 KiB) to one of them; ``bench.py`` reports both latencies next to RCCL's on multi-GPU
+runs.
 """
 from __future__ import annotations
 
@@ -88,7 +95,11 @@ class Comm:
             self.rank = dist.get_rank()
             self.pg_backend = dist.get_backend()
         self.stats = {"calls": 0, "bytes": 0, "seconds": 0.0}
-        self._symm: dict = {}   # (dtype, numel) -> symmetric-memory buffer of the p2p all-reduce
+        self._p2p = None        # parallel/p2p.P2PAllReduce, created by the first p2p all-reduce
+        # algorithm of sum all-reduces up to _ONESHOT_MAX_BYTES when the caller names none:
+        # None (library collective), "oneshot" or "p2p" (env AVMI_SMALL_ALLREDUCE, or set by a tuner
+        # such as bench.py's, which times the candidates on the job's own GPUs)
+        self.small_allreduce = "p2p" if _P2P_ENV else ("oneshot" if _ONESHOT_ENV else None)
 
     @classmethod
     def emulated_rccl(cls, device: str | None = None, **kw) -> "Comm":
@@ -125,16 +136,17 @@ class Comm:
     def all_reduce(self, t: torch.Tensor, op: str = "sum", algo: str | None = None) -> torch.Tensor:
         """In-place all-reduce (sum|max|min|prod); returns ``t``.  ``algo``: None (library
         collective, or the env-selected small-message path), "ring" (library), "oneshot"
-        (all-gather + rank-ordered local reduction)."""
+        (all-gather + rank-ordered local reduction), "p2p" (hand-written peer-mapped kernel, sums of
+        device tensors; anything else falls back to the library collective)."""
         if not self.is_distributed:
             return t
         small = t.numel() * t.element_size() <= _ONESHOT_MAX_BYTES
-        if algo is None and op == "sum" and small and (_ONESHOT_ENV or _P2P_ENV):
-            algo = "p2p" if _P2P_ENV else "oneshot"
+        if algo is None and op == "sum" and small and self.small_allreduce:
+            algo = self.small_allreduce
         if algo == "p2p":
-            if op == "sum" and t.is_cuda and self.pg_backend == "nccl":
-                return self._all_reduce_p2p(t)
-            algo = None                       # not on RCCL / not a device sum: the library collective
+            if op == "sum" and self._all_reduce_p2p(t) is not None:
+                return t
+            algo = None                       # not a device sum the kernel takes: the library collective
         if algo == "oneshot":
             return self._all_reduce_oneshot(t, op)
         t0 = time.perf_counter()
@@ -147,27 +159,27 @@ class Comm:
         self._account(t, t0)
         return t
 
-    def _all_reduce_p2p(self, t: torch.Tensor) -> torch.Tensor:
-        """SURVEY §5.8's one-shot all-reduce over xGMI peer reads: the operand is staged in a
-        symmetric-memory buffer (allocated once per (dtype, size) and rendezvoused by all ranks —
-        every peer maps every other peer's buffer), then ONE kernel per rank reads all peers'
-        buffers directly and sums them (``torch.ops.symm_mem.one_shot_all_reduce``, PyTorch's
-        P2P kernel; no ring steps, no RCCL proxy).  Opt-in (``algo="p2p"`` or
-        ``AVMI_SMALL_ALLREDUCE=p2p``); verified in this build at world 1 only
-        (tests/test_comm.py::test_p2p_all_reduce_world1_gpu) — the single-GPU boxes cannot run the
-        multi-peer case."""
-        import torch.distributed._symmetric_memory as symm
+    def p2p(self):
+        """The peer-mapped all-reduce state (``parallel/p2p.py``), created on first use — a
+        collective: every rank reaches its first p2p all-reduce together."""
+        if self._p2p is None:
+            from .p2p import P2PAllReduce
+            self._p2p = P2PAllReduce(self, self.device)
+        return self._p2p
+
+    def _all_reduce_p2p(self, t: torch.Tensor) -> torch.Tensor | None:
+        """The hand-written peer-mapped sum (comm.hip); None when ``t`` does not qualify (host
+        tensor, unsupported dtype, larger than the staging capacity) — the caller then takes the
+        library collective.  The decision depends only on shape / dtype / device type, which every
+        rank shares, so all ranks take the same path."""
+        from .p2p import P2PAllReduce
+        if not P2PAllReduce.supports(t) or self.device.type != "cuda":
+            return None
+        p = self.p2p()
+        if t.numel() * t.element_size() > p.cap_bytes:
+            return None
         t0 = time.perf_counter()
-        group = dist.group.WORLD.group_name
-        key = (t.dtype, t.numel(), t.device.index)
-        buf = self._symm.get(key)
-        if buf is None:                        # collective: every rank reaches this call together
-            buf = symm.empty(t.numel(), dtype=t.dtype, device=t.device)
-            symm.rendezvous(buf, group)
-            self._symm[key] = buf
-        buf.copy_(t.reshape(-1))
-        out = torch.ops.symm_mem.one_shot_all_reduce(buf, "sum", group)
-        t.copy_(out.view_as(t))
+        p.all_reduce(t)
         self._account(t, t0)
         return t
 
@@ -387,6 +399,9 @@ class Comm:
         return float(t.item())
 
     def shutdown(self) -> None:
+        if self._p2p is not None:
+            self._p2p.close()
+            self._p2p = None
         if self._owns_pg and dist.is_initialized():
             dist.destroy_process_group()
             self._owns_pg = False

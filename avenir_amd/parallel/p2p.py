@@ -1,0 +1,98 @@
+"""Peer-mapped small-message all-reduce: the Python side of ``csrc/kernels/comm.hip``.
+
+Every counting model of the reference ends a pass with a combiner + reducer shuffle of a KB-scale
+count table (e.g. ``src/main/java/org/avenir/bayesian/BayesianDistribution.java:72-79``).  Here the
+table is summed by ONE hand-written kernel per rank that reads the peers' staged copies directly:
+
+* at construction every rank allocates its staging region (4 x ``cap_bytes``) and an uncached
+  flag array, exports both with ``hipIpcGetMemHandle``, exchanges the handles ONCE through the
+  process group (``all_gather_object``: gloo or RCCL) and maps every peer's regions with
+  ``hipIpcOpenMemHandle`` — over xGMI between GPUs of one node, or through the same HBM when several
+  ranks share one device (the multi-process rehearsal available on single-GPU boxes);
+* each call bumps an epoch that every rank counts identically (collectives are called in the same
+  order everywhere) and launches the one-shot kernel (messages up to ``oneshot_max`` bytes: every
+  rank reads all W stagings) or the two-shot kernel (reduce-scatter + all-gather through the
+  result stagings: 2 (W-1)/W of the message read per rank);
+* the sum is taken in rank order, so the result is bit-identical on every rank and every run —
+  the same contract as ``Comm._all_reduce_oneshot`` but without the all-gather round;
+* waits are bounded in the kernel (``timeout_s``); a timed-out wait sets a status word that
+  :meth:`check` turns into an exception instead of a hang.
+
+Teardown is collective too: :meth:`close` unmaps the peers' regions, barriers, then frees the
+rank's own region (a peer must never read freed memory).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _native
+
+_DTYPES = (torch.float32, torch.float64, torch.int32, torch.int64)
+
+
+class P2PError(RuntimeError):
+    pass
+
+
+class P2PAllReduce:
+    """One communicator's peer-mapped all-reduce state.  Construct on every rank together."""
+
+    def __init__(self, comm, device: torch.device, cap_bytes: int | None = None,
+                 oneshot_max: int | None = None, timeout_s: float | None = None):
+        if device.type != "cuda":
+            raise ValueError("the peer-mapped all-reduce needs device tensors")
+        cap = int(cap_bytes or os.environ.get("AVMI_P2P_CAP", str(8 << 20)))
+        self.oneshot_max = int(oneshot_max or os.environ.get("AVMI_P2P_ONESHOT_MAX", str(256 << 10)))
+        self.comm = comm
+        self.device = device
+        self.world, self.rank = comm.world, comm.rank
+        uncached = os.environ.get("AVMI_P2P_UNCACHED", "0") == "1"
+        self._h = _native.C().P2PComm(device.index, cap, uncached)
+        self.cap_bytes = int(self._h.cap_bytes)
+        self._h.set_timeout(float(timeout_s or os.environ.get("AVMI_P2P_TIMEOUT_S", "10")))
+        handles = comm.all_gather_object(bytes(self._h.handles()))
+        self._h.open(list(handles), self.rank, self.world)
+        comm.barrier()
+        self.epoch = 0
+        self.calls = {"oneshot": 0, "twoshot": 0}
+
+    @staticmethod
+    def supports(t: torch.Tensor) -> bool:
+        return t.is_cuda and t.dtype in _DTYPES
+
+    def all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
+        """In-place sum of ``t`` over all ranks (stream-ordered on the current stream); returns ``t``.
+        ``algo``: None (by size), "oneshot" or "twoshot"."""
+        if t.numel() == 0:
+            return t
+        nbytes = t.numel() * t.element_size()
+        if nbytes > self.cap_bytes:
+            raise ValueError(f"p2p all-reduce: {nbytes} bytes exceed the staging capacity {self.cap_bytes}")
+        two = (algo == "twoshot") if algo is not None else nbytes > self.oneshot_max
+        x = t
+        if not t.is_contiguous() or t.data_ptr() % 16 != 0:
+            x = t.contiguous().clone()
+        self.epoch += 1
+        self._h.all_reduce(x, self.epoch, two)
+        self.calls["twoshot" if two else "oneshot"] += 1
+        if x is not t:
+            t.copy_(x)
+        return t
+
+    def check(self) -> None:
+        """Raise if any wait of this rank's kernels timed out (synchronises the device)."""
+        if int(self._h.status()) != 0:
+            raise P2PError(f"rank {self.rank}: a peer-mapped all-reduce wait timed out "
+                           f"(epoch <= {self.epoch}); the peers are out of step or gone")
+
+    def close(self) -> None:
+        """Collective: unmap peers, barrier, free this rank's region."""
+        if self._h is None:
+            return
+        torch.cuda.synchronize(self.device)
+        self._h.close_peers()
+        self.comm.barrier()
+        self._h.release()
+        self._h = None

@@ -23,7 +23,8 @@ CSV parsing and packing are NOT in the timed steps (the headline is the on-devic
 * ``ingest`` (1 GPU by default, ``--ingest-rows``) — the end-to-end job time for a CSV file of
   ``2^26`` records written beforehand: native K1 parse -> device -> fit -> model text lines.
 * ``rccl_all_reduce`` (more than one GPU) — all-reduce latency at 8 KB and bus bandwidth at
-  1 MB / 64 MB over the job's GPUs.
+  1 MB / 64 MB over the job's GPUs, next to the deterministic all-gather path and the hand-written
+  peer-mapped one-shot / two-shot kernels (``algo="p2p"``, csrc/kernels/comm.hip).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows-per-gpu R] [--layout L]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -75,7 +76,65 @@ def _allreduce_probe(comm, dev) -> list:
         t = _timed(lambda: [comm.all_reduce(x, algo="oneshot") for _ in range(iters)], dev) / iters
         t = comm.reduce_max_scalar(t)
         out.append({"bytes": nbytes, "algo": "allgather_ordered_sum", "us": t * 1e6})
+    # hand-written peer-mapped kernels (csrc/kernels/comm.hip): one-shot / two-shot over xGMI
+    try:
+        for nbytes, iters in ((8 << 10, 100), (64 << 10, 100), (1 << 20, 50)):
+            x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+            for _ in range(5):
+                comm.all_reduce(x, algo="p2p")
+            comm.barrier()
+            t = _timed(lambda: [comm.all_reduce(x, algo="p2p") for _ in range(iters)], dev) / iters
+            x.fill_(float(comm.rank + 1))
+            comm.all_reduce(x, algo="p2p")
+            comm.p2p().check()
+            exact = bool((x == float(W * (W + 1) // 2)).all().item())
+            t = comm.reduce_max_scalar(t)
+            out.append({"bytes": nbytes, "algo": "p2p_" + ("oneshot" if nbytes <= comm.p2p().oneshot_max else "twoshot"),
+                        "us": t * 1e6, "exact": exact})
+    except Exception as e:          # the probe must never cost the measured headline
+        out.append({"algo": "p2p", "error": repr(e)})
     return out
+
+
+def _pick_small_allreduce(comm, like: torch.Tensor, mode: str) -> dict:
+    """Choose the algorithm of the model's count-table all-reduce on this job's GPUs, before the
+    timed steps: the hand-written peer-mapped kernel (``p2p``) is taken only if it is exact on an
+    integer probe, its status is clean on every rank, and it is faster than RCCL at the table's
+    size (max over ranks).  ``mode``: auto | rccl | p2p."""
+    info = {"mode": mode, "bytes": like.numel() * like.element_size()}
+    if mode == "rccl" or comm.world == 1 or like.device.type != "cuda":
+        info["chosen"] = "rccl"
+        return info
+    W = comm.world
+    x = torch.empty_like(like)
+    try:
+        ok = True
+        for i in range(20):
+            x.fill_(comm.rank + 1 + i)
+            comm.all_reduce(x, algo="p2p")
+            ok &= bool((x == W * (W + 1) // 2 + W * i).all().item())
+        comm.p2p().check()
+        okt = torch.tensor([1 if ok else 0], device=like.device)
+        comm.all_reduce(okt, "min")
+        info["p2p_exact"] = bool(okt.item())
+        times = {}
+        for name, fn in (("rccl", lambda: comm.all_reduce(x, algo="ring")),
+                         ("p2p", lambda: comm.all_reduce(x, algo="p2p"))):
+            for _ in range(5):
+                fn()
+            comm.barrier()
+            times[name] = comm.reduce_max_scalar(_timed(lambda: [fn() for _ in range(50)], like.device) / 50)
+        comm.p2p().check()
+        info.update({f"{k}_us": v * 1e6 for k, v in times.items()})
+        use = info["p2p_exact"] and (mode == "p2p" or times["p2p"] < times["rccl"])
+    except Exception as e:      # no peer mapping on this node: the library collective
+        info["p2p_error"] = repr(e)
+        use = False
+    flag = torch.tensor([1 if use else 0], device=like.device)
+    comm.all_reduce(flag, "min")                      # every rank takes the same path
+    info["chosen"] = "p2p" if int(flag.item()) else "rccl"
+    comm.small_allreduce = "p2p" if info["chosen"] == "p2p" else None
+    return info
 
 
 def _ingest(rows: int, schema, dev, comm) -> dict:
@@ -133,6 +192,9 @@ def main() -> int:
     ap.add_argument("--layout", choices=["rowpacked", "columns"], default="rowpacked",
                     help="device layout of the encoded records: one 16-bit word per record "
                          "(2 B/record) or one uint8 column per feature + label (6 B/record)")
+    ap.add_argument("--small-allreduce", choices=["auto", "rccl", "p2p"], default="auto",
+                    help="algorithm of the count-table all-reduce on >1 GPU: auto = the faster of RCCL "
+                         "and the hand-written peer-mapped kernel, timed on the job's GPUs before the steps")
     ap.add_argument("--probe-allreduce", action="store_true",
                     help="run the all-reduce probe on any device (it runs by default on >1 GPU)")
     ap.add_argument("--ingest-rows", type=int, default=-1,
@@ -182,6 +244,10 @@ def main() -> int:
         # run on a side stream that overlaps the next step's histogram (models/bayes.py)
         nb.fit(table)
 
+    allreduce_choice = None
+    if comm.world > 1:
+        nb.fit(table)                     # sizes the count table
+        allreduce_choice = _pick_small_allreduce(comm, nb._both, args.small_allreduce)
     for _ in range(args.warmup):
         step()
     if dev.type == "cuda":
@@ -206,7 +272,7 @@ def main() -> int:
 
     ms = dt * 1000.0 / args.steps
     rows_per_s = n * comm.world * args.steps / dt
-    extra = {"layout": args.layout, "ms_per_step": ms, "hbm_gbps_per_gpu": n * bytes_per_row / (ms / 1000.0) / 1e9}
+    extra = {"layout": args.layout, "ms_per_step": ms, "count_allreduce": allreduce_choice, "hbm_gbps_per_gpu": n * bytes_per_row / (ms / 1000.0) / 1e9}
     if args.layout == "rowpacked" and table.rowpack is not None:
         rp, table.rowpack = table.rowpack, None
         k = max(1, min(args.steps, 5))

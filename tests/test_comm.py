@@ -48,28 +48,3 @@ def _p2p_fallback(rank, world):
 
 def test_p2p_all_reduce_falls_back_off_rccl():
     assert all(run_world(_p2p_fallback, 2, timeout=300))
-
-
-@pytest.mark.gpu
-def test_p2p_all_reduce_world1_gpu(cuda):
-    """The symmetric-memory one-shot path runs on ROCm: a one-rank RCCL group, the buffer
-    rendezvoused and reduced by torch.ops.symm_mem.one_shot_all_reduce (identity at world 1; the
-    multi-peer case needs more than the one GPU of a test box)."""
-    import os
-    import torch.distributed as dist
-    from avenir_amd.parallel.comm import Comm
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = "29617"
-    dev = torch.device(cuda)
-    dev = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    try:
-        comm = Comm(device="cuda")
-        x = torch.randn(3000, device=dev)
-        y = x.clone()
-        comm._all_reduce_p2p(y)
-        comm._all_reduce_p2p(y)            # second call reuses the rendezvoused buffer
-        torch.cuda.synchronize()
-        assert torch.equal(x, y) and len(comm._symm) == 1
-    finally:
-        dist.destroy_process_group()

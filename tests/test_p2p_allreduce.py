@@ -1,0 +1,147 @@
+"""Hand-written peer-mapped all-reduce (csrc/kernels/comm.hip, parallel/p2p.py).
+
+GPU tests: 2 and 4 processes share cuda:0 (the ``gloo:cuda`` harness of ``_dist.py``: gloo only
+carries the one-time IPC handle exchange and barriers).  Each rank maps its peers' staging buffers
+with hipIpcOpenMemHandle and runs 1,000 back-to-back all-reduces of CHANGING data with no host sync
+in between; every result must be bit-equal to the rank-ordered host sum ((x0 + x1) + x2) + ...
+(fp32 random values, so another summation order would differ), for 8 KB and 64 KB (one-shot) and
+1 MB / odd-sized (two-shot) messages of float32 / float64 / int64.  The reference's counterpart
+is the combiner + reducer shuffle of a count table
+(src/main/java/org/avenir/bayesian/BayesianDistribution.java:72-79).
+"""
+import time
+
+import pytest
+import torch
+
+from _dist import run_world
+
+POOL = 8
+
+
+def _pool(world, n, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    if dtype.is_floating_point:
+        return torch.randn(POOL, world, n, generator=g, dtype=dtype)
+    return torch.randint(-(1 << 40), 1 << 40, (POOL, world, n), generator=g, dtype=dtype)
+
+
+def _scale(i, dtype):
+    # float: powers of two keep the rank-ordered sum's bits exact under scaling; int: any factor
+    return float(2.0 ** (i % 5 - 2)) if dtype.is_floating_point else (i % 7) - 3
+
+
+def _ordered_sum(rows):
+    acc = rows[0].clone()
+    for k in range(1, rows.shape[0]):
+        acc += rows[k]
+    return acc
+
+
+def _p2p_world(rank, world, cases, iters):
+    from avenir_amd.parallel.comm import get_comm
+    comm = get_comm()
+    dev = comm.device
+    out = {}
+    for (n, dtype_name, algo) in cases:
+        dtype = getattr(torch, dtype_name)
+        pool = _pool(world, n, dtype, seed=1000 + n)
+        mine = pool[:, rank].to(dev)                             # [POOL, n] this rank's operands
+        res = torch.empty((iters, n), dtype=dtype, device=dev)
+        x = torch.empty(n, dtype=dtype, device=dev)
+        for i in range(iters):                                    # back to back: no host sync
+            torch.mul(mine[i % POOL], _scale(i, dtype), out=x)
+            comm.p2p().all_reduce(x, algo=algo)
+            res[i].copy_(x)
+        comm.p2p().check()
+        got = res.cpu()
+        bad = 0
+        for j in range(POOL):
+            ref = _ordered_sum(pool[j])
+            for i in range(j, iters, POOL):
+                if not torch.equal(got[i], ref * _scale(i, dtype)):
+                    bad += 1
+        out[(n, dtype_name, algo)] = (bad, got[-1].numpy().tobytes())
+    # latency at 8 KB (one-shot) and 1 MB (two-shot), fp32, after the correctness runs
+    lat = {}
+    for nbytes in (8 << 10, 64 << 10, 1 << 20):
+        x = torch.ones(nbytes // 4, device=dev)
+        for _ in range(20):
+            comm.p2p().all_reduce(x)
+        torch.cuda.synchronize()
+        comm.barrier()
+        k = 200
+        t0 = time.perf_counter()
+        for _ in range(k):
+            comm.p2p().all_reduce(x)
+        torch.cuda.synchronize()
+        lat[nbytes] = (time.perf_counter() - t0) / k * 1e6
+    comm.p2p().check()
+    return out, lat, dict(comm.p2p().calls)
+
+
+CASES = [(2048, "float32", None), (16384, "float32", None), (1024, "int64", None), (8192, "int64", None),
+         (262144, "float32", None), (12345, "float64", "twoshot"), (4097, "float32", "oneshot")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_p2p_all_reduce_multiprocess_gpu(world):
+    res = run_world(_p2p_world, world, CASES, 1000, timeout=600, comm="gloo:cuda")
+    for rank, (out, lat, calls) in enumerate(res):
+        for key, (bad, last) in out.items():
+            assert bad == 0, f"rank {rank} case {key}: {bad} of 1000 results differ from the rank-ordered sum"
+            assert last == res[0][0][key][1]                      # bit-identical on every rank
+        assert calls["oneshot"] > 0 and calls["twoshot"] > 0
+    lat0 = res[0][1]
+    print(f"p2p all-reduce, {world} processes on one GPU: " +
+          ", ".join(f"{b >> 10} KiB {us:.1f} us" for b, us in lat0.items()))
+
+
+def _p2p_small_world(rank, world):
+    """Comm.all_reduce(algo="p2p") routes device sums to the kernel and anything else (max, bool)
+    to the library collective; results match the library all-reduce exactly for integers."""
+    from avenir_amd.parallel.comm import get_comm
+    comm = get_comm()
+    dev = comm.device
+    c = torch.arange(37 * 5, device=dev, dtype=torch.int64).view(37, 5) * (rank + 1)
+    a = c.clone()
+    comm.all_reduce(a, algo="p2p")
+    m = torch.full((3,), float(rank), device=dev)
+    comm.all_reduce(m, "max", algo="p2p")
+    strided = torch.arange(64, device=dev, dtype=torch.float64).view(8, 8).t() * (rank + 1)
+    s = strided.clone()
+    comm.all_reduce(s, algo="p2p")                              # non-contiguous operand
+    comm.p2p().check()
+    tot = sum(range(1, world + 1))
+    return (torch.equal(a.cpu(), torch.arange(37 * 5).view(37, 5) * tot),
+            m.cpu().tolist() == [float(world - 1)] * 3,
+            torch.equal(s.cpu(), torch.arange(64, dtype=torch.float64).view(8, 8).t() * tot))
+
+
+@pytest.mark.gpu
+def test_comm_routes_p2p_gpu():
+    for ok in run_world(_p2p_small_world, 2, timeout=300, comm="gloo:cuda"):
+        assert all(ok), ok
+
+
+def _host_fallback(rank, world):
+    from avenir_amd.parallel.comm import get_comm
+    comm = get_comm()
+    x = torch.arange(64, dtype=torch.float64) * (rank + 1)
+    a, b = x.clone(), x.clone()
+    comm.all_reduce(a)
+    comm.all_reduce(b, algo="p2p")          # host tensors: the library collective
+    return torch.equal(a, b) and comm._p2p is None
+
+
+def test_p2p_host_tensors_fall_back():
+    assert all(run_world(_host_fallback, 2, timeout=300))
+
+
+def test_p2p_reference_sum_is_order_sensitive():
+    """The oracle must be able to tell summation orders apart (else the GPU test proves nothing)."""
+    pool = _pool(4, 16384, torch.float32, seed=1)
+    fwd = _ordered_sum(pool[0])
+    rev = _ordered_sum(pool[0].flip(0))
+    assert not torch.equal(fwd, rev)
