@@ -342,6 +342,8 @@ def cond_prob_joiner(args):
         files += input_files(args.model)
     prob_files = [f for f in files if f.name.startswith(pref)]
     pair_files = [f for f in files if not f.name.startswith(pref)]
+    if ctx.native_delim() is not None and prob_files and pair_files:
+        return _cond_prob_joiner_native(ctx, prob_files, pair_files)
     sp = ctx.split
     post = {}
     for f in prob_files:
@@ -367,6 +369,57 @@ def cond_prob_joiner(args):
             c, pr = post[p[0]]
             out.append(d.join([p[1], p[4], p[0], p[2], c, pr]))
     ctx.emit(out)
+
+
+def _cond_prob_joiner_native(ctx, prob_files, pair_files):
+    """Native, data-parallel join (J/knn/FeatureCondProbJoiner.java:105-178 without the shuffle).
+
+    * The posterior table (one prob-only line per TRAINING record, the small side) is tokenized
+      whole by every rank — ``id,prior,cls,prob,...,cls,prob,actualClass`` — and reduced on the
+      device to one (class code, probability code) per line: the first ``cls`` equal to the line's
+      last token (the reducer's ``classVal`` search, :152-158), as strings of its dictionary.
+    * The distance pairs (``trainId,testId,dist,trainClass,testClass``: the O(test x train) side)
+      are tokenized by byte range — each rank reads only its range — with only ``trainId``
+      dictionary-coded; one host pass over the DICTIONARY (not the pairs) maps train-id codes to
+      posterior lines, and the join itself is one device gather.
+    * Output ``testId,testClass,trainId,dist,trainClass,postProb`` (:170-175) is assembled by the
+      native formatter from raw input fields and the posterior strings (device formatter for
+      large outputs).  Pairs whose training id has no posterior line are dropped."""
+    lit = ctx.native_delim()
+    prob = ctx.records([str(f) for f in prob_files], shard=False, modes="", tail_mode="d")
+    P = prob.n_lines
+    dev = prob.device
+    M, cnt = prob.padded(dtype=torch.int32)
+    if P and M.shape[1] >= 4:
+        last = prob.codes[prob.off[1:] - 1].to(torch.int32)
+        cand = M[:, 2:M.shape[1] - 1:2]                                  # cls tokens at 2, 4, ...
+        pos = 2 + 2 * torch.arange(cand.shape[1], device=dev)
+        match = (cand == last.view(-1, 1)) & (pos.view(1, -1) < (cnt.view(-1, 1) - 1))
+        has = match.any(1)
+        first = match.int().argmax(1)
+        rows = torch.arange(P, device=dev)
+        cls_code = M[rows, 2 + 2 * first]
+        prob_code = M[rows, 3 + 2 * first]
+    else:
+        has = torch.zeros(P, dtype=torch.bool, device=dev)
+        cls_code = prob_code = torch.zeros(P, dtype=torch.int32, device=dev)
+    ids = prob.strings(M[:, 0].cpu()) if P else []
+    ok_host = has.cpu().tolist()
+    line_of = {}
+    for i, (k, ok) in enumerate(zip(ids, ok_host)):
+        if ok and k not in line_of:
+            line_of[k] = i
+    pairs = ctx.records([str(f) for f in pair_files], modes="d", tail_mode="x")
+    lut = torch.tensor([line_of.get(v, -1) for v in pairs.vocab] + [-1], dtype=torch.int64, device=pairs.device)
+    tid = pairs.field(0).long()
+    line = lut[torch.where(tid >= 0, tid, torch.full_like(tid, len(pairs.vocab)))]
+    keep = torch.nonzero(line >= 0).view(-1)
+    sel = line[keep].to(cls_code.device)
+    spans = pairs.line_spans().select(keep)
+    cols = [spans.column("rf", 1, lit), spans.column("rf", 4, lit), spans.column("rf", 0, lit),
+            spans.column("rf", 2, lit), ("s", prob.vocab, cls_code[sel].to(pairs.device)),
+            ("s", prob.vocab, prob_code[sel].to(pairs.device))]
+    ctx.emit_columns(cols, int(keep.numel()))
 
 
 @job("nearestNeighbor", "kNN from precomputed distance pairs (J/knn/NearestNeighbor.java, nen.*; R/knn.sh knnClassifier)")

@@ -93,6 +93,32 @@ def setup(job: str, d: str, n: int, dev: str):
     raise SystemExit(f"unknown job {job}")
 
 
+def setup_fcb(d: str, n: int):
+    """featureCondProbJoiner on ``n`` distance pairs (``trainId,testId,dist,trainCls,testCls``;
+    4,096 training records x n / 4,096 test records) plus a 4,096-line posterior file."""
+    import numpy as np
+    ntr = 4096
+    nte = max(1, n // ntr)
+    rng = np.random.default_rng(7)
+    pdir = os.path.join(d, "fcb_in")
+    os.makedirs(pdir, exist_ok=True)
+    cls = ["pass", "fail"]
+    with open(os.path.join(pdir, "prDistr-00000"), "w") as fh:
+        for t in range(ntr):
+            p = rng.random()
+            fh.write(f"T{t},{rng.random():.4f},pass,{p:.6f},fail,{1 - p:.6f},{cls[t % 2]}\n")
+    head = [f"T{t}," for t in range(ntr)]
+    tail = [f",{cls[t % 2]}," for t in range(ntr)]
+    with open(os.path.join(pdir, "part-00000"), "w") as fh:
+        for q in range(nte):
+            dist = rng.integers(0, 100000, ntr).tolist()
+            qs = f"Q{q},"
+            qc = cls[q % 2] + "\n"
+            fh.write("".join(h + qs + str(v) + tl + qc for h, v, tl in zip(head, dist, tail)))
+    cfg = _props(d, "fcb.properties", "fcb.feature.cond.prob.split.prefix=prDistr\n")
+    return ["featureCondProbJoiner", "-i", pdir, "-c", cfg], os.path.join(pdir, "part-00000")
+
+
 def setup_rs(d: str, n: int):
     """recordSimilarity on ``n`` records x 8 uniform dims: the all-pairs ring
     with a distance threshold that keeps ~1e-4 of the pairs."""
@@ -122,7 +148,12 @@ def main() -> int:
     d = tempfile.mkdtemp(prefix="avmi_pred_", dir=args.dir)
     for job in args.jobs.split(","):
         n_rec = args.rs_records if job == "rs" else args.records
-        argv, data = setup_rs(d, n_rec) if job == "rs" else setup(job, d, args.records, dev)
+        if job == "rs":
+            argv, data = setup_rs(d, n_rec)
+        elif job == "fcb":
+            argv, data = setup_fcb(d, n_rec)
+        else:
+            argv, data = setup(job, d, args.records, dev)
         best = None
         for rep in range(args.reps):
             # a fresh output path per run (a job writes a new output; re-using one would time the
