@@ -1448,7 +1448,8 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
   const int64_t B = y.size(0), N = y.size(1);
   TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
               "alpha / G must be [B, >= N]");
-  TORCH_CHECK(h >= 1 && h <= 64 && N >= 1 && N <= (1 << 18), "1 <= h <= 64, 1 <= N <= 2^18");
+  TORCH_CHECK(h >= 1 && h <= 64 && N >= 1 && N <= (1 << 26) && (N <= (1 << 18) || h == 64),
+              "1 <= h <= 64, 1 <= N <= 2^26 (h = 64 above 2^18)");
   CHECK_DEV(ws);
   CHECK_DTYPE(ws, at::kLong);
   CHECK_DEV(ok);
@@ -1459,7 +1460,7 @@ void smo_ws_select(const at::Tensor& alpha, const at::Tensor& G, const at::Tenso
   // graph capture these come from the capture's private pool)
   const int64_t parts = avk::smo_ws_select_parts((int)N);
   auto cand = at::empty({2, B, parts, 2, h}, y.options().dtype(at::kInt));  // rows, then float values
-  auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
+  auto cnt = at::empty({B, std::max<int64_t>(parts, 64), 2}, y.options().dtype(at::kInt));  // <= 64 streaming parts
   avk::smo_ws_select(alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)N,
                      (int)alpha.size(1), (float)C, (int)h, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()),
                      ok.data_ptr<bool>(), gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(),
@@ -1552,7 +1553,7 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
   }
   TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
   const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
-  TORCH_CHECK(N >= 1 && N <= (1 << 18), "1 <= N <= 2^18");
+  TORCH_CHECK(N >= 1 && N <= (1 << 26), "1 <= N <= 2^26");
   TORCH_CHECK(K.dim() == 3 && (K.size(0) == B || K.size(0) == 1) && K.size(1) == N && K.size(2) == N,
               "K must be [B or 1 (shared by all problems), N, N]");
   const long long kbs = K.size(0) == 1 ? 0LL : (long long)N * N;
@@ -1570,7 +1571,7 @@ int64_t smo_ws_run(const at::Tensor& K, at::Tensor& alpha, at::Tensor& G, const 
   DevGuard g(y.device());
   const int64_t parts = avk::smo_ws_select_parts((int)N);
   auto cand = at::empty({2, B, parts, 2, Q / 2}, y.options().dtype(at::kInt));  // rows, then float values
-  auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
+  auto cnt = at::empty({B, std::max<int64_t>(parts, 64), 2}, y.options().dtype(at::kInt));  // <= 64 streaming parts
   auto Kws = at::empty({B, Q, Q}, K.options());
   auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
   auto gap_next = at::empty({B}, y.options());
@@ -1622,7 +1623,7 @@ int64_t smo_ws_run_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, do
   }
   TORCH_CHECK(y.dim() == 2, "y must be [B, N]");
   const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
-  TORCH_CHECK(N >= 1 && N <= (1 << 18), "1 <= N <= 2^18");
+  TORCH_CHECK(N >= 1 && N <= (1 << 26), "1 <= N <= 2^26");
   const avk::SvmKerX k = make_kerx(X, xn, B, N, kind, gamma, coef0, degree);
   TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
               "alpha / G must be [B, >= N]");
@@ -1638,7 +1639,7 @@ int64_t smo_ws_run_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, do
   DevGuard g(y.device());
   const int64_t parts = avk::smo_ws_select_parts((int)N);
   auto cand = at::empty({2, B, parts, 2, Q / 2}, y.options().dtype(at::kInt));
-  auto cnt = at::empty({B, parts, 2}, y.options().dtype(at::kInt));
+  auto cnt = at::empty({B, std::max<int64_t>(parts, 64), 2}, y.options().dtype(at::kInt));  // <= 64 streaming parts
   auto Kws = at::empty({B, Q, Q}, y.options());
   auto host_gap = at::empty({2 * B}, at::TensorOptions().dtype(at::kFloat).pinned_memory(true));
   return avk::smo_ws_run(nullptr, (int)N, alpha.data_ptr<float>(), G.data_ptr<float>(), y.data_ptr<float>(), (int)B,

@@ -1242,6 +1242,100 @@ __global__ __launch_bounds__(SEL_T) void smo_ws_topk_part_kernel(const float* __
   if (lane == 0) cnt[((long long)b * parts + p) * 2 + w] = np;
 }
 
+// Streaming top-k part selection for large N (no row cap): the first level of the two-level
+// selection when N is too large for register-resident blocks (select_part_per(N) == 0, N > 2^17).
+// Part p of problem b owns the 64-row blocks p, p + parts, .. (block-cyclic as above), ``per``
+// blocks per wave, walked in chunks of 4 blocks whose alpha / G / y loads are issued together
+// (12 loads in flight per lane).  Every lane keeps its own 4 largest keys per side in a sorted
+// register list (compare-swap insertion), so the wave's 4 largest per side are exact for ANY per
+// (they can all sit in one lane); then waves 0 / 1 take the HP largest of the 16 waves' 4
+// candidates, as in smo_ws_topk_part_kernel.  The host picks per so that parts <= 64 and
+// parts x HP <= 256 (the 512-thread rank merge).
+template <int HP>
+__global__ __launch_bounds__(SEL_T) void smo_ws_topk_stream_kernel(const float* __restrict__ alpha,
+                                                                   const float* __restrict__ G,
+                                                                   const float* __restrict__ y, int N, int ldag,
+                                                                   float C, int parts, int per,
+                                                                   int* __restrict__ cand, int* __restrict__ cnt,
+                                                                   float* __restrict__ candv,
+                                                                   const float* __restrict__ gap, float skip) {
+  constexpr int NW = SEL_T / 64, HW = 4, CH = 4;
+  static_assert(HP >= 4 && HP <= 64, "HP");
+  __shared__ unsigned long long s_k[2][NW * HW];
+  const int b = blockIdx.y, p = blockIdx.x;
+  if (ws_done(gap, b, skip)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* ab = alpha + (long long)b * ldag;
+  const float* gb = G + (long long)b * ldag;
+  const float* yb = y + (long long)b * N;
+  unsigned long long top[2][HW];
+#pragma unroll
+  for (int i = 0; i < HW; ++i) top[0][i] = top[1][i] = 0ull;
+  for (int j0 = 0; j0 < per; j0 += CH) {
+    float yv[CH], av[CH], gv[CH];
+    long long nv[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const long long blk = (long long)((j0 + c) * NW + wv) * parts + p;
+      nv[c] = blk * 64 + lane;
+      const bool in = j0 + c < per && nv[c] < N;
+      yv[c] = in ? yb[nv[c]] : 0.f;
+      av[c] = in ? ab[nv[c]] : 0.f;
+      gv[c] = in ? gb[nv[c]] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const float v = yv[c] != 0.f ? ws_violation(w, yv[c], av[c], gv[c], C) : -INFINITY;
+        unsigned long long k = v > -INFINITY ? ((unsigned long long)order_key(v) << 32) | (unsigned)~(unsigned)nv[c] : 0ull;
+#pragma unroll
+        for (int i = 0; i < HW; ++i) {  // sorted descending: bubble k into place
+          const unsigned long long t = top[w][i];
+          const bool gt = k > t;
+          top[w][i] = gt ? k : t;
+          k = gt ? t : k;
+        }
+      }
+    }
+  }
+  for (int it = 0; it < HW; ++it) {  // the wave's HW largest per side: pop the lane heads
+    unsigned long long m0 = top[0][0], m1 = top[1][0];
+    wave_max2_u64(m0, m1);
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const unsigned long long m = w ? m1 : m0;
+      if (m != 0ull && top[w][0] == m) {
+#pragma unroll
+        for (int i = 0; i + 1 < HW; ++i) top[w][i] = top[w][i + 1];
+        top[w][HW - 1] = 0ull;
+      }
+    }
+    if (lane == 0) {
+      s_k[0][wv * HW + it] = m0;
+      s_k[1][wv * HW + it] = m1;
+    }
+  }
+  __syncthreads();
+  if (wv >= 2) return;
+  const int w = wv;
+  unsigned long long c0 = s_k[w][lane];  // NW * HW = 64 candidates: one per lane
+  int* cb = cand + ((long long)b * parts + p) * 2 * HP + w * HP;
+  float* vb = candv + ((long long)b * parts + p) * 2 * HP + w * HP;
+  int np = 0;
+  for (int it = 0; it < HP; ++it) {
+    const unsigned long long m = wave_max_u64(c0);
+    if (c0 == m) c0 = 0ull;
+    if (m == 0ull) break;  // wave-uniform
+    if (lane == 0) {
+      cb[it] = (int)~(unsigned)m;
+      vb[it] = order_key_inv((unsigned)(m >> 32));
+    }
+    ++np;
+  }
+  if (lane == 0) cnt[((long long)b * parts + p) * 2 + w] = np;
+}
+
 // Rank merge of the parts' candidates (replaces the radix merge for the two-level path): the
 // parts hand over (row, violation) pairs, so every candidate's 64-bit key (order_key(v) << 32 |
 // ~row: larger = more violating, ties to the lower row — the same order as the radix selection)
@@ -1856,9 +1950,17 @@ static int select_part_per(int N, int h) {
   return 0;
 }
 
+// large N (no register-resident part size): the streaming parts, <= 64 parts x 4 candidates per
+// side = 4 x h slots of the [parts][2][h] allocation
+static void stream_plan(int N, int* parts, int* per) {
+  const long long blocks = ((long long)N + 63) / 64;
+  *per = (int)((blocks + 64LL * (SEL_T / 64) - 1) / (64LL * (SEL_T / 64)));  // parts <= 64
+  *parts = (int)((blocks + (long long)*per * (SEL_T / 64) - 1) / ((long long)*per * (SEL_T / 64)));
+}
+
 int smo_ws_select_parts(int N) {
   const int per = select_part_per(N, 64);
-  return per ? (N + per * SEL_T - 1) / (per * SEL_T) : 1;
+  return per ? (N + per * SEL_T - 1) / (per * SEL_T) : 4;
 }
 
 // The rank merge of a two-level selection, when the caller launches it itself (fused with the gather)
@@ -1943,6 +2045,32 @@ static void select_impl(const float* alpha, const float* G, const float* y, int 
       return;
     }
   }
+  if (!per && cand && h == 64) {
+    // large N: streaming parts (<= 64) + the rank merge over <= 256 candidates per side
+    int parts = 0, sper = 0;
+    stream_plan(N, &parts, &sper);
+    const int hp = parts * 4 <= 128 ? (parts * 8 <= 128 ? 8 : 4) : 4;
+    float* candv = reinterpret_cast<float*>(cand + (long long)B * smo_ws_select_parts(N) * 2 * h);
+    const dim3 pg(parts, B);
+    if (hp == 8)
+      smo_ws_topk_stream_kernel<8><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, parts, sper, cand, cnt, candv,
+                                                             gap, skip);
+    else
+      smo_ws_topk_stream_kernel<4><<<pg, SEL_T, 0, stream>>>(alpha, G, y, N, ldag, C, parts, sper, cand, cnt, candv,
+                                                             gap, skip);
+    AV_HIP_CHECK(hipGetLastError());
+    if (plan) {
+      *plan = MergePlan{parts, hp, hp, parts * hp <= 128 ? 256 : 512, candv};
+      return;
+    }
+    if (parts * hp <= 128)
+      smo_ws_merge_rank_kernel<256><<<B, 256, 0, stream>>>(h, hp, hp, parts, cand, cnt, candv, ws, ok, gap, skip);
+    else
+      smo_ws_merge_rank_kernel<512><<<B, 512, 0, stream>>>(h, hp, hp, parts, cand, cnt, candv, ws, ok, gap, skip);
+    AV_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (N > (1 << 18)) throw std::runtime_error("smo_ws_select: N > 2^18 needs the candidate buffers (cand)");
   if (N <= 4 * SEL_T) {
     smo_ws_select2_kernel<4><<<B, SEL_T, lds, stream>>>(alpha, G, y, N, ldag, C, h, ws, ok, gap, skip);
   } else if (cand && per) {

@@ -48,6 +48,8 @@ def main() -> int:
     ap.add_argument("--paths", default="dense,implicit")
     ap.add_argument("--sklearn", action="store_true")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--sklearn-sub", type=int, default=0,
+                    help="also fit sklearn on a random subsample of this many rows and compare held-out accuracy")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     gamma = 0.5
@@ -73,10 +75,22 @@ def main() -> int:
                 best = (dt, m, peak) if best is None or dt < best[0] else best
             dt, m, peak = best
             acc = float((m.predict(X) == y).float().mean())
+            Xt, yt = problem(20000, args.d, seed=11)
+            held = float((m.predict(Xt) == yt).float().mean())
             rec = {"bench": "svm_fit", "N": N, "d": args.d, "path": path, "seconds": round(dt, 5),
                    "outer_steps": S.LAST_SOLVE.get("outer"), "solver": S.LAST_SOLVE.get("solver"),
                    "support_vectors": int(m.support_.numel()), "train_acc": acc,
+                   "heldout_acc": held, "inner_steps": int(sum(m.iters)),
+                   "inner_per_outer": sum(m.iters) / max(1, S.LAST_SOLVE.get("outer") or 1),
                    "peak_bytes": int(peak), "dense_matrix_bytes": 4 * N * N}
+            if args.sklearn_sub:
+                from sklearn.svm import SVC as SKSVC
+                sub = torch.randperm(N, generator=torch.Generator().manual_seed(3))[:args.sklearn_sub].to(X.device)
+                t0 = time.perf_counter()
+                skm = SKSVC(C=1.0, kernel="rbf", gamma=gamma, tol=1e-3).fit(X[sub].cpu().numpy(), y[sub].cpu().numpy())
+                rec["sklearn_sub_rows"] = args.sklearn_sub
+                rec["sklearn_sub_s"] = time.perf_counter() - t0
+                rec["sklearn_sub_heldout_acc"] = float((skm.predict(Xt.cpu().numpy()) == yt.cpu().numpy()).mean())
             if sk:
                 rec.update(sk)
                 rec["speedup_vs_sklearn"] = sk["sklearn_s"] / dt

@@ -96,7 +96,19 @@ def forest():
     torch.cuda.synchronize()
 
 
-TARGETS = {"rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
+def kmeans():
+    """K16 Lloyd pass at 16.7 M rows x 16 dims x 16 centroids."""
+    from avenir_amd.models.cluster import kmeans_step
+    g = torch.Generator(device="cuda").manual_seed(0)
+    n, D, k = 1 << 24, 16, 16
+    X = torch.randn((n, D), device="cuda", generator=g)
+    C = X[torch.randint(0, n, (k,), device="cuda", generator=g)].clone()
+    for _ in range(6):
+        kmeans_step(X, [C])
+    torch.cuda.synchronize()
+
+
+TARGETS = {"kmeans": kmeans, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
            "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest}
 
 if __name__ == "__main__":

@@ -4,7 +4,7 @@
 # WRITE_SIZE) so no block exceeds its counter slots.  Summary: scripts/pmc_summary.py.
 set -eo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
-O=gpurun_out/pmc
+O=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $O
 timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 SQ=""
