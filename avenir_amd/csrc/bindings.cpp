@@ -2349,7 +2349,7 @@ static uint32_t fnv1a_fold(const std::string& v) {
   return h ^ (h >> 15);
 }
 
-py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std::string& delim, bool skip_header,
+py::object csv_parse_device(const std::string& path, py::list specs_py, const std::string& delim, bool skip_header,
                            int64_t rank, int64_t world, const at::Tensor& like) {
   CHECK_DEV(like);
   TORCH_CHECK(delim.size() == 1, "device CSV parse: single-character delimiter");
@@ -2547,6 +2547,9 @@ py::tuple csv_parse_device(const std::string& path, py::list specs_py, const std
                         reinterpret_cast<unsigned long long*>((last_group ? bad : bad_scratch).data_ptr<int64_t>()),
                         stream);
   }
+  // a token of > 19 significant digits the device could not round for certain: the caller
+  // re-parses the file on the host (strtod), so both paths keep giving the same bits
+  if (avk::csv_slow_tokens_take(stream) != 0) return py::none();
   py::list cols;
   for (auto& o : outs) cols.append(o);
   // the rows' byte spans in the file (raw-line output of the jobs: data/lines.py)
@@ -2983,6 +2986,8 @@ py::object text_tokenize_device(std::vector<std::string> paths, int64_t rank, in
     TORCH_CHECK(cap < (1LL << 31), "device tokenizer: dictionary table exceeds 2^31 slots");
     cap <<= 2;  // more distinct values than the table holds at load 1/2: retry with a 4x table
   }
+  // a number of > 19 significant digits the device could not round for certain: host tokenizer
+  if (avk::rec_slow_tokens_take(stream) != 0) return py::none();
   // ---- dense codes in first-occurrence order ----
   auto used = at::nonzero(first != -1).view({-1});
   const int64_t D = used.numel();

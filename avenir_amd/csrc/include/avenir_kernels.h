@@ -234,6 +234,10 @@ void class_histogram_dense(const uint32_t* dense, long long n, int B, const int*
                            hipStream_t stream);
 // K1 device CSV parse (csv.hip)
 long long csv_chunks(long long size);
+// tokens parsed since the last call whose rounding the device could not settle (then re-parse on the
+// host); synchronises the stream
+unsigned long long csv_slow_tokens_take(hipStream_t stream);
+unsigned long long rec_slow_tokens_take(hipStream_t stream);
 void csv_newline_counts(const uint8_t* bytes, long long size, unsigned* counts, hipStream_t stream);
 void csv_newline_positions(const uint8_t* bytes, long long size, const long long* offsets, long long* pos,
                            hipStream_t stream);

@@ -140,9 +140,16 @@ __device__ __forceinline__ bool is_space(uint8_t c) { return c == ' ' || c == '\
 
 // the host parser's decimal conversion (csrc/host/csv.cpp parse_double, avenir_numparse.h), NaN on
 // garbage / empty; [p, e) is trimmed by the caller
+// tokens of more than 19 significant digits whose rounding the device cannot settle (see
+// avenir_numparse.h tier 3): counted here, read and reset by avk::csv_slow_tokens_take; the host
+// then re-parses the file with the host parser (strtod for those tokens)
+__device__ unsigned long long g_csv_slow_tokens;
+
 __device__ double dev_parse_double(const uint8_t* p, const uint8_t* e) {
   bool slow;
-  return avnum::parse_decimal(reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(e), &slow);
+  const double v = avnum::parse_decimal(reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(e), &slow);
+  if (slow) atomicAdd(&g_csv_slow_tokens, 1ull);
+  return v;
 }
 
 constexpr int CSV_MAX_SPECS = 64;  // columns per parse pass (the host splits wider schemas)
@@ -272,6 +279,18 @@ __global__ __launch_bounds__(CT) void csv_parse_kernel(const uint8_t* __restrict
 }  // namespace
 
 namespace avk {
+
+unsigned long long csv_slow_tokens_take(hipStream_t stream) {
+  unsigned long long v = 0, zero = 0;
+  AV_HIP_CHECK(hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_csv_slow_tokens), sizeof(v), 0, hipMemcpyDeviceToHost, stream));
+  AV_HIP_CHECK(hipStreamSynchronize(stream));
+  if (v) {
+    AV_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_csv_slow_tokens), &zero, sizeof(zero), 0, hipMemcpyHostToDevice, stream));
+    AV_HIP_CHECK(hipStreamSynchronize(stream));
+  }
+  return v;
+}
+
 
 long long csv_chunks(long long size) { return (size + CHUNK - 1) / CHUNK; }
 

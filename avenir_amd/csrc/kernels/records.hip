@@ -69,11 +69,17 @@ __device__ __forceinline__ unsigned hash32(const uint8_t* p, int n) {
 
 // host parse_num semantics (records.cpp, avenir_numparse.h): trim, [+-]digits[.digits][e[+-]digits],
 // correctly rounded on the fast path, NaN otherwise
+// tokens whose rounding the device cannot settle (> 19 significant digits, avenir_numparse.h tier
+// 3): counted, read and reset by avk::rec_slow_tokens_take; the host then tokenizes the shard itself
+__device__ unsigned long long g_rec_slow_tokens;
+
 __device__ double parse_num(const uint8_t* p, const uint8_t* e) {
   while (p < e && is_ws(*p)) ++p;
   while (e > p && is_ws(e[-1])) --e;
   bool slow;
-  return avnum::parse_decimal(reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(e), &slow);
+  const double v = avnum::parse_decimal(reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(e), &slow);
+  if (slow) atomicAdd(&g_rec_slow_tokens, 1ull);
+  return v;
 }
 
 __global__ __launch_bounds__(RT) void rec_lines_kernel(const uint8_t* __restrict__ bytes,
@@ -281,6 +287,18 @@ TokArgs make_args(const char* delims, int ndelims, const char* modes, int nmodes
 }  // namespace
 
 namespace avk {
+
+unsigned long long rec_slow_tokens_take(hipStream_t stream) {
+  unsigned long long v = 0, zero = 0;
+  AV_HIP_CHECK(hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_rec_slow_tokens), sizeof(v), 0, hipMemcpyDeviceToHost, stream));
+  AV_HIP_CHECK(hipStreamSynchronize(stream));
+  if (v) {
+    AV_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_rec_slow_tokens), &zero, sizeof(zero), 0, hipMemcpyHostToDevice, stream));
+    AV_HIP_CHECK(hipStreamSynchronize(stream));
+  }
+  return v;
+}
+
 
 void rec_lines(const uint8_t* bytes, const long long* nlpos, long long nraw, const char* delims, int ndelims,
                long long* lstart, long long* lend, int* ntok, hipStream_t stream) {

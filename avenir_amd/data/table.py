@@ -449,8 +449,10 @@ def _load_csv_device(C, path, schema, delim, skip_header, rank, world, dev, feat
     if any(sp[1] not in (CAT, BUCKET, FLOAT) for sp in specs):
         return None
     like = torch.empty(0, device=dev)
-    cols, n, _bad, _total, r0, starts, ends, fbytes = C.csv_parse_device(str(path), specs, _literal(delim or ","),
-                                                                         skip_header, int(rank), int(world), like)
+    r = C.csv_parse_device(str(path), specs, _literal(delim or ","), skip_header, int(rank), int(world), like)
+    if r is None:       # a number the device could not round for certain: the host parser (strtod)
+        return None
+    cols, n, _bad, _total, r0, starts, ends, fbytes = r
     ld = pad16(n)
     cdt = torch.uint16 if wide else torch.uint8
     codes = (torch.stack([c[:ld] for c in cols[: len(binned)]]) if binned

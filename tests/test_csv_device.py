@@ -104,3 +104,34 @@ def test_device_csv_wide_schema_over_32mb(cuda, tmp_path):
     assert gpu.codes.shape[0] + gpu.numeric.shape[0] >= 79
     assert gpu.lines[:100].tolist() == cpu.lines[:100].tolist()
     assert gpu.lines[-3:].tolist() == cpu.lines[-3:].tolist() and len(gpu.lines) == len(cpu.lines)
+
+
+@pytest.mark.gpu
+def test_device_csv_full_precision_doubles(cuda, tmp_path, monkeypatch):
+    """the device CSV parser rounds full-precision doubles (repr / Java Double.toString,
+    subnormals, long exponents: the Eisel-Lemire tier of avenir_numparse.h) exactly as the host
+    parser, so the column bits do not depend on which parser the file size picks; a token the
+    device cannot settle (> 19 digits on a rounding midpoint) sends the file to the host parser."""
+    import random
+    import struct
+    monkeypatch.setattr(TB, "_GPU_CSV_MIN_BYTES", 0)
+    rnd = random.Random(11)
+    vals = []
+    while len(vals) < 20000:
+        d = struct.unpack("<d", struct.pack("<Q", rnd.getrandbits(64)))[0]
+        if d == d and abs(d) < 1e300:
+            vals.append(repr(d))
+    vals += [repr(rnd.uniform(1, 10) * 10.0 ** -rnd.randint(300, 323)) for _ in range(500)]
+    fields = [{"name": "id", "ordinal": 0, "id": True, "dataType": "string"},
+              {"name": "x", "ordinal": 1, "dataType": "double", "feature": True},
+              {"name": "cls", "ordinal": 2, "dataType": "categorical", "classAttribute": True,
+               "cardinality": ["T", "F"]}]
+    schema = FeatureSchema.from_json({"fields": fields})
+    p = tmp_path / "dbl.csv"
+    p.write_text("".join(f"r{i},{v},{'TF'[i % 2]}\n" for i, v in enumerate(vals)))
+    for raw in (False, True):
+        cpu, gpu = _compare(p, schema, raw_numeric=raw)
+    p2 = tmp_path / "amb.csv"
+    p2.write_text("".join(f"r{i},{'9007199254740993.0000000000001' if i == 5 else v},{'TF'[i % 2]}\n"
+                          for i, v in enumerate(vals[:3000])))
+    _compare(p2, schema, raw_numeric=True)

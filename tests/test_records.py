@@ -259,21 +259,64 @@ def test_numeric_tokens_are_correctly_rounded(tmp_path):
         assert a == w and b == w, (t, a, b, w)
 
 
+def _hard_tokens(n=3000, seed=5):
+    """Full-precision doubles (repr: up to 17 digits, any exponent), subnormals, 18-19 digit
+    mantissas and long exponents: the Eisel-Lemire tier of avenir_numparse.h."""
+    import random as _r
+    import struct
+    rnd = _r.Random(seed)
+    out = []
+    while len(out) < n:
+        d = struct.unpack("<d", struct.pack("<Q", rnd.getrandbits(64)))[0]
+        if math.isfinite(d):
+            out.append(repr(d))
+    out += [repr(rnd.uniform(1, 10) * 10.0 ** -rnd.randint(300, 323)) for _ in range(300)]        # subnormals
+    out += [f"{rnd.randint(10**17, 10**19 - 1)}e{rnd.randint(-330, 290)}" for _ in range(300)]      # 18-19 digits
+    out += ["2.4703282292062328e-324", "2.2250738585072011e-308", "1.7976931348623158e308", "9007199254740993"]
+    return out
+
+
+@pytest.mark.skipif(not _native.available(), reason="native extension not built")
+def test_host_parser_correctly_rounds_full_precision_doubles(tmp_path):
+    toks = _hard_tokens()
+    p = tmp_path / "hard.txt"
+    p.write_text("".join(f"r{i},{t}\n" for i, t in enumerate(toks)))
+    nat = R.read_records(str(p), modes="xn", numeric=True).field(1, numeric=True).tolist()
+    assert nat == [float(t) for t in toks]
+
+
 @pytest.mark.gpu
 def test_device_numeric_tokens_match_host(tmp_path, cuda, monkeypatch):
-    """The device tokenizer shares the parser: identical bits on the fast path (every token of up
-    to 15 significant digits and |exponent| <= 22)."""
-    p = _num_file(tmp_path, reps=400)
+    """The device tokenizer shares the parser: identical bits for EVERY token — the
+    Clinger fast path, full-precision doubles, subnormals and > 19-digit mantissas through
+    Eisel-Lemire — and equal to Python's float()."""
+    toks = _NUM_TOKENS * 50 + _hard_tokens()
+    p = tmp_path / "nums.txt"
+    p.write_text("".join(f"r{i},{t}\n" for i, t in enumerate(toks)))
     monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
     dev = R.read_records(str(p), device=cuda, modes="xn", numeric=True)
     assert dev.stats.get("path") == "device"
     host = R.read_records(str(p), modes="xn", numeric=True)
     a, b = dev.field(1, numeric=True).cpu(), host.field(1, numeric=True)
-    fast = torch.tensor([len(t.strip().lstrip("+-").replace(".", "").lstrip("0")) <= 15 and "e" not in t.lower()
-                         for t in _NUM_TOKENS] * 400)
     assert torch.equal(torch.isnan(a), torch.isnan(b))
-    ok = fast & ~torch.isnan(b)
+    ok = ~torch.isnan(b)
     assert torch.equal(a[ok], b[ok])
+    want = torch.tensor([_py_float(t) for t in toks], dtype=torch.float64)
+    assert torch.equal(a[ok], want[ok])
+
+
+@pytest.mark.gpu
+def test_device_tokenizer_hands_undecidable_numbers_to_the_host(tmp_path, cuda, monkeypatch):
+    """A 29-digit token a hair above the midpoint 2^53 + 1: its first 19 digits alone sit exactly on
+    the midpoint (round to even -> 2^53), so the device cannot settle it; the shard goes to the
+    host tokenizer (strtod), which rounds up to 2^53 + 2 like Python's float()."""
+    tok = "9007199254740993.0000000000001"
+    p = tmp_path / "amb.txt"
+    p.write_text("".join(f"r{i},{tok if i == 777 else '1.5'}\n" for i in range(2000)))
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)
+    rec = R.read_records(str(p), device=cuda, modes="xn", numeric=True)
+    assert rec.stats.get("path") == "host"
+    assert rec.field(1, numeric=True)[777].item() == float(tok) == 9007199254740994.0
 
 
 def test_format_lines_pyrepr_and_raw_kinds(tmp_path):
