@@ -326,7 +326,7 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
         outer = 1
         from ..utils.hipgraph import capturing
         g = torch.cuda.CUDAGraph()
-        with capturing(g):
+        with capturing(g, device=st.K.device):
             for _ in range(check_every):
                 st.step()
             st.refresh_gap()

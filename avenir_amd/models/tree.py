@@ -1442,7 +1442,7 @@ class GradientBoostedTrees:
                     st["F"].copy_(Fsave)
                 torch.cuda.current_stream(dev).wait_stream(s_)
                 gr = torch.cuda.CUDAGraph()
-                with capturing(gr):                  # no allocator flush per fit (utils/hipgraph.py)
+                with capturing(gr, device=dev):      # no allocator flush per fit (utils/hipgraph.py)
                     self._build_tree(st, k)
                 graphs[k] = gr
             graphs[k].replay()
@@ -1482,7 +1482,7 @@ class GradientBoostedTrees:
                 torch.cuda.synchronize(dev)
                 marks.append(("round0", _time.perf_counter()))
             round_graph = torch.cuda.CUDAGraph()
-            with capturing(round_graph):
+            with capturing(round_graph, device=dev):
                 round_body()
             if timing:
                 torch.cuda.synchronize(dev)

@@ -205,7 +205,7 @@ class GraphedStep:
             torch.cuda.current_stream().wait_stream(s)
             from ..utils.hipgraph import capturing
             self.graph = torch.cuda.CUDAGraph()
-            with capturing(self.graph):
+            with capturing(self.graph, device=self.sx.device):
                 self.sloss = self.fn(self.sx, self.sy)
             with torch.no_grad():
                 if snap is not None:

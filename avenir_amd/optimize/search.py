@@ -17,7 +17,11 @@ Reference behaviour:
 MI355X design: the population / the set of chains / the set of islands is the batch axis of
 device tensors.  Simulated annealing over an :class:`AssignmentDomain` runs entirely inside one
 K22 kernel launch (one chain per lane, solution tile in LDS); the other optimisers issue a few
-batched tensor ops per generation.  Chains and islands are indexed GLOBALLY (their random streams
+batched tensor ops per generation — except that the genetic algorithm runs one generation per
+ISLAND (each island draws from its own generator, keyed by global island index, so that results do
+not depend on the world size): its launches per generation grow with the islands on a rank (~12
+small ops each), which is fine for the reference's few islands per partition but not for hundreds.
+Chains and islands are indexed GLOBALLY (their random streams
 are keyed by global index, not by rank): rank r runs its block of them, the W-rank run equals one
 process running all of them, the global best is one tiny all-gather, and checkpoints re-deal the
 chains / islands over any world size on resume.
@@ -102,8 +106,9 @@ class SimulatedAnnealing:
         d = self.domain
         kernel_ok = isinstance(d, AssignmentDomain) and self.step == 1 and d.L <= 512
         use_kernel = kernel_ok if self.use_kernel is None else (self.use_kernel and kernel_ok)
+        chain_base = None
         if use_kernel:
-            best, bc, stats, gen = self._run_kernel(comm, init)
+            best, bc, stats, gen, chain_base = self._run_kernel(comm, init)
         else:
             seed = self.seed + 1_000_003 * comm.rank
             gen = _gen(d.device, seed)
@@ -114,7 +119,15 @@ class SimulatedAnnealing:
                                device=d.device) as lp:
                 best, bc, stats = self._generic(sol, d.evaluate(sol), gen, lp)
         if self.locally_optimize:
-            best, bc = local_focussed(d, best, bc, self.local_iters, gen)
+            if chain_base is None:      # generic path: the rank's generator (as its chains)
+                best, bc = local_focussed(d, best, bc, self.local_iters, gen)
+            else:                       # kernel path: one generator per GLOBAL chain, so the result
+                outs = [local_focussed(d, best[p:p + 1], bc[p:p + 1], self.local_iters,  # does not depend on W
+                                       _gen(d.device, self.seed + 1_000_003 + chain_base + p))
+                        for p in range(best.shape[0])]
+                if outs:
+                    best = torch.cat([o[0] for o in outs])
+                    bc = torch.cat([o[1] for o in outs])
         b, c = _global_best(comm, bc, best)
         return OptResult(b, c, bc, best, stats=stats)
 
@@ -129,7 +142,7 @@ class SimulatedAnnealing:
         from ..data.table import shard_range
         d = self.domain
         W, r = comm.world, comm.rank
-        gen = _gen(d.device, self.seed + 1_000_003 * r)          # local search only
+        gen = None                                               # local search: per global chain (run)
         stats = {"better": 0, "worse_accepted": 0, "rejected": 0}
         best = bc = temp = None
         b0 = 0
@@ -169,7 +182,7 @@ class SimulatedAnnealing:
                                "chains": total}, force=True)
         if best is None:                                   # no moves at all
             best, bc = sol.clone(), cost.clone()
-        return best.long(), bc, self._global_stats(comm, stats), gen
+        return best.long(), bc, self._global_stats(comm, stats), gen, a
 
     @staticmethod
     def _global_stats(comm, stats: dict) -> dict:

@@ -17,16 +17,23 @@ import torch
 
 
 @contextlib.contextmanager
-def capturing(graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Stream | None" = None):
+def capturing(graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Stream | None" = None,
+              device: "torch.device | int | str | None" = None):
     """Capture the work issued inside the block into ``graph`` (on ``stream`` or a new side stream
-    ordered after the current one); the current stream waits for the side stream afterwards."""
-    s = stream if stream is not None else torch.cuda.Stream()
-    cur = torch.cuda.current_stream()
-    s.wait_stream(cur)
-    with torch.cuda.stream(s):
-        graph.capture_begin()
-        try:
-            yield graph
-        finally:
-            graph.capture_end()
-    cur.wait_stream(s)
+    ordered after the current one); the current stream waits for the side stream afterwards.
+    ``device``: the device of the captured work (default: ``stream``'s, else the current device) —
+    the side stream, the ordering and the capture all happen with that device current, so work on
+    a device other than the current one is captured rather than launched outside the graph."""
+    if device is None:
+        device = stream.device if stream is not None else torch.cuda.current_device()
+    with torch.cuda.device(device):
+        s = stream if stream is not None else torch.cuda.Stream(device=device)
+        cur = torch.cuda.current_stream(device)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            graph.capture_begin()
+            try:
+                yield graph
+            finally:
+                graph.capture_end()
+        cur.wait_stream(s)

@@ -229,7 +229,9 @@ def _optimisers(rank, world, seed):
     sa = SimulatedAnnealing(_domain(), n_chains=16, iters=200, t0=5.0, cooling=0.97, seed=seed, comm=comm).run()
     ga = GeneticAlgorithm(_domain(), islands=2, pool=12, mating=6, replacement=6, generations=15, seed=seed,
                           comm=comm).run()
-    return float(sa.best_cost), float(ga.best_cost)
+    sal = SimulatedAnnealing(_domain(), n_chains=16, iters=100, t0=5.0, cooling=0.97, seed=seed, comm=comm,
+                             locally_optimize=True, local_iters=20).run()
+    return float(sa.best_cost), float(ga.best_cost), float(sal.best_cost)
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -243,6 +245,10 @@ def test_optimiser_islands_equal_independent_runs(world):
                                       seed=5).run().best_cost)
     ga_ref = float(GeneticAlgorithm(_domain(), islands=2 * world, pool=12, mating=6, replacement=6, generations=15,
                                     seed=5).run().best_cost)
-    for sa_c, ga_c in got:
+    # local search after the walk: keyed by global chain too
+    sal_ref = float(SimulatedAnnealing(_domain(), n_chains=16 * world, iters=100, t0=5.0, cooling=0.97, seed=5,
+                                       locally_optimize=True, local_iters=20).run().best_cost)
+    for sa_c, ga_c, sal_c in got:
         assert sa_c == pytest.approx(sa_ref, rel=1e-6)
         assert ga_c == pytest.approx(ga_ref, rel=1e-6)
+        assert sal_c == pytest.approx(sal_ref, rel=1e-6)
