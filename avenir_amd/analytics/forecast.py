@@ -4,9 +4,21 @@ Reference: ``ProphetForcaster`` (P/unsupv/profo.py:35-286) wraps fbprophet (piec
 with changepoints, Fourier seasonalities, holiday effects; train / validate / save / forecast).
 fbprophet is not available, so this is a compact re-implementation of the same additive model
 solved as ONE regularised least-squares problem on the device (MAP estimate with a Laplace-like
-L1 prior on changepoint deltas approximated by ridge, no MCMC / uncertainty sampling):
+L1 prior on changepoint deltas approximated by ridge):
 
     y(t) = k t + m + sum_j delta_j (t - s_j)_+ + sum_seasons Fourier(t) + sum_h beta_h 1[t in h]
+
+Uncertainty intervals (``train.uncertainty.samples``, ``train.interval.width``,
+``train.mcmc.samples`` of P/unsupv/profo.py:58-60), drawn as fbprophet does, all samples as one
+device batch:
+* future trend: every future time point is a new changepoint with the history's changepoint rate,
+  its rate change ~ Laplace(0, mean |delta_j|) (fbprophet's ``sample_predictive_trend``);
+* observation noise ~ N(0, sigma) (the residual scale);
+* with ``mcmc_samples`` > 0 also parameter uncertainty: the coefficients are drawn from the EXACT
+  Gaussian posterior of this linear-Gaussian model, N(beta_MAP, (X'X / s^2 + Lambda)^-1), which is
+  what an MCMC chain over it converges to (fbprophet runs Stan's NUTS because its Laplace
+  changepoint prior is not conjugate; the ridge prior here is).
+``yhat_lower`` / ``yhat_upper`` are the sample quantiles at (1 -/+ width) / 2.
 
 Forecast parity with fbprophet is unpinned.  Save/load use the framework container format.
 """
@@ -23,13 +35,17 @@ DAY = 86400.0
 class AdditiveForecaster:
     def __init__(self, n_changepoints: int = 25, changepoint_range: float = 0.8, changepoint_prior: float = 0.05,
                  yearly: int = 10, weekly: int = 3, daily: int = 0, seasonality_prior: float = 10.0,
-                 holidays: dict[str, Sequence[float]] | None = None, holiday_window_s: float = DAY, device="cpu"):
+                 holidays: dict[str, Sequence[float]] | None = None, holiday_window_s: float = DAY, device="cpu",
+                 interval_width: float = 0.8, uncertainty_samples: int = 1000, mcmc_samples: int = 0, seed: int = 0):
         self.ncp, self.cpr, self.cp_prior = n_changepoints, changepoint_range, changepoint_prior
         self.seas = [(365.25 * DAY, yearly), (7 * DAY, weekly), (DAY, daily)]
         self.s_prior = seasonality_prior
         self.holidays = {k: list(v) for k, v in (holidays or {}).items()}
         self.hw = holiday_window_s
         self.device = torch.device(device)
+        self.interval_width, self.unc_samples, self.mcmc = float(interval_width), int(uncertainty_samples), int(mcmc_samples)
+        self.seed = int(seed)
+        self.cov = None
 
     def _design(self, t: torch.Tensor) -> torch.Tensor:
         ts = (t - self.t0) / self.scale_t                       # scaled time in [0, 1] over training
@@ -63,10 +79,18 @@ class AdditiveForecaster:
         XtX, Xty = X.T @ X, X.T @ ys
         b0 = torch.linalg.solve(XtX + 1e-6 * torch.diag(reg) + eye, Xty)
         s2 = float(((ys - X @ b0) ** 2).mean()) + 1e-12
-        self.beta = torch.linalg.solve(XtX / s2 + torch.diag(reg) + eye, Xty / s2)
+        prec = XtX / s2 + torch.diag(reg) + eye
+        self.beta = torch.linalg.solve(prec, Xty / s2)
+        self.cov = torch.linalg.inv(prec)                     # exact posterior covariance (scaled units)
+        self.cov = 0.5 * (self.cov + self.cov.T)
         resid = ys - X @ self.beta
         self.sigma = float(resid.std()) * self.y_scale
+        self.n_hist = int(t.numel())
+        self.t_hist = t
         return self
+
+    def history_times(self) -> torch.Tensor:
+        return self.t_hist if getattr(self, "t_hist", None) is not None else torch.empty(0, dtype=torch.float64)
 
     def predict(self, t) -> dict[str, torch.Tensor]:
         t = torch.as_tensor(t, dtype=torch.float64, device=self.device)
@@ -74,8 +98,40 @@ class AdditiveForecaster:
         yhat = (X @ self.beta) * self.y_scale
         nt = 2 + len(self.cps)
         trend = (X[:, :nt] @ self.beta[:nt]) * self.y_scale
-        return {"yhat": yhat, "trend": trend, "seasonal": yhat - trend,
-                "yhat_lower": yhat - 1.96 * self.sigma, "yhat_upper": yhat + 1.96 * self.sigma}
+        lo, hi = self._intervals(t, X, yhat)
+        return {"yhat": yhat, "trend": trend, "seasonal": yhat - trend, "yhat_lower": lo, "yhat_upper": hi}
+
+    def _intervals(self, t: torch.Tensor, X: torch.Tensor, yhat: torch.Tensor):
+        S = self.unc_samples
+        if S <= 0 or t.numel() == 0:
+            return yhat.clone(), yhat.clone()
+        g = torch.Generator(device=self.device).manual_seed(self.seed)
+        f64 = dict(dtype=torch.float64, device=self.device)
+        if self.mcmc > 0 and self.cov is not None:            # parameter draws from the posterior
+            L = torch.linalg.cholesky(self.cov + 1e-12 * torch.eye(self.cov.shape[0], **f64))
+            B = self.beta.view(1, -1) + torch.randn((S, self.beta.numel()), generator=g, **f64) @ L.T
+            ys = (B @ X.T) * self.y_scale                                        # [S, T]
+        else:
+            ys = yhat.view(1, -1).expand(S, -1).clone()
+        # future trend changepoints (scaled time > 1): rate p per future point, Laplace deltas
+        ts = (t - self.t0) / self.scale_t
+        fut = ts > 1.0
+        if bool(fut.any()) and self.cps:
+            deltas = self.beta[2:2 + len(self.cps)]
+            lam = float(deltas.abs().mean()) + 1e-8
+            p = len(self.cps) / max(1, getattr(self, "n_hist", len(self.cps) * 10))
+            tf = ts[fut]
+            z = (torch.rand((S, tf.numel()), generator=g, **f64) < p).double()
+            u = torch.rand((S, tf.numel()), generator=g, **f64) - 0.5
+            lap = -lam * torch.sign(u) * torch.log1p(-2 * u.abs())                # Laplace(0, lam)
+            zd = z * lap
+            add = tf.view(1, -1) * zd.cumsum(1) - (zd * tf.view(1, -1)).cumsum(1)  # sum_j d_j (t - s_j)
+            ys[:, fut] = ys[:, fut] + add * self.y_scale
+        ys = ys + self.sigma * torch.randn(ys.shape, generator=g, **f64)
+        w = self.interval_width
+        q = torch.tensor([(1 - w) / 2, (1 + w) / 2], **f64)
+        qs = torch.quantile(ys, q, dim=0)
+        return qs[0], qs[1]
 
     def future_times(self, periods: int, freq_s: float = DAY, last: float | None = None) -> torch.Tensor:
         start = last if last is not None else self.t0 + self.scale_t
@@ -90,9 +146,11 @@ class AdditiveForecaster:
 
     def save(self, path):
         from ..utils import checkpoint as C
-        C.save(path, {"beta": self.beta}, {"t0": self.t0, "scale_t": self.scale_t, "y_scale": self.y_scale,
-                                           "cps": self.cps, "sigma": self.sigma, "seas": self.seas,
-                                           "holidays": self.holidays, "hw": self.hw})
+        C.save(path, {"beta": self.beta, "cov": self.cov, "t_hist": self.t_hist},
+               {"t0": self.t0, "scale_t": self.scale_t, "y_scale": self.y_scale, "cps": self.cps, "sigma": self.sigma,
+                "seas": self.seas, "holidays": self.holidays, "hw": self.hw, "n_hist": self.n_hist,
+                "interval_width": self.interval_width, "unc_samples": self.unc_samples, "mcmc": self.mcmc,
+                "seed": self.seed})
 
     @classmethod
     def load(cls, path, device="cpu"):
@@ -103,4 +161,9 @@ class AdditiveForecaster:
         f.t0, f.scale_t, f.y_scale, f.cps, f.sigma = m["t0"], m["scale_t"], m["y_scale"], m["cps"], m["sigma"]
         f.seas = [tuple(s) for s in m["seas"]]
         f.holidays, f.hw = m["holidays"], m["hw"]
+        f.cov = t["cov"].double() if "cov" in t else None
+        f.t_hist = t["t_hist"].double() if "t_hist" in t else None
+        f.n_hist = int(m.get("n_hist", 0))
+        f.interval_width, f.unc_samples = float(m.get("interval_width", 0.8)), int(m.get("unc_samples", 1000))
+        f.mcmc, f.seed = int(m.get("mcmc", 0)), int(m.get("seed", 0))
         return f

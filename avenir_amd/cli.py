@@ -24,6 +24,7 @@ from .jobs import JOBS  # noqa: F401  (registers every job)
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="avenir_amd", description=__doc__.split("\n\n")[0])
     ap.add_argument("job", nargs="?", help="job name (see --list)")
+    ap.add_argument("rest", nargs="*", help="positional arguments of an app driver verb (e.g. ctrace simu 1000 y)")
     ap.add_argument("--list", action="store_true")
     ap.add_argument("--input", "-i")
     ap.add_argument("--output", "-o")
@@ -47,7 +48,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv: list[str] | None = None) -> int:
-    args = build_parser().parse_args(argv)
+    args = build_parser().parse_intermixed_args(argv)
     if args.list or not args.job:
         for n, (_, h) in sorted(JOBS.items()):
             print(f"{n:36s} {h}")

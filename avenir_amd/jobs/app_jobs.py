@@ -1,0 +1,1059 @@
+"""The reference's application drivers as CLI verbs: ``python -m avenir_amd <app> <op> <args...>``.
+
+Each reference driver is a script run as ``./<app>.py <op> <args>`` (or ``./<app>.py <props>
+[k=v ...]`` with the op in ``common.mode``); here each is one job whose positional arguments after
+the job name follow the script's.  Output goes to stdout (as the scripts print it) or to ``-o``.
+
+* ``ctrace simu <numIter> <y|n> | train <props> | pred <props>``      P/app/ctrace.py:153-178
+* ``priceRl train <numIter> [cpDir] | inctr <cp> <numIter> [cpDir] | tract <numIter> |
+  loact <cp> [state] | crstate``                                       P/app/price_rl.py:270-334
+* ``backOrder simu <numIter> | grmo | train <props> | pred <props> |
+  infer <props> <dataFile> <v1,v2,..>``                                P/app/back_order.py:223-252
+* ``rbm <props> [k=v ...]`` (common.mode train | reconstruct | missing) P/app/rbmd.py:19-118
+* ``tsgen <op> <props> [override]`` (rg rnp gen rw ar sine ccorr corr aol) P/app/tsgen.py:137-466
+* ``tsexp <op> <props>`` (desc diff trend acf pacf ccf adf kpss jarqBera shapWilk dagast andar
+  hist cov pcorr srcorr krcorr cscorr ancorr contab stt ks2s mawh wilcox krwa freid zhangc
+  zhanga zhangk)                                                        P/app/tsexp.py:238-499
+* ``zhtst zc <size> <numIter> | st <size> | di <size>``                 P/app/zhtst.py:107-159
+* ``forecast <props> [k=v ...]`` (common.mode train | forecast | validate | shuffle |
+  randomize)                                                            P/app/profod.py:27-56
+* ``classifier --mode explain --kind rf|gbt|svm -c clf.props <lime.props> <record>`` (LIME,
+  P/app/intrd.py:59-89) lives with the classifier job (jobs/core.py).
+
+The computations are the framework's device implementations (models/montecarlo, nn/*, apps/*,
+analytics/*); plots of the reference become printed numbers.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from .common import job
+
+
+# ---------------------------------------------------------------------------------------------
+# plumbing
+# ---------------------------------------------------------------------------------------------
+def _rest(args, n_min: int, usage: str) -> list[str]:
+    rest = list(getattr(args, "rest", None) or [])
+    if len(rest) < n_min:
+        raise SystemExit(f"usage: {usage}")
+    return rest
+
+
+class _Out:
+    """stdout, or the ``-o`` file (created / truncated on first write)."""
+
+    def __init__(self, args):
+        self.path = getattr(args, "output", None)
+        self._fh = None
+
+    def __call__(self, line: str = "") -> None:
+        if self.path is None:
+            print(line)
+            return
+        if self._fh is None:
+            Path(self.path).parent.mkdir(parents=True, exist_ok=True)
+            self._fh = open(self.path, "w")
+        self._fh.write(line + "\n")
+
+    def lines(self, lines) -> None:
+        if self.path is None:
+            sys.stdout.write("".join(l + "\n" for l in lines))
+        else:
+            for l in lines:
+                self(l)
+
+    def close(self):
+        if self._fh is not None:
+            self._fh.close()
+
+
+def _props(path: str, overrides: list[str] | None = None) -> dict[str, str]:
+    from ..utils.config import read_properties
+    conf = dict(read_properties(path))
+    for kv in overrides or []:
+        if "=" in kv:
+            k, v = kv.split("=", 1)
+            conf[k.strip()] = v.strip()
+    return conf
+
+
+def _get(conf: dict, key: str, default=None):
+    v = conf.get(key, "_")
+    if v is None or str(v).strip() in ("_", ""):
+        return default
+    if str(v).strip().lower() == "none":
+        return None
+    return str(v).strip()
+
+
+def _bool(conf, key, default=False) -> bool:
+    v = _get(conf, key)
+    return default if v is None else v.lower() == "true"
+
+
+def _dev(args):
+    from ..nn.common import pick_device
+    return pick_device(getattr(args, "device", None) or "auto")
+
+
+def _model_path(conf: dict, default_dir="model") -> str:
+    d = _get(conf, "common.model.directory", default_dir)
+    f = _get(conf, "common.model.file")
+    if f is None:
+        raise SystemExit("missing model file name (common.model.file)")
+    return os.path.join(d, f)
+
+
+def _resolve(conf_path: str, p: str | None) -> str | None:
+    """Data paths in a properties file are relative to the working directory (as the scripts run),
+    else to the properties file's directory."""
+    if p is None or os.path.isabs(p) or os.path.exists(p):
+        return p
+    q = os.path.join(os.path.dirname(os.path.abspath(conf_path)), p)
+    return q if os.path.exists(q) else p
+
+
+def _disc_weights(weights, g, n, device):
+    w = torch.tensor(weights, dtype=torch.float64, device=device)
+    return torch.multinomial(w / w.sum(), n, replacement=True, generator=g)
+
+
+# ---------------------------------------------------------------------------------------------
+# ctrace (P/app/ctrace.py)
+# ---------------------------------------------------------------------------------------------
+def contact_traces(n_people: int, seed: int = 0, device="cpu") -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """ctrace.py ``simu`` for ``n_people`` people at once (the reference calls ``contact`` once per
+    contact and evaluates every 5th): 5 contacts each, day ~ U[1, 15) floored, exposure 1..4 with
+    weights 60/24/8/2 (:160-161); sorted by day descending; mask on w.p. 0.7, flipped per contact
+    w.p. 0.1 (a running XOR), vulnerability w.p. 0.4, area 1..3 w.p. 60/30/10; a contact's exposure
+    is dropped w.p. 0.4; viral load = sum over exposed contacts of 6 s / (1 + s), s = e^{k (v0 + 15
+    - day)} with (v0, k) by exposure level and mask, + 0.8 / 2.0 in areas 2 / 3 (:56-99); infected
+    when the load exceeds 7.3 (+0.2 if not vulnerable), w.p. 0.9 within 3 of the threshold
+    (:101-111).  Returns (records [P, 5, 5] int: day, exposure, mask, vulnerable, area;
+    infection [P] int; load [P])."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    P = n_people
+    u = lambda *s: torch.rand(s, device=dev, generator=g, dtype=torch.float64)
+    day = (1 + 14 * u(P, 5)).floor().long()
+    expo = 1 + _disc_weights([60, 24, 8, 2], g, P * 5, dev).view(P, 5)
+    day, order = day.sort(dim=1, descending=True, stable=True)
+    expo = expo.gather(1, order)
+    mask0 = (u(P) >= 0.3).long()
+    vulnerable = (u(P) < 0.4).long()
+    area = 1 + _disc_weights([60, 30, 10], g, P, dev)
+    flips = (u(P, 5) < 0.1).long()
+    mask = (mask0.view(-1, 1) + flips.cumsum(1)) % 2
+    expo = torch.where(u(P, 5) < 0.4, torch.zeros_like(expo), expo)
+    v0 = torch.tensor([[0.0, 0.0], [-10.0, -12.0], [-8.0, -10.0], [-5.0, -7.5], [-3.0, -5.5]],
+                      dtype=torch.float64, device=dev)
+    kk = torch.tensor([0.0, 0.2, 0.4, 0.6, 0.9], dtype=torch.float64, device=dev)
+    vld = v0[expo, mask] + torch.where(area == 2, 0.8, torch.where(area == 3, 2.0, 0.0)).view(-1, 1).double()
+    s = torch.exp(kk[expo] * (vld + (15 - day).double()))
+    load = torch.where(expo > 0, 6 * s / (1 + s), torch.zeros_like(s)).sum(1)
+    thr = torch.where(vulnerable == 1, 7.3, 7.5).double()
+    inf = torch.where(load > thr, torch.where(load < thr + 3.0, (u(P) < 0.9).long(), torch.ones_like(vulnerable)),
+                      torch.zeros_like(vulnerable))
+    rec = torch.stack([day, expo, mask, vulnerable.view(-1, 1).expand(P, 5), area.view(-1, 1).expand(P, 5)], 2)
+    return rec, inf, load
+
+
+def _lstm_train(conf_path: str, conf: dict, dev, out: _Out):
+    from ..nn.sequence import LstmNetwork
+    net = LstmNetwork.from_config(conf, device=dev)
+    x, y = _lstm_data(net, conf_path, conf, "train.data.file")
+    net.fit(x, y)
+    out(f"training loss {net.losses[-1]:.6f} after {len(net.losses)} iterations" if net.losses else "no training data")
+    va = _resolve(conf_path, _get(conf, "valid.data.file"))
+    if va:
+        xv, yv = _lstm_data(net, conf_path, conf, "valid.data.file")
+        pred = net.predict(xv, "binary").cpu().view(-1)
+        out(_score_line(_get(conf, "valid.accuracy.metric", "acc"), yv.long().view(-1), pred))
+    if _bool(conf, "train.model.save"):
+        p = _model_path(conf)
+        Path(p).parent.mkdir(parents=True, exist_ok=True)
+        net.save(p)
+        out(f"model saved {p}")
+    return net
+
+
+def _score_line(metric: str, y: torch.Tensor, pred: torch.Tensor) -> str:
+    from ..utils.metrics import perf_metric
+    m = {"acc": "accuracy", "rec": "recall", "prec": "precision"}.get(metric, metric)
+    return f"perf score {float(perf_metric(m, y.cpu(), pred.cpu())):.3f}"
+
+
+def _lstm_data(net, conf_path, conf, key, with_target=True):
+    path = _resolve(conf_path, _get(conf, key))
+    if path is None:
+        raise SystemExit(f"missing {key}")
+    cols = [int(v) for v in _get(conf, "train.data.feat.cols", "0,0").split(",")]
+    tcol = int(_get(conf, "train.data.target.col", "-1")) if with_target else -1
+    delim = _get(conf, "train.data.delim", ",")
+    scale = _get(conf, "common.scaling.method", "zscale") if _get(conf, "common.preprocessing") == "scale" else None
+    return net.load_data(path, delim, cols[0], cols[1], tcol, scale)
+
+
+@job("ctrace", "contact-tracing app (P/app/ctrace.py): ctrace simu <numIter> <y|n> | train <props> | pred <props>")
+def ctrace(args):
+    rest = _rest(args, 1, "ctrace simu <numIter> <y|n> | train <props> | pred <props>")
+    op, out = rest[0], _Out(args)
+    if op == "simu":
+        n_iter = int(rest[1]) if len(rest) > 1 else 1000
+        target = (rest[2] if len(rest) > 2 else "y") == "y"
+        rec, inf, _ = contact_traces(n_iter // 5, seed=args.seed or 0, device=_dev(args))
+        rows = rec.view(rec.shape[0], -1).cpu().tolist()
+        iv = inf.cpu().tolist()
+        out.lines(",".join(map(str, r)) + (f",{i}" if target else "") for r, i in zip(rows, iv))
+    elif op in ("train", "pred"):
+        if len(rest) < 2:
+            raise SystemExit(f"usage: ctrace {op} <props>")
+        conf = _props(rest[1], rest[2:])
+        dev = _dev(args)
+        if op == "train":
+            _lstm_train(rest[1], conf, dev, out)
+        else:
+            from ..nn.sequence import LstmNetwork
+            net = LstmNetwork.from_config(conf, device=dev)
+            if _bool(conf, "predict.use.saved.model", True) and os.path.exists(_model_path(conf)):
+                net.restore(_model_path(conf))
+            else:
+                net = _lstm_train(rest[1], conf, dev, _Out(type("A", (), {"output": os.devnull})()))
+            x = _lstm_data(net, rest[1], conf, "predict.data.file", with_target=False)
+            kind = _get(conf, "predict.output", "binary")
+            pr = net.predict(x, "binary" if kind == "binary" else "raw").cpu()
+            path = _resolve(rest[1], _get(conf, "predict.data.file"))
+            recs = [l for l in Path(path).read_text().splitlines() if l.strip()]
+            if kind == "binary":
+                out.lines(f"{r}\t{int(p)}" for r, p in zip(recs, pr.view(-1).tolist()))
+            else:
+                out.lines(f"{r}\t" + ",".join(f"{v:.3f}" for v in p) for r, p in zip(recs, pr.view(len(recs), -1).tolist()))
+    else:
+        raise SystemExit("invalid command")
+    out.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# priceRl (P/app/price_rl.py)
+# ---------------------------------------------------------------------------------------------
+def _pricing_agent(dev, seed):
+    from ..nn.rl import DQNAgent, PricingEnv
+    env = PricingEnv(n_envs=64, device=dev, seed=seed)
+    # createConfig (:175-189): lr 0.002, gamma 0.8, train batch 256, hiddens [128, 128, 128]
+    return DQNAgent(env, lr=0.002, gamma=0.8, batch=256, hiddens=(128, 128, 128), buffer=10000, eps_end=0.01,
+                    seed=seed)
+
+
+def rand_pricing_state(p, g: np.random.Generator) -> list[int]:
+    """``randState`` (:254-265): a random past-price prefix of 5..T-1 steps, the time one-hot and a
+    cycle offset."""
+    grid = np.arange(p.price_min, p.price_max, p.price_step)
+    T = p.T
+    st = [0] * p.state_size
+    t = int(g.integers(5, T))
+    for i in range(t):
+        st[i] = int(grid[int(g.integers(0, len(grid)))])
+    st[T + t] = 1
+    st[-1] = int(g.integers(0, p.cyc_period + 1))
+    return st
+
+
+@job("priceRl", "DQN price optimisation app (P/app/price_rl.py): priceRl train <numIter> [cpDir] | "
+     "inctr <cp> <numIter> [cpDir] | tract <numIter> | loact <cp> [state] | crstate")
+def price_rl(args):
+    rest = _rest(args, 1, "priceRl train|inctr|tract|loact|crstate ...")
+    op, out = rest[0], _Out(args)
+    dev, seed = _dev(args), args.seed or 0
+    g = np.random.default_rng(seed)
+
+    def train(agent, n):
+        for i in range(n):
+            agent.train(iterations=1)
+            out(f"**** iteration {i}  mean episode reward {agent.episode_rewards[-1]:.1f}  "
+                f"epsilon {agent.epsilon():.3f}")
+
+    def save(agent, cp_dir):
+        if cp_dir:
+            if not os.path.isdir(cp_dir):
+                raise ValueError("provided checkpoint directory does not exist")
+            p = os.path.join(cp_dir, f"checkpoint-{agent.steps}")
+            agent.save(p)
+            out(f"checkpoint {p}")
+
+    def action(agent, state):
+        out("state:")
+        out(str(state))
+        a = agent.act(torch.tensor([state], dtype=torch.float32, device=agent.device), greedy=True)
+        out("action:")
+        out(str(int(a[0])))
+
+    if op == "train":
+        agent = _pricing_agent(dev, seed)
+        train(agent, int(rest[1]))
+        save(agent, rest[2] if len(rest) > 2 else None)
+    elif op == "inctr":
+        if not os.path.isfile(rest[1]):
+            raise ValueError("provided checkpoint file does not exist")
+        agent = _pricing_agent(dev, seed)
+        agent.restore(rest[1])
+        train(agent, int(rest[2]))
+        save(agent, rest[3] if len(rest) > 3 else None)
+    elif op == "tract":
+        agent = _pricing_agent(dev, seed)
+        train(agent, int(rest[1]))
+        action(agent, rand_pricing_state(agent.env.p, g))
+    elif op == "loact":
+        if not os.path.isfile(rest[1]):
+            raise ValueError("provided checkpoint file does not exist")
+        agent = _pricing_agent(dev, seed)
+        agent.restore(rest[1])
+        if len(rest) > 2:
+            state = [int(v) for v in rest[2].split(",")]
+            assert len(state) == agent.env.p.state_size, "invalid state size"
+        else:
+            out("creating random but valid state")
+            state = rand_pricing_state(agent.env.p, g)
+        action(agent, state)
+    elif op == "crstate":
+        from ..nn.rl import PricingParams
+        out(str(rand_pricing_state(PricingParams(), g)))
+    else:
+        raise ValueError("invalid command")
+    out.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# backOrder (P/app/back_order.py) and the tnn train / predict drivers
+# ---------------------------------------------------------------------------------------------
+BACK_ORDER_GRAPH = {
+    "nodes": ["dem", "prevDem", "partMarg", "prodDownTm", "partOrd", "boPartOrd", "prCap", "boPrCap", "bo", "profit"],
+    "edges": [("dem", "boPartOrd"), ("prevDem", "partOrd"), ("partMarg", "partOrd"), ("partOrd", "boPartOrd"),
+              ("prodDownTm", "prCap"), ("prCap", "boPrCap"), ("dem", "boPrCap"), ("boPartOrd", "bo"),
+              ("boPrCap", "bo")],
+}
+
+
+def _tnn(conf_path, conf, dev):
+    from ..nn.mlp import FeedForwardNetwork
+    net = FeedForwardNetwork.from_config(conf, device=dev)
+    return net
+
+
+def _tnn_data(net, conf_path, key, include_out=True):
+    path = _resolve(conf_path, _get(net.conf, key))
+    if path is None:
+        raise SystemExit(f"missing {key}")
+    return path, net.prep_data(path, include_out)
+
+
+def tnn_train(conf_path: str, conf: dict, dev, out: _Out):
+    """``FeedForwardNetwork.batchTrain`` (P/supv/tnn.py:356-421): mini-batch training, the
+    validation score, optional checkpoint."""
+    torch.manual_seed(9999)
+    net = _tnn(conf_path, conf, dev)
+    _, (x, y) = _tnn_data(net, conf_path, "train.data.file")
+    net.fit(x, y, track_interval=int(_get(conf, "train.batch.intv", "5")) if _bool(conf, "train.track.error") else 0)
+    if _get(conf, "valid.data.file"):
+        _, (xv, yv) = _tnn_data(net, conf_path, "valid.data.file")
+        out(f"perf score {net.evaluate_model(xv, yv):.3f}")
+    if _bool(conf, "train.model.save"):
+        p = _model_path(conf)
+        Path(p).parent.mkdir(parents=True, exist_ok=True)
+        net.save(p)
+        out("model saved")
+    return net
+
+
+def _tnn_model(conf_path, conf, dev):
+    net = _tnn(conf_path, conf, dev)
+    if _bool(conf, "predict.use.saved.model", True) and os.path.exists(_model_path(conf)):
+        net.restore(_model_path(conf))
+        return net
+    return tnn_train(conf_path, conf, dev, _Out(type("A", (), {"output": os.devnull})()))
+
+
+def tnn_predict(conf_path: str, conf: dict, dev, out: _Out):
+    """``FeedForwardNetwork.predict`` + ``printPrediction`` (:425-449, :305-320): each input record
+    padded to ``predict.feat.pad.size`` followed by its prediction."""
+    net = _tnn_model(conf_path, conf, dev)
+    path, x = _tnn_data(net, conf_path, "predict.data.file", include_out=False)
+    kind = _get(conf, "predict.output", "binary")
+    pr = net.predict(x, "binary" if kind == "binary" and net.loss_name != "mse" else "raw").cpu()
+    pad = int(_get(conf, "predict.feat.pad.size", "60"))
+    recs = [l for l in Path(path).read_text().splitlines() if l.strip()]
+    vals = pr.view(len(recs), -1).tolist()
+    out.lines(r.ljust(pad) + "\t" + ",".join(f"{v:.3f}" if isinstance(v, float) else str(v) for v in p)
+              for r, p in zip(recs, vals))
+
+
+@job("backOrder", "manufacturing back-order app (P/app/back_order.py): backOrder simu <numIter> | grmo | "
+     "train <props> | pred <props> | infer <props> <dataFile> <v1,v2,..>")
+def back_order(args):
+    rest = _rest(args, 1, "backOrder simu|grmo|train|pred|infer ...")
+    op, out, dev = rest[0], _Out(args), _dev(args)
+    if op == "simu":
+        from ..apps.supply import SupplyChainSimulation
+        sim = SupplyChainSimulation(device=str(dev), seed=args.seed or 0).simulate(int(rest[1]))
+        out.lines(SupplyChainSimulation.lines(sim.cpu()))
+    elif op == "grmo":
+        out("nodes: " + ",".join(BACK_ORDER_GRAPH["nodes"]))
+        for a, b in BACK_ORDER_GRAPH["edges"]:
+            out(f"{a} -> {b}")
+    elif op == "train":
+        tnn_train(rest[1], _props(rest[1]), dev, out)
+    elif op == "pred":
+        tnn_predict(rest[1], _props(rest[1]), dev, out)
+    elif op == "infer":
+        from ..apps.supply import back_order_intervention
+        from ..nn.common import load_data_file
+        conf = _props(rest[1])
+        net = _tnn_model(rest[1], conf, dev)
+        fields = [int(v) for v in _get(conf, "train.data.fields").split(",")]
+        feats = [int(v) for v in _get(conf, "train.data.feature.fields").split(",")]
+        _, feat = load_data_file(rest[2], ",", fields, feats)
+        X = torch.tensor(np.asarray(feat, dtype=np.float64))
+        values = [int(v) for v in rest[3].split(",")]
+        scale = _get(conf, "common.scaling.method", "zscale") if _get(conf, "common.preprocessing") == "scale" else None
+        res = back_order_intervention(lambda Xi: net.predict(Xi.to(net.device))[:, 0].cpu(), X, 4, values, scale)
+        for v, p in res:
+            out(f"back order {int(v) if float(v).is_integer() else v}\tunit profit {p:.2f}")
+    else:
+        raise SystemExit("invalid command")
+    out.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# rbm (P/app/rbmd.py + P/unsupv/rbm.py)
+# ---------------------------------------------------------------------------------------------
+def _rbm_data(conf_path, conf, key_file, key_fields):
+    path = _resolve(conf_path, _get(conf, key_file))
+    fields = _get(conf, key_fields)
+    cols = [int(v) for v in fields.split(",")] if fields else None
+    return torch.tensor(np.loadtxt(path, delimiter=",", usecols=cols, ndmin=2), dtype=torch.float32)
+
+
+@job("rbm", "RBM app (P/app/rbmd.py): rbm <props> [k=v ...], common.mode = train | reconstruct | missing")
+def rbm(args):
+    from ..nn.unsupervised import RestrictedBoltzmannMachine as RBM
+    rest = _rest(args, 1, "rbm <props> [k=v ...]")
+    conf = _props(rest[0], rest[1:])
+    out, dev = _Out(args), _dev(args)
+    mode = _get(conf, "common.mode", "train")
+    out("running mode: " + mode)
+
+    def build(nv):
+        return RBM(nv, int(_get(conf, "train.num.components")), lr=float(_get(conf, "train.learning.rate", "0.1")),
+                   batch_size=int(_get(conf, "train.batch.size", "10")), num_iter=int(_get(conf, "train.num.iter", "10")),
+                   seed=int(_get(conf, "train.random.state", "0")), device=dev)
+
+    def train():
+        x = _rbm_data(rest[0], conf, "train.data.file", "train.data.fields")
+        m = build(x.shape[1]).fit(x.to(dev))
+        if _bool(conf, "train.model.save"):
+            p = _model_path(conf)
+            Path(p).parent.mkdir(parents=True, exist_ok=True)
+            m.save(p)
+            out("...saving model")
+        return m
+
+    def model():
+        if _bool(conf, "analyze.use.saved.model", True) and os.path.exists(_model_path(conf)):
+            out("...loading model")
+            x = _rbm_data(rest[0], conf, "analyze.data.file", "analyze.data.fields")
+            return build(x.shape[1]).restore(_model_path(conf))
+        return train()
+
+    if mode == "train":
+        train()
+    elif mode == "reconstruct":
+        m = model()
+        x = _rbm_data(rest[0], conf, "analyze.data.file", "analyze.data.fields").to(dev)
+        rec = m.gibbs(x).cpu().int().tolist()
+        out.lines("[" + " ".join(str(v) for v in r) + "]" for r in rec)
+    elif mode == "missing":
+        m = model()
+        x = _rbm_data(rest[0], conf, "analyze.data.file", "analyze.data.fields").to(dev)
+        b, e = int(_get(conf, "analyze.missing.beg.col")), int(_get(conf, "analyze.missing.end.col"))
+        pred = rbm_missing_by_sampling(m, x, b, e, int(_get(conf, "analyze.missing.initial.count", "10")),
+                                       int(_get(conf, "analyze.missing.iter.count", "100")),
+                                       _bool(conf, "analyze.missing.all.initial", True), seed=args.seed or 0)
+        out("predicted missing values")
+        for i, p in enumerate(pred):
+            out(f"sample  {i}  value  {p}")
+        if _bool(conf, "analyze.missing.validate"):
+            vp = _resolve(rest[0], _get(conf, "analyze.missing.validate.file.path"))
+            actual = [",".join(l.split(",")[b:e]) for l in Path(vp).read_text().splitlines() if l.strip()]
+            assert len(actual) == len(pred), "un equal size of predicted and validation"
+            acc = 100.0 * sum(p == a for p, a in zip(pred, actual)) / len(pred)
+            out(f"accuracy {acc:.3f}")
+    else:
+        raise SystemExit(f"invalid mode {mode}")
+    out.close()
+
+
+def rbm_missing_by_sampling(m, x: torch.Tensor, b: int, e: int, n_init: int, n_iter: int, all_initial: bool,
+                            seed: int = 0) -> list[str]:
+    """``missingValueBySampling`` (rbmd.py:26-88): for each initial value of the missing block (every
+    one-hot vector, or random ones), ``n_iter`` Gibbs reconstructions of every sample; the block's
+    most frequent reconstructed value per sample is the imputation.  The reconstructions of all
+    samples are one device batch per step; the block values are counted as integer codes."""
+    size = e - b
+    assert size > 0, "invalid missing columns"
+    if all_initial:
+        n_init = size if size > 1 else 2
+    g = torch.Generator(device=x.device).manual_seed(seed)
+    n = x.shape[0]
+    counts = torch.zeros((n, 1 << size), dtype=torch.long, device=x.device)
+    w = (2 ** torch.arange(size - 1, -1, -1, device=x.device)).long()
+    for inv in range(n_init):
+        d = x.clone()
+        if size > 1:
+            idx = torch.full((n,), inv, device=x.device) if all_initial else \
+                torch.randint(0, size, (n,), device=x.device, generator=g)
+            d[:, b:e] = torch.nn.functional.one_hot(idx.long(), size).float()
+        else:
+            d[:, b] = float(inv) if all_initial else torch.randint(0, 2, (n,), device=x.device, generator=g).float()
+        for _ in range(n_iter):
+            r = m.gibbs(d)
+            code = (r[:, b:e].round().long() * w).sum(1)
+            counts[torch.arange(n, device=x.device), code] += 1
+    best = counts.argmax(1).tolist()
+    return [",".join(str((c >> (size - 1 - j)) & 1) for j in range(size)) for c in best]
+
+
+# ---------------------------------------------------------------------------------------------
+# tsgen (P/app/tsgen.py)
+# ---------------------------------------------------------------------------------------------
+_UNIT_S = {"s": 1, "m": 60, "h": 3600, "d": 86400, "w": 7 * 86400}
+
+
+def _ts_window(conf, now: float | None = None) -> tuple[int, int]:
+    """(past, current) epoch seconds of ``window.size`` (e.g. ``3_d``), the start aligned down to
+    ``window.samp.align.unit`` (``pastTime`` / ``timeAlign`` of P/lib/util.py)."""
+    size, unit = _get(conf, "window.size").split("_")
+    cur = int(now if now is not None else _get(conf, "window.now", None) or __import__("time").time())
+    past = cur - int(size) * _UNIT_S[unit]
+    al = _get(conf, "window.samp.align.unit")
+    if al:
+        past -= past % _UNIT_S[al]
+    return past, cur
+
+
+def _ts_times(conf, g: torch.Generator) -> list[int]:
+    past, cur = _ts_window(conf)
+    kind = _get(conf, "window.samp.interval.type", "fixed")
+    params = _get(conf, "window.samp.interval.params").split(",")
+    if kind == "fixed":
+        step = int(params[0])
+        return list(range(past, cur, step))
+    mean, sd = float(params[0]), float(params[1])
+    out, t = [], past
+    while t < cur:
+        out.append(t)
+        t += max(1, int(mean + sd * float(torch.randn((), generator=g, dtype=torch.float64))))
+    return out
+
+
+def _fmt_time(t: int, fmt: str) -> str:
+    if fmt == "epoch":
+        return str(t)
+    import datetime as _dt
+    return _dt.datetime.fromtimestamp(t).strftime("%Y-%m-%d %H:%M:%S")
+
+
+def _fmt_val(v: float, conf) -> str:
+    if _get(conf, "output.value.type", "float") == "int":
+        return str(int(v))
+    return f"{v:.{int(_get(conf, 'output.value.precision', '3'))}f}"
+
+
+def ts_generate(op: str, conf: dict, seed: int = 0, device="cpu", conf_path: str = "") -> list[str]:
+    """The series of ``tsgen.py <op>`` as text lines ``time,value`` (or the extended records of
+    ``corr`` / ``ccorr``).  Values of a whole window are generated at once on ``device``; only AR
+    recurrences step through time (vectorised over nothing else: one series)."""
+    import datetime as _dt
+    dev = torch.device(device)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    gd = torch.Generator(device=dev).manual_seed(seed)
+    fmt = _get(conf, "output.time.format", "epoch")
+    randn = lambda n, m=0.0, s=1.0: m + s * torch.randn(n, generator=gd, device=dev, dtype=torch.float64)
+    if op in ("corr", "ccorr"):
+        path = _resolve(conf_path, _get(conf, f"{op}.file.path"))
+        col = int(_get(conf, f"{op}.file.col"))
+        recs = [l.split(",") for l in Path(path).read_text().splitlines() if l.strip()]
+        ref = torch.tensor([float(r[col]) for r in recs], dtype=torch.float64, device=dev)
+        if op == "corr":
+            scale, sd = float(_get(conf, "corr.scale", "1.0")), float(_get(conf, "corr.noise.stddev", "0.1"))
+            lag = int(_get(conf, "corr.lag", "0"))
+            vals = (ref * scale + randn(ref.numel(), 0.0, sd)).tolist()
+            out = []
+            for i, r in enumerate(recs):
+                if i >= lag:
+                    r = list(r)
+                    r[col] = f"{vals[i]:.3f}"
+                    out.append(",".join(r))
+            return out
+        rp = [float(v) for v in _get(conf, "ts.random.params", "0,0").split(",")]
+        cors = [float(v) for v in (_get(conf, "ccorr.co.params") or "").split(",") if v]
+        unco = [float(v) for v in (_get(conf, "ccorr.unco.params") or "").split(",") if v]
+        cols = [c * ref + randn(ref.numel(), rp[0], rp[1]) for c in cors]
+        if unco:
+            t = torch.tensor([float(r[0]) for r in recs], dtype=torch.float64, device=dev)
+            cols.append(_sines(unco, t, g) + randn(ref.numel(), rp[0], rp[1]))
+        vals = [c.tolist() for c in cols]
+        return [",".join(r + [_fmt_val(v[i], conf) for v in vals]) for i, r in enumerate(recs)]
+    times = _ts_times(conf, g)
+    n = len(times)
+    t = torch.tensor(times, dtype=torch.float64, device=dev)
+    if op == "rg":
+        m, s = (float(v) for v in _get(conf, "gr.distr").split(","))
+        vals = randn(n, m, s)
+    elif op == "rnp":
+        d = [float(v) for v in _get(conf, "npr.distr").split(",")]
+        lo, bw, w = d[0], d[1], d[2:]
+        k = _disc_weights(w, gd, n, dev)
+        vals = lo + (k.double() + torch.rand(n, generator=gd, device=dev, dtype=torch.float64)) * bw
+    elif op == "gen":
+        base = _get(conf, "ts.base", "mean")
+        bp = _get(conf, "ts.base.params").split(",")
+        rnd = _bool(conf, "ts.random", True)
+        rp = [float(v) for v in (_get(conf, "ts.random.params") or "0,0").split(",")]
+        noise = randn(n, rp[0], rp[1]) if rnd and rp[1] else torch.zeros(n, dtype=torch.float64, device=dev)
+        if base == "mean":
+            vals = float(bp[0]) + noise
+        else:
+            vals = _ar([float(v) for v in _get(conf, "ar.params").split(",")], noise)
+        cnt = torch.arange(n, dtype=torch.float64, device=dev)
+        tr, tp = _get(conf, "ts.trend", "nothing"), [float(v) for v in (_get(conf, "ts.trend.params") or "0").split(",")]
+        if tr == "linear":
+            vals = vals + cnt * tp[0]
+        elif tr == "quadratic":
+            vals = vals + tp[0] * cnt + tp[1] * cnt * cnt
+        elif tr == "logistic":
+            ex = torch.exp(-tp[0] * cnt)
+            vals = vals + tp[0] * (1 - ex) / (1 + ex)
+        cycles = [c for c in (_get(conf, "ts.cycles") or "").split(",") if c and c != "nothing"]
+        if cycles:
+            dts = [_dt.datetime.fromtimestamp(x) for x in times]
+            for c in cycles:
+                cv = torch.tensor([float(v) for v in _get(conf, f"ts.cycle.{c}.params").split(",")],
+                                  dtype=torch.float64, device=dev)
+                idx = {"year": [d.month - 1 for d in dts], "week": [d.weekday() for d in dts],
+                       "day": [d.hour for d in dts]}[c]
+                vals = vals + cv[torch.tensor(idx, device=dev)]
+    elif op == "rw":
+        init, rg = float(_get(conf, "rw.init.value", "5.0")), float(_get(conf, "rw.range", "1.0"))
+        steps = (torch.rand(n, generator=gd, device=dev, dtype=torch.float64) * 2 - 1) * rg
+        vals = init + torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), steps[:-1].cumsum(0)])
+    elif op == "ar":
+        rp = [float(v) for v in _get(conf, "ts.random.params").split(",")]
+        skip = 6
+        vals = _ar([float(v) for v in _get(conf, "ar.params").split(",")], randn(n + skip, rp[0], rp[1]))[skip:]
+        times = times[:vals.numel()]
+        vals = vals[: len(times)]
+    elif op == "sine":
+        rp = [float(v) for v in _get(conf, "ts.random.params").split(",")]
+        vals = _sines([float(v) for v in _get(conf, "si.params").split(",")], t, g) + randn(n, rp[0], rp[1])
+    elif op == "aol":
+        return []                                  # a no-op in the reference too (tsgen.py:464-465)
+    else:
+        raise ValueError("ivalid time series type")
+    return [f"{_fmt_time(tm, fmt)},{_fmt_val(v, conf)}" for tm, v in zip(times, vals.tolist())]
+
+
+def _ar(params: list[float], noise: torch.Tensor) -> torch.Tensor:
+    """x_t = c + sum_i a_i x_{t-i} + e_t with the reference's history order (arValue)."""
+    c, a = params[0], params[1:]
+    x = torch.zeros(noise.numel(), dtype=torch.float64, device=noise.device)
+    hist = [0.0] * len(a)
+    e = noise.tolist()
+    out = []
+    for i in range(noise.numel()):
+        v = c + sum(ai * hi for ai, hi in zip(a, hist)) + e[i]
+        hist = [v] + hist[:-1] if hist else hist
+        out.append(v)
+    x[:] = torch.tensor(out, dtype=torch.float64)
+    return x
+
+
+def _sines(params: list[float], t: torch.Tensor, g: torch.Generator) -> torch.Tensor:
+    """sinComponents + addSines: (amplitude, period) pairs with a random phase each."""
+    v = torch.zeros_like(t)
+    for i in range(0, len(params), 2):
+        amp, per = params[i], params[i + 1]
+        ph = float(torch.rand((), generator=g, dtype=torch.float64)) * 2 * math.pi
+        v = v + amp * torch.sin(ph + 2 * math.pi * torch.remainder(t, per) / per)
+    return v
+
+
+@job("tsgen", "time-series generator app (P/app/tsgen.py): tsgen <rg|rnp|gen|rw|ar|sine|ccorr|corr|aol> <props> [override]")
+def tsgen(args):
+    rest = _rest(args, 2, "tsgen <op> <props> [override props]")
+    conf = _props(rest[1])
+    if len(rest) > 2:
+        conf.update(_props(rest[2]))
+    out = _Out(args)
+    out.lines(ts_generate(rest[0], conf, seed=args.seed or 0, device=str(_dev(args)), conf_path=rest[1]))
+    out.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# tsexp (P/app/tsexp.py)
+# ---------------------------------------------------------------------------------------------
+def _ts_column(conf_path, conf, extra=False) -> list[float]:
+    sfx = ".extra" if extra else ""
+    path = _resolve(conf_path, _get(conf, "data.filePath" + sfx))
+    col = int(_get(conf, "data.col.index" + sfx))
+    vals = [float(l.split(",")[col]) for l in Path(path).read_text().splitlines() if l.strip()]
+    rr = _get(conf, "data.row.range" + sfx, "all")
+    if rr != "all":
+        a, b = (int(v) for v in rr.split(","))
+        vals = vals[a:b]
+    return vals
+
+
+def _stat_lines(stat, pvalue, null_msg, alt_msg) -> list[str]:
+    """``printStat`` (tsexp.py:228-234)."""
+    return [f"stat:   {stat:.3f}", f"pvalue: {pvalue:.3f}", null_msg if pvalue > 0.05 else alt_msg]
+
+
+def ts_explore(op: str, conf_path: str, conf: dict, device="cpu") -> list[str]:
+    """``tsexp.py <op>`` through :class:`~avenir_amd.analytics.explorer.DataExplorer` (device
+    statistics); the plots become printed values."""
+    from ..analytics.explorer import DataExplorer
+    ex = DataExplorer(device=device)
+    if op == "desc":                       # pandas head / describe of the numeric columns
+        path = _resolve(conf_path, _get(conf, "data.filePath"))
+        recs = [l.split(",") for l in Path(path).read_text().splitlines() if l.strip()]
+        out = ["head"] + [",".join(r) for r in recs[:5]]
+        out.append("col,count,mean,std,min,25%,50%,75%,max")
+        for j in range(len(recs[0]) if recs else 0):
+            try:
+                c = torch.tensor([float(r[j]) for r in recs], dtype=torch.float64)
+            except ValueError:
+                out.append(f"{j},{len(recs)},categorical,{len(set(r[j] for r in recs))} distinct")
+                continue
+            q = torch.quantile(c, torch.tensor([0.25, 0.5, 0.75], dtype=torch.float64)).tolist()
+            out.append(f"{j},{c.numel()},{float(c.mean()):.6f},{float(c.std()):.6f},{float(c.min()):g},"
+                       + ",".join(f"{v:g}" for v in q) + f",{float(c.max()):g}")
+        return out
+    if op == "cov":
+        pcs = [pc.split(":") for pc in _get(conf, "cov.file.paths").split(",")]
+        for i, (p, c) in enumerate(pcs):
+            vals = [float(l.split(",")[int(c)]) for l in Path(_resolve(conf_path, p)).read_text().splitlines() if l.strip()]
+            ex.addListNumericData(vals, f"s{i}")
+        cov = ex.getCovar(*[f"s{i}" for i in range(len(pcs))])
+        return ["co variance matrix"] + [" ".join(f"{v:.6f}" for v in r) for r in np.atleast_2d(cov).tolist()]
+    if op in ("cscorr", "contab", "ancorr"):
+        p1 = _resolve(conf_path, _get(conf, "data.filePath"))
+        p2 = _resolve(conf_path, _get(conf, "data.filePath.extra") or _get(conf, "data.filePath"))
+        c1, c2 = int(_get(conf, "data.col.index")), int(_get(conf, "data.col.index.extra"))
+        a = [l.split(",")[c1] for l in Path(p1).read_text().splitlines() if l.strip()]
+        b = [l.split(",")[c2] for l in Path(p2).read_text().splitlines() if l.strip()]
+        if op == "ancorr":
+            gb = int(_get(conf, "ancorr.grby.col"))
+            num, cat = (b, a) if gb == 0 else (a, b)
+            ex.addListNumericData([float(v) for v in num], "x")
+            ex.addCatListData(cat, "g")
+            r = ex.getAnovaCorr("x", "g")
+            return _stat_lines(r["stat"], r["pvalue"], "probably uncorrelated", "probably correlated")
+        ex.addCatListData(a, "a")
+        ex.addCatListData(b, "b")
+        if op == "contab":
+            t = ex.getConTab("a", "b")["table"]
+            return [" ".join(str(int(v)) for v in r) for r in np.atleast_2d(t).tolist()]
+        r = ex.getChiSqCorr("a", "b")
+        return _stat_lines(r["stat"], r["pvalue"], "probably uncorrelated", "probably correlated") + \
+            [f"dof {r.get('dof')}"]
+    data = _ts_column(conf_path, conf)
+    ex.addListNumericData(data, "d")
+    two = {"pcorr": ("getPearsonCorr", "probably uncorrelated", "probably correlated"),
+           "srcorr": ("getSpearmanRankCorr", "probably uncorrelated", "probably correlated"),
+           "krcorr": ("getKendalRankCorr", "probably uncorrelated", "probably correlated"),
+           "stt": ("testTwoSampleStudent", "probably same distribution", "probably same distribution"),
+           "ks2s": ("testTwoSampleKs", "probably same distribution", "probably same distribution"),
+           "mawh": ("testTwoSampleMw", "probably same distribution", "probably same distribution"),
+           "wilcox": ("testTwoSampleWilcox", "probably same distribution", "probably same distribution"),
+           "krwa": ("testTwoSampleKw", "probably same distribution", "probably same distribution")}
+    if op in two or op in ("ccf", "freid", "zhangc", "zhanga", "zhangk"):
+        ex.addListNumericData(_ts_column(conf_path, conf, extra=True), "e")
+    if op in two:
+        fn, m0, m1 = two[op]
+        r = getattr(ex, fn)("d", "e")
+        return _stat_lines(r["stat"], r["pvalue"], m0, m1)
+    if op == "freid":
+        ex.addListNumericData(_ts_column(conf_path, conf, extra=True), "e2")
+        r = ex.testTwoSampleFriedman("d", "e", "e2")
+        return _stat_lines(r["stat"], r["pvalue"], "probably same distribution", "probably same distribution")
+    if op in ("zhangc", "zhanga", "zhangk"):
+        r = getattr(ex, {"zhangc": "testTwoSampleZc", "zhanga": "testTwoSampleZa", "zhangk": "testTwoSampleZk"}[op])("d", "e")
+        name = {"zhangc": "ZhangC", "zhanga": "ZhangA", "zhangk": "ZhangK"}[op]
+        return [f"two sample {name} stat {float(r['stat']):.3f}"]
+    if op == "draw":
+        return [f"{v:g}" for v in data]
+    if op == "diff":
+        x = torch.tensor(data, dtype=torch.float64)
+        for _ in range(int(_get(conf, "diff.order", "1"))):
+            x = x[1:] - x[:-1]
+        return [f"{v:.6f}" for v in x.tolist()]
+    if op == "trend":
+        r = ex.getTrend("d")
+        out = [f"R square {float(r['r square error']):.6f}",
+               f"intercept  {float(r['intercept']):.6f} coeffficient {float(r['coeff'][0]):.6f} "]
+        if _bool(conf, "trend.remove"):
+            out += ["detrended"] + [f"{v:.6f}" for v in ex.deTrend("d", r["trend"]).tolist()]
+        return out
+    if op in ("acf", "pacf"):
+        if op == "acf" and _bool(conf, "acf.diff"):
+            ex.addListNumericData(np.diff(np.asarray(data)).tolist(), "d")
+        lags = int(_get(conf, f"{op}.lags", "40"))
+        r = ex.getAutoCorr("d", lags) if op == "acf" else ex.getParAutoCorr("d", lags)
+        vals = r["autoCorr"] if op == "acf" else r["partAutoCorr"]
+        return [f"{i},{float(v):.6f}" for i, v in enumerate(vals)]
+    if op == "ccf":
+        r = ex.getCrossCorr("d", "e", int(_get(conf, "ccf.maxlags", "10")))
+        vals = r["crossCorr"]
+        return [f"{i},{float(v):.6f}" for i, v in enumerate(vals)]
+    if op in ("adf", "kpss"):
+        # statistic + decision at the 5 % critical value (no p-value: statsmodels' response
+        # surfaces are not available; parity unpinned)
+        if op == "adf":
+            r = ex.testStationaryAdf("d", _get(conf, "adf.regression", "c"))
+        else:
+            r = ex.testStationaryKpss("d", _get(conf, "kpss.regression", "c"))
+        out = [f"stat:   {r['stat']:.3f}", "probably stationary" if r["stationary"] else "probably not stationary",
+               "critial values:"]
+        return out + [f"   {k} : {v}" for k, v in r["critical values"].items()]
+    if op in ("jarqBera", "shapWilk", "dagast"):
+        r = getattr(ex, {"jarqBera": "testNormalJarqBera", "shapWilk": "testNormalShapWilk",
+                         "dagast": "testNormalDagast"}[op])("d")
+        return _stat_lines(r["stat"], r["pvalue"], "probably gaussian", "probably not gaussian")
+    if op == "andar":
+        r = ex.testDistrAnderson("d")
+        sl = r["significance levels"]
+        out = [f"stat {r['stat']:.3f}"]
+        for s, cv in zip(sl, r["critical values"]):
+            if int(s) == 5:
+                out.append(("probably gaussian" if r["stat"] < cv else "probably not gaussian") + f" at the {s:.1f} level")
+        return out
+    if op == "hist":
+        x = torch.tensor(data, dtype=torch.float64)
+        h = torch.histc(x, bins=10, min=float(x.min()), max=float(x.max()))
+        if _bool(conf, "hist.cumulative"):
+            h = h.cumsum(0)
+        edges = torch.linspace(float(x.min()), float(x.max()), 11).tolist()
+        return [f"{edges[i]:.3f},{edges[i + 1]:.3f},{h[i]:g}" for i in range(10)]
+    raise ValueError("unknown command")
+
+
+@job("tsexp", "time-series exploration app (P/app/tsexp.py): tsexp <op> <props>")
+def tsexp(args):
+    rest = _rest(args, 2, "tsexp <op> <props>")
+    conf = _props(rest[1])
+    out = _Out(args)
+    out.lines(ts_explore(rest[0], rest[1], conf, device=str(_dev(args))))
+    out.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# zhtst (P/app/zhtst.py)
+# ---------------------------------------------------------------------------------------------
+def zc_stat(ranks: torch.Tensor, l1: int, l2: int) -> torch.Tensor:
+    """Zhang's Zc two-sample statistic from the pooled ranks of the sorted samples (zcStat,
+    zhtst.py:37-53), for a batch of rank vectors [B, l1 + l2] at once."""
+    ranks = torch.as_tensor(ranks, dtype=torch.float64)
+    r = ranks.view(-1, l1 + l2)
+    l = l1 + l2
+    i1 = torch.arange(1, l1 + 1, dtype=torch.float64, device=r.device)
+    i2 = torch.arange(1, l2 + 1, dtype=torch.float64, device=r.device)
+    s1 = (torch.log(l1 / (i1 - 0.5) - 1.0) * torch.log(l / (r[:, :l1] - 0.5) - 1.0)).sum(1)
+    s2 = (torch.log(l2 / (i2 - 0.5) - 1.0) * torch.log(l / (r[:, l1:] - 0.5) - 1.0)).sum(1)
+    return (s1 + s2) / l
+
+
+def zh_rank_samples(B: int, m1, s1, m2, s2, half: int, noise: int, g: torch.Generator, device="cpu") -> torch.Tensor:
+    """``RankSampler.createSample`` for B draws at once: two gaussian samples of ``half`` values,
+    ``noise`` random swaps between them, each sorted, pooled ranks (1-based, count of smaller)."""
+    dev = torch.device(device)
+    m1, s1, m2, s2 = (torch.as_tensor(v, dtype=torch.float64, device=dev).view(-1, 1) for v in (m1, s1, m2, s2))
+    v1 = m1 + s1 * torch.randn((B, half), generator=g, device=dev, dtype=torch.float64)
+    v2 = m2 + s2 * torch.randn((B, half), generator=g, device=dev, dtype=torch.float64)
+    rows = torch.arange(B, device=dev)
+    for _ in range(noise):
+        i = torch.randint(0, half, (B,), generator=g, device=dev)
+        j = torch.randint(0, half, (B,), generator=g, device=dev)
+        a, b = v1[rows, i].clone(), v2[rows, j].clone()
+        v1[rows, i], v2[rows, j] = b, a
+    v1, v2 = v1.sort(1).values, v2.sort(1).values
+    pooled = torch.cat([v1, v2], 1)
+    srt = pooled.sort(1).values
+    ranks = torch.searchsorted(srt.contiguous(), pooled.contiguous(), right=False) + 1
+    return ranks
+
+
+@job("zhtst", "Zhang two-sample statistic app (P/app/zhtst.py): zhtst zc <size> <numIter> | st <size> | di <size>")
+def zhtst(args):
+    rest = _rest(args, 2, "zhtst zc|st|di <sampSize> [numIter]")
+    op, size = rest[0], int(rest[1])
+    half = size // 2
+    out, dev = _Out(args), _dev(args)
+    g = torch.Generator(device=dev).manual_seed(args.seed or 0)
+    if op == "zc":
+        n_iter = int(rest[2]) if len(rest) > 2 else 1000
+        data = zh_rank_samples(1, 5.0, 0.5, 10.0, 1.0, half, 2, g, dev)
+        stat = float(zc_stat(data, half, half)[0])
+        out(f"diff distr stat {stat:.5f}")
+        # the Monte Carlo null: random (m, s) pairs from U[5, 10] x U[0.5, 1] per sample
+        u = lambda: 5.0 + 5.0 * torch.rand(n_iter, generator=g, device=dev, dtype=torch.float64)
+        v = lambda: 0.5 + 0.5 * torch.rand(n_iter, generator=g, device=dev, dtype=torch.float64)
+        sims = zc_stat(zh_rank_samples(n_iter, u(), v(), u(), v(), half, 2, g, dev), half, half).sort().values.cpu()
+        n = sims.numel()
+        out("lower critical values")
+        for p in (1.0, 2.5, 5.0, 10.0):
+            out(f"{p / 100:.5f}  {float(sims[min(n - 1, int(p / 100 * n))]):.5f}")
+        out("upper critical values")
+        for p in (1.0, 2.5, 5.0, 10.0):
+            out(f"{1 - p / 100:.5f}  {float(sims[max(0, n - 1 - int(p / 100 * n))]):.5f}")
+        out(f"actual stat {stat:.5f}")
+    elif op == "st":
+        base = torch.arange(1, size + 1, dtype=torch.float64, device=dev)
+        for s in range(11):
+            r = base.repeat(20, 1)
+            rows = torch.arange(20, device=dev)
+            for _ in range(s):
+                i = torch.randint(0, size, (20,), generator=g, device=dev)
+                j = torch.randint(0, size, (20,), generator=g, device=dev)
+                a, b = r[rows, i].clone(), r[rows, j].clone()
+                r[rows, i], r[rows, j] = b, a
+            out(f"shuffle {s}  stat {float(zc_stat(r, half, half).mean()):.5f}")
+    elif op == "di":
+        d = zh_rank_samples(1, 5.0, 0.5, 10.0, 1.0, half, 0, g, dev)
+        out(f"diff distr stat {float(zc_stat(d, half, half)[0]):.5f}")
+        s = zh_rank_samples(1, 5.0, 0.5, 5.0, 0.5, half, 0, g, dev)
+        out(f"same distr stat {float(zc_stat(s, half, half)[0]):.5f}")
+    else:
+        raise ValueError("invalid op")
+    out.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# forecast (P/app/profod.py + P/unsupv/profo.py)
+# ---------------------------------------------------------------------------------------------
+def _ts_file(path, fmt):
+    import datetime as _dt
+    ts, ys = [], []
+    for l in Path(path).read_text().splitlines():
+        if not l.strip():
+            continue
+        d, y = l.split(",")[:2]
+        d = d.strip()
+        try:
+            t = float(d)
+        except ValueError:
+            t = _dt.datetime.strptime(d, fmt or "%Y-%m-%d %H:%M:%S").timestamp()
+        ts.append(t)
+        ys.append(float(y))
+    return torch.tensor(ts, dtype=torch.float64), torch.tensor(ys, dtype=torch.float64)
+
+
+_FREQ_S = {"H": 3600.0, "h": 3600.0, "D": 86400.0, "d": 86400.0, "W": 7 * 86400.0, "min": 60.0, "T": 60.0,
+           "S": 1.0, "s": 1.0}
+
+
+@job("forecast", "additive forecaster app (P/app/profod.py): forecast <props> [k=v ...], "
+     "common.mode = train | forecast | validate | shuffle | randomize", aliases=("profod",))
+def forecast(args):
+    from ..analytics.forecast import AdditiveForecaster
+    rest = _rest(args, 1, "forecast <props> [k=v ...]")
+    cp = rest[0]
+    conf = _props(cp, rest[1:])
+    out, dev = _Out(args), _dev(args)
+    mode = _get(conf, "common.mode", "train")
+    out("running mode: " + mode)
+    fmt = _get(conf, "train.data.new.dateformat")
+
+    def seas(key, default):
+        v = _get(conf, key, "auto")
+        return default if v in ("auto", "True", "true") else (0 if v in ("False", "false") else int(v))
+
+    def build():
+        return AdditiveForecaster(
+            n_changepoints=int(_get(conf, "train.num.changepoints", "25")),
+            changepoint_range=float(_get(conf, "train.changepoint.range", "0.8")),
+            changepoint_prior=float(_get(conf, "train.changepoint.prior.scale", "0.05")),
+            yearly=seas("train.yearly.seasonality", 10), weekly=seas("train.weekly.seasonality", 3),
+            daily=seas("train.daily.seasonality", 4),
+            seasonality_prior=float(_get(conf, "train.seasonality.prior.scale", "10.0")),
+            interval_width=float(_get(conf, "train.interval.width", "0.8")),
+            uncertainty_samples=int(_get(conf, "train.uncertainty.samples", "1000")),
+            mcmc_samples=int(_get(conf, "train.mcmc.samples", "0")), device=str(dev), seed=args.seed or 0)
+
+    def train():
+        t, y = _ts_file(_resolve(cp, _get(conf, "train.data.file")), fmt)
+        m = build().fit(t, y)
+        if _bool(conf, "train.model.save"):
+            p = _model_path(conf)
+            Path(p).parent.mkdir(parents=True, exist_ok=True)
+            m.save(p)
+            out("model saved")
+        return m
+
+    def model():
+        if _bool(conf, "forecast.use.saved.model", True) and os.path.exists(_model_path(conf)):
+            return AdditiveForecaster.load(_model_path(conf), device=str(dev))
+        return train()
+
+    def do_forecast(m):
+        window = int(_get(conf, "forecast.window"))
+        step = _FREQ_S[_get(conf, "forecast.unit", "D")]
+        tf = m.future_times(window, step)
+        if _bool(conf, "forecast.include.history"):
+            tf = torch.cat([m.history_times(), tf])
+        p = m.predict(tf)
+        lines = ["ds,yhat,yhat_lower,yhat_upper,trend"]
+        for i in range(tf.numel()):
+            lines.append(f"{int(tf[i])},{float(p['yhat'][i]):.3f},{float(p['yhat_lower'][i]):.3f},"
+                         f"{float(p['yhat_upper'][i]):.3f},{float(p['trend'][i]):.3f}")
+        of = _get(conf, "forecast.output.file")
+        if of:
+            Path(of).write_text("\n".join(lines) + "\n")
+        return p, lines
+
+    if mode in ("train", "training"):
+        train()
+    elif mode == "forecast":
+        _, lines = do_forecast(model())
+        out.lines(lines[:5])
+    elif mode == "validate":
+        t, y = _ts_file(_resolve(cp, _get(conf, "forecast.validate.file")), fmt)
+        p, _ = do_forecast(model())
+        f = p["yhat"].cpu()
+        assert f.numel() == y.numel(), "validation data size does not match with forecast data size"
+        metric = _get(conf, "forecast.validate.error.metric", "MSE")
+        e = (f - y).abs()
+        err = float((e * e).mean() if metric == "MSE" else e.mean())
+        out(f"Error {metric} {err:.3f}")
+    elif mode in ("shuffle", "randomize"):
+        src = _resolve(cp, _get(conf, "predictability.input.file" if mode == "shuffle" else "rand.input.file"))
+        dst = _get(conf, "predictability.shuffled.file" if mode == "shuffle" else "rand.shuffled.file")
+        recs = [l.split(",") for l in Path(src).read_text().splitlines() if l.strip()]
+        y = torch.tensor([float(r[1]) for r in recs], dtype=torch.float64)
+        g = torch.Generator().manual_seed(args.seed or 0)
+        if mode == "shuffle":             # blockShuffle: blocks of block.size values in random order
+            bs = int(_get(conf, "predictability.block.size", "8"))
+            nb = -(-y.numel() // bs)
+            order = torch.randperm(nb, generator=g)
+            sh = torch.cat([y[b * bs:(b + 1) * bs] for b in order.tolist()])
+        else:                              # sampleWithReplace
+            sh = y[torch.randint(0, y.numel(), (y.numel(),), generator=g)]
+        Path(dst).write_text("".join(f"{r[0]},{v:.3f}\n" for r, v in zip(recs, sh.tolist())))
+    else:
+        raise ValueError("invalid command")
+    out.close()

@@ -11,6 +11,7 @@ import math
 import sys
 from pathlib import Path
 
+import numpy as np
 import torch
 
 from .. import _native
@@ -837,12 +838,45 @@ def classifier(args):
            "lr": SV.LogisticRegressionDiscriminant}[args.kind]
     c = cls(args.config, device=args.device)
     mode = args.mode or c.getMode()
+    if mode == "explain":
+        return _classifier_explain(c, args)
     res = {"training": c.train, "train": c.train, "trainValidate": c.trainValidate,
            "trainValidateSearch": c.trainValidateSearch, "validate": c.validate, "predict": c.predict,
            "predictProb": c.predictProb, "autoTrain": c.autoTrain}[mode]()
     if isinstance(res, torch.Tensor):
         res = res.cpu().tolist()
     print(json.dumps(res, default=str))
+
+
+def _classifier_explain(clf, args):
+    """``intrd.py explain <clf> <clfConf> <limeConf> <record>`` (P/app/intrd.py:69-89): a LIME
+    surrogate (analytics/interpret.LimeTabular) around the record, built from the classifier's
+    training features, with the LimeInterpreter keys of P/mlextra/interpret.py:38-56
+    (``inter.feature.names``, ``inter.kernel.width``, ``data.cat.values`` -> categorical columns,
+    ``inter.random.state``, ``explain.num.features``, ``explain.num.samples``); prints the top
+    features and their weights as lime's ``as_list()``."""
+    from ..analytics.interpret import LimeTabular
+    from ..utils.config import read_properties
+    rest = list(getattr(args, "rest", None) or [])
+    if len(rest) < 2:
+        raise SystemExit("usage: classifier --mode explain --kind K -c clf.props <lime.props> <record>")
+    lc = read_properties(rest[0])
+    get = lambda k, d=None: (d if lc.get(k, "_").strip() in ("_", "") else lc[k].strip())
+    names = get("inter.feature.names").split(",")
+    cats = [int(it.split(":")[0]) for it in get("data.cat.values", "").split(",") if it] \
+        if get("data.cat.values") else []
+    X, _ = clf.prepTrainingData()
+    rec = np.array([float(v) for v in rest[1].split(",")], dtype=np.float32)
+    clf._ensure_model()
+    kw = get("inter.kernel.width")
+    lime = LimeTabular(torch.tensor(X), names, kernel_width=float(kw) if kw else None, categorical=cats,
+                       seed=int(get("inter.random.state", "100")))
+    pf = lambda P: torch.as_tensor(np.asarray(clf.model.predict_proba(P.cpu().numpy())), dtype=torch.float32)
+    exp = lime.explain(torch.tensor(rec), pf, label=1, num_samples=int(get("explain.num.samples", "5000")),
+                       num_features=int(get("explain.num.features", "10")))
+    print("model explanation")
+    for name, w in exp["explanation"]:
+        print(str((name, w)))
 
 
 @job("autoSupervisedLearning", "TPE search over classifiers and their hyper-parameters (P/app/autosupv.py): "

@@ -161,6 +161,20 @@ class RestrictedBoltzmannMachine:
         vf[r, idx] = 1 - vf[r, idx]
         return v.shape[1] * torch.nn.functional.logsigmoid(self.free_energy(vf) - self.free_energy(v))
 
+    def save(self, path):
+        """Weights and biases in the framework's container (utils/checkpoint.py; the reference
+        pickles the sklearn estimator with joblib, P/unsupv/rbm.py:127-133)."""
+        from ..utils import checkpoint as C
+        C.save(path, {"W": self.W, "bh": self.bh, "bv": self.bv},
+               {"lr": self.lr, "batch_size": self.batch_size, "num_iter": self.num_iter})
+
+    def restore(self, path) -> "RestrictedBoltzmannMachine":
+        from ..utils import checkpoint as C
+        t, m = C.load(path, self.device)
+        self.W, self.bh, self.bv = t["W"].float(), t["bh"].float(), t["bv"].float()
+        self.lr, self.batch_size, self.num_iter = m["lr"], m["batch_size"], m["num_iter"]
+        return self
+
     @torch.no_grad()
     def impute(self, x: torch.Tensor, missing: torch.Tensor, n_iter: int = 100, init: float | None = None):
         """Fill ``missing`` (bool mask) entries by Gibbs sampling with observed units clamped; the
