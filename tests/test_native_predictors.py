@@ -172,6 +172,40 @@ def _close(a: list[str], b: list[str], rel=1e-4, abs_=2e-3):
             assert abs(fu - fv) <= abs_ + rel * abs(fv), (x, y)
 
 
+def _knn_tie_rows(data, schema_path, k: int, rel: float = 2e-5) -> set[int]:
+    """Rows whose k-th and (k+1)-th nearest training records are equidistant up to fp32 rounding
+    under the knnClassifier distance (min-max scaled numeric terms + a weight-2 category mismatch,
+    1 against a missing value), computed in fp64 on the host: the only rows where two correct
+    implementations (fp32 MFMA vs fp64, or mixed vs one-hot) may pick different neighbour sets."""
+    import torch
+    from avenir_amd.data import table as TBm
+    from avenir_amd.jobs.core import _category_codes, _numeric_block
+    from avenir_amd.utils.schema import FeatureSchema
+    schema = FeatureSchema.from_json(Path(schema_path))
+    t = TBm.load_csv(str(data), schema, raw_numeric=True)
+    X = _numeric_block(t).double()
+    lo, hi = X.min(0).values, X.max(0).values
+    X = (X - lo) / (hi - lo).clamp_min(1e-12)
+    C = _category_codes(t).long()
+    d2 = torch.cdist(X, X) ** 2
+    for f in range(C.shape[1]):
+        a, b = C[:, f].view(-1, 1), C[:, f].view(1, -1)
+        d2 += torch.where((a < 0) & (b < 0), 0.0, torch.where((a < 0) | (b < 0), 1.0, torch.where(a != b, 2.0, 0.0)))
+    srt = d2.clamp_min(0).sqrt().sort(1).values
+    dk, dk1 = srt[:, k - 1], srt[:, k]
+    return set(torch.nonzero((dk1 - dk).abs() <= rel * (1 + dk)).view(-1).tolist())
+
+
+def _assert_knn_equal_except_ties(a: list[str], b: list[str], tmp_path, k: int):
+    """Every differing prediction must sit on a row where the k-th neighbour is tied."""
+    assert len(a) == len(b)
+    assert [x.rsplit(",", 1)[0] for x in a] == [y.rsplit(",", 1)[0] for y in b]
+    diff = [i for i, (x, y) in enumerate(zip(a, b)) if x != y]
+    if diff:
+        ties = _knn_tie_rows(tmp_path / "hangup.csv", tmp_path / "hangup.json", k)
+        assert set(diff) <= ties, f"non-tie rows differ: {sorted(set(diff) - ties)[:10]}"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
 def test_native_predictors_gpu_equal_cpu(tmp_path, name, monkeypatch):
@@ -186,8 +220,7 @@ def test_native_predictors_gpu_equal_cpu(tmp_path, name, monkeypatch):
     if name in ("mmc", "nbp", "nbp_fp"):
         _close(g, c)
     elif name == "knn":      # equidistant neighbours: MFMA fp32 vs fp64 distances may break ties apart
-        assert len(g) == len(c) and sum(a != b for a, b in zip(g, c)) <= 0.03 * len(c)
-        assert [a.rsplit(",", 1)[0] for a in g] == [b.rsplit(",", 1)[0] for b in c]
+        _assert_knn_equal_except_ties(g, c, tmp_path, 5)
     else:
         assert g == c
 
@@ -238,4 +271,4 @@ def test_knn_job_mixed_path_matches_one_hot_fallback(tmp_path, monkeypatch):
     monkeypatch.setattr(D, "mixed_knn_max_dims", lambda: 0)
     _run(argv + ["-o", tmp_path / "onehot.txt", "-c", cfg, "--device", "cpu"])
     a, b = _lines(tmp_path / "mixed.txt"), _lines(tmp_path / "onehot.txt")
-    assert len(a) == len(b) and sum(x != y for x, y in zip(a, b)) <= 0.03 * len(b)
+    _assert_knn_equal_except_ties(a, b, tmp_path, 5)
