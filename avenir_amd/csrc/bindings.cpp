@@ -1616,7 +1616,8 @@ static avk::SvmKerX make_kerx(const at::Tensor& X, const at::Tensor& xn, int64_t
 int64_t smo_ws_run_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, double gamma, double coef0,
                      int64_t degree, at::Tensor& alpha, at::Tensor& G, const at::Tensor& y, double C, double eps,
                      int64_t inner_iter, double rel_tol, int64_t max_outer, int64_t check_every, at::Tensor& ws,
-                     at::Tensor& ok, at::Tensor& dA, at::Tensor& inner_total, at::Tensor& gap) {
+                     at::Tensor& ok, at::Tensor& dA, at::Tensor& inner_total, at::Tensor& gap, int64_t cache_slots,
+                     const c10::optional<at::Tensor>& cache_stats) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&alpha, &G, &y, &gap, &dA}) {
     CHECK_DEV((*t));
     CHECK_DTYPE((*t), at::kFloat);
@@ -1625,6 +1626,37 @@ int64_t smo_ws_run_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, do
   const int64_t B = y.size(0), N = y.size(1), Q = avk::smo_ws_size();
   TORCH_CHECK(N >= 1 && N <= (1 << 26), "1 <= N <= 2^26");
   const avk::SvmKerX k = make_kerx(X, xn, B, N, kind, gamma, coef0, degree);
+  // kernel-row cache (one problem on a shared X): S slots in sets of 8 + Q transient rows
+  constexpr int kWays = 8;
+  const int64_t S = cache_slots > 0 ? std::max<int64_t>(kWays, cache_slots / kWays * kWays) : 0;
+  TORCH_CHECK(S == 0 || (B == 1 && k.xbs == 0), "the row cache needs one problem on a shared X");
+  TORCH_CHECK(S <= 16384, "at most 16384 cache slots");
+  at::Tensor c_rows, c_tag, c_stamp, c_slot_of, c_step, c_ws_slot, c_miss_q, c_miss_cnt, c_stats;
+  avk::SvmCache cache{};
+  if (S > 0) {
+    auto iopt = y.options().dtype(at::kInt);
+    c_rows = at::empty({(S + Q) * N}, y.options());
+    c_tag = at::full({S}, -1, iopt);
+    c_stamp = at::zeros({S}, iopt);
+    c_slot_of = at::full({N}, -1, iopt);
+    c_step = at::zeros({1}, iopt);
+    c_ws_slot = at::zeros({Q}, y.options().dtype(at::kLong));
+    c_miss_q = at::zeros({Q}, iopt);
+    c_miss_cnt = at::zeros({1}, iopt);
+    if (cache_stats.has_value() && cache_stats->defined()) {
+      CHECK_DEV((*cache_stats));
+      CHECK_DTYPE((*cache_stats), at::kLong);
+      TORCH_CHECK(cache_stats->numel() == 2, "cache_stats must be int64 [2]");
+      c_stats = *cache_stats;
+    } else {
+      c_stats = at::zeros({2}, y.options().dtype(at::kLong));
+    }
+    cache = avk::SvmCache{c_rows.data_ptr<float>(), c_tag.data_ptr<int>(), c_stamp.data_ptr<int>(),
+                          c_slot_of.data_ptr<int>(), c_step.data_ptr<int>(),
+                          reinterpret_cast<long long*>(c_ws_slot.data_ptr<int64_t>()), c_miss_q.data_ptr<int>(),
+                          c_miss_cnt.data_ptr<int>(), reinterpret_cast<unsigned long long*>(c_stats.data_ptr<int64_t>()),
+                          (int)S, kWays};
+  }
   TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == B && alpha.size(1) >= N && G.sizes() == alpha.sizes(),
               "alpha / G must be [B, >= N]");
   CHECK_DEV(ws);
@@ -1647,7 +1679,7 @@ int64_t smo_ws_run_x(const at::Tensor& X, const at::Tensor& xn, int64_t kind, do
                          (int)check_every, reinterpret_cast<long long*>(ws.data_ptr<int64_t>()), ok.data_ptr<bool>(),
                          dA.data_ptr<float>(), reinterpret_cast<long long*>(inner_total.data_ptr<int64_t>()),
                          gap.data_ptr<float>(), cand.data_ptr<int>(), cnt.data_ptr<int>(), Kws.data_ptr<float>(),
-                         host_gap.data_ptr<float>(), 0, cur_stream(y), &k);
+                         host_gap.data_ptr<float>(), 0, cur_stream(y), &k, nullptr, S > 0 ? &cache : nullptr);
 }
 
 // one implicit-kernel gather (K[ws, ws] -> [B, Q, Q]) and one gradient update (tests / oracles)
@@ -3762,7 +3794,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("smo_ws_select", &smo_ws_select);
   m.def("smo_ws_update", &smo_ws_update);
   m.def("smo_ws_run", &smo_ws_run);
-  m.def("smo_ws_run_x", &smo_ws_run_x);
+  m.def("smo_ws_run_x", &smo_ws_run_x, py::arg("X"), py::arg("xn"), py::arg("kind"), py::arg("gamma"),
+        py::arg("coef0"), py::arg("degree"), py::arg("alpha"), py::arg("G"), py::arg("y"), py::arg("C"), py::arg("eps"),
+        py::arg("inner_iter"), py::arg("rel_tol"), py::arg("max_outer"), py::arg("check_every"), py::arg("ws"),
+        py::arg("ok"), py::arg("dA"), py::arg("inner_total"), py::arg("gap"), py::arg("cache_slots") = 0,
+        py::arg("cache_stats") = py::none());
   m.def("smo_ws_gather_x", &smo_ws_gather_x);
   m.def("smo_ws_update_x", &smo_ws_update_x);
   m.def("svm_kernel_matrix", &svm_kernel_matrix);

@@ -138,6 +138,26 @@ struct SvmKerX {
 };
 void smo_ws_gather_x(const SvmKerX& k, const long long* ws, const bool* ok, float* Kws, int B, int N, const float* gap,
                      float skip, hipStream_t stream);
+// HBM cache of kernel rows K[r, 0..N) for the implicit-kernel solver (one problem, shared X):
+// S slots in sets of `ways`, LRU within a set by last-used step; slots S..S+Q-1 are transient rows
+// for misses a full set cannot take.  All state lives on the device (graph-capturable).
+struct SvmCache {
+  float* rows;                // [S + Q][N]
+  int* tag;                   // [S] cached row or -1
+  int* stamp;                 // [S] step of last use
+  int* slot_of;               // [N] slot of a row or -1 (validated against tag)
+  int* step;                  // [1] step counter (advanced by the lookup kernel)
+  long long* ws_slot;         // [Q] row of the cache holding K[ws[q], :] this step
+  int* miss_q;                // [Q] working-set positions whose row must be computed this step
+  int* miss_cnt;              // [1]
+  unsigned long long* stats;  // [2] hits, misses (cumulative)
+  int S, ways;
+};
+// one outer step's gradient update through the cache: lookup / LRU replacement, the missing rows
+// computed from X into their slots, then G[n] += y[n] sum_q dA_q rows[slot_q][n] (dense update)
+void smo_ws_update_cached(const SvmKerX& k, const SvmCache& c, const long long* ws, const float* dA, const bool* ok,
+                          const float* y, float* G, int N, int ldag, int Q, const float* gap, float skip,
+                          hipStream_t stream);
 void smo_ws_update_x(const SvmKerX& k, const long long* ws, const float* dA, const bool* ok, const float* y, float* G,
                      int B, int N, int ldag, int Q, const float* gap, float skip, hipStream_t stream);
 // K [na, nb] = k(a_i, b_j) through f32 MFMA (v_mfma_f32_16x16x4_f32) for any d; a.X / a.xn are the
@@ -149,7 +169,7 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
                      float* host_gap, long long kbs, hipStream_t stream, const SvmKerX* kx = nullptr,
-                     float* gap_next = nullptr);
+                     float* gap_next = nullptr, const SvmCache* cache = nullptr);
 void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* ok, float* alpha, const float* G,
                         const float* y, int ldag, const float* gap, int B, float C, float eps, int max_iter, float* dA,
                         long long* inner_total, float* Kws, float rel_tol, long long kbs, hipStream_t stream);

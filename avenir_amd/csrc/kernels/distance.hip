@@ -534,6 +534,12 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
                                                            int* __restrict__ outD, int a_row0) {
   __shared__ float As[64][DMAX + 1];
   const int a0 = a_row0 + blockIdx.y * 64;
+  // self-join: a workgroup whose whole j-range lies at or below its first i keeps nothing (about
+  // half the grid of a diagonal block): leave before touching memory (uniform per workgroup)
+  if (tri) {
+    const long long j_last = b_base + min(nB, (int)(blockIdx.x + 1) * 256) - 1;
+    if (j_last <= a_base + a0) return;
+  }
   for (int e = threadIdx.x; e < 64 * DMAX; e += 256) {   // columns D..DMAX-1 zero (b[] is zero there too)
     const int r = e / DMAX, c = e - r * DMAX;
     As[r][c] = (a0 + r < nA && c < D) ? A[(long long)(a0 + r) * D + c] : 0.f;
@@ -544,10 +550,13 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
   float b[DMAX];
 #pragma unroll
   for (int c = 0; c < DMAX; ++c) b[c] = c < D ? B[(long long)j * D + c] : 0.f;
-  const int na = min(64, nA - a0);
+  int na = min(64, nA - a0);
   const long long gj = b_base + j;
+  if (tri) {  // rows r with a_base + a0 + r < gj only (j > i in global order)
+    const long long lim = gj - a_base - a0;
+    na = lim <= 0 ? 0 : (lim < na ? (int)lim : na);
+  }
   for (int r = 0; r < na; ++r) {
-    if (tri && gj <= a_base + a0 + r) continue;
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < DMAX; ++c) {

@@ -1751,6 +1751,209 @@ __global__ __launch_bounds__(UPX_T) void smo_ws_update_x_kernel(const avk::SvmKe
   G[(long long)b * ldag + n] += y[(long long)b * N + n] * acc;
 }
 
+// ---- kernel-row cache (the reference memoises kernel values, J/discriminant/
+// SequentialMinimalOptimization.java:511-524; libsvm keeps an LRU row cache, P/supv/svm.py:83-121).
+// svm_cache_lookup_kernel: ONE workgroup.  The slot metadata (tag, stamp) is staged in LDS; each
+// active working-set entry (ok, dA != 0: the rows the update reads) looks its row up through
+// slot_of (validated against tag) and stamps a hit with this step; a miss takes, among the ways of
+// its set (row % nsets) not used this step, the rank-th least recently used, rank = its order among
+// this step's misses of the same set (all choices computed from the same pre-update stamps, so no
+// two misses take one way), or a transient slot S + q when the set has no free way left.  Metadata
+// goes back to global memory at the end; the compact miss list drives the fill kernel.
+__global__ __launch_bounds__(1024) void svm_cache_lookup_kernel(avk::SvmCache c, const long long* __restrict__ ws,
+                                                                const float* __restrict__ dA,
+                                                                const bool* __restrict__ ok, int Q,
+                                                                const float* __restrict__ gap, float skip) {
+  extern __shared__ int cache_sm[];
+  int* s_tag = cache_sm;
+  int* s_stamp = cache_sm + c.S;
+  __shared__ int s_step, s_set[WS_Q], s_miss[WS_Q], s_choice[WS_Q], s_hits;
+  __shared__ long long s_row[WS_Q];
+  if (ws_done(gap, 0, skip)) return;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < c.S; i += 1024) {
+    s_tag[i] = c.tag[i];
+    s_stamp[i] = c.stamp[i];
+  }
+  if (tid == 0) {
+    s_step = c.step[0] + 1;
+    c.step[0] = s_step;
+    s_hits = 0;
+  }
+  __syncthreads();
+  const int step = s_step, nsets = c.S / c.ways;
+  const bool mine = tid < Q;
+  bool active = false, hit = false;
+  long long row = 0;
+  if (mine) {
+    active = ok[tid] && dA[tid] != 0.f;
+    row = ws[tid];
+    s_row[tid] = row;
+    if (active) {
+      const int sl = c.slot_of[row];
+      hit = sl >= 0 && sl < c.S && s_tag[sl] == (int)row;
+      if (hit) {
+        s_stamp[sl] = step;
+        c.ws_slot[tid] = sl;
+        atomicAdd(&s_hits, 1);
+      }
+    }
+    s_miss[tid] = active && !hit;
+    s_set[tid] = (int)(row % nsets);
+  }
+  __syncthreads();
+  if (mine && s_miss[tid]) {
+    const int set = s_set[tid];
+    int rank = 0;
+    for (int p = 0; p < tid; ++p) rank += (s_miss[p] && s_set[p] == set) ? 1 : 0;
+    int choice = -1;
+    for (int w = 0; w < c.ways && choice < 0; ++w) {
+      const int sw = set * c.ways + w;
+      if (s_stamp[sw] == step) continue;
+      int pos = 0;
+      for (int v = 0; v < c.ways; ++v) {
+        const int sv = set * c.ways + v;
+        if (s_stamp[sv] == step) continue;
+        pos += (s_stamp[sv] < s_stamp[sw] || (s_stamp[sv] == s_stamp[sw] && v < w)) ? 1 : 0;
+      }
+      if (pos == rank) choice = sw;
+    }
+    s_choice[tid] = choice;
+  }
+  __syncthreads();
+  if (mine && s_miss[tid]) {
+    const int choice = s_choice[tid];
+    int slot = c.S + tid;  // transient row: the set is full this step
+    if (choice >= 0) {
+      const int old = s_tag[choice];
+      if (old >= 0) c.slot_of[old] = -1;
+      s_tag[choice] = (int)row;
+      s_stamp[choice] = step;
+      c.slot_of[row] = choice;
+      slot = choice;
+    }
+    c.ws_slot[tid] = slot;
+    int mpos = 0;
+    for (int p = 0; p < tid; ++p) mpos += s_miss[p] ? 1 : 0;
+    c.miss_q[mpos] = tid;
+  }
+  __syncthreads();
+  for (int i = tid; i < c.S; i += 1024) {
+    c.tag[i] = s_tag[i];
+    c.stamp[i] = s_stamp[i];
+  }
+  if (tid == 0) {
+    int m = 0;
+    for (int p = 0; p < Q; ++p) m += s_miss[p] ? 1 : 0;
+    c.miss_cnt[0] = m;
+    c.stats[0] += (unsigned long long)s_hits;
+    c.stats[1] += (unsigned long long)m;
+  }
+}
+
+// the missing rows K[ws[q], n] into their slots, D <= DP <= 64: one thread per n, the missing rows
+// of X in LDS (broadcast reads), RBF from squared differences.  Grid N / 256.
+template <int DP>
+__global__ __launch_bounds__(UPX_T) void svm_cache_fill_kernel(const avk::SvmKerX k, avk::SvmCache c,
+                                                               const long long* __restrict__ ws, int N,
+                                                               const float* __restrict__ gap, float skip) {
+  __shared__ float s_x[WS_Q][DP];
+  __shared__ long long s_slot[WS_Q];
+  if (ws_done(gap, 0, skip)) return;
+  const int cnt = c.miss_cnt[0];
+  if (cnt == 0) return;
+  const int D = k.D;
+  for (int e = threadIdx.x; e < cnt * DP; e += UPX_T) {
+    const int m = e / DP, d = e % DP;
+    const int q = c.miss_q[m];
+    s_x[m][d] = d < D ? k.X[ws[q] * D + d] : 0.f;
+    if (d == 0) s_slot[m] = c.ws_slot[q];
+  }
+  __syncthreads();
+  const int n = blockIdx.x * UPX_T + threadIdx.x;
+  if (n >= N) return;
+  float xr[DP];
+#pragma unroll
+  for (int d = 0; d < DP; ++d) xr[d] = d < D ? k.X[(long long)n * D + d] : 0.f;
+  for (int m = 0; m < cnt; ++m) {
+    float v;
+    if (k.kind == 2) {
+      float d2 = 0.f;
+#pragma unroll
+      for (int d = 0; d < DP; ++d) {
+        const float df = s_x[m][d] - xr[d];
+        d2 = fmaf(df, df, d2);
+      }
+      v = __expf(-k.gamma * d2);
+    } else {
+      float dot = 0.f;
+#pragma unroll
+      for (int d = 0; d < DP; ++d) dot = fmaf(s_x[m][d], xr[d], dot);
+      v = kfun_dot(k.kind, dot, 0.f, 0.f, k.gamma, k.coef0, k.degree);
+    }
+    c.rows[s_slot[m] * N + n] = v;
+  }
+}
+
+// the same fill for any D: missing rows in groups of 16, D in LDS chunks of 64, 16 accumulators per
+// thread (x_n re-read per group from L2)
+__global__ __launch_bounds__(UPX_T) void svm_cache_fill_any_kernel(const avk::SvmKerX k, avk::SvmCache c,
+                                                                   const long long* __restrict__ ws, int N,
+                                                                   const float* __restrict__ gap, float skip) {
+  constexpr int GQ = 16, CH = 64;
+  __shared__ float s_x[GQ][CH];
+  __shared__ long long s_row[WS_Q], s_slot[WS_Q];
+  if (ws_done(gap, 0, skip)) return;
+  const int cnt = c.miss_cnt[0];
+  if (cnt == 0) return;
+  const int D = k.D;
+  for (int m = threadIdx.x; m < cnt; m += UPX_T) {
+    const int q = c.miss_q[m];
+    s_row[m] = ws[q];
+    s_slot[m] = c.ws_slot[q];
+  }
+  __syncthreads();
+  const int n = blockIdx.x * UPX_T + threadIdx.x;
+  const bool in = n < N;
+  const float* xn = k.X + (long long)(in ? n : 0) * D;
+  for (int g0 = 0; g0 < cnt; g0 += GQ) {
+    const int gn = min(GQ, cnt - g0);
+    float acc[GQ];
+#pragma unroll
+    for (int i = 0; i < GQ; ++i) acc[i] = 0.f;
+    for (int d0 = 0; d0 < D; d0 += CH) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < GQ * CH; e += UPX_T) {
+        const int i = e / CH, d = e % CH;
+        s_x[i][d] = (i < gn && d0 + d < D) ? k.X[s_row[g0 + i] * D + d0 + d] : 0.f;
+      }
+      __syncthreads();
+      const int dl = min(CH, D - d0);
+      for (int d = 0; d < dl; ++d) {
+        const float xv = xn[d0 + d];
+#pragma unroll
+        for (int i = 0; i < GQ; ++i) {
+          if (k.kind == 2) {
+            const float df = s_x[i][d] - xv;
+            acc[i] = fmaf(df, df, acc[i]);
+          } else {
+            acc[i] = fmaf(s_x[i][d], xv, acc[i]);
+          }
+        }
+      }
+    }
+    if (in) {
+#pragma unroll
+      for (int i = 0; i < GQ; ++i) {
+        if (i >= gn) break;
+        const float v = k.kind == 2 ? __expf(-k.gamma * acc[i])
+                                    : kfun_dot(k.kind, acc[i], 0.f, 0.f, k.gamma, k.coef0, k.degree);
+        c.rows[s_slot[g0 + i] * N + n] = v;
+      }
+    }
+  }
+}
+
 // The same update for any D through f32 MFMA: the Q x 64 block of dot products of a workgroup (4
 // waves x 16 columns, 8 row tiles of 16 per wave) accumulates v_mfma_f32_16x16x4_f32 over D in LDS
 // chunks of 64 (working-set rows and the 64 column rows staged per chunk), then the epilogue maps
@@ -1917,6 +2120,35 @@ void smo_ws_update_x(const SvmKerX& k, const long long* ws, const float* dA, con
 #undef AV_UX
   }
   AV_HIP_CHECK(hipGetLastError());
+}
+
+void smo_ws_update_cached(const SvmKerX& k, const SvmCache& c, const long long* ws, const float* dA, const bool* ok,
+                          const float* y, float* G, int N, int ldag, int Q, const float* gap, float skip,
+                          hipStream_t stream) {
+  if (N <= 0) return;
+  if (Q > WS_Q) throw std::runtime_error("smo_ws_update_cached: Q <= 128");
+  if (c.S <= 0 || c.ways <= 0 || c.S % c.ways) throw std::runtime_error("smo_ws_update_cached: S must be a multiple of ways");
+  const size_t lds = 2 * sizeof(int) * (size_t)c.S;
+  if (lds > 128 * 1024) throw std::runtime_error("smo_ws_update_cached: at most 16384 slots");
+  if (lds > 64 * 1024)
+    AV_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(svm_cache_lookup_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  svm_cache_lookup_kernel<<<1, 1024, lds, stream>>>(c, ws, dA, ok, Q, gap, skip);
+  AV_HIP_CHECK(hipGetLastError());
+  const dim3 grid((N + UPX_T - 1) / UPX_T);
+  if (k.D <= 64) {
+#define AV_CF(DP) svm_cache_fill_kernel<DP><<<grid, UPX_T, 0, stream>>>(k, c, ws, N, gap, skip)
+    if (k.D <= 8) AV_CF(8);
+    else if (k.D <= 16) AV_CF(16);
+    else if (k.D <= 32) AV_CF(32);
+    else AV_CF(64);
+#undef AV_CF
+  } else {
+    svm_cache_fill_any_kernel<<<grid, UPX_T, 0, stream>>>(k, c, ws, N, gap, skip);
+  }
+  AV_HIP_CHECK(hipGetLastError());
+  // the dense update reads K[ws_slot[q], n] from the cache rows
+  smo_ws_update(c.rows, c.ws_slot, dA, ok, y, G, 1, N, ldag, Q, gap, skip, 0, stream);
 }
 
 void svm_kernel_matrix_mfma(const SvmKerX& a, const float* Bx, const float* bn, int na, int nb, float* K,
@@ -2152,8 +2384,10 @@ void smo_ws_solve_fused(const float* K, int N, const long long* ws, const bool* 
 long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float* y, int B, int ldag, float C,
                      float eps, int inner_iter, float rel_tol, long long max_outer, int check_every, long long* ws,
                      bool* ok, float* dA, long long* inner_total, float* gap, int* cand, int* cnt, float* Kws,
-                     float* host_gap, long long kbs, hipStream_t caller, const SvmKerX* kx, float* gap_next) {
+                     float* host_gap, long long kbs, hipStream_t caller, const SvmKerX* kx, float* gap_next,
+                     const SvmCache* cache) {
   if (B <= 0 || N <= 0 || max_outer <= 0) return 0;
+  if (cache && (B != 1 || !kx || kx->xbs != 0)) throw std::runtime_error("smo_ws_run: the row cache needs one problem on X");
   // merge fused into the gather (explicit K, a rank-merge selection, gap_next scratch given)
   const bool fuse = gap_next && !kx && Kws && !env_off("AVMI_SMO_FUSED_GATHER");
   const int Q = WS_Q, h = WS_Q / 2;
@@ -2197,7 +2431,10 @@ long long smo_ws_run(const float* K, int N, float* alpha, float* G, const float*
         smo_ws_solve_kernel<<<B, WSS_T, 0, stream>>>(Kws, ws, ok, alpha, G, y, N, ldag, gap, C, eps, rel_tol,
                                                      inner_iter, dA, inner_total);
         AV_HIP_CHECK(hipGetLastError());
-        smo_ws_update_x(*kx, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);
+        if (cache)
+          smo_ws_update_cached(*kx, *cache, ws, dA, ok, y, G, N, ldag, Q, gap, eps, stream);
+        else
+          smo_ws_update_x(*kx, ws, dA, ok, y, G, B, N, ldag, Q, gap, eps, stream);
         continue;
       }
       smo_ws_solve_fused(K, N, ws, ok, alpha, G, y, ldag, gap, B, C, eps, inner_iter, dA, inner_total, Kws, rel_tol,

@@ -1026,6 +1026,8 @@ def record_similarity(args):
         b0 = int(bbase.cpu()[0]) if bbase.numel() else 0
         blocks.append(LineSpans.from_packed(bb, bo))
         nb = Bc.shape[0]
+        if rB is None and nb and b0 + nb - 1 <= a_base:
+            continue        # self-join hop entirely at or below this rank's rows: no j > i (still forwarded)
         if fused and nb and A.shape[0]:
             # GPU: one fused distance + threshold + append launch per hop (distance.hip
             # pairs_within_kernel), pairs sorted by (i, j) — no [tile, nB] distance blocks

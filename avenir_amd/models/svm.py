@@ -12,9 +12,11 @@ MFMA for any other d / kernel) and run SMO inside one persistent workgroup per p
 larger ones run the working-set decomposition, either over that dense K or — above
 ``DENSE_MAX_N`` rows, or when K would not fit — over an IMPLICIT kernel: every outer step
 recomputes the Q x Q sub-problem block and the Q x N gradient-update rows from the rows of X
-(``smo_ws_run_x``; VALU from squared differences for d <= 64, f32 MFMA beyond).  Recomputing those
-Q N D FMAs is cheaper than reading the same rows from an HBM row cache, so memory is O(N D):
-N = 262 144 x 16 needs ~30 MB instead of the 275 GB N x N matrix.  B problems — one-vs-rest
+(``smo_ws_run_x``; VALU from squared differences for d <= 64, f32 MFMA beyond), so memory is
+O(N D): N = 262 144 x 16 needs ~30 MB instead of the 275 GB N x N matrix.  For wide rows (D >= 64
+by default) an HBM LRU cache of kernel rows (``row_cache_slots``) serves the rows the working
+sets revisit and only the misses are recomputed.  There is no row cap: the working-set selection
+streams any N (the streaming top-k parts of svm.hip).  B problems — one-vs-rest
 classes or cascade shards — are B workgroups of ONE launch.  The CPU path runs the same algorithm
 in numpy.
 """
@@ -99,6 +101,33 @@ def use_implicit(n: int, n_mats: int, device) -> bool:
         return True
     free, _ = torch.cuda.mem_get_info(torch.device(device))
     return 4.0 * n * n * n_mats > 0.5 * free
+
+
+#: kernel-row cache of the implicit solver: "auto" (on when recomputing a row costs more than
+#: reading it back: D >= AVMI_SVM_CACHE_MIN_D, default 64), "0" (off) or a slot count
+ROW_CACHE = __import__("os").environ.get("AVMI_SVM_CACHE", "auto")
+ROW_CACHE_MIN_D = int(__import__("os").environ.get("AVMI_SVM_CACHE_MIN_D", "64"))
+
+
+def row_cache_slots(K: "ImplicitKernel", B: int) -> int:
+    """Slots of the HBM kernel-row cache (svm.hip svm_cache_lookup_kernel) for an implicit-kernel
+    solve: 0 when off (several problems, per-problem X, small D under "auto"); else up to 4,096
+    rows, sized to a quarter of the device's free memory (one slot = N fp32 values).  Every outer
+    step the working set's rows come from the cache (LRU within 8-way sets) and only the misses are
+    recomputed from X — the reference's SMO memoises kernel values the same way
+    (J/discriminant/SequentialMinimalOptimization.java:511-524)."""
+    if B != 1 or K.X.dim() == 3 or K.device.type != "cuda":
+        return 0
+    mode = str(ROW_CACHE)
+    if mode in ("0", "off", "false"):
+        return 0
+    D = int(K.X.shape[-1])
+    if mode == "auto" and D < ROW_CACHE_MIN_D:
+        return 0
+    want = 4096 if mode in ("auto", "on", "1", "true") else int(mode)
+    free, _ = torch.cuda.mem_get_info(K.device)
+    fit = int(0.25 * free // (4 * K.N)) - 128
+    return max(0, min(want, fit, 16384)) // 8 * 8
 
 
 def smo_reference(K: np.ndarray, y: np.ndarray, C: float, eps: float = 1e-3, max_iter: int = 100000,
@@ -308,8 +337,15 @@ def smo_decomposition(K: torch.Tensor, y: torch.Tensor, C: float, eps: float = 1
         dA = torch.zeros((B, Q), device=dev)
         inner_total = torch.zeros(B, dtype=torch.long, device=dev)
         gap = torch.full((B,), float("inf"), device=dev)
+        slots = row_cache_slots(K, B)
+        stats = torch.zeros(2, dtype=torch.long, device=dev)
         outer = int(_native.C().smo_ws_run_x(*K.args(), alpha, G, yf, float(C), float(eps), int(inner_iter),
-                                             float(rel_tol), int(max_outer), 8, ws, ok, dA, inner_total, gap))
+                                             float(rel_tol), int(max_outer), 8, ws, ok, dA, inner_total, gap,
+                                             cache_slots=slots, cache_stats=stats))
+        if slots:
+            h, m = (int(v) for v in stats.tolist())
+            LAST_SOLVE.update(cache_slots=slots, cache_hits=h, cache_misses=m,
+                              cache_hit_rate=h / max(1, h + m))
         return alpha[:, :N].contiguous(), G[:, :N].contiguous(), outer, inner_total
     st = _WorkingSetSMO(K, y, C, eps, inner_iter, Q, fused, rel_tol)
     outer = 0

@@ -48,10 +48,13 @@ def main() -> int:
     ap.add_argument("--paths", default="dense,implicit")
     ap.add_argument("--sklearn", action="store_true")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--cache", default=None, help="kernel-row cache: auto | 0 | slots (models/svm.py ROW_CACHE)")
     ap.add_argument("--sklearn-sub", type=int, default=0,
                     help="also fit sklearn on a random subsample of this many rows and compare held-out accuracy")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
+    if args.cache is not None:
+        S.ROW_CACHE = args.cache
     gamma = 0.5
     Xw, yw = problem(512, args.d)
     for path in args.paths.split(","):
@@ -81,6 +84,7 @@ def main() -> int:
                    "outer_steps": S.LAST_SOLVE.get("outer"), "solver": S.LAST_SOLVE.get("solver"),
                    "support_vectors": int(m.support_.numel()), "train_acc": acc,
                    "heldout_acc": held, "inner_steps": int(sum(m.iters)),
+                   "cache": {k: v for k, v in S.LAST_SOLVE.items() if k.startswith("cache")},
                    "inner_per_outer": sum(m.iters) / max(1, S.LAST_SOLVE.get("outer") or 1),
                    "peak_bytes": int(peak), "dense_matrix_bytes": 4 * N * N}
             if args.sklearn_sub:

@@ -108,7 +108,65 @@ def kmeans():
     torch.cuda.synchronize()
 
 
-TARGETS = {"kmeans": kmeans, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
+def fmt():
+    """format.hip (fmt_len_kernel / fmt_write_kernel): 2^24 rows of int / float / string-table columns
+    formatted on the device into a file."""
+    import tempfile
+    from avenir_amd.data.records import format_lines
+    n = 1 << 24
+    g = torch.Generator(device="cuda").manual_seed(0)
+    ids = torch.randint(0, 1 << 30, (n,), generator=g, device="cuda")
+    v = torch.randn(n, generator=g, device="cuda", dtype=torch.float64) * 100
+    cls = torch.randint(0, 3, (n,), generator=g, device="cuda", dtype=torch.int32)
+    path = os.path.join(tempfile.gettempdir(), f"avmi_fmt_{os.getpid()}.txt")
+    try:
+        for _ in range(3):
+            format_lines([("i", ids), ("f", v, 3), ("s", ["low", "mid", "high"], cls)], n, ",", path=path)
+        torch.cuda.synchronize()
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+
+
+def pairs():
+    """distance.hip pairs_within_kernel: the recordSimilarity self-join of 2^17 x 8 rows."""
+    from avenir_amd import _native
+    g = torch.Generator(device="cuda").manual_seed(0)
+    A = torch.rand((1 << 17, 8), generator=g, device="cuda")
+    for _ in range(3):
+        _native.C().pairs_within(A, A, 8 ** 0.5, 1000.0, 100.0, True, 0, 0)
+    torch.cuda.synchronize()
+
+
+def split():
+    """split.hip ref_split_score_kernel (K7): a reference-split random forest level-wise build."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from bench_models import _numeric_table
+    from avenir_amd.models.tree import RandomForest, TreeParams
+    t = _numeric_table(1 << 20, 16, 2)
+    for f in t.schema.feature_fields:
+        f.max_split = 3
+    p = TreeParams(binary=False, stopping="maxDepth", max_depth=5, sub_sampling="withReplace",
+                   attr_selection="randomNotUsedYet", random_attr_count=4, split_selection="randomAmongTop",
+                   top_split_count=3, max_bins=8)
+    RandomForest(t.schema, 10, p, "all").fit(t)
+    torch.cuda.synchronize()
+
+
+def lstm():
+    """rnn_f32.hip lstm_fwd_f32_kernel / lstm_bwd_f32_kernel: training steps of the reference's
+    contact-tracing LSTM shape scaled to 65,536 sequences (input 5, hidden 100, 2 layers, T 5)."""
+    from avenir_amd.ops.rnn import FusedLSTM
+    torch.manual_seed(0)
+    m = FusedLSTM(5, 100, 2, precision="fp32").cuda()
+    x = torch.randn(65536, 5, 5, device="cuda")
+    for _ in range(4):
+        out, _ = m(x)
+        out[:, -1].sum().backward()
+    torch.cuda.synchronize()
+
+
+TARGETS = {"kmeans": kmeans, "fmt": fmt, "pairs": pairs, "split": split, "lstm": lstm, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
            "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest}
 
 if __name__ == "__main__":
