@@ -20,8 +20,10 @@ CSV parsing and packing are NOT in the timed steps (the headline is the on-devic
 ``extra`` reports them separately:
 
 * ``columns_rows_per_s_per_gpu`` — the same training step over the uint8 code columns.
-* ``ingest`` (1 GPU by default, ``--ingest-rows``) — the end-to-end job time for a CSV file of
-  ``2^26`` records written beforehand: native K1 parse -> device -> fit -> model text lines.
+* ``ingest`` (``--ingest-rows``; default 2^26 records on one GPU, 2^24 per rank on more) — the
+  end-to-end job time for a CSV file written beforehand: native K1 parse -> device -> fit -> model
+  text lines; on several GPUs every rank ingests its own file and ``job_rows_per_s`` is the total
+  over the slowest rank's time.
 * ``rccl_all_reduce`` (more than one GPU) — all-reduce latency at 8 KB and bus bandwidth at
   1 MB / 64 MB over the job's GPUs, next to the deterministic all-gather path and the hand-written
   peer-mapped one-shot / two-shot kernels (``algo="p2p"``, csrc/kernels/comm.hip).
@@ -165,11 +167,11 @@ def _ingest(rows: int, schema, dev, comm) -> dict:
         out["first_load_s"] = _timed(load, dev)
         t = None
         out["load_s"] = _timed(load, dev)
-        nb = NaiveBayes(schema)
+        nb = NaiveBayes(schema, comm=comm)        # one distributed job: the fit all-reduces the counts
         out["fit_s"] = _timed(lambda: nb.fit(t), dev)
         lines = []
         out["model_lines_s"] = _timed(lambda: lines.extend(nb.model_lines()), dev)
-        assert int(nb.class_n.sum().item()) == rows
+        assert int(nb.class_n.sum().item()) == rows * comm.world
         total = out["load_s"] + out["fit_s"] + out["model_lines_s"]
         cold = out["first_load_s"] + out["fit_s"] + out["model_lines_s"]
         out.update(rows=rows, file_bytes=nbytes, total_s=total, rows_per_s=rows / total,
@@ -198,8 +200,8 @@ def main() -> int:
     ap.add_argument("--probe-allreduce", action="store_true",
                     help="run the all-reduce probe on any device (it runs by default on >1 GPU)")
     ap.add_argument("--ingest-rows", type=int, default=-1,
-                    help="rows of the ingest-inclusive CSV measurement (0 = skip; default 2^26 on "
-                         "a single GPU, skipped on more)")
+                    help="rows per rank of the ingest-inclusive CSV measurement (0 = skip; default 2^26 "
+                         "on a single GPU, 2^24 per rank on more)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -286,9 +288,22 @@ def main() -> int:
             extra["rccl_all_reduce"] = _allreduce_probe(comm, dev)
         except Exception as e:      # a probe failure must not lose the measured headline
             extra["rccl_all_reduce"] = {"error": repr(e)}
-    ingest_rows = args.ingest_rows if args.ingest_rows >= 0 else ((1 << 26) if comm.world == 1 else 0)
+    # every rank ingests its own file (2^26 records on one GPU; 2^24 per rank on more, so 8 ranks'
+    # files fit /dev/shm together); the job's rate is the sum of records over the SLOWEST rank's time
+    ingest_rows = args.ingest_rows if args.ingest_rows >= 0 else ((1 << 26) if comm.world == 1 else (1 << 24))
     if ingest_rows > 0 and (dev.type == "cuda" or args.ingest_rows > 0):
-        extra["ingest"] = _ingest(ingest_rows, schema, dev, comm)
+        try:
+            comm.barrier()
+            ing = _ingest(ingest_rows, schema, dev, comm)
+            if comm.world > 1:
+                for k in ("total_s", "cold_total_s", "load_s", "first_load_s"):
+                    ing[k] = comm.reduce_max_scalar(float(ing[k]))
+                ing["job_rows"] = ingest_rows * comm.world
+                ing["job_rows_per_s"] = ingest_rows * comm.world / ing["total_s"]
+                ing["job_cold_rows_per_s"] = ingest_rows * comm.world / ing["cold_total_s"]
+            extra["ingest"] = ing
+        except Exception as e:      # the ingest extra must never cost the measured headline
+            extra["ingest"] = {"error": repr(e)}
     if args.predict:
         pr_n = min(n, 1 << 26)
         sub = Table(schema, pr_n, codes[:, : ((pr_n + 15) // 16) * 16].contiguous(), feats,
