@@ -3638,8 +3638,34 @@ std::vector<at::Tensor> ref_split_score(const at::Tensor& hist, const at::Tensor
   return {top, topv, segc, cinfo};
 }
 
+// One launch re-lays an fp32 layer's parameters (rnn_f32.hip lstm_pack_f32_kernel): w_ih [4H, I],
+// w_hh [4H, H], b_ih / b_hh [4H] or None -> wfrag [NW,4,HP/4,64], wfragT [NW,HP,64], wihk [4HP, I], biask [4HP].
+std::vector<at::Tensor> lstm_pack_f32(const at::Tensor& w_ih, const at::Tensor& w_hh,
+                                      const c10::optional<at::Tensor>& b_ih, const c10::optional<at::Tensor>& b_hh) {
+  CHECK_DEV(w_ih);
+  CHECK_DTYPE(w_ih, at::kFloat);
+  CHECK_DEV(w_hh);
+  CHECK_DTYPE(w_hh, at::kFloat);
+  TORCH_CHECK(w_hh.dim() == 2 && w_hh.size(0) == 4 * w_hh.size(1) && w_hh.is_contiguous(), "w_hh must be [4H, H]");
+  const int64_t H = w_hh.size(1), KS = lstm_ks(H), HP = 32 * KS;
+  TORCH_CHECK(w_ih.dim() == 2 && w_ih.size(0) == 4 * H && w_ih.size(1) >= 1 && w_ih.is_contiguous(),
+              "w_ih must be [4H, I]");
+  const int64_t I = w_ih.size(1);
+  check_opt_f32(b_ih, 4 * H, "b_ih");
+  check_opt_f32(b_hh, 4 * H, "b_hh");
+  DevGuard g(w_hh.device());
+  auto f32 = w_hh.options();
+  auto wfrag = at::empty({2 * KS, 4, HP / 4, 64}, f32), wfragT = at::empty({2 * KS, HP, 64}, f32);
+  auto wihk = at::empty({4 * HP, I}, f32), biask = at::empty({4 * HP}, f32);
+  avk::lstm_pack_f32(w_ih.data_ptr<float>(), w_hh.data_ptr<float>(), ptr_or_null<float>(b_ih), ptr_or_null<float>(b_hh),
+                     (int)H, (int)I, (int)KS, wfrag.data_ptr<float>(), wfragT.data_ptr<float>(), wihk.data_ptr<float>(),
+                     biask.data_ptr<float>(), cur_stream(w_hh));
+  return {wfrag, wfragT, wihk, biask};
+}
+
 // fp32 recurrence (rnn_f32.hip): xw [B, T, 4HP] fp32 kernel order (input projection + biases);
-// wfrag [NW, 4, HP/4, 64] fp32.  Returns hseq [B,T,H], cseq [B,T,HP] (+ gates [B,T,4HP] fp32).
+// wfrag [NW, 4, HP/4, 64] fp32.  Returns hseq [B,T,H], cseq [B,T,HP] (+ gates [B,T,4HP] fp32 and
+// hprev [B,T,H] = h_{t-1} when training).
 std::vector<at::Tensor> lstm_forward_f32(const at::Tensor& xw, const at::Tensor& wfrag,
                                          const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
                                          int64_t H, bool training) {
@@ -3658,16 +3684,20 @@ std::vector<at::Tensor> lstm_forward_f32(const at::Tensor& xw, const at::Tensor&
   DevGuard g(xw.device());
   auto f32 = xw.options();
   auto hseq = at::empty({B, T, H}, f32), cseq = at::empty({B, T, HP}, f32);
-  at::Tensor gates;
-  if (training) gates = at::empty({B, T, 4 * HP}, f32);
+  at::Tensor gates, hprev;
+  if (training) {
+    gates = at::empty({B, T, 4 * HP}, f32);
+    hprev = at::empty({B, T, H}, f32);
+  }
   avk::lstm_fwd_f32(xw.data_ptr<float>(), wfrag.data_ptr<float>(), ptr_or_null<float>(h0), ptr_or_null<float>(c0),
                     (int)B, (int)T, (int)H, (int)KS, hseq.data_ptr<float>(), cseq.data_ptr<float>(),
-                    training ? gates.data_ptr<float>() : nullptr, cur_stream(xw));
-  if (training) return {hseq, cseq, gates};
+                    training ? gates.data_ptr<float>() : nullptr, training ? hprev.data_ptr<float>() : nullptr,
+                    cur_stream(xw));
+  if (training) return {hseq, cseq, gates, hprev};
   return {hseq, cseq};
 }
 
-// fp32 backward recurrence: dz [B,T,4HP] fp32 (kernel order), dh0, dc0 [B,H]; wfragT [NW, HP, 64] fp32
+// fp32 backward recurrence: dz [B,T,4H] fp32 (torch gate order), dh0, dc0 [B,H]; wfragT [NW, HP, 64] fp32
 std::vector<at::Tensor> lstm_backward_f32(const at::Tensor& dhseq, const at::Tensor& gates, const at::Tensor& cseq,
                                           const c10::optional<at::Tensor>& c0, const c10::optional<at::Tensor>& dhn,
                                           const c10::optional<at::Tensor>& dcn, const at::Tensor& wfragT, int64_t H) {
@@ -3688,7 +3718,7 @@ std::vector<at::Tensor> lstm_backward_f32(const at::Tensor& dhseq, const at::Ten
   check_opt_f32(dhn, B * H, "dhn");
   check_opt_f32(dcn, B * H, "dcn");
   DevGuard g(dhseq.device());
-  auto dz = at::empty({B, T, 4 * HP}, dhseq.options());
+  auto dz = at::empty({B, T, 4 * H}, dhseq.options());
   auto dh0 = at::empty({B, H}, dhseq.options()), dc0 = at::empty({B, H}, dhseq.options());
   avk::lstm_bwd_f32(dhseq.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), ptr_or_null<float>(c0),
                     ptr_or_null<float>(dhn), ptr_or_null<float>(dcn), wfragT.data_ptr<float>(), (int)B, (int)T, (int)H,
@@ -3837,6 +3867,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);
   m.def("lstm_forward_f32", &lstm_forward_f32);
+  m.def("lstm_pack_f32", &lstm_pack_f32);
   m.def("ref_split_score", &ref_split_score);
   m.def("lstm_backward_f32", &lstm_backward_f32);
 

@@ -18,7 +18,8 @@
 // kernel, so the gate math is shared), and the accumulators start from xw_t.  h_t goes through LDS
 // as fp32 (double-buffered, one barrier per step); the B operand of k-step s is one float per lane,
 // h[seq l&15][unit 4s + (l>>4)] (rows padded to HP + 1 floats: conflict-free).
-// Weight-gradient GEMMs (dzᵀ·h_{t-1}, dzᵀ·x, Σdz) and dx = dz·W_ih run as fp32 library GEMMs.
+// Weight-gradient GEMMs (dzᵀ·h_{t-1}, dzᵀ·x, Σdz) and dx = dz·W_ih run as fp32 library GEMMs on dz in
+// torch gate order; lstm_pack_f32_kernel re-lays the parameters for a step in one launch.
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -37,13 +38,15 @@ __device__ __forceinline__ float tanh_(float x) {
 //   wfrag  [NW][4][KS4][64] fp32: A-fragment of W_hh for (wave, gate, k-step of 4), KS4 = HP / 4
 //   h0, c0 [B, H] or null;  hseq [B, T, H], cseq [B, T, HP] fp32 out
 //   gates  [B, T, 4HP] fp32 post-activation (kernel order) out or null
+//   hprev  [B, T, H] fp32 out or null: h_{t-1} at t (h0 / zeros at t = 0), the B operand rows of the
+//          backward's dW_hh GEMM, written here so the backward needs no shifted copy of hseq
 template <int KS, int RT>
 __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __restrict__ xw,
                                                                 const float* __restrict__ wfrag,
                                                                 const float* __restrict__ h0,
                                                                 const float* __restrict__ c0, int B, int T, int H,
                                                                 float* __restrict__ hseq, float* __restrict__ cseq,
-                                                                float* __restrict__ gates) {
+                                                                float* __restrict__ gates, float* __restrict__ hprev) {
   constexpr int HP = 32 * KS, KS4 = HP / 4, G4P = 4 * HP, NT = 128 * KS, LROW = HP + 1;
   __shared__ float sbuf[2][RT * 16][LROW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -72,7 +75,9 @@ __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __r
     for (int r = 0; r < 4; ++r) {
       const bool ok = u0 + r < H;
       c[rt][r] = (ok && c0) ? c0[grow * H + u0 + r] : 0.f;
-      sbuf[0][lr][u0 + r] = (ok && h0) ? h0[grow * H + u0 + r] : 0.f;
+      const float hv = (ok && h0) ? h0[grow * H + u0 + r] : 0.f;
+      sbuf[0][lr][u0 + r] = hv;
+      if (hprev && ok && rok[rt]) hprev[grow * TH + u0 + r] = hv;
     }
   }
   // xw_t of this lane's four units of every gate, prefetched one step ahead
@@ -119,12 +124,19 @@ __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __r
       if (rok[rt]) {
         *reinterpret_cast<f32x4*>(cseq + lrow[rt] * THP + (long long)t * HP + u0 + row0 * THP) = c[rt];
         float* hp = hseq + (row0 + lrow[rt]) * TH + (long long)t * H + u0;
+        float* pp = (hprev && t + 1 < T) ? hprev + (row0 + lrow[rt]) * TH + (long long)(t + 1) * H + u0 : nullptr;
         if (vec_h) {
-          if (u0 < H) *reinterpret_cast<f32x4*>(hp) = hn;
+          if (u0 < H) {
+            *reinterpret_cast<f32x4*>(hp) = hn;
+            if (pp) *reinterpret_cast<f32x4*>(pp) = hn;
+          }
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (u0 + r < H) hp[r] = hn[r];
+            if (u0 + r < H) {
+              hp[r] = hn[r];
+              if (pp) pp[r] = hn[r];
+            }
         }
         if (gates) {
           float* gp = gates + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
@@ -142,7 +154,8 @@ __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __r
 // dhseq [B, T, H]; gates [B, T, 4HP] fp32 kernel order; cseq [B, T, HP]; c0 / dhn / dcn [B, H] or null
 // wfragT [NW][4HP/4][64] fp32: A-fragment of W_hhᵀ for dhᵀ = W_hhᵀ·dzᵀ, k over the 4·HP gate rows
 //        gate-major (k = g·HP + u): lane l of k-step s holds W_hh[k = 4s + (l>>4)][unit 16w + (l&15)]
-// dz [B, T, 4HP] fp32 out (kernel order); dh0 / dc0 [B, H] out
+// dz [B, T, 4H] fp32 out in torch.nn.LSTM gate order (column g·H + u, padding dropped), so the
+//    weight-gradient GEMMs land in the parameters' own row order; dh0 / dc0 [B, H] out
 template <int KS, int RT>
 __global__ __launch_bounds__(128 * KS) void lstm_bwd_f32_kernel(
     const float* __restrict__ dhseq, const float* __restrict__ gates, const float* __restrict__ cseq,
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(128 * KS) void lstm_bwd_f32_kernel(
   const int col = lane & 15, quad = lane >> 4;
   const int u0 = 16 * w + 4 * quad, kc0 = 64 * w + 4 * quad;
   const long long row0 = (long long)blockIdx.x * (RT * 16);
-  const long long TG = (long long)T * G4P, THP = (long long)T * HP, TH = (long long)T * H;
+  const long long TG = (long long)T * G4P, THP = (long long)T * HP, TH = (long long)T * H, T4H = 4 * TH;
   const bool vec_h = (H & 3) == 0;
 
   float wb[KB];
@@ -234,12 +247,23 @@ __global__ __launch_bounds__(128 * KS) void lstm_bwd_f32_kernel(
         zr[2 * HP + r] = zg[rt][r];
         zr[3 * HP + r] = zo[rt][r];
       }
-      if (rok[rt]) {
-        float* zp = dz + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
-        *reinterpret_cast<f32x4*>(zp) = zi[rt];
-        *reinterpret_cast<f32x4*>(zp + 16) = zf[rt];
-        *reinterpret_cast<f32x4*>(zp + 32) = zg[rt];
-        *reinterpret_cast<f32x4*>(zp + 48) = zo[rt];
+      if (rok[rt] && u0 < H) {
+        float* zp = dz + (row0 + lrow[rt]) * T4H + (long long)t * 4 * H + u0;
+        if (vec_h) {
+          *reinterpret_cast<f32x4*>(zp) = zi[rt];
+          *reinterpret_cast<f32x4*>(zp + H) = zf[rt];
+          *reinterpret_cast<f32x4*>(zp + 2 * H) = zg[rt];
+          *reinterpret_cast<f32x4*>(zp + 3 * H) = zo[rt];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (u0 + r < H) {
+              zp[r] = zi[rt][r];
+              zp[H + r] = zf[rt][r];
+              zp[2 * H + r] = zg[rt][r];
+              zp[3 * H + r] = zo[rt][r];
+            }
+        }
       }
     }
     __syncthreads();
@@ -268,19 +292,72 @@ __global__ __launch_bounds__(128 * KS) void lstm_bwd_f32_kernel(
     }
 }
 
+// One launch re-lays the parameters for a step (replacing ~a dozen small copy / scatter launches):
+//   wfrag  [NW][4][HP/4][64]  forward A-fragments of W_hh (lane l, k-step s: W_hh[g·H + 16w + (l&15)][4s + (l>>4)])
+//   wfragT [NW][HP][64]       backward A-fragments of W_hhᵀ (k = 4s + (l>>4) over the gate-major 4·HP rows)
+//   wihk   [4HP, I]           W_ih rows in kernel gate order (the input-projection GEMM's operand)
+//   biask  [4HP]              b_ih + b_hh in kernel gate order
+// Padded units / columns are zero.  Flat grid-stride over the four outputs.
+__global__ __launch_bounds__(256) void lstm_pack_f32_kernel(const float* __restrict__ w_ih,
+                                                            const float* __restrict__ w_hh,
+                                                            const float* __restrict__ b_ih,
+                                                            const float* __restrict__ b_hh, int H, int I, int HP,
+                                                            float* __restrict__ wfrag, float* __restrict__ wfragT,
+                                                            float* __restrict__ wihk, float* __restrict__ biask) {
+  const long long n1 = 4LL * HP * HP, n3 = 4LL * HP * I, n = 2 * n1 + n3 + 4 * HP;
+  const int KS4 = HP / 4;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    if (e < n1) {
+      const int lane = (int)(e & 63);
+      const long long rest = e >> 6;
+      const int s = (int)(rest % KS4), g = (int)((rest / KS4) & 3), w = (int)(rest / (4 * KS4));
+      const int u = 16 * w + (lane & 15), k = 4 * s + (lane >> 4);
+      wfrag[e] = (u < H && k < H) ? w_hh[(long long)(g * H + u) * H + k] : 0.f;
+    } else if (e < 2 * n1) {
+      const long long f = e - n1;
+      const int lane = (int)(f & 63);
+      const long long rest = f >> 6;
+      const int s = (int)(rest % HP), w = (int)(rest / HP);
+      const int k = 4 * s + (lane >> 4), g = k / HP, uu = k % HP, cu = 16 * w + (lane & 15);
+      wfragT[f] = (uu < H && cu < H) ? w_hh[(long long)(g * H + uu) * H + cu] : 0.f;
+    } else {
+      const long long f = e - 2 * n1;
+      const int kc = f < n3 ? (int)(f / I) : (int)(f - n3);
+      const int w = kc >> 6, g = (kc >> 4) & 3, u = 16 * w + (kc & 15);
+      if (f < n3) {
+        const int j = (int)(f % I);
+        wihk[f] = u < H ? w_ih[(long long)(g * H + u) * I + j] : 0.f;
+      } else {
+        float b = 0.f;
+        if (u < H) b = (b_ih ? b_ih[g * H + u] : 0.f) + (b_hh ? b_hh[g * H + u] : 0.f);
+        biask[kc] = b;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 namespace avk {
 
+void lstm_pack_f32(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, int H, int I, int KS,
+                   float* wfrag, float* wfragT, float* wihk, float* biask, hipStream_t s) {
+  const int HP = 32 * KS;
+  const long long n = 8LL * HP * HP + 4LL * HP * I + 4LL * HP;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 2048);
+  lstm_pack_f32_kernel<<<grid, 256, 0, s>>>(w_ih, w_hh, b_ih, b_hh, H, I, HP, wfrag, wfragT, wihk, biask);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
 // RT = 1 throughout: the f32 weight fragments take HP (forward) / 4·HP/4 (backward) VGPRs per
 // lane, leaving no room for a second tile's accumulators at HP = 128.
 void lstm_fwd_f32(const float* xw, const float* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
-                  float* hseq, float* cseq, float* gates, hipStream_t s) {
+                  float* hseq, float* cseq, float* gates, float* hprev, hipStream_t s) {
   const int grid = (B + 15) / 16;
   switch (KS) {
-    case 1: lstm_fwd_f32_kernel<1, 1><<<grid, 128, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates); break;
-    case 2: lstm_fwd_f32_kernel<2, 1><<<grid, 256, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates); break;
-    case 4: lstm_fwd_f32_kernel<4, 1><<<grid, 512, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates); break;
+    case 1: lstm_fwd_f32_kernel<1, 1><<<grid, 128, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates, hprev); break;
+    case 2: lstm_fwd_f32_kernel<2, 1><<<grid, 256, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates, hprev); break;
+    case 4: lstm_fwd_f32_kernel<4, 1><<<grid, 512, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates, hprev); break;
     default: throw std::runtime_error("lstm_fwd_f32: KS in {1, 2, 4}");
   }
   AV_HIP_CHECK(hipGetLastError());

@@ -21,8 +21,9 @@ on the GPU; that path is selected by shape, never by a missing extension.
 ``nn.LSTM``) runs the fp32 twin of the kernels (csrc/kernels/rnn_f32.hip): the recurrence on
 v_mfma_f32_16x16x4_f32 with W_hh resident in VGPRs as f32 fragments, every stored intermediate
 fp32, and the input projection x·W_ihᵀ + b of all timesteps as one fp32 GEMM ahead of it (the f32
-fragments of W_hh alone take HP VGPRs).  Backward: one fp32 recurrence launch + fp32 GEMMs for
-dW_hh = dzᵀ·h_{t-1}, dW_ih = dzᵀ·x, db = Σdz and dx = dz·W_ih.  ``precision="bf16"`` opts into the
+fragments of W_hh alone take HP VGPRs); one ``lstm_pack_f32`` launch re-lays the parameters per
+optimizer step.  Backward: one fp32 recurrence launch writing dz in torch gate order + fp32 GEMMs
+for dW_hh = dzᵀ·h_{t-1} (rows written by the forward), dW_ih = dzᵀ·x, db = Σdz and dx = dz·W_ih.  ``precision="bf16"`` opts into the
 mixed-precision kernel above.  Both are checked against the fp32 oracle and ``nn.LSTM``
 (tests/test_rnn.py).
 """
@@ -132,29 +133,39 @@ def to_kernel_order(w: torch.Tensor, H: int) -> torch.Tensor:
     return out
 
 
-class _FragCacheF32:
-    """The fp32 fragments of W_hh, keyed like :class:`_FragCache`."""
+class _PackCacheF32:
+    """The fp32 layer's re-laid parameters (``lstm_pack_f32``: W_hh fragments, W_hhᵀ fragments,
+    kernel-order W_ih and b_ih + b_hh — ONE launch), keyed on the four tensors' (storage, version):
+    inference re-uses them across calls, training re-packs once per optimizer step.  Inside a
+    HIP-graph capture the pack is recorded, so replays re-pack."""
 
     def __init__(self, size: int = 16):
         self.size, self.d = size, {}
 
-    def get(self, w_hh: torch.Tensor, H: int):
+    @staticmethod
+    def _pack(w_ih, w_hh, b_ih, b_hh):
+        c = lambda t: None if t is None else t.detach().float().contiguous()
+        return tuple(_native.C().lstm_pack_f32(c(w_ih), c(w_hh), c(b_ih), c(b_hh)))
+
+    def get(self, w_ih, w_hh, b_ih, b_hh):
+        ts = (w_ih, w_hh, b_ih, b_hh)
         if torch.cuda.is_current_stream_capturing():
-            return pack_weights_f32(w_hh, H)
-        key = (w_hh.data_ptr(), w_hh._version, tuple(w_hh.shape), H)
+            return self._pack(*ts)
+        key = tuple((t.data_ptr(), t._version, tuple(t.shape)) if t is not None else None for t in ts)
         hit = self.d.get(key)
-        # the entry must belong to THIS live tensor: a freed tensor's memory (same address, shape
+        # the entry must belong to THESE live tensors: a freed tensor's memory (same address, shape
         # and version 0) may be re-used by a new one with different values
-        if hit is not None and hit[0]() is w_hh:
+        if hit is not None and all((r is None and t is None) or (r is not None and r() is t)
+                                   for r, t in zip(hit[0], ts)):
             return hit[1]
         if len(self.d) >= self.size:
             self.d.pop(next(iter(self.d)))
-        frags = pack_weights_f32(w_hh, H)
-        self.d[key] = (weakref.ref(w_hh), frags)
-        return frags
+        packed = self._pack(*ts)
+        self.d[key] = (tuple(None if t is None else weakref.ref(t) for t in ts), packed)
+        return packed
 
 
-_frags_f32 = _FragCacheF32()
+_packs_f32 = _PackCacheF32()
 
 
 class _FragCache:
@@ -235,55 +246,51 @@ class _LstmLayer(torch.autograd.Function):
 
 
 class _LstmLayerF32(torch.autograd.Function):
-    """One fp32 layer: forward = one fp32 GEMM (input projection of all timesteps, kernel gate
-    order) + ONE recurrence launch; backward = one recurrence launch + fp32 GEMMs for dx, dW_ih,
-    dW_hh and db."""
+    """One fp32 layer.  Forward: ONE pack launch (skipped while the parameters are unchanged) + one
+    fp32 GEMM (input projection of all timesteps, kernel gate order, biases fused) + ONE recurrence
+    launch, which also writes h_{t-1} rows for the backward.  Backward: one recurrence launch that
+    writes dz in torch gate order, then fp32 GEMMs straight into the parameters' layouts
+    (dx = dz·W_ih, dW_ih = dzᵀ·x, dW_hh = dzᵀ·h_{t-1}) and one column sum for the biases — no
+    gathers, no shifted copies."""
 
     @staticmethod
-    def forward(ctx, x, w_ih, w_hh, b, h0, c0):
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0, c0):
         B, T, I = x.shape
         H = w_hh.shape[1]
         HP = padded_hidden(H)
-        frag, frag_t = _frags_f32.get(w_hh, H)
-        w_ih_k = to_kernel_order(w_ih.detach().float(), H)                      # [4HP, I]
-        bias = to_kernel_order(b.detach().float(), H) if b is not None else None
-        x2 = x.reshape(B * T, I)
-        xw = (torch.addmm(bias, x2, w_ih_k.t()) if bias is not None else x2 @ w_ih_k.t()).view(B, T, 4 * HP)
+        frag, frag_t, w_ih_k, bias = _packs_f32.get(w_ih, w_hh, b_ih, b_hh)
+        xw = torch.addmm(bias, x.reshape(B * T, I), w_ih_k.t()).view(B, T, 4 * HP)
         need = any(ctx.needs_input_grad)
-        outs = _native.C().lstm_forward_f32(xw.contiguous(), frag, h0, c0, H, bool(need))
+        outs = _native.C().lstm_forward_f32(xw, frag, h0, c0, H, bool(need))
         hseq, cseq = outs[0], outs[1]
         if need:
-            ctx.save_for_backward(x, w_ih_k, hseq, cseq, outs[2], h0, c0, frag_t)
-        ctx.has_b, ctx.dims = b is not None, (B, T, I, H)
+            ctx.save_for_backward(x, w_ih, cseq, outs[2], outs[3], c0, frag_t)
+        ctx.dims = (B, T, I, H)
         return hseq, hseq[:, -1], cseq[:, -1, :H]
 
     @staticmethod
     def backward(ctx, dhseq, dhn, dcn):
-        x, w_ih_k, hseq, cseq, gates, h0, c0, frag_t = ctx.saved_tensors
+        x, w_ih, cseq, gates, hprev, c0, frag_t = ctx.saved_tensors
         B, T, I, H = ctx.dims
-        HP = padded_hidden(H)
-        _, _, inv = kernel_gate_order(H, cseq.device)
         if dhseq is None:
             dhseq = cseq.new_zeros(B, T, H)
         dz, dh0, dc0 = _native.C().lstm_backward_f32(dhseq.contiguous(), gates, cseq, c0,
                                                      None if dhn is None else dhn.contiguous(),
                                                      None if dcn is None else dcn.contiguous(), frag_t, H)
-        dz2 = dz.view(B * T, 4 * HP)                                   # fp32, kernel order
+        dz2 = dz.view(B * T, 4 * H)                                    # fp32, torch gate order
         need = ctx.needs_input_grad
-        dx = (dz2 @ w_ih_k).view(B, T, I) if need[0] else None
-        dw_ih = dw_hh = db = None
-        if need[1]:
-            dw_ih = (dz2.t() @ x.reshape(B * T, I)).index_select(0, inv)
-        if need[2]:
-            hprev = torch.cat([h0.view(B, 1, H) if h0 is not None else hseq.new_zeros(B, 1, H), hseq[:, :-1]], 1)
-            dw_hh = (dz2.t() @ hprev.reshape(B * T, H)).index_select(0, inv)
-        if need[3] and ctx.has_b:
-            db = dz2.sum(0).index_select(0, inv)
-        return dx, dw_ih, dw_hh, db, (dh0 if need[4] else None), (dc0 if need[5] else None)
+        dx = (dz2 @ w_ih.detach().float()).view(B, T, I) if need[0] else None
+        dw_ih = dz2.t() @ x.reshape(B * T, I) if need[1] else None
+        dw_hh = dz2.t() @ hprev.view(B * T, H) if need[2] else None
+        db = dz2.sum(0) if (need[3] or need[4]) else None
+        # the same tensor for both biases: autograd copies it when both accumulate
+        return (dx, dw_ih, dw_hh, db if need[3] else None, db if need[4] else None,
+                (dh0 if need[5] else None), (dc0 if need[6] else None))
 
 
-def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None, precision: str = "fp32"):
-    """One batch-first LSTM layer: (hseq [B,T,H], h_T [B,H], c_T [B,H]).
+def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None, precision: str = "fp32", b_hh=None):
+    """One batch-first LSTM layer: (hseq [B,T,H], h_T [B,H], c_T [B,H]).  ``b`` (+ ``b_hh``, the
+    torch.nn.LSTM split of the bias; added together) is the gate bias.
 
     GPU tensors with H <= 128 run the fused HIP kernels (raising if the extension is missing):
     ``precision="fp32"`` the fp32 recurrence (any input size: the input projection is a GEMM),
@@ -295,8 +302,12 @@ def lstm_layer(x, w_ih, w_hh, b=None, h0=None, c0=None, precision: str = "fp32")
         h0 = None if h0 is None else h0.float().contiguous()
         c0 = None if c0 is None else c0.float().contiguous()
         if precision == "fp32":
-            return _LstmLayerF32.apply(x, w_ih, w_hh, b, h0, c0)
+            return _LstmLayerF32.apply(x, w_ih, w_hh, b, b_hh, h0, c0)
+        if b_hh is not None:
+            b = b_hh if b is None else b + b_hh
         return _LstmLayer.apply(x, w_ih, w_hh, b, h0, c0)
+    if b_hh is not None:
+        b = b_hh if b is None else b + b_hh
     hseq, (h, c) = lstm_reference(x, w_ih, w_hh, b, h0, c0)
     return hseq, h, c
 
@@ -353,13 +364,12 @@ class FusedLSTM(torch.nn.Module):
         hs, cs = [], []
         out = x
         for l in range(L):
-            b = None
-            if self.bias:
-                b = getattr(self, f"bias_ih_l{l}") + getattr(self, f"bias_hh_l{l}")
+            b_ih = getattr(self, f"bias_ih_l{l}") if self.bias else None
+            b_hh = getattr(self, f"bias_hh_l{l}") if self.bias else None
             h0 = hx[0][l] if hx is not None else None
             c0 = hx[1][l] if hx is not None else None
-            out, h, c = lstm_layer(out, getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"), b, h0, c0,
-                                   self.precision)
+            out, h, c = lstm_layer(out, getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"), b_ih, h0, c0,
+                                   self.precision, b_hh=b_hh)
             hs.append(h)
             cs.append(c)
             if self.dropout > 0 and self.training and l < L - 1:

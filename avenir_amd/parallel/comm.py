@@ -325,21 +325,14 @@ class Comm:
 
     def ring_pass(self, t: torch.Tensor) -> torch.Tensor:
         """Send ``t`` to rank+1 and receive from rank-1 (systolic all-pairs schedule).  Shapes may
-        differ between ranks: the dim-0 length travels first."""
+        differ between ranks: the dim-0 length travels first.  Both exchanges are batched P2P groups
+        (at world 2 the send and the receive share one peer, and a lone RCCL send of a large
+        buffer would wait for a receive queued behind it)."""
         if not self.is_distributed:
             return t
-        nxt, prv = (self.rank + 1) % self.world, (self.rank - 1) % self.world
-        x, moved = self._prep(t.contiguous())
-        n_out = torch.tensor([x.shape[0]], dtype=torch.long, device=x.device)
-        n_in = torch.empty_like(n_out)
-        reqs = [dist.isend(n_out, nxt), dist.irecv(n_in, prv)]
-        for r in reqs:
-            r.wait()
-        recv = torch.empty((int(n_in.item()),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        reqs = [dist.isend(x, nxt), dist.irecv(recv, prv)]
-        for r in reqs:
-            r.wait()
-        return recv.to(t.device) if moved else recv
+        n_out = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
+        n_in = self.ring_pass_finish(self.ring_pass_start(n_out, 1))
+        return self.ring_pass_finish(self.ring_pass_start(t, int(n_in.item())))
 
     def ring_pass_start(self, t: torch.Tensor, recv_rows: int):
         """Post the send of ``t`` to rank+1 and the receive of ``recv_rows`` rows (same trailing

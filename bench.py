@@ -139,6 +139,55 @@ def _pick_small_allreduce(comm, like: torch.Tensor, mode: str) -> dict:
     return info
 
 
+def _comm_selftest(comm, dev) -> dict:
+    """The library collectives other than all-reduce that the framework's jobs use, run on THIS
+    job's GPUs (RCCL over xGMI when the driver launches several ranks), checked for content and
+    timed (max over ranks): the systolic ring of recordSimilarity / the kNN joins
+    (``ring_pass_start`` = one ``batch_isend_irecv`` group, and ``ring_iter``), the uneven
+    ``all_to_all_single`` of ``all_to_all_v`` / ``fetch_rows``, ``all_gather_v`` and
+    ``barrier(device_ids=...)``.  Runs after the timed steps."""
+    W, r = comm.world, comm.rank
+    out = {}
+    # ring: 64 MiB per rank -> per-link bandwidth of the neighbour exchange
+    n = 16 << 20
+    x = torch.full((n,), float(r), device=dev)
+    y = comm.ring_pass_finish(comm.ring_pass_start(x, n))
+    ok = bool((y == float((r - 1) % W)).all().item())
+    comm.barrier()
+    t = comm.reduce_max_scalar(_timed(lambda: [comm.ring_pass_finish(comm.ring_pass_start(x, n)) for _ in range(5)], dev) / 5)
+    out["ring_batch_isend_irecv"] = {"ok": ok, "bytes": 4 * n, "ms": t * 1e3, "GBps": 4 * n / t / 1e9}
+    del x, y
+    # ring_iter over two tensors of rank-dependent length
+    blocks = [torch.full((r + 3, 4), r, dtype=torch.int64, device=dev), torch.full((r + 3,), 2.0 * r, device=dev)]
+    seen, ok = [], True
+    for owner, blk in comm.ring_iter(blocks):
+        seen.append(owner)
+        ok &= blk[0].shape[0] == owner + 3 and bool((blk[0] == owner).all().item()) and bool((blk[1] == 2.0 * owner).all().item())
+    out["ring_iter"] = {"ok": bool(ok and seen == [(r - s) % W for s in range(W)])}
+    # uneven all-to-all: rank a sends cnt(a, b) rows [a, b, i] to rank b; large uneven pass timed
+    cnt = lambda a, b: 1 + (7 * a + 3 * b) % 11
+    chunks = [torch.stack([torch.full((cnt(r, b),), r), torch.full((cnt(r, b),), b), torch.arange(cnt(r, b))], 1).to(dev)
+              for b in range(W)]
+    got = comm.all_to_all_v(chunks)
+    ok = all(g.shape[0] == cnt(a, r) and bool((g[:, 0] == a).all().item()) and bool((g[:, 1] == r).all().item())
+             and bool((g[:, 2] == torch.arange(cnt(a, r), device=dev)).all().item()) for a, g in enumerate(got))
+    big = [torch.full(((1 << 18) * (1 + (r + b) % 3), 16), float(r), device=dev) for b in range(W)]
+    comm.all_to_all_v(big)
+    comm.barrier()
+    t = comm.reduce_max_scalar(_timed(lambda: [comm.all_to_all_v(big) for _ in range(3)], dev) / 3)
+    sent = sum(c.numel() * 4 for c in big)
+    out["all_to_all_v"] = {"ok": bool(ok), "bytes_sent_per_rank": sent, "ms": t * 1e3, "GBps_per_rank": sent / t / 1e9}
+    del big
+    g = comm.all_gather_v(torch.full((r + 1, 3), r, dtype=torch.int32, device=dev))
+    ref = torch.cat([torch.full((a + 1, 3), a, dtype=torch.int32) for a in range(W)])
+    out["all_gather_v"] = {"ok": bool(torch.equal(g.cpu(), ref))}
+    comm.barrier()
+    t = comm.reduce_max_scalar(_timed(lambda: [comm.barrier() for _ in range(20)], dev) / 20)
+    out["barrier"] = {"ok": True, "us": t * 1e6}
+    out["ok"] = all(v.get("ok", False) for v in out.values() if isinstance(v, dict))
+    return out
+
+
 def _ingest(rows: int, schema, dev, comm) -> dict:
     """CSV file -> ``load_csv`` (native K1 parse, device upload) -> fit -> model lines, every rank on
     its own file of ``rows`` records (written before timing, outside the clock)."""
@@ -288,6 +337,11 @@ def main() -> int:
             extra["rccl_all_reduce"] = _allreduce_probe(comm, dev)
         except Exception as e:      # a probe failure must not lose the measured headline
             extra["rccl_all_reduce"] = {"error": repr(e)}
+        if os.environ.get("AVMI_BENCH_COMM_SELFTEST", "1") != "0":
+            try:
+                extra["comm_selftest"] = _comm_selftest(comm, dev)
+            except Exception as e:
+                extra["comm_selftest"] = {"error": repr(e)}
     # every rank ingests its own file (2^26 records on one GPU; 2^24 per rank on more, so 8 ranks'
     # files fit /dev/shm together); the job's rate is the sum of records over the SLOWEST rank's time
     ingest_rows = args.ingest_rows if args.ingest_rows >= 0 else ((1 << 26) if comm.world == 1 else (1 << 24))

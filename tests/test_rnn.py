@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from avenir_amd.ops import rnn
+from avenir_amd import _native
 
 
 @pytest.mark.parametrize("H,I", [(20, 5), (64, 64), (100, 100), (37, 128)])
@@ -56,6 +57,44 @@ def test_pack_weights_f32_fragment_maps(H):
         assert fwd[wv, g, s, lane].item() == w(g * HP + 16 * wv + col, 4 * s + q)
         k = int(torch.randint(0, HP, (1,), generator=g_))
         assert bwd[wv, k, lane].item() == w(4 * k + q, 16 * wv + col)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,I", [(20, 3), (100, 1), (100, 100), (128, 7)])
+def test_lstm_pack_f32_kernel_matches_python_packers(cuda, H, I):
+    """rnn_f32.hip lstm_pack_f32_kernel (one launch) == the documented fragment maps + kernel gate
+    order + the summed biases."""
+    torch.manual_seed(H + I)
+    w_ih, w_hh = torch.randn(4 * H, I, device=cuda), torch.randn(4 * H, H, device=cuda)
+    b_ih, b_hh = torch.randn(4 * H, device=cuda), torch.randn(4 * H, device=cuda)
+    frag, frag_t, wihk, biask = _native.C().lstm_pack_f32(w_ih, w_hh, b_ih, b_hh)
+    f_ref, ft_ref = rnn.pack_weights_f32(w_hh, H)
+    assert torch.equal(frag, f_ref) and torch.equal(frag_t, ft_ref)
+    assert torch.equal(wihk, rnn.to_kernel_order(w_ih, H))
+    assert torch.equal(biask, rnn.to_kernel_order(b_ih + b_hh, H))
+    _, _, _, b1 = _native.C().lstm_pack_f32(w_ih, w_hh, None, b_hh)
+    assert torch.equal(b1, rnn.to_kernel_order(b_hh, H))
+
+
+@pytest.mark.gpu
+def test_fused_lstm_module_matches_torch_lstm_gpu(cuda):
+    """The fp32 module (split biases, torch-order dz, forward-written h_{t-1} rows) against
+    torch.nn.LSTM on the GPU: outputs and every parameter's gradient."""
+    torch.manual_seed(0)
+    ref = torch.nn.LSTM(5, 100, 2, batch_first=True).to(cuda)
+    mine = rnn.FusedLSTM(5, 100, 2).to(cuda)
+    mine.load_state_dict(ref.state_dict())
+    x = torch.randn(300, 5, 5, device=cuda)
+    h0, c0 = torch.randn(2, 300, 100, device=cuda), torch.randn(2, 300, 100, device=cuda)
+    o1, (h1, c1) = ref(x, (h0, c0))
+    o2, (h2, c2) = mine(x, (h0, c0))
+    torch.testing.assert_close(o2, o1, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(c2, c1, atol=1e-4, rtol=1e-4)
+    (o1.square().sum() + c1.sum()).backward()
+    (o2.square().sum() + c2.sum()).backward()
+    for (n, p1), p2 in zip(ref.named_parameters(), mine.parameters()):
+        rel = (p2.grad - p1.grad).norm() / p1.grad.norm()
+        assert rel.item() < 1e-4, (n, rel.item())
 
 
 def test_fused_lstm_module_matches_torch_lstm_cpu():
