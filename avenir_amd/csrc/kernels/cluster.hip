@@ -286,20 +286,28 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
   }
 }
 
-// kmeans_score_kernel: the same pass with the SCORING on the matrix cores too.  A wave owns a
-// 64-row tile; lane l loads rows r0 + 16 s + (l & 15), dims 16 b + 4 (l >> 4) .. +3 as one float4
-// per (16-row sub-tile s, 16-dim block b) — each load instruction reads 16 contiguous rows (1 KiB),
-// fully coalesced.  Those registers ARE the B operand of v_mfma_f32_16x16x4_f32 for the product
-// x . c over a permuted reduction index (step m of block b sums dims 16 b + 4 k + m over k, the A
-// operand holds the centroids in the same order, loaded once per workgroup), so a sub-tile x
-// centroid-block product is 4 DB MFMAs and lane l receives the dot products of row 16 s + (l & 15)
-// with centroids 16 cb + 4 (l >> 4) + q.  The per-run argmin (||c||^2 - 2 x.c, ties to the lower
-// centroid) is a float compare / select per (row, centroid) pair plus two cross-row-group swaps
-// (v_permlane32_swap, v_permlane16_swap) — instead of 8 packed FMAs per pair on the VALU.  SSE
-// adds the tile's ||x||^2 once (the same for every run) instead of per-row norms.  The partial
-// sums stay the one-hot MFMA of kmeans_mfma_kernel; MR = 1 keeps one run's SSE / argmin state
-// (the common case) and frees the registers of 16 (occupancy).
-template <int D, int KBLK, int MR>
+// kmeans_score_kernel: the same pass with the SCORING on the matrix cores too (one run, R = 1: the
+// job's k-means; batched runs keep kmeans_mfma_kernel).  A wave owns a 64-row tile; lane l = 16 g + c
+// loads rows r0 + 16 s + c, dims 16 b + 4 g .. +3 as one float4 per (16-row sub-tile s, 16-dim
+// block b) — each load instruction reads 16 contiguous rows (1 KiB), fully coalesced.  Per tile:
+//   * scoring: those registers ARE the B operand of v_mfma_f32_16x16x4_f32 for x . c over a
+//     permuted reduction index (step m of block b sums dims 16 b + 4 k + m; the A operand holds the
+//     centroids in the same order).  The accumulators START at -||c||^2 / 2, so each MFMA chain
+//     yields s'(x, c) = x . c - ||c||^2 / 2 = -(||c||^2 - 2 x.c) / 2 with no epilogue arithmetic; 4
+//     sub-tiles x centroid blocks are independent chains issued back to back;
+//   * a 4 x 4 register transpose across the row groups — 8 v_permlane32_swap + 8 v_permlane16_swap
+//     per 16 centroids, no copies — leaves lane l holding ALL the centroid scores of ITS row
+//     r0 + l in a fixed register order (register 4 j + q = centroid 16 cb + 4 j + q);
+//   * the argmax of s' is then a strict-> scan in ascending centroid order inside the lane (ties go
+//     to the lower centroid, as a sequential scan); the row's squared distance to it is -2 s' + ||x||^2
+//     (SSE adds the tile's ||x||^2 once);
+//   * partial sums: the one-hot MFMA of kmeans_mfma_kernel with reduction step s over rows 16 g + s,
+//     so the one-hot operand of 4 steps is ONE 16-byte LDS read of the assignments, and the
+//     row-major staging tile is padded (row stride DP + 4, 16 floats per 16-row group) against
+//     LDS bank conflicts.
+// Two register tiles alternate (explicit ping-pong, no copies) so the next tile's loads are in
+// flight during this one's work.
+template <int D, int KBLK>
 __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restrict__ X, long long n,
                                                           const float* __restrict__ C2, const float* __restrict__ Cn,
                                                           const int* __restrict__ roff, int R, int K,
@@ -307,22 +315,24 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
                                                           double* __restrict__ sse_partial) {
   constexpr int DP = D < 16 ? 16 : D;  // staged row width of the partial-sum tile
   constexpr int DB = DP / 16;          // 16-dim blocks
+  constexpr int RS = DP + 4;           // padded row stride of the staging tile
+  constexpr int XS = 64 * RS + 64;     // floats per wave
   extern __shared__ float lds[];
-  float* xs_all = lds;                                                 // [4 waves][64][DP]
-  int* asg_all = reinterpret_cast<int*>(xs_all + 4 * 64 * DP);         // [4 waves][64][R]
-  unsigned* cnt = reinterpret_cast<unsigned*>(asg_all + 4 * 64 * R);   // [K]
+  float* xs_all = lds;                                                 // [4 waves][XS]
+  int* asg_all = reinterpret_cast<int*>(xs_all + 4 * XS);              // [4 waves][64]
+  unsigned* cnt = reinterpret_cast<unsigned*>(asg_all + 4 * 64);       // [K]
   float* red = reinterpret_cast<float*>(cnt + K);                      // [K][D]
-  __shared__ double sred[4][MR];
-  __shared__ int s_off[MAX_RUNS + 1];
+  __shared__ double sred[4];
   for (int i = threadIdx.x; i < K; i += KB) cnt[i] = 0u;
   for (int i = threadIdx.x; i < K * D; i += KB) red[i] = 0.f;
-  for (int i = threadIdx.x; i <= R; i += KB) s_off[i] = roff[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
-  float* xs = xs_all + w * 64 * DP;
-  int* asg = asg_all + w * 64 * R;
-  // scoring A operand: centroid 16 cb + col, dim 16 b + 4 grp + m; ||c||^2 of the lane's 4 result rows
-  float ac[KBLK][DB][4], cn[KBLK][4];
+  float* xs = xs_all + w * XS;
+  int* asg = asg_all + w * 64;
+  // scoring A operand: centroid 16 cb + col, dim 16 b + 4 grp + m; accumulator start -||c||^2 / 2 of
+  // the lane's 4 result rows (centroids 16 cb + 4 grp + q; -inf past K: never the argmax)
+  float ac[KBLK][DB][4];
+  f32x4 cinit[KBLK];
 #pragma unroll
   for (int cb = 0; cb < KBLK; ++cb) {
     const int c = cb * 16 + col;
@@ -336,21 +346,13 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int cq = cb * 16 + 4 * grp + q;
-      cn[cb][q] = cq < K ? Cn[cq] : INFINITY;
+      cinit[cb][q] = cq < K ? -0.5f * Cn[cq] : -INFINITY;
     }
   }
-  // partial-sum A operand (one-hot of the assignments), as in kmeans_mfma_kernel
-  float a_centf[KBLK];
-  int a_runc[KBLK];
+  // partial-sum A operand: lane supplies one-hot[centroid 16 cb + col][row]
+  int a_cent[KBLK];
 #pragma unroll
-  for (int cb = 0; cb < KBLK; ++cb) {
-    const int c = cb * 16 + col;
-    int rr = -1;
-    for (int r = 0; r < R; ++r)
-      if (c >= s_off[r] && c < s_off[r + 1]) rr = r;
-    a_centf[cb] = rr >= 0 ? (float)c : -2.f;
-    a_runc[cb] = rr >= 0 ? rr : 0;
-  }
+  for (int cb = 0; cb < KBLK; ++cb) a_cent[cb] = cb * 16 + col < K ? cb * 16 + col : -2;
   f32x4 acc[2][KBLK][DB];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -358,10 +360,7 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
     for (int cb = 0; cb < KBLK; ++cb)
 #pragma unroll
       for (int db = 0; db < DB; ++db) acc[h][cb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  double sse[MR];
-#pragma unroll
-  for (int r = 0; r < MR; ++r) sse[r] = 0.0;
-  double xsq = 0.0;  // this lane's share of sum ||x||^2 over the valid rows
+  double sse = 0.0, xsq = 0.0;
   const long long ntiles = (n + 63) / 64;
   const long long gw = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
   auto load_tile = [&](long long t, f32x4 (&v)[4][DB]) {
@@ -384,17 +383,8 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
       }
     }
   };
-  f32x4 xnext[4][DB];
-  if (gw < ntiles) load_tile(gw, xnext);
-  for (long long t = gw; t < ntiles; t += nw) {
-    f32x4 xv[4][DB];
-#pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-      for (int b = 0; b < DB; ++b) xv[sb][b] = xnext[sb][b];
-    if (t + nw < ntiles) load_tile(t + nw, xnext);  // next tile's loads in flight during this one
-    // ||x||^2 of the tile (padding rows / dims are zero)
-    float xs2 = 0.f;
+  auto body = [&](long long t, f32x4 (&xv)[4][DB]) {
+    float xs2 = 0.f;  // ||x||^2 of the tile (padding rows / dims are zero)
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
@@ -402,109 +392,104 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
 #pragma unroll
         for (int m = 0; m < 4; ++m) xs2 = fmaf(xv[sb][b][m], xv[sb][b][m], xs2);
     xsq += (double)xs2;
-    // scoring: row 16 sb + col against centroids 16 cb + 4 grp + q
-    float rbest[MR];
-    int ridx[MR];
+    // s'(row 16 sb + col, centroid 16 cb + 4 grp + q) in dot[sb][cb][q]
+    f32x4 dot[4][KBLK];
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb) {
-      float best[MR];
-      int bidx[MR];
+    for (int b = 0; b < DB; ++b)
 #pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        best[r] = INFINITY;
-        bidx[r] = r < R ? s_off[r] : 0;
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int cb = 0; cb < KBLK; ++cb)
+#pragma unroll
+          for (int sb = 0; sb < 4; ++sb)
+            dot[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[cb][b][m], xv[sb][b][m],
+                                                               (b == 0 && m == 0) ? cinit[cb] : dot[sb][cb], 0, 0, 0);
+    // transpose: afterwards dot[j][cb][q] = s'(row 16 grp + col, centroid 16 cb + 4 j + q)
+#pragma unroll
+    for (int cb = 0; cb < KBLK; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int lo = 0; lo < 2; ++lo) {  // row groups g <-> g ^ 2: pairs (0, 2), (1, 3)
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(dot[lo][cb][q]),
+                                                          __float_as_uint(dot[lo + 2][cb][q]), false, false);
+          dot[lo][cb][q] = __uint_as_float(r[0]);
+          dot[lo + 2][cb][q] = __uint_as_float(r[1]);
+        }
+#pragma unroll
+        for (int lo = 0; lo < 4; lo += 2) {  // row groups g <-> g ^ 1: pairs (0, 1), (2, 3)
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(dot[lo][cb][q]),
+                                                          __float_as_uint(dot[lo + 1][cb][q]), false, false);
+          dot[lo][cb][q] = __uint_as_float(r[0]);
+          dot[lo + 1][cb][q] = __uint_as_float(r[1]);
+        }
       }
+    float best = dot[0][0][0];
+    int bi = 0;
 #pragma unroll
-      for (int cb = 0; cb < KBLK; ++cb) {
-        f32x4 dot = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int cb = 0; cb < KBLK; ++cb)
 #pragma unroll
-        for (int b = 0; b < DB; ++b)
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-            dot = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[cb][b][m], xv[sb][b][m], dot, 0, 0, 0);
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int c = cb * 16 + 4 * grp + q;
-          const float sc = fmaf(-2.f, dot[q], cn[cb][q]);
-          if constexpr (MR == 1) {
-            if (sc < best[0]) { best[0] = sc; bidx[0] = c; }
-          } else {
-#pragma unroll
-            for (int r = 0; r < MR; ++r)
-              if (r < R && c >= s_off[r] && c < s_off[r + 1] && sc < best[r]) { best[r] = sc; bidx[r] = c; }
-          }
+          if (cb == 0 && j == 0 && q == 0) continue;
+          const float v = dot[j][cb][q];
+          const bool gt = v > best;
+          best = gt ? v : best;
+          bi = gt ? cb * 16 + 4 * j + q : bi;
         }
-      }
-      // min over the 4 row groups (lanes col, col + 16, col + 32, col + 48); ties -> lower centroid
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        if (r >= R) break;
-        {
-          const auto pv = __builtin_amdgcn_permlane32_swap(__float_as_uint(best[r]), __float_as_uint(best[r]), false, false);
-          const auto pi = __builtin_amdgcn_permlane32_swap((unsigned)bidx[r], (unsigned)bidx[r], false, false);
-          const float ov = __uint_as_float(lane < 32 ? pv[1] : pv[0]);
-          const int oi = (int)(lane < 32 ? pi[1] : pi[0]);
-          if (ov < best[r] || (ov == best[r] && oi < bidx[r])) { best[r] = ov; bidx[r] = oi; }
-        }
-        {
-          const auto pv = __builtin_amdgcn_permlane16_swap(__float_as_uint(best[r]), __float_as_uint(best[r]), false, false);
-          const auto pi = __builtin_amdgcn_permlane16_swap((unsigned)bidx[r], (unsigned)bidx[r], false, false);
-          const bool odd = (lane >> 4) & 1;
-          const float ov = __uint_as_float(odd ? pv[0] : pv[1]);
-          const int oi = (int)(odd ? pi[0] : pi[1]);
-          if (ov < best[r] || (ov == best[r] && oi < bidx[r])) { best[r] = ov; bidx[r] = oi; }
-        }
-        if (grp == sb) {  // lane l = 16 sb + col keeps its own row's result
-          rbest[r] = best[r];
-          ridx[r] = bidx[r];
-        }
-      }
-    }
     const long long row = t * 64 + lane;
     const bool ok = row < n;
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      if (r >= R) break;
-      const int bj = ridx[r];
-      if (ok) {
-        if (assign) assign[(long long)r * n + row] = bj - s_off[r];
-        sse[r] += (double)rbest[r];
-        atomicAdd(&cnt[bj], 1u);
-      }
-      asg[lane * R + r] = ok ? bj : -1;
+    if (ok) {
+      if (assign) assign[row] = bi;
+      sse += (double)(-2.f * best);
+      atomicAdd(&cnt[bi], 1u);
     }
-    // stage the tile row-major for the partial-sum MFMAs: lane writes its 4-dim pieces
+    asg[lane] = ok ? bi : -1;
+    // stage the tile row-major (padded) for the partial-sum MFMAs: lane writes its 4-dim pieces
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
       for (int b = 0; b < DB; ++b) {
         const int d = b * 16 + 4 * grp;
-        *reinterpret_cast<float4*>(xs + (sb * 16 + col) * DP + d) =
+        *reinterpret_cast<float4*>(xs + (sb * 16 + col) * RS + 16 * sb + d) =
             make_float4(xv[sb][b][0], xv[sb][b][1], xv[sb][b][2], xv[sb][b][3]);
       }
+    // wave-private strip: LDS executes one wave's instructions in order
     __builtin_amdgcn_wave_barrier();
+    const float* xr = xs + 16 * grp * RS + 16 * grp + col;  // row 16 grp, dim col
 #pragma unroll
     for (int s0 = 0; s0 < 16; s0 += 4) {
-      float a[4][KBLK], bb[4][DB];
+      const int4 a4 = *reinterpret_cast<const int4*>(asg + 16 * grp + s0);
+      const int a[4] = {a4.x, a4.y, a4.z, a4.w};
+      float bb[4][DB];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int rr = 4 * (s0 + q) + grp;
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int cb = 0; cb < KBLK; ++cb) a[q][cb] = (float)asg[rr * R + a_runc[cb]];
-#pragma unroll
-        for (int db = 0; db < DB; ++db) bb[q][db] = xs[rr * DP + db * 16 + col];
-      }
+        for (int db = 0; db < DB; ++db) bb[q][db] = xr[(s0 + q) * RS + db * 16];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int cb = 0; cb < KBLK; ++cb) {
-          const float av = a[q][cb] == a_centf[cb] ? 1.f : 0.f;
+          const float av = a[q] == a_cent[cb] ? 1.f : 0.f;
 #pragma unroll
           for (int db = 0; db < DB; ++db)
             acc[q & 1][cb][db] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bb[q][db], acc[q & 1][cb][db], 0, 0, 0);
         }
     }
     __builtin_amdgcn_wave_barrier();
+  };
+  f32x4 xa[4][DB], xb[4][DB];
+  long long t = gw;
+  if (t < ntiles) load_tile(t, xa);
+  while (t < ntiles) {
+    if (t + nw < ntiles) load_tile(t + nw, xb);
+    body(t, xa);
+    t += nw;
+    if (t >= ntiles) break;
+    if (t + nw < ntiles) load_tile(t + nw, xa);
+    body(t, xb);
+    t += nw;
   }
 #pragma unroll
   for (int cb = 0; cb < KBLK; ++cb)
@@ -515,24 +500,15 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
         const int c = cb * 16 + 4 * grp + q, d = db * 16 + col;
         if (c < K && d < D) atomicAdd(&red[c * D + d], acc[0][cb][db][q] + acc[1][cb][db][q]);
       }
-  const double xw = av::wave_sum(xsq);
-#pragma unroll
-  for (int r = 0; r < MR; ++r) {
-    if (r >= R) break;
-    const double v = av::wave_sum(sse[r]) + xw;
-    if (lane == 0) sred[w][r] = v;
-  }
+  const double v = av::wave_sum(sse) + av::wave_sum(xsq);
+  if (lane == 0) sred[w] = v;
   __syncthreads();
   float* out = partial + (long long)blockIdx.x * K * (D + 1);
   for (int i = threadIdx.x; i < K * (D + 1); i += KB) {
     const int c = i / (D + 1), d = i - c * (D + 1);
     out[i] = d < D ? red[c * D + d] : (float)cnt[c];
   }
-  for (int r = threadIdx.x; r < R; r += KB) {
-    double s = 0.0;
-    for (int q = 0; q < 4; ++q) s += sred[q][r];
-    sse_partial[(long long)blockIdx.x * R + r] = s;
-  }
+  if (threadIdx.x == 0) sse_partial[blockIdx.x] = ((sred[0] + sred[1]) + sred[2]) + sred[3];
 }
 
 // out[o] = sum_g partial[g][o] (o < KD1) and out[KD1 + r] = sum_g ssep[g][r]: 16 outputs x 64
@@ -632,9 +608,9 @@ KmVariant km_variant(int D, int K, int R) {
   // one run (R = 1: the job's k-means; batched runs keep the packed-FMA kernel, whose registers
   // grow less with R) and up to 2 blocks of 16 centroids x 16 dims of accumulators
   if (!valu_score && R == 1 && D >= 4 && KBt * (DP / 16) <= 2) {
-    const size_t lds = sizeof(float) * (4 * 64 * (size_t)DP + 4 * 64 * (size_t)R + K + (size_t)K * D);
+    const size_t lds = sizeof(float) * (4 * (64 * (size_t)(DP + 4) + 64) + 4 * 64 + K + (size_t)K * D);
 #define AVK_KMS(DD, KK) \
-  if (D == DD && KBt == KK) return {(const void*)kmeans_score_kernel<DD, KK, 1>, lds, true};
+  if (D == DD && KBt == KK) return {(const void*)kmeans_score_kernel<DD, KK>, lds, true};
     AVK_KMS(4, 1) AVK_KMS(4, 2)
     AVK_KMS(8, 1) AVK_KMS(8, 2)
     AVK_KMS(16, 1) AVK_KMS(16, 2)

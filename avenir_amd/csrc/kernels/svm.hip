@@ -1895,65 +1895,6 @@ __global__ __launch_bounds__(UPX_T) void svm_cache_fill_kernel(const avk::SvmKer
   }
 }
 
-// the same fill for any D: missing rows in groups of 16, D in LDS chunks of 64, 16 accumulators per
-// thread (x_n re-read per group from L2)
-__global__ __launch_bounds__(UPX_T) void svm_cache_fill_any_kernel(const avk::SvmKerX k, avk::SvmCache c,
-                                                                   const long long* __restrict__ ws, int N,
-                                                                   const float* __restrict__ gap, float skip) {
-  constexpr int GQ = 16, CH = 64;
-  __shared__ float s_x[GQ][CH];
-  __shared__ long long s_row[WS_Q], s_slot[WS_Q];
-  if (ws_done(gap, 0, skip)) return;
-  const int cnt = c.miss_cnt[0];
-  if (cnt == 0) return;
-  const int D = k.D;
-  for (int m = threadIdx.x; m < cnt; m += UPX_T) {
-    const int q = c.miss_q[m];
-    s_row[m] = ws[q];
-    s_slot[m] = c.ws_slot[q];
-  }
-  __syncthreads();
-  const int n = blockIdx.x * UPX_T + threadIdx.x;
-  const bool in = n < N;
-  const float* xn = k.X + (long long)(in ? n : 0) * D;
-  for (int g0 = 0; g0 < cnt; g0 += GQ) {
-    const int gn = min(GQ, cnt - g0);
-    float acc[GQ];
-#pragma unroll
-    for (int i = 0; i < GQ; ++i) acc[i] = 0.f;
-    for (int d0 = 0; d0 < D; d0 += CH) {
-      __syncthreads();
-      for (int e = threadIdx.x; e < GQ * CH; e += UPX_T) {
-        const int i = e / CH, d = e % CH;
-        s_x[i][d] = (i < gn && d0 + d < D) ? k.X[s_row[g0 + i] * D + d0 + d] : 0.f;
-      }
-      __syncthreads();
-      const int dl = min(CH, D - d0);
-      for (int d = 0; d < dl; ++d) {
-        const float xv = xn[d0 + d];
-#pragma unroll
-        for (int i = 0; i < GQ; ++i) {
-          if (k.kind == 2) {
-            const float df = s_x[i][d] - xv;
-            acc[i] = fmaf(df, df, acc[i]);
-          } else {
-            acc[i] = fmaf(s_x[i][d], xv, acc[i]);
-          }
-        }
-      }
-    }
-    if (in) {
-#pragma unroll
-      for (int i = 0; i < GQ; ++i) {
-        if (i >= gn) break;
-        const float v = k.kind == 2 ? __expf(-k.gamma * acc[i])
-                                    : kfun_dot(k.kind, acc[i], 0.f, 0.f, k.gamma, k.coef0, k.degree);
-        c.rows[s_slot[g0 + i] * N + n] = v;
-      }
-    }
-  }
-}
-
 // The same update for any D through f32 MFMA: the Q x 64 block of dot products of a workgroup (4
 // waves x 16 columns, 8 row tiles of 16 per wave) accumulates v_mfma_f32_16x16x4_f32 over D in LDS
 // chunks of 64 (working-set rows and the 64 column rows staged per chunk), then the epilogue maps
@@ -2028,6 +1969,69 @@ __global__ __launch_bounds__(UPM_T) void smo_ws_update_x_mfma_kernel(const avk::
   part += __shfl_xor(part, 16, 64);
   part += __shfl_xor(part, 32, 64);
   if (lane < 16 && n < N) G[(long long)b * ldag + n] += y[(long long)b * N + n] * part;
+}
+
+// The cache fill for any D through f32 MFMA (the tiling of smo_ws_update_x_mfma_kernel): the
+// workgroup's 64 columns x the step's missing rows (<= 128, 16-row tiles) accumulate
+// v_mfma_f32_16x16x4_f32 over D in LDS chunks of 64; the epilogue maps each dot product through
+// the kernel (RBF from the norms, as the uncached update) and writes it to the row's slot: per
+// missing row, each wave stores 16 consecutive columns.
+__global__ __launch_bounds__(UPM_T) void svm_cache_fill_mfma_kernel(const avk::SvmKerX k, avk::SvmCache c,
+                                                                    const long long* __restrict__ ws, int N,
+                                                                    const float* __restrict__ gap, float skip) {
+  __shared__ long long s_row[WS_Q], s_slot[WS_Q];
+  __shared__ float s_nq[WS_Q];
+  __shared__ float s_a[WS_Q][UPM_KC + 1];
+  __shared__ float s_b[64][UPM_KC + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (ws_done(gap, 0, skip)) return;
+  const int cnt = c.miss_cnt[0];
+  if (cnt == 0) return;
+  const int D = k.D;
+  for (int m = threadIdx.x; m < WS_Q; m += UPM_T) {
+    const bool in = m < cnt;
+    const long long r = in ? ws[c.miss_q[m]] : 0;
+    s_row[m] = r;
+    s_slot[m] = in ? c.ws_slot[c.miss_q[m]] : 0;
+    s_nq[m] = in ? k.xn[r] : 0.f;
+  }
+  const int n0 = blockIdx.x * 64;
+  const int tiles = (cnt + 15) / 16;
+  f32x4 acc[WS_Q / 16];
+#pragma unroll
+  for (int t = 0; t < WS_Q / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < D; kc += UPM_KC) {
+    __syncthreads();  // the previous chunk is consumed (first pass: s_row is written)
+    const int kw = min(UPM_KC, D - kc);
+    for (int e = threadIdx.x; e < tiles * 16 * UPM_KC; e += UPM_T) {
+      const int m = e / UPM_KC, d = e % UPM_KC;
+      s_a[m][d] = (m < cnt && d < kw) ? k.X[s_row[m] * D + kc + d] : 0.f;
+    }
+    for (int e = threadIdx.x; e < 64 * UPM_KC; e += UPM_T) {
+      const int cc = e / UPM_KC, d = e % UPM_KC;
+      s_b[cc][d] = (n0 + cc < N && d < kw) ? k.X[(long long)(n0 + cc) * D + kc + d] : 0.f;
+    }
+    __syncthreads();
+    const int col = w * 16 + (lane & 15), kq = lane >> 4;
+    for (int kk = 0; kk < kw; kk += 4) {
+      const float bv = s_b[col][kk + kq];
+#pragma unroll
+      for (int t = 0; t < WS_Q / 16; ++t)
+        if (t < tiles) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(s_a[t * 16 + (lane & 15)][kk + kq], bv, acc[t], 0, 0, 0);
+    }
+  }
+  const int n = n0 + w * 16 + (lane & 15);
+  if (n >= N) return;
+  const float nn = k.xn[n];
+#pragma unroll
+  for (int t = 0; t < WS_Q / 16; ++t) {
+    if (t >= tiles) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = t * 16 + 4 * (lane >> 4) + r;
+      if (m < cnt) c.rows[s_slot[m] * N + n] = kfun_dot(k.kind, acc[t][r], s_nq[m], nn, k.gamma, k.coef0, k.degree);
+    }
+  }
 }
 
 // K[i][j] = k(a_i, b_j) for any d by f32 MFMA: a 64 x 64 output tile per workgroup, wave w owns rows
@@ -2144,7 +2148,7 @@ void smo_ws_update_cached(const SvmKerX& k, const SvmCache& c, const long long* 
     else AV_CF(64);
 #undef AV_CF
   } else {
-    svm_cache_fill_any_kernel<<<grid, UPX_T, 0, stream>>>(k, c, ws, N, gap, skip);
+    svm_cache_fill_mfma_kernel<<<dim3((N + 63) / 64), UPM_T, 0, stream>>>(k, c, ws, N, gap, skip);
   }
   AV_HIP_CHECK(hipGetLastError());
   // the dense update reads K[ws_slot[q], n] from the cache rows

@@ -104,15 +104,18 @@ def use_implicit(n: int, n_mats: int, device) -> bool:
 
 
 #: kernel-row cache of the implicit solver: "auto" (on when recomputing a row costs more than
-#: reading it back: D >= AVMI_SVM_CACHE_MIN_D, default 64), "0" (off) or a slot count
+#: reading it back, D >= AVMI_SVM_CACHE_MIN_D (default 64), AND the cache holds at least a quarter
+#: of the rows — measured: with 4,096 slots for 65,536-262,144 rows the hit rate is 0.01-4 % and
+#: the cache only adds traffic), "0" (off) or a slot count
 ROW_CACHE = __import__("os").environ.get("AVMI_SVM_CACHE", "auto")
 ROW_CACHE_MIN_D = int(__import__("os").environ.get("AVMI_SVM_CACHE_MIN_D", "64"))
 
 
 def row_cache_slots(K: "ImplicitKernel", B: int) -> int:
     """Slots of the HBM kernel-row cache (svm.hip svm_cache_lookup_kernel) for an implicit-kernel
-    solve: 0 when off (several problems, per-problem X, small D under "auto"); else up to 4,096
-    rows, sized to a quarter of the device's free memory (one slot = N fp32 values).  Every outer
+    solve: 0 when off (several problems, per-problem X; under "auto" small D or fewer than N / 4
+    slots); else up to 16,384 rows ("auto": N / 2), within a quarter of the device's free memory
+    (one slot = N fp32 values).  Every outer
     step the working set's rows come from the cache (LRU within 8-way sets) and only the misses are
     recomputed from X — the reference's SMO memoises kernel values the same way
     (J/discriminant/SequentialMinimalOptimization.java:511-524)."""
@@ -124,10 +127,14 @@ def row_cache_slots(K: "ImplicitKernel", B: int) -> int:
     D = int(K.X.shape[-1])
     if mode == "auto" and D < ROW_CACHE_MIN_D:
         return 0
-    want = 4096 if mode in ("auto", "on", "1", "true") else int(mode)
+    N = K.N
+    want = (N + 1) // 2 if mode in ("auto", "on", "1", "true") else int(mode)
     free, _ = torch.cuda.mem_get_info(K.device)
-    fit = int(0.25 * free // (4 * K.N)) - 128
-    return max(0, min(want, fit, 16384)) // 8 * 8
+    fit = int(0.25 * free // (4 * N)) - 128
+    slots = max(0, min(want, fit, 16384)) // 8 * 8
+    if mode == "auto" and 4 * slots < N:
+        return 0
+    return slots
 
 
 def smo_reference(K: np.ndarray, y: np.ndarray, C: float, eps: float = 1e-3, max_iter: int = 100000,

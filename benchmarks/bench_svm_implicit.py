@@ -23,10 +23,18 @@ from avenir_amd.models import svm as S  # noqa: E402
 
 
 def problem(N, d, seed=9):
+    """XOR labels.  d <= 16: on two of d standard-normal features (the earlier profiles' problem);
+    wider: the rows lie near an 8-dimensional subspace (X = Z A + 0.1 noise) and the label is the
+    XOR of two latent coordinates, so an RBF kernel on all d features can learn it."""
     g = torch.Generator(device="cuda").manual_seed(seed)
-    X = torch.randn((N, d), device="cuda", generator=g)
-    y = (X[:, 0] * X[:, 1] > 0).long()
-    return X, y
+    if d <= 16:
+        X = torch.randn((N, d), device="cuda", generator=g)
+        return X, (X[:, 0] * X[:, 1] > 0).long()
+    ga = torch.Generator(device="cuda").manual_seed(1234)       # one subspace for train and test
+    A = torch.randn((8, d), device="cuda", generator=ga) / 8 ** 0.5
+    Z = torch.randn((N, 8), device="cuda", generator=g)
+    X = Z @ A + 0.1 * torch.randn((N, d), device="cuda", generator=g)
+    return X, (Z[:, 0] * Z[:, 1] > 0).long()
 
 
 def fit(X, y, path, gamma):
@@ -51,11 +59,12 @@ def main() -> int:
     ap.add_argument("--cache", default=None, help="kernel-row cache: auto | 0 | slots (models/svm.py ROW_CACHE)")
     ap.add_argument("--sklearn-sub", type=int, default=0,
                     help="also fit sklearn on a random subsample of this many rows and compare held-out accuracy")
+    ap.add_argument("--gamma", type=float, default=0.5)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     if args.cache is not None:
         S.ROW_CACHE = args.cache
-    gamma = 0.5
+    gamma = args.gamma
     Xw, yw = problem(512, args.d)
     for path in args.paths.split(","):
         fit(Xw, yw, path, gamma)                     # warm-up: kernels, graphs, allocator
