@@ -3639,7 +3639,8 @@ std::vector<at::Tensor> ref_split_score(const at::Tensor& hist, const at::Tensor
 }
 
 // One launch re-lays an fp32 layer's parameters (rnn_f32.hip lstm_pack_f32_kernel): w_ih [4H, I],
-// w_hh [4H, H], b_ih / b_hh [4H] or None -> wfrag [NW,4,HP/4,64], wfragT [NW,HP,64], wihk [4HP, I], biask [4HP].
+// w_hh [4H, H], b_ih / b_hh [4H] or None -> wfrag [NW,4,HP/4,64], wfragT [NW,HP,64], wihk [4HP, I], biask [4HP],
+// wxfrag [NW,4,2,64] (I <= 8; empty otherwise).
 std::vector<at::Tensor> lstm_pack_f32(const at::Tensor& w_ih, const at::Tensor& w_hh,
                                       const c10::optional<at::Tensor>& b_ih, const c10::optional<at::Tensor>& b_hh) {
   CHECK_DEV(w_ih);
@@ -3657,43 +3658,70 @@ std::vector<at::Tensor> lstm_pack_f32(const at::Tensor& w_ih, const at::Tensor& 
   auto f32 = w_hh.options();
   auto wfrag = at::empty({2 * KS, 4, HP / 4, 64}, f32), wfragT = at::empty({2 * KS, HP, 64}, f32);
   auto wihk = at::empty({4 * HP, I}, f32), biask = at::empty({4 * HP}, f32);
+  // W_ih fragments of the in-kernel projection (narrow inputs only)
+  auto wxfrag = I <= 8 ? at::empty({2 * KS, 4, 2, 64}, f32) : at::empty({0}, f32);
   avk::lstm_pack_f32(w_ih.data_ptr<float>(), w_hh.data_ptr<float>(), ptr_or_null<float>(b_ih), ptr_or_null<float>(b_hh),
                      (int)H, (int)I, (int)KS, wfrag.data_ptr<float>(), wfragT.data_ptr<float>(), wihk.data_ptr<float>(),
-                     biask.data_ptr<float>(), cur_stream(w_hh));
-  return {wfrag, wfragT, wihk, biask};
+                     biask.data_ptr<float>(), I <= 8 ? wxfrag.data_ptr<float>() : nullptr, cur_stream(w_hh));
+  return {wfrag, wfragT, wihk, biask, wxfrag};
 }
 
-// fp32 recurrence (rnn_f32.hip): xw [B, T, 4HP] fp32 kernel order (input projection + biases);
-// wfrag [NW, 4, HP/4, 64] fp32.  Returns hseq [B,T,H], cseq [B,T,HP] (+ gates [B,T,4HP] fp32 and
-// hprev [B,T,H] = h_{t-1} when training).
-std::vector<at::Tensor> lstm_forward_f32(const at::Tensor& xw, const at::Tensor& wfrag,
+// fp32 recurrence (rnn_f32.hip).  Input: xw [B, T, 4HP] fp32 kernel order (input projection + biases)
+// OR, for I <= 8, (x [B, T, I], wxfrag, biask) and the projection runs in the kernel; x is also needed
+// when training (the [h_{t-1} | x_t | 1] rows).  wfrag [NW, 4, HP/4, 64] fp32.  Returns hseq [B,T,H],
+// cseq [B,T,HP] (+ gates [B,T,4HP] fp32 and hx [B,T,H+I+1] when training).
+std::vector<at::Tensor> lstm_forward_f32(const c10::optional<at::Tensor>& xw, const at::Tensor& wfrag,
                                          const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
-                                         int64_t H, bool training) {
+                                         int64_t H, bool training, const c10::optional<at::Tensor>& x,
+                                         const c10::optional<at::Tensor>& wxfrag,
+                                         const c10::optional<at::Tensor>& biask) {
   const int64_t KS = lstm_ks(H), HP = 32 * KS;
-  CHECK_DEV(xw);
-  CHECK_DTYPE(xw, at::kFloat);
-  TORCH_CHECK(xw.dim() == 3 && xw.size(2) == 4 * HP && xw.is_contiguous(), "xw must be [B, T, 4HP] contiguous");
-  TORCH_CHECK(aligned(xw, 16), "xw must be 16-byte aligned");
-  const int64_t B = xw.size(0), T = xw.size(1);
+  const bool has_xw = xw.has_value() && xw->defined(), has_x = x.has_value() && x->defined();
+  TORCH_CHECK(has_xw || has_x, "lstm_forward_f32: xw or x required");
+  TORCH_CHECK(!training || has_x, "lstm_forward_f32: training needs x");
+  int64_t B, T, I = 0;
+  if (has_x) {
+    CHECK_DEV((*x));
+    CHECK_DTYPE((*x), at::kFloat);
+    TORCH_CHECK(x->dim() == 3 && x->is_contiguous(), "x must be [B, T, I] contiguous");
+    B = x->size(0), T = x->size(1), I = x->size(2);
+  }
+  if (has_xw) {
+    CHECK_DEV((*xw));
+    CHECK_DTYPE((*xw), at::kFloat);
+    TORCH_CHECK(xw->dim() == 3 && xw->size(2) == 4 * HP && xw->is_contiguous(), "xw must be [B, T, 4HP] contiguous");
+    TORCH_CHECK(aligned(*xw, 16), "xw must be 16-byte aligned");
+    TORCH_CHECK(!has_x || (xw->size(0) == B && xw->size(1) == T), "xw / x shapes differ");
+    B = xw->size(0), T = xw->size(1);
+  } else {
+    TORCH_CHECK(I >= 1 && I <= 8, "in-kernel projection needs 1 <= I <= 8");
+    TORCH_CHECK(wxfrag.has_value() && wxfrag->defined() && biask.has_value() && biask->defined(),
+                "in-kernel projection needs wxfrag and biask");
+    check_opt_f32(wxfrag, 2 * KS * 4 * 2 * 64, "wxfrag");
+    check_opt_f32(biask, 4 * HP, "biask");
+    TORCH_CHECK(aligned(*biask, 16), "biask must be 16-byte aligned");
+  }
   TORCH_CHECK(B >= 1 && T >= 1, "empty LSTM input");
   CHECK_DEV(wfrag);
   CHECK_DTYPE(wfrag, at::kFloat);
   TORCH_CHECK(wfrag.numel() == 2 * KS * 4 * (HP / 4) * 64, "wfrag must be [NW, 4, HP/4, 64]");
   check_opt_f32(h0, B * H, "h0");
   check_opt_f32(c0, B * H, "c0");
-  DevGuard g(xw.device());
-  auto f32 = xw.options();
+  DevGuard g(wfrag.device());
+  auto f32 = wfrag.options();
   auto hseq = at::empty({B, T, H}, f32), cseq = at::empty({B, T, HP}, f32);
-  at::Tensor gates, hprev;
+  at::Tensor gates, hx;
   if (training) {
     gates = at::empty({B, T, 4 * HP}, f32);
-    hprev = at::empty({B, T, H}, f32);
+    hx = at::empty({B, T, H + I + 1}, f32);
   }
-  avk::lstm_fwd_f32(xw.data_ptr<float>(), wfrag.data_ptr<float>(), ptr_or_null<float>(h0), ptr_or_null<float>(c0),
-                    (int)B, (int)T, (int)H, (int)KS, hseq.data_ptr<float>(), cseq.data_ptr<float>(),
-                    training ? gates.data_ptr<float>() : nullptr, training ? hprev.data_ptr<float>() : nullptr,
-                    cur_stream(xw));
-  if (training) return {hseq, cseq, gates, hprev};
+  avk::lstm_fwd_f32(has_xw ? xw->data_ptr<float>() : nullptr, has_x ? x->data_ptr<float>() : nullptr,
+                    has_xw ? nullptr : wxfrag->data_ptr<float>(), has_xw ? nullptr : biask->data_ptr<float>(),
+                    wfrag.data_ptr<float>(), ptr_or_null<float>(h0), ptr_or_null<float>(c0), (int)B, (int)T, (int)H,
+                    (int)I, (int)KS, hseq.data_ptr<float>(), cseq.data_ptr<float>(),
+                    training ? gates.data_ptr<float>() : nullptr, training ? hx.data_ptr<float>() : nullptr,
+                    cur_stream(wfrag));
+  if (training) return {hseq, cseq, gates, hx};
   return {hseq, cseq};
 }
 
@@ -3866,7 +3894,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_ks", &lstm_ks);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);
-  m.def("lstm_forward_f32", &lstm_forward_f32);
+  m.def("lstm_forward_f32", &lstm_forward_f32, py::arg("xw"), py::arg("wfrag"), py::arg("h0"), py::arg("c0"),
+        py::arg("H"), py::arg("training"), py::arg("x") = py::none(), py::arg("wxfrag") = py::none(),
+        py::arg("biask") = py::none());
   m.def("lstm_pack_f32", &lstm_pack_f32);
   m.def("ref_split_score", &ref_split_score);
   m.def("lstm_backward_f32", &lstm_backward_f32);

@@ -184,10 +184,11 @@ void ref_split_score(const long long* hist, int A, int C, int TBt, const int* sp
                      double* segc, double* cinfo, double* scratch, hipStream_t stream);
 
 // ---- rnn_f32.hip (K27 fp32) ------------------------------------------------------------------
-void lstm_fwd_f32(const float* xw, const float* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
-                  float* hseq, float* cseq, float* gates, float* hprev, hipStream_t s);
+void lstm_fwd_f32(const float* xw, const float* x, const float* wxfrag, const float* biask, const float* wfrag,
+                  const float* h0, const float* c0, int B, int T, int H, int I, int KS, float* hseq, float* cseq,
+                  float* gates, float* hx, hipStream_t s);
 void lstm_pack_f32(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, int H, int I, int KS,
-                   float* wfrag, float* wfragT, float* wihk, float* biask, hipStream_t s);
+                   float* wfrag, float* wfragT, float* wihk, float* biask, float* wxfrag, hipStream_t s);
 void lstm_bwd_f32(const float* dhseq, const float* gates, const float* cseq, const float* c0, const float* dhn,
                   const float* dcn, const float* wfragT, int B, int T, int H, int KS, float* dz, float* dh0,
                   float* dc0, hipStream_t s);

@@ -305,10 +305,10 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
 //     so the one-hot operand of 4 steps is ONE 16-byte LDS read of the assignments, and the
 //     row-major staging tile is padded (row stride DP + 4, 16 floats per 16-row group) against
 //     LDS bank conflicts.
-// Two register tiles alternate (explicit ping-pong, no copies) so the next tile's loads are in
-// flight during this one's work.
+// Three register tiles rotate (no copies) so the next two tiles' loads are in flight during this
+// one's work.
 template <int D, int KBLK>
-__global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restrict__ X, long long n,
+__global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? 3 : 2) void kmeans_score_kernel(const float* __restrict__ X, long long n,
                                                           const float* __restrict__ C2, const float* __restrict__ Cn,
                                                           const int* __restrict__ roff, int R, int K,
                                                           int* __restrict__ assign, float* __restrict__ partial,
@@ -479,16 +479,23 @@ __global__ __launch_bounds__(KB) void kmeans_score_kernel(const float* __restric
     }
     __builtin_amdgcn_wave_barrier();
   };
-  f32x4 xa[4][DB], xb[4][DB];
+  // three register tiles in rotation: the loads of the next TWO tiles are in flight during this
+  // one's work (one tile ahead left HBM at ~3.9 TB/s: too few bytes in flight at 3 waves / SIMD)
+  f32x4 xa[4][DB], xb[4][DB], xc[4][DB];
   long long t = gw;
   if (t < ntiles) load_tile(t, xa);
+  if (t + nw < ntiles) load_tile(t + nw, xb);
   while (t < ntiles) {
-    if (t + nw < ntiles) load_tile(t + nw, xb);
+    if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xc);
     body(t, xa);
     t += nw;
     if (t >= ntiles) break;
-    if (t + nw < ntiles) load_tile(t + nw, xa);
+    if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xa);
     body(t, xb);
+    t += nw;
+    if (t >= ntiles) break;
+    if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xb);
+    body(t, xc);
     t += nw;
   }
 #pragma unroll

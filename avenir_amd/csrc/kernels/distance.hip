@@ -18,6 +18,7 @@
 // tiles.  L1 / Lp metrics run the same tile on the VALU (4 x 4 distances per thread) through an
 // LDS distance tile scanned by 4 threads per query.
 #include "avenir_common.h"
+#include <cmath>
 #include "avenir_kernels.h"
 
 namespace {
@@ -524,15 +525,21 @@ __global__ __launch_bounds__(MX_T) void mixed_knn_merge_kernel(const float* __re
 // scale) is at most ``thr`` (and j > i in global order for a self-join).  Instead of materialising
 // [tile, nB] distance blocks and compacting them with a sort / nonzero per tile, each workgroup
 // holds 64 A rows in LDS, each lane one B row in registers, and the kept pairs are appended with
-// one atomic per pair (the host sorts them by (i, j) afterwards: deterministic output).
+// one atomic per pair (the host sorts them by (i, j) afterwards: deterministic output).  Almost
+// every pair of a selective join is rejected: ``s_max`` (host-computed, an upper bound of the
+// squared distance any kept pair can have) rejects them on the squared distance alone, so the
+// division, square root and rounding of the exact test run only for candidates.  The A rows are
+// broadcast LDS reads (every lane reads the same row: no bank conflicts at any stride), 4 floats
+// per read, and 4 A rows per iteration keep 4 independent accumulations in flight.
 template <int DMAX>
 __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restrict__ A, int nA,
                                                            const float* __restrict__ B, int nB, int D, float nf,
-                                                           float scale, float thr, int tri, long long a_base,
-                                                           long long b_base, int* __restrict__ cnt, long long cap,
-                                                           long long* __restrict__ outI, long long* __restrict__ outJ,
-                                                           int* __restrict__ outD, int a_row0) {
-  __shared__ float As[64][DMAX + 1];
+                                                           float scale, float thr, float s_max, int tri,
+                                                           long long a_base, long long b_base, int* __restrict__ cnt,
+                                                           long long cap, long long* __restrict__ outI,
+                                                           long long* __restrict__ outJ, int* __restrict__ outD,
+                                                           int a_row0) {
+  __shared__ float4 As[64][DMAX / 4];
   const int a0 = a_row0 + blockIdx.y * 64;
   // self-join: a workgroup whose whole j-range lies at or below its first i keeps nothing (about
   // half the grid of a diagonal block): leave before touching memory (uniform per workgroup)
@@ -540,9 +547,10 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
     const long long j_last = b_base + min(nB, (int)(blockIdx.x + 1) * 256) - 1;
     if (j_last <= a_base + a0) return;
   }
+  float* Af = reinterpret_cast<float*>(As);
   for (int e = threadIdx.x; e < 64 * DMAX; e += 256) {   // columns D..DMAX-1 zero (b[] is zero there too)
     const int r = e / DMAX, c = e - r * DMAX;
-    As[r][c] = (a0 + r < nA && c < D) ? A[(long long)(a0 + r) * D + c] : 0.f;
+    Af[e] = (a0 + r < nA && c < D) ? A[(long long)(a0 + r) * D + c] : 0.f;
   }
   __syncthreads();
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -556,14 +564,8 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
     const long long lim = gj - a_base - a0;
     na = lim <= 0 ? 0 : (lim < na ? (int)lim : na);
   }
-  for (int r = 0; r < na; ++r) {
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < DMAX; ++c) {
-      const float d = As[r][c] - b[c];   // zero beyond D on both sides
-      s = fmaf(d, d, s);
-    }
-    const float dist = rintf(sqrtf(s) / nf * scale);   // torch.round: half to even
+  auto emit = [&](int r, float s2) {
+    const float dist = rintf(sqrtf(s2) / nf * scale);   // torch.round: half to even
     if (dist <= thr) {
       const int k = atomicAdd(cnt, 1);
       if ((long long)k < cap) {
@@ -572,6 +574,31 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
         outD[k] = (int)dist;
       }
     }
+  };
+  auto sqd = [&](int r) {
+    float s2 = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < DMAX / 4; ++c4) {
+      const float4 a = As[r][c4];   // zero beyond D on both sides
+      const float d0 = a.x - b[4 * c4], d1 = a.y - b[4 * c4 + 1], d2 = a.z - b[4 * c4 + 2], d3 = a.w - b[4 * c4 + 3];
+      s2 = fmaf(d0, d0, s2);
+      s2 = fmaf(d1, d1, s2);
+      s2 = fmaf(d2, d2, s2);
+      s2 = fmaf(d3, d3, s2);
+    }
+    return s2;
+  };
+  int r = 0;
+  for (; r + 4 <= na; r += 4) {
+    const float s0 = sqd(r), s1 = sqd(r + 1), s2 = sqd(r + 2), s3 = sqd(r + 3);
+    if (s0 <= s_max) emit(r, s0);
+    if (s1 <= s_max) emit(r + 1, s1);
+    if (s2 <= s_max) emit(r + 2, s2);
+    if (s3 <= s_max) emit(r + 3, s3);
+  }
+  for (; r < na; ++r) {
+    const float s0 = sqd(r);
+    if (s0 <= s_max) emit(r, s0);
   }
 }
 
@@ -685,16 +712,24 @@ long long pairs_within(const float* A, int nA, const float* B, int nB, int D, fl
                        int* outD, hipStream_t stream) {
   if (nA <= 0 || nB <= 0) return 0;
   if (D < 1 || D > 64) throw std::runtime_error("pairs_within: 1 <= D <= 64");
+  // a kept pair has rint(sqrt(s) / nf * scale) <= thr, so sqrt(s) / nf * scale < thr + 1 and
+  // s < ((thr + 1) nf / scale)^2; the factor 1.001 covers the fp32 evaluation of both sides
+  float s_max = INFINITY;
+  if (std::isfinite(thr) && scale > 0.f && nf > 0.f) {
+    const double bound = ((double)thr + 1.0) * (double)nf / (double)scale;
+    s_max = bound < 0.0 ? -1.f : (float)(bound * bound * 1.001);
+  }
   AV_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), stream));
   // grid.y is capped at 65535 workgroups: A is covered in row chunks of 64 x 65535
   const int CH = 64 * 65535;
   for (int a_row0 = 0; a_row0 < nA; a_row0 += CH) {
     const int rows = std::min(CH, nA - a_row0);
     const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((rows + 63) / 64));
-#define AV_PW(DM)                                                                                                  \
-  pairs_within_kernel<DM><<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, tri, a_base, b_base, cnt, cap, \
-                                                    outI, outJ, outD, a_row0)
-    if (D <= 8) AV_PW(8);
+#define AV_PW(DM)                                                                                                \
+  pairs_within_kernel<DM><<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, s_max, tri, a_base, b_base, \
+                                                    cnt, cap, outI, outJ, outD, a_row0)
+    if (D <= 4) AV_PW(4);
+    else if (D <= 8) AV_PW(8);
     else if (D <= 16) AV_PW(16);
     else if (D <= 32) AV_PW(32);
     else AV_PW(64);

@@ -34,33 +34,63 @@ __device__ __forceinline__ float tanh_(float x) {
 }
 
 // Layouts (kernel order of the 4·HP gate columns: kc = 64·w + 16·g + i for unit u = 16·w + i, gate g):
-//   xw     [B, T, 4HP] fp32, kernel order: x_t·W_ihᵀ + b_ih + b_hh (zero for padded units)
+//   xw     [B, T, 4HP] fp32, kernel order: x_t·W_ihᵀ + b_ih + b_hh (zero for padded units)  (PX = 0)
+//   x      [B, T, I] fp32 (PX = 1: the input itself, I <= 8; also copied into hx when training)
+//   wxfrag [NW][4][2][64] fp32 (PX = 1): A-fragments of W_ih, lane l of k-step s: W_ih[g·H + 16w + (l&15)][4s + (l>>4)]
+//   biask  [4HP] fp32 kernel order (PX = 1): b_ih + b_hh, the accumulators' start
 //   wfrag  [NW][4][KS4][64] fp32: A-fragment of W_hh for (wave, gate, k-step of 4), KS4 = HP / 4
 //   h0, c0 [B, H] or null;  hseq [B, T, H], cseq [B, T, HP] fp32 out
 //   gates  [B, T, 4HP] fp32 post-activation (kernel order) out or null
-//   hprev  [B, T, H] fp32 out or null: h_{t-1} at t (h0 / zeros at t = 0), the B operand rows of the
-//          backward's dW_hh GEMM, written here so the backward needs no shifted copy of hseq
-template <int KS, int RT>
-__global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __restrict__ xw,
-                                                                const float* __restrict__ wfrag,
-                                                                const float* __restrict__ h0,
-                                                                const float* __restrict__ c0, int B, int T, int H,
-                                                                float* __restrict__ hseq, float* __restrict__ cseq,
-                                                                float* __restrict__ gates, float* __restrict__ hprev) {
+//   hx     [B, T, H + I + 1] fp32 out or null: [h_{t-1} | x_t | 1] (h0 / zeros at t = 0) — the B
+//          operand rows of the backward's ONE weight-gradient GEMM (dW_hh, dW_ih and db together)
+struct F32Fwd {
+  const float* xw;
+  const float* x;
+  const float* wxfrag;
+  const float* biask;
+  const float* wfrag;
+  const float* h0;
+  const float* c0;
+  int B, T, H, I;
+  float* hseq;
+  float* cseq;
+  float* gates;
+  float* hx;
+};
+
+// PX = 1: the input projection of a narrow input (I <= 8) runs INSIDE the recurrence as two extra
+// MFMA k-steps per gate (x_t as the B operand, W_ih fragments in 8 VGPRs), so the layer needs no
+// projection GEMM and no B·T·4HP xw tensor.
+template <int KS, int RT, int PX>
+__global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const F32Fwd a) {
   constexpr int HP = 32 * KS, KS4 = HP / 4, G4P = 4 * HP, NT = 128 * KS, LROW = HP + 1;
   __shared__ float sbuf[2][RT * 16][LROW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int col = lane & 15, quad = lane >> 4;
   const int u0 = 16 * w + 4 * quad, kc0 = 64 * w + 4 * quad;
+  const int B = a.B, T = a.T, H = a.H, I = a.I;
   const long long row0 = (long long)blockIdx.x * (RT * 16);
-  const long long TG = (long long)T * G4P, THP = (long long)T * HP, TH = (long long)T * H;
+  const long long TG = (long long)T * G4P, THP = (long long)T * HP, TH = (long long)T * H, TI = (long long)T * I;
+  const int HXS = H + I + 1;
+  const long long THX = (long long)T * HXS;
   const bool vec_h = (H & 3) == 0;
+  float* __restrict__ hx = a.hx;
 
   float wf[4][KS4];
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int s = 0; s < KS4; ++s) wf[g][s] = wfrag[((w * 4 + g) * KS4 + s) * 64 + lane];
+    for (int s = 0; s < KS4; ++s) wf[g][s] = a.wfrag[((w * 4 + g) * KS4 + s) * 64 + lane];
+  float wx[4][2];
+  f32x4 bk[4];
+  if constexpr (PX) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) wx[g][s] = a.wxfrag[((w * 4 + g) * 2 + s) * 64 + lane];
+      bk[g] = *reinterpret_cast<const f32x4*>(a.biask + kc0 + 16 * g);
+    }
+  }
 
   int lrow[RT];
   bool rok[RT];
@@ -74,23 +104,38 @@ __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __r
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool ok = u0 + r < H;
-      c[rt][r] = (ok && c0) ? c0[grow * H + u0 + r] : 0.f;
-      const float hv = (ok && h0) ? h0[grow * H + u0 + r] : 0.f;
+      c[rt][r] = (ok && a.c0) ? a.c0[grow * H + u0 + r] : 0.f;
+      const float hv = (ok && a.h0) ? a.h0[grow * H + u0 + r] : 0.f;
       sbuf[0][lr][u0 + r] = hv;
-      if (hprev && ok && rok[rt]) hprev[grow * TH + u0 + r] = hv;
+      if (hx && ok && rok[rt]) hx[grow * THX + u0 + r] = hv;
     }
   }
-  // xw_t of this lane's four units of every gate, prefetched one step ahead
+  if (hx) {  // the [x_t | 1] columns of every step of this workgroup's rows
+    const int rows = (int)min((long long)RT * 16, (long long)B - row0), per = I + 1;
+    for (int e = tid; e < rows * T * per; e += NT) {
+      const int r = e / (T * per), rest = e - r * (T * per), t = rest / per, i = rest - t * per;
+      const long long grow = row0 + r;
+      hx[grow * THX + (long long)t * HXS + H + i] = i < I ? a.x[grow * TI + (long long)t * I + i] : 1.f;
+    }
+  }
+  // xw_t (PX = 0) or x_t (PX = 1) of this lane, prefetched one step ahead
   f32x4 xn[RT][4];
-  auto load_xw = [&](int t) {
+  float xi[RT][2];
+  auto load_in = [&](int t) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      const float* src = xw + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
+      if constexpr (PX) {
+        const float* src = a.x + (row0 + lrow[rt]) * TI + (long long)t * I;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) xn[rt][g] = *reinterpret_cast<const f32x4*>(src + 16 * g);
+        for (int s = 0; s < 2; ++s) xi[rt][s] = 4 * s + quad < I ? src[4 * s + quad] : 0.f;
+      } else {
+        const float* src = a.xw + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xn[rt][g] = *reinterpret_cast<const f32x4*>(src + 16 * g);
+      }
     }
   };
-  load_xw(0);
+  load_in(0);
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1;
@@ -98,8 +143,16 @@ __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __r
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[rt][g] = xn[rt][g];
-    if (t + 1 < T) load_xw(t + 1);
+      for (int g = 0; g < 4; ++g) {
+        if constexpr (PX) {
+          acc[rt][g] = bk[g];
+#pragma unroll
+          for (int s = 0; s < 2; ++s) acc[rt][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wx[g][s], xi[rt][s], acc[rt][g], 0, 0, 0);
+        } else {
+          acc[rt][g] = xn[rt][g];
+        }
+      }
+    if (t + 1 < T) load_in(t + 1);
 #pragma unroll
     for (int s = 0; s < KS4; ++s)
 #pragma unroll
@@ -122,24 +175,23 @@ __global__ __launch_bounds__(128 * KS) void lstm_fwd_f32_kernel(const float* __r
         sbuf[cur ^ 1][rt * 16 + col][u0 + r] = hn[r];
       }
       if (rok[rt]) {
-        *reinterpret_cast<f32x4*>(cseq + lrow[rt] * THP + (long long)t * HP + u0 + row0 * THP) = c[rt];
-        float* hp = hseq + (row0 + lrow[rt]) * TH + (long long)t * H + u0;
-        float* pp = (hprev && t + 1 < T) ? hprev + (row0 + lrow[rt]) * TH + (long long)(t + 1) * H + u0 : nullptr;
+        *reinterpret_cast<f32x4*>(a.cseq + lrow[rt] * THP + (long long)t * HP + u0 + row0 * THP) = c[rt];
+        float* hp = a.hseq + (row0 + lrow[rt]) * TH + (long long)t * H + u0;
         if (vec_h) {
-          if (u0 < H) {
-            *reinterpret_cast<f32x4*>(hp) = hn;
-            if (pp) *reinterpret_cast<f32x4*>(pp) = hn;
-          }
+          if (u0 < H) *reinterpret_cast<f32x4*>(hp) = hn;
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (u0 + r < H) {
-              hp[r] = hn[r];
-              if (pp) pp[r] = hn[r];
-            }
+            if (u0 + r < H) hp[r] = hn[r];
         }
-        if (gates) {
-          float* gp = gates + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
+        if (hx && t + 1 < T) {
+          float* pp = hx + (row0 + lrow[rt]) * THX + (long long)(t + 1) * HXS + u0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (u0 + r < H) pp[r] = hn[r];
+        }
+        if (a.gates) {
+          float* gp = a.gates + (row0 + lrow[rt]) * TG + (long long)t * G4P + kc0;
           *reinterpret_cast<f32x4*>(gp) = ig;
           *reinterpret_cast<f32x4*>(gp + 16) = fg;
           *reinterpret_cast<f32x4*>(gp + 32) = gg;
@@ -297,14 +349,17 @@ __global__ __launch_bounds__(128 * KS) void lstm_bwd_f32_kernel(
 //   wfragT [NW][HP][64]       backward A-fragments of W_hhᵀ (k = 4s + (l>>4) over the gate-major 4·HP rows)
 //   wihk   [4HP, I]           W_ih rows in kernel gate order (the input-projection GEMM's operand)
 //   biask  [4HP]              b_ih + b_hh in kernel gate order
-// Padded units / columns are zero.  Flat grid-stride over the four outputs.
+//   wxfrag [NW][4][2][64]     (I <= 8, else null) W_ih A-fragments of the in-kernel projection
+// Padded units / columns are zero.  Flat grid-stride over the outputs.
 __global__ __launch_bounds__(256) void lstm_pack_f32_kernel(const float* __restrict__ w_ih,
                                                             const float* __restrict__ w_hh,
                                                             const float* __restrict__ b_ih,
                                                             const float* __restrict__ b_hh, int H, int I, int HP,
                                                             float* __restrict__ wfrag, float* __restrict__ wfragT,
-                                                            float* __restrict__ wihk, float* __restrict__ biask) {
-  const long long n1 = 4LL * HP * HP, n3 = 4LL * HP * I, n = 2 * n1 + n3 + 4 * HP;
+                                                            float* __restrict__ wihk, float* __restrict__ biask,
+                                                            float* __restrict__ wxfrag) {
+  const long long n1 = 4LL * HP * HP, n3 = 4LL * HP * I, n5 = wxfrag ? (long long)(HP / 16) * 4 * 2 * 64 : 0;
+  const long long n = 2 * n1 + n3 + 4 * HP + n5;
   const int KS4 = HP / 4;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     if (e < n1) {
@@ -320,6 +375,13 @@ __global__ __launch_bounds__(256) void lstm_pack_f32_kernel(const float* __restr
       const int s = (int)(rest % HP), w = (int)(rest / HP);
       const int k = 4 * s + (lane >> 4), g = k / HP, uu = k % HP, cu = 16 * w + (lane & 15);
       wfragT[f] = (uu < H && cu < H) ? w_hh[(long long)(g * H + uu) * H + cu] : 0.f;
+    } else if (e >= 2 * n1 + n3 + 4 * HP) {
+      const long long f = e - (2 * n1 + n3 + 4 * HP);
+      const int lane = (int)(f & 63);
+      const long long rest = f >> 6;
+      const int s = (int)(rest & 1), g = (int)((rest >> 1) & 3), w = (int)(rest >> 3);
+      const int u = 16 * w + (lane & 15), k = 4 * s + (lane >> 4);
+      wxfrag[f] = (u < H && k < I) ? w_ih[(long long)(g * H + u) * I + k] : 0.f;
     } else {
       const long long f = e - 2 * n1;
       const int kc = f < n3 ? (int)(f / I) : (int)(f - n3);
@@ -341,25 +403,32 @@ __global__ __launch_bounds__(256) void lstm_pack_f32_kernel(const float* __restr
 namespace avk {
 
 void lstm_pack_f32(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, int H, int I, int KS,
-                   float* wfrag, float* wfragT, float* wihk, float* biask, hipStream_t s) {
+                   float* wfrag, float* wfragT, float* wihk, float* biask, float* wxfrag, hipStream_t s) {
   const int HP = 32 * KS;
-  const long long n = 8LL * HP * HP + 4LL * HP * I + 4LL * HP;
+  const long long n = 8LL * HP * HP + 4LL * HP * I + 4LL * HP + (wxfrag ? (HP / 16) * 4 * 2 * 64 : 0);
   const int grid = (int)std::min<long long>((n + 255) / 256, 2048);
-  lstm_pack_f32_kernel<<<grid, 256, 0, s>>>(w_ih, w_hh, b_ih, b_hh, H, I, HP, wfrag, wfragT, wihk, biask);
+  lstm_pack_f32_kernel<<<grid, 256, 0, s>>>(w_ih, w_hh, b_ih, b_hh, H, I, HP, wfrag, wfragT, wihk, biask, wxfrag);
   AV_HIP_CHECK(hipGetLastError());
 }
 
 // RT = 1 throughout: the f32 weight fragments take HP (forward) / 4·HP/4 (backward) VGPRs per
 // lane, leaving no room for a second tile's accumulators at HP = 128.
-void lstm_fwd_f32(const float* xw, const float* wfrag, const float* h0, const float* c0, int B, int T, int H, int KS,
-                  float* hseq, float* cseq, float* gates, float* hprev, hipStream_t s) {
+void lstm_fwd_f32(const float* xw, const float* x, const float* wxfrag, const float* biask, const float* wfrag,
+                  const float* h0, const float* c0, int B, int T, int H, int I, int KS, float* hseq, float* cseq,
+                  float* gates, float* hx, hipStream_t s) {
   const int grid = (B + 15) / 16;
+  const F32Fwd a{xw, x, wxfrag, biask, wfrag, h0, c0, B, T, H, I, hseq, cseq, gates, hx};
+  const bool px = xw == nullptr;
+  if (px && (I > 8 || !x || !wxfrag || !biask)) throw std::runtime_error("lstm_fwd_f32: in-kernel projection needs I <= 8");
+#define AV_LF(KS_, NT_) \
+  (px ? lstm_fwd_f32_kernel<KS_, 1, 1><<<grid, NT_, 0, s>>>(a) : lstm_fwd_f32_kernel<KS_, 1, 0><<<grid, NT_, 0, s>>>(a))
   switch (KS) {
-    case 1: lstm_fwd_f32_kernel<1, 1><<<grid, 128, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates, hprev); break;
-    case 2: lstm_fwd_f32_kernel<2, 1><<<grid, 256, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates, hprev); break;
-    case 4: lstm_fwd_f32_kernel<4, 1><<<grid, 512, 0, s>>>(xw, wfrag, h0, c0, B, T, H, hseq, cseq, gates, hprev); break;
+    case 1: AV_LF(1, 128); break;
+    case 2: AV_LF(2, 256); break;
+    case 4: AV_LF(4, 512); break;
     default: throw std::runtime_error("lstm_fwd_f32: KS in {1, 2, 4}");
   }
+#undef AV_LF
   AV_HIP_CHECK(hipGetLastError());
 }
 

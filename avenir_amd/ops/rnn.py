@@ -21,9 +21,11 @@ on the GPU; that path is selected by shape, never by a missing extension.
 ``nn.LSTM``) runs the fp32 twin of the kernels (csrc/kernels/rnn_f32.hip): the recurrence on
 v_mfma_f32_16x16x4_f32 with W_hh resident in VGPRs as f32 fragments, every stored intermediate
 fp32, and the input projection x·W_ihᵀ + b of all timesteps as one fp32 GEMM ahead of it (the f32
-fragments of W_hh alone take HP VGPRs); one ``lstm_pack_f32`` launch re-lays the parameters per
-optimizer step.  Backward: one fp32 recurrence launch writing dz in torch gate order + fp32 GEMMs
-for dW_hh = dzᵀ·h_{t-1} (rows written by the forward), dW_ih = dzᵀ·x, db = Σdz and dx = dz·W_ih.  ``precision="bf16"`` opts into the
+fragments of W_hh alone take HP VGPRs) — except for inputs of <= 8 features (the reference's first
+layer), whose projection runs inside the recurrence as two extra MFMA k-steps per gate; one
+``lstm_pack_f32`` launch re-lays the parameters per optimizer step.  Backward: one fp32 recurrence
+launch writing dz in torch gate order + ONE fp32 GEMM dzᵀ·[h_{t-1} | x | 1] (rows written by the
+forward) for dW_hh, dW_ih and db together, and dx = dz·W_ih.  ``precision="bf16"`` opts into the
 mixed-precision kernel above.  Both are checked against the fp32 oracle and ``nn.LSTM``
 (tests/test_rnn.py).
 """
@@ -246,31 +248,34 @@ class _LstmLayer(torch.autograd.Function):
 
 
 class _LstmLayerF32(torch.autograd.Function):
-    """One fp32 layer.  Forward: ONE pack launch (skipped while the parameters are unchanged) + one
-    fp32 GEMM (input projection of all timesteps, kernel gate order, biases fused) + ONE recurrence
-    launch, which also writes h_{t-1} rows for the backward.  Backward: one recurrence launch that
-    writes dz in torch gate order, then fp32 GEMMs straight into the parameters' layouts
-    (dx = dz·W_ih, dW_ih = dzᵀ·x, dW_hh = dzᵀ·h_{t-1}) and one column sum for the biases — no
-    gathers, no shifted copies."""
+    """One fp32 layer.  Forward: ONE pack launch (skipped while the parameters are unchanged) + ONE
+    recurrence launch — for inputs of <= 8 features the input projection runs inside it (extra MFMA
+    k-steps), wider inputs get one fp32 projection GEMM (kernel gate order, biases fused) ahead of
+    it.  The recurrence also writes the [h_{t-1} | x_t | 1] rows for the backward.  Backward: one
+    recurrence launch writing dz in torch gate order, then ONE fp32 GEMM dzᵀ·[h_{t-1} | x | 1] for
+    dW_hh, dW_ih and the bias gradient together, and dx = dz·W_ih."""
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0, c0):
         B, T, I = x.shape
         H = w_hh.shape[1]
         HP = padded_hidden(H)
-        frag, frag_t, w_ih_k, bias = _packs_f32.get(w_ih, w_hh, b_ih, b_hh)
-        xw = torch.addmm(bias, x.reshape(B * T, I), w_ih_k.t()).view(B, T, 4 * HP)
+        frag, frag_t, w_ih_k, bias, wxfrag = _packs_f32.get(w_ih, w_hh, b_ih, b_hh)
         need = any(ctx.needs_input_grad)
-        outs = _native.C().lstm_forward_f32(xw, frag, h0, c0, H, bool(need))
+        if I <= 8:
+            outs = _native.C().lstm_forward_f32(None, frag, h0, c0, H, bool(need), x=x, wxfrag=wxfrag, biask=bias)
+        else:
+            xw = torch.addmm(bias, x.reshape(B * T, I), w_ih_k.t()).view(B, T, 4 * HP)
+            outs = _native.C().lstm_forward_f32(xw, frag, h0, c0, H, bool(need), x=x if need else None)
         hseq, cseq = outs[0], outs[1]
         if need:
-            ctx.save_for_backward(x, w_ih, cseq, outs[2], outs[3], c0, frag_t)
+            ctx.save_for_backward(w_ih, cseq, outs[2], outs[3], c0, frag_t)
         ctx.dims = (B, T, I, H)
         return hseq, hseq[:, -1], cseq[:, -1, :H]
 
     @staticmethod
     def backward(ctx, dhseq, dhn, dcn):
-        x, w_ih, cseq, gates, hprev, c0, frag_t = ctx.saved_tensors
+        w_ih, cseq, gates, hx, c0, frag_t = ctx.saved_tensors
         B, T, I, H = ctx.dims
         if dhseq is None:
             dhseq = cseq.new_zeros(B, T, H)
@@ -280,10 +285,14 @@ class _LstmLayerF32(torch.autograd.Function):
         dz2 = dz.view(B * T, 4 * H)                                    # fp32, torch gate order
         need = ctx.needs_input_grad
         dx = (dz2 @ w_ih.detach().float()).view(B, T, I) if need[0] else None
-        dw_ih = dz2.t() @ x.reshape(B * T, I) if need[1] else None
-        dw_hh = dz2.t() @ hprev.view(B * T, H) if need[2] else None
-        db = dz2.sum(0) if (need[3] or need[4]) else None
-        # the same tensor for both biases: autograd copies it when both accumulate
+        dw_ih = dw_hh = db = None
+        if any(need[1:5]):
+            dwcat = dz2.t() @ hx.view(B * T, H + I + 1)                 # [4H, H + I + 1]
+            dw_hh = dwcat[:, :H] if need[2] else None
+            dw_ih = dwcat[:, H:H + I] if need[1] else None
+            db = dwcat[:, H + I] if (need[3] or need[4]) else None
+        # views of one GEMM output (autograd lays each out like its parameter); the same bias
+        # gradient for both biases (autograd copies it when both accumulate)
         return (dx, dw_ih, dw_hh, db if need[3] else None, db if need[4] else None,
                 (dh0 if need[5] else None), (dc0 if need[6] else None))
 

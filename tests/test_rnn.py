@@ -67,13 +67,21 @@ def test_lstm_pack_f32_kernel_matches_python_packers(cuda, H, I):
     torch.manual_seed(H + I)
     w_ih, w_hh = torch.randn(4 * H, I, device=cuda), torch.randn(4 * H, H, device=cuda)
     b_ih, b_hh = torch.randn(4 * H, device=cuda), torch.randn(4 * H, device=cuda)
-    frag, frag_t, wihk, biask = _native.C().lstm_pack_f32(w_ih, w_hh, b_ih, b_hh)
+    frag, frag_t, wihk, biask, wx = _native.C().lstm_pack_f32(w_ih, w_hh, b_ih, b_hh)
     f_ref, ft_ref = rnn.pack_weights_f32(w_hh, H)
     assert torch.equal(frag, f_ref) and torch.equal(frag_t, ft_ref)
     assert torch.equal(wihk, rnn.to_kernel_order(w_ih, H))
     assert torch.equal(biask, rnn.to_kernel_order(b_ih + b_hh, H))
-    _, _, _, b1 = _native.C().lstm_pack_f32(w_ih, w_hh, None, b_hh)
+    _, _, _, b1, _ = _native.C().lstm_pack_f32(w_ih, w_hh, None, b_hh)
     assert torch.equal(b1, rnn.to_kernel_order(b_hh, H))
+    if I <= 8:   # W_ih fragments of the in-kernel projection: lane q*16 + col of k-step s holds W_ih[g*H + 16w + col, 4s + q]
+        HP = rnn.padded_hidden(H)
+        wp = torch.zeros((4, HP, 8), device=cuda)
+        wp[:, :H, :I] = w_ih.view(4, H, I)
+        ref = wp.view(4, HP // 16, 16, 2, 4).permute(1, 0, 3, 4, 2).reshape(HP // 16, 4, 2, 64)
+        assert torch.equal(wx, ref)
+    else:
+        assert wx.numel() == 0
 
 
 @pytest.mark.gpu
