@@ -13,7 +13,7 @@ larger ones run the working-set decomposition, either over that dense K or — a
 ``DENSE_MAX_N`` rows, or when K would not fit — over an IMPLICIT kernel: every outer step
 recomputes the Q x Q sub-problem block and the Q x N gradient-update rows from the rows of X
 (``smo_ws_run_x``; VALU from squared differences for d <= 64, f32 MFMA beyond), so memory is
-O(N D): N = 262 144 x 16 needs ~30 MB instead of the 275 GB N x N matrix.  For wide rows (D >= 64
+O(N D): N = 262 144 x 16 needs ~30 MB instead of the 275 GB N x N matrix.  For wide rows (D >= 256
 by default) an HBM LRU cache of kernel rows (``row_cache_slots``) serves the rows the working
 sets revisit and only the misses are recomputed.  There is no row cap: the working-set selection
 streams any N (the streaming top-k parts of svm.hip).  B problems — one-vs-rest
@@ -104,11 +104,13 @@ def use_implicit(n: int, n_mats: int, device) -> bool:
 
 
 #: kernel-row cache of the implicit solver: "auto" (on when recomputing a row costs more than
-#: reading it back, D >= AVMI_SVM_CACHE_MIN_D (default 64), AND the cache holds at least a quarter
-#: of the rows — measured: with 4,096 slots for 65,536-262,144 rows the hit rate is 0.01-4 % and
-#: the cache only adds traffic), "0" (off) or a slot count
+#: reading it back, D >= AVMI_SVM_CACHE_MIN_D (default 256), AND the cache holds at least a quarter
+#: of the rows), "0" (off) or a slot count.  Measured (profiles/r5_svm_cache_*): 16,384 rows at
+#: d = 512, 73 % hits: 0.140 s vs 0.158 s; at d = 128, 77 % hits: 0.072 s vs 0.065 s (the f32-MFMA
+#: row recompute is cheaper than the cache traffic); 4,096 slots for 65,536-262,144 rows: 0.01-4 %
+#: hits, up to 5x slower — hence the quarter-of-the-rows rule
 ROW_CACHE = __import__("os").environ.get("AVMI_SVM_CACHE", "auto")
-ROW_CACHE_MIN_D = int(__import__("os").environ.get("AVMI_SVM_CACHE_MIN_D", "64"))
+ROW_CACHE_MIN_D = int(__import__("os").environ.get("AVMI_SVM_CACHE_MIN_D", "256"))
 
 
 def row_cache_slots(K: "ImplicitKernel", B: int) -> int:
