@@ -528,10 +528,13 @@ __global__ __launch_bounds__(MX_T) void mixed_knn_merge_kernel(const float* __re
 // one atomic per pair (the host sorts them by (i, j) afterwards: deterministic output).  Almost
 // every pair of a selective join is rejected: ``s_max`` (host-computed, an upper bound of the
 // squared distance any kept pair can have) rejects them on the squared distance alone, so the
-// division, square root and rounding of the exact test run only for candidates.  The A rows are
-// broadcast LDS reads (every lane reads the same row: no bank conflicts at any stride), 4 floats
-// per read, and 4 A rows per iteration keep 4 independent accumulations in flight.
-template <int DMAX>
+// division, square root and rounding of the exact test run only for candidates.  A workgroup
+// stages AR A rows (256 for rows of <= 16 floats, else 64) so each thread scores up to AR pairs
+// per launch-and-stage (64 left the kernel dominated by workgroup overhead: 9.1 ms for 8.6e9 pairs
+// at d = 8, VALU busy 1.4 from address and staging work).  The A rows are broadcast LDS reads
+// (every lane reads the same row: no bank conflicts at any stride), 4 floats per read, and 4 A rows
+// per iteration keep 4 independent accumulations in flight.
+template <int DMAX, int AR>
 __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restrict__ A, int nA,
                                                            const float* __restrict__ B, int nB, int D, float nf,
                                                            float scale, float thr, float s_max, int tri,
@@ -539,8 +542,8 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
                                                            long long cap, long long* __restrict__ outI,
                                                            long long* __restrict__ outJ, int* __restrict__ outD,
                                                            int a_row0) {
-  __shared__ float4 As[64][DMAX / 4];
-  const int a0 = a_row0 + blockIdx.y * 64;
+  __shared__ float4 As[AR][DMAX / 4];
+  const int a0 = a_row0 + blockIdx.y * AR;
   // self-join: a workgroup whose whole j-range lies at or below its first i keeps nothing (about
   // half the grid of a diagonal block): leave before touching memory (uniform per workgroup)
   if (tri) {
@@ -548,17 +551,19 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
     if (j_last <= a_base + a0) return;
   }
   float* Af = reinterpret_cast<float*>(As);
-  for (int e = threadIdx.x; e < 64 * DMAX; e += 256) {   // columns D..DMAX-1 zero (b[] is zero there too)
+  for (int e = threadIdx.x; e < AR * DMAX; e += 256) {   // columns D..DMAX-1 zero (b[] is zero there too)
     const int r = e / DMAX, c = e - r * DMAX;
     Af[e] = (a0 + r < nA && c < D) ? A[(long long)(a0 + r) * D + c] : 0.f;
   }
   __syncthreads();
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= nB) return;
-  float b[DMAX];
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 b[DMAX / 2];   // packed pairs: the differences and squares run as v_pk_add_f32 / v_pk_fma_f32
 #pragma unroll
-  for (int c = 0; c < DMAX; ++c) b[c] = c < D ? B[(long long)j * D + c] : 0.f;
-  int na = min(64, nA - a0);
+  for (int c = 0; c < DMAX / 2; ++c)
+    b[c] = f2{2 * c < D ? B[(long long)j * D + 2 * c] : 0.f, 2 * c + 1 < D ? B[(long long)j * D + 2 * c + 1] : 0.f};
+  int na = min(AR, nA - a0);
   const long long gj = b_base + j;
   if (tri) {  // rows r with a_base + a0 + r < gj only (j > i in global order)
     const long long lim = gj - a_base - a0;
@@ -576,25 +581,25 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
     }
   };
   auto sqd = [&](int r) {
-    float s2 = 0.f;
+    f2 acc = f2{0.f, 0.f};
 #pragma unroll
     for (int c4 = 0; c4 < DMAX / 4; ++c4) {
       const float4 a = As[r][c4];   // zero beyond D on both sides
-      const float d0 = a.x - b[4 * c4], d1 = a.y - b[4 * c4 + 1], d2 = a.z - b[4 * c4 + 2], d3 = a.w - b[4 * c4 + 3];
-      s2 = fmaf(d0, d0, s2);
-      s2 = fmaf(d1, d1, s2);
-      s2 = fmaf(d2, d2, s2);
-      s2 = fmaf(d3, d3, s2);
+      const f2 d0 = f2{a.x, a.y} - b[2 * c4], d1 = f2{a.z, a.w} - b[2 * c4 + 1];
+      acc = __builtin_elementwise_fma(d0, d0, acc);
+      acc = __builtin_elementwise_fma(d1, d1, acc);
     }
-    return s2;
+    return acc.x + acc.y;
   };
   int r = 0;
   for (; r + 4 <= na; r += 4) {
     const float s0 = sqd(r), s1 = sqd(r + 1), s2 = sqd(r + 2), s3 = sqd(r + 3);
-    if (s0 <= s_max) emit(r, s0);
-    if (s1 <= s_max) emit(r + 1, s1);
-    if (s2 <= s_max) emit(r + 2, s2);
-    if (s3 <= s_max) emit(r + 3, s3);
+    if (fminf(fminf(s0, s1), fminf(s2, s3)) <= s_max) {  // one branch per 4 pairs (rarely taken)
+      if (s0 <= s_max) emit(r, s0);
+      if (s1 <= s_max) emit(r + 1, s1);
+      if (s2 <= s_max) emit(r + 2, s2);
+      if (s3 <= s_max) emit(r + 3, s3);
+    }
   }
   for (; r < na; ++r) {
     const float s0 = sqd(r);
@@ -720,21 +725,21 @@ long long pairs_within(const float* A, int nA, const float* B, int nB, int D, fl
     s_max = bound < 0.0 ? -1.f : (float)(bound * bound * 1.001);
   }
   AV_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), stream));
-  // grid.y is capped at 65535 workgroups: A is covered in row chunks of 64 x 65535
-  const int CH = 64 * 65535;
-  for (int a_row0 = 0; a_row0 < nA; a_row0 += CH) {
-    const int rows = std::min(CH, nA - a_row0);
-    const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((rows + 63) / 64));
-#define AV_PW(DM)                                                                                                \
-  pairs_within_kernel<DM><<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, s_max, tri, a_base, b_base, \
-                                                    cnt, cap, outI, outJ, outD, a_row0)
-    if (D <= 4) AV_PW(4);
-    else if (D <= 8) AV_PW(8);
-    else if (D <= 16) AV_PW(16);
-    else if (D <= 32) AV_PW(32);
-    else AV_PW(64);
-#undef AV_PW
-  }
+  // grid.y is capped at 65535 workgroups: A is covered in row chunks of AR x 65535
+  auto run = [&](auto kern, int AR) {
+    const int CH = AR * 65535;
+    for (int a_row0 = 0; a_row0 < nA; a_row0 += CH) {
+      const int rows = std::min(CH, nA - a_row0);
+      const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((rows + AR - 1) / AR));
+      kern<<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, s_max, tri, a_base, b_base, cnt, cap, outI, outJ,
+                                     outD, a_row0);
+    }
+  };
+  if (D <= 4) run(pairs_within_kernel<4, 256>, 256);
+  else if (D <= 8) run(pairs_within_kernel<8, 256>, 256);
+  else if (D <= 16) run(pairs_within_kernel<16, 256>, 256);
+  else if (D <= 32) run(pairs_within_kernel<32, 64>, 64);
+  else run(pairs_within_kernel<64, 64>, 64);
   AV_HIP_CHECK(hipGetLastError());
   int h = 0;
   AV_HIP_CHECK(hipMemcpyAsync(&h, cnt, sizeof(int), hipMemcpyDeviceToHost, stream));
