@@ -3189,7 +3189,7 @@ py::object format_columns_file_py(py::list cols_py, int64_t n, const std::string
 
 // pairs_within(A f32 [nA, D], B f32 [nB, D], nf, scale, thr, tri, a_base, b_base) -> (I, J, dist):
 // the pairs with round(|a - b| / nf * scale) <= thr (j > i in global order when ``tri``), sorted by
-// (i, j).  Counts first into a buffer sized from an estimate, re-runs once when it overflows.
+// (i, j).  Segmented output buffers sized from an estimate, re-run once when a segment overflows.
 py::tuple pairs_within(const at::Tensor& A, const at::Tensor& B, double nf, double scale, double thr, bool tri,
                        int64_t a_base, int64_t b_base) {
   CHECK_DEV(A);
@@ -3203,25 +3203,37 @@ py::tuple pairs_within(const at::Tensor& A, const at::Tensor& B, double nf, doub
   DevGuard g(A.device());
   hipStream_t stream = cur_stream(A);
   const int nA = (int)A.size(0), nB = (int)B.size(0), D = (int)A.size(1);
-  auto cnt = at::zeros({1}, A.options().dtype(at::kInt));
-  long long cap = std::max<long long>(1 << 20, ((long long)nA + nB) * 4);
+  const int S = avk::pairs_within_segments();
+  auto cnt = at::empty({avk::pairs_within_counter_ints()}, A.options().dtype(at::kInt));
+  long long seg_cap = (std::max<long long>(1 << 20, ((long long)nA + nB) * 4) + S - 1) / S;
+  std::vector<long long> counts(S);
   for (int attempt = 0; attempt < 2; ++attempt) {
-    auto I = at::empty({cap}, A.options().dtype(at::kLong));
-    auto J = at::empty({cap}, A.options().dtype(at::kLong));
-    auto Dd = at::empty({cap}, A.options().dtype(at::kInt));
-    const long long found = avk::pairs_within(A.data_ptr<float>(), nA, B.data_ptr<float>(), nB, D, (float)nf,
-                                              (float)scale, (float)thr, tri ? 1 : 0, a_base, b_base,
-                                              cnt.data_ptr<int>(), cap,
-                                              reinterpret_cast<long long*>(I.data_ptr<int64_t>()),
-                                              reinterpret_cast<long long*>(J.data_ptr<int64_t>()), Dd.data_ptr<int>(),
-                                              stream);
-    TORCH_CHECK(found >= 0 && found < (1LL << 31) - 1, "pairs_within: pair count overflows int32");
-    if (found <= cap) {
-      auto i = I.narrow(0, 0, found), j = J.narrow(0, 0, found), d = Dd.narrow(0, 0, found);
-      auto order = (i * (int64_t)std::max(nB, 1) + j).argsort();
-      return py::make_tuple(i.index({order}), j.index({order}), d.index({order}).to(at::kLong));
+    auto K = at::empty({seg_cap * S}, A.options().dtype(at::kLong));
+    auto Dd = at::empty({seg_cap * S}, A.options().dtype(at::kInt));
+    const long long mx = avk::pairs_within(A.data_ptr<float>(), nA, B.data_ptr<float>(), nB, D, (float)nf, (float)scale,
+                                           (float)thr, tri ? 1 : 0, a_base, b_base, cnt.data_ptr<int>(), seg_cap,
+                                           reinterpret_cast<long long*>(K.data_ptr<int64_t>()), Dd.data_ptr<int>(),
+                                           counts.data(), stream);
+    TORCH_CHECK(mx >= 0 && mx < (1LL << 31) - 1, "pairs_within: pair count overflows int32");
+    if (mx <= seg_cap) {
+      // the filled prefix of every segment, then one sort by key = i * nB + j
+      std::vector<at::Tensor> ks, ds;
+      for (int c = 0; c < S; ++c)
+        if (counts[c]) {
+          ks.push_back(K.narrow(0, c * seg_cap, counts[c]));
+          ds.push_back(Dd.narrow(0, c * seg_cap, counts[c]));
+        }
+      if (ks.empty()) {
+        auto e = at::empty({0}, A.options().dtype(at::kLong));
+        return py::make_tuple(e, e.clone(), e.clone());
+      }
+      auto k = at::cat(ks), d = at::cat(ds);
+      auto sorted = k.sort();
+      auto key = std::get<0>(sorted), order = std::get<1>(sorted);
+      const int64_t nb = std::max(nB, 1);
+      return py::make_tuple(key.div(nb, "floor"), key.remainder(nb), d.index({order}).to(at::kLong));
     }
-    cap = found;
+    seg_cap = mx;
   }
   TORCH_CHECK(false, "pairs_within: pair buffer overflow after resize");
   return py::make_tuple();

@@ -383,8 +383,10 @@ void sgns_step(float* Win, float* Wout, float* gIn, float* gOut, float* cIn, flo
 
 // ---- distance.hip: threshold pairs (recordSimilarity) ----------------------------------------
 long long pairs_within(const float* A, int nA, const float* B, int nB, int D, float nf, float scale, float thr, int tri,
-                       long long a_base, long long b_base, int* cnt, long long cap, long long* outI, long long* outJ,
-                       int* outD, hipStream_t stream);
+                       long long a_base, long long b_base, int* cnt, long long seg_cap, long long* outK, int* outD,
+                       long long* seg_counts, hipStream_t stream);
+int pairs_within_segments();
+int pairs_within_counter_ints();
 // ---- format.hip: output rows formatted on the device ------------------------------------------
 struct DevFmtCol {
   enum Kind : int { STR = 0, F64 = 1, I64 = 2, LIT = 3, LIST = 4, GLUE = 5, RAW = 6, FIELD = 7, TAIL = 8,

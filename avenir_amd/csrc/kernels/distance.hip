@@ -524,25 +524,29 @@ __global__ __launch_bounds__(MX_T) void mixed_knn_merge_kernel(const float* __re
 // The job keeps (i, j) pairs whose scaled, rounded euclidean distance round(sqrt(|a-b|^2) / nf *
 // scale) is at most ``thr`` (and j > i in global order for a self-join).  Instead of materialising
 // [tile, nB] distance blocks and compacting them with a sort / nonzero per tile, each workgroup
-// holds 64 A rows in LDS, each lane one B row in registers, and the kept pairs are appended with
-// one atomic per pair (the host sorts them by (i, j) afterwards: deterministic output).  Almost
-// every pair of a selective join is rejected: ``s_max`` (host-computed, an upper bound of the
-// squared distance any kept pair can have) rejects them on the squared distance alone, so the
-// division, square root and rounding of the exact test run only for candidates.  A workgroup
-// stages AR A rows (256 for rows of <= 16 floats, else 64) so each thread scores up to AR pairs
-// per launch-and-stage (64 left the kernel dominated by workgroup overhead: 9.1 ms for 8.6e9 pairs
-// at d = 8, VALU busy 1.4 from address and staging work).  The A rows are broadcast LDS reads
-// (every lane reads the same row: no bank conflicts at any stride), 4 floats per read, and 4 A rows
-// per iteration keep 4 independent accumulations in flight.
+// holds AR A rows in LDS (256 for rows of <= 16 floats, else 64), each lane one B row in registers.
+// Almost every pair of a selective join is rejected: ``s_max`` (host-computed, an upper bound of
+// the squared distance any kept pair can have) rejects them on the squared distance alone, so the
+// division, square root and rounding of the exact test run only for candidates.  The A rows are
+// broadcast LDS reads (every lane reads the same row: no bank conflicts), 4 floats per read; the
+// differences and squares are packed fp32 (v_pk_add_f32 / v_pk_fma_f32) with 4 rows in flight.
+// Kept pairs (key i * nB + j, distance) go to an LDS list with LDS atomics; at the end ONE global
+// atomic per workgroup reserves its slots in one of PW_SEGS output segments (workgroup id modulo
+// PW_SEGS, each segment's counter on its own 128-byte line).  Round 4 appended every pair with a
+// global atomic on one counter: ~800 k same-address atomics serialised at ~11 ns each were the
+// kernel's 9 ms (VALU busy 0.29 after the packed-math rewrite, the time unchanged).
+constexpr int PW_SEGS = 64, PW_CSTRIDE = 32, PW_LIST = 512;
 template <int DMAX, int AR>
 __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restrict__ A, int nA,
                                                            const float* __restrict__ B, int nB, int D, float nf,
                                                            float scale, float thr, float s_max, int tri,
                                                            long long a_base, long long b_base, int* __restrict__ cnt,
-                                                           long long cap, long long* __restrict__ outI,
-                                                           long long* __restrict__ outJ, int* __restrict__ outD,
-                                                           int a_row0) {
+                                                           long long seg_cap, long long* __restrict__ outK,
+                                                           int* __restrict__ outD, int a_row0) {
   __shared__ float4 As[AR][DMAX / 4];
+  __shared__ long long s_key[PW_LIST];
+  __shared__ int s_d[PW_LIST];
+  __shared__ int s_n, s_base;
   const int a0 = a_row0 + blockIdx.y * AR;
   // self-join: a workgroup whose whole j-range lies at or below its first i keeps nothing (about
   // half the grid of a diagonal block): leave before touching memory (uniform per workgroup)
@@ -550,33 +554,45 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
     const long long j_last = b_base + min(nB, (int)(blockIdx.x + 1) * 256) - 1;
     if (j_last <= a_base + a0) return;
   }
+  const int seg = (int)((blockIdx.y * (long long)gridDim.x + blockIdx.x) % PW_SEGS);
+  int* seg_cnt = cnt + seg * PW_CSTRIDE;
+  long long* seg_key = outK + seg * seg_cap;
+  int* seg_d = outD + seg * seg_cap;
   float* Af = reinterpret_cast<float*>(As);
   for (int e = threadIdx.x; e < AR * DMAX; e += 256) {   // columns D..DMAX-1 zero (b[] is zero there too)
     const int r = e / DMAX, c = e - r * DMAX;
     Af[e] = (a0 + r < nA && c < D) ? A[(long long)(a0 + r) * D + c] : 0.f;
   }
+  if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= nB) return;
+  const bool active = j < nB;
   typedef float f2 __attribute__((ext_vector_type(2)));
-  f2 b[DMAX / 2];   // packed pairs: the differences and squares run as v_pk_add_f32 / v_pk_fma_f32
+  f2 b[DMAX / 2];   // packed pairs
 #pragma unroll
   for (int c = 0; c < DMAX / 2; ++c)
-    b[c] = f2{2 * c < D ? B[(long long)j * D + 2 * c] : 0.f, 2 * c + 1 < D ? B[(long long)j * D + 2 * c + 1] : 0.f};
-  int na = min(AR, nA - a0);
+    b[c] = f2{active && 2 * c < D ? B[(long long)j * D + 2 * c] : 0.f,
+              active && 2 * c + 1 < D ? B[(long long)j * D + 2 * c + 1] : 0.f};
+  int na = active ? min(AR, nA - a0) : 0;
   const long long gj = b_base + j;
-  if (tri) {  // rows r with a_base + a0 + r < gj only (j > i in global order)
+  if (tri && active) {  // rows r with a_base + a0 + r < gj only (j > i in global order)
     const long long lim = gj - a_base - a0;
     na = lim <= 0 ? 0 : (lim < na ? (int)lim : na);
   }
   auto emit = [&](int r, float s2) {
     const float dist = rintf(sqrtf(s2) / nf * scale);   // torch.round: half to even
     if (dist <= thr) {
-      const int k = atomicAdd(cnt, 1);
-      if ((long long)k < cap) {
-        outI[k] = a0 + r;
-        outJ[k] = j;
-        outD[k] = (int)dist;
+      const long long key = (long long)(a0 + r) * nB + j;
+      const int k = atomicAdd(&s_n, 1);
+      if (k < PW_LIST) {
+        s_key[k] = key;
+        s_d[k] = (int)dist;
+      } else {  // the workgroup's list is full: straight to its segment
+        const int g = atomicAdd(seg_cnt, 1);
+        if ((long long)g < seg_cap) {
+          seg_key[g] = key;
+          seg_d[g] = (int)dist;
+        }
       }
     }
   };
@@ -605,6 +621,17 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
     const float s0 = sqd(r);
     if (s0 <= s_max) emit(r, s0);
   }
+  __syncthreads();
+  const int n = min(s_n, PW_LIST);
+  if (n == 0) return;  // uniform
+  if (threadIdx.x == 0) s_base = atomicAdd(seg_cnt, n);
+  __syncthreads();
+  const long long base = s_base;
+  for (int k = threadIdx.x; k < n; k += 256)
+    if (base + k < seg_cap) {
+      seg_key[base + k] = s_key[k];
+      seg_d[base + k] = s_d[k];
+    }
 }
 
 }  // namespace
@@ -710,11 +737,14 @@ void cluster_accumulate(const float* X, long long N, int D, const int* assign, i
 }
 
 
-// pairs (i, j) with round(|a_i - b_j| / nf * scale) <= thr; returns the number found (the first
-// ``cap`` are written; the caller re-runs with a larger buffer when it exceeds cap)
+// pairs (i, j) with round(|a_i - b_j| / nf * scale) <= thr, as keys i * nB + j and distances in
+// PW_SEGS segments of seg_cap entries; cnt = PW_SEGS counters PW_CSTRIDE ints apart.  Returns the
+// largest segment count (the caller re-runs with a larger seg_cap when it exceeds seg_cap) and
+// copies the counts to seg_counts[PW_SEGS] (host).
 long long pairs_within(const float* A, int nA, const float* B, int nB, int D, float nf, float scale, float thr, int tri,
-                       long long a_base, long long b_base, int* cnt, long long cap, long long* outI, long long* outJ,
-                       int* outD, hipStream_t stream) {
+                       long long a_base, long long b_base, int* cnt, long long seg_cap, long long* outK, int* outD,
+                       long long* seg_counts, hipStream_t stream) {
+  for (int c = 0; c < PW_SEGS; ++c) seg_counts[c] = 0;
   if (nA <= 0 || nB <= 0) return 0;
   if (D < 1 || D > 64) throw std::runtime_error("pairs_within: 1 <= D <= 64");
   // a kept pair has rint(sqrt(s) / nf * scale) <= thr, so sqrt(s) / nf * scale < thr + 1 and
@@ -724,14 +754,14 @@ long long pairs_within(const float* A, int nA, const float* B, int nB, int D, fl
     const double bound = ((double)thr + 1.0) * (double)nf / (double)scale;
     s_max = bound < 0.0 ? -1.f : (float)(bound * bound * 1.001);
   }
-  AV_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), stream));
+  AV_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * PW_SEGS * PW_CSTRIDE, stream));
   // grid.y is capped at 65535 workgroups: A is covered in row chunks of AR x 65535
   auto run = [&](auto kern, int AR) {
     const int CH = AR * 65535;
     for (int a_row0 = 0; a_row0 < nA; a_row0 += CH) {
       const int rows = std::min(CH, nA - a_row0);
       const dim3 grid((unsigned)((nB + 255) / 256), (unsigned)((rows + AR - 1) / AR));
-      kern<<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, s_max, tri, a_base, b_base, cnt, cap, outI, outJ,
+      kern<<<grid, 256, 0, stream>>>(A, nA, B, nB, D, nf, scale, thr, s_max, tri, a_base, b_base, cnt, seg_cap, outK,
                                      outD, a_row0);
     }
   };
@@ -741,10 +771,18 @@ long long pairs_within(const float* A, int nA, const float* B, int nB, int D, fl
   else if (D <= 32) run(pairs_within_kernel<32, 64>, 64);
   else run(pairs_within_kernel<64, 64>, 64);
   AV_HIP_CHECK(hipGetLastError());
-  int h = 0;
-  AV_HIP_CHECK(hipMemcpyAsync(&h, cnt, sizeof(int), hipMemcpyDeviceToHost, stream));
+  int h[PW_SEGS * PW_CSTRIDE];
+  AV_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, stream));
   AV_HIP_CHECK(hipStreamSynchronize(stream));
-  return h;
+  long long mx = 0;
+  for (int c = 0; c < PW_SEGS; ++c) {
+    seg_counts[c] = h[c * PW_CSTRIDE];
+    mx = std::max<long long>(mx, h[c * PW_CSTRIDE]);
+  }
+  return mx;
 }
+
+int pairs_within_segments() { return PW_SEGS; }
+int pairs_within_counter_ints() { return PW_SEGS * PW_CSTRIDE; }
 
 }  // namespace avk

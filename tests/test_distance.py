@@ -393,3 +393,8 @@ def test_pairs_within_kernel_vs_fp64(cuda, D):
         assert len(got ^ exp) <= 0.002 * len(exp) + 2           # fp32 vs fp64 at the threshold edge
         for a, b, dd in zip(i.tolist()[:500], j.tolist()[:500], d.tolist()[:500]):
             assert abs(dd - ref[a, b]) <= 1
+    # every pair kept: 4 M pairs overflow the first segment sizing -> the one re-run; all present, sorted
+    A2, B2 = torch.rand(2000, D, generator=g), torch.rand(2000, D, generator=g)
+    i, j, d = _native.C().pairs_within(A2.to(cuda), B2.to(cuda), nf, scale, 1e9, False, 0, 0)
+    assert i.numel() == 2000 * 2000
+    assert bool(((i * 2000 + j) == torch.arange(2000 * 2000, device=i.device)).all())
