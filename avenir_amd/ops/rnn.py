@@ -147,7 +147,10 @@ class _PackCacheF32:
     @staticmethod
     def _pack(w_ih, w_hh, b_ih, b_hh):
         c = lambda t: None if t is None else t.detach().float().contiguous()
-        return tuple(_native.C().lstm_pack_f32(c(w_ih), c(w_hh), c(b_ih), c(b_hh)))
+        packed = tuple(_native.C().lstm_pack_f32(c(w_ih), c(w_hh), c(b_ih), c(b_hh)))
+        # W_ih^T [I, 4H] for dx = dz W_ih on the f32-MFMA GEMM (wide inputs only)
+        wt = c(w_ih).t().contiguous() if w_ih.shape[1] > 8 else None
+        return packed + (wt,)
 
     def get(self, w_ih, w_hh, b_ih, b_hh):
         ts = (w_ih, w_hh, b_ih, b_hh)
@@ -247,6 +250,11 @@ class _LstmLayer(torch.autograd.Function):
         return dx, dw_ih, dw_hh, db, (dh0 if need[4] else None), (dc0 if need[5] else None)
 
 
+#: the fp32 layer's plain GEMMs (wide-input projection, dx): "mfma" = the f32-MFMA tile kernel of
+#: mlp.hip (linear_act_fwd: exact-f32 v_mfma_f32_32x32x2_f32, bias in the epilogue), "blas" = hipBLASLt
+LSTM_GEMM = __import__("os").environ.get("AVMI_LSTM_GEMM", "mfma")
+
+
 class _LstmLayerF32(torch.autograd.Function):
     """One fp32 layer.  Forward: ONE pack launch (skipped while the parameters are unchanged) + ONE
     recurrence launch — for inputs of <= 8 features the input projection runs inside it (extra MFMA
@@ -260,22 +268,24 @@ class _LstmLayerF32(torch.autograd.Function):
         B, T, I = x.shape
         H = w_hh.shape[1]
         HP = padded_hidden(H)
-        frag, frag_t, w_ih_k, bias, wxfrag = _packs_f32.get(w_ih, w_hh, b_ih, b_hh)
+        frag, frag_t, w_ih_k, bias, wxfrag, w_ih_t = _packs_f32.get(w_ih, w_hh, b_ih, b_hh)
         need = any(ctx.needs_input_grad)
         if I <= 8:
             outs = _native.C().lstm_forward_f32(None, frag, h0, c0, H, bool(need), x=x, wxfrag=wxfrag, biask=bias)
         else:
-            xw = torch.addmm(bias, x.reshape(B * T, I), w_ih_k.t()).view(B, T, 4 * HP)
+            x2 = x.reshape(B * T, I)
+            xw = (_native.C().linear_act_fwd(x2, w_ih_k, bias, 0) if LSTM_GEMM == "mfma"
+                  else torch.addmm(bias, x2, w_ih_k.t())).view(B, T, 4 * HP)
             outs = _native.C().lstm_forward_f32(xw, frag, h0, c0, H, bool(need), x=x if need else None)
         hseq, cseq = outs[0], outs[1]
         if need:
-            ctx.save_for_backward(w_ih, cseq, outs[2], outs[3], c0, frag_t)
+            ctx.save_for_backward(w_ih, cseq, outs[2], outs[3], c0, frag_t, w_ih_t)
         ctx.dims = (B, T, I, H)
         return hseq, hseq[:, -1], cseq[:, -1, :H]
 
     @staticmethod
     def backward(ctx, dhseq, dhn, dcn):
-        w_ih, cseq, gates, hx, c0, frag_t = ctx.saved_tensors
+        w_ih, cseq, gates, hx, c0, frag_t, w_ih_t = ctx.saved_tensors
         B, T, I, H = ctx.dims
         if dhseq is None:
             dhseq = cseq.new_zeros(B, T, H)
@@ -284,7 +294,12 @@ class _LstmLayerF32(torch.autograd.Function):
                                                      None if dcn is None else dcn.contiguous(), frag_t, H)
         dz2 = dz.view(B * T, 4 * H)                                    # fp32, torch gate order
         need = ctx.needs_input_grad
-        dx = (dz2 @ w_ih.detach().float()).view(B, T, I) if need[0] else None
+        dx = None
+        if need[0]:
+            if LSTM_GEMM == "mfma" and w_ih_t is not None:
+                dx = _native.C().linear_act_fwd(dz2, w_ih_t, None, 0).view(B, T, I)
+            else:
+                dx = (dz2 @ w_ih.detach().float()).view(B, T, I)
         dw_ih = dw_hh = db = None
         if any(need[1:5]):
             dwcat = dz2.t() @ hx.view(B * T, H + I + 1)                 # [4H, H + I + 1]
