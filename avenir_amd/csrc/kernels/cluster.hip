@@ -307,8 +307,10 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
 //     LDS bank conflicts.
 // Three register tiles rotate (no copies) so the next two tiles' loads are in flight during this
 // one's work.
-template <int D, int KBLK>
-__global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? 3 : 2) void kmeans_score_kernel(const float* __restrict__ X, long long n,
+// NBUF register tiles in rotation (3: two tiles of loads in flight, 3 waves / SIMD; 2: one tile
+// ahead at 4 waves / SIMD — AVMI_KMEANS_NBUF=2 for the A/B)
+template <int D, int KBLK, int NBUF>
+__global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 2) void kmeans_score_kernel(const float* __restrict__ X, long long n,
                                                           const float* __restrict__ C2, const float* __restrict__ Cn,
                                                           const int* __restrict__ roff, int R, int K,
                                                           int* __restrict__ assign, float* __restrict__ partial,
@@ -479,24 +481,37 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? 3 : 2) void kmeans_sco
     }
     __builtin_amdgcn_wave_barrier();
   };
-  // three register tiles in rotation: the loads of the next TWO tiles are in flight during this
-  // one's work (one tile ahead left HBM at ~3.9 TB/s: too few bytes in flight at 3 waves / SIMD)
+  // register tiles in rotation: with three, the loads of the next TWO tiles are in flight during
+  // this one's work (one tile ahead left HBM at ~3.9 TB/s at 3 waves / SIMD)
   f32x4 xa[4][DB], xb[4][DB], xc[4][DB];
   long long t = gw;
-  if (t < ntiles) load_tile(t, xa);
-  if (t + nw < ntiles) load_tile(t + nw, xb);
-  while (t < ntiles) {
-    if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xc);
-    body(t, xa);
-    t += nw;
-    if (t >= ntiles) break;
-    if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xa);
-    body(t, xb);
-    t += nw;
-    if (t >= ntiles) break;
-    if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xb);
-    body(t, xc);
-    t += nw;
+  if constexpr (NBUF == 3) {
+    if (t < ntiles) load_tile(t, xa);
+    if (t + nw < ntiles) load_tile(t + nw, xb);
+    while (t < ntiles) {
+      if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xc);
+      body(t, xa);
+      t += nw;
+      if (t >= ntiles) break;
+      if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xa);
+      body(t, xb);
+      t += nw;
+      if (t >= ntiles) break;
+      if (t + 2 * nw < ntiles) load_tile(t + 2 * nw, xb);
+      body(t, xc);
+      t += nw;
+    }
+  } else {
+    if (t < ntiles) load_tile(t, xa);
+    while (t < ntiles) {
+      if (t + nw < ntiles) load_tile(t + nw, xb);
+      body(t, xa);
+      t += nw;
+      if (t >= ntiles) break;
+      if (t + nw < ntiles) load_tile(t + nw, xa);
+      body(t, xb);
+      t += nw;
+    }
   }
 #pragma unroll
   for (int cb = 0; cb < KBLK; ++cb)
@@ -608,6 +623,10 @@ KmVariant km_variant(int D, int K, int R) {
   const int DP = D < 16 ? 16 : D;
   int KBt = 1;
   while (KBt * 16 < K) KBt *= 2;
+  static const bool nbuf2 = [] {
+    const char* e = std::getenv("AVMI_KMEANS_NBUF");
+    return e && e[0] == '2';
+  }();
   static const bool valu_score = [] {
     const char* e = std::getenv("AVMI_KMEANS_SCORE");
     return e && (e[0] == 'v' || e[0] == 'V');  // "valu": the packed-FMA scoring kernel (A/B)
@@ -617,7 +636,8 @@ KmVariant km_variant(int D, int K, int R) {
   if (!valu_score && R == 1 && D >= 4 && KBt * (DP / 16) <= 2) {
     const size_t lds = sizeof(float) * (4 * (64 * (size_t)(DP + 4) + 64) + 4 * 64 + K + (size_t)K * D);
 #define AVK_KMS(DD, KK) \
-  if (D == DD && KBt == KK) return {(const void*)kmeans_score_kernel<DD, KK>, lds, true};
+  if (D == DD && KBt == KK)                                                                   \
+    return {nbuf2 ? (const void*)kmeans_score_kernel<DD, KK, 2> : (const void*)kmeans_score_kernel<DD, KK, 3>, lds, true};
     AVK_KMS(4, 1) AVK_KMS(4, 2)
     AVK_KMS(8, 1) AVK_KMS(8, 2)
     AVK_KMS(16, 1) AVK_KMS(16, 2)
