@@ -307,8 +307,9 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
 //     LDS bank conflicts.
 // Three register tiles rotate (no copies) so the next two tiles' loads are in flight during this
 // one's work.
-// NBUF register tiles in rotation (3: two tiles of loads in flight, 3 waves / SIMD; 2: one tile
-// ahead at 4 waves / SIMD — AVMI_KMEANS_NBUF=2 for the A/B)
+// NBUF register tiles in rotation: 2 (the default) keeps one tile of loads ahead at 4 waves / SIMD
+// (120 VGPRs), 3 keeps two ahead at 3 waves / SIMD (162 VGPRs; AVMI_KMEANS_NBUF=3).  Measured at
+// 16.7 M x 16, k = 16: 253.5 vs 263.6 us per pass (profiles/r5_kmeans_nbuf_ab.txt); 5 waves spill.
 template <int D, int KBLK, int NBUF>
 __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 2) void kmeans_score_kernel(const float* __restrict__ X, long long n,
                                                           const float* __restrict__ C2, const float* __restrict__ Cn,
@@ -625,7 +626,7 @@ KmVariant km_variant(int D, int K, int R) {
   while (KBt * 16 < K) KBt *= 2;
   static const bool nbuf2 = [] {
     const char* e = std::getenv("AVMI_KMEANS_NBUF");
-    return e && e[0] == '2';
+    return !(e && e[0] == '3');
   }();
   static const bool valu_score = [] {
     const char* e = std::getenv("AVMI_KMEANS_SCORE");
