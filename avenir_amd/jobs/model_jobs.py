@@ -1054,6 +1054,22 @@ def record_similarity(args):
                 J.append(jj + b0)
                 Dv.append(D[qi, jj].long())
                 H.append(torch.full_like(jj, h) * (1 << 40) + jj)
+    sp_own = spB if rB is not None else spA
+    if (I and not comm.is_distributed and dev.type == "cuda" and spA.dev is not None and sp_own.dev is not None
+            and I[0].is_cuda):
+        # one rank: both sides' lines are this rank's uploaded bytes, so the pairs stay on the
+        # device and the output rows are formatted there (format.hip) instead of on the host
+        I, J, Dv = torch.cat(I), torch.cat(J), torch.cat(Dv)
+        if len(Dv) > 1:
+            order = torch.argsort(I * max(1, NB) + J)
+            I, J, Dv = I[order], J[order], Dv[order]
+        spI, spJ = spA.select(I), sp_own.select(J - b_rec.line_base)
+        cols = [spI.column("rf", idc, lit), spJ.column("rf", idc, lit)]
+        if out_rec:
+            cols += [spI.column("r", delims=lit), spJ.column("r", delims=lit)]
+        cols.append(("i", Dv))
+        ctx.emit_columns(cols, int(I.numel()))
+        return
     if I:
         I, J, Dv, H = torch.cat(I), torch.cat(J), torch.cat(Dv), torch.cat(H)
         order = torch.argsort(I * max(1, NB) + J)

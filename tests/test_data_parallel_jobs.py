@@ -199,3 +199,30 @@ def test_record_similarity_fused_kernel_matches_tiles(cuda, tmp_path, monkeypatc
     assert len(common) >= 0.99 * max(len(a), len(b)) and len(a) > 100
     assert all(abs(a[k] - b[k]) <= 1 for k in common)
     assert all(v >= 119 for k, v in a.items() if k not in b) and all(v >= 119 for k, v in b.items() if k not in a)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("out_rec", [False, True])
+def test_record_similarity_device_formatter_equals_host(cuda, tmp_path, monkeypatch, out_rec):
+    """One rank on the GPU: the pairs stay on the device and the rows are formatted by format.hip
+    (ids and whole records taken from the uploaded line bytes) — byte-identical to the host
+    formatter's output of the same pairs."""
+    import numpy as np
+    from avenir_amd.cli import main
+    from avenir_amd.data import records as R
+    rng = np.random.default_rng(9)
+    X = rng.random((2500, 8))
+    data = tmp_path / "rs.csv"
+    data.write_text("\n".join(f"r{i}," + ",".join(f"{v:.5f}" for v in row) for i, row in enumerate(X)) + "\n")
+    cfg = tmp_path / "rs.properties"
+    cfg.write_text("resi.attr.ordinals=1,2,3,4,5,6,7,8\nresi.id.ordinal=0\nresi.distance.scale=1000\n"
+                   f"resi.dist.threshold=150\nresi.output.record={'true' if out_rec else 'false'}\n")
+    monkeypatch.setattr(R, "DEVICE_MIN_BYTES", 0)            # the device tokenizer (line bytes on the GPU)
+    outs = {}
+    for mode in ("device", "host"):
+        monkeypatch.setattr(R, "DEVICE_FORMAT_MIN_ROWS", 0)
+        monkeypatch.setenv("AVMI_DEVICE_FORMAT", "1" if mode == "device" else "0")
+        out = tmp_path / f"{mode}.txt"
+        assert main(["recordSimilarity", "-i", str(data), "-o", str(out), "-c", str(cfg), "--device", "cuda"]) == 0
+        outs[mode] = out.read_bytes()
+    assert outs["device"] == outs["host"] and outs["device"].count(b"\n") > 100
