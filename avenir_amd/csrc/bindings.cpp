@@ -3650,6 +3650,26 @@ std::vector<at::Tensor> ref_split_score(const at::Tensor& hist, const at::Tensor
   return {top, topv, segc, cinfo};
 }
 
+// C [M, N] = A^T B for A [K, M], B [K, N] fp32 (gemm.hip: split-K f32 MFMA + ordered slice sum)
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B) {
+  CHECK_DEV(A);
+  CHECK_DTYPE(A, at::kFloat);
+  CHECK_DEV(B);
+  CHECK_DTYPE(B, at::kFloat);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0) && A.is_contiguous() && B.is_contiguous(),
+              "gemm_tn: A [K, M], B [K, N] contiguous");
+  TORCH_CHECK(A.size(0) < (1LL << 31) && A.size(1) < (1LL << 31) && B.size(1) < (1LL << 31), "gemm_tn: dims < 2^31");
+  const int K = (int)A.size(0), M = (int)A.size(1), N = (int)B.size(1);
+  DevGuard g(A.device());
+  auto C = at::empty({M, N}, A.options());
+  if (K == 0) return C.zero_();
+  const int S = avk::gemm_tn_slices(K, M, N);
+  auto part = at::empty({(int64_t)S * M * N}, A.options());
+  avk::gemm_tn(A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(), part.data_ptr<float>(), K, M, N, S,
+               cur_stream(A));
+  return C;
+}
+
 // One launch re-lays an fp32 layer's parameters (rnn_f32.hip lstm_pack_f32_kernel): w_ih [4H, I],
 // w_hh [4H, H], b_ih / b_hh [4H] or None -> wfrag [NW,4,HP/4,64], wfragT [NW,HP,64], wihk [4HP, I], biask [4HP],
 // wxfrag [NW,4,2,64] (I <= 8; empty otherwise).
@@ -3910,6 +3930,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("H"), py::arg("training"), py::arg("x") = py::none(), py::arg("wxfrag") = py::none(),
         py::arg("biask") = py::none());
   m.def("lstm_pack_f32", &lstm_pack_f32);
+  m.def("gemm_tn", &gemm_tn);
   m.def("ref_split_score", &ref_split_score);
   m.def("lstm_backward_f32", &lstm_backward_f32);
 

@@ -183,6 +183,10 @@ void ref_split_score(const long long* hist, int A, int C, int TBt, const int* sp
                      const unsigned char* cand, int F, int algo, int k, int G2, long long* top, double* topv,
                      double* segc, double* cinfo, double* scratch, hipStream_t stream);
 
+// ---- gemm.hip: split-K fp32 A^T B (weight gradients over a long row dimension) ---------------
+int gemm_tn_slices(int K, int M, int N);
+void gemm_tn(const float* A, const float* B, float* C, float* partial, int K, int M, int N, int S, hipStream_t stream);
+
 // ---- rnn_f32.hip (K27 fp32) ------------------------------------------------------------------
 void lstm_fwd_f32(const float* xw, const float* x, const float* wxfrag, const float* biask, const float* wfrag,
                   const float* h0, const float* c0, int B, int T, int H, int I, int KS, float* hseq, float* cseq,

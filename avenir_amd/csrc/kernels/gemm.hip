@@ -1,0 +1,119 @@
+// Split-K fp32 "Aᵀ·B" GEMM for weight gradients: C[M, N] = Σ_k A[k, m] · B[k, n] with A [K, M] and
+// B [K, N] both row-major over the long reduction dimension K (e.g. the LSTM's dW = dzᵀ·[h_{t-1} | x | 1]
+// over all B·T rows: K = 5,000, M = 4H = 400, N = H + I + 1 ≈ 106).  Such a product has few output
+// tiles (7 x 2 here) and a long K: hipBLASLt's pick ran at ~30 TFLOP/s (26 us, the LSTM trace).  Here
+// the K range is split over S slices so the grid has hundreds of workgroups; each workgroup stages
+// 32-row chunks of its A and B columns with coalesced row loads (the next chunk register-prefetched
+// during the MFMAs), multiplies a 64 x 64 output tile on v_mfma_f32_32x32x2_f32 (exact-f32 products,
+// one 32 x 32 quarter per wave) and writes its partial tile; a second kernel sums the S partials of
+// every output in slice order (deterministic, no float atomics).
+#include "avenir_common.h"
+#include "avenir_kernels.h"
+
+namespace {
+
+constexpr int GT = 256;   // threads
+constexpr int TM = 64;    // output rows (A columns) per workgroup
+constexpr int TN = 64;    // output cols (B columns) per workgroup
+constexpr int KC = 32;    // K rows per LDS chunk
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// one K chunk of the A and B tiles in registers: KC rows x 64 columns each = 2048 floats per
+// operand, 8 per thread (rows tid / 64 + 4 i, column tid % 64: coalesced 256-byte row segments)
+struct TnChunk {
+  float a[8], b[8];
+  __device__ __forceinline__ void load(const float* __restrict__ A, const float* __restrict__ B, int k0, int k1, int m0,
+                                       int n0, int M, int N) {
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = k0 + r0 + 4 * i;
+      const bool kin = k < k1;
+      a[i] = (kin && m0 + c < M) ? A[(long long)k * M + m0 + c] : 0.f;
+      b[i] = (kin && n0 + c < N) ? B[(long long)k * N + n0 + c] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float (*sA)[TM + 1], float (*sB)[TN + 1]) const {
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sA[r0 + 4 * i][c] = a[i];
+      sB[r0 + 4 * i][c] = b[i];
+    }
+  }
+};
+
+// grid (N tiles, M tiles, S slices); partial [S, M, N]
+__global__ __launch_bounds__(GT) void gemm_tn_partial_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                             float* __restrict__ partial, int K, int M, int N,
+                                                             int kper) {
+  __shared__ float sA[KC][TM + 1];
+  __shared__ float sB[KC][TN + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  const int k0 = blockIdx.z * kper, k1 = min(K, k0 + kper);
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  TnChunk pre;
+  if (k0 < k1) pre.load(A, B, k0, k1, m0, n0, M, N);
+  for (int kc = k0; kc < k1; kc += KC) {
+    __syncthreads();  // the previous chunk's operand reads are done
+    pre.store(sA, sB);
+    __syncthreads();
+    if (kc + KC < k1) pre.load(A, B, kc + KC, k1, m0, n0, M, N);  // in flight during the MFMAs
+    const int li = lane & 31, lk = lane >> 5;
+#pragma unroll
+    for (int k = 0; k < KC; k += 2) {
+      // A operand: A'[i = m][k] = A[k][m]; B operand: B[k][j = n]
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[k + lk][wm * 32 + li], sB[k + lk][wn * 32 + li], acc, 0, 0, 0);
+    }
+  }
+  // C/D map of 32x32x2: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  const int n = n0 + wn * 32 + (lane & 31);
+  if (n >= N) return;
+  float* P = partial + (long long)blockIdx.z * M * N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (m < M) P[(long long)m * N + n] = acc[r];
+  }
+}
+
+// C[e] = Σ_s partial[s][e] in slice order
+__global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __restrict__ partial, float* __restrict__ C,
+                                                            long long MN, int S) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= MN) return;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += partial[k * MN + e];
+  C[e] = s;
+}
+
+}  // namespace
+
+namespace avk {
+
+int gemm_tn_slices(int K, int M, int N) {
+  const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  // enough workgroups for the chip (~1024), each slice at least 2 chunks of K
+  long long s = (1024 + tiles - 1) / tiles;
+  s = std::min<long long>(s, std::max(1, K / (2 * KC)));
+  return (int)std::max(1LL, std::min(s, 128LL));
+}
+
+void gemm_tn(const float* A, const float* B, float* C, float* partial, int K, int M, int N, int S, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  if (S < 1) throw std::runtime_error("gemm_tn: S >= 1");
+  const int kper = ((K + S - 1) / S + KC - 1) / KC * KC;
+  const dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)S);
+  gemm_tn_partial_kernel<<<grid, GT, 0, stream>>>(A, B, partial, K, M, N, kper);
+  AV_HIP_CHECK(hipGetLastError());
+  const long long MN = (long long)M * N;
+  gemm_tn_reduce_kernel<<<(unsigned)((MN + 255) / 256), 256, 0, stream>>>(partial, C, MN, S);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace avk

@@ -27,10 +27,12 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+// gate nonlinearities with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of the IEEE
+// division sequence (~10 instructions each, 5 per hidden unit per step on the recurrence's path)
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_(float x) {
   const float e = __expf(-2.f * fabsf(x));
-  return copysignf((1.f - e) / (1.f + e), x);
+  return copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
 }
 
 // Layouts (kernel order of the 4·HP gate columns: kc = 64·w + 16·g + i for unit u = 16·w + i, gate g):

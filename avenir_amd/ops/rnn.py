@@ -250,8 +250,9 @@ class _LstmLayer(torch.autograd.Function):
         return dx, dw_ih, dw_hh, db, (dh0 if need[4] else None), (dc0 if need[5] else None)
 
 
-#: the fp32 layer's plain GEMMs (wide-input projection, dx): "mfma" = the f32-MFMA tile kernel of
-#: mlp.hip (linear_act_fwd: exact-f32 v_mfma_f32_32x32x2_f32, bias in the epilogue), "blas" = hipBLASLt
+#: the fp32 layer's plain GEMMs: "mfma" = the wide-input projection and dx on the f32-MFMA tile
+#: kernel of mlp.hip (linear_act_fwd: exact-f32 v_mfma_f32_32x32x2_f32, bias in the epilogue) and
+#: the weight-gradient product on gemm.hip's split-K kernel (gemm_tn); "blas" = hipBLASLt for all
 LSTM_GEMM = __import__("os").environ.get("AVMI_LSTM_GEMM", "mfma")
 
 
@@ -302,7 +303,9 @@ class _LstmLayerF32(torch.autograd.Function):
                 dx = (dz2 @ w_ih.detach().float()).view(B, T, I)
         dw_ih = dw_hh = db = None
         if any(need[1:5]):
-            dwcat = dz2.t() @ hx.view(B * T, H + I + 1)                 # [4H, H + I + 1]
+            hx2 = hx.view(B * T, H + I + 1)
+            dwcat = (_native.C().gemm_tn(dz2, hx2) if LSTM_GEMM == "mfma"
+                     else dz2.t() @ hx2)                                 # [4H, H + I + 1]
             dw_hh = dwcat[:, :H] if need[2] else None
             dw_ih = dwcat[:, H:H + I] if need[1] else None
             db = dwcat[:, H + I] if (need[3] or need[4]) else None
