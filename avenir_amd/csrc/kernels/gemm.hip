@@ -82,13 +82,22 @@ __global__ __launch_bounds__(GT) void gemm_tn_partial_kernel(const float* __rest
   }
 }
 
-// C[e] = Σ_s partial[s][e] in slice order
+// C[e] = Σ_s partial[s][e] in slice order; the loads of 8 slices are issued together (a plain
+// loop left one dependent load chain per output: 14.6 us for 42 k outputs x 74 slices)
 __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __restrict__ partial, float* __restrict__ C,
                                                             long long MN, int S) {
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= MN) return;
   float s = 0.f;
-  for (int k = 0; k < S; ++k) s += partial[k * MN + e];
+  int k = 0;
+  for (; k + 8 <= S; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = partial[(long long)(k + u) * MN + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < S; ++k) s += partial[(long long)k * MN + e];
   C[e] = s;
 }
 
@@ -98,9 +107,10 @@ namespace avk {
 
 int gemm_tn_slices(int K, int M, int N) {
   const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  // enough workgroups for the chip (~1024), each slice at least 2 chunks of K
-  long long s = (1024 + tiles - 1) / tiles;
-  s = std::min<long long>(s, std::max(1, K / (2 * KC)));
+  // one workgroup per CU (256), each slice at least 4 chunks of K: more slices only moved the time
+  // into the partial traffic and the slice sum (74 slices of 2 chunks: 17.6 + 14.6 us at K = 5,000)
+  long long s = (256 + tiles - 1) / tiles;
+  s = std::min<long long>(s, std::max(1, K / (4 * KC)));
   return (int)std::max(1LL, std::min(s, 128LL));
 }
 
