@@ -316,6 +316,7 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
                                                           const int* __restrict__ roff, int R, int K,
                                                           int* __restrict__ assign, float* __restrict__ partial,
                                                           double* __restrict__ sse_partial) {
+  static_assert(D % 4 == 0, "kmeans_score_kernel: rows of whole float4s (D in {4, 8, 16, 32})");
   constexpr int DP = D < 16 ? 16 : D;  // staged row width of the partial-sum tile
   constexpr int DB = DP / 16;          // 16-dim blocks
   constexpr int RS = DP + 4;           // padded row stride of the staging tile
@@ -329,7 +330,10 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
   for (int i = threadIdx.x; i < K; i += KB) cnt[i] = 0u;
   for (int i = threadIdx.x; i < K * D; i += KB) red[i] = 0.f;
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
+  // the wave index read into a scalar register: the tile loop below is then uniform per wave (a
+  // VGPR loop counter made it an exec-masked loop, with a full vmcnt(0) wait at its head)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), grp = lane >> 4,
+            col = lane & 15;
   float* xs = xs_all + w * XS;
   int* asg = asg_all + w * 64;
   // scoring A operand: centroid 16 cb + col, dim 16 b + 4 grp + m; accumulator start -||c||^2 / 2 of
@@ -366,34 +370,39 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
   double sse = 0.0, xsq = 0.0;
   const long long ntiles = (n + 63) / 64;
   const long long gw = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
+  // branch-free raw loads: rows past n read the last row, dims past D read dims 0..3 — never
+  // masked here (a select right after the load made the waitcnt pass wait for it at once, and loads
+  // under per-lane branches made it wait for ALL outstanding loads before each tile's MFMAs).  The
+  // extra values are harmless: padded dims meet zero centroid coordinates in the scoring MFMAs and
+  // are never summed (red[] keeps d < D), padded rows have no assignment (-1: a zero one-hot
+  // row) — only ||x||^2 masks them, in body().
   auto load_tile = [&](long long t, f32x4 (&v)[4][DB]) {
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
       const long long row = t * 64 + sb * 16 + col;
+      const long long rr = row < n ? row : n - 1;
 #pragma unroll
       for (int b = 0; b < DB; ++b) {
         const int d = b * 16 + 4 * grp;
-        if (row < n && d < D) {
-          if constexpr (D % 4 == 0) {
-            const float4 u = *reinterpret_cast<const float4*>(X + row * D + d);
-            v[sb][b] = f32x4{u.x, u.y, u.z, u.w};
-          } else {
-            v[sb][b] = f32x4{X[row * D + d], d + 1 < D ? X[row * D + d + 1] : 0.f, 0.f, 0.f};
-          }
-        } else {
-          v[sb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        const int dd = d < D ? d : 0;
+        const float4 u = *reinterpret_cast<const float4*>(X + rr * D + dd);
+        v[sb][b] = f32x4{u.x, u.y, u.z, u.w};
       }
     }
   };
   auto body = [&](long long t, f32x4 (&xv)[4][DB]) {
-    float xs2 = 0.f;  // ||x||^2 of the tile (padding rows / dims are zero)
+    float xs2 = 0.f;  // ||x||^2 of the tile's valid rows and dims
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
+    for (int sb = 0; sb < 4; ++sb) {
+      const bool rin = t * 64 + sb * 16 + col < n;
 #pragma unroll
-      for (int b = 0; b < DB; ++b)
+      for (int b = 0; b < DB; ++b) {
+        float q = 0.f;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) xs2 = fmaf(xv[sb][b][m], xv[sb][b][m], xs2);
+        for (int m = 0; m < 4; ++m) q = fmaf(xv[sb][b][m], xv[sb][b][m], q);
+        xs2 += (rin && b * 16 + 4 * grp < D) ? q : 0.f;
+      }
+    }
     xsq += (double)xs2;
     // s'(row 16 sb + col, centroid 16 cb + 4 grp + q) in dot[sb][cb][q]
     f32x4 dot[4][KBLK];
@@ -503,13 +512,19 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
       t += nw;
     }
   } else {
+    // the prefetch is unconditional (past the last tile it re-reads the last tile): a prefetch
+    // under a branch made the waitcnt pass assume it might be missing and wait for part of it
+    // before the current tile's MFMAs
+    const long long last = ntiles - 1;
     if (t < ntiles) load_tile(t, xa);
     while (t < ntiles) {
-      if (t + nw < ntiles) load_tile(t + nw, xb);
+      load_tile(t + nw < ntiles ? t + nw : last, xb);
+      __builtin_amdgcn_sched_barrier(0);  // issue the prefetch before this tile's work
       body(t, xa);
       t += nw;
       if (t >= ntiles) break;
-      if (t + nw < ntiles) load_tile(t + nw, xa);
+      load_tile(t + nw < ntiles ? t + nw : last, xa);
+      __builtin_amdgcn_sched_barrier(0);
       body(t, xb);
       t += nw;
     }
