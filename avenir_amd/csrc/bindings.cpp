@@ -2150,7 +2150,7 @@ at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::o
   CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
   CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
   TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "X [M, K], W [N, K]");
-  TORCH_CHECK(act >= 0 && act <= 5, "activation code 0..5");
+  TORCH_CHECK(act >= 0 && act <= 6, "activation code 0..6 (6 = gelu, forward only)");
   TORCH_CHECK(X.size(0) < (1LL << 31) && W.size(0) < (1LL << 31) && X.size(1) < (1LL << 31), "dims < 2^31");
   auto Xc = X.contiguous(), Wc = W.contiguous();
   at::Tensor bc;
@@ -3650,6 +3650,65 @@ std::vector<at::Tensor> ref_split_score(const at::Tensor& hist, const at::Tensor
   return {top, topv, segc, cinfo};
 }
 
+// LN(x + res) * gamma + beta over the last dim (transformer.hip); res may be None
+at::Tensor add_layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& res, const at::Tensor& gamma,
+                         const at::Tensor& beta, double eps) {
+  CHECK_DEV(x);
+  CHECK_DTYPE(x, at::kFloat);
+  TORCH_CHECK(x.is_contiguous() && x.dim() >= 1, "add_layernorm: x contiguous");
+  const int64_t H = x.size(-1), rows = x.numel() / std::max<int64_t>(1, H);
+  TORCH_CHECK(H >= 4 && H <= 1024 && H % 4 == 0, "add_layernorm: 4 <= H <= 1024, H % 4 == 0");
+  check_opt_f32(res, x.numel(), "res");
+  check_opt_f32(gamma, H, "gamma");
+  check_opt_f32(beta, H, "beta");
+  TORCH_CHECK(aligned(x, 16) && aligned(gamma, 16) && aligned(beta, 16) && (!res.has_value() || aligned(*res, 16)),
+              "add_layernorm: 16-byte aligned tensors");
+  DevGuard g(x.device());
+  auto out = at::empty_like(x);
+  avk::add_layernorm(x.data_ptr<float>(), ptr_or_null<float>(res), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                     out.data_ptr<float>(), rows, (int)H, (float)eps, cur_stream(x));
+  return out;
+}
+
+// LN(word[ids] + pos[s] + type[tt]) for ids / tt int64 [B, S] (tt may be None: type 0)
+at::Tensor embed_layernorm(const at::Tensor& ids, const c10::optional<at::Tensor>& tt, const at::Tensor& word,
+                           const at::Tensor& pos, const at::Tensor& type, const at::Tensor& gamma,
+                           const at::Tensor& beta, double eps) {
+  CHECK_DEV(ids);
+  CHECK_DTYPE(ids, at::kLong);
+  TORCH_CHECK(ids.dim() == 2 && ids.is_contiguous(), "embed_layernorm: ids [B, S]");
+  const int64_t B = ids.size(0), S = ids.size(1), H = word.size(1);
+  TORCH_CHECK(H >= 4 && H <= 1024 && H % 4 == 0, "embed_layernorm: 4 <= H <= 1024, H % 4 == 0");
+  for (const at::Tensor* t : {&word, &pos, &type}) {
+    CHECK_DEV((*t));
+    CHECK_DTYPE((*t), at::kFloat);
+    TORCH_CHECK(t->dim() == 2 && t->size(1) == H && t->is_contiguous() && aligned(*t, 16), "embedding tables [n, H]");
+  }
+  TORCH_CHECK(S <= pos.size(0), "embed_layernorm: sequence longer than the position table");
+  check_opt_f32(gamma, H, "gamma");
+  check_opt_f32(beta, H, "beta");
+  // host-side index validation (no out-of-bounds gathers)
+  auto idc = ids.cpu();
+  const auto mm = at::aminmax(idc);
+  TORCH_CHECK(std::get<0>(mm).item<int64_t>() >= 0 && std::get<1>(mm).item<int64_t>() < word.size(0),
+              "embed_layernorm: token id out of range");
+  if (tt.has_value() && tt->defined()) {
+    CHECK_DEV((*tt));
+    CHECK_DTYPE((*tt), at::kLong);
+    TORCH_CHECK(tt->sizes() == ids.sizes() && tt->is_contiguous(), "token types [B, S]");
+    const auto tm = at::aminmax(tt->cpu());
+    TORCH_CHECK(std::get<0>(tm).item<int64_t>() >= 0 && std::get<1>(tm).item<int64_t>() < type.size(0),
+                "embed_layernorm: token type out of range");
+  }
+  DevGuard g(ids.device());
+  auto out = at::empty({B, S, H}, word.options());
+  avk::embed_layernorm(reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()),
+                       tt.has_value() && tt->defined() ? reinterpret_cast<const long long*>(tt->data_ptr<int64_t>()) : nullptr,
+                       word.data_ptr<float>(), pos.data_ptr<float>(), type.data_ptr<float>(), gamma.data_ptr<float>(),
+                       beta.data_ptr<float>(), out.data_ptr<float>(), B * S, (int)S, (int)H, (float)eps, cur_stream(word));
+  return out;
+}
+
 // C [M, N] = A^T B for A [K, M], B [K, N] fp32 (gemm.hip: split-K f32 MFMA + ordered slice sum)
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B) {
   CHECK_DEV(A);
@@ -3931,6 +3990,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("biask") = py::none());
   m.def("lstm_pack_f32", &lstm_pack_f32);
   m.def("gemm_tn", &gemm_tn);
+  m.def("add_layernorm", &add_layernorm);
+  m.def("embed_layernorm", &embed_layernorm);
   m.def("ref_split_score", &ref_split_score);
   m.def("lstm_backward_f32", &lstm_backward_f32);
 

@@ -183,6 +183,13 @@ void ref_split_score(const long long* hist, int A, int C, int TBt, const int* sp
                      const unsigned char* cand, int F, int algo, int k, int G2, long long* top, double* topv,
                      double* segc, double* cinfo, double* scratch, hipStream_t stream);
 
+// ---- transformer.hip: encoder epilogues (BERT for semantic search) -----------------------------
+void add_layernorm(const float* x, const float* res, const float* gamma, const float* beta, float* out, long long rows,
+                   int H, float eps, hipStream_t stream);
+void embed_layernorm(const long long* ids, const long long* tt, const float* word, const float* pos, const float* type,
+                     const float* gamma, const float* beta, float* out, long long rows, int S, int H, float eps,
+                     hipStream_t stream);
+
 // ---- gemm.hip: split-K fp32 A^T B (weight gradients over a long row dimension) ---------------
 int gemm_tn_slices(int K, int M, int N);
 void gemm_tn(const float* A, const float* B, float* C, float* partial, int K, int M, int N, int S, hipStream_t stream);

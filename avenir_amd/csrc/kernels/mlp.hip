@@ -25,9 +25,11 @@ constexpr int KC = 32;   // K chunk in LDS
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// act codes: 0 identity, 1 relu, 2 sigmoid, 3 tanh, 4 leaky relu (0.01), 5 elu (alpha 1)
+// act codes: 0 identity, 1 relu, 2 sigmoid, 3 tanh, 4 leaky relu (0.01), 5 elu (alpha 1),
+// 6 gelu (erf form, torch.nn.functional.gelu / BERT's "gelu"; forward only)
 __device__ __forceinline__ float act_fwd(float z, int act) {
   switch (act) {
+    case 6: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
     case 1: return fmaxf(z, 0.f);
     case 2: return 1.f / (1.f + expf(-z));
     case 3: return tanhf(z);

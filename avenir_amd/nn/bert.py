@@ -1,0 +1,270 @@
+"""BERT encoder for semantic search (the reference's P/app/ssearch.py:184-300 embeds
+documents and queries with spaCy-transformers' ``en_trf_bertbaseuncased_lg`` and compares their
+token / sentence vectors).
+
+The module takes a Hugging Face BERT state dict as is (``BertModel`` parameter names, loaded with
+``torch.load(weights_only=True)`` or safetensors) and a WordPiece vocabulary (``tokenizers``), so a
+user's bert-base-uncased checkpoint drops in; no weights ship with the framework (none can be
+fetched here), and the tests pin the ARCHITECTURE against ``transformers.BertModel`` with random
+weights instead.
+
+MI355X path (inference, fp32 like the reference's model):
+* embeddings: word + position + token-type gathers, the sum and the LayerNorm in ONE kernel
+  (transformer.hip ``embed_layernorm_kernel``);
+* per layer: the Q, K, V projections as ONE f32-MFMA GEMM with concatenated weights (mlp.hip
+  ``linear_act_fwd``), attention scores / softmax / context as batched library GEMMs (hipBLASLt),
+  the output projection, then residual + LayerNorm in ONE pass (``add_layernorm_kernel``); the
+  feed-forward up-projection with bias + GELU in the GEMM's epilogue, the down-projection, residual +
+  LayerNorm again.
+CPU tensors run the same math with torch ops.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import asdict, dataclass, fields
+
+import torch
+
+from .. import _native
+
+#: activation code of mlp.hip's linear_act_fwd for the erf GELU
+_GELU = 6
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    layer_norm_eps: float = 1e-12
+    hidden_act: str = "gelu"
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "BertConfig":
+        names = {f.name for f in fields(cls)}
+        return cls(**{k: v for k, v in d.items() if k in names})
+
+    @classmethod
+    def from_json(cls, path: str) -> "BertConfig":
+        with open(path) as fh:
+            return cls.from_dict(json.load(fh))
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+
+def _layer_names(i: int) -> dict:
+    p = f"encoder.layer.{i}."
+    return {"q": p + "attention.self.query", "k": p + "attention.self.key", "v": p + "attention.self.value",
+            "o": p + "attention.output.dense", "ln1": p + "attention.output.LayerNorm",
+            "up": p + "intermediate.dense", "down": p + "output.dense", "ln2": p + "output.LayerNorm"}
+
+
+class BertEncoder(torch.nn.Module):
+    """``forward(input_ids [B, S], attention_mask [B, S] = None, token_type_ids = None) ->
+    last hidden state [B, S, H]`` — the same function as ``transformers.BertModel(...)
+    .last_hidden_state`` (eval mode), parameters under the same names."""
+
+    def __init__(self, config: BertConfig):
+        super().__init__()
+        if config.hidden_act not in ("gelu",):
+            raise ValueError(f"hidden_act {config.hidden_act!r}: only the erf GELU of bert-base is implemented")
+        if config.hidden_size % config.num_attention_heads:
+            raise ValueError("hidden_size must be a multiple of num_attention_heads")
+        self.config = config
+        H, I = config.hidden_size, config.intermediate_size
+        P = torch.nn.Parameter
+        self.params = torch.nn.ParameterDict()
+
+        def add(name, *shape, ones=False):
+            t = torch.ones(*shape) if ones else torch.zeros(*shape)
+            self.params[name.replace(".", "__")] = P(t)
+
+        add("embeddings.word_embeddings.weight", config.vocab_size, H)
+        add("embeddings.position_embeddings.weight", config.max_position_embeddings, H)
+        add("embeddings.token_type_embeddings.weight", config.type_vocab_size, H)
+        add("embeddings.LayerNorm.weight", H, ones=True)
+        add("embeddings.LayerNorm.bias", H)
+        for i in range(config.num_hidden_layers):
+            n = _layer_names(i)
+            for k in ("q", "k", "v", "o"):
+                add(n[k] + ".weight", H, H)
+                add(n[k] + ".bias", H)
+            add(n["up"] + ".weight", I, H)
+            add(n["up"] + ".bias", I)
+            add(n["down"] + ".weight", H, I)
+            add(n["down"] + ".bias", H)
+            for k in ("ln1", "ln2"):
+                add(n[k] + ".weight", H, ones=True)
+                add(n[k] + ".bias", H)
+        self._qkv_cache: dict = {}
+        self.reset_parameters()
+
+    def reset_parameters(self, std: float = 0.02, seed: int = 0):
+        g = torch.Generator().manual_seed(seed)
+        for name, p in self.params.items():
+            if name.endswith("weight") and p.dim() == 2:
+                with torch.no_grad():
+                    p.copy_(torch.randn(p.shape, generator=g) * std)
+
+    def p(self, name: str) -> torch.Tensor:
+        return self.params[name.replace(".", "__")]
+
+    # -- loading -------------------------------------------------------------------------------
+    def load_hf_state_dict(self, sd: dict, strict: bool = True) -> "BertEncoder":
+        """A ``transformers.BertModel`` state dict (keys with or without the ``bert.`` prefix of
+        task models; the pooler and heads are ignored)."""
+        own = {k.replace("__", "."): k for k in self.params.keys()}
+        seen = set()
+        for k, v in sd.items():
+            kk = k[5:] if k.startswith("bert.") else k
+            if kk in own:
+                tgt = self.params[own[kk]]
+                if tuple(tgt.shape) != tuple(v.shape):
+                    raise ValueError(f"{k}: shape {tuple(v.shape)} != {tuple(tgt.shape)}")
+                with torch.no_grad():
+                    tgt.copy_(v.to(tgt.dtype))
+                seen.add(kk)
+        missing = set(own) - seen
+        if strict and missing:
+            raise KeyError(f"missing BERT parameters: {sorted(missing)[:5]} ...")
+        self._qkv_cache.clear()
+        return self
+
+    @classmethod
+    def from_pretrained_dir(cls, path: str, device="cpu") -> "BertEncoder":
+        """A directory with ``config.json`` and ``model.safetensors`` or ``pytorch_model.bin``
+        (loaded without executing anything from the file)."""
+        cfg = BertConfig.from_json(os.path.join(path, "config.json"))
+        m = cls(cfg)
+        st = os.path.join(path, "model.safetensors")
+        if os.path.exists(st):
+            from safetensors.torch import load_file
+            sd = load_file(st)
+        else:
+            sd = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)
+        return m.load_hf_state_dict(sd).to(device).eval()
+
+    # -- forward -------------------------------------------------------------------------------
+    def _qkv(self, i: int):
+        """[3H, H] weights and [3H] bias of layer i's Q, K, V (cached per parameter version)."""
+        n = _layer_names(i)
+        ps = [self.p(n[k] + s) for k in ("q", "k", "v") for s in (".weight", ".bias")]
+        key = (i,) + tuple((t.data_ptr(), t._version) for t in ps)
+        hit = self._qkv_cache.get(i)
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        W = torch.cat([ps[0], ps[2], ps[4]], 0).detach().contiguous()
+        b = torch.cat([ps[1], ps[3], ps[5]], 0).detach().contiguous()
+        self._qkv_cache[i] = (key, W, b)
+        return W, b
+
+    def _linear(self, x2, W, b, act: int = 0):
+        if x2.is_cuda:
+            return _native.C().linear_act_fwd(x2, W, b, act)
+        y = torch.nn.functional.linear(x2, W, b)
+        return torch.nn.functional.gelu(y) if act == _GELU else y
+
+    def _add_ln(self, x, res, g, b):
+        eps = self.config.layer_norm_eps
+        if x.is_cuda:
+            return _native.C().add_layernorm(x.contiguous(), None if res is None else res.contiguous(), g.detach(),
+                                             b.detach(), eps)
+        return torch.nn.functional.layer_norm(x if res is None else x + res, (x.shape[-1],), g, b, eps)
+
+    @torch.no_grad()
+    def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
+                token_type_ids: torch.Tensor | None = None) -> torch.Tensor:
+        cfg = self.config
+        B, S = input_ids.shape
+        H, nh = cfg.hidden_size, cfg.num_attention_heads
+        dh = H // nh
+        ids = input_ids.long().contiguous()
+        tt = None if token_type_ids is None else token_type_ids.long().contiguous()
+        word, pos = self.p("embeddings.word_embeddings.weight"), self.p("embeddings.position_embeddings.weight")
+        typ = self.p("embeddings.token_type_embeddings.weight")
+        g0, b0 = self.p("embeddings.LayerNorm.weight"), self.p("embeddings.LayerNorm.bias")
+        if ids.is_cuda:
+            x = _native.C().embed_layernorm(ids, tt, word.detach(), pos.detach(), typ.detach(), g0.detach(),
+                                            b0.detach(), cfg.layer_norm_eps)
+        else:
+            e = word[ids] + typ[tt if tt is not None else torch.zeros_like(ids)] + pos[:S].unsqueeze(0)
+            x = torch.nn.functional.layer_norm(e, (H,), g0, b0, cfg.layer_norm_eps)
+        # additive mask: 0 where attended, the dtype minimum where padded (as transformers)
+        bias = None
+        if attention_mask is not None:
+            m = attention_mask.to(x.dtype).view(B, 1, 1, S)
+            bias = (1.0 - m) * torch.finfo(x.dtype).min
+        scale = 1.0 / math.sqrt(dh)
+        for i in range(cfg.num_hidden_layers):
+            n = _layer_names(i)
+            x2 = x.reshape(B * S, H)
+            Wqkv, bqkv = self._qkv(i)
+            qkv = self._linear(x2, Wqkv, bqkv).view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4)   # [3, B, nh, S, dh]
+            q, k, v = qkv[0], qkv[1], qkv[2]
+            sc = torch.matmul(q, k.transpose(-1, -2)) * scale
+            if bias is not None:
+                sc = sc + bias
+            ctx = torch.matmul(torch.softmax(sc, dim=-1), v).permute(0, 2, 1, 3).reshape(B * S, H)
+            a = self._linear(ctx.contiguous(), self.p(n["o"] + ".weight").detach(), self.p(n["o"] + ".bias").detach())
+            x2 = self._add_ln(a, x2, self.p(n["ln1"] + ".weight"), self.p(n["ln1"] + ".bias"))
+            h = self._linear(x2, self.p(n["up"] + ".weight").detach(), self.p(n["up"] + ".bias").detach(), _GELU)
+            o = self._linear(h, self.p(n["down"] + ".weight").detach(), self.p(n["down"] + ".bias").detach())
+            x = self._add_ln(o, x2, self.p(n["ln2"] + ".weight"), self.p(n["ln2"] + ".bias")).view(B, S, H)
+        return x
+
+
+class WordPiece:
+    """BERT's uncased WordPiece tokenizer over a ``vocab.txt`` (the ``tokenizers`` library), or —
+    for tests without a vocabulary — a hashing stand-in mapping each word to one id."""
+
+    def __init__(self, vocab_path: str | None = None, vocab_size: int = 30522, lowercase: bool = True):
+        self.vocab_size = vocab_size
+        self.tok = None
+        if vocab_path is not None:
+            from tokenizers import BertWordPieceTokenizer
+            self.tok = BertWordPieceTokenizer(vocab_path, lowercase=lowercase)
+            self.vocab_size = self.tok.get_vocab_size()
+        self.cls_id, self.sep_id = (self.tok.token_to_id("[CLS]"), self.tok.token_to_id("[SEP]")) if self.tok else (1, 2)
+
+    def word_ids(self, word: str) -> list[int]:
+        if self.tok is not None:
+            return self.tok.encode(word, add_special_tokens=False).ids or [self.tok.token_to_id("[UNK]")]
+        import zlib
+        return [3 + zlib.crc32(word.encode()) % (self.vocab_size - 3)]
+
+
+def bert_embedder(model: BertEncoder, tokenizer: WordPiece, max_len: int | None = None):
+    """``embed(tokens) -> [n_tokens, H]`` contextual token vectors for :class:`~avenir_amd.text.
+    semsearch.SemanticSearch`: the token sequence is encoded as ONE [CLS] ... [SEP] input (windows
+    of ``max_len`` word pieces for long texts), and each token's vector is the mean of its word
+    pieces' last hidden states — the alignment spaCy-transformers uses for ``token.vector``."""
+    dev = next(model.parameters()).device
+    L = max_len or model.config.max_position_embeddings
+
+    def emb(tokens):
+        if not tokens:
+            return torch.zeros((0, model.config.hidden_size), device=dev)
+        pieces, owner = [], []
+        for t, w in enumerate(tokens):
+            ids = tokenizer.word_ids(w)
+            pieces += ids
+            owner += [t] * len(ids)
+        out = torch.zeros((len(tokens), model.config.hidden_size), device=dev)
+        cnt = torch.zeros(len(tokens), device=dev)
+        step = L - 2
+        for s0 in range(0, len(pieces), step):
+            ids = [tokenizer.cls_id] + pieces[s0:s0 + step] + [tokenizer.sep_id]
+            h = model(torch.tensor([ids], device=dev))[0, 1:-1]
+            ow = torch.tensor(owner[s0:s0 + step], device=dev)
+            out.index_add_(0, ow, h)
+            cnt.index_add_(0, ow, torch.ones_like(ow, dtype=torch.float32))
+        return out / cnt.clamp_min(1).view(-1, 1)
+    emb.model = model
+    return emb

@@ -1,0 +1,111 @@
+"""BERT encoder of semantic search (nn/bert.py) against transformers.BertModel (random weights: no
+pretrained checkpoint can be fetched here, so the architecture is what is pinned), the
+transformer.hip epilogues against torch, and SemanticSearch over BERT token vectors."""
+import pytest
+import torch
+
+from avenir_amd.nn.bert import BertConfig, BertEncoder, WordPiece, bert_embedder
+
+transformers = pytest.importorskip("transformers")
+
+
+def _pair(H=64, L=2, heads=4, I=128, V=300, P=64, seed=0):
+    cfg = transformers.BertConfig(vocab_size=V, hidden_size=H, num_hidden_layers=L, num_attention_heads=heads,
+                                  intermediate_size=I, max_position_embeddings=P)
+    torch.manual_seed(seed)
+    ref = transformers.BertModel(cfg).eval()
+    with torch.no_grad():          # non-trivial LayerNorm parameters and biases
+        for n, p in ref.named_parameters():
+            if "LayerNorm" in n or n.endswith("bias"):
+                p.add_(0.1 * torch.randn_like(p))
+    mine = BertEncoder(BertConfig.from_dict(cfg.to_dict())).load_hf_state_dict(ref.state_dict(), strict=True)
+    return ref, mine
+
+
+def _inputs(B=3, S=17, V=300, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, V, (B, S), generator=g)
+    mask = torch.ones(B, S, dtype=torch.long)
+    mask[1, 12:] = 0
+    mask[2, 5:] = 0
+    tt = torch.zeros(B, S, dtype=torch.long)
+    tt[:, S // 2:] = 1
+    return ids, mask, tt
+
+
+def test_bert_encoder_matches_transformers_cpu():
+    ref, mine = _pair()
+    ids, mask, tt = _inputs()
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=mask, token_type_ids=tt).last_hidden_state
+    got = mine(ids, mask, tt)
+    keep = mask.bool()
+    assert torch.allclose(got[keep], want[keep], atol=1e-5, rtol=1e-5)
+
+
+def test_bert_state_dict_prefix_and_strict():
+    ref, mine = _pair()
+    sd = {"bert." + k: v for k, v in ref.state_dict().items()}
+    BertEncoder(mine.config).load_hf_state_dict(sd)
+    with pytest.raises(KeyError):
+        BertEncoder(mine.config).load_hf_state_dict({k: v for k, v in ref.state_dict().items() if "layer.1." not in k})
+
+
+def test_semantic_search_with_bert_vectors():
+    from avenir_amd.text.semsearch import ALGOS, SemanticSearch
+    _, mine = _pair(V=1000, P=128)
+    ss = SemanticSearch(bert_embedder(mine, WordPiece(vocab_size=1000)))
+    docs = ["apple fruit fiber vitamin sugar.", "smartphone market share apple iphone samsung.",
+            "peach fruit sugar vitamin potassium."]
+    for d in docs:
+        ss.add(d)
+    for algo in ALGOS:
+        s = ss.scores("fruit vitamin sugar", algo)
+        assert s.shape == (3,) and bool(torch.isfinite(s).all())
+
+
+@pytest.mark.gpu
+def test_bert_encoder_gpu_kernels_match_transformers(cuda):
+    ref, mine = _pair(H=128, L=2, heads=4, I=512, V=500, P=64)
+    ids, mask, tt = _inputs(B=4, S=33, V=500)
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=mask, token_type_ids=tt).last_hidden_state
+    got = mine.to(cuda)(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu()
+    keep = mask.bool()
+    assert torch.allclose(got[keep], want[keep], atol=2e-4, rtol=2e-4), (got[keep] - want[keep]).abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H", [64, 128, 260, 768, 1024])
+def test_add_layernorm_and_embed_layernorm_kernels(cuda, H):
+    from avenir_amd import _native
+    g = torch.Generator().manual_seed(H)
+    x, r = torch.randn(37, 5, H, generator=g), torch.randn(37, 5, H, generator=g)
+    gam, bet = torch.randn(H, generator=g), torch.randn(H, generator=g)
+    got = _native.C().add_layernorm(x.to(cuda), r.to(cuda), gam.to(cuda), bet.to(cuda), 1e-12).cpu()
+    want = torch.nn.functional.layer_norm((x + r).double(), (H,), gam.double(), bet.double(), 1e-12)
+    assert torch.allclose(got.double(), want, atol=2e-5, rtol=1e-5)
+    got0 = _native.C().add_layernorm(x.to(cuda), None, gam.to(cuda), bet.to(cuda), 1e-5).cpu()
+    assert torch.allclose(got0.double(), torch.nn.functional.layer_norm(x.double(), (H,), gam.double(), bet.double(),
+                                                                          1e-5), atol=2e-5, rtol=1e-5)
+    word, pos, typ = (torch.randn(n, H, generator=g) for n in (50, 16, 2))
+    ids = torch.randint(0, 50, (3, 16), generator=g)
+    tt = torch.randint(0, 2, (3, 16), generator=g)
+    got = _native.C().embed_layernorm(ids.to(cuda), tt.to(cuda), word.to(cuda), pos.to(cuda), typ.to(cuda),
+                                      gam.to(cuda), bet.to(cuda), 1e-12).cpu()
+    e = word[ids].double() + typ[tt].double() + pos.double().unsqueeze(0)
+    want = torch.nn.functional.layer_norm(e, (H,), gam.double(), bet.double(), 1e-12)
+    assert torch.allclose(got.double(), want, atol=2e-5, rtol=1e-5)
+    with pytest.raises(RuntimeError):
+        _native.C().embed_layernorm(torch.full((1, 4), 50, device=cuda), None, word.to(cuda), pos.to(cuda),
+                                    typ.to(cuda), gam.to(cuda), bet.to(cuda), 1e-12)
+
+
+@pytest.mark.gpu
+def test_linear_gelu_epilogue(cuda):
+    from avenir_amd import _native
+    g = torch.Generator().manual_seed(0)
+    X, W, b = torch.randn(300, 96, generator=g), torch.randn(200, 96, generator=g) * 0.1, torch.randn(200, generator=g)
+    got = _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 6).cpu()
+    want = torch.nn.functional.gelu(X.double() @ W.double().T + b.double())
+    assert torch.allclose(got.double(), want, atol=1e-4, rtol=1e-4)
