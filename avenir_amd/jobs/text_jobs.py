@@ -390,14 +390,28 @@ def text_classifier(args):
      aliases=("ssearch",))
 def semantic_search(args):
     """Algorithms: tokenMax, tokenAvMax, tokenMaxAv, tokenAv, tokenMed, sentAv, sentMed, sentMax,
-    docAv (text/semsearch.py).  The embedder is trained on the corpus itself (no spacy model)."""
-    from ..text.semsearch import ALGOS, search_corpus
+    docAv (text/semsearch.py).  Embedder: with ``bert.model.dir`` (a directory holding a Hugging
+    Face BERT ``config.json``, ``model.safetensors`` or ``pytorch_model.bin`` and ``vocab.txt`` —
+    e.g. bert-base-uncased, the model behind the reference's spaCy pipeline) the contextual token
+    vectors of nn/bert.py; otherwise a skip-gram embedder trained on the corpus itself."""
+    from ..text.semsearch import ALGOS, SemanticSearch, search_corpus
     ctx = JobContext(args)
     algo = args.mode or "tokenAvMax"
     if algo not in ALGOS:
         raise SystemExit(f"invalid algorithm {algo}; one of {', '.join(ALGOS)}")
     texts, names = _docs(_input(ctx))
-    ss = search_corpus(texts, dim=ctx.get_int("embed.dim", 100), epochs=ctx.get_int("embed.epochs", 10),
-                       device=ctx.device, seed=args.seed)
+    bert_dir = ctx.get("bert.model.dir", None)
+    if bert_dir:
+        import os
+        from ..nn.bert import BertEncoder, WordPiece, bert_embedder
+        enc = BertEncoder.from_pretrained_dir(bert_dir, device=ctx.device)
+        vocab = os.path.join(bert_dir, "vocab.txt")
+        ss = SemanticSearch(bert_embedder(enc, WordPiece(vocab if os.path.exists(vocab) else None,
+                                                         enc.config.vocab_size)), device=ctx.device)
+        for t in texts:
+            ss.add(t)
+    else:
+        ss = search_corpus(texts, dim=ctx.get_int("embed.dim", 100), epochs=ctx.get_int("embed.epochs", 10),
+                           device=ctx.device, seed=args.seed)
     top = int(args.k or len(texts))
     _out(ctx, [f"{i},{names[i]},{s:.6f}" for i, s in ss.search(args.name or "", algo, top)])

@@ -11,11 +11,12 @@ weights instead.
 MI355X path (inference, fp32 like the reference's model):
 * embeddings: word + position + token-type gathers, the sum and the LayerNorm in ONE kernel
   (transformer.hip ``embed_layernorm_kernel``);
-* per layer: the Q, K, V projections as ONE f32-MFMA GEMM with concatenated weights (mlp.hip
-  ``linear_act_fwd``), attention scores / softmax / context as batched library GEMMs (hipBLASLt),
-  the output projection, then residual + LayerNorm in ONE pass (``add_layernorm_kernel``); the
-  feed-forward up-projection with bias + GELU in the GEMM's epilogue, the down-projection, residual +
-  LayerNorm again.
+* per layer: the Q, K, V projections as ONE GEMM with concatenated weights, attention scores /
+  softmax / context as batched library GEMMs (hipBLASLt), the output projection, then residual +
+  LayerNorm in ONE pass (``add_layernorm_kernel``); the feed-forward up-projection with bias + GELU,
+  the down-projection, residual + LayerNorm again.  Projections of up to ``MFMA_MAX_ROWS`` rows (a
+  query, a short document) run on mlp.hip's f32-MFMA tile kernel with bias and GELU in its
+  epilogue; larger batches on hipBLASLt (profiles/r5_bert_base_bench.jsonl).
 CPU tensors run the same math with torch ops.
 """
 from __future__ import annotations
@@ -165,8 +166,13 @@ class BertEncoder(torch.nn.Module):
         self._qkv_cache[i] = (key, W, b)
         return W, b
 
+    #: rows from which the projections run on hipBLASLt (+ a separate erf-GELU pass) instead of the
+    #: f32-MFMA tile kernel with the GELU epilogue: measured at bert-base shapes, the tile kernel wins
+    #: at B x S = 128 (2.40 vs 3.00 ms per encoder pass) and loses at 4,096-16,384 rows (8.2 vs 6.6 ms)
+    MFMA_MAX_ROWS = int(os.environ.get("AVMI_BERT_MFMA_MAX_ROWS", "1024"))
+
     def _linear(self, x2, W, b, act: int = 0):
-        if x2.is_cuda:
+        if x2.is_cuda and x2.shape[0] <= self.MFMA_MAX_ROWS:
             return _native.C().linear_act_fwd(x2, W, b, act)
         y = torch.nn.functional.linear(x2, W, b)
         return torch.nn.functional.gelu(y) if act == _GELU else y

@@ -109,3 +109,27 @@ def test_linear_gelu_epilogue(cuda):
     got = _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 6).cpu()
     want = torch.nn.functional.gelu(X.double() @ W.double().T + b.double())
     assert torch.allclose(got.double(), want, atol=1e-4, rtol=1e-4)
+
+
+def test_semantic_search_job_with_a_bert_model_dir(tmp_path):
+    """The semanticSearch CLI job on a Hugging Face model directory (config.json +
+    model.safetensors + vocab.txt, written by transformers.save_pretrained)."""
+    from avenir_amd.cli import main
+    words = "apple fruit fiber vitamin sugar smartphone market share iphone samsung peach potassium".split()
+    vocab = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"] + words + [".", ","]
+    ref, _ = _pair(V=len(vocab), P=64)
+    d = tmp_path / "bert"
+    ref.save_pretrained(str(d))
+    (d / "vocab.txt").write_text("\n".join(vocab) + "\n")
+    corpus = tmp_path / "docs"
+    corpus.mkdir()
+    (corpus / "d1.txt").write_text("apple fruit fiber vitamin sugar.")
+    (corpus / "d2.txt").write_text("smartphone market share apple iphone samsung.")
+    (corpus / "d3.txt").write_text("peach fruit sugar vitamin potassium.")
+    cfg = tmp_path / "ss.properties"
+    cfg.write_text(f"bert.model.dir={d}\n")
+    out = tmp_path / "out.txt"
+    assert main(["semanticSearch", "-i", str(corpus), "-o", str(out), "-c", str(cfg), "--mode", "docAv",
+                 "--name", "fruit vitamin"]) == 0
+    lines = out.read_text().split()
+    assert len(lines) == 3 and all(len(l.split(",")) == 3 for l in lines)
