@@ -206,12 +206,22 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       const float qn = gq < M ? sqn[my_q] : INFINITY;  // padded query rows never insert
       const int jb = (int)(r0 - rb) + wr * 32 + 4 * (lane >> 5);
       if (r0 + BR <= re && !exclude_self) {
-        // full tile, no self exclusion (uniform): 3 VALU ops + one compare per candidate
-#pragma unroll 2
+        // full tile, no self exclusion (uniform): the lane's 16 distances, then ONE test of their
+        // minimum against the current k-th best — once the lists have filled, a tile rarely holds
+        // a better candidate, and the per-candidate compare-and-branch was the kernel's VALU / SALU
+        // bound at small D
+        float dv[16];
+#pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ro = (r & 3) + 8 * (r >> 2);
-          const float dist = fmaxf(fmaf(-2.f, acc[r], qn + srn[wr * 32 + 4 * (lane >> 5) + ro]), 0.f);
-          topk_insert<K>(bd, bi, dist, jb + ro);
+          dv[r] = fmaxf(fmaf(-2.f, acc[r], qn + srn[wr * 32 + 4 * (lane >> 5) + ro]), 0.f);
+        }
+        float mn = dv[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mn = fminf(mn, dv[r]);
+        if (mn < bd[K - 1]) {
+#pragma unroll 2
+          for (int r = 0; r < 16; ++r) topk_insert<K>(bd, bi, dv[r], jb + (r & 3) + 8 * (r >> 2));
         }
       } else {
 #pragma unroll 2
