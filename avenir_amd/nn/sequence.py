@@ -10,6 +10,11 @@ activation, seq-to-one (last step) or seq-to-seq.  Differences from the referenc
   :267-273, which breaks GPU training);
 * one checkpoint key (the reference saves under ``train.save.model`` but reads
   ``train.model.save``, :84 vs :337).
+Data-parallel training (SURVEY N7 "optional DDP over RCCL"): with a multi-rank communicator every
+rank fits its own row shard; the replicas start from rank 0's parameters, and each step sums the
+gradients of all ranks in ONE coalesced all-reduce (RCCL over xGMI on GPUs) before clipping and the
+optimiser — the global-batch gradient, so W ranks of local batch b train like one process with
+batch W x b.
 """
 from __future__ import annotations
 
@@ -17,6 +22,7 @@ import numpy as np
 import torch
 
 from ..ops.rnn import FusedLSTM
+from ..parallel.comm import get_comm
 from .common import (GraphedStep, _cfg, create_activation, create_loss, load_checkpoint, optimizer_from_config, pick_device,
                      save_checkpoint, scale_data)
 
@@ -48,6 +54,7 @@ class LstmNetwork(torch.nn.Module):
                                                capturable=self.device.type == "cuda" and graph)
         self.conf = conf
         self.losses: list[float] = []
+        self._dp = None          # the communicator of a data-parallel fit
 
     @classmethod
     def from_config(cls, conf, device=None) -> "LstmNetwork":
@@ -106,33 +113,63 @@ class LstmNetwork(torch.nn.Module):
             out = out.reshape(-1, out.shape[-1])
         loss = self.loss_fn(out, tgt)
         loss.backward()
+        if self._dp is not None:
+            self._allreduce_grads(self._dp)
         if self.grad_clip:
             torch.nn.utils.clip_grad_norm_(self.parameters(), self.grad_clip, foreach=True)
         self.optimizer.step()
         return loss.detach()
 
-    def fit(self, x: torch.Tensor, y: torch.Tensor, num_iter: int | None = None, seed: int = 0) -> "LstmNetwork":
+    def _allreduce_grads(self, comm):
+        """Average the gradients over the ranks: one flat buffer, one all-reduce."""
+        grads = [p.grad for p in self.parameters() if p.grad is not None]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        comm.all_reduce(flat)
+        flat.div_(comm.world)
+        off = 0
+        for g in grads:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+
+    def fit(self, x: torch.Tensor, y: torch.Tensor, num_iter: int | None = None, seed: int = 0,
+            comm=None) -> "LstmNetwork":
         """``num_iter`` epochs of shuffled fixed-size mini-batches.  On the GPU the whole step
-        (fused-LSTM forward, loss, backward, clipping, optimiser) is one captured HIP graph."""
+        (fused-LSTM forward, loss, backward, clipping, optimiser) is one captured HIP graph.  With a
+        multi-rank communicator (``comm`` or the process default) each rank passes its own rows:
+        replicas synchronised from rank 0, gradients averaged every step, the same number of steps
+        on every rank (the smallest shard's), eager steps."""
+        comm = comm if comm is not None else get_comm()
+        dp = comm if comm.is_distributed else None
         x = x.to(self.device).float()
         tgt = self._target(y.to(self.device))
         n = x.shape[0]
         bs = min(self.batch_size, n)
         nb = max(n // bs, 1)
+        if dp is not None:
+            for p in self.parameters():
+                dp.broadcast(p.data, 0)
+            t = torch.tensor([nb], dtype=torch.long)
+            dp.all_reduce(t, "min")
+            nb = int(t)
         g = torch.Generator().manual_seed(seed)
         self.train()
+        self._dp = dp
         step = None
-        for _ in range(num_iter if num_iter is not None else self.num_iter):
-            perm = torch.randperm(n, generator=g).to(self.device)[: nb * bs]
-            xb = x[perm].view((nb, bs) + tuple(x.shape[1:]))
-            yb = tgt[perm].view((nb, bs) + tuple(tgt.shape[1:]))
-            if step is None:
-                step = GraphedStep(self._step, xb[0], yb[0], enabled=self.use_graph and self.device.type == "cuda",
-                                   model=self, optimizer=self.optimizer)
-            tot = torch.zeros((), device=self.device)
-            for b in range(nb):
-                tot += step(xb[b], yb[b])
-            self.losses.append(float(tot) / nb)
+        try:
+            for _ in range(num_iter if num_iter is not None else self.num_iter):
+                perm = torch.randperm(n, generator=g).to(self.device)[: nb * bs]
+                xb = x[perm].view((nb, bs) + tuple(x.shape[1:]))
+                yb = tgt[perm].view((nb, bs) + tuple(tgt.shape[1:]))
+                if step is None:
+                    step = GraphedStep(self._step, xb[0], yb[0],
+                                       enabled=self.use_graph and self.device.type == "cuda" and dp is None,
+                                       model=self, optimizer=self.optimizer)
+                tot = torch.zeros((), device=self.device)
+                for b in range(nb):
+                    tot += step(xb[b], yb[b])
+                self.losses.append(float(tot) / nb)
+        finally:
+            self._dp = None
         self.eval()
         return self
 

@@ -1,0 +1,41 @@
+"""LstmNetwork data-parallel training: W ranks with local batch b train like one process with
+batch W x b (replicas from rank 0, gradients averaged each step) — gloo ranks on the CPU."""
+import torch
+
+from tests._dist import run_world
+
+
+def _data(n=64, T=5, I=2, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(n, T * I, generator=g)
+    y = (x.sum(1) > T * I / 2).float()
+    return x, y
+
+
+def _net(seed):
+    from avenir_amd.nn.sequence import LstmNetwork
+    torch.manual_seed(seed)
+    return LstmNetwork(2, 8, 1, num_layers=2, seq_len=5, batch_size=1 << 20, lr=0.01, num_iter=3, device="cpu",
+                       out_sequence=False)
+
+
+def _rank_fit(rank, world):
+    x, y = _data()
+    net = _net(seed=100 + rank)          # different local init: the fit must start from rank 0's
+    sh = slice(rank * (64 // world), (rank + 1) * (64 // world))
+    net.fit(net.to_sequences(x[sh]), y[sh], num_iter=3)
+    return {k: v.detach().clone() for k, v in net.state_dict().items()}, net.losses
+
+
+def test_two_ranks_equal_one_process_with_the_global_batch():
+    x, y = _data()
+    ref = _net(seed=100)                 # rank 0's initialisation
+    ref.fit(ref.to_sequences(x), y, num_iter=3)
+    res = run_world(_rank_fit, 2)
+    (sd0, l0), (sd1, l1) = res
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd0[k], v, atol=2e-6, rtol=1e-5), k
+        assert torch.equal(sd0[k], sd1[k]), k          # replicas identical
+    # the local losses average to the global-batch loss
+    for a, b, c in zip(l0, l1, ref.losses):
+        assert abs((a + b) / 2 - c) < 1e-5
