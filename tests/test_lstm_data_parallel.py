@@ -39,3 +39,33 @@ def test_two_ranks_equal_one_process_with_the_global_batch():
     # the local losses average to the global-batch loss
     for a, b, c in zip(l0, l1, ref.losses):
         assert abs((a + b) / 2 - c) < 1e-5
+
+
+def _rank_fit_gpu(rank, world):
+    import torch as T
+    from avenir_amd.nn.sequence import LstmNetwork
+    x, y = _data()
+    T.manual_seed(100 + rank)
+    net = LstmNetwork(2, 8, 1, num_layers=2, seq_len=5, batch_size=1 << 20, lr=0.01, num_iter=3, device="cuda",
+                      out_sequence=False)
+    sh = slice(rank * (64 // world), (rank + 1) * (64 // world))
+    net.fit(net.to_sequences(x[sh]), y[sh], num_iter=3)
+    return {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_the_gpu_equal_one_process(cuda):
+    """The fused fp32 LSTM kernels in both ranks (sharing cuda:0, gradients over gloo)."""
+    from avenir_amd.nn.sequence import LstmNetwork
+    x, y = _data()
+    torch.manual_seed(100)
+    ref = LstmNetwork(2, 8, 1, num_layers=2, seq_len=5, batch_size=1 << 20, lr=0.01, num_iter=3, device=cuda,
+                      out_sequence=False)
+    ref.fit(ref.to_sequences(x), y, num_iter=3)
+    sd0, sd1 = run_world(_rank_fit_gpu, 2, comm="gloo:cuda")
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd0[k], v.cpu(), atol=1e-5, rtol=1e-4), k
+        assert torch.equal(sd0[k], sd1[k]), k
