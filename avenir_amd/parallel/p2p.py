@@ -36,6 +36,13 @@ class P2PError(RuntimeError):
     pass
 
 
+def _agree(comm, ok: bool) -> bool:
+    """All ranks' ``ok`` AND-ed (one min all-reduce through the library collective)."""
+    f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm.device)
+    comm.all_reduce(f, "min", algo="ring")
+    return bool(f.item())
+
+
 class P2PAllReduce:
     """One communicator's peer-mapped all-reduce state.  Construct on every rank together."""
 
@@ -49,12 +56,39 @@ class P2PAllReduce:
         self.device = device
         self.world, self.rank = comm.world, comm.rank
         uncached = os.environ.get("AVMI_P2P_UNCACHED", "0") == "1"
-        self._h = _native.C().P2PComm(device.index, cap, uncached)
-        self.cap_bytes = int(self._h.cap_bytes)
-        self._h.set_timeout(float(timeout_s or os.environ.get("AVMI_P2P_TIMEOUT_S", "10")))
-        handles = comm.all_gather_object(bytes(self._h.handles()))
-        self._h.open(list(handles), self.rank, self.world)
-        comm.barrier()
+        # every step that can fail on ONE rank (allocation, export, mapping a peer) is followed by
+        # an agreement all-reduce, so all ranks raise together and the collective sequence of the
+        # caller stays aligned (a rank leaving early would pair its next collective with a peer's
+        # barrier here)
+        self._h, err = None, None
+        try:
+            self._h = _native.C().P2PComm(device.index, cap, uncached)
+            self.cap_bytes = int(self._h.cap_bytes)
+            self._h.set_timeout(float(timeout_s or os.environ.get("AVMI_P2P_TIMEOUT_S", "10")))
+            mine = bytes(self._h.handles())
+        except Exception as e:     # noqa: BLE001 - reported through the agreement below
+            err, mine = e, b""
+        handles = comm.all_gather_object(mine)
+        if err is None and all(handles):
+            try:
+                self._h.open(list(handles), self.rank, self.world)
+            except Exception as e:  # noqa: BLE001
+                err = e
+        elif err is None:
+            err = P2PError("a peer could not export its staging region")
+        if not _agree(comm, err is None):
+            h, self._h = self._h, None
+            if h is not None:
+                try:
+                    h.close_peers()
+                except Exception:  # noqa: BLE001 - nothing mapped yet
+                    pass
+            comm.barrier()         # every rank: no peer still maps this rank's region
+            if h is not None:
+                h.release()
+            raise P2PError(f"rank {self.rank}: peer-mapped all-reduce unavailable "
+                           f"({err!r} here)" if err is not None else
+                           f"rank {self.rank}: peer-mapped all-reduce unavailable on another rank")
         self.epoch = 0
         self.calls = {"oneshot": 0, "twoshot": 0}
 
@@ -80,6 +114,10 @@ class P2PAllReduce:
         if x is not t:
             t.copy_(x)
         return t
+
+    def ok(self) -> bool:
+        """True when no wait of this rank's kernels timed out (synchronises the device; local)."""
+        return int(self._h.status()) == 0
 
     def check(self) -> None:
         """Raise if any wait of this rank's kernels timed out (synchronises the device)."""

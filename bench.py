@@ -79,22 +79,30 @@ def _allreduce_probe(comm, dev) -> list:
         t = comm.reduce_max_scalar(t)
         out.append({"bytes": nbytes, "algo": "allgather_ordered_sum", "us": t * 1e6})
     # hand-written peer-mapped kernels (csrc/kernels/comm.hip): one-shot / two-shot over xGMI
+    # (construction agrees over ranks and raises on all of them together; the kernels' waits are
+    # bounded, so a rank out of step shows as a status word, and every rank reaches every collective)
     try:
-        for nbytes, iters in ((8 << 10, 100), (64 << 10, 100), (1 << 20, 50)):
-            x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
-            for _ in range(5):
-                comm.all_reduce(x, algo="p2p")
-            comm.barrier()
-            t = _timed(lambda: [comm.all_reduce(x, algo="p2p") for _ in range(iters)], dev) / iters
-            x.fill_(float(comm.rank + 1))
-            comm.all_reduce(x, algo="p2p")
-            comm.p2p().check()
-            exact = bool((x == float(W * (W + 1) // 2)).all().item())
-            t = comm.reduce_max_scalar(t)
-            out.append({"bytes": nbytes, "algo": "p2p_" + ("oneshot" if nbytes <= comm.p2p().oneshot_max else "twoshot"),
-                        "us": t * 1e6, "exact": exact})
+        p = comm.p2p()
     except Exception as e:          # the probe must never cost the measured headline
         out.append({"algo": "p2p", "error": repr(e)})
+        return out
+    for nbytes, iters in ((8 << 10, 100), (64 << 10, 100), (1 << 20, 50)):
+        x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+        for _ in range(5):
+            comm.all_reduce(x, algo="p2p")
+        f = torch.tensor([1 if p.ok() else 0], device=dev)
+        comm.all_reduce(f, "min", algo="ring")
+        if not bool(f.item()):                      # out of step: every later call would wait out its bound
+            out.append({"bytes": nbytes, "algo": "p2p", "error": "a bounded wait timed out on some rank"})
+            break
+        comm.barrier()
+        t = _timed(lambda: [comm.all_reduce(x, algo="p2p") for _ in range(iters)], dev) / iters
+        x.fill_(float(comm.rank + 1))
+        comm.all_reduce(x, algo="p2p")
+        exact = bool((x == float(W * (W + 1) // 2)).all().item()) and p.ok()
+        t = comm.reduce_max_scalar(t)
+        out.append({"bytes": nbytes, "algo": "p2p_" + ("oneshot" if nbytes <= p.oneshot_max else "twoshot"),
+                    "us": t * 1e6, "exact": exact})
     return out
 
 
@@ -109,32 +117,42 @@ def _pick_small_allreduce(comm, like: torch.Tensor, mode: str) -> dict:
         return info
     W = comm.world
     x = torch.empty_like(like)
+
+    def agree(ok: bool) -> bool:                      # every rank takes the same branch
+        f = torch.tensor([1 if ok else 0], device=like.device)
+        comm.all_reduce(f, "min", algo="ring")
+        return bool(f.item())
+
+    # Every step below is either a kernel (bounded waits: a peer that is out of step sets a status
+    # word, never hangs) or a collective that ALL ranks reach: a failure on one rank is carried by
+    # the agreement all-reduces, never by an exception that would skip a collective on that rank.
+    use = False
     try:
+        p = comm.p2p()                                # collective; raises on every rank together
+    except Exception as e:      # no peer mapping on this node: the library collective
+        info["p2p_error"] = repr(e)
+        p = None
+    if p is not None:
         ok = True
         for i in range(20):
             x.fill_(comm.rank + 1 + i)
             comm.all_reduce(x, algo="p2p")
             ok &= bool((x == W * (W + 1) // 2 + W * i).all().item())
-        comm.p2p().check()
-        okt = torch.tensor([1 if ok else 0], device=like.device)
-        comm.all_reduce(okt, "min")
-        info["p2p_exact"] = bool(okt.item())
-        times = {}
-        for name, fn in (("rccl", lambda: comm.all_reduce(x, algo="ring")),
-                         ("p2p", lambda: comm.all_reduce(x, algo="p2p"))):
-            for _ in range(5):
-                fn()
-            comm.barrier()
-            times[name] = comm.reduce_max_scalar(_timed(lambda: [fn() for _ in range(50)], like.device) / 50)
-        comm.p2p().check()
-        info.update({f"{k}_us": v * 1e6 for k, v in times.items()})
-        use = info["p2p_exact"] and (mode == "p2p" or times["p2p"] < times["rccl"])
-    except Exception as e:      # no peer mapping on this node: the library collective
-        info["p2p_error"] = repr(e)
-        use = False
-    flag = torch.tensor([1 if use else 0], device=like.device)
-    comm.all_reduce(flag, "min")                      # every rank takes the same path
-    info["chosen"] = "p2p" if int(flag.item()) else "rccl"
+            if i == 0 and not agree(ok and p.ok()):   # out of step: stop before 19 more bounded waits
+                ok = False
+                break
+        info["p2p_exact"] = agree(ok and p.ok())
+        if info["p2p_exact"]:
+            times = {}
+            for name, fn in (("rccl", lambda: comm.all_reduce(x, algo="ring")),
+                             ("p2p", lambda: comm.all_reduce(x, algo="p2p"))):
+                for _ in range(5):
+                    fn()
+                comm.barrier()
+                times[name] = comm.reduce_max_scalar(_timed(lambda: [fn() for _ in range(50)], like.device) / 50)
+            info.update({f"{k}_us": v * 1e6 for k, v in times.items()})
+            use = agree(p.ok()) and (mode == "p2p" or times["p2p"] < times["rccl"])
+    info["chosen"] = "p2p" if use else "rccl"
     comm.small_allreduce = "p2p" if info["chosen"] == "p2p" else None
     return info
 

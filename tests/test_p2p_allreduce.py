@@ -145,3 +145,51 @@ def test_p2p_reference_sum_is_order_sensitive():
     fwd = _ordered_sum(pool[0])
     rev = _ordered_sum(pool[0].flip(0))
     assert not torch.equal(fwd, rev)
+
+
+class _FakeHandle:
+    """Stands in for the native P2PComm on CPU: rank 1 fails to map its peers."""
+    released = False
+
+    def __init__(self, dev, cap, uncached):
+        self.cap_bytes = cap
+
+    def set_timeout(self, s):
+        pass
+
+    def handles(self):
+        return b"h"
+
+    def open(self, handles, rank, world):
+        if rank == 1:
+            raise RuntimeError("ipc open (data): invalid argument")
+
+    def close_peers(self):
+        pass
+
+    def release(self):
+        _FakeHandle.released = True
+
+
+def _p2p_open_fails_on_one_rank(rank, world):
+    from avenir_amd import _native
+    from avenir_amd.parallel import comm as C
+    from avenir_amd.parallel.p2p import P2PAllReduce, P2PError
+
+    class _Lib:
+        P2PComm = _FakeHandle
+    _native.C = lambda: _Lib
+    c = C.get_comm()
+    with pytest.raises(P2PError):
+        P2PAllReduce(c, torch.device("cuda", 0))
+    # the collective sequence is still aligned on every rank after the failure
+    x = torch.tensor([float(rank + 1)])
+    c.all_reduce(x)
+    return float(x.item()), _FakeHandle.released
+
+
+def test_p2p_construction_failure_on_one_rank_raises_everywhere():
+    """A peer mapping that fails on ONE rank makes every rank raise (agreement all-reduce), frees
+    every rank's region after a common barrier, and leaves the ranks' collectives in step."""
+    out = run_world(_p2p_open_fails_on_one_rank, 2)
+    assert out == [(3.0, True), (3.0, True)]
