@@ -12,7 +12,7 @@ MI355X path (inference, fp32 like the reference's model):
 * embeddings: word + position + token-type gathers, the sum and the LayerNorm in ONE kernel
   (transformer.hip ``embed_layernorm_kernel``);
 * per layer: the Q, K, V projections as ONE GEMM with concatenated weights, attention scores /
-  softmax / context as batched library GEMMs (hipBLASLt), the output projection, then residual +
+  mask / softmax / context in torch's fused attention kernel, the output projection, then residual +
   LayerNorm in ONE pass (``add_layernorm_kernel``); the feed-forward up-projection with bias + GELU,
   the down-projection, residual + LayerNorm again.  Projections of up to ``MFMA_MAX_ROWS`` rows (a
   query, a short document) run on mlp.hip's f32-MFMA tile kernel with bias and GELU in its
@@ -214,10 +214,10 @@ class BertEncoder(torch.nn.Module):
             Wqkv, bqkv = self._qkv(i)
             qkv = self._linear(x2, Wqkv, bqkv).view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4)   # [3, B, nh, S, dh]
             q, k, v = qkv[0], qkv[1], qkv[2]
-            sc = torch.matmul(q, k.transpose(-1, -2)) * scale
-            if bias is not None:
-                sc = sc + bias
-            ctx = torch.matmul(torch.softmax(sc, dim=-1), v).permute(0, 2, 1, 3).reshape(B * S, H)
+            # fused scores / mask / softmax / context (one library attention kernel instead of
+            # two batched GEMMs, a mask add and a softmax pass over [B, nh, S, S])
+            ctx = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=scale)
+            ctx = ctx.permute(0, 2, 1, 3).reshape(B * S, H)
             a = self._linear(ctx.contiguous(), self.p(n["o"] + ".weight").detach(), self.p(n["o"] + ".bias").detach())
             x2 = self._add_ln(a, x2, self.p(n["ln1"] + ".weight"), self.p(n["ln1"] + ".bias"))
             h = self._linear(x2, self.p(n["up"] + ".weight").detach(), self.p(n["up"] + ".bias").detach(), _GELU)
