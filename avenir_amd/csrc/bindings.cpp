@@ -2161,8 +2161,12 @@ at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::o
   }
   auto Y = at::empty({X.size(0), W.size(0)}, X.options());
   DevGuard g(X.device());
+  const int M = (int)X.size(0), N = (int)W.size(0), K = (int)X.size(1);
+  const int S = avk::linear_act_fwd_slices(M, N, K);
+  at::Tensor part;
+  if (S > 1) part = at::empty({(long long)S * M * N}, X.options());
   avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), bc.defined() ? bc.data_ptr<float>() : nullptr,
-                      Y.data_ptr<float>(), (int)X.size(0), (int)W.size(0), (int)X.size(1), (int)act, cur_stream(X));
+                      Y.data_ptr<float>(), M, N, K, (int)act, cur_stream(X), S > 1 ? part.data_ptr<float>() : nullptr, S);
   return Y;
 }
 

@@ -243,9 +243,11 @@ void forest_split(const long long* hist, const uint8_t* fmask, const int* bins, 
 void forest_part_count(const uint8_t* codes, long long ld, const int* item_node, const long long* item_start,
                        const int* item_len, int n_items, const int* feat, const int* thr, int* item_left,
                        hipStream_t stream);
-// K27 fused Linear + bias + activation (mlp.hip)
+// K27 fused Linear + bias + activation (mlp.hip); with S > 1 and a partial buffer of S*M*N floats
+// the K range is split over S slices (linear_act_fwd_slices picks S for few output tiles over a long K)
+int linear_act_fwd_slices(int M, int N, int K);
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
-                    hipStream_t stream);
+                    hipStream_t stream, float* partial = nullptr, int S = 1);
 int linear_act_bwd_blocks(int M);
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream);

@@ -110,6 +110,11 @@ int gemm_tn_slices(int K, int M, int N) {
   // one workgroup per CU (256), each slice at least 4 chunks of K: more slices only moved the time
   // into the partial traffic and the slice sum (74 slices of 2 chunks: 17.6 + 14.6 us at K = 5,000)
   long long s = (256 + tiles - 1) / tiles;
+  // a long K (65,536 sequences x T 5 = 327,680 rows): one workgroup per CU is ONE wave per SIMD and
+  // the staging latency is exposed (0.89 ms, MFMA busy 28 %, profiles/r5_round5_kernels_pmc.jsonl);
+  // four per CU once every slice still holds >= 16 chunks (the partials stay < 1/16 of the input)
+  const long long s4 = (1024 + tiles - 1) / tiles;
+  if ((long long)K >= s4 * 16 * KC) s = s4;
   s = std::min<long long>(s, std::max(1, K / (4 * KC)));
   return (int)std::max(1LL, std::min(s, 128LL));
 }

@@ -56,8 +56,9 @@ __device__ __forceinline__ float act_grad_from_y(float y, int act) {
 template <bool VEC>
 struct ChunkRegs {
   float x[8], w[8];
+  // rows of length K (the stride); columns k >= kend read as zero (the end of a split-K slice)
   __device__ __forceinline__ void load(const float* __restrict__ X, const float* __restrict__ W, long long m0, int n0,
-                                       int k0, int M, int N, int K) {
+                                       int k0, int M, int N, int K, int kend) {
     const int tid = threadIdx.x;
     if constexpr (VEC) {
 #pragma unroll
@@ -66,8 +67,8 @@ struct ChunkRegs {
         const long long m = m0 + row;
         const int n = n0 + row, k = k0 + c;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-        if (m < M && k < K) a = *reinterpret_cast<const float4*>(X + m * K + k);
-        if (n < N && k < K) b = *reinterpret_cast<const float4*>(W + (long long)n * K + k);
+        if (m < M && k < kend) a = *reinterpret_cast<const float4*>(X + m * K + k);
+        if (n < N && k < kend) b = *reinterpret_cast<const float4*>(W + (long long)n * K + k);
         x[4 * i] = a.x; x[4 * i + 1] = a.y; x[4 * i + 2] = a.z; x[4 * i + 3] = a.w;
         w[4 * i] = b.x; w[4 * i + 1] = b.y; w[4 * i + 2] = b.z; w[4 * i + 3] = b.w;
       }
@@ -77,8 +78,8 @@ struct ChunkRegs {
         const int e = tid + MT * i, row = e / KC, c = e % KC;
         const long long m = m0 + row;
         const int n = n0 + row, k = k0 + c;
-        x[i] = (m < M && k < K) ? X[m * K + k] : 0.f;
-        w[i] = (n < N && k < K) ? W[(long long)n * K + k] : 0.f;
+        x[i] = (m < M && k < kend) ? X[m * K + k] : 0.f;
+        w[i] = (n < N && k < kend) ? W[(long long)n * K + k] : 0.f;
       }
     }
   }
@@ -105,26 +106,30 @@ struct ChunkRegs {
   }
 };
 
-template <bool VEC>
+// SPLIT: blockIdx.z is a slice [z kper, (z + 1) kper) of K and the raw tile goes to
+// P[z][M][N] (bias and activation applied by linear_splitk_epilogue_kernel after the slice sum)
+template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W,
                                                              const float* __restrict__ b, float* __restrict__ Y,
-                                                             int M, int N, int K, int act) {
+                                                             int M, int N, int K, int act, int kper) {
   __shared__ float sX[TM][KC + 1];
   __shared__ float sW[TN][KC + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const long long m0 = (long long)blockIdx.y * TM;
   const int n0 = blockIdx.x * TN;
+  const int kb = SPLIT ? (int)blockIdx.z * kper : 0;
+  const int ke = SPLIT ? min(K, kb + kper) : K;
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   ChunkRegs<VEC> pre;
-  pre.load(X, W, m0, n0, 0, M, N, K);
-  for (int k0 = 0; k0 < K; k0 += KC) {
+  pre.load(X, W, m0, n0, kb, M, N, K, ke);
+  for (int k0 = kb; k0 < ke; k0 += KC) {
     __syncthreads();  // previous chunk's MFMA reads are done
     pre.store(sX, sW);
     __syncthreads();
-    if (k0 + KC < K) pre.load(X, W, m0, n0, k0 + KC, M, N, K);  // in flight during the MFMAs
+    if (k0 + KC < ke) pre.load(X, W, m0, n0, k0 + KC, M, N, K, ke);  // in flight during the MFMAs
     const int li = lane & 31, lk = lane >> 5;
 #pragma unroll
     for (int k = 0; k < KC; k += 2) {
@@ -136,12 +141,42 @@ __global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restr
   // epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   const int col = n0 + wn * 32 + (lane & 31);
   if (col >= N) return;
-  const float bias = b ? b[col] : 0.f;
+  if constexpr (SPLIT) {
+    float* P = Y + (long long)blockIdx.z * M * N;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const long long row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < M) Y[row * N + col] = act_fwd(acc[r] + bias, act);
+    for (int r = 0; r < 16; ++r) {
+      const long long row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) P[row * N + col] = acc[r];
+    }
+  } else {
+    const float bias = b ? b[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long long row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) Y[row * N + col] = act_fwd(acc[r] + bias, act);
+    }
   }
+}
+
+// Y[e] = act(sum_s P[s][e] + b[e % N]): the S slices summed in slice order (deterministic), the
+// loads of 8 slices issued together
+__global__ __launch_bounds__(256) void linear_splitk_epilogue_kernel(const float* __restrict__ P,
+                                                                     const float* __restrict__ b,
+                                                                     float* __restrict__ Y, long long MN, int N,
+                                                                     int S, int act) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= MN) return;
+  float s = 0.f;
+  int k = 0;
+  for (; k + 8 <= S; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = P[(long long)(k + u) * MN + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < S; ++k) s += P[(long long)k * MN + e];
+  Y[e] = act_fwd(s + (b ? b[e % N] : 0.f), act);
 }
 
 // dZ = dY * act'(Y); partial[blockIdx.y][n] = sum over this block's rows of dZ[., n]
@@ -286,14 +321,36 @@ __global__ __launch_bounds__(64 * RG) void slice_sum_kernel(const float* __restr
 
 namespace avk {
 
+int linear_act_fwd_slices(int M, int N, int K) {
+  const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  if (tiles >= 256) return 1;
+  // a few output tiles over a long K (a query's rows through a BERT projection: 2 x 12 tiles
+  // over K = 3,072): split K so ~512 workgroups cover the 256 CUs, each slice >= 4 chunks
+  long long s = (512 + tiles - 1) / tiles;
+  s = std::min<long long>(s, K / (4 * KC));
+  return (int)std::max(1LL, std::min(s, 64LL));
+}
+
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
-                    hipStream_t stream) {
+                    hipStream_t stream, float* partial, int S) {
   if (M <= 0 || N <= 0) return;
-  dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
-  if (vec) linear_act_fwd_kernel<true><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act);
-  else linear_act_fwd_kernel<false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act);
+  if (S > 1 && partial != nullptr) {
+    const int kper = ((K + S - 1) / S + KC - 1) / KC * KC;
+    S = (K + kper - 1) / kper;  // no empty slice
+    dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)S);
+    if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, b, partial, M, N, K, act, kper);
+    else linear_act_fwd_kernel<false, true><<<grid, MT, 0, stream>>>(X, W, b, partial, M, N, K, act, kper);
+    AV_HIP_CHECK(hipGetLastError());
+    const long long MN = (long long)M * N;
+    linear_splitk_epilogue_kernel<<<(unsigned)((MN + 255) / 256), 256, 0, stream>>>(partial, b, Y, MN, N, S, act);
+    AV_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
+  if (vec) linear_act_fwd_kernel<true, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K);
+  else linear_act_fwd_kernel<false, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -166,8 +166,50 @@ def lstm():
     torch.cuda.synchronize()
 
 
+def gemm_tn():
+    """gemm.hip gemm_tn_partial_kernel / gemm_tn_reduce_kernel: the LSTM weight gradient of 65,536
+    sequences x T 5 (K = 327,680 rows, M = 4H = 400, N = H + I + 1 = 106)."""
+    from avenir_amd import _native
+    g = torch.Generator(device="cuda").manual_seed(0)
+    A = torch.randn((327680, 400), generator=g, device="cuda")
+    B = torch.randn((327680, 106), generator=g, device="cuda")
+    for _ in range(4):
+        _native.C().gemm_tn(A, B)
+    torch.cuda.synchronize()
+
+
+def bert():
+    """transformer.hip add_layernorm / embed_layernorm and mlp.hip's GELU tile epilogue: 12 encoder
+    passes of the bert-base shape at B 1 x S 128 (the query path of semantic search)."""
+    from avenir_amd.nn.bert import BertConfig, BertEncoder
+    torch.manual_seed(0)
+    m = BertEncoder(BertConfig()).cuda()
+    ids = torch.randint(0, 30522, (1, 128), device="cuda")
+    mask = torch.ones_like(ids)
+    for _ in range(12):
+        m(ids, mask)
+    torch.cuda.synchronize()
+
+
+def svm_select():
+    """svm.hip smo_ws_topk_stream_kernel + the rank merge: the working-set selection at 1,048,576 rows."""
+    from avenir_amd import _native
+    g = torch.Generator(device="cuda").manual_seed(7)
+    N, C = 1 << 20, 1.0
+    y = torch.where(torch.rand(1, N, generator=g, device="cuda") < 0.5, 1.0, -1.0)
+    a = torch.rand(1, N, generator=g, device="cuda") * C
+    G = torch.randn(1, N, generator=g, device="cuda")
+    ws = torch.zeros((1, 128), dtype=torch.long, device="cuda")
+    ok = torch.zeros((1, 128), dtype=torch.bool, device="cuda")
+    gap = torch.full((1,), float("inf"), device="cuda")
+    for _ in range(20):
+        _native.C().smo_ws_select(a, G, y, C, 64, ws, ok, gap)
+    torch.cuda.synchronize()
+
+
 TARGETS = {"kmeans": kmeans, "fmt": fmt, "pairs": pairs, "split": split, "lstm": lstm, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
-           "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest}
+           "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest,
+           "gemm_tn": gemm_tn, "bert": bert, "svm_select": svm_select}
 
 if __name__ == "__main__":
     TARGETS[sys.argv[1]]()

@@ -115,8 +115,8 @@ def test_incremental_pca_kernel_matches_cpu(cuda):
     streams = [{f"k{j}": (torch.randn(40 + 7 * j, D, generator=g, dtype=torch.float64) * torch.linspace(3, 0.1, D,
                 dtype=torch.float64)) @ mix for j in range(5)} for _ in range(2)]
     a, b = IncrementalPCA(D, init_hidden=1, forget=0.97), IncrementalPCA(D, init_hidden=1, forget=0.97, device=cuda)
-    for s in streams:
-        sa, sb = a.update(s), b.update(s)
+    for i, s in enumerate(streams):     # host streams, then device streams (padded on the device)
+        sa, sb = a.update(s), b.update(s if i == 0 else {k: v.to(cuda) for k, v in s.items()})
     for key in sa:
         assert sa[key].num_hidden == sb[key].num_hidden and sa[key].count == sb[key].count
         assert torch.allclose(sa[key].components, sb[key].components.cpu(), rtol=1e-8, atol=1e-9)

@@ -6,7 +6,7 @@ from avenir_amd import _native
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,M,N", [(5000, 400, 106), (5000, 400, 201), (777, 33, 65), (64, 1, 1), (100_000, 64, 64),
+@pytest.mark.parametrize("K,M,N", [(5000, 400, 106), (5000, 400, 201), (777, 33, 65), (64, 1, 1), (100_000, 64, 64), (40_000, 400, 106),
                                    (31, 130, 70), (3, 5, 7)])
 def test_gemm_tn_vs_fp64(cuda, K, M, N):
     g = torch.Generator().manual_seed(K + M + N)
@@ -18,3 +18,18 @@ def test_gemm_tn_vs_fp64(cuda, K, M, N):
     # deterministic: the slices are summed in a fixed order
     C2 = _native.C().gemm_tn(A.to(cuda), B.to(cuda)).cpu()
     assert torch.equal(C, C2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(128, 768, 3072), (128, 2304, 768), (1, 3072, 768), (37, 200, 1000), (130, 130, 4099)])
+@pytest.mark.parametrize("act", [0, 1, 6])
+def test_linear_act_fwd_split_k_vs_fp64(cuda, M, N, K, act):
+    """mlp.hip's split-K path (few output tiles over a long K: slices of K summed in order, then
+    bias + activation) against fp64; deterministic across calls."""
+    g = torch.Generator().manual_seed(M + N + K + act)
+    X, W, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / K ** 0.5, torch.randn(N, generator=g)
+    Y = _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), act).cpu()
+    z = X.double() @ W.double().t() + b.double()
+    ref = {0: z, 1: torch.relu(z), 6: torch.nn.functional.gelu(z)}[act]
+    assert (Y.double() - ref).abs().max().item() <= 2e-5 * (K ** 0.5)
+    assert torch.equal(Y, _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), act).cpu())
