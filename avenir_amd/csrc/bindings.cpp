@@ -3677,7 +3677,7 @@ at::Tensor add_layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& r
 // LN(word[ids] + pos[s] + type[tt]) for ids / tt int64 [B, S] (tt may be None: type 0)
 at::Tensor embed_layernorm(const at::Tensor& ids, const c10::optional<at::Tensor>& tt, const at::Tensor& word,
                            const at::Tensor& pos, const at::Tensor& type, const at::Tensor& gamma,
-                           const at::Tensor& beta, double eps) {
+                           const at::Tensor& beta, double eps, bool validate) {
   CHECK_DEV(ids);
   CHECK_DTYPE(ids, at::kLong);
   TORCH_CHECK(ids.dim() == 2 && ids.is_contiguous(), "embed_layernorm: ids [B, S]");
@@ -3691,25 +3691,31 @@ at::Tensor embed_layernorm(const at::Tensor& ids, const c10::optional<at::Tensor
   TORCH_CHECK(S <= pos.size(0), "embed_layernorm: sequence longer than the position table");
   check_opt_f32(gamma, H, "gamma");
   check_opt_f32(beta, H, "beta");
-  // host-side index validation (no out-of-bounds gathers)
-  auto idc = ids.cpu();
-  const auto mm = at::aminmax(idc);
-  TORCH_CHECK(std::get<0>(mm).item<int64_t>() >= 0 && std::get<1>(mm).item<int64_t>() < word.size(0),
-              "embed_layernorm: token id out of range");
+  // host-side index validation (a device -> host copy: callers that checked the ids before their
+  // upload pass validate=False; the kernel clamps every gather into the tables regardless)
+  if (validate) {
+    const auto mm = at::aminmax(ids.cpu());
+    TORCH_CHECK(std::get<0>(mm).item<int64_t>() >= 0 && std::get<1>(mm).item<int64_t>() < word.size(0),
+                "embed_layernorm: token id out of range");
+  }
   if (tt.has_value() && tt->defined()) {
     CHECK_DEV((*tt));
     CHECK_DTYPE((*tt), at::kLong);
     TORCH_CHECK(tt->sizes() == ids.sizes() && tt->is_contiguous(), "token types [B, S]");
-    const auto tm = at::aminmax(tt->cpu());
-    TORCH_CHECK(std::get<0>(tm).item<int64_t>() >= 0 && std::get<1>(tm).item<int64_t>() < type.size(0),
-                "embed_layernorm: token type out of range");
+    if (validate) {
+      const auto tm = at::aminmax(tt->cpu());
+      TORCH_CHECK(std::get<0>(tm).item<int64_t>() >= 0 && std::get<1>(tm).item<int64_t>() < type.size(0),
+                  "embed_layernorm: token type out of range");
+    }
   }
+  TORCH_CHECK(word.size(0) >= 1 && type.size(0) >= 1, "embed_layernorm: empty embedding table");
   DevGuard g(ids.device());
   auto out = at::empty({B, S, H}, word.options());
   avk::embed_layernorm(reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()),
                        tt.has_value() && tt->defined() ? reinterpret_cast<const long long*>(tt->data_ptr<int64_t>()) : nullptr,
                        word.data_ptr<float>(), pos.data_ptr<float>(), type.data_ptr<float>(), gamma.data_ptr<float>(),
-                       beta.data_ptr<float>(), out.data_ptr<float>(), B * S, (int)S, (int)H, (float)eps, cur_stream(word));
+                       beta.data_ptr<float>(), out.data_ptr<float>(), B * S, (int)S, (int)H, (float)eps, word.size(0),
+                       (int)type.size(0), cur_stream(word));
   return out;
 }
 
@@ -3995,7 +4001,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_pack_f32", &lstm_pack_f32);
   m.def("gemm_tn", &gemm_tn);
   m.def("add_layernorm", &add_layernorm);
-  m.def("embed_layernorm", &embed_layernorm);
+  m.def("embed_layernorm", &embed_layernorm, py::arg("ids"), py::arg("tt"), py::arg("word"), py::arg("pos"),
+        py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("validate") = true);
   m.def("ref_split_score", &ref_split_score);
   m.def("lstm_backward_f32", &lstm_backward_f32);
 

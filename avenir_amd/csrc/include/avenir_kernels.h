@@ -188,7 +188,7 @@ void add_layernorm(const float* x, const float* res, const float* gamma, const f
                    int H, float eps, hipStream_t stream);
 void embed_layernorm(const long long* ids, const long long* tt, const float* word, const float* pos, const float* type,
                      const float* gamma, const float* beta, float* out, long long rows, int S, int H, float eps,
-                     hipStream_t stream);
+                     long long nword, int ntype, hipStream_t stream);
 
 // ---- gemm.hip: split-K fp32 A^T B (weight gradients over a long row dimension) ---------------
 int gemm_tn_slices(int K, int M, int N);

@@ -76,11 +76,15 @@ __global__ __launch_bounds__(256) void embed_layernorm_kernel(const long long* _
                                                               const float* __restrict__ type,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* __restrict__ out,
-                                                              long long rows, int S, int H, float eps) {
+                                                              long long rows, int S, int H, float eps,
+                                                              long long nword, int ntype) {
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
-  const long long id = ids[row], t = tt ? tt[row] : 0;
+  // ids are range-checked by the binding unless the caller validated them already (host tensors
+  // before their upload); the clamp keeps every gather inside the tables either way
+  const long long id = min(max(ids[row], 0LL), nword - 1);
+  const long long t = tt ? min(max(tt[row], 0LL), (long long)ntype - 1) : 0;
   const int s = (int)(row % S);
   float4 v[LN_MAXV];
 #pragma unroll
@@ -111,11 +115,12 @@ void add_layernorm(const float* x, const float* res, const float* gamma, const f
 
 void embed_layernorm(const long long* ids, const long long* tt, const float* word, const float* pos, const float* type,
                      const float* gamma, const float* beta, float* out, long long rows, int S, int H, float eps,
-                     hipStream_t stream) {
+                     long long nword, int ntype, hipStream_t stream) {
   if (rows <= 0) return;
+  if (nword < 1 || ntype < 1) throw std::runtime_error("embed_layernorm: empty embedding table");
   if (H < 4 || H > 1024 || H % 4) throw std::runtime_error("embed_layernorm: 4 <= H <= 1024, H % 4 == 0");
   embed_layernorm_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(ids, tt, word, pos, type, gamma, beta, out,
-                                                                         rows, S, H, eps);
+                                                                         rows, S, H, eps, nword, ntype);
   AV_HIP_CHECK(hipGetLastError());
 }
 

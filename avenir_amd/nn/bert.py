@@ -136,6 +136,7 @@ class BertEncoder(torch.nn.Module):
         if strict and missing:
             raise KeyError(f"missing BERT parameters: {sorted(missing)[:5]} ...")
         self._qkv_cache.clear()
+        self.__dict__["_graphs"] = {}
         return self
 
     @classmethod
@@ -184,9 +185,76 @@ class BertEncoder(torch.nn.Module):
                                              b.detach(), eps)
         return torch.nn.functional.layer_norm(x if res is None else x + res, (x.shape[-1],), g, b, eps)
 
+    #: batches of up to this many tokens replay a captured HIP graph of the whole pass, one per
+    #: (B, S, mask, token types) shape seen at least twice (the launch-bound regime: ~150 launches
+    #: per pass at B x S = 128); 0 disables.  Graphs are dropped when parameters change.
+    GRAPH_MAX_ROWS = int(os.environ.get("AVMI_BERT_GRAPH_MAX_ROWS", "1024"))
+    GRAPH_CACHE = 16
+
+    def _check_ids(self, ids: torch.Tensor, tt: torch.Tensor | None) -> None:
+        """Range check of HOST token ids / types (no device synchronisation)."""
+        V, T = self.config.vocab_size, self.config.type_vocab_size
+        if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= V):
+            raise RuntimeError("BertEncoder: token id out of range")
+        if tt is not None and tt.numel() and (int(tt.min()) < 0 or int(tt.max()) >= T):
+            raise RuntimeError("BertEncoder: token type out of range")
+
+    def _apply(self, fn, *a, **k):          # .to() / .cuda(): captured graphs hold the old storage
+        self._graphs = {}
+        self._qkv_cache.clear()
+        return super()._apply(fn, *a, **k)
+
     @torch.no_grad()
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
                 token_type_ids: torch.Tensor | None = None) -> torch.Tensor:
+        """Last hidden states [B, S, H].  Inputs may be host tensors (checked on the host, then
+        uploaded) or device tensors (checked by one device -> host copy)."""
+        dev = self.p("embeddings.word_embeddings.weight").device
+        if dev.type != "cuda":
+            return self._forward(input_ids, attention_mask, token_type_ids, True)
+        validated = False
+        if not input_ids.is_cuda:
+            self._check_ids(input_ids, token_type_ids)
+            validated = True
+        ids = input_ids.to(dev, torch.long).contiguous()
+        tt = None if token_type_ids is None else token_type_ids.to(dev, torch.long).contiguous()
+        mask = None if attention_mask is None else attention_mask.to(dev)
+        if (self.GRAPH_MAX_ROWS and ids.numel() <= self.GRAPH_MAX_ROWS
+                and not torch.cuda.is_current_stream_capturing()):
+            if not validated:
+                self._check_ids(ids.cpu(), None if tt is None else tt.cpu())
+            return self._graph_forward(ids, mask, tt)
+        return self._forward(ids, mask, tt, not validated)
+
+    def _graph_forward(self, ids, mask, tt):
+        key = (tuple(ids.shape), None if mask is None else mask.dtype, tt is not None)
+        ver = tuple(p._version for p in self.params.values())
+        graphs = self.__dict__.setdefault("_graphs", {})
+        ent = graphs.get(key)
+        if ent is None or ent[0] != ver:
+            seen = self.__dict__.setdefault("_graph_seen", {})
+            seen[key] = seen.get(key, 0) + 1
+            if seen[key] < 2:                  # a one-off shape: not worth a capture
+                return self._forward(ids, mask, tt, False)
+            static = (ids.clone(), None if mask is None else mask.clone(), None if tt is None else tt.clone())
+            self._forward(*static, False)        # warm-up: fills the Q/K/V cache outside the graph
+            from ..utils.hipgraph import capturing
+            g = torch.cuda.CUDAGraph()
+            with capturing(g, device=ids.device):
+                out = self._forward(*static, False)
+            if len(graphs) >= self.GRAPH_CACHE:
+                graphs.pop(next(iter(graphs)))
+            ent = graphs[key] = (ver, g, static, out)
+        _, g, static, out = ent
+        static[0].copy_(ids)
+        if mask is not None:
+            static[1].copy_(mask)
+        if tt is not None:
+            static[2].copy_(tt)
+        g.replay()
+        return out.clone()
+
+    def _forward(self, input_ids, attention_mask, token_type_ids, validate: bool) -> torch.Tensor:
         cfg = self.config
         B, S = input_ids.shape
         H, nh = cfg.hidden_size, cfg.num_attention_heads
@@ -198,7 +266,7 @@ class BertEncoder(torch.nn.Module):
         g0, b0 = self.p("embeddings.LayerNorm.weight"), self.p("embeddings.LayerNorm.bias")
         if ids.is_cuda:
             x = _native.C().embed_layernorm(ids, tt, word.detach(), pos.detach(), typ.detach(), g0.detach(),
-                                            b0.detach(), cfg.layer_norm_eps)
+                                            b0.detach(), cfg.layer_norm_eps, validate)
         else:
             e = word[ids] + typ[tt if tt is not None else torch.zeros_like(ids)] + pos[:S].unsqueeze(0)
             x = torch.nn.functional.layer_norm(e, (H,), g0, b0, cfg.layer_norm_eps)
@@ -267,7 +335,7 @@ def bert_embedder(model: BertEncoder, tokenizer: WordPiece, max_len: int | None 
         step = L - 2
         for s0 in range(0, len(pieces), step):
             ids = [tokenizer.cls_id] + pieces[s0:s0 + step] + [tokenizer.sep_id]
-            h = model(torch.tensor([ids], device=dev))[0, 1:-1]
+            h = model(torch.tensor([ids]))[0, 1:-1]          # host ids: checked on the host, then uploaded
             ow = torch.tensor(owner[s0:s0 + step], device=dev)
             out.index_add_(0, ow, h)
             cnt.index_add_(0, ow, torch.ones_like(ow, dtype=torch.float32))

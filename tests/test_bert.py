@@ -133,3 +133,32 @@ def test_semantic_search_job_with_a_bert_model_dir(tmp_path):
                  "--name", "fruit vitamin"]) == 0
     lines = out.read_text().split()
     assert len(lines) == 3 and all(len(l.split(",")) == 3 for l in lines)
+
+
+@pytest.mark.gpu
+def test_bert_graph_replay_matches_eager(cuda):
+    """Small batches replay a captured HIP graph from the second call of a shape on: same output as
+    the eager pass, host and device inputs, recapture after an in-place parameter change, and
+    out-of-range ids rejected before anything runs."""
+    ref, mine = _pair(H=128, L=2, heads=4, I=512, V=500, P=64)
+    mine = mine.to(cuda)
+    ids, mask, tt = _inputs(B=2, S=19, V=500)
+    eager = mine._forward(ids.to(cuda), mask.to(cuda), tt.to(cuda), True).cpu()
+    outs = [mine(ids, mask, tt).cpu() for _ in range(3)]                     # host inputs
+    outs += [mine(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu() for _ in range(2)]  # device inputs
+    assert len(mine._graphs) == 1
+    for o in outs:
+        assert torch.equal(o, eager)
+    with torch.no_grad():
+        mine.p("encoder.layer.1.output.dense.bias").add_(0.5)
+    eager2 = mine._forward(ids.to(cuda), mask.to(cuda), tt.to(cuda), True).cpu()
+    assert not torch.equal(eager2, eager)
+    assert torch.equal(mine(ids, mask, tt).cpu(), eager2)
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=mask, token_type_ids=tt).last_hidden_state
+    keep = mask.bool()
+    assert not torch.allclose(eager2[keep], want[keep], atol=1e-3)      # the edit is visible
+    with pytest.raises(RuntimeError):
+        mine(torch.full((2, 19), 500), mask, tt)
+    with pytest.raises(RuntimeError):
+        mine(torch.full((2, 19), 500, device=cuda), mask, tt)
