@@ -3674,6 +3674,63 @@ at::Tensor add_layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& r
   return out;
 }
 
+// LN(X W^T + b + res) for X [M, K], W [N, K], res [M, N]: the projection feeding a residual +
+// LayerNorm.  With the split-K tile (few output tiles over a long K) the slice sum, bias, residual
+// and LayerNorm run in ONE pass over the partials (no [M, N] projection output, no epilogue launch).
+at::Tensor linear_add_layernorm(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b,
+                                const at::Tensor& res, const at::Tensor& gamma, const at::Tensor& beta, double eps) {
+  CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
+  CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
+  TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "X [M, K], W [N, K]");
+  const int64_t M = X.size(0), N = W.size(0), K = X.size(1);
+  TORCH_CHECK(M < (1LL << 31) && K < (1LL << 31), "dims < 2^31");
+  TORCH_CHECK(N >= 4 && N <= 1024 && N % 4 == 0, "linear_add_layernorm: 4 <= N <= 1024, N % 4 == 0");
+  CHECK_DEV(res); CHECK_DTYPE(res, at::kFloat);
+  TORCH_CHECK(res.is_contiguous() && res.numel() == M * N && aligned(res, 16), "res [M, N] contiguous");
+  check_opt_f32(b, N, "bias");
+  check_opt_f32(gamma, N, "gamma");
+  check_opt_f32(beta, N, "beta");
+  TORCH_CHECK(aligned(gamma, 16) && aligned(beta, 16) && (!b.has_value() || !b->defined() || aligned(*b, 16)),
+              "linear_add_layernorm: 16-byte aligned parameters");
+  auto Xc = X.contiguous(), Wc = W.contiguous();
+  DevGuard g(X.device());
+  auto out = at::empty({M, N}, X.options());
+  const int S = avk::linear_act_fwd_slices((int)M, (int)N, (int)K);
+  if (S > 1) {
+    auto part = at::empty({(long long)S * M * N}, X.options());
+    const int Se = avk::linear_splitk_partial(Xc.data_ptr<float>(), Wc.data_ptr<float>(), part.data_ptr<float>(),
+                                              (int)M, (int)N, (int)K, S, cur_stream(X));
+    avk::add_layernorm_slices(part.data_ptr<float>(), Se, M * N, ptr_or_null<float>(b), res.data_ptr<float>(),
+                              gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr<float>(), M, (int)N,
+                              (float)eps, cur_stream(X));
+  } else {
+    auto y = at::empty({M, N}, X.options());
+    avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), ptr_or_null<float>(b), y.data_ptr<float>(),
+                        (int)M, (int)N, (int)K, 0, cur_stream(X));
+    avk::add_layernorm(y.data_ptr<float>(), res.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                       out.data_ptr<float>(), M, (int)N, (float)eps, cur_stream(X));
+  }
+  return out;
+}
+
+// softmax(q k^T * scale + kbias) v per head from the fused projection qkv [B*S, 3H] (Q | K | V,
+// heads of 64 columns) -> [B*S, H]; kbias [B, S] additive per key or None
+at::Tensor attention_f32(const at::Tensor& qkv, const c10::optional<at::Tensor>& kbias, int64_t B, int64_t S,
+                         int64_t nh, double scale) {
+  CHECK_DEV(qkv); CHECK_DTYPE(qkv, at::kFloat);
+  TORCH_CHECK(B >= 1 && S >= 1 && nh >= 1, "attention_f32: B, S, nh >= 1");
+  const int64_t H = nh * 64;
+  TORCH_CHECK(qkv.is_contiguous() && qkv.numel() == B * S * 3 * H && aligned(qkv, 16),
+              "attention_f32: qkv [B*S, 3 * nh * 64] contiguous, 16-byte aligned");
+  TORCH_CHECK(B * S < (1LL << 31) && S < (1LL << 30) && B < 65536 && nh < 65536, "attention_f32: sizes");
+  check_opt_f32(kbias, B * S, "kbias");
+  DevGuard g(qkv.device());
+  auto out = at::empty({B * S, H}, qkv.options());
+  avk::attention_f32(qkv.data_ptr<float>(), ptr_or_null<float>(kbias), out.data_ptr<float>(), (int)B, (int)S, (int)nh,
+                     (float)scale, cur_stream(qkv));
+  return out;
+}
+
 // LN(word[ids] + pos[s] + type[tt]) for ids / tt int64 [B, S] (tt may be None: type 0)
 at::Tensor embed_layernorm(const at::Tensor& ids, const c10::optional<at::Tensor>& tt, const at::Tensor& word,
                            const at::Tensor& pos, const at::Tensor& type, const at::Tensor& gamma,
@@ -4001,6 +4058,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_pack_f32", &lstm_pack_f32);
   m.def("gemm_tn", &gemm_tn);
   m.def("add_layernorm", &add_layernorm);
+  m.def("linear_add_layernorm", &linear_add_layernorm);
+  m.def("attention_f32", &attention_f32);
   m.def("embed_layernorm", &embed_layernorm, py::arg("ids"), py::arg("tt"), py::arg("word"), py::arg("pos"),
         py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("validate") = true);
   m.def("ref_split_score", &ref_split_score);

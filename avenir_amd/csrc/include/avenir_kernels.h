@@ -186,6 +186,13 @@ void ref_split_score(const long long* hist, int A, int C, int TBt, const int* sp
 // ---- transformer.hip: encoder epilogues (BERT for semantic search) -----------------------------
 void add_layernorm(const float* x, const float* res, const float* gamma, const float* beta, float* out, long long rows,
                    int H, float eps, hipStream_t stream);
+// out = LN(sum_{s < S} partial[s] + bias + res) (transformer.hip; S = 1, bias = null: LN(x + res))
+void add_layernorm_slices(const float* partial, int S, long long sstride, const float* bias, const float* res,
+                          const float* gamma, const float* beta, float* out, long long rows, int H, float eps,
+                          hipStream_t stream);
+// multi-head attention, head dim 64: qkv [B*S, 3H] (Q | K | V, heads of 64), kbias [B, S] additive or null
+void attention_f32(const float* qkv, const float* kbias, float* out, int B, int S, int nh, float scale,
+                   hipStream_t stream);
 void embed_layernorm(const long long* ids, const long long* tt, const float* word, const float* pos, const float* type,
                      const float* gamma, const float* beta, float* out, long long rows, int S, int H, float eps,
                      long long nword, int ntype, hipStream_t stream);
@@ -246,6 +253,9 @@ void forest_part_count(const uint8_t* codes, long long ld, const int* item_node,
 // K27 fused Linear + bias + activation (mlp.hip); with S > 1 and a partial buffer of S*M*N floats
 // the K range is split over S slices (linear_act_fwd_slices picks S for few output tiles over a long K)
 int linear_act_fwd_slices(int M, int N, int K);
+// the raw split-K partial products [S_eff][M][N] of X W^T (no bias / activation); returns S_eff
+int linear_splitk_partial(const float* X, const float* W, float* partial, int M, int N, int K, int S,
+                          hipStream_t stream);
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                     hipStream_t stream, float* partial = nullptr, int S = 1);
 int linear_act_bwd_blocks(int M);

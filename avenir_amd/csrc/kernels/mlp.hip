@@ -106,6 +106,8 @@ struct ChunkRegs {
   }
 };
 
+// (a second register set holding chunk c + 2 in flight measured slower at the 128-row split-K
+// shapes: 12.1 vs 10.4 us per projection, profiles/r5_bert_kernel_stats_v3.csv)
 // SPLIT: blockIdx.z is a slice [z kper, (z + 1) kper) of K and the raw tile goes to
 // P[z][M][N] (bias and activation applied by linear_splitk_epilogue_kernel after the slice sum)
 template <bool VEC, bool SPLIT>
@@ -331,18 +333,27 @@ int linear_act_fwd_slices(int M, int N, int K) {
   return (int)std::max(1LL, std::min(s, 64LL));
 }
 
+int linear_splitk_partial(const float* X, const float* W, float* partial, int M, int N, int K, int S,
+                          hipStream_t stream) {
+  const int kper = ((K + S - 1) / S + KC - 1) / KC * KC;
+  S = (K + kper - 1) / kper;  // no empty slice
+  if (M <= 0 || N <= 0) return S;
+  const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(W) % 16 == 0);
+  dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)S);
+  if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper);
+  else linear_act_fwd_kernel<false, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper);
+  AV_HIP_CHECK(hipGetLastError());
+  return S;
+}
+
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                     hipStream_t stream, float* partial, int S) {
   if (M <= 0 || N <= 0) return;
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
   if (S > 1 && partial != nullptr) {
-    const int kper = ((K + S - 1) / S + KC - 1) / KC * KC;
-    S = (K + kper - 1) / kper;  // no empty slice
-    dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)S);
-    if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, b, partial, M, N, K, act, kper);
-    else linear_act_fwd_kernel<false, true><<<grid, MT, 0, stream>>>(X, W, b, partial, M, N, K, act, kper);
-    AV_HIP_CHECK(hipGetLastError());
+    S = linear_splitk_partial(X, W, partial, M, N, K, S, stream);
     const long long MN = (long long)M * N;
     linear_splitk_epilogue_kernel<<<(unsigned)((MN + 255) / 256), 256, 0, stream>>>(partial, b, Y, MN, N, S, act);
     AV_HIP_CHECK(hipGetLastError());

@@ -10,13 +10,17 @@ weights instead.
 
 MI355X path (inference, fp32 like the reference's model):
 * embeddings: word + position + token-type gathers, the sum and the LayerNorm in ONE kernel
-  (transformer.hip ``embed_layernorm_kernel``);
-* per layer: the Q, K, V projections as ONE GEMM with concatenated weights, attention scores /
-  mask / softmax / context in torch's fused attention kernel, the output projection, then residual +
-  LayerNorm in ONE pass (``add_layernorm_kernel``); the feed-forward up-projection with bias + GELU,
-  the down-projection, residual + LayerNorm again.  Projections of up to ``MFMA_MAX_ROWS`` rows (a
-  query, a short document) run on mlp.hip's f32-MFMA tile kernel with bias and GELU in its
-  epilogue; larger batches on hipBLASLt (profiles/r5_bert_base_bench.jsonl).
+  (transformer.hip ``embed_layernorm_kernel``; host token ids are range-checked before their
+  upload, so no device synchronisation per pass);
+* per layer: the Q, K, V projections as ONE GEMM with concatenated weights; attention in ONE
+  transformer.hip kernel (``attn_f32_kernel``, head dim 64: scores, mask, online softmax and
+  context on fp32 MFMA, read from the fused [B*S, 3H] projection and written as [B*S, H], no head
+  transposes; torch's fused attention for other head sizes); the output projection with its bias,
+  the residual and the LayerNorm in one split-K + LayerNorm pass (``linear_add_layernorm``); the
+  feed-forward up-projection with bias + GELU in the tile epilogue; the down-projection fused with
+  its residual + LayerNorm the same way.  Projections of up to ``MFMA_MAX_ROWS`` rows (a query, a
+  short document) run on mlp.hip's f32-MFMA tile kernel (split over K when it has few output
+  tiles); larger batches on hipBLASLt (profiles/r5_bert_base_bench.jsonl).
 CPU tensors run the same math with torch ops.
 """
 from __future__ import annotations
@@ -136,7 +140,6 @@ class BertEncoder(torch.nn.Module):
         if strict and missing:
             raise KeyError(f"missing BERT parameters: {sorted(missing)[:5]} ...")
         self._qkv_cache.clear()
-        self.__dict__["_graphs"] = {}
         return self
 
     @classmethod
@@ -185,12 +188,6 @@ class BertEncoder(torch.nn.Module):
                                              b.detach(), eps)
         return torch.nn.functional.layer_norm(x if res is None else x + res, (x.shape[-1],), g, b, eps)
 
-    #: batches of up to this many tokens replay a captured HIP graph of the whole pass, one per
-    #: (B, S, mask, token types) shape seen at least twice (the launch-bound regime: ~150 launches
-    #: per pass at B x S = 128); 0 disables.  Graphs are dropped when parameters change.
-    GRAPH_MAX_ROWS = int(os.environ.get("AVMI_BERT_GRAPH_MAX_ROWS", "1024"))
-    GRAPH_CACHE = 16
-
     def _check_ids(self, ids: torch.Tensor, tt: torch.Tensor | None) -> None:
         """Range check of HOST token ids / types (no device synchronisation)."""
         V, T = self.config.vocab_size, self.config.type_vocab_size
@@ -199,10 +196,17 @@ class BertEncoder(torch.nn.Module):
         if tt is not None and tt.numel() and (int(tt.min()) < 0 or int(tt.max()) >= T):
             raise RuntimeError("BertEncoder: token type out of range")
 
-    def _apply(self, fn, *a, **k):          # .to() / .cuda(): captured graphs hold the old storage
-        self._graphs = {}
+    def _apply(self, fn, *a, **k):          # .to() / .cuda(): the Q/K/V cache holds the old storage
         self._qkv_cache.clear()
         return super()._apply(fn, *a, **k)
+
+    def _linear_ln(self, x2, W, b, res, g, bb):
+        """LN(x2 W^T + b + res): one fused split-K + LayerNorm pass for a query's rows on the GPU."""
+        N = W.shape[0]
+        if x2.is_cuda and x2.shape[0] <= self.MFMA_MAX_ROWS and N <= 1024 and N % 4 == 0:
+            return _native.C().linear_add_layernorm(x2, W, b, res.contiguous(), g.detach(), bb.detach(),
+                                                    self.config.layer_norm_eps)
+        return self._add_ln(self._linear(x2, W, b), res, g, bb)
 
     @torch.no_grad()
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
@@ -219,40 +223,7 @@ class BertEncoder(torch.nn.Module):
         ids = input_ids.to(dev, torch.long).contiguous()
         tt = None if token_type_ids is None else token_type_ids.to(dev, torch.long).contiguous()
         mask = None if attention_mask is None else attention_mask.to(dev)
-        if (self.GRAPH_MAX_ROWS and ids.numel() <= self.GRAPH_MAX_ROWS
-                and not torch.cuda.is_current_stream_capturing()):
-            if not validated:
-                self._check_ids(ids.cpu(), None if tt is None else tt.cpu())
-            return self._graph_forward(ids, mask, tt)
         return self._forward(ids, mask, tt, not validated)
-
-    def _graph_forward(self, ids, mask, tt):
-        key = (tuple(ids.shape), None if mask is None else mask.dtype, tt is not None)
-        ver = tuple(p._version for p in self.params.values())
-        graphs = self.__dict__.setdefault("_graphs", {})
-        ent = graphs.get(key)
-        if ent is None or ent[0] != ver:
-            seen = self.__dict__.setdefault("_graph_seen", {})
-            seen[key] = seen.get(key, 0) + 1
-            if seen[key] < 2:                  # a one-off shape: not worth a capture
-                return self._forward(ids, mask, tt, False)
-            static = (ids.clone(), None if mask is None else mask.clone(), None if tt is None else tt.clone())
-            self._forward(*static, False)        # warm-up: fills the Q/K/V cache outside the graph
-            from ..utils.hipgraph import capturing
-            g = torch.cuda.CUDAGraph()
-            with capturing(g, device=ids.device):
-                out = self._forward(*static, False)
-            if len(graphs) >= self.GRAPH_CACHE:
-                graphs.pop(next(iter(graphs)))
-            ent = graphs[key] = (ver, g, static, out)
-        _, g, static, out = ent
-        static[0].copy_(ids)
-        if mask is not None:
-            static[1].copy_(mask)
-        if tt is not None:
-            static[2].copy_(tt)
-        g.replay()
-        return out.clone()
 
     def _forward(self, input_ids, attention_mask, token_type_ids, validate: bool) -> torch.Tensor:
         cfg = self.config
@@ -275,22 +246,26 @@ class BertEncoder(torch.nn.Module):
         if attention_mask is not None:
             m = attention_mask.to(x.dtype).view(B, 1, 1, S)
             bias = (1.0 - m) * torch.finfo(x.dtype).min
+        kbias = None if bias is None else bias.view(B, S).contiguous()
         scale = 1.0 / math.sqrt(dh)
         for i in range(cfg.num_hidden_layers):
             n = _layer_names(i)
             x2 = x.reshape(B * S, H)
             Wqkv, bqkv = self._qkv(i)
-            qkv = self._linear(x2, Wqkv, bqkv).view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4)   # [3, B, nh, S, dh]
-            q, k, v = qkv[0], qkv[1], qkv[2]
-            # fused scores / mask / softmax / context (one library attention kernel instead of
-            # two batched GEMMs, a mask add and a softmax pass over [B, nh, S, S])
-            ctx = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=scale)
-            ctx = ctx.permute(0, 2, 1, 3).reshape(B * S, H)
-            a = self._linear(ctx.contiguous(), self.p(n["o"] + ".weight").detach(), self.p(n["o"] + ".bias").detach())
-            x2 = self._add_ln(a, x2, self.p(n["ln1"] + ".weight"), self.p(n["ln1"] + ".bias"))
+            qkv2 = self._linear(x2, Wqkv, bqkv)                                   # [B*S, 3H]
+            if qkv2.is_cuda and dh == 64:
+                # transformer.hip attention: straight from [B*S, 3H] to [B*S, H], no head transposes
+                ctx = _native.C().attention_f32(qkv2, kbias, B, S, nh, scale)
+            else:
+                qkv = qkv2.view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4)            # [3, B, nh, S, dh]
+                ctx = torch.nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=bias,
+                                                                       scale=scale)
+                ctx = ctx.permute(0, 2, 1, 3).reshape(B * S, H)
+            x2 = self._linear_ln(ctx.contiguous(), self.p(n["o"] + ".weight").detach(), self.p(n["o"] + ".bias").detach(),
+                                 x2, self.p(n["ln1"] + ".weight"), self.p(n["ln1"] + ".bias"))
             h = self._linear(x2, self.p(n["up"] + ".weight").detach(), self.p(n["up"] + ".bias").detach(), _GELU)
-            o = self._linear(h, self.p(n["down"] + ".weight").detach(), self.p(n["down"] + ".bias").detach())
-            x = self._add_ln(o, x2, self.p(n["ln2"] + ".weight"), self.p(n["ln2"] + ".bias")).view(B, S, H)
+            x = self._linear_ln(h, self.p(n["down"] + ".weight").detach(), self.p(n["down"] + ".bias").detach(),
+                                x2, self.p(n["ln2"] + ".weight"), self.p(n["ln2"] + ".bias")).view(B, S, H)
         return x
 
 

@@ -40,14 +40,8 @@ def main():
             got = mine(ids, mask)
             err = float((got - want).abs().max())
             t_ref = timed(lambda: ref(input_ids=ids, attention_mask=mask))
-            t_mine = timed(lambda: mine(ids, mask))            # graph replay where B x S qualifies
-            graphed = bool(getattr(mine, "_graphs", {}))
-            mine.GRAPH_MAX_ROWS, keep = 0, mine.GRAPH_MAX_ROWS
-            t_eager = timed(lambda: mine(ids, mask))
-            mine.GRAPH_MAX_ROWS = keep
-            mine._graphs = {}
+            t_mine = timed(lambda: mine(ids, mask))
         print(json.dumps({"bench": "bert_base_encoder", "B": B, "S": S, "ours_ms": t_mine * 1e3,
-                          "ours_eager_ms": t_eager * 1e3, "graph": graphed,
                           "transformers_ms": t_ref * 1e3, "speedup": t_ref / t_mine, "max_abs_diff": err,
                           "tokens_per_s": B * S / t_mine}), flush=True)
 
