@@ -325,7 +325,9 @@ namespace avk {
 
 int linear_act_fwd_slices(int M, int N, int K) {
   const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  if (tiles >= 256) return 1;
+  // (K < 512: at most 16 chunks per tile, where the extra epilogue launch costs more than the
+  // parallelism gains — the LSTM's dx = dZ W_ih at 5,000 x 5 x 400)
+  if (tiles >= 256 || K < 16 * KC) return 1;
   // a few output tiles over a long K (a query's rows through a BERT projection: 2 x 12 tiles
   // over K = 3,072): split K so ~512 workgroups cover the 256 CUs, each slice >= 4 chunks
   long long s = (512 + tiles - 1) / tiles;
