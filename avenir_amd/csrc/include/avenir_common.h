@@ -21,6 +21,28 @@ void av_report_hip_error(hipError_t e, const char* expr, const char* file, int l
 
 namespace av {
 
+// ---- XCD-aware tile order ------------------------------------------------------------------------
+// The dispatcher hands workgroup i of a launch to XCD i % 8 (round robin over the 8 XCDs, each with
+// its own L2).  xcd_remap turns the flat dispatch id into a logical id such that every XCD runs a
+// CONTIGUOUS range of logical ids (XCD x: ids [x q + min(x, r), ... + q + (x < r)) for total = 8 q
+// + r) — a bijection, so neighbouring tiles in the logical order share one L2.
+constexpr int AV_NUM_XCD = 8;
+__device__ __forceinline__ int xcd_remap(int pid, int total) {
+  const int q = total / AV_NUM_XCD, r = total % AV_NUM_XCD;
+  const int x = pid % AV_NUM_XCD, i = pid / AV_NUM_XCD;
+  return x * q + (x < r ? x : r) + i;
+}
+// logical id -> (tile row, tile col) in groups of G tile rows: consecutive ids walk the G rows of
+// a group for one tile column, then the next column — a column's operand tile is reused by G
+// neighbours and a group's row operands by every column.
+__device__ __forceinline__ void grouped_tile(int lid, int ntm, int ntn, int G, int& tm, int& tn) {
+  const int per = G * ntn, g = lid / per, first = g * G;
+  const int gs = (ntm - first) < G ? (ntm - first) : G;
+  const int in = lid - g * per;
+  tm = first + in % gs;
+  tn = in / gs;
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 

@@ -12,6 +12,7 @@
 //   the stored output, so no pre-activation tensor is kept), per-block column partials reduced on
 //   the host side of the op; dX = dZ W and dW = dZ^T X are plain GEMMs (hipBLASLt).
 #include <algorithm>
+#include <cstdlib>
 
 #include "avenir_common.h"
 #include "avenir_kernels.h"
@@ -113,13 +114,19 @@ struct ChunkRegs {
 template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W,
                                                              const float* __restrict__ b, float* __restrict__ Y,
-                                                             int M, int N, int K, int act, int kper) {
+                                                             int M, int N, int K, int act, int kper, int xcd) {
   __shared__ float sX[TM][KC + 1];
   __shared__ float sW[TN][KC + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const long long m0 = (long long)blockIdx.y * TM;
-  const int n0 = blockIdx.x * TN;
+  int tm = blockIdx.y, tn = blockIdx.x;
+  if (xcd) {  // XCD-contiguous ranges of 8-row tile groups: an XCD's L2 holds its X band and reuses
+              // each W tile across the group's rows
+    const int ntn = gridDim.x, ntm = gridDim.y;
+    av::grouped_tile(av::xcd_remap(blockIdx.y * ntn + blockIdx.x, ntm * ntn), ntm, ntn, 8, tm, tn);
+  }
+  const long long m0 = (long long)tm * TM;
+  const int n0 = tn * TN;
   const int kb = SPLIT ? (int)blockIdx.z * kper : 0;
   const int ke = SPLIT ? min(K, kb + kper) : K;
   f32x16 acc;
@@ -323,6 +330,15 @@ __global__ __launch_bounds__(64 * RG) void slice_sum_kernel(const float* __restr
 
 namespace avk {
 
+// AVMI_XCD_TILES=0 restores the dispatch order (A/B switch)
+static bool xcd_tiles_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("AVMI_XCD_TILES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int linear_act_fwd_slices(int M, int N, int K) {
   const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   // (K < 512: at most 16 chunks per tile, where the extra epilogue launch costs more than the
@@ -343,8 +359,8 @@ int linear_splitk_partial(const float* X, const float* W, float* partial, int M,
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
   dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)S);
-  if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper);
-  else linear_act_fwd_kernel<false, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper);
+  if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0);
+  else linear_act_fwd_kernel<false, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0);
   AV_HIP_CHECK(hipGetLastError());
   return S;
 }
@@ -362,8 +378,9 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
     return;
   }
   dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
-  if (vec) linear_act_fwd_kernel<true, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K);
-  else linear_act_fwd_kernel<false, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K);
+  const int xcd = xcd_tiles_enabled() && grid.x * grid.y >= 64 ? 1 : 0;
+  if (vec) linear_act_fwd_kernel<true, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
+  else linear_act_fwd_kernel<false, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -33,3 +33,15 @@ def test_linear_act_fwd_split_k_vs_fp64(cuda, M, N, K, act):
     ref = {0: z, 1: torch.relu(z), 6: torch.nn.functional.gelu(z)}[act]
     assert (Y.double() - ref).abs().max().item() <= 2e-5 * (K ** 0.5)
     assert torch.equal(Y, _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), act).cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(700, 650, 96), (4096, 3072, 64), (65, 4100, 32)])
+def test_linear_act_fwd_xcd_tile_order(cuda, M, N, K):
+    """The XCD-aware grouped tile order (>= 64 output tiles, counts not a multiple of 8, a partial
+    last group of tile rows) still covers every output tile exactly once."""
+    g = torch.Generator().manual_seed(M + N)
+    X, W, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / K ** 0.5, torch.randn(N, generator=g)
+    Y = _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 1).cpu()
+    ref = torch.relu(X.double() @ W.double().t() + b.double())
+    assert (Y.double() - ref).abs().max().item() <= 1e-4
