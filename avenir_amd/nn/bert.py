@@ -33,6 +33,7 @@ from dataclasses import asdict, dataclass, fields
 import torch
 
 from .. import _native
+from ..utils.params import param_epoch
 
 #: activation code of mlp.hip's linear_act_fwd for the erf GELU
 _GELU = 6
@@ -161,7 +162,7 @@ class BertEncoder(torch.nn.Module):
         """[3H, H] weights and [3H] bias of layer i's Q, K, V (cached per parameter version)."""
         n = _layer_names(i)
         ps = [self.p(n[k] + s) for k in ("q", "k", "v") for s in (".weight", ".bias")]
-        key = (i,) + tuple((t.data_ptr(), t._version) for t in ps)
+        key = (i, param_epoch()) + tuple((t.data_ptr(), t._version) for t in ps)
         hit = self._qkv_cache.get(i)
         if hit is not None and hit[0] == key:
             return hit[1], hit[2]

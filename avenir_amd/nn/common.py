@@ -49,15 +49,25 @@ def create_loss(name: str, reduction: str = "mean"):
 def create_optimizer(params, name: str, lr: float = 1e-4, weight_decay: float = 0.0, momentum: float = 0.0,
                      eps: float = 1e-8, dampening: float = 0.0, nesterov: bool = False,
                      betas: Sequence[float] = (0.9, 0.999), alpha: float = 0.99, capturable: bool = False):
+    """The reference's optimiser names (P/lib/tnn.py).  GPU parameters take torch's fused
+    single-kernel Adam / AdamW: the multi-tensor (foreach) update was 4 launches, ~45 us of a
+    0.55 ms LSTM training step at the reference shape (profiles/r5_lstm_fp32_v4_kernel_stats.csv).
+    (A fused step does not bump the parameters' version counters; the framework's packed-parameter
+    caches key on utils/params.param_epoch() as well, which every optimizer step advances.)"""
+    params = list(params)
+    flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
+    fused = (bool(flat) and all(p.is_cuda and p.dtype == torch.float32 for p in flat)
+             and os.environ.get("AVMI_FUSED_OPT", "1") != "0")           # A/B switch
+    fk = {"fused": True} if fused else {}
     if name == "sgd":
         return torch.optim.SGD(params, lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                                nesterov=nesterov)
     if name == "adam":
         return torch.optim.Adam(params, lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
-                                capturable=capturable)
+                                capturable=capturable, **fk)
     if name == "adamw":
         return torch.optim.AdamW(params, lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
-                                 capturable=capturable)
+                                 capturable=capturable, **fk)
     if name == "rmsprop":
         return torch.optim.RMSprop(params, lr=lr, alpha=alpha, eps=eps, weight_decay=weight_decay, momentum=momentum,
                                    capturable=capturable)

@@ -155,9 +155,14 @@ class LstmNetwork(torch.nn.Module):
         self.train()
         self._dp = dp
         step = None
+        # no host synchronisation inside the loop: the epoch permutations go up from pinned memory
+        # without blocking, and the epoch losses stay on the device until the fit ends
+        dev_losses = []
+        pin = self.device.type == "cuda"
         try:
             for _ in range(num_iter if num_iter is not None else self.num_iter):
-                perm = torch.randperm(n, generator=g).to(self.device)[: nb * bs]
+                perm = torch.randperm(n, generator=g)
+                perm = (perm.pin_memory().to(self.device, non_blocking=True) if pin else perm)[: nb * bs]
                 xb = x[perm].view((nb, bs) + tuple(x.shape[1:]))
                 yb = tgt[perm].view((nb, bs) + tuple(tgt.shape[1:]))
                 if step is None:
@@ -167,7 +172,9 @@ class LstmNetwork(torch.nn.Module):
                 tot = torch.zeros((), device=self.device)
                 for b in range(nb):
                     tot += step(xb[b], yb[b])
-                self.losses.append(float(tot) / nb)
+                dev_losses.append(tot / nb)
+            if dev_losses:
+                self.losses.extend(torch.stack(dev_losses).tolist())
         finally:
             self._dp = None
         self.eval()

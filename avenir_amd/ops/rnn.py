@@ -38,6 +38,7 @@ import weakref
 import torch
 
 from .. import _native
+from ..utils.params import param_epoch
 
 MAX_FUSED_HIDDEN = 128
 
@@ -137,7 +138,8 @@ def to_kernel_order(w: torch.Tensor, H: int) -> torch.Tensor:
 
 class _PackCacheF32:
     """The fp32 layer's re-laid parameters (``lstm_pack_f32``: W_hh fragments, W_hhᵀ fragments,
-    kernel-order W_ih and b_ih + b_hh — ONE launch), keyed on the four tensors' (storage, version):
+    kernel-order W_ih and b_ih + b_hh — ONE launch), keyed on the four tensors' (storage, version)
+    and the optimizer-step epoch (utils/params.py: fused optimizers do not bump versions):
     inference re-uses them across calls, training re-packs once per optimizer step.  Inside a
     HIP-graph capture the pack is recorded, so replays re-pack."""
 
@@ -156,7 +158,8 @@ class _PackCacheF32:
         ts = (w_ih, w_hh, b_ih, b_hh)
         if torch.cuda.is_current_stream_capturing():
             return self._pack(*ts)
-        key = tuple((t.data_ptr(), t._version, tuple(t.shape)) if t is not None else None for t in ts)
+        key = (param_epoch(),) + tuple((t.data_ptr(), t._version, tuple(t.shape)) if t is not None else None
+                                       for t in ts)
         hit = self.d.get(key)
         # the entry must belong to THESE live tensors: a freed tensor's memory (same address, shape
         # and version 0) may be re-used by a new one with different values
@@ -184,7 +187,7 @@ class _FragCache:
     def get(self, w_ih: torch.Tensor, w_hh: torch.Tensor, H: int):
         if torch.cuda.is_current_stream_capturing():
             return pack_weights(w_ih, w_hh, H)
-        key = (w_ih.data_ptr(), w_ih._version, tuple(w_ih.shape), w_hh.data_ptr(), w_hh._version, H)
+        key = (param_epoch(), w_ih.data_ptr(), w_ih._version, tuple(w_ih.shape), w_hh.data_ptr(), w_hh._version, H)
         hit = self.d.get(key)
         if hit is not None and hit[0]() is w_ih and hit[1]() is w_hh:     # the same live tensors
             return hit[2]

@@ -208,3 +208,37 @@ def test_mlp_fused_trains_on_gpu(cuda):
     assert any(type(l).__name__ == "FusedLinear" for l in m.layers)
     m.fit(x, y)
     assert m.evaluate_model(x, y, "accuracy") > 0.95
+
+
+def test_optimizer_steps_advance_the_param_epoch():
+    """Fused optimizers update parameters without bumping their version counters; the packed-weight
+    caches also key on the process-wide optimizer-step epoch, which every step advances."""
+    from avenir_amd.utils.params import param_epoch
+    p = torch.nn.Parameter(torch.randn(5))
+    opt = torch.optim.Adam([p], lr=0.1, fused=True)
+    p.grad = torch.ones(5)
+    e, v = param_epoch(), p._version
+    opt.step()
+    assert param_epoch() == e + 1
+    assert p._version == v          # why the epoch is needed (torch behaviour this guards against)
+
+
+@pytest.mark.gpu
+def test_fused_lstm_with_a_fused_optimizer_matches_foreach(cuda):
+    """Eager training of the fused LSTM with torch's fused Adam equals the foreach Adam: the
+    packed-weight cache must see fused updates (they leave the version counters alone)."""
+    from avenir_amd.ops.rnn import FusedLSTM
+    res = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        m = FusedLSTM(3, 16, 2).to(cuda)
+        opt = torch.optim.Adam(m.parameters(), lr=0.05, fused=fused)
+        x = torch.randn(32, 5, 3, device=cuda)
+        for _ in range(4):
+            opt.zero_grad()
+            out, _ = m(x)
+            out[:, -1].pow(2).sum().backward()
+            opt.step()
+        res.append({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    for k in res[0]:
+        assert torch.allclose(res[0][k], res[1][k], atol=1e-5), k
