@@ -345,7 +345,10 @@ int linear_act_fwd_slices(int M, int N, int K) {
   // parallelism gains — the LSTM's dx = dZ W_ih at 5,000 x 5 x 400)
   if (tiles >= 256 || K < 16 * KC) return 1;
   // a few output tiles over a long K (a query's rows through a BERT projection: 2 x 12 tiles
-  // over K = 3,072): split K so ~512 workgroups cover the 256 CUs, each slice >= 4 chunks
+  // over K = 3,072): split K so ~512 workgroups cover the 256 CUs, each slice >= 4 chunks.
+  // (Tried and measured slower: one-shot slices that issue all 128 K-columns' loads at once, 16.6
+  // -> 20.8 us at 128 x 768 x 3,072 — so not per-chunk latency; likely the re-reads of X by every N tile and of W by
+  // both M tiles, an estimated ~38 MB of L2 / MALL traffic: profiles/r5_splitk_oneshot_ab.jsonl)
   long long s = (512 + tiles - 1) / tiles;
   s = std::min<long long>(s, K / (4 * KC));
   return (int)std::max(1LL, std::min(s, 64LL));
