@@ -167,6 +167,85 @@ __global__ __launch_bounds__(MT) void linear_act_fwd_kernel(const float* __restr
   }
 }
 
+// Large outputs (>= 1,024 rows and columns): a 128 x 128 tile per workgroup, each wave a 64 x 64
+// quarter as 2 x 2 v_mfma_f32_32x32x2_f32 blocks, so every A / B value read from LDS feeds two
+// MFMAs and each K chunk brings 16 MACs per staged byte (the 64 x 64 tile: 8).  Chunks of 32 K
+// columns register-prefetched during the MFMAs, as the 64 x 64 kernel.  VEC (K % 4 == 0,
+// 16-byte-aligned operands) only.
+constexpr int TB = 128, KCB = 32, LSB = KCB + 1;
+__global__ __launch_bounds__(MT) void linear_act_fwd_big_kernel(const float* __restrict__ X,
+                                                                const float* __restrict__ W,
+                                                                const float* __restrict__ b, float* __restrict__ Y,
+                                                                int M, int N, int K, int act, int xcd) {
+  __shared__ float sX[TB][LSB];
+  __shared__ float sW[TB][LSB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm = blockIdx.y, tn = blockIdx.x;
+  if (xcd) av::grouped_tile(av::xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y), gridDim.y,
+                            gridDim.x, 8, tm, tn);
+  const long long m0 = (long long)tm * TB;
+  const int n0 = tn * TB;
+  // thread's staging slots: 4 float4 of X and 4 of W per chunk (rows e >> 3, columns (e & 7) * 4)
+  float4 px[4], pw[4];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + MT * i, r = e >> 3, c = (e & 7) * 4, k = k0 + c;
+      const long long m = m0 + r;
+      const int n = n0 + r;
+      px[i] = (m < M && k < K) ? *reinterpret_cast<const float4*>(X + m * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pw[i] = (n < N && k < K) ? *reinterpret_cast<const float4*>(W + (long long)n * K + k)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  load(0);
+  const int li = lane & 31, lk = lane >> 5;
+  for (int k0 = 0; k0 < K; k0 += KCB) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + MT * i, r = e >> 3, c = (e & 7) * 4;
+      sX[r][c] = px[i].x; sX[r][c + 1] = px[i].y; sX[r][c + 2] = px[i].z; sX[r][c + 3] = px[i].w;
+      sW[r][c] = pw[i].x; sW[r][c + 1] = pw[i].y; sW[r][c + 2] = pw[i].z; sW[r][c + 3] = pw[i].w;
+    }
+    __syncthreads();
+    if (k0 + KCB < K) load(k0 + KCB);
+#pragma unroll
+    for (int k = 0; k < KCB; k += 2) {
+      float a[2], w[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = sX[wm * 64 + 32 * i + li][k + lk];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) w[j] = sW[wn * 64 + 32 * j + li][k + lk];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], w[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+    if (col >= N) continue;
+    const float bias = b ? b[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < M) Y[row * N + col] = act_fwd(acc[i][j][r] + bias, act);
+      }
+  }
+}
+
 // Y[e] = act(sum_s P[s][e] + b[e % N]): the S slices summed in slice order (deterministic), the
 // loads of 8 slices issued together
 __global__ __launch_bounds__(256) void linear_splitk_epilogue_kernel(const float* __restrict__ P,
@@ -339,6 +418,15 @@ static bool xcd_tiles_enabled() {
   return on;
 }
 
+// AVMI_BIG_TILES=0: the 64 x 64 tile for every shape (A/B switch)
+static bool big_tiles_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("AVMI_BIG_TILES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int linear_act_fwd_slices(int M, int N, int K) {
   const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   // (K < 512: at most 16 chunks per tile, where the extra epilogue launch costs more than the
@@ -377,6 +465,13 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
     S = linear_splitk_partial(X, W, partial, M, N, K, S, stream);
     const long long MN = (long long)M * N;
     linear_splitk_epilogue_kernel<<<(unsigned)((MN + 255) / 256), 256, 0, stream>>>(partial, b, Y, MN, N, S, act);
+    AV_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (vec && M >= 1024 && N >= 1024 && big_tiles_enabled()) {
+    dim3 gb((unsigned)((N + TB - 1) / TB), (unsigned)((M + TB - 1) / TB));
+    const int xcd = xcd_tiles_enabled() && gb.x * gb.y >= 64 ? 1 : 0;
+    linear_act_fwd_big_kernel<<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, xcd);
     AV_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -36,7 +36,7 @@ def test_linear_act_fwd_split_k_vs_fp64(cuda, M, N, K, act):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(700, 650, 96), (4096, 3072, 64), (65, 4100, 32)])
+@pytest.mark.parametrize("M,N,K", [(700, 650, 96), (4096, 3072, 64), (65, 4100, 32), (1030, 1100, 100), (2048, 2304, 768)])
 def test_linear_act_fwd_xcd_tile_order(cuda, M, N, K):
     """The XCD-aware grouped tile order (>= 64 output tiles, counts not a multiple of 8, a partial
     last group of tile rows) still covers every output tile exactly once."""
