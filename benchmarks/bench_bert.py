@@ -46,5 +46,33 @@ def main():
                           "tokens_per_s": B * S / t_mine}), flush=True)
 
 
+def corpus():
+    """semanticSearch's corpus encoding: 256 synthetic documents of ~100 words (5 sentences each),
+    one encoder pass per document / sentence (``add``) against the batched ``add_many``."""
+    import random
+    from avenir_amd.nn.bert import WordPiece, bert_embedder
+    from avenir_amd.text.semsearch import SemanticSearch
+    torch.manual_seed(0)
+    enc = BertEncoder(BertConfig()).to("cuda")
+    emb = bert_embedder(enc, WordPiece())
+    rnd = random.Random(0)
+    words = [f"w{i}" for i in range(5000)]
+    docs = [". ".join(" ".join(rnd.choice(words) for _ in range(20)) for _ in range(5)) + "." for _ in range(256)]
+    res = {}
+    for name, fn in (("add", lambda: [ss.add(d) for d in docs]), ("add_many", lambda: ss.add_many(docs))):
+        ss = SemanticSearch(emb, device="cuda")
+        fn()                                      # warm-up
+        ss = SemanticSearch(emb, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        res[name] = time.perf_counter() - t0
+    print(json.dumps({"bench": "semantic_search_corpus_encoding", "docs": len(docs), "add_s": res["add"],
+                      "add_many_s": res["add_many"], "speedup": res["add"] / res["add_many"],
+                      "docs_per_s": len(docs) / res["add_many"]}), flush=True)
+
+
 if __name__ == "__main__":
     main()
+    corpus()

@@ -194,3 +194,39 @@ def test_bert_host_ids_and_range_checks(cuda):
         mine(torch.full((3, 19), 500), mask, tt)
     with pytest.raises(RuntimeError):
         mine(torch.full((3, 19), 500, device=cuda), mask, tt)
+
+
+def _ss_pair(device="cpu"):
+    from avenir_amd.text.semsearch import SemanticSearch
+    _, mine = _pair(V=1000, P=32)
+    mine = mine.to(device)
+    emb = bert_embedder(mine, WordPiece(vocab_size=1000), max_len=12, batch_tokens=64)
+    docs = ["apple fruit fiber vitamin sugar. sweet and fresh apples taste good.",
+            "smartphone market share apple iphone samsung.", "",
+            "peach fruit sugar vitamin potassium, a long document with many words that needs more than one "
+            "window of word pieces to encode.", "short."]
+    one = SemanticSearch(emb, device=device)
+    for d in docs:
+        one.add(d)
+    return one, SemanticSearch(emb, device=device).add_many(docs)
+
+
+def _check_batched(one, many):
+    from avenir_amd.text.semsearch import ALGOS
+    assert len(many.docs) == len(one.docs)
+    for a, b in zip(one.tok_emb + one.sent_emb, many.tok_emb + many.sent_emb):
+        assert a.shape == b.shape and torch.allclose(a.cpu(), b.cpu(), atol=1e-4)
+    for algo in ALGOS:
+        assert torch.allclose(one.scores("fruit vitamin sugar", algo).cpu(), many.scores("fruit vitamin sugar", algo).cpu(),
+                              atol=1e-4), algo
+
+
+def test_semantic_search_batched_corpus_equals_one_by_one():
+    """add_many: every document's and sentence's windows in padded, length-sorted encoder batches
+    (windows of 12 pieces, 64-token batches here) == adding the documents one at a time."""
+    _check_batched(*_ss_pair())
+
+
+@pytest.mark.gpu
+def test_semantic_search_batched_corpus_gpu(cuda):
+    _check_batched(*_ss_pair(cuda))
