@@ -184,7 +184,8 @@ struct Tab {
 // the rows split over ``nthreads`` threads, each formatting its block into its own buffer
 static std::vector<std::string> format_parts(const std::vector<FmtCol>& cols, int64_t n, const std::string& delim,
                                              int nthreads) {
-  for (const auto& c : cols) {
+  // (no rows: empty columns hold no buffers — an empty selection of lines has null span pointers)
+  for (const auto& c : (n > 0 ? cols : std::vector<FmtCol>{})) {
     if ((c.kind == FmtCol::STR || c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) && (!c.table || !c.idx))
       throw std::runtime_error("format_columns: string column without table / index");
     if ((c.kind == FmtCol::LIST || c.kind == FmtCol::PAIRS) && !c.off)

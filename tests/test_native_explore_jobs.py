@@ -383,3 +383,33 @@ def test_distance_store_native_equals_python(tmp_path):
     for f in ("indptr.npy", "cols.npy", "vals.npy"):
         assert np.array_equal(np.load(tmp_path / "native" / f), np.load(tmp_path / "py" / f)), f
     assert (tmp_path / "native" / "entities.json").read_text() == (tmp_path / "py" / "entities.json").read_text()
+
+
+@pytest.mark.parametrize("name", ["spc", "rue", "pro"])
+def test_jobs_with_no_output_rows(tmp_path, name):
+    """A job whose selection keeps no line writes an empty output (the native formatter got null
+    span pointers for an empty selection and raised)."""
+    argv, cfg = _setup(tmp_path, name, False)
+    text = cfg.read_text()
+    text = {"spc": lambda t: t.replace("score.threshold=0.55", "score.threshold=1.5"),
+            "rue": lambda t: t,
+            "pro": lambda t: t.replace("5 gt 0.5", "5 gt 5.0")}[name](text)
+    cfg.write_text(text)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "out"), "-c", str(cfg), "--device", "cpu"]) == 0
+    if name != "rue":
+        assert _lines(tmp_path / "out") == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["spc", "pro", "usb"])
+def test_jobs_with_no_output_rows_gpu(tmp_path, name):
+    """The same on the device paths (device tokenizer, device formatter)."""
+    argv, cfg = _setup(tmp_path, name, False)
+    text = cfg.read_text()
+    text = {"spc": lambda t: t.replace("score.threshold=0.55", "score.threshold=1.5"),
+            "pro": lambda t: t.replace("5 gt 0.5", "5 gt 5.0"),
+            "usb": lambda t: t}[name](text)
+    cfg.write_text(text)
+    assert main([str(a) for a in argv] + ["-o", str(tmp_path / "out"), "-c", str(cfg), "--device", "cuda"]) == 0
+    if name != "usb":
+        assert _lines(tmp_path / "out") == []
