@@ -413,3 +413,20 @@ def test_jobs_with_no_output_rows_gpu(tmp_path, name):
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "out"), "-c", str(cfg), "--device", "cuda"]) == 0
     if name != "usb":
         assert _lines(tmp_path / "out") == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["loo", "loo_test", "nuc", "hash", "dummy", "rue", "nads"])
+def test_gpu_equals_cpu(tmp_path, name):
+    """The device paths of the record-wise jobs (device tokenizer, LDS-privatised statistics,
+    device formatter) write what the host paths write."""
+    argv, cfg = _setup(tmp_path, name, False)
+    outs = {}
+    for dev in ("cpu", "cuda"):
+        assert main([str(a) for a in argv] + ["-o", str(tmp_path / dev), "-c", str(cfg), "--device", dev]) == 0
+        outs[dev] = _lines(tmp_path / dev)
+        if name == "loo":
+            outs[dev + "_stat"] = _lines(tmp_path / "stat_lit.txt")
+    assert outs["cpu"] and outs["cpu"] == outs["cuda"]
+    if name == "loo":
+        assert outs["cpu_stat"] == outs["cuda_stat"]
