@@ -450,7 +450,7 @@ def spc(args):
         met_l = rule.evaluate(RecordColumns(rec, [o for o, m in fm.items() if m == "n"])).double()
         comm = ctx.comm
         pair = torch.stack([t_l, met_l], 1)
-        allp = comm.all_gather_v(pair.cpu()) if comm.is_distributed else pair.cpu()
+        allp = comm.all_gather_v(pair) if comm.is_distributed else pair     # scored on the job's device
         score = _locality_scores(allp[:, 0], allp[:, 1], span)
         base = rec.line_base
         sc = score[base: base + rec.n_lines]
@@ -473,7 +473,7 @@ def _locality_scores(t: torch.Tensor, met: torch.Tensor, span: float) -> torch.T
     ts, ms = t[order], met[order]
     cm = torch.cumsum(ms, 0)
     lo = torch.searchsorted(ts, ts - span, right=False)
-    idx = torch.arange(len(ts))
+    idx = torch.arange(len(ts), device=t.device)
     n_in = (idx - lo + 1).double()
     met_in = cm - torch.where(lo > 0, cm[(lo - 1).clamp_min(0)], torch.zeros_like(cm))
     score = torch.zeros_like(t)

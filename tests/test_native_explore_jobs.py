@@ -416,7 +416,7 @@ def test_jobs_with_no_output_rows_gpu(tmp_path, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["loo", "loo_test", "nuc", "hash", "dummy", "rue", "nads"])
+@pytest.mark.parametrize("name", ["loo", "loo_test", "nuc", "hash", "dummy", "rue", "nads", "spc", "bag"])
 def test_gpu_equals_cpu(tmp_path, name):
     """The device paths of the record-wise jobs (device tokenizer, LDS-privatised statistics,
     device formatter) write what the host paths write."""
