@@ -528,15 +528,16 @@ def _bagging_native(ctx, rec, bagging_indices):
     n = len(spans)
     sizes = comm.all_gather_object(n) if comm.is_distributed else [n]
     base, total = sum(sizes[: comm.rank]), sum(sizes)
+    fast = not comm.is_distributed and spans.dev is not None
     idx = bagging_indices(n, ctx.get_int("batch.size", 10000), seed=ctx.get_int("random.seed", 0), base=base,
-                          total=total).long()
-    local = (idx >= base) & (idx < base + n)
-    if not comm.is_distributed and spans.dev is not None:
+                          total=total, device=spans.dev[1].device if fast else "cpu").long()
+    if fast:
         # one process with the device tokenizer: every pick is a local line — a device selection of
         # the uploaded line bytes, formatted by format.hip (no host line index, no host copy)
         sel = spans.select(idx - base)
         ctx.emit_columns([sel.column("r", delims=ctx.native_delim())], len(sel))
         return
+    local = (idx >= base) & (idx < base + n)
     _, addr, ln = spans.spans()
     out_a = torch.zeros(idx.numel(), dtype=torch.int64)
     out_l = torch.zeros(idx.numel(), dtype=torch.int64)

@@ -115,12 +115,14 @@ def bagging_indices(n: int, batch_size: int | None = None, seed: int = 0, base: 
     from ..ops import resample_ops as RS
     total = n if total is None else total
     bs = batch_size or total
-    g = torch.arange(base, base + n, dtype=torch.long)
+    dev = torch.device(device)
+    g = torch.arange(base, base + n, dtype=torch.long, device=dev)
     b0 = (g // bs) * bs
     b1 = torch.clamp(b0 + bs, max=total)
-    u = RS.uniform(seed, RS.STREAM_BAGGING, base, n, "cpu").double()
-    pick = b0 + torch.minimum((u * (b1 - b0).double()).long(), (b1 - b0 - 1).clamp_min(0))
-    return pick.to(device)
+    # the draws on the target device (resample_uniform_kernel: the same Philox values as the host
+    # twin; the numpy twin took ~0.1 s of a 2^21-record job)
+    u = RS.uniform(seed, RS.STREAM_BAGGING, base, n, dev).double()
+    return b0 + torch.minimum((u * (b1 - b0).double()).long(), (b1 - b0 - 1).clamp_min(0))
 
 
 class AdaBoost:
