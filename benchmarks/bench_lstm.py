@@ -23,7 +23,9 @@ from avenir_amd.ops.rnn import FusedLSTM  # noqa: E402
 CONFIGS = [
     dict(name="reference_ct", B=1000, T=5, I=5, H=100, L=2, O=2),
     dict(name="b8k_t16_h64", B=8192, T=16, I=32, H=64, L=2, O=2),
-    dict(name="b64k_t32_h128", B=65536, T=32, I=16, H=128, L=2, O=2),
+    # MIOpen's graph capture at this size aborts the process inside hipBLASLt ("operation not
+    # permitted when stream is capturing" -> core dump), so that one arm is not run
+    dict(name="b64k_t32_h128", B=65536, T=32, I=16, H=128, L=2, O=2, skip=("miopen_graph",)),
 ]
 
 
@@ -120,6 +122,10 @@ def main():
             continue
         res = {}
         for impl in args.impls.split(","):
+            if impl in cfg.get("skip", ()):
+                print(json.dumps({"bench": "lstm", "config": cfg["name"], "impl": impl,
+                                  "skipped": "library graph capture aborts the process at this size"}), flush=True)
+                continue
             try:
                 res[impl] = run(cfg, impl, args.steps, args.warmup)
             except Exception as e:           # e.g. a library LSTM that refuses graph capture
