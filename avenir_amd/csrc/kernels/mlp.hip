@@ -427,6 +427,19 @@ static bool big_tiles_enabled() {
   return on;
 }
 
+// workgroups the split-K slices aim at (AVMI_SPLITK_TARGET, default 512): fewer slices mean longer
+// slices but less partial traffic for the slice sum / fused LayerNorm that follows (BERT B 1 x S 128,
+// 3 interleaved runs each: 512 -> 1.018 ms, 384 -> 1.014 ms per pass, within noise:
+// profiles/r5_splitk_target_ab.jsonl)
+static long long split_target() {
+  static const long long t = [] {
+    const char* e = std::getenv("AVMI_SPLITK_TARGET");
+    const long long v = e ? std::atoll(e) : 512;
+    return v >= 64 ? v : 512;
+  }();
+  return t;
+}
+
 int linear_act_fwd_slices(int M, int N, int K) {
   const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   // (K < 512: at most 16 chunks per tile, where the extra epilogue launch costs more than the
@@ -437,7 +450,7 @@ int linear_act_fwd_slices(int M, int N, int K) {
   // (Tried and measured slower: one-shot slices that issue all 128 K-columns' loads at once, 16.6
   // -> 20.8 us at 128 x 768 x 3,072 — so not per-chunk latency; likely the re-reads of X by every N tile and of W by
   // both M tiles, an estimated ~38 MB of L2 / MALL traffic: profiles/r5_splitk_oneshot_ab.jsonl)
-  long long s = (512 + tiles - 1) / tiles;
+  long long s = (split_target() + tiles - 1) / tiles;
   s = std::min<long long>(s, K / (4 * KC));
   return (int)std::max(1LL, std::min(s, 64LL));
 }
