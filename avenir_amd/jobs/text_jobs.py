@@ -241,13 +241,24 @@ def text_encoder(args):
             items = sorted(fr.items(), key=lambda t: -t[1]) if isinstance(fr, dict) else fr
             _out(ctx, [f"{' '.join(k) if isinstance(k, tuple) else k},{v:.6f}" for k, v in items])
             return
-        ng.getNGramIndex()
-        lines = []
-        for d in docs:
-            v = ng.getVector(d, True, True)
-            if int((v != 0).sum()) > 0:
-                lines.append(",".join(f"{x:.6f}" for x in v.tolist()))
-        _out(ctx, lines)
+        # the [docs, n-grams] count matrix from one scatter-add, rows normalised, and the text from
+        # the native formatter (a per-document Python vector build and per-value f-string took
+        # 1.5 s for 6,000 documents)
+        idx = ng.getNGramIndex()
+        V = len(idx)
+        ids = [[idx[g] for g in ng.toNGram(d) if g in idx] for d in docs]
+        flat = torch.tensor([r * V + j for r, row in enumerate(ids) for j in row], dtype=torch.long)
+        M = torch.zeros(len(docs) * max(V, 1))
+        if flat.numel():
+            M.index_add_(0, flat, torch.ones(flat.numel()))
+        M = M.view(len(docs), max(V, 1))[:, :V]
+        keep = (M != 0).any(1)
+        M = M[keep]
+        M = M / M.sum(1, keepdim=True)
+        if getattr(ctx.args, "output", None) and V:
+            ctx.emit_columns([("f", M[:, j].double().contiguous(), 6) for j in range(V)], int(M.shape[0]))
+        else:
+            _out(ctx, [",".join(f"{x:.6f}" for x in row) for row in M.tolist()])
         return
     from ..nn.unsupervised import AutoEncoder
     ae = AutoEncoder.from_config(ctx.cfg, device=ctx.device)

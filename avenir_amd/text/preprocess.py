@@ -344,11 +344,12 @@ class NGram:
     def getVector(self, words, by_count: bool = True, normalized: bool = False) -> torch.Tensor:
         idx = self.getNGramIndex()
         v = torch.zeros(len(idx))
-        for g in self.toNGram(words):
-            if g in idx:
-                v[idx[g]] += 1 if by_count else 0
-                if not by_count:
-                    v[idx[g]] = 1
+        hit = torch.tensor([idx[g] for g in self.toNGram(words) if g in idx], dtype=torch.long)
+        if hit.numel():
+            if by_count:
+                v.index_add_(0, hit, torch.ones(hit.numel()))
+            else:
+                v[hit] = 1.0
         if normalized and v.sum() > 0:
             v /= v.sum()
         return v

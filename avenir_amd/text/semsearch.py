@@ -165,13 +165,20 @@ def corpus_embedder(docs: Sequence[str], dim: int = 100, epochs: int = 10, windo
             v = fallback([tokens[k] for k in unk]).to(W.device)
             out[unk] = v / v.norm(dim=1, keepdim=True).clamp_min(1e-12) * scale
         return out
+
+    def many(token_lists):
+        """``emb`` of many token lists with one vocabulary lookup and one gather."""
+        lens = [len(t) for t in token_lists]
+        flat = [t for ts in token_lists for t in ts]
+        if not flat:
+            return [torch.zeros((0, dim), device=W.device) for _ in token_lists]
+        return list(torch.split(emb(flat), lens))
     emb.model = w2v
+    emb.many = many
     return emb
 
 
 def search_corpus(docs: Sequence[str], dim: int = 100, epochs: int = 10, device="cpu", seed: int = 0) -> SemanticSearch:
     """A :class:`SemanticSearch` over ``docs`` with the corpus-trained embedder."""
     ss = SemanticSearch(corpus_embedder(docs, dim, epochs, device=device, seed=seed), device=device)
-    for d in docs:
-        ss.add(d)
-    return ss
+    return ss.add_many(docs)

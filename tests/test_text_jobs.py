@@ -5,6 +5,7 @@ import json
 import random
 
 import pytest
+import torch
 
 from avenir_amd.cli import JOBS, main
 
@@ -147,3 +148,39 @@ def test_text_classifier_and_search(tmp_path, capsys):
           "--k", "5", "--output", str(out)])
     hits = [l.split(",")[1].rsplit("/", 1)[1] for l in out.read_text().splitlines()]
     assert len(hits) == 5 and sum(h.startswith("space") for h in hits) >= 4
+
+
+def test_text_encoder_vectorise_equals_per_document_vectors(tmp_path):
+    """The one-scatter vectorise output == each document's getVector, formatted per value."""
+    from avenir_amd.jobs.text_jobs import _clean, _docs
+    from avenir_amd.text.preprocess import BiGram
+    d = _corpus(tmp_path, n_per=20)
+    out = tmp_path / "vec.csv"
+    main(["textEncoder", "--mode", "vectorise", "--kind", "bi", "--input", str(d), "--output", str(out)])
+    texts, _ = _docs(str(d))
+    docs = _clean(texts)
+    ng = BiGram()
+    for x in docs:
+        ng.countDocNGrams(x)
+    ng.remLowCount(3)
+    ref = []
+    for x in docs:
+        v = ng.getVector(x, True, True)
+        if int((v != 0).sum()) > 0:
+            ref.append(",".join(f"{y:.6f}" for y in v.tolist()))
+    assert out.read_text().splitlines() == ref
+
+
+def test_corpus_embedder_batched_adds_equal_one_by_one(tmp_path):
+    """search_corpus adds the corpus through the embedder's batched lookup: same vectors as one
+    add per document (vocabulary words and hashed unknown words alike)."""
+    from avenir_amd.text.semsearch import SemanticSearch, corpus_embedder
+    d = _corpus(tmp_path, n_per=4)
+    docs = [f.read_text() for f in sorted(d.iterdir())] + ["zzz unknownword rocket.", ""]
+    emb = corpus_embedder(docs, dim=16, epochs=2)
+    one = SemanticSearch(emb)
+    for x in docs:
+        one.add(x)
+    many = SemanticSearch(emb).add_many(docs)
+    for a, b in zip(one.tok_emb + one.sent_emb, many.tok_emb + many.sent_emb):
+        assert torch.equal(a, b)
