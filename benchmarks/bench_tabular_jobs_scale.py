@@ -36,6 +36,25 @@ def main_(argv=None) -> int:
                          f"crc.dest.attributes={','.join(map(str, ords[1:]))}\n")
         jobs = {"bayesianDistribution": ["--schema", str(schema)], "cramerCorrelation": ["-c", str(props)],
                 "mutualInformation": ["--schema", str(schema)]}
+        # the model builders on the call-hangup schema (tests/test_cli.py's configurations)
+        hdata, hschema = tmp / "hangup.csv", tmp / "hangup.json"
+        hdata.write_text("\n".join(synth.call_hangup_lines(args.rows // 4, seed=2)) + "\n")
+        hschema.write_text(json.dumps(synth.CALL_HANGUP_SCHEMA))
+        tcfg = tmp / "detr.properties"
+        tcfg.write_text("dtb.split.algorithm=giniIndex\ndtb.path.stopping.strategy=maxDepth\ndtb.max.depth.limit=2\n"
+                        "dtb.num.trees=3\n")
+        lcfg = tmp / "lr.properties"
+        lcfg.write_text("lor.iteration.limit=5\nlor.positive.class.value=T\n")
+        for job, cfg in (("decisionTree", tcfg), ("randomForest", tcfg), ("logisticRegression", lcfg)):
+            times = []
+            for rep in range(2):
+                t0 = time.perf_counter()
+                assert main([job, "-i", str(hdata), "-o", str(tmp / f"{job}{rep}"), "-c", str(cfg), "--schema",
+                             str(hschema), "--device", args.device]) == 0
+                times.append(time.perf_counter() - t0)
+            print(json.dumps({"bench": "tabular_job_scale", "job": job, "rows": args.rows // 4,
+                              "file_bytes": os.path.getsize(hdata), "cold_s": times[0], "warm_s": times[1],
+                              "rows_per_s": (args.rows // 4) / times[1]}), flush=True)
         for job, extra in jobs.items():
             times = []
             for rep in range(2):
