@@ -359,28 +359,26 @@ def _num_distr_native(ctx, rec, kords, attrs, prec):
     from ..data.records import sorted_key_tuples
     g, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], ctx.comm) if kords else \
         (torch.zeros(rec.n_lines, dtype=torch.long, device=rec.device), 1, torch.zeros((1, 0), dtype=torch.long))
-    # the histograms and moments on the job's device: bincount privatises a few bins per block
-    # (a host index_add_ per statistic took most of the job at 2^21 records)
-    dev = rec.device
-    g = g.to(dev)
+    g = g.cpu()
     keys = [tuple(rec.vocab[c] for c in row) for row in ktab.tolist()]
     d = ctx.delim_out
     out = []
     for a in attrs:
         bw = float(ctx.cfg.values.get(f"attrBinWidth.{a}", ctx.get_float("bin.width", 1.0)))
-        x = rec.field(a, numeric=True).double()
+        x = rec.field(a, numeric=True).double().cpu()
         b = torch.floor(x / bw).long()
         n = x.numel()
-        lh = torch.stack([b.min(), b.max()]).cpu() if n else torch.zeros(2, dtype=torch.long)
-        lo, hi = lh[:1].clone(), lh[1:].clone()
+        lo = torch.tensor([int(b.min()) if n else 0])
+        hi = torch.tensor([int(b.max()) if n else 0])
         if ctx.comm.is_distributed:
             ctx.comm.all_reduce(lo, "min")
             ctx.comm.all_reduce(hi, "max")
         B = int(hi - lo) + 1
-        Hh = torch.bincount(g * B + (b - int(lo)), minlength=G * B)[: G * B].view(G, B).cpu()
-        mom = torch.stack([torch.bincount(g, minlength=G)[:G].double(),
-                           torch.bincount(g, weights=x, minlength=G)[:G].double(),
-                           torch.bincount(g, weights=x * x, minlength=G)[:G].double()], 1).cpu()
+        Hh = torch.zeros(G * B, dtype=torch.long).index_add_(0, g * B + (b - int(lo)), torch.ones_like(b)).view(G, B)
+        mom = torch.zeros((G, 3), dtype=torch.float64)
+        mom[:, 0].index_add_(0, g, torch.ones_like(x))
+        mom[:, 1].index_add_(0, g, x)
+        mom[:, 2].index_add_(0, g, x * x)
         ctx.all_reduce(Hh, mom)
         for i, k in enumerate(keys):
             cnt = float(mom[i, 0])
