@@ -37,6 +37,16 @@ class P2PComm {
     flags_ = static_cast<unsigned*>(f);
     status_ = reinterpret_cast<int*>(flags_ + kFlagWords);
     hip_ok(hipMemset(flags_, 0, kFlagWords * sizeof(unsigned) + 256), "flag memset");
+    // the host-visible status word: pinned, coherent and mapped, so the host reads a kernel's
+    // verdict once the kernel has finished without synchronising the device
+    void* hs = nullptr;
+    hip_ok(hipHostMalloc(&hs, 256, hipHostMallocMapped | hipHostMallocCoherent), "host status alloc");
+    host_status_ = static_cast<volatile int*>(hs);
+    *host_status_ = 0;
+    void* hsd = nullptr;
+    hip_ok(hipHostGetDevicePointer(&hsd, hs, 0), "host status device pointer");
+    host_status_dev_ = static_cast<int*>(hsd);
+    hip_ok(hipEventCreateWithFlags(&last_, hipEventDisableTiming), "event create");
     hip_ok(hipMemset(data_, 0, 4 * (size_t)cap_), "data memset");
     hip_ok(hipDeviceSynchronize(), "sync");
     int khz = 0;
@@ -71,6 +81,7 @@ class P2PComm {
     view_.world = (int)world;
     view_.cap_bytes = cap_;
     view_.status = status_;
+    view_.host_status = host_status_dev_;
     for (int64_t k = 0; k < world; ++k) {
       if (k == rank) {
         view_.data[k] = data_;
@@ -93,7 +104,10 @@ class P2PComm {
     open_ = true;
   }
 
-  void set_timeout(double seconds) { timeout_ticks_ = (int64_t)(seconds * clock_khz_ * 1000.0); }
+  void set_timeout(double seconds) {
+    TORCH_CHECK(seconds > 0 && seconds < 1e7, "p2p: timeout out of range");
+    timeout_ticks_ = (int64_t)(seconds * clock_khz_ * 1000.0);
+  }
 
   // in-place sum of t over all ranks; epoch >= 1, strictly increasing by 1 per call on every rank
   void all_reduce(at::Tensor& t, int64_t epoch, bool two_shot) {
@@ -101,7 +115,7 @@ class P2PComm {
     TORCH_CHECK(t.is_cuda() && t.device().index() == device_, "p2p: tensor must live on the communicator's device");
     TORCH_CHECK(t.is_contiguous(), "p2p: tensor must be contiguous");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "p2p: tensor must be 16-byte aligned");
-    TORCH_CHECK(epoch >= 1 && epoch <= 0x7FFFFFFF, "p2p: epoch out of range");
+    TORCH_CHECK(epoch >= 1 && epoch <= avk::P2P_MAX_EPOCH, "p2p: epoch out of range");
     int dt;
     switch (t.scalar_type()) {
       case at::kFloat: dt = avk::P2P_F32; break;
@@ -114,10 +128,39 @@ class P2PComm {
     TORCH_CHECK(nbytes <= cap_, "p2p: message of ", nbytes, " bytes exceeds the staging capacity ", cap_);
     DevGuard g(t.device());
     hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_).stream();
+    // the staging parities are reused by epoch order, so consecutive calls must run in order: a
+    // call issued on another stream than the previous one first waits for that one
+    if (have_last_ && st != last_stream_) hip_ok(hipStreamWaitEvent(st, last_, 0), "stream wait");
     avk::p2p_all_reduce(t.data_ptr(), t.numel(), dt, view_, (unsigned)epoch, two_shot ? 1 : 0, timeout_ticks_, st);
+    hip_ok(hipEventRecord(last_, st), "event record");
+    last_stream_ = st;
+    have_last_ = true;
   }
 
-  // 0 = healthy; 1 = a wait timed out (synchronises the device)
+  // the host-visible status of the kernels that have FINISHED: 0 healthy, 1 a wait here timed out,
+  // 2 a peer reported a failure (no device synchronisation)
+  int64_t host_status() const { return host_status_ != nullptr ? *host_status_ : 0; }
+
+  // block the host until the last call's kernel has finished
+  void sync_last() const {
+    if (have_last_) hip_ok(hipEventSynchronize(last_), "event sync");
+  }
+
+  // true when the last call's kernel has finished (hipEventQuery; no synchronisation)
+  bool last_done() const { return !have_last_ || hipEventQuery(last_) == hipSuccess; }
+
+  // poison this rank's flags in every peer (their next wait on us ends with status 2), then wait
+  // for it: the failing rank's last act on the channel before it raises
+  void poison() {
+    TORCH_CHECK(open_, "p2p: open() the peers first");
+    DevGuard g(c10::Device(c10::DeviceType::CUDA, device_));
+    hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_).stream();
+    if (have_last_ && st != last_stream_) hip_ok(hipStreamWaitEvent(st, last_, 0), "stream wait");
+    avk::p2p_poison(view_, st);
+    hip_ok(hipStreamSynchronize(st), "poison sync");
+  }
+
+  // 0 = healthy; 1 = a wait timed out; 2 = a peer failed (synchronises the device)
   int64_t status() const {
     int s = 0;
     DevGuard g(c10::Device(c10::DeviceType::CUDA, device_));
@@ -138,9 +181,15 @@ class P2PComm {
     close_peers();
     (void)hipFree(data_);
     (void)hipFree(flags_);
+    if (host_status_ != nullptr) (void)hipHostFree(const_cast<int*>(host_status_));
+    if (last_ != nullptr) (void)hipEventDestroy(last_);
     data_ = nullptr;
     flags_ = nullptr;
     status_ = nullptr;
+    host_status_ = nullptr;
+    host_status_dev_ = nullptr;
+    last_ = nullptr;
+    have_last_ = false;
   }
 
  private:
@@ -149,6 +198,11 @@ class P2PComm {
   void* data_ = nullptr;
   unsigned* flags_ = nullptr;
   int* status_ = nullptr;
+  volatile int* host_status_ = nullptr;
+  int* host_status_dev_ = nullptr;
+  hipEvent_t last_ = nullptr;
+  hipStream_t last_stream_ = nullptr;
+  bool have_last_ = false;
   int clock_khz_ = 100000;
   int64_t timeout_ticks_ = 0;
   bool open_ = false;
@@ -167,6 +221,10 @@ void register_comm(py::module_& m) {
       .def("set_timeout", &P2PComm::set_timeout)
       .def("all_reduce", &P2PComm::all_reduce)
       .def("status", &P2PComm::status)
+      .def("host_status", &P2PComm::host_status)
+      .def("last_done", &P2PComm::last_done)
+      .def("sync_last", &P2PComm::sync_last, py::call_guard<py::gil_scoped_release>())
+      .def("poison", &P2PComm::poison)
       .def("close_peers", &P2PComm::close_peers)
       .def("release", &P2PComm::release);
 }

@@ -30,10 +30,15 @@
 //   e + 1 kernel observed every peer's e + 1 flag, and a peer raises that only after its own
 //   e kernel (which read our parity-(e & 1) buffers) completed in stream order.  So no end
 //   barrier is needed, and flags never need resetting.
-// Termination: every wait has a wall-clock bound (s_memrealtime, 100 MHz); on expiry the kernel
-//   records status = 1, stops waiting and drains (the result is then garbage and the host raises
-//   on its next status check).  A kernel that finds status already set waits for nothing, so a
-//   broken world cannot stack up timeouts.
+// Termination and failure reporting: every wait has a wall-clock bound (s_memrealtime, 100 MHz;
+//   the communicator's timeout, 600 s by default like the process group's); on expiry the kernel
+//   records status = 1 — in its uncached device word AND in a pinned host-mapped word the host
+//   reads without synchronising — stops waiting and drains.  The result is then garbage, and
+//   parallel/comm.py raises P2PError at the rank's next collective or status check, before any
+//   job writes output.  A kernel that finds status already set waits for nothing and raises its
+//   flags with the poison bit (P2P_POISON), so a peer's wait on it ends at once with status 2 —
+//   the failure propagates through the flags themselves instead of a cascade of timeouts (the
+//   host's p2p_poison launch does the same for every block before a failing rank raises).
 // Index safety: all indices are < units(n) (checked per unit against n for the operand); the
 //   staging buffers hold cap >= n * sizeof(T) bytes (checked by the binding), flag indices are
 //   src < P2P_MAX_RANKS, b < gridDim.x <= P2P_MAX_BLOCKS (checked by the launcher).
@@ -99,21 +104,36 @@ __device__ __forceinline__ void store_full(T* p, long long u, const Unit<T>& r) 
 // Publish this block's stores to every peer: each wave waits for its own stores and writes the L2
 // back (system-scope release fence), then one lane per peer raises the flag in that peer's array.
 // Then lanes 0..W-1 of wave 0 wait for the peers' flags in our own array; everyone acquires.
+__device__ __forceinline__ void fail(int* status, int* host_status, int code) {
+  __hip_atomic_store(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(host_status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void block_exchange(const PeerPtrs& P, int rank, int world, int b, unsigned sig,
-                                               int* status, long long timeout, bool skip_wait) {
+                                               int* status, int* host_status, long long timeout,
+                                               bool failed) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   const int t = threadIdx.x;
   if (t < world && t != rank) {
-    __hip_atomic_store(P.flags[t] + rank * avk::P2P_MAX_BLOCKS + b, sig, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    if (!skip_wait) {
+    __hip_atomic_store(P.flags[t] + rank * avk::P2P_MAX_BLOCKS + b, failed ? (sig | avk::P2P_POISON) : sig,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!failed) {
       unsigned* f = P.flags[rank] + t * avk::P2P_MAX_BLOCKS + b;
       const long long t0 = wall_clock64();
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < sig) {
+      for (;;) {
+        const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v >= sig) {
+          if (v & avk::P2P_POISON) fail(status, host_status, 2);   // the peer failed before us
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
         if (wall_clock64() - t0 > timeout) {
-          __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          fail(status, host_status, 1);
+          // overwrite the flag we raised for the late peer with the poisoned one: when its kernel
+          // arrives it fails too (status 2) instead of completing against our abandoned call
+          __hip_atomic_store(P.flags[t] + rank * avk::P2P_MAX_BLOCKS + b, sig | avk::P2P_POISON,
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
@@ -121,6 +141,16 @@ __device__ __forceinline__ void block_exchange(const PeerPtrs& P, int rank, int 
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+// every peer's flag slots for this rank, every block: poisoned (one thread per slot)
+__global__ __launch_bounds__(P2P_T) void p2p_poison_kernel(PeerPtrs P, int rank, int world) {
+  for (int i = threadIdx.x; i < world * avk::P2P_MAX_BLOCKS; i += P2P_T) {
+    const int peer = i / avk::P2P_MAX_BLOCKS;
+    if (peer == rank) continue;
+    __hip_atomic_store(P.flags[peer] + rank * avk::P2P_MAX_BLOCKS + i % avk::P2P_MAX_BLOCKS, 0xFFFFFFFFu,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 template <typename T>
@@ -133,7 +163,8 @@ __device__ __forceinline__ void add_unit(Unit<T>& a, const Unit<T>& b) {
 template <typename T>
 __global__ __launch_bounds__(P2P_T) void p2p_oneshot_kernel(T* __restrict__ x, long long n, PeerPtrs P, int rank,
                                                             int world, unsigned epoch, long long cap_elems,
-                                                            long long per, int* status, long long timeout) {
+                                                            long long per, int* status, int* host_status,
+                                                            long long timeout) {
   const int b = blockIdx.x;
   const long long nu = (n + Unit<T>::K - 1) / Unit<T>::K;
   const long long lo = (long long)b * per;
@@ -141,8 +172,8 @@ __global__ __launch_bounds__(P2P_T) void p2p_oneshot_kernel(T* __restrict__ x, l
   const long long poff = (long long)(epoch & 1u) * 2 * cap_elems;  // input staging of this parity
   T* mine = reinterpret_cast<T*>(P.data[rank]) + poff;
   for (long long u = lo + threadIdx.x; u < hi; u += P2P_T) store_full(mine, u, load_unit(x, u, n));
-  const bool skip = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  block_exchange(P, rank, world, b, 2u * epoch, status, timeout, skip);
+  const bool failed = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  block_exchange(P, rank, world, b, 2u * epoch, status, host_status, timeout, failed);
   for (long long u = lo + threadIdx.x; u < hi; u += P2P_T) {
     Unit<T> acc = load_full(reinterpret_cast<const T*>(P.data[0]) + poff, u);
     for (int k = 1; k < world; ++k) add_unit(acc, load_full(reinterpret_cast<const T*>(P.data[k]) + poff, u));
@@ -157,7 +188,7 @@ template <typename T>
 __global__ __launch_bounds__(P2P_T) void p2p_twoshot_kernel(T* __restrict__ x, long long n, PeerPtrs P, int rank,
                                                             int world, unsigned epoch, long long cap_elems,
                                                             long long S, long long C, int* status,
-                                                            long long timeout) {
+                                                            int* host_status, long long timeout) {
   const int b = blockIdx.x;
   const long long nu = (n + Unit<T>::K - 1) / Unit<T>::K;
   const long long poff = (long long)(epoch & 1u) * 2 * cap_elems;
@@ -169,8 +200,8 @@ __global__ __launch_bounds__(P2P_T) void p2p_twoshot_kernel(T* __restrict__ x, l
     hi = hi < nu ? hi : nu;
     for (long long u = lo + threadIdx.x; u < hi; u += P2P_T) store_full(mine, u, load_unit(x, u, n));
   }
-  const bool skip = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  block_exchange(P, rank, world, b, 2u * epoch - 1u, status, timeout, skip);
+  const bool failed = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  block_exchange(P, rank, world, b, 2u * epoch - 1u, status, host_status, timeout, failed);
   {
     const long long lo = rank * S + (long long)b * C;
     long long hi = lo + C < (rank + 1) * S ? lo + C : (rank + 1) * S;
@@ -183,7 +214,9 @@ __global__ __launch_bounds__(P2P_T) void p2p_twoshot_kernel(T* __restrict__ x, l
       store_unit(x, u, n, acc);
     }
   }
-  block_exchange(P, rank, world, b, 2u * epoch, status, timeout, skip);
+  // a wait of phase A that failed poisons phase B's flags too
+  block_exchange(P, rank, world, b, 2u * epoch, status, host_status, timeout,
+                 failed || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0);
   for (int s = 0; s < world; ++s) {
     if (s == rank) continue;
     const long long lo = s * S + (long long)b * C;
@@ -209,12 +242,12 @@ void launch(void* x, long long n, const avk::P2PView& v, unsigned epoch, int two
     int B = (int)std::min<long long>(avk::P2P_MAX_BLOCKS, std::max<long long>(1, (S + 4 * P2P_T - 1) / (4 * P2P_T)));
     const long long C = (S + B - 1) / B;
     hipLaunchKernelGGL(p2p_twoshot_kernel<T>, dim3(B), dim3(P2P_T), 0, st, reinterpret_cast<T*>(x), n, P, v.rank,
-                       v.world, epoch, cap_elems, S, C, v.status, timeout);
+                       v.world, epoch, cap_elems, S, C, v.status, v.host_status, timeout);
   } else {
     int B = (int)std::min<long long>(avk::P2P_MAX_BLOCKS, std::max<long long>(1, (nu + 4 * P2P_T - 1) / (4 * P2P_T)));
     const long long per = (nu + B - 1) / B;
     hipLaunchKernelGGL(p2p_oneshot_kernel<T>, dim3(B), dim3(P2P_T), 0, st, reinterpret_cast<T*>(x), n, P, v.rank,
-                       v.world, epoch, cap_elems, per, v.status, timeout);
+                       v.world, epoch, cap_elems, per, v.status, v.host_status, timeout);
   }
   AV_HIP_CHECK(hipGetLastError());
 }
@@ -227,7 +260,8 @@ void p2p_all_reduce(void* x, long long n, int dtype, const P2PView& v, unsigned 
                     long long timeout_ticks, hipStream_t st) {
   if (v.world < 1 || v.world > P2P_MAX_RANKS || v.rank < 0 || v.rank >= v.world)
     throw std::invalid_argument("p2p_all_reduce: bad rank / world");
-  if (epoch == 0 || epoch > 0x7FFFFFFFu) throw std::invalid_argument("p2p_all_reduce: epoch out of range");
+  if (epoch == 0 || epoch > P2P_MAX_EPOCH) throw std::invalid_argument("p2p_all_reduce: epoch out of range");
+  if (v.status == nullptr || v.host_status == nullptr) throw std::invalid_argument("p2p_all_reduce: no status words");
   if (n <= 0) return;
   switch (dtype) {
     case P2P_F32: launch<float>(x, n, v, epoch, two_shot, timeout_ticks, st); break;
@@ -236,6 +270,18 @@ void p2p_all_reduce(void* x, long long n, int dtype, const P2PView& v, unsigned 
     case P2P_I64: launch<long long>(x, n, v, epoch, two_shot, timeout_ticks, st); break;
     default: throw std::invalid_argument("p2p_all_reduce: unsupported dtype");
   }
+}
+
+void p2p_poison(const P2PView& v, hipStream_t st) {
+  if (v.world < 1 || v.world > P2P_MAX_RANKS || v.rank < 0 || v.rank >= v.world)
+    throw std::invalid_argument("p2p_poison: bad rank / world");
+  PeerPtrs P{};
+  for (int k = 0; k < v.world; ++k) {
+    P.data[k] = reinterpret_cast<char*>(v.data[k]);
+    P.flags[k] = v.flags[k];
+  }
+  hipLaunchKernelGGL(p2p_poison_kernel, dim3(1), dim3(P2P_T), 0, st, P, v.rank, v.world);
+  AV_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace avk

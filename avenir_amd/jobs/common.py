@@ -244,6 +244,12 @@ class JobContext:
         return self.comm.rank == 0
 
     # -- output -------------------------------------------------------------------------------
+    def check(self) -> None:
+        """Output gate: raise P2PError if a peer-mapped sum of this rank failed (local; waits for
+        the last one), so no output is ever written from a failed collective.  Every emit method
+        calls it; jobs that write files themselves call it first."""
+        self.comm.check()
+
     def _target(self, out: str | None = None) -> tuple[Path, bool]:
         p = Path(out or self.args.output)
         is_dir = p.is_dir() or (p.suffix == "" and not p.exists())
@@ -251,6 +257,7 @@ class JobContext:
 
     def emit(self, lines: list[str], out: str | None = None) -> Path | None:
         """Map-side output: per-rank part file into a directory, or rank-ordered single file."""
+        self.check()
         p, is_dir = self._target(out)
         if is_dir:
             p.mkdir(parents=True, exist_ok=True)
@@ -266,6 +273,7 @@ class JobContext:
     def emit_text(self, text: bytes, out: str | None = None) -> Path | None:
         """Map-side output of pre-formatted text (data/records.format_lines): this rank's part file
         into a directory, or the rank-ordered concatenation written by rank 0."""
+        self.check()
         p, is_dir = self._target(out)
         if is_dir:
             p.mkdir(parents=True, exist_ok=True)
@@ -284,6 +292,7 @@ class JobContext:
         """Map-side output of ``data/records.format_lines`` columns: this rank's part file into a
         directory (or the whole file when not distributed) written straight from the native
         formatter's threads; a single-file output of several ranks is gathered to rank 0."""
+        self.check()
         from ..data.records import format_lines
         p, is_dir = self._target(out)
         if is_dir or not self.comm.is_distributed:
@@ -298,6 +307,7 @@ class JobContext:
 
     def emit_root_columns(self, cols: list, n: int, out: str | None = None, name: str = "part-00000") -> Path | None:
         """Reduce-side output of ``format_lines`` columns: rank 0 writes them."""
+        self.check()
         from ..data.records import format_lines
         if not self.is_root:
             return None
@@ -311,6 +321,7 @@ class JobContext:
 
     def emit_root_text(self, text: bytes, out: str | None = None, name: str = "part-00000") -> Path | None:
         """Reduce-side output of pre-formatted text: rank 0 writes it."""
+        self.check()
         if not self.is_root:
             return None
         p, is_dir = self._target(out)
@@ -323,6 +334,7 @@ class JobContext:
 
     def emit_root(self, lines: list[str], out: str | None = None, name: str = "part-00000") -> Path | None:
         """Reduce-side output: rank 0 writes the (already reduced) result."""
+        self.check()
         if not self.is_root:
             return None
         p, is_dir = self._target(out)
@@ -333,6 +345,7 @@ class JobContext:
         return p
 
     def emit_json(self, obj, out: str | None = None) -> None:
+        self.check()
         if self.is_root:
             p = Path(out or self.args.output)
             p.parent.mkdir(parents=True, exist_ok=True)

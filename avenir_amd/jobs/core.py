@@ -137,6 +137,7 @@ def dec_tree(args):
     p.stopping, p.max_depth = "maxDepth", level
     tree = DecisionTreeBuilder(t.schema, p, comm=ctx.comm).fit(t)
     js = tree.to_decision_paths(int(n))
+    ctx.check()
     if ctx.is_root:
         Path(out_path).parent.mkdir(parents=True, exist_ok=True)
         Path(out_path).write_text(json.dumps(js, indent=1))
@@ -162,6 +163,7 @@ def rafo(args):
     p.sub_sampling = ctx.get_str("sub.sampling.strategy", "withReplace")
     rf = RandomForest(t.schema, ctx.get_int("num.trees", 10), p, ctx.get_str("max.features", "sqrt")).fit(t)
     if ctx.is_root:
+        ctx.check()
         out = Path(args.output)
         out.mkdir(parents=True, exist_ok=True)
         for i, tr in enumerate(rf.trees):

@@ -745,6 +745,7 @@ def loo_encoding(args):
             cnt.index_add_(0, kk, torch.ones_like(yv))
             sm.index_add_(0, kk, yv)
         ctx.all_reduce(cnt, sm)
+        ctx.check()
         if stat_path and ctx.is_root:
             from pathlib import Path
             Path(stat_path).parent.mkdir(parents=True, exist_ok=True)
@@ -807,6 +808,7 @@ def _loo_native(ctx, rec, cat, cls_ord, pos, reg, sd, prec, train, stat_path):
             cnt.index_add_(0, flat, torch.ones(flat.numel(), dtype=torch.float64, device=dev))
             sm.index_add_(0, flat, yv.view(-1, 1).expand(n, F).reshape(-1))
         ctx.all_reduce(cnt, sm)
+        ctx.check()
         if stat_path and ctx.is_root:
             from pathlib import Path
             ch, sh = cnt.view(F, V).cpu(), sm.view(F, V).cpu()
@@ -954,6 +956,7 @@ def incremental_pca(args):
     states = ipca.update(streams)
     lines = [l for k in keys for l in states[k].serialize(d, prec)]
     lines = ctx.gather_lines(lines)
+    ctx.check()
     if sp and ctx.is_root:
         Path(sp).parent.mkdir(parents=True, exist_ok=True)
         Path(sp).write_text("\n".join(lines) + "\n")

@@ -698,6 +698,7 @@ def _report_error_rate(ctx, err: torch.Tensor) -> None:
     ctx.all_reduce(err)
     rate = float(err[0]) / max(float(err[1]), 1)
     ep = ctx.cfg.values.get("map.error.rate.file.path")
+    ctx.check()
     if ep and ctx.is_root:
         Path(ep).parent.mkdir(parents=True, exist_ok=True)
         Path(ep).write_text(f"errorRate={rate:.6f}\n")
@@ -790,6 +791,7 @@ def data_partitioner(args):
     for r, s in zip(rows, seg):
         by[s].append(d.join(r))
     base = Path(args.output) / f"split={attr}"
+    ctx.check()
     for s, ls in sorted(by.items()):
         p = base / f"segment={s}"
         p.mkdir(parents=True, exist_ok=True)

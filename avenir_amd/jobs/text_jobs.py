@@ -192,6 +192,7 @@ def term_distr(args):
     if mode == "buildBaseTf":
         if not args.model:
             raise SystemExit("buildBaseTf needs --model <file>")
+        ctx.check()
         if ctx.is_root:
             tf.save(args.model)
         ctx.report({"terms": len(tf.counts), "docs": tf.n_docs})
@@ -269,6 +270,7 @@ def text_encoder(args):
                                        delimiter=",", ndmin=2)).float()
     if mode == "train":
         ae.fit(data, seed=args.seed)
+        ctx.check()
         if mpath is not None and ctx.is_root:
             mpath.parent.mkdir(parents=True, exist_ok=True)
             ae.save(mpath)
@@ -349,6 +351,7 @@ def word_to_vec(args):
                      epochs=ctx.get_int("train.epochs", 5), seed=args.seed, device=ctx.device).fit(_clean(texts))
         if not args.model:
             raise SystemExit("train needs --model <file>")
+        ctx.check()
         if ctx.is_root:
             m.save(args.model)
         ctx.report({"vocab": len(m.vocab.index), "dim": m.dim})

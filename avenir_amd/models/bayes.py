@@ -76,6 +76,7 @@ class NaiveBayes:
         self._tables: dict | None = None
         self._ready = None            # event after the side-stream all-reduce / finalize (GPU, >1 rank)
         self._side = None
+        self._comm = None             # the communicator of a side-stream (unchecked) reduce
 
     # The model tensors are read through properties: when the all-reduce of a multi-GPU fit runs on
     # the side stream, the first read on another stream waits for it (see _reduce_on_side_stream).
@@ -113,6 +114,9 @@ class NaiveBayes:
         if ev is None:
             return
         self._ready = None
+        comm = self.__dict__.get("_comm")
+        if comm is not None:
+            comm.check(block=False)       # raise now if a finished p2p sum of this fit failed
         cur = torch.cuda.current_stream(self._both.device)
         cur.wait_event(ev)
         ts = [self._both, self._moments] + (list(self._tables.values()) if self._tables else [])
@@ -130,9 +134,13 @@ class NaiveBayes:
         side = _side_stream(both.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            comm.all_reduce(both)
+            # unchecked (asynchronous) on the peer-mapped path: a failed wait surfaces at the
+            # communicator's next collective, at the first host read of the model, or at the output
+            # gate of a job (Comm.check)
+            comm.all_reduce(both, checked=False)
             if moments.numel():
-                comm.all_reduce(moments)
+                comm.all_reduce(moments, checked=False)
+        self._comm = comm
         both.record_stream(side)
         if moments.numel():
             moments.record_stream(side)

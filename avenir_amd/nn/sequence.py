@@ -23,6 +23,7 @@ import torch
 
 from ..ops.rnn import FusedLSTM
 from ..parallel.comm import get_comm
+from ..utils.params import bump_param_epoch
 from .common import (GraphedStep, _cfg, create_activation, create_loss, load_checkpoint, optimizer_from_config, pick_device,
                      save_checkpoint, scale_data)
 
@@ -146,9 +147,12 @@ class LstmNetwork(torch.nn.Module):
         bs = min(self.batch_size, n)
         nb = max(n // bs, 1)
         if dp is not None:
-            for p in self.parameters():
-                dp.broadcast(p.data, 0)
-            t = torch.tensor([nb], dtype=torch.long)
+            with torch.no_grad():
+                for p in self.parameters():
+                    dp.broadcast(p, 0)
+            bump_param_epoch()          # the packed-weight caches must not serve pre-broadcast weights
+            # on the communicator's device: an RCCL group takes device tensors only
+            t = torch.tensor([nb], dtype=torch.long, device=self.device)
             dp.all_reduce(t, "min")
             nb = int(t)
         g = torch.Generator().manual_seed(seed)

@@ -31,9 +31,19 @@ Deterministic small-message all-reduce, two variants, both bit-identical on ever
 * ``algo="oneshot"``: an all-gather of every rank's buffer (RCCL's collective) followed by a local
   sum in rank order; any reduction op, any device.
 
-``AVMI_SMALL_ALLREDUCE=p2p|oneshot`` routes sum reductions up to ``AVMI_ONESHOT_MAX_BYTES``
-(default 64 KiB) to one of them; ``bench.py`` reports both latencies next to RCCL's on multi-GPU
-runs.
+Selection of sum reductions up to ``AVMI_ONESHOT_MAX_BYTES`` (default 64 KiB) when the caller names
+no algorithm: ``AVMI_SMALL_ALLREDUCE`` = ``auto`` (default) | ``p2p`` | ``oneshot`` | ``rccl``.
+``auto``: at the first such all-reduce of a device tensor on a multi-rank communicator, every rank
+runs the same probe (:meth:`Comm._auto_small_allreduce`): build the peer-mapped state (agreed over
+ranks; unavailable -> the library collective), check it exact on integer sums, time it against
+the library collective at the message's size, and take it only if every rank found it exact and
+it is faster (max over ranks).  The choice is cached per communicator.
+
+Failure reporting of the p2p path is loud (``parallel/p2p.py``): a checked call raises
+``P2PError`` on the rank whose wait failed and on the late peer; unchecked calls (the NB
+side-stream overlap) are checked at the next collective of this communicator (non-blocking) and
+by :meth:`Comm.check` — which every job output method calls before writing
+(``jobs/common.py``) — so no job writes output computed from a failed sum.
 """
 from __future__ import annotations
 
@@ -50,8 +60,9 @@ from ..utils import logging as alog
 from ..utils.tracing import traced
 
 _COMM: "Comm | None" = None
-_ONESHOT_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "") == "oneshot"
-_P2P_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "") == "p2p"
+_SMALL_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "auto").strip().lower() or "auto"
+if _SMALL_ENV not in ("auto", "p2p", "oneshot", "rccl"):
+    raise ValueError(f"AVMI_SMALL_ALLREDUCE={_SMALL_ENV!r}: expected auto, p2p, oneshot or rccl")
 _ONESHOT_MAX_BYTES = int(os.environ.get("AVMI_ONESHOT_MAX_BYTES", str(64 << 10)))
 
 
@@ -95,11 +106,15 @@ class Comm:
             self.rank = dist.get_rank()
             self.pg_backend = dist.get_backend()
         self.stats = {"calls": 0, "bytes": 0, "seconds": 0.0}
-        self._p2p = None        # parallel/p2p.P2PAllReduce, created by the first p2p all-reduce
+        # parallel/p2p.P2PAllReduce, created by the first p2p all-reduce; False once its agreed
+        # construction failed (no peer mapping on this node): the library collective from then on
+        self._p2p = None
+        self._p2p_unchecked = False     # an unchecked p2p call may not have been checked yet
         # algorithm of sum all-reduces up to _ONESHOT_MAX_BYTES when the caller names none:
-        # None (library collective), "oneshot" or "p2p" (env AVMI_SMALL_ALLREDUCE, or set by a tuner
-        # such as bench.py's, which times the candidates on the job's own GPUs)
-        self.small_allreduce = "p2p" if _P2P_ENV else ("oneshot" if _ONESHOT_ENV else None)
+        # None (library collective), "oneshot", "p2p", or "auto" (probe at the first one: see
+        # _auto_small_allreduce); env AVMI_SMALL_ALLREDUCE, or set by a tuner such as bench.py's
+        self.small_allreduce = {"rccl": None}.get(_SMALL_ENV, _SMALL_ENV)
+        self.small_allreduce_probe: dict | None = None
 
     @classmethod
     def emulated_rccl(cls, device: str | None = None, **kw) -> "Comm":
@@ -133,18 +148,26 @@ class Comm:
 
     # ------------------------------------------------------------------------------------------
     @traced("comm.all_reduce", nbytes=lambda self, t, *a, **k: t.numel() * t.element_size(), device=lambda self, t, *a, **k: t.device)
-    def all_reduce(self, t: torch.Tensor, op: str = "sum", algo: str | None = None) -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", algo: str | None = None,
+                   checked: bool = True) -> torch.Tensor:
         """In-place all-reduce (sum|max|min|prod); returns ``t``.  ``algo``: None (library
-        collective, or the env-selected small-message path), "ring" (library), "oneshot"
-        (all-gather + rank-ordered local reduction), "p2p" (hand-written peer-mapped kernel, sums of
-        device tensors; anything else falls back to the library collective)."""
+        collective, or the selected small-message path), "ring" (library), "oneshot" (all-gather +
+        rank-ordered local reduction), "p2p" (hand-written peer-mapped kernel, sums of device
+        tensors; anything else falls back to the library collective).  ``checked=False`` lets a
+        p2p sum stay asynchronous (see the module docstring)."""
         if not self.is_distributed:
             return t
+        self._guard()
         small = t.numel() * t.element_size() <= _ONESHOT_MAX_BYTES
         if algo is None and op == "sum" and small and self.small_allreduce:
-            algo = self.small_allreduce
+            if self.small_allreduce == "auto":
+                if self._auto_eligible(t):
+                    self._auto_small_allreduce(t)
+                    algo = self.small_allreduce
+            else:
+                algo = self.small_allreduce
         if algo == "p2p":
-            if op == "sum" and self._all_reduce_p2p(t) is not None:
+            if op == "sum" and self._all_reduce_p2p(t, checked) is not None:
                 return t
             algo = None                       # not a device sum the kernel takes: the library collective
         if algo == "oneshot":
@@ -159,29 +182,126 @@ class Comm:
         self._account(t, t0)
         return t
 
+    # ---- peer-mapped path: construction, selection, failure gate ------------------------------
     def p2p(self):
         """The peer-mapped all-reduce state (``parallel/p2p.py``), created on first use — a
-        collective: every rank reaches its first p2p all-reduce together."""
+        collective: every rank reaches its first p2p all-reduce together.  None when it is
+        unavailable on this node (the agreed construction failed on some rank: every rank gets None
+        together, and remembers it, so later calls take the library collective at once)."""
         if self._p2p is None:
-            from .p2p import P2PAllReduce
-            self._p2p = P2PAllReduce(self, self.device)
-        return self._p2p
+            from .p2p import P2PAllReduce, P2PError
+            try:
+                self._p2p = P2PAllReduce(self, self.device)
+            except P2PError as e:
+                alog.get_logger("comm").warning("peer-mapped all-reduce unavailable: %s", e)
+                self._p2p = False
+                if self.small_allreduce in ("p2p", "auto"):
+                    self.small_allreduce = None
+        return self._p2p or None
 
-    def _all_reduce_p2p(self, t: torch.Tensor) -> torch.Tensor | None:
+    def _auto_eligible(self, t: torch.Tensor) -> bool:
+        from .p2p import P2PAllReduce
+        return self.device.type == "cuda" and P2PAllReduce.supports(t) and t.device == self.device
+
+    def _auto_small_allreduce(self, like: torch.Tensor) -> str | None:
+        """Collective, once per communicator: pick the small-sum algorithm (module docstring).
+        Every rank reaches it at the same all-reduce (same size, same dtype class by the collective
+        contract) and takes the same branch: construction and the verdict are both agreed."""
+        info: dict = {"bytes": like.numel() * like.element_size()}
+        choice = None
+        p = self.p2p()
+        if p is None:
+            info["p2p"] = "unavailable"
+        else:
+            exact, t_p2p, t_lib = self._probe_p2p(p, like)
+            info.update(exact_here=exact, p2p_us_here=t_p2p * 1e6, lib_us_here=t_lib * 1e6)
+            use, t_p2p, t_lib = self._agree_small_choice(exact, t_p2p, t_lib)
+            info.update(p2p_us=t_p2p * 1e6, lib_us=t_lib * 1e6)
+            choice = "p2p" if use else None
+        info["chosen"] = choice or "library"
+        self.small_allreduce = choice
+        self.small_allreduce_probe = info
+        alog.get_logger("comm").info("small all-reduce selection: %s", info)
+        return choice
+
+    def _probe_p2p(self, p, like: torch.Tensor, rounds: int = 8, iters: int = 30) -> tuple[bool, float, float]:
+        """This rank's measurements: the kernel exact on integer sums of ``like``'s size (checked
+        calls: a failed wait raises P2PError on the ranks involved), then the mean time of the
+        kernel and of the library collective at that size."""
+        W = self.world
+        n = max(1, like.numel())
+        xi = torch.empty(n, dtype=torch.int64, device=like.device)
+        exact = True
+        for i in range(rounds):
+            xi.fill_(self.rank + 1 + i)
+            p.all_reduce(xi)
+            exact &= bool((xi == W * (W + 1) // 2 + W * i).all().item())
+        x = torch.ones_like(like).contiguous()
+
+        def timed(fn) -> float:
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize(like.device)
+            self.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize(like.device)
+            return (time.perf_counter() - t0) / iters
+
+        t_lib = timed(lambda: self.all_reduce(x, algo="ring"))
+        t_p2p = timed(lambda: p.all_reduce(x, checked=False))
+        p.check(block=True)
+        return exact, t_p2p, t_lib
+
+    def _agree_small_choice(self, exact: bool, t_p2p: float, t_lib: float) -> tuple[bool, float, float]:
+        """One max all-reduce of (not exact, p2p time, library time) over the ranks: the kernel is
+        chosen only if it was exact on EVERY rank and faster by the slowest rank's clock."""
+        dev = self.device if self.pg_backend == "nccl" else "cpu"
+        f = torch.tensor([0.0 if exact else 1.0, float(t_p2p), float(t_lib)], dtype=torch.float64, device=dev)
+        self.all_reduce(f, "max", algo="ring")
+        bad, tp, tl = f.tolist()
+        return (bad == 0.0 and tp < tl), tp, tl
+
+    def _all_reduce_p2p(self, t: torch.Tensor, checked: bool = True) -> torch.Tensor | None:
         """The hand-written peer-mapped sum (comm.hip); None when ``t`` does not qualify (host
-        tensor, unsupported dtype, larger than the staging capacity) — the caller then takes the
-        library collective.  The decision depends only on shape / dtype / device type, which every
-        rank shares, so all ranks take the same path."""
+        tensor, unsupported dtype, larger than the staging capacity, peer mapping unavailable) —
+        the caller then takes the library collective.  The decision depends only on shape / dtype /
+        device type and agreed state, which every rank shares, so all ranks take the same path."""
         from .p2p import P2PAllReduce
         if not P2PAllReduce.supports(t) or self.device.type != "cuda":
             return None
         p = self.p2p()
-        if t.numel() * t.element_size() > p.cap_bytes:
+        if p is None or t.numel() * t.element_size() > p.cap_bytes:
             return None
         t0 = time.perf_counter()
-        p.all_reduce(t)
+        _maybe_delay_p2p(self.rank)
+        p.all_reduce(t, checked=checked)
+        if not checked:
+            self._p2p_unchecked = True
         self._account(t, t0)
         return t
+
+    @property
+    def p2p_calls(self) -> int:
+        """Number of peer-mapped all-reduce kernels this communicator launched."""
+        return sum(self._p2p.calls.values()) if self._p2p else 0
+
+    def _guard(self) -> None:
+        """Entry of every collective: raise P2PError if an unchecked p2p call of this rank has
+        failed (non-blocking: only kernels that already finished are seen)."""
+        if self._p2p_unchecked and self._p2p:
+            self._p2p.check(block=False)
+
+    def check(self, block: bool = True) -> None:
+        """Raise P2PError if any p2p all-reduce of this rank failed.  ``block`` waits for the last
+        one first.  Local (no collective): the job output methods call it before writing, so a
+        rank never writes output computed from a failed sum; the peers of a failed rank fail on
+        their own (poisoned flags) or at their next collective."""
+        if self._p2p:
+            self._p2p.check(block=block)
+            if block:
+                self._p2p_unchecked = False
 
     def _all_reduce_oneshot(self, t: torch.Tensor, op: str) -> torch.Tensor:
         """One all-gather of every rank's buffer, then the reduction over ranks in rank order."""
@@ -224,6 +344,7 @@ class Comm:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if not self.is_distributed:
             return t
+        self._guard()
         t0 = time.perf_counter()
         x, moved = self._prep(t)
         dist.broadcast(x, src)
@@ -235,6 +356,7 @@ class Comm:
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
         if not self.is_distributed:
             return obj
+        self._guard()
         box = [obj]
         dist.broadcast_object_list(box, src)
         return box[0]
@@ -242,6 +364,7 @@ class Comm:
     def all_gather_object(self, obj: Any) -> list[Any]:
         if not self.is_distributed:
             return [obj]
+        self._guard()
         out: list[Any] = [None] * self.world
         dist.all_gather_object(out, obj)
         return out
@@ -251,6 +374,7 @@ class Comm:
         """Equal-shape all-gather -> [world, *t.shape]."""
         if not self.is_distributed:
             return t.unsqueeze(0)
+        self._guard()
         x, moved = self._prep(t.contiguous())
         flat = torch.empty((self.world * x.numel(),), dtype=x.dtype, device=x.device)
         dist.all_gather_into_tensor(flat, x.reshape(-1))
@@ -379,6 +503,7 @@ class Comm:
 
     def barrier(self) -> None:
         if self.is_distributed:
+            self._guard()
             if self.pg_backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
@@ -392,9 +517,10 @@ class Comm:
         return float(t.item())
 
     def shutdown(self) -> None:
-        if self._p2p is not None:
+        if self._p2p:
+            self.check()                      # a failed sum surfaces before a clean exit
             self._p2p.close()
-            self._p2p = None
+        self._p2p = None
         if self._owns_pg and dist.is_initialized():
             dist.destroy_process_group()
             self._owns_pg = False
@@ -430,6 +556,15 @@ def timed_collective(name: str, warn_s: float = 30.0):
     dt = time.perf_counter() - t0
     if dt > warn_s:
         alog.get_logger("comm").warning("collective %s took %.1fs", name, dt)
+
+
+def _maybe_delay_p2p(rank: int) -> None:
+    """Fault injection for the peer-mapped path (tests): ``AVMI_FAULT_P2P_SLEEP_RANK`` sleeps
+    ``AVMI_FAULT_P2P_SLEEP_S`` seconds before each of its p2p launches — a rank late past the
+    peers' wait bound, as a slow shard read would make it."""
+    r = os.environ.get("AVMI_FAULT_P2P_SLEEP_RANK")
+    if r is not None and int(r) == rank:
+        time.sleep(float(os.environ.get("AVMI_FAULT_P2P_SLEEP_S", "0")))
 
 
 def maybe_inject_fault(iteration: int, rank: int | None = None) -> None:

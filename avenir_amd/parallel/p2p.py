@@ -15,8 +15,18 @@ table is summed by ONE hand-written kernel per rank that reads the peers' staged
   result stagings: 2 (W-1)/W of the message read per rank);
 * the sum is taken in rank order, so the result is bit-identical on every rank and every run —
   the same contract as ``Comm._all_reduce_oneshot`` but without the all-gather round;
-* waits are bounded in the kernel (``timeout_s``); a timed-out wait sets a status word that
-  :meth:`check` turns into an exception instead of a hang.
+* waits are bounded in the kernel (``timeout_s``: ``AVMI_P2P_TIMEOUT_S``, else the communicator's
+  process-group timeout, 600 s by default — ranks minutes apart in host work are ordinary).  A
+  timed-out wait records status 1 in a pinned host-mapped word and POISONS the flag it raised for
+  the late peer, whose kernel then records status 2 when it arrives; a rank whose status is set
+  raises poisoned flags on every later call.  Every call is CHECKED by default: the host waits for
+  the kernel's event and raises :class:`P2PError` (after poisoning every peer's flags) when the
+  status is set — a garbage sum is never returned.  ``checked=False`` (the NB side-stream overlap)
+  leaves the check to the communicator's next collective or output gate (``Comm.check``).
+
+Staging memory is uncached when any peer sits on another device (``AVMI_P2P_UNCACHED`` overrides):
+peers read it over xGMI while the owner's kernel is still running, so no line may linger in an
+L2; ranks that share one device keep the cached default (same L2, release / acquire fences).
 
 Teardown is collective too: :meth:`close` unmaps the peers' regions, barriers, then frees the
 rank's own region (a peer must never read freed memory).
@@ -32,13 +42,30 @@ from .. import _native
 _DTYPES = (torch.float32, torch.float64, torch.int32, torch.int64)
 
 
+_MAX_EPOCH = 0x3FFFFFFF   # avk::P2P_MAX_EPOCH: 2 * epoch stays below the poison bit
+
+
 class P2PError(RuntimeError):
     pass
 
 
+def _device_identity(device: torch.device) -> str:
+    """Host name + device UUID (or PCI bus id): equal for ranks sharing one GPU."""
+    import socket
+    try:
+        props = torch.cuda.get_device_properties(device)
+        uid = getattr(props, "uuid", None)
+        if uid is None:
+            uid = f"{getattr(props, 'pci_bus_id', '?')}:{getattr(props, 'pci_device_id', '?')}"
+    except Exception:  # noqa: BLE001 - no device runtime (CPU tests): the ordinal stands in
+        uid = str(device)
+    return f"{socket.gethostname()}/{uid}"
+
+
 def _agree(comm, ok: bool) -> bool:
     """All ranks' ``ok`` AND-ed (one min all-reduce through the library collective)."""
-    f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm.device)
+    f = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                     device=comm.device if getattr(comm, "pg_backend", "nccl") == "nccl" else "cpu")
     comm.all_reduce(f, "min", algo="ring")
     return bool(f.item())
 
@@ -55,7 +82,16 @@ class P2PAllReduce:
         self.comm = comm
         self.device = device
         self.world, self.rank = comm.world, comm.rank
-        uncached = os.environ.get("AVMI_P2P_UNCACHED", "0") == "1"
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("AVMI_P2P_TIMEOUT_S", getattr(comm, "timeout_s", 600.0)))
+        self.timeout_s = float(timeout_s)
+        env_unc = os.environ.get("AVMI_P2P_UNCACHED")
+        if env_unc is not None:
+            uncached = env_unc == "1"
+        else:                      # peers on other devices read our staging mid-kernel over xGMI
+            ids = comm.all_gather_object(_device_identity(device))
+            uncached = any(i != ids[0] for i in ids)
+        self.uncached = uncached
         # every step that can fail on ONE rank (allocation, export, mapping a peer) is followed by
         # an agreement all-reduce, so all ranks raise together and the collective sequence of the
         # caller stays aligned (a rank leaving early would pair its next collective with a peer's
@@ -64,7 +100,7 @@ class P2PAllReduce:
         try:
             self._h = _native.C().P2PComm(device.index, cap, uncached)
             self.cap_bytes = int(self._h.cap_bytes)
-            self._h.set_timeout(float(timeout_s or os.environ.get("AVMI_P2P_TIMEOUT_S", "10")))
+            self._h.set_timeout(self.timeout_s)
             mine = bytes(self._h.handles())
         except Exception as e:     # noqa: BLE001 - reported through the agreement below
             err, mine = e, b""
@@ -90,20 +126,27 @@ class P2PAllReduce:
                            f"({err!r} here)" if err is not None else
                            f"rank {self.rank}: peer-mapped all-reduce unavailable on another rank")
         self.epoch = 0
+        self.failed = 0
         self.calls = {"oneshot": 0, "twoshot": 0}
 
     @staticmethod
     def supports(t: torch.Tensor) -> bool:
         return t.is_cuda and t.dtype in _DTYPES
 
-    def all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, algo: str | None = None, checked: bool = True) -> torch.Tensor:
         """In-place sum of ``t`` over all ranks (stream-ordered on the current stream); returns ``t``.
-        ``algo``: None (by size), "oneshot" or "twoshot"."""
+        ``algo``: None (by size), "oneshot" or "twoshot".  ``checked``: wait for the kernel and
+        raise :class:`P2PError` if a wait failed (default); otherwise the caller checks later."""
+        if self._h is None:
+            raise P2PError(f"rank {self.rank}: the peer-mapped all-reduce is closed")
+        self.check(block=False)                 # a failure seen since the last call: never launch on it
         if t.numel() == 0:
             return t
         nbytes = t.numel() * t.element_size()
         if nbytes > self.cap_bytes:
             raise ValueError(f"p2p all-reduce: {nbytes} bytes exceed the staging capacity {self.cap_bytes}")
+        if self.epoch >= _MAX_EPOCH:
+            raise P2PError(f"rank {self.rank}: p2p epoch space exhausted; rebuild the communicator")
         two = (algo == "twoshot") if algo is not None else nbytes > self.oneshot_max
         x = t
         if not t.is_contiguous() or t.data_ptr() % 16 != 0:
@@ -113,24 +156,44 @@ class P2PAllReduce:
         self.calls["twoshot" if two else "oneshot"] += 1
         if x is not t:
             t.copy_(x)
+        if checked:
+            self.check(block=True)
         return t
 
-    def ok(self) -> bool:
-        """True when no wait of this rank's kernels timed out (synchronises the device; local)."""
-        return int(self._h.status()) == 0
+    def status(self, block: bool = False) -> int:
+        """0 healthy, 1 a wait of this rank timed out, 2 a peer reported a failure.  ``block``
+        waits for the last call's kernel first; otherwise only finished kernels are seen."""
+        if self._h is None:
+            return 0
+        if block:
+            self._h.sync_last()
+        return int(self._h.host_status())
 
-    def check(self) -> None:
-        """Raise if any wait of this rank's kernels timed out (synchronises the device)."""
-        if int(self._h.status()) != 0:
-            raise P2PError(f"rank {self.rank}: a peer-mapped all-reduce wait timed out "
-                           f"(epoch <= {self.epoch}); the peers are out of step or gone")
+    def ok(self) -> bool:
+        """True when no wait of this rank's kernels failed (waits for the last call; local)."""
+        return self.status(block=True) == 0
+
+    def check(self, block: bool = True) -> None:
+        """Raise :class:`P2PError` if a wait of this rank's kernels failed, after poisoning every
+        peer's flags so their next wait on this rank fails at once instead of timing out."""
+        st = self.status(block)
+        if st != 0:
+            self.failed = st
+            try:
+                self._h.poison()
+            except Exception:  # noqa: BLE001 - the channel is already broken; the raise matters
+                pass
+            what = "a wait timed out here" if st == 1 else "a peer reported a failure"
+            raise P2PError(f"rank {self.rank}: peer-mapped all-reduce failed at epoch <= {self.epoch} "
+                           f"({what}); the ranks are out of step or a peer is gone")
 
     def close(self) -> None:
         """Collective: unmap peers, barrier, free this rank's region."""
         if self._h is None:
             return
         torch.cuda.synchronize(self.device)
-        self._h.close_peers()
+        self._h.close_peers()   # even after a failure: the barrier keeps every rank's region mapped
+                                # until no peer's kernel can still read it
         self.comm.barrier()
         self._h.release()
         self._h = None

@@ -22,6 +22,12 @@ def _bump(optimizer, args, kwargs) -> None:
 register_optimizer_step_post_hook(_bump)
 
 
+def bump_param_epoch() -> None:
+    """Invalidate every packed-parameter cache: for in-place writes that bypass autograd's
+    version counter (a broadcast into ``p.data``, a ``load_state_dict`` copy)."""
+    _EPOCH[0] += 1
+
+
 def param_epoch() -> int:
     """Number of optimizer steps taken in this process (any optimizer, any parameters)."""
     return _EPOCH[0]

@@ -81,10 +81,9 @@ def _allreduce_probe(comm, dev) -> list:
     # hand-written peer-mapped kernels (csrc/kernels/comm.hip): one-shot / two-shot over xGMI
     # (construction agrees over ranks and raises on all of them together; the kernels' waits are
     # bounded, so a rank out of step shows as a status word, and every rank reaches every collective)
-    try:
-        p = comm.p2p()
-    except Exception as e:          # the probe must never cost the measured headline
-        out.append({"algo": "p2p", "error": repr(e)})
+    p = comm.p2p()                  # collective; None on every rank together when unavailable
+    if p is None:
+        out.append({"algo": "p2p", "error": "peer-mapped all-reduce unavailable on this node"})
         return out
     for nbytes, iters in ((8 << 10, 100), (64 << 10, 100), (1 << 20, 50)):
         x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
@@ -114,6 +113,13 @@ def _pick_small_allreduce(comm, like: torch.Tensor, mode: str) -> dict:
     info = {"mode": mode, "bytes": like.numel() * like.element_size()}
     if mode == "rccl" or comm.world == 1 or like.device.type != "cuda":
         info["chosen"] = "rccl"
+        comm.small_allreduce = None
+        return info
+    if mode == "auto":
+        # the communicator's own default selection (Comm._auto_small_allreduce), made at the
+        # first count-table all-reduce of the sizing fit — the same probe every job runs
+        info.update(comm.small_allreduce_probe or {})
+        info["chosen"] = "p2p" if comm.small_allreduce == "p2p" else "rccl"
         return info
     W = comm.world
     x = torch.empty_like(like)
@@ -127,12 +133,10 @@ def _pick_small_allreduce(comm, like: torch.Tensor, mode: str) -> dict:
     # word, never hangs) or a collective that ALL ranks reach: a failure on one rank is carried by
     # the agreement all-reduces, never by an exception that would skip a collective on that rank.
     use = False
-    try:
-        p = comm.p2p()                                # collective; raises on every rank together
-    except Exception as e:      # no peer mapping on this node: the library collective
-        info["p2p_error"] = repr(e)
-        p = None
-    if p is not None:
+    p = comm.p2p()                                    # collective; None on every rank together
+    if p is None:
+        info["p2p_error"] = "peer-mapped all-reduce unavailable on this node"
+    else:
         ok = True
         for i in range(20):
             x.fill_(comm.rank + 1 + i)
@@ -262,8 +266,9 @@ def main() -> int:
                     help="device layout of the encoded records: one 16-bit word per record "
                          "(2 B/record) or one uint8 column per feature + label (6 B/record)")
     ap.add_argument("--small-allreduce", choices=["auto", "rccl", "p2p"], default="auto",
-                    help="algorithm of the count-table all-reduce on >1 GPU: auto = the faster of RCCL "
-                         "and the hand-written peer-mapped kernel, timed on the job's GPUs before the steps")
+                    help="algorithm of the count-table all-reduce on >1 GPU: auto = the communicator's "
+                         "default selection (the faster of RCCL and the hand-written peer-mapped "
+                         "kernel if it is exact, probed on the job's GPUs at the first such all-reduce)")
     ap.add_argument("--probe-allreduce", action="store_true",
                     help="run the all-reduce probe on any device (it runs by default on >1 GPU)")
     ap.add_argument("--ingest-rows", type=int, default=-1,
@@ -333,6 +338,7 @@ def main() -> int:
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    comm.check()                          # a failed peer-mapped sum in the timed steps raises here
     dt = comm.reduce_max_scalar(dt)
 
     # sanity: the model must have counted every record of every rank in the last step

@@ -193,3 +193,138 @@ def test_p2p_construction_failure_on_one_rank_raises_everywhere():
     every rank's region after a common barrier, and leaves the ranks' collectives in step."""
     out = run_world(_p2p_open_fails_on_one_rank, 2)
     assert out == [(3.0, True), (3.0, True)]
+
+
+# ---- round 6: the peer-mapped path as the safe default ------------------------------------------
+
+def _auto_choices(rank, world):
+    """The agreed verdict of the selection probe, with this rank's measurements injected."""
+    from avenir_amd.parallel import comm as C
+    c = C.get_comm()
+    like = torch.zeros(16, dtype=torch.int64)
+    c.p2p = lambda: object()                        # stands in for a constructed P2PAllReduce
+    out = []
+    for exact, tp, tl in ((rank != 1, 1e-6, 2e-6),                       # rank 1 not exact
+                          (True, 3e-6 if rank == 1 else 1e-6, 2e-6),      # slower on rank 1's clock
+                          (True, 1e-6, 2e-6)):                            # exact and faster everywhere
+        c._probe_p2p = lambda p, l, _r=(exact, tp, tl): _r
+        c.small_allreduce = "auto"
+        out.append(c._auto_small_allreduce(like))
+        out.append(c.small_allreduce_probe["chosen"])
+    return out
+
+
+def test_auto_selection_is_agreed_over_ranks():
+    """One rank that finds the kernel inexact (or slower) keeps EVERY rank on the library
+    collective; the kernel is taken only when all ranks found it exact and faster."""
+    for got in run_world(_auto_choices, 2):
+        assert got == [None, "library", None, "library", "p2p", "p2p"]
+
+
+def _p2p_unavailable(rank, world):
+    from avenir_amd import _native
+    from avenir_amd.parallel import comm as C
+
+    class _Lib:
+        P2PComm = _FakeHandle
+    _native.C = lambda: _Lib
+    c = C.get_comm()
+    c.device = torch.device("cuda", 0)              # as on a GPU node; nothing is launched
+    c.small_allreduce = "p2p"
+    first = c.p2p()                                 # agreed failure: None on every rank, no raise
+    n0 = c.stats["calls"]
+    second = c.p2p()                                # remembered: no second construction round
+    x = torch.tensor([float(rank + 1)])
+    c.all_reduce(x)                                 # the library collective
+    return first is None, second is None, c._p2p is False, c.small_allreduce, c.stats["calls"] - n0, float(x)
+
+
+def test_p2p_unavailable_degrades_to_library():
+    """a node without peer mapping degrades to the library collective (once, on every
+    rank together) instead of raising from every later all-reduce."""
+    for got in run_world(_p2p_unavailable, 2):
+        assert got == (True, True, True, None, 1, 3.0)
+
+
+def _default_path(rank, world):
+    """No algorithm named, no env: the first small device sum runs the probe; the kernel must win
+    over the gloo-carried library path here, and every later small sum takes it (counted)."""
+    from avenir_amd.parallel.comm import get_comm
+    comm = get_comm()
+    dev = comm.device
+    assert comm.small_allreduce == "auto"
+    res = []
+    for i in range(50):
+        x = torch.full((513,), rank + 1 + i, dtype=torch.int64, device=dev)
+        comm.all_reduce(x)
+        res.append(bool((x == world * (world + 1) // 2 + world * i).all().item()))
+    comm.check()
+    return all(res), comm.small_allreduce, comm.p2p_calls, comm.small_allreduce_probe
+
+
+@pytest.mark.gpu
+def test_default_small_allreduce_takes_p2p_gpu():
+    for ok, chosen, calls, probe in run_world(_default_path, 2, timeout=300, comm="gloo:cuda"):
+        assert ok and chosen == "p2p", probe
+        assert calls >= 50, calls
+
+
+def _run_rank_procs(args, world, env_extra, timeout=240):
+    import os
+    import subprocess
+    import sys
+    from _dist import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PYTHONPATH=root, **env_extra)
+        procs.append(subprocess.Popen([sys.executable, "-m", "avenir_amd"] + args, env=env, cwd=root,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    out = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, e = p.communicate()
+        out.append((p.returncode, o.decode(errors="replace"), e.decode(errors="replace")))
+    return out
+
+
+@pytest.mark.gpu
+def test_p2p_timeout_fails_the_job_on_every_rank(tmp_path):
+    """Fault injection: in a 2-rank bayesianDistribution job on one GPU, rank 1
+    reaches the count all-reduce 6 s late, past the 2 s wait bound.  Rank 0's wait times out
+    (status 1; it poisons the flag it raised for rank 1), rank 1's kernel then finds the poison
+    (status 2): BOTH ranks exit non-zero with P2PError, and no model file is written."""
+    from avenir_amd.data import synth
+    data, schema = tmp_path / "churn.csv", tmp_path / "churn.json"
+    synth.write_churn(data, 5001, seed=3, schema_path=schema)
+    model = tmp_path / "nb_model.txt"
+    res = _run_rank_procs(["bayesianDistribution", "-i", str(data), "-o", str(model), "--schema", str(schema),
+                           "--device", "cuda"], 2,
+                          {"AVENIR_COMM_BACKEND": "gloo", "AVMI_SMALL_ALLREDUCE": "p2p", "AVMI_P2P_TIMEOUT_S": "2",
+                           "AVMI_FAULT_P2P_SLEEP_RANK": "1", "AVMI_FAULT_P2P_SLEEP_S": "6"})
+    for rank, (rc, _o, err) in enumerate(res):
+        assert rc != 0, f"rank {rank} exited 0:\n{err[-3000:]}"
+        assert "P2PError" in err, f"rank {rank}:\n{err[-3000:]}"
+    assert not model.exists()
+
+
+@pytest.mark.gpu
+def test_p2p_healthy_job_writes_the_single_rank_model(tmp_path):
+    """The same job without the fault: the default selection, exit 0 on both ranks, and the model
+    equal to the one-process job's."""
+    from avenir_amd.cli import main
+    from avenir_amd.data import synth
+    data, schema = tmp_path / "churn.csv", tmp_path / "churn.json"
+    synth.write_churn(data, 5001, seed=3, schema_path=schema)
+    one, two = tmp_path / "nb1.txt", tmp_path / "nb2.txt"
+    assert main(["bayesianDistribution", "-i", str(data), "-o", str(one), "--schema", str(schema), "--device", "cuda"]) == 0
+    res = _run_rank_procs(["bayesianDistribution", "-i", str(data), "-o", str(two), "--schema", str(schema),
+                           "--device", "cuda"], 2, {"AVENIR_COMM_BACKEND": "gloo"})
+    for rank, (rc, _o, err) in enumerate(res):
+        assert rc == 0, f"rank {rank}:\n{err[-3000:]}"
+    assert two.read_text() == one.read_text()

@@ -126,6 +126,8 @@ def _all_models(rank, world, churn, hang, seqs, tagged, tx, dev="cpu"):
     obs = torch.randint(0, 4, (1601,), generator=gh).to(torch.int16)
     path, score = SO.viterbi_long(_shard(obs, rank, world).to(dev), lA.to(dev), lB.to(dev), lp.to(dev), chunk=64)
     out["viterbi"] = (path.tolist(), round(float(score), 6))
+    comm.check()
+    out["p2p_calls"] = comm.p2p_calls             # small device sums that took the peer-mapped kernel
     return out
 
 
@@ -179,7 +181,10 @@ def test_world_size_equivalence_device_tensors(comm):
     ref = run_world(_all_models, 1, *args, "cuda", timeout=600, comm=comm)[0]
     for world in (2, 4):
         # the device Viterbi scan accumulates in fp32 per chunk: the score depends on the chunking
-        _compare(run_world(_all_models, world, *args, "cuda", timeout=600, comm=comm), ref, world, score_rel=1e-6)
+        res = run_world(_all_models, world, *args, "cuda", timeout=600, comm=comm)
+        _compare(res, ref, world, score_rel=1e-6)
+        # the default small-sum selection took the hand-written kernel on every rank
+        assert all(r["p2p_calls"] > 0 for r in res), [r["p2p_calls"] for r in res]
 
 
 def _cli_ranks(rank, world, data, schema, model, out_dir, out_file):
