@@ -2146,7 +2146,9 @@ std::vector<at::Tensor> forest_bootstrap(const at::Tensor& codes, const at::Tens
 }
 
 // K27: Y = act(X W^T + b) and its backward epilogue (dZ = dY * act'(Y), db = colsum dZ).
-at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b, int64_t act) {
+at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b, int64_t act,
+                          int64_t prec) {
+  TORCH_CHECK(prec == -1 || prec == 0 || prec == 3 || prec == 6, "prec: -1 (default), 0 (f32), 3 or 6 (split bf16)");
   CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
   CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
   TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "X [M, K], W [N, K]");
@@ -2166,7 +2168,8 @@ at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::o
   at::Tensor part;
   if (S > 1) part = at::empty({(long long)S * M * N}, X.options());
   avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), bc.defined() ? bc.data_ptr<float>() : nullptr,
-                      Y.data_ptr<float>(), M, N, K, (int)act, cur_stream(X), S > 1 ? part.data_ptr<float>() : nullptr, S);
+                      Y.data_ptr<float>(), M, N, K, (int)act, cur_stream(X), S > 1 ? part.data_ptr<float>() : nullptr, S,
+                      (int)prec);
   return Y;
 }
 
@@ -3678,7 +3681,9 @@ at::Tensor add_layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& r
 // LayerNorm.  With the split-K tile (few output tiles over a long K) the slice sum, bias, residual
 // and LayerNorm run in ONE pass over the partials (no [M, N] projection output, no epilogue launch).
 at::Tensor linear_add_layernorm(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b,
-                                const at::Tensor& res, const at::Tensor& gamma, const at::Tensor& beta, double eps) {
+                                const at::Tensor& res, const at::Tensor& gamma, const at::Tensor& beta, double eps,
+                                int64_t prec) {
+  TORCH_CHECK(prec == -1 || prec == 0 || prec == 3 || prec == 6, "prec: -1 (default), 0 (f32), 3 or 6 (split bf16)");
   CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
   CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
   TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "X [M, K], W [N, K]");
@@ -3699,14 +3704,14 @@ at::Tensor linear_add_layernorm(const at::Tensor& X, const at::Tensor& W, const 
   if (S > 1) {
     auto part = at::empty({(long long)S * M * N}, X.options());
     const int Se = avk::linear_splitk_partial(Xc.data_ptr<float>(), Wc.data_ptr<float>(), part.data_ptr<float>(),
-                                              (int)M, (int)N, (int)K, S, cur_stream(X));
+                                              (int)M, (int)N, (int)K, S, cur_stream(X), (int)prec);
     avk::add_layernorm_slices(part.data_ptr<float>(), Se, M * N, ptr_or_null<float>(b), res.data_ptr<float>(),
                               gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr<float>(), M, (int)N,
                               (float)eps, cur_stream(X));
   } else {
     auto y = at::empty({M, N}, X.options());
     avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), ptr_or_null<float>(b), y.data_ptr<float>(),
-                        (int)M, (int)N, (int)K, 0, cur_stream(X));
+                        (int)M, (int)N, (int)K, 0, cur_stream(X), nullptr, 1, (int)prec);
     avk::add_layernorm(y.data_ptr<float>(), res.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                        out.data_ptr<float>(), M, (int)N, (float)eps, cur_stream(X));
   }
@@ -4046,7 +4051,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("forest_bootstrap", &forest_bootstrap);
   m.def("csv_parse_device", &csv_parse_device);
   m.def("forest_predict_bin", &forest_predict_bin);
-  m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0);
+  m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0,
+        py::arg("prec") = -1);
+  m.def("f32_gemm_mode", &avk::f32_gemm_mode);
   m.def("linear_act_bwd", &linear_act_bwd);
   m.def("linear_act_backward", &linear_act_backward);
   m.def("lstm_ks", &lstm_ks);
@@ -4058,7 +4065,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_pack_f32", &lstm_pack_f32);
   m.def("gemm_tn", &gemm_tn);
   m.def("add_layernorm", &add_layernorm);
-  m.def("linear_add_layernorm", &linear_add_layernorm);
+  m.def("linear_add_layernorm", &linear_add_layernorm, py::arg("X"), py::arg("W"), py::arg("b"), py::arg("res"),
+        py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("prec") = -1);
   m.def("attention_f32", &attention_f32);
   m.def("embed_layernorm", &embed_layernorm, py::arg("ids"), py::arg("tt"), py::arg("word"), py::arg("pos"),
         py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("validate") = true);

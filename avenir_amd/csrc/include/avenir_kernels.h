@@ -253,11 +253,15 @@ void forest_part_count(const uint8_t* codes, long long ld, const int* item_node,
 // K27 fused Linear + bias + activation (mlp.hip); with S > 1 and a partial buffer of S*M*N floats
 // the K range is split over S slices (linear_act_fwd_slices picks S for few output tiles over a long K)
 int linear_act_fwd_slices(int M, int N, int K);
+// arithmetic of the fp32 GEMM tiles: 0 exact-f32 MFMA, 3 split-bf16 x3 (~2^-16 per product), 6
+// split-bf16 x6 (fp32-level error); f32_gemm_mode() is the process default (AVMI_F32_GEMM = f32 |
+// bf16x3 | bf16x6, default bf16x6), a call's prec < 0 takes it
+int f32_gemm_mode();
 // the raw split-K partial products [S_eff][M][N] of X W^T (no bias / activation); returns S_eff
 int linear_splitk_partial(const float* X, const float* W, float* partial, int M, int N, int K, int S,
-                          hipStream_t stream);
+                          hipStream_t stream, int prec = -1);
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
-                    hipStream_t stream, float* partial = nullptr, int S = 1);
+                    hipStream_t stream, float* partial = nullptr, int S = 1, int prec = -1);
 int linear_act_bwd_blocks(int M);
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream);
@@ -444,11 +448,18 @@ enum P2PDtype { P2P_F32 = 0, P2P_F64 = 1, P2P_I32 = 2, P2P_I64 = 3 };
 struct P2PView {
   void* data[P2P_MAX_RANKS];       // every rank's data region as mapped in this process
   unsigned* flags[P2P_MAX_RANKS];  // every rank's flag array as mapped in this process
-  int* status;                     // this rank's status word
+  int* status;                     // this rank's status word (device, uncached: the kernels' own check)
+  int* host_status;                // its host-visible copy (pinned, coherent, mapped): 1 = a wait
+                                   // timed out here, 2 = a peer reported a failure
   long long cap_bytes;             // bytes of ONE staging buffer (4 per data region)
   int rank, world;
 };
+constexpr unsigned P2P_POISON = 0x80000000u;   // flag bit: "the rank that raised this has failed"
+constexpr unsigned P2P_MAX_EPOCH = 0x3FFFFFFFu;  // so 2 * epoch never reaches the poison bit
 void p2p_all_reduce(void* x, long long n, int dtype, const P2PView& v, unsigned epoch, int two_shot,
                     long long timeout_ticks, hipStream_t st);
+// raise the poison flag in every peer's array for every block: their next wait on this rank ends
+// at once and records status 2 (the failing rank's last act before it raises on the host)
+void p2p_poison(const P2PView& v, hipStream_t st);
 
 }  // namespace avk

@@ -13,6 +13,7 @@
 //   the host side of the op; dX = dZ W and dW = dZ^T X are plain GEMMs (hipBLASLt).
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "avenir_common.h"
 #include "avenir_kernels.h"
@@ -246,6 +247,157 @@ __global__ __launch_bounds__(MT) void linear_act_fwd_big_kernel(const float* __r
   }
 }
 
+// ---- split-bf16 tiles: fp32 GEMM on the bf16 matrix cores ----------------------------------------
+// CDNA4's fp32 MFMA (v_mfma_f32_32x32x2_f32) runs at the packed-fp32 VALU rate, 1/16 of the bf16
+// MFMA.  Every fp32 operand is split ONCE while it is staged into LDS into NS bf16 terms,
+// x = x_0 + x_1 (+ x_2), each the round-to-nearest bf16 of the remaining residual (the residual
+// x - x_0 is exact in fp32), and the tile is accumulated in fp32 on v_mfma_f32_32x32x16_bf16 over
+// the cross products that matter:
+//   NS = 2 ("bf16x3"): x_1 w_0 + x_0 w_1 + x_0 w_0 — inputs carried to ~16 significand bits, the
+//                      dropped x_1 w_1 ~ 2^-18 |x w|: per-product error ~2^-17 relative;
+//   NS = 3 ("bf16x6"): + x_2 w_0 + x_1 w_1 + x_0 w_2 — ~24 bits, fp32-level error.
+// bf16 has fp32's exponent range, so no scaling is needed (an input of +-inf yields NaN here).  The
+// small terms are accumulated first (products of one term order per pass over the wave's blocks,
+// so consecutive MFMAs never hit the same accumulator).
+// LDS image per term: [rows][32 k + 8 pad] bf16, 80-byte rows: a lane's fragment (8 consecutive k
+// of one row) is one ds_read_b128 and the 16 rows of a 16-lane group land on 16 disjoint 4-bank
+// groups (row r at bank 20 r mod 64).  Tile = 64 WB x 64 WB outputs, 4 waves, each a (32 WB)^2
+// quarter as WB x WB 32 x 32 blocks; the next chunk's fp32 loads are register-prefetched during
+// the MFMAs of the current one (as the fp32 tiles above).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned pack_bf16(float a, float b) {  // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
+}
+__device__ __forceinline__ float bf16_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+
+// split 4 consecutive fp32 values into NS bf16 terms and store each term's 8 bytes at `dst[t]`
+template <int NS>
+__device__ __forceinline__ void split_store4(float4 v, unsigned short* const* dst, int off) {
+  float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    const unsigned p0 = pack_bf16(r[0], r[1]), p1 = pack_bf16(r[2], r[3]);
+    *reinterpret_cast<uint2*>(dst[t] + off) = make_uint2(p0, p1);
+    if (t + 1 < NS) {
+      r[0] -= bf16_lo(p0); r[1] -= bf16_hi(p0);
+      r[2] -= bf16_lo(p1); r[3] -= bf16_hi(p1);
+    }
+  }
+}
+
+template <int WB, int NS, bool SPLIT, int SKC>
+__global__ __launch_bounds__(MT) void linear_act_fwd_sbf16_kernel(const float* __restrict__ X,
+                                                                  const float* __restrict__ W,
+                                                                  const float* __restrict__ b, float* __restrict__ Y,
+                                                                  int M, int N, int K, int act, int kper, int xcd) {
+  constexpr int TR = 64 * WB;        // tile rows = tile cols
+  constexpr int SROW = SKC + 8;      // LDS row (bf16): 80 or 144 bytes, conflict-free b128 reads
+  constexpr int F4R = SKC / 4;       // float4 per row and chunk
+  constexpr int PF = TR * F4R / MT;  // float4 of each operand per thread and chunk
+  __shared__ __attribute__((aligned(16))) unsigned short sX[NS][TR][SROW];
+  __shared__ __attribute__((aligned(16))) unsigned short sW[NS][TR][SROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm = blockIdx.y, tn = blockIdx.x;
+  if (xcd) av::grouped_tile(av::xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y), gridDim.y,
+                            gridDim.x, 8, tm, tn);
+  const long long m0 = (long long)tm * TR;
+  const int n0 = tn * TR;
+  const int kb = SPLIT ? (int)blockIdx.z * kper : 0;
+  const int ke = SPLIT ? min(K, kb + kper) : K;
+  float4 px[PF], pw[PF];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + MT * i, r = e / F4R, k = k0 + (e % F4R) * 4;
+      const long long m = m0 + r;
+      const int n = n0 + r;
+      px[i] = (m < M && k < ke) ? *reinterpret_cast<const float4*>(X + m * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pw[i] = (n < N && k < ke) ? *reinterpret_cast<const float4*>(W + (long long)n * K + k)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  f32x16 acc[WB][WB];
+#pragma unroll
+  for (int i = 0; i < WB; ++i)
+#pragma unroll
+    for (int j = 0; j < WB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  unsigned short* dX[NS];
+  unsigned short* dW[NS];
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    dX[t] = &sX[t][0][0];
+    dW[t] = &sW[t][0][0];
+  }
+  load(kb);
+  const int li = lane & 31, lh = (lane >> 5) * 8;
+  for (int k0 = kb; k0 < ke; k0 += SKC) {
+    __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + MT * i, off = (e / F4R) * SROW + (e % F4R) * 4;
+      split_store4<NS>(px[i], dX, off);
+      split_store4<NS>(pw[i], dW, off);
+    }
+    __syncthreads();
+    if (k0 + SKC < ke) load(k0 + SKC);  // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < SKC; ks += 16) {
+      bf16x8 a[NS][WB], w[NS][WB];
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+#pragma unroll
+        for (int i = 0; i < WB; ++i) a[t][i] = *reinterpret_cast<const bf16x8*>(&sX[t][wm * 32 * WB + 32 * i + li][ks + lh]);
+#pragma unroll
+        for (int j = 0; j < WB; ++j) w[t][j] = *reinterpret_cast<const bf16x8*>(&sW[t][wn * 32 * WB + 32 * j + li][ks + lh]);
+      }
+      // term orders, smallest first: (order 2: x2w0, x1w1, x0w2), (order 1: x1w0, x0w1), (order 0)
+#pragma unroll
+      for (int ord = NS - 1; ord >= 0; --ord)
+#pragma unroll
+        for (int ta = ord; ta >= 0; --ta) {
+          const int tw = ord - ta;
+#pragma unroll
+          for (int i = 0; i < WB; ++i)
+#pragma unroll
+            for (int j = 0; j < WB; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ta][i], w[tw][j], acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+  // epilogue: C/D map of 32x32x16 (as 32x32x2) col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+#pragma unroll
+  for (int j = 0; j < WB; ++j) {
+    const int col = n0 + wn * 32 * WB + 32 * j + (lane & 31);
+    if (col >= N) continue;
+    if constexpr (SPLIT) {
+      float* P = Y + (long long)blockIdx.z * M * N;
+#pragma unroll
+      for (int i = 0; i < WB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long row = m0 + wm * 32 * WB + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < M) P[row * N + col] = acc[i][j][r];
+        }
+    } else {
+      const float bias = b ? b[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < WB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long row = m0 + wm * 32 * WB + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < M) Y[row * N + col] = act_fwd(acc[i][j][r] + bias, act);
+        }
+    }
+  }
+}
+
 // Y[e] = act(sum_s P[s][e] + b[e % N]): the S slices summed in slice order (deterministic), the
 // loads of 8 slices issued together
 __global__ __launch_bounds__(256) void linear_splitk_epilogue_kernel(const float* __restrict__ P,
@@ -440,6 +592,33 @@ static long long split_target() {
   return t;
 }
 
+// fp32 GEMM arithmetic of the K27 tiles (AVMI_F32_GEMM, read once): "f32" = exact-f32 MFMA,
+// "bf16x3" = split-bf16 with 3 products, "bf16x6" = split-bf16 with 6 products (default: the error
+// of the exact-f32 tiles or lower, faster at every measured shape: profiles/r6_gemm_*.jsonl)
+int f32_gemm_mode() {
+  static const int mode = [] {
+    const char* e = std::getenv("AVMI_F32_GEMM");
+    if (e == nullptr) return 6;
+    const std::string v(e);
+    if (v == "f32") return 0;
+    if (v == "bf16x3") return 3;
+    return 6;
+  }();
+  return mode;
+}
+
+// K chunk of the split-bf16 tiles (AVMI_SBF16_KC = 32 | 64 overrides): x3 64 (a few % faster at
+// the large shapes), x6 32 (at 64 its 128 x 128 tile drops to one wave per SIMD: up to 20 % slower;
+// profiles/r6_gemm_bf16x*_kc*.jsonl)
+static int sbf16_kc(int mode) {
+  static const int kc = [] {
+    const char* e = std::getenv("AVMI_SBF16_KC");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (kc == 32 || kc == 64) return kc;
+  return mode == 3 ? 64 : 32;
+}
+
 int linear_act_fwd_slices(int M, int N, int K) {
   const long long tiles = (long long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   // (K < 512: at most 16 chunks per tile, where the extra epilogue launch costs more than the
@@ -456,41 +635,51 @@ int linear_act_fwd_slices(int M, int N, int K) {
 }
 
 int linear_splitk_partial(const float* X, const float* W, float* partial, int M, int N, int K, int S,
-                          hipStream_t stream) {
+                          hipStream_t stream, int prec) {
   const int kper = ((K + S - 1) / S + KC - 1) / KC * KC;
   S = (K + kper - 1) / kper;  // no empty slice
   if (M <= 0 || N <= 0) return S;
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
   dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)S);
-  if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0);
+  const int mode = prec >= 0 ? prec : f32_gemm_mode();
+  if (vec && mode == 3)
+    (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<1, 2, true, 32><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0) : linear_act_fwd_sbf16_kernel<1, 2, true, 64><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0));
+  else if (vec && mode == 6)
+    (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<1, 3, true, 32><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0) : linear_act_fwd_sbf16_kernel<1, 3, true, 64><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0));
+  else if (vec) linear_act_fwd_kernel<true, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0);
   else linear_act_fwd_kernel<false, true><<<grid, MT, 0, stream>>>(X, W, nullptr, partial, M, N, K, 0, kper, 0);
   AV_HIP_CHECK(hipGetLastError());
   return S;
 }
 
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
-                    hipStream_t stream, float* partial, int S) {
+                    hipStream_t stream, float* partial, int S, int prec) {
   if (M <= 0 || N <= 0) return;
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
   if (S > 1 && partial != nullptr) {
-    S = linear_splitk_partial(X, W, partial, M, N, K, S, stream);
+    S = linear_splitk_partial(X, W, partial, M, N, K, S, stream, prec);
     const long long MN = (long long)M * N;
     linear_splitk_epilogue_kernel<<<(unsigned)((MN + 255) / 256), 256, 0, stream>>>(partial, b, Y, MN, N, S, act);
     AV_HIP_CHECK(hipGetLastError());
     return;
   }
+  const int mode = prec >= 0 ? prec : f32_gemm_mode();
   if (vec && M >= 1024 && N >= 1024 && big_tiles_enabled()) {
     dim3 gb((unsigned)((N + TB - 1) / TB), (unsigned)((M + TB - 1) / TB));
     const int xcd = xcd_tiles_enabled() && gb.x * gb.y >= 64 ? 1 : 0;
-    linear_act_fwd_big_kernel<<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, xcd);
+    if (mode == 3) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<2, 2, false, 32><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<2, 2, false, 64><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
+    else if (mode == 6) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<2, 3, false, 32><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<2, 3, false, 64><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
+    else linear_act_fwd_big_kernel<<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, xcd);
     AV_HIP_CHECK(hipGetLastError());
     return;
   }
   dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
   const int xcd = xcd_tiles_enabled() && grid.x * grid.y >= 64 ? 1 : 0;
-  if (vec) linear_act_fwd_kernel<true, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
+  if (vec && mode == 3) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<1, 2, false, 32><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<1, 2, false, 64><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
+  else if (vec && mode == 6) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<1, 3, false, 32><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<1, 3, false, 64><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
+  else if (vec) linear_act_fwd_kernel<true, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
   else linear_act_fwd_kernel<false, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
   AV_HIP_CHECK(hipGetLastError());
 }

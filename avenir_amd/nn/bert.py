@@ -172,13 +172,18 @@ class BertEncoder(torch.nn.Module):
         return W, b
 
     #: rows from which the projections run on hipBLASLt (+ a separate erf-GELU pass) instead of the
-    #: f32-MFMA tile kernel with the GELU epilogue: measured at bert-base shapes, the tile kernel wins
-    #: at B x S = 128 (2.40 vs 3.00 ms per encoder pass) and loses at 4,096-16,384 rows (8.2 vs 6.6 ms)
-    MFMA_MAX_ROWS = int(os.environ.get("AVMI_BERT_MFMA_MAX_ROWS", "1024"))
+    #: tile kernels with the GELU epilogue.  Round 5 (exact-f32 MFMA tiles) stopped at 1,024 rows
+    #: (8.2 vs 6.6 ms per pass at 4-16 k rows); the split-bf16 tiles beat hipBLASLt's fp32 GEMM at
+    #: every bert-base shape (1.4-1.6x at 4,096 rows, profiles/r6_gemm_*.jsonl), so no limit by default
+    MFMA_MAX_ROWS = int(os.environ.get("AVMI_BERT_MFMA_MAX_ROWS", str(1 << 62)))
+    #: arithmetic of the projections (mlp.hip prec): 3 = split-bf16 x3 (inference default: max error
+    #: ~2e-5 at unit-scale activations, inside the fp32 parity bar against transformers), 6 = x6
+    #: (fp32-level error), 0 = exact-f32 MFMA.  AVMI_BERT_GEMM = bf16x3 | bf16x6 | f32
+    GEMM_PREC = {"bf16x3": 3, "bf16x6": 6, "f32": 0}[os.environ.get("AVMI_BERT_GEMM", "bf16x3")]
 
     def _linear(self, x2, W, b, act: int = 0):
         if x2.is_cuda and x2.shape[0] <= self.MFMA_MAX_ROWS:
-            return _native.C().linear_act_fwd(x2, W, b, act)
+            return _native.C().linear_act_fwd(x2, W, b, act, self.GEMM_PREC)
         y = torch.nn.functional.linear(x2, W, b)
         return torch.nn.functional.gelu(y) if act == _GELU else y
 
@@ -206,7 +211,7 @@ class BertEncoder(torch.nn.Module):
         N = W.shape[0]
         if x2.is_cuda and x2.shape[0] <= self.MFMA_MAX_ROWS and N <= 1024 and N % 4 == 0:
             return _native.C().linear_add_layernorm(x2, W, b, res.contiguous(), g.detach(), bb.detach(),
-                                                    self.config.layer_norm_eps)
+                                                    self.config.layer_norm_eps, self.GEMM_PREC)
         return self._add_ln(self._linear(x2, W, b), res, g, bb)
 
     @torch.no_grad()

@@ -41,7 +41,7 @@ def main():
             err = float((got - want).abs().max())
             t_ref = timed(lambda: ref(input_ids=ids, attention_mask=mask))
             t_mine = timed(lambda: mine(ids, mask))
-        print(json.dumps({"bench": "bert_base_encoder", "B": B, "S": S, "ours_ms": t_mine * 1e3,
+        print(json.dumps({"bench": "bert_base_encoder", "gemm": os.environ.get("AVMI_BERT_GEMM", "bf16x3"), "B": B, "S": S, "ours_ms": t_mine * 1e3,
                           "transformers_ms": t_ref * 1e3, "speedup": t_ref / t_mine, "max_abs_diff": err,
                           "tokens_per_s": B * S / t_mine}), flush=True)
 

@@ -14,6 +14,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from avenir_amd import _native  # noqa: E402
 
+MODE = os.environ.get("AVMI_F32_GEMM", "bf16x3")
+
 
 def timed(fn, reps=50):
     for _ in range(3):
@@ -44,16 +46,22 @@ def main():
             ref = lambda: torch.nn.functional.linear(X, W, b)
         t_r = timed(ref)
         err = float((C.linear_act_fwd(X, W, b, act) - ref()).abs().max())
-        print(json.dumps({"op": "linear_act_fwd", "M": M, "N": N, "K": K, "act": act, "us": t_k * 1e6,
+        # error against an fp64 oracle, for the kernel and for the library's fp32 GEMM
+        z64 = torch.nn.functional.linear(X.double(), W.double(), b.double())
+        y64 = (torch.nn.functional.gelu(z64) if act == 6 else torch.relu(z64) if act == 1 else z64)
+        e_k = float((C.linear_act_fwd(X, W, b, act).double() - y64).abs().max())
+        e_t = float((ref().double() - y64).abs().max())
+        print(json.dumps({"op": "linear_act_fwd", "mode": MODE, "M": M, "N": N, "K": K, "act": act, "us": t_k * 1e6,
                           "torch_us": t_r * 1e6, "speedup": t_r / t_k, "TFLOPs": 2 * M * N * K / t_k / 1e12,
-                          "max_abs_diff": err}), flush=True)
+                          "max_abs_diff": err, "err_fp64": e_k, "torch_err_fp64": e_t,
+                          "err_over_sqrtK": e_k / K ** 0.5}), flush=True)
     for K, M, N in ((5000, 400, 106), (327680, 400, 106), (65536, 400, 201)):
         A = torch.randn(K, M, generator=g, device="cuda")
         B = torch.randn(K, N, generator=g, device="cuda")
         t_k = timed(lambda: C.gemm_tn(A, B), reps=20)
         t_r = timed(lambda: A.t() @ B, reps=20)
         err = float((C.gemm_tn(A, B) - A.t() @ B).abs().max())
-        print(json.dumps({"op": "gemm_tn", "K": K, "M": M, "N": N, "us": t_k * 1e6, "torch_us": t_r * 1e6,
+        print(json.dumps({"op": "gemm_tn", "mode": MODE, "K": K, "M": M, "N": N, "us": t_k * 1e6, "torch_us": t_r * 1e6,
                           "speedup": t_r / t_k, "TFLOPs": 2 * M * N * K / t_k / 1e12, "max_abs_diff": err}), flush=True)
 
 
