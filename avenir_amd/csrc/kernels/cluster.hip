@@ -32,6 +32,7 @@
 // scoring and the MFMAs removed streams the data in 182 us (5.9 TB/s), so the pass is bound by the
 // f32 scoring VALU work (16 packed FMAs + argmin per centroid pair per row), not by HBM.
 #include <cstdlib>
+#include <string>
 
 #include "avenir_common.h"
 #include "avenir_kernels.h"
@@ -42,6 +43,34 @@ constexpr int KB = 256;
 constexpr int MAX_RUNS = 16;  // per-run SSE lives in (statically indexed) registers
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// split-bf16 helpers of the kmeans_score_kernel SB variants (see there): RNE pack of two floats
+// (v_cvt_pk_bf16_f32) and the values of a packed pair back in fp32
+__device__ __forceinline__ unsigned km_pack(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a, b}, bf16x2v));
+}
+__device__ __forceinline__ float km_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float km_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+// 4 floats -> T bf16 terms, term t as two packed u32 (dims 0,1 | 2,3)
+template <int T>
+__device__ __forceinline__ void km_split4(float v0, float v1, float v2, float v3, unsigned (&o)[T][2]) {
+  float r[4] = {v0, v1, v2, v3};
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    o[t][0] = km_pack(r[0], r[1]);
+    o[t][1] = km_pack(r[2], r[3]);
+    if (t + 1 < T) {
+      r[0] -= km_lo(o[t][0]); r[1] -= km_hi(o[t][0]);
+      r[2] -= km_lo(o[t][1]); r[3] -= km_hi(o[t][1]);
+    }
+  }
+}
+__device__ __forceinline__ bf16x8 km_frag(unsigned a0, unsigned a1, unsigned b0, unsigned b1) {
+  return __builtin_bit_cast(bf16x8, (u32x4){a0, a1, b0, b1});
+}
 
 __device__ __forceinline__ float pair_at(const float* C2, int D, int j, int d) {
   return C2[(long long)(j >> 1) * 2 * D + 2 * d + (j & 1)];
@@ -310,7 +339,19 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
 // NBUF register tiles in rotation: 2 (the default) keeps one tile of loads ahead at 4 waves / SIMD
 // (120 VGPRs), 3 keeps two ahead at 3 waves / SIMD (162 VGPRs; AVMI_KMEANS_NBUF=3).  Measured at
 // 16.7 M x 16, k = 16: 253.5 vs 263.6 us per pass (profiles/r5_kmeans_nbuf_ab.txt); 5 waves spill.
-template <int D, int KBLK, int NBUF>
+// SB (split-bf16 variant, D in {16, 32}): the fp32 MFMAs become v_mfma_f32_16x16x32_bf16 over
+// split operands.  CDNA4's fp32 MFMA runs at 1/16 of the bf16 rate, so the 32 fp32 MFMAs of a tile
+// (1,024 cycles) were the matrix half of the pass's issue-bound budget.
+//   scoring: the lane's float4 (row 16 sb + col, dims 16 b + 4 g ..+3) is split into 3 bf16 terms
+//     x0 + x1 + x2 and a fragment's 8 k-slots hold two terms of those 4 dims, the centroid
+//     fragment the matching terms: [x0|x1].[c0|c0] + [x0|x1].[c1|c1] + [x0|x2].[c2|c0] = the 6
+//     cross products of fp32-level accuracy (SB = 3) in 3 MFMAs per 16 rows x 16 dims; SB = 2
+//     keeps [x0|x1].[c0|c0] + [x0|x1].[c1|0] (2 MFMAs, ~2^-17 per product);
+//   partial sums: the one-hot is exact in bf16, the staged rows go in as [x0|x1] over 4 rows per
+//     row group: 16 rows per MFMA, 4 per tile instead of 16 (x0 + x1 carries ~2^-18 relative of
+//     each summed coordinate).
+// Per tile 12 + 4 bf16 MFMAs of 16 cycles (256) instead of 32 fp32 ones of 32 (1,024).
+template <int D, int KBLK, int NBUF, int SB = 0>
 __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 2) void kmeans_score_kernel(const float* __restrict__ X, long long n,
                                                           const float* __restrict__ C2, const float* __restrict__ Cn,
                                                           const int* __restrict__ roff, int R, int K,
@@ -355,6 +396,26 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
       const int cq = cb * 16 + 4 * grp + q;
       cinit[cb][q] = cq < K ? -0.5f * Cn[cq] : -INFINITY;
     }
+  }
+  static_assert(SB == 0 || ((D == 16 || D == 32) && (SB == 2 || SB == 3)), "split-bf16 scoring: D 16 / 32, SB 2 / 3");
+  // split-bf16 centroid fragments: [term pair][cb][b], slots j < 4 / j >= 4 = the two terms of
+  // dims 16 b + 4 grp + (j & 3) of centroid 16 cb + col
+  bf16x8 cfr[SB == 0 ? 1 : SB][KBLK][DB];
+  if constexpr (SB != 0) {
+#pragma unroll
+    for (int cb = 0; cb < KBLK; ++cb)
+#pragma unroll
+      for (int b = 0; b < DB; ++b) {
+        unsigned ct[3][2];
+        km_split4<3>(ac[cb][b][0], ac[cb][b][1], ac[cb][b][2], ac[cb][b][3], ct);
+        cfr[0][cb][b] = km_frag(ct[0][0], ct[0][1], ct[0][0], ct[0][1]);                  // [c0|c0]
+        if constexpr (SB == 3) {
+          cfr[1][cb][b] = km_frag(ct[1][0], ct[1][1], ct[1][0], ct[1][1]);                // [c1|c1]
+          cfr[2][cb][b] = km_frag(ct[2][0], ct[2][1], ct[0][0], ct[0][1]);                // [c2|c0]
+        } else {
+          cfr[1][cb][b] = km_frag(ct[1][0], ct[1][1], 0u, 0u);                            // [c1|0]
+        }
+      }
   }
   // partial-sum A operand: lane supplies one-hot[centroid 16 cb + col][row]
   int a_cent[KBLK];
@@ -406,16 +467,43 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
     xsq += (double)xs2;
     // s'(row 16 sb + col, centroid 16 cb + 4 grp + q) in dot[sb][cb][q]
     f32x4 dot[4][KBLK];
+    if constexpr (SB == 0) {
 #pragma unroll
-    for (int b = 0; b < DB; ++b)
+      for (int b = 0; b < DB; ++b)
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int cb = 0; cb < KBLK; ++cb)
+          for (int cb = 0; cb < KBLK; ++cb)
 #pragma unroll
-          for (int sb = 0; sb < 4; ++sb)
-            dot[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[cb][b][m], xv[sb][b][m],
-                                                               (b == 0 && m == 0) ? cinit[cb] : dot[sb][cb], 0, 0, 0);
+            for (int sb = 0; sb < 4; ++sb)
+              dot[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[cb][b][m], xv[sb][b][m],
+                                                                 (b == 0 && m == 0) ? cinit[cb] : dot[sb][cb], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int cb = 0; cb < KBLK; ++cb)
+#pragma unroll
+        for (int sb = 0; sb < 4; ++sb) dot[sb][cb] = cinit[cb];
+      // one 16-row sub-tile at a time (its fragments die before the next one's split: the x6
+      // fragments of all four sub-tiles at once spilled at 4 waves / SIMD); smallest products first
+#pragma unroll
+      for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+        for (int b = 0; b < DB; ++b) {
+          unsigned xt[3][2];
+          km_split4<SB>(xv[sb][b][0], xv[sb][b][1], xv[sb][b][2], xv[sb][b][3],
+                        reinterpret_cast<unsigned (&)[SB][2]>(xt));
+          const bf16x8 f01 = km_frag(xt[0][0], xt[0][1], xt[1][0], xt[1][1]);                  // [x0|x1]
+#pragma unroll
+          for (int cb = 0; cb < KBLK; ++cb) {
+            if constexpr (SB == 3) {
+              const bf16x8 f02 = km_frag(xt[0][0], xt[0][1], xt[2][0], xt[2][1]);              // [x0|x2]
+              dot[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cfr[2][cb][b], f02, dot[sb][cb], 0, 0, 0);
+            }
+            dot[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cfr[1][cb][b], f01, dot[sb][cb], 0, 0, 0);
+            dot[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cfr[0][cb][b], f01, dot[sb][cb], 0, 0, 0);
+          }
+        }
+    }
     // transpose: afterwards dot[j][cb][q] = s'(row 16 grp + col, centroid 16 cb + 4 j + q)
 #pragma unroll
     for (int cb = 0; cb < KBLK; ++cb)
@@ -479,15 +567,36 @@ __global__ __launch_bounds__(KB, (KBLK == 1 && D <= 16) ? (NBUF == 2 ? 4 : 3) : 
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int db = 0; db < DB; ++db) bb[q][db] = xr[(s0 + q) * RS + db * 16];
+      if constexpr (SB == 0) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cb = 0; cb < KBLK; ++cb) {
+            const float av = a[q] == a_cent[cb] ? 1.f : 0.f;
+#pragma unroll
+            for (int db = 0; db < DB; ++db)
+              acc[q & 1][cb][db] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bb[q][db], acc[q & 1][cb][db], 0, 0, 0);
+          }
+      } else {
+        // k-slot 8 grp + j: row 16 grp + s0 + (j & 3), term j >> 2 (one-hot repeated: exact in bf16)
+        bf16x8 xb[DB];
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          unsigned xt[2][2];
+          km_split4<2>(bb[0][db], bb[1][db], bb[2][db], bb[3][db], xt);
+          xb[db] = km_frag(xt[0][0], xt[0][1], xt[1][0], xt[1][1]);
+        }
 #pragma unroll
         for (int cb = 0; cb < KBLK; ++cb) {
-          const float av = a[q] == a_cent[cb] ? 1.f : 0.f;
+          const unsigned one = 0x3F80u;  // bf16 1.0
+          const unsigned h0 = (a[0] == a_cent[cb] ? one : 0u) | ((a[1] == a_cent[cb] ? one : 0u) << 16);
+          const unsigned h1 = (a[2] == a_cent[cb] ? one : 0u) | ((a[3] == a_cent[cb] ? one : 0u) << 16);
+          const bf16x8 oh = km_frag(h0, h1, h0, h1);
 #pragma unroll
           for (int db = 0; db < DB; ++db)
-            acc[q & 1][cb][db] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bb[q][db], acc[q & 1][cb][db], 0, 0, 0);
+            acc[(s0 >> 2) & 1][cb][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh, xb[db], acc[(s0 >> 2) & 1][cb][db], 0, 0, 0);
         }
+      }
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -647,10 +756,24 @@ KmVariant km_variant(int D, int K, int R) {
     const char* e = std::getenv("AVMI_KMEANS_SCORE");
     return e && (e[0] == 'v' || e[0] == 'V');  // "valu": the packed-FMA scoring kernel (A/B)
   }();
+  // AVMI_KMEANS_MFMA = f32 | bf16x3 (default) | bf16x6: the arithmetic of kmeans_score_kernel.
+  // At 16.7 M x 16, k = 16: f32 253.5 us, x3 199.6 us, x6 217.1 us per pass; x3 passes the fp64
+  // oracle with its fp32 tie tolerance (profiles/r6_kmeans_split_bf16.jsonl, r6_kmeans_tests_bf16x3.log)
+  static const int sbm = [] {
+    const char* e = std::getenv("AVMI_KMEANS_MFMA");
+    if (e == nullptr) return 2;
+    const std::string v(e);
+    return v == "f32" ? 0 : (v == "bf16x6" ? 3 : 2);
+  }();
   // one run (R = 1: the job's k-means; batched runs keep the packed-FMA kernel, whose registers
   // grow less with R) and up to 2 blocks of 16 centroids x 16 dims of accumulators
   if (!valu_score && R == 1 && D >= 4 && KBt * (DP / 16) <= 2) {
     const size_t lds = sizeof(float) * (4 * (64 * (size_t)(DP + 4) + 64) + 4 * 64 + K + (size_t)K * D);
+#define AVK_KMSB(DD, KK) \
+  if (D == DD && KBt == KK && sbm != 0)                                                       \
+    return {sbm == 3 ? (const void*)kmeans_score_kernel<DD, KK, 2, 3> : (const void*)kmeans_score_kernel<DD, KK, 2, 2>, lds, true};
+    AVK_KMSB(16, 1) AVK_KMSB(16, 2) AVK_KMSB(32, 1)
+#undef AVK_KMSB
 #define AVK_KMS(DD, KK) \
   if (D == DD && KBt == KK)                                                                   \
     return {nbuf2 ? (const void*)kmeans_score_kernel<DD, KK, 2> : (const void*)kmeans_score_kernel<DD, KK, 3>, lds, true};
