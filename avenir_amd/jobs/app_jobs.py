@@ -266,9 +266,10 @@ def rand_pricing_state(p, g: np.random.Generator) -> list[int]:
 
 
 @job("priceRl", "DQN price optimisation app (P/app/price_rl.py): priceRl train <numIter> [cpDir] | "
-     "inctr <cp> <numIter> [cpDir] | tract <numIter> | loact <cp> [state] | crstate")
+     "inctr <cp> <numIter> [cpDir] | tract <numIter> | loact <cp> [state] | crstate | "
+     "serve <port> [cp|-] [train] | client <url> <numEpisodes> [train] [offpolicy] [stopAtReward]")
 def price_rl(args):
-    rest = _rest(args, 1, "priceRl train|inctr|tract|loact|crstate ...")
+    rest = _rest(args, 1, "priceRl train|inctr|tract|loact|crstate|serve|client ...")
     op, out = rest[0], _Out(args)
     dev, seed = _dev(args), args.seed or 0
     g = np.random.default_rng(seed)
@@ -324,6 +325,22 @@ def price_rl(args):
     elif op == "crstate":
         from ..nn.rl import PricingParams
         out(str(rand_pricing_state(PricingParams(), g)))
+    elif op == "serve":
+        # price_rl_srv.py: the policy behind HTTP (blocks); optional checkpoint and server-side training
+        from .app_more_jobs import PolicyHTTPServer
+        agent = _pricing_agent(dev, seed)
+        if len(rest) > 2 and rest[2] != "-":
+            agent.restore(rest[2])
+        srv = PolicyHTTPServer(agent, train=len(rest) > 3 and rest[3] == "train")
+        out(f"policy server on 127.0.0.1:{int(rest[1])}")
+        out.close()
+        srv.serve(int(rest[1]))
+    elif op == "client":
+        # price_rl_clnt.py: episodes against a running policy server
+        from .app_more_jobs import policy_client
+        flags = set(rest[3:])
+        stop = next((float(f) for f in rest[3:] if f.replace(".", "", 1).lstrip("-").isdigit()), float("inf"))
+        policy_client(rest[1], int(rest[2]), "train" in flags, "offpolicy" in flags, stop, out, seed=seed, device=dev)
     else:
         raise ValueError("invalid command")
     out.close()
