@@ -93,13 +93,21 @@ class PricingEnv:
 
 
 class QNetwork(torch.nn.Module):
-    def __init__(self, n_in: int, n_actions: int, hiddens=(128, 128, 128)):
+    """Hidden layers as the framework's fused Linear + ReLU (nn/mlp.py ``FusedLinear`` -> the K27
+    kernel of mlp.hip on the GPU, forward and backward); ``fused=False`` builds the plain
+    ``torch.nn`` twin with the same parameter names (``net.<2i>.weight``)."""
+
+    def __init__(self, n_in: int, n_actions: int, hiddens=(128, 128, 128), fused: bool = True):
         super().__init__()
+        from .mlp import FusedLinear
         layers, d = [], n_in
         for h in hiddens:
-            layers += [torch.nn.Linear(d, h), torch.nn.ReLU()]
+            if fused:
+                layers += [FusedLinear(d, h, "relu"), torch.nn.Identity()]
+            else:
+                layers += [torch.nn.Linear(d, h), torch.nn.ReLU()]
             d = h
-        layers.append(torch.nn.Linear(d, n_actions))
+        layers.append(FusedLinear(d, n_actions, "none") if fused else torch.nn.Linear(d, n_actions))
         self.net = torch.nn.Sequential(*layers)
 
     def forward(self, x):
@@ -107,21 +115,37 @@ class QNetwork(torch.nn.Module):
 
 
 class DQNAgent:
-    """Double DQN with a device replay ring and a periodically synced target network."""
+    """Double DQN with a device replay ring and a periodically synced target network.
+
+    On the GPU one ``learn`` — replay sampling, the double-DQN target, the Huber loss, backward,
+    fused Adam and the target-network sync — is ONE captured HIP graph (``graph=True``): the
+    replay size and the update counter live on the device, the sampling draws from the agent's
+    generator (registered with the graph, so replays continue its Philox stream exactly as eager
+    calls would) and the sync is a masked ``lerp`` (weight 1 every ``target_sync`` updates, else
+    0) instead of a host branch.  ``fused=False`` / ``graph=False`` give the eager ``torch.nn``
+    twin used by the equivalence tests."""
 
     def __init__(self, env: PricingEnv, lr: float = 0.002, gamma: float = 0.8, batch: int = 256,
                  hiddens=(128, 128, 128), buffer: int = 100_000, eps_start: float = 1.0, eps_end: float = 0.05,
-                 eps_decay_steps: int = 2000, target_sync: int = 200, reward_scale: float = 1e-6, seed: int = 0):
+                 eps_decay_steps: int = 2000, target_sync: int = 200, reward_scale: float = 1e-6, seed: int = 0,
+                 fused: bool = True, graph: bool = True):
         self.env = env
         dev = env.device
         self.device = dev
         S, A = env.p.state_size, env.n_actions
         self.scale = torch.tensor([1.0 / env.p.price_max] * env.p.T + [1.0] * env.p.T + [1.0 / env.p.cyc_period],
                                   device=dev)
-        self.q = QNetwork(S, A, hiddens).to(dev)
-        self.q_tgt = QNetwork(S, A, hiddens).to(dev)
+        self.q = QNetwork(S, A, hiddens, fused=fused).to(dev)
+        self.q_tgt = QNetwork(S, A, hiddens, fused=fused).to(dev)
         self.q_tgt.load_state_dict(self.q.state_dict())
-        self.opt = torch.optim.Adam(self.q.parameters(), lr=lr)
+        cuda = dev.type == "cuda"
+        # fused single-kernel Adam, capturable (its step counter on the device) on the GPU
+        self.opt = torch.optim.Adam(self.q.parameters(), lr=lr, fused=True if cuda else None, capturable=cuda)
+        self.use_graph = bool(graph and cuda)
+        self._graph = None
+        self._gloss = None
+        self._size_dev = torch.zeros((), device=dev)              # replay fill level (float, for sampling)
+        self._steps_dev = torch.zeros((), dtype=torch.long, device=dev)
         self.gamma, self.batch, self.reward_scale = gamma, batch, reward_scale
         self.cap = buffer
         self.buf_s = torch.zeros((buffer, S), device=dev)
@@ -157,11 +181,12 @@ class DQNAgent:
         self.buf_d[idx] = float(d)
         self.ptr = (self.ptr + n) % self.cap
         self.size = min(self.size + n, self.cap)
+        self._size_dev.fill_(float(self.size))        # a fill kernel: no host synchronisation
 
-    def learn(self):
-        if self.size < self.batch:
-            return None
-        i = torch.randint(0, self.size, (self.batch,), device=self.device, generator=self.g)
+    def _learn_body(self) -> torch.Tensor:
+        """One Double-DQN update; device-only (capturable)."""
+        u = torch.rand((self.batch,), device=self.device, generator=self.g)
+        i = (u * self._size_dev).long().clamp_max(self.cap - 1)
         s, a, r, s2, d = self.buf_s[i] * self.scale, self.buf_a[i], self.buf_r[i] * self.reward_scale, \
             self.buf_s2[i] * self.scale, self.buf_d[i]
         with torch.no_grad():
@@ -169,13 +194,57 @@ class DQNAgent:
             tgt = r + self.gamma * (1 - d) * self.q_tgt(s2).gather(1, a2).squeeze(1)
         q = self.q(s).gather(1, a.view(-1, 1)).squeeze(1)
         loss = torch.nn.functional.smooth_l1_loss(q, tgt)
-        self.opt.zero_grad()
+        self.opt.zero_grad(set_to_none=False)
         loss.backward()
         self.opt.step()
-        self.steps += 1
-        if self.steps % self.target_sync == 0:
-            self.q_tgt.load_state_dict(self.q.state_dict())
+        with torch.no_grad():
+            self._steps_dev += 1
+            m = (self._steps_dev % self.target_sync == 0).to(torch.float32)
+            for t, p in zip(self.q_tgt.parameters(), self.q.parameters()):
+                t.lerp_(p, m)                             # target sync: weight 1 every target_sync updates
         return loss.detach()
+
+    def _capture(self):
+        """Warm up (allocator pools, Adam state) on a side stream, restore every piece of state the
+        warm-up touched, then capture one update."""
+        from ..utils.hipgraph import capturing
+        ps = [t for m in (self.q, self.q_tgt) for t in m.parameters()]
+        snap = [t.detach().clone() for t in ps]
+        ost = {id(p): {k: v.clone() for k, v in st.items() if torch.is_tensor(v)} for p, st in self.opt.state.items()}
+        gst, steps0 = self.g.get_state(), self._steps_dev.clone()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                self._learn_body()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        with torch.no_grad():
+            for t, v in zip(ps, snap):
+                t.copy_(v)
+            for p, st in self.opt.state.items():   # restored moments (restore()) or a fresh state
+                old = ost.get(id(p), {})
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        v.copy_(old[k]) if k in old else v.zero_()
+            self._steps_dev.copy_(steps0)
+        self.g.set_state(gst)
+        self._graph = torch.cuda.CUDAGraph()
+        self._graph.register_generator_state(self.g)
+        with capturing(self._graph, device=self.device):
+            self._gloss = self._learn_body()
+
+    def learn(self):
+        if self.size < self.batch:
+            return None
+        if self.use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+            loss = self._gloss
+        else:
+            loss = self._learn_body()
+        self.steps += 1
+        return loss
 
     def train(self, iterations: int = 50, updates_per_step: int = 1):
         """One iteration = one episode of all E environments (T-1 steps)."""
@@ -214,6 +283,8 @@ class DQNAgent:
         st = load_checkpoint(path, self.q, self.opt)
         self.q_tgt.load_state_dict(self.q.state_dict())
         self.steps = int(st.get("steps", 0))
+        self._steps_dev.fill_(self.steps)
+        self._graph = None                   # re-capture: the optimiser state tensors were replaced
 
 
 class PolicyServer:

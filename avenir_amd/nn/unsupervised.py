@@ -19,32 +19,48 @@ from .common import _cfg, create_activation, create_loss, load_checkpoint, optim
     save_checkpoint
 
 
+def _stack(dims: Sequence[int], acts: Sequence[str | None], fused: bool) -> torch.nn.Sequential:
+    """Linear (+ activation) layers; a Linear + activation the K27 kernel covers is ONE fused layer
+    (nn/mlp.py ``FusedLinear``, an ``Identity`` keeps the activation's index, so the parameter
+    names equal the ``torch.nn`` twin's)."""
+    from ..ops.mlp_ops import ACT_CODES
+    from .mlp import FusedLinear
+    out = []
+    for i in range(len(dims) - 1):
+        name = acts[i] if i < len(acts) else None
+        a = create_activation(name)
+        if fused and a is not None and name in ACT_CODES:
+            out += [FusedLinear(dims[i], dims[i + 1], name), torch.nn.Identity()]
+            continue
+        out.append(torch.nn.Linear(dims[i], dims[i + 1]))
+        if a is not None:
+            out.append(a)
+    return torch.nn.Sequential(*out)
+
+
 class AutoEncoder(torch.nn.Module):
+    """On the GPU the layers run the fused Linear + activation kernels and one mini-batch step
+    (forward, loss, backward, optimiser) is a captured HIP graph replayed per batch (the batch's
+    noise is drawn outside the graph into its static input); ``fused=False`` / ``graph=False``
+    give the eager ``torch.nn`` twin."""
+
     def __init__(self, n_in: int, hidden: Sequence[int], enc_act: Sequence[str | None], dec_act: Sequence[str | None],
                  lr: float = 1e-3, weight_decay: float = 1e-5, batch_size: int = 128, noise_scale: float = 0.0,
-                 num_iter: int = 100, loss: str = "mse", optimizer: str = "adam", device=None):
+                 num_iter: int = 100, loss: str = "mse", optimizer: str = "adam", device=None, fused: bool = True,
+                 graph: bool = True):
         super().__init__()
-        enc, dims = [], [n_in] + list(hidden)
-        for i in range(len(hidden)):
-            enc.append(torch.nn.Linear(dims[i], dims[i + 1]))
-            a = create_activation(enc_act[i] if i < len(enc_act) else None)
-            if a is not None:
-                enc.append(a)
-        dec = []
-        rd = list(reversed(dims))
-        for i in range(len(hidden)):
-            dec.append(torch.nn.Linear(rd[i], rd[i + 1]))
-            a = create_activation(dec_act[i] if i < len(dec_act) else None)
-            if a is not None:
-                dec.append(a)
-        self.encoder, self.decoder = torch.nn.Sequential(*enc), torch.nn.Sequential(*dec)
+        dims = [n_in] + list(hidden)
+        self.encoder = _stack(dims, enc_act, fused)
+        self.decoder = _stack(list(reversed(dims)), dec_act, fused)
+        self.use_graph = graph
         self.batch_size, self.noise, self.num_iter = batch_size, noise_scale, num_iter
         self.loss_fn = create_loss(loss)
         self.device = pick_device(device)
         self.to(self.device)
         self.optimizer = optimizer_from_config(self.parameters(), {"train.optimizer": optimizer,
                                                                    "train.opt.learning.rate": lr,
-                                                                   "train.opt.weight.decay": weight_decay})
+                                                                   "train.opt.weight.decay": weight_decay},
+                                               capturable=self.device.type == "cuda")
         self.losses: list[float] = []
 
     @classmethod
@@ -61,25 +77,40 @@ class AutoEncoder(torch.nn.Module):
     def forward(self, x):
         return self.decoder(self.encoder(x))
 
+    def _step(self, inp, target):
+        self.optimizer.zero_grad(set_to_none=False)
+        loss = self.loss_fn(self(inp), target)
+        loss.backward()
+        self.optimizer.step()
+        return loss.detach()
+
     def fit(self, x: torch.Tensor, num_iter: int | None = None, seed: int = 0) -> "AutoEncoder":
+        from .common import GraphedStep
         x = x.to(self.device).float()
         n = x.shape[0]
         bs = min(self.batch_size, n)
+        nb = max(n // bs, 1)
         g = torch.Generator(device=self.device).manual_seed(seed)
         self.train()
+        # the captured step is kept across fit() calls of the same batch shape (a new capture per
+        # call cost more than its replays saved at one epoch per call: profiles/r6_rl_unsup.jsonl)
+        key = (bs, x.shape[1], self.use_graph)
+        step = self._gstep if getattr(self, "_gkey", None) == key else None
+        ep_losses = []                  # on the device until the fit ends: no host sync per epoch
         for _ in range(num_iter if num_iter is not None else self.num_iter):
             perm = torch.randperm(n, device=self.device, generator=g)
             tot = torch.zeros((), device=self.device)
-            nb = max(n // bs, 1)
             for b in range(nb):
                 xb = x[perm[b * bs:(b + 1) * bs]]
                 inp = xb + self.noise * torch.randn(xb.shape, device=self.device, generator=g) if self.noise else xb
-                self.optimizer.zero_grad()
-                loss = self.loss_fn(self(inp), xb)
-                loss.backward()
-                self.optimizer.step()
-                tot += loss.detach()
-            self.losses.append(float(tot) / nb)
+                if step is None:
+                    step = GraphedStep(self._step, inp, xb, enabled=self.use_graph and self.device.type == "cuda",
+                                       model=self, optimizer=self.optimizer)
+                    self._gstep, self._gkey = step, key
+                tot += step(inp, xb)
+            ep_losses.append(tot / nb)
+        if ep_losses:
+            self.losses.extend(torch.stack(ep_losses).tolist())
         self.eval()
         return self
 
@@ -118,6 +149,9 @@ class RestrictedBoltzmannMachine:
                    _cfg(conf, "train.batch.size", 10), _cfg(conf, "train.num.iter", 10), device=device)
 
     def hidden_prob(self, v):
+        if v.is_cuda and v.dim() == 2:
+            from ..ops.mlp_ops import linear_act
+            return linear_act(v.contiguous(), self.W, self.bh, "sigmoid")   # K27 fused GEMM + sigmoid
         return torch.sigmoid(v @ self.W.T + self.bh)
 
     def visible_prob(self, h):
@@ -129,23 +163,56 @@ class RestrictedBoltzmannMachine:
     def gibbs(self, v):
         return self._bern(self.visible_prob(self._bern(self.hidden_prob(v))))
 
-    def fit(self, x: torch.Tensor) -> "RestrictedBoltzmannMachine":
+    def _cd_step(self, v, chain, u_h, u_v, lr: float):
+        """One PCD-1 update from uniforms drawn outside (device-only, capturable, in place): the
+        hidden probabilities are the fused Linear + sigmoid kernel on the GPU."""
+        hp = self.hidden_prob(v)
+        hs = (u_h < self.hidden_prob(chain)).float()
+        chain.copy_((u_v < self.visible_prob(hs)).float())
+        hn = self.hidden_prob(chain)
+        self.W.add_(hp.T @ v - hn.T @ chain, alpha=lr)
+        self.bh.add_(hp.sum(0) - hn.sum(0), alpha=lr)
+        self.bv.add_(v.sum(0) - chain.sum(0), alpha=lr)
+
+    def fit(self, x: torch.Tensor, graph: bool = True) -> "RestrictedBoltzmannMachine":
+        """PCD-1 over shuffled mini-batches.  The uniforms of a step are drawn in the eager
+        order (hidden sample, then visible) into static buffers, so the graphed replay (GPU:
+        the whole step is ONE HIP graph) consumes the generator exactly like the eager loop."""
+        from ..utils.hipgraph import capturing
         x = x.to(self.device).float()
-        n = x.shape[0]
+        n, V = x.shape
+        H = self.W.shape[0]
         bs = min(self.batch_size, n)
-        chain = torch.zeros((bs, x.shape[1]), device=self.device)
+        lr = self.lr / bs
+        chain = torch.zeros((bs, V), device=self.device)
+        sv = torch.zeros((bs, V), device=self.device)
+        u_h = torch.empty((bs, H), device=self.device)
+        u_v = torch.empty((bs, V), device=self.device)
+        use_graph = graph and self.device.type == "cuda"
+        cg = None
         for _ in range(self.num_iter):
             perm = torch.randperm(n, device=self.device, generator=self.g)
             for b in range(n // bs):
-                v = x[perm[b * bs:(b + 1) * bs]]
-                hp = self.hidden_prob(v)
-                hs = self._bern(self.hidden_prob(chain))
-                chain = self._bern(self.visible_prob(hs))
-                hn = self.hidden_prob(chain)
-                lr = self.lr / bs
-                self.W += lr * (hp.T @ v - hn.T @ chain)
-                self.bh += lr * (hp.sum(0) - hn.sum(0))
-                self.bv += lr * (v.sum(0) - chain.sum(0))
+                sv.copy_(x[perm[b * bs:(b + 1) * bs]])
+                torch.rand((bs, H), device=self.device, generator=self.g, out=u_h)
+                torch.rand((bs, V), device=self.device, generator=self.g, out=u_v)
+                if use_graph and cg is None:
+                    # warm-up on a side stream with the state restored afterwards, then capture
+                    snap = [t.clone() for t in (self.W, self.bh, self.bv, chain)]
+                    side = torch.cuda.Stream(self.device)
+                    side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(side):
+                        self._cd_step(sv, chain, u_h, u_v, lr)
+                    torch.cuda.current_stream(self.device).wait_stream(side)
+                    for t, s0 in zip((self.W, self.bh, self.bv, chain), snap):
+                        t.copy_(s0)
+                    cg = torch.cuda.CUDAGraph()
+                    with capturing(cg, device=self.device):
+                        self._cd_step(sv, chain, u_h, u_v, lr)
+                if cg is not None:
+                    cg.replay()
+                else:
+                    self._cd_step(sv, chain, u_h, u_v, lr)
             self.pseudo_ll.append(float(self.score_samples(x).mean()))
         return self
 
