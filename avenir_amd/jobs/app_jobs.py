@@ -1008,6 +1008,8 @@ def forecast(args):
             yearly=seas("train.yearly.seasonality", 10), weekly=seas("train.weekly.seasonality", 3),
             daily=seas("train.daily.seasonality", 4),
             seasonality_prior=float(_get(conf, "train.seasonality.prior.scale", "10.0")),
+            seasonality_mode=str(_get(conf, "train.seasonality.mode", "additive")),
+            holidays_prior=float(_get(conf, "train.holidays.prior.scale", "10.0")),
             interval_width=float(_get(conf, "train.interval.width", "0.8")),
             uncertainty_samples=int(_get(conf, "train.uncertainty.samples", "1000")),
             mcmc_samples=int(_get(conf, "train.mcmc.samples", "0")), device=str(dev), seed=args.seed or 0)

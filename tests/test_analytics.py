@@ -166,3 +166,65 @@ def test_ice_and_lime():
     assert names[0] == "a" and names[-1] == "c"
     coefs = dict(e["explanation"])
     assert coefs["a"] > 0 > coefs["b"]
+
+
+def _mult_series(device="cpu", amp=0.3, days=120, seed=0):
+    import math
+    g = torch.Generator().manual_seed(seed)
+    t = torch.arange(days * 24, dtype=torch.float64) * 3600.0
+    trend = 50.0 + 0.4 * t / 86400.0
+    season = 1.0 + amp * torch.sin(2 * math.pi * t / (7 * 86400.0))
+    y = trend * season + 0.2 * torch.randn(t.shape, generator=g, dtype=torch.float64)
+    return t.to(device), y.to(device), trend, season
+
+
+def _fitted_amplitude(f, t0):
+    import math
+    wk = t0 + torch.arange(7 * 48, dtype=torch.float64) * 1800.0
+    p = f.predict(wk)
+    fac = (p["yhat"] / p["trend"] - 1.0).cpu()
+    return float((fac.max() - fac.min()) / 2)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_forecaster_multiplicative_recovers_seasonal_amplitude(device):
+    """train.seasonality.mode=multiplicative (P/unsupv/profo.py:54,276): y = trend (1 + s(t)); the
+    fitted seasonal factor's amplitude is within 5 % of the true 0.3, and the additive model on
+    the same series is worse (its seasonal term cannot grow with the trend)."""
+    from avenir_amd.analytics.forecast import AdditiveForecaster
+    t, y, trend, season = _mult_series(device)
+    kw = dict(n_changepoints=5, yearly=0, weekly=3, daily=0, device=device, uncertainty_samples=0)
+    fm = AdditiveForecaster(seasonality_mode="multiplicative", **kw).fit(t, y)
+    amp = _fitted_amplitude(fm, float(t[-1]) + 3600.0)
+    assert abs(amp - 0.3) <= 0.05 * 0.3, amp
+    fa = AdditiveForecaster(**kw).fit(t, y)
+    err_m = float(((fm.predict(t)["yhat"] - y) ** 2).mean())
+    err_a = float(((fa.predict(t)["yhat"] - y) ** 2).mean())
+    assert err_m < 0.5 * err_a, (err_m, err_a)
+    # save / load keeps the mode
+    import tempfile, os
+    p = os.path.join(tempfile.mkdtemp(), "m.pt")
+    fm.save(p)
+    g = AdditiveForecaster.load(p, device=device)
+    assert g.mode == "multiplicative" and torch.allclose(g.predict(t)["yhat"], fm.predict(t)["yhat"])
+
+
+def test_forecaster_holiday_prior_is_separate():
+    """train.holidays.prior.scale: a tight holiday prior shrinks the holiday effect, the seasonal
+    fit is unchanged."""
+    import math
+    from avenir_amd.analytics.forecast import AdditiveForecaster
+    t = torch.arange(200 * 24, dtype=torch.float64) * 3600.0
+    hol = [d * 86400.0 for d in (30, 80, 130, 180)]
+    y = 20 + 3 * torch.sin(2 * math.pi * t / (7 * 86400.0))
+    on = torch.zeros_like(t, dtype=torch.bool)
+    for h in hol:
+        on |= (t - h).abs() < 86400.0
+    y = y + 5.0 * on.double() + 0.3 * torch.randn(t.shape, generator=torch.Generator().manual_seed(1),
+                                                   dtype=torch.float64)
+    kw = dict(n_changepoints=3, yearly=0, weekly=3, daily=0, holidays={"h": hol}, uncertainty_samples=0)
+    wide = AdditiveForecaster(holidays_prior=10.0, **kw).fit(t, y)
+    tight = AdditiveForecaster(holidays_prior=1e-4, **kw).fit(t, y)
+    assert wide.beta[-1] * wide.y_scale == pytest.approx(5.0, rel=0.05)
+    assert abs(float(tight.beta[-1] * tight.y_scale)) < 0.5
+    assert torch.allclose(wide.beta[5:-1], tight.beta[5:-1], atol=0.01)     # weekly terms (scaled units)
