@@ -1350,6 +1350,43 @@ void sa_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict
                  cur_stream(cost));
 }
 
+void ga_assign(const at::Tensor& cost, const c10::optional<at::Tensor>& conflict, double invalid, at::Tensor& pop,
+               at::Tensor& pop_cost, at::Tensor& hist, int64_t G, int64_t m, int64_t r, bool purge_first, bool mutate,
+               bool swap, int64_t seed, int64_t island_base, int64_t gen_base) {
+  CHECK_DEV(cost);
+  CHECK_DTYPE(cost, at::kFloat);
+  TORCH_CHECK(cost.dim() == 2 && cost.size(1) >= 2 && cost.is_contiguous(), "cost must be contiguous [L, V>=2]");
+  TORCH_CHECK(gen_base >= 0 && gen_base + G < (1LL << 40), "generation counter out of range");
+  const int64_t L = cost.size(0), V = cost.size(1);
+  TORCH_CHECK(V <= 32767, "V too large");
+  CHECK_DEV(pop);
+  CHECK_DTYPE(pop, at::kShort);
+  TORCH_CHECK(pop.dim() == 3 && pop.size(2) == L && pop.is_contiguous(), "pop must be contiguous [islands, P, L]");
+  const int64_t I = pop.size(0), P = pop.size(1);
+  if (pop.numel())
+    TORCH_CHECK(pop.min().item<int>() >= 0 && pop.max().item<int>() < V, "solution values out of range");
+  CHECK_DEV(pop_cost);
+  CHECK_DTYPE(pop_cost, at::kFloat);
+  TORCH_CHECK(pop_cost.is_contiguous() && pop_cost.numel() == I * P, "pop_cost must be [islands, P]");
+  CHECK_DEV(hist);
+  CHECK_DTYPE(hist, at::kFloat);
+  TORCH_CHECK(hist.is_contiguous() && hist.numel() == I * G, "hist must be [islands, G]");
+  const uint8_t* cf = nullptr;
+  if (conflict.has_value() && conflict->defined()) {
+    CHECK_DEV((*conflict));
+    CHECK_DTYPE((*conflict), at::kByte);
+    TORCH_CHECK(conflict->dim() == 2 && conflict->size(0) == L && conflict->size(1) == L && conflict->is_contiguous(),
+                "conflict [L, L]");
+    cf = conflict->data_ptr<uint8_t>();
+  }
+  DevGuard g(cost.device());
+  avk::ga_assign(cost.data_ptr<float>(), (int)L, (int)V, cf, (float)invalid, pop.data_ptr<int16_t>(),
+                 pop_cost.data_ptr<float>(), hist.data_ptr<float>(), (int)I, (int)P, (int)G, (int)m, (int)r,
+                 purge_first ? 1 : 0, mutate ? 1 : 0, swap ? 1 : 0, (unsigned long long)seed, (long long)island_base,
+                 (int)gen_base,
+                 cur_stream(cost));
+}
+
 // ---------------------------------------------------------------------------------------------
 // generalised linear models (K13)
 // ---------------------------------------------------------------------------------------------
@@ -4005,6 +4042,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bandit_select", &bandit_select);
   m.def("sample", &sample);
   m.def("sa_assign", &sa_assign);
+  m.def("ga_assign", &ga_assign);
+  m.def("ga_assign_lds", [](int64_t P, int64_t L, int64_t r) { return (int64_t)avk::ga_assign_lds((int)P, (int)L, (int)r); });
   m.def("smote_lines", &smote_lines);
   m.def("format_device", &format_device);
   m.def("pairs_within", &pairs_within);

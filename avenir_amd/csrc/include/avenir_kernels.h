@@ -105,6 +105,12 @@ void sample(int dist, long long n, const float* params, const float* table, int 
             unsigned long long offset, float* out, hipStream_t stream);
 
 // ---- optim.hip (K22) -----------------------------------------------------------------------
+// island GA over an assignment domain: pop [islands][P][L] and pop_cost [islands][P] in / out,
+// hist [islands][G] the best cost at each generation's start (optim.hip)
+size_t ga_assign_lds(int P, int L, int r);
+void ga_assign(const float* cost, int L, int V, const uint8_t* conflict, float invalid, short* pop, float* pop_cost,
+               float* hist, int islands, int P, int G, int m, int r, int purge_first, int mutate, int swap,
+               unsigned long long seed, long long island_base, int gen_base, hipStream_t stream);
 void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
                short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
                int geometric, int max_retry, unsigned long long seed, unsigned long long offset,

@@ -8,6 +8,8 @@
 // [L][V] cost table and an [L][L] conflict table, and every lane runs one chain for `iters`
 // Metropolis steps: O(1) cost delta per move, O(L) validity check, Philox randomness, geometric or
 // linear cooling — the whole optimisation is one kernel launch for thousands of chains.
+#include <stdexcept>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -106,9 +108,186 @@ __global__ __launch_bounds__(64) void sa_assign_kernel(
   }
 }
 
+// ---- island genetic algorithm: one workgroup (one wave) per island, G generations per launch ----
+// Reference: Spark GA — an independent GA per partition (S/optimize/GeneticAlgorithm.scala:70-163) —
+// and the Python GeneticAlgorithmOptimizer (P/mlextra/optpopu.py:98-187: pool, mating list,
+// replacement, purge).  An island's pool [P][L], its costs and the children of a generation live in
+// LDS; per generation, one lane per member / pair / child:
+//   1. rank the pool by (cost, index) (lane j counts the members ahead of member j) -> ord[];
+//      hist[g] = the best cost at the generation's start;
+//   2. pair k < r draws Philox(seed, 256 (gen_base + g) + k, island): parents ord[a], ord[b] (a != b) from the
+//      m best, crossover point x in [1, L), children a[:x] b[x:] and b[:x] a[x:]; with `mutate`,
+//      Philox(seed ^ M, 16 ctr + try, island) moves one position of each child to a different
+//      value (a swap move with `swap`), retried until the child is valid (<= 10 tries);
+//   3. lane c < 2r prices child c: fp32 sum of C[l][s_l] in position order times 1/L, or
+//      `invalid` when two conflicting positions share a value;
+//   4. the best r children by (cost, index) replace the worst r members (purge_first) or join the
+//      pool, whose best P by (cost, index; members before children) survive — written to the other
+//      pool buffer in rank order.
+// The island's stream is keyed by its GLOBAL index (island_base + blockIdx.x), so any world size
+// yields the same islands; optimize/ga.py::ga_assign_reference is the bit-exact host twin.
+constexpr int GA_MAX_TRY = 10;
+
+__device__ __forceinline__ bool ga_valid(const short* s, int L, const uint8_t* __restrict__ conflict) {
+  if (conflict)
+    for (int i = 0; i < L; ++i)
+      for (int j = i + 1; j < L; ++j)
+        if (s[i] == s[j] && conflict[(long long)i * L + j]) return false;
+  return true;
+}
+
+__device__ __forceinline__ float ga_price(const short* s, int L, int V, const float* __restrict__ cost,
+                                          const uint8_t* __restrict__ conflict, float invL, float invalid) {
+  float acc = 0.f;
+  for (int l = 0; l < L; ++l) acc += cost[(long long)l * V + s[l]];
+  return ga_valid(s, L, conflict) ? acc * invL : invalid;
+}
+
+__global__ __launch_bounds__(64) void ga_assign_kernel(
+    const float* __restrict__ cost, int L, int V, const uint8_t* __restrict__ conflict, float invalid,
+    short* __restrict__ pop, float* __restrict__ pop_cost, float* __restrict__ hist, int P, int G, int m, int r,
+    int purge_first, int mutate, int swap, unsigned long long seed, long long island_base, int gen_base) {
+  extern __shared__ unsigned char ga_lds[];
+  short* pa = reinterpret_cast<short*>(ga_lds);   // [P][L] current pool
+  short* pb = pa + (size_t)P * L;                 // [P][L] next pool
+  short* kid = pb + (size_t)P * L;                // [2r][L] children
+  float* pc = reinterpret_cast<float*>(kid + (size_t)2 * r * L);  // [P] pool costs
+  float* pc2 = pc + P;                            // [P] next pool costs
+  float* kc = pc2 + P;                            // [2r] child costs
+  int* ord = reinterpret_cast<int*>(kc + 2 * r);  // [P] pool order
+  int* kord = ord + P;                            // [2r] child order
+  int* nsrc = kord + 2 * r;                       // [P] source of next pool slot (>= P: child)
+  const int lane = threadIdx.x;
+  const long long isl = blockIdx.x;
+  const unsigned long long gi = (unsigned long long)(island_base + isl);
+  const float invL = 1.f / (float)L;
+  short* gpop = pop + isl * P * L;
+  for (int e = lane; e < P * L; e += 64) pa[e] = gpop[e];
+  if (lane < P) pc[lane] = pop_cost[isl * P + lane];
+  __syncthreads();
+  for (int g = 0; g < G; ++g) {
+    // 1. rank
+    if (lane < P) {
+      const float c = pc[lane];
+      int rk = 0;
+      for (int j = 0; j < P; ++j) rk += (pc[j] < c) || (pc[j] == c && j < lane);
+      ord[rk] = lane;
+    }
+    __syncthreads();
+    if (lane == 0) hist[isl * G + g] = pc[ord[0]];
+    // 2. children
+    if (lane < r) {
+      const unsigned long long ctr = 256ull * (unsigned long long)(gen_base + g) + lane;
+      const av::u4 R = av::philox_draw(seed, ctr, gi);
+      const int a = min((int)(av::u32_to_unit(R.x) * (float)m), m - 1);
+      int b = 0;
+      if (m > 1) {
+        b = min((int)(av::u32_to_unit(R.y) * (float)(m - 1)), m - 2);
+        b += b >= a;
+      }
+      const int x = L > 1 ? 1 + min((int)(av::u32_to_unit(R.z) * (float)(L - 1)), L - 2) : 0;
+      const short* A = pa + (size_t)ord[a] * L;
+      const short* B = pa + (size_t)ord[b] * L;
+      short* c1 = kid + (size_t)(2 * lane) * L;
+      short* c2 = c1 + L;
+      for (int l = 0; l < L; ++l) {
+        c1[l] = l < x ? A[l] : B[l];
+        c2[l] = l < x ? B[l] : A[l];
+      }
+      if (mutate) {
+        // one position to a different value (with `swap`, the first other position holding that
+        // value takes the old one: the domain's swap move), redrawn up to GA_MAX_TRY times until
+        // the child is valid; the last attempt stays otherwise (BasicSearchDomain.mutateSolution)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          short* c = h == 0 ? c1 : c2;
+          for (int t = 0; t < GA_MAX_TRY; ++t) {
+            const av::u4 Q = av::philox_draw(seed ^ 0xD1B54A32D192ED03ull, ctr * 16ull + t, gi);
+            const unsigned qp = h == 0 ? Q.x : Q.z, qv = h == 0 ? Q.y : Q.w;
+            const int pos = min((int)(av::u32_to_unit(qp) * (float)L), L - 1);
+            const int old = c[pos];
+            int v = min((int)(av::u32_to_unit(qv) * (float)(V - 1)), V - 2);
+            v += v >= old;
+            int holder = -1;
+            if (swap)
+              for (int j = 0; j < L; ++j)
+                if (j != pos && c[j] == v) { holder = j; break; }
+            if (holder >= 0) c[holder] = (short)old;
+            c[pos] = (short)v;
+            if (t == GA_MAX_TRY - 1 || ga_valid(c, L, conflict)) break;
+            c[pos] = (short)old;
+            if (holder >= 0) c[holder] = (short)v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // 3. price the children
+    if (lane < 2 * r) kc[lane] = ga_price(kid + (size_t)lane * L, L, V, cost, conflict, invL, invalid);
+    __syncthreads();
+    if (lane < 2 * r) {
+      const float c = kc[lane];
+      int rk = 0;
+      for (int j = 0; j < 2 * r; ++j) rk += (kc[j] < c) || (kc[j] == c && j < lane);
+      kord[rk] = lane;
+    }
+    __syncthreads();
+    // 4. replacement: the source of every next-pool slot
+    if (purge_first) {
+      if (lane < P) nsrc[lane] = lane < P - r ? ord[lane] : P + kord[lane - (P - r)];
+    } else if (lane < P + r) {
+      // candidate lane: member ord-independent index (lane < P) or child kord[lane - P]; its rank
+      // among all candidates by (cost, candidate index)
+      const int src = lane < P ? lane : P + kord[lane - P];
+      const float c = lane < P ? pc[lane] : kc[src - P];
+      int rk = 0;
+      for (int j = 0; j < P + r; ++j) {
+        const int sj = j < P ? j : P + kord[j - P];
+        const float cj = j < P ? pc[j] : kc[sj - P];
+        rk += (cj < c) || (cj == c && j < lane);
+      }
+      if (rk < P) nsrc[rk] = src;
+    }
+    __syncthreads();
+    for (int e = lane; e < P * L; e += 64) {
+      const int slot = e / L, l = e - slot * L;
+      const int src = nsrc[slot];
+      pb[e] = src < P ? pa[(size_t)src * L + l] : kid[(size_t)(src - P) * L + l];
+    }
+    if (lane < P) {
+      const int src = nsrc[lane];
+      pc2[lane] = src < P ? pc[src] : kc[src - P];
+    }
+    __syncthreads();
+    short* t = pa; pa = pb; pb = t;
+    float* tc = pc; pc = pc2; pc2 = tc;
+  }
+  for (int e = lane; e < P * L; e += 64) gpop[e] = pa[e];
+  if (lane < P) pop_cost[isl * P + lane] = pc[lane];
+}
+
 }  // namespace
 
 namespace avk {
+
+size_t ga_assign_lds(int P, int L, int r) {
+  return (size_t)(2 * P + 2 * r) * L * sizeof(short) + (size_t)(2 * P + 2 * r) * sizeof(float) +
+         (size_t)(2 * P + 2 * r) * sizeof(int);
+}
+
+void ga_assign(const float* cost, int L, int V, const uint8_t* conflict, float invalid, short* pop, float* pop_cost,
+               float* hist, int islands, int P, int G, int m, int r, int purge_first, int mutate, int swap,
+               unsigned long long seed, long long island_base, int gen_base, hipStream_t stream) {
+  if (islands <= 0 || G <= 0) return;
+  if (P < 2 || P > 64 || r < 1 || 2 * r > 64 || r > P || m < 1 || m > P || L < 1 || V < 2)
+    throw std::invalid_argument("ga_assign: 2 <= P <= 64, 1 <= r <= min(P, 32), 1 <= m <= P, L >= 1, V >= 2");
+  if (!purge_first && P + r > 64) throw std::invalid_argument("ga_assign: P + r <= 64 when children join the pool");
+  const size_t lds = ga_assign_lds(P, L, r);
+  if (lds > 64 * 1024) throw std::invalid_argument("ga_assign: pool, children and costs exceed 64 KiB of LDS");
+  ga_assign_kernel<<<islands, 64, lds, stream>>>(cost, L, V, conflict, invalid, pop, pop_cost, hist, P, G, m, r,
+                                                 purge_first, mutate, swap, seed, island_base, gen_base);
+  AV_HIP_CHECK(hipGetLastError());
+}
 
 void sa_assign(const float* cost, int L, int V, const uint8_t* conflict, int swap, short* sol, float* cur_cost,
                short* best_sol, float* best_cost, int P, int iters, float t0, float cool, int interval,
