@@ -4041,6 +4041,29 @@ PYBIND11_MODULE(_C, m) {
   m.def("build_bitsets", &build_bitsets);
   m.def("bandit_select", &bandit_select);
   m.def("sample", &sample);
+  m.def("philox_normal", [](int64_t seed, int64_t offset, int64_t index_base, int64_t n, bool pairs,
+                            c10::optional<at::Device> device) {
+    TORCH_CHECK(n >= 0 && index_base >= 0, "philox_normal: n, index_base >= 0");
+    if (device.has_value() && device->is_cuda()) {
+      auto out = pairs ? at::empty({n, 2}, at::TensorOptions().dtype(at::kDouble).device(*device))
+                       : at::empty({n}, at::TensorOptions().dtype(at::kDouble).device(*device));
+      DevGuard g(*device);
+      avk::philox_normal((unsigned long long)seed, (unsigned long long)offset, (unsigned long long)index_base, n,
+                         out.data_ptr<double>(), pairs ? 1 : 0, cur_stream(out));
+      return out;
+    }
+    auto out = pairs ? at::empty({n, 2}, at::TensorOptions().dtype(at::kDouble))
+                     : at::empty({n}, at::TensorOptions().dtype(at::kDouble));
+    {
+      py::gil_scoped_release nogil;
+      const unsigned hc = std::thread::hardware_concurrency();
+      avh::philox_normal((uint64_t)seed, (uint64_t)offset, (uint64_t)index_base, n, out.data_ptr<double>(),
+                         (int)std::min(16u, hc ? hc : 4u), pairs ? 1 : 0);
+    }
+    return out;
+  }, "N(0,1) draws of Philox(seed, offset, index_base + i), host, fp64 (pairs: both Box-Muller outputs)",
+        py::arg("seed"), py::arg("offset"), py::arg("index_base"), py::arg("n"), py::arg("pairs") = false,
+        py::arg("device") = py::none());
   m.def("sa_assign", &sa_assign);
   m.def("ga_assign", &ga_assign);
   m.def("ga_assign_lds", [](int64_t P, int64_t L, int64_t r) { return (int64_t)avk::ga_assign_lds((int)P, (int)L, (int)r); });

@@ -112,9 +112,13 @@ inline void put_double(Out& o, double v, int prec) {
   auto res = prec >= 0 ? std::to_chars(o.w, o.w + F64_BOUND, v, std::chars_format::fixed, prec)
                        : std::to_chars(o.w, o.w + F64_BOUND, v, std::chars_format::general, 6);  // "{:g}"
   if (res.ec != std::errc()) {  // beyond the bound (very large values at a high precision)
-    const int len = snprintf(nullptr, 0, prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
+    // one format with a precision argument in both cases ("%.*g" at 6 == "%g"), so the varargs
+    // always match the format (int precision, double value)
+    const char* fmt = prec >= 0 ? "%.*f" : "%.*g";
+    const int p = prec >= 0 ? prec : 6;
+    const int len = snprintf(nullptr, 0, fmt, p, v);
     std::string tmp((size_t)len + 1, '\0');
-    snprintf(tmp.data(), tmp.size(), prec >= 0 ? "%.*f" : "%g", prec >= 0 ? prec : 6, v);
+    snprintf(tmp.data(), tmp.size(), fmt, p, v);
     o.commit();
     o.ensure((size_t)len + (1u << 20));  // the rest of the row: its bound was reserved before
     o.put(tmp.data(), (size_t)len);

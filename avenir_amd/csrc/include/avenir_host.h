@@ -214,4 +214,9 @@ int64_t write_coded_csv(const std::string& path, const uint8_t* codes, int ncol,
                         const std::vector<std::vector<std::string>>& vocab, const std::string& id_prefix,
                         char delim, int nthreads);
 
+// Gaussian draws out[i] = N(0, 1) of Philox(seed, offset, index_base + i), fp64, threaded (host/random.cpp);
+// with `pairs`, both Box-Muller outputs per index: out [n][2]
+void philox_normal(uint64_t seed, uint64_t offset, uint64_t index_base, int64_t n, double* out, int nthreads,
+                   int pairs = 0);
+
 }  // namespace avh

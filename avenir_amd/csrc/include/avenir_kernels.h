@@ -101,6 +101,10 @@ void bandit_select(int algo, int G, int A, int batch, const int* trials, const f
                    int* out, hipStream_t stream);
 
 // ---- sampler.hip (K21) ---------------------------------------------------------------------
+// fp64 N(0,1) of Philox(seed, offset, index_base + i) (pairs: both Box-Muller outputs, out [n][2]);
+// the device twin of avh::philox_normal (sampler.hip)
+void philox_normal(unsigned long long seed, unsigned long long offset, unsigned long long index_base, long long n,
+                   double* out, int pairs, hipStream_t stream);
 void sample(int dist, long long n, const float* params, const float* table, int nbins, unsigned long long seed,
             unsigned long long offset, float* out, hipStream_t stream);
 

@@ -144,29 +144,31 @@ __global__ __launch_bounds__(KB) void kmeans_step_kernel(const float* __restrict
     for (int d = 0; d < D; ++d) xn = fmaf(x[d], x[d], xn);
 #pragma unroll
     for (int r = 0; r < MAX_RUNS; ++r) {
-      if (r >= R) break;
-      float best = INFINITY;
-      int bj = s_off[r];
-      for (int j = s_off[r]; j < s_off[r + 1]; ++j) {
-        float dot = 0.f;
+      if (r < R) {   // a guard, not a break: the loop unrolls fully (sse[] stays in registers)
+        float best = INFINITY;
+        int bj = s_off[r];
+        for (int j = s_off[r]; j < s_off[r + 1]; ++j) {
+          float dot = 0.f;
 #pragma unroll
-        for (int d = 0; d < D; ++d) dot = fmaf(x[d], cen[j * D + d], dot);
-        const float dist = cnorm[j] - 2.f * dot;
-        if (dist < best) { best = dist; bj = j; }
+          for (int d = 0; d < D; ++d) dot = fmaf(x[d], cen[j * D + d], dot);
+          const float dist = cnorm[j] - 2.f * dot;
+          if (dist < best) { best = dist; bj = j; }
+        }
+        if (assign) assign[(long long)r * n + row] = bj - s_off[r];
+        sse[r] += (double)fmaxf(best + xn, 0.f);
+        float* a = acc + bj * (D + 1);
+#pragma unroll
+        for (int d = 0; d < D; ++d) atomicAdd(&a[d], x[d]);
+        atomicAdd(&a[D], 1.f);
       }
-      if (assign) assign[(long long)r * n + row] = bj - s_off[r];
-      sse[r] += (double)fmaxf(best + xn, 0.f);
-      float* a = acc + bj * (D + 1);
-#pragma unroll
-      for (int d = 0; d < D; ++d) atomicAdd(&a[d], x[d]);
-      atomicAdd(&a[D], 1.f);
     }
   }
 #pragma unroll
   for (int r = 0; r < MAX_RUNS; ++r) {
-    if (r >= R) break;
-    const double v = av::wave_sum(sse[r]);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][r] = v;
+    if (r < R) {
+      const double v = av::wave_sum(sse[r]);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][r] = v;
+    }
   }
   __syncthreads();
   float* out = partial + (long long)blockIdx.x * K * (D + 1);
@@ -240,17 +242,18 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
     for (int d = 0; d < D; ++d) xn = fmaf(x[d], x[d], xn);
 #pragma unroll
     for (int r = 0; r < MAX_RUNS; ++r) {
-      if (r >= R) break;
-      const int j0 = __builtin_amdgcn_readfirstlane(roff[r]), j1 = __builtin_amdgcn_readfirstlane(roff[r + 1]);
-      float best;
-      int bj;
-      score_run<D>(x, C2, Cn, j0, j1, best, bj);
-      if (ok) {
-        if (assign) assign[(long long)r * n + row] = bj - j0;
-        sse[r] += (double)fmaxf(best + xn, 0.f);
-        atomicAdd(&cnt[bj], 1u);
+      if (r < R) {   // a guard, not a break: the loop unrolls fully (sse[] stays in registers)
+        const int j0 = __builtin_amdgcn_readfirstlane(roff[r]), j1 = __builtin_amdgcn_readfirstlane(roff[r + 1]);
+        float best;
+        int bj;
+        score_run<D>(x, C2, Cn, j0, j1, best, bj);
+        if (ok) {
+          if (assign) assign[(long long)r * n + row] = bj - j0;
+          sse[r] += (double)fmaxf(best + xn, 0.f);
+          atomicAdd(&cnt[bj], 1u);
+        }
+        asg[lane * R + r] = ok ? bj : -1;
       }
-      asg[lane * R + r] = ok ? bj : -1;
     }
     float xp[DP];  // zero-padded copy (compile-time indices: stays in registers)
 #pragma unroll
@@ -298,9 +301,10 @@ __global__ __launch_bounds__(KB) void kmeans_mfma_kernel(const float* __restrict
       }
 #pragma unroll
   for (int r = 0; r < MAX_RUNS; ++r) {
-    if (r >= R) break;
-    const double v = av::wave_sum(sse[r]);
-    if (lane == 0) sred[w][r] = v;
+    if (r < R) {   // a guard, not a break: the loop unrolls fully (sse[] stays in registers)
+      const double v = av::wave_sum(sse[r]);
+      if (lane == 0) sred[w][r] = v;
+    }
   }
   __syncthreads();
   float* out = partial + (long long)blockIdx.x * K * (D + 1);

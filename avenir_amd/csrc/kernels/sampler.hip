@@ -4,6 +4,8 @@
 // per-record JVM samplers used by SMOTE / bagging / MC (J/explore, P/mlextra/mcsim.py:184-212):
 // every element i of a draw is a pure function of (seed, offset, i), so a Monte-Carlo run sharded
 // over any number of GPUs / workgroups reproduces the single-device stream exactly.
+#include <algorithm>
+
 #include "avenir_common.h"
 #include "avenir_kernels.h"
 
@@ -78,6 +80,30 @@ __device__ float poisson_draw(float lam, unsigned long long seed, unsigned long 
   return lam;
 }
 
+// fp64 Gaussian pairs of Philox(seed, offset, index_base + i): the device twin of
+// csrc/host/random.cpp (same counters, 53-bit uniforms, Box-Muller in double precision)
+__device__ __forceinline__ double unit53(uint32_t a, uint32_t b) {
+  const unsigned long long m = ((unsigned long long)a << 21) ^ (unsigned long long)(b >> 11);
+  return ((double)(m & ((1ull << 53) - 1)) + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+__global__ __launch_bounds__(256) void philox_normal_kernel(unsigned long long seed, unsigned long long offset,
+                                                            unsigned long long index_base, long long n,
+                                                            double* __restrict__ out, int pairs) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const av::u4 r = av::philox_draw(seed, offset, index_base + (unsigned long long)i);
+    const double u1 = unit53(r.x, r.y), u2 = unit53(r.z, r.w);
+    const double rad = sqrt(-2.0 * log(u1)), a = 6.283185307179586476925 * u2;
+    if (pairs) {
+      out[2 * i] = rad * cos(a);
+      out[2 * i + 1] = rad * sin(a);
+    } else {
+      out[i] = rad * cos(a);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void sample_kernel(int dist, long long n, const float* __restrict__ p,
                                                      const float* __restrict__ table, int nbins,
                                                      unsigned long long seed, unsigned long long offset,
@@ -127,6 +153,14 @@ __global__ __launch_bounds__(256) void sample_kernel(int dist, long long n, cons
 }  // namespace
 
 namespace avk {
+
+void philox_normal(unsigned long long seed, unsigned long long offset, unsigned long long index_base, long long n,
+                   double* out, int pairs, hipStream_t stream) {
+  if (n <= 0) return;
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  philox_normal_kernel<<<(unsigned)blocks, 256, 0, stream>>>(seed, offset, index_base, n, out, pairs);
+  AV_HIP_CHECK(hipGetLastError());
+}
 
 void sample(int dist, long long n, const float* params, const float* table, int nbins, unsigned long long seed,
             unsigned long long offset, float* out, hipStream_t stream) {

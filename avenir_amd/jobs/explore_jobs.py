@@ -757,15 +757,17 @@ def loo_encoding(args):
         for l in ctx.all_lines(stat_path):
             p = ctx.split(l)
             stats[(int(p[0]), p[1])] = (float(p[2]), float(p[3]))
-    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + ctx.comm.rank)
+    seed = ctx.get_int("random.seed", 0)
+    base = ctx.line_base(len(rows)) if train else 0
     out = []
     d = ctx.delim_out
     enc = {}
-    for o in cat:
+    zc: dict = {}
+    for j, o in enumerate(cat):
         c = torch.tensor([stats[(o, r[o])][0] for r in rows], dtype=torch.float64)
         s = torch.tensor([stats[(o, r[o])][1] for r in rows], dtype=torch.float64)
         if train:
-            noise = 1.0 + (torch.randn(len(rows), generator=g, dtype=torch.float64) * sd).clamp(-3 * sd, 3 * sd)
+            noise = 1.0 + (_loo_noise(seed, j, base, len(rows), None, zc) * sd).clamp(-3 * sd, 3 * sd)
             enc[o] = ((s - yv) / (c - 1 + reg) * noise).tolist()
         else:
             enc[o] = (s / (c + reg)).tolist()
@@ -775,6 +777,25 @@ def loo_encoding(args):
             r[o] = fmt(enc[o][i], prec)
         out.append(d.join(r))
     ctx.emit(out)
+
+
+def _loo_noise(seed: int, field: int, base: int, n: int, device=None, cache: dict | None = None) -> torch.Tensor:
+    """N(0, 1) noise of the leave-one-out encoding: Philox(seed, field j, GLOBAL line index) from
+    the threaded host generator (csrc/host/random.cpp), so a line's noise depends neither on the
+    rank that reads it nor on the device (the reference draws from a per-partition
+    java.util.Random, S/explore/CategoricalLeaveOneOutEncoding.scala:80-136; torch.randn of 2^21
+    doubles on one CPU thread was 25 ms of a 74 ms job, profiles/r6_slow_jobs.jsonl)."""
+    from .. import _native
+    # fields 2k and 2k + 1 share one Philox draw per line (the two Box-Muller outputs); a device
+    # path draws on the GPU with the same fp64 formula (sampler.hip::philox_normal_kernel)
+    key = int(field) // 2
+    if cache is not None and key in cache:
+        return cache[key][:, int(field) % 2]
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    z = _native.C().philox_normal(int(seed), key, int(base), int(n), True, dev if dev.type == "cuda" else None)
+    if cache is not None:
+        cache[key] = z
+    return z[:, int(field) % 2]
 
 
 def _loo_native(ctx, rec, cat, cls_ord, pos, reg, sd, prec, train, stat_path):
@@ -832,12 +853,14 @@ def _loo_native(ctx, rec, cat, cls_ord, pos, reg, sd, prec, train, stat_path):
             if j is not None and c is not None:
                 cnt[j * V + c], sm[j * V + c] = float(p[2]), float(p[3])
         cnt, sm = cnt.to(dev), sm.to(dev)
-    g = torch.Generator().manual_seed(ctx.get_int("random.seed", 0) + ctx.comm.rank)
+    seed = ctx.get_int("random.seed", 0)
+    base = ctx.line_base(n) if train else 0
     c_, s_ = cnt[flat].view(n, F), sm[flat].view(n, F)
     rep = {}
+    zc: dict = {}
     for j, o in enumerate(cat):
         if train:
-            noise = (1.0 + (torch.randn(n, generator=g, dtype=torch.float64) * sd).clamp(-3 * sd, 3 * sd)).to(dev)
+            noise = 1.0 + (_loo_noise(seed, j, base, n, dev, zc).to(dev) * sd).clamp(-3 * sd, 3 * sd)
             e = (s_[:, j] - yv) / (c_[:, j] - 1 + reg) * noise
         else:
             e = s_[:, j] / (c_[:, j] + reg)

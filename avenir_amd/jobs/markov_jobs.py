@@ -415,9 +415,12 @@ def cgs(args):
         C = comm.all_gather_v(C.to(cdev))
     if not ctx.is_root:
         return
-    C = unique_rows(C.cpu().long()) if C.numel() else C.cpu().long().view(0, k + 1)
-    kc = keys.cpu()
-    cols = [("s", rec.vocab, kc[C[:, j]].int().contiguous()) for j in range(k + 1)]
+    # the union's sort on the device (a host unique of the candidates was ~20 ms of the 78 ms job
+    # at 800 k sequences: profiles/r6_slow_jobs.jsonl); only the code columns come back
+    C = C.to(rec.device).long()
+    C = unique_rows(C) if C.numel() else C.view(0, k + 1)
+    kc = keys.to(C.device)
+    cols = [("s", rec.vocab, kc[C[:, j]].int().cpu().contiguous()) for j in range(k + 1)]
     ctx.emit_root_columns(cols, int(C.shape[0]))
 
 

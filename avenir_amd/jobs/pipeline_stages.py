@@ -359,27 +359,47 @@ def _num_distr_native(ctx, rec, kords, attrs, prec):
     from ..data.records import sorted_key_tuples
     g, G, ktab = sorted_key_tuples(rec, [rec.field(o) for o in kords], ctx.comm) if kords else \
         (torch.zeros(rec.n_lines, dtype=torch.long, device=rec.device), 1, torch.zeros((1, 0), dtype=torch.long))
-    g = g.cpu()
+    on_dev = rec.device.type == "cuda"
+    if not on_dev:
+        g = g.cpu()
     keys = [tuple(rec.vocab[c] for c in row) for row in ktab.tolist()]
     d = ctx.delim_out
     out = []
     for a in attrs:
         bw = float(ctx.cfg.values.get(f"attrBinWidth.{a}", ctx.get_float("bin.width", 1.0)))
-        x = rec.field(a, numeric=True).double().cpu()
+        x = rec.field(a, numeric=True).double()
+        if not on_dev:
+            x = x.cpu()
         b = torch.floor(x / bw).long()
         n = x.numel()
-        lo = torch.tensor([int(b.min()) if n else 0])
-        hi = torch.tensor([int(b.max()) if n else 0])
+        # bin range: one device reduction, one host read of both ends
+        lo, hi = (torch.stack([b.min(), b.max()]).cpu() if n else torch.zeros(2, dtype=torch.long)).view(2, 1)
         if ctx.comm.is_distributed:
             ctx.comm.all_reduce(lo, "min")
             ctx.comm.all_reduce(hi, "max")
         B = int(hi - lo) + 1
-        Hh = torch.zeros(G * B, dtype=torch.long).index_add_(0, g * B + (b - int(lo)), torch.ones_like(b)).view(G, B)
-        mom = torch.zeros((G, 3), dtype=torch.float64)
-        mom[:, 0].index_add_(0, g, torch.ones_like(x))
-        mom[:, 1].index_add_(0, g, x)
-        mom[:, 2].index_add_(0, g, x * x)
+        if on_dev and G * B < (1 << 20):
+            # K23 LDS-privatised (code, value) sums (ops/encode_ops.loo_stats): the joint (key, bin)
+            # counts and the per-key sums of x and x^2 as three passes over the device columns —
+            # a global index_add onto G * B slots serialises on its atomics (the host index_add
+            # was 13 ms of a 41 ms job at 2^21 records: profiles/r6_slow_jobs.jsonl)
+            from ..ops.encode_ops import loo_stats
+            gi = g.int().view(1, -1)
+            kb = (g * B + (b - int(lo))).int().view(1, -1)
+            _, kc = loo_stats(kb, n, torch.zeros(n, dtype=torch.float64, device=x.device), G * B + 1)
+            s1, k1 = loo_stats(gi, n, x, G + 1)
+            s2, _ = loo_stats(gi, n, x * x, G + 1)
+            Hh = kc[0, :G * B].long().view(G, B)
+            mom = torch.stack([k1[0, :G].double(), s1[0, :G], s2[0, :G]], 1)
+        else:
+            Hh = torch.zeros(G * B, dtype=torch.long, device=b.device).index_add_(
+                0, g * B + (b - int(lo)), torch.ones_like(b)).view(G, B)
+            mom = torch.zeros((G, 3), dtype=torch.float64, device=x.device)
+            mom[:, 0].index_add_(0, g, torch.ones_like(x))
+            mom[:, 1].index_add_(0, g, x)
+            mom[:, 2].index_add_(0, g, x * x)
         ctx.all_reduce(Hh, mom)
+        Hh, mom = Hh.cpu(), mom.cpu()
         for i, k in enumerate(keys):
             cnt = float(mom[i, 0])
             if cnt == 0:

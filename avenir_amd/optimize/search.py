@@ -79,6 +79,13 @@ def _global_best(comm: Comm, cost: torch.Tensor, sol: torch.Tensor) -> tuple[tor
 # simulated annealing
 # ================================================================================================
 class SimulatedAnnealing:
+    """Batched SA chains.  The one-launch K22 kernel (``sa_assign_kernel``) takes assignment domains
+    with single-position moves (``max.step.size`` = 1) and L <= 512 positions (the [L][64]
+    solution tile of a wave lives in LDS).  Multi-position steps, larger L and other domains run
+    the batched generic path: every chain of the rank advances together, one set of tensor ops
+    per move (documented limit; the reference's task-schedule configurations all use step 1 and
+    tens of positions)."""
+
     def __init__(self, domain: SearchDomain, n_chains: int = 8, iters: int = 300, t0: float = 30.0,
                  cooling: float = 0.99, geometric: bool = True, interval: int = 2, step: int = 1,
                  max_retry: int = 3, seed: int = 0, locally_optimize: bool = False, local_iters: int = 50,

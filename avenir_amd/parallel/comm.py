@@ -141,9 +141,12 @@ class Comm:
         self.stats["seconds"] += time.perf_counter() - t0
 
     def _prep(self, t: torch.Tensor) -> tuple[torch.Tensor, bool]:
-        """gloo only handles CPU tensors, RCCL only GPU tensors: move if needed."""
+        """gloo only handles CPU tensors, RCCL only GPU tensors: move if needed (a host tensor
+        handed to an RCCL group — a job's small host-side counters — goes through the device)."""
         if self.pg_backend == "gloo" and t.is_cuda:
             return t.cpu(), True
+        if self.pg_backend == "nccl" and not t.is_cuda and self.device.type == "cuda":
+            return t.to(self.device), True
         return t, False
 
     # ------------------------------------------------------------------------------------------

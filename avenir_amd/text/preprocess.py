@@ -263,11 +263,59 @@ class TextPreProcessor:
         return {f"contains({w})": (w in d) for w in word_features}
 
 
-def clean_tokens(text: str, pp: TextPreProcessor | None = None, stem: bool = False, min_len: int = 2) -> list[str]:
+def clean_tokens_reference(text: str, pp: TextPreProcessor | None = None, stem: bool = False,
+                           min_len: int = 2) -> list[str]:
+    """The step-by-step pipeline (contractions, tokens, lower case, punctuation, stop words, short
+    words): the oracle of :func:`clean_tokens`."""
     pp = pp or TextPreProcessor()
     w = pp.removeStopwords(pp.removePunctuation(pp.toLowercase(pp.tokenize(pp.replaceContractions(text)))))
     w = pp.removeShortWords(w, min_len)
     return pp.stemWords(w) if stem else w
+
+
+# clean_tokens in one pass: the contraction table as ONE alternation (its keys in table order, so
+# "won't" / "can't" win over "n't" at their position, as the sequential substitutions; none of the
+# replacements contains an apostrophe, so no substitution can feed a later one), one precompiled
+# tokeniser, and the per-word punctuation regex replaced by deleting ' and - inside alphanumeric
+# tokens (the only non-word characters the tokeniser lets into them).  The semantic-search corpus
+# spent most of its host time in ~3.5 M uncached re.sub calls of the step-by-step version.
+_CONTR_RE = re.compile("|".join(re.escape(k) for k in CONTRACTIONS), re.IGNORECASE)
+_CONTR_LOWER = {k.lower(): v for k, v in CONTRACTIONS.items()}
+_TOKEN_RE = re.compile(r"[A-Za-z0-9]+(?:['\-][A-Za-z0-9]+)*|[^\sA-Za-z0-9]")
+_WORDCHAR_RE = re.compile(r"\w")
+_DROP_APOS_HYPHEN = str.maketrans("", "", "'-")
+
+
+_ASCII_WORD_RE = re.compile(r"[a-z0-9]+(?:['\-][a-z0-9]+)*")
+
+
+def _contraction(m) -> str:
+    return _CONTR_LOWER[m.group(0).lower()]
+
+
+def clean_tokens(text: str, pp: TextPreProcessor | None = None, stem: bool = False, min_len: int = 2) -> list[str]:
+    text = _CONTR_RE.sub(_contraction, text)
+    if min_len >= 2 and text.isascii():
+        # ASCII fast path: lower-casing first tokenises identically; the single-character tokens
+        # are punctuation (dropped) or "_" (shorter than min_len), so only words are matched
+        out = []
+        for t in _ASCII_WORD_RE.findall(text.lower()):
+            if "'" in t or "-" in t:
+                t = t.translate(_DROP_APOS_HYPHEN)
+            if len(t) >= min_len and t not in STOP_WORDS:
+                out.append(t)
+        return [porter_stem(w) for w in out] if stem else out
+    out = []
+    for t in _TOKEN_RE.findall(text):
+        t = t.lower()
+        c = t[0]
+        if "a" <= c <= "z" or "0" <= c <= "9":
+            t = t.translate(_DROP_APOS_HYPHEN)
+        elif not _WORDCHAR_RE.match(t):
+            continue
+        if len(t) >= min_len and t not in STOP_WORDS:
+            out.append(t)
+    return [porter_stem(w) for w in out] if stem else out
 
 
 # ------------------------------------------------------------------------------------------------

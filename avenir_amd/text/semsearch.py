@@ -43,26 +43,53 @@ class SemanticSearch:
         self.docs.append(text)
         return self
 
-    def add_many(self, texts: Sequence[str]):
-        """``add`` for a whole corpus: with an embedder that has ``many`` (nn/bert.py's), the tokens
-        of every document and every sentence are embedded in one batched call."""
+    def add_many(self, texts: Sequence[str], sent_tokens: Sequence[Sequence[Sequence[str]]] | None = None):
+        """``add`` for a whole corpus: with an embedder that has ``many`` (nn/bert.py's, the corpus
+        embedder's), the tokens of every document and every sentence are embedded in one batched
+        call, and the sentence means and all normalisations are batched reductions.
+
+        A document's cleaned tokens are exactly the concatenation of its sentences' (tokens and
+        contractions never span the whitespace split_sentences cuts at), so with a context-free
+        embedder (``emb.context_free``, the corpus embedder) every token is looked up once and the
+        document rows are the sentence rows; ``sent_tokens`` (per document, per sentence) may be
+        passed in when the caller already cleaned them."""
         many = getattr(self.embed, "many", None)
         if many is None:
             for t in texts:
                 self.add(t)
             return self
-        toks = [clean_tokens(t) for t in texts]
-        sents = [[s for s in (clean_tokens(x) for x in split_sentences(t)) if s] for t in texts]
-        flat = toks + [s for ss in sents for s in ss]
-        embs = many(flat)
-        nt = len(texts)
-        k = nt
+        if sent_tokens is None:
+            sent_tokens = [[clean_tokens(x) for x in split_sentences(t)] for t in texts]
+        sents = [[s for s in ss if s] for ss in sent_tokens]
+        ns = [len(ss) for ss in sents]
+        flat_sents = [s for ss in sents for s in ss]
+        if getattr(self.embed, "context_free", False):
+            toks = [[w for s in ss for w in s] for ss in sents]
+            E = torch.cat([e.float() for e in many(flat_sents)], 0) if flat_sents else torch.zeros((0, 1))
+            E = E.to(self.device)
+            doc_rows = E                                         # sentence rows in document order
+        else:
+            toks = [clean_tokens(t) for t in texts]
+            embs = many(toks + flat_sents)
+            doc_rows = torch.cat([e.float() for e, t in zip(embs[:len(texts)], toks) if t], 0).to(self.device) \
+                if any(toks) else torch.zeros((0, 1), device=self.device)
+            E = torch.cat([e.float() for e in embs[len(texts):]], 0).to(self.device) if flat_sents else \
+                torch.zeros((0, doc_rows.shape[1]), device=self.device)
+        # sentence means: one segmented sum over the sentence rows
+        lens = torch.tensor([len(s) for s in flat_sents], dtype=torch.long, device=self.device)
+        if flat_sents:
+            seg = torch.repeat_interleave(torch.arange(len(flat_sents), device=self.device), lens)
+            S = torch.zeros((len(flat_sents), E.shape[1]), device=self.device).index_add_(0, seg, E)
+            S = _norm(S / lens.view(-1, 1).float())
+        else:
+            S = torch.zeros((0, max(1, E.shape[1])), device=self.device)
+        Tn = _norm(doc_rows)
+        tl = [len(t) for t in toks]
+        tok_parts = list(torch.split(Tn, tl)) if Tn.shape[0] else [Tn[:0]] * len(texts)
+        sent_parts = list(torch.split(S, ns)) if S.shape[0] else [S[:0]] * len(texts)
         for i, t in enumerate(texts):
-            e = embs[i].float().to(self.device) if toks[i] else torch.zeros((0, 1))
-            self.tok_emb.append(_norm(e))
-            se = [embs[k + j].float().mean(0) for j in range(len(sents[i]))]
-            k += len(sents[i])
-            self.sent_emb.append(_norm(torch.stack(se).to(self.device)) if se else e[:0])
+            self.tok_emb.append(tok_parts[i] if tl[i] else torch.zeros((0, 1), device=self.device))
+            self.sent_emb.append(sent_parts[i] if ns[i] else torch.zeros((0, 1), device=self.device))
             self.docs.append(t)
         return self
 
@@ -138,15 +165,16 @@ def hashing_embedder(dim: int = 256, seed: int = 0):
 
 
 def corpus_embedder(docs: Sequence[str], dim: int = 100, epochs: int = 10, window: int = 5, device="cpu",
-                    seed: int = 0):
+                    seed: int = 0, sentences: Sequence[Sequence[str]] | None = None):
     """Document embedder trained on the corpus itself: skip-gram Word2Vec (negative sampling, on
     ``device``) over the cleaned sentences of ``docs``; tokens outside its vocabulary fall back to
     scaled hashing vectors.  Stands in for ssearch.py's spaCy-transformers BERT encoder
     (P/app/ssearch.py:184-186), which needs pretrained weights this environment cannot fetch —
     parity unpinned; the tests check retrieval quality on a seeded topical corpus instead."""
     from .models import Word2Vec
-    sents = [clean_tokens(s) for d in docs for s in split_sentences(d)]
-    sents = [s for s in sents if s]
+    if sentences is None:
+        sentences = [clean_tokens(s) for d in docs for s in split_sentences(d)]
+    sents = [s for s in sentences if s]
     w2v = Word2Vec(dim=dim, window=window, epochs=epochs, seed=seed, device=device).fit(sents)
     fallback = hashing_embedder(dim, seed)
     W = w2v.W
@@ -175,10 +203,14 @@ def corpus_embedder(docs: Sequence[str], dim: int = 100, epochs: int = 10, windo
         return list(torch.split(emb(flat), lens))
     emb.model = w2v
     emb.many = many
+    emb.context_free = True           # a token's vector does not depend on its neighbours
     return emb
 
 
 def search_corpus(docs: Sequence[str], dim: int = 100, epochs: int = 10, device="cpu", seed: int = 0) -> SemanticSearch:
     """A :class:`SemanticSearch` over ``docs`` with the corpus-trained embedder."""
-    ss = SemanticSearch(corpus_embedder(docs, dim, epochs, device=device, seed=seed), device=device)
-    return ss.add_many(docs)
+    sent_tokens = [[clean_tokens(x) for x in split_sentences(d)] for d in docs]     # cleaned once
+    emb = corpus_embedder(docs, dim, epochs, device=device, seed=seed,
+                          sentences=[s for ss in sent_tokens for s in ss])
+    ss = SemanticSearch(emb, device=device)
+    return ss.add_many(docs, sent_tokens=sent_tokens)

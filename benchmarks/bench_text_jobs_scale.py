@@ -29,6 +29,7 @@ def main_(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--per", type=int, default=2000)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("stages", nargs="*", help="stage names (default: all)")
     args = ap.parse_args(argv)
     tmp = Path(tempfile.mkdtemp(prefix="avmi_text_scale_"))
     try:
@@ -52,6 +53,8 @@ def main_(argv=None) -> int:
                                       "-D", "embed.epochs=3"],
         }
         for name, cmd in stages.items():
+            if args.stages and name not in args.stages:
+                continue
             times = []
             for _ in range(2):
                 t0 = time.perf_counter()

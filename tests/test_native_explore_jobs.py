@@ -236,7 +236,7 @@ def _world(rank, world, argv, out, cfg):
     return True
 
 
-@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote", "relief", "bag", "nor", "pro", "tef", "tra", "uvc", "tig", "tig_rep", "nads"])
+@pytest.mark.parametrize("name", ["rue", "usb", "abe", "hash", "dummy", "lmap", "ipca", "spc", "ctime", "etd", "iim", "smote", "relief", "bag", "nor", "pro", "tef", "tra", "uvc", "tig", "tig_rep", "nads", "loo"])
 def test_world2_equals_world1(tmp_path, name):
     argv, cfg = _setup(tmp_path, name, False)
     assert main([str(a) for a in argv] + ["-o", str(tmp_path / "w1"), "-c", str(cfg), "--device", "cpu"]) == 0

@@ -235,3 +235,21 @@ def test_word2vec_and_doc2vec_kernel(cuda):
     same = [(D[i] @ D[j]).item() for i in range(20) for j in range(20) if i != j and labels[i] == labels[j]]
     diff = [(D[i] @ D[j]).item() for i in range(20) for j in range(20) if labels[i] != labels[j]]
     assert np.mean(same) > np.mean(diff) + 0.2
+
+
+def test_clean_tokens_one_pass_equals_stepwise_pipeline():
+    """The one-pass clean_tokens (one contraction alternation, one tokeniser, ASCII fast path)
+    equals the step-by-step pipeline on fuzzed text: contractions in any case, apostrophes and
+    hyphens inside and around words, unicode letters, underscores, numbers, punctuation."""
+    import random
+    from avenir_amd.text.preprocess import clean_tokens, clean_tokens_reference
+    rng = random.Random(0)
+    frags = ["won't", "Won't", "CAN'T", "can't", "don't", "isn't", "they're", "it's", "I'd", "we'll", "you've", "I'm",
+             "o'brien", "well-known", "rock'n'roll", "-", "'", "--", "a-", "students'", "naïve", "café", "É", "_",
+             "__init__", "x_y", "3.14", "1,000", "42", "e-mail", "Hello", "WORLD", "the", "and", "a", "!", "?", "(",
+             "\"", "$5", "@home", "#tag", "Zürich", "n't", "'s", "can'tn't", "a'", "'a", "K", "ﬁne", "a-'b"]
+    for _ in range(5000):
+        text = " ".join(rng.choice(frags) + rng.choice([".", ",", "", ""]) for _ in range(rng.randint(1, 12)))
+        for stem in (False, True):
+            for ml in (1, 2, 3):
+                assert clean_tokens(text, stem=stem, min_len=ml) == clean_tokens_reference(text, stem=stem, min_len=ml)

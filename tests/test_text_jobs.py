@@ -183,4 +183,5 @@ def test_corpus_embedder_batched_adds_equal_one_by_one(tmp_path):
         one.add(x)
     many = SemanticSearch(emb).add_many(docs)
     for a, b in zip(one.tok_emb + one.sent_emb, many.tok_emb + many.sent_emb):
-        assert torch.equal(a, b)
+        # the batched sentence means are one segmented sum (another summation order than .mean)
+        assert a.shape == b.shape and torch.allclose(a, b, rtol=1e-5, atol=1e-6)
