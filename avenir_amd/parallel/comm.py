@@ -64,6 +64,7 @@ _SMALL_ENV = os.environ.get("AVMI_SMALL_ALLREDUCE", "auto").strip().lower() or "
 if _SMALL_ENV not in ("auto", "p2p", "oneshot", "rccl"):
     raise ValueError(f"AVMI_SMALL_ALLREDUCE={_SMALL_ENV!r}: expected auto, p2p, oneshot or rccl")
 _ONESHOT_MAX_BYTES = int(os.environ.get("AVMI_ONESHOT_MAX_BYTES", str(64 << 10)))
+_PROBE_TIMEOUT_S = float(os.environ.get("AVMI_P2P_PROBE_TIMEOUT_S", "10"))
 
 
 class CollectiveTimeout(RuntimeError):
@@ -228,17 +229,42 @@ class Comm:
         return choice
 
     def _probe_p2p(self, p, like: torch.Tensor, rounds: int = 8, iters: int = 30) -> tuple[bool, float, float]:
-        """This rank's measurements: the kernel exact on integer sums of ``like``'s size (checked
-        calls: a failed wait raises P2PError on the ranks involved), then the mean time of the
-        kernel and of the library collective at that size."""
+        """This rank's measurements: the kernel exact on integer sums of ``like``'s size, then the
+        mean time of the kernel and of the library collective at that size.
+
+        The exactness rounds start behind a barrier and run under a short wait bound
+        (``AVMI_P2P_PROBE_TIMEOUT_S``, 10 s): a node whose peer mapping does not deliver (flags
+        never seen across devices, a peer gone) fails HERE, in seconds, instead of at the job's
+        first real sum after the full wait bound.  A P2PError in these rounds is caught; exactness
+        is then agreed over the ranks (one library all-reduce) BEFORE the timing rounds, so every
+        rank runs the same collectives, and an inexact verdict anywhere retires the kernel on every
+        rank (closed together; later small sums take the library collective)."""
+        from .p2p import P2PError
         W = self.world
         n = max(1, like.numel())
         xi = torch.empty(n, dtype=torch.int64, device=like.device)
         exact = True
-        for i in range(rounds):
-            xi.fill_(self.rank + 1 + i)
-            p.all_reduce(xi)
-            exact &= bool((xi == W * (W + 1) // 2 + W * i).all().item())
+        old = p.timeout_s
+        self.barrier()
+        try:
+            p.set_timeout(min(old, _PROBE_TIMEOUT_S))
+            for i in range(rounds):
+                xi.fill_(self.rank + 1 + i)
+                p.all_reduce(xi)
+                exact &= bool((xi == W * (W + 1) // 2 + W * i).all().item())
+        except P2PError as e:
+            alog.get_logger("comm").warning("peer-mapped all-reduce failed its probe: %s", e)
+            exact = False
+        dev = self.device if self.pg_backend == "nccl" else "cpu"
+        f = torch.tensor([0.0 if exact else 1.0], dtype=torch.float64, device=dev)
+        self.all_reduce(f, "max", algo="ring")
+        if float(f.item()) != 0.0:
+            try:
+                p.close()                     # collective: every rank reaches it (agreed verdict)
+            finally:
+                self._p2p = False
+            return False, float("inf"), 0.0
+        p.set_timeout(old)
         x = torch.ones_like(like).contiguous()
 
         def timed(fn) -> float:

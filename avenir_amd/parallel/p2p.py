@@ -160,6 +160,12 @@ class P2PAllReduce:
             self.check(block=True)
         return t
 
+    def set_timeout(self, seconds: float) -> None:
+        """Bound of every later kernel wait (the selection probe runs under a short one)."""
+        self.timeout_s = float(seconds)
+        if self._h is not None:
+            self._h.set_timeout(self.timeout_s)
+
     def status(self, block: bool = False) -> int:
         """0 healthy, 1 a wait of this rank timed out, 2 a peer reported a failure.  ``block``
         waits for the last call's kernel first; otherwise only finished kernels are seen."""

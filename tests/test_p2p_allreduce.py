@@ -221,6 +221,51 @@ def test_auto_selection_is_agreed_over_ranks():
         assert got == [None, "library", None, "library", "p2p", "p2p"]
 
 
+class _FailingP2P:
+    """A constructed peer-mapped state whose waits stop delivering after two good rounds: rank 1
+    times out, rank 0 then sees the poisoned flag — both raise P2PError from inside the probe."""
+
+    def __init__(self, comm):
+        self.comm, self.timeout_s, self.timeouts, self.calls, self.closed = comm, 600.0, [], 0, False
+
+    def set_timeout(self, s):
+        self.timeout_s = s
+        self.timeouts.append(s)
+
+    def all_reduce(self, t, checked=True):
+        from avenir_amd.parallel.p2p import P2PError
+        self.calls += 1
+        if self.calls > 2:
+            raise P2PError(f"rank {self.comm.rank}: injected")
+        return self.comm.all_reduce(t, algo="ring")
+
+    def close(self):
+        self.comm.barrier()
+        self.closed = True
+
+
+def _probe_fails(rank, world):
+    from avenir_amd.parallel import comm as C
+    c = C.get_comm()
+    fake = _FailingP2P(c)
+    c._p2p = fake
+    c.small_allreduce = "auto"
+    choice = c._auto_small_allreduce(torch.zeros(16, dtype=torch.int64))
+    x = torch.full((8,), rank + 1, dtype=torch.int64)
+    c.all_reduce(x)                                 # later small sums: the library collective
+    return (choice, c.small_allreduce, c._p2p, fake.closed, fake.timeouts[0], c.small_allreduce_probe["chosen"],
+            x.tolist())
+
+
+def test_probe_failure_retires_the_kernel_on_every_rank():
+    """A peer mapping that stops delivering fails the selection probe under its short wait bound
+    (not the job's 600 s one); exactness is agreed before the timing rounds, so the ranks stay in
+    step, close the kernel state together and take the library collective from then on."""
+    from avenir_amd.parallel import comm as C
+    for got in run_world(_probe_fails, 2):
+        assert got == (None, None, False, True, C._PROBE_TIMEOUT_S, "library", [3] * 8)
+
+
 def _p2p_unavailable(rank, world):
     from avenir_amd import _native
     from avenir_amd.parallel import comm as C
