@@ -1004,7 +1004,7 @@ void forest_predict_bin(const at::Tensor& codes, int64_t n, const at::Tensor& no
 // distance / kNN / clustering (K9/K11)
 // ---------------------------------------------------------------------------------------------
 py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t q_base, int64_t r_base,
-                   bool exclude_self, int64_t splits, int64_t metric, double p) {
+                   bool exclude_self, int64_t splits, int64_t metric, double p, int64_t prec) {
   CHECK_DEV(Q);
   CHECK_DTYPE(Q, at::kFloat);
   CHECK_DEV(R);
@@ -1023,7 +1023,7 @@ py::tuple knn_topk(const at::Tensor& Q, const at::Tensor& R, int64_t k, int64_t 
   DevGuard g(Q.device());
   avk::knn_topk(Q.data_ptr<float>(), M, R.data_ptr<float>(), N, (int)D, (int)k, q_base, r_base,
                 exclude_self ? 1 : 0, od.data_ptr<float>(), reinterpret_cast<long long*>(oi.data_ptr<int64_t>()),
-                (int)splits, (int)metric, (float)p, cur_stream(Q));
+                (int)splits, (int)metric, (float)p, cur_stream(Q), (int)prec);
   return py::make_tuple(od, oi, splits);
 }
 
@@ -3819,7 +3819,7 @@ at::Tensor embed_layernorm(const at::Tensor& ids, const c10::optional<at::Tensor
 }
 
 // C [M, N] = A^T B for A [K, M], B [K, N] fp32 (gemm.hip: split-K f32 MFMA + ordered slice sum)
-at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B) {
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, int64_t prec) {
   CHECK_DEV(A);
   CHECK_DTYPE(A, at::kFloat);
   CHECK_DEV(B);
@@ -3834,7 +3834,7 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B) {
   const int S = avk::gemm_tn_slices(K, M, N);
   auto part = at::empty({(int64_t)S * M * N}, A.options());
   avk::gemm_tn(A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(), part.data_ptr<float>(), K, M, N, S,
-               cur_stream(A));
+               cur_stream(A), (int)prec);
   return C;
 }
 
@@ -4030,7 +4030,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbt_assign", &gbt_assign);
   m.def("tree_assign", &tree_assign);
   m.def("tree_predict", &tree_predict);
-  m.def("knn_topk", &knn_topk);
+  m.def("knn_topk", &knn_topk, py::arg("Q"), py::arg("R"), py::arg("k"), py::arg("q_base"), py::arg("r_base"),
+        py::arg("exclude_self"), py::arg("splits"), py::arg("metric"), py::arg("p"), py::arg("prec") = -1);
+  m.def("knn_mode", &avk::knn_mode);
   m.def("knn_vote", &knn_vote);
   m.def("cluster_accumulate", &cluster_accumulate);
   m.def("viterbi", &viterbi);
@@ -4125,7 +4127,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("H"), py::arg("training"), py::arg("x") = py::none(), py::arg("wxfrag") = py::none(),
         py::arg("biask") = py::none());
   m.def("lstm_pack_f32", &lstm_pack_f32);
-  m.def("gemm_tn", &gemm_tn);
+  m.def("gemm_tn", &gemm_tn, py::arg("A"), py::arg("B"), py::arg("prec") = -1);
+  m.def("gemm_tn_mode", &avk::gemm_tn_mode);
   m.def("add_layernorm", &add_layernorm);
   m.def("linear_add_layernorm", &linear_add_layernorm, py::arg("X"), py::arg("W"), py::arg("b"), py::arg("res"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("prec") = -1);

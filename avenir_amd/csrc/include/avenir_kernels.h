@@ -67,7 +67,9 @@ void tree_predict(const uint8_t* codes, long long ld, long long n, const int* fe
 // ---- distance.hip (K9/K11) -----------------------------------------------------------------
 void knn_topk(const float* Q, long long M, const float* R, long long N, int D, int k,
               long long q_index_base, long long r_index_base, int exclude_self, float* out_d,
-              long long* out_i, int splits, int metric, float p, hipStream_t stream);
+              long long* out_i, int splits, int metric, float p, hipStream_t stream, int prec = -1);
+// squared-euclidean dot products: 0 fp32 MFMA, 3 / 6 split-bf16 (AVMI_KNN_MFMA; default bf16x6)
+int knn_mode();
 void knn_vote(const float* dist, const long long* idx, long long M, int k, const long long* ys,
               const float* post, int post_mode, int C, int kern, float kparam, float scale, float kscale,
               int invdist, float thr, int pos, float* scores, float* prob, long long* pred, hipStream_t stream);
@@ -209,7 +211,11 @@ void embed_layernorm(const long long* ids, const long long* tt, const float* wor
 
 // ---- gemm.hip: split-K fp32 A^T B (weight gradients over a long row dimension) ---------------
 int gemm_tn_slices(int K, int M, int N);
-void gemm_tn(const float* A, const float* B, float* C, float* partial, int K, int M, int N, int S, hipStream_t stream);
+// prec: -1 the process default (gemm_tn_mode(): AVMI_GEMM_TN, else f32_gemm_mode()), 0 fp32 MFMA,
+// 3 split-bf16 x3, 6 split-bf16 x6 (avenir_sbf16.h)
+void gemm_tn(const float* A, const float* B, float* C, float* partial, int K, int M, int N, int S, hipStream_t stream,
+             int prec = -1);
+int gemm_tn_mode();
 
 // ---- rnn_f32.hip (K27 fp32) ------------------------------------------------------------------
 void lstm_fwd_f32(const float* xw, const float* x, const float* wxfrag, const float* biask, const float* wfrag,

@@ -20,6 +20,7 @@
 #include "avenir_common.h"
 #include <cmath>
 #include "avenir_kernels.h"
+#include "avenir_sbf16.h"
 
 namespace {
 
@@ -46,6 +47,34 @@ __device__ __forceinline__ f32x16 mfma_chunk(const float* __restrict__ qrow, con
   return acc;
 }
 
+// the same chunk on the bf16 matrix cores (avenir_sbf16.h): each lane splits its 8 consecutive
+// features of the reference row (A) and of the query row (B) into NS bf16 terms per 16 k — the
+// fp32 LDS image (and the norms read from it) is unchanged
+template <int N, int NS>
+__device__ __forceinline__ f32x16 mfma_chunk_sb(const float* __restrict__ rrow, const float* __restrict__ qrow, int lh,
+                                                f32x16 acc) {
+#pragma unroll
+  for (int k = 0; k < N; k += 16) {
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = rrow[k + lh + j];
+      b[j] = qrow[k + lh + j];
+    }
+    sbf::u32x4 ta[NS], tb[NS];
+    sbf::split8<NS>(a, ta);
+    sbf::split8<NS>(b, tb);
+    sbf::bf16x8 fa[NS], fb[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      fa[t] = sbf::frag(ta[t]);
+      fb[t] = sbf::frag(tb[t]);
+    }
+    sbf::mfma32_terms<NS>(fa, fb, acc);
+  }
+  return acc;
+}
+
 template <int K>
 __device__ __forceinline__ void topk_insert(float (&bd)[K], int (&bi)[K], float d, int j) {
   if (d < bd[K - 1]) {
@@ -67,10 +96,11 @@ __device__ __forceinline__ void topk_insert(float (&bd)[K], int (&bi)[K], float 
 // lists.  qstride = the query rows' LDS stride in floats (padded by one against bank conflicts).
 constexpr int QRES = 256;
 __host__ __device__ inline int knn_qstride(int D) { return (D <= QRES ? ((D + KC - 1) / KC) * KC : KC) + 1; }
-// the distance tile sD exists only for the VALU metrics (MET != 0 scans it for the top-k)
+// the distance tile sD exists only for the VALU metrics (MET 1 / 2 scan it for the top-k)
 __host__ __device__ inline int knn_off_sr(int qs) { return BQ * qs * 4; }
 __host__ __device__ inline int knn_off_sd(int qs) { return knn_off_sr(qs) + BR * (KC + 1) * 4; }
-__host__ __device__ inline int knn_off_qn(int qs, int met) { return knn_off_sd(qs) + (met ? BQ * (BR + 1) * 4 : 0); }
+__host__ __device__ inline bool knn_valu(int met) { return met == 1 || met == 2; }
+__host__ __device__ inline int knn_off_qn(int qs, int met) { return knn_off_sd(qs) + (knn_valu(met) ? BQ * (BR + 1) * 4 : 0); }
 __host__ __device__ inline int knn_off_rn(int qs, int met) { return knn_off_qn(qs, met) + BQ * 4; }
 __host__ __device__ inline int knn_lds_bytes(int K, int D, int met) {
   const int main = knn_off_rn(knn_qstride(D), met) + BR * 4;
@@ -78,7 +108,8 @@ __host__ __device__ inline int knn_lds_bytes(int K, int D, int met) {
 }
 
 // MET: 0 = squared euclidean on MFMA (||q||^2 + ||r||^2 - 2 q.r), 1 = L1 (VALU), 2 = sum |q - r|^p
-// (VALU; the caller takes the p-th root of the selected values — the order is the same).
+// (VALU; the caller takes the p-th root of the selected values — the order is the same), 3 / 4 =
+// squared euclidean with the dot products in split-bf16 x3 / x6 on the bf16 MFMA.
 template <int K, int MET>
 __global__ __launch_bounds__(KT) void knn_mfma_kernel(
     const float* __restrict__ Q, long long M, const float* __restrict__ R, long long N, int D,
@@ -94,6 +125,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   float(*mD)[4][K] = reinterpret_cast<float(*)[4][K]>(smem);
   int(*mI)[4][K] = reinterpret_cast<int(*)[4][K]>(smem + BQ * 4 * K * 4);
 
+  constexpr bool EU = MET == 0 || MET >= 3;  // squared euclidean on the matrix cores
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wq = wave >> 1, wr = wave & 1;
@@ -112,8 +144,8 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
   for (int s = 0; s < K; ++s) { bd[s] = INFINITY; bi[s] = -1; }
   // top-k owner of each (query, partial list): MET 0 takes candidates straight from the MFMA
   // accumulator (lane = one query column, 16 reference rows), the VALU metrics from the sD tile
-  const int my_q = MET == 0 ? (wq * 32 + (lane & 31)) : (tid >> 2);
-  const int part = MET == 0 ? (wr * 2 + (lane >> 5)) : (tid & 3);
+  const int my_q = EU ? (wq * 32 + (lane & 31)) : (tid >> 2);
+  const int part = EU ? (wr * 2 + (lane >> 5)) : (tid & 3);
 
   // A query block whose features fit one chunk is staged once; reference chunks are prefetched
   // into registers one step ahead (the global loads of the next chunk / tile are in flight during
@@ -164,7 +196,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
       __syncthreads();
       if (ci + 1 < nchunk) load_r(r0, d0 + KC);
       else if (r0 + BR < re) load_r(r0 + BR, 0);
-      if constexpr (MET == 0) {
+      if constexpr (EU) {
         // norms over a half or a whole chunk; the MFMA chain always covers the whole (zero-padded)
         // chunk: a second, half-length unrolled chain cost more in VGPRs / occupancy than the
         // skipped MFMAs saved (measured at D = 16 and 32)
@@ -178,7 +210,8 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         const int li = lane & 31, lk = lane >> 5;
         // A = references (rows of the 32 x 32 block), B = queries (columns): each lane's 16
         // accumulators are 16 reference distances of ONE query
-        acc = mfma_chunk<KC>(sR[wr * 32 + li], sQ + (wq * 32 + li) * qs + qo, lk, acc);
+        if constexpr (MET == 0) acc = mfma_chunk<KC>(sR[wr * 32 + li], sQ + (wq * 32 + li) * qs + qo, lk, acc);
+        else acc = mfma_chunk_sb<KC, MET == 3 ? 2 : 3>(sR[wr * 32 + li], sQ + (wq * 32 + li) * qs + qo, lk * 8, acc);
       } else {
         for (int c = 0; c < kend; ++c) {
           float qa[4], rv[4];
@@ -196,7 +229,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
         }
       }
     }
-    if constexpr (MET == 0) {
+    if constexpr (EU) {
       if (tid < BR) srn[tid] = rn_acc;
       else if (first_tile && tid < BR + BQ) sqn[tid - BR] = qn_acc;
       __syncthreads();
@@ -248,7 +281,7 @@ __global__ __launch_bounds__(KT) void knn_mfma_kernel(
           sD[qi][rj] = dist;
         }
     }
-    if constexpr (MET != 0) {
+    if constexpr (!EU) {
       __syncthreads();
 #pragma unroll 4
       for (int c = 0; c < 16; ++c) {
@@ -648,10 +681,19 @@ __global__ __launch_bounds__(256) void pairs_within_kernel(const float* __restri
 
 namespace avk {
 
+int knn_mode() {
+  static const int mode = sbf::env_mode("AVMI_KNN_MFMA", 6);
+  return mode;
+}
+
 void knn_topk(const float* Q, long long M, const float* R, long long N, int D, int k,
               long long q_index_base, long long r_index_base, int exclude_self, float* out_d,
-              long long* out_i, int splits, int metric, float p, hipStream_t stream) {
+              long long* out_i, int splits, int metric, float p, hipStream_t stream, int prec) {
   if (M <= 0 || N <= 0) return;
+  if (metric == 0) {  // squared euclidean: fp32 MFMA or the split-bf16 dot products
+    const int mode = prec >= 0 ? prec : knn_mode();
+    metric = mode == 3 ? 3 : mode == 6 ? 4 : 0;
+  }
   const long long per = ((N + splits - 1) / splits + BR - 1) / BR * BR;
   dim3 grid((unsigned)((M + BQ - 1) / BQ), (unsigned)splits);
   auto launch = [&](auto kern, int K) {
@@ -674,6 +716,8 @@ void knn_topk(const float* Q, long long M, const float* R, long long N, int D, i
   if (metric == 0) { AV_KNN_MET(0) }
   else if (metric == 1) { AV_KNN_MET(1) }
   else if (metric == 2) { AV_KNN_MET(2) }
+  else if (metric == 3) { AV_KNN_MET(3) }
+  else if (metric == 4) { AV_KNN_MET(4) }
   else throw std::runtime_error("knn_topk: unknown metric");
 #undef AV_KNN_MET
   AV_HIP_CHECK(hipGetLastError());

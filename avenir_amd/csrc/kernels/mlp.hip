@@ -289,13 +289,19 @@ __device__ __forceinline__ void split_store4(float4 v, unsigned short* const* ds
   }
 }
 
-template <int WB, int NS, bool SPLIT, int SKC>
-__global__ __launch_bounds__(MT) void linear_act_fwd_sbf16_kernel(const float* __restrict__ X,
+// SWZ: the term images unpadded, [rows][SKC] bf16, the 16-byte k-segment s of row r stored at
+// s ^ ((r / (128 / SKC)) & (SKC / 8 - 1)) — the 16 rows a 16-lane group reads still land on 16
+// disjoint 4-bank groups, and the x6 128 x 128 tile drops from 61,440 to 49,152 bytes of LDS, so three
+// workgroups fit a CU (with OCC = 3 waves / SIMD asked of the register allocator): 768 output tiles
+// (4,096 x 3,072 or 16,384 x 768 outputs) are then one round over 256 CUs instead of 1.5.
+template <int WB, int NS, bool SPLIT, int SKC, bool SWZ = false, int OCC = 1>
+__global__ __launch_bounds__(MT, OCC) void linear_act_fwd_sbf16_kernel(const float* __restrict__ X,
                                                                   const float* __restrict__ W,
                                                                   const float* __restrict__ b, float* __restrict__ Y,
                                                                   int M, int N, int K, int act, int kper, int xcd) {
   constexpr int TR = 64 * WB;        // tile rows = tile cols
-  constexpr int SROW = SKC + 8;      // LDS row (bf16): 80 or 144 bytes, conflict-free b128 reads
+  constexpr int SROW = SWZ ? SKC : SKC + 8;  // LDS row (bf16): swizzled, or 80 / 144 padded bytes
+  constexpr int RSH = SKC == 32 ? 2 : 1;     // rows per 256 bytes = 1 << RSH (swizzle period)
   constexpr int F4R = SKC / 4;       // float4 per row and chunk
   constexpr int PF = TR * F4R / MT;  // float4 of each operand per thread and chunk
   __shared__ __attribute__((aligned(16))) unsigned short sX[NS][TR][SROW];
@@ -341,7 +347,9 @@ __global__ __launch_bounds__(MT) void linear_act_fwd_sbf16_kernel(const float* _
     __syncthreads();  // the previous chunk's fragment reads are done
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
-      const int e = tid + MT * i, off = (e / F4R) * SROW + (e % F4R) * 4;
+      const int e = tid + MT * i, r = e / F4R, k4 = (e % F4R) * 4;
+      const int off = SWZ ? r * SROW + ((((k4 >> 3) ^ (r >> RSH)) & (SKC / 8 - 1)) << 3) + (k4 & 7)
+                          : r * SROW + k4;
       split_store4<NS>(px[i], dX, off);
       split_store4<NS>(pw[i], dW, off);
     }
@@ -350,12 +358,21 @@ __global__ __launch_bounds__(MT) void linear_act_fwd_sbf16_kernel(const float* _
 #pragma unroll
     for (int ks = 0; ks < SKC; ks += 16) {
       bf16x8 a[NS][WB], w[NS][WB];
+      auto col = [&](int r) __attribute__((always_inline)) {
+        return SWZ ? ((((ks + lh) >> 3) ^ (r >> RSH)) & (SKC / 8 - 1)) << 3 : ks + lh;
+      };
 #pragma unroll
       for (int t = 0; t < NS; ++t) {
 #pragma unroll
-        for (int i = 0; i < WB; ++i) a[t][i] = *reinterpret_cast<const bf16x8*>(&sX[t][wm * 32 * WB + 32 * i + li][ks + lh]);
+        for (int i = 0; i < WB; ++i) {
+          const int r = wm * 32 * WB + 32 * i + li;
+          a[t][i] = *reinterpret_cast<const bf16x8*>(&sX[t][r][col(r)]);
+        }
 #pragma unroll
-        for (int j = 0; j < WB; ++j) w[t][j] = *reinterpret_cast<const bf16x8*>(&sW[t][wn * 32 * WB + 32 * j + li][ks + lh]);
+        for (int j = 0; j < WB; ++j) {
+          const int r = wn * 32 * WB + 32 * j + li;
+          w[t][j] = *reinterpret_cast<const bf16x8*>(&sW[t][r][col(r)]);
+        }
       }
       // term orders, smallest first: (order 2: x2w0, x1w1, x0w2), (order 1: x1w0, x0w1), (order 0)
 #pragma unroll
@@ -610,6 +627,15 @@ int f32_gemm_mode() {
 // K chunk of the split-bf16 tiles (AVMI_SBF16_KC = 32 | 64 overrides): x3 64 (a few % faster at
 // the large shapes), x6 32 (at 64 its 128 x 128 tile drops to one wave per SIMD: up to 20 % slower;
 // profiles/r6_gemm_bf16x*_kc*.jsonl)
+// the swizzled three-per-CU x6 tile (AVMI_SBF16_SWZ = 0 turns it off)
+static bool sbf16_swz() {
+  static const bool on = [] {
+    const char* e = std::getenv("AVMI_SBF16_SWZ");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 static int sbf16_kc(int mode) {
   static const int kc = [] {
     const char* e = std::getenv("AVMI_SBF16_KC");
@@ -670,6 +696,8 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
     dim3 gb((unsigned)((N + TB - 1) / TB), (unsigned)((M + TB - 1) / TB));
     const int xcd = xcd_tiles_enabled() && gb.x * gb.y >= 64 ? 1 : 0;
     if (mode == 3) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<2, 2, false, 32><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<2, 2, false, 64><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
+    else if (mode == 6 && sbf16_kc(mode) == 32 && sbf16_swz())
+      linear_act_fwd_sbf16_kernel<2, 3, false, 32, true, 3><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
     else if (mode == 6) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<2, 3, false, 32><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<2, 3, false, 64><<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
     else linear_act_fwd_big_kernel<<<gb, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, xcd);
     AV_HIP_CHECK(hipGetLastError());

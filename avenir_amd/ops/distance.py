@@ -47,11 +47,13 @@ def _cpu_topk(Q, R, k, metric, p, exclude_self, q_base, r_base, chunk=4096):
 
 @traced("knn", flops=lambda Q, R, *a, **k: 2.0 * Q.shape[0] * R.shape[0] * Q.shape[1], device=lambda Q, *a, **k: Q.device)
 def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: float = 2.0,
-        exclude_self: bool = False, q_base: int = 0, r_base: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+        exclude_self: bool = False, q_base: int = 0, r_base: int = 0, prec: int = -1) -> tuple[torch.Tensor, torch.Tensor]:
     """k nearest references of every query: (dist float32 [M, k] ascending, idx int64 [M, k]);
     idx = -1 / dist = inf when fewer than k candidates.  ``sqeuclidean`` returns squared distances,
     ``cosine`` returns 1 - cos.  On the GPU every metric with k <= 64 runs the fused distance +
-    top-k kernel (K9); larger k use chunked device distance blocks + ``torch.topk``."""
+    top-k kernel (K9); larger k use chunked device distance blocks + ``torch.topk``.  ``prec``
+    (euclidean family on the GPU): -1 the process default (``AVMI_KNN_MFMA``, bf16x6), 0 fp32 MFMA,
+    3 / 6 split-bf16 x3 / x6 dot products."""
     Q = Q.float().contiguous()
     R = R.float().contiguous()
     if metric == "minkowski" and p == 2.0:
@@ -65,7 +67,7 @@ def knn(Q: torch.Tensor, R: torch.Tensor, k: int, metric: str = "euclidean", p: 
             Q = torch.nn.functional.normalize(Q, dim=1)
             R = torch.nn.functional.normalize(R, dim=1)
         d, i, splits = _native.C().knn_topk(Q, R, int(k), int(q_base), int(r_base), bool(exclude_self), 0,
-                                            kmet, float(p))
+                                            kmet, float(p), int(prec))
         if splits > 1:  # merge the per-split top-k slabs [S, M, k] -> [M, k]
             d = d.permute(1, 0, 2).reshape(Q.shape[0], -1)
             i = i.permute(1, 0, 2).reshape(Q.shape[0], -1)

@@ -147,6 +147,23 @@ def test_knn_mfma_gpu(cuda, M, N, Dm, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", [0, 3, 6])
+@pytest.mark.parametrize("M,N,Dm,k", [(1000, 5000, 16, 5), (513, 1000, 70, 32), (257, 2000, 200, 10),
+                                       (100, 1500, 300, 5)])
+def test_knn_every_mode_gpu(cuda, M, N, Dm, k, prec):
+    """The squared-euclidean dot products on fp32 MFMA (0) and on split-bf16 x3 / x6 (3 / 6)
+    against the fp64 oracle at the same tolerances."""
+    g = torch.Generator().manual_seed(M + prec)
+    Q, R = torch.randn(M, Dm, generator=g), torch.randn(N, Dm, generator=g)
+    d, i = D.knn(Q.to(cuda), R.to(cuda), k, prec=prec)
+    bd, bi = _brute(Q, R, k)
+    assert torch.allclose(d.cpu(), bd, atol=2e-3, rtol=1e-4)
+    assert float((i.cpu() == bi).float().mean()) > 0.995
+    d2, i2 = D.knn(R[:300].to(cuda), R.to(cuda), 4, exclude_self=True, prec=prec)
+    assert not bool((i2.cpu() == torch.arange(300).view(-1, 1)).any())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("metric,p,k", [("manhattan", 1.0, 5), ("minkowski", 3.0, 7), ("euclidean", 2.0, 50),
                                         ("manhattan", 1.0, 64), ("minkowski", 1.5, 1), ("cosine", 2.0, 40)])
 def test_knn_metrics_and_large_k_gpu(cuda, metric, p, k):

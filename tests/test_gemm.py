@@ -21,6 +21,19 @@ def test_gemm_tn_vs_fp64(cuda, K, M, N):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", [0, 3, 6])
+@pytest.mark.parametrize("K,M,N", [(5000, 400, 106), (777, 33, 65), (100_000, 64, 64), (31, 130, 70)])
+def test_gemm_tn_every_mode_vs_fp64(cuda, K, M, N, prec):
+    """fp32 MFMA (0) and the split-bf16 x3 / x6 paths (3 / 6) all within the fp32 tolerance."""
+    g = torch.Generator().manual_seed(K + M + N + prec)
+    A, B = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g)
+    C = _native.C().gemm_tn(A.to(cuda), B.to(cuda), prec=prec).cpu()
+    err = (C.double() - A.double().t() @ B.double()).abs().max().item()
+    assert err <= 1e-5 * (K ** 0.5) * 4, err
+    assert torch.equal(C, _native.C().gemm_tn(A.to(cuda), B.to(cuda), prec=prec).cpu())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(128, 768, 3072), (128, 2304, 768), (1, 3072, 768), (37, 200, 1000), (130, 130, 4099)])
 @pytest.mark.parametrize("act", [0, 1, 6])
 def test_linear_act_fwd_split_k_vs_fp64(cuda, M, N, K, act):
