@@ -178,6 +178,19 @@ def gemm_tn():
     torch.cuda.synchronize()
 
 
+def k27():
+    """mlp.hip linear_act_fwd (K27) at 4,096 x 3,072 x 768 + GELU, the BERT FFN-up shape at 32 x 128
+    tokens; the arithmetic mode from AVMI_F32_GEMM."""
+    from avenir_amd import _native
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = torch.randn((4096, 768), generator=g, device="cuda")
+    W = torch.randn((3072, 768), generator=g, device="cuda") / 768 ** 0.5
+    b = torch.randn(3072, generator=g, device="cuda")
+    for _ in range(6):
+        _native.C().linear_act_fwd(X, W, b, 6)
+    torch.cuda.synchronize()
+
+
 def bert():
     """transformer.hip add_layernorm / embed_layernorm and mlp.hip's GELU tile epilogue: 12 encoder
     passes of the bert-base shape at B 1 x S 128 (the query path of semantic search)."""
@@ -209,7 +222,7 @@ def svm_select():
 
 TARGETS = {"kmeans": kmeans, "fmt": fmt, "pairs": pairs, "split": split, "lstm": lstm, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
            "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest,
-           "gemm_tn": gemm_tn, "bert": bert, "svm_select": svm_select}
+           "gemm_tn": gemm_tn, "k27": k27, "bert": bert, "svm_select": svm_select}
 
 if __name__ == "__main__":
     TARGETS[sys.argv[1]]()
