@@ -210,10 +210,13 @@ class _DoublingComm:
     backend = "nccl"
     rank, world = 0, 2
 
-    def all_reduce(self, t, op="sum"):
+    def all_reduce(self, t, op="sum", checked=True):
         torch.cuda._sleep(2_000_000)          # a slow collective: exposes missing waits
         t.add_(t.clone())
         return t
+
+    def check(self, block=True):              # Comm's p2p status gate: nothing can fail here
+        pass
 
 
 @pytest.mark.gpu
