@@ -525,13 +525,19 @@ def _string_order(rec: Records, idx: torch.Tensor) -> torch.Tensor | None:
         b = torch.where(j < lens.view(-1, 1), vb[pos] if vb.numel() else torch.zeros_like(pos, dtype=torch.uint8),
                         torch.zeros((), dtype=torch.uint8, device=dev))
     else:
-        enc = [rec.vocab[i].encode() for i in idx.tolist()]
-        if enc and max(len(e) for e in enc) > W:
-            return None
         import numpy as np
+        voc = rec.vocab
+        enc = [voc[i].encode() for i in idx.tolist()]
+        ln = np.fromiter(map(len, enc), dtype=np.int64, count=len(enc))
+        if ln.size and int(ln.max()) > W:
+            return None
+        # one joined buffer scattered into the [n, W] byte matrix (no per-entry numpy call)
+        flat = np.frombuffer(b"".join(enc), dtype=np.uint8)
         arr = np.zeros((len(enc), W), dtype=np.uint8)
-        for r, e in enumerate(enc):
-            arr[r, : len(e)] = np.frombuffer(e, dtype=np.uint8)
+        if flat.size:
+            starts = np.cumsum(ln) - ln
+            row = np.repeat(np.arange(len(enc)), ln)
+            arr[row, np.arange(flat.size) - np.repeat(starts, ln)] = flat
         b = torch.from_numpy(arr).to(dev)
         lens = None
     words = _pack_words(b, lens)
