@@ -2182,9 +2182,30 @@ std::vector<at::Tensor> forest_bootstrap(const at::Tensor& codes, const at::Tens
   return {cb, lb, wb, per_tree};
 }
 
+// bf16 term-plane scratch of K27's large-shape split-bf16 path (undefined when not taken)
+static at::Tensor k27_planes(const at::Tensor& like, long long M, long long N, long long K, int64_t prec) {
+  const long long nb = avk::linear_act_fwd_planes_bytes((int)M, (int)N, (int)K, (int)prec);
+  return nb > 0 ? at::empty({nb}, like.options().dtype(at::kByte)) : at::Tensor();
+}
+static void* ptr_or_null_t(const at::Tensor& t) { return t.defined() ? t.data_ptr() : nullptr; }
+
 // K27: Y = act(X W^T + b) and its backward epilogue (dZ = dY * act'(Y), db = colsum dZ).
+// W's bf16 term planes for linear_act_fwd(..., w_planes=) (None when the planes path is off for prec)
+py::object sbf16_weight_planes(const at::Tensor& W, int64_t prec) {
+  CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
+  TORCH_CHECK(W.dim() == 2 && W.size(0) < (1LL << 31) && W.size(1) < (1LL << 31), "W [N, K]");
+  TORCH_CHECK(prec == -1 || prec == 0 || prec == 3 || prec == 6, "prec: -1 (default), 0, 3 or 6");
+  const long long nb = avk::sbf16_weight_planes_bytes((int)W.size(0), (int)W.size(1), (int)prec);
+  if (nb == 0) return py::none();
+  auto Wc = W.contiguous();
+  auto out = at::empty({nb}, W.options().dtype(at::kByte));
+  DevGuard g(W.device());
+  avk::sbf16_weight_planes(Wc.data_ptr<float>(), (int)W.size(0), (int)W.size(1), (int)prec, out.data_ptr(), cur_stream(W));
+  return py::cast(out);
+}
+
 at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b, int64_t act,
-                          int64_t prec) {
+                          int64_t prec, const c10::optional<at::Tensor>& w_planes) {
   TORCH_CHECK(prec == -1 || prec == 0 || prec == 3 || prec == 6, "prec: -1 (default), 0 (f32), 3 or 6 (split bf16)");
   CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
   CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
@@ -2202,11 +2223,20 @@ at::Tensor linear_act_fwd(const at::Tensor& X, const at::Tensor& W, const c10::o
   DevGuard g(X.device());
   const int M = (int)X.size(0), N = (int)W.size(0), K = (int)X.size(1);
   const int S = avk::linear_act_fwd_slices(M, N, K);
-  at::Tensor part;
+  at::Tensor part, planes;
   if (S > 1) part = at::empty({(long long)S * M * N}, X.options());
+  else planes = k27_planes(X, M, N, K, prec);
+  const void* wp = nullptr;
+  if (w_planes.has_value() && w_planes->defined()) {
+    CHECK_DEV((*w_planes));
+    TORCH_CHECK(w_planes->scalar_type() == at::kByte && w_planes->is_contiguous() &&
+                    w_planes->numel() == avk::sbf16_weight_planes_bytes(N, K, (int)prec),
+                "w_planes: sbf16_weight_planes(W, prec) of this W and prec");
+    wp = w_planes->data_ptr();
+  }
   avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), bc.defined() ? bc.data_ptr<float>() : nullptr,
                       Y.data_ptr<float>(), M, N, K, (int)act, cur_stream(X), S > 1 ? part.data_ptr<float>() : nullptr, S,
-                      (int)prec);
+                      (int)prec, ptr_or_null_t(planes), wp);
   return Y;
 }
 
@@ -2262,7 +2292,9 @@ py::tuple linear_act_backward(const at::Tensor& dY, const at::Tensor& Y, const a
   if (!need_dx) return py::make_tuple(py::none(), dW, db);
   auto Wt = W.t().contiguous();  // [K, N]
   auto dX = at::empty({M, K}, X.options());
-  avk::linear_act_fwd(dZ.data_ptr<float>(), Wt.data_ptr<float>(), nullptr, dX.data_ptr<float>(), M, K, N, 0, st);
+  auto planes = k27_planes(X, M, K, N, -1);
+  avk::linear_act_fwd(dZ.data_ptr<float>(), Wt.data_ptr<float>(), nullptr, dX.data_ptr<float>(), M, K, N, 0, st,
+                      nullptr, 1, -1, ptr_or_null_t(planes));
   return py::make_tuple(dX, dW, db);
 }
 
@@ -3719,7 +3751,7 @@ at::Tensor add_layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& r
 // and LayerNorm run in ONE pass over the partials (no [M, N] projection output, no epilogue launch).
 at::Tensor linear_add_layernorm(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& b,
                                 const at::Tensor& res, const at::Tensor& gamma, const at::Tensor& beta, double eps,
-                                int64_t prec) {
+                                int64_t prec, const c10::optional<at::Tensor>& w_planes) {
   TORCH_CHECK(prec == -1 || prec == 0 || prec == 3 || prec == 6, "prec: -1 (default), 0 (f32), 3 or 6 (split bf16)");
   CHECK_DEV(X); CHECK_DTYPE(X, at::kFloat);
   CHECK_DEV(W); CHECK_DTYPE(W, at::kFloat);
@@ -3747,8 +3779,17 @@ at::Tensor linear_add_layernorm(const at::Tensor& X, const at::Tensor& W, const 
                               (float)eps, cur_stream(X));
   } else {
     auto y = at::empty({M, N}, X.options());
+    auto planes = k27_planes(X, M, N, K, prec);
+    const void* wp = nullptr;
+    if (w_planes.has_value() && w_planes->defined()) {
+      CHECK_DEV((*w_planes));
+      TORCH_CHECK(w_planes->scalar_type() == at::kByte && w_planes->is_contiguous() &&
+                      w_planes->numel() == avk::sbf16_weight_planes_bytes((int)N, (int)K, (int)prec),
+                  "w_planes: sbf16_weight_planes(W, prec) of this W and prec");
+      wp = w_planes->data_ptr();
+    }
     avk::linear_act_fwd(Xc.data_ptr<float>(), Wc.data_ptr<float>(), ptr_or_null<float>(b), y.data_ptr<float>(),
-                        (int)M, (int)N, (int)K, 0, cur_stream(X), nullptr, 1, (int)prec);
+                        (int)M, (int)N, (int)K, 0, cur_stream(X), nullptr, 1, (int)prec, ptr_or_null_t(planes), wp);
     avk::add_layernorm(y.data_ptr<float>(), res.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                        out.data_ptr<float>(), M, (int)N, (float)eps, cur_stream(X));
   }
@@ -4116,7 +4157,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("csv_parse_device", &csv_parse_device);
   m.def("forest_predict_bin", &forest_predict_bin);
   m.def("linear_act_fwd", &linear_act_fwd, py::arg("X"), py::arg("W"), py::arg("b") = py::none(), py::arg("act") = 0,
-        py::arg("prec") = -1);
+        py::arg("prec") = -1, py::arg("w_planes") = py::none());
+  m.def("sbf16_weight_planes", &sbf16_weight_planes, py::arg("W"), py::arg("prec") = -1);
+  m.def("linear_act_fwd_planes_bytes", [](int64_t M, int64_t N, int64_t K, int64_t prec) {
+    return avk::linear_act_fwd_planes_bytes((int)M, (int)N, (int)K, (int)prec); },
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("prec") = -1);
   m.def("f32_gemm_mode", &avk::f32_gemm_mode);
   m.def("linear_act_bwd", &linear_act_bwd);
   m.def("linear_act_backward", &linear_act_backward);
@@ -4131,7 +4176,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn_mode", &avk::gemm_tn_mode);
   m.def("add_layernorm", &add_layernorm);
   m.def("linear_add_layernorm", &linear_add_layernorm, py::arg("X"), py::arg("W"), py::arg("b"), py::arg("res"),
-        py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("prec") = -1);
+        py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("prec") = -1, py::arg("w_planes") = py::none());
   m.def("attention_f32", &attention_f32);
   m.def("embed_layernorm", &embed_layernorm, py::arg("ids"), py::arg("tt"), py::arg("word"), py::arg("pos"),
         py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("validate") = true);

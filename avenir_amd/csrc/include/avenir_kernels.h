@@ -276,8 +276,16 @@ int f32_gemm_mode();
 // the raw split-K partial products [S_eff][M][N] of X W^T (no bias / activation); returns S_eff
 int linear_splitk_partial(const float* X, const float* W, float* partial, int M, int N, int K, int S,
                           hipStream_t stream, int prec = -1);
+// bytes of bf16 term-plane scratch the large-shape split-bf16 path of linear_act_fwd takes (its
+// `planes` argument); 0 when that path is not taken for this shape / mode (AVMI_SBF16_PLANES=0: never)
+long long linear_act_fwd_planes_bytes(int M, int N, int K, int prec = -1);
+// bf16 term planes of a weight W [N, K] in the planes path's layout (reusable for any X while W and
+// the mode are unchanged: linear_act_fwd's w_planes skips W's split); 0 bytes = path off for prec
+long long sbf16_weight_planes_bytes(int N, int K, int prec = -1);
+void sbf16_weight_planes(const float* W, int N, int K, int prec, void* out, hipStream_t stream);
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
-                    hipStream_t stream, float* partial = nullptr, int S = 1, int prec = -1);
+                    hipStream_t stream, float* partial = nullptr, int S = 1, int prec = -1, void* planes = nullptr,
+                    const void* w_planes = nullptr);
 int linear_act_bwd_blocks(int M);
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream);

@@ -574,6 +574,185 @@ __global__ __launch_bounds__(64 * RG) void slice_sum_kernel(const float* __restr
   }
 }
 
+// ---- pre-split ("planes") path of the split-bf16 tiles at large shapes ------------------------
+// The in-loop split of linear_act_fwd_sbf16_kernel spends ~1.1k VALU cycles per wave and K chunk
+// and a register-staged, single-buffered chunk that exposes the L2 / MALL latency: at 4,096 x 3,072
+// x 768 (x6) its MFMA pipes are busy 34 % of the kernel (profiles/r6_k27_pmc_4096x3072x768.jsonl).
+// Here one streaming pass writes each operand as NS bf16 term planes, and the GEMM tile reads them
+// through a 3-stage LDS ring filled by global_load_lds_dwordx4 (no VGPR staging, no VALU in the K
+// loop): stage t + 2 is in flight while stage t feeds the MFMAs, one counted vmcnt and one barrier
+// per 32-deep K step.  Plane layout [t][Rp / 16][Kp / 32][16][32] (rows zero-padded to Rp, a
+// multiple of 128, K to Kp, a multiple of 32): each 16-row x 32-k block is one contiguous KiB, so a
+// DMA wave-instruction reads 8 whole 128-byte lines (row-major planes cost 16 half-used lines per
+// instruction, the other halves re-fetched a stage later: 204 vs 147 us for the in-loop split tile
+// at 4,096 x 3,072 x 768).
+
+// in [R][K] fp32 -> out planes (layout above, blocks of RPB = 512 / BK rows x BK k); one thread per
+// 8 k of one row, a wave per 1-KiB block
+template <int NS, int BK>
+__global__ __launch_bounds__(256) void sbf16_split_rows_kernel(const float* __restrict__ in,
+                                                               unsigned short* __restrict__ out, long long R, int K,
+                                                               long long Rp, int Kp, bool vec) {
+  // grid (Rp / RPB, ceil(kb / 4)): wave w of a workgroup writes block (blockIdx.x, 4 blockIdx.y + w)
+  constexpr int SEGS = BK / 8, RPB = 512 / BK;
+  const int kb = Kp / BK, lane = threadIdx.x & 63;
+  const int kc = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (kc >= kb) return;
+  const int seg = lane % SEGS, rr = lane / SEGS;
+  const long long blk = (long long)blockIdx.x * kb + kc;
+  const long long r = (long long)blockIdx.x * RPB + rr;
+  const int k = kc * BK + seg * 8;
+  float v[8];
+  if (r >= R) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  } else {
+    const float* src = in + r * K + k;
+    if (vec && k + 8 <= K) {
+      const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = k + j < K ? src[j] : 0.f;
+    }
+  }
+  const long long plane = Rp * (long long)Kp;
+  unsigned short* dst = out + blk * 512 + rr * BK + seg * 8;
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    uint4 u;
+    u.x = pack_bf16(v[0], v[1]); u.y = pack_bf16(v[2], v[3]);
+    u.z = pack_bf16(v[4], v[5]); u.w = pack_bf16(v[6], v[7]);
+    *reinterpret_cast<uint4*>(dst + t * plane) = u;
+    if (t + 1 < NS) {
+      v[0] -= bf16_lo(u.x); v[1] -= bf16_hi(u.x); v[2] -= bf16_lo(u.y); v[3] -= bf16_hi(u.y);
+      v[4] -= bf16_lo(u.z); v[5] -= bf16_hi(u.z); v[6] -= bf16_lo(u.w); v[7] -= bf16_hi(u.w);
+    }
+  }
+}
+
+// 16-byte k-segment swizzle of a tile row in LDS (conflict-free ds_read_b128 of 16 rows per lane
+// group): 4 segments per row (BK 32) -> seg ^ ((row >> 2) & 3); 2 (BK 16) -> seg ^ ((row >> 3) & 1)
+template <int BK>
+__device__ __forceinline__ int seg_swz(int row, int seg) {
+  if constexpr (BK == 32) return seg ^ ((row >> 2) & 3);
+  else return seg ^ ((row >> 3) & 1);
+}
+
+// 128 x 128 output tile, 4 waves as 2 x 2, each 64 x 64 (2 x 2 v_mfma_f32_32x32x16_bf16 blocks).
+// LDS stage = 2 NS plane tiles (X terms, then W terms) of [128 rows][BK bf16], the k-segments of a
+// row swizzled (seg_swz).  LDS-DMA writes lane-linearly (1 KiB = one plane block per
+// wave-instruction), so the swizzle goes on the SOURCE address: lane i of an instruction fetches
+// row i / SEGS, segment seg_swz(row, i % SEGS) of its block.  NST-stage ring: BK 32 (48 KiB stages
+// at x6) fits one workgroup per CU, BK 16 two (x6) or three (x3).  All LDS is one __shared__ array
+// and the K loop has no VGPR-destination global load, so the compiler's waits stay the counted
+// ones written here.  ABL (A/B of the pipeline's parts): 1 drops the MFMAs, 2 the K loop's DMA.
+template <int NS, int BK, int NST, int ABL = 0>
+__global__ __launch_bounds__(MT) void linear_act_fwd_planes_kernel(const unsigned short* __restrict__ Xp,
+                                                                   const unsigned short* __restrict__ Wp,
+                                                                   const float* __restrict__ b, float* __restrict__ Y,
+                                                                   int M, int N, int Kp, int act, int xcd) {
+  constexpr int TR = 128, SEGS = BK / 8, RPB = 512 / BK, PLANE = TR * BK * 2, STAGE = 2 * NS * PLANE;
+  constexpr int PER_WAVE = 2 * NS * (TR / RPB) / 4;  // LDS-DMA instructions per wave and stage
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm = blockIdx.y, tn = blockIdx.x;
+  if (xcd) av::grouped_tile(av::xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y), gridDim.y,
+                            gridDim.x, 8, tm, tn);
+  const long long m0 = (long long)tm * TR;
+  const int n0 = tn * TR;
+  const long long kb = Kp / BK;
+  const long long xplane = (long long)gridDim.y * TR * Kp, wplane = (long long)gridDim.x * TR * Kp;
+  // this lane's source in its block for each of the wave's DMA instructions (+ 512 per stage)
+  const int lrow = lane / SEGS, lseg = seg_swz<BK>(lrow, lane % SEGS);
+  const unsigned short* src[PER_WAVE];
+  int dst[PER_WAVE];
+#pragma unroll
+  for (int q = 0; q < PER_WAVE; ++q) {
+    const int j = wave + 4 * q, pt = j / (TR / RPB), rb = j % (TR / RPB);
+    if (pt < NS) src[q] = Xp + pt * xplane + ((m0 / RPB + rb) * kb) * 512 + lrow * BK + lseg * 8;
+    else src[q] = Wp + (pt - NS) * wplane + ((n0 / RPB + rb) * kb) * 512 + lrow * BK + lseg * 8;
+    dst[q] = pt * PLANE + rb * 1024;
+  }
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    unsigned char* base = lds + (t % NST) * STAGE;
+#pragma unroll
+    for (int q = 0; q < PER_WAVE; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(src[q] + (long long)t * 512),
+                                       (__attribute__((address_space(3))) void*)(base + dst[q]), 16, 0, 0);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int T = Kp / BK;
+  issue(0);
+  if (NST == 3 && T > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  const int li = lane & 31, lh = lane >> 5;
+  for (int t = 0; t < T; ++t) {
+    if (ABL != 2 && t + NST - 1 < T) issue(t + NST - 1);
+    const unsigned char* sb = lds + (t % NST) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 a[NS][2], w[NS][2];
+#pragma unroll
+      for (int p = 0; p < NS; ++p) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = wm * 64 + 32 * i + li;
+          a[p][i] = *reinterpret_cast<const bf16x8*>(sb + p * PLANE + (r * SEGS + seg_swz<BK>(r, ks * 2 + lh)) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = wn * 64 + 32 * j + li;
+          w[p][j] = *reinterpret_cast<const bf16x8*>(sb + (NS + p) * PLANE + (r * SEGS + seg_swz<BK>(r, ks * 2 + lh)) * 16);
+        }
+      }
+      // term orders, smallest first (as linear_act_fwd_sbf16_kernel)
+#pragma unroll
+      for (int ord = NS - 1; ord >= 0; --ord)
+#pragma unroll
+        for (int ta = ord; ta >= 0; --ta)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              if constexpr (ABL == 1) asm volatile("" ::"v"(a[ta][i]), "v"(w[ord - ta][j]));
+              else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ta][i], w[ord - ta][j], acc[i][j], 0, 0, 0);
+            }
+    }
+    // retire this wave's DMA of stage t + 1 (stage t + 2's stays in flight), then one barrier: after
+    // it every wave's stage t + 1 has landed and every wave is done reading stage t (re-filled at t + 1)
+    if (NST == 3 && t + 2 < T) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+    if (col >= N) continue;
+    const float bias = b ? b[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < M) Y[row * N + col] = act_fwd(acc[i][j][r] + bias, act);
+      }
+  }
+}
+
 }  // namespace
 
 namespace avk {
@@ -679,11 +858,115 @@ int linear_splitk_partial(const float* X, const float* W, float* partial, int M,
   return S;
 }
 
+// the pre-split planes path (AVMI_SBF16_PLANES=0 turns it off): split-bf16 modes, outputs of at
+// least 1,024 x 1,024 (where the 128 x 128 tiles are taken)
+static bool planes_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("AVMI_SBF16_PLANES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// fewest 128 x 128 output tiles that take the planes path (AVMI_PLANES_MIN_TILES, default 640: at
+// 768 tiles it beats the in-loop split tile by 4-26 % per call, at 512 and 192 it loses 10-30 %,
+// profiles/r6_k27_planes_*.jsonl)
+static long long planes_min_tiles() {
+  static const long long n = [] {
+    const char* e = std::getenv("AVMI_PLANES_MIN_TILES");
+    return e ? std::atoll(e) : 640LL;
+  }();
+  return n;
+}
+
+long long linear_act_fwd_planes_bytes(int M, int N, int K, int prec) {
+  const int mode = prec >= 0 ? prec : f32_gemm_mode();
+  if (mode == 0 || !planes_enabled() || M <= 0 || N <= 0 || K <= 0 || K > (1 << 20)) return 0;
+  const long long tiles = ((long long)M + 127) / 128 * (((long long)N + 127) / 128);
+  if (tiles < planes_min_tiles()) return 0;
+  const long long Kp = ((long long)K + 31) / 32 * 32;
+  const long long Mp = ((long long)M + 127) / 128 * 128, Np = ((long long)N + 127) / 128 * 128;
+  return (mode == 6 ? 3LL : 2LL) * (Mp + Np) * Kp * 2;
+}
+
+// K step of the planes tile (AVMI_PLANES_BK = 16 | 32, default 16)
+static int planes_bk() {
+  static const int bk = [] {
+    const char* e = std::getenv("AVMI_PLANES_BK");
+    return e && std::atoi(e) == 32 ? 32 : 16;
+  }();
+  return bk;
+}
+
+// LDS stages of the BK 16 ring (AVMI_PLANES_NST = 2 | 3, default 2)
+static int planes_nst() {
+  static const int n = [] {
+    const char* e = std::getenv("AVMI_PLANES_NST");
+    return e && std::atoi(e) == 3 ? 3 : 2;
+  }();
+  return n;
+}
+
+// the NS term planes of rows [R][K] (layout of the BK tile) into `out`
+template <int NS, int BK>
+static void split_rows(const float* A, int R, int K, void* out, hipStream_t stream) {
+  const int Kp = (K + 31) / 32 * 32;
+  const long long Rp = ((long long)R + 127) / 128 * 128;
+  const bool vec = K % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0;
+  const unsigned gk = (unsigned)((Kp / BK + 3) / 4);
+  sbf16_split_rows_kernel<NS, BK><<<dim3((unsigned)(Rp / (512 / BK)), gk), 256, 0, stream>>>(
+      A, static_cast<unsigned short*>(out), R, K, Rp, Kp, vec);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+template <int NS, int BK, int NST>
+static void linear_act_fwd_planes(const float* X, const float* W, const float* b, float* Y, int M, int N, int K,
+                                  int act, hipStream_t stream, void* planes, const void* w_planes) {
+  const int Kp = (K + 31) / 32 * 32;
+  const long long Mp = ((long long)M + 127) / 128 * 128;
+  unsigned short* Xp = static_cast<unsigned short*>(planes);
+  const unsigned short* Wp = static_cast<const unsigned short*>(w_planes);
+  split_rows<NS, BK>(X, M, K, Xp, stream);
+  if (Wp == nullptr) {
+    unsigned short* w = Xp + NS * Mp * Kp;
+    split_rows<NS, BK>(W, N, K, w, stream);
+    Wp = w;
+  }
+  dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
+  const int xcd = xcd_tiles_enabled() && grid.x * grid.y >= 64 ? 1 : 0;
+  static const int abl = [] { const char* e = std::getenv("AVMI_PLANES_ABL"); return e ? std::atoi(e) : 0; }();
+  if (abl == 1) linear_act_fwd_planes_kernel<NS, BK, NST, 1><<<grid, MT, 0, stream>>>(Xp, Wp, b, Y, M, N, Kp, act, xcd);
+  else if (abl == 2) linear_act_fwd_planes_kernel<NS, BK, NST, 2><<<grid, MT, 0, stream>>>(Xp, Wp, b, Y, M, N, Kp, act, xcd);
+  else linear_act_fwd_planes_kernel<NS, BK, NST><<<grid, MT, 0, stream>>>(Xp, Wp, b, Y, M, N, Kp, act, xcd);
+  AV_HIP_CHECK(hipGetLastError());
+}
+
+long long sbf16_weight_planes_bytes(int N, int K, int prec) {
+  const int mode = prec >= 0 ? prec : f32_gemm_mode();
+  if (mode == 0 || !planes_enabled() || N <= 0 || K <= 0 || K > (1 << 20)) return 0;
+  const long long Kp = ((long long)K + 31) / 32 * 32, Np = ((long long)N + 127) / 128 * 128;
+  return (mode == 6 ? 3LL : 2LL) * Np * Kp * 2;
+}
+
+void sbf16_weight_planes(const float* W, int N, int K, int prec, void* out, hipStream_t stream) {
+  if (sbf16_weight_planes_bytes(N, K, prec) == 0) return;
+  const bool x6 = (prec >= 0 ? prec : f32_gemm_mode()) == 6;
+  if (planes_bk() == 32) (x6 ? split_rows<3, 32> : split_rows<2, 32>)(W, N, K, out, stream);
+  else (x6 ? split_rows<3, 16> : split_rows<2, 16>)(W, N, K, out, stream);
+}
+
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
-                    hipStream_t stream, float* partial, int S, int prec) {
+                    hipStream_t stream, float* partial, int S, int prec, void* planes, const void* w_planes) {
   if (M <= 0 || N <= 0) return;
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
+  if (planes != nullptr && S <= 1 && linear_act_fwd_planes_bytes(M, N, K, prec) > 0) {
+    const bool x6 = (prec >= 0 ? prec : f32_gemm_mode()) == 6;
+    if (planes_bk() == 32) (x6 ? linear_act_fwd_planes<3, 32, 3> : linear_act_fwd_planes<2, 32, 3>)(X, W, b, Y, M, N, K, act, stream, planes, w_planes);
+    else if (planes_nst() == 3) (x6 ? linear_act_fwd_planes<3, 16, 3> : linear_act_fwd_planes<2, 16, 3>)(X, W, b, Y, M, N, K, act, stream, planes, w_planes);
+    else (x6 ? linear_act_fwd_planes<3, 16, 2> : linear_act_fwd_planes<2, 16, 2>)(X, W, b, Y, M, N, K, act, stream, planes, w_planes);
+    return;
+  }
   if (S > 1 && partial != nullptr) {
     S = linear_splitk_partial(X, W, partial, M, N, K, S, stream, prec);
     const long long MN = (long long)M * N;

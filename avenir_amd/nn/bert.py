@@ -141,6 +141,7 @@ class BertEncoder(torch.nn.Module):
         if strict and missing:
             raise KeyError(f"missing BERT parameters: {sorted(missing)[:5]} ...")
         self._qkv_cache.clear()
+        self.__dict__.pop("_planes_cache", None)
         return self
 
     @classmethod
@@ -181,9 +182,24 @@ class BertEncoder(torch.nn.Module):
     #: (fp32-level error), 0 = exact-f32 MFMA.  AVMI_BERT_GEMM = bf16x3 | bf16x6 | f32
     GEMM_PREC = {"bf16x3": 3, "bf16x6": 6, "f32": 0}[os.environ.get("AVMI_BERT_GEMM", "bf16x3")]
 
+    def _weight_planes(self, x2, W):
+        """W's cached bf16 term planes when this call takes mlp.hip's pre-split planes path (large
+        row counts): the weight is split once per (W, version, optimiser epoch), not per call."""
+        C = _native.C()
+        if C.linear_act_fwd_planes_bytes(x2.shape[0], W.shape[0], W.shape[1], self.GEMM_PREC) == 0:
+            return None
+        cache = self.__dict__.setdefault("_planes_cache", {})
+        key = (W._version, param_epoch())
+        hit = cache.get(id(W))
+        if hit is not None and hit[0] is W and hit[1] == key:
+            return hit[2]
+        p = C.sbf16_weight_planes(W.detach(), self.GEMM_PREC)
+        cache[id(W)] = (W, key, p)          # holds W: its id cannot be reused while cached
+        return p
+
     def _linear(self, x2, W, b, act: int = 0):
         if x2.is_cuda and x2.shape[0] <= self.MFMA_MAX_ROWS:
-            return _native.C().linear_act_fwd(x2, W, b, act, self.GEMM_PREC)
+            return _native.C().linear_act_fwd(x2, W, b, act, self.GEMM_PREC, self._weight_planes(x2, W))
         y = torch.nn.functional.linear(x2, W, b)
         return torch.nn.functional.gelu(y) if act == _GELU else y
 
@@ -204,6 +220,7 @@ class BertEncoder(torch.nn.Module):
 
     def _apply(self, fn, *a, **k):          # .to() / .cuda(): the Q/K/V cache holds the old storage
         self._qkv_cache.clear()
+        self.__dict__.pop("_planes_cache", None)
         return super()._apply(fn, *a, **k)
 
     def _linear_ln(self, x2, W, b, res, g, bb):
@@ -211,7 +228,8 @@ class BertEncoder(torch.nn.Module):
         N = W.shape[0]
         if x2.is_cuda and x2.shape[0] <= self.MFMA_MAX_ROWS and N <= 1024 and N % 4 == 0:
             return _native.C().linear_add_layernorm(x2, W, b, res.contiguous(), g.detach(), bb.detach(),
-                                                    self.config.layer_norm_eps, self.GEMM_PREC)
+                                                    self.config.layer_norm_eps, self.GEMM_PREC,
+                                                    self._weight_planes(x2, W))
         return self._add_ln(self._linear(x2, W, b), res, g, bb)
 
     @torch.no_grad()

@@ -76,6 +76,22 @@ def test_bert_encoder_gpu_kernels_match_transformers(cuda):
 
 
 @pytest.mark.gpu
+def test_bert_encoder_large_batch_planes_path_matches_transformers(cuda):
+    """16,384 token rows: the Q/K/V and FFN-up projections take mlp.hip's pre-split planes path with
+    the encoder's cached weight planes; parity with transformers, the second (cached) pass identical."""
+    ref, mine = _pair(H=256, L=2, heads=4, I=1024, V=500, P=128)
+    ids, mask, tt = _inputs(B=128, S=128, V=500)
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=mask, token_type_ids=tt).last_hidden_state
+    m = mine.to(cuda)
+    got = m(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu()
+    assert len(m.__dict__.get("_planes_cache", {})) > 0
+    keep = mask.bool()
+    assert torch.allclose(got[keep], want[keep], atol=2e-4, rtol=2e-4), (got[keep] - want[keep]).abs().max()
+    assert torch.equal(got, m(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H", [64, 128, 260, 768, 1024])
 def test_add_layernorm_and_embed_layernorm_kernels(cuda, H):
     from avenir_amd import _native

@@ -58,3 +58,40 @@ def test_linear_act_fwd_xcd_tile_order(cuda, M, N, K):
     Y = _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 1).cpu()
     ref = torch.relu(X.double() @ W.double().t() + b.double())
     assert (Y.double() - ref).abs().max().item() <= 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", [3, 6])
+@pytest.mark.parametrize("M,N,K", [(4100, 2600, 100), (4096, 2560, 768), (3000, 3500, 1), (2600, 4100, 33),
+                                   (3300, 3200, 1027)])
+def test_linear_act_fwd_planes_vs_fp64(cuda, M, N, K, prec):
+    """The pre-split term-plane path (outputs >= 1,024 x 1,024 in the split-bf16 modes: bf16 term
+    planes with K zero-padded to 32, LDS-DMA ring): ragged tile edges (clamped source rows), K not a
+    multiple of 32 or of 4, against fp64 at the mode's tolerance; deterministic across calls."""
+    g = torch.Generator().manual_seed(M + N + K + prec)
+    X, W, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / K ** 0.5, torch.randn(N, generator=g)
+    C = _native.C()
+    assert C.linear_act_fwd_planes_bytes(M, N, K, prec) > 0          # the shape takes the planes path
+    Y = C.linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 6, prec).cpu()
+    ref = torch.nn.functional.gelu(X.double() @ W.double().t() + b.double())
+    err = (Y.double() - ref).abs().max().item()
+    assert err <= (2e-5 if prec == 6 else 1.5e-4) * max(1.0, K ** 0.25), err
+    assert torch.equal(Y, C.linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 6, prec).cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", [3, 6])
+def test_linear_act_fwd_cached_weight_planes(cuda, prec):
+    """w_planes (the weight's bf16 term planes, split once) gives the bit-identical result of the
+    per-call split; a mismatched planes tensor is refused."""
+    g = torch.Generator().manual_seed(prec)
+    M, N, K = 4096, 2600, 200
+    X, W, b = (torch.randn(M, K, generator=g).to(cuda), (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda),
+               torch.randn(N, generator=g).to(cuda))
+    C = _native.C()
+    assert C.linear_act_fwd_planes_bytes(M, N, K, prec) > 0
+    P = C.sbf16_weight_planes(W, prec)
+    assert torch.equal(C.linear_act_fwd(X, W, b, 1, prec, P), C.linear_act_fwd(X, W, b, 1, prec))
+    with pytest.raises(RuntimeError):
+        C.linear_act_fwd(X, W, b, 1, prec, P[:-2])
+    assert C.sbf16_weight_planes(W, 0) is None
