@@ -886,7 +886,9 @@ long long linear_act_fwd_planes_bytes(int M, int N, int K, int prec) {
   if (tiles < planes_min_tiles()) return 0;
   const long long Kp = ((long long)K + 31) / 32 * 32;
   const long long Mp = ((long long)M + 127) / 128 * 128, Np = ((long long)N + 127) / 128 * 128;
-  return (mode == 6 ? 3LL : 2LL) * (Mp + Np) * Kp * 2;
+  const long long bytes = (mode == 6 ? 3LL : 2LL) * (Mp + Np) * Kp * 2;
+  // scratch bound (the in-loop tile needs none): 1.5x the operands' fp32 bytes, at most 2 GiB
+  return bytes <= (2LL << 30) ? bytes : 0;
 }
 
 // K step of the planes tile (AVMI_PLANES_BK = 16 | 32, default 16)

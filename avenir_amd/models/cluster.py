@@ -26,6 +26,51 @@ from ..parallel.comm import Comm, get_comm
 from ..utils.resilience import IterationLoop, RecoveryConfig
 
 
+def kmeanspp_seed_batch(samples: list[torch.Tensor], ks: list[int], us: list[torch.Tensor],
+                        max_elems: int = 1 << 26) -> list[torch.Tensor]:
+    """Greedy k-means++ (Arthur & Vassilvitskii 2007, as scikit-learn) for several runs at once.
+    Run r seeds ``ks[r]`` centres from its sample ``samples[r]`` [m, D]; per centre it draws
+    L = ``us[r].shape[1]`` candidates by D^2 inverse-CDF sampling (the uniforms ``us[r]`` [k, L],
+    row 0's first entry picks the first centre) and keeps the one that lowers the potential most.
+    Runs with samples of one shape advance together: per centre index one cumsum, one batched
+    searchsorted, one batched distance and one argmin over [R, L, m] — chunked so R L m stays
+    under ``max_elems`` — with finished runs (k reached) frozen by a mask.  No host round trip."""
+    out: list[torch.Tensor | None] = [None] * len(samples)
+    by_shape: dict[tuple, list[int]] = {}
+    for r, S in enumerate(samples):
+        by_shape.setdefault((tuple(S.shape), us[r].shape[1], S.device), []).append(r)
+    for (shape, L, dev), rs in by_shape.items():
+        m = shape[0]
+        step = max(1, max_elems // max(1, L * m))
+        for c0 in range(0, len(rs), step):
+            grp = rs[c0:c0 + step]
+            S = torch.stack([samples[r] for r in grp]).float()                       # [R, m, D]
+            R, kmax = len(grp), max(ks[r] for r in grp)
+            U = torch.zeros((R, kmax, L), dtype=torch.float64)
+            for j, r in enumerate(grp):
+                U[j, : ks[r]] = us[r]
+            U = U.to(dev)
+            kk = torch.tensor([ks[r] for r in grp], device=dev)
+            ar = torch.arange(R, device=dev)
+            Sd = S.double()
+            i0 = (U[:, 0, 0] * m).long().clamp_max(m - 1)
+            idx = torch.zeros((R, kmax), dtype=torch.long, device=dev)
+            idx[:, 0] = i0
+            d2 = ((S - S[ar, i0].unsqueeze(1)) ** 2).sum(2).double()                # [R, m]
+            for i in range(1, kmax):
+                cum = torch.cumsum(d2, 1)
+                cand = torch.searchsorted(cum, cum[:, -1:] * U[:, i], right=True).clamp_max(m - 1)   # [R, L]
+                dc = torch.cdist(Sd[ar.unsqueeze(1), cand], Sd).square()            # [R, L, m]
+                pot = torch.minimum(dc, d2.unsqueeze(1))
+                best = pot.sum(2).argmin(1)                                          # [R]
+                live = kk > i
+                idx[:, i] = torch.where(live, cand[ar, best], 0)
+                d2 = torch.where(live.unsqueeze(1), pot[ar, best], d2)
+            for j, r in enumerate(grp):
+                out[r] = S[j, idx[j, : ks[r]]]
+    return out
+
+
 @dataclass
 class KMeansRun:
     k: int
@@ -113,20 +158,16 @@ class KMeans:
         self.best: dict[int, KMeansRun] = {}
 
     # ------------------------------------------------------------------------------------------
-    def _init_centroids(self, X: torch.Tensor, k: int, seed: int) -> torch.Tensor:
-        """k-means++ (D^2 sampling) on a gathered sample; identical on every rank (broadcast)."""
-        comm = self.comm or get_comm()
-        g = torch.Generator(device="cpu")
-        g.manual_seed(seed)
-        # sample up to 64k points overall for seeding, in O(m) and on X's device: every row when
-        # the shard fits; m distinct rows of a random affine permutation i -> (a i + b) mod n
-        # (gcd(a, n) = 1) up to 4 m rows; m uniform draws above (duplicates are harmless).  Only
-        # scalars come from the host generator, so CPU and GPU sample the same rows (a host
-        # randperm per run was 27 ms of kMeansPlusPlusCluster's 69: profiles/r6_slow_jobs.jsonl)
+    def _seed_sample(self, X: torch.Tensor, g: torch.Generator, comm) -> torch.Tensor:
+        """A run's seeding sample: up to 64k points overall, in O(m) and on X's device: every row
+        when the shard fits; m distinct rows of a random affine permutation i -> (a i + b) mod n
+        (gcd(a, n) = 1) up to 4 m rows; m uniform draws above (duplicates are harmless).  Only
+        scalars come from the host generator, so CPU and GPU sample the same rows (a host randperm
+        per run was 27 ms of kMeansPlusPlusCluster's 69: profiles/r6_slow_jobs.jsonl)."""
         n = X.shape[0]
         m = min(n, max(1, 65536 // max(comm.world, 1)))
         if m >= n:
-            sel = torch.arange(n, device=X.device)
+            sel = None
         elif n <= 4 * m:
             a = int(torch.randint(1, n, (1,), generator=g))
             while math.gcd(a, n) != 1:
@@ -135,33 +176,30 @@ class KMeans:
             sel = (torch.arange(m, device=X.device, dtype=torch.long) * a + b) % n
         else:
             sel = torch.randint(0, n, (m,), generator=g).to(X.device)
-        S = X[sel].float()
+        S = (X if sel is None else X[sel]).float()
         if comm.is_distributed:
             S = comm.all_gather_v(S)
+        return S
+
+    def _init_centroids_all(self, X: torch.Tensor, specs: list[tuple[int, int]]) -> list[torch.Tensor]:
+        """Initial centroids of every (k, seed) run, identical on every rank (rank 0's, broadcast).
+        k-means++ seeding runs for ALL runs of the fit together (:func:`kmeanspp_seed_batch`): one
+        set of batched tensor ops per centre index instead of one per centre per run (63 runs of
+        the kMeansPlusPlusCluster sweep spent 29 of its 46 ms in per-run seeding loops)."""
+        comm = self.comm or get_comm()
+        gens = [torch.Generator(device="cpu").manual_seed(sd) for _, sd in specs]
+        samples = [self._seed_sample(X, g, comm) for g in gens]
         if self.init == "random":
-            C = S[torch.randperm(S.shape[0], generator=g)[:k].to(S.device)]
+            Cs = [S[torch.randperm(S.shape[0], generator=g)[:k].to(S.device)]
+                  for (k, _), S, g in zip(specs, samples, gens)]
         else:
-            # greedy k-means++ (Arthur & Vassilvitskii 2007, as scikit-learn): per centre draw
-            # L = 2 + ln k candidates by D^2 inverse-CDF sampling and keep the one that lowers the
-            # potential most; all on the device, no host round trip per centre
-            L = 2 + int(math.log(max(k, 2)))
-            u = torch.rand((k, L), generator=g, dtype=torch.float64)
-            m = S.shape[0]
-            idx = [torch.full((1,), min(int(float(u[0, 0]) * m), m - 1), dtype=torch.long, device=S.device)]
-            d2 = ((S - S.index_select(0, idx[0])) ** 2).sum(1).double()
-            uu = u.to(S.device)
-            for i in range(1, k):
-                cum = torch.cumsum(d2, 0)
-                cand = torch.searchsorted(cum, cum[-1:] * uu[i], right=True).clamp_max(m - 1)   # [L]
-                dc = torch.cdist(S.index_select(0, cand).double(), S.double()).square()       # [L, m]
-                pot = torch.minimum(dc, d2.unsqueeze(0))                                     # [L, m]
-                best = pot.sum(1).argmin().view(1)
-                idx.append(cand.index_select(0, best))
-                d2 = pot.index_select(0, best)[0]
-            C = S.index_select(0, torch.cat(idx))
+            ks = [k for k, _ in specs]
+            L = [2 + int(math.log(max(k, 2))) for k in ks]
+            us = [torch.rand((k, l), generator=g, dtype=torch.float64) for k, l, g in zip(ks, L, gens)]
+            Cs = kmeanspp_seed_batch(samples, ks, us)
         if comm.is_distributed:
-            C = comm.broadcast(C.contiguous(), 0)
-        return C.contiguous()
+            Cs = [comm.broadcast(C.contiguous(), 0) for C in Cs]
+        return [C.contiguous() for C in Cs]
 
     def _step(self, X: torch.Tensor, Cs: list[torch.Tensor]):
         """CPU oracle of one Lloyd pass -> per run (sums f64 [k, D], counts [k], sse f64 [1])."""
@@ -216,7 +254,7 @@ class KMeans:
         self._tol_eff = self._effective_tol(X, comm)
         Xp = self._padded(X)
         specs = [(k, self.seed * 1009 + k * 31 + r) for k in self.ks for r in range(self.n_init)]
-        runs = [KMeansRun(k, sd, self._init_centroids(X, k, sd)) for k, sd in specs]
+        runs = [KMeansRun(k, sd, C) for (k, sd), C in zip(specs, self._init_centroids_all(X, specs))]
         self.best = {}
         for gi, grp in enumerate(self._groups(specs, Xp.shape[1] if Xp is not None else None)):
             with IterationLoop(f"kmeans.g{gi}", self.recovery, comm, device=X.device) as lp:
