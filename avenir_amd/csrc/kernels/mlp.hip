@@ -882,6 +882,7 @@ static long long planes_min_tiles() {
 long long linear_act_fwd_planes_bytes(int M, int N, int K, int prec) {
   const int mode = prec >= 0 ? prec : f32_gemm_mode();
   if (mode == 0 || !planes_enabled() || M <= 0 || N <= 0 || K <= 0 || K > (1 << 20)) return 0;
+  M = std::min(M, 1 << 22);  // linear_act_fwd runs larger M in row chunks of 2^22 over one scratch
   const long long tiles = ((long long)M + 127) / 128 * (((long long)N + 127) / 128);
   if (tiles < planes_min_tiles()) return 0;
   const long long Kp = ((long long)K + 31) / 32 * 32;
@@ -960,6 +961,14 @@ void sbf16_weight_planes(const float* W, int N, int K, int prec, void* out, hipS
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                     hipStream_t stream, float* partial, int S, int prec, void* planes, const void* w_planes) {
   if (M <= 0 || N <= 0) return;
+  // row chunks of 2^22: the tile grids put the row tiles on grid.y (<= 65,535 tiles of 64 rows)
+  constexpr int MAXR = 1 << 22;
+  if (M > MAXR) {
+    for (int m0 = 0; m0 < M; m0 += MAXR)
+      linear_act_fwd(X + (long long)m0 * K, W, b, Y + (long long)m0 * N, std::min(MAXR, M - m0), N, K, act, stream,
+                     nullptr, 1, prec, planes, w_planes);
+    return;
+  }
   const bool vec = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(W) % 16 == 0);
   if (planes != nullptr && S <= 1 && linear_act_fwd_planes_bytes(M, N, K, prec) > 0) {

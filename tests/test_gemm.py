@@ -95,3 +95,14 @@ def test_linear_act_fwd_cached_weight_planes(cuda, prec):
     with pytest.raises(RuntimeError):
         C.linear_act_fwd(X, W, b, 1, prec, P[:-2])
     assert C.sbf16_weight_planes(W, 0) is None
+
+
+@pytest.mark.gpu
+def test_linear_act_fwd_beyond_the_row_grid_limit(cuda):
+    """More than 2^22 rows (65,535 row tiles of 64): the forward runs in row chunks."""
+    g = torch.Generator().manual_seed(5)
+    M, N, K = (1 << 22) + 4100, 8, 4
+    X, W, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    Y = _native.C().linear_act_fwd(X.to(cuda), W.to(cuda), b.to(cuda), 1).cpu()
+    ref = torch.relu(X.double() @ W.double().t() + b.double())
+    assert (Y.double() - ref).abs().max().item() <= 1e-4
