@@ -869,15 +869,17 @@ static bool planes_enabled() {
   return on;
 }
 
-// fewest 128 x 128 output tiles that take the planes path (AVMI_PLANES_MIN_TILES, default 640: at
-// 768 tiles it beats the in-loop split tile by 4-26 % per call, at 512 and 192 it loses 10-30 %,
-// profiles/r6_k27_planes_*.jsonl)
-static long long planes_min_tiles() {
+// fewest 128 x 128 output tiles that take the planes path (AVMI_PLANES_MIN_TILES overrides): the
+// planes tile runs three workgroups per CU (768 in one round), the in-loop x3 tile two (512), the
+// in-loop x6 tile three.  Measured (profiles/r6_k27_thresh_bf16x*_p*.jsonl, planes vs in-loop):
+// x3 576 tiles 74 vs 104 us, 768 96 vs 116, 1,152 123 vs 160, 512 82 vs 71, 384 67 vs 61;
+// x6 768 139 vs 146, 576 111 vs 112, 512 118 vs 107, 384 88 vs 85.  So x3 from 513, x6 from 640.
+static long long planes_min_tiles(int mode) {
   static const long long n = [] {
     const char* e = std::getenv("AVMI_PLANES_MIN_TILES");
-    return e ? std::atoll(e) : 640LL;
+    return e ? std::atoll(e) : -1LL;
   }();
-  return n;
+  return n >= 0 ? n : (mode == 3 ? 513LL : 640LL);
 }
 
 long long linear_act_fwd_planes_bytes(int M, int N, int K, int prec) {
@@ -885,7 +887,7 @@ long long linear_act_fwd_planes_bytes(int M, int N, int K, int prec) {
   if (mode == 0 || !planes_enabled() || M <= 0 || N <= 0 || K <= 0 || K > (1 << 20)) return 0;
   M = std::min(M, 1 << 22);  // linear_act_fwd runs larger M in row chunks of 2^22 over one scratch
   const long long tiles = ((long long)M + 127) / 128 * (((long long)N + 127) / 128);
-  if (tiles < planes_min_tiles()) return 0;
+  if (tiles < planes_min_tiles(mode)) return 0;
   const long long Kp = ((long long)K + 31) / 32 * 32;
   const long long Mp = ((long long)M + 127) / 128 * 128, Np = ((long long)N + 127) / 128 * 128;
   const long long bytes = (mode == 6 ? 3LL : 2LL) * (Mp + Np) * Kp * 2;

@@ -167,6 +167,8 @@ class BertEncoder(torch.nn.Module):
         hit = self._qkv_cache.get(i)
         if hit is not None and hit[0] == key:
             return hit[1], hit[2]
+        if hit is not None:                 # the old fused weight's planes go with it
+            self.__dict__.get("_planes_cache", {}).pop((hit[1].data_ptr(), tuple(hit[1].shape)), None)
         W = torch.cat([ps[0], ps[2], ps[4]], 0).detach().contiguous()
         b = torch.cat([ps[1], ps[3], ps[5]], 0).detach().contiguous()
         self._qkv_cache[i] = (key, W, b)
@@ -188,13 +190,17 @@ class BertEncoder(torch.nn.Module):
         C = _native.C()
         if C.linear_act_fwd_planes_bytes(x2.shape[0], W.shape[0], W.shape[1], self.GEMM_PREC) == 0:
             return None
+        # keyed by storage (callers pass fresh .detach() views; a detached view shares the
+        # parameter's version counter); the entry holds W, so its address cannot be reused by
+        # another tensor while cached
         cache = self.__dict__.setdefault("_planes_cache", {})
-        key = (W._version, param_epoch())
-        hit = cache.get(id(W))
-        if hit is not None and hit[0] is W and hit[1] == key:
+        addr = (W.data_ptr(), tuple(W.shape))
+        key = (W._version, param_epoch(), self.GEMM_PREC)
+        hit = cache.get(addr)
+        if hit is not None and hit[1] == key:
             return hit[2]
         p = C.sbf16_weight_planes(W.detach(), self.GEMM_PREC)
-        cache[id(W)] = (W, key, p)          # holds W: its id cannot be reused while cached
+        cache[addr] = (W, key, p)
         return p
 
     def _linear(self, x2, W, b, act: int = 0):

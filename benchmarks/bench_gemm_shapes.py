@@ -32,7 +32,8 @@ def main():
     C = _native.C()
     g = torch.Generator(device="cuda").manual_seed(0)
     for M, N, K, act in ((128, 2304, 768, 0), (128, 768, 768, 0), (128, 3072, 768, 6), (128, 768, 3072, 0),
-                         (1, 3072, 768, 6), (4096, 3072, 768, 6), (4096, 768, 3072, 0), (16384, 768, 768, 0),
+                         (1, 3072, 768, 6), (4096, 3072, 768, 6), (4096, 2304, 768, 0), (4096, 768, 768, 0), (4096, 768, 3072, 0),
+                         (16384, 768, 768, 0), (8192, 2304, 768, 0), (2048, 3072, 768, 6),
                          (8192, 1024, 1024, 1), (5000, 400, 5, 0), (5000, 100, 400, 0)):
         X = torch.randn(M, K, generator=g, device="cuda")
         W = torch.randn(N, K, generator=g, device="cuda") / K ** 0.5

@@ -204,6 +204,19 @@ def bert():
     torch.cuda.synchronize()
 
 
+def bert32():
+    """The bert-base encoder at B 32 x S 128 (4,096 token rows: the planes path for Q/K/V and FFN-up,
+    the in-loop split tiles for the 768-column projections): 6 passes."""
+    from avenir_amd.nn.bert import BertConfig, BertEncoder
+    torch.manual_seed(0)
+    m = BertEncoder(BertConfig()).cuda()
+    ids = torch.randint(0, 30522, (32, 128), device="cuda")
+    mask = torch.ones_like(ids)
+    for _ in range(6):
+        m(ids, mask)
+    torch.cuda.synchronize()
+
+
 def svm_select():
     """svm.hip smo_ws_topk_stream_kernel + the rank merge: the working-set selection at 1,048,576 rows."""
     from avenir_amd import _native
@@ -222,7 +235,7 @@ def svm_select():
 
 TARGETS = {"kmeans": kmeans, "fmt": fmt, "pairs": pairs, "split": split, "lstm": lstm, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
            "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest,
-           "gemm_tn": gemm_tn, "k27": k27, "bert": bert, "svm_select": svm_select}
+           "gemm_tn": gemm_tn, "k27": k27, "bert": bert, "bert32": bert32, "svm_select": svm_select}
 
 if __name__ == "__main__":
     TARGETS[sys.argv[1]]()

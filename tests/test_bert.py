@@ -85,10 +85,14 @@ def test_bert_encoder_large_batch_planes_path_matches_transformers(cuda):
         want = ref(input_ids=ids, attention_mask=mask, token_type_ids=tt).last_hidden_state
     m = mine.to(cuda)
     got = m(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu()
-    assert len(m.__dict__.get("_planes_cache", {})) > 0
+    cache = dict(m.__dict__.get("_planes_cache", {}))
+    assert len(cache) > 0
     keep = mask.bool()
     assert torch.allclose(got[keep], want[keep], atol=2e-4, rtol=2e-4), (got[keep] - want[keep]).abs().max()
     assert torch.equal(got, m(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu())
+    # the second pass reused every cached weight split (same planes tensors, no new entries)
+    after = m.__dict__["_planes_cache"]
+    assert after.keys() == cache.keys() and all(after[k][2] is cache[k][2] for k in cache)
 
 
 @pytest.mark.gpu
