@@ -93,6 +93,15 @@ def test_bert_encoder_large_batch_planes_path_matches_transformers(cuda):
     # the second pass reused every cached weight split (same planes tensors, no new entries)
     after = m.__dict__["_planes_cache"]
     assert after.keys() == cache.keys() and all(after[k][2] is cache[k][2] for k in cache)
+    # an in-place weight update (version bump) and one of the fused Q/K/V weights invalidate their
+    # cached planes: parity with the equally updated reference still holds
+    with torch.no_grad():
+        for name in ("encoder.layer.0.intermediate.dense.weight", "encoder.layer.1.attention.self.key.weight"):
+            dict(ref.named_parameters())[name].mul_(1.25)
+            m.p(name).mul_(1.25)
+        want = ref(input_ids=ids, attention_mask=mask, token_type_ids=tt).last_hidden_state
+    got = m(ids.to(cuda), mask.to(cuda), tt.to(cuda)).cpu()
+    assert torch.allclose(got[keep], want[keep], atol=2e-4, rtol=2e-4), (got[keep] - want[keep]).abs().max()
 
 
 @pytest.mark.gpu
