@@ -162,8 +162,21 @@ def test_linear_act_kernel_matches_torch(cuda, act, M, K, N):
     yg = linear_act(xg, Wg, bg, act)
     yg.backward(gy.float().to(cuda))
     assert torch.allclose(yg.detach().cpu().double(), yr.detach(), atol=1e-4, rtol=1e-4)
-    for a, r in ((xg.grad, xr.grad), (Wg.grad, Wr.grad), (bg.grad, br.grad)):
+    # the kernel's derivative is taken from its own stored output, so at a kink (relu / leaky relu
+    # / elu at z ~ 0) the fp64 forward's decision is not the reference: in any split-bf16 mode a
+    # few of 1.3 M pre-activations within the GEMM's error of 0 land on the other side.  The
+    # gradient oracle is the fp64 backward of that same decision (dZ from the GPU's y).
+    y = yg.detach().cpu().double()
+    code = ACT_CODES[act]
+    dact = {0: torch.ones_like(y), 1: (y > 0).double(), 2: y * (1 - y), 3: 1 - y * y,
+            4: torch.where(y > 0, 1.0, 0.01).double(), 5: torch.where(y > 0, 1.0, y + 1)}[code]
+    dz = gy * dact
+    for a, r in ((xg.grad, dz @ W), (Wg.grad, dz.t() @ x), (bg.grad, dz.sum(0))):
         assert torch.allclose(a.cpu().double(), r, atol=1e-3, rtol=1e-3)
+    # and with the fp64 forward's decisions wherever the two agree (away from the kink)
+    if code in (0, 2, 3):
+        for a, r in ((xg.grad, xr.grad), (Wg.grad, Wr.grad), (bg.grad, br.grad)):
+            assert torch.allclose(a.cpu().double(), r, atol=1e-3, rtol=1e-3)
 
 
 @pytest.mark.gpu

@@ -34,11 +34,18 @@ def test_dqn_graphed_fused_update_equals_torch_twin(cuda):
         la.append(float(a.learn()))
         lb.append(float(b.learn()))
     assert a._graph is not None and b._graph is None
-    assert torch.allclose(torch.tensor(la), torch.tensor(lb), rtol=2e-3, atol=1e-7), (la, lb)
+    # fp32-level GEMMs (the default x6 split, or exact f32) track the torch twin to fp32 rounding;
+    # the reduced-precision x3 mode (~2^-17 per product, AVMI_F32_GEMM=bf16x3) to within Adam's
+    # step size: Adam normalises near-zero gradients, so a 2^-17 difference there moves a
+    # parameter by up to lr per update
+    from avenir_amd import _native
+    x3 = _native.C().f32_gemm_mode() == 3
+    rl, ap = (2e-2, 25 * 2e-3) if x3 else (2e-3, 2e-5)
+    assert torch.allclose(torch.tensor(la), torch.tensor(lb), rtol=rl, atol=1e-7), (la, lb)
     for (n, p), q in zip(a.q.named_parameters(), b.q.parameters()):
-        assert torch.allclose(p, q, rtol=1e-3, atol=2e-5), n
+        assert torch.allclose(p, q, rtol=1e-3, atol=ap), n
     for p, q in zip(a.q_tgt.parameters(), b.q_tgt.parameters()):
-        assert torch.allclose(p, q, rtol=1e-3, atol=2e-5)
+        assert torch.allclose(p, q, rtol=1e-3, atol=ap)
     assert int(a._steps_dev) == 25 == a.steps
 
 
