@@ -217,6 +217,24 @@ def bert32():
     torch.cuda.synchronize()
 
 
+def dqn():
+    """DQNAgent.learn (hiddens [128, 128, 128], batch 256, the reference sizes) replayed as its HIP
+    graph: 50 updates after a short fill of the replay ring."""
+    from avenir_amd.nn.rl import DQNAgent, PricingEnv
+    torch.manual_seed(0)
+    env = PricingEnv(64, device="cuda", seed=1)
+    ag = DQNAgent(env, batch=256, seed=1)
+    s = env.reset()
+    for _ in range(8):
+        a = ag.act(s)
+        s2, r, done = env.step(a)
+        ag._store(s, a, r, s2, done)
+        s = s2
+    for _ in range(50):
+        ag.learn()
+    torch.cuda.synchronize()
+
+
 def svm_select():
     """svm.hip smo_ws_topk_stream_kernel + the rank merge: the working-set selection at 1,048,576 rows."""
     from avenir_amd import _native
@@ -235,7 +253,7 @@ def svm_select():
 
 TARGETS = {"kmeans": kmeans, "fmt": fmt, "pairs": pairs, "split": split, "lstm": lstm, "rowpack": rowpack, "columns": columns, "knn16": lambda: _knn(16), "knn64": lambda: _knn(64),
            "knn256": lambda: _knn(256), "smo_ws": smo_ws, "forest": forest,
-           "gemm_tn": gemm_tn, "k27": k27, "bert": bert, "bert32": bert32, "svm_select": svm_select}
+           "gemm_tn": gemm_tn, "k27": k27, "bert": bert, "bert32": bert32, "dqn": dqn, "svm_select": svm_select}
 
 if __name__ == "__main__":
     TARGETS[sys.argv[1]]()
