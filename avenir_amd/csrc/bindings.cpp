@@ -2248,7 +2248,7 @@ std::vector<at::Tensor> linear_act_bwd(const at::Tensor& dY, const at::Tensor& Y
   const int M = (int)Y.size(0), N = (int)Y.size(1);
   auto dYc = dY.contiguous(), Yc = Y.contiguous();
   auto dZ = at::empty_like(Yc);
-  auto part = at::empty({std::max(1, avk::linear_act_bwd_blocks(M)), N}, Y.options());
+  auto part = at::empty({std::max(1, avk::linear_act_bwd_blocks(M, N)), N}, Y.options());
   DevGuard g(Y.device());
   if (M == 0) part.zero_();
   avk::linear_act_bwd(dYc.data_ptr<float>(), Yc.data_ptr<float>(), dZ.data_ptr<float>(), part.data_ptr<float>(), M,

@@ -286,7 +286,8 @@ void sbf16_weight_planes(const float* W, int N, int K, int prec, void* out, hipS
 void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                     hipStream_t stream, float* partial = nullptr, int S = 1, int prec = -1, void* planes = nullptr,
                     const void* w_planes = nullptr);
-int linear_act_bwd_blocks(int M);
+int linear_act_bwd_rows(int M, int N);
+int linear_act_bwd_blocks(int M, int N);
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream);
 // out [N*K + N] = (dW = dZ^T X row-major [N, K], db = colsum dZ) with dZ = dY * act'(Y) fused (dZ

@@ -436,24 +436,38 @@ __global__ __launch_bounds__(256) void linear_splitk_epilogue_kernel(const float
   Y[e] = act_fwd(s + (b ? b[e % N] : 0.f), act);
 }
 
-// dZ = dY * act'(Y); partial[blockIdx.y][n] = sum over this block's rows of dZ[., n]
+// dZ = dY * act'(Y); partial[blockIdx.y][n] = sum over this block's `rows` rows of dZ[., n].
+// `rows` (linear_act_bwd_rows: 16..256) gives small M enough workgroups, and a thread's rows are
+// walked 4 at a time with their loads issued together: a DQN layer (256 x 128) took 20.5 us in 2
+// workgroups of 64 dependent row iterations (profiles/r6_dqn_kernel_stats.csv)
 constexpr int BR_ROWS = 256;
 __global__ __launch_bounds__(MT) void linear_act_bwd_kernel(const float* __restrict__ dY, const float* __restrict__ Y,
                                                              float* __restrict__ dZ, float* __restrict__ partial,
-                                                             int M, int N, int act) {
+                                                             int M, int N, int act, int rows) {
   __shared__ float s[MT / 64][64];
   const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + c;
-  const long long r0 = (long long)blockIdx.y * BR_ROWS;
+  const long long r0 = (long long)blockIdx.y * rows;
+  const long long r1 = r0 + rows < M ? r0 + rows : M;
   float acc = 0.f;
   if (n < N) {
-    for (int i = rg; i < BR_ROWS; i += MT / 64) {
-      const long long m = r0 + i;
-      if (m >= M) break;
-      const long long o = m * N + n;
-      const float g = dY[o] * act_grad_from_y(Y[o], act);
-      dZ[o] = g;
-      acc += g;
+    for (long long m0 = r0 + rg; m0 < r1; m0 += 4 * (MT / 64)) {
+      float dy[4], yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long m = m0 + u * (MT / 64);
+        dy[u] = m < r1 ? dY[m * N + n] : 0.f;
+        yv[u] = m < r1 ? Y[m * N + n] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long m = m0 + u * (MT / 64);
+        if (m < r1) {
+          const float g = dy[u] * act_grad_from_y(yv[u], act);
+          dZ[m * N + n] = g;
+          acc += g;
+        }
+      }
     }
   }
   s[rg][c] = acc;
@@ -1009,13 +1023,23 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
   AV_HIP_CHECK(hipGetLastError());
 }
 
-int linear_act_bwd_blocks(int M) { return (M + BR_ROWS - 1) / BR_ROWS; }
+// rows per workgroup: ~512 workgroups over the (64-column, row-block) grid, 16..256 rows each
+int linear_act_bwd_rows(int M, int N) {
+  const long long nb = (N + 63) / 64;
+  long long r = 16;
+  while (r < BR_ROWS && ((long long)M + r - 1) / r * nb > 512) r *= 2;
+  return (int)r;
+}
+int linear_act_bwd_blocks(int M, int N) {
+  const int r = linear_act_bwd_rows(M, N);
+  return (M + r - 1) / r;
+}
 
 void linear_act_bwd(const float* dY, const float* Y, float* dZ, float* partial, int M, int N, int act,
                     hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
-  dim3 grid((unsigned)((N + 63) / 64), (unsigned)linear_act_bwd_blocks(M));
-  linear_act_bwd_kernel<<<grid, MT, 0, stream>>>(dY, Y, dZ, partial, M, N, act);
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)linear_act_bwd_blocks(M, N));
+  linear_act_bwd_kernel<<<grid, MT, 0, stream>>>(dY, Y, dZ, partial, M, N, act, linear_act_bwd_rows(M, N));
   AV_HIP_CHECK(hipGetLastError());
 }
 

@@ -4,14 +4,16 @@
 the bias and activation applied in the accumulator epilogue (torch: addmm + a separate activation
 pass over [M, N]).  The backward is one MFMA kernel forming ``dZ = dY * act'(Y)`` in its tiles and
 reducing ``dW = dZ^T X`` and the bias gradient over row slices (a fixed-order slice sum after it),
-then ``dX = dZ W`` on the forward MFMA kernel (layers up to 64 x 64; the library GEMM for ``dW``
-reduced all M rows inside one or two output tiles).  Wider layers: one fused ``dZ`` + bias-gradient
+then ``dX = dZ W`` on the forward MFMA kernel (layers up to 64 x 64, or up to 512 x 512 at <= 4,096
+rows; the library GEMM for ``dW`` reduced all M rows inside one or two output tiles).  Wider layers: one fused ``dZ`` + bias-gradient
 pass, then two hipBLASLt GEMMs.  CPU
 tensors run the plain PyTorch composition (the numerics oracle of the GPU tests).
 
 Reference: FeedForwardNetwork layer construction, P/supv/tnn.py:100-145.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -20,7 +22,11 @@ from .. import _native
 # layers up to this width (both N and K) take the fused weight-gradient backward (one 64 x 64 dW
 # tile per row slice: the reference's networks, e.g. R/tnn_bo.properties 8-wide); wider layers re-read
 # their inputs per tile there and use the fused dZ pass + hipBLASLt GEMMs instead
-FUSED_BWD_MAX = 64
+FUSED_BWD_MAX = int(os.environ.get("AVMI_FUSED_BWD_MAX", "64"))
+# ... and at small row counts up to this width too: there the re-reads are a few hundred KB and the
+# two library GEMMs cost 13-20 us each at 256 x 128 x 128 (the DQN's layers: a graphed update 334 ->
+# 273 us, the autoencoder step 187 -> 160 us; profiles/r6_rl_bwd_ab.jsonl)
+FUSED_BWD_SMALL_M, FUSED_BWD_SMALL_MAX = 4096, 512
 
 ACT_CODES = {None: 0, "none": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leakyRelu": 4, "elu": 5}
 
@@ -53,7 +59,9 @@ class _LinearAct(torch.autograd.Function):
     def backward(ctx, gy):
         x, W, y = ctx.saved_tensors
         N, K = W.shape
-        if N <= FUSED_BWD_MAX and K <= FUSED_BWD_MAX:
+        M = x.shape[0]
+        if (N <= FUSED_BWD_MAX and K <= FUSED_BWD_MAX) or \
+                (M <= FUSED_BWD_SMALL_M and N <= FUSED_BWD_SMALL_MAX and K <= FUSED_BWD_SMALL_MAX):
             gx, gW, db = _native.C().linear_act_backward(gy.contiguous(), y, x, W, ctx.code,
                                                          bool(ctx.needs_input_grad[0]))
             return gx, (gW if ctx.needs_input_grad[1] else None), (db if ctx.has_b else None), None
