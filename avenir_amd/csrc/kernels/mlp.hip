@@ -830,6 +830,15 @@ static bool sbf16_swz() {
   return on;
 }
 
+// AVMI_SBF16_SMALLK_KC64=0: the x6 64 x 64 tile keeps 32-deep chunks at K <= 128 (A/B switch)
+static bool small_k_kc64() {
+  static const bool on = [] {
+    const char* e = std::getenv("AVMI_SBF16_SMALLK_KC64");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int sbf16_kc(int mode) {
   static const int kc = [] {
     const char* e = std::getenv("AVMI_SBF16_KC");
@@ -1017,7 +1026,10 @@ void linear_act_fwd(const float* X, const float* W, const float* b, float* Y, in
   dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM));
   const int xcd = xcd_tiles_enabled() && grid.x * grid.y >= 64 ? 1 : 0;
   if (vec && mode == 3) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<1, 2, false, 32><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<1, 2, false, 64><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
-  else if (vec && mode == 6) (sbf16_kc(mode) == 32 ? linear_act_fwd_sbf16_kernel<1, 3, false, 32><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<1, 3, false, 64><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
+  // (x6, 64 x 64 tile: K <= 128 in 64-deep chunks — the latency-bound small GEMMs of the DQN /
+  // autoencoder layers take half the chunk round trips; graphed DQN update 266 -> 262 us, ~1 %:
+  // profiles/r6_rl_kc64_ab.jsonl)
+  else if (vec && mode == 6) ((sbf16_kc(mode) == 32 && !(K <= 128 && small_k_kc64())) ? linear_act_fwd_sbf16_kernel<1, 3, false, 32><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd) : linear_act_fwd_sbf16_kernel<1, 3, false, 64><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd));
   else if (vec) linear_act_fwd_kernel<true, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
   else linear_act_fwd_kernel<false, false><<<grid, MT, 0, stream>>>(X, W, b, Y, M, N, K, act, K, xcd);
   AV_HIP_CHECK(hipGetLastError());
@@ -1063,6 +1075,11 @@ void linear_act_wgrad(const float* dY, const float* Y, const float* X, float* dZ
   const long long E = (long long)N * K + N;
   const unsigned ex = (unsigned)((E + 63) / 64);
   const int S2 = (S + 63) / 64;
+  if (S2 == 1) {  // <= 64 slices: one fixed-order pass straight into out (the second was a copy)
+    slice_sum_kernel<<<dim3(ex, 1), 64 * RG, 0, stream>>>(pW, out, S, 64, E);
+    AV_HIP_CHECK(hipGetLastError());
+    return;
+  }
   slice_sum_kernel<<<dim3(ex, (unsigned)S2), 64 * RG, 0, stream>>>(pW, tmp, S, 64, E);
   AV_HIP_CHECK(hipGetLastError());
   slice_sum_kernel<<<dim3(ex, 1), 64 * RG, 0, stream>>>(tmp, out, S2, S2, E);
