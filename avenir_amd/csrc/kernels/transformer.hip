@@ -64,34 +64,53 @@ __global__ __launch_bounds__(64 * RPB) void add_layernorm_kernel(const float* __
   const long long row = (long long)blockIdx.x * RPB + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
+  // every chunk's slice loads of a batch are issued together (a 128 x 768 projection summed over 21
+  // slices was ~18 dependent load round trips per row, 8.2 us: profiles/r6_bert1_kernel_stats.csv);
+  // each element still adds its slices in slice order
   float4 v[LN_MAXV];
+  const float* __restrict__ px = x + row * H + 4 * lane;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i)
+    v[i] = 4 * (lane + 64 * i) < H ? *reinterpret_cast<const float4*>(px + 256 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = 1;
+  for (; k + 4 <= S; k += 4) {
+    float4 p[LN_MAXV][4];
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        p[i][u] = 4 * (lane + 64 * i) < H ? *reinterpret_cast<const float4*>(px + 256 * i + (k + u) * sstride)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[i].x += p[i][u].x; v[i].y += p[i][u].y; v[i].z += p[i][u].z; v[i].w += p[i][u].w;
+      }
+  }
+  for (; k < S; ++k) {
+    float4 p[LN_MAXV];
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i)
+      p[i] = 4 * (lane + 64 * i) < H ? *reinterpret_cast<const float4*>(px + 256 * i + k * sstride)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      v[i].x += p[i].x; v[i].y += p[i].y; v[i].z += p[i].z; v[i].w += p[i].w;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < LN_MAXV; ++i) {
     const int c0 = 4 * (lane + 64 * i);
-    v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c0 < H) {
-      const float* __restrict__ px = x + row * H + c0;
-      float4 a = *reinterpret_cast<const float4*>(px);
-      int k = 1;
-      for (; k + 8 <= S; k += 8) {  // 8 slices' loads in flight, added in slice order
-        float4 p[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) p[u] = *reinterpret_cast<const float4*>(px + (k + u) * sstride);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          a.x += p[u].x; a.y += p[u].y; a.z += p[u].z; a.w += p[u].w;
-        }
-      }
-      for (; k < S; ++k) {
-        const float4 p = *reinterpret_cast<const float4*>(px + k * sstride);
-        a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
-      }
       if (bias) {
         const float4 bb = *reinterpret_cast<const float4*>(bias + c0);
-        a.x += bb.x; a.y += bb.y; a.z += bb.z; a.w += bb.w;
+        v[i].x += bb.x; v[i].y += bb.y; v[i].z += bb.z; v[i].w += bb.w;
       }
-      const float4 b = res ? *reinterpret_cast<const float4*>(res + row * H + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      v[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      if (res) {
+        const float4 b = *reinterpret_cast<const float4*>(res + row * H + c0);
+        v[i] = make_float4(v[i].x + b.x, v[i].y + b.y, v[i].z + b.z, v[i].w + b.w);
+      }
     }
   }
   ln_row(v, H, gamma, beta, eps, out + row * H);
