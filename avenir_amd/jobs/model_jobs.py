@@ -142,11 +142,13 @@ def kmeanspp(args):
     d = ctx.delim_out
     out, cents = [], []
     local = _LocalComm()
-    for k, X in groups:
-        X = X.to(ctx.device)
-        kk = [c for c in ks if c <= X.shape[0]]
-        km = KMeans(kk, n_init=ctx.get_int("num.clustGroup", 10), max_iter=ctx.get_int("num.iter", 10),
-                    init="k-means++", comm=local).fit(X)
+    Xs = [X.to(ctx.device) for _, X in groups]
+    models = [KMeans([c for c in ks if c <= X.shape[0]], n_init=ctx.get_int("num.clustGroup", 10),
+                     max_iter=ctx.get_int("num.iter", 10), init="k-means++", comm=local) for X in Xs]
+    inits = KMeans.init_many(models, Xs)        # every group's seeding in one batched pass
+    for (k, _), X, km, C0 in zip(groups, Xs, models, inits):
+        kk = km.ks
+        km.fit(X, init_centroids=C0)
         for c in kk:
             run = km.best[c]
             out.append(d.join(list(k) + [str(c), fmt(run.sse, prec)]))

@@ -36,30 +36,43 @@ def kmeanspp_seed_batch(samples: list[torch.Tensor], ks: list[int], us: list[tor
     searchsorted, one batched distance and one argmin over [R, L, m] — chunked so R L m stays
     under ``max_elems`` — with finished runs (k reached) frozen by a mask.  No host round trip."""
     out: list[torch.Tensor | None] = [None] * len(samples)
-    by_shape: dict[tuple, list[int]] = {}
+    by_key: dict[tuple, list[int]] = {}
     for r, S in enumerate(samples):
-        by_shape.setdefault((tuple(S.shape), us[r].shape[1], S.device), []).append(r)
-    for (shape, L, dev), rs in by_shape.items():
-        m = shape[0]
-        step = max(1, max_elems // max(1, L * m))
+        by_key.setdefault((S.shape[1], us[r].shape[1], S.device), []).append(r)
+    for (D, L, dev), rs in by_key.items():
+        # samples of different sizes (the key groups of a job) share a launch, zero-padded to the
+        # chunk's largest: a padded row has D^2 weight 0, so it is never drawn and adds 0 to every
+        # potential; the first centre and the candidate clamp use the run's own size
+        rs = sorted(rs, key=lambda r: samples[r].shape[0])
+        step = max(1, max_elems // max(1, L * samples[rs[-1]].shape[0]))
         for c0 in range(0, len(rs), step):
             grp = rs[c0:c0 + step]
-            S = torch.stack([samples[r] for r in grp]).float()                       # [R, m, D]
-            R, kmax = len(grp), max(ks[r] for r in grp)
+            ms = [samples[r].shape[0] for r in grp]
+            m, R, kmax = max(ms), len(grp), max(ks[r] for r in grp)
+            if min(ms) == m:
+                S = torch.stack([samples[r] for r in grp]).float()                   # [R, m, D]
+            else:
+                S = torch.zeros((R, m, D), dtype=torch.float32, device=dev)
+                for j, r in enumerate(grp):
+                    S[j, : ms[j]] = samples[r]
             U = torch.zeros((R, kmax, L), dtype=torch.float64)
             for j, r in enumerate(grp):
                 U[j, : ks[r]] = us[r]
             U = U.to(dev)
             kk = torch.tensor([ks[r] for r in grp], device=dev)
+            mr = torch.tensor(ms, device=dev)
             ar = torch.arange(R, device=dev)
             Sd = S.double()
-            i0 = (U[:, 0, 0] * m).long().clamp_max(m - 1)
+            i0 = torch.minimum((U[:, 0, 0] * mr.double()).long(), mr - 1)
             idx = torch.zeros((R, kmax), dtype=torch.long, device=dev)
             idx[:, 0] = i0
             d2 = ((S - S[ar, i0].unsqueeze(1)) ** 2).sum(2).double()                # [R, m]
+            if min(ms) != m:
+                d2 = d2 * (torch.arange(m, device=dev) < mr.unsqueeze(1))
             for i in range(1, kmax):
                 cum = torch.cumsum(d2, 1)
-                cand = torch.searchsorted(cum, cum[:, -1:] * U[:, i], right=True).clamp_max(m - 1)   # [R, L]
+                cand = torch.minimum(torch.searchsorted(cum, cum[:, -1:] * U[:, i], right=True),
+                                     (mr - 1).unsqueeze(1))                          # [R, L]
                 dc = torch.cdist(Sd[ar.unsqueeze(1), cand], Sd).square()            # [R, L, m]
                 pot = torch.minimum(dc, d2.unsqueeze(1))
                 best = pot.sum(2).argmin(1)                                          # [R]
@@ -186,20 +199,47 @@ class KMeans:
         k-means++ seeding runs for ALL runs of the fit together (:func:`kmeanspp_seed_batch`): one
         set of batched tensor ops per centre index instead of one per centre per run (63 runs of
         the kMeansPlusPlusCluster sweep spent 29 of its 46 ms in per-run seeding loops)."""
-        comm = self.comm or get_comm()
-        gens = [torch.Generator(device="cpu").manual_seed(sd) for _, sd in specs]
-        samples = [self._seed_sample(X, g, comm) for g in gens]
-        if self.init == "random":
-            Cs = [S[torch.randperm(S.shape[0], generator=g)[:k].to(S.device)]
-                  for (k, _), S, g in zip(specs, samples, gens)]
-        else:
-            ks = [k for k, _ in specs]
-            L = [2 + int(math.log(max(k, 2))) for k in ks]
-            us = [torch.rand((k, l), generator=g, dtype=torch.float64) for k, l, g in zip(ks, L, gens)]
-            Cs = kmeanspp_seed_batch(samples, ks, us)
-        if comm.is_distributed:
-            Cs = [comm.broadcast(C.contiguous(), 0) for C in Cs]
-        return [C.contiguous() for C in Cs]
+        return KMeans.init_many([self], [X])[0]
+
+    def run_specs(self) -> list[tuple[int, int]]:
+        """(k, seed) of every run of a fit, in run order."""
+        return [(k, self.seed * 1009 + k * 31 + r) for k in self.ks for r in range(self.n_init)]
+
+    @staticmethod
+    def init_many(models: list["KMeans"], Xs: list[torch.Tensor]) -> list[list[torch.Tensor]]:
+        """Initial centroids of every run of several independent fits (model i on Xs[i]), the
+        k-means++ seeding of all of them in ONE :func:`kmeanspp_seed_batch` pass (the
+        kMeansPlusPlusCluster job seeds all its key groups together)."""
+        per_model, kpp = [], []
+        for km, X in zip(models, Xs):
+            comm = km.comm or get_comm()
+            specs = km.run_specs()
+            X = X.float().contiguous()
+            gens = [torch.Generator(device="cpu").manual_seed(sd) for _, sd in specs]
+            samples = [km._seed_sample(X, g, comm) for g in gens]
+            if km.init == "random":
+                per_model.append([S[torch.randperm(S.shape[0], generator=g)[:k].to(S.device)]
+                                  for (k, _), S, g in zip(specs, samples, gens)])
+            else:
+                ks = [k for k, _ in specs]
+                us = [torch.rand((k, 2 + int(math.log(max(k, 2)))), generator=g, dtype=torch.float64)
+                      for k, g in zip(ks, gens)]
+                per_model.append(None)
+                kpp.append((len(per_model) - 1, samples, ks, us))
+        if kpp:
+            flat = kmeanspp_seed_batch([S for _, ss, _, _ in kpp for S in ss], [k for _, _, ks, _ in kpp for k in ks],
+                                       [u for _, _, _, us in kpp for u in us])
+            o = 0
+            for i, ss, _, _ in kpp:
+                per_model[i] = flat[o:o + len(ss)]
+                o += len(ss)
+        out = []
+        for km, Cs in zip(models, per_model):
+            comm = km.comm or get_comm()
+            if comm.is_distributed:
+                Cs = [comm.broadcast(C.contiguous(), 0) for C in Cs]
+            out.append([C.contiguous() for C in Cs])
+        return out
 
     def _step(self, X: torch.Tensor, Cs: list[torch.Tensor]):
         """CPU oracle of one Lloyd pass -> per run (sums f64 [k, D], counts [k], sse f64 [1])."""
@@ -244,7 +284,7 @@ class KMeans:
             groups.append(cur)
         return groups
 
-    def fit(self, X: torch.Tensor) -> "KMeans":
+    def fit(self, X: torch.Tensor, init_centroids: list[torch.Tensor] | None = None) -> "KMeans":
         """All (k, init) runs advance together (S/cluster/KmeansCluster.scala keys by
         (numClusters, initGroup)).  GPU: per iteration ONE fused assignment launch for a group of
         runs, one reduction launch, one RCCL all-reduce of the flat [K (D+1) + R] statistics when
@@ -253,8 +293,10 @@ class KMeans:
         X = X.float().contiguous()
         self._tol_eff = self._effective_tol(X, comm)
         Xp = self._padded(X)
-        specs = [(k, self.seed * 1009 + k * 31 + r) for k in self.ks for r in range(self.n_init)]
-        runs = [KMeansRun(k, sd, C) for (k, sd), C in zip(specs, self._init_centroids_all(X, specs))]
+        specs = self.run_specs()
+        if init_centroids is None:                 # (``init_centroids``: from init_many)
+            init_centroids = self._init_centroids_all(X, specs)
+        runs = [KMeansRun(k, sd, C) for (k, sd), C in zip(specs, init_centroids)]
         self.best = {}
         for gi, grp in enumerate(self._groups(specs, Xp.shape[1] if Xp is not None else None)):
             with IterationLoop(f"kmeans.g{gi}", self.recovery, comm, device=X.device) as lp:
